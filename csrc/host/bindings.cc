@@ -1,0 +1,281 @@
+// pybind11 bindings of the host (CPU) native library: bitstream primitives,
+// CAVLC writer, independent decoder, CPU reference encoder, Annex-B tools.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "annexb.h"
+#include "cavlc_writer.h"
+#include "cpu_encoder.h"
+#include "h264_decoder.h"
+#include "lowres.h"
+
+namespace py = pybind11;
+using namespace mivc;
+using namespace mivc::h264;
+
+namespace {
+
+py::bytes to_bytes(const std::vector<uint8_t>& v) {
+  return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+}
+
+template <class T>
+T dget(const py::dict& d, const char* k, T def) {
+  if (d.contains(k)) return d[k].cast<T>();
+  return def;
+}
+
+EncoderConfig cfg_from(const py::dict& d) {
+  EncoderConfig c;
+  c.width = dget<int>(d, "width", 0);
+  c.height = dget<int>(d, "height", 0);
+  c.fps = dget<double>(d, "fps", 30.0);
+  c.qp = dget<int>(d, "qp", 26);
+  c.crf = dget<double>(d, "crf", -1.0);
+  c.keyint = dget<int>(d, "keyint", 250);
+  c.me_range = dget<int>(d, "me_range", 16);
+  c.subpel = dget<int>(d, "subpel", 2);
+  c.use_i4x4 = dget<int>(d, "i4x4", 1);
+  c.deblock = dget<int>(d, "deblock", 1);
+  c.chroma_qp_offset = dget<int>(d, "chroma_qp_offset", 0);
+  c.vui = dget<int>(d, "vui", 1);
+  return c;
+}
+
+py::dict picture_to_dict(const DecodedPicture& p) {
+  py::dict d;
+  d["width"] = p.width;
+  d["height"] = p.height;
+  d["coded_width"] = p.coded_width;
+  d["coded_height"] = p.coded_height;
+  d["frame_num"] = p.frame_num;
+  d["idr"] = p.idr;
+  d["slice_type"] = p.slice_type;
+  std::vector<uint8_t> i420 = p.cropped_i420();
+  py::array_t<uint8_t> a(static_cast<py::ssize_t>(i420.size()));
+  std::memcpy(a.mutable_data(), i420.data(), i420.size());
+  d["i420"] = a;
+  py::array_t<uint8_t> y({p.coded_height, p.coded_width});
+  std::memcpy(y.mutable_data(), p.y.data(), p.y.size());
+  d["y_coded"] = y;
+  py::array_t<uint8_t> u({p.coded_height / 2, p.coded_width / 2});
+  std::memcpy(u.mutable_data(), p.u.data(), p.u.size());
+  d["u_coded"] = u;
+  py::array_t<uint8_t> v({p.coded_height / 2, p.coded_width / 2});
+  std::memcpy(v.mutable_data(), p.v.data(), p.v.size());
+  d["v_coded"] = v;
+  py::array_t<int8_t> k(static_cast<py::ssize_t>(p.mb_kind.size()));
+  std::memcpy(k.mutable_data(), p.mb_kind.data(), p.mb_kind.size());
+  d["mb_kind"] = k;
+  py::array_t<int8_t> q(static_cast<py::ssize_t>(p.mb_qp.size()));
+  std::memcpy(q.mutable_data(), p.mb_qp.data(), p.mb_qp.size());
+  d["mb_qp"] = q;
+  py::array_t<int16_t> mv(static_cast<py::ssize_t>(p.mv.size()));
+  std::memcpy(mv.mutable_data(), p.mv.data(), p.mv.size() * 2);
+  d["mv"] = mv;
+  return d;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_host, m) {
+  m.doc() = "govideocompressor_amd host native library (bitstream, CAVLC, decoder, CPU encoder)";
+
+  m.def("exp_golomb", [](const std::vector<int64_t>& vals, bool signed_) {
+    BitWriter bw;
+    for (int64_t v : vals) {
+      if (signed_) bw.put_se(static_cast<int32_t>(v)); else bw.put_ue(static_cast<uint32_t>(v));
+    }
+    size_t bits = bw.bit_pos();
+    bw.align_zero();
+    return py::make_tuple(to_bytes(bw.bytes()), bits);
+  });
+  m.def("read_exp_golomb", [](py::bytes data, int count, bool signed_) {
+    std::string s = data;
+    BitReader br(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+    std::vector<int64_t> out;
+    for (int i = 0; i < count; ++i) out.push_back(signed_ ? br.get_se() : static_cast<int64_t>(br.get_ue()));
+    return out;
+  });
+  m.def("cavlc_block", [](const std::vector<int>& coef, int start, int end, int max_num, int nc) {
+    std::vector<int16_t> c(16, 0);
+    for (size_t i = 0; i < coef.size() && i < 16; ++i) c[i] = static_cast<int16_t>(coef[i]);
+    BitWriter bw;
+    int tc = cavlc_write_block(bw, c.data(), start, end, max_num, nc);
+    size_t bits = bw.bit_pos();
+    bw.align_zero();
+    return py::make_tuple(to_bytes(bw.bytes()), bits, tc);
+  });
+  m.def("table", [](const std::string& name) {
+    std::vector<std::vector<int>> out;
+    auto row = [&](const uint8_t* p, int n) { out.emplace_back(p, p + n); };
+    if (name == "coeff_token_len") for (int t = 0; t < 4; ++t) row(kCoeffTokenLen[t], 68);
+    else if (name == "coeff_token_bits") for (int t = 0; t < 4; ++t) row(kCoeffTokenBits[t], 68);
+    else if (name == "chroma_dc_coeff_token") { row(kChromaDcCoeffTokenLen, 20); row(kChromaDcCoeffTokenBits, 20); }
+    else if (name == "total_zeros_len") for (int t = 0; t < 15; ++t) row(kTotalZerosLen[t], 16);
+    else if (name == "total_zeros_bits") for (int t = 0; t < 15; ++t) row(kTotalZerosBits[t], 16);
+    else if (name == "chroma_dc_total_zeros_len") for (int t = 0; t < 3; ++t) row(kChromaDcTotalZerosLen[t], 4);
+    else if (name == "chroma_dc_total_zeros_bits") for (int t = 0; t < 3; ++t) row(kChromaDcTotalZerosBits[t], 4);
+    else if (name == "run_before_len") for (int t = 0; t < 7; ++t) row(kRunBeforeLen[t], 15);
+    else if (name == "run_before_bits") for (int t = 0; t < 7; ++t) row(kRunBeforeBits[t], 15);
+    else if (name == "intra_cbp") row(kGolombToIntraCbp, 48);
+    else if (name == "inter_cbp") row(kGolombToInterCbp, 48);
+    else if (name == "zigzag") row(kZigzag4x4, 16);
+    else throw std::runtime_error("unknown table " + name);
+    return out;
+  });
+
+  m.def("parameter_sets", [](const py::dict& cfg) {
+    EncoderConfig c = cfg_from(cfg);
+    return to_bytes(write_parameter_sets(make_sps(c), make_pps(c)));
+  });
+
+  // Write one slice NAL from MB decision arrays (uint8 [N,48] headers, int16 [N,408] coefficients).
+  m.def(
+      "write_slice",
+      [](const py::dict& cfg, const py::dict& fp, py::array_t<uint8_t, py::array::c_style> hdr,
+         py::array_t<int16_t, py::array::c_style> coef) {
+        EncoderConfig c = cfg_from(cfg);
+        SPS sps = make_sps(c);
+        PPS pps = make_pps(c);
+        int nmb = sps.width_mbs * sps.height_mbs;
+        if (hdr.size() != static_cast<py::ssize_t>(nmb) * 48) throw std::runtime_error("header array has wrong size");
+        if (coef.size() != static_cast<py::ssize_t>(nmb) * kCoefPerMb) throw std::runtime_error("coef array has wrong size");
+        SliceHeader sh;
+        bool idr = dget<int>(fp, "idr", 0) != 0;
+        sh.nal_unit_type = idr ? NAL_IDR : NAL_SLICE;
+        sh.nal_ref_idc = idr ? 3 : 2;
+        sh.slice_type = dget<int>(fp, "slice_type", idr ? SLICE_I : SLICE_P);
+        sh.frame_num = dget<int>(fp, "frame_num", 0);
+        sh.idr_pic_id = dget<int>(fp, "idr_pic_id", 0);
+        sh.slice_qp_delta = dget<int>(fp, "qp", 26) - pps.pic_init_qp;
+        sh.disable_deblocking_filter_idc = c.deblock ? 0 : 1;
+        SliceStats st;
+        std::vector<uint8_t> nal;
+        {
+          py::gil_scoped_release rel;
+          nal = write_slice_nal(sps, pps, sh, reinterpret_cast<const MbHeader*>(hdr.data()), coef.data(), nmb, &st);
+        }
+        py::dict stats;
+        stats["bits"] = st.bits;
+        stats["skipped"] = st.skipped;
+        stats["intra"] = st.intra;
+        stats["coded_inter"] = st.coded_inter;
+        return py::make_tuple(to_bytes(nal), stats);
+      },
+      py::arg("cfg"), py::arg("frame"), py::arg("hdr"), py::arg("coef"));
+
+  m.def(
+      "decode",
+      [](py::bytes data, bool skip_deblock) {
+        std::string s = data;
+        Decoder dec;
+        dec.set_skip_deblock(skip_deblock);
+        {
+          py::gil_scoped_release rel;
+          dec.decode(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+          dec.flush();
+        }
+        py::list out;
+        for (const DecodedPicture& p : dec.out()) out.append(picture_to_dict(p));
+        return out;
+      },
+      py::arg("data"), py::arg("skip_deblock") = false);
+
+  py::class_<CpuEncoder>(m, "CpuEncoder")
+      .def(py::init([](const py::dict& cfg) { return new CpuEncoder(cfg_from(cfg)); }))
+      .def("encode",
+           [](CpuEncoder& e, py::array_t<uint8_t, py::array::c_style> frames, int nframes, int idr_pic_id) {
+             std::vector<uint8_t> out;
+             {
+               py::gil_scoped_release rel;
+               out = e.encode(frames.data(), nframes, idr_pic_id);
+             }
+             return to_bytes(out);
+           })
+      .def("stats",
+           [](CpuEncoder& e) {
+             py::list l;
+             for (const FrameStats& s : e.stats()) {
+               py::dict d;
+               d["type"] = s.type;
+               d["qp"] = s.qp;
+               d["bytes"] = s.bytes;
+               d["psnr_y"] = s.psnr_y;
+               l.append(d);
+             }
+             return l;
+           })
+      .def("recon_unfiltered",
+           [](CpuEncoder& e) {
+             const std::vector<uint8_t>& r = e.recon_unfiltered();
+             py::array_t<uint8_t> a(static_cast<py::ssize_t>(r.size()));
+             std::memcpy(a.mutable_data(), r.data(), r.size());
+             return a;
+           })
+      .def("recon", [](CpuEncoder& e) {
+        const std::vector<uint8_t>& r = e.recon();
+        py::array_t<uint8_t> a(static_cast<py::ssize_t>(r.size()));
+        std::memcpy(a.mutable_data(), r.data(), r.size());
+        return a;
+      });
+
+  m.def("parse_nals", [](py::bytes data) {
+    std::string s = data;
+    std::vector<NalUnit> v = parse_annexb(reinterpret_cast<const uint8_t*>(s.data()), s.size(), false);
+    py::list l;
+    for (const NalUnit& u : v) l.append(py::make_tuple(u.nal_unit_type, u.nal_ref_idc, u.offset, u.size));
+    return l;
+  });
+  m.def("split_at_idr", [](py::bytes data, int min_frames) {
+    std::string s = data;
+    std::vector<std::pair<size_t, size_t>> cuts;
+    {
+      py::gil_scoped_release rel;
+      cuts = split_annexb_at_idr(reinterpret_cast<const uint8_t*>(s.data()), s.size(), min_frames);
+    }
+    return cuts;
+  });
+  m.def("stream_info", [](py::bytes data) {
+    std::string s = data;
+    StreamInfo si = probe_annexb(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+    py::dict d;
+    d["width"] = si.width;
+    d["height"] = si.height;
+    d["fps"] = si.fps;
+    d["frames"] = si.frames;
+    d["idr_frames"] = si.idr_frames;
+    d["profile_idc"] = si.profile_idc;
+    d["level_idc"] = si.level_idc;
+    d["entropy"] = si.cabac ? "cabac" : "cavlc";
+    return d;
+  });
+  m.def("concat", [](const std::vector<py::bytes>& parts) {
+    std::vector<std::string> ss;
+    for (const py::bytes& b : parts) ss.push_back(b);
+    std::vector<std::pair<const uint8_t*, size_t>> v;
+    for (const std::string& s : ss) v.emplace_back(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+    return to_bytes(concat_annexb(v));
+  });
+  m.def("mp4_mux", [](py::bytes data, double fps) {
+    std::string s = data;
+    return to_bytes(mux_mp4(reinterpret_cast<const uint8_t*>(s.data()), s.size(), fps));
+  });
+  m.def("mp4_demux", [](py::bytes data) {
+    std::string s = data;
+    return to_bytes(demux_mp4_to_annexb(reinterpret_cast<const uint8_t*>(s.data()), s.size()));
+  });
+  m.def(
+      "lowres_costs",
+      [](py::array_t<uint8_t, py::array::c_style> frames, int width, int height, int nframes) {
+        std::vector<float> intra(nframes), inter(nframes);
+        {
+          py::gil_scoped_release rel;
+          lowres_frame_costs(frames.data(), width, height, nframes, intra.data(), inter.data());
+        }
+        return py::make_tuple(intra, inter);
+      });
+}

@@ -1,0 +1,67 @@
+// CPU reference H.264 encoder (the "cpu_ref" backend).
+//
+// Role: (1) the always-available backend for BASELINE config 1 (the reference's
+// CPU `ffmpeg -vcodec libx264` subprocess, client.go:115, when no ffmpeg binary
+// exists -- this image has none) and for CPU-only tests of the job API and the
+// distributed pipeline; (2) a readable, scalar statement of the encoding
+// algorithm that the gfx950 kernels implement in parallel form.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../common/h264_mb.h"
+#include "h264_syntax.h"
+
+namespace mivc {
+namespace h264 {
+
+struct EncoderConfig {
+  int width = 0, height = 0;
+  double fps = 30.0;
+  int qp = 26;          // used when crf < 0
+  double crf = -1.0;    // >= 0 selects the CRF rate control (per-frame QP from complexity)
+  int keyint = 250;     // IDR period inside a segment
+  int me_range = 16;
+  int subpel = 2;       // 0 integer, 1 half, 2 quarter
+  int use_i4x4 = 1;
+  int deblock = 1;
+  int chroma_qp_offset = 0;
+  int aud = 0;
+  int vui = 1;
+};
+
+struct FrameStats {
+  int type = 0;  // SliceType
+  int qp = 0;
+  int bytes = 0;
+  double psnr_y = 0;
+};
+
+class CpuEncoder {
+ public:
+  explicit CpuEncoder(const EncoderConfig& cfg);
+  // Encode frames of one closed-GOP segment (I420, tightly packed, width*height*3/2 bytes each).
+  // Returns the Annex-B stream (SPS/PPS + slices).  idr_pic_id distinguishes
+  // consecutive segments once concatenated.
+  std::vector<uint8_t> encode(const uint8_t* frames, int nframes, int idr_pic_id);
+  const std::vector<FrameStats>& stats() const { return stats_; }
+  // Reconstructed (decoded, deblocked, cropped) frames of the last encode()
+  const std::vector<uint8_t>& recon() const { return recon_; }
+  // Encoder-side (pre-deblocking) reconstruction in coded size (Y then U, V per frame):
+  // must equal the decoder's output with the loop filter disabled.
+  const std::vector<uint8_t>& recon_unfiltered() const { return recon_unf_; }
+
+ private:
+  EncoderConfig cfg_;
+  std::vector<FrameStats> stats_;
+  std::vector<uint8_t> recon_;
+  std::vector<uint8_t> recon_unf_;
+};
+
+// Shared helpers exposed for tests
+SPS make_sps(const EncoderConfig& cfg);
+PPS make_pps(const EncoderConfig& cfg);
+
+}  // namespace h264
+}  // namespace mivc

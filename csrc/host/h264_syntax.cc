@@ -1,0 +1,355 @@
+#include "h264_syntax.h"
+
+#include <cmath>
+#include <stdexcept>
+
+namespace mivc {
+namespace h264 {
+
+static bool high_profile(int p) {
+  return p == 100 || p == 110 || p == 122 || p == 244 || p == 44 || p == 83 || p == 86 || p == 118 ||
+         p == 128 || p == 138 || p == 139 || p == 134 || p == 135;
+}
+
+void write_sps(BitWriter& bw, const SPS& s) {
+  bw.put(s.profile_idc, 8);
+  bw.put(s.constraint_flags & 0xFC, 8);  // 6 constraint flags + reserved_zero_2bits
+  bw.put(s.level_idc, 8);
+  bw.put_ue(s.sps_id);
+  if (high_profile(s.profile_idc)) {
+    bw.put_ue(s.chroma_format_idc);
+    bw.put_ue(s.bit_depth_luma - 8);
+    bw.put_ue(s.bit_depth_chroma - 8);
+    bw.put_bit(0);  // qpprime_y_zero_transform_bypass_flag
+    bw.put_bit(0);  // seq_scaling_matrix_present_flag
+  }
+  bw.put_ue(s.log2_max_frame_num - 4);
+  bw.put_ue(s.poc_type);
+  if (s.poc_type == 0) bw.put_ue(s.log2_max_poc_lsb - 4);
+  if (s.poc_type == 1) throw std::runtime_error("poc_type 1 not written");
+  bw.put_ue(s.max_num_ref_frames);
+  bw.put_bit(s.gaps_allowed);
+  bw.put_ue(s.width_mbs - 1);
+  bw.put_ue(s.height_mbs - 1);
+  bw.put_bit(1);  // frame_mbs_only_flag
+  bw.put_bit(s.direct_8x8_inference);
+  bool crop = s.crop_left || s.crop_right || s.crop_top || s.crop_bottom;
+  bw.put_bit(crop);
+  if (crop) {
+    bw.put_ue(s.crop_left);
+    bw.put_ue(s.crop_right);
+    bw.put_ue(s.crop_top);
+    bw.put_ue(s.crop_bottom);
+  }
+  bw.put_bit(s.vui_present);
+  if (s.vui_present) {
+    bw.put_bit(0);  // aspect_ratio_info_present_flag
+    bw.put_bit(0);  // overscan_info_present_flag
+    bw.put_bit(0);  // video_signal_type_present_flag
+    bw.put_bit(0);  // chroma_loc_info_present_flag
+    bw.put_bit(1);  // timing_info_present_flag
+    bw.put(s.num_units_in_tick, 32);
+    bw.put(s.time_scale, 32);
+    bw.put_bit(s.fixed_frame_rate);
+    bw.put_bit(0);  // nal_hrd_parameters_present_flag
+    bw.put_bit(0);  // vcl_hrd_parameters_present_flag
+    bw.put_bit(0);  // pic_struct_present_flag
+    bw.put_bit(1);  // bitstream_restriction_flag
+    bw.put_bit(1);  // motion_vectors_over_pic_boundaries_flag
+    bw.put_ue(0);   // max_bytes_per_pic_denom
+    bw.put_ue(0);   // max_bits_per_mb_denom
+    bw.put_ue(16);  // log2_max_mv_length_horizontal
+    bw.put_ue(16);  // log2_max_mv_length_vertical
+    bw.put_ue(0);   // max_num_reorder_frames (no B-frames)
+    bw.put_ue(s.max_num_ref_frames);  // max_dec_frame_buffering
+  }
+  bw.trailing();
+}
+
+void write_pps(BitWriter& bw, const PPS& p) {
+  bw.put_ue(p.pps_id);
+  bw.put_ue(p.sps_id);
+  bw.put_bit(p.entropy_coding_mode);
+  bw.put_bit(p.bottom_field_pic_order_present);
+  bw.put_ue(0);  // num_slice_groups_minus1
+  bw.put_ue(p.num_ref_idx_l0_default - 1);
+  bw.put_ue(p.num_ref_idx_l1_default - 1);
+  bw.put_bit(p.weighted_pred);
+  bw.put(p.weighted_bipred_idc, 2);
+  bw.put_se(p.pic_init_qp - 26);
+  bw.put_se(p.pic_init_qs - 26);
+  bw.put_se(p.chroma_qp_index_offset);
+  bw.put_bit(p.deblocking_filter_control_present);
+  bw.put_bit(p.constrained_intra_pred);
+  bw.put_bit(p.redundant_pic_cnt_present);
+  if (p.transform_8x8_mode || p.second_chroma_qp_index_offset != p.chroma_qp_index_offset) {
+    bw.put_bit(p.transform_8x8_mode);
+    bw.put_bit(0);  // pic_scaling_matrix_present_flag
+    bw.put_se(p.second_chroma_qp_index_offset);
+  }
+  bw.trailing();
+}
+
+void write_slice_header(BitWriter& bw, const SliceHeader& h, const SPS& s, const PPS& p) {
+  bw.put_ue(h.first_mb);
+  bw.put_ue(h.slice_type + 5);
+  bw.put_ue(h.pps_id);
+  bw.put(h.frame_num & ((1u << s.log2_max_frame_num) - 1), s.log2_max_frame_num);
+  if (h.nal_unit_type == NAL_IDR) bw.put_ue(h.idr_pic_id);
+  if (s.poc_type == 0) bw.put(h.poc_lsb & ((1u << s.log2_max_poc_lsb) - 1), s.log2_max_poc_lsb);
+  if (h.slice_type == SLICE_P) {
+    bw.put_bit(h.num_ref_idx_override);
+    if (h.num_ref_idx_override) bw.put_ue(h.num_ref_idx_l0_active - 1);
+    bw.put_bit(0);  // ref_pic_list_modification_flag_l0
+  }
+  if (h.nal_ref_idc) {
+    if (h.nal_unit_type == NAL_IDR) {
+      bw.put_bit(h.no_output_of_prior_pics);
+      bw.put_bit(h.long_term_reference);
+    } else {
+      bw.put_bit(0);  // adaptive_ref_pic_marking_mode_flag (sliding window)
+    }
+  }
+  if (p.entropy_coding_mode && h.slice_type != SLICE_I) bw.put_ue(h.cabac_init_idc);
+  bw.put_se(h.slice_qp_delta);
+  if (p.deblocking_filter_control_present) {
+    bw.put_ue(h.disable_deblocking_filter_idc);
+    if (h.disable_deblocking_filter_idc != 1) {
+      bw.put_se(h.alpha_offset_div2);
+      bw.put_se(h.beta_offset_div2);
+    }
+  }
+}
+
+static void skip_scaling_list(BitReader& br, int size) {
+  int last = 8, next = 8;
+  for (int j = 0; j < size; ++j) {
+    if (next != 0) {
+      int delta = br.get_se();
+      next = (last + delta + 256) % 256;
+    }
+    last = next == 0 ? last : next;
+  }
+}
+
+static void skip_hrd(BitReader& br) {
+  int cpb_cnt = br.get_ue() + 1;
+  br.get(4);
+  br.get(4);
+  for (int i = 0; i < cpb_cnt; ++i) {
+    br.get_ue();
+    br.get_ue();
+    br.get_bit();
+  }
+  br.get(5);
+  br.get(5);
+  br.get(5);
+  br.get(5);
+}
+
+SPS parse_sps(BitReader& br) {
+  SPS s;
+  s.profile_idc = br.get(8);
+  s.constraint_flags = br.get(8);
+  s.level_idc = br.get(8);
+  s.sps_id = br.get_ue();
+  if (s.sps_id > 31) throw std::runtime_error("bad sps id");
+  if (high_profile(s.profile_idc)) {
+    s.chroma_format_idc = br.get_ue();
+    if (s.chroma_format_idc == 3) br.get_bit();
+    s.bit_depth_luma = br.get_ue() + 8;
+    s.bit_depth_chroma = br.get_ue() + 8;
+    br.get_bit();
+    if (br.get_bit()) {
+      int n = s.chroma_format_idc != 3 ? 8 : 12;
+      for (int i = 0; i < n; ++i)
+        if (br.get_bit()) skip_scaling_list(br, i < 6 ? 16 : 64);
+      throw std::runtime_error("scaling matrices not supported");
+    }
+  }
+  if (s.chroma_format_idc != 1 || s.bit_depth_luma != 8) throw std::runtime_error("only 8-bit 4:2:0 supported");
+  s.log2_max_frame_num = br.get_ue() + 4;
+  s.poc_type = br.get_ue();
+  if (s.poc_type == 0) {
+    s.log2_max_poc_lsb = br.get_ue() + 4;
+  } else if (s.poc_type == 1) {
+    s.delta_pic_order_always_zero = br.get_bit();
+    br.get_se();
+    br.get_se();
+    int n = br.get_ue();
+    for (int i = 0; i < n; ++i) br.get_se();
+  }
+  s.max_num_ref_frames = br.get_ue();
+  s.gaps_allowed = br.get_bit();
+  s.width_mbs = br.get_ue() + 1;
+  s.height_mbs = br.get_ue() + 1;
+  s.frame_mbs_only = br.get_bit();
+  if (!s.frame_mbs_only) throw std::runtime_error("interlaced streams not supported");
+  s.direct_8x8_inference = br.get_bit();
+  if (br.get_bit()) {
+    s.crop_left = br.get_ue();
+    s.crop_right = br.get_ue();
+    s.crop_top = br.get_ue();
+    s.crop_bottom = br.get_ue();
+  }
+  s.vui_present = br.get_bit();
+  if (s.vui_present) {
+    if (br.get_bit()) {  // aspect_ratio_info_present_flag
+      if (br.get(8) == 255) {
+        br.get(16);
+        br.get(16);
+      }
+    }
+    if (br.get_bit()) br.get_bit();  // overscan
+    if (br.get_bit()) {              // video_signal_type
+      br.get(3);
+      br.get_bit();
+      if (br.get_bit()) {
+        br.get(8);
+        br.get(8);
+        br.get(8);
+      }
+    }
+    if (br.get_bit()) {
+      br.get_ue();
+      br.get_ue();
+    }
+    if (br.get_bit()) {
+      s.num_units_in_tick = br.get(32);
+      s.time_scale = br.get(32);
+      s.fixed_frame_rate = br.get_bit();
+    }
+    int nal_hrd = br.get_bit();
+    if (nal_hrd) skip_hrd(br);
+    int vcl_hrd = br.get_bit();
+    if (vcl_hrd) skip_hrd(br);
+    if (nal_hrd || vcl_hrd) br.get_bit();
+    br.get_bit();  // pic_struct_present_flag
+    if (br.get_bit()) {
+      br.get_bit();
+      for (int i = 0; i < 6; ++i) br.get_ue();
+    }
+  }
+  return s;
+}
+
+PPS parse_pps(BitReader& br, const SPS* sps_table) {
+  PPS p;
+  p.pps_id = br.get_ue();
+  p.sps_id = br.get_ue();
+  if (p.pps_id > 255 || p.sps_id > 31) throw std::runtime_error("bad pps");
+  p.entropy_coding_mode = br.get_bit();
+  p.bottom_field_pic_order_present = br.get_bit();
+  if (br.get_ue() != 0) throw std::runtime_error("slice groups (FMO) not supported");
+  p.num_ref_idx_l0_default = br.get_ue() + 1;
+  p.num_ref_idx_l1_default = br.get_ue() + 1;
+  p.weighted_pred = br.get_bit();
+  p.weighted_bipred_idc = br.get(2);
+  p.pic_init_qp = 26 + br.get_se();
+  p.pic_init_qs = 26 + br.get_se();
+  p.chroma_qp_index_offset = br.get_se();
+  p.deblocking_filter_control_present = br.get_bit();
+  p.constrained_intra_pred = br.get_bit();
+  p.redundant_pic_cnt_present = br.get_bit();
+  p.second_chroma_qp_index_offset = p.chroma_qp_index_offset;
+  if (br.more_rbsp_data()) {
+    p.transform_8x8_mode = br.get_bit();
+    if (br.get_bit()) throw std::runtime_error("pic scaling matrices not supported");
+    p.second_chroma_qp_index_offset = br.get_se();
+  }
+  (void)sps_table;
+  return p;
+}
+
+SliceHeader parse_slice_header(BitReader& br, int nal_unit_type, int nal_ref_idc, const SPS* sps_table,
+                               const PPS* pps_table) {
+  SliceHeader h;
+  h.nal_unit_type = nal_unit_type;
+  h.nal_ref_idc = nal_ref_idc;
+  h.first_mb = br.get_ue();
+  int st = br.get_ue();
+  h.slice_type = st % 5;
+  if (h.slice_type > 2) throw std::runtime_error("SP/SI slices not supported");
+  h.pps_id = br.get_ue();
+  const PPS& p = pps_table[h.pps_id];
+  const SPS& s = sps_table[p.sps_id];
+  h.frame_num = br.get(s.log2_max_frame_num);
+  if (nal_unit_type == NAL_IDR) h.idr_pic_id = br.get_ue();
+  if (s.poc_type == 0) {
+    h.poc_lsb = br.get(s.log2_max_poc_lsb);
+    if (p.bottom_field_pic_order_present) br.get_se();
+  }
+  if (s.poc_type == 1 && !s.delta_pic_order_always_zero) {
+    br.get_se();
+    if (p.bottom_field_pic_order_present) br.get_se();
+  }
+  if (p.redundant_pic_cnt_present) br.get_ue();
+  if (h.slice_type == SLICE_B) throw std::runtime_error("B slices not supported");
+  h.num_ref_idx_l0_active = p.num_ref_idx_l0_default;
+  if (h.slice_type == SLICE_P) {
+    h.num_ref_idx_override = br.get_bit();
+    if (h.num_ref_idx_override) h.num_ref_idx_l0_active = br.get_ue() + 1;
+    if (br.get_bit()) {  // ref_pic_list_modification_flag_l0
+      int idc;
+      do {
+        idc = br.get_ue();
+        if (idc == 0 || idc == 1 || idc == 2) br.get_ue();
+      } while (idc != 3);
+      // our decoder keeps a single short-term reference; reordering is a no-op then
+    }
+  }
+  if (p.weighted_pred && h.slice_type == SLICE_P) throw std::runtime_error("weighted prediction not supported");
+  if (nal_ref_idc) {
+    if (nal_unit_type == NAL_IDR) {
+      h.no_output_of_prior_pics = br.get_bit();
+      h.long_term_reference = br.get_bit();
+    } else {
+      h.adaptive_ref_pic_marking = br.get_bit();
+      if (h.adaptive_ref_pic_marking) {
+        int op;
+        do {
+          op = br.get_ue();
+          if (op == 1 || op == 3) br.get_ue();
+          if (op == 2) br.get_ue();
+          if (op == 3 || op == 6) br.get_ue();
+          if (op == 4) br.get_ue();
+        } while (op != 0);
+      }
+    }
+  }
+  if (p.entropy_coding_mode && h.slice_type != SLICE_I) h.cabac_init_idc = br.get_ue();
+  h.slice_qp_delta = br.get_se();
+  h.qp = p.pic_init_qp + h.slice_qp_delta;
+  if (p.deblocking_filter_control_present) {
+    h.disable_deblocking_filter_idc = br.get_ue();
+    if (h.disable_deblocking_filter_idc != 1) {
+      h.alpha_offset_div2 = br.get_se();
+      h.beta_offset_div2 = br.get_se();
+    }
+  }
+  return h;
+}
+
+int choose_level(int width_mbs, int height_mbs, double fps) {
+  struct L {
+    int idc;
+    double max_mbps;
+    int max_fs;
+  };
+  static const L lv[] = {{10, 1485, 99},        {11, 3000, 396},       {12, 6000, 396},
+                         {13, 11880, 396},      {20, 11880, 396},      {21, 19800, 792},
+                         {22, 20250, 1620},     {30, 40500, 1620},     {31, 108000, 3600},
+                         {32, 216000, 5120},    {40, 245760, 8192},    {42, 522240, 8704},
+                         {50, 589824, 22080},   {51, 983040, 36864},   {52, 2073600, 36864},
+                         {60, 4177920, 139264}, {61, 8355840, 139264}, {62, 16711680, 139264}};
+  int fs = width_mbs * height_mbs;
+  double mbps = fs * fps;
+  for (const L& l : lv) {
+    double maxdim = std::sqrt(8.0 * l.max_fs);
+    if (fs <= l.max_fs && mbps <= l.max_mbps && width_mbs <= maxdim && height_mbs <= maxdim) return l.idc;
+  }
+  return 62;
+}
+
+}  // namespace h264
+}  // namespace mivc

@@ -1,0 +1,89 @@
+// H.264 high-level syntax: sequence/picture parameter sets and slice headers
+// (clauses 7.3.2.1, 7.3.2.2, 7.3.3) -- writer for our encoder and parser for the
+// independent decoder.
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "bitstream.h"
+
+namespace mivc {
+namespace h264 {
+
+enum NalType { NAL_SLICE = 1, NAL_IDR = 5, NAL_SEI = 6, NAL_SPS = 7, NAL_PPS = 8, NAL_AUD = 9 };
+enum SliceType { SLICE_P = 0, SLICE_B = 1, SLICE_I = 2 };
+
+struct SPS {
+  int profile_idc = 66;
+  int constraint_flags = 0xC0;  // constraint_set0..5 (bit7 = set0); 0xC0 = Constrained Baseline
+  int level_idc = 40;
+  int sps_id = 0;
+  int chroma_format_idc = 1;
+  int bit_depth_luma = 8, bit_depth_chroma = 8;
+  int log2_max_frame_num = 16;
+  int poc_type = 2;
+  int log2_max_poc_lsb = 8;
+  int max_num_ref_frames = 1;
+  int gaps_allowed = 0;
+  int width_mbs = 0, height_mbs = 0;
+  int frame_mbs_only = 1;
+  int direct_8x8_inference = 1;
+  int crop_left = 0, crop_right = 0, crop_top = 0, crop_bottom = 0;  // in crop units (2 for 4:2:0)
+  // VUI timing (optional)
+  int vui_present = 0;
+  uint32_t num_units_in_tick = 1, time_scale = 60;
+  int fixed_frame_rate = 1;
+  // poc type 1 fields (parsed only)
+  int delta_pic_order_always_zero = 0;
+};
+
+struct PPS {
+  int pps_id = 0, sps_id = 0;
+  int entropy_coding_mode = 0;  // 0 = CAVLC, 1 = CABAC
+  int bottom_field_pic_order_present = 0;
+  int num_ref_idx_l0_default = 1, num_ref_idx_l1_default = 1;
+  int weighted_pred = 0, weighted_bipred_idc = 0;
+  int pic_init_qp = 26, pic_init_qs = 26;
+  int chroma_qp_index_offset = 0;
+  int deblocking_filter_control_present = 1;
+  int constrained_intra_pred = 0;
+  int redundant_pic_cnt_present = 0;
+  int transform_8x8_mode = 0;
+  int second_chroma_qp_index_offset = 0;
+};
+
+struct SliceHeader {
+  int nal_unit_type = NAL_IDR;
+  int nal_ref_idc = 3;
+  int first_mb = 0;
+  int slice_type = SLICE_I;  // 0..2 (we write +5: all slices of the picture share the type)
+  int pps_id = 0;
+  int frame_num = 0;
+  int idr_pic_id = 0;
+  int poc_lsb = 0;
+  int num_ref_idx_l0_active = 1;
+  int num_ref_idx_override = 0;
+  int slice_qp_delta = 0;
+  int disable_deblocking_filter_idc = 0;
+  int alpha_offset_div2 = 0, beta_offset_div2 = 0;
+  int cabac_init_idc = 0;
+  int no_output_of_prior_pics = 0, long_term_reference = 0;
+  int adaptive_ref_pic_marking = 0;
+  // derived by the parser
+  int qp = 26;
+};
+
+void write_sps(BitWriter& bw, const SPS& s);
+void write_pps(BitWriter& bw, const PPS& p);
+void write_slice_header(BitWriter& bw, const SliceHeader& h, const SPS& s, const PPS& p);
+
+SPS parse_sps(BitReader& br);
+PPS parse_pps(BitReader& br, const SPS* sps_table);
+SliceHeader parse_slice_header(BitReader& br, int nal_unit_type, int nal_ref_idc, const SPS* sps_table,
+                               const PPS* pps_table);
+
+// Pick level_idc from picture size and frame rate (Table A-1 MaxFS / MaxMBPS).
+int choose_level(int width_mbs, int height_mbs, double fps);
+
+}  // namespace h264
+}  // namespace mivc
