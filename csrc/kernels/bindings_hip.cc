@@ -1,0 +1,103 @@
+// pybind11 shims for the gfx950 kernels.  Tensors cross the boundary as raw
+// device pointers (torch.Tensor.data_ptr()) and the HIP stream as an integer
+// (torch.cuda.current_stream().cuda_stream), so this module needs neither torch
+// headers nor a JIT: it is built in-tree by govideocompressor_amd/_build.py.
+#include <pybind11/pybind11.h>
+
+#include <cstdint>
+
+namespace py = pybind11;
+
+extern "C" {
+void mivc_launch_synth(uint8_t* y, uint8_t* u, uint8_t* v, int width, int height, int slots, int frames, int frame0,
+                       uint32_t seed, void* stream);
+void mivc_launch_prep(const uint8_t* in_y, const uint8_t* in_u, const uint8_t* in_v, int w, int h,
+                      int64_t in_stride_y, int64_t in_stride_c, int nframes, uint8_t* out_y, uint8_t* out_u,
+                      uint8_t* out_v, int ow, int oh, int W, int H, void* stream);
+void mivc_launch_rgb_to_i420(const uint8_t* rgb, int w, int h, int nframes, uint8_t* y, uint8_t* u, uint8_t* v,
+                             void* stream);
+void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref_y, const int16_t* pred_mv,
+                    int16_t* out_mv, int* out_cost, uint8_t* out_pred, int* out_intra_cost, const int* qp, int range,
+                    int subpel, void* stream);
+void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* src_u,
+                              const uint8_t* src_v, const uint8_t* ref_y, const uint8_t* ref_u, const uint8_t* ref_v,
+                              uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const uint8_t* pred_y,
+                              const int16_t* mv, const int* me_cost, const int* intra_cost, const int* qp,
+                              int chroma_qp_offset, void* hdr, int16_t* coef, uint8_t* nz, uint8_t* intra_flag,
+                              int* intra_count, void* stream);
+void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* src_u,
+                              const uint8_t* src_v, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const int* qp,
+                              int chroma_qp_offset, void* hdr, int16_t* coef, uint8_t* nz,
+                              const uint8_t* intra_flag, const int* intra_count, int* ticket, int* progress, int* err,
+                              int use_i4x4, void* stream);
+void mivc_launch_deblock(int B, int wmb, int hmb, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const void* hdr,
+                         const uint8_t* nz, int chroma_qp_offset, int alpha_off, int beta_off, int* ticket,
+                         int* progress, int* err, void* stream);
+void mivc_launch_sse(int B, int W, int H, int w, int h, const uint8_t* sy, const uint8_t* su, const uint8_t* sv,
+                     const uint8_t* ry, const uint8_t* ru, const uint8_t* rv, unsigned long long* sse,
+                     float* ssim_sum, void* stream);
+}
+
+namespace {
+template <class T>
+T* P(uintptr_t p) {
+  return reinterpret_cast<T*>(p);
+}
+void* S(uintptr_t s) { return reinterpret_cast<void*>(s); }
+}  // namespace
+
+PYBIND11_MODULE(_hip, m) {
+  m.doc() = "govideocompressor_amd gfx950 kernels (raw-pointer launch shims)";
+  m.attr("arch") = "gfx950";
+
+  m.def("synth", [](uintptr_t y, uintptr_t u, uintptr_t v, int w, int h, int slots, int frames, int frame0,
+                    uint32_t seed, uintptr_t stream) {
+    mivc_launch_synth(P<uint8_t>(y), P<uint8_t>(u), P<uint8_t>(v), w, h, slots, frames, frame0, seed, S(stream));
+  });
+  m.def("prep", [](uintptr_t iy, uintptr_t iu, uintptr_t iv, int w, int h, int64_t sy, int64_t sc, int n,
+                   uintptr_t oy, uintptr_t ou, uintptr_t ov, int ow, int oh, int W, int H, uintptr_t stream) {
+    mivc_launch_prep(P<uint8_t>(iy), P<uint8_t>(iu), P<uint8_t>(iv), w, h, sy, sc, n, P<uint8_t>(oy), P<uint8_t>(ou),
+                     P<uint8_t>(ov), ow, oh, W, H, S(stream));
+  });
+  m.def("rgb_to_i420", [](uintptr_t rgb, int w, int h, int n, uintptr_t y, uintptr_t u, uintptr_t v,
+                          uintptr_t stream) {
+    mivc_launch_rgb_to_i420(P<uint8_t>(rgb), w, h, n, P<uint8_t>(y), P<uint8_t>(u), P<uint8_t>(v), S(stream));
+  });
+  m.def("me", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref, uintptr_t pred_mv, uintptr_t out_mv,
+                 uintptr_t out_cost, uintptr_t out_pred, uintptr_t out_intra, uintptr_t qp, int range, int subpel,
+                 uintptr_t stream) {
+    mivc_launch_me(B, wmb, hmb, P<uint8_t>(src), P<uint8_t>(ref), P<int16_t>(pred_mv), P<int16_t>(out_mv),
+                   P<int>(out_cost), P<uint8_t>(out_pred), P<int>(out_intra), P<int>(qp), range, subpel, S(stream));
+  });
+  m.def("encode_inter",
+        [](int B, int wmb, int hmb, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t fy, uintptr_t fu,
+           uintptr_t fv, uintptr_t ry, uintptr_t ru, uintptr_t rv, uintptr_t pred, uintptr_t mv, uintptr_t me_cost,
+           uintptr_t intra_cost, uintptr_t qp, int cqo, uintptr_t hdr, uintptr_t coef, uintptr_t nz,
+           uintptr_t intra_flag, uintptr_t intra_count, uintptr_t stream) {
+          mivc_launch_encode_inter(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), P<uint8_t>(fy),
+                                   P<uint8_t>(fu), P<uint8_t>(fv), P<uint8_t>(ry), P<uint8_t>(ru), P<uint8_t>(rv),
+                                   P<uint8_t>(pred), P<int16_t>(mv), P<int>(me_cost), P<int>(intra_cost), P<int>(qp),
+                                   cqo, P<void>(hdr), P<int16_t>(coef), P<uint8_t>(nz), P<uint8_t>(intra_flag),
+                                   P<int>(intra_count), S(stream));
+        });
+  m.def("encode_intra", [](int B, int wmb, int hmb, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t ry,
+                           uintptr_t ru, uintptr_t rv, uintptr_t qp, int cqo, uintptr_t hdr, uintptr_t coef,
+                           uintptr_t nz, uintptr_t intra_flag, uintptr_t intra_count, uintptr_t ticket,
+                           uintptr_t progress, uintptr_t err, int use_i4x4, uintptr_t stream) {
+    mivc_launch_encode_intra(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), P<uint8_t>(ry),
+                             P<uint8_t>(ru), P<uint8_t>(rv), P<int>(qp), cqo, P<void>(hdr), P<int16_t>(coef),
+                             P<uint8_t>(nz), P<uint8_t>(intra_flag), P<int>(intra_count), P<int>(ticket),
+                             P<int>(progress), P<int>(err), use_i4x4, S(stream));
+  });
+  m.def("deblock", [](int B, int wmb, int hmb, uintptr_t ry, uintptr_t ru, uintptr_t rv, uintptr_t hdr, uintptr_t nz,
+                      int cqo, int alpha_off, int beta_off, uintptr_t ticket, uintptr_t progress, uintptr_t err,
+                      uintptr_t stream) {
+    mivc_launch_deblock(B, wmb, hmb, P<uint8_t>(ry), P<uint8_t>(ru), P<uint8_t>(rv), P<void>(hdr), P<uint8_t>(nz),
+                        cqo, alpha_off, beta_off, P<int>(ticket), P<int>(progress), P<int>(err), S(stream));
+  });
+  m.def("sse", [](int B, int W, int H, int w, int h, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t ry,
+                  uintptr_t ru, uintptr_t rv, uintptr_t sse, uintptr_t ssim, uintptr_t stream) {
+    mivc_launch_sse(B, W, H, w, h, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), P<uint8_t>(ry), P<uint8_t>(ru),
+                    P<uint8_t>(rv), P<unsigned long long>(sse), P<float>(ssim), S(stream));
+  });
+}

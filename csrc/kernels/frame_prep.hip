@@ -1,0 +1,101 @@
+// Frame preparation: display-size I420 -> coded-size (multiple of 16) planar
+// frames with edge replication, optional separable resampling (the `-s WxH`
+// scaling the reference's operators passed to ffmpeg, server.go:87-90), and a
+// packed-RGB -> I420 colour conversion (BT.601 limited range) entry point.
+// SURVEY.md K-C2 (csc_scale).
+#include "kcommon.h"
+
+namespace mivc {
+namespace gpu {
+
+struct PrepArgs {
+  const uint8_t* in_y;  // [N, h, w]
+  const uint8_t* in_u;  // [N, h/2, w/2]
+  const uint8_t* in_v;
+  int w, h;             // input size
+  int64_t in_frame_stride_y, in_frame_stride_c;  // elements between consecutive input frames
+  uint8_t* out_y;       // [N, H, W] coded
+  uint8_t* out_u;
+  uint8_t* out_v;
+  int ow, oh;           // output display size (== w,h when not scaling)
+  int W, H;             // coded size
+};
+
+// bilinear sample of an 8-bit plane at (fx, fy) in input pixel units
+__device__ __forceinline__ int bilinear(const uint8_t* p, int w, int h, float fx, float fy) {
+  fx = fminf(fmaxf(fx, 0.f), static_cast<float>(w - 1));
+  fy = fminf(fmaxf(fy, 0.f), static_cast<float>(h - 1));
+  int x0 = static_cast<int>(fx), y0 = static_cast<int>(fy);
+  int x1 = min(x0 + 1, w - 1), y1 = min(y0 + 1, h - 1);
+  float tx = fx - x0, ty = fy - y0;
+  float a = p[y0 * w + x0] * (1 - tx) + p[y0 * w + x1] * tx;
+  float b = p[y1 * w + x0] * (1 - tx) + p[y1 * w + x1] * tx;
+  return static_cast<int>(a * (1 - ty) + b * ty + 0.5f);
+}
+
+__global__ void prep_plane(PrepArgs a, int plane) {
+  int x = blockIdx.x * blockDim.x + threadIdx.x;
+  int y = blockIdx.y;
+  int n = blockIdx.z;
+  int sh = plane ? 1 : 0;
+  int W = a.W >> sh, H = a.H >> sh;
+  if (x >= W) return;
+  int w = a.w >> sh, h = a.h >> sh, ow = a.ow >> sh, oh = a.oh >> sh;
+  const uint8_t* in = plane == 0 ? a.in_y : (plane == 1 ? a.in_u : a.in_v);
+  in += n * (plane ? a.in_frame_stride_c : a.in_frame_stride_y);
+  uint8_t* out = plane == 0 ? a.out_y : (plane == 1 ? a.out_u : a.out_v);
+  out += static_cast<size_t>(n) * W * H;
+  int cx = min(x, ow - 1), cy = min(y, oh - 1);  // edge replication into the coded padding
+  int v;
+  if (ow == w && oh == h) {
+    v = in[static_cast<size_t>(cy) * w + cx];
+  } else {
+    float fx = (cx + 0.5f) * w / ow - 0.5f, fy = (cy + 0.5f) * h / oh - 0.5f;
+    v = bilinear(in, w, h, fx, fy);
+  }
+  out[static_cast<size_t>(y) * W + x] = static_cast<uint8_t>(v);
+}
+
+// packed RGB24 [N, h, w, 3] -> I420 display-size planes (BT.601 limited range)
+__global__ void rgb_to_i420(const uint8_t* rgb, int w, int h, uint8_t* oy, uint8_t* ou, uint8_t* ov) {
+  int x2 = blockIdx.x * blockDim.x + threadIdx.x;  // chroma column
+  int y2 = blockIdx.y;
+  int n = blockIdx.z;
+  if (x2 >= w / 2) return;
+  const uint8_t* f = rgb + static_cast<size_t>(n) * w * h * 3;
+  float su = 0, sv = 0;
+  for (int dy = 0; dy < 2; ++dy)
+    for (int dx = 0; dx < 2; ++dx) {
+      int x = 2 * x2 + dx, y = 2 * y2 + dy;
+      const uint8_t* p = f + (static_cast<size_t>(y) * w + x) * 3;
+      float r = p[0], g = p[1], b = p[2];
+      float Y = 16.f + 0.257f * r + 0.504f * g + 0.098f * b;
+      su += 128.f - 0.148f * r - 0.291f * g + 0.439f * b;
+      sv += 128.f + 0.439f * r - 0.368f * g - 0.071f * b;
+      oy[static_cast<size_t>(n) * w * h + static_cast<size_t>(y) * w + x] = static_cast<uint8_t>(fminf(fmaxf(Y + 0.5f, 0.f), 255.f));
+    }
+  size_t ci = static_cast<size_t>(n) * (w / 2) * (h / 2) + static_cast<size_t>(y2) * (w / 2) + x2;
+  ou[ci] = static_cast<uint8_t>(fminf(fmaxf(su * 0.25f + 0.5f, 0.f), 255.f));
+  ov[ci] = static_cast<uint8_t>(fminf(fmaxf(sv * 0.25f + 0.5f, 0.f), 255.f));
+}
+
+}  // namespace gpu
+}  // namespace mivc
+
+using namespace mivc::gpu;
+
+extern "C" void mivc_launch_prep(const uint8_t* in_y, const uint8_t* in_u, const uint8_t* in_v, int w, int h,
+                                 int64_t in_stride_y, int64_t in_stride_c, int nframes, uint8_t* out_y, uint8_t* out_u,
+                                 uint8_t* out_v, int ow, int oh, int W, int H, void* stream) {
+  PrepArgs a{in_y, in_u, in_v, w, h, in_stride_y, in_stride_c, out_y, out_u, out_v, ow, oh, W, H};
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(prep_plane, dim3((W + 255) / 256, H, nframes), dim3(256), 0, s, a, 0);
+  hipLaunchKernelGGL(prep_plane, dim3((W / 2 + 255) / 256, H / 2, nframes), dim3(256), 0, s, a, 1);
+  hipLaunchKernelGGL(prep_plane, dim3((W / 2 + 255) / 256, H / 2, nframes), dim3(256), 0, s, a, 2);
+}
+
+extern "C" void mivc_launch_rgb_to_i420(const uint8_t* rgb, int w, int h, int nframes, uint8_t* y, uint8_t* u,
+                                        uint8_t* v, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(rgb_to_i420, dim3((w / 2 + 127) / 128, h / 2, nframes), dim3(128), 0, s, rgb, w, h, y, u, v);
+}

@@ -101,7 +101,7 @@ def build_hip(nproc: int = 8) -> str:
         "-fPIC",
         "-fvisibility=hidden",
         "-munsafe-fp-atomics",
-        "-Wno-unused-result",
+        "-Wno-unused-result", "-Wno-unused-value",
     ]
     jobs = []
     objs = []

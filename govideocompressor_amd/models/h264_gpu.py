@@ -1,0 +1,285 @@
+"""MI355X H.264 encoder: B closed-GOP segments encoded concurrently on one GPU.
+
+This is the MI355X-native replacement of the reference worker's codec call
+(``ffmpeg -i <idx>.mp4 -threads 4 -vcodec libx264 c<idx>.mp4``, client.go:101-130;
+preset expansion at server.go:67-71).  Where the reference runs one segment per
+3-vCPU droplet, here a *batch* of segments shares one GPU: every kernel launch
+covers all B slots, so the serial wavefront stages (intra coding, deblocking)
+still expose B x (MB rows) independent waves.
+
+Per frame step t (frame t of every slot):
+  prep (pad/scale) -> [P: me -> encode_inter] -> encode_intra (wavefront)
+  -> deblock (wavefront) -> metrics, then the decision records (MbHeader +
+  coefficients) are copied to pinned host memory on a side stream and CAVLC
+  coded by a host thread pool while the GPU runs step t+1.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import math
+import os
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ..ops import native
+
+MB_HDR_BYTES = 48
+COEF_PER_MB = 408
+
+
+@dataclass
+class H264Params:
+    width: int
+    height: int
+    fps: float = 30.0
+    crf: float | None = 23.0       # CRF (None -> fixed qp)
+    qp: int = 26                    # used when crf is None
+    ip_offset: int = 3              # I-frame QP = P QP - ip_offset (ipratio 1.4)
+    me_range: int = 16
+    subpel: int = 2
+    i4x4: bool = True
+    deblock: bool = True
+    chroma_qp_offset: int = 0
+    vui: bool = True
+
+    def host_cfg(self) -> dict:
+        return dict(width=self.width, height=self.height, fps=self.fps, qp=self.qp,
+                    deblock=int(self.deblock), chroma_qp_offset=self.chroma_qp_offset,
+                    vui=int(self.vui))
+
+    def frame_qps(self) -> tuple[int, int]:
+        """(qp_I, qp_P).  CRF maps to the P-frame QP (x264 scale without MB-tree);
+        per-frame adaptation is done by :mod:`govideocompressor_amd.rc`."""
+        qp_p = int(round(self.crf)) if self.crf is not None else int(self.qp)
+        qp_p = max(0, min(51, qp_p))
+        return max(0, qp_p - self.ip_offset), qp_p
+
+
+@dataclass
+class SegmentResult:
+    bitstream: bytes
+    frames: int
+    bits: list[int] = field(default_factory=list)
+    psnr_y: float = 0.0
+    psnr_u: float = 0.0
+    psnr_v: float = 0.0
+    ssim_y: float = 0.0
+
+
+def _resolve(device) -> torch.device:
+    d = torch.device(device)
+    if d.type == "cuda" and d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return d
+
+
+class GpuH264Encoder:
+    """Batched gfx950 H.264 encoder (Constrained Baseline profile, CAVLC)."""
+
+    def __init__(self, params: H264Params, slots: int, device: str | torch.device = "cuda",
+                 entropy_threads: int | None = None):
+        if params.width % 2 or params.height % 2:
+            raise ValueError("width and height must be even")
+        self.p = params
+        self.B = int(slots)
+        self.dev = _resolve(device)
+        self.hip = native.hip()
+        self.host = native.host()
+        self.wmb = (params.width + 15) // 16
+        self.hmb = (params.height + 15) // 16
+        self.W, self.H = self.wmb * 16, self.hmb * 16
+        self.nmb = self.wmb * self.hmb
+        B, H, W, nmb, dev = self.B, self.H, self.W, self.nmb, self.dev
+        u8, i16, i32 = torch.uint8, torch.int16, torch.int32
+
+        def planes():
+            return (torch.zeros((B, H, W), dtype=u8, device=dev),
+                    torch.zeros((B, H // 2, W // 2), dtype=u8, device=dev),
+                    torch.zeros((B, H // 2, W // 2), dtype=u8, device=dev))
+
+        self.src = planes()
+        self.rec = [planes(), planes()]  # ping-pong: current recon / reference
+        self.hdr = [torch.zeros((B, nmb, MB_HDR_BYTES), dtype=u8, device=dev) for _ in range(2)]
+        self.coef = [torch.zeros((B, nmb, COEF_PER_MB), dtype=i16, device=dev) for _ in range(2)]
+        self.nz = torch.zeros((B, nmb, 16), dtype=u8, device=dev)
+        self.mv = torch.zeros((B, nmb, 2), dtype=i16, device=dev)
+        self.prev_mv = torch.zeros((B, nmb, 2), dtype=i16, device=dev)
+        self.me_cost = torch.zeros((B, nmb), dtype=i32, device=dev)
+        self.intra_cost = torch.zeros((B, nmb), dtype=i32, device=dev)
+        self.pred = torch.zeros((B, nmb, 256), dtype=u8, device=dev)
+        self.intra_flag = torch.zeros((B, nmb), dtype=u8, device=dev)
+        self.intra_count = torch.zeros((B,), dtype=i32, device=dev)
+        self.qp = torch.zeros((B,), dtype=i32, device=dev)
+        self.ticket = torch.zeros((1,), dtype=i32, device=dev)
+        self.progress = torch.zeros((B * self.hmb,), dtype=i32, device=dev)
+        self.err = torch.zeros((1,), dtype=i32, device=dev)
+        # pinned staging for the entropy stage (double-buffered)
+        self.h_hdr = [torch.empty((B, nmb, MB_HDR_BYTES), dtype=u8).pin_memory() for _ in range(2)]
+        self.h_coef = [torch.empty((B, nmb, COEF_PER_MB), dtype=i16).pin_memory() for _ in range(2)]
+        self.copy_stream = torch.cuda.Stream(device=dev)
+        self.copy_done = [torch.cuda.Event() for _ in range(2)]
+        self.compute_done = [torch.cuda.Event() for _ in range(2)]
+        nthreads = entropy_threads or min(16, max(2, (os.cpu_count() or 4)))
+        self.pool = cf.ThreadPoolExecutor(max_workers=nthreads)
+        self.cfg = params.host_cfg()
+        self.timings: dict[str, float] = {}
+
+    # ------------------------------------------------------------------ helpers
+    @staticmethod
+    def _ptr(t: torch.Tensor) -> int:
+        return t.data_ptr()
+
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.dev).cuda_stream
+
+    def parameter_sets(self) -> bytes:
+        return self.host.parameter_sets(self.cfg)
+
+    # ------------------------------------------------------------------ stages
+    def _prep(self, y, u, v, t: int):
+        """y/u/v: [B, F, h, w] display-size planes on the device; pads frame t of every slot."""
+        B, F, h, w = y.shape
+        cs = u.shape[2] * u.shape[3]
+        self.hip.prep(y[:, t].data_ptr(), u[:, t].data_ptr(), v[:, t].data_ptr(), w, h, F * h * w, F * cs, B,
+                      self._ptr(self.src[0]), self._ptr(self.src[1]), self._ptr(self.src[2]),
+                      self.p.width, self.p.height, self.W, self.H, self._stream())
+
+    def _encode_frame(self, idr: bool, cur, ref, hdr, coef):
+        s = self._stream()
+        B, wmb, hmb = self.B, self.wmb, self.hmb
+        sy, su, sv = (self._ptr(x) for x in self.src)
+        ry, ru, rv = (self._ptr(x) for x in cur)
+        if not idr:
+            fy, fu, fv = (self._ptr(x) for x in ref)
+            self.intra_count.zero_()
+            self.hip.me(B, wmb, hmb, sy, fy, self._ptr(self.prev_mv), self._ptr(self.mv), self._ptr(self.me_cost),
+                        self._ptr(self.pred), self._ptr(self.intra_cost), self._ptr(self.qp),
+                        self.p.me_range, self.p.subpel, s)
+            self.hip.encode_inter(B, wmb, hmb, sy, su, sv, fy, fu, fv, ry, ru, rv, self._ptr(self.pred),
+                                  self._ptr(self.mv), self._ptr(self.me_cost), self._ptr(self.intra_cost),
+                                  self._ptr(self.qp), self.p.chroma_qp_offset, self._ptr(hdr), self._ptr(coef),
+                                  self._ptr(self.nz), self._ptr(self.intra_flag), self._ptr(self.intra_count), s)
+            self.prev_mv.copy_(self.mv)
+            flag_ptr, count_ptr = self._ptr(self.intra_flag), self._ptr(self.intra_count)
+        else:
+            self.prev_mv.zero_()
+            flag_ptr, count_ptr = 0, 0
+        self.hip.encode_intra(B, wmb, hmb, sy, su, sv, ry, ru, rv, self._ptr(self.qp), self.p.chroma_qp_offset,
+                              self._ptr(hdr), self._ptr(coef), self._ptr(self.nz), flag_ptr, count_ptr,
+                              self._ptr(self.ticket), self._ptr(self.progress), self._ptr(self.err),
+                              int(self.p.i4x4), s)
+        if self.p.deblock:
+            self.hip.deblock(B, wmb, hmb, ry, ru, rv, self._ptr(hdr), self._ptr(self.nz), self.p.chroma_qp_offset,
+                             0, 0, self._ptr(self.ticket), self._ptr(self.progress), self._ptr(self.err), s)
+
+    # ------------------------------------------------------------------ entropy (host)
+    def _write_slices(self, k: int, t: int, qp_frame: int, idr: bool, idr_base: int) -> list[tuple[bytes, int]]:
+        self.copy_done[k].synchronize()
+        hdr = self.h_hdr[k].numpy()
+        coef = self.h_coef[k].numpy()
+
+        def one(b: int):
+            fp = dict(idr=int(idr), frame_num=t, idr_pic_id=(idr_base + b) & 0xFFFF, qp=qp_frame)
+            nal, st = self.host.write_slice(self.cfg, fp, hdr[b], coef[b])
+            return nal, st["bits"]
+
+        return list(self.pool.map(one, range(self.B)))
+
+    # ------------------------------------------------------------------ public API
+    @torch.no_grad()
+    def encode(self, y: torch.Tensor, u: torch.Tensor, v: torch.Tensor, idr_base: int = 0,
+               keep_recon: bool = False, metrics: bool = True) -> list[SegmentResult]:
+        """Encode B segments of F frames each.
+
+        y: [B, F, h, w] uint8 (device), u/v: [B, F, h/2, w/2].  Each slot's output is a
+        self-contained Annex-B segment (SPS/PPS + IDR + P...), i.e. one "piece" of the
+        reference's split directory, with idr_pic_id = idr_base + slot.
+        """
+        B, F = y.shape[0], y.shape[1]
+        if B != self.B:
+            raise ValueError(f"encoder was built for {self.B} slots, got {B}")
+        if y.shape[2] != self.p.height or y.shape[3] != self.p.width:
+            raise ValueError("frame size mismatch")
+        torch.cuda.set_device(self.dev)
+        qp_i, qp_p = self.p.frame_qps()
+        self.err.zero_()
+        sse = torch.zeros((F, B, 3), dtype=torch.int64, device=self.dev)
+        ssim = torch.zeros((F, B), dtype=torch.float32, device=self.dev)
+        pending: list[cf.Future] = [None, None]  # type: ignore[list-item]
+        outs: list[list[tuple[bytes, int]]] = [None] * F  # type: ignore[list-item]
+        recons = [] if keep_recon else None
+        main = torch.cuda.current_stream(self.dev)
+        for t in range(F):
+            k = t & 1
+            idr = t == 0
+            qpf = qp_i if idr else qp_p
+            # the device/pinned buffers of slot k were last used by step t-2: wait for them
+            if pending[k] is not None:
+                outs[t - 2] = pending[k].result()
+                pending[k] = None
+            main.wait_event(self.copy_done[k]) if t >= 2 else None
+            cur, ref = self.rec[k], self.rec[1 - k]
+            self._prep(y, u, v, t)
+            self.qp.fill_(qpf)
+            self._encode_frame(idr, cur, ref, self.hdr[k], self.coef[k])
+            if metrics:
+                self.hip.sse(B, self.W, self.H, self.p.width, self.p.height, self._ptr(self.src[0]),
+                             self._ptr(self.src[1]), self._ptr(self.src[2]), self._ptr(cur[0]), self._ptr(cur[1]),
+                             self._ptr(cur[2]), sse[t].data_ptr(), ssim[t].data_ptr(), self._stream())
+            if keep_recon:
+                recons.append(tuple(c.clone() for c in cur))
+            self.compute_done[k].record(main)
+            with torch.cuda.stream(self.copy_stream):
+                self.copy_stream.wait_event(self.compute_done[k])
+                self.h_hdr[k].copy_(self.hdr[k], non_blocking=True)
+                self.h_coef[k].copy_(self.coef[k], non_blocking=True)
+                self.copy_done[k].record(self.copy_stream)
+            pending[k] = self.pool.submit(self._write_slices, k, t, qpf, idr, idr_base)
+        for t in range(max(0, F - 2), F):
+            k = t & 1
+            if pending[k] is not None:
+                outs[t] = pending[k].result()
+                pending[k] = None
+        torch.cuda.synchronize(self.dev)
+        if int(self.err.item()) != 0:
+            raise RuntimeError("wavefront progress timeout in an encode kernel")
+        ps = self.parameter_sets()
+        results = []
+        sse_h = sse.cpu().numpy().astype(np.float64)
+        ssim_h = ssim.cpu().numpy()
+        npx = self.p.width * self.p.height
+        nwin = (self.p.width // 8) * (self.p.height // 8)
+        for b in range(B):
+            nals = [outs[t][b][0] for t in range(F)]
+            r = SegmentResult(bitstream=ps + b"".join(nals), frames=F, bits=[outs[t][b][1] for t in range(F)])
+            if metrics:
+                def psnr(ssev, n):
+                    mse = ssev / n
+                    return 100.0 if mse <= 1e-10 else 10.0 * math.log10(255.0 ** 2 / mse)
+                r.psnr_y = float(np.mean([psnr(sse_h[t, b, 0], npx) for t in range(F)]))
+                r.psnr_u = float(np.mean([psnr(sse_h[t, b, 1], npx / 4) for t in range(F)]))
+                r.psnr_v = float(np.mean([psnr(sse_h[t, b, 2], npx / 4) for t in range(F)]))
+                r.ssim_y = float(ssim_h[:, b].sum() / (F * max(1, nwin)))
+            results.append(r)
+        if keep_recon:
+            self.last_recon = recons
+        return results
+
+    def close(self):
+        self.pool.shutdown(wait=True)
+
+
+def synth_clip(slots: int, frames: int, width: int, height: int, seed: int = 0, frame0: int = 0,
+               device: str | torch.device = "cuda"):
+    """Generate B x F synthetic I420 frames directly in HBM (see csrc/kernels/synth.hip)."""
+    hip = native.hip()
+    dev = _resolve(device)
+    y = torch.empty((slots, frames, height, width), dtype=torch.uint8, device=dev)
+    u = torch.empty((slots, frames, height // 2, width // 2), dtype=torch.uint8, device=dev)
+    v = torch.empty_like(u)
+    hip.synth(y.data_ptr(), u.data_ptr(), v.data_ptr(), width, height, slots, frames, frame0, seed,
+              torch.cuda.current_stream(dev).cuda_stream)
+    return y, u, v

@@ -1,0 +1,51 @@
+"""GPU H.264 encoder: the reconstruction the kernels produce must equal what the
+independent CPU decoder reconstructs from the emitted bitstream, bit for bit
+(SURVEY.md §4.2 tiers T1/T2)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(width, height, slots, frames, **kw):
+    import torch
+    from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
+
+    p = H264Params(width=width, height=height, **kw)
+    enc = GpuH264Encoder(p, slots=slots)
+    y, u, v = synth_clip(slots, frames, width, height, seed=3)
+    res = enc.encode(y, u, v, keep_recon=True)
+    torch.cuda.synchronize()
+    return enc, res, (y, u, v)
+
+
+def _check_roundtrip(host, enc, res, width, height):
+    for b, r in enumerate(res):
+        pics = host.decode(r.bitstream)
+        assert len(pics) == r.frames
+        for t, pic in enumerate(pics):
+            ry, ru, rv = (x[b].cpu().numpy() for x in enc.last_recon[t])
+            dy, du, dv = pic["y_coded"], pic["u_coded"], pic["v_coded"]
+            assert np.array_equal(dy, ry), f"slot {b} frame {t}: luma mismatch ({(dy != ry).sum()} px)"
+            assert np.array_equal(du, ru), f"slot {b} frame {t}: Cb mismatch"
+            assert np.array_equal(dv, rv), f"slot {b} frame {t}: Cr mismatch"
+
+
+@pytest.mark.parametrize("qp", [22, 30])
+def test_gpu_h264_roundtrip_small(host, qp):
+    enc, res, _ = _run(176, 144, slots=2, frames=4, crf=None, qp=qp)
+    _check_roundtrip(host, enc, res, 176, 144)
+    for r in res:
+        assert r.psnr_y > 30
+
+
+def test_gpu_h264_roundtrip_no_deblock_no_i4(host):
+    enc, res, _ = _run(176, 144, slots=2, frames=3, crf=None, qp=26, deblock=False, i4x4=False)
+    _check_roundtrip(host, enc, res, 176, 144)
+
+
+def test_gpu_h264_roundtrip_1080p(host):
+    enc, res, _ = _run(1920, 1080, slots=2, frames=3, crf=23)
+    _check_roundtrip(host, enc, res, 1920, 1080)
+    for r in res:
+        assert r.psnr_y > 33
