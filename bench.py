@@ -1,0 +1,131 @@
+#!/usr/bin/env python3
+"""Headline benchmark: whole-node encoded frames/sec, 1080p30 synthetic YUV -> H.264 CRF23.
+
+Metric/config from BASELINE.json ("encoded frames/sec (whole node), 1080p30->H.264
+CRF23, at 1/2/4/8 MI355X").  One process per GPU (torch.distributed.run), weak
+scaling: every rank encodes B closed-GOP segments of F frames per step.  A timed step is
+
+    synthesize B*F new 1080p frames in HBM (new content every step)
+    -> batched GPU encode (ME, TQ, intra/deblock wavefronts, CAVLC)
+    -> gather every rank's segment bitstreams to all ranks (RCCL all_gather over xGMI)
+    -> rank 0 concatenates the pieces in segment order (the reference's concat.sh)
+
+bracketed by barrier + torch.cuda.synchronize(); the step time is the max over ranks.
+The reference publishes no numbers, so vs_baseline is null.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--slots", type=int, default=int(os.environ.get("MIVC_BENCH_SLOTS", "32")),
+                    help="segments encoded concurrently per GPU")
+    ap.add_argument("--frames", type=int, default=int(os.environ.get("MIVC_BENCH_FRAMES", "60")),
+                    help="frames per segment (GOP length)")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--crf", type=float, default=23.0)
+    ap.add_argument("--json-out", default=None)
+    a = ap.parse_args()
+
+    import torch
+
+    from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
+    from govideocompressor_amd.ops import native
+    from govideocompressor_amd.parallel import dist as D
+
+    env = D.init(prefer_gpu=True)
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU")
+    if env.world != a.gpus:
+        if env.is_main:
+            print(f"warning: --gpus {a.gpus} but WORLD_SIZE {env.world}", file=sys.stderr)
+    host = native.host()
+    p = H264Params(width=a.width, height=a.height, fps=30.0, crf=a.crf)
+    enc = GpuH264Encoder(p, slots=a.slots, device=env.device,
+                         entropy_threads=int(os.environ.get("MIVC_ENTROPY_THREADS", "16")))
+    B, F = a.slots, a.frames
+
+    def one_step(step: int):
+        seed = 1000 + step * 7919 + env.rank * 104729
+        y, u, v = synth_clip(B, F, a.width, a.height, seed=seed, device=env.device)
+        res = enc.encode(y, u, v, idr_base=env.rank * B)
+        g = D.BitstreamGather(env, [r.bitstream for r in res]).start()
+        pieces = g.wait()
+        merged = None
+        if env.is_main:
+            ordered = [pc for rank_pieces in pieces for pc in rank_pieces]
+            merged = host.concat(ordered)
+        return res, merged
+
+    for w in range(a.warmup):
+        one_step(-1 - w)
+    D.barrier(env)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    last = None
+    for s in range(a.steps):
+        last = one_step(s)
+    torch.cuda.synchronize()
+    D.barrier(env)
+    t1 = time.perf_counter()
+    elapsed = D.max_over_ranks(env, t1 - t0)
+    res, merged = last
+    total_frames = env.world * B * F * a.steps
+    fps = total_frames / elapsed
+    # quality / rate of the last step (this rank), averaged over ranks
+    psnr = D.sum_over_ranks(env, sum(r.psnr_y for r in res) / len(res)) / env.world
+    ssim = D.sum_over_ranks(env, sum(r.ssim_y for r in res) / len(res)) / env.world
+    nbytes = D.sum_over_ranks(env, float(sum(len(r.bitstream) for r in res)))
+    kbps = nbytes * 8 / (env.world * B * F / p.fps) / 1000.0
+    if env.is_main:
+        out = {
+            "metric": "encoded frames/sec (whole node), 1080p30->H.264 CRF23",
+            "value": round(fps, 2),
+            "unit": "frames/s",
+            "n_gpus": env.world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1000.0, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "uint8 (8-bit 4:2:0 samples, int32 transforms)",
+            "data": "synthetic (GPU-generated moving-texture YUV, new content every step)",
+            "config": {
+                "model": "H.264 Constrained Baseline CAVLC, gfx950 batched encoder",
+                "resolution": f"{a.width}x{a.height}",
+                "fps": 30,
+                "crf": a.crf,
+                "global_batch": env.world * B * F,
+                "seq_len": F,
+                "segments_per_gpu": B,
+                "parallelism": f"dp{env.world} (segment-parallel)",
+            },
+            "quality": {"psnr_y_db": round(psnr, 3), "ssim_y": round(ssim, 4), "bitrate_kbps": round(kbps, 1),
+                        "merged_bytes": len(merged) if merged is not None else 0},
+            "timings_rank0_s": {k: round(v, 3) for k, v in enc.timings.items()},
+        }
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    enc.close()
+    D.shutdown(env)
+
+
+if __name__ == "__main__":
+    main()

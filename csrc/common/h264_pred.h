@@ -97,7 +97,8 @@ MIVC_HD int i4_pred_sample(int mode, int av, const int* e, int x, int y) {
 }
 
 // 16x16 luma: top[16], left[16], tl.  Plane parameters precomputed by the caller via i16_plane_params.
-MIVC_HD void i16_plane_params(const int* top, const int* left, int tl, int* a, int* b, int* c) {
+template <class T>
+MIVC_HD void i16_plane_params(const T* top, const T* left, int tl, int* a, int* b, int* c) {
   int H = 0, V = 0;
   for (int i = 0; i < 8; ++i) {
     H += (i + 1) * (top[8 + i] - (i == 7 ? tl : top[6 - i]));
@@ -107,7 +108,8 @@ MIVC_HD void i16_plane_params(const int* top, const int* left, int tl, int* a, i
   *b = (5 * H + 32) >> 6;
   *c = (5 * V + 32) >> 6;
 }
-MIVC_HD int i16_dc(const int* top, const int* left, int av) {
+template <class T>
+MIVC_HD int i16_dc(const T* top, const T* left, int av) {
   int st = 0, sl = 0;
   for (int i = 0; i < 16; ++i) {
     st += top[i];
@@ -120,7 +122,8 @@ MIVC_HD int i16_dc(const int* top, const int* left, int av) {
 }
 
 // chroma 8x8 (4:2:0) DC for 4x4 block (bx,by)
-MIVC_HD int chroma_dc(const int* top, const int* left, int av, int bx, int by) {
+template <class T>
+MIVC_HD int chroma_dc(const T* top, const T* left, int av, int bx, int by) {
   int st = 0, sl = 0;
   for (int i = 0; i < 4; ++i) {
     st += top[bx * 4 + i];
@@ -142,7 +145,8 @@ MIVC_HD int chroma_dc(const int* top, const int* left, int av, int bx, int by) {
   if (t) return (st + 2) >> 2;
   return 128;
 }
-MIVC_HD void chroma_plane_params(const int* top, const int* left, int tl, int* a, int* b, int* c) {
+template <class T>
+MIVC_HD void chroma_plane_params(const T* top, const T* left, int tl, int* a, int* b, int* c) {
   int H = 0, V = 0;
   for (int i = 0; i < 4; ++i) {
     H += (i + 1) * (top[4 + i] - (i == 3 ? tl : top[2 - i]));

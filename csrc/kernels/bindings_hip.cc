@@ -28,11 +28,11 @@ void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t* src_y, con
 void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* src_u,
                               const uint8_t* src_v, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const int* qp,
                               int chroma_qp_offset, void* hdr, int16_t* coef, uint8_t* nz,
-                              const uint8_t* intra_flag, const int* intra_count, int* ticket, int* progress, int* err,
-                              int use_i4x4, void* stream);
+                              const uint8_t* intra_flag, const int* intra_count, int* err, int use_i4x4,
+                              void* stream);
 void mivc_launch_deblock(int B, int wmb, int hmb, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const void* hdr,
-                         const uint8_t* nz, int chroma_qp_offset, int alpha_off, int beta_off, int* ticket,
-                         int* progress, int* err, void* stream);
+                         const uint8_t* nz, int chroma_qp_offset, int alpha_off, int beta_off, int* err,
+                         void* stream);
 void mivc_launch_sse(int B, int W, int H, int w, int h, const uint8_t* sy, const uint8_t* su, const uint8_t* sv,
                      const uint8_t* ry, const uint8_t* ru, const uint8_t* rv, unsigned long long* sse,
                      float* ssim_sum, void* stream);
@@ -82,18 +82,17 @@ PYBIND11_MODULE(_hip, m) {
         });
   m.def("encode_intra", [](int B, int wmb, int hmb, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t ry,
                            uintptr_t ru, uintptr_t rv, uintptr_t qp, int cqo, uintptr_t hdr, uintptr_t coef,
-                           uintptr_t nz, uintptr_t intra_flag, uintptr_t intra_count, uintptr_t ticket,
-                           uintptr_t progress, uintptr_t err, int use_i4x4, uintptr_t stream) {
+                           uintptr_t nz, uintptr_t intra_flag, uintptr_t intra_count, uintptr_t err, int use_i4x4,
+                           uintptr_t stream) {
     mivc_launch_encode_intra(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), P<uint8_t>(ry),
                              P<uint8_t>(ru), P<uint8_t>(rv), P<int>(qp), cqo, P<void>(hdr), P<int16_t>(coef),
-                             P<uint8_t>(nz), P<uint8_t>(intra_flag), P<int>(intra_count), P<int>(ticket),
-                             P<int>(progress), P<int>(err), use_i4x4, S(stream));
+                             P<uint8_t>(nz), P<uint8_t>(intra_flag), P<int>(intra_count), P<int>(err), use_i4x4,
+                             S(stream));
   });
   m.def("deblock", [](int B, int wmb, int hmb, uintptr_t ry, uintptr_t ru, uintptr_t rv, uintptr_t hdr, uintptr_t nz,
-                      int cqo, int alpha_off, int beta_off, uintptr_t ticket, uintptr_t progress, uintptr_t err,
-                      uintptr_t stream) {
+                      int cqo, int alpha_off, int beta_off, uintptr_t err, uintptr_t stream) {
     mivc_launch_deblock(B, wmb, hmb, P<uint8_t>(ry), P<uint8_t>(ru), P<uint8_t>(rv), P<void>(hdr), P<uint8_t>(nz),
-                        cqo, alpha_off, beta_off, P<int>(ticket), P<int>(progress), P<int>(err), S(stream));
+                        cqo, alpha_off, beta_off, P<int>(err), S(stream));
   });
   m.def("sse", [](int B, int W, int H, int w, int h, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t ry,
                   uintptr_t ru, uintptr_t rv, uintptr_t sse, uintptr_t ssim, uintptr_t stream) {

@@ -4,7 +4,8 @@
 // filter reads samples MB n's horizontal edges already modified, and MB (x, y)'s
 // top edge reads samples MB (x+1, y-1)'s left edge modified.  So MB (x, y) runs
 // after (x-1, y) and (x+1, y-1): the same row wavefront as intra coding (one
-// wave64 per MB row, ticketed rows, agent-scope progress counters).  Inside an
+// workgroup of kDeblockWaves wave64s per frame, wave w owns rows w, w+kDeblockWaves,
+// ..., LDS row-progress counters at workgroup scope).  Inside an
 // MB the 16 lines of an edge are filtered in parallel (lanes 0-15 luma, 16-31
 // chroma), edges in the normative order (vertical left->right, then horizontal
 // top->bottom).  Boundary strengths are derived per MB from the decision
@@ -23,10 +24,10 @@ struct DeblockArgs {
   const uint8_t* nz;   // [B, nmb, 16] raster
   int chroma_qp_offset;
   int alpha_off, beta_off;  // slice_alpha_c0_offset_div2*2, slice_beta_offset_div2*2
-  int* ticket;
-  int* progress;
   int* err;
 };
+
+constexpr int kDeblockWaves = 16;
 
 constexpr int LT = 20;  // luma tile stride: 4 halo + 16
 constexpr int CT = 10;  // chroma tile stride: 2 halo + 8
@@ -96,9 +97,9 @@ __device__ __forceinline__ void blk_mv(const MbHeader& h, int r, int* mv) {
   mv[1] = h.mv[q][1];
 }
 
-__device__ void deblock_mb(const DeblockArgs& a, DeblockShared& S, int slot, int mx, int my) {
+__device__ __forceinline__ void deblock_mb(const DeblockArgs& a, DeblockShared& S, int slot, int mx, int my) {
   const Geom& g = a.g;
-  const int lane = threadIdx.x;
+  const int lane = lane_id();
   const int W = g.W, cw = g.cw();
   const size_t o = static_cast<size_t>(slot) * g.nmb() + my * g.wmb + mx;
   uint8_t* recy = a.rec_y + slot * g.ysize();
@@ -164,7 +165,7 @@ __device__ void deblock_mb(const DeblockArgs& a, DeblockShared& S, int slot, int
     }
     S.bs[dir][e][k] = bs;
   }
-  __syncthreads();
+  wave_sync();
 
   const int qpq = a.hdr[o].qp;
   // ---- vertical edges, then horizontal edges
@@ -195,7 +196,7 @@ __device__ void deblock_mb(const DeblockArgs& a, DeblockShared& S, int slot, int
           filter_line(q0, dir == 0 ? 1 : CT, bs, h264::kAlpha[ia], h264::kBeta[ib], tc0, true);
         }
       }
-      __syncthreads();
+      wave_sync();
     }
   }
   // ---- write back: MB interior + modified halo (3 luma / 1 chroma lines)
@@ -224,7 +225,7 @@ __device__ void deblock_mb(const DeblockArgs& a, DeblockShared& S, int slot, int
       rc[static_cast<size_t>(my * 8 + r) * cw + mx * 8 - 1] = t[(r + 2) * CT + 1];
     }
   }
-  __syncthreads();
+  wave_sync();
   // ---- keep this MB's right edge for the next iteration (final values)
   if (lane < 16)
     for (int c = 0; c < 4; ++c) S.left_y[lane][c] = S.ty[(lane + 4) * LT + 16 + c];
@@ -235,21 +236,22 @@ __device__ void deblock_mb(const DeblockArgs& a, DeblockShared& S, int slot, int
   if (lane == 0) S.saved_x = mx;
 }
 
-__global__ __launch_bounds__(64) void deblock_wavefront(DeblockArgs a) {
-  __shared__ DeblockShared S;
+__global__ __launch_bounds__(64 * kDeblockWaves) void deblock_wavefront(DeblockArgs a) {
+  __shared__ DeblockShared SS[kDeblockWaves];
+  __shared__ int prog[kMaxRows];
   const Geom& g = a.g;
-  const int t = draw_ticket(a.ticket);
-  if (t >= g.B * g.hmb) return;
-  const int slot = t / g.hmb, y = t % g.hmb;
-  if (threadIdx.x == 0) S.saved_x = -2;
+  const int slot = blockIdx.x;
+  for (int i = threadIdx.x; i < g.hmb; i += blockDim.x) prog[i] = 0;
+  const int w = wave_id();
+  if (lane_id() == 0) SS[w].saved_x = -2;
   __syncthreads();
-  for (int x = 0; x < g.wmb; ++x) {
-    if (y > 0 && !wait_progress(a.progress + t - 1, min(x + 2, g.wmb), a.err)) {
-      publish_progress(a.progress + t, g.wmb);
-      return;
+  DeblockShared& S = SS[w];
+  for (int y = w; y < g.hmb; y += kDeblockWaves) {
+    for (int x = 0; x < g.wmb; ++x) {
+      if (y > 0) row_wait(prog, y - 1, min(x + 2, g.wmb), a.err);
+      deblock_mb(a, S, slot, x, y);
+      row_publish(prog, y, x + 1);
     }
-    deblock_mb(a, S, slot, x, y);
-    publish_progress(a.progress + t, x + 1);
   }
 }
 
@@ -260,7 +262,7 @@ using namespace mivc::gpu;
 
 extern "C" void mivc_launch_deblock(int B, int wmb, int hmb, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v,
                                     const void* hdr, const uint8_t* nz, int chroma_qp_offset, int alpha_off,
-                                    int beta_off, int* ticket, int* progress, int* err, void* stream) {
+                                    int beta_off, int* err, void* stream) {
   DeblockArgs a;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.rec_y = rec_y;
@@ -271,11 +273,6 @@ extern "C" void mivc_launch_deblock(int B, int wmb, int hmb, uint8_t* rec_y, uin
   a.chroma_qp_offset = chroma_qp_offset;
   a.alpha_off = alpha_off;
   a.beta_off = beta_off;
-  a.ticket = ticket;
-  a.progress = progress;
   a.err = err;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  hipMemsetAsync(ticket, 0, sizeof(int), s);
-  hipMemsetAsync(progress, 0, sizeof(int) * B * hmb, s);
-  hipLaunchKernelGGL(deblock_wavefront, dim3(B * hmb), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(deblock_wavefront, dim3(B), dim3(64 * kDeblockWaves), 0, static_cast<hipStream_t>(stream), a);
 }

@@ -56,6 +56,30 @@ __global__ void prep_plane(PrepArgs a, int plane) {
   out[static_cast<size_t>(y) * W + x] = static_cast<uint8_t>(v);
 }
 
+// Fast path (no resampling, 16-byte aligned rows): one thread per 16 output bytes.
+__global__ void prep_plane_copy16(PrepArgs a, int plane) {
+  int x = (blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  int y = blockIdx.y;
+  int n = blockIdx.z;
+  int sh = plane ? 1 : 0;
+  int W = a.W >> sh, H = a.H >> sh;
+  if (x >= W) return;
+  int w = a.w >> sh, h = a.h >> sh;
+  const uint8_t* in = plane == 0 ? a.in_y : (plane == 1 ? a.in_u : a.in_v);
+  in += n * (plane ? a.in_frame_stride_c : a.in_frame_stride_y);
+  uint8_t* out = plane == 0 ? a.out_y : (plane == 1 ? a.out_u : a.out_v);
+  out += static_cast<size_t>(n) * W * H + static_cast<size_t>(y) * W + x;
+  const uint8_t* row = in + static_cast<size_t>(min(y, h - 1)) * w;
+  if (x + 16 <= w) {
+    *reinterpret_cast<uint4*>(out) = *reinterpret_cast<const uint4*>(row + x);
+  } else {
+    uint8_t b[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) b[k] = row[min(x + k, w - 1)];
+    *reinterpret_cast<uint4*>(out) = *reinterpret_cast<const uint4*>(b);
+  }
+}
+
 // packed RGB24 [N, h, w, 3] -> I420 display-size planes (BT.601 limited range)
 __global__ void rgb_to_i420(const uint8_t* rgb, int w, int h, uint8_t* oy, uint8_t* ou, uint8_t* ov) {
   int x2 = blockIdx.x * blockDim.x + threadIdx.x;  // chroma column
@@ -89,6 +113,15 @@ extern "C" void mivc_launch_prep(const uint8_t* in_y, const uint8_t* in_u, const
                                  uint8_t* out_v, int ow, int oh, int W, int H, void* stream) {
   PrepArgs a{in_y, in_u, in_v, w, h, in_stride_y, in_stride_c, out_y, out_u, out_v, ow, oh, W, H};
   hipStream_t s = static_cast<hipStream_t>(stream);
+  bool aligned = (w % 32 == 0) && (in_stride_y % 16 == 0) && (in_stride_c % 16 == 0) &&
+                 (reinterpret_cast<uintptr_t>(in_y) % 16 == 0) && (reinterpret_cast<uintptr_t>(in_u) % 16 == 0) &&
+                 (reinterpret_cast<uintptr_t>(in_v) % 16 == 0) && W % 32 == 0;
+  if (ow == w && oh == h && aligned) {
+    hipLaunchKernelGGL(prep_plane_copy16, dim3((W / 16 + 63) / 64, H, nframes), dim3(64), 0, s, a, 0);
+    hipLaunchKernelGGL(prep_plane_copy16, dim3((W / 32 + 63) / 64, H / 2, nframes), dim3(64), 0, s, a, 1);
+    hipLaunchKernelGGL(prep_plane_copy16, dim3((W / 32 + 63) / 64, H / 2, nframes), dim3(64), 0, s, a, 2);
+    return;
+  }
   hipLaunchKernelGGL(prep_plane, dim3((W + 255) / 256, H, nframes), dim3(256), 0, s, a, 0);
   hipLaunchKernelGGL(prep_plane, dim3((W / 2 + 255) / 256, H / 2, nframes), dim3(256), 0, s, a, 1);
   hipLaunchKernelGGL(prep_plane, dim3((W / 2 + 255) / 256, H / 2, nframes), dim3(256), 0, s, a, 2);

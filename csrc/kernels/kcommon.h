@@ -42,49 +42,43 @@ __device__ __forceinline__ int satd16(int* r) {
   return h264::satd4x4(r);
 }
 
-// ---------------------------------------------------------------- inter-workgroup hand-off
-// Producer (all threads of the workgroup call): publish `value` into *flag after every
-// thread's global stores are complete.  Recipe per MI355X guide §6 Guideline 16 R1.
-__device__ __forceinline__ void publish_progress(int* flag, int value) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+// ---------------------------------------------------------------- in-workgroup wavefront
+// The serial stages (intra coding, deblocking) run one workgroup per frame with
+// kWaves waves; wave w owns MB rows w, w + kWaves, ...  Row progress lives in LDS
+// and is exchanged at workgroup scope: all waves of a workgroup share one CU and
+// its vector L1, so release/acquire at workgroup scope is an s_waitcnt, not a
+// cache write-back/invalidate (agent-scope fences cost 1.7-7 us per hand-off on
+// MI355X, guide §Persistent kernels price list; the first version of these
+// kernels spent ~20 us per MB step there).
+constexpr int kMaxRows = 272;  // 8K: 4320 / 16 = 270 MB rows
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+
+// order LDS/global accesses between lanes of one wave (no hardware barrier needed)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Consumer: wait until *flag >= target (bounded spin), then acquire.
-// Returns false on timeout (the kernel then sets an error word and bails out).
-__device__ __forceinline__ bool wait_progress(int* flag, int target, int* err) {
-  __shared__ int ok;
-  if (threadIdx.x == 0) {
-    long long spins = 0;
-    int v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    while (v < target) {
-      __builtin_amdgcn_s_sleep(1);
-      v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (++spins > (1ll << 26)) break;  // ~seconds: never hang the GPU
-      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+// wait until prog[row] >= target (bounded: a bug must not hang the GPU)
+__device__ __forceinline__ void row_wait(int* prog, int row, int target, int* err) {
+  int spins = 0;
+  while (__hip_atomic_load(prog + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
+    __builtin_amdgcn_s_sleep(2);
+    if (++spins > (1 << 24)) {
+      if (lane_id() == 0) atomicOr(err, 1);
+      break;
     }
-    ok = v >= target;
-    if (!ok) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  __syncthreads();
-  return ok;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// Dynamic row ticket (deadlock-free wavefront order regardless of dispatch order):
-// the workgroup that draws ticket t processes row t; row t-1 was drawn earlier by a
-// workgroup that is already running.
-__device__ __forceinline__ int draw_ticket(int* counter) {
-  __shared__ int t;
-  if (threadIdx.x == 0) t = atomicAdd(counter, 1);
-  __syncthreads();
-  return t;
+// publish prog[row] = value after this wave's global stores
+__device__ __forceinline__ void row_publish(int* prog, int row, int value) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (lane_id() == 0) __hip_atomic_store(prog + row, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 }  // namespace gpu

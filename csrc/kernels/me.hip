@@ -93,7 +93,7 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
     int dy = p / side, dx = p % side;
     int w0 = dx >> 2, sh = dx & 3;
     uint32_t sad = 0;
-#pragma unroll 4
+#pragma unroll
     for (int r = 0; r < 16; ++r) {
       const uint32_t* rowp = s_win + (dy + r) * kWinWords + w0;
       uint32_t a0 = rowp[0], a1 = rowp[1], a2 = rowp[2], a3 = rowp[3], a4 = rowp[4];
@@ -203,43 +203,50 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
     return s;
   };
 
+  // candidate c of a 3x3 ring (0 = centre, 1..8 = the 8 neighbours) -> offsets in units of `step`
+  auto ring = [](int c, int step, int* dx, int* dy) {
+    int idx = c == 0 ? 4 : (c <= 4 ? c - 1 : c);
+    *dx = (idx % 3 - 1) * step;
+    *dy = (idx / 3 - 1) * step;
+  };
   int best_cost;
+  int hx = 0, hy = 0;
   {
-    // pass over center + 8 half-pel neighbours (3 passes of 4 candidates)
-    const int hofs[9][2] = {{0, 0}, {-2, -2}, {0, -2}, {2, -2}, {-2, 0}, {2, 0}, {-2, 2}, {0, 2}, {2, 2}};
+    // centre + 8 half-pel neighbours (3 passes of 4 candidates, 16 lanes each)
     int bkey = 0x7FFFFFFF;
-    int ncand_h = a.subpel >= 1 ? 9 : 1;
+    const int ncand_h = a.subpel >= 1 ? 9 : 1;
     for (int base = 0; base < ncand_h; base += 4) {
       int ci = base + (lane >> 4);
       int c = ci < ncand_h ? ci : 0;
-      int s = satd_cand(hofs[c][0], hofs[c][1]);
-      int mvx = best_mvx + hofs[c][0], mvy = best_mvy + hofs[c][1];
+      int ox, oy;
+      ring(c, 2, &ox, &oy);
+      int s = satd_cand(ox, oy);
+      int mvx = best_mvx + ox, mvy = best_mvy + oy;
       int cost = s + lambda * (h264::se_bits(mvx - pmx) + h264::se_bits(mvy - pmy));
       int key = ci < ncand_h ? ((cost << 4) | c) : 0x7FFFFFFF;
       bkey = key < bkey ? key : bkey;
     }
     bkey = wave_min_key(bkey);
-    int c = bkey & 15;
     best_cost = bkey >> 4;
-    int hx = hofs[c][0], hy = hofs[c][1];
+    ring(bkey & 15, 2, &hx, &hy);
     if (a.subpel >= 2) {
-      const int qofs[8][2] = {{-1, -1}, {0, -1}, {1, -1}, {-1, 0}, {1, 0}, {-1, 1}, {0, 1}, {1, 1}};
-      int qkey = (best_cost << 4) | 15;
-      for (int base = 0; base < 8; base += 4) {
+      int qkey = (best_cost << 4) | 0;
+      for (int base = 1; base < 9; base += 4) {
         int ci = base + (lane >> 4);
-        int s = satd_cand(hx + qofs[ci][0], hy + qofs[ci][1]);
-        int mvx = best_mvx + hx + qofs[ci][0], mvy = best_mvy + hy + qofs[ci][1];
+        int ox, oy;
+        ring(ci, 1, &ox, &oy);
+        int s = satd_cand(hx + ox, hy + oy);
+        int mvx = best_mvx + hx + ox, mvy = best_mvy + hy + oy;
         int cost = s + lambda * (h264::se_bits(mvx - pmx) + h264::se_bits(mvy - pmy));
         int key = (cost << 4) | ci;
         qkey = key < qkey ? key : qkey;
       }
       qkey = wave_min_key(qkey);
-      int qc = qkey & 15;
       best_cost = qkey >> 4;
-      if (qc != 15) {
-        hx += qofs[qc][0];
-        hy += qofs[qc][1];
-      }
+      int qx, qy;
+      ring(qkey & 15, 1, &qx, &qy);
+      hx += qx;
+      hy += qy;
     }
     best_mvx += hx;
     best_mvy += hy;

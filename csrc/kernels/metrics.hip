@@ -6,34 +6,50 @@
 namespace mivc {
 namespace gpu {
 
-// sse: [B, 3] uint64 (Y, U, V).  One block of 256 threads per (row-group, slot).
+// sse: [B, 3] uint64 (Y, U, V).  Grid (blocks_per_slot, B); each block strides over
+// rows, each thread over 16-byte column chunks; one atomic per block and plane.
+__device__ __forceinline__ unsigned sq_diff16(uint4 a, uint4 b, int valid) {
+  const uint8_t* pa = reinterpret_cast<const uint8_t*>(&a);
+  const uint8_t* pb = reinterpret_cast<const uint8_t*>(&b);
+  unsigned s = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    int d = static_cast<int>(pa[k]) - pb[k];
+    s += k < valid ? static_cast<unsigned>(d * d) : 0u;
+  }
+  return s;
+}
+
 __global__ void sse_planes(const uint8_t* sy, const uint8_t* su, const uint8_t* sv, const uint8_t* ry,
                            const uint8_t* ru, const uint8_t* rv, int W, int H, int w, int h,
                            unsigned long long* sse) {
-  int slot = blockIdx.y;
-  int row = blockIdx.x;  // luma row; chroma handled by even rows
+  const int slot = blockIdx.y;
   const size_t yo = static_cast<size_t>(slot) * W * H, co = static_cast<size_t>(slot) * (W / 2) * (H / 2);
   unsigned long long acc[3] = {0, 0, 0};
-  if (row < h) {
-    for (int x = threadIdx.x; x < w; x += blockDim.x) {
-      int d = static_cast<int>(sy[yo + static_cast<size_t>(row) * W + x]) - ry[yo + static_cast<size_t>(row) * W + x];
-      acc[0] += static_cast<unsigned long long>(d * d);
-    }
-    if ((row & 1) == 0) {
-      int cr = row >> 1;
-      for (int x = threadIdx.x; x < w / 2; x += blockDim.x) {
-        size_t i = co + static_cast<size_t>(cr) * (W / 2) + x;
-        int du = static_cast<int>(su[i]) - ru[i];
-        int dv = static_cast<int>(sv[i]) - rv[i];
-        acc[1] += static_cast<unsigned long long>(du * du);
-        acc[2] += static_cast<unsigned long long>(dv * dv);
-      }
-    }
+  const int chunks_y = (w + 15) / 16, chunks_c = (w / 2 + 15) / 16;
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+  for (int i = tid; i < chunks_y * h; i += nth) {
+    int r = i / chunks_y, c = (i % chunks_y) * 16;
+    size_t off = yo + static_cast<size_t>(r) * W + c;
+    acc[0] += sq_diff16(*reinterpret_cast<const uint4*>(sy + off), *reinterpret_cast<const uint4*>(ry + off), w - c);
   }
+  for (int i = tid; i < chunks_c * (h / 2); i += nth) {
+    int r = i / chunks_c, c = (i % chunks_c) * 16;
+    size_t off = co + static_cast<size_t>(r) * (W / 2) + c;
+    acc[1] += sq_diff16(*reinterpret_cast<const uint4*>(su + off), *reinterpret_cast<const uint4*>(ru + off), w / 2 - c);
+    acc[2] += sq_diff16(*reinterpret_cast<const uint4*>(sv + off), *reinterpret_cast<const uint4*>(rv + off), w / 2 - c);
+  }
+  __shared__ unsigned long long red[3][4];
   for (int p = 0; p < 3; ++p) {
     unsigned long long v = acc[p];
     for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    if ((threadIdx.x & 63) == 0 && v) atomicAdd(sse + slot * 3 + p, v);
+    if ((threadIdx.x & 63) == 0) red[p][threadIdx.x >> 6] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    unsigned long long v = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) v += red[threadIdx.x][k];
+    if (v) atomicAdd(sse + slot * 3 + threadIdx.x, v);
   }
 }
 
@@ -77,7 +93,7 @@ extern "C" void mivc_launch_sse(int B, int W, int H, int w, int h, const uint8_t
                                 const uint8_t* sv, const uint8_t* ry, const uint8_t* ru, const uint8_t* rv,
                                 unsigned long long* sse, float* ssim_sum, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(sse_planes, dim3(h, B), dim3(256), 0, s, sy, su, sv, ry, ru, rv, W, H, w, h, sse);
+  hipLaunchKernelGGL(sse_planes, dim3(32, B), dim3(256), 0, s, sy, su, sv, ry, ru, rv, W, H, w, h, sse);
   if (ssim_sum) {
     int nwin = (w / 8) * (h / 8);
     hipLaunchKernelGGL(ssim8, dim3((nwin + 255) / 256, B), dim3(256), 0, s, sy, ry, W, H, w, h, ssim_sum);

@@ -113,8 +113,6 @@ class GpuH264Encoder:
         self.intra_flag = torch.zeros((B, nmb), dtype=u8, device=dev)
         self.intra_count = torch.zeros((B,), dtype=i32, device=dev)
         self.qp = torch.zeros((B,), dtype=i32, device=dev)
-        self.ticket = torch.zeros((1,), dtype=i32, device=dev)
-        self.progress = torch.zeros((B * self.hmb,), dtype=i32, device=dev)
         self.err = torch.zeros((1,), dtype=i32, device=dev)
         # pinned staging for the entropy stage (double-buffered)
         self.h_hdr = [torch.empty((B, nmb, MB_HDR_BYTES), dtype=u8).pin_memory() for _ in range(2)]
@@ -169,15 +167,16 @@ class GpuH264Encoder:
             flag_ptr, count_ptr = 0, 0
         self.hip.encode_intra(B, wmb, hmb, sy, su, sv, ry, ru, rv, self._ptr(self.qp), self.p.chroma_qp_offset,
                               self._ptr(hdr), self._ptr(coef), self._ptr(self.nz), flag_ptr, count_ptr,
-                              self._ptr(self.ticket), self._ptr(self.progress), self._ptr(self.err),
-                              int(self.p.i4x4), s)
+                              self._ptr(self.err), int(self.p.i4x4), s)
         if self.p.deblock:
             self.hip.deblock(B, wmb, hmb, ry, ru, rv, self._ptr(hdr), self._ptr(self.nz), self.p.chroma_qp_offset,
-                             0, 0, self._ptr(self.ticket), self._ptr(self.progress), self._ptr(self.err), s)
+                             0, 0, self._ptr(self.err), s)
 
     # ------------------------------------------------------------------ entropy (host)
     def _write_slices(self, k: int, t: int, qp_frame: int, idr: bool, idr_base: int) -> list[tuple[bytes, int]]:
+        t0 = time.perf_counter()
         self.copy_done[k].synchronize()
+        t1 = time.perf_counter()
         hdr = self.h_hdr[k].numpy()
         coef = self.h_coef[k].numpy()
 
@@ -186,7 +185,11 @@ class GpuH264Encoder:
             nal, st = self.host.write_slice(self.cfg, fp, hdr[b], coef[b])
             return nal, st["bits"]
 
-        return list(self.pool.map(one, range(self.B)))
+        out = list(self.pool.map(one, range(self.B)))
+        t2 = time.perf_counter()
+        self.timings["entropy_wait_gpu_s"] = self.timings.get("entropy_wait_gpu_s", 0.0) + (t1 - t0)
+        self.timings["entropy_s"] = self.timings.get("entropy_s", 0.0) + (t2 - t1)
+        return out
 
     # ------------------------------------------------------------------ public API
     @torch.no_grad()
@@ -218,7 +221,9 @@ class GpuH264Encoder:
             qpf = qp_i if idr else qp_p
             # the device/pinned buffers of slot k were last used by step t-2: wait for them
             if pending[k] is not None:
+                tw = time.perf_counter()
                 outs[t - 2] = pending[k].result()
+                self.timings["host_blocked_s"] = self.timings.get("host_blocked_s", 0.0) + time.perf_counter() - tw
                 pending[k] = None
             main.wait_event(self.copy_done[k]) if t >= 2 else None
             cur, ref = self.rec[k], self.rec[1 - k]
@@ -280,6 +285,6 @@ def synth_clip(slots: int, frames: int, width: int, height: int, seed: int = 0, 
     y = torch.empty((slots, frames, height, width), dtype=torch.uint8, device=dev)
     u = torch.empty((slots, frames, height // 2, width // 2), dtype=torch.uint8, device=dev)
     v = torch.empty_like(u)
-    hip.synth(y.data_ptr(), u.data_ptr(), v.data_ptr(), width, height, slots, frames, frame0, seed,
+    hip.synth(y.data_ptr(), u.data_ptr(), v.data_ptr(), width, height, slots, frames, frame0, seed & 0xFFFFFFFF,
               torch.cuda.current_stream(dev).cuda_stream)
     return y, u, v

@@ -1,0 +1,179 @@
+"""Process-group setup and the collectives of the distributed encode.
+
+One process per GPU (``torch.distributed.run``), backend ``nccl`` (= RCCL on
+ROCm, riding xGMI inside an MI355X node) when the ranks own GPUs, ``gloo`` for
+CPU-only runs and tests.  The reference has no collectives at all -- its data
+plane is HTTP in / FTP out (client.go:92-94, 142-172) and its control plane a
+TCP text protocol (server.go:91-121).  Intra-node, the equivalents are:
+
+* CC-1 ``allreduce_stats``: two-pass rate-control statistics (sum of per-rank
+  contributions into one zero-initialised tensor).
+* CC-2/CC-3 ``gather_bitstreams``: segment byte sizes, then one
+  ``all_gather_into_tensor`` of padded uint8 buffers -> rank 0 concatenates the
+  pieces in segment order (the ``concat.sh`` merge of server.go:349-361).
+* CC-4 ``broadcast_object``: segment plan / encoder config.
+* CC-5 ``barrier``: timing fences.
+
+xGMI sizing: payloads are KB (stats) to tens of MB (bitstreams), i.e. latency
+bound; one all-gather per batch, issued async so it overlaps the next batch.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistEnv:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def initialized(self) -> bool:
+        return self.world > 1 and dist.is_initialized()
+
+
+def init(prefer_gpu: bool = True, timeout_s: int = 600) -> DistEnv:
+    """Initialise from torchrun-style env vars (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_*)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    use_gpu = prefer_gpu and torch.cuda.is_available()
+    if use_gpu:
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+        device = torch.device("cuda", torch.cuda.current_device())
+    else:
+        device = torch.device("cpu")
+    env = DistEnv(rank=rank, world=world, local_rank=local, device=device)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = "nccl" if use_gpu else "gloo"
+        if not dist.is_initialized():
+            kw = {}
+            if use_gpu:
+                kw["device_id"] = device
+            dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                    timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        env.backend = backend
+    return env
+
+
+def shutdown(env: DistEnv) -> None:
+    if env.initialized:
+        dist.destroy_process_group()
+
+
+def barrier(env: DistEnv) -> None:
+    if env.initialized:
+        if env.backend == "nccl":
+            dist.barrier(device_ids=[env.device.index])
+        else:
+            dist.barrier()
+
+
+def max_over_ranks(env: DistEnv, value: float) -> float:
+    if not env.initialized:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=env.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(env: DistEnv, value: float) -> float:
+    if not env.initialized:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=env.device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def allreduce_stats(env: DistEnv, stats: torch.Tensor, async_op: bool = False):
+    """CC-1: every rank fills the rows of *its* segments in a zero-initialised
+    [n_frames_total, k] tensor; after the SUM every rank holds the global stats."""
+    if not env.initialized:
+        return None
+    return dist.all_reduce(stats, op=dist.ReduceOp.SUM, async_op=async_op)
+
+
+def broadcast_object(env: DistEnv, obj, src: int = 0):
+    """CC-4: segment plan / config from rank 0."""
+    if not env.initialized:
+        return obj
+    box = [obj]
+    dist.broadcast_object_list(box, src=src)
+    return box[0]
+
+
+class BitstreamGather:
+    """CC-2 + CC-3: gather variable-size per-rank byte payloads to every rank.
+
+    Rank r contributes ``pieces`` (list of bytes, one per local segment).  The
+    payload travels as uint8 device tensors through ``all_gather_into_tensor``
+    (RCCL over xGMI for nccl; gloo on CPU).  ``start()`` issues the collectives
+    asynchronously so the caller can overlap them with the next batch;
+    ``wait()`` returns ``list[list[bytes]]`` indexed [rank][piece].
+    """
+
+    def __init__(self, env: DistEnv, pieces: list[bytes]):
+        self.env = env
+        self.pieces = pieces
+        self.works = []
+
+    def start(self) -> "BitstreamGather":
+        env = self.env
+        if not env.initialized:
+            return self
+        dev = env.device
+        sizes = torch.tensor([len(p) for p in self.pieces], dtype=torch.int64, device=dev)
+        n = torch.tensor([len(self.pieces)], dtype=torch.int64, device=dev)
+        ns = torch.empty(env.world, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(ns, n)
+        self.max_n = int(ns.max().item())
+        pad_sizes = torch.zeros(self.max_n, dtype=torch.int64, device=dev)
+        pad_sizes[: len(self.pieces)] = sizes
+        self.all_sizes = torch.empty(env.world * self.max_n, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(self.all_sizes, pad_sizes)
+        self.ns = ns.cpu().tolist()
+        sizes_h = self.all_sizes.cpu().view(env.world, self.max_n)
+        self.sizes_h = sizes_h
+        per_rank = sizes_h.sum(dim=1)
+        self.max_bytes = int(per_rank.max().item())
+        payload = b"".join(self.pieces)
+        buf = torch.zeros(max(1, self.max_bytes), dtype=torch.uint8)
+        if payload:
+            buf[: len(payload)] = torch.frombuffer(bytearray(payload), dtype=torch.uint8)
+        self.send = buf.to(dev, non_blocking=True)
+        self.recv = torch.empty(env.world * max(1, self.max_bytes), dtype=torch.uint8, device=dev)
+        self.works.append(dist.all_gather_into_tensor(self.recv, self.send, async_op=True))
+        return self
+
+    def wait(self) -> list[list[bytes]]:
+        env = self.env
+        if not env.initialized:
+            return [list(self.pieces)]
+        for w in self.works:
+            w.wait()
+        blob = self.recv.cpu().numpy().tobytes()
+        stride = max(1, self.max_bytes)
+        out = []
+        for r in range(env.world):
+            base = r * stride
+            off = 0
+            lst = []
+            for i in range(self.ns[r]):
+                sz = int(self.sizes_h[r, i])
+                lst.append(blob[base + off: base + off + sz])
+                off += sz
+            out.append(lst)
+        return out
