@@ -26,6 +26,9 @@ namespace h264 {
 // position (x + 4*y) inside the 4x4 block.
 static constexpr uint8_t kZigzag4x4[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
 
+// inverse: raster position (x + 4*y) -> scan index
+static constexpr uint8_t kZigzagInv4x4[16] = {0, 1, 5, 6, 2, 4, 7, 12, 3, 8, 11, 13, 9, 10, 14, 15};
+
 // luma4x4BlkIdx (clause 6.4.3, 8x8 Z-order) -> x,y of the 4x4 block in 4-sample units.
 static constexpr uint8_t kBlkX[16] = {0, 1, 0, 1, 2, 3, 2, 3, 0, 1, 0, 1, 2, 3, 2, 3};
 static constexpr uint8_t kBlkY[16] = {0, 0, 1, 1, 0, 0, 1, 1, 2, 2, 3, 3, 2, 2, 3, 3};
@@ -144,6 +147,10 @@ static constexpr uint8_t kGolombToInterCbp[48] = {
     0,  16, 1,  2,  4,  8,  32, 3,  5,  10, 12, 15, 47, 7,  11, 13,
     14, 6,  9,  31, 35, 37, 42, 44, 33, 34, 36, 40, 39, 43, 45, 46,
     17, 18, 20, 24, 19, 21, 26, 28, 23, 27, 29, 30, 22, 25, 38, 41};
+
+// inverse of the above: cbp -> codeNum
+static constexpr uint8_t kIntraCbpToCode[48] = {3, 29, 30, 17, 31, 18, 37, 8, 32, 38, 19, 9, 20, 10, 11, 2, 16, 33, 34, 21, 35, 22, 39, 4, 36, 40, 23, 5, 24, 6, 7, 1, 41, 42, 43, 25, 44, 26, 46, 12, 45, 47, 27, 13, 28, 14, 15, 0};
+static constexpr uint8_t kInterCbpToCode[48] = {0, 2, 3, 7, 4, 8, 17, 13, 5, 18, 9, 14, 10, 15, 16, 11, 1, 32, 33, 36, 34, 37, 44, 40, 35, 45, 38, 41, 39, 42, 43, 19, 6, 24, 25, 20, 26, 21, 46, 28, 27, 47, 22, 29, 23, 30, 31, 12};
 
 // ---------------------------------------------------------------- helpers
 MIVC_HD int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }

@@ -12,6 +12,10 @@
 #include "h264_decoder.h"
 #include "lowres.h"
 
+namespace mivc {
+int selftest_i4_taps(int trials, uint32_t seed);
+}
+
 namespace py = pybind11;
 using namespace mivc;
 using namespace mivc::h264;
@@ -128,6 +132,8 @@ PYBIND11_MODULE(_host, m) {
     return out;
   });
 
+  m.def("selftest_i4_taps", &mivc::selftest_i4_taps);
+
   m.def("parameter_sets", [](const py::dict& cfg) {
     EncoderConfig c = cfg_from(cfg);
     return to_bytes(write_parameter_sets(make_sps(c), make_pps(c)));
@@ -222,6 +228,55 @@ PYBIND11_MODULE(_host, m) {
         std::memcpy(a.mutable_data(), r.data(), r.size());
         return a;
       });
+
+  // Slice header as big-endian bit-order words (for the GPU CAVLC kernels) + bit count.
+  m.def("slice_header_bits", [](const py::dict& cfg, const py::dict& fp) {
+    EncoderConfig c = cfg_from(cfg);
+    SPS sps = make_sps(c);
+    PPS pps = make_pps(c);
+    SliceHeader sh;
+    bool idr = dget<int>(fp, "idr", 0) != 0;
+    sh.nal_unit_type = idr ? NAL_IDR : NAL_SLICE;
+    sh.nal_ref_idc = idr ? 3 : 2;
+    sh.slice_type = dget<int>(fp, "slice_type", idr ? SLICE_I : SLICE_P);
+    sh.frame_num = dget<int>(fp, "frame_num", 0);
+    sh.idr_pic_id = dget<int>(fp, "idr_pic_id", 0);
+    sh.slice_qp_delta = dget<int>(fp, "qp", 26) - pps.pic_init_qp;
+    sh.disable_deblocking_filter_idc = c.deblock ? 0 : 1;
+    BitWriter bw;
+    write_slice_header(bw, sh, sps, pps);
+    size_t nbits = bw.bit_pos();
+    bw.align_zero();
+    std::vector<uint32_t> words((bw.bytes().size() + 3) / 4, 0);
+    for (size_t i = 0; i < bw.bytes().size(); ++i) words[i / 4] |= static_cast<uint32_t>(bw.bytes()[i]) << (24 - 8 * (i % 4));
+    return py::make_tuple(words, nbits);
+  });
+  // RBSP -> Annex-B NAL unit (start code, header byte, emulation prevention)
+  m.def("nal_wrap", [](py::bytes rbsp, int nal_ref_idc, int nal_unit_type) {
+    std::string s = rbsp;
+    std::vector<uint8_t> v(s.begin(), s.end()), out;
+    out.reserve(v.size() + v.size() / 64 + 8);
+    append_nal(out, nal_ref_idc, nal_unit_type, v);
+    return to_bytes(out);
+  });
+  // batched: one buffer of concatenated RBSPs + sizes -> list of NAL byte strings
+  m.def("nal_wrap_many", [](py::array_t<uint8_t, py::array::c_style> buf, const std::vector<int64_t>& sizes,
+                            int nal_ref_idc, int nal_unit_type) {
+    std::vector<std::vector<uint8_t>> outs(sizes.size());
+    {
+      py::gil_scoped_release rel;
+      const uint8_t* p = buf.data();
+      for (size_t i = 0; i < sizes.size(); ++i) {
+        std::vector<uint8_t> v(p, p + sizes[i]);
+        outs[i].reserve(v.size() + v.size() / 64 + 8);
+        append_nal(outs[i], nal_ref_idc, nal_unit_type, v);
+        p += sizes[i];
+      }
+    }
+    py::list l;
+    for (auto& o : outs) l.append(to_bytes(o));
+    return l;
+  });
 
   m.def("parse_nals", [](py::bytes data) {
     std::string s = data;

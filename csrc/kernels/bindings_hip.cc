@@ -33,6 +33,11 @@ void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t* src_y, con
 void mivc_launch_deblock(int B, int wmb, int hmb, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const void* hdr,
                          const uint8_t* nz, int chroma_qp_offset, int alpha_off, int beta_off, int* err,
                          void* stream);
+size_t mivc_cavlc_mb_bytes();
+void mivc_launch_cavlc(int B, int wmb, int hmb, const void* hdr, const int16_t* coef, void* mbs, int* len,
+                       long long* off, int* trail, long long* total_bits, int* slot_bytes, uint32_t* words,
+                       long long cap_words, const uint32_t* hdr_bits, const int* hdr_nbits, int pslice, int slice_qp,
+                       uint8_t* out, long long* out_off, void* stream);
 void mivc_launch_sse(int B, int W, int H, int w, int h, const uint8_t* sy, const uint8_t* su, const uint8_t* sv,
                      const uint8_t* ry, const uint8_t* ru, const uint8_t* rv, unsigned long long* sse,
                      float* ssim_sum, void* stream);
@@ -93,6 +98,16 @@ PYBIND11_MODULE(_hip, m) {
                       int cqo, int alpha_off, int beta_off, uintptr_t err, uintptr_t stream) {
     mivc_launch_deblock(B, wmb, hmb, P<uint8_t>(ry), P<uint8_t>(ru), P<uint8_t>(rv), P<void>(hdr), P<uint8_t>(nz),
                         cqo, alpha_off, beta_off, P<int>(err), S(stream));
+  });
+  m.def("cavlc_mb_bytes", []() { return mivc_cavlc_mb_bytes(); });
+  m.def("cavlc", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t coef, uintptr_t mbs, uintptr_t len, uintptr_t off,
+                    uintptr_t trail, uintptr_t total_bits, uintptr_t slot_bytes, uintptr_t words, long long cap_words,
+                    uintptr_t hdr_bits, uintptr_t hdr_nbits, int pslice, int slice_qp, uintptr_t out, uintptr_t out_off,
+                    uintptr_t stream) {
+    mivc_launch_cavlc(B, wmb, hmb, P<void>(hdr), P<int16_t>(coef), P<void>(mbs), P<int>(len), P<long long>(off),
+                      P<int>(trail), P<long long>(total_bits), P<int>(slot_bytes), P<uint32_t>(words), cap_words,
+                      P<uint32_t>(hdr_bits), P<int>(hdr_nbits), pslice, slice_qp, P<uint8_t>(out),
+                      P<long long>(out_off), S(stream));
   });
   m.def("sse", [](int B, int W, int H, int w, int h, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t ry,
                   uintptr_t ru, uintptr_t rv, uintptr_t sse, uintptr_t ssim, uintptr_t stream) {

@@ -9,6 +9,7 @@
 // For P frames only MBs flagged by encode_inter (intra_flag) are coded here; the
 // others were reconstructed by encode_inter and only advance the row counter.
 #include "kcommon.h"
+#include "../common/h264_i4_taps.h"
 
 namespace mivc {
 namespace gpu {
@@ -44,6 +45,8 @@ struct IntraShared {
   int lv16dc[16];          // I16 dequantised DC per block position (raster)
   int dc16[16];            // forward DC coefficients (raster)
   uint8_t top16[16], left16[16];
+  int e4[16];              // Intra4x4 neighbour vector of the current block
+  int cdcp[2][4];          // chroma DC predictions per (comp, block)
   uint8_t modes4[16];
   int cost4;
   int mode16, cost16;
@@ -116,21 +119,42 @@ __device__ __forceinline__ int i16_pred(int mode, const IntraShared& S, int dc, 
 
 __device__ __forceinline__ int chroma_pred(int mode, const IntraShared& S, int comp, int mbav, int pa, int pb, int pc,
                                            int X, int Y) {
-  if (mode == 0) return h264::chroma_dc(S.ctop[comp] + 1, S.cleft[comp], mbav, X >> 2, Y >> 2);
+  (void)mbav;
+  if (mode == 0) return S.cdcp[comp][(Y >> 2) * 2 + (X >> 2)];
   if (mode == 1) return S.cleft[comp][Y];
   if (mode == 2) return S.ctop[comp][1 + X];
   return h264::clip1((pa + pb * (X - 3) + pc * (Y - 3) + 16) >> 5);
 }
 
+__device__ __forceinline__ int i4_tap_lds(uint32_t t, const int* e) {
+  return (static_cast<int>((t >> 12) & 7) * e[t & 15] + static_cast<int>((t >> 15) & 7) * e[(t >> 4) & 15] +
+          static_cast<int>((t >> 18) & 7) * e[(t >> 8) & 15] + 2) >> 2;
+}
+
+__device__ __forceinline__ int wave_min(int v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// Lane layout used throughout: a 4x4 block is held by 4 consecutive lanes, one row each
+// (see grp_* in kcommon.h), so a wave processes 16 blocks (a whole 16x16 MB) at once.
 __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared& S, int slot, int mx, int my) {
   const Geom& g = a.g;
   const int lane = lane_id();
+  const int gb = lane & ~3, gy = lane & 3;
   const int W = g.W, cw = g.cw();
   const int X0 = mx * 16, Y0 = my * 16;
   const size_t o = static_cast<size_t>(slot) * g.nmb() + my * g.wmb + mx;
   const int qp = a.qp[slot];
   const int qpc = h264::chroma_qp(qp, a.chroma_qp_offset);
   const int lambda = h264::kLambda[qp];
+  const int qbits = 15 + qp / 6, qbits_c = 15 + qpc / 6;
   const uint8_t* srcy = a.src_y + slot * g.ysize();
   uint8_t* recy = a.rec_y + slot * g.ysize();
   int mbav = 0;
@@ -141,7 +165,6 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
 
   // ---- stage source and reconstructed neighbourhood
   {
-    // 64 lanes x 4 bytes = source MB
     int r = lane >> 2, c4 = (lane & 3) * 4;
     uint32_t w = *reinterpret_cast<const uint32_t*>(srcy + static_cast<size_t>(Y0 + r) * W + X0 + c4);
     *reinterpret_cast<uint32_t*>(S.src + r * 16 + c4) = w;
@@ -196,109 +219,131 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
   if (lane < 16) {
     S.top16[lane] = S.tile[1 + lane];
     S.left16[lane] = S.tile[(lane + 1) * TS];
+  } else if (lane < 24) {  // chroma DC predictions per (comp, block)
+    int c = (lane - 16) >> 2, b = (lane - 16) & 3;
+    S.cdcp[c][b] = h264::chroma_dc(S.ctop[c] + 1, S.cleft[c], mbav, b & 1, b >> 1);
   }
   wave_sync();
 
-  // ---- Intra16x16 decision: lane = mode * 16 + block
+  // ---- Intra16x16 decision: one mode per pass, lane = raster block * 4 + row
+  const int tl16 = S.tile[0];
+  int pa16 = 0, pb16 = 0, pc16 = 0;
+  if ((mbav & (h264::AV_TOP | h264::AV_LEFT | h264::AV_TOPLEFT)) == (h264::AV_TOP | h264::AV_LEFT | h264::AV_TOPLEFT))
+    h264::i16_plane_params(S.top16, S.left16, tl16, &pa16, &pb16, &pc16);
+  const int dc16 = h264::i16_dc(S.top16, S.left16, mbav);
+  int mode16 = 2, cost16 = 0x3FFFFFFF;
   {
-    int mode = lane >> 4, blk = lane & 15;
-    bool ok = h264::i16_mode_ok(mode, mbav);
-    int tl = S.tile[0];
-    int pa = 0, pb = 0, pc = 0, dc = 0;
-    if (mode == 3 && ok) h264::i16_plane_params(S.top16, S.left16, tl, &pa, &pb, &pc);
-    if (mode == 2) dc = h264::i16_dc(S.top16, S.left16, mbav);
-    int bx4 = (blk & 3) * 4, by4 = (blk >> 2) * 4;
-    int r[16];
-#pragma unroll
-    for (int y = 0; y < 4; ++y)
+    const int rb = lane >> 2, rbx = (rb & 3) * 4, rby = (rb >> 2) * 4;
+    for (int m = 0; m < 4; ++m) {
+      if (!h264::i16_mode_ok(m, mbav)) continue;
+      int v[4];
 #pragma unroll
       for (int x = 0; x < 4; ++x)
-        r[y * 4 + x] = static_cast<int>(S.src[(by4 + y) * 16 + bx4 + x]) - i16_pred(mode, S, dc, pa, pb, pc, bx4 + x, by4 + y);
-    int s = h264::satd4x4(r);
-#pragma unroll
-    for (int off = 8; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
-    int key = ok ? ((s + lambda * 4) << 2) | mode : 0x7FFFFFFF;
-    key = min(key, __shfl_xor(key, 16, 64));
-    key = min(key, __shfl_xor(key, 32, 64));
-    if (lane == 0) {
-      S.mode16 = key & 3;
-      S.cost16 = key >> 2;
+        v[x] = static_cast<int>(S.src[(rby + gy) * 16 + rbx + x]) - i16_pred(m, S, dc16, pa16, pb16, pc16, rbx + x, rby + gy);
+      int sblk = grp_satd4x4(v, gy);
+      int tot = wave_sum(gy == 0 ? sblk : 0) + lambda * 4;
+      if (tot < cost16) {
+        cost16 = tot;
+        mode16 = m;
+      }
     }
   }
-  // ---- chroma mode decision: lane = mode * 8 + (comp*4 + block), lanes 0..31
+  // ---- chroma decision: 2 passes; lanes 0-31 mode 2p, lanes 32-63 mode 2p+1; (lane&31) = cblk*4 + row
+  const int cl = lane & 31, cblk = cl >> 2, ccomp = cblk >> 2, cb = cblk & 3;
+  const int cbx = (cb & 1) * 4, cby = (cb >> 1) * 4;
+  int cpa = 0, cpb = 0, cpc = 0;
+  if ((mbav & (h264::AV_TOP | h264::AV_LEFT | h264::AV_TOPLEFT)) == (h264::AV_TOP | h264::AV_LEFT | h264::AV_TOPLEFT))
+    h264::chroma_plane_params(S.ctop[ccomp] + 1, S.cleft[ccomp], static_cast<int>(S.ctop[ccomp][0]), &cpa, &cpb, &cpc);
+  int cmode = 0;
   {
-    int mode = (lane >> 3) & 3, cbk = lane & 7, comp = cbk >> 2, b = cbk & 3;
-    bool ok = lane < 32 && h264::chroma_mode_ok(mode, mbav);
-    int tl = S.ctop[comp][0];
-    int pa = 0, pb = 0, pc = 0;
-    if (mode == 3 && ok) h264::chroma_plane_params(S.ctop[comp] + 1, S.cleft[comp], tl, &pa, &pb, &pc);
-    int bx = (b & 1) * 4, by = (b >> 1) * 4;
-    int r[16];
+    int ckey = 0x7FFFFFFF;
+    for (int pass = 0; pass < 2; ++pass) {
+      int m = pass * 2 + (lane >> 5);
+      bool ok = h264::chroma_mode_ok(m, mbav);
+      int v[4];
 #pragma unroll
-    for (int y = 0; y < 4; ++y)
+      for (int x = 0; x < 4; ++x) {
+        int pv = chroma_pred(m, S, ccomp, mbav, cpa, cpb, cpc, cbx + x, cby + gy);
+        v[x] = static_cast<int>(S.srcc[ccomp][(cby + gy) * 8 + cbx + x]) - pv;
+      }
+      int sblk = grp_satd4x4(v, gy);
+      int t = gy == 0 ? sblk : 0;
 #pragma unroll
-      for (int x = 0; x < 4; ++x)
-        r[y * 4 + x] = static_cast<int>(S.srcc[comp][(by + y) * 8 + bx + x]) -
-                       (ok ? chroma_pred(mode, S, comp, mbav, pa, pb, pc, bx + x, by + y) : 0);
-    int s = h264::satd4x4(r);
-#pragma unroll
-    for (int off = 4; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
-    int key = ok ? (s << 2) | mode : 0x7FFFFFFF;
-    key = min(key, __shfl_xor(key, 8, 64));
-    key = min(key, __shfl_xor(key, 16, 64));
-    if (lane == 0) S.cmode = key & 3;
+      for (int off = 16; off >= 1; off >>= 1) t += __shfl_xor(t, off, 64);  // sum within the half-wave
+      int key = ok ? (t << 2) | m : 0x7FFFFFFF;
+      ckey = min(ckey, key);
+    }
+    ckey = wave_min(ckey);
+    cmode = ckey & 3;
   }
-  wave_sync();
 
-  // ---- Intra4x4 trial (closed loop, sequential over the 16 blocks)
+  // ---- Intra4x4 trial (closed loop over the 16 blocks; 9 modes ranked in parallel)
   bool use4 = false;
   if (a.use_i4x4) {
     for (int i = lane; i < 17 * TS; i += 64) S.t4[i] = S.tile[i];
     wave_sync();
     int total = lambda * 8;
+    const int qm = qp % 6, qs = qp / 6;
+    const int mf0 = h264::kQuantMF[qm][0], mf1 = h264::kQuantMF[qm][1], mf2 = h264::kQuantMF[qm][2];
+    const int dv0 = h264::kDequantV[qm][0], dv1 = h264::kDequantV[qm][1], dv2 = h264::kDequantV[qm][2];
     for (int blk = 0; blk < 16; ++blk) {
       int e[13], av;
       i4_neighbours(S.t4, blk, mbav, e, &av);
-      int bx = h264::kBlkX[blk], by = h264::kBlkY[blk];
+      if (lane < 13) S.e4[lane] = e[lane < 13 ? lane : 0];
+      const int bx = h264::kBlkX[blk], by = h264::kBlkY[blk];
       int ma = bx > 0 ? S.modes4[h264::kRasterToBlk[(bx - 1) + 4 * by]] : S.left_modes[by];
       int mb_ = by > 0 ? S.modes4[h264::kRasterToBlk[bx + 4 * (by - 1)]] : S.top_modes[bx];
       bool dcpred = (bx == 0 && !(mbav & h264::AV_LEFT)) || (by == 0 && !(mbav & h264::AV_TOP));
       int pm = dcpred ? 2 : min(ma, mb_);
-      int key = 0x7FFFFFFF;
-      if (lane < 9 && h264::i4_mode_ok(lane, av)) {
-        int pred[16], r[16];
-        i4_pred_block(lane, av, e, pred);
-#pragma unroll
-        for (int y = 0; y < 4; ++y)
-#pragma unroll
-          for (int x = 0; x < 4; ++x) r[y * 4 + x] = static_cast<int>(S.src[(by * 4 + y) * 16 + bx * 4 + x]) - pred[y * 4 + x];
-        int cost = h264::satd4x4(r) + lambda * (lane == pm ? 1 : 4);
-        key = (cost << 4) | lane;
-      }
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) key = min(key, __shfl_xor(key, off, 64));  // wave-uniform
-      int mode = key & 15;
-      total += key >> 4;
-      // TQ + recon of the chosen mode: 16 lanes, one sample each (transform via the block owner)
-      if (lane == 0) {
-        S.modes4[blk] = static_cast<uint8_t>(mode);
-        int pred[16], res[16];
-        i4_pred_block(mode, av, e, pred);
-#pragma unroll
-        for (int y = 0; y < 4; ++y)
-#pragma unroll
-          for (int x = 0; x < 4; ++x) res[y * 4 + x] = static_cast<int>(S.src[(by * 4 + y) * 16 + bx * 4 + x]) - pred[y * 4 + x];
-        tq_intra(res, qp, S.c4[blk], false, nullptr);
-        h264::inverse_core4x4(res);
-#pragma unroll
-        for (int y = 0; y < 4; ++y)
-#pragma unroll
-          for (int x = 0; x < 4; ++x)
-            S.t4[(by * 4 + 1 + y) * TS + bx * 4 + 1 + x] = static_cast<uint8_t>(h264::clip1(pred[y * 4 + x] + res[y * 4 + x]));
+      int dcv;
+      {
+        bool t = av & h264::AV_TOP, l = av & h264::AV_LEFT;
+        int st = e[1] + e[2] + e[3] + e[4], sl = e[9] + e[10] + e[11] + e[12];
+        dcv = (t && l) ? (st + sl + 4) >> 3 : (l ? (sl + 2) >> 2 : (t ? (st + 2) >> 2 : 128));
       }
       wave_sync();
+      // mode ranking: lane = mode * 4 + row (lanes 0..35)
+      int m = lane >> 2;
+      bool valid = m < 9 && h264::i4_mode_ok(m, av);
+      int mm = m < 9 ? m : 0;
+      int v[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        int pv = mm == 2 ? dcv : i4_tap_lds(h264::kI4Taps[mm][gy * 4 + x], S.e4);
+        v[x] = static_cast<int>(S.src[(by * 4 + gy) * 16 + bx * 4 + x]) - pv;
+      }
+      int sblk = grp_satd4x4(v, gy);
+      int key = (valid && gy == 0) ? ((sblk + lambda * (m == pm ? 1 : 4)) << 4) | m : 0x7FFFFFFF;
+      key = wave_min(key);
+      const int mode = key & 15;
+      total += key >> 4;
+      // transform / quantise / reconstruct the chosen mode (every group computes the same block)
+      int pr[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        pr[x] = mode == 2 ? dcv : i4_tap_lds(h264::kI4Taps[mode][gy * 4 + x], S.e4);
+        v[x] = static_cast<int>(S.src[(by * 4 + gy) * 16 + bx * 4 + x]) - pr[x];
+      }
+      grp_fwd4x4(v, gb, gy);
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        int cls = pos_class(x, gy);
+        int mf = cls == 0 ? mf0 : (cls == 1 ? mf1 : mf2);
+        int dq = cls == 0 ? dv0 : (cls == 1 ? dv1 : dv2);
+        int lv = h264::quant_coef(v[x], mf, qbits, 21);
+        if (lane < 4) S.c4[blk][h264::kZigzagInv4x4[gy * 4 + x]] = static_cast<int16_t>(lv);
+        v[x] = (lv * dq) << qs;
+      }
+      grp_inv4x4(v, gb, gy);
+      if (lane < 4) {
+        uint8_t* row = S.t4 + (by * 4 + 1 + gy) * TS + bx * 4 + 1;
+#pragma unroll
+        for (int x = 0; x < 4; ++x) row[x] = static_cast<uint8_t>(h264::clip1(pr[x] + v[x]));
+      }
+      if (lane == 0) S.modes4[blk] = static_cast<uint8_t>(mode);
+      wave_sync();
     }
-    use4 = total < S.cost16;
+    use4 = total < cost16;
   }
 
   MbHeader* h = a.hdr + o;
@@ -318,26 +363,26 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
       h->i4_modes[lane] = S.modes4[lane];
     }
   } else {
-    // ---- Intra16x16 encode
-    const int mode = S.mode16;
-    int tl = S.tile[0];
-    int pa = 0, pb = 0, pc = 0, dc = 0;
-    if (mode == 3) h264::i16_plane_params(S.top16, S.left16, tl, &pa, &pb, &pc);
-    if (mode == 2) dc = h264::i16_dc(S.top16, S.left16, mbav);
-    int pred[16], res[16];
-    const int blk = lane & 15;
+    // ---- Intra16x16 encode: lane = blkIdx * 4 + row
+    const int blk = lane >> 2;
     const int bx4 = h264::kBlkX[blk] * 4, by4 = h264::kBlkY[blk] * 4;
-    if (lane < 16) {
+    int pr[4], v[4];
 #pragma unroll
-      for (int y = 0; y < 4; ++y)
+    for (int x = 0; x < 4; ++x) {
+      pr[x] = i16_pred(mode16, S, dc16, pa16, pb16, pc16, bx4 + x, by4 + gy);
+      v[x] = static_cast<int>(S.src[(by4 + gy) * 16 + bx4 + x]) - pr[x];
+    }
+    grp_fwd4x4(v, gb, gy);
+    if (gy == 0) S.dc16[h264::kBlkX[blk] + 4 * h264::kBlkY[blk]] = v[0];
+    const int qm = qp % 6, qs = qp / 6;
+    bool any = false;
 #pragma unroll
-        for (int x = 0; x < 4; ++x) {
-          pred[y * 4 + x] = i16_pred(mode, S, dc, pa, pb, pc, bx4 + x, by4 + y);
-          res[y * 4 + x] = static_cast<int>(S.src[(by4 + y) * 16 + bx4 + x]) - pred[y * 4 + x];
-        }
-      int dcc;
-      tq_intra(res, qp, S.c16[blk], true, &dcc);
-      S.dc16[h264::kBlkX[blk] + 4 * h264::kBlkY[blk]] = dcc;
+    for (int x = 0; x < 4; ++x) {
+      int cls = pos_class(x, gy);
+      int lv = (gy == 0 && x == 0) ? 0 : h264::quant_coef(v[x], h264::kQuantMF[qm][cls], qbits, 21);
+      S.c16[blk][h264::kZigzagInv4x4[gy * 4 + x]] = static_cast<int16_t>(lv);
+      any |= lv != 0;
+      v[x] = (lv * h264::kDequantV[qm][cls]) << qs;
     }
     wave_sync();
     if (lane == 0) {
@@ -345,34 +390,28 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
 #pragma unroll
       for (int i = 0; i < 16; ++i) d[i] = S.dc16[i];
       h264::hadamard4x4(d);
-      int qbits = 15 + qp / 6;
-      int lv[16];
+      int lvd[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) lv[r] = h264::quant_coef(d[r] >> 1, h264::kQuantMF[qp % 6][0], qbits + 1, 21);
+      for (int r = 0; r < 16; ++r) lvd[r] = h264::quant_coef(d[r] >> 1, h264::kQuantMF[qm][0], qbits + 1, 21);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) coef[h264::COEF_LUMA_DC + i] = static_cast<int16_t>(lv[h264::kZigzag4x4[i]]);
-      h264::hadamard4x4(lv);
-      int ls = 16 * h264::kDequantV[qp % 6][0];
+      for (int i = 0; i < 16; ++i) coef[h264::COEF_LUMA_DC + i] = static_cast<int16_t>(lvd[h264::kZigzag4x4[i]]);
+      h264::hadamard4x4(lvd);
+      int ls = 16 * h264::kDequantV[qm][0];
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        S.lv16dc[r] = qp >= 36 ? (lv[r] * ls) << (qp / 6 - 6) : (lv[r] * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
+        S.lv16dc[r] = qp >= 36 ? (lvd[r] * ls) << (qp / 6 - 6) : (lvd[r] * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
     }
     wave_sync();
-    if (lane < 16) {
-      res[0] = S.lv16dc[h264::kBlkX[blk] + 4 * h264::kBlkY[blk]];
-      h264::inverse_core4x4(res);
-      bool any = false;
+    if (gy == 0) v[0] = S.lv16dc[h264::kBlkX[blk] + 4 * h264::kBlkY[blk]];
+    grp_inv4x4(v, gb, gy);
+    uint8_t* row = S.tile + (by4 + gy + 1) * TS + bx4 + 1;
 #pragma unroll
-      for (int k = 1; k < 16; ++k) any |= S.c16[blk][k] != 0;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) coef[h264::COEF_LUMA + blk * 16 + k] = S.c16[blk][k];
-      a.nz[o * 16 + h264::kBlkX[blk] + 4 * h264::kBlkY[blk]] = any;
-#pragma unroll
-      for (int y = 0; y < 4; ++y)
-#pragma unroll
-        for (int x = 0; x < 4; ++x)
-          S.tile[(by4 + y + 1) * TS + bx4 + x + 1] = static_cast<uint8_t>(h264::clip1(pred[y * 4 + x] + res[y * 4 + x]));
-    }
+    for (int x = 0; x < 4; ++x) row[x] = static_cast<uint8_t>(h264::clip1(pr[x] + v[x]));
+    any |= __shfl_xor(static_cast<int>(any), 1, 64) != 0;
+    any |= __shfl_xor(static_cast<int>(any), 2, 64) != 0;
+    if (gy == 0) a.nz[o * 16 + h264::kBlkX[blk] + 4 * h264::kBlkY[blk]] = any;
+    wave_sync();
+    for (int i = lane; i < 256; i += 64) coef[h264::COEF_LUMA + i] = S.c16[i >> 4][i & 15];
   }
   wave_sync();
   {  // ---- write luma reconstruction
@@ -382,98 +421,66 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
     for (int k = 0; k < 4; ++k) word |= static_cast<uint32_t>(S.tile[(y + 1) * TS + x4 + k + 1]) << (8 * k);
     *reinterpret_cast<uint32_t*>(recy + static_cast<size_t>(Y0 + y) * W + X0 + x4) = word;
   }
-  // ---- chroma encode (lanes 0..7: comp*4 + block)
-  int cres[16], cpred[16], clv[16];
-  const int cmode = S.cmode;
-  const int comp = (lane >> 2) & 1, cb = lane & 3;
-  if (lane < 8) {
-    int tl = S.ctop[comp][0];
-    int pa = 0, pb = 0, pc = 0;
-    if (cmode == 3) h264::chroma_plane_params(S.ctop[comp] + 1, S.cleft[comp], tl, &pa, &pb, &pc);
-    int bx = (cb & 1) * 4, by = (cb >> 1) * 4;
+  // ---- chroma encode: (lane & 31) = cblk*4 + row; lanes 32-63 duplicate lanes 0-31
+  {
+    const int qm = qpc % 6, qs = qpc / 6;
+    int pr[4], v[4];
 #pragma unroll
-    for (int y = 0; y < 4; ++y)
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        cpred[y * 4 + x] = chroma_pred(cmode, S, comp, mbav, pa, pb, pc, bx + x, by + y);
-        cres[y * 4 + x] = static_cast<int>(S.srcc[comp][(by + y) * 8 + bx + x]) - cpred[y * 4 + x];
-      }
-    h264::forward_core4x4(cres);
-    S.cdc[comp][cb] = cres[0];
-    int qbits = 15 + qpc / 6;
-#pragma unroll
-    for (int r = 0; r < 16; ++r)
-      clv[r] = r == 0 ? 0 : h264::quant_coef(cres[r], h264::kQuantMF[qpc % 6][h264::kPosClass[r]], qbits, 21);
-  }
-  wave_sync();
-  if (lane == 0 || lane == 4) {
-    int c = lane >> 2;
-    int d0 = S.cdc[c][0], d1 = S.cdc[c][1], d2 = S.cdc[c][2], d3 = S.cdc[c][3];
-    int f0 = d0 + d1 + d2 + d3, f1 = d0 - d1 + d2 - d3, f2 = d0 + d1 - d2 - d3, f3 = d0 - d1 - d2 + d3;
-    int qbits = 15 + qpc / 6, mf = h264::kQuantMF[qpc % 6][0];
-    S.clev[c][0] = h264::quant_coef(f0, mf, qbits + 1, 21);
-    S.clev[c][1] = h264::quant_coef(f1, mf, qbits + 1, 21);
-    S.clev[c][2] = h264::quant_coef(f2, mf, qbits + 1, 21);
-    S.clev[c][3] = h264::quant_coef(f3, mf, qbits + 1, 21);
-  }
-  wave_sync();
-  int cx7[4] = {0, 0, 0, 0};
-  if (lane < 8) {
-    int16_t* dst = coef + h264::COEF_CHROMA_AC + (comp * 4 + cb) * 16;
-    bool any_ac = false;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      int v = i == 0 ? 0 : clv[h264::kZigzag4x4[i]];
-      dst[i] = static_cast<int16_t>(v);
-      any_ac |= v != 0;
+    for (int x = 0; x < 4; ++x) {
+      pr[x] = chroma_pred(cmode, S, ccomp, mbav, cpa, cpb, cpc, cbx + x, cby + gy);
+      v[x] = static_cast<int>(S.srcc[ccomp][(cby + gy) * 8 + cbx + x]) - pr[x];
     }
-    int c0 = S.clev[comp][0], c1 = S.clev[comp][1], c2 = S.clev[comp][2], c3 = S.clev[comp][3];
-    if (cb == 0) {
-      coef[h264::COEF_CHROMA_DC + comp * 4 + 0] = static_cast<int16_t>(c0);
-      coef[h264::COEF_CHROMA_DC + comp * 4 + 1] = static_cast<int16_t>(c1);
-      coef[h264::COEF_CHROMA_DC + comp * 4 + 2] = static_cast<int16_t>(c2);
-      coef[h264::COEF_CHROMA_DC + comp * 4 + 3] = static_cast<int16_t>(c3);
+    grp_fwd4x4(v, gb, gy);
+    if (gy == 0 && lane < 32) S.cdc[ccomp][cb] = v[0];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      int cls = pos_class(x, gy);
+      int lv = (gy == 0 && x == 0) ? 0 : h264::quant_coef(v[x], h264::kQuantMF[qm][cls], qbits_c, 21);
+      if (lane < 32) coef[h264::COEF_CHROMA_AC + (ccomp * 4 + cb) * 16 + h264::kZigzagInv4x4[gy * 4 + x]] = static_cast<int16_t>(lv);
+      v[x] = (lv * h264::kDequantV[qm][cls]) << qs;
     }
-    int f;
-    if (cb == 0) f = c0 + c1 + c2 + c3;
-    else if (cb == 1) f = c0 - c1 + c2 - c3;
-    else if (cb == 2) f = c0 + c1 - c2 - c3;
-    else f = c0 - c1 - c2 + c3;
-    int ls = 16 * h264::kDequantV[qpc % 6][0];
+    wave_sync();
+    if (lane < 2) {
+      int c = lane;
+      int d0 = S.cdc[c][0], d1 = S.cdc[c][1], d2 = S.cdc[c][2], d3 = S.cdc[c][3];
+      int f0 = d0 + d1 + d2 + d3, f1 = d0 - d1 + d2 - d3, f2 = d0 + d1 - d2 - d3, f3 = d0 - d1 - d2 + d3;
+      int mf = h264::kQuantMF[qm][0];
+      int l0 = h264::quant_coef(f0, mf, qbits_c + 1, 21), l1 = h264::quant_coef(f1, mf, qbits_c + 1, 21);
+      int l2 = h264::quant_coef(f2, mf, qbits_c + 1, 21), l3 = h264::quant_coef(f3, mf, qbits_c + 1, 21);
+      coef[h264::COEF_CHROMA_DC + c * 4 + 0] = static_cast<int16_t>(l0);
+      coef[h264::COEF_CHROMA_DC + c * 4 + 1] = static_cast<int16_t>(l1);
+      coef[h264::COEF_CHROMA_DC + c * 4 + 2] = static_cast<int16_t>(l2);
+      coef[h264::COEF_CHROMA_DC + c * 4 + 3] = static_cast<int16_t>(l3);
+      int g0 = l0 + l1 + l2 + l3, g1 = l0 - l1 + l2 - l3, g2 = l0 + l1 - l2 - l3, g3 = l0 - l1 - l2 + l3;
+      int ls = 16 * h264::kDequantV[qm][0];
+      S.clev[c][0] = ((g0 * ls) << qs) >> 5;
+      S.clev[c][1] = ((g1 * ls) << qs) >> 5;
+      S.clev[c][2] = ((g2 * ls) << qs) >> 5;
+      S.clev[c][3] = ((g3 * ls) << qs) >> 5;
+    }
+    wave_sync();
+    if (gy == 0) v[0] = S.clev[ccomp][cb];
+    grp_inv4x4(v, gb, gy);
+    uint32_t word = 0;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) cres[r] = r == 0 ? 0 : h264::dequant_coef(clv[r], qpc, r);
-    cres[0] = ((f * ls) << (qpc / 6)) >> 5;
-    bool any = any_ac || c0 || c1 || c2 || c3;
-    if (any) h264::inverse_core4x4(cres);
-    uint8_t* recc = (comp == 0 ? a.rec_u : a.rec_v) + slot * g.csize();
-    int bx = (cb & 1) * 4, by = (cb >> 1) * 4;
-#pragma unroll
-    for (int y = 0; y < 4; ++y) {
-      uint32_t word = 0;
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-        word |= static_cast<uint32_t>(h264::clip1(cpred[y * 4 + x] + (any ? cres[y * 4 + x] : 0))) << (8 * x);
-      *reinterpret_cast<uint32_t*>(recc + static_cast<size_t>(my * 8 + by + y) * cw + mx * 8 + bx) = word;
-      cx7[y] = static_cast<int>(word >> 24);
+    for (int x = 0; x < 4; ++x) word |= static_cast<uint32_t>(h264::clip1(pr[x] + v[x])) << (8 * x);
+    if (lane < 32) {
+      uint8_t* recc = (ccomp == 0 ? a.rec_u : a.rec_v) + slot * g.csize();
+      *reinterpret_cast<uint32_t*>(recc + static_cast<size_t>(my * 8 + cby + gy) * cw + mx * 8 + cbx) = word;
+      if (cb & 1) S.saved_c[ccomp][(cb >> 1) * 4 + gy] = static_cast<uint8_t>(word >> 24);
     }
   }
   // ---- keep this MB's right edge in LDS for the next iteration of this wave
-  if (lane < 16) {
-    S.saved_y[lane] = S.tile[(lane + 1) * TS + 16];
-  }
+  if (lane < 16) S.saved_y[lane] = S.tile[(lane + 1) * TS + 16];
   if (lane >= 16 && lane < 20) {
     int i = lane - 16;
     S.saved_modes[i] = use4 ? S.modes4[h264::kRasterToBlk[3 + 4 * i]] : 2;
-  }
-  if (lane < 8 && (cb & 1)) {  // right column chroma blocks (b = 1, 3) hold x = 7
-#pragma unroll
-    for (int y = 0; y < 4; ++y) S.saved_c[comp][(cb >> 1) * 4 + y] = static_cast<uint8_t>(cx7[y]);
   }
   if (lane == 63) {
     S.saved_x = mx;
     h->kind = use4 ? h264::MBK_I4x4 : h264::MBK_I16x16;
     h->qp = static_cast<int8_t>(qp);
-    h->i16_mode = static_cast<uint8_t>(S.mode16);
+    h->i16_mode = static_cast<uint8_t>(mode16);
     h->chroma_mode = static_cast<uint8_t>(cmode);
     h->flags = 0;
 #pragma unroll

@@ -81,5 +81,60 @@ __device__ __forceinline__ void row_publish(int* prog, int row, int value) {
   if (lane_id() == 0) __hip_atomic_store(prog + row, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// ---------------------------------------------------------------- lane-parallel 4x4 transforms
+// A 4x4 block lives in a group of 4 consecutive lanes (base = lane & ~3); lane base+y
+// holds row y in v[0..3].  Row passes are in-register, column passes exchange the
+// group's rows with ds_bpermute (__shfl).  Every lane of the wave must execute these
+// (uniform control flow) because shuffles read other lanes' registers.
+__device__ __forceinline__ int sel4(int y, int a, int b, int c, int d) { return y == 0 ? a : (y == 1 ? b : (y == 2 ? c : d)); }
+
+// forward integer core transform (encoder side)
+__device__ __forceinline__ void grp_fwd4x4(int* v, int base, int y) {
+  int s03 = v[0] + v[3], d03 = v[0] - v[3], s12 = v[1] + v[2], d12 = v[1] - v[2];
+  int t[4] = {s03 + s12, 2 * d03 + d12, s03 - s12, d03 - 2 * d12};
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    int c0 = __shfl(t[x], base + 0, 64), c1 = __shfl(t[x], base + 1, 64);
+    int c2 = __shfl(t[x], base + 2, 64), c3 = __shfl(t[x], base + 3, 64);
+    int a = c0 + c3, b = c0 - c3, c = c1 + c2, d = c1 - c2;
+    v[x] = sel4(y, a + c, 2 * b + d, a - c, b - 2 * d);
+  }
+}
+
+// normative inverse core transform (clause 8.5.12.2: rows, then columns, then (x+32)>>6)
+__device__ __forceinline__ void grp_inv4x4(int* v, int base, int y) {
+  int e0 = v[0] + v[2], e1 = v[0] - v[2], e2 = (v[1] >> 1) - v[3], e3 = v[1] + (v[3] >> 1);
+  int f[4] = {e0 + e3, e1 + e2, e1 - e2, e0 - e3};
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    int c0 = __shfl(f[x], base + 0, 64), c1 = __shfl(f[x], base + 1, 64);
+    int c2 = __shfl(f[x], base + 2, 64), c3 = __shfl(f[x], base + 3, 64);
+    int g0 = c0 + c2, g1 = c0 - c2, g2 = (c1 >> 1) - c3, g3 = c1 + (c3 >> 1);
+    v[x] = (sel4(y, g0 + g3, g1 + g2, g1 - g2, g0 - g3) + 32) >> 6;
+  }
+}
+
+// SATD of the group's block (sum |Hadamard| / 2), returned on every lane of the group
+__device__ __forceinline__ int grp_satd4x4(const int* v, int y) {
+  int a = v[0] + v[1], b = v[2] + v[3], c = v[0] - v[1], d = v[2] - v[3];
+  int h[4] = {a + b, a - b, c - d, c + d};
+  int s = 0;
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    int p = __shfl_xor(h[x], 1, 64);
+    int u = (y & 1) ? p - h[x] : h[x] + p;
+    int q = __shfl_xor(u, 2, 64);
+    int w = (y & 2) ? q - u : u + q;
+    s += w < 0 ? -w : w;
+  }
+  s += __shfl_xor(s, 1, 64);
+  s += __shfl_xor(s, 2, 64);
+  return s >> 1;
+}
+
+__device__ __forceinline__ int pos_class(int x, int y) {
+  return ((x | y) & 1) == 0 ? 0 : (((x & y) & 1) ? 1 : 2);
+}
+
 }  // namespace gpu
 }  // namespace mivc

@@ -57,15 +57,48 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   __shared__ int16_t s_B1[25 * 20];
   __shared__ uint8_t s_b[20 * 20], s_h[20 * 20], s_j[20 * 20];
 
-  int pmx = 0, pmy = 0;
-  if (a.pred_mv) {
-    pmx = a.pred_mv[(static_cast<size_t>(slot) * g.nmb() + mb) * 2];
-    pmy = a.pred_mv[(static_cast<size_t>(slot) * g.nmb() + mb) * 2 + 1];
-  }
-  int cx = clampi((pmx + 2) >> 2, -128, 128), cy = clampi((pmy + 2) >> 2, -128, 128);
-
-  // ---- stage source MB and reference window
+  // ---- stage the source MB first (needed to rank the search-centre candidates)
   for (int i = lane; i < 256; i += 64) s_src[i] = src[static_cast<size_t>(Y0 + (i >> 4)) * W + X0 + (i & 15)];
+  __syncthreads();
+  // ---- search centre: best (SAD + mv cost) of the temporal predictors at this MB and its
+  // left/top/right neighbours in the previous frame, and the zero vector
+  int pmx = 0, pmy = 0;
+  int cx = 0, cy = 0;
+  if (a.pred_mv) {
+    const int16_t* pm = a.pred_mv + static_cast<size_t>(slot) * g.nmb() * 2;
+    pmx = pm[mb * 2];
+    pmy = pm[mb * 2 + 1];
+    int cand[5][2];
+    int nc = 0;
+    cand[nc][0] = (pmx + 2) >> 2; cand[nc][1] = (pmy + 2) >> 2; ++nc;
+    if (mx > 0) { cand[nc][0] = (pm[(mb - 1) * 2] + 2) >> 2; cand[nc][1] = (pm[(mb - 1) * 2 + 1] + 2) >> 2; ++nc; }
+    if (my > 0) { cand[nc][0] = (pm[(mb - g.wmb) * 2] + 2) >> 2; cand[nc][1] = (pm[(mb - g.wmb) * 2 + 1] + 2) >> 2; ++nc; }
+    if (mx < g.wmb - 1) { cand[nc][0] = (pm[(mb + 1) * 2] + 2) >> 2; cand[nc][1] = (pm[(mb + 1) * 2 + 1] + 2) >> 2; ++nc; }
+    cand[nc][0] = 0; cand[nc][1] = 0; ++nc;
+    int best = 0x7FFFFFFF;
+    const int r = lane >> 2, c4 = (lane & 3) * 4;
+    for (int k = 0; k < nc; ++k) {
+      int dx = clampi(cand[k][0], -128, 128), dy = clampi(cand[k][1], -128, 128);
+      int yy = clampi(Y0 + r + dy, 0, H - 1);
+      const uint8_t* rp = ref + static_cast<size_t>(yy) * W;
+      int sad = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        int d = static_cast<int>(s_src[r * 16 + c4 + q]) - rp[clampi(X0 + c4 + q + dx, 0, W - 1)];
+        sad += d < 0 ? -d : d;
+      }
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) sad += __shfl_xor(sad, off, 64);
+      int cost = sad + lambda * (h264::se_bits(dx * 4 - pmx) + h264::se_bits(dy * 4 - pmy));
+      if (cost < best) {
+        best = cost;
+        cx = dx;
+        cy = dy;
+      }
+    }
+  }
+
+  // ---- stage the reference window
   const int wx0 = X0 + cx - R, wy0 = Y0 + cy - R;
   const int wrows = 16 + 2 * R, wbytes = (16 + 2 * R + 4);
   for (int i = lane; i < wrows * kWinWords; i += 64) {

@@ -38,7 +38,7 @@ class H264Params:
     crf: float | None = 23.0       # CRF (None -> fixed qp)
     qp: int = 26                    # used when crf is None
     ip_offset: int = 3              # I-frame QP = P QP - ip_offset (ipratio 1.4)
-    me_range: int = 16
+    me_range: int = 8              # integer full-search radius around the best predictor
     subpel: int = 2
     i4x4: bool = True
     deblock: bool = True
@@ -80,9 +80,12 @@ class GpuH264Encoder:
     """Batched gfx950 H.264 encoder (Constrained Baseline profile, CAVLC)."""
 
     def __init__(self, params: H264Params, slots: int, device: str | torch.device = "cuda",
-                 entropy_threads: int | None = None):
+                 entropy_threads: int | None = None, entropy: str = "gpu"):
         if params.width % 2 or params.height % 2:
             raise ValueError("width and height must be even")
+        if entropy not in ("gpu", "cpu"):
+            raise ValueError("entropy must be 'gpu' or 'cpu'")
+        self.entropy = entropy
         self.p = params
         self.B = int(slots)
         self.dev = _resolve(device)
@@ -115,8 +118,30 @@ class GpuH264Encoder:
         self.qp = torch.zeros((B,), dtype=i32, device=dev)
         self.err = torch.zeros((1,), dtype=i32, device=dev)
         # pinned staging for the entropy stage (double-buffered)
-        self.h_hdr = [torch.empty((B, nmb, MB_HDR_BYTES), dtype=u8).pin_memory() for _ in range(2)]
-        self.h_coef = [torch.empty((B, nmb, COEF_PER_MB), dtype=i16).pin_memory() for _ in range(2)]
+        if entropy == "cpu":
+            self.h_hdr = [torch.empty((B, nmb, MB_HDR_BYTES), dtype=u8).pin_memory() for _ in range(2)]
+            self.h_coef = [torch.empty((B, nmb, COEF_PER_MB), dtype=i16).pin_memory() for _ in range(2)]
+        else:
+            i64 = torch.int64
+            mbb = int(self.hip.cavlc_mb_bytes())
+            # worst case ~3.3 kbit per MB (I_PCM-like); 4 kbit per MB + header slack
+            self.cap_words = nmb * 128 + 64
+            self.cav_mbs = torch.zeros((B, nmb, mbb), dtype=u8, device=dev)
+            self.cav_len = torch.zeros((B, nmb), dtype=i32, device=dev)
+            self.cav_off = torch.zeros((B, nmb), dtype=i64, device=dev)
+            self.cav_trail = torch.zeros((B,), dtype=i32, device=dev)
+            self.cav_total = torch.zeros((B,), dtype=i64, device=dev)
+            self.cav_words = torch.zeros((B, self.cap_words), dtype=torch.int32, device=dev)
+            self.cav_out_off = torch.zeros((B,), dtype=i64, device=dev)
+            self.cav_hdr_bits = [torch.zeros((B, 16), dtype=i32, device=dev) for _ in range(2)]
+            self.cav_hdr_nbits = [torch.zeros((B,), dtype=i32, device=dev) for _ in range(2)]
+            self.h_hdr_bits = [torch.zeros((B, 16), dtype=i32).pin_memory() for _ in range(2)]
+            self.h_hdr_nbits = [torch.zeros((B,), dtype=i32).pin_memory() for _ in range(2)]
+            self.cav_sizes = [torch.zeros((B,), dtype=i32, device=dev) for _ in range(2)]
+            self.h_sizes = [torch.zeros((B,), dtype=i32).pin_memory() for _ in range(2)]
+            self.cav_out = [torch.zeros((B * self.cap_words * 4,), dtype=u8, device=dev) for _ in range(2)]
+            self.h_out = [torch.empty((B * self.cap_words * 4,), dtype=u8).pin_memory() for _ in range(2)]
+            self.out_done = [torch.cuda.Event() for _ in range(2)]
         self.copy_stream = torch.cuda.Stream(device=dev)
         self.copy_done = [torch.cuda.Event() for _ in range(2)]
         self.compute_done = [torch.cuda.Event() for _ in range(2)]
@@ -171,6 +196,48 @@ class GpuH264Encoder:
         if self.p.deblock:
             self.hip.deblock(B, wmb, hmb, ry, ru, rv, self._ptr(hdr), self._ptr(self.nz), self.p.chroma_qp_offset,
                              0, 0, self._ptr(self.err), s)
+
+    # ------------------------------------------------------------------ entropy (GPU CAVLC)
+    def _frame_params(self, b: int, t: int, qp_frame: int, idr: bool, idr_base: int) -> dict:
+        return dict(idr=int(idr), frame_num=t, idr_pic_id=(idr_base + b) & 0xFFFF, qp=qp_frame)
+
+    def _gpu_cavlc(self, k: int, t: int, qp_frame: int, idr: bool, idr_base: int):
+        """Launch the CAVLC kernels for the current frame step on the compute stream."""
+        hb, hn = self.h_hdr_bits[k], self.h_hdr_nbits[k]
+        hbn, hnn = hb.numpy(), hn.numpy()
+        cache = {}
+        for b in range(self.B):
+            fp = self._frame_params(b, t, qp_frame, idr, idr_base)
+            key = fp["idr_pic_id"] if idr else -1
+            if key not in cache:
+                cache[key] = self.host.slice_header_bits(self.cfg, fp)
+            words, nbits = cache[key]
+            hbn[b, :] = 0
+            hbn[b, : len(words)] = np.array(words, dtype=np.uint32).view(np.int32)
+            hnn[b] = nbits
+        self.cav_hdr_bits[k].copy_(hb, non_blocking=True)
+        self.cav_hdr_nbits[k].copy_(hn, non_blocking=True)
+        P = self._ptr
+        self.hip.cavlc(self.B, self.wmb, self.hmb, P(self.hdr[k]), P(self.coef[k]), P(self.cav_mbs), P(self.cav_len),
+                       P(self.cav_off), P(self.cav_trail), P(self.cav_total), P(self.cav_sizes[k]),
+                       P(self.cav_words), self.cap_words, P(self.cav_hdr_bits[k]), P(self.cav_hdr_nbits[k]),
+                       0 if idr else 1, qp_frame, P(self.cav_out[k]), P(self.cav_out_off), self._stream())
+
+    def _collect_gpu_slices(self, k: int, idr: bool) -> list[tuple[bytes, int]]:
+        t0 = time.perf_counter()
+        self.copy_done[k].synchronize()
+        t1 = time.perf_counter()
+        sizes = self.h_sizes[k].numpy().astype(np.int64).tolist()
+        total = int(sum(sizes))
+        with torch.cuda.device(self.dev), torch.cuda.stream(self.copy_stream):
+            self.h_out[k][:total].copy_(self.cav_out[k][:total], non_blocking=True)
+            self.out_done[k].record(self.copy_stream)
+        self.out_done[k].synchronize()
+        nals = self.host.nal_wrap_many(self.h_out[k][:total].numpy(), sizes, 3 if idr else 2, 5 if idr else 1)
+        t2 = time.perf_counter()
+        self.timings["entropy_wait_gpu_s"] = self.timings.get("entropy_wait_gpu_s", 0.0) + (t1 - t0)
+        self.timings["entropy_s"] = self.timings.get("entropy_s", 0.0) + (t2 - t1)
+        return [(n, len(n) * 8) for n in nals]
 
     # ------------------------------------------------------------------ entropy (host)
     def _write_slices(self, k: int, t: int, qp_frame: int, idr: bool, idr_base: int) -> list[tuple[bytes, int]]:
@@ -236,13 +303,21 @@ class GpuH264Encoder:
                              self._ptr(cur[2]), sse[t].data_ptr(), ssim[t].data_ptr(), self._stream())
             if keep_recon:
                 recons.append(tuple(c.clone() for c in cur))
+            if self.entropy == "gpu":
+                self._gpu_cavlc(k, t, qpf, idr, idr_base)
             self.compute_done[k].record(main)
             with torch.cuda.stream(self.copy_stream):
                 self.copy_stream.wait_event(self.compute_done[k])
-                self.h_hdr[k].copy_(self.hdr[k], non_blocking=True)
-                self.h_coef[k].copy_(self.coef[k], non_blocking=True)
+                if self.entropy == "gpu":
+                    self.h_sizes[k].copy_(self.cav_sizes[k], non_blocking=True)
+                else:
+                    self.h_hdr[k].copy_(self.hdr[k], non_blocking=True)
+                    self.h_coef[k].copy_(self.coef[k], non_blocking=True)
                 self.copy_done[k].record(self.copy_stream)
-            pending[k] = self.pool.submit(self._write_slices, k, t, qpf, idr, idr_base)
+            if self.entropy == "gpu":
+                pending[k] = self.pool.submit(self._collect_gpu_slices, k, idr)
+            else:
+                pending[k] = self.pool.submit(self._write_slices, k, t, qpf, idr, idr_base)
         for t in range(max(0, F - 2), F):
             k = t & 1
             if pending[k] is not None:
