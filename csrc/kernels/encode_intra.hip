@@ -501,15 +501,31 @@ __global__ __launch_bounds__(64 * kIntraWaves) void encode_intra_wavefront(Intra
   if (lane_id() == 0) SS[w].saved_x = -2;
   __syncthreads();
   IntraShared& S = SS[w];
+  const int lane = lane_id();
   for (int y = w; y < g.hmb; y += kIntraWaves) {
-    for (int x = 0; x < g.wmb; ++x) {
-      const size_t o = static_cast<size_t>(slot) * g.nmb() + y * g.wmb + x;
-      if (!a.intra_flag || a.intra_flag[o]) {
+    if (!a.intra_flag) {  // I frame: every MB
+      for (int x = 0; x < g.wmb; ++x) {
         if (y > 0) row_wait(prog, y - 1, min(x + 2, g.wmb), a.err);
         encode_intra_mb(a, S, slot, x, y);
+        row_publish(prog, y, x + 1);
       }
-      row_publish(prog, y, x + 1);
+      continue;
     }
+    // P frame: fetch the row's intra flags 64 at a time and visit only flagged MBs
+    const size_t rowo = static_cast<size_t>(slot) * g.nmb() + static_cast<size_t>(y) * g.wmb;
+    for (int x0 = 0; x0 < g.wmb; x0 += 64) {
+      const int xl = x0 + lane;
+      unsigned long long mask = __ballot(xl < g.wmb && a.intra_flag[rowo + xl] != 0);
+      while (mask) {
+        const int x = x0 + __builtin_ctzll(mask);
+        mask &= mask - 1;
+        if (x > 0) row_publish(prog, y, x);  // MBs before x in this row are final (inter)
+        if (y > 0) row_wait(prog, y - 1, min(x + 2, g.wmb), a.err);
+        encode_intra_mb(a, S, slot, x, y);
+        row_publish(prog, y, x + 1);
+      }
+    }
+    row_publish(prog, y, g.wmb);
   }
 }
 
