@@ -30,7 +30,7 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--slots", type=int, default=int(os.environ.get("MIVC_BENCH_SLOTS", "32")),
+    ap.add_argument("--slots", type=int, default=int(os.environ.get("MIVC_BENCH_SLOTS", "256")),
                     help="segments encoded concurrently per GPU")
     ap.add_argument("--frames", type=int, default=int(os.environ.get("MIVC_BENCH_FRAMES", "60")),
                     help="frames per segment (GOP length)")

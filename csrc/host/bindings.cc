@@ -294,6 +294,17 @@ PYBIND11_MODULE(_host, m) {
     }
     return cuts;
   });
+  m.def("split_pieces", [](py::bytes data, int min_frames) {
+    std::string s = data;
+    std::vector<std::vector<uint8_t>> pieces;
+    {
+      py::gil_scoped_release rel;
+      pieces = split_annexb_pieces(reinterpret_cast<const uint8_t*>(s.data()), s.size(), min_frames);
+    }
+    py::list l;
+    for (auto& pc : pieces) l.append(to_bytes(pc));
+    return l;
+  });
   m.def("stream_info", [](py::bytes data) {
     std::string s = data;
     StreamInfo si = probe_annexb(reinterpret_cast<const uint8_t*>(s.data()), s.size());

@@ -1,0 +1,99 @@
+"""CPU reference backend: the native C++ :class:`CpuEncoder` (csrc/host/cpu_encoder.cc).
+
+Stands in for the reference's CPU ``ffmpeg -vcodec libx264`` (client.go:115) when
+no GPU is present (config 1 plumbing, CPU-only tests of the job API).  Same
+bitstream syntax and QP policy as the GPU encoder (I-frame QP = P QP - 3).
+Pieces are encoded in parallel threads (the C++ encoder releases the GIL).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import time
+
+import numpy as np
+
+from ..jobs.ffargs import EncoderConfig
+from ..utils import yuv
+from .common import BackendError, PieceJob, PieceResult, idr_id, load_clip, output_size, unit_plan, write_log, write_output
+
+
+def resize_clip(clip: yuv.Clip, ow: int, oh: int) -> yuv.Clip:
+    """Bilinear resample (half-pixel centres, like the gfx950 prep kernel)."""
+    if (ow, oh) == (clip.width, clip.height):
+        return clip
+
+    def rs(p: np.ndarray, w: int, h: int) -> np.ndarray:
+        F, ih, iw = p.shape
+        fx = np.clip((np.arange(w) + 0.5) * iw / w - 0.5, 0, iw - 1)
+        fy = np.clip((np.arange(h) + 0.5) * ih / h - 0.5, 0, ih - 1)
+        x0 = fx.astype(np.int64)
+        y0 = fy.astype(np.int64)
+        x1 = np.minimum(x0 + 1, iw - 1)
+        y1 = np.minimum(y0 + 1, ih - 1)
+        tx = (fx - x0)[None, None, :]
+        ty = (fy - y0)[None, :, None]
+        q = p.astype(np.float32)
+        a = q[:, y0][:, :, x0] * (1 - tx) + q[:, y0][:, :, x1] * tx
+        b = q[:, y1][:, :, x0] * (1 - tx) + q[:, y1][:, :, x1] * tx
+        return (a * (1 - ty) + b * ty + 0.5).astype(np.uint8)
+    return yuv.Clip(rs(clip.y, ow, oh), rs(clip.u, ow // 2, oh // 2), rs(clip.v, ow // 2, oh // 2), clip.fps)
+
+
+class CpuBackend:
+    name = "cpu"
+
+    def __init__(self, threads: int | None = None):
+        from ..ops import native
+        self.host = native.host()
+        self.pool = cf.ThreadPoolExecutor(max_workers=threads or min(8, os.cpu_count() or 2))
+
+    def encode_clip(self, key: str, clip: yuv.Clip, cfg: EncoderConfig) -> tuple[bytes, dict]:
+        t0 = time.perf_counter()
+        ow, oh = output_size(cfg, clip)
+        clip = resize_clip(clip, ow, oh)
+        fps = cfg.fps or clip.fps
+        qp = cfg.qp if cfg.qp is not None else int(round(cfg.crf if cfg.crf is not None else 23))
+        hcfg = dict(width=ow, height=oh, fps=fps, qp=max(0, min(51, qp)), keyint=1 << 30)
+        parts, psnr = [], []
+        for u, (s, c) in enumerate(unit_plan(clip.frames, cfg.keyint)):
+            enc = self.host.CpuEncoder(hcfg)
+            parts.append(enc.encode(clip.slice(s, c).i420(), c, idr_id(key, u)))
+            psnr += [st["psnr_y"] for st in enc.stats()]
+        stream = self.host.concat(parts)
+        st = {"backend": "cpu", "idx": key, "frames": clip.frames, "width": ow, "height": oh, "fps": fps,
+              "stream_bytes": len(stream), "psnr_y": float(np.mean(psnr)) if psnr else 0.0,
+              "config": cfg.as_dict(), "seconds": time.perf_counter() - t0}
+        return stream, st
+
+    def encode_clips(self, items: list[tuple[str, yuv.Clip]], cfg: EncoderConfig) -> dict[str, tuple[bytes, dict]]:
+        self._check(cfg)
+        res = self.pool.map(lambda kc: self.encode_clip(kc[0], kc[1], cfg), items)
+        return {k: r for (k, _), r in zip(items, res)}
+
+    @staticmethod
+    def _check(cfg: EncoderConfig):
+        if cfg.codec != "h264":
+            raise BackendError(f"codec {cfg.codec} is not available in the cpu backend")
+        if cfg.bit_depth != 8:
+            raise BackendError("10-bit output is not supported by the cpu backend")
+
+    def _one(self, j: PieceJob, cfg: EncoderConfig) -> PieceResult:
+        try:
+            clip = load_clip(j.in_path)
+        except Exception as e:  # noqa: BLE001
+            return PieceResult(j.idx, False, f"load: {e}")
+        stream, st = self.encode_clip(j.idx, clip, cfg)
+        st["bytes"] = write_output(j, stream, st["fps"])
+        write_log(j, st)
+        return PieceResult(j.idx, True, stats=st)
+
+    def transcode(self, jobs: list[PieceJob], cfg: EncoderConfig) -> list[PieceResult]:
+        try:
+            self._check(cfg)
+        except BackendError as e:
+            return [PieceResult(j.idx, False, str(e)) for j in jobs]
+        return list(self.pool.map(lambda j: self._one(j, cfg), jobs))
+
+    def close(self):
+        self.pool.shutdown(wait=False)

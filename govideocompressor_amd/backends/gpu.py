@@ -1,0 +1,150 @@
+"""gfx950 backend: a batch of pieces -> one batched GPU encode.
+
+The reference worker runs one ``ffmpeg`` process per lease (client.go:101-130).
+An MI355X worker holds several leases at once (worker ``--leases K``) and feeds
+every closed-GOP unit of every piece into ONE :class:`GpuH264Encoder` call: the
+wavefront kernels then see ``units x MB-rows`` independent waves instead of one
+segment's worth, which is what fills 256 CUs.
+
+Units of unequal length are padded to the longest by repeating their last frame;
+the padded frames' NALs are dropped (P frames only reference earlier frames, so
+truncating a closed GOP leaves a conformant stream).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import time
+
+import numpy as np
+
+from ..jobs.ffargs import EncoderConfig
+from ..utils import yuv  # noqa: F401  (type of encode_clips items)
+from .common import (BackendError, PieceJob, PieceResult, Timer, idr_id, load_clip, output_size, unit_plan,
+                     write_log, write_output)
+
+
+class GpuBackend:
+    name = "gpu"
+
+    def __init__(self, device: str = "cuda", entropy: str = "gpu", max_slots: int = 256):
+        import torch
+        if not torch.cuda.is_available():
+            raise BackendError("gpu backend requested but no GPU is visible")
+        from ..ops import native
+        native.hip()  # fail loudly if the gfx950 extension is missing
+        self.torch = torch
+        self.device = torch.device(device)
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.entropy = entropy
+        self.max_slots = max_slots
+        self._enc = {}
+        self._io = cf.ThreadPoolExecutor(max_workers=8)
+
+    def _encoder(self, params, slots: int):
+        from ..models.h264_gpu import GpuH264Encoder
+        key = (params.width, params.height, params.crf, params.qp, slots)
+        enc = self._enc.get(key)
+        if enc is None:
+            for k in list(self._enc):         # keep one encoder resident; HBM is reused
+                self._enc.pop(k).close()
+            enc = GpuH264Encoder(params, slots=slots, device=self.device, entropy=self.entropy)
+            self._enc[key] = enc
+        return enc
+
+    def encode_clips(self, items: list[tuple[str, "yuv.Clip"]], cfg: EncoderConfig,
+                     tm: Timer | None = None) -> dict[str, tuple[bytes, dict]]:
+        """Encode several clips (pieces/segments) together.  ``items``: (index token, clip).
+        Returns token -> (Annex-B stream, stats).  Raises on failure."""
+        from ..models.h264_gpu import H264Params
+        from ..ops import native
+        if cfg.codec != "h264":
+            raise BackendError(f"codec {cfg.codec} is not available in the gpu backend")
+        if cfg.bit_depth != 8:
+            raise BackendError("10-bit H.264 output needs High 10; not supported")
+        tm = tm or Timer()
+        host = native.host()
+        out: dict[str, tuple[bytes, dict]] = {}
+        clips = dict(items)
+        groups: dict[tuple, list[str]] = {}
+        for key, c in items:
+            groups.setdefault((c.width, c.height, output_size(cfg, c)), []).append(key)
+        for (w, h, (ow, oh)), keys in groups.items():
+            units = []  # (key, unit_no, start, count)
+            for key in keys:
+                for u, (s, c) in enumerate(unit_plan(clips[key].frames, cfg.keyint)):
+                    units.append((key, u, s, c))
+            fps = cfg.fps or clips[keys[0]].fps
+            params = H264Params(width=ow, height=oh, fps=fps, crf=cfg.crf, qp=cfg.qp if cfg.qp is not None else 26)
+            unit_out = []
+            for b0 in range(0, len(units), self.max_slots):
+                unit_out += self._encode_chunk(units[b0:b0 + self.max_slots], clips, params, w, h, tm)
+            for key in keys:
+                parts = sorted((x for x in unit_out if x[0] == key), key=lambda x: x[1])
+                stream = host.concat([p[2] for p in parts])
+                st = {"backend": "gpu", "idx": key, "frames": clips[key].frames, "units": len(parts),
+                      "width": ow, "height": oh, "fps": fps, "stream_bytes": len(stream),
+                      "psnr_y": float(np.mean([p[3] for p in parts])), "ssim_y": float(np.mean([p[4] for p in parts])),
+                      "config": cfg.as_dict()}
+                out[key] = (stream, st)
+        return out
+
+    def transcode(self, jobs: list[PieceJob], cfg: EncoderConfig) -> list[PieceResult]:
+        tm = Timer()
+        t0 = time.perf_counter()
+        results: dict[str, PieceResult] = {}
+        items = []
+        futs = {j.idx: self._io.submit(load_clip, j.in_path) for j in jobs}
+        for j in jobs:
+            try:
+                items.append((j.idx, futs[j.idx].result()))
+            except Exception as e:  # noqa: BLE001 - reported to the coordinator
+                results[j.idx] = PieceResult(j.idx, False, f"load: {e}")
+        tm.add("load_s", time.perf_counter() - t0)
+        if items:
+            try:
+                enc = self.encode_clips(items, cfg, tm)
+            except Exception as e:  # noqa: BLE001
+                for key, _ in items:
+                    results[key] = PieceResult(key, False, f"encode: {e}")
+                enc = {}
+            for j in jobs:
+                if j.idx in enc:
+                    stream, st = enc[j.idx]
+                    st["bytes"] = write_output(j, stream, st["fps"])
+                    st["timings"] = dict(tm.t)
+                    write_log(j, st)
+                    results[j.idx] = PieceResult(j.idx, True, stats=st)
+        return [results[j.idx] for j in jobs]
+
+    def _encode_chunk(self, chunk, clips, params, w: int, h: int, tm: Timer):
+        torch = self.torch
+        B = len(chunk)
+        F = max(c for *_, c in chunk)
+        t0 = time.perf_counter()
+        y = torch.empty((B, F, h, w), dtype=torch.uint8).pin_memory()
+        u = torch.empty((B, F, h // 2, w // 2), dtype=torch.uint8).pin_memory()
+        v = torch.empty_like(u).pin_memory()
+        yn, un, vn = y.numpy(), u.numpy(), v.numpy()
+        for b, (key, _, s, c) in enumerate(chunk):
+            cl = clips[key]
+            yn[b, :c], un[b, :c], vn[b, :c] = cl.y[s:s + c], cl.u[s:s + c], cl.v[s:s + c]
+            if c < F:
+                yn[b, c:], un[b, c:], vn[b, c:] = cl.y[s + c - 1], cl.u[s + c - 1], cl.v[s + c - 1]
+        dy = y.to(self.device, non_blocking=True)
+        du = u.to(self.device, non_blocking=True)
+        dv = v.to(self.device, non_blocking=True)
+        tm.add("upload_s", time.perf_counter() - t0)
+        t1 = time.perf_counter()
+        enc = self._encoder(params, B)
+        res = enc.encode(dy, du, dv, idr_ids=[idr_id(key, un_) for key, un_, _, _ in chunk])
+        tm.add("encode_s", time.perf_counter() - t1)
+        ps = enc.parameter_sets()
+        return [(key, un_, ps + b"".join(res[b].nals[:c]), res[b].psnr_y, res[b].ssim_y)
+                for b, (key, un_, s, c) in enumerate(chunk)]
+
+    def close(self):
+        for e in self._enc.values():
+            e.close()
+        self._enc.clear()
+        self._io.shutdown(wait=False)

@@ -62,6 +62,7 @@ class H264Params:
 class SegmentResult:
     bitstream: bytes
     frames: int
+    nals: list[bytes] = field(default_factory=list)   # per-frame slice NALs (bitstream = SPS/PPS + nals)
     bits: list[int] = field(default_factory=list)
     psnr_y: float = 0.0
     psnr_u: float = 0.0
@@ -198,16 +199,16 @@ class GpuH264Encoder:
                              0, 0, self._ptr(self.err), s)
 
     # ------------------------------------------------------------------ entropy (GPU CAVLC)
-    def _frame_params(self, b: int, t: int, qp_frame: int, idr: bool, idr_base: int) -> dict:
-        return dict(idr=int(idr), frame_num=t, idr_pic_id=(idr_base + b) & 0xFFFF, qp=qp_frame)
+    def _frame_params(self, b: int, t: int, qp_frame: int, idr: bool, idr_ids: list[int]) -> dict:
+        return dict(idr=int(idr), frame_num=t, idr_pic_id=idr_ids[b] & 0xFFFF, qp=qp_frame)
 
-    def _gpu_cavlc(self, k: int, t: int, qp_frame: int, idr: bool, idr_base: int):
+    def _gpu_cavlc(self, k: int, t: int, qp_frame: int, idr: bool, idr_ids: list[int]):
         """Launch the CAVLC kernels for the current frame step on the compute stream."""
         hb, hn = self.h_hdr_bits[k], self.h_hdr_nbits[k]
         hbn, hnn = hb.numpy(), hn.numpy()
         cache = {}
         for b in range(self.B):
-            fp = self._frame_params(b, t, qp_frame, idr, idr_base)
+            fp = self._frame_params(b, t, qp_frame, idr, idr_ids)
             key = fp["idr_pic_id"] if idr else -1
             if key not in cache:
                 cache[key] = self.host.slice_header_bits(self.cfg, fp)
@@ -240,7 +241,7 @@ class GpuH264Encoder:
         return [(n, len(n) * 8) for n in nals]
 
     # ------------------------------------------------------------------ entropy (host)
-    def _write_slices(self, k: int, t: int, qp_frame: int, idr: bool, idr_base: int) -> list[tuple[bytes, int]]:
+    def _write_slices(self, k: int, t: int, qp_frame: int, idr: bool, idr_ids: list[int]) -> list[tuple[bytes, int]]:
         t0 = time.perf_counter()
         self.copy_done[k].synchronize()
         t1 = time.perf_counter()
@@ -248,7 +249,7 @@ class GpuH264Encoder:
         coef = self.h_coef[k].numpy()
 
         def one(b: int):
-            fp = dict(idr=int(idr), frame_num=t, idr_pic_id=(idr_base + b) & 0xFFFF, qp=qp_frame)
+            fp = self._frame_params(b, t, qp_frame, idr, idr_ids)
             nal, st = self.host.write_slice(self.cfg, fp, hdr[b], coef[b])
             return nal, st["bits"]
 
@@ -261,18 +262,27 @@ class GpuH264Encoder:
     # ------------------------------------------------------------------ public API
     @torch.no_grad()
     def encode(self, y: torch.Tensor, u: torch.Tensor, v: torch.Tensor, idr_base: int = 0,
-               keep_recon: bool = False, metrics: bool = True) -> list[SegmentResult]:
+               keep_recon: bool = False, metrics: bool = True, idr_ids: list[int] | None = None) -> list[SegmentResult]:
         """Encode B segments of F frames each.
 
         y: [B, F, h, w] uint8 (device), u/v: [B, F, h/2, w/2].  Each slot's output is a
         self-contained Annex-B segment (SPS/PPS + IDR + P...), i.e. one "piece" of the
-        reference's split directory, with idr_pic_id = idr_base + slot.
+        reference's split directory, with idr_pic_id = idr_ids[slot] (default idr_base + slot).
+        When (h, w) differs from the configured size the prep kernel resamples (``-s WxH``).
         """
         B, F = y.shape[0], y.shape[1]
         if B != self.B:
             raise ValueError(f"encoder was built for {self.B} slots, got {B}")
-        if y.shape[2] != self.p.height or y.shape[3] != self.p.width:
-            raise ValueError("frame size mismatch")
+        if y.dtype != torch.uint8 or y.device != self.dev or y.dim() != 4:
+            raise ValueError("y must be a uint8 [B, F, h, w] tensor on the encoder's device")
+        h, w = y.shape[2], y.shape[3]
+        if h % 2 or w % 2 or tuple(u.shape) != (B, F, h // 2, w // 2) or tuple(v.shape) != tuple(u.shape):
+            raise ValueError("u/v must be [B, F, h/2, w/2] with even h, w")
+        if not (y.is_contiguous() and u.is_contiguous() and v.is_contiguous()):
+            raise ValueError("planes must be contiguous")
+        idr_ids = list(idr_ids) if idr_ids is not None else [idr_base + b for b in range(B)]
+        if len(idr_ids) != B:
+            raise ValueError("idr_ids needs one entry per slot")
         torch.cuda.set_device(self.dev)
         qp_i, qp_p = self.p.frame_qps()
         self.err.zero_()
@@ -304,7 +314,7 @@ class GpuH264Encoder:
             if keep_recon:
                 recons.append(tuple(c.clone() for c in cur))
             if self.entropy == "gpu":
-                self._gpu_cavlc(k, t, qpf, idr, idr_base)
+                self._gpu_cavlc(k, t, qpf, idr, idr_ids)
             self.compute_done[k].record(main)
             with torch.cuda.stream(self.copy_stream):
                 self.copy_stream.wait_event(self.compute_done[k])
@@ -317,7 +327,7 @@ class GpuH264Encoder:
             if self.entropy == "gpu":
                 pending[k] = self.pool.submit(self._collect_gpu_slices, k, idr)
             else:
-                pending[k] = self.pool.submit(self._write_slices, k, t, qpf, idr, idr_base)
+                pending[k] = self.pool.submit(self._write_slices, k, t, qpf, idr, idr_ids)
         for t in range(max(0, F - 2), F):
             k = t & 1
             if pending[k] is not None:
@@ -334,7 +344,7 @@ class GpuH264Encoder:
         nwin = (self.p.width // 8) * (self.p.height // 8)
         for b in range(B):
             nals = [outs[t][b][0] for t in range(F)]
-            r = SegmentResult(bitstream=ps + b"".join(nals), frames=F, bits=[outs[t][b][1] for t in range(F)])
+            r = SegmentResult(bitstream=ps + b"".join(nals), frames=F, nals=nals, bits=[outs[t][b][1] for t in range(F)])
             if metrics:
                 def psnr(ssev, n):
                     mse = ssev / n

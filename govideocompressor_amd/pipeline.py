@@ -1,0 +1,138 @@
+"""Single-node, multi-GPU file encode: ``mivc encode`` (SURVEY.md 2.5 / CS-6 collapsed).
+
+The reference's operator workflow is split -> coordinate -> N workers ->
+concat.sh (CS-6).  On one MI355X node the same data flow runs as one process per
+GPU with no files in between:
+
+1. every rank probes the input and builds the same segment plan (closed GOPs;
+   rank 0's plan is broadcast as a consistency check, CC-4);
+2. segments are assigned statically (cost-balanced) or claimed dynamically in
+   batch-sized chunks from the TCPStore ticket counter (the pull scheduling of
+   server.go:175-189);
+3. each rank reads/decodes only its own segments, encodes them as one batched GPU
+   call per chunk and keeps the bitstreams;
+4. one RCCL all-gather of the bitstreams (CC-2/CC-3) and rank 0 concatenates them in
+   segment order into the output (the concat.sh step, server.go:349-361).
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+
+import numpy as np
+
+from .backends import get_backend
+from .jobs import ffargs
+from .parallel import dist as D
+from .parallel.tickets import TicketDispenser
+from .segment import plan as P
+from .segment.probe import annexb_of, probe
+from .utils import yuv
+
+
+def _segments(path: str, info, world: int, slots: int, seg_frames: int | None, gop: int | None):
+    """Returns (kind, segment list).  Raw: frame ranges; compressed: IDR-aligned pieces."""
+    if info.kind in ("h264", "mp4"):
+        from .ops import native
+        h = native.host()
+        target = seg_frames or max(1, info.frames // max(1, world * slots))
+        pieces = h.split_pieces(annexb_of(path, info.kind), target)
+        return "pieces", pieces
+    if seg_frames:
+        pl = P.fixed_plan(info.frames, seg_frames)
+    else:
+        pl = P.balanced_plan(info.frames, world=world, per_rank=slots, min_frames=max(8, gop or 8), gop=gop)
+    return "ranges", pl
+
+
+def _load_segment(path: str, info, kind: str, segs, i: int) -> yuv.Clip:
+    if kind == "pieces":
+        from .ops import native
+        h = native.host()
+        pics = h.decode(segs[i])
+        buf = np.concatenate([p["i420"] for p in pics])
+        return yuv.Clip.from_i420(buf, pics[0]["width"], pics[0]["height"], info.fps)
+    s, c, _ = (int(x) for x in segs[i])
+    if info.kind == "y4m":
+        return yuv.read_y4m(path, s, c)
+    return yuv.read_yuv(path, info.width, info.height, info.fps, info.bit_depth, s, c)
+
+
+def encode_file(path: str, output: str, args: str = "264", backend: str = "auto", slots: int = 16,
+                seg_frames: int | None = None, schedule: str = "static", raw_size: tuple[int, int] | None = None,
+                fps: float = 30.0, log=print) -> dict:
+    env = D.init(prefer_gpu=(backend in ("auto", "gpu")))
+    cfg = ffargs.parse(args)
+    w, h = raw_size or (0, 0)
+    info = probe(path, w, h, fps)
+    kind, segs = _segments(path, info, env.world, slots, seg_frames, cfg.keyint)
+    n = len(segs)
+    sig = (kind, n, int(np.sum([len(x) for x in segs])) if kind == "pieces" else int(np.sum(segs[:, 1])))
+    sig0 = D.broadcast_object(env, sig)
+    if sig0 != sig:
+        raise RuntimeError(f"rank {env.rank}: segment plan differs from rank 0 ({sig} vs {sig0})")
+    be = get_backend(backend, **({"device": str(env.device)} if backend in ("gpu",) or
+                                 (backend == "auto" and env.device.type == "cuda") else {}))
+    impl = be.impl
+    t0 = time.perf_counter()
+    mine: dict[int, bytes] = {}
+    stats: list[dict] = []
+
+    def run(idxs: list[int]):
+        items = [(str(i), _load_segment(path, info, kind, segs, i)) for i in idxs]
+        res = impl.encode_clips(items, cfg)
+        for i in idxs:
+            stream, st = res[str(i)]
+            mine[i] = stream
+            stats.append(st)
+
+    if schedule == "dynamic":
+        td = TicketDispenser(n)
+        while True:
+            got = td.claim(slots)
+            if not got:
+                break
+            run(got)
+    else:
+        if kind == "ranges":
+            my = P.shard(segs, env.rank, env.world, by_cost=True)
+        else:
+            my = list(range(env.rank, n, env.world))
+        for b in range(0, len(my), slots):
+            run(my[b:b + slots])
+    t_enc = time.perf_counter() - t0
+    order = sorted(mine)
+    # CC-2/CC-3: bitstreams + their segment indices to every rank
+    idx_blob = json.dumps(order).encode()
+    g = D.BitstreamGather(env, [idx_blob] + [mine[i] for i in order]).start()
+    gathered = g.wait()
+    out = {"segments": n, "world": env.world, "encode_s_rank": t_enc}
+    if env.is_main:
+        by_idx: dict[int, bytes] = {}
+        for rank_pieces in gathered:
+            ids = json.loads(rank_pieces[0].decode())
+            for i, pc in zip(ids, rank_pieces[1:]):
+                by_idx[i] = pc
+        missing = [i for i in range(n) if i not in by_idx]
+        if missing:
+            raise RuntimeError(f"segments never encoded: {missing[:8]}")
+        from .ops import native
+        hst = native.host()
+        stream = hst.concat([by_idx[i] for i in range(n)])
+        out_fps = cfg.fps or info.fps
+        data = hst.mp4_mux(stream, out_fps) if output.lower().endswith(".mp4") else stream
+        with open(output + ".part", "wb") as f:
+            f.write(data)
+        os.replace(output + ".part", output)
+        frames = info.frames
+        out.update(output=output, bytes=len(data), frames=frames,
+                   psnr_y_rank0=float(np.mean([s["psnr_y"] for s in stats])) if stats else 0.0)
+    wall = D.max_over_ranks(env, time.perf_counter() - t0)
+    out["wall_s"] = wall
+    if env.is_main:
+        out["fps"] = info.frames / wall if wall > 0 else 0.0
+        log(json.dumps(out))
+    be.close()
+    D.shutdown(env)
+    return out

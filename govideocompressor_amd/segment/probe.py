@@ -1,0 +1,110 @@
+"""Container / stream probe (the reference's ``GetSumTime``, server.go:239-265).
+
+The reference runs ``ffmpeg -i <file>``, regex-matches ``Duration: HH:MM:SS``
+from stderr and returns ``h*3600 + m*60 + s + 1`` -- fractional seconds are
+dropped and one second is added (server.go:262).  When the regex does not match
+it panics on an empty slice (defect D2).  Here the duration comes from the
+stream itself:
+
+* raw ``.yuv``  -- geometry/fps/bit depth given by the caller, frames = size / frame bytes
+* ``.y4m``      -- header (W, H, F, C)
+* ``.264/.h264`` Annex-B -- SPS (geometry, VUI timing) + access-unit count (C++ probe)
+* ``.mp4``      -- demuxed by the native ISO-BMFF reader, then as Annex-B
+
+and :func:`reference_seconds` reproduces the reference's integer arithmetic.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import asdict, dataclass
+
+from ..utils import yuv
+
+
+class ProbeError(ValueError):
+    pass
+
+
+@dataclass
+class MediaInfo:
+    path: str
+    kind: str           # yuv | y4m | h264 | mp4
+    width: int
+    height: int
+    fps: float
+    frames: int
+    bit_depth: int = 8
+    bytes: int = 0
+    idr_frames: int = 0
+    entropy: str = ""   # cavlc | cabac for compressed inputs
+    profile_idc: int = 0
+
+    @property
+    def duration_s(self) -> float:
+        return self.frames / self.fps if self.fps > 0 else 0.0
+
+    def as_dict(self) -> dict:
+        d = asdict(self)
+        d["duration_s"] = self.duration_s
+        return d
+
+
+def kind_of(path: str) -> str:
+    ext = os.path.splitext(path)[1].lower()
+    if ext in (".yuv", ".i420", ".raw"):
+        return "yuv"
+    if ext == ".y4m":
+        return "y4m"
+    if ext in (".264", ".h264", ".avc", ".bin"):
+        return "h264"
+    if ext in (".mp4", ".m4v", ".mov"):
+        return "mp4"
+    # sniff
+    with open(path, "rb") as f:
+        head = f.read(16)
+    if head.startswith(b"YUV4MPEG2"):
+        return "y4m"
+    if head[:4] in (b"\x00\x00\x00\x01",) or head[:3] == b"\x00\x00\x01":
+        return "h264"
+    if head[4:8] == b"ftyp":
+        return "mp4"
+    raise ProbeError(f"cannot tell the container of {path}; use .yuv/.y4m/.264/.mp4")
+
+
+def annexb_of(path: str, kind: str | None = None) -> bytes:
+    from ..ops import native
+    kind = kind or kind_of(path)
+    with open(path, "rb") as f:
+        data = f.read()
+    if kind == "mp4":
+        return native.host().mp4_demux(data)
+    if kind == "h264":
+        return data
+    raise ProbeError(f"{path} is not a compressed stream")
+
+
+def probe(path: str, width: int = 0, height: int = 0, fps: float = 30.0, bit_depth: int = 8) -> MediaInfo:
+    if not os.path.isfile(path):
+        raise ProbeError(f"no such file: {path}")
+    size = os.path.getsize(path)
+    kind = kind_of(path)
+    if kind == "yuv":
+        if width <= 0 or height <= 0:
+            raise ProbeError("raw .yuv input needs its geometry (--size WxH)")
+        fb = yuv.frame_bytes(width, height, bit_depth)
+        return MediaInfo(path, kind, width, height, fps, size // fb, bit_depth, size)
+    if kind == "y4m":
+        with open(path, "rb") as f:
+            hd = yuv.parse_y4m_header(f.read(256))
+        return MediaInfo(path, kind, hd.width, hd.height, hd.fps, hd.frames_in(size), hd.bit_depth, size)
+    from ..ops import native
+    info = native.host().stream_info(annexb_of(path, kind))
+    if info["width"] <= 0:
+        raise ProbeError(f"{path}: no H.264 sequence parameter set found")
+    return MediaInfo(path, kind, info["width"], info["height"], info["fps"] or fps, info["frames"], 8, size,
+                     info["idr_frames"], info["entropy"], info["profile_idc"])
+
+
+def reference_seconds(info: MediaInfo) -> int:
+    """``GetSumTime``: whole seconds of the Duration line, plus one (server.go:250-262)."""
+    return int(info.duration_s) + 1
