@@ -60,7 +60,7 @@ def cmd_server_c(a) -> int:
     co = Coordinator(a.fileName, expand_preset(a.ff), pieces=pieces, port=int(a.port), host=a.host,
                      out_root=a.out, lease_timeout=a.lease_timeout, max_retries=a.retries,
                      delete_source=not a.keep_source, merge=a.merge, http_port=a.http_port, http_auth=auth,
-                     log=lambda s: print(s, flush=True))
+                     log=lambda s: print(s, flush=True), src_root=a.src_root)
     return co.run()
 
 
@@ -195,6 +195,7 @@ def build_parser() -> argparse.ArgumentParser:
     c.add_argument("--keep-source", action="store_true", help="do not delete a source piece on success")
     c.add_argument("--merge", action="store_true", help="merge the outputs when every piece is done")
     c.add_argument("--http-port", type=int, default=None, help="serve pieces / accept outputs over HTTP")
+    c.add_argument("--src-root", default=None, help="root the job's <dir> is relative to (default: CWD)")
     c.set_defaults(fn=cmd_server_c)
     t = ss.add_parser("t", help="Touch client")
     t.add_argument("duration", nargs="?", default="11")

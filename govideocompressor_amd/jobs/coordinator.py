@@ -83,9 +83,17 @@ class Coordinator:
                  host: str = "0.0.0.0", out_root: str = "out", lease_timeout: float = 600.0, max_retries: int = 3,
                  delete_source: bool = True, merge: bool = False, http_port: int | None = None,
                  http_auth: tuple[str, str] | None = None, log=print, state_file: bool = True,
-                 hello_wait: float = 0.25):
-        self.dir = split_dir[:-1] if split_dir.endswith("/") and len(split_dir) > 1 else split_dir
-        self.args = args
+                 hello_wait: float = 0.25, src_root: str | None = None):
+        # the split directory on this host, and the token workers receive: its path relative to
+        # the shared source root (the reference's nginx root = the coordinator's CWD, client.go:92)
+        self.src_root = os.path.abspath(src_root or os.getcwd())
+        self.dir = os.path.abspath(split_dir)
+        rel = os.path.relpath(self.dir, self.src_root)
+        if rel == "." or rel.startswith(".."):
+            raise ValueError(f"split directory {split_dir} is not inside the source root {self.src_root}")
+        self.token = rel.replace(os.sep, "/")
+        from .ffargs import expand_preset
+        self.args = expand_preset(args)   # "264"/"265" shorthands (server.go:67-71)
         self.port = port
         self.host = host
         self.out_root = out_root
@@ -177,7 +185,7 @@ class Coordinator:
             if c.closed:
                 continue
             idx = self.queue.pop()
-            job = proto.Job(self.dir, idx, self.args)
+            job = proto.Job(self.token, idx, self.args)
             try:
                 c.writer.write(job.encode(v1=c.v1))
             except Exception as e:  # noqa: BLE001
@@ -189,7 +197,7 @@ class Coordinator:
             p.state, p.attempts, p.worker = "leased", p.attempts + 1, c.worker or c.peer
             p.leased_at = p.last_beat = time.monotonic()
             c.lease = idx
-            self.log(f"[{now_str()}]OnConnect send success[{self.dir};{idx}]")
+            self.log(f"[{now_str()}]OnConnect send success[{self.token};{idx}]")
 
     def _on_reply(self, c: _Conn, r: proto.Reply):
         idx = r.idx
@@ -312,11 +320,11 @@ class Coordinator:
             M.make_concat_script(self.out_dir)
 
     async def run_async(self) -> int:
-        self.log(f"c:[{self.dir}] [{self.args}] [{';'.join(self.pieces) if self.partial else ''}]")
+        self.log(f"c:[{self.token}] [{self.args}] [{';'.join(self.pieces) if self.partial else ''}]")
         if not self.args.strip():
             self.log("warning: empty conversion arguments -- every worker will fail the job")
         try:
-            proto.Job(self.dir, "0", self.args).encode()
+            proto.Job(self.token, "0", self.args).encode()
         except proto.ProtocolError as e:
             self.log(f"bad input argument: {e}")
             return 2
@@ -331,9 +339,8 @@ class Coordinator:
         self.port = server.sockets[0].getsockname()[1]
         if self.http_port is not None:
             from .transport import PieceHttpServer
-            src_root = os.getcwd()  # nginx-style root: the job's <dir> is relative to it (client.go:92)
             user, pw = self.http_auth or (None, None)
-            self.http = PieceHttpServer(src_root, self.out_root, self.host, self.http_port, user, pw).start()
+            self.http = PieceHttpServer(self.src_root, self.out_root, self.host, self.http_port, user, pw).start()
             self.http_port = self.http.port
         self.listening()
         self._check_done()

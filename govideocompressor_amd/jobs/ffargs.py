@@ -74,6 +74,15 @@ def _bitrate(v: str) -> int:
 
 def parse(args: str) -> EncoderConfig:
     """Parse an ffmpeg-style argument string into an EncoderConfig."""
+    try:
+        return _parse(args)
+    except FfArgsError:
+        raise
+    except ValueError as e:  # numeric conversions, shlex quoting
+        raise FfArgsError(f"bad argument value: {e}") from None
+
+
+def _parse(args: str) -> EncoderConfig:
     args = expand_preset(args)
     if not args.strip():
         # reference: empty args make every worker fail with "转换参数为空" (client.go:87-90)
