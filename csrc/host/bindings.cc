@@ -6,6 +6,7 @@
 
 #include <cstring>
 
+#include "../common/h264_enc_math.h"
 #include "annexb.h"
 #include "cavlc_writer.h"
 #include "cpu_encoder.h"
@@ -128,6 +129,7 @@ PYBIND11_MODULE(_host, m) {
     else if (name == "intra_cbp") row(kGolombToIntraCbp, 48);
     else if (name == "inter_cbp") row(kGolombToInterCbp, 48);
     else if (name == "zigzag") row(kZigzag4x4, 16);
+    else if (name == "lambda") out.emplace_back(kLambda, kLambda + 52);
     else throw std::runtime_error("unknown table " + name);
     return out;
   });

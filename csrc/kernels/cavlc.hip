@@ -48,6 +48,7 @@ struct CavlcArgs {
   const int16_t* coef;
   CavlcMb* mbs;
   int* len;              // [B, nmb] bits per MB (0 if skipped)
+  uint16_t* blen;        // [B, nmb, 28] bits per syntax slot (header + residual blocks)
   long long* off;        // [B, nmb] bit offset of each MB
   int* trail;            // [B] trailing skip run
   long long* total_bits; // [B]
@@ -138,31 +139,23 @@ __device__ __forceinline__ void put_level(S& s, int level_code, int sl) {
   }
 }
 
-// c: 16 coefficients in scan order.  Returns TotalCoeff.
+// c: 16 coefficients in scan order (a register array: every loop below is fully
+// unrolled so no index is dynamic and nothing spills to scratch).  Returns TotalCoeff.
 template <class S>
-__device__ int cavlc_block(S& s, const int* c, int start, int end, int maxnum, int nc) {
-  int levels[16], runs[16];
-  int total = 0, total_zeros = 0;
-  int last = -1;
-  for (int i = end; i >= start; --i)
-    if (c[i]) { last = i; break; }
-  if (last >= 0) {
-    int run = 0;
-    for (int i = last; i >= start; --i) {
-      if (c[i]) {
-        if (total > 0) runs[total - 1] = run;
-        levels[total++] = c[i];
-        run = 0;
-      } else {
-        ++run;
-        ++total_zeros;
-      }
-    }
-    runs[total - 1] = run;
-  }
+__device__ __forceinline__ int cavlc_block(S& s, const int (&c)[16], int start, int end, int maxnum, int nc) {
+  uint32_t nz = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) nz |= (i >= start && i <= end && c[i] != 0) ? (1u << i) : 0u;
+  const int total = __popc(nz);
+  // trailing ones: leading run (from the highest frequency) of |level| == 1, at most 3
   int t1 = 0;
-  for (int i = 0; i < total && t1 < 3; ++i) {
-    if (levels[i] == 1 || levels[i] == -1) ++t1; else break;
+  bool t1open = true;
+#pragma unroll
+  for (int i = 15; i >= 0; --i) {
+    if (nz & (1u << i)) {
+      bool one = c[i] == 1 || c[i] == -1;
+      if (t1open && one && t1 < 3) ++t1; else t1open = false;
+    }
   }
   if (nc == -1) {
     s.put(h264::kChromaDcCoeffTokenBits[total * 4 + t1], h264::kChromaDcCoeffTokenLen[total * 4 + t1]);
@@ -171,28 +164,55 @@ __device__ int cavlc_block(S& s, const int* c, int start, int end, int maxnum, i
     s.put(h264::kCoeffTokenBits[t][total * 4 + t1], h264::kCoeffTokenLen[t][total * 4 + t1]);
   }
   if (total == 0) return 0;
-  for (int i = 0; i < t1; ++i) s.put(levels[i] < 0 ? 1u : 0u, 1);
+  const int last = 31 - __clz(nz);
+  const int total_zeros = (last - start + 1) - total;
+  int k = 0;
   int sl = (total > 10 && t1 < 3) ? 1 : 0;
-  for (int i = t1; i < total; ++i) {
-    int lv = levels[i];
-    int code = lv > 0 ? 2 * lv - 2 : -2 * lv - 1;
-    if (i == t1 && t1 < 3) code -= 2;
-    put_level(s, code, sl);
-    if (sl == 0) sl = 1;
-    int al = lv < 0 ? -lv : lv;
-    if (al > (3 << (sl - 1)) && sl < 6) ++sl;
+#pragma unroll
+  for (int i = 15; i >= 0; --i) {
+    if (nz & (1u << i)) {
+      int lv = c[i];
+      if (k < t1) {
+        s.put(lv < 0 ? 1u : 0u, 1);
+      } else {
+        int code = lv > 0 ? 2 * lv - 2 : -2 * lv - 1;
+        if (k == t1 && t1 < 3) code -= 2;
+        put_level(s, code, sl);
+        if (sl == 0) sl = 1;
+        int al = lv < 0 ? -lv : lv;
+        if (al > (3 << (sl - 1)) && sl < 6) ++sl;
+      }
+      ++k;
+    }
   }
   if (total < end - start + 1) {
     if (maxnum == 4) s.put(h264::kChromaDcTotalZerosBits[total - 1][total_zeros], h264::kChromaDcTotalZerosLen[total - 1][total_zeros]);
     else s.put(h264::kTotalZerosBits[total - 1][total_zeros], h264::kTotalZerosLen[total - 1][total_zeros]);
   }
   int zl = total_zeros;
-  for (int i = 0; i < total - 1 && zl > 0; ++i) {
-    int t = (zl < 7 ? zl : 7) - 1;
-    s.put(h264::kRunBeforeBits[t][runs[i]], h264::kRunBeforeLen[t][runs[i]]);
-    zl -= runs[i];
+#pragma unroll
+  for (int i = 15; i >= 1; --i) {
+    uint32_t lower = nz & ((1u << i) - 1u);
+    if ((nz & (1u << i)) && lower != 0 && zl > 0) {
+      int run = i - (31 - __clz(lower)) - 1;
+      int t = (zl < 7 ? zl : 7) - 1;
+      s.put(h264::kRunBeforeBits[t][run], h264::kRunBeforeLen[t][run]);
+      zl -= run;
+    }
   }
   return total;
+}
+
+// 16 int16 coefficients (32 contiguous bytes) -> registers with two 16-byte loads
+__device__ __forceinline__ void load16(const int16_t* p, int (&v)[16]) {
+  const uint4 q0 = reinterpret_cast<const uint4*>(p)[0];
+  const uint4 q1 = reinterpret_cast<const uint4*>(p)[1];
+  const uint32_t w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    v[2 * i] = static_cast<int16_t>(w[i] & 0xFFFFu);
+    v[2 * i + 1] = static_cast<int16_t>(w[i] >> 16);
+  }
 }
 
 // ---------------------------------------------------------------- helpers
@@ -389,7 +409,7 @@ __global__ __launch_bounds__(1024) void cavlc_scan(CavlcArgs a) {
 // lane 0: macroblock header; lanes 1..: residual blocks in coding order.
 // Block slots: 1 = I16 DC, 2..17 = luma blkIdx 0..15, 18..19 = chroma DC, 20..27 = chroma AC.
 template <class S>
-__device__ void mb_header_bits(S& s, const CavlcMb& m, const MbHeader& h, bool pslice) {
+__device__ __forceinline__ void mb_header_bits(S& s, const CavlcMb& m, const MbHeader& h, bool pslice) {
   if (pslice) put_ue(s, static_cast<uint32_t>(m.run));
   const int cbp = m.cbp, cl = cbp & 15, cc = cbp >> 4;
   const int ioff = pslice ? 5 : 0;
@@ -414,30 +434,36 @@ __device__ void mb_header_bits(S& s, const CavlcMb& m, const MbHeader& h, bool p
 }
 
 template <class S>
-__device__ void mb_block_bits(S& s, int slotid, const CavlcMb* mbs, size_t base, int wmb, int mx, int my, const CavlcMb& m,
-                              const int16_t* c) {
+__device__ __forceinline__ void mb_block_bits(S& s, int slotid, const CavlcMb* mbs, size_t base, int wmb, int mx, int my,
+                                              const CavlcMb& m, const int16_t* c) {
   const int cbp = m.cbp, cl = cbp & 15, cc = cbp >> 4;
   int v[16];
   if (slotid == 1) {
     if (m.kind != h264::MBK_I16x16) return;
-    for (int i = 0; i < 16; ++i) v[i] = c[h264::COEF_LUMA_DC + i];
+    load16(c + h264::COEF_LUMA_DC, v);
     cavlc_block(s, v, 0, 15, 16, nc_luma(mbs, base, wmb, mx, my, m.tc, 0, 0));
   } else if (slotid < 18) {
     int blk = slotid - 2;
     if (!(cl & (1 << (blk >> 2)))) return;
-    for (int i = 0; i < 16; ++i) v[i] = c[h264::COEF_LUMA + blk * 16 + i];
+    load16(c + h264::COEF_LUMA + blk * 16, v);
     int nc = nc_luma(mbs, base, wmb, mx, my, m.tc, h264::kBlkX[blk], h264::kBlkY[blk]);
     if (m.kind == h264::MBK_I16x16) cavlc_block(s, v, 1, 15, 15, nc);
     else cavlc_block(s, v, 0, 15, 16, nc);
   } else if (slotid < 20) {
     if (!cc) return;
     int comp = slotid - 18;
-    for (int i = 0; i < 4; ++i) v[i] = c[h264::COEF_CHROMA_DC + comp * 4 + i];
+    const uint2 q = *reinterpret_cast<const uint2*>(c + h264::COEF_CHROMA_DC + comp * 4);
+    v[0] = static_cast<int16_t>(q.x & 0xFFFFu);
+    v[1] = static_cast<int16_t>(q.x >> 16);
+    v[2] = static_cast<int16_t>(q.y & 0xFFFFu);
+    v[3] = static_cast<int16_t>(q.y >> 16);
+#pragma unroll
+    for (int i = 4; i < 16; ++i) v[i] = 0;
     cavlc_block(s, v, 0, 3, 4, -1);
   } else if (slotid < 28) {
     if (!(cc & 2)) return;
     int k = slotid - 20, comp = k >> 2, b = k & 3;
-    for (int i = 0; i < 16; ++i) v[i] = c[h264::COEF_CHROMA_AC + k * 16 + i];
+    load16(c + h264::COEF_CHROMA_AC + k * 16, v);
     cavlc_block(s, v, 1, 15, 15, nc_chroma(mbs, base, wmb, mx, my, m.tc, comp, b & 1, b >> 1));
   }
 }
@@ -454,23 +480,27 @@ __device__ __forceinline__ int lane_exscan32(int v, int lane) {
 }
 
 // ---------------------------------------------------------------- K3: lengths
+// Two MBs per wave (lanes 0-31 and 32-63; 28 syntax slots each).  The bit length of
+// every slot is kept (blen) so the writer knows its lane offsets without re-running
+// the coder.
 __global__ __launch_bounds__(64) void cavlc_length(CavlcArgs a) {
   const Geom& g = a.g;
-  const int mb = blockIdx.x, slot = blockIdx.y, lane = threadIdx.x;
+  const int lane = threadIdx.x, sub = lane & 31;
+  const int mb = blockIdx.x * 2 + (lane >> 5), slot = blockIdx.y;
+  if (mb >= g.nmb()) return;
   const int mx = mb % g.wmb, my = mb / g.wmb;
   const size_t base = static_cast<size_t>(slot) * g.nmb();
   const CavlcMb& m = a.mbs[base + mb];
-  if (!m.coded) {
-    if (lane == 0) a.len[base + mb] = 0;
-    return;
-  }
   LenSink s;
-  if (lane == 0) mb_header_bits(s, m, a.hdr[base + mb], a.pslice);
-  else if (lane < 28) mb_block_bits(s, lane, a.mbs, base, g.wmb, mx, my, m, a.coef + (base + mb) * h264::kCoefPerMb);
+  if (m.coded) {
+    if (sub == 0) mb_header_bits(s, m, a.hdr[base + mb], a.pslice);
+    else if (sub < 28) mb_block_bits(s, sub, a.mbs, base, g.wmb, mx, my, m, a.coef + (base + mb) * h264::kCoefPerMb);
+  }
+  if (sub < 28) a.blen[(base + mb) * 28 + sub] = static_cast<uint16_t>(s.n);
   int n = s.n;
 #pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) n += __shfl_xor(n, off, 64);
-  if (lane == 0) a.len[base + mb] = n;
+  for (int off = 16; off >= 1; off >>= 1) n += __shfl_xor(n, off, 64);
+  if (sub == 0) a.len[base + mb] = n;
 }
 
 // ---------------------------------------------------------------- K4: offsets + header/trailer
@@ -521,20 +551,19 @@ __global__ __launch_bounds__(1024) void cavlc_offsets(CavlcArgs a) {
 // ---------------------------------------------------------------- K5: write
 __global__ __launch_bounds__(64) void cavlc_write(CavlcArgs a) {
   const Geom& g = a.g;
-  const int mb = blockIdx.x, slot = blockIdx.y, lane = threadIdx.x;
+  const int lane = threadIdx.x, sub = lane & 31;
+  const int mb = blockIdx.x * 2 + (lane >> 5), slot = blockIdx.y;
+  if (mb >= g.nmb()) return;
   const int mx = mb % g.wmb, my = mb / g.wmb;
   const size_t base = static_cast<size_t>(slot) * g.nmb();
   const CavlcMb& m = a.mbs[base + mb];
-  if (!m.coded) return;
+  const int n = sub < 28 ? a.blen[(base + mb) * 28 + sub] : 0;
+  const int pre = lane_exscan32(n, lane);
+  if (!m.coded || n == 0) return;
   const int16_t* c = a.coef + (base + mb) * h264::kCoefPerMb;
-  LenSink ls;
-  if (lane == 0) mb_header_bits(ls, m, a.hdr[base + mb], a.pslice);
-  else if (lane < 28) mb_block_bits(ls, lane, a.mbs, base, g.wmb, mx, my, m, c);
-  int pre = lane_exscan32(ls.n, lane);
-  if (lane >= 28 || ls.n == 0) return;
   WordSink ws(a.words + slot * a.cap_words, a.off[base + mb] + pre);
-  if (lane == 0) mb_header_bits(ws, m, a.hdr[base + mb], a.pslice);
-  else mb_block_bits(ws, lane, a.mbs, base, g.wmb, mx, my, m, c);
+  if (sub == 0) mb_header_bits(ws, m, a.hdr[base + mb], a.pslice);
+  else mb_block_bits(ws, sub, a.mbs, base, g.wmb, mx, my, m, c);
   ws.flush();
 }
 
@@ -558,7 +587,8 @@ __global__ __launch_bounds__(256) void cavlc_compact(CavlcArgs a) {
 
 using namespace mivc::gpu;
 
-extern "C" size_t mivc_cavlc_mb_bytes() { return sizeof(CavlcMb); }
+// per-MB scratch the caller allocates: the analysis record + 28 slot lengths
+extern "C" size_t mivc_cavlc_mb_bytes() { return sizeof(CavlcMb) + 28 * sizeof(uint16_t); }
 
 extern "C" void mivc_launch_cavlc(int B, int wmb, int hmb, const void* hdr, const int16_t* coef, void* mbs, int* len,
                                   long long* off, int* trail, long long* total_bits, int* slot_bytes, uint32_t* words,
@@ -568,7 +598,9 @@ extern "C" void mivc_launch_cavlc(int B, int wmb, int hmb, const void* hdr, cons
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.hdr = static_cast<const mivc::h264::MbHeader*>(hdr);
   a.coef = coef;
+  const int nmb = wmb * hmb;
   a.mbs = static_cast<CavlcMb*>(mbs);
+  a.blen = reinterpret_cast<uint16_t*>(static_cast<CavlcMb*>(mbs) + static_cast<size_t>(nmb) * B);
   a.len = len;
   a.off = off;
   a.trail = trail;
@@ -583,12 +615,11 @@ extern "C" void mivc_launch_cavlc(int B, int wmb, int hmb, const void* hdr, cons
   a.out = out;
   a.out_off = out_off;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const int nmb = wmb * hmb;
   hipMemsetAsync(words, 0, sizeof(uint32_t) * cap_words * B, s);
   hipLaunchKernelGGL(cavlc_analyze, dim3(nmb, B), dim3(64), 0, s, a);
   hipLaunchKernelGGL(cavlc_scan, dim3(B), dim3(1024), 0, s, a);
-  hipLaunchKernelGGL(cavlc_length, dim3(nmb, B), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(cavlc_length, dim3((nmb + 1) / 2, B), dim3(64), 0, s, a);
   hipLaunchKernelGGL(cavlc_offsets, dim3(B), dim3(1024), 0, s, a);
-  hipLaunchKernelGGL(cavlc_write, dim3(nmb, B), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(cavlc_write, dim3((nmb + 1) / 2, B), dim3(64), 0, s, a);
   hipLaunchKernelGGL(cavlc_compact, dim3(B), dim3(256), 0, s, a);
 }

@@ -1,11 +1,24 @@
 // Motion estimation for P macroblocks:
-//   1. integer full search in a (2R+1)^2 window around a temporal predictor,
-//      SAD with v_sad_u8 on a reference window staged in LDS (unaligned rows
-//      re-aligned with v_alignbyte_b32);
-//   2. half-sample then quarter-sample refinement around the best integer
-//      vector, on half-pel planes (b, h, j of clause 8.4.2.2.1) computed once per
-//      MB into LDS; cost = SATD (4x4 Hadamard) + lambda * |mvd| bits.
-// One wave64 per macroblock; grid = (nmb, B).
+//   1. search centre = best (SAD + mv cost) of the temporal predictors of this MB and
+//      its left/top/right neighbours and the zero vector;
+//   2. integer full search in a (2R+1)^2 window around it, SAD with v_sad_u8 on a
+//      reference window staged in LDS (row words re-aligned with v_alignbyte_b32);
+//   3. half- then quarter-sample refinement around the best integer vector on the
+//      G/b/h/j planes of clause 8.4.2.2.1 built in LDS from the same window;
+//      cost = SATD (4x4 Hadamard) + lambda * |mvd| bits;
+//   4. the final luma prediction and an open-loop Intra16x16 SATD estimate.
+//
+// Latency structure (the v1 kernel spent most of its time waiting on ~30
+// serialised global loads per MB): every global access is issued in one batch per
+// phase -- the source MB, its intra neighbours and the 5 candidate blocks together,
+// then the whole reference window as aligned dwords (at most 15 in flight per
+// lane) -- and the window carries enough margin that the sub-pel planes come from
+// LDS.  Quarter-sample interpolation is branch-free: every position is the
+// rounded average of two samples of the 4 planes (kQOff), so the four 16-lane
+// candidate groups of a wave never diverge.
+//
+// One wave64 per macroblock; the workgroup id is remapped so each XCD walks a
+// contiguous run of MBs (window rows are shared through that XCD's L2).
 #include "kcommon.h"
 
 namespace mivc {
@@ -26,8 +39,33 @@ struct MeArgs {
 };
 
 constexpr int kMaxR = 16;
-constexpr int kWinRows = 16 + 2 * kMaxR;      // 48
-constexpr int kWinWords = (16 + 2 * kMaxR + 4) / 4;  // 13 words (52 bytes) per row
+constexpr int kML = 4;                                   // window margin left/top (6-tap + qpel)
+constexpr int kMR = 6;                                   // margin right/bottom
+constexpr int kWinRowsMax = 16 + 2 * kMaxR + kML + kMR;  // 58
+constexpr int kWinPitch = 17;                            // words per LDS row (odd: bank spread)
+constexpr int kLoadsPerLane = (kWinRowsMax * 16 + 63) / 64;  // 16 words per row at most
+
+// quarter-sample position (xf, yf) -> two LDS offsets into the plane block P[4][20*20]
+// (plane 0 = G integer, 1 = b half-x, 2 = h half-y, 3 = j centre); sample = (A + B + 1) >> 1
+#define QO(p, du, dv) ((p) * 400 + (dv) * 20 + (du))
+__constant__ short kQOff[16][2] = {
+    {QO(0, 0, 0), QO(0, 0, 0)}, {QO(0, 0, 0), QO(1, 0, 0)}, {QO(1, 0, 0), QO(1, 0, 0)}, {QO(0, 1, 0), QO(1, 0, 0)},
+    {QO(0, 0, 0), QO(2, 0, 0)}, {QO(1, 0, 0), QO(2, 0, 0)}, {QO(3, 0, 0), QO(1, 0, 0)}, {QO(1, 0, 0), QO(2, 1, 0)},
+    {QO(2, 0, 0), QO(2, 0, 0)}, {QO(3, 0, 0), QO(2, 0, 0)}, {QO(3, 0, 0), QO(3, 0, 0)}, {QO(3, 0, 0), QO(2, 1, 0)},
+    {QO(0, 0, 1), QO(2, 0, 0)}, {QO(1, 0, 1), QO(2, 0, 0)}, {QO(3, 0, 0), QO(1, 0, 1)}, {QO(1, 0, 1), QO(2, 1, 0)},
+};
+#undef QO
+
+// Exp-Golomb length of se(v) with a count-leading-zeros instead of a loop
+__device__ __forceinline__ int mvbits(int v) {
+  uint32_t x = (v <= 0 ? static_cast<uint32_t>(-2 * v) : static_cast<uint32_t>(2 * v - 1)) + 1u;
+  return 2 * (31 - __clz(x)) + 1;
+}
+
+// per-byte rounding average (a + b + 1) >> 1 of two packed words
+__device__ __forceinline__ uint32_t avg4(uint32_t a, uint32_t b) {
+  return (a | b) - (((a ^ b) >> 1) & 0x7F7F7F7Fu);
+}
 
 __device__ __forceinline__ int wave_min_key(int key) {
 #pragma unroll
@@ -38,9 +76,132 @@ __device__ __forceinline__ int wave_min_key(int key) {
   return key;
 }
 
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+struct MeShared {
+  uint32_t win[kWinRowsMax * kWinPitch];  // reference window, aligned words
+  alignas(16) uint32_t src[64];            // source MB (16 rows x 4 words)
+  int nb[36];                              // source intra neighbours: top[16], left[16], tl
+  int16_t B1[25 * 20];                     // horizontal 6-tap intermediates
+  uint32_t P32[404];                       // G, b, h, j planes (20x20 bytes each) + pad
+  short qoff[32];                          // kQOff copy (lane-varying index -> LDS, not constant)
+};
+
+// Stage rows [wy, wy+rows) x bytes [xa, xa + 4*words) of the reference, clamped to the frame.
+// All loads are issued before the first LDS store.
+__device__ __forceinline__ void stage_window(MeShared& S, const uint8_t* ref, int W, int H, int xa, int wy,
+                                             int rows, int words, int lane) {
+  const int n = rows * words;
+  uint32_t v[kLoadsPerLane];
+  const bool inside = xa >= 0 && xa + 4 * words <= W;
+  if (inside) {
+#pragma unroll
+    for (int k = 0; k < kLoadsPerLane; ++k) {
+      int i = lane + 64 * k;
+      int r = i / words, w = i - r * words;
+      int yy = clampi(wy + r, 0, H - 1);
+      v[k] = i < n ? *reinterpret_cast<const uint32_t*>(ref + static_cast<size_t>(yy) * W + xa + 4 * w) : 0u;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kLoadsPerLane; ++k) {
+      int i = lane + 64 * k;
+      int r = i / words, w = i - r * words;
+      const uint8_t* row = ref + static_cast<size_t>(clampi(wy + r, 0, H - 1)) * W;
+      uint32_t word = 0;
+      if (i < n) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) word |= static_cast<uint32_t>(row[clampi(xa + 4 * w + b, 0, W - 1)]) << (8 * b);
+      }
+      v[k] = word;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kLoadsPerLane; ++k) {
+    int i = lane + 64 * k;
+    int r = i / words, w = i - r * words;
+    if (i < n) S.win[r * kWinPitch + w] = v[k];
+  }
+}
+
+// Integer search for a compile-time radius: lane = (dx, dy-group of DYN rows).  The lane
+// keeps DYN realigned window rows in registers as a sliding window over the source rows,
+// so each window row is read from LDS once (5 words) and feeds DYN candidates' SADs:
+// ~5x less LDS traffic per candidate than one-candidate-per-lane.  Source rows are LDS
+// broadcasts.
+template <int R>
+__device__ __forceinline__ int int_search_fixed(const MeShared& S, int sh0, int lane, int lambda, int cx, int cy,
+                                                int pmx, int pmy) {
+  constexpr int side = 2 * R + 1;
+  constexpr int G = 64 / side;
+  constexpr int DYN = (side + G - 1) / G;
+  const int g = lane / side, dx = lane - g * side;
+  const int dy0 = g * DYN;
+  const int bo = sh0 + kML + dx;
+  const int w0 = bo >> 2, sh = bo & 3;
+  const int rowbase = g < G ? kML + dy0 : kML;  // idle lanes read valid rows
+  // wv[j] = realigned words of window row (rowbase + r + j) while processing source row r
+  uint32_t wv[DYN][4];
+  auto loadrow = [&](int row, uint32_t (&o)[4]) {
+    const uint32_t* rp = S.win + row * kWinPitch + w0;
+    const uint32_t a0 = rp[0], a1 = rp[1], a2 = rp[2], a3 = rp[3], a4 = rp[4];
+    o[0] = __builtin_amdgcn_alignbyte(a1, a0, sh);
+    o[1] = __builtin_amdgcn_alignbyte(a2, a1, sh);
+    o[2] = __builtin_amdgcn_alignbyte(a3, a2, sh);
+    o[3] = __builtin_amdgcn_alignbyte(a4, a3, sh);
+  };
+#pragma unroll
+  for (int j = 0; j < DYN; ++j) loadrow(rowbase + j, wv[j]);
+  uint32_t acc[DYN];
+#pragma unroll
+  for (int j = 0; j < DYN; ++j) acc[j] = 0;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const uint4 sv = *reinterpret_cast<const uint4*>(S.src + 4 * r);  // LDS broadcast
+#pragma unroll
+    for (int j = 0; j < DYN; ++j) {
+      acc[j] = sad4(sv.x, wv[j][0], acc[j]);
+      acc[j] = sad4(sv.y, wv[j][1], acc[j]);
+      acc[j] = sad4(sv.z, wv[j][2], acc[j]);
+      acc[j] = sad4(sv.w, wv[j][3], acc[j]);
+    }
+    // pin the row's SADs here: the sad intrinsic is pure, and without this the IR
+    // optimiser sinks every SAD below all window loads (194 VGPRs live instead of 46)
+#pragma unroll
+    for (int j = 0; j < DYN; ++j) asm volatile("" : "+v"(acc[j]));
+    if (r < 15) {
+#pragma unroll
+      for (int j = 0; j + 1 < DYN; ++j)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) wv[j][k] = wv[j + 1][k];
+      loadrow(rowbase + r + DYN, wv[DYN - 1]);
+    }
+  }
+  int best = 0x7FFFFFFF;
+#pragma unroll
+  for (int j = 0; j < DYN; ++j) {
+    const int dy = dy0 + j;
+    const int mvx = (cx + dx - R) * 4, mvy = (cy + dy - R) * 4;
+    const int cost = static_cast<int>(acc[j]) + lambda * (mvbits(mvx - pmx) + mvbits(mvy - pmy));
+    const int key = (g < G && dy < side) ? ((cost << 12) | (dy * side + dx)) : 0x7FFFFFFF;
+    best = key < best ? key : best;
+  }
+  return best;
+}
+
 __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   const Geom& g = a.g;
-  const int mb = blockIdx.x, slot = blockIdx.y;
+  // XCD-aware remap: hardware deals workgroups round-robin over the 8 XCDs; give each XCD
+  // a contiguous range of (slot, MB) so neighbouring windows share its L2.
+  const int nmb = g.nmb();
+  const int total = nmb * g.B;
+  int lin = blockIdx.y * gridDim.x + blockIdx.x;
+  if ((total & 7) == 0) lin = (lin & 7) * (total >> 3) + (lin >> 3);
+  const int slot = lin / nmb, mb = lin - slot * nmb;
   const int mx = mb % g.wmb, my = mb / g.wmb;
   const int lane = threadIdx.x;
   const int X0 = mx * 16, Y0 = my * 16;
@@ -51,191 +212,182 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   const int lambda = h264::kLambda[qp];
   const int R = a.range < kMaxR ? a.range : kMaxR;
 
-  __shared__ uint32_t s_win[kWinRows * kWinWords];
-  __shared__ uint8_t s_src[256];
-  __shared__ uint8_t s_G[26 * 26];
-  __shared__ int16_t s_B1[25 * 20];
-  __shared__ uint8_t s_b[20 * 20], s_h[20 * 20], s_j[20 * 20];
+  __shared__ MeShared S;
 
-  // ---- stage the source MB first (needed to rank the search-centre candidates)
-  for (int i = lane; i < 256; i += 64) s_src[i] = src[static_cast<size_t>(Y0 + (i >> 4)) * W + X0 + (i & 15)];
-  __syncthreads();
-  // ---- search centre: best (SAD + mv cost) of the temporal predictors at this MB and its
-  // left/top/right neighbours in the previous frame, and the zero vector
+  // ---- phase 0: source MB, its intra neighbours, candidate vectors (one batch of loads)
+  const int r4 = lane >> 2, c4 = (lane & 3) * 4;
+  const uint32_t my_src = *reinterpret_cast<const uint32_t*>(src + static_cast<size_t>(Y0 + r4) * W + X0 + c4);
+  int nbv = 0;
+  if (lane < 16) nbv = my > 0 ? src[static_cast<size_t>(Y0 - 1) * W + X0 + lane] : 0;
+  else if (lane < 32) nbv = mx > 0 ? src[static_cast<size_t>(Y0 + lane - 16) * W + X0 - 1] : 0;
+  else if (lane == 32) nbv = (mx > 0 && my > 0) ? src[static_cast<size_t>(Y0 - 1) * W + X0 - 1] : 0;
   int pmx = 0, pmy = 0;
-  int cx = 0, cy = 0;
+  int cand_x[5] = {0, 0, 0, 0, 0}, cand_y[5] = {0, 0, 0, 0, 0};
   if (a.pred_mv) {
-    const int16_t* pm = a.pred_mv + static_cast<size_t>(slot) * g.nmb() * 2;
+    const int16_t* pm = a.pred_mv + static_cast<size_t>(slot) * nmb * 2;
     pmx = pm[mb * 2];
     pmy = pm[mb * 2 + 1];
-    int cand[5][2];
-    int nc = 0;
-    cand[nc][0] = (pmx + 2) >> 2; cand[nc][1] = (pmy + 2) >> 2; ++nc;
-    if (mx > 0) { cand[nc][0] = (pm[(mb - 1) * 2] + 2) >> 2; cand[nc][1] = (pm[(mb - 1) * 2 + 1] + 2) >> 2; ++nc; }
-    if (my > 0) { cand[nc][0] = (pm[(mb - g.wmb) * 2] + 2) >> 2; cand[nc][1] = (pm[(mb - g.wmb) * 2 + 1] + 2) >> 2; ++nc; }
-    if (mx < g.wmb - 1) { cand[nc][0] = (pm[(mb + 1) * 2] + 2) >> 2; cand[nc][1] = (pm[(mb + 1) * 2 + 1] + 2) >> 2; ++nc; }
-    cand[nc][0] = 0; cand[nc][1] = 0; ++nc;
+    cand_x[0] = (pmx + 2) >> 2;
+    cand_y[0] = (pmy + 2) >> 2;
+    if (mx > 0) { cand_x[1] = (pm[(mb - 1) * 2] + 2) >> 2; cand_y[1] = (pm[(mb - 1) * 2 + 1] + 2) >> 2; }
+    if (my > 0) { cand_x[2] = (pm[(mb - g.wmb) * 2] + 2) >> 2; cand_y[2] = (pm[(mb - g.wmb) * 2 + 1] + 2) >> 2; }
+    if (mx < g.wmb - 1) { cand_x[3] = (pm[(mb + 1) * 2] + 2) >> 2; cand_y[3] = (pm[(mb + 1) * 2 + 1] + 2) >> 2; }
+  }
+  uint32_t cref[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    cand_x[k] = clampi(cand_x[k], -128, 128);
+    cand_y[k] = clampi(cand_y[k], -128, 128);
+    const uint8_t* rp = ref + static_cast<size_t>(clampi(Y0 + r4 + cand_y[k], 0, H - 1)) * W;
+    uint32_t w = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) w |= static_cast<uint32_t>(rp[clampi(X0 + c4 + b + cand_x[k], 0, W - 1)]) << (8 * b);
+    cref[k] = w;
+  }
+  S.src[lane] = my_src;
+  if (lane < 33) S.nb[lane] = nbv;
+  if (lane < 32) S.qoff[lane] = kQOff[lane >> 1][lane & 1];
+  int cx = 0, cy = 0;
+  {
     int best = 0x7FFFFFFF;
-    const int r = lane >> 2, c4 = (lane & 3) * 4;
-    for (int k = 0; k < nc; ++k) {
-      int dx = clampi(cand[k][0], -128, 128), dy = clampi(cand[k][1], -128, 128);
-      int yy = clampi(Y0 + r + dy, 0, H - 1);
-      const uint8_t* rp = ref + static_cast<size_t>(yy) * W;
-      int sad = 0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        int d = static_cast<int>(s_src[r * 16 + c4 + q]) - rp[clampi(X0 + c4 + q + dx, 0, W - 1)];
-        sad += d < 0 ? -d : d;
-      }
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) sad += __shfl_xor(sad, off, 64);
-      int cost = sad + lambda * (h264::se_bits(dx * 4 - pmx) + h264::se_bits(dy * 4 - pmy));
+    for (int k = 0; k < 5; ++k) {
+      int sad = wave_sum(static_cast<int>(sad4(my_src, cref[k], 0)));
+      int cost = sad + lambda * (mvbits(cand_x[k] * 4 - pmx) + mvbits(cand_y[k] * 4 - pmy));
       if (cost < best) {
         best = cost;
-        cx = dx;
-        cy = dy;
+        cx = cand_x[k];
+        cy = cand_y[k];
       }
     }
   }
 
-  // ---- stage the reference window
-  const int wx0 = X0 + cx - R, wy0 = Y0 + cy - R;
-  const int wrows = 16 + 2 * R, wbytes = (16 + 2 * R + 4);
-  for (int i = lane; i < wrows * kWinWords; i += 64) {
-    int r = i / kWinWords, w = i % kWinWords;
-    uint32_t word = 0;
-    int yy = clampi(wy0 + r, 0, H - 1);
-    const uint8_t* row = ref + static_cast<size_t>(yy) * W;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      int xx = wx0 + w * 4 + k;
-      uint32_t px = (w * 4 + k < wbytes) ? row[clampi(xx, 0, W - 1)] : 0u;
-      word |= px << (8 * k);
-    }
-    s_win[r * kWinWords + w] = word;
-  }
+  // ---- phase 1: reference window around the centre, with margins for the sub-pel planes
+  const int wrows = 16 + 2 * R + kML + kMR;
+  int wx = X0 + cx - R - kML;
+  int xa = wx & ~3, sh0 = wx - xa;
+  const int wwords = (wrows + 3) / 4 + 1;
+  stage_window(S, ref, W, H, xa, Y0 + cy - R - kML, wrows, wwords, lane);
   __syncthreads();
-  uint32_t srcw[64];
-#pragma unroll
-  for (int i = 0; i < 64; ++i) srcw[i] = reinterpret_cast<const uint32_t*>(s_src)[i];
 
-  // ---- integer full search
-  const int side = 2 * R + 1, ncand = side * side;
-  int best_key = 0x7FFFFFFF;
-  for (int p = lane; p < ncand; p += 64) {
-    int dy = p / side, dx = p % side;
-    int w0 = dx >> 2, sh = dx & 3;
-    uint32_t sad = 0;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const uint32_t* rowp = s_win + (dy + r) * kWinWords + w0;
-      uint32_t a0 = rowp[0], a1 = rowp[1], a2 = rowp[2], a3 = rowp[3], a4 = rowp[4];
-      uint32_t b0 = __builtin_amdgcn_alignbyte(a1, a0, sh);
-      uint32_t b1 = __builtin_amdgcn_alignbyte(a2, a1, sh);
-      uint32_t b2 = __builtin_amdgcn_alignbyte(a3, a2, sh);
-      uint32_t b3 = __builtin_amdgcn_alignbyte(a4, a3, sh);
-      sad = sad4(srcw[r * 4 + 0], b0, sad);
-      sad = sad4(srcw[r * 4 + 1], b1, sad);
-      sad = sad4(srcw[r * 4 + 2], b2, sad);
-      sad = sad4(srcw[r * 4 + 3], b3, sad);
+  // ---- phase 2: integer full search
+  const int side = 2 * R + 1;
+  int best_key;
+  if (R == 8) {
+    best_key = int_search_fixed<8>(S, sh0, lane, lambda, cx, cy, pmx, pmy);
+  } else {
+    const int ncand = side * side;
+    best_key = 0x7FFFFFFF;
+    for (int p = lane; p < ncand; p += 64) {
+      int dy = p / side, dx = p - dy * side;
+      int bo = sh0 + kML + dx;
+      int w0 = bo >> 2, sh = bo & 3;
+      uint32_t sad = 0;
+#pragma unroll 4
+      for (int r = 0; r < 16; ++r) {
+        const uint32_t* rowp = S.win + (kML + dy + r) * kWinPitch + w0;
+        const uint4 sv = *reinterpret_cast<const uint4*>(S.src + r * 4);
+        uint32_t a0 = rowp[0], a1 = rowp[1], a2 = rowp[2], a3 = rowp[3], a4 = rowp[4];
+        sad = sad4(sv.x, __builtin_amdgcn_alignbyte(a1, a0, sh), sad);
+        sad = sad4(sv.y, __builtin_amdgcn_alignbyte(a2, a1, sh), sad);
+        sad = sad4(sv.z, __builtin_amdgcn_alignbyte(a3, a2, sh), sad);
+        sad = sad4(sv.w, __builtin_amdgcn_alignbyte(a4, a3, sh), sad);
+      }
+      int mvx = (cx + dx - R) * 4, mvy = (cy + dy - R) * 4;
+      int cost = static_cast<int>(sad) + lambda * (mvbits(mvx - pmx) + mvbits(mvy - pmy));
+      int key = (cost << 12) | p;
+      best_key = key < best_key ? key : best_key;
     }
-    int mvx = (cx + dx - R) * 4, mvy = (cy + dy - R) * 4;
-    int cost = static_cast<int>(sad) + lambda * (h264::se_bits(mvx - pmx) + h264::se_bits(mvy - pmy));
-    int key = (cost << 12) | p;
-    best_key = key < best_key ? key : best_key;
   }
-  // zero vector (may lie outside the window)
-  {
-    uint32_t sad = 0;
-    int r = lane >> 2, c4 = (lane & 3) * 4;
-    const uint8_t* rp = ref + static_cast<size_t>(Y0 + r) * W + X0 + c4;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      int d = static_cast<int>(s_src[r * 16 + c4 + k]) - rp[k];
-      sad += d < 0 ? -d : d;
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) sad += __shfl_xor(static_cast<int>(sad), off, 64);
-    int cost = static_cast<int>(sad) + lambda * (h264::se_bits(-pmx) + h264::se_bits(-pmy));
+  // the zero vector lies outside the window only when the centre is more than R away
+  const bool zero_outside = cx < -R || cx > R || cy < -R || cy > R;
+  if (zero_outside) {
+    int sad = wave_sum(static_cast<int>(sad4(my_src, *reinterpret_cast<const uint32_t*>(
+                                                          ref + static_cast<size_t>(Y0 + r4) * W + X0 + c4), 0)));
+    int cost = sad + lambda * (mvbits(-pmx) + mvbits(-pmy));
     int key = (cost << 12) | 4095;
     best_key = key < best_key ? key : best_key;
   }
   best_key = wave_min_key(best_key);
-  int bp = best_key & 4095;
+  const int bp = best_key & 4095;
   int bx, by;  // integer displacement
   if (bp == 4095) {
     bx = 0;
     by = 0;
+    // re-stage the window around the zero vector for the sub-pel planes (rare)
+    __syncthreads();
+    cx = 0;
+    cy = 0;
+    wx = X0 - R - kML;
+    xa = wx & ~3;
+    sh0 = wx - xa;
+    stage_window(S, ref, W, H, xa, Y0 - R - kML, wrows, wwords, lane);
+    __syncthreads();
   } else {
-    bx = cx + (bp % side) - R;
-    by = cy + (bp / side) - R;
+    by = bp / side;
+    bx = cx + (bp - by * side) - R;
+    by = cy + by - R;
   }
   int best_mvx = bx * 4, best_mvy = by * 4;
 
-  // ---- sub-pel refinement
-  // planes origin: integer (bx-2, by-2) relative to the MB; G origin (bx-4, by-4)
-  for (int i = lane; i < 26 * 26; i += 64) {
-    int r = i / 26, c = i % 26;
-    int yy = clampi(Y0 + by - 4 + r, 0, H - 1), xx = clampi(X0 + bx - 4 + c, 0, W - 1);
-    s_G[i] = ref[static_cast<size_t>(yy) * W + xx];
-  }
-  __syncthreads();
+  // ---- phase 3: sub-pel planes from the window.  s_G(r, c) = pixel (bx-4+c, by-4+r)
+  const uint8_t* winb = reinterpret_cast<const uint8_t*>(S.win);
+  const int gx0 = sh0 + bx - cx + R, gy0 = by - cy + R;  // window byte column / row of pixel (bx-4, by-4)
+  auto Gs = [&](int r, int c) -> int { return winb[(gy0 + r) * (kWinPitch * 4) + gx0 + c]; };
   for (int i = lane; i < 25 * 20; i += 64) {
-    int r = i / 20, u = i % 20;
-    const uint8_t* gr = s_G + r * 26 + u;
-    s_B1[i] = static_cast<int16_t>(h264::tap6(gr[0], gr[1], gr[2], gr[3], gr[4], gr[5]));
+    int r = i / 20, u = i - r * 20;
+    S.B1[i] = static_cast<int16_t>(h264::tap6(Gs(r, u), Gs(r, u + 1), Gs(r, u + 2), Gs(r, u + 3), Gs(r, u + 4),
+                                               Gs(r, u + 5)));
   }
   __syncthreads();
+  uint8_t* Pb = reinterpret_cast<uint8_t*>(S.P32);
   for (int i = lane; i < 400; i += 64) {
-    int v = i / 20, u = i % 20;
-    s_b[i] = static_cast<uint8_t>(h264::clip1((s_B1[(v + 2) * 20 + u] + 16) >> 5));
-    const uint8_t* gc = s_G + v * 26 + u + 2;
-    s_h[i] = static_cast<uint8_t>(h264::clip1((h264::tap6(gc[0], gc[26], gc[52], gc[78], gc[104], gc[130]) + 16) >> 5));
-    const int16_t* bc = s_B1 + v * 20 + u;
+    int v = i / 20, u = i - v * 20;
+    Pb[i] = static_cast<uint8_t>(Gs(v + 2, u + 2));
+    Pb[400 + i] = static_cast<uint8_t>(h264::clip1((S.B1[(v + 2) * 20 + u] + 16) >> 5));
+    Pb[800 + i] = static_cast<uint8_t>(h264::clip1(
+        (h264::tap6(Gs(v, u + 2), Gs(v + 1, u + 2), Gs(v + 2, u + 2), Gs(v + 3, u + 2), Gs(v + 4, u + 2),
+                    Gs(v + 5, u + 2)) + 16) >> 5));
+    const int16_t* bc = S.B1 + v * 20 + u;
     int j1 = h264::tap6(bc[0], bc[20], bc[40], bc[60], bc[80], bc[100]);
-    s_j[i] = static_cast<uint8_t>(h264::clip1((j1 + 512) >> 10));
+    Pb[1200 + i] = static_cast<uint8_t>(h264::clip1((j1 + 512) >> 10));
   }
+  if (lane < 4) S.P32[400 + lane] = 0;
   __syncthreads();
 
-  auto G = [&](int u, int v) -> int { return s_G[(v + 2) * 26 + u + 2]; };
-  auto qpel = [&](int u, int v, int xf, int yf) -> int {
-    if (xf == 0 && yf == 0) return G(u, v);
-    if (yf == 0) {
-      int b = s_b[v * 20 + u];
-      if (xf == 2) return b;
-      return ((xf == 1 ? G(u, v) : G(u + 1, v)) + b + 1) >> 1;
-    }
-    if (xf == 0) {
-      int h = s_h[v * 20 + u];
-      if (yf == 2) return h;
-      return ((yf == 1 ? G(u, v) : G(u, v + 1)) + h + 1) >> 1;
-    }
-    if (xf == 2 && yf == 2) return s_j[v * 20 + u];
-    if (xf == 2) return (s_j[v * 20 + u] + (yf == 1 ? s_b[v * 20 + u] : s_b[(v + 1) * 20 + u]) + 1) >> 1;
-    if (yf == 2) return (s_j[v * 20 + u] + (xf == 1 ? s_h[v * 20 + u] : s_h[v * 20 + u + 1]) + 1) >> 1;
-    int b = yf == 1 ? s_b[v * 20 + u] : s_b[(v + 1) * 20 + u];
-    int h = xf == 1 ? s_h[v * 20 + u] : s_h[v * 20 + u + 1];
-    return (b + h + 1) >> 1;
+  // 4 consecutive plane bytes at byte offset `off` (any alignment) as one word
+  auto load4 = [&](int off) -> uint32_t {
+    const int w = off >> 2;
+    return __builtin_amdgcn_alignbyte(S.P32[w + 1], S.P32[w], off & 3);
   };
+  // 4 predicted samples of a row starting at plane coords (u, v) (G(u,v) = pixel (bx-2+u, by-2+v))
+  auto pred4 = [&](int u, int v, int offa, int offb) -> uint32_t {
+    const int base = v * 20 + u;
+    return avg4(load4(base + offa), load4(base + offb));
+  };
+  const uint8_t* srcb = reinterpret_cast<const uint8_t*>(S.src);
   // SATD of candidate (dqx, dqy) quarter offsets relative to (4bx, 4by): this lane does 4x4 block (lane&15)
+  const int blk = lane & 15;
+  const int px0 = (blk & 3) * 4, py0 = (blk >> 2) * 4;
+  uint32_t srow[4];
+#pragma unroll
+  for (int y = 0; y < 4; ++y) srow[y] = S.src[(py0 + y) * 4 + (px0 >> 2)];
   auto satd_cand = [&](int dqx, int dqy) -> int {
-    int blk = lane & 15;
-    int px0 = (blk & 3) * 4, py0 = (blk >> 2) * 4;
-    int xf = dqx & 3, yf = dqy & 3, ox = dqx >> 2, oy = dqy >> 2;
+    int q = (dqy & 3) * 4 + (dqx & 3), ox = dqx >> 2, oy = dqy >> 2;
+    int offa = S.qoff[2 * q], offb = S.qoff[2 * q + 1];
     int r[16];
 #pragma unroll
-    for (int y = 0; y < 4; ++y)
+    for (int y = 0; y < 4; ++y) {
+      const uint32_t pw = pred4(px0 + ox + 2, py0 + y + oy + 2, offa, offb);
 #pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        int u = px0 + x + ox + 2, v = py0 + y + oy + 2;
-        r[y * 4 + x] = static_cast<int>(s_src[(py0 + y) * 16 + px0 + x]) - qpel(u, v, xf, yf);
-      }
+      for (int x = 0; x < 4; ++x)
+        r[y * 4 + x] = static_cast<int>((srow[y] >> (8 * x)) & 255u) - static_cast<int>((pw >> (8 * x)) & 255u);
+    }
     int s = h264::satd4x4(r);
 #pragma unroll
     for (int off = 8; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
     return s;
   };
-
   // candidate c of a 3x3 ring (0 = centre, 1..8 = the 8 neighbours) -> offsets in units of `step`
   auto ring = [](int c, int step, int* dx, int* dy) {
     int idx = c == 0 ? 4 : (c <= 4 ? c - 1 : c);
@@ -245,7 +397,6 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   int best_cost;
   int hx = 0, hy = 0;
   {
-    // centre + 8 half-pel neighbours (3 passes of 4 candidates, 16 lanes each)
     int bkey = 0x7FFFFFFF;
     const int ncand_h = a.subpel >= 1 ? 9 : 1;
     for (int base = 0; base < ncand_h; base += 4) {
@@ -255,7 +406,7 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
       ring(c, 2, &ox, &oy);
       int s = satd_cand(ox, oy);
       int mvx = best_mvx + ox, mvy = best_mvy + oy;
-      int cost = s + lambda * (h264::se_bits(mvx - pmx) + h264::se_bits(mvy - pmy));
+      int cost = s + lambda * (mvbits(mvx - pmx) + mvbits(mvy - pmy));
       int key = ci < ncand_h ? ((cost << 4) | c) : 0x7FFFFFFF;
       bkey = key < bkey ? key : bkey;
     }
@@ -270,7 +421,7 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
         ring(ci, 1, &ox, &oy);
         int s = satd_cand(hx + ox, hy + oy);
         int mvx = best_mvx + hx + ox, mvy = best_mvy + hy + oy;
-        int cost = s + lambda * (h264::se_bits(mvx - pmx) + h264::se_bits(mvy - pmy));
+        int cost = s + lambda * (mvbits(mvx - pmx) + mvbits(mvy - pmy));
         int key = (cost << 4) | ci;
         qkey = key < qkey ? key : qkey;
       }
@@ -284,32 +435,22 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
     best_mvx += hx;
     best_mvy += hy;
   }
-  const size_t o = static_cast<size_t>(slot) * g.nmb() + mb;
-  // ---- final luma prediction for the chosen vector
+  const size_t o = static_cast<size_t>(slot) * nmb + mb;
+  // ---- phase 4: final luma prediction for the chosen vector (lane = row lane>>2, 4 columns)
   {
     int dqx = best_mvx - 4 * bx, dqy = best_mvy - 4 * by;
-    int xf = dqx & 3, yf = dqy & 3, ox = dqx >> 2, oy = dqy >> 2;
-    uint32_t word = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      int i = lane * 4 + k;
-      int px = i & 15, py = i >> 4;
-      word |= static_cast<uint32_t>(qpel(px + ox + 2, py + oy + 2, xf, yf)) << (8 * k);
-    }
-    reinterpret_cast<uint32_t*>(a.out_pred + o * 256)[lane] = word;
+    int q = (dqy & 3) * 4 + (dqx & 3), ox = dqx >> 2, oy = dqy >> 2;
+    int offa = S.qoff[2 * q], offb = S.qoff[2 * q + 1];
+    reinterpret_cast<uint32_t*>(a.out_pred + o * 256)[lane] = pred4(c4 + ox + 2, r4 + oy + 2, offa, offb);
   }
-  // ---- open-loop Intra16x16 estimate on source pixels: lane = mode * 16 + block
+  // ---- phase 5: open-loop Intra16x16 estimate on source pixels: lane = mode * 16 + block
   {
     int mode = lane >> 4, blk = lane & 15;
     bool has_top = my > 0, has_left = mx > 0;
     bool ok = (mode == 0 && has_top) || (mode == 1 && has_left) || mode == 2 || (mode == 3 && has_top && has_left);
-    int top[16], left[16], tl = 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      top[i] = has_top ? src[static_cast<size_t>(Y0 - 1) * W + X0 + i] : 0;
-      left[i] = has_left ? src[static_cast<size_t>(Y0 + i) * W + X0 - 1] : 0;
-    }
-    if (has_top && has_left) tl = src[static_cast<size_t>(Y0 - 1) * W + X0 - 1];
+    const int* top = S.nb;
+    const int* left = S.nb + 16;
+    int tl = S.nb[32];
     int pa = 0, pb = 0, pc = 0, dc = 0;
     if (mode == 3 && ok) h264::i16_plane_params(top, left, tl, &pa, &pb, &pc);
     if (mode == 2) dc = h264::i16_dc(top, left, (has_top ? h264::AV_TOP : 0) | (has_left ? h264::AV_LEFT : 0));
@@ -324,7 +465,7 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
         else if (mode == 1) pv = left[Y];
         else if (mode == 2) pv = dc;
         else pv = h264::clip1((pa + pb * (X - 7) + pc * (Y - 7) + 16) >> 5);
-        r[y * 4 + x] = static_cast<int>(s_src[Y * 16 + X]) - pv;
+        r[y * 4 + x] = static_cast<int>(srcb[Y * 16 + X]) - pv;
       }
     int s = h264::satd4x4(r);
 #pragma unroll
@@ -359,7 +500,7 @@ extern "C" void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, co
   a.out_pred = out_pred;
   a.out_intra_cost = out_intra_cost;
   a.qp = qp;
-  a.range = range;
+  a.range = range < kMaxR ? range : kMaxR;
   a.subpel = subpel;
   hipLaunchKernelGGL(me_p16x16, dim3(wmb * hmb, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
 }
