@@ -131,16 +131,8 @@ __device__ __forceinline__ int i4_tap_lds(uint32_t t, const int* e) {
           static_cast<int>((t >> 18) & 7) * e[(t >> 8) & 15] + 2) >> 2;
 }
 
-__device__ __forceinline__ int wave_min(int v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
-  return v;
-}
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
+__device__ __forceinline__ int wave_min(int v) { return min64(v); }
+__device__ __forceinline__ int wave_sum(int v) { return sum64(v); }
 
 // Lane layout used throughout: a 4x4 block is held by 4 consecutive lanes, one row each
 // (see grp_* in kcommon.h), so a wave processes 16 blocks (a whole 16x16 MB) at once.
@@ -267,9 +259,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
         v[x] = static_cast<int>(S.srcc[ccomp][(cby + gy) * 8 + cbx + x]) - pv;
       }
       int sblk = grp_satd4x4(v, gy);
-      int t = gy == 0 ? sblk : 0;
-#pragma unroll
-      for (int off = 16; off >= 1; off >>= 1) t += __shfl_xor(t, off, 64);  // sum within the half-wave
+      int t = sum32(gy == 0 ? sblk : 0);  // sum within the half-wave
       int key = ok ? (t << 2) | m : 0x7FFFFFFF;
       ckey = min(ckey, key);
     }
@@ -407,8 +397,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
     uint8_t* row = S.tile + (by4 + gy + 1) * TS + bx4 + 1;
 #pragma unroll
     for (int x = 0; x < 4; ++x) row[x] = static_cast<uint8_t>(h264::clip1(pr[x] + v[x]));
-    any |= __shfl_xor(static_cast<int>(any), 1, 64) != 0;
-    any |= __shfl_xor(static_cast<int>(any), 2, 64) != 0;
+    any = sum4(static_cast<int>(any)) != 0;
     if (gy == 0) a.nz[o * 16 + h264::kBlkX[blk] + 4 * h264::kBlkY[blk]] = any;
     wave_sync();
     for (int i = lane; i < 256; i += 64) coef[h264::COEF_LUMA + i] = S.c16[i >> 4][i & 15];

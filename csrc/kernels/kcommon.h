@@ -81,10 +81,63 @@ __device__ __forceinline__ void row_publish(int* prog, int row, int value) {
   if (lane_id() == 0) __hip_atomic_store(prog + row, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// ---------------------------------------------------------------- cross-lane primitives
+// HIP's __shfl* lower to ds_bpermute_b32, which goes through the LDS crossbar (~50+
+// cycles of latency per hop).  The wavefront kernels are chains of small cross-lane
+// steps (4x4 transforms, SATD, mode minima), so every hop here is a DPP modifier on a
+// VALU op (quad_perm / row mirrors, a few cycles) or a gfx950 v_permlane{16,32}_swap.
+constexpr int kDppQuadXor1 = 0xB1;      // quad_perm [1,0,3,2]
+constexpr int kDppQuadXor2 = 0x4E;      // quad_perm [2,3,0,1]
+constexpr int kDppRowMirror = 0x140;    // lane i <- 15 - i within a row of 16
+constexpr int kDppRowHalfMirror = 0x141;// lane i <- 7 - i within each half row
+
+template <int CTRL>
+__device__ __forceinline__ int dpp(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+// value of lane (lane & ~3) + K, for every lane of the quad
+template <int K>
+__device__ __forceinline__ int quad_bcast(int v) {
+  return dpp<K * 0x55>(v);
+}
+// reductions: results are valid on every lane of the reduced group
+__device__ __forceinline__ int sum4(int v) {
+  v += dpp<kDppQuadXor1>(v);
+  return v + dpp<kDppQuadXor2>(v);
+}
+__device__ __forceinline__ int sum16(int v) {
+  v = sum4(v);
+  v += dpp<kDppRowHalfMirror>(v);
+  return v + dpp<kDppRowMirror>(v);
+}
+__device__ __forceinline__ int sum32(int v) {  // within each half wave
+  v = sum16(v);
+  auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  return static_cast<int>(p[0]) + static_cast<int>(p[1]);
+}
+__device__ __forceinline__ int sum64(int v) {
+  v = sum32(v);
+  auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return static_cast<int>(p[0]) + static_cast<int>(p[1]);
+}
+__device__ __forceinline__ int min16(int v) {
+  v = min(v, dpp<kDppQuadXor1>(v));
+  v = min(v, dpp<kDppQuadXor2>(v));
+  v = min(v, dpp<kDppRowHalfMirror>(v));
+  return min(v, dpp<kDppRowMirror>(v));
+}
+__device__ __forceinline__ int min64(int v) {
+  v = min16(v);
+  auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  v = min(static_cast<int>(p[0]), static_cast<int>(p[1]));
+  auto q = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return min(static_cast<int>(q[0]), static_cast<int>(q[1]));
+}
+
 // ---------------------------------------------------------------- lane-parallel 4x4 transforms
 // A 4x4 block lives in a group of 4 consecutive lanes (base = lane & ~3); lane base+y
 // holds row y in v[0..3].  Row passes are in-register, column passes exchange the
-// group's rows with ds_bpermute (__shfl).  Every lane of the wave must execute these
+// group's rows with DPP quad broadcasts.  Every lane of the wave must execute these
 // (uniform control flow) because shuffles read other lanes' registers.
 __device__ __forceinline__ int sel4(int y, int a, int b, int c, int d) { return y == 0 ? a : (y == 1 ? b : (y == 2 ? c : d)); }
 
@@ -94,8 +147,8 @@ __device__ __forceinline__ void grp_fwd4x4(int* v, int base, int y) {
   int t[4] = {s03 + s12, 2 * d03 + d12, s03 - s12, d03 - 2 * d12};
 #pragma unroll
   for (int x = 0; x < 4; ++x) {
-    int c0 = __shfl(t[x], base + 0, 64), c1 = __shfl(t[x], base + 1, 64);
-    int c2 = __shfl(t[x], base + 2, 64), c3 = __shfl(t[x], base + 3, 64);
+    int c0 = quad_bcast<0>(t[x]), c1 = quad_bcast<1>(t[x]);
+    int c2 = quad_bcast<2>(t[x]), c3 = quad_bcast<3>(t[x]);
     int a = c0 + c3, b = c0 - c3, c = c1 + c2, d = c1 - c2;
     v[x] = sel4(y, a + c, 2 * b + d, a - c, b - 2 * d);
   }
@@ -107,8 +160,8 @@ __device__ __forceinline__ void grp_inv4x4(int* v, int base, int y) {
   int f[4] = {e0 + e3, e1 + e2, e1 - e2, e0 - e3};
 #pragma unroll
   for (int x = 0; x < 4; ++x) {
-    int c0 = __shfl(f[x], base + 0, 64), c1 = __shfl(f[x], base + 1, 64);
-    int c2 = __shfl(f[x], base + 2, 64), c3 = __shfl(f[x], base + 3, 64);
+    int c0 = quad_bcast<0>(f[x]), c1 = quad_bcast<1>(f[x]);
+    int c2 = quad_bcast<2>(f[x]), c3 = quad_bcast<3>(f[x]);
     int g0 = c0 + c2, g1 = c0 - c2, g2 = (c1 >> 1) - c3, g3 = c1 + (c3 >> 1);
     v[x] = (sel4(y, g0 + g3, g1 + g2, g1 - g2, g0 - g3) + 32) >> 6;
   }
@@ -121,15 +174,13 @@ __device__ __forceinline__ int grp_satd4x4(const int* v, int y) {
   int s = 0;
 #pragma unroll
   for (int x = 0; x < 4; ++x) {
-    int p = __shfl_xor(h[x], 1, 64);
+    int p = dpp<kDppQuadXor1>(h[x]);
     int u = (y & 1) ? p - h[x] : h[x] + p;
-    int q = __shfl_xor(u, 2, 64);
+    int q = dpp<kDppQuadXor2>(u);
     int w = (y & 2) ? q - u : u + q;
     s += w < 0 ? -w : w;
   }
-  s += __shfl_xor(s, 1, 64);
-  s += __shfl_xor(s, 2, 64);
-  return s >> 1;
+  return sum4(s) >> 1;
 }
 
 __device__ __forceinline__ int pos_class(int x, int y) {

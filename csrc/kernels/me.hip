@@ -67,20 +67,8 @@ __device__ __forceinline__ uint32_t avg4(uint32_t a, uint32_t b) {
   return (a | b) - (((a ^ b) >> 1) & 0x7F7F7F7Fu);
 }
 
-__device__ __forceinline__ int wave_min_key(int key) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    int o = __shfl_xor(key, off, 64);
-    key = o < key ? o : key;
-  }
-  return key;
-}
-
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
+__device__ __forceinline__ int wave_min_key(int key) { return min64(key); }
+__device__ __forceinline__ int wave_sum(int v) { return sum64(v); }
 
 struct MeShared {
   uint32_t win[kWinRowsMax * kWinPitch];  // reference window, aligned words
@@ -383,10 +371,7 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
       for (int x = 0; x < 4; ++x)
         r[y * 4 + x] = static_cast<int>((srow[y] >> (8 * x)) & 255u) - static_cast<int>((pw >> (8 * x)) & 255u);
     }
-    int s = h264::satd4x4(r);
-#pragma unroll
-    for (int off = 8; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
-    return s;
+    return sum16(h264::satd4x4(r));
   };
   // candidate c of a 3x3 ring (0 = centre, 1..8 = the 8 neighbours) -> offsets in units of `step`
   auto ring = [](int c, int step, int* dx, int* dy) {
@@ -467,12 +452,8 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
         else pv = h264::clip1((pa + pb * (X - 7) + pc * (Y - 7) + 16) >> 5);
         r[y * 4 + x] = static_cast<int>(srcb[Y * 16 + X]) - pv;
       }
-    int s = h264::satd4x4(r);
-#pragma unroll
-    for (int off = 8; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
-    int key = ok ? s : 0x3FFFFFFF;
-    key = min(key, __shfl_xor(key, 16, 64));
-    key = min(key, __shfl_xor(key, 32, 64));
+    int s = sum16(h264::satd4x4(r));
+    int key = min64(ok ? s : 0x3FFFFFFF);
     if (lane == 0) {
       a.out_mv[o * 2] = static_cast<int16_t>(best_mvx);
       a.out_mv[o * 2 + 1] = static_cast<int16_t>(best_mvy);
