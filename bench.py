@@ -117,6 +117,7 @@ def main() -> None:
             "quality": {"psnr_y_db": round(psnr, 3), "ssim_y": round(ssim, 4), "bitrate_kbps": round(kbps, 1),
                         "merged_bytes": len(merged) if merged is not None else 0},
             "timings_rank0_s": {k: round(v, 3) for k, v in enc.timings.items()},
+            "encoder_stats_rank0": {k: round(v, 4) for k, v in enc.stats.items()},
         }
         line = json.dumps(out)
         print(line, flush=True)

@@ -18,6 +18,14 @@ using h264::MbHeader;
 
 constexpr int kIntraWaves = 8;
 
+#ifdef MIVC_INTRA_PROFILE
+__device__ unsigned long long g_intra_prof[16][16];  // [mb][phase] for slot 0, wave 0
+__device__ int g_intra_prof_n;
+#define PROF(ph) do { if (slot == 0 && wave_id() == 0 && lane == 0 && prof_mb < 16) g_intra_prof[prof_mb][ph] = clock64(); } while (0)
+#else
+#define PROF(ph) do {} while (0)
+#endif
+
 struct IntraArgs {
   Geom g;
   const uint8_t *src_y, *src_u, *src_v;
@@ -46,6 +54,7 @@ struct IntraShared {
   int dc16[16];            // forward DC coefficients (raster)
   uint8_t top16[16], left16[16];
   int e4[16];              // Intra4x4 neighbour vector of the current block
+  uint32_t p4[40];         // Intra4x4 ranking: predicted row (4 packed samples) per (mode, row)
   int cdcp[2][4];          // chroma DC predictions per (comp, block)
   uint8_t modes4[16];
   int cost4;
@@ -136,9 +145,17 @@ __device__ __forceinline__ int wave_sum(int v) { return sum64(v); }
 
 // Lane layout used throughout: a 4x4 block is held by 4 consecutive lanes, one row each
 // (see grp_* in kcommon.h), so a wave processes 16 blocks (a whole 16x16 MB) at once.
-__device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared& S, int slot, int mx, int my) {
+// tapw[x]: this lane's Intra4x4 tap word for (mode = lane >> 2, row = lane & 3, column x),
+// loaded once per kernel (a lane-varying index into __constant__ would be a vector
+// memory load on every block)
+__device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared& S, int slot, int mx, int my,
+                                                const uint32_t (&tapw)[4]) {
   const Geom& g = a.g;
   const int lane = lane_id();
+#ifdef MIVC_INTRA_PROFILE
+  const int prof_mb = my == 0 ? mx : 99;
+#endif
+  PROF(0);
   const int gb = lane & ~3, gy = lane & 3;
   const int W = g.W, cw = g.cw();
   const int X0 = mx * 16, Y0 = my * 16;
@@ -216,6 +233,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
     S.cdcp[c][b] = h264::chroma_dc(S.ctop[c] + 1, S.cleft[c], mbav, b & 1, b >> 1);
   }
   wave_sync();
+  PROF(1);
 
   // ---- Intra16x16 decision: one mode per pass, lane = raster block * 4 + row
   const int tl16 = S.tile[0];
@@ -240,6 +258,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
       }
     }
   }
+  PROF(2);
   // ---- chroma decision: 2 passes; lanes 0-31 mode 2p, lanes 32-63 mode 2p+1; (lane&31) = cblk*4 + row
   const int cl = lane & 31, cblk = cl >> 2, ccomp = cblk >> 2, cb = cblk & 3;
   const int cbx = (cb & 1) * 4, cby = (cb >> 1) * 4;
@@ -267,6 +286,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
     cmode = ckey & 3;
   }
 
+  PROF(3);
   // ---- Intra4x4 trial (closed loop over the 16 blocks; 9 modes ranked in parallel)
   bool use4 = false;
   if (a.use_i4x4) {
@@ -297,11 +317,14 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
       bool valid = m < 9 && h264::i4_mode_ok(m, av);
       int mm = m < 9 ? m : 0;
       int v[4];
+      uint32_t pw = 0;
 #pragma unroll
       for (int x = 0; x < 4; ++x) {
-        int pv = mm == 2 ? dcv : i4_tap_lds(h264::kI4Taps[mm][gy * 4 + x], S.e4);
+        int pv = mm == 2 ? dcv : i4_tap_lds(tapw[x], S.e4);
+        pw |= static_cast<uint32_t>(pv) << (8 * x);
         v[x] = static_cast<int>(S.src[(by * 4 + gy) * 16 + bx * 4 + x]) - pv;
       }
+      if (lane < 36) S.p4[lane] = pw;
       int sblk = grp_satd4x4(v, gy);
       int key = (valid && gy == 0) ? ((sblk + lambda * (m == pm ? 1 : 4)) << 4) | m : 0x7FFFFFFF;
       key = wave_min(key);
@@ -309,9 +332,11 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
       total += key >> 4;
       // transform / quantise / reconstruct the chosen mode (every group computes the same block)
       int pr[4];
+      wave_sync();
+      const uint32_t prw = S.p4[mode * 4 + gy];
 #pragma unroll
       for (int x = 0; x < 4; ++x) {
-        pr[x] = mode == 2 ? dcv : i4_tap_lds(h264::kI4Taps[mode][gy * 4 + x], S.e4);
+        pr[x] = static_cast<int>((prw >> (8 * x)) & 255u);
         v[x] = static_cast<int>(S.src[(by * 4 + gy) * 16 + bx * 4 + x]) - pr[x];
       }
       grp_fwd4x4(v, gb, gy);
@@ -321,7 +346,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
         int mf = cls == 0 ? mf0 : (cls == 1 ? mf1 : mf2);
         int dq = cls == 0 ? dv0 : (cls == 1 ? dv1 : dv2);
         int lv = h264::quant_coef(v[x], mf, qbits, 21);
-        if (lane < 4) S.c4[blk][h264::kZigzagInv4x4[gy * 4 + x]] = static_cast<int16_t>(lv);
+        if (lane < 4) S.c4[blk][zzinv(x, gy)] = static_cast<int16_t>(lv);
         v[x] = (lv * dq) << qs;
       }
       grp_inv4x4(v, gb, gy);
@@ -336,6 +361,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
     use4 = total < cost16;
   }
 
+  PROF(4);
   MbHeader* h = a.hdr + o;
   int16_t* coef = a.coef + o * h264::kCoefPerMb;
   if (use4) {
@@ -370,7 +396,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
     for (int x = 0; x < 4; ++x) {
       int cls = pos_class(x, gy);
       int lv = (gy == 0 && x == 0) ? 0 : h264::quant_coef(v[x], h264::kQuantMF[qm][cls], qbits, 21);
-      S.c16[blk][h264::kZigzagInv4x4[gy * 4 + x]] = static_cast<int16_t>(lv);
+      S.c16[blk][zzinv(x, gy)] = static_cast<int16_t>(lv);
       any |= lv != 0;
       v[x] = (lv * h264::kDequantV[qm][cls]) << qs;
     }
@@ -403,6 +429,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
     for (int i = lane; i < 256; i += 64) coef[h264::COEF_LUMA + i] = S.c16[i >> 4][i & 15];
   }
   wave_sync();
+  PROF(5);
   {  // ---- write luma reconstruction
     int y = lane >> 2, x4 = (lane & 3) * 4;
     uint32_t word = 0;
@@ -425,7 +452,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
     for (int x = 0; x < 4; ++x) {
       int cls = pos_class(x, gy);
       int lv = (gy == 0 && x == 0) ? 0 : h264::quant_coef(v[x], h264::kQuantMF[qm][cls], qbits_c, 21);
-      if (lane < 32) coef[h264::COEF_CHROMA_AC + (ccomp * 4 + cb) * 16 + h264::kZigzagInv4x4[gy * 4 + x]] = static_cast<int16_t>(lv);
+      if (lane < 32) coef[h264::COEF_CHROMA_AC + (ccomp * 4 + cb) * 16 + zzinv(x, gy)] = static_cast<int16_t>(lv);
       v[x] = (lv * h264::kDequantV[qm][cls]) << qs;
     }
     wave_sync();
@@ -459,6 +486,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
       if (cb & 1) S.saved_c[ccomp][(cb >> 1) * 4 + gy] = static_cast<uint8_t>(word >> 24);
     }
   }
+  PROF(6);
   // ---- keep this MB's right edge in LDS for the next iteration of this wave
   if (lane < 16) S.saved_y[lane] = S.tile[(lane + 1) * TS + 16];
   if (lane >= 16 && lane < 20) {
@@ -477,6 +505,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
   }
   if (!use4 && lane >= 32 && lane < 48) h->i4_modes[lane - 32] = 2;
   wave_sync();
+  PROF(7);
 }
 
 __global__ __launch_bounds__(64 * kIntraWaves) void encode_intra_wavefront(IntraArgs a) {
@@ -491,12 +520,21 @@ __global__ __launch_bounds__(64 * kIntraWaves) void encode_intra_wavefront(Intra
   __syncthreads();
   IntraShared& S = SS[w];
   const int lane = lane_id();
+  uint32_t tapw[4];
+  {
+    const int m = lane >> 2 < 9 ? lane >> 2 : 0, r = lane & 3;
+#pragma unroll
+    for (int x = 0; x < 4; ++x) tapw[x] = h264::kI4Taps[m][r * 4 + x];
+  }
   for (int y = w; y < g.hmb; y += kIntraWaves) {
     if (!a.intra_flag) {  // I frame: every MB
       for (int x = 0; x < g.wmb; ++x) {
         if (y > 0) row_wait(prog, y - 1, min(x + 2, g.wmb), a.err);
-        encode_intra_mb(a, S, slot, x, y);
+        encode_intra_mb(a, S, slot, x, y, tapw);
         row_publish(prog, y, x + 1);
+#ifdef MIVC_INTRA_PROFILE
+        if (slot == 0 && w == 0 && lane == 0 && y == 0 && x < 16) g_intra_prof[x][8] = clock64();
+#endif
       }
       continue;
     }
@@ -510,7 +548,7 @@ __global__ __launch_bounds__(64 * kIntraWaves) void encode_intra_wavefront(Intra
         mask &= mask - 1;
         if (x > 0) row_publish(prog, y, x);  // MBs before x in this row are final (inter)
         if (y > 0) row_wait(prog, y - 1, min(x + 2, g.wmb), a.err);
-        encode_intra_mb(a, S, slot, x, y);
+        encode_intra_mb(a, S, slot, x, y, tapw);
         row_publish(prog, y, x + 1);
       }
     }
@@ -547,3 +585,9 @@ extern "C" void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t*
   a.use_i4x4 = use_i4x4;
   hipLaunchKernelGGL(encode_intra_wavefront, dim3(B), dim3(64 * kIntraWaves), 0, static_cast<hipStream_t>(stream), a);
 }
+
+#ifdef MIVC_INTRA_PROFILE
+extern "C" void mivc_intra_prof_read(unsigned long long* out) {
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(g_intra_prof), sizeof(unsigned long long) * 256);
+}
+#endif

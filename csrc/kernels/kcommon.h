@@ -183,6 +183,16 @@ __device__ __forceinline__ int grp_satd4x4(const int* v, int y) {
   return sum4(s) >> 1;
 }
 
+// inverse 4x4 zigzag (raster (x, y) -> scan index) without a memory table: one packed
+// word per column, so a lane-varying y never turns into a vector load from __constant__
+__device__ __forceinline__ int zzinv(int x, int y) {
+  const uint32_t w = x == 0 ? (0u | 2u << 8 | 3u << 16 | 9u << 24)
+                   : x == 1 ? (1u | 4u << 8 | 8u << 16 | 10u << 24)
+                   : x == 2 ? (5u | 7u << 8 | 11u << 16 | 14u << 24)
+                            : (6u | 12u << 8 | 13u << 16 | 15u << 24);
+  return static_cast<int>((w >> (8 * y)) & 255u);
+}
+
 __device__ __forceinline__ int pos_class(int x, int y) {
   return ((x | y) & 1) == 0 ? 0 : (((x & y) & 1) ? 1 : 2);
 }

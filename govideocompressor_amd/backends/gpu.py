@@ -38,19 +38,16 @@ class GpuBackend:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.entropy = entropy
         self.max_slots = max_slots
-        self._enc = {}
+        from ..models.h264_gpu import GpuH264Encoder
+        from ..runtime import EncoderPool, StageStreams
+        self._pool = EncoderPool(lambda p, b: GpuH264Encoder(p, slots=b, device=self.device, entropy=self.entropy),
+                                 max_resident=1)
+        self._streams = StageStreams(self.device)
         self._io = cf.ThreadPoolExecutor(max_workers=8)
 
     def _encoder(self, params, slots: int):
-        from ..models.h264_gpu import GpuH264Encoder
-        key = (params.width, params.height, params.crf, params.qp, slots)
-        enc = self._enc.get(key)
-        if enc is None:
-            for k in list(self._enc):         # keep one encoder resident; HBM is reused
-                self._enc.pop(k).close()
-            enc = GpuH264Encoder(params, slots=slots, device=self.device, entropy=self.entropy)
-            self._enc[key] = enc
-        return enc
+        key = (params.width, params.height, params.fps, params.crf, params.qp, slots)
+        return self._pool.get(key, params, slots)
 
     def encode_clips(self, items: list[tuple[str, "yuv.Clip"]], cfg: EncoderConfig,
                      tm: Timer | None = None) -> dict[str, tuple[bytes, dict]]:
@@ -131,9 +128,8 @@ class GpuBackend:
             yn[b, :c], un[b, :c], vn[b, :c] = cl.y[s:s + c], cl.u[s:s + c], cl.v[s:s + c]
             if c < F:
                 yn[b, c:], un[b, c:], vn[b, c:] = cl.y[s + c - 1], cl.u[s + c - 1], cl.v[s + c - 1]
-        dy = y.to(self.device, non_blocking=True)
-        du = u.to(self.device, non_blocking=True)
-        dv = v.to(self.device, non_blocking=True)
+        (dy, du, dv), ev = self._streams.upload([y, u, v], self.device)
+        self._streams.wait(ev)
         tm.add("upload_s", time.perf_counter() - t0)
         t1 = time.perf_counter()
         enc = self._encoder(params, B)
@@ -144,7 +140,5 @@ class GpuBackend:
                 for b, (key, un_, s, c) in enumerate(chunk)]
 
     def close(self):
-        for e in self._enc.values():
-            e.close()
-        self._enc.clear()
+        self._pool.close()
         self._io.shutdown(wait=False)

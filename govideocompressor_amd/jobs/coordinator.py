@@ -27,6 +27,7 @@ import time
 from collections import deque
 from dataclasses import asdict, dataclass, field
 
+from ..obs import get_logger
 from ..segment import merge as M
 from ..segment.split import piece_files
 from . import protocol as proto
@@ -129,6 +130,7 @@ class Coordinator:
         self.done_event: asyncio.Event | None = None
         self.t_start = time.time()
         self.http = None
+        self.jlog = get_logger("coordinator")
 
     # ------------------------------------------------------------------ state file
     def _load_state(self) -> dict:
@@ -168,6 +170,7 @@ class Coordinator:
 
     def _requeue(self, idx: str, reason: str):
         p = self.pieces[idx]
+        self.jlog.event("requeue", piece=idx, reason=reason, attempts=p.attempts)
         p.worker, p.reason = "", reason
         if p.attempts > self.max_retries:
             p.state = "failed"
@@ -198,6 +201,7 @@ class Coordinator:
             p.leased_at = p.last_beat = time.monotonic()
             c.lease = idx
             self.log(f"[{now_str()}]OnConnect send success[{self.token};{idx}]")
+            self.jlog.event("dispatch", piece=idx, worker=p.worker, attempt=p.attempts)
 
     def _on_reply(self, c: _Conn, r: proto.Reply):
         idx = r.idx
@@ -218,6 +222,8 @@ class Coordinator:
                 except (OSError, ValueError):
                     p.stats = {}
             self.log(f"###[{now_str()}] [{idx}]piece convert success")
+            self.jlog.event("success", piece=idx, worker=c.worker or c.peer,
+                            lease_s=round(time.monotonic() - p.leased_at, 3), stats=p.stats)
             if self.delete_source:
                 files = piece_files(self.dir)
                 if idx in files:

@@ -32,6 +32,7 @@ import threading
 import time
 from dataclasses import dataclass, field
 
+from ..obs import get_logger
 from . import protocol as proto
 from .coordinator import out_dir_name
 from .transport import TransportError
@@ -221,7 +222,11 @@ class Worker:
                 jobs.append(PieceJob(j.idx, local, os.path.join(odir, f"{j.idx}.{self.out_ext}"),
                                      os.path.join(odir, f"c{j.idx}.{self.out_ext}.log")))
                 ready.append(ls)
+            t0 = time.perf_counter()
             results = self.backend.run(jobs, args) if jobs else []
+            get_logger("worker").event("batch", worker=self.worker_id, pieces=[j.idx for j in jobs],
+                                       seconds=round(time.perf_counter() - t0, 4),
+                                       ok=[r.ok for r in results])
             for ls, pj, r in zip(ready, jobs, results):
                 j = ls.job
                 try:

@@ -41,6 +41,10 @@ class H264Params:
     me_range: int = 8              # integer full-search radius around the best predictor
     subpel: int = 2
     i4x4: bool = True
+    # Intra4x4 trial for the (rare) intra MBs of P frames.  Off by default: a P-frame
+    # intra MB is coded by the wavefront kernel, whose latency (x chain length) is
+    # dominated by the 16 serial I4x4 block trials; these MBs are ~0.1-1% of a P frame.
+    i4x4_in_p: bool = False
     deblock: bool = True
     chroma_qp_offset: int = 0
     vui: bool = True
@@ -118,6 +122,7 @@ class GpuH264Encoder:
         self.intra_count = torch.zeros((B,), dtype=i32, device=dev)
         self.qp = torch.zeros((B,), dtype=i32, device=dev)
         self.err = torch.zeros((1,), dtype=i32, device=dev)
+        self.p_intra_mbs = torch.zeros((), dtype=torch.int64, device=dev)  # intra MBs coded in P frames
         # pinned staging for the entropy stage (double-buffered)
         if entropy == "cpu":
             self.h_hdr = [torch.empty((B, nmb, MB_HDR_BYTES), dtype=u8).pin_memory() for _ in range(2)]
@@ -150,6 +155,7 @@ class GpuH264Encoder:
         self.pool = cf.ThreadPoolExecutor(max_workers=nthreads)
         self.cfg = params.host_cfg()
         self.timings: dict[str, float] = {}
+        self.stats: dict[str, float] = {}
 
     # ------------------------------------------------------------------ helpers
     @staticmethod
@@ -187,13 +193,14 @@ class GpuH264Encoder:
                                   self._ptr(self.qp), self.p.chroma_qp_offset, self._ptr(hdr), self._ptr(coef),
                                   self._ptr(self.nz), self._ptr(self.intra_flag), self._ptr(self.intra_count), s)
             self.prev_mv.copy_(self.mv)
+            self.p_intra_mbs += self.intra_count.sum()
             flag_ptr, count_ptr = self._ptr(self.intra_flag), self._ptr(self.intra_count)
         else:
             self.prev_mv.zero_()
             flag_ptr, count_ptr = 0, 0
         self.hip.encode_intra(B, wmb, hmb, sy, su, sv, ry, ru, rv, self._ptr(self.qp), self.p.chroma_qp_offset,
                               self._ptr(hdr), self._ptr(coef), self._ptr(self.nz), flag_ptr, count_ptr,
-                              self._ptr(self.err), int(self.p.i4x4), s)
+                              self._ptr(self.err), int(self.p.i4x4 and (idr or self.p.i4x4_in_p)), s)
         if self.p.deblock:
             self.hip.deblock(B, wmb, hmb, ry, ru, rv, self._ptr(hdr), self._ptr(self.nz), self.p.chroma_qp_offset,
                              0, 0, self._ptr(self.err), s)
@@ -334,6 +341,9 @@ class GpuH264Encoder:
                 outs[t] = pending[k].result()
                 pending[k] = None
         torch.cuda.synchronize(self.dev)
+        if F > 1:
+            self.stats["p_intra_ratio"] = float(self.p_intra_mbs.item()) / (B * (F - 1) * self.nmb)
+        self.p_intra_mbs.zero_()
         if int(self.err.item()) != 0:
             raise RuntimeError("wavefront progress timeout in an encode kernel")
         ps = self.parameter_sets()

@@ -1,0 +1,47 @@
+"""Device discovery and selection: one process per GPU (LOCAL_RANK -> device)."""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+
+@dataclass
+class DeviceInfo:
+    index: int
+    name: str
+    arch: str
+    cus: int
+    hbm_bytes: int
+
+    def fits(self, nbytes: int, reserve: float = 0.1) -> bool:
+        return nbytes <= self.hbm_bytes * (1.0 - reserve)
+
+
+def local_device():
+    """The torch device this process owns: ``cuda:LOCAL_RANK`` (modulo visible GPUs) or cpu."""
+    import torch
+    if not torch.cuda.is_available():
+        return torch.device("cpu")
+    n = torch.cuda.device_count()
+    idx = int(os.environ.get("LOCAL_RANK", "0")) % max(1, n)
+    return torch.device("cuda", idx)
+
+
+def device_info(index: int = 0) -> DeviceInfo | None:
+    import torch
+    if not torch.cuda.is_available():
+        return None
+    p = torch.cuda.get_device_properties(index)
+    arch = getattr(p, "gcnArchName", "") or ""
+    return DeviceInfo(index, p.name, arch.split(":")[0], p.multi_processor_count, p.total_memory)
+
+
+def slots_for(width: int, height: int, frames: int, info: DeviceInfo | None, cap: int = 512) -> int:
+    """Segments to encode concurrently on one GPU: enough to put >= 1 frame wavefront on
+    every CU, bounded by HBM (input clip + encoder state per slot)."""
+    if info is None:
+        return 1
+    coded = ((width + 15) // 16 * 16) * ((height + 15) // 16 * 16)
+    per_slot = coded * 3 // 2 * (frames + 4) + coded // 256 * (48 + 816 + 400)
+    by_mem = max(1, int(info.hbm_bytes * 0.6) // max(1, per_slot))
+    return max(1, min(cap, by_mem, max(info.cus, 1)))
