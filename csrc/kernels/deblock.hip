@@ -30,14 +30,16 @@ struct DeblockArgs {
 constexpr int kDeblockWaves = 16;
 
 constexpr int LT = 20;  // luma tile stride: 4 halo + 16
-constexpr int CT = 10;  // chroma tile stride: 2 halo + 8
+constexpr int CT = 12;  // chroma tile stride: 4 halo (2 used) + 8 -- rows stay 4-byte aligned
 
 struct DeblockShared {
-  uint8_t ty[LT * LT];
-  uint8_t tc[2][CT * CT];
-  int bs[2][4][4];         // [dir][edge][segment]
-  uint8_t left_y[16][4];   // previous MB's columns 12..15 after filtering
-  uint8_t left_c[2][8][2]; // previous MB's chroma columns 6..7
+  alignas(16) uint8_t ty[LT * LT];
+  alignas(16) uint8_t tc[2][CT * 10];
+  alignas(16) uint32_t hdrw[3][12];  // MbHeader of the current, left and top MB
+  uint8_t nzb[3][16];                // their non-zero flags
+  int bs[2][4][4];                   // [dir][edge][segment]
+  uint32_t left_y[16];               // previous MB's columns 12..15 after filtering (one word per row)
+  uint32_t left_c[2][8];             // previous MB's chroma columns 4..7
   int saved_x;
 };
 
@@ -97,68 +99,96 @@ __device__ __forceinline__ void blk_mv(const MbHeader& h, int r, int* mv) {
   mv[1] = h.mv[q][1];
 }
 
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
 __device__ __forceinline__ void deblock_mb(const DeblockArgs& a, DeblockShared& S, int slot, int mx, int my) {
   const Geom& g = a.g;
   const int lane = lane_id();
   const int W = g.W, cw = g.cw();
   const size_t o = static_cast<size_t>(slot) * g.nmb() + my * g.wmb + mx;
   uint8_t* recy = a.rec_y + slot * g.ysize();
-  const int X0 = mx * 16, Y0 = my * 16;
+  uint8_t* recc[2] = {a.rec_u + slot * g.csize(), a.rec_v + slot * g.csize()};
+  const int X0 = mx * 16, Y0 = my * 16, XC = mx * 8, YC = my * 8;
   const bool has_left = mx > 0, has_top = my > 0;
+  const bool left_saved = S.saved_x == mx - 1;
 
-  // ---- load tiles
-  for (int i = lane; i < 16 * 16; i += 64) {
-    int r = i >> 4, c = i & 15;
-    S.ty[(r + 4) * LT + c + 4] = recy[static_cast<size_t>(Y0 + r) * W + X0 + c];
+  // ---- phase 1: every global read of this MB in one batch (dwords), then the LDS stores
+  const uint32_t* hdr32 = reinterpret_cast<const uint32_t*>(a.hdr);
+  uint32_t la, lb = 0, lc = 0, ld = 0;
+  {
+    const int r = lane >> 2, c4 = (lane & 3) * 4;
+    la = *reinterpret_cast<const uint32_t*>(recy + static_cast<size_t>(Y0 + r) * W + X0 + c4);
   }
-  if (has_top)
-    for (int i = lane; i < 4 * 16; i += 64) {
-      int r = i >> 4, c = i & 15;
-      S.ty[r * LT + c + 4] = recy[static_cast<size_t>(Y0 - 4 + r) * W + X0 + c];
-    }
-  if (has_left && lane < 16) {
-    for (int c = 0; c < 4; ++c) {
-      S.ty[(lane + 4) * LT + c] =
-          S.saved_x == mx - 1 ? S.left_y[lane][c] : recy[static_cast<size_t>(Y0 + lane) * W + X0 - 4 + c];
-    }
+  if (lane < 16) {
+    if (has_top) lb = *reinterpret_cast<const uint32_t*>(recy + static_cast<size_t>(Y0 - 4 + (lane >> 2)) * W + X0 + (lane & 3) * 4);
+  } else if (lane < 32) {
+    if (has_left && !left_saved) lb = *reinterpret_cast<const uint32_t*>(recy + static_cast<size_t>(Y0 + lane - 16) * W + X0 - 4);
+  } else {
+    const int comp = (lane - 32) >> 4, i = lane & 15;
+    lb = *reinterpret_cast<const uint32_t*>(recc[comp] + static_cast<size_t>(YC + (i >> 1)) * cw + XC + (i & 1) * 4);
   }
-  for (int comp = 0; comp < 2; ++comp) {
-    uint8_t* rc = (comp == 0 ? a.rec_u : a.rec_v) + slot * g.csize();
-    uint8_t* t = S.tc[comp];
-    {
-      int r = lane >> 3, c = lane & 7;
-      t[(r + 2) * CT + c + 2] = rc[static_cast<size_t>(my * 8 + r) * cw + mx * 8 + c];
-    }
-    if (has_top && lane < 16) {
-      int r = lane >> 3, c = lane & 7;
-      t[r * CT + c + 2] = rc[static_cast<size_t>(my * 8 - 2 + r) * cw + mx * 8 + c];
-    }
-    if (has_left && lane < 16) {
-      int r = lane >> 1, c = lane & 1;
-      t[(r + 2) * CT + c] =
-          S.saved_x == mx - 1 ? S.left_c[comp][r][c] : rc[static_cast<size_t>(my * 8 + r) * cw + mx * 8 - 2 + c];
-    }
+  if (lane < 8) {
+    const int comp = lane >> 2, r = (lane >> 1) & 1, h = lane & 1;
+    if (has_top) lc = *reinterpret_cast<const uint32_t*>(recc[comp] + static_cast<size_t>(YC - 2 + r) * cw + XC + h * 4);
+  } else if (lane < 24) {
+    const int comp = (lane - 8) >> 3, r = (lane - 8) & 7;
+    if (has_left && !left_saved) lc = *reinterpret_cast<const uint32_t*>(recc[comp] + static_cast<size_t>(YC + r) * cw + XC - 4);
+  } else if (lane < 60) {
+    const int which = (lane - 24) / 12, k = (lane - 24) % 12;
+    const bool ok = which == 0 || (which == 1 ? has_left : has_top);
+    const size_t mbo = which == 0 ? o : (which == 1 ? o - 1 : o - g.wmb);
+    if (ok) lc = hdr32[mbo * 12 + k];
   }
+  if (lane < 12) {
+    const int which = lane >> 2, k = lane & 3;
+    const bool ok = which == 0 || (which == 1 ? has_left : has_top);
+    const size_t mbo = which == 0 ? o : (which == 1 ? o - 1 : o - g.wmb);
+    if (ok) ld = reinterpret_cast<const uint32_t*>(a.nz)[mbo * 4 + k];
+  }
+  {
+    const int r = lane >> 2, c4 = (lane & 3) * 4;
+    *reinterpret_cast<uint32_t*>(&S.ty[(r + 4) * LT + 4 + c4]) = la;
+  }
+  if (lane < 16) {
+    if (has_top) *reinterpret_cast<uint32_t*>(&S.ty[(lane >> 2) * LT + 4 + (lane & 3) * 4]) = lb;
+  } else if (lane < 32) {
+    if (has_left) *reinterpret_cast<uint32_t*>(&S.ty[(lane - 16 + 4) * LT]) = left_saved ? S.left_y[lane - 16] : lb;
+  } else {
+    const int comp = (lane - 32) >> 4, i = lane & 15;
+    *reinterpret_cast<uint32_t*>(&S.tc[comp][((i >> 1) + 2) * CT + 4 + (i & 1) * 4]) = lb;
+  }
+  if (lane < 8) {
+    const int comp = lane >> 2, r = (lane >> 1) & 1, h = lane & 1;
+    if (has_top) *reinterpret_cast<uint32_t*>(&S.tc[comp][r * CT + 4 + h * 4]) = lc;
+  } else if (lane < 24) {
+    const int comp = (lane - 8) >> 3, r = (lane - 8) & 7;
+    if (has_left) *reinterpret_cast<uint32_t*>(&S.tc[comp][(r + 2) * CT]) = left_saved ? S.left_c[comp][r] : lc;
+  } else if (lane < 60) {
+    S.hdrw[(lane - 24) / 12][(lane - 24) % 12] = lc;
+  }
+  if (lane < 12) reinterpret_cast<uint32_t*>(S.nzb[lane >> 2])[lane & 3] = ld;
+  wave_sync();
+
   // ---- boundary strengths: lane = dir*16 + edge*4 + seg
+  const MbHeader* HQ = reinterpret_cast<const MbHeader*>(S.hdrw[0]);
   if (lane < 32) {
     int dir = lane >> 4, e = (lane >> 2) & 3, k = lane & 3;
-    const MbHeader& Q = a.hdr[o];
     int bs = 0;
     bool mbedge = e == 0;
     bool avail = !mbedge || (dir == 0 ? has_left : has_top);
     if (avail) {
-      size_t op = mbedge ? (dir == 0 ? o - 1 : o - g.wmb) : o;
-      const MbHeader& P = a.hdr[op];
+      const int pw = mbedge ? (dir == 0 ? 1 : 2) : 0;
+      const MbHeader* HP = reinterpret_cast<const MbHeader*>(S.hdrw[pw]);
       int rq = dir == 0 ? (e + 4 * k) : (k + 4 * e);
       int rp = dir == 0 ? (mbedge ? 3 + 4 * k : e - 1 + 4 * k) : (mbedge ? k + 12 : k + 4 * (e - 1));
-      bool iq = h264::mbk_is_intra(Q.kind), ip = h264::mbk_is_intra(P.kind);
+      bool iq = h264::mbk_is_intra(HQ->kind), ip = h264::mbk_is_intra(HP->kind);
       if (mbedge && (iq || ip)) bs = 4;
       else if (iq || ip) bs = 3;
-      else if (a.nz[op * 16 + rp] || a.nz[o * 16 + rq]) bs = 2;
+      else if (S.nzb[pw][rp] || S.nzb[0][rq]) bs = 2;
       else {
         int mp[2], mq[2];
-        blk_mv(P, rp, mp);
-        blk_mv(Q, rq, mq);
+        blk_mv(*HP, rp, mp);
+        blk_mv(*HQ, rq, mq);
         int dx = mp[0] - mq[0], dy = mp[1] - mq[1];
         bs = (dx >= 4 || dx <= -4 || dy >= 4 || dy <= -4) ? 1 : 0;
       }
@@ -167,73 +197,90 @@ __device__ __forceinline__ void deblock_mb(const DeblockArgs& a, DeblockShared& 
   }
   wave_sync();
 
-  const int qpq = a.hdr[o].qp;
+  // QPs are uniform: read them into SGPRs so the alpha/beta/tc0 lookups are scalar loads
+  const int qpq = uni(HQ->qp);
+  const int qpl = uni(reinterpret_cast<const MbHeader*>(S.hdrw[1])->qp);
+  const int qpt = uni(reinterpret_cast<const MbHeader*>(S.hdrw[2])->qp);
   // ---- vertical edges, then horizontal edges
   for (int dir = 0; dir < 2; ++dir) {
     for (int e = 0; e < 4; ++e) {
       if (e == 0 && !(dir == 0 ? has_left : has_top)) continue;
-      int qpp = e == 0 ? a.hdr[dir == 0 ? o - 1 : o - g.wmb].qp : qpq;
+      const int qpp = e == 0 ? (dir == 0 ? qpl : qpt) : qpq;
       if (lane < 16) {
         int bs = S.bs[dir][e][lane >> 2];
+        const int qpav = (qpp + qpq + 1) >> 1;
+        const int ia = clampi(qpav + a.alpha_off, 0, 51), ib = clampi(qpav + a.beta_off, 0, 51);
+        const int t1 = h264::kTc0[ia][0], t2 = h264::kTc0[ia][1], t3 = h264::kTc0[ia][2];
+        const int alpha = h264::kAlpha[ia], beta = h264::kBeta[ib];
         if (bs) {
-          int qpav = (qpp + qpq + 1) >> 1;
-          int ia = clampi(qpav + a.alpha_off, 0, 51), ib = clampi(qpav + a.beta_off, 0, 51);
-          int tc0 = bs < 4 ? h264::kTc0[ia][bs - 1] : 0;
+          int tc0 = bs == 1 ? t1 : (bs == 2 ? t2 : (bs == 3 ? t3 : 0));
           uint8_t* q0 = dir == 0 ? &S.ty[(lane + 4) * LT + 4 + 4 * e] : &S.ty[(4 + 4 * e) * LT + 4 + lane];
-          filter_line(q0, dir == 0 ? 1 : LT, bs, h264::kAlpha[ia], h264::kBeta[ib], tc0, false);
+          filter_line(q0, dir == 0 ? 1 : LT, bs, alpha, beta, tc0, false);
         }
       } else if (lane < 32 && (e == 0 || e == 2)) {
         int comp = (lane - 16) >> 3, i = (lane - 16) & 7;
         int bs = S.bs[dir][e][i >> 1];
+        const int cp = h264::chroma_qp(qpp, a.chroma_qp_offset), cq = h264::chroma_qp(qpq, a.chroma_qp_offset);
+        const int qpav = (cp + cq + 1) >> 1;
+        const int ia = clampi(qpav + a.alpha_off, 0, 51), ib = clampi(qpav + a.beta_off, 0, 51);
+        const int t1 = h264::kTc0[ia][0], t2 = h264::kTc0[ia][1], t3 = h264::kTc0[ia][2];
+        const int alpha = h264::kAlpha[ia], beta = h264::kBeta[ib];
         if (bs) {
-          int cp = h264::chroma_qp(qpp, a.chroma_qp_offset), cq = h264::chroma_qp(qpq, a.chroma_qp_offset);
-          int qpav = (cp + cq + 1) >> 1;
-          int ia = clampi(qpav + a.alpha_off, 0, 51), ib = clampi(qpav + a.beta_off, 0, 51);
-          int tc0 = bs < 4 ? h264::kTc0[ia][bs - 1] : 0;
+          int tc0 = bs == 1 ? t1 : (bs == 2 ? t2 : (bs == 3 ? t3 : 0));
           int ce = e >> 1;
           uint8_t* t = S.tc[comp];
-          uint8_t* q0 = dir == 0 ? &t[(i + 2) * CT + 2 + 4 * ce] : &t[(2 + 4 * ce) * CT + 2 + i];
-          filter_line(q0, dir == 0 ? 1 : CT, bs, h264::kAlpha[ia], h264::kBeta[ib], tc0, true);
+          uint8_t* q0 = dir == 0 ? &t[(i + 2) * CT + 4 + 4 * ce] : &t[(2 + 4 * ce) * CT + 4 + i];
+          filter_line(q0, dir == 0 ? 1 : CT, bs, alpha, beta, tc0, true);
         }
       }
       wave_sync();
     }
   }
-  // ---- write back: MB interior + modified halo (3 luma / 1 chroma lines)
-  for (int i = lane; i < 16 * 16; i += 64) {
-    int r = i >> 4, c = i & 15;
-    recy[static_cast<size_t>(Y0 + r) * W + X0 + c] = S.ty[(r + 4) * LT + c + 4];
+  // ---- write back (dwords): MB interior + the modified halo (3 luma / 1 chroma lines; the
+  // 4th luma / 2nd chroma column of the left halo is rewritten unchanged -- its MB is final)
+  {
+    const int r = lane >> 2, c4 = (lane & 3) * 4;
+    *reinterpret_cast<uint32_t*>(recy + static_cast<size_t>(Y0 + r) * W + X0 + c4) =
+        *reinterpret_cast<const uint32_t*>(&S.ty[(r + 4) * LT + 4 + c4]);
   }
-  if (has_top && lane < 48) {
-    int r = lane >> 4, c = lane & 15;  // rows -3..-1
-    recy[static_cast<size_t>(Y0 - 3 + r) * W + X0 + c] = S.ty[(r + 1) * LT + c + 4];
-  }
-  if (has_left && lane < 48) {
-    int r = lane / 3, c = lane % 3;  // cols -3..-1
-    recy[static_cast<size_t>(Y0 + r) * W + X0 - 3 + c] = S.ty[(r + 4) * LT + c + 1];
-  }
-  for (int comp = 0; comp < 2; ++comp) {
-    uint8_t* rc = (comp == 0 ? a.rec_u : a.rec_v) + slot * g.csize();
-    const uint8_t* t = S.tc[comp];
-    {
-      int r = lane >> 3, c = lane & 7;
-      rc[static_cast<size_t>(my * 8 + r) * cw + mx * 8 + c] = t[(r + 2) * CT + c + 2];
+  if (lane < 12) {
+    if (has_top) {
+      const int r = 1 + (lane >> 2), c4 = (lane & 3) * 4;  // rows -3..-1
+      *reinterpret_cast<uint32_t*>(recy + static_cast<size_t>(Y0 - 4 + r) * W + X0 + c4) =
+          *reinterpret_cast<const uint32_t*>(&S.ty[r * LT + 4 + c4]);
     }
-    if (has_top && lane < 8) rc[static_cast<size_t>(my * 8 - 1) * cw + mx * 8 + lane] = t[1 * CT + lane + 2];
-    if (has_left && lane >= 8 && lane < 16) {
-      int r = lane - 8;
-      rc[static_cast<size_t>(my * 8 + r) * cw + mx * 8 - 1] = t[(r + 2) * CT + 1];
+  } else if (lane < 28) {
+    if (has_left) {
+      const int r = lane - 12;
+      *reinterpret_cast<uint32_t*>(recy + static_cast<size_t>(Y0 + r) * W + X0 - 4) =
+          *reinterpret_cast<const uint32_t*>(&S.ty[(r + 4) * LT]);
+    }
+  } else if (lane < 60) {
+    const int comp = (lane - 28) >> 4, i = (lane - 28) & 15;
+    *reinterpret_cast<uint32_t*>(recc[comp] + static_cast<size_t>(YC + (i >> 1)) * cw + XC + (i & 1) * 4) =
+        *reinterpret_cast<const uint32_t*>(&S.tc[comp][((i >> 1) + 2) * CT + 4 + (i & 1) * 4]);
+  }
+  if (lane < 4) {
+    if (has_top) {
+      const int comp = lane >> 1, h = lane & 1;  // chroma row -1
+      *reinterpret_cast<uint32_t*>(recc[comp] + static_cast<size_t>(YC - 1) * cw + XC + h * 4) =
+          *reinterpret_cast<const uint32_t*>(&S.tc[comp][1 * CT + 4 + h * 4]);
+    }
+  } else if (lane < 20) {
+    if (has_left) {
+      const int comp = (lane - 4) >> 3, r = (lane - 4) & 7;  // chroma column -1 (word -4..-1)
+      *reinterpret_cast<uint32_t*>(recc[comp] + static_cast<size_t>(YC + r) * cw + XC - 4) =
+          *reinterpret_cast<const uint32_t*>(&S.tc[comp][(r + 2) * CT]);
     }
   }
-  wave_sync();
   // ---- keep this MB's right edge for the next iteration (final values)
-  if (lane < 16)
-    for (int c = 0; c < 4; ++c) S.left_y[lane][c] = S.ty[(lane + 4) * LT + 16 + c];
-  if (lane >= 16 && lane < 48) {
-    int comp = (lane - 16) >> 4, r = ((lane - 16) >> 1) & 7, c = lane & 1;
-    S.left_c[comp][r][c] = S.tc[comp][(r + 2) * CT + 8 + c];
+  if (lane < 16) S.left_y[lane] = *reinterpret_cast<const uint32_t*>(&S.ty[(lane + 4) * LT + 16]);
+  else if (lane < 32) {
+    const int comp = (lane - 16) >> 3, r = (lane - 16) & 7;
+    S.left_c[comp][r] = *reinterpret_cast<const uint32_t*>(&S.tc[comp][(r + 2) * CT + 8]);
   }
   if (lane == 0) S.saved_x = mx;
+  wave_sync();
 }
 
 __global__ __launch_bounds__(64 * kDeblockWaves) void deblock_wavefront(DeblockArgs a) {
