@@ -37,7 +37,7 @@ size_t mivc_cavlc_mb_bytes();
 void mivc_launch_cavlc(int B, int wmb, int hmb, const void* hdr, const int16_t* coef, void* mbs, int* len,
                        long long* off, int* trail, long long* total_bits, int* slot_bytes, uint32_t* words,
                        long long cap_words, const uint32_t* hdr_bits, const int* hdr_nbits, int pslice, int slice_qp,
-                       uint8_t* out, long long* out_off, void* stream);
+                       const int* slot_qp, uint8_t* out, long long* out_off, void* stream);
 void mivc_launch_sse(int B, int W, int H, int w, int h, const uint8_t* sy, const uint8_t* su, const uint8_t* sv,
                      const uint8_t* ry, const uint8_t* ru, const uint8_t* rv, unsigned long long* sse,
                      float* ssim_sum, void* stream);
@@ -102,11 +102,11 @@ PYBIND11_MODULE(_hip, m) {
   m.def("cavlc_mb_bytes", []() { return mivc_cavlc_mb_bytes(); });
   m.def("cavlc", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t coef, uintptr_t mbs, uintptr_t len, uintptr_t off,
                     uintptr_t trail, uintptr_t total_bits, uintptr_t slot_bytes, uintptr_t words, long long cap_words,
-                    uintptr_t hdr_bits, uintptr_t hdr_nbits, int pslice, int slice_qp, uintptr_t out, uintptr_t out_off,
-                    uintptr_t stream) {
+                    uintptr_t hdr_bits, uintptr_t hdr_nbits, int pslice, int slice_qp, uintptr_t slot_qp,
+                    uintptr_t out, uintptr_t out_off, uintptr_t stream) {
     mivc_launch_cavlc(B, wmb, hmb, P<void>(hdr), P<int16_t>(coef), P<void>(mbs), P<int>(len), P<long long>(off),
                       P<int>(trail), P<long long>(total_bits), P<int>(slot_bytes), P<uint32_t>(words), cap_words,
-                      P<uint32_t>(hdr_bits), P<int>(hdr_nbits), pslice, slice_qp, P<uint8_t>(out),
+                      P<uint32_t>(hdr_bits), P<int>(hdr_nbits), pslice, slice_qp, P<int>(slot_qp), P<uint8_t>(out),
                       P<long long>(out_off), S(stream));
   });
   m.def("sse", [](int B, int W, int H, int w, int h, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t ry,

@@ -59,6 +59,7 @@ struct CavlcArgs {
   const int* hdr_nbits;      // [B]
   int pslice;
   int slice_qp;
+  const int* slot_qp;    // [B] per-slot slice QP (null: slice_qp for every slot)
   uint8_t* out;          // compacted bytes
   long long* out_off;    // [B] byte offset of every slot in `out`
 };
@@ -394,7 +395,7 @@ __global__ __launch_bounds__(1024) void cavlc_scan(CavlcArgs a) {
       lc = i;
     }
     if (m.has_delta) {
-      int prev = ld >= 0 ? a.hdr[base + ld].qp : a.slice_qp;
+      int prev = ld >= 0 ? a.hdr[base + ld].qp : (a.slot_qp ? a.slot_qp[slot] : a.slice_qp);
       int d = a.hdr[base + i].qp - prev;
       if (d < -26) d += 52;
       if (d > 25) d -= 52;
@@ -593,7 +594,8 @@ extern "C" size_t mivc_cavlc_mb_bytes() { return sizeof(CavlcMb) + 28 * sizeof(u
 extern "C" void mivc_launch_cavlc(int B, int wmb, int hmb, const void* hdr, const int16_t* coef, void* mbs, int* len,
                                   long long* off, int* trail, long long* total_bits, int* slot_bytes, uint32_t* words,
                                   long long cap_words, const uint32_t* hdr_bits, const int* hdr_nbits, int pslice,
-                                  int slice_qp, uint8_t* out, long long* out_off, void* stream) {
+                                  int slice_qp, const int* slot_qp, uint8_t* out, long long* out_off,
+                                  void* stream) {
   CavlcArgs a;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.hdr = static_cast<const mivc::h264::MbHeader*>(hdr);
@@ -612,6 +614,7 @@ extern "C" void mivc_launch_cavlc(int B, int wmb, int hmb, const void* hdr, cons
   a.hdr_nbits = hdr_nbits;
   a.pslice = pslice;
   a.slice_qp = slice_qp;
+  a.slot_qp = slot_qp;
   a.out = out;
   a.out_off = out_off;
   hipStream_t s = static_cast<hipStream_t>(stream);

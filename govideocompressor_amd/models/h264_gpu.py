@@ -146,8 +146,11 @@ class GpuH264Encoder:
             self.cav_sizes = [torch.zeros((B,), dtype=i32, device=dev) for _ in range(2)]
             self.h_sizes = [torch.zeros((B,), dtype=i32).pin_memory() for _ in range(2)]
             self.cav_out = [torch.zeros((B * self.cap_words * 4,), dtype=u8, device=dev) for _ in range(2)]
-            self.h_out = [torch.empty((B * self.cap_words * 4,), dtype=u8).pin_memory() for _ in range(2)]
+            # compressed bytes land in one of 3 pinned host buffers (grown on demand): frame t's
+            # NAL wrapping may still read buffer t%3 while frames t+1, t+2 are copied out
+            self.h_out: list = [None, None, None]
             self.out_done = [torch.cuda.Event() for _ in range(2)]
+            self.copy_pool = cf.ThreadPoolExecutor(max_workers=1)
         self.copy_stream = torch.cuda.Stream(device=dev)
         self.copy_done = [torch.cuda.Event() for _ in range(2)]
         self.compute_done = [torch.cuda.Event() for _ in range(2)]
@@ -209,14 +212,15 @@ class GpuH264Encoder:
     def _frame_params(self, b: int, t: int, qp_frame: int, idr: bool, idr_ids: list[int]) -> dict:
         return dict(idr=int(idr), frame_num=t, idr_pic_id=idr_ids[b] & 0xFFFF, qp=qp_frame)
 
-    def _gpu_cavlc(self, k: int, t: int, qp_frame: int, idr: bool, idr_ids: list[int]):
-        """Launch the CAVLC kernels for the current frame step on the compute stream."""
+    def _gpu_cavlc(self, k: int, t: int, qps_t, idr: bool, idr_ids: list[int]):
+        """Launch the CAVLC kernels for the current frame step on the compute stream.
+        qps_t: per-slot slice QP of this frame step (sequence of B ints)."""
         hb, hn = self.h_hdr_bits[k], self.h_hdr_nbits[k]
         hbn, hnn = hb.numpy(), hn.numpy()
         cache = {}
         for b in range(self.B):
-            fp = self._frame_params(b, t, qp_frame, idr, idr_ids)
-            key = fp["idr_pic_id"] if idr else -1
+            fp = self._frame_params(b, t, int(qps_t[b]), idr, idr_ids)
+            key = (fp["idr_pic_id"] if idr else -1, fp["qp"])
             if key not in cache:
                 cache[key] = self.host.slice_header_bits(self.cfg, fp)
             words, nbits = cache[key]
@@ -229,26 +233,42 @@ class GpuH264Encoder:
         self.hip.cavlc(self.B, self.wmb, self.hmb, P(self.hdr[k]), P(self.coef[k]), P(self.cav_mbs), P(self.cav_len),
                        P(self.cav_off), P(self.cav_trail), P(self.cav_total), P(self.cav_sizes[k]),
                        P(self.cav_words), self.cap_words, P(self.cav_hdr_bits[k]), P(self.cav_hdr_nbits[k]),
-                       0 if idr else 1, qp_frame, P(self.cav_out[k]), P(self.cav_out_off), self._stream())
+                       0 if idr else 1, int(qps_t[0]), P(self.qp), P(self.cav_out[k]), P(self.cav_out_off),
+                       self._stream())
 
-    def _collect_gpu_slices(self, k: int, idr: bool) -> list[tuple[bytes, int]]:
+    def _copy_out(self, t: int, k: int, idr: bool, copied, wrap_futs):
+        """Copy thread (frames in order): sizes -> compressed bytes D2H, then hand the NAL
+        wrapping to the pool.  ``copied[t]`` releases the device buffers of slot k for frame
+        t + 2 as soon as the bytes are on the host; the wrapping is off that critical path."""
         t0 = time.perf_counter()
         self.copy_done[k].synchronize()
         t1 = time.perf_counter()
         sizes = self.h_sizes[k].numpy().astype(np.int64).tolist()
         total = int(sum(sizes))
+        h = t % 3
+        if t >= 3:
+            wrap_futs[t - 3].result()  # host buffer h is free again
+        buf = self.h_out[h]
+        if buf is None or buf.numel() < total:
+            buf = self.h_out[h] = torch.empty((max(total, 1 << 26),), dtype=torch.uint8).pin_memory()
         with torch.cuda.device(self.dev), torch.cuda.stream(self.copy_stream):
-            self.h_out[k][:total].copy_(self.cav_out[k][:total], non_blocking=True)
+            buf[:total].copy_(self.cav_out[k][:total], non_blocking=True)
             self.out_done[k].record(self.copy_stream)
         self.out_done[k].synchronize()
-        nals = self.host.nal_wrap_many(self.h_out[k][:total].numpy(), sizes, 3 if idr else 2, 5 if idr else 1)
+        copied[t].set()
         t2 = time.perf_counter()
         self.timings["entropy_wait_gpu_s"] = self.timings.get("entropy_wait_gpu_s", 0.0) + (t1 - t0)
-        self.timings["entropy_s"] = self.timings.get("entropy_s", 0.0) + (t2 - t1)
+        self.timings["d2h_s"] = self.timings.get("d2h_s", 0.0) + (t2 - t1)
+        wrap_futs[t] = self.pool.submit(self._wrap, buf, total, sizes, idr)
+
+    def _wrap(self, buf, total: int, sizes: list[int], idr: bool) -> list[tuple[bytes, int]]:
+        t0 = time.perf_counter()
+        nals = self.host.nal_wrap_many(buf[:total].numpy(), sizes, 3 if idr else 2, 5 if idr else 1)
+        self.timings["entropy_s"] = self.timings.get("entropy_s", 0.0) + (time.perf_counter() - t0)
         return [(n, len(n) * 8) for n in nals]
 
     # ------------------------------------------------------------------ entropy (host)
-    def _write_slices(self, k: int, t: int, qp_frame: int, idr: bool, idr_ids: list[int]) -> list[tuple[bytes, int]]:
+    def _write_slices(self, k: int, t: int, qps_t, idr: bool, idr_ids: list[int]) -> list[tuple[bytes, int]]:
         t0 = time.perf_counter()
         self.copy_done[k].synchronize()
         t1 = time.perf_counter()
@@ -256,7 +276,7 @@ class GpuH264Encoder:
         coef = self.h_coef[k].numpy()
 
         def one(b: int):
-            fp = self._frame_params(b, t, qp_frame, idr, idr_ids)
+            fp = self._frame_params(b, t, int(qps_t[b]), idr, idr_ids)
             nal, st = self.host.write_slice(self.cfg, fp, hdr[b], coef[b])
             return nal, st["bits"]
 
@@ -269,13 +289,16 @@ class GpuH264Encoder:
     # ------------------------------------------------------------------ public API
     @torch.no_grad()
     def encode(self, y: torch.Tensor, u: torch.Tensor, v: torch.Tensor, idr_base: int = 0,
-               keep_recon: bool = False, metrics: bool = True, idr_ids: list[int] | None = None) -> list[SegmentResult]:
+               keep_recon: bool = False, metrics: bool = True, idr_ids: list[int] | None = None,
+               qps=None) -> list[SegmentResult]:
         """Encode B segments of F frames each.
 
         y: [B, F, h, w] uint8 (device), u/v: [B, F, h/2, w/2].  Each slot's output is a
         self-contained Annex-B segment (SPS/PPS + IDR + P...), i.e. one "piece" of the
         reference's split directory, with idr_pic_id = idr_ids[slot] (default idr_base + slot).
         When (h, w) differs from the configured size the prep kernel resamples (``-s WxH``).
+        ``qps``: optional [B, F] per-frame QPs from the rate control (default: the params' CRF/QP,
+        I frames 3 lower).
         """
         B, F = y.shape[0], y.shape[1]
         if B != self.B:
@@ -292,27 +315,44 @@ class GpuH264Encoder:
             raise ValueError("idr_ids needs one entry per slot")
         torch.cuda.set_device(self.dev)
         qp_i, qp_p = self.p.frame_qps()
+        if qps is None:
+            qps_h = np.full((B, F), qp_p, dtype=np.int32)
+            qps_h[:, 0] = qp_i
+        else:
+            qps_h = np.clip(np.asarray(qps, dtype=np.int32).reshape(B, F), 0, 51)
+        qps_d = torch.from_numpy(np.ascontiguousarray(qps_h.T)).to(self.dev)  # [F, B]
         self.err.zero_()
         sse = torch.zeros((F, B, 3), dtype=torch.int64, device=self.dev)
         ssim = torch.zeros((F, B), dtype=torch.float32, device=self.dev)
         pending: list[cf.Future] = [None, None]  # type: ignore[list-item]
         outs: list[list[tuple[bytes, int]]] = [None] * F  # type: ignore[list-item]
+        import threading
+        copied = [threading.Event() for _ in range(F)]
+        copy_futs: list = [None] * F
+        wrap_futs: list = [None] * F
+
+        def wait_copied(i: int):
+            while not copied[i].wait(0.5):
+                if copy_futs[i].done() and copy_futs[i].exception() is not None:
+                    raise copy_futs[i].exception()
         recons = [] if keep_recon else None
         main = torch.cuda.current_stream(self.dev)
         for t in range(F):
             k = t & 1
             idr = t == 0
-            qpf = qp_i if idr else qp_p
+            qpt = qps_h[:, t]
             # the device/pinned buffers of slot k were last used by step t-2: wait for them
-            if pending[k] is not None:
-                tw = time.perf_counter()
+            tw = time.perf_counter()
+            if self.entropy == "gpu" and t >= 2:
+                wait_copied(t - 2)
+            elif pending[k] is not None:
                 outs[t - 2] = pending[k].result()
-                self.timings["host_blocked_s"] = self.timings.get("host_blocked_s", 0.0) + time.perf_counter() - tw
                 pending[k] = None
+            self.timings["host_blocked_s"] = self.timings.get("host_blocked_s", 0.0) + time.perf_counter() - tw
             main.wait_event(self.copy_done[k]) if t >= 2 else None
             cur, ref = self.rec[k], self.rec[1 - k]
             self._prep(y, u, v, t)
-            self.qp.fill_(qpf)
+            self.qp.copy_(qps_d[t])
             self._encode_frame(idr, cur, ref, self.hdr[k], self.coef[k])
             if metrics:
                 self.hip.sse(B, self.W, self.H, self.p.width, self.p.height, self._ptr(self.src[0]),
@@ -321,7 +361,7 @@ class GpuH264Encoder:
             if keep_recon:
                 recons.append(tuple(c.clone() for c in cur))
             if self.entropy == "gpu":
-                self._gpu_cavlc(k, t, qpf, idr, idr_ids)
+                self._gpu_cavlc(k, t, qpt, idr, idr_ids)
             self.compute_done[k].record(main)
             with torch.cuda.stream(self.copy_stream):
                 self.copy_stream.wait_event(self.compute_done[k])
@@ -332,9 +372,14 @@ class GpuH264Encoder:
                     self.h_coef[k].copy_(self.coef[k], non_blocking=True)
                 self.copy_done[k].record(self.copy_stream)
             if self.entropy == "gpu":
-                pending[k] = self.pool.submit(self._collect_gpu_slices, k, idr)
+                copy_futs[t] = self.copy_pool.submit(self._copy_out, t, k, idr, copied, wrap_futs)
             else:
-                pending[k] = self.pool.submit(self._write_slices, k, t, qpf, idr, idr_ids)
+                pending[k] = self.pool.submit(self._write_slices, k, t, qpt, idr, idr_ids)
+        if self.entropy == "gpu":
+            for t in range(F):
+                copy_futs[t].result()
+            for t in range(F):
+                outs[t] = wrap_futs[t].result()
         for t in range(max(0, F - 2), F):
             k = t & 1
             if pending[k] is not None:
@@ -370,6 +415,8 @@ class GpuH264Encoder:
 
     def close(self):
         self.pool.shutdown(wait=True)
+        if hasattr(self, "copy_pool"):
+            self.copy_pool.shutdown(wait=True)
 
 
 def synth_clip(slots: int, frames: int, width: int, height: int, seed: int = 0, frame0: int = 0,

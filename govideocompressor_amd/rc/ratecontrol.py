@@ -1,0 +1,140 @@
+"""Rate control: CRF and two-pass average bitrate over closed-GOP segments.
+
+Reference: the rate is whatever ``-crf`` / ``-b:v`` ffmpeg receives in the worker's
+argument string (``-threads 4 -vcodec libx265 -crf 26`` / libx264's default CRF 23,
+server.go:67-71); every segment is rate-controlled independently, so quality and
+rate jump at segment boundaries.
+
+Here:
+
+* **CRF** (x264-style, without MB-tree): a frame's quantiser scale follows the
+  blurred lowres complexity ``C`` of its frame type,
+  ``qscale = C^(1-qcomp) / rate_factor``, ``rate_factor = base^(1-qcomp) / qp2qscale(crf)``,
+  with ``qcomp = 0.6`` and the I/P offset of ``ipratio = 1.4`` (3 QP).
+* **Two-pass ABR**: pass 1 measures per-frame bits at a fixed QP (or uses lowres
+  complexity when no pass-1 encode is available).  The per-frame statistics of
+  *all* segments of *all* ranks are summed into one global tensor with a single
+  all-reduce (CC-1, RCCL over xGMI on a GPU node), so every rank solves the same
+  global rate factor: the bitrate budget is shared across segment boundaries
+  instead of being met segment by segment.
+
+The model of bits versus quantiser is the standard ``bits ~ qscale^-1`` around the
+pass-1 point, refined with the measured exponent when two points are available.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+QCOMP = 0.6
+IP_OFFSET = 3          # I-frame QP = P QP - 3 (ipratio 1.4)
+QP_MIN, QP_MAX = 0, 51
+
+
+def qp2qscale(qp: float) -> float:
+    return 0.85 * 2.0 ** ((qp - 12.0) / 6.0)
+
+
+def qscale2qp(q: float) -> float:
+    return 12.0 + 6.0 * math.log2(max(q, 1e-9) / 0.85)
+
+
+def clamp_qp(qp: float) -> int:
+    return int(max(QP_MIN, min(QP_MAX, round(qp))))
+
+
+@dataclass
+class FrameStats:
+    """Per-frame statistics of one segment: [n_frames, 4] = (cost_intra, cost_inter, bits, qp)."""
+    data: np.ndarray
+
+    @staticmethod
+    def from_costs(intra, inter, bits=None, qp=None) -> "FrameStats":
+        n = len(intra)
+        d = np.zeros((n, 4), dtype=np.float64)
+        d[:, 0] = intra
+        d[:, 1] = inter
+        if bits is not None:
+            d[:, 2] = bits
+        if qp is not None:
+            d[:, 3] = qp
+        return FrameStats(d)
+
+
+def frame_complexity(intra: np.ndarray, inter: np.ndarray, keyint: int | None = None) -> np.ndarray:
+    """Complexity used for frame f: intra cost for key frames, inter cost otherwise."""
+    n = len(intra)
+    c = np.array(inter, dtype=np.float64, copy=True)
+    g = keyint if keyint and keyint > 0 else n
+    c[::g] = np.asarray(intra, dtype=np.float64)[::g]
+    return np.maximum(c, 1.0)
+
+
+def crf_qps(intra: np.ndarray, inter: np.ndarray, crf: float, mb_count: int, keyint: int | None = None,
+            blur: float = 0.5) -> np.ndarray:
+    """Per-frame QPs of a CRF encode of one segment (x264 rc_crf without MB-tree).
+
+    ``mb_count`` = 16x16 macroblocks per frame; complexities are per frame lowres SATD
+    sums (half-resolution 8x8 blocks: one per MB)."""
+    cplx = frame_complexity(intra, inter, keyint)
+    # temporal blur of the complexity (x264 keeps a decaying sum)
+    blurred = np.empty_like(cplx)
+    acc, w = 0.0, 0.0
+    for i, c in enumerate(cplx):
+        acc = acc * blur + c
+        w = w * blur + 1.0
+        blurred[i] = acc / w
+    base = 80.0 * mb_count  # x264: base complexity (shift for a "typical" frame)
+    rate_factor = base ** (1.0 - QCOMP) / qp2qscale(crf)
+    qs = blurred ** (1.0 - QCOMP) / rate_factor
+    qp = np.array([qscale2qp(q) for q in qs])
+    g = keyint if keyint and keyint > 0 else len(qp)
+    qp[::g] -= IP_OFFSET
+    return np.array([clamp_qp(q) for q in qp], dtype=np.int32)
+
+
+def abr_solve(stats: np.ndarray, target_bits: float, exponent: float = 1.0) -> float:
+    """Global QP offset so that the predicted total bits hit ``target_bits``.
+
+    ``stats``: [n_frames_total, 4] pass-1 statistics (bits measured at qp).  Predicted
+    bits of frame f at QP qp_f + d: bits_f * (qscale(qp_f) / qscale(qp_f + d))^exponent
+    = bits_f * 2^(-exponent * d / 6).  Solved in closed form."""
+    b1 = float(np.sum(stats[:, 2]))
+    if b1 <= 0 or target_bits <= 0:
+        return 0.0
+    return -6.0 / exponent * math.log2(target_bits / b1)
+
+
+def abr_qps(stats: np.ndarray, target_bits: float, exponent: float = 1.0) -> np.ndarray:
+    d = abr_solve(stats, target_bits, exponent)
+    return np.array([clamp_qp(q + d) for q in stats[:, 3]], dtype=np.int32)
+
+
+def estimate_exponent(bits_a: float, qp_a: float, bits_b: float, qp_b: float) -> float:
+    """bits ~ qscale^-e: e from two encodes of the same content."""
+    if bits_a <= 0 or bits_b <= 0 or qp_a == qp_b:
+        return 1.0
+    return -math.log2(bits_b / bits_a) * 6.0 / (qp_b - qp_a)
+
+
+class GlobalStats:
+    """CC-1: every rank writes the rows of its own segments into a zero-initialised
+    [n_frames_total, 4] tensor; one SUM all-reduce gives every rank the global table."""
+
+    def __init__(self, n_frames_total: int, env=None):
+        import torch
+        self.env = env
+        dev = env.device if env is not None else torch.device("cpu")
+        self.t = torch.zeros((n_frames_total, 4), dtype=torch.float64, device=dev)
+
+    def put(self, frame0: int, stats: np.ndarray):
+        import torch
+        self.t[frame0:frame0 + len(stats)] = torch.from_numpy(np.asarray(stats, dtype=np.float64)).to(self.t.device)
+
+    def reduce(self) -> np.ndarray:
+        from ..parallel import dist as D
+        if self.env is not None:
+            D.allreduce_stats(self.env, self.t)
+        return self.t.cpu().numpy()

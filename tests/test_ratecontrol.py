@@ -1,0 +1,43 @@
+"""Rate control math (CRF mapping, two-pass ABR solve) and the CC-1 statistics table."""
+import numpy as np
+
+from govideocompressor_amd.rc import ratecontrol as rc
+
+
+def test_qscale_roundtrip():
+    for qp in (0, 12, 23, 36, 51):
+        assert abs(rc.qscale2qp(rc.qp2qscale(qp)) - qp) < 1e-9
+
+
+def test_crf_qps_monotonic_in_crf_and_complexity():
+    intra = np.full(10, 8000.0 * 80)
+    inter = np.full(10, 3000.0 * 80)
+    q23 = rc.crf_qps(intra, inter, 23, mb_count=8160)
+    q30 = rc.crf_qps(intra, inter, 30, mb_count=8160)
+    assert (q30 >= q23).all() and (q30 > q23).any()
+    assert q23[0] == q23[1] - rc.IP_OFFSET or q23[0] < q23[1]        # key frame gets a lower QP
+    hard = rc.crf_qps(intra * 4, inter * 4, 23, mb_count=8160)
+    assert (hard >= q23).all() and hard[5] > q23[5]                   # qcomp: complex frames get higher QP
+    gop = rc.crf_qps(intra, inter, 23, mb_count=8160, keyint=5)
+    assert gop[5] < gop[4]
+
+
+def test_abr_solve_hits_target():
+    rng = np.random.default_rng(0)
+    stats = np.zeros((50, 4))
+    stats[:, 2] = rng.uniform(1e5, 3e5, 50)   # pass-1 bits
+    stats[:, 3] = 26
+    tot = stats[:, 2].sum()
+    d = rc.abr_solve(stats, tot / 2)
+    assert abs(d - 6.0) < 1e-9                 # half the bits = +6 QP at exponent 1
+    q = rc.abr_qps(stats, tot / 2)
+    assert (q == 32).all()
+    assert abs(rc.estimate_exponent(1000, 20, 500, 26) - 1.0) < 1e-9
+
+
+def test_global_stats_single_process():
+    g = rc.GlobalStats(6)
+    g.put(0, np.ones((3, 4)))
+    g.put(3, 2 * np.ones((3, 4)))
+    t = g.reduce()
+    assert t[:, 0].tolist() == [1, 1, 1, 2, 2, 2]
