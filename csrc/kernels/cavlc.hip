@@ -263,48 +263,56 @@ __device__ __forceinline__ int nc_chroma(const CavlcMb* mbs, size_t base, int wm
 }
 
 // ---------------------------------------------------------------- K1: analyze
+// Two MBs per wave (lanes 0-31 and 32-63).  Per half: lanes 0-15 count the non-zero
+// coefficients of the 16 luma blocks, 16-23 the chroma AC blocks (two 16-byte loads
+// each), lane 24 the 8 chroma DC levels; then lane 0 derives cbp / skip / mvd and lanes
+// 0-15 the Intra4x4 mode codes.
 __global__ __launch_bounds__(64) void cavlc_analyze(CavlcArgs a) {
   const Geom& g = a.g;
-  const int mb = blockIdx.x, slot = blockIdx.y, lane = threadIdx.x;
-  const int mx = mb % g.wmb, my = mb / g.wmb;
+  const int lane = threadIdx.x, sub = lane & 31, half = lane >> 5;
+  const int mb = blockIdx.x * 2 + half, slot = blockIdx.y;
+  __shared__ int s_tc[2][24];
+  __shared__ int s_dc[2];
+  const bool active = mb < g.nmb();
+  const int mbc = active ? mb : 0;
+  const int mx = mbc % g.wmb, my = mbc / g.wmb;
   const size_t base = static_cast<size_t>(slot) * g.nmb();
-  const size_t o = base + mb;
+  const size_t o = base + mbc;
   const MbHeader& h = a.hdr[o];
   const int16_t* c = a.coef + o * h264::kCoefPerMb;
   CavlcMb& m = a.mbs[o];
-  __shared__ int s_tc[24];
-  __shared__ int s_dc;
-  if (lane == 0) s_dc = 0;
-  __syncthreads();
-  // TotalCoeff per block
-  if (lane < 16) {
-    int start = h.kind == h264::MBK_I16x16 ? 1 : 0;
-    int n = 0;
-    for (int i = start; i < 16; ++i) n += c[h264::COEF_LUMA + lane * 16 + i] != 0;
-    s_tc[lane] = n;
-  } else if (lane < 24) {
-    int n = 0;
-    for (int i = 1; i < 16; ++i) n += c[h264::COEF_CHROMA_AC + (lane - 16) * 16 + i] != 0;
-    s_tc[lane] = n;
-  } else if (lane < 32) {
-    if (c[h264::COEF_CHROMA_DC + lane - 24]) atomicOr(&s_dc, 1);
+  const int kind0 = h.kind;
+  int n = 0;
+  if (sub < 24) {
+    int v[16];
+    load16(c + (sub < 16 ? h264::COEF_LUMA + sub * 16 : h264::COEF_CHROMA_AC + (sub - 16) * 16), v);
+    const int start = sub >= 16 ? 1 : (kind0 == h264::MBK_I16x16 ? 1 : 0);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) n += (i >= start && v[i] != 0) ? 1 : 0;
+  } else if (sub == 24) {
+    const uint4 q = *reinterpret_cast<const uint4*>(c + h264::COEF_CHROMA_DC);
+    n = (q.x | q.y | q.z | q.w) != 0;
   }
+  if (sub < 24) s_tc[half][sub] = n;
+  else if (sub == 24) s_dc[half] = n;
   __syncthreads();
-  if (lane < 24) m.tc[lane] = static_cast<uint8_t>(s_tc[lane]);
-  if (lane == 0) {
+  if (!active) return;
+  if (sub < 24) m.tc[sub] = static_cast<uint8_t>(n);
+  if (sub == 0) {
+    const int* tc = s_tc[half];
     int luma = 0;
     for (int b8 = 0; b8 < 4; ++b8)
-      if (s_tc[b8 * 4] | s_tc[b8 * 4 + 1] | s_tc[b8 * 4 + 2] | s_tc[b8 * 4 + 3]) luma |= 1 << b8;
-    const bool i16 = h.kind == h264::MBK_I16x16;
+      if (tc[b8 * 4] | tc[b8 * 4 + 1] | tc[b8 * 4 + 2] | tc[b8 * 4 + 3]) luma |= 1 << b8;
+    const bool i16 = kind0 == h264::MBK_I16x16;
     if (i16 && luma) luma = 15;
     int chroma = 0;
     for (int i = 16; i < 24; ++i)
-      if (s_tc[i]) chroma = 2;
-    if (!chroma && s_dc) chroma = 1;
+      if (tc[i]) chroma = 2;
+    if (!chroma && s_dc[half]) chroma = 1;
     int cbp = luma | (chroma << 4);
     m.cbp = static_cast<uint8_t>(cbp);
-    const bool inter = !h264::mbk_is_intra(h.kind);
-    int kind = h.kind == h264::MBK_PSKIP ? h264::MBK_P16x16 : h.kind;
+    const bool inter = !h264::mbk_is_intra(kind0);
+    int kind = kind0 == h264::MBK_PSKIP ? h264::MBK_P16x16 : kind0;
     m.kind = static_cast<uint8_t>(kind);
     m.has_delta = (cbp != 0 || i16) ? 1 : 0;
     m.coded = 1;
@@ -315,7 +323,8 @@ __global__ __launch_bounds__(64) void cavlc_analyze(CavlcArgs a) {
       NbMv A = nb_mv(a.hdr, base, g.wmb, g.hmb, mx - 1, my, 1);
       NbMv B = nb_mv(a.hdr, base, g.wmb, g.hmb, mx, my - 1, 2);
       NbMv C = nb_mv(a.hdr, base, g.wmb, g.hmb, mx + 1, my - 1, 2);
-      if (!C.avail) C = nb_mv(a.hdr, base, g.wmb, g.hmb, mx - 1, my - 1, 3);
+      NbMv D = nb_mv(a.hdr, base, g.wmb, g.hmb, mx - 1, my - 1, 3);
+      if (!C.avail) C = D;
       // P_Skip predictor
       int smv[2] = {0, 0};
       bool zero = !A.avail || !B.avail || (A.ref == 0 && A.mv[0] == 0 && A.mv[1] == 0) ||
@@ -341,8 +350,8 @@ __global__ __launch_bounds__(64) void cavlc_analyze(CavlcArgs a) {
       m.mvd[1] = static_cast<int16_t>(h.mv[0][1] - pmv[1]);
     }
   }
-  if (h.kind == h264::MBK_I4x4 && lane < 16) {
-    const int blk = lane, bx = h264::kBlkX[blk], by = h264::kBlkY[blk];
+  if (kind0 == h264::MBK_I4x4 && sub < 16) {
+    const int blk = sub, bx = h264::kBlkX[blk], by = h264::kBlkY[blk];
     int ma, mbm;
     bool dcpred = false;
     if (bx > 0) ma = h.i4_modes[h264::kRasterToBlk[(bx - 1) + 4 * by]];
@@ -619,7 +628,7 @@ extern "C" void mivc_launch_cavlc(int B, int wmb, int hmb, const void* hdr, cons
   a.out_off = out_off;
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipMemsetAsync(words, 0, sizeof(uint32_t) * cap_words * B, s);
-  hipLaunchKernelGGL(cavlc_analyze, dim3(nmb, B), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(cavlc_analyze, dim3((nmb + 1) / 2, B), dim3(64), 0, s, a);
   hipLaunchKernelGGL(cavlc_scan, dim3(B), dim3(1024), 0, s, a);
   hipLaunchKernelGGL(cavlc_length, dim3((nmb + 1) / 2, B), dim3(64), 0, s, a);
   hipLaunchKernelGGL(cavlc_offsets, dim3(B), dim3(1024), 0, s, a);

@@ -181,6 +181,13 @@ __device__ __forceinline__ int int_search_fixed(const MeShared& S, int sh0, int 
   return best;
 }
 
+#ifdef MIVC_ME_PROFILE
+__device__ unsigned long long g_me_prof[64][12];
+#define MPROF(ph) do { if (lin < 64 && lane == 0) g_me_prof[lin][ph] = clock64(); } while (0)
+#else
+#define MPROF(ph) do {} while (0)
+#endif
+
 __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   const Geom& g = a.g;
   // XCD-aware remap: hardware deals workgroups round-robin over the 8 XCDs; give each XCD
@@ -202,6 +209,7 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
 
   __shared__ MeShared S;
 
+  MPROF(0);
   // ---- phase 0: source MB, its intra neighbours, candidate vectors (one batch of loads)
   const int r4 = lane >> 2, c4 = (lane & 3) * 4;
   const uint32_t my_src = *reinterpret_cast<const uint32_t*>(src + static_cast<size_t>(Y0 + r4) * W + X0 + c4);
@@ -250,6 +258,7 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
     }
   }
 
+  MPROF(1);
   // ---- phase 1: reference window around the centre, with margins for the sub-pel planes
   const int wrows = 16 + 2 * R + kML + kMR;
   int wx = X0 + cx - R - kML;
@@ -258,6 +267,7 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   stage_window(S, ref, W, H, xa, Y0 + cy - R - kML, wrows, wwords, lane);
   __syncthreads();
 
+  MPROF(2);
   // ---- phase 2: integer full search
   const int side = 2 * R + 1;
   int best_key;
@@ -318,6 +328,7 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   }
   int best_mvx = bx * 4, best_mvy = by * 4;
 
+  MPROF(3);
   // ---- phase 3: sub-pel planes from the window.  s_G(r, c) = pixel (bx-4+c, by-4+r)
   const uint8_t* winb = reinterpret_cast<const uint8_t*>(S.win);
   const int gx0 = sh0 + bx - cx + R, gy0 = by - cy + R;  // window byte column / row of pixel (bx-4, by-4)
@@ -343,6 +354,7 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   if (lane < 4) S.P32[400 + lane] = 0;
   __syncthreads();
 
+  MPROF(4);
   // 4 consecutive plane bytes at byte offset `off` (any alignment) as one word
   auto load4 = [&](int off) -> uint32_t {
     const int w = off >> 2;
@@ -398,6 +410,7 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
     bkey = wave_min_key(bkey);
     best_cost = bkey >> 4;
     ring(bkey & 15, 2, &hx, &hy);
+    MPROF(5);
     if (a.subpel >= 2) {
       int qkey = (best_cost << 4) | 0;
       for (int base = 1; base < 9; base += 4) {
@@ -417,10 +430,12 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
       hx += qx;
       hy += qy;
     }
+    MPROF(6);
     best_mvx += hx;
     best_mvy += hy;
   }
   const size_t o = static_cast<size_t>(slot) * nmb + mb;
+  MPROF(7);
   // ---- phase 4: final luma prediction for the chosen vector (lane = row lane>>2, 4 columns)
   {
     int dqx = best_mvx - 4 * bx, dqy = best_mvy - 4 * by;
@@ -428,6 +443,7 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
     int offa = S.qoff[2 * q], offb = S.qoff[2 * q + 1];
     reinterpret_cast<uint32_t*>(a.out_pred + o * 256)[lane] = pred4(c4 + ox + 2, r4 + oy + 2, offa, offb);
   }
+  MPROF(8);
   // ---- phase 5: open-loop Intra16x16 estimate on source pixels: lane = mode * 16 + block
   {
     int mode = lane >> 4, blk = lane & 15;
@@ -461,7 +477,13 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
       a.out_intra_cost[o] = key + lambda * 4;
     }
   }
+  MPROF(9);
 }
+#ifdef MIVC_ME_PROFILE
+extern "C" void mivc_me_prof_read(unsigned long long* out) {
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(g_me_prof), sizeof(unsigned long long) * 64 * 12);
+}
+#endif
 
 }  // namespace gpu
 }  // namespace mivc

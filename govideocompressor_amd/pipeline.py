@@ -79,8 +79,12 @@ def encode_file(path: str, output: str, args: str = "264", backend: str = "auto"
     mine: dict[int, bytes] = {}
     stats: list[dict] = []
 
+    import concurrent.futures as cf
+    loader = cf.ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4))  # native decode releases the GIL
+
     def run(idxs: list[int]):
-        items = [(str(i), _load_segment(path, info, kind, segs, i)) for i in idxs]
+        clips = list(loader.map(lambda i: _load_segment(path, info, kind, segs, i), idxs))
+        items = [(str(i), c) for i, c in zip(idxs, clips)]
         res = impl.encode_clips(items, cfg)
         for i in idxs:
             stream, st = res[str(i)]
@@ -133,6 +137,7 @@ def encode_file(path: str, output: str, args: str = "264", backend: str = "auto"
     if env.is_main:
         out["fps"] = info.frames / wall if wall > 0 else 0.0
         log(json.dumps(out))
+    loader.shutdown(wait=False)
     be.close()
     D.shutdown(env)
     return out
