@@ -4,7 +4,11 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <atomic>
 #include <cstring>
+#include <stdexcept>
+#include <string>
+#include <thread>
 
 #include "../common/h264_enc_math.h"
 #include "annexb.h"
@@ -81,6 +85,99 @@ py::dict picture_to_dict(const DecodedPicture& p) {
   py::array_t<int16_t> mv(static_cast<py::ssize_t>(p.mv.size()));
   std::memcpy(mv.mutable_data(), p.mv.data(), p.mv.size() * 2);
   d["mv"] = mv;
+  return d;
+}
+
+// Entropy decode of one segment for GPU reconstruction (Decoder::set_parse_only).
+struct ParsedSegment {
+  std::vector<DecodedPicture> pics;
+  std::string error;
+};
+
+ParsedSegment parse_one(const std::string& s) {
+  ParsedSegment r;
+  try {
+    Decoder dec;
+    dec.set_parse_only(true);
+    dec.decode(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+    dec.flush();
+    r.pics = std::move(dec.out());
+  } catch (const std::exception& e) {
+    r.error = e.what();
+  }
+  return r;
+}
+
+template <class T>
+py::array_t<T> vec_array(const std::vector<std::vector<T>*>& parts, std::vector<py::ssize_t> shape) {
+  py::array_t<T> a(shape);
+  T* d = a.mutable_data();
+  for (const std::vector<T>* v : parts) {
+    std::memcpy(d, v->data(), v->size() * sizeof(T));
+    d += v->size();
+  }
+  return a;
+}
+
+py::dict segment_to_dict(ParsedSegment& seg) {
+  py::dict d;
+  if (!seg.error.empty()) {
+    d["error"] = seg.error;
+    return d;
+  }
+  d["error"] = py::none();
+  const py::ssize_t P = static_cast<py::ssize_t>(seg.pics.size());
+  d["n"] = P;
+  if (P == 0) return d;
+  const DecodedPicture& p0 = seg.pics[0];
+  const py::ssize_t nmb = static_cast<py::ssize_t>(p0.blk_mask.size());
+  d["width"] = p0.width;
+  d["height"] = p0.height;
+  d["coded_width"] = p0.coded_width;
+  d["coded_height"] = p0.coded_height;
+  d["crop_x"] = p0.crop_x;
+  d["crop_y"] = p0.crop_y;
+  std::vector<std::vector<uint8_t>*> hdr;
+  std::vector<std::vector<uint32_t>*> mask, off;
+  std::vector<std::vector<int16_t>*> coef;
+  py::array_t<int64_t> pic_off(P + 1);
+  py::array_t<int32_t> meta({P, static_cast<py::ssize_t>(11)});
+  int64_t* po = pic_off.mutable_data();
+  int32_t* mt = meta.mutable_data();
+  po[0] = 0;
+  bool same_geom = true;
+  for (py::ssize_t i = 0; i < P; ++i) {
+    DecodedPicture& p = seg.pics[i];
+    same_geom = same_geom && p.coded_width == p0.coded_width && p.coded_height == p0.coded_height &&
+                static_cast<py::ssize_t>(p.blk_mask.size()) == nmb;
+    hdr.push_back(&p.hdr);
+    mask.push_back(&p.blk_mask);
+    off.push_back(&p.blk_off);
+    coef.push_back(&p.coef);
+    po[i + 1] = po[i] + static_cast<int64_t>(p.coef.size() / 16);
+    int32_t* m = mt + i * 11;
+    m[0] = p.pic_id;
+    m[1] = p.ref_id;
+    m[2] = p.nal_ref;
+    m[3] = p.idr;
+    m[4] = p.slice_type;
+    m[5] = p.slice_qp;
+    m[6] = p.alpha_off;
+    m[7] = p.beta_off;
+    m[8] = p.chroma_qp_offset;
+    m[9] = p.deblock;
+    m[10] = p.gpu_ok ? 1 : 0;
+  }
+  if (!same_geom) {
+    d["error"] = std::string("resolution changes inside the segment");
+    return d;
+  }
+  d["hdr"] = vec_array<uint8_t>(hdr, {P, nmb, static_cast<py::ssize_t>(sizeof(MbHeader))});
+  d["mask"] = vec_array<uint32_t>(mask, {P, nmb});
+  d["off"] = vec_array<uint32_t>(off, {P, nmb});
+  d["coef"] = vec_array<int16_t>(coef, {static_cast<py::ssize_t>(po[P] * 16)});
+  d["pic_off"] = pic_off;
+  d["meta"] = meta;
   return d;
 }
 
@@ -192,6 +289,30 @@ PYBIND11_MODULE(_host, m) {
         return out;
       },
       py::arg("data"), py::arg("skip_deblock") = false);
+
+  m.def(
+      "parse",
+      [](const std::vector<py::bytes>& segments, int threads) {
+        // entropy decode only (CAVLC -> MbHeader + packed levels), one thread per segment
+        std::vector<std::string> in;
+        for (const py::bytes& b : segments) in.emplace_back(b);
+        std::vector<ParsedSegment> res(in.size());
+        {
+          py::gil_scoped_release rel;
+          std::atomic<size_t> next{0};
+          int nt = std::max(1, std::min<int>(threads, static_cast<int>(in.size())));
+          std::vector<std::thread> pool;
+          for (int t = 0; t < nt; ++t)
+            pool.emplace_back([&] {
+              for (size_t i = next++; i < in.size(); i = next++) res[i] = parse_one(in[i]);
+            });
+          for (std::thread& th : pool) th.join();
+        }
+        py::list out;
+        for (ParsedSegment& r : res) out.append(segment_to_dict(r));
+        return out;
+      },
+      py::arg("segments"), py::arg("threads") = 1);
 
   py::class_<CpuEncoder>(m, "CpuEncoder")
       .def(py::init([](const py::dict& cfg) { return new CpuEncoder(cfg_from(cfg)); }))

@@ -46,15 +46,22 @@ struct Pic {
   std::vector<int16_t> mv;      // [mb][16][2] raster
   std::vector<int8_t> ref;      // [mb][16] raster (ref idx, -1 intra)
   std::vector<int> refpic;      // [mb][16] raster (ref picture id, -1 intra)
-  void init(int w, int h) {
+  std::vector<uint8_t> rec_hdr; // parse-only: [mb][48] MbHeader
+  std::vector<int16_t> rec_coef;// parse-only: non-zero 16-level blocks, packed
+  std::vector<uint32_t> rec_mask, rec_off;  // parse-only: [mb] block mask / first block
+  bool gpu_ok = true;
+  int nslices = 0;
+  void init(int w, int h, bool planes = true) {
     wmb = w;
     hmb = h;
     W = w * 16;
     H = h * 16;
     size_t n = static_cast<size_t>(w) * h;
-    Y.assign(static_cast<size_t>(W) * H, 0);
-    U.assign(static_cast<size_t>(W / 2) * (H / 2), 0);
-    V.assign(U.size(), 0);
+    if (planes) {
+      Y.assign(static_cast<size_t>(W) * H, 0);
+      U.assign(static_cast<size_t>(W / 2) * (H / 2), 0);
+      V.assign(U.size(), 0);
+    }
     slice.assign(n, -1);
     kind.assign(n, 0);
     qp.assign(n, 0);
@@ -65,6 +72,14 @@ struct Pic {
     mv.assign(n * 32, 0);
     ref.assign(n * 16, -1);
     refpic.assign(n * 16, -1);
+  }
+  void init_records() {
+    size_t n = static_cast<size_t>(wmb) * hmb;
+    rec_hdr.assign(n * sizeof(MbHeader), 0);
+    rec_mask.assign(n, 0);
+    rec_off.assign(n, 0);
+    rec_coef.clear();
+    rec_coef.reserve(n * 64);
   }
   int px(int x, int y) const { return Y[static_cast<size_t>(y) * W + x]; }
 };
@@ -147,6 +162,7 @@ struct Decoder::Impl {
   int max_frame_num = 16;
   int max_refs = 1;
   bool skip_deblock = false;
+  bool parse_only = false;
 
   // per-slice state
   SliceHeader sh;
@@ -186,7 +202,7 @@ struct Decoder::Impl {
   // ------------------------------------------------------------ picture management
   void finish_picture(std::vector<DecodedPicture>& out) {
     if (!cur) return;
-    if (!skip_deblock) deblock_picture();
+    if (!skip_deblock && !parse_only) deblock_picture();
     DecodedPicture d;
     d.coded_width = cur->W;
     d.coded_height = cur->H;
@@ -206,6 +222,23 @@ struct Decoder::Impl {
     d.mv = cur->mv;
     d.ref = cur->ref;
     d.nz = cur->nz;
+    if (parse_only) {
+      d.hdr = std::move(cur->rec_hdr);
+      d.coef = std::move(cur->rec_coef);
+      d.blk_mask = std::move(cur->rec_mask);
+      d.blk_off = std::move(cur->rec_off);
+      d.slice_qp = pic_slice_qp;
+      d.pic_id = cur->id;
+      d.ref_id = pic_ref_id;
+      d.nal_ref = cur_nal_ref != 0;
+      d.alpha_off = slices.empty() ? 0 : slices[0].alpha_off;
+      d.beta_off = slices.empty() ? 0 : slices[0].beta_off;
+      d.chroma_qp_offset = slices.empty() ? 0 : slices[0].cb_off;
+      d.deblock = slices.empty() ? 1 : (slices[0].disable_idc != 1);
+      bool ok = cur->gpu_ok && cur->nslices == 1;
+      for (const SliceParams& sp2 : slices) ok = ok && sp2.cb_off == sp2.cr_off && sp2.disable_idc != 2;
+      d.gpu_ok = ok;
+    }
     (void)n;
     out.push_back(std::move(d));
     if (cur_nal_ref) {
@@ -216,9 +249,13 @@ struct Decoder::Impl {
     cur.reset();
   }
 
+  int pic_slice_qp = 0, pic_ref_id = -1;
   void start_picture(const SliceHeader& h) {
     cur = std::make_shared<Pic>();
-    cur->init(sp->width_mbs, sp->height_mbs);
+    cur->init(sp->width_mbs, sp->height_mbs, !parse_only);
+    if (parse_only) cur->init_records();
+    pic_slice_qp = h.qp;
+    pic_ref_id = -1;
     cur->frame_num = h.frame_num;
     cur->idr = h.nal_unit_type == NAL_IDR;
     cur->slice_type = h.slice_type;
@@ -275,7 +312,13 @@ struct Decoder::Impl {
     spar.cr_off = p->second_chroma_qp_index_offset;
     slices.push_back(spar);
     slice_idx = static_cast<int>(slices.size()) - 1;
+    cur->nslices = static_cast<int>(slices.size());
+    if (h.num_ref_idx_l0_active > 1 || p->constrained_intra_pred) cur->gpu_ok = false;
     build_ref_list();
+    if (!ref_list.empty()) {
+      if (pic_ref_id >= 0 && pic_ref_id != ref_list[0]->id) cur->gpu_ok = false;
+      pic_ref_id = ref_list[0]->id;
+    }
 
     int nmb = cur->wmb * cur->hmb;
     int addr = h.first_mb;
@@ -383,7 +426,34 @@ struct Decoder::Impl {
                 (B.ref == 0 && B.mv[0] == 0 && B.mv[1] == 0);
     if (!zero) pred_mv(addr, 0, 0, 16, 16, 0, 0, 0, mv);
     assign_part(addr, 0, 0, 4, 4, 0, mv[0], mv[1]);
+    if (parse_only) {
+      cur->rec_off[addr] = static_cast<uint32_t>(cur->rec_coef.size() / 16);
+      store_record(addr, MBK_PSKIP, 0, qp, 0, 0, nullptr);
+      return;
+    }
     inter_pred(addr);
+  }
+
+  // parse-only: MbHeader + levels of MB addr (lum/lumdc/cdc/cac already in the records)
+  void store_record(int addr, int kind, int cbp, int qp, int i16_mode, int chroma_mode, const int* i4modes) {
+    MbHeader h{};
+    h.kind = static_cast<uint8_t>(kind);
+    h.cbp = static_cast<uint8_t>(cbp);
+    h.qp = static_cast<int8_t>(qp);
+    h.i16_mode = static_cast<uint8_t>(i16_mode);
+    h.chroma_mode = static_cast<uint8_t>(chroma_mode);
+    for (int q = 0; q < 4; ++q) {
+      int r0 = (q & 1) * 2 + (q >> 1) * 8;  // top-left 4x4 block of quadrant q
+      h.mv[q][0] = cur->mv[addr * 32 + 2 * r0];
+      h.mv[q][1] = cur->mv[addr * 32 + 2 * r0 + 1];
+      for (int k = 0; k < 4; ++k) {  // the quadrant must carry one vector (no sub-8x8 split)
+        int r = r0 + (k & 1) + (k >> 1) * 4;
+        if (cur->mv[addr * 32 + 2 * r] != h.mv[q][0] || cur->mv[addr * 32 + 2 * r + 1] != h.mv[q][1])
+          cur->gpu_ok = false;
+      }
+    }
+    for (int b = 0; b < 16; ++b) h.i4_modes[b] = static_cast<uint8_t>(i4modes ? i4modes[b] : 2);
+    std::memcpy(cur->rec_hdr.data() + static_cast<size_t>(addr) * sizeof(MbHeader), &h, sizeof(MbHeader));
   }
 
   // ------------------------------------------------------------ inter prediction (8.4.2.2)
@@ -825,6 +895,7 @@ struct Decoder::Impl {
       cur->qp[addr] = static_cast<int8_t>(qp);
       cur->qp_dbk[addr] = 0;
       for (int i = 0; i < 16; ++i) blk_done[i] = 1;
+      cur->gpu_ok = false;
       return;
     }
     // ---- prediction syntax
@@ -945,6 +1016,36 @@ struct Decoder::Impl {
       for (int i = 0; i < 16; ++i) any |= lum[blk][i] != 0;
       if (kind == MBK_I16x16) any |= lumdc[blk] != 0;  // not used for bS (intra), informative
       cur->nz[addr * 16 + kBlkX[blk] + 4 * kBlkY[blk]] = any;
+    }
+    if (parse_only) {
+      // packed levels: one 16-entry block per non-zero block, in mask-bit order
+      // (bits 0-15 luma blkIdx, 16 luma DC, 17 chroma DC Cb|Cr, 18-25 chroma AC comp*4+b)
+      uint32_t mask = 0;
+      cur->rec_off[addr] = static_cast<uint32_t>(cur->rec_coef.size() / 16);
+      auto put = [&](int bit, const int* v, int n, const int* v2) {
+        bool any = false;
+        for (int i = 0; i < n; ++i) any |= v[i] != 0 || (v2 && v2[i] != 0);
+        if (!any) return;
+        mask |= 1u << bit;
+        size_t b = cur->rec_coef.size();
+        cur->rec_coef.resize(b + 16, 0);
+        for (int i = 0; i < n; ++i) cur->rec_coef[b + i] = static_cast<int16_t>(v[i]);
+        if (v2)
+          for (int i = 0; i < n; ++i) cur->rec_coef[b + n + i] = static_cast<int16_t>(v2[i]);
+      };
+      for (int blk = 0; blk < 16; ++blk) put(blk, lum[blk], 16, nullptr);
+      if (kind == MBK_I16x16) put(16, lumdc, 16, nullptr);
+      put(17, cdc[0], 4, cdc[1]);
+      for (int cc = 0; cc < 2; ++cc)
+        for (int b = 0; b < 4; ++b) put(18 + cc * 4 + b, cac[cc][b], 16, nullptr);
+      cur->rec_mask[addr] = mask;
+      if (kind != MBK_I4x4 && kind != MBK_I16x16 && kind != MBK_P16x16 && kind != MBK_P16x8 &&
+          kind != MBK_P8x16 && kind != MBK_P8x8)
+        cur->gpu_ok = false;
+      store_record(addr, kind, cbp_luma | (cbp_chroma << 4), qp, i16_mode, chroma_mode,
+                   kind == MBK_I4x4 ? i4modes : nullptr);
+      for (int i = 0; i < 16; ++i) blk_done[i] = 1;
+      return;
     }
     for (int i = 0; i < 16; ++i) blk_done[i] = 0;
     // ---- reconstruction
@@ -1217,6 +1318,8 @@ void Decoder::decode(const uint8_t* data, size_t n) {
 }
 
 void Decoder::flush() { impl_->finish_picture(out_); }
+
+void Decoder::set_parse_only(bool v) { impl_->parse_only = v; }
 
 }  // namespace h264
 }  // namespace mivc

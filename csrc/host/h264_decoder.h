@@ -32,6 +32,18 @@ struct DecodedPicture {
   std::vector<int16_t> mv;            // [mb][16][2] quarter-pel L0 MV per 4x4 block
   std::vector<int8_t> ref;            // [mb][16]
   std::vector<uint8_t> nz;            // [mb][16] non-zero luma coefficients per 4x4 block
+  // parse-only mode (GPU reconstruction): per-MB decision records in the encoder's layout
+  // (csrc/common/h264_mb.h: MbHeader + kCoefPerMb levels), plus the slice parameters
+  std::vector<uint8_t> hdr;           // [mb][48] MbHeader
+  std::vector<int16_t> coef;          // packed 16-level blocks (scan order, not dequantised)
+  std::vector<uint32_t> blk_mask;     // [mb] which blocks are present: bits 0-15 luma (blkIdx),
+                                      // 16 I16x16 DC, 17 chroma DC (Cb 0-3, Cr 4-7), 18-25 chroma AC
+  std::vector<uint32_t> blk_off;      // [mb] index of the MB's first block in coef (units of 16)
+  int pic_id = 0, ref_id = -1;        // decode-order id of this picture / of its L0 ref 0
+  int nal_ref = 1;
+  int slice_qp = 0, alpha_off = 0, beta_off = 0, chroma_qp_offset = 0, deblock = 1;
+  bool gpu_ok = true;                 // false: a feature the GPU path does not cover (sub-8x8
+                                      // partitions, >1 reference, I_PCM, several slices ...)
   // copy the cropped planes out as one contiguous I420 frame
   std::vector<uint8_t> cropped_i420() const;
 };
@@ -47,6 +59,8 @@ class Decoder {
   std::vector<DecodedPicture>& out() { return out_; }
   // Disable the in-loop filter (testing only: lets a test compare unfiltered recon)
   void set_skip_deblock(bool v) { skip_deblock_ = v; }
+  // Entropy-decode only: fill DecodedPicture::hdr/coef/nz and skip pixel reconstruction
+  void set_parse_only(bool v);
 
   struct Impl;
 

@@ -33,6 +33,10 @@ void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t* src_y, con
 void mivc_launch_deblock(int B, int wmb, int hmb, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const void* hdr,
                          const uint8_t* nz, int chroma_qp_offset, int alpha_off, int beta_off, int* err,
                          void* stream);
+void mivc_launch_decode_picture(int B, int wmb, int hmb, const uint8_t* ref_y, const uint8_t* ref_u,
+                                const uint8_t* ref_v, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const void* hdr,
+                                const uint32_t* mask, const uint32_t* off, const int16_t* coef, const int8_t* run,
+                                int any_p, int chroma_qp_offset, uint8_t* nz, int* err, void* stream);
 size_t mivc_cavlc_mb_bytes();
 void mivc_launch_cavlc(int B, int wmb, int hmb, const void* hdr, const int16_t* coef, void* mbs, int* len,
                        long long* off, int* trail, long long* total_bits, int* slot_bytes, uint32_t* words,
@@ -98,6 +102,13 @@ PYBIND11_MODULE(_hip, m) {
                       int cqo, int alpha_off, int beta_off, uintptr_t err, uintptr_t stream) {
     mivc_launch_deblock(B, wmb, hmb, P<uint8_t>(ry), P<uint8_t>(ru), P<uint8_t>(rv), P<void>(hdr), P<uint8_t>(nz),
                         cqo, alpha_off, beta_off, P<int>(err), S(stream));
+  });
+  m.def("decode_picture", [](int B, int wmb, int hmb, uintptr_t ry, uintptr_t ru, uintptr_t rv, uintptr_t y,
+                             uintptr_t u, uintptr_t v, uintptr_t hdr, uintptr_t mask, uintptr_t off, uintptr_t coef,
+                             uintptr_t run, int any_p, int cqo, uintptr_t nz, uintptr_t err, uintptr_t stream) {
+    mivc_launch_decode_picture(B, wmb, hmb, P<uint8_t>(ry), P<uint8_t>(ru), P<uint8_t>(rv), P<uint8_t>(y),
+                               P<uint8_t>(u), P<uint8_t>(v), P<void>(hdr), P<uint32_t>(mask), P<uint32_t>(off),
+                               P<int16_t>(coef), P<int8_t>(run), any_p, cqo, P<uint8_t>(nz), P<int>(err), S(stream));
   });
   m.def("cavlc_mb_bytes", []() { return mivc_cavlc_mb_bytes(); });
   m.def("cavlc", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t coef, uintptr_t mbs, uintptr_t len, uintptr_t off,

@@ -41,7 +41,7 @@ struct IntraArgs {
   int use_i4x4;
 };
 
-constexpr int TS = 24;  // tile stride
+constexpr int TS = kTileStride;
 
 struct IntraShared {
   uint8_t tile[17 * TS];   // reconstructed neighbourhood + current MB (luma); row 0 / col 0 = neighbours
@@ -71,30 +71,6 @@ struct IntraShared {
   uint8_t saved_c[2][8];
   int saved_modes[4];
 };
-
-__device__ __forceinline__ void i4_neighbours(const uint8_t* t, int blk, int mbav, int* e, int* av_out) {
-  int bx = h264::kBlkX[blk], by = h264::kBlkY[blk];
-  bool left = bx > 0 || (mbav & h264::AV_LEFT), top = by > 0 || (mbav & h264::AV_TOP);
-  int av = 0;
-  if (left) av |= h264::AV_LEFT;
-  if (top) av |= h264::AV_TOP;
-  if (left && top) av |= h264::AV_TOPLEFT;
-  bool tr;
-  if (blk == 3 || blk == 7 || blk == 11 || blk == 13 || blk == 15) tr = false;
-  else if (blk == 5) tr = (mbav & h264::AV_TOPRIGHT) != 0;
-  else if (blk == 0 || blk == 1 || blk == 4) tr = (mbav & h264::AV_TOP) != 0;
-  else tr = true;
-  if (tr) av |= h264::AV_TOPRIGHT;
-  const uint8_t* row = t + (by * 4) * TS + bx * 4;  // tile row above the block, col of x = -1
-  e[0] = row[0];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) e[1 + i] = row[1 + i];
-#pragma unroll
-  for (int i = 4; i < 8; ++i) e[1 + i] = tr ? row[1 + i] : row[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) e[9 + i] = t[(by * 4 + 1 + i) * TS + bx * 4];
-  *av_out = av;
-}
 
 // 4x4 intra prediction sample at compile-time (x, y) for a runtime mode
 __device__ __forceinline__ void i4_pred_block(int mode, int av, const int* e, int* pred) {

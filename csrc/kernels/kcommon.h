@@ -197,5 +197,36 @@ __device__ __forceinline__ int pos_class(int x, int y) {
   return ((x | y) & 1) == 0 ? 0 : (((x & y) & 1) ? 1 : 2);
 }
 
+
+// ---------------------------------------------------------------- intra neighbourhood tiles
+// Luma tile of the intra kernels (encoder and decoder): row 0 = the row above the MB
+// (x = -1 .. 19, top-right included), column 0 = the column to its left.
+constexpr int kTileStride = 24;
+
+// Intra4x4 neighbour vector e[13] of block blk (see h264::i4_pred_sample) + availability
+__device__ __forceinline__ void i4_neighbours(const uint8_t* t, int blk, int mbav, int* e, int* av_out) {
+  int bx = h264::kBlkX[blk], by = h264::kBlkY[blk];
+  bool left = bx > 0 || (mbav & h264::AV_LEFT), top = by > 0 || (mbav & h264::AV_TOP);
+  int av = 0;
+  if (left) av |= h264::AV_LEFT;
+  if (top) av |= h264::AV_TOP;
+  if (left && top) av |= h264::AV_TOPLEFT;
+  bool tr;
+  if (blk == 3 || blk == 7 || blk == 11 || blk == 13 || blk == 15) tr = false;
+  else if (blk == 5) tr = (mbav & h264::AV_TOPRIGHT) != 0;
+  else if (blk == 0 || blk == 1 || blk == 4) tr = (mbav & h264::AV_TOP) != 0;
+  else tr = true;
+  if (tr) av |= h264::AV_TOPRIGHT;
+  const uint8_t* row = t + (by * 4) * kTileStride + bx * 4;  // tile row above the block, col of x = -1
+  e[0] = row[0];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) e[1 + i] = row[1 + i];
+#pragma unroll
+  for (int i = 4; i < 8; ++i) e[1 + i] = tr ? row[1 + i] : row[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) e[9 + i] = t[(by * 4 + 1 + i) * kTileStride + bx * 4];
+  *av_out = av;
+}
+
 }  // namespace gpu
 }  // namespace mivc

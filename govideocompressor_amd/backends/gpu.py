@@ -44,6 +44,7 @@ class GpuBackend:
                                  max_resident=1)
         self._streams = StageStreams(self.device)
         self._io = cf.ThreadPoolExecutor(max_workers=8)
+        self._decoder = None
 
     def _encoder(self, params, slots: int):
         key = (params.width, params.height, params.fps, params.crf, params.qp, slots)
@@ -86,13 +87,50 @@ class GpuBackend:
                 out[key] = (stream, st)
         return out
 
+    def decoder(self):
+        """The batched GPU H.264 decoder (host CAVLC parse + gfx950 reconstruction)."""
+        if self._decoder is None:
+            from ..models.h264_decode_gpu import GpuH264Decoder
+            self._decoder = GpuH264Decoder(self.device)
+        return self._decoder
+
+    def decode_streams(self, streams: list[bytes], fps: float = 30.0):
+        """Annex-B segments -> device-resident clips (``DecodedSegment``), one batched call."""
+        return self.decoder().decode(streams, fps)
+
+    def _load_compressed(self, jobs: list[PieceJob]) -> dict[str, object]:
+        """Compressed pieces (.264/.mp4, CAVLC) decode together on the GPU."""
+        from ..ops import native
+        from ..segment.probe import annexb_of, kind_of
+        host = native.host()
+        streams, keys, fps = [], [], 30.0
+        for j in jobs:
+            st = annexb_of(j.in_path, kind_of(j.in_path))
+            info = host.stream_info(st)
+            if info["entropy"] == "cabac":
+                raise BackendError("input uses CABAC; this build decodes CAVLC H.264 only")
+            fps = info["fps"] or fps
+            streams.append(st)
+            keys.append(j.idx)
+        return dict(zip(keys, self.decode_streams(streams, fps)))
+
     def transcode(self, jobs: list[PieceJob], cfg: EncoderConfig) -> list[PieceResult]:
+        from ..segment.probe import kind_of
         tm = Timer()
         t0 = time.perf_counter()
         results: dict[str, PieceResult] = {}
         items = []
-        futs = {j.idx: self._io.submit(load_clip, j.in_path) for j in jobs}
-        for j in jobs:
+        comp = [j for j in jobs if kind_of(j.in_path) in ("h264", "mp4")]
+        raw = [j for j in jobs if j not in comp]
+        futs = {j.idx: self._io.submit(load_clip, j.in_path) for j in raw}
+        if comp:
+            try:
+                dec = self._load_compressed(comp)
+                items += [(j.idx, dec[j.idx]) for j in comp]
+            except Exception as e:  # noqa: BLE001 - reported to the coordinator
+                for j in comp:
+                    results[j.idx] = PieceResult(j.idx, False, f"decode: {e}")
+        for j in raw:
             try:
                 items.append((j.idx, futs[j.idx].result()))
             except Exception as e:  # noqa: BLE001 - reported to the coordinator
@@ -119,6 +157,18 @@ class GpuBackend:
         B = len(chunk)
         F = max(c for *_, c in chunk)
         t0 = time.perf_counter()
+        if isinstance(clips[chunk[0][0]].y, torch.Tensor):  # device-resident (GPU-decoded) clips
+            dy = torch.empty((B, F, h, w), dtype=torch.uint8, device=self.device)
+            du = torch.empty((B, F, h // 2, w // 2), dtype=torch.uint8, device=self.device)
+            dv = torch.empty_like(du)
+            for b, (key, _, s, c) in enumerate(chunk):
+                cl = clips[key]
+                for dst, src in ((dy, cl.y), (du, cl.u), (dv, cl.v)):
+                    dst[b, :c].copy_(src[s:s + c])
+                    if c < F:
+                        dst[b, c:].copy_(src[s + c - 1].expand(F - c, *src.shape[1:]))
+            tm.add("upload_s", time.perf_counter() - t0)
+            return self._run_encoder(chunk, params, dy, du, dv, tm)
         y = torch.empty((B, F, h, w), dtype=torch.uint8).pin_memory()
         u = torch.empty((B, F, h // 2, w // 2), dtype=torch.uint8).pin_memory()
         v = torch.empty_like(u).pin_memory()
@@ -131,6 +181,10 @@ class GpuBackend:
         (dy, du, dv), ev = self._streams.upload([y, u, v], self.device)
         self._streams.wait(ev)
         tm.add("upload_s", time.perf_counter() - t0)
+        return self._run_encoder(chunk, params, dy, du, dv, tm)
+
+    def _run_encoder(self, chunk, params, dy, du, dv, tm: Timer):
+        B = len(chunk)
         t1 = time.perf_counter()
         enc = self._encoder(params, B)
         res = enc.encode(dy, du, dv, idr_ids=[idr_id(key, un_) for key, un_, _, _ in chunk])

@@ -82,8 +82,16 @@ def encode_file(path: str, output: str, args: str = "264", backend: str = "auto"
     import concurrent.futures as cf
     loader = cf.ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4))  # native decode releases the GIL
 
+    gpu_decode = kind == "pieces" and hasattr(impl, "decode_streams")
+    dec_stats: dict[str, float] = {}
+
     def run(idxs: list[int]):
-        clips = list(loader.map(lambda i: _load_segment(path, info, kind, segs, i), idxs))
+        if gpu_decode:  # compressed input on a GPU rank: batched GPU decode, frames stay on the device
+            clips = impl.decode_streams([segs[i] for i in idxs], info.fps)
+            for k, v in impl.decoder().stats.items():
+                dec_stats[k] = dec_stats.get(k, 0) + v
+        else:
+            clips = list(loader.map(lambda i: _load_segment(path, info, kind, segs, i), idxs))
         items = [(str(i), c) for i, c in zip(idxs, clips)]
         res = impl.encode_clips(items, cfg)
         for i in idxs:
@@ -111,7 +119,8 @@ def encode_file(path: str, output: str, args: str = "264", backend: str = "auto"
     idx_blob = json.dumps(order).encode()
     g = D.BitstreamGather(env, [idx_blob] + [mine[i] for i in order]).start()
     gathered = g.wait()
-    out = {"segments": n, "world": env.world, "encode_s_rank": t_enc}
+    out = {"segments": n, "world": env.world, "encode_s_rank": t_enc,
+           "decode": ("gpu" if gpu_decode else "cpu"), "decode_stats_rank": dec_stats}
     if env.is_main:
         by_idx: dict[int, bytes] = {}
         for rank_pieces in gathered:

@@ -1,0 +1,155 @@
+"""Random H.264 decision-record streams (test / benchmark inputs for the decoders).
+
+A stream is written from random per-MB records through the host CAVLC writer
+(``_host.write_slice``): I pictures mix Intra16x16 and Intra4x4 MBs with random
+*legal* prediction modes; P pictures mix P_Skip, P_L0_16x16, 16x8, 8x16, 8x8
+(8x8 sub-blocks) and intra MBs with random motion vectors, per-MB QP deltas and
+sparse random levels.  The result exercises every syntax path the GPU decoder
+reconstructs, which encoder-produced streams (16x16 motion only) do not.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .. import ops  # noqa: F401  (package import order)
+
+# MbHeader byte offsets (csrc/common/h264_mb.h)
+_KIND, _CBP, _QP, _I16, _CHROMA, _FLAGS, _MV, _I4 = 0, 1, 2, 3, 4, 5, 8, 24
+I4x4, I16x16, P16x16, PSKIP, P16x8, P8x16, P8x8 = 0, 1, 2, 3, 5, 6, 7
+
+_BLK_X = [0, 1, 0, 1, 2, 3, 2, 3, 0, 1, 0, 1, 2, 3, 2, 3]
+_BLK_Y = [0, 0, 1, 1, 0, 0, 1, 1, 2, 2, 3, 3, 2, 2, 3, 3]
+
+
+def _i4_modes_ok(rng, mx: int, my: int) -> list[int]:
+    out = []
+    for b in range(16):
+        bx, by = _BLK_X[b], _BLK_Y[b]
+        left = bx > 0 or mx > 0
+        top = by > 0 or my > 0
+        ok = [2]
+        if top:
+            ok += [0, 3, 7]
+        if left:
+            ok += [1, 8]
+        if top and left:
+            ok += [4, 5, 6]
+        out.append(int(rng.choice(ok)))
+    return out
+
+
+def _i16_mode(rng, mx: int, my: int) -> int:
+    ok = [2] + ([0] if my > 0 else []) + ([1] if mx > 0 else []) + ([3] if mx > 0 and my > 0 else [])
+    return int(rng.choice(ok))
+
+
+def _chroma_mode(rng, mx: int, my: int) -> int:
+    ok = [0] + ([1] if mx > 0 else []) + ([2] if my > 0 else []) + ([3] if mx > 0 and my > 0 else [])
+    return int(rng.choice(ok))
+
+
+def _levels(rng, n: int, density: float, start: int = 0) -> np.ndarray:
+    v = np.zeros(n, np.int16)
+    pos = np.arange(start, n)
+    keep = pos[rng.random(len(pos)) < density]
+    v[keep] = rng.integers(-4, 5, len(keep))
+    return v
+
+
+def _intra_record(rng, h, c, mx, my, qp, density, allow_i4=True):
+    if allow_i4 and rng.random() < 0.5:
+        h[_KIND] = I4x4
+        h[_I4:_I4 + 16] = _i4_modes_ok(rng, mx, my)
+        for b in range(16):
+            c[b * 16:(b + 1) * 16] = _levels(rng, 16, density)
+    else:
+        h[_KIND] = I16x16
+        h[_I16] = _i16_mode(rng, mx, my)
+        for b in range(16):
+            c[b * 16:(b + 1) * 16] = _levels(rng, 16, density, start=1) if rng.random() < 0.5 else 0
+        c[256:272] = _levels(rng, 16, density * 2)
+        h[_I4:_I4 + 16] = 2
+    h[_CHROMA] = _chroma_mode(rng, mx, my)
+    h[_QP] = qp
+    c[272:280] = _levels(rng, 8, density)
+    for b in range(8):
+        c[280 + b * 16:280 + (b + 1) * 16] = _levels(rng, 16, density / 2, start=1)
+
+
+def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp: int = 28,
+                  density: float = 0.15, intra_in_p: float = 0.1, mv_range: int = 48, keyint: int = 0) -> bytes:
+    """Annex-B stream of ``frames`` pictures (IDR + P) from random decision records."""
+    rng = np.random.default_rng(seed)
+    cfg = dict(width=width, height=height, qp=qp)
+    wmb, hmb = (width + 15) // 16, (height + 15) // 16
+    nmb = wmb * hmb
+    out = [host.parameter_sets(cfg)]
+    fn = 0
+    idr_id = 0
+    for t in range(frames):
+        idr = t == 0 or (keyint > 0 and t % keyint == 0)
+        if idr:
+            fn = 0
+        sqp = int(np.clip(qp + rng.integers(-2, 3), 10, 48))
+        hdr = np.zeros((nmb, 48), np.uint8)
+        coef = np.zeros((nmb, 408), np.int16)
+        for mb in range(nmb):
+            mx, my = mb % wmb, mb // wmb
+            h, c = hdr[mb], coef[mb]
+            mqp = int(np.clip(sqp + rng.integers(-3, 4), 0, 51))
+            if idr or rng.random() < intra_in_p:
+                _intra_record(rng, h, c, mx, my, mqp, density)
+                continue
+            r = rng.random()
+            kind = PSKIP if r < 0.25 else (P16x16 if r < 0.5 else (P16x8 if r < 0.65 else (P8x16 if r < 0.8 else P8x8)))
+            mv = rng.integers(-mv_range, mv_range + 1, (4, 2))
+            if kind in (PSKIP, P16x16):
+                mv[:] = mv[0]
+            elif kind == P16x8:
+                mv[1], mv[3] = mv[0], mv[2]
+            elif kind == P8x16:
+                mv[2], mv[3] = mv[0], mv[1]
+            h[_KIND] = kind
+            h[_QP] = mqp
+            h[_MV:_MV + 16] = np.frombuffer(mv.astype(np.int16).tobytes(), np.uint8)
+            if kind != PSKIP:
+                for b in range(16):
+                    c[b * 16:(b + 1) * 16] = _levels(rng, 16, density) if rng.random() < 0.6 else 0
+                c[272:280] = _levels(rng, 8, density)
+                for b in range(8):
+                    c[280 + b * 16:280 + (b + 1) * 16] = _levels(rng, 16, density / 2, start=1)
+        fp = dict(idr=int(idr), qp=sqp, frame_num=fn, idr_pic_id=idr_id)
+        nal, _ = host.write_slice(cfg, fp, hdr, coef)
+        out.append(nal)
+        if idr:
+            idr_id += 1
+        fn = (fn + 1) % 16
+    return b"".join(out)
+
+
+def unpack_levels(seg: dict, t: int) -> np.ndarray:
+    """Dense [nmb, 408] levels of picture t of a ``_host.parse`` segment (inverse of the
+    packed block format; used by the round-trip tests)."""
+    mask, off = seg["mask"][t], seg["off"][t]
+    base = int(seg["pic_off"][t])
+    coef = seg["coef"]
+    nmb = mask.shape[0]
+    out = np.zeros((nmb, 408), np.int16)
+    for mb in range(nmb):
+        m = int(mask[mb])
+        k = base + int(off[mb])
+        for bit in range(26):
+            if not (m >> bit) & 1:
+                continue
+            blk = coef[k * 16:(k + 1) * 16]
+            k += 1
+            if bit < 16:
+                out[mb, bit * 16:(bit + 1) * 16] = blk
+            elif bit == 16:
+                out[mb, 256:272] = blk
+            elif bit == 17:
+                out[mb, 272:280] = blk[:8]
+            else:
+                j = bit - 18
+                out[mb, 280 + j * 16:280 + (j + 1) * 16] = blk
+    return out
