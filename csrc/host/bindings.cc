@@ -15,6 +15,7 @@
 #include "cavlc_writer.h"
 #include "cpu_encoder.h"
 #include "h264_decoder.h"
+#include "hevc_codec.h"
 #include "lowres.h"
 
 namespace mivc {
@@ -181,6 +182,54 @@ py::dict segment_to_dict(ParsedSegment& seg) {
   return d;
 }
 
+hevc::HevcConfig hevc_cfg_from(const py::dict& d) {
+  hevc::HevcConfig c;
+  c.width = dget<int>(d, "width", 0);
+  c.height = dget<int>(d, "height", 0);
+  c.bit_depth = dget<int>(d, "bit_depth", 8);
+  c.fps = dget<double>(d, "fps", 30.0);
+  c.sao = dget<int>(d, "sao", 1);
+  c.deblock = dget<int>(d, "deblock", 1);
+  c.max_merge = dget<int>(d, "max_merge", 5);
+  if (c.width <= 0 || c.height <= 0 || (c.width & 1) || (c.height & 1)) throw std::runtime_error("HEVC: bad size");
+  if (c.bit_depth != 8 && c.bit_depth != 10) throw std::runtime_error("HEVC: bit_depth must be 8 or 10");
+  if (c.max_merge < 1 || c.max_merge > 5) throw std::runtime_error("HEVC: max_merge in 1..5");
+  return c;
+}
+
+template <class T>
+py::array_t<T> to_array(const std::vector<T>& v, std::vector<py::ssize_t> shape) {
+  py::array_t<T> a(shape);
+  std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(T));
+  return a;
+}
+
+py::dict hevc_picture_to_dict(const hevc::HevcPicture& p) {
+  py::dict d;
+  d["width"] = p.width;
+  d["height"] = p.height;
+  d["coded_width"] = p.coded_width;
+  d["coded_height"] = p.coded_height;
+  d["bit_depth"] = p.bit_depth;
+  d["poc"] = p.poc;
+  d["idr"] = p.idr;
+  d["slice_type"] = p.slice_type;
+  d["qp"] = p.qp;
+  const py::ssize_t H = p.coded_height, W = p.coded_width;
+  d["y"] = to_array(p.y, {H, W});
+  d["u"] = to_array(p.u, {H / 2, W / 2});
+  d["v"] = to_array(p.v, {H / 2, W / 2});
+  std::vector<uint8_t> ctu(p.ctu.size() * sizeof(hevc::CtuInfo)), cu(p.cu.size() * sizeof(hevc::CuInfo));
+  if (!ctu.empty()) std::memcpy(ctu.data(), p.ctu.data(), ctu.size());
+  if (!cu.empty()) std::memcpy(cu.data(), p.cu.data(), cu.size());
+  d["ctu"] = to_array(ctu, {static_cast<py::ssize_t>(p.ctu.size()), static_cast<py::ssize_t>(sizeof(hevc::CtuInfo))});
+  d["cu"] = to_array(cu, {static_cast<py::ssize_t>(p.cu.size()), static_cast<py::ssize_t>(sizeof(hevc::CuInfo))});
+  d["coef_y"] = to_array(p.coef_y, {H, W});
+  d["coef_cb"] = to_array(p.coef_cb, {H / 2, W / 2});
+  d["coef_cr"] = to_array(p.coef_cr, {H / 2, W / 2});
+  return d;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_host, m) {
@@ -227,6 +276,13 @@ PYBIND11_MODULE(_host, m) {
     else if (name == "inter_cbp") row(kGolombToInterCbp, 48);
     else if (name == "zigzag") row(kZigzag4x4, 16);
     else if (name == "lambda") out.emplace_back(kLambda, kLambda + 52);
+    else if (name == "hevc_dct32") {
+      for (int k = 0; k < 32; ++k) {
+        std::vector<int> r(32);
+        for (int n = 0; n < 32; ++n) r[n] = hevc::dct_coef(k, n);
+        out.push_back(r);
+      }
+    }
     else throw std::runtime_error("unknown table " + name);
     return out;
   });
@@ -313,6 +369,60 @@ PYBIND11_MODULE(_host, m) {
         return out;
       },
       py::arg("segments"), py::arg("threads") = 1);
+
+  // ---------------------------------------------------------------- HEVC
+  m.def("hevc_parameter_sets", [](const py::dict& cfg) { return to_bytes(hevc::hevc_parameter_sets(hevc_cfg_from(cfg))); });
+  m.def(
+      "hevc_write_slice",
+      [](const py::dict& cfg, const py::dict& fp, py::array_t<uint8_t, py::array::c_style> ctu,
+         py::array_t<uint8_t, py::array::c_style> cu, py::array_t<int16_t, py::array::c_style> cy,
+         py::array_t<int16_t, py::array::c_style> cb, py::array_t<int16_t, py::array::c_style> cr) {
+        hevc::HevcConfig c = hevc_cfg_from(cfg);
+        hevc::HevcFrameParams f;
+        f.idr = dget<int>(fp, "idr", 1);
+        f.poc = dget<int>(fp, "poc", 0);
+        f.qp = dget<int>(fp, "qp", 30);
+        f.slice_type = f.idr ? 2 : dget<int>(fp, "slice_type", 1);
+        const py::ssize_t nctu = static_cast<py::ssize_t>(c.wctb()) * c.hctb();
+        const py::ssize_t W = c.coded_width(), H = c.coded_height();
+        if (ctu.size() != nctu * 32) throw std::runtime_error("ctu records: wrong size");
+        if (cu.size() != nctu * hevc::kCusPerCtb * 8) throw std::runtime_error("cu records: wrong size");
+        if (cy.size() != W * H || cb.size() != W * H / 4 || cr.size() != W * H / 4)
+          throw std::runtime_error("coefficient planes: wrong size");
+        hevc::HevcSliceStats st;
+        std::vector<uint8_t> nal;
+        {
+          py::gil_scoped_release rel;
+          nal = hevc::hevc_write_slice(c, f, reinterpret_cast<const hevc::CtuInfo*>(ctu.data()),
+                                       reinterpret_cast<const hevc::CuInfo*>(cu.data()), cy.data(), cb.data(), cr.data(),
+                                       &st);
+        }
+        py::dict stats;
+        stats["bins"] = st.bins;
+        stats["bytes"] = st.bytes;
+        stats["intra_cus"] = st.intra_cus;
+        stats["inter_cus"] = st.inter_cus;
+        stats["skip_cus"] = st.skip_cus;
+        stats["merge_cus"] = st.merge_cus;
+        return py::make_tuple(to_bytes(nal), stats);
+      },
+      py::arg("cfg"), py::arg("frame"), py::arg("ctu"), py::arg("cu"), py::arg("coef_y"), py::arg("coef_cb"),
+      py::arg("coef_cr"));
+  m.def(
+      "hevc_decode",
+      [](py::bytes data, bool skip_filters) {
+        std::string s = data;
+        hevc::HevcDecoder dec;
+        dec.set_skip_loop_filters(skip_filters);
+        {
+          py::gil_scoped_release rel;
+          dec.decode(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+        }
+        py::list out;
+        for (const hevc::HevcPicture& p : dec.out()) out.append(hevc_picture_to_dict(p));
+        return out;
+      },
+      py::arg("data"), py::arg("skip_filters") = false);
 
   py::class_<CpuEncoder>(m, "CpuEncoder")
       .def(py::init([](const py::dict& cfg) { return new CpuEncoder(cfg_from(cfg)); }))

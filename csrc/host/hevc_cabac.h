@@ -1,0 +1,250 @@
+// HEVC CABAC arithmetic coding engines (clause 9.3), encoder and decoder.
+//
+// The encoder follows the low/range formulation with deferred carry handling
+// (outstanding 0xFF bytes); the decoder is the normative 9-bit offset engine.  Both
+// use the context tables of csrc/common/hevc_tables.h.
+#pragma once
+#include <cstdint>
+#include <stdexcept>
+#include <vector>
+
+#include "../common/hevc_tables.h"
+#include "bitstream.h"
+
+namespace mivc {
+namespace hevc {
+
+struct CtxState {
+  uint8_t state = 0;
+  uint8_t mps = 0;
+};
+
+// 9.3.2.2: contexts initialised for a slice of the given initType and SliceQpY
+inline void init_contexts(CtxState* ctx, int init_type, int slice_qp) {
+  const int qp = slice_qp < 0 ? 0 : (slice_qp > 51 ? 51 : slice_qp);
+  for (int i = 0; i < kNumCtx; ++i) {
+    const int v = kCtxInit[init_type][i];
+    const int m = (v >> 4) * 5 - 45, n = ((v & 15) << 3) - 16;
+    int pre = ((m * qp) >> 4) + n;
+    pre = pre < 1 ? 1 : (pre > 126 ? 126 : pre);
+    if (pre <= 63) {
+      ctx[i].state = static_cast<uint8_t>(63 - pre);
+      ctx[i].mps = 0;
+    } else {
+      ctx[i].state = static_cast<uint8_t>(pre - 64);
+      ctx[i].mps = 1;
+    }
+  }
+}
+
+class CabacEncoder {
+ public:
+  explicit CabacEncoder(BitWriter& bw) : bw_(bw) {}
+
+  void start() {
+    low_ = 0;
+    range_ = 510;
+    bits_left_ = 23;
+    num_buffered_ = 0;
+    buffered_ = 0xFF;
+    bins_ = 0;
+  }
+
+  void encode(int bin, CtxState& c) {
+    ++bins_;
+    const uint32_t lps = kRangeLps[c.state][(range_ >> 6) & 3];
+    range_ -= lps;
+    if (bin != c.mps) {
+      const int nb = renorm_bits(lps);
+      low_ = (low_ + range_) << nb;
+      range_ = lps << nb;
+      if (c.state == 0) c.mps = static_cast<uint8_t>(1 - c.mps);
+      c.state = kTransIdxLps[c.state];
+      bits_left_ -= nb;
+    } else {
+      if (c.state < 62) ++c.state;
+      if (range_ >= 256) return;
+      low_ <<= 1;
+      range_ <<= 1;
+      --bits_left_;
+    }
+    if (bits_left_ < 12) write_out();
+  }
+
+  void bypass(int bin) {
+    ++bins_;
+    low_ <<= 1;
+    if (bin) low_ += range_;
+    if (--bits_left_ < 12) write_out();
+  }
+
+  // n bypass bins, most significant first (n <= 16 per call keeps low_ in range)
+  void bypass_bits(uint32_t v, int n) {
+    while (n > 8) {
+      n -= 8;
+      bypass_chunk((v >> n) & 255u, 8);
+    }
+    if (n > 0) bypass_chunk(v & ((1u << n) - 1u), n);
+  }
+
+  void terminate(int bin) {
+    ++bins_;
+    range_ -= 2;
+    if (bin) {
+      low_ += range_;
+      low_ <<= 7;
+      range_ = 2 << 7;
+      bits_left_ -= 7;
+    } else if (range_ >= 256) {
+      return;
+    } else {
+      low_ <<= 1;
+      range_ <<= 1;
+      --bits_left_;
+    }
+    if (bits_left_ < 12) write_out();
+  }
+
+  // flush after the terminating bin of the slice (end_of_slice_segment_flag == 1)
+  void finish() {
+    if ((low_ >> (32 - bits_left_)) != 0) {
+      bw_.put(buffered_ + 1, 8);
+      while (num_buffered_ > 1) {
+        bw_.put(0x00, 8);
+        --num_buffered_;
+      }
+      low_ -= 1u << (32 - bits_left_);
+    } else {
+      if (num_buffered_ > 0) bw_.put(buffered_, 8);
+      while (num_buffered_ > 1) {
+        bw_.put(0xFF, 8);
+        --num_buffered_;
+      }
+    }
+    bw_.put(low_ >> 8, 24 - bits_left_);
+  }
+
+  uint64_t bins() const { return bins_; }
+
+ private:
+  static int renorm_bits(uint32_t lps) {
+    int n = 0;
+    while ((lps << n) < 256) ++n;
+    return n;
+  }
+  void bypass_chunk(uint32_t v, int n) {
+    bins_ += n;
+    low_ <<= n;
+    low_ += range_ * v;
+    bits_left_ -= n;
+    if (bits_left_ < 12) write_out();
+  }
+  void write_out() {
+    const uint32_t lead = low_ >> (24 - bits_left_);
+    bits_left_ += 8;
+    low_ &= 0xFFFFFFFFu >> bits_left_;
+    if (lead == 0xFF) {
+      ++num_buffered_;
+    } else if (num_buffered_ > 0) {
+      const uint32_t carry = lead >> 8;
+      bw_.put(buffered_ + carry, 8);
+      buffered_ = lead & 0xFF;
+      const uint32_t fill = (0xFF + carry) & 0xFF;
+      while (num_buffered_ > 1) {
+        bw_.put(fill, 8);
+        --num_buffered_;
+      }
+    } else {
+      num_buffered_ = 1;
+      buffered_ = lead;
+    }
+  }
+
+  BitWriter& bw_;
+  uint32_t low_ = 0, range_ = 510;
+  int bits_left_ = 23;
+  int num_buffered_ = 0;
+  uint32_t buffered_ = 0xFF;
+  uint64_t bins_ = 0;
+};
+
+class CabacDecoder {
+ public:
+  CabacDecoder(const uint8_t* p, size_t n, size_t byte_pos) : p_(p), n_(n), pos_(byte_pos * 8) {}
+
+  void start() {
+    range_ = 510;
+    offset_ = read_bits(9);
+  }
+
+  int decode(CtxState& c) {
+    const uint32_t lps = kRangeLps[c.state][(range_ >> 6) & 3];
+    range_ -= lps;
+    int bin;
+    if (offset_ >= range_) {
+      bin = 1 - c.mps;
+      offset_ -= range_;
+      range_ = lps;
+      if (c.state == 0) c.mps = static_cast<uint8_t>(1 - c.mps);
+      c.state = kTransIdxLps[c.state];
+    } else {
+      bin = c.mps;
+      if (c.state < 62) ++c.state;
+    }
+    while (range_ < 256) {
+      range_ <<= 1;
+      offset_ = (offset_ << 1) | read_bit();
+    }
+    return bin;
+  }
+
+  int bypass() {
+    offset_ = (offset_ << 1) | read_bit();
+    if (offset_ >= range_) {
+      offset_ -= range_;
+      return 1;
+    }
+    return 0;
+  }
+
+  uint32_t bypass_bits(int n) {
+    uint32_t v = 0;
+    for (int i = 0; i < n; ++i) v = (v << 1) | static_cast<uint32_t>(bypass());
+    return v;
+  }
+
+  int terminate() {
+    range_ -= 2;
+    if (offset_ >= range_) return 1;
+    while (range_ < 256) {
+      range_ <<= 1;
+      offset_ = (offset_ << 1) | read_bit();
+    }
+    return 0;
+  }
+
+ private:
+  uint32_t read_bit() {
+    if (pos_ >= n_ * 8) {
+      ++pos_;
+      if (pos_ > n_ * 8 + 64) throw std::runtime_error("CABAC: read past the end of the slice data");
+      return 0;
+    }
+    const uint32_t b = (p_[pos_ >> 3] >> (7 - (pos_ & 7))) & 1u;
+    ++pos_;
+    return b;
+  }
+  uint32_t read_bits(int n) {
+    uint32_t v = 0;
+    for (int i = 0; i < n; ++i) v = (v << 1) | read_bit();
+    return v;
+  }
+
+  const uint8_t* p_;
+  size_t n_;
+  size_t pos_;
+  uint32_t range_ = 510, offset_ = 0;
+};
+
+}  // namespace hevc
+}  // namespace mivc

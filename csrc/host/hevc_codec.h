@@ -1,0 +1,85 @@
+// HEVC (H.265) Main / Main 10 bitstream layer: parameter sets, slice headers and the
+// CABAC coding of CTUs from decision records (hevc_writer.cc), plus an independent
+// decoder (hevc_decoder.cc) that is the conformance oracle of the test-suite.
+//
+// Coding tools used by this encoder: 32x32 CTBs, CU quadtree
+// 32/16/8, PART_2Nx2N, TU = CU (max_transform_hierarchy_depth 0), 35 intra modes
+// with DM chroma, P slices with one reference picture (merge/skip + AMVP), flat
+// quantisation with one QP per slice, deblocking and SAO, no tiles/WPP (every
+// picture is one slice; pictures entropy-code in parallel on host threads).
+//
+// Reference parity: `-vcodec libx265 -crf 26` (server.go:67-68, client.go:115).
+#pragma once
+#include <cstdint>
+#include <memory>
+#include <vector>
+
+#include "../common/hevc_tables.h"
+
+namespace mivc {
+namespace hevc {
+
+struct HevcConfig {
+  int width = 0, height = 0;   // display size
+  int bit_depth = 8;           // 8 (Main) or 10 (Main 10)
+  double fps = 30.0;
+  int sao = 1;
+  int deblock = 1;
+  int max_merge = 5;
+  int coded_width() const { return (width + kCtb - 1) / kCtb * kCtb; }
+  int coded_height() const { return (height + kCtb - 1) / kCtb * kCtb; }
+  int wctb() const { return coded_width() / kCtb; }
+  int hctb() const { return coded_height() / kCtb; }
+};
+
+struct HevcFrameParams {
+  int idr = 1;
+  int poc = 0;          // picture order count (decode order == output order)
+  int qp = 30;          // SliceQpY
+  int slice_type = 2;   // 2 = I, 1 = P
+};
+
+struct HevcSliceStats {
+  uint64_t bins = 0;
+  uint64_t bytes = 0;
+  int intra_cus = 0, inter_cus = 0, skip_cus = 0, merge_cus = 0;
+};
+
+// VPS + SPS + PPS as Annex-B NAL units
+std::vector<uint8_t> hevc_parameter_sets(const HevcConfig& cfg);
+
+// One slice NAL (Annex-B) for a whole picture.  ctu: [wctb*hctb]; cu: [wctb*hctb*16]
+// (z-order granules); coef planes sized like the coded picture (luma) / half (chroma).
+std::vector<uint8_t> hevc_write_slice(const HevcConfig& cfg, const HevcFrameParams& fp, const CtuInfo* ctu,
+                                      const CuInfo* cu, const int16_t* coef_y, const int16_t* coef_cb,
+                                      const int16_t* coef_cr, HevcSliceStats* stats);
+
+struct HevcPicture {
+  int width = 0, height = 0;            // cropped (display) size
+  int coded_width = 0, coded_height = 0;
+  int bit_depth = 8;
+  int poc = 0, idr = 0, slice_type = 2, qp = 0;
+  std::vector<uint16_t> y, u, v;        // coded-size planes
+  // parse records (the encoder's decision format, see hevc_tables.h)
+  std::vector<CtuInfo> ctu;
+  std::vector<CuInfo> cu;
+  std::vector<int16_t> coef_y, coef_cb, coef_cr;
+};
+
+class HevcDecoder {
+ public:
+  HevcDecoder();
+  ~HevcDecoder();
+  void decode(const uint8_t* data, size_t n);
+  std::vector<HevcPicture>& out() { return out_; }
+  void set_skip_loop_filters(bool v) { skip_filters_ = v; }  // tests: unfiltered reconstruction
+  struct Impl;
+
+ private:
+  std::unique_ptr<Impl> impl_;
+  std::vector<HevcPicture> out_;
+  bool skip_filters_ = false;
+};
+
+}  // namespace hevc
+}  // namespace mivc

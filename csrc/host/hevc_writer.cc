@@ -1,0 +1,766 @@
+// HEVC parameter sets, slice header and CABAC slice data from decision records.
+// Clause numbers refer to ITU-T H.265.  See hevc_codec.h for the coding-tool subset.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+
+#include "bitstream.h"
+#include "hevc_cabac.h"
+#include "hevc_codec.h"
+
+namespace mivc {
+namespace hevc {
+
+namespace {
+
+enum NalType { NAL_TRAIL_R = 1, NAL_IDR_W_RADL = 19, NAL_VPS = 32, NAL_SPS = 33, NAL_PPS = 34 };
+
+void append_hevc_nal(std::vector<uint8_t>& out, int type, const std::vector<uint8_t>& rbsp) {
+  static const uint8_t sc[4] = {0, 0, 0, 1};
+  out.insert(out.end(), sc, sc + 4);
+  out.push_back(static_cast<uint8_t>((type & 63) << 1));  // forbidden 0, type, layer id 0 (high bit)
+  out.push_back(1);                                       // layer id low bits 0, temporal_id_plus1 = 1
+  int zeros = 0;
+  for (uint8_t b : rbsp) {
+    if (zeros >= 2 && b <= 3) {
+      out.push_back(3);
+      zeros = 0;
+    }
+    out.push_back(b);
+    zeros = (b == 0) ? zeros + 1 : 0;
+  }
+}
+
+int level_idc(const HevcConfig& c) {
+  const int64_t ps = static_cast<int64_t>(c.coded_width()) * c.coded_height();
+  const double sps = ps * c.fps;
+  // Table A.8 (MaxLumaPs, MaxLumaSr); level_idc = 30 * level
+  if (ps <= 552960 && sps <= 16588800) return 93;      // 3.1
+  if (ps <= 2228224 && sps <= 66846720) return 120;    // 4
+  if (ps <= 2228224 && sps <= 133693440) return 123;   // 4.1
+  if (ps <= 8912896 && sps <= 267386880) return 150;   // 5
+  if (ps <= 8912896 && sps <= 534773760) return 153;   // 5.1
+  if (ps <= 35651584 && sps <= 1069547520) return 180; // 6
+  if (ps <= 35651584 && sps <= 2139095040) return 183; // 6.1
+  return 186;                                          // 6.2
+}
+
+void profile_tier_level(BitWriter& bw, const HevcConfig& c) {
+  const int profile = c.bit_depth > 8 ? 2 : 1;  // Main 10 / Main
+  bw.put(0, 2);            // general_profile_space
+  bw.put(0, 1);            // general_tier_flag
+  bw.put(profile, 5);      // general_profile_idc
+  for (int j = 0; j < 32; ++j) bw.put_bit(j == profile || (profile == 1 && j == 2));
+  bw.put_bit(1);           // general_progressive_source_flag
+  bw.put_bit(0);           // general_interlaced_source_flag
+  bw.put_bit(0);           // general_non_packed_constraint_flag
+  bw.put_bit(1);           // general_frame_only_constraint_flag
+  bw.put(0, 32);           // general_reserved_zero_43bits (+ inbld flag)
+  bw.put(0, 12);
+  bw.put(level_idc(c), 8); // general_level_idc
+}
+
+}  // namespace
+
+std::vector<uint8_t> hevc_parameter_sets(const HevcConfig& c) {
+  std::vector<uint8_t> out;
+  {  // 7.3.2.1 video_parameter_set_rbsp
+    BitWriter bw;
+    bw.put(0, 4);        // vps_video_parameter_set_id
+    bw.put_bit(1);       // vps_base_layer_internal_flag
+    bw.put_bit(1);       // vps_base_layer_available_flag
+    bw.put(0, 6);        // vps_max_layers_minus1
+    bw.put(0, 3);        // vps_max_sub_layers_minus1
+    bw.put_bit(1);       // vps_temporal_id_nesting_flag
+    bw.put(0xFFFF, 16);  // vps_reserved_0xffff_16bits
+    profile_tier_level(bw, c);
+    bw.put_bit(1);       // vps_sub_layer_ordering_info_present_flag
+    bw.put_ue(1);        // vps_max_dec_pic_buffering_minus1
+    bw.put_ue(0);        // vps_max_num_reorder_pics
+    bw.put_ue(0);        // vps_max_latency_increase_plus1
+    bw.put(0, 6);        // vps_max_layer_id
+    bw.put_ue(0);        // vps_num_layer_sets_minus1
+    bw.put_bit(0);       // vps_timing_info_present_flag
+    bw.put_bit(0);       // vps_extension_flag
+    bw.trailing();
+    append_hevc_nal(out, NAL_VPS, bw.bytes());
+  }
+  {  // 7.3.2.2 seq_parameter_set_rbsp
+    BitWriter bw;
+    bw.put(0, 4);        // sps_video_parameter_set_id
+    bw.put(0, 3);        // sps_max_sub_layers_minus1
+    bw.put_bit(1);       // sps_temporal_id_nesting_flag
+    profile_tier_level(bw, c);
+    bw.put_ue(0);        // sps_seq_parameter_set_id
+    bw.put_ue(1);        // chroma_format_idc 4:2:0
+    bw.put_ue(c.coded_width());
+    bw.put_ue(c.coded_height());
+    const int crop_r = (c.coded_width() - c.width) / 2, crop_b = (c.coded_height() - c.height) / 2;
+    bw.put_bit(crop_r || crop_b);  // conformance_window_flag
+    if (crop_r || crop_b) {
+      bw.put_ue(0);
+      bw.put_ue(crop_r);
+      bw.put_ue(0);
+      bw.put_ue(crop_b);
+    }
+    bw.put_ue(c.bit_depth - 8);  // bit_depth_luma_minus8
+    bw.put_ue(c.bit_depth - 8);  // bit_depth_chroma_minus8
+    bw.put_ue(8 - 4);            // log2_max_pic_order_cnt_lsb_minus4 (8 bits)
+    bw.put_bit(1);               // sps_sub_layer_ordering_info_present_flag
+    bw.put_ue(1);                // sps_max_dec_pic_buffering_minus1
+    bw.put_ue(0);                // sps_max_num_reorder_pics
+    bw.put_ue(0);                // sps_max_latency_increase_plus1
+    bw.put_ue(kMinCbLog2 - 3);   // log2_min_luma_coding_block_size_minus3
+    bw.put_ue(kCtbLog2 - kMinCbLog2);  // log2_diff_max_min_luma_coding_block_size
+    bw.put_ue(0);                // log2_min_luma_transform_block_size_minus2 (4x4)
+    bw.put_ue(3);                // log2_diff_max_min_luma_transform_block_size (32x32)
+    bw.put_ue(0);                // max_transform_hierarchy_depth_inter
+    bw.put_ue(0);                // max_transform_hierarchy_depth_intra
+    bw.put_bit(0);               // scaling_list_enabled_flag
+    bw.put_bit(0);               // amp_enabled_flag
+    bw.put_bit(c.sao ? 1 : 0);   // sample_adaptive_offset_enabled_flag
+    bw.put_bit(0);               // pcm_enabled_flag
+    bw.put_ue(1);                // num_short_term_ref_pic_sets
+    // st_ref_pic_set(0): the previous picture
+    bw.put_ue(1);                // num_negative_pics
+    bw.put_ue(0);                // num_positive_pics
+    bw.put_ue(0);                // delta_poc_s0_minus1
+    bw.put_bit(1);               // used_by_curr_pic_s0_flag
+    bw.put_bit(0);               // long_term_ref_pics_present_flag
+    bw.put_bit(0);               // sps_temporal_mvp_enabled_flag
+    bw.put_bit(1);               // strong_intra_smoothing_enabled_flag
+    bw.put_bit(0);               // vui_parameters_present_flag
+    bw.put_bit(0);               // sps_extension_present_flag
+    bw.trailing();
+    append_hevc_nal(out, NAL_SPS, bw.bytes());
+  }
+  {  // 7.3.2.3 pic_parameter_set_rbsp
+    BitWriter bw;
+    bw.put_ue(0);   // pps_pic_parameter_set_id
+    bw.put_ue(0);   // pps_seq_parameter_set_id
+    bw.put_bit(0);  // dependent_slice_segments_enabled_flag
+    bw.put_bit(0);  // output_flag_present_flag
+    bw.put(0, 3);   // num_extra_slice_header_bits
+    bw.put_bit(0);  // sign_data_hiding_enabled_flag
+    bw.put_bit(0);  // cabac_init_present_flag
+    bw.put_ue(0);   // num_ref_idx_l0_default_active_minus1
+    bw.put_ue(0);   // num_ref_idx_l1_default_active_minus1
+    bw.put_se(0);   // init_qp_minus26
+    bw.put_bit(0);  // constrained_intra_pred_flag
+    bw.put_bit(0);  // transform_skip_enabled_flag
+    bw.put_bit(0);  // cu_qp_delta_enabled_flag
+    bw.put_se(0);   // pps_cb_qp_offset
+    bw.put_se(0);   // pps_cr_qp_offset
+    bw.put_bit(0);  // pps_slice_chroma_qp_offsets_present_flag
+    bw.put_bit(0);  // weighted_pred_flag
+    bw.put_bit(0);  // weighted_bipred_flag
+    bw.put_bit(0);  // transquant_bypass_enabled_flag
+    bw.put_bit(0);  // tiles_enabled_flag
+    bw.put_bit(0);  // entropy_coding_sync_enabled_flag
+    bw.put_bit(0);  // pps_loop_filter_across_slices_enabled_flag
+    bw.put_bit(c.deblock ? 0 : 1);  // deblocking_filter_control_present_flag
+    if (!c.deblock) {
+      bw.put_bit(0);  // deblocking_filter_override_enabled_flag
+      bw.put_bit(1);  // pps_deblocking_filter_disabled_flag
+    }
+    bw.put_bit(0);  // pps_scaling_list_data_present_flag
+    bw.put_bit(0);  // lists_modification_present_flag
+    bw.put_ue(0);   // log2_parallel_merge_level_minus2
+    bw.put_bit(0);  // slice_segment_header_extension_present_flag
+    bw.put_bit(0);  // pps_extension_present_flag
+    bw.trailing();
+    append_hevc_nal(out, NAL_PPS, bw.bytes());
+  }
+  return out;
+}
+
+namespace {
+
+// ------------------------------------------------------------------ slice writer state
+struct Writer {
+  const HevcConfig& c;
+  const HevcFrameParams& fp;
+  const CtuInfo* ctu;
+  const CuInfo* cu;
+  const int16_t* coef[3];
+  CabacEncoder& e;
+  CtxState ctx[kNumCtx];
+  HevcSliceStats st;
+  int W, H, wctb, hctb, w8, h8;
+  bool pslice;
+  // per 8x8 granule of the picture (raster): state of already-coded CUs
+  std::vector<int8_t> depth, skip, pred, mode;
+  std::vector<int16_t> mvx, mvy;
+  std::vector<uint8_t> coded;
+
+  Writer(const HevcConfig& cfg, const HevcFrameParams& f, const CtuInfo* ct, const CuInfo* cu_, const int16_t* cy,
+         const int16_t* cb, const int16_t* cr, CabacEncoder& enc)
+      : c(cfg), fp(f), ctu(ct), cu(cu_), e(enc) {
+    coef[0] = cy;
+    coef[1] = cb;
+    coef[2] = cr;
+    W = c.coded_width();
+    H = c.coded_height();
+    wctb = c.wctb();
+    hctb = c.hctb();
+    w8 = W / 8;
+    h8 = H / 8;
+    pslice = fp.slice_type == 1;
+    const size_t n = static_cast<size_t>(w8) * h8;
+    depth.assign(n, 0);
+    skip.assign(n, 0);
+    pred.assign(n, 0);
+    mode.assign(n, 1);
+    mvx.assign(n, 0);
+    mvy.assign(n, 0);
+    coded.assign(n, 0);
+    init_contexts(ctx, pslice ? 1 : 0, fp.qp);
+  }
+
+  size_t g(int x, int y) const { return static_cast<size_t>(y >> 3) * w8 + (x >> 3); }
+  bool inside(int x, int y) const { return x >= 0 && y >= 0 && x < W && y < H; }
+  // 6.4.1 z-scan availability at 8x8 granularity (the granule is coded iff already visited)
+  bool avail(int x, int y) const { return inside(x, y) && coded[g(x, y)]; }
+
+  const CuInfo& cu_at(int x, int y) const {
+    const int ci = (y >> kCtbLog2) * wctb + (x >> kCtbLog2);
+    return cu[static_cast<size_t>(ci) * kCusPerCtb + zorder8((x & (kCtb - 1)) >> 3, (y & (kCtb - 1)) >> 3)];
+  }
+
+  // ---------------------------------------------------------------- SAO (7.3.8.3)
+  static bool same_sao(const CtuInfo& a, const CtuInfo& b) {
+    for (int k = 0; k < 2; ++k)
+      if (a.sao_type[k] != b.sao_type[k] || (a.sao_type[k] == 2 && a.sao_class[k] != b.sao_class[k])) return false;
+    for (int ci = 0; ci < 3; ++ci) {
+      const int t = a.sao_type[ci ? 1 : 0];
+      if (t == 0) continue;
+      if (t == 1 && a.sao_band[ci] != b.sao_band[ci]) return false;
+      for (int i = 0; i < 4; ++i)
+        if (a.sao_off[ci][i] != b.sao_off[ci][i]) return false;
+    }
+    return true;
+  }
+
+  void write_sao(int rx, int ry) {
+    const CtuInfo& t = ctu[ry * wctb + rx];
+    if (rx > 0 && same_sao(t, ctu[ry * wctb + rx - 1])) {
+      e.encode(1, ctx[CTX_SAO_MERGE]);
+      return;
+    }
+    if (rx > 0) e.encode(0, ctx[CTX_SAO_MERGE]);
+    if (ry > 0 && same_sao(t, ctu[(ry - 1) * wctb + rx])) {
+      e.encode(1, ctx[CTX_SAO_MERGE]);
+      return;
+    }
+    if (ry > 0) e.encode(0, ctx[CTX_SAO_MERGE]);
+    const int cmax = (1 << (std::min(c.bit_depth, 10) - 5)) - 1;
+    for (int ci = 0; ci < 3; ++ci) {
+      const int type = t.sao_type[ci ? 1 : 0];
+      if (ci < 2) {  // sao_type_idx_luma / _chroma: TR cMax 2, first bin context coded
+        if (type == 0) {
+          e.encode(0, ctx[CTX_SAO_TYPE]);
+        } else {
+          e.encode(1, ctx[CTX_SAO_TYPE]);
+          e.bypass(type == 2);
+        }
+      }
+      if (type == 0) continue;
+      for (int i = 0; i < 4; ++i) {
+        int a = std::abs(static_cast<int>(t.sao_off[ci][i]));
+        if (a > cmax) throw std::runtime_error("SAO offset out of range");
+        for (int k = 0; k < a; ++k) e.bypass(1);  // TR, bypass
+        if (a < cmax) e.bypass(0);
+      }
+      if (type == 1) {
+        for (int i = 0; i < 4; ++i)
+          if (t.sao_off[ci][i] != 0) e.bypass(t.sao_off[ci][i] < 0);
+        e.bypass_bits(t.sao_band[ci] & 31, 5);
+      } else {
+        if (t.sao_off[ci][0] < 0 || t.sao_off[ci][1] < 0 || t.sao_off[ci][2] > 0 || t.sao_off[ci][3] > 0)
+          throw std::runtime_error("edge-offset signs violate 7.4.9.3.2");
+        if (ci < 2) e.bypass_bits(t.sao_class[ci] & 3, 2);
+      }
+    }
+  }
+
+  // ---------------------------------------------------------------- residual coding (7.3.8.11)
+  void write_last(int v, int log2, int cidx, int ctx_base) {
+    static const int grp[32] = {0, 1, 2, 3, 4, 4, 5, 5, 6, 6, 6, 6, 7, 7, 7, 7,
+                                8, 8, 8, 8, 8, 8, 8, 8, 9, 9, 9, 9, 9, 9, 9, 9};
+    const int prefix = grp[v];
+    const int cmax = (log2 << 1) - 1;
+    int off, shift;
+    if (cidx == 0) {
+      off = 3 * (log2 - 2) + ((log2 - 1) >> 2);
+      shift = (log2 + 1) >> 2;
+    } else {
+      off = 15;
+      shift = log2 - 2;
+    }
+    for (int i = 0; i < prefix; ++i) e.encode(1, ctx[ctx_base + off + (i >> shift)]);
+    if (prefix < cmax) e.encode(0, ctx[ctx_base + off + (prefix >> shift)]);
+  }
+  void write_last_suffix(int v) {
+    static const int grp[32] = {0, 1, 2, 3, 4, 4, 5, 5, 6, 6, 6, 6, 7, 7, 7, 7,
+                                8, 8, 8, 8, 8, 8, 8, 8, 9, 9, 9, 9, 9, 9, 9, 9};
+    static const int mn[10] = {0, 1, 2, 3, 4, 6, 8, 12, 16, 24};
+    const int prefix = grp[v];
+    if (prefix > 3) e.bypass_bits(v - mn[prefix], (prefix >> 1) - 1);
+  }
+
+  void write_remaining(int v, int rice) {
+    if (v < (3 << rice)) {
+      const int len = v >> rice;
+      e.bypass_bits((1u << (len + 1)) - 2, len + 1);
+      e.bypass_bits(v & ((1 << rice) - 1), rice);
+    } else {
+      int len = rice;
+      int s = v - (3 << rice);
+      while (s >= (1 << len)) {
+        s -= 1 << len;
+        ++len;
+      }
+      const int ones = 3 + len + 1 - rice;
+      // ones-1 ones and a zero, then len bits (may exceed 16 in total: split)
+      for (int i = 0; i < ones - 1; ++i) e.bypass(1);
+      e.bypass(0);
+      e.bypass_bits(static_cast<uint32_t>(s), len);
+    }
+  }
+
+  void write_residual(const int16_t* blk, int stride, int log2, int cidx, int scan_idx) {
+    const int log2sb = log2 - 2, nsb = 1 << log2sb;
+    int sbx[64], sby[64], px[16], py[16];
+    for (int i = 0; i < nsb * nsb; ++i) {
+      const int p = scan_pos(scan_idx, log2sb, i);
+      sbx[i] = p & 255;
+      sby[i] = p >> 8;
+    }
+    for (int i = 0; i < 16; ++i) {
+      const int p = scan_pos(scan_idx, 2, i);
+      px[i] = p & 255;
+      py[i] = p >> 8;
+    }
+    auto at = [&](int i, int p) { return static_cast<int>(blk[(sby[i] * 4 + py[p]) * stride + sbx[i] * 4 + px[p]]); };
+    int last_i = -1, last_p = -1;
+    for (int i = nsb * nsb - 1; i >= 0 && last_i < 0; --i)
+      for (int p = 15; p >= 0; --p)
+        if (at(i, p) != 0) {
+          last_i = i;
+          last_p = p;
+          break;
+        }
+    if (last_i < 0) throw std::runtime_error("residual_coding of an all-zero block");
+    int lx = sbx[last_i] * 4 + px[last_p], ly = sby[last_i] * 4 + py[last_p];
+    if (scan_idx == 2) std::swap(lx, ly);
+    write_last(lx, log2, cidx, CTX_LAST_X);
+    write_last(ly, log2, cidx, CTX_LAST_Y);
+    write_last_suffix(lx);
+    write_last_suffix(ly);
+
+    uint8_t csbf[8][8] = {};
+    int c1 = 1;
+    bool first_sb = true;
+    for (int i = last_i; i >= 0; --i) {
+      const int xs = sbx[i], ys = sby[i];
+      bool nonzero = false;
+      for (int p = 0; p < 16; ++p) nonzero |= at(i, p) != 0;
+      bool infer_dc = false;
+      if (i < last_i && i > 0) {
+        int cs = 0;
+        if (xs < nsb - 1) cs += csbf[xs + 1][ys];
+        if (ys < nsb - 1) cs += csbf[xs][ys + 1];
+        e.encode(nonzero, ctx[CTX_CSBF + std::min(cs, 1) + (cidx ? 2 : 0)]);
+        csbf[xs][ys] = nonzero;
+        infer_dc = true;
+      } else {
+        csbf[xs][ys] = 1;
+      }
+      if (!csbf[xs][ys]) continue;
+      int prev_csbf = 0;
+      if (xs < nsb - 1) prev_csbf += csbf[xs + 1][ys];
+      if (ys < nsb - 1) prev_csbf += csbf[xs][ys + 1] << 1;
+      // significance
+      int vals[16], nsig = 0;
+      if (i == last_i) vals[nsig++] = at(i, last_p);
+      for (int p = (i == last_i ? last_p - 1 : 15); p >= 0; --p) {
+        const int v = at(i, p);
+        if (p > 0 || !infer_dc) {
+          const int xc = xs * 4 + px[p], yc = ys * 4 + py[p];
+          e.encode(v != 0, ctx[CTX_SIG + sig_ctx(xc, yc, log2, cidx, scan_idx, prev_csbf, xs, ys)]);
+          if (v != 0) infer_dc = false;
+        }
+        if (v != 0) vals[nsig++] = v;
+      }
+      // greater1 / greater2
+      int ctx_set = (i == 0 || cidx > 0) ? 0 : 2;
+      if (!first_sb && c1 == 0) ++ctx_set;
+      first_sb = false;
+      c1 = 1;
+      int g1_first = -1;
+      int g1[16] = {};
+      for (int k = 0; k < nsig && k < 8; ++k) {
+        const int a = std::abs(vals[k]);
+        g1[k] = a > 1;
+        e.encode(g1[k], ctx[CTX_GT1 + (cidx ? 16 : 0) + ctx_set * 4 + c1]);
+        if (g1[k]) {
+          c1 = 0;
+          if (g1_first < 0) g1_first = k;
+        } else if (c1 > 0 && c1 < 3) {
+          ++c1;
+        }
+      }
+      int g2 = 0;
+      if (g1_first >= 0) {
+        g2 = std::abs(vals[g1_first]) > 2;
+        e.encode(g2, ctx[CTX_GT2 + (cidx ? 4 : 0) + ctx_set]);
+      }
+      for (int k = 0; k < nsig; ++k) e.bypass(vals[k] < 0);
+      int rice = 0;
+      for (int k = 0; k < nsig; ++k) {
+        const int a = std::abs(vals[k]);
+        const int base = 1 + (k < 8 ? g1[k] : 0) + (k == g1_first ? g2 : 0);
+        const int thr = k < 8 ? (k == g1_first ? 3 : 2) : 1;
+        if (base == thr) {
+          write_remaining(a - base, rice);
+          if (a > 3 * (1 << rice)) rice = std::min(rice + 1, 4);
+        }
+      }
+    }
+  }
+
+  static int sig_ctx(int xc, int yc, int log2, int cidx, int scan_idx, int prev_csbf, int xs, int ys) {
+    static const uint8_t map4[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
+    int s;
+    if (log2 == 2) {
+      s = map4[(yc << 2) + xc];
+    } else if (xc + yc == 0) {
+      s = 0;
+    } else {
+      const int xp = xc & 3, yp = yc & 3;
+      if (prev_csbf == 0) s = (xp + yp == 0) ? 2 : (xp + yp < 3) ? 1 : 0;
+      else if (prev_csbf == 1) s = (yp == 0) ? 2 : (yp == 1) ? 1 : 0;
+      else if (prev_csbf == 2) s = (xp == 0) ? 2 : (xp == 1) ? 1 : 0;
+      else s = 2;
+      if (cidx == 0) {
+        if (xs + ys > 0) s += 3;
+        s += log2 == 3 ? (scan_idx == 0 ? 9 : 15) : 21;
+      } else {
+        s += log2 == 3 ? 9 : 12;
+      }
+    }
+    return cidx == 0 ? s : 27 + s;
+  }
+
+  static int mdcs(int mode) { return (mode >= 6 && mode <= 14) ? 2 : ((mode >= 22 && mode <= 30) ? 1 : 0); }
+
+  bool any_nonzero(int cidx, int x, int y, int n) const {
+    const int stride = cidx ? W / 2 : W;
+    const int16_t* p = coef[cidx] + static_cast<size_t>(y) * stride + x;
+    for (int r = 0; r < n; ++r)
+      for (int k = 0; k < n; ++k)
+        if (p[r * stride + k]) return true;
+    return false;
+  }
+
+  // ---------------------------------------------------------------- inter prediction helpers
+  struct Mv {
+    int x, y;
+    bool operator==(const Mv& o) const { return x == o.x && y == o.y; }
+  };
+  bool inter_avail(int x, int y) const { return avail(x, y) && pred[g(x, y)] == CU_INTER; }
+  Mv mv_at(int x, int y) const { return Mv{mvx[g(x, y)], mvy[g(x, y)]}; }
+
+  // 8.5.3.2.2-8.5.3.2.5 merge candidates of a 2Nx2N PU (P slice, no temporal candidate)
+  int merge_list(int x, int y, int n, Mv* out) const {
+    int k = 0;
+    const int xa1 = x - 1, ya1 = y + n - 1, xb1 = x + n - 1, yb1 = y - 1;
+    const bool a1 = inter_avail(xa1, ya1), b1 = inter_avail(xb1, yb1);
+    const bool b0 = inter_avail(x + n, y - 1), a0 = inter_avail(x - 1, y + n), b2 = inter_avail(x - 1, y - 1);
+    Mv ma1 = a1 ? mv_at(xa1, ya1) : Mv{0, 0}, mb1 = b1 ? mv_at(xb1, yb1) : Mv{0, 0};
+    if (a1) out[k++] = ma1;
+    if (b1 && !(a1 && ma1 == mb1)) out[k++] = mb1;
+    if (b0) {
+      Mv m = mv_at(x + n, y - 1);
+      if (!(b1 && mb1 == m)) out[k++] = m;
+    }
+    if (a0) {
+      Mv m = mv_at(x - 1, y + n);
+      if (!(a1 && ma1 == m)) out[k++] = m;
+    }
+    if (b2 && k < 4) {
+      Mv m = mv_at(x - 1, y - 1);
+      if (!(a1 && ma1 == m) && !(b1 && mb1 == m)) out[k++] = m;
+    }
+    while (k < c.max_merge) out[k++] = Mv{0, 0};
+    return k;
+  }
+
+  // 8.5.3.2.6-8.5.3.2.7 AMVP candidates (one reference picture: no scaling)
+  void amvp_list(int x, int y, int n, Mv* out) const {
+    const bool a0 = inter_avail(x - 1, y + n), a1 = inter_avail(x - 1, y + n - 1);
+    bool fa = false, fb = false;
+    Mv ma{0, 0}, mb{0, 0};
+    if (a0) {
+      ma = mv_at(x - 1, y + n);
+      fa = true;
+    } else if (a1) {
+      ma = mv_at(x - 1, y + n - 1);
+      fa = true;
+    }
+    const int bx[3] = {x + n, x + n - 1, x - 1};
+    for (int k = 0; k < 3 && !fb; ++k)
+      if (inter_avail(bx[k], y - 1)) {
+        mb = mv_at(bx[k], y - 1);
+        fb = true;
+      }
+    const bool scaled = a0 || a1;
+    if (!scaled && fb) {
+      ma = mb;
+      fa = true;
+    }
+    // (the re-derivation of B for !scaled finds the same candidate: one reference picture)
+    int k = 0;
+    if (fa) out[k++] = ma;
+    if (fb && !(fa && ma == mb)) out[k++] = mb;
+    while (k < 2) out[k++] = Mv{0, 0};
+  }
+
+  // ---------------------------------------------------------------- coding unit (7.3.8.5)
+  void mark(int x, int y, int n, int d, int sk, int pm, int md, Mv mv) {
+    for (int yy = y; yy < y + n; yy += 8)
+      for (int xx = x; xx < x + n; xx += 8) {
+        const size_t k = g(xx, yy);
+        depth[k] = static_cast<int8_t>(d);
+        skip[k] = static_cast<int8_t>(sk);
+        pred[k] = static_cast<int8_t>(pm);
+        mode[k] = static_cast<int8_t>(md);
+        mvx[k] = static_cast<int16_t>(mv.x);
+        mvy[k] = static_cast<int16_t>(mv.y);
+        coded[k] = 1;
+      }
+  }
+
+  void write_cu(int x, int y, int log2, int d) {
+    const int n = 1 << log2;
+    const CuInfo& ci = cu_at(x, y);
+    const bool cb_y = any_nonzero(0, x, y, n);
+    const bool cb_cb = any_nonzero(1, x / 2, y / 2, n / 2), cb_cr = any_nonzero(2, x / 2, y / 2, n / 2);
+    const bool intra = ci.pred == CU_INTRA || !pslice;
+    const Mv mv{ci.mv[0], ci.mv[1]};
+    if (pslice) {
+      int skip_ctx = (avail(x - 1, y) && skip[g(x - 1, y)]) + (avail(x, y - 1) && skip[g(x, y - 1)]);
+      int midx = -1;
+      Mv ml[5];
+      if (!intra) {
+        const int nm = merge_list(x, y, n, ml);
+        for (int k = 0; k < nm; ++k)
+          if (ml[k] == mv) {
+            midx = k;
+            break;
+          }
+      }
+      const bool is_skip = !intra && midx >= 0 && !cb_y && !cb_cb && !cb_cr;
+      e.encode(is_skip, ctx[CTX_CU_SKIP + skip_ctx]);
+      if (is_skip) {
+        write_merge_idx(midx);
+        mark(x, y, n, d, 1, CU_INTER, 1, mv);
+        ++st.skip_cus;
+        return;
+      }
+      e.encode(intra, ctx[CTX_PRED_MODE]);
+      if (!intra) {
+        e.encode(1, ctx[CTX_PART_MODE]);  // PART_2Nx2N
+        const bool merge = midx >= 0;
+        e.encode(merge, ctx[CTX_MERGE_FLAG]);
+        if (merge) {
+          write_merge_idx(midx);
+          ++st.merge_cus;
+        } else {
+          Mv ap[2];
+          amvp_list(x, y, n, ap);
+          auto cost = [&](const Mv& p) { return std::abs(mv.x - p.x) + std::abs(mv.y - p.y); };
+          const int idx = cost(ap[1]) < cost(ap[0]) ? 1 : 0;
+          write_mvd_pair(mv.x - ap[idx].x, mv.y - ap[idx].y);
+          e.encode(idx, ctx[CTX_MVP_IDX]);
+        }
+        const bool root = cb_y || cb_cb || cb_cr;
+        if (!merge) e.encode(root, ctx[CTX_RQT_ROOT_CBF]);
+        mark(x, y, n, d, 0, CU_INTER, 1, mv);
+        ++st.inter_cus;
+        if (root) write_tu(x, y, log2, false, 0, cb_y, cb_cb, cb_cr);
+        return;
+      }
+    }
+    // intra CU
+    if (log2 == kMinCbLog2) e.encode(1, ctx[CTX_PART_MODE]);  // PART_2Nx2N
+    const int m = ci.mode;
+    if (m > 34) throw std::runtime_error("intra mode out of range");
+    // 8.4.2 most probable modes
+    int ca = 1, cb = 1;
+    if (avail(x - 1, y) && pred[g(x - 1, y)] == CU_INTRA) ca = mode[g(x - 1, y)];
+    if (avail(x, y - 1) && pred[g(x, y - 1)] == CU_INTRA && ((y - 1) >> kCtbLog2) == (y >> kCtbLog2)) cb = mode[g(x, y - 1)];
+    int cand[3];
+    if (ca == cb) {
+      if (ca < 2) {
+        cand[0] = 0;
+        cand[1] = 1;
+        cand[2] = 26;
+      } else {
+        cand[0] = ca;
+        cand[1] = 2 + ((ca + 29) % 32);
+        cand[2] = 2 + ((ca - 2 + 1) % 32);
+      }
+    } else {
+      cand[0] = ca;
+      cand[1] = cb;
+      cand[2] = (ca != 0 && cb != 0) ? 0 : ((ca != 1 && cb != 1) ? 1 : 26);
+    }
+    int mpm = -1;
+    for (int k = 0; k < 3; ++k)
+      if (cand[k] == m) mpm = k;
+    e.encode(mpm >= 0, ctx[CTX_PREV_INTRA]);
+    if (mpm >= 0) {
+      e.bypass(mpm > 0);
+      if (mpm > 0) e.bypass(mpm > 1);
+    } else {
+      std::sort(cand, cand + 3);
+      int rem = m;
+      for (int k = 2; k >= 0; --k)
+        if (rem > cand[k]) --rem;
+      e.bypass_bits(rem, 5);
+    }
+    e.encode(0, ctx[CTX_CHROMA_MODE]);  // intra_chroma_pred_mode = 4 (DM)
+    mark(x, y, n, d, 0, CU_INTRA, m, Mv{0, 0});
+    ++st.intra_cus;
+    write_tu(x, y, log2, true, m, cb_y, cb_cb, cb_cr);
+  }
+
+  void write_merge_idx(int idx) {
+    if (c.max_merge <= 1) return;
+    e.encode(idx > 0, ctx[CTX_MERGE_IDX]);
+    for (int k = 1; k < c.max_merge - 1 && idx >= k; ++k) e.bypass(idx > k);
+  }
+
+  void write_mvd_pair(int dx, int dy) {
+    const int ax = std::abs(dx), ay = std::abs(dy);
+    e.encode(ax > 0, ctx[CTX_MVD_G0]);
+    e.encode(ay > 0, ctx[CTX_MVD_G0]);
+    if (ax > 0) e.encode(ax > 1, ctx[CTX_MVD_G1]);
+    if (ay > 0) e.encode(ay > 1, ctx[CTX_MVD_G1]);
+    if (ax > 0) {
+      if (ax > 1) write_eg1(ax - 2);
+      e.bypass(dx < 0);
+    }
+    if (ay > 0) {
+      if (ay > 1) write_eg1(ay - 2);
+      e.bypass(dy < 0);
+    }
+  }
+  void write_eg1(uint32_t v) {  // 9.3.3.3 k-th order Exp-Golomb, k = 1
+    int k = 1;
+    while (v >= (1u << k)) {
+      e.bypass(1);
+      v -= 1u << k;
+      ++k;
+    }
+    e.bypass(0);
+    while (k--) e.bypass((v >> k) & 1);
+  }
+
+  // transform_tree at depth 0 with TU = CU (7.3.8.8 / 7.3.8.10)
+  void write_tu(int x, int y, int log2, bool intra, int m, bool cb_y, bool cb_cb, bool cb_cr) {
+    e.encode(cb_cb, ctx[CTX_CBF_CHROMA + 0]);
+    e.encode(cb_cr, ctx[CTX_CBF_CHROMA + 0]);
+    if (intra || cb_cb || cb_cr) e.encode(cb_y, ctx[CTX_CBF_LUMA + 1]);
+    else if (!cb_y) throw std::runtime_error("inter TU: cbf_luma inferred 1 but the luma block is empty");
+    const int stride = W, cstride = W / 2;
+    if (cb_y) {
+      const int scan = (intra && log2 == 3) ? mdcs(m) : 0;
+      write_residual(coef[0] + static_cast<size_t>(y) * stride + x, stride, log2, 0, scan);
+    }
+    const int scan_c = (intra && log2 - 1 == 2) ? mdcs(m) : 0;
+    if (cb_cb) write_residual(coef[1] + static_cast<size_t>(y / 2) * cstride + x / 2, cstride, log2 - 1, 1, scan_c);
+    if (cb_cr) write_residual(coef[2] + static_cast<size_t>(y / 2) * cstride + x / 2, cstride, log2 - 1, 2, scan_c);
+  }
+
+  // coding_quadtree (7.3.8.4) of one CTB
+  void write_ctu(int rx, int ry) {
+    const CtuInfo& t = ctu[ry * wctb + rx];
+    const int x0 = rx * kCtb, y0 = ry * kCtb;
+    auto split_ctx = [&](int x, int y, int d) {
+      return (avail(x - 1, y) && depth[g(x - 1, y)] > d) + (avail(x, y - 1) && depth[g(x, y - 1)] > d);
+    };
+    const bool s32 = t.split & 1;
+    e.encode(s32, ctx[CTX_SPLIT_CU + split_ctx(x0, y0, 0)]);
+    if (!s32) {
+      write_cu(x0, y0, 5, 0);
+      return;
+    }
+    for (int q = 0; q < 4; ++q) {
+      const int x1 = x0 + (q & 1) * 16, y1 = y0 + (q >> 1) * 16;
+      const bool s16 = (t.split >> (1 + q)) & 1;
+      e.encode(s16, ctx[CTX_SPLIT_CU + split_ctx(x1, y1, 1)]);
+      if (!s16) {
+        write_cu(x1, y1, 4, 1);
+        continue;
+      }
+      for (int r = 0; r < 4; ++r) write_cu(x1 + (r & 1) * 8, y1 + (r >> 1) * 8, 3, 2);
+    }
+  }
+};
+
+}  // namespace
+
+std::vector<uint8_t> hevc_write_slice(const HevcConfig& c, const HevcFrameParams& fp, const CtuInfo* ctu,
+                                      const CuInfo* cu, const int16_t* coef_y, const int16_t* coef_cb,
+                                      const int16_t* coef_cr, HevcSliceStats* stats) {
+  BitWriter bw;
+  // 7.3.6.1 slice_segment_header
+  const bool idr = fp.idr != 0;
+  bw.put_bit(1);              // first_slice_segment_in_pic_flag
+  if (idr) bw.put_bit(0);     // no_output_of_prior_pics_flag
+  bw.put_ue(0);               // slice_pic_parameter_set_id
+  bw.put_ue(fp.slice_type);   // slice_type
+  if (!idr) {
+    bw.put(fp.poc & 255, 8);  // slice_pic_order_cnt_lsb
+    bw.put_bit(1);            // short_term_ref_pic_set_sps_flag (the single SPS set: no index bits)
+  }
+  if (c.sao) {
+    bw.put_bit(1);            // slice_sao_luma_flag
+    bw.put_bit(1);            // slice_sao_chroma_flag
+  }
+  if (fp.slice_type == 1) {
+    bw.put_bit(0);            // num_ref_idx_active_override_flag
+    bw.put_ue(5 - c.max_merge);  // five_minus_max_num_merge_cand
+  }
+  bw.put_se(fp.qp - 26);      // slice_qp_delta (init_qp 26)
+  // byte_alignment()
+  bw.put_bit(1);
+  bw.align_zero();
+  CabacEncoder enc(bw);
+  enc.start();
+  Writer w(c, fp, ctu, cu, coef_y, coef_cb, coef_cr, enc);
+  const int n = c.wctb() * c.hctb();
+  for (int i = 0; i < n; ++i) {
+    const int rx = i % c.wctb(), ry = i / c.wctb();
+    if (c.sao) w.write_sao(rx, ry);
+    w.write_ctu(rx, ry);
+    enc.terminate(i == n - 1);  // end_of_slice_segment_flag
+  }
+  enc.finish();
+  bw.put_bit(1);  // rbsp_slice_segment_trailing_bits: stop bit + alignment
+  bw.align_zero();
+  std::vector<uint8_t> out;
+  append_hevc_nal(out, idr ? NAL_IDR_W_RADL : NAL_TRAIL_R, bw.bytes());
+  if (stats) {
+    *stats = w.st;
+    stats->bins = enc.bins();
+    stats->bytes = out.size();
+  }
+  return out;
+}
+
+}  // namespace hevc
+}  // namespace mivc

@@ -1,0 +1,112 @@
+"""Random HEVC decision-record streams (test inputs for the HEVC writer/decoder pair).
+
+Records follow csrc/common/hevc_tables.h: a 32-byte ``CtuInfo`` per 32x32 CTB, an
+8-byte ``CuInfo`` per 8x8 granule (z-order, replicated over each CU) and level planes
+shaped like the picture.  Pictures mix every CU size, all 35 intra modes, inter CUs
+with random motion (skip / merge / AMVP chosen by the writer), sparse random levels
+with occasional large magnitudes (escape codes) and random SAO parameters.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+CTB = 32
+
+
+def _zorder8(gx: int, gy: int) -> int:
+    return (gx & 1) | ((gy & 1) << 1) | ((gx & 2) << 1) | ((gy & 2) << 2)
+
+
+def _cu_list(split: int):
+    """(x, y, size) of the CUs of a CTB in coding order for a split byte."""
+    if not split & 1:
+        return [(0, 0, 32)]
+    out = []
+    for q in range(4):
+        x1, y1 = (q & 1) * 16, (q >> 1) * 16
+        if (split >> (1 + q)) & 1:
+            out += [(x1 + (r & 1) * 8, y1 + (r >> 1) * 8, 8) for r in range(4)]
+        else:
+            out.append((x1, y1, 16))
+    return out
+
+
+def _levels(rng, n: int, density: float) -> np.ndarray:
+    blk = np.zeros((n, n), np.int16)
+    if rng.random() < 0.3:
+        return blk
+    mask = rng.random((n, n)) < density * (1.0 + 3.0 * (np.add.outer(np.arange(n), np.arange(n)) < n // 2))
+    vals = rng.integers(-3, 4, (n, n))
+    big = rng.random((n, n)) < 0.03
+    vals = np.where(big, rng.integers(-600, 601, (n, n)), vals)
+    blk[mask] = vals[mask]
+    return blk
+
+
+def random_records(rng, width: int, height: int, pslice: bool, bit_depth: int = 8, density: float = 0.08,
+                   intra_in_p: float = 0.2, mv_range: int = 64, sao: bool = True):
+    W, H = -(-width // CTB) * CTB, -(-height // CTB) * CTB
+    wc, hc = W // CTB, H // CTB
+    ctu = np.zeros((wc * hc, 32), np.uint8)
+    cu = np.zeros((wc * hc * 16, 8), np.uint8)
+    cy = np.zeros((H, W), np.int16)
+    cb = np.zeros((H // 2, W // 2), np.int16)
+    cr = np.zeros((H // 2, W // 2), np.int16)
+    cmax = (1 << (min(bit_depth, 10) - 5)) - 1
+    for i in range(wc * hc):
+        rx, ry = i % wc, i // wc
+        r = rng.random()
+        split = 0 if r < 0.25 else (1 | (int(rng.integers(0, 16)) << 1))
+        ctu[i, 0] = split
+        if sao:
+            t = ctu[i]
+            for k in range(2):
+                t[2 + k] = int(rng.integers(0, 3))
+                t[4 + k] = int(rng.integers(0, 4))
+            t[6:9] = rng.integers(0, 32, 3)
+            off = np.zeros((3, 4), np.int8)
+            for c in range(3):
+                typ = t[2 + (1 if c else 0)]
+                a = rng.integers(0, cmax + 1, 4)
+                if typ == 1:
+                    off[c] = a * rng.choice([-1, 1], 4)
+                elif typ == 2:
+                    off[c] = [a[0], a[1], -a[2], -a[3]]
+            t[10:22] = off.reshape(-1).view(np.uint8)
+            if rx > 0 and rng.random() < 0.2:   # exercise sao_merge_left
+                t[2:22] = ctu[i - 1, 2:22]
+        for (x, y, n) in _cu_list(split):
+            intra = (not pslice) or rng.random() < intra_in_p
+            rec = np.zeros(8, np.uint8)
+            rec[0] = 0 if intra else 1
+            if intra:
+                rec[1] = int(rng.integers(0, 35))
+            else:
+                mv = rng.integers(-mv_range, mv_range + 1, 2).astype(np.int16)
+                if rng.random() < 0.3:
+                    mv[:] = 0
+                rec[4:8] = mv.view(np.uint8)
+            for gy in range(y // 8, (y + n) // 8):
+                for gx in range(x // 8, (x + n) // 8):
+                    cu[i * 16 + _zorder8(gx, gy)] = rec
+            X, Y = rx * CTB + x, ry * CTB + y
+            cy[Y:Y + n, X:X + n] = _levels(rng, n, density)
+            cb[Y // 2:(Y + n) // 2, X // 2:(X + n) // 2] = _levels(rng, n // 2, density)
+            cr[Y // 2:(Y + n) // 2, X // 2:(X + n) // 2] = _levels(rng, n // 2, density)
+    return ctu, cu, cy, cb, cr
+
+
+def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp: int = 30, bit_depth: int = 8,
+                  **kw) -> tuple[bytes, list]:
+    """Annex-B HEVC stream (IDR + P pictures) and the records it was written from."""
+    rng = np.random.default_rng(seed)
+    cfg = dict(width=width, height=height, bit_depth=bit_depth)
+    out = [host.hevc_parameter_sets(cfg)]
+    recs = []
+    for t in range(frames):
+        r = random_records(rng, width, height, pslice=t > 0, bit_depth=bit_depth, **kw)
+        fqp = int(np.clip(qp + rng.integers(-3, 4), 0, 51))
+        nal, _ = host.hevc_write_slice(cfg, dict(idr=int(t == 0), poc=t, qp=fqp, slice_type=1 if t else 2), *r)
+        out.append(nal)
+        recs.append(r)
+    return b"".join(out), recs

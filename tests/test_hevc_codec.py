@@ -1,0 +1,99 @@
+"""HEVC host layer: parameter sets, CABAC slice writer and
+the independent decoder.
+
+* random decision records (every CU size, all 35 intra modes, skip / merge / AMVP
+  inter CUs, escape-coded levels, SAO band / edge / merge) survive writer -> decoder
+  exactly (levels, CU tree, modes, motion vectors, SAO parameters), Main and Main 10;
+* the DCT matrix construction reproduces the standard's rows;
+* reconstruction sanity: flat DC pictures, zero-motion copies.
+"""
+import numpy as np
+import pytest
+
+from govideocompressor_amd.utils.hevc_synth import random_records, random_stream
+
+
+def _norm_sao(c):
+    c = c.copy()
+    for t in c:
+        off = t[10:22].view(np.int8).reshape(3, 4).copy()
+        for ci in range(3):
+            typ = t[2 + (1 if ci else 0)]
+            if typ != 1:
+                t[6 + ci] = 0
+            if typ == 0:
+                off[ci] = 0
+        for k in range(2):
+            if t[2 + k] != 2:
+                t[4 + k] = 0
+        t[10:22] = off.reshape(-1).view(np.uint8)
+    return c[:, 2:22]
+
+
+@pytest.mark.parametrize("w,h,bd,seed", [(64, 64, 8, 1), (96, 64, 10, 2), (80, 48, 8, 3), (160, 96, 10, 4)])
+def test_hevc_records_roundtrip(host, w, h, bd, seed):
+    s, recs = random_stream(host, w, h, 4, seed=seed, bit_depth=bd)
+    pics = host.hevc_decode(s)
+    assert len(pics) == 4
+    for t, (p, (ctu, cu, cy, cb, cr)) in enumerate(zip(pics, recs)):
+        assert p["idr"] == (t == 0) and p["poc"] == t and p["bit_depth"] == bd
+        assert (p["width"], p["height"]) == (w, h)
+        assert np.array_equal(p["coef_y"], cy) and np.array_equal(p["coef_cb"], cb) and np.array_equal(p["coef_cr"], cr)
+        assert np.array_equal(p["ctu"][:, 0], ctu[:, 0])
+        assert np.array_equal(_norm_sao(p["ctu"]), _norm_sao(ctu))
+        assert np.array_equal(p["cu"][:, 0], cu[:, 0])
+        assert np.array_equal(p["cu"][:, 1], np.where(cu[:, 0] == 0, cu[:, 1], 0))
+        assert np.array_equal(p["cu"][:, 4:8], cu[:, 4:8])
+        assert p["y"].max() <= (1 << bd) - 1
+
+
+def test_hevc_dct_matrix(host):
+    m = np.asarray(host.table("hevc_dct32"), dtype=np.int64).reshape(32, 32)
+    assert list(m[1, :8]) == [90, 90, 88, 85, 82, 78, 73, 67]
+    assert list(m[2, :8]) == [90, 87, 80, 70, 57, 43, 25, 9]
+    assert list(m[4, :4]) == [89, 75, 50, 18]
+    assert list(m[8, :2]) == [83, 36] and list(m[16, :4]) == [64, -64, -64, 64]
+    g = m @ m.T   # near-orthogonal with norm 64^2 * 32
+    assert np.all(np.abs(np.diag(g) - 64 * 64 * 32) < 64 * 32) and np.max(np.abs(g - np.diag(np.diag(g)))) < 600
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+def test_hevc_flat_dc_and_zero_motion(host, bd):
+    w, h = 64, 64
+    cfg = dict(width=w, height=h, bit_depth=bd, sao=0)
+    ctu = np.zeros((4, 32), np.uint8)
+    cu = np.zeros((64, 8), np.uint8)
+    cu[:, 1] = 1   # DC everywhere
+    z = np.zeros((h, w), np.int16)
+    zc = np.zeros((h // 2, w // 2), np.int16)
+    s = host.hevc_parameter_sets(cfg)
+    s += host.hevc_write_slice(cfg, dict(idr=1, poc=0, qp=30), ctu, cu, z, zc, zc)[0]
+    # a P picture of zero-motion inter CUs with a luma DC residual in CTB 0
+    cup = np.zeros((64, 8), np.uint8)
+    cup[:, 0] = 1
+    zy = z.copy()
+    zy[0, 0] = 8
+    s += host.hevc_write_slice(cfg, dict(idr=0, poc=1, qp=30, slice_type=1), ctu, cup, zy, zc, zc)[0]
+    pics = host.hevc_decode(s)
+    mid = 1 << (bd - 1)
+    assert np.all(pics[0]["y"] == mid) and np.all(pics[0]["u"] == mid)
+    # residual of a lone DC level in a 32x32 TU: flat offset inside CTB 0 (deblocking may touch its edges)
+    y1 = pics[1]["y"].astype(int)
+    assert np.all(y1[36:, :] == mid) and np.all(y1[:, 36:] == mid)
+    inner = y1[:28, :28]
+    assert np.all(inner == inner[0, 0]) and inner[0, 0] > mid
+
+
+def test_hevc_parameter_sets_shape(host):
+    ps = host.hevc_parameter_sets(dict(width=1920, height=1080))
+    nal_types = [(ps[i + 4] >> 1) & 63 for i in range(len(ps) - 4) if ps[i:i + 4] == b"\x00\x00\x00\x01"]
+    assert nal_types == [32, 33, 34]
+
+
+def test_hevc_writer_rejects_bad_records(host):
+    rng = np.random.default_rng(0)
+    ctu, cu, cy, cb, cr = random_records(rng, 64, 64, pslice=False)
+    ctu[0, 2] = 2
+    ctu[0, 10:14] = np.array([-1, 0, 0, 0], np.int8).view(np.uint8)   # negative edge offset in category 1
+    with pytest.raises(Exception):
+        host.hevc_write_slice(dict(width=64, height=64), dict(idr=1, poc=0, qp=30), ctu, cu, cy, cb, cr)
