@@ -37,6 +37,16 @@ void mivc_launch_decode_picture(int B, int wmb, int hmb, const uint8_t* ref_y, c
                                 const uint8_t* ref_v, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const void* hdr,
                                 const uint32_t* mask, const uint32_t* off, const int16_t* coef, const int8_t* run,
                                 int any_p, int chroma_qp_offset, uint8_t* nz, int* err, void* stream);
+void mivc_launch_hevc_prep(int B, const void* src, long long slot_stride, int pitch, int bps, int w, int h,
+                           uint16_t* dst, int W, int H, int shift, void* stream);
+void mivc_launch_hevc_intra(int B, int W, int H, const uint16_t* sy, const uint16_t* su, const uint16_t* sv,
+                            uint16_t* ry, uint16_t* ru, uint16_t* rv, void* ctu, void* cu, int16_t* cy, int16_t* cu_,
+                            int16_t* cv, const int* qp, const int8_t* run, int bd, int analyze, int* err, void* stream);
+void mivc_launch_hevc_deblock(int B, int W, int H, int bd, uint16_t* y, uint16_t* u, uint16_t* v, const void* cu,
+                              const int* qp, const int8_t* run, void* stream);
+void mivc_launch_hevc_sao(int B, int W, int H, int bd, const uint16_t* dy, const uint16_t* du, const uint16_t* dv,
+                          uint16_t* y, uint16_t* u, uint16_t* v, const uint16_t* sy, const uint16_t* su,
+                          const uint16_t* sv, void* ctu, const int* qp, const int8_t* run, int enable, void* stream);
 size_t mivc_cavlc_mb_bytes();
 void mivc_launch_cavlc(int B, int wmb, int hmb, const void* hdr, const int16_t* coef, void* mbs, int* len,
                        long long* off, int* trail, long long* total_bits, int* slot_bytes, uint32_t* words,
@@ -109,6 +119,30 @@ PYBIND11_MODULE(_hip, m) {
     mivc_launch_decode_picture(B, wmb, hmb, P<uint8_t>(ry), P<uint8_t>(ru), P<uint8_t>(rv), P<uint8_t>(y),
                                P<uint8_t>(u), P<uint8_t>(v), P<void>(hdr), P<uint32_t>(mask), P<uint32_t>(off),
                                P<int16_t>(coef), P<int8_t>(run), any_p, cqo, P<uint8_t>(nz), P<int>(err), S(stream));
+  });
+  // ---- HEVC
+  m.def("hevc_prep", [](int B, uintptr_t src, long long slot_stride, int pitch, int bps, int w, int h, uintptr_t dst,
+                        int W, int H, int shift, uintptr_t stream) {
+    mivc_launch_hevc_prep(B, P<void>(src), slot_stride, pitch, bps, w, h, P<uint16_t>(dst), W, H, shift, S(stream));
+  });
+  m.def("hevc_intra", [](int B, int W, int H, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t ry, uintptr_t ru,
+                         uintptr_t rv, uintptr_t ctu, uintptr_t cu, uintptr_t cy, uintptr_t cu_, uintptr_t cv,
+                         uintptr_t qp, uintptr_t run, int bd, int analyze, uintptr_t err, uintptr_t stream) {
+    mivc_launch_hevc_intra(B, W, H, P<uint16_t>(sy), P<uint16_t>(su), P<uint16_t>(sv), P<uint16_t>(ry), P<uint16_t>(ru),
+                           P<uint16_t>(rv), P<void>(ctu), P<void>(cu), P<int16_t>(cy), P<int16_t>(cu_), P<int16_t>(cv),
+                           P<int>(qp), P<int8_t>(run), bd, analyze, P<int>(err), S(stream));
+  });
+  m.def("hevc_deblock", [](int B, int W, int H, int bd, uintptr_t y, uintptr_t u, uintptr_t v, uintptr_t cu,
+                           uintptr_t qp, uintptr_t run, uintptr_t stream) {
+    mivc_launch_hevc_deblock(B, W, H, bd, P<uint16_t>(y), P<uint16_t>(u), P<uint16_t>(v), P<void>(cu), P<int>(qp),
+                             P<int8_t>(run), S(stream));
+  });
+  m.def("hevc_sao", [](int B, int W, int H, int bd, uintptr_t dy, uintptr_t du, uintptr_t dv, uintptr_t y, uintptr_t u,
+                       uintptr_t v, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t ctu, uintptr_t qp, uintptr_t run,
+                       int enable, uintptr_t stream) {
+    mivc_launch_hevc_sao(B, W, H, bd, P<uint16_t>(dy), P<uint16_t>(du), P<uint16_t>(dv), P<uint16_t>(y), P<uint16_t>(u),
+                         P<uint16_t>(v), P<uint16_t>(sy), P<uint16_t>(su), P<uint16_t>(sv), P<void>(ctu), P<int>(qp),
+                         P<int8_t>(run), enable, S(stream));
   });
   m.def("cavlc_mb_bytes", []() { return mivc_cavlc_mb_bytes(); });
   m.def("cavlc", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t coef, uintptr_t mbs, uintptr_t len, uintptr_t off,

@@ -1,0 +1,273 @@
+// Device helpers of the HEVC kernels (gfx950): wave-level integer transforms through
+// LDS, intra reference-sample construction (8.4.4.2.2 availability + substitution,
+// 8.4.4.2.3 filtering) and intra sample prediction (8.4.4.2.4 - 8.4.4.2.6).
+//
+// Samples are uint16 for 8- and 10-bit content (one code path; the bit depth is a
+// runtime parameter).  A transform of an n x n block (n = 4..32) is two matrix
+// products done by one wave64: lane (ti, tj) owns a T x T output tile (T = n / 8,
+// 8 x 8 tiles), the DCT matrix lives in LDS as int16.
+#pragma once
+#include "kcommon.h"
+#include "../common/hevc_tables.h"
+
+namespace mivc {
+namespace gpu {
+namespace hv {
+
+using hevc::dct_coef;
+
+// ---------------------------------------------------------------- DCT matrix in LDS
+struct DctLds {
+  int16_t m[32][32];
+};
+__device__ __forceinline__ void dct_lds_init(DctLds& D) {
+  for (int i = threadIdx.x; i < 1024; i += blockDim.x) D.m[i >> 5][i & 31] = static_cast<int16_t>(dct_coef(i >> 5, i & 31));
+}
+// entry (k, m) of the n-point matrix
+__device__ __forceinline__ int cn(const DctLds& D, int log2n, int k, int m) { return D.m[k << (5 - log2n)][m]; }
+
+// ---------------------------------------------------------------- wave matrix product
+// out(i, j) = sum_k A(i, k) * B(k, j), i, j, k < n.  Every lane must call (no lane-
+// dependent early exit before): lanes beyond the tile grid idle inside.
+template <int T, class FA, class FB, class FO>
+__device__ __forceinline__ void wave_matmul_t(int n, FA A, FB B, FO out) {
+  const int lane = lane_id();
+  const int tiles = n / T;
+  if (lane < tiles * tiles) {
+    const int i0 = (lane / tiles) * T, j0 = (lane % tiles) * T;
+    int acc[T][T];
+#pragma unroll
+    for (int r = 0; r < T; ++r)
+#pragma unroll
+      for (int c = 0; c < T; ++c) acc[r][c] = 0;
+    for (int k = 0; k < n; ++k) {
+      int a[T], b[T];
+#pragma unroll
+      for (int r = 0; r < T; ++r) a[r] = A(i0 + r, k);
+#pragma unroll
+      for (int c = 0; c < T; ++c) b[c] = B(k, j0 + c);
+#pragma unroll
+      for (int r = 0; r < T; ++r)
+#pragma unroll
+        for (int c = 0; c < T; ++c) acc[r][c] += a[r] * b[c];
+    }
+#pragma unroll
+    for (int r = 0; r < T; ++r)
+#pragma unroll
+      for (int c = 0; c < T; ++c) out(i0 + r, j0 + c, acc[r][c]);
+  }
+}
+template <class FA, class FB, class FO>
+__device__ __forceinline__ void wave_matmul(int n, FA A, FB B, FO out) {
+  if (n == 32) wave_matmul_t<4>(n, A, B, out);
+  else if (n == 16) wave_matmul_t<2>(n, A, B, out);
+  else wave_matmul_t<1>(n, A, B, out);
+}
+
+// ---------------------------------------------------------------- transform + quantisation of one block
+// R: residual (in) / reconstructed residual (out), int32 [n][n] in LDS, row stride 32.
+// S: scratch int32 [32][32].  Levels go to lev (global, row stride lstride).  Returns
+// (on every lane) whether any level is non-zero.
+struct TqParams {
+  int log2n, bd, qp;  // qp: Qp' (QpY + QpBdOffset, or the chroma equivalent)
+  bool intra;
+};
+
+__device__ __forceinline__ bool transform_quant_block(const DctLds& D, int* R, int* S, int16_t* lev, int lstride,
+                                                      const TqParams& p) {
+  const int n = 1 << p.log2n, lg = p.log2n;
+  // forward, stage 1 (rows): S[y][k] = (sum_x R[y][x] * C[k][x] + rnd) >> sh1
+  const int sh1 = lg + p.bd - 9, r1 = 1 << (sh1 - 1);
+  wave_matmul(n, [&](int y, int x) { return R[y * 32 + x]; }, [&](int x, int k) { return cn(D, lg, k, x); },
+              [&](int y, int k, int v) { S[y * 32 + k] = (v + r1) >> sh1; });
+  wave_sync();
+  // stage 2 (columns): coefficient (v, u) = (sum_y C[v][y] * S[y][u] + rnd) >> sh2
+  const int sh2 = lg + 6, r2 = 1 << (sh2 - 1);
+  const int qm = p.qp % 6, qs = p.qp / 6;
+  const int qbits = 14 + qs + (15 - p.bd - lg);
+  const int qscale = hevc::kQuantScale[qm];
+  const int64_t qoff = static_cast<int64_t>(p.intra ? 171 : 85) << (qbits - 9);
+  const int dscale = 16 * hevc::kLevelScale[qm];
+  const int dsh = p.bd + lg - 5;
+  const int64_t drnd = 1ll << (dsh - 1);
+  int any = 0;
+  wave_matmul(n, [&](int v, int y) { return cn(D, lg, v, y); }, [&](int y, int u) { return S[y * 32 + u]; },
+              [&](int v, int u, int c) {
+                c = (c + r2) >> sh2;
+                const int a = c < 0 ? -c : c;
+                int l = static_cast<int>((static_cast<int64_t>(a) * qscale + qoff) >> qbits);
+                l = l > 32767 ? 32767 : l;
+                l = c < 0 ? -l : l;
+                lev[v * lstride + u] = static_cast<int16_t>(l);
+                any |= l != 0;
+                // dequantise (8.6.3, flat scaling) into R for the inverse transform
+                int64_t d = ((static_cast<int64_t>(l) * dscale) << qs) + drnd;
+                d >>= dsh;
+                R[v * 32 + u] = static_cast<int>(d < -32768 ? -32768 : (d > 32767 ? 32767 : d));
+              });
+  wave_sync();
+  const bool nz = __ballot(any) != 0;
+  if (!nz) return false;  // residual is zero: R is all zero too
+  // inverse, stage 1 (columns): S[y][x] = clip16((sum_k C[k][y] * R[k][x] + 64) >> 7)
+  wave_matmul(n, [&](int y, int k) { return cn(D, lg, k, y); }, [&](int k, int x) { return R[k * 32 + x]; },
+              [&](int y, int x, int v) {
+                v = (v + 64) >> 7;
+                S[y * 32 + x] = v < -32768 ? -32768 : (v > 32767 ? 32767 : v);
+              });
+  wave_sync();
+  // stage 2 (rows): R[y][x] = (sum_k S[y][k] * C[k][x] + rnd) >> (20 - bd)
+  const int sh4 = 20 - p.bd, r4 = 1 << (sh4 - 1);
+  wave_matmul(n, [&](int y, int k) { return S[y * 32 + k]; }, [&](int k, int x) { return cn(D, lg, k, x); },
+              [&](int y, int x, int v) { R[y * 32 + x] = (v + r4) >> sh4; });
+  wave_sync();
+  return true;
+}
+
+// ---------------------------------------------------------------- intra reference samples
+// p[0 .. 4n]: p[2n - 1 - y] = p(-1, y) for y = -1 .. 2n-1 (index 2n = corner),
+// p[2n + 1 + x] = p(x, -1).  `avail(i)` / `fetch(i)` give availability and value of
+// entry i; substitution per 8.4.4.2.2 (nearest available entry before i in this
+// order, or the first available one), done wave-parallel with ballots.
+template <class FAV, class FGET>
+__device__ __forceinline__ void build_refs(int* p, int n, int bd, FAV avail, FGET fetch) {
+  const int lane = lane_id();
+  const int E = 4 * n + 1;
+  const int i0 = lane, i1 = lane + 64;
+  const bool a0 = i0 < E && avail(i0);
+  const bool a1 = i1 < E && avail(i1);
+  const unsigned long long b0 = __ballot(a0), b1 = __ballot(a1);
+  const bool a2 = E > 128 && avail(128);  // uniform
+  if (a0) p[i0] = fetch(i0);
+  if (a1) p[i1] = fetch(i1);
+  if (lane == 0 && a2) p[128] = fetch(128);
+  wave_sync();
+  const bool none = b0 == 0 && b1 == 0 && !a2;
+  int first = 0;
+  if (b0) first = __builtin_ctzll(b0);
+  else if (b1) first = 64 + __builtin_ctzll(b1);
+  else first = 128;
+  auto src_of = [&](int i) {
+    // highest available index < i
+    if (i < 64) {
+      const unsigned long long m = i ? (b0 & ((1ull << i) - 1ull)) : 0ull;
+      if (m) return 63 - __builtin_clzll(m);
+      return -1;
+    }
+    if (i < 128) {
+      const unsigned long long m = (i - 64) ? (b1 & ((1ull << (i - 64)) - 1ull)) : 0ull;
+      if (m) return 64 + 63 - __builtin_clzll(m);
+      if (b0) return 63 - __builtin_clzll(b0);
+      return -1;
+    }
+    if (b1) return 64 + 63 - __builtin_clzll(b1);
+    if (b0) return 63 - __builtin_clzll(b0);
+    return -1;
+  };
+  int v0 = 0, v1 = 0, v2 = 0;
+  const int mid = 1 << (bd - 1);
+  if (i0 < E && !a0) {
+    const int s = src_of(i0);
+    v0 = none ? mid : p[s >= 0 ? s : first];
+  }
+  if (i1 < E && !a1) {
+    const int s = src_of(i1);
+    v1 = none ? mid : p[s >= 0 ? s : first];
+  }
+  if (lane == 0 && E > 128 && !a2) {
+    const int s = src_of(128);
+    v2 = none ? mid : p[s >= 0 ? s : first];
+  }
+  wave_sync();
+  if (i0 < E && !a0) p[i0] = v0;
+  if (i1 < E && !a1) p[i1] = v1;
+  if (lane == 0 && E > 128 && !a2) p[128] = v2;
+  wave_sync();
+}
+
+// 8.4.4.2.3 filtering of luma references (q: output array, same layout)
+__device__ __forceinline__ bool intra_filter_flag(int mode, int n) {
+  if (mode == 1 || n == 4) return false;
+  const int d0 = mode - 26 < 0 ? 26 - mode : mode - 26, d1 = mode - 10 < 0 ? 10 - mode : mode - 10;
+  const int md = d0 < d1 ? d0 : d1;
+  const int thr = n == 8 ? 7 : (n == 16 ? 1 : 0);
+  return md > thr;
+}
+__device__ __forceinline__ void filter_refs(const int* p, int* q, int n, int bd, bool strong_enabled) {
+  const int lane = lane_id();
+  const int E = 4 * n + 1, c = 2 * n;
+  const int tl = p[c], bl = p[0], tr = p[E - 1];
+  const bool bi = strong_enabled && n == 32 &&
+                  abs(tl + tr - 2 * p[c + 1 + (n - 1)]) < (1 << (bd - 5)) &&
+                  abs(tl + bl - 2 * p[c - 1 - (n - 1)]) < (1 << (bd - 5));
+  for (int i = lane; i < E; i += 64) {
+    int v;
+    if (i == 0 || i == E - 1 || (bi && i == c)) {
+      v = p[i];
+    } else if (bi) {
+      if (i < c) {
+        const int y = c - 1 - i;  // 0..62
+        v = ((63 - y) * tl + (y + 1) * bl + 32) >> 6;
+      } else {
+        const int x = i - c - 1;
+        v = ((63 - x) * tl + (x + 1) * tr + 32) >> 6;
+      }
+    } else {
+      v = (p[i - 1] + 2 * p[i] + p[i + 1] + 2) >> 2;
+    }
+    q[i] = v;
+  }
+  wave_sync();
+}
+
+// one predicted sample (8.4.4.2.4 - 8.4.4.2.6); dc: precomputed DC value (mode 1);
+// edge: luma block smaller than 32 (DC / pure horizontal / pure vertical boundary filters)
+__device__ __forceinline__ int intra_pred_sample(const int* p, int n, int log2n, int mode, int x, int y, int dc,
+                                                 bool edge, int maxv) {
+  const int c = 2 * n;
+  auto L = [&](int yy) { return p[c - 1 - yy]; };
+  auto T = [&](int xx) { return p[c + 1 + xx]; };
+  if (mode == 0) return ((n - 1 - x) * L(y) + (x + 1) * T(n) + (n - 1 - y) * T(x) + (y + 1) * L(n) + n) >> (log2n + 1);
+  if (mode == 1) {
+    if (!edge) return dc;
+    if (x == 0 && y == 0) return (L(0) + 2 * dc + T(0) + 2) >> 2;
+    if (y == 0) return (T(x) + 3 * dc + 2) >> 2;
+    if (x == 0) return (L(y) + 3 * dc + 2) >> 2;
+    return dc;
+  }
+  const int ang = hevc::kIntraPredAngle[mode];
+  const int inv = (mode >= 11 && mode <= 25) ? hevc::kInvAngle[mode - 11] : 0;
+  if (mode >= 18) {
+    const int idx = ((y + 1) * ang) >> 5, fact = ((y + 1) * ang) & 31;
+    const int k0 = x + idx + 1;
+    auto R = [&](int k) { return k >= 0 ? T(k - 1) : L(-1 + ((k * inv + 128) >> 8)); };
+    int v = fact ? ((32 - fact) * R(k0) + fact * R(k0 + 1) + 16) >> 5 : R(k0);
+    if (mode == 26 && edge && x == 0) {
+      v = T(0) + ((L(y) - L(-1)) >> 1);
+      v = v < 0 ? 0 : (v > maxv ? maxv : v);
+    }
+    return v;
+  }
+  const int idx = ((x + 1) * ang) >> 5, fact = ((x + 1) * ang) & 31;
+  const int k0 = y + idx + 1;
+  auto R = [&](int k) { return k >= 0 ? L(k - 1) : T(-1 + ((k * inv + 128) >> 8)); };
+  int v = fact ? ((32 - fact) * R(k0) + fact * R(k0 + 1) + 16) >> 5 : R(k0);
+  if (mode == 10 && edge && y == 0) {
+    v = L(0) + ((T(x) - T(-1)) >> 1);
+    v = v < 0 ? 0 : (v > maxv ? maxv : v);
+  }
+  return v;
+}
+
+// DC value of the reference array (wave reduction)
+__device__ __forceinline__ int intra_dc(const int* p, int n, int log2n) {
+  const int lane = lane_id();
+  const int c = 2 * n;
+  int s = 0;
+  if (lane < n) s = p[c + 1 + lane] + p[c - 1 - lane];
+  s = sum64(s);
+  return (s + n) >> (log2n + 1);
+}
+
+}  // namespace hv
+}  // namespace gpu
+}  // namespace mivc

@@ -1,0 +1,395 @@
+// HEVC picture-level kernels: source preparation, in-loop
+// deblocking (8.7.2) and sample adaptive offset (8.7.3) with the encoder's SAO
+// parameter decision.
+//
+// Unlike H.264, HEVC deblocking has no raster-order dependency: all vertical edges
+// of the picture are filtered first (8-sample grid, decisions read 4 samples and
+// modify at most 3 on each side, so edges are independent), then all horizontal
+// edges.  Each is one fully parallel launch: a thread owns one 4-sample edge
+// segment (luma, plus its 2 chroma lines on the 16-sample chroma grid).  SAO reads the
+// deblocked picture (a copy) and writes the final reconstruction; one workgroup per
+// CTB gathers edge-/band-offset statistics against the source in LDS, picks the
+// cheapest of {off, 4 edge classes, band} per component with an SSE + lambda * bits
+// estimate, stores the parameters for the CABAC writer and applies them.
+#include "kcommon.h"
+#include "../common/hevc_tables.h"
+
+namespace mivc {
+namespace gpu {
+
+using hevc::CtuInfo;
+using hevc::CuInfo;
+
+// ============================================================== source preparation
+// src: slot b, frame plane at base + b * slot_stride (bytes per sample = bps), rows of
+// `pitch` samples, w x h valid; dst: [B] padded W x H uint16 planes (edge replication)
+__global__ void hevc_prep_plane(const uint8_t* src, long long slot_stride, int pitch, int bps, int w, int h,
+                                uint16_t* dst, int W, int H, int shift) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  const int b = blockIdx.z;
+  if (x >= W) return;
+  const int sx = min(x, w - 1), sy = min(y, h - 1);
+  const uint8_t* s = src + b * slot_stride;
+  int v;
+  if (bps == 1) v = s[static_cast<size_t>(sy) * pitch + sx];
+  else v = reinterpret_cast<const uint16_t*>(s)[static_cast<size_t>(sy) * pitch + sx];
+  dst[static_cast<size_t>(b) * W * H + static_cast<size_t>(y) * W + x] = static_cast<uint16_t>(v << shift);
+}
+
+// ============================================================== deblocking
+struct HevcDbkArgs {
+  int B, W, H, wctb, bd;
+  uint16_t *y, *u, *v;
+  const CuInfo* cu;  // [B, nctb * 16]
+  const int* qp;     // [B]
+  const int8_t* run; // [B]
+  int dir;           // 0 vertical edges, 1 horizontal edges
+};
+
+__device__ __forceinline__ const CuInfo& cu_at(const HevcDbkArgs& a, int slot, int x, int y) {
+  const int nctb = a.wctb * (a.H / 32);
+  const int ci = (y >> 5) * a.wctb + (x >> 5);
+  return a.cu[(static_cast<size_t>(slot) * nctb + ci) * 16 + hevc::zorder8((x & 31) >> 3, (y & 31) >> 3)];
+}
+
+__device__ __forceinline__ int clip3i(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
+
+__global__ void hevc_deblock(HevcDbkArgs a) {
+  const int slot = blockIdx.y;
+  if (a.run[slot] == 0) return;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  // segments: vertical edges x = 8k (k >= 1), rows of 4; horizontal edges y = 8k, columns of 4
+  int xq, yq;
+  if (a.dir == 0) {
+    const int per_row = a.W / 8 - 1;
+    if (idx >= per_row * (a.H / 4)) return;
+    xq = (idx % per_row + 1) * 8;
+    yq = (idx / per_row) * 4;
+  } else {
+    const int per_row = a.W / 4;
+    if (idx >= per_row * (a.H / 8 - 1)) return;
+    xq = (idx % per_row) * 4;
+    yq = (idx / per_row + 1) * 8;
+  }
+  const int xp = a.dir == 0 ? xq - 1 : xq, yp = a.dir == 0 ? yq : yq - 1;
+  const CuInfo& Q = cu_at(a, slot, xq, yq);
+  const CuInfo& P = cu_at(a, slot, xp, yp);
+  const int lq = 3 + ((Q.flags >> 1) & 3);
+  const int pos = a.dir == 0 ? xq : yq;
+  if (pos & ((1 << lq) - 1)) return;  // not a CU (TU = PU) boundary
+  int bs;
+  if (P.pred == hevc::CU_INTRA || Q.pred == hevc::CU_INTRA) bs = 2;
+  else if ((P.cbf & 1) || (Q.cbf & 1)) bs = 1;
+  else if (abs(P.mv[0] - Q.mv[0]) >= 4 || abs(P.mv[1] - Q.mv[1]) >= 4) bs = 1;
+  else bs = 0;
+  if (!bs) return;
+  const int bd = a.bd, maxv = (1 << bd) - 1;
+  const int qpl = a.qp[slot];  // one QP per picture: QpP == QpQ
+  const int qb = clip3i(0, 51, qpl), qt = clip3i(0, 53, qpl + 2 * (bs - 1));
+  const int beta = hevc::kBetaTable[qb] << (bd - 8), tc = hevc::kTcTable[qt] << (bd - 8);
+  const int W = a.W;
+  uint16_t* py = a.y + static_cast<size_t>(slot) * W * a.H;
+  uint16_t* s0 = py + static_cast<size_t>(yq) * W + xq;
+  const int step = a.dir == 0 ? W : 1, across = a.dir == 0 ? 1 : W;
+  auto Ps = [&](int l, int i) -> uint16_t& { return s0[l * step - (i + 1) * across]; };
+  auto Qs = [&](int l, int i) -> uint16_t& { return s0[l * step + i * across]; };
+  const int dp0 = abs(Ps(0, 2) - 2 * Ps(0, 1) + Ps(0, 0)), dp3 = abs(Ps(3, 2) - 2 * Ps(3, 1) + Ps(3, 0));
+  const int dq0 = abs(Qs(0, 2) - 2 * Qs(0, 1) + Qs(0, 0)), dq3 = abs(Qs(3, 2) - 2 * Qs(3, 1) + Qs(3, 0));
+  const int dpq0 = dp0 + dq0, dpq3 = dp3 + dq3, dp = dp0 + dp3, dq = dq0 + dq3;
+  if (dpq0 + dpq3 < beta) {
+    auto dsam = [&](int l, int dpq) {
+      return 2 * dpq < (beta >> 2) && abs(Ps(l, 3) - Ps(l, 0)) + abs(Qs(l, 0) - Qs(l, 3)) < (beta >> 3) &&
+             abs(Ps(l, 0) - Qs(l, 0)) < ((5 * tc + 1) >> 1);
+    };
+    const bool strong = dsam(0, dpq0) && dsam(3, dpq3);
+    const bool dep = dp < ((beta + (beta >> 1)) >> 3), deq = dq < ((beta + (beta >> 1)) >> 3);
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      const int p0 = Ps(l, 0), p1 = Ps(l, 1), p2 = Ps(l, 2), p3 = Ps(l, 3);
+      const int q0 = Qs(l, 0), q1 = Qs(l, 1), q2 = Qs(l, 2), q3 = Qs(l, 3);
+      if (strong) {
+        Ps(l, 0) = static_cast<uint16_t>(clip3i(p0 - 2 * tc, p0 + 2 * tc, (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3));
+        Ps(l, 1) = static_cast<uint16_t>(clip3i(p1 - 2 * tc, p1 + 2 * tc, (p2 + p1 + p0 + q0 + 2) >> 2));
+        Ps(l, 2) = static_cast<uint16_t>(clip3i(p2 - 2 * tc, p2 + 2 * tc, (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3));
+        Qs(l, 0) = static_cast<uint16_t>(clip3i(q0 - 2 * tc, q0 + 2 * tc, (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3));
+        Qs(l, 1) = static_cast<uint16_t>(clip3i(q1 - 2 * tc, q1 + 2 * tc, (p0 + q0 + q1 + q2 + 2) >> 2));
+        Qs(l, 2) = static_cast<uint16_t>(clip3i(q2 - 2 * tc, q2 + 2 * tc, (p0 + q0 + q1 + 3 * q2 + 2 * q3 + 4) >> 3));
+      } else {
+        int delta = (9 * (q0 - p0) - 3 * (q1 - p1) + 8) >> 4;
+        if (abs(delta) >= tc * 10) continue;
+        delta = clip3i(-tc, tc, delta);
+        Ps(l, 0) = static_cast<uint16_t>(clip3i(0, maxv, p0 + delta));
+        Qs(l, 0) = static_cast<uint16_t>(clip3i(0, maxv, q0 - delta));
+        if (dep) Ps(l, 1) = static_cast<uint16_t>(clip3i(0, maxv, p1 + clip3i(-(tc >> 1), tc >> 1, (((p2 + p0 + 1) >> 1) - p1 + delta) >> 1)));
+        if (deq) Qs(l, 1) = static_cast<uint16_t>(clip3i(0, maxv, q1 + clip3i(-(tc >> 1), tc >> 1, (((q2 + q0 + 1) >> 1) - q1 - delta) >> 1)));
+      }
+    }
+  }
+  // chroma: bS 2 on the 16-luma-sample grid, 2 chroma lines per luma segment
+  if (bs == 2 && !(pos & 15)) {
+    const int qpc = hevc::chroma_qp_map(qpl);
+    const int tcc = hevc::kTcTable[clip3i(0, 53, qpc + 2)] << (bd - 8);
+    const int cw = W / 2;
+    for (int c = 0; c < 2; ++c) {
+      uint16_t* pc = (c == 0 ? a.u : a.v) + static_cast<size_t>(slot) * cw * (a.H / 2);
+      uint16_t* q = pc + static_cast<size_t>(yq / 2) * cw + xq / 2;
+      const int st = a.dir == 0 ? cw : 1, ac = a.dir == 0 ? 1 : cw;
+#pragma unroll
+      for (int l = 0; l < 2; ++l) {
+        uint16_t* s = q + l * st;
+        const int p0 = s[-ac], p1 = s[-2 * ac], q0 = s[0], q1 = s[ac];
+        const int delta = clip3i(-tcc, tcc, ((((q0 - p0) << 2) + p1 - q1 + 4) >> 3));
+        s[-ac] = static_cast<uint16_t>(clip3i(0, maxv, p0 + delta));
+        s[0] = static_cast<uint16_t>(clip3i(0, maxv, q0 - delta));
+      }
+    }
+  }
+}
+
+// ============================================================== SAO
+struct HevcSaoArgs {
+  int B, W, H, wctb, hctb, bd;
+  const uint16_t *dy, *du, *dv;   // deblocked copy (input)
+  uint16_t *y, *u, *v;            // output (final reconstruction)
+  const uint16_t *sy, *su, *sv;   // source
+  CtuInfo* ctu;
+  const int* qp;
+  const int8_t* run;
+  int enable;
+};
+
+struct SaoShared {
+  int eo_cnt[3][4][4], eo_sum[3][4][4];   // [comp][class][category 1..4]
+  int bo_cnt[3][32], bo_sum[3][32];
+  int type[2], cls[2], band[3];
+  int off[3][4];
+};
+
+__device__ __forceinline__ int sgn(int v) { return (v > 0) - (v < 0); }
+
+__device__ __forceinline__ int sao_round_div(int s, int n) {
+  if (n == 0) return 0;
+  const int a = s < 0 ? -s : s;
+  const int q = (a + n / 2) / n;
+  return s < 0 ? -q : q;
+}
+
+// distortion change of adding offset o to n samples whose source - recon sum is s
+__device__ __forceinline__ long long sao_dd(int n, int s, int o) {
+  return static_cast<long long>(n) * o * o - 2ll * o * s;
+}
+
+__global__ __launch_bounds__(256) void hevc_sao(HevcSaoArgs a) {
+  __shared__ SaoShared S;
+  const int ci = blockIdx.x, slot = blockIdx.y;
+  if (a.run[slot] == 0) return;
+  const int rx = ci % a.wctb, ry = ci / a.wctb;
+  const int tid = threadIdx.x;
+  const int bd = a.bd, maxv = (1 << bd) - 1;
+  for (int i = tid; i < 3 * 16; i += 256) {
+    (&S.eo_cnt[0][0][0])[i] = 0;
+    (&S.eo_sum[0][0][0])[i] = 0;
+  }
+  for (int i = tid; i < 3 * 32; i += 256) {
+    (&S.bo_cnt[0][0])[i] = 0;
+    (&S.bo_sum[0][0])[i] = 0;
+  }
+  __syncthreads();
+  static constexpr int hp[4][2] = {{-1, 1}, {0, 0}, {-1, 1}, {1, -1}};
+  static constexpr int vp[4][2] = {{0, 0}, {-1, 1}, {-1, 1}, {-1, 1}};
+  // ---- statistics (luma 1024 samples, chroma 2 x 256)
+  if (a.enable) {
+    for (int i = tid; i < 1024 + 512; i += 256) {
+      int c, x, y;
+      if (i < 1024) {
+        c = 0;
+        x = i & 31;
+        y = i >> 5;
+      } else {
+        c = 1 + ((i - 1024) >> 8);
+        x = (i - 1024) & 15;
+        y = ((i - 1024) >> 4) & 15;
+      }
+      const int pw = c ? a.W / 2 : a.W, ph = c ? a.H / 2 : a.H, cs = c ? 16 : 32;
+      const size_t ps = static_cast<size_t>(pw) * ph;
+      const uint16_t* d = (c == 0 ? a.dy : (c == 1 ? a.du : a.dv)) + slot * ps;
+      const uint16_t* s = (c == 0 ? a.sy : (c == 1 ? a.su : a.sv)) + slot * ps;
+      const int X = rx * cs + x, Y = ry * cs + y;
+      const int v = d[static_cast<size_t>(Y) * pw + X];
+      const int diff = static_cast<int>(s[static_cast<size_t>(Y) * pw + X]) - v;
+      const int b = v >> (bd - 5);
+      atomicAdd(&S.bo_cnt[c][b], 1);
+      atomicAdd(&S.bo_sum[c][b], diff);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int xa = X + hp[k][0], ya = Y + vp[k][0], xb = X + hp[k][1], yb = Y + vp[k][1];
+        if (xa < 0 || ya < 0 || xb < 0 || yb < 0 || xa >= pw || xb >= pw || ya >= ph || yb >= ph) continue;
+        int e = 2 + sgn(v - d[static_cast<size_t>(ya) * pw + xa]) + sgn(v - d[static_cast<size_t>(yb) * pw + xb]);
+        if (e <= 2) e = (e == 2) ? 0 : e + 1;
+        if (!e) continue;
+        atomicAdd(&S.eo_cnt[c][k][e - 1], 1);
+        atomicAdd(&S.eo_sum[c][k][e - 1], diff);
+      }
+    }
+  }
+  __syncthreads();
+  // ---- decision (thread 0: luma, thread 1: chroma pair)
+  if (tid < 2) {
+    const int qp = a.qp[slot];
+    const double lam = 0.57 * exp2((qp - 12) / 3.0) * static_cast<double>(1 << (2 * (bd - 8)));
+    const int cmax = (1 << (min(bd, 10) - 5)) - 1;
+    const int c0 = tid == 0 ? 0 : 1, nc = tid == 0 ? 1 : 2;
+    double best = 0.0;  // "off": no change, ~1 bit for the type
+    int btype = 0, bcls = 0, bband[2] = {0, 0}, boff[2][4] = {};
+    best = lam * 1.0;
+    if (a.enable) {
+      for (int k = 0; k < 4; ++k) {  // edge offset classes
+        double cost = lam * (1 + 2);
+        int o[2][4];
+        for (int cc = 0; cc < nc; ++cc) {
+          const int c = c0 + cc;
+          for (int e = 0; e < 4; ++e) {
+            int v = sao_round_div(S.eo_sum[c][k][e], S.eo_cnt[c][k][e]);
+            v = e < 2 ? clampi(v, 0, cmax) : clampi(v, -cmax, 0);
+            // shrink while it does not pay
+            while (v != 0) {
+              const double d0 = static_cast<double>(sao_dd(S.eo_cnt[c][k][e], S.eo_sum[c][k][e], v)) + lam * (v < 0 ? -v : v);
+              const int v2 = v > 0 ? v - 1 : v + 1;
+              const double d1 = static_cast<double>(sao_dd(S.eo_cnt[c][k][e], S.eo_sum[c][k][e], v2)) + lam * (v2 < 0 ? -v2 : v2);
+              if (d1 <= d0) v = v2;
+              else break;
+            }
+            o[cc][e] = v;
+            cost += static_cast<double>(sao_dd(S.eo_cnt[c][k][e], S.eo_sum[c][k][e], v)) + lam * ((v < 0 ? -v : v) + 1);
+          }
+        }
+        if (cost < best) {
+          best = cost;
+          btype = 2;
+          bcls = k;
+          for (int cc = 0; cc < nc; ++cc)
+            for (int e = 0; e < 4; ++e) boff[cc][e] = o[cc][e];
+        }
+      }
+      {  // band offset: best 4-band window per component
+        double cost = lam * 1;
+        int o[2][4], pos[2];
+        for (int cc = 0; cc < nc; ++cc) {
+          const int c = c0 + cc;
+          double bestw = 1e300;
+          int bpos = 0, bo[4] = {};
+          for (int p = 0; p < 32; ++p) {
+            double w = lam * 5;
+            int oo[4];
+            for (int k = 0; k < 4; ++k) {
+              const int b = (p + k) & 31;
+              int v = clampi(sao_round_div(S.bo_sum[c][b], S.bo_cnt[c][b]), -cmax, cmax);
+              const double dv = static_cast<double>(sao_dd(S.bo_cnt[c][b], S.bo_sum[c][b], v)) + lam * ((v < 0 ? -v : v) + (v != 0));
+              if (dv > lam) v = 0;
+              oo[k] = v;
+              w += v ? static_cast<double>(sao_dd(S.bo_cnt[c][b], S.bo_sum[c][b], v)) + lam * ((v < 0 ? -v : v) + 1) : lam;
+            }
+            if (w < bestw) {
+              bestw = w;
+              bpos = p;
+              for (int k = 0; k < 4; ++k) bo[k] = oo[k];
+            }
+          }
+          cost += bestw;
+          pos[cc] = bpos;
+          for (int k = 0; k < 4; ++k) o[cc][k] = bo[k];
+        }
+        if (cost < best) {
+          best = cost;
+          btype = 1;
+          for (int cc = 0; cc < nc; ++cc) {
+            bband[cc] = pos[cc];
+            for (int k = 0; k < 4; ++k) boff[cc][k] = o[cc][k];
+          }
+        }
+      }
+    }
+    S.type[tid] = btype;
+    S.cls[tid] = bcls;
+    for (int cc = 0; cc < nc; ++cc) {
+      S.band[c0 + cc] = bband[cc];
+      for (int k = 0; k < 4; ++k) S.off[c0 + cc][k] = boff[cc][k];
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    CtuInfo* t = a.ctu + static_cast<size_t>(slot) * a.wctb * a.hctb + ci;
+    for (int k = 0; k < 2; ++k) {
+      t->sao_type[k] = static_cast<uint8_t>(S.type[k]);
+      t->sao_class[k] = static_cast<uint8_t>(S.cls[k]);
+    }
+    for (int c = 0; c < 3; ++c) {
+      t->sao_band[c] = static_cast<uint8_t>(S.band[c]);
+      for (int k = 0; k < 4; ++k) t->sao_off[c][k] = static_cast<int8_t>(S.type[c ? 1 : 0] ? S.off[c][k] : 0);
+    }
+  }
+  // ---- apply (reads the deblocked copy, writes the output)
+  for (int i = tid; i < 1024 + 512; i += 256) {
+    int c, x, y;
+    if (i < 1024) {
+      c = 0;
+      x = i & 31;
+      y = i >> 5;
+    } else {
+      c = 1 + ((i - 1024) >> 8);
+      x = (i - 1024) & 15;
+      y = ((i - 1024) >> 4) & 15;
+    }
+    const int pw = c ? a.W / 2 : a.W, ph = c ? a.H / 2 : a.H, cs = c ? 16 : 32;
+    const size_t ps = static_cast<size_t>(pw) * ph;
+    const uint16_t* d = (c == 0 ? a.dy : (c == 1 ? a.du : a.dv)) + slot * ps;
+    uint16_t* o = (c == 0 ? a.y : (c == 1 ? a.u : a.v)) + slot * ps;
+    const int X = rx * cs + x, Y = ry * cs + y;
+    const int v = d[static_cast<size_t>(Y) * pw + X];
+    const int type = S.type[c ? 1 : 0];
+    int r = v;
+    if (type == 1) {
+      const int k = ((v >> (bd - 5)) - S.band[c]) & 31;
+      if (k < 4) r = clampi(v + S.off[c][k], 0, maxv);
+    } else if (type == 2) {
+      const int k = S.cls[c ? 1 : 0];
+      const int xa = X + hp[k][0], ya = Y + vp[k][0], xb = X + hp[k][1], yb = Y + vp[k][1];
+      if (!(xa < 0 || ya < 0 || xb < 0 || yb < 0 || xa >= pw || xb >= pw || ya >= ph || yb >= ph)) {
+        int e = 2 + sgn(v - d[static_cast<size_t>(ya) * pw + xa]) + sgn(v - d[static_cast<size_t>(yb) * pw + xb]);
+        if (e <= 2) e = (e == 2) ? 0 : e + 1;
+        if (e) r = clampi(v + S.off[c][e - 1], 0, maxv);
+      }
+    }
+    o[static_cast<size_t>(Y) * pw + X] = static_cast<uint16_t>(r);
+  }
+}
+
+}  // namespace gpu
+}  // namespace mivc
+
+using namespace mivc::gpu;
+
+extern "C" void mivc_launch_hevc_prep(int B, const void* src, long long slot_stride, int pitch, int bps, int w, int h,
+                                      uint16_t* dst, int W, int H, int shift, void* stream) {
+  dim3 grid((W + 255) / 256, H, B);
+  hipLaunchKernelGGL(hevc_prep_plane, grid, dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const uint8_t*>(src), slot_stride, pitch, bps, w, h, dst, W, H, shift);
+}
+
+extern "C" void mivc_launch_hevc_deblock(int B, int W, int H, int bd, uint16_t* y, uint16_t* u, uint16_t* v,
+                                         const void* cu, const int* qp, const int8_t* run, void* stream) {
+  HevcDbkArgs a{B, W, H, W / 32, bd, y, u, v, static_cast<const CuInfo*>(cu), qp, run, 0};
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int nv = (W / 8 - 1) * (H / 4), nh = (W / 4) * (H / 8 - 1);
+  if (nv > 0) hipLaunchKernelGGL(hevc_deblock, dim3((nv + 255) / 256, B), dim3(256), 0, s, a);
+  a.dir = 1;
+  if (nh > 0) hipLaunchKernelGGL(hevc_deblock, dim3((nh + 255) / 256, B), dim3(256), 0, s, a);
+}
+
+extern "C" void mivc_launch_hevc_sao(int B, int W, int H, int bd, const uint16_t* dy, const uint16_t* du,
+                                     const uint16_t* dv, uint16_t* y, uint16_t* u, uint16_t* v, const uint16_t* sy,
+                                     const uint16_t* su, const uint16_t* sv, void* ctu, const int* qp,
+                                     const int8_t* run, int enable, void* stream) {
+  HevcSaoArgs a{B, W, H, W / 32, H / 32, bd, dy, du, dv, y, u, v, sy, su, sv, static_cast<CtuInfo*>(ctu), qp, run, enable};
+  hipLaunchKernelGGL(hevc_sao, dim3((W / 32) * (H / 32), B), dim3(256), 0, static_cast<hipStream_t>(stream), a);
+}

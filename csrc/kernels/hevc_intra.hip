@@ -1,0 +1,508 @@
+// HEVC intra coding on gfx950: open-loop analysis + closed-loop
+// reconstruction.
+//
+// * hevc_intra_analyze (grid = CTBs x slots, 256 threads): every CU of the 32/16/8
+//   quadtree x all 35 modes is predicted from *source* neighbours (normative
+//   availability, substitution and filtering) and costed with 8x8 Hadamard SATD; the
+//   CTB then picks the best mode per CU and the split that minimises SATD + lambda *
+//   bits.  No dependency between CTBs: the whole picture is analysed in parallel.
+// * hevc_intra_recon (grid = slots, 8 waves per workgroup): CTBs in wavefront order
+//   (MB-row progress counters in LDS, 2-CTB lag as the H.264 kernels), CUs in z-order
+//   inside a CTB: reference samples from the reconstruction, prediction, forward
+//   transform, quantisation, dequantisation and the normative inverse transform
+//   (wave-level matrix products in LDS, hevc_common.h).  In P pictures only intra
+//   CUs are visited (inter CUs were reconstructed by hevc_inter).
+#include "hevc_common.h"
+
+namespace mivc {
+namespace gpu {
+
+using hevc::CtuInfo;
+using hevc::CuInfo;
+using hevc::zorder8;
+
+struct HevcGeom {
+  int B, W, H, wctb, hctb;
+  __host__ __device__ size_t ysize() const { return static_cast<size_t>(W) * H; }
+  __host__ __device__ size_t csize() const { return static_cast<size_t>(W / 2) * (H / 2); }
+  __host__ __device__ int nctb() const { return wctb * hctb; }
+};
+
+struct HevcIntraArgs {
+  HevcGeom g;
+  const uint16_t *src_y, *src_u, *src_v;  // [B] padded source planes
+  uint16_t *rec_y, *rec_u, *rec_v;        // [B] reconstruction (unfiltered)
+  CtuInfo* ctu;                           // [B, nctb]
+  CuInfo* cu;                             // [B, nctb * 16]
+  int16_t *coef_y, *coef_u, *coef_v;      // [B] level planes
+  const int* qp;                          // [B] QpY
+  const int8_t* run;                      // [B] 0 idle, 1 all CUs (I picture), 2 intra CUs only (P picture)
+  int bd;
+  int* err;
+};
+
+// luma neighbour (xr, yr) of a CTB-relative CU position: z-scan availability (6.4.1)
+// at 8x8 granularity; zcur = z-order index of the current CU's first granule
+__device__ __forceinline__ bool nb_avail(int xr, int yr, int zcur, int rx, int ry, int wctb) {
+  if (yr < 0) {
+    if (ry == 0) return false;
+    if (xr < 0) return rx > 0;
+    if (xr >= 32) return rx + 1 < wctb && xr < 64;
+    return true;
+  }
+  if (yr >= 32) return false;
+  if (xr < 0) return rx > 0;
+  if (xr >= 32) return false;
+  return zorder8(xr >> 3, yr >> 3) < zcur;
+}
+
+__device__ __forceinline__ void ref_pos(int i, int n, int cx, int cy, int* x, int* y) {
+  if (i < 2 * n) {
+    *x = cx - 1;
+    *y = cy + 2 * n - 1 - i;
+  } else if (i == 2 * n) {
+    *x = cx - 1;
+    *y = cy - 1;
+  } else {
+    *x = cx + i - 2 * n - 1;
+    *y = cy - 1;
+  }
+}
+
+__device__ __forceinline__ int lambda_satd(int qp, int bd) {
+  return static_cast<int>(0.755f * exp2f((qp - 12) / 6.0f) * static_cast<float>(1 << (bd - 8)) + 0.5f);
+}
+
+// 8x8 Hadamard SATD (x265 / HM normalisation: (sum |H| + 2) >> 2)
+__device__ __forceinline__ int satd8x8(int (&d)[64]) {
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    int* v = d + r * 8;
+#pragma unroll
+    for (int s = 1; s < 8; s <<= 1)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (!(i & s)) {
+          const int a = v[i], b = v[i + s];
+          v[i] = a + b;
+          v[i + s] = a - b;
+        }
+  }
+  int sum = 0;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+#pragma unroll
+    for (int s = 1; s < 8; s <<= 1)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (!(i & s)) {
+          const int a = d[i * 8 + c], b = d[(i + s) * 8 + c];
+          d[i * 8 + c] = a + b;
+          d[(i + s) * 8 + c] = a - b;
+        }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sum += abs(d[i * 8 + c]);
+  }
+  return (sum + 2) >> 2;
+}
+
+// ============================================================== analysis
+constexpr int kCuCount = 21;  // 1 x 32, 4 x 16, 16 x 8
+struct AnalyzeShared {
+  int16_t ext[65 * 65];        // source samples, x, y in [-1, 63] relative to the CTB
+  int refs[2][917];            // per CU: unfiltered / filtered reference arrays
+  int cost[kCuCount][36];
+  int dc[kCuCount];
+  int best_mode[kCuCount], best_cost[kCuCount];
+};
+
+__device__ __forceinline__ void cu_of(int c, int* cx, int* cy, int* n, int* off) {
+  if (c == 0) {
+    *cx = 0;
+    *cy = 0;
+    *n = 32;
+    *off = 0;
+  } else if (c < 5) {
+    const int q = c - 1;
+    *cx = (q & 1) * 16;
+    *cy = (q >> 1) * 16;
+    *n = 16;
+    *off = 129 + q * 65;
+  } else {
+    const int k = c - 5;  // z-order of the 8x8 CU inside the CTB
+    *cx = ((k & 1) | ((k >> 1) & 2)) * 8;
+    *cy = (((k >> 1) & 1) | ((k >> 2) & 2)) * 8;
+    *n = 8;
+    *off = 129 + 4 * 65 + k * 33;
+  }
+}
+
+__global__ __launch_bounds__(256) void hevc_intra_analyze(HevcIntraArgs a) {
+  __shared__ AnalyzeShared S;
+  const HevcGeom& g = a.g;
+  const int ci = blockIdx.x, slot = blockIdx.y;
+  if (a.run[slot] == 0) return;
+  const int rx = ci % g.wctb, ry = ci / g.wctb;
+  const int X0 = rx * 32, Y0 = ry * 32;
+  const int tid = threadIdx.x;
+  const int bd = a.bd, maxv = (1 << bd) - 1;
+  const uint16_t* src = a.src_y + slot * g.ysize();
+  for (int i = tid; i < 65 * 65; i += 256) {
+    const int y = i / 65 - 1, x = i % 65 - 1;
+    const int xx = clampi(X0 + x, 0, g.W - 1), yy = clampi(Y0 + y, 0, g.H - 1);
+    S.ext[i] = static_cast<int16_t>(src[static_cast<size_t>(yy) * g.W + xx]);
+  }
+  for (int i = tid; i < kCuCount * 36; i += 256) (&S.cost[0][0])[i] = 0;
+  __syncthreads();
+  // reference arrays of the 21 CUs: availability + serial substitution, one thread per CU
+  if (tid < kCuCount) {
+    int cx, cy, n, off;
+    cu_of(tid, &cx, &cy, &n, &off);
+    const int zc = zorder8(cx >> 3, cy >> 3);
+    const int E = 4 * n + 1;
+    int* p = S.refs[0] + off;
+    int first = -1;
+    for (int i = 0; i < E; ++i) {
+      int x, y;
+      ref_pos(i, n, cx, cy, &x, &y);
+      if (nb_avail(x, y, zc, rx, ry, g.wctb)) {
+        p[i] = S.ext[(y + 1) * 65 + x + 1];
+        if (first < 0) first = i;
+      } else {
+        p[i] = -1;
+      }
+    }
+    if (first < 0) {
+      for (int i = 0; i < E; ++i) p[i] = 1 << (bd - 1);
+    } else {
+      if (p[0] < 0) p[0] = p[first];
+      for (int i = 1; i < E; ++i)
+        if (p[i] < 0) p[i] = p[i - 1];
+    }
+    // filtered copy (8.4.4.2.3; strong smoothing for 32x32)
+    int* q = S.refs[1] + off;
+    const int c = 2 * n, tl = p[c], bl = p[0], tr = p[E - 1];
+    const bool bi = n == 32 && abs(tl + tr - 2 * p[c + n]) < (1 << (bd - 5)) && abs(tl + bl - 2 * p[c - n]) < (1 << (bd - 5));
+    for (int i = 0; i < E; ++i) {
+      if (i == 0 || i == E - 1) q[i] = p[i];
+      else if (bi) q[i] = i == c ? tl : (i < c ? ((63 - (c - 1 - i)) * tl + (c - i) * bl + 32) >> 6
+                                              : ((63 - (i - c - 1)) * tl + (i - c) * tr + 32) >> 6);
+      else q[i] = (p[i - 1] + 2 * p[i] + p[i + 1] + 2) >> 2;
+    }
+    int s = n;
+    for (int k = 0; k < n; ++k) s += p[c + 1 + k] + p[c - 1 - k];
+    const int lg = n == 32 ? 5 : (n == 16 ? 4 : 3);
+    S.dc[tid] = s >> (lg + 1);
+  }
+  __syncthreads();
+  // SATD of every (CU, mode, 8x8 block)
+  for (int it = tid; it < 3 * 560; it += 256) {
+    const int level = it / 560, j = it % 560;
+    const int mode = j >> 4, k = j & 15;
+    int c, bx, by;
+    if (level == 0) {
+      c = 0;
+      bx = k & 3;
+      by = k >> 2;
+    } else if (level == 1) {
+      c = 1 + (k >> 2);
+      bx = k & 1;
+      by = (k >> 1) & 1;
+    } else {
+      c = 5 + k;
+      bx = 0;
+      by = 0;
+    }
+    int cx, cy, n, off;
+    cu_of(c, &cx, &cy, &n, &off);
+    const int lg = n == 32 ? 5 : (n == 16 ? 4 : 3);
+    const int* p = S.refs[hv::intra_filter_flag(mode, n) ? 1 : 0] + off;
+    const int dc = S.dc[c];
+    int d[64];
+#pragma unroll
+    for (int y = 0; y < 8; ++y)
+#pragma unroll
+      for (int x = 0; x < 8; ++x) {
+        const int px = bx * 8 + x, py = by * 8 + y;
+        const int pv = hv::intra_pred_sample(p, n, lg, mode, px, py, dc, n < 32, maxv);
+        d[y * 8 + x] = S.ext[(cy + py + 1) * 65 + cx + px + 1] - pv;
+      }
+    atomicAdd(&S.cost[c][mode], satd8x8(d));
+  }
+  __syncthreads();
+  const int qp = a.qp[slot];
+  const int lam = lambda_satd(qp, bd);
+  if (tid < kCuCount) {
+    int bm = 0, bc = 0x7FFFFFFF;
+    for (int m = 0; m < 35; ++m) {
+      const int cst = S.cost[tid][m] + lam * (m < 2 ? 3 : 5);
+      if (cst < bc) {
+        bc = cst;
+        bm = m;
+      }
+    }
+    S.best_mode[tid] = bm;
+    S.best_cost[tid] = bc + lam * 4;  // CU overhead: split flag, chroma mode, cbfs
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int split = 0, c16sum = 0;
+    for (int q = 0; q < 4; ++q) {
+      int s8 = 0;
+      for (int r = 0; r < 4; ++r) s8 += S.best_cost[5 + q * 4 + r];
+      const int c16 = S.best_cost[1 + q];
+      if (s8 < c16) {
+        split |= 1 << (1 + q);
+        c16sum += s8;
+      } else {
+        c16sum += c16;
+      }
+    }
+    if (c16sum < S.best_cost[0]) split |= 1;
+    else split = 0;
+    CtuInfo* t = a.ctu + static_cast<size_t>(slot) * g.nctb() + ci;
+    t->split = static_cast<uint8_t>(split);
+    t->qp = static_cast<int8_t>(qp);
+    S.best_cost[0] = split;  // broadcast
+  }
+  __syncthreads();
+  if (tid < 16) {
+    const int split = S.best_cost[0];
+    // granule z-index tid -> the chosen CU covering it
+    const int gx = (tid & 1) | ((tid >> 1) & 2), gy = ((tid >> 1) & 1) | ((tid >> 2) & 2);
+    const int q = (gx >> 1) + 2 * (gy >> 1);
+    int m, lg;
+    if (!(split & 1)) {
+      m = S.best_mode[0];
+      lg = 5;
+    } else if (!((split >> (1 + q)) & 1)) {
+      m = S.best_mode[1 + q];
+      lg = 4;
+    } else {
+      m = S.best_mode[5 + tid];
+      lg = 3;
+    }
+    CuInfo c{};
+    c.pred = hevc::CU_INTRA;
+    c.mode = static_cast<uint8_t>(m);
+    c.flags = static_cast<uint8_t>((lg - 3) << 1);
+    a.cu[(static_cast<size_t>(slot) * g.nctb() + ci) * 16 + tid] = c;
+  }
+}
+
+// ============================================================== closed-loop reconstruction
+constexpr int kHevcIntraWaves = 8;
+constexpr int RT = 65;  // recon tile stride (x = -1 .. 63)
+constexpr int CT2 = 33; // chroma recon tile stride (x = -1 .. 31)
+
+struct ReconShared {
+  uint16_t rt[33 * RT];          // luma: row 0 = y -1 (x -1..63), rows 1..32 = y 0..31, col 0 = x -1
+  uint16_t rc[2][17 * CT2];      // chroma tiles, same layout (x -1..31, y -1..15)
+  int p[129], q[129];            // reference arrays (unfiltered, filtered)
+  int R[32 * 32], S[32 * 32];    // residual / transform scratch
+  uint16_t pred[32 * 32];
+  int saved_x;
+  uint16_t saved_y[32];
+  uint16_t saved_c[2][16];
+};
+
+// reconstruct one CU component: refs from the LDS tile, predict, transform/quantise, store
+template <bool LUMA>
+__device__ __forceinline__ bool recon_block(const HevcIntraArgs& a, ReconShared& S, const hv::DctLds& D, int slot,
+                                            int comp, int rx, int ry, int cx, int cy, int log2n, int mode, int zc, int qpp) {
+  const HevcGeom& g = a.g;
+  const int lane = lane_id();
+  const int n = 1 << log2n;
+  const int bd = a.bd, maxv = (1 << bd) - 1;
+  const int sc = LUMA ? 0 : 1;  // component -> luma coordinate shift
+  const int stride = LUMA ? RT : CT2;
+  uint16_t* tile = LUMA ? S.rt : S.rc[comp - 1];
+  // 1. reference samples (availability from the luma granule of each sample)
+  hv::build_refs(S.p, n, bd,
+                 [&](int i) {
+                   int x, y;
+                   ref_pos(i, n, cx, cy, &x, &y);
+                   return nb_avail(x << sc, y << sc, zc, rx, ry, g.wctb);
+                 },
+                 [&](int i) {
+                   int x, y;
+                   ref_pos(i, n, cx, cy, &x, &y);
+                   return static_cast<int>(tile[(y + 1) * stride + x + 1]);
+                 });
+  const int* p = S.p;
+  if (LUMA && hv::intra_filter_flag(mode, n)) {
+    hv::filter_refs(S.p, S.q, n, bd, true);
+    p = S.q;
+  }
+  const int dc = hv::intra_dc(p, n, log2n);
+  // 2. prediction and residual
+  const uint16_t* src = (LUMA ? a.src_y : (comp == 1 ? a.src_u : a.src_v)) + slot * (LUMA ? g.ysize() : g.csize());
+  const int pw = LUMA ? g.W : g.W / 2;
+  const int X0 = (rx * 32 >> sc) + cx, Y0 = (ry * 32 >> sc) + cy;
+  for (int i = lane; i < n * n; i += 64) {
+    const int x = i & (n - 1), y = i >> log2n;
+    const int pv = hv::intra_pred_sample(p, n, log2n, mode, x, y, dc, LUMA && n < 32, maxv);
+    S.pred[i] = static_cast<uint16_t>(pv);
+    S.R[y * 32 + x] = static_cast<int>(src[static_cast<size_t>(Y0 + y) * pw + X0 + x]) - pv;
+  }
+  wave_sync();
+  // 3. transform / quantisation / reconstruction
+  int16_t* lev = (LUMA ? a.coef_y : (comp == 1 ? a.coef_u : a.coef_v)) + slot * (LUMA ? g.ysize() : g.csize()) +
+                 static_cast<size_t>(Y0) * pw + X0;
+  hv::TqParams tp{log2n, bd, qpp, true};
+  const bool nz = hv::transform_quant_block(D, S.R, S.S, lev, pw, tp);
+  uint16_t* rec = (LUMA ? a.rec_y : (comp == 1 ? a.rec_u : a.rec_v)) + slot * (LUMA ? g.ysize() : g.csize());
+  for (int i = lane; i < n * n; i += 64) {
+    const int x = i & (n - 1), y = i >> log2n;
+    int v = S.pred[i] + (nz ? S.R[y * 32 + x] : 0);
+    v = v < 0 ? 0 : (v > maxv ? maxv : v);
+    tile[(cy + y + 1) * stride + cx + x + 1] = static_cast<uint16_t>(v);
+    rec[static_cast<size_t>(Y0 + y) * pw + X0 + x] = static_cast<uint16_t>(v);
+  }
+  wave_sync();
+  return nz;
+}
+
+__device__ void hevc_recon_ctb(const HevcIntraArgs& a, ReconShared& S, const hv::DctLds& D, int slot, int rx, int ry,
+                               int run) {
+  const HevcGeom& g = a.g;
+  const int lane = lane_id();
+  const int X0 = rx * 32, Y0 = ry * 32;
+  const size_t cb = static_cast<size_t>(slot) * g.nctb() + ry * g.wctb + rx;
+  const uint16_t* recy = a.rec_y + slot * g.ysize();
+  const uint16_t* recu = a.rec_u + slot * g.csize();
+  const uint16_t* recv = a.rec_v + slot * g.csize();
+  const int cw = g.W / 2;
+  // ---- stage the neighbourhood: row above (x -1..63), left column, and (P) the CTB interior
+  for (int i = lane; i < 65; i += 64) {
+    const int x = X0 - 1 + i;
+    S.rt[i] = (ry > 0 && x >= 0 && x < g.W) ? recy[static_cast<size_t>(Y0 - 1) * g.W + x] : 0;
+  }
+  if (lane < 32) {
+    uint16_t v = 0;
+    if (rx > 0) v = S.saved_x == rx - 1 ? S.saved_y[lane] : recy[static_cast<size_t>(Y0 + lane) * g.W + X0 - 1];
+    S.rt[(lane + 1) * RT] = v;
+  } else {
+    const int c = (lane - 32) >> 4, i = (lane - 32) & 15;
+    const uint16_t* rc = c == 0 ? recu : recv;
+    uint16_t v = 0;
+    if (rx > 0) v = S.saved_x == rx - 1 ? S.saved_c[c][i] : rc[static_cast<size_t>(Y0 / 2 + i) * cw + X0 / 2 - 1];
+    S.rc[c][(i + 1) * CT2] = v;
+  }
+  for (int i = lane; i < 2 * 33; i += 64) {
+    const int c = i / 33, k = i % 33;
+    const uint16_t* rc = c == 0 ? recu : recv;
+    const int x = X0 / 2 - 1 + k;
+    S.rc[c][k] = (ry > 0 && x >= 0 && x < cw) ? rc[static_cast<size_t>(Y0 / 2 - 1) * cw + x] : 0;
+  }
+  if (run == 2) {  // P picture: inter CUs of this CTB are already reconstructed
+    for (int i = lane; i < 32 * 32; i += 64) {
+      const int y = i >> 5, x = i & 31;
+      S.rt[(y + 1) * RT + x + 1] = recy[static_cast<size_t>(Y0 + y) * g.W + X0 + x];
+    }
+    for (int i = lane; i < 2 * 256; i += 64) {
+      const int c = i >> 8, k = i & 255, y = k >> 4, x = k & 15;
+      S.rc[c][(y + 1) * CT2 + x + 1] = (c == 0 ? recu : recv)[static_cast<size_t>(Y0 / 2 + y) * cw + X0 / 2 + x];
+    }
+  }
+  wave_sync();
+  const int split = __builtin_amdgcn_readfirstlane(a.ctu[cb].split);
+  const int qpy = a.qp[slot];
+  const int off = 6 * (a.bd - 8);
+  const int qpl = qpy + off;
+  const int qpc = hevc::chroma_qp_map(clampi(qpy, -off, 57)) + off;
+  // ---- CUs in z-order
+  for (int k = 0; k < 16;) {
+    const int q = k >> 2;
+    int log2n;
+    if (!(split & 1)) log2n = 5;
+    else if (!((split >> (1 + q)) & 1)) log2n = 4;
+    else log2n = 3;
+    const int step = 1 << (2 * (log2n - 3));  // granules covered
+    CuInfo* cu = a.cu + cb * 16 + k;
+    const int pred = __builtin_amdgcn_readfirstlane(cu->pred);
+    if (run == 1 || pred == hevc::CU_INTRA) {
+      const int mode = __builtin_amdgcn_readfirstlane(cu->mode);
+      const int gx = (k & 1) | ((k >> 1) & 2), gy = ((k >> 1) & 1) | ((k >> 2) & 2);
+      const int cx = gx * 8, cy = gy * 8;
+      const bool ny = recon_block<true>(a, S, D, slot, 0, rx, ry, cx, cy, log2n, mode, k, qpl);
+      const bool nu = recon_block<false>(a, S, D, slot, 1, rx, ry, cx / 2, cy / 2, log2n - 1, mode, k, qpc);
+      const bool nv = recon_block<false>(a, S, D, slot, 2, rx, ry, cx / 2, cy / 2, log2n - 1, mode, k, qpc);
+      if (lane < step) {
+        CuInfo* c = a.cu + cb * 16 + k + lane;
+        c->cbf = static_cast<uint8_t>(ny | (nu << 1) | (nv << 2));
+        c->pred = hevc::CU_INTRA;
+      }
+    }
+    k += step;
+  }
+  // ---- keep this CTB's right column for the next CTB of the row
+  if (lane < 32) S.saved_y[lane] = S.rt[(lane + 1) * RT + 32];
+  else {
+    const int c = (lane - 32) >> 4, i = (lane - 32) & 15;
+    S.saved_c[c][i] = S.rc[c][(i + 1) * CT2 + 16];
+  }
+  if (lane == 0) S.saved_x = rx;
+  wave_sync();
+}
+
+__global__ __launch_bounds__(64 * kHevcIntraWaves) void hevc_intra_recon(HevcIntraArgs a) {
+  __shared__ ReconShared SS[kHevcIntraWaves];
+  __shared__ hv::DctLds D;
+  __shared__ int prog[kMaxRows];
+  const HevcGeom& g = a.g;
+  const int slot = blockIdx.x;
+  const int run = a.run[slot];
+  if (run == 0) return;
+  hv::dct_lds_init(D);
+  for (int i = threadIdx.x; i < g.hctb; i += blockDim.x) prog[i] = 0;
+  const int w = wave_id();
+  if (lane_id() == 0) SS[w].saved_x = -2;
+  __syncthreads();
+  ReconShared& S = SS[w];
+  for (int y = w; y < g.hctb; y += kHevcIntraWaves) {
+    for (int x = 0; x < g.wctb; ++x) {
+      if (y > 0) row_wait(prog, y - 1, min(x + 2, g.wctb), a.err);
+      hevc_recon_ctb(a, S, D, slot, x, y, run);
+      row_publish(prog, y, x + 1);
+    }
+  }
+}
+
+}  // namespace gpu
+}  // namespace mivc
+
+using namespace mivc::gpu;
+
+static HevcIntraArgs make_intra_args(int B, int W, int H, const uint16_t* sy, const uint16_t* su, const uint16_t* sv,
+                                     uint16_t* ry, uint16_t* ru, uint16_t* rv, void* ctu, void* cu, int16_t* cy,
+                                     int16_t* cu_, int16_t* cv, const int* qp, const int8_t* run, int bd, int* err) {
+  HevcIntraArgs a;
+  a.g = HevcGeom{B, W, H, W / 32, H / 32};
+  a.src_y = sy;
+  a.src_u = su;
+  a.src_v = sv;
+  a.rec_y = ry;
+  a.rec_u = ru;
+  a.rec_v = rv;
+  a.ctu = static_cast<CtuInfo*>(ctu);
+  a.cu = static_cast<CuInfo*>(cu);
+  a.coef_y = cy;
+  a.coef_u = cu_;
+  a.coef_v = cv;
+  a.qp = qp;
+  a.run = run;
+  a.bd = bd;
+  a.err = err;
+  return a;
+}
+
+extern "C" void mivc_launch_hevc_intra(int B, int W, int H, const uint16_t* sy, const uint16_t* su, const uint16_t* sv,
+                                       uint16_t* ry, uint16_t* ru, uint16_t* rv, void* ctu, void* cu, int16_t* cy,
+                                       int16_t* cu_, int16_t* cv, const int* qp, const int8_t* run, int bd, int analyze,
+                                       int* err, void* stream) {
+  HevcIntraArgs a = make_intra_args(B, W, H, sy, su, sv, ry, ru, rv, ctu, cu, cy, cu_, cv, qp, run, bd, err);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (analyze) hipLaunchKernelGGL(hevc_intra_analyze, dim3(a.g.nctb(), B), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(hevc_intra_recon, dim3(B), dim3(64 * kHevcIntraWaves), 0, s, a);
+}
