@@ -12,6 +12,15 @@
 
 namespace mivc {
 namespace gpu {
+
+// batched HEVC picture geometry (coded size, multiple of the 32x32 CTB)
+struct HevcGeom {
+  int B, W, H, wctb, hctb;
+  __host__ __device__ size_t ysize() const { return static_cast<size_t>(W) * H; }
+  __host__ __device__ size_t csize() const { return static_cast<size_t>(W / 2) * (H / 2); }
+  __host__ __device__ int nctb() const { return wctb * hctb; }
+};
+
 namespace hv {
 
 using hevc::dct_coef;

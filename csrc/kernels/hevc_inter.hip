@@ -1,0 +1,291 @@
+// HEVC P pictures on gfx950.
+//
+// Motion comes from the batched motion-estimation kernel (me.hip) run on 8-bit
+// proxies of the source and the reference reconstruction (one vector per 16x16
+// block).  Here:
+//
+// * hevc_p_decide (grid = CTBs x slots, one wave): per 16x16 quadrant, inter (ME
+//   cost) versus the best intra choice of the open-loop analysis (16x16 or four
+//   8x8); four inter quadrants with one vector become a 32x32 inter CU.  Writes the
+//   CTB split and the CU records (the CABAC writer turns zero-residual CUs whose
+//   vector equals a merge candidate into skip CUs).
+// * hevc_inter_cu (grid = CTBs*4 x slots, one wave per 16x16 quadrant or 32x32
+//   CU): normative HEVC motion compensation (8-tap luma, 4-tap chroma, separable
+//   through LDS, default weighted prediction), transform / quantisation with the
+//   inter rounding offset, reconstruction.  No dependency between CUs: fully
+//   parallel; the intra CUs of the picture are then coded by hevc_intra_recon.
+#include "hevc_common.h"
+
+namespace mivc {
+namespace gpu {
+
+using hevc::CtuInfo;
+using hevc::CuInfo;
+
+struct HevcInterArgs {
+  HevcGeom g;
+  const uint16_t *src_y, *src_u, *src_v;
+  const uint16_t *ref_y, *ref_u, *ref_v;
+  uint16_t *rec_y, *rec_u, *rec_v;
+  CtuInfo* ctu;
+  CuInfo* cu;
+  int16_t *coef_y, *coef_u, *coef_v;
+  const int* qp;
+  const int8_t* run;
+  const int* cand;       // [B, nctb, 2, 21] intra analysis: best cost / mode per CU
+  const int16_t* mv;     // [B, nmb16, 2] quarter-sample vectors per 16x16 block
+  const int* me_cost;    // [B, nmb16] (8-bit proxy units)
+  int bd;
+};
+
+__device__ __forceinline__ int lambda_satd_i(int qp, int bd) {
+  return static_cast<int>(0.755f * exp2f((qp - 12) / 6.0f) * static_cast<float>(1 << (bd - 8)) + 0.5f);
+}
+
+// ============================================================== decision
+__global__ __launch_bounds__(64) void hevc_p_decide(HevcInterArgs a) {
+  const HevcGeom& g = a.g;
+  const int ci = blockIdx.x, slot = blockIdx.y;
+  if (a.run[slot] != 2) return;
+  const int lane = threadIdx.x;
+  const int rx = ci % g.wctb, ry = ci / g.wctb;
+  const size_t cb = static_cast<size_t>(slot) * g.nctb() + ci;
+  const int* cd = a.cand + cb * 42;
+  const int wmb = g.W / 16, nmb = wmb * (g.H / 16);
+  const int qp = a.qp[slot];
+  const int lam = lambda_satd_i(qp, a.bd);
+  __shared__ int s_inter[4], s_mvx[4], s_mvy[4], s_split8[4], s_intra[4];
+  __shared__ int s_split;
+  if (lane < 4) {
+    const int q = lane;
+    const int mb = (ry * 2 + (q >> 1)) * wmb + rx * 2 + (q & 1);
+    const size_t o = static_cast<size_t>(slot) * nmb + mb;
+    const int inter = (a.me_cost[o] << (a.bd - 8)) + lam * 3;
+    int s8 = 0;
+    for (int r = 0; r < 4; ++r) s8 += cd[5 + q * 4 + r];
+    const int c16 = cd[1 + q];
+    s_split8[q] = s8 < c16;
+    s_intra[q] = s8 < c16 ? s8 : c16;
+    s_inter[q] = inter;
+    s_mvx[q] = a.mv[o * 2];
+    s_mvy[q] = a.mv[o * 2 + 1];
+  }
+  __syncthreads();
+  if (lane == 0) {
+    int n_inter = 0, icost = 0, tcost = 0;
+    for (int q = 0; q < 4; ++q) {
+      const bool inter = s_inter[q] < s_intra[q];
+      n_inter += inter;
+      icost += s_intra[q];
+      tcost += inter ? s_inter[q] : s_intra[q];
+    }
+    int split;
+    if (n_inter == 0) {
+      // the analysis' own 32-vs-16 choice
+      split = icost < cd[0] ? 1 : 0;
+      for (int q = 0; q < 4; ++q) split |= (split & 1) && s_split8[q] ? 1 << (1 + q) : 0;
+      for (int q = 0; q < 4; ++q) s_inter[q] = 0x7FFFFFFF;  // mark intra
+    } else {
+      const bool same = n_inter == 4 && s_mvx[0] == s_mvx[1] && s_mvx[0] == s_mvx[2] && s_mvx[0] == s_mvx[3] &&
+                        s_mvy[0] == s_mvy[1] && s_mvy[0] == s_mvy[2] && s_mvy[0] == s_mvy[3];
+      split = same ? 0 : 1;
+      for (int q = 0; q < 4; ++q) {
+        const bool inter = s_inter[q] < s_intra[q];
+        if (!inter && s_split8[q]) split |= 1 << (1 + q);
+        if (!inter) s_inter[q] = 0x7FFFFFFF;
+      }
+    }
+    s_split = split;
+    a.ctu[cb].split = static_cast<uint8_t>(split);
+    a.ctu[cb].qp = static_cast<int8_t>(qp);
+  }
+  __syncthreads();
+  if (lane < 16) {
+    const int k = lane;
+    const int gx = (k & 1) | ((k >> 1) & 2), gy = ((k >> 1) & 1) | ((k >> 2) & 2);
+    const int q = (gx >> 1) + 2 * (gy >> 1);
+    const int split = s_split;
+    CuInfo c{};
+    int lg;
+    if (!(split & 1)) lg = 5;
+    else if (!((split >> (1 + q)) & 1)) lg = 4;
+    else lg = 3;
+    c.flags = static_cast<uint8_t>((lg - 3) << 1);
+    if (s_inter[q] != 0x7FFFFFFF) {
+      c.pred = hevc::CU_INTER;
+      c.mv[0] = static_cast<int16_t>(s_mvx[q]);
+      c.mv[1] = static_cast<int16_t>(s_mvy[q]);
+    } else {
+      c.pred = hevc::CU_INTRA;
+      const int idx = lg == 5 ? 0 : (lg == 4 ? 1 + q : 5 + k);
+      c.mode = static_cast<uint8_t>(cd[21 + idx]);
+    }
+    a.cu[cb * 16 + k] = c;
+  }
+}
+
+// ============================================================== inter reconstruction
+constexpr int kLumaTapsD[4][8] = {{0, 0, 0, 64, 0, 0, 0, 0},
+                                  {-1, 4, -10, 58, 17, -5, 1, 0},
+                                  {-1, 4, -11, 40, 40, -11, 4, -1},
+                                  {0, 1, -5, 17, 58, -10, 4, -1}};
+constexpr int kChromaTapsD[8][4] = {{0, 64, 0, 0},    {-2, 58, 10, -2}, {-4, 54, 16, -2}, {-6, 46, 28, -4},
+                                    {-4, 36, 36, -4}, {-4, 28, 46, -6}, {-2, 16, 54, -4}, {-2, 10, 58, -2}};
+
+struct InterShared {
+  uint16_t win[39 * 39];  // reference window (n + 7)^2
+  int tmp[39 * 32];       // horizontal pass
+  int R[32 * 32], S[32 * 32];
+  uint16_t pred[32 * 32];
+};
+
+// motion-compensated prediction of one n x n block of a component into S.pred
+// (8.5.3.3.3 fractional interpolation + 8.5.3.3.4.2 default weighted prediction)
+template <int NT>
+__device__ __forceinline__ void mc_block(InterShared& S, const uint16_t* ref, int pw, int ph, int bx, int by, int n,
+                                         int mvx, int mvy, int bd) {
+  const int lane = lane_id();
+  const int fb = NT == 8 ? 2 : 3;  // fraction bits
+  const int half = NT / 2 - 1;     // taps before the sample
+  const int fx = mvx & ((1 << fb) - 1), fy = mvy & ((1 << fb) - 1);
+  const int ix = bx + (mvx >> fb) - half, iy = by + (mvy >> fb) - half;
+  const int wn = n + NT - 1;
+  for (int i = lane; i < wn * wn; i += 64) {
+    const int r = i / wn, c = i - r * wn;
+    const int x = clampi(ix + c, 0, pw - 1), y = clampi(iy + r, 0, ph - 1);
+    S.win[r * wn + c] = ref[static_cast<size_t>(y) * pw + x];
+  }
+  wave_sync();
+  const int sh1 = bd - 8 < 4 ? bd - 8 : 4;
+  const int wsh = 14 - bd, woff = 1 << (wsh - 1);
+  const int maxv = (1 << bd) - 1;
+  auto tap = [&](int f, int k) { return NT == 8 ? kLumaTapsD[f][k] : kChromaTapsD[f][k]; };
+  if (fx != 0 && fy != 0) {  // separable: horizontal pass over n + NT - 1 rows
+    for (int i = lane; i < wn * n; i += 64) {
+      const int r = i / n, x = i - r * n;
+      int s = 0;
+#pragma unroll
+      for (int k = 0; k < NT; ++k) s += tap(fx, k) * S.win[r * wn + x + k];
+      S.tmp[r * 32 + x] = s >> sh1;
+    }
+    wave_sync();
+  }
+  for (int i = lane; i < n * n; i += 64) {
+    const int y = i / n, x = i - y * n;
+    int v;
+    if (fx == 0 && fy == 0) {
+      v = static_cast<int>(S.win[(y + half) * wn + x + half]) << wsh;
+    } else if (fy == 0) {
+      int s = 0;
+#pragma unroll
+      for (int k = 0; k < NT; ++k) s += tap(fx, k) * S.win[(y + half) * wn + x + k];
+      v = s >> sh1;
+    } else if (fx == 0) {
+      int s = 0;
+#pragma unroll
+      for (int k = 0; k < NT; ++k) s += tap(fy, k) * S.win[(y + k) * wn + x + half];
+      v = s >> sh1;
+    } else {
+      int s = 0;
+#pragma unroll
+      for (int k = 0; k < NT; ++k) s += tap(fy, k) * S.tmp[(y + k) * 32 + x];
+      v = s >> 6;
+    }
+    v = (v + woff) >> wsh;
+    S.pred[i] = static_cast<uint16_t>(v < 0 ? 0 : (v > maxv ? maxv : v));
+  }
+  wave_sync();
+}
+
+__global__ __launch_bounds__(64) void hevc_inter_cu(HevcInterArgs a) {
+  __shared__ InterShared S;
+  __shared__ hv::DctLds D;
+  const HevcGeom& g = a.g;
+  const int task = blockIdx.x, slot = blockIdx.y;
+  if (a.run[slot] != 2) return;
+  const int ci = task >> 2, q = task & 3;
+  const size_t cb = static_cast<size_t>(slot) * g.nctb() + ci;
+  const int kq = q * 4;  // z-index of the quadrant's first granule
+  CuInfo* cu = a.cu + cb * 16;
+  const int pred = cu[kq].pred;
+  const int lg = 3 + ((cu[kq].flags >> 1) & 3);
+  if (pred != hevc::CU_INTER) return;
+  if (lg == 5 && q != 0) return;  // the 32x32 CU is handled by quadrant 0
+  if (lg == 3) return;            // inter CUs are 16x16 or 32x32
+  hv::dct_lds_init(D);
+  __syncthreads();
+  const int lane = lane_id();
+  const int n = 1 << lg;
+  const int rx = ci % g.wctb, ry = ci / g.wctb;
+  const int X0 = rx * 32 + (lg == 5 ? 0 : (q & 1) * 16), Y0 = ry * 32 + (lg == 5 ? 0 : (q >> 1) * 16);
+  const int mvx = cu[kq].mv[0], mvy = cu[kq].mv[1];
+  const int bd = a.bd, maxv = (1 << bd) - 1;
+  const int qpy = a.qp[slot], off = 6 * (bd - 8);
+  const int qpl = qpy + off, qpc = hevc::chroma_qp_map(clampi(qpy, -off, 57)) + off;
+  int cbf = 0;
+  for (int c = 0; c < 3; ++c) {
+    const int pw = c ? g.W / 2 : g.W, ph = c ? g.H / 2 : g.H, bs = c ? n / 2 : n;
+    const int bx = c ? X0 / 2 : X0, by = c ? Y0 / 2 : Y0;
+    const size_t ps = c ? g.csize() : g.ysize();
+    const uint16_t* ref = (c == 0 ? a.ref_y : (c == 1 ? a.ref_u : a.ref_v)) + slot * ps;
+    const uint16_t* src = (c == 0 ? a.src_y : (c == 1 ? a.src_u : a.src_v)) + slot * ps;
+    uint16_t* rec = (c == 0 ? a.rec_y : (c == 1 ? a.rec_u : a.rec_v)) + slot * ps;
+    int16_t* lev = (c == 0 ? a.coef_y : (c == 1 ? a.coef_u : a.coef_v)) + slot * ps + static_cast<size_t>(by) * pw + bx;
+    if (c == 0) mc_block<8>(S, ref, pw, ph, bx, by, bs, mvx, mvy, bd);
+    else mc_block<4>(S, ref, pw, ph, bx, by, bs, mvx, mvy, bd);
+    for (int i = lane; i < bs * bs; i += 64) {
+      const int y = i / bs, x = i - y * bs;
+      S.R[y * 32 + x] = static_cast<int>(src[static_cast<size_t>(by + y) * pw + bx + x]) - S.pred[i];
+    }
+    wave_sync();
+    const int l2 = c ? lg - 1 : lg;
+    hv::TqParams tp{l2, bd, c ? qpc : qpl, false};
+    const bool nz = hv::transform_quant_block(D, S.R, S.S, lev, pw, tp);
+    cbf |= nz << c;
+    for (int i = lane; i < bs * bs; i += 64) {
+      const int y = i / bs, x = i - y * bs;
+      int v = S.pred[i] + (nz ? S.R[y * 32 + x] : 0);
+      rec[static_cast<size_t>(by + y) * pw + bx + x] = static_cast<uint16_t>(v < 0 ? 0 : (v > maxv ? maxv : v));
+    }
+    wave_sync();
+  }
+  const int ng = lg == 5 ? 16 : 4;
+  if (lane < ng) cu[kq + lane].cbf = static_cast<uint8_t>(cbf);
+}
+
+}  // namespace gpu
+}  // namespace mivc
+
+using namespace mivc::gpu;
+
+extern "C" void mivc_launch_hevc_inter(int B, int W, int H, const uint16_t* sy, const uint16_t* su, const uint16_t* sv,
+                                       const uint16_t* fy, const uint16_t* fu, const uint16_t* fv, uint16_t* ry,
+                                       uint16_t* ru, uint16_t* rv, void* ctu, void* cu, int16_t* cy, int16_t* cu_,
+                                       int16_t* cv, const int* qp, const int8_t* run, const int* cand,
+                                       const int16_t* mv, const int* me_cost, int bd, void* stream) {
+  HevcInterArgs a;
+  a.g = HevcGeom{B, W, H, W / 32, H / 32};
+  a.src_y = sy;
+  a.src_u = su;
+  a.src_v = sv;
+  a.ref_y = fy;
+  a.ref_u = fu;
+  a.ref_v = fv;
+  a.rec_y = ry;
+  a.rec_u = ru;
+  a.rec_v = rv;
+  a.ctu = static_cast<CtuInfo*>(ctu);
+  a.cu = static_cast<CuInfo*>(cu);
+  a.coef_y = cy;
+  a.coef_u = cu_;
+  a.coef_v = cv;
+  a.qp = qp;
+  a.run = run;
+  a.cand = cand;
+  a.mv = mv;
+  a.me_cost = me_cost;
+  a.bd = bd;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(hevc_p_decide, dim3(a.g.nctb(), B), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(hevc_inter_cu, dim3(a.g.nctb() * 4, B), dim3(64), 0, s, a);
+}

@@ -21,13 +21,6 @@ using hevc::CtuInfo;
 using hevc::CuInfo;
 using hevc::zorder8;
 
-struct HevcGeom {
-  int B, W, H, wctb, hctb;
-  __host__ __device__ size_t ysize() const { return static_cast<size_t>(W) * H; }
-  __host__ __device__ size_t csize() const { return static_cast<size_t>(W / 2) * (H / 2); }
-  __host__ __device__ int nctb() const { return wctb * hctb; }
-};
-
 struct HevcIntraArgs {
   HevcGeom g;
   const uint16_t *src_y, *src_u, *src_v;  // [B] padded source planes
@@ -37,6 +30,7 @@ struct HevcIntraArgs {
   int16_t *coef_y, *coef_u, *coef_v;      // [B] level planes
   const int* qp;                          // [B] QpY
   const int8_t* run;                      // [B] 0 idle, 1 all CUs (I picture), 2 intra CUs only (P picture)
+  int* cand;                              // [B, nctb, 2, 21] best cost / mode per CU of the analysis (may be null)
   int bd;
   int* err;
 };
@@ -243,6 +237,11 @@ __global__ __launch_bounds__(256) void hevc_intra_analyze(HevcIntraArgs a) {
     }
     S.best_mode[tid] = bm;
     S.best_cost[tid] = bc + lam * 4;  // CU overhead: split flag, chroma mode, cbfs
+    if (a.cand) {
+      int* cd = a.cand + (static_cast<size_t>(slot) * g.nctb() + ci) * 42;
+      cd[tid] = bc + lam * 4;
+      cd[21 + tid] = bm;
+    }
   }
   __syncthreads();
   if (tid == 0) {
@@ -476,7 +475,8 @@ using namespace mivc::gpu;
 
 static HevcIntraArgs make_intra_args(int B, int W, int H, const uint16_t* sy, const uint16_t* su, const uint16_t* sv,
                                      uint16_t* ry, uint16_t* ru, uint16_t* rv, void* ctu, void* cu, int16_t* cy,
-                                     int16_t* cu_, int16_t* cv, const int* qp, const int8_t* run, int bd, int* err) {
+                                     int16_t* cu_, int16_t* cv, const int* qp, const int8_t* run, int* cand, int bd,
+                                     int* err) {
   HevcIntraArgs a;
   a.g = HevcGeom{B, W, H, W / 32, H / 32};
   a.src_y = sy;
@@ -492,6 +492,7 @@ static HevcIntraArgs make_intra_args(int B, int W, int H, const uint16_t* sy, co
   a.coef_v = cv;
   a.qp = qp;
   a.run = run;
+  a.cand = cand;
   a.bd = bd;
   a.err = err;
   return a;
@@ -499,10 +500,10 @@ static HevcIntraArgs make_intra_args(int B, int W, int H, const uint16_t* sy, co
 
 extern "C" void mivc_launch_hevc_intra(int B, int W, int H, const uint16_t* sy, const uint16_t* su, const uint16_t* sv,
                                        uint16_t* ry, uint16_t* ru, uint16_t* rv, void* ctu, void* cu, int16_t* cy,
-                                       int16_t* cu_, int16_t* cv, const int* qp, const int8_t* run, int bd, int analyze,
-                                       int* err, void* stream) {
-  HevcIntraArgs a = make_intra_args(B, W, H, sy, su, sv, ry, ru, rv, ctu, cu, cy, cu_, cv, qp, run, bd, err);
+                                       int16_t* cu_, int16_t* cv, const int* qp, const int8_t* run, int* cand, int bd,
+                                       int analyze, int recon, int* err, void* stream) {
+  HevcIntraArgs a = make_intra_args(B, W, H, sy, su, sv, ry, ru, rv, ctu, cu, cy, cu_, cv, qp, run, cand, bd, err);
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (analyze) hipLaunchKernelGGL(hevc_intra_analyze, dim3(a.g.nctb(), B), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(hevc_intra_recon, dim3(B), dim3(64 * kHevcIntraWaves), 0, s, a);
+  if (recon) hipLaunchKernelGGL(hevc_intra_recon, dim3(B), dim3(64 * kHevcIntraWaves), 0, s, a);
 }

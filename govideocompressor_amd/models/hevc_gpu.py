@@ -43,7 +43,10 @@ class HevcParams:
     sao: bool = True
     deblock: bool = True
     intra_only: bool = False
+    keyint: int = 0                 # IDR period inside a segment (0: the first picture only)
     max_merge: int = 5
+    me_range: int = 8
+    subpel: int = 2
 
     def host_cfg(self) -> dict:
         return dict(width=self.width, height=self.height, bit_depth=self.bit_depth, fps=self.fps,
@@ -95,6 +98,16 @@ class GpuHevcEncoder:
         self.rec = [planes(), planes()]      # current / reference
         self.dbk = planes()                  # deblocked copy (SAO input)
         self.coef = planes(i16)
+        self.wmb, self.hmb = W // 16, H // 16
+        nmb = self.wmb * self.hmb
+        self.src8 = torch.zeros((B, H, W), dtype=torch.uint8, device=dev)   # motion-search proxies
+        self.ref8 = torch.zeros((B, H, W), dtype=torch.uint8, device=dev)
+        self.mv = torch.zeros((B, nmb, 2), dtype=torch.int16, device=dev)
+        self.prev_mv = torch.zeros((B, nmb, 2), dtype=torch.int16, device=dev)
+        self.me_cost = torch.zeros((B, nmb), dtype=torch.int32, device=dev)
+        self.me_intra = torch.zeros((B, nmb), dtype=torch.int32, device=dev)
+        self.me_pred = torch.zeros((B, nmb, 256), dtype=torch.uint8, device=dev)
+        self.cand = torch.zeros((B, self.nctb, 42), dtype=torch.int32, device=dev)
         self.ctu = torch.zeros((B, self.nctb, 32), dtype=torch.uint8, device=dev)
         self.cu = torch.zeros((B, self.nctb * 16, 8), dtype=torch.uint8, device=dev)
         self.qp = torch.zeros((B,), dtype=torch.int32, device=dev)
@@ -155,17 +168,31 @@ class GpuHevcEncoder:
         bd = self.p.bit_depth
         for t in range(F):
             t0 = time.perf_counter()
-            idr = t == 0 or self.p.intra_only
+            idr = t == 0 or self.p.intra_only or (self.p.keyint > 0 and t % self.p.keyint == 0)
             self._prep(y, u, v, t)
             self.qp.copy_(torch.from_numpy(np.ascontiguousarray(qps[:, t])).to(self.dev))
-            cur = self.rec[t % 2]
+            cur, ref = self.rec[t % 2], self.rec[(t + 1) % 2]
+            intra_args = (B, self.W, self.H, p(self.src[0]), p(self.src[1]), p(self.src[2]), p(cur[0]), p(cur[1]),
+                          p(cur[2]), p(self.ctu), p(self.cu), p(self.coef[0]), p(self.coef[1]), p(self.coef[2]),
+                          p(self.qp), p(self.run), p(self.cand), bd)
             if idr:
                 self.run.fill_(1)
-                self.hip.hevc_intra(B, self.W, self.H, p(self.src[0]), p(self.src[1]), p(self.src[2]), p(cur[0]),
-                                    p(cur[1]), p(cur[2]), p(self.ctu), p(self.cu), p(self.coef[0]), p(self.coef[1]),
-                                    p(self.coef[2]), p(self.qp), p(self.run), bd, 1, p(self.err), s)
+                self.hip.hevc_intra(*intra_args, 1, 1, p(self.err), s)
             else:
-                raise NotImplementedError("P pictures: see hevc_inter")
+                self.run.fill_(2)
+                self.hip.hevc_intra(*intra_args, 1, 0, p(self.err), s)   # open-loop intra candidates
+                sh = bd - 8
+                self.src8.copy_((self.src[0] >> sh).to(torch.uint8))
+                self.ref8.copy_((ref[0] >> sh).to(torch.uint8))
+                self.hip.me(B, self.wmb, self.hmb, p(self.src8), p(self.ref8), p(self.prev_mv), p(self.mv),
+                            p(self.me_cost), p(self.me_pred), p(self.me_intra), p(self.qp), self.p.me_range,
+                            self.p.subpel, s)
+                self.hip.hevc_inter(B, self.W, self.H, p(self.src[0]), p(self.src[1]), p(self.src[2]), p(ref[0]),
+                                    p(ref[1]), p(ref[2]), p(cur[0]), p(cur[1]), p(cur[2]), p(self.ctu), p(self.cu),
+                                    p(self.coef[0]), p(self.coef[1]), p(self.coef[2]), p(self.qp), p(self.run),
+                                    p(self.cand), p(self.mv), p(self.me_cost), bd, s)
+                self.hip.hevc_intra(*intra_args, 0, 1, p(self.err), s)   # intra CUs, wavefront
+                self.prev_mv.copy_(self.mv)
             if self.p.deblock:
                 self.hip.hevc_deblock(B, self.W, self.H, bd, p(cur[0]), p(cur[1]), p(cur[2]), p(self.cu), p(self.qp),
                                       p(self.run), s)

@@ -49,3 +49,12 @@ def test_gpu_hevc_intra_main10_cropped(host):
     res, rec = _encode(120, 68, 2, 2, bd=10, intra_only=True, crf=None, qp=27)
     _compare(host, res, rec)
     assert all(r.psnr_y > 30 for r in res)
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+def test_gpu_hevc_p_pictures_match_decoder(host, bd):
+    res, rec = _encode(128, 96, 5, 3, bd=bd, crf=None, qp=30)
+    _compare(host, res, rec)
+    for r in res:
+        assert all(b > 0 for b in r.bits)
+        assert sum(r.bits[1:]) / (r.frames - 1) < r.bits[0]   # P pictures are cheaper than the IDR
