@@ -13,8 +13,13 @@
    (the driver's headline metric).
 3. 4K30 H.264 -> H.264 transcode, segment-parallel: a 4K CAVLC stream is made
    (untimed) with the GPU encoder, then decode + re-encode is timed end to end.
-4. 1080p30 HEVC -- not implemented in this build (reported as such).
-5. 8K60 10-bit HEVC two-pass -- not implemented in this build (reported as such).
+4. 1080p30 synthetic YUV -> HEVC CRF26 (the reference's "265" preset) on MI355X:
+   batched GPU HEVC encoder (CTU intra analysis/reconstruction, P pictures, deblock,
+   SAO) + host CABAC.
+5. 8K60 synthetic 10-bit YUV -> HEVC Main 10, two-pass average bitrate: pass 1 at the
+   CRF QPs, per-frame statistics summed over ranks with one all-reduce (CC-1; RCCL
+   over xGMI on a multi-GPU node), global rate solve, pass 2 at the solved QPs; both
+   passes are timed.
 
 Multi-GPU runs (``--gpus N``, N > 1) are launched one process per GPU with
 ``torch.distributed.run``; this harness never starts them itself on a 1-GPU box.
@@ -150,6 +155,85 @@ def config3(args) -> list[dict]:
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def _hevc_run(args, W, H, B, F, bd, crf, two_pass_kbps=None, fps=30.0):
+    """Encode B segments x F frames of synthetic W x H content with the GPU HEVC encoder;
+    returns (frames/s over the timed steps, details)."""
+    import numpy as np
+    import torch
+
+    from govideocompressor_amd.models.h264_gpu import synth_clip
+    from govideocompressor_amd.models.hevc_gpu import GpuHevcEncoder, HevcParams
+    from govideocompressor_amd.parallel import dist as D
+    from govideocompressor_amd.rc import GlobalStats, abr_qps
+
+    env = D.init(prefer_gpu=True)
+    enc = GpuHevcEncoder(HevcParams(width=W, height=H, fps=fps, crf=crf, bit_depth=bd), slots=B, device=env.device)
+
+    def clip(step):
+        y, u, v = synth_clip(B, F, W, H, seed=500 + step * 7 + env.rank * 131, device=env.device)
+        if bd == 10:
+            y, u, v = (x.to(torch.int16) * 4 for x in (y, u, v))
+        return y, u, v
+
+    def step(k, quality=False):
+        y, u, v = clip(k)
+        if two_pass_kbps is None:
+            return enc.encode(y, u, v, metrics=quality), None
+        r1 = enc.encode(y, u, v, metrics=False)                      # pass 1 at the CRF QPs
+        qi, qp = enc.p.frame_qps()
+        n = B * F
+        gs = GlobalStats(n * env.world, env)
+        st = np.zeros((n, 4))
+        st[:, 2] = [b for r in r1 for b in r.bits]
+        st[:, 3] = [qi if t == 0 else qp for _ in range(B) for t in range(F)]
+        gs.put(env.rank * n, st)
+        glob = gs.reduce()                                             # CC-1 all-reduce
+        target = two_pass_kbps * 1000.0 * (n * env.world) / fps
+        qps_all = abr_qps(glob, target)
+        mine = qps_all[env.rank * n:(env.rank + 1) * n].reshape(B, F)
+        r2 = enc.encode(y, u, v, qps=mine, metrics=quality)            # pass 2
+        return r2, dict(pass1_bits=float(np.sum(st[:, 2])), target_bits=target / env.world,
+                        pass2_bits=float(sum(sum(r.bits) for r in r2)))
+
+    res, info = step(-1, quality=True)                                 # warmup (+ PSNR)
+    psnr = float(np.mean([r.psnr_y for r in res]))
+    torch.cuda.synchronize()
+    D.barrier(env)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        res, info = step(k)
+    torch.cuda.synchronize()
+    D.barrier(env)
+    dt = D.max_over_ranks(env, time.perf_counter() - t0)
+    bits = sum(sum(r.bits) for r in res)
+    enc.close()
+    fps_out = B * F * args.steps * env.world / dt
+    return fps_out, dict(psnr_y_warmup=round(psnr, 2), kbps_per_stream=round(bits / (B * F) * fps / 1000, 1),
+                         ms_per_step=round(dt / args.steps * 1000, 1), timings=enc.timings, rc=info, world=env.world)
+
+
+def config4(args) -> list[dict]:
+    import torch
+    if not torch.cuda.is_available():
+        return [{"config": 4, "value": None, "note": "needs a GPU"}]
+    B, F = args.slots4, args.frames4
+    v, d = _hevc_run(args, 1920, 1080, B, F, 8, 26.0)
+    return [{"config": 4, "metric": "encoded frames/sec (whole node), 1080p30 -> HEVC CRF26", "value": round(v, 2),
+             "unit": "frames/s", "n_gpus": d["world"], "segments_per_gpu": B, "frames_per_segment": F,
+             "dtype": "int (8-bit video)", "data": "synthetic 1080p30 YUV", **d}]
+
+
+def config5(args) -> list[dict]:
+    import torch
+    if not torch.cuda.is_available():
+        return [{"config": 5, "value": None, "note": "needs a GPU"}]
+    B, F = args.slots5, args.frames5
+    v, d = _hevc_run(args, 7680, 4320, B, F, 10, 26.0, two_pass_kbps=args.kbps5, fps=60.0)
+    return [{"config": 5, "metric": "encoded frames/sec (whole node), 8K60 10-bit HEVC two-pass", "value": round(v, 2),
+             "unit": "frames/s", "n_gpus": d["world"], "segments_per_gpu": B, "frames_per_segment": F,
+             "target_kbps": args.kbps5, "data": "synthetic 8K60 10-bit YUV", **d}]
+
+
 def config_na(n: int, what: str) -> list[dict]:
     return [{"config": n, "value": None, "note": f"not implemented in this build: {what}"}]
 
@@ -164,6 +248,11 @@ def main():
     ap.add_argument("--workers", type=int, default=4)
     ap.add_argument("--frames3", type=int, default=30)
     ap.add_argument("--segments3", type=int, default=16)
+    ap.add_argument("--slots4", type=int, default=64)
+    ap.add_argument("--frames4", type=int, default=30)
+    ap.add_argument("--slots5", type=int, default=4)
+    ap.add_argument("--frames5", type=int, default=8)
+    ap.add_argument("--kbps5", type=float, default=80000.0)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     todo = [1, 2, 3, 4, 5] if a.all else [a.config]
@@ -175,9 +264,9 @@ def main():
         elif c == 3:
             recs = config3(a)
         elif c == 4:
-            recs = config_na(4, "HEVC encoder")
+            recs = config4(a)
         else:
-            recs = config_na(5, "HEVC 10-bit encoder")
+            recs = config5(a)
         for r in recs:
             emit(r, a.out)
 

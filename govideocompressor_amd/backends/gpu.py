@@ -39,15 +39,22 @@ class GpuBackend:
         self.entropy = entropy
         self.max_slots = max_slots
         from ..models.h264_gpu import GpuH264Encoder
+        from ..models.hevc_gpu import GpuHevcEncoder, HevcParams
         from ..runtime import EncoderPool, StageStreams
-        self._pool = EncoderPool(lambda p, b: GpuH264Encoder(p, slots=b, device=self.device, entropy=self.entropy),
-                                 max_resident=1)
+
+        def make(p, b):
+            if isinstance(p, HevcParams):
+                return GpuHevcEncoder(p, slots=b, device=self.device)
+            return GpuH264Encoder(p, slots=b, device=self.device, entropy=self.entropy)
+
+        self._pool = EncoderPool(make, max_resident=1)
         self._streams = StageStreams(self.device)
         self._io = cf.ThreadPoolExecutor(max_workers=8)
         self._decoder = None
 
     def _encoder(self, params, slots: int):
-        key = (params.width, params.height, params.fps, params.crf, params.qp, slots)
+        key = (type(params).__name__, params.width, params.height, params.fps, params.crf, params.qp,
+               getattr(params, "bit_depth", 8), slots)
         return self._pool.get(key, params, slots)
 
     def encode_clips(self, items: list[tuple[str, "yuv.Clip"]], cfg: EncoderConfig,
@@ -55,10 +62,11 @@ class GpuBackend:
         """Encode several clips (pieces/segments) together.  ``items``: (index token, clip).
         Returns token -> (Annex-B stream, stats).  Raises on failure."""
         from ..models.h264_gpu import H264Params
+        from ..models.hevc_gpu import HevcParams
         from ..ops import native
-        if cfg.codec != "h264":
+        if cfg.codec not in ("h264", "hevc"):
             raise BackendError(f"codec {cfg.codec} is not available in the gpu backend")
-        if cfg.bit_depth != 8:
+        if cfg.bit_depth != 8 and cfg.codec == "h264":
             raise BackendError("10-bit H.264 output needs High 10; not supported")
         tm = tm or Timer()
         host = native.host()
@@ -73,14 +81,20 @@ class GpuBackend:
                 for u, (s, c) in enumerate(unit_plan(clips[key].frames, cfg.keyint)):
                     units.append((key, u, s, c))
             fps = cfg.fps or clips[keys[0]].fps
-            params = H264Params(width=ow, height=oh, fps=fps, crf=cfg.crf, qp=cfg.qp if cfg.qp is not None else 26)
+            if cfg.codec == "hevc":
+                if (ow, oh) != (w, h):
+                    raise BackendError("scaling is not available in the HEVC path")
+                params = HevcParams(width=ow, height=oh, fps=fps, crf=cfg.crf, qp=cfg.qp if cfg.qp is not None else 30,
+                                    bit_depth=cfg.bit_depth)
+            else:
+                params = H264Params(width=ow, height=oh, fps=fps, crf=cfg.crf, qp=cfg.qp if cfg.qp is not None else 26)
             unit_out = []
             for b0 in range(0, len(units), self.max_slots):
                 unit_out += self._encode_chunk(units[b0:b0 + self.max_slots], clips, params, w, h, tm)
             for key in keys:
                 parts = sorted((x for x in unit_out if x[0] == key), key=lambda x: x[1])
                 stream = host.concat([p[2] for p in parts])
-                st = {"backend": "gpu", "idx": key, "frames": clips[key].frames, "units": len(parts),
+                st = {"backend": "gpu", "codec": cfg.codec, "idx": key, "frames": clips[key].frames, "units": len(parts),
                       "width": ow, "height": oh, "fps": fps, "stream_bytes": len(stream),
                       "psnr_y": float(np.mean([p[3] for p in parts])), "ssim_y": float(np.mean([p[4] for p in parts])),
                       "config": cfg.as_dict()}
@@ -187,10 +201,13 @@ class GpuBackend:
         B = len(chunk)
         t1 = time.perf_counter()
         enc = self._encoder(params, B)
-        res = enc.encode(dy, du, dv, idr_ids=[idr_id(key, un_) for key, un_, _, _ in chunk])
+        if hasattr(enc, "encode") and type(params).__name__ == "HevcParams":
+            res = enc.encode(dy, du, dv)
+        else:
+            res = enc.encode(dy, du, dv, idr_ids=[idr_id(key, un_) for key, un_, _, _ in chunk])
         tm.add("encode_s", time.perf_counter() - t1)
         ps = enc.parameter_sets()
-        return [(key, un_, ps + b"".join(res[b].nals[:c]), res[b].psnr_y, res[b].ssim_y)
+        return [(key, un_, ps + b"".join(res[b].nals[:c]), res[b].psnr_y, getattr(res[b], "ssim_y", 0.0))
                 for b, (key, un_, s, c) in enumerate(chunk)]
 
     def close(self):

@@ -58,3 +58,22 @@ def test_gpu_hevc_p_pictures_match_decoder(host, bd):
     for r in res:
         assert all(b > 0 for b in r.bits)
         assert sum(r.bits[1:]) / (r.frames - 1) < r.bits[0]   # P pictures are cheaper than the IDR
+
+
+def test_gpu_backend_hevc_preset(host, tmp_path):
+    """The reference's "265" preset through the GPU backend: pieces -> HEVC streams."""
+    from govideocompressor_amd.backends import get_backend
+    from govideocompressor_amd.jobs import ffargs
+    from govideocompressor_amd.utils import yuv
+    be = get_backend("gpu")
+    clips = [(str(i), yuv.synth_clip_cpu(6, 160, 96, seed=i)) for i in range(3)]
+    out = be.impl.encode_clips(clips, ffargs.parse(ffargs.expand_preset("265")))
+    for key, c in clips:
+        stream, st = out[key]
+        pics = host.hevc_decode(stream)
+        assert len(pics) == 6 and st["codec"] == "hevc"
+        ref = c.y.astype(np.float64)
+        dec = np.stack([p["y"][:96, :160] for p in pics]).astype(np.float64)
+        mse = np.mean((ref - dec) ** 2)
+        assert 10 * np.log10(255 ** 2 / mse) > 30
+    be.close()
