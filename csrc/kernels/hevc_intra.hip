@@ -189,10 +189,12 @@ __global__ __launch_bounds__(256) void hevc_intra_analyze(HevcIntraArgs a) {
     S.dc[tid] = s >> (lg + 1);
   }
   __syncthreads();
-  // SATD of every (CU, mode, 8x8 block)
-  for (int it = tid; it < 3 * 560; it += 256) {
-    const int level = it / 560, j = it % 560;
-    const int mode = j >> 4, k = j & 15;
+  // SATD of every (CU, mode, 8x8 block): a wave takes one mode at a time (uniform control
+  // flow through the predictor); lanes 0-15 the 16 blocks of the 32x32 CU, 16-31 the
+  // 4 x 4 blocks of the 16x16 CUs, 32-47 the 16 8x8 CUs
+  {
+    const int w = tid >> 6, lane = tid & 63;
+    const int level = lane >> 4, k = lane & 15;
     int c, bx, by;
     if (level == 0) {
       c = 0;
@@ -207,21 +209,25 @@ __global__ __launch_bounds__(256) void hevc_intra_analyze(HevcIntraArgs a) {
       bx = 0;
       by = 0;
     }
-    int cx, cy, n, off;
-    cu_of(c, &cx, &cy, &n, &off);
+    int cx = 0, cy = 0, n = 8, off = 0;
+    if (lane < 48) cu_of(c, &cx, &cy, &n, &off);
     const int lg = n == 32 ? 5 : (n == 16 ? 4 : 3);
-    const int* p = S.refs[hv::intra_filter_flag(mode, n) ? 1 : 0] + off;
-    const int dc = S.dc[c];
-    int d[64];
+    const int dc = lane < 48 ? S.dc[c] : 0;
+    for (int mode = w; mode < 35; mode += 4) {
+      if (lane < 48) {
+        const int* p = S.refs[hv::intra_filter_flag(mode, n) ? 1 : 0] + off;
+        int d[64];
 #pragma unroll
-    for (int y = 0; y < 8; ++y)
+        for (int y = 0; y < 8; ++y)
 #pragma unroll
-      for (int x = 0; x < 8; ++x) {
-        const int px = bx * 8 + x, py = by * 8 + y;
-        const int pv = hv::intra_pred_sample(p, n, lg, mode, px, py, dc, n < 32, maxv);
-        d[y * 8 + x] = S.ext[(cy + py + 1) * 65 + cx + px + 1] - pv;
+          for (int x = 0; x < 8; ++x) {
+            const int px = bx * 8 + x, py = by * 8 + y;
+            const int pv = hv::intra_pred_sample(p, n, lg, mode, px, py, dc, n < 32, maxv);
+            d[y * 8 + x] = S.ext[(cy + py + 1) * 65 + cx + px + 1] - pv;
+          }
+        atomicAdd(&S.cost[c][mode], satd8x8(d));
       }
-    atomicAdd(&S.cost[c][mode], satd8x8(d));
+    }
   }
   __syncthreads();
   const int qp = a.qp[slot];

@@ -97,7 +97,8 @@ class GpuHevcEncoder:
         self.src = planes()
         self.rec = [planes(), planes()]      # current / reference
         self.dbk = planes()                  # deblocked copy (SAO input)
-        self.coef = planes(i16)
+        self.coefs = [planes(i16), planes(i16)]  # double-buffered: copy-out of t overlaps t + 1
+        self.coef = self.coefs[0]
         self.wmb, self.hmb = W // 16, H // 16
         nmb = self.wmb * self.hmb
         self.src8 = torch.zeros((B, H, W), dtype=torch.uint8, device=dev)   # motion-search proxies
@@ -108,14 +109,25 @@ class GpuHevcEncoder:
         self.me_intra = torch.zeros((B, nmb), dtype=torch.int32, device=dev)
         self.me_pred = torch.zeros((B, nmb, 256), dtype=torch.uint8, device=dev)
         self.cand = torch.zeros((B, self.nctb, 42), dtype=torch.int32, device=dev)
-        self.ctu = torch.zeros((B, self.nctb, 32), dtype=torch.uint8, device=dev)
-        self.cu = torch.zeros((B, self.nctb * 16, 8), dtype=torch.uint8, device=dev)
+        self.ctus = [torch.zeros((B, self.nctb, 32), dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.cus = [torch.zeros((B, self.nctb * 16, 8), dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.ctu, self.cu = self.ctus[0], self.cus[0]
+        self.copy_stream = torch.cuda.Stream(device=dev)
+        self.copy_done = [torch.cuda.Event() for _ in range(2)]
+        self.host_bufs = None  # lazily: 3 sets of pinned host buffers
         self.qp = torch.zeros((B,), dtype=torch.int32, device=dev)
         self.run = torch.zeros((B,), dtype=torch.int8, device=dev)
         self.err = torch.zeros((1,), dtype=torch.int32, device=dev)
         self.params_nal = self.host.hevc_parameter_sets(params.host_cfg())
         self.pool = cf.ThreadPoolExecutor(max_workers=entropy_threads or min(16, os.cpu_count() or 4))
         self.timings: dict[str, float] = {}
+
+    def _host_buffers(self):
+        if self.host_bufs is None:
+            def pin(t):
+                return torch.empty(t.shape, dtype=t.dtype).pin_memory()
+            self.host_bufs = [[pin(self.ctus[0]), pin(self.cus[0]), *(pin(c) for c in self.coefs[0])] for _ in range(3)]
+        return self.host_bufs
 
     def parameter_sets(self) -> bytes:
         return self.params_nal
@@ -160,6 +172,7 @@ class GpuHevcEncoder:
         cfg = self.p.host_cfg()
         nals: list[list] = [[None] * F for _ in range(B)]
         futs = []
+        pending: list[list] = [[], [], []]
         sse = []
         recon = [] if keep_recon else None
         t_gpu = t_host = 0.0
@@ -172,6 +185,10 @@ class GpuHevcEncoder:
             self._prep(y, u, v, t)
             self.qp.copy_(torch.from_numpy(np.ascontiguousarray(qps[:, t])).to(self.dev))
             cur, ref = self.rec[t % 2], self.rec[(t + 1) % 2]
+            kb = t % 2
+            # the copy-out of step t - 2 must have read these buffers before they are rewritten
+            torch.cuda.current_stream(self.dev).wait_event(self.copy_done[kb])
+            self.coef, self.ctu, self.cu = self.coefs[kb], self.ctus[kb], self.cus[kb]
             intra_args = (B, self.W, self.H, p(self.src[0]), p(self.src[1]), p(self.src[2]), p(cur[0]), p(cur[1]),
                           p(cur[2]), p(self.ctu), p(self.cu), p(self.coef[0]), p(self.coef[1]), p(self.coef[2]),
                           p(self.qp), p(self.run), p(self.cand), bd)
@@ -207,16 +224,36 @@ class GpuHevcEncoder:
                 sse.append((d * d).sum(dim=(1, 2)).to(torch.float64))
             if keep_recon:
                 recon.append(tuple(c.clone() for c in cur))
-            # records to the host (synchronous for now), CABAC on the thread pool
-            ctu = self.ctu.cpu().numpy()
-            cu = self.cu.cpu().numpy()
-            cy, cb, cr = (c.cpu().numpy() for c in self.coef)
+            # records to pinned host memory on the copy stream; CABAC on the thread pool
+            hb = t % 3
+            if pending[hb]:  # the CABAC jobs of step t - 3 still read this host buffer set
+                for f in pending[hb]:
+                    f.result()
+                pending[hb] = []
+            host = self._host_buffers()[hb]
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.dev))
+            with torch.cuda.stream(self.copy_stream):
+                self.copy_stream.wait_event(ev)
+                for dst, src_t in zip(host, (self.ctu, self.cu, *self.coef)):
+                    dst.copy_(src_t, non_blocking=True)
+                done = torch.cuda.Event()
+                done.record(self.copy_stream)
+                self.copy_done[kb].record(self.copy_stream)
+            ctu, cu, cy, cb, cr = (h_.numpy() for h_ in host)
             t1 = time.perf_counter()
             t_gpu += t1 - t0
-            for b in range(B):
+
+            def job(b, t=t, idr=idr, done=done, ctu=ctu, cu=cu, cy=cy, cb=cb, cr=cr):
+                if b == 0 or not done.query():
+                    done.synchronize()
                 fp = dict(idr=int(idr), poc=t, qp=int(qps[b, t]), slice_type=2 if idr else 1)
-                futs.append((b, t, self.pool.submit(self.host.hevc_write_slice, cfg, fp, ctu[b], cu[b], cy[b], cb[b],
-                                                    cr[b])))
+                return self.host.hevc_write_slice(cfg, fp, ctu[b], cu[b], cy[b], cb[b], cr[b])
+
+            for b in range(B):
+                f = self.pool.submit(job, b)
+                futs.append((b, t, f))
+                pending[hb].append(f)
         if int(self.err.item()) != 0:
             raise RuntimeError("HEVC encoder: wavefront progress timeout")
         t2 = time.perf_counter()
