@@ -267,6 +267,88 @@ __device__ __forceinline__ int intra_pred_sample(const int* p, int n, int log2n,
   return v;
 }
 
+// 8x8 block of the prediction of an n x n block (n >= 8) at offset (ox, oy): angular
+// modes load 9 reference samples per row (vertical family) or column (horizontal
+// family) and interpolate 8 outputs from registers.
+__device__ __forceinline__ void intra_pred8(const int* p, int n, int log2n, int mode, int ox, int oy, int dc, bool edge,
+                                            int maxv, int (&o)[64]) {
+  const int c = 2 * n;
+  auto L = [&](int yy) { return p[c - 1 - yy]; };
+  auto T = [&](int xx) { return p[c + 1 + xx]; };
+  if (mode == 0) {
+    const int tn = T(n), ln = L(n);
+    int lv[8], tv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      lv[k] = L(oy + k);
+      tv[k] = T(ox + k);
+    }
+#pragma unroll
+    for (int y = 0; y < 8; ++y)
+#pragma unroll
+      for (int x = 0; x < 8; ++x) {
+        const int X = ox + x, Y = oy + y;
+        o[y * 8 + x] = ((n - 1 - X) * lv[y] + (X + 1) * tn + (n - 1 - Y) * tv[x] + (Y + 1) * ln + n) >> (log2n + 1);
+      }
+    return;
+  }
+  if (mode == 1) {
+#pragma unroll
+    for (int i = 0; i < 64; ++i) o[i] = dc;
+    if (edge) {
+      if (oy == 0)
+#pragma unroll
+        for (int x = 0; x < 8; ++x) o[x] = (T(ox + x) + 3 * dc + 2) >> 2;
+      if (ox == 0)
+#pragma unroll
+        for (int y = 0; y < 8; ++y) o[y * 8] = (L(oy + y) + 3 * dc + 2) >> 2;
+      if (ox == 0 && oy == 0) o[0] = (L(0) + 2 * dc + T(0) + 2) >> 2;
+    }
+    return;
+  }
+  const int ang = hevc::kIntraPredAngle[mode];
+  const int inv = (mode >= 11 && mode <= 25) ? hevc::kInvAngle[mode - 11] : 0;
+  if (mode >= 18) {
+#pragma unroll
+    for (int y = 0; y < 8; ++y) {
+      const int Y = oy + y;
+      const int idx = ((Y + 1) * ang) >> 5, f = ((Y + 1) * ang) & 31;
+      const int base = ox + idx + 1;
+      int r[9];
+#pragma unroll
+      for (int j = 0; j < 9; ++j) {
+        const int k = base + j;
+        r[j] = k >= 0 ? T(k - 1) : L(-1 + ((k * inv + 128) >> 8));
+      }
+#pragma unroll
+      for (int x = 0; x < 8; ++x) o[y * 8 + x] = f ? ((32 - f) * r[x] + f * r[x + 1] + 16) >> 5 : r[x];
+      if (mode == 26 && edge && ox == 0) {
+        const int v = T(0) + ((L(Y) - L(-1)) >> 1);
+        o[y * 8] = v < 0 ? 0 : (v > maxv ? maxv : v);
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int x = 0; x < 8; ++x) {
+    const int X = ox + x;
+    const int idx = ((X + 1) * ang) >> 5, f = ((X + 1) * ang) & 31;
+    const int base = oy + idx + 1;
+    int r[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int k = base + j;
+      r[j] = k >= 0 ? L(k - 1) : T(-1 + ((k * inv + 128) >> 8));
+    }
+#pragma unroll
+    for (int y = 0; y < 8; ++y) o[y * 8 + x] = f ? ((32 - f) * r[y] + f * r[y + 1] + 16) >> 5 : r[y];
+    if (mode == 10 && edge && oy == 0) {
+      const int v = L(0) + ((T(X) - T(-1)) >> 1);
+      o[x] = v < 0 ? 0 : (v > maxv ? maxv : v);
+    }
+  }
+}
+
 // DC value of the reference array (wave reduction)
 __device__ __forceinline__ int intra_dc(const int* p, int n, int log2n) {
   const int lane = lane_id();

@@ -213,18 +213,18 @@ __global__ __launch_bounds__(256) void hevc_intra_analyze(HevcIntraArgs a) {
     if (lane < 48) cu_of(c, &cx, &cy, &n, &off);
     const int lg = n == 32 ? 5 : (n == 16 ? 4 : 3);
     const int dc = lane < 48 ? S.dc[c] : 0;
+    int sv[64];  // this lane's 8x8 source block, loaded once for all modes
+#pragma unroll
+    for (int y = 0; y < 8; ++y)
+#pragma unroll
+      for (int x = 0; x < 8; ++x) sv[y * 8 + x] = lane < 48 ? S.ext[(cy + by * 8 + y + 1) * 65 + cx + bx * 8 + x + 1] : 0;
     for (int mode = w; mode < 35; mode += 4) {
       if (lane < 48) {
         const int* p = S.refs[hv::intra_filter_flag(mode, n) ? 1 : 0] + off;
         int d[64];
+        hv::intra_pred8(p, n, lg, mode, bx * 8, by * 8, dc, n < 32, maxv, d);
 #pragma unroll
-        for (int y = 0; y < 8; ++y)
-#pragma unroll
-          for (int x = 0; x < 8; ++x) {
-            const int px = bx * 8 + x, py = by * 8 + y;
-            const int pv = hv::intra_pred_sample(p, n, lg, mode, px, py, dc, n < 32, maxv);
-            d[y * 8 + x] = S.ext[(cy + py + 1) * 65 + cx + px + 1] - pv;
-          }
+        for (int i = 0; i < 64; ++i) d[i] = sv[i] - d[i];
         atomicAdd(&S.cost[c][mode], satd8x8(d));
       }
     }
