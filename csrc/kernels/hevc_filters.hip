@@ -25,15 +25,33 @@ using hevc::CuInfo;
 // `pitch` samples, w x h valid; dst: [B] padded W x H uint16 planes (edge replication)
 __global__ void hevc_prep_plane(const uint8_t* src, long long slot_stride, int pitch, int bps, int w, int h,
                                 uint16_t* dst, int W, int H, int shift) {
-  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  const int x0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4, y = blockIdx.y;
   const int b = blockIdx.z;
-  if (x >= W) return;
-  const int sx = min(x, w - 1), sy = min(y, h - 1);
+  if (x0 >= W) return;
+  const int sy = min(y, h - 1);
   const uint8_t* s = src + b * slot_stride;
-  int v;
-  if (bps == 1) v = s[static_cast<size_t>(sy) * pitch + sx];
-  else v = reinterpret_cast<const uint16_t*>(s)[static_cast<size_t>(sy) * pitch + sx];
-  dst[static_cast<size_t>(b) * W * H + static_cast<size_t>(y) * W + x] = static_cast<uint16_t>(v << shift);
+  uint16_t v[4];
+  if (bps == 1) {
+    const uint8_t* row = s + static_cast<size_t>(sy) * pitch;
+    if (x0 + 3 < w && !(reinterpret_cast<uintptr_t>(row + x0) & 3)) {
+      const uint32_t wd = *reinterpret_cast<const uint32_t*>(row + x0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = static_cast<uint16_t>(((wd >> (8 * k)) & 255u) << shift);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = static_cast<uint16_t>(row[min(x0 + k, w - 1)] << shift);
+    }
+  } else {
+    const uint16_t* row = reinterpret_cast<const uint16_t*>(s) + static_cast<size_t>(sy) * pitch;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = static_cast<uint16_t>(row[min(x0 + k, w - 1)] << shift);
+  }
+  uint16_t* d = dst + static_cast<size_t>(b) * W * H + static_cast<size_t>(y) * W + x0;
+  if (x0 + 3 < W) {
+    *reinterpret_cast<uint2*>(d) = make_uint2(v[0] | (static_cast<uint32_t>(v[1]) << 16), v[2] | (static_cast<uint32_t>(v[3]) << 16));
+  } else {
+    for (int k = 0; k < 4 && x0 + k < W; ++k) d[k] = v[k];
+  }
 }
 
 // ============================================================== deblocking
@@ -371,7 +389,7 @@ using namespace mivc::gpu;
 
 extern "C" void mivc_launch_hevc_prep(int B, const void* src, long long slot_stride, int pitch, int bps, int w, int h,
                                       uint16_t* dst, int W, int H, int shift, void* stream) {
-  dim3 grid((W + 255) / 256, H, B);
+  dim3 grid((W / 4 + 255) / 256 + 1, H, B);
   hipLaunchKernelGGL(hevc_prep_plane, grid, dim3(256), 0, static_cast<hipStream_t>(stream),
                      static_cast<const uint8_t*>(src), slot_stride, pitch, bps, w, h, dst, W, H, shift);
 }

@@ -106,6 +106,7 @@ struct AnalyzeShared {
   int16_t ext[65 * 65];        // source samples, x, y in [-1, 63] relative to the CTB
   int refs[2][917];            // per CU: unfiltered / filtered reference arrays
   int cost[kCuCount][36];
+  uint8_t done[kCuCount][36];  // (CU, mode) evaluated
   int dc[kCuCount];
   int best_mode[kCuCount], best_cost[kCuCount];
 };
@@ -146,7 +147,10 @@ __global__ __launch_bounds__(256) void hevc_intra_analyze(HevcIntraArgs a) {
     const int xx = clampi(X0 + x, 0, g.W - 1), yy = clampi(Y0 + y, 0, g.H - 1);
     S.ext[i] = static_cast<int16_t>(src[static_cast<size_t>(yy) * g.W + xx]);
   }
-  for (int i = tid; i < kCuCount * 36; i += 256) (&S.cost[0][0])[i] = 0;
+  for (int i = tid; i < kCuCount * 36; i += 256) {
+    (&S.cost[0][0])[i] = 0;
+    (&S.done[0][0])[i] = 0;
+  }
   __syncthreads();
   // reference arrays of the 21 CUs: availability + serial substitution, one thread per CU
   if (tid < kCuCount) {
@@ -189,12 +193,12 @@ __global__ __launch_bounds__(256) void hevc_intra_analyze(HevcIntraArgs a) {
     S.dc[tid] = s >> (lg + 1);
   }
   __syncthreads();
-  // SATD of every (CU, mode, 8x8 block): a wave takes one mode at a time (uniform control
-  // flow through the predictor); lanes 0-15 the 16 blocks of the 32x32 CU, 16-31 the
-  // 4 x 4 blocks of the 16x16 CUs, 32-47 the 16 8x8 CUs
-  {
-    const int w = tid >> 6, lane = tid & 63;
-    const int level = lane >> 4, k = lane & 15;
+  // SATD of (CU, mode, 8x8 block) items, coarse to fine: 11 seed modes (planar, DC and
+  // every 4th angular direction) for every CU, then best-angular +-2, then +-1.  An
+  // item index i < 48 names the (CU, block): 0-15 the blocks of the 32x32 CU, 16-31
+  // the 4 x 4 blocks of the 16x16 CUs, 32-47 the 16 8x8 CUs.
+  auto eval = [&](int slot48, int mode) {
+    const int level = slot48 >> 4, k = slot48 & 15;
     int c, bx, by;
     if (level == 0) {
       c = 0;
@@ -209,25 +213,47 @@ __global__ __launch_bounds__(256) void hevc_intra_analyze(HevcIntraArgs a) {
       bx = 0;
       by = 0;
     }
-    int cx = 0, cy = 0, n = 8, off = 0;
-    if (lane < 48) cu_of(c, &cx, &cy, &n, &off);
+    int cx, cy, n, off;
+    cu_of(c, &cx, &cy, &n, &off);
     const int lg = n == 32 ? 5 : (n == 16 ? 4 : 3);
-    const int dc = lane < 48 ? S.dc[c] : 0;
-    int sv[64];  // this lane's 8x8 source block, loaded once for all modes
+    const int* p = S.refs[hv::intra_filter_flag(mode, n) ? 1 : 0] + off;
+    int d[64];
+    hv::intra_pred8(p, n, lg, mode, bx * 8, by * 8, S.dc[c], n < 32, maxv, d);
 #pragma unroll
     for (int y = 0; y < 8; ++y)
 #pragma unroll
-      for (int x = 0; x < 8; ++x) sv[y * 8 + x] = lane < 48 ? S.ext[(cy + by * 8 + y + 1) * 65 + cx + bx * 8 + x + 1] : 0;
-    for (int mode = w; mode < 35; mode += 4) {
-      if (lane < 48) {
-        const int* p = S.refs[hv::intra_filter_flag(mode, n) ? 1 : 0] + off;
-        int d[64];
-        hv::intra_pred8(p, n, lg, mode, bx * 8, by * 8, dc, n < 32, maxv, d);
-#pragma unroll
-        for (int i = 0; i < 64; ++i) d[i] = sv[i] - d[i];
-        atomicAdd(&S.cost[c][mode], satd8x8(d));
-      }
+      for (int x = 0; x < 8; ++x) d[y * 8 + x] = S.ext[(cy + by * 8 + y + 1) * 65 + cx + bx * 8 + x + 1] - d[y * 8 + x];
+    atomicAdd(&S.cost[c][mode], satd8x8(d));
+    S.done[c][mode] = 1;
+  };
+  {
+    for (int it = tid; it < 11 * 48; it += 256) {
+      const int si = it / 48;
+      eval(it % 48, si < 2 ? si : 2 + 4 * (si - 2));  // seeds 0, 1, 2, 6, ..., 34
     }
+  }
+  __syncthreads();
+  for (int step = 2; step >= 1; step >>= 1) {
+    if (tid < kCuCount) {  // best angular so far -> its two neighbours at distance step
+      int bm = 2, bc = 0x7FFFFFFF;
+      for (int m = 2; m < 35; ++m) {
+        const int cst = S.cost[tid][m];
+        if (S.done[tid][m] && cst < bc) {
+          bc = cst;
+          bm = m;
+        }
+      }
+      S.best_mode[tid] = bm;
+    }
+    __syncthreads();
+    if (tid < 96) {
+      const int slot48 = tid % 48;
+      const int level = slot48 >> 4, k = slot48 & 15;
+      const int c = level == 0 ? 0 : (level == 1 ? 1 + (k >> 2) : 5 + k);
+      const int m = S.best_mode[c] + (tid < 48 ? -step : step);
+      if (m >= 2 && m <= 34 && !S.done[c][m]) eval(slot48, m);
+    }
+    __syncthreads();
   }
   __syncthreads();
   const int qp = a.qp[slot];
@@ -235,6 +261,7 @@ __global__ __launch_bounds__(256) void hevc_intra_analyze(HevcIntraArgs a) {
   if (tid < kCuCount) {
     int bm = 0, bc = 0x7FFFFFFF;
     for (int m = 0; m < 35; ++m) {
+      if (!S.done[tid][m]) continue;
       const int cst = S.cost[tid][m] + lam * (m < 2 ? 3 : 5);
       if (cst < bc) {
         bc = cst;
