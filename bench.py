@@ -6,6 +6,7 @@ CRF23, at 1/2/4/8 MI355X").  One process per GPU (torch.distributed.run), weak
 scaling: every rank encodes B closed-GOP segments of F frames per step.  A timed step is
 
     synthesize B*F new 1080p frames in HBM (new content every step)
+    -> GPU lookahead over all B*F frames (lowres search + MFMA Hadamard SATD) -> CRF QPs
     -> batched GPU encode (ME, TQ, intra/deblock wavefronts, CAVLC)
     -> gather every rank's segment bitstreams to all ranks (RCCL all_gather over xGMI)
     -> rank 0 concatenates the pieces in segment order (the reference's concat.sh)
@@ -114,7 +115,7 @@ def main() -> None:
             "dtype": "uint8 (8-bit 4:2:0 samples, int32 transforms)",
             "data": "synthetic (GPU-generated moving-texture YUV, new content every step)",
             "config": {
-                "model": "H.264 Constrained Baseline CAVLC, gfx950 batched encoder",
+                "model": "H.264 Constrained Baseline CAVLC, gfx950 batched encoder, CRF from GPU lookahead",
                 "resolution": f"{a.width}x{a.height}",
                 "fps": 30,
                 "crf": a.crf,

@@ -179,13 +179,13 @@ def _hevc_run(args, W, H, B, F, bd, crf, two_pass_kbps=None, fps=30.0):
         y, u, v = clip(k)
         if two_pass_kbps is None:
             return enc.encode(y, u, v, metrics=quality), None
-        r1 = enc.encode(y, u, v, metrics=False)                      # pass 1 at the CRF QPs
-        qi, qp = enc.p.frame_qps()
+        q1 = enc.crf_qps(y)                                           # GPU lookahead -> CRF QPs
+        r1 = enc.encode(y, u, v, qps=q1, metrics=False)               # pass 1 at the CRF QPs
         n = B * F
         gs = GlobalStats(n * env.world, env)
         st = np.zeros((n, 4))
         st[:, 2] = [b for r in r1 for b in r.bits]
-        st[:, 3] = [qi if t == 0 else qp for _ in range(B) for t in range(F)]
+        st[:, 3] = q1.reshape(-1)
         gs.put(env.rank * n, st)
         glob = gs.reduce()                                             # CC-1 all-reduce
         target = two_pass_kbps * 1000.0 * (n * env.world) / fps

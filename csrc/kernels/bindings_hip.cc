@@ -5,6 +5,7 @@
 #include <pybind11/pybind11.h>
 
 #include <cstdint>
+#include <stdexcept>
 
 namespace py = pybind11;
 
@@ -61,6 +62,9 @@ void mivc_launch_cavlc(int B, int wmb, int hmb, const void* hdr, const int16_t* 
 void mivc_launch_sse(int B, int W, int H, int w, int h, const uint8_t* sy, const uint8_t* su, const uint8_t* sv,
                      const uint8_t* ry, const uint8_t* ru, const uint8_t* rv, unsigned long long* sse,
                      float* ssim_sum, void* stream);
+long long mivc_lookahead_low_bytes(int w, int h, int N);
+int mivc_launch_lookahead(const uint8_t* y, int w, int h, long long fstride, int N, int F, uint8_t* low,
+                          unsigned long long* frame_cost, int* blk_cost, int range, void* stream);
 }
 
 namespace {
@@ -174,5 +178,12 @@ PYBIND11_MODULE(_hip, m) {
                   uintptr_t ru, uintptr_t rv, uintptr_t sse, uintptr_t ssim, uintptr_t stream) {
     mivc_launch_sse(B, W, H, w, h, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), P<uint8_t>(ry), P<uint8_t>(ru),
                     P<uint8_t>(rv), P<unsigned long long>(sse), P<float>(ssim), S(stream));
+  });
+  m.def("lookahead_low_bytes", [](int w, int h, int n) { return mivc_lookahead_low_bytes(w, h, n); });
+  m.def("lookahead", [](uintptr_t y, int w, int h, long long fstride, int n, int f, uintptr_t low, uintptr_t frame_cost,
+                        uintptr_t blk_cost, int range, uintptr_t stream) {
+    int rc = mivc_launch_lookahead(P<uint8_t>(y), w, h, fstride, n, f, P<uint8_t>(low),
+                                   P<unsigned long long>(frame_cost), P<int>(blk_cost), range, S(stream));
+    if (rc != 0) throw std::invalid_argument("lookahead: bad geometry or range (4, 6, 8)");
   });
 }

@@ -1,0 +1,291 @@
+// Lookahead with the SATD Hadamard on the matrix cores (K-C6).
+//
+// The reference gets its frame-level rate control from libx264's lookahead inside
+// the worker's ffmpeg (client.go:115, `-vcodec libx264` = CRF 23 by default,
+// server.go:70).  Here every frame of every segment slot is analysed in ONE pass,
+// before the encode: the lookahead has no reconstruction dependency, so B x F
+// frames (15360 at the headline config) are independent work.
+//
+//   la_downscale  half-resolution luma ("lowres", 2x2 box) with a replicated border,
+//                 so the search and the intra neighbours never clamp.
+//   la_cost       per 8x8 lowres block (one per 16x16 macroblock):
+//                   * inter: integer full search (2R+1)^2 against the previous lowres
+//                     frame of the same segment, SAD (v_sad_u8) + 2 * |mv|;
+//                   * intra: DC / horizontal / vertical predictions from the lowres
+//                     neighbours;
+//                   * cost of each of the 4 candidates = 8x8 Hadamard SATD of the
+//                     residual, computed as ONE int8 GEMM on MFMA:
+//                       D[64 x 16 blocks] = (H8 (x) H8)[64 x 64] . vec(S - P)[64 x 16]
+//                     H8 (x) H8 is the Sylvester H64 (entries (-1)^popcount(i & k)),
+//                     and S - P in [-255, 255] does not fit int8, so
+//                       H.(S - P) = H.(S - 128) + (-H).(P - 128)
+//                     (u8 ^ 0x80 is u8 - 128 as int8): the source half is computed
+//                     once per block and is the accumulator input of every candidate.
+//                     4 x mfma_i32_16x16x64_i8 per candidate per 16 blocks; the int32
+//                     accumulation is exact.
+//                 frame sums (intra, min(intra, inter)) -> [N, 2] u64, optional
+//                 per-block costs for the numerics tests.
+//
+// Layout: one wave64 = a strip of 16 horizontally adjacent blocks.  Lane l owns block
+// column c = l & 15 and rows 2g, 2g+1 (g = l >> 4) of it: exactly the B-operand
+// fragment of mfma_i32_16x16x64_i8 (16 int8 of k = 16g + j, k = 8 * row + col), so
+// the source and the predictions are loaded straight into MFMA operands.  The A
+// operand (H64, 4 row tiles of 16) is generated in registers.  SADs of the search
+// are summed over the four row groups of a column with two v_permlane{16,32}_swap.
+#include "kcommon.h"
+
+namespace mivc {
+namespace gpu {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+constexpr int kLaPad = 16;  // replicated border of the lowres planes (bytes / rows)
+
+struct LaGeom {
+  int w, h;          // full-resolution display size of the input (even)
+  long long fstride; // bytes between consecutive input luma frames
+  int N, F;          // frames in total (slot-major), frames per segment
+  int lbw, lbh;      // lowres 8x8 blocks per row / column
+  int ls, lrows;     // lowres plane pitch and rows (with the border)
+  long long lsize;   // bytes per lowres plane
+};
+
+__global__ void la_downscale(const uint8_t* __restrict__ y, LaGeom g, uint8_t* __restrict__ low) {
+  const int qw = g.ls >> 2;  // dwords per lowres row
+  const long long total = static_cast<long long>(g.N) * g.lrows * qw;
+  const long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int n = static_cast<int>(i / (static_cast<long long>(g.lrows) * qw));
+  const int rem = static_cast<int>(i - static_cast<long long>(n) * g.lrows * qw);
+  const int py = rem / qw, px4 = (rem - py * qw) * 4;
+  const int lw = g.w >> 1, lh = g.h >> 1;
+  const int ly = clampi(py - kLaPad, 0, lh - 1);
+  const uint8_t* r0 = y + n * g.fstride + static_cast<long long>(2 * ly) * g.w;
+  const uint8_t* r1 = r0 + g.w;
+  const int lx0 = px4 - kLaPad;
+  uint32_t out = 0;
+  if (lx0 >= 0 && lx0 + 4 <= lw && (g.w & 3) == 0 && (g.fstride & 3) == 0) {
+    // interior: 8 source bytes per row, dword aligned (lx0 is a multiple of 4)
+    const uint2 a = *reinterpret_cast<const uint2*>(r0 + 2 * lx0);
+    const uint2 b = *reinterpret_cast<const uint2*>(r1 + 2 * lx0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t wa = k < 2 ? a.x : a.y, wb = k < 2 ? b.x : b.y;
+      const int sh = (k & 1) * 16;
+      const uint32_t s = ((wa >> sh) & 255u) + ((wa >> (sh + 8)) & 255u) + ((wb >> sh) & 255u) +
+                         ((wb >> (sh + 8)) & 255u);
+      out |= ((s + 2u) >> 2) << (8 * k);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int lx = clampi(lx0 + k, 0, lw - 1);
+      const uint32_t s = r0[2 * lx] + r0[2 * lx + 1] + r1[2 * lx] + r1[2 * lx + 1];
+      out |= ((s + 2u) >> 2) << (8 * k);
+    }
+  }
+  *reinterpret_cast<uint32_t*>(low + n * g.lsize + static_cast<long long>(py) * g.ls + px4) = out;
+}
+
+// v(l) + v(l ^ 16) + v(l ^ 32) + v(l ^ 48): the sum over the four row groups of a block column
+__device__ __forceinline__ int sum_col_groups(int v) {
+  auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  v = static_cast<int>(p[0]) + static_cast<int>(p[1]);
+  auto q = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return static_cast<int>(q[0]) + static_cast<int>(q[1]);
+}
+
+// sum |D| of one candidate: D = accS + (-H) . (P - 128), 4 row tiles of 16
+__device__ __forceinline__ int satd_mfma(const v4i (&negH)[4], const v4i (&accS)[4], v4i pf) {
+  int s = 0;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const v4i d = __builtin_amdgcn_mfma_i32_16x16x64_i8(negH[t], pf, accS[t], 0, 0, 0);
+    s += abs(d[0]) + abs(d[1]) + abs(d[2]) + abs(d[3]);
+  }
+  return (sum_col_groups(s) + 2) >> 2;
+}
+
+__device__ __forceinline__ v4i as_s8(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  v4i r;
+  r[0] = static_cast<int>(a ^ 0x80808080u);
+  r[1] = static_cast<int>(b ^ 0x80808080u);
+  r[2] = static_cast<int>(c ^ 0x80808080u);
+  r[3] = static_cast<int>(d ^ 0x80808080u);
+  return r;
+}
+
+struct LaArgs {
+  LaGeom g;
+  const uint8_t* low;
+  unsigned long long* frame_cost;  // [N, 2]: sum intra, sum min(intra, inter)
+  int* blk_cost;                   // optional [N, 2, lbh, lbw]: intra, inter (inter = intra on key frames)
+};
+
+template <int R>
+__global__ __launch_bounds__(256) void la_cost(LaArgs a) {
+  const LaGeom& g = a.g;
+  constexpr int side = 2 * R + 1;
+  const int nstrips = (g.lbw + 15) >> 4;
+  const int per_frame = nstrips * g.lbh;
+  const long long waves = static_cast<long long>(per_frame) * g.N;
+  const int nwg = static_cast<int>((waves + 3) >> 2);
+  int lin = blockIdx.x;
+  if ((nwg & 7) == 0) lin = (lin & 7) * (nwg >> 3) + (lin >> 3);  // each XCD walks a contiguous range
+  const long long wv = static_cast<long long>(lin) * 4 + wave_id();
+  if (wv >= waves) return;  // wave-uniform
+  const int n = static_cast<int>(wv / per_frame);
+  const int rem = static_cast<int>(wv - static_cast<long long>(n) * per_frame);
+  const int by = rem / nstrips, strip = rem - by * nstrips;
+  const int lane = lane_id(), c = lane & 15, grp = lane >> 4;
+  const int bx = strip * 16 + c;
+  const bool valid = bx < g.lbw;
+  const int bxc = valid ? bx : g.lbw - 1;  // idle columns read a valid block
+  const int f = n % g.F;
+  const bool has_ref = f > 0;
+
+  // H64 row tiles as int8 A operands (and their negation): row i = 16t + (l & 15), k = 16 grp + j
+  v4i H[4], negH[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t wp = 0, wn = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int i = 16 * t + c, k = 16 * grp + 4 * q + b;
+        const bool neg = __builtin_popcount(i & k) & 1;
+        wp |= (neg ? 0xFFu : 0x01u) << (8 * b);
+        wn |= (neg ? 0x01u : 0xFFu) << (8 * b);
+      }
+      H[t][q] = static_cast<int>(wp);
+      negH[t][q] = static_cast<int>(wn);
+    }
+  }
+
+  const uint8_t* cur = a.low + n * g.lsize;
+  const int X0 = kLaPad + bxc * 8, Y0 = kLaPad + by * 8;
+  const int ry = Y0 + 2 * grp;  // this lane's two rows
+  const uint8_t* c0 = cur + static_cast<long long>(ry) * g.ls + X0;
+  const uint2 s0 = *reinterpret_cast<const uint2*>(c0);
+  const uint2 s1 = *reinterpret_cast<const uint2*>(c0 + g.ls);
+  // intra neighbours: the row above (8 bytes) and this lane's two left samples
+  const uint2 top = *reinterpret_cast<const uint2*>(cur + static_cast<long long>(Y0 - 1) * g.ls + X0);
+  const uint32_t l0 = c0[-1], l1 = c0[g.ls - 1];
+
+  // source half of every candidate's Hadamard: H . (S - 128)
+  const v4i sf = as_s8(s0.x, s0.y, s1.x, s1.y);
+  v4i accS[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) accS[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[t], sf, v4i{0, 0, 0, 0}, 0, 0, 0);
+
+  // ---- intra: DC, H, V
+  auto bsum = [](uint32_t w) { return (w & 255u) + ((w >> 8) & 255u) + ((w >> 16) & 255u) + (w >> 24); };
+  const int tsum = static_cast<int>(bsum(top.x) + bsum(top.y));
+  const int lsum = sum_col_groups(static_cast<int>(l0 + l1));
+  const uint32_t dc = static_cast<uint32_t>((tsum + lsum + 8) >> 4) * 0x01010101u;
+  const uint32_t h0 = l0 * 0x01010101u, h1 = l1 * 0x01010101u;
+  int intra = satd_mfma(negH, accS, as_s8(dc, dc, dc, dc));
+  intra = min(intra, satd_mfma(negH, accS, as_s8(h0, h0, h1, h1)));
+  intra = min(intra, satd_mfma(negH, accS, as_s8(top.x, top.y, top.x, top.y)));
+  intra += 5;  // mode-cost bias
+
+  int inter = intra;
+  if (has_ref) {  // frame-uniform
+    const uint8_t* ref = cur - g.lsize;
+    // ---- integer full search: lane accumulates the SAD of its two rows, then the column sum
+    int best = 0x7FFFFFFF;
+    for (int dy = -R; dy <= R; ++dy) {
+      uint32_t w0[7], w1[7];
+      const uint32_t* p0 = reinterpret_cast<const uint32_t*>(ref + static_cast<long long>(ry + dy) * g.ls + X0 - 8);
+      const uint32_t* p1 = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(p0) + g.ls);
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        w0[k] = p0[k];
+        w1[k] = p1[k];
+      }
+#pragma unroll
+      for (int dx = -R; dx <= R; ++dx) {
+        const int o = 8 + dx, wi = o >> 2, sh = o & 3;
+        const uint32_t a0 = __builtin_amdgcn_alignbyte(w0[wi + 1], w0[wi], sh);
+        const uint32_t a1 = __builtin_amdgcn_alignbyte(w0[wi + 2], w0[wi + 1], sh);
+        const uint32_t b0 = __builtin_amdgcn_alignbyte(w1[wi + 1], w1[wi], sh);
+        const uint32_t b1 = __builtin_amdgcn_alignbyte(w1[wi + 2], w1[wi + 1], sh);
+        uint32_t sad = sad4(s0.x, a0, 0);
+        sad = sad4(s0.y, a1, sad);
+        sad = sad4(s1.x, b0, sad);
+        sad = sad4(s1.y, b1, sad);
+        const int cost = sum_col_groups(static_cast<int>(sad)) + 2 * (abs(dx) + abs(dy));
+        const int key = (cost << 9) | ((dy + R) * side + (dx + R));
+        best = min(best, key);
+      }
+    }
+    const int bi = best & 511;
+    const int mdy = bi / side - R, mdx = bi % side - R;
+    // best prediction rows (unaligned 8 bytes: three aligned dwords + alignbyte)
+    const int xo = X0 + mdx;
+    const int xa = xo & ~3, shb = xo & 3;
+    const uint32_t* q0 = reinterpret_cast<const uint32_t*>(ref + static_cast<long long>(ry + mdy) * g.ls + xa);
+    const uint32_t* q1 = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(q0) + g.ls);
+    const uint32_t e0 = q0[0], e1 = q0[1], e2 = q0[2], f0 = q1[0], f1 = q1[1], f2 = q1[2];
+    const v4i pf = as_s8(__builtin_amdgcn_alignbyte(e1, e0, shb), __builtin_amdgcn_alignbyte(e2, e1, shb),
+                         __builtin_amdgcn_alignbyte(f1, f0, shb), __builtin_amdgcn_alignbyte(f2, f1, shb));
+    inter = satd_mfma(negH, accS, pf) + 2 * (abs(mdx) + abs(mdy));
+  }
+  const int pcost = min(intra, inter);
+  if (a.blk_cost && grp == 0 && valid) {
+    const long long base = static_cast<long long>(n) * 2 * g.lbh * g.lbw + static_cast<long long>(by) * g.lbw + bx;
+    a.blk_cost[base] = intra;
+    a.blk_cost[base + static_cast<long long>(g.lbh) * g.lbw] = inter;
+  }
+  const bool mine = grp == 0 && valid;
+  const int si = sum64(mine ? intra : 0), sp = sum64(mine ? pcost : 0);
+  if (lane == 0) {
+    atomicAdd(a.frame_cost + 2 * n, static_cast<unsigned long long>(si));
+    atomicAdd(a.frame_cost + 2 * n + 1, static_cast<unsigned long long>(sp));
+  }
+}
+
+}  // namespace gpu
+}  // namespace mivc
+
+using namespace mivc::gpu;
+
+// Bytes of the lowres workspace for N frames of w x h.
+extern "C" long long mivc_lookahead_low_bytes(int w, int h, int N) {
+  const int lbw = ((w >> 1) + 7) >> 3, lbh = ((h >> 1) + 7) >> 3;
+  return static_cast<long long>(N) * (lbw * 8 + 2 * kLaPad) * (lbh * 8 + 2 * kLaPad);
+}
+
+// y: luma of N = B*F frames (slot-major), frame f of slot b at y + (b*F + f) * fstride.
+// low: workspace of mivc_lookahead_low_bytes(); frame_cost: [N, 2] u64 (zeroed here);
+// blk_cost: optional [N, 2, lbh, lbw] int32.
+extern "C" int mivc_launch_lookahead(const uint8_t* y, int w, int h, long long fstride, int N, int F, uint8_t* low,
+                                     unsigned long long* frame_cost, int* blk_cost, int range, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (w < 16 || h < 16 || (w & 1) || (h & 1) || N <= 0 || F <= 0 || N % F) return -1;
+  if (range != 4 && range != 6 && range != 8) return -2;
+  LaGeom g{};
+  g.w = w;
+  g.h = h;
+  g.fstride = fstride;
+  g.N = N;
+  g.F = F;
+  g.lbw = ((w >> 1) + 7) >> 3;
+  g.lbh = ((h >> 1) + 7) >> 3;
+  g.ls = g.lbw * 8 + 2 * kLaPad;
+  g.lrows = g.lbh * 8 + 2 * kLaPad;
+  g.lsize = static_cast<long long>(g.ls) * g.lrows;
+  hipMemsetAsync(frame_cost, 0, sizeof(unsigned long long) * 2 * N, s);
+  const long long dwords = static_cast<long long>(N) * g.lrows * (g.ls >> 2);
+  hipLaunchKernelGGL(la_downscale, dim3(static_cast<unsigned>((dwords + 255) / 256)), dim3(256), 0, s, y, g, low);
+  LaArgs a{g, low, frame_cost, blk_cost};
+  const long long waves = static_cast<long long>((g.lbw + 15) >> 4) * g.lbh * N;
+  const dim3 grid(static_cast<unsigned>((waves + 3) >> 2));
+  switch (range) {
+    case 4: hipLaunchKernelGGL(la_cost<4>, grid, dim3(256), 0, s, a); break;
+    case 6: hipLaunchKernelGGL(la_cost<6>, grid, dim3(256), 0, s, a); break;
+    default: hipLaunchKernelGGL(la_cost<8>, grid, dim3(256), 0, s, a); break;
+  }
+  return 0;
+}

@@ -48,6 +48,9 @@ class H264Params:
     deblock: bool = True
     chroma_qp_offset: int = 0
     vui: bool = True
+    # CRF per-frame QPs from the GPU lookahead (rc/lookahead.py); False = flat CRF QP
+    lookahead: bool = True
+    la_range: int = 6
 
     def host_cfg(self) -> dict:
         return dict(width=self.width, height=self.height, fps=self.fps, qp=self.qp,
@@ -286,6 +289,22 @@ class GpuH264Encoder:
         self.timings["entropy_s"] = self.timings.get("entropy_s", 0.0) + (t2 - t1)
         return out
 
+    # ------------------------------------------------------------------ rate control
+    def crf_qps(self, y: torch.Tensor) -> np.ndarray:
+        """[B, F] CRF QPs of a batch: GPU lookahead frame costs -> x264-style CRF curve."""
+        from ..rc.lookahead import GpuLookahead
+        from ..rc.ratecontrol import crf_qps_batch
+
+        if getattr(self, "_la", None) is None:
+            self._la = GpuLookahead(self.dev, self.p.la_range)
+        t0 = time.perf_counter()
+        costs = self._la.frame_costs(y).cpu().numpy()
+        lbw, lbh = GpuLookahead.block_grid(y.shape[3], y.shape[2])
+        q = crf_qps_batch(costs, float(self.p.crf), lbw * lbh)
+        self.timings["lookahead_s"] = self.timings.get("lookahead_s", 0.0) + time.perf_counter() - t0
+        self.stats["mean_qp"] = float(q.mean())
+        return q
+
     # ------------------------------------------------------------------ public API
     @torch.no_grad()
     def encode(self, y: torch.Tensor, u: torch.Tensor, v: torch.Tensor, idr_base: int = 0,
@@ -315,6 +334,8 @@ class GpuH264Encoder:
             raise ValueError("idr_ids needs one entry per slot")
         torch.cuda.set_device(self.dev)
         qp_i, qp_p = self.p.frame_qps()
+        if qps is None and self.p.crf is not None and self.p.lookahead:
+            qps = self.crf_qps(y)
         if qps is None:
             qps_h = np.full((B, F), qp_p, dtype=np.int32)
             qps_h[:, 0] = qp_i

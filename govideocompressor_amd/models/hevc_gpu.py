@@ -47,6 +47,9 @@ class HevcParams:
     max_merge: int = 5
     me_range: int = 8
     subpel: int = 2
+    # CRF per-frame QPs from the GPU lookahead (rc/lookahead.py); False = flat CRF QP
+    lookahead: bool = True
+    la_range: int = 6
 
     def host_cfg(self) -> dict:
         return dict(width=self.width, height=self.height, bit_depth=self.bit_depth, fps=self.fps,
@@ -155,6 +158,24 @@ class GpuHevcEncoder:
             self.hip.hevc_prep(B, plane.data_ptr(), src.stride(0) * bps, src.stride(2), bps, ww, hh, dst.data_ptr(),
                                dst.shape[2], dst.shape[1], shift, s)
 
+    # ------------------------------------------------------------------ rate control
+    def crf_qps(self, y: torch.Tensor) -> np.ndarray:
+        """[B, F] CRF QPs: GPU lookahead on the (8-bit proxy of the) luma -> CRF curve."""
+        from ..rc.lookahead import GpuLookahead
+        from ..rc.ratecontrol import crf_qps_batch
+
+        if getattr(self, "_la", None) is None:
+            self._la = GpuLookahead(self.dev, self.p.la_range)
+        t0 = time.perf_counter()
+        y8 = y
+        if y.dtype != torch.uint8:
+            y8 = (y >> (self.p.bit_depth - 8)).clamp_(0, 255).to(torch.uint8)
+        costs = self._la.frame_costs(y8.contiguous()).cpu().numpy()
+        lbw, lbh = GpuLookahead.block_grid(y.shape[3], y.shape[2])
+        q = crf_qps_batch(costs, float(self.p.crf), lbw * lbh, keyint=self.p.keyint or None)
+        self.timings["lookahead_s"] = self.timings.get("lookahead_s", 0.0) + time.perf_counter() - t0
+        return q
+
     # ------------------------------------------------------------------ encode
     def encode(self, y: torch.Tensor, u: torch.Tensor, v: torch.Tensor, qps: np.ndarray | None = None,
                keep_recon: bool = False, metrics: bool = True) -> list[HevcSegmentResult]:
@@ -167,6 +188,8 @@ class GpuHevcEncoder:
         if y.device != self.dev:
             raise ValueError("inputs must live on the encoder's device")
         qi, qpp = self.p.frame_qps()
+        if qps is None and self.p.crf is not None and self.p.lookahead and not self.p.intra_only:
+            qps = self.crf_qps(y)
         if qps is None:
             qps = np.array([[qi if t == 0 else qpp for t in range(F)] for _ in range(B)], dtype=np.int32)
         cfg = self.p.host_cfg()

@@ -1,0 +1,131 @@
+"""GPU lookahead: lowres frame costs of B segments x F frames in one pass.
+
+Reference behaviour replaced: the per-frame quantiser of libx264's CRF mode
+(``-vcodec libx264`` -> CRF 23 default, server.go:67-71, run by the worker at
+client.go:115) comes from x264's half-resolution lookahead.  Here the lookahead
+is ``csrc/kernels/lookahead.hip``: a 2x2 downscale, an integer full search per
+8x8 lowres block, DC/H/V intra candidates and the 8x8 Hadamard SATD of every
+candidate as an int8 GEMM on the MFMA units.  Every frame of every slot is
+independent work, so one launch covers the whole batch; the [B, F, 2] frame
+costs feed :func:`~govideocompressor_amd.rc.ratecontrol.crf_qps_batch`.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..ops import native
+
+RANGES = (4, 6, 8)
+
+
+class GpuLookahead:
+    """Lowres cost analysis on gfx950 (workspace cached across calls)."""
+
+    def __init__(self, device: str | torch.device = "cuda", search_range: int = 6):
+        if search_range not in RANGES:
+            raise ValueError(f"search_range must be one of {RANGES}")
+        self.dev = torch.device(device)
+        if self.dev.type == "cuda" and self.dev.index is None:
+            self.dev = torch.device("cuda", torch.cuda.current_device())
+        self.range = int(search_range)
+        self.hip = native.hip()
+        self._low: torch.Tensor | None = None
+        self._cost: torch.Tensor | None = None
+
+    @staticmethod
+    def block_grid(width: int, height: int) -> tuple[int, int]:
+        """(lowres 8x8 blocks per row, per column) = one per 16x16 macroblock."""
+        return ((width // 2) + 7) // 8, ((height // 2) + 7) // 8
+
+    def _workspace(self, w: int, h: int, n: int) -> tuple[torch.Tensor, torch.Tensor]:
+        need = int(self.hip.lookahead_low_bytes(w, h, n))
+        if self._low is None or self._low.numel() < need:
+            self._low = torch.empty((need,), dtype=torch.uint8, device=self.dev)
+        if self._cost is None or self._cost.shape[0] < n:
+            self._cost = torch.empty((n, 2), dtype=torch.int64, device=self.dev)
+        return self._low, self._cost[:n]
+
+    @torch.no_grad()
+    def frame_costs(self, y: torch.Tensor, block_costs: bool = False):
+        """y: [B, F, h, w] uint8 luma on the device (the encoder's input layout).
+
+        Returns a device tensor [B, F, 2] int64 = (sum of intra costs, sum of
+        min(intra, inter) costs) per frame (the first frame of a segment is intra
+        only), and with ``block_costs`` also [B, F, 2, lbh, lbw] int32 per-block costs.
+        """
+        if y.dtype != torch.uint8 or y.dim() != 4 or y.device != self.dev:
+            raise ValueError("y must be a uint8 [B, F, h, w] tensor on the lookahead's device")
+        if y.stride(3) != 1 or y.stride(2) != y.shape[3] or y.stride(0) != y.shape[1] * y.stride(1):
+            raise ValueError("y frames must be dense rows with slot-major frame order")
+        B, F, h, w = y.shape
+        if h % 2 or w % 2 or h < 16 or w < 16:
+            raise ValueError("frame size must be even and at least 16x16")
+        n = B * F
+        low, cost = self._workspace(w, h, n)
+        blk = None
+        if block_costs:
+            lbw, lbh = self.block_grid(w, h)
+            blk = torch.zeros((B, F, 2, lbh, lbw), dtype=torch.int32, device=self.dev)
+        self.hip.lookahead(y.data_ptr(), w, h, y.stride(1), n, F, low.data_ptr(), cost.data_ptr(),
+                           blk.data_ptr() if blk is not None else 0, self.range,
+                           torch.cuda.current_stream(self.dev).cuda_stream)
+        out = cost.view(B, F, 2)
+        return (out, blk) if block_costs else out
+
+
+def lookahead_reference(y: np.ndarray, search_range: int = 6) -> tuple[np.ndarray, np.ndarray]:
+    """Plain numpy model of ``lookahead.hip`` (the numerics-test oracle).
+
+    y: [B, F, h, w] uint8.  Returns (frame costs [B, F, 2] int64, block costs
+    [B, F, 2, lbh, lbw] int64).  SATD = (sum |H64 . vec(S - P)| + 2) >> 2 with
+    H64[i, k] = (-1)^popcount(i & k) and vec index k = 8 * row + col.
+    """
+    B, F, h, w = y.shape
+    R, pad = search_range, 16
+    lw, lh = w // 2, h // 2
+    lbw, lbh = (lw + 7) // 8, (lh + 7) // 8
+    ls, lr = lbw * 8 + 2 * pad, lbh * 8 + 2 * pad
+    px = np.clip(np.arange(ls) - pad, 0, lw - 1)
+    py = np.clip(np.arange(lr) - pad, 0, lh - 1)
+    yy = y.astype(np.int64)
+    s = (yy[..., 0::2, 0::2][..., :lh, :lw] + yy[..., 0::2, 1::2][..., :lh, :lw] +
+         yy[..., 1::2, 0::2][..., :lh, :lw] + yy[..., 1::2, 1::2][..., :lh, :lw] + 2) >> 2
+    low = s[..., py, :][..., :, px]  # [B, F, lr, ls]
+    idx = np.arange(64)
+    pc = np.vectorize(lambda v: bin(v).count("1"))(idx[:, None] & idx[None, :])
+    H = np.where(pc % 2 == 1, -1, 1).astype(np.int64)
+
+    def satd(res: np.ndarray) -> int:
+        return int((np.abs(H @ res.reshape(64)).sum() + 2) >> 2)
+
+    blk = np.zeros((B, F, 2, lbh, lbw), dtype=np.int64)
+    side = 2 * R + 1
+    for b in range(B):
+        for f in range(F):
+            cur = low[b, f]
+            ref = low[b, f - 1] if f > 0 else None
+            for by in range(lbh):
+                for bx in range(lbw):
+                    X0, Y0 = pad + 8 * bx, pad + 8 * by
+                    S = cur[Y0:Y0 + 8, X0:X0 + 8]
+                    top = cur[Y0 - 1, X0:X0 + 8]
+                    left = cur[Y0:Y0 + 8, X0 - 1]
+                    dc = (int(top.sum()) + int(left.sum()) + 8) >> 4
+                    intra = min(satd(S - dc), satd(S - left[:, None]), satd(S - top[None, :])) + 5
+                    inter = intra
+                    if ref is not None:
+                        best = None
+                        for dy in range(-R, R + 1):
+                            for dx in range(-R, R + 1):
+                                P = ref[Y0 + dy:Y0 + dy + 8, X0 + dx:X0 + dx + 8]
+                                key = (int(np.abs(S - P).sum()) + 2 * (abs(dx) + abs(dy)), (dy + R) * side + dx + R)
+                                if best is None or key < best[0]:
+                                    best = (key, dx, dy)
+                        _, mdx, mdy = best
+                        P = ref[Y0 + mdy:Y0 + mdy + 8, X0 + mdx:X0 + mdx + 8]
+                        inter = satd(S - P) + 2 * (abs(mdx) + abs(mdy))
+                    blk[b, f, 0, by, bx] = intra
+                    blk[b, f, 1, by, bx] = inter
+    frame = np.stack([blk[:, :, 0].sum(axis=(2, 3)), np.minimum(blk[:, :, 0], blk[:, :, 1]).sum(axis=(2, 3))], axis=-1)
+    return frame, blk

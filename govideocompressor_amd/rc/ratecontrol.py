@@ -95,6 +95,34 @@ def crf_qps(intra: np.ndarray, inter: np.ndarray, crf: float, mb_count: int, key
     return np.array([clamp_qp(q) for q in qp], dtype=np.int32)
 
 
+def crf_qps_batch(costs: np.ndarray, crf: float, mb_count: int, keyint: int | None = None, blur: float = 0.5,
+                  qp_min: int = QP_MIN, qp_max: int = QP_MAX) -> np.ndarray:
+    """:func:`crf_qps` for B closed-GOP segments at once.
+
+    ``costs``: [B, F, 2] lowres frame costs (intra, min(intra, inter)) as produced by
+    :class:`~govideocompressor_amd.rc.lookahead.GpuLookahead`; frame 0 of each segment
+    is the IDR (intra complexity, QP - IP_OFFSET), and so is every ``keyint``-th frame.
+    Returns [B, F] int32 QPs."""
+    c = np.asarray(costs, dtype=np.float64)
+    B, F = c.shape[0], c.shape[1]
+    g = keyint if keyint and keyint > 0 else F
+    cplx = np.maximum(c[:, :, 1].copy(), 1.0)
+    cplx[:, ::g] = np.maximum(c[:, ::g, 0], 1.0)
+    blurred = np.empty_like(cplx)
+    acc = np.zeros(B)
+    wsum = 0.0
+    for t in range(F):
+        acc = acc * blur + cplx[:, t]
+        wsum = wsum * blur + 1.0
+        blurred[:, t] = acc / wsum
+    base = 80.0 * mb_count
+    rate_factor = base ** (1.0 - QCOMP) / qp2qscale(crf)
+    qs = np.maximum(blurred ** (1.0 - QCOMP) / rate_factor, 1e-9)
+    qp = 12.0 + 6.0 * np.log2(qs / 0.85)
+    qp[:, ::g] -= IP_OFFSET
+    return np.clip(np.round(qp), max(QP_MIN, qp_min), min(QP_MAX, qp_max)).astype(np.int32)
+
+
 def abr_solve(stats: np.ndarray, target_bits: float, exponent: float = 1.0) -> float:
     """Global QP offset so that the predicted total bits hit ``target_bits``.
 
