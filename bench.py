@@ -8,8 +8,10 @@ scaling: every rank encodes B closed-GOP segments of F frames per step.  A timed
     synthesize B*F new 1080p frames in HBM (new content every step)
     -> GPU lookahead over all B*F frames (lowres search + MFMA Hadamard SATD) -> CRF QPs
     -> batched GPU encode (ME, TQ, intra/deblock wavefronts, CAVLC)
-    -> gather every rank's segment bitstreams to all ranks (RCCL all_gather over xGMI)
-    -> rank 0 concatenates the pieces in segment order (the reference's concat.sh)
+    -> merge: piece sizes + packed bitstreams all-gathered over xGMI (RCCL), rank 0
+       copies every rank's bytes back to back into ONE Annex-B stream in segment order
+       (the reference's concat.sh); runs on a side stream/thread, overlapping the next
+       step's encode, and the next step's input synthesis is queued before it
 
 bracketed by barrier + torch.cuda.synchronize(); the step time is the max over ranks.
 The reference publishes no numbers, so vs_baseline is null.
@@ -17,6 +19,7 @@ The reference publishes no numbers, so vs_baseline is null.
 from __future__ import annotations
 
 import argparse
+import concurrent.futures as cf
 import json
 import os
 import sys
@@ -46,7 +49,6 @@ def main() -> None:
     import torch
 
     from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
-    from govideocompressor_amd.ops import native
     from govideocompressor_amd.parallel import dist as D
 
     env = D.init(prefer_gpu=True)
@@ -55,50 +57,65 @@ def main() -> None:
     if env.world != a.gpus:
         if env.is_main:
             print(f"warning: --gpus {a.gpus} but WORLD_SIZE {env.world}", file=sys.stderr)
-    host = native.host()
     p = H264Params(width=a.width, height=a.height, fps=30.0, crf=a.crf)
     enc = GpuH264Encoder(p, slots=a.slots, device=env.device,
                          entropy_threads=int(os.environ.get("MIVC_ENTROPY_THREADS", "16")))
     B, F = a.slots, a.frames
 
-    def one_step(step: int, metrics: bool):
+    merger = D.SegmentMerge(env)
+    merge_stream = torch.cuda.Stream(device=env.device)
+    merge_pool = cf.ThreadPoolExecutor(max_workers=1)
+
+    def synth(step: int):
         seed = 1000 + step * 7919 + env.rank * 104729
-        y, u, v = synth_clip(B, F, a.width, a.height, seed=seed, device=env.device)
-        res = enc.encode(y, u, v, idr_base=env.rank * B, metrics=metrics)
-        g = D.BitstreamGather(env, [r.bitstream for r in res]).start()
-        pieces = g.wait()
-        merged = None
-        if env.is_main:
-            ordered = [pc for rank_pieces in pieces for pc in rank_pieces]
-            merged = host.concat(ordered)
-        return res, merged
+        return synth_clip(B, F, a.width, a.height, seed=seed, device=env.device)
+
+    def merge(res):
+        # CC-2/CC-3 + concat on a side stream: overlaps the next batch's encode
+        with torch.cuda.device(env.device), torch.cuda.stream(merge_stream):
+            return merger.run([r.parts() for r in res])
+
+    def run_steps(first: int, n: int, metrics_first: bool = False):
+        """n steps: synthesize (new content) -> lookahead + encode -> merge on rank 0.
+        The next step's input synthesis is queued on the GPU before this step's merge
+        runs on the host, and the merge of step k overlaps the encode of step k + 1."""
+        clip = synth(first)
+        fut = None
+        for k in range(n):
+            y, u, v = clip
+            res = enc.encode(y, u, v, idr_base=env.rank * B, metrics=(metrics_first and k == 0))
+            del y, u, v
+            clip = synth(first + k + 1) if k + 1 < n else None
+            if fut is not None:
+                fut.result()
+            fut = merge_pool.submit(merge, res)
+            if k == 0:
+                first_res = res
+        merged = fut.result()
+        return first_res, res, merged
 
     # PSNR/SSIM are measured on the (untimed) first warmup step: quality measurement is not
     # part of encoding (an ffmpeg/x264 encode computes none unless asked); the timed steps
     # encode the same content distribution (new seed per step).
     qres = None
-    for w in range(a.warmup):
-        r, _ = one_step(-1 - w, metrics=(w == 0 and a.quality))
-        if w == 0:
-            qres = r
+    if a.warmup:
+        qres, _, _ = run_steps(-100, a.warmup, metrics_first=a.quality)
     D.barrier(env)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    last = None
-    for s in range(a.steps):
-        last = one_step(s, metrics=False)
+    _, res, merged = run_steps(0, a.steps)
     torch.cuda.synchronize()
     D.barrier(env)
     t1 = time.perf_counter()
     elapsed = D.max_over_ranks(env, t1 - t0)
-    res, merged = last
+    merge_pool.shutdown()
     total_frames = env.world * B * F * a.steps
     fps = total_frames / elapsed
     # quality of the warmup step, rate of the last timed step (this rank), averaged over ranks
     q = qres if (qres is not None and a.quality) else None
     psnr = D.sum_over_ranks(env, sum(r.psnr_y for r in q) / len(q) if q else 0.0) / env.world
     ssim = D.sum_over_ranks(env, sum(r.ssim_y for r in q) / len(q) if q else 0.0) / env.world
-    nbytes = D.sum_over_ranks(env, float(sum(len(r.bitstream) for r in res)))
+    nbytes = D.sum_over_ranks(env, float(sum(r.nbytes() for r in res)))
     kbps = nbytes * 8 / (env.world * B * F / p.fps) / 1000.0
     if env.is_main:
         out = {

@@ -19,7 +19,7 @@ import concurrent.futures as cf
 import math
 import os
 import time
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 
 import numpy as np
 import torch
@@ -65,16 +65,34 @@ class H264Params:
         return max(0, qp_p - self.ip_offset), qp_p
 
 
-@dataclass
 class SegmentResult:
-    bitstream: bytes
-    frames: int
-    nals: list[bytes] = field(default_factory=list)   # per-frame slice NALs (bitstream = SPS/PPS + nals)
-    bits: list[int] = field(default_factory=list)
-    psnr_y: float = 0.0
-    psnr_u: float = 0.0
-    psnr_v: float = 0.0
-    ssim_y: float = 0.0
+    """One encoded closed-GOP segment: parameter sets + one slice NAL per frame.
+
+    ``bitstream`` (the Annex-B piece) is joined on first access; the segment merge
+    packs ``parts()`` straight into its staging buffer instead."""
+
+    __slots__ = ("frames", "nals", "bits", "header", "psnr_y", "psnr_u", "psnr_v", "ssim_y", "_bs")
+
+    def __init__(self, frames: int, nals: list[bytes] | None = None, bits: list[int] | None = None,
+                 header: bytes = b"", bitstream: bytes | None = None):
+        self.frames = frames
+        self.nals = list(nals or [])
+        self.bits = list(bits or [])
+        self.header = header
+        self._bs = bitstream
+        self.psnr_y = self.psnr_u = self.psnr_v = self.ssim_y = 0.0
+
+    @property
+    def bitstream(self) -> bytes:
+        if self._bs is None:
+            self._bs = self.header + b"".join(self.nals)
+        return self._bs
+
+    def parts(self) -> list[bytes]:
+        return [self._bs] if self._bs is not None else [self.header, *self.nals]
+
+    def nbytes(self) -> int:
+        return len(self._bs) if self._bs is not None else len(self.header) + sum(len(n) for n in self.nals)
 
 
 def _resolve(device) -> torch.device:
@@ -420,7 +438,7 @@ class GpuH264Encoder:
         nwin = (self.p.width // 8) * (self.p.height // 8)
         for b in range(B):
             nals = [outs[t][b][0] for t in range(F)]
-            r = SegmentResult(bitstream=ps + b"".join(nals), frames=F, nals=nals, bits=[outs[t][b][1] for t in range(F)])
+            r = SegmentResult(frames=F, nals=nals, bits=[outs[t][b][1] for t in range(F)], header=ps)
             if metrics:
                 def psnr(ssev, n):
                     mse = ssev / n

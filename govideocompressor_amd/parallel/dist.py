@@ -177,3 +177,110 @@ class BitstreamGather:
                 off += sz
             out.append(lst)
         return out
+
+
+class SegmentMerge:
+    """CC-2 + CC-3 + K-D: every rank's segment bitstreams -> ONE Annex-B stream on rank 0.
+
+    The reference collects worker outputs over FTP (client.go:142-172) and stream-copies
+    them in ``filelist.txt`` order with ``concat.sh`` (server.go:325-361).  Here, per
+    batch:
+
+    1. each rank packs its pieces (rank-major segment order) into a pinned host
+       buffer -- on one rank this packing IS the concatenation;
+    2. piece sizes: one tiny ``all_gather_into_tensor`` (CC-2);
+    3. payload: H2D of the packed bytes, one ``all_gather_into_tensor`` of
+       [world x max_bytes] (CC-3, RCCL over xGMI);
+    4. rank 0 alone copies each rank's used prefix back to a pinned host buffer,
+       back to back, so the DMA engine does the compaction: no host memcpy of the
+       other ranks' bytes, and no other rank pays a device-to-host copy.
+
+    Buffers are kept and grown (x1.25) across calls.  ``run`` uses the caller's
+    current stream, so a caller on a side stream overlaps the merge with compute.
+    """
+
+    def __init__(self, env: DistEnv):
+        self.env = env
+        self._pack: torch.Tensor | None = None
+        self._out: torch.Tensor | None = None
+        self._send: torch.Tensor | None = None
+        self._recv: torch.Tensor | None = None
+
+    @staticmethod
+    def _grow(buf, n: int, pinned: bool, device=None):
+        if buf is not None and buf.numel() >= n:
+            return buf
+        cap = max(1 << 20, int(n * 1.25))
+        if pinned:
+            t = torch.empty((cap,), dtype=torch.uint8)
+            return t.pin_memory() if torch.cuda.is_available() else t
+        return torch.empty((cap,), dtype=torch.uint8, device=device)
+
+    def _pack_local(self, pieces) -> tuple["np.ndarray", list[int]]:
+        import numpy as np
+
+        parts = [p if isinstance(p, (list, tuple)) else [p] for p in pieces]
+        sizes = [sum(len(x) for x in ps) for ps in parts]
+        total = sum(sizes)
+        self._pack = self._grow(self._pack, total, pinned=True)
+        arr = self._pack.numpy()
+        off = 0
+        for ps in parts:
+            for x in ps:
+                n = len(x)
+                if n:
+                    arr[off:off + n] = np.frombuffer(x, dtype=np.uint8)
+                    off += n
+        return arr[:total], sizes
+
+    @staticmethod
+    def _check_start_codes(buf, sizes) -> None:
+        off = 0
+        for n in sizes:
+            if n:
+                h = bytes(buf[off:off + 4])
+                if not (h[:3] == b"\0\0\1" or h == b"\0\0\0\1"):
+                    raise RuntimeError("segment merge: a piece does not start with an Annex-B start code")
+            off += n
+
+    def run(self, pieces) -> "np.ndarray | None":
+        """pieces: this rank's segments (bytes, or a list of byte parts each).
+        Returns the merged stream (uint8 view of a pinned buffer, valid until the next
+        call) on rank 0, ``None`` on the other ranks."""
+        import numpy as np
+
+        env = self.env
+        local, sizes = self._pack_local(pieces)
+        self._check_start_codes(local, sizes)
+        if not env.initialized:
+            return local
+        dev = env.device
+        n_loc = torch.tensor([local.size], dtype=torch.int64, device=dev)
+        all_n = torch.empty(env.world, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(all_n, n_loc)
+        per_rank = all_n.cpu().tolist()
+        stride = max(1, max(per_rank))
+        self._send = self._grow(self._send, stride, pinned=False, device=dev)
+        self._recv = self._grow(self._recv, env.world * stride, pinned=False, device=dev)
+        send = self._send[:stride]
+        if local.size:
+            send[:local.size].copy_(self._pack[:local.size], non_blocking=True)
+        recv = self._recv[:env.world * stride]
+        dist.all_gather_into_tensor(recv, send)
+        if not env.is_main:
+            # the staging buffer is reused by the next call: wait for the H2D read
+            torch.cuda.current_stream(dev).synchronize() if dev.type == "cuda" else None
+            return None
+        total = sum(per_rank)
+        self._out = self._grow(self._out, total, pinned=True)
+        off = 0
+        for r, n in enumerate(per_rank):
+            if n:
+                self._out[off:off + n].copy_(recv[r * stride: r * stride + n], non_blocking=True)
+            off += n
+        if dev.type == "cuda":
+            torch.cuda.current_stream(dev).synchronize()
+        out = self._out.numpy()[:total]
+        if out.size and not (bytes(out[:3]) == b"\0\0\1" or bytes(out[:4]) == b"\0\0\0\1"):
+            raise RuntimeError("segment merge: merged stream does not start with a start code")
+        return np.asarray(out)

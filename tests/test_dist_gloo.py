@@ -76,6 +76,52 @@ def test_collectives_gloo():
     assert sorted(tickets) == list(range(23))
 
 
+def _merge(rank, world, port, q):
+    _env(rank, world, port)
+    from govideocompressor_amd.parallel import dist as D
+    env = D.init(prefer_gpu=False)
+    try:
+        m = D.SegmentMerge(env)
+        outs = []
+        for it in range(2):  # buffers are reused across calls
+            sc = b"\0\0\0\1"
+            if rank == 1:
+                pieces = []  # a rank with nothing to contribute
+            else:
+                pieces = [sc + bytes([rank, it]) * (5 + rank), [sc, bytes([9]) * (3 + it), bytes([rank])]]
+            got = m.run(pieces)
+            outs.append(None if got is None else bytes(got))
+        bad = None
+        try:
+            m.run([b"\1\2\3\4\5"])
+        except RuntimeError as e:
+            bad = str(e)
+        q.put((rank, outs, bad))
+    finally:
+        D.shutdown(env)
+
+
+def test_segment_merge_gloo():
+    world, port = 3, _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_merge, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)])
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    sc = b"\0\0\0\1"
+    for it in range(2):
+        want = b""
+        for r in (0, 2):
+            want += sc + bytes([r, it]) * (5 + r) + sc + bytes([9]) * (3 + it) + bytes([r])
+        assert res[0][1][it] == want
+        assert res[1][1][it] is None and res[2][1][it] is None
+    assert all(bad and "start code" in bad for _, _, bad in res)
+
+
 def _encode(rank, world, port, src, out, schedule):
     _env(rank, world, port)
     from govideocompressor_amd.pipeline import encode_file
