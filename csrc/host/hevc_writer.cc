@@ -329,30 +329,61 @@ struct Writer {
     }
   }
 
+  // scan orders (6.5.3-6.5.5) as tables: [scan_idx][log2 of the grid side 0..3][position] -> x | y << 4
+  struct ScanTables {
+    uint8_t t[3][4][64];
+    ScanTables() {
+      for (int s = 0; s < 3; ++s)
+        for (int l = 0; l < 4; ++l)
+          for (int i = 0; i < (1 << (2 * l)); ++i) {
+            const int p = scan_pos(s, l, i);
+            t[s][l][i] = static_cast<uint8_t>((p & 255) | ((p >> 8) << 4));
+          }
+    }
+  };
+  static const ScanTables& scans() {
+    static const ScanTables tables;
+    return tables;
+  }
+
+  // 7.3.8.11 residual_coding.  The coefficient groups are visited through the scan
+  // tables; each group's 16 levels are gathered once (4 row loads) and an all-zero
+  // group costs 4 loads, so sparse 32x32 blocks are cheap.
   void write_residual(const int16_t* blk, int stride, int log2, int cidx, int scan_idx) {
-    const int log2sb = log2 - 2, nsb = 1 << log2sb;
-    int sbx[64], sby[64], px[16], py[16];
-    for (int i = 0; i < nsb * nsb; ++i) {
-      const int p = scan_pos(scan_idx, log2sb, i);
-      sbx[i] = p & 255;
-      sby[i] = p >> 8;
-    }
-    for (int i = 0; i < 16; ++i) {
-      const int p = scan_pos(scan_idx, 2, i);
-      px[i] = p & 255;
-      py[i] = p >> 8;
-    }
-    auto at = [&](int i, int p) { return static_cast<int>(blk[(sby[i] * 4 + py[p]) * stride + sbx[i] * 4 + px[p]]); };
+    const int log2sb = log2 - 2, nsb = 1 << log2sb, nsbsq = nsb * nsb;
+    const uint8_t* sbs = scans().t[scan_idx][log2sb];
+    const uint8_t* ps = scans().t[scan_idx][2];
+    auto group_rows = [&](int i, int16_t (&rows)[4][4]) {
+      const int xs = sbs[i] & 15, ys = sbs[i] >> 4;
+      const int16_t* b = blk + static_cast<size_t>(ys * 4) * stride + xs * 4;
+      for (int r = 0; r < 4; ++r) std::memcpy(rows[r], b + static_cast<size_t>(r) * stride, sizeof(rows[r]));
+    };
+    auto any_row = [](const int16_t (&rows)[4][4]) {
+      uint64_t a = 0;
+      for (int r = 0; r < 4; ++r) {
+        uint64_t w;
+        std::memcpy(&w, rows[r], 8);
+        a |= w;
+      }
+      return a != 0;
+    };
+    // last significant group / position
     int last_i = -1, last_p = -1;
-    for (int i = nsb * nsb - 1; i >= 0 && last_i < 0; --i)
+    int16_t lv[16];
+    for (int i = nsbsq - 1; i >= 0 && last_i < 0; --i) {
+      int16_t rows[4][4];
+      group_rows(i, rows);
+      if (!any_row(rows)) continue;
+      for (int p = 0; p < 16; ++p) lv[p] = rows[ps[p] >> 4][ps[p] & 15];
       for (int p = 15; p >= 0; --p)
-        if (at(i, p) != 0) {
+        if (lv[p] != 0) {
           last_i = i;
           last_p = p;
           break;
         }
+    }
     if (last_i < 0) throw std::runtime_error("residual_coding of an all-zero block");
-    int lx = sbx[last_i] * 4 + px[last_p], ly = sby[last_i] * 4 + py[last_p];
+    int lx = (sbs[last_i] & 15) * 4 + (ps[last_p] & 15), ly = (sbs[last_i] >> 4) * 4 + (ps[last_p] >> 4);
     if (scan_idx == 2) std::swap(lx, ly);
     write_last(lx, log2, cidx, CTX_LAST_X);
     write_last(ly, log2, cidx, CTX_LAST_Y);
@@ -363,9 +394,19 @@ struct Writer {
     int c1 = 1;
     bool first_sb = true;
     for (int i = last_i; i >= 0; --i) {
-      const int xs = sbx[i], ys = sby[i];
-      bool nonzero = false;
-      for (int p = 0; p < 16; ++p) nonzero |= at(i, p) != 0;
+      const int xs = sbs[i] & 15, ys = sbs[i] >> 4;
+      int16_t lvl[16];
+      bool nonzero;
+      if (i == last_i) {
+        std::memcpy(lvl, lv, sizeof(lvl));
+        nonzero = true;
+      } else {
+        int16_t rows[4][4];
+        group_rows(i, rows);
+        nonzero = any_row(rows);
+        if (nonzero)
+          for (int p = 0; p < 16; ++p) lvl[p] = rows[ps[p] >> 4][ps[p] & 15];
+      }
       bool infer_dc = false;
       if (i < last_i && i > 0) {
         int cs = 0;
@@ -376,6 +417,7 @@ struct Writer {
         infer_dc = true;
       } else {
         csbf[xs][ys] = 1;
+        if (!nonzero) std::memset(lvl, 0, sizeof(lvl));  // DC group of a block: coded even if empty
       }
       if (!csbf[xs][ys]) continue;
       int prev_csbf = 0;
@@ -383,11 +425,11 @@ struct Writer {
       if (ys < nsb - 1) prev_csbf += csbf[xs][ys + 1] << 1;
       // significance
       int vals[16], nsig = 0;
-      if (i == last_i) vals[nsig++] = at(i, last_p);
+      if (i == last_i) vals[nsig++] = lvl[last_p];
       for (int p = (i == last_i ? last_p - 1 : 15); p >= 0; --p) {
-        const int v = at(i, p);
+        const int v = lvl[p];
         if (p > 0 || !infer_dc) {
-          const int xc = xs * 4 + px[p], yc = ys * 4 + py[p];
+          const int xc = xs * 4 + (ps[p] & 15), yc = ys * 4 + (ps[p] >> 4);
           e.encode(v != 0, ctx[CTX_SIG + sig_ctx(xc, yc, log2, cidx, scan_idx, prev_csbf, xs, ys)]);
           if (v != 0) infer_dc = false;
         }
@@ -416,7 +458,9 @@ struct Writer {
         g2 = std::abs(vals[g1_first]) > 2;
         e.encode(g2, ctx[CTX_GT2 + (cidx ? 4 : 0) + ctx_set]);
       }
-      for (int k = 0; k < nsig; ++k) e.bypass(vals[k] < 0);
+      uint32_t signs = 0;
+      for (int k = 0; k < nsig; ++k) signs = (signs << 1) | (vals[k] < 0);
+      e.bypass_bits(signs, nsig);
       int rice = 0;
       for (int k = 0; k < nsig; ++k) {
         const int a = std::abs(vals[k]);
@@ -455,12 +499,18 @@ struct Writer {
 
   static int mdcs(int mode) { return (mode >= 6 && mode <= 14) ? 2 : ((mode >= 22 && mode <= 30) ? 1 : 0); }
 
-  bool any_nonzero(int cidx, int x, int y, int n) const {
+  bool any_nonzero(int cidx, int x, int y, int n) const {  // n is a multiple of 4
     const int stride = cidx ? W / 2 : W;
     const int16_t* p = coef[cidx] + static_cast<size_t>(y) * stride + x;
-    for (int r = 0; r < n; ++r)
-      for (int k = 0; k < n; ++k)
-        if (p[r * stride + k]) return true;
+    for (int r = 0; r < n; ++r) {
+      uint64_t a = 0;
+      for (int k = 0; k < n; k += 4) {
+        uint64_t w;
+        std::memcpy(&w, p + static_cast<size_t>(r) * stride + k, 8);
+        a |= w;
+      }
+      if (a) return true;
+    }
     return false;
   }
 

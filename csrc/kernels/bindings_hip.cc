@@ -38,8 +38,6 @@ void mivc_launch_decode_picture(int B, int wmb, int hmb, const uint8_t* ref_y, c
                                 const uint8_t* ref_v, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const void* hdr,
                                 const uint32_t* mask, const uint32_t* off, const int16_t* coef, const int8_t* run,
                                 int any_p, int chroma_qp_offset, uint8_t* nz, int* err, void* stream);
-void mivc_launch_hevc_prep(int B, const void* src, long long slot_stride, int pitch, int bps, int w, int h,
-                           uint16_t* dst, int W, int H, int shift, void* stream);
 void mivc_launch_hevc_intra(int B, int W, int H, const uint16_t* sy, const uint16_t* su, const uint16_t* sv,
                             uint16_t* ry, uint16_t* ru, uint16_t* rv, void* ctu, void* cu, int16_t* cy, int16_t* cu_,
                             int16_t* cv, const int* qp, const int8_t* run, int* cand, int bd, int analyze, int recon,
@@ -63,6 +61,10 @@ void mivc_launch_sse(int B, int W, int H, int w, int h, const uint8_t* sy, const
                      const uint8_t* ry, const uint8_t* ru, const uint8_t* rv, unsigned long long* sse,
                      float* ssim_sum, void* stream);
 long long mivc_lookahead_low_bytes(int w, int h, int N);
+int mivc_launch_hevc_prep_frame(int B, const void* sy, const void* su, const void* sv, long long ss_y, long long ss_c,
+                                int pitch_y, int pitch_c, int bps, int w, int h, uint16_t* dy, uint16_t* du,
+                                uint16_t* dv, uint8_t* d8, int W, int H, int shift, int bd, void* stream);
+int mivc_launch_hevc_proxy8(const uint16_t* src, uint8_t* dst, long long n, int shift, void* stream);
 int mivc_launch_lookahead(const uint8_t* y, int w, int h, long long fstride, int N, int F, uint8_t* low,
                           unsigned long long* frame_cost, int* blk_cost, int range, void* stream);
 }
@@ -131,9 +133,17 @@ PYBIND11_MODULE(_hip, m) {
                                P<int16_t>(coef), P<int8_t>(run), any_p, cqo, P<uint8_t>(nz), P<int>(err), S(stream));
   });
   // ---- HEVC
-  m.def("hevc_prep", [](int B, uintptr_t src, long long slot_stride, int pitch, int bps, int w, int h, uintptr_t dst,
-                        int W, int H, int shift, uintptr_t stream) {
-    mivc_launch_hevc_prep(B, P<void>(src), slot_stride, pitch, bps, w, h, P<uint16_t>(dst), W, H, shift, S(stream));
+  m.def("hevc_prep_frame", [](int B, uintptr_t sy, uintptr_t su, uintptr_t sv, long long ss_y, long long ss_c,
+                              int pitch_y, int pitch_c, int bps, int w, int h, uintptr_t dy, uintptr_t du, uintptr_t dv,
+                              uintptr_t d8, int W, int H, int shift, int bd, uintptr_t stream) {
+    if (mivc_launch_hevc_prep_frame(B, P<void>(sy), P<void>(su), P<void>(sv), ss_y, ss_c, pitch_y, pitch_c, bps, w, h,
+                                    P<uint16_t>(dy), P<uint16_t>(du), P<uint16_t>(dv), P<uint8_t>(d8), W, H, shift, bd,
+                                    S(stream)) != 0)
+      throw std::invalid_argument("hevc_prep_frame: bad geometry");
+  });
+  m.def("hevc_proxy8", [](uintptr_t src, uintptr_t dst, long long n, int shift, uintptr_t stream) {
+    if (mivc_launch_hevc_proxy8(P<uint16_t>(src), P<uint8_t>(dst), n, shift, S(stream)) != 0)
+      throw std::invalid_argument("hevc_proxy8: n must be a multiple of 8");
   });
   m.def("hevc_intra", [](int B, int W, int H, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t ry, uintptr_t ru,
                          uintptr_t rv, uintptr_t ctu, uintptr_t cu, uintptr_t cy, uintptr_t cu_, uintptr_t cv,

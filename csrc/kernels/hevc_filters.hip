@@ -7,7 +7,8 @@
 // modify at most 3 on each side, so edges are independent), then all horizontal
 // edges.  Each is one fully parallel launch: a thread owns one 4-sample edge
 // segment (luma, plus its 2 chroma lines on the 16-sample chroma grid).  SAO reads the
-// deblocked picture (a copy) and writes the final reconstruction; one workgroup per
+// deblocked picture and writes every sample of the final reconstruction into a second
+// buffer (the encoder ping-pongs the two); one workgroup per
 // CTB gathers edge-/band-offset statistics against the source in LDS, picks the
 // cheapest of {off, 4 edge classes, band} per component with an SSE + lambda * bits
 // estimate, stores the parameters for the CABAC writer and applies them.
@@ -21,36 +22,98 @@ using hevc::CtuInfo;
 using hevc::CuInfo;
 
 // ============================================================== source preparation
-// src: slot b, frame plane at base + b * slot_stride (bytes per sample = bps), rows of
-// `pitch` samples, w x h valid; dst: [B] padded W x H uint16 planes (edge replication)
-__global__ void hevc_prep_plane(const uint8_t* src, long long slot_stride, int pitch, int bps, int w, int h,
-                                uint16_t* dst, int W, int H, int shift) {
-  const int x0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4, y = blockIdx.y;
-  const int b = blockIdx.z;
-  if (x0 >= W) return;
-  const int sy = min(y, h - 1);
-  const uint8_t* s = src + b * slot_stride;
-  uint16_t v[4];
-  if (bps == 1) {
-    const uint8_t* row = s + static_cast<size_t>(sy) * pitch;
-    if (x0 + 3 < w && !(reinterpret_cast<uintptr_t>(row + x0) & 3)) {
-      const uint32_t wd = *reinterpret_cast<const uint32_t*>(row + x0);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = static_cast<uint16_t>(((wd >> (8 * k)) & 255u) << shift);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = static_cast<uint16_t>(row[min(x0 + k, w - 1)] << shift);
+// Fused source preparation of a whole frame step: the three planes of every slot in
+// one launch, 8 output samples (one 16-byte store) per work item, grid-stride (a
+// per-row launch issues B x H tiny workgroups and is workgroup-dispatch bound: 1.8 ms
+// per plane at B = 64), plus the 8-bit luma proxy the motion search reads (dst8).
+struct HevcPrepArgs {
+  const uint8_t* src[3];   // frame t of slot 0 per plane; slot b at + b * slot_stride[p]
+  long long slot_stride[3];  // bytes
+  int pitch[3];              // samples per input row
+  int bps;                   // input bytes per sample (1 or 2)
+  int w, h;                  // luma display size
+  uint16_t* dst[3];          // [B] padded planes (W x H, W/2 x H/2)
+  uint8_t* dst8;             // [B] W x H luma proxy = dst >> (bd - 8) (may be null)
+  int W, H, B, shift, bd;
+};
+
+__global__ __launch_bounds__(256) void hevc_prep_frame(HevcPrepArgs a) {
+  const long long ly = static_cast<long long>(a.W / 8) * a.H;       // luma units per slot
+  const long long cu = static_cast<long long>(a.W / 16) * (a.H / 2);  // units per chroma plane
+  const long long per_slot = ly + 2 * cu;
+  const long long total = per_slot * a.B;
+  for (long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int b = static_cast<int>(i / per_slot);
+    long long r = i - static_cast<long long>(b) * per_slot;
+    int p = 0;
+    if (r >= ly) {
+      r -= ly;
+      p = 1 + static_cast<int>(r / cu);
+      r -= (p - 1) * cu;
     }
-  } else {
-    const uint16_t* row = reinterpret_cast<const uint16_t*>(s) + static_cast<size_t>(sy) * pitch;
+    const int PW = p ? a.W / 2 : a.W, PH = p ? a.H / 2 : a.H;
+    const int pw = p ? a.w / 2 : a.w, ph = p ? a.h / 2 : a.h;
+    const int upr = PW / 8;
+    const int y = static_cast<int>(r / upr), x0 = static_cast<int>(r - static_cast<long long>(y) * upr) * 8;
+    const int sy = min(y, ph - 1);
+    const uint8_t* row = a.src[p] + b * a.slot_stride[p] + static_cast<long long>(sy) * a.pitch[p] * a.bps;
+    uint32_t v[8];
+    if (a.bps == 1) {
+      if (x0 + 8 <= pw && !(reinterpret_cast<uintptr_t>(row + x0) & 7)) {
+        const uint2 wd = *reinterpret_cast<const uint2*>(row + x0);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = static_cast<uint16_t>(row[min(x0 + k, w - 1)] << shift);
+        for (int k = 0; k < 8; ++k) v[k] = ((k < 4 ? wd.x : wd.y) >> (8 * (k & 3))) & 255u;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = row[min(x0 + k, pw - 1)];
+      }
+    } else {
+      const uint16_t* r16 = reinterpret_cast<const uint16_t*>(row);
+      if (x0 + 8 <= pw && !(reinterpret_cast<uintptr_t>(r16 + x0) & 15)) {
+        const uint4 wd = *reinterpret_cast<const uint4*>(r16 + x0);
+        const uint32_t q[4] = {wd.x, wd.y, wd.z, wd.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = (q[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = r16[min(x0 + k, pw - 1)];
+      }
+    }
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = (v[2 * k] << a.shift) | ((v[2 * k + 1] << a.shift) << 16);
+    uint16_t* d = a.dst[p] + static_cast<size_t>(b) * PW * PH + static_cast<size_t>(y) * PW + x0;
+    *reinterpret_cast<uint4*>(d) = make_uint4(o[0], o[1], o[2], o[3]);
+    if (p == 0 && a.dst8) {
+      const int s8 = a.bd - 8;
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        lo |= (((v[k] << a.shift) >> s8) & 255u) << (8 * k);
+        hi |= (((v[k + 4] << a.shift) >> s8) & 255u) << (8 * k);
+      }
+      *reinterpret_cast<uint2*>(a.dst8 + static_cast<size_t>(b) * PW * PH + static_cast<size_t>(y) * PW + x0) =
+          make_uint2(lo, hi);
+    }
   }
-  uint16_t* d = dst + static_cast<size_t>(b) * W * H + static_cast<size_t>(y) * W + x0;
-  if (x0 + 3 < W) {
-    *reinterpret_cast<uint2*>(d) = make_uint2(v[0] | (static_cast<uint32_t>(v[1]) << 16), v[2] | (static_cast<uint32_t>(v[3]) << 16));
-  } else {
-    for (int k = 0; k < 4 && x0 + k < W; ++k) d[k] = v[k];
+}
+
+// 8-bit proxy of a u16 plane batch (reference picture for the motion search): 8 samples per item
+__global__ __launch_bounds__(256) void hevc_proxy8(const uint16_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                   long long n8, int shift) {
+  for (long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; i < n8;
+       i += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const uint4 w = reinterpret_cast<const uint4*>(src)[i];
+    const uint32_t q[4] = {w.x, w.y, w.z, w.w};
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t a0 = ((q[k] & 0xFFFFu) >> shift) & 255u, a1 = ((q[k] >> 16) >> shift) & 255u;
+      if (k < 2) lo |= (a0 | (a1 << 8)) << (16 * k);
+      else hi |= (a0 | (a1 << 8)) << (16 * (k - 2));
+    }
+    reinterpret_cast<uint2*>(dst)[i] = make_uint2(lo, hi);
   }
 }
 
@@ -387,11 +450,47 @@ __global__ __launch_bounds__(256) void hevc_sao(HevcSaoArgs a) {
 
 using namespace mivc::gpu;
 
-extern "C" void mivc_launch_hevc_prep(int B, const void* src, long long slot_stride, int pitch, int bps, int w, int h,
-                                      uint16_t* dst, int W, int H, int shift, void* stream) {
-  dim3 grid((W / 4 + 255) / 256 + 1, H, B);
-  hipLaunchKernelGGL(hevc_prep_plane, grid, dim3(256), 0, static_cast<hipStream_t>(stream),
-                     static_cast<const uint8_t*>(src), slot_stride, pitch, bps, w, h, dst, W, H, shift);
+static unsigned grid_for(long long items) {
+  const long long g = (items + 255) / 256;
+  return static_cast<unsigned>(g < 8192 ? (g > 0 ? g : 1) : 8192);  // 32 x 256 CUs, grid-stride beyond
+}
+
+// src*: frame t of slot 0 per plane; strides in bytes, pitches in samples.  W % 16 == 0, H % 2 == 0.
+extern "C" int mivc_launch_hevc_prep_frame(int B, const void* sy, const void* su, const void* sv, long long ss_y,
+                                           long long ss_c, int pitch_y, int pitch_c, int bps, int w, int h,
+                                           uint16_t* dy, uint16_t* du, uint16_t* dv, uint8_t* d8, int W, int H,
+                                           int shift, int bd, void* stream) {
+  if ((W & 15) || (H & 1) || w > W || h > H || (bps != 1 && bps != 2) || bd < 8) return -1;
+  HevcPrepArgs a{};
+  a.src[0] = static_cast<const uint8_t*>(sy);
+  a.src[1] = static_cast<const uint8_t*>(su);
+  a.src[2] = static_cast<const uint8_t*>(sv);
+  a.slot_stride[0] = ss_y;
+  a.slot_stride[1] = a.slot_stride[2] = ss_c;
+  a.pitch[0] = pitch_y;
+  a.pitch[1] = a.pitch[2] = pitch_c;
+  a.bps = bps;
+  a.w = w;
+  a.h = h;
+  a.dst[0] = dy;
+  a.dst[1] = du;
+  a.dst[2] = dv;
+  a.dst8 = d8;
+  a.W = W;
+  a.H = H;
+  a.B = B;
+  a.shift = shift;
+  a.bd = bd;
+  const long long items = static_cast<long long>(B) * (W / 8) * H * 3 / 2;
+  hipLaunchKernelGGL(hevc_prep_frame, dim3(grid_for(items)), dim3(256), 0, static_cast<hipStream_t>(stream), a);
+  return 0;
+}
+
+extern "C" int mivc_launch_hevc_proxy8(const uint16_t* src, uint8_t* dst, long long n, int shift, void* stream) {
+  if (n % 8) return -1;
+  hipLaunchKernelGGL(hevc_proxy8, dim3(grid_for(n / 8)), dim3(256), 0, static_cast<hipStream_t>(stream), src, dst,
+                     n / 8, shift);
+  return 0;
 }
 
 extern "C" void mivc_launch_hevc_deblock(int B, int W, int H, int bd, uint16_t* y, uint16_t* u, uint16_t* v,

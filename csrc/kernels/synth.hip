@@ -12,8 +12,8 @@
 // periodic canvas (its lattice wraps at the canvas size), and the three object
 // textures once into per-slot tiles; a frame is then a bilinear sample of the
 // canvas at the frame's fractional pan offset (uniform weights), the object tiles
-// at integer positions, one sine and one hash per pixel.  Four pixels per thread,
-// one dword store each.
+// at integer positions, one sine per pixel and one hash per 4 pixels (see the
+// frame kernels below for the launch shape).
 #include <algorithm>
 
 #include "kcommon.h"
@@ -123,105 +123,177 @@ struct FrameArgs {
   uint8_t *y, *u, *v;  // [slots*frames, h, w] display-size frames
 };
 
-__global__ void synth_frame_luma(FrameArgs a) {
-  const SynthGeom& g = a.g;
-  const int x4 = (blockIdx.x * blockDim.x + threadIdx.x) * 4, y = blockIdx.y, fz = blockIdx.z;
-  if (x4 >= g.width) return;
-  const int slot = fz / g.frames, f = fz % g.frames + g.frame0;
-  const uint32_t ss = slot_seed(g, slot);
-  // per-slot global motion (pan) in pixels/frame, sub-pixel
-  const float vx = ((hash3(ss, 1, 0) & 255) / 255.f - 0.5f) * 6.f;
-  const float vy = ((hash3(ss, 2, 0) & 255) / 255.f - 0.5f) * 3.f;
-  const float fx = vx * f, fy = vy * f;
-  const float ix = floorf(fx), iy = floorf(fy);
-  const float tx = fx - ix, ty = fy - iy;
-  int cy0 = (y + static_cast<int>(iy)) % g.ch;
-  cy0 = cy0 < 0 ? cy0 + g.ch : cy0;
-  const int cy1 = cy0 + 1 == g.ch ? 0 : cy0 + 1;
-  const uint8_t* r0 = a.cy + (static_cast<size_t>(slot) * g.ch + cy0) * g.cw;
-  const uint8_t* r1 = a.cy + (static_cast<size_t>(slot) * g.ch + cy1) * g.cw;
+// A frame step is B*F frames of W x H: the per-row launch of the first version issued
+// ~50M 256-thread workgroups per 1080p batch and was bound by workgroup dispatch
+// (131 ms for 15360 frames, ~250 GB/s).  Here a fixed grid strides over 16-pixel
+// runs: one unit = 16 consecutive pixels of one row, one 16-byte store; the canvas
+// bytes of a run come from 5 aligned dword loads + v_alignbyte, and one hash feeds the
+// sensor noise of 4 pixels.
+__device__ __forceinline__ int noise5(uint32_t h, int k) { return static_cast<int>(((h >> (8 * k)) & 255u) % 5u) - 2; }
+
+struct FrameConst {
+  int slot, f;
+  uint32_t ss;
   int obx[3], oby[3];
+};
+
+__device__ __forceinline__ FrameConst frame_const(const SynthGeom& g, int fz) {
+  FrameConst c;
+  c.slot = fz / g.frames;
+  c.f = fz % g.frames + g.frame0;
+  c.ss = slot_seed(g, c.slot);
 #pragma unroll
-  for (int o = 0; o < 3; ++o) object_pos(g, slot, o, f, g.width, g.height, g.ow[o], g.oh[o], 1.f, &obx[o], &oby[o]);
-  uint32_t w = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int x = x4 + k;
-    int cx0 = (x + static_cast<int>(ix)) % g.cw;
+  for (int o = 0; o < 3; ++o) object_pos(g, c.slot, o, c.f, g.width, g.height, g.ow[o], g.oh[o], 1.f, &c.obx[o], &c.oby[o]);
+  return c;
+}
+
+__global__ __launch_bounds__(256) void synth_frame_luma(FrameArgs a) {
+  const SynthGeom& g = a.g;
+  const int runs = (g.width + 15) >> 4;
+  const long long total = static_cast<long long>(g.slots) * g.frames * g.height * runs;
+  for (long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int fz = static_cast<int>(i / (static_cast<long long>(g.height) * runs));
+    const int rem = static_cast<int>(i - static_cast<long long>(fz) * g.height * runs);
+    const int y = rem / runs, x16 = (rem - y * runs) * 16;
+    const FrameConst fc = frame_const(g, fz);
+    // per-slot global motion (pan) in pixels/frame, sub-pixel
+    const float vx = ((hash3(fc.ss, 1, 0) & 255) / 255.f - 0.5f) * 6.f;
+    const float vy = ((hash3(fc.ss, 2, 0) & 255) / 255.f - 0.5f) * 3.f;
+    const float fx = vx * fc.f, fy = vy * fc.f;
+    const float ixf = floorf(fx), iyf = floorf(fy);
+    const float tx = fx - ixf, ty = fy - iyf;
+    int cy0 = (y + static_cast<int>(iyf)) % g.ch;
+    cy0 = cy0 < 0 ? cy0 + g.ch : cy0;
+    const int cy1 = cy0 + 1 == g.ch ? 0 : cy0 + 1;
+    const uint8_t* r0 = a.cy + (static_cast<size_t>(fc.slot) * g.ch + cy0) * g.cw;
+    const uint8_t* r1 = a.cy + (static_cast<size_t>(fc.slot) * g.ch + cy1) * g.cw;
+    int cx0 = (x16 + static_cast<int>(ixf)) % g.cw;
     cx0 = cx0 < 0 ? cx0 + g.cw : cx0;
-    const int cx1 = cx0 + 1 == g.cw ? 0 : cx0 + 1;
-    float top = r0[cx0] * (1.f - tx) + r0[cx1] * tx, bot = r1[cx0] * (1.f - tx) + r1[cx1] * tx;
-    float lum = top * (1.f - ty) + bot * ty + 20.f * __sinf(0.01f * (x + y) + 0.03f * f);
+    uint8_t t0[20], t1[20];
+    if (cx0 + 17 <= g.cw) {  // the run's 17 canvas bytes are contiguous (cw is a multiple of 4)
+      const int ca = cx0 & ~3, sh = cx0 & 3;
+      uint32_t w0[6], w1[6];
 #pragma unroll
-    for (int o = 0; o < 3; ++o) {
-      int lx = x - obx[o], ly = y - oby[o];
-      lx = lx < 0 ? lx + g.width : lx;  // wrap-around
-      ly = ly < 0 ? ly + g.height : ly;
-      if (lx < g.ow[o] && ly < g.oh[o])
-        lum = a.tiles[(static_cast<size_t>(slot) * 3 + o) * a.tile_stride + static_cast<size_t>(ly) * g.ow[o] + lx];
+      for (int k = 0; k < 6; ++k) {
+        const int o = min(ca + 4 * k, g.cw - 4);
+        w0[k] = *reinterpret_cast<const uint32_t*>(r0 + o);
+        w1[k] = *reinterpret_cast<const uint32_t*>(r1 + o);
+      }
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const uint32_t u0 = __builtin_amdgcn_alignbyte(w0[k + 1], w0[k], sh);
+        const uint32_t u1 = __builtin_amdgcn_alignbyte(w1[k + 1], w1[k], sh);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          t0[4 * k + b] = static_cast<uint8_t>(u0 >> (8 * b));
+          t1[4 * k + b] = static_cast<uint8_t>(u1 >> (8 * b));
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 17; ++k) {
+        const int cx = cx0 + k >= g.cw ? cx0 + k - g.cw : cx0 + k;
+        t0[k] = r0[cx];
+        t1[k] = r1[cx];
+      }
     }
-    const int n = static_cast<int>(hash3(static_cast<uint32_t>(x), static_cast<uint32_t>(y), ss ^ (f * 2654435761u)) % 5u) - 2;
-    int v = static_cast<int>(lum + 0.5f) + n;
-    v = v < 0 ? 0 : (v > 255 ? 255 : v);
-    w |= static_cast<uint32_t>(v) << (8 * k);
-  }
-  uint8_t* dst = a.y + (static_cast<size_t>(fz) * g.height + y) * g.width + x4;
-  if (x4 + 4 <= g.width && (reinterpret_cast<uintptr_t>(dst) & 3) == 0) {
-    *reinterpret_cast<uint32_t*>(dst) = w;
-  } else {
-    for (int k = 0; k < 4 && x4 + k < g.width; ++k) dst[k] = static_cast<uint8_t>(w >> (8 * k));
+    const float w00 = (1.f - tx) * (1.f - ty), w10 = tx * (1.f - ty), w01 = (1.f - tx) * ty, w11 = tx * ty;
+    uint32_t h4[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      h4[q] = hash3(static_cast<uint32_t>(x16 + 4 * q), static_cast<uint32_t>(y), fc.ss ^ (fc.f * 2654435761u));
+    uint32_t out[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int k = 4 * q + b, x = x16 + k;
+        float lum = t0[k] * w00 + t0[k + 1] * w10 + t1[k] * w01 + t1[k + 1] * w11 +
+                    20.f * __sinf(0.01f * (x + y) + 0.03f * fc.f);
+#pragma unroll
+        for (int o = 0; o < 3; ++o) {
+          int lx = x - fc.obx[o], ly = y - fc.oby[o];
+          lx = lx < 0 ? lx + g.width : lx;  // wrap-around
+          ly = ly < 0 ? ly + g.height : ly;
+          if (lx < g.ow[o] && ly < g.oh[o])
+            lum = a.tiles[(static_cast<size_t>(fc.slot) * 3 + o) * a.tile_stride + static_cast<size_t>(ly) * g.ow[o] + lx];
+        }
+        int v = static_cast<int>(lum + 0.5f) + noise5(h4[q], b);
+        v = v < 0 ? 0 : (v > 255 ? 255 : v);
+        w |= static_cast<uint32_t>(v) << (8 * b);
+      }
+      out[q] = w;
+    }
+    uint8_t* dst = a.y + (static_cast<size_t>(fz) * g.height + y) * g.width + x16;
+    if (x16 + 16 <= g.width && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+      *reinterpret_cast<uint4*>(dst) = make_uint4(out[0], out[1], out[2], out[3]);
+    } else {
+      for (int k = 0; k < 16 && x16 + k < g.width; ++k) dst[k] = static_cast<uint8_t>(out[k >> 2] >> (8 * (k & 3)));
+    }
   }
 }
 
-__global__ void synth_frame_chroma(FrameArgs a) {
+__global__ __launch_bounds__(256) void synth_frame_chroma(FrameArgs a) {
   const SynthGeom& g = a.g;
   const int w2 = g.width / 2, h2 = g.height / 2, ccw = g.cw / 2, cch = g.ch / 2;
-  const int x4 = (blockIdx.x * blockDim.x + threadIdx.x) * 4, y = blockIdx.y, fz = blockIdx.z;
-  if (x4 >= w2) return;
-  const int slot = fz / g.frames, f = fz % g.frames + g.frame0;
-  const uint32_t ss = slot_seed(g, slot);
-  const float vx = ((hash3(ss, 1, 0) & 255) / 255.f - 0.5f) * 3.f;
-  const float vy = ((hash3(ss, 2, 0) & 255) / 255.f - 0.5f) * 1.5f;
-  const int ix = static_cast<int>(floorf(vx * f)), iy = static_cast<int>(floorf(vy * f));
-  int cyy = (y + iy) % cch;
-  cyy = cyy < 0 ? cyy + cch : cyy;
-  const size_t rowo = (static_cast<size_t>(slot) * cch + cyy) * ccw;
-  int obx[3], oby[3];
-#pragma unroll
-  for (int o = 0; o < 3; ++o) {
-    object_pos(g, slot, o, f, g.width, g.height, g.ow[o], g.oh[o], 1.f, &obx[o], &oby[o]);
-    obx[o] >>= 1;
-    oby[o] >>= 1;
-  }
-  uint32_t wu = 0, wv = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int x = x4 + k;
-    int cxx = (x + ix) % ccw;
-    cxx = cxx < 0 ? cxx + ccw : cxx;
-    int cu = a.cu[rowo + cxx] + static_cast<int>(10.f * __sinf(0.02f * x));
-    int cv = a.cv[rowo + cxx] + static_cast<int>(10.f * __cosf(0.02f * y));
+  const int runs = (w2 + 15) >> 4;
+  const long long total = static_cast<long long>(g.slots) * g.frames * h2 * runs;
+  for (long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int fz = static_cast<int>(i / (static_cast<long long>(h2) * runs));
+    const int rem = static_cast<int>(i - static_cast<long long>(fz) * h2 * runs);
+    const int y = rem / runs, x16 = (rem - y * runs) * 16;
+    FrameConst fc = frame_const(g, fz);
+    const float vx = ((hash3(fc.ss, 1, 0) & 255) / 255.f - 0.5f) * 3.f;
+    const float vy = ((hash3(fc.ss, 2, 0) & 255) / 255.f - 0.5f) * 1.5f;
+    const int ix = static_cast<int>(floorf(vx * fc.f)), iy = static_cast<int>(floorf(vy * fc.f));
+    int cyy = (y + iy) % cch;
+    cyy = cyy < 0 ? cyy + cch : cyy;
+    const size_t rowo = (static_cast<size_t>(fc.slot) * cch + cyy) * ccw;
 #pragma unroll
     for (int o = 0; o < 3; ++o) {
-      int lx = x - obx[o], ly = y - oby[o];
-      lx = lx < 0 ? lx + w2 : lx;
-      ly = ly < 0 ? ly + h2 : ly;
-      if (lx < g.ow[o] / 2 && ly < g.oh[o] / 2) {
-        cu = 90 + 50 * o;
-        cv = 170 - 40 * o;
-      }
+      fc.obx[o] >>= 1;
+      fc.oby[o] >>= 1;
     }
-    wu |= static_cast<uint32_t>(clampi(cu, 0, 255)) << (8 * k);
-    wv |= static_cast<uint32_t>(clampi(cv, 0, 255)) << (8 * k);
-  }
-  const size_t idx = (static_cast<size_t>(fz) * h2 + y) * w2 + x4;
-  if (x4 + 4 <= w2 && ((reinterpret_cast<uintptr_t>(a.u + idx) | reinterpret_cast<uintptr_t>(a.v + idx)) & 3) == 0) {
-    *reinterpret_cast<uint32_t*>(a.u + idx) = wu;
-    *reinterpret_cast<uint32_t*>(a.v + idx) = wv;
-  } else {
-    for (int k = 0; k < 4 && x4 + k < w2; ++k) {
-      a.u[idx + k] = static_cast<uint8_t>(wu >> (8 * k));
-      a.v[idx + k] = static_cast<uint8_t>(wv >> (8 * k));
+    const float cv_row = 10.f * __cosf(0.02f * y);
+    uint32_t ou[4], ov[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t wu = 0, wv = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int x = x16 + 4 * q + b;
+        int cxx = (x + ix) % ccw;
+        cxx = cxx < 0 ? cxx + ccw : cxx;
+        int cu = a.cu[rowo + cxx] + static_cast<int>(10.f * __sinf(0.02f * x));
+        int cv = a.cv[rowo + cxx] + static_cast<int>(cv_row);
+#pragma unroll
+        for (int o = 0; o < 3; ++o) {
+          int lx = x - fc.obx[o], ly = y - fc.oby[o];
+          lx = lx < 0 ? lx + w2 : lx;
+          ly = ly < 0 ? ly + h2 : ly;
+          if (lx < g.ow[o] / 2 && ly < g.oh[o] / 2) {
+            cu = 90 + 50 * o;
+            cv = 170 - 40 * o;
+          }
+        }
+        wu |= static_cast<uint32_t>(clampi(cu, 0, 255)) << (8 * b);
+        wv |= static_cast<uint32_t>(clampi(cv, 0, 255)) << (8 * b);
+      }
+      ou[q] = wu;
+      ov[q] = wv;
+    }
+    const size_t idx = (static_cast<size_t>(fz) * h2 + y) * w2 + x16;
+    if (x16 + 16 <= w2 && ((reinterpret_cast<uintptr_t>(a.u + idx) | reinterpret_cast<uintptr_t>(a.v + idx)) & 15) == 0) {
+      *reinterpret_cast<uint4*>(a.u + idx) = make_uint4(ou[0], ou[1], ou[2], ou[3]);
+      *reinterpret_cast<uint4*>(a.v + idx) = make_uint4(ov[0], ov[1], ov[2], ov[3]);
+    } else {
+      for (int k = 0; k < 16 && x16 + k < w2; ++k) {
+        a.u[idx + k] = static_cast<uint8_t>(ou[k >> 2] >> (8 * (k & 3)));
+        a.v[idx + k] = static_cast<uint8_t>(ov[k >> 2] >> (8 * (k & 3)));
+      }
     }
   }
 }
@@ -262,8 +334,13 @@ extern "C" void mivc_launch_synth(uint8_t* y, uint8_t* u, uint8_t* v, int width,
   int omw = std::max(g.ow[0], std::max(g.ow[1], g.ow[2])), omh = std::max(g.oh[0], std::max(g.oh[1], g.oh[2]));
   hipLaunchKernelGGL(synth_objects, dim3((omw + 255) / 256, omh, slots * 3), dim3(256), 0, s, g, tiles, tile_stride);
   FrameArgs fa{g, cy, cu, cv, tiles, tile_stride, y, u, v};
-  hipLaunchKernelGGL(synth_frame_luma, dim3((width / 4 + 255) / 256 + 1, height, slots * frames), dim3(256), 0, s, fa);
-  hipLaunchKernelGGL(synth_frame_chroma, dim3((width / 8 + 255) / 256 + 1, height / 2, slots * frames), dim3(256), 0, s,
-                     fa);
+  // grid-stride over 16-pixel runs: 32 workgroups per CU (256 CUs) at most
+  auto grid = [](long long units) {
+    const long long g = (units + 255) / 256;
+    return dim3(static_cast<unsigned>(g < 8192 ? (g > 0 ? g : 1) : 8192));
+  };
+  const long long fr = static_cast<long long>(slots) * frames;
+  hipLaunchKernelGGL(synth_frame_luma, grid(fr * height * ((width + 15) / 16)), dim3(256), 0, s, fa);
+  hipLaunchKernelGGL(synth_frame_chroma, grid(fr * (height / 2) * ((width / 2 + 15) / 16)), dim3(256), 0, s, fa);
   hipFreeAsync(ws, s);
 }

@@ -99,7 +99,7 @@ class GpuHevcEncoder:
 
         self.src = planes()
         self.rec = [planes(), planes()]      # current / reference
-        self.dbk = planes()                  # deblocked copy (SAO input)
+        self.dbk = planes()                  # SAO output ping-pong buffer
         self.coefs = [planes(i16), planes(i16)]  # double-buffered: copy-out of t overlaps t + 1
         self.coef = self.coefs[0]
         self.wmb, self.hmb = W // 16, H // 16
@@ -146,17 +146,20 @@ class GpuHevcEncoder:
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.dev).cuda_stream
 
-    def _prep(self, y, u, v, t: int):
+    def _prep(self, y, u, v, t: int, proxy: bool = False):
+        """Frame t of every slot -> padded uint16 planes (+ the 8-bit luma proxy of the
+        motion search): one fused launch for the three planes."""
         B, F, h, w = y.shape
         bps = y.element_size()
         in_bd = 8 if bps == 1 else self.p.bit_depth
         shift = self.p.bit_depth - in_bd
-        s = self._stream()
-        for src, dst, (ww, hh) in ((y, self.src[0], (w, h)), (u, self.src[1], (w // 2, h // 2)),
-                                   (v, self.src[2], (w // 2, h // 2))):
-            plane = src[:, t]
-            self.hip.hevc_prep(B, plane.data_ptr(), src.stride(0) * bps, src.stride(2), bps, ww, hh, dst.data_ptr(),
-                               dst.shape[2], dst.shape[1], shift, s)
+        ys, us, vs = y[:, t], u[:, t], v[:, t]
+        if ys.stride(2) != 1 or us.stride(2) != 1 or vs.stride(2) != 1 or us.stride(0) != vs.stride(0):
+            raise ValueError("input planes need unit sample stride and equal chroma slot strides")
+        self.hip.hevc_prep_frame(B, ys.data_ptr(), us.data_ptr(), vs.data_ptr(), ys.stride(0) * bps, us.stride(0) * bps,
+                                 ys.stride(1), us.stride(1), bps, w, h, self.src[0].data_ptr(), self.src[1].data_ptr(),
+                                 self.src[2].data_ptr(), self.src8.data_ptr() if proxy else 0, self.W, self.H, shift,
+                                 self.p.bit_depth, self._stream())
 
     # ------------------------------------------------------------------ rate control
     def crf_qps(self, y: torch.Tensor) -> np.ndarray:
@@ -193,20 +196,23 @@ class GpuHevcEncoder:
         if qps is None:
             qps = np.array([[qi if t == 0 else qpp for t in range(F)] for _ in range(B)], dtype=np.int32)
         cfg = self.p.host_cfg()
+        qps = np.clip(np.asarray(qps, dtype=np.int32).reshape(B, F), 0, 51)
+        qps_d = torch.from_numpy(np.ascontiguousarray(qps.T)).to(self.dev)  # [F, B], one upload
         nals: list[list] = [[None] * F for _ in range(B)]
         futs = []
         pending: list[list] = [[], [], []]
         sse = []
         recon = [] if keep_recon else None
-        t_gpu = t_host = 0.0
+        t_gpu = t_host = t_blocked = 0.0
+        cabac_s = [0.0]
         p = self._p
         s = self._stream()
         bd = self.p.bit_depth
         for t in range(F):
             t0 = time.perf_counter()
             idr = t == 0 or self.p.intra_only or (self.p.keyint > 0 and t % self.p.keyint == 0)
-            self._prep(y, u, v, t)
-            self.qp.copy_(torch.from_numpy(np.ascontiguousarray(qps[:, t])).to(self.dev))
+            self._prep(y, u, v, t, proxy=not idr)
+            self.qp.copy_(qps_d[t])  # device-to-device: no host sync inside the frame loop
             cur, ref = self.rec[t % 2], self.rec[(t + 1) % 2]
             kb = t % 2
             # the copy-out of step t - 2 must have read these buffers before they are rewritten
@@ -221,9 +227,7 @@ class GpuHevcEncoder:
             else:
                 self.run.fill_(2)
                 self.hip.hevc_intra(*intra_args, 1, 0, p(self.err), s)   # open-loop intra candidates
-                sh = bd - 8
-                self.src8.copy_((self.src[0] >> sh).to(torch.uint8))
-                self.ref8.copy_((ref[0] >> sh).to(torch.uint8))
+                self.hip.hevc_proxy8(p(ref[0]), p(self.ref8), ref[0].numel(), bd - 8, s)
                 self.hip.me(B, self.wmb, self.hmb, p(self.src8), p(self.ref8), p(self.prev_mv), p(self.mv),
                             p(self.me_cost), p(self.me_pred), p(self.me_intra), p(self.qp), self.p.me_range,
                             self.p.subpel, s)
@@ -237,11 +241,14 @@ class GpuHevcEncoder:
                 self.hip.hevc_deblock(B, self.W, self.H, bd, p(cur[0]), p(cur[1]), p(cur[2]), p(self.cu), p(self.qp),
                                       p(self.run), s)
             if self.p.sao:
-                for k in range(3):
-                    self.dbk[k].copy_(cur[k])
-                self.hip.hevc_sao(B, self.W, self.H, bd, p(self.dbk[0]), p(self.dbk[1]), p(self.dbk[2]), p(cur[0]),
-                                  p(cur[1]), p(cur[2]), p(self.src[0]), p(self.src[1]), p(self.src[2]), p(self.ctu),
-                                  p(self.qp), p(self.run), 1, s)
+                # SAO reads the deblocked picture and writes every sample of the output:
+                # ping-pong with the spare buffer instead of copying the input
+                out_pl = self.dbk
+                self.hip.hevc_sao(B, self.W, self.H, bd, p(cur[0]), p(cur[1]), p(cur[2]), p(out_pl[0]),
+                                  p(out_pl[1]), p(out_pl[2]), p(self.src[0]), p(self.src[1]), p(self.src[2]),
+                                  p(self.ctu), p(self.qp), p(self.run), 1, s)
+                self.dbk = cur
+                self.rec[t % 2] = cur = out_pl
             if metrics:
                 d = (cur[0][:, :h, :w].to(torch.int32) - self.src[0][:, :h, :w].to(torch.int32))
                 sse.append((d * d).sum(dim=(1, 2)).to(torch.float64))
@@ -250,9 +257,11 @@ class GpuHevcEncoder:
             # records to pinned host memory on the copy stream; CABAC on the thread pool
             hb = t % 3
             if pending[hb]:  # the CABAC jobs of step t - 3 still read this host buffer set
+                tb = time.perf_counter()
                 for f in pending[hb]:
                     f.result()
                 pending[hb] = []
+                t_blocked += time.perf_counter() - tb
             host = self._host_buffers()[hb]
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.dev))
@@ -271,7 +280,10 @@ class GpuHevcEncoder:
                 if b == 0 or not done.query():
                     done.synchronize()
                 fp = dict(idr=int(idr), poc=t, qp=int(qps[b, t]), slice_type=2 if idr else 1)
-                return self.host.hevc_write_slice(cfg, fp, ctu[b], cu[b], cy[b], cb[b], cr[b])
+                tj = time.perf_counter()
+                r = self.host.hevc_write_slice(cfg, fp, ctu[b], cu[b], cy[b], cb[b], cr[b])
+                cabac_s[0] += time.perf_counter() - tj
+                return r
 
             for b in range(B):
                 f = self.pool.submit(job, b)
@@ -286,7 +298,8 @@ class GpuHevcEncoder:
             nals[b][t] = nal
             bits[b][t] = 8 * len(nal)
         t_host = time.perf_counter() - t2
-        self.timings = dict(gpu_s=t_gpu, host_wait_s=t_host)
+        self.timings = dict(loop_s=t_gpu, loop_blocked_on_cabac_s=t_blocked, host_wait_s=t_host,
+                            cabac_thread_s=cabac_s[0], cabac_ms_per_picture=1000.0 * cabac_s[0] / max(1, B * F))
         out = []
         maxv = float((1 << bd) - 1)
         for b in range(B):
