@@ -21,6 +21,9 @@
 // contiguous run of MBs (window rows are shared through that XCD's L2).
 #include "kcommon.h"
 
+#include <cstdio>
+#include <cstdlib>
+
 namespace mivc {
 namespace gpu {
 
@@ -36,7 +39,10 @@ struct MeArgs {
   const int* qp;           // [B] frame QP per slot
   int range;               // integer radius, <= 16
   int subpel;              // 0 none, 1 half, 2 quarter
+  const uint8_t* hp;       // [B, 3, H + 8, W + 8] b / h / j half-sample planes of ref_y (margin 4)
 };
+
+constexpr int kHpM = 4;  // half-sample plane margin (samples); coordinates clamp into it exactly
 
 constexpr int kMaxR = 16;
 constexpr int kML = 4;                                   // window margin left/top (6-tap + qpel)
@@ -74,15 +80,17 @@ struct MeShared {
   uint32_t win[kWinRowsMax * kWinPitch];  // reference window, aligned words
   alignas(16) uint32_t src[64];            // source MB (16 rows x 4 words)
   int nb[36];                              // source intra neighbours: top[16], left[16], tl
-  int16_t B1[25 * 20];                     // horizontal 6-tap intermediates
   uint32_t P32[404];                       // G, b, h, j planes (20x20 bytes each) + pad
   short qoff[32];                          // kQOff copy (lane-varying index -> LDS, not constant)
 };
 
 // Stage rows [wy, wy+rows) x bytes [xa, xa + 4*words) of the reference, clamped to the frame.
-// All loads are issued before the first LDS store.
+// All loads are issued before the first LDS store.  WORDS > 0: compile-time row width
+// (the lane -> (row, word) split is then a multiply, not a 30-instruction division).
+template <int WORDS>
 __device__ __forceinline__ void stage_window(MeShared& S, const uint8_t* ref, int W, int H, int xa, int wy,
-                                             int rows, int words, int lane) {
+                                             int rows, int words_rt, int lane) {
+  const int words = WORDS > 0 ? WORDS : words_rt;
   const int n = rows * words;
   uint32_t v[kLoadsPerLane];
   const bool inside = xa >= 0 && xa + 4 * words <= W;
@@ -114,6 +122,14 @@ __device__ __forceinline__ void stage_window(MeShared& S, const uint8_t* ref, in
     int r = i / words, w = i - r * words;
     if (i < n) S.win[r * kWinPitch + w] = v[k];
   }
+}
+
+// 4 bytes of a frame row at byte column x (any alignment, x .. x+3 inside the row)
+__device__ __forceinline__ uint32_t load4u(const uint8_t* row, int x) {
+  const int a = x & ~3, sh = x & 3;
+  const uint32_t w0 = *reinterpret_cast<const uint32_t*>(row + a);
+  if (sh == 0) return w0;
+  return __builtin_amdgcn_alignbyte(*reinterpret_cast<const uint32_t*>(row + a + 4), w0, sh);
 }
 
 // Integer search for a compile-time radius: lane = (dx, dy-group of DYN rows).  The lane
@@ -181,6 +197,75 @@ __device__ __forceinline__ int int_search_fixed(const MeShared& S, int sh0, int 
   return best;
 }
 
+// four values in [0, 255] -> one little-endian word, via v_perm_b32 only
+__device__ __forceinline__ uint32_t pack4_u8(const int* v) {
+  const uint32_t lo = __builtin_amdgcn_perm(static_cast<uint32_t>(v[1]), static_cast<uint32_t>(v[0]), 0x0c0c0400u);
+  const uint32_t hi = __builtin_amdgcn_perm(static_cast<uint32_t>(v[3]), static_cast<uint32_t>(v[2]), 0x0c0c0400u);
+  return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+}
+
+// Frame-level half-sample planes of a reference batch (clause 8.4.2.2.1): for every
+// integer position (x, y) of a (W + 8) x (H + 8) grid (margin kHpM, coordinates of the
+// reference clamped to the picture = the normative edge extension):
+//   b = half between x and x+1, h = half between y and y+1, j = centre.
+// Values outside the margin equal the margin's (all 6 taps replicate), so a consumer
+// clamps coordinates into [-4, W+3] x [-4, H+3] exactly.  One item = 4 columns of a row.
+__global__ __launch_bounds__(256) void me_halfpel_planes(const uint8_t* __restrict__ ref, int B, int W, int H,
+                                                         uint8_t* __restrict__ hp) {
+  const int PW = W + 2 * kHpM, PH = H + 2 * kHpM;
+  const int qpr = PW / 4;
+  const long long total = static_cast<long long>(B) * PH * qpr;
+  for (long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int b = static_cast<int>(i / (static_cast<long long>(PH) * qpr));
+    const int rem = static_cast<int>(i - static_cast<long long>(b) * PH * qpr);
+    const int py = rem / qpr, px = (rem - py * qpr) * 4;
+    const int y = py - kHpM, x0 = px - kHpM;
+    const uint8_t* fr = ref + static_cast<size_t>(b) * W * H;
+    int p[6][9];  // rows y-2 .. y+3, columns x0-2 .. x0+6
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      const uint8_t* row = fr + static_cast<size_t>(clampi(y - 2 + r, 0, H - 1)) * W;
+      if (x0 - 4 >= 0 && x0 + 8 <= W) {
+        const uint32_t w0 = *reinterpret_cast<const uint32_t*>(row + x0 - 4);
+        const uint32_t w1 = *reinterpret_cast<const uint32_t*>(row + x0);
+        const uint32_t w2 = *reinterpret_cast<const uint32_t*>(row + x0 + 4);
+        p[r][0] = (w0 >> 16) & 255;
+        p[r][1] = w0 >> 24;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) p[r][2 + k] = (w1 >> (8 * k)) & 255;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) p[r][6 + k] = (w2 >> (8 * k)) & 255;
+      } else {
+#pragma unroll
+        for (int c = 0; c < 9; ++c) p[r][c] = row[clampi(x0 - 2 + c, 0, W - 1)];
+      }
+    }
+    int b1[6][4];
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        b1[r][k] = h264::tap6(p[r][k], p[r][k + 1], p[r][k + 2], p[r][k + 3], p[r][k + 4], p[r][k + 5]);
+    int bv[4], hv[4], jv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      bv[k] = h264::clip1((b1[2][k] + 16) >> 5);
+      hv[k] = h264::clip1((h264::tap6(p[0][k + 2], p[1][k + 2], p[2][k + 2], p[3][k + 2], p[4][k + 2],
+                                      p[5][k + 2]) + 16) >> 5);
+      jv[k] = h264::clip1((h264::tap6(b1[0][k], b1[1][k], b1[2][k], b1[3][k], b1[4][k], b1[5][k]) + 512) >> 10);
+    }
+    // byte packing through v_perm: a shift/or packing of clip((x + r) >> n) values gets
+    // selected to gfx950's v_ashr_pk_u8_i32, whose high half the backend assumes is zero
+    // (it is not): bytes 2-3 came out 255 on some inputs (test_me_halfpel_planes_match_numpy)
+    const uint32_t wb = pack4_u8(bv), wh = pack4_u8(hv), wj = pack4_u8(jv);
+    uint8_t* o = hp + static_cast<size_t>(b) * 3 * PW * PH + static_cast<size_t>(py) * PW + px;
+    *reinterpret_cast<uint32_t*>(o) = wb;
+    *reinterpret_cast<uint32_t*>(o + static_cast<size_t>(PW) * PH) = wh;
+    *reinterpret_cast<uint32_t*>(o + 2 * static_cast<size_t>(PW) * PH) = wj;
+  }
+}
+
 #ifdef MIVC_ME_PROFILE
 __device__ unsigned long long g_me_prof[64][12];
 #define MPROF(ph) do { if (lin < 64 && lane == 0) g_me_prof[lin][ph] = clock64(); } while (0)
@@ -235,9 +320,14 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
     cand_x[k] = clampi(cand_x[k], -128, 128);
     cand_y[k] = clampi(cand_y[k], -128, 128);
     const uint8_t* rp = ref + static_cast<size_t>(clampi(Y0 + r4 + cand_y[k], 0, H - 1)) * W;
+    const int xs = X0 + c4 + cand_x[k];
     uint32_t w = 0;
+    if (xs >= 0 && xs + 4 <= W) {
+      w = load4u(rp, xs);
+    } else {
 #pragma unroll
-    for (int b = 0; b < 4; ++b) w |= static_cast<uint32_t>(rp[clampi(X0 + c4 + b + cand_x[k], 0, W - 1)]) << (8 * b);
+      for (int b = 0; b < 4; ++b) w |= static_cast<uint32_t>(rp[clampi(xs + b, 0, W - 1)]) << (8 * b);
+    }
     cref[k] = w;
   }
   S.src[lane] = my_src;
@@ -264,7 +354,8 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   int wx = X0 + cx - R - kML;
   int xa = wx & ~3, sh0 = wx - xa;
   const int wwords = (wrows + 3) / 4 + 1;
-  stage_window(S, ref, W, H, xa, Y0 + cy - R - kML, wrows, wwords, lane);
+  if (R == 8) stage_window<(16 + 16 + kML + kMR + 3) / 4 + 1>(S, ref, W, H, xa, Y0 + cy - R - kML, wrows, wwords, lane);
+  else stage_window<0>(S, ref, W, H, xa, Y0 + cy - R - kML, wrows, wwords, lane);
   __syncthreads();
 
   MPROF(2);
@@ -319,7 +410,7 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
     wx = X0 - R - kML;
     xa = wx & ~3;
     sh0 = wx - xa;
-    stage_window(S, ref, W, H, xa, Y0 - R - kML, wrows, wwords, lane);
+    stage_window<0>(S, ref, W, H, xa, Y0 - R - kML, wrows, wwords, lane);
     __syncthreads();
   } else {
     by = bp / side;
@@ -329,27 +420,48 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   int best_mvx = bx * 4, best_mvy = by * 4;
 
   MPROF(3);
-  // ---- phase 3: sub-pel planes from the window.  s_G(r, c) = pixel (bx-4+c, by-4+r)
+  // ---- phase 3: sub-pel planes around (bx, by).  G comes from the LDS window; b, h, j
+  // (clause 8.4.2.2.1 half-sample planes) are staged from the frame-level planes built
+  // once per reference picture by me_halfpel_planes (the per-MB 6-tap filtering they
+  // replace was ~20% of this kernel's instructions).  P(u, v) = plane at (X0+bx-2+u, Y0+by-2+v).
   const uint8_t* winb = reinterpret_cast<const uint8_t*>(S.win);
   const int gx0 = sh0 + bx - cx + R, gy0 = by - cy + R;  // window byte column / row of pixel (bx-4, by-4)
-  auto Gs = [&](int r, int c) -> int { return winb[(gy0 + r) * (kWinPitch * 4) + gx0 + c]; };
-  for (int i = lane; i < 25 * 20; i += 64) {
-    int r = i / 20, u = i - r * 20;
-    S.B1[i] = static_cast<int16_t>(h264::tap6(Gs(r, u), Gs(r, u + 1), Gs(r, u + 2), Gs(r, u + 3), Gs(r, u + 4),
-                                               Gs(r, u + 5)));
-  }
-  __syncthreads();
   uint8_t* Pb = reinterpret_cast<uint8_t*>(S.P32);
-  for (int i = lane; i < 400; i += 64) {
-    int v = i / 20, u = i - v * 20;
-    Pb[i] = static_cast<uint8_t>(Gs(v + 2, u + 2));
-    Pb[400 + i] = static_cast<uint8_t>(h264::clip1((S.B1[(v + 2) * 20 + u] + 16) >> 5));
-    Pb[800 + i] = static_cast<uint8_t>(h264::clip1(
-        (h264::tap6(Gs(v, u + 2), Gs(v + 1, u + 2), Gs(v + 2, u + 2), Gs(v + 3, u + 2), Gs(v + 4, u + 2),
-                    Gs(v + 5, u + 2)) + 16) >> 5));
-    const int16_t* bc = S.B1 + v * 20 + u;
-    int j1 = h264::tap6(bc[0], bc[20], bc[40], bc[60], bc[80], bc[100]);
-    Pb[1200 + i] = static_cast<uint8_t>(h264::clip1((j1 + 512) >> 10));
+  {
+    const int PW = W + 2 * kHpM, PH = H + 2 * kHpM;
+    const uint8_t* hp = a.hp + static_cast<size_t>(slot) * 3 * PW * PH;
+    const int x0 = X0 + bx - 2, y0 = Y0 + by - 2;  // frame coordinates of P(0, 0)
+    const bool xin = x0 >= -kHpM && x0 + 20 <= W + kHpM;
+    // 3 planes x 20 rows x 5 words = 300 words; lane item i -> (plane, row, word)
+    uint32_t v[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int i = lane + 64 * k;
+      const int pl = i / 100, rem = i - pl * 100, r = rem / 5, w = rem - r * 5;
+      const int yy = clampi(y0 + r, -kHpM, H + kHpM - 1) + kHpM;
+      const uint8_t* row = hp + static_cast<size_t>(pl < 3 ? pl : 2) * PW * PH + static_cast<size_t>(yy) * PW;
+      uint32_t word = 0;
+      if (i < 300) {
+        if (xin) {
+          word = load4u(row, x0 + kHpM + 4 * w);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            word |= static_cast<uint32_t>(row[clampi(x0 + 4 * w + q, -kHpM, W + kHpM - 1) + kHpM]) << (8 * q);
+        }
+      }
+      v[k] = word;
+    }
+    // G plane from the integer window (byte-granular: the window is not word aligned here)
+    for (int i = lane; i < 400; i += 64) {
+      const int vv = i / 20, u = i - vv * 20;
+      Pb[i] = winb[(gy0 + vv + 2) * (kWinPitch * 4) + gx0 + u + 2];
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int i = lane + 64 * k;
+      if (i < 300) S.P32[100 + i] = v[k];  // plane p (1..3) starts at word 100 * p; rows of 5 words
+    }
   }
   if (lane < 4) S.P32[400 + lane] = 0;
   __syncthreads();
@@ -490,11 +602,33 @@ extern "C" void mivc_me_prof_read(unsigned long long* out) {
 
 using namespace mivc::gpu;
 
+// b / h / j planes of B reference pictures into hp ([B, 3, H + 8, W + 8], margin 4)
+extern "C" void mivc_launch_me_halfpel(int B, int W, int H, const uint8_t* ref_y, uint8_t* hp, void* stream) {
+  const long long items = static_cast<long long>(B) * (H + 2 * kHpM) * ((W + 2 * kHpM) / 4);
+  const long long g = (items + 255) / 256;
+  hipLaunchKernelGGL(me_halfpel_planes, dim3(static_cast<unsigned>(g < 8192 ? g : 8192)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), ref_y, B, W, H, hp);
+}
+
 extern "C" void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref_y,
                                const int16_t* pred_mv, int16_t* out_mv, int* out_cost, uint8_t* out_pred,
-                               int* out_intra_cost, const int* qp, int range, int subpel, void* stream) {
+                               int* out_intra_cost, const int* qp, int range, int subpel, uint8_t* hp_buf,
+                               void* stream) {
+  // hp_buf: caller-owned [B, 3, H + 8, W + 8] (+64 bytes slack) half-sample plane scratch,
+  // resident across frames; nullptr -> stream-ordered scratch for this call only.
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int W = wmb * 16, H = hmb * 16;
+  uint8_t* hp = hp_buf;
+  if (!hp) {
+    const size_t hp_bytes = static_cast<size_t>(B) * 3 * (W + 2 * kHpM) * (H + 2 * kHpM) + 64;
+    if (hipMallocAsync(reinterpret_cast<void**>(&hp), hp_bytes, s) != hipSuccess) {
+      fprintf(stderr, "mivc_launch_me: hipMallocAsync(%zu) failed\n", hp_bytes);
+      abort();
+    }
+  }
+  mivc_launch_me_halfpel(B, W, H, ref_y, hp, stream);
   MeArgs a;
-  a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
+  a.g = Geom{B, wmb, hmb, W, H};
   a.src_y = src_y;
   a.ref_y = ref_y;
   a.pred_mv = pred_mv;
@@ -505,5 +639,7 @@ extern "C" void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, co
   a.qp = qp;
   a.range = range < kMaxR ? range : kMaxR;
   a.subpel = subpel;
-  hipLaunchKernelGGL(me_p16x16, dim3(wmb * hmb, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
+  a.hp = hp;
+  hipLaunchKernelGGL(me_p16x16, dim3(wmb * hmb, B), dim3(64), 0, s, a);
+  if (!hp_buf) (void)hipFreeAsync(hp, s);
 }

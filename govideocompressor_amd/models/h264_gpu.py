@@ -139,6 +139,8 @@ class GpuH264Encoder:
         self.me_cost = torch.zeros((B, nmb), dtype=i32, device=dev)
         self.intra_cost = torch.zeros((B, nmb), dtype=i32, device=dev)
         self.pred = torch.zeros((B, nmb, 256), dtype=u8, device=dev)
+        # resident b / h / j half-sample planes of the reference (margin 4, + load slack)
+        self.me_hp = torch.empty(B * 3 * (H + 8) * (W + 8) + 64, dtype=u8, device=dev)
         self.intra_flag = torch.zeros((B, nmb), dtype=u8, device=dev)
         self.intra_count = torch.zeros((B,), dtype=i32, device=dev)
         self.qp = torch.zeros((B,), dtype=i32, device=dev)
@@ -211,7 +213,7 @@ class GpuH264Encoder:
             self.intra_count.zero_()
             self.hip.me(B, wmb, hmb, sy, fy, self._ptr(self.prev_mv), self._ptr(self.mv), self._ptr(self.me_cost),
                         self._ptr(self.pred), self._ptr(self.intra_cost), self._ptr(self.qp),
-                        self.p.me_range, self.p.subpel, s)
+                        self.p.me_range, self.p.subpel, s, self._ptr(self.me_hp))
             self.hip.encode_inter(B, wmb, hmb, sy, su, sv, fy, fu, fv, ry, ru, rv, self._ptr(self.pred),
                                   self._ptr(self.mv), self._ptr(self.me_cost), self._ptr(self.intra_cost),
                                   self._ptr(self.qp), self.p.chroma_qp_offset, self._ptr(hdr), self._ptr(coef),

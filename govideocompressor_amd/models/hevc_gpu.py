@@ -111,6 +111,7 @@ class GpuHevcEncoder:
         self.me_cost = torch.zeros((B, nmb), dtype=torch.int32, device=dev)
         self.me_intra = torch.zeros((B, nmb), dtype=torch.int32, device=dev)
         self.me_pred = torch.zeros((B, nmb, 256), dtype=torch.uint8, device=dev)
+        self.me_hp = torch.empty(B * 3 * (H + 8) * (W + 8) + 64, dtype=torch.uint8, device=dev)
         self.cand = torch.zeros((B, self.nctb, 42), dtype=torch.int32, device=dev)
         self.ctus = [torch.zeros((B, self.nctb, 32), dtype=torch.uint8, device=dev) for _ in range(2)]
         self.cus = [torch.zeros((B, self.nctb * 16, 8), dtype=torch.uint8, device=dev) for _ in range(2)]
@@ -230,7 +231,7 @@ class GpuHevcEncoder:
                 self.hip.hevc_proxy8(p(ref[0]), p(self.ref8), ref[0].numel(), bd - 8, s)
                 self.hip.me(B, self.wmb, self.hmb, p(self.src8), p(self.ref8), p(self.prev_mv), p(self.mv),
                             p(self.me_cost), p(self.me_pred), p(self.me_intra), p(self.qp), self.p.me_range,
-                            self.p.subpel, s)
+                            self.p.subpel, s, p(self.me_hp))
                 self.hip.hevc_inter(B, self.W, self.H, p(self.src[0]), p(self.src[1]), p(self.src[2]), p(ref[0]),
                                     p(ref[1]), p(ref[2]), p(cur[0]), p(cur[1]), p(cur[2]), p(self.ctu), p(self.cu),
                                     p(self.coef[0]), p(self.coef[1]), p(self.coef[2]), p(self.qp), p(self.run),

@@ -193,3 +193,26 @@ def test_me_matches_numpy_reference(host, R, seed, with_pred):
     assert np.array_equal(cost.cpu().numpy(), rcost)
     assert np.array_equal(outp.cpu().numpy().astype(np.int64), rpred)
     assert np.array_equal(intra.cpu().numpy(), rintra)
+
+
+@pytest.mark.parametrize("W,H", [(64, 48), (176, 144)])
+def test_me_halfpel_planes_match_numpy(W, H):
+    """Frame-level b / h / j planes (margin 4) against the numpy 6-tap statement."""
+    import torch
+    from govideocompressor_amd.ops import native
+    hip = native.hip()
+    rng = np.random.default_rng(W)
+    refs = rng.integers(0, 256, size=(2, H, W)).astype(np.uint8)
+    dev = torch.device("cuda")
+    tr = torch.from_numpy(refs).to(dev)
+    M = 4
+    hp = torch.zeros((2, 3, H + 2 * M, W + 2 * M), dtype=torch.uint8, device=dev)
+    hip.me_halfpel(2, W, H, tr.data_ptr(), hp.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = hp.cpu().numpy().astype(np.int64)
+    for b in range(2):
+        pl = _Planes(refs[b])
+        sl = (slice(PAD - M, PAD + H + M), slice(PAD - M, PAD + W + M))
+        for k, plane in enumerate((pl.b, pl.h, pl.j)):
+            d = np.argwhere(got[b, k] != plane[sl])
+            assert len(d) == 0, (b, "bhj"[k], len(d), d[:8], [(int(got[b, k][tuple(e)]), int(plane[sl][tuple(e)])) for e in d[:8]])
