@@ -47,9 +47,7 @@ constexpr int kHpM = 4;  // half-sample plane margin (samples); coordinates clam
 constexpr int kMaxR = 16;
 constexpr int kML = 4;                                   // window margin left/top (6-tap + qpel)
 constexpr int kMR = 6;                                   // margin right/bottom
-constexpr int kWinRowsMax = 16 + 2 * kMaxR + kML + kMR;  // 58
 constexpr int kWinPitch = 17;                            // words per LDS row (odd: bank spread)
-constexpr int kLoadsPerLane = (kWinRowsMax * 16 + 63) / 64;  // 16 words per row at most
 
 // quarter-sample position (xf, yf) -> two LDS offsets into the plane block P[4][20*20]
 // (plane 0 = G integer, 1 = b half-x, 2 = h half-y, 3 = j centre); sample = (A + B + 1) >> 1
@@ -76,8 +74,13 @@ __device__ __forceinline__ uint32_t avg4(uint32_t a, uint32_t b) {
 __device__ __forceinline__ int wave_min_key(int key) { return min64(key); }
 __device__ __forceinline__ int wave_sum(int v) { return sum64(v); }
 
+// LDS of one workgroup, sized for the largest radius its kernel instance accepts
+// (me_p16x16<8> fits 31 workgroups per CU by LDS instead of 22 for radius 16).
+template <int MAXR>
 struct MeShared {
-  uint32_t win[kWinRowsMax * kWinPitch];  // reference window, aligned words
+  static constexpr int kRows = 16 + 2 * MAXR + kML + kMR;
+  static constexpr int kLoads = (kRows * 16 + 63) / 64;  // window words per lane (16 words per row at most)
+  uint32_t win[kRows * kWinPitch];         // reference window, aligned words
   alignas(16) uint32_t src[64];            // source MB (16 rows x 4 words)
   int nb[36];                              // source intra neighbours: top[16], left[16], tl
   uint32_t P32[404];                       // G, b, h, j planes (20x20 bytes each) + pad
@@ -87,11 +90,12 @@ struct MeShared {
 // Stage rows [wy, wy+rows) x bytes [xa, xa + 4*words) of the reference, clamped to the frame.
 // All loads are issued before the first LDS store.  WORDS > 0: compile-time row width
 // (the lane -> (row, word) split is then a multiply, not a 30-instruction division).
-template <int WORDS>
-__device__ __forceinline__ void stage_window(MeShared& S, const uint8_t* ref, int W, int H, int xa, int wy,
+template <int WORDS, class SH>
+__device__ __forceinline__ void stage_window(SH& S, const uint8_t* ref, int W, int H, int xa, int wy,
                                              int rows, int words_rt, int lane) {
   const int words = WORDS > 0 ? WORDS : words_rt;
   const int n = rows * words;
+  constexpr int kLoadsPerLane = SH::kLoads;
   uint32_t v[kLoadsPerLane];
   const bool inside = xa >= 0 && xa + 4 * words <= W;
   if (inside) {
@@ -137,8 +141,8 @@ __device__ __forceinline__ uint32_t load4u(const uint8_t* row, int x) {
 // so each window row is read from LDS once (5 words) and feeds DYN candidates' SADs:
 // ~5x less LDS traffic per candidate than one-candidate-per-lane.  Source rows are LDS
 // broadcasts.
-template <int R>
-__device__ __forceinline__ int int_search_fixed(const MeShared& S, int sh0, int lane, int lambda, int cx, int cy,
+template <int R, class SH>
+__device__ __forceinline__ int int_search_fixed(const SH& S, int sh0, int lane, int lambda, int cx, int cy,
                                                 int pmx, int pmy) {
   constexpr int side = 2 * R + 1;
   constexpr int G = 64 / side;
@@ -209,44 +213,64 @@ __device__ __forceinline__ uint32_t pack4_u8(const int* v) {
 // reference clamped to the picture = the normative edge extension):
 //   b = half between x and x+1, h = half between y and y+1, j = centre.
 // Values outside the margin equal the margin's (all 6 taps replicate), so a consumer
-// clamps coordinates into [-4, W+3] x [-4, H+3] exactly.  One item = 4 columns of a row.
-__global__ __launch_bounds__(256) void me_halfpel_planes(const uint8_t* __restrict__ ref, int B, int W, int H,
+// clamps coordinates into [-4, W+3] x [-4, H+3] exactly.
+// Grid (column quads / 64, row groups / 4, slot); a thread produces 4 columns x kHpRows
+// rows, sliding a 6-row window of source rows and horizontal intermediates down.
+constexpr int kHpRows = 8;
+
+__device__ __forceinline__ void hp_load_row(const uint8_t* fr, int W, int H, int y, int x0, bool xin, int* p) {
+  const uint8_t* row = fr + static_cast<size_t>(clampi(y, 0, H - 1)) * W;
+  if (xin) {
+    const uint32_t w0 = *reinterpret_cast<const uint32_t*>(row + x0 - 4);
+    const uint32_t w1 = *reinterpret_cast<const uint32_t*>(row + x0);
+    const uint32_t w2 = *reinterpret_cast<const uint32_t*>(row + x0 + 4);
+    p[0] = __builtin_amdgcn_ubfe(w0, 16, 8);
+    p[1] = __builtin_amdgcn_ubfe(w0, 24, 8);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) p[2 + k] = __builtin_amdgcn_ubfe(w1, 8 * k, 8);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) p[6 + k] = __builtin_amdgcn_ubfe(w2, 8 * k, 8);
+  } else {
+#pragma unroll
+    for (int c = 0; c < 9; ++c) p[c] = row[clampi(x0 - 2 + c, 0, W - 1)];
+  }
+}
+
+__global__ __launch_bounds__(256) void me_halfpel_planes(const uint8_t* __restrict__ ref, int W, int H,
                                                          uint8_t* __restrict__ hp) {
   const int PW = W + 2 * kHpM, PH = H + 2 * kHpM;
-  const int qpr = PW / 4;
-  const long long total = static_cast<long long>(B) * PH * qpr;
-  for (long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
-       i += static_cast<long long>(gridDim.x) * blockDim.x) {
-    const int b = static_cast<int>(i / (static_cast<long long>(PH) * qpr));
-    const int rem = static_cast<int>(i - static_cast<long long>(b) * PH * qpr);
-    const int py = rem / qpr, px = (rem - py * qpr) * 4;
-    const int y = py - kHpM, x0 = px - kHpM;
-    const uint8_t* fr = ref + static_cast<size_t>(b) * W * H;
-    int p[6][9];  // rows y-2 .. y+3, columns x0-2 .. x0+6
+  const int q = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int py0 = (blockIdx.y * 4 + (threadIdx.x >> 6)) * kHpRows;
+  if (q >= PW / 4 || py0 >= PH) return;
+  const int slot = blockIdx.z;
+  const int x0 = 4 * q - kHpM, y0 = py0 - kHpM;
+  const uint8_t* fr = ref + static_cast<size_t>(slot) * W * H;
+  const bool xin = x0 - 4 >= 0 && x0 + 8 <= W;
+  // window: source rows y-2 .. y+3 (p) and their horizontal 6-tap sums (b1)
+  int p[6][9], b1[6][4];
 #pragma unroll
-    for (int r = 0; r < 6; ++r) {
-      const uint8_t* row = fr + static_cast<size_t>(clampi(y - 2 + r, 0, H - 1)) * W;
-      if (x0 - 4 >= 0 && x0 + 8 <= W) {
-        const uint32_t w0 = *reinterpret_cast<const uint32_t*>(row + x0 - 4);
-        const uint32_t w1 = *reinterpret_cast<const uint32_t*>(row + x0);
-        const uint32_t w2 = *reinterpret_cast<const uint32_t*>(row + x0 + 4);
-        p[r][0] = (w0 >> 16) & 255;
-        p[r][1] = w0 >> 24;
+  for (int r = 0; r < 5; ++r) {
+    hp_load_row(fr, W, H, y0 - 2 + r, x0, xin, p[r + 1]);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) p[r][2 + k] = (w1 >> (8 * k)) & 255;
+    for (int k = 0; k < 4; ++k)
+      b1[r + 1][k] = h264::tap6(p[r + 1][k], p[r + 1][k + 1], p[r + 1][k + 2], p[r + 1][k + 3], p[r + 1][k + 4],
+                                p[r + 1][k + 5]);
+  }
+  const size_t plane = static_cast<size_t>(PW) * PH;
+  uint8_t* o = hp + static_cast<size_t>(slot) * 3 * plane + static_cast<size_t>(py0) * PW + 4 * q;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) p[r][6 + k] = (w2 >> (8 * k)) & 255;
-      } else {
+  for (int t = 0; t < kHpRows; ++t) {
 #pragma unroll
-        for (int c = 0; c < 9; ++c) p[r][c] = row[clampi(x0 - 2 + c, 0, W - 1)];
-      }
+    for (int r = 0; r < 5; ++r) {
+#pragma unroll
+      for (int c = 0; c < 9; ++c) p[r][c] = p[r + 1][c];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) b1[r][k] = b1[r + 1][k];
     }
-    int b1[6][4];
+    hp_load_row(fr, W, H, y0 + t + 3, x0, xin, p[5]);
 #pragma unroll
-    for (int r = 0; r < 6; ++r)
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        b1[r][k] = h264::tap6(p[r][k], p[r][k + 1], p[r][k + 2], p[r][k + 3], p[r][k + 4], p[r][k + 5]);
+    for (int k = 0; k < 4; ++k)
+      b1[5][k] = h264::tap6(p[5][k], p[5][k + 1], p[5][k + 2], p[5][k + 3], p[5][k + 4], p[5][k + 5]);
     int bv[4], hv[4], jv[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -258,11 +282,12 @@ __global__ __launch_bounds__(256) void me_halfpel_planes(const uint8_t* __restri
     // byte packing through v_perm: a shift/or packing of clip((x + r) >> n) values gets
     // selected to gfx950's v_ashr_pk_u8_i32, whose high half the backend assumes is zero
     // (it is not): bytes 2-3 came out 255 on some inputs (test_me_halfpel_planes_match_numpy)
-    const uint32_t wb = pack4_u8(bv), wh = pack4_u8(hv), wj = pack4_u8(jv);
-    uint8_t* o = hp + static_cast<size_t>(b) * 3 * PW * PH + static_cast<size_t>(py) * PW + px;
-    *reinterpret_cast<uint32_t*>(o) = wb;
-    *reinterpret_cast<uint32_t*>(o + static_cast<size_t>(PW) * PH) = wh;
-    *reinterpret_cast<uint32_t*>(o + 2 * static_cast<size_t>(PW) * PH) = wj;
+    if (py0 + t < PH) {
+      *reinterpret_cast<uint32_t*>(o) = pack4_u8(bv);
+      *reinterpret_cast<uint32_t*>(o + plane) = pack4_u8(hv);
+      *reinterpret_cast<uint32_t*>(o + 2 * plane) = pack4_u8(jv);
+    }
+    o += PW;
   }
 }
 
@@ -273,6 +298,7 @@ __device__ unsigned long long g_me_prof[64][12];
 #define MPROF(ph) do {} while (0)
 #endif
 
+template <int MAXR>
 __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   const Geom& g = a.g;
   // XCD-aware remap: hardware deals workgroups round-robin over the 8 XCDs; give each XCD
@@ -290,9 +316,9 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   const int W = g.W, H = g.H;
   const int qp = a.qp[slot];
   const int lambda = h264::kLambda[qp];
-  const int R = a.range < kMaxR ? a.range : kMaxR;
+  const int R = a.range < MAXR ? a.range : MAXR;
 
-  __shared__ MeShared S;
+  __shared__ MeShared<MAXR> S;
 
   MPROF(0);
   // ---- phase 0: source MB, its intra neighbours, candidate vectors (one batch of loads)
@@ -403,15 +429,6 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   if (bp == 4095) {
     bx = 0;
     by = 0;
-    // re-stage the window around the zero vector for the sub-pel planes (rare)
-    __syncthreads();
-    cx = 0;
-    cy = 0;
-    wx = X0 - R - kML;
-    xa = wx & ~3;
-    sh0 = wx - xa;
-    stage_window<0>(S, ref, W, H, xa, Y0 - R - kML, wrows, wwords, lane);
-    __syncthreads();
   } else {
     by = bp / side;
     bx = cx + (bp - by * side) - R;
@@ -420,47 +437,51 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   int best_mvx = bx * 4, best_mvy = by * 4;
 
   MPROF(3);
-  // ---- phase 3: sub-pel planes around (bx, by).  G comes from the LDS window; b, h, j
-  // (clause 8.4.2.2.1 half-sample planes) are staged from the frame-level planes built
-  // once per reference picture by me_halfpel_planes (the per-MB 6-tap filtering they
-  // replace was ~20% of this kernel's instructions).  P(u, v) = plane at (X0+bx-2+u, Y0+by-2+v).
-  const uint8_t* winb = reinterpret_cast<const uint8_t*>(S.win);
-  const int gx0 = sh0 + bx - cx + R, gy0 = by - cy + R;  // window byte column / row of pixel (bx-4, by-4)
-  uint8_t* Pb = reinterpret_cast<uint8_t*>(S.P32);
+  // ---- phase 3: sub-pel planes around (bx, by): G from the reference, b, h, j (clause
+  // 8.4.2.2.1 half-sample planes) from the frame-level planes built once per reference
+  // picture by me_halfpel_planes (the per-MB 6-tap filtering they replace was ~20% of
+  // this kernel's instructions).  P(u, v) = plane at (X0+bx-2+u, Y0+by-2+v).
   {
     const int PW = W + 2 * kHpM, PH = H + 2 * kHpM;
     const uint8_t* hp = a.hp + static_cast<size_t>(slot) * 3 * PW * PH;
     const int x0 = X0 + bx - 2, y0 = Y0 + by - 2;  // frame coordinates of P(0, 0)
     const bool xin = x0 >= -kHpM && x0 + 20 <= W + kHpM;
-    // 3 planes x 20 rows x 5 words = 300 words; lane item i -> (plane, row, word)
-    uint32_t v[5];
+    // 4 planes (G from the reference itself, b / h / j from hp) x 20 rows x 5 words =
+    // 400 words, one batch of loads; lane item i -> (plane, row, word)
+    const bool gin = x0 >= 0 && x0 + 20 <= W;
+    uint32_t v[7];
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {
+    for (int k = 0; k < 7; ++k) {
       const int i = lane + 64 * k;
       const int pl = i / 100, rem = i - pl * 100, r = rem / 5, w = rem - r * 5;
-      const int yy = clampi(y0 + r, -kHpM, H + kHpM - 1) + kHpM;
-      const uint8_t* row = hp + static_cast<size_t>(pl < 3 ? pl : 2) * PW * PH + static_cast<size_t>(yy) * PW;
       uint32_t word = 0;
-      if (i < 300) {
-        if (xin) {
-          word = load4u(row, x0 + kHpM + 4 * w);
-        } else {
+      if (i < 400) {
+        if (pl == 0) {
+          const uint8_t* row = ref + static_cast<size_t>(clampi(y0 + r, 0, H - 1)) * W;
+          if (gin) {
+            word = load4u(row, x0 + 4 * w);
+          } else {
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
-            word |= static_cast<uint32_t>(row[clampi(x0 + 4 * w + q, -kHpM, W + kHpM - 1) + kHpM]) << (8 * q);
+            for (int q = 0; q < 4; ++q) word |= static_cast<uint32_t>(row[clampi(x0 + 4 * w + q, 0, W - 1)]) << (8 * q);
+          }
+        } else {
+          const int yy = clampi(y0 + r, -kHpM, H + kHpM - 1) + kHpM;
+          const uint8_t* row = hp + static_cast<size_t>(pl - 1) * PW * PH + static_cast<size_t>(yy) * PW;
+          if (xin) {
+            word = load4u(row, x0 + kHpM + 4 * w);
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              word |= static_cast<uint32_t>(row[clampi(x0 + 4 * w + q, -kHpM, W + kHpM - 1) + kHpM]) << (8 * q);
+          }
         }
       }
       v[k] = word;
     }
-    // G plane from the integer window (byte-granular: the window is not word aligned here)
-    for (int i = lane; i < 400; i += 64) {
-      const int vv = i / 20, u = i - vv * 20;
-      Pb[i] = winb[(gy0 + vv + 2) * (kWinPitch * 4) + gx0 + u + 2];
-    }
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {
+    for (int k = 0; k < 7; ++k) {
       const int i = lane + 64 * k;
-      if (i < 300) S.P32[100 + i] = v[k];  // plane p (1..3) starts at word 100 * p; rows of 5 words
+      if (i < 400) S.P32[i] = v[k];  // plane p starts at word 100 * p; rows of 5 words
     }
   }
   if (lane < 4) S.P32[400 + lane] = 0;
@@ -603,11 +624,11 @@ extern "C" void mivc_me_prof_read(unsigned long long* out) {
 using namespace mivc::gpu;
 
 // b / h / j planes of B reference pictures into hp ([B, 3, H + 8, W + 8], margin 4)
+// b / h / j planes of B reference pictures into hp ([B, 3, H + 8, W + 8], margin 4)
 extern "C" void mivc_launch_me_halfpel(int B, int W, int H, const uint8_t* ref_y, uint8_t* hp, void* stream) {
-  const long long items = static_cast<long long>(B) * (H + 2 * kHpM) * ((W + 2 * kHpM) / 4);
-  const long long g = (items + 255) / 256;
-  hipLaunchKernelGGL(me_halfpel_planes, dim3(static_cast<unsigned>(g < 8192 ? g : 8192)), dim3(256), 0,
-                     static_cast<hipStream_t>(stream), ref_y, B, W, H, hp);
+  const int PW = W + 2 * kHpM, PH = H + 2 * kHpM;
+  const dim3 grid((PW / 4 + 63) / 64, (PH + 4 * kHpRows - 1) / (4 * kHpRows), B);
+  hipLaunchKernelGGL(me_halfpel_planes, grid, dim3(256), 0, static_cast<hipStream_t>(stream), ref_y, W, H, hp);
 }
 
 extern "C" void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref_y,
@@ -640,6 +661,7 @@ extern "C" void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, co
   a.range = range < kMaxR ? range : kMaxR;
   a.subpel = subpel;
   a.hp = hp;
-  hipLaunchKernelGGL(me_p16x16, dim3(wmb * hmb, B), dim3(64), 0, s, a);
+  if (a.range <= 8) hipLaunchKernelGGL(me_p16x16<8>, dim3(wmb * hmb, B), dim3(64), 0, s, a);
+  else hipLaunchKernelGGL(me_p16x16<kMaxR>, dim3(wmb * hmb, B), dim3(64), 0, s, a);
   if (!hp_buf) (void)hipFreeAsync(hp, s);
 }
