@@ -75,6 +75,35 @@ __device__ __forceinline__ void row_wait(int* prog, int row, int target, int* er
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+// row_wait whose acquire orders LDS only (the producer hands data over through LDS)
+__device__ __forceinline__ void row_wait_lds(int* prog, int row, int target, int* err) {
+  int spins = 0;
+  while (__hip_atomic_load(prog + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > (1 << 24)) {
+      if (lane_id() == 0) atomicOr(err, 1);
+      break;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// four values in [0, 255] -> one little-endian word, via v_perm_b32 only.  (A shift/or
+// packing of clip((x + r) >> n) values gets selected to gfx950's v_ashr_pk_u8_i32, whose
+// high half the backend wrongly assumes is zero.)
+__device__ __forceinline__ uint32_t pack4_u8(const int* v) {
+  const uint32_t lo = __builtin_amdgcn_perm(static_cast<uint32_t>(v[1]), static_cast<uint32_t>(v[0]), 0x0c0c0400u);
+  const uint32_t hi = __builtin_amdgcn_perm(static_cast<uint32_t>(v[3]), static_cast<uint32_t>(v[2]), 0x0c0c0400u);
+  return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+}
+
+// publish prog[row] = value after this wave's LDS stores only (global stores are not
+// waited for: the consumer reads nothing this wave stored to global memory)
+__device__ __forceinline__ void row_publish_lds(int* prog, int row, int value) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  if (lane_id() == 0) __hip_atomic_store(prog + row, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // publish prog[row] = value after this wave's global stores
 __device__ __forceinline__ void row_publish(int* prog, int row, int value) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");

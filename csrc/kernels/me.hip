@@ -201,13 +201,6 @@ __device__ __forceinline__ int int_search_fixed(const SH& S, int sh0, int lane, 
   return best;
 }
 
-// four values in [0, 255] -> one little-endian word, via v_perm_b32 only
-__device__ __forceinline__ uint32_t pack4_u8(const int* v) {
-  const uint32_t lo = __builtin_amdgcn_perm(static_cast<uint32_t>(v[1]), static_cast<uint32_t>(v[0]), 0x0c0c0400u);
-  const uint32_t hi = __builtin_amdgcn_perm(static_cast<uint32_t>(v[3]), static_cast<uint32_t>(v[2]), 0x0c0c0400u);
-  return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
-}
-
 // Frame-level half-sample planes of a reference batch (clause 8.4.2.2.1): for every
 // integer position (x, y) of a (W + 8) x (H + 8) grid (margin kHpM, coordinates of the
 // reference clamped to the picture = the normative edge extension):
