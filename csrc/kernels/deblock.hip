@@ -62,7 +62,7 @@ struct DeblockShared {
 };
 
 struct DeblockTables {
-  int alpha[52], beta[52], tc0[52][3];
+  int alpha[52], beta[52], tc0[52][3], cqp[52];
 };
 
 // Filter one line across an edge (clause 8.7.2.3/8.7.2.4), branch-free.  P = p3 p2 p1 p0
@@ -135,11 +135,20 @@ __global__ __launch_bounds__(64 * kDeblockWaves) void deblock_wavefront(DeblockA
     T.tc0[i][0] = h264::kTc0[i][0];
     T.tc0[i][1] = h264::kTc0[i][1];
     T.tc0[i][2] = h264::kTc0[i][2];
+    T.cqp[i] = h264::kChromaQp[i];
   }
   __syncthreads();
-  const int w = wave_id(), lane = lane_id();
-  const int half = lane >> 5, hl = lane & 31;
+  const int w = wave_id();
+  // lane-derived values are recomputed per step from an opaque lane id instead of being
+  // hoisted out of the loops (at 16 waves the hoisted addresses spilled to scratch)
+  auto opaque_lane = []() { int l = lane_id(); asm volatile("" : "+v"(l)); return l; };
+  const int half = lane_id() >> 5;
   DeblockShared& S = SS[w][half];
+#define DB_LANE_VALUES                                                     \
+  const int lane = opaque_lane(), hl = lane & 31;                          \
+  const bool is_c = hl >= 16; /* 0..15 luma lines, 16..23 Cb, 24..31 Cr */ \
+  const int ccomp = (hl - 16) >> 3, cline = hl & 7;                        \
+  const int line = is_c ? cline : hl;
   const int W = g.W, cw = g.cw(), wmb = g.wmb, hmb = g.hmb;
   uint8_t* recy = a.rec_y + slot * g.ysize();
   uint8_t* const rcu = a.rec_u + slot * g.csize();
@@ -147,9 +156,6 @@ __global__ __launch_bounds__(64 * kDeblockWaves) void deblock_wavefront(DeblockA
   auto recc = [&](int c) { return c ? rcv : rcu; };
   const uint32_t* hdr32 = reinterpret_cast<const uint32_t*>(a.hdr) + static_cast<size_t>(slot) * g.nmb() * 12;
   const uint32_t* nz32 = reinterpret_cast<const uint32_t*>(a.nz) + static_cast<size_t>(slot) * g.nmb() * 4;
-  const bool is_c = hl >= 16;  // half lanes 0..15 luma lines, 16..23 Cb, 24..31 Cr
-  const int ccomp = (hl - 16) >> 3, cline = hl & 7;
-  const int line = is_c ? cline : hl;
 
   // unfiltered inputs of MB (x, y), branch-free (three loads per lane, lane-selected
   // addresses) so that they stay in flight across the previous MB's filtering:
@@ -157,6 +163,8 @@ __global__ __launch_bounds__(64 * kDeblockWaves) void deblock_wavefront(DeblockA
   //   lane one record word: 0..11 current header, 12..23 top header, 24..27 current nz,
   //   28..31 top nz
   auto load_inputs = [&](int x, int y, uint32_t (&v)[5]) {
+    DB_LANE_VALUES
+    (void)line;
     const uint8_t* a1 = recy + static_cast<size_t>(y * 16 + (hl & 15)) * W + x * 16;
     const uint8_t* a2 = a1 + 8;
     if (is_c) a1 = a2 = recc(ccomp) + static_cast<size_t>(y * 8 + cline) * cw + x * 8;
@@ -178,12 +186,13 @@ __global__ __launch_bounds__(64 * kDeblockWaves) void deblock_wavefront(DeblockA
     const bool last_row = y == hmb - 1;
     const bool has_top = y > 0;
     // this wave's lower ring still holds bottom edges of row yl - 32 until row yl - 31 used them
-    if (half && yl >= 2 * kDeblockWaves && row_ok) row_wait_lds(prog, yl - 2 * kDeblockWaves + 1, wmb, a.err);
+    if (half && yl >= 2 * kDeblockWaves && row_ok && (lane_id() & 31) == 0) row_wait_lds(prog, yl - 2 * kDeblockWaves + 1, wmb, a.err);
     uint32_t nxt[5] = {0, 0, 0, 0, 0};
     if (!half) load_inputs(0, y, nxt);
     for (int step = 0; step < wmb + 2; ++step) {
       const int x = half ? step - 2 : step;
       const bool act = row_ok && x >= 0 && x < wmb;
+      DB_LANE_VALUES
       const uint32_t cur[5] = {nxt[0], nxt[1], nxt[2], nxt[3], nxt[4]};
       if (row_ok && x + 1 >= 0 && x + 1 < wmb) load_inputs(x + 1, y, nxt);
       if (act) {
@@ -225,8 +234,8 @@ __global__ __launch_bounds__(64 * kDeblockWaves) void deblock_wavefront(DeblockA
           const int qpn = reinterpret_cast<const MbHeader*>(S.hdrw[dir == 0 ? 1 : 2])->qp;
           int qq = qpq, qn = inner ? qpq : qpn;
           if (ch) {
-            qq = h264::chroma_qp(qq, a.chroma_qp_offset);
-            qn = h264::chroma_qp(qn, a.chroma_qp_offset);
+            qq = T.cqp[clampi(qq + a.chroma_qp_offset, 0, 51)];
+            qn = T.cqp[clampi(qn + a.chroma_qp_offset, 0, 51)];
           }
           const int qpav = (qq + qn + 1) >> 1;
           const int ia = clampi(qpav + a.alpha_off, 0, 51), ib = clampi(qpav + a.beta_off, 0, 51);
