@@ -147,30 +147,67 @@ __device__ __forceinline__ FrameConst frame_const(const SynthGeom& g, int fz) {
   return c;
 }
 
+// Per-frame constants are computed once per workgroup (grid = (run blocks, frames)), the
+// objects are tested once per 16-pixel run (per-pixel tests only where a run meets one),
+// and the per-pixel sine comes from one sin/cos pair per run by angle addition.
+struct FrameShared {
+  FrameConst fc;
+  int ix, iy;
+  float w00, w10, w01, w11;
+};
+
+// sin(a + d * k), cos(d * k) for k = 0..15 by angle addition from one sin/cos pair
+template <int N>
+__device__ __forceinline__ void sin_run(float a, float d, float (&out)[N]) {
+  const float s0 = __sinf(a), c0 = __cosf(a);
+#pragma unroll
+  for (int k = 0; k < N; ++k) out[k] = s0 * cosf(d * k) + c0 * sinf(d * k);  // constants after unrolling
+}
+
+// does the run [x16, x16 + 16) of row y meet object o (wrapping display coordinates)?
+__device__ __forceinline__ bool run_meets(int x16, int y, int obx, int oby, int ow, int oh, int w, int h) {
+  int ly = y - oby;
+  ly = ly < 0 ? ly + h : ly;
+  if (ly >= oh) return false;
+  int lx = x16 - obx;
+  lx = lx < 0 ? lx + w : lx;
+  return lx < ow || lx + 16 > w;
+}
+
 __global__ __launch_bounds__(256) void synth_frame_luma(FrameArgs a) {
   const SynthGeom& g = a.g;
   const int runs = (g.width + 15) >> 4;
-  const long long total = static_cast<long long>(g.slots) * g.frames * g.height * runs;
-  for (long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
-       i += static_cast<long long>(gridDim.x) * blockDim.x) {
-    const int fz = static_cast<int>(i / (static_cast<long long>(g.height) * runs));
-    const int rem = static_cast<int>(i - static_cast<long long>(fz) * g.height * runs);
-    const int y = rem / runs, x16 = (rem - y * runs) * 16;
-    const FrameConst fc = frame_const(g, fz);
-    // per-slot global motion (pan) in pixels/frame, sub-pixel
-    const float vx = ((hash3(fc.ss, 1, 0) & 255) / 255.f - 0.5f) * 6.f;
-    const float vy = ((hash3(fc.ss, 2, 0) & 255) / 255.f - 0.5f) * 3.f;
-    const float fx = vx * fc.f, fy = vy * fc.f;
-    const float ixf = floorf(fx), iyf = floorf(fy);
-    const float tx = fx - ixf, ty = fy - iyf;
-    int cy0 = (y + static_cast<int>(iyf)) % g.ch;
+  const int nfr = g.slots * g.frames;
+  __shared__ FrameShared F;
+  for (int fz = blockIdx.y; fz < nfr; fz += gridDim.y) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      F.fc = frame_const(g, fz);
+      // per-slot global motion (pan) in pixels/frame, sub-pixel
+      const float vx = ((hash3(F.fc.ss, 1, 0) & 255) / 255.f - 0.5f) * 6.f;
+      const float vy = ((hash3(F.fc.ss, 2, 0) & 255) / 255.f - 0.5f) * 3.f;
+      const float fx = vx * F.fc.f, fy = vy * F.fc.f;
+      const float ixf = floorf(fx), iyf = floorf(fy);
+      const float tx = fx - ixf, ty = fy - iyf;
+      F.ix = static_cast<int>(ixf);
+      F.iy = static_cast<int>(iyf);
+      F.w00 = (1.f - tx) * (1.f - ty);
+      F.w10 = tx * (1.f - ty);
+      F.w01 = (1.f - tx) * ty;
+      F.w11 = tx * ty;
+    }
+    __syncthreads();
+    const FrameConst& fc = F.fc;
+    for (int item = blockIdx.x * blockDim.x + threadIdx.x; item < g.height * runs; item += gridDim.x * blockDim.x) {
+    const int y = item / runs, x16 = (item - y * runs) * 16;
+    int cy0 = (y + F.iy) % g.ch;
     cy0 = cy0 < 0 ? cy0 + g.ch : cy0;
     const int cy1 = cy0 + 1 == g.ch ? 0 : cy0 + 1;
     const uint8_t* r0 = a.cy + (static_cast<size_t>(fc.slot) * g.ch + cy0) * g.cw;
     const uint8_t* r1 = a.cy + (static_cast<size_t>(fc.slot) * g.ch + cy1) * g.cw;
-    int cx0 = (x16 + static_cast<int>(ixf)) % g.cw;
+    int cx0 = (x16 + F.ix) % g.cw;
     cx0 = cx0 < 0 ? cx0 + g.cw : cx0;
-    uint8_t t0[20], t1[20];
+    uint32_t u0w[5], u1w[5];
     if (cx0 + 17 <= g.cw) {  // the run's 17 canvas bytes are contiguous (cw is a multiple of 4)
       const int ca = cx0 & ~3, sh = cx0 & 3;
       uint32_t w0[6], w1[6];
@@ -182,55 +219,61 @@ __global__ __launch_bounds__(256) void synth_frame_luma(FrameArgs a) {
       }
 #pragma unroll
       for (int k = 0; k < 5; ++k) {
-        const uint32_t u0 = __builtin_amdgcn_alignbyte(w0[k + 1], w0[k], sh);
-        const uint32_t u1 = __builtin_amdgcn_alignbyte(w1[k + 1], w1[k], sh);
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          t0[4 * k + b] = static_cast<uint8_t>(u0 >> (8 * b));
-          t1[4 * k + b] = static_cast<uint8_t>(u1 >> (8 * b));
-        }
+        u0w[k] = __builtin_amdgcn_alignbyte(w0[k + 1], w0[k], sh);
+        u1w[k] = __builtin_amdgcn_alignbyte(w1[k + 1], w1[k], sh);
       }
     } else {
 #pragma unroll
-      for (int k = 0; k < 17; ++k) {
-        const int cx = cx0 + k >= g.cw ? cx0 + k - g.cw : cx0 + k;
-        t0[k] = r0[cx];
-        t1[k] = r1[cx];
+      for (int k = 0; k < 5; ++k) {
+        uint32_t v0 = 0, v1 = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          int cx = cx0 + 4 * k + b;
+          cx = cx >= g.cw ? cx - g.cw : cx;
+          v0 |= static_cast<uint32_t>(r0[cx]) << (8 * b);
+          v1 |= static_cast<uint32_t>(r1[cx]) << (8 * b);
+        }
+        u0w[k] = v0;
+        u1w[k] = v1;
       }
     }
-    const float w00 = (1.f - tx) * (1.f - ty), w10 = tx * (1.f - ty), w01 = (1.f - tx) * ty, w11 = tx * ty;
-    uint32_t h4[4];
+    auto t0 = [&](int k) { return static_cast<float>((u0w[k >> 2] >> (8 * (k & 3))) & 255u); };
+    auto t1 = [&](int k) { return static_cast<float>((u1w[k >> 2] >> (8 * (k & 3))) & 255u); };
+    float sn[16];
+    sin_run(0.01f * (x16 + y) + 0.03f * fc.f, 0.01f, sn);
+    int lum[16];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      h4[q] = hash3(static_cast<uint32_t>(x16 + 4 * q), static_cast<uint32_t>(y), fc.ss ^ (fc.f * 2654435761u));
+    for (int k = 0; k < 16; ++k)
+      lum[k] = static_cast<int>(t0(k) * F.w00 + t0(k + 1) * F.w10 + t1(k) * F.w01 + t1(k + 1) * F.w11 + 20.f * sn[k] +
+                                0.5f);
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      if (run_meets(x16, y, fc.obx[o], fc.oby[o], g.ow[o], g.oh[o], g.width, g.height)) {
+        int ly = y - fc.oby[o];
+        ly = ly < 0 ? ly + g.height : ly;
+        const uint8_t* trow = a.tiles + (static_cast<size_t>(fc.slot) * 3 + o) * a.tile_stride + static_cast<size_t>(ly) * g.ow[o];
+        for (int k = 0; k < 16; ++k) {
+          int lx = x16 + k - fc.obx[o];
+          lx = lx < 0 ? lx + g.width : lx;  // wrap-around
+          if (lx < g.ow[o]) lum[k] = trow[lx];
+        }
+      }
+    }
     uint32_t out[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      uint32_t w = 0;
+      const uint32_t h = hash3(static_cast<uint32_t>(x16 + 4 * q), static_cast<uint32_t>(y), fc.ss ^ (fc.f * 2654435761u));
+      int v4[4];
 #pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const int k = 4 * q + b, x = x16 + k;
-        float lum = t0[k] * w00 + t0[k + 1] * w10 + t1[k] * w01 + t1[k + 1] * w11 +
-                    20.f * __sinf(0.01f * (x + y) + 0.03f * fc.f);
-#pragma unroll
-        for (int o = 0; o < 3; ++o) {
-          int lx = x - fc.obx[o], ly = y - fc.oby[o];
-          lx = lx < 0 ? lx + g.width : lx;  // wrap-around
-          ly = ly < 0 ? ly + g.height : ly;
-          if (lx < g.ow[o] && ly < g.oh[o])
-            lum = a.tiles[(static_cast<size_t>(fc.slot) * 3 + o) * a.tile_stride + static_cast<size_t>(ly) * g.ow[o] + lx];
-        }
-        int v = static_cast<int>(lum + 0.5f) + noise5(h4[q], b);
-        v = v < 0 ? 0 : (v > 255 ? 255 : v);
-        w |= static_cast<uint32_t>(v) << (8 * b);
-      }
-      out[q] = w;
+      for (int b = 0; b < 4; ++b) v4[b] = clampi(lum[4 * q + b] + noise5(h, b), 0, 255);
+      out[q] = pack4_u8(v4);
     }
     uint8_t* dst = a.y + (static_cast<size_t>(fz) * g.height + y) * g.width + x16;
     if (x16 + 16 <= g.width && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
       *reinterpret_cast<uint4*>(dst) = make_uint4(out[0], out[1], out[2], out[3]);
     } else {
       for (int k = 0; k < 16 && x16 + k < g.width; ++k) dst[k] = static_cast<uint8_t>(out[k >> 2] >> (8 * (k & 3)));
+    }
     }
   }
 }
@@ -239,51 +282,93 @@ __global__ __launch_bounds__(256) void synth_frame_chroma(FrameArgs a) {
   const SynthGeom& g = a.g;
   const int w2 = g.width / 2, h2 = g.height / 2, ccw = g.cw / 2, cch = g.ch / 2;
   const int runs = (w2 + 15) >> 4;
-  const long long total = static_cast<long long>(g.slots) * g.frames * h2 * runs;
-  for (long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
-       i += static_cast<long long>(gridDim.x) * blockDim.x) {
-    const int fz = static_cast<int>(i / (static_cast<long long>(h2) * runs));
-    const int rem = static_cast<int>(i - static_cast<long long>(fz) * h2 * runs);
-    const int y = rem / runs, x16 = (rem - y * runs) * 16;
-    FrameConst fc = frame_const(g, fz);
-    const float vx = ((hash3(fc.ss, 1, 0) & 255) / 255.f - 0.5f) * 3.f;
-    const float vy = ((hash3(fc.ss, 2, 0) & 255) / 255.f - 0.5f) * 1.5f;
-    const int ix = static_cast<int>(floorf(vx * fc.f)), iy = static_cast<int>(floorf(vy * fc.f));
-    int cyy = (y + iy) % cch;
+  const int nfr = g.slots * g.frames;
+  __shared__ FrameShared F;
+  for (int fz = blockIdx.y; fz < nfr; fz += gridDim.y) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      F.fc = frame_const(g, fz);
+      const float vx = ((hash3(F.fc.ss, 1, 0) & 255) / 255.f - 0.5f) * 3.f;
+      const float vy = ((hash3(F.fc.ss, 2, 0) & 255) / 255.f - 0.5f) * 1.5f;
+      F.ix = static_cast<int>(floorf(vx * F.fc.f));
+      F.iy = static_cast<int>(floorf(vy * F.fc.f));
+#pragma unroll
+      for (int o = 0; o < 3; ++o) {
+        F.fc.obx[o] >>= 1;
+        F.fc.oby[o] >>= 1;
+      }
+    }
+    __syncthreads();
+    const FrameConst& fc = F.fc;
+    for (int item = blockIdx.x * blockDim.x + threadIdx.x; item < h2 * runs; item += gridDim.x * blockDim.x) {
+    const int y = item / runs, x16 = (item - y * runs) * 16;
+    int cyy = (y + F.iy) % cch;
     cyy = cyy < 0 ? cyy + cch : cyy;
     const size_t rowo = (static_cast<size_t>(fc.slot) * cch + cyy) * ccw;
+    int cx0 = (x16 + F.ix) % ccw;
+    cx0 = cx0 < 0 ? cx0 + ccw : cx0;
+    uint32_t uw[4], vw[4];
+    if (cx0 + 20 <= ccw) {  // contiguous: 5 aligned words + alignbyte
+      const int ca = cx0 & ~3, sh = cx0 & 3;
+      uint32_t a0[5], b0[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        a0[k] = *reinterpret_cast<const uint32_t*>(a.cu + rowo + ca + 4 * k);
+        b0[k] = *reinterpret_cast<const uint32_t*>(a.cv + rowo + ca + 4 * k);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uw[k] = __builtin_amdgcn_alignbyte(a0[k + 1], a0[k], sh);
+        vw[k] = __builtin_amdgcn_alignbyte(b0[k + 1], b0[k], sh);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint32_t p = 0, q = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          int cx = cx0 + 4 * k + b;
+          cx = cx >= ccw ? cx - ccw : cx;
+          p |= static_cast<uint32_t>(a.cu[rowo + cx]) << (8 * b);
+          q |= static_cast<uint32_t>(a.cv[rowo + cx]) << (8 * b);
+        }
+        uw[k] = p;
+        vw[k] = q;
+      }
+    }
+    float sn[16];
+    sin_run(0.02f * x16, 0.02f, sn);
+    const int cv_row = static_cast<int>(10.f * __cosf(0.02f * y));
+    int cu[16], cv[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      cu[k] = static_cast<int>((uw[k >> 2] >> (8 * (k & 3))) & 255u) + static_cast<int>(10.f * sn[k]);
+      cv[k] = static_cast<int>((vw[k >> 2] >> (8 * (k & 3))) & 255u) + cv_row;
+    }
 #pragma unroll
     for (int o = 0; o < 3; ++o) {
-      fc.obx[o] >>= 1;
-      fc.oby[o] >>= 1;
+      if (run_meets(x16, y, fc.obx[o], fc.oby[o], g.ow[o] / 2, g.oh[o] / 2, w2, h2)) {
+        for (int k = 0; k < 16; ++k) {
+          int lx = x16 + k - fc.obx[o];
+          lx = lx < 0 ? lx + w2 : lx;
+          if (lx < g.ow[o] / 2) {
+            cu[k] = 90 + 50 * o;
+            cv[k] = 170 - 40 * o;
+          }
+        }
+      }
     }
-    const float cv_row = 10.f * __cosf(0.02f * y);
     uint32_t ou[4], ov[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      uint32_t wu = 0, wv = 0;
+      int pu[4], pv[4];
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
-        const int x = x16 + 4 * q + b;
-        int cxx = (x + ix) % ccw;
-        cxx = cxx < 0 ? cxx + ccw : cxx;
-        int cu = a.cu[rowo + cxx] + static_cast<int>(10.f * __sinf(0.02f * x));
-        int cv = a.cv[rowo + cxx] + static_cast<int>(cv_row);
-#pragma unroll
-        for (int o = 0; o < 3; ++o) {
-          int lx = x - fc.obx[o], ly = y - fc.oby[o];
-          lx = lx < 0 ? lx + w2 : lx;
-          ly = ly < 0 ? ly + h2 : ly;
-          if (lx < g.ow[o] / 2 && ly < g.oh[o] / 2) {
-            cu = 90 + 50 * o;
-            cv = 170 - 40 * o;
-          }
-        }
-        wu |= static_cast<uint32_t>(clampi(cu, 0, 255)) << (8 * b);
-        wv |= static_cast<uint32_t>(clampi(cv, 0, 255)) << (8 * b);
+        pu[b] = clampi(cu[4 * q + b], 0, 255);
+        pv[b] = clampi(cv[4 * q + b], 0, 255);
       }
-      ou[q] = wu;
-      ov[q] = wv;
+      ou[q] = pack4_u8(pu);
+      ov[q] = pack4_u8(pv);
     }
     const size_t idx = (static_cast<size_t>(fz) * h2 + y) * w2 + x16;
     if (x16 + 16 <= w2 && ((reinterpret_cast<uintptr_t>(a.u + idx) | reinterpret_cast<uintptr_t>(a.v + idx)) & 15) == 0) {
@@ -294,6 +379,7 @@ __global__ __launch_bounds__(256) void synth_frame_chroma(FrameArgs a) {
         a.u[idx + k] = static_cast<uint8_t>(ou[k >> 2] >> (8 * (k & 3)));
         a.v[idx + k] = static_cast<uint8_t>(ov[k >> 2] >> (8 * (k & 3)));
       }
+    }
     }
   }
 }
@@ -334,13 +420,12 @@ extern "C" void mivc_launch_synth(uint8_t* y, uint8_t* u, uint8_t* v, int width,
   int omw = std::max(g.ow[0], std::max(g.ow[1], g.ow[2])), omh = std::max(g.oh[0], std::max(g.oh[1], g.oh[2]));
   hipLaunchKernelGGL(synth_objects, dim3((omw + 255) / 256, omh, slots * 3), dim3(256), 0, s, g, tiles, tile_stride);
   FrameArgs fa{g, cy, cu, cv, tiles, tile_stride, y, u, v};
-  // grid-stride over 16-pixel runs: 32 workgroups per CU (256 CUs) at most
-  auto grid = [](long long units) {
-    const long long g = (units + 255) / 256;
-    return dim3(static_cast<unsigned>(g < 8192 ? (g > 0 ? g : 1) : 8192));
-  };
+  // grid: (16-pixel-run blocks of one frame, frames); frames beyond 65535 stride
   const long long fr = static_cast<long long>(slots) * frames;
-  hipLaunchKernelGGL(synth_frame_luma, grid(fr * height * ((width + 15) / 16)), dim3(256), 0, s, fa);
-  hipLaunchKernelGGL(synth_frame_chroma, grid(fr * (height / 2) * ((width / 2 + 15) / 16)), dim3(256), 0, s, fa);
+  const unsigned gy = static_cast<unsigned>(fr < 65535 ? fr : 65535);
+  const int lruns = height * ((width + 15) / 16), cruns = (height / 2) * ((width / 2 + 15) / 16);
+  // 8 runs per thread: per-frame setup and workgroup dispatch amortised over 2048 runs
+  hipLaunchKernelGGL(synth_frame_luma, dim3((lruns + 2047) / 2048, gy), dim3(256), 0, s, fa);
+  hipLaunchKernelGGL(synth_frame_chroma, dim3((cruns + 2047) / 2048, gy), dim3(256), 0, s, fa);
   hipFreeAsync(ws, s);
 }
