@@ -8,7 +8,7 @@
 //     decimation, dequantisation and the normative inverse transform, so the
 //     reconstruction written here is exactly what a decoder produces.
 // SURVEY.md K-C8.  One wave64 per macroblock: lanes 0-15 luma 4x4 blocks,
-// lanes 16-23 chroma 4x4 blocks; grid = (nmb, B).
+// lanes 16-23 chroma 4x4 blocks (two MBs per wave, see encode_inter_mb).
 #include "kcommon.h"
 
 namespace mivc {
@@ -34,205 +34,259 @@ struct InterArgs {
   int* intra_count;        // [B]
 };
 
-// x264 decimate_score for a 4x4 block in scan order (start..15)
+// x264 decimate_score of a 4x4 block in scan order (start..15), branch-free: 9 if any
+// |level| > 1, else the sum over non-zero levels of kTab[zeros between it and the
+// previous non-zero level (or `start`)], kTab = {3, 2, 2, 1, 1, 1, 0, ...}.
 __device__ __forceinline__ int decimate_score(const int* scan, int start) {
-  const int tab[16] = {3, 2, 2, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  int idx = 15;
-  while (idx >= start && scan[idx] == 0) --idx;
-  int score = 0;
-  while (idx >= start) {
-    int v = scan[idx--];
-    if (v > 1 || v < -1) return 9;
-    int run = 0;
-    while (idx >= start && scan[idx] == 0) {
-      --idx;
-      ++run;
-    }
-    score += tab[run];
+  int score = 0, last = start - 1;
+  bool big = false;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if (i < start) continue;
+    const int v = scan[i];
+    const bool nzv = v != 0;
+    big |= v > 1 || v < -1;
+    const int run = i - last - 1;
+    const int t = run == 0 ? 3 : (run <= 2 ? 2 : (run <= 5 ? 1 : 0));
+    score += nzv ? t : 0;
+    last = nzv ? i : last;
   }
-  return score;
+  return big ? 9 : score;
 }
 
+// 4 bytes of a reference row starting at byte x (any alignment), from an aligned dword pair
+__device__ __forceinline__ uint32_t ld4(const uint8_t* row, int x) {
+  const int a = x & ~3;
+  const uint32_t w0 = *reinterpret_cast<const uint32_t*>(row + a), w1 = *reinterpret_cast<const uint32_t*>(row + a + 4);
+  return __builtin_amdgcn_alignbyte(w1, w0, x & 3);
+}
+
+// Two macroblocks per wave64 (lanes 0-31 MB 2i, 32-63 MB 2i+1); in each half lanes 0-15
+// code the luma 4x4 blocks (blkIdx order), 16-23 the chroma 4x4 blocks, 24-31 records.
+// Rows move as dwords (prediction, source, reference, reconstruction), levels as
+// 16-byte stores, and the decimation score is branch-free.
 __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
   const Geom& g = a.g;
-  const int mb = blockIdx.x, slot = blockIdx.y;
-  const int mx = mb % g.wmb, my = mb / g.wmb;
-  const int lane = threadIdx.x;
-  const size_t o = static_cast<size_t>(slot) * g.nmb() + mb;
-  const int W = g.W, cw = g.cw();
+  const int lane = threadIdx.x, half = lane >> 5, hl = lane & 31;
+  const int nmb = g.nmb();
+  const int mb = blockIdx.x * 2 + half, slot = blockIdx.y;
+  const bool live = mb < nmb;
+  const int mbc = live ? mb : nmb - 1;
+  const int mx = mbc % g.wmb, my = mbc / g.wmb;
+  const size_t o = static_cast<size_t>(slot) * nmb + mbc;
+  const int W = g.W, cw = g.cw(), CH = g.ch();
   const int qp = a.qp[slot];
   const int qpc = h264::chroma_qp(qp, a.chroma_qp_offset);
 
-  __shared__ int s_score[24];
-  __shared__ int s_cdc[2][4];
-  __shared__ int s_clev[2][4];
-  __shared__ int s_flags[4];  // [0] luma 8x8 keep mask, [1] chroma AC keep mask (bit per comp), [2] cbp
+  __shared__ int s_score[2][24];
+  __shared__ int s_cdc[2][2][4];
+  __shared__ int s_clev[2][2][4];
+  __shared__ int s_flags[2][2];  // [half][0] luma 8x8 keep mask, [1] chroma AC keep mask (bit per comp)
 
   const int mvx = a.mv[o * 2], mvy = a.mv[o * 2 + 1];
   const bool go_intra = a.intra_cost[o] < a.me_cost[o];
   MbHeader* h = a.hdr + o;
   int16_t* coef = a.coef + o * h264::kCoefPerMb;
-  if (go_intra) {
+  if (live && go_intra && hl == 0) {
     // the wavefront kernel encodes this MB closed-loop; leave a consistent placeholder
-    if (lane == 0) {
-      a.intra_flag[o] = 1;
-      atomicAdd(a.intra_count + slot, 1);
-      h->kind = h264::MBK_I16x16;
-    }
-    return;
+    a.intra_flag[o] = 1;
+    atomicAdd(a.intra_count + slot, 1);
+    h->kind = h264::MBK_I16x16;
   }
+  const bool work = live && !go_intra;
 
-  const uint8_t* srcy = a.src_y + slot * g.ysize();
-  const uint8_t* pred = a.pred_y + o * 256;
   int lv[16];     // raster levels of this lane's block
   int res[16];    // residual / reconstruction scratch
-  int pr[16];     // prediction
-  int comp = 0, cb = 0;
+  uint32_t prw[4];  // prediction rows (4 bytes each)
+  const int comp = (hl - 16) >> 2, cb = (hl - 16) & 3;
   const int X0 = mx * 16, Y0 = my * 16;
+  const int lbx = (((hl >> 2) & 1) * 2 + (hl & 1)) * 4, lby = (((hl >> 3) & 1) * 2 + ((hl >> 1) & 1)) * 4;
+  const int cbx = (cb & 1) * 4, cby = (cb >> 1) * 4;
 
-  if (lane < 16) {
-    // ---- luma block (blkIdx order)
-    int bx = h264::kBlkX[lane] * 4, by = h264::kBlkY[lane] * 4;
+  if (work && hl < 16) {
+    // ---- luma block: residual against the ME prediction, forward transform, quantisation
+    const uint8_t* srcy = a.src_y + slot * g.ysize() + static_cast<size_t>(Y0 + lby) * W + X0 + lbx;
+    const uint8_t* pred = a.pred_y + o * 256 + lby * 16 + lbx;
+    uint32_t sw[4];
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      prw[y] = *reinterpret_cast<const uint32_t*>(pred + y * 16);
+      sw[y] = *reinterpret_cast<const uint32_t*>(srcy + static_cast<size_t>(y) * W);
+    }
 #pragma unroll
     for (int y = 0; y < 4; ++y)
 #pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        pr[y * 4 + x] = pred[(by + y) * 16 + bx + x];
-        res[y * 4 + x] = static_cast<int>(srcy[static_cast<size_t>(Y0 + by + y) * W + X0 + bx + x]) - pr[y * 4 + x];
-      }
+      for (int x = 0; x < 4; ++x)
+        res[y * 4 + x] = static_cast<int>(__builtin_amdgcn_ubfe(sw[y], 8 * x, 8)) -
+                         static_cast<int>(__builtin_amdgcn_ubfe(prw[y], 8 * x, 8));
     h264::forward_core4x4(res);
-    int qbits = 15 + qp / 6;
+    const int qbits = 15 + qp / 6;
 #pragma unroll
     for (int r = 0; r < 16; ++r) lv[r] = h264::quant_coef(res[r], h264::kQuantMF[qp % 6][h264::kPosClass[r]], qbits, 11);
     int scan[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) scan[i] = lv[h264::kZigzag4x4[i]];
-    s_score[lane] = decimate_score(scan, 0);
-  } else if (lane < 24) {
-    // ---- chroma block: MC + residual + forward + AC quant; DC handled after exchange
-    comp = (lane - 16) >> 2;
-    cb = (lane - 16) & 3;
+    s_score[half][hl] = decimate_score(scan, 0);
+  } else if (work && hl < 24) {
+    // ---- chroma block: eighth-sample MC (clause 8.4.2.2.2) + residual + forward + AC quant
     const uint8_t* srcc = (comp == 0 ? a.src_u : a.src_v) + slot * g.csize();
     const uint8_t* refc = (comp == 0 ? a.ref_u : a.ref_v) + slot * g.csize();
-    int CH = g.ch();
-    int bx = (cb & 1) * 4, by = (cb >> 1) * 4;
-    int xf = mvx & 7, yf = mvy & 7;
+    const int xf = mvx & 7, yf = mvy & 7;
+    const int px0 = mx * 8 + cbx, py0 = my * 8 + cby;
+    const int xi = px0 + (mvx >> 3), yi = py0 + (mvy >> 3);
+    int rw[5][5];  // reference samples (rows yi..yi+4, cols xi..xi+4), edge-clamped
+    if (xi >= 0 && xi + 8 <= cw && yi >= 0 && yi + 5 <= CH) {
 #pragma unroll
-    for (int y = 0; y < 4; ++y)
+      for (int r = 0; r < 5; ++r) {
+        const uint8_t* row = refc + static_cast<size_t>(yi + r) * cw;
+        const uint32_t w4 = ld4(row, xi), w5 = row[xi + 4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) rw[r][c] = __builtin_amdgcn_ubfe(w4, 8 * c, 8);
+        rw[r][4] = w5;
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 5; ++r) {
+        const uint8_t* row = refc + static_cast<size_t>(clampi(yi + r, 0, CH - 1)) * cw;
+#pragma unroll
+        for (int c = 0; c < 5; ++c) rw[r][c] = row[clampi(xi + c, 0, cw - 1)];
+      }
+    }
+    uint32_t sw[4];
+#pragma unroll
+    for (int y = 0; y < 4; ++y) sw[y] = *reinterpret_cast<const uint32_t*>(srcc + static_cast<size_t>(py0 + y) * cw + px0);
+    const int wA = (8 - xf) * (8 - yf), wB = xf * (8 - yf), wC = (8 - xf) * yf, wD = xf * yf;
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      int pv[4];
 #pragma unroll
       for (int x = 0; x < 4; ++x) {
-        int px = mx * 8 + bx + x, py = my * 8 + by + y;
-        int xi = px + (mvx >> 3), yi = py + (mvy >> 3);
-        int x0 = clampi(xi, 0, cw - 1), x1 = clampi(xi + 1, 0, cw - 1);
-        int y0 = clampi(yi, 0, CH - 1), y1 = clampi(yi + 1, 0, CH - 1);
-        int A = refc[static_cast<size_t>(y0) * cw + x0], B = refc[static_cast<size_t>(y0) * cw + x1];
-        int C = refc[static_cast<size_t>(y1) * cw + x0], D = refc[static_cast<size_t>(y1) * cw + x1];
-        pr[y * 4 + x] = ((8 - xf) * (8 - yf) * A + xf * (8 - yf) * B + (8 - xf) * yf * C + xf * yf * D + 32) >> 6;
-        res[y * 4 + x] = static_cast<int>(srcc[static_cast<size_t>(py) * cw + px]) - pr[y * 4 + x];
+        pv[x] = (wA * rw[y][x] + wB * rw[y][x + 1] + wC * rw[y + 1][x] + wD * rw[y + 1][x + 1] + 32) >> 6;
+        res[y * 4 + x] = static_cast<int>(__builtin_amdgcn_ubfe(sw[y], 8 * x, 8)) - pv[x];
       }
+      prw[y] = pack4_u8(pv);
+    }
     h264::forward_core4x4(res);
-    s_cdc[comp][cb] = res[0];
-    int qbits = 15 + qpc / 6;
+    s_cdc[half][comp][cb] = res[0];
+    const int qbits = 15 + qpc / 6;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) lv[r] = r == 0 ? 0 : h264::quant_coef(res[r], h264::kQuantMF[qpc % 6][h264::kPosClass[r]], qbits, 11);
+    for (int r = 0; r < 16; ++r)
+      lv[r] = r == 0 ? 0 : h264::quant_coef(res[r], h264::kQuantMF[qpc % 6][h264::kPosClass[r]], qbits, 11);
     int scan[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) scan[i] = lv[h264::kZigzag4x4[i]];
-    s_score[lane] = decimate_score(scan, 1);
+    s_score[half][hl] = decimate_score(scan, 1);
   }
-  __syncthreads();
-  if (lane == 16 || lane == 20) {
+  wave_sync();
+  if (work && (hl == 16 || hl == 20)) {
     // chroma DC: 2x2 Hadamard + quantisation with qbits+1
-    int c = lane == 16 ? 0 : 1;
-    int d0 = s_cdc[c][0], d1 = s_cdc[c][1], d2 = s_cdc[c][2], d3 = s_cdc[c][3];
-    int f[4] = {d0 + d1 + d2 + d3, d0 - d1 + d2 - d3, d0 + d1 - d2 - d3, d0 - d1 - d2 + d3};
-    int qbits = 15 + qpc / 6;
+    const int c = hl == 16 ? 0 : 1;
+    const int d0 = s_cdc[half][c][0], d1 = s_cdc[half][c][1], d2 = s_cdc[half][c][2], d3 = s_cdc[half][c][3];
+    const int f[4] = {d0 + d1 + d2 + d3, d0 - d1 + d2 - d3, d0 + d1 - d2 - d3, d0 - d1 - d2 + d3};
+    const int qbits = 15 + qpc / 6;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) s_clev[c][i] = h264::quant_coef(f[i], h264::kQuantMF[qpc % 6][0], qbits + 1, 11);
+    for (int i = 0; i < 4; ++i) s_clev[half][c][i] = h264::quant_coef(f[i], h264::kQuantMF[qpc % 6][0], qbits + 1, 11);
   }
-  if (lane == 0) {
+  if (work && hl == 0) {
     int keep = 0, total = 0;
+#pragma unroll
     for (int b8 = 0; b8 < 4; ++b8) {
-      int s = s_score[b8 * 4] + s_score[b8 * 4 + 1] + s_score[b8 * 4 + 2] + s_score[b8 * 4 + 3];
-      if (s >= 4) keep |= 1 << b8;
-      total += s;
+      const int sc = s_score[half][b8 * 4] + s_score[half][b8 * 4 + 1] + s_score[half][b8 * 4 + 2] +
+                     s_score[half][b8 * 4 + 3];
+      if (sc >= 4) keep |= 1 << b8;
+      total += sc;
     }
     if (total < 6) keep = 0;
     int ckeep = 0;
+#pragma unroll
     for (int c = 0; c < 2; ++c) {
-      int s = s_score[16 + 4 * c] + s_score[17 + 4 * c] + s_score[18 + 4 * c] + s_score[19 + 4 * c];
-      if (s >= 7) ckeep |= 1 << c;
+      const int sc = s_score[half][16 + 4 * c] + s_score[half][17 + 4 * c] + s_score[half][18 + 4 * c] +
+                     s_score[half][19 + 4 * c];
+      if (sc >= 7) ckeep |= 1 << c;
     }
-    s_flags[0] = keep;
-    s_flags[1] = ckeep;
+    s_flags[half][0] = keep;
+    s_flags[half][1] = ckeep;
   }
-  __syncthreads();
-  if (lane < 16) {
-    int b8 = lane >> 2;
-    bool keep = (s_flags[0] >> b8) & 1;
+  wave_sync();
+  if (!work) return;
+  auto store_levels = [](int16_t* dst, const int* v) {  // 16 levels, 16-byte aligned
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = (static_cast<uint32_t>(v[2 * i]) & 0xFFFFu) | (static_cast<uint32_t>(v[2 * i + 1]) << 16);
+    reinterpret_cast<uint4*>(dst)[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    reinterpret_cast<uint4*>(dst)[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  };
+  if (hl < 16) {
+    const bool keep = (s_flags[half][0] >> (hl >> 2)) & 1;
+    int sv[16];
     bool any = false;
-    int16_t* dst = coef + h264::COEF_LUMA + lane * 16;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      int v = keep ? lv[h264::kZigzag4x4[i]] : 0;
-      dst[i] = static_cast<int16_t>(v);
-      any |= v != 0;
+      sv[i] = keep ? lv[h264::kZigzag4x4[i]] : 0;
+      any |= sv[i] != 0;
     }
+    store_levels(coef + h264::COEF_LUMA + hl * 16, sv);
 #pragma unroll
     for (int r = 0; r < 16; ++r) res[r] = keep ? h264::dequant_coef(lv[r], qp, r) : 0;
     if (any) h264::inverse_core4x4(res);
-    int bx = h264::kBlkX[lane] * 4, by = h264::kBlkY[lane] * 4;
-    uint8_t* recy = a.rec_y + slot * g.ysize();
+    uint8_t* recy = a.rec_y + slot * g.ysize() + static_cast<size_t>(Y0 + lby) * W + X0 + lbx;
 #pragma unroll
     for (int y = 0; y < 4; ++y) {
-      uint32_t word = 0;
+      int v4[4];
 #pragma unroll
-      for (int x = 0; x < 4; ++x) word |= static_cast<uint32_t>(h264::clip1(pr[y * 4 + x] + (any ? res[y * 4 + x] : 0))) << (8 * x);
-      *reinterpret_cast<uint32_t*>(recy + static_cast<size_t>(Y0 + by + y) * W + X0 + bx) = word;
+      for (int x = 0; x < 4; ++x)
+        v4[x] = h264::clip1(static_cast<int>(__builtin_amdgcn_ubfe(prw[y], 8 * x, 8)) + (any ? res[y * 4 + x] : 0));
+      *reinterpret_cast<uint32_t*>(recy + static_cast<size_t>(y) * W) = pack4_u8(v4);
     }
-    a.nz[o * 16 + h264::kBlkX[lane] + 4 * h264::kBlkY[lane]] = any;
-  } else if (lane < 24) {
-    bool keep_ac = (s_flags[1] >> comp) & 1;
-    int16_t* dst = coef + h264::COEF_CHROMA_AC + (comp * 4 + cb) * 16;
+    a.nz[o * 16 + (lbx >> 2) + lby] = any;
+  } else if (hl < 24) {
+    const bool keep_ac = (s_flags[half][1] >> comp) & 1;
+    int sv[16];
     bool any_ac = false;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      int v = (keep_ac && i > 0) ? lv[h264::kZigzag4x4[i]] : 0;
-      dst[i] = static_cast<int16_t>(v);
-      any_ac |= v != 0;
+      sv[i] = (keep_ac && i > 0) ? lv[h264::kZigzag4x4[i]] : 0;
+      any_ac |= sv[i] != 0;
     }
-    const int* cl = s_clev[comp];
-    if (cb == 0)
-      for (int i = 0; i < 4; ++i) coef[h264::COEF_CHROMA_DC + comp * 4 + i] = static_cast<int16_t>(cl[i]);
-    int f[4] = {cl[0] + cl[1] + cl[2] + cl[3], cl[0] - cl[1] + cl[2] - cl[3], cl[0] + cl[1] - cl[2] - cl[3],
-                cl[0] - cl[1] - cl[2] + cl[3]};
-    int ls = 16 * h264::kDequantV[qpc % 6][0];
+    store_levels(coef + h264::COEF_CHROMA_AC + (comp * 4 + cb) * 16, sv);
+    const int* cl = s_clev[half][comp];
+    const int f[4] = {cl[0] + cl[1] + cl[2] + cl[3], cl[0] - cl[1] + cl[2] - cl[3], cl[0] + cl[1] - cl[2] - cl[3],
+                      cl[0] - cl[1] - cl[2] + cl[3]};
+    const int ls = 16 * h264::kDequantV[qpc % 6][0];
 #pragma unroll
     for (int r = 0; r < 16; ++r) res[r] = (keep_ac && r > 0) ? h264::dequant_coef(lv[r], qpc, r) : 0;
     res[0] = ((f[cb] * ls) << (qpc / 6)) >> 5;
-    bool any = any_ac || cl[0] || cl[1] || cl[2] || cl[3];
+    const bool any = any_ac || cl[0] || cl[1] || cl[2] || cl[3];
     if (any) h264::inverse_core4x4(res);
-    uint8_t* recc = (comp == 0 ? a.rec_u : a.rec_v) + slot * g.csize();
-    int bx = (cb & 1) * 4, by = (cb >> 1) * 4;
+    uint8_t* recc = (comp == 0 ? a.rec_u : a.rec_v) + slot * g.csize() + static_cast<size_t>(my * 8 + cby) * cw + mx * 8 + cbx;
 #pragma unroll
     for (int y = 0; y < 4; ++y) {
-      uint32_t word = 0;
+      int v4[4];
 #pragma unroll
-      for (int x = 0; x < 4; ++x) word |= static_cast<uint32_t>(h264::clip1(pr[y * 4 + x] + (any ? res[y * 4 + x] : 0))) << (8 * x);
-      *reinterpret_cast<uint32_t*>(recc + static_cast<size_t>(my * 8 + by + y) * cw + mx * 8 + bx) = word;
+      for (int x = 0; x < 4; ++x)
+        v4[x] = h264::clip1(static_cast<int>(__builtin_amdgcn_ubfe(prw[y], 8 * x, 8)) + (any ? res[y * 4 + x] : 0));
+      *reinterpret_cast<uint32_t*>(recc + static_cast<size_t>(y) * cw) = pack4_u8(v4);
     }
-  } else if (lane < 40) {
-    coef[h264::COEF_LUMA_DC + (lane - 24)] = 0;
-  } else if (lane == 40) {
+  } else if (hl == 24) {
+    // chroma DC levels (Cb then Cr, 8 x int16 = 16 bytes at COEF_CHROMA_DC)
+    const int* c0 = s_clev[half][0];
+    const int* c1 = s_clev[half][1];
+    auto p2 = [](int lo, int hi) { return (static_cast<uint32_t>(lo) & 0xFFFFu) | (static_cast<uint32_t>(hi) << 16); };
+    *reinterpret_cast<uint4*>(coef + h264::COEF_CHROMA_DC) = make_uint4(p2(c0[0], c0[1]), p2(c0[2], c0[3]),
+                                                                        p2(c1[0], c1[1]), p2(c1[2], c1[3]));
+  } else if (hl == 25 || hl == 26) {
+    // luma DC (unused for P16x16): zero
+    reinterpret_cast<uint4*>(coef + h264::COEF_LUMA_DC)[hl - 25] = make_uint4(0, 0, 0, 0);
+  } else if (hl == 27) {
     h->kind = h264::MBK_P16x16;
     h->qp = static_cast<int8_t>(qp);
     h->i16_mode = 0;
     h->chroma_mode = 0;
     h->flags = 0;
-    for (int q = 0; q < 4; ++q) {
-      h->mv[q][0] = static_cast<int16_t>(mvx);
-      h->mv[q][1] = static_cast<int16_t>(mvy);
-    }
+    const uint32_t mvw = (static_cast<uint32_t>(mvx) & 0xFFFFu) | (static_cast<uint32_t>(mvy) << 16);
+    uint2* mvp = reinterpret_cast<uint2*>(&h->mv[0][0]);  // 8-byte aligned
+    mvp[0] = make_uint2(mvw, mvw);
+    mvp[1] = make_uint2(mvw, mvw);
     a.intra_flag[o] = 0;
   }
 }
@@ -271,5 +325,5 @@ extern "C" void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t*
   a.nz = nz;
   a.intra_flag = intra_flag;
   a.intra_count = intra_count;
-  hipLaunchKernelGGL(encode_inter_mb, dim3(wmb * hmb, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
+  hipLaunchKernelGGL(encode_inter_mb, dim3((wmb * hmb + 1) / 2, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
 }
