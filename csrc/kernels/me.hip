@@ -49,9 +49,13 @@ constexpr int kML = 4;                                   // window margin left/t
 constexpr int kMR = 6;                                   // margin right/bottom
 constexpr int kWinPitch = 17;                            // words per LDS row (odd: bank spread)
 
-// quarter-sample position (xf, yf) -> two LDS offsets into the plane block P[4][20*20]
-// (plane 0 = G integer, 1 = b half-x, 2 = h half-y, 3 = j centre); sample = (A + B + 1) >> 1
-#define QO(p, du, dv) ((p) * 400 + (dv) * 20 + (du))
+// quarter-sample position (xf, yf) -> two LDS offsets into the plane block P[4][20 rows x
+// kPP bytes] (plane 0 = G integer, 1 = b half-x, 2 = h half-y, 3 = j centre); sample =
+// (A + B + 1) >> 1.  Plane rows are staged as aligned words (kPP = 24 bytes), so a
+// plane sample (u, v) sits at byte v * kPP + u + sh, sh = the region's misalignment.
+constexpr int kPP = 24;
+constexpr int kPlane = 20 * kPP;
+#define QO(p, du, dv) ((p) * kPlane + (dv) * kPP + (du))
 __constant__ short kQOff[16][2] = {
     {QO(0, 0, 0), QO(0, 0, 0)}, {QO(0, 0, 0), QO(1, 0, 0)}, {QO(1, 0, 0), QO(1, 0, 0)}, {QO(0, 1, 0), QO(1, 0, 0)},
     {QO(0, 0, 0), QO(2, 0, 0)}, {QO(1, 0, 0), QO(2, 0, 0)}, {QO(3, 0, 0), QO(1, 0, 0)}, {QO(1, 0, 0), QO(2, 1, 0)},
@@ -80,10 +84,12 @@ template <int MAXR>
 struct MeShared {
   static constexpr int kRows = 16 + 2 * MAXR + kML + kMR;
   static constexpr int kLoads = (kRows * 16 + 63) / 64;  // window words per lane (16 words per row at most)
-  uint32_t win[kRows * kWinPitch];         // reference window, aligned words
+  union {                                  // the window is dead once the sub-pel planes are staged
+    uint32_t win[kRows * kWinPitch];       // reference window, aligned words
+    uint32_t P32[4 * kPlane / 4 + 4];      // G, b, h, j planes (20 rows x kPP bytes each) + pad
+  };
   alignas(16) uint32_t src[64];            // source MB (16 rows x 4 words)
   int nb[36];                              // source intra neighbours: top[16], left[16], tl
-  uint32_t P32[404];                       // G, b, h, j planes (20x20 bytes each) + pad
   short qoff[32];                          // kQOff copy (lane-varying index -> LDS, not constant)
 };
 
@@ -352,12 +358,68 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   S.src[lane] = my_src;
   if (lane < 33) S.nb[lane] = nbv;
   if (lane < 32) S.qoff[lane] = kQOff[lane >> 1][lane & 1];
+  wave_sync();
+  // this lane's 4x4 source block (lane & 15) for the SATDs below
+  const int blk = lane & 15;
+  const int px0 = (blk & 3) * 4, py0 = (blk >> 2) * 4;
+  uint32_t srow[4];
+#pragma unroll
+  for (int y = 0; y < 4; ++y) srow[y] = S.src[(py0 + y) * 4 + (px0 >> 2)];
+  // ---- open-loop Intra16x16 estimate on source pixels: lane = mode * 16 + block.  Runs
+  // while the candidate reference loads are in flight (it needs only the source MB).
+  // Every mode is written as pred(x, y) = clip((K + CX[x] + RY[y]) >> 5) with per-lane
+  // K, CX, RY (V: CX = 32 top, H: RY = 32 left, DC: K = 32 dc + 16, plane: the linear
+  // form); the neighbour sums behind DC and plane are row reductions of the neighbour
+  // registers (H = sum (t - 7) top[t] - 8 tl, V alike).
+  int intra_key;
+  {
+    const int mode = lane >> 4;
+    const bool has_top = my > 0, has_left = mx > 0;
+    const bool ok = (mode == 0 && has_top) || (mode == 1 && has_left) || mode == 2 || (mode == 3 && has_top && has_left);
+    const int pk = sum16(lane < 32 ? nbv * ((lane & 15) - 7) + (nbv << 16) : 0);  // weighted + 65536 * plain
+    const int ptop = __builtin_amdgcn_readlane(pk, 0), pleft = __builtin_amdgcn_readlane(pk, 16);
+    const int tl = __builtin_amdgcn_readlane(nbv, 32);
+    const int st = (ptop + 32768) >> 16, sl = (pleft + 32768) >> 16;
+    const int Hs = ptop - st * 65536 - 8 * tl, Vs = pleft - sl * 65536 - 8 * tl;
+    const int pa = 16 * (__builtin_amdgcn_readlane(nbv, 31) + __builtin_amdgcn_readlane(nbv, 15));
+    const int pb = (5 * Hs + 32) >> 6, pc = (5 * Vs + 32) >> 6;
+    const int dc = (has_top && has_left) ? (st + sl + 16) >> 5 : (has_left ? (sl + 8) >> 4 : (has_top ? (st + 8) >> 4 : 128));
+    const int bx4 = px0, by4 = py0;
+    const int4 top4 = *reinterpret_cast<const int4*>(S.nb + bx4);
+    const int4 left4 = *reinterpret_cast<const int4*>(S.nb + 16 + by4);
+    const int tv[4] = {top4.x, top4.y, top4.z, top4.w}, lv4[4] = {left4.x, left4.y, left4.z, left4.w};
+    const int K = mode == 2 ? 32 * dc + 16 : (mode == 3 ? pa + pb * (bx4 - 7) + pc * (by4 - 7) + 16 : 16);
+    int r[16];
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      const int ry = mode == 1 ? 32 * lv4[y] : (mode == 3 ? pc * y : 0);
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const int cxv = mode == 0 ? 32 * tv[x] : (mode == 3 ? pb * x : 0);
+        const int pv = clampi((K + cxv + ry) >> 5, 0, 255);
+        r[y * 4 + x] = static_cast<int>(__builtin_amdgcn_ubfe(srow[y], 8 * x, 8)) - pv;
+      }
+    }
+    const int sv = sum16(h264::satd4x4(r));
+    intra_key = min64(ok ? sv : 0x3FFFFFFF);
+  }
   int cx = 0, cy = 0;
   {
+    // per-lane SADs are <= 1020, so two candidates share one wave reduction (16-bit halves)
+    int csad[5];
+    {
+      const uint32_t p01 = static_cast<uint32_t>(wave_sum(static_cast<int>(sad4(my_src, cref[0], 0) | (sad4(my_src, cref[1], 0) << 16))));
+      const uint32_t p23 = static_cast<uint32_t>(wave_sum(static_cast<int>(sad4(my_src, cref[2], 0) | (sad4(my_src, cref[3], 0) << 16))));
+      csad[0] = p01 & 0xFFFFu;
+      csad[1] = p01 >> 16;
+      csad[2] = p23 & 0xFFFFu;
+      csad[3] = p23 >> 16;
+      csad[4] = wave_sum(static_cast<int>(sad4(my_src, cref[4], 0)));
+    }
     int best = 0x7FFFFFFF;
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
-      int sad = wave_sum(static_cast<int>(sad4(my_src, cref[k], 0)));
+      int sad = csad[k];
       int cost = sad + lambda * (mvbits(cand_x[k] * 4 - pmx) + mvbits(cand_y[k] * 4 - pmy));
       if (cost < best) {
         best = cost;
@@ -438,46 +500,50 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
     const int PW = W + 2 * kHpM, PH = H + 2 * kHpM;
     const uint8_t* hp = a.hp + static_cast<size_t>(slot) * 3 * PW * PH;
     const int x0 = X0 + bx - 2, y0 = Y0 + by - 2;  // frame coordinates of P(0, 0)
-    const bool xin = x0 >= -kHpM && x0 + 20 <= W + kHpM;
-    // 4 planes (G from the reference itself, b / h / j from hp) x 20 rows x 5 words =
-    // 400 words, one batch of loads; lane item i -> (plane, row, word)
-    const bool gin = x0 >= 0 && x0 + 20 <= W;
-    uint32_t v[7];
+    // aligned words covering bytes x0 .. x0 + 19 of every row: 6 per row from xa = x0 & ~3
+    const int xa = x0 & ~3;
+    const bool gin = xa >= 0 && xa + kPP <= W;                      // reference row, no clamping
+    const bool xin = xa + kHpM >= 0 && xa + kHpM + kPP <= PW;       // half-sample plane row
+    // 4 planes (G from the reference itself, b / h / j from hp) x 20 rows x 6 words =
+    // 480 words, one batch of loads; lane item i -> (plane, row, word)
+    uint32_t v[8];
 #pragma unroll
-    for (int k = 0; k < 7; ++k) {
+    for (int k = 0; k < 8; ++k) {
       const int i = lane + 64 * k;
-      const int pl = i / 100, rem = i - pl * 100, r = rem / 5, w = rem - r * 5;
+      const int pl = i / 120, rem = i - pl * 120, r = rem / 6, w = rem - r * 6;
       uint32_t word = 0;
-      if (i < 400) {
+      if (i < 480) {
         if (pl == 0) {
           const uint8_t* row = ref + static_cast<size_t>(clampi(y0 + r, 0, H - 1)) * W;
           if (gin) {
-            word = load4u(row, x0 + 4 * w);
+            word = *reinterpret_cast<const uint32_t*>(row + xa + 4 * w);
           } else {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) word |= static_cast<uint32_t>(row[clampi(x0 + 4 * w + q, 0, W - 1)]) << (8 * q);
+            for (int q = 0; q < 4; ++q) word |= static_cast<uint32_t>(row[clampi(xa + 4 * w + q, 0, W - 1)]) << (8 * q);
           }
         } else {
           const int yy = clampi(y0 + r, -kHpM, H + kHpM - 1) + kHpM;
           const uint8_t* row = hp + static_cast<size_t>(pl - 1) * PW * PH + static_cast<size_t>(yy) * PW;
           if (xin) {
-            word = load4u(row, x0 + kHpM + 4 * w);
+            word = *reinterpret_cast<const uint32_t*>(row + xa + kHpM + 4 * w);
           } else {
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-              word |= static_cast<uint32_t>(row[clampi(x0 + 4 * w + q, -kHpM, W + kHpM - 1) + kHpM]) << (8 * q);
+              word |= static_cast<uint32_t>(row[clampi(xa + 4 * w + q, -kHpM, W + kHpM - 1) + kHpM]) << (8 * q);
           }
         }
       }
       v[k] = word;
     }
+    wave_sync();  // last window reads (integer search) before the planes overwrite it
 #pragma unroll
-    for (int k = 0; k < 7; ++k) {
+    for (int k = 0; k < 8; ++k) {
       const int i = lane + 64 * k;
-      if (i < 400) S.P32[i] = v[k];  // plane p starts at word 100 * p; rows of 5 words
+      if (i < 480) S.P32[i] = v[k];  // plane p starts at word 120 * p; rows of 6 words
     }
   }
-  if (lane < 4) S.P32[400 + lane] = 0;
+  if (lane < 4) S.P32[4 * kPlane / 4 + lane] = 0;
+  const int psh = (X0 + bx - 2) & 3;  // misalignment of the staged plane rows
   __syncthreads();
 
   MPROF(4);
@@ -488,16 +554,10 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   };
   // 4 predicted samples of a row starting at plane coords (u, v) (G(u,v) = pixel (bx-2+u, by-2+v))
   auto pred4 = [&](int u, int v, int offa, int offb) -> uint32_t {
-    const int base = v * 20 + u;
+    const int base = v * kPP + u + psh;
     return avg4(load4(base + offa), load4(base + offb));
   };
-  const uint8_t* srcb = reinterpret_cast<const uint8_t*>(S.src);
   // SATD of candidate (dqx, dqy) quarter offsets relative to (4bx, 4by): this lane does 4x4 block (lane&15)
-  const int blk = lane & 15;
-  const int px0 = (blk & 3) * 4, py0 = (blk >> 2) * 4;
-  uint32_t srow[4];
-#pragma unroll
-  for (int y = 0; y < 4; ++y) srow[y] = S.src[(py0 + y) * 4 + (px0 >> 2)];
   auto satd_cand = [&](int dqx, int dqy) -> int {
     int q = (dqy & 3) * 4 + (dqx & 3), ox = dqx >> 2, oy = dqy >> 2;
     int offa = S.qoff[2 * q], offb = S.qoff[2 * q + 1];
@@ -570,38 +630,11 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
     reinterpret_cast<uint32_t*>(a.out_pred + o * 256)[lane] = pred4(c4 + ox + 2, r4 + oy + 2, offa, offb);
   }
   MPROF(8);
-  // ---- phase 5: open-loop Intra16x16 estimate on source pixels: lane = mode * 16 + block
-  {
-    int mode = lane >> 4, blk = lane & 15;
-    bool has_top = my > 0, has_left = mx > 0;
-    bool ok = (mode == 0 && has_top) || (mode == 1 && has_left) || mode == 2 || (mode == 3 && has_top && has_left);
-    const int* top = S.nb;
-    const int* left = S.nb + 16;
-    int tl = S.nb[32];
-    int pa = 0, pb = 0, pc = 0, dc = 0;
-    if (mode == 3 && ok) h264::i16_plane_params(top, left, tl, &pa, &pb, &pc);
-    if (mode == 2) dc = h264::i16_dc(top, left, (has_top ? h264::AV_TOP : 0) | (has_left ? h264::AV_LEFT : 0));
-    int bx4 = (blk & 3) * 4, by4 = (blk >> 2) * 4;
-    int r[16];
-#pragma unroll
-    for (int y = 0; y < 4; ++y)
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        int X = bx4 + x, Y = by4 + y, pv;
-        if (mode == 0) pv = top[X];
-        else if (mode == 1) pv = left[Y];
-        else if (mode == 2) pv = dc;
-        else pv = h264::clip1((pa + pb * (X - 7) + pc * (Y - 7) + 16) >> 5);
-        r[y * 4 + x] = static_cast<int>(srcb[Y * 16 + X]) - pv;
-      }
-    int s = sum16(h264::satd4x4(r));
-    int key = min64(ok ? s : 0x3FFFFFFF);
-    if (lane == 0) {
-      a.out_mv[o * 2] = static_cast<int16_t>(best_mvx);
-      a.out_mv[o * 2 + 1] = static_cast<int16_t>(best_mvy);
-      a.out_cost[o] = best_cost;
-      a.out_intra_cost[o] = key + lambda * 4;
-    }
+  if (lane == 0) {
+    a.out_mv[o * 2] = static_cast<int16_t>(best_mvx);
+    a.out_mv[o * 2 + 1] = static_cast<int16_t>(best_mvy);
+    a.out_cost[o] = best_cost;
+    a.out_intra_cost[o] = intra_key + lambda * 4;
   }
   MPROF(9);
 }
