@@ -57,7 +57,7 @@ size_t mivc_cavlc_mb_bytes();
 void mivc_launch_cavlc(int B, int wmb, int hmb, const void* hdr, const int16_t* coef, void* mbs, int* len,
                        long long* off, int* trail, long long* total_bits, int* slot_bytes, uint32_t* words,
                        long long cap_words, const uint32_t* hdr_bits, const int* hdr_nbits, int pslice, int slice_qp,
-                       const int* slot_qp, uint8_t* out, long long* out_off, void* stream);
+                       const int* slot_qp, uint8_t* out, long long* out_off, const uint8_t* nz, void* stream);
 void mivc_launch_sse(int B, int W, int H, int w, int h, const uint8_t* sy, const uint8_t* su, const uint8_t* sv,
                      const uint8_t* ry, const uint8_t* ru, const uint8_t* rv, unsigned long long* sse,
                      float* ssim_sum, void* stream);
@@ -185,12 +185,15 @@ PYBIND11_MODULE(_hip, m) {
   m.def("cavlc", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t coef, uintptr_t mbs, uintptr_t len, uintptr_t off,
                     uintptr_t trail, uintptr_t total_bits, uintptr_t slot_bytes, uintptr_t words, long long cap_words,
                     uintptr_t hdr_bits, uintptr_t hdr_nbits, int pslice, int slice_qp, uintptr_t slot_qp,
-                    uintptr_t out, uintptr_t out_off, uintptr_t stream) {
+                    uintptr_t out, uintptr_t out_off, uintptr_t stream, uintptr_t nz) {
     mivc_launch_cavlc(B, wmb, hmb, P<void>(hdr), P<int16_t>(coef), P<void>(mbs), P<int>(len), P<long long>(off),
                       P<int>(trail), P<long long>(total_bits), P<int>(slot_bytes), P<uint32_t>(words), cap_words,
                       P<uint32_t>(hdr_bits), P<int>(hdr_nbits), pslice, slice_qp, P<int>(slot_qp), P<uint8_t>(out),
-                      P<long long>(out_off), S(stream));
-  });
+                      P<long long>(out_off), P<uint8_t>(nz), S(stream));
+  }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("hdr"), py::arg("coef"), py::arg("mbs"), py::arg("len"),
+     py::arg("off"), py::arg("trail"), py::arg("total_bits"), py::arg("slot_bytes"), py::arg("words"),
+     py::arg("cap_words"), py::arg("hdr_bits"), py::arg("hdr_nbits"), py::arg("pslice"), py::arg("slice_qp"),
+     py::arg("slot_qp"), py::arg("out"), py::arg("out_off"), py::arg("stream"), py::arg("nz") = 0);
   m.def("sse", [](int B, int W, int H, int w, int h, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t ry,
                   uintptr_t ru, uintptr_t rv, uintptr_t sse, uintptr_t ssim, uintptr_t stream) {
     mivc_launch_sse(B, W, H, w, h, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), P<uint8_t>(ry), P<uint8_t>(ru),

@@ -62,6 +62,8 @@ struct CavlcArgs {
   const int* slot_qp;    // [B] per-slot slice QP (null: slice_qp for every slot)
   uint8_t* out;          // compacted bytes
   long long* out_off;    // [B] byte offset of every slot in `out`
+  const uint8_t* nz;     // [B, nmb, 16] raster luma non-zero flags from the encoder (nullable):
+                         // all-zero blocks of inter MBs are not loaded
 };
 
 // ---------------------------------------------------------------- bit sinks
@@ -455,7 +457,11 @@ __device__ __forceinline__ void mb_block_bits(S& s, int slotid, const CavlcMb* m
   } else if (slotid < 18) {
     int blk = slotid - 2;
     if (!(cl & (1 << (blk >> 2)))) return;
-    load16(c + h264::COEF_LUMA + blk * 16, v);
+    if (m.tc[blk]) load16(c + h264::COEF_LUMA + blk * 16, v);  // TotalCoeff 0: no load
+    else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = 0;
+    }
     int nc = nc_luma(mbs, base, wmb, mx, my, m.tc, h264::kBlkX[blk], h264::kBlkY[blk]);
     if (m.kind == h264::MBK_I16x16) cavlc_block(s, v, 1, 15, 15, nc);
     else cavlc_block(s, v, 0, 15, 16, nc);
@@ -473,7 +479,11 @@ __device__ __forceinline__ void mb_block_bits(S& s, int slotid, const CavlcMb* m
   } else if (slotid < 28) {
     if (!(cc & 2)) return;
     int k = slotid - 20, comp = k >> 2, b = k & 3;
-    load16(c + h264::COEF_CHROMA_AC + k * 16, v);
+    if (m.tc[16 + k]) load16(c + h264::COEF_CHROMA_AC + k * 16, v);
+    else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = 0;
+    }
     cavlc_block(s, v, 1, 15, 15, nc_chroma(mbs, base, wmb, mx, my, m.tc, comp, b & 1, b >> 1));
   }
 }
@@ -604,8 +614,9 @@ extern "C" void mivc_launch_cavlc(int B, int wmb, int hmb, const void* hdr, cons
                                   long long* off, int* trail, long long* total_bits, int* slot_bytes, uint32_t* words,
                                   long long cap_words, const uint32_t* hdr_bits, const int* hdr_nbits, int pslice,
                                   int slice_qp, const int* slot_qp, uint8_t* out, long long* out_off,
-                                  void* stream) {
+                                  const uint8_t* nz, void* stream) {
   CavlcArgs a;
+  a.nz = nz;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.hdr = static_cast<const mivc::h264::MbHeader*>(hdr);
   a.coef = coef;

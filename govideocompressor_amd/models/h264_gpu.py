@@ -51,6 +51,9 @@ class H264Params:
     # CRF per-frame QPs from the GPU lookahead (rc/lookahead.py); False = flat CRF QP
     lookahead: bool = True
     la_range: int = 6
+    # x264 --scenecut: a P frame whose lowres inter cost saves less than this percent of
+    # its intra cost is coded all-intra (I4x4/I16x16 MBs) at the I-frame QP; 0 disables
+    scenecut: int = 40
 
     def host_cfg(self) -> dict:
         return dict(width=self.width, height=self.height, fps=self.fps, qp=self.qp,
@@ -203,7 +206,9 @@ class GpuH264Encoder:
                       self._ptr(self.src[0]), self._ptr(self.src[1]), self._ptr(self.src[2]),
                       self.p.width, self.p.height, self.W, self.H, self._stream())
 
-    def _encode_frame(self, idr: bool, cur, ref, hdr, coef):
+    def _encode_frame(self, idr: bool, cur, ref, hdr, coef, cut=None):
+        """cut: optional [B] bool device tensor -- slots whose frame is a scene cut (every MB
+        intra, as an I picture would be)."""
         s = self._stream()
         B, wmb, hmb = self.B, self.wmb, self.hmb
         sy, su, sv = (self._ptr(x) for x in self.src)
@@ -214,6 +219,8 @@ class GpuH264Encoder:
             self.hip.me(B, wmb, hmb, sy, fy, self._ptr(self.prev_mv), self._ptr(self.mv), self._ptr(self.me_cost),
                         self._ptr(self.pred), self._ptr(self.intra_cost), self._ptr(self.qp),
                         self.p.me_range, self.p.subpel, s, self._ptr(self.me_hp))
+            if cut is not None:
+                self.intra_cost.masked_fill_(cut[:, None], -1)  # intra beats any inter cost
             self.hip.encode_inter(B, wmb, hmb, sy, su, sv, fy, fu, fv, ry, ru, rv, self._ptr(self.pred),
                                   self._ptr(self.mv), self._ptr(self.me_cost), self._ptr(self.intra_cost),
                                   self._ptr(self.qp), self.p.chroma_qp_offset, self._ptr(hdr), self._ptr(coef),
@@ -226,7 +233,8 @@ class GpuH264Encoder:
             flag_ptr, count_ptr = 0, 0
         self.hip.encode_intra(B, wmb, hmb, sy, su, sv, ry, ru, rv, self._ptr(self.qp), self.p.chroma_qp_offset,
                               self._ptr(hdr), self._ptr(coef), self._ptr(self.nz), flag_ptr, count_ptr,
-                              self._ptr(self.err), int(self.p.i4x4 and (idr or self.p.i4x4_in_p)), s)
+                              self._ptr(self.err),
+                              int(self.p.i4x4 and (idr or self.p.i4x4_in_p or cut is not None)), s)
         if self.p.deblock:
             self.hip.deblock(B, wmb, hmb, ry, ru, rv, self._ptr(hdr), self._ptr(self.nz), self.p.chroma_qp_offset,
                              0, 0, self._ptr(self.err), s)
@@ -257,7 +265,7 @@ class GpuH264Encoder:
                        P(self.cav_off), P(self.cav_trail), P(self.cav_total), P(self.cav_sizes[k]),
                        P(self.cav_words), self.cap_words, P(self.cav_hdr_bits[k]), P(self.cav_hdr_nbits[k]),
                        0 if idr else 1, int(qps_t[0]), P(self.qp), P(self.cav_out[k]), P(self.cav_out_off),
-                       self._stream())
+                       self._stream(), P(self.nz))
 
     def _copy_out(self, t: int, k: int, idr: bool, copied, wrap_futs):
         """Copy thread (frames in order): sizes -> compressed bytes D2H, then hand the NAL
@@ -320,7 +328,10 @@ class GpuH264Encoder:
         t0 = time.perf_counter()
         costs = self._la.frame_costs(y).cpu().numpy()
         lbw, lbh = GpuLookahead.block_grid(y.shape[3], y.shape[2])
-        q = crf_qps_batch(costs, float(self.p.crf), lbw * lbh)
+        from ..rc.ratecontrol import scenecut_flags
+        self._scenecuts = scenecut_flags(costs, float(self.p.scenecut))
+        q = crf_qps_batch(costs, float(self.p.crf), lbw * lbh, scenecuts=self._scenecuts)
+        self.stats["scenecuts"] = int(self._scenecuts.sum())
         self.timings["lookahead_s"] = self.timings.get("lookahead_s", 0.0) + time.perf_counter() - t0
         self.stats["mean_qp"] = float(q.mean())
         return q
@@ -354,8 +365,11 @@ class GpuH264Encoder:
             raise ValueError("idr_ids needs one entry per slot")
         torch.cuda.set_device(self.dev)
         qp_i, qp_p = self.p.frame_qps()
+        self._scenecuts = None
         if qps is None and self.p.crf is not None and self.p.lookahead:
             qps = self.crf_qps(y)
+        cuts_h = self._scenecuts if self._scenecuts is not None else np.zeros((B, F), dtype=bool)
+        cuts_d = torch.from_numpy(np.ascontiguousarray(cuts_h.T)).to(self.dev)  # [F, B]
         if qps is None:
             qps_h = np.full((B, F), qp_p, dtype=np.int32)
             qps_h[:, 0] = qp_i
@@ -394,7 +408,8 @@ class GpuH264Encoder:
             cur, ref = self.rec[k], self.rec[1 - k]
             self._prep(y, u, v, t)
             self.qp.copy_(qps_d[t])
-            self._encode_frame(idr, cur, ref, self.hdr[k], self.coef[k])
+            self._encode_frame(idr, cur, ref, self.hdr[k], self.coef[k],
+                               cuts_d[t] if (not idr and cuts_h[:, t].any()) else None)
             if metrics:
                 self.hip.sse(B, self.W, self.H, self.p.width, self.p.height, self._ptr(self.src[0]),
                              self._ptr(self.src[1]), self._ptr(self.src[2]), self._ptr(cur[0]), self._ptr(cur[1]),

@@ -95,19 +95,44 @@ def crf_qps(intra: np.ndarray, inter: np.ndarray, crf: float, mb_count: int, key
     return np.array([clamp_qp(q) for q in qp], dtype=np.int32)
 
 
+def scenecut_flags(costs: np.ndarray, scenecut: float = 40.0, keyint: int | None = None) -> np.ndarray:
+    """[B, F] scene-cut decisions from lowres frame costs (x264 ``--scenecut``, default 40).
+
+    Frame t of a segment is a scene cut when motion compensation from t - 1 saves less
+    than ``scenecut`` percent of its intra cost: ``cost_best >= (1 - scenecut / 100) *
+    cost_intra`` with ``cost_best = sum of per-block min(intra, inter)`` (x264 compares the
+    P cost with the I cost of the candidate frame the same way, slicetype.c
+    ``scenecut_internal``).  Key frames (frame 0, every ``keyint``-th) are not flagged:
+    they are intra already.  ``scenecut <= 0`` disables detection."""
+    c = np.asarray(costs, dtype=np.float64)
+    B, F = c.shape[0], c.shape[1]
+    flags = np.zeros((B, F), dtype=bool)
+    if scenecut <= 0 or F < 2:
+        return flags
+    intra, best = c[:, :, 0], c[:, :, 1]
+    flags = best >= (1.0 - scenecut / 100.0) * np.maximum(intra, 1.0)
+    g = keyint if keyint and keyint > 0 else F
+    flags[:, ::g] = False
+    return flags
+
+
 def crf_qps_batch(costs: np.ndarray, crf: float, mb_count: int, keyint: int | None = None, blur: float = 0.5,
-                  qp_min: int = QP_MIN, qp_max: int = QP_MAX) -> np.ndarray:
+                  qp_min: int = QP_MIN, qp_max: int = QP_MAX, scenecuts: np.ndarray | None = None) -> np.ndarray:
     """:func:`crf_qps` for B closed-GOP segments at once.
 
     ``costs``: [B, F, 2] lowres frame costs (intra, min(intra, inter)) as produced by
     :class:`~govideocompressor_amd.rc.lookahead.GpuLookahead`; frame 0 of each segment
-    is the IDR (intra complexity, QP - IP_OFFSET), and so is every ``keyint``-th frame.
+    is the IDR (intra complexity, QP - IP_OFFSET), and so is every ``keyint``-th frame and
+    every frame flagged in ``scenecuts`` ([B, F] bool, see :func:`scenecut_flags`).
     Returns [B, F] int32 QPs."""
     c = np.asarray(costs, dtype=np.float64)
     B, F = c.shape[0], c.shape[1]
     g = keyint if keyint and keyint > 0 else F
-    cplx = np.maximum(c[:, :, 1].copy(), 1.0)
-    cplx[:, ::g] = np.maximum(c[:, ::g, 0], 1.0)
+    key = np.zeros((B, F), dtype=bool)
+    key[:, ::g] = True
+    if scenecuts is not None:
+        key |= np.asarray(scenecuts, dtype=bool)
+    cplx = np.maximum(np.where(key, c[:, :, 0], c[:, :, 1]), 1.0)
     blurred = np.empty_like(cplx)
     acc = np.zeros(B)
     wsum = 0.0
@@ -119,7 +144,7 @@ def crf_qps_batch(costs: np.ndarray, crf: float, mb_count: int, keyint: int | No
     rate_factor = base ** (1.0 - QCOMP) / qp2qscale(crf)
     qs = np.maximum(blurred ** (1.0 - QCOMP) / rate_factor, 1e-9)
     qp = 12.0 + 6.0 * np.log2(qs / 0.85)
-    qp[:, ::g] -= IP_OFFSET
+    qp[key] -= IP_OFFSET
     return np.clip(np.round(qp), max(QP_MIN, qp_min), min(QP_MAX, qp_max)).astype(np.int32)
 
 

@@ -93,3 +93,28 @@ def test_gpu_per_frame_qps(host):
         pics = host.decode(out["gpu"][b])
         assert [int(np.median(p["mb_qp"])) for p in pics] == qps[b].tolist()
     torch.cuda.synchronize()
+
+
+def test_gpu_scenecut_codes_cut_frames_intra(host):
+    """A hard cut inside a segment: the lookahead flags it (x264 --scenecut 40), the frame
+    is coded with every MB intra at the I-frame QP, and the recon still roundtrips."""
+    import numpy as np
+    import torch
+    from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
+
+    w, h, B, F, cut = 176, 144, 2, 6, 3
+    a = synth_clip(B, F, w, h, seed=2)
+    b = synth_clip(B, F, w, h, seed=77)
+    y, u, v = (torch.cat([pa[:, :cut], pb[:, cut:]], dim=1).contiguous() for pa, pb in zip(a, b))
+    enc = GpuH264Encoder(H264Params(width=w, height=h), slots=B)
+    res = enc.encode(y, u, v, keep_recon=True)
+    torch.cuda.synchronize()
+    assert enc._scenecuts[:, cut].all() and enc.stats["scenecuts"] >= B
+    _check_roundtrip(host, enc, res, w, h)
+    for r in res:
+        pics = host.decode(r.bitstream)
+        kinds = np.asarray(pics[cut]["mb_kind"])
+        assert np.isin(kinds, [0, 1, 4]).all()          # I4x4 / I16x16 / I_PCM only
+        assert np.isin(np.asarray(pics[cut + 1]["mb_kind"]), [2, 3, 5, 6, 7]).mean() > 0.5
+        assert r.psnr_y > 30
+    enc.close()

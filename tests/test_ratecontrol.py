@@ -41,3 +41,19 @@ def test_global_stats_single_process():
     g.put(3, 2 * np.ones((3, 4)))
     t = g.reduce()
     assert t[:, 0].tolist() == [1, 1, 1, 2, 2, 2]
+
+
+def test_scenecut_flags_and_keyframe_qps():
+    B, F = 2, 6
+    costs = np.zeros((B, F, 2))
+    costs[:, :, 0] = 1000.0          # intra cost
+    costs[:, :, 1] = 200.0           # inter predicts well ...
+    costs[0, 3, 1] = 950.0           # ... except at a cut in slot 0, frame 3
+    costs[1, 0, 1] = 1000.0          # frame 0 is a key frame anyway: never flagged
+    f = rc.scenecut_flags(costs, 40.0)
+    assert f.tolist() == [[False, False, False, True, False, False], [False] * 6]
+    assert not rc.scenecut_flags(costs, 0.0).any()
+    q = rc.crf_qps_batch(costs, 23.0, 100, scenecuts=f)
+    q0 = rc.crf_qps_batch(costs, 23.0, 100)
+    assert q[0, 3] < q0[0, 3]        # intra complexity and the I-frame offset at the cut
+    assert (q[1] == q0[1]).all()
