@@ -50,6 +50,7 @@ class HevcParams:
     # CRF per-frame QPs from the GPU lookahead (rc/lookahead.py); False = flat CRF QP
     lookahead: bool = True
     la_range: int = 6
+    scenecut: int = 40   # x264/x265 --scenecut: cut frames are coded all-intra at the I QP (0: off)
 
     def host_cfg(self) -> dict:
         return dict(width=self.width, height=self.height, bit_depth=self.bit_depth, fps=self.fps,
@@ -125,6 +126,7 @@ class GpuHevcEncoder:
         self.params_nal = self.host.hevc_parameter_sets(params.host_cfg())
         self.pool = cf.ThreadPoolExecutor(max_workers=entropy_threads or min(16, os.cpu_count() or 4))
         self.timings: dict[str, float] = {}
+        self.stats: dict[str, float] = {}
 
     def _host_buffers(self):
         if self.host_bufs is None:
@@ -176,7 +178,11 @@ class GpuHevcEncoder:
             y8 = (y >> (self.p.bit_depth - 8)).clamp_(0, 255).to(torch.uint8)
         costs = self._la.frame_costs(y8.contiguous()).cpu().numpy()
         lbw, lbh = GpuLookahead.block_grid(y.shape[3], y.shape[2])
-        q = crf_qps_batch(costs, float(self.p.crf), lbw * lbh, keyint=self.p.keyint or None)
+        from ..rc.ratecontrol import scenecut_flags
+        self._scenecuts = scenecut_flags(costs, float(self.p.scenecut), keyint=self.p.keyint or None)
+        q = crf_qps_batch(costs, float(self.p.crf), lbw * lbh, keyint=self.p.keyint or None,
+                          scenecuts=self._scenecuts)
+        self.stats["scenecuts"] = int(self._scenecuts.sum())
         self.timings["lookahead_s"] = self.timings.get("lookahead_s", 0.0) + time.perf_counter() - t0
         return q
 
@@ -192,8 +198,11 @@ class GpuHevcEncoder:
         if y.device != self.dev:
             raise ValueError("inputs must live on the encoder's device")
         qi, qpp = self.p.frame_qps()
+        self._scenecuts = None
         if qps is None and self.p.crf is not None and self.p.lookahead and not self.p.intra_only:
             qps = self.crf_qps(y)
+        cuts_h = self._scenecuts if self._scenecuts is not None else np.zeros((B, F), dtype=bool)
+        cuts_d = torch.from_numpy(np.ascontiguousarray(cuts_h.T)).to(self.dev)  # [F, B]
         if qps is None:
             qps = np.array([[qi if t == 0 else qpp for t in range(F)] for _ in range(B)], dtype=np.int32)
         cfg = self.p.host_cfg()
@@ -232,6 +241,8 @@ class GpuHevcEncoder:
                 self.hip.me(B, self.wmb, self.hmb, p(self.src8), p(self.ref8), p(self.prev_mv), p(self.mv),
                             p(self.me_cost), p(self.me_pred), p(self.me_intra), p(self.qp), self.p.me_range,
                             self.p.subpel, s, p(self.me_hp))
+                if cuts_h[:, t].any():  # scene cut: every CU of these slots goes intra
+                    self.me_cost.masked_fill_(cuts_d[t][:, None], 1 << 26)
                 self.hip.hevc_inter(B, self.W, self.H, p(self.src[0]), p(self.src[1]), p(self.src[2]), p(ref[0]),
                                     p(ref[1]), p(ref[2]), p(cur[0]), p(cur[1]), p(cur[2]), p(self.ctu), p(self.cu),
                                     p(self.coef[0]), p(self.coef[1]), p(self.coef[2]), p(self.qp), p(self.run),

@@ -77,3 +77,22 @@ def test_gpu_backend_hevc_preset(host, tmp_path):
         mse = np.mean((ref - dec) ** 2)
         assert 10 * np.log10(255 ** 2 / mse) > 30
     be.close()
+
+
+def test_gpu_hevc_scenecut(host):
+    """A hard cut inside a segment is detected by the lookahead and the cut picture is
+    coded with intra CUs only; the reconstruction stays bit-exact with the decoder."""
+    from govideocompressor_amd.models.h264_gpu import synth_clip
+    from govideocompressor_amd.models.hevc_gpu import GpuHevcEncoder, HevcParams
+    w, h, B, F, cut = 128, 96, 2, 5, 2
+    a = synth_clip(B, F, w, h, seed=7)
+    b = synth_clip(B, F, w, h, seed=99)
+    y, u, v = (torch.cat([pa[:, :cut], pb[:, cut:]], dim=1).contiguous() for pa, pb in zip(a, b))
+    enc = GpuHevcEncoder(HevcParams(width=w, height=h), slots=B)
+    res = enc.encode(y, u, v, keep_recon=True)
+    rec = enc.last_recon
+    assert enc._scenecuts[:, cut].all() and enc.stats["scenecuts"] >= B
+    enc.close()
+    _compare(host, res, rec)
+    for r in res:
+        assert r.bits[cut] > 1.3 * r.bits[cut + 1]   # the all-intra cut picture costs more than a P picture
