@@ -58,10 +58,12 @@ def init(prefer_gpu: bool = True, timeout_s: int = 600) -> DistEnv:
     env = DistEnv(rank=rank, world=world, local_rank=local, device=device)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "nccl" if use_gpu else "gloo"
+        # MIVC_DIST_BACKEND=gloo: host collectives even when encoding on GPUs (lets several
+        # ranks share one GPU for a rehearsal of the multi-GPU flow; RCCL needs one GPU per rank)
+        backend = os.environ.get("MIVC_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         if not dist.is_initialized():
             kw = {}
-            if use_gpu:
+            if use_gpu and backend == "nccl":
                 kw["device_id"] = device
             dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
@@ -82,10 +84,15 @@ def barrier(env: DistEnv) -> None:
             dist.barrier()
 
 
+def coll_device(env: DistEnv) -> torch.device:
+    """Device of the tensors handed to collectives: the GPU under RCCL, the host under gloo."""
+    return env.device if env.backend == "nccl" else torch.device("cpu")
+
+
 def max_over_ranks(env: DistEnv, value: float) -> float:
     if not env.initialized:
         return value
-    t = torch.tensor([value], dtype=torch.float64, device=env.device)
+    t = torch.tensor([value], dtype=torch.float64, device=coll_device(env))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -93,7 +100,7 @@ def max_over_ranks(env: DistEnv, value: float) -> float:
 def sum_over_ranks(env: DistEnv, value: float) -> float:
     if not env.initialized:
         return value
-    t = torch.tensor([value], dtype=torch.float64, device=env.device)
+    t = torch.tensor([value], dtype=torch.float64, device=coll_device(env))
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
 
@@ -134,7 +141,7 @@ class BitstreamGather:
         env = self.env
         if not env.initialized:
             return self
-        dev = env.device
+        dev = coll_device(env)
         sizes = torch.tensor([len(p) for p in self.pieces], dtype=torch.int64, device=dev)
         n = torch.tensor([len(self.pieces)], dtype=torch.int64, device=dev)
         ns = torch.empty(env.world, dtype=torch.int64, device=dev)
@@ -254,7 +261,7 @@ class SegmentMerge:
         self._check_start_codes(local, sizes)
         if not env.initialized:
             return local
-        dev = env.device
+        dev = coll_device(env)
         n_loc = torch.tensor([local.size], dtype=torch.int64, device=dev)
         all_n = torch.empty(env.world, dtype=torch.int64, device=dev)
         dist.all_gather_into_tensor(all_n, n_loc)

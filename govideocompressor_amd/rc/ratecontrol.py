@@ -179,7 +179,8 @@ class GlobalStats:
     def __init__(self, n_frames_total: int, env=None):
         import torch
         self.env = env
-        dev = env.device if env is not None else torch.device("cpu")
+        from ..parallel.dist import coll_device
+        dev = coll_device(env) if env is not None else torch.device("cpu")
         self.t = torch.zeros((n_frames_total, 4), dtype=torch.float64, device=dev)
 
     def put(self, frame0: int, stats: np.ndarray):
