@@ -1,0 +1,138 @@
+// Adaptive quantisation for the H.264 encoder (SURVEY.md K-C11, x264 --aq-mode 1, the
+// libx264 default of the reference's "264" preset, server.go:69-70).
+//
+//   h264_aq_offsets   per-MB QP offsets from the AC energy of the source MB:
+//                     energy = var(Y 16x16) + var(Cb 8x8) + var(Cr 8x8) (sum of squares minus
+//                     squared sum / n, x264 ac_energy_var), offset = round(strength * 1.0397 *
+//                     (log2(energy) - 14.427)), the x264 formula for 8-bit video.
+//   h264_qp_flags     per MB: does it carry mb_qp_delta (coded residual, or Intra16x16)?
+//   h264_qp_fixup     an MB without mb_qp_delta inherits QP_pred (the QP of the previous MB
+//                     in decoding order, the slice QP for the first): clause 7.4.5.  Its
+//                     decision record gets that QP so that deblocking (which reads QP_Y of
+//                     every MB) matches a decoder.  Per slot: segmented scan over raster order.
+#include <cmath>
+
+#include "kcommon.h"
+
+namespace mivc {
+namespace gpu {
+
+using h264::MbHeader;
+
+// one wave per MB, 4 MBs per workgroup.  Lanes: luma row l >> 2 (4 px); lanes 0..15 also
+// Cb row l >> 1 (4 px), lanes 16..31 Cr.
+__global__ __launch_bounds__(256) void h264_aq_offsets(Geom g, const uint8_t* __restrict__ sy,
+                                                       const uint8_t* __restrict__ su, const uint8_t* __restrict__ sv,
+                                                       float strength, int8_t* __restrict__ out) {
+  const int lane = lane_id();
+  const int nmb = g.nmb();
+  const int mb = blockIdx.x * 4 + wave_id(), slot = blockIdx.y;
+  if (mb >= nmb) return;  // wave-uniform
+  const int mx = mb % g.wmb, my = mb / g.wmb;
+  const uint32_t wy = *reinterpret_cast<const uint32_t*>(sy + slot * g.ysize() +
+                                                         static_cast<size_t>(my * 16 + (lane >> 2)) * g.W + mx * 16 +
+                                                         (lane & 3) * 4);
+  uint32_t wc = 0;
+  if (lane < 32) {
+    const uint8_t* c = (lane < 16 ? su : sv) + slot * g.csize();
+    const int l = lane & 15;
+    wc = *reinterpret_cast<const uint32_t*>(c + static_cast<size_t>(my * 8 + (l >> 1)) * g.cw() + mx * 8 + (l & 1) * 4);
+  }
+  int s = 0, ss = 0, cs = 0, css = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int p = __builtin_amdgcn_ubfe(wy, 8 * k, 8), q = __builtin_amdgcn_ubfe(wc, 8 * k, 8);
+    s += p;
+    ss += p * p;
+    cs += q;
+    css += q * q;
+  }
+  s = sum64(s);
+  ss = sum64(ss);
+  cs = sum16(cs);   // per 16-lane row: row 0 Cb, row 1 Cr
+  css = sum16(css);
+  const int su_ = __builtin_amdgcn_readlane(cs, 0), ssu = __builtin_amdgcn_readlane(css, 0);
+  const int sv_ = __builtin_amdgcn_readlane(cs, 16), ssv = __builtin_amdgcn_readlane(css, 16);
+  if (lane == 0) {
+    const uint32_t e = static_cast<uint32_t>(ss - ((s * s) >> 8)) + static_cast<uint32_t>(ssu - ((su_ * su_) >> 6)) +
+                       static_cast<uint32_t>(ssv - ((sv_ * sv_) >> 6));
+    const float adj = strength * 1.0397f * (log2f(static_cast<float>(e > 1u ? e : 1u)) - 14.427f);
+    out[static_cast<size_t>(slot) * nmb + mb] = static_cast<int8_t>(clampi(static_cast<int>(rintf(adj)), -24, 24));
+  }
+}
+
+// Two MBs per wave (halves); per half lanes 0..15 luma blocks, 16..23 chroma AC (from
+// coefficient 1), 24 chroma DC: the MB carries mb_qp_delta iff any is non-zero or it is
+// Intra16x16 (CAVLC/CABAC syntax: coded_block_pattern != 0 || I16x16).
+__global__ __launch_bounds__(64) void h264_qp_flags(Geom g, const MbHeader* __restrict__ hdr,
+                                                    const int16_t* __restrict__ coef, uint8_t* __restrict__ flags) {
+  const int lane = lane_id(), sub = lane & 31, half = lane >> 5;
+  const int nmb = g.nmb();
+  const int mb = blockIdx.x * 2 + half, slot = blockIdx.y;
+  const bool live = mb < nmb;
+  const size_t o = static_cast<size_t>(slot) * nmb + (live ? mb : 0);
+  const int16_t* c = coef + o * h264::kCoefPerMb;
+  bool nz = false;
+  if (live && sub < 24) {
+    const uint4* p = reinterpret_cast<const uint4*>(c + (sub < 16 ? h264::COEF_LUMA + sub * 16
+                                                                  : h264::COEF_CHROMA_AC + (sub - 16) * 16));
+    const uint4 q0 = p[0], q1 = p[1];
+    const uint32_t first = sub < 16 ? q0.x : (q0.x & 0xFFFF0000u);  // chroma AC: position 0 unused
+    nz = (first | q0.y | q0.z | q0.w | q1.x | q1.y | q1.z | q1.w) != 0;
+  } else if (live && sub == 24) {
+    const uint4 q = *reinterpret_cast<const uint4*>(c + h264::COEF_CHROMA_DC);
+    nz = (q.x | q.y | q.z | q.w) != 0;
+  }
+  const uint64_t bal = __ballot(nz);
+  const uint32_t mine = half ? static_cast<uint32_t>(bal >> 32) : static_cast<uint32_t>(bal);
+  if (live && sub == 0) flags[o] = (mine != 0 || hdr[o].kind == h264::MBK_I16x16) ? 1 : 0;
+}
+
+// One workgroup per slot: chunked segmented scan of "last MB with mb_qp_delta".
+__global__ __launch_bounds__(1024) void h264_qp_fixup(Geom g, MbHeader* __restrict__ hdr,
+                                                      const uint8_t* __restrict__ flags, const int* __restrict__ slice_qp) {
+  const int slot = blockIdx.x, n = g.nmb();
+  const size_t base = static_cast<size_t>(slot) * n;
+  __shared__ int s_last[1024];
+  const int per = (n + blockDim.x - 1) / blockDim.x;
+  const int i0 = threadIdx.x * per, i1 = min(n, i0 + per);
+  int last = -1;
+  for (int i = i0; i < i1; ++i)
+    if (flags[base + i]) last = i;
+  s_last[threadIdx.x] = last;
+  __syncthreads();
+  for (int off = 1; off < blockDim.x; off <<= 1) {  // inclusive max-scan (Hillis-Steele)
+    const int v = threadIdx.x >= off ? s_last[threadIdx.x - off] : -1;
+    __syncthreads();
+    s_last[threadIdx.x] = max(s_last[threadIdx.x], v);
+    __syncthreads();
+  }
+  last = threadIdx.x > 0 ? s_last[threadIdx.x - 1] : -1;
+  int qp = last >= 0 ? hdr[base + last].qp : slice_qp[slot];
+  for (int i = i0; i < i1; ++i) {
+    if (flags[base + i]) qp = hdr[base + i].qp;
+    else hdr[base + i].qp = static_cast<int8_t>(qp);
+  }
+}
+
+}  // namespace gpu
+}  // namespace mivc
+
+using namespace mivc::gpu;
+
+extern "C" void mivc_launch_aq_offsets(int B, int wmb, int hmb, const uint8_t* sy, const uint8_t* su,
+                                       const uint8_t* sv, float strength, int8_t* out, void* stream) {
+  const Geom g{B, wmb, hmb, wmb * 16, hmb * 16};
+  hipLaunchKernelGGL(h264_aq_offsets, dim3((wmb * hmb + 3) / 4, B), dim3(256), 0, static_cast<hipStream_t>(stream), g,
+                     sy, su, sv, strength, out);
+}
+
+extern "C" void mivc_launch_qp_fixup(int B, int wmb, int hmb, void* hdr, const int16_t* coef, uint8_t* flags,
+                                     const int* slice_qp, void* stream) {
+  const Geom g{B, wmb, hmb, wmb * 16, hmb * 16};
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(h264_qp_flags, dim3((wmb * hmb + 1) / 2, B), dim3(64), 0, s, g,
+                     static_cast<const mivc::h264::MbHeader*>(hdr), coef, flags);
+  hipLaunchKernelGGL(h264_qp_fixup, dim3(B), dim3(1024), 0, s, g, static_cast<mivc::h264::MbHeader*>(hdr), flags,
+                     slice_qp);
+}

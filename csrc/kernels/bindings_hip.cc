@@ -19,19 +19,23 @@ void mivc_launch_rgb_to_i420(const uint8_t* rgb, int w, int h, int nframes, uint
                              void* stream);
 void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref_y, const int16_t* pred_mv,
                     int16_t* out_mv, int* out_cost, uint8_t* out_pred, int* out_intra_cost, const int* qp, int range,
-                    int subpel, uint8_t* hp, void* stream);
+                    int subpel, uint8_t* hp, const int8_t* aq, void* stream);
+void mivc_launch_aq_offsets(int B, int wmb, int hmb, const uint8_t* sy, const uint8_t* su, const uint8_t* sv,
+                            float strength, int8_t* out, void* stream);
+void mivc_launch_qp_fixup(int B, int wmb, int hmb, void* hdr, const int16_t* coef, uint8_t* flags, const int* slice_qp,
+                          void* stream);
 void mivc_launch_me_halfpel(int B, int W, int H, const uint8_t* ref_y, uint8_t* hp, void* stream);
 void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* src_u,
                               const uint8_t* src_v, const uint8_t* ref_y, const uint8_t* ref_u, const uint8_t* ref_v,
                               uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const uint8_t* pred_y,
                               const int16_t* mv, const int* me_cost, const int* intra_cost, const int* qp,
                               int chroma_qp_offset, void* hdr, int16_t* coef, uint8_t* nz, uint8_t* intra_flag,
-                              int* intra_count, void* stream);
+                              int* intra_count, const int8_t* aq, void* stream);
 void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* src_u,
                               const uint8_t* src_v, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const int* qp,
                               int chroma_qp_offset, void* hdr, int16_t* coef, uint8_t* nz,
                               const uint8_t* intra_flag, const int* intra_count, int* err, int use_i4x4,
-                              void* stream);
+                              const int8_t* aq, void* stream);
 void mivc_launch_deblock(int B, int wmb, int hmb, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const void* hdr,
                          const uint8_t* nz, int chroma_qp_offset, int alpha_off, int beta_off, int* err,
                          void* stream);
@@ -97,13 +101,22 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("me", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref, uintptr_t pred_mv, uintptr_t out_mv,
                  uintptr_t out_cost, uintptr_t out_pred, uintptr_t out_intra, uintptr_t qp, int range, int subpel,
-                 uintptr_t stream, uintptr_t hp) {
+                 uintptr_t stream, uintptr_t hp, uintptr_t aq) {
     mivc_launch_me(B, wmb, hmb, P<uint8_t>(src), P<uint8_t>(ref), P<int16_t>(pred_mv), P<int16_t>(out_mv),
                    P<int>(out_cost), P<uint8_t>(out_pred), P<int>(out_intra), P<int>(qp), range, subpel,
-                   P<uint8_t>(hp), S(stream));
+                   P<uint8_t>(hp), P<int8_t>(aq), S(stream));
   }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("src"), py::arg("ref"), py::arg("pred_mv"),
      py::arg("out_mv"), py::arg("out_cost"), py::arg("out_pred"), py::arg("out_intra"), py::arg("qp"),
-     py::arg("range"), py::arg("subpel"), py::arg("stream"), py::arg("hp") = 0);
+     py::arg("range"), py::arg("subpel"), py::arg("stream"), py::arg("hp") = 0, py::arg("aq") = 0);
+  m.def("aq_offsets", [](int B, int wmb, int hmb, uintptr_t sy, uintptr_t su, uintptr_t sv, float strength,
+                         uintptr_t out, uintptr_t stream) {
+    mivc_launch_aq_offsets(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), strength, P<int8_t>(out),
+                           S(stream));
+  });
+  m.def("qp_fixup", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t coef, uintptr_t flags, uintptr_t slice_qp,
+                       uintptr_t stream) {
+    mivc_launch_qp_fixup(B, wmb, hmb, P<void>(hdr), P<int16_t>(coef), P<uint8_t>(flags), P<int>(slice_qp), S(stream));
+  });
   m.def("me_halfpel", [](int B, int W, int H, uintptr_t ref, uintptr_t hp, uintptr_t stream) {
     mivc_launch_me_halfpel(B, W, H, P<uint8_t>(ref), P<uint8_t>(hp), S(stream));
   });
@@ -111,22 +124,28 @@ PYBIND11_MODULE(_hip, m) {
         [](int B, int wmb, int hmb, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t fy, uintptr_t fu,
            uintptr_t fv, uintptr_t ry, uintptr_t ru, uintptr_t rv, uintptr_t pred, uintptr_t mv, uintptr_t me_cost,
            uintptr_t intra_cost, uintptr_t qp, int cqo, uintptr_t hdr, uintptr_t coef, uintptr_t nz,
-           uintptr_t intra_flag, uintptr_t intra_count, uintptr_t stream) {
+           uintptr_t intra_flag, uintptr_t intra_count, uintptr_t stream, uintptr_t aq) {
           mivc_launch_encode_inter(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), P<uint8_t>(fy),
                                    P<uint8_t>(fu), P<uint8_t>(fv), P<uint8_t>(ry), P<uint8_t>(ru), P<uint8_t>(rv),
                                    P<uint8_t>(pred), P<int16_t>(mv), P<int>(me_cost), P<int>(intra_cost), P<int>(qp),
                                    cqo, P<void>(hdr), P<int16_t>(coef), P<uint8_t>(nz), P<uint8_t>(intra_flag),
-                                   P<int>(intra_count), S(stream));
-        });
+                                   P<int>(intra_count), P<int8_t>(aq), S(stream));
+        }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("sy"), py::arg("su"), py::arg("sv"), py::arg("fy"),
+        py::arg("fu"), py::arg("fv"), py::arg("ry"), py::arg("ru"), py::arg("rv"), py::arg("pred"), py::arg("mv"),
+        py::arg("me_cost"), py::arg("intra_cost"), py::arg("qp"), py::arg("cqo"), py::arg("hdr"), py::arg("coef"),
+        py::arg("nz"), py::arg("intra_flag"), py::arg("intra_count"), py::arg("stream"), py::arg("aq") = 0);
   m.def("encode_intra", [](int B, int wmb, int hmb, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t ry,
                            uintptr_t ru, uintptr_t rv, uintptr_t qp, int cqo, uintptr_t hdr, uintptr_t coef,
                            uintptr_t nz, uintptr_t intra_flag, uintptr_t intra_count, uintptr_t err, int use_i4x4,
-                           uintptr_t stream) {
+                           uintptr_t stream, uintptr_t aq) {
     mivc_launch_encode_intra(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), P<uint8_t>(ry),
                              P<uint8_t>(ru), P<uint8_t>(rv), P<int>(qp), cqo, P<void>(hdr), P<int16_t>(coef),
                              P<uint8_t>(nz), P<uint8_t>(intra_flag), P<int>(intra_count), P<int>(err), use_i4x4,
-                             S(stream));
-  });
+                             P<int8_t>(aq), S(stream));
+  }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("sy"), py::arg("su"), py::arg("sv"), py::arg("ry"),
+     py::arg("ru"), py::arg("rv"), py::arg("qp"), py::arg("cqo"), py::arg("hdr"), py::arg("coef"), py::arg("nz"),
+     py::arg("intra_flag"), py::arg("intra_count"), py::arg("err"), py::arg("use_i4x4"), py::arg("stream"),
+     py::arg("aq") = 0);
   m.def("deblock", [](int B, int wmb, int hmb, uintptr_t ry, uintptr_t ru, uintptr_t rv, uintptr_t hdr, uintptr_t nz,
                       int cqo, int alpha_off, int beta_off, uintptr_t err, uintptr_t stream) {
     mivc_launch_deblock(B, wmb, hmb, P<uint8_t>(ry), P<uint8_t>(ru), P<uint8_t>(rv), P<void>(hdr), P<uint8_t>(nz),

@@ -26,6 +26,7 @@ struct InterArgs {
   const int* me_cost;      // [B, nmb]
   const int* intra_cost;   // [B, nmb]
   const int* qp;           // [B]
+  const int8_t* aq;        // [B, nmb] adaptive-quantisation QP offsets (nullable)
   int chroma_qp_offset;
   MbHeader* hdr;           // [B, nmb]
   int16_t* coef;           // [B, nmb, 408]
@@ -75,7 +76,7 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
   const int mx = mbc % g.wmb, my = mbc / g.wmb;
   const size_t o = static_cast<size_t>(slot) * nmb + mbc;
   const int W = g.W, cw = g.cw(), CH = g.ch();
-  const int qp = a.qp[slot];
+  const int qp = clampi(a.qp[slot] + (a.aq ? a.aq[o] : 0), 0, 51);
   const int qpc = h264::chroma_qp(qp, a.chroma_qp_offset);
 
   __shared__ int s_score[2][24];
@@ -302,7 +303,7 @@ extern "C" void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t*
                                          const uint8_t* pred_y, const int16_t* mv, const int* me_cost,
                                          const int* intra_cost, const int* qp, int chroma_qp_offset, void* hdr,
                                          int16_t* coef, uint8_t* nz, uint8_t* intra_flag, int* intra_count,
-                                         void* stream) {
+                                         const int8_t* aq, void* stream) {
   InterArgs a;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.src_y = src_y;
@@ -325,5 +326,6 @@ extern "C" void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t*
   a.nz = nz;
   a.intra_flag = intra_flag;
   a.intra_count = intra_count;
+  a.aq = aq;
   hipLaunchKernelGGL(encode_inter_mb, dim3((wmb * hmb + 1) / 2, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
 }

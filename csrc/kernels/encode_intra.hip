@@ -31,6 +31,7 @@ struct IntraArgs {
   const uint8_t *src_y, *src_u, *src_v;
   uint8_t *rec_y, *rec_u, *rec_v;
   const int* qp;
+  const int8_t* aq;  // [B, nmb] adaptive-quantisation QP offsets (nullable)
   int chroma_qp_offset;
   MbHeader* hdr;
   int16_t* coef;
@@ -136,7 +137,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
   const int W = g.W, cw = g.cw();
   const int X0 = mx * 16, Y0 = my * 16;
   const size_t o = static_cast<size_t>(slot) * g.nmb() + my * g.wmb + mx;
-  const int qp = a.qp[slot];
+  const int qp = clampi(a.qp[slot] + (a.aq ? a.aq[o] : 0), 0, 51);
   const int qpc = h264::chroma_qp(qp, a.chroma_qp_offset);
   const int lambda = h264::kLambda[qp];
   const int qbits = 15 + qp / 6, qbits_c = 15 + qpc / 6;
@@ -541,8 +542,9 @@ extern "C" void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t*
                                          const uint8_t* src_v, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v,
                                          const int* qp, int chroma_qp_offset, void* hdr, int16_t* coef, uint8_t* nz,
                                          const uint8_t* intra_flag, const int* intra_count, int* err, int use_i4x4,
-                                         void* stream) {
+                                         const int8_t* aq, void* stream) {
   IntraArgs a;
+  a.aq = aq;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.src_y = src_y;
   a.src_u = src_u;

@@ -40,6 +40,7 @@ struct MeArgs {
   int range;               // integer radius, <= 16
   int subpel;              // 0 none, 1 half, 2 quarter
   const uint8_t* hp;       // [B, 3, H + 8, W + 8] b / h / j half-sample planes of ref_y (margin 4)
+  const int8_t* aq;        // [B, nmb] adaptive-quantisation QP offsets (nullable)
 };
 
 constexpr int kHpM = 4;  // half-sample plane margin (samples); coordinates clamp into it exactly
@@ -313,7 +314,7 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   const uint8_t* src = a.src_y + slot * g.ysize();
   const uint8_t* ref = a.ref_y + slot * g.ysize();
   const int W = g.W, H = g.H;
-  const int qp = a.qp[slot];
+  const int qp = clampi(a.qp[slot] + (a.aq ? a.aq[static_cast<size_t>(slot) * nmb + mb] : 0), 0, 51);
   const int lambda = h264::kLambda[qp];
   const int R = a.range < MAXR ? a.range : MAXR;
 
@@ -660,7 +661,7 @@ extern "C" void mivc_launch_me_halfpel(int B, int W, int H, const uint8_t* ref_y
 extern "C" void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref_y,
                                const int16_t* pred_mv, int16_t* out_mv, int* out_cost, uint8_t* out_pred,
                                int* out_intra_cost, const int* qp, int range, int subpel, uint8_t* hp_buf,
-                               void* stream) {
+                               const int8_t* aq, void* stream) {
   // hp_buf: caller-owned [B, 3, H + 8, W + 8] (+64 bytes slack) half-sample plane scratch,
   // resident across frames; nullptr -> stream-ordered scratch for this call only.
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -687,6 +688,7 @@ extern "C" void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, co
   a.range = range < kMaxR ? range : kMaxR;
   a.subpel = subpel;
   a.hp = hp;
+  a.aq = aq;
   if (a.range <= 8) hipLaunchKernelGGL(me_p16x16<8>, dim3(wmb * hmb, B), dim3(64), 0, s, a);
   else hipLaunchKernelGGL(me_p16x16<kMaxR>, dim3(wmb * hmb, B), dim3(64), 0, s, a);
   if (!hp_buf) (void)hipFreeAsync(hp, s);

@@ -54,6 +54,9 @@ class H264Params:
     # x264 --scenecut: a P frame whose lowres inter cost saves less than this percent of
     # its intra cost is coded all-intra (I4x4/I16x16 MBs) at the I-frame QP; 0 disables
     scenecut: int = 40
+    # x264 --aq-mode 1 (variance AQ): per-MB QP offset strength * 1.0397 * (log2(AC energy)
+    # - 14.427); 0 disables (every MB at the frame QP)
+    aq_strength: float = 1.0
 
     def host_cfg(self) -> dict:
         return dict(width=self.width, height=self.height, fps=self.fps, qp=self.qp,
@@ -145,6 +148,8 @@ class GpuH264Encoder:
         # resident b / h / j half-sample planes of the reference (margin 4, + load slack)
         self.me_hp = torch.empty(B * 3 * (H + 8) * (W + 8) + 64, dtype=u8, device=dev)
         self.intra_flag = torch.zeros((B, nmb), dtype=u8, device=dev)
+        self.aq = torch.zeros((B, nmb), dtype=torch.int8, device=dev)     # per-MB QP offsets (AQ)
+        self.qp_flags = torch.zeros((B, nmb), dtype=u8, device=dev)       # MB carries mb_qp_delta
         self.intra_count = torch.zeros((B,), dtype=i32, device=dev)
         self.qp = torch.zeros((B,), dtype=i32, device=dev)
         self.err = torch.zeros((1,), dtype=i32, device=dev)
@@ -213,18 +218,22 @@ class GpuH264Encoder:
         B, wmb, hmb = self.B, self.wmb, self.hmb
         sy, su, sv = (self._ptr(x) for x in self.src)
         ry, ru, rv = (self._ptr(x) for x in cur)
+        aq = 0
+        if self.p.aq_strength > 0:
+            aq = self._ptr(self.aq)
+            self.hip.aq_offsets(B, wmb, hmb, sy, su, sv, float(self.p.aq_strength), aq, s)
         if not idr:
             fy, fu, fv = (self._ptr(x) for x in ref)
             self.intra_count.zero_()
             self.hip.me(B, wmb, hmb, sy, fy, self._ptr(self.prev_mv), self._ptr(self.mv), self._ptr(self.me_cost),
                         self._ptr(self.pred), self._ptr(self.intra_cost), self._ptr(self.qp),
-                        self.p.me_range, self.p.subpel, s, self._ptr(self.me_hp))
+                        self.p.me_range, self.p.subpel, s, self._ptr(self.me_hp), aq)
             if cut is not None:
                 self.intra_cost.masked_fill_(cut[:, None], -1)  # intra beats any inter cost
             self.hip.encode_inter(B, wmb, hmb, sy, su, sv, fy, fu, fv, ry, ru, rv, self._ptr(self.pred),
                                   self._ptr(self.mv), self._ptr(self.me_cost), self._ptr(self.intra_cost),
                                   self._ptr(self.qp), self.p.chroma_qp_offset, self._ptr(hdr), self._ptr(coef),
-                                  self._ptr(self.nz), self._ptr(self.intra_flag), self._ptr(self.intra_count), s)
+                                  self._ptr(self.nz), self._ptr(self.intra_flag), self._ptr(self.intra_count), s, aq)
             self.prev_mv.copy_(self.mv)
             self.p_intra_mbs += self.intra_count.sum()
             flag_ptr, count_ptr = self._ptr(self.intra_flag), self._ptr(self.intra_count)
@@ -234,7 +243,12 @@ class GpuH264Encoder:
         self.hip.encode_intra(B, wmb, hmb, sy, su, sv, ry, ru, rv, self._ptr(self.qp), self.p.chroma_qp_offset,
                               self._ptr(hdr), self._ptr(coef), self._ptr(self.nz), flag_ptr, count_ptr,
                               self._ptr(self.err),
-                              int(self.p.i4x4 and (idr or self.p.i4x4_in_p or cut is not None)), s)
+                              int(self.p.i4x4 and (idr or self.p.i4x4_in_p or cut is not None)), s, aq)
+        if aq:
+            # MBs without mb_qp_delta take QP_pred (clause 7.4.5): their records must say so
+            # before deblocking reads every MB's QP
+            self.hip.qp_fixup(B, wmb, hmb, self._ptr(hdr), self._ptr(coef), self._ptr(self.qp_flags),
+                              self._ptr(self.qp), s)
         if self.p.deblock:
             self.hip.deblock(B, wmb, hmb, ry, ru, rv, self._ptr(hdr), self._ptr(self.nz), self.p.chroma_qp_offset,
                              0, 0, self._ptr(self.err), s)

@@ -78,7 +78,7 @@ def test_gpu_per_frame_qps(host):
     w, h, B, F = 176, 144, 3, 5
     rng = np.random.default_rng(4)
     qps = rng.integers(18, 40, size=(B, F))
-    p = H264Params(width=w, height=h)
+    p = H264Params(width=w, height=h, aq_strength=0.0)  # every MB at its frame's QP
     y, u, v = synth_clip(B, F, w, h, seed=2)
     out = {}
     for mode in ("cpu", "gpu"):
@@ -118,3 +118,30 @@ def test_gpu_scenecut_codes_cut_frames_intra(host):
         assert np.isin(np.asarray(pics[cut + 1]["mb_kind"]), [2, 3, 5, 6, 7]).mean() > 0.5
         assert r.psnr_y > 30
     enc.close()
+
+
+def test_gpu_adaptive_quant(host):
+    """x264-style variance AQ: per-MB QPs differ inside a picture, MBs without
+    mb_qp_delta carry QP_pred in their records (deblocking stays bit-exact), and the GPU
+    CAVLC equals the host writer on the same records."""
+    import numpy as np
+    import torch
+    from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
+
+    w, h, B, F = 176, 144, 2, 4
+    y, u, v = synth_clip(B, F, w, h, seed=11)
+    out = {}
+    for mode in ("cpu", "gpu"):
+        enc = GpuH264Encoder(H264Params(width=w, height=h, crf=None, qp=28, aq_strength=1.0), slots=B, entropy=mode)
+        res = enc.encode(y, u, v, keep_recon=(mode == "gpu"))
+        out[mode] = [r.bitstream for r in res]
+        if mode == "gpu":
+            _check_roundtrip(host, enc, res, w, h)
+            offs = enc.aq.cpu().numpy()
+            assert offs.std() > 0.5 and abs(int(offs.max())) <= 24
+        enc.close()
+    assert out["gpu"] == out["cpu"]
+    for b in range(B):
+        pics = host.decode(out["gpu"][b])
+        assert any(np.unique(np.asarray(p["mb_qp"])).size > 3 for p in pics)
+    torch.cuda.synchronize()

@@ -36,7 +36,7 @@ def main():
         def launch():
             lib.mivc_launch_me(B, enc.wmb, enc.hmb, P(enc.src[0]), P(enc.rec[0][0]), P(enc.prev_mv), P(enc.mv),
                                P(enc.me_cost), P(enc.pred), P(enc.intra_cost), P(enc.qp), a.range, a.subpel,
-                               P(enc.me_hp), s)
+                               P(enc.me_hp), None, s)
         launch()
         torch.cuda.synchronize()
         out = (enc.mv.clone(), enc.me_cost.clone(), enc.pred.clone())
