@@ -6,6 +6,8 @@
 //                     squared sum / n, x264 ac_energy_var), offset = round(strength * 1.0397 *
 //                     (log2(energy) - 14.427)), the x264 formula for 8-bit video.
 //   h264_qp_flags     per MB: does it carry mb_qp_delta (coded residual, or Intra16x16)?
+//                     (luma from the encoder's non-zero flags, which hold for every MB kind
+//                     but Intra16x16, whose flag is set regardless)
 //   h264_qp_fixup     an MB without mb_qp_delta inherits QP_pred (the QP of the previous MB
 //                     in decoding order, the slice QP for the first): clause 7.4.5.  Its
 //                     decision record gets that QP so that deblocking (which reads QP_Y of
@@ -19,53 +21,58 @@ namespace gpu {
 
 using h264::MbHeader;
 
-// one wave per MB, 4 MBs per workgroup.  Lanes: luma row l >> 2 (4 px); lanes 0..15 also
-// Cb row l >> 1 (4 px), lanes 16..31 Cr.
+// 16 lanes per MB (4 MBs per wave, 16 per 256-thread workgroup): lane l of a group sums
+// luma row l (4 dwords) and, for l < 8 Cb row l / for l >= 8 Cr row l - 8 (2 dwords); the
+// group reductions are DPP row sums.
 __global__ __launch_bounds__(256) void h264_aq_offsets(Geom g, const uint8_t* __restrict__ sy,
                                                        const uint8_t* __restrict__ su, const uint8_t* __restrict__ sv,
                                                        float strength, int8_t* __restrict__ out) {
-  const int lane = lane_id();
+  const int l = lane_id() & 15;
   const int nmb = g.nmb();
-  const int mb = blockIdx.x * 4 + wave_id(), slot = blockIdx.y;
-  if (mb >= nmb) return;  // wave-uniform
-  const int mx = mb % g.wmb, my = mb / g.wmb;
-  const uint32_t wy = *reinterpret_cast<const uint32_t*>(sy + slot * g.ysize() +
-                                                         static_cast<size_t>(my * 16 + (lane >> 2)) * g.W + mx * 16 +
-                                                         (lane & 3) * 4);
-  uint32_t wc = 0;
-  if (lane < 32) {
-    const uint8_t* c = (lane < 16 ? su : sv) + slot * g.csize();
-    const int l = lane & 15;
-    wc = *reinterpret_cast<const uint32_t*>(c + static_cast<size_t>(my * 8 + (l >> 1)) * g.cw() + mx * 8 + (l & 1) * 4);
-  }
+  const int mb = blockIdx.x * 16 + (threadIdx.x >> 4), slot = blockIdx.y;
+  const bool live = mb < nmb;
+  const int mbc = live ? mb : nmb - 1;
+  const int mx = mbc % g.wmb, my = mbc / g.wmb;
+  const uint4 wy = *reinterpret_cast<const uint4*>(sy + slot * g.ysize() + static_cast<size_t>(my * 16 + l) * g.W + mx * 16);
+  const uint8_t* c = (l < 8 ? su : sv) + slot * g.csize();
+  const uint2 wc = *reinterpret_cast<const uint2*>(c + static_cast<size_t>(my * 8 + (l & 7)) * g.cw() + mx * 8);
   int s = 0, ss = 0, cs = 0, css = 0;
+  const uint32_t ly[4] = {wy.x, wy.y, wy.z, wy.w}, lc[2] = {wc.x, wc.y};
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int p = __builtin_amdgcn_ubfe(wy, 8 * k, 8), q = __builtin_amdgcn_ubfe(wc, 8 * k, 8);
-    s += p;
-    ss += p * p;
-    cs += q;
-    css += q * q;
-  }
-  s = sum64(s);
-  ss = sum64(ss);
-  cs = sum16(cs);   // per 16-lane row: row 0 Cb, row 1 Cr
-  css = sum16(css);
-  const int su_ = __builtin_amdgcn_readlane(cs, 0), ssu = __builtin_amdgcn_readlane(css, 0);
-  const int sv_ = __builtin_amdgcn_readlane(cs, 16), ssv = __builtin_amdgcn_readlane(css, 16);
-  if (lane == 0) {
-    const uint32_t e = static_cast<uint32_t>(ss - ((s * s) >> 8)) + static_cast<uint32_t>(ssu - ((su_ * su_) >> 6)) +
-                       static_cast<uint32_t>(ssv - ((sv_ * sv_) >> 6));
+  for (int w = 0; w < 4; ++w)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int p = __builtin_amdgcn_ubfe(ly[w], 8 * k, 8);
+      s += p;
+      ss += p * p;
+    }
+#pragma unroll
+  for (int w = 0; w < 2; ++w)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int q = __builtin_amdgcn_ubfe(lc[w], 8 * k, 8);
+      cs += q;
+      css += q * q;
+    }
+  // Cb in lanes 0..7, Cr in 8..15 of the group: reduce each half-row separately
+  const int cb_s = sum8(cs), cb_ss = sum8(css);
+  s = sum16(s);
+  ss = sum16(ss);
+  const int cr_s = __shfl(cb_s, (lane_id() & ~15) + 8, 64), cr_ss = __shfl(cb_ss, (lane_id() & ~15) + 8, 64);
+  if (live && l == 0) {
+    const uint32_t e = static_cast<uint32_t>(ss - ((s * s) >> 8)) + static_cast<uint32_t>(cb_ss - ((cb_s * cb_s) >> 6)) +
+                       static_cast<uint32_t>(cr_ss - ((cr_s * cr_s) >> 6));
     const float adj = strength * 1.0397f * (log2f(static_cast<float>(e > 1u ? e : 1u)) - 14.427f);
     out[static_cast<size_t>(slot) * nmb + mb] = static_cast<int8_t>(clampi(static_cast<int>(rintf(adj)), -24, 24));
   }
 }
 
-// Two MBs per wave (halves); per half lanes 0..15 luma blocks, 16..23 chroma AC (from
-// coefficient 1), 24 chroma DC: the MB carries mb_qp_delta iff any is non-zero or it is
-// Intra16x16 (CAVLC/CABAC syntax: coded_block_pattern != 0 || I16x16).
+// Two MBs per wave (halves).  The MB carries mb_qp_delta iff it is Intra16x16 or has a
+// non-zero level (coded_block_pattern != 0): luma from the encoder's per-block non-zero
+// flags (lane 9, 16 bytes), chroma AC from coefficient 1 (lanes 0..7), chroma DC (lane 8).
 __global__ __launch_bounds__(64) void h264_qp_flags(Geom g, const MbHeader* __restrict__ hdr,
-                                                    const int16_t* __restrict__ coef, uint8_t* __restrict__ flags) {
+                                                    const int16_t* __restrict__ coef, const uint8_t* __restrict__ nzf,
+                                                    uint8_t* __restrict__ flags) {
   const int lane = lane_id(), sub = lane & 31, half = lane >> 5;
   const int nmb = g.nmb();
   const int mb = blockIdx.x * 2 + half, slot = blockIdx.y;
@@ -73,19 +80,22 @@ __global__ __launch_bounds__(64) void h264_qp_flags(Geom g, const MbHeader* __re
   const size_t o = static_cast<size_t>(slot) * nmb + (live ? mb : 0);
   const int16_t* c = coef + o * h264::kCoefPerMb;
   bool nz = false;
-  if (live && sub < 24) {
-    const uint4* p = reinterpret_cast<const uint4*>(c + (sub < 16 ? h264::COEF_LUMA + sub * 16
-                                                                  : h264::COEF_CHROMA_AC + (sub - 16) * 16));
+  if (live && sub < 8) {
+    const uint4* p = reinterpret_cast<const uint4*>(c + h264::COEF_CHROMA_AC + sub * 16);
     const uint4 q0 = p[0], q1 = p[1];
-    const uint32_t first = sub < 16 ? q0.x : (q0.x & 0xFFFF0000u);  // chroma AC: position 0 unused
-    nz = (first | q0.y | q0.z | q0.w | q1.x | q1.y | q1.z | q1.w) != 0;
-  } else if (live && sub == 24) {
+    nz = ((q0.x & 0xFFFF0000u) | q0.y | q0.z | q0.w | q1.x | q1.y | q1.z | q1.w) != 0;  // position 0 unused
+  } else if (live && sub == 8) {
     const uint4 q = *reinterpret_cast<const uint4*>(c + h264::COEF_CHROMA_DC);
     nz = (q.x | q.y | q.z | q.w) != 0;
+  } else if (live && sub == 9) {
+    const uint4 q = *reinterpret_cast<const uint4*>(nzf + o * 16);
+    nz = (q.x | q.y | q.z | q.w) != 0;
+  } else if (live && sub == 10) {
+    nz = hdr[o].kind == h264::MBK_I16x16;
   }
   const uint64_t bal = __ballot(nz);
   const uint32_t mine = half ? static_cast<uint32_t>(bal >> 32) : static_cast<uint32_t>(bal);
-  if (live && sub == 0) flags[o] = (mine != 0 || hdr[o].kind == h264::MBK_I16x16) ? 1 : 0;
+  if (live && sub == 0) flags[o] = mine != 0 ? 1 : 0;
 }
 
 // One workgroup per slot: chunked segmented scan of "last MB with mb_qp_delta".
@@ -123,16 +133,16 @@ using namespace mivc::gpu;
 extern "C" void mivc_launch_aq_offsets(int B, int wmb, int hmb, const uint8_t* sy, const uint8_t* su,
                                        const uint8_t* sv, float strength, int8_t* out, void* stream) {
   const Geom g{B, wmb, hmb, wmb * 16, hmb * 16};
-  hipLaunchKernelGGL(h264_aq_offsets, dim3((wmb * hmb + 3) / 4, B), dim3(256), 0, static_cast<hipStream_t>(stream), g,
+  hipLaunchKernelGGL(h264_aq_offsets, dim3((wmb * hmb + 15) / 16, B), dim3(256), 0, static_cast<hipStream_t>(stream), g,
                      sy, su, sv, strength, out);
 }
 
-extern "C" void mivc_launch_qp_fixup(int B, int wmb, int hmb, void* hdr, const int16_t* coef, uint8_t* flags,
-                                     const int* slice_qp, void* stream) {
+extern "C" void mivc_launch_qp_fixup(int B, int wmb, int hmb, void* hdr, const int16_t* coef, const uint8_t* nz,
+                                     uint8_t* flags, const int* slice_qp, void* stream) {
   const Geom g{B, wmb, hmb, wmb * 16, hmb * 16};
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(h264_qp_flags, dim3((wmb * hmb + 1) / 2, B), dim3(64), 0, s, g,
-                     static_cast<const mivc::h264::MbHeader*>(hdr), coef, flags);
+                     static_cast<const mivc::h264::MbHeader*>(hdr), coef, nz, flags);
   hipLaunchKernelGGL(h264_qp_fixup, dim3(B), dim3(1024), 0, s, g, static_cast<mivc::h264::MbHeader*>(hdr), flags,
                      slice_qp);
 }

@@ -22,8 +22,8 @@ void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t
                     int subpel, uint8_t* hp, const int8_t* aq, void* stream);
 void mivc_launch_aq_offsets(int B, int wmb, int hmb, const uint8_t* sy, const uint8_t* su, const uint8_t* sv,
                             float strength, int8_t* out, void* stream);
-void mivc_launch_qp_fixup(int B, int wmb, int hmb, void* hdr, const int16_t* coef, uint8_t* flags, const int* slice_qp,
-                          void* stream);
+void mivc_launch_qp_fixup(int B, int wmb, int hmb, void* hdr, const int16_t* coef, const uint8_t* nz, uint8_t* flags,
+                          const int* slice_qp, void* stream);
 void mivc_launch_me_halfpel(int B, int W, int H, const uint8_t* ref_y, uint8_t* hp, void* stream);
 void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* src_u,
                               const uint8_t* src_v, const uint8_t* ref_y, const uint8_t* ref_u, const uint8_t* ref_v,
@@ -113,9 +113,10 @@ PYBIND11_MODULE(_hip, m) {
     mivc_launch_aq_offsets(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), strength, P<int8_t>(out),
                            S(stream));
   });
-  m.def("qp_fixup", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t coef, uintptr_t flags, uintptr_t slice_qp,
-                       uintptr_t stream) {
-    mivc_launch_qp_fixup(B, wmb, hmb, P<void>(hdr), P<int16_t>(coef), P<uint8_t>(flags), P<int>(slice_qp), S(stream));
+  m.def("qp_fixup", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t coef, uintptr_t nz, uintptr_t flags,
+                       uintptr_t slice_qp, uintptr_t stream) {
+    mivc_launch_qp_fixup(B, wmb, hmb, P<void>(hdr), P<int16_t>(coef), P<uint8_t>(nz), P<uint8_t>(flags),
+                         P<int>(slice_qp), S(stream));
   });
   m.def("me_halfpel", [](int B, int W, int H, uintptr_t ref, uintptr_t hp, uintptr_t stream) {
     mivc_launch_me_halfpel(B, W, H, P<uint8_t>(ref), P<uint8_t>(hp), S(stream));

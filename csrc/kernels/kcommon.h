@@ -134,6 +134,10 @@ __device__ __forceinline__ int sum4(int v) {
   v += dpp<kDppQuadXor1>(v);
   return v + dpp<kDppQuadXor2>(v);
 }
+__device__ __forceinline__ int sum8(int v) {  // within each 8-lane half row
+  v = sum4(v);
+  return v + dpp<kDppRowHalfMirror>(v);
+}
 __device__ __forceinline__ int sum16(int v) {
   v = sum4(v);
   v += dpp<kDppRowHalfMirror>(v);

@@ -247,8 +247,8 @@ class GpuH264Encoder:
         if aq:
             # MBs without mb_qp_delta take QP_pred (clause 7.4.5): their records must say so
             # before deblocking reads every MB's QP
-            self.hip.qp_fixup(B, wmb, hmb, self._ptr(hdr), self._ptr(coef), self._ptr(self.qp_flags),
-                              self._ptr(self.qp), s)
+            self.hip.qp_fixup(B, wmb, hmb, self._ptr(hdr), self._ptr(coef), self._ptr(self.nz),
+                              self._ptr(self.qp_flags), self._ptr(self.qp), s)
         if self.p.deblock:
             self.hip.deblock(B, wmb, hmb, ry, ru, rv, self._ptr(hdr), self._ptr(self.nz), self.p.chroma_qp_offset,
                              0, 0, self._ptr(self.err), s)

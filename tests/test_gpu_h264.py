@@ -139,6 +139,18 @@ def test_gpu_adaptive_quant(host):
             _check_roundtrip(host, enc, res, w, h)
             offs = enc.aq.cpu().numpy()
             assert offs.std() > 0.5 and abs(int(offs.max())) <= 24
+            # golden: x264 ac_energy (luma 16x16 + chroma 8x8 variances) of the last frame
+            sy, su, sv = (x.cpu().numpy().astype(np.int64) for x in enc.src)
+            for bb in range(B):
+                for my in range(enc.hmb):
+                    for mx in range(enc.wmb):
+                        e = 0
+                        for pl, n in ((sy[bb, my * 16:my * 16 + 16, mx * 16:mx * 16 + 16], 8),
+                                      (su[bb, my * 8:my * 8 + 8, mx * 8:mx * 8 + 8], 6),
+                                      (sv[bb, my * 8:my * 8 + 8, mx * 8:mx * 8 + 8], 6)):
+                            e += int((pl * pl).sum()) - ((int(pl.sum()) ** 2) >> n)
+                        ref = int(np.rint(1.0397 * (np.log2(max(e, 1)) - 14.427)))
+                        assert abs(int(offs[bb, my * enc.wmb + mx]) - max(-24, min(24, ref))) <= 1
         enc.close()
     assert out["gpu"] == out["cpu"]
     for b in range(B):
