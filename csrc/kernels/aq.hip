@@ -5,6 +5,7 @@
 //                     energy = var(Y 16x16) + var(Cb 8x8) + var(Cr 8x8) (sum of squares minus
 //                     squared sum / n, x264 ac_energy_var), offset = round(strength * 1.0397 *
 //                     (log2(energy) - 14.427)), the x264 formula for 8-bit video.
+//                     (+ the MB-tree offset of the MB when given, mbtree.hip)
 //   h264_qp_flags     per MB: does it carry mb_qp_delta (coded residual, or Intra16x16)?
 //                     (luma from the encoder's non-zero flags, which hold for every MB kind
 //                     but Intra16x16, whose flag is set regardless)
@@ -26,7 +27,8 @@ using h264::MbHeader;
 // group reductions are DPP row sums.
 __global__ __launch_bounds__(256) void h264_aq_offsets(Geom g, const uint8_t* __restrict__ sy,
                                                        const uint8_t* __restrict__ su, const uint8_t* __restrict__ sv,
-                                                       float strength, int8_t* __restrict__ out) {
+                                                       float strength, const float* __restrict__ extra,
+                                                       long long extra_stride, int8_t* __restrict__ out) {
   const int l = lane_id() & 15;
   const int nmb = g.nmb();
   const int mb = blockIdx.x * 16 + (threadIdx.x >> 4), slot = blockIdx.y;
@@ -62,7 +64,8 @@ __global__ __launch_bounds__(256) void h264_aq_offsets(Geom g, const uint8_t* __
   if (live && l == 0) {
     const uint32_t e = static_cast<uint32_t>(ss - ((s * s) >> 8)) + static_cast<uint32_t>(cb_ss - ((cb_s * cb_s) >> 6)) +
                        static_cast<uint32_t>(cr_ss - ((cr_s * cr_s) >> 6));
-    const float adj = strength * 1.0397f * (log2f(static_cast<float>(e > 1u ? e : 1u)) - 14.427f);
+    float adj = strength * 1.0397f * (log2f(static_cast<float>(e > 1u ? e : 1u)) - 14.427f);
+    if (extra) adj += extra[slot * extra_stride + mb];  // MB-tree offset of this frame
     out[static_cast<size_t>(slot) * nmb + mb] = static_cast<int8_t>(clampi(static_cast<int>(rintf(adj)), -24, 24));
   }
 }
@@ -130,11 +133,14 @@ __global__ __launch_bounds__(1024) void h264_qp_fixup(Geom g, MbHeader* __restri
 
 using namespace mivc::gpu;
 
+// extra: optional per-MB float QP offsets added before rounding (MB-tree), slot s of this
+// frame at extra + s * extra_stride
 extern "C" void mivc_launch_aq_offsets(int B, int wmb, int hmb, const uint8_t* sy, const uint8_t* su,
-                                       const uint8_t* sv, float strength, int8_t* out, void* stream) {
+                                       const uint8_t* sv, float strength, const float* extra, long long extra_stride,
+                                       int8_t* out, void* stream) {
   const Geom g{B, wmb, hmb, wmb * 16, hmb * 16};
   hipLaunchKernelGGL(h264_aq_offsets, dim3((wmb * hmb + 15) / 16, B), dim3(256), 0, static_cast<hipStream_t>(stream), g,
-                     sy, su, sv, strength, out);
+                     sy, su, sv, strength, extra, extra_stride, out);
 }
 
 extern "C" void mivc_launch_qp_fixup(int B, int wmb, int hmb, void* hdr, const int16_t* coef, const uint8_t* nz,

@@ -21,7 +21,9 @@ void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t
                     int16_t* out_mv, int* out_cost, uint8_t* out_pred, int* out_intra_cost, const int* qp, int range,
                     int subpel, uint8_t* hp, const int8_t* aq, void* stream);
 void mivc_launch_aq_offsets(int B, int wmb, int hmb, const uint8_t* sy, const uint8_t* su, const uint8_t* sv,
-                            float strength, int8_t* out, void* stream);
+                            float strength, const float* extra, long long extra_stride, int8_t* out, void* stream);
+void mivc_launch_mbtree(int B, int F, int lbw, int lbh, const int* blk_cost, const int* blk_mv, float* prop,
+                        float strength, float* out, void* stream);
 void mivc_launch_qp_fixup(int B, int wmb, int hmb, void* hdr, const int16_t* coef, const uint8_t* nz, uint8_t* flags,
                           const int* slice_qp, void* stream);
 void mivc_launch_me_halfpel(int B, int W, int H, const uint8_t* ref_y, uint8_t* hp, void* stream);
@@ -71,7 +73,7 @@ int mivc_launch_hevc_prep_frame(int B, const void* sy, const void* su, const voi
                                 uint16_t* dv, uint8_t* d8, int W, int H, int shift, int bd, void* stream);
 int mivc_launch_hevc_proxy8(const uint16_t* src, uint8_t* dst, long long n, int shift, void* stream);
 int mivc_launch_lookahead(const uint8_t* y, int w, int h, long long fstride, int N, int F, uint8_t* low,
-                          unsigned long long* frame_cost, int* blk_cost, int range, void* stream);
+                          unsigned long long* frame_cost, int* blk_cost, int* blk_mv, int range, void* stream);
 }
 
 namespace {
@@ -109,9 +111,15 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("out_mv"), py::arg("out_cost"), py::arg("out_pred"), py::arg("out_intra"), py::arg("qp"),
      py::arg("range"), py::arg("subpel"), py::arg("stream"), py::arg("hp") = 0, py::arg("aq") = 0);
   m.def("aq_offsets", [](int B, int wmb, int hmb, uintptr_t sy, uintptr_t su, uintptr_t sv, float strength,
-                         uintptr_t out, uintptr_t stream) {
-    mivc_launch_aq_offsets(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), strength, P<int8_t>(out),
-                           S(stream));
+                         uintptr_t out, uintptr_t stream, uintptr_t extra, long long extra_stride) {
+    mivc_launch_aq_offsets(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), strength, P<float>(extra),
+                           extra_stride, P<int8_t>(out), S(stream));
+  }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("sy"), py::arg("su"), py::arg("sv"), py::arg("strength"),
+     py::arg("out"), py::arg("stream"), py::arg("extra") = 0, py::arg("extra_stride") = 0);
+  m.def("mbtree", [](int B, int F, int lbw, int lbh, uintptr_t blk_cost, uintptr_t blk_mv, uintptr_t prop,
+                     float strength, uintptr_t out, uintptr_t stream) {
+    mivc_launch_mbtree(B, F, lbw, lbh, P<int>(blk_cost), P<int>(blk_mv), P<float>(prop), strength, P<float>(out),
+                       S(stream));
   });
   m.def("qp_fixup", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t coef, uintptr_t nz, uintptr_t flags,
                        uintptr_t slice_qp, uintptr_t stream) {
@@ -221,9 +229,11 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("lookahead_low_bytes", [](int w, int h, int n) { return mivc_lookahead_low_bytes(w, h, n); });
   m.def("lookahead", [](uintptr_t y, int w, int h, long long fstride, int n, int f, uintptr_t low, uintptr_t frame_cost,
-                        uintptr_t blk_cost, int range, uintptr_t stream) {
+                        uintptr_t blk_cost, int range, uintptr_t stream, uintptr_t blk_mv) {
     int rc = mivc_launch_lookahead(P<uint8_t>(y), w, h, fstride, n, f, P<uint8_t>(low),
-                                   P<unsigned long long>(frame_cost), P<int>(blk_cost), range, S(stream));
+                                   P<unsigned long long>(frame_cost), P<int>(blk_cost), P<int>(blk_mv), range,
+                                   S(stream));
     if (rc != 0) throw std::invalid_argument("lookahead: bad geometry or range (4, 6, 8)");
-  });
+  }, py::arg("y"), py::arg("w"), py::arg("h"), py::arg("fstride"), py::arg("n"), py::arg("f"), py::arg("low"),
+     py::arg("frame_cost"), py::arg("blk_cost"), py::arg("range"), py::arg("stream"), py::arg("blk_mv") = 0);
 }

@@ -120,6 +120,7 @@ struct LaArgs {
   const uint8_t* low;
   unsigned long long* frame_cost;  // [N, 2]: sum intra, sum min(intra, inter)
   int* blk_cost;                   // optional [N, 2, lbh, lbw]: intra, inter (inter = intra on key frames)
+  int* blk_mv;                     // optional [N, lbh, lbw]: lowres integer vector (dx & 0xFFFF) | (dy << 16)
 };
 
 template <int R>
@@ -191,6 +192,7 @@ __global__ __launch_bounds__(256) void la_cost(LaArgs a) {
   intra += 5;  // mode-cost bias
 
   int inter = intra;
+  int mvx = 0, mvy = 0;
   if (has_ref) {  // frame-uniform
     const uint8_t* ref = cur - g.lsize;
     // ---- integer full search: lane accumulates the SAD of its two rows, then the column sum
@@ -231,6 +233,8 @@ __global__ __launch_bounds__(256) void la_cost(LaArgs a) {
     const v4i pf = as_s8(__builtin_amdgcn_alignbyte(e1, e0, shb), __builtin_amdgcn_alignbyte(e2, e1, shb),
                          __builtin_amdgcn_alignbyte(f1, f0, shb), __builtin_amdgcn_alignbyte(f2, f1, shb));
     inter = satd_mfma(negH, accS, pf) + 2 * (abs(mdx) + abs(mdy));
+    mvx = mdx;
+    mvy = mdy;
   }
   const int pcost = min(intra, inter);
   if (a.blk_cost && grp == 0 && valid) {
@@ -238,6 +242,9 @@ __global__ __launch_bounds__(256) void la_cost(LaArgs a) {
     a.blk_cost[base] = intra;
     a.blk_cost[base + static_cast<long long>(g.lbh) * g.lbw] = inter;
   }
+  if (a.blk_mv && grp == 0 && valid)
+    a.blk_mv[static_cast<long long>(n) * g.lbh * g.lbw + static_cast<long long>(by) * g.lbw + bx] =
+        (mvx & 0xFFFF) | (mvy << 16);
   const bool mine = grp == 0 && valid;
   const int si = sum64(mine ? intra : 0), sp = sum64(mine ? pcost : 0);
   if (lane == 0) {
@@ -261,7 +268,8 @@ extern "C" long long mivc_lookahead_low_bytes(int w, int h, int N) {
 // low: workspace of mivc_lookahead_low_bytes(); frame_cost: [N, 2] u64 (zeroed here);
 // blk_cost: optional [N, 2, lbh, lbw] int32.
 extern "C" int mivc_launch_lookahead(const uint8_t* y, int w, int h, long long fstride, int N, int F, uint8_t* low,
-                                     unsigned long long* frame_cost, int* blk_cost, int range, void* stream) {
+                                     unsigned long long* frame_cost, int* blk_cost, int* blk_mv, int range,
+                                     void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (w < 16 || h < 16 || (w & 1) || (h & 1) || N <= 0 || F <= 0 || N % F) return -1;
   if (range != 4 && range != 6 && range != 8) return -2;
@@ -279,7 +287,7 @@ extern "C" int mivc_launch_lookahead(const uint8_t* y, int w, int h, long long f
   hipMemsetAsync(frame_cost, 0, sizeof(unsigned long long) * 2 * N, s);
   const long long dwords = static_cast<long long>(N) * g.lrows * (g.ls >> 2);
   hipLaunchKernelGGL(la_downscale, dim3(static_cast<unsigned>((dwords + 255) / 256)), dim3(256), 0, s, y, g, low);
-  LaArgs a{g, low, frame_cost, blk_cost};
+  LaArgs a{g, low, frame_cost, blk_cost, blk_mv};
   const long long waves = static_cast<long long>((g.lbw + 15) >> 4) * g.lbh * N;
   const dim3 grid(static_cast<unsigned>((waves + 3) >> 2));
   switch (range) {

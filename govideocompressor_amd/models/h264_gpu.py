@@ -57,6 +57,9 @@ class H264Params:
     # x264 --aq-mode 1 (variance AQ): per-MB QP offset strength * 1.0397 * (log2(AC energy)
     # - 14.427); 0 disables (every MB at the frame QP)
     aq_strength: float = 1.0
+    # x264 --mbtree (default on): lookahead propagation of inter-frame references -> per-MB
+    # QP offsets (csrc/kernels/mbtree.hip), with x264's CRF compensation; needs the lookahead
+    mbtree: bool = True
 
     def host_cfg(self) -> dict:
         return dict(width=self.width, height=self.height, fps=self.fps, qp=self.qp,
@@ -127,6 +130,7 @@ class GpuH264Encoder:
         self.hmb = (params.height + 15) // 16
         self.W, self.H = self.wmb * 16, self.hmb * 16
         self.nmb = self.wmb * self.hmb
+        self._mbtree = None  # [B, F, nmb] MB-tree QP offsets of the batch being encoded
         B, H, W, nmb, dev = self.B, self.H, self.W, self.nmb, self.dev
         u8, i16, i32 = torch.uint8, torch.int16, torch.int32
 
@@ -211,7 +215,7 @@ class GpuH264Encoder:
                       self._ptr(self.src[0]), self._ptr(self.src[1]), self._ptr(self.src[2]),
                       self.p.width, self.p.height, self.W, self.H, self._stream())
 
-    def _encode_frame(self, idr: bool, cur, ref, hdr, coef, cut=None):
+    def _encode_frame(self, idr: bool, cur, ref, hdr, coef, cut=None, t: int = 0):
         """cut: optional [B] bool device tensor -- slots whose frame is a scene cut (every MB
         intra, as an I picture would be)."""
         s = self._stream()
@@ -219,9 +223,13 @@ class GpuH264Encoder:
         sy, su, sv = (self._ptr(x) for x in self.src)
         ry, ru, rv = (self._ptr(x) for x in cur)
         aq = 0
-        if self.p.aq_strength > 0:
+        mbt = self._mbtree
+        if self.p.aq_strength > 0 or mbt is not None:
             aq = self._ptr(self.aq)
-            self.hip.aq_offsets(B, wmb, hmb, sy, su, sv, float(self.p.aq_strength), aq, s)
+            extra, stride = 0, 0
+            if mbt is not None and mbt.shape[2] == self.nmb:  # [B, F, nmb] float offsets of this batch
+                extra, stride = mbt.data_ptr() + t * self.nmb * 4, mbt.shape[1] * self.nmb
+            self.hip.aq_offsets(B, wmb, hmb, sy, su, sv, float(self.p.aq_strength), aq, s, extra, stride)
         if not idr:
             fy, fu, fv = (self._ptr(x) for x in ref)
             self.intra_count.zero_()
@@ -340,11 +348,17 @@ class GpuH264Encoder:
         if getattr(self, "_la", None) is None:
             self._la = GpuLookahead(self.dev, self.p.la_range)
         t0 = time.perf_counter()
-        costs = self._la.frame_costs(y).cpu().numpy()
+        from ..rc.ratecontrol import MBTREE_STRENGTH, scenecut_flags
         lbw, lbh = GpuLookahead.block_grid(y.shape[3], y.shape[2])
-        from ..rc.ratecontrol import scenecut_flags
+        # MB-tree needs the lookahead's block grid to be the coded MB grid (no -s resize)
+        use_mbtree = self.p.mbtree and lbw * lbh == self.nmb
+        if use_mbtree:
+            costs_d, self._mbtree = self._la.mbtree(y, MBTREE_STRENGTH)
+            costs = costs_d.cpu().numpy()
+        else:
+            costs = self._la.frame_costs(y).cpu().numpy()
         self._scenecuts = scenecut_flags(costs, float(self.p.scenecut))
-        q = crf_qps_batch(costs, float(self.p.crf), lbw * lbh, scenecuts=self._scenecuts)
+        q = crf_qps_batch(costs, float(self.p.crf), lbw * lbh, scenecuts=self._scenecuts, mbtree=use_mbtree)
         self.stats["scenecuts"] = int(self._scenecuts.sum())
         self.timings["lookahead_s"] = self.timings.get("lookahead_s", 0.0) + time.perf_counter() - t0
         self.stats["mean_qp"] = float(q.mean())
@@ -380,6 +394,7 @@ class GpuH264Encoder:
         torch.cuda.set_device(self.dev)
         qp_i, qp_p = self.p.frame_qps()
         self._scenecuts = None
+        self._mbtree = None
         if qps is None and self.p.crf is not None and self.p.lookahead:
             qps = self.crf_qps(y)
         cuts_h = self._scenecuts if self._scenecuts is not None else np.zeros((B, F), dtype=bool)
@@ -423,7 +438,7 @@ class GpuH264Encoder:
             self._prep(y, u, v, t)
             self.qp.copy_(qps_d[t])
             self._encode_frame(idr, cur, ref, self.hdr[k], self.coef[k],
-                               cuts_d[t] if (not idr and cuts_h[:, t].any()) else None)
+                               cuts_d[t] if (not idr and cuts_h[:, t].any()) else None, t)
             if metrics:
                 self.hip.sse(B, self.W, self.H, self.p.width, self.p.height, self._ptr(self.src[0]),
                              self._ptr(self.src[1]), self._ptr(self.src[2]), self._ptr(cur[0]), self._ptr(cur[1]),

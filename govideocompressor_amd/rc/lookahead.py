@@ -47,12 +47,30 @@ class GpuLookahead:
         return self._low, self._cost[:n]
 
     @torch.no_grad()
-    def frame_costs(self, y: torch.Tensor, block_costs: bool = False):
+    def mbtree(self, y: torch.Tensor, strength: float = 2.0):
+        """Frame costs plus MB-tree QP offsets (csrc/kernels/mbtree.hip).
+
+        Returns ([B, F, 2] int64 frame costs, [B, F, lbh * lbw] float32 per-MB QP offsets,
+        one lowres 8x8 block per 16x16 MB), both on the device."""
+        B, F, h, w = y.shape
+        lbw, lbh = self.block_grid(w, h)
+        costs, blk, mv = self.frame_costs(y, block_costs=True, block_mvs=True)
+        n = B * F * lbw * lbh
+        if getattr(self, "_prop", None) is None or self._prop.numel() < n:
+            self._prop = torch.empty((n,), dtype=torch.float32, device=self.dev)
+        out = torch.empty((B, F, lbh * lbw), dtype=torch.float32, device=self.dev)
+        self.hip.mbtree(B, F, lbw, lbh, blk.data_ptr(), mv.data_ptr(), self._prop.data_ptr(), float(strength),
+                        out.data_ptr(), torch.cuda.current_stream(self.dev).cuda_stream)
+        return costs, out
+
+    @torch.no_grad()
+    def frame_costs(self, y: torch.Tensor, block_costs: bool = False, block_mvs: bool = False):
         """y: [B, F, h, w] uint8 luma on the device (the encoder's input layout).
 
         Returns a device tensor [B, F, 2] int64 = (sum of intra costs, sum of
         min(intra, inter) costs) per frame (the first frame of a segment is intra
-        only), and with ``block_costs`` also [B, F, 2, lbh, lbw] int32 per-block costs.
+        only), and with ``block_costs`` also [B, F, 2, lbh, lbw] int32 per-block costs
+        (and with ``block_mvs`` [B, F, lbh, lbw] int32 packed lowres vectors, dx | dy << 16).
         """
         if y.dtype != torch.uint8 or y.dim() != 4 or y.device != self.dev:
             raise ValueError("y must be a uint8 [B, F, h, w] tensor on the lookahead's device")
@@ -63,14 +81,18 @@ class GpuLookahead:
             raise ValueError("frame size must be even and at least 16x16")
         n = B * F
         low, cost = self._workspace(w, h, n)
-        blk = None
+        blk = mv = None
+        lbw, lbh = self.block_grid(w, h)
         if block_costs:
-            lbw, lbh = self.block_grid(w, h)
             blk = torch.zeros((B, F, 2, lbh, lbw), dtype=torch.int32, device=self.dev)
+        if block_mvs:
+            mv = torch.zeros((B, F, lbh, lbw), dtype=torch.int32, device=self.dev)
         self.hip.lookahead(y.data_ptr(), w, h, y.stride(1), n, F, low.data_ptr(), cost.data_ptr(),
                            blk.data_ptr() if blk is not None else 0, self.range,
-                           torch.cuda.current_stream(self.dev).cuda_stream)
+                           torch.cuda.current_stream(self.dev).cuda_stream, mv.data_ptr() if mv is not None else 0)
         out = cost.view(B, F, 2)
+        if block_mvs:
+            return out, blk, mv
         return (out, blk) if block_costs else out
 
 

@@ -30,6 +30,10 @@ import numpy as np
 
 QCOMP = 0.6
 IP_OFFSET = 3          # I-frame QP = P QP - 3 (ipratio 1.4)
+# x264 ratecontrol.c: with MB-tree the CRF constant is taken (1 - qcomp) * 13.5 QP higher;
+# the (mostly negative) MB-tree offsets bring propagated blocks back down
+MBTREE_CRF_OFFSET = (1.0 - QCOMP) * 13.5
+MBTREE_STRENGTH = 5.0 * (1.0 - QCOMP)
 QP_MIN, QP_MAX = 0, 51
 
 
@@ -117,7 +121,8 @@ def scenecut_flags(costs: np.ndarray, scenecut: float = 40.0, keyint: int | None
 
 
 def crf_qps_batch(costs: np.ndarray, crf: float, mb_count: int, keyint: int | None = None, blur: float = 0.5,
-                  qp_min: int = QP_MIN, qp_max: int = QP_MAX, scenecuts: np.ndarray | None = None) -> np.ndarray:
+                  qp_min: int = QP_MIN, qp_max: int = QP_MAX, scenecuts: np.ndarray | None = None,
+                  mbtree: bool = False) -> np.ndarray:
     """:func:`crf_qps` for B closed-GOP segments at once.
 
     ``costs``: [B, F, 2] lowres frame costs (intra, min(intra, inter)) as produced by
@@ -141,7 +146,7 @@ def crf_qps_batch(costs: np.ndarray, crf: float, mb_count: int, keyint: int | No
         wsum = wsum * blur + 1.0
         blurred[:, t] = acc / wsum
     base = 80.0 * mb_count
-    rate_factor = base ** (1.0 - QCOMP) / qp2qscale(crf)
+    rate_factor = base ** (1.0 - QCOMP) / qp2qscale(crf + (MBTREE_CRF_OFFSET if mbtree else 0.0))
     qs = np.maximum(blurred ** (1.0 - QCOMP) / rate_factor, 1e-9)
     qp = 12.0 + 6.0 * np.log2(qs / 0.85)
     qp[key] -= IP_OFFSET

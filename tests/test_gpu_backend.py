@@ -39,7 +39,7 @@ def test_gpu_backend_batch(tmp_path, host):
         assert len(pics) == c.frames
         assert sum(p["idr"] for p in pics) == (c.frames + 4) // 5
         y = np.stack([p["i420"][: 176 * 144].reshape(144, 176) for p in pics])
-        assert _psnr(y, c.y) > 28  # CRF 23 with variance AQ (x264 defaults) on noise-textured content
+        assert _psnr(y, c.y) > 27  # CRF 23 with AQ + MB-tree (x264 defaults) on noise-textured content
         assert os.path.exists(j.log_path)
 
 
@@ -71,4 +71,4 @@ def test_pipeline_encode_file_gpu(tmp_path, host):
     pics = host.decode(open(out, "rb").read())
     assert len(pics) == 40
     y = np.stack([p["i420"][: 320 * 240].reshape(240, 320) for p in pics])
-    assert _psnr(y, c.y) > 28  # CRF 23 with variance AQ (x264 defaults)
+    assert _psnr(y, c.y) > 27  # CRF 23 with AQ + MB-tree (x264 defaults)

@@ -90,3 +90,47 @@ def test_encoder_uses_lookahead_qps():
     assert "lookahead_s" in enc.timings
     enc.close()
     torch.cuda.synchronize()
+
+
+def _mbtree_reference(blk, mv, strength):
+    """numpy statement of csrc/kernels/mbtree.hip (x264 macroblock_tree_propagate)."""
+    B, F, _, lbh, lbw = blk.shape
+    prop = np.zeros((B, F, lbh, lbw))
+    for b in range(B):
+        for t in range(F - 1, 0, -1):
+            for by in range(lbh):
+                for bx in range(lbw):
+                    intra = float(blk[b, t, 0, by, bx])
+                    inter = min(float(blk[b, t, 1, by, bx]), intra)
+                    if intra <= 0 or inter >= intra:
+                        continue
+                    amount = (prop[b, t, by, bx] + intra) * (intra - inter) / intra
+                    m = int(mv[b, t, by, bx])
+                    dx = ((m & 0xFFFF) ^ 0x8000) - 0x8000
+                    dy = m >> 16
+                    x, y = bx * 8 + dx, by * 8 + dy
+                    x0, y0, fx, fy = x >> 3, y >> 3, x & 7, y & 7
+                    for cy, wy in ((y0, 8 - fy), (y0 + 1, fy)):
+                        for cx, wx in ((x0, 8 - fx), (x0 + 1, fx)):
+                            if wx * wy and 0 <= cx < lbw and 0 <= cy < lbh:
+                                prop[b, t - 1, cy, cx] += amount * wx * wy / 64.0
+    intra = np.maximum(blk[:, :, 0].astype(np.float64), 1.0)
+    return -strength * np.log2((intra + prop) / intra)
+
+
+@pytest.mark.gpu
+def test_mbtree_matches_reference():
+    import torch
+
+    from govideocompressor_amd.models.h264_gpu import synth_clip
+    from govideocompressor_amd.rc.lookahead import GpuLookahead
+
+    y, _, _ = synth_clip(2, 5, 160, 96, seed=3, device="cuda:0")
+    la = GpuLookahead("cuda:0", 6)
+    _, blk, mv = la.frame_costs(y, block_costs=True, block_mvs=True)
+    _, off = la.mbtree(y, 2.0)
+    torch.cuda.synchronize()
+    ref = _mbtree_reference(blk.cpu().numpy().astype(np.int64), mv.cpu().numpy(), 2.0)
+    got = off.cpu().numpy().reshape(ref.shape)
+    assert np.allclose(got, ref, rtol=1e-4, atol=1e-3)
+    assert (got[:, -1] == 0).all() and got[:, 0].mean() < -0.1  # early frames are referenced
