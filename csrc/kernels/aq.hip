@@ -70,15 +70,16 @@ __global__ __launch_bounds__(256) void h264_aq_offsets(Geom g, const uint8_t* __
   }
 }
 
-// Two MBs per wave (halves).  The MB carries mb_qp_delta iff it is Intra16x16 or has a
-// non-zero level (coded_block_pattern != 0): luma from the encoder's per-block non-zero
-// flags (lane 9, 16 bytes), chroma AC from coefficient 1 (lanes 0..7), chroma DC (lane 8).
-__global__ __launch_bounds__(64) void h264_qp_flags(Geom g, const MbHeader* __restrict__ hdr,
-                                                    const int16_t* __restrict__ coef, const uint8_t* __restrict__ nzf,
-                                                    uint8_t* __restrict__ flags) {
-  const int lane = lane_id(), sub = lane & 31, half = lane >> 5;
+// 16 lanes per MB (16 MBs per 256-thread workgroup).  The MB carries mb_qp_delta iff it
+// is Intra16x16 or has a non-zero level (coded_block_pattern != 0): luma from the encoder's
+// per-block non-zero flags (lane 9, 16 bytes), chroma AC from coefficient 1 (lanes 0..7),
+// chroma DC (lane 8), the MB kind (lane 10).
+__global__ __launch_bounds__(256) void h264_qp_flags(Geom g, const MbHeader* __restrict__ hdr,
+                                                     const int16_t* __restrict__ coef, const uint8_t* __restrict__ nzf,
+                                                     uint8_t* __restrict__ flags) {
+  const int lane = lane_id(), sub = lane & 15, grp = lane >> 4;
   const int nmb = g.nmb();
-  const int mb = blockIdx.x * 2 + half, slot = blockIdx.y;
+  const int mb = blockIdx.x * 16 + (threadIdx.x >> 4), slot = blockIdx.y;
   const bool live = mb < nmb;
   const size_t o = static_cast<size_t>(slot) * nmb + (live ? mb : 0);
   const int16_t* c = coef + o * h264::kCoefPerMb;
@@ -97,8 +98,7 @@ __global__ __launch_bounds__(64) void h264_qp_flags(Geom g, const MbHeader* __re
     nz = hdr[o].kind == h264::MBK_I16x16;
   }
   const uint64_t bal = __ballot(nz);
-  const uint32_t mine = half ? static_cast<uint32_t>(bal >> 32) : static_cast<uint32_t>(bal);
-  if (live && sub == 0) flags[o] = mine != 0 ? 1 : 0;
+  if (live && sub == 0) flags[o] = ((bal >> (16 * grp)) & 0xFFFFu) != 0 ? 1 : 0;
 }
 
 // One workgroup per slot: chunked segmented scan of "last MB with mb_qp_delta".
@@ -147,7 +147,7 @@ extern "C" void mivc_launch_qp_fixup(int B, int wmb, int hmb, void* hdr, const i
                                      uint8_t* flags, const int* slice_qp, void* stream) {
   const Geom g{B, wmb, hmb, wmb * 16, hmb * 16};
   hipStream_t s = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(h264_qp_flags, dim3((wmb * hmb + 1) / 2, B), dim3(64), 0, s, g,
+  hipLaunchKernelGGL(h264_qp_flags, dim3((wmb * hmb + 15) / 16, B), dim3(256), 0, s, g,
                      static_cast<const mivc::h264::MbHeader*>(hdr), coef, nz, flags);
   hipLaunchKernelGGL(h264_qp_fixup, dim3(B), dim3(1024), 0, s, g, static_cast<mivc::h264::MbHeader*>(hdr), flags,
                      slice_qp);

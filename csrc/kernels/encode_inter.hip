@@ -76,8 +76,21 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
   const int mx = mbc % g.wmb, my = mbc / g.wmb;
   const size_t o = static_cast<size_t>(slot) * nmb + mbc;
   const int W = g.W, cw = g.cw(), CH = g.ch();
-  const int qp = clampi(a.qp[slot] + (a.aq ? a.aq[o] : 0), 0, 51);
-  const int qpc = h264::chroma_qp(qp, a.chroma_qp_offset);
+  // QP is uniform within each half-wave (one MB) but, with adaptive quantisation, not
+  // across the wave: fetch both halves' QPs into SGPRs so every table row below is a
+  // scalar load, then select per lane
+  const int qp_l = clampi(a.qp[slot] + (a.aq ? a.aq[o] : 0), 0, 51);
+  const int qp0 = __builtin_amdgcn_readlane(qp_l, 0), qp1 = __builtin_amdgcn_readlane(qp_l, 32);
+  const int qpc0 = h264::chroma_qp(qp0, a.chroma_qp_offset), qpc1 = h264::chroma_qp(qp1, a.chroma_qp_offset);
+  const int qp = half ? qp1 : qp0, qpc = half ? qpc1 : qpc0;
+  int mf[3], mfc[3], dv[3], dvc[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    mf[c] = half ? h264::kQuantMF[qp1 % 6][c] : h264::kQuantMF[qp0 % 6][c];
+    mfc[c] = half ? h264::kQuantMF[qpc1 % 6][c] : h264::kQuantMF[qpc0 % 6][c];
+    dv[c] = half ? h264::kDequantV[qp1 % 6][c] : h264::kDequantV[qp0 % 6][c];
+    dvc[c] = half ? h264::kDequantV[qpc1 % 6][c] : h264::kDequantV[qpc0 % 6][c];
+  }
 
   __shared__ int s_score[2][24];
   __shared__ int s_cdc[2][2][4];
@@ -123,7 +136,7 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
     h264::forward_core4x4(res);
     const int qbits = 15 + qp / 6;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) lv[r] = h264::quant_coef(res[r], h264::kQuantMF[qp % 6][h264::kPosClass[r]], qbits, 11);
+    for (int r = 0; r < 16; ++r) lv[r] = h264::quant_coef(res[r], mf[h264::kPosClass[r]], qbits, 11);
     int scan[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) scan[i] = lv[h264::kZigzag4x4[i]];
@@ -172,7 +185,7 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
     const int qbits = 15 + qpc / 6;
 #pragma unroll
     for (int r = 0; r < 16; ++r)
-      lv[r] = r == 0 ? 0 : h264::quant_coef(res[r], h264::kQuantMF[qpc % 6][h264::kPosClass[r]], qbits, 11);
+      lv[r] = r == 0 ? 0 : h264::quant_coef(res[r], mfc[h264::kPosClass[r]], qbits, 11);
     int scan[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) scan[i] = lv[h264::kZigzag4x4[i]];
@@ -186,7 +199,7 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
     const int f[4] = {d0 + d1 + d2 + d3, d0 - d1 + d2 - d3, d0 + d1 - d2 - d3, d0 - d1 - d2 + d3};
     const int qbits = 15 + qpc / 6;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) s_clev[half][c][i] = h264::quant_coef(f[i], h264::kQuantMF[qpc % 6][0], qbits + 1, 11);
+    for (int i = 0; i < 4; ++i) s_clev[half][c][i] = h264::quant_coef(f[i], mfc[0], qbits + 1, 11);
   }
   if (work && hl == 0) {
     int keep = 0, total = 0;
@@ -228,7 +241,7 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
     }
     store_levels(coef + h264::COEF_LUMA + hl * 16, sv);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) res[r] = keep ? h264::dequant_coef(lv[r], qp, r) : 0;
+    for (int r = 0; r < 16; ++r) res[r] = keep ? (lv[r] * dv[h264::kPosClass[r]]) << (qp / 6) : 0;
     if (any) h264::inverse_core4x4(res);
     uint8_t* recy = a.rec_y + slot * g.ysize() + static_cast<size_t>(Y0 + lby) * W + X0 + lbx;
 #pragma unroll
@@ -253,9 +266,9 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
     const int* cl = s_clev[half][comp];
     const int f[4] = {cl[0] + cl[1] + cl[2] + cl[3], cl[0] - cl[1] + cl[2] - cl[3], cl[0] + cl[1] - cl[2] - cl[3],
                       cl[0] - cl[1] - cl[2] + cl[3]};
-    const int ls = 16 * h264::kDequantV[qpc % 6][0];
+    const int ls = 16 * dvc[0];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) res[r] = (keep_ac && r > 0) ? h264::dequant_coef(lv[r], qpc, r) : 0;
+    for (int r = 0; r < 16; ++r) res[r] = (keep_ac && r > 0) ? (lv[r] * dvc[h264::kPosClass[r]]) << (qpc / 6) : 0;
     res[0] = ((f[cb] * ls) << (qpc / 6)) >> 5;
     const bool any = any_ac || cl[0] || cl[1] || cl[2] || cl[3];
     if (any) h264::inverse_core4x4(res);
