@@ -33,6 +33,7 @@ constexpr int kRingU = 4;       // bottom-edge slots from a wave's upper half to
 constexpr int LT = 20;          // luma tile stride: 4 halo + 16 (rows -4..15, cols -4..15)
 constexpr int CT = 12;          // chroma tile stride: 4 halo + 8 (rows -4..7, cols -4..7)
 constexpr int kSlotWords = 24;  // luma rows 12..15 (16 words) + Cb/Cr rows 6..7 (2 x 4 words)
+constexpr int kMaxCols = 480;   // MB columns (8K: 7680 / 16)
 
 // Layout.  Wave w deblocks MB rows 2w + 32k (upper half-wave, lanes
 // 0..31) and 2w + 32k + 1 (lower half, lanes 32..63) in lock step, the lower half two MBs
@@ -122,7 +123,12 @@ __device__ __forceinline__ void edges4(uint32_t (&d)[5], const DeblockShared& S,
 
 __global__ __launch_bounds__(64 * kDeblockWaves) void deblock_wavefront(DeblockArgs a) {
   __shared__ DeblockShared SS[kDeblockWaves][2];
-  __shared__ uint32_t ringL[kDeblockWaves][kRing][kSlotWords];   // lower half -> next wave's upper half
+  __shared__ uint32_t ringL[kDeblockWaves - 1][kRing][kSlotWords];  // lower half -> next wave's upper half
+  // The last wave's lower row feeds the FIRST row of the next band, which wave 0 starts only
+  // after its own band is done: a short ring there would make the last wave wait on a row
+  // that waits on it (a deadlock once the row is wider than the waves' combined slack), so
+  // that hand-off gets one slot per MB column.
+  __shared__ uint32_t ringB[kMaxCols][kSlotWords];
   __shared__ uint32_t ringU[kDeblockWaves][kRingU][kSlotWords];  // upper half -> own lower half
   __shared__ int prog[kMaxRows];
   __shared__ DeblockTables T;
@@ -186,7 +192,12 @@ __global__ __launch_bounds__(64 * kDeblockWaves) void deblock_wavefront(DeblockA
     const bool last_row = y == hmb - 1;
     const bool has_top = y > 0;
     // this wave's lower ring still holds bottom edges of row yl - 32 until row yl - 31 used them
-    if (half && yl >= 2 * kDeblockWaves && row_ok && (lane_id() & 31) == 0) row_wait_lds(prog, yl - 2 * kDeblockWaves + 1, wmb, a.err);
+    // (waves 0..14) this wave's lower ring still holds bottom edges of row yl - 32 until row
+    // yl - 31 (the next wave's upper row of the previous band) used them.  The last wave's
+    // band hand-off buffer is guarded per column instead (see below): a whole-row wait
+    // there would wait on the next band's first row, which waits on this wave.
+    if (half && w < kDeblockWaves - 1 && yl >= 2 * kDeblockWaves && row_ok && (lane_id() & 31) == 0)
+      row_wait_lds(prog, yl - 2 * kDeblockWaves + 1, wmb, a.err);
     uint32_t nxt[5] = {0, 0, 0, 0, 0};
     if (!half) load_inputs(0, y, nxt);
     for (int step = 0; step < wmb + 2; ++step) {
@@ -252,7 +263,7 @@ __global__ __launch_bounds__(64 * kDeblockWaves) void deblock_wavefront(DeblockA
           if (!half) row_wait_lds(prog, y - 1, min(x + 2, wmb), a.err);
           if (hl < kSlotWords) {
             const uint32_t v = half ? ringU[w][x % kRingU][hl]
-                                    : ringL[(w + kDeblockWaves - 1) % kDeblockWaves][x % kRing][hl];
+                                    : (w == 0 ? ringB[x][hl] : ringL[w - 1][x % kRing][hl]);
             if (hl < 16) *reinterpret_cast<uint32_t*>(&S.ty[(hl >> 2) * LT + 4 + (hl & 3) * 4]) = v;
             else {
               const int c = (hl - 16) >> 2, r = ((hl - 16) >> 1) & 1, h = hl & 1;
@@ -365,7 +376,17 @@ __global__ __launch_bounds__(64 * kDeblockWaves) void deblock_wavefront(DeblockA
             vp = h == 0 ? S.bot_c[c][r] : *reinterpret_cast<const uint32_t*>(&S.tc[c][(r + 10) * CT]);
             vc = *reinterpret_cast<const uint32_t*>(&S.tc[c][(r + 10) * CT + 4 + 4 * h]);
           }
-          if (half) {
+          if (half && w == kDeblockWaves - 1) {
+            // column c of the previous band's hand-off was consumed by row y - 31 at its step c
+            if (has_left) {
+              if (y >= 2 * kDeblockWaves) row_wait_lds(prog, y - 2 * kDeblockWaves + 1, x, a.err);
+              ringB[x - 1][hl] = vp;
+            }
+            if (last_col) {
+              if (y >= 2 * kDeblockWaves) row_wait_lds(prog, y - 2 * kDeblockWaves + 1, x + 1, a.err);
+              ringB[x][hl] = vc;
+            }
+          } else if (half) {
             if (has_left) {
               if (x - 1 >= kRing) row_wait_lds(prog, y + 1, x - kRing, a.err);
               ringL[w][(x - 1) % kRing][hl] = vp;

@@ -80,8 +80,8 @@ __device__ __forceinline__ void row_wait_lds(int* prog, int row, int target, int
   int spins = 0;
   while (__hip_atomic_load(prog + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
     __builtin_amdgcn_s_sleep(1);
-    if (++spins > (1 << 24)) {
-      if (lane_id() == 0) atomicOr(err, 1);
+    if (++spins > (1 << 22)) {
+      atomicOr(err, 1);  // any waiting lane (callers wait from divergent lane subsets)
       break;
     }
   }

@@ -157,3 +157,11 @@ def test_gpu_adaptive_quant(host):
         pics = host.decode(out["gpu"][b])
         assert any(np.unique(np.asarray(p["mb_qp"])).size > 3 for p in pics)
     torch.cuda.synchronize()
+
+
+def test_gpu_h264_wide_multiband_roundtrip(host):
+    """Rows wider than the deblocking waves' combined ring slack, over several 32-row bands
+    (the band-boundary hand-off of deblock.hip): bit-exact and no wavefront stall."""
+    enc, res, _ = _run(4096, 544, slots=1, frames=2, crf=None, qp=30)
+    _check_roundtrip(host, enc, res, 4096, 544)
+    assert int(enc.err.item()) == 0
