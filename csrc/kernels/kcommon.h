@@ -50,7 +50,23 @@ __device__ __forceinline__ int satd16(int* r) {
 // cache write-back/invalidate (agent-scope fences cost 1.7-7 us per hand-off on
 // MI355X, guide §Persistent kernels price list; the first version of these
 // kernels spent ~20 us per MB step there).
-constexpr int kMaxRows = 272;  // 8K: 4320 / 16 = 270 MB rows
+constexpr int kMaxRows = 272;
+
+// Keep memory freed with hipFreeAsync in the device's default pool (release threshold
+// "never"): by default the pool hands it back to the driver at every synchronisation, and
+// the next stream-ordered allocation of the same size re-maps it (~100 ms for a GB-sized
+// per-batch workspace).  Host-side helper for the launchers.
+inline void keep_async_pool() {
+  static bool done[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || done[dev]) return;
+  hipMemPool_t pool;
+  if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+    uint64_t thr = ~0ull;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+  }
+  done[dev] = true;
+}  // 8K: 4320 / 16 = 270 MB rows
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }

@@ -669,6 +669,7 @@ extern "C" void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, co
   uint8_t* hp = hp_buf;
   if (!hp) {
     const size_t hp_bytes = static_cast<size_t>(B) * 3 * (W + 2 * kHpM) * (H + 2 * kHpM) + 64;
+    keep_async_pool();
     if (hipMallocAsync(reinterpret_cast<void**>(&hp), hp_bytes, s) != hipSuccess) {
       fprintf(stderr, "mivc_launch_me: hipMallocAsync(%zu) failed\n", hp_bytes);
       abort();

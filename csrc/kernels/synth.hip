@@ -411,6 +411,7 @@ extern "C" void mivc_launch_synth(uint8_t* y, uint8_t* u, uint8_t* v, int width,
   const size_t ysz = static_cast<size_t>(g.cw) * g.ch, csz = ysz / 4;
   const size_t bytes = slots * (ysz + 2 * csz + 3 * tile_stride);
   uint8_t* ws = nullptr;
+  keep_async_pool();
   if (hipMallocAsync(reinterpret_cast<void**>(&ws), bytes, s) != hipSuccess) return;
   uint8_t* cy = ws;
   uint8_t* cu = cy + slots * ysz;
