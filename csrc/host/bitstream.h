@@ -154,6 +154,7 @@ struct NalUnit {
   size_t offset = 0;       // offset of the start code in the Annex-B stream
   size_t size = 0;         // bytes incl. start code
   std::vector<uint8_t> rbsp;  // payload with emulation-prevention bytes removed
+  std::vector<uint32_t> epb;  // rbsp index of the byte each removed emulation-prevention byte preceded
 };
 
 // Split an Annex-B byte stream into NAL units (B.2) and unescape the payloads.
@@ -190,6 +191,7 @@ inline std::vector<NalUnit> parse_annexb(const uint8_t* p, size_t n, bool unesca
         uint8_t c = p[j];
         if (zeros >= 2 && c == 3) {
           zeros = 0;
+          u.epb.push_back(static_cast<uint32_t>(u.rbsp.size()));
           continue;
         }
         u.rbsp.push_back(c);

@@ -213,6 +213,15 @@ class CabacDecoder {
     return v;
   }
 
+  // after a terminating bin equal to 1 the engine has consumed the flush's final 1 bit;
+  // skip the alignment zeros to the next substream
+  void align() {
+    while (pos_ & 7) {
+      if (read_bit() != 0) throw std::runtime_error("CABAC: non-zero alignment bit");
+    }
+  }
+  size_t byte_pos() const { return pos_ >> 3; }
+
   int terminate() {
     range_ -= 2;
     if (offset_ >= range_) return 1;

@@ -26,6 +26,8 @@ struct HevcConfig {
   int sao = 1;
   int deblock = 1;
   int max_merge = 5;
+  int wpp = 0;                 // entropy_coding_sync_enabled_flag: one CABAC substream per CTB row
+  int threads = 1;             // host threads coding the WPP substreams of one picture
   int coded_width() const { return (width + kCtb - 1) / kCtb * kCtb; }
   int coded_height() const { return (height + kCtb - 1) / kCtb * kCtb; }
   int wctb() const { return coded_width() / kCtb; }

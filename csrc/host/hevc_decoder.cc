@@ -182,7 +182,7 @@ struct HevcDecoder::Impl {
     p.bypass = br.get(1);
     p.tiles = br.get(1);
     p.wpp = br.get(1);
-    if (p.sign_hiding || p.tskip || p.bypass || p.tiles || p.wpp || p.weighted || p.constrained_intra ||
+    if (p.sign_hiding || p.tskip || p.bypass || p.tiles || p.weighted || p.constrained_intra ||
         p.slice_chroma_offsets || p.dep_slices || p.output_flag || p.extra_bits)
       throw std::runtime_error("HEVC: PPS tool outside the supported subset");
     p.lf_across_slices = br.get(1);
@@ -288,6 +288,17 @@ struct HevcDecoder::Impl {
     deblock = !pps.deblock_disabled;
     if (pps.deblock_override && br.get(1)) throw std::runtime_error("HEVC: deblocking override unsupported");
     if (pps.lf_across_slices && (sao_luma || sao_chroma || deblock)) br.get(1);
+    std::vector<uint32_t> entry;  // entry_point_offset_minus1 + 1 (escaped bytes, 7.4.7.1)
+    if (pps.wpp) {
+      const uint32_t ne = br.get_ue();
+      const int ctb = 1 << sps.log2_ctb;
+      if (ne != static_cast<uint32_t>((sps.H + ctb - 1) / ctb - 1)) throw std::runtime_error("HEVC: WPP entry points != CTB rows - 1");
+      if (ne > 0) {
+        const int len = br.get_ue() + 1;
+        if (len > 32) throw std::runtime_error("HEVC: offset_len_minus1 out of range");
+        for (uint32_t k = 0; k < ne; ++k) entry.push_back(br.get(len) + 1);
+      }
+    }
     if (pps.ext_header) {
       const int n = br.get_ue();
       for (int i = 0; i < n; ++i) br.get(8);
@@ -303,12 +314,35 @@ struct HevcDecoder::Impl {
     dec.start();
     init_contexts(ctx, slice_type == 2 ? 0 : 1, qp);
     const int nctb = wctb * hctb;
+    const size_t data0 = 1 + br.pos() / 8;  // rbsp index of the slice data
+    auto escaped = [&](size_t r) {  // rbsp index -> byte offset in the escaped NAL payload
+      size_t k = 0;
+      while (k < nal.epb.size() && nal.epb[k] < r) ++k;
+      return r + k;
+    };
+    size_t sub_start = data0;
+    CtxState wpp_ctx[kNumCtx];
     for (int i = 0; i < nctb; ++i) {
       const int rx = i % wctb, ry = i / wctb;
+      if (pps.wpp && rx == 0 && ry > 0) {
+        // 9.3.1: new substream, contexts synchronised from CTB (1, ry-1) when it exists
+        const size_t at = 1 + dec.byte_pos();
+        if (escaped(at) - escaped(sub_start) != entry[ry - 1])
+          throw std::runtime_error("HEVC: WPP entry point offset mismatch");
+        sub_start = at;
+        dec.start();
+        if (wctb >= 2) std::copy(wpp_ctx, wpp_ctx + kNumCtx, ctx);
+        else init_contexts(ctx, slice_type == 2 ? 0 : 1, qp);
+      }
       if (sps.sao && (sao_luma || sao_chroma)) parse_sao(rx, ry);
       coding_quadtree(rx << sps.log2_ctb, ry << sps.log2_ctb, sps.log2_ctb, 0, rx, ry);
       const int end = dec.terminate();
       if (end != (i == nctb - 1)) throw std::runtime_error("HEVC: end_of_slice_segment_flag mismatch");
+      if (pps.wpp && rx == 1) std::copy(ctx, ctx + kNumCtx, wpp_ctx);
+      if (pps.wpp && rx == wctb - 1 && i != nctb - 1) {
+        if (dec.terminate() != 1) throw std::runtime_error("HEVC: end_of_subset_one_bit != 1");
+        dec.align();  // byte_alignment(): the flush's final 1 bit is alignment_bit_equal_to_one
+      }
     }
     cd = nullptr;
     if (!skip_filters) {

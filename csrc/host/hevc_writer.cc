@@ -1,9 +1,14 @@
 // HEVC parameter sets, slice header and CABAC slice data from decision records.
 // Clause numbers refer to ITU-T H.265.  See hevc_codec.h for the coding-tool subset.
 #include <algorithm>
+#include <array>
+#include <memory>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
+#include <exception>
 #include <stdexcept>
+#include <thread>
 
 #include "bitstream.h"
 #include "hevc_cabac.h"
@@ -157,7 +162,7 @@ std::vector<uint8_t> hevc_parameter_sets(const HevcConfig& c) {
     bw.put_bit(0);  // weighted_bipred_flag
     bw.put_bit(0);  // transquant_bypass_enabled_flag
     bw.put_bit(0);  // tiles_enabled_flag
-    bw.put_bit(0);  // entropy_coding_sync_enabled_flag
+    bw.put_bit(c.wpp ? 1 : 0);  // entropy_coding_sync_enabled_flag
     bw.put_bit(0);  // pps_loop_filter_across_slices_enabled_flag
     bw.put_bit(c.deblock ? 0 : 1);  // deblocking_filter_control_present_flag
     if (!c.deblock) {
@@ -178,6 +183,14 @@ std::vector<uint8_t> hevc_parameter_sets(const HevcConfig& c) {
 namespace {
 
 // ------------------------------------------------------------------ slice writer state
+struct PicState {
+  std::vector<int8_t> depth, skip, pred, mode;
+  std::vector<int16_t> mvx, mvy;
+  std::vector<uint8_t> coded;
+  explicit PicState(size_t n)
+      : depth(n, 0), skip(n, 0), pred(n, 0), mode(n, 1), mvx(n, 0), mvy(n, 0), coded(n, 0) {}
+};
+
 struct Writer {
   const HevcConfig& c;
   const HevcFrameParams& fp;
@@ -189,14 +202,17 @@ struct Writer {
   HevcSliceStats st;
   int W, H, wctb, hctb, w8, h8;
   bool pslice;
-  // per 8x8 granule of the picture (raster): state of already-coded CUs
-  std::vector<int8_t> depth, skip, pred, mode;
-  std::vector<int16_t> mvx, mvy;
-  std::vector<uint8_t> coded;
+  // per 8x8 granule of the picture (raster): state of already-coded CUs, shared by the
+  // substream writers of one picture (WPP rows only read granules their 2-CTB lag
+  // guarantees are final)
+  std::vector<int8_t>&depth, &skip, &pred, &mode;
+  std::vector<int16_t>&mvx, &mvy;
+  std::vector<uint8_t>& coded;
 
   Writer(const HevcConfig& cfg, const HevcFrameParams& f, const CtuInfo* ct, const CuInfo* cu_, const int16_t* cy,
-         const int16_t* cb, const int16_t* cr, CabacEncoder& enc)
-      : c(cfg), fp(f), ctu(ct), cu(cu_), e(enc) {
+         const int16_t* cb, const int16_t* cr, CabacEncoder& enc, PicState& ps)
+      : c(cfg), fp(f), ctu(ct), cu(cu_), e(enc), depth(ps.depth), skip(ps.skip), pred(ps.pred), mode(ps.mode),
+        mvx(ps.mvx), mvy(ps.mvy), coded(ps.coded) {
     coef[0] = cy;
     coef[1] = cb;
     coef[2] = cr;
@@ -207,14 +223,6 @@ struct Writer {
     w8 = W / 8;
     h8 = H / 8;
     pslice = fp.slice_type == 1;
-    const size_t n = static_cast<size_t>(w8) * h8;
-    depth.assign(n, 0);
-    skip.assign(n, 0);
-    pred.assign(n, 0);
-    mode.assign(n, 1);
-    mvx.assign(n, 0);
-    mvy.assign(n, 0);
-    coded.assign(n, 0);
     init_contexts(ctx, pslice ? 1 : 0, fp.qp);
   }
 
@@ -786,27 +794,129 @@ std::vector<uint8_t> hevc_write_slice(const HevcConfig& c, const HevcFrameParams
     bw.put_ue(5 - c.max_merge);  // five_minus_max_num_merge_cand
   }
   bw.put_se(fp.qp - 26);      // slice_qp_delta (init_qp 26)
-  // byte_alignment()
-  bw.put_bit(1);
-  bw.align_zero();
-  CabacEncoder enc(bw);
-  enc.start();
-  Writer w(c, fp, ctu, cu, coef_y, coef_cb, coef_cr, enc);
-  const int n = c.wctb() * c.hctb();
-  for (int i = 0; i < n; ++i) {
-    const int rx = i % c.wctb(), ry = i / c.wctb();
-    if (c.sao) w.write_sao(rx, ry);
-    w.write_ctu(rx, ry);
-    enc.terminate(i == n - 1);  // end_of_slice_segment_flag
+  const int wctb = c.wctb(), hctb = c.hctb(), n = wctb * hctb;
+  PicState ps(static_cast<size_t>(c.coded_width() / 8) * (c.coded_height() / 8));
+  HevcSliceStats total;
+  std::vector<uint8_t> data;  // slice_segment_data() (RBSP, before emulation prevention)
+  if (!c.wpp) {
+    // byte_alignment()
+    bw.put_bit(1);
+    bw.align_zero();
+    CabacEncoder enc(bw);
+    enc.start();
+    Writer w(c, fp, ctu, cu, coef_y, coef_cb, coef_cr, enc, ps);
+    for (int i = 0; i < n; ++i) {
+      const int rx = i % wctb, ry = i / wctb;
+      if (c.sao) w.write_sao(rx, ry);
+      w.write_ctu(rx, ry);
+      enc.terminate(i == n - 1);  // end_of_slice_segment_flag
+    }
+    enc.finish();
+    bw.put_bit(1);  // rbsp_slice_segment_trailing_bits: stop bit + alignment
+    bw.align_zero();
+    total = w.st;
+    total.bins = enc.bins();
+  } else {
+    // Wavefront parallel processing (7.3.8.1, 9.3.1, 9.3.2.4): one substream per CTB row,
+    // each row's contexts synchronised from the row above after its second CTB, rows coded
+    // by `threads` host threads with a 2-CTB lag.
+    std::vector<BitWriter> sub(hctb);
+    std::vector<std::array<CtxState, kNumCtx>> saved(hctb);
+    std::vector<HevcSliceStats> rst(hctb);
+    std::unique_ptr<std::atomic<int>[]> prog(new std::atomic<int>[hctb]);
+    for (int r = 0; r < hctb; ++r) prog[r].store(0, std::memory_order_relaxed);
+    std::atomic<bool> abort{false};
+    std::exception_ptr err;
+    std::atomic<int> err_set{0};
+    auto wait_for = [&](int r, int need) {
+      while (prog[r].load(std::memory_order_acquire) < need) {
+        if (abort.load(std::memory_order_relaxed)) throw std::runtime_error("HEVC WPP: aborted");
+        std::this_thread::yield();
+      }
+    };
+    const int T = std::max(1, std::min(c.threads, hctb));
+    auto worker = [&](int t) {
+      try {
+        for (int ry = t; ry < hctb; ry += T) {
+          CabacEncoder enc(sub[ry]);
+          enc.start();
+          Writer w(c, fp, ctu, cu, coef_y, coef_cb, coef_cr, enc, ps);
+          if (ry > 0 && wctb >= 2) {  // 9.3.2.4 sync from CTB (1, ry-1)
+            wait_for(ry - 1, 2);
+            std::copy(saved[ry - 1].begin(), saved[ry - 1].end(), w.ctx);
+          }
+          for (int rx = 0; rx < wctb; ++rx) {
+            if (ry > 0) wait_for(ry - 1, std::min(rx + 2, wctb));
+            if (c.sao) w.write_sao(rx, ry);
+            w.write_ctu(rx, ry);
+            const bool last = ry == hctb - 1 && rx == wctb - 1;
+            enc.terminate(last);  // end_of_slice_segment_flag
+            if (rx == 1) std::copy(w.ctx, w.ctx + kNumCtx, saved[ry].begin());
+            if (rx == wctb - 1 && !last) enc.terminate(1);  // end_of_subset_one_bit
+            if (rx == wctb - 1) {
+              enc.finish();
+              // byte_alignment() after end_of_subset_one_bit; the last row's stop bit is the
+              // rbsp_slice_segment_trailing_bits
+              sub[ry].put_bit(1);
+              sub[ry].align_zero();
+              rst[ry] = w.st;
+              rst[ry].bins = enc.bins();
+            }
+            prog[ry].store(rx + 1, std::memory_order_release);
+          }
+        }
+      } catch (...) {
+        if (err_set.exchange(1) == 0) err = std::current_exception();
+        abort.store(true);
+      }
+    };
+    if (T == 1) {
+      worker(0);
+    } else {
+      std::vector<std::thread> th;
+      for (int t = 0; t < T; ++t) th.emplace_back(worker, t);
+      for (auto& x : th) x.join();
+    }
+    if (err) std::rethrow_exception(err);
+    // entry points count emulation prevention bytes (7.4.7.1): every substream ends in a
+    // non-zero byte, so its escaped size does not depend on its neighbours
+    std::vector<uint32_t> esc(hctb);
+    for (int r = 0; r < hctb; ++r) {
+      const std::vector<uint8_t>& b = sub[r].bytes();
+      uint32_t extra = 0;
+      int zeros = 0;
+      for (uint8_t v : b) {
+        if (zeros >= 2 && v <= 3) {
+          ++extra;
+          zeros = 0;
+        }
+        zeros = v == 0 ? zeros + 1 : 0;
+      }
+      esc[r] = static_cast<uint32_t>(b.size()) + extra;
+      data.insert(data.end(), b.begin(), b.end());
+      total.bins += rst[r].bins;
+      total.intra_cus += rst[r].intra_cus;
+      total.inter_cus += rst[r].inter_cus;
+      total.skip_cus += rst[r].skip_cus;
+      total.merge_cus += rst[r].merge_cus;
+    }
+    bw.put_ue(hctb - 1);  // num_entry_point_offsets
+    if (hctb > 1) {
+      uint32_t mx = 1;
+      for (int r = 0; r + 1 < hctb; ++r) mx = std::max(mx, esc[r]);
+      int len = 1;
+      while (len < 32 && (static_cast<uint64_t>(mx - 1) >> len) != 0) ++len;
+      bw.put_ue(len - 1);  // offset_len_minus1
+      for (int r = 0; r + 1 < hctb; ++r) bw.put(esc[r] - 1, len);  // entry_point_offset_minus1
+    }
+    bw.put_bit(1);  // byte_alignment()
+    bw.align_zero();
+    bw.append_bytes(data.data(), data.size());
   }
-  enc.finish();
-  bw.put_bit(1);  // rbsp_slice_segment_trailing_bits: stop bit + alignment
-  bw.align_zero();
   std::vector<uint8_t> out;
   append_hevc_nal(out, idr ? NAL_IDR_W_RADL : NAL_TRAIL_R, bw.bytes());
   if (stats) {
-    *stats = w.st;
-    stats->bins = enc.bins();
+    *stats = total;
     stats->bytes = out.size();
   }
   return out;

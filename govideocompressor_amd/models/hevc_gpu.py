@@ -51,10 +51,13 @@ class HevcParams:
     lookahead: bool = True
     la_range: int = 6
     scenecut: int = 40   # x264/x265 --scenecut: cut frames are coded all-intra at the I QP (0: off)
+    # x265 --wpp (its default): one CABAC substream per CTB row; the host codes the rows of
+    # one picture on several threads when fewer pictures than entropy threads are in flight
+    wpp: bool = True
 
     def host_cfg(self) -> dict:
         return dict(width=self.width, height=self.height, bit_depth=self.bit_depth, fps=self.fps,
-                    sao=int(self.sao), deblock=int(self.deblock), max_merge=self.max_merge)
+                    sao=int(self.sao), deblock=int(self.deblock), max_merge=self.max_merge, wpp=int(self.wpp))
 
     def frame_qps(self) -> tuple[int, int]:
         qp_p = int(round(self.crf)) if self.crf is not None else int(self.qp)
@@ -206,6 +209,8 @@ class GpuHevcEncoder:
         if qps is None:
             qps = np.array([[qi if t == 0 else qpp for t in range(F)] for _ in range(B)], dtype=np.int32)
         cfg = self.p.host_cfg()
+        if self.p.wpp:  # spread the pool's threads over the B pictures of a step
+            cfg["threads"] = max(1, min(32, self.pool._max_workers // max(1, B)))
         qps = np.clip(np.asarray(qps, dtype=np.int32).reshape(B, F), 0, 51)
         qps_d = torch.from_numpy(np.ascontiguousarray(qps.T)).to(self.dev)  # [F, B], one upload
         nals: list[list] = [[None] * F for _ in range(B)]

@@ -97,10 +97,11 @@ def random_records(rng, width: int, height: int, pslice: bool, bit_depth: int = 
 
 
 def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp: int = 30, bit_depth: int = 8,
-                  **kw) -> tuple[bytes, list]:
-    """Annex-B HEVC stream (IDR + P pictures) and the records it was written from."""
+                  host_cfg: dict | None = None, **kw) -> tuple[bytes, list]:
+    """Annex-B HEVC stream (IDR + P pictures) and the records it was written from.
+    ``host_cfg`` adds writer options (e.g. ``wpp=1, threads=4``)."""
     rng = np.random.default_rng(seed)
-    cfg = dict(width=width, height=height, bit_depth=bit_depth)
+    cfg = dict(width=width, height=height, bit_depth=bit_depth, **(host_cfg or {}))
     out = [host.hevc_parameter_sets(cfg)]
     recs = []
     for t in range(frames):

@@ -47,6 +47,25 @@ def test_hevc_records_roundtrip(host, w, h, bd, seed):
         assert p["y"].max() <= (1 << bd) - 1
 
 
+@pytest.mark.parametrize("w,h,bd,seed", [(32, 96, 8, 5), (64, 64, 8, 6), (320, 192, 10, 7), (352, 288, 8, 8)])
+def test_hevc_wpp_roundtrip(host, w, h, bd, seed):
+    """WPP (entropy_coding_sync, x265's default): one substream per CTB row with context
+    sync after the second CTB of the row above, entry points in the slice header.  The
+    decoder checks every entry point against the escaped substream sizes; the threaded
+    writer must produce the same bytes as the single-threaded one."""
+    s1, recs = random_stream(host, w, h, 3, seed=seed, bit_depth=bd, host_cfg=dict(wpp=1, threads=1))
+    s4, _ = random_stream(host, w, h, 3, seed=seed, bit_depth=bd, host_cfg=dict(wpp=1, threads=4))
+    s0, _ = random_stream(host, w, h, 3, seed=seed, bit_depth=bd)
+    assert s1 == s4 and s1 != s0
+    pics = host.hevc_decode(s1)
+    ref = host.hevc_decode(s0)
+    assert len(pics) == 3
+    for p, q, (ctu, cu, cy, cb, cr) in zip(pics, ref, recs):
+        assert np.array_equal(p["coef_y"], cy) and np.array_equal(p["coef_cb"], cb) and np.array_equal(p["coef_cr"], cr)
+        assert np.array_equal(p["cu"], q["cu"]) and np.array_equal(p["ctu"], q["ctu"])
+        assert np.array_equal(p["y"], q["y"]) and np.array_equal(p["u"], q["u"])
+
+
 def test_hevc_dct_matrix(host):
     m = np.asarray(host.table("hevc_dct32"), dtype=np.int64).reshape(32, 32)
     assert list(m[1, :8]) == [90, 90, 88, 85, 82, 78, 73, 67]
