@@ -67,9 +67,15 @@ def output_size(cfg: EncoderConfig, clip: yuv.Clip) -> tuple[int, int]:
 
 
 def write_output(job: PieceJob, stream: bytes, fps: float) -> int:
-    """Write an Annex-B stream as ``.mp4`` (native muxer) or raw ``.264`` by extension."""
+    """Write an Annex-B stream as ``.mp4`` (``avc1`` native muxer, ``hvc1`` for HEVC) or raw by extension."""
     from ..ops import native
-    data = native.host().mp4_mux(stream, fps) if job.out_path.lower().endswith(".mp4") else stream
+    from ..segment import mp4_hevc
+    if not job.out_path.lower().endswith(".mp4"):
+        data = stream
+    elif mp4_hevc.is_hevc_annexb(stream):
+        data = mp4_hevc.mux(stream, fps)
+    else:
+        data = native.host().mp4_mux(stream, fps)
     tmp = job.out_path + ".part"
     with open(tmp, "wb") as f:
         f.write(data)

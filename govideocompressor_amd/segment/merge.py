@@ -17,6 +17,7 @@ import re
 import sys
 
 from ..ops import native
+from . import mp4_hevc
 
 _LINE = re.compile(r"^\s*file\s+'([^']+)'\s*$")
 
@@ -63,6 +64,8 @@ def load_annexb(path: str) -> bytes:
     with open(path, "rb") as f:
         data = f.read()
     if data[4:8] == b"ftyp" or path.lower().endswith((".mp4", ".m4v", ".mov")):
+        if mp4_hevc.is_hevc_mp4(data):
+            return mp4_hevc.demux(data)
         return native.host().mp4_demux(data)
     return data
 
@@ -75,7 +78,9 @@ def merge_files(files: list[str], out_path: str, fps: float | None = None) -> in
         raise FileNotFoundError(f"missing pieces: {missing[:5]}{'...' if len(missing) > 5 else ''}")
     h = native.host()
     stream = h.concat([load_annexb(f) for f in files])
-    if out_path.lower().endswith((".mp4", ".m4v", ".mov")):
+    if out_path.lower().endswith((".mp4", ".m4v", ".mov")) and mp4_hevc.is_hevc_annexb(stream):
+        data = mp4_hevc.mux(stream, fps or 30.0)
+    elif out_path.lower().endswith((".mp4", ".m4v", ".mov")):
         if fps is None:
             fps = h.stream_info(stream)["fps"] or 30.0
         data = h.mp4_mux(stream, fps)
