@@ -79,6 +79,25 @@ def test_gpu_backend_hevc_preset(host, tmp_path):
     be.close()
 
 
+def test_gpu_backend_hevc_mp4_piece(host, tmp_path):
+    """Job path with the reference's piece naming (``<idx>.mp4``, client.go:54): the HEVC
+    piece is written as an hvc1 MP4 that demuxes back to a decodable stream."""
+    from govideocompressor_amd.backends import PieceJob, get_backend
+    from govideocompressor_amd.segment import mp4_hevc
+    from govideocompressor_amd.utils import yuv
+    c = yuv.synth_clip_cpu(5, 160, 96, seed=3)
+    src = tmp_path / "0.y4m"
+    yuv.write_y4m(str(src), c)
+    be = get_backend("gpu")
+    (r,) = be.run([PieceJob("0", str(src), str(tmp_path / "c0.mp4"))], "-c:v libx265 -crf 26")
+    be.close()
+    assert r.ok, r.reason
+    data = open(tmp_path / "c0.mp4", "rb").read()
+    assert mp4_hevc.is_hevc_mp4(data)
+    pics = host.hevc_decode(mp4_hevc.demux(data))
+    assert len(pics) == 5 and pics[0]["idr"]
+
+
 def test_gpu_hevc_scenecut(host):
     """A hard cut inside a segment is detected by the lookahead and the cut picture is
     coded with intra CUs only; the reconstruction stays bit-exact with the decoder."""
