@@ -25,7 +25,9 @@ def is_hevc_annexb(data: bytes) -> bool:
     if not nals:
         return False
     h = nals[0]
-    return len(h) >= 2 and (h[0] >> 1) & 0x3F in (_VPS, _SPS, _PPS, _AUD) and (h[1] & 0x7) >= 1
+    # forbidden_zero_bit = 0, nuh_layer_id = 0, nuh_temporal_id_plus1 >= 1
+    return (len(h) >= 2 and h[0] & 0x81 == 0 and h[1] >> 3 == 0 and (h[1] & 0x7) >= 1
+            and (h[0] >> 1) & 0x3F in (_VPS, _SPS, _PPS, _AUD))
 
 
 def split_nals(data: bytes) -> list[bytes]:

@@ -41,6 +41,7 @@ def test_h264_streams_not_taken_for_hevc(host):
     assert not mp4_hevc.is_hevc_annexb(host.parameter_sets(dict(width=64, height=48)))
     assert not mp4_hevc.is_hevc_annexb(b"\x00\x00\x00\x01\x67\x42\xc0\x1e" + bytes(16))
     assert not mp4_hevc.is_hevc_annexb(b"\x00\x00\x00\x01\x09\xf0")
+    assert not mp4_hevc.is_hevc_annexb(b"\x00\x00\x00\x01\x41\x9a\x02\x10")  # H.264 P slice (nal_ref_idc 2)
 
 
 def test_hevc_mp4_merge(host, tmp_path):
