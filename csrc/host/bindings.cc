@@ -297,7 +297,7 @@ PYBIND11_MODULE(_host, m) {
     return to_bytes(write_parameter_sets(make_sps(c), make_pps(c)));
   });
 
-  // Write one slice NAL from MB decision arrays (uint8 [N,48] headers, int16 [N,408] coefficients).
+  // Write one slice NAL from MB decision arrays (uint8 [N,64] headers, int16 [N,408] coefficients).
   m.def(
       "write_slice",
       [](const py::dict& cfg, const py::dict& fp, py::array_t<uint8_t, py::array::c_style> hdr,
@@ -306,7 +306,7 @@ PYBIND11_MODULE(_host, m) {
         SPS sps = make_sps(c);
         PPS pps = make_pps(c);
         int nmb = sps.width_mbs * sps.height_mbs;
-        if (hdr.size() != static_cast<py::ssize_t>(nmb) * 48) throw std::runtime_error("header array has wrong size");
+        if (hdr.size() != static_cast<py::ssize_t>(nmb * sizeof(MbHeader))) throw std::runtime_error("header array has wrong size");
         if (coef.size() != static_cast<py::ssize_t>(nmb) * kCoefPerMb) throw std::runtime_error("coef array has wrong size");
         SliceHeader sh;
         bool idr = dget<int>(fp, "idr", 0) != 0;

@@ -195,7 +195,7 @@ class SliceWriter {
       if (pslice && inter && cbp == 0 && (mb.kind == MBK_P16x16 || mb.kind == MBK_PSKIP)) {
         int smv[2];
         skip_mv(mx, my, addr, smv);
-        if (smv[0] == mb.mv[0][0] && smv[1] == mb.mv[0][1]) {
+        if (smv[0] == mb.mv[0][0][0] && smv[1] == mb.mv[0][0][1]) {
           m.kind = MBK_PSKIP;
           std::fill(m.tc, m.tc + 24, 0);
           for (int b = 0; b < 16; ++b) {
@@ -413,12 +413,12 @@ class SliceWriter {
       int p[2];
       if (kind == MBK_P16x16) {
         mvp(mx, my, &m, 0, 0, 4, 0, 0, p);
-        bw.put_se(mb.mv[0][0] - p[0]);
-        bw.put_se(mb.mv[0][1] - p[1]);
-        set_part(0, 0, 4, 4, mb.mv[0][0], mb.mv[0][1]);
+        bw.put_se(mb.mv[0][0][0] - p[0]);
+        bw.put_se(mb.mv[0][0][1] - p[1]);
+        set_part(0, 0, 4, 4, mb.mv[0][0][0], mb.mv[0][0][1]);
       } else if (kind == MBK_P16x8) {
         for (int part = 0; part < 2; ++part) {
-          const int16_t* v = mb.mv[part * 2];
+          const int16_t* v = mb.mv[0][part * 2];
           mvp(mx, my, &m, 0, part * 2, 4, 1, part, p);
           bw.put_se(v[0] - p[0]);
           bw.put_se(v[1] - p[1]);
@@ -426,7 +426,7 @@ class SliceWriter {
         }
       } else if (kind == MBK_P8x16) {
         for (int part = 0; part < 2; ++part) {
-          const int16_t* v = mb.mv[part];
+          const int16_t* v = mb.mv[0][part];
           mvp(mx, my, &m, part * 2, 0, 2, 2, part, p);
           bw.put_se(v[0] - p[0]);
           bw.put_se(v[1] - p[1]);
@@ -437,9 +437,9 @@ class SliceWriter {
         for (int s = 0; s < 4; ++s) {
           int bx = (s & 1) * 2, by = (s >> 1) * 2;
           mvp(mx, my, &m, bx, by, 2, 0, 0, p);
-          bw.put_se(mb.mv[s][0] - p[0]);
-          bw.put_se(mb.mv[s][1] - p[1]);
-          set_part(bx, by, 2, 2, mb.mv[s][0], mb.mv[s][1]);
+          bw.put_se(mb.mv[0][s][0] - p[0]);
+          bw.put_se(mb.mv[0][s][1] - p[1]);
+          set_part(bx, by, 2, 2, mb.mv[0][s][0], mb.mv[0][s][1]);
         }
       }
       for (int r = 0; r < 16; ++r) {

@@ -77,6 +77,7 @@ class FrameEncoder {
 
   void encode(const Planes& src, const Planes* ref, bool islice, int qp) {
     std::memset(mbs_.data(), 0, mbs_.size() * sizeof(MbHeader));
+    for (MbHeader& h : mbs_) std::memset(h.ref, 0xFF, sizeof(h.ref));  // no list used until inter
     std::fill(coef_.begin(), coef_.end(), 0);
     src_ = &src;
     ref_ = ref;
@@ -498,8 +499,9 @@ class FrameEncoder {
       if (cinter <= c16) {
         hdr.kind = MBK_P16x16;
         for (int q = 0; q < 4; ++q) {
-          hdr.mv[q][0] = static_cast<int16_t>(mvx);
-          hdr.mv[q][1] = static_cast<int16_t>(mvy);
+          hdr.mv[0][q][0] = static_cast<int16_t>(mvx);
+          hdr.mv[0][q][1] = static_cast<int16_t>(mvy);
+          hdr.ref[0][q] = 0;
         }
         mvs_[2 * addr] = mvx;
         mvs_[2 * addr + 1] = mvy;

@@ -46,7 +46,7 @@ struct Pic {
   std::vector<int16_t> mv;      // [mb][16][2] raster
   std::vector<int8_t> ref;      // [mb][16] raster (ref idx, -1 intra)
   std::vector<int> refpic;      // [mb][16] raster (ref picture id, -1 intra)
-  std::vector<uint8_t> rec_hdr; // parse-only: [mb][48] MbHeader
+  std::vector<uint8_t> rec_hdr; // parse-only: [mb][64] MbHeader
   std::vector<int16_t> rec_coef;// parse-only: non-zero 16-level blocks, packed
   std::vector<uint32_t> rec_mask, rec_off;  // parse-only: [mb] block mask / first block
   bool gpu_ok = true;
@@ -444,11 +444,13 @@ struct Decoder::Impl {
     h.chroma_mode = static_cast<uint8_t>(chroma_mode);
     for (int q = 0; q < 4; ++q) {
       int r0 = (q & 1) * 2 + (q >> 1) * 8;  // top-left 4x4 block of quadrant q
-      h.mv[q][0] = cur->mv[addr * 32 + 2 * r0];
-      h.mv[q][1] = cur->mv[addr * 32 + 2 * r0 + 1];
+      h.mv[0][q][0] = cur->mv[addr * 32 + 2 * r0];
+      h.mv[0][q][1] = cur->mv[addr * 32 + 2 * r0 + 1];
+      h.ref[0][q] = cur->ref[addr * 16 + r0];
+      h.ref[1][q] = -1;
       for (int k = 0; k < 4; ++k) {  // the quadrant must carry one vector (no sub-8x8 split)
         int r = r0 + (k & 1) + (k >> 1) * 4;
-        if (cur->mv[addr * 32 + 2 * r] != h.mv[q][0] || cur->mv[addr * 32 + 2 * r + 1] != h.mv[q][1])
+        if (cur->mv[addr * 32 + 2 * r] != h.mv[0][q][0] || cur->mv[addr * 32 + 2 * r + 1] != h.mv[0][q][1])
           cur->gpu_ok = false;
       }
     }

@@ -34,7 +34,7 @@ struct DecodedPicture {
   std::vector<uint8_t> nz;            // [mb][16] non-zero luma coefficients per 4x4 block
   // parse-only mode (GPU reconstruction): per-MB decision records in the encoder's layout
   // (csrc/common/h264_mb.h: MbHeader + kCoefPerMb levels), plus the slice parameters
-  std::vector<uint8_t> hdr;           // [mb][48] MbHeader
+  std::vector<uint8_t> hdr;           // [mb][64] MbHeader
   std::vector<int16_t> coef;          // packed 16-level blocks (scan order, not dequantised)
   std::vector<uint32_t> blk_mask;     // [mb] which blocks are present: bits 0-15 luma (blkIdx),
                                       // 16 I16x16 DC, 17 chroma DC (Cb 0-3, Cr 4-7), 18-25 chroma AC

@@ -234,8 +234,8 @@ __device__ __forceinline__ NbMv nb_mv(const MbHeader* hdr, size_t base, int wmb,
   const MbHeader& h = hdr[base + y * wmb + x];
   if (h264::mbk_is_intra(h.kind)) return r;
   r.ref = 0;
-  r.mv[0] = h.mv[quad][0];
-  r.mv[1] = h.mv[quad][1];
+  r.mv[0] = h.mv[0][quad][0];
+  r.mv[1] = h.mv[0][quad][1];
   return r;
 }
 
@@ -344,12 +344,12 @@ __global__ __launch_bounds__(64) void cavlc_analyze(CavlcArgs a) {
         pmv[1] = med3(A.mv[1], Bm.mv[1], Cm.mv[1]);
       }
       if (!zero) { smv[0] = pmv[0]; smv[1] = pmv[1]; }
-      if (a.pslice && cbp == 0 && h.mv[0][0] == smv[0] && h.mv[0][1] == smv[1]) {
+      if (a.pslice && cbp == 0 && h.mv[0][0][0] == smv[0] && h.mv[0][0][1] == smv[1]) {
         m.coded = 0;
         m.has_delta = 0;
       }
-      m.mvd[0] = static_cast<int16_t>(h.mv[0][0] - pmv[0]);
-      m.mvd[1] = static_cast<int16_t>(h.mv[0][1] - pmv[1]);
+      m.mvd[0] = static_cast<int16_t>(h.mv[0][0][0] - pmv[0]);
+      m.mvd[1] = static_cast<int16_t>(h.mv[0][0][1] - pmv[1]);
     }
   }
   if (kind0 == h264::MBK_I4x4 && sub < 16) {

@@ -52,7 +52,7 @@ constexpr int kMaxCols = 480;   // MB columns (8K: 7680 / 16)
 struct DeblockShared {
   alignas(16) uint8_t ty[LT * LT];
   alignas(16) uint8_t tc[2][CT * CT];
-  alignas(16) uint32_t hdrw[3][12];  // MbHeader of the current, left and top MB
+  alignas(16) uint32_t hdrw[3][12];  // first 48 B of the MbHeader of the current, left and top MB
   uint32_t nzw[3][4];                // their non-zero flags (16 bytes each)
   int bs[2][4][4];                   // [dir][edge][segment]
   int par[2][2][2][5];               // [dir][mb edge / inner][luma / chroma]: alpha, beta, tc0 for bS 1..3
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(64 * kDeblockWaves) void deblock_wavefront(DeblockA
   uint8_t* const rcu = a.rec_u + slot * g.csize();
   uint8_t* const rcv = a.rec_v + slot * g.csize();
   auto recc = [&](int c) { return c ? rcv : rcu; };
-  const uint32_t* hdr32 = reinterpret_cast<const uint32_t*>(a.hdr) + static_cast<size_t>(slot) * g.nmb() * 12;
+  const uint32_t* hdr32 = reinterpret_cast<const uint32_t*>(a.hdr) + static_cast<size_t>(slot) * g.nmb() * 16;
   const uint32_t* nz32 = reinterpret_cast<const uint32_t*>(a.nz) + static_cast<size_t>(slot) * g.nmb() * 4;
 
   // unfiltered inputs of MB (x, y), branch-free (three loads per lane, lane-selected
@@ -176,8 +176,8 @@ __global__ __launch_bounds__(64 * kDeblockWaves) void deblock_wavefront(DeblockA
     if (is_c) a1 = a2 = recc(ccomp) + static_cast<size_t>(y * 8 + cline) * cw + x * 8;
     const size_t mb = static_cast<size_t>(y) * wmb + x;
     const size_t mbt = y > 0 ? mb - wmb : mb;
-    const uint32_t* a3 = hl < 12 ? hdr32 + mb * 12 + hl
-                                 : (hl < 24 ? hdr32 + mbt * 12 + (hl - 12)
+    const uint32_t* a3 = hl < 12 ? hdr32 + mb * 16 + hl
+                                 : (hl < 24 ? hdr32 + mbt * 16 + (hl - 12)
                                             : (hl < 28 ? nz32 + mb * 4 + (hl - 24) : nz32 + mbt * 4 + (hl - 28)));
     const uint2 q1 = *reinterpret_cast<const uint2*>(a1);
     const uint2 q2 = *reinterpret_cast<const uint2*>(a2);
@@ -233,7 +233,7 @@ __global__ __launch_bounds__(64 * kDeblockWaves) void deblock_wavefront(DeblockA
             else if (nzbp[rp] || nzb0[rq]) bs = 2;
             else {
               const int qp_ = ((rp >> 3) & 1) * 2 + ((rp & 3) >> 1), qq_ = ((rq >> 3) & 1) * 2 + ((rq & 3) >> 1);
-              const int dx = HP->mv[qp_][0] - HQ->mv[qq_][0], dy = HP->mv[qp_][1] - HQ->mv[qq_][1];
+              const int dx = HP->mv[0][qp_][0] - HQ->mv[0][qq_][0], dy = HP->mv[0][qp_][1] - HQ->mv[0][qq_][1];
               bs = (dx >= 4 || dx <= -4 || dy >= 4 || dy <= -4) ? 1 : 0;
             }
           }

@@ -103,8 +103,8 @@ __global__ __launch_bounds__(64) void decode_inter_mb(DecodeArgs a) {
   const int qp = H->qp;
   const int qpc = h264::chroma_qp(qp, a.chroma_qp_offset);
   const uint32_t mask = a.mask[o], off = a.off[o];
-  const int m0x = H->mv[0][0], m0y = H->mv[0][1], m1x = H->mv[1][0], m1y = H->mv[1][1];
-  const int m2x = H->mv[2][0], m2y = H->mv[2][1], m3x = H->mv[3][0], m3y = H->mv[3][1];
+  const int m0x = H->mv[0][0][0], m0y = H->mv[0][0][1], m1x = H->mv[0][1][0], m1y = H->mv[0][1][1];
+  const int m2x = H->mv[0][2][0], m2y = H->mv[0][2][1], m3x = H->mv[0][3][0], m3y = H->mv[0][3][1];
 
   // ---- stage the four quadrant windows of the reference (clamped: unrestricted MVs)
   const uint8_t* refy = a.ref_y + slot * g.ysize();

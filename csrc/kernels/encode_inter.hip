@@ -298,9 +298,9 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
     h->chroma_mode = 0;
     h->flags = 0;
     const uint32_t mvw = (static_cast<uint32_t>(mvx) & 0xFFFFu) | (static_cast<uint32_t>(mvy) << 16);
-    uint2* mvp = reinterpret_cast<uint2*>(&h->mv[0][0]);  // 8-byte aligned
-    mvp[0] = make_uint2(mvw, mvw);
-    mvp[1] = make_uint2(mvw, mvw);
+    uint4* mvp = reinterpret_cast<uint4*>(&h->mv[0][0][0]);  // 16-byte aligned
+    mvp[0] = make_uint4(mvw, mvw, mvw, mvw);
+    *reinterpret_cast<uint2*>(&h->ref[0][0]) = make_uint2(0u, 0xFFFFFFFFu);  // L0 ref 0, L1 unused
     a.intra_flag[o] = 0;
   }
 }

@@ -478,7 +478,8 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
     h->chroma_mode = static_cast<uint8_t>(cmode);
     h->flags = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) h->mv[q][0] = h->mv[q][1] = 0;
+    for (int q = 0; q < 4; ++q) h->mv[0][q][0] = h->mv[0][q][1] = h->mv[1][q][0] = h->mv[1][q][1] = 0;
+    *reinterpret_cast<uint2*>(&h->ref[0][0]) = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
   }
   if (!use4 && lane >= 32 && lane < 48) h->i4_modes[lane - 32] = 2;
   wave_sync();

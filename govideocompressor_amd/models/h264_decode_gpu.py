@@ -149,7 +149,7 @@ class GpuH264Decoder:
         B = len(segs)
         F = max(int(s["n"]) for s in segs)
         # ---- pack the batch: [F, B, nmb, ...] records, one flat level array
-        hdr = np.zeros((F, B, nmb, 48), np.uint8)
+        hdr = np.zeros((F, B, nmb, 64), np.uint8)
         mask = np.zeros((F, B, nmb), np.uint32)
         off = np.zeros((F, B, nmb), np.uint32)
         run = np.zeros((F, B), np.int8)

@@ -26,7 +26,7 @@ import torch
 
 from ..ops import native
 
-MB_HDR_BYTES = 48
+MB_HDR_BYTES = 64
 COEF_PER_MB = 408
 
 

@@ -42,6 +42,6 @@ def slots_for(width: int, height: int, frames: int, info: DeviceInfo | None, cap
     if info is None:
         return 1
     coded = ((width + 15) // 16 * 16) * ((height + 15) // 16 * 16)
-    per_slot = coded * 3 // 2 * (frames + 4) + coded // 256 * (48 + 816 + 400)
+    per_slot = coded * 3 // 2 * (frames + 4) + coded // 256 * (64 + 816 + 400)
     by_mem = max(1, int(info.hbm_bytes * 0.6) // max(1, per_slot))
     return max(1, min(cap, by_mem, max(info.cus, 1)))

@@ -14,7 +14,8 @@ import numpy as np
 from .. import ops  # noqa: F401  (package import order)
 
 # MbHeader byte offsets (csrc/common/h264_mb.h)
-_KIND, _CBP, _QP, _I16, _CHROMA, _FLAGS, _MV, _I4 = 0, 1, 2, 3, 4, 5, 8, 24
+_KIND, _CBP, _QP, _I16, _CHROMA, _FLAGS, _REF, _MV, _I4 = 0, 1, 2, 3, 4, 5, 8, 16, 48
+HDR_BYTES = 64
 I4x4, I16x16, P16x16, PSKIP, P16x8, P8x16, P8x8 = 0, 1, 2, 3, 5, 6, 7
 
 _BLK_X = [0, 1, 0, 1, 2, 3, 2, 3, 0, 1, 0, 1, 2, 3, 2, 3]
@@ -91,7 +92,8 @@ def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp:
         if idr:
             fn = 0
         sqp = int(np.clip(qp + rng.integers(-2, 3), 10, 48))
-        hdr = np.zeros((nmb, 48), np.uint8)
+        hdr = np.zeros((nmb, HDR_BYTES), np.uint8)
+        hdr[:, _REF:_REF + 8] = 0xFF
         coef = np.zeros((nmb, 408), np.int16)
         for mb in range(nmb):
             mx, my = mb % wmb, mb // wmb
@@ -112,6 +114,7 @@ def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp:
             h[_KIND] = kind
             h[_QP] = mqp
             h[_MV:_MV + 16] = np.frombuffer(mv.astype(np.int16).tobytes(), np.uint8)
+            h[_REF:_REF + 4] = 0
             if kind != PSKIP:
                 for b in range(16):
                     c[b * 16:(b + 1) * 16] = _levels(rng, 16, density) if rng.random() < 0.6 else 0

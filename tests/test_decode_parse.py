@@ -44,13 +44,13 @@ def test_parse_matches_full_decode(host):
     pics = host.decode(s)
     seg = host.parse([s], 2)[0]
     nmb = (w // 16) * (h // 16)
-    assert seg["hdr"].shape == (5, nmb, 48)
+    assert seg["hdr"].shape == (5, nmb, 64)
     for t, p in enumerate(pics):
         hd = seg["hdr"][t]
         kinds = hd[:, 0].astype(np.int8)
         assert np.array_equal(kinds, p["mb_kind"])
         assert np.array_equal(hd[:, 2].astype(np.int8), p["mb_qp"])
-        mv = np.frombuffer(hd[:, 8:24].tobytes(), np.int16).reshape(nmb, 4, 2)
+        mv = np.frombuffer(hd[:, 16:32].tobytes(), np.int16).reshape(nmb, 4, 2)
         dmv = p["mv"].reshape(nmb, 16, 2)
         for q, r in enumerate((0, 2, 8, 10)):
             assert np.array_equal(mv[:, q], dmv[:, r])
