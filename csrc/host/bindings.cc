@@ -12,6 +12,7 @@
 
 #include "../common/h264_enc_math.h"
 #include "annexb.h"
+#include "cabac_writer.h"
 #include "cavlc_writer.h"
 #include "cpu_encoder.h"
 #include "h264_decoder.h"
@@ -52,6 +53,12 @@ EncoderConfig cfg_from(const py::dict& d) {
   c.deblock = dget<int>(d, "deblock", 1);
   c.chroma_qp_offset = dget<int>(d, "chroma_qp_offset", 0);
   c.vui = dget<int>(d, "vui", 1);
+  c.cabac = dget<int>(d, "cabac", 0);
+  c.t8x8 = dget<int>(d, "t8x8", 0);
+  c.bframes = dget<int>(d, "bframes", 0);
+  c.refs = dget<int>(d, "refs", 1);
+  c.weighted_bipred = dget<int>(d, "weighted_bipred", 0);
+  if (c.refs < 1 || c.refs > 16) throw std::runtime_error("refs must be in 1..16");
   return c;
 }
 
@@ -182,6 +189,29 @@ py::dict segment_to_dict(ParsedSegment& seg) {
   return d;
 }
 
+// Slice header of one picture from the frame-parameter dict: idr, slice_type, frame_num,
+// idr_pic_id, qp, poc (POC type 0), nal_ref_idc, num_ref (L0 / L1 active), direct_spatial.
+SliceHeader slice_header_from(const EncoderConfig& c, const SPS& sps, const PPS& pps, const py::dict& fp) {
+  SliceHeader sh;
+  bool idr = dget<int>(fp, "idr", 0) != 0;
+  sh.nal_unit_type = idr ? NAL_IDR : NAL_SLICE;
+  sh.slice_type = dget<int>(fp, "slice_type", idr ? SLICE_I : SLICE_P);
+  sh.nal_ref_idc = dget<int>(fp, "nal_ref_idc", idr ? 3 : (sh.slice_type == SLICE_B ? 0 : 2));
+  sh.frame_num = dget<int>(fp, "frame_num", 0);
+  sh.idr_pic_id = dget<int>(fp, "idr_pic_id", 0);
+  sh.poc_lsb = dget<int>(fp, "poc", 0);
+  sh.slice_qp_delta = dget<int>(fp, "qp", 26) - pps.pic_init_qp;
+  sh.disable_deblocking_filter_idc = c.deblock ? 0 : 1;
+  sh.num_ref_idx_l0_active = dget<int>(fp, "num_ref_l0", pps.num_ref_idx_l0_default);
+  sh.num_ref_idx_l1_active = dget<int>(fp, "num_ref_l1", pps.num_ref_idx_l1_default);
+  sh.num_ref_idx_override = (sh.num_ref_idx_l0_active != pps.num_ref_idx_l0_default ||
+                             sh.num_ref_idx_l1_active != pps.num_ref_idx_l1_default) ? 1 : 0;
+  sh.direct_spatial = dget<int>(fp, "direct_spatial", 1);
+  sh.cabac_init_idc = 0;
+  (void)sps;
+  return sh;
+}
+
 hevc::HevcConfig hevc_cfg_from(const py::dict& d) {
   hevc::HevcConfig c;
   c.width = dget<int>(d, "width", 0);
@@ -308,20 +338,14 @@ PYBIND11_MODULE(_host, m) {
         int nmb = sps.width_mbs * sps.height_mbs;
         if (hdr.size() != static_cast<py::ssize_t>(nmb * sizeof(MbHeader))) throw std::runtime_error("header array has wrong size");
         if (coef.size() != static_cast<py::ssize_t>(nmb) * kCoefPerMb) throw std::runtime_error("coef array has wrong size");
-        SliceHeader sh;
-        bool idr = dget<int>(fp, "idr", 0) != 0;
-        sh.nal_unit_type = idr ? NAL_IDR : NAL_SLICE;
-        sh.nal_ref_idc = idr ? 3 : 2;
-        sh.slice_type = dget<int>(fp, "slice_type", idr ? SLICE_I : SLICE_P);
-        sh.frame_num = dget<int>(fp, "frame_num", 0);
-        sh.idr_pic_id = dget<int>(fp, "idr_pic_id", 0);
-        sh.slice_qp_delta = dget<int>(fp, "qp", 26) - pps.pic_init_qp;
-        sh.disable_deblocking_filter_idc = c.deblock ? 0 : 1;
+        SliceHeader sh = slice_header_from(c, sps, pps, fp);
         SliceStats st;
         std::vector<uint8_t> nal;
         {
           py::gil_scoped_release rel;
-          nal = write_slice_nal(sps, pps, sh, reinterpret_cast<const MbHeader*>(hdr.data()), coef.data(), nmb, &st);
+          const MbHeader* mh = reinterpret_cast<const MbHeader*>(hdr.data());
+          nal = pps.entropy_coding_mode ? write_slice_nal_cabac(sps, pps, sh, mh, coef.data(), nmb, &st)
+                                        : write_slice_nal(sps, pps, sh, mh, coef.data(), nmb, &st);
         }
         py::dict stats;
         stats["bits"] = st.bits;
@@ -470,17 +494,11 @@ PYBIND11_MODULE(_host, m) {
     EncoderConfig c = cfg_from(cfg);
     SPS sps = make_sps(c);
     PPS pps = make_pps(c);
-    SliceHeader sh;
-    bool idr = dget<int>(fp, "idr", 0) != 0;
-    sh.nal_unit_type = idr ? NAL_IDR : NAL_SLICE;
-    sh.nal_ref_idc = idr ? 3 : 2;
-    sh.slice_type = dget<int>(fp, "slice_type", idr ? SLICE_I : SLICE_P);
-    sh.frame_num = dget<int>(fp, "frame_num", 0);
-    sh.idr_pic_id = dget<int>(fp, "idr_pic_id", 0);
-    sh.slice_qp_delta = dget<int>(fp, "qp", 26) - pps.pic_init_qp;
-    sh.disable_deblocking_filter_idc = c.deblock ? 0 : 1;
+    SliceHeader sh = slice_header_from(c, sps, pps, fp);
     BitWriter bw;
     write_slice_header(bw, sh, sps, pps);
+    if (pps.entropy_coding_mode)
+      while (!bw.byte_aligned()) bw.put_bit(1);  // cabac_alignment_one_bit: slice data starts byte-aligned
     size_t nbits = bw.bit_pos();
     bw.align_zero();
     std::vector<uint32_t> words((bw.bytes().size() + 3) / 4, 0);

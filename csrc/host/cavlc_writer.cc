@@ -135,7 +135,7 @@ int derive_cbp(const MbHeader& mb, const int16_t* coef) {
     bool nz = false;
     for (int b = 0; b < 4 && !nz; ++b) {
       const int16_t* c = coef + COEF_LUMA + (b8 * 4 + b) * 16;
-      for (int i = (mb.kind == MBK_I16x16 ? 1 : 0); i < 16; ++i)
+      for (int i = (mb.kind == MBK_I16x16 && !(mb.flags & MBF_T8x8) ? 1 : 0); i < 16; ++i)
         if (c[i]) {
           nz = true;
           break;
@@ -344,8 +344,8 @@ class SliceWriter {
     const MbCtx* A = nb_block(mx, my, &cur, bx - 1, by, &ra);
     const MbCtx* B = nb_block(mx, my, &cur, bx, by - 1, &rb);
     if (!A || !B) return 2;
-    int ma = (A->kind == MBK_I4x4) ? A->i4[kRasterToBlk[ra]] : 2;
-    int mb = (B->kind == MBK_I4x4) ? B->i4[kRasterToBlk[rb]] : 2;
+    int ma = (A->kind == MBK_I4x4 || A->kind == MBK_I8x8) ? A->i4[kRasterToBlk[ra]] : 2;
+    int mb = (B->kind == MBK_I4x4 || B->kind == MBK_I8x8) ? B->i4[kRasterToBlk[rb]] : 2;
     return std::min(ma, mb);
   }
 
@@ -368,7 +368,8 @@ class SliceWriter {
       case MBK_P16x8: bw.put_ue(1); break;
       case MBK_P8x16: bw.put_ue(2); break;
       case MBK_P8x8: bw.put_ue(3); break;
-      case MBK_I4x4: bw.put_ue(intra_offset + 0); break;
+      case MBK_I4x4:
+      case MBK_I8x8: bw.put_ue(intra_offset + 0); break;
       case MBK_I16x16:
         bw.put_ue(intra_offset + 1 + mb.i16_mode + 4 * cbp_chroma + (cbp_luma ? 12 : 0));
         break;
@@ -382,7 +383,24 @@ class SliceWriter {
       qp_prev = qp_prev;  // QP unchanged (QP'Y of I_PCM for deblocking handled by decoder: qPp = 0)
       return;
     }
+    const bool t8 = (kind == MBK_I8x8) || ((mb.flags & MBF_T8x8) && !mbk_is_intra(kind));
+    if ((kind == MBK_I4x4 || kind == MBK_I8x8) && pps_.transform_8x8_mode) bw.put_bit(kind == MBK_I8x8);
+    if (kind == MBK_I8x8 && !pps_.transform_8x8_mode) throw std::runtime_error("I8x8 without transform_8x8_mode");
     // ---- prediction info
+    if (kind == MBK_I8x8) {
+      for (int b8 = 0; b8 < 4; ++b8) {
+        int bx = (b8 & 1) * 2, by = (b8 >> 1) * 2;
+        int pred = pred_i4_mode(mx, my, m, bx, by);
+        int mode = mb.i4_modes[b8 * 4];
+        if (mode == pred) {
+          bw.put_bit(1);
+        } else {
+          bw.put_bit(0);
+          bw.put(mode < pred ? mode : mode - 1, 3);
+        }
+        for (int k = 0; k < 4; ++k) m.i4[kRasterToBlk[bx + (k & 1) + 4 * (by + (k >> 1))]] = static_cast<uint8_t>(mode);
+      }
+    }
     if (kind == MBK_I4x4) {
       for (int blk = 0; blk < 16; ++blk) {
         int bx = kBlkX[blk], by = kBlkY[blk];
@@ -397,7 +415,7 @@ class SliceWriter {
         m.i4[blk] = static_cast<uint8_t>(mode);
       }
     }
-    if (kind == MBK_I4x4 || kind == MBK_I16x16) bw.put_ue(mb.chroma_mode);
+    if (kind == MBK_I4x4 || kind == MBK_I16x16 || kind == MBK_I8x8) bw.put_ue(mb.chroma_mode);
     if (!mbk_is_intra(kind)) {
       reset_cur();
       auto set_part = [&](int bx, int by, int w4, int h4, int mvx, int mvy) {
@@ -458,6 +476,7 @@ class SliceWriter {
           break;
         }
       bw.put_ue(code);
+      if (cbp_luma && pps_.transform_8x8_mode && !mbk_is_intra(kind)) bw.put_bit(t8 ? 1 : 0);
     }
     if (cbp_luma == 0 && cbp_chroma == 0 && kind != MBK_I16x16) return;
     // ---- mb_qp_delta
@@ -477,6 +496,11 @@ class SliceWriter {
         if (!(cbp_luma & (1 << b8))) continue;
         int nc = nc_luma(mx, my, m, kBlkX[blk], kBlkY[blk]);
         const int16_t* blkc = c + COEF_LUMA + blk * 16;
+        int16_t il[16];
+        if (t8 && pps_.transform_8x8_mode) {  // 8x8 levels as four interleaved 4x4 blocks (7.3.5.3.2)
+          for (int i = 0; i < 16; ++i) il[i] = c[COEF_LUMA + b8 * 64 + 4 * i + b4];
+          blkc = il;
+        }
         int tc = kind == MBK_I16x16 ? cavlc_write_block(bw, blkc, 1, 15, 15, nc)
                                     : cavlc_write_block(bw, blkc, 0, 15, 16, nc);
         m.tc[blk] = static_cast<uint8_t>(tc);

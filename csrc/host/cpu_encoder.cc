@@ -1,4 +1,5 @@
 #include "cpu_encoder.h"
+#include "cabac_writer.h"
 
 #include <algorithm>
 #include <climits>
@@ -20,12 +21,26 @@ SPS make_sps(const EncoderConfig& cfg) {
   s.height_mbs = (cfg.height + 15) / 16;
   s.crop_right = (s.width_mbs * 16 - cfg.width) / 2;
   s.crop_bottom = (s.height_mbs * 16 - cfg.height) / 2;
-  s.profile_idc = 66;
-  s.constraint_flags = 0xC0;  // Constrained Baseline
+  if (cfg.t8x8) {
+    s.profile_idc = 100;  // High
+    s.constraint_flags = 0;
+  } else if (cfg.cabac || cfg.bframes > 0) {
+    s.profile_idc = 77;   // Main
+    s.constraint_flags = 0x40;  // constraint_set1 (Main-compatible)
+  } else {
+    s.profile_idc = 66;
+    s.constraint_flags = 0xC0;  // Constrained Baseline
+  }
   s.level_idc = choose_level(s.width_mbs, s.height_mbs, cfg.fps);
-  s.poc_type = 2;
   s.log2_max_frame_num = 16;
-  s.max_num_ref_frames = 1;
+  if (cfg.bframes > 0) {
+    s.poc_type = 0;
+    s.log2_max_poc_lsb = 16;
+    s.max_num_reorder = 1;  // B pictures are output one behind their future anchor
+  } else {
+    s.poc_type = 2;
+  }
+  s.max_num_ref_frames = std::max(1, cfg.refs) + (cfg.bframes > 0 ? 1 : 0);
   s.vui_present = cfg.vui;
   // time_scale / (2 * num_units_in_tick) = fps
   s.num_units_in_tick = 1000;
@@ -36,6 +51,10 @@ SPS make_sps(const EncoderConfig& cfg) {
 PPS make_pps(const EncoderConfig& cfg) {
   PPS p;
   p.pic_init_qp = 26;
+  p.entropy_coding_mode = cfg.cabac ? 1 : 0;
+  p.transform_8x8_mode = cfg.t8x8 ? 1 : 0;
+  p.num_ref_idx_l0_default = std::max(1, cfg.refs);
+  p.weighted_bipred_idc = cfg.bframes > 0 ? cfg.weighted_bipred : 0;
   p.chroma_qp_index_offset = cfg.chroma_qp_offset;
   p.second_chroma_qp_index_offset = cfg.chroma_qp_offset;
   p.deblocking_filter_control_present = 1;
@@ -658,7 +677,9 @@ std::vector<uint8_t> CpuEncoder::encode(const uint8_t* frames, int nframes, int 
     sh.slice_qp_delta = qp - pps.pic_init_qp;
     sh.disable_deblocking_filter_idc = cfg_.deblock ? 0 : 1;
     std::vector<uint8_t> nal =
-        write_slice_nal(sps, pps, sh, fe.mbs_.data(), fe.coef_.data(), sps.width_mbs * sps.height_mbs);
+        pps.entropy_coding_mode
+            ? write_slice_nal_cabac(sps, pps, sh, fe.mbs_.data(), fe.coef_.data(), sps.width_mbs * sps.height_mbs)
+            : write_slice_nal(sps, pps, sh, fe.mbs_.data(), fe.coef_.data(), sps.width_mbs * sps.height_mbs);
     out.insert(out.end(), nal.begin(), nal.end());
     recon_unf_.insert(recon_unf_.end(), fe.rec_.y.begin(), fe.rec_.y.end());
     recon_unf_.insert(recon_unf_.end(), fe.rec_.u.begin(), fe.rec_.u.end());

@@ -29,6 +29,13 @@ struct EncoderConfig {
   int chroma_qp_offset = 0;
   int aud = 0;
   int vui = 1;
+  // tool set: entropy 0 CAVLC / 1 CABAC; t8x8 = High profile 8x8 transform (+ I8x8);
+  // bframes = consecutive B pictures (POC type 0 and reordering); refs = active L0 refs
+  int cabac = 0;
+  int t8x8 = 0;
+  int bframes = 0;
+  int refs = 1;
+  int weighted_bipred = 0;  // 2 = implicit weights (x264 --weightb)
 };
 
 struct FrameStats {

@@ -1,4 +1,5 @@
-// Independent H.264 decoder (CAVLC; I and P slices; 8-bit 4:2:0; progressive).
+// Independent H.264 decoder (CAVLC + CABAC; I, P and B slices; Baseline/Main/High;
+// 8-bit 4:2:0; progressive).
 //
 // Written directly from ITU-T H.264 clauses 7-9 and kept deliberately separate
 // from the encoder-side writer (cavlc_writer.cc) and the HIP kernels: it shares
@@ -23,6 +24,7 @@ struct DecodedPicture {
   int coded_width = 0, coded_height = 0;
   int crop_x = 0, crop_y = 0;
   int frame_num = 0;
+  int poc = 0;                        // PicOrderCnt (pictures come out in increasing POC)
   int idr = 0;
   int slice_type = 0;
   std::vector<uint8_t> y, u, v;       // coded size planes
@@ -52,8 +54,8 @@ class Decoder {
  public:
   Decoder();
   ~Decoder();
-  // Decode a complete Annex-B stream; pictures are appended to out() in
-  // decoding order (== output order: no B-frames are supported).
+  // Decode a complete Annex-B stream; pictures are appended to out() in output
+  // (display) order -- in parse-only mode in decoding order.
   void decode(const uint8_t* data, size_t n);
   void flush();
   std::vector<DecodedPicture>& out() { return out_; }

@@ -60,7 +60,7 @@ void write_sps(BitWriter& bw, const SPS& s) {
     bw.put_ue(0);   // max_bits_per_mb_denom
     bw.put_ue(16);  // log2_max_mv_length_horizontal
     bw.put_ue(16);  // log2_max_mv_length_vertical
-    bw.put_ue(0);   // max_num_reorder_frames (no B-frames)
+    bw.put_ue(s.max_num_reorder);   // max_num_reorder_frames (consecutive B-frames)
     bw.put_ue(s.max_num_ref_frames);  // max_dec_frame_buffering
   }
   bw.trailing();
@@ -97,11 +97,18 @@ void write_slice_header(BitWriter& bw, const SliceHeader& h, const SPS& s, const
   bw.put(h.frame_num & ((1u << s.log2_max_frame_num) - 1), s.log2_max_frame_num);
   if (h.nal_unit_type == NAL_IDR) bw.put_ue(h.idr_pic_id);
   if (s.poc_type == 0) bw.put(h.poc_lsb & ((1u << s.log2_max_poc_lsb) - 1), s.log2_max_poc_lsb);
-  if (h.slice_type == SLICE_P) {
+  if (h.slice_type == SLICE_B) bw.put_bit(h.direct_spatial);
+  if (h.slice_type == SLICE_P || h.slice_type == SLICE_B) {
     bw.put_bit(h.num_ref_idx_override);
-    if (h.num_ref_idx_override) bw.put_ue(h.num_ref_idx_l0_active - 1);
+    if (h.num_ref_idx_override) {
+      bw.put_ue(h.num_ref_idx_l0_active - 1);
+      if (h.slice_type == SLICE_B) bw.put_ue(h.num_ref_idx_l1_active - 1);
+    }
     bw.put_bit(0);  // ref_pic_list_modification_flag_l0
+    if (h.slice_type == SLICE_B) bw.put_bit(0);  // ref_pic_list_modification_flag_l1
   }
+  if ((p.weighted_pred && h.slice_type == SLICE_P) || (p.weighted_bipred_idc == 1 && h.slice_type == SLICE_B))
+    throw std::runtime_error("explicit weighted prediction is not written");
   if (h.nal_ref_idc) {
     if (h.nal_unit_type == NAL_IDR) {
       bw.put_bit(h.no_output_of_prior_pics);
@@ -174,10 +181,13 @@ SPS parse_sps(BitReader& br) {
     s.log2_max_poc_lsb = br.get_ue() + 4;
   } else if (s.poc_type == 1) {
     s.delta_pic_order_always_zero = br.get_bit();
-    br.get_se();
-    br.get_se();
+    s.offset_for_non_ref_pic = br.get_se();
+    s.offset_for_top_to_bottom = br.get_se();
     int n = br.get_ue();
-    for (int i = 0; i < n; ++i) br.get_se();
+    if (n > 255) throw std::runtime_error("bad num_ref_frames_in_pic_order_cnt_cycle");
+    for (int i = 0; i < n; ++i) s.offset_for_ref_frame.push_back(br.get_se());
+  } else if (s.poc_type != 2) {
+    throw std::runtime_error("bad pic_order_cnt_type");
   }
   s.max_num_ref_frames = br.get_ue();
   s.gaps_allowed = br.get_bit();
@@ -226,8 +236,11 @@ SPS parse_sps(BitReader& br) {
     if (nal_hrd || vcl_hrd) br.get_bit();
     br.get_bit();  // pic_struct_present_flag
     if (br.get_bit()) {
+      s.vui_reorder_present = 1;
       br.get_bit();
-      for (int i = 0; i < 6; ++i) br.get_ue();
+      for (int i = 0; i < 4; ++i) br.get_ue();
+      s.max_num_reorder = br.get_ue();
+      br.get_ue();
     }
   }
   return s;
@@ -277,28 +290,63 @@ SliceHeader parse_slice_header(BitReader& br, int nal_unit_type, int nal_ref_idc
   if (nal_unit_type == NAL_IDR) h.idr_pic_id = br.get_ue();
   if (s.poc_type == 0) {
     h.poc_lsb = br.get(s.log2_max_poc_lsb);
-    if (p.bottom_field_pic_order_present) br.get_se();
+    if (p.bottom_field_pic_order_present) h.poc_bottom_delta = br.get_se();
   }
   if (s.poc_type == 1 && !s.delta_pic_order_always_zero) {
-    br.get_se();
-    if (p.bottom_field_pic_order_present) br.get_se();
+    h.delta_poc[0] = br.get_se();
+    if (p.bottom_field_pic_order_present) h.delta_poc[1] = br.get_se();
   }
-  if (p.redundant_pic_cnt_present) br.get_ue();
-  if (h.slice_type == SLICE_B) throw std::runtime_error("B slices not supported");
+  if (p.redundant_pic_cnt_present && br.get_ue() != 0) throw std::runtime_error("redundant pictures not supported");
+  if (h.slice_type == SLICE_B) h.direct_spatial = br.get_bit();
   h.num_ref_idx_l0_active = p.num_ref_idx_l0_default;
-  if (h.slice_type == SLICE_P) {
+  h.num_ref_idx_l1_active = p.num_ref_idx_l1_default;
+  if (h.slice_type == SLICE_P || h.slice_type == SLICE_B) {
     h.num_ref_idx_override = br.get_bit();
-    if (h.num_ref_idx_override) h.num_ref_idx_l0_active = br.get_ue() + 1;
-    if (br.get_bit()) {  // ref_pic_list_modification_flag_l0
-      int idc;
-      do {
-        idc = br.get_ue();
-        if (idc == 0 || idc == 1 || idc == 2) br.get_ue();
-      } while (idc != 3);
-      // our decoder keeps a single short-term reference; reordering is a no-op then
+    if (h.num_ref_idx_override) {
+      h.num_ref_idx_l0_active = br.get_ue() + 1;
+      if (h.slice_type == SLICE_B) h.num_ref_idx_l1_active = br.get_ue() + 1;
+    }
+    if (h.num_ref_idx_l0_active > 32 || h.num_ref_idx_l1_active > 32) throw std::runtime_error("too many references");
+    for (int l = 0; l < (h.slice_type == SLICE_B ? 2 : 1); ++l) {
+      if (!br.get_bit()) continue;  // ref_pic_list_modification_flag_lX
+      for (int guard = 0;; ++guard) {
+        if (guard > 64) throw std::runtime_error("ref_pic_list_modification too long");
+        int idc = br.get_ue();
+        if (idc == 3) break;
+        if (idc > 2) throw std::runtime_error("bad modification_of_pic_nums_idc");
+        h.mods[l].push_back(RefMod{idc, static_cast<int>(br.get_ue())});
+      }
     }
   }
-  if (p.weighted_pred && h.slice_type == SLICE_P) throw std::runtime_error("weighted prediction not supported");
+  if ((p.weighted_pred && h.slice_type == SLICE_P) || (p.weighted_bipred_idc == 1 && h.slice_type == SLICE_B)) {
+    h.has_weights = true;
+    WeightTable& w = h.wt;
+    w.luma_log2 = br.get_ue();
+    w.chroma_log2 = br.get_ue();
+    if (w.luma_log2 > 7 || w.chroma_log2 > 7) throw std::runtime_error("bad weight denominator");
+    for (int l = 0; l < (h.slice_type == SLICE_B ? 2 : 1); ++l) {
+      int n = l ? h.num_ref_idx_l1_active : h.num_ref_idx_l0_active;
+      for (int i = 0; i < n; ++i) {
+        w.lflag[l][i] = static_cast<uint8_t>(br.get_bit());
+        w.lw[l][i] = 1 << w.luma_log2;
+        w.lo[l][i] = 0;
+        if (w.lflag[l][i]) {
+          w.lw[l][i] = br.get_se();
+          w.lo[l][i] = br.get_se();
+        }
+        w.cflag[l][i] = static_cast<uint8_t>(br.get_bit());
+        for (int c = 0; c < 2; ++c) {
+          w.cw[l][i][c] = 1 << w.chroma_log2;
+          w.co[l][i][c] = 0;
+        }
+        if (w.cflag[l][i])
+          for (int c = 0; c < 2; ++c) {
+            w.cw[l][i][c] = br.get_se();
+            w.co[l][i][c] = br.get_se();
+          }
+      }
+    }
+  }
   if (nal_ref_idc) {
     if (nal_unit_type == NAL_IDR) {
       h.no_output_of_prior_pics = br.get_bit();
@@ -306,14 +354,18 @@ SliceHeader parse_slice_header(BitReader& br, int nal_unit_type, int nal_ref_idc
     } else {
       h.adaptive_ref_pic_marking = br.get_bit();
       if (h.adaptive_ref_pic_marking) {
-        int op;
-        do {
-          op = br.get_ue();
-          if (op == 1 || op == 3) br.get_ue();
-          if (op == 2) br.get_ue();
-          if (op == 3 || op == 6) br.get_ue();
-          if (op == 4) br.get_ue();
-        } while (op != 0);
+        for (int guard = 0;; ++guard) {
+          if (guard > 128) throw std::runtime_error("dec_ref_pic_marking too long");
+          Mmco m;
+          m.op = br.get_ue();
+          if (m.op == 0) break;
+          if (m.op > 6) throw std::runtime_error("bad memory_management_control_operation");
+          if (m.op == 1 || m.op == 3) m.diff_minus1 = br.get_ue();
+          if (m.op == 2) m.long_term_pic_num = br.get_ue();
+          if (m.op == 3 || m.op == 6) m.long_term_frame_idx = br.get_ue();
+          if (m.op == 4) m.max_long_term_frame_idx_plus1 = br.get_ue();
+          h.mmco.push_back(m);
+        }
       }
     }
   }

@@ -33,8 +33,12 @@ struct SPS {
   int vui_present = 0;
   uint32_t num_units_in_tick = 1, time_scale = 60;
   int fixed_frame_rate = 1;
-  // poc type 1 fields (parsed only)
+  int max_num_reorder = 0;      // VUI bitstream_restriction max_num_reorder_frames (written)
+  int vui_reorder_present = 0;  // parsed: bitstream_restriction present
+  // poc type 1 fields
   int delta_pic_order_always_zero = 0;
+  int offset_for_non_ref_pic = 0, offset_for_top_to_bottom = 0;
+  std::vector<int> offset_for_ref_frame;
 };
 
 struct PPS {
@@ -50,6 +54,24 @@ struct PPS {
   int redundant_pic_cnt_present = 0;
   int transform_8x8_mode = 0;
   int second_chroma_qp_index_offset = 0;
+};
+
+// ref_pic_list_modification() operation (7.3.3.1)
+struct RefMod {
+  int idc;    // modification_of_pic_nums_idc 0..2
+  int value;  // abs_diff_pic_num_minus1 or long_term_pic_num
+};
+// dec_ref_pic_marking() memory_management_control_operation (7.3.3.3)
+struct Mmco {
+  int op;
+  int diff_minus1 = 0, long_term_pic_num = 0, long_term_frame_idx = 0, max_long_term_frame_idx_plus1 = 0;
+};
+// pred_weight_table() (7.3.3.2)
+struct WeightTable {
+  int luma_log2 = 0, chroma_log2 = 0;
+  // [list][ref_idx]: luma weight, offset, chroma weight[2], offset[2]; flag = explicitly present
+  int lw[2][32], lo[2][32], cw[2][32][2], co[2][32][2];
+  uint8_t lflag[2][32], cflag[2][32];
 };
 
 struct SliceHeader {
@@ -69,6 +91,14 @@ struct SliceHeader {
   int cabac_init_idc = 0;
   int no_output_of_prior_pics = 0, long_term_reference = 0;
   int adaptive_ref_pic_marking = 0;
+  int num_ref_idx_l1_active = 1;
+  int direct_spatial = 1;       // direct_spatial_mv_pred_flag (B)
+  int poc_bottom_delta = 0;
+  int delta_poc[2] = {0, 0};    // poc type 1
+  std::vector<RefMod> mods[2];
+  std::vector<Mmco> mmco;
+  bool has_weights = false;
+  WeightTable wt;
   // derived by the parser
   int qp = 26;
 };

@@ -16,7 +16,11 @@ from .. import ops  # noqa: F401  (package import order)
 # MbHeader byte offsets (csrc/common/h264_mb.h)
 _KIND, _CBP, _QP, _I16, _CHROMA, _FLAGS, _REF, _MV, _I4 = 0, 1, 2, 3, 4, 5, 8, 16, 48
 HDR_BYTES = 64
-I4x4, I16x16, P16x16, PSKIP, P16x8, P8x16, P8x8 = 0, 1, 2, 3, 5, 6, 7
+I4x4, I16x16, P16x16, PSKIP, P16x8, P8x16, P8x8, I8x8 = 0, 1, 2, 3, 5, 6, 7, 8
+MBF_T8x8 = 2
+_ZZ8 = [0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6, 7, 14,
+        21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53,
+        60, 61, 54, 47, 55, 62, 63]
 
 _BLK_X = [0, 1, 0, 1, 2, 3, 2, 3, 0, 1, 0, 1, 2, 3, 2, 3]
 _BLK_Y = [0, 0, 1, 1, 0, 0, 1, 1, 2, 2, 3, 3, 2, 2, 3, 3]
@@ -34,6 +38,24 @@ def _i4_modes_ok(rng, mx: int, my: int) -> list[int]:
         if left:
             ok += [1, 8]
         if top and left:
+            ok += [4, 5, 6]
+        out.append(int(rng.choice(ok)))
+    return out
+
+
+def _i8_modes_ok(rng, mx: int, my: int) -> list[int]:
+    """Legal Intra8x8 modes per 8x8 block (8.3.2.2): availability of top / left / top-left."""
+    out = []
+    for b8 in range(4):
+        top = b8 >= 2 or my > 0
+        left = (b8 & 1) == 1 or mx > 0
+        tl = (b8 == 3) or (b8 == 0 and mx > 0 and my > 0) or (b8 == 1 and my > 0) or (b8 == 2 and mx > 0)
+        ok = [2]
+        if top:
+            ok += [0, 3, 7]
+        if left:
+            ok += [1, 8]
+        if top and left and tl:
             ok += [4, 5, 6]
         out.append(int(rng.choice(ok)))
     return out
@@ -57,8 +79,14 @@ def _levels(rng, n: int, density: float, start: int = 0) -> np.ndarray:
     return v
 
 
-def _intra_record(rng, h, c, mx, my, qp, density, allow_i4=True):
-    if allow_i4 and rng.random() < 0.5:
+def _intra_record(rng, h, c, mx, my, qp, density, allow_i4=True, t8x8=False):
+    if t8x8 and rng.random() < 0.35:
+        h[_KIND] = I8x8
+        modes = _i8_modes_ok(rng, mx, my)
+        h[_I4:_I4 + 16] = np.repeat(modes, 4)
+        for b8 in range(4):
+            c[b8 * 64:(b8 + 1) * 64] = _levels(rng, 64, density / 2) if rng.random() < 0.7 else 0
+    elif allow_i4 and rng.random() < 0.5:
         h[_KIND] = I4x4
         h[_I4:_I4 + 16] = _i4_modes_ok(rng, mx, my)
         for b in range(16):
@@ -78,10 +106,14 @@ def _intra_record(rng, h, c, mx, my, qp, density, allow_i4=True):
 
 
 def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp: int = 28,
-                  density: float = 0.15, intra_in_p: float = 0.1, mv_range: int = 48, keyint: int = 0) -> bytes:
-    """Annex-B stream of ``frames`` pictures (IDR + P) from random decision records."""
+                  density: float = 0.15, intra_in_p: float = 0.1, mv_range: int = 48, keyint: int = 0,
+                  cabac: bool = False, t8x8: bool = False, records: list | None = None) -> bytes:
+    """Annex-B stream of ``frames`` pictures (IDR + P) from random decision records.
+
+    cabac / t8x8 select the entropy coder and the High-profile 8x8 transform (I8x8 MBs and
+    8x8-transformed inter MBs).  ``records``, if given, receives (hdr, coef) per picture."""
     rng = np.random.default_rng(seed)
-    cfg = dict(width=width, height=height, qp=qp)
+    cfg = dict(width=width, height=height, qp=qp, cabac=int(cabac), t8x8=int(t8x8))
     wmb, hmb = (width + 15) // 16, (height + 15) // 16
     nmb = wmb * hmb
     out = [host.parameter_sets(cfg)]
@@ -100,7 +132,7 @@ def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp:
             h, c = hdr[mb], coef[mb]
             mqp = int(np.clip(sqp + rng.integers(-3, 4), 0, 51))
             if idr or rng.random() < intra_in_p:
-                _intra_record(rng, h, c, mx, my, mqp, density)
+                _intra_record(rng, h, c, mx, my, mqp, density, t8x8=t8x8)
                 continue
             r = rng.random()
             kind = PSKIP if r < 0.25 else (P16x16 if r < 0.5 else (P16x8 if r < 0.65 else (P8x16 if r < 0.8 else P8x8)))
@@ -116,14 +148,21 @@ def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp:
             h[_MV:_MV + 16] = np.frombuffer(mv.astype(np.int16).tobytes(), np.uint8)
             h[_REF:_REF + 4] = 0
             if kind != PSKIP:
-                for b in range(16):
-                    c[b * 16:(b + 1) * 16] = _levels(rng, 16, density) if rng.random() < 0.6 else 0
+                if t8x8 and rng.random() < 0.5:
+                    h[_FLAGS] = MBF_T8x8
+                    for b8 in range(4):
+                        c[b8 * 64:(b8 + 1) * 64] = _levels(rng, 64, density / 2) if rng.random() < 0.6 else 0
+                else:
+                    for b in range(16):
+                        c[b * 16:(b + 1) * 16] = _levels(rng, 16, density) if rng.random() < 0.6 else 0
                 c[272:280] = _levels(rng, 8, density)
                 for b in range(8):
                     c[280 + b * 16:280 + (b + 1) * 16] = _levels(rng, 16, density / 2, start=1)
         fp = dict(idr=int(idr), qp=sqp, frame_num=fn, idr_pic_id=idr_id)
         nal, _ = host.write_slice(cfg, fp, hdr, coef)
         out.append(nal)
+        if records is not None:
+            records.append((hdr, coef))
         if idr:
             idr_id += 1
         fn = (fn + 1) % 16
