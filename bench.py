@@ -137,7 +137,7 @@ def main() -> None:
             "dtype": "uint8 (8-bit 4:2:0 samples, int32 transforms)",
             "data": "synthetic (GPU-generated moving-texture YUV, new content every step)",
             "config": {
-                "model": "H.264 Constrained Baseline CAVLC, gfx950 batched encoder, CRF from GPU lookahead",
+                "model": f"H.264 {p.profile_name()}, gfx950 batched encoder, CRF from GPU lookahead",
                 "resolution": f"{a.width}x{a.height}",
                 "fps": 30,
                 "crf": a.crf,

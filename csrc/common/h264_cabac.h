@@ -201,30 +201,46 @@ MIVC_HD int cabac_med3(int a, int b, int c) {
   return c > mx ? mx : (c < mn ? mn : c);
 }
 
+// Non-zero block mask of a record: bits 0-15 luma 4x4 blocks (blkIdx; I16x16: AC levels
+// 1..15 only; 8x8 transform: 16-level chunk k of 8x8 block b8 at bit b8 * 4 + k), bit 16
+// luma DC, bits 17 / 18 Cb / Cr DC, bits 19-26 chroma AC (comp * 4 + blk, levels 1..15).
+enum : uint32_t { NZ_LUMA_DC = 1u << 16, NZ_CDC = 3u << 17, NZ_CAC = 0xFFu << 19 };
+MIVC_HD uint32_t cabac_block_mask(const MbHeader& h, const int16_t* c) {
+  uint32_t m = 0;
+  const bool i16 = h.kind == MBK_I16x16;
+  for (int b = 0; b < 16; ++b)
+    for (int i = (i16 ? 1 : 0); i < 16; ++i)
+      if (c[COEF_LUMA + b * 16 + i]) {
+        m |= 1u << b;
+        break;
+      }
+  for (int i = 0; i < 16; ++i)
+    if (i16 && c[COEF_LUMA_DC + i]) m |= NZ_LUMA_DC;
+  for (int k = 0; k < 2; ++k)
+    for (int i = 0; i < 4; ++i)
+      if (c[COEF_CHROMA_DC + k * 4 + i]) m |= 1u << (17 + k);
+  for (int b = 0; b < 8; ++b)
+    for (int i = 1; i < 16; ++i)
+      if (c[COEF_CHROMA_AC + b * 16 + i]) {
+        m |= 1u << (19 + b);
+        break;
+      }
+  return m;
+}
+
 // Cbp of a record as the syntax codes it (luma bits of 8x8 blocks with non-zero levels,
-// chroma 0/1/2).  I16x16: luma 0 or 15.
-MIVC_HD int cabac_record_cbp(const MbHeader& h, const int16_t* c) {
+// chroma 0/1/2; I16x16: luma 0 or 15), from its block mask.
+MIVC_HD int cabac_mask_cbp(const MbHeader& h, uint32_t m) {
   if (h.kind == MBK_IPCM) return 0x2F;
   int luma = 0;
-  const bool i16 = h.kind == MBK_I16x16;
-  const bool t8 = (h.flags & MBF_T8x8) != 0;
-  for (int b8 = 0; b8 < 4; ++b8) {
-    bool nz = false;
-    for (int i = 0; i < 64 && !nz; ++i) {
-      if (!t8 && i16 && (i & 15) == 0) continue;
-      nz = c[COEF_LUMA + b8 * 64 + i] != 0;
-    }
-    if (nz) luma |= 1 << b8;
-  }
-  if (i16 && luma) luma = 15;
-  int chroma = 0;
-  for (int i = 0; i < 128 && !chroma; ++i)
-    if ((i & 15) && c[COEF_CHROMA_AC + i]) chroma = 2;
-  if (!chroma)
-    for (int i = 0; i < 8; ++i)
-      if (c[COEF_CHROMA_DC + i]) chroma = 1;
+  for (int b8 = 0; b8 < 4; ++b8)
+    if ((m >> (b8 * 4)) & 15u) luma |= 1 << b8;
+  if (h.kind == MBK_I16x16 && luma) luma = 15;
+  const int chroma = (m & NZ_CAC) ? 2 : ((m & NZ_CDC) ? 1 : 0);
   return luma | (chroma << 4);
 }
+
+MIVC_HD int cabac_record_cbp(const MbHeader& h, const int16_t* c) { return cabac_mask_cbp(h, cabac_block_mask(h, c)); }
 
 // B mb_type value (Table 7-14) of an inter record (B16x16 / B16x8 / B8x16 / B8x8; the
 // prediction list(s) of each partition are the lists with ref >= 0)
@@ -251,15 +267,20 @@ struct CabacMbWriter {
   int last_qp;         // QP_Y of the previous MB in decoding order
   int last_dqp;        // that MB coded a non-zero mb_qp_delta
   int mx, my;
+  uint32_t mbmask;     // non-zero block mask of the MB being coded
   // statistics
   int n_skip, n_intra, n_inter;
 
-  MIVC_HD void begin(const CabacSliceInfo& s, CabacNb* rowbuf, uint8_t* states, CabacBuf* out) {
+  // states_ready: the caller already initialised the contexts (the GPU kernel does it
+  // with all lanes); row_ready: the row buffer is already marked unavailable
+  MIVC_HD void begin(const CabacSliceInfo& s, CabacNb* rowbuf, uint8_t* states, CabacBuf* out,
+                     bool states_ready = false, bool row_ready = false) {
     si = s;
     row = rowbuf;
-    for (int i = 0; i < s.wmb; ++i) row[i].avail = 0;
+    if (!row_ready)
+      for (int i = 0; i < s.wmb; ++i) row[i].avail = 0;
     tl.avail = 0;
-    cabac_init_contexts(states, s.slice_type == SLICE_I ? 0 : 1 /* cabac_init_idc 0 */, s.slice_qp);
+    if (!states_ready) cabac_init_contexts(states, s.slice_type == SLICE_I ? 0 : 1 /* cabac_init_idc 0 */, s.slice_qp);
     e.init(states, out);
     last_qp = s.slice_qp;
     last_dqp = 0;
@@ -594,8 +615,13 @@ struct CabacMbWriter {
   }
 
   // ---------------------------------------------------------------- residual_block_cabac
-  // c: n coefficients in scan order (levelListIdx order); cat 0..5; cbf_inc < 0: no flag
-  MIVC_HD int put_block(const int16_t* c, int n, int cat, int cbf_inc) {
+  // c: n coefficients in scan order (levelListIdx order); cat 0..5; cbf_inc < 0: no flag;
+  // nonzero = false: the block is known to be all zero (only coded_block_flag = 0)
+  MIVC_HD int put_block(const int16_t* c, int n, int cat, int cbf_inc, bool nonzero = true) {
+    if (!nonzero) {
+      if (cbf_inc >= 0) e.decision(CTX_CBF + kCbfCatOffset[cat] + cbf_inc, 0);
+      return 0;
+    }
     int last = -1;
     for (int i = n - 1; i >= 0; --i)
       if (c[i]) {
@@ -678,12 +704,14 @@ struct CabacMbWriter {
   // ---------------------------------------------------------------- one macroblock
   // h / c: the record; skip_ok: the encoder's motion equals the skip / direct motion
   // (P: derived here; B: the caller's direct derivation).  b_code: B mb_type value.
-  MIVC_HD void code_mb(int mbx, int mby, const MbHeader& h, const int16_t* c, int b_code = 0, const int8_t* b_sub = nullptr) {
+  MIVC_HD void code_mb(int mbx, int mby, const MbHeader& h, const int16_t* c, int b_code = 0, const int8_t* b_sub = nullptr,
+                       const uint32_t* mask_in = nullptr) {
     mx = mbx;
     my = mby;
     const bool pslice = si.slice_type == SLICE_P, bslice = si.slice_type == SLICE_B;
     int kind = h.kind;
-    const int cbp = cabac_record_cbp(h, c);
+    mbmask = mask_in ? *mask_in : cabac_block_mask(h, c);
+    const int cbp = cabac_mask_cbp(h, mbmask);
     const bool intra = mbk_is_intra(kind);
     // ---- reset the current MB context
     cur.avail = 1;
@@ -785,7 +813,7 @@ struct CabacMbWriter {
     last_qp = h.qp;
     // luma
     if (kind == MBK_I16x16) {
-      const int f = put_block(c + COEF_LUMA_DC, 16, 0, cbf_dc_inc(0, true));
+      const int f = put_block(c + COEF_LUMA_DC, 16, 0, cbf_dc_inc(0, true), (mbmask & NZ_LUMA_DC) != 0);
       cur.cbf_dc |= f;
     }
     for (int b8 = 0; b8 < 4; ++b8) {
@@ -801,8 +829,9 @@ struct CabacMbWriter {
         const int x4 = kBlkX[blk], y4 = kBlkY[blk];
         const int inc = cbf_luma_inc(x4, y4, intra);
         int f;
-        if (kind == MBK_I16x16) f = put_block(c + COEF_LUMA + blk * 16 + 1, 15, 1, inc);
-        else f = put_block(c + COEF_LUMA + blk * 16, 16, 2, inc);
+        const bool nzb = (mbmask >> blk) & 1u;
+        if (kind == MBK_I16x16) f = put_block(c + COEF_LUMA + blk * 16 + 1, 15, 1, inc, nzb);
+        else f = put_block(c + COEF_LUMA + blk * 16, 16, 2, inc, nzb);
         if (f) cur.cbf_luma |= static_cast<uint16_t>(1u << (x4 + 4 * y4));
       }
     }
@@ -810,7 +839,8 @@ struct CabacMbWriter {
     const int cc = cbp >> 4;
     if (cc) {
       for (int comp = 0; comp < 2; ++comp) {
-        const int f = put_block(c + COEF_CHROMA_DC + comp * 4, 4, 3, cbf_dc_inc(1 + comp, intra));
+        const int f = put_block(c + COEF_CHROMA_DC + comp * 4, 4, 3, cbf_dc_inc(1 + comp, intra),
+                                ((mbmask >> (17 + comp)) & 1u) != 0);
         cur.cbf_dc |= static_cast<uint8_t>(f << (1 + comp));
       }
     }
@@ -818,7 +848,7 @@ struct CabacMbWriter {
       for (int comp = 0; comp < 2; ++comp)
         for (int b = 0; b < 4; ++b) {
           const int f = put_block(c + COEF_CHROMA_AC + (comp * 4 + b) * 16 + 1, 15, 4,
-                                  cbf_cac_inc(comp, b & 1, b >> 1, intra));
+                                  cbf_cac_inc(comp, b & 1, b >> 1, intra), ((mbmask >> (19 + comp * 4 + b)) & 1u) != 0);
           cur.cbf_cac[comp] |= static_cast<uint8_t>(f << b);
         }
     }
@@ -905,15 +935,17 @@ struct CabacMbWriter {
 // b_codes / b_subs: optional per-MB B mb_type value and sub_mb_types (B slices).
 MIVC_HD size_t cabac_write_slice_data(CabacMbWriter& w, const CabacSliceInfo& si, CabacNb* rowbuf, uint8_t* states,
                                       CabacBuf* out, const MbHeader* hdr, const int16_t* coef, int n,
-                                      const uint8_t* b_codes = nullptr, const int8_t* b_subs = nullptr) {
-  w.begin(si, rowbuf, states, out);
+                                      const uint8_t* b_codes = nullptr, const int8_t* b_subs = nullptr,
+                                      const uint32_t* masks = nullptr, bool states_ready = false,
+                                      bool row_ready = false) {
+  w.begin(si, rowbuf, states, out, states_ready, row_ready);
   const int end = si.first_mb + n;
   for (int addr = si.first_mb; addr < end; ++addr) {
     const int mx = addr % si.wmb, my = addr / si.wmb;
     if (mx == 0) w.tl.avail = 0;
     CabacNb top_old = rowbuf[mx];
     w.code_mb(mx, my, hdr[addr], coef + static_cast<size_t>(addr) * kCoefPerMb, b_codes ? b_codes[addr] : 0,
-              b_subs ? b_subs + static_cast<size_t>(addr) * 4 : nullptr);
+              b_subs ? b_subs + static_cast<size_t>(addr) * 4 : nullptr, masks ? masks + addr : nullptr);
     w.tl = top_old;  // MB (mx, my-1) is the top-left of MB (mx+1, my)
     w.e.terminate(addr == end - 1 ? 1 : 0);
   }

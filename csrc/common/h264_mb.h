@@ -13,6 +13,8 @@
 namespace mivc {
 namespace h264 {
 
+enum SliceType { SLICE_P = 0, SLICE_B = 1, SLICE_I = 2 };
+
 enum MbKind : uint8_t {
   MBK_I4x4 = 0,
   MBK_I16x16 = 1,

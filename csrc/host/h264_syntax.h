@@ -5,13 +5,13 @@
 #include <cstdint>
 #include <vector>
 
+#include "../common/h264_mb.h"
 #include "bitstream.h"
 
 namespace mivc {
 namespace h264 {
 
 enum NalType { NAL_SLICE = 1, NAL_IDR = 5, NAL_SEI = 6, NAL_SPS = 7, NAL_PPS = 8, NAL_AUD = 9 };
-enum SliceType { SLICE_P = 0, SLICE_B = 1, SLICE_I = 2 };
 
 struct SPS {
   int profile_idc = 66;

@@ -60,11 +60,16 @@ class H264Params:
     # x264 --mbtree (default on): lookahead propagation of inter-frame references -> per-MB
     # QP offsets (csrc/kernels/mbtree.hip), with x264's CRF compensation; needs the lookahead
     mbtree: bool = True
+    # entropy coder: CABAC (x264's default; Main profile) or CAVLC (Constrained Baseline)
+    cabac: bool = True
 
     def host_cfg(self) -> dict:
         return dict(width=self.width, height=self.height, fps=self.fps, qp=self.qp,
                     deblock=int(self.deblock), chroma_qp_offset=self.chroma_qp_offset,
-                    vui=int(self.vui))
+                    vui=int(self.vui), cabac=int(self.cabac))
+
+    def profile_name(self) -> str:
+        return "Main CABAC" if self.cabac else "Constrained Baseline CAVLC"
 
     def frame_qps(self) -> tuple[int, int]:
         """(qp_I, qp_P).  CRF maps to the P-frame QP (x264 scale without MB-tree);
@@ -112,7 +117,8 @@ def _resolve(device) -> torch.device:
 
 
 class GpuH264Encoder:
-    """Batched gfx950 H.264 encoder (Constrained Baseline profile, CAVLC)."""
+    """Batched gfx950 H.264 encoder: Main profile with GPU CABAC (default) or Constrained
+    Baseline with GPU CAVLC; ``entropy="cpu"`` codes the slices with the host writers."""
 
     def __init__(self, params: H264Params, slots: int, device: str | torch.device = "cuda",
                  entropy_threads: int | None = None, entropy: str = "gpu"):
@@ -186,6 +192,13 @@ class GpuH264Encoder:
             self.h_out: list = [None, None, None]
             self.out_done = [torch.cuda.Event() for _ in range(2)]
             self.copy_pool = cf.ThreadPoolExecutor(max_workers=1)
+            if params.cabac:
+                # per-slot slice RBSP scratch (worst case ~3 kbit per MB, as for CAVLC) and the
+                # per-MB non-zero block masks of the serial coder
+                self.cab_cap = nmb * 384 + 4096
+                self.cab_slot = torch.empty((B * self.cab_cap,), dtype=u8, device=dev)
+                self.cab_mask = torch.zeros((B, nmb), dtype=torch.int32, device=dev)
+                self.cav_out = [torch.zeros((B * self.cab_cap,), dtype=u8, device=dev) for _ in range(2)]
         self.copy_stream = torch.cuda.Stream(device=dev)
         self.copy_done = [torch.cuda.Event() for _ in range(2)]
         self.compute_done = [torch.cuda.Event() for _ in range(2)]
@@ -265,9 +278,20 @@ class GpuH264Encoder:
     def _frame_params(self, b: int, t: int, qp_frame: int, idr: bool, idr_ids: list[int]) -> dict:
         return dict(idr=int(idr), frame_num=t, idr_pic_id=idr_ids[b] & 0xFFFF, qp=qp_frame)
 
-    def _gpu_cavlc(self, k: int, t: int, qps_t, idr: bool, idr_ids: list[int]):
-        """Launch the CAVLC kernels for the current frame step on the compute stream.
-        qps_t: per-slot slice QP of this frame step (sequence of B ints)."""
+    def _gpu_cabac(self, k: int, t: int, qps_t, idr: bool, idr_ids: list[int], qp_dev: torch.Tensor):
+        """Launch the CABAC kernels for the current frame step on the *copy* stream, so the
+        serial slice coding of frame t overlaps the encode of frame t + 1 (the records are
+        double-buffered; the main stream waits for copy_done[k] before reusing them).
+        qp_dev: [B] int32 slice QPs of this step in a buffer that outlives the launch."""
+        self._header_bits(k, t, qps_t, idr, idr_ids)
+        P = self._ptr
+        self.hip.cabac(self.B, self.wmb, self.hmb, P(self.hdr[k]), P(self.coef[k]), P(self.cab_mask), P(self.cab_slot),
+                       self.cab_cap, P(self.cav_sizes[k]), P(self.cav_hdr_bits[k]), P(self.cav_hdr_nbits[k]),
+                       P(qp_dev), 2 if idr else 0, 1, 1, 0, P(self.cav_out[k]), P(self.cav_out_off), P(self.err),
+                       self.copy_stream.cuda_stream)
+
+    def _header_bits(self, k: int, t: int, qps_t, idr: bool, idr_ids: list[int]):
+        """Slice headers of this step -> pinned host words -> device (current stream)."""
         hb, hn = self.h_hdr_bits[k], self.h_hdr_nbits[k]
         hbn, hnn = hb.numpy(), hn.numpy()
         cache = {}
@@ -282,6 +306,11 @@ class GpuH264Encoder:
             hnn[b] = nbits
         self.cav_hdr_bits[k].copy_(hb, non_blocking=True)
         self.cav_hdr_nbits[k].copy_(hn, non_blocking=True)
+
+    def _gpu_cavlc(self, k: int, t: int, qps_t, idr: bool, idr_ids: list[int]):
+        """Launch the CAVLC kernels for the current frame step on the compute stream.
+        qps_t: per-slot slice QP of this frame step (sequence of B ints)."""
+        self._header_bits(k, t, qps_t, idr, idr_ids)
         P = self._ptr
         self.hip.cavlc(self.B, self.wmb, self.hmb, P(self.hdr[k]), P(self.coef[k]), P(self.cav_mbs), P(self.cav_len),
                        P(self.cav_off), P(self.cav_trail), P(self.cav_total), P(self.cav_sizes[k]),
@@ -445,12 +474,14 @@ class GpuH264Encoder:
                              self._ptr(cur[2]), sse[t].data_ptr(), ssim[t].data_ptr(), self._stream())
             if keep_recon:
                 recons.append(tuple(c.clone() for c in cur))
-            if self.entropy == "gpu":
+            if self.entropy == "gpu" and not self.p.cabac:
                 self._gpu_cavlc(k, t, qpt, idr, idr_ids)
             self.compute_done[k].record(main)
             with torch.cuda.stream(self.copy_stream):
                 self.copy_stream.wait_event(self.compute_done[k])
                 if self.entropy == "gpu":
+                    if self.p.cabac:
+                        self._gpu_cabac(k, t, qpt, idr, idr_ids, qps_d[t])
                     self.h_sizes[k].copy_(self.cav_sizes[k], non_blocking=True)
                 else:
                     self.h_hdr[k].copy_(self.hdr[k], non_blocking=True)
@@ -474,7 +505,10 @@ class GpuH264Encoder:
         if F > 1:
             self.stats["p_intra_ratio"] = float(self.p_intra_mbs.item()) / (B * (F - 1) * self.nmb)
         self.p_intra_mbs.zero_()
-        if int(self.err.item()) != 0:
+        err = int(self.err.item())
+        if err & 2:
+            raise RuntimeError("CABAC slice output overflowed its buffer")
+        if err != 0:
             raise RuntimeError("wavefront progress timeout in an encode kernel")
         ps = self.parameter_sets()
         results = []
