@@ -12,9 +12,12 @@
 //   spec becomes carry propagation into a pending byte followed by a run of 0xFF bytes.
 //   The first bit the spec suppresses (firstBitFlag) is always 0 and is dropped as the
 //   carry position of the first byte.
-// * CabacMbWriter: macroblock_layer() / residual() binarisation and context selection
+// * CabacMbCoder: macroblock_layer() / residual() binarisation and context selection
 //   (clauses 9.3.2, 9.3.3.1) from MbHeader records (h264_mb.h), for I, P and B slices,
-//   4x4 and 8x8 transforms, partitions at 8x8 granularity.
+//   4x4 and 8x8 transforms, partitions at 8x8 granularity.  All context selection is
+//   derived from the records (cabac_prepare_mb + cabac_qp_chain), never from the coder,
+//   so every macroblock can be binarised independently: the GPU binarises a whole
+//   picture in parallel into 16-bit symbols and runs only the arithmetic coder serially.
 #pragma once
 #include <cstddef>
 #include <cstdint>
@@ -131,6 +134,13 @@ struct CabacEncoder {
     ++nbits;
     if (nbits >= 8) drain();
   }
+  // n (1..10) bypass bins at once, the first in bit n-1 of `bits`: each EncodeBypass is
+  // low = 2 * low + b * range, so n of them are low * 2^n + range * bits
+  MIVC_HD void bypass_bits(uint32_t bits, int n) {
+    low = (low << n) + range * bits;
+    nbits += n;
+    if (nbits >= 8) drain();
+  }
   // EncodeTerminate (9.3.4.5); bin = 1 also flushes (EncodeFlush) and writes the
   // rbsp_stop_one_bit plus zero alignment, i.e. the slice data is complete.
   MIVC_HD void terminate(int bin) {
@@ -167,14 +177,67 @@ struct CabacEncoder {
   }
 };
 
-// ---------------------------------------------------------------- neighbour context
-// What later macroblocks need to know about a coded one (kept per MB in a row buffer).
+// ---------------------------------------------------------------- symbol sinks
+// The macroblock binariser (CabacMbCoder) writes into a sink with the engine's interface:
+// decision(ctx, bin), bypass(bin), terminate(bin), bypass_eg(v, k).  CabacEncoder codes
+// directly (host writer); the symbol sinks below record 16-bit symbols instead, so the
+// GPU binarises every macroblock in parallel and only the arithmetic coding is serial:
+//   regular    0 b ccccccccc          bin b with context c (< 512)
+//   bypass     10 nnnn bbbbbbbbbb     n (1..10) bypass bins, first bin in bit n-1
+//   terminate  11 ............ b      end_of_slice / I_PCM terminate bin
+template <class Emit>
+struct CabacSymbolPacker {
+  Emit out;
+  int nb = 0;        // pending bypass bins
+  uint32_t bits = 0;
+  MIVC_HD void flush_bypass() {
+    if (nb) out.emit(static_cast<uint16_t>(0x8000u | (static_cast<uint32_t>(nb) << 10) | bits));
+    nb = 0;
+    bits = 0;
+  }
+  MIVC_HD void decision(int ctx, int bin) {
+    flush_bypass();
+    out.emit(static_cast<uint16_t>((bin ? 0x200u : 0u) | static_cast<uint32_t>(ctx)));
+  }
+  MIVC_HD void bypass(int bin) {
+    bits = (bits << 1) | (bin ? 1u : 0u);
+    if (++nb == 10) flush_bypass();
+  }
+  MIVC_HD void terminate(int bin) {
+    flush_bypass();
+    out.emit(static_cast<uint16_t>(0xC000u | (bin ? 1u : 0u)));
+  }
+  MIVC_HD void bypass_eg(uint32_t v, int k) {
+    while (v >= (1u << k)) {
+      bypass(1);
+      v -= 1u << k;
+      ++k;
+    }
+    bypass(0);
+    while (k--) bypass((v >> k) & 1);
+  }
+};
+struct CabacCountEmit {
+  int n = 0;
+  MIVC_HD void emit(uint16_t) { ++n; }
+};
+struct CabacStoreEmit {
+  uint16_t* p;
+  int n = 0;
+  MIVC_HD void emit(uint16_t s) { p[n++] = s; }
+};
+
+// ---------------------------------------------------------------- per-MB coding state
+// Everything the binarisation of an MB and of its later neighbours needs, computed from
+// the decision records alone (cabac_prepare_mb) plus the mb_qp_delta chain
+// (cabac_qp_chain).  Because nothing here depends on the arithmetic coder, every MB of a
+// slice can be binarised independently.
 struct alignas(8) CabacNb {
-  uint8_t avail;       // coded in this slice
-  uint8_t kind;        // MbKind as coded (MBK_PSKIP for P_Skip)
+  uint8_t avail;       // coded in this slice (set by prepare)
+  uint8_t kind;        // MbKind as coded (MBK_PSKIP for P_Skip, MBK_BDIRECT for B_Skip / B_Direct_16x16)
   uint8_t skip;        // mb_skip_flag
   uint8_t cbp;         // luma bits 0-3 | chroma << 4 (I_PCM: 0x2F)
-  uint8_t t8x8;
+  uint8_t t8x8;        // transform_size_8x8_flag as coded (0 when not coded)
   uint8_t chroma_mode; // intra_chroma_pred_mode (0 for inter / I_PCM)
   uint8_t direct;      // bit q: quadrant q predicted in direct mode
   uint8_t cbf_dc;      // bit0 luma DC, bit1 Cb DC, bit2 Cr DC
@@ -182,8 +245,15 @@ struct alignas(8) CabacNb {
   uint8_t cbf_cac[2];  // chroma AC, bit = raster 2x2 block
   int8_t ref[2][4];    // per quadrant and list (-1: list unused / intra)
   int16_t mv[2][4][2];
-  uint8_t mvd[2][4][2];  // min(|mvd|, 255) per quadrant, list, component
+  int16_t mvd[2][4][2];  // mvd per quadrant, list, component (0 where none is coded)
   uint8_t i4[16];      // Intra4x4/8x8 pred mode per raster 4x4 (2 = DC for non-NxN)
+  uint8_t i16_mode;
+  uint8_t b_code;      // B mb_type (Table 7-14)
+  int8_t dqp;          // mb_qp_delta (if coded)
+  uint8_t prev_dqp_nz; // the previous MB in decoding order coded a non-zero mb_qp_delta
+  int8_t qp;           // QP_Y of the record
+  uint8_t pad[3];
+  uint32_t mask;       // non-zero block mask (cabac_block_mask)
 };
 
 struct CabacSliceInfo {
@@ -256,119 +326,275 @@ MIVC_HD int cabac_b_code(const MbHeader& h) {
   return 4 + 2 * idx + (h.kind == MBK_B16x8 ? 0 : 1);
 }
 
-// Macroblock-layer writer.  The caller owns the row buffer (wmb CabacNb entries) and
-// codes MBs of one slice in raster order; see cabac_write_slice_data for the loop.
-struct CabacMbWriter {
-  CabacEncoder e;
-  CabacSliceInfo si;
-  CabacNb* row;        // [wmb]: entry mx is MB (mx, my-1) before MB (mx, my) is coded
-  CabacNb tl;          // MB (mx-1, my-1), saved before row[mx-1] was overwritten
-  CabacNb cur;         // the MB being coded
-  int last_qp;         // QP_Y of the previous MB in decoding order
-  int last_dqp;        // that MB coded a non-zero mb_qp_delta
-  int mx, my;
-  uint32_t mbmask;     // non-zero block mask of the MB being coded
-  // statistics
-  int n_skip, n_intra, n_inter;
-
-  // states_ready: the caller already initialised the contexts (the GPU kernel does it
-  // with all lanes); row_ready: the row buffer is already marked unavailable
-  MIVC_HD void begin(const CabacSliceInfo& s, CabacNb* rowbuf, uint8_t* states, CabacBuf* out,
-                     bool states_ready = false, bool row_ready = false) {
-    si = s;
-    row = rowbuf;
-    if (!row_ready)
-      for (int i = 0; i < s.wmb; ++i) row[i].avail = 0;
-    tl.avail = 0;
-    if (!states_ready) cabac_init_contexts(states, s.slice_type == SLICE_I ? 0 : 1 /* cabac_init_idc 0 */, s.slice_qp);
-    e.init(states, out);
-    last_qp = s.slice_qp;
-    last_dqp = 0;
-    n_skip = n_intra = n_inter = 0;
+// Partition layout of an inter MB kind: np partitions starting at quadrants qfirst[],
+// width w4[] (4x4 units), shape 0 generic / 1 16x8 / 2 8x16, quadrant masks pm[].
+struct CabacParts {
+  int np, shape;
+  int qfirst[4], w4[4], pm[4];
+};
+MIVC_HD CabacParts cabac_parts(int kind) {
+  CabacParts p{};
+  if (kind == MBK_P16x16 || kind == MBK_B16x16 || kind == MBK_PSKIP) {
+    p.np = 1; p.shape = 0; p.qfirst[0] = 0; p.w4[0] = 4; p.pm[0] = 0xF;
+  } else if (kind == MBK_P16x8 || kind == MBK_B16x8) {
+    p.np = 2; p.shape = 1; p.qfirst[0] = 0; p.qfirst[1] = 2; p.w4[0] = p.w4[1] = 4; p.pm[0] = 0x3; p.pm[1] = 0xC;
+  } else if (kind == MBK_P8x16 || kind == MBK_B8x16) {
+    p.np = 2; p.shape = 2; p.qfirst[0] = 0; p.qfirst[1] = 1; p.w4[0] = p.w4[1] = 2; p.pm[0] = 0x5; p.pm[1] = 0xA;
+  } else {
+    p.np = 4; p.shape = 0;
+    for (int q = 0; q < 4; ++q) { p.qfirst[q] = q; p.w4[q] = 2; p.pm[q] = 1 << q; }
   }
+  return p;
+}
 
-  // ---------------------------------------------------------------- neighbour access
-  // MB holding the 4x4 block at (x4, y4) relative to the current MB (x4, y4 in -1..4);
-  // nullptr when unavailable.  Blocks inside the current MB return &cur.
-  MIVC_HD const CabacNb* nb_mb(int x4, int y4) const {
+// Neighbourhood of one MB inside a picture-sized table of records / states.
+struct CabacView {
+  int wmb, first_mb;
+  int addr, mx, my;
+  MIVC_HD void at(int a, int w, int first) {
+    wmb = w;
+    first_mb = first;
+    addr = a;
+    mx = a % w;
+    my = a / w;
+  }
+  // address of the MB holding the 4x4 block (x4, y4) relative to this MB (-1..4), or -1
+  MIVC_HD int mb_of(int x4, int y4) const {
+    int n;
     if (y4 < 0) {
-      if (x4 < 0) return (mx > 0 && tl.avail) ? &tl : nullptr;
-      if (x4 < 4) return row[mx].avail ? &row[mx] : nullptr;
-      return (mx + 1 < si.wmb && row[mx + 1].avail) ? &row[mx + 1] : nullptr;
+      if (my == 0) return -1;
+      if (x4 < 0) n = mx > 0 ? addr - wmb - 1 : -1;
+      else if (x4 < 4) n = addr - wmb;
+      else n = mx + 1 < wmb ? addr - wmb + 1 : -1;
+    } else if (y4 < 4) {
+      if (x4 < 0) n = mx > 0 ? addr - 1 : -1;
+      else if (x4 < 4) n = addr;
+      else return -1;
+    } else {
+      return -1;
     }
-    if (y4 > 3) return nullptr;
-    if (x4 < 0) return (mx > 0 && row[mx - 1].avail) ? &row[mx - 1] : nullptr;
-    if (x4 > 3) return nullptr;
-    return &cur;
+    return n >= first_mb ? n : -1;
   }
-  MIVC_HD bool top_avail() const { return row[mx].avail != 0; }
-  MIVC_HD bool left_avail() const { return mx > 0 && row[mx - 1].avail; }
-  MIVC_HD const CabacNb* A() const { return left_avail() ? &row[mx - 1] : nullptr; }
-  MIVC_HD const CabacNb* B() const { return top_avail() ? &row[mx] : nullptr; }
-
   static MIVC_HD int quad_of(int x4, int y4) { return (((x4 + 4) & 3) >> 1) + 2 * (((y4 + 4) & 3) >> 1); }
   static MIVC_HD int rast_of(int x4, int y4) { return ((x4 + 4) & 3) + 4 * ((y4 + 4) & 3); }
+};
 
-  // ---------------------------------------------------------------- motion vector prediction (8.4.1.3)
-  // partition with top-left 4x4 (bx, by), width w4 (4x4 units), shape 0 generic, 1 16x8,
-  // 2 8x16; done = quadrants of the current MB already assigned (bit mask).
-  MIVC_HD void mvp(int list, int ref, int bx, int by, int w4, int shape, int part, int done, int out[2]) const {
-    struct N {
-      bool avail;
-      int ref;
-      int mv[2];
-    };
-    auto get = [&](int x4, int y4) -> N {
-      N n{false, -1, {0, 0}};
-      const CabacNb* m = nb_mb(x4, y4);
-      if (!m) return n;
-      const int q = quad_of(x4, y4);
-      if (m == &cur && !((done >> q) & 1)) return n;
-      n.avail = true;
-      if (mbk_is_intra(m->kind)) return n;
-      n.ref = m->ref[list][q];
-      if (n.ref >= 0) {
-        n.mv[0] = m->mv[list][q][0];
-        n.mv[1] = m->mv[list][q][1];
+// ---------------------------------------------------------------- motion vector prediction (8.4.1.3)
+// From the records: partition with top-left 4x4 (bx, by), width w4, shape 0/1/2, part index;
+// done = quadrants of MB v.addr already assigned (the record's own MVs count for them).
+MIVC_HD void cabac_mvp(const CabacView& v, const MbHeader* hdr, int list, int ref, int bx, int by, int w4, int shape,
+                       int part, int done, int out[2]) {
+  struct N {
+    bool avail;
+    int ref;
+    int mv[2];
+  };
+  auto get = [&](int x4, int y4) -> N {
+    N n{false, -1, {0, 0}};
+    const int a = v.mb_of(x4, y4);
+    if (a < 0) return n;
+    const int q = CabacView::quad_of(x4, y4);
+    if (a == v.addr && !((done >> q) & 1)) return n;
+    n.avail = true;
+    const MbHeader& m = hdr[a];
+    if (mbk_is_intra(m.kind)) return n;
+    n.ref = m.ref[list][q];
+    if (n.ref >= 0) {
+      n.mv[0] = m.mv[list][q][0];
+      n.mv[1] = m.mv[list][q][1];
+    }
+    return n;
+  };
+  N a = get(bx - 1, by), b = get(bx, by - 1), c = get(bx + w4, by - 1);
+  if (!c.avail) c = get(bx - 1, by - 1);
+  if (shape == 1) {
+    if (part == 0 && b.ref == ref) { out[0] = b.mv[0]; out[1] = b.mv[1]; return; }
+    if (part == 1 && a.ref == ref) { out[0] = a.mv[0]; out[1] = a.mv[1]; return; }
+  } else if (shape == 2) {
+    if (part == 0 && a.ref == ref) { out[0] = a.mv[0]; out[1] = a.mv[1]; return; }
+    if (part == 1 && c.ref == ref) { out[0] = c.mv[0]; out[1] = c.mv[1]; return; }
+  }
+  if (!b.avail && !c.avail && a.avail) {
+    b = a;
+    c = a;
+  }
+  const int match = (a.ref == ref) + (b.ref == ref) + (c.ref == ref);
+  if (match == 1) {
+    const N& m = a.ref == ref ? a : (b.ref == ref ? b : c);
+    out[0] = m.mv[0];
+    out[1] = m.mv[1];
+    return;
+  }
+  out[0] = cabac_med3(a.mv[0], b.mv[0], c.mv[0]);
+  out[1] = cabac_med3(a.mv[1], b.mv[1], c.mv[1]);
+}
+
+// P_Skip motion (8.4.1.1) from the records
+MIVC_HD void cabac_pskip_mv(const CabacView& v, const MbHeader* hdr, int out[2]) {
+  out[0] = out[1] = 0;
+  const int a = v.mb_of(-1, 0), b = v.mb_of(0, -1);
+  if (a < 0 || b < 0) return;
+  const MbHeader& A = hdr[a];
+  const MbHeader& B = hdr[b];
+  if (!mbk_is_intra(A.kind) && A.ref[0][1] == 0 && A.mv[0][1][0] == 0 && A.mv[0][1][1] == 0) return;
+  if (!mbk_is_intra(B.kind) && B.ref[0][2] == 0 && B.mv[0][2][0] == 0 && B.mv[0][2][1] == 0) return;
+  cabac_mvp(v, hdr, 0, 0, 0, 0, 4, 0, 0, 0, out);
+}
+
+// Coding state of MB addr from its record (and its neighbours' records).  mask: the
+// record's non-zero block mask (cabac_block_mask).  dqp / prev_dqp_nz are set later by
+// cabac_qp_chain.
+MIVC_HD void cabac_prepare_mb(const CabacSliceInfo& si, const MbHeader* hdr, int addr, uint32_t mask, CabacNb& n) {
+  CabacView v;
+  v.at(addr, si.wmb, si.first_mb);
+  const MbHeader& h = hdr[addr];
+  const bool pslice = si.slice_type == SLICE_P, bslice = si.slice_type == SLICE_B;
+  int kind = h.kind;
+  const bool intra = mbk_is_intra(kind);
+  const int cbp = cabac_mask_cbp(h, mask);
+  n.avail = 1;
+  n.skip = 0;
+  n.cbp = static_cast<uint8_t>(cbp);
+  n.t8x8 = 0;
+  n.chroma_mode = 0;
+  n.direct = 0;
+  n.cbf_dc = 0;
+  n.cbf_luma = 0;
+  n.cbf_cac[0] = n.cbf_cac[1] = 0;
+  n.i16_mode = h.i16_mode;
+  n.qp = h.qp;
+  n.mask = mask;
+  n.dqp = 0;
+  n.prev_dqp_nz = 0;
+  n.b_code = 0;
+  for (int l = 0; l < 2; ++l)
+    for (int q = 0; q < 4; ++q) {
+      n.ref[l][q] = intra ? -1 : h.ref[l][q];
+      n.mv[l][q][0] = intra ? 0 : h.mv[l][q][0];
+      n.mv[l][q][1] = intra ? 0 : h.mv[l][q][1];
+      n.mvd[l][q][0] = n.mvd[l][q][1] = 0;
+    }
+  for (int i = 0; i < 16; ++i) n.i4[i] = 2;
+  // ---- skip
+  bool skip = false;
+  if (pslice && (kind == MBK_P16x16 || kind == MBK_PSKIP) && cbp == 0 && h.ref[0][0] == 0) {
+    int smv[2];
+    cabac_pskip_mv(v, hdr, smv);
+    skip = smv[0] == h.mv[0][0][0] && smv[1] == h.mv[0][0][1];
+  } else if (bslice && kind == MBK_BDIRECT && cbp == 0) {
+    skip = true;
+  }
+  if (skip) {
+    n.skip = 1;
+    n.kind = static_cast<uint8_t>(pslice ? MBK_PSKIP : MBK_BDIRECT);
+    n.cbp = 0;
+    if (bslice) n.direct = 0xF;
+    return;
+  }
+  if (kind == MBK_PSKIP) kind = MBK_P16x16;
+  n.kind = static_cast<uint8_t>(kind);
+  if (bslice && !intra) n.b_code = static_cast<uint8_t>(cabac_b_code(h));
+  // ---- intra modes
+  if (kind == MBK_I4x4)
+    for (int blk = 0; blk < 16; ++blk) n.i4[kBlkX[blk] + 4 * kBlkY[blk]] = h.i4_modes[blk];
+  if (kind == MBK_I8x8)
+    for (int b8 = 0; b8 < 4; ++b8)
+      for (int k = 0; k < 4; ++k)
+        n.i4[(b8 & 1) * 2 + (k & 1) + 4 * ((b8 >> 1) * 2 + (k >> 1))] = h.i4_modes[b8 * 4];
+  if (intra) n.chroma_mode = h.chroma_mode;
+  // ---- transform size as coded
+  if (kind == MBK_I8x8) n.t8x8 = 1;
+  else if (!intra && (cbp & 15) && si.t8x8_mode && (h.flags & MBF_T8x8)) n.t8x8 = 1;
+  // ---- direct / mvd (partition order, list 0 then list 1)
+  if (kind == MBK_BDIRECT) {
+    n.direct = 0xF;
+  } else if (!intra) {
+    const CabacParts P = cabac_parts(kind);
+    const int dir_mask = kind == MBK_B8x8 ? (h.sub_direct & 15) : 0;
+    n.direct = static_cast<uint8_t>(dir_mask);
+    for (int l = 0; l < 2; ++l) {
+      int done = 0;
+      for (int p = 0; p < P.np; ++p) {
+        const int q = P.qfirst[p];
+        if (((dir_mask >> q) & 1) || h.ref[l][q] < 0) {
+          done |= P.pm[p];
+          continue;
+        }
+        int pm[2];
+        cabac_mvp(v, hdr, l, h.ref[l][q], (q & 1) * 2, (q >> 1) * 2, P.w4[p], P.shape, p, done, pm);
+        const int dx = h.mv[l][q][0] - pm[0], dy = h.mv[l][q][1] - pm[1];
+        for (int k = 0; k < 4; ++k)
+          if ((P.pm[p] >> k) & 1) {
+            n.mvd[l][k][0] = static_cast<int16_t>(dx);
+            n.mvd[l][k][1] = static_cast<int16_t>(dy);
+          }
+        done |= P.pm[p];
       }
-      return n;
-    };
-    N a = get(bx - 1, by), b = get(bx, by - 1), c = get(bx + w4, by - 1);
-    // C inside the current MB below-right of a finished partition is "not yet decoded";
-    // a C to the right of the MB below the top row is unavailable (nb_mb returns null)
-    if (!c.avail) c = get(bx - 1, by - 1);
-    if (shape == 1) {
-      if (part == 0 && b.ref == ref) { out[0] = b.mv[0]; out[1] = b.mv[1]; return; }
-      if (part == 1 && a.ref == ref) { out[0] = a.mv[0]; out[1] = a.mv[1]; return; }
-    } else if (shape == 2) {
-      if (part == 0 && a.ref == ref) { out[0] = a.mv[0]; out[1] = a.mv[1]; return; }
-      if (part == 1 && c.ref == ref) { out[0] = c.mv[0]; out[1] = c.mv[1]; return; }
     }
-    if (!b.avail && !c.avail && a.avail) {
-      b = a;
-      c = a;
-    }
-    const int match = (a.ref == ref) + (b.ref == ref) + (c.ref == ref);
-    if (match == 1) {
-      const N& m = a.ref == ref ? a : (b.ref == ref ? b : c);
-      out[0] = m.mv[0];
-      out[1] = m.mv[1];
-      return;
-    }
-    out[0] = cabac_med3(a.mv[0], b.mv[0], c.mv[0]);
-    out[1] = cabac_med3(a.mv[1], b.mv[1], c.mv[1]);
   }
+  // ---- coded_block_flags as neighbours see them
+  const int cc = cbp >> 4;
+  if (kind == MBK_I16x16 && (mask & NZ_LUMA_DC)) n.cbf_dc |= 1;
+  if (cc) n.cbf_dc |= static_cast<uint8_t>(((mask >> 17) & 3u) << 1);
+  if (cc == 2) {
+    n.cbf_cac[0] = static_cast<uint8_t>((mask >> 19) & 15u);
+    n.cbf_cac[1] = static_cast<uint8_t>((mask >> 23) & 15u);
+  }
+  for (int b8 = 0; b8 < 4; ++b8) {
+    if (!((cbp >> b8) & 1)) continue;
+    const int x4 = (b8 & 1) * 2, y4 = (b8 >> 1) * 2;
+    if (n.t8x8) {
+      n.cbf_luma |= static_cast<uint16_t>(0x33u << (x4 + 4 * y4));  // 8x8 blocks: flag inferred 1
+      continue;
+    }
+    for (int b4 = 0; b4 < 4; ++b4) {
+      const int blk = b8 * 4 + b4;
+      if ((mask >> blk) & 1u) n.cbf_luma |= static_cast<uint16_t>(1u << (kBlkX[blk] + 4 * kBlkY[blk]));
+    }
+  }
+}
 
-  // P_Skip motion (8.4.1.1)
-  MIVC_HD void pskip_mv(int out[2]) const {
-    out[0] = out[1] = 0;
-    const CabacNb* a = A();
-    const CabacNb* b = B();
-    if (!a || !b) return;
-    if (!mbk_is_intra(a->kind) && a->ref[0][1] == 0 && a->mv[0][1][0] == 0 && a->mv[0][1][1] == 0) return;
-    if (!mbk_is_intra(b->kind) && b->ref[0][2] == 0 && b->mv[0][2][0] == 0 && b->mv[0][2][1] == 0) return;
-    mvp(0, 0, 0, 0, 4, 0, 0, 0, out);
+// mb_qp_delta of every MB of a slice (QP_pred chain, 7.4.5) and the context flag of its
+// first bin: nb[first_mb .. first_mb + n).  Serial; the GPU runs it as a scan.
+MIVC_HD void cabac_qp_chain(const CabacSliceInfo& si, CabacNb* nb, int n) {
+  int last_qp = si.slice_qp, last_nz = 0;
+  for (int a = si.first_mb; a < si.first_mb + n; ++a) {
+    CabacNb& m = nb[a];
+    const bool has = !m.skip && (m.cbp != 0 || m.kind == MBK_I16x16);
+    m.prev_dqp_nz = static_cast<uint8_t>(last_nz);
+    if (has) {
+      int d = m.qp - last_qp;
+      if (d < -26) d += 52;
+      if (d > 25) d -= 52;
+      m.dqp = static_cast<int8_t>(d);
+      last_qp = m.qp;
+      last_nz = d != 0;
+    } else {
+      m.dqp = 0;
+      last_nz = 0;
+    }
   }
+}
+
+// ---------------------------------------------------------------- macroblock binariser
+// Binarises MB addr (7.3.5 / 9.3.2 / 9.3.3.1) into sink E, followed by its
+// end_of_slice_flag.  nb: prepared coding states of the whole picture.
+template <class E>
+struct CabacMbCoder {
+  E& e;
+  const CabacSliceInfo& si;
+  const CabacNb* nb;
+  CabacView v;
+  const CabacNb* cur;
+
+  MIVC_HD CabacMbCoder(E& e_, const CabacSliceInfo& s, const CabacNb* table) : e(e_), si(s), nb(table), cur(nullptr) {}
+
+  MIVC_HD const CabacNb* nb_mb(int x4, int y4) const {
+    const int a = v.mb_of(x4, y4);
+    return a < 0 ? nullptr : &nb[a];
+  }
+  MIVC_HD const CabacNb* A() const { return nb_mb(-1, 0); }
+  MIVC_HD const CabacNb* B() const { return nb_mb(0, -1); }
 
   // ---------------------------------------------------------------- syntax elements
   MIVC_HD void put_mb_skip(int skip) {
@@ -378,8 +604,7 @@ struct CabacMbWriter {
     e.decision((si.slice_type == SLICE_B ? CTX_MB_SKIP_B : CTX_MB_SKIP_P) + inc, skip);
   }
 
-  // I mb_type bins after the prefix: offset = first context of the I binarisation
-  // (3 in I slices with neighbour ctx for bin 0; 17 / 32 suffix in P / B slices)
+  // I mb_type (I slices: with the neighbour context of bin 0; P / B: the suffix)
   MIVC_HD void put_mb_type_i(int kind, int i16_mode, int cbp, bool islice) {
     if (islice) {
       const CabacNb* a = A();
@@ -422,69 +647,48 @@ struct CabacMbWriter {
     }
   }
 
-  // B mb_type (Table 9-37(b)); bits = the bin string after bin 0, MSB first, nb bins
+  // B mb_type (Table 9-37(b)); code: B mb_type value 0..22, 23 = intra prefix
   MIVC_HD void put_mb_type_b(int kind, int i16_mode, int cbp, int code) {
     const CabacNb* a = A();
     const CabacNb* b = B();
     const int inc = (a && !a->skip && a->kind != MBK_BDIRECT) + (b && !b->skip && b->kind != MBK_BDIRECT);
-    if (kind == MBK_BDIRECT) {
+    if (code == 0) {
       e.decision(CTX_MB_TYPE_B + inc, 0);
       return;
     }
     e.decision(CTX_MB_TYPE_B + inc, 1);
-    // code: B mb_type value 1..22 (Table 7-14), 23 = intra prefix
     if (code <= 2) {  // B_L0_16x16 "100", B_L1_16x16 "101"
       e.decision(CTX_MB_TYPE_B + 3, 0);
       e.decision(CTX_MB_TYPE_B + 5, code - 1);
       return;
     }
     e.decision(CTX_MB_TYPE_B + 3, 1);
-    int bits, nb;
-    if (code <= 10) { bits = code - 3; nb = 4; }                // 1 1 0 xxx: 3..10 -> 0000..0111 (4 bins incl. the 0)
-    else if (code == 11) { bits = 0x3E; nb = 0; }               // handled below
-    else if (code == 22) { bits = 0x1F; nb = 0; }
-    else if (code == 23) { bits = 0x1D; nb = 0; }
-    else { bits = code - 12 + 0x10; nb = 5; }                   // 12..21: 1 1 1 0 xxx / 1 1 1 1 0 xx
-    if (code <= 10) {
-      // bins 2..5: 0 b b b
+    if (code <= 10) {  // 1 1 0 b b b
+      const int v3 = code - 3;
       e.decision(CTX_MB_TYPE_B + 4, 0);
-      e.decision(CTX_MB_TYPE_B + 5, (bits >> 2) & 1);
-      e.decision(CTX_MB_TYPE_B + 5, (bits >> 1) & 1);
-      e.decision(CTX_MB_TYPE_B + 5, bits & 1);
+      e.decision(CTX_MB_TYPE_B + 5, (v3 >> 2) & 1);
+      e.decision(CTX_MB_TYPE_B + 5, (v3 >> 1) & 1);
+      e.decision(CTX_MB_TYPE_B + 5, v3 & 1);
       return;
     }
     e.decision(CTX_MB_TYPE_B + 4, 1);
-    if (code == 11) {  // 1 1 1 1 1 0
+    if (code == 11 || code == 22 || code == 23) {  // 1 1 1 1 1 0 / 1 1 1 1 1 1 / 1 1 1 1 0 1
       e.decision(CTX_MB_TYPE_B + 5, 1);
-      e.decision(CTX_MB_TYPE_B + 5, 1);
-      e.decision(CTX_MB_TYPE_B + 5, 0);
+      e.decision(CTX_MB_TYPE_B + 5, code == 23 ? 0 : 1);
+      e.decision(CTX_MB_TYPE_B + 5, code == 11 ? 0 : 1);
+      if (code == 23) put_mb_type_i(kind, i16_mode, cbp, false);
       return;
     }
-    if (code == 22) {  // B_8x8: 1 1 1 1 1 1
-      e.decision(CTX_MB_TYPE_B + 5, 1);
-      e.decision(CTX_MB_TYPE_B + 5, 1);
-      e.decision(CTX_MB_TYPE_B + 5, 1);
-      return;
-    }
-    if (code == 23) {  // intra prefix: 1 1 1 1 0 1
-      e.decision(CTX_MB_TYPE_B + 5, 1);
-      e.decision(CTX_MB_TYPE_B + 5, 0);
-      e.decision(CTX_MB_TYPE_B + 5, 1);
-      put_mb_type_i(kind, i16_mode, cbp, false);
-      return;
-    }
-    // 12..21 -> bins 3..6 = 4-bit value (code - 12) with 12..19 = 0xxx, 20..21 = 100x
-    const int v = code - 12;
-    e.decision(CTX_MB_TYPE_B + 5, (v >> 3) & 1);
-    e.decision(CTX_MB_TYPE_B + 5, (v >> 2) & 1);
-    e.decision(CTX_MB_TYPE_B + 5, (v >> 1) & 1);
-    e.decision(CTX_MB_TYPE_B + 5, v & 1);
-    (void)nb;
+    // 12..21: bins 3..6 = the 4-bit value code - 12
+    const int v4 = code - 12;
+    e.decision(CTX_MB_TYPE_B + 5, (v4 >> 3) & 1);
+    e.decision(CTX_MB_TYPE_B + 5, (v4 >> 2) & 1);
+    e.decision(CTX_MB_TYPE_B + 5, (v4 >> 1) & 1);
+    e.decision(CTX_MB_TYPE_B + 5, v4 & 1);
   }
 
   MIVC_HD void put_sub_mb_type_b(int code) {
-    // Table 9-38: 0 direct "0", 1 "100", 2 "101", 3 "11000", 4 "11001", 5 "11010", 6 "11011",
-    // 7 "111000", 8 "111001", 9 "111010", 10 "111011", 11 "11110", 12 "11111"
+    // Table 9-38: 0 "0", 1 "100", 2 "101", 3..6 "110xx", 7..10 "1110xx", 11 "11110", 12 "11111"
     if (code == 0) { e.decision(CTX_SUB_MB_B, 0); return; }
     e.decision(CTX_SUB_MB_B, 1);
     if (code <= 2) {
@@ -511,47 +715,47 @@ struct CabacMbWriter {
   }
 
   MIVC_HD void put_ref_idx(int list, int q, int ref) {
-    // neighbours A / B of the partition's top-left 4x4 (quadrant granularity)
     const int x4 = (q & 1) * 2, y4 = (q >> 1) * 2;
-    auto cond = [&](const CabacNb* m, int qn) -> int {
+    auto cond = [&](int xn, int yn) -> int {
+      const CabacNb* m = nb_mb(xn, yn);
       if (!m || m->skip || mbk_is_intra(m->kind)) return 0;
+      const int qn = CabacView::quad_of(xn, yn);
       if ((m->direct >> qn) & 1) return 0;
       return m->ref[list][qn] > 0;
     };
-    const CabacNb* a = nb_mb(x4 - 1, y4);
-    const CabacNb* b = nb_mb(x4, y4 - 1);
-    const int inc = cond(a, quad_of(x4 - 1, y4)) + 2 * cond(b, quad_of(x4, y4 - 1));
+    const int inc = cond(x4 - 1, y4) + 2 * cond(x4, y4 - 1);
     e.decision(CTX_REF_IDX + inc, ref > 0);
     if (ref == 0) return;
     for (int k = 1; k < ref; ++k) e.decision(CTX_REF_IDX + (k == 1 ? 4 : 5), 1);
     e.decision(CTX_REF_IDX + (ref == 1 ? 4 : 5), 0);
   }
 
-  MIVC_HD void put_mvd(int list, int q, int comp, int v) {
+  MIVC_HD void put_mvd(int list, int q, int comp, int val) {
     const int x4 = (q & 1) * 2, y4 = (q >> 1) * 2;
-    auto absn = [&](const CabacNb* m, int qn) -> int {
+    auto absn = [&](int xn, int yn) -> int {
+      const CabacNb* m = nb_mb(xn, yn);
       if (!m) return 0;
-      return m->mvd[list][qn][comp];
+      const int d = m->mvd[list][CabacView::quad_of(xn, yn)][comp];
+      return d < 0 ? -d : d;
     };
-    const int sum = absn(nb_mb(x4 - 1, y4), quad_of(x4 - 1, y4)) + absn(nb_mb(x4, y4 - 1), quad_of(x4, y4 - 1));
+    const int sum = absn(x4 - 1, y4) + absn(x4, y4 - 1);
     const int base = comp ? CTX_MVD_Y : CTX_MVD_X;
     const int inc0 = sum < 3 ? 0 : (sum > 32 ? 2 : 1);
-    const int av = v < 0 ? -v : v;
+    const int av = val < 0 ? -val : val;
     const int pre = av < 9 ? av : 9;
     e.decision(base + inc0, pre > 0);
     if (pre > 0) {
       for (int k = 1; k < pre; ++k) e.decision(base + (k < 4 ? k + 2 : 6), 1);
       if (pre < 9) e.decision(base + (pre < 4 ? pre + 2 : 6), 0);
       if (av >= 9) e.bypass_eg(static_cast<uint32_t>(av - 9), 3);
-      e.bypass(v < 0);
+      e.bypass(val < 0);
     }
   }
 
-  MIVC_HD void put_cbp(int cbp, bool intra_cur) {
-    (void)intra_cur;
+  MIVC_HD void put_cbp(int cbp) {
     const CabacNb* a = A();
     const CabacNb* b = B();
-    // unavailable neighbours and I_PCM count as "all blocks coded"
+    // unavailable neighbours and I_PCM count as "all luma blocks coded" / chroma 0 / 2
     const int la = a ? (a->kind == MBK_IPCM ? 0x2F : a->cbp) : 0x0F;
     const int lb = b ? (b->kind == MBK_IPCM ? 0x2F : b->cbp) : 0x0F;
     for (int b8 = 0; b8 < 4; ++b8) {
@@ -566,9 +770,9 @@ struct CabacMbWriter {
     if (cc) e.decision(CTX_CBP_CHROMA + 4 + (ca == 2) + 2 * (cb == 2), cc == 2);
   }
 
-  MIVC_HD void put_qp_delta(int d) {
+  MIVC_HD void put_qp_delta(int d, int prev_nz) {
     const int m = d > 0 ? 2 * d - 1 : -2 * d;
-    e.decision(CTX_QP_DELTA + (last_dqp ? 1 : 0), m > 0);
+    e.decision(CTX_QP_DELTA + (prev_nz ? 1 : 0), m > 0);
     if (m > 0) {
       for (int k = 1; k < m; ++k) e.decision(CTX_QP_DELTA + (k == 1 ? 2 : 3), 1);
       e.decision(CTX_QP_DELTA + (m == 1 ? 2 : 3), 0);
@@ -592,8 +796,8 @@ struct CabacMbWriter {
     const CabacNb* a = nb_mb(x4 - 1, y4);
     const CabacNb* b = nb_mb(x4, y4 - 1);
     if (!a || !b) return 2;
-    const int ma = (a->kind == MBK_I4x4 || a->kind == MBK_I8x8) ? a->i4[rast_of(x4 - 1, y4)] : 2;
-    const int mb = (b->kind == MBK_I4x4 || b->kind == MBK_I8x8) ? b->i4[rast_of(x4, y4 - 1)] : 2;
+    const int ma = (a->kind == MBK_I4x4 || a->kind == MBK_I8x8) ? a->i4[CabacView::rast_of(x4 - 1, y4)] : 2;
+    const int mb = (b->kind == MBK_I4x4 || b->kind == MBK_I8x8) ? b->i4[CabacView::rast_of(x4, y4 - 1)] : 2;
     return ma < mb ? ma : mb;
   }
   MIVC_HD void put_intra_mode(int mode, int pred) {
@@ -617,23 +821,23 @@ struct CabacMbWriter {
   // ---------------------------------------------------------------- residual_block_cabac
   // c: n coefficients in scan order (levelListIdx order); cat 0..5; cbf_inc < 0: no flag;
   // nonzero = false: the block is known to be all zero (only coded_block_flag = 0)
-  MIVC_HD int put_block(const int16_t* c, int n, int cat, int cbf_inc, bool nonzero = true) {
+  MIVC_HD void put_block(const int16_t* c, int n, int cat, int cbf_inc, bool nonzero) {
     if (!nonzero) {
       if (cbf_inc >= 0) e.decision(CTX_CBF + kCbfCatOffset[cat] + cbf_inc, 0);
-      return 0;
+      return;
     }
+    int vals[64];
     int last = -1;
-    for (int i = n - 1; i >= 0; --i)
-      if (c[i]) {
-        last = i;
-        break;
-      }
+    for (int i = 0; i < n; ++i) {
+      vals[i] = c[i];
+      if (vals[i]) last = i;
+    }
     if (cbf_inc >= 0) {
       e.decision(CTX_CBF + kCbfCatOffset[cat] + cbf_inc, last >= 0);
-      if (last < 0) return 0;
+      if (last < 0) return;
     }
     for (int i = 0; i < n - 1; ++i) {
-      const int sig = c[i] != 0;
+      const int sig = vals[i] != 0;
       int sctx, lctx;
       if (cat == 5) {
         sctx = CTX_SIG8x8 + kSig8x8Frame[i];
@@ -653,9 +857,9 @@ struct CabacMbWriter {
     const int gmax = cat == 3 ? 3 : 4;
     int ngt1 = 0, neq1 = 0;
     for (int i = last; i >= 0; --i) {
-      const int v = c[i];
-      if (!v) continue;
-      const int a1 = (v < 0 ? -v : v) - 1;
+      const int val = vals[i];
+      if (!val) continue;
+      const int a1 = (val < 0 ? -val : val) - 1;
       e.decision(abase + (ngt1 ? 0 : (neq1 + 1 < 4 ? neq1 + 1 : 4)), a1 > 0);
       if (a1 > 0) {
         const int ctx1 = abase + 5 + (ngt1 < gmax ? ngt1 : gmax);
@@ -667,9 +871,8 @@ struct CabacMbWriter {
       } else {
         ++neq1;
       }
-      e.bypass(v < 0);
+      e.bypass(val < 0);
     }
-    return 1;
   }
 
   // coded_block_flag ctxIdxInc of a luma 4x4 block at raster (x4, y4) of the current MB
@@ -678,7 +881,7 @@ struct CabacMbWriter {
       const CabacNb* m = nb_mb(xn, yn);
       if (!m) return intra ? 1 : 0;
       if (m->kind == MBK_IPCM) return 1;
-      return (m->cbf_luma >> rast_of(xn, yn)) & 1;
+      return (m->cbf_luma >> CabacView::rast_of(xn, yn)) & 1;
     };
     return cond(x4 - 1, y4) + 2 * cond(x4, y4 - 1);
   }
@@ -696,180 +899,16 @@ struct CabacMbWriter {
       if (m->kind == MBK_IPCM) return 1;
       return (m->cbf_cac[comp] >> blk) & 1;
     };
-    const int a = cx > 0 ? cond(&cur, cy * 2) : cond(A(), cy * 2 + 1);
-    const int b = cy > 0 ? cond(&cur, cx) : cond(B(), 2 + cx);
+    const int a = cx > 0 ? cond(cur, cy * 2) : cond(A(), cy * 2 + 1);
+    const int b = cy > 0 ? cond(cur, cx) : cond(B(), 2 + cx);
     return a + 2 * b;
   }
 
-  // ---------------------------------------------------------------- one macroblock
-  // h / c: the record; skip_ok: the encoder's motion equals the skip / direct motion
-  // (P: derived here; B: the caller's direct derivation).  b_code: B mb_type value.
-  MIVC_HD void code_mb(int mbx, int mby, const MbHeader& h, const int16_t* c, int b_code = 0, const int8_t* b_sub = nullptr,
-                       const uint32_t* mask_in = nullptr) {
-    mx = mbx;
-    my = mby;
-    const bool pslice = si.slice_type == SLICE_P, bslice = si.slice_type == SLICE_B;
-    int kind = h.kind;
-    mbmask = mask_in ? *mask_in : cabac_block_mask(h, c);
-    const int cbp = cabac_mask_cbp(h, mbmask);
-    const bool intra = mbk_is_intra(kind);
-    // ---- reset the current MB context
-    cur.avail = 1;
-    cur.skip = 0;
-    cur.cbp = static_cast<uint8_t>(cbp);
-    cur.t8x8 = 0;
-    cur.chroma_mode = 0;
-    cur.direct = 0;
-    cur.cbf_dc = 0;
-    cur.cbf_luma = 0;
-    cur.cbf_cac[0] = cur.cbf_cac[1] = 0;
-    for (int l = 0; l < 2; ++l)
-      for (int q = 0; q < 4; ++q) {
-        cur.ref[l][q] = intra ? -1 : h.ref[l][q];
-        cur.mv[l][q][0] = intra ? 0 : h.mv[l][q][0];
-        cur.mv[l][q][1] = intra ? 0 : h.mv[l][q][1];
-        cur.mvd[l][q][0] = cur.mvd[l][q][1] = 0;
-      }
-    for (int i = 0; i < 16; ++i) cur.i4[i] = 2;
-    cur.kind = static_cast<uint8_t>(kind == MBK_PSKIP ? MBK_P16x16 : kind);
-    // ---- skip
-    bool skip = false;
-    if (pslice && (kind == MBK_P16x16 || kind == MBK_PSKIP) && cbp == 0 && h.ref[0][0] == 0) {
-      int smv[2];
-      pskip_mv(smv);
-      skip = smv[0] == h.mv[0][0][0] && smv[1] == h.mv[0][0][1];
-    } else if (bslice && kind == MBK_BDIRECT && cbp == 0) {
-      skip = true;
-    }
-    if (pslice || bslice) put_mb_skip(skip ? 1 : 0);
-    if (skip) {
-      cur.skip = 1;
-      cur.kind = static_cast<uint8_t>(pslice ? MBK_PSKIP : MBK_BDIRECT);
-      cur.cbp = 0;
-      if (bslice) cur.direct = 0xF;
-      last_dqp = 0;
-      ++n_skip;
-      finish_mb();
-      return;
-    }
-    if (kind == MBK_PSKIP) kind = MBK_P16x16;
-    cur.kind = static_cast<uint8_t>(kind);
-    const bool t8 = (h.flags & MBF_T8x8) != 0 && si.t8x8_mode;
-    // ---- mb_type
-    if (pslice) put_mb_type_p(kind, h.i16_mode, cbp);
-    else if (bslice) put_mb_type_b(kind, h.i16_mode, cbp, intra ? 23 : (b_code ? b_code : cabac_b_code(h)));
-    else put_mb_type_i(kind, h.i16_mode, cbp, true);
-    if (intra) ++n_intra; else ++n_inter;
-    // ---- prediction
-    if (kind == MBK_I4x4 || kind == MBK_I8x8) {
-      if (si.t8x8_mode) put_t8x8(kind == MBK_I8x8);
-      cur.t8x8 = kind == MBK_I8x8;
-      if (kind == MBK_I4x4) {
-        for (int blk = 0; blk < 16; ++blk) {
-          const int x4 = kBlkX[blk], y4 = kBlkY[blk];
-          const int mode = h.i4_modes[blk];
-          put_intra_mode(mode, pred_intra_mode(x4, y4));
-          cur.i4[x4 + 4 * y4] = static_cast<uint8_t>(mode);
-        }
-      } else {
-        for (int b8 = 0; b8 < 4; ++b8) {
-          const int x4 = (b8 & 1) * 2, y4 = (b8 >> 1) * 2;
-          const int mode = h.i4_modes[b8 * 4];
-          put_intra_mode(mode, pred_intra_mode(x4, y4));
-          for (int k = 0; k < 4; ++k) cur.i4[x4 + (k & 1) + 4 * (y4 + (k >> 1))] = static_cast<uint8_t>(mode);
-        }
-      }
-    }
-    if (intra) {
-      put_chroma_mode(h.chroma_mode);
-      cur.chroma_mode = h.chroma_mode;
-    } else {
-      code_inter_pred(h, kind, b_code, b_sub);
-    }
-    // ---- coded_block_pattern, transform size
-    if (kind != MBK_I16x16) {
-      put_cbp(cbp, intra);
-      if ((cbp & 15) && si.t8x8_mode && !intra && kind != MBK_I8x8) {
-        bool ok = true;
-        if (kind == MBK_B8x8) ok = true;  // sub-blocks are 8x8 or direct (direct_8x8_inference = 1)
-        if (ok) {
-          put_t8x8(t8 ? 1 : 0);
-          cur.t8x8 = t8;
-        }
-      }
-    }
-    const bool t8_res = cur.t8x8 != 0;
-    // ---- mb_qp_delta + residual
-    if (cbp == 0 && kind != MBK_I16x16) {
-      last_dqp = 0;
-      finish_mb();
-      return;
-    }
-    int d = h.qp - last_qp;
-    if (d < -26) d += 52;
-    if (d > 25) d -= 52;
-    put_qp_delta(d);
-    last_dqp = d != 0;
-    last_qp = h.qp;
-    // luma
-    if (kind == MBK_I16x16) {
-      const int f = put_block(c + COEF_LUMA_DC, 16, 0, cbf_dc_inc(0, true), (mbmask & NZ_LUMA_DC) != 0);
-      cur.cbf_dc |= f;
-    }
-    for (int b8 = 0; b8 < 4; ++b8) {
-      if (!((cbp >> b8) & 1)) continue;
-      if (t8_res) {
-        put_block(c + COEF_LUMA + b8 * 64, 64, 5, -1);
-        const int x4 = (b8 & 1) * 2, y4 = (b8 >> 1) * 2;
-        cur.cbf_luma |= static_cast<uint16_t>(0x33u << (x4 + 4 * y4));
-        continue;
-      }
-      for (int b4 = 0; b4 < 4; ++b4) {
-        const int blk = b8 * 4 + b4;
-        const int x4 = kBlkX[blk], y4 = kBlkY[blk];
-        const int inc = cbf_luma_inc(x4, y4, intra);
-        int f;
-        const bool nzb = (mbmask >> blk) & 1u;
-        if (kind == MBK_I16x16) f = put_block(c + COEF_LUMA + blk * 16 + 1, 15, 1, inc, nzb);
-        else f = put_block(c + COEF_LUMA + blk * 16, 16, 2, inc, nzb);
-        if (f) cur.cbf_luma |= static_cast<uint16_t>(1u << (x4 + 4 * y4));
-      }
-    }
-    // chroma
-    const int cc = cbp >> 4;
-    if (cc) {
-      for (int comp = 0; comp < 2; ++comp) {
-        const int f = put_block(c + COEF_CHROMA_DC + comp * 4, 4, 3, cbf_dc_inc(1 + comp, intra),
-                                ((mbmask >> (17 + comp)) & 1u) != 0);
-        cur.cbf_dc |= static_cast<uint8_t>(f << (1 + comp));
-      }
-    }
-    if (cc == 2) {
-      for (int comp = 0; comp < 2; ++comp)
-        for (int b = 0; b < 4; ++b) {
-          const int f = put_block(c + COEF_CHROMA_AC + (comp * 4 + b) * 16 + 1, 15, 4,
-                                  cbf_cac_inc(comp, b & 1, b >> 1, intra), ((mbmask >> (19 + comp * 4 + b)) & 1u) != 0);
-          cur.cbf_cac[comp] |= static_cast<uint8_t>(f << b);
-        }
-    }
-    finish_mb();
-  }
-
-  MIVC_HD void code_inter_pred(const MbHeader& h, int kind, int b_code, const int8_t* b_sub) {
+  MIVC_HD void put_inter_pred(const MbHeader& h, int kind) {
     const bool bslice = si.slice_type == SLICE_B;
-    // partitions (quadrant masks): 16x16: {0xF}; 16x8: {0x3, 0xC}; 8x16: {0x5, 0xA}; 8x8: 4
-    int np, qfirst[4], w4[4], shape;
-    if (kind == MBK_P16x16 || kind == MBK_B16x16) { np = 1; qfirst[0] = 0; w4[0] = 4; shape = 0; }
-    else if (kind == MBK_P16x8 || kind == MBK_B16x8) { np = 2; qfirst[0] = 0; qfirst[1] = 2; w4[0] = w4[1] = 4; shape = 1; }
-    else if (kind == MBK_P8x16 || kind == MBK_B8x16) { np = 2; qfirst[0] = 0; qfirst[1] = 1; w4[0] = w4[1] = 2; shape = 2; }
-    else { np = 4; for (int q = 0; q < 4; ++q) { qfirst[q] = q; w4[q] = 2; } shape = 0; }
-    const bool sub8 = np == 4;
-    const int dir_mask = kind == MBK_B8x8 ? (h.sub_direct & 15) : 0;
-    auto pmask = [&](int p) -> int {
-      if (!sub8) return shape == 0 ? 0xF : (shape == 1 ? (p ? 0xC : 0x3) : (p ? 0xA : 0x5));
-      return 1 << p;
-    };
-    (void)b_code;
+    const CabacParts P = cabac_parts(kind);
+    const bool sub8 = P.np == 4;
+    const int dir_mask = cur->direct;
     if (sub8) {
       if (bslice) {
         for (int s = 0; s < 4; ++s) {
@@ -878,77 +917,166 @@ struct CabacMbWriter {
             const bool l0 = h.ref[0][s] >= 0, l1 = h.ref[1][s] >= 0;
             code = (l0 && l1) ? 3 : (l1 ? 2 : 1);
           }
-          put_sub_mb_type_b(b_sub ? b_sub[s] : code);
+          put_sub_mb_type_b(code);
         }
-        cur.direct = static_cast<uint8_t>(dir_mask);
       } else {
         for (int s = 0; s < 4; ++s) e.decision(CTX_SUB_MB_P, 1);  // P_L0_8x8
       }
     }
-    // ref_idx, all partitions of list 0 then list 1
     for (int l = 0; l < 2; ++l) {
       if (si.num_ref[l] <= 1) continue;
-      for (int p = 0; p < np; ++p) {
-        const int q = qfirst[p];
-        if (sub8 && ((dir_mask >> q) & 1)) continue;
-        if (h.ref[l][q] < 0) continue;
+      for (int p = 0; p < P.np; ++p) {
+        const int q = P.qfirst[p];
+        if (((dir_mask >> q) & 1) || h.ref[l][q] < 0) continue;
         put_ref_idx(l, q, h.ref[l][q]);
       }
     }
-    // mvd, list 0 then list 1; the MVs of earlier partitions are visible to later ones
-    int done = 0;
-    for (int l = 0; l < 2; ++l) {
-      done = 0;
-      for (int p = 0; p < np; ++p) {
-        const int q = qfirst[p];
-        const int m = pmask(p);
-        if (sub8 && ((dir_mask >> q) & 1)) {
-          done |= m;
-          continue;
+    for (int l = 0; l < 2; ++l)
+      for (int p = 0; p < P.np; ++p) {
+        const int q = P.qfirst[p];
+        if (((dir_mask >> q) & 1) || h.ref[l][q] < 0) continue;
+        put_mvd(l, q, 0, cur->mvd[l][q][0]);
+        put_mvd(l, q, 1, cur->mvd[l][q][1]);
+      }
+  }
+
+  // ---------------------------------------------------------------- one macroblock
+  MIVC_HD void code_mb(int addr, const MbHeader& h, const int16_t* c, bool last_in_slice) {
+    v.at(addr, si.wmb, si.first_mb);
+    cur = &nb[addr];
+    const bool pslice = si.slice_type == SLICE_P, bslice = si.slice_type == SLICE_B;
+    if (pslice || bslice) put_mb_skip(cur->skip);
+    if (!cur->skip) code_mb_layer(h, c);
+    e.terminate(last_in_slice ? 1 : 0);
+  }
+
+  MIVC_HD void code_mb_layer(const MbHeader& h, const int16_t* c) {
+    const bool pslice = si.slice_type == SLICE_P, bslice = si.slice_type == SLICE_B;
+    const int kind = cur->kind;
+    const int cbp = cur->cbp;
+    const uint32_t mask = cur->mask;
+    const bool intra = mbk_is_intra(kind);
+    // ---- mb_type
+    if (pslice) put_mb_type_p(kind, h.i16_mode, cbp);
+    else if (bslice) put_mb_type_b(kind, h.i16_mode, cbp, intra ? 23 : cur->b_code);
+    else put_mb_type_i(kind, h.i16_mode, cbp, true);
+    // ---- prediction
+    if (kind == MBK_I4x4 || kind == MBK_I8x8) {
+      if (si.t8x8_mode) put_t8x8(kind == MBK_I8x8);
+      if (kind == MBK_I4x4) {
+        for (int blk = 0; blk < 16; ++blk) {
+          const int x4 = kBlkX[blk], y4 = kBlkY[blk];
+          put_intra_mode(h.i4_modes[blk], pred_intra_mode(x4, y4));
         }
-        if (h.ref[l][q] < 0) {
-          done |= m;
-          continue;
-        }
-        int pm[2];
-        mvp(l, h.ref[l][q], (q & 1) * 2, (q >> 1) * 2, w4[p], shape, p, done, pm);
-        const int dx = h.mv[l][q][0] - pm[0], dy = h.mv[l][q][1] - pm[1];
-        put_mvd(l, q, 0, dx);
-        put_mvd(l, q, 1, dy);
-        const int ax = dx < 0 ? -dx : dx, ay = dy < 0 ? -dy : dy;
-        for (int k = 0; k < 4; ++k)
-          if ((m >> k) & 1) {
-            cur.mvd[l][k][0] = static_cast<uint8_t>(ax > 255 ? 255 : ax);
-            cur.mvd[l][k][1] = static_cast<uint8_t>(ay > 255 ? 255 : ay);
-          }
-        done |= m;
+      } else {
+        for (int b8 = 0; b8 < 4; ++b8) put_intra_mode(h.i4_modes[b8 * 4], pred_intra_mode((b8 & 1) * 2, (b8 >> 1) * 2));
       }
     }
+    if (intra) put_chroma_mode(h.chroma_mode);
+    else put_inter_pred(h, kind);
+    // ---- coded_block_pattern, transform size
+    if (kind != MBK_I16x16) {
+      put_cbp(cbp);
+      if ((cbp & 15) && si.t8x8_mode && !intra) put_t8x8(cur->t8x8);
+    }
+    if (cbp == 0 && kind != MBK_I16x16) return;
+    put_qp_delta(cur->dqp, cur->prev_dqp_nz);
+    // ---- residual: luma
+    if (kind == MBK_I16x16) put_block(c + COEF_LUMA_DC, 16, 0, cbf_dc_inc(0, true), (mask & NZ_LUMA_DC) != 0);
+    for (int b8 = 0; b8 < 4; ++b8) {
+      if (!((cbp >> b8) & 1)) continue;
+      if (cur->t8x8) {
+        put_block(c + COEF_LUMA + b8 * 64, 64, 5, -1, true);
+        continue;
+      }
+      for (int b4 = 0; b4 < 4; ++b4) {
+        const int blk = b8 * 4 + b4;
+        const int inc = cbf_luma_inc(kBlkX[blk], kBlkY[blk], intra);
+        const bool nzb = (mask >> blk) & 1u;
+        if (kind == MBK_I16x16) put_block(c + COEF_LUMA + blk * 16 + 1, 15, 1, inc, nzb);
+        else put_block(c + COEF_LUMA + blk * 16, 16, 2, inc, nzb);
+      }
+    }
+    // ---- chroma
+    const int cc = cbp >> 4;
+    if (cc)
+      for (int comp = 0; comp < 2; ++comp)
+        put_block(c + COEF_CHROMA_DC + comp * 4, 4, 3, cbf_dc_inc(1 + comp, intra), ((mask >> (17 + comp)) & 1u) != 0);
+    if (cc == 2)
+      for (int comp = 0; comp < 2; ++comp)
+        for (int b = 0; b < 4; ++b)
+          put_block(c + COEF_CHROMA_AC + (comp * 4 + b) * 16 + 1, 15, 4, cbf_cac_inc(comp, b & 1, b >> 1, intra),
+                    ((mask >> (19 + comp * 4 + b)) & 1u) != 0);
   }
-
-  MIVC_HD void finish_mb() { row[mx] = cur; }
 };
 
-// Code MB records [first_mb, first_mb + n) of one picture as slice data; returns the
-// number of bytes written (slice_data only: the caller writes the slice header, which
-// ends byte-aligned with cabac_alignment_one_bits, and the NAL framing).
-// b_codes / b_subs: optional per-MB B mb_type value and sub_mb_types (B slices).
-MIVC_HD size_t cabac_write_slice_data(CabacMbWriter& w, const CabacSliceInfo& si, CabacNb* rowbuf, uint8_t* states,
-                                      CabacBuf* out, const MbHeader* hdr, const int16_t* coef, int n,
-                                      const uint8_t* b_codes = nullptr, const int8_t* b_subs = nullptr,
-                                      const uint32_t* masks = nullptr, bool states_ready = false,
-                                      bool row_ready = false) {
-  w.begin(si, rowbuf, states, out, states_ready, row_ready);
+// One recorded symbol through the arithmetic coder (what the GPU's serial stage does).
+MIVC_HD void cabac_code_symbol(CabacEncoder& e, uint16_t s) {
+  if (!(s & 0x8000u)) e.decision(s & 0x1FF, (s >> 9) & 1);
+  else if (!(s & 0x4000u)) e.bypass_bits(s & 0x3FFu, (s >> 10) & 15);
+  else e.terminate(s & 1);
+}
+
+// ---------------------------------------------------------------- serial slice writer (host)
+struct CabacSliceStats {
+  int skipped = 0, intra = 0, inter = 0;
+};
+
+// Code MB records [first_mb, first_mb + n) of one picture as slice data into `out`
+// (the caller writes the byte-aligned slice header and the NAL framing).  nb: scratch
+// of width_mbs * height_mbs entries; masks: optional precomputed block masks.
+MIVC_HD size_t cabac_write_slice_data(const CabacSliceInfo& si, CabacNb* nb, uint8_t* states, CabacBuf* out,
+                                      const MbHeader* hdr, const int16_t* coef, int n, CabacEncoder* enc_out = nullptr,
+                                      CabacSliceStats* st = nullptr) {
   const int end = si.first_mb + n;
-  for (int addr = si.first_mb; addr < end; ++addr) {
-    const int mx = addr % si.wmb, my = addr / si.wmb;
-    if (mx == 0) w.tl.avail = 0;
-    CabacNb top_old = rowbuf[mx];
-    w.code_mb(mx, my, hdr[addr], coef + static_cast<size_t>(addr) * kCoefPerMb, b_codes ? b_codes[addr] : 0,
-              b_subs ? b_subs + static_cast<size_t>(addr) * 4 : nullptr, masks ? masks + addr : nullptr);
-    w.tl = top_old;  // MB (mx, my-1) is the top-left of MB (mx+1, my)
-    w.e.terminate(addr == end - 1 ? 1 : 0);
+  for (int a = si.first_mb; a < end; ++a)
+    cabac_prepare_mb(si, hdr, a, cabac_block_mask(hdr[a], coef + static_cast<size_t>(a) * kCoefPerMb), nb[a]);
+  cabac_qp_chain(si, nb, n);
+  CabacEncoder e;
+  cabac_init_contexts(states, si.slice_type == SLICE_I ? 0 : 1 /* cabac_init_idc 0 */, si.slice_qp);
+  e.init(states, out);
+  CabacMbCoder<CabacEncoder> coder(e, si, nb);
+  for (int a = si.first_mb; a < end; ++a) {
+    coder.code_mb(a, hdr[a], coef + static_cast<size_t>(a) * kCoefPerMb, a == end - 1);
+    if (st) {
+      if (nb[a].skip) ++st->skipped;
+      else if (mbk_is_intra(nb[a].kind)) ++st->intra;
+      else ++st->inter;
+    }
   }
+  if (enc_out) *enc_out = e;
+  return out->n;
+}
+
+// The same slice data through the GPU decomposition: every MB binarised on its own into
+// symbols (any order), then the symbols arithmetic-coded in MB order.  Must produce the
+// bytes of cabac_write_slice_data (a CPU test pins it).  syms: scratch >= total symbols.
+inline size_t cabac_write_slice_data_symbols(const CabacSliceInfo& si, CabacNb* nb, uint8_t* states, CabacBuf* out,
+                                             const MbHeader* hdr, const int16_t* coef, int n, uint16_t* syms,
+                                             size_t cap_syms, int* nsyms_out) {
+  const int end = si.first_mb + n;
+  for (int a = end - 1; a >= si.first_mb; --a)  // reverse order: nothing depends on coding order
+    cabac_prepare_mb(si, hdr, a, cabac_block_mask(hdr[a], coef + static_cast<size_t>(a) * kCoefPerMb), nb[a]);
+  cabac_qp_chain(si, nb, n);
+  size_t total = 0;
+  for (int a = si.first_mb; a < end; ++a) {
+    CabacSymbolPacker<CabacCountEmit> cnt;
+    CabacMbCoder<CabacSymbolPacker<CabacCountEmit>> c1(cnt, si, nb);
+    c1.code_mb(a, hdr[a], coef + static_cast<size_t>(a) * kCoefPerMb, a == end - 1);
+    cnt.flush_bypass();
+    if (total + cnt.out.n > cap_syms) return 0;
+    CabacSymbolPacker<CabacStoreEmit> st;
+    st.out.p = syms + total;
+    CabacMbCoder<CabacSymbolPacker<CabacStoreEmit>> c2(st, si, nb);
+    c2.code_mb(a, hdr[a], coef + static_cast<size_t>(a) * kCoefPerMb, a == end - 1);
+    st.flush_bypass();
+    total += st.out.n;
+  }
+  if (nsyms_out) *nsyms_out = static_cast<int>(total);
+  CabacEncoder e;
+  cabac_init_contexts(states, si.slice_type == SLICE_I ? 0 : 1, si.slice_qp);
+  e.init(states, out);
+  for (size_t i = 0; i < total; ++i) cabac_code_symbol(e, syms[i]);
   return out->n;
 }
 

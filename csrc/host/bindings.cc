@@ -356,6 +356,24 @@ PYBIND11_MODULE(_host, m) {
       },
       py::arg("cfg"), py::arg("frame"), py::arg("hdr"), py::arg("coef"));
 
+  // CABAC slice data two ways: the serial writer and the GPU's symbol decomposition
+  m.def("cabac_slice_data_two_ways", [](const py::dict& cfg, const py::dict& fp, py::array_t<uint8_t, py::array::c_style> hdr,
+                                         py::array_t<int16_t, py::array::c_style> coef) {
+    EncoderConfig c = cfg_from(cfg);
+    c.cabac = 1;
+    SPS sps = make_sps(c);
+    PPS pps = make_pps(c);
+    int nmb = sps.width_mbs * sps.height_mbs;
+    if (hdr.size() != static_cast<py::ssize_t>(nmb * sizeof(MbHeader))) throw std::runtime_error("header array has wrong size");
+    if (coef.size() != static_cast<py::ssize_t>(nmb) * kCoefPerMb) throw std::runtime_error("coef array has wrong size");
+    SliceHeader sh = slice_header_from(c, sps, pps, fp);
+    const MbHeader* mh = reinterpret_cast<const MbHeader*>(hdr.data());
+    std::vector<uint8_t> a = cabac_slice_data(sps, pps, sh, mh, coef.data(), nmb);
+    int nsyms = 0;
+    std::vector<uint8_t> b = cabac_slice_data_symbols(sps, pps, sh, mh, coef.data(), nmb, &nsyms);
+    return py::make_tuple(to_bytes(a), to_bytes(b), nsyms);
+  });
+
   m.def(
       "decode",
       [](py::bytes data, bool skip_deblock) {

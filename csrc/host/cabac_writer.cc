@@ -30,26 +30,50 @@ std::vector<uint8_t> cabac_slice_data(const SPS& sps, const PPS& pps, const Slic
   si.num_ref[1] = sh.num_ref_idx_l1_active;
   si.t8x8_mode = pps.transform_8x8_mode;
   si.slice_qp = pps.pic_init_qp + sh.slice_qp_delta;
-  std::vector<CabacNb> row(static_cast<size_t>(sps.width_mbs));
+  std::vector<CabacNb> nb(static_cast<size_t>(nmb));
   std::vector<uint8_t> out(static_cast<size_t>(num_mbs) * 160 + 4096);
   uint8_t states[kCabacContexts];
   for (int attempt = 0; attempt < 2; ++attempt) {
     CabacBuf buf{out.data(), out.size(), 0, 0};
-    CabacMbWriter w;
-    cabac_write_slice_data(w, si, row.data(), states, &buf, mbs, coef, num_mbs);
-    if (w.e.bad) throw std::runtime_error("CABAC carry past the start of the slice");
+    CabacEncoder e;
+    CabacSliceStats st{};
+    cabac_write_slice_data(si, nb.data(), states, &buf, mbs, coef, num_mbs, &e, &st);
+    if (e.bad) throw std::runtime_error("CABAC carry past the start of the slice");
     if (!buf.overflow) {
       out.resize(buf.n);
       if (stats) {
-        stats->skipped = w.n_skip;
-        stats->intra = w.n_intra;
-        stats->coded_inter = w.n_inter;
+        stats->skipped = st.skipped;
+        stats->intra = st.intra;
+        stats->coded_inter = st.inter;
       }
       return out;
     }
     out.assign(buf.n + 64, 0);
   }
   throw std::runtime_error("CABAC output buffer overflow");
+}
+
+std::vector<uint8_t> cabac_slice_data_symbols(const SPS& sps, const PPS& pps, const SliceHeader& sh, const MbHeader* mbs,
+                                              const int16_t* coef, int num_mbs, int* nsyms) {
+  const int nmb = sps.width_mbs * sps.height_mbs;
+  CabacSliceInfo si{};
+  si.slice_type = sh.slice_type;
+  si.wmb = sps.width_mbs;
+  si.hmb = sps.height_mbs;
+  si.first_mb = sh.first_mb;
+  si.num_ref[0] = sh.num_ref_idx_l0_active;
+  si.num_ref[1] = sh.num_ref_idx_l1_active;
+  si.t8x8_mode = pps.transform_8x8_mode;
+  si.slice_qp = pps.pic_init_qp + sh.slice_qp_delta;
+  std::vector<CabacNb> nb(static_cast<size_t>(nmb));
+  std::vector<uint16_t> syms(static_cast<size_t>(num_mbs) * 20000 + 1024);
+  std::vector<uint8_t> out(static_cast<size_t>(num_mbs) * 4000 + 4096);
+  uint8_t states[kCabacContexts];
+  CabacBuf buf{out.data(), out.size(), 0, 0};
+  cabac_write_slice_data_symbols(si, nb.data(), states, &buf, mbs, coef, num_mbs, syms.data(), syms.size(), nsyms);
+  if (buf.overflow) throw std::runtime_error("CABAC symbol path overflow");
+  out.resize(buf.n);
+  return out;
 }
 
 std::vector<uint8_t> write_slice_nal_cabac(const SPS& sps, const PPS& pps, const SliceHeader& sh, const MbHeader* mbs,

@@ -22,5 +22,10 @@ std::vector<uint8_t> write_slice_nal_cabac(const SPS& sps, const PPS& pps, const
 std::vector<uint8_t> cabac_slice_data(const SPS& sps, const PPS& pps, const SliceHeader& sh, const MbHeader* mbs,
                                       const int16_t* coef, int num_mbs, SliceStats* stats = nullptr);
 
+// Slice data through the symbol path (per-MB binarisation, then arithmetic coding): the
+// decomposition the GPU uses.  Returns the bytes and the symbol count.
+std::vector<uint8_t> cabac_slice_data_symbols(const SPS& sps, const PPS& pps, const SliceHeader& sh, const MbHeader* mbs,
+                                              const int16_t* coef, int num_mbs, int* nsyms);
+
 }  // namespace h264
 }  // namespace mivc

@@ -60,10 +60,12 @@ void mivc_launch_hevc_sao(int B, int W, int H, int bd, const uint16_t* dy, const
                           uint16_t* y, uint16_t* u, uint16_t* v, const uint16_t* sy, const uint16_t* su,
                           const uint16_t* sv, void* ctu, const int* qp, const int8_t* run, int enable, void* stream);
 size_t mivc_cavlc_mb_bytes();
-void mivc_launch_cabac(int B, int wmb, int hmb, const void* hdr, const int16_t* coef, uint32_t* mask,
-                       uint8_t* slot_out, long long cap, int* slot_bytes, const uint32_t* hdr_bits,
-                       const int* hdr_nbits, const int* slot_qp, int slice_type, int num_ref_l0, int num_ref_l1,
-                       int t8x8_mode, uint8_t* out, long long* out_off, int* err, void* stream);
+size_t mivc_cabac_nb_bytes();
+void mivc_launch_cabac(int B, int wmb, int hmb, const void* hdr, const int16_t* coef, uint32_t* mask, void* nb,
+                       int* cnt, long long* off, int* total, uint16_t* syms, long long cap_syms, uint8_t* slot_out,
+                       long long cap, int* slot_bytes, const uint32_t* hdr_bits, const int* hdr_nbits,
+                       const int* slot_qp, int slice_type, int num_ref_l0, int num_ref_l1, int t8x8_mode,
+                       uint8_t* out, long long* out_off, int* err, void* stream);
 void mivc_launch_cavlc(int B, int wmb, int hmb, const void* hdr, const int16_t* coef, void* mbs, int* len,
                        long long* off, int* trail, long long* total_bits, int* slot_bytes, uint32_t* words,
                        long long cap_words, const uint32_t* hdr_bits, const int* hdr_nbits, int pslice, int slice_qp,
@@ -214,12 +216,16 @@ PYBIND11_MODULE(_hip, m) {
                          P<int8_t>(run), enable, S(stream));
   });
   m.def("cavlc_mb_bytes", []() { return mivc_cavlc_mb_bytes(); });
-  m.def("cabac", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t coef, uintptr_t mask, uintptr_t slot_out,
+  m.def("cabac_nb_bytes", []() { return mivc_cabac_nb_bytes(); });
+  m.def("cabac", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t coef, uintptr_t mask, uintptr_t nb, uintptr_t cnt,
+                    uintptr_t off, uintptr_t total, uintptr_t syms, long long cap_syms, uintptr_t slot_out,
                     long long cap, uintptr_t slot_bytes, uintptr_t hdr_bits, uintptr_t hdr_nbits, uintptr_t slot_qp,
                     int slice_type, int num_ref_l0, int num_ref_l1, int t8x8_mode, uintptr_t out, uintptr_t out_off,
                     uintptr_t err, uintptr_t stream) {
-    if (wmb > 512) throw std::runtime_error("cabac: picture wider than 8192 samples");
-    mivc_launch_cabac(B, wmb, hmb, P<void>(hdr), P<int16_t>(coef), P<uint32_t>(mask), P<uint8_t>(slot_out), cap,
+    if (cap_syms % 8 != 0) throw std::invalid_argument("cabac: cap_syms must be a multiple of 8");
+    if ((syms & 15) != 0) throw std::invalid_argument("cabac: symbol buffer must be 16-byte aligned");
+    mivc_launch_cabac(B, wmb, hmb, P<void>(hdr), P<int16_t>(coef), P<uint32_t>(mask), P<void>(nb), P<int>(cnt),
+                      P<long long>(off), P<int>(total), P<uint16_t>(syms), cap_syms, P<uint8_t>(slot_out), cap,
                       P<int>(slot_bytes), P<uint32_t>(hdr_bits), P<int>(hdr_nbits), P<int>(slot_qp), slice_type,
                       num_ref_l0, num_ref_l1, t8x8_mode, P<uint8_t>(out), P<long long>(out_off), P<int>(err),
                       S(stream));

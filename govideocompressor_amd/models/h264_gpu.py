@@ -193,11 +193,18 @@ class GpuH264Encoder:
             self.out_done = [torch.cuda.Event() for _ in range(2)]
             self.copy_pool = cf.ThreadPoolExecutor(max_workers=1)
             if params.cabac:
-                # per-slot slice RBSP scratch (worst case ~3 kbit per MB, as for CAVLC) and the
-                # per-MB non-zero block masks of the serial coder
+                # per-slot slice RBSP scratch (worst case ~3 kbit per MB, as for CAVLC), the
+                # per-MB coding state of the parallel binariser and the 16-bit symbol buffer of
+                # the serial arithmetic coder (all used on the copy stream only)
                 self.cab_cap = nmb * 384 + 4096
+                self.cab_cap_syms = nmb * 512 + 64
                 self.cab_slot = torch.empty((B * self.cab_cap,), dtype=u8, device=dev)
                 self.cab_mask = torch.zeros((B, nmb), dtype=torch.int32, device=dev)
+                self.cab_nb = torch.zeros((B, nmb, int(self.hip.cabac_nb_bytes())), dtype=u8, device=dev)
+                self.cab_cnt = torch.zeros((B, nmb), dtype=i32, device=dev)
+                self.cab_off = torch.zeros((B, nmb), dtype=i64, device=dev)
+                self.cab_total = torch.zeros((B,), dtype=i32, device=dev)
+                self.cab_syms = torch.empty((B * self.cab_cap_syms,), dtype=torch.int16, device=dev)
                 self.cav_out = [torch.zeros((B * self.cab_cap,), dtype=u8, device=dev) for _ in range(2)]
         self.copy_stream = torch.cuda.Stream(device=dev)
         self.copy_done = [torch.cuda.Event() for _ in range(2)]
@@ -285,8 +292,9 @@ class GpuH264Encoder:
         qp_dev: [B] int32 slice QPs of this step in a buffer that outlives the launch."""
         self._header_bits(k, t, qps_t, idr, idr_ids)
         P = self._ptr
-        self.hip.cabac(self.B, self.wmb, self.hmb, P(self.hdr[k]), P(self.coef[k]), P(self.cab_mask), P(self.cab_slot),
-                       self.cab_cap, P(self.cav_sizes[k]), P(self.cav_hdr_bits[k]), P(self.cav_hdr_nbits[k]),
+        self.hip.cabac(self.B, self.wmb, self.hmb, P(self.hdr[k]), P(self.coef[k]), P(self.cab_mask), P(self.cab_nb),
+                       P(self.cab_cnt), P(self.cab_off), P(self.cab_total), P(self.cab_syms), self.cab_cap_syms,
+                       P(self.cab_slot), self.cab_cap, P(self.cav_sizes[k]), P(self.cav_hdr_bits[k]), P(self.cav_hdr_nbits[k]),
                        P(qp_dev), 2 if idr else 0, 1, 1, 0, P(self.cav_out[k]), P(self.cav_out_off), P(self.err),
                        self.copy_stream.cuda_stream)
 

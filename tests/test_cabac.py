@@ -130,3 +130,18 @@ def test_cabac_large_levels_and_mvds(host):
     want_mv = np.frombuffer(hdr2[:, 16:20].tobytes(), np.int16).reshape(nmb, 2)
     assert np.array_equal(got_mv, want_mv)
     assert len(host.decode(s)) == 2
+
+
+@pytest.mark.parametrize("t8,seed", [(False, 21), (True, 22)])
+def test_cabac_symbol_decomposition_is_exact(host, t8, seed):
+    """The GPU's decomposition (each MB binarised on its own into 16-bit symbols, any order;
+    then the symbols arithmetic-coded in MB order, bypass bins batched) yields exactly the
+    serial writer's bytes."""
+    w, h = 96, 80
+    recs = []
+    random_stream(host, w, h, 4, seed=seed, cabac=True, t8x8=t8, records=recs)
+    cfg = dict(width=w, height=h, qp=28, cabac=1, t8x8=int(t8))
+    for t, (hdr, coef) in enumerate(recs):
+        fp = dict(idr=int(t == 0), qp=27 + t, frame_num=t)
+        a, b, nsyms = host.cabac_slice_data_two_ways(cfg, fp, hdr, coef)
+        assert a == b and nsyms > 0
