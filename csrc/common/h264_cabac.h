@@ -1010,12 +1010,123 @@ struct CabacMbCoder {
   }
 };
 
-// One recorded symbol through the arithmetic coder (what the GPU's serial stage does).
+// One recorded symbol through the arithmetic coder.
 MIVC_HD void cabac_code_symbol(CabacEncoder& e, uint16_t s) {
   if (!(s & 0x8000u)) e.decision(s & 0x1FF, (s >> 9) & 1);
   else if (!(s & 0x4000u)) e.bypass_bits(s & 0x3FFu, (s >> 10) & 15);
   else e.terminate(s & 1);
 }
+
+// The GPU's serial stage: CabacEncoder over recorded symbols with one branch-free update
+// for the three common symbol kinds, so the 64 slices of a wave (one per lane) do not
+// serialise on divergent paths.  Decision, bypass batch and terminate(0) (= the MPS path
+// with rLPS 2 and no context) share
+//     low' = (low + add) << n + range * bypass_bits,  range' = new_range << n;
+// terminate(1), the last symbol of every slice, is finish().  Context states are read
+// at st[ctx * stride] (the GPU keeps one LDS column per lane); lps / trans are the
+// flattened Table 9-44 / transIdxLPS.  Out: put(int byte).
+template <class Out>
+struct CabacSymbolCoder {
+  uint32_t low, range;
+  int nbits, pend, nff, bad;
+  Out out;
+
+  MIVC_HD void init() {
+    low = 0;
+    range = 510;
+    nbits = -1;
+    pend = -1;
+    nff = 0;
+    bad = 0;
+  }
+  MIVC_HD void put_byte(uint32_t v) {
+    const int b = static_cast<int>(v & 0xFFu);
+    if (v >> 8) {
+      if (pend < 0) bad = 1;
+      if (nff > 0) {
+        out.put(pend + 1);
+        for (int k = 0; k < nff - 1; ++k) out.put(0);
+        pend = 0;
+        nff = 0;
+      } else {
+        pend += 1;
+      }
+    }
+    if (b == 0xFF) {
+      ++nff;
+    } else {
+      if (pend >= 0) {
+        out.put(pend);
+        for (int k = 0; k < nff; ++k) out.put(0xFF);
+      }
+      pend = b;
+      nff = 0;
+    }
+  }
+  MIVC_HD void drain() {
+    while (nbits >= 8) {
+      const int sh = nbits + 2;
+      const uint32_t v = low >> sh;
+      low &= (1u << sh) - 1u;
+      nbits -= 8;
+      put_byte(v);
+    }
+  }
+  MIVC_HD void step(uint32_t sym, uint8_t* st, int stride, const uint8_t* lps, const uint8_t* trans) {
+    const bool dec = !(sym & 0x8000u);
+    const bool byp = (sym & 0xC000u) == 0x8000u;
+    uint8_t* sp = st + (dec ? (sym & 0x1FFu) : 0u) * static_cast<uint32_t>(stride);
+    const int sv = dec ? *sp : 0;
+    int pst = sv >> 1, mps = sv & 1;
+    const uint32_t rlps = dec ? lps[pst * 4 + ((range >> 6) & 3)] : 2u;
+    const uint32_t r1 = range - rlps;
+    const bool lpsb = dec && static_cast<int>((sym >> 9) & 1u) != mps;
+    const uint32_t nr = lpsb ? rlps : r1;
+    const uint32_t add = lpsb ? r1 : 0u;
+    if (dec) {
+      if (lpsb) {
+        mps ^= pst == 0 ? 1 : 0;
+        pst = trans[pst];
+      } else {
+        pst = pst < 62 ? pst + 1 : 62;
+      }
+      *sp = static_cast<uint8_t>((pst << 1) | mps);
+    }
+    const int shd = cabac_clz32(nr) - 23;
+    const int n = byp ? static_cast<int>((sym >> 10) & 15u) : (shd > 0 ? shd : 0);
+    low = ((low + add) << n) + (byp ? range * (sym & 0x3FFu) : 0u);
+    range = byp ? range : (nr << n);
+    nbits += n;
+    if (nbits >= 8) drain();
+  }
+  // EncodeTerminate(1) + EncodeFlush + rbsp_stop_one_bit + alignment (CabacEncoder::terminate)
+  MIVC_HD void finish() {
+    range -= 2;
+    low += range;
+    range = 2;
+    low <<= 7;
+    nbits += 7;
+    drain();
+    low |= 0x80u;
+    low <<= 3;
+    nbits += 3;
+    drain();
+    if (nbits > 0) {
+      low <<= 8 - nbits;
+      nbits = 8;
+      drain();
+    }
+    if (pend >= 0) out.put(pend);
+    for (int k = 0; k < nff; ++k) out.put(0xFF);
+    pend = -1;
+    nff = 0;
+  }
+};
+
+struct CabacBufRef {
+  CabacBuf* b;
+  MIVC_HD void put(int v) { b->put(v); }
+};
 
 // ---------------------------------------------------------------- serial slice writer (host)
 struct CabacSliceStats {
@@ -1073,11 +1184,14 @@ inline size_t cabac_write_slice_data_symbols(const CabacSliceInfo& si, CabacNb* 
     total += st.out.n;
   }
   if (nsyms_out) *nsyms_out = static_cast<int>(total);
-  CabacEncoder e;
+  if (total == 0 || syms[total - 1] != 0xC001u) return 0;  // slices end in end_of_slice_flag = 1
   cabac_init_contexts(states, si.slice_type == SLICE_I ? 0 : 1, si.slice_qp);
-  e.init(states, out);
-  for (size_t i = 0; i < total; ++i) cabac_code_symbol(e, syms[i]);
-  return out->n;
+  CabacSymbolCoder<CabacBufRef> e;
+  e.out.b = out;
+  e.init();
+  for (size_t i = 0; i + 1 < total; ++i) e.step(syms[i], states, 1, &kCabacRangeLPS[0][0], kCabacTransLPS);
+  e.finish();
+  return e.bad ? 0 : out->n;
 }
 
 }  // namespace h264

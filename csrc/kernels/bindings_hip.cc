@@ -61,11 +61,15 @@ void mivc_launch_hevc_sao(int B, int W, int H, int bd, const uint16_t* dy, const
                           const uint16_t* sv, void* ctu, const int* qp, const int8_t* run, int enable, void* stream);
 size_t mivc_cavlc_mb_bytes();
 size_t mivc_cabac_nb_bytes();
-void mivc_launch_cabac(int B, int wmb, int hmb, const void* hdr, const int16_t* coef, uint32_t* mask, void* nb,
-                       int* cnt, long long* off, int* total, uint16_t* syms, long long cap_syms, uint8_t* slot_out,
-                       long long cap, int* slot_bytes, const uint32_t* hdr_bits, const int* hdr_nbits,
-                       const int* slot_qp, int slice_type, int num_ref_l0, int num_ref_l1, int t8x8_mode,
-                       uint8_t* out, long long* out_off, int* err, void* stream);
+int mivc_cabac_gap();
+void mivc_launch_cabac_bin(int B, int wmb, int hmb, const void* hdr, const int16_t* coef, uint32_t* mask, void* nb,
+                           int* cnt, long long* off, int* tot, uint16_t* pool, long long pool_cap,
+                           long long* pool_used, long long* base, int* total, const int* slot_qp, int slice_type,
+                           int num_ref_l0, int num_ref_l1, int t8x8_mode, int* err, void* stream);
+void mivc_launch_cabac_code(int L, int B, uint16_t* pool, const long long* base, const int* total,
+                            const uint32_t* hdr_bits, const int* hdr_nbits, const int* slot_qp,
+                            unsigned long long itypes, int* bytes, uint8_t* out, long long* out_off, int* err,
+                            void* stream);
 void mivc_launch_cavlc(int B, int wmb, int hmb, const void* hdr, const int16_t* coef, void* mbs, int* len,
                        long long* off, int* trail, long long* total_bits, int* slot_bytes, uint32_t* words,
                        long long cap_words, const uint32_t* hdr_bits, const int* hdr_nbits, int pslice, int slice_qp,
@@ -217,18 +221,25 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("cavlc_mb_bytes", []() { return mivc_cavlc_mb_bytes(); });
   m.def("cabac_nb_bytes", []() { return mivc_cabac_nb_bytes(); });
-  m.def("cabac", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t coef, uintptr_t mask, uintptr_t nb, uintptr_t cnt,
-                    uintptr_t off, uintptr_t total, uintptr_t syms, long long cap_syms, uintptr_t slot_out,
-                    long long cap, uintptr_t slot_bytes, uintptr_t hdr_bits, uintptr_t hdr_nbits, uintptr_t slot_qp,
-                    int slice_type, int num_ref_l0, int num_ref_l1, int t8x8_mode, uintptr_t out, uintptr_t out_off,
-                    uintptr_t err, uintptr_t stream) {
-    if (cap_syms % 8 != 0) throw std::invalid_argument("cabac: cap_syms must be a multiple of 8");
-    if ((syms & 15) != 0) throw std::invalid_argument("cabac: symbol buffer must be 16-byte aligned");
-    mivc_launch_cabac(B, wmb, hmb, P<void>(hdr), P<int16_t>(coef), P<uint32_t>(mask), P<void>(nb), P<int>(cnt),
-                      P<long long>(off), P<int>(total), P<uint16_t>(syms), cap_syms, P<uint8_t>(slot_out), cap,
-                      P<int>(slot_bytes), P<uint32_t>(hdr_bits), P<int>(hdr_nbits), P<int>(slot_qp), slice_type,
-                      num_ref_l0, num_ref_l1, t8x8_mode, P<uint8_t>(out), P<long long>(out_off), P<int>(err),
-                      S(stream));
+  m.def("cabac_gap", []() { return mivc_cabac_gap(); });
+  m.def("cabac_bin", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t coef, uintptr_t mask, uintptr_t nb,
+                        uintptr_t cnt, uintptr_t off, uintptr_t tot, uintptr_t pool, long long pool_cap,
+                        uintptr_t pool_used, uintptr_t base, uintptr_t total, uintptr_t slot_qp, int slice_type,
+                        int num_ref_l0, int num_ref_l1, int t8x8_mode, uintptr_t err, uintptr_t stream) {
+    if ((pool & 15) != 0) throw std::invalid_argument("cabac_bin: symbol pool must be 16-byte aligned");
+    if (B < 1 || wmb < 1 || hmb < 1) throw std::invalid_argument("cabac_bin: bad geometry");
+    mivc_launch_cabac_bin(B, wmb, hmb, P<void>(hdr), P<int16_t>(coef), P<uint32_t>(mask), P<void>(nb), P<int>(cnt),
+                          P<long long>(off), P<int>(tot), P<uint16_t>(pool), pool_cap, P<long long>(pool_used),
+                          P<long long>(base), P<int>(total), P<int>(slot_qp), slice_type, num_ref_l0, num_ref_l1,
+                          t8x8_mode, P<int>(err), S(stream));
+  });
+  m.def("cabac_code", [](int L, int B, uintptr_t pool, uintptr_t base, uintptr_t total, uintptr_t hdr_bits,
+                         uintptr_t hdr_nbits, uintptr_t slot_qp, unsigned long long itypes, uintptr_t bytes,
+                         uintptr_t out, uintptr_t out_off, uintptr_t err, uintptr_t stream) {
+    if (B < 1 || L < 1 || L % B != 0 || L / B > 64) throw std::invalid_argument("cabac_code: L must be G * B, G <= 64");
+    mivc_launch_cabac_code(L, B, P<uint16_t>(pool), P<long long>(base), P<int>(total), P<uint32_t>(hdr_bits),
+                           P<int>(hdr_nbits), P<int>(slot_qp), itypes, P<int>(bytes), P<uint8_t>(out),
+                           P<long long>(out_off), P<int>(err), S(stream));
   });
   m.def("cavlc", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t coef, uintptr_t mbs, uintptr_t len, uintptr_t off,
                     uintptr_t trail, uintptr_t total_bits, uintptr_t slot_bytes, uintptr_t words, long long cap_words,

@@ -5,19 +5,26 @@
 // the decision records (csrc/common/h264_cabac.h: cabac_prepare_mb + cabac_qp_chain), so
 // the binarisation of every macroblock of every slot runs in parallel and records
 // 16-bit symbols; the serial stage is a tight arithmetic-coding loop over them.  The
-// binariser is the shared host/device code, so the bytes equal the host writer's (CPU
-// test oracle; tests/test_cabac.py pins the symbol decomposition on the CPU).
+// binariser and the symbol coder are the shared host/device code, so the bytes equal the
+// host writer's (tests/test_cabac.py pins the decomposition on the CPU).
 //
-// Kernels (batched over B slots; each (slot, frame) picture is one slice):
-//   cabac_mask    (nmb/2 x B, wave64)    non-zero mask of every 4x4 / DC block of every MB
-//   cabac_prep    (nmb/64 x B, 64)       lane per MB: coding state (skip, cbp, mvd, cbf ...)
-//   cabac_chain   (B, 1024)              mb_qp_delta chain (QP_pred scan) per slot
-//   cabac_count   (nmb/64 x B, 64)       lane per MB: symbol count
-//   cabac_offsets (B, 1024)              exclusive scan of the counts, capacity check
-//   cabac_bins    (nmb/64 x B, 64)       lane per MB: symbols
-//   cabac_arith   (B/64, 64)             lane per slot: context states (LDS, one column per
-//                                         lane), slice header bytes, arithmetic coding
-//   cabac_compact (B, 256)               slot outputs packed back to back
+// Two launches:
+//   mivc_launch_cabac_bin   one frame step (B slots, one slice each), into a symbol pool
+//     cabac_mask    (nmb/2 x B, wave64)    non-zero mask of every 4x4 / DC block
+//     cabac_prep    (nmb/64 x B, 64)       lane per MB: coding state (skip, cbp, mvd, cbf ...)
+//     cabac_chain   (B, 1024)              mb_qp_delta chain (QP_pred scan) per slot
+//     cabac_count   (nmb/64 x B, 64)       lane per MB: symbol count
+//     cabac_offsets (B, 1024)              per-slot exclusive scan of the counts
+//     cabac_alloc   (1, 1024)              slot regions in the pool (scan over slots)
+//     cabac_bins    (nmb/64 x B, 64)       lane per MB: symbols, staged to 16-byte stores
+//   mivc_launch_cabac_code  G frame steps at once (G * B slices: one lane each)
+//     cabac_arith   (G*B/64, 64)           context states in LDS (one column per lane),
+//                                          header bytes + arithmetic coding, output written
+//                                          in place over the slice's consumed symbols
+//     cabac_compact (G*B, 256)             slice outputs packed back to back
+// The serial stage is latency-bound (a chain of dependent LDS reads per bin), so its
+// throughput scales with the number of independent slices in flight: grouping G frame
+// steps multiplies the waves the chip runs at once by G.
 #include "kcommon.h"
 // after kcommon.h: the shared headers' MIVC_HD needs the HIP runtime declarations
 #include "../common/h264_cabac.h"
@@ -29,32 +36,32 @@ using h264::CabacNb;
 using h264::CabacSliceInfo;
 using h264::MbHeader;
 
-struct CabacArgs {
+// symbols reserved in front of every slice's symbols: the slice header bytes are written
+// there, so the in-place output (<= header + 10 bits per symbol) never overtakes the reads
+constexpr int kCabacGap = 64;
+
+struct CabacBinArgs {
   Geom g;
-  const MbHeader* hdr;       // [B, nmb]
-  const int16_t* coef;       // [B, nmb, 408]
-  uint32_t* mask;            // [B, nmb]
-  CabacNb* nb;               // [B, nmb]
-  int* cnt;                  // [B, nmb] symbols per MB
-  long long* off;            // [B, nmb] symbol offset per MB
-  int* total;                // [B] symbols per slot
-  uint16_t* syms;            // [B, cap_syms]
-  long long cap_syms;
-  uint8_t* slot_out;         // [B, cap] per-slot slice RBSP (header + data)
-  long long cap;
-  int* slot_bytes;           // [B] (-1: overflow)
-  const uint32_t* hdr_bits;  // [B, 16] slice header incl. cabac_alignment_one_bits, big-endian words
-  const int* hdr_nbits;      // [B] (a multiple of 8)
-  const int* slot_qp;        // [B] slice QP
+  const MbHeader* hdr;    // [B, nmb]
+  const int16_t* coef;    // [B, nmb, 408]
+  uint32_t* mask;         // [B, nmb]
+  CabacNb* nb;            // [B, nmb]
+  int* cnt;               // [B, nmb] symbols per MB
+  long long* off;         // [B, nmb] symbol offset of the MB inside its slice
+  int* tot;               // [B] symbols per slice (scratch)
+  uint16_t* pool;         // symbol pool of the group
+  long long pool_cap;     // symbols
+  long long* pool_used;   // [1] running allocation of the group
+  long long* base;        // [B] out: slice region start (symbols, a multiple of 8)
+  int* total;             // [B] out: symbols of the slice (-1: pool exhausted)
+  const int* slot_qp;     // [B] slice QP
   int slice_type;
   int num_ref_l0, num_ref_l1;
   int t8x8_mode;
-  uint8_t* out;              // compacted
-  long long* out_off;        // [B]
   int* err;
 };
 
-__device__ __forceinline__ CabacSliceInfo slice_info(const CabacArgs& a, int slot) {
+__device__ __forceinline__ CabacSliceInfo slice_info(const CabacBinArgs& a, int slot) {
   CabacSliceInfo si{};
   si.slice_type = a.slice_type;
   si.wmb = a.g.wmb;
@@ -67,7 +74,7 @@ __device__ __forceinline__ CabacSliceInfo slice_info(const CabacArgs& a, int slo
   return si;
 }
 
-__global__ __launch_bounds__(64) void cabac_mask(CabacArgs a) {
+__global__ __launch_bounds__(64) void cabac_mask(CabacBinArgs a) {
   const Geom& g = a.g;
   const int lane = threadIdx.x, sub = lane & 31;
   const int mb = blockIdx.x * 2 + (lane >> 5), slot = blockIdx.y;
@@ -95,7 +102,7 @@ __global__ __launch_bounds__(64) void cabac_mask(CabacArgs a) {
   if (live && sub == 0) a.mask[o] = m;
 }
 
-__global__ __launch_bounds__(64) void cabac_prep(CabacArgs a) {
+__global__ __launch_bounds__(64) void cabac_prep(CabacBinArgs a) {
   const int mb = blockIdx.x * 64 + threadIdx.x, slot = blockIdx.y;
   if (mb >= a.g.nmb()) return;
   const CabacSliceInfo si = slice_info(a, slot);
@@ -106,7 +113,7 @@ __global__ __launch_bounds__(64) void cabac_prep(CabacArgs a) {
 // mb_qp_delta chain (cabac_qp_chain as a scan): MB i codes a delta iff it is not skipped
 // and (cbp != 0 or I16x16); its delta is QP_i - QP of the last earlier delta MB (or the
 // slice QP); its first-bin context is "MB i-1 coded a non-zero delta".
-__global__ __launch_bounds__(1024) void cabac_chain(CabacArgs a) {
+__global__ __launch_bounds__(1024) void cabac_chain(CabacBinArgs a) {
   const int slot = blockIdx.x, n = a.g.nmb();
   CabacNb* nb = a.nb + static_cast<size_t>(slot) * n;
   __shared__ int s_last[1024];
@@ -142,7 +149,7 @@ __global__ __launch_bounds__(1024) void cabac_chain(CabacArgs a) {
     nb[i].prev_dqp_nz = static_cast<uint8_t>(i > 0 && has(i - 1) && nb[i - 1].dqp != 0);
 }
 
-__global__ __launch_bounds__(64) void cabac_count(CabacArgs a) {
+__global__ __launch_bounds__(64) void cabac_count(CabacBinArgs a) {
   const int mb = blockIdx.x * 64 + threadIdx.x, slot = blockIdx.y, n = a.g.nmb();
   if (mb >= n) return;
   const CabacSliceInfo si = slice_info(a, slot);
@@ -154,7 +161,24 @@ __global__ __launch_bounds__(64) void cabac_count(CabacArgs a) {
   a.cnt[base + mb] = s.out.n;
 }
 
-__global__ __launch_bounds__(1024) void cabac_offsets(CabacArgs a) {
+// Block-wide exclusive scan helper (blockDim.x == 1024): returns the exclusive prefix of
+// `v` over the threads and the block total.
+__device__ __forceinline__ long long block_scan_excl(long long v, long long* s, long long& total) {
+  s[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 1; o < blockDim.x; o <<= 1) {
+    const long long w = threadIdx.x >= o ? s[threadIdx.x - o] : 0;
+    __syncthreads();
+    s[threadIdx.x] += w;
+    __syncthreads();
+  }
+  total = s[blockDim.x - 1];
+  const long long ex = s[threadIdx.x] - v;
+  __syncthreads();
+  return ex;
+}
+
+__global__ __launch_bounds__(1024) void cabac_offsets(CabacBinArgs a) {
   const int slot = blockIdx.x, n = a.g.nmb();
   const size_t base = static_cast<size_t>(slot) * n;
   __shared__ long long s_sum[1024];
@@ -162,100 +186,125 @@ __global__ __launch_bounds__(1024) void cabac_offsets(CabacArgs a) {
   const int i0 = threadIdx.x * per, i1 = min(n, i0 + per);
   long long loc = 0;
   for (int i = i0; i < i1; ++i) loc += a.cnt[base + i];
-  s_sum[threadIdx.x] = loc;
-  __syncthreads();
-  for (int o = 1; o < blockDim.x; o <<= 1) {
-    const long long v = threadIdx.x >= o ? s_sum[threadIdx.x - o] : 0;
-    __syncthreads();
-    s_sum[threadIdx.x] += v;
-    __syncthreads();
-  }
-  long long p = threadIdx.x > 0 ? s_sum[threadIdx.x - 1] : 0;
+  long long tot;
+  long long p = block_scan_excl(loc, s_sum, tot);
   for (int i = i0; i < i1; ++i) {
     a.off[base + i] = p;
     p += a.cnt[base + i];
   }
-  if (threadIdx.x == blockDim.x - 1) {
-    const long long tot = s_sum[blockDim.x - 1];
-    const bool fits = tot <= a.cap_syms;
-    a.total[slot] = fits ? static_cast<int>(tot) : -1;
-    if (!fits) atomicOr(a.err, 2);
+  if (threadIdx.x == 0) a.tot[slot] = static_cast<int>(tot);
+}
+
+// Slice regions of this frame step in the group's pool: kCabacGap + symbols, rounded to
+// 8 symbols (16-byte aligned), allocated back to back after the group's earlier steps.
+__global__ __launch_bounds__(1024) void cabac_alloc(CabacBinArgs a) {
+  __shared__ long long s_sum[1024];
+  const int B = a.g.B;
+  const int per = (B + blockDim.x - 1) / blockDim.x;
+  const int i0 = threadIdx.x * per, i1 = min(B, i0 + per);
+  auto region = [&](int s) { return (static_cast<long long>(a.tot[s]) + kCabacGap + 7) & ~7ll; };
+  long long loc = 0;
+  for (int i = i0; i < i1; ++i) loc += region(i);
+  long long sum;
+  long long p = block_scan_excl(loc, s_sum, sum);
+  const long long start = *a.pool_used;
+  const bool fits = start + sum + 32 <= a.pool_cap;  // + 32: the coder's read-ahead
+  for (int i = i0; i < i1; ++i) {
+    a.base[i] = start + p;
+    a.total[i] = fits ? a.tot[i] : -1;
+    p += region(i);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (fits) *a.pool_used = start + sum;
+    else atomicOr(a.err, 4);
   }
 }
 
-__global__ __launch_bounds__(64) void cabac_bins(CabacArgs a) {
+// Symbol sink of cabac_bins: symbols go through an 8-entry LDS stage per lane and leave
+// as 16-byte stores (an MB's first and last partial chunks element by element, since the
+// neighbouring MBs' lanes own the rest of those chunks).
+struct StagedEmit {
+  uint16_t* g;     // slice symbols (16-byte aligned)
+  uint16_t* lds;   // this lane's stage
+  long long start; // first symbol index of this MB
+  long long pos;   // next symbol index
+  int n;
+  __device__ void emit(uint16_t s) {
+    lds[pos & 7] = s;
+    ++pos;
+    ++n;
+    if ((pos & 7) == 0) {
+      const long long c0 = pos - 8;
+      if (c0 >= start) {
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(lds);
+        *reinterpret_cast<uint4*>(g + c0) = make_uint4(w[0], w[1], w[2], w[3]);
+      } else {
+        for (long long i = start; i < pos; ++i) g[i] = lds[i & 7];
+      }
+    }
+  }
+  __device__ void finish() {
+    const long long c0 = pos & ~7ll;
+    for (long long i = c0 > start ? c0 : start; i < pos; ++i) g[i] = lds[i & 7];
+  }
+};
+
+__global__ __launch_bounds__(64) void cabac_bins(CabacBinArgs a) {
+  __shared__ __attribute__((aligned(16))) uint16_t stage[64 * 8];
   const int mb = blockIdx.x * 64 + threadIdx.x, slot = blockIdx.y, n = a.g.nmb();
   if (mb >= n || a.total[slot] < 0) return;
   const CabacSliceInfo si = slice_info(a, slot);
   const size_t base = static_cast<size_t>(slot) * n;
-  h264::CabacSymbolPacker<h264::CabacStoreEmit> s;
-  s.out.p = a.syms + static_cast<size_t>(slot) * a.cap_syms + a.off[base + mb];
-  h264::CabacMbCoder<h264::CabacSymbolPacker<h264::CabacStoreEmit>> coder(s, si, a.nb + base);
+  h264::CabacSymbolPacker<StagedEmit> s;
+  s.out.g = a.pool + a.base[slot] + kCabacGap;
+  s.out.lds = stage + threadIdx.x * 8;
+  s.out.start = s.out.pos = a.off[base + mb];
+  s.out.n = 0;
+  h264::CabacMbCoder<h264::CabacSymbolPacker<StagedEmit>> coder(s, si, a.nb + base);
   coder.code_mb(mb, a.hdr[base + mb], a.coef + (base + mb) * h264::kCoefPerMb, mb == n - 1);
   s.flush_bypass();
+  s.out.finish();
 }
 
 // ---------------------------------------------------------------- serial arithmetic coding
-// One lane per slot (64 slots per wave).  The context states of lane l live in LDS column
-// l (st[ctx * 64 + l]: lanes reading the same context hit distinct bytes), the LPS tables
-// in LDS; coder registers stay in VGPRs.  Byte-oriented coder of h264::CabacEncoder.
-struct ArithState {
-  uint32_t low, range;
-  int nbits, pend, nff, bad;
-  uint8_t* o;
-  long long n, cap;
+struct CabacCodeArgs {
+  int L;                     // slices: G frame steps x B slots (lane l = step * B + slot)
+  int B;
+  uint16_t* pool;
+  const long long* base;     // [L]
+  const int* total;          // [L]
+  const uint32_t* hdr_bits;  // [L, 16] slice header incl. cabac_alignment_one_bits, big-endian words
+  const int* hdr_nbits;      // [L] (a multiple of 8)
+  const int* slot_qp;        // [L] slice QP
+  unsigned long long itypes; // bit g: frame step g is an I slice (else P)
+  int* bytes;                // [L] out: slice RBSP bytes (-1: error)
+  uint8_t* out;              // compacted slices
+  long long* out_off;        // [L]
+  int* err;
 };
 
-__device__ __forceinline__ void ar_out(ArithState& s, int b) {
-  if (s.n < s.cap) s.o[s.n] = static_cast<uint8_t>(b);
-  ++s.n;
-}
-__device__ __forceinline__ void ar_put_byte(ArithState& s, uint32_t v) {
-  const int b = static_cast<int>(v & 0xFFu);
-  if (v >> 8) {
-    if (s.pend < 0) s.bad = 1;
-    if (s.nff > 0) {
-      ar_out(s, s.pend + 1);
-      for (int k = 0; k < s.nff - 1; ++k) ar_out(s, 0);
-      s.pend = 0;
-      s.nff = 0;
-    } else {
-      s.pend += 1;
-    }
+struct InPlaceOut {
+  uint8_t* p;
+  long long n, cap;
+  __device__ void put(int b) {
+    if (n < cap) p[n] = static_cast<uint8_t>(b);
+    ++n;
   }
-  if (b == 0xFF) {
-    ++s.nff;
-  } else {
-    if (s.pend >= 0) {
-      ar_out(s, s.pend);
-      for (int k = 0; k < s.nff; ++k) ar_out(s, 0xFF);
-    }
-    s.pend = b;
-    s.nff = 0;
-  }
-}
-__device__ __forceinline__ void ar_drain(ArithState& s) {
-  while (s.nbits >= 8) {
-    const int sh = s.nbits + 2;
-    const uint32_t v = s.low >> sh;
-    s.low &= (1u << sh) - 1u;
-    s.nbits -= 8;
-    ar_put_byte(s, v);
-  }
-}
+};
 
-__global__ __launch_bounds__(64) void cabac_arith(CabacArgs a) {
+__global__ __launch_bounds__(64) void cabac_arith(CabacCodeArgs a) {
   __shared__ uint8_t st[h264::kCabacContexts * 64];
   __shared__ uint8_t lps[64 * 4];
   __shared__ uint8_t trans[64];
   const int lane = threadIdx.x;
-  const int slot = blockIdx.x * 64 + lane;
-  const bool live = slot < a.g.B;
+  const int l = blockIdx.x * 64 + lane;
+  const bool live = l < a.L;
   for (int i = lane; i < 256; i += 64) lps[i] = h264::kCabacRangeLPS[i >> 2][i & 3];
   trans[lane] = h264::kCabacTransLPS[lane];
-  // context states of every lane's slice (its own slice QP)
-  const int qp = live ? h264::clip3(0, 51, a.slot_qp[slot]) : 26;
-  const int table = a.slice_type == h264::SLICE_I ? 0 : 1;  // cabac_init_idc 0
+  // context states of this lane's slice (its slice type and QP; cabac_init_idc 0)
+  const int qp = live ? h264::clip3(0, 51, a.slot_qp[l]) : 26;
+  const int table = live && ((a.itypes >> (l / a.B)) & 1ull) ? 0 : 1;
   for (int i = 0; i < h264::kCabacContexts; ++i) {
     const int r = i < 276 ? i : (i >= 399 && i <= 435 ? i - 399 + 276 : -1);
     uint8_t v = 0;
@@ -268,102 +317,58 @@ __global__ __launch_bounds__(64) void cabac_arith(CabacArgs a) {
   }
   __syncthreads();
   if (!live) return;
-  const int total = a.total[slot];
-  if (total < 0) {
-    a.slot_bytes[slot] = -1;
+  const int total = a.total[l];
+  const uint16_t* sy = a.pool + a.base[l] + kCabacGap;
+  if (total < 0) {  // pool exhausted (reported by cabac_alloc)
+    a.bytes[l] = -1;
     return;
   }
-  ArithState s;
-  s.o = a.slot_out + static_cast<size_t>(slot) * a.cap;
-  s.cap = a.cap;
-  const int hbytes = a.hdr_nbits[slot] >> 3;
-  for (int i = 0; i < hbytes; ++i) s.o[i] = static_cast<uint8_t>(a.hdr_bits[slot * 16 + (i >> 2)] >> (24 - 8 * (i & 3)));
-  s.n = hbytes;
-  s.low = 0;
-  s.range = 510;
-  s.nbits = -1;
-  s.pend = -1;
-  s.nff = 0;
-  s.bad = 0;
-  const uint16_t* sy = a.syms + static_cast<size_t>(slot) * a.cap_syms;
-  uint4 buf = make_uint4(0, 0, 0, 0);
-  for (int i = 0; i < total; ++i) {
-    if ((i & 7) == 0) buf = *reinterpret_cast<const uint4*>(sy + i);  // 8 symbols (cap is a multiple of 8)
-    const uint32_t w = (i & 4) ? ((i & 2) ? buf.w : buf.z) : ((i & 2) ? buf.y : buf.x);
-    const uint32_t sym = (i & 1) ? (w >> 16) : (w & 0xFFFFu);
-    if (!(sym & 0x8000u)) {
-      // EncodeDecision
-      const int ctx = sym & 0x1FF, bin = (sym >> 9) & 1;
-      uint8_t* sp = &st[ctx * 64 + lane];
-      const int sv = *sp;
-      int pst = sv >> 1, mps = sv & 1;
-      const uint32_t rlps = lps[pst * 4 + ((s.range >> 6) & 3)];
-      s.range -= rlps;
-      if (bin != mps) {
-        s.low += s.range;
-        s.range = rlps;
-        mps ^= pst == 0;
-        pst = trans[pst];
-      } else {
-        pst = min(pst + 1, 62);
-      }
-      *sp = static_cast<uint8_t>((pst << 1) | mps);
-      if (s.range < 256) {
-        const int sh = __clz(static_cast<int>(s.range)) - 23;
-        s.range <<= sh;
-        s.low <<= sh;
-        s.nbits += sh;
-      }
-    } else if (!(sym & 0x4000u)) {
-      // n bypass bins at once
-      const int nb = (sym >> 10) & 15;
-      s.low = (s.low << nb) + s.range * (sym & 0x3FFu);
-      s.nbits += nb;
-    } else {
-      // EncodeTerminate (+ EncodeFlush and the stop bit on the last MB)
-      s.range -= 2;
-      if (!(sym & 1)) {
-        if (s.range < 256) {
-          s.range <<= 1;
-          s.low <<= 1;
-          s.nbits += 1;
-        }
-      } else {
-        s.low += s.range;
-        s.range = 2;
-        s.low <<= 7;
-        s.nbits += 7;
-        ar_drain(s);
-        s.low |= 0x80u;
-        s.low <<= 3;
-        s.nbits += 3;
-        ar_drain(s);
-        if (s.nbits > 0) {
-          s.low <<= 8 - s.nbits;
-          s.nbits = 8;
-          ar_drain(s);
-        }
-        if (s.pend >= 0) ar_out(s, s.pend);
-        for (int k = 0; k < s.nff; ++k) ar_out(s, 0xFF);
-        s.pend = -1;
-        s.nff = 0;
-      }
-    }
-    if (s.nbits >= 8) ar_drain(s);
+  if (total == 0 || sy[total - 1] != 0xC001u) {
+    a.bytes[l] = -1;
+    atomicOr(a.err, 8);
+    return;
   }
-  const bool bad = s.bad || s.n > s.cap;
-  a.slot_bytes[slot] = bad ? -1 : static_cast<int>(s.n);
-  if (bad) atomicOr(a.err, 2);
+  h264::CabacSymbolCoder<InPlaceOut> c;
+  c.out.p = reinterpret_cast<uint8_t*>(a.pool + a.base[l]);
+  c.out.cap = 2ll * (((static_cast<long long>(total) + kCabacGap + 7) & ~7ll));
+  const int hbytes = a.hdr_nbits[l] >> 3;
+  for (int i = 0; i < hbytes; ++i) c.out.p[i] = static_cast<uint8_t>(a.hdr_bits[l * 16 + (i >> 2)] >> (24 - 8 * (i & 3)));
+  c.out.n = hbytes;
+  c.init();
+  // symbols 8 at a time, the next 8 already in flight
+  const uint4* q = reinterpret_cast<const uint4*>(sy);
+  uint4 cur = q[0], nxt = q[1];
+  const int n = total - 1;  // the last symbol is end_of_slice_flag = 1: finish()
+  for (int i0 = 0; i0 < n; i0 += 8) {
+    const uint32_t w[4] = {cur.x, cur.y, cur.z, cur.w};
+    cur = nxt;
+    nxt = q[(i0 >> 3) + 2];
+    const int m = min(8, n - i0);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k < m) c.step((k & 1) ? (w[k >> 1] >> 16) : (w[k >> 1] & 0xFFFFu), st + lane, 64, lps, trans);
+    }
+  }
+  c.finish();
+  const bool bad = c.bad || c.out.n > c.out.cap;
+  a.bytes[l] = bad ? -1 : static_cast<int>(c.out.n);
+  if (bad) atomicOr(a.err, 8);
 }
 
-__global__ __launch_bounds__(256) void cabac_compact(CabacArgs a) {
-  const int slot = blockIdx.x;
-  long long off = 0;
-  for (int s = 0; s < slot; ++s) off += a.slot_bytes[s] > 0 ? a.slot_bytes[s] : 0;
-  if (threadIdx.x == 0) a.out_off[slot] = off;
-  const int nbytes = a.slot_bytes[slot];
+__global__ __launch_bounds__(256) void cabac_compact(CabacCodeArgs a) {
+  const int l = blockIdx.x;
+  __shared__ long long s_off;
+  if (threadIdx.x == 0) s_off = 0;
+  __syncthreads();
+  long long part = 0;
+  for (int s = threadIdx.x; s < l; s += blockDim.x) part += a.bytes[s] > 0 ? a.bytes[s] : 0;
+  atomicAdd(reinterpret_cast<unsigned long long*>(&s_off), static_cast<unsigned long long>(part));
+  __syncthreads();
+  const long long off = s_off;
+  if (threadIdx.x == 0) a.out_off[l] = off;
+  const int nbytes = a.bytes[l];
   if (nbytes <= 0) return;
-  const uint8_t* src = a.slot_out + static_cast<size_t>(slot) * a.cap;
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(a.pool + a.base[l]);
   uint8_t* dst = a.out + off;
   for (int i = threadIdx.x; i < nbytes; i += blockDim.x) dst[i] = src[i];
 }
@@ -374,19 +379,16 @@ __global__ __launch_bounds__(256) void cabac_compact(CabacArgs a) {
 using namespace mivc::gpu;
 
 extern "C" size_t mivc_cabac_nb_bytes() { return sizeof(CabacNb); }
+extern "C" int mivc_cabac_gap() { return kCabacGap; }
 
-// Scratch (all device memory, caller-owned): mask [B, nmb] u32, nb [B, nmb] CabacNb,
-// cnt [B, nmb] i32, off [B, nmb] i64, total [B] i32, syms [B, cap_syms] u16 (cap_syms a
-// multiple of 8), slot_out [B, cap] u8.  hdr_bits / hdr_nbits: slice header incl. the
-// cabac_alignment_one_bits (byte-aligned).  Results: out (compacted), slot_bytes,
-// out_off; err |= 2 on overflow.
-extern "C" void mivc_launch_cabac(int B, int wmb, int hmb, const void* hdr, const int16_t* coef, uint32_t* mask,
-                                  void* nb, int* cnt, long long* off, int* total, uint16_t* syms, long long cap_syms,
-                                  uint8_t* slot_out, long long cap, int* slot_bytes, const uint32_t* hdr_bits,
-                                  const int* hdr_nbits, const int* slot_qp, int slice_type, int num_ref_l0,
-                                  int num_ref_l1, int t8x8_mode, uint8_t* out, long long* out_off, int* err,
-                                  void* stream) {
-  CabacArgs a;
+// One frame step's slices -> symbols in the group pool (pool_used advances; base/total
+// describe each slice's region).  Scratch: mask, nb, cnt, off [B, nmb], tot [B].
+extern "C" void mivc_launch_cabac_bin(int B, int wmb, int hmb, const void* hdr, const int16_t* coef, uint32_t* mask,
+                                      void* nb, int* cnt, long long* off, int* tot, uint16_t* pool,
+                                      long long pool_cap, long long* pool_used, long long* base, int* total,
+                                      const int* slot_qp, int slice_type, int num_ref_l0, int num_ref_l1,
+                                      int t8x8_mode, int* err, void* stream) {
+  CabacBinArgs a;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.hdr = static_cast<const MbHeader*>(hdr);
   a.coef = coef;
@@ -394,21 +396,17 @@ extern "C" void mivc_launch_cabac(int B, int wmb, int hmb, const void* hdr, cons
   a.nb = static_cast<CabacNb*>(nb);
   a.cnt = cnt;
   a.off = off;
+  a.tot = tot;
+  a.pool = pool;
+  a.pool_cap = pool_cap;
+  a.pool_used = pool_used;
+  a.base = base;
   a.total = total;
-  a.syms = syms;
-  a.cap_syms = cap_syms;
-  a.slot_out = slot_out;
-  a.cap = cap;
-  a.slot_bytes = slot_bytes;
-  a.hdr_bits = hdr_bits;
-  a.hdr_nbits = hdr_nbits;
   a.slot_qp = slot_qp;
   a.slice_type = slice_type;
   a.num_ref_l0 = num_ref_l0;
   a.num_ref_l1 = num_ref_l1;
   a.t8x8_mode = t8x8_mode;
-  a.out = out;
-  a.out_off = out_off;
   a.err = err;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int nmb = wmb * hmb;
@@ -418,7 +416,31 @@ extern "C" void mivc_launch_cabac(int B, int wmb, int hmb, const void* hdr, cons
   hipLaunchKernelGGL(cabac_chain, dim3(B), dim3(1024), 0, s, a);
   hipLaunchKernelGGL(cabac_count, mbgrid, dim3(64), 0, s, a);
   hipLaunchKernelGGL(cabac_offsets, dim3(B), dim3(1024), 0, s, a);
+  hipLaunchKernelGGL(cabac_alloc, dim3(1), dim3(1024), 0, s, a);
   hipLaunchKernelGGL(cabac_bins, mbgrid, dim3(64), 0, s, a);
-  hipLaunchKernelGGL(cabac_arith, dim3((B + 63) / 64), dim3(64), 0, s, a);
-  hipLaunchKernelGGL(cabac_compact, dim3(B), dim3(256), 0, s, a);
+}
+
+// L = G * B slices (frame step g of the group, slot b at l = g * B + b) -> slice RBSPs
+// (header + CABAC data + stop bit), compacted in l order into `out`.
+extern "C" void mivc_launch_cabac_code(int L, int B, uint16_t* pool, const long long* base, const int* total,
+                                       const uint32_t* hdr_bits, const int* hdr_nbits, const int* slot_qp,
+                                       unsigned long long itypes, int* bytes, uint8_t* out, long long* out_off,
+                                       int* err, void* stream) {
+  CabacCodeArgs a;
+  a.L = L;
+  a.B = B;
+  a.pool = pool;
+  a.base = base;
+  a.total = total;
+  a.hdr_bits = hdr_bits;
+  a.hdr_nbits = hdr_nbits;
+  a.slot_qp = slot_qp;
+  a.itypes = itypes;
+  a.bytes = bytes;
+  a.out = out;
+  a.out_off = out_off;
+  a.err = err;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(cabac_arith, dim3((L + 63) / 64), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(cabac_compact, dim3(L), dim3(256), 0, s, a);
 }

@@ -121,7 +121,11 @@ class GpuH264Encoder:
     Baseline with GPU CAVLC; ``entropy="cpu"`` codes the slices with the host writers."""
 
     def __init__(self, params: H264Params, slots: int, device: str | torch.device = "cuda",
-                 entropy_threads: int | None = None, entropy: str = "gpu"):
+                 entropy_threads: int | None = None, entropy: str = "gpu", cabac_group: int | None = None):
+        """cabac_group: frame steps whose slices the GPU CABAC arithmetic coder runs at once
+        (default 8; its serial stage runs one slice per lane, so throughput scales with it).
+        The symbol pool budget per MB is MIVC_CABAC_SYMS_PER_MB (default 128 per frame step,
+        shared by the steps of a group)."""
         if params.width % 2 or params.height % 2:
             raise ValueError("width and height must be even")
         if entropy not in ("gpu", "cpu"):
@@ -168,6 +172,8 @@ class GpuH264Encoder:
         if entropy == "cpu":
             self.h_hdr = [torch.empty((B, nmb, MB_HDR_BYTES), dtype=u8).pin_memory() for _ in range(2)]
             self.h_coef = [torch.empty((B, nmb, COEF_PER_MB), dtype=i16).pin_memory() for _ in range(2)]
+        elif params.cabac:
+            self._alloc_cabac(cabac_group)
         else:
             i64 = torch.int64
             mbb = int(self.hip.cavlc_mb_bytes())
@@ -192,20 +198,6 @@ class GpuH264Encoder:
             self.h_out: list = [None, None, None]
             self.out_done = [torch.cuda.Event() for _ in range(2)]
             self.copy_pool = cf.ThreadPoolExecutor(max_workers=1)
-            if params.cabac:
-                # per-slot slice RBSP scratch (worst case ~3 kbit per MB, as for CAVLC), the
-                # per-MB coding state of the parallel binariser and the 16-bit symbol buffer of
-                # the serial arithmetic coder (all used on the copy stream only)
-                self.cab_cap = nmb * 384 + 4096
-                self.cab_cap_syms = nmb * 512 + 64
-                self.cab_slot = torch.empty((B * self.cab_cap,), dtype=u8, device=dev)
-                self.cab_mask = torch.zeros((B, nmb), dtype=torch.int32, device=dev)
-                self.cab_nb = torch.zeros((B, nmb, int(self.hip.cabac_nb_bytes())), dtype=u8, device=dev)
-                self.cab_cnt = torch.zeros((B, nmb), dtype=i32, device=dev)
-                self.cab_off = torch.zeros((B, nmb), dtype=i64, device=dev)
-                self.cab_total = torch.zeros((B,), dtype=i32, device=dev)
-                self.cab_syms = torch.empty((B * self.cab_cap_syms,), dtype=torch.int16, device=dev)
-                self.cav_out = [torch.zeros((B * self.cab_cap,), dtype=u8, device=dev) for _ in range(2)]
         self.copy_stream = torch.cuda.Stream(device=dev)
         self.copy_done = [torch.cuda.Event() for _ in range(2)]
         self.compute_done = [torch.cuda.Event() for _ in range(2)]
@@ -214,6 +206,52 @@ class GpuH264Encoder:
         self.cfg = params.host_cfg()
         self.timings: dict[str, float] = {}
         self.stats: dict[str, float] = {}
+
+    def _alloc_cabac(self, group: int | None):
+        """GPU CABAC buffers.  Per frame step (copy stream): block masks, per-MB coding state
+        and symbol counts.  Per group of G steps, double-buffered (group g binarises into
+        ring g % 2 while the arithmetic coder drains ring (g - 1) % 2 on the entropy stream):
+        the symbol pool (slice outputs are written over their consumed symbols), slice
+        regions / symbol totals, slice headers, output sizes and the compacted bytes."""
+        B, nmb, dev = self.B, self.nmb, self.dev
+        u8, i32, i64 = torch.uint8, torch.int32, torch.int64
+        G = int(group or os.environ.get("MIVC_CABAC_GROUP", 8))
+        if not 1 <= G <= 64:
+            raise ValueError("cabac_group must be in 1..64")
+        self.cab_G = G
+        # pool budget: an average per MB and frame step plus one picture's worth of intra-heavy
+        # headroom per group (IDR / scene cuts / low QPs run to several hundred symbols per MB)
+        per_mb = int(os.environ.get("MIVC_CABAC_SYMS_PER_MB", 96))
+        peak_mb = int(os.environ.get("MIVC_CABAC_PEAK_SYMS_PER_MB", 768))
+        gap = int(self.hip.cabac_gap())
+        L = G * B
+        self.cab_pool_cap = B * nmb * (G * per_mb + peak_mb) + L * (gap + 8) + 64
+        self.cab_pool = [torch.empty((self.cab_pool_cap + 64,), dtype=torch.int16, device=dev) for _ in range(2)]
+        self.cab_pool_used = torch.zeros((2,), dtype=i64, device=dev)
+        # slice RBSP <= header (64 B) + 10 bits per symbol + flush: 1.25 bytes per pool symbol
+        comp_cap = (self.cab_pool_cap * 5) // 4 + 80 * L
+        self.cab_comp = [torch.empty((comp_cap,), dtype=u8, device=dev) for _ in range(2)]
+        self.cab_comp_off = [torch.zeros((L,), dtype=i64, device=dev) for _ in range(2)]
+        self.cab_base = [torch.zeros((L,), dtype=i64, device=dev) for _ in range(2)]
+        self.cab_total = [torch.zeros((L,), dtype=i32, device=dev) for _ in range(2)]
+        self.cab_bytes = [torch.zeros((L,), dtype=i32, device=dev) for _ in range(2)]
+        self.h_cab_bytes = [torch.zeros((L,), dtype=i32).pin_memory() for _ in range(2)]
+        self.h_pool_used = [torch.zeros((1,), dtype=i64).pin_memory() for _ in range(2)]
+        self.cab_hdr_bits = [torch.zeros((L, 16), dtype=i32, device=dev) for _ in range(2)]
+        self.cab_hdr_nbits = [torch.zeros((L,), dtype=i32, device=dev) for _ in range(2)]
+        self.h_cab_hdr_bits = [torch.zeros((L, 16), dtype=i32).pin_memory() for _ in range(2)]
+        self.h_cab_hdr_nbits = [torch.zeros((L,), dtype=i32).pin_memory() for _ in range(2)]
+        self.cab_mask = torch.zeros((B, nmb), dtype=i32, device=dev)
+        self.cab_nb = torch.zeros((B, nmb, int(self.hip.cabac_nb_bytes())), dtype=u8, device=dev)
+        self.cab_cnt = torch.zeros((B, nmb), dtype=i32, device=dev)
+        self.cab_off = torch.zeros((B, nmb), dtype=i64, device=dev)
+        self.cab_tot = torch.zeros((B,), dtype=i32, device=dev)
+        self.entropy_stream = torch.cuda.Stream(device=dev)
+        self.d2h_stream = torch.cuda.Stream(device=dev)  # the copy thread's byte copies
+        self.cab_bin_done = [torch.cuda.Event() for _ in range(2)]
+        self.cab_done = [torch.cuda.Event() for _ in range(2)]
+        self.h_cab_out: list = [None, None]
+        self.copy_pool = cf.ThreadPoolExecutor(max_workers=1)
 
     # ------------------------------------------------------------------ helpers
     @staticmethod
@@ -285,22 +323,98 @@ class GpuH264Encoder:
     def _frame_params(self, b: int, t: int, qp_frame: int, idr: bool, idr_ids: list[int]) -> dict:
         return dict(idr=int(idr), frame_num=t, idr_pic_id=idr_ids[b] & 0xFFFF, qp=qp_frame)
 
-    def _gpu_cabac(self, k: int, t: int, qps_t, idr: bool, idr_ids: list[int], qp_dev: torch.Tensor):
-        """Launch the CABAC kernels for the current frame step on the *copy* stream, so the
-        serial slice coding of frame t overlaps the encode of frame t + 1 (the records are
-        double-buffered; the main stream waits for copy_done[k] before reusing them).
+    def _gpu_cabac_bin(self, k: int, t: int, qps_t, idr: bool, idr_ids: list[int], qp_dev: torch.Tensor):
+        """Binarise frame step t (records hdr[k]/coef[k]) into the symbol pool of its group
+        ring, on the *copy* stream (the caller's current stream): the records are free
+        again once this is done, whatever the arithmetic coder is doing.
         qp_dev: [B] int32 slice QPs of this step in a buffer that outlives the launch."""
-        self._header_bits(k, t, qps_t, idr, idr_ids)
+        G, B = self.cab_G, self.B
+        r, j = (t // G) & 1, t % G
+        if j == 0:
+            self.cab_pool_used[r].zero_()
+        self._header_bits_into(self.h_cab_hdr_bits[r][j * B:(j + 1) * B], self.h_cab_hdr_nbits[r][j * B:(j + 1) * B],
+                               self.cab_hdr_bits[r][j * B:(j + 1) * B], self.cab_hdr_nbits[r][j * B:(j + 1) * B],
+                               t, qps_t, idr, idr_ids)
         P = self._ptr
-        self.hip.cabac(self.B, self.wmb, self.hmb, P(self.hdr[k]), P(self.coef[k]), P(self.cab_mask), P(self.cab_nb),
-                       P(self.cab_cnt), P(self.cab_off), P(self.cab_total), P(self.cab_syms), self.cab_cap_syms,
-                       P(self.cab_slot), self.cab_cap, P(self.cav_sizes[k]), P(self.cav_hdr_bits[k]), P(self.cav_hdr_nbits[k]),
-                       P(qp_dev), 2 if idr else 0, 1, 1, 0, P(self.cav_out[k]), P(self.cav_out_off), P(self.err),
-                       self.copy_stream.cuda_stream)
+        self.hip.cabac_bin(B, self.wmb, self.hmb, P(self.hdr[k]), P(self.coef[k]), P(self.cab_mask), P(self.cab_nb),
+                           P(self.cab_cnt), P(self.cab_off), P(self.cab_tot), P(self.cab_pool[r]), self.cab_pool_cap,
+                           self.cab_pool_used[r].data_ptr(), self.cab_base[r][j * B:].data_ptr(),
+                           self.cab_total[r][j * B:].data_ptr(), P(qp_dev), 2 if idr else 0, 1, 1, 0, P(self.err),
+                           self.copy_stream.cuda_stream)
+
+    def _gpu_cabac_code(self, t0: int, n: int, qps_d: torch.Tensor):
+        """Arithmetic-code the n frame steps t0 .. t0 + n - 1 of a group (n * B slices) on
+        the entropy stream, after their binarisation; sizes go to pinned host memory."""
+        G, B = self.cab_G, self.B
+        r = (t0 // G) & 1
+        self.cab_bin_done[r].record(self.copy_stream)
+        itypes = 1 if t0 == 0 else 0  # frame step 0 is the IDR picture
+        P = self._ptr
+        es = self.entropy_stream
+        with torch.cuda.stream(es):
+            es.wait_event(self.cab_bin_done[r])
+            self.hip.cabac_code(n * B, B, P(self.cab_pool[r]), P(self.cab_base[r]), P(self.cab_total[r]),
+                                P(self.cab_hdr_bits[r]), P(self.cab_hdr_nbits[r]), qps_d[t0].data_ptr(), itypes,
+                                P(self.cab_bytes[r]), P(self.cab_comp[r]), P(self.cab_comp_off[r]), P(self.err),
+                                es.cuda_stream)
+            self.h_cab_bytes[r][: n * B].copy_(self.cab_bytes[r][: n * B], non_blocking=True)
+            self.h_pool_used[r].copy_(self.cab_pool_used[r:r + 1], non_blocking=True)
+            self.cab_done[r].record(es)
+
+    def _copy_out_group(self, g: int, t0: int, n: int, copied, wrap_futs):
+        """Copy thread (groups in order): sizes -> compacted bytes D2H -> NAL wrapping of each
+        frame step on the pool.  ``copied[g]`` releases ring g % 2 (pool, headers, pinned
+        sizes) for group g + 2."""
+        B, G = self.B, self.cab_G
+        r = g & 1
+        t_0 = time.perf_counter()
+        self.cab_done[r].synchronize()
+        t_1 = time.perf_counter()
+        sizes = self.h_cab_bytes[r][: n * B].numpy().astype(np.int64)
+        used = int(self.h_pool_used[r][0])
+        self.stats["cabac_pool_peak"] = max(self.stats.get("cabac_pool_peak", 0.0), used / self.cab_pool_cap)
+        self.stats["cabac_syms_per_mb_peak"] = max(self.stats.get("cabac_syms_per_mb_peak", 0.0),
+                                                   used / (n * B * self.nmb))
+        if (sizes < 0).any():
+            err = int(self.err.item())
+            for f in range(t0, t0 + n):  # nothing of this group will be wrapped
+                wrap_futs[f] = self.pool.submit(lambda: [(b"", 0)] * B)
+            copied[g].set()
+            if err & 4:
+                raise RuntimeError("GPU CABAC: symbol pool exhausted (raise MIVC_CABAC_SYMS_PER_MB / "
+                                   "MIVC_CABAC_PEAK_SYMS_PER_MB or lower cabac_group)")
+            raise RuntimeError("GPU CABAC: arithmetic coder error")
+        total = int(sizes.sum())
+        if g >= 2:
+            for t in range(t0 - 2 * G, t0 - G):
+                wrap_futs[t].result()  # host buffer r is free again
+        buf = self.h_cab_out[r]
+        if buf is None or buf.numel() < total:
+            buf = self.h_cab_out[r] = torch.empty((max(total, 1 << 26),), dtype=torch.uint8).pin_memory()
+        ds = self.d2h_stream
+        with torch.cuda.device(self.dev), torch.cuda.stream(ds):
+            ds.wait_event(self.cab_done[r])
+            buf[:total].copy_(self.cab_comp[r][:total], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(ds)
+        ev.synchronize()
+        copied[g].set()
+        t_2 = time.perf_counter()
+        self.timings["entropy_wait_gpu_s"] = self.timings.get("entropy_wait_gpu_s", 0.0) + (t_1 - t_0)
+        self.timings["d2h_s"] = self.timings.get("d2h_s", 0.0) + (t_2 - t_1)
+        off = 0
+        for jj in range(n):
+            sz = sizes[jj * B:(jj + 1) * B]
+            nb = int(sz.sum())
+            wrap_futs[t0 + jj] = self.pool.submit(self._wrap, buf[off:off + nb], nb, sz.tolist(), t0 + jj == 0)
+            off += nb
 
     def _header_bits(self, k: int, t: int, qps_t, idr: bool, idr_ids: list[int]):
         """Slice headers of this step -> pinned host words -> device (current stream)."""
-        hb, hn = self.h_hdr_bits[k], self.h_hdr_nbits[k]
+        self._header_bits_into(self.h_hdr_bits[k], self.h_hdr_nbits[k], self.cav_hdr_bits[k], self.cav_hdr_nbits[k],
+                               t, qps_t, idr, idr_ids)
+
+    def _header_bits_into(self, hb, hn, db, dn, t: int, qps_t, idr: bool, idr_ids: list[int]):
         hbn, hnn = hb.numpy(), hn.numpy()
         cache = {}
         for b in range(self.B):
@@ -312,8 +426,8 @@ class GpuH264Encoder:
             hbn[b, :] = 0
             hbn[b, : len(words)] = np.array(words, dtype=np.uint32).view(np.int32)
             hnn[b] = nbits
-        self.cav_hdr_bits[k].copy_(hb, non_blocking=True)
-        self.cav_hdr_nbits[k].copy_(hn, non_blocking=True)
+        db.copy_(hb, non_blocking=True)
+        dn.copy_(hn, non_blocking=True)
 
     def _gpu_cavlc(self, k: int, t: int, qps_t, idr: bool, idr_ids: list[int]):
         """Launch the CAVLC kernels for the current frame step on the compute stream.
@@ -456,6 +570,16 @@ class GpuH264Encoder:
             while not copied[i].wait(0.5):
                 if copy_futs[i].done() and copy_futs[i].exception() is not None:
                     raise copy_futs[i].exception()
+        cabac_gpu = self.entropy == "gpu" and self.p.cabac
+        G = self.cab_G if cabac_gpu else 1
+        ngroups = (F + G - 1) // G
+        group_copied = [threading.Event() for _ in range(ngroups)]
+        group_futs: list = [None] * ngroups
+
+        def wait_group(i: int):
+            while not group_copied[i].wait(0.5):
+                if group_futs[i].done() and group_futs[i].exception() is not None:
+                    raise group_futs[i].exception()
         recons = [] if keep_recon else None
         main = torch.cuda.current_stream(self.dev)
         for t in range(F):
@@ -464,7 +588,10 @@ class GpuH264Encoder:
             qpt = qps_h[:, t]
             # the device/pinned buffers of slot k were last used by step t-2: wait for them
             tw = time.perf_counter()
-            if self.entropy == "gpu" and t >= 2:
+            if cabac_gpu:
+                if t % G == 0 and t >= 2 * G:
+                    wait_group(t // G - 2)  # ring (t // G) % 2 is free again
+            elif self.entropy == "gpu" and t >= 2:
                 wait_copied(t - 2)
             elif pending[k] is not None:
                 outs[t - 2] = pending[k].result()
@@ -487,19 +614,30 @@ class GpuH264Encoder:
             self.compute_done[k].record(main)
             with torch.cuda.stream(self.copy_stream):
                 self.copy_stream.wait_event(self.compute_done[k])
-                if self.entropy == "gpu":
-                    if self.p.cabac:
-                        self._gpu_cabac(k, t, qpt, idr, idr_ids, qps_d[t])
+                if cabac_gpu:
+                    self._gpu_cabac_bin(k, t, qpt, idr, idr_ids, qps_d[t])
+                elif self.entropy == "gpu":
                     self.h_sizes[k].copy_(self.cav_sizes[k], non_blocking=True)
                 else:
                     self.h_hdr[k].copy_(self.hdr[k], non_blocking=True)
                     self.h_coef[k].copy_(self.coef[k], non_blocking=True)
                 self.copy_done[k].record(self.copy_stream)
-            if self.entropy == "gpu":
+            if cabac_gpu:
+                if t % G == G - 1 or t == F - 1:
+                    g, t0 = t // G, t - t % G
+                    self._gpu_cabac_code(t0, t - t0 + 1, qps_d)
+                    group_futs[g] = self.copy_pool.submit(self._copy_out_group, g, t0, t - t0 + 1, group_copied,
+                                                          wrap_futs)
+            elif self.entropy == "gpu":
                 copy_futs[t] = self.copy_pool.submit(self._copy_out, t, k, idr, copied, wrap_futs)
             else:
                 pending[k] = self.pool.submit(self._write_slices, k, t, qpt, idr, idr_ids)
-        if self.entropy == "gpu":
+        if cabac_gpu:
+            for f in group_futs:
+                f.result()
+            for t in range(F):
+                outs[t] = wrap_futs[t].result()
+        elif self.entropy == "gpu":
             for t in range(F):
                 copy_futs[t].result()
             for t in range(F):
@@ -514,8 +652,8 @@ class GpuH264Encoder:
             self.stats["p_intra_ratio"] = float(self.p_intra_mbs.item()) / (B * (F - 1) * self.nmb)
         self.p_intra_mbs.zero_()
         err = int(self.err.item())
-        if err & 2:
-            raise RuntimeError("CABAC slice output overflowed its buffer")
+        if err & 14:
+            raise RuntimeError(f"GPU CABAC failed (err={err:#x}: 4 = symbol pool exhausted, 8 = coder error)")
         if err != 0:
             raise RuntimeError("wavefront progress timeout in an encode kernel")
         ps = self.parameter_sets()

@@ -91,6 +91,26 @@ def test_gpu_entropy_matches_host_writer(host, cabac):
         torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("group", [1, 2, 3])
+def test_gpu_cabac_groups_match_host_writer(host, group):
+    """The arithmetic coder runs over groups of frame steps from a double-buffered symbol
+    pool: group sizes that wrap the ring several times (and leave a partial last group)
+    give the host writer's bytes."""
+    import torch
+    from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
+
+    w, h, B, F = 176, 144, 3, 7
+    p = H264Params(width=w, height=h, crf=None, qp=26)
+    y, u, v = synth_clip(B, F, w, h, seed=13)
+    out = {}
+    for mode in ("cpu", "gpu"):
+        enc = GpuH264Encoder(p, slots=B, entropy=mode, cabac_group=group)
+        out[mode] = [r.bitstream for r in enc.encode(y, u, v)]
+        enc.close()
+    assert out["gpu"] == out["cpu"]
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("cabac", [True, False])
 def test_gpu_per_frame_qps(host, cabac):
     """Rate-control QPs per (slot, frame): GPU entropy coder == host writer, and the recon roundtrips."""
