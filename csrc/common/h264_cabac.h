@@ -1024,55 +1024,36 @@ MIVC_HD void cabac_code_symbol(CabacEncoder& e, uint16_t s) {
 //     low' = (low + add) << n + range * bypass_bits,  range' = new_range << n;
 // terminate(1), the last symbol of every slice, is finish().  Context states are read
 // at st[ctx * stride] (the GPU keeps one LDS column per lane); lps / trans are the
-// flattened Table 9-44 / transIdxLPS.  Out: put(int byte).
+// flattened Table 9-44 / transIdxLPS.
+//
+// `low` is 64-bit so bytes can be drained lazily: a symbol adds at most 10 bits, so after
+// a drain (nbits < 8) four more symbols fit (< 48 + 10 bits) before the next one.  A wave
+// then takes the divergent byte-output path once per 4 symbols instead of once per symbol.
+// Out: byte9(v) takes one output byte whose bit 8 is a carry into the bytes before it
+// (false: a carry with no byte to take it); finish() ends the byte stream.
 template <class Out>
 struct CabacSymbolCoder {
-  uint32_t low, range;
-  int nbits, pend, nff, bad;
+  uint64_t low;
+  uint32_t range;
+  int nbits, bad;
   Out out;
 
   MIVC_HD void init() {
     low = 0;
     range = 510;
     nbits = -1;
-    pend = -1;
-    nff = 0;
     bad = 0;
-  }
-  MIVC_HD void put_byte(uint32_t v) {
-    const int b = static_cast<int>(v & 0xFFu);
-    if (v >> 8) {
-      if (pend < 0) bad = 1;
-      if (nff > 0) {
-        out.put(pend + 1);
-        for (int k = 0; k < nff - 1; ++k) out.put(0);
-        pend = 0;
-        nff = 0;
-      } else {
-        pend += 1;
-      }
-    }
-    if (b == 0xFF) {
-      ++nff;
-    } else {
-      if (pend >= 0) {
-        out.put(pend);
-        for (int k = 0; k < nff; ++k) out.put(0xFF);
-      }
-      pend = b;
-      nff = 0;
-    }
   }
   MIVC_HD void drain() {
     while (nbits >= 8) {
       const int sh = nbits + 2;
-      const uint32_t v = low >> sh;
-      low &= (1u << sh) - 1u;
+      const uint32_t v = static_cast<uint32_t>(low >> sh);
+      low &= (1ull << sh) - 1ull;
       nbits -= 8;
-      put_byte(v);
+      if (!out.byte9(v)) bad = 1;
     }
   }
-  MIVC_HD void step(uint32_t sym, uint8_t* st, int stride, const uint8_t* lps, const uint8_t* trans) {
+  MIVC_HD void step_nodrain(uint32_t sym, uint8_t* st, int stride, const uint8_t* lps, const uint8_t* trans) {
     const bool dec = !(sym & 0x8000u);
     const bool byp = (sym & 0xC000u) == 0x8000u;
     uint8_t* sp = st + (dec ? (sym & 0x1FFu) : 0u) * static_cast<uint32_t>(stride);
@@ -1084,23 +1065,24 @@ struct CabacSymbolCoder {
     const uint32_t nr = lpsb ? rlps : r1;
     const uint32_t add = lpsb ? r1 : 0u;
     if (dec) {
-      if (lpsb) {
-        mps ^= pst == 0 ? 1 : 0;
-        pst = trans[pst];
-      } else {
-        pst = pst < 62 ? pst + 1 : 62;
-      }
-      *sp = static_cast<uint8_t>((pst << 1) | mps);
+      const int up = pst < 62 ? pst + 1 : 62;
+      const int dn = trans[pst];
+      mps ^= (lpsb && pst == 0) ? 1 : 0;
+      *sp = static_cast<uint8_t>(((lpsb ? dn : up) << 1) | mps);
     }
     const int shd = cabac_clz32(nr) - 23;
     const int n = byp ? static_cast<int>((sym >> 10) & 15u) : (shd > 0 ? shd : 0);
-    low = ((low + add) << n) + (byp ? range * (sym & 0x3FFu) : 0u);
+    low = ((low + add) << n) + (byp ? static_cast<uint64_t>(range) * (sym & 0x3FFu) : 0ull);
     range = byp ? range : (nr << n);
     nbits += n;
+  }
+  MIVC_HD void step(uint32_t sym, uint8_t* st, int stride, const uint8_t* lps, const uint8_t* trans) {
+    step_nodrain(sym, st, stride, lps, trans);
     if (nbits >= 8) drain();
   }
   // EncodeTerminate(1) + EncodeFlush + rbsp_stop_one_bit + alignment (CabacEncoder::terminate)
   MIVC_HD void finish() {
+    drain();
     range -= 2;
     low += range;
     range = 2;
@@ -1116,8 +1098,45 @@ struct CabacSymbolCoder {
       nbits = 8;
       drain();
     }
-    if (pend >= 0) out.put(pend);
-    for (int k = 0; k < nff; ++k) out.put(0xFF);
+    out.finish();
+  }
+};
+
+// Byte output with x264-style carry resolution: the last non-0xFF byte is held back with
+// a count of 0xFF bytes after it until a later byte shows whether a carry reaches them.
+template <class Sink>
+struct CabacPendingOut {
+  Sink sink;  // put(int byte)
+  int pend = -1, nff = 0;
+  MIVC_HD bool byte9(uint32_t v) {
+    const int b = static_cast<int>(v & 0xFFu);
+    bool ok = true;
+    if (v >> 8) {
+      if (pend < 0) ok = false;
+      if (nff > 0) {
+        sink.put(pend + 1);
+        for (int k = 0; k < nff - 1; ++k) sink.put(0);
+        pend = 0;
+        nff = 0;
+      } else {
+        pend += 1;
+      }
+    }
+    if (b == 0xFF) {
+      ++nff;
+    } else {
+      if (pend >= 0) {
+        sink.put(pend);
+        for (int k = 0; k < nff; ++k) sink.put(0xFF);
+      }
+      pend = b;
+      nff = 0;
+    }
+    return ok;
+  }
+  MIVC_HD void finish() {
+    if (pend >= 0) sink.put(pend);
+    for (int k = 0; k < nff; ++k) sink.put(0xFF);
     pend = -1;
     nff = 0;
   }
@@ -1186,10 +1205,13 @@ inline size_t cabac_write_slice_data_symbols(const CabacSliceInfo& si, CabacNb* 
   if (nsyms_out) *nsyms_out = static_cast<int>(total);
   if (total == 0 || syms[total - 1] != 0xC001u) return 0;  // slices end in end_of_slice_flag = 1
   cabac_init_contexts(states, si.slice_type == SLICE_I ? 0 : 1, si.slice_qp);
-  CabacSymbolCoder<CabacBufRef> e;
-  e.out.b = out;
+  CabacSymbolCoder<CabacPendingOut<CabacBufRef>> e;
+  e.out.sink.b = out;
   e.init();
-  for (size_t i = 0; i + 1 < total; ++i) e.step(syms[i], states, 1, &kCabacRangeLPS[0][0], kCabacTransLPS);
+  for (size_t i = 0; i + 1 < total; ++i) {  // drained every 4 symbols, as the GPU coder does
+    e.step_nodrain(syms[i], states, 1, &kCabacRangeLPS[0][0], kCabacTransLPS);
+    if ((i & 3) == 3) e.drain();
+  }
   e.finish();
   return e.bad ? 0 : out->n;
 }

@@ -18,7 +18,7 @@
 //     cabac_alloc   (1, 1024)              slot regions in the pool (scan over slots)
 //     cabac_bins    (nmb/64 x B, 64)       lane per MB: symbols, staged to 16-byte stores
 //   mivc_launch_cabac_code  G frame steps at once (G * B slices: one lane each)
-//     cabac_arith   (G*B/64, 64)           context states in LDS (one column per lane),
+//     cabac_arith   (G*B/lpw, 64)          context states in LDS (one column per lane),
 //                                          header bytes + arithmetic coding, output written
 //                                          in place over the slice's consumed symbols
 //     cabac_compact (G*B, 256)             slice outputs packed back to back
@@ -39,6 +39,8 @@ using h264::MbHeader;
 // symbols reserved in front of every slice's symbols: the slice header bytes are written
 // there, so the in-place output (<= header + 10 bits per symbol) never overtakes the reads
 constexpr int kCabacGap = 64;
+// symbols past a slice's end the arithmetic coder may load (its next-block prefetch)
+constexpr int kArithReadAhead = 160;
 
 struct CabacBinArgs {
   Geom g;
@@ -208,7 +210,7 @@ __global__ __launch_bounds__(1024) void cabac_alloc(CabacBinArgs a) {
   long long sum;
   long long p = block_scan_excl(loc, s_sum, sum);
   const long long start = *a.pool_used;
-  const bool fits = start + sum + 32 <= a.pool_cap;  // + 32: the coder's read-ahead
+  const bool fits = start + sum + kArithReadAhead <= a.pool_cap;  // the coder's read-ahead
   for (int i = i0; i < i1; ++i) {
     a.base[i] = start + p;
     a.total[i] = fits ? a.tot[i] : -1;
@@ -271,6 +273,8 @@ __global__ __launch_bounds__(64) void cabac_bins(CabacBinArgs a) {
 struct CabacCodeArgs {
   int L;                     // slices: G frame steps x B slots (lane l = step * B + slot)
   int B;
+  int lpw;                   // live lanes per wave (the coder is latency-bound: spreading few
+                             // slices over more waves / SIMDs buys throughput)
   uint16_t* pool;
   const long long* base;     // [L]
   const int* total;          // [L]
@@ -284,22 +288,77 @@ struct CabacCodeArgs {
   int* err;
 };
 
-struct InPlaceOut {
-  uint8_t* p;
-  long long n, cap;
-  __device__ void put(int b) {
-    if (n < cap) p[n] = static_cast<uint8_t>(b);
+// Output of one lane's slice: bytes collect in a 256-byte LDS ring and leave as aligned
+// dword stores at block ends, so no global store sits between a symbol block's load and
+// its use (stores count in vmcnt on CDNA: a store inside the coding loop made every
+// prefetch wait drain to vmcnt(0)).  Carries are resolved in the ring: `hold` is the last
+// byte that can still take one (the last non-0xFF arithmetic byte; the 0xFF bytes after it
+// become 0x00), and only bytes before it are flushed.
+struct RingOut {
+  uint8_t* p;          // global slice output (in place over the consumed symbols; 16-byte aligned)
+  uint8_t* ring;       // this lane's LDS ring
+  long long n, flushed, cap;
+  long long arith0;    // first arithmetic byte (after the slice header)
+  long long hold;      // -1 until the first non-0xFF arithmetic byte
+  int ovf;
+  __device__ void start(long long header_bytes) {
+    arith0 = header_bytes;
+    hold = -1;
+  }
+  __device__ void flush_words() {
+    const long long e = (hold >= 0 ? hold : arith0) & ~3ll;
+    for (; flushed < e; flushed += 4) {
+      const uint32_t w = *reinterpret_cast<const uint32_t*>(ring + (flushed & 255));
+      if (flushed + 4 <= cap) *reinterpret_cast<uint32_t*>(p + flushed) = w;
+    }
+  }
+  __device__ void put(int b) {  // slice header bytes
+    ring[n & 255] = static_cast<uint8_t>(b);
     ++n;
+  }
+  __device__ bool byte9(uint32_t v) {
+    if (v >> 8) {
+      if (hold < 0) return false;
+      ring[hold & 255] += 1;
+      for (long long i = hold + 1; i < n; ++i) ring[i & 255] = 0;
+    }
+    if (n - flushed >= 240) flush_words();
+    if (n - flushed >= 256) {  // a 0xFF run longer than the ring: never seen in practice
+      ovf = 1;
+      return false;
+    }
+    const uint32_t b = v & 0xFFu;
+    ring[n & 255] = static_cast<uint8_t>(b);
+    if (b != 0xFFu) hold = n;
+    ++n;
+    return true;
+  }
+  __device__ void finish() {
+    hold = n;  // every byte is final
+    flush_words();
+    for (; flushed < n; ++flushed)
+      if (flushed < cap) p[flushed] = ring[flushed & 255];
   }
 };
 
+constexpr int kArithBlock = 64;         // symbols per lane per block (8 x 16-byte loads)
+constexpr int kArithInStride = 9;       // uint4 per lane in LDS (8 + 1 pad: conflict-free b128 reads)
+constexpr int kArithRingStride = 260;   // bytes per lane ring (256 + 4 pad)
+
+// One lane per slice (a.lpw live lanes per wave).  Per block of 64 symbols: the next block's 8 loads are issued first,
+// the current block is coded from LDS (context states, symbols and output ring are all
+// LDS, so the loop waits only on lgkmcnt), then the next block lands in LDS and the ring's
+// complete dwords are stored.  The only vmcnt wait per block covers loads and stores issued
+// a whole block earlier.
 __global__ __launch_bounds__(64) void cabac_arith(CabacCodeArgs a) {
   __shared__ uint8_t st[h264::kCabacContexts * 64];
   __shared__ uint8_t lps[64 * 4];
   __shared__ uint8_t trans[64];
+  __shared__ uint4 sin[64 * kArithInStride];
+  __shared__ __attribute__((aligned(16))) uint8_t ring[64 * kArithRingStride];
   const int lane = threadIdx.x;
-  const int l = blockIdx.x * 64 + lane;
-  const bool live = l < a.L;
+  const int l = blockIdx.x * a.lpw + lane;
+  const bool live = lane < a.lpw && l < a.L;
   for (int i = lane; i < 256; i += 64) lps[i] = h264::kCabacRangeLPS[i >> 2][i & 3];
   trans[lane] = h264::kCabacTransLPS[lane];
   // context states of this lane's slice (its slice type and QP; cabac_init_idc 0)
@@ -328,26 +387,56 @@ __global__ __launch_bounds__(64) void cabac_arith(CabacCodeArgs a) {
     atomicOr(a.err, 8);
     return;
   }
-  h264::CabacSymbolCoder<InPlaceOut> c;
+  h264::CabacSymbolCoder<RingOut> c;
   c.out.p = reinterpret_cast<uint8_t*>(a.pool + a.base[l]);
+  c.out.ring = ring + lane * kArithRingStride;
   c.out.cap = 2ll * (((static_cast<long long>(total) + kCabacGap + 7) & ~7ll));
-  const int hbytes = a.hdr_nbits[l] >> 3;
-  for (int i = 0; i < hbytes; ++i) c.out.p[i] = static_cast<uint8_t>(a.hdr_bits[l * 16 + (i >> 2)] >> (24 - 8 * (i & 3)));
-  c.out.n = hbytes;
-  c.init();
-  // symbols 8 at a time, the next 8 already in flight
+  c.out.n = c.out.flushed = 0;
+  c.out.ovf = 0;
   const uint4* q = reinterpret_cast<const uint4*>(sy);
-  uint4 cur = q[0], nxt = q[1];
-  const int n = total - 1;  // the last symbol is end_of_slice_flag = 1: finish()
-  for (int i0 = 0; i0 < n; i0 += 8) {
-    const uint32_t w[4] = {cur.x, cur.y, cur.z, cur.w};
-    cur = nxt;
-    nxt = q[(i0 >> 3) + 2];
-    const int m = min(8, n - i0);
+  uint4* my = sin + lane * kArithInStride;
+  {
+    uint4 t[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      if (k < m) c.step((k & 1) ? (w[k >> 1] >> 16) : (w[k >> 1] & 0xFFFFu), st + lane, 64, lps, trans);
+    for (int k = 0; k < 8; ++k) t[k] = q[k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) my[k] = t[k];
+  }
+  const int hbytes = a.hdr_nbits[l] >> 3;
+  for (int i = 0; i < hbytes; ++i) c.out.put(static_cast<uint8_t>(a.hdr_bits[l * 16 + (i >> 2)] >> (24 - 8 * (i & 3))));
+  c.out.start(hbytes);
+  c.init();
+  const int n = total - 1;  // the last symbol is end_of_slice_flag = 1: finish()
+  for (int b0 = 0; b0 < n; b0 += kArithBlock) {
+    // read-ahead (the pool keeps slack past every slice): plain registers, not an array,
+    // so nothing is staged through scratch
+    const uint4* nq = q + (b0 >> 3) + 8;
+    const uint4 n0 = nq[0], n1 = nq[1], n2 = nq[2], n3 = nq[3], n4 = nq[4], n5 = nq[5], n6 = nq[6], n7 = nq[7];
+    const int m = min(kArithBlock, n - b0);
+    for (int ch = 0; ch * 8 < m; ++ch) {
+      const uint4 cw = my[ch];
+      const int mm = min(8, m - ch * 8);
+      // lazy draining: at most 4 symbols (<= 40 bits) between drains (see CabacSymbolCoder)
+      c.step_nodrain(cw.x & 0xFFFFu, st + lane, 64, lps, trans);
+      if (mm > 1) c.step_nodrain(cw.x >> 16, st + lane, 64, lps, trans);
+      if (mm > 2) c.step_nodrain(cw.y & 0xFFFFu, st + lane, 64, lps, trans);
+      if (mm > 3) c.step_nodrain(cw.y >> 16, st + lane, 64, lps, trans);
+      c.drain();
+      if (mm > 4) c.step_nodrain(cw.z & 0xFFFFu, st + lane, 64, lps, trans);
+      if (mm > 5) c.step_nodrain(cw.z >> 16, st + lane, 64, lps, trans);
+      if (mm > 6) c.step_nodrain(cw.w & 0xFFFFu, st + lane, 64, lps, trans);
+      if (mm > 7) c.step_nodrain(cw.w >> 16, st + lane, 64, lps, trans);
+      c.drain();
     }
+    my[0] = n0;
+    my[1] = n1;
+    my[2] = n2;
+    my[3] = n3;
+    my[4] = n4;
+    my[5] = n5;
+    my[6] = n6;
+    my[7] = n7;
+    c.out.flush_words();
   }
   c.finish();
   const bool bad = c.bad || c.out.n > c.out.cap;
@@ -380,6 +469,7 @@ using namespace mivc::gpu;
 
 extern "C" size_t mivc_cabac_nb_bytes() { return sizeof(CabacNb); }
 extern "C" int mivc_cabac_gap() { return kCabacGap; }
+extern "C" int mivc_cabac_read_ahead() { return kArithReadAhead; }
 
 // One frame step's slices -> symbols in the group pool (pool_used advances; base/total
 // describe each slice's region).  Scratch: mask, nb, cnt, off [B, nmb], tot [B].
@@ -441,6 +531,9 @@ extern "C" void mivc_launch_cabac_code(int L, int B, uint16_t* pool, const long 
   a.out_off = out_off;
   a.err = err;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  // full waves: spreading the slices over more, partly empty waves was measured slower
+  // (the coder's issue cycles come out of the concurrently running encode kernels)
+  a.lpw = 64;
   hipLaunchKernelGGL(cabac_arith, dim3((L + 63) / 64), dim3(64), 0, s, a);
   hipLaunchKernelGGL(cabac_compact, dim3(L), dim3(256), 0, s, a);
 }

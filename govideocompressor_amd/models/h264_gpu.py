@@ -123,7 +123,7 @@ class GpuH264Encoder:
     def __init__(self, params: H264Params, slots: int, device: str | torch.device = "cuda",
                  entropy_threads: int | None = None, entropy: str = "gpu", cabac_group: int | None = None):
         """cabac_group: frame steps whose slices the GPU CABAC arithmetic coder runs at once
-        (default 8; its serial stage runs one slice per lane, so throughput scales with it).
+        (default 20; its serial stage runs one slice per lane, so throughput scales with it).
         The symbol pool budget per MB is MIVC_CABAC_SYMS_PER_MB (default 128 per frame step,
         shared by the steps of a group)."""
         if params.width % 2 or params.height % 2:
@@ -215,7 +215,7 @@ class GpuH264Encoder:
         regions / symbol totals, slice headers, output sizes and the compacted bytes."""
         B, nmb, dev = self.B, self.nmb, self.dev
         u8, i32, i64 = torch.uint8, torch.int32, torch.int64
-        G = int(group or os.environ.get("MIVC_CABAC_GROUP", 8))
+        G = int(group or os.environ.get("MIVC_CABAC_GROUP", 20))
         if not 1 <= G <= 64:
             raise ValueError("cabac_group must be in 1..64")
         self.cab_G = G

@@ -1,0 +1,5 @@
+# GPU CABAC check: byte-exactness tests, then the bench at the given group sizes
+set -o pipefail
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_h264.py -k "cabac or entropy or qps" > gpurun_out/t.log 2>&1 || exit 1
+for g in "$@"; do MIVC_CABAC_GROUP=$g timeout -k 10 200 python bench.py --steps 3 --warmup 1 > gpurun_out/b$g.log 2>&1 || exit 1; done
