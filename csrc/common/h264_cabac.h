@@ -905,6 +905,7 @@ struct CabacMbCoder {
   }
 
   MIVC_HD void put_inter_pred(const MbHeader& h, int kind) {
+    if (kind == MBK_BDIRECT) return;  // B_Direct_16x16: no mb_pred (motion is derived)
     const bool bslice = si.slice_type == SLICE_B;
     const CabacParts P = cabac_parts(kind);
     const bool sub8 = P.np == 4;

@@ -69,6 +69,7 @@ py::dict picture_to_dict(const DecodedPicture& p) {
   d["coded_width"] = p.coded_width;
   d["coded_height"] = p.coded_height;
   d["frame_num"] = p.frame_num;
+  d["poc"] = p.poc;
   d["idr"] = p.idr;
   d["slice_type"] = p.slice_type;
   std::vector<uint8_t> i420 = p.cropped_i420();

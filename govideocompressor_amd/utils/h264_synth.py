@@ -195,3 +195,38 @@ def unpack_levels(seg: dict, t: int) -> np.ndarray:
                 j = bit - 18
                 out[mb, 280 + j * 16:280 + (j + 1) * 16] = blk
     return out
+
+
+# ---------------------------------------------------------------- B pictures (temporal direct)
+B16x16, BDIRECT = 9, 13
+
+
+def _trunc_div(a: int, b: int) -> int:
+    """C integer division (rounds toward zero), as the spec's "/" operator."""
+    q = abs(a) // abs(b)
+    return q if (a >= 0) == (b >= 0) else -q
+
+
+def temporal_direct(col_hdr: np.ndarray, poc_cur: int, poc_l0: int, poc_l1: int):
+    """Temporal direct motion (clause 8.4.1.2.3, frame MBs, direct_8x8_inference_flag = 1)
+    for every MB of a B picture whose RefPicList1[0] is the P picture ``col_hdr``
+    ([nmb, 64] MbHeader bytes) and whose RefPicList0[0] is that picture's own reference.
+
+    Returns (mvL0, mvL1) as int [nmb, 4, 2] per 8x8 quadrant; refIdxL0 = refIdxL1 = 0.
+    Co-located intra MBs give mvCol = 0; with direct_8x8_inference the corner 4x4 block of
+    each co-located quadrant supplies mvCol, i.e. that quadrant's MV."""
+    nmb = col_hdr.shape[0]
+    kinds = col_hdr[:, _KIND]
+    mv_col = np.frombuffer(np.ascontiguousarray(col_hdr[:, _MV:_MV + 16]).tobytes(), np.int16).reshape(nmb, 4, 2)
+    mv_col = mv_col.astype(np.int64)
+    intra = np.isin(kinds, [I4x4, I16x16, 4, I8x8])
+    mv_col = np.where(intra[:, None, None], 0, mv_col)
+    tb = int(np.clip(poc_cur - poc_l0, -128, 127))
+    td = int(np.clip(poc_l1 - poc_l0, -128, 127))
+    if td == 0:
+        return mv_col.copy(), np.zeros_like(mv_col)
+    tx = _trunc_div(16384 + abs(_trunc_div(td, 2)), td)
+    dsf = int(np.clip((tb * tx + 32) >> 6, -1024, 1023))
+    mv_l0 = (dsf * mv_col + 128) >> 8
+    mv_l1 = mv_l0 - mv_col
+    return mv_l0, mv_l1
