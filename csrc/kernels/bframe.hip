@@ -1,0 +1,289 @@
+// B-picture motion: temporal direct derivation and the B_16x16 mode decision
+// (x264's default --bframes 3 behind the reference's `-vcodec libx264`, server.go:69-70).
+//
+// The GPU codes B pictures with *temporal* direct prediction (direct_spatial_mv_pred_flag
+// = 0, x264 --direct temporal): the direct motion of a macroblock depends only on the
+// co-located macroblock of RefPicList1[0] and on POC distances (clause 8.4.1.2.3), never
+// on its neighbours in the current picture, so every MB of every slot decides in parallel
+// (spatial direct needs the neighbours' final motion: a raster-order dependency).
+//
+//   b_direct_mv  (thread per MB)   direct MVs per list / 8x8 quadrant + the ME predictors
+//   b_decide     (wave per MB)     candidates B_L0_16x16 / B_L1_16x16 (the two ME searches),
+//                                  B_Bi_16x16 (both ME vectors) and B_Direct_16x16 (B_Skip
+//                                  when no residual survives): luma motion compensation from
+//                                  the anchors' frame-level half-sample planes, 4x4 SATD,
+//                                  cost = SATD + lambda * bits; writes the winner's MbHeader
+//                                  motion fields and its luma prediction for encode_inter.
+#include "kcommon.h"
+
+namespace mivc {
+namespace gpu {
+
+using h264::MbHeader;
+
+constexpr int kHpMargin = 4;  // me_halfpel_planes margin (csrc/kernels/me.hip)
+
+struct BDirectArgs {
+  Geom g;
+  const MbHeader* col;  // [B, nmb] records of RefPicList1[0] (a P anchor)
+  int dsf;              // DistScaleFactor; ignored when direct_copy
+  int direct_copy;      // td == 0: mvL0 = mvCol, mvL1 = 0
+  int16_t* dmv;         // [B, nmb, 2, 4, 2] direct vectors (list, quadrant, xy)
+  int16_t* pm0;         // [B, nmb, 2] ME predictor L0 (mean of the direct vectors)
+  int16_t* pm1;         // [B, nmb, 2] ME predictor L1
+};
+
+__global__ __launch_bounds__(256) void b_direct_mv(BDirectArgs a) {
+  const int mb = blockIdx.x * 256 + threadIdx.x, slot = blockIdx.y;
+  const int nmb = a.g.nmb();
+  if (mb >= nmb) return;
+  const size_t o = static_cast<size_t>(slot) * nmb + mb;
+  const MbHeader& c = a.col[o];
+  const bool intra = h264::mbk_is_intra(c.kind);
+  int v[2][4][2];
+  int s[2][2] = {{0, 0}, {0, 0}};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    // direct_8x8_inference: the corner 4x4 block of co-located quadrant q, i.e. its vector;
+    // a P anchor predicts from list 0 only
+    const int cx = intra || c.ref[0][q] < 0 ? 0 : c.mv[0][q][0];
+    const int cy = intra || c.ref[0][q] < 0 ? 0 : c.mv[0][q][1];
+    int l0x, l0y;
+    if (a.direct_copy) {
+      l0x = cx;
+      l0y = cy;
+    } else {
+      l0x = (a.dsf * cx + 128) >> 8;
+      l0y = (a.dsf * cy + 128) >> 8;
+    }
+    v[0][q][0] = l0x;
+    v[0][q][1] = l0y;
+    v[1][q][0] = a.direct_copy ? 0 : l0x - cx;
+    v[1][q][1] = a.direct_copy ? 0 : l0y - cy;
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+      s[l][0] += v[l][q][0];
+      s[l][1] += v[l][q][1];
+    }
+  }
+  int16_t* d = a.dmv + o * 16;
+#pragma unroll
+  for (int l = 0; l < 2; ++l)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      d[l * 8 + q * 2] = static_cast<int16_t>(v[l][q][0]);
+      d[l * 8 + q * 2 + 1] = static_cast<int16_t>(v[l][q][1]);
+    }
+  a.pm0[o * 2] = static_cast<int16_t>((s[0][0] + 2) >> 2);
+  a.pm0[o * 2 + 1] = static_cast<int16_t>((s[0][1] + 2) >> 2);
+  a.pm1[o * 2] = static_cast<int16_t>((s[1][0] + 2) >> 2);
+  a.pm1[o * 2 + 1] = static_cast<int16_t>((s[1][1] + 2) >> 2);
+}
+
+struct BDecideArgs {
+  Geom g;
+  const uint8_t* src_y;            // [B, H, W]
+  const uint8_t *ref0, *ref1;      // anchors' luma (RefPicList0[0], RefPicList1[0])
+  const uint8_t *hp0, *hp1;        // their b / h / j planes [B, 3, H + 8, W + 8]
+  const int16_t *mv0, *mv1;        // [B, nmb, 2] ME vectors per list
+  const int *cost0, *cost1;        // ME costs (SATD + lambda * mv bits)
+  const uint8_t *pred0, *pred1;    // ME luma predictions [B, nmb, 256]
+  const int16_t *pm0, *pm1;        // ME predictors
+  const int16_t* dmv;              // [B, nmb, 2, 4, 2]
+  const int* qp;                   // [B]
+  const int8_t* aq;                // [B, nmb] (nullable)
+  MbHeader* hdr;                   // out: kind / ref / mv
+  uint8_t* pred_out;               // out: [B, nmb, 256]
+  int* cost_out;                   // out: [B, nmb] the winner's cost (vs the intra estimate)
+};
+
+// Quarter-sample luma position (xf, yf) = two (plane, du, dv) taps averaged (the G/b/h/j
+// form of clause 8.4.2.2.1 used by me.hip): plane 0 = integer samples, 1 = b (half x),
+// 2 = h (half y), 3 = j (centre).
+__constant__ int8_t kQTap[16][2][3] = {
+    {{0, 0, 0}, {0, 0, 0}}, {{0, 0, 0}, {1, 0, 0}}, {{1, 0, 0}, {1, 0, 0}}, {{0, 1, 0}, {1, 0, 0}},
+    {{0, 0, 0}, {2, 0, 0}}, {{1, 0, 0}, {2, 0, 0}}, {{3, 0, 0}, {1, 0, 0}}, {{1, 0, 0}, {2, 1, 0}},
+    {{2, 0, 0}, {2, 0, 0}}, {{3, 0, 0}, {2, 0, 0}}, {{3, 0, 0}, {3, 0, 0}}, {{3, 0, 0}, {2, 1, 0}},
+    {{0, 0, 1}, {2, 0, 0}}, {{1, 0, 1}, {2, 0, 0}}, {{3, 0, 0}, {1, 0, 1}}, {{1, 0, 1}, {2, 1, 0}},
+};
+
+__device__ __forceinline__ uint32_t avg4b(uint32_t a, uint32_t b) { return (a | b) - (((a ^ b) >> 1) & 0x7F7F7F7Fu); }
+
+// 4 consecutive samples (u .. u+3, v) of one plane; coordinates clamp to the plane's
+// extension (integer plane: the picture; half-sample planes: their 4-sample margin)
+__device__ __forceinline__ uint32_t plane4(const uint8_t* G, const uint8_t* hp, int W, int H, int pl, int u, int v) {
+  const uint8_t* row;
+  int lo, hi, base;
+  if (pl == 0) {
+    row = G + static_cast<size_t>(clampi(v, 0, H - 1)) * W;
+    lo = 0;
+    hi = W - 1;
+    base = 0;
+  } else {
+    const int PW = W + 2 * kHpMargin, PH = H + 2 * kHpMargin;
+    row = hp + static_cast<size_t>(pl - 1) * PW * PH +
+          static_cast<size_t>(clampi(v, -kHpMargin, H + kHpMargin - 1) + kHpMargin) * PW;
+    lo = -kHpMargin;
+    hi = W + kHpMargin - 1;
+    base = kHpMargin;
+  }
+  const int x = u + base, a = x & ~3;
+  if (u >= lo && u + 3 <= hi && a + 8 <= hi + base + 1) {
+    const uint32_t w0 = *reinterpret_cast<const uint32_t*>(row + a);
+    const uint32_t w1 = *reinterpret_cast<const uint32_t*>(row + a + 4);
+    return __builtin_amdgcn_alignbyte(w1, w0, x & 3);
+  }
+  uint32_t w = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) w |= static_cast<uint32_t>(row[clampi(u + k, lo, hi) + base]) << (8 * k);
+  return w;
+}
+
+// predicted samples (x .. x+3, y) of a 16x16 block displaced by the quarter-sample vector
+__device__ __forceinline__ uint32_t mc4(const uint8_t* G, const uint8_t* hp, int W, int H, int x, int y, int mvx,
+                                        int mvy) {
+  const int q = (mvy & 3) * 4 + (mvx & 3);
+  const int xi = x + (mvx >> 2), yi = y + (mvy >> 2);
+  const uint32_t A = plane4(G, hp, W, H, kQTap[q][0][0], xi + kQTap[q][0][1], yi + kQTap[q][0][2]);
+  const uint32_t Bv = plane4(G, hp, W, H, kQTap[q][1][0], xi + kQTap[q][1][1], yi + kQTap[q][1][2]);
+  return avg4b(A, Bv);
+}
+
+__device__ __forceinline__ int mvbits_se(int v) {
+  const uint32_t x = (v <= 0 ? static_cast<uint32_t>(-2 * v) : static_cast<uint32_t>(2 * v - 1)) + 1u;
+  return 2 * (31 - __clz(x)) + 1;
+}
+
+// One wave per MB: lane = (row lane >> 2, columns 4 * (lane & 3) .. +3).
+__global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
+  const Geom& g = a.g;
+  const int nmb = g.nmb();
+  const int mb = blockIdx.x, slot = blockIdx.y;
+  const int lane = threadIdx.x;
+  const size_t o = static_cast<size_t>(slot) * nmb + mb;
+  const int mx = mb % g.wmb, my = mb / g.wmb;
+  const int W = g.W, H = g.H;
+  const int r = lane >> 2, c0 = (lane & 3) * 4;
+  const int X = mx * 16 + c0, Y = my * 16 + r;
+  const int q = (r >> 3) * 2 + (c0 >> 3);  // 8x8 quadrant of this lane's samples
+  const size_t yo = static_cast<size_t>(slot) * g.ysize();
+  const size_t ho = static_cast<size_t>(slot) * 3 * (W + 2 * kHpMargin) * (H + 2 * kHpMargin);
+  const uint8_t *G0 = a.ref0 + yo, *G1 = a.ref1 + yo, *H0 = a.hp0 + ho, *H1 = a.hp1 + ho;
+  const int16_t* dm = a.dmv + o * 16;
+  const int m0x = a.mv0[o * 2], m0y = a.mv0[o * 2 + 1], m1x = a.mv1[o * 2], m1y = a.mv1[o * 2 + 1];
+  const uint32_t src = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y) * W + X);
+  // direct: per-quadrant vectors of both lists; bi: the two ME vectors
+  const uint32_t pd = avg4b(mc4(G0, H0, W, H, X, Y, dm[q * 2], dm[q * 2 + 1]),
+                            mc4(G1, H1, W, H, X, Y, dm[8 + q * 2], dm[8 + q * 2 + 1]));
+  const uint32_t pb = avg4b(mc4(G0, H0, W, H, X, Y, m0x, m0y), mc4(G1, H1, W, H, X, Y, m1x, m1y));
+  __shared__ int s_res[2][256];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int sv = static_cast<int>((src >> (8 * k)) & 255u);
+    s_res[0][r * 16 + c0 + k] = sv - static_cast<int>((pd >> (8 * k)) & 255u);
+    s_res[1][r * 16 + c0 + k] = sv - static_cast<int>((pb >> (8 * k)) & 255u);
+  }
+  wave_sync();
+  int satd = 0;
+  if (lane < 32) {
+    const int cand = lane >> 4, blk = lane & 15, bx = (blk & 3) * 4, by = (blk >> 2) * 4;
+    int rr[16];
+#pragma unroll
+    for (int y = 0; y < 4; ++y)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) rr[y * 4 + x] = s_res[cand][(by + y) * 16 + bx + x];
+    satd = h264::satd4x4(rr);
+  }
+  satd = sum16(satd);
+  const int satd_direct = __builtin_amdgcn_readlane(satd, 0), satd_bi = __builtin_amdgcn_readlane(satd, 16);
+  const int qp = clampi(a.qp[slot] + (a.aq ? a.aq[o] : 0), 0, 51);
+  const int lambda = h264::kLambda[qp];
+  // mb_type / motion bits (CABAC-ish): direct "0"; L0 / L1 "10x"; Bi "110000" + two mvds
+  const int c_direct = satd_direct + lambda * 1;
+  const int c_l0 = a.cost0[o] + lambda * 3;
+  const int c_l1 = a.cost1[o] + lambda * 3;
+  const int c_bi = satd_bi + lambda * (6 + mvbits_se(m0x - a.pm0[o * 2]) + mvbits_se(m0y - a.pm0[o * 2 + 1]) +
+                                       mvbits_se(m1x - a.pm1[o * 2]) + mvbits_se(m1y - a.pm1[o * 2 + 1]));
+  int mode = 0, best = c_direct;  // 0 direct, 1 L0, 2 L1, 3 Bi
+  if (c_l0 < best) { mode = 1; best = c_l0; }
+  if (c_l1 < best) { mode = 2; best = c_l1; }
+  if (c_bi < best) { mode = 3; best = c_bi; }
+  uint32_t pw;
+  if (mode == 0) pw = pd;
+  else if (mode == 3) pw = pb;
+  else pw = *reinterpret_cast<const uint32_t*>((mode == 1 ? a.pred0 : a.pred1) + o * 256 + r * 16 + c0);
+  *reinterpret_cast<uint32_t*>(a.pred_out + o * 256 + r * 16 + c0) = pw;
+  if (lane == 0) {
+    MbHeader* h = a.hdr + o;
+    h->kind = mode == 0 ? h264::MBK_BDIRECT : h264::MBK_B16x16;
+    h->sub_direct = 0;
+    const bool u0 = mode != 2, u1 = mode != 1;
+    const uint32_t r0 = u0 ? 0u : 0xFFFFFFFFu, r1 = u1 ? 0u : 0xFFFFFFFFu;
+    *reinterpret_cast<uint2*>(&h->ref[0][0]) = make_uint2(r0, r1);
+    uint32_t w[2][4];
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
+      if (mode == 0) {
+        x0 = dm[qq * 2]; y0 = dm[qq * 2 + 1]; x1 = dm[8 + qq * 2]; y1 = dm[8 + qq * 2 + 1];
+      } else {
+        if (u0) { x0 = m0x; y0 = m0y; }
+        if (u1) { x1 = m1x; y1 = m1y; }
+      }
+      w[0][qq] = (static_cast<uint32_t>(x0) & 0xFFFFu) | (static_cast<uint32_t>(y0) << 16);
+      w[1][qq] = (static_cast<uint32_t>(x1) & 0xFFFFu) | (static_cast<uint32_t>(y1) << 16);
+    }
+    uint4* mvp = reinterpret_cast<uint4*>(&h->mv[0][0][0]);  // 16-byte aligned
+    mvp[0] = make_uint4(w[0][0], w[0][1], w[0][2], w[0][3]);
+    mvp[1] = make_uint4(w[1][0], w[1][1], w[1][2], w[1][3]);
+    a.cost_out[o] = best;
+  }
+}
+
+}  // namespace gpu
+}  // namespace mivc
+
+using namespace mivc::gpu;
+
+extern "C" void mivc_launch_b_direct(int B, int wmb, int hmb, const void* col, int dsf, int direct_copy, int16_t* dmv,
+                                     int16_t* pm0, int16_t* pm1, void* stream) {
+  BDirectArgs a;
+  a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
+  a.col = static_cast<const MbHeader*>(col);
+  a.dsf = dsf;
+  a.direct_copy = direct_copy;
+  a.dmv = dmv;
+  a.pm0 = pm0;
+  a.pm1 = pm1;
+  hipLaunchKernelGGL(b_direct_mv, dim3((wmb * hmb + 255) / 256, B), dim3(256), 0, static_cast<hipStream_t>(stream), a);
+}
+
+extern "C" void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref0,
+                                     const uint8_t* ref1, const uint8_t* hp0, const uint8_t* hp1, const int16_t* mv0,
+                                     const int16_t* mv1, const int* cost0, const int* cost1, const uint8_t* pred0,
+                                     const uint8_t* pred1, const int16_t* pm0, const int16_t* pm1, const int16_t* dmv,
+                                     const int* qp, const int8_t* aq, void* hdr, uint8_t* pred_out, int* cost_out,
+                                     void* stream) {
+  BDecideArgs a;
+  a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
+  a.src_y = src_y;
+  a.ref0 = ref0;
+  a.ref1 = ref1;
+  a.hp0 = hp0;
+  a.hp1 = hp1;
+  a.mv0 = mv0;
+  a.mv1 = mv1;
+  a.cost0 = cost0;
+  a.cost1 = cost1;
+  a.pred0 = pred0;
+  a.pred1 = pred1;
+  a.pm0 = pm0;
+  a.pm1 = pm1;
+  a.dmv = dmv;
+  a.qp = qp;
+  a.aq = aq;
+  a.hdr = static_cast<MbHeader*>(hdr);
+  a.pred_out = pred_out;
+  a.cost_out = cost_out;
+  hipLaunchKernelGGL(b_decide, dim3(wmb * hmb, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
+}

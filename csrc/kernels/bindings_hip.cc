@@ -19,7 +19,14 @@ void mivc_launch_rgb_to_i420(const uint8_t* rgb, int w, int h, int nframes, uint
                              void* stream);
 void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref_y, const int16_t* pred_mv,
                     int16_t* out_mv, int* out_cost, uint8_t* out_pred, int* out_intra_cost, const int* qp, int range,
-                    int subpel, uint8_t* hp, const int8_t* aq, void* stream);
+                    int subpel, uint8_t* hp, const int8_t* aq, int planes_ready, void* stream);
+void mivc_launch_b_direct(int B, int wmb, int hmb, const void* col, int dsf, int direct_copy, int16_t* dmv,
+                          int16_t* pm0, int16_t* pm1, void* stream);
+void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref0, const uint8_t* ref1,
+                          const uint8_t* hp0, const uint8_t* hp1, const int16_t* mv0, const int16_t* mv1,
+                          const int* cost0, const int* cost1, const uint8_t* pred0, const uint8_t* pred1,
+                          const int16_t* pm0, const int16_t* pm1, const int16_t* dmv, const int* qp, const int8_t* aq,
+                          void* hdr, uint8_t* pred_out, int* cost_out, void* stream);
 void mivc_launch_aq_offsets(int B, int wmb, int hmb, const uint8_t* sy, const uint8_t* su, const uint8_t* sv,
                             float strength, const float* extra, long long extra_stride, int8_t* out, void* stream);
 void mivc_launch_mbtree(int B, int F, int lbw, int lbh, const int* blk_cost, const int* blk_mv, float* prop,
@@ -32,7 +39,8 @@ void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t* src_y, con
                               uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const uint8_t* pred_y,
                               const int16_t* mv, const int* me_cost, const int* intra_cost, const int* qp,
                               int chroma_qp_offset, void* hdr, int16_t* coef, uint8_t* nz, uint8_t* intra_flag,
-                              int* intra_count, const int8_t* aq, void* stream);
+                              int* intra_count, const int8_t* aq, const uint8_t* ref1_u, const uint8_t* ref1_v,
+                              int bmode, void* stream);
 void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* src_u,
                               const uint8_t* src_v, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const int* qp,
                               int chroma_qp_offset, void* hdr, int16_t* coef, uint8_t* nz,
@@ -113,13 +121,29 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("me", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref, uintptr_t pred_mv, uintptr_t out_mv,
                  uintptr_t out_cost, uintptr_t out_pred, uintptr_t out_intra, uintptr_t qp, int range, int subpel,
-                 uintptr_t stream, uintptr_t hp, uintptr_t aq) {
+                 uintptr_t stream, uintptr_t hp, uintptr_t aq, int planes_ready) {
+    if (planes_ready && !hp) throw std::invalid_argument("me: planes_ready needs the hp buffer");
     mivc_launch_me(B, wmb, hmb, P<uint8_t>(src), P<uint8_t>(ref), P<int16_t>(pred_mv), P<int16_t>(out_mv),
                    P<int>(out_cost), P<uint8_t>(out_pred), P<int>(out_intra), P<int>(qp), range, subpel,
-                   P<uint8_t>(hp), P<int8_t>(aq), S(stream));
+                   P<uint8_t>(hp), P<int8_t>(aq), planes_ready, S(stream));
   }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("src"), py::arg("ref"), py::arg("pred_mv"),
      py::arg("out_mv"), py::arg("out_cost"), py::arg("out_pred"), py::arg("out_intra"), py::arg("qp"),
-     py::arg("range"), py::arg("subpel"), py::arg("stream"), py::arg("hp") = 0, py::arg("aq") = 0);
+     py::arg("range"), py::arg("subpel"), py::arg("stream"), py::arg("hp") = 0, py::arg("aq") = 0,
+     py::arg("planes_ready") = 0);
+  m.def("b_direct", [](int B, int wmb, int hmb, uintptr_t col, int dsf, int direct_copy, uintptr_t dmv, uintptr_t pm0,
+                       uintptr_t pm1, uintptr_t stream) {
+    mivc_launch_b_direct(B, wmb, hmb, P<void>(col), dsf, direct_copy, P<int16_t>(dmv), P<int16_t>(pm0),
+                         P<int16_t>(pm1), S(stream));
+  });
+  m.def("b_decide", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref0, uintptr_t ref1, uintptr_t hp0,
+                       uintptr_t hp1, uintptr_t mv0, uintptr_t mv1, uintptr_t cost0, uintptr_t cost1, uintptr_t pred0,
+                       uintptr_t pred1, uintptr_t pm0, uintptr_t pm1, uintptr_t dmv, uintptr_t qp, uintptr_t aq,
+                       uintptr_t hdr, uintptr_t pred_out, uintptr_t cost_out, uintptr_t stream) {
+    mivc_launch_b_decide(B, wmb, hmb, P<uint8_t>(src), P<uint8_t>(ref0), P<uint8_t>(ref1), P<uint8_t>(hp0),
+                         P<uint8_t>(hp1), P<int16_t>(mv0), P<int16_t>(mv1), P<int>(cost0), P<int>(cost1),
+                         P<uint8_t>(pred0), P<uint8_t>(pred1), P<int16_t>(pm0), P<int16_t>(pm1), P<int16_t>(dmv),
+                         P<int>(qp), P<int8_t>(aq), P<void>(hdr), P<uint8_t>(pred_out), P<int>(cost_out), S(stream));
+  });
   m.def("aq_offsets", [](int B, int wmb, int hmb, uintptr_t sy, uintptr_t su, uintptr_t sv, float strength,
                          uintptr_t out, uintptr_t stream, uintptr_t extra, long long extra_stride) {
     mivc_launch_aq_offsets(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), strength, P<float>(extra),
@@ -143,16 +167,20 @@ PYBIND11_MODULE(_hip, m) {
         [](int B, int wmb, int hmb, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t fy, uintptr_t fu,
            uintptr_t fv, uintptr_t ry, uintptr_t ru, uintptr_t rv, uintptr_t pred, uintptr_t mv, uintptr_t me_cost,
            uintptr_t intra_cost, uintptr_t qp, int cqo, uintptr_t hdr, uintptr_t coef, uintptr_t nz,
-           uintptr_t intra_flag, uintptr_t intra_count, uintptr_t stream, uintptr_t aq) {
+           uintptr_t intra_flag, uintptr_t intra_count, uintptr_t stream, uintptr_t aq, uintptr_t ref1_u,
+           uintptr_t ref1_v, int bmode) {
+          if (bmode && (!ref1_u || !ref1_v)) throw std::invalid_argument("encode_inter: B mode needs the list-1 chroma");
           mivc_launch_encode_inter(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), P<uint8_t>(fy),
                                    P<uint8_t>(fu), P<uint8_t>(fv), P<uint8_t>(ry), P<uint8_t>(ru), P<uint8_t>(rv),
                                    P<uint8_t>(pred), P<int16_t>(mv), P<int>(me_cost), P<int>(intra_cost), P<int>(qp),
                                    cqo, P<void>(hdr), P<int16_t>(coef), P<uint8_t>(nz), P<uint8_t>(intra_flag),
-                                   P<int>(intra_count), P<int8_t>(aq), S(stream));
+                                   P<int>(intra_count), P<int8_t>(aq), P<uint8_t>(ref1_u), P<uint8_t>(ref1_v), bmode,
+                                   S(stream));
         }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("sy"), py::arg("su"), py::arg("sv"), py::arg("fy"),
         py::arg("fu"), py::arg("fv"), py::arg("ry"), py::arg("ru"), py::arg("rv"), py::arg("pred"), py::arg("mv"),
         py::arg("me_cost"), py::arg("intra_cost"), py::arg("qp"), py::arg("cqo"), py::arg("hdr"), py::arg("coef"),
-        py::arg("nz"), py::arg("intra_flag"), py::arg("intra_count"), py::arg("stream"), py::arg("aq") = 0);
+        py::arg("nz"), py::arg("intra_flag"), py::arg("intra_count"), py::arg("stream"), py::arg("aq") = 0,
+        py::arg("ref1_u") = 0, py::arg("ref1_v") = 0, py::arg("bmode") = 0);
   m.def("encode_intra", [](int B, int wmb, int hmb, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t ry,
                            uintptr_t ru, uintptr_t rv, uintptr_t qp, int cqo, uintptr_t hdr, uintptr_t coef,
                            uintptr_t nz, uintptr_t intra_flag, uintptr_t intra_count, uintptr_t err, int use_i4x4,

@@ -232,9 +232,23 @@ __global__ __launch_bounds__(64 * kDeblockWaves) void deblock_wavefront(DeblockA
             else if (iq || ip) bs = 3;
             else if (nzbp[rp] || nzb0[rq]) bs = 2;
             else {
+              // bS 1: different reference pictures / number of vectors, or a vector component
+              // differing by >= 4 quarter samples (clause 8.7.2.1).  Reference identity is
+              // (list, ref_idx): the encoder's lists hold disjoint pictures (past anchors in
+              // list 0, the future anchor in list 1), and the GPU decode path takes P only.
               const int qp_ = ((rp >> 3) & 1) * 2 + ((rp & 3) >> 1), qq_ = ((rq >> 3) & 1) * 2 + ((rq & 3) >> 1);
-              const int dx = HP->mv[0][qp_][0] - HQ->mv[0][qq_][0], dy = HP->mv[0][qp_][1] - HQ->mv[0][qq_][1];
-              bs = (dx >= 4 || dx <= -4 || dy >= 4 || dy <= -4) ? 1 : 0;
+              bool diff = false;
+#pragma unroll
+              for (int l = 0; l < 2; ++l) {
+                const int fp = HP->ref[l][qp_], fq = HQ->ref[l][qq_];
+                if ((fp >= 0) != (fq >= 0) || (fp >= 0 && fp != fq)) {
+                  diff = true;
+                } else if (fp >= 0) {
+                  const int dx = HP->mv[l][qp_][0] - HQ->mv[l][qq_][0], dy = HP->mv[l][qp_][1] - HQ->mv[l][qq_][1];
+                  diff |= dx >= 4 || dx <= -4 || dy >= 4 || dy <= -4;
+                }
+              }
+              bs = diff ? 1 : 0;
             }
           }
           S.bs[dir][e][k] = bs;

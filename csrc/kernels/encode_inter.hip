@@ -33,7 +33,46 @@ struct InterArgs {
   uint8_t* nz;             // [B, nmb, 16] luma nonzero flags (raster 4x4)
   uint8_t* intra_flag;     // [B, nmb]
   int* intra_count;        // [B]
+  // B pictures (bmode): the motion of every MB is already in hdr (kind / ref / mv per
+  // quadrant, written by b_decide); chroma predicts from ref (list 0) and / or ref1
+  // (list 1), averaged for bi-prediction; pred_y is b_decide's luma prediction
+  const uint8_t *ref1_u, *ref1_v;
+  int bmode;
 };
+
+// Eighth-sample chroma prediction (clause 8.4.2.2.2) of a 4x4 block at (px0, py0) of a
+// cw x ch plane with vector (mvx, mvy) (quarter-luma = eighth-chroma units).
+__device__ __forceinline__ void chroma_mc4x4(const uint8_t* refc, int cw, int CH, int px0, int py0, int mvx, int mvy,
+                                             int (&pv)[4][4]) {
+  const int xf = mvx & 7, yf = mvy & 7;
+  const int xi = px0 + (mvx >> 3), yi = py0 + (mvy >> 3);
+  int rw[5][5];  // reference samples (rows yi..yi+4, cols xi..xi+4), edge-clamped
+  if (xi >= 0 && xi + 8 <= cw && yi >= 0 && yi + 5 <= CH) {
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      const uint8_t* row = refc + static_cast<size_t>(yi + r) * cw;
+      const int a = xi & ~3;
+      const uint32_t w0 = *reinterpret_cast<const uint32_t*>(row + a), w1 = *reinterpret_cast<const uint32_t*>(row + a + 4);
+      const uint32_t w4 = __builtin_amdgcn_alignbyte(w1, w0, xi & 3), w5 = row[xi + 4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) rw[r][c] = __builtin_amdgcn_ubfe(w4, 8 * c, 8);
+      rw[r][4] = w5;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      const uint8_t* row = refc + static_cast<size_t>(clampi(yi + r, 0, CH - 1)) * cw;
+#pragma unroll
+      for (int c = 0; c < 5; ++c) rw[r][c] = row[clampi(xi + c, 0, cw - 1)];
+    }
+  }
+  const int wA = (8 - xf) * (8 - yf), wB = xf * (8 - yf), wC = (8 - xf) * yf, wD = xf * yf;
+#pragma unroll
+  for (int y = 0; y < 4; ++y)
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+      pv[y][x] = (wA * rw[y][x] + wB * rw[y][x + 1] + wC * rw[y + 1][x] + wD * rw[y + 1][x + 1] + 32) >> 6;
+}
 
 // x264 decimate_score of a 4x4 block in scan order (start..15), branch-free: 9 if any
 // |level| > 1, else the sum over non-zero levels of kTab[zeros between it and the
@@ -97,7 +136,7 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
   __shared__ int s_clev[2][2][4];
   __shared__ int s_flags[2][2];  // [half][0] luma 8x8 keep mask, [1] chroma AC keep mask (bit per comp)
 
-  const int mvx = a.mv[o * 2], mvy = a.mv[o * 2 + 1];
+  const int mvx = a.bmode ? 0 : a.mv[o * 2], mvy = a.bmode ? 0 : a.mv[o * 2 + 1];
   const bool go_intra = a.intra_cost[o] < a.me_cost[o];
   MbHeader* h = a.hdr + o;
   int16_t* coef = a.coef + o * h264::kCoefPerMb;
@@ -144,41 +183,31 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
   } else if (work && hl < 24) {
     // ---- chroma block: eighth-sample MC (clause 8.4.2.2.2) + residual + forward + AC quant
     const uint8_t* srcc = (comp == 0 ? a.src_u : a.src_v) + slot * g.csize();
-    const uint8_t* refc = (comp == 0 ? a.ref_u : a.ref_v) + slot * g.csize();
-    const int xf = mvx & 7, yf = mvy & 7;
     const int px0 = mx * 8 + cbx, py0 = my * 8 + cby;
-    const int xi = px0 + (mvx >> 3), yi = py0 + (mvy >> 3);
-    int rw[5][5];  // reference samples (rows yi..yi+4, cols xi..xi+4), edge-clamped
-    if (xi >= 0 && xi + 8 <= cw && yi >= 0 && yi + 5 <= CH) {
-#pragma unroll
-      for (int r = 0; r < 5; ++r) {
-        const uint8_t* row = refc + static_cast<size_t>(yi + r) * cw;
-        const uint32_t w4 = ld4(row, xi), w5 = row[xi + 4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) rw[r][c] = __builtin_amdgcn_ubfe(w4, 8 * c, 8);
-        rw[r][4] = w5;
-      }
+    int pv[4][4];
+    if (!a.bmode) {
+      chroma_mc4x4((comp == 0 ? a.ref_u : a.ref_v) + slot * g.csize(), cw, CH, px0, py0, mvx, mvy, pv);
     } else {
+      // the 4x4 chroma block cb covers luma quadrant cb: its lists and vectors
+      const bool u0 = h->ref[0][cb] >= 0, u1 = h->ref[1][cb] >= 0;
+      int p1[4][4];
+      if (u0) chroma_mc4x4((comp == 0 ? a.ref_u : a.ref_v) + slot * g.csize(), cw, CH, px0, py0, h->mv[0][cb][0],
+                           h->mv[0][cb][1], pv);
+      if (u1) chroma_mc4x4((comp == 0 ? a.ref1_u : a.ref1_v) + slot * g.csize(), cw, CH, px0, py0,
+                           h->mv[1][cb][0], h->mv[1][cb][1], p1);
 #pragma unroll
-      for (int r = 0; r < 5; ++r) {
-        const uint8_t* row = refc + static_cast<size_t>(clampi(yi + r, 0, CH - 1)) * cw;
+      for (int y = 0; y < 4; ++y)
 #pragma unroll
-        for (int c = 0; c < 5; ++c) rw[r][c] = row[clampi(xi + c, 0, cw - 1)];
-      }
+        for (int x = 0; x < 4; ++x) pv[y][x] = u0 ? (u1 ? (pv[y][x] + p1[y][x] + 1) >> 1 : pv[y][x]) : p1[y][x];
     }
     uint32_t sw[4];
 #pragma unroll
     for (int y = 0; y < 4; ++y) sw[y] = *reinterpret_cast<const uint32_t*>(srcc + static_cast<size_t>(py0 + y) * cw + px0);
-    const int wA = (8 - xf) * (8 - yf), wB = xf * (8 - yf), wC = (8 - xf) * yf, wD = xf * yf;
 #pragma unroll
     for (int y = 0; y < 4; ++y) {
-      int pv[4];
 #pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        pv[x] = (wA * rw[y][x] + wB * rw[y][x + 1] + wC * rw[y + 1][x] + wD * rw[y + 1][x + 1] + 32) >> 6;
-        res[y * 4 + x] = static_cast<int>(__builtin_amdgcn_ubfe(sw[y], 8 * x, 8)) - pv[x];
-      }
-      prw[y] = pack4_u8(pv);
+      for (int x = 0; x < 4; ++x) res[y * 4 + x] = static_cast<int>(__builtin_amdgcn_ubfe(sw[y], 8 * x, 8)) - pv[y][x];
+      prw[y] = pack4_u8(pv[y]);
     }
     h264::forward_core4x4(res);
     s_cdc[half][comp][cb] = res[0];
@@ -292,16 +321,17 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
     // luma DC (unused for P16x16): zero
     reinterpret_cast<uint4*>(coef + h264::COEF_LUMA_DC)[hl - 25] = make_uint4(0, 0, 0, 0);
   } else if (hl == 27) {
-    h->kind = h264::MBK_P16x16;
     h->qp = static_cast<int8_t>(qp);
     h->i16_mode = 0;
     h->chroma_mode = 0;
     h->flags = 0;
+    a.intra_flag[o] = 0;
+    if (a.bmode) return;  // kind / ref / mv are b_decide's
+    h->kind = h264::MBK_P16x16;
     const uint32_t mvw = (static_cast<uint32_t>(mvx) & 0xFFFFu) | (static_cast<uint32_t>(mvy) << 16);
     uint4* mvp = reinterpret_cast<uint4*>(&h->mv[0][0][0]);  // 16-byte aligned
     mvp[0] = make_uint4(mvw, mvw, mvw, mvw);
     *reinterpret_cast<uint2*>(&h->ref[0][0]) = make_uint2(0u, 0xFFFFFFFFu);  // L0 ref 0, L1 unused
-    a.intra_flag[o] = 0;
   }
 }
 
@@ -316,7 +346,8 @@ extern "C" void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t*
                                          const uint8_t* pred_y, const int16_t* mv, const int* me_cost,
                                          const int* intra_cost, const int* qp, int chroma_qp_offset, void* hdr,
                                          int16_t* coef, uint8_t* nz, uint8_t* intra_flag, int* intra_count,
-                                         const int8_t* aq, void* stream) {
+                                         const int8_t* aq, const uint8_t* ref1_u, const uint8_t* ref1_v, int bmode,
+                                         void* stream) {
   InterArgs a;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.src_y = src_y;
@@ -340,5 +371,8 @@ extern "C" void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t*
   a.intra_flag = intra_flag;
   a.intra_count = intra_count;
   a.aq = aq;
+  a.ref1_u = ref1_u;
+  a.ref1_v = ref1_v;
+  a.bmode = bmode;
   hipLaunchKernelGGL(encode_inter_mb, dim3((wmb * hmb + 1) / 2, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
 }

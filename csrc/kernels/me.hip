@@ -661,9 +661,11 @@ extern "C" void mivc_launch_me_halfpel(int B, int W, int H, const uint8_t* ref_y
 extern "C" void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref_y,
                                const int16_t* pred_mv, int16_t* out_mv, int* out_cost, uint8_t* out_pred,
                                int* out_intra_cost, const int* qp, int range, int subpel, uint8_t* hp_buf,
-                               const int8_t* aq, void* stream) {
+                               const int8_t* aq, int planes_ready, void* stream) {
   // hp_buf: caller-owned [B, 3, H + 8, W + 8] (+64 bytes slack) half-sample plane scratch,
   // resident across frames; nullptr -> stream-ordered scratch for this call only.
+  // planes_ready: hp_buf already holds ref_y's planes (an anchor's planes are built once
+  // and shared by the P picture and the B pictures that reference it).
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int W = wmb * 16, H = hmb * 16;
   uint8_t* hp = hp_buf;
@@ -675,7 +677,7 @@ extern "C" void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, co
       abort();
     }
   }
-  mivc_launch_me_halfpel(B, W, H, ref_y, hp, stream);
+  if (!(planes_ready && hp_buf)) mivc_launch_me_halfpel(B, W, H, ref_y, hp, stream);
   MeArgs a;
   a.g = Geom{B, wmb, hmb, W, H};
   a.src_y = src_y;

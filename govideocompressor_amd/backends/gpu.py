@@ -204,10 +204,12 @@ class GpuBackend:
         if hasattr(enc, "encode") and type(params).__name__ == "HevcParams":
             res = enc.encode(dy, du, dv)
         else:
-            res = enc.encode(dy, du, dv, idr_ids=[idr_id(key, un_) for key, un_, _, _ in chunk])
+            # a short segment (padded to F frames) must end on an anchor to be cut there
+            res = enc.encode(dy, du, dv, idr_ids=[idr_id(key, un_) for key, un_, _, _ in chunk],
+                             anchors_at=sorted({c - 1 for _, _, _, c in chunk}))
         tm.add("encode_s", time.perf_counter() - t1)
         ps = enc.parameter_sets()
-        return [(key, un_, ps + b"".join(res[b].nals[:c]), res[b].psnr_y, getattr(res[b], "ssim_y", 0.0))
+        return [(key, un_, ps + b"".join(res[b].display_prefix(c)), res[b].psnr_y, getattr(res[b], "ssim_y", 0.0))
                 for b, (key, un_, s, c) in enumerate(chunk)]
 
     def close(self):

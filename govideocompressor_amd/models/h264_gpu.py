@@ -62,14 +62,24 @@ class H264Params:
     mbtree: bool = True
     # entropy coder: CABAC (x264's default; Main profile) or CAVLC (Constrained Baseline)
     cabac: bool = True
+    # x264 --bframes 3: B pictures between P anchors (non-reference, temporal direct); CABAC
+    # only (the Baseline CAVLC path has no B slices).  b_qp_offset: x264 --pbratio 1.3
+    bframes: int = 3
+    b_qp_offset: int = 2
+
+    def eff_bframes(self) -> int:
+        return max(0, int(self.bframes)) if self.cabac else 0
 
     def host_cfg(self) -> dict:
         return dict(width=self.width, height=self.height, fps=self.fps, qp=self.qp,
                     deblock=int(self.deblock), chroma_qp_offset=self.chroma_qp_offset,
-                    vui=int(self.vui), cabac=int(self.cabac))
+                    vui=int(self.vui), cabac=int(self.cabac), bframes=self.eff_bframes())
 
     def profile_name(self) -> str:
-        return "Main CABAC" if self.cabac else "Constrained Baseline CAVLC"
+        if not self.cabac:
+            return "Constrained Baseline CAVLC"
+        nb = self.eff_bframes()
+        return "Main CABAC" + (f" {nb}B temporal-direct" if nb else "")
 
     def frame_qps(self) -> tuple[int, int]:
         """(qp_I, qp_P).  CRF maps to the P-frame QP (x264 scale without MB-tree);
@@ -79,21 +89,79 @@ class H264Params:
         return max(0, qp_p - self.ip_offset), qp_p
 
 
+@dataclass(frozen=True)
+class PicPlan:
+    """One picture of a closed GOP in coding order."""
+    d: int          # display index
+    kind: str       # "I", "P" or "B"
+    frame_num: int
+    poc: int        # PicOrderCnt (2 * display index)
+    anchor: int     # I / P: anchor ordinal (its recon / half-sample buffer is anchor & 1); B: -1
+    l0: int = -1    # display index of RefPicList0[0] (P, B)
+    l1: int = -1    # display index of RefPicList1[0] (B)
+    l1_anchor: int = -1  # B: anchor ordinal of RefPicList1[0]
+
+    @property
+    def slice_type(self) -> int:  # SliceType (csrc/common/h264_mb.h)
+        return {"P": 0, "B": 1, "I": 2}[self.kind]
+
+    @property
+    def nal_ref_idc(self) -> int:
+        return {"I": 3, "P": 2, "B": 0}[self.kind]
+
+
+def gop_plan(frames: int, bframes: int, anchors_at=()) -> list[PicPlan]:
+    """Coding order of a closed GOP of ``frames`` pictures: I0, then every anchor (P at
+    display indices 0, bframes + 1, ... and the last picture) followed by the B pictures
+    before it (x264's fixed --b-adapt 0 pattern, no pyramid).  frame_num counts reference
+    pictures (clause 7.4.3); B pictures are non-reference.
+
+    anchors_at: extra display indices that must be anchors.  A picture d that is an anchor
+    ends a coding-order prefix holding exactly pictures 0..d, so a segment shorter than the
+    batch (padded to F frames) is cut there (SegmentResult.display_prefix)."""
+    if frames < 1:
+        return []
+    step = max(0, int(bframes)) + 1
+    anchors = set(range(0, frames, step)) | {frames - 1} | {int(d) for d in anchors_at if 0 <= int(d) < frames}
+    if step > 1:  # keep every B run <= bframes after inserting the extra anchors
+        out_a, prev = [0], 0
+        for a in sorted(anchors - {0}):
+            while a - prev > step:
+                prev += step
+                out_a.append(prev)
+            out_a.append(a)
+            prev = a
+        anchors = out_a
+    else:
+        anchors = sorted(anchors)
+    out = [PicPlan(0, "I", 0, 0, 0)]
+    fn = 1
+    for i in range(1, len(anchors)):
+        a0, a1 = anchors[i - 1], anchors[i]
+        out.append(PicPlan(a1, "P", fn & 0xFFFF, 2 * a1, i, l0=a0))
+        fn += 1
+        for d in range(a0 + 1, a1):
+            out.append(PicPlan(d, "B", fn & 0xFFFF, 2 * d, -1, l0=a0, l1=a1, l1_anchor=i))
+    return out
+
+
 class SegmentResult:
     """One encoded closed-GOP segment: parameter sets + one slice NAL per frame.
 
     ``bitstream`` (the Annex-B piece) is joined on first access; the segment merge
     packs ``parts()`` straight into its staging buffer instead."""
 
-    __slots__ = ("frames", "nals", "bits", "header", "psnr_y", "psnr_u", "psnr_v", "ssim_y", "_bs")
+    __slots__ = ("frames", "nals", "bits", "header", "psnr_y", "psnr_u", "psnr_v", "ssim_y", "_bs", "order")
 
     def __init__(self, frames: int, nals: list[bytes] | None = None, bits: list[int] | None = None,
-                 header: bytes = b"", bitstream: bytes | None = None):
+                 header: bytes = b"", bitstream: bytes | None = None, order: list[int] | None = None):
         self.frames = frames
         self.nals = list(nals or [])
         self.bits = list(bits or [])
         self.header = header
         self._bs = bitstream
+        # display index of each NAL (coding order); identity without B pictures
+        self.order = list(order) if order is not None else list(range(len(self.nals)))
         self.psnr_y = self.psnr_u = self.psnr_v = self.ssim_y = 0.0
 
     @property
@@ -101,6 +169,14 @@ class SegmentResult:
         if self._bs is None:
             self._bs = self.header + b"".join(self.nals)
         return self._bs
+
+    def display_prefix(self, c: int) -> list[bytes]:
+        """The slice NALs of display pictures 0..c-1 (a coding-order prefix when c-1 was an
+        anchor: encode(anchors_at=...))."""
+        out = [n for n, d in zip(self.nals, self.order) if d < c]
+        if any(d >= c for d in self.order[:len(out)]):
+            raise ValueError(f"pictures 0..{c - 1} are not a coding-order prefix (encode with anchors_at)")
+        return out
 
     def parts(self) -> list[bytes]:
         return [self._bs] if self._bs is not None else [self.header, *self.nals]
@@ -150,7 +226,10 @@ class GpuH264Encoder:
                     torch.zeros((B, H // 2, W // 2), dtype=u8, device=dev))
 
         self.src = planes()
-        self.rec = [planes(), planes()]  # ping-pong: current recon / reference
+        self.nb = params.eff_bframes()
+        # anchors (I / P) alternate between rec[0] and rec[1]; B pictures (never referenced)
+        # reconstruct into rec[2]
+        self.rec = [planes(), planes()] + ([planes()] if self.nb else [])
         self.hdr = [torch.zeros((B, nmb, MB_HDR_BYTES), dtype=u8, device=dev) for _ in range(2)]
         self.coef = [torch.zeros((B, nmb, COEF_PER_MB), dtype=i16, device=dev) for _ in range(2)]
         self.nz = torch.zeros((B, nmb, 16), dtype=u8, device=dev)
@@ -159,8 +238,20 @@ class GpuH264Encoder:
         self.me_cost = torch.zeros((B, nmb), dtype=i32, device=dev)
         self.intra_cost = torch.zeros((B, nmb), dtype=i32, device=dev)
         self.pred = torch.zeros((B, nmb, 256), dtype=u8, device=dev)
-        # resident b / h / j half-sample planes of the reference (margin 4, + load slack)
-        self.me_hp = torch.empty(B * 3 * (H + 8) * (W + 8) + 64, dtype=u8, device=dev)
+        # resident b / h / j half-sample planes of the two latest anchors (margin 4, + load
+        # slack), built once per anchor and shared by the P and B pictures that reference it
+        self.me_hp = [torch.empty(B * 3 * (H + 8) * (W + 8) + 64, dtype=u8, device=dev) for _ in range(2)]
+        if self.nb:
+            # B pictures: the list-1 search, temporal direct vectors and the mode decision
+            self.mv1 = torch.zeros((B, nmb, 2), dtype=i16, device=dev)
+            self.me_cost1 = torch.zeros((B, nmb), dtype=i32, device=dev)
+            self.pred1 = torch.zeros((B, nmb, 256), dtype=u8, device=dev)
+            self.pred_b = torch.zeros((B, nmb, 256), dtype=u8, device=dev)
+            self.cost_b = torch.zeros((B, nmb), dtype=i32, device=dev)
+            self.pm0 = torch.zeros((B, nmb, 2), dtype=i16, device=dev)
+            self.pm1 = torch.zeros((B, nmb, 2), dtype=i16, device=dev)
+            self.dmv = torch.zeros((B, nmb, 16), dtype=i16, device=dev)
+            self.col_hdr = torch.zeros((B, nmb, MB_HDR_BYTES), dtype=u8, device=dev)
         self.intra_flag = torch.zeros((B, nmb), dtype=u8, device=dev)
         self.aq = torch.zeros((B, nmb), dtype=torch.int8, device=dev)     # per-MB QP offsets (AQ)
         self.qp_flags = torch.zeros((B, nmb), dtype=u8, device=dev)       # MB carries mb_qp_delta
@@ -273,57 +364,98 @@ class GpuH264Encoder:
                       self._ptr(self.src[0]), self._ptr(self.src[1]), self._ptr(self.src[2]),
                       self.p.width, self.p.height, self.W, self.H, self._stream())
 
-    def _encode_frame(self, idr: bool, cur, ref, hdr, coef, cut=None, t: int = 0):
-        """cut: optional [B] bool device tensor -- slots whose frame is a scene cut (every MB
-        intra, as an I picture would be)."""
+    @staticmethod
+    def _dist_scale(poc: int, poc0: int, poc1: int) -> tuple[int, int]:
+        """(DistScaleFactor, direct_copy) of temporal direct (clause 8.4.1.2.3; C division)."""
+        def tdiv(x: int, y: int) -> int:
+            q = abs(x) // abs(y)
+            return q if (x >= 0) == (y >= 0) else -q
+        tb = max(-128, min(127, poc - poc0))
+        td = max(-128, min(127, poc1 - poc0))
+        if td == 0:
+            return 0, 1
+        tx = tdiv(16384 + abs(tdiv(td, 2)), td)
+        return max(-1024, min(1023, (tb * tx + 32) >> 6)), 0
+
+    def _encode_frame(self, pic: PicPlan, cur, ref0, ref1, hdr, coef, cut=None):
+        """One picture of every slot.  ref0 / ref1: the RefPicList0[0] / RefPicList1[0]
+        reconstructions (P: ref0; B: both).  cut: optional [B] bool device tensor -- slots
+        whose picture is a scene cut (every MB intra, as an I picture would be)."""
         s = self._stream()
         B, wmb, hmb = self.B, self.wmb, self.hmb
-        sy, su, sv = (self._ptr(x) for x in self.src)
-        ry, ru, rv = (self._ptr(x) for x in cur)
+        P = self._ptr
+        sy, su, sv = (P(x) for x in self.src)
+        ry, ru, rv = (P(x) for x in cur)
+        idr = pic.kind == "I"
         aq = 0
         mbt = self._mbtree
         if self.p.aq_strength > 0 or mbt is not None:
-            aq = self._ptr(self.aq)
+            aq = P(self.aq)
             extra, stride = 0, 0
-            if mbt is not None and mbt.shape[2] == self.nmb:  # [B, F, nmb] float offsets of this batch
-                extra, stride = mbt.data_ptr() + t * self.nmb * 4, mbt.shape[1] * self.nmb
+            # MB-tree offsets belong to referenced pictures; B pictures get variance AQ only
+            if mbt is not None and mbt.shape[2] == self.nmb and pic.kind != "B":
+                extra, stride = mbt.data_ptr() + pic.d * self.nmb * 4, mbt.shape[1] * self.nmb
             self.hip.aq_offsets(B, wmb, hmb, sy, su, sv, float(self.p.aq_strength), aq, s, extra, stride)
-        if not idr:
-            fy, fu, fv = (self._ptr(x) for x in ref)
+        cqo = self.p.chroma_qp_offset
+        if pic.kind == "P":
+            fy, fu, fv = (P(x) for x in ref0)
             self.intra_count.zero_()
-            self.hip.me(B, wmb, hmb, sy, fy, self._ptr(self.prev_mv), self._ptr(self.mv), self._ptr(self.me_cost),
-                        self._ptr(self.pred), self._ptr(self.intra_cost), self._ptr(self.qp),
-                        self.p.me_range, self.p.subpel, s, self._ptr(self.me_hp), aq)
+            self.hip.me(B, wmb, hmb, sy, fy, P(self.prev_mv), P(self.mv), P(self.me_cost), P(self.pred),
+                        P(self.intra_cost), P(self.qp), self.p.me_range, self.p.subpel, s,
+                        P(self.me_hp[(pic.anchor - 1) & 1]), aq, 1)
             if cut is not None:
                 self.intra_cost.masked_fill_(cut[:, None], -1)  # intra beats any inter cost
-            self.hip.encode_inter(B, wmb, hmb, sy, su, sv, fy, fu, fv, ry, ru, rv, self._ptr(self.pred),
-                                  self._ptr(self.mv), self._ptr(self.me_cost), self._ptr(self.intra_cost),
-                                  self._ptr(self.qp), self.p.chroma_qp_offset, self._ptr(hdr), self._ptr(coef),
-                                  self._ptr(self.nz), self._ptr(self.intra_flag), self._ptr(self.intra_count), s, aq)
+            self.hip.encode_inter(B, wmb, hmb, sy, su, sv, fy, fu, fv, ry, ru, rv, P(self.pred), P(self.mv),
+                                  P(self.me_cost), P(self.intra_cost), P(self.qp), cqo, P(hdr), P(coef), P(self.nz),
+                                  P(self.intra_flag), P(self.intra_count), s, aq)
             self.prev_mv.copy_(self.mv)
+        elif pic.kind == "B":
+            f0y, f0u, f0v = (P(x) for x in ref0)
+            f1y, f1u, f1v = (P(x) for x in ref1)
+            hp0, hp1 = P(self.me_hp[(pic.l1_anchor - 1) & 1]), P(self.me_hp[pic.l1_anchor & 1])
+            dsf, copy = self._dist_scale(pic.poc, 2 * pic.l0, 2 * pic.l1)
+            self.hip.b_direct(B, wmb, hmb, P(self.col_hdr), dsf, copy, P(self.dmv), P(self.pm0), P(self.pm1), s)
+            self.intra_count.zero_()
+            self.hip.me(B, wmb, hmb, sy, f0y, P(self.pm0), P(self.mv), P(self.me_cost), P(self.pred),
+                        P(self.intra_cost), P(self.qp), self.p.me_range, self.p.subpel, s, hp0, aq, 1)
+            self.hip.me(B, wmb, hmb, sy, f1y, P(self.pm1), P(self.mv1), P(self.me_cost1), P(self.pred1),
+                        P(self.intra_cost), P(self.qp), self.p.me_range, self.p.subpel, s, hp1, aq, 1)
+            self.hip.b_decide(B, wmb, hmb, sy, f0y, f1y, hp0, hp1, P(self.mv), P(self.mv1), P(self.me_cost),
+                              P(self.me_cost1), P(self.pred), P(self.pred1), P(self.pm0), P(self.pm1), P(self.dmv),
+                              P(self.qp), aq, P(hdr), P(self.pred_b), P(self.cost_b), s)
+            if cut is not None:
+                self.intra_cost.masked_fill_(cut[:, None], -1)
+            self.hip.encode_inter(B, wmb, hmb, sy, su, sv, f0y, f0u, f0v, ry, ru, rv, P(self.pred_b), P(self.mv),
+                                  P(self.cost_b), P(self.intra_cost), P(self.qp), cqo, P(hdr), P(coef), P(self.nz),
+                                  P(self.intra_flag), P(self.intra_count), s, aq, f1u, f1v, 1)
+        if pic.kind != "I":
             self.p_intra_mbs += self.intra_count.sum()
-            flag_ptr, count_ptr = self._ptr(self.intra_flag), self._ptr(self.intra_count)
+            flag_ptr, count_ptr = P(self.intra_flag), P(self.intra_count)
         else:
             self.prev_mv.zero_()
             flag_ptr, count_ptr = 0, 0
-        self.hip.encode_intra(B, wmb, hmb, sy, su, sv, ry, ru, rv, self._ptr(self.qp), self.p.chroma_qp_offset,
-                              self._ptr(hdr), self._ptr(coef), self._ptr(self.nz), flag_ptr, count_ptr,
-                              self._ptr(self.err),
+        self.hip.encode_intra(B, wmb, hmb, sy, su, sv, ry, ru, rv, P(self.qp), cqo, P(hdr), P(coef), P(self.nz),
+                              flag_ptr, count_ptr, P(self.err),
                               int(self.p.i4x4 and (idr or self.p.i4x4_in_p or cut is not None)), s, aq)
         if aq:
             # MBs without mb_qp_delta take QP_pred (clause 7.4.5): their records must say so
             # before deblocking reads every MB's QP
-            self.hip.qp_fixup(B, wmb, hmb, self._ptr(hdr), self._ptr(coef), self._ptr(self.nz),
-                              self._ptr(self.qp_flags), self._ptr(self.qp), s)
+            self.hip.qp_fixup(B, wmb, hmb, P(hdr), P(coef), P(self.nz), P(self.qp_flags), P(self.qp), s)
         if self.p.deblock:
-            self.hip.deblock(B, wmb, hmb, ry, ru, rv, self._ptr(hdr), self._ptr(self.nz), self.p.chroma_qp_offset,
-                             0, 0, self._ptr(self.err), s)
+            self.hip.deblock(B, wmb, hmb, ry, ru, rv, P(hdr), P(self.nz), cqo, 0, 0, P(self.err), s)
+        if pic.kind != "B":
+            # the anchor's half-sample planes (shared by every picture that references it) and,
+            # for the B pictures after it, its motion as the temporal-direct co-located field
+            self.hip.me_halfpel(B, self.W, self.H, ry, P(self.me_hp[pic.anchor & 1]), s)
+            if self.nb and pic.kind == "P":
+                self.col_hdr.copy_(hdr)
 
     # ------------------------------------------------------------------ entropy (GPU CAVLC)
-    def _frame_params(self, b: int, t: int, qp_frame: int, idr: bool, idr_ids: list[int]) -> dict:
-        return dict(idr=int(idr), frame_num=t, idr_pic_id=idr_ids[b] & 0xFFFF, qp=qp_frame)
+    def _frame_params(self, b: int, pic: PicPlan, qp_frame: int, idr_ids: list[int]) -> dict:
+        return dict(idr=int(pic.kind == "I"), frame_num=pic.frame_num, idr_pic_id=idr_ids[b] & 0xFFFF, qp=qp_frame,
+                    slice_type=pic.slice_type, nal_ref_idc=pic.nal_ref_idc, poc=pic.poc, direct_spatial=0)
 
-    def _gpu_cabac_bin(self, k: int, t: int, qps_t, idr: bool, idr_ids: list[int], qp_dev: torch.Tensor):
+    def _gpu_cabac_bin(self, k: int, t: int, pic: PicPlan, qps_t, idr_ids: list[int], qp_dev: torch.Tensor):
         """Binarise frame step t (records hdr[k]/coef[k]) into the symbol pool of its group
         ring, on the *copy* stream (the caller's current stream): the records are free
         again once this is done, whatever the arithmetic coder is doing.
@@ -334,12 +466,12 @@ class GpuH264Encoder:
             self.cab_pool_used[r].zero_()
         self._header_bits_into(self.h_cab_hdr_bits[r][j * B:(j + 1) * B], self.h_cab_hdr_nbits[r][j * B:(j + 1) * B],
                                self.cab_hdr_bits[r][j * B:(j + 1) * B], self.cab_hdr_nbits[r][j * B:(j + 1) * B],
-                               t, qps_t, idr, idr_ids)
+                               pic, qps_t, idr_ids)
         P = self._ptr
         self.hip.cabac_bin(B, self.wmb, self.hmb, P(self.hdr[k]), P(self.coef[k]), P(self.cab_mask), P(self.cab_nb),
                            P(self.cab_cnt), P(self.cab_off), P(self.cab_tot), P(self.cab_pool[r]), self.cab_pool_cap,
                            self.cab_pool_used[r].data_ptr(), self.cab_base[r][j * B:].data_ptr(),
-                           self.cab_total[r][j * B:].data_ptr(), P(qp_dev), 2 if idr else 0, 1, 1, 0, P(self.err),
+                           self.cab_total[r][j * B:].data_ptr(), P(qp_dev), pic.slice_type, 1, 1, 0, P(self.err),
                            self.copy_stream.cuda_stream)
 
     def _gpu_cabac_code(self, t0: int, n: int, qps_d: torch.Tensor):
@@ -361,7 +493,7 @@ class GpuH264Encoder:
             self.h_pool_used[r].copy_(self.cab_pool_used[r:r + 1], non_blocking=True)
             self.cab_done[r].record(es)
 
-    def _copy_out_group(self, g: int, t0: int, n: int, copied, wrap_futs):
+    def _copy_out_group(self, g: int, t0: int, n: int, copied, wrap_futs, plan: list[PicPlan]):
         """Copy thread (groups in order): sizes -> compacted bytes D2H -> NAL wrapping of each
         frame step on the pool.  ``copied[g]`` releases ring g % 2 (pool, headers, pinned
         sizes) for group g + 2."""
@@ -406,19 +538,20 @@ class GpuH264Encoder:
         for jj in range(n):
             sz = sizes[jj * B:(jj + 1) * B]
             nb = int(sz.sum())
-            wrap_futs[t0 + jj] = self.pool.submit(self._wrap, buf[off:off + nb], nb, sz.tolist(), t0 + jj == 0)
+            wrap_futs[t0 + jj] = self.pool.submit(self._wrap, buf[off:off + nb], nb, sz.tolist(), plan[t0 + jj])
             off += nb
 
-    def _header_bits(self, k: int, t: int, qps_t, idr: bool, idr_ids: list[int]):
+    def _header_bits(self, k: int, pic: PicPlan, qps_t, idr_ids: list[int]):
         """Slice headers of this step -> pinned host words -> device (current stream)."""
         self._header_bits_into(self.h_hdr_bits[k], self.h_hdr_nbits[k], self.cav_hdr_bits[k], self.cav_hdr_nbits[k],
-                               t, qps_t, idr, idr_ids)
+                               pic, qps_t, idr_ids)
 
-    def _header_bits_into(self, hb, hn, db, dn, t: int, qps_t, idr: bool, idr_ids: list[int]):
+    def _header_bits_into(self, hb, hn, db, dn, pic: PicPlan, qps_t, idr_ids: list[int]):
+        idr = pic.kind == "I"
         hbn, hnn = hb.numpy(), hn.numpy()
         cache = {}
         for b in range(self.B):
-            fp = self._frame_params(b, t, int(qps_t[b]), idr, idr_ids)
+            fp = self._frame_params(b, pic, int(qps_t[b]), idr_ids)
             key = (fp["idr_pic_id"] if idr else -1, fp["qp"])
             if key not in cache:
                 cache[key] = self.host.slice_header_bits(self.cfg, fp)
@@ -429,10 +562,13 @@ class GpuH264Encoder:
         db.copy_(hb, non_blocking=True)
         dn.copy_(hn, non_blocking=True)
 
-    def _gpu_cavlc(self, k: int, t: int, qps_t, idr: bool, idr_ids: list[int]):
+    def _gpu_cavlc(self, k: int, pic: PicPlan, qps_t, idr_ids: list[int]):
         """Launch the CAVLC kernels for the current frame step on the compute stream.
         qps_t: per-slot slice QP of this frame step (sequence of B ints)."""
-        self._header_bits(k, t, qps_t, idr, idr_ids)
+        if pic.kind == "B":
+            raise ValueError("the GPU CAVLC path codes I / P slices only")
+        idr = pic.kind == "I"
+        self._header_bits(k, pic, qps_t, idr_ids)
         P = self._ptr
         self.hip.cavlc(self.B, self.wmb, self.hmb, P(self.hdr[k]), P(self.coef[k]), P(self.cav_mbs), P(self.cav_len),
                        P(self.cav_off), P(self.cav_trail), P(self.cav_total), P(self.cav_sizes[k]),
@@ -440,7 +576,7 @@ class GpuH264Encoder:
                        0 if idr else 1, int(qps_t[0]), P(self.qp), P(self.cav_out[k]), P(self.cav_out_off),
                        self._stream(), P(self.nz))
 
-    def _copy_out(self, t: int, k: int, idr: bool, copied, wrap_futs):
+    def _copy_out(self, t: int, k: int, pic: PicPlan, copied, wrap_futs):
         """Copy thread (frames in order): sizes -> compressed bytes D2H, then hand the NAL
         wrapping to the pool.  ``copied[t]`` releases the device buffers of slot k for frame
         t + 2 as soon as the bytes are on the host; the wrapping is off that critical path."""
@@ -463,16 +599,16 @@ class GpuH264Encoder:
         t2 = time.perf_counter()
         self.timings["entropy_wait_gpu_s"] = self.timings.get("entropy_wait_gpu_s", 0.0) + (t1 - t0)
         self.timings["d2h_s"] = self.timings.get("d2h_s", 0.0) + (t2 - t1)
-        wrap_futs[t] = self.pool.submit(self._wrap, buf, total, sizes, idr)
+        wrap_futs[t] = self.pool.submit(self._wrap, buf, total, sizes, pic)
 
-    def _wrap(self, buf, total: int, sizes: list[int], idr: bool) -> list[tuple[bytes, int]]:
+    def _wrap(self, buf, total: int, sizes: list[int], pic: PicPlan) -> list[tuple[bytes, int]]:
         t0 = time.perf_counter()
-        nals = self.host.nal_wrap_many(buf[:total].numpy(), sizes, 3 if idr else 2, 5 if idr else 1)
+        nals = self.host.nal_wrap_many(buf[:total].numpy(), sizes, pic.nal_ref_idc, 5 if pic.kind == "I" else 1)
         self.timings["entropy_s"] = self.timings.get("entropy_s", 0.0) + (time.perf_counter() - t0)
         return [(n, len(n) * 8) for n in nals]
 
     # ------------------------------------------------------------------ entropy (host)
-    def _write_slices(self, k: int, t: int, qps_t, idr: bool, idr_ids: list[int]) -> list[tuple[bytes, int]]:
+    def _write_slices(self, k: int, pic: PicPlan, qps_t, idr_ids: list[int]) -> list[tuple[bytes, int]]:
         t0 = time.perf_counter()
         self.copy_done[k].synchronize()
         t1 = time.perf_counter()
@@ -480,7 +616,7 @@ class GpuH264Encoder:
         coef = self.h_coef[k].numpy()
 
         def one(b: int):
-            fp = self._frame_params(b, t, int(qps_t[b]), idr, idr_ids)
+            fp = self._frame_params(b, pic, int(qps_t[b]), idr_ids)
             nal, st = self.host.write_slice(self.cfg, fp, hdr[b], coef[b])
             return nal, st["bits"]
 
@@ -519,7 +655,7 @@ class GpuH264Encoder:
     @torch.no_grad()
     def encode(self, y: torch.Tensor, u: torch.Tensor, v: torch.Tensor, idr_base: int = 0,
                keep_recon: bool = False, metrics: bool = True, idr_ids: list[int] | None = None,
-               qps=None) -> list[SegmentResult]:
+               qps=None, anchors_at=()) -> list[SegmentResult]:
         """Encode B segments of F frames each.
 
         y: [B, F, h, w] uint8 (device), u/v: [B, F, h/2, w/2].  Each slot's output is a
@@ -546,16 +682,28 @@ class GpuH264Encoder:
         qp_i, qp_p = self.p.frame_qps()
         self._scenecuts = None
         self._mbtree = None
+        self._from_la = False
         if qps is None and self.p.crf is not None and self.p.lookahead:
             qps = self.crf_qps(y)
+            self._from_la = True
         cuts_h = self._scenecuts if self._scenecuts is not None else np.zeros((B, F), dtype=bool)
-        cuts_d = torch.from_numpy(np.ascontiguousarray(cuts_h.T)).to(self.dev)  # [F, B]
+        # a scene cut (in any slot) becomes an anchor, so the pictures after it predict from
+        # the new scene instead of across the cut (x264 places an I / P picture there)
+        plan = gop_plan(F, self.nb, set(anchors_at) | {d for d in range(1, F) if cuts_h[:, d].any()})
+        order = [pic.d for pic in plan]  # display index of each coding step
         if qps is None:
             qps_h = np.full((B, F), qp_p, dtype=np.int32)
             qps_h[:, 0] = qp_i
         else:
             qps_h = np.clip(np.asarray(qps, dtype=np.int32).reshape(B, F), 0, 51)
-        qps_d = torch.from_numpy(np.ascontiguousarray(qps_h.T)).to(self.dev)  # [F, B]
+        if self.nb and (qps is None or self._from_la):
+            # B pictures one pbratio step above their anchors (x264 --pbratio 1.3 = +2 QP)
+            bd = [pic.d for pic in plan if pic.kind == "B"]
+            qps_h[:, bd] = np.minimum(qps_h[:, bd] + int(self.p.b_qp_offset), 51)
+        # per coding step (rows), [F, B]: the entropy stages index coding steps
+        qps_d = torch.from_numpy(np.ascontiguousarray(qps_h[:, order].T)).to(self.dev)
+        cuts_c = cuts_h[:, order]
+        cuts_d = torch.from_numpy(np.ascontiguousarray(cuts_c.T)).to(self.dev)  # [F, B] coding order
         self.err.zero_()
         sse = torch.zeros((F, B, 3), dtype=torch.int64, device=self.dev)
         ssim = torch.zeros((F, B), dtype=torch.float32, device=self.dev)
@@ -580,12 +728,13 @@ class GpuH264Encoder:
             while not group_copied[i].wait(0.5):
                 if group_futs[i].done() and group_futs[i].exception() is not None:
                     raise group_futs[i].exception()
-        recons = [] if keep_recon else None
+        recons = [None] * F if keep_recon else None
         main = torch.cuda.current_stream(self.dev)
-        for t in range(F):
+        for t in range(F):  # t: coding step
             k = t & 1
-            idr = t == 0
-            qpt = qps_h[:, t]
+            pic = plan[t]
+            idr = pic.kind == "I"
+            qpt = qps_h[:, pic.d]
             # the device/pinned buffers of slot k were last used by step t-2: wait for them
             tw = time.perf_counter()
             if cabac_gpu:
@@ -598,24 +747,27 @@ class GpuH264Encoder:
                 pending[k] = None
             self.timings["host_blocked_s"] = self.timings.get("host_blocked_s", 0.0) + time.perf_counter() - tw
             main.wait_event(self.copy_done[k]) if t >= 2 else None
-            cur, ref = self.rec[k], self.rec[1 - k]
-            self._prep(y, u, v, t)
+            if pic.kind == "B":
+                cur, ref0, ref1 = self.rec[2], self.rec[(pic.l1_anchor - 1) & 1], self.rec[pic.l1_anchor & 1]
+            else:
+                cur, ref0, ref1 = self.rec[pic.anchor & 1], self.rec[(pic.anchor - 1) & 1], None
+            self._prep(y, u, v, pic.d)
             self.qp.copy_(qps_d[t])
-            self._encode_frame(idr, cur, ref, self.hdr[k], self.coef[k],
-                               cuts_d[t] if (not idr and cuts_h[:, t].any()) else None, t)
+            self._encode_frame(pic, cur, ref0, ref1, self.hdr[k], self.coef[k],
+                               cuts_d[t] if (not idr and cuts_c[:, t].any()) else None)
             if metrics:
                 self.hip.sse(B, self.W, self.H, self.p.width, self.p.height, self._ptr(self.src[0]),
                              self._ptr(self.src[1]), self._ptr(self.src[2]), self._ptr(cur[0]), self._ptr(cur[1]),
-                             self._ptr(cur[2]), sse[t].data_ptr(), ssim[t].data_ptr(), self._stream())
+                             self._ptr(cur[2]), sse[pic.d].data_ptr(), ssim[pic.d].data_ptr(), self._stream())
             if keep_recon:
-                recons.append(tuple(c.clone() for c in cur))
+                recons[pic.d] = tuple(c.clone() for c in cur)
             if self.entropy == "gpu" and not self.p.cabac:
-                self._gpu_cavlc(k, t, qpt, idr, idr_ids)
+                self._gpu_cavlc(k, pic, qpt, idr_ids)
             self.compute_done[k].record(main)
             with torch.cuda.stream(self.copy_stream):
                 self.copy_stream.wait_event(self.compute_done[k])
                 if cabac_gpu:
-                    self._gpu_cabac_bin(k, t, qpt, idr, idr_ids, qps_d[t])
+                    self._gpu_cabac_bin(k, t, pic, qpt, idr_ids, qps_d[t])
                 elif self.entropy == "gpu":
                     self.h_sizes[k].copy_(self.cav_sizes[k], non_blocking=True)
                 else:
@@ -627,11 +779,11 @@ class GpuH264Encoder:
                     g, t0 = t // G, t - t % G
                     self._gpu_cabac_code(t0, t - t0 + 1, qps_d)
                     group_futs[g] = self.copy_pool.submit(self._copy_out_group, g, t0, t - t0 + 1, group_copied,
-                                                          wrap_futs)
+                                                          wrap_futs, plan)
             elif self.entropy == "gpu":
-                copy_futs[t] = self.copy_pool.submit(self._copy_out, t, k, idr, copied, wrap_futs)
+                copy_futs[t] = self.copy_pool.submit(self._copy_out, t, k, pic, copied, wrap_futs)
             else:
-                pending[k] = self.pool.submit(self._write_slices, k, t, qpt, idr, idr_ids)
+                pending[k] = self.pool.submit(self._write_slices, k, pic, qpt, idr_ids)
         if cabac_gpu:
             for f in group_futs:
                 f.result()
@@ -664,7 +816,7 @@ class GpuH264Encoder:
         nwin = (self.p.width // 8) * (self.p.height // 8)
         for b in range(B):
             nals = [outs[t][b][0] for t in range(F)]
-            r = SegmentResult(frames=F, nals=nals, bits=[outs[t][b][1] for t in range(F)], header=ps)
+            r = SegmentResult(frames=F, nals=nals, bits=[outs[t][b][1] for t in range(F)], header=ps, order=order)
             if metrics:
                 def psnr(ssev, n):
                     mse = ssev / n

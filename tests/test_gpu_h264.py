@@ -57,7 +57,7 @@ def test_gpu_cabac_smaller_than_cavlc(host):
     y, u, v = synth_clip(2, 6, 352, 288, seed=5)
     size = {}
     for cabac in (True, False):
-        enc = GpuH264Encoder(H264Params(width=352, height=288, crf=None, qp=27, cabac=cabac), slots=2)
+        enc = GpuH264Encoder(H264Params(width=352, height=288, crf=None, qp=27, cabac=cabac, bframes=0), slots=2)
         size[cabac] = sum(r.nbytes() for r in enc.encode(y, u, v))
         enc.close()
     torch.cuda.synchronize()
@@ -158,7 +158,8 @@ def test_gpu_scenecut_codes_cut_frames_intra(host):
         pics = host.decode(r.bitstream)
         kinds = np.asarray(pics[cut]["mb_kind"])
         assert np.isin(kinds, [0, 1, 4]).all()          # I4x4 / I16x16 / I_PCM only
-        assert np.isin(np.asarray(pics[cut + 1]["mb_kind"]), [2, 3, 5, 6, 7]).mean() > 0.5
+        inter = [2, 3, 5, 6, 7, 9, 10, 11, 12, 13]  # P and B kinds: the cut is an anchor
+        assert np.isin(np.asarray(pics[cut + 1]["mb_kind"]), inter).mean() > 0.5
         assert r.psnr_y > 30
     enc.close()
 
@@ -208,3 +209,52 @@ def test_gpu_h264_wide_multiband_roundtrip(host):
     enc, res, _ = _run(4096, 544, slots=1, frames=2, crf=None, qp=30)
     _check_roundtrip(host, enc, res, 4096, 544)
     assert int(enc.err.item()) == 0
+
+
+@pytest.mark.parametrize("bframes,frames", [(3, 9), (2, 7), (1, 4)])
+def test_gpu_bframes_roundtrip(host, bframes, frames):
+    """B pictures (temporal direct, B_16x16 L0 / L1 / Bi): decoder output == GPU recon for
+    every picture in display order; slice types follow the I P B.. coding order."""
+    enc, res, _ = _run(176, 144, slots=3, frames=frames, crf=None, qp=27, bframes=bframes)
+    _check_roundtrip(host, enc, res, 176, 144)
+    from govideocompressor_amd.models.h264_gpu import gop_plan
+    plan = gop_plan(frames, bframes)
+    pics = host.decode(res[0].bitstream)
+    kinds = {p.d: p.kind for p in plan}
+    assert [{"I": 2, "P": 0, "B": 1}[kinds[d]] for d in range(frames)] == [p["slice_type"] % 5 for p in pics]
+    assert res[0].order == [p.d for p in plan]
+
+
+def test_gpu_bframes_save_bits(host):
+    """x264's --bframes 3 trade: fewer bits than P-only at a small quality cost."""
+    import torch
+    from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
+
+    y, u, v = synth_clip(2, 13, 352, 288, seed=7)
+    out = {}
+    for nb in (0, 3):
+        enc = GpuH264Encoder(H264Params(width=352, height=288, crf=None, qp=27, bframes=nb), slots=2)
+        res = enc.encode(y, u, v)
+        out[nb] = (sum(len(r.bitstream) for r in res), float(np.mean([r.psnr_y for r in res])))
+        enc.close()
+    torch.cuda.synchronize()
+    assert out[3][0] < out[0][0], out
+    assert out[3][1] > out[0][1] - 1.5, out
+
+
+def test_gpu_short_segment_display_prefix(host):
+    """A segment shorter than the batch ends on a forced anchor: its display prefix is a
+    decodable stream of exactly its pictures (the worker backend's padded chunks)."""
+    import torch
+    from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
+
+    y, u, v = synth_clip(2, 10, 176, 144, seed=9)
+    enc = GpuH264Encoder(H264Params(width=176, height=144, crf=None, qp=28, bframes=3), slots=2)
+    res = enc.encode(y, u, v, keep_recon=True, anchors_at=[5])
+    torch.cuda.synchronize()
+    ps = enc.parameter_sets()
+    pics = host.decode(ps + b"".join(res[1].display_prefix(6)))
+    assert len(pics) == 6
+    for t, pic in enumerate(pics):
+        assert np.array_equal(pic["y_coded"], enc.last_recon[t][0][1].cpu().numpy())
+    enc.close()
