@@ -12,10 +12,10 @@
 //   mivc_launch_cabac_bin   one frame step (B slots, one slice each), into a symbol pool
 //     cabac_mask    (nmb/2 x B, wave64)    non-zero mask of every 4x4 / DC block
 //     cabac_prep    (nmb/64 x B, 64)       lane per MB: coding state (skip, cbp, mvd, cbf ...)
-//     cabac_chain   (B, 1024)              mb_qp_delta chain (QP_pred scan) per slot
+//     cabac_chain   (B, 64)                mb_qp_delta chain (QP_pred scan) per slot
 //     cabac_count   (nmb/64 x B, 64)       lane per MB: symbol count
-//     cabac_offsets (B, 1024)              per-slot exclusive scan of the counts
-//     cabac_alloc   (1, 1024)              slot regions in the pool (scan over slots)
+//     cabac_offsets (B, 64)                per-slot exclusive scan of the counts
+//     cabac_alloc   (1, 64)                slot regions in the pool (scan over slots)
 //     cabac_bins    (nmb/64 x B, 64)       lane per MB: symbols, staged to 16-byte stores
 //   mivc_launch_cabac_code  G frame steps at once (G * B slices: one lane each)
 //     cabac_arith   (G*B/lpw, 64)          context states in LDS (one column per lane),
@@ -112,28 +112,43 @@ __global__ __launch_bounds__(64) void cabac_prep(CabacBinArgs a) {
   h264::cabac_prepare_mb(si, a.hdr + base, mb, a.mask[base + mb], a.nb[base + mb]);
 }
 
+// Wave-wide inclusive scans (one-wave workgroups: the per-slot scans below run beside the
+// encode kernels on the copy stream, and a 1024-thread workgroup waited for a whole CU's
+// worth of free wave slots -- 4-8 ms per launch instead of tens of microseconds).
+__device__ __forceinline__ long long wave_scan_add(long long v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const long long y = __shfl_up(v, o, 64);
+    if (lane >= o) v += y;
+  }
+  return v;
+}
+__device__ __forceinline__ int wave_scan_max(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(v, o, 64);
+    if (lane >= o) v = max(v, y);
+  }
+  return v;
+}
+
 // mb_qp_delta chain (cabac_qp_chain as a scan): MB i codes a delta iff it is not skipped
 // and (cbp != 0 or I16x16); its delta is QP_i - QP of the last earlier delta MB (or the
-// slice QP); its first-bin context is "MB i-1 coded a non-zero delta".
-__global__ __launch_bounds__(1024) void cabac_chain(CabacBinArgs a) {
-  const int slot = blockIdx.x, n = a.g.nmb();
+// slice QP); its first-bin context is "MB i-1 coded a non-zero delta".  One wave per slot.
+__global__ __launch_bounds__(64) void cabac_chain(CabacBinArgs a) {
+  const int slot = blockIdx.x, n = a.g.nmb(), lane = threadIdx.x;
   CabacNb* nb = a.nb + static_cast<size_t>(slot) * n;
-  __shared__ int s_last[1024];
-  const int per = (n + blockDim.x - 1) / blockDim.x;
-  const int i0 = threadIdx.x * per, i1 = min(n, i0 + per);
+  const int per = (n + 63) / 64;
+  const int i0 = lane * per, i1 = min(n, i0 + per);
   auto has = [&](int i) { return !nb[i].skip && (nb[i].cbp != 0 || nb[i].kind == h264::MBK_I16x16); };
   int ld = -1;
   for (int i = i0; i < i1; ++i)
     if (has(i)) ld = i;
-  s_last[threadIdx.x] = ld;
-  __syncthreads();
-  for (int o = 1; o < blockDim.x; o <<= 1) {
-    const int v = threadIdx.x >= o ? s_last[threadIdx.x - o] : -1;
-    __syncthreads();
-    s_last[threadIdx.x] = max(s_last[threadIdx.x], v);
-    __syncthreads();
-  }
-  ld = threadIdx.x > 0 ? s_last[threadIdx.x - 1] : -1;
+  const int incl = wave_scan_max(ld);
+  ld = __shfl_up(incl, 1, 64);
+  if (lane == 0) ld = -1;
   int last_qp = ld >= 0 ? nb[ld].qp : a.slot_qp[slot];
   for (int i = i0; i < i1; ++i) {
     if (has(i)) {
@@ -146,8 +161,10 @@ __global__ __launch_bounds__(1024) void cabac_chain(CabacBinArgs a) {
       nb[i].dqp = 0;
     }
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < n; i += blockDim.x)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  for (int i = lane; i < n; i += 64)
     nb[i].prev_dqp_nz = static_cast<uint8_t>(i > 0 && has(i - 1) && nb[i - 1].dqp != 0);
 }
 
@@ -163,52 +180,36 @@ __global__ __launch_bounds__(64) void cabac_count(CabacBinArgs a) {
   a.cnt[base + mb] = s.out.n;
 }
 
-// Block-wide exclusive scan helper (blockDim.x == 1024): returns the exclusive prefix of
-// `v` over the threads and the block total.
-__device__ __forceinline__ long long block_scan_excl(long long v, long long* s, long long& total) {
-  s[threadIdx.x] = v;
-  __syncthreads();
-  for (int o = 1; o < blockDim.x; o <<= 1) {
-    const long long w = threadIdx.x >= o ? s[threadIdx.x - o] : 0;
-    __syncthreads();
-    s[threadIdx.x] += w;
-    __syncthreads();
-  }
-  total = s[blockDim.x - 1];
-  const long long ex = s[threadIdx.x] - v;
-  __syncthreads();
-  return ex;
-}
-
-__global__ __launch_bounds__(1024) void cabac_offsets(CabacBinArgs a) {
-  const int slot = blockIdx.x, n = a.g.nmb();
+// Symbol offsets of every MB inside its slice: one wave per slot.
+__global__ __launch_bounds__(64) void cabac_offsets(CabacBinArgs a) {
+  const int slot = blockIdx.x, n = a.g.nmb(), lane = threadIdx.x;
   const size_t base = static_cast<size_t>(slot) * n;
-  __shared__ long long s_sum[1024];
-  const int per = (n + blockDim.x - 1) / blockDim.x;
-  const int i0 = threadIdx.x * per, i1 = min(n, i0 + per);
+  const int per = (n + 63) / 64;
+  const int i0 = lane * per, i1 = min(n, i0 + per);
   long long loc = 0;
   for (int i = i0; i < i1; ++i) loc += a.cnt[base + i];
-  long long tot;
-  long long p = block_scan_excl(loc, s_sum, tot);
+  const long long incl = wave_scan_add(loc);
+  long long p = incl - loc;
   for (int i = i0; i < i1; ++i) {
     a.off[base + i] = p;
     p += a.cnt[base + i];
   }
-  if (threadIdx.x == 0) a.tot[slot] = static_cast<int>(tot);
+  if (lane == 63) a.tot[slot] = static_cast<int>(incl);
 }
 
 // Slice regions of this frame step in the group's pool: kCabacGap + symbols, rounded to
 // 8 symbols (16-byte aligned), allocated back to back after the group's earlier steps.
-__global__ __launch_bounds__(1024) void cabac_alloc(CabacBinArgs a) {
-  __shared__ long long s_sum[1024];
-  const int B = a.g.B;
-  const int per = (B + blockDim.x - 1) / blockDim.x;
-  const int i0 = threadIdx.x * per, i1 = min(B, i0 + per);
+// One wave.
+__global__ __launch_bounds__(64) void cabac_alloc(CabacBinArgs a) {
+  const int B = a.g.B, lane = threadIdx.x;
+  const int per = (B + 63) / 64;
+  const int i0 = lane * per, i1 = min(B, i0 + per);
   auto region = [&](int s) { return (static_cast<long long>(a.tot[s]) + kCabacGap + 7) & ~7ll; };
   long long loc = 0;
   for (int i = i0; i < i1; ++i) loc += region(i);
-  long long sum;
-  long long p = block_scan_excl(loc, s_sum, sum);
+  const long long incl = wave_scan_add(loc);
+  const long long sum = __shfl(incl, 63, 64);
+  long long p = incl - loc;
   const long long start = *a.pool_used;
   const bool fits = start + sum + kArithReadAhead <= a.pool_cap;  // the coder's read-ahead
   for (int i = i0; i < i1; ++i) {
@@ -216,8 +217,7 @@ __global__ __launch_bounds__(1024) void cabac_alloc(CabacBinArgs a) {
     a.total[i] = fits ? a.tot[i] : -1;
     p += region(i);
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
+  if (lane == 0) {
     if (fits) *a.pool_used = start + sum;
     else atomicOr(a.err, 4);
   }
@@ -503,10 +503,10 @@ extern "C" void mivc_launch_cabac_bin(int B, int wmb, int hmb, const void* hdr, 
   const dim3 mbgrid((nmb + 63) / 64, B);
   hipLaunchKernelGGL(cabac_mask, dim3((nmb + 1) / 2, B), dim3(64), 0, s, a);
   hipLaunchKernelGGL(cabac_prep, mbgrid, dim3(64), 0, s, a);
-  hipLaunchKernelGGL(cabac_chain, dim3(B), dim3(1024), 0, s, a);
+  hipLaunchKernelGGL(cabac_chain, dim3(B), dim3(64), 0, s, a);
   hipLaunchKernelGGL(cabac_count, mbgrid, dim3(64), 0, s, a);
-  hipLaunchKernelGGL(cabac_offsets, dim3(B), dim3(1024), 0, s, a);
-  hipLaunchKernelGGL(cabac_alloc, dim3(1), dim3(1024), 0, s, a);
+  hipLaunchKernelGGL(cabac_offsets, dim3(B), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(cabac_alloc, dim3(1), dim3(64), 0, s, a);
   hipLaunchKernelGGL(cabac_bins, mbgrid, dim3(64), 0, s, a);
 }
 

@@ -437,6 +437,7 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   int xa = wx & ~3, sh0 = wx - xa;
   const int wwords = (wrows + 3) / 4 + 1;
   if (R == 8) stage_window<(16 + 16 + kML + kMR + 3) / 4 + 1>(S, ref, W, H, xa, Y0 + cy - R - kML, wrows, wwords, lane);
+  else if (R == 4) stage_window<(16 + 8 + kML + kMR + 3) / 4 + 1>(S, ref, W, H, xa, Y0 + cy - R - kML, wrows, wwords, lane);
   else stage_window<0>(S, ref, W, H, xa, Y0 + cy - R - kML, wrows, wwords, lane);
   __syncthreads();
 
@@ -446,6 +447,8 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   int best_key;
   if (R == 8) {
     best_key = int_search_fixed<8>(S, sh0, lane, lambda, cx, cy, pmx, pmy);
+  } else if (R == 4) {  // B pictures: 81 candidates around the temporal-direct predictor
+    best_key = int_search_fixed<4>(S, sh0, lane, lambda, cx, cy, pmx, pmy);
   } else {
     const int ncand = side * side;
     best_key = 0x7FFFFFFF;

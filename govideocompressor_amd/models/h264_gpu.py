@@ -66,6 +66,9 @@ class H264Params:
     # only (the Baseline CAVLC path has no B slices).  b_qp_offset: x264 --pbratio 1.3
     bframes: int = 3
     b_qp_offset: int = 2
+    # integer search radius of the two B-picture searches (their predictors are the scaled
+    # co-located vectors of temporal direct, so a small window suffices)
+    b_me_range: int = int(os.environ.get("MIVC_B_ME_RANGE", 4))
 
     def eff_bframes(self) -> int:
         return max(0, int(self.bframes)) if self.cabac else 0
@@ -416,10 +419,11 @@ class GpuH264Encoder:
             dsf, copy = self._dist_scale(pic.poc, 2 * pic.l0, 2 * pic.l1)
             self.hip.b_direct(B, wmb, hmb, P(self.col_hdr), dsf, copy, P(self.dmv), P(self.pm0), P(self.pm1), s)
             self.intra_count.zero_()
+            br = self.p.b_me_range
             self.hip.me(B, wmb, hmb, sy, f0y, P(self.pm0), P(self.mv), P(self.me_cost), P(self.pred),
-                        P(self.intra_cost), P(self.qp), self.p.me_range, self.p.subpel, s, hp0, aq, 1)
+                        P(self.intra_cost), P(self.qp), br, self.p.subpel, s, hp0, aq, 1)
             self.hip.me(B, wmb, hmb, sy, f1y, P(self.pm1), P(self.mv1), P(self.me_cost1), P(self.pred1),
-                        P(self.intra_cost), P(self.qp), self.p.me_range, self.p.subpel, s, hp1, aq, 1)
+                        P(self.intra_cost), P(self.qp), br, self.p.subpel, s, hp1, aq, 1)
             self.hip.b_decide(B, wmb, hmb, sy, f0y, f1y, hp0, hp1, P(self.mv), P(self.mv1), P(self.me_cost),
                               P(self.me_cost1), P(self.pred), P(self.pred1), P(self.pm0), P(self.pm1), P(self.dmv),
                               P(self.qp), aq, P(hdr), P(self.pred_b), P(self.cost_b), s)
@@ -522,7 +526,8 @@ class GpuH264Encoder:
                 wrap_futs[t].result()  # host buffer r is free again
         buf = self.h_cab_out[r]
         if buf is None or buf.numel() < total:
-            buf = self.h_cab_out[r] = torch.empty((max(total, 1 << 26),), dtype=torch.uint8).pin_memory()
+            # pinning is slow (~ms per 10 MB): grow with headroom so it happens once or twice
+            buf = self.h_cab_out[r] = torch.empty((max(total + total // 2, 1 << 27),), dtype=torch.uint8).pin_memory()
         ds = self.d2h_stream
         with torch.cuda.device(self.dev), torch.cuda.stream(ds):
             ds.wait_event(self.cab_done[r])

@@ -2,4 +2,4 @@
 set -o pipefail
 export TMPDIR=/tmp
 out=$1; shift
-cd /tmp && MIVC_CABAC_GROUP=${MIVC_CABAC_GROUP:-8} timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/$out -o run -- python3 $GRAFT_REPO_ROOT/bench.py "$@" > $GRAFT_REPO_ROOT/gpurun_out/$out.log 2>&1
+cd /tmp && MIVC_CABAC_GROUP=${MIVC_CABAC_GROUP:-20} timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/$out -o run -- python3 $GRAFT_REPO_ROOT/bench.py "$@" > $GRAFT_REPO_ROOT/gpurun_out/$out.log 2>&1
