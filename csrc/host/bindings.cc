@@ -534,22 +534,32 @@ PYBIND11_MODULE(_host, m) {
   });
   // batched: one buffer of concatenated RBSPs + sizes -> list of NAL byte strings
   m.def("nal_wrap_many", [](py::array_t<uint8_t, py::array::c_style> buf, const std::vector<int64_t>& sizes,
-                            int nal_ref_idc, int nal_unit_type) {
+                            int nal_ref_idc, int nal_unit_type, int align) {
+    // slice RBSPs back to back in buf, each starting at a multiple of `align` bytes
+    if (align < 1 || (align & (align - 1))) throw std::invalid_argument("nal_wrap_many: align must be a power of 2");
+    int64_t need = 0;
+    for (int64_t sz : sizes) {
+      if (sz < 0) throw std::invalid_argument("nal_wrap_many: negative size");
+      need = ((need + align - 1) & ~static_cast<int64_t>(align - 1)) + sz;
+    }
+    if (need > static_cast<int64_t>(buf.size())) throw std::invalid_argument("nal_wrap_many: sizes exceed the buffer");
     std::vector<std::vector<uint8_t>> outs(sizes.size());
     {
       py::gil_scoped_release rel;
       const uint8_t* p = buf.data();
+      int64_t off = 0;
       for (size_t i = 0; i < sizes.size(); ++i) {
-        std::vector<uint8_t> v(p, p + sizes[i]);
+        off = (off + align - 1) & ~static_cast<int64_t>(align - 1);
+        std::vector<uint8_t> v(p + off, p + off + sizes[i]);
         outs[i].reserve(v.size() + v.size() / 64 + 8);
         append_nal(outs[i], nal_ref_idc, nal_unit_type, v);
-        p += sizes[i];
+        off += sizes[i];
       }
     }
     py::list l;
     for (auto& o : outs) l.append(to_bytes(o));
     return l;
-  });
+  }, py::arg("buf"), py::arg("sizes"), py::arg("nal_ref_idc"), py::arg("nal_unit_type"), py::arg("align") = 1);
 
   m.def("parse_nals", [](py::bytes data) {
     std::string s = data;

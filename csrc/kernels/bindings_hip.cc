@@ -77,7 +77,7 @@ void mivc_launch_cabac_bin(int B, int wmb, int hmb, const void* hdr, const int16
 void mivc_launch_cabac_code(int L, int B, uint16_t* pool, const long long* base, const int* total,
                             const uint32_t* hdr_bits, const int* hdr_nbits, const int* slot_qp,
                             unsigned long long itypes, int* bytes, uint8_t* out, long long* out_off, int* err,
-                            void* stream);
+                            uint8_t* host_out, long long host_cap, void* stream);
 void mivc_launch_cavlc(int B, int wmb, int hmb, const void* hdr, const int16_t* coef, void* mbs, int* len,
                        long long* off, int* trail, long long* total_bits, int* slot_bytes, uint32_t* words,
                        long long cap_words, const uint32_t* hdr_bits, const int* hdr_nbits, int pslice, int slice_qp,
@@ -263,11 +263,13 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("cabac_code", [](int L, int B, uintptr_t pool, uintptr_t base, uintptr_t total, uintptr_t hdr_bits,
                          uintptr_t hdr_nbits, uintptr_t slot_qp, unsigned long long itypes, uintptr_t bytes,
-                         uintptr_t out, uintptr_t out_off, uintptr_t err, uintptr_t stream) {
+                         uintptr_t out, uintptr_t out_off, uintptr_t err, uintptr_t stream, uintptr_t host_out,
+                         long long host_cap) {
     if (B < 1 || L < 1 || L % B != 0 || L / B > 64) throw std::invalid_argument("cabac_code: L must be G * B, G <= 64");
+    if ((out & 15) || (host_out & 15)) throw std::invalid_argument("cabac_code: output buffers must be 16-byte aligned");
     mivc_launch_cabac_code(L, B, P<uint16_t>(pool), P<long long>(base), P<int>(total), P<uint32_t>(hdr_bits),
                            P<int>(hdr_nbits), P<int>(slot_qp), itypes, P<int>(bytes), P<uint8_t>(out),
-                           P<long long>(out_off), P<int>(err), S(stream));
+                           P<long long>(out_off), P<int>(err), P<uint8_t>(host_out), host_cap, S(stream));
   });
   m.def("cavlc", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t coef, uintptr_t mbs, uintptr_t len, uintptr_t off,
                     uintptr_t trail, uintptr_t total_bits, uintptr_t slot_bytes, uintptr_t words, long long cap_words,

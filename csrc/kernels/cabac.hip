@@ -21,7 +21,8 @@
 //     cabac_arith   (G*B/lpw, 64)          context states in LDS (one column per lane),
 //                                          header bytes + arithmetic coding, output written
 //                                          in place over the slice's consumed symbols
-//     cabac_compact (G*B, 256)             slice outputs packed back to back
+//     cabac_compact (G*B, 256)             slice outputs packed (16-byte aligned starts),
+//                                          straight into pinned host memory when they fit
 // The serial stage is latency-bound (a chain of dependent LDS reads per bin), so its
 // throughput scales with the number of independent slices in flight: grouping G frame
 // steps multiplies the waves the chip runs at once by G.
@@ -283,9 +284,11 @@ struct CabacCodeArgs {
   const int* slot_qp;        // [L] slice QP
   unsigned long long itypes; // bit g: frame step g is an I slice (else P)
   int* bytes;                // [L] out: slice RBSP bytes (-1: error)
-  uint8_t* out;              // compacted slices
+  uint8_t* out;              // compacted slices (device; used when they exceed host_cap)
   long long* out_off;        // [L]
   int* err;
+  uint8_t* host_out;         // pinned host buffer, device-visible (nullable)
+  long long host_cap;
 };
 
 // Output of one lane's slice: bytes collect in a 256-byte LDS ring and leave as aligned
@@ -444,22 +447,33 @@ __global__ __launch_bounds__(64) void cabac_arith(CabacCodeArgs a) {
   if (bad) atomicOr(a.err, 8);
 }
 
+// Slice outputs packed in l order, each starting on a 16-byte boundary, with 16-byte
+// stores (the region bases in the pool are 16-byte aligned).  Into pinned host memory when
+// the whole group fits host_cap (zero-copy: the bytes cross PCIe inside this kernel, in
+// stream order after the coder, so no D2H copy has to be ordered against the next group),
+// else into the device buffer.
 __global__ __launch_bounds__(256) void cabac_compact(CabacCodeArgs a) {
   const int l = blockIdx.x;
-  __shared__ long long s_off;
-  if (threadIdx.x == 0) s_off = 0;
+  __shared__ unsigned long long s_off, s_tot;
+  if (threadIdx.x == 0) s_off = s_tot = 0;
   __syncthreads();
-  long long part = 0;
-  for (int s = threadIdx.x; s < l; s += blockDim.x) part += a.bytes[s] > 0 ? a.bytes[s] : 0;
-  atomicAdd(reinterpret_cast<unsigned long long*>(&s_off), static_cast<unsigned long long>(part));
+  unsigned long long part = 0, tot = 0;
+  for (int s = threadIdx.x; s < a.L; s += blockDim.x) {
+    const unsigned long long r16 = a.bytes[s] > 0 ? ((static_cast<unsigned long long>(a.bytes[s]) + 15ull) & ~15ull) : 0ull;
+    tot += r16;
+    if (s < l) part += r16;
+  }
+  atomicAdd(&s_off, part);
+  atomicAdd(&s_tot, tot);
   __syncthreads();
-  const long long off = s_off;
+  const long long off = static_cast<long long>(s_off);
+  const bool host = a.host_out && static_cast<long long>(s_tot) <= a.host_cap;
   if (threadIdx.x == 0) a.out_off[l] = off;
   const int nbytes = a.bytes[l];
   if (nbytes <= 0) return;
-  const uint8_t* src = reinterpret_cast<const uint8_t*>(a.pool + a.base[l]);
-  uint8_t* dst = a.out + off;
-  for (int i = threadIdx.x; i < nbytes; i += blockDim.x) dst[i] = src[i];
+  const uint4* src = reinterpret_cast<const uint4*>(a.pool + a.base[l]);
+  uint4* dst = reinterpret_cast<uint4*>((host ? a.host_out : a.out) + off);
+  for (int i = threadIdx.x; i < (nbytes + 15) / 16; i += blockDim.x) dst[i] = src[i];
 }
 
 }  // namespace gpu
@@ -515,7 +529,7 @@ extern "C" void mivc_launch_cabac_bin(int B, int wmb, int hmb, const void* hdr, 
 extern "C" void mivc_launch_cabac_code(int L, int B, uint16_t* pool, const long long* base, const int* total,
                                        const uint32_t* hdr_bits, const int* hdr_nbits, const int* slot_qp,
                                        unsigned long long itypes, int* bytes, uint8_t* out, long long* out_off,
-                                       int* err, void* stream) {
+                                       int* err, uint8_t* host_out, long long host_cap, void* stream) {
   CabacCodeArgs a;
   a.L = L;
   a.B = B;
@@ -530,6 +544,15 @@ extern "C" void mivc_launch_cabac_code(int L, int B, uint16_t* pool, const long 
   a.out = out;
   a.out_off = out_off;
   a.err = err;
+  a.host_out = nullptr;
+  a.host_cap = 0;
+  if (host_out) {
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, host_out, 0) == hipSuccess && dp) {
+      a.host_out = static_cast<uint8_t*>(dp);
+      a.host_cap = host_cap;
+    }
+  }
   hipStream_t s = static_cast<hipStream_t>(stream);
   // full waves: spreading the slices over more, partly empty waves was measured slower
   // (the coder's issue cycles come out of the concurrently running encode kernels)

@@ -341,10 +341,12 @@ class GpuH264Encoder:
         self.cab_off = torch.zeros((B, nmb), dtype=i64, device=dev)
         self.cab_tot = torch.zeros((B,), dtype=i32, device=dev)
         self.entropy_stream = torch.cuda.Stream(device=dev)
-        self.d2h_stream = torch.cuda.Stream(device=dev)  # the copy thread's byte copies
         self.cab_bin_done = [torch.cuda.Event() for _ in range(2)]
         self.cab_done = [torch.cuda.Event() for _ in range(2)]
-        self.h_cab_out: list = [None, None]
+        # the coder's compaction writes the slice bytes straight into these pinned buffers
+        # (one per ring; a group that does not fit falls back to the device buffer + D2H)
+        self.cab_host_cap = min(comp_cap, int(os.environ.get("MIVC_CABAC_HOST_MB", 1024)) << 20)
+        self.h_cab_out = [torch.empty((self.cab_host_cap,), dtype=u8).pin_memory() for _ in range(2)]
         self.copy_pool = cf.ThreadPoolExecutor(max_workers=1)
 
     # ------------------------------------------------------------------ helpers
@@ -459,13 +461,29 @@ class GpuH264Encoder:
         return dict(idr=int(pic.kind == "I"), frame_num=pic.frame_num, idr_pic_id=idr_ids[b] & 0xFFFF, qp=qp_frame,
                     slice_type=pic.slice_type, nal_ref_idc=pic.nal_ref_idc, poc=pic.poc, direct_spatial=0)
 
-    def _gpu_cabac_bin(self, k: int, t: int, pic: PicPlan, qps_t, idr_ids: list[int], qp_dev: torch.Tensor):
+    @staticmethod
+    def _cabac_groups(F: int, G: int) -> list[tuple[int, int]]:
+        """(first step, steps) of the arithmetic-coder groups of an F-step batch: G steps each,
+        the last full-size group split in two so the coder's tail after the final encode
+        kernel (nothing left to overlap it with) is half a group."""
+        sizes = [G] * (F // G) + ([F % G] if F % G else [])
+        if sizes and sizes[-1] > max(1, G // 2):
+            last = sizes.pop()
+            sizes += [(last + 1) // 2, last // 2]
+        out, t0 = [], 0
+        for n in sizes:
+            out.append((t0, n))
+            t0 += n
+        return out
+
+    def _gpu_cabac_bin(self, k: int, g: int, j: int, pic: PicPlan, qps_t, idr_ids: list[int],
+                       qp_dev: torch.Tensor):
         """Binarise frame step t (records hdr[k]/coef[k]) into the symbol pool of its group
         ring, on the *copy* stream (the caller's current stream): the records are free
         again once this is done, whatever the arithmetic coder is doing.
         qp_dev: [B] int32 slice QPs of this step in a buffer that outlives the launch."""
         G, B = self.cab_G, self.B
-        r, j = (t // G) & 1, t % G
+        r = g & 1
         if j == 0:
             self.cab_pool_used[r].zero_()
         self._header_bits_into(self.h_cab_hdr_bits[r][j * B:(j + 1) * B], self.h_cab_hdr_nbits[r][j * B:(j + 1) * B],
@@ -478,11 +496,11 @@ class GpuH264Encoder:
                            self.cab_total[r][j * B:].data_ptr(), P(qp_dev), pic.slice_type, 1, 1, 0, P(self.err),
                            self.copy_stream.cuda_stream)
 
-    def _gpu_cabac_code(self, t0: int, n: int, qps_d: torch.Tensor):
+    def _gpu_cabac_code(self, g: int, t0: int, n: int, qps_d: torch.Tensor):
         """Arithmetic-code the n frame steps t0 .. t0 + n - 1 of a group (n * B slices) on
         the entropy stream, after their binarisation; sizes go to pinned host memory."""
         G, B = self.cab_G, self.B
-        r = (t0 // G) & 1
+        r = g & 1
         self.cab_bin_done[r].record(self.copy_stream)
         itypes = 1 if t0 == 0 else 0  # frame step 0 is the IDR picture
         P = self._ptr
@@ -492,15 +510,17 @@ class GpuH264Encoder:
             self.hip.cabac_code(n * B, B, P(self.cab_pool[r]), P(self.cab_base[r]), P(self.cab_total[r]),
                                 P(self.cab_hdr_bits[r]), P(self.cab_hdr_nbits[r]), qps_d[t0].data_ptr(), itypes,
                                 P(self.cab_bytes[r]), P(self.cab_comp[r]), P(self.cab_comp_off[r]), P(self.err),
-                                es.cuda_stream)
+                                es.cuda_stream, P(self.h_cab_out[r]), self.cab_host_cap)
             self.h_cab_bytes[r][: n * B].copy_(self.cab_bytes[r][: n * B], non_blocking=True)
             self.h_pool_used[r].copy_(self.cab_pool_used[r:r + 1], non_blocking=True)
             self.cab_done[r].record(es)
 
-    def _copy_out_group(self, g: int, t0: int, n: int, copied, wrap_futs, plan: list[PicPlan]):
-        """Copy thread (groups in order): sizes -> compacted bytes D2H -> NAL wrapping of each
-        frame step on the pool.  ``copied[g]`` releases ring g % 2 (pool, headers, pinned
-        sizes) for group g + 2."""
+    def _copy_out_group(self, g: int, t0: int, n: int, copied, wrap_futs, plan: list[PicPlan], groups):
+        """Copy thread (groups in order): wait for the coder, then hand each frame step's
+        slices (already in pinned host memory, 16-byte aligned) to the NAL-wrapping pool.
+        ``copied[g]`` (set once the wraps are submitted) releases ring g % 2 (pool, headers,
+        pinned sizes) for group g + 2; the host buffer itself is reused by group g + 2's
+        coder only after these wraps finished (the main thread waits for them)."""
         B, G = self.B, self.cab_G
         r = g & 1
         t_0 = time.perf_counter()
@@ -520,31 +540,28 @@ class GpuH264Encoder:
                 raise RuntimeError("GPU CABAC: symbol pool exhausted (raise MIVC_CABAC_SYMS_PER_MB / "
                                    "MIVC_CABAC_PEAK_SYMS_PER_MB or lower cabac_group)")
             raise RuntimeError("GPU CABAC: arithmetic coder error")
-        total = int(sizes.sum())
-        if g >= 2:
-            for t in range(t0 - 2 * G, t0 - G):
-                wrap_futs[t].result()  # host buffer r is free again
+        r16 = (sizes + 15) & ~15
+        total = int(r16.sum())
         buf = self.h_cab_out[r]
-        if buf is None or buf.numel() < total:
-            # pinning is slow (~ms per 10 MB): grow with headroom so it happens once or twice
-            buf = self.h_cab_out[r] = torch.empty((max(total + total // 2, 1 << 27),), dtype=torch.uint8).pin_memory()
-        ds = self.d2h_stream
-        with torch.cuda.device(self.dev), torch.cuda.stream(ds):
-            ds.wait_event(self.cab_done[r])
-            buf[:total].copy_(self.cab_comp[r][:total], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(ds)
-        ev.synchronize()
-        copied[g].set()
+        if total > self.cab_host_cap:
+            # the group did not fit the pinned buffer: the compaction left it on the device
+            buf = torch.empty((total,), dtype=torch.uint8).pin_memory()
+            with torch.cuda.device(self.dev), torch.cuda.stream(self.entropy_stream):
+                buf.copy_(self.cab_comp[r][:total], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.entropy_stream)
+            ev.synchronize()
+            self.stats["cabac_host_spills"] = self.stats.get("cabac_host_spills", 0) + 1
         t_2 = time.perf_counter()
         self.timings["entropy_wait_gpu_s"] = self.timings.get("entropy_wait_gpu_s", 0.0) + (t_1 - t_0)
         self.timings["d2h_s"] = self.timings.get("d2h_s", 0.0) + (t_2 - t_1)
         off = 0
         for jj in range(n):
             sz = sizes[jj * B:(jj + 1) * B]
-            nb = int(sz.sum())
-            wrap_futs[t0 + jj] = self.pool.submit(self._wrap, buf[off:off + nb], nb, sz.tolist(), plan[t0 + jj])
+            nb = int(r16[jj * B:(jj + 1) * B].sum())
+            wrap_futs[t0 + jj] = self.pool.submit(self._wrap, buf[off:off + nb], nb, sz.tolist(), plan[t0 + jj], 16)
             off += nb
+        copied[g].set()
 
     def _header_bits(self, k: int, pic: PicPlan, qps_t, idr_ids: list[int]):
         """Slice headers of this step -> pinned host words -> device (current stream)."""
@@ -606,9 +623,10 @@ class GpuH264Encoder:
         self.timings["d2h_s"] = self.timings.get("d2h_s", 0.0) + (t2 - t1)
         wrap_futs[t] = self.pool.submit(self._wrap, buf, total, sizes, pic)
 
-    def _wrap(self, buf, total: int, sizes: list[int], pic: PicPlan) -> list[tuple[bytes, int]]:
+    def _wrap(self, buf, total: int, sizes: list[int], pic: PicPlan, align: int = 1) -> list[tuple[bytes, int]]:
         t0 = time.perf_counter()
-        nals = self.host.nal_wrap_many(buf[:total].numpy(), sizes, pic.nal_ref_idc, 5 if pic.kind == "I" else 1)
+        nals = self.host.nal_wrap_many(buf[:total].numpy(), sizes, pic.nal_ref_idc, 5 if pic.kind == "I" else 1,
+                                       align)
         self.timings["entropy_s"] = self.timings.get("entropy_s", 0.0) + (time.perf_counter() - t0)
         return [(n, len(n) * 8) for n in nals]
 
@@ -724,8 +742,12 @@ class GpuH264Encoder:
                 if copy_futs[i].done() and copy_futs[i].exception() is not None:
                     raise copy_futs[i].exception()
         cabac_gpu = self.entropy == "gpu" and self.p.cabac
-        G = self.cab_G if cabac_gpu else 1
-        ngroups = (F + G - 1) // G
+        groups = self._cabac_groups(F, self.cab_G) if cabac_gpu else [(t, 1) for t in range(F)]
+        step_group = {}
+        for gi, (a0, an) in enumerate(groups):
+            for jj in range(an):
+                step_group[a0 + jj] = (gi, jj)
+        ngroups = len(groups)
         group_copied = [threading.Event() for _ in range(ngroups)]
         group_futs: list = [None] * ngroups
 
@@ -743,8 +765,9 @@ class GpuH264Encoder:
             # the device/pinned buffers of slot k were last used by step t-2: wait for them
             tw = time.perf_counter()
             if cabac_gpu:
-                if t % G == 0 and t >= 2 * G:
-                    wait_group(t // G - 2)  # ring (t // G) % 2 is free again
+                gi, jj = step_group[t]
+                if jj == 0 and gi >= 2:
+                    wait_group(gi - 2)  # ring gi % 2 is free again
             elif self.entropy == "gpu" and t >= 2:
                 wait_copied(t - 2)
             elif pending[k] is not None:
@@ -772,7 +795,7 @@ class GpuH264Encoder:
             with torch.cuda.stream(self.copy_stream):
                 self.copy_stream.wait_event(self.compute_done[k])
                 if cabac_gpu:
-                    self._gpu_cabac_bin(k, t, pic, qpt, idr_ids, qps_d[t])
+                    self._gpu_cabac_bin(k, gi, jj, pic, qpt, idr_ids, qps_d[t])
                 elif self.entropy == "gpu":
                     self.h_sizes[k].copy_(self.cav_sizes[k], non_blocking=True)
                 else:
@@ -780,11 +803,19 @@ class GpuH264Encoder:
                     self.h_coef[k].copy_(self.coef[k], non_blocking=True)
                 self.copy_done[k].record(self.copy_stream)
             if cabac_gpu:
-                if t % G == G - 1 or t == F - 1:
-                    g, t0 = t // G, t - t % G
-                    self._gpu_cabac_code(t0, t - t0 + 1, qps_d)
-                    group_futs[g] = self.copy_pool.submit(self._copy_out_group, g, t0, t - t0 + 1, group_copied,
-                                                          wrap_futs, plan)
+                if jj == groups[gi][1] - 1:
+                    t0 = groups[gi][0]
+                    if gi >= 2:
+                        # this group's compaction overwrites host buffer gi % 2: group gi - 2's
+                        # wraps must be done reading it (copied[gi - 2] was waited for above)
+                        tw = time.perf_counter()
+                        a0, an = groups[gi - 2]
+                        for tt in range(a0, a0 + an):
+                            wrap_futs[tt].result()
+                        self.timings["host_blocked_s"] += time.perf_counter() - tw
+                    self._gpu_cabac_code(gi, t0, t - t0 + 1, qps_d)
+                    group_futs[gi] = self.copy_pool.submit(self._copy_out_group, gi, t0, t - t0 + 1, group_copied,
+                                                           wrap_futs, plan, groups)
             elif self.entropy == "gpu":
                 copy_futs[t] = self.copy_pool.submit(self._copy_out, t, k, pic, copied, wrap_futs)
             else:
