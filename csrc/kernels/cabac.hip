@@ -344,6 +344,39 @@ struct RingOut {
   }
 };
 
+// Branch-free symbol step of the GPU coder (the bytes equal CabacSymbolCoder::step_nodrain,
+// which the host tests pin): every symbol reads and writes a context state -- bypass and
+// terminate symbols use a dummy context row -- and one 8-byte table entry per state holds
+// the four rLPS values and both transitions, so a symbol costs two dependent LDS reads and
+// no exec-mask branches (the generic step branched around its LDS accesses).
+constexpr int kDummyCtx = h264::kCabacContexts;  // extra LDS row absorbing non-decision symbols
+
+template <class C>
+__device__ __forceinline__ void fast_step(C& c, uint32_t sym, uint8_t* st_lane, const uint2* tab) {
+  const bool dec = !(sym & 0x8000u);
+  const bool byp = (sym & 0xC000u) == 0x8000u;
+  uint8_t* sp = st_lane + (dec ? (sym & 0x1FFu) : static_cast<uint32_t>(kDummyCtx)) * 64u;
+  const uint32_t sv = *sp;
+  const uint32_t pst = sv >> 1, mps = sv & 1u;
+  const uint2 t = tab[pst];
+  const uint32_t rl = (t.x >> ((c.range >> 3) & 24u)) & 0xFFu;
+  const uint32_t rlps = dec ? rl : 2u;
+  const uint32_t r1 = c.range - rlps;
+  const bool lpsb = dec && ((sym >> 9) & 1u) != mps;
+  const uint32_t nr = lpsb ? rlps : r1;
+  const uint32_t add = lpsb ? r1 : 0u;
+  const uint32_t npst = lpsb ? (t.y & 0xFFu) : ((t.y >> 8) & 0xFFu);
+  const uint32_t nmps = mps ^ ((lpsb && pst == 0) ? 1u : 0u);
+  *sp = static_cast<uint8_t>((npst << 1) | nmps);
+  const int shd = h264::cabac_clz32(nr) - 23;
+  const int n = byp ? static_cast<int>((sym >> 10) & 15u) : (shd > 0 ? shd : 0);
+  const uint32_t bterm = c.range * (byp ? (sym & 0x3FFu) : 0u);  // < 2^19
+  const uint32_t nrs = nr << n;
+  c.low = ((c.low + add) << n) + bterm;
+  c.range = byp ? c.range : nrs;
+  c.nbits += n;
+}
+
 constexpr int kArithBlock = 64;         // symbols per lane per block (8 x 16-byte loads)
 constexpr int kArithInStride = 9;       // uint4 per lane in LDS (8 + 1 pad: conflict-free b128 reads)
 constexpr int kArithRingStride = 260;   // bytes per lane ring (256 + 4 pad)
@@ -354,16 +387,20 @@ constexpr int kArithRingStride = 260;   // bytes per lane ring (256 + 4 pad)
 // complete dwords are stored.  The only vmcnt wait per block covers loads and stores issued
 // a whole block earlier.
 __global__ __launch_bounds__(64) void cabac_arith(CabacCodeArgs a) {
-  __shared__ uint8_t st[h264::kCabacContexts * 64];
-  __shared__ uint8_t lps[64 * 4];
-  __shared__ uint8_t trans[64];
+  __shared__ uint8_t st[(h264::kCabacContexts + 1) * 64];
+  __shared__ uint2 tab[64];
   __shared__ uint4 sin[64 * kArithInStride];
   __shared__ __attribute__((aligned(16))) uint8_t ring[64 * kArithRingStride];
   const int lane = threadIdx.x;
   const int l = blockIdx.x * a.lpw + lane;
   const bool live = lane < a.lpw && l < a.L;
-  for (int i = lane; i < 256; i += 64) lps[i] = h264::kCabacRangeLPS[i >> 2][i & 3];
-  trans[lane] = h264::kCabacTransLPS[lane];
+  tab[lane] = make_uint2(static_cast<uint32_t>(h264::kCabacRangeLPS[lane][0]) |
+                            (static_cast<uint32_t>(h264::kCabacRangeLPS[lane][1]) << 8) |
+                            (static_cast<uint32_t>(h264::kCabacRangeLPS[lane][2]) << 16) |
+                            (static_cast<uint32_t>(h264::kCabacRangeLPS[lane][3]) << 24),
+                        static_cast<uint32_t>(h264::kCabacTransLPS[lane]) |
+                            (static_cast<uint32_t>(lane < 62 ? lane + 1 : 62) << 8));
+  st[kDummyCtx * 64 + lane] = 0;
   // context states of this lane's slice (its slice type and QP; cabac_init_idc 0)
   const int qp = live ? h264::clip3(0, 51, a.slot_qp[l]) : 26;
   const int table = live && ((a.itypes >> (l / a.B)) & 1ull) ? 0 : 1;
@@ -419,16 +456,19 @@ __global__ __launch_bounds__(64) void cabac_arith(CabacCodeArgs a) {
     for (int ch = 0; ch * 8 < m; ++ch) {
       const uint4 cw = my[ch];
       const int mm = min(8, m - ch * 8);
-      // lazy draining: at most 4 symbols (<= 40 bits) between drains (see CabacSymbolCoder)
-      c.step_nodrain(cw.x & 0xFFFFu, st + lane, 64, lps, trans);
-      if (mm > 1) c.step_nodrain(cw.x >> 16, st + lane, 64, lps, trans);
-      if (mm > 2) c.step_nodrain(cw.y & 0xFFFFu, st + lane, 64, lps, trans);
-      if (mm > 3) c.step_nodrain(cw.y >> 16, st + lane, 64, lps, trans);
+      // lazy draining: at most 4 symbols (<= 40 bits) between drains (see CabacSymbolCoder).
+      // Symbols past the slice's end become 0x8000 (a bypass batch of no bins: a no-op),
+      // so every lane runs the same straight-line code.
+      auto sym = [&](uint32_t w, int k) { return k < mm ? w : 0x8000u; };
+      fast_step(c, sym(cw.x & 0xFFFFu, 0), st + lane, tab);
+      fast_step(c, sym(cw.x >> 16, 1), st + lane, tab);
+      fast_step(c, sym(cw.y & 0xFFFFu, 2), st + lane, tab);
+      fast_step(c, sym(cw.y >> 16, 3), st + lane, tab);
       c.drain();
-      if (mm > 4) c.step_nodrain(cw.z & 0xFFFFu, st + lane, 64, lps, trans);
-      if (mm > 5) c.step_nodrain(cw.z >> 16, st + lane, 64, lps, trans);
-      if (mm > 6) c.step_nodrain(cw.w & 0xFFFFu, st + lane, 64, lps, trans);
-      if (mm > 7) c.step_nodrain(cw.w >> 16, st + lane, 64, lps, trans);
+      fast_step(c, sym(cw.z & 0xFFFFu, 4), st + lane, tab);
+      fast_step(c, sym(cw.z >> 16, 5), st + lane, tab);
+      fast_step(c, sym(cw.w & 0xFFFFu, 6), st + lane, tab);
+      fast_step(c, sym(cw.w >> 16, 7), st + lane, tab);
       c.drain();
     }
     my[0] = n0;
