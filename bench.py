@@ -43,6 +43,8 @@ def main() -> None:
     ap.add_argument("--crf", type=float, default=23.0)
     ap.add_argument("--bframes", type=int, default=int(os.environ.get("MIVC_BENCH_BFRAMES", "3")),
                     help="B pictures between anchors (x264 default 3)")
+    ap.add_argument("--cavlc", action="store_true",
+                    help="Constrained Baseline CAVLC (the round-1 encoder) instead of Main CABAC")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--no-quality", dest="quality", action="store_false",
                     help="skip the PSNR/SSIM measurement of the first warmup step")
@@ -59,7 +61,7 @@ def main() -> None:
     if env.world != a.gpus:
         if env.is_main:
             print(f"warning: --gpus {a.gpus} but WORLD_SIZE {env.world}", file=sys.stderr)
-    p = H264Params(width=a.width, height=a.height, fps=30.0, crf=a.crf, bframes=a.bframes)
+    p = H264Params(width=a.width, height=a.height, fps=30.0, crf=a.crf, bframes=a.bframes, cabac=not a.cavlc)
     enc = GpuH264Encoder(p, slots=a.slots, device=env.device,
                          entropy_threads=int(os.environ.get("MIVC_ENTROPY_THREADS", "16")))
     B, F = a.slots, a.frames

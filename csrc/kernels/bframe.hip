@@ -240,6 +240,98 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- P_Skip-aware vector choice
+// ME prices vectors against a temporal predictor, so on noisy content neighbouring MBs of
+// one uniform motion pick slightly different quarter-sample vectors and none of them can
+// be coded as P_Skip (mv == the skip predictor, no residual) -- every MB pays mb_type +
+// mvd bins even where the residual quantises to zero.  This pass (Jacobi, over the whole
+// picture in parallel) offers each MB the P_Skip predictor computed from its neighbours'
+// current vectors (clause 8.4.1.1: 0 if A or B is unavailable or a zero vector, else the
+// median of A, B, C/D) and takes it when SATD(skip prediction) <= SATD(own vector) +
+// lambda * mvd bits.  Two passes let a uniform field settle; the writer still derives
+// skip exactly from the final records.
+struct PRefineArgs {
+  Geom g;
+  const uint8_t* src_y;
+  const uint8_t* ref;       // G plane of the reference
+  const uint8_t* hp;        // its half-sample planes
+  const int16_t* mv_in;     // [B, nmb, 2]
+  int16_t* mv_out;          // [B, nmb, 2]
+  int* cost;                // [B, nmb] ME cost (SATD + lambda * bits vs pm), updated in place
+  const int16_t* pm;        // [B, nmb, 2] the ME's predictor (to recover the SATD part of cost)
+  uint8_t* pred;            // [B, nmb, 256] luma prediction, rewritten for MBs that switch
+  const int* qp;
+  const int8_t* aq;
+};
+
+__device__ __forceinline__ int median3(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
+
+__global__ __launch_bounds__(64) void p_mv_refine(PRefineArgs a) {
+  const Geom& g = a.g;
+  const int nmb = g.nmb();
+  const int mb = blockIdx.x, slot = blockIdx.y, lane = threadIdx.x;
+  const size_t o = static_cast<size_t>(slot) * nmb + mb;
+  const int mx = mb % g.wmb, my = mb / g.wmb;
+  const int16_t* mv = a.mv_in + static_cast<size_t>(slot) * nmb * 2;
+  const int cx = mv[mb * 2], cy = mv[mb * 2 + 1];
+  // P_Skip predictor from the neighbours' current vectors (all list 0, ref 0)
+  const bool hasA = mx > 0, hasB = my > 0, hasC = my > 0 && mx < g.wmb - 1, hasD = mx > 0 && my > 0;
+  int sx = 0, sy = 0;
+  if (hasA && hasB) {
+    const int ax = mv[(mb - 1) * 2], ay = mv[(mb - 1) * 2 + 1];
+    const int bx = mv[(mb - g.wmb) * 2], by = mv[(mb - g.wmb) * 2 + 1];
+    if (!((ax == 0 && ay == 0) || (bx == 0 && by == 0))) {
+      const int cn = hasC ? mb - g.wmb + 1 : (hasD ? mb - g.wmb - 1 : -1);
+      const int ccx = cn >= 0 ? mv[cn * 2] : 0, ccy = cn >= 0 ? mv[cn * 2 + 1] : 0;
+      sx = median3(ax, bx, ccx);
+      sy = median3(ay, by, ccy);
+    }
+  }
+  if (sx == cx && sy == cy) {
+    if (lane == 0) {
+      a.mv_out[o * 2] = static_cast<int16_t>(cx);
+      a.mv_out[o * 2 + 1] = static_cast<int16_t>(cy);
+    }
+    return;
+  }
+  const int W = g.W, H = g.H;
+  const int r = lane >> 2, c0 = (lane & 3) * 4;
+  const int X = mx * 16 + c0, Y = my * 16 + r;
+  const size_t yo = static_cast<size_t>(slot) * g.ysize();
+  const uint8_t* G0 = a.ref + yo;
+  const uint8_t* H0 = a.hp + static_cast<size_t>(slot) * 3 * (W + 2 * kHpMargin) * (H + 2 * kHpMargin);
+  const uint32_t src = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y) * W + X);
+  const uint32_t ps = mc4(G0, H0, W, H, X, Y, sx, sy);
+  __shared__ int s_res[256];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    s_res[r * 16 + c0 + k] = static_cast<int>((src >> (8 * k)) & 255u) - static_cast<int>((ps >> (8 * k)) & 255u);
+  wave_sync();
+  int satd = 0;
+  if (lane < 16) {
+    const int bx = (lane & 3) * 4, by = (lane >> 2) * 4;
+    int rr[16];
+#pragma unroll
+    for (int y = 0; y < 4; ++y)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) rr[y * 4 + x] = s_res[(by + y) * 16 + bx + x];
+    satd = h264::satd4x4(rr);
+  }
+  satd = __builtin_amdgcn_readlane(sum16(satd), 0);
+  const int qp = clampi(a.qp[slot] + (a.aq ? a.aq[o] : 0), 0, 51);
+  const int lambda = h264::kLambda[qp];
+  const int pmx = a.pm ? a.pm[o * 2] : 0, pmy = a.pm ? a.pm[o * 2 + 1] : 0;
+  const int satd_me = a.cost[o] - lambda * (mvbits_se(cx - pmx) + mvbits_se(cy - pmy));
+  const int c_me = satd_me + lambda * (mvbits_se(cx - sx) + mvbits_se(cy - sy) + 1);
+  const bool take = satd <= c_me;
+  if (take) *reinterpret_cast<uint32_t*>(a.pred + o * 256 + r * 16 + c0) = ps;
+  if (lane == 0) {
+    a.mv_out[o * 2] = static_cast<int16_t>(take ? sx : cx);
+    a.mv_out[o * 2 + 1] = static_cast<int16_t>(take ? sy : cy);
+    if (take) a.cost[o] = satd + lambda * (mvbits_se(sx - pmx) + mvbits_se(sy - pmy));
+  }
+}
+
 }  // namespace gpu
 }  // namespace mivc
 
@@ -286,4 +378,23 @@ extern "C" void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src
   a.pred_out = pred_out;
   a.cost_out = cost_out;
   hipLaunchKernelGGL(b_decide, dim3(wmb * hmb, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
+}
+
+extern "C" void mivc_launch_p_refine(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref,
+                                     const uint8_t* hp, const int16_t* mv_in, int16_t* mv_out, int* cost,
+                                     const int16_t* pm, uint8_t* pred, const int* qp, const int8_t* aq,
+                                     void* stream) {
+  PRefineArgs a;
+  a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
+  a.src_y = src_y;
+  a.ref = ref;
+  a.hp = hp;
+  a.mv_in = mv_in;
+  a.mv_out = mv_out;
+  a.cost = cost;
+  a.pm = pm;
+  a.pred = pred;
+  a.qp = qp;
+  a.aq = aq;
+  hipLaunchKernelGGL(p_mv_refine, dim3(wmb * hmb, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
 }

@@ -22,6 +22,9 @@ void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t
                     int subpel, uint8_t* hp, const int8_t* aq, int planes_ready, void* stream);
 void mivc_launch_b_direct(int B, int wmb, int hmb, const void* col, int dsf, int direct_copy, int16_t* dmv,
                           int16_t* pm0, int16_t* pm1, void* stream);
+void mivc_launch_p_refine(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref, const uint8_t* hp,
+                          const int16_t* mv_in, int16_t* mv_out, int* cost, const int16_t* pm, uint8_t* pred,
+                          const int* qp, const int8_t* aq, void* stream);
 void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref0, const uint8_t* ref1,
                           const uint8_t* hp0, const uint8_t* hp1, const int16_t* mv0, const int16_t* mv1,
                           const int* cost0, const int* cost1, const uint8_t* pred0, const uint8_t* pred1,
@@ -134,6 +137,14 @@ PYBIND11_MODULE(_hip, m) {
                        uintptr_t pm1, uintptr_t stream) {
     mivc_launch_b_direct(B, wmb, hmb, P<void>(col), dsf, direct_copy, P<int16_t>(dmv), P<int16_t>(pm0),
                          P<int16_t>(pm1), S(stream));
+  });
+  m.def("p_refine", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref, uintptr_t hp, uintptr_t mv_in,
+                       uintptr_t mv_out, uintptr_t cost, uintptr_t pm, uintptr_t pred, uintptr_t qp, uintptr_t aq,
+                       uintptr_t stream) {
+    if (mv_in == mv_out) throw std::invalid_argument("p_refine: mv_in and mv_out must differ (Jacobi pass)");
+    mivc_launch_p_refine(B, wmb, hmb, P<uint8_t>(src), P<uint8_t>(ref), P<uint8_t>(hp), P<int16_t>(mv_in),
+                         P<int16_t>(mv_out), P<int>(cost), P<int16_t>(pm), P<uint8_t>(pred), P<int>(qp),
+                         P<int8_t>(aq), S(stream));
   });
   m.def("b_decide", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref0, uintptr_t ref1, uintptr_t hp0,
                        uintptr_t hp1, uintptr_t mv0, uintptr_t mv1, uintptr_t cost0, uintptr_t cost1, uintptr_t pred0,

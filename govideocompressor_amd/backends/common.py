@@ -66,13 +66,16 @@ def output_size(cfg: EncoderConfig, clip: yuv.Clip) -> tuple[int, int]:
     return clip.width, clip.height
 
 
-def write_output(job: PieceJob, stream: bytes, fps: float) -> int:
-    """Write an Annex-B stream as ``.mp4`` (``avc1`` native muxer, ``hvc1`` for HEVC) or raw by extension."""
+def write_output(job: PieceJob, stream: bytes, fps: float, codec: str | None = None) -> int:
+    """Write an Annex-B stream as ``.mp4`` (``avc1`` native muxer, ``hvc1`` for HEVC) or raw by
+    extension.  ``codec`` ("h264" / "hevc", from the job's EncoderConfig) picks the sample
+    entry; without it the stream's first NAL header decides."""
     from ..ops import native
     from ..segment import mp4_hevc
+    hevc = mp4_hevc.is_hevc_annexb(stream) if codec is None else codec == "hevc"
     if not job.out_path.lower().endswith(".mp4"):
         data = stream
-    elif mp4_hevc.is_hevc_annexb(stream):
+    elif hevc:
         data = mp4_hevc.mux(stream, fps)
     else:
         data = native.host().mp4_mux(stream, fps)

@@ -160,7 +160,7 @@ class GpuBackend:
             for j in jobs:
                 if j.idx in enc:
                     stream, st = enc[j.idx]
-                    st["bytes"] = write_output(j, stream, st["fps"])
+                    st["bytes"] = write_output(j, stream, st["fps"], cfg.codec)
                     st["timings"] = dict(tm.t)
                     write_log(j, st)
                     results[j.idx] = PieceResult(j.idx, True, stats=st)

@@ -69,6 +69,9 @@ class H264Params:
     # integer search radius of the two B-picture searches (their predictors are the scaled
     # co-located vectors of temporal direct, so a small window suffices)
     b_me_range: int = int(os.environ.get("MIVC_B_ME_RANGE", 4))
+    # Jacobi passes of the P_Skip-aware vector choice after ME (csrc/kernels/bframe.hip
+    # p_mv_refine): 0 disables
+    skip_refine: int = int(os.environ.get("MIVC_SKIP_REFINE", 2))
 
     def eff_bframes(self) -> int:
         return max(0, int(self.bframes)) if self.cabac else 0
@@ -237,6 +240,7 @@ class GpuH264Encoder:
         self.coef = [torch.zeros((B, nmb, COEF_PER_MB), dtype=i16, device=dev) for _ in range(2)]
         self.nz = torch.zeros((B, nmb, 16), dtype=u8, device=dev)
         self.mv = torch.zeros((B, nmb, 2), dtype=i16, device=dev)
+        self.mv_tmp = torch.zeros((B, nmb, 2), dtype=i16, device=dev)
         self.prev_mv = torch.zeros((B, nmb, 2), dtype=i16, device=dev)
         self.me_cost = torch.zeros((B, nmb), dtype=i32, device=dev)
         self.intra_cost = torch.zeros((B, nmb), dtype=i32, device=dev)
@@ -405,9 +409,15 @@ class GpuH264Encoder:
         if pic.kind == "P":
             fy, fu, fv = (P(x) for x in ref0)
             self.intra_count.zero_()
+            hp = P(self.me_hp[(pic.anchor - 1) & 1])
             self.hip.me(B, wmb, hmb, sy, fy, P(self.prev_mv), P(self.mv), P(self.me_cost), P(self.pred),
-                        P(self.intra_cost), P(self.qp), self.p.me_range, self.p.subpel, s,
-                        P(self.me_hp[(pic.anchor - 1) & 1]), aq, 1)
+                        P(self.intra_cost), P(self.qp), self.p.me_range, self.p.subpel, s, hp, aq, 1)
+            for it in range(int(self.p.skip_refine)):
+                a_, b_ = (self.mv, self.mv_tmp) if it % 2 == 0 else (self.mv_tmp, self.mv)
+                self.hip.p_refine(B, wmb, hmb, sy, fy, hp, P(a_), P(b_), P(self.me_cost), P(self.prev_mv),
+                                  P(self.pred), P(self.qp), aq, s)
+            if int(self.p.skip_refine) % 2:
+                self.mv.copy_(self.mv_tmp)
             if cut is not None:
                 self.intra_cost.masked_fill_(cut[:, None], -1)  # intra beats any inter cost
             self.hip.encode_inter(B, wmb, hmb, sy, su, sv, fy, fu, fv, ry, ru, rv, P(self.pred), P(self.mv),

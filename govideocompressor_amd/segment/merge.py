@@ -70,15 +70,31 @@ def load_annexb(path: str) -> bytes:
     return data
 
 
+def piece_fps(path: str) -> float | None:
+    """Frame rate recorded in an MP4 piece (mdhd / stts), None for Annex-B pieces."""
+    with open(path, "rb") as f:
+        data = f.read()
+    if data[4:8] != b"ftyp" and not path.lower().endswith((".mp4", ".m4v", ".mov")):
+        return None
+    return mp4_hevc.track_fps(data)
+
+
 def merge_files(files: list[str], out_path: str, fps: float | None = None) -> int:
     """Concatenate pieces in order into ``out_path`` (.mp4 -> MP4 mux, otherwise Annex-B).
-    Returns the number of bytes written."""
+    Every piece must carry the same codec.  Returns the number of bytes written."""
     missing = [f for f in files if not os.path.exists(f)]
     if missing:
         raise FileNotFoundError(f"missing pieces: {missing[:5]}{'...' if len(missing) > 5 else ''}")
     h = native.host()
-    stream = h.concat([load_annexb(f) for f in files])
+    parts = [load_annexb(f) for f in files]
+    codecs = {("hevc" if mp4_hevc.is_hevc_annexb(p) else "h264") for p in parts if p}
+    if len(codecs) > 1:
+        raise ValueError(f"pieces mix codecs {sorted(codecs)}: re-encode them with one -vcodec")
+    stream = h.concat(parts)
     if out_path.lower().endswith((".mp4", ".m4v", ".mov")) and mp4_hevc.is_hevc_annexb(stream):
+        if fps is None and files:
+            # the HEVC SPS carries no timing: take the pieces' own MP4 rate
+            fps = piece_fps(files[0])
         data = mp4_hevc.mux(stream, fps or 30.0)
     elif out_path.lower().endswith((".mp4", ".m4v", ".mov")):
         if fps is None:

@@ -16,6 +16,9 @@ from __future__ import annotations
 import struct
 
 _VPS, _SPS, _PPS, _AUD = 32, 33, 34, 35
+# NAL types that belong to the picture they follow: end of sequence / bitstream, filler
+# data, suffix SEI (Table 7-1)
+_SUFFIX = (36, 37, 38, 40)
 
 
 def is_hevc_annexb(data: bytes) -> bool:
@@ -149,17 +152,24 @@ def mux(stream: bytes, fps: float = 30.0) -> bytes:
                 if 16 <= t <= 21:
                     sync.append(len(samples))
                 pending = bytearray()
+            elif not samples:
+                raise ValueError("hevc mp4 mux: a slice segment precedes the first picture start")
             samples[-1] += rec
+        elif t in _SUFFIX and samples:
+            samples[-1] += rec  # suffix SEI / EOS / EOB / filler: the current picture's
         else:
             pending += rec  # prefix SEI etc. belong to the next picture
     if not samples or not sps or not pps:
         raise ValueError("hevc mp4 mux: stream has no pictures or no SPS/PPS")
+    if pending:
+        samples[-1] += pending  # trailing non-VCL NALs stay with the last picture
     info = parse_sps(sps[0])
     w, h = info["width"], info["height"]
     fps = fps if fps and fps > 0 else 30.0
     timescale, delta = int(round(fps * 1000)), 1000
     n = len(samples)
     media_dur, movie_dur = n * delta, int(round(n * 1000.0 / fps))
+    v1 = media_dur > 0xFFFFFFFF or movie_dur > 0xFFFFFFFF  # 64-bit durations (version 1 boxes)
     mdat_body = b"".join(bytes(s) for s in samples)
 
     ftyp = _box(b"ftyp", b"isom", struct.pack(">I", 512), b"isomiso2hvc1mp41")
@@ -180,12 +190,20 @@ def mux(stream: bytes, fps: float = 30.0) -> bytes:
                     stco)
         minf = _box(b"minf", _full(b"vmhd", 0, 1, bytes(8)),
                     _box(b"dinf", _full(b"dref", 0, 0, struct.pack(">I", 1), _full(b"url ", 0, 1))), stbl)
-        mdia = _box(b"mdia", _full(b"mdhd", 0, 0, struct.pack(">IIIIHH", 0, 0, timescale, media_dur, 0x55C4, 0)),
+        if v1:
+            mdhd = _full(b"mdhd", 1, 0, struct.pack(">QQIQHH", 0, 0, timescale, media_dur, 0x55C4, 0))
+            tkhd = _full(b"tkhd", 1, 3, struct.pack(">QQIIQ", 0, 0, 1, 0, movie_dur), bytes(8),
+                         struct.pack(">hhhH", 0, 0, 0, 0), _MATRIX, struct.pack(">II", w << 16, h << 16))
+            mvhd = _full(b"mvhd", 1, 0, struct.pack(">QQIQ", 0, 0, 1000, movie_dur), struct.pack(">IH", 0x10000, 0x100),
+                         bytes(10), _MATRIX, bytes(24), struct.pack(">I", 2))
+        else:
+            mdhd = _full(b"mdhd", 0, 0, struct.pack(">IIIIHH", 0, 0, timescale, media_dur, 0x55C4, 0))
+            tkhd = _full(b"tkhd", 0, 3, struct.pack(">IIIII", 0, 0, 1, 0, movie_dur), bytes(8),
+                         struct.pack(">hhhH", 0, 0, 0, 0), _MATRIX, struct.pack(">II", w << 16, h << 16))
+            mvhd = _full(b"mvhd", 0, 0, struct.pack(">IIII", 0, 0, 1000, movie_dur), struct.pack(">IH", 0x10000, 0x100),
+                         bytes(10), _MATRIX, bytes(24), struct.pack(">I", 2))
+        mdia = _box(b"mdia", mdhd,
                     _full(b"hdlr", 0, 0, struct.pack(">I", 0), b"vide", bytes(12), b"VideoHandler\x00"), minf)
-        tkhd = _full(b"tkhd", 0, 3, struct.pack(">IIIII", 0, 0, 1, 0, movie_dur), bytes(8),
-                     struct.pack(">hhhH", 0, 0, 0, 0), _MATRIX, struct.pack(">II", w << 16, h << 16))
-        mvhd = _full(b"mvhd", 0, 0, struct.pack(">IIII", 0, 0, 1000, movie_dur), struct.pack(">IH", 0x10000, 0x100),
-                     bytes(10), _MATRIX, bytes(24), struct.pack(">I", 2))
         return _box(b"moov", mvhd, _box(b"trak", tkhd, mdia))
 
     size = len(moov(0))
@@ -224,6 +242,22 @@ def is_hevc_mp4(data: bytes) -> bool:
     except ValueError:
         return False
     return data[s + 12:s + 16] in (b"hvc1", b"hev1")
+
+
+def track_fps(data: bytes) -> float | None:
+    """Frame rate of an MP4's (first) track: mdhd timescale / the first stts delta."""
+    try:
+        ms, me = _find(data, 0, len(data), [b"moov", b"trak", b"mdia", b"mdhd"])
+        ver = data[ms]
+        timescale = struct.unpack(">I", data[ms + (20 if ver == 1 else 12):ms + (24 if ver == 1 else 16)])[0]
+        ts, te = _find(data, 0, len(data), [b"moov", b"trak", b"mdia", b"minf", b"stbl", b"stts"])
+        n = struct.unpack(">I", data[ts + 4:ts + 8])[0]
+        if n < 1 or timescale <= 0:
+            return None
+        delta = struct.unpack(">I", data[ts + 12:ts + 16])[0]
+        return timescale / delta if delta > 0 else None
+    except (ValueError, struct.error, IndexError):
+        return None
 
 
 def demux(data: bytes) -> bytes:

@@ -77,6 +77,9 @@ def annexb_of(path: str, kind: str | None = None) -> bytes:
     with open(path, "rb") as f:
         data = f.read()
     if kind == "mp4":
+        from . import mp4_hevc
+        if mp4_hevc.is_hevc_mp4(data):
+            return mp4_hevc.demux(data)
         return native.host().mp4_demux(data)
     if kind == "h264":
         return data

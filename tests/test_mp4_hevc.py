@@ -37,6 +37,10 @@ def test_hevc_mp4_roundtrip(host, w, h, bd, wpp):
     _same_pics(host.hevc_decode(back), host.hevc_decode(s))
 
 
+def _hevc_stream(host, w, h, n):
+    return random_stream(host, w, h, n, seed=5)[0]
+
+
 def test_h264_streams_not_taken_for_hevc(host):
     assert not mp4_hevc.is_hevc_annexb(host.parameter_sets(dict(width=64, height=48)))
     assert not mp4_hevc.is_hevc_annexb(b"\x00\x00\x00\x01\x67\x42\xc0\x1e" + bytes(16))
@@ -62,3 +66,56 @@ def test_hevc_mp4_merge(host, tmp_path):
     for p, q in zip(pics, ref):
         assert np.array_equal(p["y"], q["y"])
     assert os.path.getsize(out) == len(data)
+
+
+def test_merge_keeps_piece_frame_rate(host, tmp_path):
+    """merged HEVC .mp4 takes the pieces' mdhd/stts rate (not a 30 fps default)."""
+    from govideocompressor_amd.segment import merge, mp4_hevc
+    stream = _hevc_stream(host, 64, 64, 3)
+    paths = []
+    for i in range(2):
+        p = tmp_path / f"{i}.mp4"
+        p.write_bytes(mp4_hevc.mux(stream, 25.0))
+        paths.append(str(p))
+    out = tmp_path / "out.mp4"
+    merge.merge_files(paths, str(out))
+    data = out.read_bytes()
+    assert abs(mp4_hevc.track_fps(data) - 25.0) < 1e-6
+
+
+def test_mux_suffix_nals_and_trailing(host):
+    """Suffix SEI / EOS stay with the picture they follow; a stray slice before any picture
+    start is rejected."""
+    from govideocompressor_amd.segment import mp4_hevc
+    stream = _hevc_stream(host, 64, 64, 2)
+    sei_suffix = b"\x00\x00\x00\x01" + bytes([40 << 1, 1]) + b"\x05\x01\xaa\x80"
+    eos = b"\x00\x00\x00\x01" + bytes([36 << 1, 1])
+    data = mp4_hevc.mux(stream + sei_suffix + eos, 30.0)
+    back = mp4_hevc.demux(data)
+    assert back.endswith(sei_suffix[4:] + b"\x00\x00\x00\x01" + eos[4:])
+    nals = mp4_hevc.split_nals(stream)
+    vcl = [n for n in nals if ((n[0] >> 1) & 0x3F) < 32]
+    bad = b"\x00\x00\x00\x01" + vcl[0][:2] + bytes([vcl[0][2] & 0x7F]) + vcl[0][3:]
+    import pytest
+    with pytest.raises(ValueError):
+        mp4_hevc.mux(b"".join(b"\x00\x00\x00\x01" + n for n in nals if ((n[0] >> 1) & 0x3F) >= 32) + bad, 30.0)
+
+
+def test_merge_rejects_mixed_codecs(host, tmp_path):
+    from govideocompressor_amd.segment import merge
+    hevc = _hevc_stream(host, 64, 64, 2)
+    h264 = host.parameter_sets(dict(width=64, height=64))
+    a, b = tmp_path / "0.264", tmp_path / "1.264"
+    a.write_bytes(hevc)
+    b.write_bytes(h264)
+    import pytest
+    with pytest.raises(ValueError, match="mix codecs"):
+        merge.merge_files([str(a), str(b)], str(tmp_path / "o.264"))
+
+
+def test_probe_annexb_of_hevc_mp4(host, tmp_path):
+    from govideocompressor_amd.segment import mp4_hevc, probe
+    stream = _hevc_stream(host, 64, 64, 2)
+    p = tmp_path / "x.mp4"
+    p.write_bytes(mp4_hevc.mux(stream, 30.0))
+    assert mp4_hevc.is_hevc_annexb(probe.annexb_of(str(p)))
