@@ -123,19 +123,23 @@ def broadcast_object(env: DistEnv, obj, src: int = 0):
 
 
 class BitstreamGather:
-    """CC-2 + CC-3: gather variable-size per-rank byte payloads to every rank.
+    """CC-2 + CC-3: gather variable-size per-rank byte payloads to rank 0.
 
-    Rank r contributes ``pieces`` (list of bytes, one per local segment).  The
-    payload travels as uint8 device tensors through ``all_gather_into_tensor``
-    (RCCL over xGMI for nccl; gloo on CPU).  ``start()`` issues the collectives
-    asynchronously so the caller can overlap them with the next batch;
-    ``wait()`` returns ``list[list[bytes]]`` indexed [rank][piece].
+    Rank r contributes ``pieces`` (list of bytes, one per local segment).  Piece counts and
+    sizes travel in two tiny ``all_gather_into_tensor`` calls (CC-2); the payload goes
+    point-to-point to rank 0 only (RCCL ``isend``/``irecv`` over xGMI for nccl, gloo on
+    CPU): (world - 1) transfers instead of an all-gather's world x world.  ``start()``
+    posts the transfers asynchronously (``async_op`` works) so the caller can overlap
+    them; ``wait()`` returns ``list[list[bytes]]`` indexed [rank][piece] on rank 0 and
+    ``None`` on the other ranks.
     """
 
-    def __init__(self, env: DistEnv, pieces: list[bytes]):
+    def __init__(self, env: DistEnv, pieces: list[bytes], root: int = 0):
         self.env = env
         self.pieces = pieces
+        self.root = root
         self.works = []
+        self.recv: dict[int, torch.Tensor] = {}
 
     def start(self) -> "BitstreamGather":
         env = self.env
@@ -146,41 +150,47 @@ class BitstreamGather:
         n = torch.tensor([len(self.pieces)], dtype=torch.int64, device=dev)
         ns = torch.empty(env.world, dtype=torch.int64, device=dev)
         dist.all_gather_into_tensor(ns, n)
-        self.max_n = int(ns.max().item())
+        self.max_n = max(1, int(ns.max().item()))
         pad_sizes = torch.zeros(self.max_n, dtype=torch.int64, device=dev)
         pad_sizes[: len(self.pieces)] = sizes
-        self.all_sizes = torch.empty(env.world * self.max_n, dtype=torch.int64, device=dev)
-        dist.all_gather_into_tensor(self.all_sizes, pad_sizes)
+        all_sizes = torch.empty(env.world * self.max_n, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(all_sizes, pad_sizes)
         self.ns = ns.cpu().tolist()
-        sizes_h = self.all_sizes.cpu().view(env.world, self.max_n)
-        self.sizes_h = sizes_h
-        per_rank = sizes_h.sum(dim=1)
-        self.max_bytes = int(per_rank.max().item())
-        payload = b"".join(self.pieces)
-        buf = torch.zeros(max(1, self.max_bytes), dtype=torch.uint8)
-        if payload:
-            buf[: len(payload)] = torch.frombuffer(bytearray(payload), dtype=torch.uint8)
-        self.send = buf.to(dev, non_blocking=True)
-        self.recv = torch.empty(env.world * max(1, self.max_bytes), dtype=torch.uint8, device=dev)
-        self.works.append(dist.all_gather_into_tensor(self.recv, self.send, async_op=True))
+        self.sizes_h = all_sizes.cpu().view(env.world, self.max_n)
+        per_rank = self.sizes_h.sum(dim=1).tolist()
+        if env.rank != self.root:
+            payload = b"".join(self.pieces)
+            if payload:
+                self.send = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(dev, non_blocking=True)
+                self.works.append(dist.isend(self.send, dst=self.root))
+            return self
+        ops = []
+        for r in range(env.world):
+            if r != self.root and per_rank[r]:
+                self.recv[r] = torch.empty(int(per_rank[r]), dtype=torch.uint8, device=dev)
+                ops.append(dist.P2POp(dist.irecv, self.recv[r], r))
+        if ops:
+            self.works += dist.batch_isend_irecv(ops)
         return self
 
-    def wait(self) -> list[list[bytes]]:
+    def wait(self) -> list[list[bytes]] | None:
         env = self.env
         if not env.initialized:
             return [list(self.pieces)]
         for w in self.works:
             w.wait()
-        blob = self.recv.cpu().numpy().tobytes()
-        stride = max(1, self.max_bytes)
+        if env.rank != self.root:
+            return None
         out = []
         for r in range(env.world):
-            base = r * stride
-            off = 0
-            lst = []
+            if r == self.root:
+                out.append(list(self.pieces))
+                continue
+            blob = self.recv[r].cpu().numpy().tobytes() if r in self.recv else b""
+            off, lst = 0, []
             for i in range(self.ns[r]):
                 sz = int(self.sizes_h[r, i])
-                lst.append(blob[base + off: base + off + sz])
+                lst.append(blob[off: off + sz])
                 off += sz
             out.append(lst)
         return out
@@ -195,12 +205,15 @@ class SegmentMerge:
 
     1. each rank packs its pieces (rank-major segment order) into a pinned host
        buffer -- on one rank this packing IS the concatenation;
-    2. piece sizes: one tiny ``all_gather_into_tensor`` (CC-2);
-    3. payload: H2D of the packed bytes, one ``all_gather_into_tensor`` of
-       [world x max_bytes] (CC-3, RCCL over xGMI);
-    4. rank 0 alone copies each rank's used prefix back to a pinned host buffer,
-       back to back, so the DMA engine does the compaction: no host memcpy of the
-       other ranks' bytes, and no other rank pays a device-to-host copy.
+    2. piece sizes: one tiny ``all_gather_into_tensor`` (CC-2) gives rank 0 every
+       rank's byte count (= the exclusive scan of output offsets);
+    3. payload (CC-3): each rank r > 0 sends its bytes point-to-point to rank 0
+       (RCCL ``send``/``recv`` over xGMI -- one link per peer, only rank 0 receives:
+       (world - 1) x batch bytes in total instead of the world x world x batch of an
+       all-gather), rank 0 posts every receive at once (``batch_isend_irecv``) straight
+       into one contiguous device buffer at each rank's offset;
+    4. rank 0 copies the received bytes back to a pinned host buffer behind its own
+       (which never leaves the host).
 
     Buffers are kept and grown (x1.25) across calls.  ``run`` uses the caller's
     current stream, so a caller on a side stream overlaps the merge with compute.
@@ -266,28 +279,45 @@ class SegmentMerge:
         all_n = torch.empty(env.world, dtype=torch.int64, device=dev)
         dist.all_gather_into_tensor(all_n, n_loc)
         per_rank = all_n.cpu().tolist()
-        stride = max(1, max(per_rank))
-        self._send = self._grow(self._send, stride, pinned=False, device=dev)
-        self._recv = self._grow(self._recv, env.world * stride, pinned=False, device=dev)
-        send = self._send[:stride]
-        if local.size:
-            send[:local.size].copy_(self._pack[:local.size], non_blocking=True)
-        recv = self._recv[:env.world * stride]
-        dist.all_gather_into_tensor(recv, send)
+        offs = [0]
+        for n in per_rank:
+            offs.append(offs[-1] + n)
+        total = offs[-1]
         if not env.is_main:
-            # the staging buffer is reused by the next call: wait for the H2D read
-            torch.cuda.current_stream(dev).synchronize() if dev.type == "cuda" else None
+            if local.size:
+                if dev.type == "cuda":
+                    self._send = self._grow(self._send, local.size, pinned=False, device=dev)
+                    send = self._send[:local.size]
+                    send.copy_(self._pack[:local.size], non_blocking=True)
+                else:
+                    send = self._pack[:local.size]
+                dist.send(send, dst=0)
+                if dev.type == "cuda":
+                    # the staging buffers are reused by the next call
+                    torch.cuda.current_stream(dev).synchronize()
             return None
-        total = sum(per_rank)
         self._out = self._grow(self._out, total, pinned=True)
-        off = 0
-        for r, n in enumerate(per_rank):
-            if n:
-                self._out[off:off + n].copy_(recv[r * stride: r * stride + n], non_blocking=True)
-            off += n
-        if dev.type == "cuda":
-            torch.cuda.current_stream(dev).synchronize()
-        out = self._out.numpy()[:total]
+        out_t = self._out
+        if local.size:
+            out_t.numpy()[:local.size] = local
+        others = total - per_rank[0]
+        if others:
+            if dev.type == "cuda":
+                self._recv = self._grow(self._recv, others, pinned=False, device=dev)
+                rbuf, base = self._recv, per_rank[0]
+            else:
+                rbuf, base = out_t, 0  # gloo: receive straight into the host output
+            ops = []
+            for r in range(1, env.world):
+                if per_rank[r]:
+                    lo = offs[r] - (base if dev.type == "cuda" else 0)
+                    ops.append(dist.P2POp(dist.irecv, rbuf[lo:lo + per_rank[r]], r))
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+            if dev.type == "cuda":
+                out_t[per_rank[0]:total].copy_(rbuf[:others], non_blocking=True)
+                torch.cuda.current_stream(dev).synchronize()
+        out = out_t.numpy()[:total]
         if out.size and not (bytes(out[:3]) == b"\0\0\1" or bytes(out[:4]) == b"\0\0\0\1"):
             raise RuntimeError("segment merge: merged stream does not start with a start code")
         return np.asarray(out)

@@ -11,8 +11,9 @@ GPU with no files in between:
    server.go:175-189);
 3. each rank reads/decodes only its own segments, encodes them as one batched GPU
    call per chunk and keeps the bitstreams;
-4. one RCCL all-gather of the bitstreams (CC-2/CC-3) and rank 0 concatenates them in
-   segment order into the output (the concat.sh step, server.go:349-361).
+4. the bitstreams go point-to-point to rank 0 (CC-2 sizes all-gather + CC-3 RCCL
+   isend/irecv) and rank 0 concatenates them in segment order into the output (the
+   concat.sh step, server.go:349-361).
 """
 from __future__ import annotations
 
@@ -115,7 +116,7 @@ def encode_file(path: str, output: str, args: str = "264", backend: str = "auto"
             run(my[b:b + slots])
     t_enc = time.perf_counter() - t0
     order = sorted(mine)
-    # CC-2/CC-3: bitstreams + their segment indices to every rank
+    # CC-2/CC-3: bitstreams + their segment indices to rank 0
     idx_blob = json.dumps(order).encode()
     g = D.BitstreamGather(env, [idx_blob] + [mine[i] for i in order]).start()
     gathered = g.wait()

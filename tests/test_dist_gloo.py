@@ -67,9 +67,12 @@ def test_collectives_gloo():
     tickets = []
     for rank, st, got, obj, mine, mx in res:
         assert [row[0] for row in st] == [1, 2, 3, 1, 2, 3]
-        assert got[0] == [b"zero"]
-        assert got[1] == [b"\x01" * 4, b"", b"\x07"]
-        assert got[2] == [b"\x02" * 7, b"", b"\x07\x07"]
+        if rank == 0:  # the payloads are gathered to rank 0 only
+            assert got[0] == [b"zero"]
+            assert got[1] == [b"\x01" * 4, b"", b"\x07"]
+            assert got[2] == [b"\x02" * 7, b"", b"\x07\x07"]
+        else:
+            assert got is None
         assert obj == {"plan": [1, 2, 3]}
         assert mx == world - 1
         tickets += mine
@@ -155,3 +158,60 @@ def test_multi_rank_encode_matches_single(tmp_path, host, schedule):
         assert p.exitcode == 0
     assert out.read_bytes() == ref.read_bytes()
     assert len(host.decode(out.read_bytes())) == 40
+
+
+def _bench_merge(rank, world, port, q, steps):
+    """bench.py's merge flow on CPU: each step the rank's pieces go through SegmentMerge on
+    a side thread (merge of step k overlaps step k + 1), rank-major order."""
+    import concurrent.futures as cf
+
+    _env(rank, world, port)
+    from govideocompressor_amd.parallel import dist as D
+    env = D.init(prefer_gpu=False)
+    try:
+        m = D.SegmentMerge(env)
+        pool = cf.ThreadPoolExecutor(max_workers=1)
+        fut, outs = None, []
+        for k in range(steps):
+            pieces = _bench_pieces(rank, k)
+            if fut is not None:
+                got = fut.result()
+                outs.append(None if got is None else bytes(got))
+            fut = pool.submit(m.run, pieces)
+        got = fut.result()
+        outs.append(None if got is None else bytes(got))
+        pool.shutdown()
+        D.barrier(env)
+        q.put((rank, outs))
+    finally:
+        D.shutdown(env)
+
+
+def _bench_pieces(rank, step, slots=3):
+    import numpy as np
+    rng = np.random.default_rng(1000 * step + rank)
+    out = []
+    for b in range(slots):
+        n = int(rng.integers(0, 4000)) if (rank + b) % 5 else 0  # some ranks / slots tiny
+        out.append([b"\0\0\0\1\x67" + bytes([rank, b, step]), rng.integers(0, 256, n, dtype=np.uint8).tobytes()])
+    return out
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_bench_merge_flow_world_4_8(world):
+    """T5 at world 4 / 8: the merged stream on rank 0 is byte-identical to world = 1's
+    concatenation of every rank's pieces (rank-major), for several pipelined steps."""
+    steps, port = 3, _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_bench_merge, args=(r, world, port, q, steps)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)])
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    for k in range(steps):
+        want = b"".join(b"".join(b"".join(parts) for parts in _bench_pieces(r, k)) for r in range(world))
+        assert res[0][1][k] == want, k
+        assert all(res[r][1][k] is None for r in range(1, world))
