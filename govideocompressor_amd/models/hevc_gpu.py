@@ -73,6 +73,10 @@ class HevcSegmentResult:
     bits: list[int] = field(default_factory=list)
     psnr_y: float = 0.0
 
+    def display_prefix(self, c: int) -> list[bytes]:
+        """Slice NALs of pictures 0..c-1 (P-only GOPs: coding order == display order)."""
+        return self.nals[:c]
+
 
 class GpuHevcEncoder:
     """Batched gfx950 HEVC encoder (Main / Main 10, CABAC)."""

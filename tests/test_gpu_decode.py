@@ -70,13 +70,23 @@ def test_gpu_decode_encoder_streams(host, dec):
     _check(host, dec, streams)
 
 
-def test_gpu_decode_gpu_encoder_stream(host, dec):
+def _gpu_encoder_streams(**kw):
     import torch
     from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
-    enc = GpuH264Encoder(H264Params(width=320, height=240, crf=23), slots=3)
+    enc = GpuH264Encoder(H264Params(width=320, height=240, crf=23, **kw), slots=3)
     y, u, v = synth_clip(3, 10, 320, 240, seed=5)
     res = enc.encode(y, u, v, metrics=False)
     streams = [r.bitstream for r in res]
     enc.close()
     torch.cuda.synchronize()
-    _check(host, dec, streams)
+    return streams
+
+
+def test_gpu_decode_gpu_encoder_stream(host, dec):
+    # Constrained Baseline CAVLC (the round-1 encoder): P pictures, one reference
+    _check(host, dec, _gpu_encoder_streams(cabac=False))
+
+
+def test_gpu_decode_gpu_encoder_cabac_b_stream(host, dec):
+    # the default encoder (Main CABAC + 3 B): decoded output matches the CPU decoder
+    _check(host, dec, _gpu_encoder_streams(), expect_gpu=False)
