@@ -102,8 +102,13 @@ def main() -> None:
     # part of encoding (an ffmpeg/x264 encode computes none unless asked); the timed steps
     # encode the same content distribution (new seed per step).
     qres = None
+    stage_ms = {}
     if a.warmup:
+        # per-stage device time (HIP events + roctx ranges) on the untimed warmup only
+        enc.stage_timer.enabled = True
         qres, _, _ = run_steps(-100, a.warmup, metrics_first=a.quality)
+        stage_ms = {k: round(v["s"] * 1000.0 / a.warmup, 2) for k, v in enc.stage_timer.summary().items()}
+        enc.stage_timer.enabled = False
         # the timed loop keeps two input batches alive (step k encodes while k + 1 is
         # synthesized): let the caching allocator map the second one before the clock starts
         spare = synth(-99)
@@ -154,6 +159,7 @@ def main() -> None:
                         "measured_on": "first warmup step (untimed)" if q else "n/a (no warmup step)",
                         "merged_bytes": len(merged) if merged is not None else 0},
             "timings_rank0_s": {k: round(v, 3) for k, v in enc.timings.items()},
+            "stage_device_ms_per_step_rank0": {"measured_on": "warmup steps (untimed)", **stage_ms},
             "encoder_stats_rank0": {k: round(v, 4) for k, v in enc.stats.items()},
         }
         line = json.dumps(out)

@@ -32,7 +32,7 @@ void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src_y, const u
                           void* hdr, uint8_t* pred_out, int* cost_out, void* stream);
 void mivc_launch_aq_offsets(int B, int wmb, int hmb, const uint8_t* sy, const uint8_t* su, const uint8_t* sv,
                             float strength, const float* extra, long long extra_stride, int8_t* out, void* stream);
-void mivc_launch_mbtree(int B, int F, int lbw, int lbh, const int* blk_cost, const int* blk_mv, float* prop,
+void mivc_launch_mbtree(int B, int F, int lbw, int lbh, const int* blk_cost, const int* blk_mv, void* prop,
                         float strength, float* out, void* stream);
 void mivc_launch_qp_fixup(int B, int wmb, int hmb, void* hdr, const int16_t* coef, const uint8_t* nz, uint8_t* flags,
                           const int* slice_qp, void* stream);
@@ -163,7 +163,7 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("out"), py::arg("stream"), py::arg("extra") = 0, py::arg("extra_stride") = 0);
   m.def("mbtree", [](int B, int F, int lbw, int lbh, uintptr_t blk_cost, uintptr_t blk_mv, uintptr_t prop,
                      float strength, uintptr_t out, uintptr_t stream) {
-    mivc_launch_mbtree(B, F, lbw, lbh, P<int>(blk_cost), P<int>(blk_mv), P<float>(prop), strength, P<float>(out),
+    mivc_launch_mbtree(B, F, lbw, lbh, P<int>(blk_cost), P<int>(blk_mv), P<void>(prop), strength, P<float>(out),
                        S(stream));
   });
   m.def("qp_fixup", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t coef, uintptr_t nz, uintptr_t flags,

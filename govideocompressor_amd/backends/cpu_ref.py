@@ -8,6 +8,7 @@ Pieces are encoded in parallel threads (the C++ encoder releases the GIL).
 from __future__ import annotations
 
 import concurrent.futures as cf
+import math
 import os
 import time
 
@@ -54,13 +55,30 @@ class CpuBackend:
         clip = resize_clip(clip, ow, oh)
         fps = cfg.fps or clip.fps
         qp = cfg.qp if cfg.qp is not None else int(round(cfg.crf if cfg.crf is not None else 23))
-        hcfg = dict(width=ow, height=oh, fps=fps, qp=max(0, min(51, qp)), keyint=1 << 30)
-        parts, psnr = [], []
-        for u, (s, c) in enumerate(unit_plan(clip.frames, cfg.keyint)):
-            enc = self.host.CpuEncoder(hcfg)
-            parts.append(enc.encode(clip.slice(s, c).i420(), c, idr_id(key, u)))
-            psnr += [st["psnr_y"] for st in enc.stats()]
-        stream = self.host.concat(parts)
+
+        def run(q: int):
+            hcfg = dict(width=ow, height=oh, fps=fps, qp=max(0, min(51, q)), keyint=1 << 30)
+            parts, psnr = [], []
+            for u, (s, c) in enumerate(unit_plan(clip.frames, cfg.keyint)):
+                enc = self.host.CpuEncoder(hcfg)
+                parts.append(enc.encode(clip.slice(s, c).i420(), c, idr_id(key, u)))
+                psnr += [st["psnr_y"] for st in enc.stats()]
+            return self.host.concat(parts), psnr
+
+        stream, psnr = run(qp)
+        if cfg.bitrate:  # ABR on the fixed-QP reference encoder: integer-QP secant search
+            target = cfg.bitrate * clip.frames / fps
+            tried = {qp: (stream, psnr)}
+            for _ in range(4):
+                bits = 8 * len(stream)
+                nq = max(0, min(51, qp + int(round(6.0 * math.log2(max(bits, 1) / target)))))
+                if nq in tried:
+                    break
+                qp = nq
+                stream, psnr = run(qp)
+                tried[qp] = (stream, psnr)
+            qp = min(tried, key=lambda q: abs(8 * len(tried[q][0]) - target))
+            stream, psnr = tried[qp]
         st = {"backend": "cpu", "idx": key, "frames": clip.frames, "width": ow, "height": oh, "fps": fps,
               "stream_bytes": len(stream), "psnr_y": float(np.mean(psnr)) if psnr else 0.0,
               "config": cfg.as_dict(), "seconds": time.perf_counter() - t0}

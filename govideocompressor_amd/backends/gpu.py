@@ -13,6 +13,7 @@ truncating a closed GOP leaves a conformant stream).
 from __future__ import annotations
 
 import concurrent.futures as cf
+import os
 import time
 
 import numpy as np
@@ -48,22 +49,33 @@ class GpuBackend:
             return GpuH264Encoder(p, slots=b, device=self.device, entropy=self.entropy)
 
         self._pool = EncoderPool(make, max_resident=1)
+        from ..runtime.device import device_info
+        from ..runtime.pool import PinnedPool
+        self._pinned = PinnedPool(max_cached=6)
+        self._info = device_info(self.device.index)
         self._streams = StageStreams(self.device)
         self._io = cf.ThreadPoolExecutor(max_workers=8)
         self._decoder = None
 
     def _encoder(self, params, slots: int):
-        key = (type(params).__name__, params.width, params.height, params.fps, params.crf, params.qp,
-               getattr(params, "bit_depth", 8), slots)
+        import dataclasses
+        key = (type(params).__name__, dataclasses.astuple(params), slots)
         return self._pool.get(key, params, slots)
 
     def encode_clips(self, items: list[tuple[str, "yuv.Clip"]], cfg: EncoderConfig,
-                     tm: Timer | None = None) -> dict[str, tuple[bytes, dict]]:
+                     tm: Timer | None = None, rate_stats: dict | None = None,
+                     qp_offsets: dict[str, float] | None = None) -> dict[str, tuple[bytes, dict]]:
         """Encode several clips (pieces/segments) together.  ``items``: (index token, clip).
-        Returns token -> (Annex-B stream, stats).  Raises on failure."""
+        Returns token -> (Annex-B stream, stats).  Raises on failure.
+
+        Rate control: CRF / QP as given; with ``cfg.bitrate`` every clip is one rate group
+        whose QP offset is solved by re-encoding the batch (:mod:`..rc.abr`), ``rate_stats``
+        carries the ``-pass 1`` statistics in (pass 2) or out (pass 1), and ``qp_offsets``
+        pins the offsets instead (the global two-pass of ``mivc encode``)."""
         from ..models.h264_gpu import H264Params
         from ..models.hevc_gpu import HevcParams
         from ..ops import native
+        from ..rc import presets
         if cfg.codec not in ("h264", "hevc"):
             raise BackendError(f"codec {cfg.codec} is not available in the gpu backend")
         if cfg.bit_depth != 8 and cfg.codec == "h264":
@@ -81,25 +93,124 @@ class GpuBackend:
                 for u, (s, c) in enumerate(unit_plan(clips[key].frames, cfg.keyint)):
                     units.append((key, u, s, c))
             fps = cfg.fps or clips[keys[0]].fps
+            crf = cfg.crf if cfg.bitrate is None else 23.0  # ABR searches an offset from CRF 23
             if cfg.codec == "hevc":
                 if (ow, oh) != (w, h):
                     raise BackendError("scaling is not available in the HEVC path")
-                params = HevcParams(width=ow, height=oh, fps=fps, crf=cfg.crf, qp=cfg.qp if cfg.qp is not None else 30,
-                                    bit_depth=cfg.bit_depth)
+                params = HevcParams(width=ow, height=oh, fps=fps, crf=crf if cfg.qp is None else None,
+                                    qp=cfg.qp if cfg.qp is not None else 30, bit_depth=cfg.bit_depth)
             else:
-                params = H264Params(width=ow, height=oh, fps=fps, crf=cfg.crf, qp=cfg.qp if cfg.qp is not None else 26)
-            unit_out = []
-            for b0 in range(0, len(units), self.max_slots):
-                unit_out += self._encode_chunk(units[b0:b0 + self.max_slots], clips, params, w, h, tm)
+                params = H264Params(width=ow, height=oh, fps=fps, crf=crf if cfg.qp is None else None,
+                                    qp=cfg.qp if cfg.qp is not None else 26)
+            params = presets.apply(params, cfg.preset)
+            # batch width: every unit at once up to what HBM holds (runtime.device.slots_for)
+            from ..runtime.device import slots_for
+            cap = min(self.max_slots, slots_for(ow, oh, max(c for *_, c in units), self._info, cap=self.max_slots))
+            chunks = [units[b0:b0 + cap] for b0 in range(0, len(units), cap)]
+            prepared = [self._prepare_chunk(ch, clips, w, h, tm) for ch in chunks]
+            rate_info: dict[str, dict] = {}
+            if cfg.bitrate is None and qp_offsets is None:
+                unit_out = [x for ch, dev in zip(chunks, prepared) for x in self._run_encoder(ch, params, *dev, tm)]
+            else:
+                unit_out, rate_info = self._encode_rate(keys, chunks, prepared, clips, params, cfg, fps, tm,
+                                                        rate_stats, qp_offsets)
             for key in keys:
-                parts = sorted((x for x in unit_out if x[0] == key), key=lambda x: x[1])
-                stream = host.concat([p[2] for p in parts])
+                parts = sorted((x for x in unit_out if x["key"] == key), key=lambda x: x["unit"])
+                stream = host.concat([p["stream"] for p in parts])
                 st = {"backend": "gpu", "codec": cfg.codec, "idx": key, "frames": clips[key].frames, "units": len(parts),
                       "width": ow, "height": oh, "fps": fps, "stream_bytes": len(stream),
-                      "psnr_y": float(np.mean([p[3] for p in parts])), "ssim_y": float(np.mean([p[4] for p in parts])),
-                      "config": cfg.as_dict()}
+                      "psnr_y": float(np.mean([p["psnr"] for p in parts])),
+                      "ssim_y": float(np.mean([p["ssim"] for p in parts])),
+                      "frame_bits": [b for p in parts for b in p["frame_bits"]],
+                      "config": cfg.as_dict(), **rate_info.get(key, {})}
                 out[key] = (stream, st)
         return out
+
+    def _encode_rate(self, keys, chunks, prepared, clips, params, cfg: EncoderConfig, fps: float, tm: Timer,
+                     rate_stats: dict | None, qp_offsets: dict[str, float] | None):
+        """ABR / two-pass / VBV over one geometry group: every key is a rate group."""
+        from ..rc import abr
+        frames = np.array([clips[k].frames for k in keys], dtype=np.float64)
+        kidx = {k: i for i, k in enumerate(keys)}
+
+        def encode_all(offsets: np.ndarray, vbv: dict[tuple, np.ndarray] | None = None):
+            outs = []
+            for ch, dev in zip(chunks, prepared):
+                F = max(c for *_, c in ch)
+                delta = np.zeros((len(ch), F))
+                for b, (key, un_, _, c) in enumerate(ch):
+                    delta[b] = offsets[kidx[key]]
+                    if vbv and (key, un_) in vbv:
+                        delta[b, :len(vbv[(key, un_)])] += vbv[(key, un_)]
+                outs += self._run_encoder(ch, params, *dev, tm, qp_delta=delta)
+            bits = np.zeros(len(keys))
+            for o in outs:
+                bits[kidx[o["key"]]] += 8 * len(o["stream"])
+            return outs, bits
+
+        if qp_offsets is not None:  # pinned offsets (global two-pass of mivc encode)
+            offs = np.array([float(qp_offsets.get(k, 0.0)) for k in keys])
+            outs, bits = encode_all(offs)
+            return outs, {k: {"qp_offset": float(offs[i]), "rate_passes": 1} for i, k in enumerate(keys)}
+        targets = float(cfg.bitrate) * frames / fps
+        search = abr.OffsetSearch(targets, max_passes=4 if cfg.two_pass != 1 else 1)
+        hist = []
+        offsets = np.zeros(len(keys))
+        seeded = cfg.two_pass == 2 and rate_stats is not None and all(k in rate_stats for k in keys)
+        if seeded:
+            search.observe([rate_stats[k]["offset"] for k in keys], [rate_stats[k]["bits"] for k in keys])
+            hist.append(None)
+            offsets = search.propose()
+        while True:
+            outs, bits = encode_all(offsets)
+            search.observe(offsets, bits)
+            hist.append(outs)
+            if search.done():
+                break
+            offsets = search.propose()
+        pick = search.best_per_group()
+        if seeded:  # the seed entry has no encode behind it
+            errs = np.stack([np.abs(b / np.maximum(targets, 1) - 1) for _, b in search.hist[1:]])
+            pick = np.argmin(errs, axis=0) + 1
+        best_off = np.array([search.hist[pick[i]][0][i] for i in range(len(keys))])
+        chosen = []
+        for i, k in enumerate(keys):
+            chosen += [o for o in hist[pick[i]] if o["key"] == k]
+        if cfg.two_pass == 1 and rate_stats is not None:
+            for i, k in enumerate(keys):
+                rate_stats[k] = {"offset": float(search.hist[-1][0][i]), "bits": float(search.hist[-1][1][i]),
+                                 "frames": int(frames[i])}
+        npass = len(search.hist) - (1 if seeded else 0)
+        vbv_passes = 0
+        if cfg.maxrate and cfg.bufsize and cfg.two_pass != 1:
+            vbv: dict[tuple, np.ndarray] = {}
+            for _ in range(2):
+                fixes = 0
+                for k in keys:
+                    parts = sorted((o for o in chosen if o["key"] == k), key=lambda o: o["unit"])
+                    fb = [b for p in parts for b in p["frame_bits"]]
+                    if abr.vbv_fill(fb, cfg.maxrate, cfg.bufsize, fps).min() >= 0:
+                        continue
+                    dq = abr.vbv_deltas(fb, cfg.maxrate, cfg.bufsize, fps)
+                    pos = 0
+                    for p in parts:
+                        n = len(p["frame_bits"])
+                        disp = np.zeros(n)
+                        disp[np.asarray(p["order"][:n])] = dq[pos:pos + n]  # coding -> display order
+                        key2 = (k, p["unit"])
+                        vbv[key2] = vbv.get(key2, np.zeros(n)) + disp
+                        pos += n
+                    fixes += 1
+                if not fixes:
+                    break
+                chosen, _ = encode_all(best_off, vbv)
+                vbv_passes += 1
+        info = {}
+        for i, k in enumerate(keys):
+            got = sum(8 * len(o["stream"]) for o in chosen if o["key"] == k)
+            info[k] = {"target_bits": float(targets[i]), "bits": float(got), "qp_offset": float(best_off[i]),
+                       "rate_passes": int(npass), "vbv_passes": vbv_passes}
+        return chosen, info
 
     def decoder(self):
         """The batched GPU H.264 decoder (host CAVLC parse + gfx950 reconstruction)."""
@@ -151,8 +262,22 @@ class GpuBackend:
                 results[j.idx] = PieceResult(j.idx, False, f"load: {e}")
         tm.add("load_s", time.perf_counter() - t0)
         if items:
+            from ..rc import abr
+            rate_stats = None
+            paths = {j.idx: abr.stats_path_for(j.out_path, cfg.passlogfile) for j in jobs}
+            if cfg.two_pass == 1:
+                rate_stats = {}
+            elif cfg.two_pass == 2:
+                rate_stats = {}
+                for j in jobs:
+                    if os.path.exists(paths[j.idx]):
+                        rate_stats.update(abr.load_stats(paths[j.idx]))
             try:
-                enc = self.encode_clips(items, cfg, tm)
+                enc = self.encode_clips(items, cfg, tm, rate_stats=rate_stats)
+                if cfg.two_pass == 1:
+                    for j in jobs:
+                        if j.idx in rate_stats:
+                            abr.save_stats(paths[j.idx], {j.idx: rate_stats[j.idx]})
             except Exception as e:  # noqa: BLE001
                 for key, _ in items:
                     results[key] = PieceResult(key, False, f"encode: {e}")
@@ -166,7 +291,8 @@ class GpuBackend:
                     results[j.idx] = PieceResult(j.idx, True, stats=st)
         return [results[j.idx] for j in jobs]
 
-    def _encode_chunk(self, chunk, clips, params, w: int, h: int, tm: Timer):
+    def _prepare_chunk(self, chunk, clips, w: int, h: int, tm: Timer):
+        """One chunk's frames as [B, F, h, w] device planes (short units padded with their last frame)."""
         torch = self.torch
         B = len(chunk)
         F = max(c for *_, c in chunk)
@@ -182,10 +308,12 @@ class GpuBackend:
                     if c < F:
                         dst[b, c:].copy_(src[s + c - 1].expand(F - c, *src.shape[1:]))
             tm.add("upload_s", time.perf_counter() - t0)
-            return self._run_encoder(chunk, params, dy, du, dv, tm)
-        y = torch.empty((B, F, h, w), dtype=torch.uint8).pin_memory()
-        u = torch.empty((B, F, h // 2, w // 2), dtype=torch.uint8).pin_memory()
-        v = torch.empty_like(u).pin_memory()
+            return dy, du, dv
+        # staging in recycled page-locked buffers (non_blocking H2D needs pinned memory;
+        # pinning fresh pages per batch costs more than the copy)
+        y = self._pinned.get(B * F * h * w).view(B, F, h, w)
+        u = self._pinned.get(B * F * (h // 2) * (w // 2)).view(B, F, h // 2, w // 2)
+        v = self._pinned.get(B * F * (h // 2) * (w // 2)).view(B, F, h // 2, w // 2)
         yn, un, vn = y.numpy(), u.numpy(), v.numpy()
         for b, (key, _, s, c) in enumerate(chunk):
             cl = clips[key]
@@ -194,23 +322,31 @@ class GpuBackend:
                 yn[b, c:], un[b, c:], vn[b, c:] = cl.y[s + c - 1], cl.u[s + c - 1], cl.v[s + c - 1]
         (dy, du, dv), ev = self._streams.upload([y, u, v], self.device)
         self._streams.wait(ev)
+        if ev is not None:
+            ev.synchronize()  # the staging buffers go back to the pool
+        for t in (y, u, v):
+            self._pinned.put(t)
         tm.add("upload_s", time.perf_counter() - t0)
-        return self._run_encoder(chunk, params, dy, du, dv, tm)
+        return dy, du, dv
 
-    def _run_encoder(self, chunk, params, dy, du, dv, tm: Timer):
-        B = len(chunk)
+    def _run_encoder(self, chunk, params, dy, du, dv, tm: Timer, qp_delta=None):
         t1 = time.perf_counter()
-        enc = self._encoder(params, B)
-        if hasattr(enc, "encode") and type(params).__name__ == "HevcParams":
-            res = enc.encode(dy, du, dv)
+        enc = self._encoder(params, len(chunk))
+        if type(params).__name__ == "HevcParams":
+            res = enc.encode(dy, du, dv, qp_delta=qp_delta)
         else:
             # a short segment (padded to F frames) must end on an anchor to be cut there
             res = enc.encode(dy, du, dv, idr_ids=[idr_id(key, un_) for key, un_, _, _ in chunk],
-                             anchors_at=sorted({c - 1 for _, _, _, c in chunk}))
+                             anchors_at=sorted({c - 1 for _, _, _, c in chunk}), qp_delta=qp_delta)
         tm.add("encode_s", time.perf_counter() - t1)
         ps = enc.parameter_sets()
-        return [(key, un_, ps + b"".join(res[b].display_prefix(c)), res[b].psnr_y, getattr(res[b], "ssim_y", 0.0))
-                for b, (key, un_, s, c) in enumerate(chunk)]
+        out = []
+        for b, (key, un_, s, c) in enumerate(chunk):
+            nals = res[b].display_prefix(c)
+            order = list(getattr(res[b], "order", range(len(nals))))[:len(nals)]
+            out.append(dict(key=key, unit=un_, stream=ps + b"".join(nals), psnr=res[b].psnr_y,
+                            ssim=getattr(res[b], "ssim_y", 0.0), frame_bits=[8 * len(n) for n in nals], order=order))
+        return out
 
     def close(self):
         self._pool.close()

@@ -12,6 +12,8 @@ same command names, flags, shorts and defaults:
 Note ``-p`` is ``--piece`` under ``c`` but ``--port`` under ``t``, as in the reference.
 New commands: ``encode`` (single-node multi-GPU file encode), ``fleet`` (local GPU
 worker launcher replacing doOpt.go), ``probe``, ``decode``, ``synth``, ``merge``.
+Every command takes ``--config FILE`` (or ``MIVC_CONFIG``): a JSON/YAML overlay of
+option defaults per command; explicit flags win.
 """
 from __future__ import annotations
 
@@ -260,8 +262,67 @@ def build_parser() -> argparse.ArgumentParser:
     return ap
 
 
+# ---------------------------------------------------------------------------- config overlay
+def _load_config(path: str) -> dict:
+    """``--config FILE`` (JSON, or YAML by extension): option defaults per command, e.g.
+    ``{"*": {...}, "encode": {"slots": 64, "args": "265"}, "server c": {"port": 9000}}``.
+    Keys are argparse destinations; explicit command-line flags still win."""
+    with open(path) as f:
+        if path.endswith((".yaml", ".yml")):
+            import yaml
+            data = yaml.safe_load(f)
+        else:
+            data = json.load(f)
+    if not isinstance(data, dict):
+        raise SystemExit(f"{path}: config must be a mapping of command -> options")
+    return data
+
+
+def _subparser(ap: argparse.ArgumentParser, path: list[str]):
+    for name in path:
+        acts = [x for x in ap._actions if isinstance(x, argparse._SubParsersAction)]
+        if not acts or name not in acts[0].choices:
+            return None
+        ap = acts[0].choices[name]
+    return ap
+
+
+def _apply_config(ap: argparse.ArgumentParser, cfg: dict, argv: list[str]) -> None:
+    words = [w for w in argv if not w.startswith("-")]
+    for section, opts in cfg.items():
+        if not isinstance(opts, dict):
+            raise SystemExit(f"config section {section!r} must be a mapping")
+        path = section.replace(".", " ").split() if section != "*" else []
+        if path and words[:len(path)] != path:
+            continue  # a section for another command
+        targets = [_subparser(ap, words[:k]) for k in range(len(words) + 1)] if not path else [_subparser(ap, path)]
+        targets = [t for t in targets if t is not None]
+        for t in targets:
+            dests = {x.dest for x in t._actions}
+            known = {k: v for k, v in opts.items() if k in dests}
+            if path:
+                unknown = set(opts) - dests
+                if unknown:
+                    raise SystemExit(f"config section {section!r}: unknown options {sorted(unknown)}")
+            t.set_defaults(**known)
+
+
 def main(argv: list[str] | None = None) -> int:
-    a = build_parser().parse_args(argv)
+    argv = list(sys.argv[1:] if argv is None else argv)
+    cfg_path = os.environ.get("MIVC_CONFIG")
+    for i, w in enumerate(argv):
+        if w == "--config" and i + 1 < len(argv):
+            cfg_path = argv[i + 1]
+            del argv[i:i + 2]
+            break
+        if w.startswith("--config="):
+            cfg_path = w.split("=", 1)[1]
+            del argv[i]
+            break
+    ap = build_parser()
+    if cfg_path:
+        _apply_config(ap, _load_config(cfg_path), argv)
+    a = ap.parse_args(argv)
     if getattr(a, "rest", None) and a.rest[:1] == ["--"]:
         a.rest = a.rest[1:]
     return int(a.fn(a) or 0)

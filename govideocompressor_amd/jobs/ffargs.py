@@ -9,9 +9,12 @@ server.go:29) with two shorthands (server.go:67-71):
 and the worker splits them on single spaces (client.go:105).  Here the same
 strings select the native codec and its rate control.  Supported subset:
 ``-vcodec/-c:v/-codec:v`` (libx264, h264, libx265, hevc, h265), ``-crf``,
-``-qp``, ``-b:v``, ``-pass``, ``-s WxH``, ``-r``, ``-g``, ``-pix_fmt``
-(yuv420p, yuv420p10le), ``-preset``, ``-tune``, ``-profile:v`` (accepted),
-``-threads`` / ``-y`` / ``-an`` / ``-acodec copy`` (accepted, no effect).
+``-qp``, ``-b:v`` (ABR, :mod:`..rc.abr`), ``-pass 1|2`` + ``-passlogfile``,
+``-maxrate``/``-bufsize`` (VBV), ``-s WxH``, ``-r``, ``-g``, ``-pix_fmt``
+(yuv420p, yuv420p10le), ``-preset`` (:mod:`..rc.presets`), ``-tune``,
+``-profile:v`` (accepted), ``-threads`` / ``-y`` / ``-an`` (accepted, no effect),
+``-acodec copy`` / ``-c:a copy`` (audio passthrough: the piece's audio track is
+copied into the output container).
 Anything else is an error reported back as ``fail;<idx>;<reason>`` rather than
 silently ignored (reference defect D11: ffmpeg failures were only noticed at
 upload time).
@@ -46,6 +49,10 @@ class EncoderConfig:
     keyint: int | None = None
     pix_fmt: str = "yuv420p"
     preset: str = "medium"
+    maxrate: int | None = None      # VBV, bits/s
+    bufsize: int | None = None      # VBV, bits
+    passlogfile: str | None = None
+    audio: str = "copy"             # "copy" (ffmpeg's default for -acodec copy pieces) or "none" (-an)
     ignored: list[str] = field(default_factory=list)
 
     @property
@@ -54,7 +61,8 @@ class EncoderConfig:
 
     def as_dict(self) -> dict:
         return dict(codec=self.codec, crf=self.crf, qp=self.qp, bitrate=self.bitrate, two_pass=self.two_pass,
-                    size=self.size, fps=self.fps, keyint=self.keyint, pix_fmt=self.pix_fmt, preset=self.preset)
+                    size=self.size, fps=self.fps, keyint=self.keyint, pix_fmt=self.pix_fmt, preset=self.preset,
+                    maxrate=self.maxrate, bufsize=self.bufsize, audio=self.audio)
 
 
 def expand_preset(args: str) -> str:
@@ -120,6 +128,12 @@ def _parse(args: str) -> EncoderConfig:
             cfg.two_pass = int(val())
             if cfg.two_pass not in (1, 2):
                 raise FfArgsError("-pass must be 1 or 2")
+        elif t == "-passlogfile":
+            cfg.passlogfile = val()
+        elif t == "-maxrate":
+            cfg.maxrate = _bitrate(val())
+        elif t == "-bufsize":
+            cfg.bufsize = _bitrate(val())
         elif t == "-s":
             v = val().lower()
             try:
@@ -141,16 +155,33 @@ def _parse(args: str) -> EncoderConfig:
         elif t in ("-preset", "-tune", "-profile:v", "-level", "-x264-params", "-x265-params"):
             v = val()
             if t == "-preset":
-                cfg.preset = v
+                from ..rc import presets
+                try:
+                    cfg.preset = presets.check(v)
+                except presets.PresetError as e:
+                    raise FfArgsError(str(e)) from None
             else:
                 cfg.ignored.append(f"{t} {v}")
-        elif t in ("-threads", "-acodec", "-c:a", "-ac", "-ar", "-b:a", "-map", "-f"):
+        elif t in ("-acodec", "-c:a", "-codec:a"):
+            a = val().lower()
+            if a != "copy":
+                raise FfArgsError(f"audio codec {a}: only stream copy (-acodec copy) is supported")
+            cfg.audio = "copy"
+        elif t == "-an":
+            cfg.audio = "none"
+        elif t in ("-threads", "-ac", "-ar", "-b:a", "-map", "-f"):
             cfg.ignored.append(f"{t} {val()}")
-        elif t in ("-y", "-an", "-n", "-hide_banner"):
+        elif t in ("-y", "-n", "-hide_banner"):
             cfg.ignored.append(t)
         else:
             raise FfArgsError(f"unsupported option {t}")
         i += 1
     if cfg.codec == "hevc" and not crf_given and cfg.qp is None and cfg.bitrate is None:
         cfg.crf = 28.0  # x265 default CRF
+    if cfg.two_pass and cfg.bitrate is None:
+        raise FfArgsError("-pass needs a target bitrate (-b:v)")
+    if (cfg.maxrate is None) != (cfg.bufsize is None):
+        raise FfArgsError("-maxrate and -bufsize go together (VBV)")
+    if cfg.bitrate is not None and cfg.bitrate <= 0:
+        raise FfArgsError("-b:v must be positive")
     return cfg

@@ -198,6 +198,10 @@ def _resolve(device) -> torch.device:
     return d
 
 
+class CabacPoolExhausted(RuntimeError):
+    """The batch's CABAC symbols outgrew the pool (very low QPs); encode() grows it and retries."""
+
+
 class GpuH264Encoder:
     """Batched gfx950 H.264 encoder: Main profile with GPU CABAC (default) or Constrained
     Baseline with GPU CAVLC; ``entropy="cpu"`` codes the slices with the host writers."""
@@ -304,8 +308,12 @@ class GpuH264Encoder:
         self.cfg = params.host_cfg()
         self.timings: dict[str, float] = {}
         self.stats: dict[str, float] = {}
+        # per-stage device time (HIP events on the encode stream, resolved lazily) and roctx
+        # ranges; off unless MIVC_STAGE_TIMING=1 or enabled by the caller (bench.py warmup)
+        from ..obs.timers import EventTimer
+        self.stage_timer = EventTimer(enabled=os.environ.get("MIVC_STAGE_TIMING", "0") == "1")
 
-    def _alloc_cabac(self, group: int | None):
+    def _alloc_cabac(self, group: int | None, grow: int = 1):
         """GPU CABAC buffers.  Per frame step (copy stream): block masks, per-MB coding state
         and symbol counts.  Per group of G steps, double-buffered (group g binarises into
         ring g % 2 while the arithmetic coder drains ring (g - 1) % 2 on the entropy stream):
@@ -319,8 +327,9 @@ class GpuH264Encoder:
         self.cab_G = G
         # pool budget: an average per MB and frame step plus one picture's worth of intra-heavy
         # headroom per group (IDR / scene cuts / low QPs run to several hundred symbols per MB)
-        per_mb = int(os.environ.get("MIVC_CABAC_SYMS_PER_MB", 96))
-        peak_mb = int(os.environ.get("MIVC_CABAC_PEAK_SYMS_PER_MB", 768))
+        per_mb = int(os.environ.get("MIVC_CABAC_SYMS_PER_MB", 96)) * grow
+        peak_mb = int(os.environ.get("MIVC_CABAC_PEAK_SYMS_PER_MB", 768)) * grow
+        self.cab_grow = grow
         gap = int(self.hip.cabac_gap())
         L = G * B
         self.cab_pool_cap = B * nmb * (G * per_mb + peak_mb) + L * (gap + 8) + 64
@@ -398,71 +407,81 @@ class GpuH264Encoder:
         idr = pic.kind == "I"
         aq = 0
         mbt = self._mbtree
+        st = self.stage_timer
         if self.p.aq_strength > 0 or mbt is not None:
             aq = P(self.aq)
             extra, stride = 0, 0
             # MB-tree offsets belong to referenced pictures; B pictures get variance AQ only
             if mbt is not None and mbt.shape[2] == self.nmb and pic.kind != "B":
                 extra, stride = mbt.data_ptr() + pic.d * self.nmb * 4, mbt.shape[1] * self.nmb
-            self.hip.aq_offsets(B, wmb, hmb, sy, su, sv, float(self.p.aq_strength), aq, s, extra, stride)
+            with st("aq"):
+                self.hip.aq_offsets(B, wmb, hmb, sy, su, sv, float(self.p.aq_strength), aq, s, extra, stride)
         cqo = self.p.chroma_qp_offset
         if pic.kind == "P":
             fy, fu, fv = (P(x) for x in ref0)
             self.intra_count.zero_()
             hp = P(self.me_hp[(pic.anchor - 1) & 1])
-            self.hip.me(B, wmb, hmb, sy, fy, P(self.prev_mv), P(self.mv), P(self.me_cost), P(self.pred),
-                        P(self.intra_cost), P(self.qp), self.p.me_range, self.p.subpel, s, hp, aq, 1)
-            for it in range(int(self.p.skip_refine)):
-                a_, b_ = (self.mv, self.mv_tmp) if it % 2 == 0 else (self.mv_tmp, self.mv)
-                self.hip.p_refine(B, wmb, hmb, sy, fy, hp, P(a_), P(b_), P(self.me_cost), P(self.prev_mv),
-                                  P(self.pred), P(self.qp), aq, s)
-            if int(self.p.skip_refine) % 2:
-                self.mv.copy_(self.mv_tmp)
+            with st("me_p"):
+                self.hip.me(B, wmb, hmb, sy, fy, P(self.prev_mv), P(self.mv), P(self.me_cost), P(self.pred),
+                            P(self.intra_cost), P(self.qp), self.p.me_range, self.p.subpel, s, hp, aq, 1)
+                for it in range(int(self.p.skip_refine)):
+                    a_, b_ = (self.mv, self.mv_tmp) if it % 2 == 0 else (self.mv_tmp, self.mv)
+                    self.hip.p_refine(B, wmb, hmb, sy, fy, hp, P(a_), P(b_), P(self.me_cost), P(self.prev_mv),
+                                      P(self.pred), P(self.qp), aq, s)
+                if int(self.p.skip_refine) % 2:
+                    self.mv.copy_(self.mv_tmp)
             if cut is not None:
                 self.intra_cost.masked_fill_(cut[:, None], -1)  # intra beats any inter cost
-            self.hip.encode_inter(B, wmb, hmb, sy, su, sv, fy, fu, fv, ry, ru, rv, P(self.pred), P(self.mv),
-                                  P(self.me_cost), P(self.intra_cost), P(self.qp), cqo, P(hdr), P(coef), P(self.nz),
-                                  P(self.intra_flag), P(self.intra_count), s, aq)
+            with st("inter"):
+                self.hip.encode_inter(B, wmb, hmb, sy, su, sv, fy, fu, fv, ry, ru, rv, P(self.pred), P(self.mv),
+                                      P(self.me_cost), P(self.intra_cost), P(self.qp), cqo, P(hdr), P(coef),
+                                      P(self.nz), P(self.intra_flag), P(self.intra_count), s, aq)
             self.prev_mv.copy_(self.mv)
         elif pic.kind == "B":
             f0y, f0u, f0v = (P(x) for x in ref0)
             f1y, f1u, f1v = (P(x) for x in ref1)
             hp0, hp1 = P(self.me_hp[(pic.l1_anchor - 1) & 1]), P(self.me_hp[pic.l1_anchor & 1])
             dsf, copy = self._dist_scale(pic.poc, 2 * pic.l0, 2 * pic.l1)
-            self.hip.b_direct(B, wmb, hmb, P(self.col_hdr), dsf, copy, P(self.dmv), P(self.pm0), P(self.pm1), s)
             self.intra_count.zero_()
             br = self.p.b_me_range
-            self.hip.me(B, wmb, hmb, sy, f0y, P(self.pm0), P(self.mv), P(self.me_cost), P(self.pred),
-                        P(self.intra_cost), P(self.qp), br, self.p.subpel, s, hp0, aq, 1)
-            self.hip.me(B, wmb, hmb, sy, f1y, P(self.pm1), P(self.mv1), P(self.me_cost1), P(self.pred1),
-                        P(self.intra_cost), P(self.qp), br, self.p.subpel, s, hp1, aq, 1)
-            self.hip.b_decide(B, wmb, hmb, sy, f0y, f1y, hp0, hp1, P(self.mv), P(self.mv1), P(self.me_cost),
-                              P(self.me_cost1), P(self.pred), P(self.pred1), P(self.pm0), P(self.pm1), P(self.dmv),
-                              P(self.qp), aq, P(hdr), P(self.pred_b), P(self.cost_b), s)
+            with st("me_b"):
+                self.hip.b_direct(B, wmb, hmb, P(self.col_hdr), dsf, copy, P(self.dmv), P(self.pm0), P(self.pm1), s)
+                self.hip.me(B, wmb, hmb, sy, f0y, P(self.pm0), P(self.mv), P(self.me_cost), P(self.pred),
+                            P(self.intra_cost), P(self.qp), br, self.p.subpel, s, hp0, aq, 1)
+                self.hip.me(B, wmb, hmb, sy, f1y, P(self.pm1), P(self.mv1), P(self.me_cost1), P(self.pred1),
+                            P(self.intra_cost), P(self.qp), br, self.p.subpel, s, hp1, aq, 1)
+            with st("b_decide"):
+                self.hip.b_decide(B, wmb, hmb, sy, f0y, f1y, hp0, hp1, P(self.mv), P(self.mv1), P(self.me_cost),
+                                  P(self.me_cost1), P(self.pred), P(self.pred1), P(self.pm0), P(self.pm1),
+                                  P(self.dmv), P(self.qp), aq, P(hdr), P(self.pred_b), P(self.cost_b), s)
             if cut is not None:
                 self.intra_cost.masked_fill_(cut[:, None], -1)
-            self.hip.encode_inter(B, wmb, hmb, sy, su, sv, f0y, f0u, f0v, ry, ru, rv, P(self.pred_b), P(self.mv),
-                                  P(self.cost_b), P(self.intra_cost), P(self.qp), cqo, P(hdr), P(coef), P(self.nz),
-                                  P(self.intra_flag), P(self.intra_count), s, aq, f1u, f1v, 1)
+            with st("inter"):
+                self.hip.encode_inter(B, wmb, hmb, sy, su, sv, f0y, f0u, f0v, ry, ru, rv, P(self.pred_b), P(self.mv),
+                                      P(self.cost_b), P(self.intra_cost), P(self.qp), cqo, P(hdr), P(coef),
+                                      P(self.nz), P(self.intra_flag), P(self.intra_count), s, aq, f1u, f1v, 1)
         if pic.kind != "I":
             self.p_intra_mbs += self.intra_count.sum()
             flag_ptr, count_ptr = P(self.intra_flag), P(self.intra_count)
         else:
             self.prev_mv.zero_()
             flag_ptr, count_ptr = 0, 0
-        self.hip.encode_intra(B, wmb, hmb, sy, su, sv, ry, ru, rv, P(self.qp), cqo, P(hdr), P(coef), P(self.nz),
-                              flag_ptr, count_ptr, P(self.err),
-                              int(self.p.i4x4 and (idr or self.p.i4x4_in_p or cut is not None)), s, aq)
+        with st("intra"):
+            self.hip.encode_intra(B, wmb, hmb, sy, su, sv, ry, ru, rv, P(self.qp), cqo, P(hdr), P(coef), P(self.nz),
+                                  flag_ptr, count_ptr, P(self.err),
+                                  int(self.p.i4x4 and (idr or self.p.i4x4_in_p or cut is not None)), s, aq)
         if aq:
             # MBs without mb_qp_delta take QP_pred (clause 7.4.5): their records must say so
             # before deblocking reads every MB's QP
             self.hip.qp_fixup(B, wmb, hmb, P(hdr), P(coef), P(self.nz), P(self.qp_flags), P(self.qp), s)
         if self.p.deblock:
-            self.hip.deblock(B, wmb, hmb, ry, ru, rv, P(hdr), P(self.nz), cqo, 0, 0, P(self.err), s)
+            with st("deblock"):
+                self.hip.deblock(B, wmb, hmb, ry, ru, rv, P(hdr), P(self.nz), cqo, 0, 0, P(self.err), s)
         if pic.kind != "B":
             # the anchor's half-sample planes (shared by every picture that references it) and,
             # for the B pictures after it, its motion as the temporal-direct co-located field
-            self.hip.me_halfpel(B, self.W, self.H, ry, P(self.me_hp[pic.anchor & 1]), s)
+            with st("halfpel"):
+                self.hip.me_halfpel(B, self.W, self.H, ry, P(self.me_hp[pic.anchor & 1]), s)
             if self.nb and pic.kind == "P":
                 self.col_hdr.copy_(hdr)
 
@@ -547,8 +566,8 @@ class GpuH264Encoder:
                 wrap_futs[f] = self.pool.submit(lambda: [(b"", 0)] * B)
             copied[g].set()
             if err & 4:
-                raise RuntimeError("GPU CABAC: symbol pool exhausted (raise MIVC_CABAC_SYMS_PER_MB / "
-                                   "MIVC_CABAC_PEAK_SYMS_PER_MB or lower cabac_group)")
+                raise CabacPoolExhausted("GPU CABAC: symbol pool exhausted (raise MIVC_CABAC_SYMS_PER_MB / "
+                                         "MIVC_CABAC_PEAK_SYMS_PER_MB or lower cabac_group)")
             raise RuntimeError("GPU CABAC: arithmetic coder error")
         r16 = (sizes + 15) & ~15
         total = int(r16.sum())
@@ -688,7 +707,24 @@ class GpuH264Encoder:
     @torch.no_grad()
     def encode(self, y: torch.Tensor, u: torch.Tensor, v: torch.Tensor, idr_base: int = 0,
                keep_recon: bool = False, metrics: bool = True, idr_ids: list[int] | None = None,
-               qps=None, anchors_at=()) -> list[SegmentResult]:
+               qps=None, anchors_at=(), qp_delta=None) -> list[SegmentResult]:
+        """See :meth:`_encode`.  A batch whose CABAC symbols overflow the pool (QPs far below
+        the budgeted ones) is encoded again with a pool grown 4x (encoding is a pure
+        function of the inputs, so the retry gives the same bytes a big pool would)."""
+        for attempt in range(3):
+            try:
+                return self._encode(y, u, v, idr_base, keep_recon, metrics, idr_ids, qps, anchors_at, qp_delta)
+            except CabacPoolExhausted:
+                if attempt == 2 or not (self.entropy == "gpu" and self.p.cabac):
+                    raise
+                torch.cuda.synchronize(self.dev)
+                self._alloc_cabac(self.cab_G, grow=self.cab_grow * 4)
+                self.stats["cabac_pool_regrow"] = self.stats.get("cabac_pool_regrow", 0) + 1
+        raise AssertionError("unreachable")
+
+    def _encode(self, y: torch.Tensor, u: torch.Tensor, v: torch.Tensor, idr_base: int = 0,
+                keep_recon: bool = False, metrics: bool = True, idr_ids: list[int] | None = None,
+                qps=None, anchors_at=(), qp_delta=None) -> list[SegmentResult]:
         """Encode B segments of F frames each.
 
         y: [B, F, h, w] uint8 (device), u/v: [B, F, h/2, w/2].  Each slot's output is a
@@ -696,7 +732,10 @@ class GpuH264Encoder:
         reference's split directory, with idr_pic_id = idr_ids[slot] (default idr_base + slot).
         When (h, w) differs from the configured size the prep kernel resamples (``-s WxH``).
         ``qps``: optional [B, F] per-frame QPs from the rate control (default: the params' CRF/QP,
-        I frames 3 lower).
+        I frames 3 lower).  ``qp_delta``: optional [B, F] float offsets (display order) added
+        to the final frame QPs -- after the lookahead CRF curve and the B-picture offset --
+        with ordered dithering, so fractional offsets move the bitrate smoothly
+        (:mod:`govideocompressor_amd.rc.abr`: -b:v, -pass 2, VBV).
         """
         B, F = y.shape[0], y.shape[1]
         if B != self.B:
@@ -733,6 +772,10 @@ class GpuH264Encoder:
             # B pictures one pbratio step above their anchors (x264 --pbratio 1.3 = +2 QP)
             bd = [pic.d for pic in plan if pic.kind == "B"]
             qps_h[:, bd] = np.minimum(qps_h[:, bd] + int(self.p.b_qp_offset), 51)
+        if qp_delta is not None:
+            from ..rc.abr import apply_delta
+            qps_h = apply_delta(qps_h, qp_delta)
+        self.last_qps = qps_h.copy()
         # per coding step (rows), [F, B]: the entropy stages index coding steps
         qps_d = torch.from_numpy(np.ascontiguousarray(qps_h[:, order].T)).to(self.dev)
         cuts_c = cuts_h[:, order]
@@ -850,6 +893,8 @@ class GpuH264Encoder:
             self.stats["p_intra_ratio"] = float(self.p_intra_mbs.item()) / (B * (F - 1) * self.nmb)
         self.p_intra_mbs.zero_()
         err = int(self.err.item())
+        if err & 4:
+            raise CabacPoolExhausted(f"GPU CABAC: symbol pool exhausted (err={err:#x})")
         if err & 14:
             raise RuntimeError(f"GPU CABAC failed (err={err:#x}: 4 = symbol pool exhausted, 8 = coder error)")
         if err != 0:

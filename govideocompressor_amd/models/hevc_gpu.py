@@ -195,7 +195,7 @@ class GpuHevcEncoder:
 
     # ------------------------------------------------------------------ encode
     def encode(self, y: torch.Tensor, u: torch.Tensor, v: torch.Tensor, qps: np.ndarray | None = None,
-               keep_recon: bool = False, metrics: bool = True) -> list[HevcSegmentResult]:
+               keep_recon: bool = False, metrics: bool = True, qp_delta=None) -> list[HevcSegmentResult]:
         """y: [B, F, h, w] (uint8, or uint16 holding bit_depth-bit samples), u/v half size.
         Every segment starts with an IDR picture; the others are P pictures
         (intra_only: IDR pictures only)."""
@@ -216,6 +216,10 @@ class GpuHevcEncoder:
         if self.p.wpp:  # spread the pool's threads over the B pictures of a step
             cfg["threads"] = max(1, min(32, self.pool._max_workers // max(1, B)))
         qps = np.clip(np.asarray(qps, dtype=np.int32).reshape(B, F), 0, 51)
+        if qp_delta is not None:
+            from ..rc.abr import apply_delta
+            qps = apply_delta(qps, qp_delta)
+        self.last_qps = qps.copy()
         qps_d = torch.from_numpy(np.ascontiguousarray(qps.T)).to(self.dev)  # [F, B], one upload
         nals: list[list] = [[None] * F for _ in range(B)]
         futs = []
@@ -242,6 +246,7 @@ class GpuHevcEncoder:
                           p(self.qp), p(self.run), p(self.cand), bd)
             if idr:
                 self.run.fill_(1)
+                self.prev_mv.zero_()  # no motion predictors across a closed GOP (or from an earlier call)
                 self.hip.hevc_intra(*intra_args, 1, 1, p(self.err), s)
             else:
                 self.run.fill_(2)

@@ -56,9 +56,11 @@ class EventTimer:
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
         a.record()
+        torch.cuda.nvtx.range_push(stage)  # roctx range for rocprofv3 --marker-trace
         try:
             yield
         finally:
+            torch.cuda.nvtx.range_pop()
             b.record()
             self.pending.append((stage, a, b))
 
@@ -75,6 +77,11 @@ class EventTimer:
     def summary(self) -> dict:
         self.resolve()
         return {k: {"s": round(v, 6), "n": self.count[k]} for k, v in self.total.items()}
+
+    def reset(self) -> None:
+        self.resolve()
+        self.total.clear()
+        self.count.clear()
 
 
 def _nvtx():

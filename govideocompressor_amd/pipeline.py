@@ -86,7 +86,7 @@ def encode_file(path: str, output: str, args: str = "264", backend: str = "auto"
     gpu_decode = kind == "pieces" and hasattr(impl, "decode_streams")
     dec_stats: dict[str, float] = {}
 
-    def run(idxs: list[int]):
+    def run(idxs: list[int], offset: float | None = None, into: dict | None = None):
         if gpu_decode:  # compressed input on a GPU rank: batched GPU decode, frames stay on the device
             clips = impl.decode_streams([segs[i] for i in idxs], info.fps)
             for k, v in impl.decoder().stats.items():
@@ -94,20 +94,52 @@ def encode_file(path: str, output: str, args: str = "264", backend: str = "auto"
         else:
             clips = list(loader.map(lambda i: _load_segment(path, info, kind, segs, i), idxs))
         items = [(str(i), c) for i, c in zip(idxs, clips)]
-        res = impl.encode_clips(items, cfg)
+        if offset is None:
+            res = impl.encode_clips(items, cfg)
+        else:
+            res = impl.encode_clips(items, cfg, qp_offsets={str(i): offset for i in idxs})
         for i in idxs:
             stream, st = res[str(i)]
-            mine[i] = stream
+            (mine if into is None else into)[i] = stream
             stats.append(st)
 
-    if schedule == "dynamic":
+    rate = None
+    if cfg.bitrate is not None and hasattr(impl, "decode_streams"):
+        # global rate control over the whole file (x264 two-pass semantics): one QP offset
+        # for every segment of every rank, solved on all-reduced bit totals (CC-1)
+        from .rc.abr import OffsetSearch
+        schedule = "static"
+        if kind == "ranges":
+            my = P.shard(segs, env.rank, env.world, by_cost=True)
+        else:
+            my = list(range(env.rank, n, env.world))
+        target = float(cfg.bitrate) * info.frames / (cfg.fps or info.fps)
+        search = OffsetSearch(np.array([target]), max_passes=4)
+        passes: list[dict] = []
+        off = 0.0
+        while True:
+            got: dict[int, bytes] = {}
+            stats.clear()
+            for b in range(0, len(my), slots):
+                run(my[b:b + slots], off, got)
+            total = D.sum_over_ranks(env, float(sum(8 * len(x) for x in got.values())))
+            search.observe([off], [total])
+            passes.append(got)
+            if search.done():
+                break
+            off = float(search.propose()[0])
+        best = search.best()
+        mine.update(passes[best])
+        rate = {"target_bits": target, "bits": float(search.hist[best][1][0]), "qp_offset": float(search.hist[best][0][0]),
+                "rate_passes": len(passes)}
+    elif schedule == "dynamic":
         td = TicketDispenser(n)
         while True:
             got = td.claim(slots)
             if not got:
                 break
             run(got)
-    else:
+    elif rate is None:
         if kind == "ranges":
             my = P.shard(segs, env.rank, env.world, by_cost=True)
         else:
@@ -120,7 +152,7 @@ def encode_file(path: str, output: str, args: str = "264", backend: str = "auto"
     idx_blob = json.dumps(order).encode()
     g = D.BitstreamGather(env, [idx_blob] + [mine[i] for i in order]).start()
     gathered = g.wait()
-    out = {"segments": n, "world": env.world, "encode_s_rank": t_enc,
+    out = {"segments": n, "world": env.world, "encode_s_rank": t_enc, "rate": rate,
            "decode": ("gpu" if gpu_decode else "cpu"), "decode_stats_rank": dec_stats}
     if env.is_main:
         by_idx: dict[int, bytes] = {}

@@ -57,7 +57,7 @@ class GpuLookahead:
         costs, blk, mv = self.frame_costs(y, block_costs=True, block_mvs=True)
         n = B * F * lbw * lbh
         if getattr(self, "_prop", None) is None or self._prop.numel() < n:
-            self._prop = torch.empty((n,), dtype=torch.float32, device=self.dev)
+            self._prop = torch.empty((n,), dtype=torch.int64, device=self.dev)  # fixed-point accumulators
         out = torch.empty((B, F, lbh * lbw), dtype=torch.float32, device=self.dev)
         self.hip.mbtree(B, F, lbw, lbh, blk.data_ptr(), mv.data_ptr(), self._prop.data_ptr(), float(strength),
                         out.data_ptr(), torch.cuda.current_stream(self.dev).cuda_stream)

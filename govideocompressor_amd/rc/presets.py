@@ -1,0 +1,78 @@
+"""``-preset`` (x264/x265 speed presets) -> encoder knobs.
+
+The reference passes ``-preset`` straight to libx264/libx265 (raw ffmpeg args,
+client.go:105-112).  The gfx950 encoders expose the same trade-off through their
+search and analysis parameters; each preset maps onto the x264 preset's intent:
+
+==========  ========================================================================
+preset      H.264 knobs (x264 equivalent)
+==========  ========================================================================
+ultrafast   CAVLC, no B, no deblock, no AQ/MB-tree/lookahead, integer-pel ME radius 4,
+            Intra16x16 only (x264: --no-cabac --bframes 0 --no-deblock --aq-mode 0
+            --subme 0 --me dia --partitions none --rc-lookahead 0)
+superfast   CABAC + 3 B, half-pel, radius 4, no MB-tree (--subme 1 --me dia --no-mbtree)
+veryfast    half-pel, radius 8 (--subme 2)
+faster      quarter-pel, radius 8, one skip-refine pass (--subme 4)
+fast        quarter-pel, radius 8 (--subme 6)
+medium      defaults (x264 defaults, the reference's "264" preset)
+slow        radius 12, B radius 6, Intra4x4 in P pictures (--me umh --subme 8)
+slower      radius 16, B radius 8, lookahead radius 8 (--subme 9 --me umh)
+veryslow    slower + three skip-refine passes (--subme 10 --me umh --merange 24)
+placebo     = veryslow
+==========  ========================================================================
+
+HEVC (x265): ultrafast..veryfast use radius 4 / half-pel / 3 merge candidates, fast and
+medium the defaults, slow and slower radius 12 / 5 candidates, veryslow/placebo radius 16.
+"""
+from __future__ import annotations
+
+import dataclasses
+
+NAMES = ("ultrafast", "superfast", "veryfast", "faster", "fast", "medium", "slow", "slower", "veryslow", "placebo")
+
+H264 = {
+    "ultrafast": dict(cabac=False, bframes=0, deblock=False, aq_strength=0.0, mbtree=False, lookahead=False,
+                      scenecut=0, subpel=0, me_range=4, i4x4=False, skip_refine=0),
+    "superfast": dict(subpel=1, me_range=4, mbtree=False, skip_refine=0, b_me_range=2),
+    "veryfast": dict(subpel=1, me_range=8, skip_refine=1),
+    "faster": dict(subpel=2, me_range=8, skip_refine=1),
+    "fast": dict(subpel=2, me_range=8),
+    "medium": dict(),
+    "slow": dict(me_range=12, b_me_range=6, i4x4_in_p=True),
+    "slower": dict(me_range=16, b_me_range=8, i4x4_in_p=True, la_range=8),
+    "veryslow": dict(me_range=16, b_me_range=8, i4x4_in_p=True, la_range=8, skip_refine=3),
+}
+H264["placebo"] = H264["veryslow"]
+
+HEVC = {
+    "ultrafast": dict(me_range=4, subpel=1, max_merge=3, la_range=4),
+    "superfast": dict(me_range=4, subpel=1, max_merge=3, la_range=4),
+    "veryfast": dict(me_range=4, subpel=2, max_merge=3),
+    "faster": dict(me_range=8, max_merge=3),
+    "fast": dict(me_range=8, max_merge=4),
+    "medium": dict(),
+    "slow": dict(me_range=12),
+    "slower": dict(me_range=12, la_range=8),
+    "veryslow": dict(me_range=16, la_range=8),
+}
+HEVC["placebo"] = HEVC["veryslow"]
+
+
+class PresetError(ValueError):
+    pass
+
+
+def check(name: str) -> str:
+    n = (name or "medium").lower()
+    if n not in NAMES:
+        raise PresetError(f"unknown preset {name} (one of {', '.join(NAMES)})")
+    return n
+
+
+def apply(params, name: str):
+    """A copy of ``params`` (H264Params or HevcParams) with the preset's knobs."""
+    n = check(name)
+    table = HEVC if type(params).__name__ == "HevcParams" else H264
+    fields = {f.name for f in dataclasses.fields(params)}
+    over = {k: v for k, v in table[n].items() if k in fields}
+    return dataclasses.replace(params, **over)

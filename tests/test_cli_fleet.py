@@ -85,3 +85,32 @@ def test_fleet_never_kills_foreign_pids(tmp_path):
     finally:
         p.kill()
         p.wait()
+
+
+def test_cli_config_overlay(tmp_path):
+    """--config FILE: per-command option defaults (JSON/YAML); explicit flags win."""
+    import json as _json
+
+    from govideocompressor_amd import cli
+    cfgp = tmp_path / "c.json"
+    cfgp.write_text(_json.dumps({"server c": {"port": 9100, "ff": "265"}, "server t": {"port": 9200}}))
+    ap = cli.build_parser()
+    argv = ["server", "c", "x.mp4"]
+    cli._apply_config(ap, cli._load_config(str(cfgp)), argv)
+    a = ap.parse_args(argv)
+    assert int(a.port) == 9100 and a.ff == "265"
+    ap = cli.build_parser()
+    argv = ["server", "c", "x.mp4", "--port", "9300"]
+    cli._apply_config(ap, cli._load_config(str(cfgp)), argv)
+    assert int(ap.parse_args(argv).port) == 9300
+    y = tmp_path / "c.yaml"
+    y.write_text("server t:\n  port: 9400\n")
+    ap = cli.build_parser()
+    argv = ["server", "t"]
+    cli._apply_config(ap, cli._load_config(str(y)), argv)
+    assert int(ap.parse_args(argv).port) == 9400
+    bad = tmp_path / "b.json"
+    bad.write_text(_json.dumps({"server c": {"nonsense": 1}}))
+    ap = cli.build_parser()
+    with pytest.raises(SystemExit):
+        cli._apply_config(ap, cli._load_config(str(bad)), ["server", "c", "x.mp4"])

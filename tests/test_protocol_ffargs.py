@@ -117,3 +117,15 @@ def test_ffargs_errors():
                 "-pix_fmt rgb24", "-crf abc", "-g x", "-vcodec \"libx264"):
         with pytest.raises(ffargs.FfArgsError):
             ffargs.parse(bad)
+
+
+def test_ffargs_rate_vbv_audio_options():
+    c = ffargs.parse("-vcodec libx264 -b:v 2M -maxrate 3M -bufsize 4M -pass 1 -passlogfile /tmp/x -preset SLOW")
+    assert (c.bitrate, c.maxrate, c.bufsize, c.two_pass, c.passlogfile, c.preset) == (
+        2_000_000, 3_000_000, 4_000_000, 1, "/tmp/x", "slow")
+    assert ffargs.parse("264 -an".replace("264", "-vcodec libx264")).audio == "none"
+    assert ffargs.parse("-vcodec libx264 -acodec copy").audio == "copy"
+    for bad in ("-vcodec libx264 -pass 2", "-vcodec libx264 -b:v 1M -maxrate 2M", "-vcodec libx264 -preset warp9",
+                "-vcodec libx264 -acodec aac", "-vcodec libx264 -b:v 0"):
+        with pytest.raises(ffargs.FfArgsError):
+            ffargs.parse(bad)

@@ -1,0 +1,82 @@
+"""Rate-control plumbing on CPU: dithered QP offsets, the ABR secant search, VBV, presets,
+two-pass stats files, and the CPU backend's -b:v search (the GPU backend is covered by
+tests/test_gpu_ratecontrol.py)."""
+import math
+
+import numpy as np
+import pytest
+
+from govideocompressor_amd.jobs import ffargs
+from govideocompressor_amd.rc import abr, presets
+
+
+def test_apply_delta_dither_mean():
+    base = np.full((3, 60), 30, dtype=np.int32)
+    for d in (-2.5, -0.3, 0.0, 0.25, 1.7):
+        q = abr.apply_delta(base, np.full(3, d))
+        assert abs(q.mean() - (30 + d)) < 0.05
+        assert q.min() >= math.floor(30 + d) and q.max() <= math.ceil(30 + d)
+    assert np.array_equal(abr.apply_delta(base, np.zeros(3)), base)
+    assert abr.apply_delta(base, np.full((3, 60), 40.0)).max() == 51
+
+
+@pytest.mark.parametrize("e", [0.8, 1.0, 1.3, 1.9])
+def test_offset_search_converges(e):
+    c = np.array([4e6, 1e6, 2.5e5])
+    targets = np.array([2e6, 2e6, 2e5])
+    s = abr.OffsetSearch(targets, tol=0.02, max_passes=5)
+    d = np.zeros(3)
+    while True:
+        s.observe(d, c * 2.0 ** (-e * d / 6.0))
+        if s.done():
+            break
+        d = s.propose()
+    best = s.best_per_group()
+    err = [abs(s.hist[best[i]][1][i] / targets[i] - 1) for i in range(3)]
+    assert max(err) < 0.02
+
+
+def test_vbv_fill_and_deltas():
+    fps, maxrate, bufsize = 30.0, 1e6, 1e6
+    bits = np.full(60, maxrate / fps)
+    bits[10] = 2.5e6  # one huge frame underflows
+    assert abr.vbv_fill(bits, maxrate, bufsize, fps).min() < 0
+    dq = abr.vbv_deltas(bits, maxrate, bufsize, fps)
+    assert dq[10] > 0 and dq[20:].max() == 0
+    fixed = bits * 2.0 ** (-dq / 6.0)
+    assert abr.vbv_fill(fixed, maxrate, bufsize, fps).min() >= 0
+
+
+def test_stats_file_roundtrip(tmp_path):
+    p = abr.stats_path_for(str(tmp_path / "7.mp4"))
+    assert p.endswith("7.mivc2pass.json")
+    assert abr.stats_path_for(str(tmp_path / "7.mp4"), "/x/log").startswith("/x/log-7")
+    abr.save_stats(p, {"7": {"offset": 0.0, "bits": 1234.0, "frames": 30}})
+    assert abr.load_stats(p)["7"]["bits"] == 1234.0
+
+
+def test_presets_apply():
+    from govideocompressor_amd.models.h264_gpu import H264Params
+    from govideocompressor_amd.models.hevc_gpu import HevcParams
+    p = H264Params(width=64, height=64)
+    assert presets.apply(p, "medium") == p
+    u = presets.apply(p, "ultrafast")
+    assert (u.cabac, u.bframes, u.deblock, u.mbtree, u.subpel) == (False, 0, False, False, 0)
+    s = presets.apply(p, "veryslow")
+    assert s.me_range == 16 and s.i4x4_in_p
+    h = presets.apply(HevcParams(width=64, height=64), "ultrafast")
+    assert h.me_range == 4 and h.max_merge == 3
+    with pytest.raises(presets.PresetError):
+        presets.check("ludicrous")
+
+
+def test_cpu_backend_bitrate_search():
+    from govideocompressor_amd.backends.cpu_ref import CpuBackend
+    from govideocompressor_amd.utils import yuv
+    clip = yuv.synth_clip_cpu(12, 96, 64, seed=3)
+    be = CpuBackend(threads=2)
+    cfg = ffargs.parse("-vcodec libx264 -b:v 300k")
+    stream, st = be.encode_clip("0", clip, cfg)
+    target = 300e3 * 12 / clip.fps
+    # integer QP steps are ~12 % apart: the closest QP lands within one half step
+    assert abs(8 * len(stream) / target - 1) < 0.2
