@@ -1,5 +1,6 @@
 #include "annexb.h"
 
+#include <algorithm>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -403,6 +404,145 @@ std::vector<uint8_t> mux_mp4(const uint8_t* p, size_t n, double fps) {
   return out;
 }
 
+H264Samples h264_samples(const uint8_t* p, size_t n) {
+  std::vector<NalUnit> raw = parse_annexb(p, n, false);
+  std::vector<Au> aus = access_units(p, n, raw);
+  if (aus.empty()) throw std::runtime_error("h264_samples: no access units");
+  H264Samples out;
+  std::vector<h264::SPS> sps_tab(32);
+  std::vector<h264::PPS> pps_tab(256);
+  std::vector<char> have_sps(32, 0), have_pps(256, 0);
+  auto unescape = [&](size_t b, size_t e, size_t cap) {
+    std::vector<uint8_t> r;
+    r.reserve(std::min(e - b, cap));
+    int zeros = 0;
+    for (size_t j = b; j < e && r.size() < cap; ++j) {
+      uint8_t c = p[j];
+      if (zeros >= 2 && c == 3) {
+        zeros = 0;
+        continue;
+      }
+      r.push_back(c);
+      zeros = (c == 0) ? zeros + 1 : 0;
+    }
+    return r;
+  };
+  // POC state (8.2.1): previous reference picture's msb/lsb (type 0), previous picture's
+  // frame_num / FrameNumOffset (types 1 and 2)
+  int prev_msb = 0, prev_lsb = 0, prev_fn = 0, prev_fno = 0;
+  long long epoch = 0;
+  bool prev_mmco5 = false;
+  std::vector<std::pair<long long, long long>> keys;  // (epoch, poc) per sample
+  size_t ni = 0;
+  for (size_t a = 0; a < aus.size(); ++a) {
+    size_t before = out.data.size();
+    bool have_key = false;
+    while (ni < raw.size() && raw[ni].offset < aus[a].end) {
+      const NalUnit& u = raw[ni++];
+      int t = u.nal_unit_type;
+      size_t hdr = u.offset + (p[u.offset + 2] == 1 ? 3 : 4);
+      size_t len = u.offset + u.size - hdr;
+      while (len > 0 && p[hdr + len - 1] == 0) --len;
+      if (len == 0) continue;
+      if (t == 7 || t == 8) {
+        std::vector<uint8_t> rb = unescape(hdr + 1, hdr + len, SIZE_MAX);
+        BitReader br(rb.data(), rb.size());
+        if (t == 7) {
+          h264::SPS s = h264::parse_sps(br);
+          if (s.sps_id < 0 || s.sps_id > 31) throw std::runtime_error("h264_samples: bad sps id");
+          sps_tab[s.sps_id] = s;
+          have_sps[s.sps_id] = 1;
+          if (out.sps.empty()) {
+            out.sps.assign(p + hdr, p + hdr + len);
+            out.width = s.width_mbs * 16 - 2 * (s.crop_left + s.crop_right);
+            out.height = s.height_mbs * 16 - 2 * (s.crop_top + s.crop_bottom);
+            if (s.vui_present && s.num_units_in_tick) out.fps = s.time_scale / (2.0 * s.num_units_in_tick);
+          }
+        } else {
+          h264::PPS q = h264::parse_pps(br, sps_tab.data());
+          if (q.pps_id < 0 || q.pps_id > 255) throw std::runtime_error("h264_samples: bad pps id");
+          pps_tab[q.pps_id] = q;
+          have_pps[q.pps_id] = 1;
+          if (out.pps.empty()) out.pps.assign(p + hdr, p + hdr + len);
+        }
+        continue;
+      }
+      if (t != 9) {
+        put32(out.data, static_cast<uint32_t>(len));
+        out.data.insert(out.data.end(), p + hdr, p + hdr + len);
+      }
+      if (have_key || t < 1 || t > 5) continue;
+      have_key = true;
+      // slice headers with long reference-list modifications / weight tables stay within 4 KiB
+      std::vector<uint8_t> rb = unescape(hdr + 1, hdr + len, 4096);
+      BitReader br(rb.data(), rb.size());
+      h264::SliceHeader h = h264::parse_slice_header(br, t, u.nal_ref_idc, sps_tab.data(), pps_tab.data());
+      if (!have_pps[h.pps_id] || !have_sps[pps_tab[h.pps_id].sps_id])
+        throw std::runtime_error("h264_samples: slice before its parameter sets");
+      const h264::SPS& sp = sps_tab[pps_tab[h.pps_id].sps_id];
+      bool idr = t == 5;
+      if (idr || prev_mmco5) {
+        ++epoch;
+        prev_msb = prev_lsb = 0;
+        prev_fno = 0;
+        if (prev_mmco5) prev_fn = 0;
+      }
+      long long poc = 0;
+      int fno = 0;
+      int max_fn = 1 << sp.log2_max_frame_num;
+      if (sp.poc_type == 0) {
+        int max_lsb = 1 << sp.log2_max_poc_lsb, lsb = h.poc_lsb, msb;
+        if (lsb < prev_lsb && prev_lsb - lsb >= max_lsb / 2) msb = prev_msb + max_lsb;
+        else if (lsb > prev_lsb && lsb - prev_lsb > max_lsb / 2) msb = prev_msb - max_lsb;
+        else msb = prev_msb;
+        poc = msb + lsb;
+        if (u.nal_ref_idc) {
+          prev_msb = msb;
+          prev_lsb = lsb;
+        }
+      } else {
+        if (idr) fno = 0;
+        else if (prev_fn > h.frame_num) fno = prev_fno + max_fn;
+        else fno = prev_fno;
+        if (sp.poc_type == 2) {
+          poc = idr ? 0 : (u.nal_ref_idc == 0 ? 2LL * (fno + h.frame_num) - 1 : 2LL * (fno + h.frame_num));
+        } else {
+          int nc = static_cast<int>(sp.offset_for_ref_frame.size());
+          long long abs_fn = nc ? fno + h.frame_num : 0;
+          if (u.nal_ref_idc == 0 && abs_fn > 0) --abs_fn;
+          long long exp = 0;
+          if (abs_fn > 0) {
+            long long delta_cycle = 0;
+            for (int v : sp.offset_for_ref_frame) delta_cycle += v;
+            long long cycle = (abs_fn - 1) / nc, in_cycle = (abs_fn - 1) % nc;
+            exp = cycle * delta_cycle;
+            for (long long i = 0; i <= in_cycle; ++i) exp += sp.offset_for_ref_frame[i];
+          }
+          if (u.nal_ref_idc == 0) exp += sp.offset_for_non_ref_pic;
+          poc = exp + h.delta_poc[0];
+        }
+        prev_fno = fno;
+        prev_fn = h.frame_num;
+      }
+      bool mmco5 = false;
+      for (const h264::Mmco& m : h.mmco) mmco5 = mmco5 || m.op == 5;
+      prev_mmco5 = mmco5;
+      keys.emplace_back(epoch, mmco5 ? (1LL << 40) : poc);  // an mmco5 picture follows its epoch
+    }
+    if (!have_key) throw std::runtime_error("h264_samples: access unit without a slice");
+    out.sizes.push_back(static_cast<uint32_t>(out.data.size() - before));
+    out.sync.push_back(aus[a].idr ? 1 : 0);
+  }
+  if (out.sps.empty() || out.pps.empty()) throw std::runtime_error("h264_samples: stream has no SPS/PPS");
+  // display index = rank of (epoch, poc)
+  std::vector<int32_t> idx(keys.size());
+  for (size_t i = 0; i < idx.size(); ++i) idx[i] = static_cast<int32_t>(i);
+  std::stable_sort(idx.begin(), idx.end(), [&](int32_t x, int32_t y) { return keys[x] < keys[y]; });
+  out.display.assign(keys.size(), 0);
+  for (size_t r = 0; r < idx.size(); ++r) out.display[idx[r]] = static_cast<int32_t>(r);
+  return out;
+}
+
 namespace {
 struct BoxRef {
   const uint8_t* p;
@@ -438,6 +578,11 @@ BoxRef must(const BoxRef& in, const char* type) {
 }  // namespace
 
 std::vector<uint8_t> demux_mp4_to_annexb(const uint8_t* p, size_t n) {
+  // every read is checked against its box (workers parse network-fetched pieces;
+  // tests/test_fuzz_parsers.py runs this under ASan + UBSan)
+  auto need = [](const BoxRef& b, size_t off, size_t len, const char* what) {
+    if (off > b.n || len > b.n - off) throw std::runtime_error(std::string("mp4 demux: truncated ") + what);
+  };
   BoxRef file{p, n};
   BoxRef moov = must(file, "moov");
   BoxRef trak = must(moov, "trak");
@@ -446,47 +591,58 @@ std::vector<uint8_t> demux_mp4_to_annexb(const uint8_t* p, size_t n) {
   BoxRef st = must(minf, "stbl");
   BoxRef stsd = must(st, "stsd");
   // stsd: fullbox(4) entry_count(4) then sample entry box
+  need(stsd, 0, 8, "stsd");
   BoxRef entries{stsd.p + 8, stsd.n - 8};
   BoxRef avc1 = must(entries, "avc1");
+  need(avc1, 0, 78, "avc1");
   BoxRef avcc_parent{avc1.p + 78, avc1.n - 78};
   BoxRef avcc = must(avcc_parent, "avcC");
+  need(avcc, 0, 6, "avcC");
   const uint8_t* c = avcc.p;
   int len_size = (c[4] & 3) + 1;
   std::vector<uint8_t> ps;
   size_t off = 5;
-  int nsps = c[off++] & 31;
   static const uint8_t sc[4] = {0, 0, 0, 1};
-  for (int i = 0; i < nsps; ++i) {
-    int l = rd16(c + off);
-    off += 2;
-    ps.insert(ps.end(), sc, sc + 4);
-    ps.insert(ps.end(), c + off, c + off + l);
-    off += l;
-  }
-  int npps = c[off++];
-  for (int i = 0; i < npps; ++i) {
-    int l = rd16(c + off);
-    off += 2;
-    ps.insert(ps.end(), sc, sc + 4);
-    ps.insert(ps.end(), c + off, c + off + l);
-    off += l;
+  for (int list = 0; list < 2; ++list) {
+    need(avcc, off, 1, "avcC");
+    int cnt = list == 0 ? (c[off] & 31) : c[off];
+    ++off;
+    for (int i = 0; i < cnt; ++i) {
+      need(avcc, off, 2, "avcC");
+      size_t l = rd16(c + off);
+      off += 2;
+      need(avcc, off, l, "avcC parameter set");
+      ps.insert(ps.end(), sc, sc + 4);
+      ps.insert(ps.end(), c + off, c + off + l);
+      off += l;
+    }
   }
   BoxRef stsz = must(st, "stsz");
+  need(stsz, 0, 12, "stsz");
   uint32_t fixed = rd32(stsz.p + 4), count = rd32(stsz.p + 8);
+  if (!fixed) need(stsz, 12, size_t(count) * 4, "stsz");
+  if (count > n) throw std::runtime_error("mp4 demux: more samples than bytes");
   std::vector<uint32_t> sizes(count);
   for (uint32_t i = 0; i < count; ++i) sizes[i] = fixed ? fixed : rd32(stsz.p + 12 + 4 * i);
   std::vector<uint64_t> chunks;
   BoxRef co{};
   if (find_box(st.p, st.n, "stco", &co)) {
+    need(co, 0, 8, "stco");
     uint32_t nc = rd32(co.p + 4);
+    need(co, 8, size_t(nc) * 4, "stco");
     for (uint32_t i = 0; i < nc; ++i) chunks.push_back(rd32(co.p + 8 + 4 * i));
   } else {
     co = must(st, "co64");
+    need(co, 0, 8, "co64");
     uint32_t nc = rd32(co.p + 4);
+    need(co, 8, size_t(nc) * 8, "co64");
     for (uint32_t i = 0; i < nc; ++i) chunks.push_back((uint64_t(rd32(co.p + 8 + 8 * i)) << 32) | rd32(co.p + 12 + 8 * i));
   }
   BoxRef stsc = must(st, "stsc");
+  need(stsc, 0, 8, "stsc");
   uint32_t nent = rd32(stsc.p + 4);
+  need(stsc, 8, size_t(nent) * 12, "stsc");
+  if (nent == 0) throw std::runtime_error("mp4 demux: empty stsc");
   std::vector<uint32_t> first_chunk(nent), per_chunk(nent);
   for (uint32_t i = 0; i < nent; ++i) {
     first_chunk[i] = rd32(stsc.p + 8 + 12 * i);
@@ -496,17 +652,18 @@ std::vector<uint8_t> demux_mp4_to_annexb(const uint8_t* p, size_t n) {
   BoxRef stss{};
   bool have_stss = find_box(st.p, st.n, "stss", &stss);
   if (have_stss) {
+    need(stss, 0, 8, "stss");
     uint32_t ns = rd32(stss.p + 4);
+    need(stss, 8, size_t(ns) * 4, "stss");
     for (uint32_t i = 0; i < ns; ++i) syncs.push_back(rd32(stss.p + 8 + 4 * i));
   }
   std::vector<uint8_t> out;
   uint32_t sample = 0;
-  size_t si = 0;
+  size_t si = 0, ei = 0;
+  uint32_t spc = per_chunk[0];
   for (size_t ch = 0; ch < chunks.size() && sample < count; ++ch) {
     uint32_t chunk_no = static_cast<uint32_t>(ch + 1);
-    uint32_t spc = per_chunk[0];
-    for (uint32_t e = 0; e < nent; ++e)
-      if (first_chunk[e] <= chunk_no) spc = per_chunk[e];
+    while (ei < nent && first_chunk[ei] <= chunk_no) spc = per_chunk[ei++];
     uint64_t pos = chunks[ch];
     for (uint32_t k = 0; k < spc && sample < count; ++k, ++sample) {
       bool is_sync = !have_stss;
@@ -514,7 +671,7 @@ std::vector<uint8_t> demux_mp4_to_annexb(const uint8_t* p, size_t n) {
       if (si < syncs.size() && syncs[si] == sample + 1) is_sync = true;
       if (is_sync) out.insert(out.end(), ps.begin(), ps.end());
       uint64_t end = pos + sizes[sample];
-      if (end > n) throw std::runtime_error("mp4 demux: sample outside file");
+      if (pos > n || end > n) throw std::runtime_error("mp4 demux: sample outside file");
       uint64_t q = pos;
       while (q + len_size <= end) {
         uint32_t l = 0;

@@ -42,4 +42,21 @@ std::vector<uint8_t> concat_annexb(const std::vector<std::pair<const uint8_t*, s
 std::vector<uint8_t> mux_mp4(const uint8_t* p, size_t n, double fps);
 std::vector<uint8_t> demux_mp4_to_annexb(const uint8_t* p, size_t n);
 
+// MP4 sample view of an H.264 Annex-B stream (for the ISO-BMFF writer in
+// govideocompressor_amd/segment/mp4.py): one sample per access unit in decoding order,
+// NALs as 4-byte-length AVCC units without SPS/PPS/AUD, sync = IDR, and the display index
+// of every sample from its picture order count (8.2.1, POC types 0/1/2; an IDR or a
+// memory_management_control_operation 5 starts a new display epoch), which the writer
+// turns into composition offsets (ctts) for B pictures.
+struct H264Samples {
+  std::vector<uint8_t> data;
+  std::vector<uint32_t> sizes;
+  std::vector<uint8_t> sync;
+  std::vector<int32_t> display;
+  std::vector<uint8_t> sps, pps;  // first SPS / PPS NAL (header byte + escaped payload)
+  int width = 0, height = 0;
+  double fps = 0.0;
+};
+H264Samples h264_samples(const uint8_t* p, size_t n);
+
 }  // namespace mivc

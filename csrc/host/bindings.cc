@@ -613,6 +613,25 @@ PYBIND11_MODULE(_host, m) {
     std::string s = data;
     return to_bytes(mux_mp4(reinterpret_cast<const uint8_t*>(s.data()), s.size(), fps));
   });
+  m.def("h264_samples", [](py::bytes data) {
+    std::string s = data;
+    H264Samples hs;
+    {
+      py::gil_scoped_release rel;
+      hs = h264_samples(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+    }
+    py::dict d;
+    d["data"] = to_bytes(hs.data);
+    d["sizes"] = hs.sizes;
+    d["sync"] = std::vector<int>(hs.sync.begin(), hs.sync.end());
+    d["display"] = hs.display;
+    d["sps"] = to_bytes(hs.sps);
+    d["pps"] = to_bytes(hs.pps);
+    d["width"] = hs.width;
+    d["height"] = hs.height;
+    d["fps"] = hs.fps;
+    return d;
+  });
   m.def("mp4_demux", [](py::bytes data) {
     std::string s = data;
     return to_bytes(demux_mp4_to_annexb(reinterpret_cast<const uint8_t*>(s.data()), s.size()));
@@ -620,6 +639,10 @@ PYBIND11_MODULE(_host, m) {
   m.def(
       "lowres_costs",
       [](py::array_t<uint8_t, py::array::c_style> frames, int width, int height, int nframes) {
+        if (width < 2 || height < 2 || nframes < 0 || width % 2 || height % 2)
+          throw std::invalid_argument("lowres_costs: bad geometry");
+        if (static_cast<size_t>(frames.size()) < static_cast<size_t>(nframes) * width * height * 3 / 2)
+          throw std::invalid_argument("lowres_costs: frame buffer smaller than nframes I420 frames");
         std::vector<float> intra(nframes), inter(nframes);
         {
           py::gil_scoped_release rel;

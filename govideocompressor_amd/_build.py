@@ -70,22 +70,40 @@ def hip_library_path() -> str:
     return os.path.join(PKG_DIR, "_hip" + EXT_SUFFIX)
 
 
-def build_host(nproc: int = 8) -> str:
+def sanitized_host_path() -> str:
+    """ASan + UBSan build of ``_host`` (outside the package: loaded only through
+    ``MIVC_HOST_LIB``, see ops/native.py)."""
+    return os.path.join(BUILD, "asan", "_host" + EXT_SUFFIX)
+
+
+def build_host(nproc: int = 8, sanitize: bool = False) -> str:
+    """``sanitize``: -fsanitize=address,undefined -O1 build for the parser hardening runs
+    (tools/asan_tests.sh: LD_PRELOAD=libasan, MIVC_HOST_LIB=<this>, the CPU test suite
+    and the fuzz tests)."""
     srcs = sorted(glob.glob(os.path.join(CSRC, "host", "*.cc")))
     hdrs = _headers("common", "host")
-    os.makedirs(os.path.join(BUILD, "host"), exist_ok=True)
-    flags = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wno-unused-function"]
+    sub = "asan" if sanitize else "host"
+    os.makedirs(os.path.join(BUILD, sub), exist_ok=True)
+    if sanitize:
+        # shift-base: the transform/quant arithmetic left-shifts negative values, which is
+        # two's-complement-defined since C++20 (and what g++/hipcc emit in C++17 mode)
+        flags = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize=shift-base",
+                 "-fno-sanitize-recover=undefined"]
+    else:
+        flags = ["-O3"]
+    flags += ["-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wno-unused-function"]
     flags += [f"-I{p}" for p in _pybind_includes()]
     jobs = []
     objs = []
     for s in srcs:
-        o = os.path.join(BUILD, "host", os.path.basename(s) + ".o")
+        o = os.path.join(BUILD, sub, os.path.basename(s) + ".o")
         objs.append(o)
         jobs.append((["g++", *flags, "-c", s, "-o", o], o, [s, *hdrs]))
     _compile_many(jobs, nproc)
-    out = host_library_path()
+    out = sanitized_host_path() if sanitize else host_library_path()
     if _stale(out, objs):
-        _run(["g++", "-shared", "-o", out, *objs, "-lpthread"])
+        link = ["-fsanitize=address,undefined"] if sanitize else []
+        _run(["g++", "-shared", *link, "-o", out, *objs, "-lpthread"])
     return out
 
 
@@ -129,13 +147,15 @@ def build_all(nproc: int = 8) -> list[str]:
 
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", nargs="?", default="all", choices=["host", "hip", "all"])
+    ap.add_argument("what", nargs="?", default="all", choices=["host", "hip", "all", "asan"])
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 4))
     a = ap.parse_args()
     if a.what in ("host", "all"):
         print(build_host(a.j))
     if a.what in ("hip", "all"):
         print(build_hip(a.j))
+    if a.what == "asan":
+        print(build_host(a.j, sanitize=True))
 
 
 if __name__ == "__main__":

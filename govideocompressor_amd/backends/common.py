@@ -66,19 +66,21 @@ def output_size(cfg: EncoderConfig, clip: yuv.Clip) -> tuple[int, int]:
     return clip.width, clip.height
 
 
-def write_output(job: PieceJob, stream: bytes, fps: float, codec: str | None = None) -> int:
-    """Write an Annex-B stream as ``.mp4`` (``avc1`` native muxer, ``hvc1`` for HEVC) or raw by
-    extension.  ``codec`` ("h264" / "hevc", from the job's EncoderConfig) picks the sample
-    entry; without it the stream's first NAL header decides."""
-    from ..ops import native
-    from ..segment import mp4_hevc
-    hevc = mp4_hevc.is_hevc_annexb(stream) if codec is None else codec == "hevc"
+def write_output(job: PieceJob, stream: bytes, fps: float, codec: str | None = None, audio: str = "copy") -> int:
+    """Write an Annex-B stream as ``.mp4`` (``avc1`` with ctts for B pictures, ``hvc1`` for
+    HEVC) or raw by extension.  ``codec`` ("h264" / "hevc", from the job's EncoderConfig)
+    picks the sample entry; without it the stream's first NAL header decides.  With
+    ``audio="copy"`` the input piece's audio tracks are stream-copied into the output
+    (the reference's pieces keep their audio: server.go:199-200)."""
+    from ..segment import mp4
     if not job.out_path.lower().endswith(".mp4"):
         data = stream
-    elif hevc:
-        data = mp4_hevc.mux(stream, fps)
     else:
-        data = native.host().mp4_mux(stream, fps)
+        extra = []
+        if audio == "copy" and job.in_path.lower().endswith((".mp4", ".m4v", ".mov")):
+            with open(job.in_path, "rb") as f:
+                extra = mp4.file_audio(f.read())
+        data = mp4.mux_video(stream, fps, codec, extra)
     tmp = job.out_path + ".part"
     with open(tmp, "wb") as f:
         f.write(data)

@@ -102,7 +102,7 @@ class CpuBackend:
         except Exception as e:  # noqa: BLE001
             return PieceResult(j.idx, False, f"load: {e}")
         stream, st = self.encode_clip(j.idx, clip, cfg)
-        st["bytes"] = write_output(j, stream, st["fps"], cfg.codec)
+        st["bytes"] = write_output(j, stream, st["fps"], cfg.codec, cfg.audio)
         write_log(j, st)
         return PieceResult(j.idx, True, stats=st)
 

@@ -285,7 +285,7 @@ class GpuBackend:
             for j in jobs:
                 if j.idx in enc:
                     stream, st = enc[j.idx]
-                    st["bytes"] = write_output(j, stream, st["fps"], cfg.codec)
+                    st["bytes"] = write_output(j, stream, st["fps"], cfg.codec, cfg.audio)
                     st["timings"] = dict(tm.t)
                     write_log(j, st)
                     results[j.idx] = PieceResult(j.idx, True, stats=st)

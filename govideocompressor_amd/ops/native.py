@@ -11,7 +11,10 @@ fallback for the GPU encode path.
 from __future__ import annotations
 
 import importlib
+import importlib.machinery
+import importlib.util
 import os
+import sys
 import threading
 
 _lock = threading.Lock()
@@ -22,6 +25,16 @@ def _load(name: str, builder):
     with _lock:
         if name in _cache:
             return _cache[name]
+        override = os.environ.get("MIVC_HOST_LIB") if name == "_host" else None
+        if override:  # e.g. the ASan/UBSan build (_build.build_host(sanitize=True))
+            full = f"govideocompressor_amd.{name}"
+            loader = importlib.machinery.ExtensionFileLoader(full, override)
+            spec = importlib.util.spec_from_file_location(full, override, loader=loader)
+            mod = importlib.util.module_from_spec(spec)
+            loader.exec_module(mod)
+            sys.modules[full] = mod
+            _cache[name] = mod
+            return mod
         try:
             mod = importlib.import_module(f"govideocompressor_amd.{name}")
         except ImportError:

@@ -167,7 +167,15 @@ def encode_file(path: str, output: str, args: str = "264", backend: str = "auto"
         hst = native.host()
         stream = hst.concat([by_idx[i] for i in range(n)])
         out_fps = cfg.fps or info.fps
-        data = hst.mp4_mux(stream, out_fps) if output.lower().endswith(".mp4") else stream
+        if output.lower().endswith(".mp4"):
+            from .segment import mp4
+            extra = []
+            if info.kind == "mp4" and cfg.audio == "copy":  # the input's audio, stream-copied
+                with open(path, "rb") as f:
+                    extra = mp4.file_audio(f.read())
+            data = mp4.mux_video(stream, out_fps, cfg.codec, extra)
+        else:
+            data = stream
         with open(output + ".part", "wb") as f:
             f.write(data)
         os.replace(output + ".part", output)

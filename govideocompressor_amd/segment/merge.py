@@ -17,7 +17,7 @@ import re
 import sys
 
 from ..ops import native
-from . import mp4_hevc
+from . import mp4, mp4_hevc
 
 _LINE = re.compile(r"^\s*file\s+'([^']+)'\s*$")
 
@@ -63,11 +63,19 @@ def read_filelist(path: str) -> list[str]:
 def load_annexb(path: str) -> bytes:
     with open(path, "rb") as f:
         data = f.read()
-    if data[4:8] == b"ftyp" or path.lower().endswith((".mp4", ".m4v", ".mov")):
-        if mp4_hevc.is_hevc_mp4(data):
-            return mp4_hevc.demux(data)
-        return native.host().mp4_demux(data)
+    if mp4.is_mp4(data) or path.lower().endswith((".mp4", ".m4v", ".mov")):
+        return mp4.annexb_from_mp4(data)
     return data
+
+
+def load_audio(path: str) -> list:
+    """The audio tracks of an MP4 piece (none for Annex-B pieces)."""
+    with open(path, "rb") as f:
+        head = f.read(8)
+    if not (mp4.is_mp4(head) or path.lower().endswith((".mp4", ".m4v", ".mov"))):
+        return []
+    with open(path, "rb") as f:
+        return mp4.file_audio(f.read())
 
 
 def piece_fps(path: str) -> float | None:
@@ -91,15 +99,21 @@ def merge_files(files: list[str], out_path: str, fps: float | None = None) -> in
     if len(codecs) > 1:
         raise ValueError(f"pieces mix codecs {sorted(codecs)}: re-encode them with one -vcodec")
     stream = h.concat(parts)
-    if out_path.lower().endswith((".mp4", ".m4v", ".mov")) and mp4_hevc.is_hevc_annexb(stream):
+    if out_path.lower().endswith((".mp4", ".m4v", ".mov")):
+        hevc = mp4_hevc.is_hevc_annexb(stream)
         if fps is None and files:
             # the HEVC SPS carries no timing: take the pieces' own MP4 rate
             fps = piece_fps(files[0])
-        data = mp4_hevc.mux(stream, fps or 30.0)
-    elif out_path.lower().endswith((".mp4", ".m4v", ".mov")):
-        if fps is None:
-            fps = h.stream_info(stream)["fps"] or 30.0
-        data = h.mp4_mux(stream, fps)
+        if fps is None and not hevc:
+            fps = h.stream_info(stream)["fps"] or None
+        # audio: every piece's track(s) appended in piece order (concat.sh -c copy keeps
+        # them, server.go:357); pieces without audio contribute nothing
+        audio = [load_audio(f) for f in files]
+        extra = []
+        if any(audio):
+            n = max(len(a) for a in audio)
+            extra = [mp4.concat([a[k] for a in audio if len(a) > k]) for k in range(n)]
+        data = mp4.mux_video(stream, fps or 30.0, "hevc" if hevc else "h264", extra)
     else:
         data = stream
     tmp = out_path + ".part"

@@ -130,8 +130,9 @@ def hvcc_record(vps: list[bytes], sps: list[bytes], pps: list[bytes]) -> bytes:
     return rec
 
 
-def mux(stream: bytes, fps: float = 30.0) -> bytes:
-    """Annex-B HEVC -> MP4 bytes (one ``hvc1`` track, one chunk, ``mdat`` after ``moov``)."""
+def hevc_track(stream: bytes, fps: float | None = 30.0):
+    """Annex-B HEVC -> one ``hvc1`` :class:`~.mp4.Track` (parameter sets in ``hvcC``)."""
+    from . import mp4
     vps, sps, pps = [], [], []
     samples: list[bytearray] = []
     sync: list[int] = []
@@ -167,53 +168,16 @@ def mux(stream: bytes, fps: float = 30.0) -> bytes:
     w, h = info["width"], info["height"]
     fps = fps if fps and fps > 0 else 30.0
     timescale, delta = int(round(fps * 1000)), 1000
-    n = len(samples)
-    media_dur, movie_dur = n * delta, int(round(n * 1000.0 / fps))
-    v1 = media_dur > 0xFFFFFFFF or movie_dur > 0xFFFFFFFF  # 64-bit durations (version 1 boxes)
-    mdat_body = b"".join(bytes(s) for s in samples)
+    entry = mp4._visual_entry(b"hvc1", w, h, _box(b"hvcC", hvcc_record(vps, sps, pps)))
+    marks = set(sync)
+    return mp4.Track(b"vide", timescale, entry, [bytes(x) for x in samples], [delta] * len(samples), None,
+                     [(i + 1) in marks for i in range(len(samples))], w, h)
 
-    ftyp = _box(b"ftyp", b"isom", struct.pack(">I", 512), b"isomiso2hvc1mp41")
-    entry = _box(b"hvc1", bytes(6), struct.pack(">H", 1), bytes(16), struct.pack(">HHII", w, h, 0x480000, 0x480000),
-                 struct.pack(">IH", 0, 1), bytes(32), struct.pack(">Hh", 0x18, -1),
-                 _box(b"hvcC", hvcc_record(vps, sps, pps)))
 
-    def moov(offset: int) -> bytes:
-        wide = offset + len(mdat_body) + 16 > 0xFFFFFFFF
-        stco = (_full(b"co64", 0, 0, struct.pack(">IQ", 1, offset)) if wide
-                else _full(b"stco", 0, 0, struct.pack(">II", 1, offset)))
-        stbl = _box(b"stbl",
-                    _full(b"stsd", 0, 0, struct.pack(">I", 1), entry),
-                    _full(b"stts", 0, 0, struct.pack(">III", 1, n, delta)),
-                    _full(b"stss", 0, 0, struct.pack(">I", len(sync)), *(struct.pack(">I", s) for s in sync)),
-                    _full(b"stsc", 0, 0, struct.pack(">IIII", 1, 1, n, 1)),
-                    _full(b"stsz", 0, 0, struct.pack(">II", 0, n), *(struct.pack(">I", len(s)) for s in samples)),
-                    stco)
-        minf = _box(b"minf", _full(b"vmhd", 0, 1, bytes(8)),
-                    _box(b"dinf", _full(b"dref", 0, 0, struct.pack(">I", 1), _full(b"url ", 0, 1))), stbl)
-        if v1:
-            mdhd = _full(b"mdhd", 1, 0, struct.pack(">QQIQHH", 0, 0, timescale, media_dur, 0x55C4, 0))
-            tkhd = _full(b"tkhd", 1, 3, struct.pack(">QQIIQ", 0, 0, 1, 0, movie_dur), bytes(8),
-                         struct.pack(">hhhH", 0, 0, 0, 0), _MATRIX, struct.pack(">II", w << 16, h << 16))
-            mvhd = _full(b"mvhd", 1, 0, struct.pack(">QQIQ", 0, 0, 1000, movie_dur), struct.pack(">IH", 0x10000, 0x100),
-                         bytes(10), _MATRIX, bytes(24), struct.pack(">I", 2))
-        else:
-            mdhd = _full(b"mdhd", 0, 0, struct.pack(">IIIIHH", 0, 0, timescale, media_dur, 0x55C4, 0))
-            tkhd = _full(b"tkhd", 0, 3, struct.pack(">IIIII", 0, 0, 1, 0, movie_dur), bytes(8),
-                         struct.pack(">hhhH", 0, 0, 0, 0), _MATRIX, struct.pack(">II", w << 16, h << 16))
-            mvhd = _full(b"mvhd", 0, 0, struct.pack(">IIII", 0, 0, 1000, movie_dur), struct.pack(">IH", 0x10000, 0x100),
-                         bytes(10), _MATRIX, bytes(24), struct.pack(">I", 2))
-        mdia = _box(b"mdia", mdhd,
-                    _full(b"hdlr", 0, 0, struct.pack(">I", 0), b"vide", bytes(12), b"VideoHandler\x00"), minf)
-        return _box(b"moov", mvhd, _box(b"trak", tkhd, mdia))
-
-    size = len(moov(0))
-    wide = len(ftyp) + size + 16 + len(mdat_body) > 0xFFFFFFFF
-    hdr = struct.pack(">I", 1) + b"mdat" + struct.pack(">Q", 16 + len(mdat_body)) if wide else \
-        struct.pack(">I", 8 + len(mdat_body)) + b"mdat"
-    m = moov(len(ftyp) + size + len(hdr))
-    if len(m) != size:  # stco -> co64 switch changed the size; recompute once
-        m = moov(len(ftyp) + len(m) + len(hdr))
-    return ftyp + m + hdr + mdat_body
+def mux(stream: bytes, fps: float = 30.0) -> bytes:
+    """Annex-B HEVC -> MP4 bytes (one ``hvc1`` track; P-only GOPs need no ``ctts``)."""
+    from . import mp4
+    return mp4.write([hevc_track(stream, fps)])
 
 
 def _children(b: bytes, start: int, end: int):
@@ -237,76 +201,26 @@ def _find(b: bytes, start: int, end: int, path: list[bytes]):
 
 
 def is_hevc_mp4(data: bytes) -> bool:
+    from . import mp4
     try:
-        s, e = _find(data, 0, len(data), [b"moov", b"trak", b"mdia", b"minf", b"stbl", b"stsd"])
-    except ValueError:
+        return mp4.video_track(mp4.read(data)).codec in (b"hvc1", b"hev1")
+    except (ValueError, struct.error, IndexError):
         return False
-    return data[s + 12:s + 16] in (b"hvc1", b"hev1")
 
 
 def track_fps(data: bytes) -> float | None:
-    """Frame rate of an MP4's (first) track: mdhd timescale / the first stts delta."""
+    """Frame rate of an MP4's video track: timescale / its (median) sample duration."""
+    from . import mp4
     try:
-        ms, me = _find(data, 0, len(data), [b"moov", b"trak", b"mdia", b"mdhd"])
-        ver = data[ms]
-        timescale = struct.unpack(">I", data[ms + (20 if ver == 1 else 12):ms + (24 if ver == 1 else 16)])[0]
-        ts, te = _find(data, 0, len(data), [b"moov", b"trak", b"mdia", b"minf", b"stbl", b"stts"])
-        n = struct.unpack(">I", data[ts + 4:ts + 8])[0]
-        if n < 1 or timescale <= 0:
-            return None
-        delta = struct.unpack(">I", data[ts + 12:ts + 16])[0]
-        return timescale / delta if delta > 0 else None
+        return mp4.track_fps(mp4.video_track(mp4.read(data))) or None
     except (ValueError, struct.error, IndexError):
         return None
 
 
 def demux(data: bytes) -> bytes:
     """``hvc1`` MP4 -> Annex-B (parameter sets from ``hvcC`` first, then every sample)."""
-    s, e = _find(data, 0, len(data), [b"moov", b"trak", b"mdia", b"minf", b"stbl"])
-    stbl = {k: (a, b_) for k, a, b_ in _children(data, s, e)}
-    ss, _ = stbl[b"stsd"]
-    ent = ss + 8
-    _, esz_kind = struct.unpack(">I4s", data[ent:ent + 8])
-    if esz_kind not in (b"hvc1", b"hev1"):
+    from . import mp4
+    t = mp4.video_track(mp4.read(data))
+    if t.codec not in (b"hvc1", b"hev1"):
         raise ValueError("mp4: not an HEVC track")
-    esz = struct.unpack(">I", data[ent:ent + 4])[0]
-    hs, he = _find(data, ent + 8 + 78, ent + esz, [b"hvcC"])
-    rec = data[hs:he]
-    nls = (rec[21] & 3) + 1
-    out = bytearray()
-    p = 23
-    for _ in range(rec[22]):
-        cnt = struct.unpack(">H", rec[p + 1:p + 3])[0]
-        p += 3
-        for _ in range(cnt):
-            ln = struct.unpack(">H", rec[p:p + 2])[0]
-            out += b"\x00\x00\x00\x01" + rec[p + 2:p + 2 + ln]
-            p += 2 + ln
-    zs, _ = stbl[b"stsz"]
-    fixed, n = struct.unpack(">II", data[zs + 4:zs + 12])
-    sizes = [fixed] * n if fixed else list(struct.unpack(f">{n}I", data[zs + 12:zs + 12 + 4 * n]))
-    if b"co64" in stbl:
-        cs, _ = stbl[b"co64"]
-        nc = struct.unpack(">I", data[cs + 4:cs + 8])[0]
-        offs = list(struct.unpack(f">{nc}Q", data[cs + 8:cs + 8 + 8 * nc]))
-    else:
-        cs, _ = stbl[b"stco"]
-        nc = struct.unpack(">I", data[cs + 4:cs + 8])[0]
-        offs = list(struct.unpack(f">{nc}I", data[cs + 8:cs + 8 + 4 * nc]))
-    sc, _ = stbl[b"stsc"]
-    ne = struct.unpack(">I", data[sc + 4:sc + 8])[0]
-    runs = [struct.unpack(">III", data[sc + 8 + 12 * i:sc + 20 + 12 * i]) for i in range(ne)]
-    k = 0
-    for ci, off in enumerate(offs):
-        per = [r[1] for r in runs if r[0] <= ci + 1][-1]
-        for _ in range(per):
-            if k >= n:
-                break
-            q, end = off, off + sizes[k]
-            while q < end:
-                ln = int.from_bytes(data[q:q + nls], "big")
-                out += b"\x00\x00\x00\x01" + data[q + nls:q + nls + ln]
-                q += nls + ln
-            off = end
-            k += 1
-    return bytes(out)
+    return mp4.video_to_annexb(t)

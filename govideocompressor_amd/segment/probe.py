@@ -77,10 +77,11 @@ def annexb_of(path: str, kind: str | None = None) -> bytes:
     with open(path, "rb") as f:
         data = f.read()
     if kind == "mp4":
-        from . import mp4_hevc
-        if mp4_hevc.is_hevc_mp4(data):
-            return mp4_hevc.demux(data)
-        return native.host().mp4_demux(data)
+        from . import mp4
+        try:
+            return mp4.annexb_from_mp4(data)  # the video trak, wherever it sits among the tracks
+        except ValueError as e:
+            raise ProbeError(f"{path}: {e}") from None
     if kind == "h264":
         return data
     raise ProbeError(f"{path} is not a compressed stream")

@@ -84,17 +84,30 @@ def split(path: str, size_mb: int = 10, seconds: float | None = None, frames: in
     ranges = []
     if compressed:
         from ..ops import native
+        from . import mp4
         h = native.host()
         pieces = h.split_pieces(annexb_of(path, info.kind), seg_frames)
+        audio, pts = [], []
+        if info.kind == "mp4":
+            # -acodec copy -map 0:0 -map 0:1 (server.go:199-200): each piece carries the audio
+            # samples of its own time span, cut at the video piece boundaries
+            with open(path, "rb") as f:
+                tracks = mp4.read(f.read())
+            audio = mp4.audio_tracks(tracks)
+            pts = mp4.video_track(tracks).pts_seconds()
+        frames = [h.stream_info(pc)["frames"] for pc in pieces]
+        starts = [sum(frames[:i]) for i in range(len(pieces))]
         for i, pc in enumerate(pieces):
             if info.kind == "mp4":
-                name, data = f"{i}.mp4", h.mp4_mux(pc, info.fps)
+                t0 = pts[starts[i]] if starts[i] < len(pts) else None
+                t1 = pts[starts[i + 1]] if i + 1 < len(pieces) and starts[i + 1] < len(pts) else None
+                extra = [mp4.cut(a, 0.0 if i == 0 else t0, t1) for a in audio] if t0 is not None else []
+                name, data = f"{i}.mp4", mp4.mux_video(pc, info.fps, "h264", [a for a in extra if a.samples])
             else:
                 name, data = f"{i}.264", pc
             with open(os.path.join(d, name), "wb") as f:
                 f.write(data)
-            si = h.stream_info(pc)
-            ranges.append({"idx": str(i), "file": name, "frames": si["frames"]})
+            ranges.append({"idx": str(i), "file": name, "frames": frames[i]})
     else:
         pl = P.fixed_plan(info.frames, seg_frames)
         for i, (s, c, _) in enumerate(pl.tolist()):

@@ -139,7 +139,7 @@ def test_i4x4_tap_table(host):
 
 def test_lowres_costs(host):
     c = yuv.synth_clip_cpu(4, 64, 48, seed=3)
-    frames = np.ascontiguousarray(c.y).reshape(-1)
+    frames = np.ascontiguousarray(c.i420())  # I420 frames back to back (luma read, chroma skipped)
     intra, inter = host.lowres_costs(frames, 64, 48, 4)
     assert len(intra) == 4 and all(x > 0 for x in intra)
     assert inter[1] <= intra[1] * 1.5
