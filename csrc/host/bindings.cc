@@ -148,9 +148,12 @@ py::dict segment_to_dict(ParsedSegment& seg) {
   d["crop_y"] = p0.crop_y;
   std::vector<std::vector<uint8_t>*> hdr;
   std::vector<std::vector<uint32_t>*> mask, off;
-  std::vector<std::vector<int16_t>*> coef;
+  std::vector<std::vector<int16_t>*> coef, mvs, wps;
+  std::vector<std::vector<int8_t>*> refs;
+  std::vector<std::vector<uint8_t>*> bss;
+  std::vector<std::vector<int32_t>*> lists;
   py::array_t<int64_t> pic_off(P + 1);
-  py::array_t<int32_t> meta({P, static_cast<py::ssize_t>(11)});
+  py::array_t<int32_t> meta({P, static_cast<py::ssize_t>(12)});
   int64_t* po = pic_off.mutable_data();
   int32_t* mt = meta.mutable_data();
   po[0] = 0;
@@ -159,12 +162,22 @@ py::dict segment_to_dict(ParsedSegment& seg) {
     DecodedPicture& p = seg.pics[i];
     same_geom = same_geom && p.coded_width == p0.coded_width && p.coded_height == p0.coded_height &&
                 static_cast<py::ssize_t>(p.blk_mask.size()) == nmb;
+    same_geom = same_geom && p.mv_l[0].size() == static_cast<size_t>(nmb) * 32 &&
+                p.mv_l[1].size() == static_cast<size_t>(nmb) * 32 && p.bs.size() == static_cast<size_t>(nmb) * 32 &&
+                p.wp.size() == static_cast<size_t>(kWpEntries) && p.list_ids.size() == 64;
     hdr.push_back(&p.hdr);
+    mvs.push_back(&p.mv_l[0]);
+    mvs.push_back(&p.mv_l[1]);
+    refs.push_back(&p.ref_l[0]);
+    refs.push_back(&p.ref_l[1]);
+    bss.push_back(&p.bs);
+    lists.push_back(&p.list_ids);
+    wps.push_back(&p.wp);
     mask.push_back(&p.blk_mask);
     off.push_back(&p.blk_off);
     coef.push_back(&p.coef);
     po[i + 1] = po[i] + static_cast<int64_t>(p.coef.size() / 16);
-    int32_t* m = mt + i * 11;
+    int32_t* m = mt + i * 12;
     m[0] = p.pic_id;
     m[1] = p.ref_id;
     m[2] = p.nal_ref;
@@ -176,6 +189,7 @@ py::dict segment_to_dict(ParsedSegment& seg) {
     m[8] = p.chroma_qp_offset;
     m[9] = p.deblock;
     m[10] = p.gpu_ok ? 1 : 0;
+    m[11] = p.poc;
   }
   if (!same_geom) {
     d["error"] = std::string("resolution changes inside the segment");
@@ -187,6 +201,11 @@ py::dict segment_to_dict(ParsedSegment& seg) {
   d["coef"] = vec_array<int16_t>(coef, {static_cast<py::ssize_t>(po[P] * 16)});
   d["pic_off"] = pic_off;
   d["meta"] = meta;
+  d["mv"] = vec_array<int16_t>(mvs, {P, 2, nmb, 16, 2});
+  d["ref"] = vec_array<int8_t>(refs, {P, 2, nmb, 16});
+  d["bs"] = vec_array<uint8_t>(bss, {P, nmb, 32});
+  d["lists"] = vec_array<int32_t>(lists, {P, 2, 32});
+  d["wp"] = vec_array<int16_t>(wps, {P, static_cast<py::ssize_t>(kWpEntries)});
   return d;
 }
 

@@ -67,6 +67,8 @@ struct Pic {
   bool gpu_ok = true;
   int nslices = 0;
   int slice_qp = 0;
+  std::vector<int32_t> list_ids;  // parse-only: reference lists of the (single) slice
+  std::vector<int16_t> wp;
   void init(int w, int h, bool planes) {
     wmb = w;
     hmb = h;
@@ -443,9 +445,17 @@ struct Decoder::Impl {
       d.beta_off = slices.empty() ? 0 : slices[0].beta_off;
       d.chroma_qp_offset = slices.empty() ? 0 : slices[0].cb_off;
       d.deblock = slices.empty() ? 1 : (slices[0].disable_idc != 1);
-      bool ok = cur->gpu_ok && cur->nslices == 1;
+      bool ok = cur->gpu_ok && cur->nslices == 1 && !cur->mmco5;
       for (const SliceParams& sp2 : slices) ok = ok && sp2.cb_off == sp2.cr_off && sp2.disable_idc != 2;
       d.gpu_ok = ok;
+      d.poc = cur->poc;
+      for (int l = 0; l < 2; ++l) {
+        d.mv_l[l] = cur->mv[l];
+        d.ref_l[l] = cur->ref[l];
+      }
+      d.list_ids = cur->list_ids.empty() ? std::vector<int32_t>(64, -1) : cur->list_ids;
+      d.wp = cur->wp.empty() ? std::vector<int16_t>(kWpEntries, 0) : cur->wp;
+      d.bs = boundary_strengths();
       out.push_back(std::move(d));
     }
     if (cur->nal_ref) mark_reference();
@@ -724,16 +734,12 @@ struct Decoder::Impl {
     slices.push_back(spar);
     slice_idx = static_cast<int>(slices.size()) - 1;
     cur->nslices = static_cast<int>(slices.size());
-    if (h.num_ref_idx_l0_active > 1 || p->constrained_intra_pred || h.slice_type == SLICE_B || p->transform_8x8_mode ||
-        h.has_weights)
-      cur->gpu_ok = false;
+    if (p->constrained_intra_pred) cur->gpu_ok = false;
     if (h.slice_type == SLICE_B) cur->slice_type = SLICE_B;
     else if (h.slice_type == SLICE_P && cur->slice_type == SLICE_I) cur->slice_type = SLICE_P;
     build_ref_lists();
-    if (!list[0].empty()) {
-      if (pic_ref_id >= 0 && pic_ref_id != list[0][0]->id) cur->gpu_ok = false;
-      pic_ref_id = list[0][0]->id;
-    }
+    if (!list[0].empty()) pic_ref_id = list[0][0]->id;
+    if (parse_only) record_lists_and_weights();
     cabac = p->entropy_coding_mode != 0;
     int nmb = cur->wmb * cur->hmb;
     int addr = h.first_mb;
@@ -983,7 +989,6 @@ struct Decoder::Impl {
       direct_pred(addr, 0xF);
       mark_done(0, 0, 4, 4);
       if (parse_only) {
-        cur->gpu_ok = false;
         cur->rec_off[addr] = static_cast<uint32_t>(cur->rec_coef.size() / 16);
         store_record(addr, MBK_BDIRECT, 0, qp, 0, 0, nullptr, 0);
         return;
@@ -1023,12 +1028,7 @@ struct Decoder::Impl {
         int r0 = (q & 1) * 2 + (q >> 1) * 8;  // top-left 4x4 block of quadrant q
         h.mv[l][q][0] = cur->mv[l][addr * 32 + 2 * r0];
         h.mv[l][q][1] = cur->mv[l][addr * 32 + 2 * r0 + 1];
-        h.ref[l][q] = cur->ref[l][addr * 16 + r0];
-        for (int k = 0; k < 4; ++k) {  // the quadrant must carry one vector (no sub-8x8 split)
-          int r = r0 + (k & 1) + (k >> 1) * 4;
-          if (cur->mv[l][addr * 32 + 2 * r] != h.mv[l][q][0] || cur->mv[l][addr * 32 + 2 * r + 1] != h.mv[l][q][1])
-            cur->gpu_ok = false;
-        }
+        h.ref[l][q] = cur->ref[l][addr * 16 + r0];  // sub-8x8 motion: DecodedPicture::mv_l
       }
     for (int b = 0; b < 16; ++b) h.i4_modes[b] = static_cast<uint8_t>(i4modes ? i4modes[b] : 2);
     std::memcpy(cur->rec_hdr.data() + static_cast<size_t>(addr) * sizeof(MbHeader), &h, sizeof(MbHeader));
@@ -2278,8 +2278,7 @@ struct Decoder::Impl {
     if (s.t8x8) {
       // 8x8 levels as 16-level chunks: chunk blk = b8 * 4 + k holds levels 16k..16k+15 of
       // 8x8 block b8, i.e. the record layout (COEF_LUMA + b8 * 64).  The GPU path reads
-      // 4x4 blocks only, so such pictures go to the CPU.
-      cur->gpu_ok = false;
+      // 8x8 transform (decode.hip inverse8x8).
       for (int blk = 0; blk < 16; ++blk) put(blk, s.lum8[blk >> 2] + 16 * (blk & 3), 16, nullptr);
     } else {
       for (int blk = 0; blk < 16; ++blk) put(blk, s.lum[blk], 16, nullptr);
@@ -2289,9 +2288,7 @@ struct Decoder::Impl {
     for (int cc = 0; cc < 2; ++cc)
       for (int b = 0; b < 4; ++b) put(18 + cc * 4 + b, s.cac[cc][b], 16, nullptr);
     cur->rec_mask[addr] = mask;
-    if (kind != MBK_I4x4 && kind != MBK_I16x16 && kind != MBK_P16x16 && kind != MBK_P16x8 && kind != MBK_P8x16 &&
-        kind != MBK_P8x8)
-      cur->gpu_ok = false;
+    if (kind == MBK_IPCM) cur->gpu_ok = false;  // I_PCM samples are not carried by the records
     store_record(addr, kind, s.cbp, qp, s.i16_mode, s.chroma_mode, (kind == MBK_I4x4 || kind == MBK_I8x8) ? s.i4 : nullptr,
                  s.t8x8);
   }
@@ -2429,6 +2426,67 @@ struct Decoder::Impl {
           }
       }
     }
+  }
+
+  // parse-only: the slice's reference lists (picture ids) and weighted-prediction table
+  void record_lists_and_weights() {
+    cur->list_ids.assign(64, -1);
+    for (int l = 0; l < 2; ++l)
+      for (size_t i = 0; i < list[l].size() && i < 32; ++i) cur->list_ids[l * 32 + i] = list[l][i]->id;
+    cur->wp.assign(kWpEntries, 0);
+    int16_t* w = cur->wp.data();
+    if (sh.has_weights) {
+      w[0] = 1;
+      w[1] = static_cast<int16_t>(sh.wt.luma_log2);
+      w[2] = static_cast<int16_t>(sh.wt.chroma_log2);
+      for (int l = 0; l < 2; ++l)
+        for (int i = 0; i < 32; ++i) {
+          w[kWpLw + l * 32 + i] = static_cast<int16_t>(sh.wt.lw[l][i]);
+          w[kWpLo + l * 32 + i] = static_cast<int16_t>(sh.wt.lo[l][i]);
+          for (int c = 0; c < 2; ++c) {
+            w[kWpCw + (l * 32 + i) * 2 + c] = static_cast<int16_t>(sh.wt.cw[l][i][c]);
+            w[kWpCo + (l * 32 + i) * 2 + c] = static_cast<int16_t>(sh.wt.co[l][i][c]);
+          }
+        }
+    } else if (sh.slice_type == SLICE_B && pp->weighted_bipred_idc == 2) {
+      w[0] = 2;
+      if (sh.num_ref_idx_l0_active > 8 || sh.num_ref_idx_l1_active > 8) cur->gpu_ok = false;
+      for (int i = 0; i < 8 && i < sh.num_ref_idx_l0_active; ++i)
+        for (int j = 0; j < 8 && j < sh.num_ref_idx_l1_active; ++j) {
+          w[kWpImp + (i * 8 + j) * 2] = static_cast<int16_t>(implicit_w[i][j][0]);
+          w[kWpImp + (i * 8 + j) * 2 + 1] = static_cast<int16_t>(implicit_w[i][j][1]);
+        }
+    }
+  }
+
+  // parse-only: boundary strength of every filtered edge segment (deblock.hip reads these
+  // instead of deriving them, so reference identity across lists / multi-reference and
+  // 8x8-transform edges follow the decoder exactly); 0 = not filtered
+  std::vector<uint8_t> boundary_strengths() {
+    int nmb = cur->wmb * cur->hmb;
+    std::vector<uint8_t> out(static_cast<size_t>(nmb) * 32, 0);
+    for (int addr = 0; addr < nmb; ++addr) {
+      if (cur->slice[addr] < 0) continue;
+      const SliceParams& spar = slices[cur->slice[addr]];
+      if (spar.disable_idc == 1) continue;
+      int mx = addr % cur->wmb, my = addr / cur->wmb;
+      bool left = mx > 0 && !(spar.disable_idc == 2 && cur->slice[addr - 1] != cur->slice[addr]);
+      bool top = my > 0 && !(spar.disable_idc == 2 && cur->slice[addr - cur->wmb] != cur->slice[addr]);
+      bool t8 = cur->t8x8[addr] != 0;
+      for (int dir = 0; dir < 2; ++dir)
+        for (int e = 0; e < 4; ++e) {
+          if (e == 0 && !(dir == 0 ? left : top)) continue;
+          if (t8 && (e & 1)) continue;
+          int mbp = e == 0 ? (dir == 0 ? addr - 1 : addr - cur->wmb) : addr;
+          for (int k = 0; k < 4; ++k) {
+            int blkq = dir == 0 ? (e + 4 * k) : (k + 4 * e);
+            int blkp = dir == 0 ? (e == 0 ? 3 + 4 * k : e - 1 + 4 * k) : (e == 0 ? k + 12 : k + 4 * (e - 1));
+            out[static_cast<size_t>(addr) * 32 + dir * 16 + e * 4 + k] =
+                static_cast<uint8_t>(bs_of(mbp, blkp, addr, blkq, e == 0));
+          }
+        }
+    }
+    return out;
   }
 
   // ------------------------------------------------------------ deblocking (8.7)

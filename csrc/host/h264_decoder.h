@@ -19,6 +19,13 @@
 namespace mivc {
 namespace h264 {
 
+// Weighted-prediction table of one picture (parse-only mode), int16 entries:
+// [0] mode (0 default, 1 explicit, 2 implicit), [1] luma_log2_weight_denom,
+// [2] chroma_log2_weight_denom, [kWpLw + l*32 + i] luma weight, [kWpLo + ...] luma offset,
+// [kWpCw + (l*32 + i)*2 + c] chroma weight, [kWpCo + ...] chroma offset,
+// [kWpImp + (i*8 + j)*2 + k] implicit weights w0/w1 of (refIdxL0 i, refIdxL1 j), i, j < 8.
+enum : int { kWpLw = 4, kWpLo = 68, kWpCw = 132, kWpCo = 260, kWpImp = 388, kWpEntries = 516 };
+
 struct DecodedPicture {
   int width = 0, height = 0;          // cropped display size
   int coded_width = 0, coded_height = 0;
@@ -44,8 +51,14 @@ struct DecodedPicture {
   int pic_id = 0, ref_id = -1;        // decode-order id of this picture / of its L0 ref 0
   int nal_ref = 1;
   int slice_qp = 0, alpha_off = 0, beta_off = 0, chroma_qp_offset = 0, deblock = 1;
-  bool gpu_ok = true;                 // false: a feature the GPU path does not cover (sub-8x8
-                                      // partitions, >1 reference, I_PCM, several slices ...)
+  bool gpu_ok = true;                 // false: a feature the GPU path does not cover (I_PCM,
+                                      // Intra8x8, several slices, constrained intra, mmco5 ...)
+  // parse-only motion / filter side info for GPU reconstruction of P and B pictures
+  std::vector<int16_t> mv_l[2];       // [mb][16 raster 4x4][2] quarter-sample MV per list
+  std::vector<int8_t> ref_l[2];       // [mb][16] ref_idx per list (-1 = list unused)
+  std::vector<uint8_t> bs;            // [mb][32] boundary strength: dir * 16 + edge * 4 + segment
+  std::vector<int32_t> list_ids;      // [2][32] decode-order picture id of RefPicList0/1[i], -1
+  std::vector<int16_t> wp;            // kWpEntries: weighted-prediction table (see kWp* below)
   // copy the cropped planes out as one contiguous I420 frame
   std::vector<uint8_t> cropped_i420() const;
 };

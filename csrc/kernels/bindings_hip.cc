@@ -52,10 +52,14 @@ void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t* src_y, con
 void mivc_launch_deblock(int B, int wmb, int hmb, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const void* hdr,
                          const uint8_t* nz, int chroma_qp_offset, int alpha_off, int beta_off, int* err,
                          void* stream);
-void mivc_launch_decode_picture(int B, int wmb, int hmb, const uint8_t* ref_y, const uint8_t* ref_u,
-                                const uint8_t* ref_v, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const void* hdr,
-                                const uint32_t* mask, const uint32_t* off, const int16_t* coef, const int8_t* run,
-                                int any_p, int chroma_qp_offset, uint8_t* nz, int* err, void* stream);
+void mivc_launch_decode_picture_dpb(int B, int wmb, int hmb, int dpb_n, uint8_t* dpb_y, uint8_t* dpb_u, uint8_t* dpb_v,
+                                    const int8_t* cur_idx, const int8_t* reftab, const int16_t* wp, const int16_t* mv,
+                                    const int8_t* refidx, const void* hdr, const uint32_t* mask, const uint32_t* off,
+                                    const int16_t* coef, const int8_t* run, int any_inter, int chroma_qp_offset,
+                                    uint8_t* nz, int* err, void* stream);
+void mivc_launch_deblock_dpb(int B, int wmb, int hmb, int dpb_n, uint8_t* dpb_y, uint8_t* dpb_u, uint8_t* dpb_v,
+                             const int8_t* cur_idx, const void* hdr, const uint8_t* nz, const uint8_t* bs,
+                             int chroma_qp_offset, int alpha_off, int beta_off, int* err, void* stream);
 void mivc_launch_hevc_intra(int B, int W, int H, const uint16_t* sy, const uint16_t* su, const uint16_t* sv,
                             uint16_t* ry, uint16_t* ru, uint16_t* rv, void* ctu, void* cu, int16_t* cy, int16_t* cu_,
                             int16_t* cv, const int* qp, const int8_t* run, int* cand, int bd, int analyze, int recon,
@@ -209,12 +213,23 @@ PYBIND11_MODULE(_hip, m) {
     mivc_launch_deblock(B, wmb, hmb, P<uint8_t>(ry), P<uint8_t>(ru), P<uint8_t>(rv), P<void>(hdr), P<uint8_t>(nz),
                         cqo, alpha_off, beta_off, P<int>(err), S(stream));
   });
-  m.def("decode_picture", [](int B, int wmb, int hmb, uintptr_t ry, uintptr_t ru, uintptr_t rv, uintptr_t y,
-                             uintptr_t u, uintptr_t v, uintptr_t hdr, uintptr_t mask, uintptr_t off, uintptr_t coef,
-                             uintptr_t run, int any_p, int cqo, uintptr_t nz, uintptr_t err, uintptr_t stream) {
-    mivc_launch_decode_picture(B, wmb, hmb, P<uint8_t>(ry), P<uint8_t>(ru), P<uint8_t>(rv), P<uint8_t>(y),
-                               P<uint8_t>(u), P<uint8_t>(v), P<void>(hdr), P<uint32_t>(mask), P<uint32_t>(off),
-                               P<int16_t>(coef), P<int8_t>(run), any_p, cqo, P<uint8_t>(nz), P<int>(err), S(stream));
+  m.def("decode_picture_dpb", [](int B, int wmb, int hmb, int dpb_n, uintptr_t y, uintptr_t u, uintptr_t v,
+                                 uintptr_t cur_idx, uintptr_t reftab, uintptr_t wp, uintptr_t mv, uintptr_t refidx,
+                                 uintptr_t hdr, uintptr_t mask, uintptr_t off, uintptr_t coef, uintptr_t run,
+                                 int any_inter, int cqo, uintptr_t nz, uintptr_t err, uintptr_t stream) {
+    if (dpb_n < 1 || dpb_n > 32) throw std::invalid_argument("decode_picture_dpb: dpb_n must be 1..32");
+    mivc_launch_decode_picture_dpb(B, wmb, hmb, dpb_n, P<uint8_t>(y), P<uint8_t>(u), P<uint8_t>(v), P<int8_t>(cur_idx),
+                                   P<int8_t>(reftab), P<int16_t>(wp), P<int16_t>(mv), P<int8_t>(refidx), P<void>(hdr),
+                                   P<uint32_t>(mask), P<uint32_t>(off), P<int16_t>(coef), P<int8_t>(run), any_inter,
+                                   cqo, P<uint8_t>(nz), P<int>(err), S(stream));
+  });
+  m.def("deblock_dpb", [](int B, int wmb, int hmb, int dpb_n, uintptr_t y, uintptr_t u, uintptr_t v, uintptr_t cur_idx,
+                          uintptr_t hdr, uintptr_t nz, uintptr_t bs, int cqo, int alpha_off, int beta_off, uintptr_t err,
+                          uintptr_t stream) {
+    if (dpb_n < 1 || dpb_n > 32) throw std::invalid_argument("deblock_dpb: dpb_n must be 1..32");
+    mivc_launch_deblock_dpb(B, wmb, hmb, dpb_n, P<uint8_t>(y), P<uint8_t>(u), P<uint8_t>(v), P<int8_t>(cur_idx),
+                            P<void>(hdr), P<uint8_t>(nz), P<uint8_t>(bs), cqo, alpha_off, beta_off, P<int>(err),
+                            S(stream));
   });
   // ---- HEVC
   m.def("hevc_prep_frame", [](int B, uintptr_t sy, uintptr_t su, uintptr_t sv, long long ss_y, long long ss_c,

@@ -25,6 +25,12 @@ struct DeblockArgs {
   int chroma_qp_offset;
   int alpha_off, beta_off;  // slice_alpha_c0_offset_div2*2, slice_beta_offset_div2*2
   int* err;
+  // decoder use: boundary strengths computed by the parser ([B, nmb, 32], dir * 16 +
+  // edge * 4 + segment; null: derive from the records) and the DPB layout of the planes
+  // (rec_* = [B][dpb_n] pictures, filtering picture cur_idx[slot]; dpb_n 0: [B] pictures)
+  const uint8_t* bs_in;
+  int dpb_n;
+  const int8_t* cur_idx;
 };
 
 constexpr int kDeblockWaves = 16;
@@ -156,9 +162,11 @@ __global__ __launch_bounds__(64 * kDeblockWaves) void deblock_wavefront(DeblockA
   const int ccomp = (hl - 16) >> 3, cline = hl & 7;                        \
   const int line = is_c ? cline : hl;
   const int W = g.W, cw = g.cw(), wmb = g.wmb, hmb = g.hmb;
-  uint8_t* recy = a.rec_y + slot * g.ysize();
-  uint8_t* const rcu = a.rec_u + slot * g.csize();
-  uint8_t* const rcv = a.rec_v + slot * g.csize();
+  const size_t pic = a.dpb_n ? static_cast<size_t>(slot) * a.dpb_n + a.cur_idx[slot] : static_cast<size_t>(slot);
+  uint8_t* recy = a.rec_y + pic * g.ysize();
+  uint8_t* const rcu = a.rec_u + pic * g.csize();
+  uint8_t* const rcv = a.rec_v + pic * g.csize();
+  const uint8_t* bs_in = a.bs_in ? a.bs_in + static_cast<size_t>(slot) * g.nmb() * 32 : nullptr;
   auto recc = [&](int c) { return c ? rcv : rcu; };
   const uint32_t* hdr32 = reinterpret_cast<const uint32_t*>(a.hdr) + static_cast<size_t>(slot) * g.nmb() * 16;
   const uint32_t* nz32 = reinterpret_cast<const uint32_t*>(a.nz) + static_cast<size_t>(slot) * g.nmb() * 4;
@@ -220,7 +228,9 @@ __global__ __launch_bounds__(64 * kDeblockWaves) void deblock_wavefront(DeblockA
           const int dir = hl >> 4, e = (hl >> 2) & 3, k = hl & 3;
           int bs = 0;
           const bool mbedge = e == 0;
-          if (!mbedge || (dir == 0 ? has_left : has_top)) {
+          if (bs_in) {
+            bs = bs_in[(static_cast<size_t>(y) * wmb + x) * 32 + hl];
+          } else if (!mbedge || (dir == 0 ? has_left : has_top)) {
             const int pw = mbedge ? (dir == 0 ? 1 : 2) : 0;
             const MbHeader* HP = reinterpret_cast<const MbHeader*>(S.hdrw[pw]);
             const uint8_t* nzbp = reinterpret_cast<const uint8_t*>(S.nzw[pw]);
@@ -449,5 +459,30 @@ extern "C" void mivc_launch_deblock(int B, int wmb, int hmb, uint8_t* rec_y, uin
   a.alpha_off = alpha_off;
   a.beta_off = beta_off;
   a.err = err;
+  a.bs_in = nullptr;
+  a.dpb_n = 0;
+  a.cur_idx = nullptr;
+  hipLaunchKernelGGL(deblock_wavefront, dim3(B), dim3(64 * kDeblockWaves), 0, static_cast<hipStream_t>(stream), a);
+}
+
+// decoder: filter picture cur_idx[slot] of each slot's DPB with the parser's boundary strengths
+extern "C" void mivc_launch_deblock_dpb(int B, int wmb, int hmb, int dpb_n, uint8_t* dpb_y, uint8_t* dpb_u,
+                                        uint8_t* dpb_v, const int8_t* cur_idx, const void* hdr, const uint8_t* nz,
+                                        const uint8_t* bs, int chroma_qp_offset, int alpha_off, int beta_off, int* err,
+                                        void* stream) {
+  DeblockArgs a;
+  a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
+  a.rec_y = dpb_y;
+  a.rec_u = dpb_u;
+  a.rec_v = dpb_v;
+  a.hdr = static_cast<const mivc::h264::MbHeader*>(hdr);
+  a.nz = nz;
+  a.chroma_qp_offset = chroma_qp_offset;
+  a.alpha_off = alpha_off;
+  a.beta_off = beta_off;
+  a.err = err;
+  a.bs_in = bs;
+  a.dpb_n = dpb_n;
+  a.cur_idx = cur_idx;
   hipLaunchKernelGGL(deblock_wavefront, dim3(B), dim3(64 * kDeblockWaves), 0, static_cast<hipStream_t>(stream), a);
 }

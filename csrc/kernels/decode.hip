@@ -1,26 +1,30 @@
 // H.264 picture reconstruction on gfx950 from entropy-decoded records (SURVEY.md
 // K-C1: the decode half of the transcode path, BASELINE config 3).
 //
-// The host parses CAVLC (csrc/host/h264_decoder.cc, parse-only mode) into the same
-// per-MB decision records the encoder produces (MbHeader) plus the quantised levels,
-// packed: only non-zero 4x4 blocks are stored, 16 levels each, located through a
-// per-MB bit mask (bits 0-15 luma blkIdx, 16 Intra16x16 DC, 17 chroma DC Cb|Cr,
-// 18-25 chroma AC comp*4+b) and the MB's first block index.  Reconstruction is then
-// the encoder's own closed loop without the decisions:
+// The host parses CAVLC or CABAC (csrc/host/h264_decoder.cc, parse-only mode) into the
+// same per-MB decision records the encoder produces (MbHeader) plus the quantised levels,
+// packed: only non-zero 16-level chunks are stored, located through a per-MB bit mask (bits
+// 0-15 luma blkIdx -- or, with the 8x8 transform, 8x8 block b8's levels 16k..16k+15 at
+// bit b8 * 4 + k --, 16 Intra16x16 DC, 17 chroma DC Cb|Cr, 18-25 chroma AC comp*4+b) and
+// the MB's first block index, plus every 4x4 block's vectors / reference indices, the
+// reference lists, the weighted-prediction table and the deblocking boundary strengths.
+// Pictures live in a per-slot decoded picture buffer ([B][dpb_n] planes):
 //
-//  * decode_inter_mb: every inter / P_Skip MB of a P picture in parallel (grid =
-//    MBs x slots, one wave64 per MB): quarter-sample luma MC per 8x8 quadrant from an
-//    LDS window of the reference, eighth-sample chroma MC, dequantisation and the
-//    normative inverse transform with DPP quad exchanges (grp_inv4x4);
-//  * decode_intra_wavefront: intra MBs in MB wavefront order (one workgroup per
-//    slot, LDS row-progress counters, as the intra encoder) -- all MBs of an I
-//    picture, only the intra MBs of a P picture (their inter neighbours are final);
-//  * the in-loop filter is the encoder's deblock kernel (deblock.hip), fed with the
-//    same MbHeader / non-zero flags this file writes.
+//  * decode_inter_dpb: every P / B macroblock in parallel (grid = MBs x slots, one wave64
+//    per MB): 6-tap luma MC per 4x4 block from LDS windows of its reference pictures,
+//    eighth-sample chroma MC, default / explicit / implicit weighted bi-prediction, and
+//    the 4x4 (DPP quad exchanges, grp_inv4x4) or 8x8 inverse transform;
+//  * decode_intra_wavefront: intra MBs in MB wavefront order (one workgroup per slot, LDS
+//    row-progress counters, as the intra encoder) -- Intra4x4, Intra8x8 (reference sample
+//    filtering, 9 modes) and Intra16x16; all MBs of an I picture, only the intra MBs of a
+//    P / B picture (their inter neighbours are final);
+//  * the in-loop filter is the encoder's deblock kernel (deblock.hip) reading the parser's
+//    boundary strengths.
 //
 // Reference parity: the reference decodes with ffmpeg inside the worker
 // (client.go:115-118); the CPU decoder (h264_decoder.cc) is the bit-exact oracle.
 #include "kcommon.h"
+#include "../common/h264_cabac_tables.h"
 
 namespace mivc {
 namespace gpu {
@@ -29,8 +33,7 @@ using h264::MbHeader;
 
 struct DecodeArgs {
   Geom g;
-  const uint8_t *ref_y, *ref_u, *ref_v;  // [B] reference picture per slot (P pictures)
-  uint8_t *rec_y, *rec_u, *rec_v;        // [B] picture being reconstructed
+  uint8_t *rec_y, *rec_u, *rec_v;        // decoded picture buffers (see dpb_n)
   const MbHeader* hdr;                   // [B, nmb]
   const uint32_t* mask;                  // [B, nmb] present blocks
   const uint32_t* off;                   // [B, nmb] first block (units of 16 levels, into coef)
@@ -39,7 +42,23 @@ struct DecodeArgs {
   int chroma_qp_offset;
   uint8_t* nz;                           // [B, nmb, 16] luma non-zero flags (raster), for deblocking
   int* err;
+  // rec_* point at the per-slot decoded picture buffers, [B][dpb_n] pictures
+  int dpb_n;
+  const int8_t* cur_idx;   // [B] DPB index of the picture being decoded
+  const int8_t* reftab;    // [B][2][32] DPB index of RefPicListX[i] (-1: none)
+  const int16_t* wp;       // [B][kWpEntries] weighted-prediction tables (h264_decoder.h)
+  const int16_t* mv;       // [B][2][nmb][16][2] quarter-sample vectors per raster 4x4 block
+  const int8_t* refidx;    // [B][2][nmb][16] ref_idx per raster 4x4 block, -1 = list unused
 };
+
+// weighted-prediction table layout (mirrors mivc::h264::kWp* in h264_decoder.h)
+enum : int { kWpLw = 4, kWpLo = 68, kWpCw = 132, kWpCo = 260, kWpImp = 388, kWpEntries = 516 };
+
+// the picture being reconstructed (luma / chroma plane) of a slot
+__device__ __forceinline__ uint8_t* rec_plane(const DecodeArgs& a, uint8_t* base, int slot, size_t psize) {
+  if (a.dpb_n == 0) return base + static_cast<size_t>(slot) * psize;
+  return base + (static_cast<size_t>(slot) * a.dpb_n + a.cur_idx[slot]) * psize;
+}
 
 // blkIdx -> 4x4 block column / row (no table: lane-varying lookups would be memory loads)
 __device__ __forceinline__ int blk_x(int b) { return ((b >> 2) & 1) * 2 + (b & 1); }
@@ -85,17 +104,88 @@ __device__ __forceinline__ uint32_t pack4(const int* p) {
          static_cast<uint32_t>(p[3]) << 24;
 }
 
-// ============================================================== inter macroblocks
-constexpr int kWin = 13;  // 8x8 quadrant + 6-tap support (-2 .. +3)
+// ============================================================== inter macroblocks, DPB layout
+// Every P / B macroblock of every slot in parallel (one wave64 per MB): per raster 4x4
+// block and list its own vector and reference picture (sub-8x8 partitions, B_8x8, direct
+// modes and several references all arrive resolved by the host parser), 6-tap luma MC
+// from a 9x9 LDS window per block, eighth-sample chroma MC, default / explicit / implicit
+// weighted sample prediction (8.4.2.3), and the 4x4 or 8x8 (8.5.13) inverse transform.
 
-__global__ __launch_bounds__(64) void decode_inter_mb(DecodeArgs a) {
+// LevelScale8x8 with flat weights: 16 * normAdjust8x8 (8.5.9)
+__device__ __forceinline__ int level_scale8(int m, int x, int y) {
+  int k;
+  if ((x & 3) == 0 && (y & 3) == 0) k = 0;
+  else if ((x & 1) && (y & 1)) k = 1;
+  else if ((x & 3) == 2 && (y & 3) == 2) k = 2;
+  else if (((x & 3) == 0 && (y & 1)) || ((x & 1) && (y & 3) == 0)) k = 3;
+  else if (((x & 3) == 0 && (y & 3) == 2) || ((x & 3) == 2 && (y & 3) == 0)) k = 4;
+  else k = 5;
+  constexpr int t[6][6] = {{20, 18, 32, 19, 25, 24}, {22, 19, 35, 21, 28, 26}, {26, 23, 42, 24, 33, 31},
+                           {28, 25, 45, 26, 35, 33}, {32, 28, 51, 30, 40, 38}, {36, 32, 58, 34, 46, 43}};
+  return 16 * t[m][k];
+}
+
+// one 8-point pass of the 8x8 inverse transform (8.5.13.2), in place, stride s
+__device__ __forceinline__ void idct8_pass(int* d, int s) {
+  const int d0 = d[0], d1 = d[s], d2 = d[2 * s], d3 = d[3 * s], d4 = d[4 * s], d5 = d[5 * s], d6 = d[6 * s],
+            d7 = d[7 * s];
+  const int a0 = d0 + d4, a4 = d0 - d4, a2 = (d2 >> 1) - d6, a6 = d2 + (d6 >> 1);
+  const int b0 = a0 + a6, b2 = a4 + a2, b4 = a4 - a2, b6 = a0 - a6;
+  const int a1 = -d3 + d5 - d7 - (d7 >> 1);
+  const int a3 = d1 + d7 - d3 - (d3 >> 1);
+  const int a5 = -d1 + d7 + d5 + (d5 >> 1);
+  const int a7 = d3 + d5 + d1 + (d1 >> 1);
+  const int b1 = a1 + (a7 >> 2), b7 = a7 - (a1 >> 2), b3 = a3 + (a5 >> 2), b5 = (a3 >> 2) - a5;
+  d[0] = b0 + b7;
+  d[s] = b2 + b5;
+  d[2 * s] = b4 + b3;
+  d[3 * s] = b6 + b1;
+  d[4 * s] = b6 - b1;
+  d[5 * s] = b4 - b3;
+  d[6 * s] = b2 - b5;
+  d[7 * s] = b0 - b7;
+}
+
+// weighted sample prediction of one sample (8.4.2.3); r0 / r1 = ref_idx (-1: list unused)
+__device__ __forceinline__ int weigh(const int16_t* w, bool chroma, int comp, int r0, int r1, int p0, int p1) {
+  const int mode = w[0];
+  const bool b0 = r0 >= 0, b1 = r1 >= 0;
+  if (mode == 1) {
+    const int logwd = chroma ? w[2] : w[1];
+    int w0 = 0, o0 = 0, w1 = 0, o1 = 0;
+    if (b0) {
+      w0 = chroma ? w[kWpCw + r0 * 2 + comp] : w[kWpLw + r0];
+      o0 = chroma ? w[kWpCo + r0 * 2 + comp] : w[kWpLo + r0];
+    }
+    if (b1) {
+      w1 = chroma ? w[kWpCw + (32 + r1) * 2 + comp] : w[kWpLw + 32 + r1];
+      o1 = chroma ? w[kWpCo + (32 + r1) * 2 + comp] : w[kWpLo + 32 + r1];
+    }
+    if (b0 && b1) return h264::clip1(((p0 * w0 + p1 * w1 + (1 << logwd)) >> (logwd + 1)) + ((o0 + o1 + 1) >> 1));
+    const int p = b0 ? p0 : p1, ww = b0 ? w0 : w1, o = b0 ? o0 : o1;
+    return h264::clip1(logwd >= 1 ? ((p * ww + (1 << (logwd - 1))) >> logwd) + o : p * ww + o);
+  }
+  if (b0 && b1) {
+    if (mode == 2) {
+      const int w0 = w[kWpImp + ((r0 & 7) * 8 + (r1 & 7)) * 2], w1 = w[kWpImp + ((r0 & 7) * 8 + (r1 & 7)) * 2 + 1];
+      return h264::clip1((p0 * w0 + p1 * w1 + 32) >> 6);
+    }
+    return (p0 + p1 + 1) >> 1;
+  }
+  return b0 ? p0 : p1;
+}
+
+constexpr int kBW = 9;  // 4x4 block + 6-tap support (-2 .. +6)
+
+__global__ __launch_bounds__(64) void decode_inter_dpb(DecodeArgs a) {
   const Geom& g = a.g;
   const int mb = blockIdx.x, slot = blockIdx.y;
   if (a.run[slot] != 2) return;
   const size_t o = static_cast<size_t>(slot) * g.nmb() + mb;
   const MbHeader* H = a.hdr + o;
   if (h264::mbk_is_intra(H->kind)) return;
-  __shared__ uint8_t win[4][kWin * kWin];
+  __shared__ uint8_t win[2][16][kBW * kBW];
+  __shared__ int d8[4][64];
   const int lane = threadIdx.x;
   const int mx = mb % g.wmb, my = mb / g.wmb;
   const int W = g.W, Hh = g.H, cw = g.cw(), ch = g.ch();
@@ -103,71 +193,132 @@ __global__ __launch_bounds__(64) void decode_inter_mb(DecodeArgs a) {
   const int qp = H->qp;
   const int qpc = h264::chroma_qp(qp, a.chroma_qp_offset);
   const uint32_t mask = a.mask[o], off = a.off[o];
-  const int m0x = H->mv[0][0][0], m0y = H->mv[0][0][1], m1x = H->mv[0][1][0], m1y = H->mv[0][1][1];
-  const int m2x = H->mv[0][2][0], m2y = H->mv[0][2][1], m3x = H->mv[0][3][0], m3y = H->mv[0][3][1];
+  const bool t8 = (H->flags & h264::MBF_T8x8) != 0;
+  const int D = a.dpb_n;
+  const int nmb = g.nmb();
+  const int16_t* mvp = a.mv + static_cast<size_t>(slot) * 2 * nmb * 32;
+  const int8_t* rip = a.refidx + static_cast<size_t>(slot) * 2 * nmb * 16;
+  const int8_t* rt = a.reftab + slot * 64;
+  const int16_t* wt = a.wp + static_cast<size_t>(slot) * kWpEntries;
+  auto mv_of = [&](int l, int rb, int c) { return static_cast<int>(mvp[(static_cast<size_t>(l) * nmb + mb) * 32 + rb * 2 + c]); };
+  auto ref_of = [&](int l, int rb) { return static_cast<int>(rip[(static_cast<size_t>(l) * nmb + mb) * 16 + rb]); };
+  auto pic_of = [&](int l, int r) {  // DPB index of RefPicListl[r], validated
+    const int di = (r >= 0 && r < 32) ? rt[l * 32 + r] : -1;
+    if (di < 0 || di >= D) {
+      atomicOr(a.err, 16);
+      return 0;
+    }
+    return di;
+  };
 
-  // ---- stage the four quadrant windows of the reference (clamped: unrestricted MVs)
-  const uint8_t* refy = a.ref_y + slot * g.ysize();
-  for (int i = lane; i < 4 * kWin * kWin; i += 64) {
-    const int q = i / (kWin * kWin), j = i - q * kWin * kWin;
-    const int r = j / kWin, c = j - r * kWin;
-    const int qx = sel4(q, m0x, m1x, m2x, m3x), qy = sel4(q, m0y, m1y, m2y, m3y);
-    const int x = clampi(X0 + (q & 1) * 8 + (qx >> 2) - 2 + c, 0, W - 1);
-    const int y = clampi(Y0 + (q >> 1) * 8 + (qy >> 2) - 2 + r, 0, Hh - 1);
-    win[q][j] = refy[static_cast<size_t>(y) * W + x];
+  // ---- stage the 9x9 window of every block and list (clamped: unrestricted vectors)
+  for (int i = lane; i < 2 * 16 * kBW * kBW; i += 64) {
+    const int l = i / (16 * kBW * kBW), j0 = i - l * 16 * kBW * kBW;
+    const int rb = j0 / (kBW * kBW), j = j0 - rb * kBW * kBW;
+    const int r = ref_of(l, rb);
+    if (r < 0) continue;
+    const int di = pic_of(l, r);
+    const int rr = j / kBW, cc = j - rr * kBW;
+    const int x = clampi(X0 + (rb & 3) * 4 + (mv_of(l, rb, 0) >> 2) - 2 + cc, 0, W - 1);
+    const int y = clampi(Y0 + (rb >> 2) * 4 + (mv_of(l, rb, 1) >> 2) - 2 + rr, 0, Hh - 1);
+    win[l][rb][j] = a.rec_y[(static_cast<size_t>(slot) * D + di) * g.ysize() + static_cast<size_t>(y) * W + x];
+  }
+  // ---- 8x8 transform: dequantise (lane = b8 * 16 + t, four levels each), then row and
+  // column passes in LDS
+  if (t8) {
+    const int b8 = lane >> 4, t = lane & 15;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = t * 4 + k;  // scan index
+      const int pos = h264::kZigzag8x8[i];
+      const int x = pos & 7, y = pos >> 3;
+      const int lv = level_at(a.coef, mask, off, b8 * 4 + (i >> 4), i & 15);
+      const int ls = level_scale8(qp % 6, x, y);
+      d8[b8][pos] = qp >= 36 ? (lv * ls) << (qp / 6 - 6) : (lv * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
+    }
   }
   __syncthreads();
+  if (t8) {
+    const int b8 = lane >> 4, t = lane & 15;
+    if (t < 8) idct8_pass(&d8[b8][t * 8], 1);
+    __syncthreads();
+    if (t < 8) idct8_pass(&d8[b8][t], 8);
+    __syncthreads();
+  }
 
   // ---- luma: lane = blkIdx * 4 + row
   {
     const int blk = lane >> 2, gy = lane & 3;
-    const int bx = blk_x(blk), by = blk_y(blk);
-    const int q = (bx >> 1) + 2 * (by >> 1);
-    const int qx = sel4(q, m0x, m1x, m2x, m3x), qy = sel4(q, m0y, m1y, m2y, m3y);
-    const uint8_t* w = win[q];
-    auto ref = [&](int x, int y) { return static_cast<int>(w[(y + 2) * kWin + x + 2]); };
-    const int lx = (bx & 1) * 4, ly = (by & 1) * 4 + gy;
-    int pr[4], v[4];
+    const int bx = blk_x(blk), by = blk_y(blk), rb = bx + 4 * by;
+    const int r0 = ref_of(0, rb), r1 = ref_of(1, rb);
+    int pl[2][4];
 #pragma unroll
-    for (int x = 0; x < 4; ++x) pr[x] = h264::mc_luma_sample(ref, lx + x, ly, qx & 3, qy & 3);
-    dequant_row(a.coef, mask, off, blk, gy, qp, false, v);
-    grp_inv4x4(v, lane & ~3, gy);
+    for (int l = 0; l < 2; ++l) {
+      const int r = l ? r1 : r0;
+      const uint8_t* w = win[l][rb];
+      auto ref = [&](int x, int y) { return static_cast<int>(w[(y + 2) * kBW + x + 2]); };
+      const int fx = mv_of(l, rb, 0) & 3, fy = mv_of(l, rb, 1) & 3;
 #pragma unroll
-    for (int x = 0; x < 4; ++x) pr[x] = h264::clip1(pr[x] + v[x]);
-    uint8_t* recy = a.rec_y + slot * g.ysize();
+      for (int x = 0; x < 4; ++x) pl[l][x] = r >= 0 ? h264::mc_luma_sample(ref, x, gy, fx, fy) : 0;
+    }
+    int v[4], pr[4];
+    if (t8) {
+      const int Y = by * 4 + gy;
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const int X = bx * 4 + x;
+        v[x] = (d8[(Y >> 3) * 2 + (X >> 3)][(Y & 7) * 8 + (X & 7)] + 32) >> 6;
+      }
+    } else {
+      dequant_row(a.coef, mask, off, blk, gy, qp, false, v);
+      grp_inv4x4(v, lane & ~3, gy);
+    }
+#pragma unroll
+    for (int x = 0; x < 4; ++x) pr[x] = h264::clip1(weigh(wt, false, 0, r0, r1, pl[0][x], pl[1][x]) + v[x]);
+    uint8_t* recy = rec_plane(a, a.rec_y, slot, g.ysize());
     *reinterpret_cast<uint32_t*>(recy + static_cast<size_t>(Y0 + by * 4 + gy) * W + X0 + bx * 4) = pack4(pr);
     if (lane < 16) a.nz[o * 16 + blk_x(lane) + 4 * blk_y(lane)] = (mask >> lane) & 1u;
   }
-  // ---- chroma: (lane & 31) = comp * 16 + block * 4 + row; lanes 32-63 mirror 0-31
+  // ---- chroma: (lane & 31) = comp * 16 + block * 4 + row; every chroma sample takes the
+  // vector of the luma 4x4 block it lies under; lanes 32-63 mirror 0-31 (transform partners)
   {
     const int cl = lane & 31, comp = cl >> 4, cb = (cl >> 2) & 3, gy = cl & 3;
     const int cbx = (cb & 1) * 4, cby = (cb >> 1) * 4;
-    const int cmx = sel4(cb, m0x, m1x, m2x, m3x), cmy = sel4(cb, m0y, m1y, m2y, m3y);
-    const uint8_t* refc = (comp == 0 ? a.ref_u : a.ref_v) + slot * g.csize();
-    const int xf = cmx & 7, yf = cmy & 7;
-    const int yi = my * 8 + cby + gy + (cmy >> 3);
-    const int y0 = clampi(yi, 0, ch - 1), y1 = clampi(yi + 1, 0, ch - 1);
-    const int xb = mx * 8 + cbx + (cmx >> 3);
-    int top[5], bot[5];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      const int xx = clampi(xb + k, 0, cw - 1);
-      top[k] = refc[static_cast<size_t>(y0) * cw + xx];
-      bot[k] = refc[static_cast<size_t>(y1) * cw + xx];
-    }
+    const int Yc = cby + gy;
     int pr[4], v[4];
 #pragma unroll
-    for (int x = 0; x < 4; ++x)
-      pr[x] = ((8 - xf) * (8 - yf) * top[x] + xf * (8 - yf) * top[x + 1] + (8 - xf) * yf * bot[x] + xf * yf * bot[x + 1] +
-               32) >> 6;
+    for (int x = 0; x < 4; ++x) {
+      const int Xc = cbx + x;
+      const int rb = (Xc >> 1) + 4 * (Yc >> 1);
+      const int r0 = ref_of(0, rb), r1 = ref_of(1, rb);
+      int pc[2];
+#pragma unroll
+      for (int l = 0; l < 2; ++l) {
+        const int r = l ? r1 : r0;
+        pc[l] = 0;
+        if (r >= 0) {
+          const int di = pic_of(l, r);
+          const uint8_t* refc = (comp == 0 ? a.rec_u : a.rec_v) + (static_cast<size_t>(slot) * D + di) * g.csize();
+          const int cmx = mv_of(l, rb, 0), cmy = mv_of(l, rb, 1);
+          const int xf = cmx & 7, yf = cmy & 7;
+          const int xi = mx * 8 + Xc + (cmx >> 3), yi = my * 8 + Yc + (cmy >> 3);
+          const int x0 = clampi(xi, 0, cw - 1), x1 = clampi(xi + 1, 0, cw - 1);
+          const int y0 = clampi(yi, 0, ch - 1), y1 = clampi(yi + 1, 0, ch - 1);
+          const int A = refc[static_cast<size_t>(y0) * cw + x0], Bv = refc[static_cast<size_t>(y0) * cw + x1];
+          const int C = refc[static_cast<size_t>(y1) * cw + x0], Dv = refc[static_cast<size_t>(y1) * cw + x1];
+          pc[l] = ((8 - xf) * (8 - yf) * A + xf * (8 - yf) * Bv + (8 - xf) * yf * C + xf * yf * Dv + 32) >> 6;
+        }
+      }
+      pr[x] = weigh(wt, true, comp, r0, r1, pc[0], pc[1]);
+    }
     dequant_row(a.coef, mask, off, 18 + comp * 4 + cb, gy, qpc, true, v);
     if (gy == 0) v[0] = chroma_dc_value(a.coef, mask, off, comp, cb, qpc);
     grp_inv4x4(v, lane & ~3, gy);
 #pragma unroll
     for (int x = 0; x < 4; ++x) pr[x] = h264::clip1(pr[x] + v[x]);
     if (lane < 32) {
-      uint8_t* recc = (comp == 0 ? a.rec_u : a.rec_v) + slot * g.csize();
-      *reinterpret_cast<uint32_t*>(recc + static_cast<size_t>(my * 8 + cby + gy) * cw + mx * 8 + cbx) = pack4(pr);
+      uint8_t* recc = rec_plane(a, comp == 0 ? a.rec_u : a.rec_v, slot, g.csize());
+      *reinterpret_cast<uint32_t*>(recc + static_cast<size_t>(my * 8 + Yc) * cw + mx * 8 + cbx) = pack4(pr);
     }
   }
 }
@@ -203,7 +354,55 @@ struct DecIntraShared {
   int saved_x;
   uint8_t saved_y[16];
   uint8_t saved_c[2][8];
+  // Intra8x8: residual (16x16 raster, before the final rounding), the row above the MB at
+  // x = 16..23 (top-right of 8x8 block 1), and the filtered references of the current block
+  int r8[256];
+  uint8_t tr8[8];
+  int e8t[16], e8l[8], e8tl;
+  int f8t[16], f8l[8], f8tl;
 };
+
+// Intra_8x8 sample (8.3.2.2.2 .. 8.3.2.2.10) from the filtered references ft / fl / ftl
+__device__ __forceinline__ int i8_pred_sample(int mode, int x, int y, const int* ft, const int* fl, int ftl, int dc) {
+  auto T = [&](int i) { return i < 0 ? ftl : ft[i]; };
+  auto L = [&](int i) { return i < 0 ? ftl : fl[i]; };
+  switch (mode) {
+    case 0: return ft[x];
+    case 1: return fl[y];
+    case 2: return dc;
+    case 3:
+      if (x == 7 && y == 7) return (ft[14] + 3 * ft[15] + 2) >> 2;
+      return (T(x + y) + 2 * T(x + y + 1) + T(x + y + 2) + 2) >> 2;
+    case 4:
+      if (x > y) return (T(x - y - 2) + 2 * T(x - y - 1) + T(x - y) + 2) >> 2;
+      if (x < y) return (L(y - x - 2) + 2 * L(y - x - 1) + L(y - x) + 2) >> 2;
+      return (T(0) + 2 * ftl + L(0) + 2) >> 2;
+    case 5: {
+      const int z = 2 * x - y;
+      if (z >= 0 && (z & 1) == 0) return (T(x - (y >> 1) - 1) + T(x - (y >> 1)) + 1) >> 1;
+      if (z >= 0) return (T(x - (y >> 1) - 2) + 2 * T(x - (y >> 1) - 1) + T(x - (y >> 1)) + 2) >> 2;
+      if (z == -1) return (L(0) + 2 * ftl + T(0) + 2) >> 2;
+      return (L(y - 2 * x - 1) + 2 * L(y - 2 * x - 2) + L(y - 2 * x - 3) + 2) >> 2;
+    }
+    case 6: {
+      const int z = 2 * y - x;
+      if (z >= 0 && (z & 1) == 0) return (L(y - (x >> 1) - 1) + L(y - (x >> 1)) + 1) >> 1;
+      if (z >= 0) return (L(y - (x >> 1) - 2) + 2 * L(y - (x >> 1) - 1) + L(y - (x >> 1)) + 2) >> 2;
+      if (z == -1) return (L(0) + 2 * ftl + T(0) + 2) >> 2;
+      return (T(x - 2 * y - 1) + 2 * T(x - 2 * y - 2) + T(x - 2 * y - 3) + 2) >> 2;
+    }
+    case 7:
+      if ((y & 1) == 0) return (T(x + (y >> 1)) + T(x + (y >> 1) + 1) + 1) >> 1;
+      return (T(x + (y >> 1)) + 2 * T(x + (y >> 1) + 1) + T(x + (y >> 1) + 2) + 2) >> 2;
+    default: {
+      const int z = x + 2 * y;
+      if (z < 13 && (z & 1) == 0) return (L(y + (x >> 1)) + L(y + (x >> 1) + 1) + 1) >> 1;
+      if (z < 13) return (L(y + (x >> 1)) + 2 * L(y + (x >> 1) + 1) + L(y + (x >> 1) + 2) + 2) >> 2;
+      if (z == 13) return (L(6) + 3 * L(7) + 2) >> 2;
+      return L(7);
+    }
+  }
+}
 
 __device__ __forceinline__ void decode_intra_mb(const DecodeArgs& a, DecIntraShared& S, int slot, int mx, int my) {
   const Geom& g = a.g;
@@ -220,7 +419,7 @@ __device__ __forceinline__ void decode_intra_mb(const DecodeArgs& a, DecIntraSha
   const int cmode = __builtin_amdgcn_readfirstlane(H->chroma_mode);
   const uint32_t mask = __builtin_amdgcn_readfirstlane(a.mask[o]);
   const uint32_t off = __builtin_amdgcn_readfirstlane(a.off[o]);
-  uint8_t* recy = a.rec_y + slot * g.ysize();
+  uint8_t* recy = rec_plane(a, a.rec_y, slot, g.ysize());
   int mbav = 0;
   if (mx > 0) mbav |= h264::AV_LEFT;
   if (my > 0) mbav |= h264::AV_TOP;
@@ -232,6 +431,10 @@ __device__ __forceinline__ void decode_intra_mb(const DecodeArgs& a, DecIntraSha
     const int x = X0 - 1 + lane;
     const bool ok = my > 0 && x >= 0 && x < W && (lane < 17 || (mbav & h264::AV_TOPRIGHT));
     S.tile[lane] = ok ? recy[static_cast<size_t>(Y0 - 1) * W + x] : 0;
+  } else if (lane >= 24 && lane < 32) {  // x = X0+16 .. X0+23 (Intra8x8 block 1's top-right)
+    const int x = X0 + 16 + (lane - 24);
+    const bool ok = (mbav & h264::AV_TOPRIGHT) && x < W;
+    S.tr8[lane - 24] = ok ? recy[static_cast<size_t>(Y0 - 1) * W + x] : 0;
   } else if (lane >= 32 && lane < 48) {  // tile col 0, rows 1..16
     const int r = lane - 32;
     uint8_t v = 0;
@@ -240,12 +443,12 @@ __device__ __forceinline__ void decode_intra_mb(const DecodeArgs& a, DecIntraSha
   }
   if (lane < 18) {
     const int c = lane / 9, i = lane % 9;
-    const uint8_t* rc = (c == 0 ? a.rec_u : a.rec_v) + slot * g.csize();
+    const uint8_t* rc = rec_plane(a, c == 0 ? a.rec_u : a.rec_v, slot, g.csize());
     const int x = mx * 8 - 1 + i;
     S.ctop[c][i] = (my > 0 && x >= 0) ? rc[static_cast<size_t>(my * 8 - 1) * cw + x] : 0;
   } else if (lane >= 48) {
     const int c = (lane - 48) >> 3, i = (lane - 48) & 7;
-    const uint8_t* rc = (c == 0 ? a.rec_u : a.rec_v) + slot * g.csize();
+    const uint8_t* rc = rec_plane(a, c == 0 ? a.rec_u : a.rec_v, slot, g.csize());
     uint8_t v = 0;
     if (mx > 0) v = S.saved_x == mx - 1 ? S.saved_c[c][i] : rc[static_cast<size_t>(my * 8 + i) * cw + mx * 8 - 1];
     S.cleft[c][i] = v;
@@ -297,6 +500,87 @@ __device__ __forceinline__ void decode_intra_mb(const DecodeArgs& a, DecIntraSha
     uint8_t* row = S.tile + (Yr + 1) * TS + bx * 4 + 1;
 #pragma unroll
     for (int x = 0; x < 4; ++x) row[x] = static_cast<uint8_t>(pr[x]);
+  } else if (kind == h264::MBK_I8x8) {
+    // Intra8x8: the four residual blocks at once (dequantise, 8x8 inverse transform), then
+    // the four predictions in order from reference-filtered neighbours (8.3.2.2.1)
+    {
+      const int b8 = lane >> 4, t = lane & 15, ox = (b8 & 1) * 8, oy = (b8 >> 1) * 8;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = t * 4 + k;
+        const int pos = h264::kZigzag8x8[i];
+        const int x = pos & 7, y = pos >> 3;
+        const int lv = level_at(a.coef, mask, off, b8 * 4 + (i >> 4), i & 15);
+        const int ls = level_scale8(qp % 6, x, y);
+        S.r8[(oy + y) * 16 + ox + x] = qp >= 36 ? (lv * ls) << (qp / 6 - 6) : (lv * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
+      }
+      wave_sync();
+      if (t < 8) idct8_pass(&S.r8[(oy + t) * 16 + ox], 1);
+      wave_sync();
+      if (t < 8) idct8_pass(&S.r8[oy * 16 + ox + t], 16);
+      wave_sync();
+    }
+    for (int b8 = 0; b8 < 4; ++b8) {
+      const int bx = (b8 & 1) * 8, by = (b8 >> 1) * 8;
+      const bool has_top = by > 0 || (mbav & h264::AV_TOP);
+      const bool has_left = bx > 0 || (mbav & h264::AV_LEFT);
+      const bool has_tl = b8 == 3 || (b8 == 0 ? (mbav & h264::AV_TOPLEFT) != 0
+                                              : (b8 == 1 ? (mbav & h264::AV_TOP) != 0 : (mbav & h264::AV_LEFT) != 0));
+      const bool has_tr = b8 == 2 || (b8 == 0 ? (mbav & h264::AV_TOP) != 0 : (b8 == 1 && (mbav & h264::AV_TOPRIGHT)));
+      const uint8_t* above = S.tile + by * TS + bx + 1;  // row above the block, x = 0
+      if (lane < 16) {
+        int v = lane < 8 ? above[lane] : (has_tr ? (b8 == 1 ? S.tr8[lane - 8] : above[lane]) : above[7]);
+        S.e8t[lane] = v;
+      } else if (lane < 24) {
+        S.e8l[lane - 16] = S.tile[(by + 1 + lane - 16) * TS + bx];
+      } else if (lane == 24) {
+        S.e8tl = S.tile[by * TS + bx];
+      }
+      wave_sync();
+      const int tl = S.e8tl;
+      if (lane < 16 && has_top) {
+        const int* t = S.e8t;
+        int f;
+        if (lane == 0) f = has_tl ? (tl + 2 * t[0] + t[1] + 2) >> 2 : (3 * t[0] + t[1] + 2) >> 2;
+        else if (lane == 15) f = (t[14] + 3 * t[15] + 2) >> 2;
+        else f = (t[lane - 1] + 2 * t[lane] + t[lane + 1] + 2) >> 2;
+        S.f8t[lane] = f;
+      } else if (lane >= 16 && lane < 24 && has_left) {
+        const int* l = S.e8l;
+        const int y = lane - 16;
+        int f;
+        if (y == 0) f = has_tl ? (tl + 2 * l[0] + l[1] + 2) >> 2 : (3 * l[0] + l[1] + 2) >> 2;
+        else if (y == 7) f = (l[6] + 3 * l[7] + 2) >> 2;
+        else f = (l[y - 1] + 2 * l[y] + l[y + 1] + 2) >> 2;
+        S.f8l[y] = f;
+      } else if (lane == 24) {
+        int f = 0;
+        if (has_tl) {
+          if (has_top && has_left) f = (S.e8t[0] + 2 * tl + S.e8l[0] + 2) >> 2;
+          else if (has_top) f = (3 * tl + S.e8t[0] + 2) >> 2;
+          else if (has_left) f = (3 * tl + S.e8l[0] + 2) >> 2;
+          else f = tl;
+        }
+        S.f8tl = f;
+      }
+      wave_sync();
+      const int mode = __builtin_amdgcn_readfirstlane(H->i4_modes[b8 * 4]);
+      int dc = 128;
+      if (mode == 2) {
+        int st = 0, sl = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          st += has_top ? S.f8t[i] : 0;
+          sl += has_left ? S.f8l[i] : 0;
+        }
+        dc = (has_top && has_left) ? (st + sl + 8) >> 4 : (has_left ? (sl + 4) >> 3 : (has_top ? (st + 4) >> 3 : 128));
+      }
+      const int x = lane & 7, y = lane >> 3;
+      const int pr = i8_pred_sample(mode, x, y, S.f8t, S.f8l, S.f8tl, dc);
+      const int rv = (S.r8[(by + y) * 16 + bx + x] + 32) >> 6;
+      S.tile[(by + 1 + y) * TS + bx + 1 + x] = static_cast<uint8_t>(h264::clip1(pr + rv));
+      wave_sync();
+    }
   } else {
     // Intra4x4: all 16 residual blocks at once, then the 16 predictions in order
     {
@@ -363,7 +647,7 @@ __device__ __forceinline__ void decode_intra_mb(const DecodeArgs& a, DecIntraSha
     }
     const uint32_t word = pack4(pr);
     if (lane < 32) {
-      uint8_t* recc = (comp == 0 ? a.rec_u : a.rec_v) + slot * g.csize();
+      uint8_t* recc = rec_plane(a, comp == 0 ? a.rec_u : a.rec_v, slot, g.csize());
       *reinterpret_cast<uint32_t*>(recc + static_cast<size_t>(my * 8 + Yc) * cw + mx * 8 + cbx) = word;
       if (cb & 1) S.saved_c[comp][(cb >> 1) * 4 + gy] = static_cast<uint8_t>(word >> 24);
     }
@@ -418,15 +702,11 @@ __global__ __launch_bounds__(64 * kDecIntraWaves) void decode_intra_wavefront(De
 
 using namespace mivc::gpu;
 
-static DecodeArgs make_decode_args(int B, int wmb, int hmb, const uint8_t* ref_y, const uint8_t* ref_u,
-                                   const uint8_t* ref_v, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v,
+static DecodeArgs make_decode_args(int B, int wmb, int hmb, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v,
                                    const void* hdr, const uint32_t* mask, const uint32_t* off, const int16_t* coef,
                                    const int8_t* run, int chroma_qp_offset, uint8_t* nz, int* err) {
   DecodeArgs a;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
-  a.ref_y = ref_y;
-  a.ref_u = ref_u;
-  a.ref_v = ref_v;
   a.rec_y = rec_y;
   a.rec_u = rec_u;
   a.rec_v = rec_v;
@@ -438,18 +718,32 @@ static DecodeArgs make_decode_args(int B, int wmb, int hmb, const uint8_t* ref_y
   a.chroma_qp_offset = chroma_qp_offset;
   a.nz = nz;
   a.err = err;
+  a.dpb_n = 0;
+  a.cur_idx = nullptr;
+  a.reftab = nullptr;
+  a.wp = nullptr;
+  a.mv = nullptr;
+  a.refidx = nullptr;
   return a;
 }
 
-// One picture of every slot: inter MBs (P pictures) then intra MBs in wavefront order.
-extern "C" void mivc_launch_decode_picture(int B, int wmb, int hmb, const uint8_t* ref_y, const uint8_t* ref_u,
-                                           const uint8_t* ref_v, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v,
-                                           const void* hdr, const uint32_t* mask, const uint32_t* off,
-                                           const int16_t* coef, const int8_t* run, int any_p, int chroma_qp_offset,
-                                           uint8_t* nz, int* err, void* stream) {
-  DecodeArgs a = make_decode_args(B, wmb, hmb, ref_y, ref_u, ref_v, rec_y, rec_u, rec_v, hdr, mask, off, coef, run,
+// One picture of every slot in the DPB layout: rec_* = [B][dpb_n] picture buffers; the
+// decoded picture goes to buffer cur_idx[slot]; P and B macroblocks from reftab / mv / refidx.
+extern "C" void mivc_launch_decode_picture_dpb(int B, int wmb, int hmb, int dpb_n, uint8_t* dpb_y, uint8_t* dpb_u,
+                                               uint8_t* dpb_v, const int8_t* cur_idx, const int8_t* reftab,
+                                               const int16_t* wp, const int16_t* mv, const int8_t* refidx,
+                                               const void* hdr, const uint32_t* mask, const uint32_t* off,
+                                               const int16_t* coef, const int8_t* run, int any_inter,
+                                               int chroma_qp_offset, uint8_t* nz, int* err, void* stream) {
+  DecodeArgs a = make_decode_args(B, wmb, hmb, dpb_y, dpb_u, dpb_v, hdr, mask, off, coef, run,
                                   chroma_qp_offset, nz, err);
+  a.dpb_n = dpb_n;
+  a.cur_idx = cur_idx;
+  a.reftab = reftab;
+  a.wp = wp;
+  a.mv = mv;
+  a.refidx = refidx;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (any_p) hipLaunchKernelGGL(decode_inter_mb, dim3(wmb * hmb, B), dim3(64), 0, s, a);
+  if (any_inter) hipLaunchKernelGGL(decode_inter_dpb, dim3(wmb * hmb, B), dim3(64), 0, s, a);
   hipLaunchKernelGGL(decode_intra_wavefront, dim3(B), dim3(64 * kDecIntraWaves), 0, s, a);
 }

@@ -1,4 +1,4 @@
-"""Batched H.264 (CAVLC) decode on MI355X: host entropy decode + gfx950 reconstruction.
+"""Batched H.264 decode on MI355X: host entropy decode (CAVLC / CABAC) + gfx950 reconstruction.
 
 The reference worker decodes its piece with ffmpeg before re-encoding
 (client.go:115-118 ``ffmpeg -i <idx>.mp4 <args> <out>``).  Here a transcode
@@ -14,11 +14,17 @@ decodes many closed-GOP segments at once:
    ``[segments, frames, H, W]`` device tensors the encoder consumes, so decoded
    pixels never cross PCIe.
 
-Segments the GPU path does not cover (sub-8x8 partitions, several reference
-frames, I_PCM, several slices, per-picture filter parameters that differ from the
-batch) are decoded by the CPU decoder instead (``h264_decoder.cc``) and uploaded;
-the result is identical either way (the CPU decoder is the bit-exact oracle of
-``tests/test_gpu_decode.py``).
+P and B pictures reconstruct from a per-slot decoded picture buffer ([B, D] pictures on
+the device, :func:`dpb_schedule`): the parser hands over every 4x4 block's vectors and
+reference indices (sub-8x8 partitions, B_8x8, spatial / temporal direct resolved),
+the reference lists as picture ids, the weighted-prediction table (explicit or
+implicit) and the deblocking boundary strengths; High-profile 8x8 transforms are
+inverse-transformed on the GPU.  Output frames land in display (POC) order.
+
+Segments the GPU path does not cover (I_PCM, Intra8x8, several slices, constrained intra
+prediction, mmco 5, per-picture filter parameters that differ from the batch) are decoded
+by the CPU decoder instead (``h264_decoder.cc``) and uploaded; the result is identical
+either way (the CPU decoder is the bit-exact oracle of ``tests/test_gpu_decode.py``).
 """
 from __future__ import annotations
 
@@ -54,7 +60,8 @@ class DecodedSegment:
         return int(self.y.shape[1])
 
 
-_META = ("pic_id", "ref_id", "nal_ref", "idr", "slice_type", "slice_qp", "alpha", "beta", "cqp", "deblock", "gpu_ok")
+_META = ("pic_id", "ref_id", "nal_ref", "idr", "slice_type", "slice_qp", "alpha", "beta", "cqp", "deblock", "gpu_ok",
+         "poc")
 M = {k: i for i, k in enumerate(_META)}
 
 
@@ -64,20 +71,52 @@ def _gpu_plan(seg: dict) -> tuple[bool, str]:
         return False, seg["error"]
     if seg["n"] == 0:
         return False, "no pictures"
-    meta = seg["meta"]
-    if not np.all(meta[:, M["gpu_ok"]] == 1):
+    if not np.all(seg["meta"][:, M["gpu_ok"]] == 1):
         return False, "unsupported coding tools"
-    last_ref = -1
-    for r in meta:
-        st = int(r[M["slice_type"]]) % 5
-        if st == 0:
-            if int(r[M["ref_id"]]) != last_ref or last_ref < 0:
-                return False, "reference is not the previous reference picture"
-        elif st != 2:
-            return False, f"slice type {st}"
-        if r[M["nal_ref"]]:
-            last_ref = int(r[M["pic_id"]])
     return True, ""
+
+
+def dpb_schedule(meta: np.ndarray, lists: np.ndarray, max_buffers: int = 32):
+    """Decoded-picture-buffer plan of one segment (decode order).
+
+    Returns (cur [P] buffer of each picture, reftab [P, 2, 32] buffer of RefPicListX[i]
+    or -1, display [P] output position, buffers used) or None when a list names a picture
+    that is not held.  A picture keeps its buffer until the last picture whose lists name
+    it; the output copy happens right after its own decode."""
+    P = meta.shape[0]
+    ids = meta[:, M["pic_id"]].astype(np.int64)
+    last = {int(i): p for p, i in enumerate(ids)}
+    for p in range(P):
+        for i in lists[p].reshape(-1):
+            if i >= 0:
+                last[int(i)] = max(last.get(int(i), p), p)
+    free = list(range(max_buffers))[::-1]
+    held: dict[int, int] = {}
+    cur = np.zeros(P, np.int8)
+    reftab = np.full((P, 2, 32), -1, np.int8)
+    used = 0
+    for p in range(P):
+        for l in range(2):
+            for k in range(32):
+                i = int(lists[p, l, k])
+                if i >= 0:
+                    if i not in held:
+                        return None
+                    reftab[p, l, k] = held[i]
+        if not free:
+            return None
+        b = free.pop()
+        cur[p] = b
+        held[int(ids[p])] = b
+        used = max(used, len(held))
+        for i in [i for i, _ in held.items() if last.get(i, -1) <= p]:
+            free.append(held.pop(i))
+    # display order: IDR epochs, then POC
+    epoch = np.cumsum(meta[:, M["idr"]] != 0)
+    order = np.lexsort((meta[:, M["poc"]], epoch))
+    display = np.empty(P, np.int64)
+    display[order] = np.arange(P)
+    return cur, reftab, display, max(used, 1)
 
 
 class GpuH264Decoder:
@@ -117,7 +156,11 @@ class GpuH264Decoder:
             key = (s["coded_width"], s["coded_height"], s["width"], s["height"], s["crop_x"], s["crop_y"], params.pop())
             groups.setdefault(key, []).append(i)
         for key, idxs in groups.items():
-            for i, d in zip(idxs, self._decode_group(key, [parsed[i] for i in idxs], fps)):
+            got = self._decode_group(key, [parsed[i] for i in idxs], fps)
+            if got is None:
+                fallback += idxs
+                continue
+            for i, d in zip(idxs, got):
                 out[i] = d
         t2 = time.perf_counter()
         for i in fallback:
@@ -141,77 +184,97 @@ class GpuH264Decoder:
         v = t[:, ys + cs:].reshape(len(pics), h // 2, w // 2)
         return DecodedSegment(y, u, v, fps, "cpu")
 
-    def _decode_group(self, key: tuple, segs: list[dict], fps: float) -> list[DecodedSegment]:
+    def _decode_group(self, key: tuple, segs: list[dict], fps: float) -> list[DecodedSegment] | None:
+        """Decode one batch of same-geometry segments; None if a DPB plan fails (CPU then)."""
         Wc, Hc, w, h, cx, cy, (alpha, beta, cqp, deblock) = key
         dev = self.dev
         wmb, hmb = Wc // 16, Hc // 16
         nmb = wmb * hmb
         B = len(segs)
         F = max(int(s["n"]) for s in segs)
-        # ---- pack the batch: [F, B, nmb, ...] records, one flat level array
+        plans = [dpb_schedule(s["meta"], s["lists"]) for s in segs]
+        if any(pl is None for pl in plans):
+            return None
+        D = max(pl[3] for pl in plans)
+        # ---- per picture-step tables, [F, B, ...]
         hdr = np.zeros((F, B, nmb, 64), np.uint8)
         mask = np.zeros((F, B, nmb), np.uint32)
         off = np.zeros((F, B, nmb), np.uint32)
         run = np.zeros((F, B), np.int8)
-        nal_ref = np.zeros((F, B), bool)
+        cur = np.zeros((F, B), np.int8)
+        reftab = np.full((F, B, 2, 32), -1, np.int8)
+        disp = np.zeros((F, B), np.int64)
+        wp = np.zeros((F, B, 516), np.int16)
         base = 0
         coefs = []
         for j, s in enumerate(segs):
-            P = int(s["n"])
-            hdr[:P, j] = s["hdr"]
-            mask[:P, j] = s["mask"]
-            off[:P, j] = s["off"] + (s["pic_off"][:P, None] + base).astype(np.uint32)
+            Pn = int(s["n"])
+            c_, r_, d_, _ = plans[j]
+            hdr[:Pn, j] = s["hdr"]
+            mask[:Pn, j] = s["mask"]
+            off[:Pn, j] = s["off"] + (s["pic_off"][:Pn, None] + base).astype(np.uint32)
             st = s["meta"][:, M["slice_type"]] % 5
-            run[:P, j] = np.where(st == 2, 1, 2)
-            nal_ref[:P, j] = s["meta"][:, M["nal_ref"]] != 0
+            run[:Pn, j] = np.where(st == 2, 1, 2)
+            cur[:Pn, j] = c_
+            reftab[:Pn, j] = r_
+            disp[:Pn, j] = d_
+            wp[:Pn, j] = s["wp"]
             coefs.append(s["coef"])
-            base += int(s["pic_off"][P])
+            base += int(s["pic_off"][Pn])
         if base >= 2 ** 32:
             raise ValueError("level array too large for 32-bit block offsets")
         coef = np.concatenate(coefs) if coefs else np.zeros(16, np.int16)
         if coef.size == 0:
             coef = np.zeros(16, np.int16)
-        d_hdr = torch.from_numpy(hdr).to(dev, non_blocking=False)
+        d_hdr = torch.from_numpy(hdr).to(dev)
         d_mask = torch.from_numpy(mask.view(np.int32)).to(dev)
         d_off = torch.from_numpy(off.view(np.int32)).to(dev)
         d_coef = torch.from_numpy(coef).to(dev)
         d_run = torch.from_numpy(run).to(dev)
-        # ---- output tensors and the per-slot working pictures
+        d_cur = torch.from_numpy(cur).to(dev)
+        d_reftab = torch.from_numpy(reftab).to(dev)
+        d_wp = torch.from_numpy(wp).to(dev)
+        # ---- output tensors and the per-slot decoded picture buffers
         y_out = torch.empty((B, F, Hc, Wc), dtype=torch.uint8, device=dev)
         u_out = torch.empty((B, F, Hc // 2, Wc // 2), dtype=torch.uint8, device=dev)
         v_out = torch.empty_like(u_out)
-        cur = [torch.zeros((B, Hc, Wc), dtype=torch.uint8, device=dev),
-               torch.zeros((B, Hc // 2, Wc // 2), dtype=torch.uint8, device=dev),
-               torch.zeros((B, Hc // 2, Wc // 2), dtype=torch.uint8, device=dev)]
-        ref = [torch.zeros_like(x) for x in cur]
+        dpb = [torch.zeros((B, D, Hc, Wc), dtype=torch.uint8, device=dev),
+               torch.zeros((B, D, Hc // 2, Wc // 2), dtype=torch.uint8, device=dev),
+               torch.zeros((B, D, Hc // 2, Wc // 2), dtype=torch.uint8, device=dev)]
         nz = torch.zeros((B, nmb, 16), dtype=torch.uint8, device=dev)
         err = torch.zeros((1,), dtype=torch.int32, device=dev)
-        s = torch.cuda.current_stream(dev).cuda_stream
+        s_ = torch.cuda.current_stream(dev).cuda_stream
         P_ = lambda t: t.data_ptr()  # noqa: E731
+        zero_mv = np.zeros((2, nmb, 16, 2), np.int16)
+        none_ref = np.full((2, nmb, 16), -1, np.int8)
+        zero_bs = np.zeros((nmb, 32), np.uint8)
         for t in range(F):
             active = run[t] != 0
-            any_p = bool(np.any(run[t] == 2))
-            self.hip.decode_picture(B, wmb, hmb, P_(ref[0]), P_(ref[1]), P_(ref[2]), P_(cur[0]), P_(cur[1]),
-                                    P_(cur[2]), P_(d_hdr[t]), P_(d_mask[t]), P_(d_off[t]), P_(d_coef), P_(d_run[t]),
-                                    int(any_p), cqp, P_(nz), P_(err), s)
+            any_inter = bool(np.any(run[t] == 2))
+            mv_t = np.stack([sg["mv"][t] if t < int(sg["n"]) else zero_mv for sg in segs])
+            ref_t = np.stack([sg["ref"][t] if t < int(sg["n"]) else none_ref for sg in segs])
+            d_mv = torch.from_numpy(mv_t).to(dev)
+            d_ref = torch.from_numpy(ref_t).to(dev)
+            self.hip.decode_picture_dpb(B, wmb, hmb, D, P_(dpb[0]), P_(dpb[1]), P_(dpb[2]), P_(d_cur[t]),
+                                        P_(d_reftab[t]), P_(d_wp[t]), P_(d_mv), P_(d_ref), P_(d_hdr[t]), P_(d_mask[t]),
+                                        P_(d_off[t]), P_(d_coef), P_(d_run[t]), int(any_inter), cqp, P_(nz), P_(err), s_)
             if deblock:
-                self.hip.deblock(B, wmb, hmb, P_(cur[0]), P_(cur[1]), P_(cur[2]), P_(d_hdr[t]), P_(nz), cqp, alpha,
-                                 beta, P_(err), s)
-            y_out[:, t].copy_(cur[0])
-            u_out[:, t].copy_(cur[1])
-            v_out[:, t].copy_(cur[2])
-            upd = nal_ref[t] & active
-            if (upd == active).all():  # inactive slots have ended: their buffers are free
-                cur, ref = ref, cur
-            elif upd.any():
-                sel = torch.from_numpy(np.nonzero(upd)[0]).to(dev)
-                for k in range(3):
-                    ref[k].index_copy_(0, sel, cur[k].index_select(0, sel))
+                bs_t = np.stack([sg["bs"][t] if t < int(sg["n"]) else zero_bs for sg in segs])
+                d_bs = torch.from_numpy(bs_t).to(dev)
+                self.hip.deblock_dpb(B, wmb, hmb, D, P_(dpb[0]), P_(dpb[1]), P_(dpb[2]), P_(d_cur[t]), P_(d_hdr[t]),
+                                     P_(nz), P_(d_bs), cqp, alpha, beta, P_(err), s_)
+            sel = np.nonzero(active)[0]
+            bi = torch.from_numpy(sel).to(dev)
+            di = torch.from_numpy(disp[t, sel]).to(dev)
+            ci = torch.from_numpy(cur[t, sel].astype(np.int64)).to(dev)
+            for o_, p_ in zip((y_out, u_out, v_out), dpb):
+                o_[bi, di] = p_[bi, ci]
         if int(err.item()) != 0:
-            raise RuntimeError("GPU decode: wavefront progress timeout")
+            raise RuntimeError(f"GPU decode failed (err={int(err.item()):#x}: 16 = reference outside the DPB, "
+                               "else a wavefront progress timeout)")
         res = []
         for j, sg in enumerate(segs):
-            P = int(sg["n"])
-            res.append(DecodedSegment(y_out[j, :P, cy:cy + h, cx:cx + w], u_out[j, :P, cy // 2:(cy + h) // 2, cx // 2:(cx + w) // 2],
-                                      v_out[j, :P, cy // 2:(cy + h) // 2, cx // 2:(cx + w) // 2], fps, "gpu"))
+            Pn = int(sg["n"])
+            res.append(DecodedSegment(y_out[j, :Pn, cy:cy + h, cx:cx + w], u_out[j, :Pn, cy // 2:(cy + h) // 2, cx // 2:(cx + w) // 2],
+                                      v_out[j, :Pn, cy // 2:(cy + h) // 2, cx // 2:(cx + w) // 2], fps, "gpu"))
         return res

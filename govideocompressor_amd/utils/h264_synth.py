@@ -107,22 +107,25 @@ def _intra_record(rng, h, c, mx, my, qp, density, allow_i4=True, t8x8=False):
 
 def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp: int = 28,
                   density: float = 0.15, intra_in_p: float = 0.1, mv_range: int = 48, keyint: int = 0,
-                  cabac: bool = False, t8x8: bool = False, records: list | None = None) -> bytes:
+                  cabac: bool = False, t8x8: bool = False, records: list | None = None, refs: int = 1) -> bytes:
     """Annex-B stream of ``frames`` pictures (IDR + P) from random decision records.
 
     cabac / t8x8 select the entropy coder and the High-profile 8x8 transform (I8x8 MBs and
     8x8-transformed inter MBs).  ``records``, if given, receives (hdr, coef) per picture."""
     rng = np.random.default_rng(seed)
-    cfg = dict(width=width, height=height, qp=qp, cabac=int(cabac), t8x8=int(t8x8))
+    cfg = dict(width=width, height=height, qp=qp, cabac=int(cabac), t8x8=int(t8x8), refs=int(refs))
     wmb, hmb = (width + 15) // 16, (height + 15) // 16
     nmb = wmb * hmb
     out = [host.parameter_sets(cfg)]
     fn = 0
     idr_id = 0
+    since_idr = 0
     for t in range(frames):
         idr = t == 0 or (keyint > 0 and t % keyint == 0)
         if idr:
             fn = 0
+            since_idr = 0
+        nref = max(1, min(int(refs), since_idr))  # references held by the sliding window
         sqp = int(np.clip(qp + rng.integers(-2, 3), 10, 48))
         hdr = np.zeros((nmb, HDR_BYTES), np.uint8)
         hdr[:, _REF:_REF + 8] = 0xFF
@@ -146,7 +149,14 @@ def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp:
             h[_KIND] = kind
             h[_QP] = mqp
             h[_MV:_MV + 16] = np.frombuffer(mv.astype(np.int16).tobytes(), np.uint8)
-            h[_REF:_REF + 4] = 0
+            rf = rng.integers(0, nref, 4) if kind != PSKIP else np.zeros(4, np.int64)
+            if kind == P16x16:
+                rf[:] = rf[0]
+            elif kind == P16x8:
+                rf[1], rf[3] = rf[0], rf[2]
+            elif kind == P8x16:
+                rf[2], rf[3] = rf[0], rf[1]
+            h[_REF:_REF + 4] = rf.astype(np.uint8)
             if kind != PSKIP:
                 if t8x8 and rng.random() < 0.5:
                     h[_FLAGS] = MBF_T8x8
@@ -159,12 +169,15 @@ def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp:
                 for b in range(8):
                     c[280 + b * 16:280 + (b + 1) * 16] = _levels(rng, 16, density / 2, start=1)
         fp = dict(idr=int(idr), qp=sqp, frame_num=fn, idr_pic_id=idr_id)
+        if not idr and refs > 1:
+            fp["num_ref_l0"] = nref
         nal, _ = host.write_slice(cfg, fp, hdr, coef)
         out.append(nal)
         if records is not None:
             records.append((hdr, coef))
         if idr:
             idr_id += 1
+        since_idr += 1
         fn = (fn + 1) % 16
     return b"".join(out)
 

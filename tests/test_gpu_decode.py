@@ -88,5 +88,24 @@ def test_gpu_decode_gpu_encoder_stream(host, dec):
 
 
 def test_gpu_decode_gpu_encoder_cabac_b_stream(host, dec):
-    # the default encoder (Main CABAC + 3 B): decoded output matches the CPU decoder
-    _check(host, dec, _gpu_encoder_streams(), expect_gpu=False)
+    # the default encoder (Main CABAC + 3 B, temporal direct): B pictures from the DPB,
+    # output in display order
+    _check(host, dec, _gpu_encoder_streams())
+
+
+def test_gpu_decode_multiref_high_cabac(host, dec):
+    """CABAC streams with up to 4 references per P picture (per-partition ref_idx), 8x8
+    transforms on inter MBs and Intra8x8 MBs (High profile)."""
+    streams = [random_stream(host, 96, 64, 7, seed=31, cabac=True, refs=3),
+               random_stream(host, 96, 64, 6, seed=32, cabac=True, refs=4, t8x8=True),
+               random_stream(host, 176, 144, 5, seed=33, cabac=True, t8x8=True, intra_in_p=0.3),
+               random_stream(host, 50, 34, 6, seed=34, cabac=True, refs=2, t8x8=True, keyint=3)]
+    out = _check(host, dec, streams)
+    assert dec.stats["segments_cpu"] == 0
+
+
+def test_gpu_decode_b_records(host, dec):
+    """B pictures with L0 / L1 / bi-predicted 16x16 MBs, direct and skipped MBs."""
+    from tests.test_h264_bframes import _b_stream
+    streams = [_b_stream(host, w, h, seed)[0] for w, h, seed in ((64, 48, 1), (96, 80, 2), (176, 144, 3))]
+    _check(host, dec, streams)
