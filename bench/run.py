@@ -11,8 +11,9 @@
    GPU backend when a GPU is visible).
 2. 1080p30 synthetic YUV -> H.264 CRF23 on MI355X: delegates to ``bench.py``
    (the driver's headline metric).
-3. 4K30 H.264 -> H.264 transcode, segment-parallel: a 4K CAVLC stream is made
-   (untimed) with the GPU encoder, then decode + re-encode is timed end to end.
+3. 4K30 H.264 -> H.264 transcode, segment-parallel: a 4K Main-profile CABAC stream with
+   3 B pictures per anchor is made (untimed) with the GPU encoder, then decode (host
+   CABAC parse + gfx950 DPB reconstruction) + re-encode is timed end to end.
 4. 1080p30 synthetic YUV -> HEVC CRF26 (the reference's "265" preset) on MI355X:
    batched GPU HEVC encoder (CTU intra analysis/reconstruction, P pictures, deblock,
    SAO) + host CABAC.
@@ -122,7 +123,7 @@ def config2(args) -> list[dict]:
 
 
 def config3(args) -> list[dict]:
-    """4K30 H.264 -> H.264: batched GPU decode (host CAVLC parse + gfx950 reconstruction) + GPU re-encode."""
+    """4K30 H.264 -> H.264: batched GPU decode (host CABAC parse + gfx950 reconstruction) + GPU re-encode."""
     import torch
     if not torch.cuda.is_available():
         return [{"config": 3, "value": None, "note": "needs a GPU"}]
@@ -149,7 +150,7 @@ def config3(args) -> list[dict]:
         return [{"config": 3, "metric": "transcoded frames/sec (whole node), 4K30 H.264->H.264", "value":
                  round(S * F / wall, 2), "unit": "frames/s", "n_gpus": 1, "frames": S * F, "segments": S,
                  "wall_s": round(wall, 3), "output_bytes": r.get("bytes"),
-                 "data": "synthetic 4K CAVLC stream made by this encoder (no reference clips available)",
+                 "data": "synthetic 4K Main CABAC + 3B stream made by this encoder (no reference clips available)",
                  "decode": r.get("decode"), "decode_stats": r.get("decode_stats_rank")}]
     finally:
         shutil.rmtree(tmp, ignore_errors=True)

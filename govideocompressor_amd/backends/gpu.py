@@ -213,7 +213,7 @@ class GpuBackend:
         return chosen, info
 
     def decoder(self):
-        """The batched GPU H.264 decoder (host CAVLC parse + gfx950 reconstruction)."""
+        """The batched GPU H.264 decoder (host CAVLC/CABAC parse + gfx950 reconstruction)."""
         if self._decoder is None:
             from ..models.h264_decode_gpu import GpuH264Decoder
             self._decoder = GpuH264Decoder(self.device)
@@ -224,7 +224,7 @@ class GpuBackend:
         return self.decoder().decode(streams, fps)
 
     def _load_compressed(self, jobs: list[PieceJob]) -> dict[str, object]:
-        """Compressed pieces (.264/.mp4, CAVLC) decode together on the GPU."""
+        """Compressed pieces (.264/.mp4; CAVLC or CABAC, I/P/B, High 8x8) decode together on the GPU."""
         from ..ops import native
         from ..segment.probe import annexb_of, kind_of
         host = native.host()
@@ -232,8 +232,6 @@ class GpuBackend:
         for j in jobs:
             st = annexb_of(j.in_path, kind_of(j.in_path))
             info = host.stream_info(st)
-            if info["entropy"] == "cabac":
-                raise BackendError("input uses CABAC; this build decodes CAVLC H.264 only")
             fps = info["fps"] or fps
             streams.append(st)
             keys.append(j.idx)
