@@ -60,6 +60,10 @@ void mivc_launch_decode_picture_dpb(int B, int wmb, int hmb, int dpb_n, uint8_t*
 void mivc_launch_deblock_dpb(int B, int wmb, int hmb, int dpb_n, uint8_t* dpb_y, uint8_t* dpb_u, uint8_t* dpb_v,
                              const int8_t* cur_idx, const void* hdr, const uint8_t* nz, const uint8_t* bs,
                              int chroma_qp_offset, int alpha_off, int beta_off, int* err, void* stream);
+int mivc_launch_scale(const void* in, int w, int h, long long in_stride, long long in_pitch, void* out, int ow, int oh,
+                      int W, int H, long long out_stride, long long out_pitch, int nframes, const int* fx,
+                      const int16_t* cx, int tx, const int* fy, const int16_t* cy, int ty, int tile_w, int tile_h,
+                      int in_cols, int in_rows, int bd, void* stream);
 void mivc_launch_hevc_intra(int B, int W, int H, const uint16_t* sy, const uint16_t* su, const uint16_t* sv,
                             uint16_t* ry, uint16_t* ru, uint16_t* rv, void* ctu, void* cu, int16_t* cy, int16_t* cu_,
                             int16_t* cv, const int* qp, const int8_t* run, int* cand, int bd, int analyze, int recon,
@@ -119,6 +123,8 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("prep", [](uintptr_t iy, uintptr_t iu, uintptr_t iv, int w, int h, int64_t sy, int64_t sc, int n,
                    uintptr_t oy, uintptr_t ou, uintptr_t ov, int ow, int oh, int W, int H, uintptr_t stream) {
+    if (ow != w || oh != h) throw std::invalid_argument("prep: resample with ops.scale (scale.hip) first");
+    if (W < w || H < h || w < 2 || h < 2) throw std::invalid_argument("prep: bad geometry");
     mivc_launch_prep(P<uint8_t>(iy), P<uint8_t>(iu), P<uint8_t>(iv), w, h, sy, sc, n, P<uint8_t>(oy), P<uint8_t>(ou),
                      P<uint8_t>(ov), ow, oh, W, H, S(stream));
   });
@@ -230,6 +236,16 @@ PYBIND11_MODULE(_hip, m) {
     mivc_launch_deblock_dpb(B, wmb, hmb, dpb_n, P<uint8_t>(y), P<uint8_t>(u), P<uint8_t>(v), P<int8_t>(cur_idx),
                             P<void>(hdr), P<uint8_t>(nz), P<uint8_t>(bs), cqo, alpha_off, beta_off, P<int>(err),
                             S(stream));
+  });
+  m.def("scale", [](uintptr_t in, int w, int h, long long in_stride, long long in_pitch, uintptr_t out, int ow, int oh,
+                    int W, int H, long long out_stride, long long out_pitch, int n, uintptr_t fx, uintptr_t cx, int tx,
+                    uintptr_t fy, uintptr_t cy, int ty, int tile_w, int tile_h, int in_cols, int in_rows, int bd,
+                    uintptr_t stream) {
+    if (w < 1 || h < 1 || ow < 1 || oh < 1 || W < ow || H < oh || tx < 1 || ty < 1 || tile_w < 1 || tile_h < 1)
+      throw std::invalid_argument("scale: bad geometry");
+    return mivc_launch_scale(P<void>(in), w, h, in_stride, in_pitch, P<void>(out), ow, oh, W, H, out_stride, out_pitch,
+                             n, P<int>(fx), P<int16_t>(cx), tx, P<int>(fy), P<int16_t>(cy), ty, tile_w, tile_h, in_cols,
+                             in_rows, bd, S(stream));
   });
   // ---- HEVC
   m.def("hevc_prep_frame", [](int B, uintptr_t sy, uintptr_t su, uintptr_t sv, long long ss_y, long long ss_c,

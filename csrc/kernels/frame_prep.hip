@@ -1,8 +1,7 @@
 // Frame preparation: display-size I420 -> coded-size (multiple of 16) planar
-// frames with edge replication, optional separable resampling (the `-s WxH`
-// scaling the reference's operators passed to ffmpeg, server.go:87-90), and a
-// packed-RGB -> I420 colour conversion (BT.601 limited range) entry point.
-// SURVEY.md K-C2 (csc_scale).
+// frames with edge replication, and a packed-RGB -> I420 colour conversion (BT.601
+// limited range, ops/scale.py rgb_to_i420).  Resampling (`-s WxH`, server.go:87-90)
+// is the bicubic filter of scale.hip.  SURVEY.md K-C2 (csc_scale).
 #include "kcommon.h"
 
 namespace mivc {
@@ -17,22 +16,11 @@ struct PrepArgs {
   uint8_t* out_y;       // [N, H, W] coded
   uint8_t* out_u;
   uint8_t* out_v;
-  int ow, oh;           // output display size (== w,h when not scaling)
+  int ow, oh;           // output display size (== w, h: inputs arrive resampled)
   int W, H;             // coded size
 };
 
-// bilinear sample of an 8-bit plane at (fx, fy) in input pixel units
-__device__ __forceinline__ int bilinear(const uint8_t* p, int w, int h, float fx, float fy) {
-  fx = fminf(fmaxf(fx, 0.f), static_cast<float>(w - 1));
-  fy = fminf(fmaxf(fy, 0.f), static_cast<float>(h - 1));
-  int x0 = static_cast<int>(fx), y0 = static_cast<int>(fy);
-  int x1 = min(x0 + 1, w - 1), y1 = min(y0 + 1, h - 1);
-  float tx = fx - x0, ty = fy - y0;
-  float a = p[y0 * w + x0] * (1 - tx) + p[y0 * w + x1] * tx;
-  float b = p[y1 * w + x0] * (1 - tx) + p[y1 * w + x1] * tx;
-  return static_cast<int>(a * (1 - ty) + b * ty + 0.5f);
-}
-
+// Copy + edge replication into the coded padding (resampling runs before, in scale.hip).
 __global__ void prep_plane(PrepArgs a, int plane) {
   int x = blockIdx.x * blockDim.x + threadIdx.x;
   int y = blockIdx.y;
@@ -40,20 +28,13 @@ __global__ void prep_plane(PrepArgs a, int plane) {
   int sh = plane ? 1 : 0;
   int W = a.W >> sh, H = a.H >> sh;
   if (x >= W) return;
-  int w = a.w >> sh, h = a.h >> sh, ow = a.ow >> sh, oh = a.oh >> sh;
+  int w = a.w >> sh, h = a.h >> sh;
   const uint8_t* in = plane == 0 ? a.in_y : (plane == 1 ? a.in_u : a.in_v);
   in += n * (plane ? a.in_frame_stride_c : a.in_frame_stride_y);
   uint8_t* out = plane == 0 ? a.out_y : (plane == 1 ? a.out_u : a.out_v);
   out += static_cast<size_t>(n) * W * H;
-  int cx = min(x, ow - 1), cy = min(y, oh - 1);  // edge replication into the coded padding
-  int v;
-  if (ow == w && oh == h) {
-    v = in[static_cast<size_t>(cy) * w + cx];
-  } else {
-    float fx = (cx + 0.5f) * w / ow - 0.5f, fy = (cy + 0.5f) * h / oh - 0.5f;
-    v = bilinear(in, w, h, fx, fy);
-  }
-  out[static_cast<size_t>(y) * W + x] = static_cast<uint8_t>(v);
+  int cx = min(x, w - 1), cy = min(y, h - 1);
+  out[static_cast<size_t>(y) * W + x] = in[static_cast<size_t>(cy) * w + cx];
 }
 
 // Fast path (no resampling, 16-byte aligned rows): one thread per 16 output bytes.
@@ -116,7 +97,8 @@ extern "C" void mivc_launch_prep(const uint8_t* in_y, const uint8_t* in_u, const
   bool aligned = (w % 32 == 0) && (in_stride_y % 16 == 0) && (in_stride_c % 16 == 0) &&
                  (reinterpret_cast<uintptr_t>(in_y) % 16 == 0) && (reinterpret_cast<uintptr_t>(in_u) % 16 == 0) &&
                  (reinterpret_cast<uintptr_t>(in_v) % 16 == 0) && W % 32 == 0;
-  if (ow == w && oh == h && aligned) {
+  if (ow != w || oh != h) return;  // scale.hip resamples before prep (the binding rejects this)
+  if (aligned) {
     hipLaunchKernelGGL(prep_plane_copy16, dim3((W / 16 + 63) / 64, H, nframes), dim3(64), 0, s, a, 0);
     hipLaunchKernelGGL(prep_plane_copy16, dim3((W / 32 + 63) / 64, H / 2, nframes), dim3(64), 0, s, a, 1);
     hipLaunchKernelGGL(prep_plane_copy16, dim3((W / 32 + 63) / 64, H / 2, nframes), dim3(64), 0, s, a, 2);

@@ -20,25 +20,12 @@ from .common import BackendError, PieceJob, PieceResult, idr_id, load_clip, outp
 
 
 def resize_clip(clip: yuv.Clip, ow: int, oh: int) -> yuv.Clip:
-    """Bilinear resample (half-pixel centres, like the gfx950 prep kernel)."""
+    """Bicubic resample (swscale's default filter family), the GPU scaler's numpy model."""
     if (ow, oh) == (clip.width, clip.height):
         return clip
-
-    def rs(p: np.ndarray, w: int, h: int) -> np.ndarray:
-        F, ih, iw = p.shape
-        fx = np.clip((np.arange(w) + 0.5) * iw / w - 0.5, 0, iw - 1)
-        fy = np.clip((np.arange(h) + 0.5) * ih / h - 0.5, 0, ih - 1)
-        x0 = fx.astype(np.int64)
-        y0 = fy.astype(np.int64)
-        x1 = np.minimum(x0 + 1, iw - 1)
-        y1 = np.minimum(y0 + 1, ih - 1)
-        tx = (fx - x0)[None, None, :]
-        ty = (fy - y0)[None, :, None]
-        q = p.astype(np.float32)
-        a = q[:, y0][:, :, x0] * (1 - tx) + q[:, y0][:, :, x1] * tx
-        b = q[:, y1][:, :, x0] * (1 - tx) + q[:, y1][:, :, x1] * tx
-        return (a * (1 - ty) + b * ty + 0.5).astype(np.uint8)
-    return yuv.Clip(rs(clip.y, ow, oh), rs(clip.u, ow // 2, oh // 2), rs(clip.v, ow // 2, oh // 2), clip.fps)
+    from ..ops.scale import scale_plane_ref
+    return yuv.Clip(scale_plane_ref(clip.y, ow, oh), scale_plane_ref(clip.u, ow // 2, oh // 2),
+                    scale_plane_ref(clip.v, ow // 2, oh // 2), clip.fps)
 
 
 class CpuBackend:

@@ -95,8 +95,6 @@ class GpuBackend:
             fps = cfg.fps or clips[keys[0]].fps
             crf = cfg.crf if cfg.bitrate is None else 23.0  # ABR searches an offset from CRF 23
             if cfg.codec == "hevc":
-                if (ow, oh) != (w, h):
-                    raise BackendError("scaling is not available in the HEVC path")
                 params = HevcParams(width=ow, height=oh, fps=fps, crf=crf if cfg.qp is None else None,
                                     qp=cfg.qp if cfg.qp is not None else 30, bit_depth=cfg.bit_depth)
             else:
@@ -108,6 +106,11 @@ class GpuBackend:
             cap = min(self.max_slots, slots_for(ow, oh, max(c for *_, c in units), self._info, cap=self.max_slots))
             chunks = [units[b0:b0 + cap] for b0 in range(0, len(units), cap)]
             prepared = [self._prepare_chunk(ch, clips, w, h, tm) for ch in chunks]
+            if (ow, oh) != (w, h):  # -s WxH: bicubic resample on the device (ops/scale.py)
+                if getattr(self, "_scaler", None) is None:
+                    from ..ops.scale import GpuScaler
+                    self._scaler = GpuScaler(self.device)
+                prepared = [self._scaler.clip(*dev, ow, oh) for dev in prepared]
             rate_info: dict[str, dict] = {}
             if cfg.bitrate is None and qp_offsets is None:
                 unit_out = [x for ch, dev in zip(chunks, prepared) for x in self._run_encoder(ch, params, *dev, tm)]

@@ -730,7 +730,8 @@ class GpuH264Encoder:
         y: [B, F, h, w] uint8 (device), u/v: [B, F, h/2, w/2].  Each slot's output is a
         self-contained Annex-B segment (SPS/PPS + IDR + P...), i.e. one "piece" of the
         reference's split directory, with idr_pic_id = idr_ids[slot] (default idr_base + slot).
-        When (h, w) differs from the configured size the prep kernel resamples (``-s WxH``).
+        When (h, w) differs from the configured size the frames are resampled first (bicubic,
+        ``-s WxH``, :mod:`govideocompressor_amd.ops.scale`).
         ``qps``: optional [B, F] per-frame QPs from the rate control (default: the params' CRF/QP,
         I frames 3 lower).  ``qp_delta``: optional [B, F] float offsets (display order) added
         to the final frame QPs -- after the lookahead CRF curve and the B-picture offset --
@@ -747,6 +748,11 @@ class GpuH264Encoder:
             raise ValueError("u/v must be [B, F, h/2, w/2] with even h, w")
         if not (y.is_contiguous() and u.is_contiguous() and v.is_contiguous()):
             raise ValueError("planes must be contiguous")
+        if (w, h) != (self.p.width, self.p.height):  # -s WxH: bicubic resample (ops/scale.py)
+            if getattr(self, "_scaler", None) is None:
+                from ..ops.scale import GpuScaler
+                self._scaler = GpuScaler(self.dev)
+            y, u, v = self._scaler.clip(y, u, v, self.p.width, self.p.height)
         idr_ids = list(idr_ids) if idr_ids is not None else [idr_base + b for b in range(B)]
         if len(idr_ids) != B:
             raise ValueError("idr_ids needs one entry per slot")
