@@ -158,7 +158,8 @@ __device__ __forceinline__ int mvbits_se(int v) {
 __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   const Geom& g = a.g;
   const int nmb = g.nmb();
-  const int mb = blockIdx.x, slot = blockIdx.y;
+  int mb, slot;
+  xcd_unit_slot(mb, slot);
   const int lane = threadIdx.x;
   const size_t o = static_cast<size_t>(slot) * nmb + mb;
   const int mx = mb % g.wmb, my = mb / g.wmb;
@@ -269,7 +270,9 @@ __device__ __forceinline__ int median3(int a, int b, int c) { return max(min(a, 
 __global__ __launch_bounds__(64) void p_mv_refine(PRefineArgs a) {
   const Geom& g = a.g;
   const int nmb = g.nmb();
-  const int mb = blockIdx.x, slot = blockIdx.y, lane = threadIdx.x;
+  int mb, slot;
+  xcd_unit_slot(mb, slot);
+  const int lane = threadIdx.x;
   const size_t o = static_cast<size_t>(slot) * nmb + mb;
   const int mx = mb % g.wmb, my = mb / g.wmb;
   const int16_t* mv = a.mv_in + static_cast<size_t>(slot) * nmb * 2;

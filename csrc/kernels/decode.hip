@@ -179,7 +179,8 @@ constexpr int kBW = 9;  // 4x4 block + 6-tap support (-2 .. +6)
 
 __global__ __launch_bounds__(64) void decode_inter_dpb(DecodeArgs a) {
   const Geom& g = a.g;
-  const int mb = blockIdx.x, slot = blockIdx.y;
+  int mb, slot;
+  xcd_unit_slot(mb, slot);
   if (a.run[slot] != 2) return;
   const size_t o = static_cast<size_t>(slot) * g.nmb() + mb;
   const MbHeader* H = a.hdr + o;

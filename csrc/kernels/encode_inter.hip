@@ -109,7 +109,9 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
   const Geom& g = a.g;
   const int lane = threadIdx.x, half = lane >> 5, hl = lane & 31;
   const int nmb = g.nmb();
-  const int mb = blockIdx.x * 2 + half, slot = blockIdx.y;
+  int ux, slot;
+  xcd_unit_slot(ux, slot);
+  const int mb = ux * 2 + half;
   const bool live = mb < nmb;
   const int mbc = live ? mb : nmb - 1;
   const int mx = mbc % g.wmb, my = mbc / g.wmb;

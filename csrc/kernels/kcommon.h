@@ -188,6 +188,18 @@ __device__ __forceinline__ int min64(int v) {
 // holds row y in v[0..3].  Row passes are in-register, column passes exchange the
 // group's rows with DPP quad broadcasts.  Every lane of the wave must execute these
 // (uniform control flow) because shuffles read other lanes' registers.
+// XCD-aware workgroup order for (x = unit within a slot, y = slot) grids: the hardware
+// deals workgroups round-robin over the 8 XCDs, so consecutive units (neighbouring MBs,
+// whose reference rows overlap) would land on 8 different L2s and every cache line would
+// be fetched 8 times; remap so each XCD walks one contiguous eighth of the grid.
+__device__ __forceinline__ void xcd_unit_slot(int& x, int& y) {
+  const int gx = static_cast<int>(gridDim.x), total = gx * static_cast<int>(gridDim.y);
+  int lin = static_cast<int>(blockIdx.y) * gx + static_cast<int>(blockIdx.x);
+  if ((total & 7) == 0) lin = (lin & 7) * (total >> 3) + (lin >> 3);
+  y = lin / gx;
+  x = lin - y * gx;
+}
+
 __device__ __forceinline__ int sel4(int y, int a, int b, int c, int d) { return y == 0 ? a : (y == 1 ? b : (y == 2 ? c : d)); }
 
 // forward integer core transform (encoder side)
