@@ -372,8 +372,8 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   // K, CX, RY (V: CX = 32 top, H: RY = 32 left, DC: K = 32 dc + 16, plane: the linear
   // form); the neighbour sums behind DC and plane are row reductions of the neighbour
   // registers (H = sum (t - 7) top[t] - 8 tl, V alike).
-  int intra_key;
-  {
+  int intra_key = 0x3FFFFFFF;
+  if (a.out_intra_cost) {  // null: the caller already has this picture's estimate (B pictures' L1 search)
     const int mode = lane >> 4;
     const bool has_top = my > 0, has_left = mx > 0;
     const bool ok = (mode == 0 && has_top) || (mode == 1 && has_left) || mode == 2 || (mode == 3 && has_top && has_left);
@@ -638,7 +638,7 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
     a.out_mv[o * 2] = static_cast<int16_t>(best_mvx);
     a.out_mv[o * 2 + 1] = static_cast<int16_t>(best_mvy);
     a.out_cost[o] = best_cost;
-    a.out_intra_cost[o] = intra_key + lambda * 4;
+    if (a.out_intra_cost) a.out_intra_cost[o] = intra_key + lambda * 4;
   }
   MPROF(9);
 }

@@ -72,6 +72,9 @@ class H264Params:
     # Jacobi passes of the P_Skip-aware vector choice after ME (csrc/kernels/bframe.hip
     # p_mv_refine): 0 disables
     skip_refine: int = int(os.environ.get("MIVC_SKIP_REFINE", 2))
+    # deblock non-reference B pictures even when neither metrics nor the reconstruction
+    # are requested (x264 --full-recon); the bitstream does not depend on it
+    full_recon: bool = False
 
     def eff_bframes(self) -> int:
         return max(0, int(self.bframes)) if self.cabac else 0
@@ -448,8 +451,9 @@ class GpuH264Encoder:
                 self.hip.b_direct(B, wmb, hmb, P(self.col_hdr), dsf, copy, P(self.dmv), P(self.pm0), P(self.pm1), s)
                 self.hip.me(B, wmb, hmb, sy, f0y, P(self.pm0), P(self.mv), P(self.me_cost), P(self.pred),
                             P(self.intra_cost), P(self.qp), br, self.p.subpel, s, hp0, aq, 1)
+                # the L1 search skips the open-loop intra estimate the L0 search just wrote
                 self.hip.me(B, wmb, hmb, sy, f1y, P(self.pm1), P(self.mv1), P(self.me_cost1), P(self.pred1),
-                            P(self.intra_cost), P(self.qp), br, self.p.subpel, s, hp1, aq, 1)
+                            0, P(self.qp), br, self.p.subpel, s, hp1, aq, 1)
             with st("b_decide"):
                 self.hip.b_decide(B, wmb, hmb, sy, f0y, f1y, hp0, hp1, P(self.mv), P(self.mv1), P(self.me_cost),
                                   P(self.me_cost1), P(self.pred), P(self.pred1), P(self.pm0), P(self.pm1),
@@ -474,7 +478,12 @@ class GpuH264Encoder:
             # MBs without mb_qp_delta take QP_pred (clause 7.4.5): their records must say so
             # before deblocking reads every MB's QP
             self.hip.qp_fixup(B, wmb, hmb, P(hdr), P(coef), P(self.nz), P(self.qp_flags), P(self.qp), s)
-        if self.p.deblock:
+        # A non-reference B picture's reconstruction feeds nothing but its own intra MBs
+        # (which predict from unfiltered samples), so its in-loop filter only matters when
+        # someone looks at the picture: metrics (PSNR / SSIM) or keep_recon.  The bitstream
+        # is identical either way (cf. x264, which reconstructs non-reference frames fully
+        # only with --full-recon).
+        if self.p.deblock and (pic.kind != "B" or self._full_recon):
             with st("deblock"):
                 self.hip.deblock(B, wmb, hmb, ry, ru, rv, P(hdr), P(self.nz), cqo, 0, 0, P(self.err), s)
         if pic.kind != "B":
@@ -748,6 +757,7 @@ class GpuH264Encoder:
             raise ValueError("u/v must be [B, F, h/2, w/2] with even h, w")
         if not (y.is_contiguous() and u.is_contiguous() and v.is_contiguous()):
             raise ValueError("planes must be contiguous")
+        self._full_recon = bool(metrics or keep_recon or self.p.full_recon)
         if (w, h) != (self.p.width, self.p.height):  # -s WxH: bicubic resample (ops/scale.py)
             if getattr(self, "_scaler", None) is None:
                 from ..ops.scale import GpuScaler

@@ -259,3 +259,15 @@ def test_gpu_short_segment_display_prefix(host):
     for t, pic in enumerate(pics):
         assert np.array_equal(pic["y_coded"], enc.last_recon[t][0][1].cpu().numpy())
     enc.close()
+
+
+def test_nonref_b_deblock_skip_keeps_bytes():
+    """Without metrics / keep_recon the non-reference B pictures skip the in-loop filter;
+    the bitstream must not change (nothing predicts from them)."""
+    from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
+    enc = GpuH264Encoder(H264Params(width=176, height=144, crf=24, bframes=3), slots=2)
+    y, u, v = synth_clip(2, 9, 176, 144, seed=8)
+    a = enc.encode(y, u, v, metrics=True)
+    b = enc.encode(y, u, v, metrics=False)
+    enc.close()
+    assert [r.bitstream for r in a] == [r.bitstream for r in b]
