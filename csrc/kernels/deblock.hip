@@ -238,7 +238,8 @@ __global__ __launch_bounds__(64 * kDeblockWaves) void deblock_wavefront(DeblockA
             const int rq = dir == 0 ? (e + 4 * k) : (k + 4 * e);
             const int rp = dir == 0 ? (mbedge ? 3 + 4 * k : e - 1 + 4 * k) : (mbedge ? k + 12 : k + 4 * (e - 1));
             const bool iq = h264::mbk_is_intra(HQ->kind), ip = h264::mbk_is_intra(HP->kind);
-            if (mbedge && (iq || ip)) bs = 4;
+            if ((e & 1) && (HQ->flags & h264::MBF_T8x8)) bs = 0;  // 8x8 transform: no 4-sample inner edges
+            else if (mbedge && (iq || ip)) bs = 4;
             else if (iq || ip) bs = 3;
             else if (nzbp[rp] || nzb0[rq]) bs = 2;
             else {

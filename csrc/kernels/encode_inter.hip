@@ -38,7 +38,77 @@ struct InterArgs {
   // (list 1), averaged for bi-prediction; pred_y is b_decide's luma prediction
   const uint8_t *ref1_u, *ref1_v;
   int bmode;
+  int t8;                  // High profile: choose the 8x8 transform per MB (sa8d < satd, as x264)
 };
+
+// ---------------------------------------------------------------- 8x8 transform (High)
+// position class of an 8x8 coefficient (normAdjust8x8 / quant8 column, 8.5.9)
+__device__ __forceinline__ int pos8(int x, int y) {
+  if ((x & 3) == 0 && (y & 3) == 0) return 0;
+  if ((x & 1) && (y & 1)) return 1;
+  if ((x & 3) == 2 && (y & 3) == 2) return 2;
+  if (((x & 3) == 0 && (y & 1)) || ((x & 1) && (y & 3) == 0)) return 3;
+  if (((x & 3) == 0 && (y & 3) == 2) || ((x & 3) == 2 && (y & 3) == 0)) return 4;
+  return 5;
+}
+__constant__ int kQuant8MF[6][6] = {{13107, 11428, 20972, 12222, 16777, 15481}, {11916, 10826, 19174, 11058, 14980, 14290},
+                                   {10082, 8943, 15978, 9675, 12710, 11985},   {9362, 8228, 14913, 8931, 11984, 11259},
+                                   {8192, 7346, 13159, 7740, 10486, 9777},     {7282, 6428, 11570, 6830, 9118, 8640}};
+__constant__ int kNorm8[6][6] = {{20, 18, 32, 19, 25, 24}, {22, 19, 35, 21, 28, 26}, {26, 23, 42, 24, 33, 31},
+                                {28, 25, 45, 26, 35, 33}, {32, 28, 51, 30, 40, 38}, {36, 32, 58, 34, 46, 43}};
+__constant__ uint8_t kZz8[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
+                                 41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
+                                 30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+// forward 8-point core transform (the inverse of 8.5.13.2), in place, stride s
+__device__ __forceinline__ void dct8_pass(int* d, int s) {
+  const int a0 = d[0] + d[7 * s], a1 = d[s] + d[6 * s], a2 = d[2 * s] + d[5 * s], a3 = d[3 * s] + d[4 * s];
+  const int a4 = d[0] - d[7 * s], a5 = d[s] - d[6 * s], a6 = d[2 * s] - d[5 * s], a7 = d[3 * s] - d[4 * s];
+  const int b0 = a0 + a3, b1 = a1 + a2, b2 = a0 - a3, b3 = a1 - a2;
+  const int b4 = a5 + a6 + ((a4 >> 1) + a4), b5 = a4 - a7 - ((a6 >> 1) + a6);
+  const int b6 = a4 + a7 - ((a5 >> 1) + a5), b7 = a5 - a6 + ((a7 >> 1) + a7);
+  d[0] = b0 + b1;
+  d[4 * s] = b0 - b1;
+  d[2 * s] = b2 + (b3 >> 1);
+  d[6 * s] = (b2 >> 1) - b3;
+  d[s] = b4 + (b7 >> 2);
+  d[7 * s] = (b4 >> 2) - b7;
+  d[3 * s] = b5 + (b6 >> 2);
+  d[5 * s] = b6 - (b5 >> 2);
+}
+// inverse 8-point pass (8.5.13.2), in place, stride s
+__device__ __forceinline__ void idct8_pass(int* d, int s) {
+  const int d0 = d[0], d1 = d[s], d2 = d[2 * s], d3 = d[3 * s], d4 = d[4 * s], d5 = d[5 * s], d6 = d[6 * s],
+            d7 = d[7 * s];
+  const int a0 = d0 + d4, a4 = d0 - d4, a2 = (d2 >> 1) - d6, a6 = d2 + (d6 >> 1);
+  const int b0 = a0 + a6, b2 = a4 + a2, b4 = a4 - a2, b6 = a0 - a6;
+  const int a1 = -d3 + d5 - d7 - (d7 >> 1), a3 = d1 + d7 - d3 - (d3 >> 1);
+  const int a5 = -d1 + d7 + d5 + (d5 >> 1), a7 = d3 + d5 + d1 + (d1 >> 1);
+  const int b1 = a1 + (a7 >> 2), b7 = a7 - (a1 >> 2), b3 = a3 + (a5 >> 2), b5 = (a3 >> 2) - a5;
+  d[0] = b0 + b7;
+  d[s] = b2 + b5;
+  d[2 * s] = b4 + b3;
+  d[3 * s] = b6 + b1;
+  d[4 * s] = b6 - b1;
+  d[5 * s] = b4 - b3;
+  d[6 * s] = b2 - b5;
+  d[7 * s] = b0 - b7;
+}
+// 8-point Hadamard pass (sa8d), in place, stride s
+__device__ __forceinline__ void had8_pass(int* d, int s) {
+  const int a0 = d[0] + d[s], a1 = d[0] - d[s], a2 = d[2 * s] + d[3 * s], a3 = d[2 * s] - d[3 * s];
+  const int a4 = d[4 * s] + d[5 * s], a5 = d[4 * s] - d[5 * s], a6 = d[6 * s] + d[7 * s], a7 = d[6 * s] - d[7 * s];
+  const int b0 = a0 + a2, b1 = a1 + a3, b2 = a0 - a2, b3 = a1 - a3;
+  const int b4 = a4 + a6, b5 = a5 + a7, b6 = a4 - a6, b7 = a5 - a7;
+  d[0] = b0 + b4;
+  d[s] = b1 + b5;
+  d[2 * s] = b2 + b6;
+  d[3 * s] = b3 + b7;
+  d[4 * s] = b0 - b4;
+  d[5 * s] = b1 - b5;
+  d[6 * s] = b2 - b6;
+  d[7 * s] = b3 - b7;
+}
 
 // Eighth-sample chroma prediction (clause 8.4.2.2.2) of a 4x4 block at (px0, py0) of a
 // cw x ch plane with vector (mvx, mvy) (quarter-luma = eighth-chroma units).
@@ -137,6 +207,13 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
   __shared__ int s_cdc[2][2][4];
   __shared__ int s_clev[2][2][4];
   __shared__ int s_flags[2][2];  // [half][0] luma 8x8 keep mask, [1] chroma AC keep mask (bit per comp)
+  // 8x8 transform path (a.t8): residual copies for the sa8d Hadamard and the transform,
+  // the 8x8 levels in scan order, per-block cost terms
+  __shared__ int s_h8[2][4][64];
+  __shared__ int s_d8[2][4][64];
+  __shared__ int16_t s_l8[2][4][64];
+  __shared__ int s_cost[2][2][16];   // [half][0: satd per 4x4 lane, 1: sa8d partial per (b8, k)]
+  __shared__ int s_t8[2][2];         // [half][0] use 8x8, [1] keep mask of the 8x8 blocks
 
   const int mvx = a.bmode ? 0 : a.mv[o * 2], mvy = a.bmode ? 0 : a.mv[o * 2 + 1];
   const bool go_intra = a.intra_cost[o] < a.me_cost[o];
@@ -174,14 +251,112 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
       for (int x = 0; x < 4; ++x)
         res[y * 4 + x] = static_cast<int>(__builtin_amdgcn_ubfe(sw[y], 8 * x, 8)) -
                          static_cast<int>(__builtin_amdgcn_ubfe(prw[y], 8 * x, 8));
-    h264::forward_core4x4(res);
-    const int qbits = 15 + qp / 6;
+    bool use8 = false;
+    if (a.t8) {
+      // transform size first (x264 analyse: sa8d of the residual < satd -> 8x8), so only the
+      // chosen transform is quantised; lanes hl = b8 * 4 + k run the 8-point passes
+      const int b8 = (lby >> 3) * 2 + (lbx >> 3), ox = lbx & 4, oy = lby & 4;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) lv[r] = h264::quant_coef(res[r], mf[h264::kPosClass[r]], qbits, 11);
-    int scan[16];
+      for (int y = 0; y < 4; ++y)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) scan[i] = lv[h264::kZigzag4x4[i]];
-    s_score[half][hl] = decimate_score(scan, 0);
+        for (int x = 0; x < 4; ++x) {
+          s_h8[half][b8][(oy + y) * 8 + ox + x] = res[y * 4 + x];
+          s_d8[half][b8][(oy + y) * 8 + ox + x] = res[y * 4 + x];
+        }
+      s_cost[half][0][hl] = h264::satd4x4(res);
+      wave_sync();
+      const int tb = hl >> 2, k = hl & 3;
+      int* hd = s_h8[half][tb];
+      had8_pass(hd + (2 * k) * 8, 1);
+      had8_pass(hd + (2 * k + 1) * 8, 1);
+      wave_sync();
+      had8_pass(hd + 2 * k, 8);
+      had8_pass(hd + 2 * k + 1, 8);
+      wave_sync();
+      int sa = 0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sa += abs(hd[k * 16 + i]);
+      s_cost[half][1][hl] = sa;
+      wave_sync();
+      if (hl == 0) {
+        int satd = 0, sa8d = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) satd += s_cost[half][0][i];
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          sa8d += (s_cost[half][1][b * 4] + s_cost[half][1][b * 4 + 1] + s_cost[half][1][b * 4 + 2] +
+                   s_cost[half][1][b * 4 + 3] + 2) >> 2;
+        s_t8[half][0] = sa8d < satd;
+      }
+      wave_sync();
+      use8 = s_t8[half][0] != 0;
+    }
+    if (!use8) {
+      h264::forward_core4x4(res);
+      const int qbits = 15 + qp / 6;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) lv[r] = h264::quant_coef(res[r], mf[h264::kPosClass[r]], qbits, 11);
+      int scan[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) scan[i] = lv[h264::kZigzag4x4[i]];
+      s_score[half][hl] = decimate_score(scan, 0);
+    } else {
+      // ---- 8x8 transform: forward passes, quantisation of scan positions 16k .. 16k + 15
+      // with this chunk's share of x264's decimate_score64 (zero runs priced 3 / 2 / 1 / 0;
+      // 9 once any |level| > 1): runs inside the chunk here, the run into its first
+      // non-zero level from the previous chunks' last
+      const int tb = hl >> 2, k = hl & 3;
+      int* dd = s_d8[half][tb];
+      dct8_pass(dd + (2 * k) * 8, 1);
+      dct8_pass(dd + (2 * k + 1) * 8, 1);
+      wave_sync();
+      dct8_pass(dd + 2 * k, 8);
+      dct8_pass(dd + 2 * k + 1, 8);
+      wave_sync();
+      const int qbits8 = 16 + qp / 6;
+      const int m = qp % 6;
+      int lastnz = -1, firstnz = -1, inner = 0;
+      bool big = false;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int idx = k * 16 + i;
+        const int pos = kZz8[idx];
+        const int mf8 = kQuant8MF[m][pos8(pos & 7, pos >> 3)];
+        const int v = h264::quant_coef(dd[pos], mf8, qbits8, 11);
+        s_l8[half][tb][idx] = static_cast<int16_t>(v);
+        const bool nzv = v != 0;
+        big |= v > 1 || v < -1;
+        const int run = idx - lastnz - 1;
+        inner += (nzv && firstnz >= 0) ? (run <= 3 ? 3 : (run <= 11 ? 2 : (run <= 23 ? 1 : 0))) : 0;
+        firstnz = (nzv && firstnz < 0) ? idx : firstnz;
+        lastnz = nzv ? idx : lastnz;
+      }
+      int* stat = &s_h8[half][tb][16 * k];  // the Hadamard copy is spent: reuse it
+      wave_sync();
+      stat[0] = lastnz;
+      wave_sync();
+      int prev = -1;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) prev = (j < k) ? max(prev, s_h8[half][tb][16 * j]) : prev;
+      const int run0 = firstnz - prev - 1;
+      const int sc = inner + (firstnz >= 0 ? (run0 <= 3 ? 3 : (run0 <= 11 ? 2 : (run0 <= 23 ? 1 : 0))) : 0);
+      wave_sync();
+      stat[1] = sc;
+      stat[2] = big;
+      wave_sync();
+      if (hl == 0) {
+        int keep = 0, total = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int* st0 = s_h8[half][b];
+          const int scb = (st0[2] | st0[18] | st0[34] | st0[50]) ? 9 : (st0[1] + st0[17] + st0[33] + st0[49]);
+          if (scb >= 4) keep |= 1 << b;
+          total += scb;
+        }
+        if (total < 6) keep = 0;
+        s_t8[half][1] = keep;
+      }
+    }
   } else if (work && hl < 24) {
     // ---- chroma block: eighth-sample MC (clause 8.4.2.2.2) + residual + forward + AC quant
     const uint8_t* srcc = (comp == 0 ? a.src_u : a.src_v) + slot * g.csize();
@@ -261,7 +436,48 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
     reinterpret_cast<uint4*>(dst)[0] = make_uint4(w[0], w[1], w[2], w[3]);
     reinterpret_cast<uint4*>(dst)[1] = make_uint4(w[4], w[5], w[6], w[7]);
   };
-  if (hl < 16) {
+  const bool use8 = a.t8 && s_t8[half][0];
+  if (hl < 16 && use8) {
+    // ---- 8x8 transform: levels in 8x8 scan order (chunk k of block b8), dequantise into
+    // the transform buffer, inverse 8x8 (lanes on rows / columns 2k, 2k + 1), then every 4x4
+    // lane adds its part of the residual to the prediction
+    const int b8 = hl >> 2, k = hl & 3;
+    const bool keep = (s_t8[half][1] >> b8) & 1;
+    int sv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sv[i] = keep ? s_l8[half][b8][k * 16 + i] : 0;
+    store_levels(coef + h264::COEF_LUMA + b8 * 64 + k * 16, sv);
+    int* dd = s_d8[half][b8];
+    const int m = qp % 6, q6 = qp / 6;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int pos = kZz8[k * 16 + i];
+      const int ls = 16 * kNorm8[m][pos8(pos & 7, pos >> 3)];
+      const int c = sv[i];
+      dd[pos] = q6 >= 6 ? (c * ls) << (q6 - 6) : (c * ls + (1 << (5 - q6))) >> (6 - q6);
+    }
+    wave_sync();
+    idct8_pass(dd + (2 * k) * 8, 1);
+    idct8_pass(dd + (2 * k + 1) * 8, 1);
+    wave_sync();
+    idct8_pass(dd + 2 * k, 8);
+    idct8_pass(dd + 2 * k + 1, 8);
+    wave_sync();
+    const int lb8 = (lby >> 3) * 2 + (lbx >> 3), ox = lbx & 4, oy = lby & 4;
+    const bool any8 = (s_t8[half][1] >> lb8) & 1;
+    uint8_t* recy = a.rec_y + slot * g.ysize() + static_cast<size_t>(Y0 + lby) * W + X0 + lbx;
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      int v4[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const int r8 = any8 ? (s_d8[half][lb8][(oy + y) * 8 + ox + x] + 32) >> 6 : 0;
+        v4[x] = h264::clip1(static_cast<int>(__builtin_amdgcn_ubfe(prw[y], 8 * x, 8)) + r8);
+      }
+      *reinterpret_cast<uint32_t*>(recy + static_cast<size_t>(y) * W) = pack4_u8(v4);
+    }
+    a.nz[o * 16 + (lbx >> 2) + lby] = any8;
+  } else if (hl < 16) {
     const bool keep = (s_flags[half][0] >> (hl >> 2)) & 1;
     int sv[16];
     bool any = false;
@@ -326,7 +542,8 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
     h->qp = static_cast<int8_t>(qp);
     h->i16_mode = 0;
     h->chroma_mode = 0;
-    h->flags = 0;
+    // transform_size_8x8_flag is only coded (and only matters) when luma levels exist
+    h->flags = (use8 && s_t8[half][1]) ? h264::MBF_T8x8 : 0;
     a.intra_flag[o] = 0;
     if (a.bmode) return;  // kind / ref / mv are b_decide's
     h->kind = h264::MBK_P16x16;
@@ -349,7 +566,7 @@ extern "C" void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t*
                                          const int* intra_cost, const int* qp, int chroma_qp_offset, void* hdr,
                                          int16_t* coef, uint8_t* nz, uint8_t* intra_flag, int* intra_count,
                                          const int8_t* aq, const uint8_t* ref1_u, const uint8_t* ref1_v, int bmode,
-                                         void* stream) {
+                                         int t8, void* stream) {
   InterArgs a;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.src_y = src_y;
@@ -376,5 +593,6 @@ extern "C" void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t*
   a.ref1_u = ref1_u;
   a.ref1_v = ref1_v;
   a.bmode = bmode;
+  a.t8 = t8;
   hipLaunchKernelGGL(encode_inter_mb, dim3((wmb * hmb + 1) / 2, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
 }

@@ -97,7 +97,8 @@ def cmd_encode(a) -> int:
         return subprocess.call(argv)
     from .pipeline import encode_file
     encode_file(a.input, a.output, args=a.ff, backend=a.backend, slots=a.slots, seg_frames=a.seg_frames,
-                schedule=a.schedule, raw_size=_wh(a.raw_size) if a.raw_size else None, fps=a.fps)
+                schedule=a.schedule, raw_size=_wh(a.raw_size) if a.raw_size else None, fps=a.fps,
+                resume=a.resume, work_dir=a.work_dir)
     return 0
 
 
@@ -227,6 +228,8 @@ def build_parser() -> argparse.ArgumentParser:
     en.add_argument("--schedule", default="static", choices=["static", "dynamic"])
     en.add_argument("--raw-size", default=None)
     en.add_argument("--fps", type=float, default=30.0)
+    en.add_argument("--resume", action="store_true", help="checkpoint every segment; skip finished ones on restart")
+    en.add_argument("--work-dir", default=None, help="checkpoint directory (default <output>.parts)")
     en.set_defaults(fn=cmd_encode)
 
     fl = sub.add_parser("fleet", help="launch / list / stop local GPU workers")

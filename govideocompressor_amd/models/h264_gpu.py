@@ -72,6 +72,9 @@ class H264Params:
     # Jacobi passes of the P_Skip-aware vector choice after ME (csrc/kernels/bframe.hip
     # p_mv_refine): 0 disables
     skip_refine: int = int(os.environ.get("MIVC_SKIP_REFINE", 2))
+    # x264 --8x8dct (default on): High profile, the 8x8 transform chosen per inter MB where
+    # its sa8d beats the 4x4 satd; CABAC only (the CAVLC path stays Constrained Baseline)
+    t8x8: bool = True
     # deblock non-reference B pictures even when neither metrics nor the reconstruction
     # are requested (x264 --full-recon); the bitstream does not depend on it
     full_recon: bool = False
@@ -79,16 +82,19 @@ class H264Params:
     def eff_bframes(self) -> int:
         return max(0, int(self.bframes)) if self.cabac else 0
 
+    def eff_t8x8(self) -> bool:
+        return bool(self.t8x8 and self.cabac)
+
     def host_cfg(self) -> dict:
         return dict(width=self.width, height=self.height, fps=self.fps, qp=self.qp,
                     deblock=int(self.deblock), chroma_qp_offset=self.chroma_qp_offset,
-                    vui=int(self.vui), cabac=int(self.cabac), bframes=self.eff_bframes())
+                    vui=int(self.vui), cabac=int(self.cabac), bframes=self.eff_bframes(), t8x8=int(self.eff_t8x8()))
 
     def profile_name(self) -> str:
         if not self.cabac:
             return "Constrained Baseline CAVLC"
         nb = self.eff_bframes()
-        return "Main CABAC" + (f" {nb}B temporal-direct" if nb else "")
+        return ("High CABAC 8x8dct" if self.eff_t8x8() else "Main CABAC") + (f" {nb}B temporal-direct" if nb else "")
 
     def frame_qps(self) -> tuple[int, int]:
         """(qp_I, qp_P).  CRF maps to the P-frame QP (x264 scale without MB-tree);
@@ -438,7 +444,8 @@ class GpuH264Encoder:
             with st("inter"):
                 self.hip.encode_inter(B, wmb, hmb, sy, su, sv, fy, fu, fv, ry, ru, rv, P(self.pred), P(self.mv),
                                       P(self.me_cost), P(self.intra_cost), P(self.qp), cqo, P(hdr), P(coef),
-                                      P(self.nz), P(self.intra_flag), P(self.intra_count), s, aq)
+                                      P(self.nz), P(self.intra_flag), P(self.intra_count), s, aq,
+                                      t8=int(self.p.eff_t8x8()))
             self.prev_mv.copy_(self.mv)
         elif pic.kind == "B":
             f0y, f0u, f0v = (P(x) for x in ref0)
@@ -463,7 +470,8 @@ class GpuH264Encoder:
             with st("inter"):
                 self.hip.encode_inter(B, wmb, hmb, sy, su, sv, f0y, f0u, f0v, ry, ru, rv, P(self.pred_b), P(self.mv),
                                       P(self.cost_b), P(self.intra_cost), P(self.qp), cqo, P(hdr), P(coef),
-                                      P(self.nz), P(self.intra_flag), P(self.intra_count), s, aq, f1u, f1v, 1)
+                                      P(self.nz), P(self.intra_flag), P(self.intra_count), s, aq, f1u, f1v, 1,
+                                      int(self.p.eff_t8x8()))
         if pic.kind != "I":
             self.p_intra_mbs += self.intra_count.sum()
             flag_ptr, count_ptr = P(self.intra_flag), P(self.intra_count)
@@ -531,7 +539,7 @@ class GpuH264Encoder:
         self.hip.cabac_bin(B, self.wmb, self.hmb, P(self.hdr[k]), P(self.coef[k]), P(self.cab_mask), P(self.cab_nb),
                            P(self.cab_cnt), P(self.cab_off), P(self.cab_tot), P(self.cab_pool[r]), self.cab_pool_cap,
                            self.cab_pool_used[r].data_ptr(), self.cab_base[r][j * B:].data_ptr(),
-                           self.cab_total[r][j * B:].data_ptr(), P(qp_dev), pic.slice_type, 1, 1, 0, P(self.err),
+                           self.cab_total[r][j * B:].data_ptr(), P(qp_dev), pic.slice_type, 1, 1, int(self.p.eff_t8x8()), P(self.err),
                            self.copy_stream.cuda_stream)
 
     def _gpu_cabac_code(self, g: int, t0: int, n: int, qps_d: torch.Tensor):

@@ -60,9 +60,77 @@ def _load_segment(path: str, info, kind: str, segs, i: int) -> yuv.Clip:
     return yuv.read_yuv(path, info.width, info.height, info.fps, info.bit_depth, s, c)
 
 
+class SegmentCheckpoint:
+    """Per-segment checkpoint of ``encode_file(resume=True)``: every encoded
+    segment is written to ``<work_dir>/<idx>.seg`` (atomic rename) and recorded in this
+    rank's ``manifest.rank<r>.json`` (size + CRC32); a restarted run with the same input
+    plan and arguments skips the segments every manifest already holds, and rank 0
+    concatenates the finished parts.  A plan or argument change invalidates the checkpoint."""
+
+    def __init__(self, work_dir: str, rank: int, sig: dict):
+        self.dir = work_dir
+        self.rank = rank
+        self.sig = sig
+        os.makedirs(work_dir, exist_ok=True)
+        self.mine: dict[str, dict] = {}
+
+    def _manifests(self):
+        return sorted(f for f in os.listdir(self.dir) if f.startswith("manifest.rank") and f.endswith(".json"))
+
+    def done(self) -> dict[int, dict]:
+        """Segments finished by any rank of an earlier run with the same plan (file checked)."""
+        import zlib
+        out = {}
+        for f in self._manifests():
+            try:
+                with open(os.path.join(self.dir, f)) as fh:
+                    m = json.load(fh)
+            except (OSError, ValueError):
+                continue
+            if m.get("sig") != self.sig:
+                continue
+            for k, v in m.get("done", {}).items():
+                pth = os.path.join(self.dir, f"{int(k)}.seg")
+                try:
+                    with open(pth, "rb") as fh:
+                        data = fh.read()
+                except OSError:
+                    continue
+                if len(data) == v["bytes"] and zlib.crc32(data) == v["crc"]:
+                    out[int(k)] = v
+        return out
+
+    def put(self, idx: int, data: bytes) -> None:
+        import zlib
+        pth = os.path.join(self.dir, f"{idx}.seg")
+        with open(pth + ".part", "wb") as fh:
+            fh.write(data)
+        os.replace(pth + ".part", pth)
+        self.mine[str(idx)] = {"bytes": len(data), "crc": zlib.crc32(data)}
+        mpath = os.path.join(self.dir, f"manifest.rank{self.rank}.json")
+        try:
+            with open(mpath) as fh:
+                old = json.load(fh)
+            if old.get("sig") == self.sig:
+                merged = {**old.get("done", {}), **self.mine}
+            else:
+                merged = dict(self.mine)
+        except (OSError, ValueError):
+            merged = dict(self.mine)
+        with open(mpath + ".part", "w") as fh:
+            json.dump({"sig": self.sig, "done": merged}, fh)
+        os.replace(mpath + ".part", mpath)
+
+    def read(self, idx: int) -> bytes:
+        with open(os.path.join(self.dir, f"{idx}.seg"), "rb") as fh:
+            return fh.read()
+
+
 def encode_file(path: str, output: str, args: str = "264", backend: str = "auto", slots: int = 16,
                 seg_frames: int | None = None, schedule: str = "static", raw_size: tuple[int, int] | None = None,
-                fps: float = 30.0, log=print) -> dict:
+                fps: float = 30.0, log=print, resume: bool = False, work_dir: str | None = None) -> dict:
+    """Encode one file on this node's ranks.  ``resume``: keep a per-segment checkpoint in
+    ``work_dir`` (default ``<output>.parts``) and skip the segments it already holds."""
     env = D.init(prefer_gpu=(backend in ("auto", "gpu")))
     cfg = ffargs.parse(args)
     w, h = raw_size or (0, 0)
@@ -73,6 +141,16 @@ def encode_file(path: str, output: str, args: str = "264", backend: str = "auto"
     sig0 = D.broadcast_object(env, sig)
     if sig0 != sig:
         raise RuntimeError(f"rank {env.rank}: segment plan differs from rank 0 ({sig} vs {sig0})")
+    ckpt = None
+    skip: set[int] = set()
+    if resume:
+        if cfg.bitrate is not None:
+            raise ValueError("resume is for CRF / QP encodes: -b:v solves one offset over the whole file")
+        plan_sig = {"input": os.path.abspath(path), "size": os.path.getsize(path), "args": args, "plan": list(sig),
+                    "seg_frames": seg_frames, "world": env.world, "slots": slots}
+        ckpt = SegmentCheckpoint(work_dir or output + ".parts", env.rank, plan_sig)
+        D.barrier(env)
+        skip = set(ckpt.done())
     be = get_backend(backend, **({"device": str(env.device)} if backend in ("gpu",) or
                                  (backend == "auto" and env.device.type == "cuda") else {}))
     impl = be.impl
@@ -102,6 +180,8 @@ def encode_file(path: str, output: str, args: str = "264", backend: str = "auto"
             stream, st = res[str(i)]
             (mine if into is None else into)[i] = stream
             stats.append(st)
+            if ckpt is not None:
+                ckpt.put(i, stream)
 
     rate = None
     if cfg.bitrate is not None and hasattr(impl, "decode_streams"):
@@ -138,12 +218,15 @@ def encode_file(path: str, output: str, args: str = "264", backend: str = "auto"
             got = td.claim(slots)
             if not got:
                 break
-            run(got)
+            got = [i for i in got if i not in skip]
+            if got:
+                run(got)
     elif rate is None:
         if kind == "ranges":
             my = P.shard(segs, env.rank, env.world, by_cost=True)
         else:
             my = list(range(env.rank, n, env.world))
+        my = [i for i in my if i not in skip]
         for b in range(0, len(my), slots):
             run(my[b:b + slots])
     t_enc = time.perf_counter() - t0
@@ -152,7 +235,7 @@ def encode_file(path: str, output: str, args: str = "264", backend: str = "auto"
     idx_blob = json.dumps(order).encode()
     g = D.BitstreamGather(env, [idx_blob] + [mine[i] for i in order]).start()
     gathered = g.wait()
-    out = {"segments": n, "world": env.world, "encode_s_rank": t_enc, "rate": rate,
+    out = {"segments": n, "world": env.world, "encode_s_rank": t_enc, "rate": rate, "resumed_segments": len(skip),
            "decode": ("gpu" if gpu_decode else "cpu"), "decode_stats_rank": dec_stats}
     if env.is_main:
         by_idx: dict[int, bytes] = {}
@@ -160,6 +243,9 @@ def encode_file(path: str, output: str, args: str = "264", backend: str = "auto"
             ids = json.loads(rank_pieces[0].decode())
             for i, pc in zip(ids, rank_pieces[1:]):
                 by_idx[i] = pc
+        for i in skip:  # finished by an earlier (interrupted) run
+            if i not in by_idx:
+                by_idx[i] = ckpt.read(i)
         missing = [i for i in range(n) if i not in by_idx]
         if missing:
             raise RuntimeError(f"segments never encoded: {missing[:8]}")

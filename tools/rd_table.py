@@ -8,7 +8,8 @@ import sys
 
 import numpy as np
 
-CFGS = [("bframes3", "Main CABAC + 3 B (temporal direct)"), ("bframes0", "Main CABAC, P only"),
+CFGS = [("bframes3", "High CABAC 8x8dct + 3 B (temporal direct)"),
+        ("bframes3no8x8dct", "Main CABAC + 3 B (temporal direct)"), ("bframes0no8x8dct", "Main CABAC, P only"),
         ("bframes0cavlc", "Constrained Baseline CAVLC (round 1)")]
 CRFS = [18, 23, 28, 33]
 
@@ -52,9 +53,10 @@ def main():
     base = data["bframes0cavlc"]
     print("\n| encoder | BD-rate vs round-1 Baseline CAVLC (PSNR-Y) |")
     print("|---|---|")
-    for tag, name in CFGS[:2]:
+    for tag, name in CFGS[:3]:
         print(f"| {name} | {bd_rate(base, data[tag]):+.1f} % |")
-    print(f"| Main CABAC + 3 B vs Main CABAC P only | {bd_rate(data['bframes0'], data['bframes3']):+.1f} % |")
+    print(f"| High 8x8dct + 3 B vs Main + 3 B | {bd_rate(data['bframes3no8x8dct'], data['bframes3']):+.1f} % |")
+    print(f"| Main + 3 B vs Main P only | {bd_rate(data['bframes0no8x8dct'], data['bframes3no8x8dct']):+.1f} % |")
 
 
 if __name__ == "__main__":
