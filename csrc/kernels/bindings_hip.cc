@@ -19,7 +19,7 @@ void mivc_launch_rgb_to_i420(const uint8_t* rgb, int w, int h, int nframes, uint
                              void* stream);
 void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref_y, const int16_t* pred_mv,
                     int16_t* out_mv, int* out_cost, uint8_t* out_pred, int* out_intra_cost, const int* qp, int range,
-                    int subpel, uint8_t* hp, const int8_t* aq, int planes_ready, void* stream);
+                    int subpel, uint8_t* hp, const int8_t* aq, int planes_ready, int early_sad, void* stream);
 void mivc_launch_b_direct(int B, int wmb, int hmb, const void* col, int dsf, int direct_copy, int16_t* dmv,
                           int16_t* pm0, int16_t* pm1, void* stream);
 void mivc_launch_p_refine(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref, const uint8_t* hp,
@@ -134,15 +134,15 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("me", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref, uintptr_t pred_mv, uintptr_t out_mv,
                  uintptr_t out_cost, uintptr_t out_pred, uintptr_t out_intra, uintptr_t qp, int range, int subpel,
-                 uintptr_t stream, uintptr_t hp, uintptr_t aq, int planes_ready) {
+                 uintptr_t stream, uintptr_t hp, uintptr_t aq, int planes_ready, int early_sad) {
     if (planes_ready && !hp) throw std::invalid_argument("me: planes_ready needs the hp buffer");
     mivc_launch_me(B, wmb, hmb, P<uint8_t>(src), P<uint8_t>(ref), P<int16_t>(pred_mv), P<int16_t>(out_mv),
                    P<int>(out_cost), P<uint8_t>(out_pred), P<int>(out_intra), P<int>(qp), range, subpel,
-                   P<uint8_t>(hp), P<int8_t>(aq), planes_ready, S(stream));
+                   P<uint8_t>(hp), P<int8_t>(aq), planes_ready, early_sad, S(stream));
   }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("src"), py::arg("ref"), py::arg("pred_mv"),
      py::arg("out_mv"), py::arg("out_cost"), py::arg("out_pred"), py::arg("out_intra"), py::arg("qp"),
      py::arg("range"), py::arg("subpel"), py::arg("stream"), py::arg("hp") = 0, py::arg("aq") = 0,
-     py::arg("planes_ready") = 0);
+     py::arg("planes_ready") = 0, py::arg("early_sad") = 0);
   m.def("b_direct", [](int B, int wmb, int hmb, uintptr_t col, int dsf, int direct_copy, uintptr_t dmv, uintptr_t pm0,
                        uintptr_t pm1, uintptr_t stream) {
     mivc_launch_b_direct(B, wmb, hmb, P<void>(col), dsf, direct_copy, P<int16_t>(dmv), P<int16_t>(pm0),

@@ -251,48 +251,9 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
       for (int x = 0; x < 4; ++x)
         res[y * 4 + x] = static_cast<int>(__builtin_amdgcn_ubfe(sw[y], 8 * x, 8)) -
                          static_cast<int>(__builtin_amdgcn_ubfe(prw[y], 8 * x, 8));
-    bool use8 = false;
-    if (a.t8) {
-      // transform size first (x264 analyse: sa8d of the residual < satd -> 8x8), so only the
-      // chosen transform is quantised; lanes hl = b8 * 4 + k run the 8-point passes
-      const int b8 = (lby >> 3) * 2 + (lbx >> 3), ox = lbx & 4, oy = lby & 4;
-#pragma unroll
-      for (int y = 0; y < 4; ++y)
-#pragma unroll
-        for (int x = 0; x < 4; ++x) {
-          s_h8[half][b8][(oy + y) * 8 + ox + x] = res[y * 4 + x];
-          s_d8[half][b8][(oy + y) * 8 + ox + x] = res[y * 4 + x];
-        }
-      s_cost[half][0][hl] = h264::satd4x4(res);
-      wave_sync();
-      const int tb = hl >> 2, k = hl & 3;
-      int* hd = s_h8[half][tb];
-      had8_pass(hd + (2 * k) * 8, 1);
-      had8_pass(hd + (2 * k + 1) * 8, 1);
-      wave_sync();
-      had8_pass(hd + 2 * k, 8);
-      had8_pass(hd + 2 * k + 1, 8);
-      wave_sync();
-      int sa = 0;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) sa += abs(hd[k * 16 + i]);
-      s_cost[half][1][hl] = sa;
-      wave_sync();
-      if (hl == 0) {
-        int satd = 0, sa8d = 0;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) satd += s_cost[half][0][i];
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-          sa8d += (s_cost[half][1][b * 4] + s_cost[half][1][b * 4 + 1] + s_cost[half][1][b * 4 + 2] +
-                   s_cost[half][1][b * 4 + 3] + 2) >> 2;
-        s_t8[half][0] = sa8d < satd;
-      }
-      wave_sync();
-      use8 = s_t8[half][0] != 0;
-    }
-    if (!use8) {
-      h264::forward_core4x4(res);
+    // 4x4 transform, quantisation and decimation score (always: most MBs end here)
+    h264::forward_core4x4(res);
+    {
       const int qbits = 15 + qp / 6;
 #pragma unroll
       for (int r = 0; r < 16; ++r) lv[r] = h264::quant_coef(res[r], mf[h264::kPosClass[r]], qbits, 11);
@@ -300,7 +261,65 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) scan[i] = lv[h264::kZigzag4x4[i]];
       s_score[half][hl] = decimate_score(scan, 0);
-    } else {
+    }
+    if (a.t8) {
+      // High profile: an MB whose 4x4 luma levels survive decimation also tries the 8x8
+      // transform -- sa8d of the residual < its satd picks it (x264 analyse), and only then
+      // is it transformed and quantised; MBs without luma residual keep the 4x4 flag-free
+      // coding (transform_size_8x8_flag is not even coded for them)
+      wave_sync();
+      if (hl == 0) {
+        int total = 0, any = 0;
+#pragma unroll
+        for (int b8 = 0; b8 < 4; ++b8) {
+          const int sc = s_score[half][b8 * 4] + s_score[half][b8 * 4 + 1] + s_score[half][b8 * 4 + 2] +
+                         s_score[half][b8 * 4 + 3];
+          any |= sc >= 4;
+          total += sc;
+        }
+        s_t8[half][2] = any && total >= 6;
+        s_t8[half][0] = 0;
+      }
+      wave_sync();
+      if (s_t8[half][2]) {
+        const int b8 = (lby >> 3) * 2 + (lbx >> 3), ox = lbx & 4, oy = lby & 4;
+        int r2[16];
+#pragma unroll
+        for (int y = 0; y < 4; ++y)
+#pragma unroll
+          for (int x = 0; x < 4; ++x) {
+            r2[y * 4 + x] = static_cast<int>(__builtin_amdgcn_ubfe(sw[y], 8 * x, 8)) -
+                            static_cast<int>(__builtin_amdgcn_ubfe(prw[y], 8 * x, 8));
+            s_h8[half][b8][(oy + y) * 8 + ox + x] = r2[y * 4 + x];
+            s_d8[half][b8][(oy + y) * 8 + ox + x] = r2[y * 4 + x];
+          }
+        s_cost[half][0][hl] = h264::satd4x4(r2);
+        wave_sync();
+        const int tb = hl >> 2, k = hl & 3;
+        int* hd = s_h8[half][tb];
+        had8_pass(hd + (2 * k) * 8, 1);
+        had8_pass(hd + (2 * k + 1) * 8, 1);
+        wave_sync();
+        had8_pass(hd + 2 * k, 8);
+        had8_pass(hd + 2 * k + 1, 8);
+        wave_sync();
+        int sa = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sa += abs(hd[k * 16 + i]);
+        s_cost[half][1][hl] = sa;
+        wave_sync();
+        if (hl == 0) {
+          int satd = 0, sa8d = 0;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) satd += s_cost[half][0][i];
+#pragma unroll
+          for (int b = 0; b < 4; ++b)
+            sa8d += (s_cost[half][1][b * 4] + s_cost[half][1][b * 4 + 1] + s_cost[half][1][b * 4 + 2] +
+                     s_cost[half][1][b * 4 + 3] + 2) >> 2;
+          s_t8[half][0] = sa8d < satd;
+        }
+        wave_sync();
+        if (s_t8[half][0]) {
       // ---- 8x8 transform: forward passes, quantisation of scan positions 16k .. 16k + 15
       // with this chunk's share of x264's decimate_score64 (zero runs priced 3 / 2 / 1 / 0;
       // 9 once any |level| > 1): runs inside the chunk here, the run into its first
@@ -355,6 +374,8 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
         }
         if (total < 6) keep = 0;
         s_t8[half][1] = keep;
+      }
+        }
       }
     }
   } else if (work && hl < 24) {

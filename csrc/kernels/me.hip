@@ -41,6 +41,7 @@ struct MeArgs {
   int subpel;              // 0 none, 1 half, 2 quarter
   const uint8_t* hp;       // [B, 3, H + 8, W + 8] b / h / j half-sample planes of ref_y (margin 4)
   const int8_t* aq;        // [B, nmb] adaptive-quantisation QP offsets (nullable)
+  int early_sad;           // > 0: skip the integer search when the best candidate's SAD <= this
 };
 
 constexpr int kHpM = 4;  // half-sample plane margin (samples); coordinates clamp into it exactly
@@ -404,7 +405,7 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
     const int sv = sum16(h264::satd4x4(r));
     intra_key = min64(ok ? sv : 0x3FFFFFFF);
   }
-  int cx = 0, cy = 0;
+  int cx = 0, cy = 0, best_sad = 0x7FFFFFFF;
   {
     // per-lane SADs are <= 1020, so two candidates share one wave reduction (16-bit halves)
     int csad[5];
@@ -426,10 +427,17 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
         best = cost;
         cx = cand_x[k];
         cy = cand_y[k];
+        best_sad = sad;
       }
     }
   }
 
+  // early termination (x264-style): a candidate already predicting the MB to within
+  // early_sad skips the window and the integer search; the sub-sample refinement below
+  // still runs around it (wave-uniform: the SADs are wave reductions)
+  const bool early = a.early_sad > 0 && best_sad <= a.early_sad;
+  int bx = cx, by = cy;  // integer displacement
+  if (!early) {
   MPROF(1);
   // ---- phase 1: reference window around the centre, with margins for the sub-pel planes
   const int wrows = 16 + 2 * R + kML + kMR;
@@ -484,7 +492,6 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   }
   best_key = wave_min_key(best_key);
   const int bp = best_key & 4095;
-  int bx, by;  // integer displacement
   if (bp == 4095) {
     bx = 0;
     by = 0;
@@ -493,6 +500,7 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
     bx = cx + (bp - by * side) - R;
     by = cy + by - R;
   }
+  }  // !early
   int best_mvx = bx * 4, best_mvy = by * 4;
 
   MPROF(3);
@@ -664,7 +672,7 @@ extern "C" void mivc_launch_me_halfpel(int B, int W, int H, const uint8_t* ref_y
 extern "C" void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref_y,
                                const int16_t* pred_mv, int16_t* out_mv, int* out_cost, uint8_t* out_pred,
                                int* out_intra_cost, const int* qp, int range, int subpel, uint8_t* hp_buf,
-                               const int8_t* aq, int planes_ready, void* stream) {
+                               const int8_t* aq, int planes_ready, int early_sad, void* stream) {
   // hp_buf: caller-owned [B, 3, H + 8, W + 8] (+64 bytes slack) half-sample plane scratch,
   // resident across frames; nullptr -> stream-ordered scratch for this call only.
   // planes_ready: hp_buf already holds ref_y's planes (an anchor's planes are built once
@@ -695,6 +703,7 @@ extern "C" void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, co
   a.subpel = subpel;
   a.hp = hp;
   a.aq = aq;
+  a.early_sad = early_sad;
   if (a.range <= 8) hipLaunchKernelGGL(me_p16x16<8>, dim3(wmb * hmb, B), dim3(64), 0, s, a);
   else hipLaunchKernelGGL(me_p16x16<kMaxR>, dim3(wmb * hmb, B), dim3(64), 0, s, a);
   if (!hp_buf) (void)hipFreeAsync(hp, s);

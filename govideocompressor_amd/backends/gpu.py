@@ -125,7 +125,7 @@ class GpuBackend:
                       "psnr_y": float(np.mean([p["psnr"] for p in parts])),
                       "ssim_y": float(np.mean([p["ssim"] for p in parts])),
                       "frame_bits": [b for p in parts for b in p["frame_bits"]],
-                      "config": cfg.as_dict(), **rate_info.get(key, {})}
+                      "timings": dict(tm.t), "config": cfg.as_dict(), **rate_info.get(key, {})}
                 out[key] = (stream, st)
         return out
 

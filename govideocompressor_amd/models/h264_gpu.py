@@ -75,6 +75,11 @@ class H264Params:
     # x264 --8x8dct (default on): High profile, the 8x8 transform chosen per inter MB where
     # its sa8d beats the 4x4 satd; CABAC only (the CAVLC path stays Constrained Baseline)
     t8x8: bool = True
+    # x264-style ME early termination: a search whose best candidate (the predictors and
+    # their neighbours) already has SAD <= this skips the window and the integer search
+    # (B pictures: the temporal-direct predictor); 0 disables
+    p_early_sad: int = int(os.environ.get("MIVC_P_EARLY_SAD", 0))
+    b_early_sad: int = int(os.environ.get("MIVC_B_EARLY_SAD", 1024))
     # deblock non-reference B pictures even when neither metrics nor the reconstruction
     # are requested (x264 --full-recon); the bitstream does not depend on it
     full_recon: bool = False
@@ -432,7 +437,8 @@ class GpuH264Encoder:
             hp = P(self.me_hp[(pic.anchor - 1) & 1])
             with st("me_p"):
                 self.hip.me(B, wmb, hmb, sy, fy, P(self.prev_mv), P(self.mv), P(self.me_cost), P(self.pred),
-                            P(self.intra_cost), P(self.qp), self.p.me_range, self.p.subpel, s, hp, aq, 1)
+                            P(self.intra_cost), P(self.qp), self.p.me_range, self.p.subpel, s, hp, aq, 1,
+                            self.p.p_early_sad)
                 for it in range(int(self.p.skip_refine)):
                     a_, b_ = (self.mv, self.mv_tmp) if it % 2 == 0 else (self.mv_tmp, self.mv)
                     self.hip.p_refine(B, wmb, hmb, sy, fy, hp, P(a_), P(b_), P(self.me_cost), P(self.prev_mv),
@@ -457,10 +463,10 @@ class GpuH264Encoder:
             with st("me_b"):
                 self.hip.b_direct(B, wmb, hmb, P(self.col_hdr), dsf, copy, P(self.dmv), P(self.pm0), P(self.pm1), s)
                 self.hip.me(B, wmb, hmb, sy, f0y, P(self.pm0), P(self.mv), P(self.me_cost), P(self.pred),
-                            P(self.intra_cost), P(self.qp), br, self.p.subpel, s, hp0, aq, 1)
+                            P(self.intra_cost), P(self.qp), br, self.p.subpel, s, hp0, aq, 1, self.p.b_early_sad)
                 # the L1 search skips the open-loop intra estimate the L0 search just wrote
                 self.hip.me(B, wmb, hmb, sy, f1y, P(self.pm1), P(self.mv1), P(self.me_cost1), P(self.pred1),
-                            0, P(self.qp), br, self.p.subpel, s, hp1, aq, 1)
+                            0, P(self.qp), br, self.p.subpel, s, hp1, aq, 1, self.p.b_early_sad)
             with st("b_decide"):
                 self.hip.b_decide(B, wmb, hmb, sy, f0y, f1y, hp0, hp1, P(self.mv), P(self.mv1), P(self.me_cost),
                                   P(self.me_cost1), P(self.pred), P(self.pred1), P(self.pm0), P(self.pm1),

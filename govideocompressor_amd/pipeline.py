@@ -164,6 +164,9 @@ def encode_file(path: str, output: str, args: str = "264", backend: str = "auto"
     gpu_decode = kind == "pieces" and hasattr(impl, "decode_streams")
     dec_stats: dict[str, float] = {}
 
+    from .obs.log import JsonLogger
+    jlog = JsonLogger(os.environ.get("MIVC_LOG_JSON"), rank=env.rank, component="encode")
+
     def run(idxs: list[int], offset: float | None = None, into: dict | None = None):
         if gpu_decode:  # compressed input on a GPU rank: batched GPU decode, frames stay on the device
             clips = impl.decode_streams([segs[i] for i in idxs], info.fps)
@@ -172,10 +175,20 @@ def encode_file(path: str, output: str, args: str = "264", backend: str = "auto"
         else:
             clips = list(loader.map(lambda i: _load_segment(path, info, kind, segs, i), idxs))
         items = [(str(i), c) for i, c in zip(idxs, clips)]
+        tb = time.perf_counter()
         if offset is None:
             res = impl.encode_clips(items, cfg)
         else:
             res = impl.encode_clips(items, cfg, qp_offsets={str(i): offset for i in idxs})
+        dt = time.perf_counter() - tb
+        if jlog.enabled:  # per-segment metrics: frames, bits, PSNR / SSIM, batch timing
+            for i in idxs:
+                st = res[str(i)][1]
+                jlog.event("segment", segment=i, frames=st.get("frames"), bits=8 * st.get("stream_bytes", 0),
+                           psnr_y=st.get("psnr_y"), ssim_y=st.get("ssim_y"), qp_offset=st.get("qp_offset"),
+                           batch_segments=len(idxs), batch_s=round(dt, 4),
+                           batch_fps=round(sum(c.frames for c in clips) / dt, 2) if dt > 0 else None,
+                           stages={k: round(v, 4) for k, v in st.get("timings", {}).items()})
         for i in idxs:
             stream, st = res[str(i)]
             (mine if into is None else into)[i] = stream
@@ -273,6 +286,8 @@ def encode_file(path: str, output: str, args: str = "264", backend: str = "auto"
     if env.is_main:
         out["fps"] = info.frames / wall if wall > 0 else 0.0
         log(json.dumps(out))
+    jlog.event("done", wall_s=round(wall, 4), segments=n, encoded_here=len(mine))
+    jlog.close()
     loader.shutdown(wait=False)
     be.close()
     D.shutdown(env)

@@ -248,3 +248,25 @@ def test_encode_file_resume_skips_finished_segments(tmp_path, host):
     r3 = encode_file(str(src), str(tmp_path / "o3.264"), args="-vcodec libx264 -crf 30", backend="cpu", slots=4,
                      seg_frames=8, log=lambda s: None, resume=True, work_dir=str(wd))
     assert r3["resumed_segments"] == 0
+
+
+def test_encode_file_json_segment_metrics(tmp_path, monkeypatch):
+    """MIVC_LOG_JSON receives one JSON line per encoded segment (frames, bits,
+    PSNR) and a closing line per rank."""
+    import json as _json
+
+    from govideocompressor_amd.pipeline import encode_file
+    from govideocompressor_amd.utils import yuv
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    src = tmp_path / "in.y4m"
+    yuv.write_y4m(str(src), yuv.synth_clip_cpu(16, 64, 48, seed=2))
+    logp = tmp_path / "log.jsonl"
+    monkeypatch.setenv("MIVC_LOG_JSON", str(logp))
+    encode_file(str(src), str(tmp_path / "o.264"), args="-vcodec libx264 -crf 26", backend="cpu", slots=2,
+                seg_frames=8, log=lambda s: None)
+    recs = [_json.loads(x) for x in logp.read_text().splitlines()]
+    segs = [r for r in recs if r["event"] == "segment"]
+    assert sorted(r["segment"] for r in segs) == [0, 1]
+    assert all(r["frames"] == 8 and r["bits"] > 0 and r["psnr_y"] > 20 and r["component"] == "encode" for r in segs)
+    assert recs[-1]["event"] == "done"
