@@ -213,7 +213,7 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
   __shared__ int s_d8[2][4][64];
   __shared__ int16_t s_l8[2][4][64];
   __shared__ int s_cost[2][2][16];   // [half][0: satd per 4x4 lane, 1: sa8d partial per (b8, k)]
-  __shared__ int s_t8[2][2];         // [half][0] use 8x8, [1] keep mask of the 8x8 blocks
+  __shared__ int s_t8[2][3];         // [half][0] use 8x8, [1] keep mask of the 8x8 blocks, [2] 8x8 tried
 
   const int mvx = a.bmode ? 0 : a.mv[o * 2], mvy = a.bmode ? 0 : a.mv[o * 2 + 1];
   const bool go_intra = a.intra_cost[o] < a.me_cost[o];
