@@ -120,8 +120,38 @@ struct FrameArgs {
   SynthGeom g;
   const uint8_t *cy, *cu, *cv, *tiles;
   size_t tile_stride;
-  uint8_t *y, *u, *v;  // [slots*frames, h, w] display-size frames
+  void *y, *u, *v;  // [slots*frames, h, w] display-size frames (uint8, or uint16 at BD 10)
 };
+
+// 16 output samples of a run: one 16-byte store at 8 bits, two at 10 bits (uint16 samples)
+template <int BD>
+__device__ __forceinline__ void store_run(void* base, size_t idx, const int (&v)[16], int valid) {
+  if constexpr (BD == 8) {
+    uint8_t* dst = static_cast<uint8_t*>(base) + idx;
+    uint32_t o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      int p4[4] = {v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+      o[q] = pack4_u8(p4);
+    }
+    if (valid >= 16 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+      *reinterpret_cast<uint4*>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
+    } else {
+      for (int k = 0; k < 16 && k < valid; ++k) dst[k] = static_cast<uint8_t>(v[k]);
+    }
+  } else {
+    uint16_t* dst = static_cast<uint16_t*>(base) + idx;
+    uint32_t o[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = static_cast<uint32_t>(v[2 * q]) | (static_cast<uint32_t>(v[2 * q + 1]) << 16);
+    if (valid >= 16 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+      reinterpret_cast<uint4*>(dst)[0] = make_uint4(o[0], o[1], o[2], o[3]);
+      reinterpret_cast<uint4*>(dst)[1] = make_uint4(o[4], o[5], o[6], o[7]);
+    } else {
+      for (int k = 0; k < 16 && k < valid; ++k) dst[k] = static_cast<uint16_t>(v[k]);
+    }
+  }
+}
 
 // A frame step is B*F frames of W x H: the per-row launch of the first version issued
 // ~50M 256-thread workgroups per 1080p batch and was bound by workgroup dispatch
@@ -130,6 +160,8 @@ struct FrameArgs {
 // bytes of a run come from 5 aligned dword loads + v_alignbyte, and one hash feeds the
 // sensor noise of 4 pixels.
 __device__ __forceinline__ int noise5(uint32_t h, int k) { return static_cast<int>(((h >> (8 * k)) & 255u) % 5u) - 2; }
+// the same +-2 (8-bit) LSB noise amplitude at 10 bits: +-8 in 10-bit steps
+__device__ __forceinline__ int noise17(uint32_t h, int k) { return static_cast<int>(((h >> (8 * k)) & 255u) % 17u) - 8; }
 
 struct FrameConst {
   int slot, f;
@@ -174,7 +206,12 @@ __device__ __forceinline__ bool run_meets(int x16, int y, int obx, int oby, int 
   return lx < ow || lx + 16 > w;
 }
 
+// BD 10: the same content computed at 10-bit precision (canvas interpolation, ramp and
+// noise keep their fractional bits; texture tiles scale by 4), not 8-bit samples << 2.
+template <int BD>
 __global__ __launch_bounds__(256) void synth_frame_luma(FrameArgs a) {
+  constexpr float S = BD == 8 ? 1.f : 4.f;
+  constexpr int kMax = (1 << BD) - 1;
   const SynthGeom& g = a.g;
   const int runs = (g.width + 15) >> 4;
   const int nfr = g.slots * g.frames;
@@ -244,7 +281,7 @@ __global__ __launch_bounds__(256) void synth_frame_luma(FrameArgs a) {
     int lum[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k)
-      lum[k] = static_cast<int>(t0(k) * F.w00 + t0(k + 1) * F.w10 + t1(k) * F.w01 + t1(k + 1) * F.w11 + 20.f * sn[k] +
+      lum[k] = static_cast<int>(S * (t0(k) * F.w00 + t0(k + 1) * F.w10 + t1(k) * F.w01 + t1(k + 1) * F.w11 + 20.f * sn[k]) +
                                 0.5f);
 #pragma unroll
     for (int o = 0; o < 3; ++o) {
@@ -255,30 +292,26 @@ __global__ __launch_bounds__(256) void synth_frame_luma(FrameArgs a) {
         for (int k = 0; k < 16; ++k) {
           int lx = x16 + k - fc.obx[o];
           lx = lx < 0 ? lx + g.width : lx;  // wrap-around
-          if (lx < g.ow[o]) lum[k] = trow[lx];
+          if (lx < g.ow[o]) lum[k] = static_cast<int>(trow[lx]) * static_cast<int>(S);
         }
       }
     }
-    uint32_t out[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const uint32_t h = hash3(static_cast<uint32_t>(x16 + 4 * q), static_cast<uint32_t>(y), fc.ss ^ (fc.f * 2654435761u));
-      int v4[4];
 #pragma unroll
-      for (int b = 0; b < 4; ++b) v4[b] = clampi(lum[4 * q + b] + noise5(h, b), 0, 255);
-      out[q] = pack4_u8(v4);
+      for (int b = 0; b < 4; ++b)
+        lum[4 * q + b] = clampi(lum[4 * q + b] + (BD == 8 ? noise5(h, b) : noise17(h, b)), 0, kMax);
     }
-    uint8_t* dst = a.y + (static_cast<size_t>(fz) * g.height + y) * g.width + x16;
-    if (x16 + 16 <= g.width && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
-      *reinterpret_cast<uint4*>(dst) = make_uint4(out[0], out[1], out[2], out[3]);
-    } else {
-      for (int k = 0; k < 16 && x16 + k < g.width; ++k) dst[k] = static_cast<uint8_t>(out[k >> 2] >> (8 * (k & 3)));
-    }
+    store_run<BD>(a.y, (static_cast<size_t>(fz) * g.height + y) * g.width + x16, lum, g.width - x16);
     }
   }
 }
 
+template <int BD>
 __global__ __launch_bounds__(256) void synth_frame_chroma(FrameArgs a) {
+  constexpr int S = BD == 8 ? 1 : 4;
+  constexpr int kMax = (1 << BD) - 1;
   const SynthGeom& g = a.g;
   const int w2 = g.width / 2, h2 = g.height / 2, ccw = g.cw / 2, cch = g.ch / 2;
   const int runs = (w2 + 15) >> 4;
@@ -338,12 +371,12 @@ __global__ __launch_bounds__(256) void synth_frame_chroma(FrameArgs a) {
     }
     float sn[16];
     sin_run(0.02f * x16, 0.02f, sn);
-    const int cv_row = static_cast<int>(10.f * __cosf(0.02f * y));
+    const int cv_row = static_cast<int>(10.f * S * __cosf(0.02f * y));
     int cu[16], cv[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-      cu[k] = static_cast<int>((uw[k >> 2] >> (8 * (k & 3))) & 255u) + static_cast<int>(10.f * sn[k]);
-      cv[k] = static_cast<int>((vw[k >> 2] >> (8 * (k & 3))) & 255u) + cv_row;
+      cu[k] = static_cast<int>((uw[k >> 2] >> (8 * (k & 3))) & 255u) * S + static_cast<int>(10.f * S * sn[k]);
+      cv[k] = static_cast<int>((vw[k >> 2] >> (8 * (k & 3))) & 255u) * S + cv_row;
     }
 #pragma unroll
     for (int o = 0; o < 3; ++o) {
@@ -352,34 +385,20 @@ __global__ __launch_bounds__(256) void synth_frame_chroma(FrameArgs a) {
           int lx = x16 + k - fc.obx[o];
           lx = lx < 0 ? lx + w2 : lx;
           if (lx < g.ow[o] / 2) {
-            cu[k] = 90 + 50 * o;
-            cv[k] = 170 - 40 * o;
+            cu[k] = (90 + 50 * o) * S;
+            cv[k] = (170 - 40 * o) * S;
           }
         }
       }
     }
-    uint32_t ou[4], ov[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      int pu[4], pv[4];
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        pu[b] = clampi(cu[4 * q + b], 0, 255);
-        pv[b] = clampi(cv[4 * q + b], 0, 255);
-      }
-      ou[q] = pack4_u8(pu);
-      ov[q] = pack4_u8(pv);
+    for (int k = 0; k < 16; ++k) {
+      cu[k] = clampi(cu[k], 0, kMax);
+      cv[k] = clampi(cv[k], 0, kMax);
     }
     const size_t idx = (static_cast<size_t>(fz) * h2 + y) * w2 + x16;
-    if (x16 + 16 <= w2 && ((reinterpret_cast<uintptr_t>(a.u + idx) | reinterpret_cast<uintptr_t>(a.v + idx)) & 15) == 0) {
-      *reinterpret_cast<uint4*>(a.u + idx) = make_uint4(ou[0], ou[1], ou[2], ou[3]);
-      *reinterpret_cast<uint4*>(a.v + idx) = make_uint4(ov[0], ov[1], ov[2], ov[3]);
-    } else {
-      for (int k = 0; k < 16 && x16 + k < w2; ++k) {
-        a.u[idx + k] = static_cast<uint8_t>(ou[k >> 2] >> (8 * (k & 3)));
-        a.v[idx + k] = static_cast<uint8_t>(ov[k >> 2] >> (8 * (k & 3)));
-      }
-    }
+    store_run<BD>(a.u, idx, cu, w2 - x16);
+    store_run<BD>(a.v, idx, cv, w2 - x16);
     }
   }
 }
@@ -389,8 +408,9 @@ __global__ __launch_bounds__(256) void synth_frame_chroma(FrameArgs a) {
 
 using namespace mivc::gpu;
 
-extern "C" void mivc_launch_synth(uint8_t* y, uint8_t* u, uint8_t* v, int width, int height, int slots, int frames,
-                                  int frame0, uint32_t seed, void* stream) {
+// bit_depth 8: uint8 planes; 10: uint16 planes holding 10-bit samples
+extern "C" void mivc_launch_synth(void* y, void* u, void* v, int width, int height, int slots, int frames, int frame0,
+                                  uint32_t seed, int bit_depth, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   SynthGeom g{};
   g.width = width;
@@ -426,7 +446,12 @@ extern "C" void mivc_launch_synth(uint8_t* y, uint8_t* u, uint8_t* v, int width,
   const unsigned gy = static_cast<unsigned>(fr < 65535 ? fr : 65535);
   const int lruns = height * ((width + 15) / 16), cruns = (height / 2) * ((width / 2 + 15) / 16);
   // 8 runs per thread: per-frame setup and workgroup dispatch amortised over 2048 runs
-  hipLaunchKernelGGL(synth_frame_luma, dim3((lruns + 2047) / 2048, gy), dim3(256), 0, s, fa);
-  hipLaunchKernelGGL(synth_frame_chroma, dim3((cruns + 2047) / 2048, gy), dim3(256), 0, s, fa);
+  if (bit_depth == 10) {
+    hipLaunchKernelGGL(synth_frame_luma<10>, dim3((lruns + 2047) / 2048, gy), dim3(256), 0, s, fa);
+    hipLaunchKernelGGL(synth_frame_chroma<10>, dim3((cruns + 2047) / 2048, gy), dim3(256), 0, s, fa);
+  } else {
+    hipLaunchKernelGGL(synth_frame_luma<8>, dim3((lruns + 2047) / 2048, gy), dim3(256), 0, s, fa);
+    hipLaunchKernelGGL(synth_frame_chroma<8>, dim3((cruns + 2047) / 2048, gy), dim3(256), 0, s, fa);
+  }
   hipFreeAsync(ws, s);
 }

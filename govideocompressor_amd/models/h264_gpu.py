@@ -958,13 +958,19 @@ class GpuH264Encoder:
 
 
 def synth_clip(slots: int, frames: int, width: int, height: int, seed: int = 0, frame0: int = 0,
-               device: str | torch.device = "cuda"):
-    """Generate B x F synthetic I420 frames directly in HBM (see csrc/kernels/synth.hip)."""
+               device: str | torch.device = "cuda", bit_depth: int = 8):
+    """Generate B x F synthetic I420 frames directly in HBM (see csrc/kernels/synth.hip).
+
+    ``bit_depth=10`` renders the same content at 10-bit precision into int16 planes
+    (values 0..1023: the canvas interpolation, ramp and noise keep their low bits)."""
+    if bit_depth not in (8, 10):
+        raise ValueError("synth_clip: bit_depth must be 8 or 10")
     hip = native.hip()
     dev = _resolve(device)
-    y = torch.empty((slots, frames, height, width), dtype=torch.uint8, device=dev)
-    u = torch.empty((slots, frames, height // 2, width // 2), dtype=torch.uint8, device=dev)
+    dt = torch.uint8 if bit_depth == 8 else torch.int16
+    y = torch.empty((slots, frames, height, width), dtype=dt, device=dev)
+    u = torch.empty((slots, frames, height // 2, width // 2), dtype=dt, device=dev)
     v = torch.empty_like(u)
     hip.synth(y.data_ptr(), u.data_ptr(), v.data_ptr(), width, height, slots, frames, frame0, seed & 0xFFFFFFFF,
-              torch.cuda.current_stream(dev).cuda_stream)
+              torch.cuda.current_stream(dev).cuda_stream, bit_depth)
     return y, u, v

@@ -15,14 +15,28 @@ pytestmark = pytest.mark.gpu
 def _encode(w, h, F, B, bd=8, **kw):
     from govideocompressor_amd.models.h264_gpu import synth_clip
     from govideocompressor_amd.models.hevc_gpu import GpuHevcEncoder, HevcParams
-    y, u, v = synth_clip(B, F, w, h, seed=7)
-    if bd == 10:
-        y, u, v = (x.to(torch.int16) * 4 + 1 for x in (y, u, v))
+    y, u, v = synth_clip(B, F, w, h, seed=7, bit_depth=bd)
     enc = GpuHevcEncoder(HevcParams(width=w, height=h, bit_depth=bd, **kw), slots=B)
     res = enc.encode(y, u, v, keep_recon=True)
     rec = enc.last_recon
     enc.close()
     return res, rec
+
+
+def test_synth_10bit_is_native_10bit():
+    """The 10-bit synth path renders the 8-bit content at 10-bit precision (low bits used),
+    within the sensor-noise amplitude of 4x the 8-bit picture."""
+    from govideocompressor_amd.models.h264_gpu import synth_clip
+    y8, u8, v8 = synth_clip(2, 3, 200, 120, seed=4)
+    y10, u10, v10 = synth_clip(2, 3, 200, 120, seed=4, bit_depth=10)
+    assert y10.dtype == torch.int16 and y10.shape == y8.shape and u10.shape == u8.shape
+    for a8, a10 in ((y8, y10), (u8, u10), (v8, v10)):
+        assert int(a10.min()) >= 0 and int(a10.max()) <= 1023
+        d = (a10.to(torch.int32) - 4 * a8.to(torch.int32)).abs().float()
+        assert float(d.mean()) < 8.0
+    frac = (y10 % 4 != 0).float().mean().item()
+    assert frac > 0.5          # not 8-bit x 4: the two low bits carry content
+    assert torch.equal(y10, synth_clip(2, 3, 200, 120, seed=4, bit_depth=10)[0])   # deterministic
 
 
 def _compare(host, res, rec, skip_filters=False):
