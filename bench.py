@@ -47,6 +47,8 @@ def main() -> None:
                     help="Constrained Baseline CAVLC (the round-1 encoder) instead of Main CABAC")
     ap.add_argument("--no-8x8dct", dest="t8x8", action="store_false",
                     help="Main profile (no High-profile 8x8 transform)")
+    ap.add_argument("--no-partitions", dest="partitions", action="store_false",
+                    help="P macroblocks 16x16 only (no P_8x8 / P_16x8 / P_8x16)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--no-quality", dest="quality", action="store_false",
                     help="skip the PSNR/SSIM measurement of the first warmup step")
@@ -64,7 +66,7 @@ def main() -> None:
         if env.is_main:
             print(f"warning: --gpus {a.gpus} but WORLD_SIZE {env.world}", file=sys.stderr)
     p = H264Params(width=a.width, height=a.height, fps=30.0, crf=a.crf, bframes=a.bframes, cabac=not a.cavlc,
-                   t8x8=a.t8x8)
+                   t8x8=a.t8x8, partitions=a.partitions)
     enc = GpuH264Encoder(p, slots=a.slots, device=env.device,
                          entropy_threads=int(os.environ.get("MIVC_ENTROPY_THREADS", "16")))
     B, F = a.slots, a.frames

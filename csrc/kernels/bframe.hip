@@ -14,6 +14,9 @@
 //                                  the anchors' frame-level half-sample planes, 4x4 SATD,
 //                                  cost = SATD + lambda * bits; writes the winner's MbHeader
 //                                  motion fields and its luma prediction for encode_inter.
+// and two P-picture passes after the 16x16 search:
+//   p_mv_refine  (wave per MB)     P_Skip-aware vector choice (Jacobi passes)
+//   p_part8x8    (wave per MB)     8x8 quadrant vectors: P_8x8 / P_16x8 / P_8x16 partitions
 #include "kcommon.h"
 
 namespace mivc {
@@ -335,6 +338,198 @@ __global__ __launch_bounds__(64) void p_mv_refine(PRefineArgs a) {
   }
 }
 
+
+// ---- P_8x8 / P_16x8 / P_8x16 partitions (x264 --partitions p8x8, its default).  After the
+// 16x16 search and the skip-aware refinement, each 8x8 quadrant of a P macroblock searches
+// its own vector: predictor candidates (the MB's vector, the left / top / top-right /
+// right / bottom MBs' vectors, zero, the temporal predictor), then a half-sample and a
+// quarter-sample ring around the best, SATD on the frame-level G/b/h/j planes.  The split
+// wins when sum(SATD_q) + lambda * (mvd bits against the partition predictors of clause
+// 8.4.1.3 + sub_mb_type overhead) beats the 16x16 cost; encode_inter then codes the four
+// vectors (as P_16x8 / P_8x16 when they pair up).
+//
+// One wave per MB: lane = quadrant (2 bits) x 4x4 block of the quadrant (2 bits) x
+// candidate slot (2 bits); block SATDs sum over lane bits 2-3, the best candidate of a
+// quadrant is a min over bits 0-1.
+struct PPartArgs {
+  Geom g;
+  const uint8_t* src_y;
+  const uint8_t* ref;
+  const uint8_t* hp;
+  const int16_t* mv;    // [B, nmb, 2] final 16x16 vectors
+  const int16_t* pm;    // [B, nmb, 2] the ME's predictor (its cost is priced against it)
+  int* cost;            // [B, nmb] in: 16x16 cost; out: the chosen mode's cost
+  uint8_t* pred;        // [B, nmb, 256] luma prediction, rewritten when the split wins
+  int16_t* mv8;         // [B, nmb, 4, 2] out: per-quadrant vectors (all equal: 16x16)
+  const int* qp;
+  const int8_t* aq;
+  int overhead;         // bits charged to the split beyond the mvds
+  int min_satd;         // 16x16 SATD at or below this: no split search
+};
+
+__device__ __forceinline__ void med_pred(int ax, int ay, bool ha, int bx, int by, bool hb, int cx, int cy, bool hc,
+                                         int* px, int* py) {
+  // clause 8.4.1.3.1 with every neighbour at ref 0: B and C unavailable, A available -> A
+  if (ha && !hb && !hc) {
+    *px = ax;
+    *py = ay;
+    return;
+  }
+  if (!ha) ax = ay = 0;
+  if (!hb) bx = by = 0;
+  if (!hc) cx = cy = 0;
+  *px = median3(ax, bx, cx);
+  *py = median3(ay, by, cy);
+}
+
+__global__ __launch_bounds__(64) void p_part8x8(PPartArgs a) {
+  const Geom& g = a.g;
+  const int nmb = g.nmb();
+  int mb, slot;
+  xcd_unit_slot(mb, slot);
+  const int lane = threadIdx.x;
+  const size_t o = static_cast<size_t>(slot) * nmb + mb;
+  const int mx = mb % g.wmb, my = mb / g.wmb;
+  const int16_t* mv = a.mv + static_cast<size_t>(slot) * nmb * 2;
+  const int vx = mv[mb * 2], vy = mv[mb * 2 + 1];
+  const int qp = clampi(a.qp[slot] + (a.aq ? a.aq[o] : 0), 0, 51);
+  const int lambda = h264::kLambda[qp];
+  const int pmx = a.pm ? a.pm[o * 2] : 0, pmy = a.pm ? a.pm[o * 2 + 1] : 0;
+  const int cost_in = a.cost[o];
+  const int satd16 = cost_in - lambda * (mvbits_se(vx - pmx) + mvbits_se(vy - pmy));
+  int16_t* m8 = a.mv8 + o * 8;
+  const uint32_t vw = (static_cast<uint32_t>(vx) & 0xFFFFu) | (static_cast<uint32_t>(vy) << 16);
+  if (satd16 <= a.min_satd) {
+    if (lane == 0) *reinterpret_cast<uint4*>(m8) = make_uint4(vw, vw, vw, vw);
+    return;
+  }
+  // neighbouring MBs' 16x16 vectors (current picture)
+  const bool hA = mx > 0, hB = my > 0, hC = my > 0 && mx < g.wmb - 1, hD = mx > 0 && my > 0;
+  const bool hR = mx < g.wmb - 1, hU = my < g.hmb - 1;
+  auto nv = [&](bool h, int n, int c) { return h ? static_cast<int>(mv[n * 2 + c]) : 0; };
+  const int Ax = nv(hA, mb - 1, 0), Ay = nv(hA, mb - 1, 1);
+  const int Bx = nv(hB, mb - g.wmb, 0), By = nv(hB, mb - g.wmb, 1);
+  const int Cx = hC ? nv(true, mb - g.wmb + 1, 0) : nv(hD, mb - g.wmb - 1, 0);
+  const int Cy = hC ? nv(true, mb - g.wmb + 1, 1) : nv(hD, mb - g.wmb - 1, 1);
+  const bool hCD = hC || hD;
+  // candidate predictors of every quadrant
+  int cvx[8], cvy[8];
+  cvx[0] = vx; cvy[0] = vy;
+  cvx[1] = hA ? Ax : vx; cvy[1] = hA ? Ay : vy;
+  cvx[2] = hB ? Bx : vx; cvy[2] = hB ? By : vy;
+  cvx[3] = hCD ? Cx : vx; cvy[3] = hCD ? Cy : vy;
+  cvx[4] = hR ? nv(true, mb + 1, 0) : vx; cvy[4] = hR ? nv(true, mb + 1, 1) : vy;
+  cvx[5] = hU ? nv(true, mb + g.wmb, 0) : vx; cvy[5] = hU ? nv(true, mb + g.wmb, 1) : vy;
+  cvx[6] = 0; cvy[6] = 0;
+  cvx[7] = pmx; cvy[7] = pmy;
+  const int q = lane >> 4, blk = (lane >> 2) & 3, c = lane & 3;
+  // search-time partition predictor (the MB's own vector stands in for its other quadrants)
+  int spx, spy;
+  if (q == 0) med_pred(Ax, Ay, hA, Bx, By, hB, Bx, By, hB, &spx, &spy);
+  else if (q == 1) med_pred(vx, vy, true, Bx, By, hB, Cx, Cy, hCD, &spx, &spy);
+  else if (q == 2) med_pred(Ax, Ay, hA, vx, vy, true, vx, vy, true, &spx, &spy);
+  else { spx = vx; spy = vy; }
+  const int W = g.W, H = g.H;
+  const int X = mx * 16 + (q & 1) * 8 + (blk & 1) * 4, Y = my * 16 + (q >> 1) * 8 + (blk >> 1) * 4;
+  const size_t yo = static_cast<size_t>(slot) * g.ysize();
+  const uint8_t* G0 = a.ref + yo;
+  const uint8_t* H0 = a.hp + static_cast<size_t>(slot) * 3 * (W + 2 * kHpMargin) * (H + 2 * kHpMargin);
+  uint32_t srow[4];
+#pragma unroll
+  for (int y = 0; y < 4; ++y) srow[y] = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y + y) * W + X);
+  // SATD of this quadrant at vector (x, y), summed over its four blocks
+  auto qsatd = [&](int x, int y) -> int {
+    int r[16];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t p = mc4(G0, H0, W, H, X, Y + k, x, y);
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        r[k * 4 + b] = static_cast<int>((srow[k] >> (8 * b)) & 255u) - static_cast<int>((p >> (8 * b)) & 255u);
+    }
+    int s = h264::satd4x4(r);
+    s += __shfl_xor(s, 4, 64);
+    s += __shfl_xor(s, 8, 64);
+    return s;
+  };
+  auto qmin = [](int k) {
+    k = min(k, __shfl_xor(k, 1, 64));
+    return min(k, __shfl_xor(k, 2, 64));
+  };
+  // stage 1: predictor candidates
+  int bvx = vx, bvy = vy, bcost = 0x7FFFFFFF;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int i = it * 4 + c;
+    const int x = clampi(cvx[i], -2048, 2047), y = clampi(cvy[i], -512, 511);
+    const int cst = qsatd(x, y) + lambda * (mvbits_se(x - spx) + mvbits_se(y - spy));
+    const int key = qmin((cst << 3) | i);
+    if ((key >> 3) < bcost) {
+      bcost = key >> 3;
+      bvx = clampi(cvx[key & 7], -2048, 2047);
+      bvy = clampi(cvy[key & 7], -512, 511);
+    }
+  }
+  // stages 2-3: half- then quarter-sample rings around the best
+#pragma unroll
+  for (int step = 2; step >= 1; --step) {
+    const int ox = bvx, oy = bvy;
+    int kbest = 0x7FFFFFFF;
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int i = it * 4 + c;                 // 0..7: the ring without its centre
+      const int idx = i < 4 ? i : i + 1;
+      const int x = ox + (idx % 3 - 1) * step, y = oy + (idx / 3 - 1) * step;
+      const int cst = qsatd(x, y) + lambda * (mvbits_se(x - spx) + mvbits_se(y - spy));
+      kbest = min(kbest, qmin((cst << 3) | i));
+    }
+    if ((kbest >> 3) < bcost) {
+      bcost = kbest >> 3;
+      const int i = kbest & 7, idx = i < 4 ? i : i + 1;
+      bvx = ox + (idx % 3 - 1) * step;
+      bvy = oy + (idx / 3 - 1) * step;
+    }
+  }
+  const int bsatd = bcost - lambda * (mvbits_se(bvx - spx) + mvbits_se(bvy - spy));
+  // every lane: all four quadrants' results (uniform per 16 lanes -> readlane)
+  int qx[4], qy[4], qs[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    qx[k] = __builtin_amdgcn_readlane(bvx, 16 * k);
+    qy[k] = __builtin_amdgcn_readlane(bvy, 16 * k);
+    qs[k] = __builtin_amdgcn_readlane(bsatd, 16 * k);
+  }
+  // exact-form partition predictors (neighbouring MBs still as their 16x16 vectors)
+  int p0x, p0y, p1x, p1y, p2x, p2y, p3x, p3y, p16x, p16y;
+  med_pred(Ax, Ay, hA, Bx, By, hB, Bx, By, hB, &p0x, &p0y);
+  med_pred(qx[0], qy[0], true, Bx, By, hB, Cx, Cy, hCD, &p1x, &p1y);
+  med_pred(Ax, Ay, hA, qx[0], qy[0], true, qx[1], qy[1], true, &p2x, &p2y);
+  med_pred(qx[2], qy[2], true, qx[1], qy[1], true, qx[0], qy[0], true, &p3x, &p3y);
+  med_pred(Ax, Ay, hA, Bx, By, hB, Cx, Cy, hCD, &p16x, &p16y);
+  const int bits8 = mvbits_se(qx[0] - p0x) + mvbits_se(qy[0] - p0y) + mvbits_se(qx[1] - p1x) + mvbits_se(qy[1] - p1y) +
+                    mvbits_se(qx[2] - p2x) + mvbits_se(qy[2] - p2y) + mvbits_se(qx[3] - p3x) + mvbits_se(qy[3] - p3y);
+  const int cost8 = qs[0] + qs[1] + qs[2] + qs[3] + lambda * (bits8 + a.overhead);
+  const int cost16 = satd16 + lambda * (mvbits_se(vx - p16x) + mvbits_se(vy - p16y));
+  const bool uniform = qx[0] == qx[1] && qx[0] == qx[2] && qx[0] == qx[3] && qy[0] == qy[1] && qy[0] == qy[2] &&
+                       qy[0] == qy[3];
+  const bool split = !uniform && cost8 < cost16;
+  if (split) {
+    // lane (q, blk, c) rewrites row c of its block
+    const uint32_t p = mc4(G0, H0, W, H, X, Y + c, bvx, bvy);
+    const int lx = (q & 1) * 8 + (blk & 1) * 4, ly = (q >> 1) * 8 + (blk >> 1) * 4 + c;
+    *reinterpret_cast<uint32_t*>(a.pred + o * 256 + ly * 16 + lx) = p;
+  }
+  if (lane == 0) {
+    if (split) {
+      auto w = [](int x, int y) { return (static_cast<uint32_t>(x) & 0xFFFFu) | (static_cast<uint32_t>(y) << 16); };
+      *reinterpret_cast<uint4*>(m8) = make_uint4(w(qx[0], qy[0]), w(qx[1], qy[1]), w(qx[2], qy[2]), w(qx[3], qy[3]));
+      a.cost[o] = cost8 - cost16 + cost_in;     // the 16x16 cost's convention, shifted by the gain
+    } else {
+      *reinterpret_cast<uint4*>(m8) = make_uint4(vw, vw, vw, vw);
+    }
+  }
+}
+
 }  // namespace gpu
 }  // namespace mivc
 
@@ -400,4 +595,25 @@ extern "C" void mivc_launch_p_refine(int B, int wmb, int hmb, const uint8_t* src
   a.qp = qp;
   a.aq = aq;
   hipLaunchKernelGGL(p_mv_refine, dim3(wmb * hmb, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
+}
+
+extern "C" void mivc_launch_p_part8(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref,
+                                    const uint8_t* hp, const int16_t* mv, const int16_t* pm, int* cost, uint8_t* pred,
+                                    int16_t* mv8, const int* qp, const int8_t* aq, int overhead, int min_satd,
+                                    void* stream) {
+  PPartArgs a;
+  a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
+  a.src_y = src_y;
+  a.ref = ref;
+  a.hp = hp;
+  a.mv = mv;
+  a.pm = pm;
+  a.cost = cost;
+  a.pred = pred;
+  a.mv8 = mv8;
+  a.qp = qp;
+  a.aq = aq;
+  a.overhead = overhead;
+  a.min_satd = min_satd;
+  hipLaunchKernelGGL(p_part8x8, dim3(wmb * hmb, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
 }

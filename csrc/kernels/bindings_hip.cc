@@ -43,7 +43,10 @@ void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t* src_y, con
                               const int16_t* mv, const int* me_cost, const int* intra_cost, const int* qp,
                               int chroma_qp_offset, void* hdr, int16_t* coef, uint8_t* nz, uint8_t* intra_flag,
                               int* intra_count, const int8_t* aq, const uint8_t* ref1_u, const uint8_t* ref1_v,
-                              int bmode, int t8, void* stream);
+                              int bmode, int t8, const int16_t* mv8, void* stream);
+void mivc_launch_p_part8(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref, const uint8_t* hp,
+                         const int16_t* mv, const int16_t* pm, int* cost, uint8_t* pred, int16_t* mv8, const int* qp,
+                         const int8_t* aq, int overhead, int min_satd, void* stream);
 void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* src_u,
                               const uint8_t* src_v, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const int* qp,
                               int chroma_qp_offset, void* hdr, int16_t* coef, uint8_t* nz,
@@ -191,19 +194,27 @@ PYBIND11_MODULE(_hip, m) {
            uintptr_t fv, uintptr_t ry, uintptr_t ru, uintptr_t rv, uintptr_t pred, uintptr_t mv, uintptr_t me_cost,
            uintptr_t intra_cost, uintptr_t qp, int cqo, uintptr_t hdr, uintptr_t coef, uintptr_t nz,
            uintptr_t intra_flag, uintptr_t intra_count, uintptr_t stream, uintptr_t aq, uintptr_t ref1_u,
-           uintptr_t ref1_v, int bmode, int t8) {
+           uintptr_t ref1_v, int bmode, int t8, uintptr_t mv8) {
           if (bmode && (!ref1_u || !ref1_v)) throw std::invalid_argument("encode_inter: B mode needs the list-1 chroma");
           mivc_launch_encode_inter(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), P<uint8_t>(fy),
                                    P<uint8_t>(fu), P<uint8_t>(fv), P<uint8_t>(ry), P<uint8_t>(ru), P<uint8_t>(rv),
                                    P<uint8_t>(pred), P<int16_t>(mv), P<int>(me_cost), P<int>(intra_cost), P<int>(qp),
                                    cqo, P<void>(hdr), P<int16_t>(coef), P<uint8_t>(nz), P<uint8_t>(intra_flag),
                                    P<int>(intra_count), P<int8_t>(aq), P<uint8_t>(ref1_u), P<uint8_t>(ref1_v), bmode,
-                                   t8, S(stream));
+                                   t8, P<int16_t>(mv8), S(stream));
         }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("sy"), py::arg("su"), py::arg("sv"), py::arg("fy"),
         py::arg("fu"), py::arg("fv"), py::arg("ry"), py::arg("ru"), py::arg("rv"), py::arg("pred"), py::arg("mv"),
         py::arg("me_cost"), py::arg("intra_cost"), py::arg("qp"), py::arg("cqo"), py::arg("hdr"), py::arg("coef"),
         py::arg("nz"), py::arg("intra_flag"), py::arg("intra_count"), py::arg("stream"), py::arg("aq") = 0,
-        py::arg("ref1_u") = 0, py::arg("ref1_v") = 0, py::arg("bmode") = 0, py::arg("t8") = 0);
+        py::arg("ref1_u") = 0, py::arg("ref1_v") = 0, py::arg("bmode") = 0, py::arg("t8") = 0, py::arg("mv8") = 0);
+  m.def("p_part8", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref, uintptr_t hp, uintptr_t mv, uintptr_t pm,
+                      uintptr_t cost, uintptr_t pred, uintptr_t mv8, uintptr_t qp, uintptr_t aq, int overhead,
+                      int min_satd, uintptr_t stream) {
+    if (!hp || !mv8) throw std::invalid_argument("p_part8: needs the half-sample planes and an mv8 buffer");
+    mivc_launch_p_part8(B, wmb, hmb, P<uint8_t>(src), P<uint8_t>(ref), P<uint8_t>(hp), P<int16_t>(mv), P<int16_t>(pm),
+                        P<int>(cost), P<uint8_t>(pred), P<int16_t>(mv8), P<int>(qp), P<int8_t>(aq), overhead, min_satd,
+                        S(stream));
+  });
   m.def("encode_intra", [](int B, int wmb, int hmb, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t ry,
                            uintptr_t ru, uintptr_t rv, uintptr_t qp, int cqo, uintptr_t hdr, uintptr_t coef,
                            uintptr_t nz, uintptr_t intra_flag, uintptr_t intra_count, uintptr_t err, int use_i4x4,

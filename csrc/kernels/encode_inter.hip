@@ -23,6 +23,7 @@ struct InterArgs {
   uint8_t *rec_y, *rec_u, *rec_v;
   const uint8_t* pred_y;   // [B, nmb, 256] from ME
   const int16_t* mv;       // [B, nmb, 2]
+  const int16_t* mv8;      // [B, nmb, 4, 2] per-quadrant vectors of P partitions (nullable: 16x16)
   const int* me_cost;      // [B, nmb]
   const int* intra_cost;   // [B, nmb]
   const int* qp;           // [B]
@@ -384,7 +385,9 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
     const int px0 = mx * 8 + cbx, py0 = my * 8 + cby;
     int pv[4][4];
     if (!a.bmode) {
-      chroma_mc4x4((comp == 0 ? a.ref_u : a.ref_v) + slot * g.csize(), cw, CH, px0, py0, mvx, mvy, pv);
+      // the 4x4 chroma block cb covers luma quadrant cb (its partition's vector)
+      const int cmx = a.mv8 ? a.mv8[o * 8 + cb * 2] : mvx, cmy = a.mv8 ? a.mv8[o * 8 + cb * 2 + 1] : mvy;
+      chroma_mc4x4((comp == 0 ? a.ref_u : a.ref_v) + slot * g.csize(), cw, CH, px0, py0, cmx, cmy, pv);
     } else {
       // the 4x4 chroma block cb covers luma quadrant cb: its lists and vectors
       const bool u0 = h->ref[0][cb] >= 0, u1 = h->ref[1][cb] >= 0;
@@ -567,10 +570,14 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
     h->flags = (use8 && s_t8[half][1]) ? h264::MBF_T8x8 : 0;
     a.intra_flag[o] = 0;
     if (a.bmode) return;  // kind / ref / mv are b_decide's
-    h->kind = h264::MBK_P16x16;
     const uint32_t mvw = (static_cast<uint32_t>(mvx) & 0xFFFFu) | (static_cast<uint32_t>(mvy) << 16);
+    uint4 q4 = make_uint4(mvw, mvw, mvw, mvw);
+    if (a.mv8) q4 = *reinterpret_cast<const uint4*>(a.mv8 + o * 8);
+    // quadrant vectors -> the cheapest partition shape that carries them
+    h->kind = (q4.x == q4.y && q4.z == q4.w) ? (q4.x == q4.z ? h264::MBK_P16x16 : h264::MBK_P16x8)
+                                             : ((q4.x == q4.z && q4.y == q4.w) ? h264::MBK_P8x16 : h264::MBK_P8x8);
     uint4* mvp = reinterpret_cast<uint4*>(&h->mv[0][0][0]);  // 16-byte aligned
-    mvp[0] = make_uint4(mvw, mvw, mvw, mvw);
+    mvp[0] = q4;
     *reinterpret_cast<uint2*>(&h->ref[0][0]) = make_uint2(0u, 0xFFFFFFFFu);  // L0 ref 0, L1 unused
   }
 }
@@ -587,7 +594,7 @@ extern "C" void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t*
                                          const int* intra_cost, const int* qp, int chroma_qp_offset, void* hdr,
                                          int16_t* coef, uint8_t* nz, uint8_t* intra_flag, int* intra_count,
                                          const int8_t* aq, const uint8_t* ref1_u, const uint8_t* ref1_v, int bmode,
-                                         int t8, void* stream) {
+                                         int t8, const int16_t* mv8, void* stream) {
   InterArgs a;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.src_y = src_y;
@@ -601,6 +608,7 @@ extern "C" void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t*
   a.rec_v = rec_v;
   a.pred_y = pred_y;
   a.mv = mv;
+  a.mv8 = bmode ? nullptr : mv8;
   a.me_cost = me_cost;
   a.intra_cost = intra_cost;
   a.qp = qp;
