@@ -361,21 +361,29 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   if (lane < 33) S.nb[lane] = nbv;
   if (lane < 32) S.qoff[lane] = kQOff[lane >> 1][lane & 1];
   wave_sync();
-  // this lane's 4x4 source block (lane & 15) for the SATDs below
-  const int blk = lane & 15;
-  const int px0 = (blk & 3) * 4, py0 = (blk >> 2) * 4;
-  uint32_t srow[4];
+  // MFMA SATD operands shared by the intra estimate and the sub-sample search (see the
+  // sub-sample section below for the formulation)
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  typedef _Float16 v4h __attribute__((ext_vector_type(4)));
+  const int mg = lane >> 4, mn = lane & 15, mb_b = mn & 3;
+  v4h negH;  // A operand: -H16[row mn][k = 4 mg + j], j = 0..3
 #pragma unroll
-  for (int y = 0; y < 4; ++y) srow[y] = S.src[(py0 + y) * 4 + (px0 >> 2)];
-  // ---- open-loop Intra16x16 estimate on source pixels: lane = mode * 16 + block.  Runs
-  // while the candidate reference loads are in flight (it needs only the source MB).
-  // Every mode is written as pred(x, y) = clip((K + CX[x] + RY[y]) >> 5) with per-lane
-  // K, CX, RY (V: CX = 32 top, H: RY = 32 left, DC: K = 32 dc + 16, plane: the linear
-  // form); the neighbour sums behind DC and plane are row reductions of the neighbour
-  // registers (H = sum (t - 7) top[t] - 8 tl, V alike).
+  for (int j = 0; j < 4; ++j) negH[j] = (__builtin_popcount(mn & (4 * mg + j)) & 1) ? _Float16(1.0f) : _Float16(-1.0f);
+  auto as_h = [](uint32_t w) -> v4h {  // 4 samples -> f16 1024 + sample
+    const uint32_t lo = __builtin_amdgcn_perm(0x64646464u, w, 0x04010400u);
+    const uint32_t hi = __builtin_amdgcn_perm(0x64646464u, w, 0x04030402u);
+    const unsigned long long v = (static_cast<unsigned long long>(hi) << 32) | lo;
+    return __builtin_bit_cast(v4h, v);
+  };
+  // ---- open-loop Intra16x16 estimate on source pixels, on MFMA like the sub-sample SATD:
+  // column n = (mode = n >> 2, block column b), lane group g = row g of block row t.
+  // Every mode is written as pred(x, y) = clip((K + CX[x] + RY[y]) >> 5) (V: CX = 32 top,
+  // H: RY = 32 left, DC: K = 32 dc + 16, plane: the linear form); the neighbour sums
+  // behind DC and plane are row reductions of the neighbour registers (H = sum (t - 7)
+  // top[t] - 8 tl, V alike).  Runs while the candidate reference loads are in flight.
   int intra_key = 0x3FFFFFFF;
   if (a.out_intra_cost) {  // null: the caller already has this picture's estimate (B pictures' L1 search)
-    const int mode = lane >> 4;
+    const int mode = mn >> 2;
     const bool has_top = my > 0, has_left = mx > 0;
     const bool ok = (mode == 0 && has_top) || (mode == 1 && has_left) || mode == 2 || (mode == 3 && has_top && has_left);
     const int pk = sum16(lane < 32 ? nbv * ((lane & 15) - 7) + (nbv << 16) : 0);  // weighted + 65536 * plain
@@ -386,24 +394,31 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
     const int pa = 16 * (__builtin_amdgcn_readlane(nbv, 31) + __builtin_amdgcn_readlane(nbv, 15));
     const int pb = (5 * Hs + 32) >> 6, pc = (5 * Vs + 32) >> 6;
     const int dc = (has_top && has_left) ? (st + sl + 16) >> 5 : (has_left ? (sl + 8) >> 4 : (has_top ? (st + 8) >> 4 : 128));
-    const int bx4 = px0, by4 = py0;
-    const int4 top4 = *reinterpret_cast<const int4*>(S.nb + bx4);
-    const int4 left4 = *reinterpret_cast<const int4*>(S.nb + 16 + by4);
-    const int tv[4] = {top4.x, top4.y, top4.z, top4.w}, lv4[4] = {left4.x, left4.y, left4.z, left4.w};
-    const int K = mode == 2 ? 32 * dc + 16 : (mode == 3 ? pa + pb * (bx4 - 7) + pc * (by4 - 7) + 16 : 16);
-    int r[16];
+    const int4 top4 = *reinterpret_cast<const int4*>(S.nb + 4 * mb_b);
+    const int cxv[4] = {mode == 0 ? 32 * top4.x : 0, mode == 0 ? 32 * top4.y : (mode == 3 ? pb : 0),
+                        mode == 0 ? 32 * top4.z : (mode == 3 ? 2 * pb : 0), mode == 0 ? 32 * top4.w : (mode == 3 ? 3 * pb : 0)};
+    const int K = mode == 2 ? 32 * dc + 16 : (mode == 3 ? pa + pb * (4 * mb_b - 7) + 16 : 16);
+    float acc = 0.f;
 #pragma unroll
-    for (int y = 0; y < 4; ++y) {
-      const int ry = mode == 1 ? 32 * lv4[y] : (mode == 3 ? pc * y : 0);
+    for (int t = 0; t < 4; ++t) {
+      const int y = 4 * t + mg;
+      const int ry = mode == 1 ? 32 * S.nb[16 + y] : (mode == 3 ? pc * (y - 7) : 0);
+      int pv[4];
 #pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        const int cxv = mode == 0 ? 32 * tv[x] : (mode == 3 ? pb * x : 0);
-        const int pv = clampi((K + cxv + ry) >> 5, 0, 255);
-        r[y * 4 + x] = static_cast<int>(__builtin_amdgcn_ubfe(srow[y], 8 * x, 8)) - pv;
-      }
+      for (int x = 0; x < 4; ++x) pv[x] = clampi((K + cxv[x] + ry) >> 5, 0, 255);
+      const uint32_t lo = (static_cast<uint32_t>(pv[0]) | (static_cast<uint32_t>(pv[1]) << 16)) | 0x64006400u;
+      const uint32_t hi = (static_cast<uint32_t>(pv[2]) | (static_cast<uint32_t>(pv[3]) << 16)) | 0x64006400u;
+      const v4h ph = __builtin_bit_cast(v4h, (static_cast<unsigned long long>(hi) << 32) | lo);
+      const v4f cs = -__builtin_amdgcn_mfma_f32_16x16x16f16(negH, as_h(S.src[y * 4 + mb_b]), v4f{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      const v4f d = __builtin_amdgcn_mfma_f32_16x16x16f16(negH, ph, cs, 0, 0, 0);
+      acc += __builtin_fabsf(d[0]) + __builtin_fabsf(d[1]) + __builtin_fabsf(d[2]) + __builtin_fabsf(d[3]);
     }
-    const int sv = sum16(h264::satd4x4(r));
-    intra_key = min64(ok ? sv : 0x3FFFFFFF);
+    int sv = static_cast<int>(acc);
+    sv += __shfl_xor(sv, 1, 64);
+    sv += __shfl_xor(sv, 2, 64);
+    sv += __shfl_xor(sv, 16, 64);
+    sv += __shfl_xor(sv, 32, 64);
+    intra_key = min64(ok ? (sv + 1) >> 1 : 0x3FFFFFFF);
   }
   int cx = 0, cy = 0, best_sad = 0x7FFFFFFF;
   {
@@ -569,19 +584,40 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
     const int base = v * kPP + u + psh;
     return avg4(load4(base + offa), load4(base + offb));
   };
-  // SATD of candidate (dqx, dqy) quarter offsets relative to (4bx, 4by): this lane does 4x4 block (lane&15)
+  // ---- sub-sample SATD on MFMA.  One v_mfma_f32_16x16x16_f16 evaluates one 4x4-block row
+  // (blocks (b, t), b = 0..3) of 4 candidates: output column n = lane & 15 = (candidate
+  // c = n >> 2, block b = n & 3) holds the 16 Hadamard coefficients (H4 (x) H4 = the
+  // Sylvester H16, entries (-1)^popcount(i & k)) of the residual s - p:
+  //     D = C_t + (-H16) . (p + 1024),   C_t = H16 (s + 1024) = H16 s + 16384 e_0
+  // with u8 samples entering as the f16 value 1024 + u8 (one v_perm puts the 0x64 exponent
+  // byte beside two samples); the 1024 offsets cancel in the DC row and every value is an
+  // integer below 2^24, so the f32 accumulation is exact.  K = 16: lane group g = lane >> 4
+  // holds row g of its block -- the prediction goes from the LDS planes straight into the B
+  // operand, with no residual or Hadamard butterflies on the VALU; |D| sums use the f32
+  // abs source modifier.  SATD = (sum |D| + 1) / 2, the scalar form up to per-block rounding.
+  v4f cS[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) cS[t] = -__builtin_amdgcn_mfma_f32_16x16x16f16(negH, as_h(S.src[(t * 4 + mg) * 4 + mb_b]),
+                                                                             v4f{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+  // SATD of this lane's candidate (quarter offsets (dqx, dqy) relative to (4bx, 4by))
   auto satd_cand = [&](int dqx, int dqy) -> int {
-    int q = (dqy & 3) * 4 + (dqx & 3), ox = dqx >> 2, oy = dqy >> 2;
-    int offa = S.qoff[2 * q], offb = S.qoff[2 * q + 1];
-    int r[16];
+    const int q = (dqy & 3) * 4 + (dqx & 3), ox = dqx >> 2, oy = dqy >> 2;
+    const int offa = S.qoff[2 * q], offb = S.qoff[2 * q + 1];
+    const int u = mb_b * 4 + ox + 2;
+    float acc = 0.f;
 #pragma unroll
-    for (int y = 0; y < 4; ++y) {
-      const uint32_t pw = pred4(px0 + ox + 2, py0 + y + oy + 2, offa, offb);
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-        r[y * 4 + x] = static_cast<int>((srow[y] >> (8 * x)) & 255u) - static_cast<int>((pw >> (8 * x)) & 255u);
+    for (int t = 0; t < 4; ++t) {
+      const v4f d = __builtin_amdgcn_mfma_f32_16x16x16f16(negH, as_h(pred4(u, t * 4 + mg + oy + 2, offa, offb)), cS[t],
+                                                          0, 0, 0);
+      acc += __builtin_fabsf(d[0]) + __builtin_fabsf(d[1]) + __builtin_fabsf(d[2]) + __builtin_fabsf(d[3]);
     }
-    return sum16(h264::satd4x4(r));
+    // the candidate's 16 lanes: block bits 0-1 and row-group bits 4-5
+    int s = static_cast<int>(acc);
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    return (s + 1) >> 1;
   };
   // candidate c of a 3x3 ring (0 = centre, 1..8 = the 8 neighbours) -> offsets in units of `step`
   auto ring = [](int c, int step, int* dx, int* dy) {
@@ -595,7 +631,7 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
     int bkey = 0x7FFFFFFF;
     const int ncand_h = a.subpel >= 1 ? 9 : 1;
     for (int base = 0; base < ncand_h; base += 4) {
-      int ci = base + (lane >> 4);
+      int ci = base + (mn >> 2);
       int c = ci < ncand_h ? ci : 0;
       int ox, oy;
       ring(c, 2, &ox, &oy);
@@ -612,7 +648,7 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
     if (a.subpel >= 2) {
       int qkey = (best_cost << 4) | 0;
       for (int base = 1; base < 9; base += 4) {
-        int ci = base + (lane >> 4);
+        int ci = base + (mn >> 2);
         int ox, oy;
         ring(ci, 1, &ox, &oy);
         int s = satd_cand(hx + ox, hy + oy);

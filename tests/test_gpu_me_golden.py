@@ -20,9 +20,15 @@ def _se_bits(v):
     return _ue_bits(-2 * v if v <= 0 else 2 * v - 1)
 
 
+_H4 = np.array([[1, 1, 1, 1], [1, 1, -1, -1], [1, -1, -1, 1], [1, -1, 1, -1]])
+
+
+def _hsum(r):
+    return int(np.abs(_H4 @ r @ _H4.T).sum())
+
+
 def _satd(r):
-    h = np.array([[1, 1, 1, 1], [1, 1, -1, -1], [1, -1, -1, 1], [1, -1, 1, -1]])
-    return int(np.abs(h @ r @ h.T).sum()) >> 1
+    return _hsum(r) >> 1
 
 
 class _Planes:
@@ -55,14 +61,16 @@ class _Planes:
             (3, 3): (b[Y + 1, X], h[Y, X + 1]),
         }
         a, c = tab[(xf, yf)]
-        return (int(a) + int(c) + 1) >> 1
+        return int(a), int(c)
 
-    def block(self, x0, y0, mvx, mvy):
+    def block(self, x0, y0, mvx, mvy, rounded=True):
+        """prediction (A + B + 1) >> 1, or the unrounded tap sum A + B (rounded=False)"""
         out = np.zeros((16, 16), dtype=np.int64)
         ix, iy, xf, yf = mvx >> 2, mvy >> 2, mvx & 3, mvy & 3
         for y in range(16):
             for x in range(16):
-                out[y, x] = self.qpel(x0 + x + ix, y0 + y + iy, xf, yf)
+                a, c = self.qpel(x0 + x + ix, y0 + y + iy, xf, yf)
+                out[y, x] = (a + c + 1) >> 1 if rounded else a + c
         return out
 
 
@@ -117,8 +125,9 @@ def _me_ref(src, ref, pred_mv, qp, R, lam_tab, wmb, hmb):
         bx, by = (0, 0) if bp == 4095 else (cx + bp % side - R, cy + bp // side - R)
 
         def cost_q(mvx, mvy):
-            P = pl.block(X0, Y0, mvx, mvy)
-            sat = sum(_satd(S[y:y + 4, x:x + 4] - P[y:y + 4, x:x + 4]) for y in range(0, 16, 4) for x in range(0, 16, 4))
+            # the MFMA form of me.hip: (sum over the MB of |H (2 (S - P))| + 2) / 4
+            T = S - pl.block(X0, Y0, mvx, mvy)
+            sat = (sum(_hsum(T[y:y + 4, x:x + 4]) for y in range(0, 16, 4) for x in range(0, 16, 4)) + 1) >> 1
             return sat + lam * (_se_bits(mvx - pmx) + _se_bits(mvy - pmy))
         bm = (bx * 4, by * 4)
         hk = min(((cost_q(bm[0] + _ring(c, 2)[0], bm[1] + _ring(c, 2)[1]) << 4) | c) for c in range(9))
@@ -150,8 +159,8 @@ def _me_ref(src, ref, pred_mv, qp, R, lam_tab, wmb, hmb):
             a, b, c = 16 * (int(left[15]) + int(top[15])), (5 * Hh + 32) >> 6, (5 * Vv + 32) >> 6
             yy, xx = np.mgrid[0:16, 0:16]
             modes.append(np.clip((a + b * (xx - 7) + c * (yy - 7) + 16) >> 5, 0, 255))
-        best_i = min(sum(_satd(S[y:y + 4, x:x + 4] - M[y:y + 4, x:x + 4]) for y in range(0, 16, 4)
-                         for x in range(0, 16, 4)) for M in modes)
+        best_i = min((sum(_hsum(S[y:y + 4, x:x + 4] - M[y:y + 4, x:x + 4]) for y in range(0, 16, 4)
+                          for x in range(0, 16, 4)) + 1) >> 1 for M in modes)
         out_intra[mb] = best_i + lam * 4
     return out_mv, out_cost, out_pred, out_intra
 
