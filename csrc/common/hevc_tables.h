@@ -223,6 +223,11 @@ static constexpr uint8_t kTransIdxLps[64] = {0,  0,  1,  2,  2,  4,  4,  5,  6, 
 // levels live in coefficient planes shaped like the picture: the level (u, v) of the
 // transform block at (x0, y0) is stored at [y0 + v][x0 + u] (TU = CU for luma,
 // half size for 4:2:0 chroma).
+// Per-CTB QP (cu_qp_delta, one quantization group per CTB = x265 --qg-size 32): `qp` is
+// the QpY the CTB is quantised with.  CUs of the CTB before the first one with a coded
+// residual (z-order granule < qp_first) carry QpY = qp_pred, the prediction from the
+// previous quantization group (8.6.1); a CTB without any coded residual has qp == qp_pred
+// after the encoder's fix-up pass (hevc_qp_fixup), and qp_first = 16.
 struct alignas(16) CtuInfo {
   uint8_t split;        // bit0: 32x32 -> 16x16; bit (1 + q): 16x16 quadrant q -> 8x8
   int8_t qp;            // QpY of the CTB
@@ -231,7 +236,9 @@ struct alignas(16) CtuInfo {
   uint8_t sao_band[3];  // band position per component
   uint8_t pad0;
   int8_t sao_off[3][4]; // offsets per component (edge: categories 1..4; band: 4 bands)
-  uint8_t pad1[8];
+  int8_t qp_pred;       // qPY_PRED of the CTB's quantization group
+  uint8_t qp_first;     // z-order granule of the first CU with a coded residual (16: none)
+  uint8_t pad1[6];
 };
 static_assert(sizeof(CtuInfo) == 32, "CtuInfo is 32 bytes");
 

@@ -4,9 +4,10 @@
 //
 // Coding tools used by this encoder: 32x32 CTBs, CU quadtree
 // 32/16/8, PART_2Nx2N, TU = CU (max_transform_hierarchy_depth 0), 35 intra modes
-// with DM chroma, P slices with one reference picture (merge/skip + AMVP), flat
-// quantisation with one QP per slice, deblocking and SAO, no tiles/WPP (every
-// picture is one slice; pictures entropy-code in parallel on host threads).
+// with DM chroma, P slices with one reference picture (merge/skip + AMVP), one QP per
+// CTB through cu_qp_delta (adaptive quantisation; or one QP per slice), deblocking and
+// SAO, WPP substreams (every picture is one slice; pictures entropy-code in parallel on
+// host threads).
 //
 // Reference parity: `-vcodec libx265 -crf 26` (server.go:67-68, client.go:115).
 #pragma once
@@ -27,6 +28,7 @@ struct HevcConfig {
   int deblock = 1;
   int max_merge = 5;
   int wpp = 0;                 // entropy_coding_sync_enabled_flag: one CABAC substream per CTB row
+  int cu_qp_delta = 0;         // cu_qp_delta_enabled_flag: per-CTB QpY from CtuInfo::qp (AQ)
   int threads = 1;             // host threads coding the WPP substreams of one picture
   int coded_width() const { return (width + kCtb - 1) / kCtb * kCtb; }
   int coded_height() const { return (height + kCtb - 1) / kCtb * kCtb; }

@@ -34,7 +34,7 @@ struct Sps {
 
 struct Pps {
   bool valid = false;
-  int sps_id = 0, init_qp = 26, cb_off = 0, cr_off = 0, num_ref_l0 = 1, log2_pml = 2;
+  int sps_id = 0, init_qp = 26, cb_off = 0, cr_off = 0, num_ref_l0 = 1, log2_pml = 2, diff_qp_depth = 0;
   bool sign_hiding = false, cabac_init_present = false, cu_qp_delta = false, tskip = false, bypass = false;
   bool tiles = false, wpp = false, deblock_disabled = false, deblock_override = false, lists_mod = false;
   bool slice_chroma_offsets = false, constrained_intra = false, weighted = false, output_flag = false;
@@ -94,6 +94,10 @@ struct HevcDecoder::Impl {
   int W = 0, H = 0, bd = 8, maxv = 255, wctb = 0, hctb = 0, slice_type = 2, qp = 26, poc = 0;
   bool idr = false, sao_luma = false, sao_chroma = false, deblock = true;
   int max_merge = 5;
+  // quantization parameters (8.6.1): QpY of the current CU, the quantization group's
+  // prediction and CuQpDeltaVal, QpY of the last CU decoded (qPY_PREV of the next group)
+  int cu_qp = 26, qg_pred = 26, qp_delta_val = 0, last_cu_qp = 26, log2_min_qg = 6;
+  bool qp_delta_coded = false;
   Picture cur;
   std::vector<int8_t> g_pred, g_skip, g_depth, g_mode, g_qp, g_cbf, g_done;  // per 4x4 luma block
   std::vector<int16_t> g_mvx, g_mvy;
@@ -174,7 +178,7 @@ struct HevcDecoder::Impl {
     p.constrained_intra = br.get(1);
     p.tskip = br.get(1);
     p.cu_qp_delta = br.get(1);
-    if (p.cu_qp_delta) throw std::runtime_error("HEVC: cu_qp_delta unsupported");
+    if (p.cu_qp_delta) p.diff_qp_depth = br.get_ue();
     p.cb_off = br.get_se();
     p.cr_off = br.get_se();
     p.slice_chroma_offsets = br.get(1);
@@ -313,6 +317,10 @@ struct HevcDecoder::Impl {
     cd = &dec;
     dec.start();
     init_contexts(ctx, slice_type == 2 ? 0 : 1, qp);
+    cu_qp = qg_pred = last_cu_qp = qp;
+    qp_delta_val = 0;
+    log2_min_qg = sps.log2_ctb - pps.diff_qp_depth;
+    if (pps.cu_qp_delta && log2_min_qg < sps.log2_min_cb) throw std::runtime_error("HEVC: diff_cu_qp_delta_depth out of range");
     const int nctb = wctb * hctb;
     const size_t data0 = 1 + br.pos() / 8;  // rbsp index of the slice data
     auto escaped = [&](size_t r) {  // rbsp index -> byte offset in the escaped NAL payload
@@ -333,6 +341,7 @@ struct HevcDecoder::Impl {
         dec.start();
         if (wctb >= 2) std::copy(wpp_ctx, wpp_ctx + kNumCtx, ctx);
         else init_contexts(ctx, slice_type == 2 ? 0 : 1, qp);
+        last_cu_qp = qp;  // 8.6.1: first quantization group of a CTB row with WPP
       }
       if (sps.sao && (sao_luma || sao_chroma)) parse_sao(rx, ry);
       coding_quadtree(rx << sps.log2_ctb, ry << sps.log2_ctb, sps.log2_ctb, 0, rx, ry);
@@ -428,6 +437,7 @@ struct HevcDecoder::Impl {
   // ------------------------------------------------------------ coding quadtree (7.3.8.4)
   void coding_quadtree(int x0, int y0, int log2, int depth, int rx, int ry) {
     const int n = 1 << log2;
+    if (pps.cu_qp_delta && log2 >= log2_min_qg) start_qg(x0, y0);
     bool split;
     if (x0 + n <= W && y0 + n <= H && log2 > sps.log2_min_cb) {
       int c = 0;
@@ -465,7 +475,7 @@ struct HevcDecoder::Impl {
         g_mode[k] = static_cast<int8_t>(mode);
         g_mvx[k] = static_cast<int16_t>(mvx);
         g_mvy[k] = static_cast<int16_t>(mvy);
-        g_qp[k] = static_cast<int8_t>(qp);
+        g_qp[k] = static_cast<int8_t>(cu_qp);
       }
     const int ctb = 1 << sps.log2_ctb;
     for (int y = y0; y < y0 + n; y += 8)
@@ -489,8 +499,62 @@ struct HevcDecoder::Impl {
       for (int x = x0; x < x0 + n; x += 4) g_done[g4(x, y)] = 1;
   }
 
+  // 8.6.1 start of a quantization group: IsCuQpDeltaCoded = 0, CuQpDeltaVal = 0 and
+  // qPY_PRED from the left / above groups when they lie in the same CTB, else qPY_PREV
+  void start_qg(int x0, int y0) {
+    qp_delta_coded = false;
+    qp_delta_val = 0;
+    const int prev = last_cu_qp;
+    const int cm = ~((1 << sps.log2_ctb) - 1);
+    auto nb = [&](int x, int y) {
+      if (!done(x, y) || (x & cm) != (x0 & cm) || (y & cm) != (y0 & cm)) return prev;
+      return static_cast<int>(g_qp[g4(x, y)]);
+    };
+    qg_pred = (nb(x0 - 1, y0) + nb(x0, y0 - 1) + 1) >> 1;
+    if (!pps.cu_qp_delta) qg_pred = qp;
+    cu_qp = qg_pred;
+    if (x0 % (1 << sps.log2_ctb) == 0 && y0 % (1 << sps.log2_ctb) == 0 && sps.log2_ctb == kCtbLog2) {
+      CtuInfo& t = rec_ctu[(y0 >> kCtbLog2) * wctb + (x0 >> kCtbLog2)];
+      t.qp = static_cast<int8_t>(qg_pred);
+      t.qp_pred = static_cast<int8_t>(qg_pred);
+      t.qp_first = 16;
+    }
+  }
+  // cu_qp_delta_abs / _sign_flag (7.3.8.10, 9.3.3.10) -> QpY of the CU (8.6.1)
+  void parse_qp_delta(int x0, int y0) {
+    int a = 0;
+    while (a < 5 && cd->decode(ctx[CTX_CU_QP_DELTA + (a > 0)])) ++a;
+    if (a == 5) {
+      int k = 0;
+      while (cd->bypass()) {
+        a += 1 << k;
+        if (++k > 30) throw std::runtime_error("HEVC: cu_qp_delta_abs suffix too long");
+      }
+      while (k--) a += cd->bypass() << k;
+    }
+    const int d = a && cd->bypass() ? -a : a;
+    const int off = 6 * (bd - 8);
+    if (d < -(26 + off / 2) || d > 25 + off / 2) throw std::runtime_error("HEVC: CuQpDeltaVal out of range");
+    qp_delta_coded = true;
+    qp_delta_val = d;
+    cu_qp = ((qg_pred + d + 52 + 2 * off) % (52 + off)) - off;
+    if (sps.log2_ctb == kCtbLog2) {
+      CtuInfo& t = rec_ctu[(y0 >> kCtbLog2) * wctb + (x0 >> kCtbLog2)];
+      t.qp = static_cast<int8_t>(cu_qp);
+      t.qp_first = static_cast<uint8_t>(zorder8((x0 & 31) >> 3, (y0 & 31) >> 3));
+    }
+  }
+
   // ------------------------------------------------------------ coding unit (7.3.8.5)
   void coding_unit(int x0, int y0, int log2, int depth, int rx, int ry) {
+    coding_unit_syntax(x0, y0, log2, depth, rx, ry);
+    // the CU's QpY (deblocking, and qPY_PREV of the next quantization group)
+    const int n = 1 << log2;
+    for (int y = y0; y < y0 + n; y += 4)
+      for (int x = x0; x < x0 + n; x += 4) g_qp[g4(x, y)] = static_cast<int8_t>(cu_qp);
+    last_cu_qp = cu_qp;
+  }
+  void coding_unit_syntax(int x0, int y0, int log2, int depth, int rx, int ry) {
     (void)rx;
     (void)ry;
     const int n = 1 << log2;
@@ -732,6 +796,7 @@ struct HevcDecoder::Impl {
     const int cbf_cr = cd->decode(ctx[CTX_CBF_CHROMA + 0]);
     int cbf_y = 1;
     if (intra || cbf_cb || cbf_cr) cbf_y = cd->decode(ctx[CTX_CBF_LUMA + 1]);
+    if (pps.cu_qp_delta && !qp_delta_coded && (cbf_y || cbf_cb || cbf_cr)) parse_qp_delta(x0, y0);
     if (log2 == 2) throw std::runtime_error("HEVC: 4x4 luma TUs unsupported");
     const int n = 1 << log2;
     for (int y = y0; y < y0 + n; y += 4)
@@ -940,10 +1005,10 @@ struct HevcDecoder::Impl {
     const int qpy_off = 6 * (bd - 8);
     int qpp;
     if (cidx == 0) {
-      qpp = qp + qpy_off;
+      qpp = cu_qp + qpy_off;
     } else {
       const int off = cidx == 1 ? pps.cb_off : pps.cr_off;
-      const int qpi = clip3(-qpy_off, 57, qp + off);
+      const int qpi = clip3(-qpy_off, 57, cu_qp + off);
       qpp = chroma_qp_map(qpi) + qpy_off;
     }
     const int bdshift = bd + log2 - 5;

@@ -154,7 +154,8 @@ std::vector<uint8_t> hevc_parameter_sets(const HevcConfig& c) {
     bw.put_se(0);   // init_qp_minus26
     bw.put_bit(0);  // constrained_intra_pred_flag
     bw.put_bit(0);  // transform_skip_enabled_flag
-    bw.put_bit(0);  // cu_qp_delta_enabled_flag
+    bw.put_bit(c.cu_qp_delta ? 1 : 0);  // cu_qp_delta_enabled_flag
+    if (c.cu_qp_delta) bw.put_ue(0);      // diff_cu_qp_delta_depth: one quantization group per CTB
     bw.put_se(0);   // pps_cb_qp_offset
     bw.put_se(0);   // pps_cr_qp_offset
     bw.put_bit(0);  // pps_slice_chroma_qp_offsets_present_flag
@@ -208,6 +209,11 @@ struct Writer {
   std::vector<int8_t>&depth, &skip, &pred, &mode;
   std::vector<int16_t>&mvx, &mvy;
   std::vector<uint8_t>& coded;
+  // cu_qp_delta state (7.4.9.14, 8.6.1): qPY_PREV of the next quantization group (the
+  // slice QP at the start of the slice and, with WPP, of every CTB row: a Writer codes
+  // one row substream or the whole slice), and whether the current CTB coded its delta
+  int qp_prev = 0, qp_ctb = 0;
+  bool qp_coded = false;
 
   Writer(const HevcConfig& cfg, const HevcFrameParams& f, const CtuInfo* ct, const CuInfo* cu_, const int16_t* cy,
          const int16_t* cb, const int16_t* cr, CabacEncoder& enc, PicState& ps)
@@ -224,6 +230,7 @@ struct Writer {
     h8 = H / 8;
     pslice = fp.slice_type == 1;
     init_contexts(ctx, pslice ? 1 : 0, fp.qp);
+    qp_prev = fp.qp;
   }
 
   size_t g(int x, int y) const { return static_cast<size_t>(y >> 3) * w8 + (x >> 3); }
@@ -716,16 +723,7 @@ struct Writer {
       e.bypass(dy < 0);
     }
   }
-  void write_eg1(uint32_t v) {  // 9.3.3.3 k-th order Exp-Golomb, k = 1
-    int k = 1;
-    while (v >= (1u << k)) {
-      e.bypass(1);
-      v -= 1u << k;
-      ++k;
-    }
-    e.bypass(0);
-    while (k--) e.bypass((v >> k) & 1);
-  }
+  void write_eg1(uint32_t v) { write_egk(v, 1); }
 
   // transform_tree at depth 0 with TU = CU (7.3.8.8 / 7.3.8.10)
   void write_tu(int x, int y, int log2, bool intra, int m, bool cb_y, bool cb_cb, bool cb_cr) {
@@ -733,6 +731,7 @@ struct Writer {
     e.encode(cb_cr, ctx[CTX_CBF_CHROMA + 0]);
     if (intra || cb_cb || cb_cr) e.encode(cb_y, ctx[CTX_CBF_LUMA + 1]);
     else if (!cb_y) throw std::runtime_error("inter TU: cbf_luma inferred 1 but the luma block is empty");
+    if (c.cu_qp_delta && !qp_coded && (cb_y || cb_cb || cb_cr)) write_qp_delta();
     const int stride = W, cstride = W / 2;
     if (cb_y) {
       const int scan = (intra && log2 == 3) ? mdcs(m) : 0;
@@ -743,10 +742,40 @@ struct Writer {
     if (cb_cr) write_residual(coef[2] + static_cast<size_t>(y / 2) * cstride + x / 2, cstride, log2 - 1, 2, scan_c);
   }
 
+  // cu_qp_delta_abs (9.3.3.10: TR prefix cMax 5, ctxInc 0 then 1; EG0 bypass suffix) and
+  // the bypass sign, in the first TU of the CTB with a coded block
+  void write_qp_delta() {
+    const int d = qp_ctb - qp_prev;
+    const int qbd = 6 * (c.bit_depth - 8);
+    if (d < -(26 + qbd / 2) || d > 25 + qbd / 2) throw std::runtime_error("HEVC: CuQpDeltaVal out of range");
+    const int a = std::abs(d), pre = std::min(a, 5);
+    for (int i = 0; i < pre; ++i) e.encode(1, ctx[CTX_CU_QP_DELTA + (i > 0)]);
+    if (pre < 5) e.encode(0, ctx[CTX_CU_QP_DELTA + (pre > 0)]);
+    else write_egk(static_cast<uint32_t>(a - 5), 0);
+    if (a) e.bypass(d < 0);
+    qp_coded = true;
+  }
+  void write_egk(uint32_t v, int k) {  // 9.3.3.3 k-th order Exp-Golomb, bypass
+    while (v >= (1u << k)) {
+      e.bypass(1);
+      v -= 1u << k;
+      ++k;
+    }
+    e.bypass(0);
+    while (k--) e.bypass((v >> k) & 1);
+  }
+
   // coding_quadtree (7.3.8.4) of one CTB
   void write_ctu(int rx, int ry) {
+    write_ctu_tree(rx, ry);
+    // QpY of the CTB's last CU: the coded QP, or the prediction when no TU carried a delta
+    if (c.cu_qp_delta && qp_coded) qp_prev = qp_ctb;
+  }
+  void write_ctu_tree(int rx, int ry) {
     const CtuInfo& t = ctu[ry * wctb + rx];
     const int x0 = rx * kCtb, y0 = ry * kCtb;
+    qp_ctb = t.qp;
+    qp_coded = false;
     auto split_ctx = [&](int x, int y, int d) {
       return (avail(x - 1, y) && depth[g(x - 1, y)] > d) + (avail(x, y - 1) && depth[g(x, y - 1)] > d);
     };

@@ -62,8 +62,10 @@ __global__ __launch_bounds__(256) void h264_aq_offsets(Geom g, const uint8_t* __
   ss = sum16(ss);
   const int cr_s = __shfl(cb_s, (lane_id() & ~15) + 8, 64), cr_ss = __shfl(cb_ss, (lane_id() & ~15) + 8, 64);
   if (live && l == 0) {
-    const uint32_t e = static_cast<uint32_t>(ss - ((s * s) >> 8)) + static_cast<uint32_t>(cb_ss - ((cb_s * cb_s) >> 6)) +
-                       static_cast<uint32_t>(cr_ss - ((cr_s * cr_s) >> 6));
+    // the squared luma sum exceeds INT_MAX once the MB mean passes 181: unsigned products
+    const uint32_t us = static_cast<uint32_t>(s);
+    const uint32_t e = (static_cast<uint32_t>(ss) - ((us * us) >> 8)) +
+                       static_cast<uint32_t>(cb_ss - ((cb_s * cb_s) >> 6)) + static_cast<uint32_t>(cr_ss - ((cr_s * cr_s) >> 6));
     float adj = strength * 1.0397f * (log2f(static_cast<float>(e > 1u ? e : 1u)) - 14.427f);
     if (extra) adj += extra[slot * extra_stride + mb];  // MB-tree offset of this frame
     out[static_cast<size_t>(slot) * nmb + mb] = static_cast<int8_t>(clampi(static_cast<int>(rintf(adj)), -24, 24));

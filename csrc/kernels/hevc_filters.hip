@@ -121,9 +121,9 @@ __global__ __launch_bounds__(256) void hevc_proxy8(const uint16_t* __restrict__ 
 struct HevcDbkArgs {
   int B, W, H, wctb, bd;
   uint16_t *y, *u, *v;
-  const CuInfo* cu;  // [B, nctb * 16]
-  const int* qp;     // [B]
-  const int8_t* run; // [B]
+  const CuInfo* cu;    // [B, nctb * 16]
+  const CtuInfo* ctu;  // [B, nctb]: QpY of the CTB's CUs (qp, qp_pred, qp_first)
+  const int8_t* run;   // [B]
   int dir;           // 0 vertical edges, 1 horizontal edges
 };
 
@@ -134,6 +134,14 @@ __device__ __forceinline__ const CuInfo& cu_at(const HevcDbkArgs& a, int slot, i
 }
 
 __device__ __forceinline__ int clip3i(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// QpY of the CU covering luma sample (x, y) (8.6.1 with one quantization group per CTB):
+// CUs before the CTB's first coded residual keep the group's prediction
+__device__ __forceinline__ int qp_at(const HevcDbkArgs& a, int slot, int x, int y) {
+  const int nctb = a.wctb * (a.H / 32);
+  const CtuInfo& t = a.ctu[static_cast<size_t>(slot) * nctb + (y >> 5) * a.wctb + (x >> 5)];
+  return hevc::zorder8((x & 31) >> 3, (y & 31) >> 3) < t.qp_first ? t.qp_pred : t.qp;
+}
 
 __global__ void hevc_deblock(HevcDbkArgs a) {
   const int slot = blockIdx.y;
@@ -165,7 +173,7 @@ __global__ void hevc_deblock(HevcDbkArgs a) {
   else bs = 0;
   if (!bs) return;
   const int bd = a.bd, maxv = (1 << bd) - 1;
-  const int qpl = a.qp[slot];  // one QP per picture: QpP == QpQ
+  const int qpl = (qp_at(a, slot, xp, yp) + qp_at(a, slot, xq, yq) + 1) >> 1;  // 8.7.2.5.3
   const int qb = clip3i(0, 51, qpl), qt = clip3i(0, 53, qpl + 2 * (bs - 1));
   const int beta = hevc::kBetaTable[qb] << (bd - 8), tc = hevc::kTcTable[qt] << (bd - 8);
   const int W = a.W;
@@ -234,7 +242,7 @@ struct HevcSaoArgs {
   uint16_t *y, *u, *v;            // output (final reconstruction)
   const uint16_t *sy, *su, *sv;   // source
   CtuInfo* ctu;
-  const int* qp;
+  const int* qp;   // [B, nctb] QpY per CTB
   const int8_t* run;
   int enable;
 };
@@ -316,7 +324,7 @@ __global__ __launch_bounds__(256) void hevc_sao(HevcSaoArgs a) {
   __syncthreads();
   // ---- decision (thread 0: luma, thread 1: chroma pair)
   if (tid < 2) {
-    const int qp = a.qp[slot];
+    const int qp = a.qp[static_cast<size_t>(slot) * a.wctb * a.hctb + ci];
     const double lam = 0.57 * exp2((qp - 12) / 3.0) * static_cast<double>(1 << (2 * (bd - 8)));
     const int cmax = (1 << (min(bd, 10) - 5)) - 1;
     const int c0 = tid == 0 ? 0 : 1, nc = tid == 0 ? 1 : 2;
@@ -445,6 +453,91 @@ __global__ __launch_bounds__(256) void hevc_sao(HevcSaoArgs a) {
   }
 }
 
+
+// ============================================================== adaptive quantisation
+// Per-CTB QP (x265 --aq-mode 1 --qg-size 32, the libx265 default family of the
+// reference's "265" preset, server.go:67-68): each 16x16 block gets x264's variance-AQ
+// offset strength * 1.0397 * (log2(AC energy) - 14.427 - 2 (bd - 8)), energy = var(Y
+// 16x16) + var(Cb 8x8) + var(Cr 8x8) at the coded bit depth (+ an optional per-block
+// float offset, e.g. MB-tree); the CTB's QP offset is the rounded mean of its four
+// blocks (x265 averages the AQ partitions of a quantization group), clamped to +-12 so
+// that consecutive CTBs stay within CuQpDeltaVal's range.  One wave per 16x16 block.
+__global__ __launch_bounds__(256) void hevc_aq_ctb(int W, int H, int bd, const uint16_t* __restrict__ sy,
+                                                   const uint16_t* __restrict__ su, const uint16_t* __restrict__ sv,
+                                                   const int* __restrict__ qp, float strength,
+                                                   const float* __restrict__ extra, long long extra_stride,
+                                                   int* __restrict__ ctb_qp, int8_t* __restrict__ mb_aq) {
+  __shared__ float s_off[4];
+  const int wctb = W / 32, nctb = wctb * (H / 32), wmb = W / 16, nmb = wmb * (H / 16);
+  const int ci = blockIdx.x, slot = blockIdx.y;
+  const int q = wave_id(), l = lane_id();
+  const int mx = (ci % wctb) * 2 + (q & 1), my = (ci / wctb) * 2 + (q >> 1);
+  const uint16_t* py = sy + static_cast<size_t>(slot) * W * H + static_cast<size_t>(my * 16 + (l >> 2)) * W + mx * 16 + (l & 3) * 4;
+  const uint2 wy = *reinterpret_cast<const uint2*>(py);
+  const int cw = W / 2;
+  const uint16_t* pc = (l < 32 ? su : sv) + static_cast<size_t>(slot) * cw * (H / 2) +
+                       static_cast<size_t>(my * 8 + ((l & 31) >> 2)) * cw + mx * 8 + (l & 3) * 2;
+  const uint32_t wc = *reinterpret_cast<const uint32_t*>(pc);
+  const int y0 = wy.x & 0xFFFF, y1 = wy.x >> 16, y2 = wy.y & 0xFFFF, y3 = wy.y >> 16;
+  const int c0 = wc & 0xFFFF, c1 = wc >> 16;
+  const int s = sum64(y0 + y1 + y2 + y3), cs = sum32(c0 + c1);
+  const int ss = sum64(y0 * y0 + y1 * y1 + y2 * y2 + y3 * y3), css = sum32(c0 * c0 + c1 * c1);
+  const int cs_v = __shfl(cs, 32, 64), css_v = __shfl(css, 32, 64);
+  if (l == 0) {
+    const long long e = (ss - ((static_cast<long long>(s) * s) >> 8)) + (css - ((static_cast<long long>(cs) * cs) >> 6)) +
+                        (css_v - ((static_cast<long long>(cs_v) * cs_v) >> 6));
+    float adj = 0.0f;
+    if (strength > 0.0f)
+      adj = strength * 1.0397f * (log2f(static_cast<float>(e > 1 ? e : 1)) - (14.427f + 2.0f * (bd - 8)));
+    if (extra) adj += extra[slot * extra_stride + my * wmb + mx];
+    s_off[q] = adj;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int off = clampi(static_cast<int>(rintf(0.25f * (s_off[0] + s_off[1] + s_off[2] + s_off[3]))), -12, 12);
+    const int base = qp[slot];
+    const int v = clampi(base + off, 0, 51);
+    ctb_qp[static_cast<size_t>(slot) * nctb + ci] = v;
+    if (mb_aq) {
+      const int r0 = (ci / wctb) * 2, c0i = (ci % wctb) * 2;
+      int8_t* m = mb_aq + static_cast<size_t>(slot) * nmb;
+      m[r0 * wmb + c0i] = m[r0 * wmb + c0i + 1] = m[(r0 + 1) * wmb + c0i] = m[(r0 + 1) * wmb + c0i + 1] =
+          static_cast<int8_t>(v - base);
+    }
+  }
+}
+
+// QpY bookkeeping after reconstruction (8.6.1, one quantization group per CTB): the
+// group's prediction is the QpY of the previous CTB in decoding order (the slice QP at
+// the start of the slice and, with WPP, of every CTB row); the CTB's delta is coded in
+// its first CU with a coded residual, earlier CUs keep the prediction, and a CTB
+// without any coded residual takes the prediction as its QpY.  Deblocking and the
+// CABAC writer read the result.  One thread per CTB row (WPP) or per slot.
+__global__ __launch_bounds__(256) void hevc_qp_fixup(int wctb, int hctb, CtuInfo* __restrict__ ctu,
+                                                     const CuInfo* __restrict__ cu, const int* __restrict__ qp,
+                                                     const int8_t* __restrict__ run, int wpp) {
+  const int slot = blockIdx.x;
+  if (run[slot] == 0) return;
+  const int nctb = wctb * hctb;
+  const int rows_per = wpp ? 1 : hctb;
+  for (int r0 = threadIdx.x * rows_per; r0 < hctb; r0 += blockDim.x * rows_per) {
+    int prev = qp[slot];
+    for (int r = r0; r < r0 + rows_per; ++r)
+      for (int x = 0; x < wctb; ++x) {
+        const size_t c = static_cast<size_t>(slot) * nctb + r * wctb + x;
+        const CuInfo* g = cu + c * 16;
+        int first = 16;
+        for (int k = 15; k >= 0; --k)
+          if (g[k].cbf) first = k;
+        CtuInfo& t = ctu[c];
+        t.qp_pred = static_cast<int8_t>(prev);
+        t.qp_first = static_cast<uint8_t>(first);
+        if (first == 16) t.qp = static_cast<int8_t>(prev);
+        prev = t.qp;
+      }
+  }
+}
+
 }  // namespace gpu
 }  // namespace mivc
 
@@ -494,8 +587,8 @@ extern "C" int mivc_launch_hevc_proxy8(const uint16_t* src, uint8_t* dst, long l
 }
 
 extern "C" void mivc_launch_hevc_deblock(int B, int W, int H, int bd, uint16_t* y, uint16_t* u, uint16_t* v,
-                                         const void* cu, const int* qp, const int8_t* run, void* stream) {
-  HevcDbkArgs a{B, W, H, W / 32, bd, y, u, v, static_cast<const CuInfo*>(cu), qp, run, 0};
+                                         const void* cu, const void* ctu, const int8_t* run, void* stream) {
+  HevcDbkArgs a{B, W, H, W / 32, bd, y, u, v, static_cast<const CuInfo*>(cu), static_cast<const CtuInfo*>(ctu), run, 0};
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int nv = (W / 8 - 1) * (H / 4), nh = (W / 4) * (H / 8 - 1);
   if (nv > 0) hipLaunchKernelGGL(hevc_deblock, dim3((nv + 255) / 256, B), dim3(256), 0, s, a);
@@ -509,4 +602,19 @@ extern "C" void mivc_launch_hevc_sao(int B, int W, int H, int bd, const uint16_t
                                      const int8_t* run, int enable, void* stream) {
   HevcSaoArgs a{B, W, H, W / 32, H / 32, bd, dy, du, dv, y, u, v, sy, su, sv, static_cast<CtuInfo*>(ctu), qp, run, enable};
   hipLaunchKernelGGL(hevc_sao, dim3((W / 32) * (H / 32), B), dim3(256), 0, static_cast<hipStream_t>(stream), a);
+}
+
+// ctb_qp: [B, nctb] int32 out; mb_aq: [B, nmb16] int8 out (may be null); extra: optional
+// per-16x16 float offsets of slot s at extra + s * extra_stride
+extern "C" void mivc_launch_hevc_aq(int B, int W, int H, int bd, const uint16_t* sy, const uint16_t* su,
+                                    const uint16_t* sv, const int* qp, float strength, const float* extra,
+                                    long long extra_stride, int* ctb_qp, int8_t* mb_aq, void* stream) {
+  hipLaunchKernelGGL(hevc_aq_ctb, dim3((W / 32) * (H / 32), B), dim3(256), 0, static_cast<hipStream_t>(stream), W, H,
+                     bd, sy, su, sv, qp, strength, extra, extra_stride, ctb_qp, mb_aq);
+}
+
+extern "C" void mivc_launch_hevc_qp_fixup(int B, int W, int H, void* ctu, const void* cu, const int* qp,
+                                          const int8_t* run, int wpp, void* stream) {
+  hipLaunchKernelGGL(hevc_qp_fixup, dim3(B), dim3(256), 0, static_cast<hipStream_t>(stream), W / 32, H / 32,
+                     static_cast<CtuInfo*>(ctu), static_cast<const CuInfo*>(cu), qp, run, wpp);
 }

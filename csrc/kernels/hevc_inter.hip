@@ -30,7 +30,7 @@ struct HevcInterArgs {
   CtuInfo* ctu;
   CuInfo* cu;
   int16_t *coef_y, *coef_u, *coef_v;
-  const int* qp;
+  const int* qp;          // [B, nctb] QpY per CTB
   const int8_t* run;
   const int* cand;       // [B, nctb, 2, 21] intra analysis: best cost / mode per CU
   const int16_t* mv;     // [B, nmb16, 2] quarter-sample vectors per 16x16 block
@@ -52,7 +52,7 @@ __global__ __launch_bounds__(64) void hevc_p_decide(HevcInterArgs a) {
   const size_t cb = static_cast<size_t>(slot) * g.nctb() + ci;
   const int* cd = a.cand + cb * 42;
   const int wmb = g.W / 16, nmb = wmb * (g.H / 16);
-  const int qp = a.qp[slot];
+  const int qp = a.qp[cb];
   const int lam = lambda_satd_i(qp, a.bd);
   __shared__ int s_inter[4], s_mvx[4], s_mvy[4], s_split8[4], s_intra[4];
   __shared__ int s_split;
@@ -220,7 +220,7 @@ __global__ __launch_bounds__(64) void hevc_inter_cu(HevcInterArgs a) {
   const int X0 = rx * 32 + (lg == 5 ? 0 : (q & 1) * 16), Y0 = ry * 32 + (lg == 5 ? 0 : (q >> 1) * 16);
   const int mvx = cu[kq].mv[0], mvy = cu[kq].mv[1];
   const int bd = a.bd, maxv = (1 << bd) - 1;
-  const int qpy = a.qp[slot], off = 6 * (bd - 8);
+  const int qpy = a.qp[cb], off = 6 * (bd - 8);
   const int qpl = qpy + off, qpc = hevc::chroma_qp_map(clampi(qpy, -off, 57)) + off;
   int cbf = 0;
   for (int c = 0; c < 3; ++c) {

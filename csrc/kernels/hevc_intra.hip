@@ -28,7 +28,7 @@ struct HevcIntraArgs {
   CtuInfo* ctu;                           // [B, nctb]
   CuInfo* cu;                             // [B, nctb * 16]
   int16_t *coef_y, *coef_u, *coef_v;      // [B] level planes
-  const int* qp;                          // [B] QpY
+  const int* qp;                          // [B, nctb] QpY per CTB (AQ, hevc_aq_ctb)
   const int8_t* run;                      // [B] 0 idle, 1 all CUs (I picture), 2 intra CUs only (P picture)
   int* cand;                              // [B, nctb, 2, 21] best cost / mode per CU of the analysis (may be null)
   int bd;
@@ -256,7 +256,7 @@ __global__ __launch_bounds__(256) void hevc_intra_analyze(HevcIntraArgs a) {
     __syncthreads();
   }
   __syncthreads();
-  const int qp = a.qp[slot];
+  const int qp = a.qp[static_cast<size_t>(slot) * g.nctb() + ci];
   const int lam = lambda_satd(qp, bd);
   if (tid < kCuCount) {
     int bm = 0, bc = 0x7FFFFFFF;
@@ -439,7 +439,7 @@ __device__ void hevc_recon_ctb(const HevcIntraArgs& a, ReconShared& S, const hv:
   }
   wave_sync();
   const int split = __builtin_amdgcn_readfirstlane(a.ctu[cb].split);
-  const int qpy = a.qp[slot];
+  const int qpy = a.qp[cb];
   const int off = 6 * (a.bd - 8);
   const int qpl = qpy + off;
   const int qpc = hevc::chroma_qp_map(clampi(qpy, -off, 57)) + off;

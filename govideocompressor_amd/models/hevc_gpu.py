@@ -5,9 +5,11 @@ client.go:115) with gfx950 kernels + a host CABAC writer:
 
 per frame step t (frame t of every slot):
   prep (u8/u16 -> padded u16 planes)
+  -> hevc_aq: per-CTB QP (variance AQ + MB-tree offsets, one quantization group per CTB)
   -> I: hevc_intra_analyze (CTB-parallel open-loop CU/mode decision)
         + hevc_intra_recon (CTB wavefront, closed loop)
      P: lookahead motion search + hevc_inter (CU-parallel) + intra CUs (wavefront)
+  -> hevc_qp_fixup (QpY of CTBs / CUs without a coded delta, 8.6.1)
   -> hevc_deblock (vertical, then horizontal edges; picture-parallel)
   -> hevc_sao (per-CTB statistics, decision, apply)
 then the decision records + level planes go to pinned host memory and a host thread
@@ -54,10 +56,21 @@ class HevcParams:
     # x265 --wpp (its default): one CABAC substream per CTB row; the host codes the rows of
     # one picture on several threads when fewer pictures than entropy threads are in flight
     wpp: bool = True
+    # x265 --aq-mode 1 --aq-strength 1.0 --qg-size 32: variance AQ per 16x16 block, averaged
+    # into one QP per CTB coded with cu_qp_delta (csrc/kernels/hevc_filters.hip hevc_aq_ctb);
+    # 0 disables
+    aq_strength: float = 1.0
+    # x265 --cutree (default on): lookahead propagation -> per-block QP offsets added before
+    # the CTB average (needs the lookahead and its block grid equal to the 16x16 grid)
+    cutree: bool = True
+
+    def adaptive_qp(self) -> bool:
+        return self.aq_strength > 0 or (self.cutree and self.lookahead and self.crf is not None)
 
     def host_cfg(self) -> dict:
         return dict(width=self.width, height=self.height, bit_depth=self.bit_depth, fps=self.fps,
-                    sao=int(self.sao), deblock=int(self.deblock), max_merge=self.max_merge, wpp=int(self.wpp))
+                    sao=int(self.sao), deblock=int(self.deblock), max_merge=self.max_merge, wpp=int(self.wpp),
+                    cu_qp_delta=int(self.adaptive_qp()))
 
     def frame_qps(self) -> tuple[int, int]:
         qp_p = int(round(self.crf)) if self.crf is not None else int(self.qp)
@@ -128,6 +141,9 @@ class GpuHevcEncoder:
         self.copy_done = [torch.cuda.Event() for _ in range(2)]
         self.host_bufs = None  # lazily: 3 sets of pinned host buffers
         self.qp = torch.zeros((B,), dtype=torch.int32, device=dev)
+        self.ctb_qp = torch.zeros((B, self.nctb), dtype=torch.int32, device=dev)  # QpY per CTB
+        self.mb_aq = torch.zeros((B, nmb), dtype=torch.int8, device=dev)           # ME lambda offsets
+        self._cutree = None  # [B, F, nmb] float MB-tree offsets of the batch being encoded
         self.run = torch.zeros((B,), dtype=torch.int8, device=dev)
         self.err = torch.zeros((1,), dtype=torch.int32, device=dev)
         self.params_nal = self.host.hevc_parameter_sets(params.host_cfg())
@@ -183,12 +199,18 @@ class GpuHevcEncoder:
         y8 = y
         if y.dtype != torch.uint8:
             y8 = (y >> (self.p.bit_depth - 8)).clamp_(0, 255).to(torch.uint8)
-        costs = self._la.frame_costs(y8.contiguous()).cpu().numpy()
         lbw, lbh = GpuLookahead.block_grid(y.shape[3], y.shape[2])
-        from ..rc.ratecontrol import scenecut_flags
+        from ..rc.ratecontrol import MBTREE_STRENGTH, scenecut_flags
+        # cutree needs the lookahead's block grid to be the coded 16x16 grid (no -s resize)
+        use_tree = self.p.cutree and lbw == self.wmb and lbh == self.hmb
+        if use_tree:
+            costs_d, self._cutree = self._la.mbtree(y8.contiguous(), MBTREE_STRENGTH)
+            costs = costs_d.cpu().numpy()
+        else:
+            costs = self._la.frame_costs(y8.contiguous()).cpu().numpy()
         self._scenecuts = scenecut_flags(costs, float(self.p.scenecut), keyint=self.p.keyint or None)
         q = crf_qps_batch(costs, float(self.p.crf), lbw * lbh, keyint=self.p.keyint or None,
-                          scenecuts=self._scenecuts)
+                          scenecuts=self._scenecuts, mbtree=use_tree)
         self.stats["scenecuts"] = int(self._scenecuts.sum())
         self.timings["lookahead_s"] = self.timings.get("lookahead_s", 0.0) + time.perf_counter() - t0
         return q
@@ -206,6 +228,7 @@ class GpuHevcEncoder:
             raise ValueError("inputs must live on the encoder's device")
         qi, qpp = self.p.frame_qps()
         self._scenecuts = None
+        self._cutree = None
         if qps is None and self.p.crf is not None and self.p.lookahead and not self.p.intra_only:
             qps = self.crf_qps(y)
         cuts_h = self._scenecuts if self._scenecuts is not None else np.zeros((B, F), dtype=bool)
@@ -236,6 +259,13 @@ class GpuHevcEncoder:
             idr = t == 0 or self.p.intra_only or (self.p.keyint > 0 and t % self.p.keyint == 0)
             self._prep(y, u, v, t, proxy=not idr)
             self.qp.copy_(qps_d[t])  # device-to-device: no host sync inside the frame loop
+            # per-CTB QPs (AQ + cutree offsets of frame t); without them every CTB at the frame QP
+            extra, estride = 0, 0
+            if self._cutree is not None and self.p.adaptive_qp():
+                extra, estride = self._cutree.data_ptr() + t * self._cutree.shape[2] * 4, self._cutree.shape[1] * self._cutree.shape[2]
+            self.hip.hevc_aq(B, self.W, self.H, bd, p(self.src[0]), p(self.src[1]), p(self.src[2]), p(self.qp),
+                             float(self.p.aq_strength) if self.p.adaptive_qp() else 0.0, extra, estride, p(self.ctb_qp),
+                             p(self.mb_aq), s)
             cur, ref = self.rec[t % 2], self.rec[(t + 1) % 2]
             kb = t % 2
             # the copy-out of step t - 2 must have read these buffers before they are rewritten
@@ -243,7 +273,7 @@ class GpuHevcEncoder:
             self.coef, self.ctu, self.cu = self.coefs[kb], self.ctus[kb], self.cus[kb]
             intra_args = (B, self.W, self.H, p(self.src[0]), p(self.src[1]), p(self.src[2]), p(cur[0]), p(cur[1]),
                           p(cur[2]), p(self.ctu), p(self.cu), p(self.coef[0]), p(self.coef[1]), p(self.coef[2]),
-                          p(self.qp), p(self.run), p(self.cand), bd)
+                          p(self.ctb_qp), p(self.run), p(self.cand), bd)
             if idr:
                 self.run.fill_(1)
                 self.prev_mv.zero_()  # no motion predictors across a closed GOP (or from an earlier call)
@@ -254,17 +284,18 @@ class GpuHevcEncoder:
                 self.hip.hevc_proxy8(p(ref[0]), p(self.ref8), ref[0].numel(), bd - 8, s)
                 self.hip.me(B, self.wmb, self.hmb, p(self.src8), p(self.ref8), p(self.prev_mv), p(self.mv),
                             p(self.me_cost), p(self.me_pred), p(self.me_intra), p(self.qp), self.p.me_range,
-                            self.p.subpel, s, p(self.me_hp))
+                            self.p.subpel, s, p(self.me_hp), p(self.mb_aq))
                 if cuts_h[:, t].any():  # scene cut: every CU of these slots goes intra
                     self.me_cost.masked_fill_(cuts_d[t][:, None], 1 << 26)
                 self.hip.hevc_inter(B, self.W, self.H, p(self.src[0]), p(self.src[1]), p(self.src[2]), p(ref[0]),
                                     p(ref[1]), p(ref[2]), p(cur[0]), p(cur[1]), p(cur[2]), p(self.ctu), p(self.cu),
-                                    p(self.coef[0]), p(self.coef[1]), p(self.coef[2]), p(self.qp), p(self.run),
+                                    p(self.coef[0]), p(self.coef[1]), p(self.coef[2]), p(self.ctb_qp), p(self.run),
                                     p(self.cand), p(self.mv), p(self.me_cost), bd, s)
                 self.hip.hevc_intra(*intra_args, 0, 1, p(self.err), s)   # intra CUs, wavefront
                 self.prev_mv.copy_(self.mv)
+            self.hip.hevc_qp_fixup(B, self.W, self.H, p(self.ctu), p(self.cu), p(self.qp), p(self.run), int(self.p.wpp), s)
             if self.p.deblock:
-                self.hip.hevc_deblock(B, self.W, self.H, bd, p(cur[0]), p(cur[1]), p(cur[2]), p(self.cu), p(self.qp),
+                self.hip.hevc_deblock(B, self.W, self.H, bd, p(cur[0]), p(cur[1]), p(cur[2]), p(self.cu), p(self.ctu),
                                       p(self.run), s)
             if self.p.sao:
                 # SAO reads the deblocked picture and writes every sample of the output:
@@ -272,7 +303,7 @@ class GpuHevcEncoder:
                 out_pl = self.dbk
                 self.hip.hevc_sao(B, self.W, self.H, bd, p(cur[0]), p(cur[1]), p(cur[2]), p(out_pl[0]),
                                   p(out_pl[1]), p(out_pl[2]), p(self.src[0]), p(self.src[1]), p(self.src[2]),
-                                  p(self.ctu), p(self.qp), p(self.run), 1, s)
+                                  p(self.ctu), p(self.ctb_qp), p(self.run), 1, s)
                 self.dbk = cur
                 self.rec[t % 2] = cur = out_pl
             if metrics:

@@ -44,7 +44,8 @@ def _levels(rng, n: int, density: float) -> np.ndarray:
 
 
 def random_records(rng, width: int, height: int, pslice: bool, bit_depth: int = 8, density: float = 0.08,
-                   intra_in_p: float = 0.2, mv_range: int = 64, sao: bool = True):
+                   intra_in_p: float = 0.2, mv_range: int = 64, sao: bool = True, ctb_qp: tuple | None = None):
+    """``ctb_qp = (qp, spread)``: per-CTB QPs qp + U[-spread, spread] (cu_qp_delta streams)."""
     W, H = -(-width // CTB) * CTB, -(-height // CTB) * CTB
     wc, hc = W // CTB, H // CTB
     ctu = np.zeros((wc * hc, 32), np.uint8)
@@ -58,6 +59,8 @@ def random_records(rng, width: int, height: int, pslice: bool, bit_depth: int = 
         r = rng.random()
         split = 0 if r < 0.25 else (1 | (int(rng.integers(0, 16)) << 1))
         ctu[i, 0] = split
+        if ctb_qp is not None:
+            ctu[i, 1] = np.int8(np.clip(ctb_qp[0] + rng.integers(-ctb_qp[1], ctb_qp[1] + 1), 0, 51)).view(np.uint8)
         if sao:
             t = ctu[i]
             for k in range(2):
@@ -97,17 +100,42 @@ def random_records(rng, width: int, height: int, pslice: bool, bit_depth: int = 
 
 
 def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp: int = 30, bit_depth: int = 8,
-                  host_cfg: dict | None = None, **kw) -> tuple[bytes, list]:
+                  host_cfg: dict | None = None, qp_spread: int = 0, **kw) -> tuple[bytes, list]:
     """Annex-B HEVC stream (IDR + P pictures) and the records it was written from.
-    ``host_cfg`` adds writer options (e.g. ``wpp=1, threads=4``)."""
+    ``host_cfg`` adds writer options (e.g. ``wpp=1, threads=4``); ``qp_spread`` > 0 gives
+    every CTB its own QP (needs ``cu_qp_delta=1`` in ``host_cfg``)."""
     rng = np.random.default_rng(seed)
     cfg = dict(width=width, height=height, bit_depth=bit_depth, **(host_cfg or {}))
     out = [host.hevc_parameter_sets(cfg)]
     recs = []
     for t in range(frames):
-        r = random_records(rng, width, height, pslice=t > 0, bit_depth=bit_depth, **kw)
         fqp = int(np.clip(qp + rng.integers(-3, 4), 0, 51))
+        r = random_records(rng, width, height, pslice=t > 0, bit_depth=bit_depth,
+                           ctb_qp=(fqp, qp_spread) if qp_spread else None, **kw)
         nal, _ = host.hevc_write_slice(cfg, dict(idr=int(t == 0), poc=t, qp=fqp, slice_type=1 if t else 2), *r)
         out.append(nal)
         recs.append(r)
     return b"".join(out), recs
+
+
+def expected_ctb_qps(ctu: np.ndarray, cy: np.ndarray, cb: np.ndarray, cr: np.ndarray, slice_qp: int,
+                     wpp: bool) -> np.ndarray:
+    """QpY per CTB a decoder derives from cu_qp_delta records (8.6.1, one quantization
+    group per CTB): the CTB's own QP when any block of it has a coded level, else the
+    prediction (the previous CTB's QpY; the slice QP at the slice start and, with WPP,
+    at every CTB row)."""
+    H, W = cy.shape
+    wc = W // CTB
+    out = np.zeros(len(ctu), np.int32)
+    prev = slice_qp
+    for i in range(len(ctu)):
+        rx, ry = i % wc, i // wc
+        if wpp and rx == 0:
+            prev = slice_qp
+        X, Y = rx * CTB, ry * CTB
+        coded = (cy[Y:Y + CTB, X:X + CTB].any() or cb[Y // 2:Y // 2 + 16, X // 2:X // 2 + 16].any()
+                 or cr[Y // 2:Y // 2 + 16, X // 2:X // 2 + 16].any())
+        q = int(ctu[i, 1].view(np.int8)) if coded else prev
+        out[i] = q
+        prev = q
+    return out

@@ -129,3 +129,29 @@ def test_gpu_hevc_scenecut(host):
     _compare(host, res, rec)
     for r in res:
         assert r.bits[cut] > 1.3 * r.bits[cut + 1]   # the all-intra cut picture costs more than a P picture
+
+
+@pytest.mark.parametrize("wpp", [True, False])
+def test_gpu_hevc_adaptive_qp(host, wpp):
+    """Per-CTB QPs (variance AQ + cutree, cu_qp_delta): the reconstruction stays bit-exact
+    with the decoder (dequantisation and deblocking at each CU's QpY), the decoded CTB QPs
+    equal the GPU's records after the QP fix-up, and they actually vary."""
+    from govideocompressor_amd.models.h264_gpu import synth_clip
+    from govideocompressor_amd.models.hevc_gpu import GpuHevcEncoder, HevcParams
+    w, h, B, F = 160, 128, 2, 4
+    y, u, v = synth_clip(B, F, w, h, seed=5)
+    enc = GpuHevcEncoder(HevcParams(width=w, height=h, wpp=wpp), slots=B)
+    assert enc.p.host_cfg()["cu_qp_delta"] == 1
+    res = enc.encode(y, u, v, keep_recon=True)
+    rec = enc.last_recon
+    ctu_last = enc.ctu.cpu().numpy()  # records of the last picture
+    enc.close()
+    _compare(host, res, rec)
+    qps = set()
+    for b, r in enumerate(res):
+        pics = host.hevc_decode(r.bitstream)
+        q = pics[-1]["ctu"][:, 1].view(np.int8)
+        assert np.array_equal(q, ctu_last[b][:, 1].view(np.int8))
+        for p in pics:
+            qps |= set(p["ctu"][:, 1].view(np.int8).tolist())
+    assert len(qps) > 3

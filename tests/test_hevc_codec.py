@@ -10,7 +10,7 @@ the independent decoder.
 import numpy as np
 import pytest
 
-from govideocompressor_amd.utils.hevc_synth import random_records, random_stream
+from govideocompressor_amd.utils.hevc_synth import expected_ctb_qps, random_records, random_stream
 
 
 def _norm_sao(c):
@@ -116,3 +116,22 @@ def test_hevc_writer_rejects_bad_records(host):
     ctu[0, 10:14] = np.array([-1, 0, 0, 0], np.int8).view(np.uint8)   # negative edge offset in category 1
     with pytest.raises(Exception):
         host.hevc_write_slice(dict(width=64, height=64), dict(idr=1, poc=0, qp=30), ctu, cu, cy, cb, cr)
+
+
+@pytest.mark.parametrize("wpp", [0, 1])
+@pytest.mark.parametrize("bd", [8, 10])
+def test_hevc_cu_qp_delta_roundtrip(host, wpp, bd):
+    """Per-CTB QPs through cu_qp_delta: the decoder reproduces the levels and derives every
+    CTB's QpY (coded delta, or the prediction for CTBs without a coded residual)."""
+    w, h = 96, 64
+    s, recs = random_stream(host, w, h, 3, seed=7 + bd, bit_depth=bd, qp_spread=12,
+                            host_cfg=dict(cu_qp_delta=1, wpp=wpp))
+    s0, _ = random_stream(host, w, h, 3, seed=7 + bd, bit_depth=bd, host_cfg=dict(wpp=wpp))
+    pics = host.hevc_decode(s, False)
+    assert len(pics) == 3
+    for p, (ctu, cu, cy, cb, cr) in zip(pics, recs):
+        assert np.array_equal(p["coef_y"], cy) and np.array_equal(p["coef_cb"], cb) and np.array_equal(p["coef_cr"], cr)
+        want = expected_ctb_qps(ctu, cy, cb, cr, p["qp"], bool(wpp))
+        assert np.array_equal(p["ctu"][:, 1].view(np.int8).astype(np.int32), want)
+    # the same records at one QP decode to a different picture: the per-CTB QPs are used
+    assert not np.array_equal(pics[0]["y"], host.hevc_decode(s0, False)[0]["y"])
