@@ -576,29 +576,53 @@ struct HevcDecoder::Impl {
     }
     bool intra = true;
     if (slice_type != 2) intra = cd->decode(ctx[CTX_PRED_MODE]);
+    bool nxn = false;
     if (!intra || log2 == sps.log2_min_cb) {
-      if (!cd->decode(ctx[CTX_PART_MODE])) throw std::runtime_error("HEVC: only PART_2Nx2N supported");
+      // part_mode (9.3.3.7): intra at the minimum CB size: 1 = PART_2Nx2N, 0 = PART_NxN
+      if (!cd->decode(ctx[CTX_PART_MODE])) {
+        if (!intra) throw std::runtime_error("HEVC: only PART_2Nx2N inter PUs supported");
+        if (log2 <= sps.log2_min_tb) throw std::runtime_error("HEVC: PART_NxN below the minimum TB size");
+        nxn = true;
+      }
     }
     if (intra) {
-      const int prev = cd->decode(ctx[CTX_PREV_INTRA]);
-      int mpm = 0, rem = 0;
-      if (prev) {
-        mpm = cd->bypass();
-        if (mpm) mpm += cd->bypass();
-      } else {
-        rem = static_cast<int>(cd->bypass_bits(5));
+      const int npu = nxn ? 4 : 1, h = nxn ? n / 2 : n;
+      int prev[4], mpm[4] = {}, rem[4] = {}, m[4];
+      for (int k = 0; k < npu; ++k) prev[k] = cd->decode(ctx[CTX_PREV_INTRA]);
+      for (int k = 0; k < npu; ++k) {
+        if (prev[k]) {
+          mpm[k] = cd->bypass();
+          if (mpm[k]) mpm[k] += cd->bypass();
+        } else {
+          rem[k] = static_cast<int>(cd->bypass_bits(5));
+        }
       }
       // chroma mode: 4 = DM
       int cm = 4;
       if (cd->decode(ctx[CTX_CHROMA_MODE])) cm = static_cast<int>(cd->bypass_bits(2));
-      const int m = derive_luma_mode(x0, y0, prev, mpm, rem);
-      int mc = m;
+      const int cu_rect[3] = {x0, y0, n};
+      for (int k = 0; k < npu; ++k)
+        m[k] = derive_luma_mode(x0 + (k & 1) * h, y0 + (k >> 1) * h, prev[k], mpm[k], rem[k], cu_rect, m);
+      int mc = m[0];  // 8.4.3: chroma from IntraPredModeY[xCb][yCb]
       if (cm != 4) {
         const int tab[4] = {0, 26, 10, 1};
-        mc = tab[cm] == m ? 34 : tab[cm];
+        mc = tab[cm] == m[0] ? 34 : tab[cm];
       }
-      set_cu(x0, y0, n, CU_INTRA, 0, depth, m, 0, 0);
-      transform_tree(x0, y0, log2, true, m, mc);
+      set_cu(x0, y0, n, CU_INTRA, 0, depth, m[0], 0, 0);
+      if (nxn) {
+        for (int k = 1; k < 4; ++k)
+          for (int y = 0; y < h; y += 4)
+            for (int x = 0; x < h; x += 4) g_mode[g4(x0 + (k & 1) * h + x, y0 + (k >> 1) * h + y)] = static_cast<int8_t>(m[k]);
+        if (sps.log2_ctb == kCtbLog2) {
+          CuInfo& c = rec_cu[static_cast<size_t>((y0 >> kCtbLog2) * wctb + (x0 >> kCtbLog2)) * kCusPerCtb +
+                             zorder8((x0 & 31) >> 3, (y0 & 31) >> 3)];
+          c.flags |= 8;
+          for (int k = 0; k < 4; ++k) reinterpret_cast<uint8_t*>(c.mv)[k] = static_cast<uint8_t>(m[k]);
+        }
+        transform_tree_nxn(x0, y0, log2, m, mc);
+      } else {
+        transform_tree(x0, y0, log2, true, m[0], mc);
+      }
       mark_done(x0, y0, n);
       return;
     }
@@ -658,8 +682,14 @@ struct HevcDecoder::Impl {
   }
 
   // 8.4.2 luma intra mode from the MPM syntax
-  int derive_luma_mode(int x0, int y0, int prev, int mpm, int rem) {
+  // cu: (x, y, n) of the current CU and the modes of its earlier PUs (NxN: the left / above
+  // neighbour of a PU may be an earlier PU of the same CU, available in z-scan order)
+  int derive_luma_mode(int x0, int y0, int prev, int mpm, int rem, const int* cu = nullptr, const int* pu_modes = nullptr) {
     auto cand_of = [&](int x, int y, bool above) {
+      if (cu && x >= cu[0] && y >= cu[1] && x < cu[0] + cu[2] && y < cu[1] + cu[2]) {
+        const int h = cu[2] / 2;
+        return pu_modes[(x - cu[0] >= h) + 2 * (y - cu[1] >= h)];
+      }
       if (!done(x, y)) return 1;
       if (g_pred[g4(x, y)] != CU_INTRA) return 1;
       if (above && (y >> sps.log2_ctb) != (y0 >> sps.log2_ctb)) return 1;
@@ -817,6 +847,36 @@ struct HevcDecoder::Impl {
       add_residual(x0 / 2, y0 / 2, log2 - 1, 1, cbf_cb);
       add_residual(x0 / 2, y0 / 2, log2 - 1, 2, cbf_cr);
     }
+  }
+
+  // transform_tree of an intra PART_NxN CU (7.3.8.8): split_transform_flag inferred 1 at
+  // depth 0 (IntraSplitFlag), chroma cbfs at depth 0, four 4x4 luma TUs (DST, z-order, each
+  // predicted from the reconstruction of the previous ones), the 4x4 chroma blocks of the
+  // CU after the last luma TU (blkIdx 3)
+  void transform_tree_nxn(int x0, int y0, int log2, const int* m, int mode_c) {
+    if (log2 - 1 != 2 || sps.depth_intra != 0) throw std::runtime_error("HEVC: NxN transform tree unsupported");
+    const int cbf_cb = cd->decode(ctx[CTX_CBF_CHROMA + 0]);
+    const int cbf_cr = cd->decode(ctx[CTX_CBF_CHROMA + 0]);
+    const int h = 1 << (log2 - 1);
+    for (int k = 0; k < 4; ++k) {
+      const int xk = x0 + (k & 1) * h, yk = y0 + (k >> 1) * h;
+      const int cbf_y = cd->decode(ctx[CTX_CBF_LUMA + 0]);  // trafoDepth 1
+      for (int y = yk; y < yk + h; y += 4)
+        for (int x = xk; x < xk + h; x += 4) g_cbf[g4(x, y)] = static_cast<int8_t>(cbf_y);
+      if (pps.cu_qp_delta && !qp_delta_coded && (cbf_y || cbf_cb || cbf_cr)) parse_qp_delta(x0, y0);
+      if (cbf_y) residual(xk, yk, 2, 0, m[k]);
+      if (k == 3) {
+        if (cbf_cb) residual(x0 / 2, y0 / 2, 2, 1, mode_c);
+        if (cbf_cr) residual(x0 / 2, y0 / 2, 2, 2, mode_c);
+      }
+      predict_intra(xk, yk, 2, 0, m[k]);
+      add_residual(xk, yk, 2, 0, cbf_y, true);
+      mark_done(xk, yk, h);
+    }
+    predict_intra(x0 / 2, y0 / 2, 2, 1, mode_c);
+    add_residual(x0 / 2, y0 / 2, 2, 1, cbf_cb);
+    predict_intra(x0 / 2, y0 / 2, 2, 2, mode_c);
+    add_residual(x0 / 2, y0 / 2, 2, 2, cbf_cr);
   }
 
   // ------------------------------------------------------------ residual_coding (7.3.8.11)
@@ -998,7 +1058,7 @@ struct HevcDecoder::Impl {
   }
 
   // ------------------------------------------------------------ scaling + inverse transform (8.6.2 - 8.6.4)
-  void add_residual(int x0, int y0, int log2, int cidx, int cbf) {
+  void add_residual(int x0, int y0, int log2, int cidx, int cbf, bool dst = false) {
     if (!cbf) return;
     const int n = 1 << log2;
     const int stride = cidx ? W / 2 : W;
@@ -1020,6 +1080,8 @@ struct HevcDecoder::Impl {
         d[y * n + x] = clip3(-32768, 32767, static_cast<int>((v + (1LL << (bdshift - 1))) >> bdshift));
       }
     const int step = 32 >> log2;
+    // 8.6.4.2 transMatrix: DCT rows of the 32-point matrix, or DST-VII (trType 1: 4x4 intra luma)
+    auto dct_coef = [&](int k, int m) { return dst ? static_cast<int>(kDst4[k / step][m]) : hevc::dct_coef(k, m); };
     // columns (vertical), then clip to 16 bits after >> 7
     for (int x = 0; x < n; ++x)
       for (int y = 0; y < n; ++y) {

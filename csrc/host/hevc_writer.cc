@@ -185,11 +185,11 @@ namespace {
 
 // ------------------------------------------------------------------ slice writer state
 struct PicState {
-  std::vector<int8_t> depth, skip, pred, mode;
+  std::vector<int8_t> depth, skip, pred, mode4;  // mode4: luma intra mode per 4x4 block (NxN PUs)
   std::vector<int16_t> mvx, mvy;
   std::vector<uint8_t> coded;
   explicit PicState(size_t n)
-      : depth(n, 0), skip(n, 0), pred(n, 0), mode(n, 1), mvx(n, 0), mvy(n, 0), coded(n, 0) {}
+      : depth(n, 0), skip(n, 0), pred(n, 0), mode4(4 * n, 1), mvx(n, 0), mvy(n, 0), coded(n, 0) {}
 };
 
 struct Writer {
@@ -206,7 +206,7 @@ struct Writer {
   // per 8x8 granule of the picture (raster): state of already-coded CUs, shared by the
   // substream writers of one picture (WPP rows only read granules their 2-CTB lag
   // guarantees are final)
-  std::vector<int8_t>&depth, &skip, &pred, &mode;
+  std::vector<int8_t>&depth, &skip, &pred, &mode4;
   std::vector<int16_t>&mvx, &mvy;
   std::vector<uint8_t>& coded;
   // cu_qp_delta state (7.4.9.14, 8.6.1): qPY_PREV of the next quantization group (the
@@ -217,7 +217,7 @@ struct Writer {
 
   Writer(const HevcConfig& cfg, const HevcFrameParams& f, const CtuInfo* ct, const CuInfo* cu_, const int16_t* cy,
          const int16_t* cb, const int16_t* cr, CabacEncoder& enc, PicState& ps)
-      : c(cfg), fp(f), ctu(ct), cu(cu_), e(enc), depth(ps.depth), skip(ps.skip), pred(ps.pred), mode(ps.mode),
+      : c(cfg), fp(f), ctu(ct), cu(cu_), e(enc), depth(ps.depth), skip(ps.skip), pred(ps.pred), mode4(ps.mode4),
         mvx(ps.mvx), mvy(ps.mvy), coded(ps.coded) {
     coef[0] = cy;
     coef[1] = cb;
@@ -234,6 +234,7 @@ struct Writer {
   }
 
   size_t g(int x, int y) const { return static_cast<size_t>(y >> 3) * w8 + (x >> 3); }
+  size_t g4(int x, int y) const { return static_cast<size_t>(y >> 2) * (2 * w8) + (x >> 2); }
   bool inside(int x, int y) const { return x >= 0 && y >= 0 && x < W && y < H; }
   // 6.4.1 z-scan availability at 8x8 granularity (the granule is coded iff already visited)
   bool avail(int x, int y) const { return inside(x, y) && coded[g(x, y)]; }
@@ -600,7 +601,7 @@ struct Writer {
         depth[k] = static_cast<int8_t>(d);
         skip[k] = static_cast<int8_t>(sk);
         pred[k] = static_cast<int8_t>(pm);
-        mode[k] = static_cast<int8_t>(md);
+        for (int q = 0; q < 4; ++q) mode4[g4(xx + (q & 1) * 4, yy + (q >> 1) * 4)] = static_cast<int8_t>(md);
         mvx[k] = static_cast<int16_t>(mv.x);
         mvy[k] = static_cast<int16_t>(mv.y);
         coded[k] = 1;
@@ -658,48 +659,83 @@ struct Writer {
         return;
       }
     }
-    // intra CU
-    if (log2 == kMinCbLog2) e.encode(1, ctx[CTX_PART_MODE]);  // PART_2Nx2N
-    const int m = ci.mode;
-    if (m > 34) throw std::runtime_error("intra mode out of range");
-    // 8.4.2 most probable modes
-    int ca = 1, cb = 1;
-    if (avail(x - 1, y) && pred[g(x - 1, y)] == CU_INTRA) ca = mode[g(x - 1, y)];
-    if (avail(x, y - 1) && pred[g(x, y - 1)] == CU_INTRA && ((y - 1) >> kCtbLog2) == (y >> kCtbLog2)) cb = mode[g(x, y - 1)];
-    int cand[3];
-    if (ca == cb) {
-      if (ca < 2) {
-        cand[0] = 0;
-        cand[1] = 1;
-        cand[2] = 26;
+    // intra CU: PART_2Nx2N, or PART_NxN at the minimum CB size (four 4x4 PUs, CuInfo flags
+    // bit 3, PU modes in the bytes of the unused motion vector)
+    const bool nxn = log2 == kMinCbLog2 && (ci.flags & 8);
+    if (log2 == kMinCbLog2) e.encode(nxn ? 0 : 1, ctx[CTX_PART_MODE]);
+    const int npu = nxn ? 4 : 1, h = nxn ? n / 2 : n;
+    int m[4], mpm[4], rem[4];
+    for (int k = 0; k < npu; ++k) {
+      m[k] = nxn ? reinterpret_cast<const uint8_t*>(ci.mv)[k] : ci.mode;
+      if (m[k] > 34) throw std::runtime_error("intra mode out of range");
+      const int xk = x + (k & 1) * h, yk = y + (k >> 1) * h;
+      // 8.4.2 most probable modes; an NxN PU's left / above neighbour may be an earlier PU
+      auto cand_of = [&](int xn, int yn, bool above) {
+        if (xn >= x && yn >= y) return m[(xn - x >= h) + 2 * (yn - y >= h)];
+        if (!avail(xn, yn) || pred[g(xn, yn)] != CU_INTRA) return 1;
+        if (above && (yn >> kCtbLog2) != (yk >> kCtbLog2)) return 1;
+        return static_cast<int>(mode4[g4(xn, yn)]);
+      };
+      const int ca = cand_of(xk - 1, yk, false), cb = cand_of(xk, yk - 1, true);
+      int cand[3];
+      if (ca == cb) {
+        if (ca < 2) {
+          cand[0] = 0;
+          cand[1] = 1;
+          cand[2] = 26;
+        } else {
+          cand[0] = ca;
+          cand[1] = 2 + ((ca + 29) % 32);
+          cand[2] = 2 + ((ca - 2 + 1) % 32);
+        }
       } else {
         cand[0] = ca;
-        cand[1] = 2 + ((ca + 29) % 32);
-        cand[2] = 2 + ((ca - 2 + 1) % 32);
+        cand[1] = cb;
+        cand[2] = (ca != 0 && cb != 0) ? 0 : ((ca != 1 && cb != 1) ? 1 : 26);
       }
-    } else {
-      cand[0] = ca;
-      cand[1] = cb;
-      cand[2] = (ca != 0 && cb != 0) ? 0 : ((ca != 1 && cb != 1) ? 1 : 26);
-    }
-    int mpm = -1;
-    for (int k = 0; k < 3; ++k)
-      if (cand[k] == m) mpm = k;
-    e.encode(mpm >= 0, ctx[CTX_PREV_INTRA]);
-    if (mpm >= 0) {
-      e.bypass(mpm > 0);
-      if (mpm > 0) e.bypass(mpm > 1);
-    } else {
+      mpm[k] = -1;
+      for (int j = 0; j < 3; ++j)
+        if (cand[j] == m[k]) mpm[k] = j;
       std::sort(cand, cand + 3);
-      int rem = m;
-      for (int k = 2; k >= 0; --k)
-        if (rem > cand[k]) --rem;
-      e.bypass_bits(rem, 5);
+      rem[k] = m[k];
+      for (int j = 2; j >= 0; --j)
+        if (rem[k] > cand[j]) --rem[k];
     }
-    e.encode(0, ctx[CTX_CHROMA_MODE]);  // intra_chroma_pred_mode = 4 (DM)
-    mark(x, y, n, d, 0, CU_INTRA, m, Mv{0, 0});
+    for (int k = 0; k < npu; ++k) e.encode(mpm[k] >= 0, ctx[CTX_PREV_INTRA]);
+    for (int k = 0; k < npu; ++k) {
+      if (mpm[k] >= 0) {
+        e.bypass(mpm[k] > 0);
+        if (mpm[k] > 0) e.bypass(mpm[k] > 1);
+      } else {
+        e.bypass_bits(rem[k], 5);
+      }
+    }
+    e.encode(0, ctx[CTX_CHROMA_MODE]);  // intra_chroma_pred_mode = 4 (DM: the mode of PU 0)
+    mark(x, y, n, d, 0, CU_INTRA, m[0], Mv{0, 0});
+    if (nxn)
+      for (int k = 1; k < 4; ++k) mode4[g4(x + (k & 1) * h, y + (k >> 1) * h)] = static_cast<int8_t>(m[k]);
     ++st.intra_cus;
-    write_tu(x, y, log2, true, m, cb_y, cb_cb, cb_cr);
+    if (nxn) write_tu_nxn(x, y, m, cb_cb, cb_cr);
+    else write_tu(x, y, log2, true, m[0], cb_y, cb_cb, cb_cr);
+  }
+
+  // transform_tree of an intra PART_NxN CU (7.3.8.8 / 7.3.8.10): chroma cbfs at depth 0,
+  // split_transform_flag inferred (IntraSplitFlag), four 4x4 luma TUs with cbf_luma at
+  // depth 1; cbfChroma of every 4x4 TU is the parent's, and the 4x4 chroma blocks follow
+  // the last luma TU (blkIdx 3)
+  void write_tu_nxn(int x, int y, const int* m, bool cb_cb, bool cb_cr) {
+    e.encode(cb_cb, ctx[CTX_CBF_CHROMA + 0]);
+    e.encode(cb_cr, ctx[CTX_CBF_CHROMA + 0]);
+    for (int k = 0; k < 4; ++k) {
+      const int xk = x + (k & 1) * 4, yk = y + (k >> 1) * 4;
+      const bool cy = any_nonzero(0, xk, yk, 4);
+      e.encode(cy, ctx[CTX_CBF_LUMA + 0]);
+      if (c.cu_qp_delta && !qp_coded && (cy || cb_cb || cb_cr)) write_qp_delta();
+      if (cy) write_residual(coef[0] + static_cast<size_t>(yk) * W + xk, W, 2, 0, mdcs(m[k]));
+    }
+    const int cstride = W / 2;
+    if (cb_cb) write_residual(coef[1] + static_cast<size_t>(y / 2) * cstride + x / 2, cstride, 2, 1, mdcs(m[0]));
+    if (cb_cr) write_residual(coef[2] + static_cast<size_t>(y / 2) * cstride + x / 2, cstride, 2, 2, mdcs(m[0]));
   }
 
   void write_merge_idx(int idx) {

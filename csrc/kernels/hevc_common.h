@@ -13,6 +13,25 @@
 namespace mivc {
 namespace gpu {
 
+// intra analysis candidates per CTB (int32): [0, 21) best cost per CU (32, 4 x 16, 16 x 8 in
+// z-order), [21, 42) its mode, [42, 58) per 8x8 CU the chosen PART_NxN PU modes (bit 24 set,
+// four 6-bit modes) or 0 (PART_2Nx2N)
+constexpr int kCandStride = 58;
+
+// z-order index of 4x4 block (gx, gy) inside a 32x32 CTB (0..63)
+__device__ __forceinline__ int zorder4(int gx, int gy) {
+  return (gx & 1) | ((gy & 1) << 1) | ((gx & 2) << 1) | ((gy & 2) << 2) | ((gx & 4) << 2) | ((gy & 4) << 3);
+}
+
+// CuInfo of an intra PART_NxN 8x8 CU from a packed candidate (bit 24 | four 6-bit modes):
+// flags bit 3, PU 0's mode in `mode`, the four PU modes in the bytes of the unused vector
+__device__ __forceinline__ void set_nxn(hevc::CuInfo& c, int packed) {
+  c.flags |= 8;
+  c.mode = static_cast<uint8_t>(packed & 63);
+  uint8_t* b = reinterpret_cast<uint8_t*>(c.mv);
+  for (int j = 0; j < 4; ++j) b[j] = static_cast<uint8_t>((packed >> (6 * j)) & 63);
+}
+
 // batched HEVC picture geometry (coded size, multiple of the 32x32 CTB)
 struct HevcGeom {
   int B, W, H, wctb, hctb;
@@ -28,9 +47,14 @@ using hevc::dct_coef;
 // ---------------------------------------------------------------- DCT matrix in LDS
 struct DctLds {
   int16_t m[32][32];
+  int16_t dst[4][4];  // DST-VII (8.6.4.2, trType 1: 4x4 intra luma)
 };
 __device__ __forceinline__ void dct_lds_init(DctLds& D) {
   for (int i = threadIdx.x; i < 1024; i += blockDim.x) D.m[i >> 5][i & 31] = static_cast<int16_t>(dct_coef(i >> 5, i & 31));
+  if (threadIdx.x < 16) {
+    const int16_t t[16] = {29, 55, 74, 84, 74, 74, 0, -74, 84, -29, -74, 55, 55, -84, 74, -29};
+    D.dst[threadIdx.x >> 2][threadIdx.x & 3] = t[threadIdx.x];
+  }
 }
 // entry (k, m) of the n-point matrix
 __device__ __forceinline__ int cn(const DctLds& D, int log2n, int k, int m) { return D.m[k << (5 - log2n)][m]; }
@@ -80,11 +104,14 @@ __device__ __forceinline__ void wave_matmul(int n, FA A, FB B, FO out) {
 struct TqParams {
   int log2n, bd, qp;  // qp: Qp' (QpY + QpBdOffset, or the chroma equivalent)
   bool intra;
+  bool dst = false;   // 4x4 intra luma: DST-VII instead of the DCT
 };
 
 __device__ __forceinline__ bool transform_quant_block(const DctLds& D, int* R, int* S, int16_t* lev, int lstride,
                                                       const TqParams& p) {
   const int n = 1 << p.log2n, lg = p.log2n;
+  const bool dst = p.dst;
+  auto cn = [&](const DctLds& M, int l2, int k, int m) { return dst ? static_cast<int>(M.dst[k][m]) : hv::cn(M, l2, k, m); };
   // forward, stage 1 (rows): S[y][k] = (sum_x R[y][x] * C[k][x] + rnd) >> sh1
   const int sh1 = lg + p.bd - 9, r1 = 1 << (sh1 - 1);
   wave_matmul(n, [&](int y, int x) { return R[y * 32 + x]; }, [&](int x, int k) { return cn(D, lg, k, x); },

@@ -32,7 +32,7 @@ struct HevcInterArgs {
   int16_t *coef_y, *coef_u, *coef_v;
   const int* qp;          // [B, nctb] QpY per CTB
   const int8_t* run;
-  const int* cand;       // [B, nctb, 2, 21] intra analysis: best cost / mode per CU
+  const int* cand;       // [B, nctb, kCandStride] intra analysis: best cost / mode per CU, NxN PUs
   const int16_t* mv;     // [B, nmb16, 2] quarter-sample vectors per 16x16 block
   const int* me_cost;    // [B, nmb16] (8-bit proxy units)
   int bd;
@@ -50,7 +50,7 @@ __global__ __launch_bounds__(64) void hevc_p_decide(HevcInterArgs a) {
   const int lane = threadIdx.x;
   const int rx = ci % g.wctb, ry = ci / g.wctb;
   const size_t cb = static_cast<size_t>(slot) * g.nctb() + ci;
-  const int* cd = a.cand + cb * 42;
+  const int* cd = a.cand + cb * kCandStride;
   const int wmb = g.W / 16, nmb = wmb * (g.H / 16);
   const int qp = a.qp[cb];
   const int lam = lambda_satd_i(qp, a.bd);
@@ -119,6 +119,7 @@ __global__ __launch_bounds__(64) void hevc_p_decide(HevcInterArgs a) {
       c.pred = hevc::CU_INTRA;
       const int idx = lg == 5 ? 0 : (lg == 4 ? 1 + q : 5 + k);
       c.mode = static_cast<uint8_t>(cd[21 + idx]);
+      if (lg == 3 && cd[42 + k]) set_nxn(c, cd[42 + k]);
     }
     a.cu[cb * 16 + k] = c;
   }

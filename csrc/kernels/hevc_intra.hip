@@ -35,8 +35,9 @@ struct HevcIntraArgs {
   int* err;
 };
 
-// luma neighbour (xr, yr) of a CTB-relative CU position: z-scan availability (6.4.1)
-// at 8x8 granularity; zcur = z-order index of the current CU's first granule
+// luma neighbour (xr, yr) of a CTB-relative block position: z-scan availability (6.4.1)
+// at the 4x4 minimum-TB granularity; zcur = z-order index (zorder4) of the current
+// block's first 4x4 block
 __device__ __forceinline__ bool nb_avail(int xr, int yr, int zcur, int rx, int ry, int wctb) {
   if (yr < 0) {
     if (ry == 0) return false;
@@ -47,7 +48,7 @@ __device__ __forceinline__ bool nb_avail(int xr, int yr, int zcur, int rx, int r
   if (yr >= 32) return false;
   if (xr < 0) return rx > 0;
   if (xr >= 32) return false;
-  return zorder8(xr >> 3, yr >> 3) < zcur;
+  return zorder4(xr >> 2, yr >> 2) < zcur;
 }
 
 __device__ __forceinline__ void ref_pos(int i, int n, int cx, int cy, int* x, int* y) {
@@ -65,6 +66,26 @@ __device__ __forceinline__ void ref_pos(int i, int n, int cx, int cy, int* x, in
 
 __device__ __forceinline__ int lambda_satd(int qp, int bd) {
   return static_cast<int>(0.755f * exp2f((qp - 12) / 6.0f) * static_cast<float>(1 << (bd - 8)) + 0.5f);
+}
+
+// 4x4 Hadamard SATD (HM normalisation: (sum |H| + 1) >> 1)
+__device__ __forceinline__ int satd4x4(int (&d)[16]) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    int* v = d + r * 4;
+    const int a0 = v[0] + v[1], a1 = v[0] - v[1], a2 = v[2] + v[3], a3 = v[2] - v[3];
+    v[0] = a0 + a2;
+    v[1] = a1 + a3;
+    v[2] = a0 - a2;
+    v[3] = a1 - a3;
+  }
+  int sum = 0;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int a0 = d[c] + d[4 + c], a1 = d[c] - d[4 + c], a2 = d[8 + c] + d[12 + c], a3 = d[8 + c] - d[12 + c];
+    sum += abs(a0 + a2) + abs(a1 + a3) + abs(a0 - a2) + abs(a1 - a3);
+  }
+  return (sum + 1) >> 1;
 }
 
 // 8x8 Hadamard SATD (x265 / HM normalisation: (sum |H| + 2) >> 2)
@@ -102,6 +123,7 @@ __device__ __forceinline__ int satd8x8(int (&d)[64]) {
 
 // ============================================================== analysis
 constexpr int kCuCount = 21;  // 1 x 32, 4 x 16, 16 x 8
+constexpr int kPuCount = 64;  // PART_NxN: four 4x4 PUs of each 8x8 CU (z-order)
 struct AnalyzeShared {
   int16_t ext[65 * 65];        // source samples, x, y in [-1, 63] relative to the CTB
   int refs[2][917];            // per CU: unfiltered / filtered reference arrays
@@ -109,7 +131,20 @@ struct AnalyzeShared {
   uint8_t done[kCuCount][36];  // (CU, mode) evaluated
   int dc[kCuCount];
   int best_mode[kCuCount], best_cost[kCuCount];
+  int refs4[kPuCount][17];     // 4x4 PUs: reference arrays (no filtering at 4x4)
+  int cost4[kPuCount][36];
+  uint8_t done4[kPuCount][36];
+  int dc4[kPuCount];
+  int best4_mode[kPuCount], best4_cost[kPuCount];
+  int nxn[16];                 // per 8x8 CU: packed PU modes (bit 24) or 0
 };
+
+// CTB-relative position of 4x4 PU `pu` (8x8 CU pu >> 2 in z-order, PU pu & 3 in raster)
+__device__ __forceinline__ void pu_of(int pu, int* px, int* py) {
+  const int k8 = pu >> 2, k = pu & 3;
+  *px = ((k8 & 1) | ((k8 >> 1) & 2)) * 8 + (k & 1) * 4;
+  *py = (((k8 >> 1) & 1) | ((k8 >> 2) & 2)) * 8 + (k >> 1) * 4;
+}
 
 __device__ __forceinline__ void cu_of(int c, int* cx, int* cy, int* n, int* off) {
   if (c == 0) {
@@ -156,7 +191,7 @@ __global__ __launch_bounds__(256) void hevc_intra_analyze(HevcIntraArgs a) {
   if (tid < kCuCount) {
     int cx, cy, n, off;
     cu_of(tid, &cx, &cy, &n, &off);
-    const int zc = zorder8(cx >> 3, cy >> 3);
+    const int zc = 4 * zorder8(cx >> 3, cy >> 3);
     const int E = 4 * n + 1;
     int* p = S.refs[0] + off;
     int first = -1;
@@ -191,6 +226,36 @@ __global__ __launch_bounds__(256) void hevc_intra_analyze(HevcIntraArgs a) {
     for (int k = 0; k < n; ++k) s += p[c + 1 + k] + p[c - 1 - k];
     const int lg = n == 32 ? 5 : (n == 16 ? 4 : 3);
     S.dc[tid] = s >> (lg + 1);
+  } else if (tid >= 64 && tid < 64 + kPuCount) {  // 4x4 PU reference arrays (z4 = PU index)
+    const int pu = tid - 64;
+    int px, py;
+    pu_of(pu, &px, &py);
+    int* p = S.refs4[pu];
+    int first = -1;
+    for (int i = 0; i < 17; ++i) {
+      int x, y;
+      ref_pos(i, 4, px, py, &x, &y);
+      if (nb_avail(x, y, pu, rx, ry, g.wctb)) {
+        p[i] = S.ext[(y + 1) * 65 + x + 1];
+        if (first < 0) first = i;
+      } else {
+        p[i] = -1;
+      }
+    }
+    if (first < 0) {
+      for (int i = 0; i < 17; ++i) p[i] = 1 << (bd - 1);
+    } else {
+      if (p[0] < 0) p[0] = p[first];
+      for (int i = 1; i < 17; ++i)
+        if (p[i] < 0) p[i] = p[i - 1];
+    }
+    int s = 4;
+    for (int k = 0; k < 4; ++k) s += p[9 + k] + p[7 - k];
+    S.dc4[pu] = s >> 3;
+  }
+  for (int i = tid; i < kPuCount * 36; i += 256) {
+    (&S.cost4[0][0])[i] = 0;
+    (&S.done4[0][0])[i] = 0;
   }
   __syncthreads();
   // SATD of (CU, mode, 8x8 block) items, coarse to fine: 11 seed modes (planar, DC and
@@ -226,10 +291,28 @@ __global__ __launch_bounds__(256) void hevc_intra_analyze(HevcIntraArgs a) {
     atomicAdd(&S.cost[c][mode], satd8x8(d));
     S.done[c][mode] = 1;
   };
+  // one 4x4 PU and mode: prediction from the source references, 4x4 Hadamard SATD
+  auto eval4 = [&](int pu, int mode) {
+    int px, py;
+    pu_of(pu, &px, &py);
+    const int* p = S.refs4[pu];
+    int d[16];
+#pragma unroll
+    for (int y = 0; y < 4; ++y)
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+        d[y * 4 + x] = S.ext[(py + y + 1) * 65 + px + x + 1] - hv::intra_pred_sample(p, 4, 2, mode, x, y, S.dc4[pu], true, maxv);
+    S.cost4[pu][mode] = satd4x4(d);
+    S.done4[pu][mode] = 1;
+  };
   {
     for (int it = tid; it < 11 * 48; it += 256) {
       const int si = it / 48;
       eval(it % 48, si < 2 ? si : 2 + 4 * (si - 2));  // seeds 0, 1, 2, 6, ..., 34
+    }
+    for (int it = tid; it < 11 * kPuCount; it += 256) {
+      const int si = it / kPuCount;
+      eval4(it % kPuCount, si < 2 ? si : 2 + 4 * (si - 2));
     }
   }
   __syncthreads();
@@ -244,6 +327,17 @@ __global__ __launch_bounds__(256) void hevc_intra_analyze(HevcIntraArgs a) {
         }
       }
       S.best_mode[tid] = bm;
+    } else if (tid >= 64 && tid < 64 + kPuCount) {
+      const int pu = tid - 64;
+      int bm = 2, bc = 0x7FFFFFFF;
+      for (int m = 2; m < 35; ++m) {
+        const int cst = S.cost4[pu][m];
+        if (S.done4[pu][m] && cst < bc) {
+          bc = cst;
+          bm = m;
+        }
+      }
+      S.best4_mode[pu] = bm;
     }
     __syncthreads();
     if (tid < 96) {
@@ -252,6 +346,10 @@ __global__ __launch_bounds__(256) void hevc_intra_analyze(HevcIntraArgs a) {
       const int c = level == 0 ? 0 : (level == 1 ? 1 + (k >> 2) : 5 + k);
       const int m = S.best_mode[c] + (tid < 48 ? -step : step);
       if (m >= 2 && m <= 34 && !S.done[c][m]) eval(slot48, m);
+    } else if (tid >= 128) {
+      const int pu = (tid - 128) & 63;
+      const int m = S.best4_mode[pu] + (tid < 192 ? -step : step);
+      if (m >= 2 && m <= 34 && !S.done4[pu][m]) eval4(pu, m);
     }
     __syncthreads();
   }
@@ -270,13 +368,43 @@ __global__ __launch_bounds__(256) void hevc_intra_analyze(HevcIntraArgs a) {
     }
     S.best_mode[tid] = bm;
     S.best_cost[tid] = bc + lam * 4;  // CU overhead: split flag, chroma mode, cbfs
-    if (a.cand) {
-      int* cd = a.cand + (static_cast<size_t>(slot) * g.nctb() + ci) * 42;
-      cd[tid] = bc + lam * 4;
-      cd[21 + tid] = bm;
+  } else if (tid >= 64 && tid < 64 + kPuCount) {
+    const int pu = tid - 64;
+    int bm = 0, bc = 0x7FFFFFFF;
+    for (int m = 0; m < 35; ++m) {
+      if (!S.done4[pu][m]) continue;
+      const int cst = S.cost4[pu][m] + lam * (m < 2 ? 3 : 5);
+      if (cst < bc) {
+        bc = cst;
+        bm = m;
+      }
+    }
+    S.best4_mode[pu] = bm;
+    S.best4_cost[pu] = bc;
+  }
+  __syncthreads();
+  if (tid < 16) {  // PART_NxN vs PART_2Nx2N per 8x8 CU (NxN: three more PU mode codes, four luma cbfs)
+    const int c8 = tid;
+    const int cn = S.best4_cost[4 * c8] + S.best4_cost[4 * c8 + 1] + S.best4_cost[4 * c8 + 2] + S.best4_cost[4 * c8 + 3] +
+                   lam * 6;
+    if (cn < S.best_cost[5 + c8]) {
+      S.best_cost[5 + c8] = cn;
+      S.nxn[c8] = (1 << 24) | S.best4_mode[4 * c8] | (S.best4_mode[4 * c8 + 1] << 6) | (S.best4_mode[4 * c8 + 2] << 12) |
+                  (S.best4_mode[4 * c8 + 3] << 18);
+    } else {
+      S.nxn[c8] = 0;
     }
   }
   __syncthreads();
+  if (a.cand && tid < kCuCount + 16) {
+    int* cd = a.cand + (static_cast<size_t>(slot) * g.nctb() + ci) * kCandStride;
+    if (tid < kCuCount) {
+      cd[tid] = S.best_cost[tid];
+      cd[21 + tid] = S.best_mode[tid];
+    } else {
+      cd[42 + tid - kCuCount] = S.nxn[tid - kCuCount];
+    }
+  }
   if (tid == 0) {
     int split = 0, c16sum = 0;
     for (int q = 0; q < 4; ++q) {
@@ -318,6 +446,7 @@ __global__ __launch_bounds__(256) void hevc_intra_analyze(HevcIntraArgs a) {
     c.pred = hevc::CU_INTRA;
     c.mode = static_cast<uint8_t>(m);
     c.flags = static_cast<uint8_t>((lg - 3) << 1);
+    if (lg == 3 && S.nxn[tid]) set_nxn(c, S.nxn[tid]);
     a.cu[(static_cast<size_t>(slot) * g.nctb() + ci) * 16 + tid] = c;
   }
 }
@@ -341,7 +470,8 @@ struct ReconShared {
 // reconstruct one CU component: refs from the LDS tile, predict, transform/quantise, store
 template <bool LUMA>
 __device__ __forceinline__ bool recon_block(const HevcIntraArgs& a, ReconShared& S, const hv::DctLds& D, int slot,
-                                            int comp, int rx, int ry, int cx, int cy, int log2n, int mode, int zc, int qpp) {
+                                            int comp, int rx, int ry, int cx, int cy, int log2n, int mode, int zc, int qpp,
+                                            bool dst = false) {
   const HevcGeom& g = a.g;
   const int lane = lane_id();
   const int n = 1 << log2n;
@@ -381,7 +511,7 @@ __device__ __forceinline__ bool recon_block(const HevcIntraArgs& a, ReconShared&
   // 3. transform / quantisation / reconstruction
   int16_t* lev = (LUMA ? a.coef_y : (comp == 1 ? a.coef_u : a.coef_v)) + slot * (LUMA ? g.ysize() : g.csize()) +
                  static_cast<size_t>(Y0) * pw + X0;
-  hv::TqParams tp{log2n, bd, qpp, true};
+  hv::TqParams tp{log2n, bd, qpp, true, dst};
   const bool nz = hv::transform_quant_block(D, S.R, S.S, lev, pw, tp);
   uint16_t* rec = (LUMA ? a.rec_y : (comp == 1 ? a.rec_u : a.rec_v)) + slot * (LUMA ? g.ysize() : g.csize());
   for (int i = lane; i < n * n; i += 64) {
@@ -457,9 +587,18 @@ __device__ void hevc_recon_ctb(const HevcIntraArgs& a, ReconShared& S, const hv:
       const int mode = __builtin_amdgcn_readfirstlane(cu->mode);
       const int gx = (k & 1) | ((k >> 1) & 2), gy = ((k >> 1) & 1) | ((k >> 2) & 2);
       const int cx = gx * 8, cy = gy * 8;
-      const bool ny = recon_block<true>(a, S, D, slot, 0, rx, ry, cx, cy, log2n, mode, k, qpl);
-      const bool nu = recon_block<false>(a, S, D, slot, 1, rx, ry, cx / 2, cy / 2, log2n - 1, mode, k, qpc);
-      const bool nv = recon_block<false>(a, S, D, slot, 2, rx, ry, cx / 2, cy / 2, log2n - 1, mode, k, qpc);
+      bool ny = false;
+      if (log2n == 3 && (__builtin_amdgcn_readfirstlane(cu->flags) & 8)) {
+        // PART_NxN: four 4x4 luma PUs in z-order, DST, each predicted from the previous ones
+        const uint32_t pm = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t*>(cu->mv));
+        for (int j = 0; j < 4; ++j)
+          ny |= recon_block<true>(a, S, D, slot, 0, rx, ry, cx + (j & 1) * 4, cy + (j >> 1) * 4, 2,
+                                  static_cast<int>((pm >> (8 * j)) & 255u), 4 * k + j, qpl, true);
+      } else {
+        ny = recon_block<true>(a, S, D, slot, 0, rx, ry, cx, cy, log2n, mode, 4 * k, qpl);
+      }
+      const bool nu = recon_block<false>(a, S, D, slot, 1, rx, ry, cx / 2, cy / 2, log2n - 1, mode, 4 * k, qpc);
+      const bool nv = recon_block<false>(a, S, D, slot, 2, rx, ry, cx / 2, cy / 2, log2n - 1, mode, 4 * k, qpc);
       if (lane < step) {
         CuInfo* c = a.cu + cb * 16 + k + lane;
         c->cbf = static_cast<uint8_t>(ny | (nu << 1) | (nv << 2));

@@ -133,7 +133,7 @@ class GpuHevcEncoder:
         self.me_intra = torch.zeros((B, nmb), dtype=torch.int32, device=dev)
         self.me_pred = torch.zeros((B, nmb, 256), dtype=torch.uint8, device=dev)
         self.me_hp = torch.empty(B * 3 * (H + 8) * (W + 8) + 64, dtype=torch.uint8, device=dev)
-        self.cand = torch.zeros((B, self.nctb, 42), dtype=torch.int32, device=dev)
+        self.cand = torch.zeros((B, self.nctb, 58), dtype=torch.int32, device=dev)  # kCandStride
         self.ctus = [torch.zeros((B, self.nctb, 32), dtype=torch.uint8, device=dev) for _ in range(2)]
         self.cus = [torch.zeros((B, self.nctb * 16, 8), dtype=torch.uint8, device=dev) for _ in range(2)]
         self.ctu, self.cu = self.ctus[0], self.cus[0]

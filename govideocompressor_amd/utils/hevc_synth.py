@@ -44,8 +44,10 @@ def _levels(rng, n: int, density: float) -> np.ndarray:
 
 
 def random_records(rng, width: int, height: int, pslice: bool, bit_depth: int = 8, density: float = 0.08,
-                   intra_in_p: float = 0.2, mv_range: int = 64, sao: bool = True, ctb_qp: tuple | None = None):
-    """``ctb_qp = (qp, spread)``: per-CTB QPs qp + U[-spread, spread] (cu_qp_delta streams)."""
+                   intra_in_p: float = 0.2, mv_range: int = 64, sao: bool = True, ctb_qp: tuple | None = None,
+                   nxn: float = 0.0):
+    """``ctb_qp = (qp, spread)``: per-CTB QPs qp + U[-spread, spread] (cu_qp_delta streams);
+    ``nxn``: probability of an 8x8 intra CU being split into four 4x4 PUs."""
     W, H = -(-width // CTB) * CTB, -(-height // CTB) * CTB
     wc, hc = W // CTB, H // CTB
     ctu = np.zeros((wc * hc, 32), np.uint8)
@@ -84,6 +86,10 @@ def random_records(rng, width: int, height: int, pslice: bool, bit_depth: int = 
             rec[0] = 0 if intra else 1
             if intra:
                 rec[1] = int(rng.integers(0, 35))
+                if n == 8 and rng.random() < nxn:   # PART_NxN: four 4x4 PUs (flags bit 3)
+                    rec[3] |= 8
+                    rec[4:8] = rng.integers(0, 35, 4)
+                    rec[4] = rec[1]
             else:
                 mv = rng.integers(-mv_range, mv_range + 1, 2).astype(np.int16)
                 if rng.random() < 0.3:

@@ -155,3 +155,16 @@ def test_gpu_hevc_adaptive_qp(host, wpp):
         for p in pics:
             qps |= set(p["ctu"][:, 1].view(np.int8).tolist())
     assert len(qps) > 3
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+def test_gpu_hevc_intra_nxn(host, bd):
+    """Intra PART_NxN (four 4x4 PUs, DST luma TUs) is chosen on detailed content at a low QP,
+    in I and P pictures, and the reconstruction stays bit-exact with the decoder."""
+    res, rec = _encode(128, 96, 3, 2, bd=bd, crf=None, qp=22)
+    _compare(host, res, rec)
+    n = 0
+    for r in res:
+        for p in host.hevc_decode(r.bitstream):
+            n += int(((p["cu"][:, 3] & 8) != 0).sum())
+    assert n > 0

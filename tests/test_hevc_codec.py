@@ -135,3 +135,23 @@ def test_hevc_cu_qp_delta_roundtrip(host, wpp, bd):
         assert np.array_equal(p["ctu"][:, 1].view(np.int8).astype(np.int32), want)
     # the same records at one QP decode to a different picture: the per-CTB QPs are used
     assert not np.array_equal(pics[0]["y"], host.hevc_decode(s0, False)[0]["y"])
+
+
+@pytest.mark.parametrize("pslice", [False, True])
+def test_hevc_intra_nxn_roundtrip(host, pslice):
+    """Intra PART_NxN CUs (four 4x4 PUs with their own modes, 4x4 DST luma TUs, chroma after
+    the last luma TU) with per-CTB QPs: levels, modes and flags decode back."""
+    w, h = 64, 64
+    s, recs = random_stream(host, w, h, 3, seed=21 + pslice, qp_spread=6, nxn=0.6, intra_in_p=0.7,
+                            host_cfg=dict(cu_qp_delta=1, wpp=1))
+    pics = host.hevc_decode(s, False)
+    n_nxn = 0
+    for p, (ctu, cu, cy, cb, cr) in zip(pics, recs):
+        assert np.array_equal(p["coef_y"], cy) and np.array_equal(p["coef_cb"], cb) and np.array_equal(p["coef_cr"], cr)
+        intra = cu[:, 0] == 0
+        nx = intra & ((cu[:, 3] & 8) != 0)
+        n_nxn += int(nx.sum())
+        assert np.array_equal(p["cu"][:, 3] & 8, np.where(nx, 8, 0))
+        assert np.array_equal(p["cu"][nx, 4:8], cu[nx, 4:8])
+        assert np.array_equal(p["cu"][intra, 1], cu[intra, 1])
+    assert n_nxn > 10
