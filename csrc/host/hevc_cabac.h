@@ -37,6 +37,19 @@ inline void init_contexts(CtxState* ctx, int init_type, int slice_qp) {
   }
 }
 
+// next state after an MPS ([0]) or LPS ([1]) bin (9.3.4.3.2.2)
+struct NextStateTable {
+  uint8_t t[2][64];
+  constexpr NextStateTable() : t() {
+    for (int i = 0; i < 64; ++i) {
+      t[0][i] = static_cast<uint8_t>(i < 62 ? i + 1 : i);
+      t[1][i] = kTransIdxLps[i];
+    }
+  }
+};
+static constexpr NextStateTable kNextStateT{};
+static constexpr const uint8_t (&kNextState)[2][64] = kNextStateT.t;
+
 class CabacEncoder {
  public:
   explicit CabacEncoder(BitWriter& bw) : bw_(bw) {}
@@ -50,25 +63,28 @@ class CabacEncoder {
     bins_ = 0;
   }
 
+  // branch-free regular bin (9.3.4.3.2): the LPS / MPS choice selects range and low with
+  // conditional moves, the renormalisation shift is a count of leading zeros, and the
+  // state transition is one table entry (an unpredictable bin costs no mispredict)
   void encode(int bin, CtxState& c) {
+    // members are read into locals before the context (uint8_t, may alias anything) is
+    // written, so they stay in registers
+    const uint32_t s = c.state, mps = c.mps;
+    uint32_t range = range_, low = low_;
+    const uint32_t lps = kRangeLps[s][(range >> 6) & 3];
+    const uint32_t rmps = range - lps;
+    const bool is_lps = static_cast<uint32_t>(bin) != mps;
+    const uint32_t r = is_lps ? lps : rmps;
+    low += is_lps ? rmps : 0u;
+    const int nb = __builtin_clz(r) - 23;  // r in [2, 510]: shifts until r >= 256
+    const int left = bits_left_ - nb;
+    range_ = r << nb;
+    low_ = low << nb;
+    bits_left_ = left;
     ++bins_;
-    const uint32_t lps = kRangeLps[c.state][(range_ >> 6) & 3];
-    range_ -= lps;
-    if (bin != c.mps) {
-      const int nb = renorm_bits(lps);
-      low_ = (low_ + range_) << nb;
-      range_ = lps << nb;
-      if (c.state == 0) c.mps = static_cast<uint8_t>(1 - c.mps);
-      c.state = kTransIdxLps[c.state];
-      bits_left_ -= nb;
-    } else {
-      if (c.state < 62) ++c.state;
-      if (range_ >= 256) return;
-      low_ <<= 1;
-      range_ <<= 1;
-      --bits_left_;
-    }
-    if (bits_left_ < 12) write_out();
+    c.mps = static_cast<uint8_t>(mps ^ static_cast<uint32_t>(is_lps && s == 0));
+    c.state = kNextState[is_lps][s];
+    if (left < 12) write_out();
   }
 
   void bypass(int bin) {

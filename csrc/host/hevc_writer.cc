@@ -365,10 +365,37 @@ struct Writer {
   // 7.3.8.11 residual_coding.  The coefficient groups are visited through the scan
   // tables; each group's 16 levels are gathered once (4 row loads) and an all-zero
   // group costs 4 loads, so sparse 32x32 blocks are cheap.
-  void write_residual(const int16_t* blk, int stride, int log2, int cidx, int scan_idx) {
+  // significance contexts (9.3.4.2.5) per (TU size, component, scan, neighbouring coded
+  // sub-block flags, first sub-block or not, position in the sub-block's scan): a table
+  // lookup per coefficient instead of the derivation
+  struct SigTables {
+    uint8_t t[4][2][3][4][2][16];
+    SigTables() {
+      for (int l = 0; l < 4; ++l)
+        for (int c = 0; c < 2; ++c)
+          for (int sc = 0; sc < 3; ++sc)
+            for (int pc = 0; pc < 4; ++pc)
+              for (int g0 = 0; g0 < 2; ++g0)
+                for (int p = 0; p < 16; ++p) {
+                  const int q = scans().t[sc][2][p];
+                  const int xs = g0 ? 0 : 1, ys = 0;  // any sub-block other than the first
+                  t[l][c][sc][pc][g0][p] = static_cast<uint8_t>(
+                      sig_ctx(xs * 4 + (q & 15), ys * 4 + (q >> 4), l + 2, c, sc, pc, xs, ys));
+                }
+    }
+  };
+  static const SigTables& sig_tables() {
+    static const SigTables tables;
+    return tables;
+  }
+
+  // gmask: bit (ys * nsb + xs) set for every non-zero 4x4 sub-block of the TU (from the
+  // CTB's sub-block map), so all-zero sub-blocks are never loaded
+  void write_residual(const int16_t* blk, int stride, int log2, int cidx, int scan_idx, uint64_t gmask) {
     const int log2sb = log2 - 2, nsb = 1 << log2sb, nsbsq = nsb * nsb;
     const uint8_t* sbs = scans().t[scan_idx][log2sb];
     const uint8_t* ps = scans().t[scan_idx][2];
+    auto gbit = [&](int i) { return (gmask >> ((sbs[i] >> 4) * nsb + (sbs[i] & 15))) & 1u; };
     auto group_rows = [&](int i, int16_t (&rows)[4][4]) {
       const int xs = sbs[i] & 15, ys = sbs[i] >> 4;
       const int16_t* b = blk + static_cast<size_t>(ys * 4) * stride + xs * 4;
@@ -387,6 +414,7 @@ struct Writer {
     int last_i = -1, last_p = -1;
     int16_t lv[16];
     for (int i = nsbsq - 1; i >= 0 && last_i < 0; --i) {
+      if (!gbit(i)) continue;
       int16_t rows[4][4];
       group_rows(i, rows);
       if (!any_row(rows)) continue;
@@ -416,6 +444,8 @@ struct Writer {
       if (i == last_i) {
         std::memcpy(lvl, lv, sizeof(lvl));
         nonzero = true;
+      } else if (!gbit(i)) {
+        nonzero = false;
       } else {
         int16_t rows[4][4];
         group_rows(i, rows);
@@ -442,11 +472,12 @@ struct Writer {
       // significance
       int vals[16], nsig = 0;
       if (i == last_i) vals[nsig++] = lvl[last_p];
+      const uint8_t* sct = sig_tables().t[log2 - 2][cidx ? 1 : 0][scan_idx][prev_csbf][xs + ys == 0 ? 1 : 0];
+      CtxState* sctx = ctx + CTX_SIG;
       for (int p = (i == last_i ? last_p - 1 : 15); p >= 0; --p) {
         const int v = lvl[p];
         if (p > 0 || !infer_dc) {
-          const int xc = xs * 4 + (ps[p] & 15), yc = ys * 4 + (ps[p] >> 4);
-          e.encode(v != 0, ctx[CTX_SIG + sig_ctx(xc, yc, log2, cidx, scan_idx, prev_csbf, xs, ys)]);
+          e.encode(v != 0, sctx[sct[p]]);
           if (v != 0) infer_dc = false;
         }
         if (v != 0) vals[nsig++] = v;
@@ -515,20 +546,50 @@ struct Writer {
 
   static int mdcs(int mode) { return (mode >= 6 && mode <= 14) ? 2 : ((mode >= 22 && mode <= 30) ? 1 : 0); }
 
-  bool any_nonzero(int cidx, int x, int y, int n) const {  // n is a multiple of 4
-    const int stride = cidx ? W / 2 : W;
-    const int16_t* p = coef[cidx] + static_cast<size_t>(y) * stride + x;
-    for (int r = 0; r < n; ++r) {
-      uint64_t a = 0;
-      for (int k = 0; k < n; k += 4) {
-        uint64_t w;
-        std::memcpy(&w, p + static_cast<size_t>(r) * stride + k, 8);
-        a |= w;
+  // non-zero 4x4 sub-blocks of the current CTB: luma bit (by * 8 + bx), chroma (by * 4 + bx)
+  uint64_t nz_luma = 0;
+  uint32_t nz_chroma[2] = {0, 0};
+  void scan_ctb_nz(int x0, int y0) {
+    nz_luma = 0;
+    for (int by = 0; by < 8; ++by)
+      for (int bx = 0; bx < 8; ++bx) {
+        const int16_t* p = coef[0] + static_cast<size_t>(y0 + by * 4) * W + x0 + bx * 4;
+        uint64_t a = 0;
+        for (int r = 0; r < 4; ++r) {
+          uint64_t w;
+          std::memcpy(&w, p + static_cast<size_t>(r) * W, 8);
+          a |= w;
+        }
+        nz_luma |= static_cast<uint64_t>(a != 0) << (by * 8 + bx);
       }
-      if (a) return true;
+    const int cw = W / 2;
+    for (int c = 0; c < 2; ++c) {
+      nz_chroma[c] = 0;
+      for (int by = 0; by < 4; ++by)
+        for (int bx = 0; bx < 4; ++bx) {
+          const int16_t* p = coef[1 + c] + static_cast<size_t>(y0 / 2 + by * 4) * cw + x0 / 2 + bx * 4;
+          uint64_t a = 0;
+          for (int r = 0; r < 4; ++r) {
+            uint64_t w;
+            std::memcpy(&w, p + static_cast<size_t>(r) * cw, 8);
+            a |= w;
+          }
+          nz_chroma[c] |= static_cast<uint32_t>(a != 0) << (by * 4 + bx);
+        }
     }
-    return false;
   }
+  // sub-block mask of an n x n block at plane position (x, y) inside the current CTB, in
+  // the block's own raster order (bit ys * (n / 4) + xs)
+  uint64_t block_mask(int cidx, int x, int y, int n) const {
+    const int side = cidx ? 4 : 8, m = cidx ? 15 : 31;
+    const uint64_t src = cidx ? nz_chroma[cidx - 1] : nz_luma;
+    const int bx0 = (x & m) >> 2, by0 = (y & m) >> 2, nb = n >> 2;
+    uint64_t out = 0;
+    for (int r = 0; r < nb; ++r)
+      out |= ((src >> ((by0 + r) * side + bx0)) & ((1ull << nb) - 1ull)) << (r * nb);
+    return out;
+  }
+  bool any_nonzero(int cidx, int x, int y, int n) const { return block_mask(cidx, x, y, n) != 0; }
 
   // ---------------------------------------------------------------- inter prediction helpers
   struct Mv {
@@ -731,11 +792,11 @@ struct Writer {
       const bool cy = any_nonzero(0, xk, yk, 4);
       e.encode(cy, ctx[CTX_CBF_LUMA + 0]);
       if (c.cu_qp_delta && !qp_coded && (cy || cb_cb || cb_cr)) write_qp_delta();
-      if (cy) write_residual(coef[0] + static_cast<size_t>(yk) * W + xk, W, 2, 0, mdcs(m[k]));
+      if (cy) write_residual(coef[0] + static_cast<size_t>(yk) * W + xk, W, 2, 0, mdcs(m[k]), 1);
     }
     const int cstride = W / 2;
-    if (cb_cb) write_residual(coef[1] + static_cast<size_t>(y / 2) * cstride + x / 2, cstride, 2, 1, mdcs(m[0]));
-    if (cb_cr) write_residual(coef[2] + static_cast<size_t>(y / 2) * cstride + x / 2, cstride, 2, 2, mdcs(m[0]));
+    if (cb_cb) write_residual(coef[1] + static_cast<size_t>(y / 2) * cstride + x / 2, cstride, 2, 1, mdcs(m[0]), 1);
+    if (cb_cr) write_residual(coef[2] + static_cast<size_t>(y / 2) * cstride + x / 2, cstride, 2, 2, mdcs(m[0]), 1);
   }
 
   void write_merge_idx(int idx) {
@@ -771,11 +832,16 @@ struct Writer {
     const int stride = W, cstride = W / 2;
     if (cb_y) {
       const int scan = (intra && log2 == 3) ? mdcs(m) : 0;
-      write_residual(coef[0] + static_cast<size_t>(y) * stride + x, stride, log2, 0, scan);
+      write_residual(coef[0] + static_cast<size_t>(y) * stride + x, stride, log2, 0, scan, block_mask(0, x, y, 1 << log2));
     }
     const int scan_c = (intra && log2 - 1 == 2) ? mdcs(m) : 0;
-    if (cb_cb) write_residual(coef[1] + static_cast<size_t>(y / 2) * cstride + x / 2, cstride, log2 - 1, 1, scan_c);
-    if (cb_cr) write_residual(coef[2] + static_cast<size_t>(y / 2) * cstride + x / 2, cstride, log2 - 1, 2, scan_c);
+    const int nc = 1 << (log2 - 1);
+    if (cb_cb)
+      write_residual(coef[1] + static_cast<size_t>(y / 2) * cstride + x / 2, cstride, log2 - 1, 1, scan_c,
+                     block_mask(1, x / 2, y / 2, nc));
+    if (cb_cr)
+      write_residual(coef[2] + static_cast<size_t>(y / 2) * cstride + x / 2, cstride, log2 - 1, 2, scan_c,
+                     block_mask(2, x / 2, y / 2, nc));
   }
 
   // cu_qp_delta_abs (9.3.3.10: TR prefix cMax 5, ctxInc 0 then 1; EG0 bypass suffix) and
@@ -812,6 +878,7 @@ struct Writer {
     const int x0 = rx * kCtb, y0 = ry * kCtb;
     qp_ctb = t.qp;
     qp_coded = false;
+    scan_ctb_nz(x0, y0);
     auto split_ctx = [&](int x, int y, int d) {
       return (avail(x - 1, y) && depth[g(x - 1, y)] > d) + (avail(x, y - 1) && depth[g(x, y - 1)] > d);
     };

@@ -79,8 +79,8 @@ void mivc_launch_hevc_inter(int B, int W, int H, const uint16_t* sy, const uint1
 void mivc_launch_hevc_deblock(int B, int W, int H, int bd, uint16_t* y, uint16_t* u, uint16_t* v, const void* cu,
                               const void* ctu, const int8_t* run, void* stream);
 void mivc_launch_hevc_aq(int B, int W, int H, int bd, const uint16_t* sy, const uint16_t* su, const uint16_t* sv,
-                         const int* qp, float strength, const float* extra, long long extra_stride, int* ctb_qp,
-                         int8_t* mb_aq, void* stream);
+                         const int* qp, float strength, const float* extra, long long extra_stride, int extra_rows,
+                         int* ctb_qp, int8_t* mb_aq, void* stream);
 void mivc_launch_hevc_qp_fixup(int B, int W, int H, void* ctu, const void* cu, const int* qp, const int8_t* run,
                                int wpp, void* stream);
 void mivc_launch_hevc_sao(int B, int W, int H, int bd, const uint16_t* dy, const uint16_t* du, const uint16_t* dv,
@@ -301,11 +301,12 @@ PYBIND11_MODULE(_hip, m) {
                              P<int8_t>(run), S(stream));
   });
   m.def("hevc_aq", [](int B, int W, int H, int bd, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t qp,
-                      float strength, uintptr_t extra, long long extra_stride, uintptr_t ctb_qp, uintptr_t mb_aq,
-                      uintptr_t stream) {
+                      float strength, uintptr_t extra, long long extra_stride, int extra_rows, uintptr_t ctb_qp,
+                      uintptr_t mb_aq, uintptr_t stream) {
     if ((W & 31) || (H & 31)) throw std::invalid_argument("hevc_aq: coded size must be a multiple of 32");
+    if (extra && (extra_rows < 0 || extra_rows > H / 16)) throw std::invalid_argument("hevc_aq: extra_rows out of range");
     mivc_launch_hevc_aq(B, W, H, bd, P<uint16_t>(sy), P<uint16_t>(su), P<uint16_t>(sv), P<int>(qp), strength,
-                        P<float>(extra), extra_stride, P<int>(ctb_qp), P<int8_t>(mb_aq), S(stream));
+                        P<float>(extra), extra_stride, extra_rows, P<int>(ctb_qp), P<int8_t>(mb_aq), S(stream));
   });
   m.def("hevc_qp_fixup", [](int B, int W, int H, uintptr_t ctu, uintptr_t cu, uintptr_t qp, uintptr_t run, int wpp,
                             uintptr_t stream) {

@@ -466,7 +466,8 @@ __global__ __launch_bounds__(256) void hevc_aq_ctb(int W, int H, int bd, const u
                                                    const uint16_t* __restrict__ su, const uint16_t* __restrict__ sv,
                                                    const int* __restrict__ qp, float strength,
                                                    const float* __restrict__ extra, long long extra_stride,
-                                                   int* __restrict__ ctb_qp, int8_t* __restrict__ mb_aq) {
+                                                   int extra_rows, int* __restrict__ ctb_qp,
+                                                   int8_t* __restrict__ mb_aq) {
   __shared__ float s_off[4];
   const int wctb = W / 32, nctb = wctb * (H / 32), wmb = W / 16, nmb = wmb * (H / 16);
   const int ci = blockIdx.x, slot = blockIdx.y;
@@ -489,7 +490,7 @@ __global__ __launch_bounds__(256) void hevc_aq_ctb(int W, int H, int bd, const u
     float adj = 0.0f;
     if (strength > 0.0f)
       adj = strength * 1.0397f * (log2f(static_cast<float>(e > 1 ? e : 1)) - (14.427f + 2.0f * (bd - 8)));
-    if (extra) adj += extra[slot * extra_stride + my * wmb + mx];
+    if (extra && my < extra_rows) adj += extra[slot * extra_stride + my * wmb + mx];
     s_off[q] = adj;
   }
   __syncthreads();
@@ -605,12 +606,13 @@ extern "C" void mivc_launch_hevc_sao(int B, int W, int H, int bd, const uint16_t
 }
 
 // ctb_qp: [B, nctb] int32 out; mb_aq: [B, nmb16] int8 out (may be null); extra: optional
-// per-16x16 float offsets of slot s at extra + s * extra_stride
+// per-16x16 float offsets of slot s at extra + s * extra_stride, rows [0, extra_rows) of
+// the W / 16 wide grid (the lookahead's grid may stop short of the 32-aligned height)
 extern "C" void mivc_launch_hevc_aq(int B, int W, int H, int bd, const uint16_t* sy, const uint16_t* su,
                                     const uint16_t* sv, const int* qp, float strength, const float* extra,
-                                    long long extra_stride, int* ctb_qp, int8_t* mb_aq, void* stream) {
+                                    long long extra_stride, int extra_rows, int* ctb_qp, int8_t* mb_aq, void* stream) {
   hipLaunchKernelGGL(hevc_aq_ctb, dim3((W / 32) * (H / 32), B), dim3(256), 0, static_cast<hipStream_t>(stream), W, H,
-                     bd, sy, su, sv, qp, strength, extra, extra_stride, ctb_qp, mb_aq);
+                     bd, sy, su, sv, qp, strength, extra, extra_stride, extra_rows, ctb_qp, mb_aq);
 }
 
 extern "C" void mivc_launch_hevc_qp_fixup(int B, int W, int H, void* ctu, const void* cu, const int* qp,

@@ -201,8 +201,10 @@ class GpuHevcEncoder:
             y8 = (y >> (self.p.bit_depth - 8)).clamp_(0, 255).to(torch.uint8)
         lbw, lbh = GpuLookahead.block_grid(y.shape[3], y.shape[2])
         from ..rc.ratecontrol import MBTREE_STRENGTH, scenecut_flags
-        # cutree needs the lookahead's block grid to be the coded 16x16 grid (no -s resize)
-        use_tree = self.p.cutree and lbw == self.wmb and lbh == self.hmb
+        # cutree needs the lookahead's block grid to be the coded 16x16 grid (no -s resize); the
+        # 32-aligned coded height may add one 16-row below the lookahead's last row
+        use_tree = self.p.cutree and lbw == self.wmb and lbh <= self.hmb
+        self._cutree_rows = lbh
         if use_tree:
             costs_d, self._cutree = self._la.mbtree(y8.contiguous(), MBTREE_STRENGTH)
             costs = costs_d.cpu().numpy()
@@ -260,12 +262,13 @@ class GpuHevcEncoder:
             self._prep(y, u, v, t, proxy=not idr)
             self.qp.copy_(qps_d[t])  # device-to-device: no host sync inside the frame loop
             # per-CTB QPs (AQ + cutree offsets of frame t); without them every CTB at the frame QP
-            extra, estride = 0, 0
+            extra, estride, erows = 0, 0, 0
             if self._cutree is not None and self.p.adaptive_qp():
-                extra, estride = self._cutree.data_ptr() + t * self._cutree.shape[2] * 4, self._cutree.shape[1] * self._cutree.shape[2]
+                ct = self._cutree
+                extra, estride, erows = ct.data_ptr() + t * ct.shape[2] * 4, ct.shape[1] * ct.shape[2], self._cutree_rows
             self.hip.hevc_aq(B, self.W, self.H, bd, p(self.src[0]), p(self.src[1]), p(self.src[2]), p(self.qp),
-                             float(self.p.aq_strength) if self.p.adaptive_qp() else 0.0, extra, estride, p(self.ctb_qp),
-                             p(self.mb_aq), s)
+                             float(self.p.aq_strength) if self.p.adaptive_qp() else 0.0, extra, estride, erows,
+                             p(self.ctb_qp), p(self.mb_aq), s)
             cur, ref = self.rec[t % 2], self.rec[(t + 1) % 2]
             kb = t % 2
             # the copy-out of step t - 2 must have read these buffers before they are rewritten

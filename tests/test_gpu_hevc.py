@@ -89,7 +89,8 @@ def test_gpu_backend_hevc_preset(host, tmp_path):
         ref = c.y.astype(np.float64)
         dec = np.stack([p["y"][:96, :160] for p in pics]).astype(np.float64)
         mse = np.mean((ref - dec) ** 2)
-        assert 10 * np.log10(255 ** 2 / mse) > 30
+        # cutree's CRF compensation ((1 - qcomp) * 13.5 QP, as x265) dominates a 6-frame piece
+        assert 10 * np.log10(255 ** 2 / mse) > 27
     be.close()
 
 
