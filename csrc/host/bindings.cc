@@ -475,6 +475,105 @@ PYBIND11_MODULE(_host, m) {
       py::arg("cfg"), py::arg("frame"), py::arg("ctu"), py::arg("cu"), py::arg("coef_y"), py::arg("coef_cb"),
       py::arg("coef_cr"));
   m.def(
+      "hevc_write_slice_packed",
+      [](const py::dict& cfg, const py::dict& fp, py::array_t<uint8_t, py::array::c_style> ctu,
+         py::array_t<uint8_t, py::array::c_style> cu, py::array_t<uint64_t, py::array::c_style> nzmap,
+         py::array_t<uint32_t, py::array::c_style> ctb_off, py::array_t<int16_t, py::array::c_style> levels) {
+        // levels in the GPU encoder's packed form (hevc::PackedLevels)
+        hevc::HevcConfig c = hevc_cfg_from(cfg);
+        hevc::HevcFrameParams f;
+        f.idr = dget<int>(fp, "idr", 1);
+        f.poc = dget<int>(fp, "poc", 0);
+        f.qp = dget<int>(fp, "qp", 30);
+        f.slice_type = f.idr ? 2 : dget<int>(fp, "slice_type", 1);
+        const py::ssize_t nctu = static_cast<py::ssize_t>(c.wctb()) * c.hctb();
+        if (ctu.size() != nctu * 32) throw std::runtime_error("ctu records: wrong size");
+        if (cu.size() != nctu * hevc::kCusPerCtb * 8) throw std::runtime_error("cu records: wrong size");
+        if (nzmap.size() != nctu * 2 || ctb_off.size() != nctu) throw std::runtime_error("packed maps: wrong size");
+        if (levels.size() % 16) throw std::runtime_error("packed levels: not whole 4x4 blocks");
+        hevc::PackedLevels pk;
+        pk.nzmap = nzmap.data();
+        pk.ctb_off = ctb_off.data();
+        pk.levels = levels.data();
+        pk.nblocks = static_cast<size_t>(levels.size() / 16);
+        hevc::HevcSliceStats st;
+        std::vector<uint8_t> nal;
+        {
+          py::gil_scoped_release rel;
+          nal = hevc::hevc_write_slice(c, f, reinterpret_cast<const hevc::CtuInfo*>(ctu.data()),
+                                       reinterpret_cast<const hevc::CuInfo*>(cu.data()), nullptr, nullptr, nullptr, &st,
+                                       &pk);
+        }
+        py::dict stats;
+        stats["bins"] = st.bins;
+        stats["bytes"] = st.bytes;
+        return py::make_tuple(to_bytes(nal), stats);
+      },
+      py::arg("cfg"), py::arg("frame"), py::arg("ctu"), py::arg("cu"), py::arg("nzmap"), py::arg("ctb_off"),
+      py::arg("levels"));
+  m.def(
+      "hevc_write_slices_packed",
+      [](const py::dict& cfg, const py::list& frames, py::array_t<uint8_t, py::array::c_style> ctu,
+         py::array_t<uint8_t, py::array::c_style> cu, py::array_t<uint64_t, py::array::c_style> nzmap,
+         py::array_t<uint32_t, py::array::c_style> ctb_off, py::array_t<int16_t, py::array::c_style> levels,
+         int threads) {
+        // One picture per slot of a batch step ([B, ...] arrays, frames[b] = frame params),
+        // coded by `threads` native threads with the GIL released for the whole batch (a
+        // Python thread per picture would queue on the GIL after every slice).
+        hevc::HevcConfig c = hevc_cfg_from(cfg);
+        const py::ssize_t B = static_cast<py::ssize_t>(frames.size());
+        const py::ssize_t nctu = static_cast<py::ssize_t>(c.wctb()) * c.hctb();
+        if (ctu.ndim() != 3 || ctu.shape(0) < B || ctu.shape(1) != nctu || ctu.shape(2) != 32)
+          throw std::runtime_error("ctu records: expected [B, nctb, 32]");
+        if (cu.size() < B * nctu * hevc::kCusPerCtb * 8) throw std::runtime_error("cu records: wrong size");
+        if (nzmap.size() < B * nctu * 2 || ctb_off.size() < B * nctu) throw std::runtime_error("packed maps: wrong size");
+        if (levels.ndim() != 2 || levels.shape(0) < B || levels.shape(1) % 16) throw std::runtime_error("packed levels: [B, 16 n]");
+        std::vector<hevc::HevcFrameParams> fps(B);
+        for (py::ssize_t b = 0; b < B; ++b) {
+          const py::dict fp = frames[b].cast<py::dict>();
+          fps[b].idr = dget<int>(fp, "idr", 1);
+          fps[b].poc = dget<int>(fp, "poc", 0);
+          fps[b].qp = dget<int>(fp, "qp", 30);
+          fps[b].slice_type = fps[b].idr ? 2 : dget<int>(fp, "slice_type", 1);
+        }
+        const size_t per_lv = static_cast<size_t>(levels.shape(1));
+        std::vector<std::vector<uint8_t>> nals(B);
+        std::vector<std::string> errs(B);
+        {
+          py::gil_scoped_release rel;
+          std::atomic<py::ssize_t> next{0};
+          auto work = [&] {
+            for (py::ssize_t b = next++; b < B; b = next++) {
+              try {
+                hevc::PackedLevels pk;
+                pk.nzmap = nzmap.data() + static_cast<size_t>(b) * nctu * 2;
+                pk.ctb_off = ctb_off.data() + static_cast<size_t>(b) * nctu;
+                pk.levels = levels.data() + static_cast<size_t>(b) * per_lv;
+                pk.nblocks = per_lv / 16;
+                nals[b] = hevc::hevc_write_slice(
+                    c, fps[b], reinterpret_cast<const hevc::CtuInfo*>(ctu.data() + static_cast<size_t>(b) * nctu * 32),
+                    reinterpret_cast<const hevc::CuInfo*>(cu.data() + static_cast<size_t>(b) * nctu * hevc::kCusPerCtb * 8),
+                    nullptr, nullptr, nullptr, nullptr, &pk);
+              } catch (const std::exception& e) {
+                errs[b] = e.what();
+              }
+            }
+          };
+          const int nt = std::max(1, std::min<int>(threads, static_cast<int>(B)));
+          std::vector<std::thread> pool;
+          for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+          work();
+          for (std::thread& th : pool) th.join();
+        }
+        for (py::ssize_t b = 0; b < B; ++b)
+          if (!errs[b].empty()) throw std::runtime_error("HEVC slice " + std::to_string(b) + ": " + errs[b]);
+        py::list out;
+        for (py::ssize_t b = 0; b < B; ++b) out.append(to_bytes(nals[b]));
+        return out;
+      },
+      py::arg("cfg"), py::arg("frames"), py::arg("ctu"), py::arg("cu"), py::arg("nzmap"), py::arg("ctb_off"),
+      py::arg("levels"), py::arg("threads") = 1);
+  m.def(
       "hevc_decode",
       [](py::bytes data, bool skip_filters) {
         std::string s = data;

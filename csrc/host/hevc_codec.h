@@ -52,11 +52,25 @@ struct HevcSliceStats {
 // VPS + SPS + PPS as Annex-B NAL units
 std::vector<uint8_t> hevc_parameter_sets(const HevcConfig& cfg);
 
+// Quantised levels in the GPU encoder's packed form (hevc_nz_pack, hevc_filters.hip): only
+// the non-zero 4x4 blocks cross PCIe.  Per CTB (raster): nzmap[2 ci] luma sub-block bits
+// (by * 8 + bx), nzmap[2 ci + 1] Cb bits 0-15 and Cr bits 16-31 (by * 4 + bx); ctb_off[ci]
+// = index of the CTB's first block in `levels`; blocks in luma, Cb, Cr, bit order, 16
+// levels each (raster inside the block).
+struct PackedLevels {
+  const uint64_t* nzmap = nullptr;
+  const uint32_t* ctb_off = nullptr;
+  const int16_t* levels = nullptr;
+  size_t nblocks = 0;  // blocks available in `levels` (bounds check)
+};
+
 // One slice NAL (Annex-B) for a whole picture.  ctu: [wctb*hctb]; cu: [wctb*hctb*16]
-// (z-order granules); coef planes sized like the coded picture (luma) / half (chroma).
+// (z-order granules); coef planes sized like the coded picture (luma) / half (chroma), or
+// null with `packed` given.
 std::vector<uint8_t> hevc_write_slice(const HevcConfig& cfg, const HevcFrameParams& fp, const CtuInfo* ctu,
                                       const CuInfo* cu, const int16_t* coef_y, const int16_t* coef_cb,
-                                      const int16_t* coef_cr, HevcSliceStats* stats);
+                                      const int16_t* coef_cr, HevcSliceStats* stats,
+                                      const PackedLevels* packed = nullptr);
 
 struct HevcPicture {
   int width = 0, height = 0;            // cropped (display) size

@@ -215,6 +215,13 @@ struct Writer {
   int qp_prev = 0, qp_ctb = 0;
   bool qp_coded = false;
 
+  // packed coefficient source (hevc_write_slice_packed): per CTB the sub-block maps
+  // (nzmap[2 * ci]: luma bit by * 8 + bx; nzmap[2 * ci + 1]: Cb bits 0-15, Cr bits 16-31,
+  // by * 4 + bx), the CTB's first block in `packed` and the non-zero 4x4 blocks (16 levels
+  // each, raster) in luma, Cb, Cr, bit order
+  const PackedLevels* pk = nullptr;
+  uint32_t ctb_base = 0;
+
   Writer(const HevcConfig& cfg, const HevcFrameParams& f, const CtuInfo* ct, const CuInfo* cu_, const int16_t* cy,
          const int16_t* cb, const int16_t* cr, CabacEncoder& enc, PicState& ps)
       : c(cfg), fp(f), ctu(ct), cu(cu_), e(enc), depth(ps.depth), skip(ps.skip), pred(ps.pred), mode4(ps.mode4),
@@ -391,15 +398,38 @@ struct Writer {
 
   // gmask: bit (ys * nsb + xs) set for every non-zero 4x4 sub-block of the TU (from the
   // CTB's sub-block map), so all-zero sub-blocks are never loaded
-  void write_residual(const int16_t* blk, int stride, int log2, int cidx, int scan_idx, uint64_t gmask) {
+  // levels of the 4x4 block at plane position (px, py) of component cidx (in the current CTB)
+  void load4x4(int cidx, int px, int py, int16_t (&rows)[4][4]) const {
+    if (pk) {
+      const int side = cidx ? 4 : 8, m = cidx ? 15 : 31;
+      const int bit = ((py & m) >> 2) * side + ((px & m) >> 2);
+      uint32_t rank;
+      if (cidx == 0) {
+        rank = static_cast<uint32_t>(__builtin_popcountll(nz_luma & ((1ull << bit) - 1ull)));
+      } else {
+        rank = static_cast<uint32_t>(__builtin_popcountll(nz_luma));
+        if (cidx == 2) rank += static_cast<uint32_t>(__builtin_popcount(nz_chroma[0]));
+        rank += static_cast<uint32_t>(__builtin_popcount(nz_chroma[cidx - 1] & ((1u << bit) - 1u)));
+      }
+      const size_t at = static_cast<size_t>(ctb_base) + rank;
+      if (at >= pk->nblocks) throw std::runtime_error("HEVC packed levels: block index out of range");
+      std::memcpy(rows, pk->levels + at * 16, 32);
+      return;
+    }
+    const int stride = cidx ? W / 2 : W;
+    const int16_t* b = coef[cidx] + static_cast<size_t>(py) * stride + px;
+    for (int r = 0; r < 4; ++r) std::memcpy(rows[r], b + static_cast<size_t>(r) * stride, sizeof(rows[r]));
+  }
+
+  // residual_coding of the (1 << log2)^2 block of component cidx at plane position (bx0, by0)
+  void write_residual(int cidx, int bx0, int by0, int log2, int scan_idx, uint64_t gmask) {
     const int log2sb = log2 - 2, nsb = 1 << log2sb, nsbsq = nsb * nsb;
     const uint8_t* sbs = scans().t[scan_idx][log2sb];
     const uint8_t* ps = scans().t[scan_idx][2];
     auto gbit = [&](int i) { return (gmask >> ((sbs[i] >> 4) * nsb + (sbs[i] & 15))) & 1u; };
     auto group_rows = [&](int i, int16_t (&rows)[4][4]) {
       const int xs = sbs[i] & 15, ys = sbs[i] >> 4;
-      const int16_t* b = blk + static_cast<size_t>(ys * 4) * stride + xs * 4;
-      for (int r = 0; r < 4; ++r) std::memcpy(rows[r], b + static_cast<size_t>(r) * stride, sizeof(rows[r]));
+      load4x4(cidx, bx0 + xs * 4, by0 + ys * 4, rows);
     };
     auto any_row = [](const int16_t (&rows)[4][4]) {
       uint64_t a = 0;
@@ -550,6 +580,14 @@ struct Writer {
   uint64_t nz_luma = 0;
   uint32_t nz_chroma[2] = {0, 0};
   void scan_ctb_nz(int x0, int y0) {
+    if (pk) {
+      const size_t ci = static_cast<size_t>(y0 / kCtb) * wctb + x0 / kCtb;
+      nz_luma = pk->nzmap[2 * ci];
+      nz_chroma[0] = static_cast<uint32_t>(pk->nzmap[2 * ci + 1] & 0xFFFFu);
+      nz_chroma[1] = static_cast<uint32_t>((pk->nzmap[2 * ci + 1] >> 16) & 0xFFFFu);
+      ctb_base = pk->ctb_off[ci];
+      return;
+    }
     nz_luma = 0;
     for (int by = 0; by < 8; ++by)
       for (int bx = 0; bx < 8; ++bx) {
@@ -792,11 +830,10 @@ struct Writer {
       const bool cy = any_nonzero(0, xk, yk, 4);
       e.encode(cy, ctx[CTX_CBF_LUMA + 0]);
       if (c.cu_qp_delta && !qp_coded && (cy || cb_cb || cb_cr)) write_qp_delta();
-      if (cy) write_residual(coef[0] + static_cast<size_t>(yk) * W + xk, W, 2, 0, mdcs(m[k]), 1);
+      if (cy) write_residual(0, xk, yk, 2, mdcs(m[k]), 1);
     }
-    const int cstride = W / 2;
-    if (cb_cb) write_residual(coef[1] + static_cast<size_t>(y / 2) * cstride + x / 2, cstride, 2, 1, mdcs(m[0]), 1);
-    if (cb_cr) write_residual(coef[2] + static_cast<size_t>(y / 2) * cstride + x / 2, cstride, 2, 2, mdcs(m[0]), 1);
+    if (cb_cb) write_residual(1, x / 2, y / 2, 2, mdcs(m[0]), 1);
+    if (cb_cr) write_residual(2, x / 2, y / 2, 2, mdcs(m[0]), 1);
   }
 
   void write_merge_idx(int idx) {
@@ -832,16 +869,12 @@ struct Writer {
     const int stride = W, cstride = W / 2;
     if (cb_y) {
       const int scan = (intra && log2 == 3) ? mdcs(m) : 0;
-      write_residual(coef[0] + static_cast<size_t>(y) * stride + x, stride, log2, 0, scan, block_mask(0, x, y, 1 << log2));
+      write_residual(0, x, y, log2, scan, block_mask(0, x, y, 1 << log2));
     }
     const int scan_c = (intra && log2 - 1 == 2) ? mdcs(m) : 0;
     const int nc = 1 << (log2 - 1);
-    if (cb_cb)
-      write_residual(coef[1] + static_cast<size_t>(y / 2) * cstride + x / 2, cstride, log2 - 1, 1, scan_c,
-                     block_mask(1, x / 2, y / 2, nc));
-    if (cb_cr)
-      write_residual(coef[2] + static_cast<size_t>(y / 2) * cstride + x / 2, cstride, log2 - 1, 2, scan_c,
-                     block_mask(2, x / 2, y / 2, nc));
+    if (cb_cb) write_residual(1, x / 2, y / 2, log2 - 1, scan_c, block_mask(1, x / 2, y / 2, nc));
+    if (cb_cr) write_residual(2, x / 2, y / 2, log2 - 1, scan_c, block_mask(2, x / 2, y / 2, nc));
   }
 
   // cu_qp_delta_abs (9.3.3.10: TR prefix cMax 5, ctxInc 0 then 1; EG0 bypass suffix) and
@@ -905,7 +938,7 @@ struct Writer {
 
 std::vector<uint8_t> hevc_write_slice(const HevcConfig& c, const HevcFrameParams& fp, const CtuInfo* ctu,
                                       const CuInfo* cu, const int16_t* coef_y, const int16_t* coef_cb,
-                                      const int16_t* coef_cr, HevcSliceStats* stats) {
+                                      const int16_t* coef_cr, HevcSliceStats* stats, const PackedLevels* packed) {
   BitWriter bw;
   // 7.3.6.1 slice_segment_header
   const bool idr = fp.idr != 0;
@@ -937,6 +970,7 @@ std::vector<uint8_t> hevc_write_slice(const HevcConfig& c, const HevcFrameParams
     CabacEncoder enc(bw);
     enc.start();
     Writer w(c, fp, ctu, cu, coef_y, coef_cb, coef_cr, enc, ps);
+    w.pk = packed;
     for (int i = 0; i < n; ++i) {
       const int rx = i % wctb, ry = i / wctb;
       if (c.sao) w.write_sao(rx, ry);
@@ -973,6 +1007,7 @@ std::vector<uint8_t> hevc_write_slice(const HevcConfig& c, const HevcFrameParams
           CabacEncoder enc(sub[ry]);
           enc.start();
           Writer w(c, fp, ctu, cu, coef_y, coef_cb, coef_cr, enc, ps);
+          w.pk = packed;
           if (ry > 0 && wctb >= 2) {  // 9.3.2.4 sync from CTB (1, ry-1)
             wait_for(ry - 1, 2);
             std::copy(saved[ry - 1].begin(), saved[ry - 1].end(), w.ctx);

@@ -81,6 +81,9 @@ void mivc_launch_hevc_deblock(int B, int W, int H, int bd, uint16_t* y, uint16_t
 void mivc_launch_hevc_aq(int B, int W, int H, int bd, const uint16_t* sy, const uint16_t* su, const uint16_t* sv,
                          const int* qp, float strength, const float* extra, long long extra_stride, int extra_rows,
                          int* ctb_qp, int8_t* mb_aq, void* stream);
+void mivc_launch_hevc_pack_levels(int B, int W, int H, const int16_t* cy, const int16_t* cb, const int16_t* cr,
+                                  unsigned long long* nzmap, int* cnt, unsigned* off, long long cap_blocks, int16_t* out,
+                                  int* err, void* stream);
 void mivc_launch_hevc_qp_fixup(int B, int W, int H, void* ctu, const void* cu, const int* qp, const int8_t* run,
                                int wpp, void* stream);
 void mivc_launch_hevc_sao(int B, int W, int H, int bd, const uint16_t* dy, const uint16_t* du, const uint16_t* dv,
@@ -307,6 +310,16 @@ PYBIND11_MODULE(_hip, m) {
     if (extra && (extra_rows < 0 || extra_rows > H / 16)) throw std::invalid_argument("hevc_aq: extra_rows out of range");
     mivc_launch_hevc_aq(B, W, H, bd, P<uint16_t>(sy), P<uint16_t>(su), P<uint16_t>(sv), P<int>(qp), strength,
                         P<float>(extra), extra_stride, extra_rows, P<int>(ctb_qp), P<int8_t>(mb_aq), S(stream));
+  });
+  m.def("hevc_pack_levels", [](int B, int W, int H, uintptr_t cy, uintptr_t cb, uintptr_t cr, uintptr_t nzmap,
+                               uintptr_t cnt, uintptr_t off, long long cap_blocks, uintptr_t out, uintptr_t err,
+                               uintptr_t stream) {
+    if ((W & 31) || (H & 31)) throw std::invalid_argument("hevc_pack_levels: coded size must be a multiple of 32");
+    if (cap_blocks < static_cast<long long>(W / 32) * (H / 32) * 96)
+      throw std::invalid_argument("hevc_pack_levels: capacity below 96 blocks per CTB");
+    mivc_launch_hevc_pack_levels(B, W, H, P<int16_t>(cy), P<int16_t>(cb), P<int16_t>(cr),
+                                 P<unsigned long long>(nzmap), P<int>(cnt), P<unsigned>(off), cap_blocks,
+                                 P<int16_t>(out), P<int>(err), S(stream));
   });
   m.def("hevc_qp_fixup", [](int B, int W, int H, uintptr_t ctu, uintptr_t cu, uintptr_t qp, uintptr_t run, int wpp,
                             uintptr_t stream) {

@@ -539,6 +539,99 @@ __global__ __launch_bounds__(256) void hevc_qp_fixup(int wctb, int hctb, CtuInfo
   }
 }
 
+
+// ============================================================== sparse level hand-off
+// Only the non-zero 4x4 blocks of the quantised levels go to the host CABAC writer
+// (hevc::PackedLevels, hevc_codec.h): hevc_nz_map finds them per CTB (one wave: lane =
+// luma 4x4 block, lanes 0..31 = chroma blocks, ballots give the masks), hevc_nz_scan turns
+// the per-CTB block counts into offsets (one workgroup per slot), hevc_nz_pack copies each
+// non-zero block (32 bytes) to its rank in the slot's packed buffer, which is pinned host
+// memory: the picture's levels cross PCIe once and only where they are non-zero.
+__global__ __launch_bounds__(64) void hevc_nz_map(int W, int H, const int16_t* __restrict__ cy,
+                                                  const int16_t* __restrict__ cb, const int16_t* __restrict__ cr,
+                                                  unsigned long long* __restrict__ nzmap, int* __restrict__ cnt) {
+  const int wctb = W / 32, nctb = wctb * (H / 32);
+  const int ci = blockIdx.x, slot = blockIdx.y, l = lane_id();
+  const int rx = ci % wctb, ry = ci / wctb;
+  const int16_t* py = cy + static_cast<size_t>(slot) * W * H + static_cast<size_t>(ry * 32 + (l >> 3) * 4) * W + rx * 32 + (l & 7) * 4;
+  uint64_t a = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) a |= *reinterpret_cast<const uint64_t*>(py + static_cast<size_t>(r) * W);
+  const unsigned long long lm = __ballot(a != 0);
+  const int cw = W / 2;
+  uint64_t c = 0;
+  if (l < 32) {
+    const int k = l & 15;
+    const int16_t* pc = (l < 16 ? cb : cr) + static_cast<size_t>(slot) * cw * (H / 2) +
+                        static_cast<size_t>(ry * 16 + (k >> 2) * 4) * cw + rx * 16 + (k & 3) * 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) c |= *reinterpret_cast<const uint64_t*>(pc + static_cast<size_t>(r) * cw);
+  }
+  const unsigned long long cm = __ballot(l < 32 && c != 0) & 0xFFFFFFFFull;
+  if (l == 0) {
+    const size_t o = static_cast<size_t>(slot) * nctb + ci;
+    nzmap[2 * o] = lm;
+    nzmap[2 * o + 1] = cm;
+    cnt[o] = __popcll(lm) + __popcll(cm);
+  }
+}
+
+// per slot: exclusive scan of the block counts (chunked serial sums + Hillis-Steele)
+__global__ __launch_bounds__(1024) void hevc_nz_scan(int nctb, const int* __restrict__ cnt, unsigned* __restrict__ off,
+                                                     long long cap, int* __restrict__ err) {
+  const int slot = blockIdx.x;
+  __shared__ int s_sum[1024];
+  const int per = (nctb + blockDim.x - 1) / blockDim.x;
+  const int i0 = threadIdx.x * per, i1 = min(nctb, i0 + per);
+  const size_t base = static_cast<size_t>(slot) * nctb;
+  int sum = 0;
+  for (int i = i0; i < i1; ++i) sum += cnt[base + i];
+  s_sum[threadIdx.x] = sum;
+  __syncthreads();
+  for (int d = 1; d < blockDim.x; d <<= 1) {
+    const int v = threadIdx.x >= d ? s_sum[threadIdx.x - d] : 0;
+    __syncthreads();
+    s_sum[threadIdx.x] += v;
+    __syncthreads();
+  }
+  int run = threadIdx.x > 0 ? s_sum[threadIdx.x - 1] : 0;
+  for (int i = i0; i < i1; ++i) {
+    off[base + i] = static_cast<unsigned>(run);
+    run += cnt[base + i];
+  }
+  if (threadIdx.x == blockDim.x - 1 && s_sum[threadIdx.x] > cap) atomicAdd(err, 1);  // cannot happen: cap = all blocks
+}
+
+__global__ __launch_bounds__(64) void hevc_nz_pack(int W, int H, const int16_t* __restrict__ cy,
+                                                   const int16_t* __restrict__ cb, const int16_t* __restrict__ cr,
+                                                   const unsigned long long* __restrict__ nzmap,
+                                                   const unsigned* __restrict__ off, long long cap,
+                                                   int16_t* __restrict__ out) {
+  const int wctb = W / 32, nctb = wctb * (H / 32);
+  const int ci = blockIdx.x, slot = blockIdx.y, l = lane_id();
+  const int rx = ci % wctb, ry = ci / wctb;
+  const size_t o = static_cast<size_t>(slot) * nctb + ci;
+  const unsigned long long lm = nzmap[2 * o], cm = nzmap[2 * o + 1];
+  int16_t* dst = out + (static_cast<size_t>(slot) * cap + off[o]) * 16;
+  const int nl = __popcll(lm);
+  if ((lm >> l) & 1ull) {
+    const int rank = __popcll(lm & ((1ull << l) - 1ull));
+    const int16_t* py = cy + static_cast<size_t>(slot) * W * H + static_cast<size_t>(ry * 32 + (l >> 3) * 4) * W + rx * 32 + (l & 7) * 4;
+    uint64_t* d = reinterpret_cast<uint64_t*>(dst + rank * 16);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) d[r] = *reinterpret_cast<const uint64_t*>(py + static_cast<size_t>(r) * W);
+  }
+  if (l < 32 && ((cm >> l) & 1ull)) {
+    const int rank = nl + __popcll(cm & ((1ull << l) - 1ull));
+    const int k = l & 15, cw = W / 2;
+    const int16_t* pc = (l < 16 ? cb : cr) + static_cast<size_t>(slot) * cw * (H / 2) +
+                        static_cast<size_t>(ry * 16 + (k >> 2) * 4) * cw + rx * 16 + (k & 3) * 4;
+    uint64_t* d = reinterpret_cast<uint64_t*>(dst + rank * 16);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) d[r] = *reinterpret_cast<const uint64_t*>(pc + static_cast<size_t>(r) * cw);
+  }
+}
+
 }  // namespace gpu
 }  // namespace mivc
 
@@ -619,4 +712,16 @@ extern "C" void mivc_launch_hevc_qp_fixup(int B, int W, int H, void* ctu, const 
                                           const int8_t* run, int wpp, void* stream) {
   hipLaunchKernelGGL(hevc_qp_fixup, dim3(B), dim3(256), 0, static_cast<hipStream_t>(stream), W / 32, H / 32,
                      static_cast<CtuInfo*>(ctu), static_cast<const CuInfo*>(cu), qp, run, wpp);
+}
+
+// levels of B slots -> packed form: nzmap [B, nctb, 2] u64, off [B, nctb] u32, out: B slots of
+// cap_blocks 4x4 blocks (pinned host memory, device-visible); cnt: [B, nctb] int scratch
+extern "C" void mivc_launch_hevc_pack_levels(int B, int W, int H, const int16_t* cy, const int16_t* cb,
+                                             const int16_t* cr, unsigned long long* nzmap, int* cnt, unsigned* off,
+                                             long long cap_blocks, int16_t* out, int* err, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int nctb = (W / 32) * (H / 32);
+  hipLaunchKernelGGL(hevc_nz_map, dim3(nctb, B), dim3(64), 0, s, W, H, cy, cb, cr, nzmap, cnt);
+  hipLaunchKernelGGL(hevc_nz_scan, dim3(B), dim3(1024), 0, s, nctb, cnt, off, cap_blocks, err);
+  hipLaunchKernelGGL(hevc_nz_pack, dim3(nctb, B), dim3(64), 0, s, W, H, cy, cb, cr, nzmap, off, cap_blocks, out);
 }

@@ -12,9 +12,10 @@ per frame step t (frame t of every slot):
   -> hevc_qp_fixup (QpY of CTBs / CUs without a coded delta, 8.6.1)
   -> hevc_deblock (vertical, then horizontal edges; picture-parallel)
   -> hevc_sao (per-CTB statistics, decision, apply)
-then the decision records + level planes go to pinned host memory and a host thread
-pool writes one CABAC slice per picture (csrc/host/hevc_writer.cc) while the GPU
-works on the next step.
+then the decision records go to pinned host memory, the non-zero 4x4 level blocks are
+packed straight into pinned host memory (hevc_pack_levels: only coded levels cross
+PCIe), and a host thread pool writes one CABAC slice per picture
+(csrc/host/hevc_writer.cc) while the GPU works on the next step.
 
 Main (8-bit) and Main 10 share one code path: samples are uint16 on the device.
 """
@@ -137,6 +138,12 @@ class GpuHevcEncoder:
         self.ctus = [torch.zeros((B, self.nctb, 32), dtype=torch.uint8, device=dev) for _ in range(2)]
         self.cus = [torch.zeros((B, self.nctb * 16, 8), dtype=torch.uint8, device=dev) for _ in range(2)]
         self.ctu, self.cu = self.ctus[0], self.cus[0]
+        # sparse level hand-off (double-buffered like the records: the copy-out of step t
+        # overlaps step t + 1)
+        self.pack_cap = self.nctb * 96  # 4x4 blocks per slot: every block of every CTB
+        self.nzmaps = [torch.zeros((B, self.nctb, 2), dtype=torch.int64, device=dev) for _ in range(2)]
+        self.nzoffs = [torch.zeros((B, self.nctb), dtype=torch.int32, device=dev) for _ in range(2)]
+        self.nzcnt = torch.zeros((B, self.nctb), dtype=torch.int32, device=dev)
         self.copy_stream = torch.cuda.Stream(device=dev)
         self.copy_done = [torch.cuda.Event() for _ in range(2)]
         self.host_bufs = None  # lazily: 3 sets of pinned host buffers
@@ -147,7 +154,10 @@ class GpuHevcEncoder:
         self.run = torch.zeros((B,), dtype=torch.int8, device=dev)
         self.err = torch.zeros((1,), dtype=torch.int32, device=dev)
         self.params_nal = self.host.hevc_parameter_sets(params.host_cfg())
-        self.pool = cf.ThreadPoolExecutor(max_workers=entropy_threads or min(16, os.cpu_count() or 4))
+        # one Python worker hands each step's B pictures to the native batch writer, which
+        # codes them on `entropy_threads` C++ threads with the GIL released
+        self.entropy_threads = entropy_threads or min(16, os.cpu_count() or 4)
+        self.pool = cf.ThreadPoolExecutor(max_workers=1)
         self.timings: dict[str, float] = {}
         self.stats: dict[str, float] = {}
 
@@ -155,7 +165,9 @@ class GpuHevcEncoder:
         if self.host_bufs is None:
             def pin(t):
                 return torch.empty(t.shape, dtype=t.dtype).pin_memory()
-            self.host_bufs = [[pin(self.ctus[0]), pin(self.cus[0]), *(pin(c) for c in self.coefs[0])] for _ in range(3)]
+            self.host_bufs = [[pin(self.ctus[0]), pin(self.cus[0]), pin(self.nzmaps[0]), pin(self.nzoffs[0]),
+                               torch.empty((self.B, self.pack_cap * 16), dtype=torch.int16).pin_memory()]
+                              for _ in range(3)]
         return self.host_bufs
 
     def parameter_sets(self) -> bytes:
@@ -238,8 +250,8 @@ class GpuHevcEncoder:
         if qps is None:
             qps = np.array([[qi if t == 0 else qpp for t in range(F)] for _ in range(B)], dtype=np.int32)
         cfg = self.p.host_cfg()
-        if self.p.wpp:  # spread the pool's threads over the B pictures of a step
-            cfg["threads"] = max(1, min(32, self.pool._max_workers // max(1, B)))
+        if self.p.wpp:  # spread the native threads over the B pictures of a step
+            cfg["threads"] = max(1, min(32, self.entropy_threads // max(1, B)))
         qps = np.clip(np.asarray(qps, dtype=np.int32).reshape(B, F), 0, 51)
         if qp_delta is not None:
             from ..rc.abr import apply_delta
@@ -323,43 +335,49 @@ class GpuHevcEncoder:
                 pending[hb] = []
                 t_blocked += time.perf_counter() - tb
             host = self._host_buffers()[hb]
+            nzmap, nzoff = self.nzmaps[kb], self.nzoffs[kb]
+            # non-zero level blocks straight into this step's pinned host buffer
+            self.hip.hevc_pack_levels(B, self.W, self.H, p(self.coef[0]), p(self.coef[1]), p(self.coef[2]), p(nzmap),
+                                      p(self.nzcnt), p(nzoff), self.pack_cap, host[4].data_ptr(), p(self.err), s)
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.dev))
             with torch.cuda.stream(self.copy_stream):
                 self.copy_stream.wait_event(ev)
-                for dst, src_t in zip(host, (self.ctu, self.cu, *self.coef)):
+                for dst, src_t in zip(host[:4], (self.ctu, self.cu, nzmap, nzoff)):
                     dst.copy_(src_t, non_blocking=True)
                 done = torch.cuda.Event()
                 done.record(self.copy_stream)
                 self.copy_done[kb].record(self.copy_stream)
-            ctu, cu, cy, cb, cr = (h_.numpy() for h_ in host)
+            ctu, cu = host[0].numpy(), host[1].numpy()
+            nz, off, lv = host[2].numpy().view(np.uint64), host[3].numpy().view(np.uint32), host[4].numpy()
             t1 = time.perf_counter()
             t_gpu += t1 - t0
 
-            def job(b, t=t, idr=idr, done=done, ctu=ctu, cu=cu, cy=cy, cb=cb, cr=cr):
-                if b == 0 or not done.query():
-                    done.synchronize()
-                fp = dict(idr=int(idr), poc=t, qp=int(qps[b, t]), slice_type=2 if idr else 1)
+            fps = [dict(idr=int(idr), poc=t, qp=int(qps[b, t]), slice_type=2 if idr else 1) for b in range(B)]
+
+            def job(done=done, fps=fps, ctu=ctu, cu=cu, nz=nz, off=off, lv=lv):
+                done.synchronize()
                 tj = time.perf_counter()
-                r = self.host.hevc_write_slice(cfg, fp, ctu[b], cu[b], cy[b], cb[b], cr[b])
+                r = self.host.hevc_write_slices_packed(cfg, fps, ctu, cu, nz, off, lv, self.entropy_threads)
                 cabac_s[0] += time.perf_counter() - tj
                 return r
 
-            for b in range(B):
-                f = self.pool.submit(job, b)
-                futs.append((b, t, f))
-                pending[hb].append(f)
+            f = self.pool.submit(job)
+            futs.append((t, f))
+            pending[hb].append(f)
         if int(self.err.item()) != 0:
             raise RuntimeError("HEVC encoder: wavefront progress timeout")
         t2 = time.perf_counter()
         bits = [[0] * F for _ in range(B)]
-        for b, t, f in futs:
-            nal, st = f.result()
-            nals[b][t] = nal
-            bits[b][t] = 8 * len(nal)
+        for t, f in futs:
+            for b, nal in enumerate(f.result()):
+                nals[b][t] = nal
+                bits[b][t] = 8 * len(nal)
         t_host = time.perf_counter() - t2
+        # cabac_batch_s: wall time of the native batch writer (entropy_threads threads)
         self.timings = dict(loop_s=t_gpu, loop_blocked_on_cabac_s=t_blocked, host_wait_s=t_host,
-                            cabac_thread_s=cabac_s[0], cabac_ms_per_picture=1000.0 * cabac_s[0] / max(1, B * F))
+                            cabac_batch_s=cabac_s[0], cabac_ms_per_picture_wall=1000.0 * cabac_s[0] / max(1, B * F),
+                            entropy_threads=self.entropy_threads)
         out = []
         maxv = float((1 << bd) - 1)
         for b in range(B):

@@ -145,3 +145,61 @@ def expected_ctb_qps(ctu: np.ndarray, cy: np.ndarray, cb: np.ndarray, cr: np.nda
         out[i] = q
         prev = q
     return out
+
+
+def pack_levels(cy: np.ndarray, cb: np.ndarray, cr: np.ndarray):
+    """Level planes -> the GPU encoder's packed form (hevc::PackedLevels, numpy model of
+    hevc_nz_map / hevc_nz_pack): per CTB sub-block maps, first-block offsets, and the
+    non-zero 4x4 blocks in luma, Cb, Cr bit order."""
+    H, W = cy.shape
+    wc, hc = W // CTB, H // CTB
+    nz = np.zeros((wc * hc, 2), np.uint64)
+    off = np.zeros(wc * hc, np.uint32)
+    blocks = []
+    n = 0
+    for ci in range(wc * hc):
+        rx, ry = ci % wc, ci // wc
+        off[ci] = n
+        lm = cm = 0
+        for by in range(8):
+            for bx in range(8):
+                b = cy[ry * 32 + by * 4:ry * 32 + by * 4 + 4, rx * 32 + bx * 4:rx * 32 + bx * 4 + 4]
+                if b.any():
+                    lm |= 1 << (by * 8 + bx)
+                    blocks.append(b.copy())
+        for c, pl in enumerate((cb, cr)):
+            for by in range(4):
+                for bx in range(4):
+                    b = pl[ry * 16 + by * 4:ry * 16 + by * 4 + 4, rx * 16 + bx * 4:rx * 16 + bx * 4 + 4]
+                    if b.any():
+                        cm |= 1 << (16 * c + by * 4 + bx)
+                        blocks.append(b.copy())
+        nz[ci] = (lm, cm)
+        n = len(blocks)
+    lv = np.stack(blocks).reshape(-1) if blocks else np.zeros(16, np.int16)
+    return nz, off, lv.astype(np.int16)
+
+
+def unpack_levels(nz: np.ndarray, off: np.ndarray, lv: np.ndarray, W: int, H: int):
+    """Inverse of :func:`pack_levels`: packed non-zero 4x4 blocks -> level planes."""
+    wc = W // CTB
+    cy = np.zeros((H, W), np.int16)
+    cb = np.zeros((H // 2, W // 2), np.int16)
+    cr = np.zeros((H // 2, W // 2), np.int16)
+    blocks = lv.reshape(-1, 4, 4)
+    for ci in range(len(off)):
+        rx, ry = ci % wc, ci // wc
+        k = int(off[ci])
+        lm, cm = int(nz[ci, 0]), int(nz[ci, 1])
+        for bit in range(64):
+            if lm >> bit & 1:
+                by, bx = divmod(bit, 8)
+                cy[ry * 32 + by * 4:ry * 32 + by * 4 + 4, rx * 32 + bx * 4:rx * 32 + bx * 4 + 4] = blocks[k]
+                k += 1
+        for bit in range(32):
+            if cm >> bit & 1:
+                pl = cb if bit < 16 else cr
+                by, bx = divmod(bit & 15, 4)
+                pl[ry * 16 + by * 4:ry * 16 + by * 4 + 4, rx * 16 + bx * 4:rx * 16 + bx * 4 + 4] = blocks[k]
+                k += 1
+    return cy, cb, cr

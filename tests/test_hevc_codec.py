@@ -10,7 +10,8 @@ the independent decoder.
 import numpy as np
 import pytest
 
-from govideocompressor_amd.utils.hevc_synth import expected_ctb_qps, random_records, random_stream
+from govideocompressor_amd.utils.hevc_synth import (expected_ctb_qps, pack_levels, random_records, random_stream,
+                                                    unpack_levels)
 
 
 def _norm_sao(c):
@@ -155,3 +156,20 @@ def test_hevc_intra_nxn_roundtrip(host, pslice):
         assert np.array_equal(p["cu"][nx, 4:8], cu[nx, 4:8])
         assert np.array_equal(p["cu"][intra, 1], cu[intra, 1])
     assert n_nxn > 10
+
+
+@pytest.mark.parametrize("wpp", [0, 1])
+def test_hevc_packed_levels_same_bytes(host, wpp):
+    """The writer's packed-level input (only non-zero 4x4 blocks, as the GPU encoder hands
+    them over) produces the same slice bytes as the level planes."""
+    rng = np.random.default_rng(5)
+    cfg = dict(width=96, height=64, cu_qp_delta=1, wpp=wpp)
+    for t in range(3):
+        ctu, cu, cy, cb, cr = random_records(rng, 96, 64, pslice=t > 0, ctb_qp=(30, 6), nxn=0.4)
+        fp = dict(idr=int(t == 0), poc=t, qp=30, slice_type=1 if t else 2)
+        a, _ = host.hevc_write_slice(cfg, fp, ctu, cu, cy, cb, cr)
+        nz, off, lv = pack_levels(cy, cb, cr)
+        b, _ = host.hevc_write_slice_packed(cfg, fp, ctu, cu, nz, off, lv)
+        assert a == b
+        for x, y in zip(unpack_levels(nz, off, lv, 96, 64), (cy, cb, cr)):
+            assert np.array_equal(x, y)

@@ -23,7 +23,18 @@ class _Spy:
     def __getattr__(self, k):
         return getattr(self._h, k)
 
-    def hevc_write_slice(self, cfg, fp, ctu, cu, cy, cb, cr):
+    def hevc_write_slices_packed(self, cfg, fps, ctu, cu, nz, off, lv, threads=1):
+        return [self.hevc_write_slice_packed(cfg, fp, ctu[b], cu[b], nz[b], off[b], lv[b])[0]
+                for b, fp in enumerate(fps)]
+
+    def hevc_write_slice_packed(self, cfg, fp, ctu, cu, nz, off, lv):
+        from govideocompressor_amd.utils.hevc_synth import unpack_levels
+        W, H = -(-cfg["width"] // 32) * 32, -(-cfg["height"] // 32) * 32
+        if fp["poc"] in (0, 1):
+            self.hevc_write_slice(cfg, fp, ctu, cu, *unpack_levels(nz, off, lv, W, H), record_only=True)
+        return self._h.hevc_write_slice_packed(cfg, fp, ctu, cu, nz, off, lv)
+
+    def hevc_write_slice(self, cfg, fp, ctu, cu, cy, cb, cr, record_only=False):
         if fp["poc"] in (0, 1):
             i = self.n
             self.n += 1
@@ -31,6 +42,8 @@ class _Spy:
                 np.ascontiguousarray(a).tofile(os.path.join(self.out, f"{i}_{name}.bin"))
             self.meta.append(dict(cfg=cfg, fp=fp, cy=list(cy.shape), cb=list(cb.shape), ctu=list(ctu.shape),
                                   cu=list(cu.shape)))
+        if record_only:
+            return None
         return self._h.hevc_write_slice(cfg, fp, ctu, cu, cy, cb, cr)
 
 
