@@ -248,6 +248,9 @@ struct HevcSaoArgs {
 };
 
 struct SaoShared {
+  // the deblocked CTB with a one-sample border (luma 34 x 34, chroma 18 x 18 each): every
+  // sample is loaded once; statistics and apply read their neighbours here
+  uint16_t tile[34 * 34 + 2 * 18 * 18];
   int eo_cnt[3][4][4], eo_sum[3][4][4];   // [comp][class][category 1..4]
   int bo_cnt[3][32], bo_sum[3][32];
   int type[2], cls[2], band[3];
@@ -283,7 +286,23 @@ __global__ __launch_bounds__(256) void hevc_sao(HevcSaoArgs a) {
     (&S.bo_cnt[0][0])[i] = 0;
     (&S.bo_sum[0][0])[i] = 0;
   }
+  for (int i = tid; i < 34 * 34 + 2 * 18 * 18; i += 256) {
+    int c = 0, k = i;
+    if (i >= 34 * 34) {
+      c = 1 + (i - 34 * 34) / (18 * 18);
+      k = (i - 34 * 34) % (18 * 18);
+    }
+    const int ts = c ? 18 : 34, cs = c ? 16 : 32;
+    const int pw = c ? a.W / 2 : a.W, ph = c ? a.H / 2 : a.H;
+    const int X = clampi(rx * cs + k % ts - 1, 0, pw - 1), Y = clampi(ry * cs + k / ts - 1, 0, ph - 1);
+    const uint16_t* d = (c == 0 ? a.dy : (c == 1 ? a.du : a.dv)) + slot * static_cast<size_t>(pw) * ph;
+    S.tile[i] = d[static_cast<size_t>(Y) * pw + X];  // border samples outside the picture: never used
+  }
   __syncthreads();
+  // sample (x, y) of component c relative to its CTB block, x, y in [-1, cs]
+  auto T = [&](int c, int x, int y) -> int {
+    return c == 0 ? S.tile[(y + 1) * 34 + x + 1] : S.tile[34 * 34 + (c - 1) * 18 * 18 + (y + 1) * 18 + x + 1];
+  };
   static constexpr int hp[4][2] = {{-1, 1}, {0, 0}, {-1, 1}, {1, -1}};
   static constexpr int vp[4][2] = {{0, 0}, {-1, 1}, {-1, 1}, {-1, 1}};
   // ---- statistics (luma 1024 samples, chroma 2 x 256)
@@ -301,10 +320,9 @@ __global__ __launch_bounds__(256) void hevc_sao(HevcSaoArgs a) {
       }
       const int pw = c ? a.W / 2 : a.W, ph = c ? a.H / 2 : a.H, cs = c ? 16 : 32;
       const size_t ps = static_cast<size_t>(pw) * ph;
-      const uint16_t* d = (c == 0 ? a.dy : (c == 1 ? a.du : a.dv)) + slot * ps;
       const uint16_t* s = (c == 0 ? a.sy : (c == 1 ? a.su : a.sv)) + slot * ps;
       const int X = rx * cs + x, Y = ry * cs + y;
-      const int v = d[static_cast<size_t>(Y) * pw + X];
+      const int v = T(c, x, y);
       const int diff = static_cast<int>(s[static_cast<size_t>(Y) * pw + X]) - v;
       const int b = v >> (bd - 5);
       atomicAdd(&S.bo_cnt[c][b], 1);
@@ -313,7 +331,7 @@ __global__ __launch_bounds__(256) void hevc_sao(HevcSaoArgs a) {
       for (int k = 0; k < 4; ++k) {
         const int xa = X + hp[k][0], ya = Y + vp[k][0], xb = X + hp[k][1], yb = Y + vp[k][1];
         if (xa < 0 || ya < 0 || xb < 0 || yb < 0 || xa >= pw || xb >= pw || ya >= ph || yb >= ph) continue;
-        int e = 2 + sgn(v - d[static_cast<size_t>(ya) * pw + xa]) + sgn(v - d[static_cast<size_t>(yb) * pw + xb]);
+        int e = 2 + sgn(v - T(c, x + hp[k][0], y + vp[k][0])) + sgn(v - T(c, x + hp[k][1], y + vp[k][1]));
         if (e <= 2) e = (e == 2) ? 0 : e + 1;
         if (!e) continue;
         atomicAdd(&S.eo_cnt[c][k][e - 1], 1);
@@ -431,10 +449,9 @@ __global__ __launch_bounds__(256) void hevc_sao(HevcSaoArgs a) {
     }
     const int pw = c ? a.W / 2 : a.W, ph = c ? a.H / 2 : a.H, cs = c ? 16 : 32;
     const size_t ps = static_cast<size_t>(pw) * ph;
-    const uint16_t* d = (c == 0 ? a.dy : (c == 1 ? a.du : a.dv)) + slot * ps;
     uint16_t* o = (c == 0 ? a.y : (c == 1 ? a.u : a.v)) + slot * ps;
     const int X = rx * cs + x, Y = ry * cs + y;
-    const int v = d[static_cast<size_t>(Y) * pw + X];
+    const int v = T(c, x, y);
     const int type = S.type[c ? 1 : 0];
     int r = v;
     if (type == 1) {
@@ -444,7 +461,7 @@ __global__ __launch_bounds__(256) void hevc_sao(HevcSaoArgs a) {
       const int k = S.cls[c ? 1 : 0];
       const int xa = X + hp[k][0], ya = Y + vp[k][0], xb = X + hp[k][1], yb = Y + vp[k][1];
       if (!(xa < 0 || ya < 0 || xb < 0 || yb < 0 || xa >= pw || xb >= pw || ya >= ph || yb >= ph)) {
-        int e = 2 + sgn(v - d[static_cast<size_t>(ya) * pw + xa]) + sgn(v - d[static_cast<size_t>(yb) * pw + xb]);
+        int e = 2 + sgn(v - T(c, x + hp[k][0], y + vp[k][0])) + sgn(v - T(c, x + hp[k][1], y + vp[k][1]));
         if (e <= 2) e = (e == 2) ? 0 : e + 1;
         if (e) r = clampi(v + S.off[c][e - 1], 0, maxv);
       }

@@ -310,10 +310,6 @@ __global__ __launch_bounds__(256) void hevc_intra_analyze(HevcIntraArgs a) {
       const int si = it / 48;
       eval(it % 48, si < 2 ? si : 2 + 4 * (si - 2));  // seeds 0, 1, 2, 6, ..., 34
     }
-    for (int it = tid; it < 11 * kPuCount; it += 256) {
-      const int si = it / kPuCount;
-      eval4(it % kPuCount, si < 2 ? si : 2 + 4 * (si - 2));
-    }
   }
   __syncthreads();
   for (int step = 2; step >= 1; step >>= 1) {
@@ -327,17 +323,6 @@ __global__ __launch_bounds__(256) void hevc_intra_analyze(HevcIntraArgs a) {
         }
       }
       S.best_mode[tid] = bm;
-    } else if (tid >= 64 && tid < 64 + kPuCount) {
-      const int pu = tid - 64;
-      int bm = 2, bc = 0x7FFFFFFF;
-      for (int m = 2; m < 35; ++m) {
-        const int cst = S.cost4[pu][m];
-        if (S.done4[pu][m] && cst < bc) {
-          bc = cst;
-          bm = m;
-        }
-      }
-      S.best4_mode[pu] = bm;
     }
     __syncthreads();
     if (tid < 96) {
@@ -346,10 +331,6 @@ __global__ __launch_bounds__(256) void hevc_intra_analyze(HevcIntraArgs a) {
       const int c = level == 0 ? 0 : (level == 1 ? 1 + (k >> 2) : 5 + k);
       const int m = S.best_mode[c] + (tid < 48 ? -step : step);
       if (m >= 2 && m <= 34 && !S.done[c][m]) eval(slot48, m);
-    } else if (tid >= 128) {
-      const int pu = (tid - 128) & 63;
-      const int m = S.best4_mode[pu] + (tid < 192 ? -step : step);
-      if (m >= 2 && m <= 34 && !S.done4[pu][m]) eval4(pu, m);
     }
     __syncthreads();
   }
@@ -368,8 +349,40 @@ __global__ __launch_bounds__(256) void hevc_intra_analyze(HevcIntraArgs a) {
     }
     S.best_mode[tid] = bm;
     S.best_cost[tid] = bc + lam * 4;  // CU overhead: split flag, chroma mode, cbfs
-  } else if (tid >= 64 && tid < 64 + kPuCount) {
-    const int pu = tid - 64;
+  }
+  __syncthreads();
+  // 4x4 PUs (PART_NxN candidates): seeds planar, DC and the parent 8x8 CU's best mode
+  // +-2 (or the pure directions when it is planar / DC), then +-1 around the best angular
+  for (int it = tid; it < 5 * kPuCount; it += 256) {
+    const int pu = it % kPuCount, si = it / kPuCount;
+    const int m8 = S.best_mode[5 + (pu >> 2)];
+    int m;
+    if (si < 2) m = si;
+    else if (m8 >= 2) m = clampi(m8 + (si - 3) * 2, 2, 34);
+    else m = si == 2 ? 10 : (si == 3 ? 26 : 18);
+    if (!S.done4[pu][m]) eval4(pu, m);  // (clamped duplicates of one PU run in one iteration: same value)
+  }
+  __syncthreads();
+  if (tid < kPuCount) {
+    int bm = 2, bc = 0x7FFFFFFF;
+    for (int m = 2; m < 35; ++m) {
+      const int cst = S.cost4[tid][m];
+      if (S.done4[tid][m] && cst < bc) {
+        bc = cst;
+        bm = m;
+      }
+    }
+    S.best4_mode[tid] = bm;
+  }
+  __syncthreads();
+  if (tid < 2 * kPuCount) {
+    const int pu = tid & 63;
+    const int m = S.best4_mode[pu] + (tid < 64 ? -1 : 1);
+    if (m >= 2 && m <= 34 && !S.done4[pu][m]) eval4(pu, m);
+  }
+  __syncthreads();
+  if (tid < kPuCount) {
+    const int pu = tid;
     int bm = 0, bc = 0x7FFFFFFF;
     for (int m = 0; m < 35; ++m) {
       if (!S.done4[pu][m]) continue;

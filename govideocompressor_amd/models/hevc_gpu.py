@@ -215,7 +215,9 @@ class GpuHevcEncoder:
         from ..rc.ratecontrol import MBTREE_STRENGTH, scenecut_flags
         # cutree needs the lookahead's block grid to be the coded 16x16 grid (no -s resize); the
         # 32-aligned coded height may add one 16-row below the lookahead's last row
-        use_tree = self.p.cutree and lbw == self.wmb and lbh <= self.hmb
+        # Pieces shorter than 8 pictures give the propagation too little to offset cutree's
+        # constant CRF compensation ((1 - qcomp) x 13.5 QP): they keep the plain CRF QPs.
+        use_tree = self.p.cutree and lbw == self.wmb and lbh <= self.hmb and y.shape[1] >= 8
         self._cutree_rows = lbh
         if use_tree:
             costs_d, self._cutree = self._la.mbtree(y8.contiguous(), MBTREE_STRENGTH)

@@ -1,4 +1,4 @@
-# usage: BENCH_ARGS="..." bash tools/gpu/pmc_bench.sh <outdir>
+# usage: [BENCH_SCRIPT=bench/run.py] BENCH_ARGS="..." bash tools/gpu/pmc_bench.sh <outdir>
 # One rocprofv3 --pmc pass per counter group (each within the per-block limits: <=8 SQ,
 # <=4 TCC with FETCH_SIZE = 3 and WRITE_SIZE = 2, <=2 GRBM), every pass under its own hard
 # time limit; counters the device does not list are dropped; stops at the first failure.
@@ -18,7 +18,7 @@ pass() {
   echo "pass $name: ${keep[*]}" >> $R/gpurun_out/$out/passes.txt
   [ ${#keep[@]} -eq 0 ] && return 0
   timeout -s KILL 240 rocprofv3 --kernel-trace --pmc "${keep[@]}" -d $R/gpurun_out/$out/$name -o run -- \
-    python3 $R/bench.py $BENCH_ARGS > $R/gpurun_out/$out/$name.log 2>&1
+    python3 $R/${BENCH_SCRIPT:-bench.py} $BENCH_ARGS > $R/gpurun_out/$out/$name.log 2>&1
 }
 pass p1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT &&
 pass p2 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE &&
