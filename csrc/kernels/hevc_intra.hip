@@ -167,7 +167,7 @@ __device__ __forceinline__ void cu_of(int c, int* cx, int* cy, int* n, int* off)
   }
 }
 
-__global__ __launch_bounds__(256) void hevc_intra_analyze(HevcIntraArgs a) {
+__global__ __launch_bounds__(256, 4) void hevc_intra_analyze(HevcIntraArgs a) {
   __shared__ AnalyzeShared S;
   const HevcGeom& g = a.g;
   const int ci = blockIdx.x, slot = blockIdx.y;
