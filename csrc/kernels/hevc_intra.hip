@@ -646,8 +646,20 @@ __global__ __launch_bounds__(64 * kHevcIntraWaves) void hevc_intra_recon(HevcInt
   ReconShared& S = SS[w];
   for (int y = w; y < g.hctb; y += kHevcIntraWaves) {
     for (int x = 0; x < g.wctb; ++x) {
-      if (y > 0) row_wait(prog, y - 1, min(x + 2, g.wctb), a.err);
-      hevc_recon_ctb(a, S, D, slot, x, y, run);
+      // P picture: a CTB without intra CUs was fully reconstructed by hevc_inter -- no wait,
+      // no staging (the next CTB then reads its left column from memory)
+      bool work = true;
+      if (run == 2) {
+        const size_t cb = (static_cast<size_t>(slot) * g.nctb() + y * g.wctb + x) * 16;
+        work = __ballot(lane_id() < 16 && a.cu[cb + lane_id()].pred == hevc::CU_INTRA) != 0;
+      }
+      if (work) {
+        if (y > 0) row_wait(prog, y - 1, min(x + 2, g.wctb), a.err);
+        hevc_recon_ctb(a, S, D, slot, x, y, run);
+      } else {
+        if (lane_id() == 0) S.saved_x = -2;
+        wave_sync();
+      }
       row_publish(prog, y, x + 1);
     }
   }
