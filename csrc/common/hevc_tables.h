@@ -248,7 +248,8 @@ struct CuInfo {
   uint8_t pred;   // CuPred
   uint8_t mode;   // intra luma mode 0..34 (intra)
   uint8_t cbf;    // informational: bit0 Y, bit1 Cb, bit2 Cr (the writer recomputes it)
-  uint8_t flags;  // bit0: the CU is 8x8-granular log2 size - 3 in bits 1-2
+  uint8_t flags;  // bits 1-2: log2 CU size - 3; bit 3: intra PART_NxN; bit 4: inter TU split once
+                  // (cbf then describes the quarter TU covering this granule)
   int16_t mv[2];  // quarter-sample L0 motion vector (inter)
 };
 static_assert(sizeof(CuInfo) == 8, "CuInfo is 8 bytes");

@@ -817,15 +817,39 @@ struct HevcDecoder::Impl {
   }
 
   // ------------------------------------------------------------ transform tree (7.3.8.8)
-  void transform_tree(int x0, int y0, int log2, bool intra, int mode_y, int mode_c) {
+  // 7.3.8.8 (2Nx2N CUs): an explicit split_transform_flag where the depth allows it (inter
+  // CUs with max_transform_hierarchy_depth_inter 1), chroma cbfs at each level with a set
+  // parent cbf, cbf_luma coded below depth 0 or whenever chroma is coded
+  void transform_tree(int x0, int y0, int log2, bool intra, int mode_y, int mode_c, int depth = 0, int pcb = 1,
+                      int pcr = 1) {
     const int max_depth = intra ? sps.depth_intra : sps.depth_inter;
-    if (log2 <= sps.log2_max_tb && log2 > sps.log2_min_tb && 0 < max_depth)
-      throw std::runtime_error("HEVC: transform tree splits unsupported");
     if (log2 > sps.log2_max_tb) throw std::runtime_error("HEVC: implicit TU split unsupported");
-    const int cbf_cb = cd->decode(ctx[CTX_CBF_CHROMA + 0]);
-    const int cbf_cr = cd->decode(ctx[CTX_CBF_CHROMA + 0]);
+    int split = 0;
+    if (log2 <= sps.log2_max_tb && log2 > sps.log2_min_tb && depth < max_depth)
+      split = cd->decode(ctx[CTX_SPLIT_TRANSFORM + 5 - log2]);
+    int cbf_cb = 0, cbf_cr = 0;
+    if (depth == 0 || pcb) cbf_cb = cd->decode(ctx[CTX_CBF_CHROMA + depth]);
+    if (depth == 0 || pcr) cbf_cr = cd->decode(ctx[CTX_CBF_CHROMA + depth]);
+    if (split) {
+      if (intra || log2 - 1 < 3) throw std::runtime_error("HEVC: transform split below 8x8 / intra unsupported");
+      const int h = 1 << (log2 - 1);
+      for (int k = 0; k < 4; ++k) {
+        const int xc = x0 + (k & 1) * h, yc = y0 + (k >> 1) * h;
+        for (int j = 0; j < h; j += 4) {  // the child's boundary is a transform edge
+          edge_v[g4(xc, yc + j)] = 1;
+          edge_h[g4(xc + j, yc)] = 1;
+        }
+        if (sps.log2_ctb == kCtbLog2)
+          for (int gy = yc; gy < yc + h; gy += 8)
+            for (int gx = xc; gx < xc + h; gx += 8)
+              rec_cu[static_cast<size_t>((gy >> kCtbLog2) * wctb + (gx >> kCtbLog2)) * kCusPerCtb +
+                     zorder8((gx & 31) >> 3, (gy & 31) >> 3)].flags |= 16;
+        transform_tree(xc, yc, log2 - 1, intra, mode_y, mode_c, depth + 1, cbf_cb, cbf_cr);
+      }
+      return;
+    }
     int cbf_y = 1;
-    if (intra || cbf_cb || cbf_cr) cbf_y = cd->decode(ctx[CTX_CBF_LUMA + 1]);
+    if (intra || depth != 0 || cbf_cb || cbf_cr) cbf_y = cd->decode(ctx[CTX_CBF_LUMA + (depth == 0 ? 1 : 0)]);
     if (pps.cu_qp_delta && !qp_delta_coded && (cbf_y || cbf_cb || cbf_cr)) parse_qp_delta(x0, y0);
     if (log2 == 2) throw std::runtime_error("HEVC: 4x4 luma TUs unsupported");
     const int n = 1 << log2;

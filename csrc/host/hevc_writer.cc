@@ -120,7 +120,7 @@ std::vector<uint8_t> hevc_parameter_sets(const HevcConfig& c) {
     bw.put_ue(kCtbLog2 - kMinCbLog2);  // log2_diff_max_min_luma_coding_block_size
     bw.put_ue(0);                // log2_min_luma_transform_block_size_minus2 (4x4)
     bw.put_ue(3);                // log2_diff_max_min_luma_transform_block_size (32x32)
-    bw.put_ue(0);                // max_transform_hierarchy_depth_inter
+    bw.put_ue(c.tu_inter_depth);  // max_transform_hierarchy_depth_inter (x265 --tu-inter-depth)
     bw.put_ue(0);                // max_transform_hierarchy_depth_intra
     bw.put_bit(0);               // scaling_list_enabled_flag
     bw.put_bit(0);               // amp_enabled_flag
@@ -754,7 +754,10 @@ struct Writer {
         if (!merge) e.encode(root, ctx[CTX_RQT_ROOT_CBF]);
         mark(x, y, n, d, 0, CU_INTER, 1, mv);
         ++st.inter_cus;
-        if (root) write_tu(x, y, log2, false, 0, cb_y, cb_cb, cb_cr);
+        if (root) {
+          if (ci.flags & 16) write_tu_inter_split(x, y, log2, cb_cb, cb_cr);
+          else write_tu(x, y, log2, false, 0, cb_y, cb_cb, cb_cr);
+        }
         return;
       }
     }
@@ -860,7 +863,33 @@ struct Writer {
   void write_eg1(uint32_t v) { write_egk(v, 1); }
 
   // transform_tree at depth 0 with TU = CU (7.3.8.8 / 7.3.8.10)
+  // inter CU whose residual quadtree splits once (CuInfo flags bit 4): split_transform_flag,
+  // chroma cbfs at depth 0, then per quarter TU (z-order) its chroma cbfs under a set parent,
+  // cbf_luma (always coded below depth 0) and the transform unit
+  void write_tu_inter_split(int x, int y, int log2, bool cb_cb, bool cb_cr) {
+    if (c.tu_inter_depth < 1 || log2 < 4) throw std::runtime_error("HEVC: inter TU split needs depth 1 and a 16x16+ CU");
+    e.encode(1, ctx[CTX_SPLIT_TRANSFORM + 5 - log2]);
+    e.encode(cb_cb, ctx[CTX_CBF_CHROMA + 0]);
+    e.encode(cb_cr, ctx[CTX_CBF_CHROMA + 0]);
+    const int h = 1 << (log2 - 1);
+    for (int k = 0; k < 4; ++k) {
+      const int xc = x + (k & 1) * h, yc = y + (k >> 1) * h;
+      const bool ccb = cb_cb && any_nonzero(1, xc / 2, yc / 2, h / 2);
+      const bool ccr = cb_cr && any_nonzero(2, xc / 2, yc / 2, h / 2);
+      if (cb_cb) e.encode(ccb, ctx[CTX_CBF_CHROMA + 1]);
+      if (cb_cr) e.encode(ccr, ctx[CTX_CBF_CHROMA + 1]);
+      const bool cy = any_nonzero(0, xc, yc, h);
+      e.encode(cy, ctx[CTX_CBF_LUMA + 0]);
+      if (c.cu_qp_delta && !qp_coded && (cy || ccb || ccr)) write_qp_delta();
+      if (cy) write_residual(0, xc, yc, log2 - 1, 0, block_mask(0, xc, yc, h));
+      if (ccb) write_residual(1, xc / 2, yc / 2, log2 - 2, 0, block_mask(1, xc / 2, yc / 2, h / 2));
+      if (ccr) write_residual(2, xc / 2, yc / 2, log2 - 2, 0, block_mask(2, xc / 2, yc / 2, h / 2));
+    }
+  }
+
   void write_tu(int x, int y, int log2, bool intra, int m, bool cb_y, bool cb_cb, bool cb_cr) {
+    // split_transform_flag 0 where the inter depth allows a split (intra: depth 0 at 2Nx2N)
+    if (!intra && c.tu_inter_depth > 0 && log2 > 2) e.encode(0, ctx[CTX_SPLIT_TRANSFORM + 5 - log2]);
     e.encode(cb_cb, ctx[CTX_CBF_CHROMA + 0]);
     e.encode(cb_cr, ctx[CTX_CBF_CHROMA + 0]);
     if (intra || cb_cb || cb_cr) e.encode(cb_y, ctx[CTX_CBF_LUMA + 1]);

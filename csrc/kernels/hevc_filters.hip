@@ -163,9 +163,9 @@ __global__ void hevc_deblock(HevcDbkArgs a) {
   const int xp = a.dir == 0 ? xq - 1 : xq, yp = a.dir == 0 ? yq : yq - 1;
   const CuInfo& Q = cu_at(a, slot, xq, yq);
   const CuInfo& P = cu_at(a, slot, xp, yp);
-  const int lq = 3 + ((Q.flags >> 1) & 3);
+  const int lq = 3 + ((Q.flags >> 1) & 3) - ((Q.flags >> 4) & 1);  // TU size (inter CUs may split once)
   const int pos = a.dir == 0 ? xq : yq;
-  if (pos & ((1 << lq) - 1)) return;  // not a CU (TU = PU) boundary
+  if (pos & ((1 << lq) - 1)) return;  // not a transform / prediction block boundary
   int bs;
   if (P.pred == hevc::CU_INTRA || Q.pred == hevc::CU_INTRA) bs = 2;
   else if ((P.cbf & 1) || (Q.cbf & 1)) bs = 1;
@@ -547,6 +547,10 @@ __global__ __launch_bounds__(256) void hevc_qp_fixup(int wctb, int hctb, CtuInfo
         int first = 16;
         for (int k = 15; k >= 0; --k)
           if (g[k].cbf) first = k;
+        if (first < 16) {  // QpY is per CU: the whole CU whose TU carries the delta takes it
+          const int lgc = (g[first].flags >> 1) & 3;
+          first &= ~((1 << (2 * lgc)) - 1);
+        }
         CtuInfo& t = ctu[c];
         t.qp_pred = static_cast<int8_t>(prev);
         t.qp_first = static_cast<uint8_t>(first);

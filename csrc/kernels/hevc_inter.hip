@@ -36,6 +36,7 @@ struct HevcInterArgs {
   const int16_t* mv;     // [B, nmb16, 2] quarter-sample vectors per 16x16 block
   const int* me_cost;    // [B, nmb16] (8-bit proxy units)
   int bd;
+  int tu_split;          // inter CUs may code their residual as four quarter TUs (RD choice)
 };
 
 __device__ __forceinline__ int lambda_satd_i(int qp, int bd) {
@@ -137,8 +138,36 @@ struct InterShared {
   uint16_t win[39 * 39];  // reference window (n + 7)^2
   int tmp[39 * 32];       // horizontal pass
   int R[32 * 32], S[32 * 32];
+  int R2[32 * 32];        // luma residual / reconstruction of the quarter-TU alternative
+  int16_t lev2[32 * 32];  // its levels
   uint16_t pred[32 * 32];
 };
+
+// rate proxy of a block's levels (bits): ~3 + 2 log2|l| per non-zero level (wave reduction)
+__device__ __forceinline__ int level_bits(const int16_t* lev, int stride, int n) {
+  int b = 0;
+  for (int i = lane_id(); i < n * n; i += 64) {
+    const int v = lev[(i / n) * stride + i % n];
+    const int m = v < 0 ? -v : v;
+    if (m) b += 3 + 2 * (31 - __builtin_clz(m));
+  }
+  return sum64(b);
+}
+
+// SSD of clip(pred + R) against the source block (wave reduction; 64-bit: 32x32 at 10 bits)
+__device__ __forceinline__ long long recon_ssd(const InterShared& S, const int* R, const uint16_t* src, int pw, int bx,
+                                               int by, int n, int maxv) {
+  long long e = 0;
+  for (int i = lane_id(); i < n * n; i += 64) {
+    const int y = i / n, x = i - y * n;
+    int v = S.pred[i] + R[y * 32 + x];
+    v = v < 0 ? 0 : (v > maxv ? maxv : v);
+    const int d = static_cast<int>(src[static_cast<size_t>(by + y) * pw + bx + x]) - v;
+    e += d * d;
+  }
+  const int lo = static_cast<int>(e & 0x3FFFFFFF), hi = static_cast<int>(e >> 30);
+  return (static_cast<long long>(sum64(hi)) << 30) + sum64(lo);
+}
 
 // motion-compensated prediction of one n x n block of a component into S.pred
 // (8.5.3.3.3 fractional interpolation + 8.5.3.3.4.2 default weighted prediction)
@@ -198,6 +227,9 @@ __device__ __forceinline__ void mc_block(InterShared& S, const uint16_t* ref, in
   wave_sync();
 }
 
+// TSPLIT: the instance with the residual-quadtree choice (its register footprint stays out of
+// the default instance)
+template <bool TSPLIT>
 __global__ __launch_bounds__(64) void hevc_inter_cu(HevcInterArgs a) {
   __shared__ InterShared S;
   __shared__ hv::DctLds D;
@@ -223,7 +255,12 @@ __global__ __launch_bounds__(64) void hevc_inter_cu(HevcInterArgs a) {
   const int bd = a.bd, maxv = (1 << bd) - 1;
   const int qpy = a.qp[cb], off = 6 * (bd - 8);
   const int qpl = qpy + off, qpc = hevc::chroma_qp_map(clampi(qpy, -off, 57)) + off;
-  int cbf = 0;
+  // residual quadtree: the luma residual is transformed both as one TU and as four quarter
+  // TUs; the cheaper by SSD + lambda * (level-bit proxy + TU overhead) wins, and chroma
+  // follows the chosen structure (max_transform_hierarchy_depth_inter 1)
+  int cbfq[4] = {0, 0, 0, 0};  // per quarter: bit c = component c has levels in that quarter's TU
+  bool split = false;
+  const int h = n >> 1;
   for (int c = 0; c < 3; ++c) {
     const int pw = c ? g.W / 2 : g.W, ph = c ? g.H / 2 : g.H, bs = c ? n / 2 : n;
     const int bx = c ? X0 / 2 : X0, by = c ? Y0 / 2 : Y0;
@@ -236,22 +273,69 @@ __global__ __launch_bounds__(64) void hevc_inter_cu(HevcInterArgs a) {
     else mc_block<4>(S, ref, pw, ph, bx, by, bs, mvx, mvy, bd);
     for (int i = lane; i < bs * bs; i += 64) {
       const int y = i / bs, x = i - y * bs;
-      S.R[y * 32 + x] = static_cast<int>(src[static_cast<size_t>(by + y) * pw + bx + x]) - S.pred[i];
+      const int r = static_cast<int>(src[static_cast<size_t>(by + y) * pw + bx + x]) - S.pred[i];
+      S.R[y * 32 + x] = r;
+      if (c == 0) S.R2[y * 32 + x] = r;
     }
     wave_sync();
     const int l2 = c ? lg - 1 : lg;
-    hv::TqParams tp{l2, bd, c ? qpc : qpl, false};
-    const bool nz = hv::transform_quant_block(D, S.R, S.S, lev, pw, tp);
-    cbf |= nz << c;
+    const int qc = c ? qpc : qpl;
+    if (TSPLIT && c == 0) {
+      const bool nz = hv::transform_quant_block(D, S.R, S.S, lev, pw, hv::TqParams{l2, bd, qc, false});
+      for (int k = 0; k < 4; ++k) cbfq[k] = nz;
+      {
+        bool nzq[4];
+        for (int k = 0; k < 4; ++k) {
+          const int o = (k >> 1) * h * 32 + (k & 1) * h;
+          nzq[k] = hv::transform_quant_block(D, S.R2 + o, S.S, S.lev2 + o, 32, hv::TqParams{l2 - 1, bd, qc, false});
+        }
+        const bool any = nzq[0] || nzq[1] || nzq[2] || nzq[3];
+        if (any) {
+          // lambda for SSD (HM: 0.57 * 2^((QP - 12) / 3), at the coded bit depth)
+          const float lam = 0.57f * exp2f((qpy - 12) / 3.0f) * static_cast<float>(1 << (2 * (bd - 8)));
+          const long long d1 = recon_ssd(S, S.R, src, pw, bx, by, n, maxv);
+          const long long d4 = recon_ssd(S, S.R2, src, pw, bx, by, n, maxv);
+          const int b1 = level_bits(lev, pw, n) + (nz ? 2 * lg + 2 : 0);
+          const int b4 = level_bits(S.lev2, 32, n) + 4 + (nzq[0] + nzq[1] + nzq[2] + nzq[3]) * (2 * lg);
+          split = static_cast<float>(d4) + lam * b4 < static_cast<float>(d1) + lam * b1;
+        }
+        if (split) {
+          for (int i = lane; i < n * n; i += 64) {
+            const int y = i / n, x = i - y * n;
+            lev[y * pw + x] = S.lev2[y * 32 + x];
+            S.R[y * 32 + x] = S.R2[y * 32 + x];
+          }
+          for (int k = 0; k < 4; ++k) cbfq[k] = nzq[k];
+        }
+        wave_sync();
+      }
+    } else if (TSPLIT && split) {
+      const int hc = bs >> 1;
+      for (int k = 0; k < 4; ++k) {
+        const int o = (k >> 1) * hc * 32 + (k & 1) * hc;
+        const bool nz = hv::transform_quant_block(D, S.R + o, S.S, lev + (k >> 1) * hc * pw + (k & 1) * hc, pw,
+                                                  hv::TqParams{l2 - 1, bd, qc, false});
+        cbfq[k] |= nz << c;
+      }
+    } else {
+      const bool nz = hv::transform_quant_block(D, S.R, S.S, lev, pw, hv::TqParams{l2, bd, qc, false});
+      for (int k = 0; k < 4; ++k) cbfq[k] |= nz << c;
+    }
+    // (a block without levels has an all-zero dequantised residual in R)
     for (int i = lane; i < bs * bs; i += 64) {
       const int y = i / bs, x = i - y * bs;
-      int v = S.pred[i] + (nz ? S.R[y * 32 + x] : 0);
+      int v = S.pred[i] + S.R[y * 32 + x];
       rec[static_cast<size_t>(by + y) * pw + bx + x] = static_cast<uint16_t>(v < 0 ? 0 : (v > maxv ? maxv : v));
     }
     wave_sync();
   }
+  // granule records: split flag; cbf = that of the TU covering the granule
   const int ng = lg == 5 ? 16 : 4;
-  if (lane < ng) cu[kq + lane].cbf = static_cast<uint8_t>(cbf);
+  if (lane < ng) {
+    const int k = lg == 5 ? lane >> 2 : lane;  // z-order: the quarter of a 32x32 CU holds 4 granules
+    cu[kq + lane].cbf = static_cast<uint8_t>(split ? cbfq[k] : cbfq[0]);
+    if (split) cu[kq + lane].flags |= 16;
+  }
 }
 
 }  // namespace gpu
@@ -263,7 +347,7 @@ extern "C" void mivc_launch_hevc_inter(int B, int W, int H, const uint16_t* sy, 
                                        const uint16_t* fy, const uint16_t* fu, const uint16_t* fv, uint16_t* ry,
                                        uint16_t* ru, uint16_t* rv, void* ctu, void* cu, int16_t* cy, int16_t* cu_,
                                        int16_t* cv, const int* qp, const int8_t* run, const int* cand,
-                                       const int16_t* mv, const int* me_cost, int bd, void* stream) {
+                                       const int16_t* mv, const int* me_cost, int bd, int tu_split, void* stream) {
   HevcInterArgs a;
   a.g = HevcGeom{B, W, H, W / 32, H / 32};
   a.src_y = sy;
@@ -286,7 +370,9 @@ extern "C" void mivc_launch_hevc_inter(int B, int W, int H, const uint16_t* sy, 
   a.mv = mv;
   a.me_cost = me_cost;
   a.bd = bd;
+  a.tu_split = tu_split;
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(hevc_p_decide, dim3(a.g.nctb(), B), dim3(64), 0, s, a);
-  hipLaunchKernelGGL(hevc_inter_cu, dim3(a.g.nctb() * 4, B), dim3(64), 0, s, a);
+  if (tu_split) hipLaunchKernelGGL(hevc_inter_cu<true>, dim3(a.g.nctb() * 4, B), dim3(64), 0, s, a);
+  else hipLaunchKernelGGL(hevc_inter_cu<false>, dim3(a.g.nctb() * 4, B), dim3(64), 0, s, a);
 }

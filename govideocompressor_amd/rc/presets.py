@@ -22,7 +22,8 @@ placebo     = veryslow
 ==========  ========================================================================
 
 HEVC (x265): ultrafast..veryfast use radius 4 / half-pel / 3 merge candidates, fast and
-medium the defaults, slow and slower radius 12 / 5 candidates, veryslow/placebo radius 16.
+medium the defaults, slow and slower radius 12 / 5 candidates, veryslow/placebo radius 16;
+slow and slower presets add the inter residual quadtree (--tu-inter-depth 1).
 """
 from __future__ import annotations
 
@@ -51,9 +52,9 @@ HEVC = {
     "faster": dict(me_range=8, max_merge=3),
     "fast": dict(me_range=8, max_merge=4),
     "medium": dict(),
-    "slow": dict(me_range=12),
-    "slower": dict(me_range=12, la_range=8),
-    "veryslow": dict(me_range=16, la_range=8),
+    "slow": dict(me_range=12, tu_inter_depth=1),
+    "slower": dict(me_range=12, la_range=8, tu_inter_depth=1),
+    "veryslow": dict(me_range=16, la_range=8, tu_inter_depth=1),
 }
 HEVC["placebo"] = HEVC["veryslow"]
 

@@ -45,9 +45,10 @@ def _levels(rng, n: int, density: float) -> np.ndarray:
 
 def random_records(rng, width: int, height: int, pslice: bool, bit_depth: int = 8, density: float = 0.08,
                    intra_in_p: float = 0.2, mv_range: int = 64, sao: bool = True, ctb_qp: tuple | None = None,
-                   nxn: float = 0.0):
+                   nxn: float = 0.0, tu_split: float = 0.0):
     """``ctb_qp = (qp, spread)``: per-CTB QPs qp + U[-spread, spread] (cu_qp_delta streams);
-    ``nxn``: probability of an 8x8 intra CU being split into four 4x4 PUs."""
+    ``nxn``: probability of an 8x8 intra CU being split into four 4x4 PUs; ``tu_split``: of a
+    16x16 / 32x32 inter CU coding its residual as four quarter TUs (needs tu_inter_depth 1)."""
     W, H = -(-width // CTB) * CTB, -(-height // CTB) * CTB
     wc, hc = W // CTB, H // CTB
     ctu = np.zeros((wc * hc, 32), np.uint8)
@@ -91,6 +92,8 @@ def random_records(rng, width: int, height: int, pslice: bool, bit_depth: int = 
                     rec[4:8] = rng.integers(0, 35, 4)
                     rec[4] = rec[1]
             else:
+                if n >= 16 and rng.random() < tu_split:   # residual quadtree split once (flags bit 4)
+                    rec[3] |= 16
                 mv = rng.integers(-mv_range, mv_range + 1, 2).astype(np.int16)
                 if rng.random() < 0.3:
                     mv[:] = 0

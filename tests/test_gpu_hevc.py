@@ -169,3 +169,14 @@ def test_gpu_hevc_intra_nxn(host, bd):
         for p in host.hevc_decode(r.bitstream):
             n += int(((p["cu"][:, 3] & 8) != 0).sum())
     assert n > 0
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+def test_gpu_hevc_inter_tu_split(host, bd):
+    """tu_inter_depth 1: inter CUs pick one TU or four quarter TUs by RD; the split CUs
+    (split_transform_flag, per-quarter cbfs, transform edges inside the CU for deblocking)
+    decode bit-exactly, and some CUs do split."""
+    res, rec = _encode(128, 96, 5, 2, bd=bd, crf=None, qp=24, tu_inter_depth=1)
+    _compare(host, res, rec)
+    n = sum(int(((p["cu"][:, 3] & 16) != 0).sum()) for r in res for p in host.hevc_decode(r.bitstream))
+    assert n > 0

@@ -173,3 +173,24 @@ def test_hevc_packed_levels_same_bytes(host, wpp):
         assert a == b
         for x, y in zip(unpack_levels(nz, off, lv, 96, 64), (cy, cb, cr)):
             assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("wpp", [0, 1])
+def test_hevc_inter_tu_split_roundtrip(host, wpp):
+    """max_transform_hierarchy_depth_inter 1: inter CUs coding their residual as four quarter
+    TUs (split_transform_flag, chroma cbfs under the parent's, cbf_luma per quarter) next to
+    unsplit ones, with per-CTB QPs and intra NxN: levels and the split flags decode back."""
+    w, h = 96, 64
+    s, recs = random_stream(host, w, h, 4, seed=33 + wpp, qp_spread=6, nxn=0.3, tu_split=0.5, intra_in_p=0.2,
+                            host_cfg=dict(cu_qp_delta=1, wpp=wpp, tu_inter_depth=1))
+    pics = host.hevc_decode(s, False)
+    n_split = 0
+    for p, (ctu, cu, cy, cb, cr) in zip(pics, recs):
+        assert np.array_equal(p["coef_y"], cy) and np.array_equal(p["coef_cb"], cb) and np.array_equal(p["coef_cr"], cr)
+        inter = cu[:, 0] == 1
+        # the decoder marks a split only for CUs that coded a residual (rqt_root_cbf)
+        dec_split = (p["cu"][:, 3] & 16) != 0
+        assert not (dec_split & ~((cu[:, 3] & 16) != 0)).any()
+        n_split += int(dec_split.sum())
+        assert np.array_equal(p["cu"][inter, 4:8], cu[inter, 4:8])
+    assert n_split > 8
