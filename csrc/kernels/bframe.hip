@@ -339,6 +339,96 @@ __global__ __launch_bounds__(64) void p_mv_refine(PRefineArgs a) {
 }
 
 
+// ---- HEVC merge-aware vector choice (the H.265 analogue of p_mv_refine): after the 16x16
+// search each block is offered the current vectors of its spatial merge neighbours (A1 left,
+// B1 above, B0 above-right, A0 below-left, B2 above-left; 8.5.3.2.3) and the zero vector;
+// the cheapest by SATD + lambda * (merge_idx bits) replaces the searched vector when it beats
+// the search's SATD + lambda * mvd bits, so the CABAC writer can code the CU as merge / skip.
+// Jacobi pass: reads mv_in, writes mv_out.  (The candidates approximate the normative merge
+// list on the 16x16 grid; the writer codes AMVP whenever the vector is not in the real list.)
+__global__ __launch_bounds__(64) void hevc_merge_refine(PRefineArgs a) {
+  const Geom& g = a.g;
+  const int nmb = g.nmb();
+  int mb, slot;
+  xcd_unit_slot(mb, slot);
+  const int lane = threadIdx.x;
+  const size_t o = static_cast<size_t>(slot) * nmb + mb;
+  const int mx = mb % g.wmb, my = mb / g.wmb;
+  const int16_t* mv = a.mv_in + static_cast<size_t>(slot) * nmb * 2;
+  const int cx = mv[mb * 2], cy = mv[mb * 2 + 1];
+  int kx[6], ky[6], nk = 0;
+  auto add = [&](bool ok, int n) {
+    if (!ok) return;
+    const int vx = mv[n * 2], vy = mv[n * 2 + 1];
+    for (int j = 0; j < nk; ++j)
+      if (kx[j] == vx && ky[j] == vy) return;
+    kx[nk] = vx;
+    ky[nk] = vy;
+    ++nk;
+  };
+  add(mx > 0, mb - 1);                              // A1
+  add(my > 0, mb - g.wmb);                          // B1
+  add(my > 0 && mx < g.wmb - 1, mb - g.wmb + 1);    // B0
+  add(mx > 0 && my < g.hmb - 1, mb + g.wmb - 1);    // A0
+  add(mx > 0 && my > 0, mb - g.wmb - 1);            // B2
+  {
+    bool z = false;
+    for (int j = 0; j < nk; ++j) z |= kx[j] == 0 && ky[j] == 0;
+    if (!z) {
+      kx[nk] = 0;
+      ky[nk] = 0;
+      ++nk;
+    }
+  }
+  const int qp = clampi(a.qp[slot] + (a.aq ? a.aq[o] : 0), 0, 51);
+  const int lambda = h264::kLambda[qp];
+  const int pmx = a.pm ? a.pm[o * 2] : 0, pmy = a.pm ? a.pm[o * 2 + 1] : 0;
+  const int c_me = a.cost[o];  // SATD + lambda * mvd bits against the search predictor
+  const int W = g.W, H = g.H;
+  const int r = lane >> 2, c0 = (lane & 3) * 4;
+  const int X = mx * 16 + c0, Y = my * 16 + r;
+  const size_t yo = static_cast<size_t>(slot) * g.ysize();
+  const uint8_t* G0 = a.ref + yo;
+  const uint8_t* H0 = a.hp + static_cast<size_t>(slot) * 3 * (W + 2 * kHpMargin) * (H + 2 * kHpMargin);
+  const uint32_t src = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y) * W + X);
+  __shared__ int s_res[256];
+  int best = c_me, bx_ = cx, by_ = cy;
+  for (int j = 0; j < nk; ++j) {
+    if (kx[j] == cx && ky[j] == cy) {  // the searched vector is itself a merge candidate
+      best = min(best, c_me - lambda * (mvbits_se(cx - pmx) + mvbits_se(cy - pmy)) + lambda * (1 + j));
+      continue;
+    }
+    const uint32_t ps = mc4(G0, H0, W, H, X, Y, kx[j], ky[j]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      s_res[r * 16 + c0 + k] = static_cast<int>((src >> (8 * k)) & 255u) - static_cast<int>((ps >> (8 * k)) & 255u);
+    wave_sync();
+    int satd = 0;
+    if (lane < 16) {
+      const int bx = (lane & 3) * 4, by = (lane >> 2) * 4;
+      int rr[16];
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int x = 0; x < 4; ++x) rr[y * 4 + x] = s_res[(by + y) * 16 + bx + x];
+      satd = h264::satd4x4(rr);
+    }
+    satd = __builtin_amdgcn_readlane(sum16(satd), 0);
+    wave_sync();
+    const int cst = satd + lambda * (1 + j);  // merge_flag + truncated-unary merge_idx
+    if (cst < best) {
+      best = cst;
+      bx_ = kx[j];
+      by_ = ky[j];
+    }
+  }
+  if (lane == 0) {
+    a.mv_out[o * 2] = static_cast<int16_t>(bx_);
+    a.mv_out[o * 2 + 1] = static_cast<int16_t>(by_);
+    a.cost[o] = best;
+  }
+}
+
 // ---- P_8x8 / P_16x8 / P_8x16 partitions (x264 --partitions p8x8, its default).  After the
 // 16x16 search and the skip-aware refinement, each 8x8 quadrant of a P macroblock searches
 // its own vector: predictor candidates (the MB's vector, the left / top / top-right /
@@ -616,4 +706,22 @@ extern "C" void mivc_launch_p_part8(int B, int wmb, int hmb, const uint8_t* src_
   a.overhead = overhead;
   a.min_satd = min_satd;
   hipLaunchKernelGGL(p_part8x8, dim3(wmb * hmb, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
+}
+
+extern "C" void mivc_launch_hevc_merge_refine(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref,
+                                              const uint8_t* hp, const int16_t* mv_in, int16_t* mv_out, int* cost,
+                                              const int16_t* pm, const int* qp, const int8_t* aq, void* stream) {
+  PRefineArgs a;
+  a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
+  a.src_y = src_y;
+  a.ref = ref;
+  a.hp = hp;
+  a.mv_in = mv_in;
+  a.mv_out = mv_out;
+  a.cost = cost;
+  a.pm = pm;
+  a.pred = nullptr;
+  a.qp = qp;
+  a.aq = aq;
+  hipLaunchKernelGGL(hevc_merge_refine, dim3(wmb * hmb, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
 }

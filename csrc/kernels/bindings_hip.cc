@@ -84,6 +84,9 @@ void mivc_launch_hevc_aq(int B, int W, int H, int bd, const uint16_t* sy, const 
 void mivc_launch_hevc_pack_levels(int B, int W, int H, const int16_t* cy, const int16_t* cb, const int16_t* cr,
                                   unsigned long long* nzmap, int* cnt, unsigned* off, long long cap_blocks, int16_t* out,
                                   int* err, void* stream);
+void mivc_launch_hevc_merge_refine(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref, const uint8_t* hp,
+                                   const int16_t* mv_in, int16_t* mv_out, int* cost, const int16_t* pm, const int* qp,
+                                   const int8_t* aq, void* stream);
 void mivc_launch_hevc_qp_fixup(int B, int W, int H, void* ctu, const void* cu, const int* qp, const int8_t* run,
                                int wpp, void* stream);
 void mivc_launch_hevc_sao(int B, int W, int H, int bd, const uint16_t* dy, const uint16_t* du, const uint16_t* dv,
@@ -320,6 +323,14 @@ PYBIND11_MODULE(_hip, m) {
     mivc_launch_hevc_pack_levels(B, W, H, P<int16_t>(cy), P<int16_t>(cb), P<int16_t>(cr),
                                  P<unsigned long long>(nzmap), P<int>(cnt), P<unsigned>(off), cap_blocks,
                                  P<int16_t>(out), P<int>(err), S(stream));
+  });
+  m.def("hevc_merge_refine", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref, uintptr_t hp, uintptr_t mv_in,
+                                uintptr_t mv_out, uintptr_t cost, uintptr_t pm, uintptr_t qp, uintptr_t aq,
+                                uintptr_t stream) {
+    if (mv_in == mv_out) throw std::invalid_argument("hevc_merge_refine: mv_in and mv_out must differ (Jacobi pass)");
+    if (!hp) throw std::invalid_argument("hevc_merge_refine: needs the half-sample planes");
+    mivc_launch_hevc_merge_refine(B, wmb, hmb, P<uint8_t>(src), P<uint8_t>(ref), P<uint8_t>(hp), P<int16_t>(mv_in),
+                                  P<int16_t>(mv_out), P<int>(cost), P<int16_t>(pm), P<int>(qp), P<int8_t>(aq), S(stream));
   });
   m.def("hevc_qp_fixup", [](int B, int W, int H, uintptr_t ctu, uintptr_t cu, uintptr_t qp, uintptr_t run, int wpp,
                             uintptr_t stream) {
