@@ -245,6 +245,7 @@ hevc::HevcConfig hevc_cfg_from(const py::dict& d) {
   c.threads = dget<int>(d, "threads", 1);
   c.cu_qp_delta = dget<int>(d, "cu_qp_delta", 0);
   c.tu_inter_depth = dget<int>(d, "tu_inter_depth", 0);
+  c.sdh = dget<int>(d, "sdh", 0);
   if (c.tu_inter_depth < 0 || c.tu_inter_depth > 1) throw std::runtime_error("HEVC: tu_inter_depth in 0..1");
   if (c.threads < 1 || c.threads > 256) throw std::runtime_error("HEVC: threads in 1..256");
   if (c.width <= 0 || c.height <= 0 || (c.width & 1) || (c.height & 1)) throw std::runtime_error("HEVC: bad size");

@@ -29,6 +29,7 @@ struct HevcConfig {
   int max_merge = 5;
   int wpp = 0;                 // entropy_coding_sync_enabled_flag: one CABAC substream per CTB row
   int cu_qp_delta = 0;         // cu_qp_delta_enabled_flag: per-CTB QpY from CtuInfo::qp (AQ)
+  int sdh = 0;                 // sign_data_hiding_enabled_flag (the levels must carry the parity)
   int tu_inter_depth = 0;      // max_transform_hierarchy_depth_inter: 1 = inter CUs may split their TU once
   int threads = 1;             // host threads coding the WPP substreams of one picture
   int coded_width() const { return (width + kCtb - 1) / kCtb * kCtb; }

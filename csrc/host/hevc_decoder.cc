@@ -186,7 +186,7 @@ struct HevcDecoder::Impl {
     p.bypass = br.get(1);
     p.tiles = br.get(1);
     p.wpp = br.get(1);
-    if (p.sign_hiding || p.tskip || p.bypass || p.tiles || p.weighted || p.constrained_intra ||
+    if (p.tskip || p.bypass || p.tiles || p.weighted || p.constrained_intra ||
         p.slice_chroma_offsets || p.dep_slices || p.output_flag || p.extra_bits)
       throw std::runtime_error("HEVC: PPS tool outside the supported subset");
     p.lf_across_slices = br.get(1);
@@ -998,10 +998,20 @@ struct HevcDecoder::Impl {
         greater1_ctx_prev = greater1_ctx;
       }
       if (last_g1_pos >= 0) g2[last_g1_pos] = cd->decode(ctx[CTX_GT2 + (cidx ? 4 : 0) + ctx_set]);
+      // 7.3.8.11 / 7.4.9.11 sign data hiding: the sign of the first significant coefficient
+      // in scan order is not coded when the group's significant span exceeds 3 positions;
+      // an odd sum of absolute levels makes it negative
+      int first_sig = -1, last_sig = -1;
+      for (int p = 0; p < 16; ++p)
+        if (sig[p]) {
+          if (first_sig < 0) first_sig = p;
+          last_sig = p;
+        }
+      const bool hidden = pps.sign_hiding && first_sig >= 0 && last_sig - first_sig > 3;
       int sign[16] = {};
       for (int p = 15; p >= 0; --p)
-        if (sig[p]) sign[p] = cd->bypass();
-      int num_sig = 0, rice = 0;
+        if (sig[p] && !(hidden && p == first_sig)) sign[p] = cd->bypass();
+      int num_sig = 0, rice = 0, sum_abs = 0;
       for (int p = 15; p >= 0; --p) {
         if (!sig[p]) continue;
         const int base = 1 + g1[p] + g2[p];
@@ -1013,6 +1023,8 @@ struct HevcDecoder::Impl {
           if (a > 3 * (1 << rice)) rice = std::min(rice + 1, 4);
         }
         ++num_sig;
+        sum_abs += a;
+        if (hidden && p == first_sig) sign[p] = sum_abs & 1;  // p == first_sig is the last one coded
         lev[(ys * 4 + py[p]) * n + xs * 4 + px[p]] = sign[p] ? -a : a;
       }
     }

@@ -147,7 +147,7 @@ std::vector<uint8_t> hevc_parameter_sets(const HevcConfig& c) {
     bw.put_bit(0);  // dependent_slice_segments_enabled_flag
     bw.put_bit(0);  // output_flag_present_flag
     bw.put(0, 3);   // num_extra_slice_header_bits
-    bw.put_bit(0);  // sign_data_hiding_enabled_flag
+    bw.put_bit(c.sdh ? 1 : 0);  // sign_data_hiding_enabled_flag
     bw.put_bit(0);  // cabac_init_present_flag
     bw.put_ue(0);   // num_ref_idx_l0_default_active_minus1
     bw.put_ue(0);   // num_ref_idx_l1_default_active_minus1
@@ -537,7 +537,22 @@ struct Writer {
       }
       uint32_t signs = 0;
       for (int k = 0; k < nsig; ++k) signs = (signs << 1) | (vals[k] < 0);
-      e.bypass_bits(signs, nsig);
+      // sign data hiding: vals[nsig - 1] is the first significant coefficient in scan order
+      int first_p = -1, last_p_g = -1;
+      for (int p = 0; p < 16; ++p)
+        if (lvl[p] != 0) {
+          if (first_p < 0) first_p = p;
+          last_p_g = p;
+        }
+      if (c.sdh && first_p >= 0 && last_p_g - first_p > 3) {
+        int sum = 0;
+        for (int k = 0; k < nsig; ++k) sum += std::abs(vals[k]);
+        if ((sum & 1) != (vals[nsig - 1] < 0 ? 1 : 0))
+          throw std::runtime_error("HEVC: sign data hiding parity does not match the hidden sign");
+        e.bypass_bits(signs >> 1, nsig - 1);
+      } else {
+        e.bypass_bits(signs, nsig);
+      }
       int rice = 0;
       for (int k = 0; k < nsig; ++k) {
         const int a = std::abs(vals[k]);

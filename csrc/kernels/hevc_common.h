@@ -105,7 +105,14 @@ struct TqParams {
   int log2n, bd, qp;  // qp: Qp' (QpY + QpBdOffset, or the chroma equivalent)
   bool intra;
   bool dst = false;   // 4x4 intra luma: DST-VII instead of the DCT
+  int sdh_scan = -1;  // >= 0: sign data hiding with this scanIdx (0 diagonal, 1 horizontal, 2 vertical)
 };
+
+// scanIdx of a TU (7.4.9.11): intra luma 4x4 / 8x8 and intra chroma 4x4 follow the mode
+__device__ __forceinline__ int tu_scan_idx(bool intra, bool luma, int log2n, int mode) {
+  if (!intra || !(log2n == 2 || (log2n == 3 && luma))) return 0;
+  return (mode >= 6 && mode <= 14) ? 2 : ((mode >= 22 && mode <= 30) ? 1 : 0);
+}
 
 __device__ __forceinline__ bool transform_quant_block(const DctLds& D, int* R, int* S, int16_t* lev, int lstride,
                                                       const TqParams& p) {
@@ -133,6 +140,16 @@ __device__ __forceinline__ bool transform_quant_block(const DctLds& D, int* R, i
                 const int a = c < 0 ? -c : c;
                 int l = static_cast<int>((static_cast<int64_t>(a) * qscale + qoff) >> qbits);
                 l = l > 32767 ? 32767 : l;
+                if (p.sdh_scan >= 0) {
+                  // level, quantisation remainder (HM deltaU) and coefficient sign, packed for
+                  // the parity pass below; dequantisation follows it
+                  const int dl = static_cast<int>(((static_cast<int64_t>(a) * qscale) - (static_cast<int64_t>(l) << qbits)) >>
+                                                  (qbits - 8));
+                  const int sl = c < 0 ? -l : l;
+                  R[v * 32 + u] = static_cast<int>((static_cast<uint32_t>(sl) & 0xFFFFu) |
+                                                   ((static_cast<uint32_t>(dl) & 0x7FFFu) << 16) | (c < 0 ? 0x80000000u : 0u));
+                  return;
+                }
                 l = c < 0 ? -l : l;
                 lev[v * lstride + u] = static_cast<int16_t>(l);
                 any |= l != 0;
@@ -142,6 +159,84 @@ __device__ __forceinline__ bool transform_quant_block(const DctLds& D, int* R, i
                 R[v * 32 + u] = static_cast<int>(d < -32768 ? -32768 : (d > 32767 ? 32767 : d));
               });
   wave_sync();
+  if (p.sdh_scan >= 0) {
+    // sign data hiding (7.4.9.11; HM's parity fix): in every 4x4 group whose significant
+    // span exceeds 3 scan positions the sum of absolute levels must be odd exactly when the
+    // first significant coefficient is negative; otherwise the cheapest +-1 change by the
+    // quantisation remainder fixes it.  One lane per group.
+    const int nsb = n >> 2, lsb = lg - 2, ngr = nsb * nsb;
+    const int lane = lane_id();
+    auto lvl_at = [&](int x, int y) { return static_cast<int>(static_cast<int16_t>(R[y * 32 + x] & 0xFFFF)); };
+    int gi = -1, gnz = 0;
+    if (lane < ngr) {
+      const int gx = lane % nsb, gy = lane / nsb;
+      for (int i = 0; i < ngr; ++i)
+        if (hevc::scan_pos(p.sdh_scan, lsb, i) == (gx | (gy << 8))) gi = i;
+      for (int y = 0; y < 4; ++y)
+        for (int x = 0; x < 4; ++x) gnz |= lvl_at(gx * 4 + x, gy * 4 + y);
+    }
+    const int lastgi = -min64(-(gnz ? gi : -1));
+    if (lane < ngr && gnz) {
+      const int gx = lane % nsb, gy = lane / nsb;
+      int px[16], py[16], lv[16], first = -1, last = -1, sum = 0;
+      for (int q = 0; q < 16; ++q) {
+        const int sp = hevc::scan_pos(p.sdh_scan, 2, q);
+        px[q] = gx * 4 + (sp & 255);
+        py[q] = gy * 4 + (sp >> 8);
+        lv[q] = lvl_at(px[q], py[q]);
+        if (lv[q]) {
+          if (first < 0) first = q;
+          last = q;
+          sum += lv[q] < 0 ? -lv[q] : lv[q];
+        }
+      }
+      const int signbit = lv[first] < 0 ? 1 : 0;
+      if (last - first > 3 && (sum & 1) != signbit) {
+        int best = 0x7FFFFFFF, bq = first, bch = 1;
+        for (int q = (gi == lastgi ? last : 15); q >= 0; --q) {
+          const int w = R[py[q] * 32 + px[q]];
+          const int dl = (w << 1) >> 17;  // 15-bit signed remainder
+          int cost, ch = 1;
+          if (lv[q] != 0) {
+            if (dl > 0) {
+              cost = -dl;
+            } else if (q == first && (lv[q] == 1 || lv[q] == -1)) {
+              cost = 0x7FFFFFFF;
+            } else {
+              cost = dl;
+              ch = -1;
+            }
+          } else if (q < first && ((static_cast<uint32_t>(w) >> 31) != static_cast<uint32_t>(signbit))) {
+            cost = 0x7FFFFFFF;
+          } else {
+            cost = -dl;
+          }
+          if (cost < best) {
+            best = cost;
+            bq = q;
+            bch = ch;
+          }
+        }
+        const int w = R[py[bq] * 32 + px[bq]];
+        const bool neg = (static_cast<uint32_t>(w) >> 31) != 0;
+        int l = lv[bq];
+        if (l == 32767 || l == -32767) bch = -1;
+        l += neg ? -bch : bch;
+        R[py[bq] * 32 + px[bq]] = static_cast<int>((static_cast<uint32_t>(w) & 0xFFFF0000u) | (static_cast<uint32_t>(l) & 0xFFFFu));
+      }
+    }
+    wave_sync();
+    for (int i = lane; i < n * n; i += 64) {  // levels out + dequantisation (8.6.3, flat scaling)
+      const int y = i >> lg, x = i & (n - 1);
+      const int l = lvl_at(x, y);
+      lev[y * lstride + x] = static_cast<int16_t>(l);
+      any |= l != 0;
+      int64_t d = ((static_cast<int64_t>(l) * dscale) << qs) + drnd;
+      d >>= dsh;
+      R[y * 32 + x] = static_cast<int>(d < -32768 ? -32768 : (d > 32767 ? 32767 : d));
+    }
+    wave_sync();
+  }
   const bool nz = __ballot(any) != 0;
   if (!nz) return false;  // residual is zero: R is all zero too
   // inverse, stage 1 (columns): S[y][x] = clip16((sum_k C[k][y] * R[k][x] + 64) >> 7)

@@ -37,6 +37,7 @@ struct HevcInterArgs {
   const int* me_cost;    // [B, nmb16] (8-bit proxy units)
   int bd;
   int tu_split;          // inter CUs may code their residual as four quarter TUs (RD choice)
+  int sdh;               // sign data hiding in the quantiser
 };
 
 __device__ __forceinline__ int lambda_satd_i(int qp, int bd) {
@@ -281,13 +282,13 @@ __global__ __launch_bounds__(64) void hevc_inter_cu(HevcInterArgs a) {
     const int l2 = c ? lg - 1 : lg;
     const int qc = c ? qpc : qpl;
     if (TSPLIT && c == 0) {
-      const bool nz = hv::transform_quant_block(D, S.R, S.S, lev, pw, hv::TqParams{l2, bd, qc, false});
+      const bool nz = hv::transform_quant_block(D, S.R, S.S, lev, pw, hv::TqParams{l2, bd, qc, false, false, a.sdh ? 0 : -1});
       for (int k = 0; k < 4; ++k) cbfq[k] = nz;
       {
         bool nzq[4];
         for (int k = 0; k < 4; ++k) {
           const int o = (k >> 1) * h * 32 + (k & 1) * h;
-          nzq[k] = hv::transform_quant_block(D, S.R2 + o, S.S, S.lev2 + o, 32, hv::TqParams{l2 - 1, bd, qc, false});
+          nzq[k] = hv::transform_quant_block(D, S.R2 + o, S.S, S.lev2 + o, 32, hv::TqParams{l2 - 1, bd, qc, false, false, a.sdh ? 0 : -1});
         }
         const bool any = nzq[0] || nzq[1] || nzq[2] || nzq[3];
         if (any) {
@@ -314,11 +315,11 @@ __global__ __launch_bounds__(64) void hevc_inter_cu(HevcInterArgs a) {
       for (int k = 0; k < 4; ++k) {
         const int o = (k >> 1) * hc * 32 + (k & 1) * hc;
         const bool nz = hv::transform_quant_block(D, S.R + o, S.S, lev + (k >> 1) * hc * pw + (k & 1) * hc, pw,
-                                                  hv::TqParams{l2 - 1, bd, qc, false});
+                                                  hv::TqParams{l2 - 1, bd, qc, false, false, a.sdh ? 0 : -1});
         cbfq[k] |= nz << c;
       }
     } else {
-      const bool nz = hv::transform_quant_block(D, S.R, S.S, lev, pw, hv::TqParams{l2, bd, qc, false});
+      const bool nz = hv::transform_quant_block(D, S.R, S.S, lev, pw, hv::TqParams{l2, bd, qc, false, false, a.sdh ? 0 : -1});
       for (int k = 0; k < 4; ++k) cbfq[k] |= nz << c;
     }
     // (a block without levels has an all-zero dequantised residual in R)
@@ -347,7 +348,8 @@ extern "C" void mivc_launch_hevc_inter(int B, int W, int H, const uint16_t* sy, 
                                        const uint16_t* fy, const uint16_t* fu, const uint16_t* fv, uint16_t* ry,
                                        uint16_t* ru, uint16_t* rv, void* ctu, void* cu, int16_t* cy, int16_t* cu_,
                                        int16_t* cv, const int* qp, const int8_t* run, const int* cand,
-                                       const int16_t* mv, const int* me_cost, int bd, int tu_split, void* stream) {
+                                       const int16_t* mv, const int* me_cost, int bd, int tu_split, int sdh,
+                                       void* stream) {
   HevcInterArgs a;
   a.g = HevcGeom{B, W, H, W / 32, H / 32};
   a.src_y = sy;
@@ -371,6 +373,7 @@ extern "C" void mivc_launch_hevc_inter(int B, int W, int H, const uint16_t* sy, 
   a.me_cost = me_cost;
   a.bd = bd;
   a.tu_split = tu_split;
+  a.sdh = sdh;
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(hevc_p_decide, dim3(a.g.nctb(), B), dim3(64), 0, s, a);
   if (tu_split) hipLaunchKernelGGL(hevc_inter_cu<true>, dim3(a.g.nctb() * 4, B), dim3(64), 0, s, a);

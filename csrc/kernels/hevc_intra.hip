@@ -33,6 +33,7 @@ struct HevcIntraArgs {
   int* cand;                              // [B, nctb, 2, 21] best cost / mode per CU of the analysis (may be null)
   int bd;
   int* err;
+  int sdh;                                // sign data hiding in the quantiser
 };
 
 // luma neighbour (xr, yr) of a CTB-relative block position: z-scan availability (6.4.1)
@@ -524,7 +525,7 @@ __device__ __forceinline__ bool recon_block(const HevcIntraArgs& a, ReconShared&
   // 3. transform / quantisation / reconstruction
   int16_t* lev = (LUMA ? a.coef_y : (comp == 1 ? a.coef_u : a.coef_v)) + slot * (LUMA ? g.ysize() : g.csize()) +
                  static_cast<size_t>(Y0) * pw + X0;
-  hv::TqParams tp{log2n, bd, qpp, true, dst};
+  hv::TqParams tp{log2n, bd, qpp, true, dst, a.sdh ? hv::tu_scan_idx(true, LUMA, log2n, mode) : -1};
   const bool nz = hv::transform_quant_block(D, S.R, S.S, lev, pw, tp);
   uint16_t* rec = (LUMA ? a.rec_y : (comp == 1 ? a.rec_u : a.rec_v)) + slot * (LUMA ? g.ysize() : g.csize());
   for (int i = lane; i < n * n; i += 64) {
@@ -673,7 +674,7 @@ using namespace mivc::gpu;
 static HevcIntraArgs make_intra_args(int B, int W, int H, const uint16_t* sy, const uint16_t* su, const uint16_t* sv,
                                      uint16_t* ry, uint16_t* ru, uint16_t* rv, void* ctu, void* cu, int16_t* cy,
                                      int16_t* cu_, int16_t* cv, const int* qp, const int8_t* run, int* cand, int bd,
-                                     int* err) {
+                                     int* err, int sdh) {
   HevcIntraArgs a;
   a.g = HevcGeom{B, W, H, W / 32, H / 32};
   a.src_y = sy;
@@ -692,14 +693,15 @@ static HevcIntraArgs make_intra_args(int B, int W, int H, const uint16_t* sy, co
   a.cand = cand;
   a.bd = bd;
   a.err = err;
+  a.sdh = sdh;
   return a;
 }
 
 extern "C" void mivc_launch_hevc_intra(int B, int W, int H, const uint16_t* sy, const uint16_t* su, const uint16_t* sv,
                                        uint16_t* ry, uint16_t* ru, uint16_t* rv, void* ctu, void* cu, int16_t* cy,
                                        int16_t* cu_, int16_t* cv, const int* qp, const int8_t* run, int* cand, int bd,
-                                       int analyze, int recon, int* err, void* stream) {
-  HevcIntraArgs a = make_intra_args(B, W, H, sy, su, sv, ry, ru, rv, ctu, cu, cy, cu_, cv, qp, run, cand, bd, err);
+                                       int analyze, int recon, int* err, int sdh, void* stream) {
+  HevcIntraArgs a = make_intra_args(B, W, H, sy, su, sv, ry, ru, rv, ctu, cu, cy, cu_, cv, qp, run, cand, bd, err, sdh);
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (analyze) hipLaunchKernelGGL(hevc_intra_analyze, dim3(a.g.nctb(), B), dim3(256), 0, s, a);
   if (recon) hipLaunchKernelGGL(hevc_intra_recon, dim3(B), dim3(64 * kHevcIntraWaves), 0, s, a);

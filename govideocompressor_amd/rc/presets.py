@@ -23,7 +23,8 @@ placebo     = veryslow
 
 HEVC (x265): ultrafast..veryfast use radius 4 / half-pel / 3 merge candidates, fast and
 medium the defaults, slow and slower radius 12 / 5 candidates, veryslow/placebo radius 16;
-slow and slower presets add the inter residual quadtree (--tu-inter-depth 1).
+slow and slower presets add the inter residual quadtree (--tu-inter-depth 1), veryslow and
+placebo also sign data hiding (--signhide).
 """
 from __future__ import annotations
 
@@ -54,7 +55,7 @@ HEVC = {
     "medium": dict(),
     "slow": dict(me_range=12, tu_inter_depth=1),
     "slower": dict(me_range=12, la_range=8, tu_inter_depth=1),
-    "veryslow": dict(me_range=16, la_range=8, tu_inter_depth=1),
+    "veryslow": dict(me_range=16, la_range=8, tu_inter_depth=1, sdh=True),
 }
 HEVC["placebo"] = HEVC["veryslow"]
 

@@ -45,7 +45,7 @@ def _levels(rng, n: int, density: float) -> np.ndarray:
 
 def random_records(rng, width: int, height: int, pslice: bool, bit_depth: int = 8, density: float = 0.08,
                    intra_in_p: float = 0.2, mv_range: int = 64, sao: bool = True, ctb_qp: tuple | None = None,
-                   nxn: float = 0.0, tu_split: float = 0.0):
+                   nxn: float = 0.0, tu_split: float = 0.0, force_split: int | None = None):
     """``ctb_qp = (qp, spread)``: per-CTB QPs qp + U[-spread, spread] (cu_qp_delta streams);
     ``nxn``: probability of an 8x8 intra CU being split into four 4x4 PUs; ``tu_split``: of a
     16x16 / 32x32 inter CU coding its residual as four quarter TUs (needs tu_inter_depth 1)."""
@@ -61,6 +61,8 @@ def random_records(rng, width: int, height: int, pslice: bool, bit_depth: int = 
         rx, ry = i % wc, i // wc
         r = rng.random()
         split = 0 if r < 0.25 else (1 | (int(rng.integers(0, 16)) << 1))
+        if force_split is not None:
+            split = force_split
         ctu[i, 0] = split
         if ctb_qp is not None:
             ctu[i, 1] = np.int8(np.clip(ctb_qp[0] + rng.integers(-ctb_qp[1], ctb_qp[1] + 1), 0, 51)).view(np.uint8)
@@ -206,3 +208,33 @@ def unpack_levels(nz: np.ndarray, off: np.ndarray, lv: np.ndarray, W: int, H: in
                 pl[ry * 16 + by * 4:ry * 16 + by * 4 + 4, rx * 16 + bx * 4:rx * 16 + bx * 4 + 4] = blocks[k]
                 k += 1
     return cy, cb, cr
+
+
+def _diag4():
+    """(x, y) of the 16 positions of a 4x4 diagonal up-right scan (6.5.3)."""
+    out = []
+    for d in range(7):
+        for y in range(d, -1, -1):
+            x = d - y
+            if x < 4 and y < 4:
+                out.append((x, y))
+    return out
+
+
+def hide_signs_diag(blk: np.ndarray) -> np.ndarray:
+    """Make a TU's levels sign-data-hiding consistent for the diagonal scan (the test model
+    of an encoder's parity fix): in every 4x4 group whose significant span exceeds 3 scan
+    positions, negate the first significant coefficient when the parity of the group's
+    absolute sum disagrees with its sign."""
+    out = blk.copy()
+    sc = _diag4()
+    n = blk.shape[0]
+    for gy in range(0, n, 4):
+        for gx in range(0, n, 4):
+            v = [int(out[gy + y, gx + x]) for x, y in sc]
+            nzp = [p for p in range(16) if v[p] != 0]
+            if nzp and nzp[-1] - nzp[0] > 3:
+                if (sum(abs(t) for t in v) & 1) != (v[nzp[0]] < 0):
+                    x, y = sc[nzp[0]]
+                    out[gy + y, gx + x] = -out[gy + y, gx + x]
+    return out

@@ -180,3 +180,10 @@ def test_gpu_hevc_inter_tu_split(host, bd):
     _compare(host, res, rec)
     n = sum(int(((p["cu"][:, 3] & 16) != 0).sum()) for r in res for p in host.hevc_decode(r.bitstream))
     assert n > 0
+
+
+def test_gpu_hevc_sign_data_hiding(host):
+    """sign_data_hiding_enabled_flag: the GPU quantiser's parity fix (intra 4x4 / 8x8 mode
+    dependent scans, inter diagonal) keeps the decoder bit-exact in I and P pictures."""
+    res, rec = _encode(128, 96, 4, 2, crf=None, qp=22, sdh=True)
+    _compare(host, res, rec)

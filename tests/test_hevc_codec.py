@@ -10,8 +10,8 @@ the independent decoder.
 import numpy as np
 import pytest
 
-from govideocompressor_amd.utils.hevc_synth import (expected_ctb_qps, pack_levels, random_records, random_stream,
-                                                    unpack_levels)
+from govideocompressor_amd.utils.hevc_synth import (expected_ctb_qps, hide_signs_diag, pack_levels, random_records,
+                                                    random_stream, unpack_levels)
 
 
 def _norm_sao(c):
@@ -194,3 +194,28 @@ def test_hevc_inter_tu_split_roundtrip(host, wpp):
         n_split += int(dec_split.sum())
         assert np.array_equal(p["cu"][inter, 4:8], cu[inter, 4:8])
     assert n_split > 8
+
+
+def test_hevc_sign_data_hiding_roundtrip(host):
+    """sign_data_hiding_enabled_flag: 32x32 inter CUs (diagonal scans) whose levels carry the
+    hidden signs in their group parities decode back exactly; levels that violate the parity
+    are refused by the writer."""
+    rng = np.random.default_rng(11)
+    cfg = dict(width=64, height=64, sdh=1, wpp=1)
+    s = host.hevc_parameter_sets(cfg)
+    ctu0, cu0, cy0, cb0, cr0 = random_records(rng, 64, 64, pslice=False, sao=False)
+    z = np.zeros_like(cy0)
+    zc = np.zeros_like(cb0)
+    s += host.hevc_write_slice(cfg, dict(idr=1, poc=0, qp=30), ctu0, cu0, z, zc, zc)[0]
+    ctu, cu, cy, cb, cr = random_records(rng, 64, 64, pslice=True, intra_in_p=0.0, force_split=0, density=0.3,
+                                         sao=False)
+    fix = lambda pl, n: np.block([[hide_signs_diag(pl[y:y + n, x:x + n]) for x in range(0, pl.shape[1], n)]
+                                  for y in range(0, pl.shape[0], n)])
+    cyf, cbf, crf = fix(cy, 32), fix(cb, 16), fix(cr, 16)
+    assert not np.array_equal(cyf, cy)
+    with pytest.raises(Exception):
+        host.hevc_write_slice(cfg, dict(idr=0, poc=1, qp=30, slice_type=1), ctu, cu, cy, cb, cr)
+    s += host.hevc_write_slice(cfg, dict(idr=0, poc=1, qp=30, slice_type=1), ctu, cu, cyf, cbf, crf)[0]
+    pics = host.hevc_decode(s, False)
+    assert np.array_equal(pics[1]["coef_y"], cyf)
+    assert np.array_equal(pics[1]["coef_cb"], cbf) and np.array_equal(pics[1]["coef_cr"], crf)
