@@ -67,7 +67,7 @@ class HevcParams:
 
     # merge-aware vector choice after the search (Jacobi passes over the spatial merge
     # neighbours' vectors, bframe.hip hevc_merge_refine); 0 disables
-    merge_refine: int = 2
+    merge_refine: int = 4  # 1080p sweep (tools/hevc_knob_sweep.py): 0 -> 2 -> 4 passes = 3584 -> 3092 -> 3042 kb/s
     # x265 --signhide: the quantiser hides one sign per 4x4 group in the parity of the group's
     # levels (sign_data_hiding_enabled_flag).  Measured on the synthetic 1080p bench content:
     # +0.25 % bits at +0.01 dB (RD-neutral) for -28 % throughput, so off by default and on
