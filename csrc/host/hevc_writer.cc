@@ -674,7 +674,8 @@ struct Writer {
       if (!(a1 && ma1 == m) && !(b1 && mb1 == m)) out[k++] = m;
     }
     while (k < c.max_merge) out[k++] = Mv{0, 0};
-    return k;
+    // the list holds MaxNumMergeCand entries: spatial candidates beyond it are not in it
+    return k < c.max_merge ? k : c.max_merge;
   }
 
   // 8.5.3.2.6-8.5.3.2.7 AMVP candidates (one reference picture: no scaling)

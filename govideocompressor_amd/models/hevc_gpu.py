@@ -47,7 +47,7 @@ class HevcParams:
     deblock: bool = True
     intra_only: bool = False
     keyint: int = 0                 # IDR period inside a segment (0: the first picture only)
-    max_merge: int = 5
+    max_merge: int = 3              # x265 --max-merge 3 (1080p sweep: 3 / 4 / 5 = 3023 / 3039 / 3042 kb/s)
     me_range: int = 8
     subpel: int = 2
     # CRF per-frame QPs from the GPU lookahead (rc/lookahead.py); False = flat CRF QP

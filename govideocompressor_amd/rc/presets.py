@@ -21,8 +21,9 @@ veryslow    slower + three skip-refine passes (--subme 10 --me umh --merange 24)
 placebo     = veryslow
 ==========  ========================================================================
 
-HEVC (x265): ultrafast..veryfast use radius 4 / half-pel / 3 merge candidates, fast and
-medium the defaults, slow and slower radius 12 / 5 candidates, veryslow/placebo radius 16;
+HEVC (x265): ultrafast..veryfast use radius 4 / half-pel, fast and medium the defaults (3
+merge candidates, as x265), slow and slower radius 12 (slower 4 candidates), veryslow/placebo
+radius 16 and 5 candidates;
 slow and slower presets add the inter residual quadtree (--tu-inter-depth 1), veryslow and
 placebo also sign data hiding (--signhide).
 """
@@ -51,11 +52,11 @@ HEVC = {
     "superfast": dict(me_range=4, subpel=1, max_merge=3, la_range=4),
     "veryfast": dict(me_range=4, subpel=2, max_merge=3),
     "faster": dict(me_range=8, max_merge=3),
-    "fast": dict(me_range=8, max_merge=4),
+    "fast": dict(me_range=8),
     "medium": dict(),
     "slow": dict(me_range=12, tu_inter_depth=1),
-    "slower": dict(me_range=12, la_range=8, tu_inter_depth=1),
-    "veryslow": dict(me_range=16, la_range=8, tu_inter_depth=1, sdh=True),
+    "slower": dict(me_range=12, la_range=8, tu_inter_depth=1, max_merge=4),
+    "veryslow": dict(me_range=16, la_range=8, tu_inter_depth=1, sdh=True, max_merge=5),
 }
 HEVC["placebo"] = HEVC["veryslow"]
 

@@ -219,3 +219,15 @@ def test_hevc_sign_data_hiding_roundtrip(host):
     pics = host.hevc_decode(s, False)
     assert np.array_equal(pics[1]["coef_y"], cyf)
     assert np.array_equal(pics[1]["coef_cb"], cbf) and np.array_equal(pics[1]["coef_cr"], crf)
+
+
+@pytest.mark.parametrize("max_merge", [1, 2, 3, 4])
+def test_hevc_short_merge_lists(host, max_merge):
+    """five_minus_max_num_merge_cand > 0: the writer's merge list stops at MaxNumMergeCand
+    (a vector matching only a later spatial candidate is coded with AMVP), so every inter
+    CU decodes to its record's vector."""
+    s, recs = random_stream(host, 96, 64, 3, seed=50 + max_merge, intra_in_p=0.1, mv_range=8,
+                            host_cfg=dict(max_merge=max_merge))
+    for p, (ctu, cu, cy, cb, cr) in zip(host.hevc_decode(s, False), recs):
+        inter = cu[:, 0] == 1
+        assert np.array_equal(p["cu"][inter, 4:8], cu[inter, 4:8])
