@@ -34,6 +34,7 @@ struct HevcIntraArgs {
   int bd;
   int* err;
   int sdh;                                // sign data hiding in the quantiser
+  int nxn_in_p;                           // evaluate PART_NxN in P pictures too
 };
 
 // luma neighbour (xr, yr) of a CTB-relative block position: z-scan availability (6.4.1)
@@ -173,6 +174,9 @@ __global__ __launch_bounds__(256, 4) void hevc_intra_analyze(HevcIntraArgs a) {
   const HevcGeom& g = a.g;
   const int ci = blockIdx.x, slot = blockIdx.y;
   if (a.run[slot] == 0) return;
+  // PART_NxN candidates in I pictures (and P pictures when asked): intra CUs are rare in P
+  // pictures and 8x8 ones rarer, the 4x4 search is a third of this kernel
+  const bool nxn_on = a.run[slot] == 1 || a.nxn_in_p;
   const int rx = ci % g.wctb, ry = ci / g.wctb;
   const int X0 = rx * 32, Y0 = ry * 32;
   const int tid = threadIdx.x;
@@ -227,7 +231,7 @@ __global__ __launch_bounds__(256, 4) void hevc_intra_analyze(HevcIntraArgs a) {
     for (int k = 0; k < n; ++k) s += p[c + 1 + k] + p[c - 1 - k];
     const int lg = n == 32 ? 5 : (n == 16 ? 4 : 3);
     S.dc[tid] = s >> (lg + 1);
-  } else if (tid >= 64 && tid < 64 + kPuCount) {  // 4x4 PU reference arrays (z4 = PU index)
+  } else if (nxn_on && tid >= 64 && tid < 64 + kPuCount) {  // 4x4 PU reference arrays (z4 = PU index)
     const int pu = tid - 64;
     int px, py;
     pu_of(pu, &px, &py);
@@ -354,7 +358,7 @@ __global__ __launch_bounds__(256, 4) void hevc_intra_analyze(HevcIntraArgs a) {
   __syncthreads();
   // 4x4 PUs (PART_NxN candidates): seeds planar, DC and the parent 8x8 CU's best mode
   // +-2 (or the pure directions when it is planar / DC), then +-1 around the best angular
-  for (int it = tid; it < 5 * kPuCount; it += 256) {
+  for (int it = tid; nxn_on && it < 5 * kPuCount; it += 256) {
     const int pu = it % kPuCount, si = it / kPuCount;
     const int m8 = S.best_mode[5 + (pu >> 2)];
     int m;
@@ -364,7 +368,7 @@ __global__ __launch_bounds__(256, 4) void hevc_intra_analyze(HevcIntraArgs a) {
     if (!S.done4[pu][m]) eval4(pu, m);  // (clamped duplicates of one PU run in one iteration: same value)
   }
   __syncthreads();
-  if (tid < kPuCount) {
+  if (nxn_on && tid < kPuCount) {
     int bm = 2, bc = 0x7FFFFFFF;
     for (int m = 2; m < 35; ++m) {
       const int cst = S.cost4[tid][m];
@@ -376,13 +380,13 @@ __global__ __launch_bounds__(256, 4) void hevc_intra_analyze(HevcIntraArgs a) {
     S.best4_mode[tid] = bm;
   }
   __syncthreads();
-  if (tid < 2 * kPuCount) {
+  if (nxn_on && tid < 2 * kPuCount) {
     const int pu = tid & 63;
     const int m = S.best4_mode[pu] + (tid < 64 ? -1 : 1);
     if (m >= 2 && m <= 34 && !S.done4[pu][m]) eval4(pu, m);
   }
   __syncthreads();
-  if (tid < kPuCount) {
+  if (nxn_on && tid < kPuCount) {
     const int pu = tid;
     int bm = 0, bc = 0x7FFFFFFF;
     for (int m = 0; m < 35; ++m) {
@@ -397,7 +401,8 @@ __global__ __launch_bounds__(256, 4) void hevc_intra_analyze(HevcIntraArgs a) {
     S.best4_cost[pu] = bc;
   }
   __syncthreads();
-  if (tid < 16) {  // PART_NxN vs PART_2Nx2N per 8x8 CU (NxN: three more PU mode codes, four luma cbfs)
+  if (tid < 16 && !nxn_on) S.nxn[tid] = 0;
+  if (nxn_on && tid < 16) {  // PART_NxN vs PART_2Nx2N per 8x8 CU (NxN: three more PU mode codes, four luma cbfs)
     const int c8 = tid;
     const int cn = S.best4_cost[4 * c8] + S.best4_cost[4 * c8 + 1] + S.best4_cost[4 * c8 + 2] + S.best4_cost[4 * c8 + 3] +
                    lam * 6;
@@ -694,6 +699,7 @@ static HevcIntraArgs make_intra_args(int B, int W, int H, const uint16_t* sy, co
   a.bd = bd;
   a.err = err;
   a.sdh = sdh;
+  a.nxn_in_p = 0;
   return a;
 }
 
