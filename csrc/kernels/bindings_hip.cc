@@ -75,7 +75,7 @@ void mivc_launch_hevc_inter(int B, int W, int H, const uint16_t* sy, const uint1
                             const uint16_t* fy, const uint16_t* fu, const uint16_t* fv, uint16_t* ry, uint16_t* ru,
                             uint16_t* rv, void* ctu, void* cu, int16_t* cy, int16_t* cu_, int16_t* cv, const int* qp,
                             const int8_t* run, const int* cand, const int16_t* mv, const int* me_cost, int bd,
-                            int tu_split, int sdh, void* stream);
+                            int tu_split, int sdh, int intra_bias, void* stream);
 void mivc_launch_hevc_deblock(int B, int W, int H, int bd, uint16_t* y, uint16_t* u, uint16_t* v, const void* cu,
                               const void* ctu, const int8_t* run, void* stream);
 void mivc_launch_hevc_aq(int B, int W, int H, int bd, const uint16_t* sy, const uint16_t* su, const uint16_t* sv,
@@ -298,11 +298,11 @@ PYBIND11_MODULE(_hip, m) {
   m.def("hevc_inter", [](int B, int W, int H, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t fy, uintptr_t fu,
                          uintptr_t fv, uintptr_t ry, uintptr_t ru, uintptr_t rv, uintptr_t ctu, uintptr_t cu, uintptr_t cy,
                          uintptr_t cu_, uintptr_t cv, uintptr_t qp, uintptr_t run, uintptr_t cand, uintptr_t mv,
-                         uintptr_t me_cost, int bd, uintptr_t stream, int tu_split, int sdh) {
+                         uintptr_t me_cost, int bd, uintptr_t stream, int tu_split, int sdh, int intra_bias) {
     mivc_launch_hevc_inter(B, W, H, P<uint16_t>(sy), P<uint16_t>(su), P<uint16_t>(sv), P<uint16_t>(fy), P<uint16_t>(fu),
                            P<uint16_t>(fv), P<uint16_t>(ry), P<uint16_t>(ru), P<uint16_t>(rv), P<void>(ctu), P<void>(cu),
                            P<int16_t>(cy), P<int16_t>(cu_), P<int16_t>(cv), P<int>(qp), P<int8_t>(run), P<int>(cand),
-                           P<int16_t>(mv), P<int>(me_cost), bd, tu_split, sdh, S(stream));
+                           P<int16_t>(mv), P<int>(me_cost), bd, tu_split, sdh, intra_bias, S(stream));
   });
   m.def("hevc_deblock", [](int B, int W, int H, int bd, uintptr_t y, uintptr_t u, uintptr_t v, uintptr_t cu,
                            uintptr_t ctu, uintptr_t run, uintptr_t stream) {

@@ -38,6 +38,7 @@ struct HevcInterArgs {
   int bd;
   int tu_split;          // inter CUs may code their residual as four quarter TUs (RD choice)
   int sdh;               // sign data hiding in the quantiser
+  int intra_bias;        // lambda multiples added to the open-loop intra costs of P pictures
 };
 
 __device__ __forceinline__ int lambda_satd_i(int qp, int bd) {
@@ -67,7 +68,7 @@ __global__ __launch_bounds__(64) void hevc_p_decide(HevcInterArgs a) {
     for (int r = 0; r < 4; ++r) s8 += cd[5 + q * 4 + r];
     const int c16 = cd[1 + q];
     s_split8[q] = s8 < c16;
-    s_intra[q] = s8 < c16 ? s8 : c16;
+    s_intra[q] = (s8 < c16 ? s8 : c16) + lam * a.intra_bias;
     s_inter[q] = inter;
     s_mvx[q] = a.mv[o * 2];
     s_mvy[q] = a.mv[o * 2 + 1];
@@ -349,7 +350,7 @@ extern "C" void mivc_launch_hevc_inter(int B, int W, int H, const uint16_t* sy, 
                                        uint16_t* ru, uint16_t* rv, void* ctu, void* cu, int16_t* cy, int16_t* cu_,
                                        int16_t* cv, const int* qp, const int8_t* run, const int* cand,
                                        const int16_t* mv, const int* me_cost, int bd, int tu_split, int sdh,
-                                       void* stream) {
+                                       int intra_bias, void* stream) {
   HevcInterArgs a;
   a.g = HevcGeom{B, W, H, W / 32, H / 32};
   a.src_y = sy;
@@ -374,6 +375,7 @@ extern "C" void mivc_launch_hevc_inter(int B, int W, int H, const uint16_t* sy, 
   a.bd = bd;
   a.tu_split = tu_split;
   a.sdh = sdh;
+  a.intra_bias = intra_bias;
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(hevc_p_decide, dim3(a.g.nctb(), B), dim3(64), 0, s, a);
   if (tu_split) hipLaunchKernelGGL(hevc_inter_cu<true>, dim3(a.g.nctb() * 4, B), dim3(64), 0, s, a);

@@ -73,6 +73,10 @@ class HevcParams:
     # +0.25 % bits at +0.01 dB (RD-neutral) for -28 % throughput, so off by default and on
     # only at -preset veryslow / placebo
     sdh: bool = False
+    # lambda multiples added to the open-loop intra cost of a 16x16 quadrant in P pictures
+    # before the inter / intra decision (the closed loop makes intra dearer than its
+    # open-loop SATD says)
+    intra_bias_p: int = 16  # 1080p sweep 0 / 16 / 32: 2984 / 2956 / 2944 kb/s at 37.132 / 37.118 / 37.111 dB
     # x265 --tu-inter-depth: 1 = inter CUs choose between one TU and four quarter TUs by RD
     # (~0.7 % BD-rate on the synthetic bench content for ~16 % of the 1080p throughput; on from
     # -preset slow)
@@ -328,7 +332,7 @@ class GpuHevcEncoder:
                                     p(ref[1]), p(ref[2]), p(cur[0]), p(cur[1]), p(cur[2]), p(self.ctu), p(self.cu),
                                     p(self.coef[0]), p(self.coef[1]), p(self.coef[2]), p(self.ctb_qp), p(self.run),
                                     p(self.cand), p(self.mv), p(self.me_cost), bd, s, int(self.p.tu_inter_depth),
-                                    int(self.p.sdh))
+                                    int(self.p.sdh), int(self.p.intra_bias_p))
                 self.hip.hevc_intra(*intra_args, 0, 1, p(self.err), s, int(self.p.sdh))   # intra CUs, wavefront
                 self.prev_mv.copy_(self.mv)
             self.hip.hevc_qp_fixup(B, self.W, self.H, p(self.ctu), p(self.cu), p(self.qp), p(self.run), int(self.p.wpp), s)
