@@ -58,6 +58,7 @@ EncoderConfig cfg_from(const py::dict& d) {
   c.bframes = dget<int>(d, "bframes", 0);
   c.refs = dget<int>(d, "refs", 1);
   c.weighted_bipred = dget<int>(d, "weighted_bipred", 0);
+  c.level_idc = dget<int>(d, "level_idc", 0);
   if (c.refs < 1 || c.refs > 16) throw std::runtime_error("refs must be in 1..16");
   return c;
 }
@@ -246,6 +247,7 @@ hevc::HevcConfig hevc_cfg_from(const py::dict& d) {
   c.cu_qp_delta = dget<int>(d, "cu_qp_delta", 0);
   c.tu_inter_depth = dget<int>(d, "tu_inter_depth", 0);
   c.sdh = dget<int>(d, "sdh", 0);
+  c.level_idc = dget<int>(d, "level_idc", 0);
   if (c.tu_inter_depth < 0 || c.tu_inter_depth > 1) throw std::runtime_error("HEVC: tu_inter_depth in 0..1");
   if (c.threads < 1 || c.threads > 256) throw std::runtime_error("HEVC: threads in 1..256");
   if (c.width <= 0 || c.height <= 0 || (c.width & 1) || (c.height & 1)) throw std::runtime_error("HEVC: bad size");

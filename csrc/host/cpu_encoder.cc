@@ -32,6 +32,13 @@ SPS make_sps(const EncoderConfig& cfg) {
     s.constraint_flags = 0xC0;  // Constrained Baseline
   }
   s.level_idc = choose_level(s.width_mbs, s.height_mbs, cfg.fps);
+  if (cfg.level_idc > 0) {
+    // -level: the requested level must admit the picture size and rate (Table A-1)
+    if (cfg.level_idc < s.level_idc)
+      throw std::runtime_error("H.264: picture size / frame rate exceed the requested level " +
+                               std::to_string(cfg.level_idc / 10) + "." + std::to_string(cfg.level_idc % 10));
+    s.level_idc = cfg.level_idc;
+  }
   s.log2_max_frame_num = 16;
   if (cfg.bframes > 0) {
     s.poc_type = 0;

@@ -36,6 +36,7 @@ struct EncoderConfig {
   int bframes = 0;
   int refs = 1;
   int weighted_bipred = 0;  // 2 = implicit weights (x264 --weightb)
+  int level_idc = 0;        // > 0: written as level_idc (-level); must fit the size / rate
 };
 
 struct FrameStats {

@@ -32,6 +32,7 @@ struct HevcConfig {
   int sdh = 0;                 // sign_data_hiding_enabled_flag (the levels must carry the parity)
   int tu_inter_depth = 0;      // max_transform_hierarchy_depth_inter: 1 = inter CUs may split their TU once
   int threads = 1;             // host threads coding the WPP substreams of one picture
+  int level_idc = 0;           // > 0: general_level_idc (30 x level, -level); must fit the size / rate
   int coded_width() const { return (width + kCtb - 1) / kCtb * kCtb; }
   int coded_height() const { return (height + kCtb - 1) / kCtb * kCtb; }
   int wctb() const { return coded_width() / kCtb; }

@@ -37,7 +37,17 @@ void append_hevc_nal(std::vector<uint8_t>& out, int type, const std::vector<uint
   }
 }
 
+int auto_level_idc(const HevcConfig& c);
+
 int level_idc(const HevcConfig& c) {
+  const int need = auto_level_idc(c);
+  if (c.level_idc <= 0) return need;
+  if (c.level_idc < need)
+    throw std::runtime_error("HEVC: picture size / frame rate exceed the requested level_idc " + std::to_string(c.level_idc));
+  return c.level_idc;
+}
+
+int auto_level_idc(const HevcConfig& c) {
   const int64_t ps = static_cast<int64_t>(c.coded_width()) * c.coded_height();
   const double sps = ps * c.fps;
   // Table A.8 (MaxLumaPs, MaxLumaSr); level_idc = 30 * level

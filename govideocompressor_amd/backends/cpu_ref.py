@@ -44,7 +44,8 @@ class CpuBackend:
         qp = cfg.qp if cfg.qp is not None else int(round(cfg.crf if cfg.crf is not None else 23))
 
         def run(q: int):
-            hcfg = dict(width=ow, height=oh, fps=fps, qp=max(0, min(51, q)), keyint=1 << 30)
+            hcfg = dict(width=ow, height=oh, fps=fps, qp=max(0, min(51, q)), keyint=1 << 30,
+                        level_idc=int(cfg.level or 0), deblock=int(cfg.opts.get("deblock", True)))
             parts, psnr = [], []
             for u, (s, c) in enumerate(unit_plan(clip.frames, cfg.keyint)):
                 enc = self.host.CpuEncoder(hcfg)
@@ -82,6 +83,11 @@ class CpuBackend:
             raise BackendError(f"codec {cfg.codec} is not available in the cpu backend")
         if cfg.bit_depth != 8:
             raise BackendError("10-bit output is not supported by the cpu backend")
+        # the reference encoder is Constrained Baseline at a fixed QP: knobs it honours are
+        # the Baseline profile itself, -level and deblocking; anything else is refused
+        extra = {k: v for k, v in cfg.opts.items() if (k, v) not in (("cabac", False), ("bframes", 0)) and k != "deblock"}
+        if extra:
+            raise BackendError(f"the cpu reference backend (Constrained Baseline, fixed QP) cannot honour {extra}")
 
     def _one(self, j: PieceJob, cfg: EncoderConfig) -> PieceResult:
         try:

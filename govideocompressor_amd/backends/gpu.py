@@ -101,6 +101,10 @@ class GpuBackend:
                 params = H264Params(width=ow, height=oh, fps=fps, crf=crf if cfg.qp is None else None,
                                     qp=cfg.qp if cfg.qp is not None else 26)
             params = presets.apply(params, cfg.preset)
+            try:
+                params = cfg.apply_opts(params)  # -profile:v / -tune / -level / -x26x-params
+            except ValueError as e:
+                raise BackendError(str(e)) from None
             # batch width: every unit at once up to what HBM holds (runtime.device.slots_for)
             from ..runtime.device import slots_for
             cap = min(self.max_slots, slots_for(ow, oh, max(c for *_, c in units), self._info, cap=self.max_slots))

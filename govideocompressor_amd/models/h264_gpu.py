@@ -92,6 +92,8 @@ class H264Params:
     # deblock non-reference B pictures even when neither metrics nor the reconstruction
     # are requested (x264 --full-recon); the bitstream does not depend on it
     full_recon: bool = False
+    # level_idc written in the SPS (-level); 0 = the lowest level the size / rate fits
+    level_idc: int = 0
 
     def eff_bframes(self) -> int:
         return max(0, int(self.bframes)) if self.cabac else 0
@@ -105,7 +107,8 @@ class H264Params:
     def host_cfg(self) -> dict:
         return dict(width=self.width, height=self.height, fps=self.fps, qp=self.qp,
                     deblock=int(self.deblock), chroma_qp_offset=self.chroma_qp_offset,
-                    vui=int(self.vui), cabac=int(self.cabac), bframes=self.eff_bframes(), t8x8=int(self.eff_t8x8()))
+                    vui=int(self.vui), cabac=int(self.cabac), bframes=self.eff_bframes(), t8x8=int(self.eff_t8x8()),
+                    level_idc=int(self.level_idc))
 
     def profile_name(self) -> str:
         if not self.cabac:

@@ -81,6 +81,8 @@ class HevcParams:
     # (~0.7 % BD-rate on the synthetic bench content for ~16 % of the 1080p throughput; on from
     # -preset slow)
     tu_inter_depth: int = 0
+    # general_level_idc (30 x level, -level); 0 = the lowest level the size / rate fits
+    level_idc: int = 0
 
     def adaptive_qp(self) -> bool:
         return self.aq_strength > 0 or (self.cutree and self.lookahead and self.crf is not None)
@@ -88,7 +90,8 @@ class HevcParams:
     def host_cfg(self) -> dict:
         return dict(width=self.width, height=self.height, bit_depth=self.bit_depth, fps=self.fps,
                     sao=int(self.sao), deblock=int(self.deblock), max_merge=self.max_merge, wpp=int(self.wpp),
-                    cu_qp_delta=int(self.adaptive_qp()), tu_inter_depth=int(self.tu_inter_depth), sdh=int(self.sdh))
+                    cu_qp_delta=int(self.adaptive_qp()), tu_inter_depth=int(self.tu_inter_depth), sdh=int(self.sdh),
+                    level_idc=int(self.level_idc))
 
     def frame_qps(self) -> tuple[int, int]:
         qp_p = int(round(self.crf)) if self.crf is not None else int(self.qp)

@@ -129,3 +129,46 @@ def test_ffargs_rate_vbv_audio_options():
                 "-vcodec libx264 -acodec aac", "-vcodec libx264 -b:v 0"):
         with pytest.raises(ffargs.FfArgsError):
             ffargs.parse(bad)
+
+
+def test_ffargs_profile_tune_level_params():
+    """-profile:v / -tune / -level / -x26x-params map onto encoder knobs."""
+    from govideocompressor_amd.models.h264_gpu import H264Params
+    from govideocompressor_amd.models.hevc_gpu import HevcParams
+    from govideocompressor_amd.ops import native
+    host = native.host()
+    c = ffargs.parse("-vcodec libx264 -profile:v baseline")
+    p = c.apply_opts(H264Params(width=640, height=360))
+    assert p.cabac is False and p.eff_bframes() == 0 and not p.eff_t8x8()
+    sps = host.stream_info(host.parameter_sets(p.host_cfg()))
+    assert sps["profile_idc"] == 66                                   # Constrained Baseline
+    p = ffargs.parse("-vcodec libx264 -profile:v main").apply_opts(H264Params(width=640, height=360))
+    assert p.cabac and not p.eff_t8x8() and host.stream_info(host.parameter_sets(p.host_cfg()))["profile_idc"] == 77
+    c = ffargs.parse("-vcodec libx264 -level 4.1 -tune zerolatency -x264-params bframes=0:aq-mode=0:keyint=48:crf=20")
+    assert (c.level, c.keyint, c.crf, c.tune) == (41, 48, 20.0, "zerolatency")
+    p = c.apply_opts(H264Params(width=1920, height=1080))
+    assert (p.bframes, p.lookahead, p.mbtree, p.aq_strength, p.level_idc) == (0, False, False, 0.0, 41)
+    assert host.stream_info(host.parameter_sets(p.host_cfg()))["level_idc"] == 41
+    with pytest.raises(RuntimeError):                                 # 1080p30 does not fit level 3
+        host.parameter_sets(ffargs.parse("-vcodec libx264 -level 3").apply_opts(H264Params(1920, 1080)).host_cfg())
+    c = ffargs.parse("-vcodec libx265 -profile:v main10 -level 5.1 -x265-params sao=0:max-merge=5:no-cutree=1")
+    assert c.bit_depth == 10 and c.level == 153 and c.crf == 28.0
+    p = c.apply_opts(HevcParams(width=1920, height=1080, bit_depth=10))
+    assert (p.sao, p.max_merge, p.cutree, p.level_idc) == (False, 5, False, 153)
+    assert ffargs.parse("-vcodec libx265 -x265-params crf=22").crf == 22.0
+    assert ffargs.parse("-vcodec libx265 -profile:v mainstillpicture").opts == {"intra_only": True}
+    assert ffargs.parse("-vcodec libx265 -tune fastdecode").opts == {"deblock": False, "sao": False}
+
+
+def test_ffargs_strict_rejections():
+    """Options the native encoders cannot honour are errors, never silently dropped."""
+    for bad in ("-vcodec libx264 -tune film", "-vcodec libx264 -tune ssim", "-vcodec libx264 -profile:v high10",
+                "-vcodec libx264 -profile:v high444", "-vcodec libx265 -profile:v main12",
+                "-vcodec libx264 -x264-params ref=3", "-vcodec libx264 -x264-params weightp=2",
+                "-vcodec libx264 -x264-params foo=1", "-vcodec libx264 -x265-params sao=0",
+                "-vcodec libx265 -x265-params bframes=4", "-vcodec libx265 -x265-params ctu=64",
+                "-vcodec libx264 -x264-params aq-mode=2", "-vcodec libx264 -x264-params deblock=1,1",
+                "-vcodec libx264 -profile:v baseline -x264-params bframes=3", "-vcodec libx264 -level 9",
+                "-vcodec libx265 -profile:v main -pix_fmt yuv420p10le", "-vcodec copy -tune psnr"):
+        with pytest.raises(ffargs.FfArgsError):
+            ffargs.parse(bad)
