@@ -169,7 +169,7 @@ def _hevc_run(args, W, H, B, F, bd, crf, two_pass_kbps=None, fps=30.0, resident=
     from govideocompressor_amd.models.h264_gpu import synth_clip
     from govideocompressor_amd.models.hevc_gpu import GpuHevcEncoder, HevcParams
     from govideocompressor_amd.parallel import dist as D
-    from govideocompressor_amd.rc import GlobalStats, abr_qps
+    from govideocompressor_amd.rc import GlobalStats, TwoPassFeedback, abr_solve
 
     env = D.init(prefer_gpu=True)
     enc = GpuHevcEncoder(HevcParams(width=W, height=H, fps=fps, crf=crf, bit_depth=bd), slots=B, device=env.device)
@@ -197,11 +197,17 @@ def _hevc_run(args, W, H, B, F, bd, crf, two_pass_kbps=None, fps=30.0, resident=
         gs.put(env.rank * n, st)
         glob = gs.reduce()                                             # CC-1 all-reduce
         target = two_pass_kbps * 1000.0 * (n * env.world) / fps
-        qps_all = abr_qps(glob, target)
-        mine = qps_all[env.rank * n:(env.rank + 1) * n].reshape(B, F)
-        r2 = enc.encode(y, u, v, qps=mine, metrics=quality)            # pass 2
-        return r2, dict(pass1_bits=float(np.sum(st[:, 2])), target_bits=target / env.world,
-                        pass2_bits=float(sum(sum(r.bits) for r in r2)))
+        # the global solve (CC-1 totals) sets this rank's share of the budget: the frames
+        # of every rank at one common offset; pass 2 then steers its share with feedback
+        d0 = abr_solve(glob, target)
+        p1 = glob[:, 2] * 2.0 ** (-d0 / 6.0)
+        share = target * float(np.sum(p1[env.rank * n:(env.rank + 1) * n])) / max(float(np.sum(p1)), 1.0)
+        fb = TwoPassFeedback(st[:, 2].reshape(B, F), q1, share)
+        r2 = enc.encode(y, u, v, metrics=quality, rate_fb=fb)          # pass 2
+        got = float(sum(sum(r.bits) for r in r2))
+        return r2, dict(pass1_bits=float(np.sum(st[:, 2])), target_bits=share, pass2_bits=got,
+                        pass2_vs_target=round(got / share, 4), exponent=round(fb.e, 3),
+                        feedback_updates=len(fb.history))
 
     res, info = step(-1, quality=True)                                 # warmup (+ PSNR)
     psnr = float(np.mean([r.psnr_y for r in res]))

@@ -109,16 +109,32 @@ class GpuBackend:
             from ..runtime.device import slots_for
             cap = min(self.max_slots, slots_for(ow, oh, max(c for *_, c in units), self._info, cap=self.max_slots))
             chunks = [units[b0:b0 + cap] for b0 in range(0, len(units), cap)]
-            prepared = [self._prepare_chunk(ch, clips, w, h, tm) for ch in chunks]
-            if (ow, oh) != (w, h):  # -s WxH: bicubic resample on the device (ops/scale.py)
-                if getattr(self, "_scaler", None) is None:
-                    from ..ops.scale import GpuScaler
-                    self._scaler = GpuScaler(self.device)
-                prepared = [self._scaler.clip(*dev, ow, oh) for dev in prepared]
+
+            def prepare(ch, w=w, h=h, ow=ow, oh=oh):
+                dev = self._prepare_chunk(ch, clips, w, h, tm)
+                if (ow, oh) != (w, h):  # -s WxH: bicubic resample on the device (ops/scale.py)
+                    if getattr(self, "_scaler", None) is None:
+                        from ..ops.scale import GpuScaler
+                        self._scaler = GpuScaler(self.device)
+                    dev = self._scaler.clip(*dev, ow, oh)
+                return dev
+
             rate_info: dict[str, dict] = {}
             if cfg.bitrate is None and qp_offsets is None:
-                unit_out = [x for ch, dev in zip(chunks, prepared) for x in self._run_encoder(ch, params, *dev, tm)]
+                # one chunk resident at a time: `cap` sizes ONE chunk to the HBM budget
+                unit_out = []
+                for ch in chunks:
+                    dev = prepare(ch)
+                    unit_out += self._run_encoder(ch, params, *dev, tm)
+                    del dev
             else:
+                # the rate search re-encodes the batch: a single chunk stays resident between
+                # passes, several chunks are re-prepared for every pass (only one fits)
+                if len(chunks) == 1:
+                    held = prepare(chunks[0])
+                    prepared = [lambda: held]
+                else:
+                    prepared = [lambda ch=ch: prepare(ch) for ch in chunks]
                 unit_out, rate_info = self._encode_rate(keys, chunks, prepared, clips, params, cfg, fps, tm,
                                                         rate_stats, qp_offsets)
             for key in keys:
@@ -142,7 +158,8 @@ class GpuBackend:
 
         def encode_all(offsets: np.ndarray, vbv: dict[tuple, np.ndarray] | None = None):
             outs = []
-            for ch, dev in zip(chunks, prepared):
+            for ch, get_dev in zip(chunks, prepared):
+                dev = get_dev()
                 F = max(c for *_, c in ch)
                 delta = np.zeros((len(ch), F))
                 for b, (key, un_, _, c) in enumerate(ch):

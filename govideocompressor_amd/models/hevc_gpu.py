@@ -254,10 +254,14 @@ class GpuHevcEncoder:
 
     # ------------------------------------------------------------------ encode
     def encode(self, y: torch.Tensor, u: torch.Tensor, v: torch.Tensor, qps: np.ndarray | None = None,
-               keep_recon: bool = False, metrics: bool = True, qp_delta=None) -> list[HevcSegmentResult]:
+               keep_recon: bool = False, metrics: bool = True, qp_delta=None, rate_fb=None) -> list[HevcSegmentResult]:
         """y: [B, F, h, w] (uint8, or uint16 holding bit_depth-bit samples), u/v half size.
         Every segment starts with an IDR picture; the others are P pictures
-        (intra_only: IDR pictures only)."""
+        (intra_only: IDR pictures only).
+
+        ``rate_fb`` (:class:`~govideocompressor_amd.rc.ratecontrol.TwoPassFeedback`): pass-2
+        rate feedback -- before every frame step the controller sees the bits of the pictures
+        whose CABAC has finished and may re-solve the QPs of the frames not yet started."""
         B, F, h, w = y.shape
         if B != self.B or (w, h) != (self.p.width, self.p.height):
             raise ValueError(f"expected [{self.B}, F, {self.p.height}, {self.p.width}], got {list(y.shape)}")
@@ -279,8 +283,10 @@ class GpuHevcEncoder:
         if qp_delta is not None:
             from ..rc.abr import apply_delta
             qps = apply_delta(qps, qp_delta)
-        self.last_qps = qps.copy()
+        if rate_fb is not None:
+            qps = np.array(rate_fb.qps, dtype=np.int32).reshape(B, F)
         qps_d = torch.from_numpy(np.ascontiguousarray(qps.T)).to(self.dev)  # [F, B], one upload
+        fb_known, fb_spent, fb_stage = 0, np.zeros((B, F)), []
         nals: list[list] = [[None] * F for _ in range(B)]
         futs = []
         pending: list[list] = [[], [], []]
@@ -293,6 +299,18 @@ class GpuHevcEncoder:
         bd = self.p.bit_depth
         for t in range(F):
             t0 = time.perf_counter()
+            if rate_fb is not None and t > 0:
+                # bits of the pictures whose CABAC jobs have finished (coding order prefix)
+                while fb_known < len(futs) and futs[fb_known][1].done():
+                    for b, nal in enumerate(futs[fb_known][1].result()):
+                        fb_spent[b, fb_known] = 8 * len(nal)
+                    fb_known += 1
+                newq = np.asarray(rate_fb.update(fb_known, fb_spent, t), dtype=np.int32)
+                if not np.array_equal(newq[:, t:], qps[:, t:]):
+                    qps[:, t:] = newq[:, t:]
+                    st = torch.from_numpy(np.ascontiguousarray(qps[:, t:].T)).pin_memory()
+                    qps_d[t:].copy_(st, non_blocking=True)  # stream-ordered before frame t's read
+                    fb_stage.append(st)  # keep the pinned source alive until the encode ends
             idr = t == 0 or self.p.intra_only or (self.p.keyint > 0 and t % self.p.keyint == 0)
             self._prep(y, u, v, t, proxy=not idr)
             self.qp.copy_(qps_d[t])  # device-to-device: no host sync inside the frame loop
@@ -395,6 +413,7 @@ class GpuHevcEncoder:
             f = self.pool.submit(job)
             futs.append((t, f))
             pending[hb].append(f)
+        self.last_qps = qps.copy()
         if int(self.err.item()) != 0:
             raise RuntimeError("HEVC encoder: wavefront progress timeout")
         t2 = time.perf_counter()

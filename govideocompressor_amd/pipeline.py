@@ -126,6 +126,22 @@ class SegmentCheckpoint:
             return fh.read()
 
 
+def content_digest(path: str, sample: int = 1 << 20, points: int = 16) -> str:
+    """Identity of an input's *content* for the resume checkpoint: a hash of the first and
+    last MiB plus ``points`` evenly spaced 1 MiB samples (raw clips of one geometry all have
+    the same size, so size + path alone would splice an old run's segments into a new clip)."""
+    import hashlib
+    h = hashlib.blake2b(digest_size=16)
+    n = os.path.getsize(path)
+    with open(path, "rb") as f:
+        offs = sorted({0, max(0, n - sample), *(k * max(0, n - sample) // max(1, points - 1) for k in range(points))})
+        for o in offs:
+            f.seek(o)
+            h.update(f.read(sample))
+    h.update(str(n).encode())
+    return h.hexdigest()
+
+
 def encode_file(path: str, output: str, args: str = "264", backend: str = "auto", slots: int = 16,
                 seg_frames: int | None = None, schedule: str = "static", raw_size: tuple[int, int] | None = None,
                 fps: float = 30.0, log=print, resume: bool = False, work_dir: str | None = None) -> dict:
@@ -146,8 +162,9 @@ def encode_file(path: str, output: str, args: str = "264", backend: str = "auto"
     if resume:
         if cfg.bitrate is not None:
             raise ValueError("resume is for CRF / QP encodes: -b:v solves one offset over the whole file")
-        plan_sig = {"input": os.path.abspath(path), "size": os.path.getsize(path), "args": args, "plan": list(sig),
-                    "seg_frames": seg_frames, "world": env.world, "slots": slots}
+        plan_sig = {"input": os.path.abspath(path), "size": os.path.getsize(path),
+                    "mtime_ns": os.stat(path).st_mtime_ns, "content": content_digest(path), "args": args,
+                    "plan": list(sig), "seg_frames": seg_frames, "world": env.world, "slots": slots}
         ckpt = SegmentCheckpoint(work_dir or output + ".parts", env.rank, plan_sig)
         D.barrier(env)
         skip = set(ckpt.done())

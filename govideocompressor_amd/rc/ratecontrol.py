@@ -19,7 +19,8 @@ Here:
   instead of being met segment by segment.
 
 The model of bits versus quantiser is the standard ``bits ~ qscale^-1`` around the
-pass-1 point, refined with the measured exponent when two points are available.
+pass-1 point; pass 2 re-solves it during the encode with the exponent measured on the
+frames already coded (:class:`TwoPassFeedback`).
 """
 from __future__ import annotations
 
@@ -175,6 +176,86 @@ def estimate_exponent(bits_a: float, qp_a: float, bits_b: float, qp_b: float) ->
     if bits_a <= 0 or bits_b <= 0 or qp_a == qp_b:
         return 1.0
     return -math.log2(bits_b / bits_a) * 6.0 / (qp_b - qp_a)
+
+
+class TwoPassFeedback:
+    """Pass-2 rate feedback: the closed-form solve of :func:`abr_solve` assumes
+    ``bits ~ qscale^-1``; real encodes deviate (the exponent depends on content, frame type
+    and QP range -- config 5 landed at 66 % of its target with it).  This controller
+    re-solves the offset of the frames not yet encoded from what pass 2 has spent so far,
+    x264-style (its 2-pass ``overflow`` compensation), with the exponent measured on the
+    frames already coded:
+
+    * ``r = spent / pass1_bits(done)`` at the mean QP offset ``d_done`` of those frames gives
+      ``e = -6 log2(r) / d_done`` (the prior when ``|d_done|`` is small), clamped and damped;
+    * the remaining budget ``target - spent`` over ``pass1_bits(rest)`` gives the offset of
+      the rest, ``d = -6 / e * log2(budget / rest1)``, dithered over the slots so that the
+      fractional part is realised on average.
+
+    One instance per rank: the global solve (CC-1) splits the file's budget into per-rank
+    shares, each rank steers its own share, so the file total follows without further
+    collectives.  Inputs are [B, F] arrays in coding order."""
+
+    def __init__(self, pass1_bits: np.ndarray, pass1_qps: np.ndarray, target_bits: float, exponent: float = 1.0,
+                 qp_min: int = QP_MIN, qp_max: int = QP_MAX):
+        self.b1 = np.asarray(pass1_bits, dtype=np.float64)
+        self.q1 = np.asarray(pass1_qps, dtype=np.float64)
+        self.target = float(target_bits)
+        self.e = float(exponent)
+        self.qmin, self.qmax = qp_min, qp_max
+        d0 = abr_solve(np.stack([np.zeros(self.b1.size), np.zeros(self.b1.size), self.b1.reshape(-1),
+                                 self.q1.reshape(-1)], axis=1), self.target, self.e)
+        self.qps = self._dither(np.full(self.b1.shape, d0), 0)
+        self.history: list[tuple[int, float, float]] = []  # (frames known, exponent, offset of the rest)
+
+    def _dither(self, d: np.ndarray, t0: int) -> np.ndarray:
+        """q1 + d rounded so that every frame step's mean offset over the slots equals d."""
+        q = self.q1 + d
+        B = q.shape[0]
+        out = np.rint(q)
+        for t in range(t0, q.shape[1]):
+            frac = q[:, t] - np.floor(q[:, t])
+            base = np.floor(q[:, t])
+            k = int(round(float(np.sum(frac))))
+            order = np.argsort(-frac, kind="stable")
+            up = np.zeros(B, dtype=bool)
+            up[order[:k]] = True
+            out[:, t] = base + up
+        return np.clip(out, self.qmin, self.qmax).astype(np.int32)
+
+    def update(self, known: int, spent_bits: np.ndarray, t_next: int) -> np.ndarray:
+        """``spent_bits``: [B, known] pass-2 bits of frames < known (all slots);
+        returns the [B, F] QPs with frames >= t_next re-solved."""
+        F = self.b1.shape[1]
+        if known <= 0 or t_next >= F:
+            return self.qps
+        spent = float(np.sum(spent_bits[:, :known]))
+        b1_done = float(np.sum(self.b1[:, :known]))
+        rest1 = float(np.sum(self.b1[:, t_next:]))
+        # mean QP offset actually used on the known frames (bits-weighted)
+        w = np.maximum(self.b1[:, :known], 1.0)
+        d_done = float(np.sum((self.qps[:, :known] - self.q1[:, :known]) * w) / np.sum(w))
+        if b1_done > 0 and spent > 0 and abs(d_done) >= 0.75:
+            e_meas = -6.0 * math.log2(spent / b1_done) / d_done
+            e_meas = min(2.5, max(0.35, e_meas))
+            # damped: trust the measurement more as more frames are known
+            a = min(0.8, known / max(1.0, F / 3.0))
+            self.e = (1.0 - a) * self.e + a * e_meas
+        # frames between `known` and `t_next` are in flight at their current QPs: predict them
+        inflight = 0.0
+        if t_next > known:
+            dq = self.qps[:, known:t_next] - self.q1[:, known:t_next]
+            inflight = float(np.sum(self.b1[:, known:t_next] * 2.0 ** (-self.e * dq / 6.0)))
+        budget = self.target - spent - inflight
+        if rest1 <= 0:
+            return self.qps
+        budget = max(budget, 0.05 * rest1)  # overshoot: coarsest allowed, never a negative budget
+        d = -6.0 / self.e * math.log2(budget / rest1)
+        d = min(24.0, max(-24.0, d))
+        new = self._dither(np.full(self.b1.shape, d), t_next)
+        self.qps = np.concatenate([self.qps[:, :t_next], new[:, t_next:]], axis=1)
+        self.history.append((known, self.e, d))
+        return self.qps
 
 
 class GlobalStats:

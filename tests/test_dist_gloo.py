@@ -248,6 +248,17 @@ def test_encode_file_resume_skips_finished_segments(tmp_path, host):
     r3 = encode_file(str(src), str(tmp_path / "o3.264"), args="-vcodec libx264 -crf 30", backend="cpu", slots=4,
                      seg_frames=8, log=lambda s: None, resume=True, work_dir=str(wd))
     assert r3["resumed_segments"] == 0
+    # the same path and byte size with different content invalidates the checkpoint too
+    r4 = encode_file(str(src), str(tmp_path / "o4.264"), args="-vcodec libx264 -crf 30", backend="cpu", slots=4,
+                     seg_frames=8, log=lambda s: None, resume=True, work_dir=str(wd))
+    assert r4["resumed_segments"] == 4
+    size = src.stat().st_size
+    yuv.write_y4m(str(src), yuv.synth_clip_cpu(32, 64, 48, seed=6))
+    assert src.stat().st_size == size
+    os.utime(src, ns=(src.stat().st_atime_ns, (tmp_path / "o4.264").stat().st_mtime_ns))
+    r5 = encode_file(str(src), str(tmp_path / "o5.264"), args="-vcodec libx264 -crf 30", backend="cpu", slots=4,
+                     seg_frames=8, log=lambda s: None, resume=True, work_dir=str(wd))
+    assert r5["resumed_segments"] == 0
 
 
 def test_encode_file_json_segment_metrics(tmp_path, monkeypatch):

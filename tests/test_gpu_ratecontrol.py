@@ -111,3 +111,20 @@ def test_global_two_pass_file(tmp_path, host):
     assert abs(8 * size / target - 1) < 0.05, res["rate"]
     pics = host.decode(out.read_bytes())
     assert len(pics) == 48
+
+
+def test_config5_two_pass_path_hits_target():
+    """bench/run.py's config-5 two-pass path (CRF pass 1, CC-1 global solve, pass 2 with
+    TwoPassFeedback) lands within +-5 % of its bitrate target on 10-bit HEVC content."""
+    import argparse
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location("bench_run", os.path.join(os.path.dirname(__file__), "..", "bench",
+                                                                             "run.py"))
+    run = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(run)
+    for kbps in (1500.0, 6000.0):
+        _, d = run._hevc_run(argparse.Namespace(steps=1), 640, 360, 4, 24, 10, 26.0, two_pass_kbps=kbps, fps=60.0,
+                             resident=True)
+        rc = d["rc"]
+        assert abs(rc["pass2_bits"] / rc["target_bits"] - 1) < 0.05, rc

@@ -80,3 +80,35 @@ def test_cpu_backend_bitrate_search():
     target = 300e3 * 12 / clip.fps
     # integer QP steps are ~12 % apart: the closest QP lands within one half step
     assert abs(8 * len(stream) / target - 1) < 0.2
+
+
+@pytest.mark.parametrize("e_true_p,target_scale", [(0.55, 1.6), (1.4, 0.6), (0.8, 1.0), (0.45, 2.5)])
+def test_two_pass_feedback_hits_target(e_true_p, target_scale):
+    """Pass-2 feedback (TwoPassFeedback) lands within 3 % of the target even when the true
+    bits/qscale exponent is far from the closed-form solve's 1.0 (config 5: -34 % before)."""
+    from govideocompressor_amd.rc import TwoPassFeedback
+    rng = np.random.default_rng(7)
+    B, F, lag = 10, 60, 3
+    q1 = np.full((B, F), 29.0)
+    q1[:, 0] = 26.0
+    b1 = rng.uniform(2e5, 6e5, (B, F))
+    b1[:, 0] *= 8.0
+    e_true = np.full((B, F), e_true_p)
+    e_true[:, 0] = 0.85
+    target = target_scale * b1.sum()
+    fb = TwoPassFeedback(b1, q1, target)
+    spent = np.zeros((B, F))
+    qps = fb.qps.copy()
+    for t in range(F):
+        known = max(0, t - lag)
+        if t > 0:
+            qps[:, t:] = fb.update(known, spent, t)[:, t:]
+        d = qps[:, t] - q1[:, t]
+        spent[:, t] = b1[:, t] * 2.0 ** (-e_true[:, t] * d / 6.0) * rng.uniform(0.95, 1.05, B)
+    assert abs(spent.sum() / target - 1.0) < 0.03, (spent.sum() / target, fb.history[-3:])
+    # the plain closed-form solve misses the same target by much more
+    from govideocompressor_amd.rc import abr_solve
+    d0 = abr_solve(np.stack([0 * b1.ravel(), 0 * b1.ravel(), b1.ravel(), q1.ravel()], 1), target)
+    open_loop = np.sum(b1 * 2.0 ** (-e_true * np.round(d0) / 6.0))
+    if target_scale != 1.0:
+        assert abs(open_loop / target - 1.0) > 0.05
