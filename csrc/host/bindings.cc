@@ -17,6 +17,7 @@
 #include "cpu_encoder.h"
 #include "h264_decoder.h"
 #include "hevc_codec.h"
+#include "hevc_dec.h"
 #include "lowres.h"
 
 namespace mivc {
@@ -286,6 +287,131 @@ py::dict hevc_picture_to_dict(const hevc::HevcPicture& p) {
   d["coef_y"] = to_array(p.coef_y, {H, W});
   d["coef_cb"] = to_array(p.coef_cb, {H / 2, W / 2});
   d["coef_cr"] = to_array(p.coef_cr, {H / 2, W / 2});
+  return d;
+}
+
+
+// general HEVC decoder output -> dict (decoding order; "display" = output position or -1)
+template <class T>
+py::array_t<uint8_t> raw_rows(const std::vector<T>& v) {
+  py::array_t<uint8_t> a({static_cast<py::ssize_t>(v.size()), static_cast<py::ssize_t>(sizeof(T))});
+  if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(T));
+  return a;
+}
+
+py::dict dec_picture_to_dict(const hevc::DecPicture& p, bool recon) {
+  py::dict d;
+  d["decode_idx"] = p.decode_idx;
+  d["poc"] = p.poc;
+  d["cvs"] = p.cvs;
+  d["output"] = p.output;
+  d["irap"] = p.irap;
+  d["idr"] = p.idr;
+  d["nal_type"] = p.nal_type;
+  d["slice_type"] = p.slice_type;
+  d["qp"] = p.slice_qp;
+  d["coded_width"] = p.W;
+  d["coded_height"] = p.H;
+  d["width"] = p.width;
+  d["height"] = p.height;
+  d["crop_x"] = p.crop_x;
+  d["crop_y"] = p.crop_y;
+  d["bit_depth"] = p.bit_depth;
+  d["log2_ctb"] = p.log2_ctb;
+  if (recon && !p.y.empty()) {
+    const py::ssize_t H = p.H, W = p.W;
+    d["y"] = to_array(p.y, {H, W});
+    d["u"] = to_array(p.u, {H / 2, W / 2});
+    d["v"] = to_array(p.v, {H / 2, W / 2});
+  }
+  return d;
+}
+
+// GPU hand-off records of one segment: every array concatenated over its pictures
+// (decoding order) with per-picture offsets; record layouts of csrc/host/hevc_dec.h
+py::dict dec_segment_records(std::vector<hevc::DecPicture>& pics, const std::vector<int>& order) {
+  py::dict d;
+  const size_t P = pics.size();
+  if (P == 0) {
+    d["n"] = 0;
+    return d;
+  }
+  const hevc::DecPicture& f = pics[0];
+  const int w4 = f.W / 4, h4 = f.H / 4, nctb = f.wctb * f.hctb;
+  std::vector<int32_t> meta(P * 24, 0), ref_ids(P * 16, -1), display(P, -1);
+  for (size_t i = 0; i < order.size(); ++i) display[order[i]] = static_cast<int32_t>(i);
+  std::vector<uint8_t> mvf, bs, ctbs, sao, scaling;
+  std::vector<hevc::DecTu> tus;
+  std::vector<hevc::DecIntraOp> ops;
+  std::vector<hevc::DecRefEntry> refs;
+  std::vector<hevc::DecSlice> slices;
+  std::vector<int16_t> coefs;
+  std::vector<int64_t> tu_off(P + 1), op_off(P + 1), ref_off(P + 1), slice_off(P + 1), coef_off(P + 1);
+  std::vector<uint32_t> ctb_ops(P * (nctb + 1));
+  mvf.reserve(P * w4 * h4 * 12);
+  for (size_t i = 0; i < P; ++i) {
+    hevc::DecPicture& p = pics[i];
+    if (p.W != f.W || p.H != f.H || p.log2_ctb != f.log2_ctb || p.bit_depth != f.bit_depth)
+      throw std::runtime_error("HEVC segment changes geometry / bit depth between pictures");
+    int32_t* m = &meta[i * 24];
+    const int vals[24] = {p.decode_idx, p.poc, p.cvs, p.output, p.irap, p.idr, p.slice_type, p.slice_qp,
+                          p.W, p.H, p.width, p.height, p.crop_x, p.crop_y, p.bit_depth, p.bit_depth_c,
+                          p.log2_ctb, p.constrained_intra, p.strong_intra, p.lf_across_tiles, p.cb_qp_off, p.cr_qp_off,
+                          p.deblock_any, p.sao_any};
+    std::copy(vals, vals + 24, m);
+    for (size_t k = 0; k < p.ref_ids.size() && k < 16; ++k) ref_ids[i * 16 + k] = p.ref_ids[k];
+    const uint8_t* mb = reinterpret_cast<const uint8_t*>(p.mvf.data());
+    mvf.insert(mvf.end(), mb, mb + p.mvf.size() * sizeof(hevc::DecMv4));
+    bs.insert(bs.end(), p.bs.begin(), p.bs.end());
+    const uint8_t* cb = reinterpret_cast<const uint8_t*>(p.ctbs.data());
+    ctbs.insert(ctbs.end(), cb, cb + p.ctbs.size() * sizeof(hevc::DecCtb));
+    const uint8_t* sb = reinterpret_cast<const uint8_t*>(p.sao.data());
+    sao.insert(sao.end(), sb, sb + p.sao.size() * sizeof(hevc::DecSao));
+    if (!p.scaling.empty()) {
+      if (scaling.empty()) scaling.assign(P * hevc::kScalingBytes, 16);
+      std::memcpy(scaling.data() + i * hevc::kScalingBytes, p.scaling.data(), hevc::kScalingBytes);
+    }
+    tu_off[i] = static_cast<int64_t>(tus.size());
+    op_off[i] = static_cast<int64_t>(ops.size());
+    ref_off[i] = static_cast<int64_t>(refs.size());
+    slice_off[i] = static_cast<int64_t>(slices.size());
+    coef_off[i] = static_cast<int64_t>(coefs.size());
+    tus.insert(tus.end(), p.tus.begin(), p.tus.end());
+    ops.insert(ops.end(), p.ops.begin(), p.ops.end());
+    refs.insert(refs.end(), p.refs.begin(), p.refs.end());
+    slices.insert(slices.end(), p.slices.begin(), p.slices.end());
+    coefs.insert(coefs.end(), p.coefs.begin(), p.coefs.end());
+    std::copy(p.ops_off.begin(), p.ops_off.end(), ctb_ops.begin() + i * (nctb + 1));
+    // the records are consumed: free them as we go (segments can be large)
+    std::vector<hevc::DecMv4>().swap(p.mvf);
+    std::vector<int16_t>().swap(p.coefs);
+  }
+  tu_off[P] = static_cast<int64_t>(tus.size());
+  op_off[P] = static_cast<int64_t>(ops.size());
+  ref_off[P] = static_cast<int64_t>(refs.size());
+  slice_off[P] = static_cast<int64_t>(slices.size());
+  coef_off[P] = static_cast<int64_t>(coefs.size());
+  const py::ssize_t Pn = static_cast<py::ssize_t>(P);
+  d["n"] = static_cast<int>(P);
+  d["meta"] = to_array(meta, {Pn, 24});
+  d["ref_ids"] = to_array(ref_ids, {Pn, 16});
+  d["display"] = to_array(display, {Pn});
+  d["mvf"] = to_array(mvf, {Pn, h4, w4, 12});
+  d["bs"] = to_array(bs, {Pn, h4, w4});
+  d["ctbs"] = to_array(ctbs, {Pn, nctb, 8});
+  d["sao"] = to_array(sao, {Pn, nctb, 24});
+  d["scaling"] = scaling.empty() ? py::array_t<uint8_t>(std::vector<py::ssize_t>{0}) : to_array(scaling, {Pn, hevc::kScalingBytes});
+  d["tus"] = raw_rows(tus);
+  d["ops"] = raw_rows(ops);
+  d["refs"] = raw_rows(refs);
+  d["slices"] = raw_rows(slices);
+  d["coefs"] = to_array(coefs, {static_cast<py::ssize_t>(coefs.size())});
+  d["ctb_ops"] = to_array(ctb_ops, {Pn, nctb + 1});
+  d["tu_off"] = to_array(tu_off, {Pn + 1});
+  d["op_off"] = to_array(op_off, {Pn + 1});
+  d["ref_off"] = to_array(ref_off, {Pn + 1});
+  d["slice_off"] = to_array(slice_off, {Pn + 1});
+  d["coef_off"] = to_array(coef_off, {Pn + 1});
   return d;
 }
 
@@ -593,6 +719,110 @@ PYBIND11_MODULE(_host, m) {
         return out;
       },
       py::arg("data"), py::arg("skip_filters") = false);
+
+
+  // ---------------------------------------------------------------- general HEVC decoder (hevc_dec.h)
+  m.def(
+      "hevc_decode_full",
+      [](py::bytes data, bool recon, bool skip_filters) {
+        std::string s = data;
+        hevc::DecodeOptions o;
+        o.recon = recon;
+        o.skip_filters = skip_filters;
+        hevc::HevcStreamDecoder dec(o);
+        {
+          py::gil_scoped_release rel;
+          dec.decode(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+        }
+        const std::vector<int> order = dec.output_order();
+        std::vector<int> display(dec.pictures().size(), -1);
+        for (size_t i = 0; i < order.size(); ++i) display[order[i]] = static_cast<int>(i);
+        py::list out;
+        for (size_t i = 0; i < dec.pictures().size(); ++i) {
+          py::dict d = dec_picture_to_dict(dec.pictures()[i], recon);
+          d["display"] = display[i];
+          out.append(d);
+        }
+        return out;
+      },
+      py::arg("data"), py::arg("recon") = true, py::arg("skip_filters") = false);
+  m.def(
+      "hevc_parse",
+      [](const std::vector<py::bytes>& segments, int threads, bool recon) {
+        // entropy decode + motion derivation of many segments, one thread per segment; the
+        // GPU records of every segment (recon: also the CPU reconstruction, for tests)
+        std::vector<std::string> in;
+        for (const py::bytes& b : segments) in.emplace_back(b);
+        std::vector<std::unique_ptr<hevc::HevcStreamDecoder>> decs(in.size());
+        std::vector<std::string> err(in.size());
+        {
+          py::gil_scoped_release rel;
+          std::atomic<size_t> next{0};
+          int nt = std::max(1, std::min<int>(threads, static_cast<int>(in.size())));
+          std::vector<std::thread> pool;
+          for (int t = 0; t < nt; ++t)
+            pool.emplace_back([&] {
+              for (size_t i = next++; i < in.size(); i = next++) {
+                hevc::DecodeOptions o;
+                o.recon = recon;
+                o.gpu_records = true;
+                decs[i].reset(new hevc::HevcStreamDecoder(o));
+                try {
+                  decs[i]->decode(reinterpret_cast<const uint8_t*>(in[i].data()), in[i].size());
+                } catch (const std::exception& e) {
+                  err[i] = e.what();
+                }
+              }
+            });
+          for (std::thread& th : pool) th.join();
+        }
+        py::list out;
+        for (size_t i = 0; i < in.size(); ++i) {
+          py::dict d;
+          if (!err[i].empty()) {
+            d["n"] = 0;
+            d["error"] = err[i];
+          } else {
+            const std::vector<int> order = decs[i]->output_order();
+            d = dec_segment_records(decs[i]->pictures(), order);
+            if (recon) {
+              py::list pl;
+              for (const hevc::DecPicture& p : decs[i]->pictures()) pl.append(dec_picture_to_dict(p, true));
+              d["pictures"] = pl;
+            }
+          }
+          decs[i].reset();
+          out.append(d);
+        }
+        return out;
+      },
+      py::arg("segments"), py::arg("threads") = 1, py::arg("recon") = false);
+  m.def("hevc_stream_info", [](py::bytes data) {
+    std::string s = data;
+    const hevc::HevcStreamInfo si = hevc::hevc_stream_info(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+    py::dict d;
+    d["width"] = si.width;
+    d["height"] = si.height;
+    d["bit_depth"] = si.bit_depth;
+    d["fps"] = si.fps;
+    d["frames"] = si.pictures;
+    d["irap_frames"] = si.irap;
+    return d;
+  });
+  m.def(
+      "hevc_split_pieces",
+      [](py::bytes data, int min_frames) {
+        std::string s = data;
+        std::vector<std::vector<uint8_t>> parts;
+        {
+          py::gil_scoped_release rel;
+          parts = hevc::hevc_split_pieces(reinterpret_cast<const uint8_t*>(s.data()), s.size(), min_frames);
+        }
+        py::list out;
+        for (const auto& p : parts) out.append(to_bytes(p));
+        return out;
+      },
+      py::arg("data"), py::arg("min_frames") = 1);
 
   py::class_<CpuEncoder>(m, "CpuEncoder")
       .def(py::init([](const py::dict& cfg) { return new CpuEncoder(cfg_from(cfg)); }))

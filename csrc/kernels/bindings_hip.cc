@@ -3,13 +3,17 @@
 // (torch.cuda.current_stream().cuda_stream), so this module needs neither torch
 // headers nor a JIT: it is built in-tree by govideocompressor_amd/_build.py.
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
 #include <cstdint>
 #include <stdexcept>
 
+#include "hevc_decode.h"
+
 namespace py = pybind11;
 
 extern "C" {
+int mivc_launch_hevc_decode(const mivc::gpu::HevcDecParams* p, int stage, void* stream);
 void mivc_launch_synth(void* y, void* u, void* v, int width, int height, int slots, int frames, int frame0,
                        uint32_t seed, int bit_depth, void* stream);
 void mivc_launch_prep(const uint8_t* in_y, const uint8_t* in_u, const uint8_t* in_v, int w, int h,
@@ -345,6 +349,58 @@ PYBIND11_MODULE(_hip, m) {
     mivc_launch_hevc_sao(B, W, H, bd, P<uint16_t>(dy), P<uint16_t>(du), P<uint16_t>(dv), P<uint16_t>(y), P<uint16_t>(u),
                          P<uint16_t>(v), P<uint16_t>(sy), P<uint16_t>(su), P<uint16_t>(sv), P<void>(ctu), P<int>(qp),
                          P<int8_t>(run), enable, S(stream));
+  });
+  // HEVC decode reconstruction (hevc_decode.hip): `p` maps HevcDecParams field names to
+  // ints (device pointers as data_ptr(), scalars); stage 0..5 (see the launcher)
+  m.def("hevc_decode_stage", [](const py::dict& p, int stage, uintptr_t stream) {
+    mivc::gpu::HevcDecParams a{};
+    auto I = [&](const char* k) -> long long {
+      if (!p.contains(k)) throw std::runtime_error(std::string("hevc_decode_stage: missing ") + k);
+      return p[k].cast<long long>();
+    };
+    auto Q = [&](const char* k) -> uintptr_t { return p.contains(k) ? p[k].cast<uintptr_t>() : 0; };
+    a.B = static_cast<int>(I("B"));
+    a.W = static_cast<int>(I("W"));
+    a.H = static_cast<int>(I("H"));
+    a.D = static_cast<int>(I("D"));
+    a.bd = static_cast<int>(I("bd"));
+    a.bdc = static_cast<int>(I("bdc"));
+    a.log2_ctb = static_cast<int>(I("log2_ctb"));
+    a.wctb = static_cast<int>(I("wctb"));
+    a.hctb = static_cast<int>(I("hctb"));
+    const std::vector<uintptr_t> dpb = p["dpb"].cast<std::vector<uintptr_t>>();
+    const std::vector<uintptr_t> res = p["res"].cast<std::vector<uintptr_t>>();
+    const std::vector<uintptr_t> tmp = p["tmp"].cast<std::vector<uintptr_t>>();
+    for (int c = 0; c < 3; ++c) {
+      a.dpb[c] = reinterpret_cast<uint16_t*>(dpb.at(c));
+      a.res[c] = reinterpret_cast<int16_t*>(res.at(c));
+      a.tmp[c] = reinterpret_cast<uint16_t*>(tmp.at(c));
+    }
+    a.cur = P<int8_t>(Q("cur"));
+    a.reftab = P<int8_t>(Q("reftab"));
+    a.run = P<int8_t>(Q("run"));
+    a.meta = P<int32_t>(Q("meta"));
+    a.mvf = P<uint8_t>(Q("mvf"));
+    a.bs = P<uint8_t>(Q("bs"));
+    a.ctbs = P<uint8_t>(Q("ctbs"));
+    a.sao = P<uint8_t>(Q("sao"));
+    a.tus = P<uint8_t>(Q("tus"));
+    a.tu_base = P<int32_t>(Q("tu_base"));
+    a.coefs = P<int16_t>(Q("coefs"));
+    a.coef_base = P<int64_t>(Q("coef_base"));
+    a.ops = P<uint8_t>(Q("ops"));
+    a.op_base = P<int32_t>(Q("op_base"));
+    a.ctb_ops = P<uint32_t>(Q("ctb_ops"));
+    a.refs = P<uint8_t>(Q("refs"));
+    a.ref_base = P<int32_t>(Q("ref_base"));
+    a.slices = P<uint8_t>(Q("slices"));
+    a.slice_base = P<int32_t>(Q("slice_base"));
+    a.scaling = P<uint8_t>(Q("scaling"));
+    a.max_tus = static_cast<int>(I("max_tus"));
+    a.err = P<int>(Q("err"));
+    if (!a.cur || !a.run || !a.meta || !a.mvf || !a.err) throw std::runtime_error("hevc_decode_stage: null pointer");
+    const int r = mivc_launch_hevc_decode(&a, stage, S(stream));
+    if (r != 0) throw std::runtime_error("hevc_decode_stage: launch failed (" + std::to_string(r) + ")");
   });
   m.def("cavlc_mb_bytes", []() { return mivc_cavlc_mb_bytes(); });
   m.def("cabac_nb_bytes", []() { return mivc_cabac_nb_bytes(); });
