@@ -22,6 +22,9 @@
 
 namespace mivc {
 int selftest_i4_taps(int trials, uint32_t seed);
+namespace hevc {
+std::vector<uint8_t> hevc_exercise(uint32_t seed);
+}
 }
 
 namespace py = pybind11;
@@ -797,6 +800,7 @@ PYBIND11_MODULE(_host, m) {
         return out;
       },
       py::arg("segments"), py::arg("threads") = 1, py::arg("recon") = false);
+  m.def("hevc_exercise", [](uint32_t seed) { return to_bytes(hevc::hevc_exercise(seed)); }, py::arg("seed"));
   m.def("hevc_stream_info", [](py::bytes data) {
     std::string s = data;
     const hevc::HevcStreamInfo si = hevc::hevc_stream_info(reinterpret_cast<const uint8_t*>(s.data()), s.size());

@@ -9,6 +9,7 @@
 #include <map>
 #include <memory>
 
+#include "hevc_ctx_tables.h"
 #include "hevc_dec_ps.h"
 
 namespace mivc {
@@ -20,73 +21,6 @@ namespace {
 
 inline int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
 inline int sgn(int v) { return (v > 0) - (v < 0); }
-
-// ---------------------------------------------------------------- contexts (9.3.2.2, Tables 9-5 .. 9-37)
-enum DCtx : int {
-  C_SAO_MERGE = 0, C_SAO_TYPE = 1, C_SPLIT_CU = 2, C_TQ_BYPASS = 5, C_SKIP = 6, C_PRED_MODE = 9, C_PART_MODE = 10,
-  C_PREV_INTRA = 14, C_CHROMA_MODE = 15, C_MERGE_FLAG = 16, C_MERGE_IDX = 17, C_INTER_PRED = 18, C_REF_IDX = 23,
-  C_MVD_G0 = 25, C_MVD_G1 = 26, C_MVP = 27, C_ROOT_CBF = 28, C_SPLIT_TF = 29, C_CBF_LUMA = 32, C_CBF_CHROMA = 34,
-  C_TSKIP = 38, C_LAST_X = 40, C_LAST_Y = 58, C_CSBF = 76, C_SIG = 80, C_GT1 = 122, C_GT2 = 146, C_QP_DELTA = 152,
-  kNumDCtx = 154
-};
-
-// clang-format off
-const uint8_t kInit[3][kNumDCtx] = {
-  { 153, 200, 139, 141, 157, 154, 154, 154, 154, 154, 184, 154, 154, 154, 184, 63, 154, 154,
-    154, 154, 154, 154, 154, 154, 154, 154, 154, 154, 154, 153, 138, 138, 111, 141, 94, 138, 182, 154,
-    139, 139,
-    110, 110, 124, 125, 140, 153, 125, 127, 140, 109, 111, 143, 127, 111, 79, 108, 123, 63,
-    110, 110, 124, 125, 140, 153, 125, 127, 140, 109, 111, 143, 127, 111, 79, 108, 123, 63,
-    91, 171, 134, 141,
-    111, 111, 125, 110, 110, 94, 124, 108, 124, 107, 125, 141, 179, 153, 125, 107, 125, 141, 179, 153,
-    125, 107, 125, 141, 179, 153, 125, 140, 139, 182, 182, 152, 136, 152, 136, 153, 136, 139, 111, 136, 139, 111,
-    140, 92, 137, 138, 140, 152, 138, 139, 153, 74, 149, 92, 139, 107, 122, 152, 140, 179, 166, 182, 140, 227, 122, 197,
-    138, 153, 136, 167, 152, 152,
-    154, 154 },
-  { 153, 185, 107, 139, 126, 154, 197, 185, 201, 149, 154, 139, 154, 154, 154, 152, 110, 122,
-    95, 79, 63, 31, 31, 153, 153, 140, 198, 168, 79, 124, 138, 94, 153, 111, 149, 107, 167, 154,
-    139, 139,
-    125, 110, 94, 110, 95, 79, 125, 111, 110, 78, 110, 111, 111, 95, 94, 108, 123, 108,
-    125, 110, 94, 110, 95, 79, 125, 111, 110, 78, 110, 111, 111, 95, 94, 108, 123, 108,
-    121, 140, 61, 154,
-    155, 154, 139, 153, 139, 123, 123, 63, 153, 166, 183, 140, 136, 153, 154, 166, 183, 140, 136, 153,
-    154, 166, 183, 140, 136, 153, 154, 170, 153, 123, 123, 107, 121, 107, 121, 167, 151, 183, 140, 151, 183, 140,
-    154, 196, 167, 167, 154, 152, 167, 182, 182, 134, 149, 136, 153, 121, 136, 122, 169, 208, 166, 167, 154, 152, 167, 182,
-    107, 167, 91, 122, 107, 167,
-    154, 154 },
-  { 153, 160, 107, 139, 126, 154, 197, 185, 201, 134, 154, 139, 154, 154, 183, 152, 154, 137,
-    95, 79, 63, 31, 31, 153, 153, 169, 198, 168, 79, 224, 167, 122, 153, 111, 149, 92, 167, 154,
-    139, 139,
-    125, 110, 124, 110, 95, 94, 125, 111, 111, 79, 125, 126, 111, 111, 79, 108, 123, 93,
-    125, 110, 124, 110, 95, 94, 125, 111, 111, 79, 125, 126, 111, 111, 79, 108, 123, 93,
-    121, 140, 61, 154,
-    170, 154, 139, 153, 139, 123, 123, 63, 124, 166, 183, 140, 136, 153, 154, 166, 183, 140, 136, 153,
-    154, 166, 183, 140, 136, 153, 154, 170, 153, 138, 138, 122, 121, 122, 121, 167, 151, 183, 140, 151, 183, 140,
-    154, 196, 196, 167, 154, 152, 167, 182, 182, 134, 149, 136, 153, 121, 136, 137, 169, 194, 166, 167, 154, 167, 137, 182,
-    107, 167, 91, 107, 107, 167,
-    154, 154 },
-};
-// clang-format on
-
-struct CtxS {
-  uint8_t state, mps;
-};
-
-void init_ctx(CtxS* c, int init_type, int qp) {
-  const int q = clip3(0, 51, qp);
-  for (int i = 0; i < kNumDCtx; ++i) {
-    const int v = kInit[init_type][i];
-    const int m = (v >> 4) * 5 - 45, n = ((v & 15) << 3) - 16;
-    const int pre = clip3(1, 126, ((m * q) >> 4) + n);
-    if (pre <= 63) {
-      c[i].state = static_cast<uint8_t>(63 - pre);
-      c[i].mps = 0;
-    } else {
-      c[i].state = static_cast<uint8_t>(pre - 64);
-      c[i].mps = 1;
-    }
-  }
-}
 
 // renormalisation shift of an LPS range (ranges 6..255, indexed by range >> 3)
 struct RenormTable {
@@ -270,8 +204,11 @@ struct StoredPic {
 struct HevcStreamDecoder::Impl {
   DecodeOptions opt;
   std::vector<DecPicture>* out = nullptr;
-  std::unique_ptr<Sps> sps_tab[16];
-  std::unique_ptr<Pps> pps_tab[64];
+  std::shared_ptr<Sps> sps_tab[16];
+  std::shared_ptr<Pps> pps_tab[64];
+  // the active parameter sets stay alive while a later NAL replaces a table entry
+  std::shared_ptr<Sps> sps_hold;
+  std::shared_ptr<Pps> pps_hold;
   const Sps* sps = nullptr;
   const Pps* pps = nullptr;
 
@@ -351,14 +288,14 @@ struct HevcStreamDecoder::Impl {
     BitReader br(u.rbsp.data() + 1, u.rbsp.size() - 1);
     if (type == VPS_NUT) return;
     if (type == SPS_NUT) {
-      auto s = std::make_unique<Sps>();
+      auto s = std::make_shared<Sps>();
       parse_sps(br, *s);
       const int id = s->id;
       sps_tab[id] = std::move(s);
       return;
     }
     if (type == PPS_NUT) {
-      auto p = std::make_unique<Pps>();
+      auto p = std::make_shared<Pps>();
       const Sps* tab[16];
       for (int i = 0; i < 16; ++i) tab[i] = sps_tab[i].get();
       parse_pps(br, *p, tab);
@@ -412,8 +349,10 @@ struct HevcStreamDecoder::Impl {
 
   // 8.3.1 POC, 8.3.2 RPS, DPB bookkeeping; returns false for a skipped RASL picture
   bool start_picture(const SliceHeader& h, int type, int tid) {
-    pps = pps_tab[h.pps_id].get();
-    const Sps* s = sps_tab[pps->sps_id].get();
+    pps_hold = pps_tab[h.pps_id];
+    pps = pps_hold.get();
+    sps_hold = sps_tab[pps->sps_id];
+    const Sps* s = sps_hold.get();
     if (!s) fail("missing SPS");
     const bool irap = is_irap(type);
     if (irap) {

@@ -46,18 +46,38 @@ def load_clip(path: str) -> yuv.Clip:
         return yuv.read_y4m(path)
     if kind == "yuv":
         raise BackendError("raw .yuv pieces carry no geometry; split them to .y4m")
+    try:
+        return decode_stream_cpu(annexb_of(path, kind))
+    except (RuntimeError, ValueError) as e:
+        raise BackendError(f"{os.path.basename(path)}: {e}") from None
+
+
+def decode_stream_cpu(stream: bytes, fps: float | None = None) -> yuv.Clip:
+    """CPU decode of an Annex-B H.264 or HEVC stream (the independent decoders of
+    csrc/host: h264_decoder.cc, hevc_dec.cc) into an 8-bit display-order clip."""
     from ..ops import native
+    from ..segment.probe import codec_of
     h = native.host()
-    stream = annexb_of(path, kind)
+    if codec_of(stream) == "hevc":
+        info = h.hevc_stream_info(stream)
+        pics = sorted((p for p in h.hevc_decode_full(stream, True, False) if p["display"] >= 0),
+                      key=lambda p: p["display"])
+        if not pics:
+            raise BackendError("no decodable pictures")
+        p0 = pics[0]
+        x0, y0, w, hh = p0["crop_x"], p0["crop_y"], p0["width"], p0["height"]
+        sh = p0["bit_depth"] - 8
+        ys = np.stack([(p["y"][y0:y0 + hh, x0:x0 + w] >> sh) for p in pics]).astype(np.uint8)
+        us = np.stack([(p["u"][y0 // 2:(y0 + hh) // 2, x0 // 2:(x0 + w) // 2] >> sh) for p in pics]).astype(np.uint8)
+        vs = np.stack([(p["v"][y0 // 2:(y0 + hh) // 2, x0 // 2:(x0 + w) // 2] >> sh) for p in pics]).astype(np.uint8)
+        return yuv.Clip(ys, us, vs, fps or info["fps"] or 30.0)
     info = h.stream_info(stream)
-    if info["entropy"] == "cabac":
-        raise BackendError("input uses CABAC; this build decodes CAVLC H.264 only")
     pics = h.decode(stream)
     if not pics:
-        raise BackendError(f"no decodable pictures in {os.path.basename(path)}")
+        raise BackendError("no decodable pictures")
     w, hh = pics[0]["width"], pics[0]["height"]
     buf = np.concatenate([p["i420"] for p in pics])
-    return yuv.Clip.from_i420(buf, w, hh, info["fps"] or 30.0)
+    return yuv.Clip.from_i420(buf, w, hh, fps or info["fps"] or 30.0)
 
 
 def output_size(cfg: EncoderConfig, clip: yuv.Clip) -> tuple[int, int]:

@@ -236,26 +236,54 @@ class GpuBackend:
                        "rate_passes": int(npass), "vbv_passes": vbv_passes}
         return chosen, info
 
-    def decoder(self):
-        """The batched GPU H.264 decoder (host CAVLC/CABAC parse + gfx950 reconstruction)."""
+    def decoder(self, codec: str = "h264"):
+        """The batched GPU decoder of ``codec``: host entropy parse + gfx950 reconstruction
+        (H.264: h264_decode_gpu, HEVC: hevc_decode_gpu)."""
         if self._decoder is None:
-            from ..models.h264_decode_gpu import GpuH264Decoder
-            self._decoder = GpuH264Decoder(self.device)
-        return self._decoder
+            self._decoder = {}
+        if codec not in self._decoder:
+            if codec == "hevc":
+                from ..models.hevc_decode_gpu import GpuHevcDecoder
+                self._decoder[codec] = GpuHevcDecoder(self.device)
+            else:
+                from ..models.h264_decode_gpu import GpuH264Decoder
+                self._decoder[codec] = GpuH264Decoder(self.device)
+        return self._decoder[codec]
 
     def decode_streams(self, streams: list[bytes], fps: float = 30.0):
-        """Annex-B segments -> device-resident clips (``DecodedSegment``), one batched call."""
-        return self.decoder().decode(streams, fps)
+        """Annex-B segments (H.264 and / or HEVC) -> device-resident 8-bit clips
+        (``DecodedSegment``), one batched call per codec."""
+        from ..segment.probe import codec_of
+        import torch
+        out = [None] * len(streams)
+        by: dict[str, list[int]] = {}
+        for i, s in enumerate(streams):
+            by.setdefault(codec_of(s), []).append(i)
+        self.decode_stats = {}
+        for codec, idxs in by.items():
+            dec = self.decoder(codec)
+            got = dec.decode([streams[i] for i in idxs], fps)
+            for k, v in dec.stats.items():
+                self.decode_stats[k] = self.decode_stats.get(k, 0) + v
+            for i, d in zip(idxs, got):
+                if d.y.dtype != torch.uint8:  # Main 10 input: the encoders take 8-bit frames
+                    from ..models.h264_decode_gpu import DecodedSegment
+                    sh = 2
+                    d = DecodedSegment((d.y >> sh).to(torch.uint8), (d.u >> sh).to(torch.uint8),
+                                       (d.v >> sh).to(torch.uint8), d.fps, d.path)
+                out[i] = d
+        return out
 
     def _load_compressed(self, jobs: list[PieceJob]) -> dict[str, object]:
-        """Compressed pieces (.264/.mp4; CAVLC or CABAC, I/P/B, High 8x8) decode together on the GPU."""
+        """Compressed pieces (.264 / .265 / .mp4: H.264 CAVLC or CABAC I/P/B High, HEVC Main /
+        Main 10) decode together on the GPU."""
         from ..ops import native
-        from ..segment.probe import annexb_of, kind_of
+        from ..segment.probe import annexb_of, codec_of, kind_of
         host = native.host()
         streams, keys, fps = [], [], 30.0
         for j in jobs:
             st = annexb_of(j.in_path, kind_of(j.in_path))
-            info = host.stream_info(st)
+            info = host.hevc_stream_info(st) if codec_of(st) == "hevc" else host.stream_info(st)
             fps = info["fps"] or fps
             streams.append(st)
             keys.append(j.idx)
@@ -267,7 +295,7 @@ class GpuBackend:
         t0 = time.perf_counter()
         results: dict[str, PieceResult] = {}
         items = []
-        comp = [j for j in jobs if kind_of(j.in_path) in ("h264", "mp4")]
+        comp = [j for j in jobs if kind_of(j.in_path) in ("h264", "hevc", "mp4")]
         raw = [j for j in jobs if j not in comp]
         futs = {j.idx: self._io.submit(load_clip, j.in_path) for j in raw}
         if comp:

@@ -34,11 +34,10 @@ from .utils import yuv
 
 def _segments(path: str, info, world: int, slots: int, seg_frames: int | None, gop: int | None):
     """Returns (kind, segment list).  Raw: frame ranges; compressed: IDR-aligned pieces."""
-    if info.kind in ("h264", "mp4"):
-        from .ops import native
-        h = native.host()
+    if info.kind in ("h264", "hevc", "mp4"):
+        from .segment.probe import split_stream
         target = seg_frames or max(1, info.frames // max(1, world * slots))
-        pieces = h.split_pieces(annexb_of(path, info.kind), target)
+        pieces = split_stream(annexb_of(path, info.kind), target)
         return "pieces", pieces
     if seg_frames:
         pl = P.fixed_plan(info.frames, seg_frames)
@@ -49,11 +48,8 @@ def _segments(path: str, info, world: int, slots: int, seg_frames: int | None, g
 
 def _load_segment(path: str, info, kind: str, segs, i: int) -> yuv.Clip:
     if kind == "pieces":
-        from .ops import native
-        h = native.host()
-        pics = h.decode(segs[i])
-        buf = np.concatenate([p["i420"] for p in pics])
-        return yuv.Clip.from_i420(buf, pics[0]["width"], pics[0]["height"], info.fps)
+        from .backends.common import decode_stream_cpu
+        return decode_stream_cpu(segs[i], info.fps)
     s, c, _ = (int(x) for x in segs[i])
     if info.kind == "y4m":
         return yuv.read_y4m(path, s, c)
@@ -187,7 +183,7 @@ def encode_file(path: str, output: str, args: str = "264", backend: str = "auto"
     def run(idxs: list[int], offset: float | None = None, into: dict | None = None):
         if gpu_decode:  # compressed input on a GPU rank: batched GPU decode, frames stay on the device
             clips = impl.decode_streams([segs[i] for i in idxs], info.fps)
-            for k, v in impl.decoder().stats.items():
+            for k, v in getattr(impl, "decode_stats", {}).items():
                 dec_stats[k] = dec_stats.get(k, 0) + v
         else:
             clips = list(loader.map(lambda i: _load_segment(path, info, kind, segs, i), idxs))

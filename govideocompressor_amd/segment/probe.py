@@ -9,7 +9,10 @@ stream itself:
 * raw ``.yuv``  -- geometry/fps/bit depth given by the caller, frames = size / frame bytes
 * ``.y4m``      -- header (W, H, F, C)
 * ``.264/.h264`` Annex-B -- SPS (geometry, VUI timing) + access-unit count (C++ probe)
-* ``.mp4``      -- demuxed by the native ISO-BMFF reader, then as Annex-B
+* ``.265/.hevc`` Annex-B -- HEVC SPS (geometry, bit depth, VUI timing) + picture count
+  (csrc/host/hevc_dec_ps.cc)
+* ``.mp4``      -- demuxed by the native ISO-BMFF reader (``avc1`` or ``hvc1``/``hev1``
+  track), then as Annex-B
 
 and :func:`reference_seconds` reproduces the reference's integer arithmetic.
 """
@@ -28,7 +31,7 @@ class ProbeError(ValueError):
 @dataclass
 class MediaInfo:
     path: str
-    kind: str           # yuv | y4m | h264 | mp4
+    kind: str           # yuv | y4m | h264 | hevc | mp4
     width: int
     height: int
     fps: float
@@ -38,6 +41,7 @@ class MediaInfo:
     idr_frames: int = 0
     entropy: str = ""   # cavlc | cabac for compressed inputs
     profile_idc: int = 0
+    codec: str = "raw"  # raw | h264 | hevc (the compressed stream's codec)
 
     @property
     def duration_s(self) -> float:
@@ -57,6 +61,8 @@ def kind_of(path: str) -> str:
         return "y4m"
     if ext in (".264", ".h264", ".avc", ".bin"):
         return "h264"
+    if ext in (".265", ".h265", ".hevc"):
+        return "hevc"
     if ext in (".mp4", ".m4v", ".mov"):
         return "mp4"
     # sniff
@@ -65,10 +71,18 @@ def kind_of(path: str) -> str:
     if head.startswith(b"YUV4MPEG2"):
         return "y4m"
     if head[:4] in (b"\x00\x00\x00\x01",) or head[:3] == b"\x00\x00\x01":
-        return "h264"
+        from .mp4_hevc import is_hevc_annexb
+        return "hevc" if is_hevc_annexb(head) else "h264"
     if head[4:8] == b"ftyp":
         return "mp4"
-    raise ProbeError(f"cannot tell the container of {path}; use .yuv/.y4m/.264/.mp4")
+    raise ProbeError(f"cannot tell the container of {path}; use .yuv/.y4m/.264/.265/.mp4")
+
+
+def codec_of(stream: bytes) -> str:
+    """Codec of an Annex-B stream from its first NAL header: "hevc" or "h264"."""
+    from .mp4_hevc import is_hevc_annexb
+    return "hevc" if is_hevc_annexb(stream) else "h264"
+
 
 
 def annexb_of(path: str, kind: str | None = None) -> bytes:
@@ -82,7 +96,7 @@ def annexb_of(path: str, kind: str | None = None) -> bytes:
             return mp4.annexb_from_mp4(data)  # the video trak, wherever it sits among the tracks
         except ValueError as e:
             raise ProbeError(f"{path}: {e}") from None
-    if kind == "h264":
+    if kind in ("h264", "hevc"):
         return data
     raise ProbeError(f"{path} is not a compressed stream")
 
@@ -102,11 +116,39 @@ def probe(path: str, width: int = 0, height: int = 0, fps: float = 30.0, bit_dep
             hd = yuv.parse_y4m_header(f.read(256))
         return MediaInfo(path, kind, hd.width, hd.height, hd.fps, hd.frames_in(size), hd.bit_depth, size)
     from ..ops import native
-    info = native.host().stream_info(annexb_of(path, kind))
+    stream = annexb_of(path, kind)
+    if codec_of(stream) == "hevc":
+        try:
+            hi = native.host().hevc_stream_info(stream)
+        except RuntimeError as e:
+            raise ProbeError(f"{path}: {e}") from None
+        if hi["width"] <= 0:
+            raise ProbeError(f"{path}: no HEVC sequence parameter set found")
+        return MediaInfo(path, kind, hi["width"], hi["height"], hi["fps"] or fps, hi["frames"], hi["bit_depth"], size,
+                         hi["irap_frames"], "cabac", 0, "hevc")
+    info = native.host().stream_info(stream)
     if info["width"] <= 0:
         raise ProbeError(f"{path}: no H.264 sequence parameter set found")
     return MediaInfo(path, kind, info["width"], info["height"], info["fps"] or fps, info["frames"], 8, size,
-                     info["idr_frames"], info["entropy"], info["profile_idc"])
+                     info["idr_frames"], info["entropy"], info["profile_idc"], "h264")
+
+
+def split_stream(stream: bytes, min_frames: int) -> list[bytes]:
+    """Keyframe-aligned pieces of an Annex-B stream (H.264: at IDR access units; HEVC: at
+    IDR / BLA / CRA-without-RASL access units), parameter sets re-emitted per piece."""
+    from ..ops import native
+    h = native.host()
+    if codec_of(stream) == "hevc":
+        return h.hevc_split_pieces(stream, min_frames)
+    return h.split_pieces(stream, min_frames)
+
+
+def stream_frames(stream: bytes) -> int:
+    from ..ops import native
+    h = native.host()
+    if codec_of(stream) == "hevc":
+        return h.hevc_stream_info(stream)["frames"]
+    return h.stream_info(stream)["frames"]
 
 
 def reference_seconds(info: MediaInfo) -> int:

@@ -6,8 +6,9 @@ then ``ffmpeg -f segment -segment_time T -c copy -reset_timestamps 1`` writes
 
 Here:
 
-* compressed input (``.264`` / ``.mp4``): the native C++ splitter cuts at the
-  first IDR access unit at or after each ``T``-second boundary and re-emits the
+* compressed input (``.264`` / ``.265`` / ``.mp4`` with an H.264 or HEVC track): the
+  native C++ splitter cuts at the first IDR access unit (HEVC: IDR / BLA / CRA without
+  RASL pictures) at or after each ``T``-second boundary and re-emits the
   parameter sets at the head of every piece (the ``-reset_timestamps`` analogue);
   pieces keep the input's container (``.mp4`` via the native muxer, or ``.264``).
   No re-encode -- a stream copy, like ``-c copy``.
@@ -27,9 +28,9 @@ import re
 
 from ..utils import yuv
 from . import plan as P
-from .probe import MediaInfo, annexb_of, probe, reference_seconds
+from .probe import MediaInfo, annexb_of, probe, reference_seconds, split_stream, stream_frames
 
-PIECE_RE = re.compile(r"^([+-]?[0-9]+)\.(mp4|264|h264|y4m)$")
+PIECE_RE = re.compile(r"^([+-]?[0-9]+)\.(mp4|264|h264|265|hevc|y4m)$")
 RAW_DEFAULT_SECONDS = 2.0
 
 
@@ -66,7 +67,7 @@ def split(path: str, size_mb: int = 10, seconds: float | None = None, frames: in
     info: MediaInfo = probe(path, width, height, fps, bit_depth)
     d = os.path.join(out_root, split_dir_name(path))
     os.makedirs(d, exist_ok=True)
-    compressed = info.kind in ("h264", "mp4")
+    compressed = info.kind in ("h264", "hevc", "mp4")
     if frames:
         seg_frames = int(frames)
         seg_s = seg_frames / info.fps
@@ -86,7 +87,7 @@ def split(path: str, size_mb: int = 10, seconds: float | None = None, frames: in
         from ..ops import native
         from . import mp4
         h = native.host()
-        pieces = h.split_pieces(annexb_of(path, info.kind), seg_frames)
+        pieces = split_stream(annexb_of(path, info.kind), seg_frames)
         audio, pts = [], []
         if info.kind == "mp4":
             # -acodec copy -map 0:0 -map 0:1 (server.go:199-200): each piece carries the audio
@@ -95,16 +96,16 @@ def split(path: str, size_mb: int = 10, seconds: float | None = None, frames: in
                 tracks = mp4.read(f.read())
             audio = mp4.audio_tracks(tracks)
             pts = mp4.video_track(tracks).pts_seconds()
-        frames = [h.stream_info(pc)["frames"] for pc in pieces]
+        frames = [stream_frames(pc) for pc in pieces]
         starts = [sum(frames[:i]) for i in range(len(pieces))]
         for i, pc in enumerate(pieces):
             if info.kind == "mp4":
                 t0 = pts[starts[i]] if starts[i] < len(pts) else None
                 t1 = pts[starts[i + 1]] if i + 1 < len(pieces) and starts[i + 1] < len(pts) else None
                 extra = [mp4.cut(a, 0.0 if i == 0 else t0, t1) for a in audio] if t0 is not None else []
-                name, data = f"{i}.mp4", mp4.mux_video(pc, info.fps, "h264", [a for a in extra if a.samples])
+                name, data = f"{i}.mp4", mp4.mux_video(pc, info.fps, info.codec, [a for a in extra if a.samples])
             else:
-                name, data = f"{i}.264", pc
+                name, data = f"{i}.{'265' if info.codec == 'hevc' else '264'}", pc
             with open(os.path.join(d, name), "wb") as f:
                 f.write(data)
             ranges.append({"idx": str(i), "file": name, "frames": frames[i]})
