@@ -1276,11 +1276,13 @@ struct HevcStreamDecoder::Impl {
     const int xb1 = xpb + pw - 1, yb1 = ypb - 1;
     bool b1 = !par_same(xb1, yb1) && !((part == P_2NxN || part == P_2NxnU || part == P_2NxnD) && pidx == 1) &&
               avail_pb(cu_x, cu_y, ncbs, xpb, ypb, pw, ph, pidx, xb1, yb1);
+    // pruning compares against availableA1 / availableB1 (before their own pruning)
+    const bool av_b1 = b1;
     if (b1 && a1 && same_motion(nbmv(xa1, ya1), nbmv(xb1, yb1))) b1 = false;
     // B0
     const int xb0 = xpb + pw, yb0 = ypb - 1;
     bool b0 = !par_same(xb0, yb0) && avail_pb(cu_x, cu_y, ncbs, xpb, ypb, pw, ph, pidx, xb0, yb0);
-    if (b0 && b1 && same_motion(nbmv(xb1, yb1), nbmv(xb0, yb0))) b0 = false;
+    if (b0 && av_b1 && same_motion(nbmv(xb1, yb1), nbmv(xb0, yb0))) b0 = false;
     // A0
     const int xa0 = xpb - 1, ya0 = ypb + ph;
     bool a0 = !par_same(xa0, ya0) && avail_pb(cu_x, cu_y, ncbs, xpb, ypb, pw, ph, pidx, xa0, ya0);
@@ -1289,7 +1291,7 @@ struct HevcStreamDecoder::Impl {
     const int xb2 = xpb - 1, yb2 = ypb - 1;
     bool b2 = !par_same(xb2, yb2) && avail_pb(cu_x, cu_y, ncbs, xpb, ypb, pw, ph, pidx, xb2, yb2);
     if (b2 && a1 && same_motion(nbmv(xa1, ya1), nbmv(xb2, yb2))) b2 = false;
-    if (b2 && b1 && same_motion(nbmv(xb1, yb1), nbmv(xb2, yb2))) b2 = false;
+    if (b2 && av_b1 && same_motion(nbmv(xb1, yb1), nbmv(xb2, yb2))) b2 = false;
     if (a0 + a1 + b0 + b1 == 4) b2 = false;
     if (a1) cand[nc++] = nbmv(xa1, ya1);
     if (b1) cand[nc++] = nbmv(xb1, yb1);

@@ -95,3 +95,21 @@ def test_server_split_and_cpu_transcode_hevc_input(tmp_path, host):
     assert n2 == 2
     data = (tmp_path / "m" / d2 / "1.mp4").read_bytes()
     assert mp4.video_track(mp4.read(data)).codec in (b"hvc1", b"hev1")
+
+
+@pytest.mark.parametrize("name", [f"p_bd{bd}_s{s}" for bd in (8, 10) for s in range(3)])
+def test_decoder_matches_gpu_encoder_reconstruction(host, name):
+    """Streams written by the GPU HEVC encoder (128x96, 5 pictures, AQ / cu_qp_delta, WPP,
+    SAO, merge with 3 candidates; tools/dump_hevc_test_streams.py on an MI355X) decode to the
+    encoder's own reconstruction (SHA-256 of its planes recorded with the streams).  This
+    pinned the merge-candidate pruning rule (B0 / B2 are compared with availableB1, not with
+    B1 after its own pruning, 8.5.3.2.3)."""
+    import hashlib
+    import json
+    import os
+    d = os.path.join(os.path.dirname(__file__), "data")
+    want = json.load(open(os.path.join(d, "hevc_gpuenc_recon_sha256.json")))[name]
+    s = open(os.path.join(d, f"hevc_gpuenc_{name}.265"), "rb").read()
+    pics = _display(host.hevc_decode_full(s, True, False))
+    planes = np.concatenate([np.concatenate([p["y"].ravel(), p["u"].ravel(), p["v"].ravel()]) for p in pics])
+    assert hashlib.sha256(planes.astype(np.uint16).tobytes()).hexdigest() == want
