@@ -11,9 +11,10 @@
    GPU backend when a GPU is visible).
 2. 1080p30 synthetic YUV -> H.264 CRF23 on MI355X: delegates to ``bench.py``
    (the driver's headline metric).
-3. 4K30 H.264 -> H.264 transcode, segment-parallel: a 4K Main-profile CABAC stream with
-   3 B pictures per anchor is made (untimed) with the GPU encoder, then decode (host
-   CABAC parse + gfx950 DPB reconstruction) + re-encode is timed end to end.
+3. 4K30 H.264 -> H.264 (and HEVC -> H.264) transcode, segment-parallel: 4K pieces (High
+   CABAC + 3 B pictures, or HEVC Main) are made (untimed) with the GPU encoders, then decode
+   (host parse of the next batch overlapping the GPU work: gfx950 DPB reconstruction) +
+   re-encode is timed end to end, next to the encode-only rate of the same batch.
 4. 1080p30 synthetic YUV -> HEVC CRF26 (the reference's "265" preset) on MI355X:
    batched GPU HEVC encoder (CTU intra analysis/reconstruction, P pictures, deblock,
    SAO) + host CABAC.
@@ -123,37 +124,60 @@ def config2(args) -> list[dict]:
 
 
 def config3(args) -> list[dict]:
-    """4K30 H.264 -> H.264: batched GPU decode (host CABAC parse + gfx950 reconstruction) + GPU re-encode."""
+    """4K30 H.264 (or HEVC) -> H.264: batched GPU decode (host parse of batch k+1 overlapping the
+    GPU work of batch k) + GPU re-encode (models/transcode.py)."""
     import torch
     if not torch.cuda.is_available():
         return [{"config": 3, "value": None, "note": "needs a GPU"}]
     from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
-    from govideocompressor_amd.pipeline import encode_file
-    from govideocompressor_amd.ops import native
-    W, H, F, S = 3840, 2160, args.frames3, args.segments3
-    tmp = tempfile.mkdtemp(prefix="mivc_cfg3_")
-    try:
-        # untimed: make the 4K input stream (S closed GOPs of F frames, concatenated)
-        enc = GpuH264Encoder(H264Params(width=W, height=H, crf=20), slots=S)
-        y, u, v = synth_clip(S, F, W, H, seed=3)
-        res = enc.encode(y, u, v, metrics=False)
-        enc.close()
-        del y, u, v
+    from govideocompressor_amd.models.hevc_gpu import GpuHevcEncoder, HevcParams
+    from govideocompressor_amd.models.transcode import GpuTranscoder
+    W, H, F, S, B = 3840, 2160, args.frames3, args.segments3, args.slots3
+    recs = []
+    for codec in args.codec3.split(","):
+        # untimed: the 4K input pieces (closed GOPs of F frames), made by this framework's encoders
+        pieces = []
+        mk = (GpuHevcEncoder(HevcParams(width=W, height=H, crf=22.0), slots=B) if codec == "hevc"
+              else GpuH264Encoder(H264Params(width=W, height=H, crf=20), slots=B))
+        for b0 in range(0, S, B):
+            y, u, v = synth_clip(B, F, W, H, seed=3 + b0)
+            pieces += [r.bitstream for r in mk.encode(y, u, v, metrics=False)][:S - b0]
+            del y, u, v
+        mk.close()
+        del mk
         torch.cuda.empty_cache()
-        src = os.path.join(tmp, "in4k.264")
-        with open(src, "wb") as f:
-            f.write(native.host().concat([r.bitstream for r in res]))
-        out = os.path.join(tmp, "out4k.264")
+        tc = GpuTranscoder(H264Params(width=W, height=H, crf=23.0), slots=B)
+        tc.run(pieces[:B], 30.0)                                   # warmup batch
+        torch.cuda.synchronize()
         t0 = time.perf_counter()
-        r = encode_file(src, out, args="264", backend="gpu", slots=S, seg_frames=F, log=lambda s: None)
+        outs = tc.run(pieces, 30.0)
+        torch.cuda.synchronize()
         wall = time.perf_counter() - t0
-        return [{"config": 3, "metric": "transcoded frames/sec (whole node), 4K30 H.264->H.264", "value":
-                 round(S * F / wall, 2), "unit": "frames/s", "n_gpus": 1, "frames": S * F, "segments": S,
-                 "wall_s": round(wall, 3), "output_bytes": r.get("bytes"),
-                 "data": "synthetic 4K Main CABAC + 3B stream made by this encoder (no reference clips available)",
-                 "decode": r.get("decode"), "decode_stats": r.get("decode_stats_rank")}]
-    finally:
-        shutil.rmtree(tmp, ignore_errors=True)
+        tm = dict(tc.timings)
+        # encode-only reference on the same batch width: the decoded frames of one batch
+        codec_in, parsed, _ = tc._parse(pieces[:B])
+        y, u, v, counts = tc._frames(codec_in, parsed, 30.0)
+        del parsed
+        torch.cuda.synchronize()
+        te = time.perf_counter()
+        for _ in range(2):
+            tc._encode(y, u, v, counts)
+        torch.cuda.synchronize()
+        enc_fps = 2 * B * F / (time.perf_counter() - te)
+        del y, u, v
+        tc.close()
+        fps = S * F / wall
+        recs.append({"config": 3, "metric": f"transcoded frames/sec (whole node), 4K30 {codec.upper()}->H.264",
+                     "value": round(fps, 2), "unit": "frames/s", "n_gpus": 1, "frames": S * F, "segments": S,
+                     "segments_per_batch": B, "wall_s": round(wall, 3),
+                     "output_bytes": sum(len(o) for o in outs), "encode_only_fps_same_batch": round(enc_fps, 1),
+                     "transcode_vs_encode_only": round(fps / enc_fps, 3),
+                     "stage_s": {k: round(v, 3) for k, v in tm.items()},
+                     "data": f"synthetic 4K {codec.upper()} pieces made by this framework's encoder "
+                             "(no reference clips available)"})
+        del pieces, outs
+        torch.cuda.empty_cache()
+    return recs
 
 
 def _hevc_run(args, W, H, B, F, bd, crf, two_pass_kbps=None, fps=30.0, resident=False):
@@ -264,7 +288,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workers", type=int, default=4)
     ap.add_argument("--frames3", type=int, default=30)
-    ap.add_argument("--segments3", type=int, default=16)
+    ap.add_argument("--segments3", type=int, default=128)
+    ap.add_argument("--slots3", type=int, default=64)
+    ap.add_argument("--codec3", default="h264,hevc")
     ap.add_argument("--slots4", type=int, default=64)
     ap.add_argument("--frames4", type=int, default=30)
     # 10 segments x 60 frames = a 10 s 8K60 clip (~60 GB of 10-bit samples) resident in HBM

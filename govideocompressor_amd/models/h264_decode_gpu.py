@@ -137,7 +137,20 @@ class GpuH264Decoder:
     def decode(self, segments: list[bytes], fps: float = 30.0) -> list[DecodedSegment]:
         import time
         t0 = time.perf_counter()
-        parsed = self.host.parse(list(segments), self.threads)
+        parsed = self.parse(segments)
+        t1 = time.perf_counter()
+        out = self.reconstruct(parsed, fps)
+        self.stats["parse_s"] = t1 - t0
+        return out
+
+    def parse(self, segments: list[bytes]):
+        """Host stage (GIL released, one C++ thread per segment): entropy decode."""
+        return list(segments), self.host.parse(list(segments), self.threads)
+
+    def reconstruct(self, parsed_in, fps: float = 30.0) -> list[DecodedSegment]:
+        """GPU stage (+ the CPU decoder for segments the GPU path does not cover)."""
+        import time
+        segments, parsed = parsed_in
         t1 = time.perf_counter()
         out: list[DecodedSegment | None] = [None] * len(segments)
         ok, fallback = [], []
@@ -165,8 +178,10 @@ class GpuH264Decoder:
         t2 = time.perf_counter()
         for i in fallback:
             out[i] = self._cpu_decode(segments[i], fps)
-        self.stats = {"parse_s": t1 - t0, "gpu_s": t2 - t1, "cpu_fallback_s": time.perf_counter() - t2,
+        self.stats = {"gpu_s": t2 - t1, "cpu_fallback_s": time.perf_counter() - t2,
                       "segments_gpu": len(segments) - len(fallback), "segments_cpu": len(fallback)}
+        if fallback or len(groups) != 1:
+            self.last_batch = None  # not one [B, F] batch tensor
         return out  # type: ignore[return-value]
 
     # ------------------------------------------------------------------ internals
@@ -234,10 +249,12 @@ class GpuH264Decoder:
         d_cur = torch.from_numpy(cur).to(dev)
         d_reftab = torch.from_numpy(reftab).to(dev)
         d_wp = torch.from_numpy(wp).to(dev)
-        # ---- output tensors and the per-slot decoded picture buffers
-        y_out = torch.empty((B, F, Hc, Wc), dtype=torch.uint8, device=dev)
-        u_out = torch.empty((B, F, Hc // 2, Wc // 2), dtype=torch.uint8, device=dev)
+        # ---- output tensors (display size, contiguous: the encoder's [B, F, h, w] input) and
+        # the per-slot decoded picture buffers
+        y_out = torch.empty((B, F, h, w), dtype=torch.uint8, device=dev)
+        u_out = torch.empty((B, F, h // 2, w // 2), dtype=torch.uint8, device=dev)
         v_out = torch.empty_like(u_out)
+        crop = ((cy, cy + h, cx, cx + w), (cy // 2, (cy + h) // 2, cx // 2, (cx + w) // 2))
         dpb = [torch.zeros((B, D, Hc, Wc), dtype=torch.uint8, device=dev),
                torch.zeros((B, D, Hc // 2, Wc // 2), dtype=torch.uint8, device=dev),
                torch.zeros((B, D, Hc // 2, Wc // 2), dtype=torch.uint8, device=dev)]
@@ -267,14 +284,15 @@ class GpuH264Decoder:
             bi = torch.from_numpy(sel).to(dev)
             di = torch.from_numpy(disp[t, sel]).to(dev)
             ci = torch.from_numpy(cur[t, sel].astype(np.int64)).to(dev)
-            for o_, p_ in zip((y_out, u_out, v_out), dpb):
-                o_[bi, di] = p_[bi, ci]
+            for k, (o_, p_) in enumerate(zip((y_out, u_out, v_out), dpb)):
+                r0, r1, c0, c1 = crop[min(k, 1)]
+                o_[bi, di] = p_[bi, ci][:, r0:r1, c0:c1]
         if int(err.item()) != 0:
             raise RuntimeError(f"GPU decode failed (err={int(err.item()):#x}: 16 = reference outside the DPB, "
                                "else a wavefront progress timeout)")
         res = []
         for j, sg in enumerate(segs):
             Pn = int(sg["n"])
-            res.append(DecodedSegment(y_out[j, :Pn, cy:cy + h, cx:cx + w], u_out[j, :Pn, cy // 2:(cy + h) // 2, cx // 2:(cx + w) // 2],
-                                      v_out[j, :Pn, cy // 2:(cy + h) // 2, cx // 2:(cx + w) // 2], fps, "gpu"))
+            res.append(DecodedSegment(y_out[j, :Pn], u_out[j, :Pn], v_out[j, :Pn], fps, "gpu"))
+        self.last_batch = (y_out, u_out, v_out)
         return res

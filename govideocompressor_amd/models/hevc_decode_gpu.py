@@ -118,8 +118,18 @@ class GpuHevcDecoder:
         """``out_dtype``: torch.uint8 for 8-bit content (the default), int16 holding
         bit_depth-bit samples otherwise."""
         t0 = time.perf_counter()
-        parsed = self.host.hevc_parse(list(segments), self.threads, False)
+        parsed = self.parse(segments)
         t1 = time.perf_counter()
+        out = self.reconstruct(parsed, fps, out_dtype)
+        self.stats = {"parse_s": t1 - t0, "gpu_s": time.perf_counter() - t1, "segments_gpu": len(segments)}
+        return out
+
+    def parse(self, segments: list[bytes]) -> list[dict]:
+        """Host stage (GIL released, one C++ thread per segment): the GPU records."""
+        return self.host.hevc_parse(list(segments), self.threads, False)
+
+    def reconstruct(self, parsed: list[dict], fps: float = 30.0, out_dtype=None) -> list[DecodedSegment]:
+        """GPU stage: parsed segments -> device frames (display order)."""
         for i, s in enumerate(parsed):
             if s.get("error"):
                 raise ValueError(f"HEVC segment {i}: {s['error']}")
@@ -134,7 +144,8 @@ class GpuHevcDecoder:
         for key, idxs in groups.items():
             for i, d in zip(idxs, self._decode_group(key, [parsed[i] for i in idxs], fps, out_dtype)):
                 out[i] = d
-        self.stats = {"parse_s": t1 - t0, "gpu_s": time.perf_counter() - t1, "segments_gpu": len(segments)}
+        if len(groups) > 1:
+            self.last_batch = None  # several geometries: no single [B, F] batch tensor
         return out  # type: ignore[return-value]
 
     # ------------------------------------------------------------------ internals
@@ -165,9 +176,11 @@ class GpuHevcDecoder:
                torch.zeros((B, H // 2, W // 2), dtype=torch.int16, device=dev),
                torch.zeros((B, H // 2, W // 2), dtype=torch.int16, device=dev)]
         tmp = [torch.empty_like(r) for r in res]
-        y_out = torch.empty((B, Fo, H, W), dtype=out_dtype, device=dev)
-        u_out = torch.empty((B, Fo, H // 2, W // 2), dtype=out_dtype, device=dev)
+        # display-size contiguous output: the encoder's [B, F, h, w] input
+        y_out = torch.empty((B, Fo, h, w), dtype=out_dtype, device=dev)
+        u_out = torch.empty((B, Fo, h // 2, w // 2), dtype=out_dtype, device=dev)
         v_out = torch.empty_like(u_out)
+        crop = ((cy, cy + h, cx, cx + w), (cy // 2, (cy + h) // 2, cx // 2, (cx + w) // 2))
         err = torch.zeros((1,), dtype=torch.int32, device=dev)
         stream = torch.cuda.current_stream(dev)
         s_ = stream.cuda_stream
@@ -277,8 +290,9 @@ class GpuHevcDecoder:
                 bo = bi[torch.from_numpy(sel).to(dev)]
                 co = ci[torch.from_numpy(sel).to(dev)]
                 do = torch.from_numpy(disp[sel]).to(dev)
-                for o_, p_ in zip((y_out, u_out, v_out), dpb):
-                    o_[bo, do] = p_[bo, co].to(out_dtype)
+                for k, (o_, p_) in enumerate(zip((y_out, u_out, v_out), dpb)):
+                    r0, r1, c0, c1 = crop[min(k, 1)]
+                    o_[bo, do] = p_[bo, co][:, r0:r1, c0:c1].to(out_dtype)
             if len(keep) > 64:  # bound the pinned staging held for in-flight copies
                 stream.synchronize()
                 keep.clear()
@@ -290,7 +304,6 @@ class GpuHevcDecoder:
         res_out = []
         for j in range(B):
             n = nout[j]
-            res_out.append(DecodedSegment(y_out[j, :n, cy:cy + h, cx:cx + w],
-                                          u_out[j, :n, cy // 2:(cy + h) // 2, cx // 2:(cx + w) // 2],
-                                          v_out[j, :n, cy // 2:(cy + h) // 2, cx // 2:(cx + w) // 2], fps, "gpu"))
+            res_out.append(DecodedSegment(y_out[j, :n], u_out[j, :n], v_out[j, :n], fps, "gpu"))
+        self.last_batch = (y_out, u_out, v_out)
         return res_out

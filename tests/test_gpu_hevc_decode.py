@@ -71,3 +71,30 @@ def test_gpu_hevc_decode_exerciser_streams(host):
     from govideocompressor_amd.models.hevc_decode_gpu import GpuHevcDecoder
     streams = [host.hevc_exercise(seed) for seed in range(12)]
     _check(host, streams, GpuHevcDecoder().decode(streams))
+
+
+@pytest.mark.parametrize("src", ["h264", "hevc"])
+def test_gpu_transcoder_round_trip(host, src):
+    """models/transcode.py: pieces (H.264 or HEVC) -> GPU decode -> GPU H.264 encode, three
+    pieces in batches of two (the host parse of batch 2 overlaps batch 1); every output piece
+    decodes (CPU decoder) to its input's frame count at a reasonable PSNR."""
+    from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
+    from govideocompressor_amd.models.hevc_gpu import GpuHevcEncoder, HevcParams
+    from govideocompressor_amd.models.transcode import GpuTranscoder
+    W, H, F = 192, 112, 9
+    y, u, v = synth_clip(3, F, W, H, seed=12)
+    enc = (GpuHevcEncoder(HevcParams(width=W, height=H, crf=22.0), slots=3) if src == "hevc"
+           else GpuH264Encoder(H264Params(width=W, height=H, crf=20), slots=3))
+    pieces = [r.bitstream for r in enc.encode(y, u, v, metrics=False)]
+    enc.close()
+    tc = GpuTranscoder(H264Params(width=W, height=H, crf=18.0), slots=2)
+    outs = tc.run(pieces, 30.0)
+    tc.close()
+    assert len(outs) == 3 and tc.timings["decode_s"] > 0
+    for b, o in enumerate(outs):
+        pics = host.decode(o)
+        assert len(pics) == F
+        got = np.stack([p["i420"][:W * H].reshape(H, W) for p in pics]).astype(np.float64)
+        ref = y[b].cpu().numpy().astype(np.float64)
+        mse = np.mean((got - ref) ** 2)
+        assert 10 * np.log10(255 ** 2 / max(mse, 1e-9)) > 30
