@@ -135,7 +135,7 @@ class GpuHevcDecoder:
                 raise ValueError(f"HEVC segment {i}: {s['error']}")
             if s["n"] == 0:
                 raise ValueError(f"HEVC segment {i}: no pictures")
-        out: list[DecodedSegment | None] = [None] * len(segments)
+        out: list[DecodedSegment | None] = [None] * len(parsed)
         groups: dict[tuple, list[int]] = {}
         for i, s in enumerate(parsed):
             m = s["meta"][0]
