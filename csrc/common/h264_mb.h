@@ -49,7 +49,12 @@ enum : int {
 enum : uint8_t {
   MBF_SKIP = 1,     // encoder proposes P_Skip / B_Skip
   MBF_T8x8 = 2,     // transform_size_8x8_flag
+  MBF_SUB4 = 4,     // decoder records: motion below 8x8; the per-4x4 vectors are a side-pool
+                    // entry whose index is in i4_modes[0..3] (uint32; inter MBs only)
 };
+
+// side-pool entry (int16 units): mv[list][raster 4x4][2], then ref_idx int8[list][raster 4x4]
+enum : int { kSubEntry = 80 };
 
 // 64 bytes; the first 48 (everything but the intra modes) are what the deblocking
 // filter reads.

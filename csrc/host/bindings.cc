@@ -15,6 +15,7 @@
 #include "cabac_writer.h"
 #include "cavlc_writer.h"
 #include "cpu_encoder.h"
+#include "decode_batch.h"
 #include "h264_decoder.h"
 #include "hevc_codec.h"
 #include "hevc_dec.h"
@@ -102,25 +103,7 @@ py::dict picture_to_dict(const DecodedPicture& p) {
   return d;
 }
 
-// Entropy decode of one segment for GPU reconstruction (Decoder::set_parse_only).
-struct ParsedSegment {
-  std::vector<DecodedPicture> pics;
-  std::string error;
-};
-
-ParsedSegment parse_one(const std::string& s) {
-  ParsedSegment r;
-  try {
-    Decoder dec;
-    dec.set_parse_only(true);
-    dec.decode(reinterpret_cast<const uint8_t*>(s.data()), s.size());
-    dec.flush();
-    r.pics = std::move(dec.out());
-  } catch (const std::exception& e) {
-    r.error = e.what();
-  }
-  return r;
-}
+using ParsedSegment = H264Parsed;  // decode_batch.h
 
 template <class T>
 py::array_t<T> vec_array(const std::vector<std::vector<T>*>& parts, std::vector<py::ssize_t> shape) {
@@ -131,6 +114,50 @@ py::array_t<T> vec_array(const std::vector<std::vector<T>*>& parts, std::vector<
     d += v->size();
   }
   return a;
+}
+
+// meta [P, 12] (decode order) of the parsed pictures; columns as in segment_to_dict
+py::array_t<int32_t> segment_meta(const ParsedSegment& seg) {
+  const py::ssize_t P = static_cast<py::ssize_t>(seg.pics.size());
+  py::array_t<int32_t> meta({P, static_cast<py::ssize_t>(12)});
+  int32_t* mt = meta.mutable_data();
+  for (py::ssize_t i = 0; i < P; ++i) {
+    const DecodedPicture& p = seg.pics[i];
+    const int32_t v[12] = {p.pic_id, p.ref_id, p.nal_ref, p.idr, p.slice_type, p.slice_qp, p.alpha_off, p.beta_off,
+                           p.chroma_qp_offset, p.deblock, p.gpu_ok ? 1 : 0, p.poc};
+    std::copy(v, v + 12, mt + i * 12);
+  }
+  return meta;
+}
+
+// the small tables of a parsed segment for the GPU decoder's planning (no per-MB records)
+py::dict segment_info(const ParsedSegment& seg) {
+  py::dict d;
+  d["error"] = seg.error.empty() ? py::object(py::none()) : py::object(py::str(seg.error));
+  const py::ssize_t P = static_cast<py::ssize_t>(seg.pics.size());
+  d["n"] = seg.error.empty() ? P : 0;
+  if (!seg.error.empty() || P == 0) return d;
+  const DecodedPicture& p0 = seg.pics[0];
+  d["width"] = p0.width;
+  d["height"] = p0.height;
+  d["coded_width"] = p0.coded_width;
+  d["coded_height"] = p0.coded_height;
+  d["crop_x"] = p0.crop_x;
+  d["crop_y"] = p0.crop_y;
+  bool same = true;
+  for (const DecodedPicture& p : seg.pics)
+    same = same && p.coded_width == p0.coded_width && p.coded_height == p0.coded_height &&
+           p.bs.size() == p0.blk_mask.size() * 16 && p.list_ids.size() == 64;
+  if (!same) {
+    d["error"] = std::string("resolution changes inside the segment");
+    d["n"] = 0;
+    return d;
+  }
+  d["meta"] = segment_meta(seg);
+  py::array_t<int32_t> lists({P, static_cast<py::ssize_t>(2), static_cast<py::ssize_t>(32)});
+  for (py::ssize_t i = 0; i < P; ++i) std::memcpy(lists.mutable_data() + i * 64, seg.pics[i].list_ids.data(), 64 * 4);
+  d["lists"] = lists;
+  return d;
 }
 
 py::dict segment_to_dict(ParsedSegment& seg) {
@@ -153,11 +180,13 @@ py::dict segment_to_dict(ParsedSegment& seg) {
   d["crop_y"] = p0.crop_y;
   std::vector<std::vector<uint8_t>*> hdr;
   std::vector<std::vector<uint32_t>*> mask, off;
-  std::vector<std::vector<int16_t>*> coef, mvs, wps;
-  std::vector<std::vector<int8_t>*> refs;
+  std::vector<std::vector<int16_t>*> coef, subs, wps;
   std::vector<std::vector<uint8_t>*> bss;
   std::vector<std::vector<int32_t>*> lists;
   py::array_t<int64_t> pic_off(P + 1);
+  py::array_t<int64_t> sub_off(P + 1);
+  int64_t* so = sub_off.mutable_data();
+  so[0] = 0;
   py::array_t<int32_t> meta({P, static_cast<py::ssize_t>(12)});
   int64_t* po = pic_off.mutable_data();
   int32_t* mt = meta.mutable_data();
@@ -167,14 +196,11 @@ py::dict segment_to_dict(ParsedSegment& seg) {
     DecodedPicture& p = seg.pics[i];
     same_geom = same_geom && p.coded_width == p0.coded_width && p.coded_height == p0.coded_height &&
                 static_cast<py::ssize_t>(p.blk_mask.size()) == nmb;
-    same_geom = same_geom && p.mv_l[0].size() == static_cast<size_t>(nmb) * 32 &&
-                p.mv_l[1].size() == static_cast<size_t>(nmb) * 32 && p.bs.size() == static_cast<size_t>(nmb) * 32 &&
+    same_geom = same_geom && p.bs.size() == static_cast<size_t>(nmb) * 16 &&
                 p.wp.size() == static_cast<size_t>(kWpEntries) && p.list_ids.size() == 64;
     hdr.push_back(&p.hdr);
-    mvs.push_back(&p.mv_l[0]);
-    mvs.push_back(&p.mv_l[1]);
-    refs.push_back(&p.ref_l[0]);
-    refs.push_back(&p.ref_l[1]);
+    subs.push_back(&p.sub);
+    so[i + 1] = so[i] + static_cast<int64_t>(p.sub.size() / kSubEntry);
     bss.push_back(&p.bs);
     lists.push_back(&p.list_ids);
     wps.push_back(&p.wp);
@@ -206,9 +232,9 @@ py::dict segment_to_dict(ParsedSegment& seg) {
   d["coef"] = vec_array<int16_t>(coef, {static_cast<py::ssize_t>(po[P] * 16)});
   d["pic_off"] = pic_off;
   d["meta"] = meta;
-  d["mv"] = vec_array<int16_t>(mvs, {P, 2, nmb, 16, 2});
-  d["ref"] = vec_array<int8_t>(refs, {P, 2, nmb, 16});
-  d["bs"] = vec_array<uint8_t>(bss, {P, nmb, 32});
+  d["sub"] = vec_array<int16_t>(subs, {static_cast<py::ssize_t>(so[P] * kSubEntry)});
+  d["sub_off"] = sub_off;
+  d["bs"] = vec_array<uint8_t>(bss, {P, nmb, 16});
   d["lists"] = vec_array<int32_t>(lists, {P, 2, 32});
   d["wp"] = vec_array<int16_t>(wps, {P, static_cast<py::ssize_t>(kWpEntries)});
   return d;
@@ -552,23 +578,59 @@ PYBIND11_MODULE(_host, m) {
         // entropy decode only (CAVLC -> MbHeader + packed levels), one thread per segment
         std::vector<std::string> in;
         for (const py::bytes& b : segments) in.emplace_back(b);
-        std::vector<ParsedSegment> res(in.size());
+        std::vector<ParsedSegment> res;
         {
           py::gil_scoped_release rel;
-          std::atomic<size_t> next{0};
-          int nt = std::max(1, std::min<int>(threads, static_cast<int>(in.size())));
-          std::vector<std::thread> pool;
-          for (int t = 0; t < nt; ++t)
-            pool.emplace_back([&] {
-              for (size_t i = next++; i < in.size(); i = next++) res[i] = parse_one(in[i]);
-            });
-          for (std::thread& th : pool) th.join();
+          res = h264_parse_many(in, threads);
         }
         py::list out;
         for (ParsedSegment& r : res) out.append(segment_to_dict(r));
         return out;
       },
       py::arg("segments"), py::arg("threads") = 1);
+
+  // parsed batch kept in C++ (models/h264_decode_gpu.py): info(i) for planning, layout / pack
+  // of one picture step straight into a pinned host buffer
+  py::class_<H264Batch>(m, "H264Batch")
+      .def("__len__", [](const H264Batch& b) { return b.segs.size(); })
+      .def("info", [](const H264Batch& b, int i) { return segment_info(b.segs.at(i)); })
+      .def("segment", [](H264Batch& b, int i) { return segment_to_dict(b.segs.at(i)); })
+      .def("layout",
+           [](const H264Batch& b, int t, const std::vector<int>& slots, int nmb) {
+             H264StepLayout L = b.layout(t, slots, nmb);
+             py::dict d;
+             d["hdr"] = L.hdr;
+             d["mask"] = L.mask;
+             d["off"] = L.off;
+             d["bs"] = L.bs;
+             d["wp"] = L.wp;
+             d["coef"] = L.coef;
+             d["sub"] = L.sub;
+             d["total"] = L.total;
+             return d;
+           })
+      .def("pack",
+           [](const H264Batch& b, int t, const std::vector<int>& slots, int nmb, uintptr_t dst, size_t capacity,
+              int threads) {
+             H264StepLayout L = b.layout(t, slots, nmb);
+             if (L.total > capacity) throw std::invalid_argument("H264Batch.pack: buffer too small");
+             py::gil_scoped_release rel;
+             b.pack(t, slots, nmb, reinterpret_cast<uint8_t*>(dst), threads);
+           },
+           py::arg("t"), py::arg("slots"), py::arg("nmb"), py::arg("dst"), py::arg("capacity"), py::arg("threads") = 4);
+  m.def(
+      "parse_batch",
+      [](const std::vector<py::bytes>& segments, int threads) {
+        std::vector<std::string> in;
+        for (const py::bytes& b : segments) in.emplace_back(b);
+        auto* batch = new H264Batch();
+        {
+          py::gil_scoped_release rel;
+          batch->segs = h264_parse_many(in, threads);
+        }
+        return batch;
+      },
+      py::arg("segments"), py::arg("threads") = 1, py::return_value_policy::take_ownership);
 
   // ---------------------------------------------------------------- HEVC
   m.def("hevc_parameter_sets", [](const py::dict& cfg) { return to_bytes(hevc::hevc_parameter_sets(hevc_cfg_from(cfg))); });

@@ -64,6 +64,7 @@ struct Pic {
   std::vector<uint8_t> rec_hdr;  // parse-only records
   std::vector<int16_t> rec_coef;
   std::vector<uint32_t> rec_mask, rec_off;
+  std::vector<int16_t> rec_sub;  // parse-only: kSubEntry int16 per MB with sub-8x8 motion
   bool gpu_ok = true;
   int nslices = 0;
   int slice_qp = 0;
@@ -110,8 +111,21 @@ struct Pic {
     rec_off.assign(n, 0);
     rec_coef.clear();
     rec_coef.reserve(n * 64);
+    rec_sub.clear();
   }
   int px(int x, int y) const { return Y[static_cast<size_t>(y) * W + x]; }
+  // back to the default state, keeping the vectors' storage (picture pool)
+  void reset_scalars() {
+    frame_num = frame_num_wrap = poc = idr = slice_type = id = nal_ref = 0;
+    short_ref = long_ref = false;
+    long_idx = -1;
+    mmco5 = false;
+    gpu_ok = true;
+    nslices = 0;
+    slice_qp = 0;
+    list_ids.clear();
+    wp.clear();
+  }
 };
 using PicPtr = std::shared_ptr<Pic>;
 
@@ -400,7 +414,7 @@ struct Decoder::Impl {
       pending.erase(pending.begin());
     }
   }
-  void fill_common(DecodedPicture& d, const Pic& p) const {
+  void fill_common(DecodedPicture& d, const Pic& p, bool side_info = true) const {
     d.coded_width = p.W;
     d.coded_height = p.H;
     d.crop_x = crop[0] * 2;
@@ -411,6 +425,7 @@ struct Decoder::Impl {
     d.poc = p.poc;
     d.idr = p.idr;
     d.slice_type = p.slice_type;
+    if (!side_info) return;
     d.mb_kind = p.kind;
     d.mb_qp = p.qp;
     d.mv = p.mv[0];
@@ -432,7 +447,7 @@ struct Decoder::Impl {
     if (!skip_deblock && !parse_only) deblock_picture();
     if (parse_only) {
       DecodedPicture d;
-      fill_common(d, *cur);
+      fill_common(d, *cur, false);
       d.hdr = std::move(cur->rec_hdr);
       d.coef = std::move(cur->rec_coef);
       d.blk_mask = std::move(cur->rec_mask);
@@ -449,10 +464,7 @@ struct Decoder::Impl {
       for (const SliceParams& sp2 : slices) ok = ok && sp2.cb_off == sp2.cr_off && sp2.disable_idc != 2;
       d.gpu_ok = ok;
       d.poc = cur->poc;
-      for (int l = 0; l < 2; ++l) {
-        d.mv_l[l] = cur->mv[l];
-        d.ref_l[l] = cur->ref[l];
-      }
+      d.sub = std::move(cur->rec_sub);
       d.list_ids = cur->list_ids.empty() ? std::vector<int32_t>(64, -1) : cur->list_ids;
       d.wp = cur->wp.empty() ? std::vector<int16_t>(kWpEntries, 0) : cur->wp;
       d.bs = boundary_strengths();
@@ -593,8 +605,22 @@ struct Decoder::Impl {
     return exp + h.delta_poc[0];
   }
 
+  // pictures nobody holds any more are reused: their per-MB arrays keep their storage
+  // (no allocation + page faults for ~13 MB of side info per 4K picture)
+  std::vector<PicPtr> pic_pool;
+  PicPtr new_pic() {
+    for (PicPtr& p : pic_pool)
+      if (p.use_count() == 1) {
+        p->reset_scalars();
+        return p;
+      }
+    auto p = std::make_shared<Pic>();
+    if (pic_pool.size() < 40) pic_pool.push_back(p);
+    return p;
+  }
+
   void start_picture(const SliceHeader& h) {
-    cur = std::make_shared<Pic>();
+    cur = new_pic();
     cur->init(sp->width_mbs, sp->height_mbs, !parse_only);
     if (parse_only) cur->init_records();
     cur->slice_qp = h.qp;
@@ -794,19 +820,16 @@ struct Decoder::Impl {
 
   void begin_mb(int addr) {
     cur->slice[addr] = slice_idx;
-    for (int i = 0; i < 16; ++i) blk_done[i] = 0;
-    for (int l = 0; l < 2; ++l)
-      for (int i = 0; i < 16; ++i) {
-        cur->ref[l][addr * 16 + i] = -1;
-        cur->refpic[l][addr * 16 + i] = -1;
-        cur->mv[l][addr * 32 + 2 * i] = cur->mv[l][addr * 32 + 2 * i + 1] = 0;
-        cur->mvd[l][addr * 32 + 2 * i] = cur->mvd[l][addr * 32 + 2 * i + 1] = 0;
-      }
-    for (int i = 0; i < 16; ++i) {
-      cur->nz[addr * 16 + i] = 0;
-      cur->i4[addr * 16 + i] = 2;
+    std::memset(blk_done, 0, sizeof(blk_done));
+    for (int l = 0; l < 2; ++l) {
+      std::memset(&cur->ref[l][addr * 16], 0xFF, 16);
+      std::memset(&cur->refpic[l][addr * 16], 0xFF, 16 * sizeof(int));
+      std::memset(&cur->mv[l][addr * 32], 0, 32 * sizeof(int16_t));
+      std::memset(&cur->mvd[l][addr * 32], 0, 32);
     }
-    for (int i = 0; i < 24; ++i) cur->tc[addr * 24 + i] = 0;
+    std::memset(&cur->nz[addr * 16], 0, 16);
+    std::memset(&cur->i4[addr * 16], 2, 16);
+    std::memset(&cur->tc[addr * 24], 0, 24);
     cur->cbf_luma[addr] = 0;
     cur->cbf_dc[addr] = 0;
     cur->cbf_cac0[addr] = cur->cbf_cac1[addr] = 0;
@@ -919,7 +942,10 @@ struct Decoder::Impl {
       for (int i = 0; i < 16; ++i) blk_done[i] = blk_tmp[i];
       bool zero_pred = refs[0] < 0 && refs[1] < 0;
       const Pic& col = *list[1][0];
-      for (int r = 0; r < 16; ++r) {
+      // direct_8x8_inference: every 4x4 of a quadrant takes the quadrant's corner co-located
+      // block, so the derivation runs once per quadrant on a 2x2 block group
+      const int step = sp->direct_8x8_inference ? 2 : 1;
+      for (int r = 0; r < 16; r += (step == 2 && (r & 3) == 2) ? 6 : step) {
         int q = ((r & 3) >> 1) + 2 * ((r >> 2) >> 1);
         if (!((quads >> q) & 1)) continue;
         int mvc[2], refc, rpc;
@@ -927,23 +953,24 @@ struct Decoder::Impl {
         bool col_zero = !col.long_ref && refc == 0 && std::abs(mvc[0]) <= 1 && std::abs(mvc[1]) <= 1;
         for (int l = 0; l < 2; ++l) {
           if (zero_pred) {
-            assign(addr, l, r & 3, r >> 2, 1, 1, 0, 0, 0);
+            assign(addr, l, r & 3, r >> 2, step, step, 0, 0, 0);
             continue;
           }
           int ref = refs[l];
           if (ref < 0) {
-            assign(addr, l, r & 3, r >> 2, 1, 1, -1, 0, 0);
+            assign(addr, l, r & 3, r >> 2, step, step, -1, 0, 0);
             continue;
           }
-          if (ref == 0 && col_zero) assign(addr, l, r & 3, r >> 2, 1, 1, 0, 0, 0);
-          else assign(addr, l, r & 3, r >> 2, 1, 1, ref, pmv[l][0], pmv[l][1]);
+          if (ref == 0 && col_zero) assign(addr, l, r & 3, r >> 2, step, step, 0, 0, 0);
+          else assign(addr, l, r & 3, r >> 2, step, step, ref, pmv[l][0], pmv[l][1]);
         }
       }
       return;
     }
     // 8.4.1.2.3 temporal
     const Pic& p1 = *list[1][0];
-    for (int r = 0; r < 16; ++r) {
+    const int step = sp->direct_8x8_inference ? 2 : 1;  // as in the spatial case
+    for (int r = 0; r < 16; r += (step == 2 && (r & 3) == 2) ? 6 : step) {
       int q = ((r & 3) >> 1) + 2 * ((r >> 2) >> 1);
       if (!((quads >> q) & 1)) continue;
       int mvc[2], refc, rpc;
@@ -973,8 +1000,8 @@ struct Decoder::Impl {
           mv1[c] = mv0[c] - mvc[c];
         }
       }
-      assign(addr, 0, r & 3, r >> 2, 1, 1, ref0, mv0[0], mv0[1]);
-      assign(addr, 1, r & 3, r >> 2, 1, 1, 0, mv1[0], mv1[1]);
+      assign(addr, 0, r & 3, r >> 2, step, step, ref0, mv0[0], mv0[1]);
+      assign(addr, 1, r & 3, r >> 2, step, step, 0, mv1[0], mv1[1]);
     }
   }
 
@@ -1023,14 +1050,39 @@ struct Decoder::Impl {
     h.chroma_mode = static_cast<uint8_t>(chroma_mode);
     h.flags = static_cast<uint8_t>(t8 ? MBF_T8x8 : 0);
     h.sub_direct = cur->direct[addr];
+    bool quad_uniform = true;
     for (int l = 0; l < 2; ++l)
       for (int q = 0; q < 4; ++q) {
         int r0 = (q & 1) * 2 + (q >> 1) * 8;  // top-left 4x4 block of quadrant q
-        h.mv[l][q][0] = cur->mv[l][addr * 32 + 2 * r0];
-        h.mv[l][q][1] = cur->mv[l][addr * 32 + 2 * r0 + 1];
-        h.ref[l][q] = cur->ref[l][addr * 16 + r0];  // sub-8x8 motion: DecodedPicture::mv_l
+        const int16_t* m0 = &cur->mv[l][addr * 32 + 2 * r0];
+        const int8_t* f0 = &cur->ref[l][addr * 16 + r0];
+        h.mv[l][q][0] = m0[0];
+        h.mv[l][q][1] = m0[1];
+        h.ref[l][q] = f0[0];
+        for (int k = 1; k < 4; ++k) {
+          int dr = (k & 1) + 4 * (k >> 1);
+          quad_uniform = quad_uniform && f0[dr] == f0[0] && m0[2 * dr] == m0[0] && m0[2 * dr + 1] == m0[1];
+        }
       }
     for (int b = 0; b < 16; ++b) h.i4_modes[b] = static_cast<uint8_t>(i4modes ? i4modes[b] : 2);
+    if (!quad_uniform && !mbk_is_intra(kind)) {
+      // motion below 8x8: the whole MB's vectors go to the side pool, i4_modes[0..3] (unused
+      // by inter MBs) hold the entry index
+      h.flags |= MBF_SUB4;
+      uint32_t idx = static_cast<uint32_t>(cur->rec_sub.size() / kSubEntry);
+      std::memcpy(h.i4_modes, &idx, 4);
+      size_t b0 = cur->rec_sub.size();
+      cur->rec_sub.resize(b0 + kSubEntry);
+      int16_t* e = cur->rec_sub.data() + b0;
+      for (int l = 0; l < 2; ++l)
+        for (int r = 0; r < 16; ++r) {
+          e[(l * 16 + r) * 2] = cur->mv[l][addr * 32 + 2 * r];
+          e[(l * 16 + r) * 2 + 1] = cur->mv[l][addr * 32 + 2 * r + 1];
+        }
+      int8_t* rf = reinterpret_cast<int8_t*>(e + 64);
+      for (int l = 0; l < 2; ++l)
+        for (int r = 0; r < 16; ++r) rf[l * 16 + r] = cur->ref[l][addr * 16 + r];
+    }
     std::memcpy(cur->rec_hdr.data() + static_cast<size_t>(addr) * sizeof(MbHeader), &h, sizeof(MbHeader));
   }
 
@@ -1194,7 +1246,7 @@ struct Decoder::Impl {
 
   // residual_block_cavlc (7.3.5.3.2); writes coefficient levels into lv[start..end]
   int read_block(BitReader& br, int* lv, int start, int end, int max_num, int nc) {
-    for (int i = 0; i < max_num; ++i) lv[i] = 0;
+    for (int i = 0; i < std::max(max_num, end + 1); ++i) lv[i] = 0;  // lv[start..end] written below
     int tc, t1;
     if (nc == -1) {
       int k = read_vlc(br, kChromaDcCoeffTokenLen, kChromaDcCoeffTokenBits, 20);
@@ -2054,11 +2106,15 @@ struct Decoder::Impl {
     cur->qp[addr] = static_cast<int8_t>(qp);
     cur->qp_dbk[addr] = static_cast<int8_t>(qp);
     // ---- residual syntax
-    std::memset(s.lum, 0, sizeof(s.lum));
-    std::memset(s.lum8, 0, sizeof(s.lum8));
-    std::memset(s.lumdc, 0, sizeof(s.lumdc));
-    std::memset(s.cdc, 0, sizeof(s.cdc));
-    std::memset(s.cac, 0, sizeof(s.cac));
+    if (!parse_only) {
+      // the parse-only path reads only the blocks the coded_block_pattern codes (every coded
+      // block is written whole by the residual parse), so it skips these 2.6 KB of clears
+      std::memset(s.lum, 0, sizeof(s.lum));
+      std::memset(s.lum8, 0, sizeof(s.lum8));
+      std::memset(s.lumdc, 0, sizeof(s.lumdc));
+      std::memset(s.cdc, 0, sizeof(s.cdc));
+      std::memset(s.cac, 0, sizeof(s.cac));
+    }
     for (int i = 0; i < 16; ++i) blk_done[i] = 1;  // for neighbour lookups inside the MB
     if (cabac) parse_residual_cabac(addr, kind, s);
     else parse_residual_cavlc(br, addr, kind, s);
@@ -2066,13 +2122,15 @@ struct Decoder::Impl {
     if (s.t8x8) {
       for (int b8 = 0; b8 < 4; ++b8) {
         bool any = false;
-        for (int i = 0; i < 64; ++i) any |= s.lum8[b8][i] != 0;
+        if (cbp_luma & (1 << b8))
+          for (int i = 0; i < 64; ++i) any |= s.lum8[b8][i] != 0;
         for (int k = 0; k < 4; ++k) cur->nz[addr * 16 + (b8 & 1) * 2 + (k & 1) + 4 * ((b8 >> 1) * 2 + (k >> 1))] = any;
       }
     } else {
       for (int blk = 0; blk < 16; ++blk) {
         bool any = false;
-        for (int i = 0; i < 16; ++i) any |= s.lum[blk][i] != 0;
+        if (cbp_luma & (1 << (blk >> 2)))
+          for (int i = 0; i < 16; ++i) any |= s.lum[blk][i] != 0;
         if (kind == MBK_I16x16) any |= s.lumdc[blk] != 0;  // not used for bS (intra), informative
         cur->nz[addr * 16 + kBlkX[blk] + 4 * kBlkY[blk]] = any;
       }
@@ -2275,18 +2333,24 @@ struct Decoder::Impl {
       if (v2)
         for (int i = 0; i < n; ++i) cur->rec_coef[b + n + i] = static_cast<int16_t>(v2[i]);
     };
+    // only the blocks the coded_block_pattern codes are read (decode_mb leaves the others
+    // uncleared in parse-only mode)
+    const int cbp_luma = s.cbp & 15, cbp_chroma = s.cbp >> 4;
     if (s.t8x8) {
       // 8x8 levels as 16-level chunks: chunk blk = b8 * 4 + k holds levels 16k..16k+15 of
       // 8x8 block b8, i.e. the record layout (COEF_LUMA + b8 * 64).  The GPU path reads
       // 8x8 transform (decode.hip inverse8x8).
-      for (int blk = 0; blk < 16; ++blk) put(blk, s.lum8[blk >> 2] + 16 * (blk & 3), 16, nullptr);
+      for (int blk = 0; blk < 16; ++blk)
+        if (cbp_luma & (1 << (blk >> 2))) put(blk, s.lum8[blk >> 2] + 16 * (blk & 3), 16, nullptr);
     } else {
-      for (int blk = 0; blk < 16; ++blk) put(blk, s.lum[blk], 16, nullptr);
+      for (int blk = 0; blk < 16; ++blk)
+        if (cbp_luma & (1 << (blk >> 2))) put(blk, s.lum[blk], 16, nullptr);
     }
     if (kind == MBK_I16x16) put(16, s.lumdc, 16, nullptr);
-    put(17, s.cdc[0], 4, s.cdc[1]);
-    for (int cc = 0; cc < 2; ++cc)
-      for (int b = 0; b < 4; ++b) put(18 + cc * 4 + b, s.cac[cc][b], 16, nullptr);
+    if (cbp_chroma) put(17, s.cdc[0], 4, s.cdc[1]);
+    if (cbp_chroma & 2)
+      for (int cc = 0; cc < 2; ++cc)
+        for (int b = 0; b < 4; ++b) put(18 + cc * 4 + b, s.cac[cc][b], 16, nullptr);
     cur->rec_mask[addr] = mask;
     if (kind == MBK_IPCM) cur->gpu_ok = false;  // I_PCM samples are not carried by the records
     store_record(addr, kind, s.cbp, qp, s.i16_mode, s.chroma_mode, (kind == MBK_I4x4 || kind == MBK_I8x8) ? s.i4 : nullptr,
@@ -2461,10 +2525,14 @@ struct Decoder::Impl {
 
   // parse-only: boundary strength of every filtered edge segment (deblock.hip reads these
   // instead of deriving them, so reference identity across lists / multi-reference and
-  // 8x8-transform edges follow the decoder exactly); 0 = not filtered
+  // 8x8-transform edges follow the decoder exactly); 0 = not filtered.  Packed 4 bits per
+  // segment: [mb][16] bytes, segment i = dir * 16 + edge * 4 + k in byte i / 2 (low nibble
+  // for even i).
   std::vector<uint8_t> boundary_strengths() {
     int nmb = cur->wmb * cur->hmb;
-    std::vector<uint8_t> out(static_cast<size_t>(nmb) * 32, 0);
+    std::vector<uint8_t> out(static_cast<size_t>(nmb) * 16, 0);
+    flat_.resize(nmb);
+    for (int a = 0; a < nmb; ++a) flat_[a] = !is_intra(a) && no_nz(a) && one_motion(a);
     for (int addr = 0; addr < nmb; ++addr) {
       if (cur->slice[addr] < 0) continue;
       const SliceParams& spar = slices[cur->slice[addr]];
@@ -2473,20 +2541,59 @@ struct Decoder::Impl {
       bool left = mx > 0 && !(spar.disable_idc == 2 && cur->slice[addr - 1] != cur->slice[addr]);
       bool top = my > 0 && !(spar.disable_idc == 2 && cur->slice[addr - cur->wmb] != cur->slice[addr]);
       bool t8 = cur->t8x8[addr] != 0;
+      const bool iq = is_intra(addr);
+      // internal edges of an inter MB with one motion for all 16 blocks and no coded luma
+      // block have bS 0 (8.7.2.1), as do the 4 segments of an MB edge between two such MBs
+      // with the same motion
+      const bool flat_q = flat_[addr] != 0;
+      uint8_t* o = &out[static_cast<size_t>(addr) * 16];
+      auto put = [&](int i, int v) { o[i >> 1] |= static_cast<uint8_t>(v << ((i & 1) * 4)); };
       for (int dir = 0; dir < 2; ++dir)
         for (int e = 0; e < 4; ++e) {
           if (e == 0 && !(dir == 0 ? left : top)) continue;
           if (t8 && (e & 1)) continue;
+          if (e > 0 && flat_q) continue;
+          const int base = dir * 16 + e * 4;
           int mbp = e == 0 ? (dir == 0 ? addr - 1 : addr - cur->wmb) : addr;
+          if (iq || (e == 0 && is_intra(mbp))) {
+            for (int k = 0; k < 4; ++k) put(base + k, e == 0 ? 4 : 3);
+            continue;
+          }
+          if (e == 0 && flat_q && flat_[mbp] && same_motion(mbp, addr)) continue;
           for (int k = 0; k < 4; ++k) {
             int blkq = dir == 0 ? (e + 4 * k) : (k + 4 * e);
             int blkp = dir == 0 ? (e == 0 ? 3 + 4 * k : e - 1 + 4 * k) : (e == 0 ? k + 12 : k + 4 * (e - 1));
-            out[static_cast<size_t>(addr) * 32 + dir * 16 + e * 4 + k] =
-                static_cast<uint8_t>(bs_of(mbp, blkp, addr, blkq, e == 0));
+            put(base + k, bs_of(mbp, blkp, addr, blkq, e == 0));
           }
         }
     }
     return out;
+  }
+  std::vector<uint8_t> flat_;  // boundary_strengths: inter MB, no coded luma, one motion
+  bool no_nz(int a) const {
+    uint64_t w0, w1;
+    std::memcpy(&w0, &cur->nz[a * 16], 8);
+    std::memcpy(&w1, &cur->nz[a * 16 + 8], 8);
+    return (w0 | w1) == 0;
+  }
+  // all 16 blocks share each list's picture and vector
+  bool one_motion(int a) const {
+    for (int l = 0; l < 2; ++l) {
+      const int* rp = &cur->refpic[l][a * 16];
+      const int16_t* m = &cur->mv[l][a * 32];
+      for (int r = 1; r < 16; ++r)
+        if (rp[r] != rp[0] || m[2 * r] != m[0] || m[2 * r + 1] != m[1]) return false;
+    }
+    return true;
+  }
+  // block 0 of MBs a and b reference the same pictures with the same vectors, per list
+  bool same_motion(int a, int b) const {
+    for (int l = 0; l < 2; ++l) {
+      if (cur->refpic[l][a * 16] != cur->refpic[l][b * 16]) return false;
+      if (cur->refpic[l][a * 16] < 0) continue;
+      if (cur->mv[l][a * 32] != cur->mv[l][b * 32] || cur->mv[l][a * 32 + 1] != cur->mv[l][b * 32 + 1]) return false;
+    }
+    return true;
   }
 
   // ------------------------------------------------------------ deblocking (8.7)

@@ -54,9 +54,11 @@ struct DecodedPicture {
   bool gpu_ok = true;                 // false: a feature the GPU path does not cover (I_PCM,
                                       // Intra8x8, several slices, constrained intra, mmco5 ...)
   // parse-only motion / filter side info for GPU reconstruction of P and B pictures
-  std::vector<int16_t> mv_l[2];       // [mb][16 raster 4x4][2] quarter-sample MV per list
-  std::vector<int8_t> ref_l[2];       // [mb][16] ref_idx per list (-1 = list unused)
-  std::vector<uint8_t> bs;            // [mb][32] boundary strength: dir * 16 + edge * 4 + segment
+  // (per-8x8 quadrant motion is in hdr; MBs with smaller partitions carry MBF_SUB4 and a
+  // kSubEntry side-pool entry, csrc/common/h264_mb.h)
+  std::vector<int16_t> sub;           // side pool, kSubEntry int16 per MBF_SUB4 macroblock
+  std::vector<uint8_t> bs;            // [mb][16] boundary strength, 4 bits per segment
+                                      // i = dir * 16 + edge * 4 + k (byte i / 2, low nibble even i)
   std::vector<int32_t> list_ids;      // [2][32] decode-order picture id of RefPicList0/1[i], -1
   std::vector<int16_t> wp;            // kWpEntries: weighted-prediction table (see kWp* below)
   // copy the cropped planes out as one contiguous I420 frame

@@ -60,12 +60,12 @@ void mivc_launch_deblock(int B, int wmb, int hmb, uint8_t* rec_y, uint8_t* rec_u
                          const uint8_t* nz, int chroma_qp_offset, int alpha_off, int beta_off, int* err,
                          void* stream);
 void mivc_launch_decode_picture_dpb(int B, int wmb, int hmb, int dpb_n, uint8_t* dpb_y, uint8_t* dpb_u, uint8_t* dpb_v,
-                                    const int8_t* cur_idx, const int8_t* reftab, const int16_t* wp, const int16_t* mv,
-                                    const int8_t* refidx, const void* hdr, const uint32_t* mask, const uint32_t* off,
+                                    const int16_t* cur_idx, const int16_t* reftab, const int16_t* wp, const int16_t* sub,
+                                    const void* hdr, const uint32_t* mask, const uint32_t* off,
                                     const int16_t* coef, const int8_t* run, int any_inter, int chroma_qp_offset,
                                     uint8_t* nz, int* err, void* stream);
 void mivc_launch_deblock_dpb(int B, int wmb, int hmb, int dpb_n, uint8_t* dpb_y, uint8_t* dpb_u, uint8_t* dpb_v,
-                             const int8_t* cur_idx, const void* hdr, const uint8_t* nz, const uint8_t* bs,
+                             const int16_t* cur_idx, const void* hdr, const uint8_t* nz, const uint8_t* bs,
                              int chroma_qp_offset, int alpha_off, int beta_off, int* err, void* stream);
 int mivc_launch_scale(const void* in, int w, int h, long long in_stride, long long in_pitch, void* out, int ow, int oh,
                       int W, int H, long long out_stride, long long out_pitch, int nframes, const int* fx,
@@ -248,20 +248,20 @@ PYBIND11_MODULE(_hip, m) {
                         cqo, alpha_off, beta_off, P<int>(err), S(stream));
   });
   m.def("decode_picture_dpb", [](int B, int wmb, int hmb, int dpb_n, uintptr_t y, uintptr_t u, uintptr_t v,
-                                 uintptr_t cur_idx, uintptr_t reftab, uintptr_t wp, uintptr_t mv, uintptr_t refidx,
+                                 uintptr_t cur_idx, uintptr_t reftab, uintptr_t wp, uintptr_t sub,
                                  uintptr_t hdr, uintptr_t mask, uintptr_t off, uintptr_t coef, uintptr_t run,
                                  int any_inter, int cqo, uintptr_t nz, uintptr_t err, uintptr_t stream) {
-    if (dpb_n < 1 || dpb_n > 32) throw std::invalid_argument("decode_picture_dpb: dpb_n must be 1..32");
-    mivc_launch_decode_picture_dpb(B, wmb, hmb, dpb_n, P<uint8_t>(y), P<uint8_t>(u), P<uint8_t>(v), P<int8_t>(cur_idx),
-                                   P<int8_t>(reftab), P<int16_t>(wp), P<int16_t>(mv), P<int8_t>(refidx), P<void>(hdr),
+    if (dpb_n < 1 || dpb_n > 32767) throw std::invalid_argument("decode_picture_dpb: dpb_n must be 1..32767");
+    mivc_launch_decode_picture_dpb(B, wmb, hmb, dpb_n, P<uint8_t>(y), P<uint8_t>(u), P<uint8_t>(v), P<int16_t>(cur_idx),
+                                   P<int16_t>(reftab), P<int16_t>(wp), P<int16_t>(sub), P<void>(hdr),
                                    P<uint32_t>(mask), P<uint32_t>(off), P<int16_t>(coef), P<int8_t>(run), any_inter,
                                    cqo, P<uint8_t>(nz), P<int>(err), S(stream));
   });
   m.def("deblock_dpb", [](int B, int wmb, int hmb, int dpb_n, uintptr_t y, uintptr_t u, uintptr_t v, uintptr_t cur_idx,
                           uintptr_t hdr, uintptr_t nz, uintptr_t bs, int cqo, int alpha_off, int beta_off, uintptr_t err,
                           uintptr_t stream) {
-    if (dpb_n < 1 || dpb_n > 32) throw std::invalid_argument("deblock_dpb: dpb_n must be 1..32");
-    mivc_launch_deblock_dpb(B, wmb, hmb, dpb_n, P<uint8_t>(y), P<uint8_t>(u), P<uint8_t>(v), P<int8_t>(cur_idx),
+    if (dpb_n < 1 || dpb_n > 32767) throw std::invalid_argument("deblock_dpb: dpb_n must be 1..32767");
+    mivc_launch_deblock_dpb(B, wmb, hmb, dpb_n, P<uint8_t>(y), P<uint8_t>(u), P<uint8_t>(v), P<int16_t>(cur_idx),
                             P<void>(hdr), P<uint8_t>(nz), P<uint8_t>(bs), cqo, alpha_off, beta_off, P<int>(err),
                             S(stream));
   });

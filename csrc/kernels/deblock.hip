@@ -30,7 +30,7 @@ struct DeblockArgs {
   // (rec_* = [B][dpb_n] pictures, filtering picture cur_idx[slot]; dpb_n 0: [B] pictures)
   const uint8_t* bs_in;
   int dpb_n;
-  const int8_t* cur_idx;
+  const int16_t* cur_idx;
 };
 
 constexpr int kDeblockWaves = 16;
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(64 * kDeblockWaves) void deblock_wavefront(DeblockA
   uint8_t* recy = a.rec_y + pic * g.ysize();
   uint8_t* const rcu = a.rec_u + pic * g.csize();
   uint8_t* const rcv = a.rec_v + pic * g.csize();
-  const uint8_t* bs_in = a.bs_in ? a.bs_in + static_cast<size_t>(slot) * g.nmb() * 32 : nullptr;
+  const uint8_t* bs_in = a.bs_in ? a.bs_in + static_cast<size_t>(slot) * g.nmb() * 16 : nullptr;
   auto recc = [&](int c) { return c ? rcv : rcu; };
   const uint32_t* hdr32 = reinterpret_cast<const uint32_t*>(a.hdr) + static_cast<size_t>(slot) * g.nmb() * 16;
   const uint32_t* nz32 = reinterpret_cast<const uint32_t*>(a.nz) + static_cast<size_t>(slot) * g.nmb() * 4;
@@ -229,7 +229,8 @@ __global__ __launch_bounds__(64 * kDeblockWaves) void deblock_wavefront(DeblockA
           int bs = 0;
           const bool mbedge = e == 0;
           if (bs_in) {
-            bs = bs_in[(static_cast<size_t>(y) * wmb + x) * 32 + hl];
+            // 4 bits per segment (h264_decoder.h DecodedPicture::bs)
+            bs = (bs_in[(static_cast<size_t>(y) * wmb + x) * 16 + (hl >> 1)] >> ((hl & 1) * 4)) & 15;
           } else if (!mbedge || (dir == 0 ? has_left : has_top)) {
             const int pw = mbedge ? (dir == 0 ? 1 : 2) : 0;
             const MbHeader* HP = reinterpret_cast<const MbHeader*>(S.hdrw[pw]);
@@ -468,7 +469,7 @@ extern "C" void mivc_launch_deblock(int B, int wmb, int hmb, uint8_t* rec_y, uin
 
 // decoder: filter picture cur_idx[slot] of each slot's DPB with the parser's boundary strengths
 extern "C" void mivc_launch_deblock_dpb(int B, int wmb, int hmb, int dpb_n, uint8_t* dpb_y, uint8_t* dpb_u,
-                                        uint8_t* dpb_v, const int8_t* cur_idx, const void* hdr, const uint8_t* nz,
+                                        uint8_t* dpb_v, const int16_t* cur_idx, const void* hdr, const uint8_t* nz,
                                         const uint8_t* bs, int chroma_qp_offset, int alpha_off, int beta_off, int* err,
                                         void* stream) {
   DeblockArgs a;

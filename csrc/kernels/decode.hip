@@ -44,11 +44,13 @@ struct DecodeArgs {
   int* err;
   // rec_* point at the per-slot decoded picture buffers, [B][dpb_n] pictures
   int dpb_n;
-  const int8_t* cur_idx;   // [B] DPB index of the picture being decoded
-  const int8_t* reftab;    // [B][2][32] DPB index of RefPicListX[i] (-1: none)
+  const int16_t* cur_idx;  // [B] DPB index of the picture being decoded
+  const int16_t* reftab;   // [B][2][32] DPB index of RefPicListX[i] (-1: none)
   const int16_t* wp;       // [B][kWpEntries] weighted-prediction tables (h264_decoder.h)
-  const int16_t* mv;       // [B][2][nmb][16][2] quarter-sample vectors per raster 4x4 block
-  const int8_t* refidx;    // [B][2][nmb][16] ref_idx per raster 4x4 block, -1 = list unused
+  // motion: per 8x8 quadrant in the MbHeader; MBF_SUB4 macroblocks (partitions below 8x8)
+  // read their per-4x4 vectors / ref_idx from side-pool entry i4_modes[0..3] of `sub`
+  // (h264::kSubEntry int16 per entry, indices already global to the batch step)
+  const int16_t* sub;
 };
 
 // weighted-prediction table layout (mirrors mivc::h264::kWp* in h264_decoder.h)
@@ -197,12 +199,22 @@ __global__ __launch_bounds__(64) void decode_inter_dpb(DecodeArgs a) {
   const bool t8 = (H->flags & h264::MBF_T8x8) != 0;
   const int D = a.dpb_n;
   const int nmb = g.nmb();
-  const int16_t* mvp = a.mv + static_cast<size_t>(slot) * 2 * nmb * 32;
-  const int8_t* rip = a.refidx + static_cast<size_t>(slot) * 2 * nmb * 16;
-  const int8_t* rt = a.reftab + slot * 64;
+  const int16_t* rt = a.reftab + slot * 64;
+  const bool sub4 = (H->flags & h264::MBF_SUB4) != 0;
+  const int16_t* se = nullptr;
+  if (sub4) {
+    uint32_t si;
+    __builtin_memcpy(&si, H->i4_modes, 4);
+    se = a.sub + static_cast<size_t>(si) * h264::kSubEntry;
+  }
   const int16_t* wt = a.wp + static_cast<size_t>(slot) * kWpEntries;
-  auto mv_of = [&](int l, int rb, int c) { return static_cast<int>(mvp[(static_cast<size_t>(l) * nmb + mb) * 32 + rb * 2 + c]); };
-  auto ref_of = [&](int l, int rb) { return static_cast<int>(rip[(static_cast<size_t>(l) * nmb + mb) * 16 + rb]); };
+  auto quad = [](int rb) { return ((rb & 3) >> 1) + 2 * (rb >> 3); };
+  auto mv_of = [&](int l, int rb, int c) {
+    return static_cast<int>(sub4 ? se[(l * 16 + rb) * 2 + c] : H->mv[l][quad(rb)][c]);
+  };
+  auto ref_of = [&](int l, int rb) {
+    return static_cast<int>(sub4 ? reinterpret_cast<const int8_t*>(se + 64)[l * 16 + rb] : H->ref[l][quad(rb)]);
+  };
   auto pic_of = [&](int l, int r) {  // DPB index of RefPicListl[r], validated
     const int di = (r >= 0 && r < 32) ? rt[l * 32 + r] : -1;
     if (di < 0 || di >= D) {
@@ -723,16 +735,16 @@ static DecodeArgs make_decode_args(int B, int wmb, int hmb, uint8_t* rec_y, uint
   a.cur_idx = nullptr;
   a.reftab = nullptr;
   a.wp = nullptr;
-  a.mv = nullptr;
-  a.refidx = nullptr;
+  a.sub = nullptr;
   return a;
 }
 
 // One picture of every slot in the DPB layout: rec_* = [B][dpb_n] picture buffers; the
-// decoded picture goes to buffer cur_idx[slot]; P and B macroblocks from reftab / mv / refidx.
+// decoded picture goes to buffer cur_idx[slot]; P and B macroblocks from reftab + the headers'
+// motion (and the side pool `sub` for MBF_SUB4 macroblocks).
 extern "C" void mivc_launch_decode_picture_dpb(int B, int wmb, int hmb, int dpb_n, uint8_t* dpb_y, uint8_t* dpb_u,
-                                               uint8_t* dpb_v, const int8_t* cur_idx, const int8_t* reftab,
-                                               const int16_t* wp, const int16_t* mv, const int8_t* refidx,
+                                               uint8_t* dpb_v, const int16_t* cur_idx, const int16_t* reftab,
+                                               const int16_t* wp, const int16_t* sub,
                                                const void* hdr, const uint32_t* mask, const uint32_t* off,
                                                const int16_t* coef, const int8_t* run, int any_inter,
                                                int chroma_qp_offset, uint8_t* nz, int* err, void* stream) {
@@ -742,8 +754,7 @@ extern "C" void mivc_launch_decode_picture_dpb(int B, int wmb, int hmb, int dpb_
   a.cur_idx = cur_idx;
   a.reftab = reftab;
   a.wp = wp;
-  a.mv = mv;
-  a.refidx = refidx;
+  a.sub = sub;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (any_inter) hipLaunchKernelGGL(decode_inter_dpb, dim3(wmb * hmb, B), dim3(64), 0, s, a);
   hipLaunchKernelGGL(decode_intra_wavefront, dim3(B), dim3(64 * kDecIntraWaves), 0, s, a);

@@ -2,15 +2,18 @@
 
 The reference worker transcodes one piece per process: ``ffmpeg -i <idx>.mp4 <args>
 c<idx>.mp4`` (client.go:101-130), decode and encode inside ffmpeg.  Here a batch of
-pieces goes through the GPU together, and the three stages overlap:
+pieces goes through the GPU together, as a three-stage pipeline:
 
-* **host parse** of batch k+1 (H.264: CAVLC / CABAC entropy decode, csrc/host/h264_decoder.cc;
-  HEVC: CABAC + motion derivation, csrc/host/hevc_dec.cc; C++ threads, GIL released) runs on a
-  worker thread while the GPU reconstructs and re-encodes batch k;
-* **GPU decode** (h264_decode_gpu / hevc_decode_gpu) writes display-size frames straight into
-  the ``[B, F, h, w]`` tensors the encoder reads -- equal-length pieces are encoded from the
+* **host parse** of batch k+2 (H.264: CAVLC / CABAC entropy decode, csrc/host/h264_decoder.cc;
+  HEVC: CABAC + motion derivation, csrc/host/hevc_dec.cc; C++ threads, GIL released) on a
+  worker thread;
+* **GPU decode** of batch k+1 on its own HIP stream, issued from a second worker thread
+  (h264_decode_gpu / hevc_decode_gpu), writing display-size frames straight into the
+  ``[B, F, h, w]`` tensors the encoder reads -- equal-length pieces are encoded from the
   decoder's output without another copy;
-* **GPU encode** with an encoder constructed once, before the first batch.
+* **GPU encode** of batch k on the main thread's stream, with an encoder constructed once,
+  before the first batch.  The decode kernels of batch k+1 fill the CUs the encoder's
+  wavefront / entropy stages leave idle.
 
 ``run`` returns one Annex-B stream per piece plus stage timings.
 """
@@ -43,6 +46,8 @@ class GpuTranscoder:
 
     def close(self):
         self.pool.shutdown(wait=True)
+        if getattr(self, "dec_pool", None) is not None:
+            self.dec_pool.shutdown(wait=True)
         self.enc.close()
 
     # ------------------------------------------------------------------ stages
@@ -95,26 +100,50 @@ class GpuTranscoder:
         return [ps + b"".join(res[b].display_prefix(counts[b])) for b in range(B)]
 
     # ------------------------------------------------------------------ public
+    def _decode_batch(self, fut):
+        """Decode thread: wait for the batch's parse, reconstruct it on the decode stream."""
+        codec, parsed, dt = fut.result()
+        with torch.cuda.stream(self.dec_stream):
+            t0 = time.perf_counter()
+            y, u, v, counts = self._frames(codec, parsed, self._fps)
+            del parsed
+            ev = torch.cuda.Event()
+            ev.record(self.dec_stream)
+            ev.synchronize()
+            return y, u, v, counts, ev, dt, time.perf_counter() - t0
+
     def run(self, pieces: list[bytes], fps: float = 30.0) -> list[bytes]:
         batches = [pieces[i:i + self.slots] for i in range(0, len(pieces), self.slots)]
         out: list[bytes] = []
-        t = dict(parse_s=0.0, parse_wait_s=0.0, decode_s=0.0, encode_s=0.0)
-        fut = self.pool.submit(self._parse, batches[0]) if batches else None
+        t = dict(parse_s=0.0, decode_s=0.0, encode_s=0.0, decode_wait_s=0.0)
+        if not batches:
+            self.timings = t
+            return out
+        self._fps = fps
+        if getattr(self, "dec_stream", None) is None:
+            self.dec_stream = torch.cuda.Stream(self.dev)
+            self.dec_pool = cf.ThreadPoolExecutor(max_workers=1)
+        main = torch.cuda.current_stream(self.dev)
+        # the decode stream starts after whatever the caller queued on the main stream
+        self.dec_stream.wait_stream(main)
+        pf = {k: self.pool.submit(self._parse, batches[k]) for k in range(min(2, len(batches)))}
+        df = {0: self.dec_pool.submit(self._decode_batch, pf.pop(0))}
         for k in range(len(batches)):
             tw = time.perf_counter()
-            codec, parsed, dt = fut.result()
-            t["parse_wait_s"] += time.perf_counter() - tw
-            t["parse_s"] += dt
-            if k + 1 < len(batches):  # host parse of the next batch overlaps this batch's GPU work
-                fut = self.pool.submit(self._parse, batches[k + 1])
-            td = time.perf_counter()
-            y, u, v, counts = self._frames(codec, parsed, fps)
-            del parsed
-            torch.cuda.current_stream(self.dev).synchronize()
+            y, u, v, counts, ev, dt_parse, dt_dec = df.pop(k).result()
+            t["decode_wait_s"] += time.perf_counter() - tw
+            t["parse_s"] += dt_parse
+            t["decode_s"] += dt_dec
+            if k + 1 < len(batches):   # GPU decode of k + 1 overlaps this batch's encode
+                df[k + 1] = self.dec_pool.submit(self._decode_batch, pf.pop(k + 1))
+            if k + 2 < len(batches):   # host parse two batches ahead
+                pf[k + 2] = self.pool.submit(self._parse, batches[k + 2])
+            main.wait_event(ev)
+            for x in (y, u, v):
+                x.record_stream(main)
             te = time.perf_counter()
-            t["decode_s"] += te - td
             out += self._encode(y, u, v, counts)
-            torch.cuda.current_stream(self.dev).synchronize()
+            main.synchronize()
             t["encode_s"] += time.perf_counter() - te
             del y, u, v
         self.timings = t
