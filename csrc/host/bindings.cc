@@ -369,7 +369,8 @@ py::dict dec_segment_records(std::vector<hevc::DecPicture>& pics, const std::vec
   const int w4 = f.W / 4, h4 = f.H / 4, nctb = f.wctb * f.hctb;
   std::vector<int32_t> meta(P * 24, 0), ref_ids(P * 16, -1), display(P, -1);
   for (size_t i = 0; i < order.size(); ++i) display[order[i]] = static_cast<int32_t>(i);
-  std::vector<uint8_t> mvf, bs, ctbs, sao, scaling;
+  std::vector<uint8_t> mvf, mvf_sub, bs, ctbs, sao, scaling;
+  std::vector<int64_t> mvf_sub_off(P + 1, 0);
   std::vector<hevc::DecTu> tus;
   std::vector<hevc::DecIntraOp> ops;
   std::vector<hevc::DecRefEntry> refs;
@@ -377,7 +378,7 @@ py::dict dec_segment_records(std::vector<hevc::DecPicture>& pics, const std::vec
   std::vector<int16_t> coefs;
   std::vector<int64_t> tu_off(P + 1), op_off(P + 1), ref_off(P + 1), slice_off(P + 1), coef_off(P + 1);
   std::vector<uint32_t> ctb_ops(P * (nctb + 1));
-  mvf.reserve(P * w4 * h4 * 12);
+  mvf.reserve(P * (w4 / 2) * (h4 / 2) * 12);
   for (size_t i = 0; i < P; ++i) {
     hevc::DecPicture& p = pics[i];
     if (p.W != f.W || p.H != f.H || p.log2_ctb != f.log2_ctb || p.bit_depth != f.bit_depth)
@@ -391,6 +392,9 @@ py::dict dec_segment_records(std::vector<hevc::DecPicture>& pics, const std::vec
     for (size_t k = 0; k < p.ref_ids.size() && k < 16; ++k) ref_ids[i * 16 + k] = p.ref_ids[k];
     const uint8_t* mb = reinterpret_cast<const uint8_t*>(p.mvf.data());
     mvf.insert(mvf.end(), mb, mb + p.mvf.size() * sizeof(hevc::DecMv4));
+    mvf_sub_off[i] = static_cast<int64_t>(mvf_sub.size() / sizeof(hevc::DecMv4));
+    const uint8_t* ms = reinterpret_cast<const uint8_t*>(p.mvf_sub.data());
+    mvf_sub.insert(mvf_sub.end(), ms, ms + p.mvf_sub.size() * sizeof(hevc::DecMv4));
     bs.insert(bs.end(), p.bs.begin(), p.bs.end());
     const uint8_t* cb = reinterpret_cast<const uint8_t*>(p.ctbs.data());
     ctbs.insert(ctbs.end(), cb, cb + p.ctbs.size() * sizeof(hevc::DecCtb));
@@ -425,7 +429,10 @@ py::dict dec_segment_records(std::vector<hevc::DecPicture>& pics, const std::vec
   d["meta"] = to_array(meta, {Pn, 24});
   d["ref_ids"] = to_array(ref_ids, {Pn, 16});
   d["display"] = to_array(display, {Pn});
-  d["mvf"] = to_array(mvf, {Pn, h4, w4, 12});
+  mvf_sub_off[P] = static_cast<int64_t>(mvf_sub.size() / sizeof(hevc::DecMv4));
+  d["mvf"] = to_array(mvf, {Pn, h4 / 2, w4 / 2, 12});
+  d["mvf_sub"] = to_array(mvf_sub, {static_cast<py::ssize_t>(mvf_sub.size() / 12), 12});
+  d["mvf_sub_off"] = to_array(mvf_sub_off, {Pn + 1});
   d["bs"] = to_array(bs, {Pn, h4, w4});
   d["ctbs"] = to_array(ctbs, {Pn, nctb, 8});
   d["sao"] = to_array(sao, {Pn, nctb, 24});
@@ -811,6 +818,90 @@ PYBIND11_MODULE(_host, m) {
         return out;
       },
       py::arg("data"), py::arg("recon") = true, py::arg("skip_filters") = false);
+  // parsed HEVC batch kept in C++ (models/hevc_decode_gpu.py): info(i) for planning,
+  // layout / pack of one picture step straight into a pinned host buffer
+  py::class_<HevcBatch>(m, "HevcBatch")
+      .def("__len__", [](const HevcBatch& b) { return b.segs.size(); })
+      .def("info",
+           [](const HevcBatch& b, int i) {
+             const HevcParsed& sp = b.segs.at(i);
+             py::dict d;
+             if (!sp.error.empty()) {
+               d["n"] = 0;
+               d["error"] = sp.error;
+               return d;
+             }
+             const std::vector<hevc::DecPicture>& pics = sp.dec->pictures();
+             const size_t P = pics.size();
+             const py::ssize_t Pn = static_cast<py::ssize_t>(P);
+             std::vector<int32_t> meta(P * 24, 0), ref_ids(P * 16, -1), display(P, -1);
+             for (size_t k = 0; k < sp.order.size(); ++k) display[sp.order[k]] = static_cast<int32_t>(k);
+             for (size_t k = 0; k < P; ++k) {
+               const hevc::DecPicture& q = pics[k];
+               const int v[24] = {q.decode_idx, q.poc, q.cvs, q.output, q.irap, q.idr, q.slice_type, q.slice_qp,
+                                  q.W, q.H, q.width, q.height, q.crop_x, q.crop_y, q.bit_depth, q.bit_depth_c,
+                                  q.log2_ctb, q.constrained_intra, q.strong_intra, q.lf_across_tiles, q.cb_qp_off,
+                                  q.cr_qp_off, q.deblock_any, q.sao_any};
+               std::copy(v, v + 24, &meta[k * 24]);
+               for (size_t r = 0; r < q.ref_ids.size() && r < 16; ++r) ref_ids[k * 16 + r] = q.ref_ids[r];
+             }
+             d["n"] = static_cast<int>(P);
+             d["error"] = py::none();
+             d["meta"] = to_array(meta, {Pn, 24});
+             d["ref_ids"] = to_array(ref_ids, {Pn, 16});
+             d["display"] = to_array(display, {Pn});
+             return d;
+           })
+      .def("layout",
+           [](const HevcBatch& b, int t, const std::vector<int>& slots) {
+             HevcStepLayout L = b.layout(t, slots);
+             py::dict d;
+             d["meta"] = L.meta;
+             d["tu_base"] = L.tu_base;
+             d["coef_base"] = L.coef_base;
+             d["op_base"] = L.op_base;
+             d["ref_base"] = L.ref_base;
+             d["slice_base"] = L.slice_base;
+             d["ctb_ops"] = L.ctb_ops;
+             d["mvf"] = L.mvf;
+             d["mvf_sub"] = L.mvf_sub;
+             d["bs"] = L.bs;
+             d["ctbs"] = L.ctbs;
+             d["sao"] = L.sao;
+             d["tus"] = L.tus;
+             d["coefs"] = L.coefs;
+             d["ops"] = L.ops;
+             d["refs"] = L.refs;
+             d["slices"] = L.slices;
+             d["scaling"] = L.scaling;
+             d["total"] = L.total;
+             d["max_tus"] = L.max_tus;
+             d["scaling_on"] = L.scaling_on;
+             d["deblock_any"] = L.deblock_any;
+             d["sao_any"] = L.sao_any;
+             return d;
+           })
+      .def("pack",
+           [](const HevcBatch& b, int t, const std::vector<int>& slots, uintptr_t dst, size_t capacity, int threads) {
+             HevcStepLayout L = b.layout(t, slots);
+             if (L.total > capacity) throw std::invalid_argument("HevcBatch.pack: buffer too small");
+             py::gil_scoped_release rel;
+             b.pack(t, slots, reinterpret_cast<uint8_t*>(dst), threads);
+           },
+           py::arg("t"), py::arg("slots"), py::arg("dst"), py::arg("capacity"), py::arg("threads") = 4);
+  m.def(
+      "hevc_parse_batch",
+      [](const std::vector<py::bytes>& segments, int threads) {
+        std::vector<std::string> in;
+        for (const py::bytes& b : segments) in.emplace_back(b);
+        auto* batch = new HevcBatch();
+        {
+          py::gil_scoped_release rel;
+          batch->segs = hevc_parse_many(in, threads, false);
+        }
+        return batch;
+      },
+      py::arg("segments"), py::arg("threads") = 1, py::return_value_policy::take_ownership);
   m.def(
       "hevc_parse",
       [](const std::vector<py::bytes>& segments, int threads, bool recon) {

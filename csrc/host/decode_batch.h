@@ -13,6 +13,8 @@
 #include <vector>
 
 #include "h264_decoder.h"
+#include "hevc_dec.h"
+#include <memory>
 
 namespace mivc {
 
@@ -46,6 +48,38 @@ class H264Batch {
 
  private:
   const h264::DecodedPicture* pic(int t, int seg) const;
+};
+
+// ---------------------------------------------------------------- HEVC
+struct HevcParsed {
+  std::unique_ptr<hevc::HevcStreamDecoder> dec;  // pictures() in decoding order
+  std::vector<int> order;                        // output order (indices into pictures())
+  std::string error;
+};
+std::vector<HevcParsed> hevc_parse_many(const std::vector<std::string>& segs, int threads, bool recon);
+
+// sections of one HEVC picture step (csrc/kernels/hevc_decode.h HevcDecParams); 256-byte aligned
+struct HevcStepLayout {
+  size_t meta = 0, tu_base = 0, coef_base = 0, op_base = 0, ref_base = 0, slice_base = 0, ctb_ops = 0;
+  size_t mvf = 0, mvf_sub = 0, bs = 0, ctbs = 0, sao = 0, tus = 0, coefs = 0, ops = 0, refs = 0, slices = 0, scaling = 0;
+  size_t total = 0;
+  int max_tus = 0;           // most transform blocks of one slot (residual grid)
+  bool scaling_on = false;   // a slot uses scaling lists (else the section is empty)
+  bool deblock_any = false, sao_any = false;
+};
+
+class HevcBatch {
+ public:
+  HevcBatch() = default;
+  HevcBatch(const HevcBatch&) = delete;  // holds the decoders (unique_ptr)
+  HevcBatch& operator=(const HevcBatch&) = delete;
+  std::vector<HevcParsed> segs;
+  // slot j reconstructs picture t (decoding order) of segment slots[j] (-1 / past its end: idle)
+  HevcStepLayout layout(int t, const std::vector<int>& slots) const;
+  void pack(int t, const std::vector<int>& slots, uint8_t* dst, int threads) const;
+
+ private:
+  const hevc::DecPicture* pic(int t, int seg) const;
 };
 
 }  // namespace mivc

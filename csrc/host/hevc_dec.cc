@@ -157,9 +157,13 @@ const int kChromaTaps[8][4] = {{0, 64, 0, 0},    {-2, 58, 10, -2}, {-4, 54, 16, 
 
 // z-order of a 4x4 block (bx, by) inside a CTB of 2^l4 x 2^l4 blocks
 inline uint32_t zorder(int bx, int by) {
-  uint32_t z = 0;
-  for (int i = 0; i < 4; ++i) z |= static_cast<uint32_t>(((bx >> i) & 1) << (2 * i)) | static_cast<uint32_t>(((by >> i) & 1) << (2 * i + 1));
-  return z;
+  // interleave the 4 low bits of bx (even bit positions) and by (odd)
+  auto spread = [](uint32_t v) {
+    v &= 15u;
+    v = (v | (v << 2)) & 0x33u;
+    return (v | (v << 1)) & 0x55u;
+  };
+  return spread(static_cast<uint32_t>(bx)) | (spread(static_cast<uint32_t>(by)) << 1);
 }
 
 enum PartMode { P_2Nx2N = 0, P_2NxN, P_Nx2N, P_NxN, P_2NxnU, P_2NxnD, P_nLx2N, P_nRx2N };
@@ -249,6 +253,7 @@ struct HevcStreamDecoder::Impl {
   std::vector<uint8_t> ct_depth, ipm, edge, cbf_y;
   std::vector<int8_t> qp_y;
   std::vector<int16_t> ctb_slice;  // per CTB (raster): slice_idx or -1 (not decoded)
+  std::vector<int32_t> ctb_saddr;  // per CTB (raster): SliceAddrRs of its slice
   enum : uint8_t { CF_INTRA = 1, CF_SKIP = 2, CF_PCM = 4, CF_BYPASS = 8, CF_INTER = 16 };
   enum : uint8_t { E_TU_V = 1, E_PU_V = 2, E_TU_H = 4, E_PU_H = 8 };
 
@@ -442,6 +447,7 @@ struct HevcStreamDecoder::Impl {
     cbf_y.assign(n4, 0);
     qp_y.assign(n4, 0);
     ctb_slice.assign(nctb, -1);
+    ctb_saddr.assign(nctb, -1);
     cur = std::make_shared<StoredPic>();
     cur->decode_idx = decode_count++;
     cur->poc = poc;
@@ -490,7 +496,8 @@ struct HevcStreamDecoder::Impl {
     d.cb_qp_off = pps->cb_qp_off;
     d.cr_qp_off = pps->cr_qp_off;
     if (opt.gpu_records) {
-      d.mvf.assign(n4, DecMv4{});
+      d.mvf.clear();
+      d.mvf_sub.clear();
       d.bs.assign(n4, 0);
       d.ctbs.assign(nctb, DecCtb{});
       d.sao.assign(nctb, DecSao{});
@@ -691,6 +698,7 @@ struct HevcStreamDecoder::Impl {
       if (ctb_addr_ts >= nctb) fail("slice data runs past the last CTB");
       ctb_addr_rs = ts2rs[ctb_addr_ts];
       ctb_slice[ctb_addr_rs] = static_cast<int16_t>(slice_idx);
+      ctb_saddr[ctb_addr_rs] = slice_addr_of(slice_idx);
       cur->ctb_slice[ctb_addr_rs] = static_cast<uint16_t>(slice_idx);
       if (opt.gpu_records) {
         DecCtb& c = dp->ctbs[ctb_addr_rs];
@@ -781,12 +789,16 @@ struct HevcStreamDecoder::Impl {
   bool avail_z(int xc, int yc, int xn, int yn) const {
     if (xn < 0 || yn < 0 || xn >= W || yn >= H) return false;
     const int rsn = (yn >> log2_ctb) * wctb + (xn >> log2_ctb);
-    const int sn = ctb_slice[rsn];
-    if (sn < 0) return false;
-    if (zaddr(xn, yn) > zaddr(xc, yc)) return false;
     const int rsc = (yc >> log2_ctb) * wctb + (xc >> log2_ctb);
-    if (slice_addr_of(sn) != slice_addr_of(ctb_slice[rsc])) return false;
-    if (tile_id[rs2ts[rsn]] != tile_id[rs2ts[rsc]]) return false;
+    if (rsn == rsc) {  // same CTB (so same slice segment and tile): z-order alone decides
+      const int m = (1 << l4) - 1;
+      return zorder((xn >> 2) & m, (yn >> 2) & m) <= zorder((xc >> 2) & m, (yc >> 2) & m);
+    }
+    if (ctb_slice[rsn] < 0) return false;
+    const int tsn = rs2ts[rsn], tsc = rs2ts[rsc];
+    if (tsn > tsc) return false;
+    if (ctb_saddr[rsn] != ctb_saddr[rsc]) return false;
+    if (tile_id[tsn] != tile_id[tsc]) return false;
     return true;
   }
   // 6.4.2 prediction block availability
@@ -1630,8 +1642,32 @@ struct HevcStreamDecoder::Impl {
     t.cidx = static_cast<uint8_t>(cidx);
     t.qp = static_cast<uint8_t>(qp);
     t.flags = flags;
+    // sparse levels: a 64-bit mask of the coded 4x4 coefficient groups (raster over the
+    // block, as 4 uint16 words), then the 16 levels (raster) of each coded group
     t.coef = static_cast<uint32_t>(d.coefs.size());
-    d.coefs.insert(d.coefs.end(), c, c + n * n);
+    const int g = n >> 2;
+    uint64_t mask = 0;
+    for (int cg = 0; cg < g * g; ++cg) {
+      const int16_t* p = c + (cg / g) * 4 * n + (cg % g) * 4;
+      uint64_t any = 0;
+      for (int r = 0; r < 4; ++r) {
+        uint64_t w;
+        std::memcpy(&w, p + r * n, 8);
+        any |= w;
+      }
+      if (any) mask |= 1ull << cg;
+    }
+    const size_t at = d.coefs.size();
+    d.coefs.resize(at + 4 + 16 * static_cast<size_t>(__builtin_popcountll(mask)));
+    int16_t* o = d.coefs.data() + at;
+    for (int k = 0; k < 4; ++k) o[k] = static_cast<int16_t>(static_cast<uint16_t>(mask >> (16 * k)));
+    o += 4;
+    for (int cg = 0; cg < g * g; ++cg) {
+      if (!((mask >> cg) & 1)) continue;
+      const int16_t* p = c + (cg / g) * 4 * n + (cg % g) * 4;
+      for (int r = 0; r < 4; ++r) std::memcpy(o + r * 4, p + r * n, 8);
+      o += 16;
+    }
     d.tus.push_back(t);
     return static_cast<uint32_t>(d.tus.size() - 1);
   }
@@ -2110,8 +2146,9 @@ struct HevcStreamDecoder::Impl {
     if (opt.gpu_records) {
       d.bs = bsv;
       const size_t n4 = static_cast<size_t>(w4) * h4;
+      std::vector<DecMv4> m4(n4);
       for (size_t k = 0; k < n4; ++k) {
-        DecMv4& m = d.mvf[k];
+        DecMv4& m = m4[k];
         const MvField& f = cur->mvf[k];
         const int x = static_cast<int>(k % w4) * 4, y = static_cast<int>(k / w4) * 4;
         const int sidx = ctb_slice[(y >> log2_ctb) * wctb + (x >> log2_ctb)];
@@ -2134,6 +2171,26 @@ struct HevcStreamDecoder::Impl {
           m.mv[0][0] = m.mv[0][1] = m.mv[1][0] = m.mv[1][1] = 0;
         }
       }
+      // 8x8 records: a coding block is >= 8x8, so flags and QpY are uniform per 8x8; only
+      // 8x4 / 4x8 prediction blocks differ inside one -- those become DM_SPLIT records whose
+      // first 4 bytes index 4 per-4x4 records (raster) in mvf_sub
+      const int w8 = w4 / 2, h8 = h4 / 2;
+      d.mvf.assign(static_cast<size_t>(w8) * h8, DecMv4{});
+      for (int by = 0; by < h8; ++by)
+        for (int bx = 0; bx < w8; ++bx) {
+          const DecMv4* c[4] = {&m4[static_cast<size_t>(2 * by) * w4 + 2 * bx], &m4[static_cast<size_t>(2 * by) * w4 + 2 * bx + 1],
+                                &m4[static_cast<size_t>(2 * by + 1) * w4 + 2 * bx],
+                                &m4[static_cast<size_t>(2 * by + 1) * w4 + 2 * bx + 1]};
+          DecMv4& o = d.mvf[static_cast<size_t>(by) * w8 + bx];
+          o = *c[0];
+          bool same = true;
+          for (int i = 1; i < 4; ++i) same = same && std::memcmp(c[i], c[0], sizeof(DecMv4)) == 0;
+          if (same) continue;
+          const uint32_t idx = static_cast<uint32_t>(d.mvf_sub.size() / 4);
+          std::memcpy(o.mv, &idx, 4);
+          o.flags |= DM_SPLIT;
+          for (int i = 0; i < 4; ++i) d.mvf_sub.push_back(*c[i]);
+        }
       uint32_t off = 0;
       for (int r = 0; r < nctb; ++r) {
         d.ops_off[r] = off;

@@ -34,7 +34,7 @@ namespace hevc {
 // work: dequantisation + inverse transforms, motion compensation, intra prediction in
 // CTB wavefront order, deblocking, SAO (csrc/kernels/hevc_decode.hip).
 
-// per 4x4 luma block
+// motion / flags / QpY of a luma block (DecPicture::mvf: 8x8 blocks, mvf_sub: 4x4 blocks)
 struct DecMv4 {
   int16_t mv[2][2];   // quarter-sample L0 / L1 vectors
   uint8_t ref[2];     // index into DecPicture::refs, 0xFF = list unused
@@ -42,7 +42,7 @@ struct DecMv4 {
   int8_t qp;          // QpY of the coding unit
 };
 static_assert(sizeof(DecMv4) == 12, "DecMv4 is 12 bytes");
-enum : uint8_t { DM_INTRA = 1, DM_NOFILTER = 2, DM_INTER = 4 };
+enum : uint8_t { DM_INTRA = 1, DM_NOFILTER = 2, DM_INTER = 4, DM_SPLIT = 8 };
 
 // deblocking edge strengths per 4x4 luma block: bits 0-1 bS of its left edge, bits 2-3 bS
 // of its top edge (0 = not filtered: not an edge, picture / slice / tile restriction or a
@@ -124,7 +124,8 @@ struct DecPicture {
   // GPU records (filled when DecodeOptions::gpu_records)
   std::vector<int> ref_ids;         // decode_idx of every picture referenced by refs
   std::vector<DecRefEntry> refs;
-  std::vector<DecMv4> mvf;          // [H/4][W/4]
+  std::vector<DecMv4> mvf;          // [H/8][W/8] per 8x8 block; DM_SPLIT: mv bytes 0-3 = entry of
+  std::vector<DecMv4> mvf_sub;      // 4 records (raster 4x4 blocks) per split 8x8 block
   std::vector<DecBs> bs;            // [H/4][W/4]
   std::vector<DecTu> tus;
   std::vector<int16_t> coefs;

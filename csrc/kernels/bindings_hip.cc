@@ -381,6 +381,7 @@ PYBIND11_MODULE(_hip, m) {
     a.run = P<int8_t>(Q("run"));
     a.meta = P<int32_t>(Q("meta"));
     a.mvf = P<uint8_t>(Q("mvf"));
+    a.mvf_sub = P<uint8_t>(Q("mvf_sub"));
     a.bs = P<uint8_t>(Q("bs"));
     a.ctbs = P<uint8_t>(Q("ctbs"));
     a.sao = P<uint8_t>(Q("sao"));
@@ -398,6 +399,17 @@ PYBIND11_MODULE(_hip, m) {
     a.scaling = P<uint8_t>(Q("scaling"));
     a.max_tus = static_cast<int>(I("max_tus"));
     a.err = P<int>(Q("err"));
+    if (p.contains("out")) {
+      const std::vector<uintptr_t> out = p["out"].cast<std::vector<uintptr_t>>();
+      for (int c = 0; c < 3; ++c) a.out[c] = reinterpret_cast<void*>(out.at(c));
+      a.out_u8 = static_cast<int>(I("out_u8"));
+      a.Fo = static_cast<int>(I("Fo"));
+      a.out_w = static_cast<int>(I("out_w"));
+      a.out_h = static_cast<int>(I("out_h"));
+      a.crop_x = static_cast<int>(I("crop_x"));
+      a.crop_y = static_cast<int>(I("crop_y"));
+      a.disp = P<int16_t>(Q("disp"));
+    }
     if (!a.cur || !a.run || !a.meta || !a.mvf || !a.err) throw std::runtime_error("hevc_decode_stage: null pointer");
     const int r = mivc_launch_hevc_decode(&a, stage, S(stream));
     if (r != 0) throw std::runtime_error("hevc_decode_stage: launch failed (" + std::to_string(r) + ")");

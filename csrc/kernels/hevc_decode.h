@@ -19,7 +19,8 @@ struct HevcDecParams {
   const int8_t* reftab;        // [B, 16] DPB buffer of every DecPicture::ref_ids entry
   const int8_t* run;           // [B] 1 = the slot decodes a picture this step
   const int32_t* meta;         // [B, 24] picture meta (hevc_parse layout)
-  const uint8_t* mvf;          // [B, h4, w4, 12]
+  const uint8_t* mvf;          // [B, H/8, W/8, 12] per 8x8 block (DM_SPLIT: index into mvf_sub)
+  const uint8_t* mvf_sub;      // [NS * 4, 12] per-4x4 records of split 8x8 blocks
   const uint8_t* bs;           // [B, h4, w4]
   const uint8_t* ctbs;         // [B, nctb, 8]
   const uint8_t* sao;          // [B, nctb, 24]
@@ -37,6 +38,10 @@ struct HevcDecParams {
   const uint8_t* scaling;      // [B, 8160] ScalingFactor, or null (flat)
   int max_tus;                 // most TUs of any slot this step (residual grid)
   int* err;
+  // stage 6 (emit): the step's pictures to their display positions of the output
+  void* out[3];                // [B, Fo, out_h, out_w] (chroma halved) uint8 (out_u8) or int16
+  int out_u8, Fo, out_w, out_h, crop_x, crop_y;
+  const int16_t* disp;         // [B] output position of this step's picture, -1 = not output
 };
 
 // meta columns (hevc_parse "meta")

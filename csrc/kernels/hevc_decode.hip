@@ -85,6 +85,8 @@ __device__ __forceinline__ Tu load_tu(const uint8_t* p) {
   return t;
 }
 
+constexpr uint8_t DM_INTRA = 1, DM_NOFILTER = 2, DM_INTER = 4, DM_SPLIT = 8;  // hevc_dec.h DecMv4
+
 struct Mv4 {
   int mv[2][2];
   int ref[2];
@@ -104,7 +106,17 @@ __device__ __forceinline__ Mv4 load_mv4(const uint8_t* p) {
   return r;
 }
 
-constexpr uint8_t DM_INTRA = 1, DM_NOFILTER = 2, DM_INTER = 4;
+// motion of the 4x4 luma block at (x, y): the 8x8 record, or for a DM_SPLIT record the
+// 4x4 entry its first 4 bytes index in mvf_sub (csrc/host/hevc_dec.h DecPicture::mvf)
+__device__ __forceinline__ Mv4 mv_at(const HevcDecParams& a, const uint8_t* mvf8, int x, int y) {
+  const uint8_t* p = mvf8 + (static_cast<size_t>(y >> 3) * (a.W >> 3) + (x >> 3)) * 12;
+  if (p[10] & DM_SPLIT) {
+    const uint32_t idx = *reinterpret_cast<const uint32_t*>(p);
+    p = a.mvf_sub + (static_cast<size_t>(idx) * 4 + ((y >> 2) & 1) * 2 + ((x >> 2) & 1)) * 12;
+  }
+  return load_mv4(p);
+}
+
 constexpr uint8_t DT_DST = 1, DT_TSKIP = 2, DT_BYPASS = 4, DT_INTRA = 8, DT_SCALING = 16, DT_PCM = 32;
 
 __device__ __forceinline__ size_t plane_size(const HevcDecParams& a, int c) {
@@ -128,11 +140,25 @@ __global__ __launch_bounds__(64) void hevcd_residual(HevcDecParams a) {
   const int lane = lane_id();
   const int n = 1 << t.log2, nn = n * n;
   const int bdv = t.cidx ? a.bdc : a.bd;
-  const int16_t* lv = a.coefs + a.coef_base[b] + t.coef;
+  // sparse levels (hevc_dec.cc push_tu): 64-bit mask of the coded 4x4 groups, then 16
+  // levels per coded group
+  const int16_t* lp = a.coefs + a.coef_base[b] + t.coef;
+  uint64_t cgm = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) cgm |= static_cast<uint64_t>(static_cast<uint16_t>(lp[k])) << (16 * k);
+  const int16_t* cgv = lp + 4;
+  const int gs = n >> 2;
+  auto lv = [&](int k) -> int {  // level at raster position k of the block
+    const int y = k >> t.log2, x = k & (n - 1);
+    const int cg = (y >> 2) * gs + (x >> 2);
+    if (!((cgm >> cg) & 1ull)) return 0;
+    const int idx = __popcll(cgm & ((1ull << cg) - 1ull));
+    return cgv[idx * 16 + (y & 3) * 4 + (x & 3)];
+  };
   const int pw = t.cidx ? a.W / 2 : a.W;
   int16_t* dst = a.res[t.cidx] + static_cast<size_t>(b) * plane_size(a, t.cidx) + static_cast<size_t>(t.y) * pw + t.x;
   if (t.flags & (DT_BYPASS | DT_PCM)) {  // residual = the coded values (PCM: the samples)
-    for (int k = lane; k < nn; k += 64) dst[(k >> t.log2) * pw + (k & (n - 1))] = lv[k];
+    for (int k = lane; k < nn; k += 64) dst[(k >> t.log2) * pw + (k & (n - 1))] = static_cast<int16_t>(lv(k));
     return;
   }
   // scaling (8.6.3): m = 16 (flat) or ScalingFactor; transform-skipped blocks > 4x4 stay flat
@@ -145,7 +171,7 @@ __global__ __launch_bounds__(64) void hevcd_residual(HevcDecParams a) {
          (((t.flags & DT_INTRA) ? 0 : 3) + t.cidx) * nn;
   for (int k = lane; k < nn; k += 64) {
     const int m = sl ? sl[k] : 16;
-    const long long v = static_cast<long long>(lv[k]) * m * ls + (1ll << (bdshift - 1));
+    const long long v = static_cast<long long>(lv(k)) * m * ls + (1ll << (bdshift - 1));
     R[(k >> t.log2) * 32 + (k & (n - 1))] = clip3d(-32768, 32767, static_cast<int>(v >> bdshift));
   }
   wave_sync();
@@ -234,13 +260,12 @@ __global__ __launch_bounds__(64) void hevcd_inter(HevcDecParams a) {
   const int w8 = a.W / 8;
   const int bx8 = static_cast<int>(blockIdx.x) % w8, by8 = static_cast<int>(blockIdx.x) / w8;
   const int lane = lane_id();
-  const int w4 = a.W / 4;
-  const uint8_t* mvf = a.mvf + static_cast<size_t>(b) * (a.H / 4) * w4 * 12;
+  const uint8_t* mvf = a.mvf + static_cast<size_t>(b) * (a.H / 8) * (a.W / 8) * 12;
   const int cur = a.cur[b];
   // luma: one sample per lane
   {
     const int x = bx8 * 8 + (lane & 7), y = by8 * 8 + (lane >> 3);
-    const Mv4 m = load_mv4(mvf + (static_cast<size_t>(y >> 2) * w4 + (x >> 2)) * 12);
+    const Mv4 m = mv_at(a, mvf, x, y);
     if (m.flags & DM_INTER) {
       int p[2] = {0, 0};
       RefE e[2];
@@ -283,7 +308,7 @@ __global__ __launch_bounds__(64) void hevcd_inter(HevcDecParams a) {
     const int c = 1 + (lane >> 4), i = lane & 15;
     const int cx = bx8 * 4 + (i & 3), cy = by8 * 4 + (i >> 2);
     const int lx = cx * 2, ly = cy * 2;
-    const Mv4 m = load_mv4(mvf + (static_cast<size_t>(ly >> 2) * w4 + (lx >> 2)) * 12);
+    const Mv4 m = mv_at(a, mvf, lx, ly);
     if (m.flags & DM_INTER) {
       const int cw = a.W / 2, ch = a.H / 2;
       int p[2] = {0, 0};
@@ -350,12 +375,12 @@ __global__ __launch_bounds__(64 * kDecIntraWaves) void hevcd_intra(HevcDecParams
   const int wave = wave_id(), lane = lane_id();
   for (int r = threadIdx.x; r < a.hctb; r += blockDim.x) prog[r] = 0;
   __syncthreads();
-  const int nctb = a.wctb * a.hctb, w4 = a.W / 4;
+  const int nctb = a.wctb * a.hctb, w8 = a.W / 8;
   const int32_t* meta = a.meta + b * HM_COLS;
   const bool cip = meta[HM_CONSTRAINED_INTRA] != 0, strong = meta[HM_STRONG_INTRA] != 0;
   const uint8_t* ctbs = a.ctbs + static_cast<size_t>(b) * nctb * 8;
   const uint8_t* slices = a.slices + static_cast<size_t>(a.slice_base[b]) * 8;
-  const uint8_t* mvf = a.mvf + static_cast<size_t>(b) * (a.H / 4) * w4 * 12;
+  const uint8_t* mvf = a.mvf + static_cast<size_t>(b) * (a.H / 8) * w8 * 12;
   const uint32_t* cops = a.ctb_ops + static_cast<size_t>(b) * (nctb + 1);
   const uint8_t* ops = a.ops + static_cast<size_t>(a.op_base[b]) * 12;
   const int cur = a.cur[b];
@@ -422,7 +447,7 @@ __global__ __launch_bounds__(64 * kDecIntraWaves) void hevcd_intra(HevcDecParams
             if (ctb_ts(rsn) > cur_ts) return false;
             if (ctb_slice_addr(rsn) != cur_slice || ctb_tile(rsn) != cur_tile) return false;
           }
-          if (cip && !(mvf[(static_cast<size_t>(yn >> 2) * w4 + (xn >> 2)) * 12 + 10] & DM_INTRA)) return false;
+          if (cip && !(mvf[(static_cast<size_t>(yn >> 3) * w8 + (xn >> 3)) * 12 + 10] & DM_INTRA)) return false;
           return true;
         };
         auto fetch = [&](int i) {
@@ -519,9 +544,9 @@ __global__ __launch_bounds__(256) void hevcd_deblock(HevcDecParams a, int dir) {
   if (!bsv) return;
   const int x = (k % w4) * 4, y = (k / w4) * 4;
   const int xp = dir == 0 ? x - 1 : x, yp = dir == 0 ? y : y - 1;
-  const uint8_t* mvf = a.mvf + static_cast<size_t>(b) * w4 * h4 * 12;
-  const uint8_t* mq = mvf + (static_cast<size_t>(y >> 2) * w4 + (x >> 2)) * 12;
-  const uint8_t* mp = mvf + (static_cast<size_t>(yp >> 2) * w4 + (xp >> 2)) * 12;
+  const uint8_t* mvf = a.mvf + static_cast<size_t>(b) * (w4 / 2) * (h4 / 2) * 12;
+  const uint8_t* mq = mvf + (static_cast<size_t>(y >> 3) * (w4 / 2) + (x >> 3)) * 12;
+  const uint8_t* mp = mvf + (static_cast<size_t>(yp >> 3) * (w4 / 2) + (xp >> 3)) * 12;
   const int qpl = (static_cast<int8_t>(mp[11]) + static_cast<int8_t>(mq[11]) + 1) >> 1;
   const bool np = (mp[10] & DM_NOFILTER) != 0, nq = (mq[10] & DM_NOFILTER) != 0;
   const int nctb = a.wctb * a.hctb;
@@ -571,9 +596,9 @@ __global__ __launch_bounds__(256) void hevcd_sao(HevcDecParams a) {
   const uint8_t* sp = a.sao + (static_cast<size_t>(b) * nctb + rs) * 24;
   const int type = sp[c];
   if (!type) return;
-  const int w4 = a.W / 4;
-  const uint8_t* mvf = a.mvf + static_cast<size_t>(b) * (a.H / 4) * w4 * 12;
-  if (mvf[(static_cast<size_t>(yl >> 2) * w4 + (xl >> 2)) * 12 + 10] & DM_NOFILTER) return;
+  const int w8 = a.W / 8;
+  const uint8_t* mvf = a.mvf + static_cast<size_t>(b) * (a.H / 8) * w8 * 12;
+  if (mvf[(static_cast<size_t>(yl >> 3) * w8 + (xl >> 3)) * 12 + 10] & DM_NOFILTER) return;
   const uint16_t* src = a.tmp[c] + static_cast<size_t>(b) * plane_size(a, c);
   const int v = src[static_cast<size_t>(y) * pw + x];
   const int bdv = c ? a.bdc : a.bd, mx = (1 << bdv) - 1;
@@ -616,12 +641,51 @@ __global__ __launch_bounds__(256) void hevcd_sao(HevcDecParams a) {
   if (o) dpb_plane(a, b, a.cur[b], c)[static_cast<size_t>(y) * pw + x] = static_cast<uint16_t>(clip3d(0, mx, v + o));
 }
 
+// stage 7: deblocked picture -> tmp (the SAO input), every running slot; 8-byte vectors
+// (plane sizes are multiples of 4 samples: W, H multiples of 8)
+__global__ __launch_bounds__(256) void hevcd_snapshot(HevcDecParams a) {
+  const int b = blockIdx.y;
+  if (!a.run[b]) return;
+  const size_t ny = static_cast<size_t>(a.W) * a.H / 4, nc = ny / 4;  // in uint64 units
+  for (size_t k = static_cast<size_t>(blockIdx.x) * 256 + threadIdx.x; k < ny + 2 * nc; k += static_cast<size_t>(gridDim.x) * 256) {
+    const int c = k < ny ? 0 : (k < ny + nc ? 1 : 2);
+    const size_t kk = c == 0 ? k : (c == 1 ? k - ny : k - ny - nc);
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(dpb_plane(a, b, a.cur[b], c));
+    uint64_t* dst = reinterpret_cast<uint64_t*>(a.tmp[c] + static_cast<size_t>(b) * plane_size(a, c));
+    dst[kk] = src[kk];
+  }
+}
+
+// stage 6: the step's pictures (cropped to the conformance window) to their display
+// positions of the [B, Fo, h, w] output -- uint8 for 8-bit output, else the int16 samples
+__global__ __launch_bounds__(256) void hevcd_emit(HevcDecParams a) {
+  const int b = blockIdx.y;
+  if (!a.run[b]) return;
+  const int d = a.disp[b];
+  if (d < 0 || d >= a.Fo) return;
+  const int w = a.out_w, h = a.out_h;
+  const size_t ny = static_cast<size_t>(w) * h, nc = static_cast<size_t>(w / 2) * (h / 2);
+  for (size_t k = static_cast<size_t>(blockIdx.x) * 256 + threadIdx.x; k < ny + 2 * nc; k += static_cast<size_t>(gridDim.x) * 256) {
+    const int c = k < ny ? 0 : (k < ny + nc ? 1 : 2);
+    const size_t kk = c == 0 ? k : (c == 1 ? k - ny : k - ny - nc);
+    const int ow = c ? w / 2 : w;
+    const int x = static_cast<int>(kk % ow), y = static_cast<int>(kk / ow);
+    const int pw = c ? a.W / 2 : a.W;
+    const int sx = x + (c ? a.crop_x / 2 : a.crop_x), sy = y + (c ? a.crop_y / 2 : a.crop_y);
+    const uint16_t v = dpb_plane(a, b, a.cur[b], c)[static_cast<size_t>(sy) * pw + sx];
+    const size_t o = (static_cast<size_t>(b) * a.Fo + d) * (c ? nc : ny) + kk;
+    if (a.out_u8) static_cast<uint8_t*>(a.out[c])[o] = static_cast<uint8_t>(v);
+    else static_cast<int16_t*>(a.out[c])[o] = static_cast<int16_t>(v);
+  }
+}
+
 }  // namespace gpu
 }  // namespace mivc
 
 using mivc::gpu::HevcDecParams;
 
-// stage: 0 residual, 1 inter, 2 intra, 3 deblock vertical, 4 deblock horizontal, 5 SAO
+// stage: 0 residual, 1 inter, 2 intra, 3 deblock vertical, 4 deblock horizontal, 5 SAO,
+// 6 emit (display-order output), 7 snapshot (deblocked copy for SAO)
 extern "C" int mivc_launch_hevc_decode(const HevcDecParams* p, int stage, void* stream) {
   const HevcDecParams& a = *p;
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -648,6 +712,15 @@ extern "C" int mivc_launch_hevc_decode(const HevcDecParams* p, int stage, void* 
       hipLaunchKernelGGL(mivc::gpu::hevcd_sao, dim3(static_cast<unsigned>((n + 255) / 256), a.B), dim3(256), 0, s, a);
       break;
     }
+    case 6:
+      if (!a.disp || !a.out[0] || !a.out[1] || !a.out[2] || a.Fo <= 0 || a.out_w <= 0 || a.out_h <= 0 ||
+          a.crop_x + a.out_w > a.W || a.crop_y + a.out_h > a.H || (a.out_w & 1) || (a.out_h & 1))
+        return -1;
+      hipLaunchKernelGGL(mivc::gpu::hevcd_emit, dim3(1024, a.B), dim3(256), 0, s, a);
+      break;
+    case 7:
+      hipLaunchKernelGGL(mivc::gpu::hevcd_snapshot, dim3(512, a.B), dim3(256), 0, s, a);
+      break;
     default:
       return -2;
   }
