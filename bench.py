@@ -29,6 +29,23 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 
+def _memory(env, merged) -> dict:
+    """Per-rank memory footprint (rank 0): HBM peak, host RSS, the pinned budget of one of
+    the ranks sharing this host, and the merge's host buffer (rank 0 only, world x bytes)."""
+    import torch
+
+    from govideocompressor_amd.runtime.device import pinned_budget
+    try:
+        import psutil
+        rss = psutil.Process().memory_info().rss
+    except Exception:  # pragma: no cover
+        rss = 0
+    return {"hbm_peak_gb": round(torch.cuda.max_memory_allocated(env.device) / 1e9, 2),
+            "hbm_reserved_gb": round(torch.cuda.max_memory_reserved(env.device) / 1e9, 2),
+            "host_rss_gb": round(rss / 1e9, 2), "pinned_budget_gb": round(pinned_budget() / 1e9, 2),
+            "merge_bytes_per_step": int(len(merged)) if merged is not None else 0}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -50,6 +67,8 @@ def main() -> None:
     ap.add_argument("--no-partitions", dest="partitions", action="store_false",
                     help="P macroblocks 16x16 only (no P_8x8 / P_16x8 / P_8x16)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--merged-out", default=None,
+                    help="rank 0 writes the last timed step's merged Annex-B stream here")
     ap.add_argument("--no-quality", dest="quality", action="store_false",
                     help="skip the PSNR/SSIM measurement of the first warmup step")
     a = ap.parse_args()
@@ -76,8 +95,10 @@ def main() -> None:
     merge_pool = cf.ThreadPoolExecutor(max_workers=1)
 
     def synth(step: int):
-        seed = 1000 + step * 7919 + env.rank * 104729
-        return synth_clip(B, F, a.width, a.height, seed=seed, device=env.device)
+        # rank r renders global slots [r * B, (r + 1) * B): the content (and so the merged
+        # stream) does not depend on how the global batch is split over ranks
+        seed = 1000 + step * 7919
+        return synth_clip(B, F, a.width, a.height, seed=seed, device=env.device, slot0=env.rank * B)
 
     def merge(res):
         # CC-2/CC-3 + concat on a side stream: overlaps the next batch's encode
@@ -166,7 +187,11 @@ def main() -> None:
             "timings_rank0_s": {k: round(v, 3) for k, v in enc.timings.items()},
             "stage_device_ms_per_step_rank0": {"measured_on": "warmup steps (untimed)", **stage_ms},
             "encoder_stats_rank0": {k: round(v, 4) for k, v in enc.stats.items()},
+            "memory_rank0": _memory(env, merged),
         }
+        if a.merged_out and merged is not None:
+            with open(a.merged_out, "wb") as f:
+                f.write(memoryview(merged))
         line = json.dumps(out)
         print(line, flush=True)
         if a.json_out:

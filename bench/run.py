@@ -288,7 +288,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workers", type=int, default=4)
     ap.add_argument("--frames3", type=int, default=30)
-    ap.add_argument("--segments3", type=int, default=128)
+    ap.add_argument("--segments3", type=int, default=256)
     ap.add_argument("--slots3", type=int, default=64)
     ap.add_argument("--codec3", default="h264,hevc")
     ap.add_argument("--slots4", type=int, default=64)

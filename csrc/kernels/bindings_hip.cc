@@ -15,7 +15,7 @@ namespace py = pybind11;
 extern "C" {
 int mivc_launch_hevc_decode(const mivc::gpu::HevcDecParams* p, int stage, void* stream);
 void mivc_launch_synth(void* y, void* u, void* v, int width, int height, int slots, int frames, int frame0,
-                       uint32_t seed, int bit_depth, void* stream);
+                       uint32_t seed, int bit_depth, int slot0, void* stream);
 void mivc_launch_prep(const uint8_t* in_y, const uint8_t* in_u, const uint8_t* in_v, int w, int h,
                       int64_t in_stride_y, int64_t in_stride_c, int nframes, uint8_t* out_y, uint8_t* out_u,
                       uint8_t* out_v, int ow, int oh, int W, int H, void* stream);
@@ -136,11 +136,12 @@ PYBIND11_MODULE(_hip, m) {
   m.attr("arch") = "gfx950";
 
   m.def("synth", [](uintptr_t y, uintptr_t u, uintptr_t v, int w, int h, int slots, int frames, int frame0,
-                    uint32_t seed, uintptr_t stream, int bit_depth) {
+                    uint32_t seed, uintptr_t stream, int bit_depth, int slot0) {
     if (bit_depth != 8 && bit_depth != 10) throw std::invalid_argument("synth: bit_depth must be 8 or 10");
-    mivc_launch_synth(P<void>(y), P<void>(u), P<void>(v), w, h, slots, frames, frame0, seed, bit_depth, S(stream));
+    mivc_launch_synth(P<void>(y), P<void>(u), P<void>(v), w, h, slots, frames, frame0, seed, bit_depth, slot0,
+                      S(stream));
   }, py::arg("y"), py::arg("u"), py::arg("v"), py::arg("w"), py::arg("h"), py::arg("slots"), py::arg("frames"),
-     py::arg("frame0"), py::arg("seed"), py::arg("stream"), py::arg("bit_depth") = 8);
+     py::arg("frame0"), py::arg("seed"), py::arg("stream"), py::arg("bit_depth") = 8, py::arg("slot0") = 0);
   m.def("prep", [](uintptr_t iy, uintptr_t iu, uintptr_t iv, int w, int h, int64_t sy, int64_t sc, int n,
                    uintptr_t oy, uintptr_t ou, uintptr_t ov, int ow, int oh, int W, int H, uintptr_t stream) {
     if (ow != w || oh != h) throw std::invalid_argument("prep: resample with ops.scale (scale.hip) first");

@@ -52,10 +52,11 @@ struct SynthGeom {
   int ow[3], oh[3];     // object tile sizes
   int frames, slots, frame0;
   uint32_t seed;
+  int slot0;            // global index of slot 0 (content depends on seed and slot0 + slot only)
 };
 
 __device__ __forceinline__ uint32_t slot_seed(const SynthGeom& g, int slot) {
-  return g.seed * 7919u + static_cast<uint32_t>(slot) * 104729u;
+  return g.seed * 7919u + static_cast<uint32_t>(g.slot0 + slot) * 104729u;
 }
 
 // ---- once per slot: background canvas (luma + 2 chroma) and object tiles
@@ -410,7 +411,7 @@ using namespace mivc::gpu;
 
 // bit_depth 8: uint8 planes; 10: uint16 planes holding 10-bit samples
 extern "C" void mivc_launch_synth(void* y, void* u, void* v, int width, int height, int slots, int frames, int frame0,
-                                  uint32_t seed, int bit_depth, void* stream) {
+                                  uint32_t seed, int bit_depth, int slot0, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   SynthGeom g{};
   g.width = width;
@@ -428,6 +429,7 @@ extern "C" void mivc_launch_synth(void* y, void* u, void* v, int width, int heig
   g.slots = slots;
   g.frame0 = frame0;
   g.seed = seed;
+  g.slot0 = slot0;
   const size_t ysz = static_cast<size_t>(g.cw) * g.ch, csz = ysz / 4;
   const size_t bytes = slots * (ysz + 2 * csz + 3 * tile_stride);
   uint8_t* ws = nullptr;

@@ -254,7 +254,7 @@ class GpuH264Decoder:
             host_buf, dev_buf = stage[k]
             L = layouts[t]
             copied[k].synchronize()            # the copy of step t - 2 has read host_buf
-            batch.pack(t, slots[t], nmb, host_buf.data_ptr(), cap, 4)
+            batch.pack(t, slots[t], nmb, host_buf.data_ptr(), cap, 8)
             with torch.cuda.stream(copy):
                 copy.wait_event(consumed[k])   # step t - 2's kernels are done with dev_buf
                 dev_buf[:L["total"]].copy_(host_buf[:L["total"]], non_blocking=True)

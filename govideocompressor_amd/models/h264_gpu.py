@@ -389,7 +389,9 @@ class GpuH264Encoder:
         self.cab_done = [torch.cuda.Event() for _ in range(2)]
         # the coder's compaction writes the slice bytes straight into these pinned buffers
         # (one per ring; a group that does not fit falls back to the device buffer + D2H)
-        self.cab_host_cap = min(comp_cap, int(os.environ.get("MIVC_CABAC_HOST_MB", 1024)) << 20)
+        # (capped by the rank's pinned budget: 8 ranks share the host, runtime/device.py)
+        from ..runtime.device import pinned_budget
+        self.cab_host_cap = min(comp_cap, int(os.environ.get("MIVC_CABAC_HOST_MB", 1024)) << 20, pinned_budget() // 4)
         self.h_cab_out = [torch.empty((self.cab_host_cap,), dtype=u8).pin_memory() for _ in range(2)]
         self.copy_pool = cf.ThreadPoolExecutor(max_workers=1)
 
@@ -981,9 +983,11 @@ class GpuH264Encoder:
 
 
 def synth_clip(slots: int, frames: int, width: int, height: int, seed: int = 0, frame0: int = 0,
-               device: str | torch.device = "cuda", bit_depth: int = 8):
+               device: str | torch.device = "cuda", bit_depth: int = 8, slot0: int = 0):
     """Generate B x F synthetic I420 frames directly in HBM (see csrc/kernels/synth.hip).
 
+    Slot ``b`` shows the content of global slot ``slot0 + b`` (a rank encoding slots
+    [r * B, (r + 1) * B) of a global batch renders exactly what one process would).
     ``bit_depth=10`` renders the same content at 10-bit precision into int16 planes
     (values 0..1023: the canvas interpolation, ramp and noise keep their low bits)."""
     if bit_depth not in (8, 10):
@@ -995,5 +999,5 @@ def synth_clip(slots: int, frames: int, width: int, height: int, seed: int = 0, 
     u = torch.empty((slots, frames, height // 2, width // 2), dtype=dt, device=dev)
     v = torch.empty_like(u)
     hip.synth(y.data_ptr(), u.data_ptr(), v.data_ptr(), width, height, slots, frames, frame0, seed & 0xFFFFFFFF,
-              torch.cuda.current_stream(dev).cuda_stream, bit_depth)
+              torch.cuda.current_stream(dev).cuda_stream, bit_depth, slot0)
     return y, u, v

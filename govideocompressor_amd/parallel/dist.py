@@ -41,7 +41,7 @@ class DistEnv:
 
     @property
     def initialized(self) -> bool:
-        return self.world > 1 and dist.is_initialized()
+        return self.backend != "none" and dist.is_initialized()
 
 
 def init(prefer_gpu: bool = True, timeout_s: int = 600) -> DistEnv:
@@ -56,7 +56,10 @@ def init(prefer_gpu: bool = True, timeout_s: int = 600) -> DistEnv:
     else:
         device = torch.device("cpu")
     env = DistEnv(rank=rank, world=world, local_rank=local, device=device)
-    if world > 1:
+    # MIVC_DIST_FORCE=1: a process group even at world 1, so the collectives themselves run
+    # (the RCCL world-1 smoke test; torchrun sets MASTER_PORT)
+    if world > 1 or os.environ.get("MIVC_DIST_FORCE") == "1":
+        os.environ.setdefault("MASTER_PORT", "29512")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # MIVC_DIST_BACKEND=gloo: host collectives even when encoding on GPUs (lets several
         # ranks share one GPU for a rehearsal of the multi-GPU flow; RCCL needs one GPU per rank)
@@ -232,8 +235,10 @@ class SegmentMerge:
             return buf
         cap = max(1 << 20, int(n * 1.25))
         if pinned:
+            from ..runtime.device import pinned_budget
             t = torch.empty((cap,), dtype=torch.uint8)
-            return t.pin_memory() if torch.cuda.is_available() else t
+            # page-locked only within the rank's budget (8 ranks share the host's RAM)
+            return t.pin_memory() if torch.cuda.is_available() and cap <= pinned_budget() // 4 else t
         return torch.empty((cap,), dtype=torch.uint8, device=device)
 
     def _pack_local(self, pieces) -> tuple["np.ndarray", list[int]]:
@@ -263,17 +268,22 @@ class SegmentMerge:
                     raise RuntimeError("segment merge: a piece does not start with an Annex-B start code")
             off += n
 
-    def run(self, pieces) -> "np.ndarray | None":
+    def run(self, pieces, sink=None) -> "np.ndarray | int | None":
         """pieces: this rank's segments (bytes, or a list of byte parts each).
         Returns the merged stream (uint8 view of a pinned buffer, valid until the next
-        call) on rank 0, ``None`` on the other ranks."""
+        call) on rank 0, ``None`` on the other ranks.  With ``sink`` (a binary file) rank 0
+        streams the merged bytes into it instead -- its own first, then every other rank's
+        through a bounded host staging buffer -- and returns the byte count: the merged
+        stream of a world-8 node never has to fit rank 0's host memory at once."""
         import numpy as np
 
         env = self.env
         local, sizes = self._pack_local(pieces)
         self._check_start_codes(local, sizes)
+        if sink is not None and env.is_main:
+            sink.write(memoryview(local))
         if not env.initialized:
-            return local
+            return int(local.size) if sink is not None else local
         dev = coll_device(env)
         n_loc = torch.tensor([local.size], dtype=torch.int64, device=dev)
         all_n = torch.empty(env.world, dtype=torch.int64, device=dev)
@@ -296,6 +306,8 @@ class SegmentMerge:
                     # the staging buffers are reused by the next call
                     torch.cuda.current_stream(dev).synchronize()
             return None
+        if sink is not None:
+            return self._recv_to_sink(per_rank, offs, dev, sink)
         self._out = self._grow(self._out, total, pinned=True)
         out_t = self._out
         if local.size:
@@ -321,3 +333,28 @@ class SegmentMerge:
         if out.size and not (bytes(out[:3]) == b"\0\0\1" or bytes(out[:4]) == b"\0\0\0\1"):
             raise RuntimeError("segment merge: merged stream does not start with a start code")
         return np.asarray(out)
+
+    def _recv_to_sink(self, per_rank: list[int], offs: list[int], dev, sink) -> int:
+        """Rank 0, streaming: every other rank's bytes (received as in ``run``) to ``sink`` in
+        rank order through a staging buffer of at most an eighth of the pinned budget."""
+        from ..runtime.device import pinned_budget
+        others = offs[-1] - per_rank[0]
+        if others:
+            self._recv = self._grow(self._recv, others, pinned=False, device=dev if dev.type == "cuda" else None)
+            ops = []
+            for r in range(1, self.env.world):
+                if per_rank[r]:
+                    lo = offs[r] - per_rank[0]
+                    ops.append(dist.P2POp(dist.irecv, self._recv[lo:lo + per_rank[r]], r))
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+            if dev.type == "cuda":
+                chunk = max(1 << 20, min(others, pinned_budget() // 8))
+                self._stage = self._grow(getattr(self, "_stage", None), chunk, pinned=True)
+                for a in range(0, others, chunk):
+                    n = min(chunk, others - a)
+                    self._stage[:n].copy_(self._recv[a:a + n])
+                    sink.write(memoryview(self._stage.numpy()[:n]))
+            else:
+                sink.write(memoryview(self._recv.numpy()[:others]))
+        return offs[-1]

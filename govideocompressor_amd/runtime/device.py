@@ -45,3 +45,29 @@ def slots_for(width: int, height: int, frames: int, info: DeviceInfo | None, cap
     per_slot = coded * 3 // 2 * (frames + 4) + coded // 256 * (64 + 816 + 400)
     by_mem = max(1, int(info.hbm_bytes * 0.6) // max(1, per_slot))
     return max(1, min(cap, by_mem, max(info.cus, 1)))
+
+
+def host_mem_total() -> int:
+    """Physical host RAM in bytes (``/proc/meminfo`` MemTotal; 64 GiB if unreadable)."""
+    try:
+        with open("/proc/meminfo") as f:
+            for line in f:
+                if line.startswith("MemTotal:"):
+                    return int(line.split()[1]) * 1024
+    except OSError:
+        pass
+    return 64 << 30
+
+
+def pinned_budget(local_world: int | None = None) -> int:
+    """Page-locked host bytes one rank may hold.
+
+    ``MIVC_PINNED_BUDGET_MB`` if set, else a quarter of host RAM shared by the ranks on this
+    host (``LOCAL_WORLD_SIZE``, torchrun's count): 8 ranks on a 2 TB MI355X node get 64 GB
+    each, one rank on a 3 GB lease box 768 MB.  Encoders size their pinned rings from it and
+    the merge falls back to pageable buffers beyond it."""
+    env = os.environ.get("MIVC_PINNED_BUDGET_MB")
+    if env:
+        return int(float(env) * (1 << 20))
+    n = local_world or int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    return max(64 << 20, host_mem_total() // 4 // max(1, n))

@@ -94,6 +94,11 @@ def _merge(rank, world, port, q):
                 pieces = [sc + bytes([rank, it]) * (5 + rank), [sc, bytes([9]) * (3 + it), bytes([rank])]]
             got = m.run(pieces)
             outs.append(None if got is None else bytes(got))
+        # streaming merge: rank 0 writes every rank's bytes to a sink instead
+        import io
+        sink = io.BytesIO() if rank == 0 else None
+        n = m.run([b"\0\0\0\1" + bytes([rank]) * (rank + 2)], sink=sink)
+        outs.append((n, sink.getvalue()) if rank == 0 else n)
         bad = None
         try:
             m.run([b"\1\2\3\4\5"])
@@ -122,6 +127,9 @@ def test_segment_merge_gloo():
             want += sc + bytes([r, it]) * (5 + r) + sc + bytes([9]) * (3 + it) + bytes([r])
         assert res[0][1][it] == want
         assert res[1][1][it] is None and res[2][1][it] is None
+    want = b"".join(sc + bytes([r]) * (r + 2) for r in range(world))
+    assert res[0][1][2] == (len(want), want)
+    assert res[1][1][2] is None and res[2][1][2] is None
     assert all(bad and "start code" in bad for _, _, bad in res)
 
 
