@@ -295,7 +295,7 @@ class GpuBackend:
         t0 = time.perf_counter()
         results: dict[str, PieceResult] = {}
         items = []
-        comp = [j for j in jobs if kind_of(j.in_path) in ("h264", "hevc", "mp4")]
+        comp = [j for j in jobs if kind_of(j.in_path) in ("h264", "hevc", "mp4", "ts", "mkv")]
         raw = [j for j in jobs if j not in comp]
         futs = {j.idx: self._io.submit(load_clip, j.in_path) for j in raw}
         if comp:

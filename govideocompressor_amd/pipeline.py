@@ -34,7 +34,7 @@ from .utils import yuv
 
 def _segments(path: str, info, world: int, slots: int, seg_frames: int | None, gop: int | None):
     """Returns (kind, segment list).  Raw: frame ranges; compressed: IDR-aligned pieces."""
-    if info.kind in ("h264", "hevc", "mp4"):
+    if info.kind in ("h264", "hevc", "mp4", "ts", "mkv"):
         from .segment.probe import split_stream
         target = seg_frames or max(1, info.frames // max(1, world * slots))
         pieces = split_stream(annexb_of(path, info.kind), target)
@@ -285,6 +285,9 @@ def encode_file(path: str, output: str, args: str = "264", backend: str = "auto"
             if info.kind == "mp4" and cfg.audio == "copy":  # the input's audio, stream-copied
                 with open(path, "rb") as f:
                     extra = mp4.file_audio(f.read())
+            elif info.kind in ("ts", "mkv") and cfg.audio == "copy":  # its AAC tracks (containers.py)
+                from .segment.containers import demux
+                extra = demux(path, info.kind).audio
             data = mp4.mux_video(stream, out_fps, cfg.codec, extra)
         else:
             data = stream

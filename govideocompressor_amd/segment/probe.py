@@ -13,12 +13,15 @@ stream itself:
   (csrc/host/hevc_dec_ps.cc)
 * ``.mp4``      -- demuxed by the native ISO-BMFF reader (``avc1`` or ``hvc1``/``hev1``
   track), then as Annex-B
+* ``.ts`` / ``.m2ts`` (MPEG-TS) and ``.mkv`` / ``.webm`` (Matroska) -- demuxed by
+  ``segment/containers.py`` (H.264 / HEVC video, AAC audio), then as Annex-B
 
 and :func:`reference_seconds` reproduces the reference's integer arithmetic.
 """
 from __future__ import annotations
 
 import os
+import struct
 from dataclasses import asdict, dataclass
 
 from ..utils import yuv
@@ -31,7 +34,7 @@ class ProbeError(ValueError):
 @dataclass
 class MediaInfo:
     path: str
-    kind: str           # yuv | y4m | h264 | hevc | mp4
+    kind: str           # yuv | y4m | h264 | hevc | mp4 | ts | mkv
     width: int
     height: int
     fps: float
@@ -65,9 +68,18 @@ def kind_of(path: str) -> str:
         return "hevc"
     if ext in (".mp4", ".m4v", ".mov"):
         return "mp4"
+    if ext in (".ts", ".m2ts", ".mts", ".m2t"):
+        return "ts"
+    if ext in (".mkv", ".webm", ".mk3d"):
+        return "mkv"
     # sniff
     with open(path, "rb") as f:
-        head = f.read(16)
+        head = f.read(189)
+    from .containers import is_mkv, is_ts
+    if is_ts(head):
+        return "ts"
+    if is_mkv(head):
+        return "mkv"
     if head.startswith(b"YUV4MPEG2"):
         return "y4m"
     if head[:4] in (b"\x00\x00\x00\x01",) or head[:3] == b"\x00\x00\x01":
@@ -75,7 +87,7 @@ def kind_of(path: str) -> str:
         return "hevc" if is_hevc_annexb(head) else "h264"
     if head[4:8] == b"ftyp":
         return "mp4"
-    raise ProbeError(f"cannot tell the container of {path}; use .yuv/.y4m/.264/.265/.mp4")
+    raise ProbeError(f"cannot tell the container of {path}; use .yuv/.y4m/.264/.265/.mp4/.ts/.mkv")
 
 
 def codec_of(stream: bytes) -> str:
@@ -98,6 +110,12 @@ def annexb_of(path: str, kind: str | None = None) -> bytes:
             raise ProbeError(f"{path}: {e}") from None
     if kind in ("h264", "hevc"):
         return data
+    if kind in ("ts", "mkv"):
+        from .containers import demux
+        try:
+            return demux(data, kind).annexb
+        except (ValueError, IndexError, struct.error) as e:
+            raise ProbeError(f"{path}: {e}") from None
     raise ProbeError(f"{path} is not a compressed stream")
 
 

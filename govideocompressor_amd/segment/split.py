@@ -31,6 +31,7 @@ from . import plan as P
 from .probe import MediaInfo, annexb_of, probe, reference_seconds, split_stream, stream_frames
 
 PIECE_RE = re.compile(r"^([+-]?[0-9]+)\.(mp4|264|h264|265|hevc|y4m)$")
+CONTAINERS = ("mp4", "ts", "mkv")  # inputs whose pieces are written as MP4 (with their audio)
 RAW_DEFAULT_SECONDS = 2.0
 
 
@@ -67,7 +68,7 @@ def split(path: str, size_mb: int = 10, seconds: float | None = None, frames: in
     info: MediaInfo = probe(path, width, height, fps, bit_depth)
     d = os.path.join(out_root, split_dir_name(path))
     os.makedirs(d, exist_ok=True)
-    compressed = info.kind in ("h264", "hevc", "mp4")
+    compressed = info.kind in ("h264", "hevc", *CONTAINERS)
     if frames:
         seg_frames = int(frames)
         seg_s = seg_frames / info.fps
@@ -87,19 +88,28 @@ def split(path: str, size_mb: int = 10, seconds: float | None = None, frames: in
         from ..ops import native
         from . import mp4
         h = native.host()
-        pieces = split_stream(annexb_of(path, info.kind), seg_frames)
         audio, pts = [], []
         if info.kind == "mp4":
+            pieces = split_stream(annexb_of(path, info.kind), seg_frames)
             # -acodec copy -map 0:0 -map 0:1 (server.go:199-200): each piece carries the audio
             # samples of its own time span, cut at the video piece boundaries
             with open(path, "rb") as f:
                 tracks = mp4.read(f.read())
             audio = mp4.audio_tracks(tracks)
             pts = mp4.video_track(tracks).pts_seconds()
+        elif info.kind in ("ts", "mkv"):
+            from .containers import demux
+            dm = demux(path, info.kind)
+            pieces = split_stream(dm.annexb, seg_frames)
+            audio, pts = dm.audio, dm.pts
+            for what in dm.dropped:
+                log(f"note: {what} is not carried into the pieces")
+        else:
+            pieces = split_stream(annexb_of(path, info.kind), seg_frames)
         frames = [stream_frames(pc) for pc in pieces]
         starts = [sum(frames[:i]) for i in range(len(pieces))]
         for i, pc in enumerate(pieces):
-            if info.kind == "mp4":
+            if info.kind in CONTAINERS:
                 t0 = pts[starts[i]] if starts[i] < len(pts) else None
                 t1 = pts[starts[i + 1]] if i + 1 < len(pieces) and starts[i + 1] < len(pts) else None
                 extra = [mp4.cut(a, 0.0 if i == 0 else t0, t1) for a in audio] if t0 is not None else []

@@ -1,0 +1,104 @@
+"""MPEG-TS and Matroska input (segment/containers.py): demux, probe, split with audio.
+
+The reference's splitter reads whatever ffmpeg opens (server.go:199-201, 241).  No ffmpeg
+or sample files exist here, so the inputs come from this repo's own minimal writers
+(utils/container_synth.py): H.264 (CABAC) and HEVC streams, AAC audio
+in ADTS (TS) or laced Matroska blocks.  Real-world TS/MKV files are parity unpinned."""
+import numpy as np
+import pytest
+
+from govideocompressor_amd.segment import containers as C
+from govideocompressor_amd.utils import container_synth as CS
+
+
+def _aac(n, seed=0):
+    rng = np.random.default_rng(seed)
+    return [bytes(rng.integers(0, 256, int(rng.integers(60, 400)), dtype=np.uint8)) for _ in range(n)]
+
+
+def _h264(host, frames=12, gop=4):
+    from govideocompressor_amd.utils.h264_synth import random_stream
+    return b"".join(random_stream(host, 96, 64, gop, seed=40 + k, cabac=True) for k in range(frames // gop))
+
+
+def _hevc(host, frames=8, gop=4):
+    from govideocompressor_amd.utils.hevc_synth import random_stream
+    return b"".join(random_stream(host, 96, 64, gop, seed=50 + k, intra_in_p=0.2, mv_range=8)[0]
+                    for k in range(frames // gop))
+
+
+def _same_pictures(host, a: bytes, b: bytes, hevc: bool):
+    if hevc:
+        pa = [p["y"] for p in host.hevc_decode_full(a, True, False)]
+        pb = [p["y"] for p in host.hevc_decode_full(b, True, False)]
+    else:
+        pa = [p["i420"] for p in host.decode(a)]
+        pb = [p["i420"] for p in host.decode(b)]
+    assert len(pa) == len(pb) > 0
+    for x, y in zip(pa, pb):
+        assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("codec", ["h264", "hevc"])
+def test_ts_demux_round_trip(host, codec):
+    stream = _h264(host) if codec == "h264" else _hevc(host)
+    frames = _aac(40)
+    ts = CS.write_ts(stream, 25.0, frames)
+    assert len(ts) % 188 == 0 and C.is_ts(ts[:189])
+    dm = C.ts_demux(ts)
+    assert dm.codec == codec
+    _same_pictures(host, stream, dm.annexb, codec == "hevc")
+    n = 12 if codec == "h264" else 8
+    assert len(dm.pts) == n and dm.pts[0] == 0.0 and abs(max(dm.pts) - (n - 1) / 25.0) < 1e-3
+    assert len(dm.audio) == 1 and dm.audio[0].samples == frames
+    assert dm.audio[0].codec == b"mp4a" and dm.audio[0].timescale == 48000
+
+
+@pytest.mark.parametrize("codec,lacing", [("h264", "ebml"), ("hevc", "xiph")])
+def test_mkv_demux_round_trip(host, codec, lacing):
+    stream = _h264(host) if codec == "h264" else _hevc(host)
+    frames = _aac(37, seed=3)
+    mkv = CS.write_mkv(stream, 25.0, frames, lacing=lacing)
+    assert C.is_mkv(mkv[:4])
+    dm = C.mkv_demux(mkv)
+    assert dm.codec == codec and (dm.width, dm.height) == (96, 64)
+    _same_pictures(host, stream, dm.annexb, codec == "hevc")
+    assert dm.pts[0] == 0.0 and sorted(dm.pts) == [round(i / 25.0, 3) for i in range(len(dm.pts))]
+    assert len(dm.audio) == 1 and dm.audio[0].samples == frames
+
+
+def test_demuxers_reject_corrupt_input():
+    with pytest.raises(ValueError):
+        C.ts_demux(b"\x47" + b"\x00" * 187 + b"\x46" + b"\x00" * 187)
+    with pytest.raises(ValueError):
+        C.mkv_demux(b"\x1a\x45\xdf\xa3\x88\x00")
+    with pytest.raises(ValueError):
+        C.ts_demux(b"\x47\x00\x00\x10" + b"\x00" * 184)  # no PAT / video
+
+
+@pytest.mark.parametrize("ext", ["ts", "mkv"])
+def test_split_ts_mkv_into_mp4_pieces_with_audio(tmp_path, host, ext):
+    """``server s clip.ts|clip.mkv``: IDR-aligned MP4 pieces, each with the AAC frames of its
+    time span; the pieces' video decodes to the whole stream's pictures."""
+    from govideocompressor_amd.segment import mp4, probe as PR
+    from govideocompressor_amd.segment.split import split
+    stream = _h264(host)
+    frames = _aac(60, seed=5)
+    data = CS.write_ts(stream, 25.0, frames) if ext == "ts" else CS.write_mkv(stream, 25.0, frames)
+    src = tmp_path / f"clip.{ext}"
+    src.write_bytes(data)
+    info = PR.probe(str(src))
+    assert (info.kind, info.codec, info.width, info.height, info.frames) == (ext, "h264", 96, 64, 12)
+    d, n = split(str(src), frames=4, out_root=str(tmp_path), log=lambda s: None)
+    assert n == 3
+    got_frames, got_audio = [], []
+    for i in range(n):
+        tr = mp4.read((tmp_path / d / f"{i}.mp4").read_bytes())
+        got_frames += [p["i420"] for p in host.decode(mp4.video_to_annexb(mp4.video_track(tr)))]
+        au = mp4.audio_tracks(tr)
+        got_audio += au[0].samples if au else []
+    want = [p["i420"] for p in host.decode(stream)]
+    assert len(got_frames) == len(want) == 12
+    assert all(np.array_equal(a, b) for a, b in zip(got_frames, want))
+    # audio: every AAC frame exactly once, in order (the last piece takes the tail)
+    assert got_audio == frames

@@ -24,7 +24,10 @@ def seeds(host):
     from govideocompressor_amd.utils import hevc_synth
     hevc, _ = hevc_synth.random_stream(host, 64, 64, 2, seed=4)
     box = mp4.write([mp4.h264_track(cavlc, 30.0)])
-    return dict(cavlc=cavlc, cabac=cabac, hevc=hevc, mp4=box)
+    from govideocompressor_amd.utils import container_synth as CS
+    aac = [bytes([k]) * (40 + k) for k in range(12)]
+    return dict(cavlc=cavlc, cabac=cabac, hevc=hevc, mp4=box, ts=CS.write_ts(cabac, 30.0, aac),
+                mkv=CS.write_mkv(hevc, 30.0, aac))
 
 
 def _mutate(data: bytes, ops) -> bytes:
@@ -88,3 +91,11 @@ def test_fuzz_random_bytes(host, data):
         _try(fn, data)
     _try(host.decode, b"\x00\x00\x00\x01\x67" + data)
     _try(host.decode, b"\x00\x00\x00\x01\x65" + data)
+
+
+@_SETTINGS
+@given(ops=_ops, which=st.sampled_from(["ts", "mkv"]))
+def test_fuzz_ts_mkv_demux(host, seeds, ops, which):
+    from govideocompressor_amd.segment import containers
+    data = _mutate(seeds[which], ops)
+    _try(containers.ts_demux if which == "ts" else containers.mkv_demux, data)
