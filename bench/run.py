@@ -233,7 +233,10 @@ def _hevc_run(args, W, H, B, F, bd, crf, two_pass_kbps=None, fps=30.0, resident=
                         pass2_vs_target=round(got / share, 4), exponent=round(fb.e, 3),
                         feedback_updates=len(fb.history))
 
+    enc.stage_timer.enabled = True                                     # HIP-event stage times, warmup only
     res, info = step(-1, quality=True)                                 # warmup (+ PSNR)
+    stage_ms = {k: round(v["s"] * 1000.0, 1) for k, v in enc.stage_timer.summary().items()}
+    enc.stage_timer.enabled = False
     psnr = float(np.mean([r.psnr_y for r in res]))
     torch.cuda.synchronize()
     D.barrier(env)
@@ -249,6 +252,7 @@ def _hevc_run(args, W, H, B, F, bd, crf, two_pass_kbps=None, fps=30.0, resident=
     fps_out = B * F * args.steps * env.world / dt
     return fps_out, dict(psnr_y_warmup=round(psnr, 2), kbps_per_stream=round(bits / (B * F) * fps / 1000, 1),
                          ms_per_step=round(dt / args.steps * 1000, 1), timings=enc.timings, rc=info, world=env.world,
+                         stage_device_ms_warmup=stage_ms, encoder_stats={k: round(v, 4) for k, v in enc.stats.items()},
                          resident_clip_gb=round(clip_gb, 1) if resident else None)
 
 

@@ -258,6 +258,7 @@ SliceHeader slice_header_from(const EncoderConfig& c, const SPS& sps, const PPS&
   sh.num_ref_idx_override = (sh.num_ref_idx_l0_active != pps.num_ref_idx_l0_default ||
                              sh.num_ref_idx_l1_active != pps.num_ref_idx_l1_default) ? 1 : 0;
   sh.direct_spatial = dget<int>(fp, "direct_spatial", 1);
+  sh.first_mb = dget<int>(fp, "first_mb", 0);  // several slices per picture: each writes its MB range
   sh.cabac_init_idc = 0;
   (void)sps;
   return sh;
@@ -527,13 +528,15 @@ PYBIND11_MODULE(_host, m) {
         if (hdr.size() != static_cast<py::ssize_t>(nmb * sizeof(MbHeader))) throw std::runtime_error("header array has wrong size");
         if (coef.size() != static_cast<py::ssize_t>(nmb) * kCoefPerMb) throw std::runtime_error("coef array has wrong size");
         SliceHeader sh = slice_header_from(c, sps, pps, fp);
+        const int num = dget<int>(fp, "num_mbs", nmb - sh.first_mb);  // MBs of this slice
+        if (sh.first_mb < 0 || num < 1 || sh.first_mb + num > nmb) throw std::runtime_error("write_slice: bad MB range");
         SliceStats st;
         std::vector<uint8_t> nal;
         {
           py::gil_scoped_release rel;
           const MbHeader* mh = reinterpret_cast<const MbHeader*>(hdr.data());
-          nal = pps.entropy_coding_mode ? write_slice_nal_cabac(sps, pps, sh, mh, coef.data(), nmb, &st)
-                                        : write_slice_nal(sps, pps, sh, mh, coef.data(), nmb, &st);
+          nal = pps.entropy_coding_mode ? write_slice_nal_cabac(sps, pps, sh, mh, coef.data(), num, &st)
+                                        : write_slice_nal(sps, pps, sh, mh, coef.data(), num, &st);
         }
         py::dict stats;
         stats["bits"] = st.bits;

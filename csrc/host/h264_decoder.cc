@@ -456,12 +456,23 @@ struct Decoder::Impl {
       d.pic_id = cur->id;
       d.ref_id = pic_ref_id;
       d.nal_ref = cur->nal_ref != 0;
-      d.alpha_off = slices.empty() ? 0 : slices[0].alpha_off;
-      d.beta_off = slices.empty() ? 0 : slices[0].beta_off;
+      // several slices reconstruct on the GPU when they share what the kernels take per
+      // picture: reference lists / weights (checked as each slice starts), the filter offsets
+      // of the filtered slices (boundary strengths already carry disable_deblocking_filter_idc
+      // 1 / 2 per edge) and the chroma QP offset; MbHeader::pad0 carries the slice for the
+      // intra kernel's neighbour availability
+      const SliceParams* f = nullptr;
+      bool ok = cur->gpu_ok && cur->nslices <= 255 && !cur->mmco5;
+      for (const SliceParams& sp2 : slices) {
+        ok = ok && sp2.cb_off == sp2.cr_off && sp2.cb_off == slices[0].cb_off;
+        if (sp2.disable_idc == 1) continue;
+        if (!f) f = &sp2;
+        ok = ok && sp2.alpha_off == f->alpha_off && sp2.beta_off == f->beta_off;
+      }
+      d.alpha_off = f ? f->alpha_off : 0;
+      d.beta_off = f ? f->beta_off : 0;
       d.chroma_qp_offset = slices.empty() ? 0 : slices[0].cb_off;
-      d.deblock = slices.empty() ? 1 : (slices[0].disable_idc != 1);
-      bool ok = cur->gpu_ok && cur->nslices == 1 && !cur->mmco5;
-      for (const SliceParams& sp2 : slices) ok = ok && sp2.cb_off == sp2.cr_off && sp2.disable_idc != 2;
+      d.deblock = f != nullptr;
       d.gpu_ok = ok;
       d.poc = cur->poc;
       d.sub = std::move(cur->rec_sub);
@@ -1050,6 +1061,7 @@ struct Decoder::Impl {
     h.chroma_mode = static_cast<uint8_t>(chroma_mode);
     h.flags = static_cast<uint8_t>(t8 ? MBF_T8x8 : 0);
     h.sub_direct = cur->direct[addr];
+    h.pad0 = static_cast<uint8_t>(slice_idx);  // slice of the MB (GPU intra availability)
     bool quad_uniform = true;
     for (int l = 0; l < 2; ++l)
       for (int q = 0; q < 4; ++q) {
@@ -2494,6 +2506,14 @@ struct Decoder::Impl {
 
   // parse-only: the slice's reference lists (picture ids) and weighted-prediction table
   void record_lists_and_weights() {
+    // a later slice of the picture must use the same lists and weights (one table per
+    // picture on the GPU): compare with the first slice's
+    std::vector<int32_t> prev_ids;
+    std::vector<int16_t> prev_wp;
+    if (cur->nslices > 1) {
+      prev_ids.swap(cur->list_ids);
+      prev_wp.swap(cur->wp);
+    }
     cur->list_ids.assign(64, -1);
     for (int l = 0; l < 2; ++l)
       for (size_t i = 0; i < list[l].size() && i < 32; ++i) cur->list_ids[l * 32 + i] = list[l][i]->id;
@@ -2521,6 +2541,7 @@ struct Decoder::Impl {
           w[kWpImp + (i * 8 + j) * 2 + 1] = static_cast<int16_t>(implicit_w[i][j][1]);
         }
     }
+    if (cur->nslices > 1 && (prev_ids != cur->list_ids || prev_wp != cur->wp)) cur->gpu_ok = false;
   }
 
   // parse-only: boundary strength of every filtered edge segment (deblock.hip reads these

@@ -74,7 +74,7 @@ int mivc_launch_scale(const void* in, int w, int h, long long in_stride, long lo
 void mivc_launch_hevc_intra(int B, int W, int H, const uint16_t* sy, const uint16_t* su, const uint16_t* sv,
                             uint16_t* ry, uint16_t* ru, uint16_t* rv, void* ctu, void* cu, int16_t* cy, int16_t* cu_,
                             int16_t* cv, const int* qp, const int8_t* run, int* cand, int bd, int analyze, int recon,
-                            int* err, int sdh, void* stream);
+                            int* err, int sdh, const uint8_t* ctb_mask, void* stream);
 void mivc_launch_hevc_inter(int B, int W, int H, const uint16_t* sy, const uint16_t* su, const uint16_t* sv,
                             const uint16_t* fy, const uint16_t* fu, const uint16_t* fv, uint16_t* ry, uint16_t* ru,
                             uint16_t* rv, void* ctu, void* cu, int16_t* cy, int16_t* cu_, int16_t* cv, const int* qp,
@@ -292,14 +292,15 @@ PYBIND11_MODULE(_hip, m) {
   m.def("hevc_intra", [](int B, int W, int H, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t ry, uintptr_t ru,
                          uintptr_t rv, uintptr_t ctu, uintptr_t cu, uintptr_t cy, uintptr_t cu_, uintptr_t cv,
                          uintptr_t qp, uintptr_t run, uintptr_t cand, int bd, int analyze, int recon, uintptr_t err,
-                         uintptr_t stream, int sdh) {
+                         uintptr_t stream, int sdh, uintptr_t ctb_mask) {
     mivc_launch_hevc_intra(B, W, H, P<uint16_t>(sy), P<uint16_t>(su), P<uint16_t>(sv), P<uint16_t>(ry), P<uint16_t>(ru),
                            P<uint16_t>(rv), P<void>(ctu), P<void>(cu), P<int16_t>(cy), P<int16_t>(cu_), P<int16_t>(cv),
-                           P<int>(qp), P<int8_t>(run), P<int>(cand), bd, analyze, recon, P<int>(err), sdh, S(stream));
+                           P<int>(qp), P<int8_t>(run), P<int>(cand), bd, analyze, recon, P<int>(err), sdh,
+                           P<uint8_t>(ctb_mask), S(stream));
   }, py::arg("B"), py::arg("W"), py::arg("H"), py::arg("sy"), py::arg("su"), py::arg("sv"), py::arg("ry"), py::arg("ru"),
      py::arg("rv"), py::arg("ctu"), py::arg("cu"), py::arg("cy"), py::arg("cu_"), py::arg("cv"), py::arg("qp"),
      py::arg("run"), py::arg("cand"), py::arg("bd"), py::arg("analyze"), py::arg("recon"), py::arg("err"),
-     py::arg("stream"), py::arg("sdh") = 0);
+     py::arg("stream"), py::arg("sdh") = 0, py::arg("ctb_mask") = 0);
   m.def("hevc_inter", [](int B, int W, int H, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t fy, uintptr_t fu,
                          uintptr_t fv, uintptr_t ry, uintptr_t ru, uintptr_t rv, uintptr_t ctu, uintptr_t cu, uintptr_t cy,
                          uintptr_t cu_, uintptr_t cv, uintptr_t qp, uintptr_t run, uintptr_t cand, uintptr_t mv,

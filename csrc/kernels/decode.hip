@@ -433,16 +433,21 @@ __device__ __forceinline__ void decode_intra_mb(const DecodeArgs& a, DecIntraSha
   const uint32_t mask = __builtin_amdgcn_readfirstlane(a.mask[o]);
   const uint32_t off = __builtin_amdgcn_readfirstlane(a.off[o]);
   uint8_t* recy = rec_plane(a, a.rec_y, slot, g.ysize());
+  // neighbour MBs are available when inside the picture and in this MB's slice (the
+  // parser's records carry the slice index in pad0; 6.4.8)
+  const int sl = __builtin_amdgcn_readfirstlane(H->pad0);
+  auto same = [&](int dx, int dy) { return static_cast<int>(H[dy * g.wmb + dx].pad0) == sl; };
   int mbav = 0;
-  if (mx > 0) mbav |= h264::AV_LEFT;
-  if (my > 0) mbav |= h264::AV_TOP;
-  if (mx > 0 && my > 0) mbav |= h264::AV_TOPLEFT;
-  if (my > 0 && mx < g.wmb - 1) mbav |= h264::AV_TOPRIGHT;
+  if (mx > 0 && same(-1, 0)) mbav |= h264::AV_LEFT;
+  if (my > 0 && same(0, -1)) mbav |= h264::AV_TOP;
+  if (mx > 0 && my > 0 && same(-1, -1)) mbav |= h264::AV_TOPLEFT;
+  if (my > 0 && mx < g.wmb - 1 && same(1, -1)) mbav |= h264::AV_TOPRIGHT;
 
   // ---- stage the reconstructed neighbourhood
   if (lane < 21) {  // tile row 0: x = X0-1 .. X0+19
     const int x = X0 - 1 + lane;
-    const bool ok = my > 0 && x >= 0 && x < W && (lane < 17 || (mbav & h264::AV_TOPRIGHT));
+    const bool ok = x < W && (lane == 0 ? (mbav & h264::AV_TOPLEFT) : lane < 17 ? (mbav & h264::AV_TOP)
+                                                                         : (mbav & h264::AV_TOPRIGHT));
     S.tile[lane] = ok ? recy[static_cast<size_t>(Y0 - 1) * W + x] : 0;
   } else if (lane >= 24 && lane < 32) {  // x = X0+16 .. X0+23 (Intra8x8 block 1's top-right)
     const int x = X0 + 16 + (lane - 24);
@@ -451,19 +456,19 @@ __device__ __forceinline__ void decode_intra_mb(const DecodeArgs& a, DecIntraSha
   } else if (lane >= 32 && lane < 48) {  // tile col 0, rows 1..16
     const int r = lane - 32;
     uint8_t v = 0;
-    if (mx > 0) v = S.saved_x == mx - 1 ? S.saved_y[r] : recy[static_cast<size_t>(Y0 + r) * W + X0 - 1];
+    if (mbav & h264::AV_LEFT) v = S.saved_x == mx - 1 ? S.saved_y[r] : recy[static_cast<size_t>(Y0 + r) * W + X0 - 1];
     S.tile[(r + 1) * TS] = v;
   }
   if (lane < 18) {
     const int c = lane / 9, i = lane % 9;
     const uint8_t* rc = rec_plane(a, c == 0 ? a.rec_u : a.rec_v, slot, g.csize());
     const int x = mx * 8 - 1 + i;
-    S.ctop[c][i] = (my > 0 && x >= 0) ? rc[static_cast<size_t>(my * 8 - 1) * cw + x] : 0;
+    S.ctop[c][i] = (i == 0 ? (mbav & h264::AV_TOPLEFT) : (mbav & h264::AV_TOP)) ? rc[static_cast<size_t>(my * 8 - 1) * cw + x] : 0;
   } else if (lane >= 48) {
     const int c = (lane - 48) >> 3, i = (lane - 48) & 7;
     const uint8_t* rc = rec_plane(a, c == 0 ? a.rec_u : a.rec_v, slot, g.csize());
     uint8_t v = 0;
-    if (mx > 0) v = S.saved_x == mx - 1 ? S.saved_c[c][i] : rc[static_cast<size_t>(my * 8 + i) * cw + mx * 8 - 1];
+    if (mbav & h264::AV_LEFT) v = S.saved_x == mx - 1 ? S.saved_c[c][i] : rc[static_cast<size_t>(my * 8 + i) * cw + mx * 8 - 1];
     S.cleft[c][i] = v;
   }
   wave_sync();

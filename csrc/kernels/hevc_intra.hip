@@ -35,7 +35,11 @@ struct HevcIntraArgs {
   int* err;
   int sdh;                                // sign data hiding in the quantiser
   int nxn_in_p;                           // evaluate PART_NxN in P pictures too
+  const uint8_t* ctb_mask;                // [B, nctb] analyse only where nonzero (P pictures: the CTBs
+                                          // where intra may beat the motion search); null = every CTB
 };
+
+constexpr int kNoIntra = 1 << 26;  // candidate cost of a CTB the analysis skipped (inter decisive)
 
 // luma neighbour (xr, yr) of a CTB-relative block position: z-scan availability (6.4.1)
 // at the 4x4 minimum-TB granularity; zcur = z-order index (zorder4) of the current
@@ -177,6 +181,15 @@ __global__ __launch_bounds__(256, 4) void hevc_intra_analyze(HevcIntraArgs a) {
   // PART_NxN candidates in I pictures (and P pictures when asked): intra CUs are rare in P
   // pictures and 8x8 ones rarer, the 4x4 search is a third of this kernel
   const bool nxn_on = a.run[slot] == 1 || a.nxn_in_p;
+  if (a.ctb_mask && !a.ctb_mask[static_cast<size_t>(slot) * g.nctb() + ci]) {
+    // inter is decisive in this CTB: no intra candidates (a cost no inter cost reaches, DC)
+    if (a.cand && threadIdx.x < kCandStride) {
+      int* cd = a.cand + (static_cast<size_t>(slot) * g.nctb() + ci) * kCandStride;
+      const int t = threadIdx.x;
+      cd[t] = t < kCuCount ? kNoIntra : (t < 2 * kCuCount ? 1 : 0);
+    }
+    return;
+  }
   const int rx = ci % g.wctb, ry = ci / g.wctb;
   const int X0 = rx * 32, Y0 = ry * 32;
   const int tid = threadIdx.x;
@@ -700,14 +713,17 @@ static HevcIntraArgs make_intra_args(int B, int W, int H, const uint16_t* sy, co
   a.err = err;
   a.sdh = sdh;
   a.nxn_in_p = 0;
+  a.ctb_mask = nullptr;
   return a;
 }
 
 extern "C" void mivc_launch_hevc_intra(int B, int W, int H, const uint16_t* sy, const uint16_t* su, const uint16_t* sv,
                                        uint16_t* ry, uint16_t* ru, uint16_t* rv, void* ctu, void* cu, int16_t* cy,
                                        int16_t* cu_, int16_t* cv, const int* qp, const int8_t* run, int* cand, int bd,
-                                       int analyze, int recon, int* err, int sdh, void* stream) {
+                                       int analyze, int recon, int* err, int sdh, const uint8_t* ctb_mask,
+                                       void* stream) {
   HevcIntraArgs a = make_intra_args(B, W, H, sy, su, sv, ry, ru, rv, ctu, cu, cy, cu_, cv, qp, run, cand, bd, err, sdh);
+  a.ctb_mask = ctb_mask;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (analyze) hipLaunchKernelGGL(hevc_intra_analyze, dim3(a.g.nctb(), B), dim3(256), 0, s, a);
   if (recon) hipLaunchKernelGGL(hevc_intra_recon, dim3(B), dim3(64 * kHevcIntraWaves), 0, s, a);

@@ -83,6 +83,11 @@ class HevcParams:
     tu_inter_depth: int = 0
     # general_level_idc (30 x level, -level); 0 = the lowest level the size / rate fits
     level_idc: int = 0
+    # P pictures: run the open-loop intra analysis only on CTBs where intra may still win --
+    # some 16x16 block whose motion cost is not below half the motion search's own Intra16x16
+    # estimate (a lower bound of the finer intra search) plus the intra bias; elsewhere inter
+    # is decisive and the CTB gets no intra candidates
+    intra_gate: bool = True
 
     def adaptive_qp(self) -> bool:
         return self.aq_strength > 0 or (self.cutree and self.lookahead and self.crf is not None)
@@ -181,6 +186,21 @@ class GpuHevcEncoder:
         self.pool = cf.ThreadPoolExecutor(max_workers=1)
         self.timings: dict[str, float] = {}
         self.stats: dict[str, float] = {}
+        self.ctb_need = torch.ones((B, self.nctb), dtype=torch.uint8, device=dev)
+        # per-stage device time (HIP events, resolved once per encode): MIVC_STAGE_TIMING=1
+        from ..obs.timers import EventTimer
+        self.stage_timer = EventTimer(enabled=os.environ.get("MIVC_STAGE_TIMING", "0") == "1")
+
+    def _intra_gate(self) -> torch.Tensor:
+        """[B, nctb] uint8: CTBs of a P picture where intra may beat the motion search (see
+        ``HevcParams.intra_gate``); the decision mirrors hevc_p_decide's costs."""
+        bd = self.p.bit_depth
+        lam = torch.floor(0.755 * torch.exp2((self.qp.float() - 12.0) / 6.0) * float(1 << (bd - 8)) + 0.5)[:, None]
+        inter = self.me_cost.float() * float(1 << (bd - 8)) + 3.0 * lam
+        intra_lb = self.me_intra.float() * float(1 << (bd - 8)) * 0.5 + float(self.p.intra_bias_p) * lam
+        need = (inter >= intra_lb).view(self.B, self.hctb, 2, self.wctb, 2)
+        self.ctb_need.copy_(need.any(dim=4).any(dim=2).view(self.B, self.nctb))
+        return self.ctb_need
 
     def _host_buffers(self):
         if self.host_bufs is None:
@@ -297,6 +317,8 @@ class GpuHevcEncoder:
         p = self._p
         s = self._stream()
         bd = self.p.bit_depth
+        st = self.stage_timer
+        gate_sum: list[torch.Tensor] = []
         for t in range(F):
             t0 = time.perf_counter()
             if rate_fb is not None and t > 0:
@@ -319,9 +341,10 @@ class GpuHevcEncoder:
             if self._cutree is not None and self.p.adaptive_qp():
                 ct = self._cutree
                 extra, estride, erows = ct.data_ptr() + t * ct.shape[2] * 4, ct.shape[1] * ct.shape[2], self._cutree_rows
-            self.hip.hevc_aq(B, self.W, self.H, bd, p(self.src[0]), p(self.src[1]), p(self.src[2]), p(self.qp),
-                             float(self.p.aq_strength) if self.p.adaptive_qp() else 0.0, extra, estride, erows,
-                             p(self.ctb_qp), p(self.mb_aq), s)
+            with st("aq"):
+                self.hip.hevc_aq(B, self.W, self.H, bd, p(self.src[0]), p(self.src[1]), p(self.src[2]), p(self.qp),
+                                 float(self.p.aq_strength) if self.p.adaptive_qp() else 0.0, extra, estride, erows,
+                                 p(self.ctb_qp), p(self.mb_aq), s)
             cur, ref = self.rec[t % 2], self.rec[(t + 1) % 2]
             kb = t % 2
             # the copy-out of step t - 2 must have read these buffers before they are rewritten
@@ -333,40 +356,52 @@ class GpuHevcEncoder:
             if idr:
                 self.run.fill_(1)
                 self.prev_mv.zero_()  # no motion predictors across a closed GOP (or from an earlier call)
-                self.hip.hevc_intra(*intra_args, 1, 1, p(self.err), s, int(self.p.sdh))
+                with st("intra_i"):
+                    self.hip.hevc_intra(*intra_args, 1, 1, p(self.err), s, int(self.p.sdh))
             else:
                 self.run.fill_(2)
-                self.hip.hevc_intra(*intra_args, 1, 0, p(self.err), s, int(self.p.sdh))   # open-loop intra candidates
-                self.hip.hevc_proxy8(p(ref[0]), p(self.ref8), ref[0].numel(), bd - 8, s)
-                self.hip.me(B, self.wmb, self.hmb, p(self.src8), p(self.ref8), p(self.prev_mv), p(self.mv),
-                            p(self.me_cost), p(self.me_pred), p(self.me_intra), p(self.qp), self.p.me_range,
-                            self.p.subpel, s, p(self.me_hp), p(self.mb_aq))
-                for it in range(int(self.p.merge_refine)):
-                    a_, b_ = (self.mv, self.mv_tmp) if it % 2 == 0 else (self.mv_tmp, self.mv)
-                    self.hip.hevc_merge_refine(B, self.wmb, self.hmb, p(self.src8), p(self.ref8), p(self.me_hp), p(a_),
-                                               p(b_), p(self.me_cost), p(self.prev_mv), p(self.qp), p(self.mb_aq), s)
-                if int(self.p.merge_refine) % 2:
-                    self.mv.copy_(self.mv_tmp)
+                with st("me"):
+                    self.hip.hevc_proxy8(p(ref[0]), p(self.ref8), ref[0].numel(), bd - 8, s)
+                    self.hip.me(B, self.wmb, self.hmb, p(self.src8), p(self.ref8), p(self.prev_mv), p(self.mv),
+                                p(self.me_cost), p(self.me_pred), p(self.me_intra), p(self.qp), self.p.me_range,
+                                self.p.subpel, s, p(self.me_hp), p(self.mb_aq))
+                with st("merge_refine"):
+                    for it in range(int(self.p.merge_refine)):
+                        a_, b_ = (self.mv, self.mv_tmp) if it % 2 == 0 else (self.mv_tmp, self.mv)
+                        self.hip.hevc_merge_refine(B, self.wmb, self.hmb, p(self.src8), p(self.ref8), p(self.me_hp),
+                                                   p(a_), p(b_), p(self.me_cost), p(self.prev_mv), p(self.qp),
+                                                   p(self.mb_aq), s)
+                    if int(self.p.merge_refine) % 2:
+                        self.mv.copy_(self.mv_tmp)
                 if cuts_h[:, t].any():  # scene cut: every CU of these slots goes intra
                     self.me_cost.masked_fill_(cuts_d[t][:, None], 1 << 26)
-                self.hip.hevc_inter(B, self.W, self.H, p(self.src[0]), p(self.src[1]), p(self.src[2]), p(ref[0]),
-                                    p(ref[1]), p(ref[2]), p(cur[0]), p(cur[1]), p(cur[2]), p(self.ctu), p(self.cu),
-                                    p(self.coef[0]), p(self.coef[1]), p(self.coef[2]), p(self.ctb_qp), p(self.run),
-                                    p(self.cand), p(self.mv), p(self.me_cost), bd, s, int(self.p.tu_inter_depth),
-                                    int(self.p.sdh), int(self.p.intra_bias_p))
-                self.hip.hevc_intra(*intra_args, 0, 1, p(self.err), s, int(self.p.sdh))   # intra CUs, wavefront
+                with st("intra_analyze"):  # open-loop intra candidates where intra may still win
+                    mask = p(self._intra_gate()) if self.p.intra_gate else 0
+                    if mask:
+                        gate_sum.append(self.ctb_need.sum(dtype=torch.int64))
+                    self.hip.hevc_intra(*intra_args, 1, 0, p(self.err), s, int(self.p.sdh), mask)
+                with st("inter"):
+                    self.hip.hevc_inter(B, self.W, self.H, p(self.src[0]), p(self.src[1]), p(self.src[2]), p(ref[0]),
+                                        p(ref[1]), p(ref[2]), p(cur[0]), p(cur[1]), p(cur[2]), p(self.ctu), p(self.cu),
+                                        p(self.coef[0]), p(self.coef[1]), p(self.coef[2]), p(self.ctb_qp), p(self.run),
+                                        p(self.cand), p(self.mv), p(self.me_cost), bd, s, int(self.p.tu_inter_depth),
+                                        int(self.p.sdh), int(self.p.intra_bias_p))
+                with st("intra_recon"):
+                    self.hip.hevc_intra(*intra_args, 0, 1, p(self.err), s, int(self.p.sdh))   # intra CUs, wavefront
                 self.prev_mv.copy_(self.mv)
             self.hip.hevc_qp_fixup(B, self.W, self.H, p(self.ctu), p(self.cu), p(self.qp), p(self.run), int(self.p.wpp), s)
             if self.p.deblock:
-                self.hip.hevc_deblock(B, self.W, self.H, bd, p(cur[0]), p(cur[1]), p(cur[2]), p(self.cu), p(self.ctu),
-                                      p(self.run), s)
+                with st("deblock"):
+                    self.hip.hevc_deblock(B, self.W, self.H, bd, p(cur[0]), p(cur[1]), p(cur[2]), p(self.cu),
+                                          p(self.ctu), p(self.run), s)
             if self.p.sao:
                 # SAO reads the deblocked picture and writes every sample of the output:
                 # ping-pong with the spare buffer instead of copying the input
                 out_pl = self.dbk
-                self.hip.hevc_sao(B, self.W, self.H, bd, p(cur[0]), p(cur[1]), p(cur[2]), p(out_pl[0]),
-                                  p(out_pl[1]), p(out_pl[2]), p(self.src[0]), p(self.src[1]), p(self.src[2]),
-                                  p(self.ctu), p(self.ctb_qp), p(self.run), 1, s)
+                with st("sao"):
+                    self.hip.hevc_sao(B, self.W, self.H, bd, p(cur[0]), p(cur[1]), p(cur[2]), p(out_pl[0]),
+                                      p(out_pl[1]), p(out_pl[2]), p(self.src[0]), p(self.src[1]), p(self.src[2]),
+                                      p(self.ctu), p(self.ctb_qp), p(self.run), 1, s)
                 self.dbk = cur
                 self.rec[t % 2] = cur = out_pl
             if metrics:
@@ -377,6 +412,8 @@ class GpuHevcEncoder:
             # records to pinned host memory on the copy stream; CABAC on the thread pool
             hb = t % 3
             if pending[hb]:  # the CABAC jobs of step t - 3 still read this host buffer set
+                # (a CABAC job first waits for its records' copy, i.e. for step t - 3's GPU work:
+                # this wait is GPU time as much as entropy time)
                 tb = time.perf_counter()
                 for f in pending[hb]:
                     f.result()
@@ -424,7 +461,15 @@ class GpuHevcEncoder:
                 bits[b][t] = 8 * len(nal)
         t_host = time.perf_counter() - t2
         # cabac_batch_s: wall time of the native batch writer (entropy_threads threads)
-        self.timings = dict(loop_s=t_gpu, loop_blocked_on_cabac_s=t_blocked, host_wait_s=t_host,
+        if gate_sum:
+            n_p = len(gate_sum)
+            self.stats["intra_analyzed_ctb_ratio"] = float(torch.stack(gate_sum).sum().item()) / (n_p * B * self.nctb)
+        if st.enabled:
+            self.stage_ms = {k: round(v["s"] * 1000.0, 2) for k, v in st.summary().items()}
+        # loop_waits_on_step_t_minus_3_s: the frame loop waiting for the CABAC jobs of step
+        # t - 3 to release their pinned host buffers -- those jobs first wait for their
+        # records' device-to-host copy, so this includes GPU completion, not only entropy coding
+        self.timings = dict(loop_s=t_gpu, loop_waits_on_step_t_minus_3_s=t_blocked, host_wait_s=t_host,
                             cabac_batch_s=cabac_s[0], cabac_ms_per_picture_wall=1000.0 * cabac_s[0] / max(1, B * F),
                             entropy_threads=self.entropy_threads)
         out = []

@@ -107,11 +107,14 @@ def _intra_record(rng, h, c, mx, my, qp, density, allow_i4=True, t8x8=False):
 
 def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp: int = 28,
                   density: float = 0.15, intra_in_p: float = 0.1, mv_range: int = 48, keyint: int = 0,
-                  cabac: bool = False, t8x8: bool = False, records: list | None = None, refs: int = 1) -> bytes:
+                  cabac: bool = False, t8x8: bool = False, records: list | None = None, refs: int = 1,
+                  slice_rows: int = 0) -> bytes:
     """Annex-B stream of ``frames`` pictures (IDR + P) from random decision records.
 
     cabac / t8x8 select the entropy coder and the High-profile 8x8 transform (I8x8 MBs and
-    8x8-transformed inter MBs).  ``records``, if given, receives (hdr, coef) per picture."""
+    8x8-transformed inter MBs).  ``records``, if given, receives (hdr, coef) per picture.
+    ``slice_rows`` > 0: every picture is coded as several slices of that many MB rows (intra
+    modes then treat each slice's first row as having no row above)."""
     rng = np.random.default_rng(seed)
     cfg = dict(width=width, height=height, qp=qp, cabac=int(cabac), t8x8=int(t8x8), refs=int(refs))
     wmb, hmb = (width + 15) // 16, (height + 15) // 16
@@ -135,7 +138,8 @@ def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp:
             h, c = hdr[mb], coef[mb]
             mqp = int(np.clip(sqp + rng.integers(-3, 4), 0, 51))
             if idr or rng.random() < intra_in_p:
-                _intra_record(rng, h, c, mx, my, mqp, density, t8x8=t8x8)
+                r0 = (my // slice_rows) * slice_rows if slice_rows else 0
+                _intra_record(rng, h, c, mx, my - r0, mqp, density, t8x8=t8x8)
                 continue
             r = rng.random()
             kind = PSKIP if r < 0.25 else (P16x16 if r < 0.5 else (P16x8 if r < 0.65 else (P8x16 if r < 0.8 else P8x8)))
@@ -171,8 +175,14 @@ def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp:
         fp = dict(idr=int(idr), qp=sqp, frame_num=fn, idr_pic_id=idr_id)
         if not idr and refs > 1:
             fp["num_ref_l0"] = nref
-        nal, _ = host.write_slice(cfg, fp, hdr, coef)
-        out.append(nal)
+        if slice_rows:
+            for r0 in range(0, hmb, slice_rows):
+                n_mbs = min(slice_rows, hmb - r0) * wmb
+                nal, _ = host.write_slice(cfg, dict(fp, first_mb=r0 * wmb, num_mbs=n_mbs), hdr, coef)
+                out.append(nal)
+        else:
+            nal, _ = host.write_slice(cfg, fp, hdr, coef)
+            out.append(nal)
         if records is not None:
             records.append((hdr, coef))
         if idr:

@@ -7,7 +7,8 @@ Checked here on the CPU:
   reproduce the original slice NALs bit for bit (so headers, motion vectors, QPs and
   every level survive the packed format);
 * consistency with the full decoder (MB kinds, QPs, motion vectors, non-zero flags);
-* the GPU-coverage flags (multi-slice / unsupported tools fall back to the CPU).
+* the GPU-coverage flags (several slices per picture stay on the GPU path; I_PCM,
+  constrained intra prediction and mmco 5 fall back to the CPU).
 """
 import numpy as np
 import pytest
@@ -74,3 +75,27 @@ def test_parse_encoder_stream_and_meta(host):
 def test_parse_reports_errors(host):
     seg = host.parse([b"\x00\x00\x00\x01\x67garbage"], 1)[0]
     assert seg["error"] is not None or seg["n"] == 0
+
+
+@pytest.mark.parametrize("cabac,rows", [(False, 2), (True, 1)])
+def test_parse_multi_slice_rewrite_roundtrip(host, cabac, rows):
+    """Pictures of several slices: the parsed records, rewritten slice by slice, reproduce
+    the stream bit for bit; every picture stays on the GPU path and the records carry each
+    MB's slice (MbHeader::pad0)."""
+    w, h, frames = 96, 80, 3
+    s = random_stream(host, w, h, frames, seed=31, slice_rows=rows, cabac=cabac, intra_in_p=0.3)
+    seg = host.parse([s], 1)[0]
+    assert seg["error"] is None and seg["n"] == frames
+    assert all(seg["meta"][t, 10] == 1 for t in range(frames))
+    wmb, hmb = w // 16, h // 16
+    cfg = dict(width=w, height=h, qp=28, cabac=int(cabac))
+    out = [host.parameter_sets(cfg)]
+    for t in range(frames):
+        hdr = np.ascontiguousarray(seg["hdr"][t])
+        assert np.array_equal(hdr[:, 7], (np.arange(wmb * hmb) // (rows * wmb)).astype(np.uint8))
+        hdr[:, 7] = 0
+        fp = dict(idr=int(t == 0), qp=int(seg["meta"][t, 5]), frame_num=t, idr_pic_id=0)
+        for r0 in range(0, hmb, rows):
+            out.append(host.write_slice(cfg, dict(fp, first_mb=r0 * wmb, num_mbs=min(rows, hmb - r0) * wmb), hdr,
+                                        unpack_levels(seg, t))[0])
+    assert b"".join(out) == s

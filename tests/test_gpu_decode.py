@@ -109,3 +109,13 @@ def test_gpu_decode_b_records(host, dec):
     from tests.test_h264_bframes import _b_stream
     streams = [_b_stream(host, w, h, seed)[0] for w, h, seed in ((64, 48, 1), (96, 80, 2), (176, 144, 3))]
     _check(host, dec, streams)
+
+
+def test_gpu_decode_multi_slice_pictures(host, dec):
+    """Pictures coded as several slices (2-row / 1-row slices, CAVLC and CABAC, High 8x8
+    with Intra8x8) reconstruct on the GPU: intra prediction treats MBs of another slice as
+    unavailable (MbHeader::pad0 carries the slice), deblocking filters across the slices."""
+    streams = [random_stream(host, 96, 64, 4, seed=61, slice_rows=2, intra_in_p=0.3),
+               random_stream(host, 112, 80, 4, seed=62, slice_rows=1, cabac=True, t8x8=True, intra_in_p=0.4),
+               random_stream(host, 96, 64, 3, seed=63, slice_rows=3, cabac=True)]
+    _check(host, dec, streams)
