@@ -107,8 +107,7 @@ MIVC_HD int scan_pos(int scan_idx, int log2size, int p) {
 }
 
 // ---------------------------------------------------------------- CABAC context initialisation (9.3.2.2)
-// initValue per context, for initType 0 (I slices) and 1 (P slices, cabac_init_flag 0).
-// Context index offsets of the syntax elements this codec uses:
+// Context index offsets of the syntax elements the encoder's CABAC writer uses:
 enum Ctx : int {
   CTX_SAO_MERGE = 0,         // 1
   CTX_SAO_TYPE = 1,          // 1
@@ -135,67 +134,12 @@ enum Ctx : int {
   CTX_GT2 = 136,             // 6 (4 luma + 2 chroma)
   CTX_REF_IDX = 142,         // 2
   CTX_CU_QP_DELTA = 144,     // 2
-  kNumCtx = 146,
+  CTX_INTER_PRED = 146,      // 5 (inter_pred_idc: ctxInc = CtDepth for the first bin, 4 for the second)
+  kNumCtx = 151,
 };
 
-// [initType 0 = I, 1 = P][ctx]
-static constexpr uint8_t kCtxInit[2][kNumCtx] = {
-    {
-        153,                                                              // sao_merge
-        200,                                                              // sao_type_idx
-        139, 141, 157,                                                    // split_cu_flag
-        154, 154, 154,                                                    // cu_skip_flag (unused in I)
-        154,                                                              // pred_mode_flag (unused in I)
-        184, 154, 154, 154,                                               // part_mode
-        184,                                                              // prev_intra_luma_pred_flag
-        63,                                                               // intra_chroma_pred_mode
-        154, 154, 154, 154, 154,                                          // merge_flag, merge_idx, mvd g0/g1, mvp (unused)
-        154,                                                              // rqt_root_cbf (unused)
-        153, 138, 138,                                                    // split_transform_flag
-        111, 141,                                                         // cbf_luma
-        94, 138, 182, 154,                                                // cbf_cb / cbf_cr
-        110, 110, 124, 125, 140, 153, 125, 127, 140, 109, 111, 143, 127, 111, 79, 108, 123, 63,  // last_x
-        110, 110, 124, 125, 140, 153, 125, 127, 140, 109, 111, 143, 127, 111, 79, 108, 123, 63,  // last_y
-        91, 171, 134, 141,                                                // coded_sub_block_flag
-        111, 111, 125, 110, 110, 94, 124, 108, 124, 107, 125, 141, 179, 153, 125, 107, 125, 141, 179, 153,
-        125, 107, 125, 141, 179, 153, 125, 140, 139, 182, 182, 152, 136, 152, 136, 153, 136, 139, 111, 136,
-        139, 111,                                                         // sig_coeff_flag
-        140, 92, 137, 138, 140, 152, 138, 139, 153, 74, 149, 92, 139, 107, 122, 152, 140, 179, 166, 182,
-        140, 227, 122, 197,                                               // greater1
-        138, 153, 136, 167, 152, 152,                                     // greater2
-        154, 154,                                                         // ref_idx (unused)
-        154, 154,                                                         // cu_qp_delta_abs
-    },
-    {
-        153,                                                              // sao_merge
-        185,                                                              // sao_type_idx
-        107, 139, 126,                                                    // split_cu_flag
-        197, 185, 201,                                                    // cu_skip_flag
-        149,                                                              // pred_mode_flag
-        154, 139, 154, 154,                                               // part_mode
-        154,                                                              // prev_intra_luma_pred_flag
-        152,                                                              // intra_chroma_pred_mode
-        110,                                                              // merge_flag
-        122,                                                              // merge_idx
-        140,                                                              // abs_mvd_greater0_flag
-        198,                                                              // abs_mvd_greater1_flag
-        168,                                                              // mvp_l0_flag
-        79,                                                               // rqt_root_cbf
-        124, 138, 94,                                                     // split_transform_flag
-        153, 111,                                                         // cbf_luma
-        149, 107, 167, 154,                                               // cbf_cb / cbf_cr
-        125, 110, 94, 110, 95, 79, 125, 111, 110, 78, 110, 111, 111, 95, 94, 108, 123, 108,  // last_x
-        125, 110, 94, 110, 95, 79, 125, 111, 110, 78, 110, 111, 111, 95, 94, 108, 123, 108,  // last_y
-        121, 140, 61, 154,                                                // coded_sub_block_flag
-        155, 154, 139, 153, 139, 123, 123, 63, 153, 166, 183, 140, 136, 153, 154, 166, 183, 140, 136, 153,
-        154, 166, 183, 140, 136, 153, 154, 170, 153, 123, 123, 107, 121, 107, 121, 167, 151, 183, 140, 151,
-        183, 140,                                                         // sig_coeff_flag
-        154, 196, 167, 167, 154, 152, 167, 182, 182, 134, 149, 136, 153, 121, 136, 122, 169, 208, 166, 167,
-        154, 152, 167, 182,                                               // greater1
-        107, 167, 91, 122, 107, 167,                                      // greater2
-        153, 153,                                                         // ref_idx
-        154, 154,                                                         // cu_qp_delta_abs
-    }};
+// initValues of these contexts for the three initTypes come from the full spec table of the
+// decoder (csrc/host/hevc_ctx_tables.h) through kWriterCtxToSpec (hevc_cabac.h)
 
 // ---------------------------------------------------------------- CABAC engine tables (9.3.4.3.2)
 static constexpr uint8_t kRangeLps[64][4] = {
@@ -244,15 +188,24 @@ static_assert(sizeof(CtuInfo) == 32, "CtuInfo is 32 bytes");
 
 enum CuPred : uint8_t { CU_INTRA = 0, CU_INTER = 1 };
 
-struct CuInfo {
+// inter prediction direction of a CU (inter_pred_idc + 1): bit 0 list 0, bit 1 list 1
+enum CuDir : uint8_t { DIR_L0 = 1, DIR_L1 = 2, DIR_BI = 3 };
+
+struct alignas(8) CuInfo {
   uint8_t pred;   // CuPred
   uint8_t mode;   // intra luma mode 0..34 (intra)
   uint8_t cbf;    // informational: bit0 Y, bit1 Cb, bit2 Cr (the writer recomputes it)
   uint8_t flags;  // bits 1-2: log2 CU size - 3; bit 3: intra PART_NxN; bit 4: inter TU split once
                   // (cbf then describes the quarter TU covering this granule)
   int16_t mv[2];  // quarter-sample L0 motion vector (inter)
+  int16_t mv1[2]; // quarter-sample L1 motion vector (inter, B slices)
+  uint8_t dir;    // CuDir of an inter CU (0 is read as DIR_L0: P-slice records)
+  uint8_t pad[3];
 };
-static_assert(sizeof(CuInfo) == 8, "CuInfo is 8 bytes");
+static_assert(sizeof(CuInfo) == 16, "CuInfo is 16 bytes");
+constexpr int kCuInfoBytes = 16;
+
+MIVC_HD int cu_dir(const CuInfo& c) { return c.dir ? c.dir : DIR_L0; }
 
 // z-order index of 8x8 granule (gx, gy) inside a 32x32 CTB
 MIVC_HD int zorder8(int gx, int gy) {

@@ -279,6 +279,8 @@ hevc::HevcConfig hevc_cfg_from(const py::dict& d) {
   c.tu_inter_depth = dget<int>(d, "tu_inter_depth", 0);
   c.sdh = dget<int>(d, "sdh", 0);
   c.level_idc = dget<int>(d, "level_idc", 0);
+  c.bframes = dget<int>(d, "bframes", 0);
+  c.tmvp = dget<int>(d, "tmvp", 0);
   if (c.tu_inter_depth < 0 || c.tu_inter_depth > 1) throw std::runtime_error("HEVC: tu_inter_depth in 0..1");
   if (c.threads < 1 || c.threads > 256) throw std::runtime_error("HEVC: threads in 1..256");
   if (c.width <= 0 || c.height <= 0 || (c.width & 1) || (c.height & 1)) throw std::runtime_error("HEVC: bad size");
@@ -453,6 +455,32 @@ py::dict dec_segment_records(std::vector<hevc::DecPicture>& pics, const std::vec
 }
 
 }  // namespace
+
+// HEVC frame parameters from a Python dict; a collocated picture's records ("col_cu",
+// uint8 [nctb * 16, 16]) are kept alive in `keep` while the GIL is released
+hevc::HevcFrameParams hevc_frame_from(const py::dict& fp, std::vector<py::array>& keep, size_t cu_bytes) {
+  hevc::HevcFrameParams f;
+  f.idr = dget<int>(fp, "idr", 1);
+  f.poc = dget<int>(fp, "poc", 0);
+  f.qp = dget<int>(fp, "qp", 30);
+  f.slice_type = f.idr ? 2 : dget<int>(fp, "slice_type", 1);
+  f.nal_ref = dget<int>(fp, "nal_ref", 1);
+  f.ref_poc[0] = dget<int>(fp, "ref_poc0", -1);
+  f.ref_poc[1] = dget<int>(fp, "ref_poc1", -1);
+  if (fp.contains("col_poc")) {
+    f.col.set = 1;
+    f.col.poc = dget<int>(fp, "col_poc", 0);
+    f.col.ref_poc[0] = dget<int>(fp, "col_ref_poc0", 0);
+    f.col.ref_poc[1] = dget<int>(fp, "col_ref_poc1", 0);
+    if (fp.contains("col_cu") && !fp["col_cu"].is_none()) {
+      auto a = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>::ensure(fp["col_cu"]);
+      if (!a || static_cast<size_t>(a.size()) != cu_bytes) throw std::runtime_error("col_cu: wrong size");
+      keep.push_back(a);
+      f.col.cu = reinterpret_cast<const hevc::CuInfo*>(a.data());
+    }
+  }
+  return f;
+}
 
 PYBIND11_MODULE(_host, m) {
   m.doc() = "govideocompressor_amd host native library (bitstream, CAVLC, decoder, CPU encoder)";
@@ -650,15 +678,12 @@ PYBIND11_MODULE(_host, m) {
          py::array_t<uint8_t, py::array::c_style> cu, py::array_t<int16_t, py::array::c_style> cy,
          py::array_t<int16_t, py::array::c_style> cb, py::array_t<int16_t, py::array::c_style> cr) {
         hevc::HevcConfig c = hevc_cfg_from(cfg);
-        hevc::HevcFrameParams f;
-        f.idr = dget<int>(fp, "idr", 1);
-        f.poc = dget<int>(fp, "poc", 0);
-        f.qp = dget<int>(fp, "qp", 30);
-        f.slice_type = f.idr ? 2 : dget<int>(fp, "slice_type", 1);
         const py::ssize_t nctu = static_cast<py::ssize_t>(c.wctb()) * c.hctb();
+        std::vector<py::array> keep;
+        const hevc::HevcFrameParams f = hevc_frame_from(fp, keep, static_cast<size_t>(nctu) * hevc::kCusPerCtb * hevc::kCuInfoBytes);
         const py::ssize_t W = c.coded_width(), H = c.coded_height();
         if (ctu.size() != nctu * 32) throw std::runtime_error("ctu records: wrong size");
-        if (cu.size() != nctu * hevc::kCusPerCtb * 8) throw std::runtime_error("cu records: wrong size");
+        if (cu.size() != nctu * hevc::kCusPerCtb * hevc::kCuInfoBytes) throw std::runtime_error("cu records: wrong size");
         if (cy.size() != W * H || cb.size() != W * H / 4 || cr.size() != W * H / 4)
           throw std::runtime_error("coefficient planes: wrong size");
         hevc::HevcSliceStats st;
@@ -687,14 +712,11 @@ PYBIND11_MODULE(_host, m) {
          py::array_t<uint32_t, py::array::c_style> ctb_off, py::array_t<int16_t, py::array::c_style> levels) {
         // levels in the GPU encoder's packed form (hevc::PackedLevels)
         hevc::HevcConfig c = hevc_cfg_from(cfg);
-        hevc::HevcFrameParams f;
-        f.idr = dget<int>(fp, "idr", 1);
-        f.poc = dget<int>(fp, "poc", 0);
-        f.qp = dget<int>(fp, "qp", 30);
-        f.slice_type = f.idr ? 2 : dget<int>(fp, "slice_type", 1);
         const py::ssize_t nctu = static_cast<py::ssize_t>(c.wctb()) * c.hctb();
+        std::vector<py::array> keep;
+        const hevc::HevcFrameParams f = hevc_frame_from(fp, keep, static_cast<size_t>(nctu) * hevc::kCusPerCtb * hevc::kCuInfoBytes);
         if (ctu.size() != nctu * 32) throw std::runtime_error("ctu records: wrong size");
-        if (cu.size() != nctu * hevc::kCusPerCtb * 8) throw std::runtime_error("cu records: wrong size");
+        if (cu.size() != nctu * hevc::kCusPerCtb * hevc::kCuInfoBytes) throw std::runtime_error("cu records: wrong size");
         if (nzmap.size() != nctu * 2 || ctb_off.size() != nctu) throw std::runtime_error("packed maps: wrong size");
         if (levels.size() % 16) throw std::runtime_error("packed levels: not whole 4x4 blocks");
         hevc::PackedLevels pk;
@@ -731,17 +753,14 @@ PYBIND11_MODULE(_host, m) {
         const py::ssize_t nctu = static_cast<py::ssize_t>(c.wctb()) * c.hctb();
         if (ctu.ndim() != 3 || ctu.shape(0) < B || ctu.shape(1) != nctu || ctu.shape(2) != 32)
           throw std::runtime_error("ctu records: expected [B, nctb, 32]");
-        if (cu.size() < B * nctu * hevc::kCusPerCtb * 8) throw std::runtime_error("cu records: wrong size");
+        if (cu.size() < B * nctu * hevc::kCusPerCtb * hevc::kCuInfoBytes) throw std::runtime_error("cu records: wrong size");
         if (nzmap.size() < B * nctu * 2 || ctb_off.size() < B * nctu) throw std::runtime_error("packed maps: wrong size");
         if (levels.ndim() != 2 || levels.shape(0) < B || levels.shape(1) % 16) throw std::runtime_error("packed levels: [B, 16 n]");
         std::vector<hevc::HevcFrameParams> fps(B);
-        for (py::ssize_t b = 0; b < B; ++b) {
-          const py::dict fp = frames[b].cast<py::dict>();
-          fps[b].idr = dget<int>(fp, "idr", 1);
-          fps[b].poc = dget<int>(fp, "poc", 0);
-          fps[b].qp = dget<int>(fp, "qp", 30);
-          fps[b].slice_type = fps[b].idr ? 2 : dget<int>(fp, "slice_type", 1);
-        }
+        std::vector<py::array> keep;
+        for (py::ssize_t b = 0; b < B; ++b)
+          fps[b] = hevc_frame_from(frames[b].cast<py::dict>(), keep,
+                                   static_cast<size_t>(nctu) * hevc::kCusPerCtb * hevc::kCuInfoBytes);
         const size_t per_lv = static_cast<size_t>(levels.shape(1));
         std::vector<std::vector<uint8_t>> nals(B);
         std::vector<std::string> errs(B);
@@ -758,7 +777,7 @@ PYBIND11_MODULE(_host, m) {
                 pk.nblocks = per_lv / 16;
                 nals[b] = hevc::hevc_write_slice(
                     c, fps[b], reinterpret_cast<const hevc::CtuInfo*>(ctu.data() + static_cast<size_t>(b) * nctu * 32),
-                    reinterpret_cast<const hevc::CuInfo*>(cu.data() + static_cast<size_t>(b) * nctu * hevc::kCusPerCtb * 8),
+                    reinterpret_cast<const hevc::CuInfo*>(cu.data() + static_cast<size_t>(b) * nctu * hevc::kCusPerCtb * hevc::kCuInfoBytes),
                     nullptr, nullptr, nullptr, nullptr, &pk);
               } catch (const std::exception& e) {
                 errs[b] = e.what();

@@ -4,12 +4,14 @@
 // (outstanding 0xFF bytes); the decoder is the normative 9-bit offset engine.  Both
 // use the context tables of csrc/common/hevc_tables.h.
 #pragma once
+#include <array>
 #include <cstdint>
 #include <stdexcept>
 #include <vector>
 
 #include "../common/hevc_tables.h"
 #include "bitstream.h"
+#include "hevc_ctx_tables.h"
 
 namespace mivc {
 namespace hevc {
@@ -20,10 +22,47 @@ struct CtxState {
 };
 
 // 9.3.2.2: contexts initialised for a slice of the given initType and SliceQpY
+// writer context index -> index in the spec initValue table (hevc_ctx_tables.h, dec::DCtx)
+inline constexpr std::array<uint8_t, kNumCtx> writer_ctx_map() {
+  std::array<uint8_t, kNumCtx> m{};
+  auto run = [&m](int w, int d, int n) {
+    for (int i = 0; i < n; ++i) m[w + i] = static_cast<uint8_t>(d + i);
+  };
+  run(CTX_SAO_MERGE, dec::C_SAO_MERGE, 1);
+  run(CTX_SAO_TYPE, dec::C_SAO_TYPE, 1);
+  run(CTX_SPLIT_CU, dec::C_SPLIT_CU, 3);
+  run(CTX_CU_SKIP, dec::C_SKIP, 3);
+  run(CTX_PRED_MODE, dec::C_PRED_MODE, 1);
+  run(CTX_PART_MODE, dec::C_PART_MODE, 4);
+  run(CTX_PREV_INTRA, dec::C_PREV_INTRA, 1);
+  run(CTX_CHROMA_MODE, dec::C_CHROMA_MODE, 1);
+  run(CTX_MERGE_FLAG, dec::C_MERGE_FLAG, 1);
+  run(CTX_MERGE_IDX, dec::C_MERGE_IDX, 1);
+  run(CTX_MVD_G0, dec::C_MVD_G0, 1);
+  run(CTX_MVD_G1, dec::C_MVD_G1, 1);
+  run(CTX_MVP_IDX, dec::C_MVP, 1);
+  run(CTX_RQT_ROOT_CBF, dec::C_ROOT_CBF, 1);
+  run(CTX_SPLIT_TRANSFORM, dec::C_SPLIT_TF, 3);
+  run(CTX_CBF_LUMA, dec::C_CBF_LUMA, 2);
+  run(CTX_CBF_CHROMA, dec::C_CBF_CHROMA, 4);
+  run(CTX_LAST_X, dec::C_LAST_X, 18);
+  run(CTX_LAST_Y, dec::C_LAST_Y, 18);
+  run(CTX_CSBF, dec::C_CSBF, 4);
+  run(CTX_SIG, dec::C_SIG, 42);
+  run(CTX_GT1, dec::C_GT1, 24);
+  run(CTX_GT2, dec::C_GT2, 6);
+  run(CTX_REF_IDX, dec::C_REF_IDX, 2);
+  run(CTX_CU_QP_DELTA, dec::C_QP_DELTA, 2);
+  run(CTX_INTER_PRED, dec::C_INTER_PRED, 5);
+  return m;
+}
+inline constexpr std::array<uint8_t, kNumCtx> kWriterCtxToSpec = writer_ctx_map();
+
+// 9.3.2.2 initialisation; init_type 0 = I, 1 = P, 2 = B (cabac_init_flag 0)
 inline void init_contexts(CtxState* ctx, int init_type, int slice_qp) {
   const int qp = slice_qp < 0 ? 0 : (slice_qp > 51 ? 51 : slice_qp);
   for (int i = 0; i < kNumCtx; ++i) {
-    const int v = kCtxInit[init_type][i];
+    const int v = dec::kInit[init_type][kWriterCtxToSpec[i]];
     const int m = (v >> 4) * 5 - 45, n = ((v & 15) << 3) - 16;
     int pre = ((m * qp) >> 4) + n;
     pre = pre < 1 ? 1 : (pre > 126 ? 126 : pre);

@@ -33,17 +33,33 @@ struct HevcConfig {
   int tu_inter_depth = 0;      // max_transform_hierarchy_depth_inter: 1 = inter CUs may split their TU once
   int threads = 1;             // host threads coding the WPP substreams of one picture
   int level_idc = 0;           // > 0: general_level_idc (30 x level, -level); must fit the size / rate
+  int bframes = 0;             // > 0: B pictures between the anchors (DPB of 2 references, 1 reordered picture)
+  int tmvp = 0;                // sps_temporal_mvp_enabled_flag: temporal merge / AMVP candidates (needs FrameParams::col)
   int coded_width() const { return (width + kCtb - 1) / kCtb * kCtb; }
   int coded_height() const { return (height + kCtb - 1) / kCtb * kCtb; }
   int wctb() const { return coded_width() / kCtb; }
   int hctb() const { return coded_height() / kCtb; }
 };
 
+// The collocated picture of temporal motion vector prediction (8.5.3.2.8): its decision
+// records (same layout as the current picture's) and the POCs its motion points to.
+struct HevcColPic {
+  int set = 0;                 // must be 1 in P / B slices when HevcConfig::tmvp is on
+  const CuInfo* cu = nullptr;  // nullptr: an intra picture (no temporal candidates)
+  int poc = 0;
+  int ref_poc[2] = {0, 0};     // POC of the col picture's RefPicList0[0] / RefPicList1[0]
+};
+
 struct HevcFrameParams {
   int idr = 1;
-  int poc = 0;          // picture order count (decode order == output order)
+  int poc = 0;          // picture order count
   int qp = 30;          // SliceQpY
-  int slice_type = 2;   // 2 = I, 1 = P
+  int slice_type = 2;   // 2 = I, 1 = P, 0 = B
+  int nal_ref = 1;      // 0: a sub-layer non-reference picture (TRAIL_N)
+  // one reference picture per list: RefPicList0[0] / RefPicList1[0] POCs (-1: P slices use
+  // poc - 1); the slice's short-term RPS holds exactly these pictures
+  int ref_poc[2] = {-1, -1};
+  HevcColPic col;       // with HevcConfig::tmvp: the collocated picture (L1[0] in B, L0[0] in P)
 };
 
 struct HevcSliceStats {

@@ -2455,8 +2455,11 @@ struct HevcStreamDecoder::Impl {
         } else {
           const MvField& m = cur->mvf[g4(x, y)];
           c.mode = 0;
-          c.mv[0] = m.mv[0][0];
-          c.mv[1] = m.mv[0][1];
+          c.mv[0] = (m.pred & 1) ? m.mv[0][0] : 0;
+          c.mv[1] = (m.pred & 1) ? m.mv[0][1] : 0;
+          c.mv1[0] = (m.pred & 2) ? m.mv[1][0] : 0;
+          c.mv1[1] = (m.pred & 2) ? m.mv[1][1] : 0;
+          c.dir = m.pred;
         }
       }
   }

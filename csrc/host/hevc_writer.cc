@@ -19,7 +19,7 @@ namespace hevc {
 
 namespace {
 
-enum NalType { NAL_TRAIL_R = 1, NAL_IDR_W_RADL = 19, NAL_VPS = 32, NAL_SPS = 33, NAL_PPS = 34 };
+enum NalType { NAL_TRAIL_N = 0, NAL_TRAIL_R = 1, NAL_IDR_W_RADL = 19, NAL_VPS = 32, NAL_SPS = 33, NAL_PPS = 34 };
 
 void append_hevc_nal(std::vector<uint8_t>& out, int type, const std::vector<uint8_t>& rbsp) {
   static const uint8_t sc[4] = {0, 0, 0, 1};
@@ -91,8 +91,8 @@ std::vector<uint8_t> hevc_parameter_sets(const HevcConfig& c) {
     bw.put(0xFFFF, 16);  // vps_reserved_0xffff_16bits
     profile_tier_level(bw, c);
     bw.put_bit(1);       // vps_sub_layer_ordering_info_present_flag
-    bw.put_ue(1);        // vps_max_dec_pic_buffering_minus1
-    bw.put_ue(0);        // vps_max_num_reorder_pics
+    bw.put_ue(c.bframes > 0 ? 2 : 1);  // vps_max_dec_pic_buffering_minus1 (B: two anchors + current)
+    bw.put_ue(c.bframes > 0 ? 1 : 0);  // vps_max_num_reorder_pics
     bw.put_ue(0);        // vps_max_latency_increase_plus1
     bw.put(0, 6);        // vps_max_layer_id
     bw.put_ue(0);        // vps_num_layer_sets_minus1
@@ -123,8 +123,8 @@ std::vector<uint8_t> hevc_parameter_sets(const HevcConfig& c) {
     bw.put_ue(c.bit_depth - 8);  // bit_depth_chroma_minus8
     bw.put_ue(8 - 4);            // log2_max_pic_order_cnt_lsb_minus4 (8 bits)
     bw.put_bit(1);               // sps_sub_layer_ordering_info_present_flag
-    bw.put_ue(1);                // sps_max_dec_pic_buffering_minus1
-    bw.put_ue(0);                // sps_max_num_reorder_pics
+    bw.put_ue(c.bframes > 0 ? 2 : 1);  // sps_max_dec_pic_buffering_minus1
+    bw.put_ue(c.bframes > 0 ? 1 : 0);  // sps_max_num_reorder_pics
     bw.put_ue(0);                // sps_max_latency_increase_plus1
     bw.put_ue(kMinCbLog2 - 3);   // log2_min_luma_coding_block_size_minus3
     bw.put_ue(kCtbLog2 - kMinCbLog2);  // log2_diff_max_min_luma_coding_block_size
@@ -143,7 +143,7 @@ std::vector<uint8_t> hevc_parameter_sets(const HevcConfig& c) {
     bw.put_ue(0);                // delta_poc_s0_minus1
     bw.put_bit(1);               // used_by_curr_pic_s0_flag
     bw.put_bit(0);               // long_term_ref_pics_present_flag
-    bw.put_bit(0);               // sps_temporal_mvp_enabled_flag
+    bw.put_bit(c.tmvp ? 1 : 0);  // sps_temporal_mvp_enabled_flag
     bw.put_bit(1);               // strong_intra_smoothing_enabled_flag
     bw.put_bit(0);               // vui_parameters_present_flag
     bw.put_bit(0);               // sps_extension_present_flag
@@ -194,12 +194,24 @@ std::vector<uint8_t> hevc_parameter_sets(const HevcConfig& c) {
 namespace {
 
 // ------------------------------------------------------------------ slice writer state
+struct Mv {
+  int x, y;
+  bool operator==(const Mv& o) const { return x == o.x && y == o.y; }
+};
+// motion of a PU: direction (bit 0 list 0, bit 1 list 1; refIdx 0 in each used list) + vectors
+struct Motion {
+  uint8_t dir = 0;
+  Mv m[2] = {{0, 0}, {0, 0}};
+  bool operator==(const Motion& o) const {
+    return dir == o.dir && (!(dir & 1) || m[0] == o.m[0]) && (!(dir & 2) || m[1] == o.m[1]);
+  }
+};
+
 struct PicState {
   std::vector<int8_t> depth, skip, pred, mode4;  // mode4: luma intra mode per 4x4 block (NxN PUs)
-  std::vector<int16_t> mvx, mvy;
+  std::vector<Motion> mot;
   std::vector<uint8_t> coded;
-  explicit PicState(size_t n)
-      : depth(n, 0), skip(n, 0), pred(n, 0), mode4(4 * n, 1), mvx(n, 0), mvy(n, 0), coded(n, 0) {}
+  explicit PicState(size_t n) : depth(n, 0), skip(n, 0), pred(n, 0), mode4(4 * n, 1), mot(n), coded(n, 0) {}
 };
 
 struct Writer {
@@ -212,12 +224,15 @@ struct Writer {
   CtxState ctx[kNumCtx];
   HevcSliceStats st;
   int W, H, wctb, hctb, w8, h8;
-  bool pslice;
+  bool inter_slice, bslice;
+  bool tmvp;         // slice_temporal_mvp_enabled_flag
+  bool col_l1;       // the collocated picture is RefPicList1[0] (B: collocated_from_l0_flag 0)
+  bool no_backward;  // NoBackwardPredFlag: no reference picture follows the current one
   // per 8x8 granule of the picture (raster): state of already-coded CUs, shared by the
   // substream writers of one picture (WPP rows only read granules their 2-CTB lag
   // guarantees are final)
   std::vector<int8_t>&depth, &skip, &pred, &mode4;
-  std::vector<int16_t>&mvx, &mvy;
+  std::vector<Motion>& mot;
   std::vector<uint8_t>& coded;
   // cu_qp_delta state (7.4.9.14, 8.6.1): qPY_PREV of the next quantization group (the
   // slice QP at the start of the slice and, with WPP, of every CTB row: a Writer codes
@@ -235,7 +250,7 @@ struct Writer {
   Writer(const HevcConfig& cfg, const HevcFrameParams& f, const CtuInfo* ct, const CuInfo* cu_, const int16_t* cy,
          const int16_t* cb, const int16_t* cr, CabacEncoder& enc, PicState& ps)
       : c(cfg), fp(f), ctu(ct), cu(cu_), e(enc), depth(ps.depth), skip(ps.skip), pred(ps.pred), mode4(ps.mode4),
-        mvx(ps.mvx), mvy(ps.mvy), coded(ps.coded) {
+        mot(ps.mot), coded(ps.coded) {
     coef[0] = cy;
     coef[1] = cb;
     coef[2] = cr;
@@ -245,8 +260,12 @@ struct Writer {
     hctb = c.hctb();
     w8 = W / 8;
     h8 = H / 8;
-    pslice = fp.slice_type == 1;
-    init_contexts(ctx, pslice ? 1 : 0, fp.qp);
+    inter_slice = fp.slice_type != 2;
+    bslice = fp.slice_type == 0;
+    tmvp = inter_slice && c.tmvp;
+    col_l1 = bslice;
+    no_backward = ref_poc(0) <= fp.poc && (!bslice || ref_poc(1) <= fp.poc);
+    init_contexts(ctx, bslice ? 2 : (inter_slice ? 1 : 0), fp.qp);
     qp_prev = fp.qp;
   }
 
@@ -655,71 +674,152 @@ struct Writer {
   bool any_nonzero(int cidx, int x, int y, int n) const { return block_mask(cidx, x, y, n) != 0; }
 
   // ---------------------------------------------------------------- inter prediction helpers
-  struct Mv {
-    int x, y;
-    bool operator==(const Mv& o) const { return x == o.x && y == o.y; }
-  };
+  // One reference picture per list (refIdx 0): a PU's motion is its direction (bit 0 list 0,
+  // bit 1 list 1) and one vector per used list.  RefPicList0[0] / RefPicList1[0] are
+  // different pictures in every B slice this writer codes.
   bool inter_avail(int x, int y) const { return avail(x, y) && pred[g(x, y)] == CU_INTER; }
-  Mv mv_at(int x, int y) const { return Mv{mvx[g(x, y)], mvy[g(x, y)]}; }
+  const Motion& mot_at(int x, int y) const { return mot[g(x, y)]; }
+  int ref_poc(int l) const { return l == 0 ? (fp.ref_poc[0] >= 0 ? fp.ref_poc[0] : fp.poc - 1) : fp.ref_poc[1]; }
 
-  // 8.5.3.2.2-8.5.3.2.5 merge candidates of a 2Nx2N PU (P slice, no temporal candidate)
-  int merge_list(int x, int y, int n, Mv* out) const {
-    int k = 0;
-    const int xa1 = x - 1, ya1 = y + n - 1, xb1 = x + n - 1, yb1 = y - 1;
-    const bool a1 = inter_avail(xa1, ya1), b1 = inter_avail(xb1, yb1);
-    const bool b0 = inter_avail(x + n, y - 1), a0 = inter_avail(x - 1, y + n), b2 = inter_avail(x - 1, y - 1);
-    Mv ma1 = a1 ? mv_at(xa1, ya1) : Mv{0, 0}, mb1 = b1 ? mv_at(xb1, yb1) : Mv{0, 0};
-    if (a1) out[k++] = ma1;
-    if (b1 && !(a1 && ma1 == mb1)) out[k++] = mb1;
-    if (b0) {
-      Mv m = mv_at(x + n, y - 1);
-      if (!(b1 && mb1 == m)) out[k++] = m;
-    }
-    if (a0) {
-      Mv m = mv_at(x - 1, y + n);
-      if (!(a1 && ma1 == m)) out[k++] = m;
-    }
-    if (b2 && k < 4) {
-      Mv m = mv_at(x - 1, y - 1);
-      if (!(a1 && ma1 == m) && !(b1 && mb1 == m)) out[k++] = m;
-    }
-    while (k < c.max_merge) out[k++] = Mv{0, 0};
-    // the list holds MaxNumMergeCand entries: spatial candidates beyond it are not in it
-    return k < c.max_merge ? k : c.max_merge;
+  static Mv scale_mv(Mv v, int td0, int tb0) {  // 8.5.3.2.8 (8-209 .. 8-213)
+    const int td = std::clamp(td0, -128, 127), tb = std::clamp(tb0, -128, 127);
+    const int tx = (16384 + (std::abs(td) >> 1)) / td;
+    const int dsf = std::clamp((tb * tx + 32) >> 6, -4096, 4095);
+    auto sc = [dsf](int m) {
+      const int p = dsf * m;
+      return std::clamp((p < 0 ? -1 : 1) * ((std::abs(p) + 127) >> 8), -32768, 32767);
+    };
+    return Mv{sc(v.x), sc(v.y)};
   }
 
-  // 8.5.3.2.6-8.5.3.2.7 AMVP candidates (one reference picture: no scaling)
-  void amvp_list(int x, int y, int n, Mv* out) const {
-    const bool a0 = inter_avail(x - 1, y + n), a1 = inter_avail(x - 1, y + n - 1);
+  // 8.5.3.2.8 / 8.5.3.2.9 temporal vector of list X (refIdx 0) for the PU (x, y, n x n)
+  bool col_at(int xc, int yc, int X, Mv* out) const {
+    if (!fp.col.cu || xc >= W || yc >= H) return false;
+    const int ci = (yc >> kCtbLog2) * wctb + (xc >> kCtbLog2);
+    const CuInfo& cc = fp.col.cu[static_cast<size_t>(ci) * kCusPerCtb + zorder8((xc & (kCtb - 1)) >> 3, (yc & (kCtb - 1)) >> 3)];
+    if (cc.pred != CU_INTER) return false;
+    const int dir = cu_dir(cc);
+    int list;
+    if (!(dir & 1)) list = 1;
+    else if (dir == DIR_L0) list = 0;
+    else list = no_backward ? X : (col_l1 ? 0 : 1);  // N = collocated_from_l0_flag
+    Mv v = list == 0 ? Mv{cc.mv[0], cc.mv[1]} : Mv{cc.mv1[0], cc.mv1[1]};
+    const int col_diff = fp.col.poc - fp.col.ref_poc[list];
+    const int cur_diff = fp.poc - ref_poc(X);
+    if (col_diff != cur_diff && col_diff != 0) v = scale_mv(v, col_diff, cur_diff);
+    *out = v;
+    return true;
+  }
+  bool temporal(int x, int y, int n, int X, Mv* out) const {
+    if (!tmvp) return false;
+    const int xbr = x + n, ybr = y + n;
+    if ((y >> kCtbLog2) == (ybr >> kCtbLog2) && ybr < H && xbr < W && col_at((xbr >> 4) << 4, (ybr >> 4) << 4, X, out))
+      return true;
+    return col_at(((x + (n >> 1)) >> 4) << 4, ((y + (n >> 1)) >> 4) << 4, X, out);
+  }
+
+  // 8.5.3.2.2-8.5.3.2.5 merge candidates of a 2Nx2N PU (MaxNumMergeCand entries)
+  int merge_list(int x, int y, int n, Motion* out) const {
+    Motion cand[8];
+    int k = 0;
+    const int xa1 = x - 1, ya1 = y + n - 1, xb1 = x + n - 1, yb1 = y - 1;
+    const bool a1 = inter_avail(xa1, ya1), av_b1 = inter_avail(xb1, yb1);
+    const Motion ma1 = a1 ? mot_at(xa1, ya1) : Motion{}, mb1 = av_b1 ? mot_at(xb1, yb1) : Motion{};
+    const bool b1 = av_b1 && !(a1 && ma1 == mb1);
+    bool b0 = inter_avail(x + n, y - 1), a0 = inter_avail(x - 1, y + n), b2 = inter_avail(x - 1, y - 1);
+    const Motion mb0 = b0 ? mot_at(x + n, y - 1) : Motion{}, ma0 = a0 ? mot_at(x - 1, y + n) : Motion{};
+    const Motion mb2 = b2 ? mot_at(x - 1, y - 1) : Motion{};
+    if (b0 && av_b1 && mb1 == mb0) b0 = false;
+    if (a0 && a1 && ma1 == ma0) a0 = false;
+    if (b2 && ((a1 && ma1 == mb2) || (av_b1 && mb1 == mb2))) b2 = false;
+    if (a0 + a1 + b0 + b1 == 4) b2 = false;
+    if (a1) cand[k++] = ma1;
+    if (b1) cand[k++] = mb1;
+    if (b0) cand[k++] = mb0;
+    if (a0) cand[k++] = ma0;
+    if (b2) cand[k++] = mb2;
+    if (k < c.max_merge && tmvp) {
+      Motion t{};
+      if (temporal(x, y, n, 0, &t.m[0])) t.dir |= DIR_L0;
+      if (bslice && temporal(x, y, n, 1, &t.m[1])) t.dir |= DIR_L1;
+      if (t.dir) cand[k++] = t;
+    }
+    const int orig = k;
+    if (bslice && orig > 1 && orig < c.max_merge) {  // combined bi-predictive candidates
+      static const int l0i[12] = {0, 1, 0, 2, 1, 2, 0, 3, 1, 3, 2, 3};
+      static const int l1i[12] = {1, 0, 2, 0, 2, 1, 3, 0, 3, 1, 3, 2};
+      for (int comb = 0; comb < orig * (orig - 1) && k < c.max_merge; ++comb) {
+        const Motion &c0 = cand[l0i[comb]], &c1 = cand[l1i[comb]];
+        // (list 0 and list 1 hold different pictures: every such pair is a new candidate)
+        if ((c0.dir & DIR_L0) && (c1.dir & DIR_L1)) cand[k++] = Motion{DIR_BI, {c0.m[0], c1.m[1]}};
+      }
+    }
+    while (k < c.max_merge) cand[k++] = Motion{static_cast<uint8_t>(bslice ? DIR_BI : DIR_L0), {{0, 0}, {0, 0}}};
+    const int nm = std::min(k, c.max_merge);
+    std::copy(cand, cand + nm, out);
+    return nm;
+  }
+
+  // 8.5.3.2.6-8.5.3.2.7 AMVP candidates of list X (refIdx 0)
+  void amvp_list(int x, int y, int n, int X, Mv* out) const {
+    const int Y = 1 - X;
+    const int tgt = ref_poc(X);
+    auto same = [&](int xn, int yn, Mv* v) {  // a neighbour vector pointing at the target picture
+      const Motion& m = mot_at(xn, yn);
+      if ((m.dir >> X) & 1 && ref_poc(X) == tgt) {
+        *v = m.m[X];
+        return true;
+      }
+      if ((m.dir >> Y) & 1 && ref_poc(Y) == tgt) {
+        *v = m.m[Y];
+        return true;
+      }
+      return false;
+    };
+    auto scaled = [&](int xn, int yn, Mv* v) {  // any vector, scaled by the POC distances
+      const Motion& m = mot_at(xn, yn);
+      for (int L : {X, Y}) {
+        if (!((m.dir >> L) & 1)) continue;
+        const int td = fp.poc - ref_poc(L), tb = fp.poc - tgt;
+        *v = (td != tb && td != 0) ? scale_mv(m.m[L], td, tb) : m.m[L];
+        return true;
+      }
+      return false;
+    };
+    const int xa[2] = {x - 1, x - 1}, ya[2] = {y + n, y + n - 1};
+    const bool ava[2] = {inter_avail(xa[0], ya[0]), inter_avail(xa[1], ya[1])};
+    const bool is_scaled = ava[0] || ava[1];
     bool fa = false, fb = false;
     Mv ma{0, 0}, mb{0, 0};
-    if (a0) {
-      ma = mv_at(x - 1, y + n);
-      fa = true;
-    } else if (a1) {
-      ma = mv_at(x - 1, y + n - 1);
-      fa = true;
-    }
-    const int bx[3] = {x + n, x + n - 1, x - 1};
+    for (int k = 0; k < 2 && !fa; ++k)
+      if (ava[k]) fa = same(xa[k], ya[k], &ma);
+    for (int k = 0; k < 2 && !fa; ++k)
+      if (ava[k]) fa = scaled(xa[k], ya[k], &ma);
+    const int xb[3] = {x + n, x + n - 1, x - 1}, yb = y - 1;
+    const bool avb[3] = {inter_avail(xb[0], yb), inter_avail(xb[1], yb), inter_avail(xb[2], yb)};
     for (int k = 0; k < 3 && !fb; ++k)
-      if (inter_avail(bx[k], y - 1)) {
-        mb = mv_at(bx[k], y - 1);
-        fb = true;
-      }
-    const bool scaled = a0 || a1;
-    if (!scaled && fb) {
+      if (avb[k]) fb = same(xb[k], yb, &mb);
+    if (!is_scaled && fb) {
       ma = mb;
       fa = true;
     }
-    // (the re-derivation of B for !scaled finds the same candidate: one reference picture)
+    if (!is_scaled) {
+      fb = false;
+      for (int k = 0; k < 3 && !fb; ++k)
+        if (avb[k]) fb = scaled(xb[k], yb, &mb);
+    }
     int k = 0;
     if (fa) out[k++] = ma;
     if (fb && !(fa && ma == mb)) out[k++] = mb;
+    if (k < 2) {
+      Mv t;
+      if (temporal(x, y, n, X, &t)) out[k++] = t;
+    }
     while (k < 2) out[k++] = Mv{0, 0};
   }
 
   // ---------------------------------------------------------------- coding unit (7.3.8.5)
-  void mark(int x, int y, int n, int d, int sk, int pm, int md, Mv mv) {
+  void mark(int x, int y, int n, int d, int sk, int pm, int md, const Motion& mv) {
     for (int yy = y; yy < y + n; yy += 8)
       for (int xx = x; xx < x + n; xx += 8) {
         const size_t k = g(xx, yy);
@@ -727,10 +827,15 @@ struct Writer {
         skip[k] = static_cast<int8_t>(sk);
         pred[k] = static_cast<int8_t>(pm);
         for (int q = 0; q < 4; ++q) mode4[g4(xx + (q & 1) * 4, yy + (q >> 1) * 4)] = static_cast<int8_t>(md);
-        mvx[k] = static_cast<int16_t>(mv.x);
-        mvy[k] = static_cast<int16_t>(mv.y);
+        mot[k] = mv;
         coded[k] = 1;
       }
+  }
+
+  // inter_pred_idc (9.3.3.7, 2Nx2N PU of a CU at depth d): PRED_BI "1", PRED_L0 "00", PRED_L1 "01"
+  void write_inter_pred_idc(int dir, int d) {
+    e.encode(dir == DIR_BI, ctx[CTX_INTER_PRED + d]);
+    if (dir != DIR_BI) e.encode(dir == DIR_L1, ctx[CTX_INTER_PRED + 4]);
   }
 
   void write_cu(int x, int y, int log2, int d) {
@@ -738,12 +843,16 @@ struct Writer {
     const CuInfo& ci = cu_at(x, y);
     const bool cb_y = any_nonzero(0, x, y, n);
     const bool cb_cb = any_nonzero(1, x / 2, y / 2, n / 2), cb_cr = any_nonzero(2, x / 2, y / 2, n / 2);
-    const bool intra = ci.pred == CU_INTRA || !pslice;
-    const Mv mv{ci.mv[0], ci.mv[1]};
-    if (pslice) {
+    const bool intra = ci.pred == CU_INTRA || !inter_slice;
+    Motion mv{static_cast<uint8_t>(cu_dir(ci)), {{ci.mv[0], ci.mv[1]}, {ci.mv1[0], ci.mv1[1]}}};
+    if (!intra && (mv.dir & ~3 || (!bslice && mv.dir != DIR_L0)))
+      throw std::runtime_error("HEVC: inter CU direction not allowed in this slice");
+    if (!(mv.dir & DIR_L0)) mv.m[0] = Mv{0, 0};
+    if (!(mv.dir & DIR_L1)) mv.m[1] = Mv{0, 0};
+    if (inter_slice) {
       int skip_ctx = (avail(x - 1, y) && skip[g(x - 1, y)]) + (avail(x, y - 1) && skip[g(x, y - 1)]);
       int midx = -1;
-      Mv ml[5];
+      Motion ml[5];
       if (!intra) {
         const int nm = merge_list(x, y, n, ml);
         for (int k = 0; k < nm; ++k)
@@ -769,12 +878,17 @@ struct Writer {
           write_merge_idx(midx);
           ++st.merge_cus;
         } else {
-          Mv ap[2];
-          amvp_list(x, y, n, ap);
-          auto cost = [&](const Mv& p) { return std::abs(mv.x - p.x) + std::abs(mv.y - p.y); };
-          const int idx = cost(ap[1]) < cost(ap[0]) ? 1 : 0;
-          write_mvd_pair(mv.x - ap[idx].x, mv.y - ap[idx].y);
-          e.encode(idx, ctx[CTX_MVP_IDX]);
+          if (bslice) write_inter_pred_idc(mv.dir, d);
+          for (int X = 0; X < 2; ++X) {
+            if (!((mv.dir >> X) & 1)) continue;
+            Mv ap[2];
+            amvp_list(x, y, n, X, ap);
+            const Mv& v = mv.m[X];
+            auto cost = [&](const Mv& p) { return std::abs(v.x - p.x) + std::abs(v.y - p.y); };
+            const int idx = cost(ap[1]) < cost(ap[0]) ? 1 : 0;
+            write_mvd_pair(v.x - ap[idx].x, v.y - ap[idx].y);  // (mvd_l1_zero_flag 0)
+            e.encode(idx, ctx[CTX_MVP_IDX]);
+          }
         }
         const bool root = cb_y || cb_cb || cb_cr;
         if (!merge) e.encode(root, ctx[CTX_RQT_ROOT_CBF]);
@@ -839,7 +953,7 @@ struct Writer {
       }
     }
     e.encode(0, ctx[CTX_CHROMA_MODE]);  // intra_chroma_pred_mode = 4 (DM: the mode of PU 0)
-    mark(x, y, n, d, 0, CU_INTRA, m[0], Mv{0, 0});
+    mark(x, y, n, d, 0, CU_INTRA, m[0], Motion{});
     if (nxn)
       for (int k = 1; k < 4; ++k) mode4[g4(x + (k & 1) * h, y + (k >> 1) * h)] = static_cast<int8_t>(m[k]);
     ++st.intra_cus;
@@ -1001,16 +1115,43 @@ std::vector<uint8_t> hevc_write_slice(const HevcConfig& c, const HevcFrameParams
   if (idr) bw.put_bit(0);     // no_output_of_prior_pics_flag
   bw.put_ue(0);               // slice_pic_parameter_set_id
   bw.put_ue(fp.slice_type);   // slice_type
+  const bool inter = fp.slice_type != 2, bslice = fp.slice_type == 0;
+  if (bslice && fp.ref_poc[1] < 0) throw std::runtime_error("HEVC: a B slice needs ref_poc[1]");
+  if (inter && c.tmvp && !fp.col.set) throw std::runtime_error("HEVC: TMVP needs the collocated picture's records");
   if (!idr) {
     bw.put(fp.poc & 255, 8);  // slice_pic_order_cnt_lsb
-    bw.put_bit(1);            // short_term_ref_pic_set_sps_flag (the single SPS set: no index bits)
+    const int r0 = fp.ref_poc[0] >= 0 ? fp.ref_poc[0] : fp.poc - 1;
+    if (inter && !bslice && r0 == fp.poc - 1) {
+      bw.put_bit(1);          // short_term_ref_pic_set_sps_flag (the single SPS set: no index bits)
+    } else {
+      // st_ref_pic_set(num_short_term_ref_pic_sets = 1) in the slice header (7.3.7): the
+      // reference pictures of this slice, all used by the current picture
+      bw.put_bit(0);          // short_term_ref_pic_set_sps_flag
+      bw.put_bit(0);          // inter_ref_pic_set_prediction_flag
+      const bool has0 = inter, has1 = bslice;
+      if ((has0 && r0 >= fp.poc) || (has1 && fp.ref_poc[1] <= fp.poc))
+        throw std::runtime_error("HEVC: RefPicList0 must precede and RefPicList1 follow the current picture");
+      bw.put_ue(has0 ? 1 : 0);  // num_negative_pics
+      bw.put_ue(has1 ? 1 : 0);  // num_positive_pics
+      if (has0) {
+        bw.put_ue(fp.poc - r0 - 1);  // delta_poc_s0_minus1
+        bw.put_bit(1);               // used_by_curr_pic_s0_flag
+      }
+      if (has1) {
+        bw.put_ue(fp.ref_poc[1] - fp.poc - 1);  // delta_poc_s1_minus1
+        bw.put_bit(1);                          // used_by_curr_pic_s1_flag
+      }
+    }
+    if (c.tmvp) bw.put_bit(1);  // slice_temporal_mvp_enabled_flag
   }
   if (c.sao) {
     bw.put_bit(1);            // slice_sao_luma_flag
     bw.put_bit(1);            // slice_sao_chroma_flag
   }
-  if (fp.slice_type == 1) {
-    bw.put_bit(0);            // num_ref_idx_active_override_flag
+  if (inter) {
+    bw.put_bit(0);            // num_ref_idx_active_override_flag (one picture per list)
+    if (bslice) bw.put_bit(0);  // mvd_l1_zero_flag
+    if (c.tmvp && bslice) bw.put_bit(0);  // collocated_from_l0_flag: the collocated picture is RefPicList1[0]
     bw.put_ue(5 - c.max_merge);  // five_minus_max_num_merge_cand
   }
   bw.put_se(fp.qp - 26);      // slice_qp_delta (init_qp 26)
@@ -1136,7 +1277,7 @@ std::vector<uint8_t> hevc_write_slice(const HevcConfig& c, const HevcFrameParams
     bw.append_bytes(data.data(), data.size());
   }
   std::vector<uint8_t> out;
-  append_hevc_nal(out, idr ? NAL_IDR_W_RADL : NAL_TRAIL_R, bw.bytes());
+  append_hevc_nal(out, idr ? NAL_IDR_W_RADL : (fp.nal_ref ? NAL_TRAIL_R : NAL_TRAIL_N), bw.bytes());
   if (stats) {
     *stats = total;
     stats->bytes = out.size();

@@ -162,7 +162,7 @@ class GpuHevcEncoder:
         self.me_hp = torch.empty(B * 3 * (H + 8) * (W + 8) + 64, dtype=torch.uint8, device=dev)
         self.cand = torch.zeros((B, self.nctb, 58), dtype=torch.int32, device=dev)  # kCandStride
         self.ctus = [torch.zeros((B, self.nctb, 32), dtype=torch.uint8, device=dev) for _ in range(2)]
-        self.cus = [torch.zeros((B, self.nctb * 16, 8), dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.cus = [torch.zeros((B, self.nctb * 16, 16), dtype=torch.uint8, device=dev) for _ in range(2)]
         self.ctu, self.cu = self.ctus[0], self.cus[0]
         # sparse level hand-off (double-buffered like the records: the copy-out of step t
         # overlaps step t + 1)
@@ -330,9 +330,9 @@ class GpuHevcEncoder:
                 newq = np.asarray(rate_fb.update(fb_known, fb_spent, t), dtype=np.int32)
                 if not np.array_equal(newq[:, t:], qps[:, t:]):
                     qps[:, t:] = newq[:, t:]
-                    st = torch.from_numpy(np.ascontiguousarray(qps[:, t:].T)).pin_memory()
-                    qps_d[t:].copy_(st, non_blocking=True)  # stream-ordered before frame t's read
-                    fb_stage.append(st)  # keep the pinned source alive until the encode ends
+                    staged = torch.from_numpy(np.ascontiguousarray(qps[:, t:].T)).pin_memory()
+                    qps_d[t:].copy_(staged, non_blocking=True)  # stream-ordered before frame t's read
+                    fb_stage.append(staged)  # keep the pinned source alive until the encode ends
             idr = t == 0 or self.p.intra_only or (self.p.keyint > 0 and t % self.p.keyint == 0)
             self._prep(y, u, v, t, proxy=not idr)
             self.qp.copy_(qps_d[t])  # device-to-device: no host sync inside the frame loop

@@ -45,14 +45,24 @@ def _levels(rng, n: int, density: float) -> np.ndarray:
 
 def random_records(rng, width: int, height: int, pslice: bool, bit_depth: int = 8, density: float = 0.08,
                    intra_in_p: float = 0.2, mv_range: int = 64, sao: bool = True, ctb_qp: tuple | None = None,
-                   nxn: float = 0.0, tu_split: float = 0.0, force_split: int | None = None):
+                   nxn: float = 0.0, tu_split: float = 0.0, force_split: int | None = None, bslice: bool = False,
+                   mv_pool: int = 0):
     """``ctb_qp = (qp, spread)``: per-CTB QPs qp + U[-spread, spread] (cu_qp_delta streams);
     ``nxn``: probability of an 8x8 intra CU being split into four 4x4 PUs; ``tu_split``: of a
-    16x16 / 32x32 inter CU coding its residual as four quarter TUs (needs tu_inter_depth 1)."""
+    16x16 / 32x32 inter CU coding its residual as four quarter TUs (needs tu_inter_depth 1);
+    ``bslice``: inter CUs predict from list 0, list 1 or both (CuInfo.dir, mv1); ``mv_pool`` > 0:
+    vectors drawn from that many values, so merge candidates (spatial, temporal, combined
+    bi-predictive, zero) match often."""
+    pool = rng.integers(-mv_range, mv_range + 1, (max(1, mv_pool), 2)).astype(np.int16) if mv_pool else None
+
+    def rand_mv():
+        if pool is not None:
+            return pool[int(rng.integers(0, len(pool)))].copy()
+        return rng.integers(-mv_range, mv_range + 1, 2).astype(np.int16)
     W, H = -(-width // CTB) * CTB, -(-height // CTB) * CTB
     wc, hc = W // CTB, H // CTB
     ctu = np.zeros((wc * hc, 32), np.uint8)
-    cu = np.zeros((wc * hc * 16, 8), np.uint8)
+    cu = np.zeros((wc * hc * 16, 16), np.uint8)
     cy = np.zeros((H, W), np.int16)
     cb = np.zeros((H // 2, W // 2), np.int16)
     cr = np.zeros((H // 2, W // 2), np.int16)
@@ -85,7 +95,7 @@ def random_records(rng, width: int, height: int, pslice: bool, bit_depth: int = 
                 t[2:22] = ctu[i - 1, 2:22]
         for (x, y, n) in _cu_list(split):
             intra = (not pslice) or rng.random() < intra_in_p
-            rec = np.zeros(8, np.uint8)
+            rec = np.zeros(16, np.uint8)
             rec[0] = 0 if intra else 1
             if intra:
                 rec[1] = int(rng.integers(0, 35))
@@ -96,10 +106,21 @@ def random_records(rng, width: int, height: int, pslice: bool, bit_depth: int = 
             else:
                 if n >= 16 and rng.random() < tu_split:   # residual quadtree split once (flags bit 4)
                     rec[3] |= 16
-                mv = rng.integers(-mv_range, mv_range + 1, 2).astype(np.int16)
+                mv = rand_mv()
                 if rng.random() < 0.3:
                     mv[:] = 0
-                rec[4:8] = mv.view(np.uint8)
+                if bslice:
+                    d = int(rng.integers(1, 4))
+                    mv1 = rand_mv()
+                    if rng.random() < 0.3:
+                        mv1[:] = 0
+                    rec[12] = d
+                    if d & 1:
+                        rec[4:8] = mv.view(np.uint8)
+                    if d & 2:
+                        rec[8:12] = mv1.view(np.uint8)
+                else:
+                    rec[4:8] = mv.view(np.uint8)
             for gy in range(y // 8, (y + n) // 8):
                 for gx in range(x // 8, (x + n) // 8):
                     cu[i * 16 + _zorder8(gx, gy)] = rec
@@ -126,6 +147,39 @@ def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp:
         nal, _ = host.hevc_write_slice(cfg, dict(idr=int(t == 0), poc=t, qp=fqp, slice_type=1 if t else 2), *r)
         out.append(nal)
         recs.append(r)
+    return b"".join(out), recs
+
+
+def random_gop_stream(host, width: int, height: int, frames: int, bframes: int = 3, seed: int = 0, qp: int = 30,
+                      bit_depth: int = 8, tmvp: bool = True, host_cfg: dict | None = None, **kw) -> tuple[bytes, list]:
+    """Annex-B HEVC stream of one closed GOP with B pictures (models/gop.py coding order:
+    I, P anchors, non-reference B pictures referencing the anchors on both sides) from
+    random records; TMVP takes the collocated records of the anchors.  Returns the stream
+    and the records per *display* index (the decoder outputs pictures in POC order)."""
+    from ..models.gop import gop_plan
+
+    rng = np.random.default_rng(seed)
+    cfg = dict(width=width, height=height, bit_depth=bit_depth, bframes=bframes, tmvp=int(tmvp), **(host_cfg or {}))
+    out = [host.hevc_parameter_sets(cfg)]
+    recs: list = [None] * frames
+    anchor_cu: dict = {}    # display index -> (cu records or None for intra, L0 reference POC)
+    for pic in gop_plan(frames, bframes):
+        fqp = int(np.clip(qp + rng.integers(-3, 4), 0, 51))
+        r = random_records(rng, width, height, pslice=pic.kind != "I", bit_depth=bit_depth, bslice=pic.kind == "B", **kw)
+        fp = dict(idr=int(pic.kind == "I"), poc=pic.d, qp=fqp, slice_type={"I": 2, "P": 1, "B": 0}[pic.kind],
+                  nal_ref=int(pic.kind != "B"))
+        if pic.kind != "I":
+            fp["ref_poc0"] = pic.l0
+            col = pic.l1 if pic.kind == "B" else pic.l0
+            if pic.kind == "B":
+                fp["ref_poc1"] = pic.l1
+            ccu, cref = anchor_cu[col]
+            fp.update(col_poc=col, col_ref_poc0=cref, col_ref_poc1=cref, col_cu=ccu)
+        nal, _ = host.hevc_write_slice(cfg, fp, *r)
+        if pic.kind != "B":
+            anchor_cu[pic.d] = (None if pic.kind == "I" else r[1].copy(), pic.l0)
+        out.append(nal)
+        recs[pic.d] = r
     return b"".join(out), recs
 
 

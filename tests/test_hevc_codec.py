@@ -82,14 +82,14 @@ def test_hevc_flat_dc_and_zero_motion(host, bd):
     w, h = 64, 64
     cfg = dict(width=w, height=h, bit_depth=bd, sao=0)
     ctu = np.zeros((4, 32), np.uint8)
-    cu = np.zeros((64, 8), np.uint8)
+    cu = np.zeros((64, 16), np.uint8)
     cu[:, 1] = 1   # DC everywhere
     z = np.zeros((h, w), np.int16)
     zc = np.zeros((h // 2, w // 2), np.int16)
     s = host.hevc_parameter_sets(cfg)
     s += host.hevc_write_slice(cfg, dict(idr=1, poc=0, qp=30), ctu, cu, z, zc, zc)[0]
     # a P picture of zero-motion inter CUs with a luma DC residual in CTB 0
-    cup = np.zeros((64, 8), np.uint8)
+    cup = np.zeros((64, 16), np.uint8)
     cup[:, 0] = 1
     zy = z.copy()
     zy[0, 0] = 8
@@ -231,3 +231,41 @@ def test_hevc_short_merge_lists(host, max_merge):
     for p, (ctu, cu, cy, cb, cr) in zip(host.hevc_decode(s, False), recs):
         inter = cu[:, 0] == 1
         assert np.array_equal(p["cu"][inter, 4:8], cu[inter, 4:8])
+
+
+@pytest.mark.parametrize("seed,tmvp,max_merge,wpp", [(0, 0, 3, 0), (1, 1, 3, 1), (2, 1, 5, 0), (3, 1, 1, 1), (4, 0, 5, 1)])
+def test_hevc_b_gop_roundtrip(host, seed, tmvp, max_merge, wpp):
+    """B pictures (x265 --bframes): I, P anchors and non-reference B slices predicting from
+    list 0, list 1 or both, with explicit slice RPS, TRAIL_N NAL units and (tmvp) temporal
+    merge / AMVP candidates from the collocated anchor's records.  Vectors come from a small
+    pool so spatial, temporal, combined bi-predictive and zero merge candidates all match;
+    the decoder must recover every direction and vector in display order."""
+    from govideocompressor_amd.utils.hevc_synth import random_gop_stream
+
+    s, recs = random_gop_stream(host, 128, 96, 9, bframes=3, seed=seed, tmvp=bool(tmvp), mv_pool=3 if seed % 2 else 0,
+                                intra_in_p=0.05, density=0.02, host_cfg=dict(max_merge=max_merge, wpp=wpp))
+    pics = host.hevc_decode(s)
+    assert len(pics) == 9
+    for d, (p, (ctu, cu, cy, cb, cr)) in enumerate(zip(pics, recs)):
+        assert p["poc"] == d
+        assert p["slice_type"] == (2 if d == 0 else (1 if d in (4, 8) else 0))
+        assert np.array_equal(p["coef_y"], cy) and np.array_equal(p["coef_cb"], cb) and np.array_equal(p["coef_cr"], cr)
+        assert np.array_equal(p["cu"][:, 0], cu[:, 0])
+        inter = cu[:, 0] == 1
+        dirs = np.where(cu[:, 12] == 0, 1, cu[:, 12])
+        assert np.array_equal(p["cu"][inter, 12], dirs[inter])
+        assert np.array_equal(p["cu"][inter, 4:12], cu[inter, 4:12])
+
+
+def test_hevc_writer_rejects_bad_b_params(host):
+    from govideocompressor_amd.utils.hevc_synth import random_records
+
+    rng = np.random.default_rng(0)
+    r = random_records(rng, 64, 64, pslice=True, bslice=True)
+    cfg = dict(width=64, height=64, bframes=3, tmvp=1)
+    with pytest.raises(RuntimeError, match="ref_poc"):
+        host.hevc_write_slice(cfg, dict(idr=0, poc=2, qp=30, slice_type=0, ref_poc0=0), *r)
+    with pytest.raises(RuntimeError, match="collocated"):
+        host.hevc_write_slice(cfg, dict(idr=0, poc=2, qp=30, slice_type=0, ref_poc0=0, ref_poc1=4), *r)
+    with pytest.raises(RuntimeError, match="direction"):   # list-1 motion in a P slice
+        host.hevc_write_slice(dict(width=64, height=64), dict(idr=0, poc=1, qp=30, slice_type=1), *r)
