@@ -429,6 +429,177 @@ __global__ __launch_bounds__(64) void hevc_merge_refine(PRefineArgs a) {
   }
 }
 
+// ---- HEVC B pictures (x265 --bframes): the two searches (list 0 against the previous
+// anchor, list 1 against the next) become one motion per 16x16 block -- L0, L1 or bi --
+// and then merge-aware passes like hevc_merge_refine, over B motion (direction + two
+// vectors).  Motion per block: mvb [B, nmb, 4] = (L0 x, y, L1 x, y), dir [B, nmb] (CuDir),
+// cost = SATD + lambda * bits and bits (so a pass can recover the SATD part).
+struct HevcBArgs {
+  Geom g;
+  const uint8_t* src_y;
+  const uint8_t *ref0, *ref1;   // 8-bit proxies of RefPicList0[0] / RefPicList1[0]
+  const uint8_t *hp0, *hp1;     // their half-sample planes
+  const int16_t *mv0, *mv1;     // [B, nmb, 2] searched vectors
+  const int *cost0, *cost1;     // their costs against pm0 / pm1
+  const int16_t *pm0, *pm1;     // search predictors
+  const int16_t* tmv;           // [B, nmb, 4] temporal merge candidate (both lists)
+  const uint8_t* tdir;          // [B, nmb] its direction (0: none)
+  const int16_t* mvb_in;        // [B, nmb, 4]
+  const uint8_t* dir_in;        // [B, nmb]
+  int16_t* mvb_out;
+  uint8_t* dir_out;
+  int* cost;                    // [B, nmb]
+  int* bits;                    // [B, nmb]
+  const int* qp;
+  const int8_t* aq;
+};
+
+// luma prediction (4 samples of row Y, columns X..X+3) of a B motion
+__device__ __forceinline__ uint32_t mc4_b(const HevcBArgs& a, const uint8_t* G0, const uint8_t* H0, const uint8_t* G1,
+                                          const uint8_t* H1, int X, int Y, int dir, int x0, int y0, int x1, int y1) {
+  const int W = a.g.W, H = a.g.H;
+  if (dir == 1) return mc4(G0, H0, W, H, X, Y, x0, y0);
+  if (dir == 2) return mc4(G1, H1, W, H, X, Y, x1, y1);
+  return avg4b(mc4(G0, H0, W, H, X, Y, x0, y0), mc4(G1, H1, W, H, X, Y, x1, y1));
+}
+
+// SATD of a 16x16 block's residual against a prediction word per lane (whole wave calls)
+__device__ __forceinline__ int satd16_words(int* s_res, uint32_t src, uint32_t pw, int r, int c0) {
+  const int lane = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    s_res[r * 16 + c0 + k] = static_cast<int>((src >> (8 * k)) & 255u) - static_cast<int>((pw >> (8 * k)) & 255u);
+  wave_sync();
+  int satd = 0;
+  if (lane < 16) {
+    const int bx = (lane & 3) * 4, by = (lane >> 2) * 4;
+    int rr[16];
+#pragma unroll
+    for (int y = 0; y < 4; ++y)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) rr[y * 4 + x] = s_res[(by + y) * 16 + bx + x];
+    satd = h264::satd4x4(rr);
+  }
+  satd = __builtin_amdgcn_readlane(sum16(satd), 0);
+  wave_sync();
+  return satd;
+}
+
+__global__ __launch_bounds__(64) void hevc_b_choose(HevcBArgs a) {
+  const Geom& g = a.g;
+  const int nmb = g.nmb();
+  int mb, slot;
+  xcd_unit_slot(mb, slot);
+  const int lane = threadIdx.x;
+  const size_t o = static_cast<size_t>(slot) * nmb + mb;
+  const int mx = mb % g.wmb, my = mb / g.wmb;
+  const int r = lane >> 2, c0 = (lane & 3) * 4;
+  const int X = mx * 16 + c0, Y = my * 16 + r;
+  const size_t yo = static_cast<size_t>(slot) * g.ysize();
+  const size_t ho = static_cast<size_t>(slot) * 3 * (g.W + 2 * kHpMargin) * (g.H + 2 * kHpMargin);
+  const uint8_t *G0 = a.ref0 + yo, *G1 = a.ref1 + yo, *H0 = a.hp0 + ho, *H1 = a.hp1 + ho;
+  const int x0 = a.mv0[o * 2], y0 = a.mv0[o * 2 + 1], x1 = a.mv1[o * 2], y1 = a.mv1[o * 2 + 1];
+  const uint32_t src = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y) * g.W + X);
+  __shared__ int s_res[256];
+  const int satd_bi = satd16_words(s_res, src, mc4_b(a, G0, H0, G1, H1, X, Y, 3, x0, y0, x1, y1), r, c0);
+  const int qp = clampi(a.qp[slot] + (a.aq ? a.aq[o] : 0), 0, 51);
+  const int lam = h264::kLambda[qp];
+  const int b0 = mvbits_se(x0 - a.pm0[o * 2]) + mvbits_se(y0 - a.pm0[o * 2 + 1]);
+  const int b1 = mvbits_se(x1 - a.pm1[o * 2]) + mvbits_se(y1 - a.pm1[o * 2 + 1]);
+  // inter_pred_idc: "1" bi, "00" / "01" single list
+  const int c_l0 = a.cost0[o] + 2 * lam, c_l1 = a.cost1[o] + 2 * lam;
+  const int c_bi = satd_bi + lam * (b0 + b1 + 1);
+  int dir = 1, best = c_l0, bits = b0 + 2;
+  if (c_l1 < best) { dir = 2; best = c_l1; bits = b1 + 2; }
+  if (c_bi < best) { dir = 3; best = c_bi; bits = b0 + b1 + 1; }
+  if (lane == 0) {
+    int16_t* m = a.mvb_out + o * 4;
+    m[0] = static_cast<int16_t>(dir & 1 ? x0 : 0);
+    m[1] = static_cast<int16_t>(dir & 1 ? y0 : 0);
+    m[2] = static_cast<int16_t>(dir & 2 ? x1 : 0);
+    m[3] = static_cast<int16_t>(dir & 2 ? y1 : 0);
+    a.dir_out[o] = static_cast<uint8_t>(dir);
+    a.cost[o] = best;
+    a.bits[o] = bits;
+  }
+}
+
+// Jacobi pass: candidates are the neighbours' current B motions (A1, B1, B0, A0, B2 of the
+// 16x16 grid), the temporal candidate and the zero bi-prediction; the cheapest by SATD +
+// lambda * (merge_flag + merge_idx) replaces the block's motion when it beats its cost
+__global__ __launch_bounds__(64) void hevc_b_merge(HevcBArgs a) {
+  const Geom& g = a.g;
+  const int nmb = g.nmb();
+  int mb, slot;
+  xcd_unit_slot(mb, slot);
+  const int lane = threadIdx.x;
+  const size_t o = static_cast<size_t>(slot) * nmb + mb;
+  const size_t sb = static_cast<size_t>(slot) * nmb;
+  const int mx = mb % g.wmb, my = mb / g.wmb;
+  int kd[7], kv[7][4], nk = 0;
+  auto add = [&](int d, const int16_t* v) {
+    if (!d) return;
+    int w[4] = {d & 1 ? v[0] : 0, d & 1 ? v[1] : 0, d & 2 ? v[2] : 0, d & 2 ? v[3] : 0};
+    for (int j = 0; j < nk; ++j)
+      if (kd[j] == d && kv[j][0] == w[0] && kv[j][1] == w[1] && kv[j][2] == w[2] && kv[j][3] == w[3]) return;
+    kd[nk] = d;
+    for (int c = 0; c < 4; ++c) kv[nk][c] = w[c];
+    ++nk;
+  };
+  auto nb = [&](bool ok, int n) {
+    if (ok) add(a.dir_in[sb + n], a.mvb_in + (sb + n) * 4);
+  };
+  nb(mx > 0, mb - 1);                              // A1
+  nb(my > 0, mb - g.wmb);                          // B1
+  nb(my > 0 && mx < g.wmb - 1, mb - g.wmb + 1);    // B0
+  nb(mx > 0 && my < g.hmb - 1, mb + g.wmb - 1);    // A0
+  nb(mx > 0 && my > 0, mb - g.wmb - 1);            // B2
+  if (a.tdir) add(a.tdir[o], a.tmv + o * 4);
+  {
+    const int16_t z[4] = {0, 0, 0, 0};
+    add(3, z);
+  }
+  const int cd = a.dir_in[o];
+  const int16_t* cv = a.mvb_in + o * 4;
+  const int qp = clampi(a.qp[slot] + (a.aq ? a.aq[o] : 0), 0, 51);
+  const int lam = h264::kLambda[qp];
+  const int c_cur = a.cost[o];
+  const int satd_cur = c_cur - lam * a.bits[o];
+  const int r = lane >> 2, c0 = (lane & 3) * 4;
+  const int X = mx * 16 + c0, Y = my * 16 + r;
+  const size_t yo = static_cast<size_t>(slot) * g.ysize();
+  const size_t ho = static_cast<size_t>(slot) * 3 * (g.W + 2 * kHpMargin) * (g.H + 2 * kHpMargin);
+  const uint8_t *G0 = a.ref0 + yo, *G1 = a.ref1 + yo, *H0 = a.hp0 + ho, *H1 = a.hp1 + ho;
+  const uint32_t src = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y) * g.W + X);
+  __shared__ int s_res[256];
+  int best = c_cur, bbits = a.bits[o], bj = -1;
+  for (int j = 0; j < nk; ++j) {
+    const bool same = kd[j] == cd && (!(cd & 1) || (kv[j][0] == cv[0] && kv[j][1] == cv[1])) &&
+                      (!(cd & 2) || (kv[j][2] == cv[2] && kv[j][3] == cv[3]));
+    int satd;
+    if (same) satd = satd_cur;
+    else satd = satd16_words(s_res, src, mc4_b(a, G0, H0, G1, H1, X, Y, kd[j], kv[j][0], kv[j][1], kv[j][2], kv[j][3]), r, c0);
+    const int cst = satd + lam * (1 + j);
+    if (cst < best) {
+      best = cst;
+      bbits = 1 + j;
+      bj = j;
+    }
+  }
+  if (lane == 0) {
+    int16_t* m = a.mvb_out + o * 4;
+    if (bj >= 0) {
+      for (int c = 0; c < 4; ++c) m[c] = static_cast<int16_t>(kv[bj][c]);
+      a.dir_out[o] = static_cast<uint8_t>(kd[bj]);
+    } else {
+      for (int c = 0; c < 4; ++c) m[c] = cv[c];
+      a.dir_out[o] = static_cast<uint8_t>(cd);
+    }
+    a.cost[o] = best;
+    a.bits[o] = bbits;
+  }
+}
+
 // ---- P_8x8 / P_16x8 / P_8x16 partitions (x264 --partitions p8x8, its default).  After the
 // 16x16 search and the skip-aware refinement, each 8x8 quadrant of a P macroblock searches
 // its own vector: predictor candidates (the MB's vector, the left / top / top-right /
@@ -724,4 +895,37 @@ extern "C" void mivc_launch_hevc_merge_refine(int B, int wmb, int hmb, const uin
   a.qp = qp;
   a.aq = aq;
   hipLaunchKernelGGL(hevc_merge_refine, dim3(wmb * hmb, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
+}
+
+extern "C" void mivc_launch_hevc_b(int mode, int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref0,
+                                   const uint8_t* ref1, const uint8_t* hp0, const uint8_t* hp1, const int16_t* mv0,
+                                   const int16_t* mv1, const int* cost0, const int* cost1, const int16_t* pm0,
+                                   const int16_t* pm1, const int16_t* tmv, const uint8_t* tdir, const int16_t* mvb_in,
+                                   const uint8_t* dir_in, int16_t* mvb_out, uint8_t* dir_out, int* cost, int* bits,
+                                   const int* qp, const int8_t* aq, void* stream) {
+  HevcBArgs a;
+  a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
+  a.src_y = src_y;
+  a.ref0 = ref0;
+  a.ref1 = ref1;
+  a.hp0 = hp0;
+  a.hp1 = hp1;
+  a.mv0 = mv0;
+  a.mv1 = mv1;
+  a.cost0 = cost0;
+  a.cost1 = cost1;
+  a.pm0 = pm0;
+  a.pm1 = pm1;
+  a.tmv = tmv;
+  a.tdir = tdir;
+  a.mvb_in = mvb_in;
+  a.dir_in = dir_in;
+  a.mvb_out = mvb_out;
+  a.dir_out = dir_out;
+  a.cost = cost;
+  a.bits = bits;
+  a.qp = qp;
+  a.aq = aq;
+  if (mode == 0) hipLaunchKernelGGL(hevc_b_choose, dim3(wmb * hmb, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
+  else hipLaunchKernelGGL(hevc_b_merge, dim3(wmb * hmb, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
 }

@@ -79,7 +79,13 @@ void mivc_launch_hevc_inter(int B, int W, int H, const uint16_t* sy, const uint1
                             const uint16_t* fy, const uint16_t* fu, const uint16_t* fv, uint16_t* ry, uint16_t* ru,
                             uint16_t* rv, void* ctu, void* cu, int16_t* cy, int16_t* cu_, int16_t* cv, const int* qp,
                             const int8_t* run, const int* cand, const int16_t* mv, const int* me_cost, int bd,
-                            int tu_split, int sdh, int intra_bias, void* stream);
+                            int tu_split, int sdh, int intra_bias, void* stream, const int16_t* mvb,
+                            const uint8_t* dirb, const uint16_t* f1y, const uint16_t* f1u, const uint16_t* f1v);
+void mivc_launch_hevc_b(int mode, int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref0, const uint8_t* ref1,
+                        const uint8_t* hp0, const uint8_t* hp1, const int16_t* mv0, const int16_t* mv1, const int* cost0,
+                        const int* cost1, const int16_t* pm0, const int16_t* pm1, const int16_t* tmv, const uint8_t* tdir,
+                        const int16_t* mvb_in, const uint8_t* dir_in, int16_t* mvb_out, uint8_t* dir_out, int* cost,
+                        int* bits, const int* qp, const int8_t* aq, void* stream);
 void mivc_launch_hevc_deblock(int B, int W, int H, int bd, uint16_t* y, uint16_t* u, uint16_t* v, const void* cu,
                               const void* ctu, const int8_t* run, void* stream);
 void mivc_launch_hevc_aq(int B, int W, int H, int bd, const uint16_t* sy, const uint16_t* su, const uint16_t* sv,
@@ -304,11 +310,36 @@ PYBIND11_MODULE(_hip, m) {
   m.def("hevc_inter", [](int B, int W, int H, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t fy, uintptr_t fu,
                          uintptr_t fv, uintptr_t ry, uintptr_t ru, uintptr_t rv, uintptr_t ctu, uintptr_t cu, uintptr_t cy,
                          uintptr_t cu_, uintptr_t cv, uintptr_t qp, uintptr_t run, uintptr_t cand, uintptr_t mv,
-                         uintptr_t me_cost, int bd, uintptr_t stream, int tu_split, int sdh, int intra_bias) {
+                         uintptr_t me_cost, int bd, uintptr_t stream, int tu_split, int sdh, int intra_bias,
+                         uintptr_t mvb, uintptr_t dirb, uintptr_t f1y, uintptr_t f1u, uintptr_t f1v) {
+    if (dirb && (!mvb || !f1y || !f1u || !f1v)) throw std::invalid_argument("hevc_inter: B motion needs mvb and list-1 planes");
     mivc_launch_hevc_inter(B, W, H, P<uint16_t>(sy), P<uint16_t>(su), P<uint16_t>(sv), P<uint16_t>(fy), P<uint16_t>(fu),
                            P<uint16_t>(fv), P<uint16_t>(ry), P<uint16_t>(ru), P<uint16_t>(rv), P<void>(ctu), P<void>(cu),
                            P<int16_t>(cy), P<int16_t>(cu_), P<int16_t>(cv), P<int>(qp), P<int8_t>(run), P<int>(cand),
-                           P<int16_t>(mv), P<int>(me_cost), bd, tu_split, sdh, intra_bias, S(stream));
+                           P<int16_t>(mv), P<int>(me_cost), bd, tu_split, sdh, intra_bias, S(stream), P<int16_t>(mvb),
+                           P<uint8_t>(dirb), P<uint16_t>(f1y), P<uint16_t>(f1u), P<uint16_t>(f1v));
+  }, py::arg("B"), py::arg("W"), py::arg("H"), py::arg("sy"), py::arg("su"), py::arg("sv"), py::arg("fy"), py::arg("fu"),
+     py::arg("fv"), py::arg("ry"), py::arg("ru"), py::arg("rv"), py::arg("ctu"), py::arg("cu"), py::arg("cy"),
+     py::arg("cu_"), py::arg("cv"), py::arg("qp"), py::arg("run"), py::arg("cand"), py::arg("mv"), py::arg("me_cost"),
+     py::arg("bd"), py::arg("stream"), py::arg("tu_split") = 0, py::arg("sdh") = 0, py::arg("intra_bias") = 0,
+     py::arg("mvb") = 0, py::arg("dirb") = 0, py::arg("f1y") = 0, py::arg("f1u") = 0, py::arg("f1v") = 0);
+  m.def("hevc_b", [](int mode, int B, int wmb, int hmb, uintptr_t src, uintptr_t ref0, uintptr_t ref1, uintptr_t hp0,
+                     uintptr_t hp1, uintptr_t mv0, uintptr_t mv1, uintptr_t cost0, uintptr_t cost1, uintptr_t pm0,
+                     uintptr_t pm1, uintptr_t tmv, uintptr_t tdir, uintptr_t mvb_in, uintptr_t dir_in, uintptr_t mvb_out,
+                     uintptr_t dir_out, uintptr_t cost, uintptr_t bits, uintptr_t qp, uintptr_t aq, uintptr_t stream) {
+    // mode 0: L0 / L1 / bi choice from the two searches; 1: one merge-aware Jacobi pass
+    if (mode != 0 && mode != 1) throw std::invalid_argument("hevc_b: mode 0 (choose) or 1 (merge pass)");
+    if (!src || !ref0 || !ref1 || !hp0 || !hp1 || !mvb_out || !dir_out || !cost || !bits || !qp)
+      throw std::invalid_argument("hevc_b: missing buffer");
+    if (mode == 0 && (!mv0 || !mv1 || !cost0 || !cost1 || !pm0 || !pm1)) throw std::invalid_argument("hevc_b: choose needs both searches");
+    if (mode == 1 && (!mvb_in || !dir_in || mvb_in == mvb_out || dir_in == dir_out))
+      throw std::invalid_argument("hevc_b: a merge pass reads and writes different motion buffers");
+    if (tdir && !tmv) throw std::invalid_argument("hevc_b: tdir needs tmv");
+    mivc_launch_hevc_b(mode, B, wmb, hmb, P<uint8_t>(src), P<uint8_t>(ref0), P<uint8_t>(ref1), P<uint8_t>(hp0),
+                       P<uint8_t>(hp1), P<int16_t>(mv0), P<int16_t>(mv1), P<int>(cost0), P<int>(cost1), P<int16_t>(pm0),
+                       P<int16_t>(pm1), P<int16_t>(tmv), P<uint8_t>(tdir), P<int16_t>(mvb_in), P<uint8_t>(dir_in),
+                       P<int16_t>(mvb_out), P<uint8_t>(dir_out), P<int>(cost), P<int>(bits), P<int>(qp), P<int8_t>(aq),
+                       S(stream));
   });
   m.def("hevc_deblock", [](int B, int W, int H, int bd, uintptr_t y, uintptr_t u, uintptr_t v, uintptr_t cu,
                            uintptr_t ctu, uintptr_t run, uintptr_t stream) {

@@ -169,8 +169,15 @@ __global__ void hevc_deblock(HevcDbkArgs a) {
   int bs;
   if (P.pred == hevc::CU_INTRA || Q.pred == hevc::CU_INTRA) bs = 2;
   else if ((P.cbf & 1) || (Q.cbf & 1)) bs = 1;
-  else if (abs(P.mv[0] - Q.mv[0]) >= 4 || abs(P.mv[1] - Q.mv[1]) >= 4) bs = 1;
-  else bs = 0;
+  else {
+    // 8.7.2.4 with one picture per list and RefPicList0[0] != RefPicList1[0]: the direction
+    // fixes the set of reference pictures; equal sets compare the vectors list by list
+    const int dp = hevc::cu_dir(P), dq = hevc::cu_dir(Q);
+    if (dp != dq) bs = 1;
+    else if ((dp & 1) && (abs(P.mv[0] - Q.mv[0]) >= 4 || abs(P.mv[1] - Q.mv[1]) >= 4)) bs = 1;
+    else if ((dp & 2) && (abs(P.mv1[0] - Q.mv1[0]) >= 4 || abs(P.mv1[1] - Q.mv1[1]) >= 4)) bs = 1;
+    else bs = 0;
+  }
   if (!bs) return;
   const int bd = a.bd, maxv = (1 << bd) - 1;
   const int qpl = (qp_at(a, slot, xp, yp) + qp_at(a, slot, xq, yq) + 1) >> 1;  // 8.7.2.5.3

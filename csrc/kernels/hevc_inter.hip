@@ -33,7 +33,10 @@ struct HevcInterArgs {
   const int* qp;          // [B, nctb] QpY per CTB
   const int8_t* run;
   const int* cand;       // [B, nctb, kCandStride] intra analysis: best cost / mode per CU, NxN PUs
-  const int16_t* mv;     // [B, nmb16, 2] quarter-sample vectors per 16x16 block
+  const int16_t* mv;     // [B, nmb16, 2] quarter-sample vectors per 16x16 block (P pictures)
+  const int16_t* mvb;    // [B, nmb16, 4] B pictures: (L0 x, y, L1 x, y) per 16x16 block, or null
+  const uint8_t* dirb;   // [B, nmb16] B pictures: CuDir per 16x16 block
+  const uint16_t *ref1_y, *ref1_u, *ref1_v;  // RefPicList1[0] (B pictures)
   const int* me_cost;    // [B, nmb16] (8-bit proxy units)
   int bd;
   int tu_split;          // inter CUs may code their residual as four quarter TUs (RD choice)
@@ -57,7 +60,7 @@ __global__ __launch_bounds__(64) void hevc_p_decide(HevcInterArgs a) {
   const int wmb = g.W / 16, nmb = wmb * (g.H / 16);
   const int qp = a.qp[cb];
   const int lam = lambda_satd_i(qp, a.bd);
-  __shared__ int s_inter[4], s_mvx[4], s_mvy[4], s_split8[4], s_intra[4];
+  __shared__ int s_inter[4], s_mvx[4], s_mvy[4], s_mv1x[4], s_mv1y[4], s_dir[4], s_split8[4], s_intra[4];
   __shared__ int s_split;
   if (lane < 4) {
     const int q = lane;
@@ -70,8 +73,19 @@ __global__ __launch_bounds__(64) void hevc_p_decide(HevcInterArgs a) {
     s_split8[q] = s8 < c16;
     s_intra[q] = (s8 < c16 ? s8 : c16) + lam * a.intra_bias;
     s_inter[q] = inter;
-    s_mvx[q] = a.mv[o * 2];
-    s_mvy[q] = a.mv[o * 2 + 1];
+    if (a.dirb) {
+      const int16_t* m = a.mvb + o * 4;
+      s_mvx[q] = m[0];
+      s_mvy[q] = m[1];
+      s_mv1x[q] = m[2];
+      s_mv1y[q] = m[3];
+      s_dir[q] = a.dirb[o];
+    } else {
+      s_mvx[q] = a.mv[o * 2];
+      s_mvy[q] = a.mv[o * 2 + 1];
+      s_mv1x[q] = s_mv1y[q] = 0;
+      s_dir[q] = hevc::DIR_L0;
+    }
   }
   __syncthreads();
   if (lane == 0) {
@@ -89,8 +103,10 @@ __global__ __launch_bounds__(64) void hevc_p_decide(HevcInterArgs a) {
       for (int q = 0; q < 4; ++q) split |= (split & 1) && s_split8[q] ? 1 << (1 + q) : 0;
       for (int q = 0; q < 4; ++q) s_inter[q] = 0x7FFFFFFF;  // mark intra
     } else {
-      const bool same = n_inter == 4 && s_mvx[0] == s_mvx[1] && s_mvx[0] == s_mvx[2] && s_mvx[0] == s_mvx[3] &&
-                        s_mvy[0] == s_mvy[1] && s_mvy[0] == s_mvy[2] && s_mvy[0] == s_mvy[3];
+      bool same = n_inter == 4;
+      for (int q = 1; q < 4; ++q)
+        same = same && s_dir[q] == s_dir[0] && s_mvx[q] == s_mvx[0] && s_mvy[q] == s_mvy[0] && s_mv1x[q] == s_mv1x[0] &&
+               s_mv1y[q] == s_mv1y[0];
       split = same ? 0 : 1;
       for (int q = 0; q < 4; ++q) {
         const bool inter = s_inter[q] < s_intra[q];
@@ -118,6 +134,9 @@ __global__ __launch_bounds__(64) void hevc_p_decide(HevcInterArgs a) {
       c.pred = hevc::CU_INTER;
       c.mv[0] = static_cast<int16_t>(s_mvx[q]);
       c.mv[1] = static_cast<int16_t>(s_mvy[q]);
+      c.mv1[0] = static_cast<int16_t>(s_mv1x[q]);
+      c.mv1[1] = static_cast<int16_t>(s_mv1y[q]);
+      c.dir = static_cast<uint8_t>(s_dir[q]);
     } else {
       c.pred = hevc::CU_INTRA;
       const int idx = lg == 5 ? 0 : (lg == 4 ? 1 + q : 5 + k);
@@ -171,11 +190,11 @@ __device__ __forceinline__ long long recon_ssd(const InterShared& S, const int* 
   return (static_cast<long long>(sum64(hi)) << 30) + sum64(lo);
 }
 
-// motion-compensated prediction of one n x n block of a component into S.pred
-// (8.5.3.3.3 fractional interpolation + 8.5.3.3.4.2 default weighted prediction)
+// motion-compensated prediction samples predSamplesLX (14-bit intermediate, 8.5.3.3.3
+// fractional interpolation) of one n x n block of a component into dst[y * n + x]
 template <int NT>
-__device__ __forceinline__ void mc_block(InterShared& S, const uint16_t* ref, int pw, int ph, int bx, int by, int n,
-                                         int mvx, int mvy, int bd) {
+__device__ __forceinline__ void mc_inter(InterShared& S, const uint16_t* ref, int pw, int ph, int bx, int by, int n,
+                                         int mvx, int mvy, int bd, int* dst) {
   const int lane = lane_id();
   const int fb = NT == 8 ? 2 : 3;  // fraction bits
   const int half = NT / 2 - 1;     // taps before the sample
@@ -189,8 +208,7 @@ __device__ __forceinline__ void mc_block(InterShared& S, const uint16_t* ref, in
   }
   wave_sync();
   const int sh1 = bd - 8 < 4 ? bd - 8 : 4;
-  const int wsh = 14 - bd, woff = 1 << (wsh - 1);
-  const int maxv = (1 << bd) - 1;
+  const int wsh = 14 - bd;
   auto tap = [&](int f, int k) { return NT == 8 ? kLumaTapsD[f][k] : kChromaTapsD[f][k]; };
   if (fx != 0 && fy != 0) {  // separable: horizontal pass over n + NT - 1 rows
     for (int i = lane; i < wn * n; i += 64) {
@@ -223,8 +241,34 @@ __device__ __forceinline__ void mc_block(InterShared& S, const uint16_t* ref, in
       for (int k = 0; k < NT; ++k) s += tap(fy, k) * S.tmp[(y + k) * 32 + x];
       v = s >> 6;
     }
-    v = (v + woff) >> wsh;
-    S.pred[i] = static_cast<uint16_t>(v < 0 ? 0 : (v > maxv ? maxv : v));
+    dst[i] = v;
+  }
+  wave_sync();
+}
+
+// prediction of one n x n block of a component into S.pred: default weighted sample
+// prediction (8.5.3.3.4.2) of one list, or the average of both (bi-prediction)
+template <int NT>
+__device__ __forceinline__ void mc_block(InterShared& S, const uint16_t* ref0, const uint16_t* ref1, int pw, int ph,
+                                         int bx, int by, int n, int dir, int mvx, int mvy, int mv1x, int mv1y, int bd) {
+  const int lane = lane_id();
+  const int maxv = (1 << bd) - 1;
+  if (dir == hevc::DIR_BI) {
+    mc_inter<NT>(S, ref0, pw, ph, bx, by, n, mvx, mvy, bd, S.R2);
+    mc_inter<NT>(S, ref1, pw, ph, bx, by, n, mv1x, mv1y, bd, S.R);
+    const int sh2 = 15 - bd, off2 = 1 << (sh2 - 1);
+    for (int i = lane; i < n * n; i += 64) {
+      const int v = (S.R2[i] + S.R[i] + off2) >> sh2;
+      S.pred[i] = static_cast<uint16_t>(v < 0 ? 0 : (v > maxv ? maxv : v));
+    }
+  } else {
+    const bool l1 = dir == hevc::DIR_L1;
+    mc_inter<NT>(S, l1 ? ref1 : ref0, pw, ph, bx, by, n, l1 ? mv1x : mvx, l1 ? mv1y : mvy, bd, S.R);
+    const int wsh = 14 - bd, woff = 1 << (wsh - 1);
+    for (int i = lane; i < n * n; i += 64) {
+      const int v = (S.R[i] + woff) >> wsh;
+      S.pred[i] = static_cast<uint16_t>(v < 0 ? 0 : (v > maxv ? maxv : v));
+    }
   }
   wave_sync();
 }
@@ -253,7 +297,8 @@ __global__ __launch_bounds__(64) void hevc_inter_cu(HevcInterArgs a) {
   const int n = 1 << lg;
   const int rx = ci % g.wctb, ry = ci / g.wctb;
   const int X0 = rx * 32 + (lg == 5 ? 0 : (q & 1) * 16), Y0 = ry * 32 + (lg == 5 ? 0 : (q >> 1) * 16);
-  const int mvx = cu[kq].mv[0], mvy = cu[kq].mv[1];
+  const int mvx = cu[kq].mv[0], mvy = cu[kq].mv[1], mv1x = cu[kq].mv1[0], mv1y = cu[kq].mv1[1];
+  const int dir = hevc::cu_dir(cu[kq]);
   const int bd = a.bd, maxv = (1 << bd) - 1;
   const int qpy = a.qp[cb], off = 6 * (bd - 8);
   const int qpl = qpy + off, qpc = hevc::chroma_qp_map(clampi(qpy, -off, 57)) + off;
@@ -268,11 +313,12 @@ __global__ __launch_bounds__(64) void hevc_inter_cu(HevcInterArgs a) {
     const int bx = c ? X0 / 2 : X0, by = c ? Y0 / 2 : Y0;
     const size_t ps = c ? g.csize() : g.ysize();
     const uint16_t* ref = (c == 0 ? a.ref_y : (c == 1 ? a.ref_u : a.ref_v)) + slot * ps;
+    const uint16_t* ref1 = a.ref1_y ? (c == 0 ? a.ref1_y : (c == 1 ? a.ref1_u : a.ref1_v)) + slot * ps : ref;
     const uint16_t* src = (c == 0 ? a.src_y : (c == 1 ? a.src_u : a.src_v)) + slot * ps;
     uint16_t* rec = (c == 0 ? a.rec_y : (c == 1 ? a.rec_u : a.rec_v)) + slot * ps;
     int16_t* lev = (c == 0 ? a.coef_y : (c == 1 ? a.coef_u : a.coef_v)) + slot * ps + static_cast<size_t>(by) * pw + bx;
-    if (c == 0) mc_block<8>(S, ref, pw, ph, bx, by, bs, mvx, mvy, bd);
-    else mc_block<4>(S, ref, pw, ph, bx, by, bs, mvx, mvy, bd);
+    if (c == 0) mc_block<8>(S, ref, ref1, pw, ph, bx, by, bs, dir, mvx, mvy, mv1x, mv1y, bd);
+    else mc_block<4>(S, ref, ref1, pw, ph, bx, by, bs, dir, mvx, mvy, mv1x, mv1y, bd);
     for (int i = lane; i < bs * bs; i += 64) {
       const int y = i / bs, x = i - y * bs;
       const int r = static_cast<int>(src[static_cast<size_t>(by + y) * pw + bx + x]) - S.pred[i];
@@ -350,7 +396,8 @@ extern "C" void mivc_launch_hevc_inter(int B, int W, int H, const uint16_t* sy, 
                                        uint16_t* ru, uint16_t* rv, void* ctu, void* cu, int16_t* cy, int16_t* cu_,
                                        int16_t* cv, const int* qp, const int8_t* run, const int* cand,
                                        const int16_t* mv, const int* me_cost, int bd, int tu_split, int sdh,
-                                       int intra_bias, void* stream) {
+                                       int intra_bias, void* stream, const int16_t* mvb, const uint8_t* dirb,
+                                       const uint16_t* f1y, const uint16_t* f1u, const uint16_t* f1v) {
   HevcInterArgs a;
   a.g = HevcGeom{B, W, H, W / 32, H / 32};
   a.src_y = sy;
@@ -371,6 +418,11 @@ extern "C" void mivc_launch_hevc_inter(int B, int W, int H, const uint16_t* sy, 
   a.run = run;
   a.cand = cand;
   a.mv = mv;
+  a.mvb = mvb;
+  a.dirb = dirb;
+  a.ref1_y = f1y;
+  a.ref1_u = f1u;
+  a.ref1_v = f1v;
   a.me_cost = me_cost;
   a.bd = bd;
   a.tu_split = tu_split;

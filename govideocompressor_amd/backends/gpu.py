@@ -383,7 +383,7 @@ class GpuBackend:
         t1 = time.perf_counter()
         enc = self._encoder(params, len(chunk))
         if type(params).__name__ == "HevcParams":
-            res = enc.encode(dy, du, dv, qp_delta=qp_delta)
+            res = enc.encode(dy, du, dv, qp_delta=qp_delta, anchors_at=sorted({c - 1 for _, _, _, c in chunk}))
         else:
             # a short segment (padded to F frames) must end on an anchor to be cut there
             res = enc.encode(dy, du, dv, idr_ids=[idr_id(key, un_) for key, un_, _, _ in chunk],

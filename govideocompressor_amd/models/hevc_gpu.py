@@ -88,6 +88,17 @@ class HevcParams:
     # estimate (a lower bound of the finer intra search) plus the intra bias; elsewhere inter
     # is decisive and the CTB gets no intra candidates
     intra_gate: bool = True
+    # x265 --bframes: non-reference B pictures between the P anchors (list 0 = the previous
+    # anchor, list 1 = the next; models/gop.py), coded b_qp_offset above their anchors
+    # (x265 --pbratio 1.3 = +2 QP); 0 = P pictures only.  keyint > 0, intra_only and the
+    # two-pass feedback encode keep P-only GOPs.
+    bframes: int = 3
+    b_qp_offset: int = 2
+    # x265 --tmvp (default on): temporal merge / AMVP candidates from the collocated anchor
+    tmvp: bool = True
+
+    def eff_bframes(self) -> int:
+        return 0 if (self.intra_only or self.keyint > 0) else max(0, int(self.bframes))
 
     def adaptive_qp(self) -> bool:
         return self.aq_strength > 0 or (self.cutree and self.lookahead and self.crf is not None)
@@ -96,7 +107,7 @@ class HevcParams:
         return dict(width=self.width, height=self.height, bit_depth=self.bit_depth, fps=self.fps,
                     sao=int(self.sao), deblock=int(self.deblock), max_merge=self.max_merge, wpp=int(self.wpp),
                     cu_qp_delta=int(self.adaptive_qp()), tu_inter_depth=int(self.tu_inter_depth), sdh=int(self.sdh),
-                    level_idc=int(self.level_idc))
+                    level_idc=int(self.level_idc), bframes=self.eff_bframes(), tmvp=int(self.tmvp and not self.intra_only))
 
     def frame_qps(self) -> tuple[int, int]:
         qp_p = int(round(self.crf)) if self.crf is not None else int(self.qp)
@@ -108,13 +119,19 @@ class HevcParams:
 class HevcSegmentResult:
     bitstream: bytes
     frames: int
-    nals: list[bytes] = field(default_factory=list)
+    nals: list[bytes] = field(default_factory=list)   # coding order
     bits: list[int] = field(default_factory=list)
     psnr_y: float = 0.0
+    order: list[int] = field(default_factory=list)    # display index of each NAL
 
     def display_prefix(self, c: int) -> list[bytes]:
-        """Slice NALs of pictures 0..c-1 (P-only GOPs: coding order == display order)."""
-        return self.nals[:c]
+        """Slice NALs of display pictures 0..c-1 (a coding-order prefix when c - 1 is an
+        anchor: encode(anchors_at=...))."""
+        order = self.order or list(range(len(self.nals)))
+        out = [n for n, d in zip(self.nals, order) if d < c]
+        if any(d >= c for d in order[:len(out)]):
+            raise ValueError(f"pictures 0..{c - 1} are not a coding-order prefix (encode with anchors_at)")
+        return out
 
 
 class GpuHevcEncoder:
@@ -145,21 +162,43 @@ class GpuHevcEncoder:
                     torch.zeros((B, H // 2, W // 2), dtype=dt, device=dev))
 
         self.src = planes()
-        self.rec = [planes(), planes()]      # current / reference
+        self.nb = params.eff_bframes()
+        # anchors (I / P) alternate between rec[0] and rec[1] (anchor ordinal & 1); B pictures
+        # (never referenced) reconstruct into rec[2]
+        self.rec = [planes(), planes()] + ([planes()] if self.nb else [])
         self.dbk = planes()                  # SAO output ping-pong buffer
         self.coefs = [planes(i16), planes(i16)]  # double-buffered: copy-out of t overlaps t + 1
         self.coef = self.coefs[0]
         self.wmb, self.hmb = W // 16, H // 16
         nmb = self.wmb * self.hmb
+        self.nmb = nmb
         self.src8 = torch.zeros((B, H, W), dtype=torch.uint8, device=dev)   # motion-search proxies
-        self.ref8 = torch.zeros((B, H, W), dtype=torch.uint8, device=dev)
+        # 8-bit proxies of the two latest anchors and their half-sample planes, built once per
+        # anchor and shared by every picture that references it
+        self.ref8s = [torch.zeros((B, H, W), dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.me_hps = [torch.empty(B * 3 * (H + 8) * (W + 8) + 64, dtype=torch.uint8, device=dev) for _ in range(2)]
         self.mv = torch.zeros((B, nmb, 2), dtype=torch.int16, device=dev)
         self.prev_mv = torch.zeros((B, nmb, 2), dtype=torch.int16, device=dev)
         self.mv_tmp = torch.zeros((B, nmb, 2), dtype=torch.int16, device=dev)
         self.me_cost = torch.zeros((B, nmb), dtype=torch.int32, device=dev)
         self.me_intra = torch.zeros((B, nmb), dtype=torch.int32, device=dev)
         self.me_pred = torch.zeros((B, nmb, 256), dtype=torch.uint8, device=dev)
-        self.me_hp = torch.empty(B * 3 * (H + 8) * (W + 8) + 64, dtype=torch.uint8, device=dev)
+        if self.nb:
+            i16_, i32_, u8_ = torch.int16, torch.int32, torch.uint8
+            self.mv1 = torch.zeros((B, nmb, 2), dtype=i16_, device=dev)
+            self.me_cost1 = torch.zeros((B, nmb), dtype=i32_, device=dev)
+            self.pm0 = torch.zeros((B, nmb, 2), dtype=i16_, device=dev)
+            self.pm1 = torch.zeros((B, nmb, 2), dtype=i16_, device=dev)
+            self.tmv = torch.zeros((B, nmb, 4), dtype=i16_, device=dev)
+            self.tdir = torch.zeros((B, nmb), dtype=u8_, device=dev)
+            self.mvb = [torch.zeros((B, nmb, 4), dtype=i16_, device=dev) for _ in range(2)]
+            self.dirb = [torch.zeros((B, nmb), dtype=u8_, device=dev) for _ in range(2)]
+            self.bcost = torch.zeros((B, nmb), dtype=i32_, device=dev)
+            self.bbits = torch.zeros((B, nmb), dtype=i32_, device=dev)
+            # motion of the latest anchor per 16x16 block (its records at each block's top-left
+            # granule: what TMVP reads after 16x16 motion compression)
+            self.col_inter = torch.zeros((B, self.hmb, self.wmb), dtype=torch.bool, device=dev)
+            self.col_mv = torch.zeros((B, self.hmb, self.wmb, 2), dtype=i32_, device=dev)
         self.cand = torch.zeros((B, self.nctb, 58), dtype=torch.int32, device=dev)  # kCandStride
         self.ctus = [torch.zeros((B, self.nctb, 32), dtype=torch.uint8, device=dev) for _ in range(2)]
         self.cus = [torch.zeros((B, self.nctb * 16, 16), dtype=torch.uint8, device=dev) for _ in range(2)]
@@ -272,16 +311,79 @@ class GpuHevcEncoder:
         self.timings["lookahead_s"] = self.timings.get("lookahead_s", 0.0) + time.perf_counter() - t0
         return q
 
+    # ------------------------------------------------------------------ B-picture helpers
+    @staticmethod
+    def _dsf(td: int, tb: int) -> int:
+        """DistScaleFactor of 8.5.3.2.8 (C division, clipped distances)."""
+        td = max(-128, min(127, td))
+        tb = max(-128, min(127, tb))
+        q = (16384 + (abs(td) >> 1)) // abs(td)
+        tx = q if td > 0 else -q
+        return max(-4096, min(4095, (tb * tx + 32) >> 6))
+
+    @staticmethod
+    def _scale(mv: torch.Tensor, td: int, tb: int) -> torch.Tensor:
+        if td == tb or td == 0:
+            return mv
+        p = mv * GpuHevcEncoder._dsf(td, tb)
+        return (torch.sign(p) * ((p.abs() + 127) >> 8)).clamp_(-32768, 32767)
+
+    def _store_col(self):
+        """The anchor just coded becomes the collocated picture of the next B pictures: its
+        records at each 16x16 block's top-left granule (z-order granules 0 / 4 / 8 / 12)."""
+        B, hc, wc = self.B, self.hctb, self.wctb
+        rec = self.cu.view(B, hc, wc, 4, 4, 16)[:, :, :, :, 0, :].reshape(B, hc, wc, 2, 2, 16)
+        rec = rec.permute(0, 1, 3, 2, 4, 5).reshape(B, self.hmb, self.wmb, 16)
+        self.col_inter.copy_(rec[..., 0] == 1)
+        self.col_mv.copy_(rec[..., 4:8].contiguous().view(torch.int16).to(torch.int32))
+
+    def _temporal_candidates(self, pic):
+        """TMVP merge candidate per 16x16 block (the writer's exact derivation for a 16x16 CU:
+        the collocated bottom-right block inside the CTB row, else the centre one) scaled to
+        both lists, and the two searches' predictors."""
+        ci, cm = self.col_inter, self.col_mv
+        br_i = torch.zeros_like(ci)
+        br_m = torch.zeros_like(cm)
+        br_i[:, :-1, :-1] = ci[:, 1:, 1:]
+        br_m[:, :-1, :-1] = cm[:, 1:, 1:]
+        even = (torch.arange(self.hmb, device=self.dev) % 2 == 0)[None, :, None]
+        use_br = br_i & even
+        sel = torch.where(use_br[..., None], br_m, cm)
+        avail = (use_br | ci).reshape(self.B, self.nmb)
+        td = pic.l1 - pic.l0  # the col anchor (list 1) predicts from list 0's picture
+        t0 = self._scale(sel, td, pic.d - pic.l0).reshape(self.B, self.nmb, 2)
+        t1 = self._scale(sel, td, pic.d - pic.l1).reshape(self.B, self.nmb, 2)
+        av = avail[..., None].to(torch.int32)
+        self.tmv[..., 0:2].copy_(t0 * av)
+        self.tmv[..., 2:4].copy_(t1 * av)
+        self.tdir.copy_(avail.to(torch.uint8) * 3)
+        self.pm0.copy_(self.tmv[..., 0:2])
+        self.pm1.copy_(self.tmv[..., 2:4])
+
+    def _plan(self, F: int, cuts_h: np.ndarray, anchors_at) -> list:
+        from .gop import PicPlan, gop_plan
+        if self.nb:
+            return gop_plan(F, self.nb, set(anchors_at) | {d for d in range(1, F) if cuts_h[:, d].any()})
+        out = []
+        for t in range(F):
+            idr = t == 0 or self.p.intra_only or (self.p.keyint > 0 and t % self.p.keyint == 0)
+            out.append(PicPlan(t, "I" if idr else "P", t, t, t, l0=-1 if idr else t - 1))
+        return out
+
     # ------------------------------------------------------------------ encode
     def encode(self, y: torch.Tensor, u: torch.Tensor, v: torch.Tensor, qps: np.ndarray | None = None,
-               keep_recon: bool = False, metrics: bool = True, qp_delta=None, rate_fb=None) -> list[HevcSegmentResult]:
+               keep_recon: bool = False, metrics: bool = True, qp_delta=None, rate_fb=None,
+               anchors_at=()) -> list[HevcSegmentResult]:
         """y: [B, F, h, w] (uint8, or uint16 holding bit_depth-bit samples), u/v half size.
-        Every segment starts with an IDR picture; the others are P pictures
-        (intra_only: IDR pictures only).
+        Every segment starts with an IDR picture; then P anchors and (bframes) the B pictures
+        between them, in coding order (models/gop.py; a scene cut becomes an anchor coded all
+        intra).  ``qps``: [B, F] display order.  ``anchors_at``: display indices that must be
+        anchors, so a segment shorter than F ends on a coding-order prefix (display_prefix).
 
         ``rate_fb`` (:class:`~govideocompressor_amd.rc.ratecontrol.TwoPassFeedback`): pass-2
         rate feedback -- before every frame step the controller sees the bits of the pictures
-        whose CABAC has finished and may re-solve the QPs of the frames not yet started."""
+        whose CABAC has finished and may re-solve the QPs of the frames not yet started (its
+        arrays are in coding order, ``self.last_order``)."""
         B, F, h, w = y.shape
         if B != self.B or (w, h) != (self.p.width, self.p.height):
             raise ValueError(f"expected [{self.B}, F, {self.p.height}, {self.p.width}], got {list(y.shape)}")
@@ -290,28 +392,40 @@ class GpuHevcEncoder:
         qi, qpp = self.p.frame_qps()
         self._scenecuts = None
         self._cutree = None
+        from_la = False
         if qps is None and self.p.crf is not None and self.p.lookahead and not self.p.intra_only:
             qps = self.crf_qps(y)
+            from_la = True
         cuts_h = self._scenecuts if self._scenecuts is not None else np.zeros((B, F), dtype=bool)
-        cuts_d = torch.from_numpy(np.ascontiguousarray(cuts_h.T)).to(self.dev)  # [F, B]
+        plan = self._plan(F, cuts_h, anchors_at)
+        order = [pic.d for pic in plan]
+        self.last_order = order
         if qps is None:
-            qps = np.array([[qi if t == 0 else qpp for t in range(F)] for _ in range(B)], dtype=np.int32)
+            qps = np.array([[qi if pic.kind == "I" else qpp for pic in sorted(plan, key=lambda q: q.d)]
+                            for _ in range(B)], dtype=np.int32)
+            from_la = True
         cfg = self.p.host_cfg()
         if self.p.wpp:  # spread the native threads over the B pictures of a step
             cfg["threads"] = max(1, min(32, self.entropy_threads // max(1, B)))
         qps = np.clip(np.asarray(qps, dtype=np.int32).reshape(B, F), 0, 51)
+        if self.nb and from_la:
+            bd_ = [pic.d for pic in plan if pic.kind == "B"]
+            qps[:, bd_] = np.minimum(qps[:, bd_] + int(self.p.b_qp_offset), 51)
         if qp_delta is not None:
             from ..rc.abr import apply_delta
             qps = apply_delta(qps, qp_delta)
+        qps_c = np.ascontiguousarray(qps[:, order])  # coding order
         if rate_fb is not None:
-            qps = np.array(rate_fb.qps, dtype=np.int32).reshape(B, F)
-        qps_d = torch.from_numpy(np.ascontiguousarray(qps.T)).to(self.dev)  # [F, B], one upload
+            qps_c = np.array(rate_fb.qps, dtype=np.int32).reshape(B, F)
+        qps_d = torch.from_numpy(np.ascontiguousarray(qps_c.T)).to(self.dev)  # [F, B] coding order, one upload
+        cuts_c = cuts_h[:, order]
+        cuts_d = torch.from_numpy(np.ascontiguousarray(cuts_c.T)).to(self.dev)  # [F, B]
         fb_known, fb_spent, fb_stage = 0, np.zeros((B, F)), []
         nals: list[list] = [[None] * F for _ in range(B)]
         futs = []
         pending: list[list] = [[], [], []]
         sse = []
-        recon = [] if keep_recon else None
+        recon = [None] * F if keep_recon else None
         t_gpu = t_host = t_blocked = 0.0
         cabac_s = [0.0]
         p = self._p
@@ -319,7 +433,14 @@ class GpuHevcEncoder:
         bd = self.p.bit_depth
         st = self.stage_timer
         gate_sum: list[torch.Tensor] = []
+        tmvp = bool(cfg.get("tmvp", 0))
+        anchor_cu: dict = {}   # display index of an anchor -> (host copy of its CU records or None, its list-0 index)
+        idr_d = 0              # display index of the latest IDR picture (POC 0)
         for t in range(F):
+            pic = plan[t]
+            d = pic.d
+            if pic.kind == "I":
+                idr_d = d
             t0 = time.perf_counter()
             if rate_fb is not None and t > 0:
                 # bits of the pictures whose CABAC jobs have finished (coding order prefix)
@@ -328,24 +449,29 @@ class GpuHevcEncoder:
                         fb_spent[b, fb_known] = 8 * len(nal)
                     fb_known += 1
                 newq = np.asarray(rate_fb.update(fb_known, fb_spent, t), dtype=np.int32)
-                if not np.array_equal(newq[:, t:], qps[:, t:]):
-                    qps[:, t:] = newq[:, t:]
-                    staged = torch.from_numpy(np.ascontiguousarray(qps[:, t:].T)).pin_memory()
+                if not np.array_equal(newq[:, t:], qps_c[:, t:]):
+                    qps_c[:, t:] = newq[:, t:]
+                    staged = torch.from_numpy(np.ascontiguousarray(qps_c[:, t:].T)).pin_memory()
                     qps_d[t:].copy_(staged, non_blocking=True)  # stream-ordered before frame t's read
                     fb_stage.append(staged)  # keep the pinned source alive until the encode ends
-            idr = t == 0 or self.p.intra_only or (self.p.keyint > 0 and t % self.p.keyint == 0)
-            self._prep(y, u, v, t, proxy=not idr)
+            idr = pic.kind == "I"
+            self._prep(y, u, v, d, proxy=not idr)
             self.qp.copy_(qps_d[t])  # device-to-device: no host sync inside the frame loop
-            # per-CTB QPs (AQ + cutree offsets of frame t); without them every CTB at the frame QP
+            # per-CTB QPs (AQ + cutree offsets of frame d); without them every CTB at the frame QP.
+            # cutree offsets belong to referenced pictures: B pictures get variance AQ only
             extra, estride, erows = 0, 0, 0
-            if self._cutree is not None and self.p.adaptive_qp():
+            if self._cutree is not None and self.p.adaptive_qp() and pic.kind != "B":
                 ct = self._cutree
-                extra, estride, erows = ct.data_ptr() + t * ct.shape[2] * 4, ct.shape[1] * ct.shape[2], self._cutree_rows
+                extra, estride, erows = ct.data_ptr() + d * ct.shape[2] * 4, ct.shape[1] * ct.shape[2], self._cutree_rows
             with st("aq"):
                 self.hip.hevc_aq(B, self.W, self.H, bd, p(self.src[0]), p(self.src[1]), p(self.src[2]), p(self.qp),
                                  float(self.p.aq_strength) if self.p.adaptive_qp() else 0.0, extra, estride, erows,
                                  p(self.ctb_qp), p(self.mb_aq), s)
-            cur, ref = self.rec[t % 2], self.rec[(t + 1) % 2]
+            if pic.kind == "B":
+                ci, r0, r1 = 2, (pic.l1_anchor - 1) & 1, pic.l1_anchor & 1
+            else:
+                ci, r0, r1 = pic.anchor & 1, (pic.anchor - 1) & 1, -1
+            cur, ref = self.rec[ci], self.rec[r0]
             kb = t % 2
             # the copy-out of step t - 2 must have read these buffers before they are rewritten
             torch.cuda.current_stream(self.dev).wait_event(self.copy_done[kb])
@@ -360,20 +486,48 @@ class GpuHevcEncoder:
                     self.hip.hevc_intra(*intra_args, 1, 1, p(self.err), s, int(self.p.sdh))
             else:
                 self.run.fill_(2)
-                with st("me"):
-                    self.hip.hevc_proxy8(p(ref[0]), p(self.ref8), ref[0].numel(), bd - 8, s)
-                    self.hip.me(B, self.wmb, self.hmb, p(self.src8), p(self.ref8), p(self.prev_mv), p(self.mv),
-                                p(self.me_cost), p(self.me_pred), p(self.me_intra), p(self.qp), self.p.me_range,
-                                self.p.subpel, s, p(self.me_hp), p(self.mb_aq))
-                with st("merge_refine"):
-                    for it in range(int(self.p.merge_refine)):
-                        a_, b_ = (self.mv, self.mv_tmp) if it % 2 == 0 else (self.mv_tmp, self.mv)
-                        self.hip.hevc_merge_refine(B, self.wmb, self.hmb, p(self.src8), p(self.ref8), p(self.me_hp),
-                                                   p(a_), p(b_), p(self.me_cost), p(self.prev_mv), p(self.qp),
-                                                   p(self.mb_aq), s)
-                    if int(self.p.merge_refine) % 2:
-                        self.mv.copy_(self.mv_tmp)
-                if cuts_h[:, t].any():  # scene cut: every CU of these slots goes intra
+                ref8, hp = self.ref8s[r0], self.me_hps[r0]
+                inter_kw = {}
+                if pic.kind == "P":
+                    with st("me"):
+                        self.hip.me(B, self.wmb, self.hmb, p(self.src8), p(ref8), p(self.prev_mv), p(self.mv),
+                                    p(self.me_cost), p(self.me_pred), p(self.me_intra), p(self.qp), self.p.me_range,
+                                    self.p.subpel, s, p(hp), p(self.mb_aq), 1)
+                    with st("merge_refine"):
+                        for it in range(int(self.p.merge_refine)):
+                            a_, b_ = (self.mv, self.mv_tmp) if it % 2 == 0 else (self.mv_tmp, self.mv)
+                            self.hip.hevc_merge_refine(B, self.wmb, self.hmb, p(self.src8), p(ref8), p(hp), p(a_), p(b_),
+                                                       p(self.me_cost), p(self.prev_mv), p(self.qp), p(self.mb_aq), s)
+                        if int(self.p.merge_refine) % 2:
+                            self.mv.copy_(self.mv_tmp)
+                else:
+                    ref8b, hpb = self.ref8s[r1], self.me_hps[r1]
+                    with st("me_b"):
+                        self._temporal_candidates(pic)
+                        self.hip.me(B, self.wmb, self.hmb, p(self.src8), p(ref8), p(self.pm0), p(self.mv),
+                                    p(self.me_cost), p(self.me_pred), p(self.me_intra), p(self.qp), self.p.me_range,
+                                    self.p.subpel, s, p(hp), p(self.mb_aq), 1)
+                        # the list-1 search skips the open-loop intra estimate the list-0 search wrote
+                        self.hip.me(B, self.wmb, self.hmb, p(self.src8), p(ref8b), p(self.pm1), p(self.mv1),
+                                    p(self.me_cost1), p(self.me_pred), 0, p(self.qp), self.p.me_range, self.p.subpel,
+                                    s, p(hpb), p(self.mb_aq), 1)
+                    with st("b_decide"):
+                        bargs = (B, self.wmb, self.hmb, p(self.src8), p(ref8), p(ref8b), p(hp), p(hpb))
+                        self.hip.hevc_b(0, *bargs, p(self.mv), p(self.mv1), p(self.me_cost), p(self.me_cost1),
+                                        p(self.pm0), p(self.pm1), 0, 0, 0, 0, p(self.mvb[0]), p(self.dirb[0]),
+                                        p(self.bcost), p(self.bbits), p(self.qp), p(self.mb_aq), s)
+                        tm_, td_ = (p(self.tmv), p(self.tdir)) if tmvp else (0, 0)
+                        for it in range(int(self.p.merge_refine)):
+                            i_, o_ = it % 2, (it + 1) % 2
+                            self.hip.hevc_b(1, *bargs, 0, 0, 0, 0, 0, 0, tm_, td_, p(self.mvb[i_]), p(self.dirb[i_]),
+                                            p(self.mvb[o_]), p(self.dirb[o_]), p(self.bcost), p(self.bbits), p(self.qp),
+                                            p(self.mb_aq), s)
+                        fin = int(self.p.merge_refine) % 2
+                        self.me_cost.copy_(self.bcost)
+                    r1p = self.rec[r1]
+                    inter_kw = dict(mvb=p(self.mvb[fin]), dirb=p(self.dirb[fin]), f1y=p(r1p[0]), f1u=p(r1p[1]),
+                                    f1v=p(r1p[2]))
+                if cuts_c[:, t].any():  # scene cut: every CU of these slots goes intra
                     self.me_cost.masked_fill_(cuts_d[t][:, None], 1 << 26)
                 with st("intra_analyze"):  # open-loop intra candidates where intra may still win
                     mask = p(self._intra_gate()) if self.p.intra_gate else 0
@@ -385,10 +539,11 @@ class GpuHevcEncoder:
                                         p(ref[1]), p(ref[2]), p(cur[0]), p(cur[1]), p(cur[2]), p(self.ctu), p(self.cu),
                                         p(self.coef[0]), p(self.coef[1]), p(self.coef[2]), p(self.ctb_qp), p(self.run),
                                         p(self.cand), p(self.mv), p(self.me_cost), bd, s, int(self.p.tu_inter_depth),
-                                        int(self.p.sdh), int(self.p.intra_bias_p))
+                                        int(self.p.sdh), int(self.p.intra_bias_p), **inter_kw)
                 with st("intra_recon"):
                     self.hip.hevc_intra(*intra_args, 0, 1, p(self.err), s, int(self.p.sdh))   # intra CUs, wavefront
-                self.prev_mv.copy_(self.mv)
+                if pic.kind == "P":
+                    self.prev_mv.copy_(self.mv)
             self.hip.hevc_qp_fixup(B, self.W, self.H, p(self.ctu), p(self.cu), p(self.qp), p(self.run), int(self.p.wpp), s)
             if self.p.deblock:
                 with st("deblock"):
@@ -403,12 +558,24 @@ class GpuHevcEncoder:
                                       p(out_pl[1]), p(out_pl[2]), p(self.src[0]), p(self.src[1]), p(self.src[2]),
                                       p(self.ctu), p(self.ctb_qp), p(self.run), 1, s)
                 self.dbk = cur
-                self.rec[t % 2] = cur = out_pl
+                self.rec[ci] = cur = out_pl
+            if pic.kind != "B":
+                # the anchor's 8-bit proxy and half-sample planes (shared by every picture that
+                # references it) and, for the B pictures after it, its motion as the col field
+                a8 = pic.anchor & 1
+                with st("halfpel"):
+                    self.hip.hevc_proxy8(p(cur[0]), p(self.ref8s[a8]), cur[0].numel(), bd - 8, s)
+                    self.hip.me_halfpel(B, self.W, self.H, p(self.ref8s[a8]), p(self.me_hps[a8]), s)
+                if self.nb:
+                    if idr:
+                        self.col_inter.zero_()
+                    else:
+                        self._store_col()
             if metrics:
-                d = (cur[0][:, :h, :w].to(torch.int32) - self.src[0][:, :h, :w].to(torch.int32))
-                sse.append((d * d).sum(dim=(1, 2)).to(torch.float64))
+                dd = (cur[0][:, :h, :w].to(torch.int32) - self.src[0][:, :h, :w].to(torch.int32))
+                sse.append((dd * dd).sum(dim=(1, 2)).to(torch.float64))
             if keep_recon:
-                recon.append(tuple(c.clone() for c in cur))
+                recon[d] = tuple(c.clone() for c in cur)
             # records to pinned host memory on the copy stream; CABAC on the thread pool
             hb = t % 3
             if pending[hb]:  # the CABAC jobs of step t - 3 still read this host buffer set
@@ -437,19 +604,43 @@ class GpuHevcEncoder:
             nz, off, lv = host[2].numpy().view(np.uint64), host[3].numpy().view(np.uint32), host[4].numpy()
             t1 = time.perf_counter()
             t_gpu += t1 - t0
+            qcol = qps_c[:, t].copy()
 
-            fps = [dict(idr=int(idr), poc=t, qp=int(qps[b, t]), slice_type=2 if idr else 1) for b in range(B)]
-
-            def job(done=done, fps=fps, ctu=ctu, cu=cu, nz=nz, off=off, lv=lv):
+            def job(done=done, pic=pic, qcol=qcol, ctu=ctu, cu=cu, nz=nz, off=off, lv=lv, i0=idr_d):
                 done.synchronize()
                 tj = time.perf_counter()
+                # POC counts display pictures from the latest IDR
+                base = dict(idr=int(pic.kind == "I"), poc=pic.d - i0, slice_type={"I": 2, "P": 1, "B": 0}[pic.kind],
+                            nal_ref=int(pic.kind != "B"))
+                if pic.kind != "I":
+                    base["ref_poc0"] = pic.l0 - i0
+                if pic.kind == "B":
+                    base["ref_poc1"] = pic.l1 - i0
+                col = None
+                if tmvp and pic.kind != "I":
+                    cd = pic.l1 if pic.kind == "B" else pic.l0
+                    col = anchor_cu[cd]
+                    base.update(col_poc=cd - i0, col_ref_poc0=col[1] - i0, col_ref_poc1=col[1] - i0)
+                fps = []
+                for b in range(B):
+                    fp = dict(base, qp=int(qcol[b]))
+                    if col is not None:
+                        fp["col_cu"] = None if col[0] is None else col[0][b]
+                    fps.append(fp)
                 r = self.host.hevc_write_slices_packed(cfg, fps, ctu, cu, nz, off, lv, self.entropy_threads)
+                if tmvp and pic.kind != "B":
+                    # the next pictures' collocated records (the host buffer set is reused at t + 3)
+                    anchor_cu[pic.d] = (None if pic.kind == "I" else cu[:B].copy(), pic.l0)
+                    for k in [k for k in anchor_cu if k < pic.l0]:
+                        del anchor_cu[k]
                 cabac_s[0] += time.perf_counter() - tj
                 return r
 
             f = self.pool.submit(job)
             futs.append((t, f))
             pending[hb].append(f)
+        qps = np.empty_like(qps_c)
+        qps[:, order] = qps_c
         self.last_qps = qps.copy()
         if int(self.err.item()) != 0:
             raise RuntimeError("HEVC encoder: wavefront progress timeout")
@@ -480,7 +671,7 @@ class GpuHevcEncoder:
                 mse = float(sum(x[b].item() for x in sse)) / (F * w * h)
                 ps = 99.0 if mse == 0 else 10.0 * np.log10(maxv * maxv / mse)
             out.append(HevcSegmentResult(bitstream=self.params_nal + b"".join(nals[b]), frames=F, nals=nals[b],
-                                         bits=bits[b], psnr_y=ps))
+                                         bits=bits[b], psnr_y=ps, order=list(order)))
         if keep_recon:
             self.last_recon = recon
         return out

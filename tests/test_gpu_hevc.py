@@ -67,11 +67,53 @@ def test_gpu_hevc_intra_main10_cropped(host):
 
 @pytest.mark.parametrize("bd", [8, 10])
 def test_gpu_hevc_p_pictures_match_decoder(host, bd):
-    res, rec = _encode(128, 96, 5, 3, bd=bd, crf=None, qp=30)
+    res, rec = _encode(128, 96, 5, 3, bd=bd, crf=None, qp=30, bframes=0)
     _compare(host, res, rec)
     for r in res:
         assert all(b > 0 for b in r.bits)
         assert sum(r.bits[1:]) / (r.frames - 1) < r.bits[0]   # P pictures are cheaper than the IDR
+
+
+@pytest.mark.parametrize("bd,tmvp", [(8, True), (10, True), (8, False)])
+def test_gpu_hevc_b_pictures_match_decoder(host, bd, tmvp):
+    """x265-style GOP: I, P anchors every 4 pictures and non-reference B pictures between
+    them (list 0 / list 1 / bi-predicted CUs, bi-prediction averaging at 14-bit precision,
+    B-aware deblocking strengths, TMVP candidates from the collocated anchor).  The GPU
+    reconstruction equals the CPU decoder's, every inter direction occurs, and the B
+    pictures cost less than the P anchors."""
+    res, rec = _encode(192, 128, 9, 2, bd=bd, crf=None, qp=28, bframes=3, tmvp=tmvp)
+    _compare(host, res, rec)
+    dirs = set()
+    for r in res:
+        assert r.order == [0, 4, 1, 2, 3, 8, 5, 6, 7]
+        pics = host.hevc_decode(r.bitstream)
+        for p in pics:
+            inter = p["cu"][:, 0] == 1
+            dirs |= set(p["cu"][inter, 12].tolist())
+        assert [p["slice_type"] for p in pics] == [2, 0, 0, 0, 1, 0, 0, 0, 1]
+        bits = dict(zip(r.order, r.bits))
+        pb = np.mean([bits[d] for d in (4, 8)])
+        bb = np.mean([bits[d] for d in (1, 2, 3, 5, 6, 7)])
+        assert bb < 0.8 * pb
+    assert {1, 2, 3} <= dirs
+
+
+def test_gpu_hevc_b_segment_prefix(host):
+    """A segment shorter than the batch ends on an anchor (anchors_at), so its pictures
+    form a coding-order prefix that decodes on its own."""
+    from govideocompressor_amd.models.h264_gpu import synth_clip
+    from govideocompressor_amd.models.hevc_gpu import GpuHevcEncoder, HevcParams
+    y, u, v = synth_clip(2, 9, 128, 96, seed=3)
+    enc = GpuHevcEncoder(HevcParams(width=128, height=96, crf=None, qp=30), slots=2)
+    res = enc.encode(y, u, v, keep_recon=True, anchors_at=[5])
+    rec = enc.last_recon
+    enc.close()
+    _compare(host, res, rec)
+    nals = res[0].display_prefix(6)
+    pics = host.hevc_decode(enc.parameter_sets() + b"".join(nals))
+    assert [p["poc"] for p in pics] == list(range(6))
+    for t, p in enumerate(pics):
+        assert np.array_equal(p["y"], rec[t][0][0].cpu().numpy().astype(np.uint16))
 
 
 def test_gpu_backend_hevc_preset(host, tmp_path):
@@ -129,7 +171,9 @@ def test_gpu_hevc_scenecut(host):
     enc.close()
     _compare(host, res, rec)
     for r in res:
-        assert r.bits[cut] > 1.3 * r.bits[cut + 1]   # the all-intra cut picture costs more than a P picture
+        bits = dict(zip(r.order, r.bits))
+        assert cut in r.order[:2]                      # the cut picture became an anchor
+        assert bits[cut] > 1.3 * bits[cut + 1]        # the all-intra cut picture costs more than a B picture
 
 
 @pytest.mark.parametrize("wpp", [True, False])
@@ -145,13 +189,13 @@ def test_gpu_hevc_adaptive_qp(host, wpp):
     assert enc.p.host_cfg()["cu_qp_delta"] == 1
     res = enc.encode(y, u, v, keep_recon=True)
     rec = enc.last_recon
-    ctu_last = enc.ctu.cpu().numpy()  # records of the last picture
+    ctu_last = enc.ctu.cpu().numpy()  # records of the last picture in coding order
     enc.close()
     _compare(host, res, rec)
     qps = set()
     for b, r in enumerate(res):
         pics = host.hevc_decode(r.bitstream)
-        q = pics[-1]["ctu"][:, 1].view(np.int8)
+        q = pics[r.order[-1]]["ctu"][:, 1].view(np.int8)
         assert np.array_equal(q, ctu_last[b][:, 1].view(np.int8))
         for p in pics:
             qps |= set(p["ctu"][:, 1].view(np.int8).tolist())
