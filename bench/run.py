@@ -211,8 +211,9 @@ def _hevc_run(args, W, H, B, F, bd, crf, two_pass_kbps=None, fps=30.0, resident=
         y, u, v = clip(k)
         if two_pass_kbps is None:
             return enc.encode(y, u, v, metrics=quality), None
-        q1 = enc.crf_qps(y)                                           # GPU lookahead -> CRF QPs
-        r1 = enc.encode(y, u, v, qps=q1, metrics=False)               # pass 1 at the CRF QPs
+        r1 = enc.encode(y, u, v, metrics=False)                       # pass 1: CRF QPs from the GPU lookahead
+        # pass-1 bits are per NAL (coding order): pair them with the QPs in coding order too
+        q1 = np.ascontiguousarray(enc.last_qps[:, enc.last_order])
         n = B * F
         gs = GlobalStats(n * env.world, env)
         st = np.zeros((n, 4))

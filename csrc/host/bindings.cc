@@ -281,6 +281,7 @@ hevc::HevcConfig hevc_cfg_from(const py::dict& d) {
   c.level_idc = dget<int>(d, "level_idc", 0);
   c.bframes = dget<int>(d, "bframes", 0);
   c.tmvp = dget<int>(d, "tmvp", 0);
+  c.pyramid = dget<int>(d, "pyramid", 0);
   if (c.tu_inter_depth < 0 || c.tu_inter_depth > 1) throw std::runtime_error("HEVC: tu_inter_depth in 0..1");
   if (c.threads < 1 || c.threads > 256) throw std::runtime_error("HEVC: threads in 1..256");
   if (c.width <= 0 || c.height <= 0 || (c.width & 1) || (c.height & 1)) throw std::runtime_error("HEVC: bad size");
@@ -467,6 +468,16 @@ hevc::HevcFrameParams hevc_frame_from(const py::dict& fp, std::vector<py::array>
   f.nal_ref = dget<int>(fp, "nal_ref", 1);
   f.ref_poc[0] = dget<int>(fp, "ref_poc0", -1);
   f.ref_poc[1] = dget<int>(fp, "ref_poc1", -1);
+  if (fp.contains("rps")) {  // [(poc, used), ...]
+    const py::list l = fp["rps"].cast<py::list>();
+    if (l.size() > 8) throw std::runtime_error("rps: at most 8 entries");
+    f.n_rps = static_cast<int>(l.size());
+    for (size_t i = 0; i < l.size(); ++i) {
+      const py::tuple e = l[i].cast<py::tuple>();
+      f.rps_poc[i] = e[0].cast<int>();
+      f.rps_used[i] = static_cast<uint8_t>(e[1].cast<int>() ? 1 : 0);
+    }
+  }
   if (fp.contains("col_poc")) {
     f.col.set = 1;
     f.col.poc = dget<int>(fp, "col_poc", 0);
@@ -744,7 +755,7 @@ PYBIND11_MODULE(_host, m) {
       [](const py::dict& cfg, const py::list& frames, py::array_t<uint8_t, py::array::c_style> ctu,
          py::array_t<uint8_t, py::array::c_style> cu, py::array_t<uint64_t, py::array::c_style> nzmap,
          py::array_t<uint32_t, py::array::c_style> ctb_off, py::array_t<int16_t, py::array::c_style> levels,
-         int threads) {
+         int threads, bool with_stats) {
         // One picture per slot of a batch step ([B, ...] arrays, frames[b] = frame params),
         // coded by `threads` native threads with the GIL released for the whole batch (a
         // Python thread per picture would queue on the GIL after every slice).
@@ -763,6 +774,7 @@ PYBIND11_MODULE(_host, m) {
                                    static_cast<size_t>(nctu) * hevc::kCusPerCtb * hevc::kCuInfoBytes);
         const size_t per_lv = static_cast<size_t>(levels.shape(1));
         std::vector<std::vector<uint8_t>> nals(B);
+        std::vector<hevc::HevcSliceStats> sts(B);
         std::vector<std::string> errs(B);
         {
           py::gil_scoped_release rel;
@@ -778,7 +790,7 @@ PYBIND11_MODULE(_host, m) {
                 nals[b] = hevc::hevc_write_slice(
                     c, fps[b], reinterpret_cast<const hevc::CtuInfo*>(ctu.data() + static_cast<size_t>(b) * nctu * 32),
                     reinterpret_cast<const hevc::CuInfo*>(cu.data() + static_cast<size_t>(b) * nctu * hevc::kCusPerCtb * hevc::kCuInfoBytes),
-                    nullptr, nullptr, nullptr, nullptr, &pk);
+                    nullptr, nullptr, nullptr, with_stats ? &sts[b] : nullptr, &pk);
               } catch (const std::exception& e) {
                 errs[b] = e.what();
               }
@@ -793,11 +805,23 @@ PYBIND11_MODULE(_host, m) {
         for (py::ssize_t b = 0; b < B; ++b)
           if (!errs[b].empty()) throw std::runtime_error("HEVC slice " + std::to_string(b) + ": " + errs[b]);
         py::list out;
-        for (py::ssize_t b = 0; b < B; ++b) out.append(to_bytes(nals[b]));
+        for (py::ssize_t b = 0; b < B; ++b) {
+          if (!with_stats) {
+            out.append(to_bytes(nals[b]));
+            continue;
+          }
+          py::dict st;
+          st["bins"] = sts[b].bins;
+          st["intra_cus"] = sts[b].intra_cus;
+          st["inter_cus"] = sts[b].inter_cus;
+          st["skip_cus"] = sts[b].skip_cus;
+          st["merge_cus"] = sts[b].merge_cus;
+          out.append(py::make_tuple(to_bytes(nals[b]), st));
+        }
         return out;
       },
       py::arg("cfg"), py::arg("frames"), py::arg("ctu"), py::arg("cu"), py::arg("nzmap"), py::arg("ctb_off"),
-      py::arg("levels"), py::arg("threads") = 1);
+      py::arg("levels"), py::arg("threads") = 1, py::arg("with_stats") = false);
   m.def(
       "hevc_decode",
       [](py::bytes data, bool skip_filters) {

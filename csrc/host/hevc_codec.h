@@ -34,6 +34,7 @@ struct HevcConfig {
   int threads = 1;             // host threads coding the WPP substreams of one picture
   int level_idc = 0;           // > 0: general_level_idc (30 x level, -level); must fit the size / rate
   int bframes = 0;             // > 0: B pictures between the anchors (DPB of 2 references, 1 reordered picture)
+  int pyramid = 0;             // reference B pictures (DPB of 3 references, 2 reordered pictures)
   int tmvp = 0;                // sps_temporal_mvp_enabled_flag: temporal merge / AMVP candidates (needs FrameParams::col)
   int coded_width() const { return (width + kCtb - 1) / kCtb * kCtb; }
   int coded_height() const { return (height + kCtb - 1) / kCtb * kCtb; }
@@ -59,6 +60,11 @@ struct HevcFrameParams {
   // one reference picture per list: RefPicList0[0] / RefPicList1[0] POCs (-1: P slices use
   // poc - 1); the slice's short-term RPS holds exactly these pictures
   int ref_poc[2] = {-1, -1};
+  // explicit short-term RPS (n_rps >= 0): every picture the DPB keeps, with used_by_curr;
+  // RefPicList0[0] / RefPicList1[0] must be the closest used picture before / after
+  int n_rps = -1;
+  int rps_poc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint8_t rps_used[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   HevcColPic col;       // with HevcConfig::tmvp: the collocated picture (L1[0] in B, L0[0] in P)
 };
 

@@ -61,6 +61,12 @@ int auto_level_idc(const HevcConfig& c) {
   return 186;                                          // 6.2
 }
 
+// DPB size / reordering of the GOP structures this encoder writes (models/gop.py): P only
+// (1 reference + current), B pictures between two anchors (2 + current, 1 reordered),
+// a pyramid with a reference B (3 + current, 2 reordered)
+int dpb_minus1(const HevcConfig& c) { return c.bframes <= 0 ? 1 : (c.pyramid && c.bframes > 1 ? 3 : 2); }
+int num_reorder(const HevcConfig& c) { return c.bframes <= 0 ? 0 : (c.pyramid && c.bframes > 1 ? 2 : 1); }
+
 void profile_tier_level(BitWriter& bw, const HevcConfig& c) {
   const int profile = c.bit_depth > 8 ? 2 : 1;  // Main 10 / Main
   bw.put(0, 2);            // general_profile_space
@@ -91,8 +97,8 @@ std::vector<uint8_t> hevc_parameter_sets(const HevcConfig& c) {
     bw.put(0xFFFF, 16);  // vps_reserved_0xffff_16bits
     profile_tier_level(bw, c);
     bw.put_bit(1);       // vps_sub_layer_ordering_info_present_flag
-    bw.put_ue(c.bframes > 0 ? 2 : 1);  // vps_max_dec_pic_buffering_minus1 (B: two anchors + current)
-    bw.put_ue(c.bframes > 0 ? 1 : 0);  // vps_max_num_reorder_pics
+    bw.put_ue(dpb_minus1(c));  // vps_max_dec_pic_buffering_minus1
+    bw.put_ue(num_reorder(c));  // vps_max_num_reorder_pics
     bw.put_ue(0);        // vps_max_latency_increase_plus1
     bw.put(0, 6);        // vps_max_layer_id
     bw.put_ue(0);        // vps_num_layer_sets_minus1
@@ -123,8 +129,8 @@ std::vector<uint8_t> hevc_parameter_sets(const HevcConfig& c) {
     bw.put_ue(c.bit_depth - 8);  // bit_depth_chroma_minus8
     bw.put_ue(8 - 4);            // log2_max_pic_order_cnt_lsb_minus4 (8 bits)
     bw.put_bit(1);               // sps_sub_layer_ordering_info_present_flag
-    bw.put_ue(c.bframes > 0 ? 2 : 1);  // sps_max_dec_pic_buffering_minus1
-    bw.put_ue(c.bframes > 0 ? 1 : 0);  // sps_max_num_reorder_pics
+    bw.put_ue(dpb_minus1(c));    // sps_max_dec_pic_buffering_minus1
+    bw.put_ue(num_reorder(c));   // sps_max_num_reorder_pics
     bw.put_ue(0);                // sps_max_latency_increase_plus1
     bw.put_ue(kMinCbLog2 - 3);   // log2_min_luma_coding_block_size_minus3
     bw.put_ue(kCtbLog2 - kMinCbLog2);  // log2_diff_max_min_luma_coding_block_size
@@ -1121,25 +1127,49 @@ std::vector<uint8_t> hevc_write_slice(const HevcConfig& c, const HevcFrameParams
   if (!idr) {
     bw.put(fp.poc & 255, 8);  // slice_pic_order_cnt_lsb
     const int r0 = fp.ref_poc[0] >= 0 ? fp.ref_poc[0] : fp.poc - 1;
-    if (inter && !bslice && r0 == fp.poc - 1) {
+    // the short-term RPS: explicit, or the list references alone (all used)
+    std::vector<std::pair<int, int>> neg, pos;  // (POC, used)
+    if (fp.n_rps >= 0) {
+      if (fp.n_rps > 8) throw std::runtime_error("HEVC: at most 8 RPS entries");
+      for (int i = 0; i < fp.n_rps; ++i) {
+        const int q = fp.rps_poc[i];
+        if (q == fp.poc) throw std::runtime_error("HEVC: the RPS holds the current picture");
+        (q < fp.poc ? neg : pos).emplace_back(q, fp.rps_used[i] ? 1 : 0);
+      }
+    } else {
+      if (inter) neg.emplace_back(r0, 1);
+      if (bslice) pos.emplace_back(fp.ref_poc[1], 1);
+    }
+    std::sort(neg.begin(), neg.end(), [](auto& a, auto& b) { return a.first > b.first; });  // closest first
+    std::sort(pos.begin(), pos.end());
+    // RefPicList0[0] = the closest used picture before (P: or after when none), RefPicList1[0]
+    // = the closest used picture after (8.3.4 with one active entry per list)
+    int l0 = -1, l1 = -1;
+    for (auto& e : neg)
+      if (e.second && l0 < 0) l0 = e.first;
+    for (auto& e : pos)
+      if (e.second && l1 < 0) l1 = e.first;
+    if (inter && (l0 != r0 || (bslice && l1 != fp.ref_poc[1])))
+      throw std::runtime_error("HEVC: RefPicList0 must precede and RefPicList1 follow the current picture (closest used RPS entries)");
+    if (inter && !bslice && neg.size() == 1 && pos.empty() && neg[0].first == fp.poc - 1 && neg[0].second) {
       bw.put_bit(1);          // short_term_ref_pic_set_sps_flag (the single SPS set: no index bits)
     } else {
-      // st_ref_pic_set(num_short_term_ref_pic_sets = 1) in the slice header (7.3.7): the
-      // reference pictures of this slice, all used by the current picture
+      // st_ref_pic_set(num_short_term_ref_pic_sets = 1) in the slice header (7.3.7)
       bw.put_bit(0);          // short_term_ref_pic_set_sps_flag
       bw.put_bit(0);          // inter_ref_pic_set_prediction_flag
-      const bool has0 = inter, has1 = bslice;
-      if ((has0 && r0 >= fp.poc) || (has1 && fp.ref_poc[1] <= fp.poc))
-        throw std::runtime_error("HEVC: RefPicList0 must precede and RefPicList1 follow the current picture");
-      bw.put_ue(has0 ? 1 : 0);  // num_negative_pics
-      bw.put_ue(has1 ? 1 : 0);  // num_positive_pics
-      if (has0) {
-        bw.put_ue(fp.poc - r0 - 1);  // delta_poc_s0_minus1
-        bw.put_bit(1);               // used_by_curr_pic_s0_flag
+      bw.put_ue(static_cast<uint32_t>(neg.size()));  // num_negative_pics
+      bw.put_ue(static_cast<uint32_t>(pos.size()));  // num_positive_pics
+      int prev = fp.poc;
+      for (auto& e : neg) {
+        bw.put_ue(prev - e.first - 1);  // delta_poc_s0_minus1
+        bw.put_bit(e.second);           // used_by_curr_pic_s0_flag
+        prev = e.first;
       }
-      if (has1) {
-        bw.put_ue(fp.ref_poc[1] - fp.poc - 1);  // delta_poc_s1_minus1
-        bw.put_bit(1);                          // used_by_curr_pic_s1_flag
+      prev = fp.poc;
+      for (auto& e : pos) {
+        bw.put_ue(e.first - prev - 1);  // delta_poc_s1_minus1
+        bw.put_bit(e.second);           // used_by_curr_pic_s1_flag
+        prev = e.first;
       }
     }
     if (c.tmvp) bw.put_bit(1);  // slice_temporal_mvp_enabled_flag

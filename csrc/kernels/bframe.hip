@@ -452,6 +452,8 @@ struct HevcBArgs {
   int* bits;                    // [B, nmb]
   const int* qp;
   const int8_t* aq;
+  int bslice;                   // 0: P picture (list 0 only)
+  int max_merge;                // MaxNumMergeCand
 };
 
 // luma prediction (4 samples of row Y, columns X..X+3) of a B motion
@@ -524,9 +526,28 @@ __global__ __launch_bounds__(64) void hevc_b_choose(HevcBArgs a) {
   }
 }
 
-// Jacobi pass: candidates are the neighbours' current B motions (A1, B1, B0, A0, B2 of the
-// 16x16 grid), the temporal candidate and the zero bi-prediction; the cheapest by SATD +
-// lambda * (merge_flag + merge_idx) replaces the block's motion when it beats its cost
+// P pictures enter the merge passes in the same form: one list-0 search, bits = its mvd bits
+__global__ __launch_bounds__(256) void hevc_b_init_p(HevcBArgs a) {
+  const int nmb = a.g.nmb();
+  const int i = blockIdx.x * 256 + threadIdx.x, slot = blockIdx.y;
+  if (i >= nmb) return;
+  const size_t o = static_cast<size_t>(slot) * nmb + i;
+  const int x0 = a.mv0[o * 2], y0 = a.mv0[o * 2 + 1];
+  int16_t* m = a.mvb_out + o * 4;
+  m[0] = static_cast<int16_t>(x0);
+  m[1] = static_cast<int16_t>(y0);
+  m[2] = m[3] = 0;
+  a.dir_out[o] = 1;
+  a.cost[o] = a.cost0[o];
+  a.bits[o] = mvbits_se(x0 - a.pm0[o * 2]) + mvbits_se(y0 - a.pm0[o * 2 + 1]);
+}
+
+// Jacobi pass.  Each block is offered the merge list the CABAC writer would build for it as a
+// 16x16 CU (8.5.3.2.2-8.5.3.2.5 on the 16x16 grid of current motions, z-scan availability in
+// a 32x32 CTB: the below-left neighbour exists only for quadrant 0, the above-right one not for
+// quadrant 3; pruning A1-B1, B1-B0, A1-A0, A1/B1-B2; the temporal candidate, combined
+// bi-predictive and zero candidates; MaxNumMergeCand entries); the cheapest by SATD + lambda *
+// (merge_flag + merge_idx bins) replaces the block's motion when it beats its cost.
 __global__ __launch_bounds__(64) void hevc_b_merge(HevcBArgs a) {
   const Geom& g = a.g;
   const int nmb = g.nmb();
@@ -536,31 +557,71 @@ __global__ __launch_bounds__(64) void hevc_b_merge(HevcBArgs a) {
   const size_t o = static_cast<size_t>(slot) * nmb + mb;
   const size_t sb = static_cast<size_t>(slot) * nmb;
   const int mx = mb % g.wmb, my = mb / g.wmb;
-  int kd[7], kv[7][4], nk = 0;
-  auto add = [&](int d, const int16_t* v) {
-    if (!d) return;
-    int w[4] = {d & 1 ? v[0] : 0, d & 1 ? v[1] : 0, d & 2 ? v[2] : 0, d & 2 ? v[3] : 0};
-    for (int j = 0; j < nk; ++j)
-      if (kd[j] == d && kv[j][0] == w[0] && kv[j][1] == w[1] && kv[j][2] == w[2] && kv[j][3] == w[3]) return;
+  const int q = (mx & 1) | ((my & 1) << 1);
+  const int maxc = a.max_merge;
+  int kd[6], kv[6][4], nk = 0;
+  auto load = [&](int n, int* d, int* w) {
+    const int dd = a.dir_in[sb + n];
+    const int16_t* v = a.mvb_in + (sb + n) * 4;
+    *d = dd;
+    w[0] = dd & 1 ? v[0] : 0;
+    w[1] = dd & 1 ? v[1] : 0;
+    w[2] = dd & 2 ? v[2] : 0;
+    w[3] = dd & 2 ? v[3] : 0;
+  };
+  auto same = [](int da, const int* wa, int db, const int* wb) {
+    return da == db && wa[0] == wb[0] && wa[1] == wb[1] && wa[2] == wb[2] && wa[3] == wb[3];
+  };
+  int dA1 = 0, dB1 = 0, dB0 = 0, dA0 = 0, dB2 = 0, wA1[4], wB1[4], wB0[4], wA0[4], wB2[4];
+  const bool a1 = mx > 0, av_b1 = my > 0;
+  bool b0 = my > 0 && mx + 1 < g.wmb && q != 3, a0 = q == 0 && mx > 0 && my + 1 < g.hmb, b2 = mx > 0 && my > 0;
+  if (a1) load(mb - 1, &dA1, wA1);
+  if (av_b1) load(mb - g.wmb, &dB1, wB1);
+  if (b0) load(mb - g.wmb + 1, &dB0, wB0);
+  if (a0) load(mb + g.wmb - 1, &dA0, wA0);
+  if (b2) load(mb - g.wmb - 1, &dB2, wB2);
+  const bool b1 = av_b1 && !(a1 && same(dA1, wA1, dB1, wB1));
+  if (b0 && av_b1 && same(dB1, wB1, dB0, wB0)) b0 = false;
+  if (a0 && a1 && same(dA1, wA1, dA0, wA0)) a0 = false;
+  if (b2 && ((a1 && same(dA1, wA1, dB2, wB2)) || (av_b1 && same(dB1, wB1, dB2, wB2)))) b2 = false;
+  if (static_cast<int>(a0) + a1 + b0 + b1 == 4) b2 = false;
+  auto push = [&](int d, const int* w) {
+    if (nk >= 6) return;
     kd[nk] = d;
     for (int c = 0; c < 4; ++c) kv[nk][c] = w[c];
     ++nk;
   };
-  auto nb = [&](bool ok, int n) {
-    if (ok) add(a.dir_in[sb + n], a.mvb_in + (sb + n) * 4);
-  };
-  nb(mx > 0, mb - 1);                              // A1
-  nb(my > 0, mb - g.wmb);                          // B1
-  nb(my > 0 && mx < g.wmb - 1, mb - g.wmb + 1);    // B0
-  nb(mx > 0 && my < g.hmb - 1, mb + g.wmb - 1);    // A0
-  nb(mx > 0 && my > 0, mb - g.wmb - 1);            // B2
-  if (a.tdir) add(a.tdir[o], a.tmv + o * 4);
-  {
-    const int16_t z[4] = {0, 0, 0, 0};
-    add(3, z);
+  if (a1) push(dA1, wA1);
+  if (b1) push(dB1, wB1);
+  if (b0) push(dB0, wB0);
+  if (a0) push(dA0, wA0);
+  if (b2) push(dB2, wB2);
+  if (nk < maxc && a.tdir && a.tdir[o]) {
+    const int td = a.bslice ? 3 : 1;
+    const int16_t* t = a.tmv + o * 4;
+    const int w[4] = {t[0], t[1], a.bslice ? t[2] : 0, a.bslice ? t[3] : 0};
+    push(td, w);
   }
+  const int orig = nk;
+  if (a.bslice && orig > 1 && orig < maxc) {
+    const int l0i[12] = {0, 1, 0, 2, 1, 2, 0, 3, 1, 3, 2, 3};
+    const int l1i[12] = {1, 0, 2, 0, 2, 1, 3, 0, 3, 1, 3, 2};
+    for (int c = 0; c < orig * (orig - 1) && nk < maxc; ++c) {
+      const int i0 = l0i[c], i1 = l1i[c];
+      if ((kd[i0] & 1) && (kd[i1] & 2)) {
+        const int w[4] = {kv[i0][0], kv[i0][1], kv[i1][2], kv[i1][3]};
+        push(3, w);
+      }
+    }
+  }
+  {
+    const int z[4] = {0, 0, 0, 0};
+    while (nk < maxc) push(a.bslice ? 3 : 1, z);
+  }
+  if (nk > maxc) nk = maxc;
   const int cd = a.dir_in[o];
-  const int16_t* cv = a.mvb_in + o * 4;
+  const int16_t* cvp = a.mvb_in + o * 4;
+  const int cw[4] = {cd & 1 ? cvp[0] : 0, cd & 1 ? cvp[1] : 0, cd & 2 ? cvp[2] : 0, cd & 2 ? cvp[3] : 0};
   const int qp = clampi(a.qp[slot] + (a.aq ? a.aq[o] : 0), 0, 51);
   const int lam = h264::kLambda[qp];
   const int c_cur = a.cost[o];
@@ -569,20 +630,24 @@ __global__ __launch_bounds__(64) void hevc_b_merge(HevcBArgs a) {
   const int X = mx * 16 + c0, Y = my * 16 + r;
   const size_t yo = static_cast<size_t>(slot) * g.ysize();
   const size_t ho = static_cast<size_t>(slot) * 3 * (g.W + 2 * kHpMargin) * (g.H + 2 * kHpMargin);
-  const uint8_t *G0 = a.ref0 + yo, *G1 = a.ref1 + yo, *H0 = a.hp0 + ho, *H1 = a.hp1 + ho;
+  const uint8_t *G0 = a.ref0 + yo, *H0 = a.hp0 + ho;
+  const uint8_t *G1 = a.bslice ? a.ref1 + yo : G0, *H1 = a.bslice ? a.hp1 + ho : H0;
   const uint32_t src = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y) * g.W + X);
   __shared__ int s_res[256];
   int best = c_cur, bbits = a.bits[o], bj = -1;
   for (int j = 0; j < nk; ++j) {
-    const bool same = kd[j] == cd && (!(cd & 1) || (kv[j][0] == cv[0] && kv[j][1] == cv[1])) &&
-                      (!(cd & 2) || (kv[j][2] == cv[2] && kv[j][3] == cv[3]));
-    int satd;
-    if (same) satd = satd_cur;
-    else satd = satd16_words(s_res, src, mc4_b(a, G0, H0, G1, H1, X, Y, kd[j], kv[j][0], kv[j][1], kv[j][2], kv[j][3]), r, c0);
-    const int cst = satd + lam * (1 + j);
+    bool dup = false;  // the same motion earlier in the list: never cheaper
+    for (int i = 0; i < j; ++i) dup = dup || same(kd[i], kv[i], kd[j], kv[j]);
+    if (dup) continue;
+    const int sat = same(kd[j], kv[j], cd, cw)
+                        ? satd_cur
+                        : satd16_words(s_res, src, mc4_b(a, G0, H0, G1, H1, X, Y, kd[j], kv[j][0], kv[j][1], kv[j][2], kv[j][3]),
+                                       r, c0);
+    const int nb = 1 + (maxc > 1 ? min(j + 1, maxc - 1) : 0);  // merge_flag + truncated-unary merge_idx
+    const int cst = sat + lam * nb;
     if (cst < best) {
       best = cst;
-      bbits = 1 + j;
+      bbits = nb;
       bj = j;
     }
   }
@@ -592,7 +657,7 @@ __global__ __launch_bounds__(64) void hevc_b_merge(HevcBArgs a) {
       for (int c = 0; c < 4; ++c) m[c] = static_cast<int16_t>(kv[bj][c]);
       a.dir_out[o] = static_cast<uint8_t>(kd[bj]);
     } else {
-      for (int c = 0; c < 4; ++c) m[c] = cv[c];
+      for (int c = 0; c < 4; ++c) m[c] = cvp[c];
       a.dir_out[o] = static_cast<uint8_t>(cd);
     }
     a.cost[o] = best;
@@ -902,7 +967,7 @@ extern "C" void mivc_launch_hevc_b(int mode, int B, int wmb, int hmb, const uint
                                    const int16_t* mv1, const int* cost0, const int* cost1, const int16_t* pm0,
                                    const int16_t* pm1, const int16_t* tmv, const uint8_t* tdir, const int16_t* mvb_in,
                                    const uint8_t* dir_in, int16_t* mvb_out, uint8_t* dir_out, int* cost, int* bits,
-                                   const int* qp, const int8_t* aq, void* stream) {
+                                   const int* qp, const int8_t* aq, void* stream, int bslice, int max_merge) {
   HevcBArgs a;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.src_y = src_y;
@@ -926,6 +991,10 @@ extern "C" void mivc_launch_hevc_b(int mode, int B, int wmb, int hmb, const uint
   a.bits = bits;
   a.qp = qp;
   a.aq = aq;
-  if (mode == 0) hipLaunchKernelGGL(hevc_b_choose, dim3(wmb * hmb, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
-  else hipLaunchKernelGGL(hevc_b_merge, dim3(wmb * hmb, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
+  a.bslice = bslice;
+  a.max_merge = max_merge;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (mode == 0) hipLaunchKernelGGL(hevc_b_choose, dim3(wmb * hmb, B), dim3(64), 0, st, a);
+  else if (mode == 1) hipLaunchKernelGGL(hevc_b_merge, dim3(wmb * hmb, B), dim3(64), 0, st, a);
+  else hipLaunchKernelGGL(hevc_b_init_p, dim3((wmb * hmb + 255) / 256, B), dim3(256), 0, st, a);
 }

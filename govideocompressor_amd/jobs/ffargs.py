@@ -194,7 +194,11 @@ H264_PARAMS = {
     "threads": ("@threads", int),
 }
 HEVC_PARAMS = {
-    "bframes": ("@bframes", _only("0")),
+    "bframes": ("bframes", _int_in(0, 8)),
+    "b-pyramid": ("pyramid", _flag),
+    "no-b-pyramid": ("pyramid", lambda v: not _flag(v)),
+    "tmvp": ("tmvp", _flag),
+    "no-tmvp": ("tmvp", lambda v: not _flag(v)),
     "keyint": ("@keyint", _int_in(1, 100000)),
     "aq-mode": ("aq_strength", _aq_mode),
     "aq-strength": ("aq_strength", _float_in(0.0, 3.0)),
@@ -226,7 +230,7 @@ _HEVC_PROFILES = {"main": {}, "main10": {}, "mainstillpicture": dict(intra_only=
 _TUNES = {
     "h264": {"psnr": dict(aq_strength=0.0), "zerolatency": dict(bframes=0, lookahead=False, mbtree=False),
              "fastdecode": dict(cabac=False, deblock=False)},
-    "hevc": {"psnr": dict(aq_strength=0.0), "zerolatency": dict(lookahead=False, cutree=False),
+    "hevc": {"psnr": dict(aq_strength=0.0), "zerolatency": dict(bframes=0, lookahead=False, cutree=False),
              "fastdecode": dict(deblock=False, sao=False)},
 }
 

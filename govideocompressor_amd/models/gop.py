@@ -63,3 +63,82 @@ def gop_plan(frames: int, bframes: int, anchors_at=()) -> list[PicPlan]:
         for d in range(a0 + 1, a1):
             out.append(PicPlan(d, "B", fn & 0xFFFF, 2 * d, -1, l0=a0, l1=a1, l1_anchor=i))
     return out
+
+
+@dataclass(frozen=True)
+class GopPic:
+    """One picture of an HEVC closed GOP in coding order (models/hevc_gpu.py).
+
+    ``rps``: the reference picture set of the picture, ``(display index, used by the
+    current picture)`` for every picture the DPB must still hold; ``slot``: the
+    reconstruction buffer (0 .. ref_slots - 1 for reference pictures, ``ref_slots`` for
+    non-reference B pictures); ``l0`` / ``l1``: display indices of RefPicList0[0] /
+    RefPicList1[0] and ``s0`` / ``s1`` their buffers."""
+    d: int
+    kind: str                # "I", "P", "B"
+    ref: bool                # referenced by later pictures (I, P, the pyramid's middle B)
+    slot: int
+    rps: tuple = ()
+    l0: int = -1
+    l1: int = -1
+    s0: int = -1
+    s1: int = -1
+
+
+def hevc_gop_plan(frames: int, bframes: int, pyramid: bool = True, anchors_at=(), ref_slots: int = 3) -> list[GopPic]:
+    """x265-style closed GOP: I0, P anchors every ``bframes + 1`` pictures (plus the last
+    picture and ``anchors_at``), each followed by the B pictures before it.  With
+    ``pyramid`` and two or more B pictures in a run, the middle one is a reference B
+    (list 0 = the previous anchor, list 1 = the new one) coded first, and the others are
+    non-reference b pictures predicting from their nearest references on both sides
+    (x265 --b-pyramid).  The DPB is simulated to give every picture its RPS and buffer."""
+    if frames < 1:
+        return []
+    step = max(0, int(bframes)) + 1
+    anchors = sorted(set(range(0, frames, step)) | {frames - 1} | {int(d) for d in anchors_at if 0 <= int(d) < frames})
+    if step > 1:  # keep every B run <= bframes after inserting the extra anchors
+        out_a, prev = [0], 0
+        for a in anchors[1:]:
+            while a - prev > step:
+                prev += step
+                out_a.append(prev)
+            out_a.append(a)
+            prev = a
+        anchors = out_a
+    # (display index, kind, ref, l0, l1) in coding order
+    seq = [(0, "I", True, -1, -1)]
+    for a0, a1 in zip(anchors, anchors[1:]):
+        seq.append((a1, "P", True, a0, -1))
+        run = list(range(a0 + 1, a1))
+        if pyramid and len(run) >= 2:
+            mid = (a0 + a1) // 2
+            seq.append((mid, "B", True, a0, a1))
+            seq += [(d, "B", False, a0, mid) for d in run if d < mid]
+            seq += [(d, "B", False, mid, a1) for d in run if d > mid]
+        else:
+            seq += [(d, "B", False, a0, a1) for d in run]
+    # a reference picture stays in the DPB until the last picture that uses it
+    last_use: dict = {}
+    for i, (d, kind, ref, l0, l1) in enumerate(seq):
+        for r in (l0, l1):
+            if r >= 0:
+                last_use[r] = i
+    dpb: dict = {}  # display index -> slot
+    out = []
+    for i, (d, kind, ref, l0, l1) in enumerate(seq):
+        if kind == "I":
+            dpb = {}
+        keep = {r: s for r, s in dpb.items() if last_use.get(r, -1) >= i}
+        dpb = keep
+        rps = tuple(sorted((r, r in (l0, l1)) for r in keep))
+        if ref:
+            free = [s for s in range(ref_slots) if s not in dpb.values()]
+            if not free:
+                raise ValueError("hevc_gop_plan: more reference pictures than buffers")
+            slot = free[0]
+        else:
+            slot = ref_slots
+        out.append(GopPic(d, kind, ref, slot, rps, l0, l1, dpb.get(l0, -1), dpb.get(l1, -1)))
+        if ref:
+            dpb[d] = slot
+    return out

@@ -88,14 +88,25 @@ class HevcParams:
     # estimate (a lower bound of the finer intra search) plus the intra bias; elsewhere inter
     # is decisive and the CTB gets no intra candidates
     intra_gate: bool = True
-    # x265 --bframes: non-reference B pictures between the P anchors (list 0 = the previous
-    # anchor, list 1 = the next; models/gop.py), coded b_qp_offset above their anchors
-    # (x265 --pbratio 1.3 = +2 QP); 0 = P pictures only.  keyint > 0, intra_only and the
-    # two-pass feedback encode keep P-only GOPs.
-    bframes: int = 3
-    b_qp_offset: int = 2
+    # x265 --bframes: B pictures between the P anchors (list 0 = the previous reference, list 1 =
+    # the next; models/gop.py hevc_gop_plan), coded b_qp_offset above their anchors; 0 = P
+    # pictures only.  keyint > 0 and intra_only keep P-only GOPs.  x265 places its 4 B frames
+    # adaptively (--b-adapt 2) at --pbratio 1.3 (+2 QP); this encoder's GOP is static (one plan
+    # per batch), so its defaults come from the 1080p CRF 22-34 sweep of the benchmark content
+    # (profiles/r3_hevc_bframes_rd.md): BD-rate vs P-only -4.4 % for 1 B at +4 QP, while runs of
+    # 2-4 B pictures lose there (+2.6 .. +7.9 % at +2 QP: the far anchors cost more than the B
+    # pictures save on this content)
+    bframes: int = 1
+    b_qp_offset: int = 4
+    # x265 --b-pyramid (default on): the middle B of a run of 2+ is a reference picture (at half
+    # the B QP offset) and the others predict from their nearest references (models/gop.py)
+    pyramid: bool = True
     # x265 --tmvp (default on): temporal merge / AMVP candidates from the collocated anchor
     tmvp: bool = True
+    # merge passes offer each 16x16 block the writer's exact merge list for a 16x16 CU
+    # (bframe.hip hevc_b_merge; P and B pictures); False: P pictures use the neighbour-vector
+    # approximation of round 2 (hevc_merge_refine)
+    merge_exact: bool = True
 
     def eff_bframes(self) -> int:
         return 0 if (self.intra_only or self.keyint > 0) else max(0, int(self.bframes))
@@ -107,7 +118,8 @@ class HevcParams:
         return dict(width=self.width, height=self.height, bit_depth=self.bit_depth, fps=self.fps,
                     sao=int(self.sao), deblock=int(self.deblock), max_merge=self.max_merge, wpp=int(self.wpp),
                     cu_qp_delta=int(self.adaptive_qp()), tu_inter_depth=int(self.tu_inter_depth), sdh=int(self.sdh),
-                    level_idc=int(self.level_idc), bframes=self.eff_bframes(), tmvp=int(self.tmvp and not self.intra_only))
+                    level_idc=int(self.level_idc), bframes=self.eff_bframes(), tmvp=int(self.tmvp and not self.intra_only),
+                    pyramid=int(self.pyramid))
 
     def frame_qps(self) -> tuple[int, int]:
         qp_p = int(round(self.crf)) if self.crf is not None else int(self.qp)
@@ -163,9 +175,10 @@ class GpuHevcEncoder:
 
         self.src = planes()
         self.nb = params.eff_bframes()
-        # anchors (I / P) alternate between rec[0] and rec[1] (anchor ordinal & 1); B pictures
-        # (never referenced) reconstruct into rec[2]
-        self.rec = [planes(), planes()] + ([planes()] if self.nb else [])
+        # reconstruction buffers: one per DPB slot of a reference picture (models/gop.py
+        # hevc_gop_plan: 2 for P-only GOPs, 3 with B pictures) + one for non-reference B pictures
+        self.ref_slots = 3 if self.nb else 2
+        self.rec = [planes() for _ in range(self.ref_slots)] + ([planes()] if self.nb else [])
         self.dbk = planes()                  # SAO output ping-pong buffer
         self.coefs = [planes(i16), planes(i16)]  # double-buffered: copy-out of t overlaps t + 1
         self.coef = self.coefs[0]
@@ -173,32 +186,35 @@ class GpuHevcEncoder:
         nmb = self.wmb * self.hmb
         self.nmb = nmb
         self.src8 = torch.zeros((B, H, W), dtype=torch.uint8, device=dev)   # motion-search proxies
-        # 8-bit proxies of the two latest anchors and their half-sample planes, built once per
-        # anchor and shared by every picture that references it
-        self.ref8s = [torch.zeros((B, H, W), dtype=torch.uint8, device=dev) for _ in range(2)]
-        self.me_hps = [torch.empty(B * 3 * (H + 8) * (W + 8) + 64, dtype=torch.uint8, device=dev) for _ in range(2)]
+        # 8-bit proxies of the reference pictures and their half-sample planes (per DPB slot),
+        # built once per reference picture and shared by every picture that references it
+        self.ref8s = [torch.zeros((B, H, W), dtype=torch.uint8, device=dev) for _ in range(self.ref_slots)]
+        self.me_hps = [torch.empty(B * 3 * (H + 8) * (W + 8) + 64, dtype=torch.uint8, device=dev)
+                       for _ in range(self.ref_slots)]
         self.mv = torch.zeros((B, nmb, 2), dtype=torch.int16, device=dev)
         self.prev_mv = torch.zeros((B, nmb, 2), dtype=torch.int16, device=dev)
         self.mv_tmp = torch.zeros((B, nmb, 2), dtype=torch.int16, device=dev)
         self.me_cost = torch.zeros((B, nmb), dtype=torch.int32, device=dev)
         self.me_intra = torch.zeros((B, nmb), dtype=torch.int32, device=dev)
         self.me_pred = torch.zeros((B, nmb, 256), dtype=torch.uint8, device=dev)
+        i16_, i32_, u8_ = torch.int16, torch.int32, torch.uint8
+        self.tmv = torch.zeros((B, nmb, 4), dtype=i16_, device=dev)
+        self.tdir = torch.zeros((B, nmb), dtype=u8_, device=dev)
+        self.mvb = [torch.zeros((B, nmb, 4), dtype=i16_, device=dev) for _ in range(2)]
+        self.dirb = [torch.zeros((B, nmb), dtype=u8_, device=dev) for _ in range(2)]
+        self.bcost = torch.zeros((B, nmb), dtype=i32_, device=dev)
+        self.bbits = torch.zeros((B, nmb), dtype=i32_, device=dev)
+        self.pm0 = torch.zeros((B, nmb, 2), dtype=i16_, device=dev)
+        self.pm1 = torch.zeros((B, nmb, 2), dtype=i16_, device=dev)
+        # motion of each reference picture (per DPB slot) per 16x16 block: its records at each
+        # block's top-left granule, what TMVP reads after 16x16 motion compression
+        R = self.ref_slots
+        self.col_dir = torch.zeros((R, B, self.hmb, self.wmb), dtype=u8_, device=dev)
+        self.col_mv0 = torch.zeros((R, B, self.hmb, self.wmb, 2), dtype=i32_, device=dev)
+        self.col_mv1 = torch.zeros((R, B, self.hmb, self.wmb, 2), dtype=i32_, device=dev)
         if self.nb:
-            i16_, i32_, u8_ = torch.int16, torch.int32, torch.uint8
             self.mv1 = torch.zeros((B, nmb, 2), dtype=i16_, device=dev)
             self.me_cost1 = torch.zeros((B, nmb), dtype=i32_, device=dev)
-            self.pm0 = torch.zeros((B, nmb, 2), dtype=i16_, device=dev)
-            self.pm1 = torch.zeros((B, nmb, 2), dtype=i16_, device=dev)
-            self.tmv = torch.zeros((B, nmb, 4), dtype=i16_, device=dev)
-            self.tdir = torch.zeros((B, nmb), dtype=u8_, device=dev)
-            self.mvb = [torch.zeros((B, nmb, 4), dtype=i16_, device=dev) for _ in range(2)]
-            self.dirb = [torch.zeros((B, nmb), dtype=u8_, device=dev) for _ in range(2)]
-            self.bcost = torch.zeros((B, nmb), dtype=i32_, device=dev)
-            self.bbits = torch.zeros((B, nmb), dtype=i32_, device=dev)
-            # motion of the latest anchor per 16x16 block (its records at each block's top-left
-            # granule: what TMVP reads after 16x16 motion compression)
-            self.col_inter = torch.zeros((B, self.hmb, self.wmb), dtype=torch.bool, device=dev)
-            self.col_mv = torch.zeros((B, self.hmb, self.wmb, 2), dtype=i32_, device=dev)
         self.cand = torch.zeros((B, self.nctb, 58), dtype=torch.int32, device=dev)  # kCandStride
         self.ctus = [torch.zeros((B, self.nctb, 32), dtype=torch.uint8, device=dev) for _ in range(2)]
         self.cus = [torch.zeros((B, self.nctb * 16, 16), dtype=torch.uint8, device=dev) for _ in range(2)]
@@ -226,6 +242,7 @@ class GpuHevcEncoder:
         self.timings: dict[str, float] = {}
         self.stats: dict[str, float] = {}
         self.ctb_need = torch.ones((B, self.nctb), dtype=torch.uint8, device=dev)
+        self.cu_stats = None  # {} -> the writer's CU counts per picture type are accumulated here
         # per-stage device time (HIP events, resolved once per encode): MIVC_STAGE_TIMING=1
         from ..obs.timers import EventTimer
         self.stage_timer = EventTimer(enabled=os.environ.get("MIVC_STAGE_TIMING", "0") == "1")
@@ -328,46 +345,68 @@ class GpuHevcEncoder:
         p = mv * GpuHevcEncoder._dsf(td, tb)
         return (torch.sign(p) * ((p.abs() + 127) >> 8)).clamp_(-32768, 32767)
 
-    def _store_col(self):
-        """The anchor just coded becomes the collocated picture of the next B pictures: its
-        records at each 16x16 block's top-left granule (z-order granules 0 / 4 / 8 / 12)."""
+    def _store_col(self, slot: int):
+        """A reference picture just coded may become the collocated picture of later B
+        pictures: its records at each 16x16 block's top-left granule (z-order granules
+        0 / 4 / 8 / 12), kept per DPB slot."""
         B, hc, wc = self.B, self.hctb, self.wctb
         rec = self.cu.view(B, hc, wc, 4, 4, 16)[:, :, :, :, 0, :].reshape(B, hc, wc, 2, 2, 16)
         rec = rec.permute(0, 1, 3, 2, 4, 5).reshape(B, self.hmb, self.wmb, 16)
-        self.col_inter.copy_(rec[..., 0] == 1)
-        self.col_mv.copy_(rec[..., 4:8].contiguous().view(torch.int16).to(torch.int32))
+        inter = rec[..., 0] == 1
+        d = rec[..., 12]
+        self.col_dir[slot].copy_(torch.where(inter, torch.where(d == 0, torch.ones_like(d), d), torch.zeros_like(d)))
+        self.col_mv0[slot].copy_(rec[..., 4:8].contiguous().view(torch.int16).to(torch.int32))
+        self.col_mv1[slot].copy_(rec[..., 8:12].contiguous().view(torch.int16).to(torch.int32))
 
-    def _temporal_candidates(self, pic):
-        """TMVP merge candidate per 16x16 block (the writer's exact derivation for a 16x16 CU:
-        the collocated bottom-right block inside the CTB row, else the centre one) scaled to
-        both lists, and the two searches' predictors."""
-        ci, cm = self.col_inter, self.col_mv
-        br_i = torch.zeros_like(ci)
-        br_m = torch.zeros_like(cm)
-        br_i[:, :-1, :-1] = ci[:, 1:, 1:]
-        br_m[:, :-1, :-1] = cm[:, 1:, 1:]
-        even = (torch.arange(self.hmb, device=self.dev) % 2 == 0)[None, :, None]
-        use_br = br_i & even
-        sel = torch.where(use_br[..., None], br_m, cm)
-        avail = (use_br | ci).reshape(self.B, self.nmb)
-        td = pic.l1 - pic.l0  # the col anchor (list 1) predicts from list 0's picture
-        t0 = self._scale(sel, td, pic.d - pic.l0).reshape(self.B, self.nmb, 2)
-        t1 = self._scale(sel, td, pic.d - pic.l1).reshape(self.B, self.nmb, 2)
-        av = avail[..., None].to(torch.int32)
-        self.tmv[..., 0:2].copy_(t0 * av)
-        self.tmv[..., 2:4].copy_(t1 * av)
-        self.tdir.copy_(avail.to(torch.uint8) * 3)
+    def _temporal_candidates(self, pic, col_refs: tuple):
+        """See _temporal_for; B pictures: the collocated picture is RefPicList1[0]."""
+        self._temporal_for(pic, pic.s1, pic.l1, col_refs, (pic.l0, pic.l1))
         self.pm0.copy_(self.tmv[..., 0:2])
         self.pm1.copy_(self.tmv[..., 2:4])
 
+    def _temporal_for(self, pic, cs: int, col: int, col_refs: tuple, targets: tuple):
+        """TMVP merge candidate per 16x16 block (the writer's derivation for a 16x16 CU: the
+        collocated bottom-right block inside the CTB row, else the centre one; a list-1-only
+        collocated block gives its list-1 vector, any other its list-0 vector
+        (collocated_from_l0_flag 0)) scaled to both lists, and the two searches' predictors.
+        cs / col: DPB slot and display index of the collocated picture, col_refs: its own list-0 /
+        list-1 references, targets: the current picture's RefPicList0[0] / RefPicList1[0] (-1: none)."""
+        cdir, m0, m1 = self.col_dir[cs], self.col_mv0[cs], self.col_mv1[cs]
+        ok = cdir != 0
+        use1 = cdir == 2
+        mv = torch.where(use1[..., None], m1, m0)
+        br_ok = torch.zeros_like(ok)
+        br_mv = torch.zeros_like(mv)
+        br_1 = torch.zeros_like(use1)
+        br_ok[:, :-1, :-1] = ok[:, 1:, 1:]
+        br_mv[:, :-1, :-1] = mv[:, 1:, 1:]
+        br_1[:, :-1, :-1] = use1[:, 1:, 1:]
+        even = (torch.arange(self.hmb, device=self.dev) % 2 == 0)[None, :, None]
+        use_br = br_ok & even
+        sel = torch.where(use_br[..., None], br_mv, mv)
+        sel1 = torch.where(use_br, br_1, use1)[..., None]
+        avail = (use_br | ok).reshape(self.B, self.nmb)
+        td0, td1 = col - col_refs[0], col - col_refs[1]   # the col block's own POC distance per list
+        for x, tgt in enumerate(targets):
+            if tgt < 0:
+                self.tmv[..., 2 * x:2 * x + 2].zero_()
+                continue
+            tb = pic.d - tgt
+            v = torch.where(sel1, self._scale(sel, td1, tb), self._scale(sel, td0, tb)).reshape(self.B, self.nmb, 2)
+            self.tmv[..., 2 * x:2 * x + 2].copy_(v * avail[..., None].to(torch.int32))
+        self.tdir.copy_(avail.to(torch.uint8) * (3 if targets[1] >= 0 else 1))
+
     def _plan(self, F: int, cuts_h: np.ndarray, anchors_at) -> list:
-        from .gop import PicPlan, gop_plan
+        from .gop import GopPic, hevc_gop_plan
         if self.nb:
-            return gop_plan(F, self.nb, set(anchors_at) | {d for d in range(1, F) if cuts_h[:, d].any()})
+            return hevc_gop_plan(F, self.nb, self.p.pyramid, set(anchors_at) | {d for d in range(1, F) if cuts_h[:, d].any()})
         out = []
         for t in range(F):
             idr = t == 0 or self.p.intra_only or (self.p.keyint > 0 and t % self.p.keyint == 0)
-            out.append(PicPlan(t, "I" if idr else "P", t, t, t, l0=-1 if idr else t - 1))
+            if idr:
+                out.append(GopPic(t, "I", True, t & 1))
+            else:
+                out.append(GopPic(t, "P", True, t & 1, ((t - 1, True),), t - 1, -1, (t - 1) & 1))
         return out
 
     # ------------------------------------------------------------------ encode
@@ -409,8 +448,11 @@ class GpuHevcEncoder:
             cfg["threads"] = max(1, min(32, self.entropy_threads // max(1, B)))
         qps = np.clip(np.asarray(qps, dtype=np.int32).reshape(B, F), 0, 51)
         if self.nb and from_la:
-            bd_ = [pic.d for pic in plan if pic.kind == "B"]
-            qps[:, bd_] = np.minimum(qps[:, bd_] + int(self.p.b_qp_offset), 51)
+            # x265 --pbratio: B pictures above their anchors; a pyramid's reference B halfway
+            bo = int(self.p.b_qp_offset)
+            for pic in plan:
+                if pic.kind == "B":
+                    qps[:, pic.d] = np.minimum(qps[:, pic.d] + (bo // 2 if pic.ref else bo), 51)
         if qp_delta is not None:
             from ..rc.abr import apply_delta
             qps = apply_delta(qps, qp_delta)
@@ -434,7 +476,9 @@ class GpuHevcEncoder:
         st = self.stage_timer
         gate_sum: list[torch.Tensor] = []
         tmvp = bool(cfg.get("tmvp", 0))
-        anchor_cu: dict = {}   # display index of an anchor -> (host copy of its CU records or None, its list-0 index)
+        anchor_cu: dict = {}   # display index of a reference picture -> (host copy of its CU records or None, l0, l1)
+        ref_lists: dict = {}   # display index of a reference picture -> its (l0, l1) display indices
+        plan_refs = {pic.d: pic.kind for pic in plan if pic.ref}
         idr_d = 0              # display index of the latest IDR picture (POC 0)
         for t in range(F):
             pic = plan[t]
@@ -460,17 +504,14 @@ class GpuHevcEncoder:
             # per-CTB QPs (AQ + cutree offsets of frame d); without them every CTB at the frame QP.
             # cutree offsets belong to referenced pictures: B pictures get variance AQ only
             extra, estride, erows = 0, 0, 0
-            if self._cutree is not None and self.p.adaptive_qp() and pic.kind != "B":
+            if self._cutree is not None and self.p.adaptive_qp() and pic.ref:
                 ct = self._cutree
                 extra, estride, erows = ct.data_ptr() + d * ct.shape[2] * 4, ct.shape[1] * ct.shape[2], self._cutree_rows
             with st("aq"):
                 self.hip.hevc_aq(B, self.W, self.H, bd, p(self.src[0]), p(self.src[1]), p(self.src[2]), p(self.qp),
                                  float(self.p.aq_strength) if self.p.adaptive_qp() else 0.0, extra, estride, erows,
                                  p(self.ctb_qp), p(self.mb_aq), s)
-            if pic.kind == "B":
-                ci, r0, r1 = 2, (pic.l1_anchor - 1) & 1, pic.l1_anchor & 1
-            else:
-                ci, r0, r1 = pic.anchor & 1, (pic.anchor - 1) & 1, -1
+            ci, r0, r1 = pic.slot, pic.s0, pic.s1
             cur, ref = self.rec[ci], self.rec[r0]
             kb = t % 2
             # the copy-out of step t - 2 must have read these buffers before they are rewritten
@@ -494,16 +535,39 @@ class GpuHevcEncoder:
                                     p(self.me_cost), p(self.me_pred), p(self.me_intra), p(self.qp), self.p.me_range,
                                     self.p.subpel, s, p(hp), p(self.mb_aq), 1)
                     with st("merge_refine"):
-                        for it in range(int(self.p.merge_refine)):
-                            a_, b_ = (self.mv, self.mv_tmp) if it % 2 == 0 else (self.mv_tmp, self.mv)
-                            self.hip.hevc_merge_refine(B, self.wmb, self.hmb, p(self.src8), p(ref8), p(hp), p(a_), p(b_),
-                                                       p(self.me_cost), p(self.prev_mv), p(self.qp), p(self.mb_aq), s)
-                        if int(self.p.merge_refine) % 2:
-                            self.mv.copy_(self.mv_tmp)
+                        if self.p.merge_exact:
+                            # the search as list-0 motion, then the writer-exact merge passes
+                            # (temporal candidates from RefPicList0[0]'s motion)
+                            tm_, td_ = 0, 0
+                            if tmvp and plan_refs.get(pic.l0, "I") != "I":
+                                self._temporal_for(pic, r0, pic.l0, ref_lists[pic.l0], (pic.l0, -1))
+                                tm_, td_ = p(self.tmv), p(self.tdir)
+                            pargs = (B, self.wmb, self.hmb, p(self.src8), p(ref8), p(ref8), p(hp), p(hp))
+                            self.hip.hevc_b(2, *pargs, p(self.mv), 0, p(self.me_cost), 0, p(self.prev_mv), 0, 0, 0, 0, 0,
+                                            p(self.mvb[0]), p(self.dirb[0]), p(self.bcost), p(self.bbits), p(self.qp),
+                                            p(self.mb_aq), s, 0, int(self.p.max_merge))
+                            for it in range(int(self.p.merge_refine)):
+                                i_, o_ = it % 2, (it + 1) % 2
+                                self.hip.hevc_b(1, *pargs, 0, 0, 0, 0, 0, 0, tm_, td_, p(self.mvb[i_]), p(self.dirb[i_]),
+                                                p(self.mvb[o_]), p(self.dirb[o_]), p(self.bcost), p(self.bbits),
+                                                p(self.qp), p(self.mb_aq), s, 0, int(self.p.max_merge))
+                            fin = int(self.p.merge_refine) % 2
+                            self.me_cost.copy_(self.bcost)
+                            self.mv.copy_(self.mvb[fin][..., 0:2])
+                            inter_kw = dict(mvb=p(self.mvb[fin]), dirb=p(self.dirb[fin]), f1y=p(ref[0]), f1u=p(ref[1]),
+                                            f1v=p(ref[2]))
+                        else:
+                            for it in range(int(self.p.merge_refine)):
+                                a_, b_ = (self.mv, self.mv_tmp) if it % 2 == 0 else (self.mv_tmp, self.mv)
+                                self.hip.hevc_merge_refine(B, self.wmb, self.hmb, p(self.src8), p(ref8), p(hp), p(a_),
+                                                           p(b_), p(self.me_cost), p(self.prev_mv), p(self.qp),
+                                                           p(self.mb_aq), s)
+                            if int(self.p.merge_refine) % 2:
+                                self.mv.copy_(self.mv_tmp)
                 else:
                     ref8b, hpb = self.ref8s[r1], self.me_hps[r1]
                     with st("me_b"):
-                        self._temporal_candidates(pic)
+                        self._temporal_candidates(pic, ref_lists[pic.l1])
                         self.hip.me(B, self.wmb, self.hmb, p(self.src8), p(ref8), p(self.pm0), p(self.mv),
                                     p(self.me_cost), p(self.me_pred), p(self.me_intra), p(self.qp), self.p.me_range,
                                     self.p.subpel, s, p(hp), p(self.mb_aq), 1)
@@ -515,13 +579,13 @@ class GpuHevcEncoder:
                         bargs = (B, self.wmb, self.hmb, p(self.src8), p(ref8), p(ref8b), p(hp), p(hpb))
                         self.hip.hevc_b(0, *bargs, p(self.mv), p(self.mv1), p(self.me_cost), p(self.me_cost1),
                                         p(self.pm0), p(self.pm1), 0, 0, 0, 0, p(self.mvb[0]), p(self.dirb[0]),
-                                        p(self.bcost), p(self.bbits), p(self.qp), p(self.mb_aq), s)
+                                        p(self.bcost), p(self.bbits), p(self.qp), p(self.mb_aq), s, 1, int(self.p.max_merge))
                         tm_, td_ = (p(self.tmv), p(self.tdir)) if tmvp else (0, 0)
                         for it in range(int(self.p.merge_refine)):
                             i_, o_ = it % 2, (it + 1) % 2
                             self.hip.hevc_b(1, *bargs, 0, 0, 0, 0, 0, 0, tm_, td_, p(self.mvb[i_]), p(self.dirb[i_]),
                                             p(self.mvb[o_]), p(self.dirb[o_]), p(self.bcost), p(self.bbits), p(self.qp),
-                                            p(self.mb_aq), s)
+                                            p(self.mb_aq), s, 1, int(self.p.max_merge))
                         fin = int(self.p.merge_refine) % 2
                         self.me_cost.copy_(self.bcost)
                     r1p = self.rec[r1]
@@ -559,18 +623,18 @@ class GpuHevcEncoder:
                                       p(self.ctu), p(self.ctb_qp), p(self.run), 1, s)
                 self.dbk = cur
                 self.rec[ci] = cur = out_pl
-            if pic.kind != "B":
-                # the anchor's 8-bit proxy and half-sample planes (shared by every picture that
-                # references it) and, for the B pictures after it, its motion as the col field
-                a8 = pic.anchor & 1
+            if pic.ref:
+                # a reference picture's 8-bit proxy and half-sample planes (shared by every
+                # picture that references it) and its motion as a collocated field
                 with st("halfpel"):
-                    self.hip.hevc_proxy8(p(cur[0]), p(self.ref8s[a8]), cur[0].numel(), bd - 8, s)
-                    self.hip.me_halfpel(B, self.W, self.H, p(self.ref8s[a8]), p(self.me_hps[a8]), s)
-                if self.nb:
+                    self.hip.hevc_proxy8(p(cur[0]), p(self.ref8s[ci]), cur[0].numel(), bd - 8, s)
+                    self.hip.me_halfpel(B, self.W, self.H, p(self.ref8s[ci]), p(self.me_hps[ci]), s)
+                ref_lists[d] = (pic.l0, pic.l1)
+                if tmvp:
                     if idr:
-                        self.col_inter.zero_()
+                        self.col_dir[ci].zero_()
                     else:
-                        self._store_col()
+                        self._store_col(ci)
             if metrics:
                 dd = (cur[0][:, :h, :w].to(torch.int32) - self.src[0][:, :h, :w].to(torch.int32))
                 sse.append((dd * dd).sum(dim=(1, 2)).to(torch.float64))
@@ -611,7 +675,7 @@ class GpuHevcEncoder:
                 tj = time.perf_counter()
                 # POC counts display pictures from the latest IDR
                 base = dict(idr=int(pic.kind == "I"), poc=pic.d - i0, slice_type={"I": 2, "P": 1, "B": 0}[pic.kind],
-                            nal_ref=int(pic.kind != "B"))
+                            nal_ref=int(pic.ref), rps=[(rd - i0, int(u)) for rd, u in pic.rps])
                 if pic.kind != "I":
                     base["ref_poc0"] = pic.l0 - i0
                 if pic.kind == "B":
@@ -620,18 +684,28 @@ class GpuHevcEncoder:
                 if tmvp and pic.kind != "I":
                     cd = pic.l1 if pic.kind == "B" else pic.l0
                     col = anchor_cu[cd]
-                    base.update(col_poc=cd - i0, col_ref_poc0=col[1] - i0, col_ref_poc1=col[1] - i0)
+                    base.update(col_poc=cd - i0, col_ref_poc0=col[1] - i0, col_ref_poc1=col[2] - i0)
                 fps = []
                 for b in range(B):
                     fp = dict(base, qp=int(qcol[b]))
                     if col is not None:
                         fp["col_cu"] = None if col[0] is None else col[0][b]
                     fps.append(fp)
-                r = self.host.hevc_write_slices_packed(cfg, fps, ctu, cu, nz, off, lv, self.entropy_threads)
-                if tmvp and pic.kind != "B":
-                    # the next pictures' collocated records (the host buffer set is reused at t + 3)
-                    anchor_cu[pic.d] = (None if pic.kind == "I" else cu[:B].copy(), pic.l0)
-                    for k in [k for k in anchor_cu if k < pic.l0]:
+                if self.cu_stats is None:
+                    r = self.host.hevc_write_slices_packed(cfg, fps, ctu, cu, nz, off, lv, self.entropy_threads)
+                else:  # diagnostics: CU mix per picture type (tools/diag/hevc_bframe_stats.py)
+                    rs = self.host.hevc_write_slices_packed(cfg, fps, ctu, cu, nz, off, lv, self.entropy_threads, True)
+                    r = [n for n, _ in rs]
+                    agg = self.cu_stats.setdefault(pic.kind + ("ref" if pic.kind == "B" and pic.ref else ""), {})
+                    for _, stt in rs:
+                        for k_, v_ in stt.items():
+                            agg[k_] = agg.get(k_, 0) + v_
+                if tmvp and pic.ref:
+                    # later pictures' collocated records (the host buffer set is reused at t + 3);
+                    # only pictures still in the DPB can be collocated pictures
+                    anchor_cu[pic.d] = (None if pic.kind == "I" else cu[:B].copy(), pic.l0, pic.l1)
+                    live = {rd for rd, _ in pic.rps} | {pic.d}
+                    for k in [k for k in anchor_cu if k not in live]:
                         del anchor_cu[k]
                 cabac_s[0] += time.perf_counter() - tj
                 return r

@@ -151,33 +151,36 @@ def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp:
 
 
 def random_gop_stream(host, width: int, height: int, frames: int, bframes: int = 3, seed: int = 0, qp: int = 30,
-                      bit_depth: int = 8, tmvp: bool = True, host_cfg: dict | None = None, **kw) -> tuple[bytes, list]:
-    """Annex-B HEVC stream of one closed GOP with B pictures (models/gop.py coding order:
-    I, P anchors, non-reference B pictures referencing the anchors on both sides) from
-    random records; TMVP takes the collocated records of the anchors.  Returns the stream
-    and the records per *display* index (the decoder outputs pictures in POC order)."""
-    from ..models.gop import gop_plan
+                      bit_depth: int = 8, tmvp: bool = True, pyramid: bool = False, host_cfg: dict | None = None,
+                      **kw) -> tuple[bytes, list]:
+    """Annex-B HEVC stream of one closed GOP with B pictures (models/gop.py hevc_gop_plan:
+    I, P anchors, B pictures referencing the pictures on both sides; ``pyramid``: the middle
+    B of a run is a reference picture) from random records, with each picture's RPS; TMVP
+    takes the collocated picture's records.  Returns the stream and the records per
+    *display* index (the decoder outputs pictures in POC order)."""
+    from ..models.gop import hevc_gop_plan
 
     rng = np.random.default_rng(seed)
-    cfg = dict(width=width, height=height, bit_depth=bit_depth, bframes=bframes, tmvp=int(tmvp), **(host_cfg or {}))
+    cfg = dict(width=width, height=height, bit_depth=bit_depth, bframes=bframes, tmvp=int(tmvp), pyramid=int(pyramid),
+               **(host_cfg or {}))
     out = [host.hevc_parameter_sets(cfg)]
     recs: list = [None] * frames
-    anchor_cu: dict = {}    # display index -> (cu records or None for intra, L0 reference POC)
-    for pic in gop_plan(frames, bframes):
+    refs: dict = {}    # display index -> (cu records or None for intra, its L0 / L1 reference indices)
+    for pic in hevc_gop_plan(frames, bframes, pyramid):
         fqp = int(np.clip(qp + rng.integers(-3, 4), 0, 51))
         r = random_records(rng, width, height, pslice=pic.kind != "I", bit_depth=bit_depth, bslice=pic.kind == "B", **kw)
         fp = dict(idr=int(pic.kind == "I"), poc=pic.d, qp=fqp, slice_type={"I": 2, "P": 1, "B": 0}[pic.kind],
-                  nal_ref=int(pic.kind != "B"))
+                  nal_ref=int(pic.ref), rps=[(d, int(u)) for d, u in pic.rps])
         if pic.kind != "I":
             fp["ref_poc0"] = pic.l0
             col = pic.l1 if pic.kind == "B" else pic.l0
             if pic.kind == "B":
                 fp["ref_poc1"] = pic.l1
-            ccu, cref = anchor_cu[col]
-            fp.update(col_poc=col, col_ref_poc0=cref, col_ref_poc1=cref, col_cu=ccu)
+            ccu, c0, c1 = refs[col]
+            fp.update(col_poc=col, col_ref_poc0=c0, col_ref_poc1=c1, col_cu=ccu)
         nal, _ = host.hevc_write_slice(cfg, fp, *r)
-        if pic.kind != "B":
-            anchor_cu[pic.d] = (None if pic.kind == "I" else r[1].copy(), pic.l0)
+        if pic.ref:
+            refs[pic.d] = (None if pic.kind == "I" else r[1].copy(), pic.l0, pic.l1)
         out.append(nal)
         recs[pic.d] = r
     return b"".join(out), recs

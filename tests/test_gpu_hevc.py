@@ -74,18 +74,19 @@ def test_gpu_hevc_p_pictures_match_decoder(host, bd):
         assert sum(r.bits[1:]) / (r.frames - 1) < r.bits[0]   # P pictures are cheaper than the IDR
 
 
-@pytest.mark.parametrize("bd,tmvp", [(8, True), (10, True), (8, False)])
-def test_gpu_hevc_b_pictures_match_decoder(host, bd, tmvp):
+@pytest.mark.parametrize("bd,tmvp,pyramid", [(8, True, True), (10, True, True), (8, False, True), (8, True, False)])
+def test_gpu_hevc_b_pictures_match_decoder(host, bd, tmvp, pyramid):
     """x265-style GOP: I, P anchors every 4 pictures and non-reference B pictures between
     them (list 0 / list 1 / bi-predicted CUs, bi-prediction averaging at 14-bit precision,
     B-aware deblocking strengths, TMVP candidates from the collocated anchor).  The GPU
     reconstruction equals the CPU decoder's, every inter direction occurs, and the B
-    pictures cost less than the P anchors."""
-    res, rec = _encode(192, 128, 9, 2, bd=bd, crf=None, qp=28, bframes=3, tmvp=tmvp)
+    pictures cost less than the P anchors.  ``pyramid``: the middle B is a reference picture
+    (coded first, at half the B QP offset) for the b pictures beside it."""
+    res, rec = _encode(192, 128, 9, 2, bd=bd, crf=None, qp=28, bframes=3, tmvp=tmvp, pyramid=pyramid)
     _compare(host, res, rec)
     dirs = set()
     for r in res:
-        assert r.order == [0, 4, 1, 2, 3, 8, 5, 6, 7]
+        assert r.order == ([0, 4, 2, 1, 3, 8, 6, 5, 7] if pyramid else [0, 4, 1, 2, 3, 8, 5, 6, 7])
         pics = host.hevc_decode(r.bitstream)
         for p in pics:
             inter = p["cu"][:, 0] == 1

@@ -233,17 +233,21 @@ def test_hevc_short_merge_lists(host, max_merge):
         assert np.array_equal(p["cu"][inter, 4:8], cu[inter, 4:8])
 
 
-@pytest.mark.parametrize("seed,tmvp,max_merge,wpp", [(0, 0, 3, 0), (1, 1, 3, 1), (2, 1, 5, 0), (3, 1, 1, 1), (4, 0, 5, 1)])
-def test_hevc_b_gop_roundtrip(host, seed, tmvp, max_merge, wpp):
+@pytest.mark.parametrize("seed,tmvp,max_merge,wpp,pyramid", [(0, 0, 3, 0, 0), (1, 1, 3, 1, 0), (2, 1, 5, 0, 1),
+                                                               (3, 1, 1, 1, 1), (4, 0, 5, 1, 1), (5, 1, 3, 0, 1)])
+def test_hevc_b_gop_roundtrip(host, seed, tmvp, max_merge, wpp, pyramid):
     """B pictures (x265 --bframes): I, P anchors and non-reference B slices predicting from
     list 0, list 1 or both, with explicit slice RPS, TRAIL_N NAL units and (tmvp) temporal
     merge / AMVP candidates from the collocated anchor's records.  Vectors come from a small
     pool so spatial, temporal, combined bi-predictive and zero merge candidates all match;
-    the decoder must recover every direction and vector in display order."""
+    the decoder must recover every direction and vector in display order.  ``pyramid``: the
+    middle B of each run is a reference picture (RPS entries kept but unused, a B picture as
+    the collocated picture of the b pictures around it)."""
     from govideocompressor_amd.utils.hevc_synth import random_gop_stream
 
     s, recs = random_gop_stream(host, 128, 96, 9, bframes=3, seed=seed, tmvp=bool(tmvp), mv_pool=3 if seed % 2 else 0,
-                                intra_in_p=0.05, density=0.02, host_cfg=dict(max_merge=max_merge, wpp=wpp))
+                                intra_in_p=0.05, density=0.02, host_cfg=dict(max_merge=max_merge, wpp=wpp),
+                                pyramid=bool(pyramid))
     pics = host.hevc_decode(s)
     assert len(pics) == 9
     for d, (p, (ctu, cu, cy, cb, cr)) in enumerate(zip(pics, recs)):

@@ -158,6 +158,10 @@ def test_ffargs_profile_tune_level_params():
     assert ffargs.parse("-vcodec libx265 -x265-params crf=22").crf == 22.0
     assert ffargs.parse("-vcodec libx265 -profile:v mainstillpicture").opts == {"intra_only": True}
     assert ffargs.parse("-vcodec libx265 -tune fastdecode").opts == {"deblock": False, "sao": False}
+    # x265's own B-picture structure on request (bframes 4 with a reference-B pyramid, TMVP)
+    p = ffargs.parse("-vcodec libx265 -x265-params bframes=4:b-pyramid=1:tmvp=1").apply_opts(HevcParams(64, 64))
+    assert (p.bframes, p.pyramid, p.tmvp, p.eff_bframes()) == (4, True, True, 4)
+    assert ffargs.parse("-vcodec libx265 -tune zerolatency").apply_opts(HevcParams(64, 64)).eff_bframes() == 0
 
 
 def test_ffargs_strict_rejections():
@@ -166,7 +170,7 @@ def test_ffargs_strict_rejections():
                 "-vcodec libx264 -profile:v high444", "-vcodec libx265 -profile:v main12",
                 "-vcodec libx264 -x264-params ref=3", "-vcodec libx264 -x264-params weightp=2",
                 "-vcodec libx264 -x264-params foo=1", "-vcodec libx264 -x265-params sao=0",
-                "-vcodec libx265 -x265-params bframes=4", "-vcodec libx265 -x265-params ctu=64",
+                "-vcodec libx265 -x265-params bframes=9", "-vcodec libx265 -x265-params ctu=16",
                 "-vcodec libx264 -x264-params aq-mode=2", "-vcodec libx264 -x264-params deblock=1,1",
                 "-vcodec libx264 -profile:v baseline -x264-params bframes=3", "-vcodec libx264 -level 9",
                 "-vcodec libx265 -profile:v main -pix_fmt yuv420p10le", "-vcodec copy -tune psnr"):
