@@ -98,6 +98,7 @@ struct BDecideArgs {
   MbHeader* hdr;                   // out: kind / ref / mv
   uint8_t* pred_out;               // out: [B, nmb, 256]
   int* cost_out;                   // out: [B, nmb] the winner's cost (vs the intra estimate)
+  int w1;                          // implicit bi-prediction weight of list 1 (32: plain average)
 };
 
 // Quarter-sample luma position (xf, yf) = two (plane, du, dv) taps averaged (the G/b/h/j
@@ -111,6 +112,20 @@ __constant__ int8_t kQTap[16][2][3] = {
 };
 
 __device__ __forceinline__ uint32_t avg4b(uint32_t a, uint32_t b) { return (a | b) - (((a ^ b) >> 1) & 0x7F7F7F7Fu); }
+
+// implicit weighted bi-prediction of 4 packed samples (8.4.2.3.2 with logWD 5, offsets 0):
+// (a * (64 - w1) + b * w1 + 32) >> 6; w1 = 32 is the plain rounded average
+__device__ __forceinline__ uint32_t wavg4b(uint32_t a, uint32_t b, int w1) {
+  if (w1 == 32) return avg4b(a, b);
+  const int w0 = 64 - w1;
+  uint32_t o = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int v = (static_cast<int>((a >> (8 * k)) & 255u) * w0 + static_cast<int>((b >> (8 * k)) & 255u) * w1 + 32) >> 6;
+    o |= static_cast<uint32_t>(clampi(v, 0, 255)) << (8 * k);
+  }
+  return o;
+}
 
 // 4 consecutive samples (u .. u+3, v) of one plane; coordinates clamp to the plane's
 // extension (integer plane: the picture; half-sample planes: their 4-sample margin)
@@ -177,9 +192,9 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   const int m0x = a.mv0[o * 2], m0y = a.mv0[o * 2 + 1], m1x = a.mv1[o * 2], m1y = a.mv1[o * 2 + 1];
   const uint32_t src = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y) * W + X);
   // direct: per-quadrant vectors of both lists; bi: the two ME vectors
-  const uint32_t pd = avg4b(mc4(G0, H0, W, H, X, Y, dm[q * 2], dm[q * 2 + 1]),
-                            mc4(G1, H1, W, H, X, Y, dm[8 + q * 2], dm[8 + q * 2 + 1]));
-  const uint32_t pb = avg4b(mc4(G0, H0, W, H, X, Y, m0x, m0y), mc4(G1, H1, W, H, X, Y, m1x, m1y));
+  const uint32_t pd = wavg4b(mc4(G0, H0, W, H, X, Y, dm[q * 2], dm[q * 2 + 1]),
+                             mc4(G1, H1, W, H, X, Y, dm[8 + q * 2], dm[8 + q * 2 + 1]), a.w1);
+  const uint32_t pb = wavg4b(mc4(G0, H0, W, H, X, Y, m0x, m0y), mc4(G1, H1, W, H, X, Y, m1x, m1y), a.w1);
   __shared__ int s_res[2][256];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -879,8 +894,9 @@ extern "C" void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src
                                      const int16_t* mv1, const int* cost0, const int* cost1, const uint8_t* pred0,
                                      const uint8_t* pred1, const int16_t* pm0, const int16_t* pm1, const int16_t* dmv,
                                      const int* qp, const int8_t* aq, void* hdr, uint8_t* pred_out, int* cost_out,
-                                     void* stream) {
+                                     void* stream, int w1) {
   BDecideArgs a;
+  a.w1 = w1;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.src_y = src_y;
   a.ref0 = ref0;

@@ -33,7 +33,7 @@ void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src_y, const u
                           const uint8_t* hp0, const uint8_t* hp1, const int16_t* mv0, const int16_t* mv1,
                           const int* cost0, const int* cost1, const uint8_t* pred0, const uint8_t* pred1,
                           const int16_t* pm0, const int16_t* pm1, const int16_t* dmv, const int* qp, const int8_t* aq,
-                          void* hdr, uint8_t* pred_out, int* cost_out, void* stream);
+                          void* hdr, uint8_t* pred_out, int* cost_out, void* stream, int w1);
 void mivc_launch_aq_offsets(int B, int wmb, int hmb, const uint8_t* sy, const uint8_t* su, const uint8_t* sv,
                             float strength, const float* extra, long long extra_stride, int8_t* out, void* stream);
 void mivc_launch_mbtree(int B, int F, int lbw, int lbh, const int* blk_cost, const int* blk_mv, void* prop,
@@ -47,7 +47,7 @@ void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t* src_y, con
                               const int16_t* mv, const int* me_cost, const int* intra_cost, const int* qp,
                               int chroma_qp_offset, void* hdr, int16_t* coef, uint8_t* nz, uint8_t* intra_flag,
                               int* intra_count, const int8_t* aq, const uint8_t* ref1_u, const uint8_t* ref1_v,
-                              int bmode, int t8, const int16_t* mv8, void* stream);
+                              int bmode, int t8, const int16_t* mv8, void* stream, int w1);
 void mivc_launch_p_part8(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref, const uint8_t* hp,
                          const int16_t* mv, const int16_t* pm, int* cost, uint8_t* pred, int16_t* mv8, const int* qp,
                          const int8_t* aq, int overhead, int min_satd, void* stream);
@@ -55,7 +55,7 @@ void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t* src_y, con
                               const uint8_t* src_v, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const int* qp,
                               int chroma_qp_offset, void* hdr, int16_t* coef, uint8_t* nz,
                               const uint8_t* intra_flag, const int* intra_count, int* err, int use_i4x4,
-                              const int8_t* aq, void* stream);
+                              const int8_t* aq, void* stream, int use_i8x8);
 void mivc_launch_deblock(int B, int wmb, int hmb, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const void* hdr,
                          const uint8_t* nz, int chroma_qp_offset, int alpha_off, int beta_off, int* err,
                          void* stream);
@@ -186,12 +186,16 @@ PYBIND11_MODULE(_hip, m) {
   m.def("b_decide", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref0, uintptr_t ref1, uintptr_t hp0,
                        uintptr_t hp1, uintptr_t mv0, uintptr_t mv1, uintptr_t cost0, uintptr_t cost1, uintptr_t pred0,
                        uintptr_t pred1, uintptr_t pm0, uintptr_t pm1, uintptr_t dmv, uintptr_t qp, uintptr_t aq,
-                       uintptr_t hdr, uintptr_t pred_out, uintptr_t cost_out, uintptr_t stream) {
+                       uintptr_t hdr, uintptr_t pred_out, uintptr_t cost_out, uintptr_t stream, int w1) {
+    if (w1 < -64 || w1 > 128) throw std::invalid_argument("b_decide: implicit weight w1 in -64..128");
     mivc_launch_b_decide(B, wmb, hmb, P<uint8_t>(src), P<uint8_t>(ref0), P<uint8_t>(ref1), P<uint8_t>(hp0),
                          P<uint8_t>(hp1), P<int16_t>(mv0), P<int16_t>(mv1), P<int>(cost0), P<int>(cost1),
                          P<uint8_t>(pred0), P<uint8_t>(pred1), P<int16_t>(pm0), P<int16_t>(pm1), P<int16_t>(dmv),
-                         P<int>(qp), P<int8_t>(aq), P<void>(hdr), P<uint8_t>(pred_out), P<int>(cost_out), S(stream));
-  });
+                         P<int>(qp), P<int8_t>(aq), P<void>(hdr), P<uint8_t>(pred_out), P<int>(cost_out), S(stream), w1);
+  }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("src"), py::arg("ref0"), py::arg("ref1"), py::arg("hp0"),
+     py::arg("hp1"), py::arg("mv0"), py::arg("mv1"), py::arg("cost0"), py::arg("cost1"), py::arg("pred0"),
+     py::arg("pred1"), py::arg("pm0"), py::arg("pm1"), py::arg("dmv"), py::arg("qp"), py::arg("aq"), py::arg("hdr"),
+     py::arg("pred_out"), py::arg("cost_out"), py::arg("stream"), py::arg("w1") = 32);
   m.def("aq_offsets", [](int B, int wmb, int hmb, uintptr_t sy, uintptr_t su, uintptr_t sv, float strength,
                          uintptr_t out, uintptr_t stream, uintptr_t extra, long long extra_stride) {
     mivc_launch_aq_offsets(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), strength, P<float>(extra),
@@ -216,19 +220,20 @@ PYBIND11_MODULE(_hip, m) {
            uintptr_t fv, uintptr_t ry, uintptr_t ru, uintptr_t rv, uintptr_t pred, uintptr_t mv, uintptr_t me_cost,
            uintptr_t intra_cost, uintptr_t qp, int cqo, uintptr_t hdr, uintptr_t coef, uintptr_t nz,
            uintptr_t intra_flag, uintptr_t intra_count, uintptr_t stream, uintptr_t aq, uintptr_t ref1_u,
-           uintptr_t ref1_v, int bmode, int t8, uintptr_t mv8) {
+           uintptr_t ref1_v, int bmode, int t8, uintptr_t mv8, int w1) {
           if (bmode && (!ref1_u || !ref1_v)) throw std::invalid_argument("encode_inter: B mode needs the list-1 chroma");
           mivc_launch_encode_inter(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), P<uint8_t>(fy),
                                    P<uint8_t>(fu), P<uint8_t>(fv), P<uint8_t>(ry), P<uint8_t>(ru), P<uint8_t>(rv),
                                    P<uint8_t>(pred), P<int16_t>(mv), P<int>(me_cost), P<int>(intra_cost), P<int>(qp),
                                    cqo, P<void>(hdr), P<int16_t>(coef), P<uint8_t>(nz), P<uint8_t>(intra_flag),
                                    P<int>(intra_count), P<int8_t>(aq), P<uint8_t>(ref1_u), P<uint8_t>(ref1_v), bmode,
-                                   t8, P<int16_t>(mv8), S(stream));
+                                   t8, P<int16_t>(mv8), S(stream), w1);
         }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("sy"), py::arg("su"), py::arg("sv"), py::arg("fy"),
         py::arg("fu"), py::arg("fv"), py::arg("ry"), py::arg("ru"), py::arg("rv"), py::arg("pred"), py::arg("mv"),
         py::arg("me_cost"), py::arg("intra_cost"), py::arg("qp"), py::arg("cqo"), py::arg("hdr"), py::arg("coef"),
         py::arg("nz"), py::arg("intra_flag"), py::arg("intra_count"), py::arg("stream"), py::arg("aq") = 0,
-        py::arg("ref1_u") = 0, py::arg("ref1_v") = 0, py::arg("bmode") = 0, py::arg("t8") = 0, py::arg("mv8") = 0);
+        py::arg("ref1_u") = 0, py::arg("ref1_v") = 0, py::arg("bmode") = 0, py::arg("t8") = 0, py::arg("mv8") = 0,
+        py::arg("w1") = 32);
   m.def("p_part8", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref, uintptr_t hp, uintptr_t mv, uintptr_t pm,
                       uintptr_t cost, uintptr_t pred, uintptr_t mv8, uintptr_t qp, uintptr_t aq, int overhead,
                       int min_satd, uintptr_t stream) {
@@ -240,15 +245,15 @@ PYBIND11_MODULE(_hip, m) {
   m.def("encode_intra", [](int B, int wmb, int hmb, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t ry,
                            uintptr_t ru, uintptr_t rv, uintptr_t qp, int cqo, uintptr_t hdr, uintptr_t coef,
                            uintptr_t nz, uintptr_t intra_flag, uintptr_t intra_count, uintptr_t err, int use_i4x4,
-                           uintptr_t stream, uintptr_t aq) {
+                           uintptr_t stream, uintptr_t aq, int use_i8x8) {
     mivc_launch_encode_intra(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), P<uint8_t>(ry),
                              P<uint8_t>(ru), P<uint8_t>(rv), P<int>(qp), cqo, P<void>(hdr), P<int16_t>(coef),
                              P<uint8_t>(nz), P<uint8_t>(intra_flag), P<int>(intra_count), P<int>(err), use_i4x4,
-                             P<int8_t>(aq), S(stream));
+                             P<int8_t>(aq), S(stream), use_i8x8);
   }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("sy"), py::arg("su"), py::arg("sv"), py::arg("ry"),
      py::arg("ru"), py::arg("rv"), py::arg("qp"), py::arg("cqo"), py::arg("hdr"), py::arg("coef"), py::arg("nz"),
      py::arg("intra_flag"), py::arg("intra_count"), py::arg("err"), py::arg("use_i4x4"), py::arg("stream"),
-     py::arg("aq") = 0);
+     py::arg("aq") = 0, py::arg("use_i8x8") = 0);
   m.def("deblock", [](int B, int wmb, int hmb, uintptr_t ry, uintptr_t ru, uintptr_t rv, uintptr_t hdr, uintptr_t nz,
                       int cqo, int alpha_off, int beta_off, uintptr_t err, uintptr_t stream) {
     mivc_launch_deblock(B, wmb, hmb, P<uint8_t>(ry), P<uint8_t>(ru), P<uint8_t>(rv), P<void>(hdr), P<uint8_t>(nz),

@@ -23,7 +23,7 @@
 //
 // Reference parity: the reference decodes with ffmpeg inside the worker
 // (client.go:115-118); the CPU decoder (h264_decoder.cc) is the bit-exact oracle.
-#include "kcommon.h"
+#include "h264_t8.h"
 #include "../common/h264_cabac_tables.h"
 
 namespace mivc {
@@ -128,25 +128,6 @@ __device__ __forceinline__ int level_scale8(int m, int x, int y) {
 }
 
 // one 8-point pass of the 8x8 inverse transform (8.5.13.2), in place, stride s
-__device__ __forceinline__ void idct8_pass(int* d, int s) {
-  const int d0 = d[0], d1 = d[s], d2 = d[2 * s], d3 = d[3 * s], d4 = d[4 * s], d5 = d[5 * s], d6 = d[6 * s],
-            d7 = d[7 * s];
-  const int a0 = d0 + d4, a4 = d0 - d4, a2 = (d2 >> 1) - d6, a6 = d2 + (d6 >> 1);
-  const int b0 = a0 + a6, b2 = a4 + a2, b4 = a4 - a2, b6 = a0 - a6;
-  const int a1 = -d3 + d5 - d7 - (d7 >> 1);
-  const int a3 = d1 + d7 - d3 - (d3 >> 1);
-  const int a5 = -d1 + d7 + d5 + (d5 >> 1);
-  const int a7 = d3 + d5 + d1 + (d1 >> 1);
-  const int b1 = a1 + (a7 >> 2), b7 = a7 - (a1 >> 2), b3 = a3 + (a5 >> 2), b5 = (a3 >> 2) - a5;
-  d[0] = b0 + b7;
-  d[s] = b2 + b5;
-  d[2 * s] = b4 + b3;
-  d[3 * s] = b6 + b1;
-  d[4 * s] = b6 - b1;
-  d[5 * s] = b4 - b3;
-  d[6 * s] = b2 - b5;
-  d[7 * s] = b0 - b7;
-}
 
 // weighted sample prediction of one sample (8.4.2.3); r0 / r1 = ref_idx (-1: list unused)
 __device__ __forceinline__ int weigh(const int16_t* w, bool chroma, int comp, int r0, int r1, int p0, int p1) {
@@ -376,46 +357,6 @@ struct DecIntraShared {
 };
 
 // Intra_8x8 sample (8.3.2.2.2 .. 8.3.2.2.10) from the filtered references ft / fl / ftl
-__device__ __forceinline__ int i8_pred_sample(int mode, int x, int y, const int* ft, const int* fl, int ftl, int dc) {
-  auto T = [&](int i) { return i < 0 ? ftl : ft[i]; };
-  auto L = [&](int i) { return i < 0 ? ftl : fl[i]; };
-  switch (mode) {
-    case 0: return ft[x];
-    case 1: return fl[y];
-    case 2: return dc;
-    case 3:
-      if (x == 7 && y == 7) return (ft[14] + 3 * ft[15] + 2) >> 2;
-      return (T(x + y) + 2 * T(x + y + 1) + T(x + y + 2) + 2) >> 2;
-    case 4:
-      if (x > y) return (T(x - y - 2) + 2 * T(x - y - 1) + T(x - y) + 2) >> 2;
-      if (x < y) return (L(y - x - 2) + 2 * L(y - x - 1) + L(y - x) + 2) >> 2;
-      return (T(0) + 2 * ftl + L(0) + 2) >> 2;
-    case 5: {
-      const int z = 2 * x - y;
-      if (z >= 0 && (z & 1) == 0) return (T(x - (y >> 1) - 1) + T(x - (y >> 1)) + 1) >> 1;
-      if (z >= 0) return (T(x - (y >> 1) - 2) + 2 * T(x - (y >> 1) - 1) + T(x - (y >> 1)) + 2) >> 2;
-      if (z == -1) return (L(0) + 2 * ftl + T(0) + 2) >> 2;
-      return (L(y - 2 * x - 1) + 2 * L(y - 2 * x - 2) + L(y - 2 * x - 3) + 2) >> 2;
-    }
-    case 6: {
-      const int z = 2 * y - x;
-      if (z >= 0 && (z & 1) == 0) return (L(y - (x >> 1) - 1) + L(y - (x >> 1)) + 1) >> 1;
-      if (z >= 0) return (L(y - (x >> 1) - 2) + 2 * L(y - (x >> 1) - 1) + L(y - (x >> 1)) + 2) >> 2;
-      if (z == -1) return (L(0) + 2 * ftl + T(0) + 2) >> 2;
-      return (T(x - 2 * y - 1) + 2 * T(x - 2 * y - 2) + T(x - 2 * y - 3) + 2) >> 2;
-    }
-    case 7:
-      if ((y & 1) == 0) return (T(x + (y >> 1)) + T(x + (y >> 1) + 1) + 1) >> 1;
-      return (T(x + (y >> 1)) + 2 * T(x + (y >> 1) + 1) + T(x + (y >> 1) + 2) + 2) >> 2;
-    default: {
-      const int z = x + 2 * y;
-      if (z < 13 && (z & 1) == 0) return (L(y + (x >> 1)) + L(y + (x >> 1) + 1) + 1) >> 1;
-      if (z < 13) return (L(y + (x >> 1)) + 2 * L(y + (x >> 1) + 1) + L(y + (x >> 1) + 2) + 2) >> 2;
-      if (z == 13) return (L(6) + 3 * L(7) + 2) >> 2;
-      return L(7);
-    }
-  }
-}
 
 __device__ __forceinline__ void decode_intra_mb(const DecodeArgs& a, DecIntraShared& S, int slot, int mx, int my) {
   const Geom& g = a.g;

@@ -9,7 +9,7 @@
 //     reconstruction written here is exactly what a decoder produces.
 // SURVEY.md K-C8.  One wave64 per macroblock: lanes 0-15 luma 4x4 blocks,
 // lanes 16-23 chroma 4x4 blocks (two MBs per wave, see encode_inter_mb).
-#include "kcommon.h"
+#include "h264_t8.h"
 
 namespace mivc {
 namespace gpu {
@@ -39,77 +39,10 @@ struct InterArgs {
   // (list 1), averaged for bi-prediction; pred_y is b_decide's luma prediction
   const uint8_t *ref1_u, *ref1_v;
   int bmode;
+  int w1;                  // B pictures: implicit bi-prediction weight of list 1 (32: average)
   int t8;                  // High profile: choose the 8x8 transform per MB (sa8d < satd, as x264)
 };
 
-// ---------------------------------------------------------------- 8x8 transform (High)
-// position class of an 8x8 coefficient (normAdjust8x8 / quant8 column, 8.5.9)
-__device__ __forceinline__ int pos8(int x, int y) {
-  if ((x & 3) == 0 && (y & 3) == 0) return 0;
-  if ((x & 1) && (y & 1)) return 1;
-  if ((x & 3) == 2 && (y & 3) == 2) return 2;
-  if (((x & 3) == 0 && (y & 1)) || ((x & 1) && (y & 3) == 0)) return 3;
-  if (((x & 3) == 0 && (y & 3) == 2) || ((x & 3) == 2 && (y & 3) == 0)) return 4;
-  return 5;
-}
-__constant__ int kQuant8MF[6][6] = {{13107, 11428, 20972, 12222, 16777, 15481}, {11916, 10826, 19174, 11058, 14980, 14290},
-                                   {10082, 8943, 15978, 9675, 12710, 11985},   {9362, 8228, 14913, 8931, 11984, 11259},
-                                   {8192, 7346, 13159, 7740, 10486, 9777},     {7282, 6428, 11570, 6830, 9118, 8640}};
-__constant__ int kNorm8[6][6] = {{20, 18, 32, 19, 25, 24}, {22, 19, 35, 21, 28, 26}, {26, 23, 42, 24, 33, 31},
-                                {28, 25, 45, 26, 35, 33}, {32, 28, 51, 30, 40, 38}, {36, 32, 58, 34, 46, 43}};
-__constant__ uint8_t kZz8[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
-                                 41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
-                                 30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
-
-// forward 8-point core transform (the inverse of 8.5.13.2), in place, stride s
-__device__ __forceinline__ void dct8_pass(int* d, int s) {
-  const int a0 = d[0] + d[7 * s], a1 = d[s] + d[6 * s], a2 = d[2 * s] + d[5 * s], a3 = d[3 * s] + d[4 * s];
-  const int a4 = d[0] - d[7 * s], a5 = d[s] - d[6 * s], a6 = d[2 * s] - d[5 * s], a7 = d[3 * s] - d[4 * s];
-  const int b0 = a0 + a3, b1 = a1 + a2, b2 = a0 - a3, b3 = a1 - a2;
-  const int b4 = a5 + a6 + ((a4 >> 1) + a4), b5 = a4 - a7 - ((a6 >> 1) + a6);
-  const int b6 = a4 + a7 - ((a5 >> 1) + a5), b7 = a5 - a6 + ((a7 >> 1) + a7);
-  d[0] = b0 + b1;
-  d[4 * s] = b0 - b1;
-  d[2 * s] = b2 + (b3 >> 1);
-  d[6 * s] = (b2 >> 1) - b3;
-  d[s] = b4 + (b7 >> 2);
-  d[7 * s] = (b4 >> 2) - b7;
-  d[3 * s] = b5 + (b6 >> 2);
-  d[5 * s] = b6 - (b5 >> 2);
-}
-// inverse 8-point pass (8.5.13.2), in place, stride s
-__device__ __forceinline__ void idct8_pass(int* d, int s) {
-  const int d0 = d[0], d1 = d[s], d2 = d[2 * s], d3 = d[3 * s], d4 = d[4 * s], d5 = d[5 * s], d6 = d[6 * s],
-            d7 = d[7 * s];
-  const int a0 = d0 + d4, a4 = d0 - d4, a2 = (d2 >> 1) - d6, a6 = d2 + (d6 >> 1);
-  const int b0 = a0 + a6, b2 = a4 + a2, b4 = a4 - a2, b6 = a0 - a6;
-  const int a1 = -d3 + d5 - d7 - (d7 >> 1), a3 = d1 + d7 - d3 - (d3 >> 1);
-  const int a5 = -d1 + d7 + d5 + (d5 >> 1), a7 = d3 + d5 + d1 + (d1 >> 1);
-  const int b1 = a1 + (a7 >> 2), b7 = a7 - (a1 >> 2), b3 = a3 + (a5 >> 2), b5 = (a3 >> 2) - a5;
-  d[0] = b0 + b7;
-  d[s] = b2 + b5;
-  d[2 * s] = b4 + b3;
-  d[3 * s] = b6 + b1;
-  d[4 * s] = b6 - b1;
-  d[5 * s] = b4 - b3;
-  d[6 * s] = b2 - b5;
-  d[7 * s] = b0 - b7;
-}
-// 8-point Hadamard pass (sa8d), in place, stride s
-__device__ __forceinline__ void had8_pass(int* d, int s) {
-  const int a0 = d[0] + d[s], a1 = d[0] - d[s], a2 = d[2 * s] + d[3 * s], a3 = d[2 * s] - d[3 * s];
-  const int a4 = d[4 * s] + d[5 * s], a5 = d[4 * s] - d[5 * s], a6 = d[6 * s] + d[7 * s], a7 = d[6 * s] - d[7 * s];
-  const int b0 = a0 + a2, b1 = a1 + a3, b2 = a0 - a2, b3 = a1 - a3;
-  const int b4 = a4 + a6, b5 = a5 + a7, b6 = a4 - a6, b7 = a5 - a7;
-  d[0] = b0 + b4;
-  d[s] = b1 + b5;
-  d[2 * s] = b2 + b6;
-  d[3 * s] = b3 + b7;
-  d[4 * s] = b0 - b4;
-  d[5 * s] = b1 - b5;
-  d[6 * s] = b2 - b6;
-  d[7 * s] = b3 - b7;
-}
 
 // Eighth-sample chroma prediction (clause 8.4.2.2.2) of a 4x4 block at (px0, py0) of a
 // cw x ch plane with vector (mvx, mvy) (quarter-luma = eighth-chroma units).
@@ -399,7 +332,8 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
 #pragma unroll
       for (int y = 0; y < 4; ++y)
 #pragma unroll
-        for (int x = 0; x < 4; ++x) pv[y][x] = u0 ? (u1 ? (pv[y][x] + p1[y][x] + 1) >> 1 : pv[y][x]) : p1[y][x];
+        for (int x = 0; x < 4; ++x)  // implicit weights (a.w1 = 32: the plain average)
+          pv[y][x] = u0 ? (u1 ? h264::clip1((pv[y][x] * (64 - a.w1) + p1[y][x] * a.w1 + 32) >> 6) : pv[y][x]) : p1[y][x];
     }
     uint32_t sw[4];
 #pragma unroll
@@ -594,8 +528,9 @@ extern "C" void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t*
                                          const int* intra_cost, const int* qp, int chroma_qp_offset, void* hdr,
                                          int16_t* coef, uint8_t* nz, uint8_t* intra_flag, int* intra_count,
                                          const int8_t* aq, const uint8_t* ref1_u, const uint8_t* ref1_v, int bmode,
-                                         int t8, const int16_t* mv8, void* stream) {
+                                         int t8, const int16_t* mv8, void* stream, int w1) {
   InterArgs a;
+  a.w1 = w1;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.src_y = src_y;
   a.src_u = src_u;

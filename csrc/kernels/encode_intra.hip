@@ -8,7 +8,7 @@
 //
 // For P frames only MBs flagged by encode_inter (intra_flag) are coded here; the
 // others were reconstructed by encode_inter and only advance the row counter.
-#include "kcommon.h"
+#include "h264_t8.h"
 #include "../common/h264_i4_taps.h"
 
 namespace mivc {
@@ -40,6 +40,7 @@ struct IntraArgs {
   const int* intra_count;     // [B] (P frames)
   int* err;
   int use_i4x4;
+  int use_i8x8;  // High profile: Intra8x8 trial (x264 --partitions i8x8, with --8x8dct)
 };
 
 constexpr int TS = kTileStride;
@@ -71,6 +72,16 @@ struct IntraShared {
   uint8_t saved_y[16];
   uint8_t saved_c[2][8];
   int saved_modes[4];
+  // Intra8x8 trial (High profile)
+  uint8_t t8[17 * TS];     // I8x8 trial reconstruction
+  uint8_t tr8[8];          // reconstructed row above the top-right MB (x = 16 .. 23)
+  int16_t c8[4][64];       // I8x8 trial levels (8x8 zig-zag order)
+  int e8t[16], e8l[8], e8tl;
+  int f8t[16], f8l[8], f8tl;
+  int h8[8][64];           // mode ranking: row Hadamards per (mode group, row, column)
+  int d8[64];              // transform buffer
+  uint8_t modes8[4];
+  uint8_t nz8;
 };
 
 // 4x4 intra prediction sample at compile-time (x, y) for a runtime mode
@@ -164,6 +175,10 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
     int x = X0 - 1 + lane;
     bool ok = my > 0 && x >= 0 && x < W && (lane < 17 || (mbav & h264::AV_TOPRIGHT));
     S.tile[lane] = ok ? recy[static_cast<size_t>(Y0 - 1) * W + x] : 0;
+  } else if (lane >= 21 && lane < 29) {  // top-right MB's bottom row x = X0+16 .. X0+23 (Intra8x8 block 1)
+    int x = X0 + 16 + lane - 21;
+    bool ok = (mbav & h264::AV_TOPRIGHT) && x < W;
+    S.tr8[lane - 21] = ok ? recy[static_cast<size_t>(Y0 - 1) * W + x] : 0;
   } else if (lane >= 32 && lane < 48) {  // tile col 0, rows 1..16
     int r = lane - 32;
     uint8_t v = 0;
@@ -191,12 +206,12 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
         lm = S.saved_modes[i];
       } else {
         const MbHeader& L = a.hdr[o - 1];
-        lm = L.kind == h264::MBK_I4x4 ? L.i4_modes[h264::kRasterToBlk[3 + 4 * i]] : 2;
+        lm = (L.kind == h264::MBK_I4x4 || L.kind == h264::MBK_I8x8) ? L.i4_modes[h264::kRasterToBlk[3 + 4 * i]] : 2;
       }
     }
     if (my > 0) {
       const MbHeader& T = a.hdr[o - g.wmb];
-      tm = T.kind == h264::MBK_I4x4 ? T.i4_modes[h264::kRasterToBlk[i + 12]] : 2;
+      tm = (T.kind == h264::MBK_I4x4 || T.kind == h264::MBK_I8x8) ? T.i4_modes[h264::kRasterToBlk[i + 12]] : 2;
     }
     S.left_modes[i] = lm;
     S.top_modes[i] = tm;
@@ -266,6 +281,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
   PROF(3);
   // ---- Intra4x4 trial (closed loop over the 16 blocks; 9 modes ranked in parallel)
   bool use4 = false;
+  int cost4 = 0x3FFFFFFF;
   if (a.use_i4x4) {
     for (int i = lane; i < 17 * TS; i += 64) S.t4[i] = S.tile[i];
     wave_sync();
@@ -336,12 +352,159 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
       wave_sync();
     }
     use4 = total < cost16;
+    cost4 = total;
+  }
+
+  // ---- Intra8x8 trial (closed loop over the four 8x8 blocks, 9 modes ranked on sa8d)
+  bool use8 = false;
+  if (a.use_i8x8) {
+    for (int i = lane; i < 17 * TS; i += 64) S.t8[i] = S.tile[i];
+    wave_sync();
+    int total8 = lambda * 8;
+    const int qm = qp % 6, q6 = qp / 6, qbits8 = 16 + qp / 6;
+    for (int b8 = 0; b8 < 4; ++b8) {
+      const int bx = (b8 & 1) * 8, by = (b8 >> 1) * 8;
+      // reference samples and their availability (8.3.2.2): block 1's top-right lies in the
+      // top-right MB, block 2's in block 1, block 3 has none
+      const bool has_top = by > 0 || (mbav & h264::AV_TOP);
+      const bool has_left = bx > 0 || (mbav & h264::AV_LEFT);
+      const bool has_tl = b8 == 3 || (b8 == 0 ? (mbav & h264::AV_TOPLEFT) != 0
+                                              : (b8 == 1 ? (mbav & h264::AV_TOP) != 0 : (mbav & h264::AV_LEFT) != 0));
+      const bool has_tr = b8 == 2 || (b8 == 0 ? (mbav & h264::AV_TOP) != 0 : (b8 == 1 && (mbav & h264::AV_TOPRIGHT)));
+      const uint8_t* above = S.t8 + by * TS + bx + 1;  // row above the block, x = 0
+      if (lane < 16) {
+        S.e8t[lane] = lane < 8 ? above[lane] : (has_tr ? (b8 == 1 ? S.tr8[lane - 8] : above[lane]) : above[7]);
+      } else if (lane < 24) {
+        S.e8l[lane - 16] = S.t8[(by + 1 + lane - 16) * TS + bx];
+      } else if (lane == 24) {
+        S.e8tl = S.t8[by * TS + bx];
+      }
+      wave_sync();
+      const int tl8 = S.e8tl;
+      if (lane < 16 && has_top) {  // 8.3.2.2.1 reference sample filtering
+        const int* t = S.e8t;
+        int f;
+        if (lane == 0) f = has_tl ? (tl8 + 2 * t[0] + t[1] + 2) >> 2 : (3 * t[0] + t[1] + 2) >> 2;
+        else if (lane == 15) f = (t[14] + 3 * t[15] + 2) >> 2;
+        else f = (t[lane - 1] + 2 * t[lane] + t[lane + 1] + 2) >> 2;
+        S.f8t[lane] = f;
+      } else if (lane >= 16 && lane < 24 && has_left) {
+        const int* l = S.e8l;
+        const int y = lane - 16;
+        int f;
+        if (y == 0) f = has_tl ? (tl8 + 2 * l[0] + l[1] + 2) >> 2 : (3 * l[0] + l[1] + 2) >> 2;
+        else if (y == 7) f = (l[6] + 3 * l[7] + 2) >> 2;
+        else f = (l[y - 1] + 2 * l[y] + l[y + 1] + 2) >> 2;
+        S.f8l[y] = f;
+      } else if (lane == 24) {
+        int f = 0;
+        if (has_tl) {
+          if (has_top && has_left) f = (S.e8t[0] + 2 * tl8 + S.e8l[0] + 2) >> 2;
+          else if (has_top) f = (3 * tl8 + S.e8t[0] + 2) >> 2;
+          else if (has_left) f = (3 * tl8 + S.e8l[0] + 2) >> 2;
+          else f = tl8;
+        }
+        S.f8tl = f;
+      }
+      wave_sync();
+      int dc8 = 128;
+      {
+        int st = 0, sl = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          st += has_top ? S.f8t[i] : 0;
+          sl += has_left ? S.f8l[i] : 0;
+        }
+        dc8 = (has_top && has_left) ? (st + sl + 8) >> 4 : (has_left ? (sl + 4) >> 3 : (has_top ? (st + 4) >> 3 : 128));
+      }
+      // predicted mode (8.3.2.1): the left / upper 8x8 block's mode; a neighbouring I4x4 MB
+      // gives its 4x4 block next to this block's first 4x4 (the writers' rule)
+      const int ma = bx > 0 ? S.modes8[b8 - 1] : S.left_modes[by >> 2];
+      const int mb_ = by > 0 ? S.modes8[b8 - 2] : S.top_modes[bx >> 2];
+      const bool dcpred = (bx == 0 && !(mbav & h264::AV_LEFT)) || (by == 0 && !(mbav & h264::AV_TOP));
+      const int pm = dcpred ? 2 : min(ma, mb_);
+      // mode ranking: lane = (mode group lane >> 3, row lane & 7); two passes cover modes 0..8
+      int key = 0x7FFFFFFF;
+      for (int pass = 0; pass < 2; ++pass) {
+        const int m = pass * 8 + (lane >> 3), r = lane & 7;
+        const bool valid = m < 9 && (m == 2 || ((m == 0 || m == 3 || m == 7) && has_top) || ((m == 1 || m == 8) && has_left) ||
+                                     ((m == 4 || m == 5 || m == 6) && has_top && has_left && has_tl));
+        int v[8];
+#pragma unroll
+        for (int x = 0; x < 8; ++x)
+          v[x] = m < 9 ? static_cast<int>(S.src[(by + r) * 16 + bx + x]) - i8_pred_sample(m, x, r, S.f8t, S.f8l, S.f8tl, dc8) : 0;
+        had8_pass(v, 1);
+#pragma unroll
+        for (int x = 0; x < 8; ++x) S.h8[lane >> 3][r * 8 + x] = v[x];
+        wave_sync();
+        const int c = lane & 7;
+#pragma unroll
+        for (int y = 0; y < 8; ++y) v[y] = S.h8[lane >> 3][y * 8 + c];
+        had8_pass(v, 1);
+        int sa = 0;
+#pragma unroll
+        for (int y = 0; y < 8; ++y) sa += v[y] < 0 ? -v[y] : v[y];
+        sa += __shfl_xor(sa, 1);
+        sa += __shfl_xor(sa, 2);
+        sa += __shfl_xor(sa, 4);
+        const int cost = ((sa + 2) >> 2) + lambda * (m == pm ? 1 : 4);
+        if (valid && c == 0) key = min(key, (cost << 4) | m);
+        wave_sync();
+      }
+      key = wave_min(key);
+      const int mode = key & 15;
+      total8 += key >> 4;
+      // transform / quantise / reconstruct the chosen mode: lane = sample (x, y) for the
+      // prediction, rows / columns on lanes 0-7 for the transform, lane = scan index for the levels
+      const int x = lane & 7, y = lane >> 3;
+      const int pr = i8_pred_sample(mode, x, y, S.f8t, S.f8l, S.f8tl, dc8);
+      S.d8[lane] = static_cast<int>(S.src[(by + y) * 16 + bx + x]) - pr;
+      wave_sync();
+      if (lane < 8) dct8_pass(S.d8 + lane * 8, 1);
+      wave_sync();
+      if (lane < 8) dct8_pass(S.d8 + lane, 8);
+      wave_sync();
+      {
+        const int pos = kZz8[lane];
+        const int cls = pos8(pos & 7, pos >> 3);
+        const int lv = h264::quant_coef(S.d8[pos], kQuant8MF[qm][cls], qbits8, 21);
+        S.c8[b8][lane] = static_cast<int16_t>(lv);
+        const int ls = 16 * kNorm8[qm][cls];
+        S.d8[pos] = q6 >= 6 ? (lv * ls) << (q6 - 6) : (lv * ls + (1 << (5 - q6))) >> (6 - q6);
+        const unsigned long long nzm = __ballot(lv != 0);
+        if (lane == 0) S.nz8 = static_cast<uint8_t>((b8 == 0 ? 0 : S.nz8) | ((nzm != 0) << b8));
+      }
+      wave_sync();
+      if (lane < 8) idct8_pass(S.d8 + lane * 8, 1);
+      wave_sync();
+      if (lane < 8) idct8_pass(S.d8 + lane, 8);
+      wave_sync();
+      S.t8[(by + 1 + y) * TS + bx + 1 + x] = static_cast<uint8_t>(h264::clip1(pr + ((S.d8[lane] + 32) >> 6)));
+      if (lane == 0) S.modes8[b8] = static_cast<uint8_t>(mode);
+      wave_sync();
+    }
+    const int best_other = use4 ? cost4 : cost16;
+    use8 = total8 < best_other;
+    if (use8) use4 = false;
   }
 
   PROF(4);
   MbHeader* h = a.hdr + o;
   int16_t* coef = a.coef + o * h264::kCoefPerMb;
-  if (use4) {
+  if (use8) {
+    for (int i = lane; i < 256; i += 64) coef[h264::COEF_LUMA + i] = S.c8[i >> 6][i & 63];
+    if (lane < 16) coef[h264::COEF_LUMA_DC + lane] = 0;
+    for (int i = lane; i < 256; i += 64) {
+      int y = i >> 4, x = i & 15;
+      S.tile[(y + 1) * TS + x + 1] = S.t8[(y + 1) * TS + x + 1];
+    }
+    if (lane < 16) {
+      // nz per 4x4 (raster): the 8x8 block covering it has levels
+      const int rx = lane & 3, ry = lane >> 2;
+      a.nz[o * 16 + lane] = (S.nz8 >> ((ry >> 1) * 2 + (rx >> 1))) & 1;
+      h->i4_modes[lane] = S.modes8[lane >> 2];  // luma4x4BlkIdx: 4 per 8x8 block
+    }
+  } else if (use4) {
     for (int i = lane; i < 256; i += 64) coef[h264::COEF_LUMA + i] = S.c4[i >> 4][i & 15];
     if (lane < 16) coef[h264::COEF_LUMA_DC + lane] = 0;
     for (int i = lane; i < 256; i += 64) {
@@ -468,20 +631,20 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
   if (lane < 16) S.saved_y[lane] = S.tile[(lane + 1) * TS + 16];
   if (lane >= 16 && lane < 20) {
     int i = lane - 16;
-    S.saved_modes[i] = use4 ? S.modes4[h264::kRasterToBlk[3 + 4 * i]] : 2;
+    S.saved_modes[i] = use4 ? S.modes4[h264::kRasterToBlk[3 + 4 * i]] : (use8 ? S.modes8[(i >> 1) * 2 + 1] : 2);
   }
   if (lane == 63) {
     S.saved_x = mx;
-    h->kind = use4 ? h264::MBK_I4x4 : h264::MBK_I16x16;
+    h->kind = use8 ? h264::MBK_I8x8 : (use4 ? h264::MBK_I4x4 : h264::MBK_I16x16);
     h->qp = static_cast<int8_t>(qp);
     h->i16_mode = static_cast<uint8_t>(mode16);
     h->chroma_mode = static_cast<uint8_t>(cmode);
-    h->flags = 0;
+    h->flags = use8 ? h264::MBF_T8x8 : 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) h->mv[0][q][0] = h->mv[0][q][1] = h->mv[1][q][0] = h->mv[1][q][1] = 0;
     *reinterpret_cast<uint2*>(&h->ref[0][0]) = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
   }
-  if (!use4 && lane >= 32 && lane < 48) h->i4_modes[lane - 32] = 2;
+  if (!use4 && !use8 && lane >= 32 && lane < 48) h->i4_modes[lane - 32] = 2;
   wave_sync();
   PROF(7);
 }
@@ -543,7 +706,7 @@ extern "C" void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t*
                                          const uint8_t* src_v, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v,
                                          const int* qp, int chroma_qp_offset, void* hdr, int16_t* coef, uint8_t* nz,
                                          const uint8_t* intra_flag, const int* intra_count, int* err, int use_i4x4,
-                                         const int8_t* aq, void* stream) {
+                                         const int8_t* aq, void* stream, int use_i8x8) {
   IntraArgs a;
   a.aq = aq;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
@@ -562,6 +725,7 @@ extern "C" void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t*
   a.intra_count = intra_count;
   a.err = err;
   a.use_i4x4 = use_i4x4;
+  a.use_i8x8 = use_i8x8;
   hipLaunchKernelGGL(encode_intra_wavefront, dim3(B), dim3(64 * kIntraWaves), 0, static_cast<hipStream_t>(stream), a);
 }
 

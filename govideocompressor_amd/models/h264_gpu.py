@@ -42,6 +42,9 @@ class H264Params:
     me_range: int = 8              # integer full-search radius around the best predictor
     subpel: int = 2
     i4x4: bool = True
+    # x264 --partitions i8x8 (its default with --8x8dct): Intra8x8 MBs (High profile) tried where
+    # Intra4x4 is (I pictures, scene cuts), closed loop with the 8x8 transform, sa8d ranking
+    i8x8: bool = True
     # Intra4x4 trial for the (rare) intra MBs of P frames.  Off by default: a P-frame
     # intra MB is coded by the wavefront kernel, whose latency (x chain length) is
     # dominated by the 16 serial I4x4 block trials; these MBs are ~0.1-1% of a P frame.
@@ -76,6 +79,9 @@ class H264Params:
     # x264 --8x8dct (default on): High profile, the 8x8 transform chosen per inter MB where
     # its sa8d beats the 4x4 satd; CABAC only (the CAVLC path stays Constrained Baseline)
     t8x8: bool = True
+    # x264 --weightb (default on): implicit weighted bi-prediction in B pictures
+    # (weighted_bipred_idc 2: list weights from the POC distances, 8.4.2.3.1)
+    weightb: bool = True
     # x264 --partitions p8x8 (default): P macroblocks may split into 8x8 quadrants with their
     # own vectors (coded as P_8x8 / P_16x8 / P_8x16); CABAC only.  part_overhead: bits
     # charged to a split beyond its mvds; part_min_satd: 16x16 SATD at or below which the
@@ -109,14 +115,16 @@ class H264Params:
         return dict(width=self.width, height=self.height, fps=self.fps, qp=self.qp,
                     deblock=int(self.deblock), chroma_qp_offset=self.chroma_qp_offset,
                     vui=int(self.vui), cabac=int(self.cabac), bframes=self.eff_bframes(), t8x8=int(self.eff_t8x8()),
+                    weighted_bipred=2 if self.weightb else 0,
                     level_idc=int(self.level_idc))
 
     def profile_name(self) -> str:
         if not self.cabac:
             return "Constrained Baseline CAVLC"
         nb = self.eff_bframes()
-        return (("High CABAC 8x8dct" if self.eff_t8x8() else "Main CABAC") + (" p8x8" if self.eff_partitions() else "")
-                + (f" {nb}B temporal-direct" if nb else ""))
+        return (("High CABAC 8x8dct" if self.eff_t8x8() else "Main CABAC") + (" i8x8" if self.eff_t8x8() and self.i8x8 else "")
+                + (" p8x8" if self.eff_partitions() else "")
+                + (f" {nb}B temporal-direct" if nb else "") + (" weightb" if nb and self.weightb else ""))
 
     def frame_qps(self) -> tuple[int, int]:
         """(qp_I, qp_P).  CRF maps to the P-frame QP (x264 scale without MB-tree);
@@ -428,6 +436,10 @@ class GpuH264Encoder:
             f1y, f1u, f1v = (P(x) for x in ref1)
             hp0, hp1 = P(self.me_hp[(pic.l1_anchor - 1) & 1]), P(self.me_hp[pic.l1_anchor & 1])
             dsf, copy = self._dist_scale(pic.poc, 2 * pic.l0, 2 * pic.l1)
+            # implicit bi-prediction weights (8.4.2.3.1): w1 = DistScaleFactor >> 2 unless out of range
+            w1 = 32
+            if self.p.weightb and not copy and -64 <= (dsf >> 2) <= 128:
+                w1 = dsf >> 2
             self.intra_count.zero_()
             br = self.p.b_me_range
             with st("me_b"):
@@ -440,24 +452,25 @@ class GpuH264Encoder:
             with st("b_decide"):
                 self.hip.b_decide(B, wmb, hmb, sy, f0y, f1y, hp0, hp1, P(self.mv), P(self.mv1), P(self.me_cost),
                                   P(self.me_cost1), P(self.pred), P(self.pred1), P(self.pm0), P(self.pm1),
-                                  P(self.dmv), P(self.qp), aq, P(hdr), P(self.pred_b), P(self.cost_b), s)
+                                  P(self.dmv), P(self.qp), aq, P(hdr), P(self.pred_b), P(self.cost_b), s, w1)
             if cut is not None:
                 self.intra_cost.masked_fill_(cut[:, None], -1)
             with st("inter"):
                 self.hip.encode_inter(B, wmb, hmb, sy, su, sv, f0y, f0u, f0v, ry, ru, rv, P(self.pred_b), P(self.mv),
                                       P(self.cost_b), P(self.intra_cost), P(self.qp), cqo, P(hdr), P(coef),
                                       P(self.nz), P(self.intra_flag), P(self.intra_count), s, aq, f1u, f1v, 1,
-                                      int(self.p.eff_t8x8()))
+                                      int(self.p.eff_t8x8()), 0, w1)
         if pic.kind != "I":
             self.p_intra_mbs += self.intra_count.sum()
             flag_ptr, count_ptr = P(self.intra_flag), P(self.intra_count)
         else:
             self.prev_mv.zero_()
             flag_ptr, count_ptr = 0, 0
+        trial = idr or self.p.i4x4_in_p or cut is not None
         with st("intra"):
             self.hip.encode_intra(B, wmb, hmb, sy, su, sv, ry, ru, rv, P(self.qp), cqo, P(hdr), P(coef), P(self.nz),
-                                  flag_ptr, count_ptr, P(self.err),
-                                  int(self.p.i4x4 and (idr or self.p.i4x4_in_p or cut is not None)), s, aq)
+                                  flag_ptr, count_ptr, P(self.err), int(self.p.i4x4 and trial), s, aq,
+                                  int(self.p.i8x8 and self.p.eff_t8x8() and trial))
         if aq:
             # MBs without mb_qp_delta take QP_pred (clause 7.4.5): their records must say so
             # before deblocking reads every MB's QP

@@ -301,3 +301,21 @@ def test_nonref_b_deblock_skip_keeps_bytes():
     b = enc.encode(y, u, v, metrics=False)
     enc.close()
     assert [r.bitstream for r in a] == [r.bitstream for r in b]
+
+
+@pytest.mark.parametrize("qp", [20, 30])
+def test_gpu_h264_intra8x8(host, qp):
+    """x264's Intra8x8 (High profile, --partitions i8x8): filtered reference samples, 9
+    modes ranked on sa8d, the 8x8 transform in the closed loop.  The CPU decoder
+    reconstructs the same pictures (8x8-transform-aware deblocking included), I8x8 MBs
+    occur, and the IDR pictures get no bigger than with Intra4x4 / Intra16x16 alone."""
+    enc, res, _ = _run(352, 288, slots=2, frames=3, crf=None, qp=qp, bframes=0)
+    _check_roundtrip(host, enc, res, 352, 288)
+    kinds = np.concatenate([np.asarray(p["mb_kind"]).ravel() for r in res for p in host.decode(r.bitstream)[:1]])
+    assert (kinds == 8).sum() > 0
+    enc0, res0, _ = _run(352, 288, slots=2, frames=3, crf=None, qp=qp, bframes=0, i8x8=False)
+    i8 = sum(len(r.nals[0]) for r in res)
+    i4 = sum(len(r.nals[0]) for r in res0)
+    assert i8 <= 1.01 * i4
+    enc.close()
+    enc0.close()
