@@ -64,6 +64,19 @@ EncoderConfig cfg_from(const py::dict& d) {
   c.refs = dget<int>(d, "refs", 1);
   c.weighted_bipred = dget<int>(d, "weighted_bipred", 0);
   c.level_idc = dget<int>(d, "level_idc", 0);
+  c.cqm = dget<int>(d, "cqm", 0);
+  c.cqm_coded = dget<int>(d, "cqm_coded", 0xFF);
+  if (c.cqm < 0 || c.cqm > 3) throw std::runtime_error("cqm in 0..3");
+  if (d.contains("cqm4")) {  // [6, 16] raster weights
+    auto a = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>::ensure(d["cqm4"]);
+    if (!a || a.size() != 96) throw std::runtime_error("cqm4: 6 x 16 weights");
+    std::memcpy(c.cqm4, a.data(), 96);
+  }
+  if (d.contains("cqm8")) {  // [2, 64]
+    auto a = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>::ensure(d["cqm8"]);
+    if (!a || a.size() != 128) throw std::runtime_error("cqm8: 2 x 64 weights");
+    std::memcpy(c.cqm8, a.data(), 128);
+  }
   if (c.refs < 1 || c.refs > 16) throw std::runtime_error("refs must be in 1..16");
   return c;
 }

@@ -49,6 +49,14 @@ SPS make_sps(const EncoderConfig& cfg) {
   }
   s.max_num_ref_frames = std::max(1, cfg.refs) + (cfg.bframes > 0 ? 1 : 0);
   s.vui_present = cfg.vui;
+  if (cfg.cqm && !cfg.t8x8) throw std::runtime_error("H.264: scaling matrices need the High profile (t8x8)");
+  if (cfg.cqm == 3) s.scaling_present = 1;  // the default matrices, overridden by the PPS lists (rule B)
+  if (cfg.cqm == 1 || cfg.cqm == 2) {
+    s.scaling_present = 1;
+    for (int i = 0; i < 8; ++i) s.sl_coded[i] = cfg.cqm == 2 && ((cfg.cqm_coded >> i) & 1);
+    std::memcpy(s.sl4, cfg.cqm4, sizeof(s.sl4));
+    std::memcpy(s.sl8, cfg.cqm8, sizeof(s.sl8));
+  }
   // time_scale / (2 * num_units_in_tick) = fps
   s.num_units_in_tick = 1000;
   s.time_scale = static_cast<uint32_t>(std::lround(cfg.fps * 2000.0));
@@ -65,6 +73,12 @@ PPS make_pps(const EncoderConfig& cfg) {
   p.chroma_qp_index_offset = cfg.chroma_qp_offset;
   p.second_chroma_qp_index_offset = cfg.chroma_qp_offset;
   p.deblocking_filter_control_present = 1;
+  if (cfg.cqm == 3) {
+    p.scaling_present = 1;
+    for (int i = 0; i < 8; ++i) p.sl_coded[i] = (cfg.cqm_coded >> i) & 1;
+    std::memcpy(p.sl4, cfg.cqm4, sizeof(p.sl4));
+    std::memcpy(p.sl8, cfg.cqm8, sizeof(p.sl8));
+  }
   return p;
 }
 
@@ -117,24 +131,37 @@ class FrameEncoder {
   std::vector<MbHeader> mbs_;
   std::vector<int16_t> coef_;
   Planes rec_;
+  // the effective scaling lists of the picture (raster; the decoder's derivation of the
+  // parameter sets this encoder wrote): [0..5] intra Y / Cb / Cr, inter Y / Cb / Cr
+  uint8_t sl4_[6][16];
 
  private:
   int sy(int x, int y) const { return src_->y[static_cast<size_t>(y) * src_->W + x]; }
 
   // ---------------------------------------------------------------- transform helpers
   // residual 4x4 (raster) -> quantised levels in scan order; returns reconstructed residual in res (raster)
-  void tq4x4(int* res, int qp, bool intra, int16_t* out_scan, bool skip_dc) {
+  // weighted LevelScale4x4 dequantisation (8.5.12.1) with scaling list wl (raster)
+  static int dequant_w(int c, int qp, int r, const uint8_t* wl) {
+    const int ls = wl[r] * kDequantV[qp % 6][kPosClass[r]];
+    if (qp >= 24) return (c * ls) << (qp / 6 - 4);
+    return (c * ls + (1 << (3 - qp / 6))) >> (4 - qp / 6);
+  }
+  // list: scaling list index (0..5: intra Y / Cb / Cr, inter Y / Cb / Cr)
+  void tq4x4(int* res, int qp, bool intra, int16_t* out_scan, bool skip_dc, int list) {
     int w[16];
     for (int i = 0; i < 16; ++i) w[i] = res[i];
     forward_core4x4(w);
     int qbits = 15 + qp / 6;
     int bias = intra ? 21 : 11;
+    const uint8_t* wl = sl4_[list];
     int lv[16];
-    for (int r = 0; r < 16; ++r) lv[r] = quant_coef(w[r], kQuantMF[qp % 6][kPosClass[r]], qbits, bias);
+    // the quantiser divides by the weight (x264-style MF * 16 / w); only the dequantisation
+    // has to match the decoder
+    for (int r = 0; r < 16; ++r) lv[r] = quant_coef(w[r], kQuantMF[qp % 6][kPosClass[r]] * 16 / wl[r], qbits, bias);
     if (skip_dc) lv[0] = 0;
     for (int i = 0; i < 16; ++i) out_scan[i] = static_cast<int16_t>(lv[kZigzag4x4[i]]);
     if (skip_dc) out_scan[0] = 0;
-    for (int r = 0; r < 16; ++r) res[r] = dequant_coef(lv[r], qp, r);
+    for (int r = 0; r < 16; ++r) res[r] = dequant_w(lv[r], qp, r, wl);
     // caller supplies DC (if skip_dc) before inverse
   }
 
@@ -211,7 +238,7 @@ class FrameEncoder {
           pred[y * 4 + x] = i4_pred_sample(best_mode, av, e, x, y);
           res[y * 4 + x] = sy(x0 + x, y0 + y) - pred[y * 4 + x];
         }
-      tq4x4(res, qp, true, coef + COEF_LUMA + blk * 16, false);
+      tq4x4(res, qp, true, coef + COEF_LUMA + blk * 16, false, 0);
       inverse_core4x4(res);
       for (int y = 0; y < 4; ++y)
         for (int x = 0; x < 4; ++x)
@@ -286,19 +313,19 @@ class FrameEncoder {
       for (int i = 0; i < 16; ++i) w[i] = res[blk][i];
       forward_core4x4(w);
       dcs[kBlkX[blk] + 4 * kBlkY[blk]] = w[0];
-      tq4x4(res[blk], qp, true, coef + COEF_LUMA + blk * 16, true);
+      tq4x4(res[blk], qp, true, coef + COEF_LUMA + blk * 16, true, 0);
     }
     // DC: Hadamard, /2, quantise with qbits+1
     hadamard4x4(dcs);
     int qbits = 15 + qp / 6;
     int dcl[16];
-    for (int r = 0; r < 16; ++r) dcl[r] = quant_coef(dcs[r] >> 1, kQuantMF[qp % 6][0], qbits + 1, 21);
+    for (int r = 0; r < 16; ++r) dcl[r] = quant_coef(dcs[r] >> 1, kQuantMF[qp % 6][0] * 16 / sl4_[0][0], qbits + 1, 21);
     for (int i = 0; i < 16; ++i) coef[COEF_LUMA_DC + i] = static_cast<int16_t>(dcl[kZigzag4x4[i]]);
     // encoder-side reconstruction of the DC path (mirrors 8.5.10)
     int f[16];
     for (int i = 0; i < 16; ++i) f[i] = dcl[i];
     hadamard4x4(f);
-    int ls = 16 * kDequantV[qp % 6][0];
+    int ls = sl4_[0][0] * kDequantV[qp % 6][0];
     for (int blk = 0; blk < 16; ++blk) {
       int rpos = kBlkX[blk] + 4 * kBlkY[blk];
       int fv = f[rpos];
@@ -380,7 +407,7 @@ class FrameEncoder {
         for (int i = 0; i < 16; ++i) w[i] = res[b][i];
         forward_core4x4(w);
         dcs[b] = w[0];
-        tq4x4(res[b], qpc, intra, coef + COEF_CHROMA_AC + (comp * 4 + b) * 16, true);
+        tq4x4(res[b], qpc, intra, coef + COEF_CHROMA_AC + (comp * 4 + b) * 16, true, (intra ? 1 : 4) + comp);
       }
       int y0 = dcs[0] + dcs[1] + dcs[2] + dcs[3];
       int y1 = dcs[0] - dcs[1] + dcs[2] - dcs[3];
@@ -390,12 +417,12 @@ class FrameEncoder {
       int qbits = 15 + qpc / 6;
       int lv[4];
       for (int i = 0; i < 4; ++i) {
-        lv[i] = quant_coef(yd[i], kQuantMF[qpc % 6][0], qbits + 1, intra ? 21 : 11);
+        lv[i] = quant_coef(yd[i], kQuantMF[qpc % 6][0] * 16 / sl4_[(intra ? 1 : 4) + comp][0], qbits + 1, intra ? 21 : 11);
         coef[COEF_CHROMA_DC + comp * 4 + i] = static_cast<int16_t>(lv[i]);
       }
       int f[4] = {lv[0] + lv[1] + lv[2] + lv[3], lv[0] - lv[1] + lv[2] - lv[3], lv[0] + lv[1] - lv[2] - lv[3],
                   lv[0] - lv[1] - lv[2] + lv[3]};
-      int ls = 16 * kDequantV[qpc % 6][0];
+      int ls = sl4_[(intra ? 1 : 4) + comp][0] * kDequantV[qpc % 6][0];
       bool any = false;
       for (int i = 0; i < 4; ++i) any |= lv[i] != 0;
       for (int b = 0; b < 4 && !any; ++b)
@@ -539,7 +566,7 @@ class FrameEncoder {
           int res[16];
           for (int y = 0; y < 4; ++y)
             for (int x = 0; x < 4; ++x) res[y * 4 + x] = sy(X0 + bx + x, Y0 + by + y) - pred[(by + y) * 16 + bx + x];
-          tq4x4(res, qp_, false, coef + COEF_LUMA + blk * 16, false);
+          tq4x4(res, qp_, false, coef + COEF_LUMA + blk * 16, false, 3);
         }
         // drop 8x8 blocks whose only content is a few +-1 levels (cheap decimation)
         for (int b8 = 0; b8 < 4; ++b8) {
@@ -559,7 +586,7 @@ class FrameEncoder {
           for (int r = 0; r < 16; ++r) res[r] = 0;
           for (int i = 0; i < 16; ++i) {
             int r = kZigzag4x4[i];
-            res[r] = dequant_coef(coef[COEF_LUMA + blk * 16 + i], qp_, r);
+            res[r] = dequant_w(coef[COEF_LUMA + blk * 16 + i], qp_, r, sl4_[3]);
           }
           inverse_core4x4(res);
           for (int y = 0; y < 4; ++y)
@@ -661,6 +688,11 @@ std::vector<uint8_t> CpuEncoder::encode(const uint8_t* frames, int nframes, int 
   Decoder dec;
   dec.decode(out.data(), out.size());
   FrameEncoder fe(cfg_, sps.width_mbs, sps.height_mbs);
+  // the lists the decoder derives from what was written (fall-back rules included)
+  {
+    uint8_t sl8[2][64];
+    dec.pps_scaling(pps.pps_id, &fe.sl4_[0][0], &sl8[0][0]);
+  }
   Planes src, ref;
   src.alloc(sps.width_mbs * 16, sps.height_mbs * 16);
   ref.alloc(src.W, src.H);

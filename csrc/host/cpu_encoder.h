@@ -37,6 +37,14 @@ struct EncoderConfig {
   int refs = 1;
   int weighted_bipred = 0;  // 2 = implicit weights (x264 --weightb)
   int level_idc = 0;        // > 0: written as level_idc (-level); must fit the size / rate
+  // scaling matrices (High profile, t8x8): 0 flat; 1 the default matrices (x264 --cqm jvt: SPS
+  // flag, no list sent); 2 the lists below in the SPS; 3 the lists below in the PPS over the
+  // default matrices in the SPS (fall-back rule B).  Lists not
+  // in cqm_coded (bit i = list i) fall back per 7.4.2.1.1 / 7.4.2.2.  Weights in raster order.
+  int cqm = 0;
+  int cqm_coded = 0xFF;
+  uint8_t cqm4[6][16] = {};
+  uint8_t cqm8[2][64] = {};
 };
 
 struct FrameStats {

@@ -188,14 +188,15 @@ void idct8(int* b) {
   for (int c = 0; c < 8; ++c) idct8_1d(b + c, 8);
   for (int i = 0; i < 64; ++i) b[i] = (b[i] + 32) >> 6;
 }
-// LevelScale4x4 with flat weights: 16 * normAdjust4x4 (8.5.9)
-int level_scale(int qp_mod6, int x, int y) {
+// LevelScale4x4 = weightScale4x4 * normAdjust4x4 (8.5.9); w = the scaling-list weight of
+// position (x, y) (16 = flat)
+int level_scale(int qp_mod6, int x, int y, int w = 16) {
   static const int v[6][3] = {{10, 16, 13}, {11, 18, 14}, {13, 20, 16}, {14, 23, 18}, {16, 25, 20}, {18, 29, 23}};
   int cls = ((x & 1) == 0 && (y & 1) == 0) ? 0 : (((x & 1) == 1 && (y & 1) == 1) ? 1 : 2);
-  return 16 * v[qp_mod6][cls];
+  return w * v[qp_mod6][cls];
 }
-// LevelScale8x8 with flat weights: 16 * normAdjust8x8 (8.5.9, eq. 8-318)
-int level_scale8(int qp_mod6, int x, int y) {
+// LevelScale8x8 = weightScale8x8 * normAdjust8x8 (8.5.9, eq. 8-318)
+int level_scale8(int qp_mod6, int x, int y, int w = 16) {
   static const int v[6][6] = {{20, 18, 32, 19, 25, 24}, {22, 19, 35, 21, 28, 26}, {26, 23, 42, 24, 33, 31},
                               {28, 25, 45, 26, 35, 33}, {32, 28, 51, 30, 40, 38}, {36, 32, 58, 34, 46, 43}};
   int k;
@@ -205,17 +206,17 @@ int level_scale8(int qp_mod6, int x, int y) {
   else if ((x % 4 == 0 && y % 2 == 1) || (x % 2 == 1 && y % 4 == 0)) k = 3;
   else if ((x % 4 == 0 && y % 4 == 2) || (x % 4 == 2 && y % 4 == 0)) k = 4;
   else k = 5;
-  return 16 * v[qp_mod6][k];
+  return w * v[qp_mod6][k];
 }
-// 8.5.12.1 scaling of one AC/4x4 coefficient
-int scale4(int c, int qp, int x, int y) {
-  int ls = level_scale(qp % 6, x, y);
+// 8.5.12.1 scaling of one AC/4x4 coefficient (w4: the block's scaling list, raster)
+int scale4(int c, int qp, int x, int y, const uint8_t* w4) {
+  int ls = level_scale(qp % 6, x, y, w4[y * 4 + x]);
   if (qp >= 24) return (c * ls) << (qp / 6 - 4);
   return (c * ls + (1 << (3 - qp / 6))) >> (4 - qp / 6);
 }
 // 8.5.13.1 scaling of one 8x8 coefficient
-int scale8(int c, int qp, int x, int y) {
-  int ls = level_scale8(qp % 6, x, y);
+int scale8(int c, int qp, int x, int y, const uint8_t* w8) {
+  int ls = level_scale8(qp % 6, x, y, w8[y * 8 + x]);
   if (qp >= 36) return (c * ls) << (qp / 6 - 6);
   return (c * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
 }
@@ -772,6 +773,14 @@ struct Decoder::Impl {
     slice_idx = static_cast<int>(slices.size()) - 1;
     cur->nslices = static_cast<int>(slices.size());
     if (p->constrained_intra_pred) cur->gpu_ok = false;
+    {  // non-flat scaling lists: the GPU reconstruction dequantises with flat weights only
+      bool flat = true;
+      for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 16; ++j) flat = flat && p->sl4[i][j] == 16;
+      for (int i = 0; i < 2 && p->transform_8x8_mode; ++i)
+        for (int j = 0; j < 64; ++j) flat = flat && p->sl8[i][j] == 16;
+      if (!flat) cur->gpu_ok = false;
+    }
     if (h.slice_type == SLICE_B) cur->slice_type = SLICE_B;
     else if (h.slice_type == SLICE_P && cur->slice_type == SLICE_I) cur->slice_type = SLICE_P;
     build_ref_lists();
@@ -2370,13 +2379,13 @@ struct Decoder::Impl {
   }
 
   // ------------------------------------------------------------ reconstruction
-  void add_residual4(int addr, int bx, int by, const int* lv, int qp, bool dc_given, int dcv) {
+  void add_residual4(int addr, int bx, int by, const int* lv, int qp, bool dc_given, int dcv, const uint8_t* w4) {
     int X0 = (addr % cur->wmb) * 16, Y0 = (addr / cur->wmb) * 16;
     int d[16];
     for (int i = 0; i < 16; ++i) d[i] = 0;
     for (int i = dc_given ? 1 : 0; i < 16; ++i) {
       int r = kZigzag4x4[i];
-      d[r] = scale4(lv[i], qp, r & 3, r >> 2);
+      d[r] = scale4(lv[i], qp, r & 3, r >> 2, w4);
     }
     if (dc_given) d[0] = dcv;
     idct4(d);
@@ -2386,13 +2395,13 @@ struct Decoder::Impl {
         o = static_cast<uint8_t>(clip_px(o + d[y * 4 + x]));
       }
   }
-  void add_residual8(int addr, int b8, const int* lv, int qp) {
+  void add_residual8(int addr, int b8, const int* lv, int qp, const uint8_t* w8) {
     int X0 = (addr % cur->wmb) * 16 + (b8 & 1) * 8, Y0 = (addr / cur->wmb) * 16 + (b8 >> 1) * 8;
     int d[64];
     for (int i = 0; i < 64; ++i) d[i] = 0;
     for (int i = 0; i < 64; ++i) {
       int r = kZigzag8x8[i];
-      d[r] = scale8(lv[i], qp, r & 7, r >> 3);
+      d[r] = scale8(lv[i], qp, r & 7, r >> 3, w8);
     }
     idct8(d);
     for (int y = 0; y < 8; ++y)
@@ -2407,6 +2416,10 @@ struct Decoder::Impl {
     int cw = cur->W / 2;
     int X0 = mx * 16, Y0 = my * 16;
     int cbp_luma = s.cbp & 15, cbp_chroma = s.cbp >> 4;
+    // the picture's scaling lists (8.5.9): intra Y / Cb / Cr, inter Y / Cb / Cr; 8x8 intra / inter
+    const int li = mbk_is_intra(kind) ? 0 : 3;
+    const uint8_t* wy4 = pp->sl4[li];
+    const uint8_t* wy8 = pp->sl8[li ? 1 : 0];
     if (kind == MBK_I4x4) {
       for (int blk = 0; blk < 16; ++blk) {
         uint8_t pred[16];
@@ -2414,7 +2427,7 @@ struct Decoder::Impl {
         int bx = kBlkX[blk] * 4, by = kBlkY[blk] * 4;
         for (int y = 0; y < 4; ++y)
           for (int x = 0; x < 4; ++x) cur->Y[static_cast<size_t>(Y0 + by + y) * cur->W + X0 + bx + x] = pred[y * 4 + x];
-        add_residual4(addr, bx, by, s.lum[blk], qp, false, 0);
+        add_residual4(addr, bx, by, s.lum[blk], qp, false, 0, wy4);
         blk_done[kBlkX[blk] + 4 * kBlkY[blk]] = 1;
       }
     } else if (kind == MBK_I8x8) {
@@ -2424,7 +2437,7 @@ struct Decoder::Impl {
         int bx = (b8 & 1) * 8, by = (b8 >> 1) * 8;
         for (int y = 0; y < 8; ++y)
           for (int x = 0; x < 8; ++x) cur->Y[static_cast<size_t>(Y0 + by + y) * cur->W + X0 + bx + x] = pred[y * 8 + x];
-        if (cbp_luma & (1 << b8)) add_residual8(addr, b8, s.lum8[b8], qp);
+        if (cbp_luma & (1 << b8)) add_residual8(addr, b8, s.lum8[b8], qp, wy8);
         mark_done(bx >> 2, by >> 2, 2, 2);
       }
     } else if (kind == MBK_I16x16) {
@@ -2449,22 +2462,22 @@ struct Decoder::Impl {
         f[8 + x] = s0 - s1 - s2 + s3;
         f[12 + x] = s0 - s1 + s2 - s3;
       }
-      int ls = level_scale(qp % 6, 0, 0);
+      int ls = level_scale(qp % 6, 0, 0, wy4[0]);
       for (int blk = 0; blk < 16; ++blk) {
         int bx = kBlkX[blk], by = kBlkY[blk];
         int fv = f[bx + 4 * by];
         int dcv = qp >= 36 ? (fv * ls) << (qp / 6 - 6) : (fv * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
-        add_residual4(addr, bx * 4, by * 4, s.lum[blk], qp, true, dcv);
+        add_residual4(addr, bx * 4, by * 4, s.lum[blk], qp, true, dcv, wy4);
       }
     } else {
       inter_pred(addr);
       if (s.t8x8) {
         for (int b8 = 0; b8 < 4; ++b8)
-          if (cbp_luma & (1 << b8)) add_residual8(addr, b8, s.lum8[b8], qp);
+          if (cbp_luma & (1 << b8)) add_residual8(addr, b8, s.lum8[b8], qp, wy8);
       } else {
         for (int blk = 0; blk < 16; ++blk) {
           if (!(cbp_luma & (1 << (blk >> 2)))) continue;
-          add_residual4(addr, kBlkX[blk] * 4, kBlkY[blk] * 4, s.lum[blk], qp, false, 0);
+          add_residual4(addr, kBlkX[blk] * 4, kBlkY[blk] * 4, s.lum[blk], qp, false, 0, wy4);
         }
       }
     }
@@ -2482,14 +2495,15 @@ struct Decoder::Impl {
       int qpc = chroma_qp(qp, comp == 0 ? pp->chroma_qp_index_offset : pp->second_chroma_qp_index_offset);
       int c0 = s.cdc[comp][0], c1 = s.cdc[comp][1], c2 = s.cdc[comp][2], c3 = s.cdc[comp][3];
       int f[4] = {c0 + c1 + c2 + c3, c0 - c1 + c2 - c3, c0 + c1 - c2 - c3, c0 - c1 - c2 + c3};
-      int ls = level_scale(qpc % 6, 0, 0);
+      const uint8_t* wc4 = pp->sl4[li + 1 + comp];
+      int ls = level_scale(qpc % 6, 0, 0, wc4[0]);
       for (int b = 0; b < 4; ++b) {
         int d[16];
         for (int i = 0; i < 16; ++i) d[i] = 0;
         if (cbp_chroma & 2)
           for (int i = 1; i < 16; ++i) {
             int r = kZigzag4x4[i];
-            d[r] = scale4(s.cac[comp][b][i], qpc, r & 3, r >> 2);
+            d[r] = scale4(s.cac[comp][b][i], qpc, r & 3, r >> 2, wc4);
           }
         d[0] = ((f[b] * ls) << (qpc / 6)) >> 5;
         bool any = cbp_chroma != 0;
@@ -2798,6 +2812,12 @@ void Decoder::flush() {
 }
 
 void Decoder::set_parse_only(bool v) { impl_->parse_only = v; }
+
+void Decoder::pps_scaling(int pps_id, uint8_t* sl4, uint8_t* sl8) const {
+  if (pps_id < 0 || pps_id > 255 || !impl_->have_pps[pps_id]) throw std::runtime_error("pps_scaling: unknown PPS");
+  std::memcpy(sl4, impl_->pps[pps_id].sl4, sizeof(impl_->pps[pps_id].sl4));
+  std::memcpy(sl8, impl_->pps[pps_id].sl8, sizeof(impl_->pps[pps_id].sl8));
+}
 
 }  // namespace h264
 }  // namespace mivc

@@ -78,6 +78,8 @@ class Decoder {
   void set_skip_deblock(bool v) { skip_deblock_ = v; }
   // Entropy-decode only: fill DecodedPicture::hdr/coef/nz and skip pixel reconstruction
   void set_parse_only(bool v);
+  // the effective scaling lists of a parsed PPS (raster weights: 6 x 16, then 2 x 64)
+  void pps_scaling(int pps_id, uint8_t* sl4, uint8_t* sl8) const;
 
   struct Impl;
 

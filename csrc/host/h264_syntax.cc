@@ -1,10 +1,93 @@
 #include "h264_syntax.h"
 
 #include <cmath>
+#include <cstring>
 #include <stdexcept>
+
+#include "../common/h264_cabac_tables.h"  // kZigzag8x8
 
 namespace mivc {
 namespace h264 {
+
+void flat_scaling(uint8_t (*sl4)[16], uint8_t (*sl8)[64]) {
+  std::memset(sl4, 16, 6 * 16);
+  std::memset(sl8, 16, 2 * 64);
+}
+SPS::SPS() { flat_scaling(sl4, sl8); }
+PPS::PPS() { flat_scaling(sl4, sl8); }
+
+namespace {
+
+// scan position -> raster index of a 4x4 / 8x8 list
+int scan_raster(int n, int j) { return n == 16 ? kZigzag4x4[j] : kZigzag8x8[j]; }
+
+// 7.3.2.1.1.1 scaling_list(): delta-coded in scan order; returns useDefaultScalingMatrixFlag
+bool read_scaling_list(BitReader& br, uint8_t* out_raster, int n) {
+  int last = 8, next = 8;
+  bool use_default = false;
+  for (int j = 0; j < n; ++j) {
+    if (next != 0) {
+      const int delta = br.get_se();
+      if (delta < -128 || delta > 127) throw std::runtime_error("delta_scale out of range");
+      next = (last + delta + 256) % 256;
+      use_default = j == 0 && next == 0;
+    }
+    const int v = next == 0 ? last : next;
+    out_raster[scan_raster(n, j)] = static_cast<uint8_t>(v);
+    last = v;
+  }
+  return use_default;
+}
+
+void write_scaling_list(BitWriter& bw, const uint8_t* raster, int n) {
+  int last = 8;
+  for (int j = 0; j < n; ++j) {
+    const int v = raster[scan_raster(n, j)];
+    if (v < 1) throw std::runtime_error("scaling list entries must be 1..255");
+    int delta = v - last;
+    if (delta > 127) delta -= 256;
+    if (delta < -128) delta += 256;
+    bw.put_se(delta);
+    last = v;
+  }
+}
+
+void default_list(int i, uint8_t* raster) {
+  const int intra = i < 3 || i == 6 ? 0 : 1;
+  if (i < 6)
+    for (int j = 0; j < 16; ++j) raster[kZigzag4x4[j]] = kDefault4x4[intra][j];
+  else
+    for (int j = 0; j < 64; ++j) raster[kZigzag8x8[j]] = kDefault8x8[intra][j];
+}
+
+// lists 0..7 (n8 = 2 for 4:2:0) with fall-back rule A (fallback == nullptr: the defaults for
+// lists 0 / 3 / 6 / 7) or rule B (fallback: the sequence-level lists)
+void read_matrix(BitReader& br, int n8, uint8_t (*sl4)[16], uint8_t (*sl8)[64], const uint8_t (*fb4)[16],
+                 const uint8_t (*fb8)[64]) {
+  for (int i = 0; i < 6 + n8; ++i) {
+    uint8_t* dst = i < 6 ? sl4[i] : sl8[i - 6];
+    const int n = i < 6 ? 16 : 64;
+    if (br.get_bit()) {
+      if (read_scaling_list(br, dst, n)) default_list(i, dst);
+    } else if (i == 0 || i == 3 || i == 6 || i == 7) {
+      if (fb4) std::memcpy(dst, i < 6 ? fb4[i] : fb8[i - 6], n);
+      else default_list(i, dst);
+    } else {
+      std::memcpy(dst, sl4[i - 1], 16);  // Cb from Y, Cr from Cb of the same kind
+    }
+  }
+  if (n8 < 2)
+    for (int i = n8; i < 2; ++i) default_list(6 + i, sl8[i]);
+}
+
+void write_matrix(BitWriter& bw, int n8, const uint8_t (*sl4)[16], const uint8_t (*sl8)[64], const uint8_t* coded) {
+  for (int i = 0; i < 6 + n8; ++i) {
+    bw.put_bit(coded[i]);
+    if (coded[i]) write_scaling_list(bw, i < 6 ? sl4[i] : sl8[i - 6], i < 6 ? 16 : 64);
+  }
+}
+
+}  // namespace
 
 static bool high_profile(int p) {
   return p == 100 || p == 110 || p == 122 || p == 244 || p == 44 || p == 83 || p == 86 || p == 118 ||
@@ -21,7 +104,8 @@ void write_sps(BitWriter& bw, const SPS& s) {
     bw.put_ue(s.bit_depth_luma - 8);
     bw.put_ue(s.bit_depth_chroma - 8);
     bw.put_bit(0);  // qpprime_y_zero_transform_bypass_flag
-    bw.put_bit(0);  // seq_scaling_matrix_present_flag
+    bw.put_bit(s.scaling_present);  // seq_scaling_matrix_present_flag
+    if (s.scaling_present) write_matrix(bw, 2, s.sl4, s.sl8, s.sl_coded);
   }
   bw.put_ue(s.log2_max_frame_num - 4);
   bw.put_ue(s.poc_type);
@@ -82,9 +166,10 @@ void write_pps(BitWriter& bw, const PPS& p) {
   bw.put_bit(p.deblocking_filter_control_present);
   bw.put_bit(p.constrained_intra_pred);
   bw.put_bit(p.redundant_pic_cnt_present);
-  if (p.transform_8x8_mode || p.second_chroma_qp_index_offset != p.chroma_qp_index_offset) {
+  if (p.transform_8x8_mode || p.scaling_present || p.second_chroma_qp_index_offset != p.chroma_qp_index_offset) {
     bw.put_bit(p.transform_8x8_mode);
-    bw.put_bit(0);  // pic_scaling_matrix_present_flag
+    bw.put_bit(p.scaling_present);  // pic_scaling_matrix_present_flag
+    if (p.scaling_present) write_matrix(bw, p.transform_8x8_mode ? 2 : 0, p.sl4, p.sl8, p.sl_coded);
     bw.put_se(p.second_chroma_qp_index_offset);
   }
   bw.trailing();
@@ -128,16 +213,6 @@ void write_slice_header(BitWriter& bw, const SliceHeader& h, const SPS& s, const
   }
 }
 
-static void skip_scaling_list(BitReader& br, int size) {
-  int last = 8, next = 8;
-  for (int j = 0; j < size; ++j) {
-    if (next != 0) {
-      int delta = br.get_se();
-      next = (last + delta + 256) % 256;
-    }
-    last = next == 0 ? last : next;
-  }
-}
 
 static void skip_hrd(BitReader& br) {
   int cpb_cnt = br.get_ue() + 1;
@@ -167,11 +242,10 @@ SPS parse_sps(BitReader& br) {
     s.bit_depth_luma = br.get_ue() + 8;
     s.bit_depth_chroma = br.get_ue() + 8;
     br.get_bit();
-    if (br.get_bit()) {
-      int n = s.chroma_format_idc != 3 ? 8 : 12;
-      for (int i = 0; i < n; ++i)
-        if (br.get_bit()) skip_scaling_list(br, i < 6 ? 16 : 64);
-      throw std::runtime_error("scaling matrices not supported");
+    s.scaling_present = br.get_bit();
+    if (s.scaling_present) {
+      if (s.chroma_format_idc == 3) throw std::runtime_error("4:4:4 scaling matrices not supported");
+      read_matrix(br, 2, s.sl4, s.sl8, nullptr, nullptr);  // fall-back rule A
     }
   }
   if (s.chroma_format_idc != 1 || s.bit_depth_luma != 8) throw std::runtime_error("only 8-bit 4:2:0 supported");
@@ -265,12 +339,24 @@ PPS parse_pps(BitReader& br, const SPS* sps_table) {
   p.constrained_intra_pred = br.get_bit();
   p.redundant_pic_cnt_present = br.get_bit();
   p.second_chroma_qp_index_offset = p.chroma_qp_index_offset;
+  // the picture's scaling lists: the sequence's unless the PPS sends its own
+  const SPS& sps = sps_table[p.sps_id];
+  std::memcpy(p.sl4, sps.sl4, sizeof(p.sl4));
+  std::memcpy(p.sl8, sps.sl8, sizeof(p.sl8));
   if (br.more_rbsp_data()) {
     p.transform_8x8_mode = br.get_bit();
-    if (br.get_bit()) throw std::runtime_error("pic scaling matrices not supported");
+    p.scaling_present = br.get_bit();
+    if (p.scaling_present) {
+      if (sps.chroma_format_idc == 3) throw std::runtime_error("4:4:4 scaling matrices not supported");
+      // fall-back rule B onto the sequence lists when the SPS has them, else rule A
+      uint8_t sl4[6][16], sl8[2][64];
+      if (sps.scaling_present) read_matrix(br, p.transform_8x8_mode ? 2 : 0, sl4, sl8, sps.sl4, sps.sl8);
+      else read_matrix(br, p.transform_8x8_mode ? 2 : 0, sl4, sl8, nullptr, nullptr);
+      std::memcpy(p.sl4, sl4, sizeof(sl4));
+      std::memcpy(p.sl8, sl8, sizeof(sl8));
+    }
     p.second_chroma_qp_index_offset = br.get_se();
   }
-  (void)sps_table;
   return p;
 }
 

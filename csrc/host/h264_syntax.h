@@ -39,6 +39,14 @@ struct SPS {
   int delta_pic_order_always_zero = 0;
   int offset_for_non_ref_pic = 0, offset_for_top_to_bottom = 0;
   std::vector<int> offset_for_ref_frame;
+  // scaling matrices (7.3.2.1.1.1): seq_scaling_matrix_present_flag and the lists after fall-back
+  // rule A, as weights in raster order: [0..5] 4x4 (Intra Y, Cb, Cr, Inter Y, Cb, Cr), [6..7] 8x8
+  // (Intra Y, Inter Y).  Writing: sl_coded[i] says whether list i is sent (else it falls back).
+  int scaling_present = 0;
+  uint8_t sl4[6][16];
+  uint8_t sl8[2][64];
+  uint8_t sl_coded[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  SPS();
 };
 
 struct PPS {
@@ -54,7 +62,17 @@ struct PPS {
   int redundant_pic_cnt_present = 0;
   int transform_8x8_mode = 0;
   int second_chroma_qp_index_offset = 0;
+  // pic_scaling_matrix_present_flag and the effective lists of the picture (fall-back rule B
+  // onto the SPS lists, or the SPS lists when absent); layout as SPS::sl4 / sl8
+  int scaling_present = 0;
+  uint8_t sl4[6][16];
+  uint8_t sl8[2][64];
+  uint8_t sl_coded[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  PPS();
 };
+
+// flat scaling weights (16) in every list
+void flat_scaling(uint8_t (*sl4)[16], uint8_t (*sl8)[64]);
 
 // ref_pic_list_modification() operation (7.3.3.1)
 struct RefMod {

@@ -143,3 +143,32 @@ def test_lowres_costs(host):
     intra, inter = host.lowres_costs(frames, 64, 48, 4)
     assert len(intra) == 4 and all(x > 0 for x in intra)
     assert inter[1] <= intra[1] * 1.5
+
+
+@pytest.mark.parametrize("cqm,coded,seed", [(1, 0xFF, 0), (2, 0xFF, 1), (2, 0b01011001, 2), (3, 0xFF, 3), (3, 0b10010110, 4)])
+def test_scaling_matrices_roundtrip(host, cqm, coded, seed):
+    """H.264 scaling matrices (7.3.2.1.1.1, 8.5.9): the default matrices (x264 --cqm jvt), custom
+    lists in the SPS, and PPS lists over SPS defaults, with lists left out so that fall-back
+    rules A and B apply.  The CPU encoder quantises and reconstructs with the weights the
+    decoder derives; the decoder's unfiltered output equals that reconstruction on every
+    frame, and the weights change the bitstream against flat matrices."""
+    rng = np.random.default_rng(seed)
+    w, h, n = 96, 64, 4
+    c = yuv.synth_clip_cpu(n, w, h, seed=seed)
+    base = dict(width=w, height=h, qp=28, keyint=2, deblock=0, t8x8=1, cabac=seed % 2)
+    cfg = dict(base, cqm=cqm, cqm_coded=coded, cqm4=rng.integers(4, 64, (6, 16)).astype(np.uint8),
+               cqm8=rng.integers(4, 64, (2, 64)).astype(np.uint8))
+    enc = host.CpuEncoder(cfg)
+    es = enc.encode(c.i420(), n, 0)
+    ru = np.asarray(enc.recon_unfiltered())
+    cw, ch = (w + 15) // 16 * 16, (h + 15) // 16 * 16
+    fs = cw * ch * 3 // 2
+    pics = host.decode(es)
+    assert len(pics) == n
+    for t, p in enumerate(pics):
+        fr = ru[t * fs:(t + 1) * fs]
+        assert np.array_equal(p["y_coded"].reshape(-1), fr[: cw * ch]), t
+        assert np.array_equal(p["u_coded"].reshape(-1), fr[cw * ch: cw * ch + cw * ch // 4]), t
+    flat = host.CpuEncoder(base).encode(c.i420(), n, 0)
+    assert flat != es
+    assert host.stream_info(es)["profile_idc"] == 100
