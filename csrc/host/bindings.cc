@@ -295,6 +295,7 @@ hevc::HevcConfig hevc_cfg_from(const py::dict& d) {
   c.bframes = dget<int>(d, "bframes", 0);
   c.tmvp = dget<int>(d, "tmvp", 0);
   c.pyramid = dget<int>(d, "pyramid", 0);
+  c.ctu64 = dget<int>(d, "ctu64", 0);
   if (c.tu_inter_depth < 0 || c.tu_inter_depth > 1) throw std::runtime_error("HEVC: tu_inter_depth in 0..1");
   if (c.threads < 1 || c.threads > 256) throw std::runtime_error("HEVC: threads in 1..256");
   if (c.width <= 0 || c.height <= 0 || (c.width & 1) || (c.height & 1)) throw std::runtime_error("HEVC: bad size");

@@ -36,6 +36,15 @@ struct HevcConfig {
   int bframes = 0;             // > 0: B pictures between the anchors (DPB of 2 references, 1 reordered picture)
   int pyramid = 0;             // reference B pictures (DPB of 3 references, 2 reordered pictures)
   int tmvp = 0;                // sps_temporal_mvp_enabled_flag: temporal merge / AMVP candidates (needs FrameParams::col)
+  // 64x64 CTUs (x265 --ctu 64): the decision records stay per 32x32 block (CtuInfo / CuInfo as
+  // for 32x32 CTBs); the writer codes each CTU's four blocks in z-order (a block's quadtree one
+  // level down), one quantization group per 32x32 block (diff_cu_qp_delta_depth 1), SAO
+  // parameters from the CTU's first block, and a 64x64 skip CU where the four blocks are one
+  // uniform residual-free motion that is in the 64x64 merge list
+  int ctu64 = 0;
+  int ctb_log2() const { return ctu64 ? 6 : kCtbLog2; }
+  int wctu() const { return (coded_width() + (1 << ctb_log2()) - 1) >> ctb_log2(); }
+  int hctu() const { return (coded_height() + (1 << ctb_log2()) - 1) >> ctb_log2(); }
   int coded_width() const { return (width + kCtb - 1) / kCtb * kCtb; }
   int coded_height() const { return (height + kCtb - 1) / kCtb * kCtb; }
   int wctb() const { return coded_width() / kCtb; }

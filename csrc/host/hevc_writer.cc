@@ -133,7 +133,7 @@ std::vector<uint8_t> hevc_parameter_sets(const HevcConfig& c) {
     bw.put_ue(num_reorder(c));   // sps_max_num_reorder_pics
     bw.put_ue(0);                // sps_max_latency_increase_plus1
     bw.put_ue(kMinCbLog2 - 3);   // log2_min_luma_coding_block_size_minus3
-    bw.put_ue(kCtbLog2 - kMinCbLog2);  // log2_diff_max_min_luma_coding_block_size
+    bw.put_ue(c.ctb_log2() - kMinCbLog2);  // log2_diff_max_min_luma_coding_block_size
     bw.put_ue(0);                // log2_min_luma_transform_block_size_minus2 (4x4)
     bw.put_ue(3);                // log2_diff_max_min_luma_transform_block_size (32x32)
     bw.put_ue(c.tu_inter_depth);  // max_transform_hierarchy_depth_inter (x265 --tu-inter-depth)
@@ -171,7 +171,8 @@ std::vector<uint8_t> hevc_parameter_sets(const HevcConfig& c) {
     bw.put_bit(0);  // constrained_intra_pred_flag
     bw.put_bit(0);  // transform_skip_enabled_flag
     bw.put_bit(c.cu_qp_delta ? 1 : 0);  // cu_qp_delta_enabled_flag
-    if (c.cu_qp_delta) bw.put_ue(0);      // diff_cu_qp_delta_depth: one quantization group per CTB
+    // diff_cu_qp_delta_depth: one quantization group per 32x32 block (per CTB, or 4 per 64x64 CTU)
+    if (c.cu_qp_delta) bw.put_ue(c.ctu64 ? 1 : 0);
     bw.put_se(0);   // pps_cb_qp_offset
     bw.put_se(0);   // pps_cr_qp_offset
     bw.put_bit(0);  // pps_slice_chroma_qp_offsets_present_flag
@@ -217,7 +218,9 @@ struct PicState {
   std::vector<int8_t> depth, skip, pred, mode4;  // mode4: luma intra mode per 4x4 block (NxN PUs)
   std::vector<Motion> mot;
   std::vector<uint8_t> coded;
-  explicit PicState(size_t n) : depth(n, 0), skip(n, 0), pred(n, 0), mode4(4 * n, 1), mot(n), coded(n, 0) {}
+  std::vector<int8_t> qpy;  // QpY of the CU covering the granule (QP prediction inside a 64x64 CTU)
+  explicit PicState(size_t n)
+      : depth(n, 0), skip(n, 0), pred(n, 0), mode4(4 * n, 1), mot(n), coded(n, 0), qpy(n, 0) {}
 };
 
 struct Writer {
@@ -240,11 +243,14 @@ struct Writer {
   std::vector<int8_t>&depth, &skip, &pred, &mode4;
   std::vector<Motion>& mot;
   std::vector<uint8_t>& coded;
+  std::vector<int8_t>& qpy;
   // cu_qp_delta state (7.4.9.14, 8.6.1): qPY_PREV of the next quantization group (the
   // slice QP at the start of the slice and, with WPP, of every CTB row: a Writer codes
   // one row substream or the whole slice), and whether the current CTB coded its delta
   int qp_prev = 0, qp_ctb = 0;
   bool qp_coded = false;
+  int qp_pred_cur = 0;  // qPY_PRED of the current quantization group (8.6.1)
+  int L = kCtbLog2;     // CtbLog2SizeY
 
   // packed coefficient source (hevc_write_slice_packed): per CTB the sub-block maps
   // (nzmap[2 * ci]: luma bit by * 8 + bx; nzmap[2 * ci + 1]: Cb bits 0-15, Cr bits 16-31,
@@ -256,7 +262,7 @@ struct Writer {
   Writer(const HevcConfig& cfg, const HevcFrameParams& f, const CtuInfo* ct, const CuInfo* cu_, const int16_t* cy,
          const int16_t* cb, const int16_t* cr, CabacEncoder& enc, PicState& ps)
       : c(cfg), fp(f), ctu(ct), cu(cu_), e(enc), depth(ps.depth), skip(ps.skip), pred(ps.pred), mode4(ps.mode4),
-        mot(ps.mot), coded(ps.coded) {
+        mot(ps.mot), coded(ps.coded), qpy(ps.qpy) {
     coef[0] = cy;
     coef[1] = cb;
     coef[2] = cr;
@@ -271,6 +277,7 @@ struct Writer {
     tmvp = inter_slice && c.tmvp;
     col_l1 = bslice;
     no_backward = ref_poc(0) <= fp.poc && (!bslice || ref_poc(1) <= fp.poc);
+    L = c.ctb_log2();
     init_contexts(ctx, bslice ? 2 : (inter_slice ? 1 : 0), fp.qp);
     qp_prev = fp.qp;
   }
@@ -300,14 +307,19 @@ struct Writer {
     return true;
   }
 
+  // SAO parameters of CTU (cx, cy): those of its first 32x32 record block
+  const CtuInfo& ctu_sao(int cx, int cy) const {
+    const int k = c.ctu64 ? 1 : 0;
+    return ctu[(cy << k) * wctb + (cx << k)];
+  }
   void write_sao(int rx, int ry) {
-    const CtuInfo& t = ctu[ry * wctb + rx];
-    if (rx > 0 && same_sao(t, ctu[ry * wctb + rx - 1])) {
+    const CtuInfo& t = ctu_sao(rx, ry);
+    if (rx > 0 && same_sao(t, ctu_sao(rx - 1, ry))) {
       e.encode(1, ctx[CTX_SAO_MERGE]);
       return;
     }
     if (rx > 0) e.encode(0, ctx[CTX_SAO_MERGE]);
-    if (ry > 0 && same_sao(t, ctu[(ry - 1) * wctb + rx])) {
+    if (ry > 0 && same_sao(t, ctu_sao(rx, ry - 1))) {
       e.encode(1, ctx[CTX_SAO_MERGE]);
       return;
     }
@@ -719,7 +731,7 @@ struct Writer {
   bool temporal(int x, int y, int n, int X, Mv* out) const {
     if (!tmvp) return false;
     const int xbr = x + n, ybr = y + n;
-    if ((y >> kCtbLog2) == (ybr >> kCtbLog2) && ybr < H && xbr < W && col_at((xbr >> 4) << 4, (ybr >> 4) << 4, X, out))
+    if ((y >> L) == (ybr >> L) && ybr < H && xbr < W && col_at((xbr >> 4) << 4, (ybr >> 4) << 4, X, out))
       return true;
     return col_at(((x + (n >> 1)) >> 4) << 4, ((y + (n >> 1)) >> 4) << 4, X, out);
   }
@@ -844,7 +856,15 @@ struct Writer {
     if (dir != DIR_BI) e.encode(dir == DIR_L1, ctx[CTX_INTER_PRED + 4]);
   }
 
+  // a CU, then the QpY of its granules (8.6.1: the quantization group's prediction until a
+  // cu_qp_delta has been coded, the coded QP from then on)
   void write_cu(int x, int y, int log2, int d) {
+    write_cu_body(x, y, log2, d);
+    const int q = qp_coded ? qp_ctb : qp_pred_cur, n = 1 << log2;
+    for (int yy = y; yy < y + n; yy += 8)
+      for (int xx = x; xx < x + n; xx += 8) qpy[g(xx, yy)] = static_cast<int8_t>(q);
+  }
+  void write_cu_body(int x, int y, int log2, int d) {
     const int n = 1 << log2;
     const CuInfo& ci = cu_at(x, y);
     const bool cb_y = any_nonzero(0, x, y, n);
@@ -921,7 +941,7 @@ struct Writer {
       auto cand_of = [&](int xn, int yn, bool above) {
         if (xn >= x && yn >= y) return m[(xn - x >= h) + 2 * (yn - y >= h)];
         if (!avail(xn, yn) || pred[g(xn, yn)] != CU_INTRA) return 1;
-        if (above && (yn >> kCtbLog2) != (yk >> kCtbLog2)) return 1;
+        if (above && (yn >> L) != (yk >> L)) return 1;
         return static_cast<int>(mode4[g4(xn, yn)]);
       };
       const int ca = cand_of(xk - 1, yk, false), cb = cand_of(xk, yk - 1, true);
@@ -1055,7 +1075,7 @@ struct Writer {
   // cu_qp_delta_abs (9.3.3.10: TR prefix cMax 5, ctxInc 0 then 1; EG0 bypass suffix) and
   // the bypass sign, in the first TU of the CTB with a coded block
   void write_qp_delta() {
-    const int d = qp_ctb - qp_prev;
+    const int d = qp_ctb - qp_pred_cur;
     const int qbd = 6 * (c.bit_depth - 8);
     if (d < -(26 + qbd / 2) || d > 25 + qbd / 2) throw std::runtime_error("HEVC: CuQpDeltaVal out of range");
     const int a = std::abs(d), pre = std::min(a, 5);
@@ -1075,37 +1095,109 @@ struct Writer {
     while (k--) e.bypass((v >> k) & 1);
   }
 
-  // coding_quadtree (7.3.8.4) of one CTB
-  void write_ctu(int rx, int ry) {
-    write_ctu_tree(rx, ry);
-    // QpY of the CTB's last CU: the coded QP, or the prediction when no TU carried a delta
-    if (c.cu_qp_delta && qp_coded) qp_prev = qp_ctb;
+  // qPY_PRED of the quantization group at (xq, yq) (8.6.1): the average of the QpY left of and
+  // above it when those lie in the same CTB, each replaced by qPY_PREV otherwise
+  int qg_pred(int xq, int yq) const {
+    auto same_ctb = [&](int x, int y) { return (x >> L) == (xq >> L) && (y >> L) == (yq >> L); };
+    const int qa = (avail(xq - 1, yq) && same_ctb(xq - 1, yq)) ? qpy[g(xq - 1, yq)] : qp_prev;
+    const int qb = (avail(xq, yq - 1) && same_ctb(xq, yq - 1)) ? qpy[g(xq, yq - 1)] : qp_prev;
+    return (qa + qb + 1) >> 1;
   }
-  void write_ctu_tree(int rx, int ry) {
+
+  // coding_quadtree (7.3.8.4) of one CTU (CTU coordinates)
+  void write_ctu(int cx, int cy) {
+    if (!c.ctu64) {
+      write_block_tree(cx, cy, 0);
+      return;
+    }
+    const int x0 = cx << 6, y0 = cy << 6;
+    const bool inside = x0 + 64 <= W && y0 + 64 <= H;
+    const bool one = inside && cu64_ok(cx, cy);
+    if (inside) e.encode(!one, ctx[CTX_SPLIT_CU + split_ctx(x0, y0, 0)]);  // else the split is inferred
+    if (one) {
+      write_cu64_skip(x0, y0);
+      return;
+    }
+    for (int q = 0; q < 4; ++q) {
+      const int bx = (x0 >> 5) + (q & 1), by = (y0 >> 5) + (q >> 1);
+      if ((bx << 5) < W && (by << 5) < H) write_block_tree(bx, by, 1);
+    }
+  }
+
+  int split_ctx(int x, int y, int d) const {
+    return (avail(x - 1, y) && depth[g(x - 1, y)] > d) + (avail(x, y - 1) && depth[g(x, y - 1)] > d);
+  }
+
+  // one 32x32 record block = one quantization group; dofs: its depth in the CTU quadtree
+  void write_block_tree(int rx, int ry, int dofs) {
     const CtuInfo& t = ctu[ry * wctb + rx];
     const int x0 = rx * kCtb, y0 = ry * kCtb;
     qp_ctb = t.qp;
     qp_coded = false;
+    qp_pred_cur = c.cu_qp_delta ? qg_pred(x0, y0) : fp.qp;
     scan_ctb_nz(x0, y0);
-    auto split_ctx = [&](int x, int y, int d) {
-      return (avail(x - 1, y) && depth[g(x - 1, y)] > d) + (avail(x, y - 1) && depth[g(x, y - 1)] > d);
-    };
     const bool s32 = t.split & 1;
-    e.encode(s32, ctx[CTX_SPLIT_CU + split_ctx(x0, y0, 0)]);
+    e.encode(s32, ctx[CTX_SPLIT_CU + split_ctx(x0, y0, dofs)]);
     if (!s32) {
-      write_cu(x0, y0, 5, 0);
-      return;
-    }
-    for (int q = 0; q < 4; ++q) {
-      const int x1 = x0 + (q & 1) * 16, y1 = y0 + (q >> 1) * 16;
-      const bool s16 = (t.split >> (1 + q)) & 1;
-      e.encode(s16, ctx[CTX_SPLIT_CU + split_ctx(x1, y1, 1)]);
-      if (!s16) {
-        write_cu(x1, y1, 4, 1);
-        continue;
+      write_cu(x0, y0, 5, dofs);
+    } else {
+      for (int q = 0; q < 4; ++q) {
+        const int x1 = x0 + (q & 1) * 16, y1 = y0 + (q >> 1) * 16;
+        const bool s16 = (t.split >> (1 + q)) & 1;
+        e.encode(s16, ctx[CTX_SPLIT_CU + split_ctx(x1, y1, dofs + 1)]);
+        if (!s16) {
+          write_cu(x1, y1, 4, dofs + 1);
+          continue;
+        }
+        for (int r = 0; r < 4; ++r) write_cu(x1 + (r & 1) * 8, y1 + (r >> 1) * 8, 3, dofs + 2);
       }
-      for (int r = 0; r < 4; ++r) write_cu(x1 + (r & 1) * 8, y1 + (r >> 1) * 8, 3, 2);
     }
+    // qPY_PREV of the next quantization group: the QpY of this group's last CU
+    if (c.cu_qp_delta) qp_prev = qp_coded ? qp_ctb : qp_pred_cur;
+  }
+
+  // a 64x64 skip CU stands for the CTU's four blocks when each is one 32x32 inter CU, all with
+  // one motion, no level anywhere, and that motion is in the 64x64 CU's merge list (the
+  // reconstruction is the same: motion compensation is per sample and every inner edge has
+  // boundary strength 0)
+  int cu64_midx = -1;
+  bool cu64_ok(int cx, int cy) {
+    const int x0 = cx << 6, y0 = cy << 6;
+    if (!inter_slice) return false;
+    Motion m0{};
+    for (int q = 0; q < 4; ++q) {
+      const int bx = (x0 >> 5) + (q & 1), by = (y0 >> 5) + (q >> 1);
+      const CtuInfo& t = ctu[by * wctb + bx];
+      const CuInfo& ci = cu[static_cast<size_t>(by * wctb + bx) * kCusPerCtb];
+      if ((t.split & 1) || ci.pred != CU_INTER) return false;
+      Motion m{static_cast<uint8_t>(cu_dir(ci)), {{ci.mv[0], ci.mv[1]}, {ci.mv1[0], ci.mv1[1]}}};
+      if (!(m.dir & DIR_L0)) m.m[0] = Mv{0, 0};
+      if (!(m.dir & DIR_L1)) m.m[1] = Mv{0, 0};
+      if (q == 0) m0 = m;
+      else if (!(m == m0)) return false;
+      scan_ctb_nz(bx << 5, by << 5);
+      if (nz_luma || nz_chroma[0] || nz_chroma[1]) return false;
+    }
+    Motion ml[5];
+    const int nm = merge_list(x0, y0, 64, ml);
+    cu64_midx = -1;
+    for (int k = 0; k < nm && cu64_midx < 0; ++k)
+      if (ml[k] == m0) cu64_midx = k;
+    cu64_mot = m0;
+    return cu64_midx >= 0;
+  }
+  Motion cu64_mot;
+  void write_cu64_skip(int x0, int y0) {
+    const int skip_ctx = (avail(x0 - 1, y0) && skip[g(x0 - 1, y0)]) + (avail(x0, y0 - 1) && skip[g(x0, y0 - 1)]);
+    e.encode(1, ctx[CTX_CU_SKIP + skip_ctx]);
+    write_merge_idx(cu64_midx);
+    mark(x0, y0, 64, 0, 1, CU_INTER, 1, cu64_mot);
+    ++st.skip_cus;
+    // one quantization group per CU at least as large as the group: QpY = the prediction
+    const int q = c.cu_qp_delta ? qg_pred(x0, y0) : fp.qp;
+    for (int yy = y0; yy < y0 + 64; yy += 8)
+      for (int xx = x0; xx < x0 + 64; xx += 8) qpy[g(xx, yy)] = static_cast<int8_t>(q);
+    if (c.cu_qp_delta) qp_prev = q;
   }
 };
 
@@ -1185,7 +1277,8 @@ std::vector<uint8_t> hevc_write_slice(const HevcConfig& c, const HevcFrameParams
     bw.put_ue(5 - c.max_merge);  // five_minus_max_num_merge_cand
   }
   bw.put_se(fp.qp - 26);      // slice_qp_delta (init_qp 26)
-  const int wctb = c.wctb(), hctb = c.hctb(), n = wctb * hctb;
+  // CTUs (64x64 with ctu64, else the 32x32 record blocks themselves)
+  const int wctb = c.wctu(), hctb = c.hctu(), n = wctb * hctb;
   PicState ps(static_cast<size_t>(c.coded_width() / 8) * (c.coded_height() / 8));
   HevcSliceStats total;
   std::vector<uint8_t> data;  // slice_segment_data() (RBSP, before emulation prevention)

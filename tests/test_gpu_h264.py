@@ -187,7 +187,7 @@ def test_gpu_scenecut_codes_cut_frames_intra(host):
     for r in res:
         pics = host.decode(r.bitstream)
         kinds = np.asarray(pics[cut]["mb_kind"])
-        assert np.isin(kinds, [0, 1, 4]).all()          # I4x4 / I16x16 / I_PCM only
+        assert np.isin(kinds, [0, 1, 4, 8]).all()       # I4x4 / I16x16 / I_PCM / I8x8 only
         inter = [2, 3, 5, 6, 7, 9, 10, 11, 12, 13]  # P and B kinds: the cut is an anchor
         assert np.isin(np.asarray(pics[cut + 1]["mb_kind"]), inter).mean() > 0.5
         assert r.psnr_y > 30
