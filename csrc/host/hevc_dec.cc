@@ -509,10 +509,13 @@ struct HevcStreamDecoder::Impl {
         d.scaling.assign(sl.f.begin(), sl.f.end());
       }
     }
-    enc_rec = opt.enc_records && log2_ctb == kCtbLog2 && log2_min_cb == kMinCbLog2;
+    // encoder records: per 32x32 block (the encoder's record unit) for 32x32 CTBs and for 64x64
+    // CTUs over a picture of whole 32x32 blocks
+    enc_rec = opt.enc_records && log2_min_cb == kMinCbLog2 &&
+              (log2_ctb == kCtbLog2 || (log2_ctb == 6 && W % 32 == 0 && H % 32 == 0));
     if (enc_rec) {
-      d.ctu.assign(nctb, CtuInfo{});
-      d.cu.assign(static_cast<size_t>(nctb) * kCusPerCtb, CuInfo{});
+      d.ctu.assign(static_cast<size_t>(W / 32) * (H / 32), CtuInfo{});
+      d.cu.assign(static_cast<size_t>(W / 32) * (H / 32) * kCusPerCtb, CuInfo{});
       d.coef_y.assign(n4 * 16, 0);
       d.coef_cb.assign(n4 * 4, 0);
       d.coef_cr.assign(n4 * 4, 0);
@@ -879,16 +882,20 @@ struct HevcStreamDecoder::Impl {
     if (!sh.sao_luma) t.type[0] = 0;
     if (!sh.sao_chroma) t.type[1] = t.type[2] = 0;
     if (opt.gpu_records) dp->sao[ctb_addr_rs] = t;
-    if (enc_rec) {
-      CtuInfo& c = dp->ctu[ctb_addr_rs];
-      c.sao_type[0] = t.type[0];
-      c.sao_type[1] = t.type[1];
-      c.sao_class[0] = t.eo[0];
-      c.sao_class[1] = t.eo[1];
-      for (int ci = 0; ci < 3; ++ci) {
-        c.sao_band[ci] = t.band[ci];
-        for (int i = 0; i < 4; ++i) c.sao_off[ci][i] = t.off[ci][i];
-      }
+    if (enc_rec) {  // every 32x32 record block of the CTB carries its parameters
+      const int x0 = (ctb_addr_rs % wctb) << log2_ctb, y0 = (ctb_addr_rs / wctb) << log2_ctb;
+      for (int y = y0; y < std::min(H, y0 + ctb); y += 32)
+        for (int x = x0; x < std::min(W, x0 + ctb); x += 32) {
+          CtuInfo& c = enc_blk(x, y);
+          c.sao_type[0] = t.type[0];
+          c.sao_type[1] = t.type[1];
+          c.sao_class[0] = t.eo[0];
+          c.sao_class[1] = t.eo[1];
+          for (int ci = 0; ci < 3; ++ci) {
+            c.sao_band[ci] = t.band[ci];
+            for (int i = 0; i < 4; ++i) c.sao_off[ci][i] = t.off[ci][i];
+          }
+        }
     }
   }
 
@@ -904,12 +911,12 @@ struct HevcStreamDecoder::Impl {
     } else {
       split = log2 > log2_min_cb;
     }
-    if (pps->cu_qp_delta && log2 >= log2_min_qg) start_qg(x0, y0);
+    if (pps->cu_qp_delta && log2 >= log2_min_qg) start_qg(x0, y0, n);
     if (split) {
-      if (enc_rec) {
-        CtuInfo& t = dp->ctu[ctb_addr_rs];
-        if (log2 == log2_ctb) t.split |= 1;
-        else if (log2 == log2_ctb - 1) t.split |= static_cast<uint8_t>(1 << (1 + ((x0 & 31) >= 16) + 2 * ((y0 & 31) >= 16)));
+      if (enc_rec) {  // split bits of the 32x32 record block (a 64x64 split has no bit)
+        CtuInfo& t = enc_blk(x0, y0);
+        if (log2 == 5) t.split |= 1;
+        else if (log2 == 4) t.split |= static_cast<uint8_t>(1 << (1 + ((x0 & 31) >= 16) + 2 * ((y0 & 31) >= 16)));
       }
       const int h = n >> 1;
       for (int q = 0; q < 4; ++q) {
@@ -921,8 +928,12 @@ struct HevcStreamDecoder::Impl {
     coding_unit(x0, y0, log2, depth);
   }
 
-  // 8.6.1: a quantization group starts
-  void start_qg(int x0, int y0) {
+  // 8.6.1: a quantization group starts (n: the size of the coding quadtree node it starts at)
+  int qg_x = 0, qg_y = 0, qg_n = 32;
+  void start_qg(int x0, int y0, int n) {
+    qg_x = x0;
+    qg_y = y0;
+    qg_n = n;
     qp_delta_coded = false;
     const int cm = ~(ctb - 1);
     auto nb = [&](int x, int y) {
@@ -931,12 +942,18 @@ struct HevcStreamDecoder::Impl {
     };
     qg_pred = (nb(x0 - 1, y0) + nb(x0, y0 - 1) + 1) >> 1;
     cu_qp = qg_pred;
-    if (enc_rec && (x0 & (ctb - 1)) == 0 && (y0 & (ctb - 1)) == 0) {
-      CtuInfo& t = dp->ctu[ctb_addr_rs];
-      t.qp = static_cast<int8_t>(qg_pred);
-      t.qp_pred = static_cast<int8_t>(qg_pred);
-      t.qp_first = 16;
-    }
+    if (enc_rec && (x0 & 31) == 0 && (y0 & 31) == 0)
+      for_qg_blocks([&](CtuInfo& t) {
+        t.qp = static_cast<int8_t>(qg_pred);
+        t.qp_pred = static_cast<int8_t>(qg_pred);
+        t.qp_first = 16;
+      });
+  }
+  // the 32x32 record blocks of the current quantization group (one, or four for a 64x64 node)
+  template <class F>
+  void for_qg_blocks(F f) {
+    for (int y = qg_y; y < std::min(H, qg_y + std::max(qg_n, 32)); y += 32)
+      for (int x = qg_x; x < std::min(W, qg_x + std::max(qg_n, 32)); x += 32) f(enc_blk(x, y));
   }
 
   // ======================================================================== coding unit (7.3.8.5)
@@ -1585,11 +1602,11 @@ struct HevcStreamDecoder::Impl {
     if (d < -(26 + qp_bd / 2) || d > 25 + qp_bd / 2) fail("CuQpDeltaVal out of range");
     qp_delta_coded = true;
     cu_qp = ((qg_pred + d + 52 + 2 * qp_bd) % (52 + qp_bd)) - qp_bd;
-    if (enc_rec) {
-      CtuInfo& t = dp->ctu[ctb_addr_rs];
-      t.qp = static_cast<int8_t>(cu_qp);
-      t.qp_first = static_cast<uint8_t>(zorder8((x0 & 31) >> 3, (y0 & 31) >> 3));
-    }
+    if (enc_rec)
+      for_qg_blocks([&](CtuInfo& t) {
+        t.qp = static_cast<int8_t>(cu_qp);
+        t.qp_first = static_cast<uint8_t>(zorder8((x0 & 31) >> 3, (y0 & 31) >> 3));
+      });
   }
 
   int qp_prime(int cidx) const {
@@ -2433,9 +2450,10 @@ struct HevcStreamDecoder::Impl {
     }
   }
 
-  // ---------------------------------------------------------------- encoder records (32x32 CTBs)
+  // ---------------------------------------------------------------- encoder records (32x32 blocks)
+  CtuInfo& enc_blk(int x, int y) { return dp->ctu[static_cast<size_t>(y >> 5) * (W / 32) + (x >> 5)]; }
   CuInfo& enc_cu_at(int x, int y) {
-    return dp->cu[static_cast<size_t>((y >> kCtbLog2) * wctb + (x >> kCtbLog2)) * kCusPerCtb + zorder8((x & 31) >> 3, (y & 31) >> 3)];
+    return dp->cu[(static_cast<size_t>(y >> 5) * (W / 32) + (x >> 5)) * kCusPerCtb + zorder8((x & 31) >> 3, (y & 31) >> 3)];
   }
   void enc_cu(int x0, int y0, int n, int pred, int pcm) {
     (void)pcm;

@@ -46,13 +46,15 @@ def _levels(rng, n: int, density: float) -> np.ndarray:
 def random_records(rng, width: int, height: int, pslice: bool, bit_depth: int = 8, density: float = 0.08,
                    intra_in_p: float = 0.2, mv_range: int = 64, sao: bool = True, ctb_qp: tuple | None = None,
                    nxn: float = 0.0, tu_split: float = 0.0, force_split: int | None = None, bslice: bool = False,
-                   mv_pool: int = 0):
+                   mv_pool: int = 0, uniform64: float = 0.0):
     """``ctb_qp = (qp, spread)``: per-CTB QPs qp + U[-spread, spread] (cu_qp_delta streams);
     ``nxn``: probability of an 8x8 intra CU being split into four 4x4 PUs; ``tu_split``: of a
     16x16 / 32x32 inter CU coding its residual as four quarter TUs (needs tu_inter_depth 1);
     ``bslice``: inter CUs predict from list 0, list 1 or both (CuInfo.dir, mv1); ``mv_pool`` > 0:
     vectors drawn from that many values, so merge candidates (spatial, temporal, combined
-    bi-predictive, zero) match often."""
+    bi-predictive, zero) match often; ``uniform64``: probability that a 64x64-aligned group of
+    four blocks is one residual-free inter motion (the CTU-64 writer codes it as a 64x64 skip CU
+    when the motion is a merge candidate)."""
     pool = rng.integers(-mv_range, mv_range + 1, (max(1, mv_pool), 2)).astype(np.int16) if mv_pool else None
 
     def rand_mv():
@@ -128,6 +130,26 @@ def random_records(rng, width: int, height: int, pslice: bool, bit_depth: int = 
             cy[Y:Y + n, X:X + n] = _levels(rng, n, density)
             cb[Y // 2:(Y + n) // 2, X // 2:(X + n) // 2] = _levels(rng, n // 2, density)
             cr[Y // 2:(Y + n) // 2, X // 2:(X + n) // 2] = _levels(rng, n // 2, density)
+    if uniform64 > 0 and pslice:
+        for gy in range(0, hc - 1, 2):
+            for gx in range(0, wc - 1, 2):
+                if rng.random() >= uniform64:
+                    continue
+                rec = np.zeros(16, np.uint8)
+                rec[0], rec[3] = 1, 2 << 1   # inter, 32x32 CU
+                mv = rand_mv() if rng.random() < 0.5 else np.zeros(2, np.int16)
+                rec[4:8] = mv.view(np.uint8)
+                if bslice:
+                    rec[12] = 1
+                for by in (gy, gy + 1):
+                    for bx in (gx, gx + 1):
+                        i = by * wc + bx
+                        ctu[i, 0] = 0
+                        cu[i * 16:(i + 1) * 16] = rec
+                Y, X = gy * CTB, gx * CTB
+                cy[Y:Y + 64, X:X + 64] = 0
+                cb[Y // 2:Y // 2 + 32, X // 2:X // 2 + 32] = 0
+                cr[Y // 2:Y // 2 + 32, X // 2:X // 2 + 32] = 0
     return ctu, cu, cy, cb, cr
 
 

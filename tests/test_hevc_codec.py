@@ -273,3 +273,45 @@ def test_hevc_writer_rejects_bad_b_params(host):
         host.hevc_write_slice(cfg, dict(idr=0, poc=2, qp=30, slice_type=0, ref_poc0=0, ref_poc1=4), *r)
     with pytest.raises(RuntimeError, match="direction"):   # list-1 motion in a P slice
         host.hevc_write_slice(dict(width=64, height=64), dict(idr=0, poc=1, qp=30, slice_type=1), *r)
+
+
+@pytest.mark.parametrize("w,h,wpp,seed", [(128, 128, 0, 0), (96, 96, 1, 1), (160, 96, 1, 2), (224, 160, 0, 3)])
+def test_hevc_ctu64_roundtrip(host, w, h, wpp, seed):
+    """64x64 CTUs (x265 --ctu 64) over the encoder's 32x32 record blocks: blocks in z-order
+    inside each CTU, partial CTUs at the picture edges (inferred splits), one quantization
+    group per 32x32 block with the in-CTU QP prediction (8.6.1), CTU-level SAO, WPP rows of
+    CTUs, and 64x64 skip CUs where four blocks share one residual-free merge motion.  The
+    decoder recovers levels, CU types, vectors and every block's coded QP."""
+    cfg = dict(ctu64=1, wpp=wpp, threads=2, cu_qp_delta=1)
+    s, recs = random_stream(host, w, h, 3, seed=seed, host_cfg=cfg, qp_spread=4, uniform64=0.5, mv_pool=2,
+                            density=0.03)
+    pics = host.hevc_decode(s)
+    assert len(pics) == 3
+    n64 = 0
+    for p, (ctu, cu, cy, cb, cr) in zip(pics, recs):
+        assert np.array_equal(p["coef_y"], cy) and np.array_equal(p["coef_cb"], cb) and np.array_equal(p["coef_cr"], cr)
+        inter = cu[:, 0] == 1
+        assert np.array_equal(p["cu"][:, 0], cu[:, 0])
+        assert np.array_equal(p["cu"][inter, 4:8], cu[inter, 4:8])
+        W = cy.shape[1]
+        for i in range(len(ctu)):
+            X, Y = (i % (W // 32)) * 32, (i // (W // 32)) * 32
+            if cy[Y:Y + 32, X:X + 32].any() or cb[Y // 2:Y // 2 + 16, X // 2:X // 2 + 16].any():
+                assert p["ctu"][i, 1] == ctu[i, 1]     # a block with levels is coded at its own QP
+        n64 += int((((p["cu"][:, 3] >> 1) & 3) == 3).sum())
+    assert n64 > 0   # some 64x64 skip CUs
+
+
+@pytest.mark.parametrize("seed,pyramid", [(0, 1), (1, 0)])
+def test_hevc_ctu64_b_gop_roundtrip(host, seed, pyramid):
+    """CTU 64 with B pictures: TMVP's bottom-right candidate stays inside the 64-row CTU line,
+    merge / AMVP neighbours follow the 64x64 z-scan availability."""
+    from govideocompressor_amd.utils.hevc_synth import random_gop_stream
+
+    s, recs = random_gop_stream(host, 160, 128, 9, seed=seed, host_cfg=dict(ctu64=1, wpp=1, threads=2), mv_pool=2,
+                                uniform64=0.4, density=0.03, pyramid=bool(pyramid))
+    pics = host.hevc_decode(s)
+    for p, (ctu, cu, cy, cb, cr) in zip(pics, recs):
+        assert np.array_equal(p["coef_y"], cy)
+        inter = cu[:, 0] == 1
+        assert np.array_equal(p["cu"][inter, 4:12], cu[inter, 4:12])
