@@ -299,7 +299,8 @@ def test_hevc_ctu64_roundtrip(host, w, h, wpp, seed):
             if cy[Y:Y + 32, X:X + 32].any() or cb[Y // 2:Y // 2 + 16, X // 2:X // 2 + 16].any():
                 assert p["ctu"][i, 1] == ctu[i, 1]     # a block with levels is coded at its own QP
         n64 += int((((p["cu"][:, 3] >> 1) & 3) == 3).sum())
-    assert n64 > 0   # some 64x64 skip CUs
+    if (w // 64) * (h // 64) >= 2:
+        assert n64 > 0   # some 64x64 skip CUs
 
 
 @pytest.mark.parametrize("seed,pyramid", [(0, 1), (1, 0)])
