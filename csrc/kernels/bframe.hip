@@ -26,14 +26,19 @@ using h264::MbHeader;
 
 constexpr int kHpMargin = 4;  // me_halfpel_planes margin (csrc/kernels/me.hip)
 
+constexpr int kMaxRefs = 4;  // list-0 pictures an encoder P picture may reference (x264 --ref)
+
 struct BDirectArgs {
   Geom g;
-  const MbHeader* col;  // [B, nmb] records of RefPicList1[0] (a P anchor)
-  int dsf;              // DistScaleFactor; ignored when direct_copy
-  int direct_copy;      // td == 0: mvL0 = mvCol, mvL1 = 0
-  int16_t* dmv;         // [B, nmb, 2, 4, 2] direct vectors (list, quadrant, xy)
-  int16_t* pm0;         // [B, nmb, 2] ME predictor L0 (mean of the direct vectors)
-  int16_t* pm1;         // [B, nmb, 2] ME predictor L1
+  const MbHeader* col;      // [B, nmb] records of RefPicList1[0] (a P anchor)
+  // per refIdxL0 r = refIdxCol (the anchor's list 0 and the B picture's list 0 order the same
+  // past anchors, so MapColToList0 is the identity): DistScaleFactor, ignored when direct_copy
+  int dsf[kMaxRefs];
+  int direct_copy[kMaxRefs];  // td == 0: mvL0 = mvCol, mvL1 = 0
+  int16_t* dmv;             // [B, nmb, 2, 4, 2] direct vectors (list, quadrant, xy)
+  int8_t* dref;             // [B, nmb, 4] refIdxL0 of each quadrant's direct prediction (nullable: all 0)
+  int16_t* pm0;             // [B, nmb, 2] ME predictor L0 (mean of the direct vectors)
+  int16_t* pm1;             // [B, nmb, 2] ME predictor L1
 };
 
 __global__ __launch_bounds__(256) void b_direct_mv(BDirectArgs a) {
@@ -44,25 +49,30 @@ __global__ __launch_bounds__(256) void b_direct_mv(BDirectArgs a) {
   const MbHeader& c = a.col[o];
   const bool intra = h264::mbk_is_intra(c.kind);
   int v[2][4][2];
+  int rq[4];
   int s[2][2] = {{0, 0}, {0, 0}};
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     // direct_8x8_inference: the corner 4x4 block of co-located quadrant q, i.e. its vector;
     // a P anchor predicts from list 0 only
-    const int cx = intra || c.ref[0][q] < 0 ? 0 : c.mv[0][q][0];
-    const int cy = intra || c.ref[0][q] < 0 ? 0 : c.mv[0][q][1];
+    const bool none = intra || c.ref[0][q] < 0;
+    const int cx = none ? 0 : c.mv[0][q][0];
+    const int cy = none ? 0 : c.mv[0][q][1];
+    const int r = none ? 0 : min(static_cast<int>(c.ref[0][q]), kMaxRefs - 1);
+    rq[q] = r;
     int l0x, l0y;
-    if (a.direct_copy) {
+    const int dcp = a.direct_copy[r], dsf = a.dsf[r];
+    if (dcp) {
       l0x = cx;
       l0y = cy;
     } else {
-      l0x = (a.dsf * cx + 128) >> 8;
-      l0y = (a.dsf * cy + 128) >> 8;
+      l0x = (dsf * cx + 128) >> 8;
+      l0y = (dsf * cy + 128) >> 8;
     }
     v[0][q][0] = l0x;
     v[0][q][1] = l0y;
-    v[1][q][0] = a.direct_copy ? 0 : l0x - cx;
-    v[1][q][1] = a.direct_copy ? 0 : l0y - cy;
+    v[1][q][0] = dcp ? 0 : l0x - cx;
+    v[1][q][1] = dcp ? 0 : l0y - cy;
 #pragma unroll
     for (int l = 0; l < 2; ++l) {
       s[l][0] += v[l][q][0];
@@ -77,6 +87,11 @@ __global__ __launch_bounds__(256) void b_direct_mv(BDirectArgs a) {
       d[l * 8 + q * 2] = static_cast<int16_t>(v[l][q][0]);
       d[l * 8 + q * 2 + 1] = static_cast<int16_t>(v[l][q][1]);
     }
+  if (a.dref) {
+    const uint32_t rw = static_cast<uint32_t>(rq[0]) | (static_cast<uint32_t>(rq[1]) << 8) |
+                        (static_cast<uint32_t>(rq[2]) << 16) | (static_cast<uint32_t>(rq[3]) << 24);
+    *reinterpret_cast<uint32_t*>(a.dref + o * 4) = rw;
+  }
   a.pm0[o * 2] = static_cast<int16_t>((s[0][0] + 2) >> 2);
   a.pm0[o * 2 + 1] = static_cast<int16_t>((s[0][1] + 2) >> 2);
   a.pm1[o * 2] = static_cast<int16_t>((s[1][0] + 2) >> 2);
@@ -98,7 +113,14 @@ struct BDecideArgs {
   MbHeader* hdr;                   // out: kind / ref / mv
   uint8_t* pred_out;               // out: [B, nmb, 256]
   int* cost_out;                   // out: [B, nmb] the winner's cost (vs the intra estimate)
-  int w1;                          // implicit bi-prediction weight of list 1 (32: plain average)
+  // implicit bi-prediction weight of list 1 (32: plain average) per refIdxL0 (the list-1
+  // picture is always RefPicList1[0]); the ME candidates use entry 0
+  int w1[kMaxRefs];
+  // direct prediction from RefPicList0[r] (r = dref per quadrant, nullable: all 0):
+  // luma / half-sample planes of every list-0 picture (entry 0 = ref0 / hp0)
+  const int8_t* dref;
+  const uint8_t* ref0k[kMaxRefs];
+  const uint8_t* hp0k[kMaxRefs];
 };
 
 // Quarter-sample luma position (xf, yf) = two (plane, du, dv) taps averaged (the G/b/h/j
@@ -192,9 +214,13 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   const int m0x = a.mv0[o * 2], m0y = a.mv0[o * 2 + 1], m1x = a.mv1[o * 2], m1y = a.mv1[o * 2 + 1];
   const uint32_t src = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y) * W + X);
   // direct: per-quadrant vectors of both lists; bi: the two ME vectors
-  const uint32_t pd = wavg4b(mc4(G0, H0, W, H, X, Y, dm[q * 2], dm[q * 2 + 1]),
-                             mc4(G1, H1, W, H, X, Y, dm[8 + q * 2], dm[8 + q * 2 + 1]), a.w1);
-  const uint32_t pb = wavg4b(mc4(G0, H0, W, H, X, Y, m0x, m0y), mc4(G1, H1, W, H, X, Y, m1x, m1y), a.w1);
+  uint32_t drw = 0;  // refIdxL0 of the four direct quadrants (bytes)
+  if (a.dref) drw = *reinterpret_cast<const uint32_t*>(a.dref + o * 4);
+  const int dr = (drw >> (8 * q)) & 255;
+  const uint8_t *GD = dr ? a.ref0k[dr] + yo : G0, *HD = dr ? a.hp0k[dr] + ho : H0;
+  const uint32_t pd = wavg4b(mc4(GD, HD, W, H, X, Y, dm[q * 2], dm[q * 2 + 1]),
+                             mc4(G1, H1, W, H, X, Y, dm[8 + q * 2], dm[8 + q * 2 + 1]), a.w1[dr]);
+  const uint32_t pb = wavg4b(mc4(G0, H0, W, H, X, Y, m0x, m0y), mc4(G1, H1, W, H, X, Y, m1x, m1y), a.w1[0]);
   __shared__ int s_res[2][256];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -237,7 +263,7 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
     h->kind = mode == 0 ? h264::MBK_BDIRECT : h264::MBK_B16x16;
     h->sub_direct = 0;
     const bool u0 = mode != 2, u1 = mode != 1;
-    const uint32_t r0 = u0 ? 0u : 0xFFFFFFFFu, r1 = u1 ? 0u : 0xFFFFFFFFu;
+    const uint32_t r0 = mode == 0 ? drw : (u0 ? 0u : 0xFFFFFFFFu), r1 = u1 ? 0u : 0xFFFFFFFFu;
     *reinterpret_cast<uint2*>(&h->ref[0][0]) = make_uint2(r0, r1);
     uint32_t w[2][4];
 #pragma unroll
@@ -876,14 +902,18 @@ __global__ __launch_bounds__(64) void p_part8x8(PPartArgs a) {
 
 using namespace mivc::gpu;
 
-extern "C" void mivc_launch_b_direct(int B, int wmb, int hmb, const void* col, int dsf, int direct_copy, int16_t* dmv,
-                                     int16_t* pm0, int16_t* pm1, void* stream) {
+extern "C" void mivc_launch_b_direct(int B, int wmb, int hmb, const void* col, const int* dsf, const int* direct_copy,
+                                     int nref, int16_t* dmv, int8_t* dref, int16_t* pm0, int16_t* pm1, void* stream) {
   BDirectArgs a;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.col = static_cast<const MbHeader*>(col);
-  a.dsf = dsf;
-  a.direct_copy = direct_copy;
+  for (int r = 0; r < kMaxRefs; ++r) {  // refIdxCol beyond the list: the last entry (never produced)
+    const int rr = r < nref ? r : nref - 1;
+    a.dsf[r] = dsf[rr];
+    a.direct_copy[r] = direct_copy[rr];
+  }
   a.dmv = dmv;
+  a.dref = dref;
   a.pm0 = pm0;
   a.pm1 = pm1;
   hipLaunchKernelGGL(b_direct_mv, dim3((wmb * hmb + 255) / 256, B), dim3(256), 0, static_cast<hipStream_t>(stream), a);
@@ -894,9 +924,16 @@ extern "C" void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src
                                      const int16_t* mv1, const int* cost0, const int* cost1, const uint8_t* pred0,
                                      const uint8_t* pred1, const int16_t* pm0, const int16_t* pm1, const int16_t* dmv,
                                      const int* qp, const int8_t* aq, void* hdr, uint8_t* pred_out, int* cost_out,
-                                     void* stream, int w1) {
+                                     void* stream, const int* w1, int nref, const int8_t* dref,
+                                     const uint8_t* const* ref0k, const uint8_t* const* hp0k) {
   BDecideArgs a;
-  a.w1 = w1;
+  for (int r = 0; r < kMaxRefs; ++r) {
+    const int rr = r < nref ? r : nref - 1;
+    a.w1[r] = w1[rr];
+    a.ref0k[r] = rr == 0 ? ref0 : ref0k[rr];
+    a.hp0k[r] = rr == 0 ? hp0 : hp0k[rr];
+  }
+  a.dref = dref;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.src_y = src_y;
   a.ref0 = ref0;

@@ -23,9 +23,13 @@ void mivc_launch_rgb_to_i420(const uint8_t* rgb, int w, int h, int nframes, uint
                              void* stream);
 void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref_y, const int16_t* pred_mv,
                     int16_t* out_mv, int* out_cost, uint8_t* out_pred, int* out_intra_cost, const int* qp, int range,
-                    int subpel, uint8_t* hp, const int8_t* aq, int planes_ready, int early_sad, void* stream);
-void mivc_launch_b_direct(int B, int wmb, int hmb, const void* col, int dsf, int direct_copy, int16_t* dmv,
-                          int16_t* pm0, int16_t* pm1, void* stream);
+                    int subpel, uint8_t* hp, const int8_t* aq, int planes_ready, int early_sad, void* stream,
+                    const int* gate_cost, int gate_thresh, const int16_t* cost_mv);
+void mivc_launch_me_ref_select(int B, int wmb, int hmb, int nref, int16_t* mv, int16_t* mv8, int* cost, uint8_t* pred,
+                               const int16_t* xmv, const int* xcost, const uint8_t* xpred, int8_t* mref, const int* qp,
+                               const int8_t* aq, void* stream);
+void mivc_launch_b_direct(int B, int wmb, int hmb, const void* col, const int* dsf, const int* direct_copy, int nref,
+                          int16_t* dmv, int8_t* dref, int16_t* pm0, int16_t* pm1, void* stream);
 void mivc_launch_p_refine(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref, const uint8_t* hp,
                           const int16_t* mv_in, int16_t* mv_out, int* cost, const int16_t* pm, uint8_t* pred,
                           const int* qp, const int8_t* aq, void* stream);
@@ -33,7 +37,8 @@ void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src_y, const u
                           const uint8_t* hp0, const uint8_t* hp1, const int16_t* mv0, const int16_t* mv1,
                           const int* cost0, const int* cost1, const uint8_t* pred0, const uint8_t* pred1,
                           const int16_t* pm0, const int16_t* pm1, const int16_t* dmv, const int* qp, const int8_t* aq,
-                          void* hdr, uint8_t* pred_out, int* cost_out, void* stream, int w1);
+                          void* hdr, uint8_t* pred_out, int* cost_out, void* stream, const int* w1, int nref,
+                          const int8_t* dref, const uint8_t* const* ref0k, const uint8_t* const* hp0k);
 void mivc_launch_aq_offsets(int B, int wmb, int hmb, const uint8_t* sy, const uint8_t* su, const uint8_t* sv,
                             float strength, const float* extra, long long extra_stride, int8_t* out, void* stream);
 void mivc_launch_mbtree(int B, int F, int lbw, int lbh, const int* blk_cost, const int* blk_mv, void* prop,
@@ -47,7 +52,8 @@ void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t* src_y, con
                               const int16_t* mv, const int* me_cost, const int* intra_cost, const int* qp,
                               int chroma_qp_offset, void* hdr, int16_t* coef, uint8_t* nz, uint8_t* intra_flag,
                               int* intra_count, const int8_t* aq, const uint8_t* ref1_u, const uint8_t* ref1_v,
-                              int bmode, int t8, const int16_t* mv8, void* stream, int w1);
+                              int bmode, int t8, const int16_t* mv8, void* stream, const int* w1, int nref,
+                              const uint8_t* const* xref_u, const uint8_t* const* xref_v, const int8_t* mref);
 void mivc_launch_p_part8(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref, const uint8_t* hp,
                          const int16_t* mv, const int16_t* pm, int* cost, uint8_t* pred, int16_t* mv8, const int* qp,
                          const int8_t* aq, int overhead, int min_satd, void* stream);
@@ -161,20 +167,34 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("me", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref, uintptr_t pred_mv, uintptr_t out_mv,
                  uintptr_t out_cost, uintptr_t out_pred, uintptr_t out_intra, uintptr_t qp, int range, int subpel,
-                 uintptr_t stream, uintptr_t hp, uintptr_t aq, int planes_ready, int early_sad) {
+                 uintptr_t stream, uintptr_t hp, uintptr_t aq, int planes_ready, int early_sad, uintptr_t gate_cost,
+                 int gate_thresh, uintptr_t cost_mv) {
     if (planes_ready && !hp) throw std::invalid_argument("me: planes_ready needs the hp buffer");
     mivc_launch_me(B, wmb, hmb, P<uint8_t>(src), P<uint8_t>(ref), P<int16_t>(pred_mv), P<int16_t>(out_mv),
                    P<int>(out_cost), P<uint8_t>(out_pred), P<int>(out_intra), P<int>(qp), range, subpel,
-                   P<uint8_t>(hp), P<int8_t>(aq), planes_ready, early_sad, S(stream));
+                   P<uint8_t>(hp), P<int8_t>(aq), planes_ready, early_sad, S(stream), P<int>(gate_cost), gate_thresh,
+                   P<int16_t>(cost_mv));
   }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("src"), py::arg("ref"), py::arg("pred_mv"),
      py::arg("out_mv"), py::arg("out_cost"), py::arg("out_pred"), py::arg("out_intra"), py::arg("qp"),
      py::arg("range"), py::arg("subpel"), py::arg("stream"), py::arg("hp") = 0, py::arg("aq") = 0,
-     py::arg("planes_ready") = 0, py::arg("early_sad") = 0);
-  m.def("b_direct", [](int B, int wmb, int hmb, uintptr_t col, int dsf, int direct_copy, uintptr_t dmv, uintptr_t pm0,
-                       uintptr_t pm1, uintptr_t stream) {
-    mivc_launch_b_direct(B, wmb, hmb, P<void>(col), dsf, direct_copy, P<int16_t>(dmv), P<int16_t>(pm0),
-                         P<int16_t>(pm1), S(stream));
+     py::arg("planes_ready") = 0, py::arg("early_sad") = 0, py::arg("gate_cost") = 0, py::arg("gate_thresh") = 0,
+     py::arg("cost_mv") = 0);
+  m.def("me_ref_select", [](int B, int wmb, int hmb, int nref, uintptr_t mv, uintptr_t mv8, uintptr_t cost,
+                            uintptr_t pred, uintptr_t xmv, uintptr_t xcost, uintptr_t xpred, uintptr_t mref,
+                            uintptr_t qp, uintptr_t aq, uintptr_t stream) {
+    if (nref < 2 || nref > 4) throw std::invalid_argument("me_ref_select: nref in 2..4");
+    mivc_launch_me_ref_select(B, wmb, hmb, nref, P<int16_t>(mv), P<int16_t>(mv8), P<int>(cost), P<uint8_t>(pred),
+                              P<int16_t>(xmv), P<int>(xcost), P<uint8_t>(xpred), P<int8_t>(mref), P<int>(qp),
+                              P<int8_t>(aq), S(stream));
   });
+  m.def("b_direct", [](int B, int wmb, int hmb, uintptr_t col, std::vector<int> dsf, std::vector<int> direct_copy,
+                       uintptr_t dmv, uintptr_t pm0, uintptr_t pm1, uintptr_t stream, uintptr_t dref) {
+    if (dsf.empty() || dsf.size() > 4 || dsf.size() != direct_copy.size())
+      throw std::invalid_argument("b_direct: one (dsf, direct_copy) pair per list-0 picture, at most 4");
+    mivc_launch_b_direct(B, wmb, hmb, P<void>(col), dsf.data(), direct_copy.data(), static_cast<int>(dsf.size()),
+                         P<int16_t>(dmv), P<int8_t>(dref), P<int16_t>(pm0), P<int16_t>(pm1), S(stream));
+  }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("col"), py::arg("dsf"), py::arg("direct_copy"),
+     py::arg("dmv"), py::arg("pm0"), py::arg("pm1"), py::arg("stream"), py::arg("dref") = 0);
   m.def("p_refine", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref, uintptr_t hp, uintptr_t mv_in,
                        uintptr_t mv_out, uintptr_t cost, uintptr_t pm, uintptr_t pred, uintptr_t qp, uintptr_t aq,
                        uintptr_t stream) {
@@ -186,16 +206,32 @@ PYBIND11_MODULE(_hip, m) {
   m.def("b_decide", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref0, uintptr_t ref1, uintptr_t hp0,
                        uintptr_t hp1, uintptr_t mv0, uintptr_t mv1, uintptr_t cost0, uintptr_t cost1, uintptr_t pred0,
                        uintptr_t pred1, uintptr_t pm0, uintptr_t pm1, uintptr_t dmv, uintptr_t qp, uintptr_t aq,
-                       uintptr_t hdr, uintptr_t pred_out, uintptr_t cost_out, uintptr_t stream, int w1) {
-    if (w1 < -64 || w1 > 128) throw std::invalid_argument("b_decide: implicit weight w1 in -64..128");
+                       uintptr_t hdr, uintptr_t pred_out, uintptr_t cost_out, uintptr_t stream, std::vector<int> w1,
+                       uintptr_t dref, std::vector<uintptr_t> ref0k, std::vector<uintptr_t> hp0k) {
+    // w1: implicit list-1 weight per list-0 picture; ref0k / hp0k: luma / half-sample planes of
+    // RefPicList0[1..] (direct prediction of quadrants whose co-located block used a farther picture)
+    if (w1.empty() || w1.size() > 4) throw std::invalid_argument("b_decide: one implicit weight per list-0 picture");
+    for (int v : w1)
+      if (v < -64 || v > 128) throw std::invalid_argument("b_decide: implicit weight w1 in -64..128");
+    const size_t n = w1.size();
+    if (n > 1 && (ref0k.size() != n - 1 || hp0k.size() != n - 1 || !dref))
+      throw std::invalid_argument("b_decide: several list-0 pictures need their planes and the direct refIdx");
+    const uint8_t* rk[4] = {nullptr, nullptr, nullptr, nullptr};
+    const uint8_t* hk[4] = {nullptr, nullptr, nullptr, nullptr};
+    for (size_t i = 1; i < n; ++i) {
+      rk[i] = P<uint8_t>(ref0k[i - 1]);
+      hk[i] = P<uint8_t>(hp0k[i - 1]);
+    }
     mivc_launch_b_decide(B, wmb, hmb, P<uint8_t>(src), P<uint8_t>(ref0), P<uint8_t>(ref1), P<uint8_t>(hp0),
                          P<uint8_t>(hp1), P<int16_t>(mv0), P<int16_t>(mv1), P<int>(cost0), P<int>(cost1),
                          P<uint8_t>(pred0), P<uint8_t>(pred1), P<int16_t>(pm0), P<int16_t>(pm1), P<int16_t>(dmv),
-                         P<int>(qp), P<int8_t>(aq), P<void>(hdr), P<uint8_t>(pred_out), P<int>(cost_out), S(stream), w1);
+                         P<int>(qp), P<int8_t>(aq), P<void>(hdr), P<uint8_t>(pred_out), P<int>(cost_out), S(stream),
+                         w1.data(), static_cast<int>(n), n > 1 ? P<int8_t>(dref) : nullptr, rk, hk);
   }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("src"), py::arg("ref0"), py::arg("ref1"), py::arg("hp0"),
      py::arg("hp1"), py::arg("mv0"), py::arg("mv1"), py::arg("cost0"), py::arg("cost1"), py::arg("pred0"),
      py::arg("pred1"), py::arg("pm0"), py::arg("pm1"), py::arg("dmv"), py::arg("qp"), py::arg("aq"), py::arg("hdr"),
-     py::arg("pred_out"), py::arg("cost_out"), py::arg("stream"), py::arg("w1") = 32);
+     py::arg("pred_out"), py::arg("cost_out"), py::arg("stream"), py::arg("w1") = std::vector<int>{32},
+     py::arg("dref") = 0, py::arg("ref0k") = std::vector<uintptr_t>{}, py::arg("hp0k") = std::vector<uintptr_t>{});
   m.def("aq_offsets", [](int B, int wmb, int hmb, uintptr_t sy, uintptr_t su, uintptr_t sv, float strength,
                          uintptr_t out, uintptr_t stream, uintptr_t extra, long long extra_stride) {
     mivc_launch_aq_offsets(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), strength, P<float>(extra),
@@ -220,20 +256,35 @@ PYBIND11_MODULE(_hip, m) {
            uintptr_t fv, uintptr_t ry, uintptr_t ru, uintptr_t rv, uintptr_t pred, uintptr_t mv, uintptr_t me_cost,
            uintptr_t intra_cost, uintptr_t qp, int cqo, uintptr_t hdr, uintptr_t coef, uintptr_t nz,
            uintptr_t intra_flag, uintptr_t intra_count, uintptr_t stream, uintptr_t aq, uintptr_t ref1_u,
-           uintptr_t ref1_v, int bmode, int t8, uintptr_t mv8, int w1) {
+           uintptr_t ref1_v, int bmode, int t8, uintptr_t mv8, std::vector<int> w1, std::vector<uintptr_t> xref_u,
+           std::vector<uintptr_t> xref_v, uintptr_t mref) {
+          // xref_u / xref_v: chroma of RefPicList0[1..]; w1: implicit list-1 weight per list-0 picture
           if (bmode && (!ref1_u || !ref1_v)) throw std::invalid_argument("encode_inter: B mode needs the list-1 chroma");
+          const size_t n = xref_u.size() + 1;
+          if (n > 4 || xref_v.size() != xref_u.size()) throw std::invalid_argument("encode_inter: at most 4 list-0 pictures");
+          if (n > 1 && !bmode && !mref) throw std::invalid_argument("encode_inter: P pictures with several references need mref");
+          std::vector<int> w(n, w1.empty() ? 32 : w1[0]);
+          for (size_t i = 0; i < n && i < w1.size(); ++i) w[i] = w1[i];
+          const uint8_t* xu[4] = {nullptr, nullptr, nullptr, nullptr};
+          const uint8_t* xv[4] = {nullptr, nullptr, nullptr, nullptr};
+          for (size_t i = 1; i < n; ++i) {
+            xu[i] = P<uint8_t>(xref_u[i - 1]);
+            xv[i] = P<uint8_t>(xref_v[i - 1]);
+          }
           mivc_launch_encode_inter(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), P<uint8_t>(fy),
                                    P<uint8_t>(fu), P<uint8_t>(fv), P<uint8_t>(ry), P<uint8_t>(ru), P<uint8_t>(rv),
                                    P<uint8_t>(pred), P<int16_t>(mv), P<int>(me_cost), P<int>(intra_cost), P<int>(qp),
                                    cqo, P<void>(hdr), P<int16_t>(coef), P<uint8_t>(nz), P<uint8_t>(intra_flag),
                                    P<int>(intra_count), P<int8_t>(aq), P<uint8_t>(ref1_u), P<uint8_t>(ref1_v), bmode,
-                                   t8, P<int16_t>(mv8), S(stream), w1);
+                                   t8, P<int16_t>(mv8), S(stream), w.data(), static_cast<int>(n), xu, xv,
+                                   bmode ? nullptr : P<int8_t>(mref));
         }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("sy"), py::arg("su"), py::arg("sv"), py::arg("fy"),
         py::arg("fu"), py::arg("fv"), py::arg("ry"), py::arg("ru"), py::arg("rv"), py::arg("pred"), py::arg("mv"),
         py::arg("me_cost"), py::arg("intra_cost"), py::arg("qp"), py::arg("cqo"), py::arg("hdr"), py::arg("coef"),
         py::arg("nz"), py::arg("intra_flag"), py::arg("intra_count"), py::arg("stream"), py::arg("aq") = 0,
         py::arg("ref1_u") = 0, py::arg("ref1_v") = 0, py::arg("bmode") = 0, py::arg("t8") = 0, py::arg("mv8") = 0,
-        py::arg("w1") = 32);
+        py::arg("w1") = std::vector<int>{32}, py::arg("xref_u") = std::vector<uintptr_t>{},
+        py::arg("xref_v") = std::vector<uintptr_t>{}, py::arg("mref") = 0);
   m.def("p_part8", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref, uintptr_t hp, uintptr_t mv, uintptr_t pm,
                       uintptr_t cost, uintptr_t pred, uintptr_t mv8, uintptr_t qp, uintptr_t aq, int overhead,
                       int min_satd, uintptr_t stream) {

@@ -39,8 +39,14 @@ struct InterArgs {
   // (list 1), averaged for bi-prediction; pred_y is b_decide's luma prediction
   const uint8_t *ref1_u, *ref1_v;
   int bmode;
-  int w1;                  // B pictures: implicit bi-prediction weight of list 1 (32: average)
+  int w1[4];               // B pictures: implicit bi-prediction weight of list 1 per refIdxL0 (32: average)
   int t8;                  // High profile: choose the 8x8 transform per MB (sa8d < satd, as x264)
+  // several list-0 pictures (x264 --ref): chroma of RefPicList0[r] (entry 0 = ref_u / ref_v);
+  // P pictures take r from mref (the reference selection, nullable: 0), B pictures from the
+  // records b_decide wrote
+  const uint8_t* refs_u[4];
+  const uint8_t* refs_v[4];
+  const int8_t* mref;      // [B, nmb] (P pictures)
 };
 
 
@@ -320,20 +326,23 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
     if (!a.bmode) {
       // the 4x4 chroma block cb covers luma quadrant cb (its partition's vector)
       const int cmx = a.mv8 ? a.mv8[o * 8 + cb * 2] : mvx, cmy = a.mv8 ? a.mv8[o * 8 + cb * 2 + 1] : mvy;
-      chroma_mc4x4((comp == 0 ? a.ref_u : a.ref_v) + slot * g.csize(), cw, CH, px0, py0, cmx, cmy, pv);
+      const int r = a.mref ? a.mref[o] : 0;
+      chroma_mc4x4((comp == 0 ? a.refs_u[r] : a.refs_v[r]) + slot * g.csize(), cw, CH, px0, py0, cmx, cmy, pv);
     } else {
       // the 4x4 chroma block cb covers luma quadrant cb: its lists and vectors
-      const bool u0 = h->ref[0][cb] >= 0, u1 = h->ref[1][cb] >= 0;
+      const int r0 = h->ref[0][cb];
+      const bool u0 = r0 >= 0, u1 = h->ref[1][cb] >= 0;
+      const int w1 = a.w1[r0 & 3];
       int p1[4][4];
-      if (u0) chroma_mc4x4((comp == 0 ? a.ref_u : a.ref_v) + slot * g.csize(), cw, CH, px0, py0, h->mv[0][cb][0],
-                           h->mv[0][cb][1], pv);
+      if (u0) chroma_mc4x4((comp == 0 ? a.refs_u[r0 & 3] : a.refs_v[r0 & 3]) + slot * g.csize(), cw, CH, px0, py0,
+                           h->mv[0][cb][0], h->mv[0][cb][1], pv);
       if (u1) chroma_mc4x4((comp == 0 ? a.ref1_u : a.ref1_v) + slot * g.csize(), cw, CH, px0, py0,
                            h->mv[1][cb][0], h->mv[1][cb][1], p1);
 #pragma unroll
       for (int y = 0; y < 4; ++y)
 #pragma unroll
         for (int x = 0; x < 4; ++x)  // implicit weights (a.w1 = 32: the plain average)
-          pv[y][x] = u0 ? (u1 ? h264::clip1((pv[y][x] * (64 - a.w1) + p1[y][x] * a.w1 + 32) >> 6) : pv[y][x]) : p1[y][x];
+          pv[y][x] = u0 ? (u1 ? h264::clip1((pv[y][x] * (64 - w1) + p1[y][x] * w1 + 32) >> 6) : pv[y][x]) : p1[y][x];
     }
     uint32_t sw[4];
 #pragma unroll
@@ -512,7 +521,8 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
                                              : ((q4.x == q4.z && q4.y == q4.w) ? h264::MBK_P8x16 : h264::MBK_P8x8);
     uint4* mvp = reinterpret_cast<uint4*>(&h->mv[0][0][0]);  // 16-byte aligned
     mvp[0] = q4;
-    *reinterpret_cast<uint2*>(&h->ref[0][0]) = make_uint2(0u, 0xFFFFFFFFu);  // L0 ref 0, L1 unused
+    const uint32_t r = a.mref ? static_cast<uint32_t>(a.mref[o]) * 0x01010101u : 0u;
+    *reinterpret_cast<uint2*>(&h->ref[0][0]) = make_uint2(r, 0xFFFFFFFFu);  // L0 ref r, L1 unused
   }
 }
 
@@ -528,9 +538,17 @@ extern "C" void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t*
                                          const int* intra_cost, const int* qp, int chroma_qp_offset, void* hdr,
                                          int16_t* coef, uint8_t* nz, uint8_t* intra_flag, int* intra_count,
                                          const int8_t* aq, const uint8_t* ref1_u, const uint8_t* ref1_v, int bmode,
-                                         int t8, const int16_t* mv8, void* stream, int w1) {
+                                         int t8, const int16_t* mv8, void* stream, const int* w1, int nref,
+                                         const uint8_t* const* xref_u, const uint8_t* const* xref_v,
+                                         const int8_t* mref) {
   InterArgs a;
-  a.w1 = w1;
+  for (int r = 0; r < 4; ++r) {
+    const int rr = r < nref ? r : 0;
+    a.refs_u[r] = rr == 0 ? ref_u : xref_u[rr];
+    a.refs_v[r] = rr == 0 ? ref_v : xref_v[rr];
+  }
+  a.mref = mref;
+  for (int r = 0; r < 4; ++r) a.w1[r] = w1[r < nref ? r : 0];
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.src_y = src_y;
   a.src_u = src_u;

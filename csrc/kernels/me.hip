@@ -42,7 +42,17 @@ struct MeArgs {
   const uint8_t* hp;       // [B, 3, H + 8, W + 8] b / h / j half-sample planes of ref_y (margin 4)
   const int8_t* aq;        // [B, nmb] adaptive-quantisation QP offsets (nullable)
   int early_sad;           // > 0: skip the integer search when the best candidate's SAD <= this
+  // extra reference pictures (--ref > 1): MBs whose list-0[0] cost is already <= gate_thresh
+  // are not searched again (out_cost = kNoCost, nothing else written)
+  const int* gate_cost;    // [B, nmb] (nullable)
+  int gate_thresh;
+  // mvd costs against this vector instead of pred_mv (nullable): a farther picture's search is
+  // centred on the distance-scaled list-0[0] vector, while its mvd is coded against the
+  // neighbours' vectors (which mostly point to RefPicList0[0])
+  const int16_t* cost_mv;
 };
+
+constexpr int kNoCost = 0x3FFFFFFF;
 
 constexpr int kHpM = 4;  // half-sample plane margin (samples); coordinates clamp into it exactly
 
@@ -320,6 +330,13 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   const int R = a.range < MAXR ? a.range : MAXR;
 
   __shared__ MeShared<MAXR> S;
+  if (a.gate_cost) {
+    const size_t og = static_cast<size_t>(slot) * nmb + mb;
+    if (a.gate_cost[og] <= a.gate_thresh) {  // wave-uniform
+      if (lane == 0) a.out_cost[og] = kNoCost;
+      return;
+    }
+  }
 
   MPROF(0);
   // ---- phase 0: source MB, its intra neighbours, candidate vectors (one batch of loads)
@@ -337,6 +354,10 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
     pmy = pm[mb * 2 + 1];
     cand_x[0] = (pmx + 2) >> 2;
     cand_y[0] = (pmy + 2) >> 2;
+    if (a.cost_mv) {
+      pmx = a.cost_mv[(static_cast<size_t>(slot) * nmb + mb) * 2];
+      pmy = a.cost_mv[(static_cast<size_t>(slot) * nmb + mb) * 2 + 1];
+    }
     if (mx > 0) { cand_x[1] = (pm[(mb - 1) * 2] + 2) >> 2; cand_y[1] = (pm[(mb - 1) * 2 + 1] + 2) >> 2; }
     if (my > 0) { cand_x[2] = (pm[(mb - g.wmb) * 2] + 2) >> 2; cand_y[2] = (pm[(mb - g.wmb) * 2 + 1] + 2) >> 2; }
     if (mx < g.wmb - 1) { cand_x[3] = (pm[(mb + 1) * 2] + 2) >> 2; cand_y[3] = (pm[(mb + 1) * 2 + 1] + 2) >> 2; }
@@ -686,6 +707,63 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   }
   MPROF(9);
 }
+// Reference selection of P macroblocks (x264 --ref N): the list-0[0] decision (16x16 search,
+// P_Skip-aware refinement and 8x8 partitions: mv / mv8 / cost / pred) against the 16x16
+// searches of RefPicList0[1 .. nref-1]; cost + lambda * ref_idx bits (CABAC unary: about 1,
+// 3, 4, 5 bits).  A farther picture that wins overwrites the decision with its vector (one
+// partition), cost and luma prediction and records its index in mref.  One wave per MB.
+struct RefSelArgs {
+  Geom g;
+  int nref;
+  int16_t* mv;                 // [B, nmb, 2]
+  int16_t* mv8;                // [B, nmb, 4, 2] (nullable)
+  int* cost;                   // [B, nmb]
+  uint8_t* pred;               // [B, nmb, 256]
+  const int16_t* xmv;          // [nref - 1, B, nmb, 2]
+  const int* xcost;            // [nref - 1, B, nmb] (kNoCost: not searched)
+  const uint8_t* xpred;        // [nref - 1, B, nmb, 256]
+  int8_t* mref;                // [B, nmb]
+  const int* qp;               // [B]
+  const int8_t* aq;            // [B, nmb] (nullable)
+};
+
+__global__ __launch_bounds__(64) void me_ref_select(RefSelArgs a) {
+  const int nmb = a.g.nmb();
+  const int mb = blockIdx.x, slot = blockIdx.y, lane = threadIdx.x;
+  const size_t o = static_cast<size_t>(slot) * nmb + mb;
+  const size_t plane = static_cast<size_t>(a.g.B) * nmb;
+  const int qp = clampi(a.qp[slot] + (a.aq ? a.aq[o] : 0), 0, 51);
+  const int lambda = h264::kLambda[qp];
+  int best = a.cost[o] + lambda, bk = 0;
+  for (int k = 1; k < a.nref; ++k) {
+    const int c = a.xcost[(k - 1) * plane + o];
+    if (c >= kNoCost) continue;
+    const int ck = c + lambda * (k + 2);
+    if (ck < best) {
+      best = ck;
+      bk = k;
+    }
+  }
+  if (bk > 0) {
+    const size_t xo = (bk - 1) * plane + o;
+    reinterpret_cast<uint32_t*>(a.pred + o * 256)[lane] = reinterpret_cast<const uint32_t*>(a.xpred + xo * 256)[lane];
+    if (lane == 0) {
+      const int16_t vx = a.xmv[xo * 2], vy = a.xmv[xo * 2 + 1];
+      a.mv[o * 2] = vx;
+      a.mv[o * 2 + 1] = vy;
+      if (a.mv8) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          a.mv8[o * 8 + q * 2] = vx;
+          a.mv8[o * 8 + q * 2 + 1] = vy;
+        }
+      }
+      a.cost[o] = a.xcost[xo];
+    }
+  }
+  if (lane == 0) a.mref[o] = static_cast<int8_t>(bk);
+}
+
 #ifdef MIVC_ME_PROFILE
 extern "C" void mivc_me_prof_read(unsigned long long* out) {
   hipMemcpyFromSymbol(out, HIP_SYMBOL(g_me_prof), sizeof(unsigned long long) * 64 * 12);
@@ -708,7 +786,8 @@ extern "C" void mivc_launch_me_halfpel(int B, int W, int H, const uint8_t* ref_y
 extern "C" void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref_y,
                                const int16_t* pred_mv, int16_t* out_mv, int* out_cost, uint8_t* out_pred,
                                int* out_intra_cost, const int* qp, int range, int subpel, uint8_t* hp_buf,
-                               const int8_t* aq, int planes_ready, int early_sad, void* stream) {
+                               const int8_t* aq, int planes_ready, int early_sad, void* stream,
+                               const int* gate_cost, int gate_thresh, const int16_t* cost_mv) {
   // hp_buf: caller-owned [B, 3, H + 8, W + 8] (+64 bytes slack) half-sample plane scratch,
   // resident across frames; nullptr -> stream-ordered scratch for this call only.
   // planes_ready: hp_buf already holds ref_y's planes (an anchor's planes are built once
@@ -740,7 +819,29 @@ extern "C" void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, co
   a.hp = hp;
   a.aq = aq;
   a.early_sad = early_sad;
+  a.gate_cost = gate_cost;
+  a.gate_thresh = gate_thresh;
+  a.cost_mv = cost_mv;
   if (a.range <= 8) hipLaunchKernelGGL(me_p16x16<8>, dim3(wmb * hmb, B), dim3(64), 0, s, a);
   else hipLaunchKernelGGL(me_p16x16<kMaxR>, dim3(wmb * hmb, B), dim3(64), 0, s, a);
   if (!hp_buf) (void)hipFreeAsync(hp, s);
+}
+
+extern "C" void mivc_launch_me_ref_select(int B, int wmb, int hmb, int nref, int16_t* mv, int16_t* mv8, int* cost,
+                                          uint8_t* pred, const int16_t* xmv, const int* xcost, const uint8_t* xpred,
+                                          int8_t* mref, const int* qp, const int8_t* aq, void* stream) {
+  RefSelArgs a;
+  a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
+  a.nref = nref;
+  a.mv = mv;
+  a.mv8 = mv8;
+  a.cost = cost;
+  a.pred = pred;
+  a.xmv = xmv;
+  a.xcost = xcost;
+  a.xpred = xpred;
+  a.mref = mref;
+  a.qp = qp;
+  a.aq = aq;
+  hipLaunchKernelGGL(me_ref_select, dim3(wmb * hmb, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
 }

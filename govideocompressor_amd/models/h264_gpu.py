@@ -101,9 +101,20 @@ class H264Params:
     full_recon: bool = False
     # level_idc written in the SPS (-level); 0 = the lowest level the size / rate fits
     level_idc: int = 0
+    # x264 --ref 3 (its default): P macroblocks choose among the 3 latest anchors (ref_idx in
+    # the records; searches of the farther pictures seeded by the distance-scaled list-0[0]
+    # vector, radius ref_range); B pictures' temporal direct follows the co-located block's
+    # reference.  CABAC only (the Baseline CAVLC path keeps one reference).  ref_gate: MBs
+    # whose list-0[0] cost (SATD + lambda * bits) is <= ref_gate are not searched in the farther pictures
+    refs: int = int(os.environ.get("MIVC_REFS", 3))
+    ref_range: int = int(os.environ.get("MIVC_REF_RANGE", 4))
+    ref_gate: int = int(os.environ.get("MIVC_REF_GATE", 0))
 
     def eff_bframes(self) -> int:
         return max(0, int(self.bframes)) if self.cabac else 0
+
+    def eff_refs(self) -> int:
+        return max(1, min(4, int(self.refs))) if self.cabac else 1
 
     def eff_t8x8(self) -> bool:
         return bool(self.t8x8 and self.cabac)
@@ -115,7 +126,7 @@ class H264Params:
         return dict(width=self.width, height=self.height, fps=self.fps, qp=self.qp,
                     deblock=int(self.deblock), chroma_qp_offset=self.chroma_qp_offset,
                     vui=int(self.vui), cabac=int(self.cabac), bframes=self.eff_bframes(), t8x8=int(self.eff_t8x8()),
-                    weighted_bipred=2 if self.weightb else 0,
+                    weighted_bipred=2 if self.weightb else 0, refs=self.eff_refs(),
                     level_idc=int(self.level_idc))
 
     def profile_name(self) -> str:
@@ -123,7 +134,7 @@ class H264Params:
             return "Constrained Baseline CAVLC"
         nb = self.eff_bframes()
         return (("High CABAC 8x8dct" if self.eff_t8x8() else "Main CABAC") + (" i8x8" if self.eff_t8x8() and self.i8x8 else "")
-                + (" p8x8" if self.eff_partitions() else "")
+                + (" p8x8" if self.eff_partitions() else "") + (f" ref{self.eff_refs()}" if self.eff_refs() > 1 else "")
                 + (f" {nb}B temporal-direct" if nb else "") + (" weightb" if nb and self.weightb else ""))
 
     def frame_qps(self) -> tuple[int, int]:
@@ -220,9 +231,11 @@ class GpuH264Encoder:
 
         self.src = planes()
         self.nb = params.eff_bframes()
-        # anchors (I / P) alternate between rec[0] and rec[1]; B pictures (never referenced)
-        # reconstruct into rec[2]
-        self.rec = [planes(), planes()] + ([planes()] if self.nb else [])
+        # anchors (I / P) rotate over rec[0 .. na - 1] (na = refs + 1: the picture being coded and
+        # the refs anchors it may reference); B pictures (never referenced) reconstruct into rec[na]
+        self.nref = params.eff_refs()
+        self.na = self.nref + 1
+        self.rec = [planes() for _ in range(self.na)] + ([planes()] if self.nb else [])
         self.hdr = [torch.zeros((B, nmb, MB_HDR_BYTES), dtype=u8, device=dev) for _ in range(2)]
         self.coef = [torch.zeros((B, nmb, COEF_PER_MB), dtype=i16, device=dev) for _ in range(2)]
         self.nz = torch.zeros((B, nmb, 16), dtype=u8, device=dev)
@@ -235,7 +248,16 @@ class GpuH264Encoder:
         self.pred = torch.zeros((B, nmb, 256), dtype=u8, device=dev)
         # resident b / h / j half-sample planes of the two latest anchors (margin 4, + load
         # slack), built once per anchor and shared by the P and B pictures that reference it
-        self.me_hp = [torch.empty(B * 3 * (H + 8) * (W + 8) + 64, dtype=u8, device=dev) for _ in range(2)]
+        self.me_hp = [torch.empty(B * 3 * (H + 8) * (W + 8) + 64, dtype=u8, device=dev) for _ in range(self.na)]
+        if self.nref > 1:
+            # searches of RefPicList0[1 ..] (P pictures) and the reference choice per MB
+            K = self.nref - 1
+            self.xmv = torch.zeros((K, B, nmb, 2), dtype=i16, device=dev)
+            self.xcost = torch.zeros((K, B, nmb), dtype=i32, device=dev)
+            self.xpred = torch.zeros((K, B, nmb, 256), dtype=u8, device=dev)
+            self.xpm = torch.zeros((B, nmb, 2), dtype=i16, device=dev)
+            self.mref = torch.zeros((B, nmb), dtype=torch.int8, device=dev)
+            self.dref = torch.zeros((B, nmb, 4), dtype=torch.int8, device=dev)
         if self.nb:
             # B pictures: the list-1 search, temporal direct vectors and the mode decision
             self.mv1 = torch.zeros((B, nmb, 2), dtype=i16, device=dev)
@@ -254,6 +276,7 @@ class GpuH264Encoder:
         self.qp = torch.zeros((B,), dtype=i32, device=dev)
         self.err = torch.zeros((1,), dtype=i32, device=dev)
         self.p_intra_mbs = torch.zeros((), dtype=torch.int64, device=dev)  # intra MBs coded in P frames
+        self.far_ref_mbs = torch.zeros((), dtype=torch.int64, device=dev)  # P MBs choosing RefPicList0[1 ..]
         # pinned staging for the entropy stage (double-buffered)
         if entropy == "cpu":
             self.h_hdr = [torch.empty((B, nmb, MB_HDR_BYTES), dtype=u8).pin_memory() for _ in range(2)]
@@ -403,10 +426,11 @@ class GpuH264Encoder:
             with st("aq"):
                 self.hip.aq_offsets(B, wmb, hmb, sy, su, sv, float(self.p.aq_strength), aq, s, extra, stride)
         cqo = self.p.chroma_qp_offset
+        na = self.na
         if pic.kind == "P":
             fy, fu, fv = (P(x) for x in ref0)
             self.intra_count.zero_()
-            hp = P(self.me_hp[(pic.anchor - 1) & 1])
+            hp = P(self.me_hp[(pic.anchor - 1) % na])
             with st("me_p"):
                 self.hip.me(B, wmb, hmb, sy, fy, P(self.prev_mv), P(self.mv), P(self.me_cost), P(self.pred),
                             P(self.intra_cost), P(self.qp), self.p.me_range, self.p.subpel, s, hp, aq, 1,
@@ -423,27 +447,62 @@ class GpuH264Encoder:
                     self.hip.p_part8(B, wmb, hmb, sy, fy, hp, P(self.mv), P(self.prev_mv), P(self.me_cost), P(self.pred),
                                      P(self.mv8), P(self.qp), aq, int(self.p.part_overhead), int(self.p.part_min_satd), s)
                 mv8 = P(self.mv8)
+            self.prev_mv.copy_(self.mv)  # next P picture's predictors: the list-0[0] vectors
+            nr = self.n_l0(pic.anchor)
+            xu, xv = [], []
+            if nr > 1:
+                # farther anchors: 16x16 searches seeded by the list-0[0] vectors scaled by the
+                # temporal distance, then the per-MB choice (cost + ref_idx bits)
+                d0 = pic.d - self.anchor_d[pic.anchor - 1]
+                with st("me_ref"):
+                    for k in range(1, nr):
+                        a_k = pic.anchor - 1 - k
+                        rk = self.rec[a_k % na]
+                        scale = (pic.d - self.anchor_d[a_k]) / max(1, d0)
+                        self.xpm.copy_((self.mv.float() * scale).round_().clamp_(-2048, 2047))
+                        self.hip.me(B, wmb, hmb, sy, P(rk[0]), P(self.xpm), P(self.xmv[k - 1]), P(self.xcost[k - 1]),
+                                    P(self.xpred[k - 1]), 0, P(self.qp), int(self.p.ref_range), self.p.subpel, s,
+                                    P(self.me_hp[a_k % na]), aq, 1, self.p.p_early_sad, P(self.me_cost),
+                                    self._ref_gate(), P(self.prev_mv))
+                        xu.append(P(rk[1]))
+                        xv.append(P(rk[2]))
+                    self.hip.me_ref_select(B, wmb, hmb, nr, P(self.mv), mv8, P(self.me_cost), P(self.pred),
+                                           P(self.xmv), P(self.xcost), P(self.xpred), P(self.mref), P(self.qp), aq, s)
+                    self.far_ref_mbs += (self.mref > 0).sum()
             if cut is not None:
                 self.intra_cost.masked_fill_(cut[:, None], -1)  # intra beats any inter cost
             with st("inter"):
                 self.hip.encode_inter(B, wmb, hmb, sy, su, sv, fy, fu, fv, ry, ru, rv, P(self.pred), P(self.mv),
                                       P(self.me_cost), P(self.intra_cost), P(self.qp), cqo, P(hdr), P(coef),
                                       P(self.nz), P(self.intra_flag), P(self.intra_count), s, aq,
-                                      t8=int(self.p.eff_t8x8()), mv8=mv8)
-            self.prev_mv.copy_(self.mv)
+                                      t8=int(self.p.eff_t8x8()), mv8=mv8, xref_u=xu, xref_v=xv,
+                                      mref=P(self.mref) if nr > 1 else 0)
         elif pic.kind == "B":
             f0y, f0u, f0v = (P(x) for x in ref0)
             f1y, f1u, f1v = (P(x) for x in ref1)
-            hp0, hp1 = P(self.me_hp[(pic.l1_anchor - 1) & 1]), P(self.me_hp[pic.l1_anchor & 1])
-            dsf, copy = self._dist_scale(pic.poc, 2 * pic.l0, 2 * pic.l1)
-            # implicit bi-prediction weights (8.4.2.3.1): w1 = DistScaleFactor >> 2 unless out of range
-            w1 = 32
-            if self.p.weightb and not copy and -64 <= (dsf >> 2) <= 128:
-                w1 = dsf >> 2
+            hp0, hp1 = P(self.me_hp[(pic.l1_anchor - 1) % na]), P(self.me_hp[pic.l1_anchor % na])
+            # list 0 = the anchors before the picture, nearest first (the list-1 anchor's own list
+            # 0, so the co-located refIdx maps to itself); per entry: temporal-direct scale and
+            # implicit bi-prediction weight (8.4.2.3.1: w1 = DistScaleFactor >> 2 unless out of range)
+            nr = self.n_l0(pic.l1_anchor)
+            dsfs, copies, w1s, r0y, r0h, xu, xv = [], [], [], [], [], [], []
+            for k in range(nr):
+                a_k = pic.l1_anchor - 1 - k
+                dsf, copy = self._dist_scale(pic.poc, 2 * self.anchor_d[a_k], 2 * pic.l1)
+                dsfs.append(dsf)
+                copies.append(copy)
+                w1s.append(dsf >> 2 if self.p.weightb and not copy and -64 <= (dsf >> 2) <= 128 else 32)
+                if k:
+                    rk = self.rec[a_k % na]
+                    r0y.append(P(rk[0]))
+                    r0h.append(P(self.me_hp[a_k % na]))
+                    xu.append(P(rk[1]))
+                    xv.append(P(rk[2]))
             self.intra_count.zero_()
             br = self.p.b_me_range
             with st("me_b"):
-                self.hip.b_direct(B, wmb, hmb, P(self.col_hdr), dsf, copy, P(self.dmv), P(self.pm0), P(self.pm1), s)
+                self.hip.b_direct(B, wmb, hmb, P(self.col_hdr), dsfs, copies, P(self.dmv), P(self.pm0), P(self.pm1), s,
+                                  P(self.dref) if nr > 1 else 0)
                 self.hip.me(B, wmb, hmb, sy, f0y, P(self.pm0), P(self.mv), P(self.me_cost), P(self.pred),
                             P(self.intra_cost), P(self.qp), br, self.p.subpel, s, hp0, aq, 1, self.p.b_early_sad)
                 # the L1 search skips the open-loop intra estimate the L0 search just wrote
@@ -452,14 +511,15 @@ class GpuH264Encoder:
             with st("b_decide"):
                 self.hip.b_decide(B, wmb, hmb, sy, f0y, f1y, hp0, hp1, P(self.mv), P(self.mv1), P(self.me_cost),
                                   P(self.me_cost1), P(self.pred), P(self.pred1), P(self.pm0), P(self.pm1),
-                                  P(self.dmv), P(self.qp), aq, P(hdr), P(self.pred_b), P(self.cost_b), s, w1)
+                                  P(self.dmv), P(self.qp), aq, P(hdr), P(self.pred_b), P(self.cost_b), s, w1s,
+                                  P(self.dref) if nr > 1 else 0, r0y, r0h)
             if cut is not None:
                 self.intra_cost.masked_fill_(cut[:, None], -1)
             with st("inter"):
                 self.hip.encode_inter(B, wmb, hmb, sy, su, sv, f0y, f0u, f0v, ry, ru, rv, P(self.pred_b), P(self.mv),
                                       P(self.cost_b), P(self.intra_cost), P(self.qp), cqo, P(hdr), P(coef),
                                       P(self.nz), P(self.intra_flag), P(self.intra_count), s, aq, f1u, f1v, 1,
-                                      int(self.p.eff_t8x8()), 0, w1)
+                                      int(self.p.eff_t8x8()), 0, w1s, xu, xv)
         if pic.kind != "I":
             self.p_intra_mbs += self.intra_count.sum()
             flag_ptr, count_ptr = P(self.intra_flag), P(self.intra_count)
@@ -487,14 +547,27 @@ class GpuH264Encoder:
             # the anchor's half-sample planes (shared by every picture that references it) and,
             # for the B pictures after it, its motion as the temporal-direct co-located field
             with st("halfpel"):
-                self.hip.me_halfpel(B, self.W, self.H, ry, P(self.me_hp[pic.anchor & 1]), s)
+                self.hip.me_halfpel(B, self.W, self.H, ry, P(self.me_hp[pic.anchor % na]), s)
             if self.nb and pic.kind == "P":
                 self.col_hdr.copy_(hdr)
 
     # ------------------------------------------------------------------ entropy (GPU CAVLC)
+    def n_l0(self, anchor: int) -> int:
+        """List-0 size of the P picture with anchor ordinal ``anchor`` and of the B pictures
+        before it: the anchors coded before it, at most eff_refs."""
+        return max(1, min(self.nref, anchor))
+
+    def _num_ref_l0(self, pic: PicPlan) -> int:
+        return {"I": 1, "P": self.n_l0(pic.anchor), "B": self.n_l0(pic.l1_anchor)}[pic.kind]
+
+    def _ref_gate(self) -> int:
+        return int(self.p.ref_gate)
+
     def _frame_params(self, b: int, pic: PicPlan, qp_frame: int, idr_ids: list[int]) -> dict:
+        n0 = self._num_ref_l0(pic)
         return dict(idr=int(pic.kind == "I"), frame_num=pic.frame_num, idr_pic_id=idr_ids[b] & 0xFFFF, qp=qp_frame,
-                    slice_type=pic.slice_type, nal_ref_idc=pic.nal_ref_idc, poc=pic.poc, direct_spatial=0)
+                    slice_type=pic.slice_type, nal_ref_idc=pic.nal_ref_idc, poc=pic.poc, direct_spatial=0,
+                    **({"num_ref_l0": n0, "num_ref_l1": 1} if pic.kind != "I" else {}))
 
     @staticmethod
     def _cabac_groups(F: int, G: int) -> list[tuple[int, int]]:
@@ -528,7 +601,8 @@ class GpuH264Encoder:
         self.hip.cabac_bin(B, self.wmb, self.hmb, P(self.hdr[k]), P(self.coef[k]), P(self.cab_mask), P(self.cab_nb),
                            P(self.cab_cnt), P(self.cab_off), P(self.cab_tot), P(self.cab_pool[r]), self.cab_pool_cap,
                            self.cab_pool_used[r].data_ptr(), self.cab_base[r][j * B:].data_ptr(),
-                           self.cab_total[r][j * B:].data_ptr(), P(qp_dev), pic.slice_type, 1, 1, int(self.p.eff_t8x8()), P(self.err),
+                           self.cab_total[r][j * B:].data_ptr(), P(qp_dev), pic.slice_type, self._num_ref_l0(pic), 1,
+                           int(self.p.eff_t8x8()), P(self.err),
                            self.copy_stream.cuda_stream)
 
     def _gpu_cabac_code(self, g: int, t0: int, n: int, qps_d: torch.Tensor):
@@ -776,6 +850,7 @@ class GpuH264Encoder:
         # the new scene instead of across the cut (x264 places an I / P picture there)
         plan = gop_plan(F, self.nb, set(anchors_at) | {d for d in range(1, F) if cuts_h[:, d].any()})
         order = [pic.d for pic in plan]  # display index of each coding step
+        self.anchor_d = {pic.anchor: pic.d for pic in plan if pic.kind != "B"}  # anchor ordinal -> display index
         if qps is None:
             qps_h = np.full((B, F), qp_p, dtype=np.int32)
             qps_h[:, 0] = qp_i
@@ -841,10 +916,11 @@ class GpuH264Encoder:
                 pending[k] = None
             self.timings["host_blocked_s"] = self.timings.get("host_blocked_s", 0.0) + time.perf_counter() - tw
             main.wait_event(self.copy_done[k]) if t >= 2 else None
+            na = self.na
             if pic.kind == "B":
-                cur, ref0, ref1 = self.rec[2], self.rec[(pic.l1_anchor - 1) & 1], self.rec[pic.l1_anchor & 1]
+                cur, ref0, ref1 = self.rec[na], self.rec[(pic.l1_anchor - 1) % na], self.rec[pic.l1_anchor % na]
             else:
-                cur, ref0, ref1 = self.rec[pic.anchor & 1], self.rec[(pic.anchor - 1) & 1], None
+                cur, ref0, ref1 = self.rec[pic.anchor % na], self.rec[(pic.anchor - 1) % na], None
             self._prep(y, u, v, pic.d)
             self.qp.copy_(qps_d[t])
             self._encode_frame(pic, cur, ref0, ref1, self.hdr[k], self.coef[k],
@@ -904,7 +980,12 @@ class GpuH264Encoder:
         torch.cuda.synchronize(self.dev)
         if F > 1:
             self.stats["p_intra_ratio"] = float(self.p_intra_mbs.item()) / (B * (F - 1) * self.nmb)
+            n_p = sum(1 for pic in plan if pic.kind == "P")
+            if self.nref > 1 and n_p:
+                # share of P-picture MBs (inter decisions before the intra override) on a farther picture
+                self.stats["p_far_ref_ratio"] = float(self.far_ref_mbs.item()) / (B * n_p * self.nmb)
         self.p_intra_mbs.zero_()
+        self.far_ref_mbs.zero_()
         err = int(self.err.item())
         if err & 4:
             raise CabacPoolExhausted(f"GPU CABAC: symbol pool exhausted (err={err:#x})")

@@ -319,3 +319,25 @@ def test_gpu_h264_intra8x8(host, qp):
     assert i8 <= 1.01 * i4
     enc.close()
     enc0.close()
+
+
+@pytest.mark.parametrize("bframes", [0, 3])
+def test_gpu_h264_multiref_roundtrip(host, bframes):
+    """x264 --ref 3: P macroblocks choose among the three latest anchors (ref_idx through the
+    GPU CABAC binariser, chroma MC from the chosen picture, deblocking across different
+    references) and B pictures' temporal direct follows the co-located block's reference
+    (per-reference DistScaleFactor and implicit weights) -- bit-exact against the CPU decoder,
+    and farther pictures are actually chosen."""
+    enc, res, _ = _run(352, 288, slots=2, frames=13, crf=None, qp=26, bframes=bframes, refs=3)
+    _check_roundtrip(host, enc, res, 352, 288)
+    assert enc.stats.get("p_far_ref_ratio", 0.0) > 0.0, enc.stats
+
+
+def test_gpu_h264_multiref_gate_and_one_ref(host):
+    """refs=1 keeps the single-reference path (no override in the slice headers); a gate that
+    skips every MB's far search leaves the decisions on RefPicList0[0] and decodes the same."""
+    enc, res, _ = _run(176, 144, slots=2, frames=9, crf=None, qp=28, bframes=3, refs=1)
+    _check_roundtrip(host, enc, res, 176, 144)
+    enc, res, _ = _run(176, 144, slots=2, frames=9, crf=None, qp=28, bframes=0, refs=2, ref_gate=1 << 20)
+    _check_roundtrip(host, enc, res, 176, 144)
+    assert enc.stats.get("p_far_ref_ratio", 1.0) == 0.0, enc.stats

@@ -25,7 +25,7 @@ s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 enc._prep(y, u, v, 1)
 hp = P(enc.me_hp[0])
 lib.mivc_launch_me(B, enc.wmb, enc.hmb, P(enc.src[0]), P(enc.rec[0][0]), P(enc.prev_mv), P(enc.mv), P(enc.me_cost),
-                   P(enc.pred), P(enc.intra_cost), P(enc.qp), R, 2, hp, None, 0, 0, s)
+                   P(enc.pred), P(enc.intra_cost), P(enc.qp), R, 2, hp, None, 0, 0, s, None, 0, None)
 torch.cuda.synchronize()
 buf = (ctypes.c_ulonglong * (64 * 12))()
 lib.mivc_me_prof_read(buf)
