@@ -63,6 +63,7 @@ EncoderConfig cfg_from(const py::dict& d) {
   c.bframes = dget<int>(d, "bframes", 0);
   c.refs = dget<int>(d, "refs", 1);
   c.weighted_bipred = dget<int>(d, "weighted_bipred", 0);
+  c.weightp = dget<int>(d, "weightp", 0);
   c.level_idc = dget<int>(d, "level_idc", 0);
   c.cqm = dget<int>(d, "cqm", 0);
   c.cqm_coded = dget<int>(d, "cqm_coded", 0xFF);
@@ -273,6 +274,29 @@ SliceHeader slice_header_from(const EncoderConfig& c, const SPS& sps, const PPS&
   sh.direct_spatial = dget<int>(fp, "direct_spatial", 1);
   sh.first_mb = dget<int>(fp, "first_mb", 0);  // several slices per picture: each writes its MB range
   sh.cabac_init_idc = 0;
+  // explicit weights of RefPicList0[0] (P slices of a weighted_pred_flag PPS): [luma log2
+  // denominator, chroma log2 denominator, luma weight, offset, Cb weight, offset, Cr weight,
+  // offset]; every other reference keeps the default weights
+  if (fp.contains("wp") && !fp["wp"].is_none()) {
+    auto v = fp["wp"].cast<std::vector<int>>();
+    if (v.size() != 8) throw std::runtime_error("wp: 8 values (denominators, luma w/o, Cb w/o, Cr w/o)");
+    WeightTable& w = sh.wt;
+    w.luma_log2 = v[0];
+    w.chroma_log2 = v[1];
+    if (w.luma_log2 < 0 || w.luma_log2 > 7 || w.chroma_log2 < 0 || w.chroma_log2 > 7)
+      throw std::runtime_error("wp: log2 denominators in 0..7");
+    for (int i = 2; i < 8; ++i)
+      if (v[i] < -128 || v[i] > 127) throw std::runtime_error("wp: weights and offsets in -128..127");
+    w.lw[0][0] = v[2];
+    w.lo[0][0] = v[3];
+    w.cw[0][0][0] = v[4];
+    w.co[0][0][0] = v[5];
+    w.cw[0][0][1] = v[6];
+    w.co[0][0][1] = v[7];
+    w.lflag[0][0] = v[2] != (1 << v[0]) || v[3] != 0;
+    w.cflag[0][0] = v[4] != (1 << v[1]) || v[5] != 0 || v[6] != (1 << v[1]) || v[7] != 0;
+    sh.has_weights = true;
+  }
   (void)sps;
   return sh;
 }

@@ -36,6 +36,7 @@ struct EncoderConfig {
   int bframes = 0;
   int refs = 1;
   int weighted_bipred = 0;  // 2 = implicit weights (x264 --weightb)
+  int weightp = 0;          // weighted_pred_flag: P slices carry pred_weight_table() (x264 --weightp)
   int level_idc = 0;        // > 0: written as level_idc (-level); must fit the size / rate
   // scaling matrices (High profile, t8x8): 0 flat; 1 the default matrices (x264 --cqm jvt: SPS
   // flag, no list sent); 2 the lists below in the SPS; 3 the lists below in the PPS over the

@@ -192,8 +192,30 @@ void write_slice_header(BitWriter& bw, const SliceHeader& h, const SPS& s, const
     bw.put_bit(0);  // ref_pic_list_modification_flag_l0
     if (h.slice_type == SLICE_B) bw.put_bit(0);  // ref_pic_list_modification_flag_l1
   }
-  if ((p.weighted_pred && h.slice_type == SLICE_P) || (p.weighted_bipred_idc == 1 && h.slice_type == SLICE_B))
-    throw std::runtime_error("explicit weighted prediction is not written");
+  if (p.weighted_bipred_idc == 1 && h.slice_type == SLICE_B)
+    throw std::runtime_error("explicit weighted bi-prediction is not written");
+  if (p.weighted_pred && h.slice_type == SLICE_P) {
+    // pred_weight_table() (7.3.3.2), list 0; references without explicit weights: flags 0
+    const WeightTable& w = h.wt;
+    const bool any = h.has_weights;
+    bw.put_ue(any ? w.luma_log2 : 0);
+    bw.put_ue(any ? w.chroma_log2 : 0);  // ChromaArrayType 1
+    for (int i = 0; i < h.num_ref_idx_l0_active; ++i) {
+      const bool lf = any && w.lflag[0][i];
+      bw.put_bit(lf);
+      if (lf) {
+        bw.put_se(w.lw[0][i]);
+        bw.put_se(w.lo[0][i]);
+      }
+      const bool cf = any && w.cflag[0][i];
+      bw.put_bit(cf);
+      if (cf)
+        for (int j = 0; j < 2; ++j) {
+          bw.put_se(w.cw[0][i][j]);
+          bw.put_se(w.co[0][i][j]);
+        }
+    }
+  }
   if (h.nal_ref_idc) {
     if (h.nal_unit_type == NAL_IDR) {
       bw.put_bit(h.no_output_of_prior_pics);

@@ -88,8 +88,8 @@ struct Mmco {
 struct WeightTable {
   int luma_log2 = 0, chroma_log2 = 0;
   // [list][ref_idx]: luma weight, offset, chroma weight[2], offset[2]; flag = explicitly present
-  int lw[2][32], lo[2][32], cw[2][32][2], co[2][32][2];
-  uint8_t lflag[2][32], cflag[2][32];
+  int lw[2][32] = {}, lo[2][32] = {}, cw[2][32][2] = {}, co[2][32][2] = {};
+  uint8_t lflag[2][32] = {}, cflag[2][32] = {};
 };
 
 struct SliceHeader {

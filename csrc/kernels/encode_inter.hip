@@ -47,7 +47,15 @@ struct InterArgs {
   const uint8_t* refs_u[4];
   const uint8_t* refs_v[4];
   const int8_t* mref;      // [B, nmb] (P pictures)
+  // explicit weighted prediction of RefPicList0[0] in P pictures (nullable): [B, 8] = luma
+  // weight, offset, log2 denominator, Cb weight, offset, Cr weight, offset, chroma denominator
+  const int* wp;
 };
+
+// clause 8.4.2.3.2 for one sample: ((p * w + 2^(d-1)) >> d) + o, clipped
+__device__ __forceinline__ int wp_sample(int p, int w, int o, int d) {
+  return h264::clip1((d >= 1 ? ((p * w + (1 << (d - 1))) >> d) : p * w) + o);
+}
 
 
 // Eighth-sample chroma prediction (clause 8.4.2.2.2) of a 4x4 block at (px0, py0) of a
@@ -184,6 +192,19 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
     for (int y = 0; y < 4; ++y) {
       prw[y] = *reinterpret_cast<const uint32_t*>(pred + y * 16);
       sw[y] = *reinterpret_cast<const uint32_t*>(srcy + static_cast<size_t>(y) * W);
+    }
+    if (a.wp && !a.bmode && !(a.mref && a.mref[o])) {  // weighted RefPicList0[0] prediction
+      const int* wt = a.wp + slot * 8;
+      const int w = wt[0], wo = wt[1], d = wt[2];
+      if (w != (1 << d) || wo != 0) {
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          int v4[4];
+#pragma unroll
+          for (int x = 0; x < 4; ++x) v4[x] = wp_sample(static_cast<int>(__builtin_amdgcn_ubfe(prw[y], 8 * x, 8)), w, wo, d);
+          prw[y] = pack4_u8(v4);
+        }
+      }
     }
 #pragma unroll
     for (int y = 0; y < 4; ++y)
@@ -328,6 +349,16 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
       const int cmx = a.mv8 ? a.mv8[o * 8 + cb * 2] : mvx, cmy = a.mv8 ? a.mv8[o * 8 + cb * 2 + 1] : mvy;
       const int r = a.mref ? a.mref[o] : 0;
       chroma_mc4x4((comp == 0 ? a.refs_u[r] : a.refs_v[r]) + slot * g.csize(), cw, CH, px0, py0, cmx, cmy, pv);
+      if (a.wp && r == 0) {
+        const int* wt = a.wp + slot * 8;
+        const int w = wt[3 + 2 * comp], wo = wt[4 + 2 * comp], d = wt[7];
+        if (w != (1 << d) || wo != 0) {
+#pragma unroll
+          for (int y = 0; y < 4; ++y)
+#pragma unroll
+            for (int x = 0; x < 4; ++x) pv[y][x] = wp_sample(pv[y][x], w, wo, d);
+        }
+      }
     } else {
       // the 4x4 chroma block cb covers luma quadrant cb: its lists and vectors
       const int r0 = h->ref[0][cb];
@@ -540,8 +571,9 @@ extern "C" void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t*
                                          const int8_t* aq, const uint8_t* ref1_u, const uint8_t* ref1_v, int bmode,
                                          int t8, const int16_t* mv8, void* stream, const int* w1, int nref,
                                          const uint8_t* const* xref_u, const uint8_t* const* xref_v,
-                                         const int8_t* mref) {
+                                         const int8_t* mref, const int* wp) {
   InterArgs a;
+  a.wp = bmode ? nullptr : wp;
   for (int r = 0; r < 4; ++r) {
     const int rr = r < nref ? r : 0;
     a.refs_u[r] = rr == 0 ? ref_u : xref_u[rr];

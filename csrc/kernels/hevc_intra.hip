@@ -3,7 +3,8 @@
 //
 // * hevc_intra_analyze (grid = CTBs x slots, 256 threads): every CU of the 32/16/8
 //   quadtree x all 35 modes is predicted from *source* neighbours (normative
-//   availability, substitution and filtering) and costed with 8x8 Hadamard SATD; the
+//   availability, substitution and filtering) and costed with 4x4 Hadamard SATDs on the
+//   matrix cores (v_mfma_f32_16x16x16_f16: 16 blocks per instruction); the
 //   CTB then picks the best mode per CU and the split that minimises SATD + lambda *
 //   bits.  No dependency between CTBs: the whole picture is analysed in parallel.
 // * hevc_intra_recon (grid = slots, 8 waves per workgroup): CTBs in wavefront order
@@ -74,59 +75,6 @@ __device__ __forceinline__ int lambda_satd(int qp, int bd) {
   return static_cast<int>(0.755f * exp2f((qp - 12) / 6.0f) * static_cast<float>(1 << (bd - 8)) + 0.5f);
 }
 
-// 4x4 Hadamard SATD (HM normalisation: (sum |H| + 1) >> 1)
-__device__ __forceinline__ int satd4x4(int (&d)[16]) {
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    int* v = d + r * 4;
-    const int a0 = v[0] + v[1], a1 = v[0] - v[1], a2 = v[2] + v[3], a3 = v[2] - v[3];
-    v[0] = a0 + a2;
-    v[1] = a1 + a3;
-    v[2] = a0 - a2;
-    v[3] = a1 - a3;
-  }
-  int sum = 0;
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const int a0 = d[c] + d[4 + c], a1 = d[c] - d[4 + c], a2 = d[8 + c] + d[12 + c], a3 = d[8 + c] - d[12 + c];
-    sum += abs(a0 + a2) + abs(a1 + a3) + abs(a0 - a2) + abs(a1 - a3);
-  }
-  return (sum + 1) >> 1;
-}
-
-// 8x8 Hadamard SATD (x265 / HM normalisation: (sum |H| + 2) >> 2)
-__device__ __forceinline__ int satd8x8(int (&d)[64]) {
-#pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    int* v = d + r * 8;
-#pragma unroll
-    for (int s = 1; s < 8; s <<= 1)
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        if (!(i & s)) {
-          const int a = v[i], b = v[i + s];
-          v[i] = a + b;
-          v[i + s] = a - b;
-        }
-  }
-  int sum = 0;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-#pragma unroll
-    for (int s = 1; s < 8; s <<= 1)
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        if (!(i & s)) {
-          const int a = d[i * 8 + c], b = d[(i + s) * 8 + c];
-          d[i * 8 + c] = a + b;
-          d[(i + s) * 8 + c] = a - b;
-        }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) sum += abs(d[i * 8 + c]);
-  }
-  return (sum + 2) >> 2;
-}
-
 // ============================================================== analysis
 constexpr int kCuCount = 21;  // 1 x 32, 4 x 16, 16 x 8
 constexpr int kPuCount = 64;  // PART_NxN: four 4x4 PUs of each 8x8 CU (z-order)
@@ -143,7 +91,38 @@ struct AnalyzeShared {
   int dc4[kPuCount];
   int best4_mode[kPuCount], best4_cost[kPuCount];
   int nxn[16];                 // per 8x8 CU: packed PU modes (bit 24) or 0
+  int rmode[128];              // refinement rounds: the mode each item evaluates (-1: none)
 };
+
+// SATD on the matrix cores.  One v_mfma_f32_16x16x16_f16 transforms 16 4x4 residual blocks:
+// B column n = block n as a 16-vector (k = 4 * row + column; lane (n = lane & 15, g = lane >> 4)
+// supplies row g), A = the Sylvester H16 = H4 (x) H4 (entries (-1)^popcount(m & k)), so column n
+// of the product holds the 2-D Hadamard coefficients of block n.  Residuals of 8- and 10-bit
+// samples are integers below 2^11 in magnitude (exact in f16) and every product sum is below
+// 2^24 (exact in the f32 accumulator).  Returns, at every lane of column n, the block's
+// sum |coefficients| (the VALU formulation's butterflies and registers are gone: a lane holds
+// 4 residuals instead of 64).
+typedef float v4f_t __attribute__((ext_vector_type(4)));
+typedef _Float16 v4h_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ v4h_t h16_rows() {
+  const int lane = threadIdx.x & 63, m = lane & 15, kg = lane >> 4;
+  v4h_t h;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) h[j] = (__builtin_popcount(m & (4 * kg + j)) & 1) ? _Float16(-1.0f) : _Float16(1.0f);
+  return h;
+}
+
+__device__ __forceinline__ int hadamard_col_sum(v4h_t H, const int (&r)[4]) {
+  v4h_t b;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) b[j] = static_cast<_Float16>(static_cast<float>(r[j]));
+  const v4f_t d = __builtin_amdgcn_mfma_f32_16x16x16f16(H, b, v4f_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+  int s = static_cast<int>(__builtin_fabsf(d[0]) + __builtin_fabsf(d[1]) + __builtin_fabsf(d[2]) + __builtin_fabsf(d[3]));
+  s += __shfl_xor(s, 16, 64);
+  s += __shfl_xor(s, 32, 64);
+  return s;
+}
 
 // CTB-relative position of 4x4 PU `pu` (8x8 CU pu >> 2 in z-order, PU pu & 3 in raster)
 __device__ __forceinline__ void pu_of(int pu, int* px, int* py) {
@@ -276,11 +255,16 @@ __global__ __launch_bounds__(256, 4) void hevc_intra_analyze(HevcIntraArgs a) {
     (&S.done4[0][0])[i] = 0;
   }
   __syncthreads();
-  // SATD of (CU, mode, 8x8 block) items, coarse to fine: 11 seed modes (planar, DC and
-  // every 4th angular direction) for every CU, then best-angular +-2, then +-1.  An
-  // item index i < 48 names the (CU, block): 0-15 the blocks of the 32x32 CU, 16-31
-  // the 4 x 4 blocks of the 16x16 CUs, 32-47 the 16 8x8 CUs.
-  auto eval = [&](int slot48, int mode) {
+  // SATD of (CU, mode, 8x8 region) items, coarse to fine: 11 seed modes (planar, DC and
+  // every 4th angular direction) for every CU, then best-angular +-2, then +-1.  An item
+  // index i < 48 names the (CU, region): 0-15 the regions of the 32x32 CU, 16-31 the 4 x 4
+  // regions of the 16x16 CUs, 32-47 the 16 8x8 CUs.  A wave evaluates 4 items per MFMA:
+  // item (lane & 15) >> 2, 4x4 block lane & 3 of its 8x8 region, row lane >> 4; the region
+  // cost is the sum of its four 4x4 Hadamard SATDs ((sum + 1) >> 1 each, HM's 4x4 form; the
+  // same scale as the 8x8 transform's (sum + 2) >> 2).
+  const int wave = tid >> 6, lane = tid & 63;
+  const v4h_t H16 = h16_rows();
+  auto eval_q = [&](int slot48, int mode, bool active) {
     const int level = slot48 >> 4, k = slot48 & 15;
     int c, bx, by;
     if (level == 0) {
@@ -300,34 +284,44 @@ __global__ __launch_bounds__(256, 4) void hevc_intra_analyze(HevcIntraArgs a) {
     cu_of(c, &cx, &cy, &n, &off);
     const int lg = n == 32 ? 5 : (n == 16 ? 4 : 3);
     const int* p = S.refs[hv::intra_filter_flag(mode, n) ? 1 : 0] + off;
-    int d[64];
-    hv::intra_pred8(p, n, lg, mode, bx * 8, by * 8, S.dc[c], n < 32, maxv, d);
+    const int b4 = lane & 3, row = lane >> 4;
+    const int X = bx * 8 + (b4 & 1) * 4, Y = by * 8 + (b4 >> 1) * 4 + row;
+    int r[4];
 #pragma unroll
-    for (int y = 0; y < 8; ++y)
-#pragma unroll
-      for (int x = 0; x < 8; ++x) d[y * 8 + x] = S.ext[(cy + by * 8 + y + 1) * 65 + cx + bx * 8 + x + 1] - d[y * 8 + x];
-    atomicAdd(&S.cost[c][mode], satd8x8(d));
-    S.done[c][mode] = 1;
+    for (int j = 0; j < 4; ++j)
+      r[j] = active ? S.ext[(cy + Y + 1) * 65 + cx + X + j + 1] -
+                          hv::intra_pred_sample(p, n, lg, mode, X + j, Y, S.dc[c], n < 32, maxv)
+                    : 0;
+    int blk = (hadamard_col_sum(H16, r) + 1) >> 1;
+    blk += __shfl_xor(blk, 1, 64);
+    blk += __shfl_xor(blk, 2, 64);
+    if (active && lane < 16 && b4 == 0) {
+      atomicAdd(&S.cost[c][mode], blk);
+      S.done[c][mode] = 1;
+    }
   };
-  // one 4x4 PU and mode: prediction from the source references, 4x4 Hadamard SATD
-  auto eval4 = [&](int pu, int mode) {
+  // 16 items (4x4 PU, mode) per MFMA: item lane & 15, row lane >> 4; prediction from the
+  // source references, 4x4 Hadamard SATD
+  auto eval4_q = [&](int pu, int mode, bool active) {
     int px, py;
     pu_of(pu, &px, &py);
     const int* p = S.refs4[pu];
-    int d[16];
+    const int row = lane >> 4;
+    int r[4];
 #pragma unroll
-    for (int y = 0; y < 4; ++y)
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-        d[y * 4 + x] = S.ext[(py + y + 1) * 65 + px + x + 1] - hv::intra_pred_sample(p, 4, 2, mode, x, y, S.dc4[pu], true, maxv);
-    S.cost4[pu][mode] = satd4x4(d);
-    S.done4[pu][mode] = 1;
-  };
-  {
-    for (int it = tid; it < 11 * 48; it += 256) {
-      const int si = it / 48;
-      eval(it % 48, si < 2 ? si : 2 + 4 * (si - 2));  // seeds 0, 1, 2, 6, ..., 34
+    for (int j = 0; j < 4; ++j)
+      r[j] = active ? S.ext[(py + row + 1) * 65 + px + j + 1] -
+                          hv::intra_pred_sample(p, 4, 2, mode, j, row, S.dc4[pu], true, maxv)
+                    : 0;
+    const int sv = (hadamard_col_sum(H16, r) + 1) >> 1;
+    if (active && lane < 16) {
+      S.cost4[pu][mode] = sv;
+      S.done4[pu][mode] = 1;
     }
+  };
+  for (int q = wave; q < 11 * 12; q += 4) {  // wave-uniform mode and CU level
+    const int si = q / 12;
+    eval_q(4 * (q % 12) + ((lane & 15) >> 2), si < 2 ? si : 2 + 4 * (si - 2), true);
   }
   __syncthreads();
   for (int step = 2; step >= 1; step >>= 1) {
@@ -343,12 +337,19 @@ __global__ __launch_bounds__(256, 4) void hevc_intra_analyze(HevcIntraArgs a) {
       S.best_mode[tid] = bm;
     }
     __syncthreads();
+    // the items of this round, decided before any of them marks its (CU, mode) done
     if (tid < 96) {
       const int slot48 = tid % 48;
       const int level = slot48 >> 4, k = slot48 & 15;
       const int c = level == 0 ? 0 : (level == 1 ? 1 + (k >> 2) : 5 + k);
       const int m = S.best_mode[c] + (tid < 48 ? -step : step);
-      if (m >= 2 && m <= 34 && !S.done[c][m]) eval(slot48, m);
+      S.rmode[tid] = (m >= 2 && m <= 34 && !S.done[c][m]) ? m : -1;
+    }
+    __syncthreads();
+    for (int q = wave; q < 24; q += 4) {
+      const int it = 4 * q + ((lane & 15) >> 2);
+      const int m = S.rmode[it];
+      eval_q(it % 48, m < 0 ? 0 : m, m >= 0);
     }
     __syncthreads();
   }
@@ -371,14 +372,16 @@ __global__ __launch_bounds__(256, 4) void hevc_intra_analyze(HevcIntraArgs a) {
   __syncthreads();
   // 4x4 PUs (PART_NxN candidates): seeds planar, DC and the parent 8x8 CU's best mode
   // +-2 (or the pure directions when it is planar / DC), then +-1 around the best angular
-  for (int it = tid; nxn_on && it < 5 * kPuCount; it += 256) {
+  // (clamped duplicates of one PU write the same value)
+  for (int q = wave; nxn_on && q < 5 * kPuCount / 16; q += 4) {
+    const int it = 16 * q + (lane & 15);
     const int pu = it % kPuCount, si = it / kPuCount;
     const int m8 = S.best_mode[5 + (pu >> 2)];
     int m;
     if (si < 2) m = si;
     else if (m8 >= 2) m = clampi(m8 + (si - 3) * 2, 2, 34);
     else m = si == 2 ? 10 : (si == 3 ? 26 : 18);
-    if (!S.done4[pu][m]) eval4(pu, m);  // (clamped duplicates of one PU run in one iteration: same value)
+    eval4_q(pu, m, true);
   }
   __syncthreads();
   if (nxn_on && tid < kPuCount) {
@@ -396,7 +399,13 @@ __global__ __launch_bounds__(256, 4) void hevc_intra_analyze(HevcIntraArgs a) {
   if (nxn_on && tid < 2 * kPuCount) {
     const int pu = tid & 63;
     const int m = S.best4_mode[pu] + (tid < 64 ? -1 : 1);
-    if (m >= 2 && m <= 34 && !S.done4[pu][m]) eval4(pu, m);
+    S.rmode[tid] = (m >= 2 && m <= 34 && !S.done4[pu][m]) ? m : -1;
+  }
+  __syncthreads();
+  for (int q = wave; nxn_on && q < 2 * kPuCount / 16; q += 4) {
+    const int it = 16 * q + (lane & 15);
+    const int m = S.rmode[it];
+    eval4_q(it & 63, m < 0 ? 0 : m, m >= 0);
   }
   __syncthreads();
   if (nxn_on && tid < kPuCount) {

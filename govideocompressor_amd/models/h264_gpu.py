@@ -28,6 +28,7 @@ from ..ops import native
 from .gop import PicPlan, gop_plan  # noqa: F401  (re-exported)
 
 MB_HDR_BYTES = 64
+WP_LOG2 = 6  # luma / chroma log2 weight denominators of explicit weighted prediction
 COEF_PER_MB = 408
 
 
@@ -107,14 +108,25 @@ class H264Params:
     # reference.  CABAC only (the Baseline CAVLC path keeps one reference).  ref_gate: MBs
     # whose list-0[0] cost (SATD + lambda * bits) is <= ref_gate are not searched in the farther pictures
     refs: int = int(os.environ.get("MIVC_REFS", 3))
+    # x264 --weightp (default 2 outside Baseline): explicit weighted prediction of a P picture's
+    # RefPicList0[0] (luma and chroma weight / offset, denominator 2^6) where the source
+    # statistics say the brightness or contrast changed (fades, flashes): the weights come from
+    # the means and variances of the two source pictures (wp_min_mean: mean change in luma
+    # levels, wp_min_scale: contrast change, either one turns weighting on).  CABAC only.
+    weightp: bool = True
+    wp_min_mean: float = 2.0
+    wp_min_scale: float = 0.08
     ref_range: int = int(os.environ.get("MIVC_REF_RANGE", 4))
-    ref_gate: int = int(os.environ.get("MIVC_REF_GATE", 0))
+    ref_gate: int = int(os.environ.get("MIVC_REF_GATE", 1500))
 
     def eff_bframes(self) -> int:
         return max(0, int(self.bframes)) if self.cabac else 0
 
     def eff_refs(self) -> int:
         return max(1, min(4, int(self.refs))) if self.cabac else 1
+
+    def eff_weightp(self) -> bool:
+        return bool(self.weightp and self.cabac)
 
     def eff_t8x8(self) -> bool:
         return bool(self.t8x8 and self.cabac)
@@ -126,7 +138,7 @@ class H264Params:
         return dict(width=self.width, height=self.height, fps=self.fps, qp=self.qp,
                     deblock=int(self.deblock), chroma_qp_offset=self.chroma_qp_offset,
                     vui=int(self.vui), cabac=int(self.cabac), bframes=self.eff_bframes(), t8x8=int(self.eff_t8x8()),
-                    weighted_bipred=2 if self.weightb else 0, refs=self.eff_refs(),
+                    weighted_bipred=2 if self.weightb else 0, refs=self.eff_refs(), weightp=int(self.eff_weightp()),
                     level_idc=int(self.level_idc))
 
     def profile_name(self) -> str:
@@ -135,6 +147,7 @@ class H264Params:
         nb = self.eff_bframes()
         return (("High CABAC 8x8dct" if self.eff_t8x8() else "Main CABAC") + (" i8x8" if self.eff_t8x8() and self.i8x8 else "")
                 + (" p8x8" if self.eff_partitions() else "") + (f" ref{self.eff_refs()}" if self.eff_refs() > 1 else "")
+                + (" weightp" if self.eff_weightp() else "")
                 + (f" {nb}B temporal-direct" if nb else "") + (" weightb" if nb and self.weightb else ""))
 
     def frame_qps(self) -> tuple[int, int]:
@@ -221,6 +234,7 @@ class GpuH264Encoder:
         self.W, self.H = self.wmb * 16, self.hmb * 16
         self.nmb = self.wmb * self.hmb
         self._mbtree = None  # [B, F, nmb] MB-tree QP offsets of the batch being encoded
+        self._wp = self._wp_on = None  # explicit weights of the batch's P pictures (see _weights)
         B, H, W, nmb, dev = self.B, self.H, self.W, self.nmb, self.dev
         u8, i16, i32 = torch.uint8, torch.int16, torch.int32
 
@@ -269,6 +283,8 @@ class GpuH264Encoder:
             self.pm1 = torch.zeros((B, nmb, 2), dtype=i16, device=dev)
             self.dmv = torch.zeros((B, nmb, 16), dtype=i16, device=dev)
             self.col_hdr = torch.zeros((B, nmb, MB_HDR_BYTES), dtype=u8, device=dev)
+        if params.eff_weightp():
+            self.src_me = torch.zeros((B, H, W), dtype=u8, device=dev)  # inverse-weighted luma for ME
         self.intra_flag = torch.zeros((B, nmb), dtype=u8, device=dev)
         self.aq = torch.zeros((B, nmb), dtype=torch.int8, device=dev)     # per-MB QP offsets (AQ)
         self.qp_flags = torch.zeros((B, nmb), dtype=u8, device=dev)       # MB carries mb_qp_delta
@@ -431,6 +447,13 @@ class GpuH264Encoder:
             fy, fu, fv = (P(x) for x in ref0)
             self.intra_count.zero_()
             hp = P(self.me_hp[(pic.anchor - 1) % na])
+            sy_full, wp = sy, 0
+            if self._wp_on is not None and self._wp_on[pic.d]:
+                # weighted RefPicList0[0]: its searches see the inverse-weighted source
+                wp = self._wp_dev[pic.d].data_ptr()
+                with st("weightp"):
+                    self.hip.wp_src(sy, P(self.src_me), self._wp_src_dev[pic.d].data_ptr(), B, self.H * self.W, s)
+                sy = P(self.src_me)
             with st("me_p"):
                 self.hip.me(B, wmb, hmb, sy, fy, P(self.prev_mv), P(self.mv), P(self.me_cost), P(self.pred),
                             P(self.intra_cost), P(self.qp), self.p.me_range, self.p.subpel, s, hp, aq, 1,
@@ -460,7 +483,7 @@ class GpuH264Encoder:
                         rk = self.rec[a_k % na]
                         scale = (pic.d - self.anchor_d[a_k]) / max(1, d0)
                         self.xpm.copy_((self.mv.float() * scale).round_().clamp_(-2048, 2047))
-                        self.hip.me(B, wmb, hmb, sy, P(rk[0]), P(self.xpm), P(self.xmv[k - 1]), P(self.xcost[k - 1]),
+                        self.hip.me(B, wmb, hmb, sy_full, P(rk[0]), P(self.xpm), P(self.xmv[k - 1]), P(self.xcost[k - 1]),
                                     P(self.xpred[k - 1]), 0, P(self.qp), int(self.p.ref_range), self.p.subpel, s,
                                     P(self.me_hp[a_k % na]), aq, 1, self.p.p_early_sad, P(self.me_cost),
                                     self._ref_gate(), P(self.prev_mv))
@@ -471,12 +494,13 @@ class GpuH264Encoder:
                     self.far_ref_mbs += (self.mref > 0).sum()
             if cut is not None:
                 self.intra_cost.masked_fill_(cut[:, None], -1)  # intra beats any inter cost
+            sy = sy_full
             with st("inter"):
                 self.hip.encode_inter(B, wmb, hmb, sy, su, sv, fy, fu, fv, ry, ru, rv, P(self.pred), P(self.mv),
                                       P(self.me_cost), P(self.intra_cost), P(self.qp), cqo, P(hdr), P(coef),
                                       P(self.nz), P(self.intra_flag), P(self.intra_count), s, aq,
                                       t8=int(self.p.eff_t8x8()), mv8=mv8, xref_u=xu, xref_v=xv,
-                                      mref=P(self.mref) if nr > 1 else 0)
+                                      mref=P(self.mref) if nr > 1 else 0, wp=wp)
         elif pic.kind == "B":
             f0y, f0u, f0v = (P(x) for x in ref0)
             f1y, f1u, f1v = (P(x) for x in ref1)
@@ -565,9 +589,56 @@ class GpuH264Encoder:
 
     def _frame_params(self, b: int, pic: PicPlan, qp_frame: int, idr_ids: list[int]) -> dict:
         n0 = self._num_ref_l0(pic)
-        return dict(idr=int(pic.kind == "I"), frame_num=pic.frame_num, idr_pic_id=idr_ids[b] & 0xFFFF, qp=qp_frame,
-                    slice_type=pic.slice_type, nal_ref_idc=pic.nal_ref_idc, poc=pic.poc, direct_spatial=0,
-                    **({"num_ref_l0": n0, "num_ref_l1": 1} if pic.kind != "I" else {}))
+        fp = dict(idr=int(pic.kind == "I"), frame_num=pic.frame_num, idr_pic_id=idr_ids[b] & 0xFFFF, qp=qp_frame,
+                  slice_type=pic.slice_type, nal_ref_idc=pic.nal_ref_idc, poc=pic.poc, direct_spatial=0,
+                  **({"num_ref_l0": n0, "num_ref_l1": 1} if pic.kind != "I" else {}))
+        if pic.kind == "P" and self._wp is not None:
+            fp["wp"] = [WP_LOG2, WP_LOG2] + [int(x) for x in self._wp[pic.d, b]]
+        return fp
+
+    def _weights(self, y, u, v, plan: list[PicPlan]) -> None:
+        """x264 --weightp: per P picture and slot, the explicit weights of RefPicList0[0] from
+        the source statistics (wp_stats: means and variances of the two pictures' planes):
+        scale = sqrt(var_cur / var_ref), offset = mean_cur - scale * mean_ref, used when the mean
+        moved by wp_min_mean levels or the contrast by wp_min_scale (fades, flashes)."""
+        self._wp = self._wp_on = None
+        if not self.p.eff_weightp() or not any(pic.kind == "P" for pic in plan):
+            return
+        B, F, h, w = y.shape
+        st = torch.empty((B, F, 6), dtype=torch.int64, device=self.dev)
+        self.hip.wp_stats(y.data_ptr(), u.data_ptr(), v.data_ptr(), w, h, B * F, st.data_ptr(), self._stream())
+        sh = st.cpu().numpy().astype(np.float64)
+        n = np.array([w * h, w * h / 4, w * h / 4])
+        mean = sh[..., 0::2] / n
+        var = np.maximum(sh[..., 1::2] / n - mean ** 2, 0.0)
+        one = 1 << WP_LOG2
+        wp = np.zeros((F, B, 6), dtype=np.int32)
+        wp[:, :, 0::2] = one
+        on = np.zeros(F, dtype=bool)
+        for pic in plan:
+            if pic.kind != "P":
+                continue
+            m1, m0 = mean[:, pic.d], mean[:, pic.l0]
+            v1, v0 = var[:, pic.d], var[:, pic.l0]
+            scale = np.where(v0 > 1e-3, np.sqrt(v1 / np.maximum(v0, 1e-3)), 1.0)
+            use = (np.abs(m1[:, 0] - m0[:, 0]) >= self.p.wp_min_mean) | (np.abs(scale[:, 0] - 1) >= self.p.wp_min_scale)
+            if not use.any():
+                continue
+            wq = np.clip(np.round(scale * one), 0, 127)
+            oq = np.clip(np.round(m1 - wq / one * m0), -128, 127)
+            for c in range(3):
+                wp[pic.d, use, 2 * c] = wq[use, c]
+                wp[pic.d, use, 2 * c + 1] = oq[use, c]
+            on[pic.d] = True
+        if not on.any():
+            return
+        self._wp, self._wp_on = wp, on
+        dev8 = np.zeros((F, B, 8), dtype=np.int32)
+        dev8[..., 0], dev8[..., 1], dev8[..., 2] = wp[..., 0], wp[..., 1], WP_LOG2
+        dev8[..., 3:7], dev8[..., 7] = wp[..., 2:6], WP_LOG2
+        self._wp_dev = torch.from_numpy(dev8).to(self.dev)
+        self._wp_src_dev = torch.from_numpy(np.ascontiguousarray(dev8[..., :3])).to(self.dev)
+        self.stats["weightp_pictures"] = int(on.sum())
 
     @staticmethod
     def _cabac_groups(F: int, G: int) -> list[tuple[int, int]]:
@@ -683,7 +754,7 @@ class GpuH264Encoder:
         cache = {}
         for b in range(self.B):
             fp = self._frame_params(b, pic, int(qps_t[b]), idr_ids)
-            key = (fp["idr_pic_id"] if idr else -1, fp["qp"])
+            key = (fp["idr_pic_id"] if idr else -1, fp["qp"], tuple(fp.get("wp", ())))
             if key not in cache:
                 cache[key] = self.host.slice_header_bits(self.cfg, fp)
             words, nbits = cache[key]
@@ -851,6 +922,7 @@ class GpuH264Encoder:
         plan = gop_plan(F, self.nb, set(anchors_at) | {d for d in range(1, F) if cuts_h[:, d].any()})
         order = [pic.d for pic in plan]  # display index of each coding step
         self.anchor_d = {pic.anchor: pic.d for pic in plan if pic.kind != "B"}  # anchor ordinal -> display index
+        self._weights(y, u, v, plan)
         if qps is None:
             qps_h = np.full((B, F), qp_p, dtype=np.int32)
             qps_h[:, 0] = qp_i

@@ -341,3 +341,43 @@ def test_gpu_h264_multiref_gate_and_one_ref(host):
     enc, res, _ = _run(176, 144, slots=2, frames=9, crf=None, qp=28, bframes=0, refs=2, ref_gate=1 << 20)
     _check_roundtrip(host, enc, res, 176, 144)
     assert enc.stats.get("p_far_ref_ratio", 1.0) == 0.0, enc.stats
+
+
+def _fade_clip(slots, frames, w, h, seed=5):
+    import torch
+    from govideocompressor_amd.models.h264_gpu import synth_clip
+    y, u, v = synth_clip(slots, frames, w, h, seed=seed)
+    f = torch.linspace(1.0, 0.35, frames, device=y.device).view(1, frames, 1, 1)
+    y = (y.float() * f + 0.5).clamp(0, 255).to(torch.uint8)
+    u = ((u.float() - 128) * f + 128.5).clamp(0, 255).to(torch.uint8)
+    v = ((v.float() - 128) * f + 128.5).clamp(0, 255).to(torch.uint8)
+    return y.contiguous(), u.contiguous(), v.contiguous()
+
+
+@pytest.mark.parametrize("bframes,refs", [(0, 1), (3, 3)])
+def test_gpu_h264_weightp_fade(host, bframes, refs):
+    """x264 --weightp on a fade to black: P pictures carry pred_weight_table() (explicit luma
+    and chroma weights of RefPicList0[0], inverse-weighted source for the motion search,
+    forward weights on the chosen prediction in encode_inter) -- bit-exact against the CPU
+    decoder, and fewer bits than the unweighted encode at the same QP."""
+    import torch
+    from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params
+    y, u, v = _fade_clip(2, 9, 352, 288)
+    out = {}
+    for wpon in (True, False):
+        enc = GpuH264Encoder(H264Params(width=352, height=288, crf=None, qp=26, bframes=bframes, refs=refs,
+                                        weightp=wpon), slots=2)
+        res = enc.encode(y, u, v, keep_recon=True)
+        torch.cuda.synchronize()
+        _check_roundtrip(host, enc, res, 352, 288)
+        out[wpon] = (sum(r.nbytes() for r in res), enc.stats.get("weightp_pictures", 0))
+        enc.close()
+    assert out[True][1] > 0 and out[False][1] == 0, out
+    assert out[True][0] < out[False][0] * 0.97, out
+
+
+def test_gpu_h264_weightp_static_content_unweighted(host):
+    """Content without brightness changes gets no weights (no pred_weight_table entries)."""
+    enc, res, _ = _run(176, 144, slots=2, frames=5, crf=None, qp=28, bframes=0)
+    _check_roundtrip(host, enc, res, 176, 144)
+    assert enc.stats.get("weightp_pictures", 0) == 0, enc.stats
