@@ -389,6 +389,49 @@ __device__ __forceinline__ int intra_pred_sample(const int* p, int n, int log2n,
   return v;
 }
 
+// Four predicted samples of an n x n block for the MFMA SATD layout (hevc_intra.hip): the 4x4
+// block at (bx, by), lane group g.  Vertical-family, planar and DC modes give row g (samples
+// (bx + j, by + g)); horizontal-family modes give column g (samples (bx + g, by + j)), so the
+// angular interpolation position is the same for all four samples and 5 reference loads
+// serve them (the Hadamard SATD of a block equals that of its transpose).  *transposed tells
+// the caller which layout was produced.
+__device__ __forceinline__ void intra_pred4(const int* p, int n, int log2n, int mode, int bx, int by, int g, int dc,
+                                            bool edge, int maxv, int (&o)[4], bool* transposed) {
+  const int c = 2 * n;
+  auto L = [&](int yy) { return p[c - 1 - yy]; };
+  auto T = [&](int xx) { return p[c + 1 + xx]; };
+  *transposed = mode >= 2 && mode < 18;
+  if (mode < 2) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = intra_pred_sample(p, n, log2n, mode, bx + j, by + g, dc, edge, maxv);
+    return;
+  }
+  const int ang = hevc::kIntraPredAngle[mode];
+  const int inv = (mode >= 11 && mode <= 25) ? hevc::kInvAngle[mode - 11] : 0;
+  const bool vert = mode >= 18;
+  const int along = vert ? by + g : bx + g;    // the coordinate the projection depends on
+  const int across = vert ? bx : by;           // first of the 4 samples' other coordinate
+  const int idx = ((along + 1) * ang) >> 5, f = ((along + 1) * ang) & 31;
+  const int k0 = across + idx + 1;
+  int r[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int k = k0 + j;
+    const int proj = -1 + ((k * inv + 128) >> 8);
+    r[j] = k >= 0 ? (vert ? T(k - 1) : L(k - 1)) : (vert ? L(proj) : T(proj));
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = f ? ((32 - f) * r[j] + f * r[j + 1] + 16) >> 5 : r[j];
+  if (edge && mode == 26 && bx == 0) {  // column x = 0 of the pure vertical mode (row layout: sample j = 0)
+    const int v = T(0) + ((L(by + g) - L(-1)) >> 1);
+    o[0] = v < 0 ? 0 : (v > maxv ? maxv : v);
+  }
+  if (edge && mode == 10 && by == 0) {  // row y = 0 of the pure horizontal mode (column layout: sample j = 0)
+    const int v = L(0) + ((T(bx + g) - T(-1)) >> 1);
+    o[0] = v < 0 ? 0 : (v > maxv ? maxv : v);
+  }
+}
+
 // 8x8 block of the prediction of an n x n block (n >= 8) at offset (ox, oy): angular
 // modes load 9 reference samples per row (vertical family) or column (horizontal
 // family) and interpolate 8 outputs from registers.

@@ -285,13 +285,15 @@ __global__ __launch_bounds__(256, 4) void hevc_intra_analyze(HevcIntraArgs a) {
     const int lg = n == 32 ? 5 : (n == 16 ? 4 : 3);
     const int* p = S.refs[hv::intra_filter_flag(mode, n) ? 1 : 0] + off;
     const int b4 = lane & 3, row = lane >> 4;
-    const int X = bx * 8 + (b4 & 1) * 4, Y = by * 8 + (b4 >> 1) * 4 + row;
-    int r[4];
+    const int X = bx * 8 + (b4 & 1) * 4, Y = by * 8 + (b4 >> 1) * 4;  // the 4x4 block in the CU
+    int pr[4], r[4];
+    bool tr;
+    hv::intra_pred4(p, n, lg, mode, X, Y, row, S.dc[c], n < 32, maxv, pr, &tr);
+    // source samples in the same layout (row `row`, or column `row` when transposed)
+    const int s0 = tr ? (cy + Y + 1) * 65 + cx + X + row + 1 : (cy + Y + row + 1) * 65 + cx + X + 1;
+    const int sd = tr ? 65 : 1;
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      r[j] = active ? S.ext[(cy + Y + 1) * 65 + cx + X + j + 1] -
-                          hv::intra_pred_sample(p, n, lg, mode, X + j, Y, S.dc[c], n < 32, maxv)
-                    : 0;
+    for (int j = 0; j < 4; ++j) r[j] = active ? S.ext[s0 + j * sd] - pr[j] : 0;
     int blk = (hadamard_col_sum(H16, r) + 1) >> 1;
     blk += __shfl_xor(blk, 1, 64);
     blk += __shfl_xor(blk, 2, 64);
@@ -307,12 +309,13 @@ __global__ __launch_bounds__(256, 4) void hevc_intra_analyze(HevcIntraArgs a) {
     pu_of(pu, &px, &py);
     const int* p = S.refs4[pu];
     const int row = lane >> 4;
-    int r[4];
+    int pr[4], r[4];
+    bool tr;
+    hv::intra_pred4(p, 4, 2, mode, 0, 0, row, S.dc4[pu], true, maxv, pr, &tr);
+    const int s0 = tr ? (py + 1) * 65 + px + row + 1 : (py + row + 1) * 65 + px + 1;
+    const int sd = tr ? 65 : 1;
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      r[j] = active ? S.ext[(py + row + 1) * 65 + px + j + 1] -
-                          hv::intra_pred_sample(p, 4, 2, mode, j, row, S.dc4[pu], true, maxv)
-                    : 0;
+    for (int j = 0; j < 4; ++j) r[j] = active ? S.ext[s0 + j * sd] - pr[j] : 0;
     const int sv = (hadamard_col_sum(H16, r) + 1) >> 1;
     if (active && lane < 16) {
       S.cost4[pu][mode] = sv;
