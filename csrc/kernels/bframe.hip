@@ -121,7 +121,13 @@ struct BDecideArgs {
   const int8_t* dref;
   const uint8_t* ref0k[kMaxRefs];
   const uint8_t* hp0k[kMaxRefs];
+  // direct_only: the pre-pass before the two ME searches -- only the direct candidate's cost
+  // (SATD + lambda) goes to cost_out; MBs whose direct cost is already low skip the searches
+  // (me.hip gate) and their list costs come back as kNoCost
+  int direct_only;
 };
+
+constexpr int kNoCostB = 0x3FFFFFFF;  // me.hip kNoCost: the MB was not searched
 
 // Quarter-sample luma position (xf, yf) = two (plane, du, dv) taps averaged (the G/b/h/j
 // form of clause 8.4.2.2.1 used by me.hip): plane 0 = integer samples, 1 = b (half x),
@@ -211,7 +217,9 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   const size_t ho = static_cast<size_t>(slot) * 3 * (W + 2 * kHpMargin) * (H + 2 * kHpMargin);
   const uint8_t *G0 = a.ref0 + yo, *G1 = a.ref1 + yo, *H0 = a.hp0 + ho, *H1 = a.hp1 + ho;
   const int16_t* dm = a.dmv + o * 16;
-  const int m0x = a.mv0[o * 2], m0y = a.mv0[o * 2 + 1], m1x = a.mv1[o * 2], m1y = a.mv1[o * 2 + 1];
+  const bool donly = a.direct_only;
+  const int m0x = donly ? 0 : a.mv0[o * 2], m0y = donly ? 0 : a.mv0[o * 2 + 1];
+  const int m1x = donly ? 0 : a.mv1[o * 2], m1y = donly ? 0 : a.mv1[o * 2 + 1];
   const uint32_t src = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y) * W + X);
   // direct: per-quadrant vectors of both lists; bi: the two ME vectors
   uint32_t drw = 0;  // refIdxL0 of the four direct quadrants (bytes)
@@ -220,7 +228,7 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   const uint8_t *GD = dr ? a.ref0k[dr] + yo : G0, *HD = dr ? a.hp0k[dr] + ho : H0;
   const uint32_t pd = wavg4b(mc4(GD, HD, W, H, X, Y, dm[q * 2], dm[q * 2 + 1]),
                              mc4(G1, H1, W, H, X, Y, dm[8 + q * 2], dm[8 + q * 2 + 1]), a.w1[dr]);
-  const uint32_t pb = wavg4b(mc4(G0, H0, W, H, X, Y, m0x, m0y), mc4(G1, H1, W, H, X, Y, m1x, m1y), a.w1[0]);
+  const uint32_t pb = donly ? pd : wavg4b(mc4(G0, H0, W, H, X, Y, m0x, m0y), mc4(G1, H1, W, H, X, Y, m1x, m1y), a.w1[0]);
   __shared__ int s_res[2][256];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -245,6 +253,11 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   const int lambda = h264::kLambda[qp];
   // mb_type / motion bits (CABAC-ish): direct "0"; L0 / L1 "10x"; Bi "110000" + two mvds
   const int c_direct = satd_direct + lambda * 1;
+  if (donly) {
+    if (lane == 0) a.cost_out[o] = c_direct;
+    return;
+  }
+  const bool searched = a.cost0[o] < kNoCostB && a.cost1[o] < kNoCostB;
   const int c_l0 = a.cost0[o] + lambda * 3;
   const int c_l1 = a.cost1[o] + lambda * 3;
   const int c_bi = satd_bi + lambda * (6 + mvbits_se(m0x - a.pm0[o * 2]) + mvbits_se(m0y - a.pm0[o * 2 + 1]) +
@@ -252,7 +265,7 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   int mode = 0, best = c_direct;  // 0 direct, 1 L0, 2 L1, 3 Bi
   if (c_l0 < best) { mode = 1; best = c_l0; }
   if (c_l1 < best) { mode = 2; best = c_l1; }
-  if (c_bi < best) { mode = 3; best = c_bi; }
+  if (searched && c_bi < best) { mode = 3; best = c_bi; }
   uint32_t pw;
   if (mode == 0) pw = pd;
   else if (mode == 3) pw = pb;
@@ -925,8 +938,9 @@ extern "C" void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src
                                      const uint8_t* pred1, const int16_t* pm0, const int16_t* pm1, const int16_t* dmv,
                                      const int* qp, const int8_t* aq, void* hdr, uint8_t* pred_out, int* cost_out,
                                      void* stream, const int* w1, int nref, const int8_t* dref,
-                                     const uint8_t* const* ref0k, const uint8_t* const* hp0k) {
+                                     const uint8_t* const* ref0k, const uint8_t* const* hp0k, int direct_only) {
   BDecideArgs a;
+  a.direct_only = direct_only;
   for (int r = 0; r < kMaxRefs; ++r) {
     const int rr = r < nref ? r : nref - 1;
     a.w1[r] = w1[rr];

@@ -42,8 +42,9 @@ struct MeArgs {
   const uint8_t* hp;       // [B, 3, H + 8, W + 8] b / h / j half-sample planes of ref_y (margin 4)
   const int8_t* aq;        // [B, nmb] adaptive-quantisation QP offsets (nullable)
   int early_sad;           // > 0: skip the integer search when the best candidate's SAD <= this
-  // extra reference pictures (--ref > 1): MBs whose list-0[0] cost is already <= gate_thresh
-  // are not searched again (out_cost = kNoCost, nothing else written)
+  // MBs whose cost from an earlier decision (gate_cost: a farther reference's list-0[0] search,
+  // a B picture's temporal direct) is already <= gate_thresh (< 0: -gate_thresh * lambda) are
+  // not searched (out_cost = kNoCost, out_intra_cost = kNoCost, nothing else written)
   const int* gate_cost;    // [B, nmb] (nullable)
   int gate_thresh;
   // mvd costs against this vector instead of pred_mv (nullable): a farther picture's search is
@@ -332,8 +333,13 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   __shared__ MeShared<MAXR> S;
   if (a.gate_cost) {
     const size_t og = static_cast<size_t>(slot) * nmb + mb;
-    if (a.gate_cost[og] <= a.gate_thresh) {  // wave-uniform
-      if (lane == 0) a.out_cost[og] = kNoCost;
+    // gate_thresh < 0: -gate_thresh lambdas of this MB's QP
+    const int thr = a.gate_thresh >= 0 ? a.gate_thresh : -a.gate_thresh * lambda;
+    if (a.gate_cost[og] <= thr) {  // wave-uniform
+      if (lane == 0) {
+        a.out_cost[og] = kNoCost;
+        if (a.out_intra_cost) a.out_intra_cost[og] = kNoCost;  // the gate's candidate is good: no intra
+      }
       return;
     }
   }

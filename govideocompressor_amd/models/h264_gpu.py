@@ -97,6 +97,9 @@ class H264Params:
     # (B pictures: the temporal-direct predictor); 0 disables
     p_early_sad: int = int(os.environ.get("MIVC_P_EARLY_SAD", 0))
     b_early_sad: int = int(os.environ.get("MIVC_B_EARLY_SAD", 1024))
+    # B macroblocks whose temporal-direct cost (SATD + lambda, a b_decide pre-pass) is <= b_gate
+    # skip both list searches (x264's early B_Skip / direct termination); 0 disables
+    b_gate: int = int(os.environ.get("MIVC_B_GATE", 0))
     # deblock non-reference B pictures even when neither metrics nor the reconstruction
     # are requested (x264 --full-recon); the bitstream does not depend on it
     full_recon: bool = False
@@ -524,14 +527,22 @@ class GpuH264Encoder:
                     xv.append(P(rk[2]))
             self.intra_count.zero_()
             br = self.p.b_me_range
+            bg = int(self.p.b_gate)
             with st("me_b"):
                 self.hip.b_direct(B, wmb, hmb, P(self.col_hdr), dsfs, copies, P(self.dmv), P(self.pm0), P(self.pm1), s,
                                   P(self.dref) if nr > 1 else 0)
+                if bg != 0:  # direct costs first: MBs that direct already predicts well are not searched
+                    self.hip.b_decide(B, wmb, hmb, sy, f0y, f1y, hp0, hp1, P(self.mv), P(self.mv1), P(self.me_cost),
+                                      P(self.me_cost1), P(self.pred), P(self.pred1), P(self.pm0), P(self.pm1),
+                                      P(self.dmv), P(self.qp), aq, P(hdr), P(self.pred_b), P(self.cost_b), s, w1s,
+                                      P(self.dref) if nr > 1 else 0, r0y, r0h, 1)
+                gate = P(self.cost_b) if bg != 0 else 0
                 self.hip.me(B, wmb, hmb, sy, f0y, P(self.pm0), P(self.mv), P(self.me_cost), P(self.pred),
-                            P(self.intra_cost), P(self.qp), br, self.p.subpel, s, hp0, aq, 1, self.p.b_early_sad)
+                            P(self.intra_cost), P(self.qp), br, self.p.subpel, s, hp0, aq, 1, self.p.b_early_sad,
+                            gate, bg)
                 # the L1 search skips the open-loop intra estimate the L0 search just wrote
                 self.hip.me(B, wmb, hmb, sy, f1y, P(self.pm1), P(self.mv1), P(self.me_cost1), P(self.pred1),
-                            0, P(self.qp), br, self.p.subpel, s, hp1, aq, 1, self.p.b_early_sad)
+                            0, P(self.qp), br, self.p.subpel, s, hp1, aq, 1, self.p.b_early_sad, gate, bg)
             with st("b_decide"):
                 self.hip.b_decide(B, wmb, hmb, sy, f0y, f1y, hp0, hp1, P(self.mv), P(self.mv1), P(self.me_cost),
                                   P(self.me_cost1), P(self.pred), P(self.pred1), P(self.pm0), P(self.pm1),
