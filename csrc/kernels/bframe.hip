@@ -125,6 +125,7 @@ struct BDecideArgs {
   // (SATD + lambda) goes to cost_out; MBs whose direct cost is already low skip the searches
   // (me.hip gate) and their list costs come back as kNoCost
   int direct_only;
+  int bparts;  // x264 --partitions b8x8: per-quadrant candidates (B_16x8 / B_8x16 / B_8x8)
 };
 
 constexpr int kNoCostB = 0x3FFFFFFF;  // me.hip kNoCost: the MB was not searched
@@ -229,26 +230,45 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   const uint32_t pd = wavg4b(mc4(GD, HD, W, H, X, Y, dm[q * 2], dm[q * 2 + 1]),
                              mc4(G1, H1, W, H, X, Y, dm[8 + q * 2], dm[8 + q * 2 + 1]), a.w1[dr]);
   const uint32_t pb = donly ? pd : wavg4b(mc4(G0, H0, W, H, X, Y, m0x, m0y), mc4(G1, H1, W, H, X, Y, m1x, m1y), a.w1[0]);
-  __shared__ int s_res[2][256];
+  // residuals of the four candidates: 0 direct, 1 bi (the two ME vectors), 2 L0, 3 L1 (the ME
+  // predictions; not needed by the direct-only pre-pass or for MBs the gate left unsearched)
+  const bool searched = !donly && a.cost0[o] < kNoCostB && a.cost1[o] < kNoCostB;
+  const uint32_t p0w = searched ? *reinterpret_cast<const uint32_t*>(a.pred0 + o * 256 + r * 16 + c0) : pd;
+  const uint32_t p1w = searched ? *reinterpret_cast<const uint32_t*>(a.pred1 + o * 256 + r * 16 + c0) : pd;
+  __shared__ int s_res[4][256];
+  __shared__ int s_satd[4][16];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int sv = static_cast<int>((src >> (8 * k)) & 255u);
     s_res[0][r * 16 + c0 + k] = sv - static_cast<int>((pd >> (8 * k)) & 255u);
     s_res[1][r * 16 + c0 + k] = sv - static_cast<int>((pb >> (8 * k)) & 255u);
+    s_res[2][r * 16 + c0 + k] = sv - static_cast<int>((p0w >> (8 * k)) & 255u);
+    s_res[3][r * 16 + c0 + k] = sv - static_cast<int>((p1w >> (8 * k)) & 255u);
   }
   wave_sync();
-  int satd = 0;
-  if (lane < 32) {
+  {  // one 4x4 SATD per lane: candidate lane >> 4, block lane & 15 (raster)
     const int cand = lane >> 4, blk = lane & 15, bx = (blk & 3) * 4, by = (blk >> 2) * 4;
     int rr[16];
 #pragma unroll
     for (int y = 0; y < 4; ++y)
 #pragma unroll
       for (int x = 0; x < 4; ++x) rr[y * 4 + x] = s_res[cand][(by + y) * 16 + bx + x];
-    satd = h264::satd4x4(rr);
+    s_satd[cand][blk] = h264::satd4x4(rr);
   }
-  satd = sum16(satd);
-  const int satd_direct = __builtin_amdgcn_readlane(satd, 0), satd_bi = __builtin_amdgcn_readlane(satd, 16);
+  wave_sync();
+  // per 8x8 quadrant and candidate (lanes 0..15: candidate lane >> 2, quadrant lane & 3)
+  int qs = 0;
+  if (lane < 16) {
+    const int cand = lane >> 2, qq = lane & 3, b0 = (qq >> 1) * 8 + (qq & 1) * 2;
+    qs = s_satd[cand][b0] + s_satd[cand][b0 + 1] + s_satd[cand][b0 + 4] + s_satd[cand][b0 + 5];
+  }
+  int qsat[4][4];  // [candidate][quadrant]
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) qsat[c][qq] = __builtin_amdgcn_readlane(qs, c * 4 + qq);
+  const int satd_direct = qsat[0][0] + qsat[0][1] + qsat[0][2] + qsat[0][3];
+  const int satd_bi = qsat[1][0] + qsat[1][1] + qsat[1][2] + qsat[1][3];
   const int qp = clampi(a.qp[slot] + (a.aq ? a.aq[o] : 0), 0, 51);
   const int lambda = h264::kLambda[qp];
   // mb_type / motion bits (CABAC-ish): direct "0"; L0 / L1 "10x"; Bi "110000" + two mvds
@@ -257,40 +277,85 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
     if (lane == 0) a.cost_out[o] = c_direct;
     return;
   }
-  const bool searched = a.cost0[o] < kNoCostB && a.cost1[o] < kNoCostB;
   const int c_l0 = a.cost0[o] + lambda * 3;
   const int c_l1 = a.cost1[o] + lambda * 3;
-  const int c_bi = satd_bi + lambda * (6 + mvbits_se(m0x - a.pm0[o * 2]) + mvbits_se(m0y - a.pm0[o * 2 + 1]) +
-                                       mvbits_se(m1x - a.pm1[o * 2]) + mvbits_se(m1y - a.pm1[o * 2 + 1]));
+  const int mvb0 = mvbits_se(m0x - a.pm0[o * 2]) + mvbits_se(m0y - a.pm0[o * 2 + 1]);
+  const int mvb1 = mvbits_se(m1x - a.pm1[o * 2]) + mvbits_se(m1y - a.pm1[o * 2 + 1]);
+  const int c_bi = satd_bi + lambda * (6 + mvb0 + mvb1);
   int mode = 0, best = c_direct;  // 0 direct, 1 L0, 2 L1, 3 Bi
   if (c_l0 < best) { mode = 1; best = c_l0; }
   if (c_l1 < best) { mode = 2; best = c_l1; }
   if (searched && c_bi < best) { mode = 3; best = c_bi; }
-  uint32_t pw;
-  if (mode == 0) pw = pd;
-  else if (mode == 3) pw = pb;
-  else pw = *reinterpret_cast<const uint32_t*>((mode == 1 ? a.pred0 : a.pred1) + o * 256 + r * 16 + c0);
+  // x264 --partitions b8x8: every quadrant picks its own candidate among the MB's motion
+  // (direct quadrant, L0, L1, bi with the two searched vectors): B_16x8 / B_8x16 when the
+  // halves agree and no quadrant is direct, else B_8x8 (direct quadrants as B_Direct_8x8).
+  // Bits: sub_mb_type (direct 1, L0 / L1 3, bi 5 bins), one full mvd per list in use, 1 bin
+  // per later partition repeating it, and the B_8x8 mb_type (~6 bins) / 16x8 pair codes.
+  int qm[4] = {mode == 0 ? 0 : (mode == 3 ? 1 : mode + 1), 0, 0, 0};  // per quadrant: 0 D, 1 Bi, 2 L0, 3 L1
+  qm[1] = qm[2] = qm[3] = qm[0];
+  int kind = mode == 0 ? h264::MBK_BDIRECT : h264::MBK_B16x16;
+  if (a.bparts && searched) {
+    int sum = 0, used0 = 0, used1 = 0, pm[4];
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      const int cd = qsat[0][qq] + lambda * 1, cb = qsat[1][qq] + lambda * 7;
+      const int c0q = qsat[2][qq] + lambda * 4, c1q = qsat[3][qq] + lambda * 4;
+      int m = 0, bc = cd;
+      if (cb < bc) { m = 1; bc = cb; }
+      if (c0q < bc) { m = 2; bc = c0q; }
+      if (c1q < bc) { m = 3; bc = c1q; }
+      pm[qq] = m;
+      sum += bc;
+      used0 |= m == 1 || m == 2;
+      used1 |= m == 1 || m == 3;
+    }
+    const bool anyd = pm[0] == 0 || pm[1] == 0 || pm[2] == 0 || pm[3] == 0;
+    const bool h2 = pm[0] == pm[1] && pm[2] == pm[3], v2 = pm[0] == pm[2] && pm[1] == pm[3];
+    const bool uni = h2 && v2;
+    if (!uni) {
+      const int shape_bits = (!anyd && (h2 || v2)) ? 7 : 6;
+      const int c_part = sum + lambda * (shape_bits + (used0 ? mvb0 : 0) + (used1 ? mvb1 : 0));
+      if (c_part < best) {
+        best = c_part;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) qm[qq] = pm[qq];
+        kind = (!anyd && h2) ? h264::MBK_B16x8 : ((!anyd && v2) ? h264::MBK_B8x16 : h264::MBK_B8x8);
+      }
+    }
+  }
+  const int lm = qm[q];  // this lane's quadrant
+  uint32_t pw = lm == 0 ? pd : (lm == 1 ? pb : (lm == 2 ? p0w : p1w));
   *reinterpret_cast<uint32_t*>(a.pred_out + o * 256 + r * 16 + c0) = pw;
   if (lane == 0) {
     MbHeader* h = a.hdr + o;
-    h->kind = mode == 0 ? h264::MBK_BDIRECT : h264::MBK_B16x16;
-    h->sub_direct = 0;
-    const bool u0 = mode != 2, u1 = mode != 1;
-    const uint32_t r0 = mode == 0 ? drw : (u0 ? 0u : 0xFFFFFFFFu), r1 = u1 ? 0u : 0xFFFFFFFFu;
-    *reinterpret_cast<uint2*>(&h->ref[0][0]) = make_uint2(r0, r1);
+    h->kind = static_cast<uint8_t>(kind);
+    int sd = 0;
     uint32_t w[2][4];
+    int8_t rf[2][4];
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) {
+      const int m = qm[qq];
       int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
-      if (mode == 0) {
+      if (m == 0) {  // direct (the whole MB or a B_Direct_8x8 quadrant)
         x0 = dm[qq * 2]; y0 = dm[qq * 2 + 1]; x1 = dm[8 + qq * 2]; y1 = dm[8 + qq * 2 + 1];
+        rf[0][qq] = static_cast<int8_t>((drw >> (8 * qq)) & 255);
+        rf[1][qq] = 0;
+        sd |= 1 << qq;
       } else {
+        const bool u0 = m != 3, u1 = m != 2;
         if (u0) { x0 = m0x; y0 = m0y; }
         if (u1) { x1 = m1x; y1 = m1y; }
+        rf[0][qq] = u0 ? 0 : -1;
+        rf[1][qq] = u1 ? 0 : -1;
       }
       w[0][qq] = (static_cast<uint32_t>(x0) & 0xFFFFu) | (static_cast<uint32_t>(y0) << 16);
       w[1][qq] = (static_cast<uint32_t>(x1) & 0xFFFFu) | (static_cast<uint32_t>(y1) << 16);
     }
+    h->sub_direct = static_cast<uint8_t>(kind == h264::MBK_B8x8 ? sd : 0);
+#pragma unroll
+    for (int l = 0; l < 2; ++l)
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) h->ref[l][qq] = rf[l][qq];
     uint4* mvp = reinterpret_cast<uint4*>(&h->mv[0][0][0]);  // 16-byte aligned
     mvp[0] = make_uint4(w[0][0], w[0][1], w[0][2], w[0][3]);
     mvp[1] = make_uint4(w[1][0], w[1][1], w[1][2], w[1][3]);
@@ -938,9 +1003,10 @@ extern "C" void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src
                                      const uint8_t* pred1, const int16_t* pm0, const int16_t* pm1, const int16_t* dmv,
                                      const int* qp, const int8_t* aq, void* hdr, uint8_t* pred_out, int* cost_out,
                                      void* stream, const int* w1, int nref, const int8_t* dref,
-                                     const uint8_t* const* ref0k, const uint8_t* const* hp0k, int direct_only) {
+                                     const uint8_t* const* ref0k, const uint8_t* const* hp0k, int direct_only, int bparts) {
   BDecideArgs a;
   a.direct_only = direct_only;
+  a.bparts = bparts;
   for (int r = 0; r < kMaxRefs; ++r) {
     const int rr = r < nref ? r : nref - 1;
     a.w1[r] = w1[rr];

@@ -88,6 +88,9 @@ class H264Params:
     # charged to a split beyond its mvds; part_min_satd: 16x16 SATD at or below which the
     # split is not searched
     partitions: bool = True
+    # x264 --partitions b8x8: B macroblocks split into quadrants that pick their own candidate
+    # (direct, L0, L1, bi of the MB's two searched vectors): B_16x8 / B_8x16 / B_8x8
+    bpartitions: bool = True
     # (1080p CRF23 sweep, profiles/r2_partition_sweep.txt: 8 / 2000 -> -0.5% bits at equal
     # PSNR for ~1% of the step time; a threshold of 0 searches every MB for the same bits)
     part_overhead: int = int(os.environ.get("MIVC_PART_OVERHEAD", 8))
@@ -98,8 +101,10 @@ class H264Params:
     p_early_sad: int = int(os.environ.get("MIVC_P_EARLY_SAD", 0))
     b_early_sad: int = int(os.environ.get("MIVC_B_EARLY_SAD", 1024))
     # B macroblocks whose temporal-direct cost (SATD + lambda, a b_decide pre-pass) is <= b_gate
-    # skip both list searches (x264's early B_Skip / direct termination); 0 disables
-    b_gate: int = int(os.environ.get("MIVC_B_GATE", 0))
+    # (< 0: -b_gate lambdas) skip both list searches and take direct (x264's early B_Skip /
+    # direct termination); 0 disables.  1080p RD sweep (profiles/r3_b_gate_rd.md): 2400 ->
+    # -8.8 % BD-rate (PSNR-Y) and +7..20 % fps against no gate
+    b_gate: int = int(os.environ.get("MIVC_B_GATE", 2400))
     # deblock non-reference B pictures even when neither metrics nor the reconstruction
     # are requested (x264 --full-recon); the bitstream does not depend on it
     full_recon: bool = False
@@ -149,7 +154,7 @@ class H264Params:
             return "Constrained Baseline CAVLC"
         nb = self.eff_bframes()
         return (("High CABAC 8x8dct" if self.eff_t8x8() else "Main CABAC") + (" i8x8" if self.eff_t8x8() and self.i8x8 else "")
-                + (" p8x8" if self.eff_partitions() else "") + (f" ref{self.eff_refs()}" if self.eff_refs() > 1 else "")
+                + (" p8x8" if self.eff_partitions() else "") + (" b8x8" if self.eff_partitions() and self.bpartitions and self.eff_bframes() else "") + (f" ref{self.eff_refs()}" if self.eff_refs() > 1 else "")
                 + (" weightp" if self.eff_weightp() else "")
                 + (f" {nb}B temporal-direct" if nb else "") + (" weightb" if nb and self.weightb else ""))
 
@@ -547,7 +552,7 @@ class GpuH264Encoder:
                 self.hip.b_decide(B, wmb, hmb, sy, f0y, f1y, hp0, hp1, P(self.mv), P(self.mv1), P(self.me_cost),
                                   P(self.me_cost1), P(self.pred), P(self.pred1), P(self.pm0), P(self.pm1),
                                   P(self.dmv), P(self.qp), aq, P(hdr), P(self.pred_b), P(self.cost_b), s, w1s,
-                                  P(self.dref) if nr > 1 else 0, r0y, r0h)
+                                  P(self.dref) if nr > 1 else 0, r0y, r0h, 0, int(self.p.eff_partitions() and self.p.bpartitions))
             if cut is not None:
                 self.intra_cost.masked_fill_(cut[:, None], -1)
             with st("inter"):

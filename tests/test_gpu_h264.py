@@ -381,3 +381,15 @@ def test_gpu_h264_weightp_static_content_unweighted(host):
     enc, res, _ = _run(176, 144, slots=2, frames=5, crf=None, qp=28, bframes=0)
     _check_roundtrip(host, enc, res, 176, 144)
     assert enc.stats.get("weightp_pictures", 0) == 0, enc.stats
+
+
+def test_gpu_h264_b_partitions_roundtrip(host):
+    """x264 --partitions b8x8: B macroblocks whose quadrants prefer different candidates
+    (direct, L0, L1, bi) are coded as B_16x8 / B_8x16 / B_8x8 (with B_Direct_8x8 quadrants);
+    the CPU decoder reconstructs the same pictures and the split shapes occur."""
+    enc, res, _ = _run(352, 288, slots=2, frames=9, crf=None, qp=24, bframes=3, b_gate=0)
+    _check_roundtrip(host, enc, res, 352, 288)
+    kinds = np.concatenate([np.asarray(p["mb_kind"]).ravel() for r in res for p in host.decode(r.bitstream)])
+    assert np.isin(kinds, [10, 11, 12]).sum() > 0, np.bincount(kinds.astype(np.int64) + 1)
+    enc, res, _ = _run(352, 288, slots=2, frames=9, crf=None, qp=24, bframes=3, b_gate=-150, bpartitions=False)
+    _check_roundtrip(host, enc, res, 352, 288)
