@@ -85,7 +85,7 @@ int mivc_launch_scale(const void* in, int w, int h, long long in_stride, long lo
 void mivc_launch_hevc_intra(int B, int W, int H, const uint16_t* sy, const uint16_t* su, const uint16_t* sv,
                             uint16_t* ry, uint16_t* ru, uint16_t* rv, void* ctu, void* cu, int16_t* cy, int16_t* cu_,
                             int16_t* cv, const int* qp, const int8_t* run, int* cand, int bd, int analyze, int recon,
-                            int* err, int sdh, const uint8_t* ctb_mask, void* stream);
+                            int* err, int sdh, const uint8_t* ctb_mask, void* stream, int ctu64);
 void mivc_launch_hevc_inter(int B, int W, int H, const uint16_t* sy, const uint16_t* su, const uint16_t* sv,
                             const uint16_t* fy, const uint16_t* fu, const uint16_t* fv, uint16_t* ry, uint16_t* ru,
                             uint16_t* rv, void* ctu, void* cu, int16_t* cy, int16_t* cu_, int16_t* cv, const int* qp,
@@ -109,10 +109,10 @@ void mivc_launch_hevc_merge_refine(int B, int wmb, int hmb, const uint8_t* src_y
                                    const int16_t* mv_in, int16_t* mv_out, int* cost, const int16_t* pm, const int* qp,
                                    const int8_t* aq, void* stream);
 void mivc_launch_hevc_qp_fixup(int B, int W, int H, void* ctu, const void* cu, const int* qp, const int8_t* run,
-                               int wpp, void* stream);
+                               int wpp, void* stream, int ctu64);
 void mivc_launch_hevc_sao(int B, int W, int H, int bd, const uint16_t* dy, const uint16_t* du, const uint16_t* dv,
                           uint16_t* y, uint16_t* u, uint16_t* v, const uint16_t* sy, const uint16_t* su,
-                          const uint16_t* sv, void* ctu, const int* qp, const int8_t* run, int enable, void* stream);
+                          const uint16_t* sv, void* ctu, const int* qp, const int8_t* run, int enable, void* stream, int ctu64);
 size_t mivc_cavlc_mb_bytes();
 size_t mivc_cabac_nb_bytes();
 int mivc_cabac_gap();
@@ -369,15 +369,15 @@ PYBIND11_MODULE(_hip, m) {
   m.def("hevc_intra", [](int B, int W, int H, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t ry, uintptr_t ru,
                          uintptr_t rv, uintptr_t ctu, uintptr_t cu, uintptr_t cy, uintptr_t cu_, uintptr_t cv,
                          uintptr_t qp, uintptr_t run, uintptr_t cand, int bd, int analyze, int recon, uintptr_t err,
-                         uintptr_t stream, int sdh, uintptr_t ctb_mask) {
+                         uintptr_t stream, int sdh, uintptr_t ctb_mask, int ctu64) {
     mivc_launch_hevc_intra(B, W, H, P<uint16_t>(sy), P<uint16_t>(su), P<uint16_t>(sv), P<uint16_t>(ry), P<uint16_t>(ru),
                            P<uint16_t>(rv), P<void>(ctu), P<void>(cu), P<int16_t>(cy), P<int16_t>(cu_), P<int16_t>(cv),
                            P<int>(qp), P<int8_t>(run), P<int>(cand), bd, analyze, recon, P<int>(err), sdh,
-                           P<uint8_t>(ctb_mask), S(stream));
+                           P<uint8_t>(ctb_mask), S(stream), ctu64);
   }, py::arg("B"), py::arg("W"), py::arg("H"), py::arg("sy"), py::arg("su"), py::arg("sv"), py::arg("ry"), py::arg("ru"),
      py::arg("rv"), py::arg("ctu"), py::arg("cu"), py::arg("cy"), py::arg("cu_"), py::arg("cv"), py::arg("qp"),
      py::arg("run"), py::arg("cand"), py::arg("bd"), py::arg("analyze"), py::arg("recon"), py::arg("err"),
-     py::arg("stream"), py::arg("sdh") = 0, py::arg("ctb_mask") = 0);
+     py::arg("stream"), py::arg("sdh") = 0, py::arg("ctb_mask") = 0, py::arg("ctu64") = 0);
   m.def("hevc_inter", [](int B, int W, int H, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t fy, uintptr_t fu,
                          uintptr_t fv, uintptr_t ry, uintptr_t ru, uintptr_t rv, uintptr_t ctu, uintptr_t cu, uintptr_t cy,
                          uintptr_t cu_, uintptr_t cv, uintptr_t qp, uintptr_t run, uintptr_t cand, uintptr_t mv,
@@ -455,16 +455,19 @@ PYBIND11_MODULE(_hip, m) {
                                   P<int16_t>(mv_out), P<int>(cost), P<int16_t>(pm), P<int>(qp), P<int8_t>(aq), S(stream));
   });
   m.def("hevc_qp_fixup", [](int B, int W, int H, uintptr_t ctu, uintptr_t cu, uintptr_t qp, uintptr_t run, int wpp,
-                            uintptr_t stream) {
-    mivc_launch_hevc_qp_fixup(B, W, H, P<void>(ctu), P<void>(cu), P<int>(qp), P<int8_t>(run), wpp, S(stream));
-  });
+                            uintptr_t stream, int ctu64) {
+    mivc_launch_hevc_qp_fixup(B, W, H, P<void>(ctu), P<void>(cu), P<int>(qp), P<int8_t>(run), wpp, S(stream), ctu64);
+  }, py::arg("B"), py::arg("W"), py::arg("H"), py::arg("ctu"), py::arg("cu"), py::arg("qp"), py::arg("run"),
+     py::arg("wpp"), py::arg("stream"), py::arg("ctu64") = 0);
   m.def("hevc_sao", [](int B, int W, int H, int bd, uintptr_t dy, uintptr_t du, uintptr_t dv, uintptr_t y, uintptr_t u,
                        uintptr_t v, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t ctu, uintptr_t qp, uintptr_t run,
-                       int enable, uintptr_t stream) {
+                       int enable, uintptr_t stream, int ctu64) {
     mivc_launch_hevc_sao(B, W, H, bd, P<uint16_t>(dy), P<uint16_t>(du), P<uint16_t>(dv), P<uint16_t>(y), P<uint16_t>(u),
                          P<uint16_t>(v), P<uint16_t>(sy), P<uint16_t>(su), P<uint16_t>(sv), P<void>(ctu), P<int>(qp),
-                         P<int8_t>(run), enable, S(stream));
-  });
+                         P<int8_t>(run), enable, S(stream), ctu64);
+  }, py::arg("B"), py::arg("W"), py::arg("H"), py::arg("bd"), py::arg("dy"), py::arg("du"), py::arg("dv"), py::arg("y"),
+     py::arg("u"), py::arg("v"), py::arg("sy"), py::arg("su"), py::arg("sv"), py::arg("ctu"), py::arg("qp"),
+     py::arg("run"), py::arg("enable"), py::arg("stream"), py::arg("ctu64") = 0);
   // HEVC decode reconstruction (hevc_decode.hip): `p` maps HevcDecParams field names to
   // ints (device pointers as data_ptr(), scalars); stage 0..5 (see the launcher)
   m.def("hevc_decode_stage", [](const py::dict& p, int stage, uintptr_t stream) {

@@ -252,6 +252,11 @@ struct HevcSaoArgs {
   const int* qp;   // [B, nctb] QpY per CTB
   const int8_t* run;
   int enable;
+  // 64x64 CTUs (one SAO parameter set per CTU): 0 = 32x32 CTBs (statistics, decision and
+  // apply per workgroup); 1 = one workgroup per CTU gathers the statistics of its four
+  // record blocks, decides and writes the parameters into all four records; 2 = one
+  // workgroup per record block applies its CTU's parameters
+  int mode;
 };
 
 struct SaoShared {
@@ -280,10 +285,18 @@ __device__ __forceinline__ long long sao_dd(int n, int s, int o) {
 
 __global__ __launch_bounds__(256) void hevc_sao(HevcSaoArgs a) {
   __shared__ SaoShared S;
-  const int ci = blockIdx.x, slot = blockIdx.y;
+  const int slot = blockIdx.y;
   if (a.run[slot] == 0) return;
-  const int rx = ci % a.wctb, ry = ci / a.wctb;
   const int tid = threadIdx.x;
+  int ci = blockIdx.x, rx = ci % a.wctb, ry = ci / a.wctb;
+  int nblk = 1;  // record blocks whose statistics feed the decision
+  if (a.mode == 1) {
+    const int wctu = (a.wctb + 1) / 2;
+    rx = (blockIdx.x % wctu) * 2;
+    ry = (blockIdx.x / wctu) * 2;
+    ci = ry * a.wctb + rx;
+    nblk = 4;
+  }
   const int bd = a.bd, maxv = (1 << bd) - 1;
   for (int i = tid; i < 3 * 16; i += 256) {
     (&S.eo_cnt[0][0][0])[i] = 0;
@@ -292,6 +305,19 @@ __global__ __launch_bounds__(256) void hevc_sao(HevcSaoArgs a) {
   for (int i = tid; i < 3 * 32; i += 256) {
     (&S.bo_cnt[0][0])[i] = 0;
     (&S.bo_sum[0][0])[i] = 0;
+  }
+  // sample (x, y) of component c relative to its CTB block, x, y in [-1, cs]
+  auto T = [&](int c, int x, int y) -> int {
+    return c == 0 ? S.tile[(y + 1) * 34 + x + 1] : S.tile[34 * 34 + (c - 1) * 18 * 18 + (y + 1) * 18 + x + 1];
+  };
+  static constexpr int hp[4][2] = {{-1, 1}, {0, 0}, {-1, 1}, {1, -1}};
+  static constexpr int vp[4][2] = {{0, 0}, {-1, 1}, {-1, 1}, {-1, 1}};
+  for (int j = 0; j < nblk; ++j) {
+  if (a.mode == 1) {
+    rx = (ci % a.wctb) + (j & 1);
+    ry = (ci / a.wctb) + (j >> 1);
+    if (rx >= a.wctb || ry >= a.hctb) continue;  // (uniform) partial CTU at the picture edge
+    __syncthreads();  // the previous block's statistics are done with the tile
   }
   for (int i = tid; i < 34 * 34 + 2 * 18 * 18; i += 256) {
     int c = 0, k = i;
@@ -306,14 +332,8 @@ __global__ __launch_bounds__(256) void hevc_sao(HevcSaoArgs a) {
     S.tile[i] = d[static_cast<size_t>(Y) * pw + X];  // border samples outside the picture: never used
   }
   __syncthreads();
-  // sample (x, y) of component c relative to its CTB block, x, y in [-1, cs]
-  auto T = [&](int c, int x, int y) -> int {
-    return c == 0 ? S.tile[(y + 1) * 34 + x + 1] : S.tile[34 * 34 + (c - 1) * 18 * 18 + (y + 1) * 18 + x + 1];
-  };
-  static constexpr int hp[4][2] = {{-1, 1}, {0, 0}, {-1, 1}, {1, -1}};
-  static constexpr int vp[4][2] = {{0, 0}, {-1, 1}, {-1, 1}, {-1, 1}};
   // ---- statistics (luma 1024 samples, chroma 2 x 256)
-  if (a.enable) {
+  if (a.enable && a.mode != 2) {
     for (int i = tid; i < 1024 + 512; i += 256) {
       int c, x, y;
       if (i < 1024) {
@@ -346,7 +366,18 @@ __global__ __launch_bounds__(256) void hevc_sao(HevcSaoArgs a) {
       }
     }
   }
+  }  // record blocks
   __syncthreads();
+  if (a.mode == 2) {  // apply the parameters its CTU's first record block carries
+    const CtuInfo* t0 = a.ctu + static_cast<size_t>(slot) * a.wctb * a.hctb + (ry & ~1) * a.wctb + (rx & ~1);
+    if (tid < 2) {
+      S.type[tid] = t0->sao_type[tid];
+      S.cls[tid] = t0->sao_class[tid];
+    }
+    if (tid < 12) S.off[tid >> 2][tid & 3] = t0->sao_off[tid >> 2][tid & 3];
+    if (tid < 3) S.band[tid] = t0->sao_band[tid];
+  }
+  if (a.mode != 2) {
   // ---- decision (thread 0: luma, thread 1: chroma pair)
   if (tid < 2) {
     const int qp = a.qp[static_cast<size_t>(slot) * a.wctb * a.hctb + ci];
@@ -431,17 +462,23 @@ __global__ __launch_bounds__(256) void hevc_sao(HevcSaoArgs a) {
     }
   }
   __syncthreads();
-  if (tid == 0) {
-    CtuInfo* t = a.ctu + static_cast<size_t>(slot) * a.wctb * a.hctb + ci;
-    for (int k = 0; k < 2; ++k) {
-      t->sao_type[k] = static_cast<uint8_t>(S.type[k]);
-      t->sao_class[k] = static_cast<uint8_t>(S.cls[k]);
-    }
-    for (int c = 0; c < 3; ++c) {
-      t->sao_band[c] = static_cast<uint8_t>(S.band[c]);
-      for (int k = 0; k < 4; ++k) t->sao_off[c][k] = static_cast<int8_t>(S.type[c ? 1 : 0] ? S.off[c][k] : 0);
+  if (tid < nblk) {  // mode 1: every record block of the CTU carries its parameters
+    const int bx = (ci % a.wctb) + (tid & 1), by = (ci / a.wctb) + (tid >> 1);
+    if (bx < a.wctb && by < a.hctb) {
+      CtuInfo* t = a.ctu + static_cast<size_t>(slot) * a.wctb * a.hctb + by * a.wctb + bx;
+      for (int k = 0; k < 2; ++k) {
+        t->sao_type[k] = static_cast<uint8_t>(S.type[k]);
+        t->sao_class[k] = static_cast<uint8_t>(S.cls[k]);
+      }
+      for (int c = 0; c < 3; ++c) {
+        t->sao_band[c] = static_cast<uint8_t>(S.band[c]);
+        for (int k = 0; k < 4; ++k) t->sao_off[c][k] = static_cast<int8_t>(S.type[c ? 1 : 0] ? S.off[c][k] : 0);
+      }
     }
   }
+  }  // decision (mode != 2)
+  if (a.mode == 1) return;  // applied by the per-block launch
+  __syncthreads();
   // ---- apply (reads the deblocked copy, writes the output)
   for (int i = tid; i < 1024 + 512; i += 256) {
     int c, x, y;
@@ -538,26 +575,62 @@ __global__ __launch_bounds__(256) void hevc_aq_ctb(int W, int H, int bd, const u
 // its first CU with a coded residual, earlier CUs keep the prediction, and a CTB
 // without any coded residual takes the prediction as its QpY.  Deblocking and the
 // CABAC writer read the result.  One thread per CTB row (WPP) or per slot.
+//
+// 64x64 CTUs (ctu64): the 32x32 record blocks are the quantization groups (diff_cu_qp_delta_depth
+// 1) of a CTU, coded in z-order; a group's prediction averages the QpY left of and above it
+// when those lie in the same CTU (the right column's top granule of the left block, the
+// bottom row's left granule of the block above), each replaced by qPY_PREV otherwise.
+__device__ __forceinline__ int qg_granule_qp(const CtuInfo& t, int z) { return z >= t.qp_first ? t.qp : t.qp_pred; }
+
 __global__ __launch_bounds__(256) void hevc_qp_fixup(int wctb, int hctb, CtuInfo* __restrict__ ctu,
                                                      const CuInfo* __restrict__ cu, const int* __restrict__ qp,
-                                                     const int8_t* __restrict__ run, int wpp) {
+                                                     const int8_t* __restrict__ run, int wpp, int ctu64) {
   const int slot = blockIdx.x;
   if (run[slot] == 0) return;
   const int nctb = wctb * hctb;
+  auto first_coded = [&](size_t c) {
+    const CuInfo* g = cu + c * 16;
+    int first = 16;
+    for (int k = 15; k >= 0; --k)
+      if (g[k].cbf) first = k;
+    if (first < 16) {  // QpY is per CU: the whole CU whose TU carries the delta takes it
+      const int lgc = (g[first].flags >> 1) & 3;
+      first &= ~((1 << (2 * lgc)) - 1);
+    }
+    return first;
+  };
+  if (ctu64) {
+    const int wctu = (wctb + 1) / 2, hctu = (hctb + 1) / 2;
+    const int rows_per = wpp ? 1 : hctu;
+    for (int r0 = threadIdx.x * rows_per; r0 < hctu; r0 += blockDim.x * rows_per) {
+      int prev = qp[slot];
+      for (int r = r0; r < r0 + rows_per; ++r)
+        for (int x = 0; x < wctu; ++x)
+          for (int q = 0; q < 4; ++q) {
+            const int bx = 2 * x + (q & 1), by = 2 * r + (q >> 1);
+            if (bx >= wctb || by >= hctb) continue;
+            const size_t base = static_cast<size_t>(slot) * nctb;
+            const size_t c = base + by * wctb + bx;
+            const int first = first_coded(c);
+            const int qa = (q & 1) ? qg_granule_qp(ctu[base + by * wctb + bx - 1], 5) : prev;
+            const int qb = (q & 2) ? qg_granule_qp(ctu[base + (by - 1) * wctb + bx], 10) : prev;
+            const int pred = (qa + qb + 1) >> 1;
+            CtuInfo& t = ctu[c];
+            t.qp_pred = static_cast<int8_t>(pred);
+            t.qp_first = static_cast<uint8_t>(first);
+            if (first == 16) t.qp = static_cast<int8_t>(pred);
+            prev = t.qp;
+          }
+    }
+    return;
+  }
   const int rows_per = wpp ? 1 : hctb;
   for (int r0 = threadIdx.x * rows_per; r0 < hctb; r0 += blockDim.x * rows_per) {
     int prev = qp[slot];
     for (int r = r0; r < r0 + rows_per; ++r)
       for (int x = 0; x < wctb; ++x) {
         const size_t c = static_cast<size_t>(slot) * nctb + r * wctb + x;
-        const CuInfo* g = cu + c * 16;
-        int first = 16;
-        for (int k = 15; k >= 0; --k)
-          if (g[k].cbf) first = k;
-        if (first < 16) {  // QpY is per CU: the whole CU whose TU carries the delta takes it
-          const int lgc = (g[first].flags >> 1) & 3;
-          first &= ~((1 << (2 * lgc)) - 1);
-        }
+        const int first = first_coded(c);
         CtuInfo& t = ctu[c];
         t.qp_pred = static_cast<int8_t>(prev);
         t.qp_first = static_cast<uint8_t>(first);
@@ -721,9 +794,18 @@ extern "C" void mivc_launch_hevc_deblock(int B, int W, int H, int bd, uint16_t* 
 extern "C" void mivc_launch_hevc_sao(int B, int W, int H, int bd, const uint16_t* dy, const uint16_t* du,
                                      const uint16_t* dv, uint16_t* y, uint16_t* u, uint16_t* v, const uint16_t* sy,
                                      const uint16_t* su, const uint16_t* sv, void* ctu, const int* qp,
-                                     const int8_t* run, int enable, void* stream) {
-  HevcSaoArgs a{B, W, H, W / 32, H / 32, bd, dy, du, dv, y, u, v, sy, su, sv, static_cast<CtuInfo*>(ctu), qp, run, enable};
-  hipLaunchKernelGGL(hevc_sao, dim3((W / 32) * (H / 32), B), dim3(256), 0, static_cast<hipStream_t>(stream), a);
+                                     const int8_t* run, int enable, void* stream, int ctu64) {
+  HevcSaoArgs a{B, W, H, W / 32, H / 32, bd, dy, du, dv, y, u, v, sy, su, sv, static_cast<CtuInfo*>(ctu), qp, run, enable,
+                0};
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (!ctu64) {
+    hipLaunchKernelGGL(hevc_sao, dim3((W / 32) * (H / 32), B), dim3(256), 0, s, a);
+    return;
+  }
+  a.mode = 1;
+  hipLaunchKernelGGL(hevc_sao, dim3(((W / 32 + 1) / 2) * ((H / 32 + 1) / 2), B), dim3(256), 0, s, a);
+  a.mode = 2;
+  hipLaunchKernelGGL(hevc_sao, dim3((W / 32) * (H / 32), B), dim3(256), 0, s, a);
 }
 
 // ctb_qp: [B, nctb] int32 out; mb_aq: [B, nmb16] int8 out (may be null); extra: optional
@@ -737,9 +819,9 @@ extern "C" void mivc_launch_hevc_aq(int B, int W, int H, int bd, const uint16_t*
 }
 
 extern "C" void mivc_launch_hevc_qp_fixup(int B, int W, int H, void* ctu, const void* cu, const int* qp,
-                                          const int8_t* run, int wpp, void* stream) {
+                                          const int8_t* run, int wpp, void* stream, int ctu64) {
   hipLaunchKernelGGL(hevc_qp_fixup, dim3(B), dim3(256), 0, static_cast<hipStream_t>(stream), W / 32, H / 32,
-                     static_cast<CtuInfo*>(ctu), static_cast<const CuInfo*>(cu), qp, run, wpp);
+                     static_cast<CtuInfo*>(ctu), static_cast<const CuInfo*>(cu), qp, run, wpp, ctu64);
 }
 
 // levels of B slots -> packed form: nzmap [B, nctb, 2] u64, off [B, nctb] u32, out: B slots of

@@ -38,24 +38,23 @@ struct HevcIntraArgs {
   int nxn_in_p;                           // evaluate PART_NxN in P pictures too
   const uint8_t* ctb_mask;                // [B, nctb] analyse only where nonzero (P pictures: the CTBs
                                           // where intra may beat the motion search); null = every CTB
+  int ctu64;                              // 64x64 CTUs: the 32x32 blocks are coded in z-order inside them
 };
 
 constexpr int kNoIntra = 1 << 26;  // candidate cost of a CTB the analysis skipped (inter decisive)
 
-// luma neighbour (xr, yr) of a CTB-relative block position: z-scan availability (6.4.1)
-// at the 4x4 minimum-TB granularity; zcur = z-order index (zorder4) of the current
-// block's first 4x4 block
-__device__ __forceinline__ bool nb_avail(int xr, int yr, int zcur, int rx, int ry, int wctb) {
-  if (yr < 0) {
-    if (ry == 0) return false;
-    if (xr < 0) return rx > 0;
-    if (xr >= 32) return rx + 1 < wctb && xr < 64;
-    return true;
-  }
-  if (yr >= 32) return false;
-  if (xr < 0) return rx > 0;
-  if (xr >= 32) return false;
-  return zorder4(xr >> 2, yr >> 2) < zcur;
+// luma neighbour (xr, yr) of a position relative to the 32x32 block (rx, ry): z-scan
+// availability (6.4.1) at the 4x4 minimum-TB granularity; zcur = z-order index (zorder4) of
+// the current block's first 4x4 block.  32x32 CTBs: blocks in raster order; 64x64 CTUs
+// (ctu64): CTUs in raster order, their four blocks in z-order.
+__device__ __forceinline__ bool nb_avail(int xr, int yr, int zcur, int rx, int ry, int wctb, int hctb, int ctu64) {
+  const int tx = rx + (xr >> 5), ty = ry + (yr >> 5);
+  if (tx < 0 || ty < 0 || tx >= wctb || ty >= hctb) return false;
+  if (tx == rx && ty == ry) return zorder4((xr & 31) >> 2, (yr & 31) >> 2) < zcur;
+  if (!ctu64) return ty < ry || (ty == ry && tx < rx);
+  const int ux = tx >> 1, uy = ty >> 1, cx = rx >> 1, cy = ry >> 1;
+  if (ux != cx || uy != cy) return uy < cy || (uy == cy && ux < cx);
+  return ((tx & 1) | ((ty & 1) << 1)) < ((rx & 1) | ((ry & 1) << 1));
 }
 
 __device__ __forceinline__ void ref_pos(int i, int n, int cx, int cy, int* x, int* y) {
@@ -195,7 +194,7 @@ __global__ __launch_bounds__(256, 4) void hevc_intra_analyze(HevcIntraArgs a) {
     for (int i = 0; i < E; ++i) {
       int x, y;
       ref_pos(i, n, cx, cy, &x, &y);
-      if (nb_avail(x, y, zc, rx, ry, g.wctb)) {
+      if (nb_avail(x, y, zc, rx, ry, g.wctb, g.hctb, a.ctu64)) {
         p[i] = S.ext[(y + 1) * 65 + x + 1];
         if (first < 0) first = i;
       } else {
@@ -232,7 +231,7 @@ __global__ __launch_bounds__(256, 4) void hevc_intra_analyze(HevcIntraArgs a) {
     for (int i = 0; i < 17; ++i) {
       int x, y;
       ref_pos(i, 4, px, py, &x, &y);
-      if (nb_avail(x, y, pu, rx, ry, g.wctb)) {
+      if (nb_avail(x, y, pu, rx, ry, g.wctb, g.hctb, a.ctu64)) {
         p[i] = S.ext[(y + 1) * 65 + x + 1];
         if (first < 0) first = i;
       } else {
@@ -506,7 +505,7 @@ struct ReconShared {
   int p[129], q[129];            // reference arrays (unfiltered, filtered)
   int R[32 * 32], S[32 * 32];    // residual / transform scratch
   uint16_t pred[32 * 32];
-  int saved_x;
+  int saved_x, saved_ry;            // block whose right column saved_y / saved_c hold
   uint16_t saved_y[32];
   uint16_t saved_c[2][16];
 };
@@ -528,12 +527,16 @@ __device__ __forceinline__ bool recon_block(const HevcIntraArgs& a, ReconShared&
                  [&](int i) {
                    int x, y;
                    ref_pos(i, n, cx, cy, &x, &y);
-                   return nb_avail(x << sc, y << sc, zc, rx, ry, g.wctb);
+                   return nb_avail(x << sc, y << sc, zc, rx, ry, g.wctb, g.hctb, a.ctu64);
                  },
                  [&](int i) {
                    int x, y;
                    ref_pos(i, n, cx, cy, &x, &y);
-                   return static_cast<int>(tile[(y + 1) * stride + x + 1]);
+                   // ctu64: the column below-left (x -1, y >= the block height) is kept in the
+                   // tile's last column, which the block itself never uses
+                   const int lim = LUMA ? 32 : 16;
+                   const bool below = y >= lim;
+                   return static_cast<int>(tile[((below ? y - lim : y) + 1) * stride + (below ? stride - 1 : x + 1)]);
                  });
   const int* p = S.p;
   if (LUMA && hv::intra_filter_flag(mode, n)) {
@@ -569,8 +572,9 @@ __device__ __forceinline__ bool recon_block(const HevcIntraArgs& a, ReconShared&
   return nz;
 }
 
-__device__ void hevc_recon_ctb(const HevcIntraArgs& a, ReconShared& S, const hv::DctLds& D, int slot, int rx, int ry,
-                               int run) {
+// (inlined at its single call site: its LDS structures stay ds_ addressed, no call frame)
+__device__ __forceinline__ void hevc_recon_ctb(const HevcIntraArgs& a, ReconShared& S, const hv::DctLds& D, int slot,
+                                               int rx, int ry, int run) {
   const HevcGeom& g = a.g;
   const int lane = lane_id();
   const int X0 = rx * 32, Y0 = ry * 32;
@@ -586,14 +590,25 @@ __device__ void hevc_recon_ctb(const HevcIntraArgs& a, ReconShared& S, const hv:
   }
   if (lane < 32) {
     uint16_t v = 0;
-    if (rx > 0) v = S.saved_x == rx - 1 ? S.saved_y[lane] : recy[static_cast<size_t>(Y0 + lane) * g.W + X0 - 1];
+    if (rx > 0) v = (S.saved_x == rx - 1 && S.saved_ry == ry) ? S.saved_y[lane] : recy[static_cast<size_t>(Y0 + lane) * g.W + X0 - 1];
     S.rt[(lane + 1) * RT] = v;
   } else {
     const int c = (lane - 32) >> 4, i = (lane - 32) & 15;
     const uint16_t* rc = c == 0 ? recu : recv;
     uint16_t v = 0;
-    if (rx > 0) v = S.saved_x == rx - 1 ? S.saved_c[c][i] : rc[static_cast<size_t>(Y0 / 2 + i) * cw + X0 / 2 - 1];
+    if (rx > 0) v = (S.saved_x == rx - 1 && S.saved_ry == ry) ? S.saved_c[c][i] : rc[static_cast<size_t>(Y0 / 2 + i) * cw + X0 / 2 - 1];
     S.rc[c][(i + 1) * CT2] = v;
+  }
+  if (a.ctu64 && !((rx | ry) & 1) && rx > 0 && ry + 1 < g.hctb) {
+    // the top-left block of a CTU: the left column below it (x -1, y 32..63; chroma y 16..31,
+    // in the previous CTU's bottom-right block) into the tile's last column (x 63 / 31 of
+    // rows 0..31 / 0..15: right of the block, never referenced by it)
+    if (lane < 32) {
+      S.rt[(lane + 1) * RT + RT - 1] = recy[static_cast<size_t>(Y0 + 32 + lane) * g.W + X0 - 1];
+    } else {
+      const int c = (lane - 32) >> 4, i = (lane - 32) & 15;
+      S.rc[c][(i + 1) * CT2 + CT2 - 1] = (c == 0 ? recu : recv)[static_cast<size_t>(Y0 / 2 + 16 + i) * cw + X0 / 2 - 1];
+    }
   }
   for (int i = lane; i < 2 * 33; i += 64) {
     const int c = i / 33, k = i % 33;
@@ -657,8 +672,15 @@ __device__ void hevc_recon_ctb(const HevcIntraArgs& a, ReconShared& S, const hv:
     const int c = (lane - 32) >> 4, i = (lane - 32) & 15;
     S.saved_c[c][i] = S.rc[c][(i + 1) * CT2 + 16];
   }
-  if (lane == 0) S.saved_x = rx;
+  if (lane == 0) {
+    S.saved_x = rx;
+    S.saved_ry = ry;
+  }
+  // the next blocks of a CTU read this one's samples back from memory (ctu64: the row above
+  // of the lower blocks, a left column across CTUs): this wave's stores before its loads
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   wave_sync();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
 __global__ __launch_bounds__(64 * kHevcIntraWaves) void hevc_intra_recon(HevcIntraArgs a) {
@@ -672,24 +694,37 @@ __global__ __launch_bounds__(64 * kHevcIntraWaves) void hevc_intra_recon(HevcInt
   hv::dct_lds_init(D);
   for (int i = threadIdx.x; i < g.hctb; i += blockDim.x) prog[i] = 0;
   const int w = wave_id();
-  if (lane_id() == 0) SS[w].saved_x = -2;
+  if (lane_id() == 0) {
+    SS[w].saved_x = -2;
+    SS[w].saved_ry = -1;
+  }
   __syncthreads();
   ReconShared& S = SS[w];
-  for (int y = w; y < g.hctb; y += kHevcIntraWaves) {
-    for (int x = 0; x < g.wctb; ++x) {
-      // P picture: a CTB without intra CUs was fully reconstructed by hevc_inter -- no wait,
-      // no staging (the next CTB then reads its left column from memory)
-      bool work = true;
-      if (run == 2) {
-        const size_t cb = (static_cast<size_t>(slot) * g.nctb() + y * g.wctb + x) * 16;
-        work = __ballot(lane_id() < 16 && a.cu[cb + lane_id()].pred == hevc::CU_INTRA) != 0;
-      }
-      if (work) {
-        if (y > 0) row_wait(prog, y - 1, min(x + 2, g.wctb), a.err);
-        hevc_recon_ctb(a, S, D, slot, x, y, run);
-      } else {
-        if (lane_id() == 0) S.saved_x = -2;
-        wave_sync();
+  // units in wavefront order (one unit row per wave, the unit above-right done first): 32x32
+  // CTBs, or (ctu64) 64x64 CTUs whose four 32x32 blocks follow in z-order
+  const int c64 = a.ctu64 ? 1 : 0;
+  const int wu = (g.wctb + c64) >> c64, hu = (g.hctb + c64) >> c64, nq = c64 ? 4 : 1;
+  for (int y = w; y < hu; y += kHevcIntraWaves) {
+    for (int x = 0; x < wu; ++x) {
+      bool waited = false;
+      for (int q = 0; q < nq; ++q) {
+        const int bx = (x << c64) + (q & 1), by = (y << c64) + (q >> 1);
+        if (bx >= g.wctb || by >= g.hctb) continue;
+        // P picture: a block without intra CUs was fully reconstructed by hevc_inter -- no
+        // wait, no staging (the next block then reads its left column from memory)
+        bool work = true;
+        if (run == 2) {
+          const size_t cb = (static_cast<size_t>(slot) * g.nctb() + by * g.wctb + bx) * 16;
+          work = __ballot(lane_id() < 16 && a.cu[cb + lane_id()].pred == hevc::CU_INTRA) != 0;
+        }
+        if (work) {
+          if (y > 0 && !waited) row_wait(prog, y - 1, min(x + 2, wu), a.err);
+          waited = true;
+          hevc_recon_ctb(a, S, D, slot, bx, by, run);
+        } else {
+          if (lane_id() == 0) S.saved_x = -2;
+          wave_sync();
+        }
       }
       row_publish(prog, y, x + 1);
     }
@@ -726,6 +761,7 @@ static HevcIntraArgs make_intra_args(int B, int W, int H, const uint16_t* sy, co
   a.sdh = sdh;
   a.nxn_in_p = 0;
   a.ctb_mask = nullptr;
+  a.ctu64 = 0;
   return a;
 }
 
@@ -733,9 +769,10 @@ extern "C" void mivc_launch_hevc_intra(int B, int W, int H, const uint16_t* sy, 
                                        uint16_t* ry, uint16_t* ru, uint16_t* rv, void* ctu, void* cu, int16_t* cy,
                                        int16_t* cu_, int16_t* cv, const int* qp, const int8_t* run, int* cand, int bd,
                                        int analyze, int recon, int* err, int sdh, const uint8_t* ctb_mask,
-                                       void* stream) {
+                                       void* stream, int ctu64) {
   HevcIntraArgs a = make_intra_args(B, W, H, sy, su, sv, ry, ru, rv, ctu, cu, cy, cu_, cv, qp, run, cand, bd, err, sdh);
   a.ctb_mask = ctb_mask;
+  a.ctu64 = ctu64;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (analyze) hipLaunchKernelGGL(hevc_intra_analyze, dim3(a.g.nctb(), B), dim3(256), 0, s, a);
   if (recon) hipLaunchKernelGGL(hevc_intra_recon, dim3(B), dim3(64 * kHevcIntraWaves), 0, s, a);

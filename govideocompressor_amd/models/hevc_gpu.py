@@ -107,6 +107,10 @@ class HevcParams:
     # (bframe.hip hevc_b_merge; P and B pictures); False: P pictures use the neighbour-vector
     # approximation of round 2 (hevc_merge_refine)
     merge_exact: bool = True
+    # x265 --ctu 64 (its default): 64x64 coding tree units over the 32x32 record blocks (the
+    # blocks are the CTU's quantization groups and are reconstructed in z-order; one SAO
+    # parameter set per CTU; 64x64 skip CUs where four blocks agree) -- False: 32x32 CTBs
+    ctu64: bool = bool(int(os.environ.get("MIVC_HEVC_CTU64", "1")))
 
     def eff_bframes(self) -> int:
         return 0 if (self.intra_only or self.keyint > 0) else max(0, int(self.bframes))
@@ -119,7 +123,7 @@ class HevcParams:
                     sao=int(self.sao), deblock=int(self.deblock), max_merge=self.max_merge, wpp=int(self.wpp),
                     cu_qp_delta=int(self.adaptive_qp()), tu_inter_depth=int(self.tu_inter_depth), sdh=int(self.sdh),
                     level_idc=int(self.level_idc), bframes=self.eff_bframes(), tmvp=int(self.tmvp and not self.intra_only),
-                    pyramid=int(self.pyramid))
+                    pyramid=int(self.pyramid), ctu64=int(self.ctu64))
 
     def frame_qps(self) -> tuple[int, int]:
         qp_p = int(round(self.crf)) if self.crf is not None else int(self.qp)
@@ -524,7 +528,7 @@ class GpuHevcEncoder:
                 self.run.fill_(1)
                 self.prev_mv.zero_()  # no motion predictors across a closed GOP (or from an earlier call)
                 with st("intra_i"):
-                    self.hip.hevc_intra(*intra_args, 1, 1, p(self.err), s, int(self.p.sdh))
+                    self.hip.hevc_intra(*intra_args, 1, 1, p(self.err), s, int(self.p.sdh), 0, int(self.p.ctu64))
             else:
                 self.run.fill_(2)
                 ref8, hp = self.ref8s[r0], self.me_hps[r0]
@@ -597,7 +601,7 @@ class GpuHevcEncoder:
                     mask = p(self._intra_gate()) if self.p.intra_gate else 0
                     if mask:
                         gate_sum.append(self.ctb_need.sum(dtype=torch.int64))
-                    self.hip.hevc_intra(*intra_args, 1, 0, p(self.err), s, int(self.p.sdh), mask)
+                    self.hip.hevc_intra(*intra_args, 1, 0, p(self.err), s, int(self.p.sdh), mask, int(self.p.ctu64))
                 with st("inter"):
                     self.hip.hevc_inter(B, self.W, self.H, p(self.src[0]), p(self.src[1]), p(self.src[2]), p(ref[0]),
                                         p(ref[1]), p(ref[2]), p(cur[0]), p(cur[1]), p(cur[2]), p(self.ctu), p(self.cu),
@@ -605,10 +609,12 @@ class GpuHevcEncoder:
                                         p(self.cand), p(self.mv), p(self.me_cost), bd, s, int(self.p.tu_inter_depth),
                                         int(self.p.sdh), int(self.p.intra_bias_p), **inter_kw)
                 with st("intra_recon"):
-                    self.hip.hevc_intra(*intra_args, 0, 1, p(self.err), s, int(self.p.sdh))   # intra CUs, wavefront
+                    self.hip.hevc_intra(*intra_args, 0, 1, p(self.err), s, int(self.p.sdh), 0,
+                                        int(self.p.ctu64))   # intra CUs, wavefront
                 if pic.kind == "P":
                     self.prev_mv.copy_(self.mv)
-            self.hip.hevc_qp_fixup(B, self.W, self.H, p(self.ctu), p(self.cu), p(self.qp), p(self.run), int(self.p.wpp), s)
+            self.hip.hevc_qp_fixup(B, self.W, self.H, p(self.ctu), p(self.cu), p(self.qp), p(self.run), int(self.p.wpp), s,
+                                   int(self.p.ctu64))
             if self.p.deblock:
                 with st("deblock"):
                     self.hip.hevc_deblock(B, self.W, self.H, bd, p(cur[0]), p(cur[1]), p(cur[2]), p(self.cu),
@@ -620,7 +626,7 @@ class GpuHevcEncoder:
                 with st("sao"):
                     self.hip.hevc_sao(B, self.W, self.H, bd, p(cur[0]), p(cur[1]), p(cur[2]), p(out_pl[0]),
                                       p(out_pl[1]), p(out_pl[2]), p(self.src[0]), p(self.src[1]), p(self.src[2]),
-                                      p(self.ctu), p(self.ctb_qp), p(self.run), 1, s)
+                                      p(self.ctu), p(self.ctb_qp), p(self.run), 1, s, int(self.p.ctu64))
                 self.dbk = cur
                 self.rec[ci] = cur = out_pl
             if pic.ref:

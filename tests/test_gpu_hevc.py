@@ -232,3 +232,17 @@ def test_gpu_hevc_sign_data_hiding(host):
     dependent scans, inter diagonal) keeps the decoder bit-exact in I and P pictures."""
     res, rec = _encode(128, 96, 4, 2, crf=None, qp=22, sdh=True)
     _compare(host, res, rec)
+
+
+@pytest.mark.parametrize("ctu64", [False, True])
+@pytest.mark.parametrize("wpp", [True, False])
+def test_gpu_hevc_ctu64(host, ctu64, wpp):
+    """x265 --ctu 64: the 32x32 record blocks are reconstructed in z-order inside 64x64 CTUs
+    (intra availability across blocks and CTUs), each block is a quantization group whose QP
+    prediction uses the left / above block of the same CTU (AQ on: CRF with variance AQ and
+    cutree), one SAO parameter set per CTU, partial CTUs at the right and bottom edges, with
+    and without WPP -- bit-exact against the CPU decoder."""
+    res, rec = _encode(160, 96, 5, 2, crf=26, bframes=1, wpp=wpp, ctu64=ctu64)
+    _compare(host, res, rec)
+    res, rec = _encode(96, 64, 2, 2, intra_only=True, crf=None, qp=27, ctu64=ctu64, wpp=wpp)
+    _compare(host, res, rec)
