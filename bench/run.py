@@ -254,7 +254,11 @@ def _hevc_run(args, W, H, B, F, bd, crf, two_pass_kbps=None, fps=30.0, resident=
     return fps_out, dict(psnr_y_warmup=round(psnr, 2), kbps_per_stream=round(bits / (B * F) * fps / 1000, 1),
                          ms_per_step=round(dt / args.steps * 1000, 1), timings=enc.timings, rc=info, world=env.world,
                          stage_device_ms_warmup=stage_ms, encoder_stats={k: round(v, 4) for k, v in enc.stats.items()},
-                         resident_clip_gb=round(clip_gb, 1) if resident else None)
+                         resident_clip_gb=round(clip_gb, 1) if resident else None,
+                         model=(f"HEVC Main{'10' if bd == 10 else ''} CTU {64 if enc.p.ctu64 else 32}, "
+                                f"{enc.p.eff_bframes()}B{' pyramid' if enc.p.pyramid else ''}"
+                                f"{' TMVP' if enc.p.tmvp else ''}, AQ + cutree, max-merge {enc.p.max_merge}, "
+                                f"SAO, WPP{', sign hiding' if enc.p.sdh else ''}"))
 
 
 def config4(args) -> list[dict]:
