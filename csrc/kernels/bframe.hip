@@ -125,6 +125,9 @@ struct BDecideArgs {
   // (SATD + lambda) goes to cost_out; MBs whose direct cost is already low skip the searches
   // (me.hip gate) and their list costs come back as kNoCost
   int direct_only;
+  // the pre-pass ran (direct_only = 1 before the searches): pred_out / cost_out hold every MB's
+  // direct prediction and cost -- unsearched MBs keep them, the others skip the direct MC
+  int have_direct;
   int bparts;  // x264 --partitions b8x8: per-quadrant candidates (B_16x8 / B_8x16 / B_8x8)
 };
 
@@ -227,12 +230,30 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   if (a.dref) drw = *reinterpret_cast<const uint32_t*>(a.dref + o * 4);
   const int dr = (drw >> (8 * q)) & 255;
   const uint8_t *GD = dr ? a.ref0k[dr] + yo : G0, *HD = dr ? a.hp0k[dr] + ho : H0;
-  const uint32_t pd = wavg4b(mc4(GD, HD, W, H, X, Y, dm[q * 2], dm[q * 2 + 1]),
-                             mc4(G1, H1, W, H, X, Y, dm[8 + q * 2], dm[8 + q * 2 + 1]), a.w1[dr]);
+  const bool searched = !donly && a.cost0[o] < kNoCostB && a.cost1[o] < kNoCostB;
+  uint32_t* pout = reinterpret_cast<uint32_t*>(a.pred_out + o * 256 + r * 16 + c0);
+  if (!donly && !searched && a.have_direct) {
+    // gated MB: B_Direct_16x16 with the pre-pass's prediction and cost
+    if (lane == 0) {
+      MbHeader* h = a.hdr + o;
+      h->kind = h264::MBK_BDIRECT;
+      h->sub_direct = 0;
+      *reinterpret_cast<uint2*>(&h->ref[0][0]) = make_uint2(drw, 0u);
+      uint4* mvp = reinterpret_cast<uint4*>(&h->mv[0][0][0]);
+      const uint4* dv = reinterpret_cast<const uint4*>(dm);  // [list][quadrant][xy] int16
+      mvp[0] = dv[0];
+      mvp[1] = dv[1];
+    }
+    return;
+  }
+  const uint32_t pd = (!donly && a.have_direct)
+                          ? *pout
+                          : wavg4b(mc4(GD, HD, W, H, X, Y, dm[q * 2], dm[q * 2 + 1]),
+                                   mc4(G1, H1, W, H, X, Y, dm[8 + q * 2], dm[8 + q * 2 + 1]), a.w1[dr]);
+  if (donly) *pout = pd;
   const uint32_t pb = donly ? pd : wavg4b(mc4(G0, H0, W, H, X, Y, m0x, m0y), mc4(G1, H1, W, H, X, Y, m1x, m1y), a.w1[0]);
   // residuals of the four candidates: 0 direct, 1 bi (the two ME vectors), 2 L0, 3 L1 (the ME
   // predictions; not needed by the direct-only pre-pass or for MBs the gate left unsearched)
-  const bool searched = !donly && a.cost0[o] < kNoCostB && a.cost1[o] < kNoCostB;
   const uint32_t p0w = searched ? *reinterpret_cast<const uint32_t*>(a.pred0 + o * 256 + r * 16 + c0) : pd;
   const uint32_t p1w = searched ? *reinterpret_cast<const uint32_t*>(a.pred1 + o * 256 + r * 16 + c0) : pd;
   __shared__ int s_res[4][256];
@@ -1003,9 +1024,10 @@ extern "C" void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src
                                      const uint8_t* pred1, const int16_t* pm0, const int16_t* pm1, const int16_t* dmv,
                                      const int* qp, const int8_t* aq, void* hdr, uint8_t* pred_out, int* cost_out,
                                      void* stream, const int* w1, int nref, const int8_t* dref,
-                                     const uint8_t* const* ref0k, const uint8_t* const* hp0k, int direct_only, int bparts) {
+                                     const uint8_t* const* ref0k, const uint8_t* const* hp0k, int direct_only, int bparts, int have_direct) {
   BDecideArgs a;
   a.direct_only = direct_only;
+  a.have_direct = have_direct;
   a.bparts = bparts;
   for (int r = 0; r < kMaxRefs; ++r) {
     const int rr = r < nref ? r : nref - 1;

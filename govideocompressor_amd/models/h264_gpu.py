@@ -552,7 +552,8 @@ class GpuH264Encoder:
                 self.hip.b_decide(B, wmb, hmb, sy, f0y, f1y, hp0, hp1, P(self.mv), P(self.mv1), P(self.me_cost),
                                   P(self.me_cost1), P(self.pred), P(self.pred1), P(self.pm0), P(self.pm1),
                                   P(self.dmv), P(self.qp), aq, P(hdr), P(self.pred_b), P(self.cost_b), s, w1s,
-                                  P(self.dref) if nr > 1 else 0, r0y, r0h, 0, int(self.p.eff_partitions() and self.p.bpartitions))
+                                  P(self.dref) if nr > 1 else 0, r0y, r0h, 0, int(self.p.eff_partitions() and self.p.bpartitions),
+                                  int(bg != 0))
             if cut is not None:
                 self.intra_cost.masked_fill_(cut[:, None], -1)
             with st("inter"):
