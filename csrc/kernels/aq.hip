@@ -24,14 +24,20 @@ using h264::MbHeader;
 
 // 16 lanes per MB (4 MBs per wave, 16 per 256-thread workgroup): lane l of a group sums
 // luma row l (4 dwords) and, for l < 8 Cb row l / for l >= 8 Cr row l - 8 (2 dwords); the
-// group reductions are DPP row sums.
+// group reductions are DPP row sums.  A workgroup walks kAqSpan groups of 16 MBs (one launch
+// of ~nmb / 16 tiny workgroups per slot was dispatch-bound: 0.56 TB/s).
+constexpr int kAqSpan = 8;
+
 __global__ __launch_bounds__(256) void h264_aq_offsets(Geom g, const uint8_t* __restrict__ sy,
                                                        const uint8_t* __restrict__ su, const uint8_t* __restrict__ sv,
                                                        float strength, const float* __restrict__ extra,
                                                        long long extra_stride, int8_t* __restrict__ out) {
   const int l = lane_id() & 15;
   const int nmb = g.nmb();
-  const int mb = blockIdx.x * 16 + (threadIdx.x >> 4), slot = blockIdx.y;
+  const int slot = blockIdx.y;
+  for (int it = 0; it < kAqSpan; ++it) {
+  const int mb = (blockIdx.x * kAqSpan + it) * 16 + (threadIdx.x >> 4);
+  if ((blockIdx.x * kAqSpan + it) * 16 >= nmb) break;  // (uniform)
   const bool live = mb < nmb;
   const int mbc = live ? mb : nmb - 1;
   const int mx = mbc % g.wmb, my = mbc / g.wmb;
@@ -69,6 +75,7 @@ __global__ __launch_bounds__(256) void h264_aq_offsets(Geom g, const uint8_t* __
     float adj = strength * 1.0397f * (log2f(static_cast<float>(e > 1u ? e : 1u)) - 14.427f);
     if (extra) adj += extra[slot * extra_stride + mb];  // MB-tree offset of this frame
     out[static_cast<size_t>(slot) * nmb + mb] = static_cast<int8_t>(clampi(static_cast<int>(rintf(adj)), -24, 24));
+  }
   }
 }
 
@@ -141,7 +148,8 @@ extern "C" void mivc_launch_aq_offsets(int B, int wmb, int hmb, const uint8_t* s
                                        const uint8_t* sv, float strength, const float* extra, long long extra_stride,
                                        int8_t* out, void* stream) {
   const Geom g{B, wmb, hmb, wmb * 16, hmb * 16};
-  hipLaunchKernelGGL(h264_aq_offsets, dim3((wmb * hmb + 15) / 16, B), dim3(256), 0, static_cast<hipStream_t>(stream), g,
+  hipLaunchKernelGGL(h264_aq_offsets, dim3((wmb * hmb + 16 * kAqSpan - 1) / (16 * kAqSpan), B), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), g,
                      sy, su, sv, strength, extra, extra_stride, out);
 }
 

@@ -258,16 +258,19 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   const uint32_t p1w = searched ? *reinterpret_cast<const uint32_t*>(a.pred1 + o * 256 + r * 16 + c0) : pd;
   __shared__ int s_res[4][256];
   __shared__ int s_satd[4][16];
+  const int ncand = donly ? 1 : 4;  // the pre-pass prices direct only
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int sv = static_cast<int>((src >> (8 * k)) & 255u);
     s_res[0][r * 16 + c0 + k] = sv - static_cast<int>((pd >> (8 * k)) & 255u);
-    s_res[1][r * 16 + c0 + k] = sv - static_cast<int>((pb >> (8 * k)) & 255u);
-    s_res[2][r * 16 + c0 + k] = sv - static_cast<int>((p0w >> (8 * k)) & 255u);
-    s_res[3][r * 16 + c0 + k] = sv - static_cast<int>((p1w >> (8 * k)) & 255u);
+    if (!donly) {
+      s_res[1][r * 16 + c0 + k] = sv - static_cast<int>((pb >> (8 * k)) & 255u);
+      s_res[2][r * 16 + c0 + k] = sv - static_cast<int>((p0w >> (8 * k)) & 255u);
+      s_res[3][r * 16 + c0 + k] = sv - static_cast<int>((p1w >> (8 * k)) & 255u);
+    }
   }
   wave_sync();
-  {  // one 4x4 SATD per lane: candidate lane >> 4, block lane & 15 (raster)
+  if (lane < 16 * ncand) {  // one 4x4 SATD per lane: candidate lane >> 4, block lane & 15 (raster)
     const int cand = lane >> 4, blk = lane & 15, bx = (blk & 3) * 4, by = (blk >> 2) * 4;
     int rr[16];
 #pragma unroll
@@ -279,11 +282,11 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   wave_sync();
   // per 8x8 quadrant and candidate (lanes 0..15: candidate lane >> 2, quadrant lane & 3)
   int qs = 0;
-  if (lane < 16) {
+  if (lane < 4 * ncand) {
     const int cand = lane >> 2, qq = lane & 3, b0 = (qq >> 1) * 8 + (qq & 1) * 2;
     qs = s_satd[cand][b0] + s_satd[cand][b0 + 1] + s_satd[cand][b0 + 4] + s_satd[cand][b0 + 5];
   }
-  int qsat[4][4];  // [candidate][quadrant]
+  int qsat[4][4];  // [candidate][quadrant] (the pre-pass: candidate 0 only)
 #pragma unroll
   for (int c = 0; c < 4; ++c)
 #pragma unroll

@@ -77,10 +77,17 @@ __device__ __forceinline__ CabacSliceInfo slice_info(const CabacBinArgs& a, int 
   return si;
 }
 
+// one wave = two MBs per step, kMaskSpan steps per workgroup (a workgroup per MB pair made
+// the launch dispatch-bound: a million one-wave workgroups per 1080p frame step)
+constexpr int kMaskSpan = 16;
+
 __global__ __launch_bounds__(64) void cabac_mask(CabacBinArgs a) {
   const Geom& g = a.g;
   const int lane = threadIdx.x, sub = lane & 31;
-  const int mb = blockIdx.x * 2 + (lane >> 5), slot = blockIdx.y;
+  const int slot = blockIdx.y;
+  for (int it = 0; it < kMaskSpan; ++it) {
+  const int mb = (blockIdx.x * kMaskSpan + it) * 2 + (lane >> 5);
+  if ((blockIdx.x * kMaskSpan + it) * 2 >= g.nmb()) break;  // (uniform)
   const bool live = mb < g.nmb();
   const size_t o = static_cast<size_t>(slot) * g.nmb() + (live ? mb : 0);
   const int16_t* c = a.coef + o * h264::kCoefPerMb;
@@ -103,6 +110,7 @@ __global__ __launch_bounds__(64) void cabac_mask(CabacBinArgs a) {
   const unsigned long long bal = __ballot(nz);
   const uint32_t m = static_cast<uint32_t>((bal >> (lane & 32)) & 0x7FFFFFFull);
   if (live && sub == 0) a.mask[o] = m;
+  }
 }
 
 __global__ __launch_bounds__(64) void cabac_prep(CabacBinArgs a) {
@@ -555,7 +563,7 @@ extern "C" void mivc_launch_cabac_bin(int B, int wmb, int hmb, const void* hdr, 
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int nmb = wmb * hmb;
   const dim3 mbgrid((nmb + 63) / 64, B);
-  hipLaunchKernelGGL(cabac_mask, dim3((nmb + 1) / 2, B), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(cabac_mask, dim3((nmb + 2 * kMaskSpan - 1) / (2 * kMaskSpan), B), dim3(64), 0, s, a);
   hipLaunchKernelGGL(cabac_prep, mbgrid, dim3(64), 0, s, a);
   hipLaunchKernelGGL(cabac_chain, dim3(B), dim3(64), 0, s, a);
   hipLaunchKernelGGL(cabac_count, mbgrid, dim3(64), 0, s, a);
