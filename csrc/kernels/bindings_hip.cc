@@ -55,7 +55,7 @@ void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t* src_y, con
                               int* intra_count, const int8_t* aq, const uint8_t* ref1_u, const uint8_t* ref1_v,
                               int bmode, int t8, const int16_t* mv8, void* stream, const int* w1, int nref,
                               const uint8_t* const* xref_u, const uint8_t* const* xref_v, const int8_t* mref,
-                              const int* wp);
+                              const int* wp, int trellis, float trellis_lambda);
 void mivc_launch_wp_stats(const uint8_t* y, const uint8_t* u, const uint8_t* v, int w, int h, int npics,
                           unsigned long long* out, void* stream);
 void mivc_launch_wp_src(const uint8_t* src, uint8_t* dst, const int* wt, int B, long long plane_bytes, void* stream);
@@ -263,7 +263,7 @@ PYBIND11_MODULE(_hip, m) {
            uintptr_t intra_cost, uintptr_t qp, int cqo, uintptr_t hdr, uintptr_t coef, uintptr_t nz,
            uintptr_t intra_flag, uintptr_t intra_count, uintptr_t stream, uintptr_t aq, uintptr_t ref1_u,
            uintptr_t ref1_v, int bmode, int t8, uintptr_t mv8, std::vector<int> w1, std::vector<uintptr_t> xref_u,
-           std::vector<uintptr_t> xref_v, uintptr_t mref, uintptr_t wp) {
+           std::vector<uintptr_t> xref_v, uintptr_t mref, uintptr_t wp, int trellis, float trellis_lambda) {
           // xref_u / xref_v: chroma of RefPicList0[1..]; w1: implicit list-1 weight per list-0 picture
           if (bmode && (!ref1_u || !ref1_v)) throw std::invalid_argument("encode_inter: B mode needs the list-1 chroma");
           const size_t n = xref_u.size() + 1;
@@ -283,14 +283,15 @@ PYBIND11_MODULE(_hip, m) {
                                    cqo, P<void>(hdr), P<int16_t>(coef), P<uint8_t>(nz), P<uint8_t>(intra_flag),
                                    P<int>(intra_count), P<int8_t>(aq), P<uint8_t>(ref1_u), P<uint8_t>(ref1_v), bmode,
                                    t8, P<int16_t>(mv8), S(stream), w.data(), static_cast<int>(n), xu, xv,
-                                   bmode ? nullptr : P<int8_t>(mref), P<int>(wp));
+                                   bmode ? nullptr : P<int8_t>(mref), P<int>(wp), trellis, trellis_lambda);
         }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("sy"), py::arg("su"), py::arg("sv"), py::arg("fy"),
         py::arg("fu"), py::arg("fv"), py::arg("ry"), py::arg("ru"), py::arg("rv"), py::arg("pred"), py::arg("mv"),
         py::arg("me_cost"), py::arg("intra_cost"), py::arg("qp"), py::arg("cqo"), py::arg("hdr"), py::arg("coef"),
         py::arg("nz"), py::arg("intra_flag"), py::arg("intra_count"), py::arg("stream"), py::arg("aq") = 0,
         py::arg("ref1_u") = 0, py::arg("ref1_v") = 0, py::arg("bmode") = 0, py::arg("t8") = 0, py::arg("mv8") = 0,
         py::arg("w1") = std::vector<int>{32}, py::arg("xref_u") = std::vector<uintptr_t>{},
-        py::arg("xref_v") = std::vector<uintptr_t>{}, py::arg("mref") = 0, py::arg("wp") = 0);
+        py::arg("xref_v") = std::vector<uintptr_t>{}, py::arg("mref") = 0, py::arg("wp") = 0, py::arg("trellis") = 0,
+        py::arg("trellis_lambda") = 1.0f);
   m.def("wp_stats", [](uintptr_t y, uintptr_t u, uintptr_t v, int w, int h, int npics, uintptr_t out, uintptr_t stream) {
     if (w % 2 || h % 2 || (w * h) % 4) throw std::invalid_argument("wp_stats: even picture sizes");
     mivc_launch_wp_stats(P<uint8_t>(y), P<uint8_t>(u), P<uint8_t>(v), w, h, npics, P<unsigned long long>(out),

@@ -50,7 +50,53 @@ struct InterArgs {
   // explicit weighted prediction of RefPicList0[0] in P pictures (nullable): [B, 8] = luma
   // weight, offset, log2 denominator, Cb weight, offset, Cr weight, offset, chroma denominator
   const int* wp;
+  // x264 --trellis 1 (its default: on the final encode of each MB): 4x4 luma levels by a
+  // rate-distortion choice instead of the dead-zone rounding (trellis_lite below); 0 = off
+  int trellis;
+  float trellis_lambda;    // multiplier of the SSD lambda 0.85 * 2^((QP - 12) / 3)
 };
+
+// Rate-distortion quantisation of one 4x4 block (x264 --trellis 1, simplified to a greedy pass
+// in reverse scan order): every coefficient chooses among 0 and the two levels around the
+// rounded quotient by SSD (pixel domain: the error of coefficient (i, j) weighs 1 / (n_i n_j),
+// n = 4, 10, 4, 10 the row norms of the core transform) + lambda * CABAC bits, with static bin
+// costs for significance / last (a coefficient above every non-zero one would become the last
+// one), greater-than-one and the unary level bins, and the sign.  Levels after the block's
+// last non-zero one are never coded, so trailing small coefficients are dropped first.
+__device__ __forceinline__ void trellis_lite4x4(const int (&w)[16], int (&lv)[16], const int (&mf)[3], int qbits,
+                                                float lam) {
+  constexpr float kInvNorm[3] = {1.0f / 16.0f, 1.0f / 100.0f, 1.0f / 40.0f};
+  constexpr float kSig0 = 0.55f, kSig1 = 1.35f, kLast0 = 0.25f, kLast1 = 2.2f, kGt1No = 0.6f, kGt1Yes = 1.7f;
+  bool seen = false;
+#pragma unroll
+  for (int i = 15; i >= 0; --i) {
+    const int r = h264::kZigzag4x4[i];
+    const int cls = h264::kPosClass[r];
+    const int a = w[r] < 0 ? -w[r] : w[r];
+    const float fm = static_cast<float>(mf[cls]);
+    const int zr = (a * mf[cls] + (1 << (qbits - 1))) >> qbits;  // |W| < 2^14, MF < 2^14
+    const float step = static_cast<float>(1 << qbits) / fm;
+    const float inv_n = kInvNorm[cls];
+    float best = static_cast<float>(a) * static_cast<float>(a) * inv_n + lam * (seen ? kSig0 : 0.0f);
+    int bl = 0;
+#pragma unroll
+    for (int d = 1; d >= 0; --d) {
+      const int l = zr - d;
+      if (l < 1) continue;
+      const float e = static_cast<float>(a) - static_cast<float>(l) * step;
+      const float bits = kSig1 + (seen ? kLast0 : kLast1) + 1.0f +
+                         (l == 1 ? kGt1No : kGt1Yes + 0.9f * static_cast<float>(min(l - 2, 13)) +
+                                                (l > 15 ? 2.0f * (31 - __clz(l - 14)) + 1.0f : 0.0f));
+      const float j = e * e * inv_n + lam * bits;
+      if (j < best) {
+        best = j;
+        bl = l;
+      }
+    }
+    lv[r] = w[r] < 0 ? -bl : bl;
+    seen |= bl != 0;
+  }
+}
 
 // clause 8.4.2.3.2 for one sample: ((p * w + 2^(d-1)) >> d) + o, clipped
 __device__ __forceinline__ int wp_sample(int p, int w, int o, int d) {
@@ -216,8 +262,12 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
     h264::forward_core4x4(res);
     {
       const int qbits = 15 + qp / 6;
+      if (a.trellis) {
+        trellis_lite4x4(res, lv, mf, qbits, a.trellis_lambda * 0.85f * exp2f((qp - 12) * (1.0f / 3.0f)));
+      } else {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) lv[r] = h264::quant_coef(res[r], mf[h264::kPosClass[r]], qbits, 11);
+        for (int r = 0; r < 16; ++r) lv[r] = h264::quant_coef(res[r], mf[h264::kPosClass[r]], qbits, 11);
+      }
       int scan[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) scan[i] = lv[h264::kZigzag4x4[i]];
@@ -571,8 +621,10 @@ extern "C" void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t*
                                          const int8_t* aq, const uint8_t* ref1_u, const uint8_t* ref1_v, int bmode,
                                          int t8, const int16_t* mv8, void* stream, const int* w1, int nref,
                                          const uint8_t* const* xref_u, const uint8_t* const* xref_v,
-                                         const int8_t* mref, const int* wp) {
+                                         const int8_t* mref, const int* wp, int trellis, float trellis_lambda) {
   InterArgs a;
+  a.trellis = trellis;
+  a.trellis_lambda = trellis_lambda;
   a.wp = bmode ? nullptr : wp;
   for (int r = 0; r < 4; ++r) {
     const int rr = r < nref ? r : 0;

@@ -105,6 +105,10 @@ class H264Params:
     # direct termination); 0 disables.  1080p RD sweep (profiles/r3_b_gate_rd.md): 2400 ->
     # -8.8 % BD-rate (PSNR-Y) and +7..20 % fps against no gate
     b_gate: int = int(os.environ.get("MIVC_B_GATE", 2400))
+    # x264 --trellis 1 (default): rate-distortion choice of the 4x4 luma levels of inter MBs
+    # (encode_inter.hip trellis_lite4x4); trellis_lambda scales its SSD lambda
+    trellis: int = int(os.environ.get("MIVC_TRELLIS", 1))
+    trellis_lambda: float = float(os.environ.get("MIVC_TRELLIS_LAMBDA", 1.0))
     # deblock non-reference B pictures even when neither metrics nor the reconstruction
     # are requested (x264 --full-recon); the bitstream does not depend on it
     full_recon: bool = False
@@ -508,7 +512,8 @@ class GpuH264Encoder:
                                       P(self.me_cost), P(self.intra_cost), P(self.qp), cqo, P(hdr), P(coef),
                                       P(self.nz), P(self.intra_flag), P(self.intra_count), s, aq,
                                       t8=int(self.p.eff_t8x8()), mv8=mv8, xref_u=xu, xref_v=xv,
-                                      mref=P(self.mref) if nr > 1 else 0, wp=wp)
+                                      mref=P(self.mref) if nr > 1 else 0, wp=wp, trellis=int(self.p.trellis),
+                                      trellis_lambda=float(self.p.trellis_lambda))
         elif pic.kind == "B":
             f0y, f0u, f0v = (P(x) for x in ref0)
             f1y, f1u, f1v = (P(x) for x in ref1)
@@ -560,7 +565,8 @@ class GpuH264Encoder:
                 self.hip.encode_inter(B, wmb, hmb, sy, su, sv, f0y, f0u, f0v, ry, ru, rv, P(self.pred_b), P(self.mv),
                                       P(self.cost_b), P(self.intra_cost), P(self.qp), cqo, P(hdr), P(coef),
                                       P(self.nz), P(self.intra_flag), P(self.intra_count), s, aq, f1u, f1v, 1,
-                                      int(self.p.eff_t8x8()), 0, w1s, xu, xv)
+                                      int(self.p.eff_t8x8()), 0, w1s, xu, xv, 0, 0, int(self.p.trellis),
+                                      float(self.p.trellis_lambda))
         if pic.kind != "I":
             self.p_intra_mbs += self.intra_count.sum()
             flag_ptr, count_ptr = P(self.intra_flag), P(self.intra_count)
