@@ -597,7 +597,19 @@ struct HevcBArgs {
   const int8_t* aq;
   int bslice;                   // 0: P picture (list 0 only)
   int max_merge;                // MaxNumMergeCand
+  int ctu_shift;                // log2(CTU size / 16): 1 for 32x32 CTBs, 2 for 64x64 CTUs
 };
+
+// z-scan availability (6.4.1) of the 16x16 block (nx, ny) for the block (mx, my) on the 16x16
+// grid: CTUs in raster order, blocks inside a CTU in z-order
+__device__ __forceinline__ bool avail16(const Geom& g, int sh, int nx, int ny, int mx, int my) {
+  if (nx < 0 || ny < 0 || nx >= g.wmb || ny >= g.hmb) return false;
+  const int ux = nx >> sh, uy = ny >> sh, cx = mx >> sh, cy = my >> sh;
+  if (ux != cx || uy != cy) return uy < cy || (uy == cy && ux < cx);
+  const int m = (1 << sh) - 1;
+  auto z = [](int x, int y) { return (x & 1) | ((y & 1) << 1) | ((x & 2) << 1) | ((y & 2) << 2); };
+  return z(nx & m, ny & m) < z(mx & m, my & m);
+}
 
 // luma prediction (4 samples of row Y, columns X..X+3) of a B motion
 __device__ __forceinline__ uint32_t mc4_b(const HevcBArgs& a, const uint8_t* G0, const uint8_t* H0, const uint8_t* G1,
@@ -717,7 +729,11 @@ __global__ __launch_bounds__(64) void hevc_b_merge(HevcBArgs a) {
   };
   int dA1 = 0, dB1 = 0, dB0 = 0, dA0 = 0, dB2 = 0, wA1[4], wB1[4], wB0[4], wA0[4], wB2[4];
   const bool a1 = mx > 0, av_b1 = my > 0;
-  bool b0 = my > 0 && mx + 1 < g.wmb && q != 3, a0 = q == 0 && mx > 0 && my + 1 < g.hmb, b2 = mx > 0 && my > 0;
+  // above-right / below-left: z-scan order inside the CTU (32x32: B0 unavailable for quadrant 3,
+  // A0 available for quadrant 0 only)
+  bool b0 = avail16(g, a.ctu_shift, mx + 1, my - 1, mx, my), a0 = avail16(g, a.ctu_shift, mx - 1, my + 1, mx, my);
+  bool b2 = mx > 0 && my > 0;
+  (void)q;
   if (a1) load(mb - 1, &dA1, wA1);
   if (av_b1) load(mb - g.wmb, &dB1, wB1);
   if (b0) load(mb - g.wmb + 1, &dB0, wB0);
@@ -1125,8 +1141,10 @@ extern "C" void mivc_launch_hevc_b(int mode, int B, int wmb, int hmb, const uint
                                    const int16_t* mv1, const int* cost0, const int* cost1, const int16_t* pm0,
                                    const int16_t* pm1, const int16_t* tmv, const uint8_t* tdir, const int16_t* mvb_in,
                                    const uint8_t* dir_in, int16_t* mvb_out, uint8_t* dir_out, int* cost, int* bits,
-                                   const int* qp, const int8_t* aq, void* stream, int bslice, int max_merge) {
+                                   const int* qp, const int8_t* aq, void* stream, int bslice, int max_merge,
+                                   int ctu64) {
   HevcBArgs a;
+  a.ctu_shift = ctu64 ? 2 : 1;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.src_y = src_y;
   a.ref0 = ref0;

@@ -96,7 +96,7 @@ void mivc_launch_hevc_b(int mode, int B, int wmb, int hmb, const uint8_t* src_y,
                         const uint8_t* hp0, const uint8_t* hp1, const int16_t* mv0, const int16_t* mv1, const int* cost0,
                         const int* cost1, const int16_t* pm0, const int16_t* pm1, const int16_t* tmv, const uint8_t* tdir,
                         const int16_t* mvb_in, const uint8_t* dir_in, int16_t* mvb_out, uint8_t* dir_out, int* cost,
-                        int* bits, const int* qp, const int8_t* aq, void* stream, int bslice, int max_merge);
+                        int* bits, const int* qp, const int8_t* aq, void* stream, int bslice, int max_merge, int ctu64);
 void mivc_launch_hevc_deblock(int B, int W, int H, int bd, uint16_t* y, uint16_t* u, uint16_t* v, const void* cu,
                               const void* ctu, const int8_t* run, void* stream);
 void mivc_launch_hevc_aq(int B, int W, int H, int bd, const uint16_t* sy, const uint16_t* su, const uint16_t* sv,
@@ -399,7 +399,7 @@ PYBIND11_MODULE(_hip, m) {
                      uintptr_t hp1, uintptr_t mv0, uintptr_t mv1, uintptr_t cost0, uintptr_t cost1, uintptr_t pm0,
                      uintptr_t pm1, uintptr_t tmv, uintptr_t tdir, uintptr_t mvb_in, uintptr_t dir_in, uintptr_t mvb_out,
                      uintptr_t dir_out, uintptr_t cost, uintptr_t bits, uintptr_t qp, uintptr_t aq, uintptr_t stream,
-                     int bslice, int max_merge) {
+                     int bslice, int max_merge, int ctu64) {
     // mode 0: L0 / L1 / bi choice from the two searches; 1: one merge-aware Jacobi pass;
     // 2: a P picture's list-0 search in the same motion form
     if (mode < 0 || mode > 2) throw std::invalid_argument("hevc_b: mode 0 (choose), 1 (merge pass) or 2 (P init)");
@@ -418,12 +418,12 @@ PYBIND11_MODULE(_hip, m) {
                        P<uint8_t>(hp1), P<int16_t>(mv0), P<int16_t>(mv1), P<int>(cost0), P<int>(cost1), P<int16_t>(pm0),
                        P<int16_t>(pm1), P<int16_t>(tmv), P<uint8_t>(tdir), P<int16_t>(mvb_in), P<uint8_t>(dir_in),
                        P<int16_t>(mvb_out), P<uint8_t>(dir_out), P<int>(cost), P<int>(bits), P<int>(qp), P<int8_t>(aq),
-                       S(stream), bslice, max_merge);
+                       S(stream), bslice, max_merge, ctu64);
   }, py::arg("mode"), py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("src"), py::arg("ref0"), py::arg("ref1"),
      py::arg("hp0"), py::arg("hp1"), py::arg("mv0"), py::arg("mv1"), py::arg("cost0"), py::arg("cost1"), py::arg("pm0"),
      py::arg("pm1"), py::arg("tmv"), py::arg("tdir"), py::arg("mvb_in"), py::arg("dir_in"), py::arg("mvb_out"),
      py::arg("dir_out"), py::arg("cost"), py::arg("bits"), py::arg("qp"), py::arg("aq"), py::arg("stream"),
-     py::arg("bslice") = 1, py::arg("max_merge") = 5);
+     py::arg("bslice") = 1, py::arg("max_merge") = 5, py::arg("ctu64") = 0);
   m.def("hevc_deblock", [](int B, int W, int H, int bd, uintptr_t y, uintptr_t u, uintptr_t v, uintptr_t cu,
                            uintptr_t ctu, uintptr_t run, uintptr_t stream) {
     mivc_launch_hevc_deblock(B, W, H, bd, P<uint16_t>(y), P<uint16_t>(u), P<uint16_t>(v), P<void>(cu), P<void>(ctu),

@@ -370,7 +370,7 @@ class GpuHevcEncoder:
 
     def _temporal_for(self, pic, cs: int, col: int, col_refs: tuple, targets: tuple):
         """TMVP merge candidate per 16x16 block (the writer's derivation for a 16x16 CU: the
-        collocated bottom-right block inside the CTB row, else the centre one; a list-1-only
+        collocated bottom-right block inside the CTU row, else the centre one; a list-1-only
         collocated block gives its list-1 vector, any other its list-0 vector
         (collocated_from_l0_flag 0)) scaled to both lists, and the two searches' predictors.
         cs / col: DPB slot and display index of the collocated picture, col_refs: its own list-0 /
@@ -385,7 +385,9 @@ class GpuHevcEncoder:
         br_ok[:, :-1, :-1] = ok[:, 1:, 1:]
         br_mv[:, :-1, :-1] = mv[:, 1:, 1:]
         br_1[:, :-1, :-1] = use1[:, 1:, 1:]
-        even = (torch.arange(self.hmb, device=self.dev) % 2 == 0)[None, :, None]
+        # the bottom-right block must lie in the same CTU row (16x16 rows per CTU: 2 or 4)
+        rows = 4 if self.p.ctu64 else 2
+        even = (torch.arange(self.hmb, device=self.dev) % rows != rows - 1)[None, :, None]
         use_br = br_ok & even
         sel = torch.where(use_br[..., None], br_mv, mv)
         sel1 = torch.where(use_br, br_1, use1)[..., None]
@@ -549,12 +551,12 @@ class GpuHevcEncoder:
                             pargs = (B, self.wmb, self.hmb, p(self.src8), p(ref8), p(ref8), p(hp), p(hp))
                             self.hip.hevc_b(2, *pargs, p(self.mv), 0, p(self.me_cost), 0, p(self.prev_mv), 0, 0, 0, 0, 0,
                                             p(self.mvb[0]), p(self.dirb[0]), p(self.bcost), p(self.bbits), p(self.qp),
-                                            p(self.mb_aq), s, 0, int(self.p.max_merge))
+                                            p(self.mb_aq), s, 0, int(self.p.max_merge), int(self.p.ctu64))
                             for it in range(int(self.p.merge_refine)):
                                 i_, o_ = it % 2, (it + 1) % 2
                                 self.hip.hevc_b(1, *pargs, 0, 0, 0, 0, 0, 0, tm_, td_, p(self.mvb[i_]), p(self.dirb[i_]),
                                                 p(self.mvb[o_]), p(self.dirb[o_]), p(self.bcost), p(self.bbits),
-                                                p(self.qp), p(self.mb_aq), s, 0, int(self.p.max_merge))
+                                                p(self.qp), p(self.mb_aq), s, 0, int(self.p.max_merge), int(self.p.ctu64))
                             fin = int(self.p.merge_refine) % 2
                             self.me_cost.copy_(self.bcost)
                             self.mv.copy_(self.mvb[fin][..., 0:2])
@@ -583,13 +585,13 @@ class GpuHevcEncoder:
                         bargs = (B, self.wmb, self.hmb, p(self.src8), p(ref8), p(ref8b), p(hp), p(hpb))
                         self.hip.hevc_b(0, *bargs, p(self.mv), p(self.mv1), p(self.me_cost), p(self.me_cost1),
                                         p(self.pm0), p(self.pm1), 0, 0, 0, 0, p(self.mvb[0]), p(self.dirb[0]),
-                                        p(self.bcost), p(self.bbits), p(self.qp), p(self.mb_aq), s, 1, int(self.p.max_merge))
+                                        p(self.bcost), p(self.bbits), p(self.qp), p(self.mb_aq), s, 1, int(self.p.max_merge), int(self.p.ctu64))
                         tm_, td_ = (p(self.tmv), p(self.tdir)) if tmvp else (0, 0)
                         for it in range(int(self.p.merge_refine)):
                             i_, o_ = it % 2, (it + 1) % 2
                             self.hip.hevc_b(1, *bargs, 0, 0, 0, 0, 0, 0, tm_, td_, p(self.mvb[i_]), p(self.dirb[i_]),
                                             p(self.mvb[o_]), p(self.dirb[o_]), p(self.bcost), p(self.bbits), p(self.qp),
-                                            p(self.mb_aq), s, 1, int(self.p.max_merge))
+                                            p(self.mb_aq), s, 1, int(self.p.max_merge), int(self.p.ctu64))
                         fin = int(self.p.merge_refine) % 2
                         self.me_cost.copy_(self.bcost)
                     r1p = self.rec[r1]
