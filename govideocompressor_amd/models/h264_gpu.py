@@ -45,7 +45,7 @@ class H264Params:
     i4x4: bool = True
     # x264 --partitions i8x8 (its default with --8x8dct): Intra8x8 MBs (High profile) tried where
     # Intra4x4 is (I pictures, scene cuts), closed loop with the 8x8 transform, sa8d ranking
-    i8x8: bool = True
+    i8x8: bool = bool(int(os.environ.get("MIVC_I8X8", "1")))
     # Intra4x4 trial for the (rare) intra MBs of P frames.  Off by default: a P-frame
     # intra MB is coded by the wavefront kernel, whose latency (x chain length) is
     # dominated by the 16 serial I4x4 block trials; these MBs are ~0.1-1% of a P frame.
@@ -90,7 +90,7 @@ class H264Params:
     partitions: bool = True
     # x264 --partitions b8x8: B macroblocks split into quadrants that pick their own candidate
     # (direct, L0, L1, bi of the MB's two searched vectors): B_16x8 / B_8x16 / B_8x8
-    bpartitions: bool = True
+    bpartitions: bool = bool(int(os.environ.get("MIVC_BPARTS", "1")))
     # (1080p CRF23 sweep, profiles/r2_partition_sweep.txt: 8 / 2000 -> -0.5% bits at equal
     # PSNR for ~1% of the step time; a threshold of 0 searches every MB for the same bits)
     part_overhead: int = int(os.environ.get("MIVC_PART_OVERHEAD", 8))
