@@ -459,16 +459,23 @@ def track_fps(t: Track) -> float:
 
 # ------------------------------------------------------------------------------- audio
 def cut(t: Track, t0: float, t1: float | None) -> Track:
-    """Samples of ``t`` whose presentation time lies in [t0, t1) seconds."""
+    """Samples of ``t`` whose presentation time lies in [t0, t1) seconds.
+
+    The first piece (t0 = 0) also keeps the samples before time 0 -- the encoder-delay
+    (priming) frames an AAC track's edit list hides -- together with the track's
+    ``media_time``, so the piece, and the merge that starts with it, play the same samples
+    from the same instant as the input."""
     pts = t.pts_seconds()
-    keep = [i for i, x in enumerate(pts) if x >= t0 - 1e-9 and (t1 is None or x < t1 - 1e-9)]
+    first = t0 <= 1e-9
+    keep = [i for i, x in enumerate(pts) if (first or x >= t0 - 1e-9) and (t1 is None or x < t1 - 1e-9)]
     return Track(t.handler, t.timescale, t.sample_entry, [t.samples[i] for i in keep], [t.durations[i] for i in keep],
                  [t.cts[i] for i in keep] if t.cts else None, [t.sync[i] for i in keep] if t.sync else None,
-                 t.width, t.height, 0, t.language)
+                 t.width, t.height, t.media_time if first else 0, t.language)
 
 
 def concat(parts: list[Track]) -> Track:
-    """Tracks appended in order (a merge's audio); every part needs the same sample entry."""
+    """Tracks appended in order (a merge's audio); every part needs the same sample entry.
+    The first part's edit (its priming samples' ``media_time``) is the result's."""
     parts = [p for p in parts if p.samples]
     if not parts:
         raise ValueError("mp4: no samples to concatenate")
@@ -476,8 +483,8 @@ def concat(parts: list[Track]) -> Track:
     for p in parts[1:]:
         if p.sample_entry != first.sample_entry or p.timescale != first.timescale:
             raise ValueError("mp4: pieces carry different audio formats; cannot stream-copy them into one track")
-    out = Track(first.handler, first.timescale, first.sample_entry, [], [], None, None, first.width, first.height, 0,
-                first.language)
+    out = Track(first.handler, first.timescale, first.sample_entry, [], [], None, None, first.width, first.height,
+                first.media_time, first.language)
     any_cts = any(p.cts for p in parts)
     any_sync = any(p.sync is not None for p in parts)
     cts, sync = [], []

@@ -66,6 +66,22 @@ def test_cut_and_concat_audio():
         mp4.concat([a, other])
 
 
+def test_audio_priming_edit_survives_cut_and_concat():
+    """An AAC track whose edit list hides one priming frame (media_time 1024): the first piece
+    keeps the priming frame and the edit, later pieces start at their own time, and the
+    concatenation plays exactly the input's samples with the input's edit."""
+    a = _audio_track(1.5, seed=11)
+    a.media_time = 1024
+    assert a.pts_seconds()[0] < 0
+    parts = [mp4.cut(a, 0.0, 0.5), mp4.cut(a, 0.5, 1.0), mp4.cut(a, 1.0, None)]
+    assert parts[0].media_time == 1024 and parts[0].samples[0] == a.samples[0]
+    assert parts[1].media_time == 0 and parts[2].media_time == 0
+    back = mp4.concat(parts)
+    assert back.samples == a.samples and back.media_time == 1024
+    rt = mp4.read(mp4.write([back]))[0]
+    assert rt.media_time == 1024 and rt.samples == a.samples
+
+
 def test_split_worker_merge_keeps_audio(tmp_path, host):
     """server s (mp4 with audio) -> every piece carries its audio span -> worker transcode
     with -acodec copy -> merge: the output audio == the input audio, sample for sample."""
@@ -74,6 +90,7 @@ def test_split_worker_merge_keeps_audio(tmp_path, host):
     from govideocompressor_amd.segment.split import split
     es, clip = _h264_stream(host, frames=36, keyint=12)
     a = _audio_track(36 / 30.0 + 0.05, seed=9)
+    a.media_time = 1024  # AAC encoder delay hidden by the edit list: kept through split and merge
     src = tmp_path / "movie.mp4"
     src.write_bytes(mp4.write([a, mp4.h264_track(es, 30.0)]))
     d, n = split(str(src), frames=12, out_root=str(tmp_path), log=lambda *_: None)
@@ -92,6 +109,7 @@ def test_split_worker_merge_keeps_audio(tmp_path, host):
     tr = mp4.read(out.read_bytes())
     aud = mp4.audio_tracks(tr)
     assert len(aud) == 1 and aud[0].samples == a.samples and aud[0].sample_entry == a.sample_entry
+    assert aud[0].media_time == 1024
     pics = host.decode(mp4.annexb_from_mp4(out.read_bytes()))
     assert len(pics) == 36
     # -an drops it
