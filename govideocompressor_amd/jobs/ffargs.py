@@ -187,8 +187,14 @@ H264_PARAMS = {
     "deblock": ("deblock", _deblock),
     "no-deblock": ("deblock", lambda v: not _flag(v)),
     "partitions": ("partitions", _partitions),
-    "ref": ("@ref", _int_in(1, 1)),
-    "weightp": ("@weightp", _only("0")),
+    "ref": ("refs", _int_in(1, 4)),
+    "weightp": ("weightp", lambda v: _int_in(0, 2)(v) > 0),
+    "weightb": ("weightb", _flag),
+    "no-weightb": ("weightb", lambda v: not _flag(v)),
+    "trellis": ("trellis", lambda v: int(_int_in(0, 2)(v) > 0)),
+    "direct": ("@direct", _only("temporal")),
+    "b-adapt": ("@b-adapt", _only("0")),
+    "b-pyramid": ("@b-pyramid", _only("none")),
     "crf": ("@crf", _float_in(0.0, 51.0)),
     "qp": ("@qp", _int_in(0, 51)),
     "threads": ("@threads", int),
@@ -217,7 +223,7 @@ HEVC_PARAMS = {
     "merange": ("me_range", _int_in(4, 16)),
     "deblock": ("deblock", _deblock),
     "no-deblock": ("deblock", lambda v: not _flag(v)),
-    "ctu": ("@ctu", _only("32")),
+    "ctu": ("ctu64", lambda v: {"32": False, "64": True}[v] if v in ("32", "64") else _only("32 or 64")(v)),
     "ref": ("@ref", _int_in(1, 1)),
     "crf": ("@crf", _float_in(0.0, 51.0)),
     "qp": ("@qp", _int_in(0, 51)),

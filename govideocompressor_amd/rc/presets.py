@@ -8,20 +8,24 @@ search and analysis parameters; each preset maps onto the x264 preset's intent:
 preset      H.264 knobs (x264 equivalent)
 ==========  ========================================================================
 ultrafast   CAVLC, no B, no deblock, no AQ/MB-tree/lookahead, integer-pel ME radius 4,
-            Intra16x16 only (x264: --no-cabac --bframes 0 --no-deblock --aq-mode 0
-            --subme 0 --me dia --partitions none --rc-lookahead 0)
-superfast   CABAC + 3 B, half-pel, radius 4, no MB-tree (--subme 1 --me dia --no-mbtree)
-veryfast    half-pel, radius 8 (--subme 2)
-faster      quarter-pel, radius 8, one skip-refine pass (--subme 4)
-fast        quarter-pel, radius 8 (--subme 6)
-medium      defaults (x264 defaults, the reference's "264" preset)
-slow        radius 12, B radius 6, Intra4x4 in P pictures (--me umh --subme 8)
-slower      radius 16, B radius 8, lookahead radius 8 (--subme 9 --me umh)
-veryslow    slower + three skip-refine passes (--subme 10 --me umh --merange 24)
+            Intra16x16 only, 1 reference (x264: --no-cabac --bframes 0 --no-deblock
+            --aq-mode 0 --subme 0 --me dia --partitions none --rc-lookahead 0 --ref 1
+            --weightp 0 --trellis 0)
+superfast   CABAC + 3 B, half-pel, radius 4, no MB-tree, no P/B partitions, 1 reference, no
+            trellis (--subme 1 --me dia --no-mbtree --partitions i8x8,i4x4 --ref 1)
+veryfast    half-pel, radius 8, 1 reference, no trellis (--subme 2 --ref 1 --trellis 0)
+faster      quarter-pel, radius 8, one skip-refine pass, 2 references (--subme 4 --ref 2)
+fast        quarter-pel, radius 8, 2 references (--subme 6 --ref 2)
+medium      defaults (x264 defaults, the reference's "264" preset: --ref 3, weightp, trellis 1)
+slow        radius 12, B radius 6, Intra4x4 in P pictures, 4 references (--me umh --subme 8
+            --ref 5)
+slower      radius 16, B radius 8, lookahead radius 8, 4 references (--subme 9 --me umh --ref 8)
+veryslow    slower + three skip-refine passes (--subme 10 --me umh --merange 24 --ref 16)
 placebo     = veryslow
 ==========  ========================================================================
 
-HEVC (x265): ultrafast..veryfast use radius 4 / half-pel, fast and medium the defaults (3
+HEVC (x265): ultrafast..veryfast use radius 4 / half-pel (ultrafast and superfast with 32x32
+CTUs, as x265), fast and medium the defaults (3
 merge candidates, as x265), slow and slower radius 12 (slower 4 candidates), veryslow/placebo
 radius 16 and 5 candidates;
 slow and slower presets add the inter residual quadtree (--tu-inter-depth 1), veryslow and
@@ -35,21 +39,22 @@ NAMES = ("ultrafast", "superfast", "veryfast", "faster", "fast", "medium", "slow
 
 H264 = {
     "ultrafast": dict(cabac=False, bframes=0, deblock=False, aq_strength=0.0, mbtree=False, lookahead=False,
-                      scenecut=0, subpel=0, me_range=4, i4x4=False, skip_refine=0),
-    "superfast": dict(subpel=1, me_range=4, mbtree=False, skip_refine=0, b_me_range=2),
-    "veryfast": dict(subpel=1, me_range=8, skip_refine=1),
-    "faster": dict(subpel=2, me_range=8, skip_refine=1),
-    "fast": dict(subpel=2, me_range=8),
+                      scenecut=0, subpel=0, me_range=4, i4x4=False, skip_refine=0, refs=1, weightp=False, trellis=0),
+    "superfast": dict(subpel=1, me_range=4, mbtree=False, skip_refine=0, b_me_range=2, refs=1, trellis=0,
+                      partitions=False, bpartitions=False),
+    "veryfast": dict(subpel=1, me_range=8, skip_refine=1, refs=1, trellis=0),
+    "faster": dict(subpel=2, me_range=8, skip_refine=1, refs=2),
+    "fast": dict(subpel=2, me_range=8, refs=2),
     "medium": dict(),
-    "slow": dict(me_range=12, b_me_range=6, i4x4_in_p=True),
-    "slower": dict(me_range=16, b_me_range=8, i4x4_in_p=True, la_range=8),
-    "veryslow": dict(me_range=16, b_me_range=8, i4x4_in_p=True, la_range=8, skip_refine=3),
+    "slow": dict(me_range=12, b_me_range=6, i4x4_in_p=True, refs=4),
+    "slower": dict(me_range=16, b_me_range=8, i4x4_in_p=True, la_range=8, refs=4),
+    "veryslow": dict(me_range=16, b_me_range=8, i4x4_in_p=True, la_range=8, skip_refine=3, refs=4),
 }
 H264["placebo"] = H264["veryslow"]
 
 HEVC = {
-    "ultrafast": dict(me_range=4, subpel=1, max_merge=3, la_range=4),
-    "superfast": dict(me_range=4, subpel=1, max_merge=3, la_range=4),
+    "ultrafast": dict(me_range=4, subpel=1, max_merge=3, la_range=4, ctu64=False),
+    "superfast": dict(me_range=4, subpel=1, max_merge=3, la_range=4, ctu64=False),
     "veryfast": dict(me_range=4, subpel=2, max_merge=3),
     "faster": dict(me_range=8, max_merge=3),
     "fast": dict(me_range=8),

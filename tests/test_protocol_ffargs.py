@@ -168,7 +168,8 @@ def test_ffargs_strict_rejections():
     """Options the native encoders cannot honour are errors, never silently dropped."""
     for bad in ("-vcodec libx264 -tune film", "-vcodec libx264 -tune ssim", "-vcodec libx264 -profile:v high10",
                 "-vcodec libx264 -profile:v high444", "-vcodec libx265 -profile:v main12",
-                "-vcodec libx264 -x264-params ref=3", "-vcodec libx264 -x264-params weightp=2",
+                "-vcodec libx264 -x264-params ref=5", "-vcodec libx264 -x264-params direct=spatial",
+                "-vcodec libx264 -x264-params b-adapt=2", "-vcodec libx264 -x264-params b-pyramid=normal",
                 "-vcodec libx264 -x264-params foo=1", "-vcodec libx264 -x265-params sao=0",
                 "-vcodec libx265 -x265-params bframes=9", "-vcodec libx265 -x265-params ctu=16",
                 "-vcodec libx264 -x264-params aq-mode=2", "-vcodec libx264 -x264-params deblock=1,1",
@@ -176,3 +177,22 @@ def test_ffargs_strict_rejections():
                 "-vcodec libx265 -profile:v main -pix_fmt yuv420p10le", "-vcodec copy -tune psnr"):
         with pytest.raises(ffargs.FfArgsError):
             ffargs.parse(bad)
+
+
+def test_ffargs_reference_and_weighting_knobs():
+    """-x264-params ref / weightp / weightb / trellis and -x265-params ctu reach the encoders;
+    the speed presets carry x264's / x265's values for them."""
+    from govideocompressor_amd.models.h264_gpu import H264Params
+    from govideocompressor_amd.models.hevc_gpu import HevcParams
+    from govideocompressor_amd.rc import presets
+    p = ffargs.parse("-vcodec libx264 -x264-params ref=1:weightp=0:trellis=0:no-weightb=1").apply_opts(H264Params(64, 64))
+    assert (p.refs, p.weightp, p.trellis, p.weightb) == (1, False, 0, False)
+    p = ffargs.parse("-vcodec libx264 -x264-params ref=4:weightp=2:trellis=2:direct=temporal").apply_opts(H264Params(64, 64))
+    assert (p.refs, p.weightp, p.trellis, p.eff_refs()) == (4, True, 1, 4)
+    assert H264Params(64, 64, cabac=False, refs=3).eff_refs() == 1     # Constrained Baseline: one reference
+    assert presets.apply(H264Params(64, 64), "ultrafast").refs == 1
+    assert presets.apply(H264Params(64, 64), "fast").refs == 2
+    assert presets.apply(H264Params(64, 64), "slow").refs == 4
+    p = ffargs.parse("-vcodec libx265 -x265-params ctu=32").apply_opts(HevcParams(64, 64))
+    assert p.ctu64 is False and HevcParams(64, 64).ctu64 is True
+    assert presets.apply(HevcParams(64, 64), "ultrafast").ctu64 is False
