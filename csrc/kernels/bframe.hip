@@ -387,6 +387,162 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- spatial direct (x264 --direct spatial)
+// 8.4.1.2.2: the direct motion of a macroblock follows its neighbours A (left), B (above) and
+// C (above-right, else D above-left) in the *current* picture: refIdxLX = MinPositive over
+// them, the 16x16 motion-vector predictor of that reference, zeroed per 8x8 quadrant where the
+// co-located block of RefPicList1[0] is static (colZeroFlag).  Neighbours' final motion exists
+// only in decoding order, so b_decide chooses the modes with the temporal-direct estimate and
+// b_spatial_fix then derives the exact motion of every direct MB / B_Direct_8x8 quadrant in an
+// MB wavefront (one wave per MB row chain, the row above two MBs ahead), marking them for
+// b_direct_pred, which rebuilds their luma prediction (fully parallel).
+struct BSpatialArgs {
+  Geom g;
+  MbHeader* hdr;         // [B, nmb] current picture (in / out)
+  const MbHeader* col;   // [B, nmb] RefPicList1[0]'s records
+  uint8_t* dirty;        // [B, nmb] out: quadrants whose direct motion was (re)derived
+  int* err;
+  // encode_inter turns an MB intra when intra_cost < cost (the decision it reads): such MBs are
+  // intra neighbours here and are not derived
+  const int* intra_cost;
+  const int* cost;
+};
+
+struct NbMv16 {
+  bool avail;
+  int ref;
+  int mv[2];
+};
+
+__device__ __forceinline__ NbMv16 nb16(const MbHeader* h, bool avail, bool intra, int l, int q) {
+  NbMv16 n{avail, -1, {0, 0}};
+  if (!avail || intra || h264::mbk_is_intra(h->kind)) return n;
+  n.ref = h->ref[l][q];
+  if (n.ref >= 0) {
+    n.mv[0] = h->mv[l][q][0];
+    n.mv[1] = h->mv[l][q][1];
+  }
+  return n;
+}
+
+__device__ __forceinline__ int med3i(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
+
+constexpr int kSpatialWaves = 4;
+
+__global__ __launch_bounds__(64 * kSpatialWaves) void b_spatial_fix(BSpatialArgs a) {
+  const Geom& g = a.g;
+  const int slot = blockIdx.x, nmb = g.nmb();
+  __shared__ int prog[kMaxRows];
+  for (int i = threadIdx.x; i < g.hmb; i += blockDim.x) prog[i] = 0;
+  __syncthreads();
+  const int w = wave_id(), lane = lane_id();
+  MbHeader* H = a.hdr + static_cast<size_t>(slot) * nmb;
+  const MbHeader* C0 = a.col + static_cast<size_t>(slot) * nmb;
+  uint8_t* D = a.dirty + static_cast<size_t>(slot) * nmb;
+  const int* IC = a.intra_cost + static_cast<size_t>(slot) * nmb;
+  const int* CB = a.cost + static_cast<size_t>(slot) * nmb;
+  auto is_intra = [&](int m) { return IC[m] < CB[m]; };
+  for (int y = w; y < g.hmb; y += kSpatialWaves) {
+    for (int x = 0; x < g.wmb; ++x) {
+      if (y > 0) row_wait(prog, y - 1, min(x + 2, g.wmb), a.err);
+      const int mb = y * g.wmb + x;
+      if (lane == 0) {
+        MbHeader& h = H[mb];
+        const int need = is_intra(mb) ? 0
+                                      : (h.kind == h264::MBK_BDIRECT ? 15 : (h.kind == h264::MBK_B8x8 ? (h.sub_direct & 15) : 0));
+        D[mb] = static_cast<uint8_t>(need);
+        if (need) {
+          const bool aA = x > 0, aB = y > 0, aC = y > 0 && x + 1 < g.wmb, aD = x > 0 && y > 0;
+          int refs[2], pmv[2][2] = {{0, 0}, {0, 0}};
+          for (int l = 0; l < 2; ++l) {
+            NbMv16 A = nb16(&H[mb - 1], aA, aA && is_intra(mb - 1), l, 1);
+            NbMv16 B = nb16(&H[mb - g.wmb], aB, aB && is_intra(mb - g.wmb), l, 2);
+            NbMv16 C = aC ? nb16(&H[mb - g.wmb + 1], true, is_intra(mb - g.wmb + 1), l, 2)
+                          : nb16(&H[mb - g.wmb - 1], aD, aD && is_intra(mb - g.wmb - 1), l, 3);
+            auto minpos = [](int p, int q) { return (p >= 0 && q >= 0) ? min(p, q) : max(p, q); };
+            refs[l] = minpos(A.ref, minpos(B.ref, C.ref));
+            if (refs[l] < 0) continue;
+            if (!B.avail && !C.avail && A.avail) {
+              B = A;
+              C = A;
+            }
+            const int r = refs[l];
+            const int match = (A.ref == r) + (B.ref == r) + (C.ref == r);
+            if (match == 1) {
+              const NbMv16& m = A.ref == r ? A : (B.ref == r ? B : C);
+              pmv[l][0] = m.mv[0];
+              pmv[l][1] = m.mv[1];
+            } else {
+              pmv[l][0] = med3i(A.mv[0], B.mv[0], C.mv[0]);
+              pmv[l][1] = med3i(A.mv[1], B.mv[1], C.mv[1]);
+            }
+          }
+          const bool zero = refs[0] < 0 && refs[1] < 0;
+          const MbHeader& c = C0[mb];
+          const bool cintra = h264::mbk_is_intra(c.kind);
+          for (int q = 0; q < 4; ++q) {
+            if (!((need >> q) & 1)) continue;
+            const bool col_zero = !cintra && c.ref[0][q] == 0 && abs(c.mv[0][q][0]) <= 1 && abs(c.mv[0][q][1]) <= 1;
+            for (int l = 0; l < 2; ++l) {
+              int r = refs[l], mx = pmv[l][0], my = pmv[l][1];
+              if (zero) {
+                r = 0;
+                mx = my = 0;
+              } else if (r < 0) {
+                mx = my = 0;
+              } else if (r == 0 && col_zero) {
+                mx = my = 0;
+              }
+              h.ref[l][q] = static_cast<int8_t>(r);
+              h.mv[l][q][0] = static_cast<int16_t>(mx);
+              h.mv[l][q][1] = static_cast<int16_t>(my);
+            }
+          }
+        }
+      }
+      row_publish(prog, y, x + 1);
+    }
+  }
+}
+
+// luma prediction of the quadrants b_spatial_fix re-derived (one wave per MB, lane = row
+// lane >> 2, columns 4 * (lane & 3) .. +3): list-0 picture ref0k[refIdxL0], list 1 = ref1,
+// bi-prediction with the implicit weight of the pair
+struct BDirectPredArgs {
+  Geom g;
+  const MbHeader* hdr;
+  const uint8_t* dirty;
+  const uint8_t *ref1, *hp1;
+  const uint8_t* ref0k[kMaxRefs];
+  const uint8_t* hp0k[kMaxRefs];
+  int w1[kMaxRefs];
+  uint8_t* pred_out;
+};
+
+__global__ __launch_bounds__(64) void b_direct_pred(BDirectPredArgs a) {
+  const Geom& g = a.g;
+  const int nmb = g.nmb();
+  int mb, slot;
+  xcd_unit_slot(mb, slot);
+  const size_t o = static_cast<size_t>(slot) * nmb + mb;
+  const int dm = a.dirty[o];
+  if (!dm) return;
+  const int lane = threadIdx.x, r = lane >> 2, c0 = (lane & 3) * 4;
+  const int q = (r >> 3) * 2 + (c0 >> 3);
+  if (!((dm >> q) & 1)) return;
+  const int mx = mb % g.wmb, my = mb / g.wmb, W = g.W, H = g.H;
+  const int X = mx * 16 + c0, Y = my * 16 + r;
+  const size_t yo = static_cast<size_t>(slot) * g.ysize();
+  const size_t ho = static_cast<size_t>(slot) * 3 * (W + 2 * kHpMargin) * (H + 2 * kHpMargin);
+  const MbHeader& h = a.hdr[o];
+  const int r0 = h.ref[0][q], r1 = h.ref[1][q];
+  uint32_t p0 = 0, p1 = 0;
+  if (r0 >= 0) p0 = mc4(a.ref0k[r0 & 3] + yo, a.hp0k[r0 & 3] + ho, W, H, X, Y, h.mv[0][q][0], h.mv[0][q][1]);
+  if (r1 >= 0) p1 = mc4(a.ref1 + yo, a.hp1 + ho, W, H, X, Y, h.mv[1][q][0], h.mv[1][q][1]);
+  const uint32_t pw = (r0 >= 0 && r1 >= 0) ? wavg4b(p0, p1, a.w1[r0 & 3]) : (r0 >= 0 ? p0 : p1);
+  *reinterpret_cast<uint32_t*>(a.pred_out + o * 256 + r * 16 + c0) = pw;
+}
+
 // ---------------------------------------------------------------- P_Skip-aware vector choice
 // ME prices vectors against a temporal predictor, so on noisy content neighbouring MBs of
 // one uniform motion pick slightly different quarter-sample vectors and none of them can
@@ -1173,4 +1329,28 @@ extern "C" void mivc_launch_hevc_b(int mode, int B, int wmb, int hmb, const uint
   if (mode == 0) hipLaunchKernelGGL(hevc_b_choose, dim3(wmb * hmb, B), dim3(64), 0, st, a);
   else if (mode == 1) hipLaunchKernelGGL(hevc_b_merge, dim3(wmb * hmb, B), dim3(64), 0, st, a);
   else hipLaunchKernelGGL(hevc_b_init_p, dim3((wmb * hmb + 255) / 256, B), dim3(256), 0, st, a);
+}
+
+extern "C" void mivc_launch_b_spatial(int B, int wmb, int hmb, void* hdr, const void* col, uint8_t* dirty,
+                                      const uint8_t* ref1, const uint8_t* hp1, const uint8_t* const* ref0k,
+                                      const uint8_t* const* hp0k, const int* w1, int nref, uint8_t* pred_out, int* err,
+                                      void* stream, const int* intra_cost, const int* cost) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  BSpatialArgs a{Geom{B, wmb, hmb, wmb * 16, hmb * 16}, static_cast<MbHeader*>(hdr), static_cast<const MbHeader*>(col),
+                 dirty, err, intra_cost, cost};
+  hipLaunchKernelGGL(b_spatial_fix, dim3(B), dim3(64 * kSpatialWaves), 0, s, a);
+  BDirectPredArgs p;
+  p.g = a.g;
+  p.hdr = static_cast<const MbHeader*>(hdr);
+  p.dirty = dirty;
+  p.ref1 = ref1;
+  p.hp1 = hp1;
+  for (int r = 0; r < kMaxRefs; ++r) {
+    const int rr = r < nref ? r : nref - 1;
+    p.ref0k[r] = ref0k[rr];
+    p.hp0k[r] = hp0k[rr];
+    p.w1[r] = w1[rr];
+  }
+  p.pred_out = pred_out;
+  hipLaunchKernelGGL(b_direct_pred, dim3(wmb * hmb, B), dim3(64), 0, s, p);
 }

@@ -28,6 +28,9 @@ void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t
 void mivc_launch_me_ref_select(int B, int wmb, int hmb, int nref, int16_t* mv, int16_t* mv8, int* cost, uint8_t* pred,
                                const int16_t* xmv, const int* xcost, const uint8_t* xpred, int8_t* mref, const int* qp,
                                const int8_t* aq, void* stream);
+void mivc_launch_b_spatial(int B, int wmb, int hmb, void* hdr, const void* col, uint8_t* dirty, const uint8_t* ref1,
+                           const uint8_t* hp1, const uint8_t* const* ref0k, const uint8_t* const* hp0k, const int* w1,
+                           int nref, uint8_t* pred_out, int* err, void* stream, const int* intra_cost, const int* cost);
 void mivc_launch_b_direct(int B, int wmb, int hmb, const void* col, const int* dsf, const int* direct_copy, int nref,
                           int16_t* dmv, int8_t* dref, int16_t* pm0, int16_t* pm1, void* stream);
 void mivc_launch_p_refine(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref, const uint8_t* hp,
@@ -191,6 +194,25 @@ PYBIND11_MODULE(_hip, m) {
     mivc_launch_me_ref_select(B, wmb, hmb, nref, P<int16_t>(mv), P<int16_t>(mv8), P<int>(cost), P<uint8_t>(pred),
                               P<int16_t>(xmv), P<int>(xcost), P<uint8_t>(xpred), P<int8_t>(mref), P<int>(qp),
                               P<int8_t>(aq), S(stream));
+  });
+  m.def("b_spatial", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t col, uintptr_t dirty, uintptr_t ref1,
+                        uintptr_t hp1, std::vector<uintptr_t> ref0k, std::vector<uintptr_t> hp0k, std::vector<int> w1,
+                        uintptr_t pred_out, uintptr_t err, uintptr_t stream, uintptr_t intra_cost, uintptr_t cost) {
+    // spatial direct: exact derivation in MB wavefront order + the luma prediction of the
+    // re-derived quadrants; ref0k / hp0k / w1: every list-0 picture (entry 0 = RefPicList0[0])
+    const size_t n = ref0k.size();
+    if (n < 1 || n > 4 || hp0k.size() != n || w1.size() != n)
+      throw std::invalid_argument("b_spatial: 1..4 list-0 pictures with planes and weights");
+    if (hmb > 272) throw std::invalid_argument("b_spatial: at most 272 MB rows");
+    const uint8_t* rk[4];
+    const uint8_t* hk[4];
+    for (size_t i = 0; i < n; ++i) {
+      rk[i] = P<uint8_t>(ref0k[i]);
+      hk[i] = P<uint8_t>(hp0k[i]);
+    }
+    mivc_launch_b_spatial(B, wmb, hmb, P<void>(hdr), P<void>(col), P<uint8_t>(dirty), P<uint8_t>(ref1), P<uint8_t>(hp1),
+                          rk, hk, w1.data(), static_cast<int>(n), P<uint8_t>(pred_out), P<int>(err), S(stream),
+                          P<int>(intra_cost), P<int>(cost));
   });
   m.def("b_direct", [](int B, int wmb, int hmb, uintptr_t col, std::vector<int> dsf, std::vector<int> direct_copy,
                        uintptr_t dmv, uintptr_t pm0, uintptr_t pm1, uintptr_t stream, uintptr_t dref) {

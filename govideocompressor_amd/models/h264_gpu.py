@@ -108,6 +108,14 @@ class H264Params:
     # x264 --trellis 1 (default): rate-distortion choice of the 4x4 luma levels of inter MBs
     # (encode_inter.hip trellis_lite4x4); trellis_lambda scales its SSD lambda
     trellis: int = int(os.environ.get("MIVC_TRELLIS", 1))
+    # x264 --direct: "temporal" (co-located motion scaled by POC distances: every MB decides in
+    # parallel) or "spatial" (the neighbours' motion: b_decide chooses with the temporal
+    # estimate, then bframe.hip b_spatial_fix derives the exact spatial motion of the direct
+    # MBs in an MB wavefront and b_direct_pred rebuilds their prediction).  Spatial is bit-exact
+    # but its modes are chosen on the temporal estimate, so direct MBs chained off zero-motion
+    # neighbours lose: +190 % BD-rate on the benchmark content (profiles/r3_direct_rd.md) until
+    # the decision itself runs in the wavefront
+    direct: str = os.environ.get("MIVC_DIRECT", "temporal")
     trellis_lambda: float = float(os.environ.get("MIVC_TRELLIS_LAMBDA", 1.0))
     # deblock non-reference B pictures even when neither metrics nor the reconstruction
     # are requested (x264 --full-recon); the bitstream does not depend on it
@@ -160,7 +168,7 @@ class H264Params:
         return (("High CABAC 8x8dct" if self.eff_t8x8() else "Main CABAC") + (" i8x8" if self.eff_t8x8() and self.i8x8 else "")
                 + (" p8x8" if self.eff_partitions() else "") + (" b8x8" if self.eff_partitions() and self.bpartitions and self.eff_bframes() else "") + (f" ref{self.eff_refs()}" if self.eff_refs() > 1 else "")
                 + (" weightp" if self.eff_weightp() else "")
-                + (f" {nb}B temporal-direct" if nb else "") + (" weightb" if nb and self.weightb else ""))
+                + (f" {nb}B {self.direct}-direct" if nb else "") + (" weightb" if nb and self.weightb else ""))
 
     def frame_qps(self) -> tuple[int, int]:
         """(qp_I, qp_P).  CRF maps to the P-frame QP (x264 scale without MB-tree);
@@ -233,6 +241,8 @@ class GpuH264Encoder:
         shared by the steps of a group)."""
         if params.width % 2 or params.height % 2:
             raise ValueError("width and height must be even")
+        if params.direct not in ("temporal", "spatial"):
+            raise ValueError("direct must be 'temporal' or 'spatial'")
         if entropy not in ("gpu", "cpu"):
             raise ValueError("entropy must be 'gpu' or 'cpu'")
         self.entropy = entropy
@@ -295,6 +305,7 @@ class GpuH264Encoder:
             self.pm1 = torch.zeros((B, nmb, 2), dtype=i16, device=dev)
             self.dmv = torch.zeros((B, nmb, 16), dtype=i16, device=dev)
             self.col_hdr = torch.zeros((B, nmb, MB_HDR_BYTES), dtype=u8, device=dev)
+            self.sp_dirty = torch.zeros((B, nmb), dtype=u8, device=dev)  # spatial direct: re-derived quadrants
         if params.eff_weightp():
             self.src_me = torch.zeros((B, H, W), dtype=u8, device=dev)  # inverse-weighted luma for ME
         self.intra_flag = torch.zeros((B, nmb), dtype=u8, device=dev)
@@ -561,6 +572,11 @@ class GpuH264Encoder:
                                   int(bg != 0))
             if cut is not None:
                 self.intra_cost.masked_fill_(cut[:, None], -1)
+            if self.p.direct == "spatial":
+                with st("b_spatial"):
+                    self.hip.b_spatial(B, wmb, hmb, P(hdr), P(self.col_hdr), P(self.sp_dirty), f1y, hp1, [f0y] + r0y,
+                                       [hp0] + r0h, w1s, P(self.pred_b), P(self.err), s, P(self.intra_cost),
+                                       P(self.cost_b))
             with st("inter"):
                 self.hip.encode_inter(B, wmb, hmb, sy, su, sv, f0y, f0u, f0v, ry, ru, rv, P(self.pred_b), P(self.mv),
                                       P(self.cost_b), P(self.intra_cost), P(self.qp), cqo, P(hdr), P(coef),
@@ -613,7 +629,8 @@ class GpuH264Encoder:
     def _frame_params(self, b: int, pic: PicPlan, qp_frame: int, idr_ids: list[int]) -> dict:
         n0 = self._num_ref_l0(pic)
         fp = dict(idr=int(pic.kind == "I"), frame_num=pic.frame_num, idr_pic_id=idr_ids[b] & 0xFFFF, qp=qp_frame,
-                  slice_type=pic.slice_type, nal_ref_idc=pic.nal_ref_idc, poc=pic.poc, direct_spatial=0,
+                  slice_type=pic.slice_type, nal_ref_idc=pic.nal_ref_idc, poc=pic.poc,
+                  direct_spatial=int(pic.kind == "B" and self.p.direct == "spatial"),
                   **({"num_ref_l0": n0, "num_ref_l1": 1} if pic.kind != "I" else {}))
         if pic.kind == "P" and self._wp is not None:
             fp["wp"] = [WP_LOG2, WP_LOG2] + [int(x) for x in self._wp[pic.d, b]]

@@ -393,3 +393,13 @@ def test_gpu_h264_b_partitions_roundtrip(host):
     assert np.isin(kinds, [10, 11, 12]).sum() > 0, np.bincount(kinds.astype(np.int64) + 1)
     enc, res, _ = _run(352, 288, slots=2, frames=9, crf=None, qp=24, bframes=3, b_gate=-150, bpartitions=False)
     _check_roundtrip(host, enc, res, 352, 288)
+
+
+@pytest.mark.parametrize("refs", [1, 3])
+def test_gpu_h264_spatial_direct_roundtrip(host, refs):
+    """x264 --direct spatial: the direct MBs' motion re-derived from their final neighbours in an
+    MB wavefront (MinPositive reference indices, the 16x16 predictor, colZeroFlag per quadrant)
+    and their prediction rebuilt -- bit-exact against the CPU decoder (direct_spatial_mv_pred_flag
+    1 in the B slice headers), with and without several reference pictures."""
+    enc, res, _ = _run(352, 288, slots=2, frames=13, crf=None, qp=26, bframes=3, refs=refs, direct="spatial")
+    _check_roundtrip(host, enc, res, 352, 288)

@@ -188,7 +188,7 @@ def test_ffargs_reference_and_weighting_knobs():
     p = ffargs.parse("-vcodec libx264 -x264-params ref=1:weightp=0:trellis=0:no-weightb=1").apply_opts(H264Params(64, 64))
     assert (p.refs, p.weightp, p.trellis, p.weightb) == (1, False, 0, False)
     p = ffargs.parse("-vcodec libx264 -x264-params ref=4:weightp=2:trellis=2:direct=temporal").apply_opts(H264Params(64, 64))
-    assert (p.refs, p.weightp, p.trellis, p.eff_refs()) == (4, True, 1, 4)
+    assert (p.refs, p.weightp, p.trellis, p.eff_refs(), p.direct) == (4, True, 1, 4, "temporal")
     assert H264Params(64, 64, cabac=False, refs=3).eff_refs() == 1     # Constrained Baseline: one reference
     assert presets.apply(H264Params(64, 64), "ultrafast").refs == 1
     assert presets.apply(H264Params(64, 64), "fast").refs == 2
