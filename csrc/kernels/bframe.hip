@@ -129,6 +129,9 @@ struct BDecideArgs {
   // direct prediction and cost -- unsearched MBs keep them, the others skip the direct MC
   int have_direct;
   int bparts;  // x264 --partitions b8x8: per-quadrant candidates (B_16x8 / B_8x16 / B_8x8)
+  // spatial direct: searched MBs keep their best explicit candidate (no direct MB / quadrant);
+  // b_spatial_decide weighs it against the exact spatial direct motion in decoding order
+  int spatial;
 };
 
 constexpr int kNoCostB = 0x3FFFFFFF;  // me.hip kNoCost: the MB was not searched
@@ -306,7 +309,8 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   const int mvb0 = mvbits_se(m0x - a.pm0[o * 2]) + mvbits_se(m0y - a.pm0[o * 2 + 1]);
   const int mvb1 = mvbits_se(m1x - a.pm1[o * 2]) + mvbits_se(m1y - a.pm1[o * 2 + 1]);
   const int c_bi = satd_bi + lambda * (6 + mvb0 + mvb1);
-  int mode = 0, best = c_direct;  // 0 direct, 1 L0, 2 L1, 3 Bi
+  const bool no_direct = a.spatial && searched;
+  int mode = 0, best = no_direct ? kNoCostB : c_direct;  // 0 direct, 1 L0, 2 L1, 3 Bi
   if (c_l0 < best) { mode = 1; best = c_l0; }
   if (c_l1 < best) { mode = 2; best = c_l1; }
   if (searched && c_bi < best) { mode = 3; best = c_bi; }
@@ -322,7 +326,7 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
     int sum = 0, used0 = 0, used1 = 0, pm[4];
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) {
-      const int cd = qsat[0][qq] + lambda * 1, cb = qsat[1][qq] + lambda * 7;
+      const int cd = no_direct ? kNoCostB : qsat[0][qq] + lambda * 1, cb = qsat[1][qq] + lambda * 7;
       const int c0q = qsat[2][qq] + lambda * 4, c1q = qsat[3][qq] + lambda * 4;
       int m = 0, bc = cd;
       if (cb < bc) { m = 1; bc = cb; }
@@ -392,20 +396,30 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
 // C (above-right, else D above-left) in the *current* picture: refIdxLX = MinPositive over
 // them, the 16x16 motion-vector predictor of that reference, zeroed per 8x8 quadrant where the
 // co-located block of RefPicList1[0] is static (colZeroFlag).  Neighbours' final motion exists
-// only in decoding order, so b_decide chooses the modes with the temporal-direct estimate and
-// b_spatial_fix then derives the exact motion of every direct MB / B_Direct_8x8 quadrant in an
-// MB wavefront (one wave per MB row chain, the row above two MBs ahead), marking them for
-// b_direct_pred, which rebuilds their luma prediction (fully parallel).
+// only in decoding order, so the direct-vs-explicit decision runs in an MB wavefront (one wave
+// per MB row, the row above two MBs ahead): b_decide (spatial = 1) leaves each searched
+// MB's best explicit candidate (B_L0/L1/Bi 16x16, 16x8, 8x16, B_8x8 without direct quadrants)
+// with its cost, and b_spatial_decide derives the exact direct motion from the final
+// neighbours, prices it (SATD of its bi-prediction + lambda) and takes it when not dearer.
+// MBs the gate left unsearched (b_decide wrote them B_Direct) are always direct.
 struct BSpatialArgs {
   Geom g;
   MbHeader* hdr;         // [B, nmb] current picture (in / out)
   const MbHeader* col;   // [B, nmb] RefPicList1[0]'s records
-  uint8_t* dirty;        // [B, nmb] out: quadrants whose direct motion was (re)derived
   int* err;
-  // encode_inter turns an MB intra when intra_cost < cost (the decision it reads): such MBs are
-  // intra neighbours here and are not derived
+  // encode_inter turns an MB intra when intra_cost < cost (the final decision): such MBs are
+  // intra neighbours for the derivation
   const int* intra_cost;
-  const int* cost;
+  int* cost;             // in: the explicit candidate's cost (unsearched: the temporal estimate); out: final
+  const uint8_t* src_y;
+  const uint8_t *ref1, *hp1;
+  const uint8_t* ref0k[kMaxRefs];
+  const uint8_t* hp0k[kMaxRefs];
+  int w1[kMaxRefs];
+  uint8_t* pred_out;     // [B, nmb, 256] rewritten for MBs that become direct
+  const int* qp;
+  const int8_t* aq;
+  int bias;              // direct taken when cost_d <= cost_e + bias * lambda
 };
 
 struct NbMv16 {
@@ -427,120 +441,140 @@ __device__ __forceinline__ NbMv16 nb16(const MbHeader* h, bool avail, bool intra
 
 __device__ __forceinline__ int med3i(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
 
-constexpr int kSpatialWaves = 4;
+constexpr int kSpatialWaves = 16;  // 16 row chains per slot: the chain (wmb + 2 hmb MBs) bounds it, not the MB count
 
-__global__ __launch_bounds__(64 * kSpatialWaves) void b_spatial_fix(BSpatialArgs a) {
+__global__ __launch_bounds__(64 * kSpatialWaves) void b_spatial_decide(BSpatialArgs a) {
   const Geom& g = a.g;
   const int slot = blockIdx.x, nmb = g.nmb();
   __shared__ int prog[kMaxRows];
+  __shared__ int s_res[kSpatialWaves][256];
   for (int i = threadIdx.x; i < g.hmb; i += blockDim.x) prog[i] = 0;
   __syncthreads();
   const int w = wave_id(), lane = lane_id();
+  const int r = lane >> 2, c0 = (lane & 3) * 4, q = (r >> 3) * 2 + (c0 >> 3);
+  const int W = g.W, Hh = g.H;
+  const size_t yo = static_cast<size_t>(slot) * g.ysize();
+  const size_t ho = static_cast<size_t>(slot) * 3 * (W + 2 * kHpMargin) * (Hh + 2 * kHpMargin);
   MbHeader* H = a.hdr + static_cast<size_t>(slot) * nmb;
   const MbHeader* C0 = a.col + static_cast<size_t>(slot) * nmb;
-  uint8_t* D = a.dirty + static_cast<size_t>(slot) * nmb;
   const int* IC = a.intra_cost + static_cast<size_t>(slot) * nmb;
-  const int* CB = a.cost + static_cast<size_t>(slot) * nmb;
+  int* CB = a.cost + static_cast<size_t>(slot) * nmb;
+  int* res = s_res[w];
   auto is_intra = [&](int m) { return IC[m] < CB[m]; };
+  const int lam_base = a.qp[slot];
   for (int y = w; y < g.hmb; y += kSpatialWaves) {
     for (int x = 0; x < g.wmb; ++x) {
       if (y > 0) row_wait(prog, y - 1, min(x + 2, g.wmb), a.err);
       const int mb = y * g.wmb + x;
+      // lane 0 derives (it alone reads / writes the records, so its own earlier stores order
+      // the left neighbour; the row above arrives through row_wait); packed per quadrant and
+      // list: ref (low 8 bits, signed) | mvx << 8 (12 bits) | mvy << 20 -- mvs fit +-2048
+      int pk[4][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
+      int forced = 0;  // b_decide left the MB direct (unsearched): no explicit candidate exists
       if (lane == 0) {
-        MbHeader& h = H[mb];
-        const int need = is_intra(mb) ? 0
-                                      : (h.kind == h264::MBK_BDIRECT ? 15 : (h.kind == h264::MBK_B8x8 ? (h.sub_direct & 15) : 0));
-        D[mb] = static_cast<uint8_t>(need);
-        if (need) {
-          const bool aA = x > 0, aB = y > 0, aC = y > 0 && x + 1 < g.wmb, aD = x > 0 && y > 0;
-          int refs[2], pmv[2][2] = {{0, 0}, {0, 0}};
+        forced = H[mb].kind == h264::MBK_BDIRECT;
+        const bool aA = x > 0, aB = y > 0, aC = y > 0 && x + 1 < g.wmb, aD = x > 0 && y > 0;
+        int refs[2], pmv[2][2] = {{0, 0}, {0, 0}};
+        for (int l = 0; l < 2; ++l) {
+          NbMv16 A = nb16(&H[mb - 1], aA, aA && is_intra(mb - 1), l, 1);
+          NbMv16 B = nb16(&H[mb - g.wmb], aB, aB && is_intra(mb - g.wmb), l, 2);
+          NbMv16 C = aC ? nb16(&H[mb - g.wmb + 1], true, is_intra(mb - g.wmb + 1), l, 2)
+                        : nb16(&H[mb - g.wmb - 1], aD, aD && is_intra(mb - g.wmb - 1), l, 3);
+          auto minpos = [](int p, int qv) { return (p >= 0 && qv >= 0) ? min(p, qv) : max(p, qv); };
+          refs[l] = minpos(A.ref, minpos(B.ref, C.ref));
+          if (refs[l] < 0) continue;
+          if (!B.avail && !C.avail && A.avail) {
+            B = A;
+            C = A;
+          }
+          const int rr = refs[l];
+          const int match = (A.ref == rr) + (B.ref == rr) + (C.ref == rr);
+          if (match == 1) {
+            const NbMv16& m = A.ref == rr ? A : (B.ref == rr ? B : C);
+            pmv[l][0] = m.mv[0];
+            pmv[l][1] = m.mv[1];
+          } else {
+            pmv[l][0] = med3i(A.mv[0], B.mv[0], C.mv[0]);
+            pmv[l][1] = med3i(A.mv[1], B.mv[1], C.mv[1]);
+          }
+        }
+        const bool zero = refs[0] < 0 && refs[1] < 0;
+        const MbHeader& c = C0[mb];
+        const bool cintra = h264::mbk_is_intra(c.kind);
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const bool col_zero = !cintra && c.ref[0][qq] == 0 && abs(c.mv[0][qq][0]) <= 1 && abs(c.mv[0][qq][1]) <= 1;
+#pragma unroll
           for (int l = 0; l < 2; ++l) {
-            NbMv16 A = nb16(&H[mb - 1], aA, aA && is_intra(mb - 1), l, 1);
-            NbMv16 B = nb16(&H[mb - g.wmb], aB, aB && is_intra(mb - g.wmb), l, 2);
-            NbMv16 C = aC ? nb16(&H[mb - g.wmb + 1], true, is_intra(mb - g.wmb + 1), l, 2)
-                          : nb16(&H[mb - g.wmb - 1], aD, aD && is_intra(mb - g.wmb - 1), l, 3);
-            auto minpos = [](int p, int q) { return (p >= 0 && q >= 0) ? min(p, q) : max(p, q); };
-            refs[l] = minpos(A.ref, minpos(B.ref, C.ref));
-            if (refs[l] < 0) continue;
-            if (!B.avail && !C.avail && A.avail) {
-              B = A;
-              C = A;
+            int rf = refs[l], mx = pmv[l][0], my = pmv[l][1];
+            if (zero) {
+              rf = 0;
+              mx = my = 0;
+            } else if (rf < 0 || (rf == 0 && col_zero)) {
+              mx = my = 0;
             }
-            const int r = refs[l];
-            const int match = (A.ref == r) + (B.ref == r) + (C.ref == r);
-            if (match == 1) {
-              const NbMv16& m = A.ref == r ? A : (B.ref == r ? B : C);
-              pmv[l][0] = m.mv[0];
-              pmv[l][1] = m.mv[1];
-            } else {
-              pmv[l][0] = med3i(A.mv[0], B.mv[0], C.mv[0]);
-              pmv[l][1] = med3i(A.mv[1], B.mv[1], C.mv[1]);
-            }
+            pk[qq][l] = (rf & 255) | ((mx & 4095) << 8) | (my << 20);
           }
-          const bool zero = refs[0] < 0 && refs[1] < 0;
-          const MbHeader& c = C0[mb];
-          const bool cintra = h264::mbk_is_intra(c.kind);
-          for (int q = 0; q < 4; ++q) {
-            if (!((need >> q) & 1)) continue;
-            const bool col_zero = !cintra && c.ref[0][q] == 0 && abs(c.mv[0][q][0]) <= 1 && abs(c.mv[0][q][1]) <= 1;
+        }
+      }
+      int mine[2] = {0, 0};
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+        for (int l = 0; l < 2; ++l) {
+          const int v = __builtin_amdgcn_readlane(pk[qq][l], 0);
+          if (qq == q) mine[l] = v;
+        }
+      const int r0 = static_cast<int8_t>(mine[0] & 255), r1 = static_cast<int8_t>(mine[1] & 255);
+      const int m0x = (mine[0] << 12) >> 20, m0y = mine[0] >> 20;
+      const int m1x = (mine[1] << 12) >> 20, m1y = mine[1] >> 20;
+      const int X = x * 16 + c0, Y = y * 16 + r;
+      uint32_t p0 = 0, p1 = 0;
+      if (r0 >= 0) p0 = mc4(a.ref0k[r0 & 3] + yo, a.hp0k[r0 & 3] + ho, W, Hh, X, Y, m0x, m0y);
+      if (r1 >= 0) p1 = mc4(a.ref1 + yo, a.hp1 + ho, W, Hh, X, Y, m1x, m1y);
+      const uint32_t pw = (r0 >= 0 && r1 >= 0) ? wavg4b(p0, p1, a.w1[r0 & 3]) : (r0 >= 0 ? p0 : p1);
+      const uint32_t src = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y) * W + X);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        res[r * 16 + c0 + k] = static_cast<int>((src >> (8 * k)) & 255u) - static_cast<int>((pw >> (8 * k)) & 255u);
+      wave_sync();
+      int satd = 0;
+      if (lane < 16) {
+        const int bx = (lane & 3) * 4, by = (lane >> 2) * 4;
+        int rr[16];
+#pragma unroll
+        for (int yy = 0; yy < 4; ++yy)
+#pragma unroll
+          for (int xx = 0; xx < 4; ++xx) rr[yy * 4 + xx] = res[(by + yy) * 16 + bx + xx];
+        satd = h264::satd4x4(rr);
+      }
+      satd = __builtin_amdgcn_readlane(sum16(satd), 0);
+      wave_sync();  // res is rewritten by the next MB
+      const size_t o = static_cast<size_t>(slot) * nmb + mb;
+      const int lambda = h264::kLambda[clampi(lam_base + (a.aq ? a.aq[o] : 0), 0, 51)];
+      const int cost_d = satd + lambda;
+      const int cost_e = __builtin_amdgcn_readfirstlane(CB[mb]);
+      if (__builtin_amdgcn_readlane(forced, 0) || cost_d <= cost_e + a.bias * lambda) {
+        *reinterpret_cast<uint32_t*>(a.pred_out + o * 256 + r * 16 + c0) = pw;
+        if (lane == 0) {
+          MbHeader& h = H[mb];
+          h.kind = h264::MBK_BDIRECT;
+          h.sub_direct = 0;
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
             for (int l = 0; l < 2; ++l) {
-              int r = refs[l], mx = pmv[l][0], my = pmv[l][1];
-              if (zero) {
-                r = 0;
-                mx = my = 0;
-              } else if (r < 0) {
-                mx = my = 0;
-              } else if (r == 0 && col_zero) {
-                mx = my = 0;
-              }
-              h.ref[l][q] = static_cast<int8_t>(r);
-              h.mv[l][q][0] = static_cast<int16_t>(mx);
-              h.mv[l][q][1] = static_cast<int16_t>(my);
+              const int v = pk[qq][l];
+              h.ref[l][qq] = static_cast<int8_t>(v & 255);
+              h.mv[l][qq][0] = static_cast<int16_t>((v << 12) >> 20);
+              h.mv[l][qq][1] = static_cast<int16_t>(v >> 20);
             }
-          }
+          CB[mb] = cost_d;
         }
       }
       row_publish(prog, y, x + 1);
     }
   }
-}
-
-// luma prediction of the quadrants b_spatial_fix re-derived (one wave per MB, lane = row
-// lane >> 2, columns 4 * (lane & 3) .. +3): list-0 picture ref0k[refIdxL0], list 1 = ref1,
-// bi-prediction with the implicit weight of the pair
-struct BDirectPredArgs {
-  Geom g;
-  const MbHeader* hdr;
-  const uint8_t* dirty;
-  const uint8_t *ref1, *hp1;
-  const uint8_t* ref0k[kMaxRefs];
-  const uint8_t* hp0k[kMaxRefs];
-  int w1[kMaxRefs];
-  uint8_t* pred_out;
-};
-
-__global__ __launch_bounds__(64) void b_direct_pred(BDirectPredArgs a) {
-  const Geom& g = a.g;
-  const int nmb = g.nmb();
-  int mb, slot;
-  xcd_unit_slot(mb, slot);
-  const size_t o = static_cast<size_t>(slot) * nmb + mb;
-  const int dm = a.dirty[o];
-  if (!dm) return;
-  const int lane = threadIdx.x, r = lane >> 2, c0 = (lane & 3) * 4;
-  const int q = (r >> 3) * 2 + (c0 >> 3);
-  if (!((dm >> q) & 1)) return;
-  const int mx = mb % g.wmb, my = mb / g.wmb, W = g.W, H = g.H;
-  const int X = mx * 16 + c0, Y = my * 16 + r;
-  const size_t yo = static_cast<size_t>(slot) * g.ysize();
-  const size_t ho = static_cast<size_t>(slot) * 3 * (W + 2 * kHpMargin) * (H + 2 * kHpMargin);
-  const MbHeader& h = a.hdr[o];
-  const int r0 = h.ref[0][q], r1 = h.ref[1][q];
-  uint32_t p0 = 0, p1 = 0;
-  if (r0 >= 0) p0 = mc4(a.ref0k[r0 & 3] + yo, a.hp0k[r0 & 3] + ho, W, H, X, Y, h.mv[0][q][0], h.mv[0][q][1]);
-  if (r1 >= 0) p1 = mc4(a.ref1 + yo, a.hp1 + ho, W, H, X, Y, h.mv[1][q][0], h.mv[1][q][1]);
-  const uint32_t pw = (r0 >= 0 && r1 >= 0) ? wavg4b(p0, p1, a.w1[r0 & 3]) : (r0 >= 0 ? p0 : p1);
-  *reinterpret_cast<uint32_t*>(a.pred_out + o * 256 + r * 16 + c0) = pw;
 }
 
 // ---------------------------------------------------------------- P_Skip-aware vector choice
@@ -1199,8 +1233,10 @@ extern "C" void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src
                                      const uint8_t* pred1, const int16_t* pm0, const int16_t* pm1, const int16_t* dmv,
                                      const int* qp, const int8_t* aq, void* hdr, uint8_t* pred_out, int* cost_out,
                                      void* stream, const int* w1, int nref, const int8_t* dref,
-                                     const uint8_t* const* ref0k, const uint8_t* const* hp0k, int direct_only, int bparts, int have_direct) {
+                                     const uint8_t* const* ref0k, const uint8_t* const* hp0k, int direct_only, int bparts, int have_direct,
+                                     int spatial) {
   BDecideArgs a;
+  a.spatial = spatial;
   a.direct_only = direct_only;
   a.have_direct = have_direct;
   a.bparts = bparts;
@@ -1331,26 +1367,30 @@ extern "C" void mivc_launch_hevc_b(int mode, int B, int wmb, int hmb, const uint
   else hipLaunchKernelGGL(hevc_b_init_p, dim3((wmb * hmb + 255) / 256, B), dim3(256), 0, st, a);
 }
 
-extern "C" void mivc_launch_b_spatial(int B, int wmb, int hmb, void* hdr, const void* col, uint8_t* dirty,
+extern "C" void mivc_launch_b_spatial(int B, int wmb, int hmb, void* hdr, const void* col, const uint8_t* src_y,
                                       const uint8_t* ref1, const uint8_t* hp1, const uint8_t* const* ref0k,
                                       const uint8_t* const* hp0k, const int* w1, int nref, uint8_t* pred_out, int* err,
-                                      void* stream, const int* intra_cost, const int* cost) {
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  BSpatialArgs a{Geom{B, wmb, hmb, wmb * 16, hmb * 16}, static_cast<MbHeader*>(hdr), static_cast<const MbHeader*>(col),
-                 dirty, err, intra_cost, cost};
-  hipLaunchKernelGGL(b_spatial_fix, dim3(B), dim3(64 * kSpatialWaves), 0, s, a);
-  BDirectPredArgs p;
-  p.g = a.g;
-  p.hdr = static_cast<const MbHeader*>(hdr);
-  p.dirty = dirty;
-  p.ref1 = ref1;
-  p.hp1 = hp1;
+                                      void* stream, const int* intra_cost, int* cost, const int* qp, const int8_t* aq,
+                                      int bias) {
+  BSpatialArgs a;
+  a.bias = bias;
+  a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
+  a.hdr = static_cast<MbHeader*>(hdr);
+  a.col = static_cast<const MbHeader*>(col);
+  a.err = err;
+  a.intra_cost = intra_cost;
+  a.cost = cost;
+  a.src_y = src_y;
+  a.ref1 = ref1;
+  a.hp1 = hp1;
   for (int r = 0; r < kMaxRefs; ++r) {
     const int rr = r < nref ? r : nref - 1;
-    p.ref0k[r] = ref0k[rr];
-    p.hp0k[r] = hp0k[rr];
-    p.w1[r] = w1[rr];
+    a.ref0k[r] = ref0k[rr];
+    a.hp0k[r] = hp0k[rr];
+    a.w1[r] = w1[rr];
   }
-  p.pred_out = pred_out;
-  hipLaunchKernelGGL(b_direct_pred, dim3(wmb * hmb, B), dim3(64), 0, s, p);
+  a.pred_out = pred_out;
+  a.qp = qp;
+  a.aq = aq;
+  hipLaunchKernelGGL(b_spatial_decide, dim3(B), dim3(64 * kSpatialWaves), 0, static_cast<hipStream_t>(stream), a);
 }

@@ -28,9 +28,10 @@ void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t
 void mivc_launch_me_ref_select(int B, int wmb, int hmb, int nref, int16_t* mv, int16_t* mv8, int* cost, uint8_t* pred,
                                const int16_t* xmv, const int* xcost, const uint8_t* xpred, int8_t* mref, const int* qp,
                                const int8_t* aq, void* stream);
-void mivc_launch_b_spatial(int B, int wmb, int hmb, void* hdr, const void* col, uint8_t* dirty, const uint8_t* ref1,
+void mivc_launch_b_spatial(int B, int wmb, int hmb, void* hdr, const void* col, const uint8_t* src, const uint8_t* ref1,
                            const uint8_t* hp1, const uint8_t* const* ref0k, const uint8_t* const* hp0k, const int* w1,
-                           int nref, uint8_t* pred_out, int* err, void* stream, const int* intra_cost, const int* cost);
+                           int nref, uint8_t* pred_out, int* err, void* stream, const int* intra_cost, int* cost,
+                           const int* qp, const int8_t* aq, int bias);
 void mivc_launch_b_direct(int B, int wmb, int hmb, const void* col, const int* dsf, const int* direct_copy, int nref,
                           int16_t* dmv, int8_t* dref, int16_t* pm0, int16_t* pm1, void* stream);
 void mivc_launch_p_refine(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref, const uint8_t* hp,
@@ -42,7 +43,7 @@ void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src_y, const u
                           const int16_t* pm0, const int16_t* pm1, const int16_t* dmv, const int* qp, const int8_t* aq,
                           void* hdr, uint8_t* pred_out, int* cost_out, void* stream, const int* w1, int nref,
                           const int8_t* dref, const uint8_t* const* ref0k, const uint8_t* const* hp0k,
-                          int direct_only, int bparts, int have_direct);
+                          int direct_only, int bparts, int have_direct, int spatial);
 void mivc_launch_aq_offsets(int B, int wmb, int hmb, const uint8_t* sy, const uint8_t* su, const uint8_t* sv,
                             float strength, const float* extra, long long extra_stride, int8_t* out, void* stream);
 void mivc_launch_mbtree(int B, int F, int lbw, int lbh, const int* blk_cost, const int* blk_mv, void* prop,
@@ -195,11 +196,12 @@ PYBIND11_MODULE(_hip, m) {
                               P<int16_t>(xmv), P<int>(xcost), P<uint8_t>(xpred), P<int8_t>(mref), P<int>(qp),
                               P<int8_t>(aq), S(stream));
   });
-  m.def("b_spatial", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t col, uintptr_t dirty, uintptr_t ref1,
+  m.def("b_spatial", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t col, uintptr_t src, uintptr_t ref1,
                         uintptr_t hp1, std::vector<uintptr_t> ref0k, std::vector<uintptr_t> hp0k, std::vector<int> w1,
-                        uintptr_t pred_out, uintptr_t err, uintptr_t stream, uintptr_t intra_cost, uintptr_t cost) {
-    // spatial direct: exact derivation in MB wavefront order + the luma prediction of the
-    // re-derived quadrants; ref0k / hp0k / w1: every list-0 picture (entry 0 = RefPicList0[0])
+                        uintptr_t pred_out, uintptr_t err, uintptr_t stream, uintptr_t intra_cost, uintptr_t cost,
+                        uintptr_t qp, uintptr_t aq, int bias) {
+    // spatial direct: exact derivation + direct-vs-explicit decision in MB wavefront order;
+    // ref0k / hp0k / w1: every list-0 picture (entry 0 = RefPicList0[0])
     const size_t n = ref0k.size();
     if (n < 1 || n > 4 || hp0k.size() != n || w1.size() != n)
       throw std::invalid_argument("b_spatial: 1..4 list-0 pictures with planes and weights");
@@ -210,9 +212,9 @@ PYBIND11_MODULE(_hip, m) {
       rk[i] = P<uint8_t>(ref0k[i]);
       hk[i] = P<uint8_t>(hp0k[i]);
     }
-    mivc_launch_b_spatial(B, wmb, hmb, P<void>(hdr), P<void>(col), P<uint8_t>(dirty), P<uint8_t>(ref1), P<uint8_t>(hp1),
+    mivc_launch_b_spatial(B, wmb, hmb, P<void>(hdr), P<void>(col), P<uint8_t>(src), P<uint8_t>(ref1), P<uint8_t>(hp1),
                           rk, hk, w1.data(), static_cast<int>(n), P<uint8_t>(pred_out), P<int>(err), S(stream),
-                          P<int>(intra_cost), P<int>(cost));
+                          P<int>(intra_cost), P<int>(cost), P<int>(qp), P<int8_t>(aq), bias);
   });
   m.def("b_direct", [](int B, int wmb, int hmb, uintptr_t col, std::vector<int> dsf, std::vector<int> direct_copy,
                        uintptr_t dmv, uintptr_t pm0, uintptr_t pm1, uintptr_t stream, uintptr_t dref) {
@@ -234,7 +236,8 @@ PYBIND11_MODULE(_hip, m) {
                        uintptr_t hp1, uintptr_t mv0, uintptr_t mv1, uintptr_t cost0, uintptr_t cost1, uintptr_t pred0,
                        uintptr_t pred1, uintptr_t pm0, uintptr_t pm1, uintptr_t dmv, uintptr_t qp, uintptr_t aq,
                        uintptr_t hdr, uintptr_t pred_out, uintptr_t cost_out, uintptr_t stream, std::vector<int> w1,
-                       uintptr_t dref, std::vector<uintptr_t> ref0k, std::vector<uintptr_t> hp0k, int direct_only, int bparts, int have_direct) {
+                       uintptr_t dref, std::vector<uintptr_t> ref0k, std::vector<uintptr_t> hp0k, int direct_only, int bparts, int have_direct,
+                       int spatial) {
     // w1: implicit list-1 weight per list-0 picture; ref0k / hp0k: luma / half-sample planes of
     // RefPicList0[1..] (direct prediction of quadrants whose co-located block used a farther picture)
     if (w1.empty() || w1.size() > 4) throw std::invalid_argument("b_decide: one implicit weight per list-0 picture");
@@ -253,13 +256,14 @@ PYBIND11_MODULE(_hip, m) {
                          P<uint8_t>(hp1), P<int16_t>(mv0), P<int16_t>(mv1), P<int>(cost0), P<int>(cost1),
                          P<uint8_t>(pred0), P<uint8_t>(pred1), P<int16_t>(pm0), P<int16_t>(pm1), P<int16_t>(dmv),
                          P<int>(qp), P<int8_t>(aq), P<void>(hdr), P<uint8_t>(pred_out), P<int>(cost_out), S(stream),
-                         w1.data(), static_cast<int>(n), n > 1 ? P<int8_t>(dref) : nullptr, rk, hk, direct_only, bparts, have_direct);
+                         w1.data(), static_cast<int>(n), n > 1 ? P<int8_t>(dref) : nullptr, rk, hk, direct_only, bparts, have_direct,
+                         spatial);
   }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("src"), py::arg("ref0"), py::arg("ref1"), py::arg("hp0"),
      py::arg("hp1"), py::arg("mv0"), py::arg("mv1"), py::arg("cost0"), py::arg("cost1"), py::arg("pred0"),
      py::arg("pred1"), py::arg("pm0"), py::arg("pm1"), py::arg("dmv"), py::arg("qp"), py::arg("aq"), py::arg("hdr"),
      py::arg("pred_out"), py::arg("cost_out"), py::arg("stream"), py::arg("w1") = std::vector<int>{32},
      py::arg("dref") = 0, py::arg("ref0k") = std::vector<uintptr_t>{}, py::arg("hp0k") = std::vector<uintptr_t>{},
-     py::arg("direct_only") = 0, py::arg("bparts") = 0, py::arg("have_direct") = 0);
+     py::arg("direct_only") = 0, py::arg("bparts") = 0, py::arg("have_direct") = 0, py::arg("spatial") = 0);
   m.def("aq_offsets", [](int B, int wmb, int hmb, uintptr_t sy, uintptr_t su, uintptr_t sv, float strength,
                          uintptr_t out, uintptr_t stream, uintptr_t extra, long long extra_stride) {
     mivc_launch_aq_offsets(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), strength, P<float>(extra),

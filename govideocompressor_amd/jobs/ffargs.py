@@ -192,9 +192,9 @@ H264_PARAMS = {
     "weightb": ("weightb", _flag),
     "no-weightb": ("weightb", lambda v: not _flag(v)),
     "trellis": ("trellis", lambda v: int(_int_in(0, 2)(v) > 0)),
-    # direct=spatial exists (H264Params.direct) but its modes are decided on the temporal estimate:
-    # measured +190 % BD-rate on the benchmark content (profiles/r3_direct_rd.md), so not offered
-    "direct": ("@direct", _only("temporal")),
+    # direct=spatial: decided in an MB wavefront (bframe.hip b_spatial_decide), -2.2 % BD-rate
+    # and ~35 % fewer frames/s than temporal on the benchmark content (profiles/r3_direct_rd.md)
+    "direct": ("direct", _only("temporal", "spatial")),
     "b-adapt": ("@b-adapt", _only("0")),
     "b-pyramid": ("@b-pyramid", _only("none")),
     "crf": ("@crf", _float_in(0.0, 51.0)),

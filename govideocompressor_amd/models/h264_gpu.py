@@ -109,13 +109,13 @@ class H264Params:
     # (encode_inter.hip trellis_lite4x4); trellis_lambda scales its SSD lambda
     trellis: int = int(os.environ.get("MIVC_TRELLIS", 1))
     # x264 --direct: "temporal" (co-located motion scaled by POC distances: every MB decides in
-    # parallel) or "spatial" (the neighbours' motion: b_decide chooses with the temporal
-    # estimate, then bframe.hip b_spatial_fix derives the exact spatial motion of the direct
-    # MBs in an MB wavefront and b_direct_pred rebuilds their prediction).  Spatial is bit-exact
-    # but its modes are chosen on the temporal estimate, so direct MBs chained off zero-motion
-    # neighbours lose: +190 % BD-rate on the benchmark content (profiles/r3_direct_rd.md) until
-    # the decision itself runs in the wavefront
+    # parallel) or "spatial" (the neighbours' motion: b_decide keeps each searched MB's best
+    # explicit candidate, then bframe.hip b_spatial_decide derives the exact spatial motion in
+    # an MB wavefront and takes direct where its SATD + lambda is not dearer; RD in
+    # profiles/r3_direct_rd.md)
     direct: str = os.environ.get("MIVC_DIRECT", "temporal")
+    # spatial direct: direct is taken when its cost <= the explicit candidate's + direct_bias * lambda
+    direct_bias: int = int(os.environ.get("MIVC_DIRECT_BIAS", 8))
     trellis_lambda: float = float(os.environ.get("MIVC_TRELLIS_LAMBDA", 1.0))
     # deblock non-reference B pictures even when neither metrics nor the reconstruction
     # are requested (x264 --full-recon); the bitstream does not depend on it
@@ -305,7 +305,6 @@ class GpuH264Encoder:
             self.pm1 = torch.zeros((B, nmb, 2), dtype=i16, device=dev)
             self.dmv = torch.zeros((B, nmb, 16), dtype=i16, device=dev)
             self.col_hdr = torch.zeros((B, nmb, MB_HDR_BYTES), dtype=u8, device=dev)
-            self.sp_dirty = torch.zeros((B, nmb), dtype=u8, device=dev)  # spatial direct: re-derived quadrants
         if params.eff_weightp():
             self.src_me = torch.zeros((B, H, W), dtype=u8, device=dev)  # inverse-weighted luma for ME
         self.intra_flag = torch.zeros((B, nmb), dtype=u8, device=dev)
@@ -548,7 +547,8 @@ class GpuH264Encoder:
                     xv.append(P(rk[2]))
             self.intra_count.zero_()
             br = self.p.b_me_range
-            bg = int(self.p.b_gate)
+            # spatial direct cannot be priced before the wavefront, so it searches every MB
+            bg = int(self.p.b_gate) if self.p.direct != "spatial" else 0
             with st("me_b"):
                 self.hip.b_direct(B, wmb, hmb, P(self.col_hdr), dsfs, copies, P(self.dmv), P(self.pm0), P(self.pm1), s,
                                   P(self.dref) if nr > 1 else 0)
@@ -569,14 +569,14 @@ class GpuH264Encoder:
                                   P(self.me_cost1), P(self.pred), P(self.pred1), P(self.pm0), P(self.pm1),
                                   P(self.dmv), P(self.qp), aq, P(hdr), P(self.pred_b), P(self.cost_b), s, w1s,
                                   P(self.dref) if nr > 1 else 0, r0y, r0h, 0, int(self.p.eff_partitions() and self.p.bpartitions),
-                                  int(bg != 0))
+                                  int(bg != 0), int(self.p.direct == "spatial"))
             if cut is not None:
                 self.intra_cost.masked_fill_(cut[:, None], -1)
             if self.p.direct == "spatial":
                 with st("b_spatial"):
-                    self.hip.b_spatial(B, wmb, hmb, P(hdr), P(self.col_hdr), P(self.sp_dirty), f1y, hp1, [f0y] + r0y,
+                    self.hip.b_spatial(B, wmb, hmb, P(hdr), P(self.col_hdr), sy, f1y, hp1, [f0y] + r0y,
                                        [hp0] + r0h, w1s, P(self.pred_b), P(self.err), s, P(self.intra_cost),
-                                       P(self.cost_b))
+                                       P(self.cost_b), P(self.qp), aq, int(self.p.direct_bias))
             with st("inter"):
                 self.hip.encode_inter(B, wmb, hmb, sy, su, sv, f0y, f0u, f0v, ry, ru, rv, P(self.pred_b), P(self.mv),
                                       P(self.cost_b), P(self.intra_cost), P(self.qp), cqo, P(hdr), P(coef),

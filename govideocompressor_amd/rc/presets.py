@@ -19,7 +19,8 @@ fast        quarter-pel, radius 8, 2 references (--subme 6 --ref 2)
 medium      defaults (x264 defaults, the reference's "264" preset: --ref 3, weightp, trellis 1)
 slow        radius 12, B radius 6, Intra4x4 in P pictures, 4 references (--me umh --subme 8
             --ref 5)
-slower      radius 16, B radius 8, lookahead radius 8, 4 references (--subme 9 --me umh --ref 8)
+slower      radius 16, B radius 8, lookahead radius 8, 4 references, spatial direct
+            (--subme 9 --me umh --ref 8 --direct spatial)
 veryslow    slower + three skip-refine passes (--subme 10 --me umh --merange 24 --ref 16)
 placebo     = veryslow
 ==========  ========================================================================
@@ -47,8 +48,8 @@ H264 = {
     "fast": dict(subpel=2, me_range=8, refs=2),
     "medium": dict(),
     "slow": dict(me_range=12, b_me_range=6, i4x4_in_p=True, refs=4),
-    "slower": dict(me_range=16, b_me_range=8, i4x4_in_p=True, la_range=8, refs=4),
-    "veryslow": dict(me_range=16, b_me_range=8, i4x4_in_p=True, la_range=8, skip_refine=3, refs=4),
+    "slower": dict(me_range=16, b_me_range=8, i4x4_in_p=True, la_range=8, refs=4, direct="spatial"),
+    "veryslow": dict(me_range=16, b_me_range=8, i4x4_in_p=True, la_range=8, skip_refine=3, refs=4, direct="spatial"),
 }
 H264["placebo"] = H264["veryslow"]
 

@@ -397,9 +397,9 @@ def test_gpu_h264_b_partitions_roundtrip(host):
 
 @pytest.mark.parametrize("refs", [1, 3])
 def test_gpu_h264_spatial_direct_roundtrip(host, refs):
-    """x264 --direct spatial: the direct MBs' motion re-derived from their final neighbours in an
+    """x264 --direct spatial: the direct MBs' motion derived from their final neighbours in an
     MB wavefront (MinPositive reference indices, the 16x16 predictor, colZeroFlag per quadrant)
-    and their prediction rebuilt -- bit-exact against the CPU decoder (direct_spatial_mv_pred_flag
+    and weighed there against each MB's explicit candidate -- bit-exact against the CPU decoder (direct_spatial_mv_pred_flag
     1 in the B slice headers), with and without several reference pictures."""
     enc, res, _ = _run(352, 288, slots=2, frames=13, crf=None, qp=26, bframes=3, refs=refs, direct="spatial")
     _check_roundtrip(host, enc, res, 352, 288)

@@ -168,7 +168,7 @@ def test_ffargs_strict_rejections():
     """Options the native encoders cannot honour are errors, never silently dropped."""
     for bad in ("-vcodec libx264 -tune film", "-vcodec libx264 -tune ssim", "-vcodec libx264 -profile:v high10",
                 "-vcodec libx264 -profile:v high444", "-vcodec libx265 -profile:v main12",
-                "-vcodec libx264 -x264-params ref=5", "-vcodec libx264 -x264-params direct=spatial",
+                "-vcodec libx264 -x264-params ref=5", "-vcodec libx264 -x264-params direct=auto",
                 "-vcodec libx264 -x264-params b-adapt=2", "-vcodec libx264 -x264-params b-pyramid=normal",
                 "-vcodec libx264 -x264-params foo=1", "-vcodec libx264 -x265-params sao=0",
                 "-vcodec libx265 -x265-params bframes=9", "-vcodec libx265 -x265-params ctu=16",
@@ -189,6 +189,10 @@ def test_ffargs_reference_and_weighting_knobs():
     assert (p.refs, p.weightp, p.trellis, p.weightb) == (1, False, 0, False)
     p = ffargs.parse("-vcodec libx264 -x264-params ref=4:weightp=2:trellis=2:direct=temporal").apply_opts(H264Params(64, 64))
     assert (p.refs, p.weightp, p.trellis, p.eff_refs(), p.direct) == (4, True, 1, 4, "temporal")
+    p = ffargs.parse("-vcodec libx264 -x264-params direct=spatial").apply_opts(H264Params(64, 64))
+    assert p.direct == "spatial"
+    assert presets.apply(H264Params(64, 64), "slower").direct == "spatial"
+    assert presets.apply(H264Params(64, 64), "medium").direct == "temporal"
     assert H264Params(64, 64, cabac=False, refs=3).eff_refs() == 1     # Constrained Baseline: one reference
     assert presets.apply(H264Params(64, 64), "ultrafast").refs == 1
     assert presets.apply(H264Params(64, 64), "fast").refs == 2
