@@ -132,6 +132,7 @@ struct BDecideArgs {
   // spatial direct: searched MBs keep their best explicit candidate (no direct MB / quadrant);
   // b_spatial_decide weighs it against the exact spatial direct motion in decoding order
   int spatial;
+  int dbias;  // temporal direct preferred by dbias * lambda in the 16x16 choice (cost_out stays unbiased)
 };
 
 constexpr int kNoCostB = 0x3FFFFFFF;  // me.hip kNoCost: the MB was not searched
@@ -310,7 +311,8 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   const int mvb1 = mvbits_se(m1x - a.pm1[o * 2]) + mvbits_se(m1y - a.pm1[o * 2 + 1]);
   const int c_bi = satd_bi + lambda * (6 + mvb0 + mvb1);
   const bool no_direct = a.spatial && searched;
-  int mode = 0, best = no_direct ? kNoCostB : c_direct;  // 0 direct, 1 L0, 2 L1, 3 Bi
+  const int dbias = no_direct ? 0 : a.dbias * lambda;
+  int mode = 0, best = no_direct ? kNoCostB : c_direct - dbias;  // 0 direct, 1 L0, 2 L1, 3 Bi
   if (c_l0 < best) { mode = 1; best = c_l0; }
   if (c_l1 < best) { mode = 2; best = c_l1; }
   if (searched && c_bi < best) { mode = 3; best = c_bi; }
@@ -387,7 +389,7 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
     uint4* mvp = reinterpret_cast<uint4*>(&h->mv[0][0][0]);  // 16-byte aligned
     mvp[0] = make_uint4(w[0][0], w[0][1], w[0][2], w[0][3]);
     mvp[1] = make_uint4(w[1][0], w[1][1], w[1][2], w[1][3]);
-    a.cost_out[o] = best;
+    a.cost_out[o] = best + (kind == h264::MBK_BDIRECT ? dbias : 0);
   }
 }
 
@@ -1234,9 +1236,10 @@ extern "C" void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src
                                      const int* qp, const int8_t* aq, void* hdr, uint8_t* pred_out, int* cost_out,
                                      void* stream, const int* w1, int nref, const int8_t* dref,
                                      const uint8_t* const* ref0k, const uint8_t* const* hp0k, int direct_only, int bparts, int have_direct,
-                                     int spatial) {
+                                     int spatial, int dbias) {
   BDecideArgs a;
   a.spatial = spatial;
+  a.dbias = dbias;
   a.direct_only = direct_only;
   a.have_direct = have_direct;
   a.bparts = bparts;

@@ -43,7 +43,7 @@ void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src_y, const u
                           const int16_t* pm0, const int16_t* pm1, const int16_t* dmv, const int* qp, const int8_t* aq,
                           void* hdr, uint8_t* pred_out, int* cost_out, void* stream, const int* w1, int nref,
                           const int8_t* dref, const uint8_t* const* ref0k, const uint8_t* const* hp0k,
-                          int direct_only, int bparts, int have_direct, int spatial);
+                          int direct_only, int bparts, int have_direct, int spatial, int dbias);
 void mivc_launch_aq_offsets(int B, int wmb, int hmb, const uint8_t* sy, const uint8_t* su, const uint8_t* sv,
                             float strength, const float* extra, long long extra_stride, int8_t* out, void* stream);
 void mivc_launch_mbtree(int B, int F, int lbw, int lbh, const int* blk_cost, const int* blk_mv, void* prop,
@@ -237,7 +237,7 @@ PYBIND11_MODULE(_hip, m) {
                        uintptr_t pred1, uintptr_t pm0, uintptr_t pm1, uintptr_t dmv, uintptr_t qp, uintptr_t aq,
                        uintptr_t hdr, uintptr_t pred_out, uintptr_t cost_out, uintptr_t stream, std::vector<int> w1,
                        uintptr_t dref, std::vector<uintptr_t> ref0k, std::vector<uintptr_t> hp0k, int direct_only, int bparts, int have_direct,
-                       int spatial) {
+                       int spatial, int dbias) {
     // w1: implicit list-1 weight per list-0 picture; ref0k / hp0k: luma / half-sample planes of
     // RefPicList0[1..] (direct prediction of quadrants whose co-located block used a farther picture)
     if (w1.empty() || w1.size() > 4) throw std::invalid_argument("b_decide: one implicit weight per list-0 picture");
@@ -257,13 +257,13 @@ PYBIND11_MODULE(_hip, m) {
                          P<uint8_t>(pred0), P<uint8_t>(pred1), P<int16_t>(pm0), P<int16_t>(pm1), P<int16_t>(dmv),
                          P<int>(qp), P<int8_t>(aq), P<void>(hdr), P<uint8_t>(pred_out), P<int>(cost_out), S(stream),
                          w1.data(), static_cast<int>(n), n > 1 ? P<int8_t>(dref) : nullptr, rk, hk, direct_only, bparts, have_direct,
-                         spatial);
+                         spatial, dbias);
   }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("src"), py::arg("ref0"), py::arg("ref1"), py::arg("hp0"),
      py::arg("hp1"), py::arg("mv0"), py::arg("mv1"), py::arg("cost0"), py::arg("cost1"), py::arg("pred0"),
      py::arg("pred1"), py::arg("pm0"), py::arg("pm1"), py::arg("dmv"), py::arg("qp"), py::arg("aq"), py::arg("hdr"),
      py::arg("pred_out"), py::arg("cost_out"), py::arg("stream"), py::arg("w1") = std::vector<int>{32},
      py::arg("dref") = 0, py::arg("ref0k") = std::vector<uintptr_t>{}, py::arg("hp0k") = std::vector<uintptr_t>{},
-     py::arg("direct_only") = 0, py::arg("bparts") = 0, py::arg("have_direct") = 0, py::arg("spatial") = 0);
+     py::arg("direct_only") = 0, py::arg("bparts") = 0, py::arg("have_direct") = 0, py::arg("spatial") = 0, py::arg("dbias") = 0);
   m.def("aq_offsets", [](int B, int wmb, int hmb, uintptr_t sy, uintptr_t su, uintptr_t sv, float strength,
                          uintptr_t out, uintptr_t stream, uintptr_t extra, long long extra_stride) {
     mivc_launch_aq_offsets(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), strength, P<float>(extra),

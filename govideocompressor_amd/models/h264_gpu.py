@@ -116,6 +116,8 @@ class H264Params:
     direct: str = os.environ.get("MIVC_DIRECT", "temporal")
     # spatial direct: direct is taken when its cost <= the explicit candidate's + direct_bias * lambda
     direct_bias: int = int(os.environ.get("MIVC_DIRECT_BIAS", 8))
+    # temporal direct: B_Direct_16x16 preferred by tdirect_bias * lambda in b_decide's choice
+    tdirect_bias: int = int(os.environ.get("MIVC_TDIRECT_BIAS", 0))
     trellis_lambda: float = float(os.environ.get("MIVC_TRELLIS_LAMBDA", 1.0))
     # deblock non-reference B pictures even when neither metrics nor the reconstruction
     # are requested (x264 --full-recon); the bitstream does not depend on it
@@ -569,7 +571,8 @@ class GpuH264Encoder:
                                   P(self.me_cost1), P(self.pred), P(self.pred1), P(self.pm0), P(self.pm1),
                                   P(self.dmv), P(self.qp), aq, P(hdr), P(self.pred_b), P(self.cost_b), s, w1s,
                                   P(self.dref) if nr > 1 else 0, r0y, r0h, 0, int(self.p.eff_partitions() and self.p.bpartitions),
-                                  int(bg != 0), int(self.p.direct == "spatial"))
+                                  int(bg != 0), int(self.p.direct == "spatial"),
+                                  int(self.p.tdirect_bias) if self.p.direct != "spatial" else 0)
             if cut is not None:
                 self.intra_cost.masked_fill_(cut[:, None], -1)
             if self.p.direct == "spatial":
