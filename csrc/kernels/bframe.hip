@@ -302,7 +302,13 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   // mb_type / motion bits (CABAC-ish): direct "0"; L0 / L1 "10x"; Bi "110000" + two mvds
   const int c_direct = satd_direct + lambda * 1;
   if (donly) {
-    if (lane == 0) a.cost_out[o] = c_direct;
+    // spatial direct: only MBs whose co-located motion is static in every quadrant (temporal
+    // direct vectors within +-1, refIdxL0 0) may skip the searches -- there spatial direct
+    // predicts zero motion too (colZeroFlag); elsewhere it is unknown before the wavefront
+    bool stat = drw == 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) stat = stat && dm[k] >= -1 && dm[k] <= 1;
+    if (lane == 0) a.cost_out[o] = (a.spatial && !stat) ? kNoCostB : c_direct;
     return;
   }
   const int c_l0 = a.cost0[o] + lambda * 3;
@@ -443,13 +449,36 @@ __device__ __forceinline__ NbMv16 nb16(const MbHeader* h, bool avail, bool intra
 
 __device__ __forceinline__ int med3i(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
 
+constexpr int kSpatialMaxCols = 480;  // MB columns (8K)
 constexpr int kSpatialWaves = 16;  // 16 row chains per slot: the chain (wmb + 2 hmb MBs) bounds it, not the MB count
 
+// packed motion of one quadrant and list: ref (low 8 bits, signed) | mvx << 8 (12 bits) |
+// mvy << 20 -- the encoder's vectors stay within +-2048 quarter samples
+__device__ __forceinline__ int pk_ref(int v) { return static_cast<int8_t>(v & 255); }
+__device__ __forceinline__ int pk_mx(int v) { return (v << 12) >> 20; }
+__device__ __forceinline__ int pk_my(int v) { return v >> 20; }
+
+__device__ __forceinline__ NbMv16 nb_packed(bool avail, bool intra, int v) {
+  NbMv16 n{avail, -1, {0, 0}};
+  if (!avail || intra) return n;
+  n.ref = pk_ref(v);
+  if (n.ref >= 0) {
+    n.mv[0] = pk_mx(v);
+    n.mv[1] = pk_my(v);
+  }
+  return n;
+}
+
+// The row above hands its final motion on through LDS, never through global memory: per MB
+// column the intra flag and the bottom quadrants (2, 3) of both lists, double-buffered by row
+// parity (row y + 1 overwrites column x of row y - 1's entries only after row y has passed
+// column x + 1, the last step that reads it).  The left neighbour stays in registers.
 __global__ __launch_bounds__(64 * kSpatialWaves) void b_spatial_decide(BSpatialArgs a) {
   const Geom& g = a.g;
   const int slot = blockIdx.x, nmb = g.nmb();
   __shared__ int prog[kMaxRows];
   __shared__ int s_res[kSpatialWaves][256];
+  __shared__ int nbq[2][kSpatialMaxCols][5];  // [row parity][column]: intra, L0 q2, L0 q3, L1 q2, L1 q3
   for (int i = threadIdx.x; i < g.hmb; i += blockDim.x) prog[i] = 0;
   __syncthreads();
   const int w = wave_id(), lane = lane_id();
@@ -462,26 +491,38 @@ __global__ __launch_bounds__(64 * kSpatialWaves) void b_spatial_decide(BSpatialA
   const int* IC = a.intra_cost + static_cast<size_t>(slot) * nmb;
   int* CB = a.cost + static_cast<size_t>(slot) * nmb;
   int* res = s_res[w];
-  auto is_intra = [&](int m) { return IC[m] < CB[m]; };
   const int lam_base = a.qp[slot];
   for (int y = w; y < g.hmb; y += kSpatialWaves) {
+    int* cur_row = &nbq[y & 1][0][0];
+    const int* up_row = &nbq[(y & 1) ^ 1][0][0];
+    int left_intra = 0, left_q1[2] = {0, 0};  // lane 0: the left MB's intra flag / quadrant 1
     for (int x = 0; x < g.wmb; ++x) {
-      if (y > 0) row_wait(prog, y - 1, min(x + 2, g.wmb), a.err);
       const int mb = y * g.wmb + x;
-      // lane 0 derives (it alone reads / writes the records, so its own earlier stores order
-      // the left neighbour; the row above arrives through row_wait); packed per quadrant and
-      // list: ref (low 8 bits, signed) | mvx << 8 (12 bits) | mvy << 20 -- mvs fit +-2048
+      const size_t o = static_cast<size_t>(slot) * nmb + mb;
+      // chain-independent inputs first (in flight during the wait)
+      const int ic = __builtin_amdgcn_readfirstlane(IC[mb]);
+      const int cost_e = __builtin_amdgcn_readfirstlane(CB[mb]);
+      const int forced = __builtin_amdgcn_readfirstlane(static_cast<int>(H[mb].kind == h264::MBK_BDIRECT));
+      const int lambda = h264::kLambda[clampi(lam_base + (a.aq ? a.aq[o] : 0), 0, 51)];
+      const MbHeader& c = C0[mb];
+      const uint2 cref = *reinterpret_cast<const uint2*>(&c.ref[0][0]);  // ref[2][4]
+      const uint4 cmv = *reinterpret_cast<const uint4*>(&c.mv[0][0][0]);  // list-0 vectors
+      const int ckind = c.kind;
+      const int X = x * 16 + c0, Y = y * 16 + r;
+      const uint32_t src = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y) * W + X);
+      if (y > 0) row_wait_lds(prog, y - 1, min(x + 2, g.wmb), a.err);
       int pk[4][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
-      int forced = 0;  // b_decide left the MB direct (unsearched): no explicit candidate exists
       if (lane == 0) {
-        forced = H[mb].kind == h264::MBK_BDIRECT;
         const bool aA = x > 0, aB = y > 0, aC = y > 0 && x + 1 < g.wmb, aD = x > 0 && y > 0;
+        const int* uB = up_row + x * 5;
+        const int* uC = up_row + (x + 1) * 5;
+        const int* uD = up_row + (x - 1) * 5;
         int refs[2], pmv[2][2] = {{0, 0}, {0, 0}};
         for (int l = 0; l < 2; ++l) {
-          NbMv16 A = nb16(&H[mb - 1], aA, aA && is_intra(mb - 1), l, 1);
-          NbMv16 B = nb16(&H[mb - g.wmb], aB, aB && is_intra(mb - g.wmb), l, 2);
-          NbMv16 C = aC ? nb16(&H[mb - g.wmb + 1], true, is_intra(mb - g.wmb + 1), l, 2)
-                        : nb16(&H[mb - g.wmb - 1], aD, aD && is_intra(mb - g.wmb - 1), l, 3);
+          NbMv16 A = nb_packed(aA, left_intra, left_q1[l]);
+          NbMv16 B = aB ? nb_packed(true, uB[0], uB[1 + 2 * l]) : NbMv16{false, -1, {0, 0}};
+          NbMv16 C = aC ? nb_packed(true, uC[0], uC[1 + 2 * l])
+                        : (aD ? nb_packed(true, uD[0], uD[2 + 2 * l]) : NbMv16{false, -1, {0, 0}});
           auto minpos = [](int p, int qv) { return (p >= 0 && qv >= 0) ? min(p, qv) : max(p, qv); };
           refs[l] = minpos(A.ref, minpos(B.ref, C.ref));
           if (refs[l] < 0) continue;
@@ -501,11 +542,13 @@ __global__ __launch_bounds__(64 * kSpatialWaves) void b_spatial_decide(BSpatialA
           }
         }
         const bool zero = refs[0] < 0 && refs[1] < 0;
-        const MbHeader& c = C0[mb];
-        const bool cintra = h264::mbk_is_intra(c.kind);
+        const bool cintra = h264::mbk_is_intra(ckind);
+        const uint32_t cmw[4] = {cmv.x, cmv.y, cmv.z, cmv.w};
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
-          const bool col_zero = !cintra && c.ref[0][qq] == 0 && abs(c.mv[0][qq][0]) <= 1 && abs(c.mv[0][qq][1]) <= 1;
+          const int cr = static_cast<int8_t>((cref.x >> (8 * qq)) & 255u);
+          const int cx = static_cast<int16_t>(cmw[qq] & 0xFFFFu), cy = static_cast<int16_t>(cmw[qq] >> 16);
+          const bool col_zero = !cintra && cr == 0 && abs(cx) <= 1 && abs(cy) <= 1;
 #pragma unroll
           for (int l = 0; l < 2; ++l) {
             int rf = refs[l], mx = pmv[l][0], my = pmv[l][1];
@@ -527,15 +570,11 @@ __global__ __launch_bounds__(64 * kSpatialWaves) void b_spatial_decide(BSpatialA
           const int v = __builtin_amdgcn_readlane(pk[qq][l], 0);
           if (qq == q) mine[l] = v;
         }
-      const int r0 = static_cast<int8_t>(mine[0] & 255), r1 = static_cast<int8_t>(mine[1] & 255);
-      const int m0x = (mine[0] << 12) >> 20, m0y = mine[0] >> 20;
-      const int m1x = (mine[1] << 12) >> 20, m1y = mine[1] >> 20;
-      const int X = x * 16 + c0, Y = y * 16 + r;
+      const int r0 = pk_ref(mine[0]), r1 = pk_ref(mine[1]);
       uint32_t p0 = 0, p1 = 0;
-      if (r0 >= 0) p0 = mc4(a.ref0k[r0 & 3] + yo, a.hp0k[r0 & 3] + ho, W, Hh, X, Y, m0x, m0y);
-      if (r1 >= 0) p1 = mc4(a.ref1 + yo, a.hp1 + ho, W, Hh, X, Y, m1x, m1y);
+      if (r0 >= 0) p0 = mc4(a.ref0k[r0 & 3] + yo, a.hp0k[r0 & 3] + ho, W, Hh, X, Y, pk_mx(mine[0]), pk_my(mine[0]));
+      if (r1 >= 0) p1 = mc4(a.ref1 + yo, a.hp1 + ho, W, Hh, X, Y, pk_mx(mine[1]), pk_my(mine[1]));
       const uint32_t pw = (r0 >= 0 && r1 >= 0) ? wavg4b(p0, p1, a.w1[r0 & 3]) : (r0 >= 0 ? p0 : p1);
-      const uint32_t src = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y) * W + X);
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         res[r * 16 + c0 + k] = static_cast<int>((src >> (8 * k)) & 255u) - static_cast<int>((pw >> (8 * k)) & 255u);
@@ -552,13 +591,38 @@ __global__ __launch_bounds__(64 * kSpatialWaves) void b_spatial_decide(BSpatialA
       }
       satd = __builtin_amdgcn_readlane(sum16(satd), 0);
       wave_sync();  // res is rewritten by the next MB
-      const size_t o = static_cast<size_t>(slot) * nmb + mb;
-      const int lambda = h264::kLambda[clampi(lam_base + (a.aq ? a.aq[o] : 0), 0, 51)];
       const int cost_d = satd + lambda;
-      const int cost_e = __builtin_amdgcn_readfirstlane(CB[mb]);
-      if (__builtin_amdgcn_readlane(forced, 0) || cost_d <= cost_e + a.bias * lambda) {
-        *reinterpret_cast<uint32_t*>(a.pred_out + o * 256 + r * 16 + c0) = pw;
-        if (lane == 0) {
+      const bool take = forced || cost_d <= cost_e + a.bias * lambda;
+      const int final_cost = take ? cost_d : cost_e;
+      const bool intra = ic < final_cost;  // encode_inter's rule
+      if (take) *reinterpret_cast<uint32_t*>(a.pred_out + o * 256 + r * 16 + c0) = pw;
+      if (lane == 0) {
+        // this MB's final motion: the direct one, else the explicit record b_decide wrote
+        int fin[4][2];
+        if (take) {
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            fin[qq][0] = pk[qq][0];
+            fin[qq][1] = pk[qq][1];
+          }
+        } else {
+          const MbHeader& h = H[mb];
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+            for (int l = 0; l < 2; ++l)
+              fin[qq][l] = (h.ref[l][qq] & 255) | ((h.mv[l][qq][0] & 4095) << 8) | (h.mv[l][qq][1] << 20);
+        }
+        int* e = cur_row + x * 5;
+        e[0] = intra;
+        e[1] = fin[2][0];
+        e[2] = fin[3][0];
+        e[3] = fin[2][1];
+        e[4] = fin[3][1];
+        left_intra = intra;
+        left_q1[0] = fin[1][0];
+        left_q1[1] = fin[1][1];
+        if (take) {
           MbHeader& h = H[mb];
           h.kind = h264::MBK_BDIRECT;
           h.sub_direct = 0;
@@ -566,15 +630,14 @@ __global__ __launch_bounds__(64 * kSpatialWaves) void b_spatial_decide(BSpatialA
           for (int qq = 0; qq < 4; ++qq)
 #pragma unroll
             for (int l = 0; l < 2; ++l) {
-              const int v = pk[qq][l];
-              h.ref[l][qq] = static_cast<int8_t>(v & 255);
-              h.mv[l][qq][0] = static_cast<int16_t>((v << 12) >> 20);
-              h.mv[l][qq][1] = static_cast<int16_t>(v >> 20);
+              h.ref[l][qq] = static_cast<int8_t>(pk_ref(pk[qq][l]));
+              h.mv[l][qq][0] = static_cast<int16_t>(pk_mx(pk[qq][l]));
+              h.mv[l][qq][1] = static_cast<int16_t>(pk_my(pk[qq][l]));
             }
           CB[mb] = cost_d;
         }
       }
-      row_publish(prog, y, x + 1);
+      row_publish_lds(prog, y, x + 1);
     }
   }
 }

@@ -205,7 +205,7 @@ PYBIND11_MODULE(_hip, m) {
     const size_t n = ref0k.size();
     if (n < 1 || n > 4 || hp0k.size() != n || w1.size() != n)
       throw std::invalid_argument("b_spatial: 1..4 list-0 pictures with planes and weights");
-    if (hmb > 272) throw std::invalid_argument("b_spatial: at most 272 MB rows");
+    if (hmb > 272 || wmb > 480) throw std::invalid_argument("b_spatial: at most 272 MB rows and 480 columns");
     const uint8_t* rk[4];
     const uint8_t* hk[4];
     for (size_t i = 0; i < n; ++i) {

@@ -116,6 +116,8 @@ class H264Params:
     direct: str = os.environ.get("MIVC_DIRECT", "temporal")
     # spatial direct: direct is taken when its cost <= the explicit candidate's + direct_bias * lambda
     direct_bias: int = int(os.environ.get("MIVC_DIRECT_BIAS", 8))
+    # spatial direct: the B gate skips the searches of MBs with static co-located motion only
+    spatial_gate: bool = os.environ.get("MIVC_SPATIAL_GATE", "1") != "0"
     # temporal direct: B_Direct_16x16 preferred by tdirect_bias * lambda in b_decide's choice
     tdirect_bias: int = int(os.environ.get("MIVC_TDIRECT_BIAS", 0))
     trellis_lambda: float = float(os.environ.get("MIVC_TRELLIS_LAMBDA", 1.0))
@@ -549,8 +551,9 @@ class GpuH264Encoder:
                     xv.append(P(rk[2]))
             self.intra_count.zero_()
             br = self.p.b_me_range
-            # spatial direct cannot be priced before the wavefront, so it searches every MB
-            bg = int(self.p.b_gate) if self.p.direct != "spatial" else 0
+            # spatial direct cannot be priced before the wavefront: its gate passes static MBs only
+            spatial = int(self.p.direct == "spatial")
+            bg = int(self.p.b_gate) if not spatial or self.p.spatial_gate else 0
             with st("me_b"):
                 self.hip.b_direct(B, wmb, hmb, P(self.col_hdr), dsfs, copies, P(self.dmv), P(self.pm0), P(self.pm1), s,
                                   P(self.dref) if nr > 1 else 0)
@@ -558,7 +561,7 @@ class GpuH264Encoder:
                     self.hip.b_decide(B, wmb, hmb, sy, f0y, f1y, hp0, hp1, P(self.mv), P(self.mv1), P(self.me_cost),
                                       P(self.me_cost1), P(self.pred), P(self.pred1), P(self.pm0), P(self.pm1),
                                       P(self.dmv), P(self.qp), aq, P(hdr), P(self.pred_b), P(self.cost_b), s, w1s,
-                                      P(self.dref) if nr > 1 else 0, r0y, r0h, 1)
+                                      P(self.dref) if nr > 1 else 0, r0y, r0h, 1, spatial=spatial)
                 gate = P(self.cost_b) if bg != 0 else 0
                 self.hip.me(B, wmb, hmb, sy, f0y, P(self.pm0), P(self.mv), P(self.me_cost), P(self.pred),
                             P(self.intra_cost), P(self.qp), br, self.p.subpel, s, hp0, aq, 1, self.p.b_early_sad,
