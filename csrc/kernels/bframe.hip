@@ -473,47 +473,62 @@ __device__ __forceinline__ NbMv16 nb_packed(bool avail, bool intra, int v) {
 // column the intra flag and the bottom quadrants (2, 3) of both lists, double-buffered by row
 // parity (row y + 1 overwrites column x of row y - 1's entries only after row y has passed
 // column x + 1, the last step that reads it).  The left neighbour stays in registers.
+// Each wave runs two MB rows in lock step (half-waves: row 2w + 32k in lanes 0..31, the row
+// below in lanes 32..63 two MBs behind), 8 samples per lane, so 16 waves cover 32 rows and
+// the per-wave serial work (not the wavefront chain) stops bounding the kernel.
 __global__ __launch_bounds__(64 * kSpatialWaves) void b_spatial_decide(BSpatialArgs a) {
   const Geom& g = a.g;
   const int slot = blockIdx.x, nmb = g.nmb();
   __shared__ int prog[kMaxRows];
-  __shared__ int s_res[kSpatialWaves][256];
+  __shared__ int s_res[kSpatialWaves][2][256];
   __shared__ int nbq[2][kSpatialMaxCols][5];  // [row parity][column]: intra, L0 q2, L0 q3, L1 q2, L1 q3
   for (int i = threadIdx.x; i < g.hmb; i += blockDim.x) prog[i] = 0;
   __syncthreads();
   const int w = wave_id(), lane = lane_id();
-  const int r = lane >> 2, c0 = (lane & 3) * 4, q = (r >> 3) * 2 + (c0 >> 3);
-  const int W = g.W, Hh = g.H;
+  const int half = lane >> 5, hl = lane & 31;
+  const int r = hl >> 1, c0 = (hl & 1) * 8, q = (r >> 3) * 2 + (c0 >> 3);
+  const int W = g.W, Hh = g.H, wmb = g.wmb, hmb = g.hmb;
   const size_t yo = static_cast<size_t>(slot) * g.ysize();
   const size_t ho = static_cast<size_t>(slot) * 3 * (W + 2 * kHpMargin) * (Hh + 2 * kHpMargin);
   MbHeader* H = a.hdr + static_cast<size_t>(slot) * nmb;
   const MbHeader* C0 = a.col + static_cast<size_t>(slot) * nmb;
   const int* IC = a.intra_cost + static_cast<size_t>(slot) * nmb;
   int* CB = a.cost + static_cast<size_t>(slot) * nmb;
-  int* res = s_res[w];
+  int* res = s_res[w][half];
   const int lam_base = a.qp[slot];
-  for (int y = w; y < g.hmb; y += kSpatialWaves) {
+  for (int yu = 2 * w; yu < hmb; yu += 2 * kSpatialWaves) {
+    const int y = yu + half;
+    const bool row_ok = y < hmb;
     int* cur_row = &nbq[y & 1][0][0];
     const int* up_row = &nbq[(y & 1) ^ 1][0][0];
-    int left_intra = 0, left_q1[2] = {0, 0};  // lane 0: the left MB's intra flag / quadrant 1
-    for (int x = 0; x < g.wmb; ++x) {
-      const int mb = y * g.wmb + x;
+    int left_intra = 0, left_q1[2] = {0, 0};  // lanes 0 / 32: the left MB's intra flag / quadrant 1
+    for (int step = 0; step < wmb + 2; ++step) {
+      const int x = half ? step - 2 : step;
+      const bool act = row_ok && x >= 0 && x < wmb;
+      const int xs = act ? x : 0, ys = act ? y : 0;  // in-range addresses for idle halves
+      const int mb = ys * wmb + xs;
       const size_t o = static_cast<size_t>(slot) * nmb + mb;
       // chain-independent inputs first (in flight during the wait)
-      const int ic = __builtin_amdgcn_readfirstlane(IC[mb]);
-      const int cost_e = __builtin_amdgcn_readfirstlane(CB[mb]);
-      const int forced = __builtin_amdgcn_readfirstlane(static_cast<int>(H[mb].kind == h264::MBK_BDIRECT));
+      const int ic = IC[mb];
+      const int cost_e = CB[mb];
+      const bool forced = H[mb].kind == h264::MBK_BDIRECT;
+      // b_decide's explicit record (kept when direct loses)
+      const uint2 href = *reinterpret_cast<const uint2*>(&H[mb].ref[0][0]);
+      const uint4 hmv0 = *reinterpret_cast<const uint4*>(&H[mb].mv[0][0][0]);
+      const uint4 hmv1 = *reinterpret_cast<const uint4*>(&H[mb].mv[1][0][0]);
       const int lambda = h264::kLambda[clampi(lam_base + (a.aq ? a.aq[o] : 0), 0, 51)];
       const MbHeader& c = C0[mb];
       const uint2 cref = *reinterpret_cast<const uint2*>(&c.ref[0][0]);  // ref[2][4]
       const uint4 cmv = *reinterpret_cast<const uint4*>(&c.mv[0][0][0]);  // list-0 vectors
       const int ckind = c.kind;
-      const int X = x * 16 + c0, Y = y * 16 + r;
-      const uint32_t src = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y) * W + X);
-      if (y > 0) row_wait_lds(prog, y - 1, min(x + 2, g.wmb), a.err);
+      const int X = xs * 16 + c0, Y = ys * 16 + r;
+      const uint2 src = *reinterpret_cast<const uint2*>(a.src_y + yo + static_cast<size_t>(Y) * W + X);
+      // the upper row waits on the row above (the previous wave's lower row); the lower row's
+      // dependency, the upper half two MBs ahead, is met by the lock step
+      if (yu > 0) row_wait_lds(prog, yu - 1, min(step + 2, wmb), a.err);
       int pk[4][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
-      if (lane == 0) {
-        const bool aA = x > 0, aB = y > 0, aC = y > 0 && x + 1 < g.wmb, aD = x > 0 && y > 0;
+      if (hl == 0 && act) {
+        const bool aA = x > 0, aB = y > 0, aC = y > 0 && x + 1 < wmb, aD = x > 0 && y > 0;
         const int* uB = up_row + x * 5;
         const int* uC = up_row + (x + 1) * 5;
         const int* uD = up_row + (x - 1) * 5;
@@ -567,21 +582,27 @@ __global__ __launch_bounds__(64 * kSpatialWaves) void b_spatial_decide(BSpatialA
       for (int qq = 0; qq < 4; ++qq)
 #pragma unroll
         for (int l = 0; l < 2; ++l) {
-          const int v = __builtin_amdgcn_readlane(pk[qq][l], 0);
-          if (qq == q) mine[l] = v;
+          const int vu = __builtin_amdgcn_readlane(pk[qq][l], 0), vl = __builtin_amdgcn_readlane(pk[qq][l], 32);
+          if (qq == q) mine[l] = half ? vl : vu;
         }
       const int r0 = pk_ref(mine[0]), r1 = pk_ref(mine[1]);
-      uint32_t p0 = 0, p1 = 0;
-      if (r0 >= 0) p0 = mc4(a.ref0k[r0 & 3] + yo, a.hp0k[r0 & 3] + ho, W, Hh, X, Y, pk_mx(mine[0]), pk_my(mine[0]));
-      if (r1 >= 0) p1 = mc4(a.ref1 + yo, a.hp1 + ho, W, Hh, X, Y, pk_mx(mine[1]), pk_my(mine[1]));
-      const uint32_t pw = (r0 >= 0 && r1 >= 0) ? wavg4b(p0, p1, a.w1[r0 & 3]) : (r0 >= 0 ? p0 : p1);
+      uint32_t pw[2];
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        res[r * 16 + c0 + k] = static_cast<int>((src >> (8 * k)) & 255u) - static_cast<int>((pw >> (8 * k)) & 255u);
+      for (int k = 0; k < 2; ++k) {
+        uint32_t p0 = 0, p1 = 0;
+        if (r0 >= 0) p0 = mc4(a.ref0k[r0 & 3] + yo, a.hp0k[r0 & 3] + ho, W, Hh, X + 4 * k, Y, pk_mx(mine[0]), pk_my(mine[0]));
+        if (r1 >= 0) p1 = mc4(a.ref1 + yo, a.hp1 + ho, W, Hh, X + 4 * k, Y, pk_mx(mine[1]), pk_my(mine[1]));
+        pw[k] = (r0 >= 0 && r1 >= 0) ? wavg4b(p0, p1, a.w1[r0 & 3]) : (r0 >= 0 ? p0 : p1);
+      }
+      const uint32_t sw[2] = {src.x, src.y};
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        res[r * 16 + c0 + k] = static_cast<int>((sw[k >> 2] >> (8 * (k & 3))) & 255u) -
+                               static_cast<int>((pw[k >> 2] >> (8 * (k & 3))) & 255u);
       wave_sync();
       int satd = 0;
-      if (lane < 16) {
-        const int bx = (lane & 3) * 4, by = (lane >> 2) * 4;
+      if (hl < 16) {  // block hl of this half's MB; rows of 16 lanes sum below
+        const int bx = (hl & 3) * 4, by = (hl >> 2) * 4;
         int rr[16];
 #pragma unroll
         for (int yy = 0; yy < 4; ++yy)
@@ -589,14 +610,14 @@ __global__ __launch_bounds__(64 * kSpatialWaves) void b_spatial_decide(BSpatialA
           for (int xx = 0; xx < 4; ++xx) rr[yy * 4 + xx] = res[(by + yy) * 16 + bx + xx];
         satd = h264::satd4x4(rr);
       }
-      satd = __builtin_amdgcn_readlane(sum16(satd), 0);
-      wave_sync();  // res is rewritten by the next MB
-      const int cost_d = satd + lambda;
-      const bool take = forced || cost_d <= cost_e + a.bias * lambda;
+      const int ssum = sum16(satd);
+      const int su = __builtin_amdgcn_readlane(ssum, 0), sl = __builtin_amdgcn_readlane(ssum, 32);
+      const int cost_d = (half ? sl : su) + lambda;
+      const bool take = act && (forced || cost_d <= cost_e + a.bias * lambda);
       const int final_cost = take ? cost_d : cost_e;
       const bool intra = ic < final_cost;  // encode_inter's rule
-      if (take) *reinterpret_cast<uint32_t*>(a.pred_out + o * 256 + r * 16 + c0) = pw;
-      if (lane == 0) {
+      if (take) *reinterpret_cast<uint2*>(a.pred_out + o * 256 + r * 16 + c0) = make_uint2(pw[0], pw[1]);
+      if (hl == 0 && act) {
         // this MB's final motion: the direct one, else the explicit record b_decide wrote
         int fin[4][2];
         if (take) {
@@ -606,12 +627,15 @@ __global__ __launch_bounds__(64 * kSpatialWaves) void b_spatial_decide(BSpatialA
             fin[qq][1] = pk[qq][1];
           }
         } else {
-          const MbHeader& h = H[mb];
+          const uint32_t hm[2][4] = {{hmv0.x, hmv0.y, hmv0.z, hmv0.w}, {hmv1.x, hmv1.y, hmv1.z, hmv1.w}};
+          const uint32_t hr[2] = {href.x, href.y};
 #pragma unroll
           for (int qq = 0; qq < 4; ++qq)
 #pragma unroll
-            for (int l = 0; l < 2; ++l)
-              fin[qq][l] = (h.ref[l][qq] & 255) | ((h.mv[l][qq][0] & 4095) << 8) | (h.mv[l][qq][1] << 20);
+            for (int l = 0; l < 2; ++l) {
+              const int mx = static_cast<int16_t>(hm[l][qq] & 0xFFFFu), my = static_cast<int16_t>(hm[l][qq] >> 16);
+              fin[qq][l] = static_cast<int>((hr[l] >> (8 * qq)) & 255u) | ((mx & 4095) << 8) | (my << 20);
+            }
         }
         int* e = cur_row + x * 5;
         e[0] = intra;
@@ -637,7 +661,11 @@ __global__ __launch_bounds__(64 * kSpatialWaves) void b_spatial_decide(BSpatialA
           CB[mb] = cost_d;
         }
       }
-      row_publish_lds(prog, y, x + 1);
+      // publish: the lower half's own next step reads the upper half's LDS entries in program
+      // order; the next wave's upper row waits on this wave's lower row (prog)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+      wave_sync();
+      if (hl == 0 && act) __hip_atomic_store(prog + y, x + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
 }
