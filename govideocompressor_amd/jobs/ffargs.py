@@ -192,8 +192,8 @@ H264_PARAMS = {
     "weightb": ("weightb", _flag),
     "no-weightb": ("weightb", lambda v: not _flag(v)),
     "trellis": ("trellis", lambda v: int(_int_in(0, 2)(v) > 0)),
-    # direct=spatial: decided in an MB wavefront (bframe.hip b_spatial_decide), -2.2 % BD-rate
-    # and ~35 % fewer frames/s than temporal on the benchmark content (profiles/r3_direct_rd.md)
+    # direct=spatial: decided in an MB wavefront (bframe.hip b_spatial_decide), -1.9 % BD-rate
+    # and ~26 % fewer frames/s than temporal on the benchmark content (profiles/r3_direct_rd.md)
     "direct": ("direct", _only("temporal", "spatial")),
     "b-adapt": ("@b-adapt", _only("0")),
     "b-pyramid": ("@b-pyramid", _only("none")),
