@@ -119,7 +119,8 @@ class H264Params:
     # spatial direct: the B gate skips the searches of MBs with static co-located motion only
     spatial_gate: bool = os.environ.get("MIVC_SPATIAL_GATE", "1") != "0"
     # temporal direct: B_Direct_16x16 preferred by tdirect_bias * lambda in b_decide's choice
-    tdirect_bias: int = int(os.environ.get("MIVC_TDIRECT_BIAS", 0))
+    # (-0.36 % BD-rate at 8, profiles/r3_direct_rd.md)
+    tdirect_bias: int = int(os.environ.get("MIVC_TDIRECT_BIAS", 8))
     trellis_lambda: float = float(os.environ.get("MIVC_TRELLIS_LAMBDA", 1.0))
     # deblock non-reference B pictures even when neither metrics nor the reconstruction
     # are requested (x264 --full-recon); the bitstream does not depend on it
