@@ -365,9 +365,12 @@ void parse_pps(BitReader& br, Pps& p, const Sps* sps_by_id[16]) {
   p.extra_bits = br.get(3);
   p.sign_hiding = br.get(1);
   p.cabac_init_present = br.get(1);
-  p.num_ref_l0 = static_cast<int>(br.get_ue()) + 1;
-  p.num_ref_l1 = static_cast<int>(br.get_ue()) + 1;
-  if (p.num_ref_l0 > 15 || p.num_ref_l1 > 15) fail("num_ref_idx_default_active out of range");
+  {
+    const uint32_t n0 = br.get_ue(), n1 = br.get_ue();  // bounded before the +1 (no wrap)
+    if (n0 > 14 || n1 > 14) fail("num_ref_idx_default_active out of range");
+    p.num_ref_l0 = static_cast<int>(n0) + 1;
+    p.num_ref_l1 = static_cast<int>(n1) + 1;
+  }
   p.init_qp = 26 + br.get_se();
   p.constrained_intra = br.get(1);
   p.transform_skip = br.get(1);
@@ -510,10 +513,19 @@ void parse_slice_header(BitReader& br, int nal_type, const Sps* const* sps_tab, 
       h.num_ref[0] = pps.num_ref_l0;
       h.num_ref[1] = h.slice_type == 0 ? pps.num_ref_l1 : 0;
       if (br.get(1)) {  // num_ref_idx_active_override_flag
-        h.num_ref[0] = static_cast<int>(br.get_ue()) + 1;
-        if (h.slice_type == 0) h.num_ref[1] = static_cast<int>(br.get_ue()) + 1;
+        // num_ref_idx_lX_active_minus1 is 0..14 (7.4.7.1): bound the raw ue(v) before the +1 so
+        // a huge value cannot wrap into a zero or negative count
+        const uint32_t n0 = br.get_ue();
+        if (n0 > 14) fail("num_ref_idx_l0_active_minus1 out of range");
+        h.num_ref[0] = static_cast<int>(n0) + 1;
+        if (h.slice_type == 0) {
+          const uint32_t n1 = br.get_ue();
+          if (n1 > 14) fail("num_ref_idx_l1_active_minus1 out of range");
+          h.num_ref[1] = static_cast<int>(n1) + 1;
+        }
       }
-      if (h.num_ref[0] > 15 || h.num_ref[1] > 15) fail("num_ref_idx_active out of range");
+      if (h.num_ref[0] < 1 || h.num_ref[0] > 15 || h.num_ref[1] < 0 || h.num_ref[1] > 15)
+        fail("num_ref_idx_active out of range");
       if (npc == 0) fail("P / B slice without reference pictures");
       if (pps.lists_modification && npc > 1) {
         const int bits = ceil_log2(npc);

@@ -250,9 +250,10 @@ class GpuBackend:
                 self._decoder[codec] = GpuH264Decoder(self.device)
         return self._decoder[codec]
 
-    def decode_streams(self, streams: list[bytes], fps: float = 30.0):
-        """Annex-B segments (H.264 and / or HEVC) -> device-resident 8-bit clips
-        (``DecodedSegment``), one batched call per codec."""
+    def decode_streams(self, streams: list[bytes], fps: float = 30.0, keep_high_bit: bool = False):
+        """Annex-B segments (H.264 and / or HEVC) -> device-resident clips (``DecodedSegment``),
+        one batched call per codec.  Main 10 pictures are rounded to 8 bits (yuv.to_8bit) unless
+        ``keep_high_bit`` (a Main 10 output: the HEVC encoder takes the 10-bit samples as they are)."""
         from ..segment.probe import codec_of
         import torch
         out = [None] * len(streams)
@@ -266,15 +267,13 @@ class GpuBackend:
             for k, v in dec.stats.items():
                 self.decode_stats[k] = self.decode_stats.get(k, 0) + v
             for i, d in zip(idxs, got):
-                if d.y.dtype != torch.uint8:  # Main 10 input: the encoders take 8-bit frames
+                if d.y.dtype != torch.uint8 and not keep_high_bit:  # Main 10 input, 8-bit output
                     from ..models.h264_decode_gpu import DecodedSegment
-                    sh = 2
-                    d = DecodedSegment((d.y >> sh).to(torch.uint8), (d.u >> sh).to(torch.uint8),
-                                       (d.v >> sh).to(torch.uint8), d.fps, d.path)
+                    d = DecodedSegment(yuv.to_8bit(d.y), yuv.to_8bit(d.u), yuv.to_8bit(d.v), d.fps, d.path)
                 out[i] = d
         return out
 
-    def _load_compressed(self, jobs: list[PieceJob]) -> dict[str, object]:
+    def _load_compressed(self, jobs: list[PieceJob], keep_high_bit: bool = False) -> dict[str, object]:
         """Compressed pieces (.264 / .265 / .mp4: H.264 CAVLC or CABAC I/P/B High, HEVC Main /
         Main 10) decode together on the GPU."""
         from ..ops import native
@@ -287,7 +286,7 @@ class GpuBackend:
             fps = info["fps"] or fps
             streams.append(st)
             keys.append(j.idx)
-        return dict(zip(keys, self.decode_streams(streams, fps)))
+        return dict(zip(keys, self.decode_streams(streams, fps, keep_high_bit)))
 
     def transcode(self, jobs: list[PieceJob], cfg: EncoderConfig) -> list[PieceResult]:
         from ..segment.probe import kind_of
@@ -300,7 +299,8 @@ class GpuBackend:
         futs = {j.idx: self._io.submit(load_clip, j.in_path) for j in raw}
         if comp:
             try:
-                dec = self._load_compressed(comp)
+                # -pix_fmt yuv420p10le with libx265: Main 10 in, Main 10 out (no 8-bit detour)
+                dec = self._load_compressed(comp, keep_high_bit=cfg.codec == "hevc" and cfg.bit_depth == 10)
                 items += [(j.idx, dec[j.idx]) for j in comp]
             except Exception as e:  # noqa: BLE001 - reported to the coordinator
                 for j in comp:
@@ -348,8 +348,9 @@ class GpuBackend:
         F = max(c for *_, c in chunk)
         t0 = time.perf_counter()
         if isinstance(clips[chunk[0][0]].y, torch.Tensor):  # device-resident (GPU-decoded) clips
-            dy = torch.empty((B, F, h, w), dtype=torch.uint8, device=self.device)
-            du = torch.empty((B, F, h // 2, w // 2), dtype=torch.uint8, device=self.device)
+            dt = clips[chunk[0][0]].y.dtype  # uint8, or int16 Main 10 samples kept for a Main 10 encode
+            dy = torch.empty((B, F, h, w), dtype=dt, device=self.device)
+            du = torch.empty((B, F, h // 2, w // 2), dtype=dt, device=self.device)
             dv = torch.empty_like(du)
             for b, (key, _, s, c) in enumerate(chunk):
                 cl = clips[key]

@@ -68,9 +68,10 @@ class H264Params:
     # entropy coder: CABAC (x264's default; Main profile) or CAVLC (Constrained Baseline)
     cabac: bool = True
     # x264 --bframes 3: B pictures between P anchors (non-reference, temporal direct); CABAC
-    # only (the Baseline CAVLC path has no B slices).  b_qp_offset: x264 --pbratio 1.3
+    # only (the Baseline CAVLC path has no B slices).  b_qp_offset: x264 --pbratio 1.3 as a QP
+    # offset (6 log2 1.3 = 2.27) over the distance-weighted QP of the B picture's references
     bframes: int = 3
-    b_qp_offset: int = 2
+    b_qp_offset: float = 6.0 * math.log2(1.3)
     # integer search radius of the two B-picture searches (their predictors are the scaled
     # co-located vectors of temporal direct, so a small window suffices)
     b_me_range: int = int(os.environ.get("MIVC_B_ME_RANGE", 4))
@@ -895,7 +896,8 @@ class GpuH264Encoder:
         else:
             costs = self._la.frame_costs(y).cpu().numpy()
         self._scenecuts = scenecut_flags(costs, float(self.p.scenecut))
-        q = crf_qps_batch(costs, float(self.p.crf), lbw * lbh, scenecuts=self._scenecuts, mbtree=use_mbtree)
+        q = crf_qps_batch(costs, float(self.p.crf), lbw * lbh, scenecuts=self._scenecuts, mbtree=use_mbtree,
+                          bframes=self.nb)
         self.stats["scenecuts"] = int(self._scenecuts.sum())
         self.timings["lookahead_s"] = self.timings.get("lookahead_s", 0.0) + time.perf_counter() - t0
         self.stats["mean_qp"] = float(q.mean())
@@ -976,9 +978,10 @@ class GpuH264Encoder:
         else:
             qps_h = np.clip(np.asarray(qps, dtype=np.int32).reshape(B, F), 0, 51)
         if self.nb and (qps is None or self._from_la):
-            # B pictures one pbratio step above their anchors (x264 --pbratio 1.3 = +2 QP)
-            bd = [pic.d for pic in plan if pic.kind == "B"]
-            qps_h[:, bd] = np.minimum(qps_h[:, bd] + int(self.p.b_qp_offset), 51)
+            # B pictures: no rate control of their own, the distance-weighted QP of their
+            # references + pbratio (x264 / x265 CRF and constant-QP rule)
+            from ..rc.ratecontrol import b_qps_from_refs
+            qps_h = b_qps_from_refs(qps_h, plan, float(self.p.b_qp_offset))
         if qp_delta is not None:
             from ..rc.abr import apply_delta
             qps_h = apply_delta(qps_h, qp_delta)

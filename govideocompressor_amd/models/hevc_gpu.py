@@ -327,7 +327,7 @@ class GpuHevcEncoder:
             costs = self._la.frame_costs(y8.contiguous()).cpu().numpy()
         self._scenecuts = scenecut_flags(costs, float(self.p.scenecut), keyint=self.p.keyint or None)
         q = crf_qps_batch(costs, float(self.p.crf), lbw * lbh, keyint=self.p.keyint or None,
-                          scenecuts=self._scenecuts, mbtree=use_tree)
+                          scenecuts=self._scenecuts, mbtree=use_tree, bframes=self.nb)
         self.stats["scenecuts"] = int(self._scenecuts.sum())
         self.timings["lookahead_s"] = self.timings.get("lookahead_s", 0.0) + time.perf_counter() - t0
         return q
@@ -454,11 +454,10 @@ class GpuHevcEncoder:
             cfg["threads"] = max(1, min(32, self.entropy_threads // max(1, B)))
         qps = np.clip(np.asarray(qps, dtype=np.int32).reshape(B, F), 0, 51)
         if self.nb and from_la:
-            # x265 --pbratio: B pictures above their anchors; a pyramid's reference B halfway
-            bo = int(self.p.b_qp_offset)
-            for pic in plan:
-                if pic.kind == "B":
-                    qps[:, pic.d] = np.minimum(qps[:, pic.d] + (bo // 2 if pic.ref else bo), 51)
+            # x265 --pbratio: a B picture takes the distance-weighted QP of its references plus
+            # the offset (half of it for a pyramid's reference B)
+            from ..rc.ratecontrol import b_qps_from_refs
+            qps = b_qps_from_refs(qps, plan, float(self.p.b_qp_offset))
         if qp_delta is not None:
             from ..rc.abr import apply_delta
             qps = apply_delta(qps, qp_delta)

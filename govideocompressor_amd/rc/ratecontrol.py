@@ -31,6 +31,16 @@ import numpy as np
 
 QCOMP = 0.6
 IP_OFFSET = 3          # I-frame QP = P QP - 3 (ipratio 1.4)
+# x264 / x265 --pbratio 1.3 and --ipratio 1.4 as QP offsets (6 log2 ratio)
+PB_OFFSET = 6.0 * math.log2(1.3)
+IP_OFFSET_F = 6.0 * math.log2(1.4)
+
+
+def crf_base_complexity(mb_count: int, bframes: int) -> float:
+    """x264 / x265 CRF reference complexity: ``mb_count * (bframes ? 120 : 80)``.  With B
+    pictures the anchors sit farther apart and cost more, so the constant grows with them;
+    using 80 with B pictures on would code every frame ~1.4 QP coarser than the same CRF."""
+    return float(mb_count) * (120.0 if int(bframes) > 0 else 80.0)
 # x264 ratecontrol.c: with MB-tree the CRF constant is taken (1 - qcomp) * 13.5 QP higher;
 # the (mostly negative) MB-tree offsets bring propagated blocks back down
 MBTREE_CRF_OFFSET = (1.0 - QCOMP) * 13.5
@@ -78,7 +88,7 @@ def frame_complexity(intra: np.ndarray, inter: np.ndarray, keyint: int | None = 
 
 
 def crf_qps(intra: np.ndarray, inter: np.ndarray, crf: float, mb_count: int, keyint: int | None = None,
-            blur: float = 0.5) -> np.ndarray:
+            blur: float = 0.5, bframes: int = 0) -> np.ndarray:
     """Per-frame QPs of a CRF encode of one segment (x264 rc_crf without MB-tree).
 
     ``mb_count`` = 16x16 macroblocks per frame; complexities are per frame lowres SATD
@@ -91,7 +101,7 @@ def crf_qps(intra: np.ndarray, inter: np.ndarray, crf: float, mb_count: int, key
         acc = acc * blur + c
         w = w * blur + 1.0
         blurred[i] = acc / w
-    base = 80.0 * mb_count  # x264: base complexity (shift for a "typical" frame)
+    base = crf_base_complexity(mb_count, bframes)  # x264: complexity of a "typical" frame
     rate_factor = base ** (1.0 - QCOMP) / qp2qscale(crf)
     qs = blurred ** (1.0 - QCOMP) / rate_factor
     qp = np.array([qscale2qp(q) for q in qs])
@@ -123,7 +133,7 @@ def scenecut_flags(costs: np.ndarray, scenecut: float = 40.0, keyint: int | None
 
 def crf_qps_batch(costs: np.ndarray, crf: float, mb_count: int, keyint: int | None = None, blur: float = 0.5,
                   qp_min: int = QP_MIN, qp_max: int = QP_MAX, scenecuts: np.ndarray | None = None,
-                  mbtree: bool = False) -> np.ndarray:
+                  mbtree: bool = False, bframes: int = 0) -> np.ndarray:
     """:func:`crf_qps` for B closed-GOP segments at once.
 
     ``costs``: [B, F, 2] lowres frame costs (intra, min(intra, inter)) as produced by
@@ -146,12 +156,54 @@ def crf_qps_batch(costs: np.ndarray, crf: float, mb_count: int, keyint: int | No
         acc = acc * blur + cplx[:, t]
         wsum = wsum * blur + 1.0
         blurred[:, t] = acc / wsum
-    base = 80.0 * mb_count
+    base = crf_base_complexity(mb_count, bframes)
     rate_factor = base ** (1.0 - QCOMP) / qp2qscale(crf + (MBTREE_CRF_OFFSET if mbtree else 0.0))
     qs = np.maximum(blurred ** (1.0 - QCOMP) / rate_factor, 1e-9)
     qp = 12.0 + 6.0 * np.log2(qs / 0.85)
     qp[key] -= IP_OFFSET
     return np.clip(np.round(qp), max(QP_MIN, qp_min), min(QP_MAX, qp_max)).astype(np.int32)
+
+
+def b_qps_from_refs(qps: np.ndarray, plans, pb_offset: float = PB_OFFSET, ip_offset: float = IP_OFFSET_F,
+                    qp_max: int = QP_MAX) -> np.ndarray:
+    """B-picture QPs from their references, the x264 / x265 CRF rule: a B picture has no rate
+    control of its own, it takes the POC-distance weighted mean QP of its nearest list-0 and
+    list-1 references (an I reference is replaced by the other side, or both I: their mean +
+    ipratio) plus ``pb_offset`` (--pbratio 1.3), half of it for a reference B (b-pyramid),
+    whose own QP is taken ``pb_offset / 2`` lower when it serves as a reference.
+
+    ``qps``: [B, F] display-order QPs (anchors already set); ``plans``: one coding-order plan
+    shared by all slots or a list of per-slot plans; a picture needs ``d``, ``kind``, ``l0``,
+    ``l1`` (display indices of the nearest references) and optionally ``ref``.  Coding order
+    guarantees a B picture's references got their QPs first.  Returns a new int32 array."""
+    q = np.asarray(qps, dtype=np.float64).copy()
+    B = q.shape[0]
+    per_slot = len(plans) == B and len(plans) > 0 and isinstance(plans[0], (list, tuple))
+    for b in range(B):
+        plan = plans[b] if per_slot else plans
+        kind = {pic.d: pic.kind for pic in plan}
+        bref = {pic.d for pic in plan if pic.kind == "B" and getattr(pic, "ref", False)}
+        for pic in plan:
+            if pic.kind != "B":
+                continue
+            d0, d1 = pic.l0, pic.l1
+            q0, q1 = q[b, d0], q[b, d1]
+            if d0 in bref:
+                q0 -= pb_offset / 2
+            if d1 in bref:
+                q1 -= pb_offset / 2
+            i0, i1 = kind.get(d0) == "I", kind.get(d1) == "I"
+            if i0 and i1:
+                v = (q0 + q1) / 2 + ip_offset
+            elif i0:
+                v = q1
+            elif i1:
+                v = q0
+            else:
+                t0, t1 = abs(pic.d - d0), abs(d1 - pic.d)
+                v = (q0 * t1 + q1 * t0) / max(1, t0 + t1)
+            q[b, pic.d] = v + (pb_offset / 2 if pic.d in bref else pb_offset)
+    return np.clip(np.round(q), QP_MIN, qp_max).astype(np.int32)
 
 
 def abr_solve(stats: np.ndarray, target_bits: float, exponent: float = 1.0) -> float:

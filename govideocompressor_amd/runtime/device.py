@@ -47,16 +47,44 @@ def slots_for(width: int, height: int, frames: int, info: DeviceInfo | None, cap
     return max(1, min(cap, by_mem, max(info.cus, 1)))
 
 
+def cgroup_mem_limit() -> int | None:
+    """The memory limit of this process's cgroup in bytes (v2 ``memory.max``, v1
+    ``memory.limit_in_bytes``), or None when unlimited / unreadable."""
+    paths = ["/sys/fs/cgroup/memory.max", "/sys/fs/cgroup/memory/memory.limit_in_bytes"]
+    try:  # the process's own cgroup v2 directory, when it is not the root
+        with open("/proc/self/cgroup") as f:
+            for line in f:
+                parts = line.strip().split(":", 2)
+                if len(parts) == 3 and parts[0] == "0" and parts[2] not in ("", "/"):
+                    paths.insert(0, "/sys/fs/cgroup" + parts[2] + "/memory.max")
+    except OSError:
+        pass
+    for p in paths:
+        try:
+            with open(p) as f:
+                v = f.read().strip()
+        except OSError:
+            continue
+        if v and v != "max" and v.isdigit() and int(v) < (1 << 60):
+            return int(v)
+    return None
+
+
 def host_mem_total() -> int:
-    """Physical host RAM in bytes (``/proc/meminfo`` MemTotal; 64 GiB if unreadable)."""
+    """Host RAM this process may use in bytes: ``/proc/meminfo`` MemTotal capped by the
+    cgroup memory limit (a container or a batch slot sees the machine's MemTotal but may
+    only hold its limit); 64 GiB if unreadable."""
+    total = 64 << 30
     try:
         with open("/proc/meminfo") as f:
             for line in f:
                 if line.startswith("MemTotal:"):
-                    return int(line.split()[1]) * 1024
+                    total = int(line.split()[1]) * 1024
+                    break
     except OSError:
         pass
-    return 64 << 30
+    lim = cgroup_mem_limit()
+    return min(total, lim) if lim else total
 
 
 def pinned_budget(local_world: int | None = None) -> int:

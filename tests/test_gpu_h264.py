@@ -256,8 +256,9 @@ def test_gpu_bframes_roundtrip(host, bframes, frames):
 
 
 def test_gpu_bframes_save_bits(host):
-    """x264's --bframes 3 trade on a small clip at fixed QP: no more than +5 % bits and a
-    small quality cost (the 1080p CRF 23 bench measures the saving: profiles/r2_rd_*.md)."""
+    """x264's --bframes 3 trade on a small clip at fixed QP (B pictures at +pbratio): a real
+    saving -- at least 8 % fewer bits -- for at most 1 dB of PSNR-Y (the 1080p RD tables in
+    profiles/ measure the BD-rate)."""
     import torch
     from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
 
@@ -269,8 +270,8 @@ def test_gpu_bframes_save_bits(host):
         out[nb] = (sum(len(r.bitstream) for r in res), float(np.mean([r.psnr_y for r in res])))
         enc.close()
     torch.cuda.synchronize()
-    assert out[3][0] < 1.05 * out[0][0], out
-    assert out[3][1] > out[0][1] - 1.5, out
+    assert out[3][0] < 0.92 * out[0][0], out
+    assert out[3][1] > out[0][1] - 1.0, out
 
 
 def test_gpu_short_segment_display_prefix(host):
