@@ -61,6 +61,7 @@ EncoderConfig cfg_from(const py::dict& d) {
   c.cabac = dget<int>(d, "cabac", 0);
   c.t8x8 = dget<int>(d, "t8x8", 0);
   c.bframes = dget<int>(d, "bframes", 0);
+  c.pyramid = dget<int>(d, "pyramid", 0);
   c.refs = dget<int>(d, "refs", 1);
   c.weighted_bipred = dget<int>(d, "weighted_bipred", 0);
   c.weightp = dget<int>(d, "weightp", 0);
@@ -273,6 +274,27 @@ SliceHeader slice_header_from(const EncoderConfig& c, const SPS& sps, const PPS&
                              sh.num_ref_idx_l1_active != pps.num_ref_idx_l1_default) ? 1 : 0;
   sh.direct_spatial = dget<int>(fp, "direct_spatial", 1);
   sh.first_mb = dget<int>(fp, "first_mb", 0);  // several slices per picture: each writes its MB range
+  // ref_pic_list_modification of list 0 / 1: [(modification_of_pic_nums_idc, abs_diff_pic_num_minus1
+  // or long_term_pic_num), ...] (the encoder's POC-distance order where the default PicNum order
+  // differs: a P picture after a reference B); mmco: [(op, value), ...] adaptive marking
+  for (int l = 0; l < 2; ++l) {
+    const char* key = l ? "mod_l1" : "mod_l0";
+    if (!fp.contains(key) || fp[key].is_none()) continue;
+    for (auto& e : fp[key].cast<std::vector<std::pair<int, int>>>()) {
+      if (e.first < 0 || e.first > 2 || e.second < 0) throw std::runtime_error("ref_pic_list_modification: bad entry");
+      sh.mods[l].push_back(RefMod{e.first, e.second});
+    }
+  }
+  if (fp.contains("mmco") && !fp["mmco"].is_none()) {
+    for (auto& e : fp["mmco"].cast<std::vector<std::pair<int, int>>>()) {
+      if (e.first != 1) throw std::runtime_error("mmco: only operation 1 (unmark a short-term picture) is written");
+      Mmco m{};
+      m.op = 1;
+      m.diff_minus1 = e.second;
+      sh.mmco.push_back(m);
+    }
+    sh.adaptive_ref_pic_marking = sh.mmco.empty() ? 0 : 1;
+  }
   sh.cabac_init_idc = 0;
   // explicit weights of RefPicList0[0] (P slices of a weighted_pred_flag PPS): [luma log2
   // denominator, chroma log2 denominator, luma weight, offset, Cb weight, offset, Cr weight,
@@ -1129,9 +1151,13 @@ PYBIND11_MODULE(_host, m) {
   });
   // batched: one buffer of concatenated RBSPs + sizes -> list of NAL byte strings
   m.def("nal_wrap_many", [](py::array_t<uint8_t, py::array::c_style> buf, const std::vector<int64_t>& sizes,
-                            int nal_ref_idc, int nal_unit_type, int align) {
-    // slice RBSPs back to back in buf, each starting at a multiple of `align` bytes
+                            int nal_ref_idc, int nal_unit_type, int align, const std::vector<int>& ref_idcs,
+                            const std::vector<int>& unit_types) {
+    // slice RBSPs back to back in buf, each starting at a multiple of `align` bytes; ref_idcs /
+    // unit_types (optional): per-slice NAL header fields (slots coding different picture types)
     if (align < 1 || (align & (align - 1))) throw std::invalid_argument("nal_wrap_many: align must be a power of 2");
+    if ((!ref_idcs.empty() && ref_idcs.size() != sizes.size()) || (!unit_types.empty() && unit_types.size() != sizes.size()))
+      throw std::invalid_argument("nal_wrap_many: one nal_ref_idc / nal_unit_type per slice");
     int64_t need = 0;
     for (int64_t sz : sizes) {
       if (sz < 0) throw std::invalid_argument("nal_wrap_many: negative size");
@@ -1147,14 +1173,15 @@ PYBIND11_MODULE(_host, m) {
         off = (off + align - 1) & ~static_cast<int64_t>(align - 1);
         std::vector<uint8_t> v(p + off, p + off + sizes[i]);
         outs[i].reserve(v.size() + v.size() / 64 + 8);
-        append_nal(outs[i], nal_ref_idc, nal_unit_type, v);
+        append_nal(outs[i], ref_idcs.empty() ? nal_ref_idc : ref_idcs[i], unit_types.empty() ? nal_unit_type : unit_types[i], v);
         off += sizes[i];
       }
     }
     py::list l;
     for (auto& o : outs) l.append(to_bytes(o));
     return l;
-  }, py::arg("buf"), py::arg("sizes"), py::arg("nal_ref_idc"), py::arg("nal_unit_type"), py::arg("align") = 1);
+  }, py::arg("buf"), py::arg("sizes"), py::arg("nal_ref_idc"), py::arg("nal_unit_type"), py::arg("align") = 1,
+     py::arg("ref_idcs") = std::vector<int>{}, py::arg("unit_types") = std::vector<int>{});
 
   m.def("parse_nals", [](py::bytes data) {
     std::string s = data;

@@ -43,7 +43,9 @@ SPS make_sps(const EncoderConfig& cfg) {
   if (cfg.bframes > 0) {
     s.poc_type = 0;
     s.log2_max_poc_lsb = 16;
-    s.max_num_reorder = 1;  // B pictures are output one behind their future anchor
+    // B pictures are output one behind their future anchor; with a reference B in between
+    // (b-pyramid) the non-reference ones wait behind two pictures
+    s.max_num_reorder = cfg.pyramid ? 2 : 1;
   } else {
     s.poc_type = 2;
   }

@@ -34,6 +34,7 @@ struct EncoderConfig {
   int cabac = 0;
   int t8x8 = 0;
   int bframes = 0;
+  int pyramid = 0;          // x264 --b-pyramid normal: some B pictures are references (reorder depth 2)
   int refs = 1;
   int weighted_bipred = 0;  // 2 = implicit weights (x264 --weightb)
   int weightp = 0;          // weighted_pred_flag: P slices carry pred_weight_table() (x264 --weightp)

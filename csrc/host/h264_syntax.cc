@@ -189,8 +189,16 @@ void write_slice_header(BitWriter& bw, const SliceHeader& h, const SPS& s, const
       bw.put_ue(h.num_ref_idx_l0_active - 1);
       if (h.slice_type == SLICE_B) bw.put_ue(h.num_ref_idx_l1_active - 1);
     }
-    bw.put_bit(0);  // ref_pic_list_modification_flag_l0
-    if (h.slice_type == SLICE_B) bw.put_bit(0);  // ref_pic_list_modification_flag_l1
+    // ref_pic_list_modification() (7.3.3.1)
+    for (int l = 0; l < (h.slice_type == SLICE_B ? 2 : 1); ++l) {
+      bw.put_bit(!h.mods[l].empty());
+      if (h.mods[l].empty()) continue;
+      for (const RefMod& m : h.mods[l]) {
+        bw.put_ue(m.idc);
+        bw.put_ue(m.value);
+      }
+      bw.put_ue(3);
+    }
   }
   if (p.weighted_bipred_idc == 1 && h.slice_type == SLICE_B)
     throw std::runtime_error("explicit weighted bi-prediction is not written");
@@ -221,7 +229,18 @@ void write_slice_header(BitWriter& bw, const SliceHeader& h, const SPS& s, const
       bw.put_bit(h.no_output_of_prior_pics);
       bw.put_bit(h.long_term_reference);
     } else {
-      bw.put_bit(0);  // adaptive_ref_pic_marking_mode_flag (sliding window)
+      // adaptive_ref_pic_marking_mode_flag: sliding window, or the listed operations (7.3.3.3)
+      bw.put_bit(h.adaptive_ref_pic_marking && !h.mmco.empty());
+      if (h.adaptive_ref_pic_marking && !h.mmco.empty()) {
+        for (const Mmco& m : h.mmco) {
+          bw.put_ue(m.op);
+          if (m.op == 1 || m.op == 3) bw.put_ue(m.diff_minus1);
+          if (m.op == 2) bw.put_ue(m.long_term_pic_num);
+          if (m.op == 3 || m.op == 6) bw.put_ue(m.long_term_frame_idx);
+          if (m.op == 4) bw.put_ue(m.max_long_term_frame_idx_plus1);
+        }
+        bw.put_ue(0);
+      }
     }
   }
   if (p.entropy_coding_mode && h.slice_type != SLICE_I) bw.put_ue(h.cabac_init_idc);

@@ -31,10 +31,17 @@ constexpr int kAqSpan = 8;
 __global__ __launch_bounds__(256) void h264_aq_offsets(Geom g, const uint8_t* __restrict__ sy,
                                                        const uint8_t* __restrict__ su, const uint8_t* __restrict__ sv,
                                                        float strength, const float* __restrict__ extra,
-                                                       long long extra_stride, int8_t* __restrict__ out) {
+                                                       long long extra_stride, int8_t* __restrict__ out,
+                                                       const SlotRoute* rt) {
   const int l = lane_id() & 15;
   const int nmb = g.nmb();
   const int slot = blockIdx.y;
+  // routed: `extra` is the batch's [B, F, nmb] MB-tree table; a slot coding a reference
+  // picture takes the row of its display index, other pictures get variance AQ only
+  if (extra && rt) {
+    const SlotRoute& r = rt[slot];
+    extra = (r.kind >= 0 && r.disp >= 0 && (r.flags & SF_REF)) ? extra + static_cast<size_t>(r.disp) * nmb : nullptr;
+  }
   for (int it = 0; it < kAqSpan; ++it) {
   const int mb = (blockIdx.x * kAqSpan + it) * 16 + (threadIdx.x >> 4);
   if ((blockIdx.x * kAqSpan + it) * 16 >= nmb) break;  // (uniform)
@@ -146,11 +153,11 @@ using namespace mivc::gpu;
 // frame at extra + s * extra_stride
 extern "C" void mivc_launch_aq_offsets(int B, int wmb, int hmb, const uint8_t* sy, const uint8_t* su,
                                        const uint8_t* sv, float strength, const float* extra, long long extra_stride,
-                                       int8_t* out, void* stream) {
+                                       int8_t* out, void* stream, const void* route) {
   const Geom g{B, wmb, hmb, wmb * 16, hmb * 16};
   hipLaunchKernelGGL(h264_aq_offsets, dim3((wmb * hmb + 16 * kAqSpan - 1) / (16 * kAqSpan), B), dim3(256), 0,
                      static_cast<hipStream_t>(stream), g,
-                     sy, su, sv, strength, extra, extra_stride, out);
+                     sy, su, sv, strength, extra, extra_stride, out, static_cast<const SlotRoute*>(route));
 }
 
 extern "C" void mivc_launch_qp_fixup(int B, int wmb, int hmb, void* hdr, const int16_t* coef, const uint8_t* nz,

@@ -39,14 +39,21 @@ struct BDirectArgs {
   int8_t* dref;             // [B, nmb, 4] refIdxL0 of each quadrant's direct prediction (nullable: all 0)
   int16_t* pm0;             // [B, nmb, 2] ME predictor L0 (mean of the direct vectors)
   int16_t* pm1;             // [B, nmb, 2] ME predictor L1
+  // routed (route.h): col is the record pool [B, nbuf, nmb]; B slots only, each with its own
+  // co-located picture (RefPicList1[0]) and its own dsf / direct_copy (SlotRoute)
+  const SlotRoute* rt;
+  int nbuf;
 };
 
 __global__ __launch_bounds__(256) void b_direct_mv(BDirectArgs a) {
   const int mb = blockIdx.x * 256 + threadIdx.x, slot = blockIdx.y;
   const int nmb = a.g.nmb();
-  if (mb >= nmb) return;
+  if (mb >= nmb || !route_active(a.rt, slot, SK_B)) return;
   const size_t o = static_cast<size_t>(slot) * nmb + mb;
-  const MbHeader& c = a.col[o];
+  const MbHeader& c = a.col[route_index(a.rt, a.nbuf, slot, RO_L1) * nmb + mb];
+  // a B picture as the co-located one (b-pyramid): a block without list-0 motion gives its
+  // list-1 motion (8.4.1.2.1); a P anchor predicts from list 0 only
+  const bool col_l1 = a.rt && a.rt[slot].col_l1;
   const bool intra = h264::mbk_is_intra(c.kind);
   int v[2][4][2];
   int rq[4];
@@ -55,13 +62,14 @@ __global__ __launch_bounds__(256) void b_direct_mv(BDirectArgs a) {
   for (int q = 0; q < 4; ++q) {
     // direct_8x8_inference: the corner 4x4 block of co-located quadrant q, i.e. its vector;
     // a P anchor predicts from list 0 only
-    const bool none = intra || c.ref[0][q] < 0;
-    const int cx = none ? 0 : c.mv[0][q][0];
-    const int cy = none ? 0 : c.mv[0][q][1];
-    const int r = none ? 0 : min(static_cast<int>(c.ref[0][q]), kMaxRefs - 1);
+    const int cl = (col_l1 && c.ref[0][q] < 0) ? 1 : 0;
+    const bool none = intra || c.ref[cl][q] < 0;
+    const int cx = none ? 0 : c.mv[cl][q][0];
+    const int cy = none ? 0 : c.mv[cl][q][1];
+    const int r = none ? 0 : min(static_cast<int>(c.ref[cl][q]), kMaxRefs - 1);
     rq[q] = r;
     int l0x, l0y;
-    const int dcp = a.direct_copy[r], dsf = a.dsf[r];
+    const int dcp = a.rt ? a.rt[slot].dcopy[r] : a.direct_copy[r], dsf = a.rt ? a.rt[slot].dsf[r] : a.dsf[r];
     if (dcp) {
       l0x = cx;
       l0y = cy;
@@ -133,6 +141,10 @@ struct BDecideArgs {
   // b_spatial_decide weighs it against the exact spatial direct motion in decoding order
   int spatial;
   int dbias;  // temporal direct preferred by dbias * lambda in the 16x16 choice (cost_out stays unbiased)
+  // routed (route.h): ref0 / ref1 / hp0 / hp1 / ref0k / hp0k are pool bases, the roles come from
+  // each B slot's SlotRoute (list-0 entries, list-1 entry, implicit weights)
+  const SlotRoute* rt;
+  int nbuf;
 };
 
 constexpr int kNoCostB = 0x3FFFFFFF;  // me.hip kNoCost: the MB was not searched
@@ -214,6 +226,7 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   const int nmb = g.nmb();
   int mb, slot;
   xcd_unit_slot(mb, slot);
+  if (!route_active(a.rt, slot, SK_B)) return;
   const int lane = threadIdx.x;
   const size_t o = static_cast<size_t>(slot) * nmb + mb;
   const int mx = mb % g.wmb, my = mb / g.wmb;
@@ -222,8 +235,12 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   const int X = mx * 16 + c0, Y = my * 16 + r;
   const int q = (r >> 3) * 2 + (c0 >> 3);  // 8x8 quadrant of this lane's samples
   const size_t yo = static_cast<size_t>(slot) * g.ysize();
-  const size_t ho = static_cast<size_t>(slot) * 3 * (W + 2 * kHpMargin) * (H + 2 * kHpMargin);
-  const uint8_t *G0 = a.ref0 + yo, *G1 = a.ref1 + yo, *H0 = a.hp0 + ho, *H1 = a.hp1 + ho;
+  const size_t hps = hp_plane_bytes(W, H);
+  const size_t s0 = route_index(a.rt, a.nbuf, slot, RO_L0), s1 = route_index(a.rt, a.nbuf, slot, RO_L1);
+  const uint8_t *G0 = a.ref0 + s0 * g.ysize(), *G1 = a.ref1 + s1 * g.ysize(), *H0 = a.hp0 + s0 * hps,
+                *H1 = a.hp1 + s1 * hps;
+  const int16_t* w1t = a.rt ? a.rt[slot].w1 : nullptr;
+  auto w1of = [&](int rr) { return w1t ? static_cast<int>(w1t[rr & 3]) : a.w1[rr & 3]; };
   const int16_t* dm = a.dmv + o * 16;
   const bool donly = a.direct_only;
   const int m0x = donly ? 0 : a.mv0[o * 2], m0y = donly ? 0 : a.mv0[o * 2 + 1];
@@ -233,7 +250,9 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   uint32_t drw = 0;  // refIdxL0 of the four direct quadrants (bytes)
   if (a.dref) drw = *reinterpret_cast<const uint32_t*>(a.dref + o * 4);
   const int dr = (drw >> (8 * q)) & 255;
-  const uint8_t *GD = dr ? a.ref0k[dr] + yo : G0, *HD = dr ? a.hp0k[dr] + ho : H0;
+  const size_t sd = route_index(a.rt, a.nbuf, slot, RO_L0 + (dr & 3));
+  const uint8_t *GD = dr ? a.ref0k[dr] + (a.rt ? sd : slot) * g.ysize() : G0,
+                *HD = dr ? a.hp0k[dr] + (a.rt ? sd : slot) * hps : H0;
   const bool searched = !donly && a.cost0[o] < kNoCostB && a.cost1[o] < kNoCostB;
   uint32_t* pout = reinterpret_cast<uint32_t*>(a.pred_out + o * 256 + r * 16 + c0);
   if (!donly && !searched && a.have_direct) {
@@ -253,9 +272,9 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   const uint32_t pd = (!donly && a.have_direct)
                           ? *pout
                           : wavg4b(mc4(GD, HD, W, H, X, Y, dm[q * 2], dm[q * 2 + 1]),
-                                   mc4(G1, H1, W, H, X, Y, dm[8 + q * 2], dm[8 + q * 2 + 1]), a.w1[dr]);
+                                   mc4(G1, H1, W, H, X, Y, dm[8 + q * 2], dm[8 + q * 2 + 1]), w1of(dr));
   if (donly) *pout = pd;
-  const uint32_t pb = donly ? pd : wavg4b(mc4(G0, H0, W, H, X, Y, m0x, m0y), mc4(G1, H1, W, H, X, Y, m1x, m1y), a.w1[0]);
+  const uint32_t pb = donly ? pd : wavg4b(mc4(G0, H0, W, H, X, Y, m0x, m0y), mc4(G1, H1, W, H, X, Y, m1x, m1y), w1of(0));
   // residuals of the four candidates: 0 direct, 1 bi (the two ME vectors), 2 L0, 3 L1 (the ME
   // predictions; not needed by the direct-only pre-pass or for MBs the gate left unsearched)
   const uint32_t p0w = searched ? *reinterpret_cast<const uint32_t*>(a.pred0 + o * 256 + r * 16 + c0) : pd;
@@ -428,6 +447,8 @@ struct BSpatialArgs {
   const int* qp;
   const int8_t* aq;
   int bias;              // direct taken when cost_d <= cost_e + bias * lambda
+  const SlotRoute* rt;   // routed (route.h): pools for col / ref1 / hp1 / ref0k / hp0k, B slots only
+  int nbuf;
 };
 
 struct NbMv16 {
@@ -479,6 +500,7 @@ __device__ __forceinline__ NbMv16 nb_packed(bool avail, bool intra, int v) {
 __global__ __launch_bounds__(64 * kSpatialWaves) void b_spatial_decide(BSpatialArgs a) {
   const Geom& g = a.g;
   const int slot = blockIdx.x, nmb = g.nmb();
+  if (!route_active(a.rt, slot, SK_B)) return;  // uniform per workgroup
   __shared__ int prog[kMaxRows];
   __shared__ int s_res[kSpatialWaves][2][256];
   __shared__ int nbq[2][kSpatialMaxCols][5];  // [row parity][column]: intra, L0 q2, L0 q3, L1 q2, L1 q3
@@ -489,9 +511,15 @@ __global__ __launch_bounds__(64 * kSpatialWaves) void b_spatial_decide(BSpatialA
   const int r = hl >> 1, c0 = (hl & 1) * 8, q = (r >> 3) * 2 + (c0 >> 3);
   const int W = g.W, Hh = g.H, wmb = g.wmb, hmb = g.hmb;
   const size_t yo = static_cast<size_t>(slot) * g.ysize();
-  const size_t ho = static_cast<size_t>(slot) * 3 * (W + 2 * kHpMargin) * (Hh + 2 * kHpMargin);
+  const size_t hps = hp_plane_bytes(W, Hh);
+  size_t sk[kMaxRefs];
+#pragma unroll
+  for (int k = 0; k < kMaxRefs; ++k) sk[k] = route_index(a.rt, a.nbuf, slot, RO_L0 + k);
+  const size_t s1 = route_index(a.rt, a.nbuf, slot, RO_L1);
+  const int16_t* w1t = a.rt ? a.rt[slot].w1 : nullptr;
+  const bool col_l1 = a.rt && a.rt[slot].col_l1;
   MbHeader* H = a.hdr + static_cast<size_t>(slot) * nmb;
-  const MbHeader* C0 = a.col + static_cast<size_t>(slot) * nmb;
+  const MbHeader* C0 = a.col + s1 * nmb;
   const int* IC = a.intra_cost + static_cast<size_t>(slot) * nmb;
   int* CB = a.cost + static_cast<size_t>(slot) * nmb;
   int* res = s_res[w][half];
@@ -520,6 +548,7 @@ __global__ __launch_bounds__(64 * kSpatialWaves) void b_spatial_decide(BSpatialA
       const MbHeader& c = C0[mb];
       const uint2 cref = *reinterpret_cast<const uint2*>(&c.ref[0][0]);  // ref[2][4]
       const uint4 cmv = *reinterpret_cast<const uint4*>(&c.mv[0][0][0]);  // list-0 vectors
+      const uint4 cmv1 = col_l1 ? *reinterpret_cast<const uint4*>(&c.mv[1][0][0]) : make_uint4(0u, 0u, 0u, 0u);
       const int ckind = c.kind;
       const int X = xs * 16 + c0, Y = ys * 16 + r;
       const uint2 src = *reinterpret_cast<const uint2*>(a.src_y + yo + static_cast<size_t>(Y) * W + X);
@@ -559,10 +588,16 @@ __global__ __launch_bounds__(64 * kSpatialWaves) void b_spatial_decide(BSpatialA
         const bool zero = refs[0] < 0 && refs[1] < 0;
         const bool cintra = h264::mbk_is_intra(ckind);
         const uint32_t cmw[4] = {cmv.x, cmv.y, cmv.z, cmv.w};
+        const uint32_t cmw1[4] = {cmv1.x, cmv1.y, cmv1.z, cmv1.w};
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
-          const int cr = static_cast<int8_t>((cref.x >> (8 * qq)) & 255u);
-          const int cx = static_cast<int16_t>(cmw[qq] & 0xFFFFu), cy = static_cast<int16_t>(cmw[qq] >> 16);
+          // 8.4.1.2.1: the co-located block's list-0 motion, or its list-1 motion when it has
+          // none (only a B picture -- b-pyramid -- can be list-1 only)
+          const int cr0 = static_cast<int8_t>((cref.x >> (8 * qq)) & 255u);
+          const bool use1 = col_l1 && cr0 < 0;
+          const int cr = use1 ? static_cast<int8_t>((cref.y >> (8 * qq)) & 255u) : cr0;
+          const uint32_t cw_ = use1 ? cmw1[qq] : cmw[qq];
+          const int cx = static_cast<int16_t>(cw_ & 0xFFFFu), cy = static_cast<int16_t>(cw_ >> 16);
           const bool col_zero = !cintra && cr == 0 && abs(cx) <= 1 && abs(cy) <= 1;
 #pragma unroll
           for (int l = 0; l < 2; ++l) {
@@ -590,9 +625,12 @@ __global__ __launch_bounds__(64 * kSpatialWaves) void b_spatial_decide(BSpatialA
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         uint32_t p0 = 0, p1 = 0;
-        if (r0 >= 0) p0 = mc4(a.ref0k[r0 & 3] + yo, a.hp0k[r0 & 3] + ho, W, Hh, X + 4 * k, Y, pk_mx(mine[0]), pk_my(mine[0]));
-        if (r1 >= 0) p1 = mc4(a.ref1 + yo, a.hp1 + ho, W, Hh, X + 4 * k, Y, pk_mx(mine[1]), pk_my(mine[1]));
-        pw[k] = (r0 >= 0 && r1 >= 0) ? wavg4b(p0, p1, a.w1[r0 & 3]) : (r0 >= 0 ? p0 : p1);
+        if (r0 >= 0)
+          p0 = mc4(a.ref0k[r0 & 3] + sk[r0 & 3] * g.ysize(), a.hp0k[r0 & 3] + sk[r0 & 3] * hps, W, Hh, X + 4 * k, Y,
+                   pk_mx(mine[0]), pk_my(mine[0]));
+        if (r1 >= 0) p1 = mc4(a.ref1 + s1 * g.ysize(), a.hp1 + s1 * hps, W, Hh, X + 4 * k, Y, pk_mx(mine[1]), pk_my(mine[1]));
+        pw[k] = (r0 >= 0 && r1 >= 0) ? wavg4b(p0, p1, w1t ? static_cast<int>(w1t[r0 & 3]) : a.w1[r0 & 3])
+                                     : (r0 >= 0 ? p0 : p1);
       }
       const uint32_t sw[2] = {src.x, src.y};
 #pragma unroll
@@ -692,6 +730,8 @@ struct PRefineArgs {
   uint8_t* pred;            // [B, nmb, 256] luma prediction, rewritten for MBs that switch
   const int* qp;
   const int8_t* aq;
+  const SlotRoute* rt;      // routed (route.h): ref / hp are pools, P slots' RefPicList0[0]
+  int nbuf;
 };
 
 __device__ __forceinline__ int median3(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
@@ -701,6 +741,7 @@ __global__ __launch_bounds__(64) void p_mv_refine(PRefineArgs a) {
   const int nmb = g.nmb();
   int mb, slot;
   xcd_unit_slot(mb, slot);
+  if (!route_active(a.rt, slot, SK_P)) return;
   const int lane = threadIdx.x;
   const size_t o = static_cast<size_t>(slot) * nmb + mb;
   const int mx = mb % g.wmb, my = mb / g.wmb;
@@ -730,8 +771,9 @@ __global__ __launch_bounds__(64) void p_mv_refine(PRefineArgs a) {
   const int r = lane >> 2, c0 = (lane & 3) * 4;
   const int X = mx * 16 + c0, Y = my * 16 + r;
   const size_t yo = static_cast<size_t>(slot) * g.ysize();
-  const uint8_t* G0 = a.ref + yo;
-  const uint8_t* H0 = a.hp + static_cast<size_t>(slot) * 3 * (W + 2 * kHpMargin) * (H + 2 * kHpMargin);
+  const size_t s0 = route_index(a.rt, a.nbuf, slot, RO_L0);
+  const uint8_t* G0 = a.ref + s0 * g.ysize();
+  const uint8_t* H0 = a.hp + s0 * hp_plane_bytes(W, H);
   const uint32_t src = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y) * W + X);
   const uint32_t ps = mc4(G0, H0, W, H, X, Y, sx, sy);
   __shared__ int s_res[256];
@@ -1133,6 +1175,8 @@ struct PPartArgs {
   const int8_t* aq;
   int overhead;         // bits charged to the split beyond the mvds
   int min_satd;         // 16x16 SATD at or below this: no split search
+  const SlotRoute* rt;  // routed (route.h): ref / hp are pools, P slots' RefPicList0[0]
+  int nbuf;
 };
 
 __device__ __forceinline__ void med_pred(int ax, int ay, bool ha, int bx, int by, bool hb, int cx, int cy, bool hc,
@@ -1155,6 +1199,7 @@ __global__ __launch_bounds__(64) void p_part8x8(PPartArgs a) {
   const int nmb = g.nmb();
   int mb, slot;
   xcd_unit_slot(mb, slot);
+  if (!route_active(a.rt, slot, SK_P)) return;
   const int lane = threadIdx.x;
   const size_t o = static_cast<size_t>(slot) * nmb + mb;
   const int mx = mb % g.wmb, my = mb / g.wmb;
@@ -1200,8 +1245,9 @@ __global__ __launch_bounds__(64) void p_part8x8(PPartArgs a) {
   const int W = g.W, H = g.H;
   const int X = mx * 16 + (q & 1) * 8 + (blk & 1) * 4, Y = my * 16 + (q >> 1) * 8 + (blk >> 1) * 4;
   const size_t yo = static_cast<size_t>(slot) * g.ysize();
-  const uint8_t* G0 = a.ref + yo;
-  const uint8_t* H0 = a.hp + static_cast<size_t>(slot) * 3 * (W + 2 * kHpMargin) * (H + 2 * kHpMargin);
+  const size_t s0 = route_index(a.rt, a.nbuf, slot, RO_L0);
+  const uint8_t* G0 = a.ref + s0 * g.ysize();
+  const uint8_t* H0 = a.hp + s0 * hp_plane_bytes(W, H);
   uint32_t srow[4];
 #pragma unroll
   for (int y = 0; y < 4; ++y) srow[y] = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y + y) * W + X);
@@ -1304,8 +1350,11 @@ __global__ __launch_bounds__(64) void p_part8x8(PPartArgs a) {
 using namespace mivc::gpu;
 
 extern "C" void mivc_launch_b_direct(int B, int wmb, int hmb, const void* col, const int* dsf, const int* direct_copy,
-                                     int nref, int16_t* dmv, int8_t* dref, int16_t* pm0, int16_t* pm1, void* stream) {
+                                     int nref, int16_t* dmv, int8_t* dref, int16_t* pm0, int16_t* pm1, void* stream,
+                                     const void* route, int nbuf) {
   BDirectArgs a;
+  a.rt = static_cast<const SlotRoute*>(route);
+  a.nbuf = nbuf;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.col = static_cast<const MbHeader*>(col);
   for (int r = 0; r < kMaxRefs; ++r) {  // refIdxCol beyond the list: the last entry (never produced)
@@ -1327,8 +1376,10 @@ extern "C" void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src
                                      const int* qp, const int8_t* aq, void* hdr, uint8_t* pred_out, int* cost_out,
                                      void* stream, const int* w1, int nref, const int8_t* dref,
                                      const uint8_t* const* ref0k, const uint8_t* const* hp0k, int direct_only, int bparts, int have_direct,
-                                     int spatial, int dbias) {
+                                     int spatial, int dbias, const void* route, int nbuf) {
   BDecideArgs a;
+  a.rt = static_cast<const SlotRoute*>(route);
+  a.nbuf = nbuf;
   a.spatial = spatial;
   a.dbias = dbias;
   a.direct_only = direct_only;
@@ -1367,8 +1418,10 @@ extern "C" void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src
 extern "C" void mivc_launch_p_refine(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref,
                                      const uint8_t* hp, const int16_t* mv_in, int16_t* mv_out, int* cost,
                                      const int16_t* pm, uint8_t* pred, const int* qp, const int8_t* aq,
-                                     void* stream) {
+                                     void* stream, const void* route, int nbuf) {
   PRefineArgs a;
+  a.rt = static_cast<const SlotRoute*>(route);
+  a.nbuf = nbuf;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.src_y = src_y;
   a.ref = ref;
@@ -1386,8 +1439,10 @@ extern "C" void mivc_launch_p_refine(int B, int wmb, int hmb, const uint8_t* src
 extern "C" void mivc_launch_p_part8(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref,
                                     const uint8_t* hp, const int16_t* mv, const int16_t* pm, int* cost, uint8_t* pred,
                                     int16_t* mv8, const int* qp, const int8_t* aq, int overhead, int min_satd,
-                                    void* stream) {
+                                    void* stream, const void* route, int nbuf) {
   PPartArgs a;
+  a.rt = static_cast<const SlotRoute*>(route);
+  a.nbuf = nbuf;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.src_y = src_y;
   a.ref = ref;
@@ -1408,6 +1463,8 @@ extern "C" void mivc_launch_hevc_merge_refine(int B, int wmb, int hmb, const uin
                                               const uint8_t* hp, const int16_t* mv_in, int16_t* mv_out, int* cost,
                                               const int16_t* pm, const int* qp, const int8_t* aq, void* stream) {
   PRefineArgs a;
+  a.rt = nullptr;
+  a.nbuf = 0;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.src_y = src_y;
   a.ref = ref;
@@ -1465,8 +1522,10 @@ extern "C" void mivc_launch_b_spatial(int B, int wmb, int hmb, void* hdr, const 
                                       const uint8_t* ref1, const uint8_t* hp1, const uint8_t* const* ref0k,
                                       const uint8_t* const* hp0k, const int* w1, int nref, uint8_t* pred_out, int* err,
                                       void* stream, const int* intra_cost, int* cost, const int* qp, const int8_t* aq,
-                                      int bias) {
+                                      int bias, const void* route, int nbuf) {
   BSpatialArgs a;
+  a.rt = static_cast<const SlotRoute*>(route);
+  a.nbuf = nbuf;
   a.bias = bias;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.hdr = static_cast<MbHeader*>(hdr);

@@ -18,39 +18,44 @@ void mivc_launch_synth(void* y, void* u, void* v, int width, int height, int slo
                        uint32_t seed, int bit_depth, int slot0, void* stream);
 void mivc_launch_prep(const uint8_t* in_y, const uint8_t* in_u, const uint8_t* in_v, int w, int h,
                       int64_t in_stride_y, int64_t in_stride_c, int nframes, uint8_t* out_y, uint8_t* out_u,
-                      uint8_t* out_v, int ow, int oh, int W, int H, void* stream);
+                      uint8_t* out_v, int ow, int oh, int W, int H, void* stream, const int* fsel);
 void mivc_launch_rgb_to_i420(const uint8_t* rgb, int w, int h, int nframes, uint8_t* y, uint8_t* u, uint8_t* v,
                              void* stream);
 void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref_y, const int16_t* pred_mv,
                     int16_t* out_mv, int* out_cost, uint8_t* out_pred, int* out_intra_cost, const int* qp, int range,
                     int subpel, uint8_t* hp, const int8_t* aq, int planes_ready, int early_sad, void* stream,
-                    const int* gate_cost, int gate_thresh, const int16_t* cost_mv);
+                    const int* gate_cost, int gate_thresh, const int16_t* cost_mv, const void* route, int nbuf,
+                    int role, int want);
 void mivc_launch_me_ref_select(int B, int wmb, int hmb, int nref, int16_t* mv, int16_t* mv8, int* cost, uint8_t* pred,
                                const int16_t* xmv, const int* xcost, const uint8_t* xpred, int8_t* mref, const int* qp,
-                               const int8_t* aq, void* stream);
+                               const int8_t* aq, void* stream, const void* route);
 void mivc_launch_b_spatial(int B, int wmb, int hmb, void* hdr, const void* col, const uint8_t* src, const uint8_t* ref1,
                            const uint8_t* hp1, const uint8_t* const* ref0k, const uint8_t* const* hp0k, const int* w1,
                            int nref, uint8_t* pred_out, int* err, void* stream, const int* intra_cost, int* cost,
-                           const int* qp, const int8_t* aq, int bias);
+                           const int* qp, const int8_t* aq, int bias, const void* route, int nbuf);
 void mivc_launch_b_direct(int B, int wmb, int hmb, const void* col, const int* dsf, const int* direct_copy, int nref,
-                          int16_t* dmv, int8_t* dref, int16_t* pm0, int16_t* pm1, void* stream);
+                          int16_t* dmv, int8_t* dref, int16_t* pm0, int16_t* pm1, void* stream, const void* route,
+                          int nbuf);
 void mivc_launch_p_refine(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref, const uint8_t* hp,
                           const int16_t* mv_in, int16_t* mv_out, int* cost, const int16_t* pm, uint8_t* pred,
-                          const int* qp, const int8_t* aq, void* stream);
+                          const int* qp, const int8_t* aq, void* stream, const void* route, int nbuf);
 void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref0, const uint8_t* ref1,
                           const uint8_t* hp0, const uint8_t* hp1, const int16_t* mv0, const int16_t* mv1,
                           const int* cost0, const int* cost1, const uint8_t* pred0, const uint8_t* pred1,
                           const int16_t* pm0, const int16_t* pm1, const int16_t* dmv, const int* qp, const int8_t* aq,
                           void* hdr, uint8_t* pred_out, int* cost_out, void* stream, const int* w1, int nref,
                           const int8_t* dref, const uint8_t* const* ref0k, const uint8_t* const* hp0k,
-                          int direct_only, int bparts, int have_direct, int spatial, int dbias);
+                          int direct_only, int bparts, int have_direct, int spatial, int dbias, const void* route,
+                          int nbuf);
 void mivc_launch_aq_offsets(int B, int wmb, int hmb, const uint8_t* sy, const uint8_t* su, const uint8_t* sv,
-                            float strength, const float* extra, long long extra_stride, int8_t* out, void* stream);
+                            float strength, const float* extra, long long extra_stride, int8_t* out, void* stream,
+                            const void* route);
 void mivc_launch_mbtree(int B, int F, int lbw, int lbh, const int* blk_cost, const int* blk_mv, void* prop,
                         float strength, float* out, void* stream);
 void mivc_launch_qp_fixup(int B, int wmb, int hmb, void* hdr, const int16_t* coef, const uint8_t* nz, uint8_t* flags,
                           const int* slice_qp, void* stream);
-void mivc_launch_me_halfpel(int B, int W, int H, const uint8_t* ref_y, uint8_t* hp, void* stream);
+void mivc_launch_me_halfpel(int B, int W, int H, const uint8_t* ref_y, uint8_t* hp, void* stream, const void* route,
+                            int nbuf);
 void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* src_u,
                               const uint8_t* src_v, const uint8_t* ref_y, const uint8_t* ref_u, const uint8_t* ref_v,
                               uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const uint8_t* pred_y,
@@ -59,21 +64,21 @@ void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t* src_y, con
                               int* intra_count, const int8_t* aq, const uint8_t* ref1_u, const uint8_t* ref1_v,
                               int bmode, int t8, const int16_t* mv8, void* stream, const int* w1, int nref,
                               const uint8_t* const* xref_u, const uint8_t* const* xref_v, const int8_t* mref,
-                              const int* wp, int trellis, float trellis_lambda);
+                              const int* wp, int trellis, float trellis_lambda, const void* route, int nbuf);
 void mivc_launch_wp_stats(const uint8_t* y, const uint8_t* u, const uint8_t* v, int w, int h, int npics,
                           unsigned long long* out, void* stream);
 void mivc_launch_wp_src(const uint8_t* src, uint8_t* dst, const int* wt, int B, long long plane_bytes, void* stream);
 void mivc_launch_p_part8(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref, const uint8_t* hp,
                          const int16_t* mv, const int16_t* pm, int* cost, uint8_t* pred, int16_t* mv8, const int* qp,
-                         const int8_t* aq, int overhead, int min_satd, void* stream);
+                         const int8_t* aq, int overhead, int min_satd, void* stream, const void* route, int nbuf);
 void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* src_u,
                               const uint8_t* src_v, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const int* qp,
                               int chroma_qp_offset, void* hdr, int16_t* coef, uint8_t* nz,
                               const uint8_t* intra_flag, const int* intra_count, int* err, int use_i4x4,
-                              const int8_t* aq, void* stream, int use_i8x8);
+                              const int8_t* aq, void* stream, int use_i8x8, const void* route, int nbuf);
 void mivc_launch_deblock(int B, int wmb, int hmb, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const void* hdr,
                          const uint8_t* nz, int chroma_qp_offset, int alpha_off, int beta_off, int* err,
-                         void* stream);
+                         void* stream, const void* route, int nbuf);
 void mivc_launch_decode_picture_dpb(int B, int wmb, int hmb, int dpb_n, uint8_t* dpb_y, uint8_t* dpb_u, uint8_t* dpb_v,
                                     const int16_t* cur_idx, const int16_t* reftab, const int16_t* wp, const int16_t* sub,
                                     const void* hdr, const uint32_t* mask, const uint32_t* off,
@@ -123,7 +128,7 @@ int mivc_cabac_gap();
 void mivc_launch_cabac_bin(int B, int wmb, int hmb, const void* hdr, const int16_t* coef, uint32_t* mask, void* nb,
                            int* cnt, long long* off, int* tot, uint16_t* pool, long long pool_cap,
                            long long* pool_used, long long* base, int* total, const int* slot_qp, int slice_type,
-                           int num_ref_l0, int num_ref_l1, int t8x8_mode, int* err, void* stream);
+                           int num_ref_l0, int num_ref_l1, int t8x8_mode, int* err, void* stream, const void* route);
 void mivc_launch_cabac_code(int L, int B, uint16_t* pool, const long long* base, const int* total,
                             const uint32_t* hdr_bits, const int* hdr_nbits, const int* slot_qp,
                             unsigned long long itypes, int* bytes, uint8_t* out, long long* out_off, int* err,
@@ -134,7 +139,7 @@ void mivc_launch_cavlc(int B, int wmb, int hmb, const void* hdr, const int16_t* 
                        const int* slot_qp, uint8_t* out, long long* out_off, const uint8_t* nz, void* stream);
 void mivc_launch_sse(int B, int W, int H, int w, int h, const uint8_t* sy, const uint8_t* su, const uint8_t* sv,
                      const uint8_t* ry, const uint8_t* ru, const uint8_t* rv, unsigned long long* sse,
-                     float* ssim_sum, void* stream);
+                     float* ssim_sum, void* stream, const void* route, int nbuf);
 long long mivc_lookahead_low_bytes(int w, int h, int N);
 int mivc_launch_hevc_prep_frame(int B, const void* sy, const void* su, const void* sv, long long ss_y, long long ss_c,
                                 int pitch_y, int pitch_c, int bps, int w, int h, uint16_t* dy, uint16_t* du,
@@ -164,12 +169,16 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("y"), py::arg("u"), py::arg("v"), py::arg("w"), py::arg("h"), py::arg("slots"), py::arg("frames"),
      py::arg("frame0"), py::arg("seed"), py::arg("stream"), py::arg("bit_depth") = 8, py::arg("slot0") = 0);
   m.def("prep", [](uintptr_t iy, uintptr_t iu, uintptr_t iv, int w, int h, int64_t sy, int64_t sc, int n,
-                   uintptr_t oy, uintptr_t ou, uintptr_t ov, int ow, int oh, int W, int H, uintptr_t stream) {
+                   uintptr_t oy, uintptr_t ou, uintptr_t ov, int ow, int oh, int W, int H, uintptr_t stream,
+                   uintptr_t fsel) {
+    // fsel (nullable): int32 [n] frame index per input slot, added to the slot's frame 0
     if (ow != w || oh != h) throw std::invalid_argument("prep: resample with ops.scale (scale.hip) first");
     if (W < w || H < h || w < 2 || h < 2) throw std::invalid_argument("prep: bad geometry");
     mivc_launch_prep(P<uint8_t>(iy), P<uint8_t>(iu), P<uint8_t>(iv), w, h, sy, sc, n, P<uint8_t>(oy), P<uint8_t>(ou),
-                     P<uint8_t>(ov), ow, oh, W, H, S(stream));
-  });
+                     P<uint8_t>(ov), ow, oh, W, H, S(stream), P<int>(fsel));
+  }, py::arg("iy"), py::arg("iu"), py::arg("iv"), py::arg("w"), py::arg("h"), py::arg("sy"), py::arg("sc"), py::arg("n"),
+     py::arg("oy"), py::arg("ou"), py::arg("ov"), py::arg("ow"), py::arg("oh"), py::arg("W"), py::arg("H"),
+     py::arg("stream"), py::arg("fsel") = 0);
   m.def("rgb_to_i420", [](uintptr_t rgb, int w, int h, int n, uintptr_t y, uintptr_t u, uintptr_t v,
                           uintptr_t stream) {
     mivc_launch_rgb_to_i420(P<uint8_t>(rgb), w, h, n, P<uint8_t>(y), P<uint8_t>(u), P<uint8_t>(v), S(stream));
@@ -177,31 +186,35 @@ PYBIND11_MODULE(_hip, m) {
   m.def("me", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref, uintptr_t pred_mv, uintptr_t out_mv,
                  uintptr_t out_cost, uintptr_t out_pred, uintptr_t out_intra, uintptr_t qp, int range, int subpel,
                  uintptr_t stream, uintptr_t hp, uintptr_t aq, int planes_ready, int early_sad, uintptr_t gate_cost,
-                 int gate_thresh, uintptr_t cost_mv) {
+                 int gate_thresh, uintptr_t cost_mv, uintptr_t route, int nbuf, int role, int want) {
     if (planes_ready && !hp) throw std::invalid_argument("me: planes_ready needs the hp buffer");
+    if (route && (nbuf < 1 || role < 0 || role > 4 || (want != 0 && want != 1) || !planes_ready))
+      throw std::invalid_argument("me: a routed search needs nbuf, a role (list-0 0..3 / list-1 4), want P/B and the planes");
     mivc_launch_me(B, wmb, hmb, P<uint8_t>(src), P<uint8_t>(ref), P<int16_t>(pred_mv), P<int16_t>(out_mv),
                    P<int>(out_cost), P<uint8_t>(out_pred), P<int>(out_intra), P<int>(qp), range, subpel,
                    P<uint8_t>(hp), P<int8_t>(aq), planes_ready, early_sad, S(stream), P<int>(gate_cost), gate_thresh,
-                   P<int16_t>(cost_mv));
+                   P<int16_t>(cost_mv), P<void>(route), nbuf, role, want);
   }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("src"), py::arg("ref"), py::arg("pred_mv"),
      py::arg("out_mv"), py::arg("out_cost"), py::arg("out_pred"), py::arg("out_intra"), py::arg("qp"),
      py::arg("range"), py::arg("subpel"), py::arg("stream"), py::arg("hp") = 0, py::arg("aq") = 0,
      py::arg("planes_ready") = 0, py::arg("early_sad") = 0, py::arg("gate_cost") = 0, py::arg("gate_thresh") = 0,
-     py::arg("cost_mv") = 0);
+     py::arg("cost_mv") = 0, py::arg("route") = 0, py::arg("nbuf") = 0, py::arg("role") = 0, py::arg("want") = 0);
   m.def("me_ref_select", [](int B, int wmb, int hmb, int nref, uintptr_t mv, uintptr_t mv8, uintptr_t cost,
                             uintptr_t pred, uintptr_t xmv, uintptr_t xcost, uintptr_t xpred, uintptr_t mref,
-                            uintptr_t qp, uintptr_t aq, uintptr_t stream) {
+                            uintptr_t qp, uintptr_t aq, uintptr_t stream, uintptr_t route) {
     if (nref < 2 || nref > 4) throw std::invalid_argument("me_ref_select: nref in 2..4");
     mivc_launch_me_ref_select(B, wmb, hmb, nref, P<int16_t>(mv), P<int16_t>(mv8), P<int>(cost), P<uint8_t>(pred),
                               P<int16_t>(xmv), P<int>(xcost), P<uint8_t>(xpred), P<int8_t>(mref), P<int>(qp),
-                              P<int8_t>(aq), S(stream));
-  });
+                              P<int8_t>(aq), S(stream), P<void>(route));
+  }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("nref"), py::arg("mv"), py::arg("mv8"), py::arg("cost"),
+     py::arg("pred"), py::arg("xmv"), py::arg("xcost"), py::arg("xpred"), py::arg("mref"), py::arg("qp"), py::arg("aq"),
+     py::arg("stream"), py::arg("route") = 0);
   m.def("b_spatial", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t col, uintptr_t src, uintptr_t ref1,
                         uintptr_t hp1, std::vector<uintptr_t> ref0k, std::vector<uintptr_t> hp0k, std::vector<int> w1,
                         uintptr_t pred_out, uintptr_t err, uintptr_t stream, uintptr_t intra_cost, uintptr_t cost,
-                        uintptr_t qp, uintptr_t aq, int bias) {
+                        uintptr_t qp, uintptr_t aq, int bias, uintptr_t route, int nbuf) {
     // spatial direct: exact derivation + direct-vs-explicit decision in MB wavefront order;
-    // ref0k / hp0k / w1: every list-0 picture (entry 0 = RefPicList0[0])
+    // ref0k / hp0k / w1: every list-0 picture (entry 0 = RefPicList0[0]); routed: the pools
     const size_t n = ref0k.size();
     if (n < 1 || n > 4 || hp0k.size() != n || w1.size() != n)
       throw std::invalid_argument("b_spatial: 1..4 list-0 pictures with planes and weights");
@@ -214,30 +227,39 @@ PYBIND11_MODULE(_hip, m) {
     }
     mivc_launch_b_spatial(B, wmb, hmb, P<void>(hdr), P<void>(col), P<uint8_t>(src), P<uint8_t>(ref1), P<uint8_t>(hp1),
                           rk, hk, w1.data(), static_cast<int>(n), P<uint8_t>(pred_out), P<int>(err), S(stream),
-                          P<int>(intra_cost), P<int>(cost), P<int>(qp), P<int8_t>(aq), bias);
-  });
+                          P<int>(intra_cost), P<int>(cost), P<int>(qp), P<int8_t>(aq), bias, P<void>(route), nbuf);
+  }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("hdr"), py::arg("col"), py::arg("src"), py::arg("ref1"),
+     py::arg("hp1"), py::arg("ref0k"), py::arg("hp0k"), py::arg("w1"), py::arg("pred_out"), py::arg("err"),
+     py::arg("stream"), py::arg("intra_cost"), py::arg("cost"), py::arg("qp"), py::arg("aq"), py::arg("bias"),
+     py::arg("route") = 0, py::arg("nbuf") = 0);
   m.def("b_direct", [](int B, int wmb, int hmb, uintptr_t col, std::vector<int> dsf, std::vector<int> direct_copy,
-                       uintptr_t dmv, uintptr_t pm0, uintptr_t pm1, uintptr_t stream, uintptr_t dref) {
+                       uintptr_t dmv, uintptr_t pm0, uintptr_t pm1, uintptr_t stream, uintptr_t dref, uintptr_t route,
+                       int nbuf) {
     if (dsf.empty() || dsf.size() > 4 || dsf.size() != direct_copy.size())
       throw std::invalid_argument("b_direct: one (dsf, direct_copy) pair per list-0 picture, at most 4");
+    if (route && nbuf < 1) throw std::invalid_argument("b_direct: a routed launch needs the pool size");
     mivc_launch_b_direct(B, wmb, hmb, P<void>(col), dsf.data(), direct_copy.data(), static_cast<int>(dsf.size()),
-                         P<int16_t>(dmv), P<int8_t>(dref), P<int16_t>(pm0), P<int16_t>(pm1), S(stream));
+                         P<int16_t>(dmv), P<int8_t>(dref), P<int16_t>(pm0), P<int16_t>(pm1), S(stream), P<void>(route),
+                         nbuf);
   }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("col"), py::arg("dsf"), py::arg("direct_copy"),
-     py::arg("dmv"), py::arg("pm0"), py::arg("pm1"), py::arg("stream"), py::arg("dref") = 0);
+     py::arg("dmv"), py::arg("pm0"), py::arg("pm1"), py::arg("stream"), py::arg("dref") = 0, py::arg("route") = 0,
+     py::arg("nbuf") = 0);
   m.def("p_refine", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref, uintptr_t hp, uintptr_t mv_in,
                        uintptr_t mv_out, uintptr_t cost, uintptr_t pm, uintptr_t pred, uintptr_t qp, uintptr_t aq,
-                       uintptr_t stream) {
+                       uintptr_t stream, uintptr_t route, int nbuf) {
     if (mv_in == mv_out) throw std::invalid_argument("p_refine: mv_in and mv_out must differ (Jacobi pass)");
     mivc_launch_p_refine(B, wmb, hmb, P<uint8_t>(src), P<uint8_t>(ref), P<uint8_t>(hp), P<int16_t>(mv_in),
                          P<int16_t>(mv_out), P<int>(cost), P<int16_t>(pm), P<uint8_t>(pred), P<int>(qp),
-                         P<int8_t>(aq), S(stream));
-  });
+                         P<int8_t>(aq), S(stream), P<void>(route), nbuf);
+  }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("src"), py::arg("ref"), py::arg("hp"), py::arg("mv_in"),
+     py::arg("mv_out"), py::arg("cost"), py::arg("pm"), py::arg("pred"), py::arg("qp"), py::arg("aq"),
+     py::arg("stream"), py::arg("route") = 0, py::arg("nbuf") = 0);
   m.def("b_decide", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref0, uintptr_t ref1, uintptr_t hp0,
                        uintptr_t hp1, uintptr_t mv0, uintptr_t mv1, uintptr_t cost0, uintptr_t cost1, uintptr_t pred0,
                        uintptr_t pred1, uintptr_t pm0, uintptr_t pm1, uintptr_t dmv, uintptr_t qp, uintptr_t aq,
                        uintptr_t hdr, uintptr_t pred_out, uintptr_t cost_out, uintptr_t stream, std::vector<int> w1,
                        uintptr_t dref, std::vector<uintptr_t> ref0k, std::vector<uintptr_t> hp0k, int direct_only, int bparts, int have_direct,
-                       int spatial, int dbias) {
+                       int spatial, int dbias, uintptr_t route, int nbuf) {
     // w1: implicit list-1 weight per list-0 picture; ref0k / hp0k: luma / half-sample planes of
     // RefPicList0[1..] (direct prediction of quadrants whose co-located block used a farther picture)
     if (w1.empty() || w1.size() > 4) throw std::invalid_argument("b_decide: one implicit weight per list-0 picture");
@@ -256,20 +278,21 @@ PYBIND11_MODULE(_hip, m) {
                          P<uint8_t>(hp1), P<int16_t>(mv0), P<int16_t>(mv1), P<int>(cost0), P<int>(cost1),
                          P<uint8_t>(pred0), P<uint8_t>(pred1), P<int16_t>(pm0), P<int16_t>(pm1), P<int16_t>(dmv),
                          P<int>(qp), P<int8_t>(aq), P<void>(hdr), P<uint8_t>(pred_out), P<int>(cost_out), S(stream),
-                         w1.data(), static_cast<int>(n), n > 1 ? P<int8_t>(dref) : nullptr, rk, hk, direct_only, bparts, have_direct,
-                         spatial, dbias);
+                         w1.data(), static_cast<int>(n), (n > 1 || route) ? P<int8_t>(dref) : nullptr, rk, hk, direct_only,
+                         bparts, have_direct, spatial, dbias, P<void>(route), nbuf);
   }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("src"), py::arg("ref0"), py::arg("ref1"), py::arg("hp0"),
      py::arg("hp1"), py::arg("mv0"), py::arg("mv1"), py::arg("cost0"), py::arg("cost1"), py::arg("pred0"),
      py::arg("pred1"), py::arg("pm0"), py::arg("pm1"), py::arg("dmv"), py::arg("qp"), py::arg("aq"), py::arg("hdr"),
      py::arg("pred_out"), py::arg("cost_out"), py::arg("stream"), py::arg("w1") = std::vector<int>{32},
      py::arg("dref") = 0, py::arg("ref0k") = std::vector<uintptr_t>{}, py::arg("hp0k") = std::vector<uintptr_t>{},
-     py::arg("direct_only") = 0, py::arg("bparts") = 0, py::arg("have_direct") = 0, py::arg("spatial") = 0, py::arg("dbias") = 0);
+     py::arg("direct_only") = 0, py::arg("bparts") = 0, py::arg("have_direct") = 0, py::arg("spatial") = 0, py::arg("dbias") = 0,
+     py::arg("route") = 0, py::arg("nbuf") = 0);
   m.def("aq_offsets", [](int B, int wmb, int hmb, uintptr_t sy, uintptr_t su, uintptr_t sv, float strength,
-                         uintptr_t out, uintptr_t stream, uintptr_t extra, long long extra_stride) {
+                         uintptr_t out, uintptr_t stream, uintptr_t extra, long long extra_stride, uintptr_t route) {
     mivc_launch_aq_offsets(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), strength, P<float>(extra),
-                           extra_stride, P<int8_t>(out), S(stream));
+                           extra_stride, P<int8_t>(out), S(stream), P<void>(route));
   }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("sy"), py::arg("su"), py::arg("sv"), py::arg("strength"),
-     py::arg("out"), py::arg("stream"), py::arg("extra") = 0, py::arg("extra_stride") = 0);
+     py::arg("out"), py::arg("stream"), py::arg("extra") = 0, py::arg("extra_stride") = 0, py::arg("route") = 0);
   m.def("mbtree", [](int B, int F, int lbw, int lbh, uintptr_t blk_cost, uintptr_t blk_mv, uintptr_t prop,
                      float strength, uintptr_t out, uintptr_t stream) {
     mivc_launch_mbtree(B, F, lbw, lbh, P<int>(blk_cost), P<int>(blk_mv), P<void>(prop), strength, P<float>(out),
@@ -280,21 +303,26 @@ PYBIND11_MODULE(_hip, m) {
     mivc_launch_qp_fixup(B, wmb, hmb, P<void>(hdr), P<int16_t>(coef), P<uint8_t>(nz), P<uint8_t>(flags),
                          P<int>(slice_qp), S(stream));
   });
-  m.def("me_halfpel", [](int B, int W, int H, uintptr_t ref, uintptr_t hp, uintptr_t stream) {
-    mivc_launch_me_halfpel(B, W, H, P<uint8_t>(ref), P<uint8_t>(hp), S(stream));
-  });
+  m.def("me_halfpel", [](int B, int W, int H, uintptr_t ref, uintptr_t hp, uintptr_t stream, uintptr_t route, int nbuf) {
+    if (route && nbuf < 1) throw std::invalid_argument("me_halfpel: a routed launch needs the pool size");
+    mivc_launch_me_halfpel(B, W, H, P<uint8_t>(ref), P<uint8_t>(hp), S(stream), P<void>(route), nbuf);
+  }, py::arg("B"), py::arg("W"), py::arg("H"), py::arg("ref"), py::arg("hp"), py::arg("stream"), py::arg("route") = 0,
+     py::arg("nbuf") = 0);
   m.def("encode_inter",
         [](int B, int wmb, int hmb, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t fy, uintptr_t fu,
            uintptr_t fv, uintptr_t ry, uintptr_t ru, uintptr_t rv, uintptr_t pred, uintptr_t mv, uintptr_t me_cost,
            uintptr_t intra_cost, uintptr_t qp, int cqo, uintptr_t hdr, uintptr_t coef, uintptr_t nz,
            uintptr_t intra_flag, uintptr_t intra_count, uintptr_t stream, uintptr_t aq, uintptr_t ref1_u,
            uintptr_t ref1_v, int bmode, int t8, uintptr_t mv8, std::vector<int> w1, std::vector<uintptr_t> xref_u,
-           std::vector<uintptr_t> xref_v, uintptr_t mref, uintptr_t wp, int trellis, float trellis_lambda) {
+           std::vector<uintptr_t> xref_v, uintptr_t mref, uintptr_t wp, int trellis, float trellis_lambda,
+           uintptr_t route, int nbuf) {
           // xref_u / xref_v: chroma of RefPicList0[1..]; w1: implicit list-1 weight per list-0 picture
           if (bmode && (!ref1_u || !ref1_v)) throw std::invalid_argument("encode_inter: B mode needs the list-1 chroma");
           const size_t n = xref_u.size() + 1;
           if (n > 4 || xref_v.size() != xref_u.size()) throw std::invalid_argument("encode_inter: at most 4 list-0 pictures");
-          if (n > 1 && !bmode && !mref) throw std::invalid_argument("encode_inter: P pictures with several references need mref");
+          if ((n > 1 || route) && !bmode && !mref)
+            throw std::invalid_argument("encode_inter: P pictures with several references need mref");
+          if (route && (nbuf < 1 || n > 1)) throw std::invalid_argument("encode_inter: routed launches take pools");
           std::vector<int> w(n, w1.empty() ? 32 : w1[0]);
           for (size_t i = 0; i < n && i < w1.size(); ++i) w[i] = w1[i];
           const uint8_t* xu[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -309,7 +337,8 @@ PYBIND11_MODULE(_hip, m) {
                                    cqo, P<void>(hdr), P<int16_t>(coef), P<uint8_t>(nz), P<uint8_t>(intra_flag),
                                    P<int>(intra_count), P<int8_t>(aq), P<uint8_t>(ref1_u), P<uint8_t>(ref1_v), bmode,
                                    t8, P<int16_t>(mv8), S(stream), w.data(), static_cast<int>(n), xu, xv,
-                                   bmode ? nullptr : P<int8_t>(mref), P<int>(wp), trellis, trellis_lambda);
+                                   bmode ? nullptr : P<int8_t>(mref), P<int>(wp), trellis, trellis_lambda, P<void>(route),
+                                   nbuf);
         }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("sy"), py::arg("su"), py::arg("sv"), py::arg("fy"),
         py::arg("fu"), py::arg("fv"), py::arg("ry"), py::arg("ru"), py::arg("rv"), py::arg("pred"), py::arg("mv"),
         py::arg("me_cost"), py::arg("intra_cost"), py::arg("qp"), py::arg("cqo"), py::arg("hdr"), py::arg("coef"),
@@ -317,7 +346,7 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("ref1_u") = 0, py::arg("ref1_v") = 0, py::arg("bmode") = 0, py::arg("t8") = 0, py::arg("mv8") = 0,
         py::arg("w1") = std::vector<int>{32}, py::arg("xref_u") = std::vector<uintptr_t>{},
         py::arg("xref_v") = std::vector<uintptr_t>{}, py::arg("mref") = 0, py::arg("wp") = 0, py::arg("trellis") = 0,
-        py::arg("trellis_lambda") = 1.0f);
+        py::arg("trellis_lambda") = 1.0f, py::arg("route") = 0, py::arg("nbuf") = 0);
   m.def("wp_stats", [](uintptr_t y, uintptr_t u, uintptr_t v, int w, int h, int npics, uintptr_t out, uintptr_t stream) {
     if (w % 2 || h % 2 || (w * h) % 4) throw std::invalid_argument("wp_stats: even picture sizes");
     mivc_launch_wp_stats(P<uint8_t>(y), P<uint8_t>(u), P<uint8_t>(v), w, h, npics, P<unsigned long long>(out),
@@ -329,29 +358,33 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("p_part8", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref, uintptr_t hp, uintptr_t mv, uintptr_t pm,
                       uintptr_t cost, uintptr_t pred, uintptr_t mv8, uintptr_t qp, uintptr_t aq, int overhead,
-                      int min_satd, uintptr_t stream) {
+                      int min_satd, uintptr_t stream, uintptr_t route, int nbuf) {
     if (!hp || !mv8) throw std::invalid_argument("p_part8: needs the half-sample planes and an mv8 buffer");
     mivc_launch_p_part8(B, wmb, hmb, P<uint8_t>(src), P<uint8_t>(ref), P<uint8_t>(hp), P<int16_t>(mv), P<int16_t>(pm),
                         P<int>(cost), P<uint8_t>(pred), P<int16_t>(mv8), P<int>(qp), P<int8_t>(aq), overhead, min_satd,
-                        S(stream));
-  });
+                        S(stream), P<void>(route), nbuf);
+  }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("src"), py::arg("ref"), py::arg("hp"), py::arg("mv"),
+     py::arg("pm"), py::arg("cost"), py::arg("pred"), py::arg("mv8"), py::arg("qp"), py::arg("aq"), py::arg("overhead"),
+     py::arg("min_satd"), py::arg("stream"), py::arg("route") = 0, py::arg("nbuf") = 0);
   m.def("encode_intra", [](int B, int wmb, int hmb, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t ry,
                            uintptr_t ru, uintptr_t rv, uintptr_t qp, int cqo, uintptr_t hdr, uintptr_t coef,
                            uintptr_t nz, uintptr_t intra_flag, uintptr_t intra_count, uintptr_t err, int use_i4x4,
-                           uintptr_t stream, uintptr_t aq, int use_i8x8) {
+                           uintptr_t stream, uintptr_t aq, int use_i8x8, uintptr_t route, int nbuf) {
     mivc_launch_encode_intra(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), P<uint8_t>(ry),
                              P<uint8_t>(ru), P<uint8_t>(rv), P<int>(qp), cqo, P<void>(hdr), P<int16_t>(coef),
                              P<uint8_t>(nz), P<uint8_t>(intra_flag), P<int>(intra_count), P<int>(err), use_i4x4,
-                             P<int8_t>(aq), S(stream), use_i8x8);
+                             P<int8_t>(aq), S(stream), use_i8x8, P<void>(route), nbuf);
   }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("sy"), py::arg("su"), py::arg("sv"), py::arg("ry"),
      py::arg("ru"), py::arg("rv"), py::arg("qp"), py::arg("cqo"), py::arg("hdr"), py::arg("coef"), py::arg("nz"),
      py::arg("intra_flag"), py::arg("intra_count"), py::arg("err"), py::arg("use_i4x4"), py::arg("stream"),
-     py::arg("aq") = 0, py::arg("use_i8x8") = 0);
+     py::arg("aq") = 0, py::arg("use_i8x8") = 0, py::arg("route") = 0, py::arg("nbuf") = 0);
   m.def("deblock", [](int B, int wmb, int hmb, uintptr_t ry, uintptr_t ru, uintptr_t rv, uintptr_t hdr, uintptr_t nz,
-                      int cqo, int alpha_off, int beta_off, uintptr_t err, uintptr_t stream) {
+                      int cqo, int alpha_off, int beta_off, uintptr_t err, uintptr_t stream, uintptr_t route, int nbuf) {
     mivc_launch_deblock(B, wmb, hmb, P<uint8_t>(ry), P<uint8_t>(ru), P<uint8_t>(rv), P<void>(hdr), P<uint8_t>(nz),
-                        cqo, alpha_off, beta_off, P<int>(err), S(stream));
-  });
+                        cqo, alpha_off, beta_off, P<int>(err), S(stream), P<void>(route), nbuf);
+  }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("ry"), py::arg("ru"), py::arg("rv"), py::arg("hdr"),
+     py::arg("nz"), py::arg("cqo"), py::arg("alpha_off"), py::arg("beta_off"), py::arg("err"), py::arg("stream"),
+     py::arg("route") = 0, py::arg("nbuf") = 0);
   m.def("decode_picture_dpb", [](int B, int wmb, int hmb, int dpb_n, uintptr_t y, uintptr_t u, uintptr_t v,
                                  uintptr_t cur_idx, uintptr_t reftab, uintptr_t wp, uintptr_t sub,
                                  uintptr_t hdr, uintptr_t mask, uintptr_t off, uintptr_t coef, uintptr_t run,
@@ -565,14 +598,17 @@ PYBIND11_MODULE(_hip, m) {
   m.def("cabac_bin", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t coef, uintptr_t mask, uintptr_t nb,
                         uintptr_t cnt, uintptr_t off, uintptr_t tot, uintptr_t pool, long long pool_cap,
                         uintptr_t pool_used, uintptr_t base, uintptr_t total, uintptr_t slot_qp, int slice_type,
-                        int num_ref_l0, int num_ref_l1, int t8x8_mode, uintptr_t err, uintptr_t stream) {
+                        int num_ref_l0, int num_ref_l1, int t8x8_mode, uintptr_t err, uintptr_t stream, uintptr_t route) {
     if ((pool & 15) != 0) throw std::invalid_argument("cabac_bin: symbol pool must be 16-byte aligned");
     if (B < 1 || wmb < 1 || hmb < 1) throw std::invalid_argument("cabac_bin: bad geometry");
     mivc_launch_cabac_bin(B, wmb, hmb, P<void>(hdr), P<int16_t>(coef), P<uint32_t>(mask), P<void>(nb), P<int>(cnt),
                           P<long long>(off), P<int>(tot), P<uint16_t>(pool), pool_cap, P<long long>(pool_used),
                           P<long long>(base), P<int>(total), P<int>(slot_qp), slice_type, num_ref_l0, num_ref_l1,
-                          t8x8_mode, P<int>(err), S(stream));
-  });
+                          t8x8_mode, P<int>(err), S(stream), P<void>(route));
+  }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("hdr"), py::arg("coef"), py::arg("mask"), py::arg("nb"),
+     py::arg("cnt"), py::arg("off"), py::arg("tot"), py::arg("pool"), py::arg("pool_cap"), py::arg("pool_used"),
+     py::arg("base"), py::arg("total"), py::arg("slot_qp"), py::arg("slice_type"), py::arg("num_ref_l0"),
+     py::arg("num_ref_l1"), py::arg("t8x8_mode"), py::arg("err"), py::arg("stream"), py::arg("route") = 0);
   m.def("cabac_code", [](int L, int B, uintptr_t pool, uintptr_t base, uintptr_t total, uintptr_t hdr_bits,
                          uintptr_t hdr_nbits, uintptr_t slot_qp, unsigned long long itypes, uintptr_t bytes,
                          uintptr_t out, uintptr_t out_off, uintptr_t err, uintptr_t stream, uintptr_t host_out,
@@ -596,10 +632,12 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("cap_words"), py::arg("hdr_bits"), py::arg("hdr_nbits"), py::arg("pslice"), py::arg("slice_qp"),
      py::arg("slot_qp"), py::arg("out"), py::arg("out_off"), py::arg("stream"), py::arg("nz") = 0);
   m.def("sse", [](int B, int W, int H, int w, int h, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t ry,
-                  uintptr_t ru, uintptr_t rv, uintptr_t sse, uintptr_t ssim, uintptr_t stream) {
+                  uintptr_t ru, uintptr_t rv, uintptr_t sse, uintptr_t ssim, uintptr_t stream, uintptr_t route, int nbuf) {
     mivc_launch_sse(B, W, H, w, h, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), P<uint8_t>(ry), P<uint8_t>(ru),
-                    P<uint8_t>(rv), P<unsigned long long>(sse), P<float>(ssim), S(stream));
-  });
+                    P<uint8_t>(rv), P<unsigned long long>(sse), P<float>(ssim), S(stream), P<void>(route), nbuf);
+  }, py::arg("B"), py::arg("W"), py::arg("H"), py::arg("w"), py::arg("h"), py::arg("sy"), py::arg("su"), py::arg("sv"),
+     py::arg("ry"), py::arg("ru"), py::arg("rv"), py::arg("sse"), py::arg("ssim"), py::arg("stream"),
+     py::arg("route") = 0, py::arg("nbuf") = 0);
   m.def("lookahead_low_bytes", [](int w, int h, int n) { return mivc_lookahead_low_bytes(w, h, n); });
   m.def("lookahead", [](uintptr_t y, int w, int h, long long fstride, int n, int f, uintptr_t low, uintptr_t frame_cost,
                         uintptr_t blk_cost, int range, uintptr_t stream, uintptr_t blk_mv) {

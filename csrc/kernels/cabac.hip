@@ -62,15 +62,17 @@ struct CabacBinArgs {
   int num_ref_l0, num_ref_l1;
   int t8x8_mode;
   int* err;
+  // routed (route.h): every slot's own slice type (its picture kind) and active list-0 size
+  const SlotRoute* rt;
 };
 
 __device__ __forceinline__ CabacSliceInfo slice_info(const CabacBinArgs& a, int slot) {
   CabacSliceInfo si{};
-  si.slice_type = a.slice_type;
+  si.slice_type = a.rt ? a.rt[slot].kind : a.slice_type;
   si.wmb = a.g.wmb;
   si.hmb = a.g.hmb;
   si.first_mb = 0;
-  si.num_ref[0] = a.num_ref_l0;
+  si.num_ref[0] = a.rt ? (a.rt[slot].kind == SK_I ? 1 : a.rt[slot].n0) : a.num_ref_l0;
   si.num_ref[1] = a.num_ref_l1;
   si.t8x8_mode = a.t8x8_mode;
   si.slice_qp = a.slot_qp[slot];
@@ -539,8 +541,9 @@ extern "C" void mivc_launch_cabac_bin(int B, int wmb, int hmb, const void* hdr, 
                                       void* nb, int* cnt, long long* off, int* tot, uint16_t* pool,
                                       long long pool_cap, long long* pool_used, long long* base, int* total,
                                       const int* slot_qp, int slice_type, int num_ref_l0, int num_ref_l1,
-                                      int t8x8_mode, int* err, void* stream) {
+                                      int t8x8_mode, int* err, void* stream, const void* route) {
   CabacBinArgs a;
+  a.rt = static_cast<const SlotRoute*>(route);
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.hdr = static_cast<const MbHeader*>(hdr);
   a.coef = coef;

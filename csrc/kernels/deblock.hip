@@ -31,6 +31,10 @@ struct DeblockArgs {
   const uint8_t* bs_in;
   int dpb_n;
   const int16_t* cur_idx;
+  // encoder routing (route.h): rec_* are pools [B, nbuf, plane]; slots whose picture is not
+  // flagged SF_DEBLOCK are left alone
+  const SlotRoute* rt;
+  int nbuf;
 };
 
 constexpr int kDeblockWaves = 16;
@@ -140,6 +144,7 @@ __global__ __launch_bounds__(64 * kDeblockWaves) void deblock_wavefront(DeblockA
   __shared__ DeblockTables T;
   const Geom& g = a.g;
   const int slot = blockIdx.x;
+  if (a.rt && (a.rt[slot].kind < 0 || !(a.rt[slot].flags & SF_DEBLOCK))) return;  // uniform per workgroup
   for (int i = threadIdx.x; i < g.hmb; i += blockDim.x) prog[i] = 0;
   for (int i = threadIdx.x; i < 52; i += blockDim.x) {
     T.alpha[i] = h264::kAlpha[i];
@@ -162,7 +167,8 @@ __global__ __launch_bounds__(64 * kDeblockWaves) void deblock_wavefront(DeblockA
   const int ccomp = (hl - 16) >> 3, cline = hl & 7;                        \
   const int line = is_c ? cline : hl;
   const int W = g.W, cw = g.cw(), wmb = g.wmb, hmb = g.hmb;
-  const size_t pic = a.dpb_n ? static_cast<size_t>(slot) * a.dpb_n + a.cur_idx[slot] : static_cast<size_t>(slot);
+  const size_t pic = a.dpb_n ? static_cast<size_t>(slot) * a.dpb_n + a.cur_idx[slot]
+                             : route_index(a.rt, a.nbuf, slot, RO_CUR);
   uint8_t* recy = a.rec_y + pic * g.ysize();
   uint8_t* const rcu = a.rec_u + pic * g.csize();
   uint8_t* const rcv = a.rec_v + pic * g.csize();
@@ -449,8 +455,10 @@ using namespace mivc::gpu;
 
 extern "C" void mivc_launch_deblock(int B, int wmb, int hmb, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v,
                                     const void* hdr, const uint8_t* nz, int chroma_qp_offset, int alpha_off,
-                                    int beta_off, int* err, void* stream) {
+                                    int beta_off, int* err, void* stream, const void* route, int nbuf) {
   DeblockArgs a;
+  a.rt = static_cast<const SlotRoute*>(route);
+  a.nbuf = nbuf;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.rec_y = rec_y;
   a.rec_u = rec_u;
@@ -473,6 +481,8 @@ extern "C" void mivc_launch_deblock_dpb(int B, int wmb, int hmb, int dpb_n, uint
                                         const uint8_t* bs, int chroma_qp_offset, int alpha_off, int beta_off, int* err,
                                         void* stream) {
   DeblockArgs a;
+  a.rt = nullptr;
+  a.nbuf = 0;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.rec_y = dpb_y;
   a.rec_u = dpb_u;

@@ -54,6 +54,10 @@ struct InterArgs {
   // rate-distortion choice instead of the dead-zone rounding (trellis_lite below); 0 = off
   int trellis;
   float trellis_lambda;    // multiplier of the SSD lambda 0.85 * 2^((QP - 12) / 3)
+  // routed (route.h): ref_* / refs_* / ref1_* / rec_* are pools [B, nbuf, plane]; slots coding a
+  // P (bmode 0) or B (bmode 1) picture take their roles and implicit weights from SlotRoute
+  const SlotRoute* rt;
+  int nbuf;
 };
 
 // Rate-distortion quantisation of one 4x4 block (x264 --trellis 1, simplified to a greedy pass
@@ -175,6 +179,8 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
   const int nmb = g.nmb();
   int ux, slot;
   xcd_unit_slot(ux, slot);
+  if (!route_active(a.rt, slot, a.bmode ? SK_B : SK_P)) return;  // wave-uniform
+  const size_t rcur = route_index(a.rt, a.nbuf, slot, RO_CUR);
   const int mb = ux * 2 + half;
   const bool live = mb < nmb;
   const int mbc = live ? mb : nmb - 1;
@@ -398,7 +404,8 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
       // the 4x4 chroma block cb covers luma quadrant cb (its partition's vector)
       const int cmx = a.mv8 ? a.mv8[o * 8 + cb * 2] : mvx, cmy = a.mv8 ? a.mv8[o * 8 + cb * 2 + 1] : mvy;
       const int r = a.mref ? a.mref[o] : 0;
-      chroma_mc4x4((comp == 0 ? a.refs_u[r] : a.refs_v[r]) + slot * g.csize(), cw, CH, px0, py0, cmx, cmy, pv);
+      chroma_mc4x4((comp == 0 ? a.refs_u[r] : a.refs_v[r]) + route_index(a.rt, a.nbuf, slot, RO_L0 + r) * g.csize(), cw,
+                   CH, px0, py0, cmx, cmy, pv);
       if (a.wp && r == 0) {
         const int* wt = a.wp + slot * 8;
         const int w = wt[3 + 2 * comp], wo = wt[4 + 2 * comp], d = wt[7];
@@ -413,11 +420,13 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
       // the 4x4 chroma block cb covers luma quadrant cb: its lists and vectors
       const int r0 = h->ref[0][cb];
       const bool u0 = r0 >= 0, u1 = h->ref[1][cb] >= 0;
-      const int w1 = a.w1[r0 & 3];
+      const int w1 = a.rt ? a.rt[slot].w1[r0 & 3] : a.w1[r0 & 3];
       int p1[4][4];
-      if (u0) chroma_mc4x4((comp == 0 ? a.refs_u[r0 & 3] : a.refs_v[r0 & 3]) + slot * g.csize(), cw, CH, px0, py0,
+      if (u0) chroma_mc4x4((comp == 0 ? a.refs_u[r0 & 3] : a.refs_v[r0 & 3]) +
+                               route_index(a.rt, a.nbuf, slot, RO_L0 + (r0 & 3)) * g.csize(), cw, CH, px0, py0,
                            h->mv[0][cb][0], h->mv[0][cb][1], pv);
-      if (u1) chroma_mc4x4((comp == 0 ? a.ref1_u : a.ref1_v) + slot * g.csize(), cw, CH, px0, py0,
+      if (u1) chroma_mc4x4((comp == 0 ? a.ref1_u : a.ref1_v) + route_index(a.rt, a.nbuf, slot, RO_L1) * g.csize(), cw,
+                           CH, px0, py0,
                            h->mv[1][cb][0], h->mv[1][cb][1], p1);
 #pragma unroll
       for (int y = 0; y < 4; ++y)
@@ -513,7 +522,7 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
     wave_sync();
     const int lb8 = (lby >> 3) * 2 + (lbx >> 3), ox = lbx & 4, oy = lby & 4;
     const bool any8 = (s_t8[half][1] >> lb8) & 1;
-    uint8_t* recy = a.rec_y + slot * g.ysize() + static_cast<size_t>(Y0 + lby) * W + X0 + lbx;
+    uint8_t* recy = a.rec_y + rcur * g.ysize() + static_cast<size_t>(Y0 + lby) * W + X0 + lbx;
 #pragma unroll
     for (int y = 0; y < 4; ++y) {
       int v4[4];
@@ -538,7 +547,7 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) res[r] = keep ? (lv[r] * dv[h264::kPosClass[r]]) << (qp / 6) : 0;
     if (any) h264::inverse_core4x4(res);
-    uint8_t* recy = a.rec_y + slot * g.ysize() + static_cast<size_t>(Y0 + lby) * W + X0 + lbx;
+    uint8_t* recy = a.rec_y + rcur * g.ysize() + static_cast<size_t>(Y0 + lby) * W + X0 + lbx;
 #pragma unroll
     for (int y = 0; y < 4; ++y) {
       int v4[4];
@@ -567,7 +576,7 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
     res[0] = ((f[cb] * ls) << (qpc / 6)) >> 5;
     const bool any = any_ac || cl[0] || cl[1] || cl[2] || cl[3];
     if (any) h264::inverse_core4x4(res);
-    uint8_t* recc = (comp == 0 ? a.rec_u : a.rec_v) + slot * g.csize() + static_cast<size_t>(my * 8 + cby) * cw + mx * 8 + cbx;
+    uint8_t* recc = (comp == 0 ? a.rec_u : a.rec_v) + rcur * g.csize() + static_cast<size_t>(my * 8 + cby) * cw + mx * 8 + cbx;
 #pragma unroll
     for (int y = 0; y < 4; ++y) {
       int v4[4];
@@ -621,8 +630,11 @@ extern "C" void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t*
                                          const int8_t* aq, const uint8_t* ref1_u, const uint8_t* ref1_v, int bmode,
                                          int t8, const int16_t* mv8, void* stream, const int* w1, int nref,
                                          const uint8_t* const* xref_u, const uint8_t* const* xref_v,
-                                         const int8_t* mref, const int* wp, int trellis, float trellis_lambda) {
+                                         const int8_t* mref, const int* wp, int trellis, float trellis_lambda,
+                                         const void* route, int nbuf) {
   InterArgs a;
+  a.rt = static_cast<const SlotRoute*>(route);
+  a.nbuf = nbuf;
   a.trellis = trellis;
   a.trellis_lambda = trellis_lambda;
   a.wp = bmode ? nullptr : wp;

@@ -41,6 +41,8 @@ struct IntraArgs {
   int* err;
   int use_i4x4;
   int use_i8x8;  // High profile: Intra8x8 trial (x264 --partitions i8x8, with --8x8dct)
+  const SlotRoute* rt;  // routed (route.h): rec_* are pools, each slot's current picture
+  int nbuf;
 };
 
 constexpr int TS = kTileStride;
@@ -153,7 +155,8 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
   const int lambda = h264::kLambda[qp];
   const int qbits = 15 + qp / 6, qbits_c = 15 + qpc / 6;
   const uint8_t* srcy = a.src_y + slot * g.ysize();
-  uint8_t* recy = a.rec_y + slot * g.ysize();
+  const size_t rcur = route_index(a.rt, a.nbuf, slot, RO_CUR);
+  uint8_t* recy = a.rec_y + rcur * g.ysize();
   int mbav = 0;
   if (mx > 0) mbav |= h264::AV_LEFT;
   if (my > 0) mbav |= h264::AV_TOP;
@@ -187,13 +190,13 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
   }
   if (lane < 18) {  // chroma neighbours: top-left + top
     int c = lane / 9, i = lane % 9;
-    const uint8_t* rc = (c == 0 ? a.rec_u : a.rec_v) + slot * g.csize();
+    const uint8_t* rc = (c == 0 ? a.rec_u : a.rec_v) + rcur * g.csize();
     int x = mx * 8 - 1 + i;
     bool ok = my > 0 && x >= 0;
     S.ctop[c][i] = ok ? rc[static_cast<size_t>(my * 8 - 1) * cw + x] : 0;
   } else if (lane >= 48) {  // chroma left
     int c = (lane - 48) >> 3, i = (lane - 48) & 7;
-    const uint8_t* rc = (c == 0 ? a.rec_u : a.rec_v) + slot * g.csize();
+    const uint8_t* rc = (c == 0 ? a.rec_u : a.rec_v) + rcur * g.csize();
     uint8_t v = 0;
     if (mx > 0) v = S.saved_x == mx - 1 ? S.saved_c[c][i] : rc[static_cast<size_t>(my * 8 + i) * cw + mx * 8 - 1];
     S.cleft[c][i] = v;
@@ -621,7 +624,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
 #pragma unroll
     for (int x = 0; x < 4; ++x) word |= static_cast<uint32_t>(h264::clip1(pr[x] + v[x])) << (8 * x);
     if (lane < 32) {
-      uint8_t* recc = (ccomp == 0 ? a.rec_u : a.rec_v) + slot * g.csize();
+      uint8_t* recc = (ccomp == 0 ? a.rec_u : a.rec_v) + rcur * g.csize();
       *reinterpret_cast<uint32_t*>(recc + static_cast<size_t>(my * 8 + cby + gy) * cw + mx * 8 + cbx) = word;
       if (cb & 1) S.saved_c[ccomp][(cb >> 1) * 4 + gy] = static_cast<uint8_t>(word >> 24);
     }
@@ -654,7 +657,8 @@ __global__ __launch_bounds__(64 * kIntraWaves) void encode_intra_wavefront(Intra
   __shared__ int prog[kMaxRows];
   const Geom& g = a.g;
   const int slot = blockIdx.x;
-  if (a.intra_flag && a.intra_count[slot] == 0) return;  // uniform per workgroup
+  if (!route_active(a.rt, slot, -1)) return;  // uniform per workgroup
+  if (a.intra_flag && a.intra_count[slot] == 0) return;
   for (int i = threadIdx.x; i < g.hmb; i += blockDim.x) prog[i] = 0;
   const int w = wave_id();
   if (lane_id() == 0) SS[w].saved_x = -2;
@@ -706,8 +710,10 @@ extern "C" void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t*
                                          const uint8_t* src_v, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v,
                                          const int* qp, int chroma_qp_offset, void* hdr, int16_t* coef, uint8_t* nz,
                                          const uint8_t* intra_flag, const int* intra_count, int* err, int use_i4x4,
-                                         const int8_t* aq, void* stream, int use_i8x8) {
+                                         const int8_t* aq, void* stream, int use_i8x8, const void* route, int nbuf) {
   IntraArgs a;
+  a.rt = static_cast<const SlotRoute*>(route);
+  a.nbuf = nbuf;
   a.aq = aq;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.src_y = src_y;

@@ -18,6 +18,10 @@ struct PrepArgs {
   uint8_t* out_v;
   int ow, oh;           // output display size (== w, h: inputs arrive resampled)
   int W, H;             // coded size
+  // per-slot frame selection (per-slot GOP plans: every slot codes its own display picture
+  // this step): input frame n starts fsel[n] frames after in_* + n * in_frame_stride (nullable)
+  const int* fsel;
+  int64_t fstep_y, fstep_c;
 };
 
 // Copy + edge replication into the coded padding (resampling runs before, in scale.hip).
@@ -31,6 +35,7 @@ __global__ void prep_plane(PrepArgs a, int plane) {
   int w = a.w >> sh, h = a.h >> sh;
   const uint8_t* in = plane == 0 ? a.in_y : (plane == 1 ? a.in_u : a.in_v);
   in += n * (plane ? a.in_frame_stride_c : a.in_frame_stride_y);
+  if (a.fsel) in += a.fsel[n] * (plane ? a.fstep_c : a.fstep_y);
   uint8_t* out = plane == 0 ? a.out_y : (plane == 1 ? a.out_u : a.out_v);
   out += static_cast<size_t>(n) * W * H;
   int cx = min(x, w - 1), cy = min(y, h - 1);
@@ -48,6 +53,7 @@ __global__ void prep_plane_copy16(PrepArgs a, int plane) {
   int w = a.w >> sh, h = a.h >> sh;
   const uint8_t* in = plane == 0 ? a.in_y : (plane == 1 ? a.in_u : a.in_v);
   in += n * (plane ? a.in_frame_stride_c : a.in_frame_stride_y);
+  if (a.fsel) in += a.fsel[n] * (plane ? a.fstep_c : a.fstep_y);
   uint8_t* out = plane == 0 ? a.out_y : (plane == 1 ? a.out_u : a.out_v);
   out += static_cast<size_t>(n) * W * H + static_cast<size_t>(y) * W + x;
   const uint8_t* row = in + static_cast<size_t>(min(y, h - 1)) * w;
@@ -91,8 +97,9 @@ using namespace mivc::gpu;
 
 extern "C" void mivc_launch_prep(const uint8_t* in_y, const uint8_t* in_u, const uint8_t* in_v, int w, int h,
                                  int64_t in_stride_y, int64_t in_stride_c, int nframes, uint8_t* out_y, uint8_t* out_u,
-                                 uint8_t* out_v, int ow, int oh, int W, int H, void* stream) {
-  PrepArgs a{in_y, in_u, in_v, w, h, in_stride_y, in_stride_c, out_y, out_u, out_v, ow, oh, W, H};
+                                 uint8_t* out_v, int ow, int oh, int W, int H, void* stream, const int* fsel) {
+  PrepArgs a{in_y, in_u, in_v, w, h, in_stride_y, in_stride_c, out_y, out_u, out_v, ow, oh, W, H,
+             fsel, static_cast<int64_t>(w) * h, static_cast<int64_t>(w / 2) * (h / 2)};
   hipStream_t s = static_cast<hipStream_t>(stream);
   bool aligned = (w % 32 == 0) && (in_stride_y % 16 == 0) && (in_stride_c % 16 == 0) &&
                  (reinterpret_cast<uintptr_t>(in_y) % 16 == 0) && (reinterpret_cast<uintptr_t>(in_u) % 16 == 0) &&

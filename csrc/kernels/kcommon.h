@@ -7,6 +7,7 @@
 #include "../common/h264_mb.h"
 #include "../common/h264_pred.h"
 #include "../common/h264_tables.h"
+#include "route.h"
 
 namespace mivc {
 namespace gpu {
@@ -29,6 +30,17 @@ struct FrameBatch {
   uint8_t* u;
   uint8_t* v;
 };
+
+// routed launches (route.h): does `slot` take part -- its picture this step is of `kind`
+// (kind < 0: any coded picture)?  Unrouted launches: every slot.
+__device__ __forceinline__ bool route_active(const SlotRoute* rt, int slot, int kind) {
+  if (!rt) return true;
+  const int k = rt[slot].kind;
+  return kind < 0 ? k >= 0 : k == kind;
+}
+
+// half-sample planes of one picture: [3, H + 8, W + 8] (me_halfpel_planes, margin 4)
+__host__ __device__ inline size_t hp_plane_bytes(int W, int H) { return static_cast<size_t>(3) * (W + 8) * (H + 8); }
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 

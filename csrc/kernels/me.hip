@@ -51,6 +51,11 @@ struct MeArgs {
   // centred on the distance-scaled list-0[0] vector, while its mvd is coded against the
   // neighbours' vectors (which mostly point to RefPicList0[0])
   const int16_t* cost_mv;
+  // routing (route.h; rt null: uniform launch): ref_y / hp are pools [B, nbuf, plane], the
+  // searched picture is role `role` of each slot, and only slots coding a `want` picture (and,
+  // for RefPicList0[role], with more than `role` active entries) are searched
+  const SlotRoute* rt;
+  int nbuf, role, want;
 };
 
 constexpr int kNoCost = 0x3FFFFFFF;
@@ -248,15 +253,19 @@ __device__ __forceinline__ void hp_load_row(const uint8_t* fr, int W, int H, int
   }
 }
 
+// routed (rt): the current picture of every slot coding a reference picture (SF_REF), from and
+// into the pools [B, nbuf, plane]
 __global__ __launch_bounds__(256) void me_halfpel_planes(const uint8_t* __restrict__ ref, int W, int H,
-                                                         uint8_t* __restrict__ hp) {
+                                                         uint8_t* __restrict__ hp, const SlotRoute* rt, int nbuf) {
   const int PW = W + 2 * kHpM, PH = H + 2 * kHpM;
   const int q = blockIdx.x * 64 + (threadIdx.x & 63);
   const int py0 = (blockIdx.y * 4 + (threadIdx.x >> 6)) * kHpRows;
   if (q >= PW / 4 || py0 >= PH) return;
   const int slot = blockIdx.z;
+  if (rt && (rt[slot].kind < 0 || !(rt[slot].flags & SF_REF))) return;
+  const size_t pslot = route_index(rt, nbuf, slot, RO_CUR);
   const int x0 = 4 * q - kHpM, y0 = py0 - kHpM;
-  const uint8_t* fr = ref + static_cast<size_t>(slot) * W * H;
+  const uint8_t* fr = ref + pslot * W * H;
   const bool xin = x0 - 4 >= 0 && x0 + 8 <= W;
   // window: source rows y-2 .. y+3 (p) and their horizontal 6-tap sums (b1)
   int p[6][9], b1[6][4];
@@ -269,7 +278,7 @@ __global__ __launch_bounds__(256) void me_halfpel_planes(const uint8_t* __restri
                                 p[r + 1][k + 5]);
   }
   const size_t plane = static_cast<size_t>(PW) * PH;
-  uint8_t* o = hp + static_cast<size_t>(slot) * 3 * plane + static_cast<size_t>(py0) * PW + 4 * q;
+  uint8_t* o = hp + pslot * 3 * plane + static_cast<size_t>(py0) * PW + 4 * q;
 #pragma unroll
   for (int t = 0; t < kHpRows; ++t) {
 #pragma unroll
@@ -323,8 +332,13 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   const int mx = mb % g.wmb, my = mb / g.wmb;
   const int lane = threadIdx.x;
   const int X0 = mx * 16, Y0 = my * 16;
+  if (a.rt) {  // wave-uniform: this slot codes another picture type / has no such reference
+    const SlotRoute& rr = a.rt[slot];
+    if (rr.kind != a.want || (a.role < RO_L1 && a.role >= rr.n0)) return;
+  }
+  const size_t rslot = route_index(a.rt, a.nbuf, slot, a.role);
   const uint8_t* src = a.src_y + slot * g.ysize();
-  const uint8_t* ref = a.ref_y + slot * g.ysize();
+  const uint8_t* ref = a.ref_y + rslot * g.ysize();
   const int W = g.W, H = g.H;
   const int qp = clampi(a.qp[slot] + (a.aq ? a.aq[static_cast<size_t>(slot) * nmb + mb] : 0), 0, 51);
   const int lambda = h264::kLambda[qp];
@@ -552,7 +566,7 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   // this kernel's instructions).  P(u, v) = plane at (X0+bx-2+u, Y0+by-2+v).
   {
     const int PW = W + 2 * kHpM, PH = H + 2 * kHpM;
-    const uint8_t* hp = a.hp + static_cast<size_t>(slot) * 3 * PW * PH;
+    const uint8_t* hp = a.hp + rslot * 3 * PW * PH;
     const int x0 = X0 + bx - 2, y0 = Y0 + by - 2;  // frame coordinates of P(0, 0)
     // aligned words covering bytes x0 .. x0 + 19 of every row: 6 per row from xa = x0 & ~3
     const int xa = x0 & ~3;
@@ -731,17 +745,20 @@ struct RefSelArgs {
   int8_t* mref;                // [B, nmb]
   const int* qp;               // [B]
   const int8_t* aq;            // [B, nmb] (nullable)
+  const SlotRoute* rt;         // routed: P slots only, each with its own active list-0 size
 };
 
 __global__ __launch_bounds__(64) void me_ref_select(RefSelArgs a) {
   const int nmb = a.g.nmb();
   const int mb = blockIdx.x, slot = blockIdx.y, lane = threadIdx.x;
+  if (!route_active(a.rt, slot, SK_P)) return;
+  const int nref = a.rt ? min(a.nref, static_cast<int>(a.rt[slot].n0)) : a.nref;
   const size_t o = static_cast<size_t>(slot) * nmb + mb;
   const size_t plane = static_cast<size_t>(a.g.B) * nmb;
   const int qp = clampi(a.qp[slot] + (a.aq ? a.aq[o] : 0), 0, 51);
   const int lambda = h264::kLambda[qp];
   int best = a.cost[o] + lambda, bk = 0;
-  for (int k = 1; k < a.nref; ++k) {
+  for (int k = 1; k < nref; ++k) {
     const int c = a.xcost[(k - 1) * plane + o];
     if (c >= kNoCost) continue;
     const int ck = c + lambda * (k + 2);
@@ -783,17 +800,20 @@ using namespace mivc::gpu;
 
 // b / h / j planes of B reference pictures into hp ([B, 3, H + 8, W + 8], margin 4)
 // b / h / j planes of B reference pictures into hp ([B, 3, H + 8, W + 8], margin 4)
-extern "C" void mivc_launch_me_halfpel(int B, int W, int H, const uint8_t* ref_y, uint8_t* hp, void* stream) {
+extern "C" void mivc_launch_me_halfpel(int B, int W, int H, const uint8_t* ref_y, uint8_t* hp, void* stream,
+                                       const void* route, int nbuf) {
   const int PW = W + 2 * kHpM, PH = H + 2 * kHpM;
   const dim3 grid((PW / 4 + 63) / 64, (PH + 4 * kHpRows - 1) / (4 * kHpRows), B);
-  hipLaunchKernelGGL(me_halfpel_planes, grid, dim3(256), 0, static_cast<hipStream_t>(stream), ref_y, W, H, hp);
+  hipLaunchKernelGGL(me_halfpel_planes, grid, dim3(256), 0, static_cast<hipStream_t>(stream), ref_y, W, H, hp,
+                     static_cast<const SlotRoute*>(route), nbuf);
 }
 
 extern "C" void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref_y,
                                const int16_t* pred_mv, int16_t* out_mv, int* out_cost, uint8_t* out_pred,
                                int* out_intra_cost, const int* qp, int range, int subpel, uint8_t* hp_buf,
                                const int8_t* aq, int planes_ready, int early_sad, void* stream,
-                               const int* gate_cost, int gate_thresh, const int16_t* cost_mv) {
+                               const int* gate_cost, int gate_thresh, const int16_t* cost_mv, const void* route,
+                               int nbuf, int role, int want) {
   // hp_buf: caller-owned [B, 3, H + 8, W + 8] (+64 bytes slack) half-sample plane scratch,
   // resident across frames; nullptr -> stream-ordered scratch for this call only.
   // planes_ready: hp_buf already holds ref_y's planes (an anchor's planes are built once
@@ -809,7 +829,11 @@ extern "C" void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, co
       abort();
     }
   }
-  if (!(planes_ready && hp_buf)) mivc_launch_me_halfpel(B, W, H, ref_y, hp, stream);
+  if (route && !(planes_ready && hp_buf)) {
+    fprintf(stderr, "mivc_launch_me: a routed search needs the resident half-sample pool\n");
+    abort();
+  }
+  if (!(planes_ready && hp_buf)) mivc_launch_me_halfpel(B, W, H, ref_y, hp, stream, nullptr, 0);
   MeArgs a;
   a.g = Geom{B, wmb, hmb, W, H};
   a.src_y = src_y;
@@ -828,6 +852,10 @@ extern "C" void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, co
   a.gate_cost = gate_cost;
   a.gate_thresh = gate_thresh;
   a.cost_mv = cost_mv;
+  a.rt = static_cast<const SlotRoute*>(route);
+  a.nbuf = nbuf;
+  a.role = role;
+  a.want = want;
   if (a.range <= 8) hipLaunchKernelGGL(me_p16x16<8>, dim3(wmb * hmb, B), dim3(64), 0, s, a);
   else hipLaunchKernelGGL(me_p16x16<kMaxR>, dim3(wmb * hmb, B), dim3(64), 0, s, a);
   if (!hp_buf) (void)hipFreeAsync(hp, s);
@@ -835,8 +863,10 @@ extern "C" void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, co
 
 extern "C" void mivc_launch_me_ref_select(int B, int wmb, int hmb, int nref, int16_t* mv, int16_t* mv8, int* cost,
                                           uint8_t* pred, const int16_t* xmv, const int* xcost, const uint8_t* xpred,
-                                          int8_t* mref, const int* qp, const int8_t* aq, void* stream) {
+                                          int8_t* mref, const int* qp, const int8_t* aq, void* stream,
+                                          const void* route) {
   RefSelArgs a;
+  a.rt = static_cast<const SlotRoute*>(route);
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.nref = nref;
   a.mv = mv;

@@ -22,22 +22,26 @@ __device__ __forceinline__ unsigned sq_diff16(uint4 a, uint4 b, int valid) {
 
 __global__ void sse_planes(const uint8_t* sy, const uint8_t* su, const uint8_t* sv, const uint8_t* ry,
                            const uint8_t* ru, const uint8_t* rv, int W, int H, int w, int h,
-                           unsigned long long* sse) {
+                           unsigned long long* sse, const SlotRoute* rt, int nbuf) {
   const int slot = blockIdx.y;
+  if (!route_active(rt, slot, -1)) return;
+  // source [B, plane]; reconstruction: [B, plane], or the slot's current picture of the pool (rt)
+  const size_t ro = route_index(rt, nbuf, slot, RO_CUR);
   const size_t yo = static_cast<size_t>(slot) * W * H, co = static_cast<size_t>(slot) * (W / 2) * (H / 2);
+  const size_t ryo = ro * W * H, rco = ro * (W / 2) * (H / 2);
   unsigned long long acc[3] = {0, 0, 0};
   const int chunks_y = (w + 15) / 16, chunks_c = (w / 2 + 15) / 16;
   const int tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
   for (int i = tid; i < chunks_y * h; i += nth) {
     int r = i / chunks_y, c = (i % chunks_y) * 16;
     size_t off = yo + static_cast<size_t>(r) * W + c;
-    acc[0] += sq_diff16(*reinterpret_cast<const uint4*>(sy + off), *reinterpret_cast<const uint4*>(ry + off), w - c);
+    acc[0] += sq_diff16(*reinterpret_cast<const uint4*>(sy + off), *reinterpret_cast<const uint4*>(ry + off - yo + ryo), w - c);
   }
   for (int i = tid; i < chunks_c * (h / 2); i += nth) {
     int r = i / chunks_c, c = (i % chunks_c) * 16;
     size_t off = co + static_cast<size_t>(r) * (W / 2) + c;
-    acc[1] += sq_diff16(*reinterpret_cast<const uint4*>(su + off), *reinterpret_cast<const uint4*>(ru + off), w / 2 - c);
-    acc[2] += sq_diff16(*reinterpret_cast<const uint4*>(sv + off), *reinterpret_cast<const uint4*>(rv + off), w / 2 - c);
+    acc[1] += sq_diff16(*reinterpret_cast<const uint4*>(su + off), *reinterpret_cast<const uint4*>(ru + off - co + rco), w / 2 - c);
+    acc[2] += sq_diff16(*reinterpret_cast<const uint4*>(sv + off), *reinterpret_cast<const uint4*>(rv + off - co + rco), w / 2 - c);
   }
   __shared__ unsigned long long red[3][4];
   for (int p = 0; p < 3; ++p) {
@@ -54,8 +58,11 @@ __global__ void sse_planes(const uint8_t* sy, const uint8_t* su, const uint8_t* 
 }
 
 // SSIM over non-overlapping 8x8 luma windows; ssim_sum: [B] float accumulators, count in windows
-__global__ void ssim8(const uint8_t* sy, const uint8_t* ry, int W, int H, int w, int h, float* ssim_sum) {
+__global__ void ssim8(const uint8_t* sy, const uint8_t* ry, int W, int H, int w, int h, float* ssim_sum,
+                      const SlotRoute* rt, int nbuf) {
   int slot = blockIdx.y;
+  if (!route_active(rt, slot, -1)) return;
+  const size_t ryo = route_index(rt, nbuf, slot, RO_CUR) * W * H;
   int wx = blockIdx.x * blockDim.x + threadIdx.x;
   int nwx = w / 8, nwy = h / 8;
   float s = 0.f;
@@ -65,7 +72,7 @@ __global__ void ssim8(const uint8_t* sy, const uint8_t* ry, int W, int H, int w,
     float ma = 0, mb = 0, va = 0, vb = 0, cov = 0;
     for (int y = 0; y < 8; ++y)
       for (int x = 0; x < 8; ++x) {
-        float A = sy[yo + static_cast<size_t>(by + y) * W + bx + x], B = ry[yo + static_cast<size_t>(by + y) * W + bx + x];
+        float A = sy[yo + static_cast<size_t>(by + y) * W + bx + x], B = ry[ryo + static_cast<size_t>(by + y) * W + bx + x];
         ma += A;
         mb += B;
         va += A * A;
@@ -91,11 +98,12 @@ using namespace mivc::gpu;
 
 extern "C" void mivc_launch_sse(int B, int W, int H, int w, int h, const uint8_t* sy, const uint8_t* su,
                                 const uint8_t* sv, const uint8_t* ry, const uint8_t* ru, const uint8_t* rv,
-                                unsigned long long* sse, float* ssim_sum, void* stream) {
+                                unsigned long long* sse, float* ssim_sum, void* stream, const void* route, int nbuf) {
   hipStream_t s = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(sse_planes, dim3(32, B), dim3(256), 0, s, sy, su, sv, ry, ru, rv, W, H, w, h, sse);
+  const SlotRoute* rt = static_cast<const SlotRoute*>(route);
+  hipLaunchKernelGGL(sse_planes, dim3(32, B), dim3(256), 0, s, sy, su, sv, ry, ru, rv, W, H, w, h, sse, rt, nbuf);
   if (ssim_sum) {
     int nwin = (w / 8) * (h / 8);
-    hipLaunchKernelGGL(ssim8, dim3((nwin + 255) / 256, B), dim3(256), 0, s, sy, ry, W, H, w, h, ssim_sum);
+    hipLaunchKernelGGL(ssim8, dim3((nwin + 255) / 256, B), dim3(256), 0, s, sy, ry, W, H, w, h, ssim_sum, rt, nbuf);
   }
 }

@@ -1,8 +1,11 @@
 """GOP structure shared by the H.264 and HEVC encoders: closed GOPs in coding order.
 
-An I picture, then P anchors every ``bframes + 1`` display pictures (and at the last
-picture and at forced anchors such as scene cuts), each followed in coding order by the
-non-reference B pictures before it -- x264 / x265 ``--b-adapt 0`` without a pyramid.
+An I picture, then P anchors (every ``bframes + 1`` display pictures for x264's fixed
+``--b-adapt 0`` pattern, wherever the lookahead put them for ``--b-adapt 1``, and at the
+last picture and at forced anchors such as scene cuts), each followed in coding order by
+the B pictures before it; with ``--b-pyramid`` the middle B of a run is a reference
+picture coded first.  H.264 plans are per slot (models/h264_gpu.py routes every slot of a
+batch through its own plan).
 """
 from __future__ import annotations
 
@@ -11,36 +14,45 @@ from dataclasses import dataclass
 
 @dataclass(frozen=True)
 class PicPlan:
-    """One picture of a closed GOP in coding order."""
+    """One picture of an H.264 closed GOP in coding order (one slot's plan, models/h264_gpu.py).
+
+    ``refs0`` / ``refs1``: display indices of the active RefPicList0 / RefPicList1 entries
+    (nearest first); ``buf``: the reconstruction pool buffer of the picture (reference
+    pictures own theirs while they are in the DPB; every non-reference B uses the scratch
+    buffer), ``bufs0`` / ``buf1`` those of its references; ``mod_l0``: the
+    ref_pic_list_modification commands that turn the default (PicNum) list-0 order into the
+    POC-distance order, empty when they agree."""
     d: int          # display index
     kind: str       # "I", "P" or "B"
     frame_num: int
     poc: int        # PicOrderCnt (2 * display index)
-    anchor: int     # I / P: anchor ordinal (its recon / half-sample buffer is anchor & 1); B: -1
+    anchor: int     # I / P: anchor ordinal; B: -1
     l0: int = -1    # display index of RefPicList0[0] (P, B)
     l1: int = -1    # display index of RefPicList1[0] (B)
-    l1_anchor: int = -1  # B: anchor ordinal of RefPicList1[0]
+    l1_anchor: int = -1  # B: anchor ordinal of RefPicList1[0] (-1 when it is a reference B)
+    ref: bool = False    # referenced by later pictures (I, P, a pyramid's reference B)
+    refs0: tuple = ()
+    refs1: tuple = ()
+    buf: int = -1
+    bufs0: tuple = ()
+    buf1: int = -1
+    mod_l0: tuple = ()
 
     @property
     def slice_type(self) -> int:  # SliceType (csrc/common/h264_mb.h)
         return {"P": 0, "B": 1, "I": 2}[self.kind]
 
     @property
-    def nal_ref_idc(self) -> int:
-        return {"I": 3, "P": 2, "B": 0}[self.kind]
+    def nal_ref_idc(self) -> int:  # x264: I 3, P 2, reference B 1, B 0
+        return {"I": 3, "P": 2, "B": 1 if self.ref else 0}[self.kind]
 
 
-def gop_plan(frames: int, bframes: int, anchors_at=()) -> list[PicPlan]:
-    """Coding order of a closed GOP of ``frames`` pictures: I0, then every anchor (P at
-    display indices 0, bframes + 1, ... and the last picture) followed by the B pictures
-    before it (x264's fixed --b-adapt 0 pattern, no pyramid).  frame_num counts reference
-    pictures (clause 7.4.3); B pictures are non-reference.
-
-    anchors_at: extra display indices that must be anchors.  A picture d that is an anchor
-    ends a coding-order prefix holding exactly pictures 0..d, so a segment shorter than the
-    batch (padded to F frames) is cut there (SegmentResult.display_prefix)."""
+def fixed_types(frames: int, bframes: int, anchors_at=()) -> str:
+    """Display-order picture types of x264's fixed --b-adapt 0 pattern: I0, P every
+    ``bframes + 1`` pictures and at the last picture and at ``anchors_at``, B between them
+    (runs never longer than ``bframes``)."""
     if frames < 1:
-        return []
+        return ""
     step = max(0, int(bframes)) + 1
     anchors = set(range(0, frames, step)) | {frames - 1} | {int(d) for d in anchors_at if 0 <= int(d) < frames}
     if step > 1:  # keep every B run <= bframes after inserting the extra anchors
@@ -51,18 +63,105 @@ def gop_plan(frames: int, bframes: int, anchors_at=()) -> list[PicPlan]:
                 out_a.append(prev)
             out_a.append(a)
             prev = a
-        anchors = out_a
-    else:
-        anchors = sorted(anchors)
-    out = [PicPlan(0, "I", 0, 0, 0)]
-    fn = 1
-    for i in range(1, len(anchors)):
-        a0, a1 = anchors[i - 1], anchors[i]
-        out.append(PicPlan(a1, "P", fn & 0xFFFF, 2 * a1, i, l0=a0))
-        fn += 1
-        for d in range(a0 + 1, a1):
-            out.append(PicPlan(d, "B", fn & 0xFFFF, 2 * d, -1, l0=a0, l1=a1, l1_anchor=i))
+        anchors = set(out_a)
+    return "".join("I" if d == 0 else ("P" if d in anchors else "B") for d in range(frames))
+
+
+def dpb_frames(refs: int, pyramid: bool, bframes: int) -> int:
+    """max_num_ref_frames of the stream (the SPS value, csrc/host/cpu_encoder.cc): the active
+    references plus one when B pictures are on (a reference B or the next anchor's slot)."""
+    return max(1, int(refs)) + (1 if int(bframes) > 0 else 0)
+
+
+def h264_plan(types: str, refs: int = 1, pyramid: bool = False, nref_frames: int | None = None) -> list[PicPlan]:
+    """Coding-order plan of one closed GOP from its display-order picture types (``"IBBBP..."``,
+    an I at 0, P anchors, B pictures between them).
+
+    * Coding order: every anchor, then the B pictures before it -- with ``pyramid`` (x264
+      --b-pyramid normal) and a run of two or more, its middle picture first, as a reference B
+      (list 0 = the earlier anchor, list 1 = the new one), the others between it and the anchors.
+    * frame_num counts reference pictures (7.4.3); the DPB is a sliding window of
+      ``nref_frames`` frames (8.2.5.3), simulated to give every picture its buffer.
+    * P lists: the DPB's pictures nearest first in POC (x264's distance order), the first
+      ``refs``; a ref_pic_list_modification is emitted where the default PicNum order differs
+      (a P after a reference B).  B lists: the default order (POC below the picture, nearest
+      first, at most ``refs``; list 1 = the nearest picture above), no modification."""
+    n = len(types)
+    if n == 0:
+        return []
+    if types[0] != "I" or any(t not in "PB" for t in types[1:]) or types[-1] == "B":
+        raise ValueError(f"h264_plan: types must be I, then P / B, ending on an anchor: {types!r}")
+    refs = max(1, int(refs))
+    nb = max((len(r) for r in types[1:].split("P") + types[1:].split("I")), default=0)
+    if nref_frames is None:
+        nref_frames = dpb_frames(refs, pyramid, nb)
+    nbuf_ref = nref_frames + 1
+    anchors = [d for d, t in enumerate(types) if t != "B"]
+    # (display, kind, ref) in coding order
+    seq = [(0, "I", True)]
+    for a0, a1 in zip(anchors, anchors[1:]):
+        seq.append((a1, types[a1], True))
+        run = list(range(a0 + 1, a1))
+        if pyramid and len(run) >= 2:
+            mid = (a0 + a1) // 2
+            seq.append((mid, "B", True))
+            seq += [(d, "B", False) for d in run if d != mid]
+        else:
+            seq += [(d, "B", False) for d in run]
+    out: list[PicPlan] = []
+    dpb: list[tuple[int, int, int]] = []  # (display, frame_num, buffer) of the reference pictures
+    prev_ref_fn = -1
+    anchor_ord = {}
+    for d, kind, ref in seq:
+        if kind == "I":
+            dpb, fn = [], 0
+        else:
+            fn = (prev_ref_fn + 1) & 0xFFFF
+        if kind != "B":
+            anchor_ord[d] = len(anchor_ord)
+        used = {b for _, _, b in dpb}
+        buf = next(b for b in range(nbuf_ref) if b not in used) if ref else nbuf_ref
+        refs0: tuple = ()
+        refs1: tuple = ()
+        mods: tuple = ()
+        if kind == "P":
+            order = sorted(dpb, key=lambda e: -e[0])[:refs]
+            refs0 = tuple(e[0] for e in order)
+            default = sorted(dpb, key=lambda e: -e[1])[:len(order)]
+            if [e[0] for e in default] != list(refs0):
+                cmds, pred = [], fn
+                for _, pn, _ in order:
+                    cmds.append((0, pred - pn - 1) if pn < pred else (1, pn - pred - 1))
+                    pred = pn
+                mods = tuple(cmds)
+        elif kind == "B":
+            below = sorted((e for e in dpb if e[0] < d), key=lambda e: -e[0])[:refs]
+            above = sorted((e for e in dpb if e[0] > d), key=lambda e: e[0])[:1]
+            refs0 = tuple(e[0] for e in below)
+            refs1 = tuple(e[0] for e in above)
+        bof = {e[0]: e[2] for e in dpb}
+        l1 = refs1[0] if refs1 else -1
+        out.append(PicPlan(d, kind, fn, 2 * d, anchor_ord.get(d, -1) if kind != "B" else -1,
+                           l0=refs0[0] if refs0 else -1, l1=l1,
+                           l1_anchor=anchor_ord.get(l1, -1) if kind == "B" else -1, ref=ref, refs0=refs0,
+                           refs1=refs1, buf=buf, bufs0=tuple(bof[r] for r in refs0), buf1=bof.get(l1, -1),
+                           mod_l0=mods))
+        if ref:
+            prev_ref_fn = fn
+            dpb.append((d, fn, buf))
+            if len(dpb) > nref_frames:  # sliding window: drop the smallest FrameNumWrap
+                dpb.remove(min(dpb, key=lambda e: e[1]))
     return out
+
+
+def gop_plan(frames: int, bframes: int, anchors_at=(), refs: int = 1, pyramid: bool = False) -> list[PicPlan]:
+    """Coding order of a closed GOP of ``frames`` pictures with x264's fixed --b-adapt 0
+    pattern (:func:`fixed_types`, :func:`h264_plan`).
+
+    anchors_at: extra display indices that must be anchors.  A picture d that is an anchor
+    ends a coding-order prefix holding exactly pictures 0..d, so a segment shorter than the
+    batch (padded to F frames) is cut there (SegmentResult.display_prefix)."""
+    return h264_plan(fixed_types(frames, bframes, anchors_at), refs, pyramid)
 
 
 @dataclass(frozen=True)

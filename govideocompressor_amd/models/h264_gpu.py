@@ -25,9 +25,17 @@ import numpy as np
 import torch
 
 from ..ops import native
-from .gop import PicPlan, gop_plan  # noqa: F401  (re-exported)
+from .gop import PicPlan, dpb_frames, fixed_types, gop_plan, h264_plan  # noqa: F401  (re-exported)
 
 MB_HDR_BYTES = 64
+NO_COST = 0x3FFFFFFF  # me.hip kNoCost
+# csrc/kernels/route.h SlotRoute (32 bytes): one per slot and coding step
+ROUTE_DTYPE = np.dtype([("kind", "i1"), ("cur", "i1"), ("n0", "i1"), ("l1", "i1"), ("l0", "i1", (4,)),
+                        ("w1", "<i2", (4,)), ("dsf", "<i2", (4,)), ("dcopy", "i1", (4,)), ("flags", "u1"),
+                        ("col_l1", "i1"), ("disp", "<i2")])
+assert ROUTE_DTYPE.itemsize == 32
+SK = {"P": 0, "B": 1, "I": 2}
+SF_REF, SF_DEBLOCK = 1, 2
 WP_LOG2 = 6  # luma / chroma log2 weight denominators of explicit weighted prediction
 COEF_PER_MB = 408
 
@@ -122,6 +130,10 @@ class H264Params:
     # temporal direct: B_Direct_16x16 preferred by tdirect_bias * lambda in b_decide's choice
     # (-0.36 % BD-rate at 8, profiles/r3_direct_rd.md)
     tdirect_bias: int = int(os.environ.get("MIVC_TDIRECT_BIAS", 8))
+    # x264 --b-pyramid normal: in a run of two or more B pictures the middle one is a reference
+    # picture (coded first, predicted from the two anchors, then a reference of the others and of
+    # the next P); needs spatial direct (temporal direct's co-located motion would come from a B)
+    pyramid: bool = os.environ.get("MIVC_PYRAMID", "0") != "0"
     trellis_lambda: float = float(os.environ.get("MIVC_TRELLIS_LAMBDA", 1.0))
     # deblock non-reference B pictures even when neither metrics nor the reconstruction
     # are requested (x264 --full-recon); the bitstream does not depend on it
@@ -148,6 +160,9 @@ class H264Params:
     def eff_bframes(self) -> int:
         return max(0, int(self.bframes)) if self.cabac else 0
 
+    def eff_pyramid(self) -> bool:
+        return bool(self.pyramid and self.eff_bframes() >= 2)
+
     def eff_refs(self) -> int:
         return max(1, min(4, int(self.refs))) if self.cabac else 1
 
@@ -165,7 +180,7 @@ class H264Params:
                     deblock=int(self.deblock), chroma_qp_offset=self.chroma_qp_offset,
                     vui=int(self.vui), cabac=int(self.cabac), bframes=self.eff_bframes(), t8x8=int(self.eff_t8x8()),
                     weighted_bipred=2 if self.weightb else 0, refs=self.eff_refs(), weightp=int(self.eff_weightp()),
-                    level_idc=int(self.level_idc))
+                    level_idc=int(self.level_idc), pyramid=int(self.eff_pyramid()))
 
     def profile_name(self) -> str:
         if not self.cabac:
@@ -174,7 +189,8 @@ class H264Params:
         return (("High CABAC 8x8dct" if self.eff_t8x8() else "Main CABAC") + (" i8x8" if self.eff_t8x8() and self.i8x8 else "")
                 + (" p8x8" if self.eff_partitions() else "") + (" b8x8" if self.eff_partitions() and self.bpartitions and self.eff_bframes() else "") + (f" ref{self.eff_refs()}" if self.eff_refs() > 1 else "")
                 + (" weightp" if self.eff_weightp() else "")
-                + (f" {nb}B {self.direct}-direct" if nb else "") + (" weightb" if nb and self.weightb else ""))
+                + (f" {nb}B" + (" b-pyramid" if self.eff_pyramid() else "") + f" {self.direct}-direct" if nb else "")
+                + (" weightb" if nb and self.weightb else ""))
 
     def frame_qps(self) -> tuple[int, int]:
         """(qp_I, qp_P).  CRF maps to the P-frame QP (x264 scale without MB-tree);
@@ -249,6 +265,10 @@ class GpuH264Encoder:
             raise ValueError("width and height must be even")
         if params.direct not in ("temporal", "spatial"):
             raise ValueError("direct must be 'temporal' or 'spatial'")
+        if params.eff_pyramid() and params.direct != "spatial":
+            # temporal direct scales the co-located block's motion by its own list-0 picture,
+            # which is the current list 0 only while RefPicList1[0] is a P anchor
+            raise ValueError("b-pyramid needs spatial direct prediction (direct='spatial')")
         if entropy not in ("gpu", "cpu"):
             raise ValueError("entropy must be 'gpu' or 'cpu'")
         self.entropy = entropy
@@ -262,7 +282,7 @@ class GpuH264Encoder:
         self.W, self.H = self.wmb * 16, self.hmb * 16
         self.nmb = self.wmb * self.hmb
         self._mbtree = None  # [B, F, nmb] MB-tree QP offsets of the batch being encoded
-        self._wp = self._wp_on = None  # explicit weights of the batch's P pictures (see _weights)
+        self._wp = self._wp_steps = None  # explicit weights of the batch's P pictures (see _weights)
         B, H, W, nmb, dev = self.B, self.H, self.W, self.nmb, self.dev
         u8, i16, i32 = torch.uint8, torch.int16, torch.int32
 
@@ -273,11 +293,23 @@ class GpuH264Encoder:
 
         self.src = planes()
         self.nb = params.eff_bframes()
-        # anchors (I / P) rotate over rec[0 .. na - 1] (na = refs + 1: the picture being coded and
-        # the refs anchors it may reference); B pictures (never referenced) reconstruct into rec[na]
         self.nref = params.eff_refs()
-        self.na = self.nref + 1
-        self.rec = [planes() for _ in range(self.na)] + ([planes()] if self.nb else [])
+        # Every slot follows its own GOP plan (models/gop.py h264_plan): its reference pictures
+        # live in a per-slot pool of reconstruction buffers [B, nbuf, plane] (the DPB's
+        # max_num_ref_frames, one more for the picture being coded, one scratch buffer for
+        # non-reference B pictures), with the half-sample planes of every reference picture
+        # (built once, shared by all pictures predicting from it) and, for B pictures, the
+        # decision records of the co-located candidates.  One SlotRoute per slot and coding
+        # step (csrc/kernels/route.h) tells the kernels which buffer plays which role.
+        self.nref_frames = dpb_frames(self.nref, params.eff_pyramid(), self.nb)
+        self.nbuf = self.nref_frames + 2
+        NB = self.nbuf
+        self.rec_pool = (torch.zeros((B, NB, H, W), dtype=u8, device=dev),
+                         torch.zeros((B, NB, H // 2, W // 2), dtype=u8, device=dev),
+                         torch.zeros((B, NB, H // 2, W // 2), dtype=u8, device=dev))
+        self.rec = [tuple(p[:, i] for p in self.rec_pool) for i in range(NB)]  # per-buffer views (tools)
+        self.hp_bytes = 3 * (H + 8) * (W + 8)
+        self.hp_pool = torch.empty(B * NB * self.hp_bytes + 64, dtype=u8, device=dev)
         self.hdr = [torch.zeros((B, nmb, MB_HDR_BYTES), dtype=u8, device=dev) for _ in range(2)]
         self.coef = [torch.zeros((B, nmb, COEF_PER_MB), dtype=i16, device=dev) for _ in range(2)]
         self.nz = torch.zeros((B, nmb, 16), dtype=u8, device=dev)
@@ -288,9 +320,8 @@ class GpuH264Encoder:
         self.me_cost = torch.zeros((B, nmb), dtype=i32, device=dev)
         self.intra_cost = torch.zeros((B, nmb), dtype=i32, device=dev)
         self.pred = torch.zeros((B, nmb, 256), dtype=u8, device=dev)
-        # resident b / h / j half-sample planes of the two latest anchors (margin 4, + load
-        # slack), built once per anchor and shared by the P and B pictures that reference it
-        self.me_hp = [torch.empty(B * 3 * (H + 8) * (W + 8) + 64, dtype=u8, device=dev) for _ in range(self.na)]
+        self.mref = torch.zeros((B, nmb), dtype=torch.int8, device=dev)
+        self.dref = torch.zeros((B, nmb, 4), dtype=torch.int8, device=dev)
         if self.nref > 1:
             # searches of RefPicList0[1 ..] (P pictures) and the reference choice per MB
             K = self.nref - 1
@@ -298,8 +329,6 @@ class GpuH264Encoder:
             self.xcost = torch.zeros((K, B, nmb), dtype=i32, device=dev)
             self.xpred = torch.zeros((K, B, nmb, 256), dtype=u8, device=dev)
             self.xpm = torch.zeros((B, nmb, 2), dtype=i16, device=dev)
-            self.mref = torch.zeros((B, nmb), dtype=torch.int8, device=dev)
-            self.dref = torch.zeros((B, nmb, 4), dtype=torch.int8, device=dev)
         if self.nb:
             # B pictures: the list-1 search, temporal direct vectors and the mode decision
             self.mv1 = torch.zeros((B, nmb, 2), dtype=i16, device=dev)
@@ -310,7 +339,8 @@ class GpuH264Encoder:
             self.pm0 = torch.zeros((B, nmb, 2), dtype=i16, device=dev)
             self.pm1 = torch.zeros((B, nmb, 2), dtype=i16, device=dev)
             self.dmv = torch.zeros((B, nmb, 16), dtype=i16, device=dev)
-            self.col_hdr = torch.zeros((B, nmb, MB_HDR_BYTES), dtype=u8, device=dev)
+            # records of every reference picture (the co-located candidates of B pictures)
+            self.col_pool = torch.zeros((B, NB, nmb, MB_HDR_BYTES), dtype=u8, device=dev)
         if params.eff_weightp():
             self.src_me = torch.zeros((B, H, W), dtype=u8, device=dev)  # inverse-weighted luma for ME
         self.intra_flag = torch.zeros((B, nmb), dtype=u8, device=dev)
@@ -435,6 +465,17 @@ class GpuH264Encoder:
                       self._ptr(self.src[0]), self._ptr(self.src[1]), self._ptr(self.src[2]),
                       self.p.width, self.p.height, self.W, self.H, self._stream())
 
+    def _prep_step(self, y, u, v, disp: np.ndarray, disp_d: torch.Tensor):
+        """Pad each slot's display picture of this coding step (``disp``: [B] display indices,
+        ``disp_d`` the same on the device): one launch, per-slot frame selection."""
+        if (disp == disp[0]).all():
+            return self._prep(y, u, v, int(disp[0]))
+        B, F, h, w = y.shape
+        cs = u.shape[2] * u.shape[3]
+        self.hip.prep(y.data_ptr(), u.data_ptr(), v.data_ptr(), w, h, F * h * w, F * cs, B,
+                      self._ptr(self.src[0]), self._ptr(self.src[1]), self._ptr(self.src[2]),
+                      self.p.width, self.p.height, self.W, self.H, self._stream(), disp_d.data_ptr())
+
     @staticmethod
     def _dist_scale(poc: int, poc0: int, poc1: int) -> tuple[int, int]:
         """(DistScaleFactor, direct_copy) of temporal direct (clause 8.4.1.2.3; C division)."""
@@ -448,160 +489,140 @@ class GpuH264Encoder:
         tx = tdiv(16384 + abs(tdiv(td, 2)), td)
         return max(-1024, min(1023, (tb * tx + 32) >> 6)), 0
 
-    def _encode_frame(self, pic: PicPlan, cur, ref0, ref1, hdr, coef, cut=None):
-        """One picture of every slot.  ref0 / ref1: the RefPicList0[0] / RefPicList1[0]
-        reconstructions (P: ref0; B: both).  cut: optional [B] bool device tensor -- slots
-        whose picture is a scene cut (every MB intra, as an I picture would be)."""
+    def _encode_step(self, st: dict, hdr, coef, cut=None):
+        """One coding step of every slot (csrc/kernels/route.h): each slot codes its own
+        picture (``st``: the step's routing and host-side tables, built by _step_tables).  P
+        and B pictures of different slots share the step: the P kernels skip the B slots and
+        the B kernels the P slots (they write disjoint per-slot rows of the shared buffers);
+        the intra, deblocking and half-sample kernels then run over all slots at once.
+        cut: optional [B] bool device tensor -- slots whose P picture is a scene cut (every MB
+        intra, as an I picture would be)."""
         s = self._stream()
         B, wmb, hmb = self.B, self.wmb, self.hmb
         P = self._ptr
         sy, su, sv = (P(x) for x in self.src)
-        ry, ru, rv = (P(x) for x in cur)
-        idr = pic.kind == "I"
+        py, pu, pv = (P(x) for x in self.rec_pool)  # reconstruction pools [B, nbuf, plane]
+        hpp = P(self.hp_pool)
+        rt, NB = st["route"], self.nbuf
         aq = 0
         mbt = self._mbtree
-        st = self.stage_timer
+        stt = self.stage_timer
         if self.p.aq_strength > 0 or mbt is not None:
             aq = P(self.aq)
             extra, stride = 0, 0
-            # MB-tree offsets belong to referenced pictures; B pictures get variance AQ only
-            if mbt is not None and mbt.shape[2] == self.nmb and pic.kind != "B":
-                extra, stride = mbt.data_ptr() + pic.d * self.nmb * 4, mbt.shape[1] * self.nmb
-            with st("aq"):
-                self.hip.aq_offsets(B, wmb, hmb, sy, su, sv, float(self.p.aq_strength), aq, s, extra, stride)
+            # MB-tree offsets belong to referenced pictures (the routing picks each slot's row)
+            if mbt is not None and mbt.shape[2] == self.nmb:
+                extra, stride = mbt.data_ptr(), mbt.shape[1] * self.nmb
+            with stt("aq"):
+                self.hip.aq_offsets(B, wmb, hmb, sy, su, sv, float(self.p.aq_strength), aq, s, extra, stride, rt)
         cqo = self.p.chroma_qp_offset
-        na = self.na
-        if pic.kind == "P":
-            fy, fu, fv = (P(x) for x in ref0)
+        inter = st["P"] or st["B"]
+        if inter:
             self.intra_count.zero_()
-            hp = P(self.me_hp[(pic.anchor - 1) % na])
-            sy_full, wp = sy, 0
-            if self._wp_on is not None and self._wp_on[pic.d]:
-                # weighted RefPicList0[0]: its searches see the inverse-weighted source
-                wp = self._wp_dev[pic.d].data_ptr()
-                with st("weightp"):
-                    self.hip.wp_src(sy, P(self.src_me), self._wp_src_dev[pic.d].data_ptr(), B, self.H * self.W, s)
-                sy = P(self.src_me)
-            with st("me_p"):
-                self.hip.me(B, wmb, hmb, sy, fy, P(self.prev_mv), P(self.mv), P(self.me_cost), P(self.pred),
-                            P(self.intra_cost), P(self.qp), self.p.me_range, self.p.subpel, s, hp, aq, 1,
-                            self.p.p_early_sad)
+        if st["P"]:
+            sy_me, wp = sy, 0
+            if st["wp"] is not None:
+                # weighted RefPicList0[0]: the searches see the inverse-weighted source (identity
+                # weights for the other slots)
+                wp = st["wp"].data_ptr()
+                with stt("weightp"):
+                    self.hip.wp_src(sy, P(self.src_me), st["wp_src"].data_ptr(), B, self.H * self.W, s)
+                sy_me = P(self.src_me)
+            with stt("me_p"):
+                self.hip.me(B, wmb, hmb, sy_me, py, P(self.prev_mv), P(self.mv), P(self.me_cost), P(self.pred),
+                            P(self.intra_cost), P(self.qp), self.p.me_range, self.p.subpel, s, hpp, aq, 1,
+                            self.p.p_early_sad, 0, 0, 0, rt, NB, 0, SK["P"])
                 for it in range(int(self.p.skip_refine)):
                     a_, b_ = (self.mv, self.mv_tmp) if it % 2 == 0 else (self.mv_tmp, self.mv)
-                    self.hip.p_refine(B, wmb, hmb, sy, fy, hp, P(a_), P(b_), P(self.me_cost), P(self.prev_mv),
-                                      P(self.pred), P(self.qp), aq, s)
+                    self.hip.p_refine(B, wmb, hmb, sy_me, py, hpp, P(a_), P(b_), P(self.me_cost), P(self.prev_mv),
+                                      P(self.pred), P(self.qp), aq, s, rt, NB)
                 if int(self.p.skip_refine) % 2:
-                    self.mv.copy_(self.mv_tmp)
+                    self.mv.copy_(torch.where(st["pmask"][:, None, None], self.mv_tmp, self.mv))
             mv8 = 0
             if self.p.eff_partitions():
-                with st("part"):
-                    self.hip.p_part8(B, wmb, hmb, sy, fy, hp, P(self.mv), P(self.prev_mv), P(self.me_cost), P(self.pred),
-                                     P(self.mv8), P(self.qp), aq, int(self.p.part_overhead), int(self.p.part_min_satd), s)
+                with stt("part"):
+                    self.hip.p_part8(B, wmb, hmb, sy_me, py, hpp, P(self.mv), P(self.prev_mv), P(self.me_cost),
+                                     P(self.pred), P(self.mv8), P(self.qp), aq, int(self.p.part_overhead),
+                                     int(self.p.part_min_satd), s, rt, NB)
                 mv8 = P(self.mv8)
-            self.prev_mv.copy_(self.mv)  # next P picture's predictors: the list-0[0] vectors
-            nr = self.n_l0(pic.anchor)
-            xu, xv = [], []
+            # the next P picture's predictors: the list-0[0] vectors of this one (P slots)
+            self.prev_mv.copy_(torch.where(st["pmask"][:, None, None], self.mv, self.prev_mv))
+            nr = st["maxn0"]
             if nr > 1:
-                # farther anchors: 16x16 searches seeded by the list-0[0] vectors scaled by the
-                # temporal distance, then the per-MB choice (cost + ref_idx bits)
-                d0 = pic.d - self.anchor_d[pic.anchor - 1]
-                with st("me_ref"):
+                # farther list-0 pictures: 16x16 searches seeded by the list-0[0] vectors scaled by
+                # the temporal distances (per slot), then the per-MB choice (cost + ref_idx bits)
+                with stt("me_ref"):
                     for k in range(1, nr):
-                        a_k = pic.anchor - 1 - k
-                        rk = self.rec[a_k % na]
-                        scale = (pic.d - self.anchor_d[a_k]) / max(1, d0)
-                        self.xpm.copy_((self.mv.float() * scale).round_().clamp_(-2048, 2047))
-                        self.hip.me(B, wmb, hmb, sy_full, P(rk[0]), P(self.xpm), P(self.xmv[k - 1]), P(self.xcost[k - 1]),
+                        self.xpm.copy_((self.mv.float() * st["xscale"][k - 1][:, None, None]).round_().clamp_(-2048, 2047))
+                        self.hip.me(B, wmb, hmb, sy, py, P(self.xpm), P(self.xmv[k - 1]), P(self.xcost[k - 1]),
                                     P(self.xpred[k - 1]), 0, P(self.qp), int(self.p.ref_range), self.p.subpel, s,
-                                    P(self.me_hp[a_k % na]), aq, 1, self.p.p_early_sad, P(self.me_cost),
-                                    self._ref_gate(), P(self.prev_mv))
-                        xu.append(P(rk[1]))
-                        xv.append(P(rk[2]))
+                                    hpp, aq, 1, self.p.p_early_sad, P(self.me_cost), self._ref_gate(),
+                                    P(self.prev_mv), rt, NB, k, SK["P"])
                     self.hip.me_ref_select(B, wmb, hmb, nr, P(self.mv), mv8, P(self.me_cost), P(self.pred),
-                                           P(self.xmv), P(self.xcost), P(self.xpred), P(self.mref), P(self.qp), aq, s)
-                    self.far_ref_mbs += (self.mref > 0).sum()
+                                           P(self.xmv), P(self.xcost), P(self.xpred), P(self.mref), P(self.qp), aq,
+                                           s, rt)
+                    self.far_ref_mbs += ((self.mref > 0) & st["pmask"][:, None]).sum()
+            else:
+                self.mref.zero_()
             if cut is not None:
                 self.intra_cost.masked_fill_(cut[:, None], -1)  # intra beats any inter cost
-            sy = sy_full
-            with st("inter"):
-                self.hip.encode_inter(B, wmb, hmb, sy, su, sv, fy, fu, fv, ry, ru, rv, P(self.pred), P(self.mv),
+            with stt("inter"):
+                self.hip.encode_inter(B, wmb, hmb, sy, su, sv, py, pu, pv, py, pu, pv, P(self.pred), P(self.mv),
                                       P(self.me_cost), P(self.intra_cost), P(self.qp), cqo, P(hdr), P(coef),
                                       P(self.nz), P(self.intra_flag), P(self.intra_count), s, aq,
-                                      t8=int(self.p.eff_t8x8()), mv8=mv8, xref_u=xu, xref_v=xv,
-                                      mref=P(self.mref) if nr > 1 else 0, wp=wp, trellis=int(self.p.trellis),
-                                      trellis_lambda=float(self.p.trellis_lambda))
-        elif pic.kind == "B":
-            f0y, f0u, f0v = (P(x) for x in ref0)
-            f1y, f1u, f1v = (P(x) for x in ref1)
-            hp0, hp1 = P(self.me_hp[(pic.l1_anchor - 1) % na]), P(self.me_hp[pic.l1_anchor % na])
-            # list 0 = the anchors before the picture, nearest first (the list-1 anchor's own list
-            # 0, so the co-located refIdx maps to itself); per entry: temporal-direct scale and
-            # implicit bi-prediction weight (8.4.2.3.1: w1 = DistScaleFactor >> 2 unless out of range)
-            nr = self.n_l0(pic.l1_anchor)
-            dsfs, copies, w1s, r0y, r0h, xu, xv = [], [], [], [], [], [], []
-            for k in range(nr):
-                a_k = pic.l1_anchor - 1 - k
-                dsf, copy = self._dist_scale(pic.poc, 2 * self.anchor_d[a_k], 2 * pic.l1)
-                dsfs.append(dsf)
-                copies.append(copy)
-                w1s.append(dsf >> 2 if self.p.weightb and not copy and -64 <= (dsf >> 2) <= 128 else 32)
-                if k:
-                    rk = self.rec[a_k % na]
-                    r0y.append(P(rk[0]))
-                    r0h.append(P(self.me_hp[a_k % na]))
-                    xu.append(P(rk[1]))
-                    xv.append(P(rk[2]))
-            self.intra_count.zero_()
+                                      t8=int(self.p.eff_t8x8()), mv8=mv8, mref=P(self.mref), wp=wp,
+                                      trellis=int(self.p.trellis), trellis_lambda=float(self.p.trellis_lambda),
+                                      route=rt, nbuf=NB)
+        if st["B"]:
             br = self.p.b_me_range
             # spatial direct cannot be priced before the wavefront: its gate passes static MBs only
             spatial = int(self.p.direct == "spatial")
             bg = int(self.p.b_gate) if not spatial or self.p.spatial_gate else 0
-            with st("me_b"):
-                self.hip.b_direct(B, wmb, hmb, P(self.col_hdr), dsfs, copies, P(self.dmv), P(self.pm0), P(self.pm1), s,
-                                  P(self.dref) if nr > 1 else 0)
+            with stt("me_b"):
+                self.hip.b_direct(B, wmb, hmb, P(self.col_pool), [0], [1], P(self.dmv), P(self.pm0), P(self.pm1), s,
+                                  P(self.dref), rt, NB)
                 if bg != 0:  # direct costs first: MBs that direct already predicts well are not searched
-                    self.hip.b_decide(B, wmb, hmb, sy, f0y, f1y, hp0, hp1, P(self.mv), P(self.mv1), P(self.me_cost),
+                    self.hip.b_decide(B, wmb, hmb, sy, py, py, hpp, hpp, P(self.mv), P(self.mv1), P(self.me_cost),
                                       P(self.me_cost1), P(self.pred), P(self.pred1), P(self.pm0), P(self.pm1),
-                                      P(self.dmv), P(self.qp), aq, P(hdr), P(self.pred_b), P(self.cost_b), s, w1s,
-                                      P(self.dref) if nr > 1 else 0, r0y, r0h, 1, spatial=spatial)
+                                      P(self.dmv), P(self.qp), aq, P(hdr), P(self.pred_b), P(self.cost_b), s, [32],
+                                      P(self.dref), [], [], 1, spatial=spatial, route=rt, nbuf=NB)
                 gate = P(self.cost_b) if bg != 0 else 0
-                self.hip.me(B, wmb, hmb, sy, f0y, P(self.pm0), P(self.mv), P(self.me_cost), P(self.pred),
-                            P(self.intra_cost), P(self.qp), br, self.p.subpel, s, hp0, aq, 1, self.p.b_early_sad,
-                            gate, bg)
+                self.hip.me(B, wmb, hmb, sy, py, P(self.pm0), P(self.mv), P(self.me_cost), P(self.pred),
+                            P(self.intra_cost), P(self.qp), br, self.p.subpel, s, hpp, aq, 1, self.p.b_early_sad,
+                            gate, bg, 0, rt, NB, 0, SK["B"])
                 # the L1 search skips the open-loop intra estimate the L0 search just wrote
-                self.hip.me(B, wmb, hmb, sy, f1y, P(self.pm1), P(self.mv1), P(self.me_cost1), P(self.pred1),
-                            0, P(self.qp), br, self.p.subpel, s, hp1, aq, 1, self.p.b_early_sad, gate, bg)
-            with st("b_decide"):
-                self.hip.b_decide(B, wmb, hmb, sy, f0y, f1y, hp0, hp1, P(self.mv), P(self.mv1), P(self.me_cost),
+                self.hip.me(B, wmb, hmb, sy, py, P(self.pm1), P(self.mv1), P(self.me_cost1), P(self.pred1), 0,
+                            P(self.qp), br, self.p.subpel, s, hpp, aq, 1, self.p.b_early_sad, gate, bg, 0, rt, NB,
+                            4, SK["B"])
+            with stt("b_decide"):
+                self.hip.b_decide(B, wmb, hmb, sy, py, py, hpp, hpp, P(self.mv), P(self.mv1), P(self.me_cost),
                                   P(self.me_cost1), P(self.pred), P(self.pred1), P(self.pm0), P(self.pm1),
-                                  P(self.dmv), P(self.qp), aq, P(hdr), P(self.pred_b), P(self.cost_b), s, w1s,
-                                  P(self.dref) if nr > 1 else 0, r0y, r0h, 0, int(self.p.eff_partitions() and self.p.bpartitions),
-                                  int(bg != 0), int(self.p.direct == "spatial"),
-                                  int(self.p.tdirect_bias) if self.p.direct != "spatial" else 0)
-            if cut is not None:
-                self.intra_cost.masked_fill_(cut[:, None], -1)
-            if self.p.direct == "spatial":
-                with st("b_spatial"):
-                    self.hip.b_spatial(B, wmb, hmb, P(hdr), P(self.col_hdr), sy, f1y, hp1, [f0y] + r0y,
-                                       [hp0] + r0h, w1s, P(self.pred_b), P(self.err), s, P(self.intra_cost),
-                                       P(self.cost_b), P(self.qp), aq, int(self.p.direct_bias))
-            with st("inter"):
-                self.hip.encode_inter(B, wmb, hmb, sy, su, sv, f0y, f0u, f0v, ry, ru, rv, P(self.pred_b), P(self.mv),
+                                  P(self.dmv), P(self.qp), aq, P(hdr), P(self.pred_b), P(self.cost_b), s, [32],
+                                  P(self.dref), [], [], 0, int(self.p.eff_partitions() and self.p.bpartitions),
+                                  int(bg != 0), spatial, int(self.p.tdirect_bias) if not spatial else 0,
+                                  route=rt, nbuf=NB)
+            if spatial:
+                with stt("b_spatial"):
+                    self.hip.b_spatial(B, wmb, hmb, P(hdr), P(self.col_pool), sy, py, hpp, [py], [hpp], [32],
+                                       P(self.pred_b), P(self.err), s, P(self.intra_cost), P(self.cost_b), P(self.qp),
+                                       aq, int(self.p.direct_bias), rt, NB)
+            with stt("inter"):
+                self.hip.encode_inter(B, wmb, hmb, sy, su, sv, py, pu, pv, py, pu, pv, P(self.pred_b), P(self.mv),
                                       P(self.cost_b), P(self.intra_cost), P(self.qp), cqo, P(hdr), P(coef),
-                                      P(self.nz), P(self.intra_flag), P(self.intra_count), s, aq, f1u, f1v, 1,
-                                      int(self.p.eff_t8x8()), 0, w1s, xu, xv, 0, 0, int(self.p.trellis),
-                                      float(self.p.trellis_lambda))
-        if pic.kind != "I":
+                                      P(self.nz), P(self.intra_flag), P(self.intra_count), s, aq, pu, pv, 1,
+                                      int(self.p.eff_t8x8()), 0, [32], [], [], 0, 0, int(self.p.trellis),
+                                      float(self.p.trellis_lambda), rt, NB)
+        if inter:
             self.p_intra_mbs += self.intra_count.sum()
             flag_ptr, count_ptr = P(self.intra_flag), P(self.intra_count)
         else:
             self.prev_mv.zero_()
             flag_ptr, count_ptr = 0, 0
-        trial = idr or self.p.i4x4_in_p or cut is not None
-        with st("intra"):
-            self.hip.encode_intra(B, wmb, hmb, sy, su, sv, ry, ru, rv, P(self.qp), cqo, P(hdr), P(coef), P(self.nz),
+        trial = not inter or self.p.i4x4_in_p or cut is not None
+        with stt("intra"):
+            self.hip.encode_intra(B, wmb, hmb, sy, su, sv, py, pu, pv, P(self.qp), cqo, P(hdr), P(coef), P(self.nz),
                                   flag_ptr, count_ptr, P(self.err), int(self.p.i4x4 and trial), s, aq,
-                                  int(self.p.i8x8 and self.p.eff_t8x8() and trial))
+                                  int(self.p.i8x8 and self.p.eff_t8x8() and trial), rt, NB)
         if aq:
             # MBs without mb_qp_delta take QP_pred (clause 7.4.5): their records must say so
             # before deblocking reads every MB's QP
@@ -610,47 +631,137 @@ class GpuH264Encoder:
         # (which predict from unfiltered samples), so its in-loop filter only matters when
         # someone looks at the picture: metrics (PSNR / SSIM) or keep_recon.  The bitstream
         # is identical either way (cf. x264, which reconstructs non-reference frames fully
-        # only with --full-recon).
-        if self.p.deblock and (pic.kind != "B" or self._full_recon):
-            with st("deblock"):
-                self.hip.deblock(B, wmb, hmb, ry, ru, rv, P(hdr), P(self.nz), cqo, 0, 0, P(self.err), s)
-        if pic.kind != "B":
-            # the anchor's half-sample planes (shared by every picture that references it) and,
-            # for the B pictures after it, its motion as the temporal-direct co-located field
-            with st("halfpel"):
-                self.hip.me_halfpel(B, self.W, self.H, ry, P(self.me_hp[pic.anchor % na]), s)
-            if self.nb and pic.kind == "P":
-                self.col_hdr.copy_(hdr)
+        # only with --full-recon): the routing flags SF_DEBLOCK accordingly.
+        if self.p.deblock and st["deblock"]:
+            with stt("deblock"):
+                self.hip.deblock(B, wmb, hmb, py, pu, pv, P(hdr), P(self.nz), cqo, 0, 0, P(self.err), s, rt, NB)
+        if st["ref"]:
+            # the reference pictures' half-sample planes (shared by every picture predicting from
+            # them) and, for B pictures, their records as co-located candidates
+            with stt("halfpel"):
+                self.hip.me_halfpel(B, self.W, self.H, py, hpp, s, rt, NB)
+            if self.nb and st["col_dst"] is not None:
+                self.col_pool.view(B * NB, self.nmb, MB_HDR_BYTES).index_copy_(
+                    0, st["col_dst"], hdr.index_select(0, st["col_src"]))
+
+    def _plans(self, F: int, cuts_h: np.ndarray, anchors_at) -> list[list[PicPlan]]:
+        """Per-slot coding-order plans: x264's fixed --b-adapt 0 pattern with anchors at the
+        forced positions and at each slot's own scene cuts.  ``anchors_at``: display indices
+        forced for every slot, or one iterable per slot."""
+        per_slot = (isinstance(anchors_at, (list, tuple)) and len(anchors_at) == self.B and len(anchors_at) > 0
+                    and all(isinstance(a, (list, tuple, set, frozenset)) for a in anchors_at))
+        common = set() if per_slot else {int(d) for d in anchors_at}
+        cache: dict[str, list[PicPlan]] = {}
+        plans = []
+        for b in range(self.B):
+            forced = {int(d) for d in anchors_at[b]} if per_slot else common
+            ty = fixed_types(F, self.nb, forced | {d for d in range(1, F) if cuts_h[b, d]})
+            if ty not in cache:
+                cache[ty] = h264_plan(ty, self.nref, self.p.eff_pyramid(), self.nref_frames)
+            plans.append(cache[ty])
+        return plans
+
+    def _step_tables(self, plans: list[list[PicPlan]], F: int) -> list[dict]:
+        """Routing of every coding step: the [F, B] SlotRoute table (one upload) and per step the
+        picture kinds present, the P-slot mask, far-reference vector scales, explicit weights
+        and the record-store indices of its reference pictures."""
+        B, NB, dev = self.B, self.nbuf, self.dev
+        rt = np.zeros((F, B), dtype=ROUTE_DTYPE)
+        rt["l1"] = -1
+        rt["l0"] = -1
+        rt["disp"] = -1
+        rt["w1"] = 32
+        rt["dcopy"] = 1
+        K = max(1, self.nref - 1)
+        xscale = np.zeros((F, K, B), dtype=np.float32)
+        deblock_nonref = bool(self._full_recon)
+        col = {}
+        colcache: dict[int, tuple] = {}  # one routing column per distinct plan (slots share plans)
+        for b in range(B):
+            key = id(plans[b])
+            if key not in colcache:
+                c = np.zeros(F, dtype=ROUTE_DTYPE)
+                c["l1"] = -1
+                c["l0"] = -1
+                c["w1"] = 32
+                c["dcopy"] = 1
+                xs = np.zeros((F, K), dtype=np.float32)
+                kinds = {pic.d: pic.kind for pic in plans[b]}
+                refs_at = []
+                for t, pic in enumerate(plans[b]):
+                    r = c[t]
+                    r["kind"] = SK[pic.kind]
+                    r["cur"] = pic.buf
+                    r["n0"] = max(1, len(pic.refs0))
+                    r["l0"][:len(pic.bufs0)] = pic.bufs0
+                    r["flags"] = (SF_REF if pic.ref else 0) | (SF_DEBLOCK if (pic.ref or deblock_nonref) else 0)
+                    r["disp"] = pic.d
+                    if pic.kind == "P":
+                        d0 = max(1, pic.d - pic.refs0[0])
+                        for k in range(1, len(pic.refs0)):
+                            xs[t, k - 1] = (pic.d - pic.refs0[k]) / d0
+                    elif pic.kind == "B":
+                        r["l1"] = pic.buf1
+                        r["col_l1"] = int(kinds[pic.l1] == "B")
+                        for k, rd in enumerate(pic.refs0):
+                            dsf, copy = self._dist_scale(pic.poc, 2 * rd, 2 * pic.l1)
+                            r["dsf"][k] = dsf
+                            r["dcopy"][k] = copy
+                            r["w1"][k] = dsf >> 2 if self.p.weightb and not copy and -64 <= (dsf >> 2) <= 128 else 32
+                    if pic.ref and pic.kind != "I":
+                        refs_at.append((t, pic.buf))
+                colcache[key] = (c, xs, refs_at)
+            c, xs, refs_at = colcache[key]
+            rt[:, b] = c
+            xscale[:, :, b] = xs
+            for t, buf in refs_at:
+                col.setdefault(t, []).append((b, b * NB + buf))
+        rt_d = torch.from_numpy(rt.view(np.uint8).reshape(F, B * 32).copy()).to(dev)
+        kinds_d = torch.from_numpy(np.ascontiguousarray(rt["kind"])).to(dev)
+        xs_d = torch.from_numpy(xscale).to(dev)
+        self._route_dev = rt_d  # keeps the table alive while the launches read it
+        steps = []
+        for t in range(F):
+            k = rt["kind"][t]
+            n0p = rt["n0"][t][k == 0]
+            st = dict(route=rt_d[t].data_ptr(), P=bool((k == 0).any()), B=bool((k == 1).any()),
+                      pmask=kinds_d[t] == 0, maxn0=int(n0p.max()) if n0p.size else 1, xscale=xs_d[t],
+                      deblock=bool((rt["flags"][t] & SF_DEBLOCK).any()), ref=bool((rt["flags"][t] & SF_REF).any()),
+                      wp=None, wp_src=None, col_src=None, col_dst=None, kinds=k)
+            if t in col:
+                src, dst = zip(*col[t])
+                st["col_src"] = torch.tensor(src, dtype=torch.long, device=dev)
+                st["col_dst"] = torch.tensor(dst, dtype=torch.long, device=dev)
+            steps.append(st)
+        return steps
 
     # ------------------------------------------------------------------ entropy (GPU CAVLC)
-    def n_l0(self, anchor: int) -> int:
-        """List-0 size of the P picture with anchor ordinal ``anchor`` and of the B pictures
-        before it: the anchors coded before it, at most eff_refs."""
-        return max(1, min(self.nref, anchor))
-
-    def _num_ref_l0(self, pic: PicPlan) -> int:
-        return {"I": 1, "P": self.n_l0(pic.anchor), "B": self.n_l0(pic.l1_anchor)}[pic.kind]
-
     def _ref_gate(self) -> int:
         return int(self.p.ref_gate)
 
-    def _frame_params(self, b: int, pic: PicPlan, qp_frame: int, idr_ids: list[int]) -> dict:
-        n0 = self._num_ref_l0(pic)
+    def _frame_params(self, b: int, pic: PicPlan, t: int, qp_frame: int, idr_ids: list[int]) -> dict:
+        """Slice-header fields of slot b's picture at coding step t."""
         fp = dict(idr=int(pic.kind == "I"), frame_num=pic.frame_num, idr_pic_id=idr_ids[b] & 0xFFFF, qp=qp_frame,
                   slice_type=pic.slice_type, nal_ref_idc=pic.nal_ref_idc, poc=pic.poc,
-                  direct_spatial=int(pic.kind == "B" and self.p.direct == "spatial"),
-                  **({"num_ref_l0": n0, "num_ref_l1": 1} if pic.kind != "I" else {}))
+                  direct_spatial=int(pic.kind == "B" and self.p.direct == "spatial"))
+        if pic.kind != "I":
+            fp["num_ref_l0"] = max(1, len(pic.refs0))
+            fp["num_ref_l1"] = 1
+            if pic.mod_l0:
+                fp["mod_l0"] = [tuple(m) for m in pic.mod_l0]
         if pic.kind == "P" and self._wp is not None:
-            fp["wp"] = [WP_LOG2, WP_LOG2] + [int(x) for x in self._wp[pic.d, b]]
+            fp["wp"] = [WP_LOG2, WP_LOG2] + [int(x) for x in self._wp[t, b]]
         return fp
 
-    def _weights(self, y, u, v, plan: list[PicPlan]) -> None:
+    def _weights(self, y, u, v, plans: list[list[PicPlan]]) -> None:
         """x264 --weightp: per P picture and slot, the explicit weights of RefPicList0[0] from
         the source statistics (wp_stats: means and variances of the two pictures' planes):
         scale = sqrt(var_cur / var_ref), offset = mean_cur - scale * mean_ref, used when the mean
-        moved by wp_min_mean levels or the contrast by wp_min_scale (fades, flashes)."""
-        self._wp = self._wp_on = None
-        if not self.p.eff_weightp() or not any(pic.kind == "P" for pic in plan):
+        moved by wp_min_mean levels or the contrast by wp_min_scale (fades, flashes).  Tables
+        are per coding step ([F, B], identity weights elsewhere)."""
+        self._wp = None
+        self._wp_steps = None
+        if not self.p.eff_weightp() or not any(pic.kind == "P" for plan in plans for pic in plan):
             return
         B, F, h, w = y.shape
         st = torch.empty((B, F, 6), dtype=torch.int64, device=self.dev)
@@ -660,33 +771,39 @@ class GpuH264Encoder:
         mean = sh[..., 0::2] / n
         var = np.maximum(sh[..., 1::2] / n - mean ** 2, 0.0)
         one = 1 << WP_LOG2
+        # every (slot, step) holding a P picture: its display index and its RefPicList0[0]'s
+        bs, ts, ds, rs = [], [], [], []
+        for b, plan in enumerate(plans):
+            for t, pic in enumerate(plan):
+                if pic.kind == "P":
+                    bs.append(b)
+                    ts.append(t)
+                    ds.append(pic.d)
+                    rs.append(pic.l0)
+        bs, ts, ds, rs = (np.array(a, dtype=np.int64) for a in (bs, ts, ds, rs))
+        m1, m0 = mean[bs, ds], mean[bs, rs]
+        v1, v0 = var[bs, ds], var[bs, rs]
+        scale = np.where(v0 > 1e-3, np.sqrt(v1 / np.maximum(v0, 1e-3)), 1.0)
+        use = (np.abs(m1[:, 0] - m0[:, 0]) >= self.p.wp_min_mean) | (np.abs(scale[:, 0] - 1) >= self.p.wp_min_scale)
+        if not use.any():
+            return
+        wq = np.clip(np.round(scale * one), 0, 127)
+        oq = np.clip(np.round(m1 - wq / one * m0), -128, 127)
         wp = np.zeros((F, B, 6), dtype=np.int32)
         wp[:, :, 0::2] = one
+        for c in range(3):
+            wp[ts[use], bs[use], 2 * c] = wq[use, c]
+            wp[ts[use], bs[use], 2 * c + 1] = oq[use, c]
         on = np.zeros(F, dtype=bool)
-        for pic in plan:
-            if pic.kind != "P":
-                continue
-            m1, m0 = mean[:, pic.d], mean[:, pic.l0]
-            v1, v0 = var[:, pic.d], var[:, pic.l0]
-            scale = np.where(v0 > 1e-3, np.sqrt(v1 / np.maximum(v0, 1e-3)), 1.0)
-            use = (np.abs(m1[:, 0] - m0[:, 0]) >= self.p.wp_min_mean) | (np.abs(scale[:, 0] - 1) >= self.p.wp_min_scale)
-            if not use.any():
-                continue
-            wq = np.clip(np.round(scale * one), 0, 127)
-            oq = np.clip(np.round(m1 - wq / one * m0), -128, 127)
-            for c in range(3):
-                wp[pic.d, use, 2 * c] = wq[use, c]
-                wp[pic.d, use, 2 * c + 1] = oq[use, c]
-            on[pic.d] = True
-        if not on.any():
-            return
-        self._wp, self._wp_on = wp, on
+        on[ts[use]] = True
+        self._wp = wp
         dev8 = np.zeros((F, B, 8), dtype=np.int32)
         dev8[..., 0], dev8[..., 1], dev8[..., 2] = wp[..., 0], wp[..., 1], WP_LOG2
         dev8[..., 3:7], dev8[..., 7] = wp[..., 2:6], WP_LOG2
-        self._wp_dev = torch.from_numpy(dev8).to(self.dev)
-        self._wp_src_dev = torch.from_numpy(np.ascontiguousarray(dev8[..., :3])).to(self.dev)
-        self.stats["weightp_pictures"] = int(on.sum())
+        wp_dev = torch.from_numpy(dev8).to(self.dev)
+        wp_src = torch.from_numpy(np.ascontiguousarray(dev8[..., :3])).to(self.dev)
+        self._wp_steps = [(wp_dev[t], wp_src[t]) if on[t] else None for t in range(F)]
+        self.stats["weightp_pictures"] = int(use.sum())
 
     @staticmethod
     def _cabac_groups(F: int, G: int) -> list[tuple[int, int]]:
@@ -703,34 +820,34 @@ class GpuH264Encoder:
             t0 += n
         return out
 
-    def _gpu_cabac_bin(self, k: int, g: int, j: int, pic: PicPlan, qps_t, idr_ids: list[int],
-                       qp_dev: torch.Tensor):
-        """Binarise frame step t (records hdr[k]/coef[k]) into the symbol pool of its group
+    def _gpu_cabac_bin(self, k: int, g: int, j: int, t: int, pics: list[PicPlan], qps_t, idr_ids: list[int],
+                       qp_dev: torch.Tensor, route: int):
+        """Binarise coding step t (records hdr[k]/coef[k]) into the symbol pool of its group
         ring, on the *copy* stream (the caller's current stream): the records are free
-        again once this is done, whatever the arithmetic coder is doing.
+        again once this is done, whatever the arithmetic coder is doing.  Every slot's slice
+        type and list size come from the step's routing.
         qp_dev: [B] int32 slice QPs of this step in a buffer that outlives the launch."""
-        G, B = self.cab_G, self.B
+        B = self.B
         r = g & 1
         if j == 0:
             self.cab_pool_used[r].zero_()
         self._header_bits_into(self.h_cab_hdr_bits[r][j * B:(j + 1) * B], self.h_cab_hdr_nbits[r][j * B:(j + 1) * B],
                                self.cab_hdr_bits[r][j * B:(j + 1) * B], self.cab_hdr_nbits[r][j * B:(j + 1) * B],
-                               pic, qps_t, idr_ids)
+                               pics, t, qps_t, idr_ids)
         P = self._ptr
         self.hip.cabac_bin(B, self.wmb, self.hmb, P(self.hdr[k]), P(self.coef[k]), P(self.cab_mask), P(self.cab_nb),
                            P(self.cab_cnt), P(self.cab_off), P(self.cab_tot), P(self.cab_pool[r]), self.cab_pool_cap,
                            self.cab_pool_used[r].data_ptr(), self.cab_base[r][j * B:].data_ptr(),
-                           self.cab_total[r][j * B:].data_ptr(), P(qp_dev), pic.slice_type, self._num_ref_l0(pic), 1,
-                           int(self.p.eff_t8x8()), P(self.err),
-                           self.copy_stream.cuda_stream)
+                           self.cab_total[r][j * B:].data_ptr(), P(qp_dev), pics[0].slice_type, 1, 1,
+                           int(self.p.eff_t8x8()), P(self.err), self.copy_stream.cuda_stream, route)
 
     def _gpu_cabac_code(self, g: int, t0: int, n: int, qps_d: torch.Tensor):
         """Arithmetic-code the n frame steps t0 .. t0 + n - 1 of a group (n * B slices) on
         the entropy stream, after their binarisation; sizes go to pinned host memory."""
-        G, B = self.cab_G, self.B
+        B = self.B
         r = g & 1
         self.cab_bin_done[r].record(self.copy_stream)
-        itypes = 1 if t0 == 0 else 0  # frame step 0 is the IDR picture
+        itypes = 1 if t0 == 0 else 0  # frame step 0 is the IDR picture of every slot
         P = self._ptr
         es = self.entropy_stream
         with torch.cuda.stream(es):
@@ -743,13 +860,13 @@ class GpuH264Encoder:
             self.h_pool_used[r].copy_(self.cab_pool_used[r:r + 1], non_blocking=True)
             self.cab_done[r].record(es)
 
-    def _copy_out_group(self, g: int, t0: int, n: int, copied, wrap_futs, plan: list[PicPlan], groups):
+    def _copy_out_group(self, g: int, t0: int, n: int, copied, wrap_futs, steps_pics: list[list[PicPlan]], groups):
         """Copy thread (groups in order): wait for the coder, then hand each frame step's
         slices (already in pinned host memory, 16-byte aligned) to the NAL-wrapping pool.
         ``copied[g]`` (set once the wraps are submitted) releases ring g % 2 (pool, headers,
         pinned sizes) for group g + 2; the host buffer itself is reused by group g + 2's
         coder only after these wraps finished (the main thread waits for them)."""
-        B, G = self.B, self.cab_G
+        B = self.B
         r = g & 1
         t_0 = time.perf_counter()
         self.cab_done[r].synchronize()
@@ -787,24 +904,27 @@ class GpuH264Encoder:
         for jj in range(n):
             sz = sizes[jj * B:(jj + 1) * B]
             nb = int(r16[jj * B:(jj + 1) * B].sum())
-            wrap_futs[t0 + jj] = self.pool.submit(self._wrap, buf[off:off + nb], nb, sz.tolist(), plan[t0 + jj], 16)
+            wrap_futs[t0 + jj] = self.pool.submit(self._wrap, buf[off:off + nb], nb, sz.tolist(), steps_pics[t0 + jj], 16)
             off += nb
         copied[g].set()
 
-    def _header_bits(self, k: int, pic: PicPlan, qps_t, idr_ids: list[int]):
+    def _header_bits(self, k: int, t: int, pics: list[PicPlan], qps_t, idr_ids: list[int]):
         """Slice headers of this step -> pinned host words -> device (current stream)."""
         self._header_bits_into(self.h_hdr_bits[k], self.h_hdr_nbits[k], self.cav_hdr_bits[k], self.cav_hdr_nbits[k],
-                               pic, qps_t, idr_ids)
+                               pics, t, qps_t, idr_ids)
 
-    def _header_bits_into(self, hb, hn, db, dn, pic: PicPlan, qps_t, idr_ids: list[int]):
-        idr = pic.kind == "I"
+    def _header_bits_into(self, hb, hn, db, dn, pics: list[PicPlan], t: int, qps_t, idr_ids: list[int]):
         hbn, hnn = hb.numpy(), hn.numpy()
         cache = {}
+        wp = self._wp
         for b in range(self.B):
-            fp = self._frame_params(b, pic, int(qps_t[b]), idr_ids)
-            key = (fp["idr_pic_id"] if idr else -1, fp["qp"], tuple(fp.get("wp", ())))
+            pic = pics[b]
+            # slots sharing a plan share its PicPlan objects: the header differs only by QP,
+            # the IDR id and the explicit weights
+            key = (id(pic), int(qps_t[b]), idr_ids[b] & 0xFFFF if pic.kind == "I" else -1,
+                   tuple(wp[t, b]) if (wp is not None and pic.kind == "P") else None)
             if key not in cache:
-                cache[key] = self.host.slice_header_bits(self.cfg, fp)
+                cache[key] = self.host.slice_header_bits(self.cfg, self._frame_params(b, pic, t, int(qps_t[b]), idr_ids))
             words, nbits = cache[key]
             hbn[b, :] = 0
             hbn[b, : len(words)] = np.array(words, dtype=np.uint32).view(np.int32)
@@ -812,13 +932,13 @@ class GpuH264Encoder:
         db.copy_(hb, non_blocking=True)
         dn.copy_(hn, non_blocking=True)
 
-    def _gpu_cavlc(self, k: int, pic: PicPlan, qps_t, idr_ids: list[int]):
+    def _gpu_cavlc(self, k: int, t: int, pics: list[PicPlan], qps_t, idr_ids: list[int]):
         """Launch the CAVLC kernels for the current frame step on the compute stream.
         qps_t: per-slot slice QP of this frame step (sequence of B ints)."""
-        if pic.kind == "B":
+        if any(pic.kind == "B" for pic in pics):
             raise ValueError("the GPU CAVLC path codes I / P slices only")
-        idr = pic.kind == "I"
-        self._header_bits(k, pic, qps_t, idr_ids)
+        idr = pics[0].kind == "I"
+        self._header_bits(k, t, pics, qps_t, idr_ids)
         P = self._ptr
         self.hip.cavlc(self.B, self.wmb, self.hmb, P(self.hdr[k]), P(self.coef[k]), P(self.cav_mbs), P(self.cav_len),
                        P(self.cav_off), P(self.cav_trail), P(self.cav_total), P(self.cav_sizes[k]),
@@ -826,7 +946,7 @@ class GpuH264Encoder:
                        0 if idr else 1, int(qps_t[0]), P(self.qp), P(self.cav_out[k]), P(self.cav_out_off),
                        self._stream(), P(self.nz))
 
-    def _copy_out(self, t: int, k: int, pic: PicPlan, copied, wrap_futs):
+    def _copy_out(self, t: int, k: int, pics: list[PicPlan], copied, wrap_futs):
         """Copy thread (frames in order): sizes -> compressed bytes D2H, then hand the NAL
         wrapping to the pool.  ``copied[t]`` releases the device buffers of slot k for frame
         t + 2 as soon as the bytes are on the host; the wrapping is off that critical path."""
@@ -849,17 +969,18 @@ class GpuH264Encoder:
         t2 = time.perf_counter()
         self.timings["entropy_wait_gpu_s"] = self.timings.get("entropy_wait_gpu_s", 0.0) + (t1 - t0)
         self.timings["d2h_s"] = self.timings.get("d2h_s", 0.0) + (t2 - t1)
-        wrap_futs[t] = self.pool.submit(self._wrap, buf, total, sizes, pic)
+        wrap_futs[t] = self.pool.submit(self._wrap, buf, total, sizes, pics)
 
-    def _wrap(self, buf, total: int, sizes: list[int], pic: PicPlan, align: int = 1) -> list[tuple[bytes, int]]:
+    def _wrap(self, buf, total: int, sizes: list[int], pics: list[PicPlan], align: int = 1) -> list[tuple[bytes, int]]:
         t0 = time.perf_counter()
-        nals = self.host.nal_wrap_many(buf[:total].numpy(), sizes, pic.nal_ref_idc, 5 if pic.kind == "I" else 1,
-                                       align)
+        refs = [pic.nal_ref_idc for pic in pics]
+        types = [5 if pic.kind == "I" else 1 for pic in pics]
+        nals = self.host.nal_wrap_many(buf[:total].numpy(), sizes, refs[0], types[0], align, refs, types)
         self.timings["entropy_s"] = self.timings.get("entropy_s", 0.0) + (time.perf_counter() - t0)
         return [(n, len(n) * 8) for n in nals]
 
     # ------------------------------------------------------------------ entropy (host)
-    def _write_slices(self, k: int, pic: PicPlan, qps_t, idr_ids: list[int]) -> list[tuple[bytes, int]]:
+    def _write_slices(self, k: int, t: int, pics: list[PicPlan], qps_t, idr_ids: list[int]) -> list[tuple[bytes, int]]:
         t0 = time.perf_counter()
         self.copy_done[k].synchronize()
         t1 = time.perf_counter()
@@ -867,7 +988,7 @@ class GpuH264Encoder:
         coef = self.h_coef[k].numpy()
 
         def one(b: int):
-            fp = self._frame_params(b, pic, int(qps_t[b]), idr_ids)
+            fp = self._frame_params(b, pics[b], t, int(qps_t[b]), idr_ids)
             nal, st = self.host.write_slice(self.cfg, fp, hdr[b], coef[b])
             return nal, st["bits"]
 
@@ -928,8 +1049,9 @@ class GpuH264Encoder:
         """Encode B segments of F frames each.
 
         y: [B, F, h, w] uint8 (device), u/v: [B, F, h/2, w/2].  Each slot's output is a
-        self-contained Annex-B segment (SPS/PPS + IDR + P...), i.e. one "piece" of the
+        self-contained Annex-B segment (SPS/PPS + IDR + P/B ...), i.e. one "piece" of the
         reference's split directory, with idr_pic_id = idr_ids[slot] (default idr_base + slot).
+        Every slot follows its own GOP plan (its scene cuts become anchors of that slot only).
         When (h, w) differs from the configured size the frames are resampled first (bicubic,
         ``-s WxH``, :mod:`govideocompressor_amd.ops.scale`).
         ``qps``: optional [B, F] per-frame QPs from the rate control (default: the params' CRF/QP,
@@ -948,6 +1070,8 @@ class GpuH264Encoder:
             raise ValueError("u/v must be [B, F, h/2, w/2] with even h, w")
         if not (y.is_contiguous() and u.is_contiguous() and v.is_contiguous()):
             raise ValueError("planes must be contiguous")
+        if F > 0xFFFF:
+            raise ValueError("at most 65535 frames per segment (frame_num / POC without wrap)")
         self._full_recon = bool(metrics or keep_recon or self.p.full_recon)
         if (w, h) != (self.p.width, self.p.height):  # -s WxH: bicubic resample (ops/scale.py)
             if getattr(self, "_scaler", None) is None:
@@ -966,12 +1090,15 @@ class GpuH264Encoder:
             qps = self.crf_qps(y)
             self._from_la = True
         cuts_h = self._scenecuts if self._scenecuts is not None else np.zeros((B, F), dtype=bool)
-        # a scene cut (in any slot) becomes an anchor, so the pictures after it predict from
-        # the new scene instead of across the cut (x264 places an I / P picture there)
-        plan = gop_plan(F, self.nb, set(anchors_at) | {d for d in range(1, F) if cuts_h[:, d].any()})
-        order = [pic.d for pic in plan]  # display index of each coding step
-        self.anchor_d = {pic.anchor: pic.d for pic in plan if pic.kind != "B"}  # anchor ordinal -> display index
-        self._weights(y, u, v, plan)
+        # a scene cut becomes an anchor of its slot, so the pictures after it predict from the
+        # new scene instead of across the cut (x264 places an I / P picture there)
+        plans = self._plans(F, cuts_h, anchors_at)
+        self.last_plans = plans
+        orders = np.array([[pic.d for pic in plans[b]] for b in range(B)], dtype=np.int64)  # [B, F] display per step
+        steps_pics = [[plans[b][t] for b in range(B)] for t in range(F)]
+        orders_d = torch.from_numpy(np.ascontiguousarray(orders.T.astype(np.int32))).to(self.dev)  # [F, B]
+        steps = self._step_tables(plans, F)
+        self._weights(y, u, v, plans)
         if qps is None:
             qps_h = np.full((B, F), qp_p, dtype=np.int32)
             qps_h[:, 0] = qp_i
@@ -981,17 +1108,22 @@ class GpuH264Encoder:
             # B pictures: no rate control of their own, the distance-weighted QP of their
             # references + pbratio (x264 / x265 CRF and constant-QP rule)
             from ..rc.ratecontrol import b_qps_from_refs
-            qps_h = b_qps_from_refs(qps_h, plan, float(self.p.b_qp_offset))
+            qps_h = b_qps_from_refs(qps_h, plans, float(self.p.b_qp_offset))
         if qp_delta is not None:
             from ..rc.abr import apply_delta
             qps_h = apply_delta(qps_h, qp_delta)
         self.last_qps = qps_h.copy()
-        # per coding step (rows), [F, B]: the entropy stages index coding steps
-        qps_d = torch.from_numpy(np.ascontiguousarray(qps_h[:, order].T)).to(self.dev)
-        cuts_c = cuts_h[:, order]
+        # per coding step (rows), [F, B]: the kernels and the entropy stages index coding steps
+        qps_c = np.take_along_axis(qps_h, orders, axis=1)
+        qps_d = torch.from_numpy(np.ascontiguousarray(qps_c.T)).to(self.dev)
+        cuts_c = np.take_along_axis(cuts_h, orders, axis=1)
         cuts_d = torch.from_numpy(np.ascontiguousarray(cuts_c.T)).to(self.dev)  # [F, B] coding order
+        if self._wp_steps is not None:
+            for t, st in enumerate(steps):
+                if self._wp_steps[t] is not None:
+                    st["wp"], st["wp_src"] = self._wp_steps[t]
         self.err.zero_()
-        sse = torch.zeros((F, B, 3), dtype=torch.int64, device=self.dev)
+        sse = torch.zeros((F, B, 3), dtype=torch.int64, device=self.dev)   # coding order
         ssim = torch.zeros((F, B), dtype=torch.float32, device=self.dev)
         pending: list[cf.Future] = [None, None]  # type: ignore[list-item]
         outs: list[list[tuple[bytes, int]]] = [None] * F  # type: ignore[list-item]
@@ -1018,13 +1150,15 @@ class GpuH264Encoder:
             while not group_copied[i].wait(0.5):
                 if group_futs[i].done() and group_futs[i].exception() is not None:
                     raise group_futs[i].exception()
-        recons = [None] * F if keep_recon else None
+        recons = None
+        if keep_recon:
+            recons = [tuple(torch.empty_like(p[:, 0]) for p in self.rec_pool) for _ in range(F)]
         main = torch.cuda.current_stream(self.dev)
         for t in range(F):  # t: coding step
             k = t & 1
-            pic = plan[t]
-            idr = pic.kind == "I"
-            qpt = qps_h[:, pic.d]
+            pics = steps_pics[t]
+            st = steps[t]
+            qpt = qps_c[:, t]
             # the device/pinned buffers of slot k were last used by step t-2: wait for them
             tw = time.perf_counter()
             if cabac_gpu:
@@ -1038,28 +1172,28 @@ class GpuH264Encoder:
                 pending[k] = None
             self.timings["host_blocked_s"] = self.timings.get("host_blocked_s", 0.0) + time.perf_counter() - tw
             main.wait_event(self.copy_done[k]) if t >= 2 else None
-            na = self.na
-            if pic.kind == "B":
-                cur, ref0, ref1 = self.rec[na], self.rec[(pic.l1_anchor - 1) % na], self.rec[pic.l1_anchor % na]
-            else:
-                cur, ref0, ref1 = self.rec[pic.anchor % na], self.rec[(pic.anchor - 1) % na], None
-            self._prep(y, u, v, pic.d)
+            self._prep_step(y, u, v, orders[:, t], orders_d[t])
             self.qp.copy_(qps_d[t])
-            self._encode_frame(pic, cur, ref0, ref1, self.hdr[k], self.coef[k],
-                               cuts_d[t] if (not idr and cuts_c[:, t].any()) else None)
+            self._encode_step(st, self.hdr[k], self.coef[k], cuts_d[t] if (t > 0 and cuts_c[:, t].any()) else None)
             if metrics:
-                self.hip.sse(B, self.W, self.H, self.p.width, self.p.height, self._ptr(self.src[0]),
-                             self._ptr(self.src[1]), self._ptr(self.src[2]), self._ptr(cur[0]), self._ptr(cur[1]),
-                             self._ptr(cur[2]), sse[pic.d].data_ptr(), ssim[pic.d].data_ptr(), self._stream())
+                P = self._ptr
+                self.hip.sse(B, self.W, self.H, self.p.width, self.p.height, P(self.src[0]), P(self.src[1]),
+                             P(self.src[2]), P(self.rec_pool[0]), P(self.rec_pool[1]), P(self.rec_pool[2]),
+                             sse[t].data_ptr(), ssim[t].data_ptr(), self._stream(), st["route"], self.nbuf)
             if keep_recon:
-                recons[pic.d] = tuple(c.clone() for c in cur)
+                bufs = torch.tensor([pic.buf for pic in pics], dtype=torch.long, device=self.dev)
+                slots = torch.arange(B, device=self.dev)
+                for d in sorted({pic.d for pic in pics}):
+                    sel = torch.tensor([b for b in range(B) if pics[b].d == d], dtype=torch.long, device=self.dev)
+                    for c in range(3):
+                        recons[d][c][sel] = self.rec_pool[c][slots[sel], bufs[sel]]
             if self.entropy == "gpu" and not self.p.cabac:
-                self._gpu_cavlc(k, pic, qpt, idr_ids)
+                self._gpu_cavlc(k, t, pics, qpt, idr_ids)
             self.compute_done[k].record(main)
             with torch.cuda.stream(self.copy_stream):
                 self.copy_stream.wait_event(self.compute_done[k])
                 if cabac_gpu:
-                    self._gpu_cabac_bin(k, gi, jj, pic, qpt, idr_ids, qps_d[t])
+                    self._gpu_cabac_bin(k, gi, jj, t, pics, qpt, idr_ids, qps_d[t], st["route"])
                 elif self.entropy == "gpu":
                     self.h_sizes[k].copy_(self.cav_sizes[k], non_blocking=True)
                 else:
@@ -1079,11 +1213,11 @@ class GpuH264Encoder:
                         self.timings["host_blocked_s"] += time.perf_counter() - tw
                     self._gpu_cabac_code(gi, t0, t - t0 + 1, qps_d)
                     group_futs[gi] = self.copy_pool.submit(self._copy_out_group, gi, t0, t - t0 + 1, group_copied,
-                                                           wrap_futs, plan, groups)
+                                                           wrap_futs, steps_pics, groups)
             elif self.entropy == "gpu":
-                copy_futs[t] = self.copy_pool.submit(self._copy_out, t, k, pic, copied, wrap_futs)
+                copy_futs[t] = self.copy_pool.submit(self._copy_out, t, k, pics, copied, wrap_futs)
             else:
-                pending[k] = self.pool.submit(self._write_slices, k, pic, qpt, idr_ids)
+                pending[k] = self.pool.submit(self._write_slices, k, t, pics, qpt, idr_ids)
         if cabac_gpu:
             for f in group_futs:
                 f.result()
@@ -1102,10 +1236,12 @@ class GpuH264Encoder:
         torch.cuda.synchronize(self.dev)
         if F > 1:
             self.stats["p_intra_ratio"] = float(self.p_intra_mbs.item()) / (B * (F - 1) * self.nmb)
-            n_p = sum(1 for pic in plan if pic.kind == "P")
+            n_p = sum(1 for plan in plans for pic in plan if pic.kind == "P")
             if self.nref > 1 and n_p:
                 # share of P-picture MBs (inter decisions before the intra override) on a farther picture
-                self.stats["p_far_ref_ratio"] = float(self.far_ref_mbs.item()) / (B * n_p * self.nmb)
+                self.stats["p_far_ref_ratio"] = float(self.far_ref_mbs.item()) / (n_p * self.nmb)
+            nbp = sum(1 for plan in plans for pic in plan if pic.kind == "B")
+            self.stats["b_ratio"] = nbp / float(B * F)
         self.p_intra_mbs.zero_()
         self.far_ref_mbs.zero_()
         err = int(self.err.item())
@@ -1123,7 +1259,8 @@ class GpuH264Encoder:
         nwin = (self.p.width // 8) * (self.p.height // 8)
         for b in range(B):
             nals = [outs[t][b][0] for t in range(F)]
-            r = SegmentResult(frames=F, nals=nals, bits=[outs[t][b][1] for t in range(F)], header=ps, order=order)
+            r = SegmentResult(frames=F, nals=nals, bits=[outs[t][b][1] for t in range(F)], header=ps,
+                              order=orders[b].tolist())
             if metrics:
                 def psnr(ssev, n):
                     mse = ssev / n

@@ -404,3 +404,41 @@ def test_gpu_h264_spatial_direct_roundtrip(host, refs):
     1 in the B slice headers), with and without several reference pictures."""
     enc, res, _ = _run(352, 288, slots=2, frames=13, crf=None, qp=26, bframes=3, refs=refs, direct="spatial")
     _check_roundtrip(host, enc, res, 352, 288)
+
+
+@pytest.mark.parametrize("pyramid", [False, True])
+def test_gpu_h264_per_slot_plans_roundtrip(host, pyramid):
+    """Every slot follows its own GOP plan (csrc/kernels/route.h): at one coding step slot 0
+    codes a P picture while slot 1 codes a B picture and slot 2 a reference B (b-pyramid),
+    each predicting from its own pool buffers.  Every slot's stream is bit-exact against
+    the CPU decoder, the plans really differ, and a P picture after a reference B carries a
+    ref_pic_list_modification (its list 0 is POC-distance ordered)."""
+    import torch
+    from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
+
+    W, H, F = 176, 144, 13
+    p = H264Params(width=W, height=H, crf=None, qp=26, bframes=3, refs=3, pyramid=pyramid,
+                   direct="spatial" if pyramid else "temporal", part_overhead=0, part_min_satd=0)
+    enc = GpuH264Encoder(p, slots=3)
+    y, u, v = synth_clip(3, F, W, H, seed=5)
+    res = enc.encode(y, u, v, keep_recon=True, anchors_at=[[], [2, 3, 7], [5, 6, 10]])
+    torch.cuda.synchronize()
+    plans = enc.last_plans
+    assert len({tuple(q.d for q in pl) for pl in plans}) == 3
+    mixed = [t for t in range(F) if len({plans[b][t].kind for b in range(3)}) > 1]
+    assert mixed, "no coding step mixed picture types"
+    if pyramid:
+        assert any(q.kind == "B" and q.ref for pl in plans for q in pl)
+        assert any(q.mod_l0 for pl in plans for q in pl)
+    _check_roundtrip(host, enc, res, W, H)
+    enc.close()
+
+
+def test_gpu_h264_pyramid_spatial_roundtrip_b8x8(host):
+    """b-pyramid with spatial direct at the default partitions (B_8x8 with direct quadrants):
+    the co-located picture of the non-reference B pictures is a reference B, whose list-1-only
+    blocks give their list-1 motion to colZeroFlag (8.4.1.2.1) -- bit-exact vs the CPU decoder."""
+    enc, res, _ = _run(352, 288, slots=2, frames=17, crf=24, bframes=3, refs=3, pyramid=True, direct="spatial")
+    _check_roundtrip(host, enc, res, 352, 288)
+    assert any(q.kind == "B" and q.ref for q in enc.last_plans[0])
+    enc.close()
