@@ -43,6 +43,9 @@ struct BDirectArgs {
   // co-located picture (RefPicList1[0]) and its own dsf / direct_copy (SlotRoute)
   const SlotRoute* rt;
   int nbuf;
+  // spatial direct (nullable): colZeroFlag of the four quadrants (bit q; 8.4.1.2.2: the
+  // co-located block is inter, its refIdxCol is 0 and both vector components are in -1..1)
+  uint8_t* czero;
 };
 
 __global__ __launch_bounds__(256) void b_direct_mv(BDirectArgs a) {
@@ -58,6 +61,7 @@ __global__ __launch_bounds__(256) void b_direct_mv(BDirectArgs a) {
   int v[2][4][2];
   int rq[4];
   int s[2][2] = {{0, 0}, {0, 0}};
+  int cz = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     // direct_8x8_inference: the corner 4x4 block of co-located quadrant q, i.e. its vector;
@@ -68,6 +72,7 @@ __global__ __launch_bounds__(256) void b_direct_mv(BDirectArgs a) {
     const int cy = none ? 0 : c.mv[cl][q][1];
     const int r = none ? 0 : min(static_cast<int>(c.ref[cl][q]), kMaxRefs - 1);
     rq[q] = r;
+    if (!none && c.ref[cl][q] == 0 && abs(cx) <= 1 && abs(cy) <= 1) cz |= 1 << q;
     int l0x, l0y;
     const int dcp = a.rt ? a.rt[slot].dcopy[r] : a.direct_copy[r], dsf = a.rt ? a.rt[slot].dsf[r] : a.dsf[r];
     if (dcp) {
@@ -100,6 +105,7 @@ __global__ __launch_bounds__(256) void b_direct_mv(BDirectArgs a) {
                         (static_cast<uint32_t>(rq[2]) << 16) | (static_cast<uint32_t>(rq[3]) << 24);
     *reinterpret_cast<uint32_t*>(a.dref + o * 4) = rw;
   }
+  if (a.czero) a.czero[o] = static_cast<uint8_t>(cz);
   a.pm0[o * 2] = static_cast<int16_t>((s[0][0] + 2) >> 2);
   a.pm0[o * 2 + 1] = static_cast<int16_t>((s[0][1] + 2) >> 2);
   a.pm1[o * 2] = static_cast<int16_t>((s[1][0] + 2) >> 2);
@@ -137,10 +143,13 @@ struct BDecideArgs {
   // direct prediction and cost -- unsearched MBs keep them, the others skip the direct MC
   int have_direct;
   int bparts;  // x264 --partitions b8x8: per-quadrant candidates (B_16x8 / B_8x16 / B_8x8)
-  // spatial direct: searched MBs keep their best explicit candidate (no direct MB / quadrant);
-  // b_spatial_decide weighs it against the exact spatial direct motion in decoding order
+  // spatial direct 1 (wavefront decision): searched MBs keep their best explicit candidate (no
+  // direct MB / quadrant); b_spatial_decide weighs it against the exact spatial direct motion
+  // in decoding order.  2 (fast): direct is priced in parallel with the pre-pass's estimate of
+  // the spatial motion (needs the pre-pass); b_spatial_exact / b_spatial_fixup make it exact
   int spatial;
-  int dbias;  // temporal direct preferred by dbias * lambda in the 16x16 choice (cost_out stays unbiased)
+  int dbias;  // direct preferred by dbias * lambda in the 16x16 choice (cost_out stays unbiased)
+  const uint8_t* czero;  // spatial == 2: colZeroFlag bits per MB (b_direct_mv)
   // routed (route.h): ref0 / ref1 / hp0 / hp1 / ref0k / hp0k are pool bases, the roles come from
   // each B slot's SlotRoute (list-0 entries, list-1 entry, implicit weights)
   const SlotRoute* rt;
@@ -220,6 +229,38 @@ __device__ __forceinline__ int mvbits_se(int v) {
   return 2 * (31 - __clz(x)) + 1;
 }
 
+struct NbMv16 {
+  bool avail;
+  int ref;
+  int mv[2];
+};
+
+__device__ __forceinline__ int med3i(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
+
+// Spatial direct of one list (8.4.1.2.2): refIdx = MinPositive over the neighbours A, B, C
+// (C replaced by D by the caller), the vector = the 16x16 motion-vector predictor of that
+// reference (8.4.1.3: a single neighbour on it gives its vector, else the median, with A
+// standing in for B and C when only A is available)
+__device__ __forceinline__ void spatial_pmv(NbMv16 A, NbMv16 B, NbMv16 C, int& ref, int& px, int& py) {
+  auto minpos = [](int p, int qv) { return (p >= 0 && qv >= 0) ? min(p, qv) : max(p, qv); };
+  ref = minpos(A.ref, minpos(B.ref, C.ref));
+  px = py = 0;
+  if (ref < 0) return;
+  if (!B.avail && !C.avail && A.avail) {
+    B = A;
+    C = A;
+  }
+  const int match = (A.ref == ref) + (B.ref == ref) + (C.ref == ref);
+  if (match == 1) {
+    const NbMv16& m = A.ref == ref ? A : (B.ref == ref ? B : C);
+    px = m.mv[0];
+    py = m.mv[1];
+  } else {
+    px = med3i(A.mv[0], B.mv[0], C.mv[0]);
+    py = med3i(A.mv[1], B.mv[1], C.mv[1]);
+  }
+}
+
 // One wave per MB: lane = (row lane >> 2, columns 4 * (lane & 3) .. +3).
 __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   const Geom& g = a.g;
@@ -243,13 +284,83 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   auto w1of = [&](int rr) { return w1t ? static_cast<int>(w1t[rr & 3]) : a.w1[rr & 3]; };
   const int16_t* dm = a.dmv + o * 16;
   const bool donly = a.direct_only;
+  const bool sfast = a.spatial == 2;
   const int m0x = donly ? 0 : a.mv0[o * 2], m0y = donly ? 0 : a.mv0[o * 2 + 1];
   const int m1x = donly ? 0 : a.mv1[o * 2], m1y = donly ? 0 : a.mv1[o * 2 + 1];
   const uint32_t src = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y) * W + X);
-  // direct: per-quadrant vectors of both lists; bi: the two ME vectors
-  uint32_t drw = 0;  // refIdxL0 of the four direct quadrants (bytes)
+  MbHeader* hrec = a.hdr + o;
+  // The direct candidate per quadrant and list: refIdx (-1: list unused) and vector.
+  //   temporal: the co-located block's scaled motion (b_direct_mv), list 1 from RefPicList1[0];
+  //   spatial (fast, spatial == 2): the pre-pass estimates 8.4.1.2.2 from the neighbours'
+  //     temporal-direct motion standing in for their final motion (colZeroFlag exact) and
+  //     leaves it in the record; the main pass prices it; b_spatial_exact later derives the
+  //     exact motion in decoding order and b_spatial_fixup re-predicts where it differs.
+  int dref_[2][4], dvx[2][4], dvy[2][4];
+  uint32_t drw = 0;  // refIdxL0 of the four temporal-direct quadrants (bytes)
   if (a.dref) drw = *reinterpret_cast<const uint32_t*>(a.dref + o * 4);
-  const int dr = (drw >> (8 * q)) & 255;
+  if (!sfast) {
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      dref_[0][qq] = (drw >> (8 * qq)) & 255;
+      dref_[1][qq] = 0;
+      dvx[0][qq] = dm[qq * 2];
+      dvy[0][qq] = dm[qq * 2 + 1];
+      dvx[1][qq] = dm[8 + qq * 2];
+      dvy[1][qq] = dm[8 + qq * 2 + 1];
+    }
+  } else if (donly) {
+    auto tmot = [&](int n, int l, int qq, bool avail) -> NbMv16 {
+      NbMv16 m{avail, -1, {0, 0}};
+      if (!avail) return m;
+      const size_t on = static_cast<size_t>(slot) * nmb + n;
+      m.ref = l == 0 ? (a.dref ? static_cast<int>(a.dref[on * 4 + qq]) : 0) : 0;
+      m.mv[0] = a.dmv[on * 16 + l * 8 + qq * 2];
+      m.mv[1] = a.dmv[on * 16 + l * 8 + qq * 2 + 1];
+      return m;
+    };
+    const bool aA = mx > 0, aB = my > 0, aC = my > 0 && mx + 1 < g.wmb, aD = mx > 0 && my > 0;
+    int sref[2], spx[2], spy[2];
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+      const NbMv16 A = tmot(mb - 1, l, 1, aA);
+      const NbMv16 Bn = tmot(mb - g.wmb, l, 2, aB);
+      const NbMv16 C = aC ? tmot(mb - g.wmb + 1, l, 2, true) : tmot(mb - g.wmb - 1, l, 3, aD);
+      spatial_pmv(A, Bn, C, sref[l], spx[l], spy[l]);
+    }
+    const bool zero = sref[0] < 0 && sref[1] < 0;
+    const int cz = a.czero ? a.czero[o] : 0;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+      for (int l = 0; l < 2; ++l) {
+        int rf = sref[l], vx = spx[l], vy = spy[l];
+        if (zero) {
+          rf = 0;
+          vx = vy = 0;
+        } else if (rf < 0 || (rf == 0 && ((cz >> qq) & 1))) {
+          vx = vy = 0;
+        }
+        dref_[l][qq] = rf;
+        dvx[l][qq] = vx;
+        dvy[l][qq] = vy;
+      }
+  } else {  // the pre-pass's estimate, left in the record
+    const uint2 hr = *reinterpret_cast<const uint2*>(&hrec->ref[0][0]);
+    const uint4 hm0 = *reinterpret_cast<const uint4*>(&hrec->mv[0][0][0]);
+    const uint4 hm1 = *reinterpret_cast<const uint4*>(&hrec->mv[1][0][0]);
+    const uint32_t w0[4] = {hm0.x, hm0.y, hm0.z, hm0.w}, w1_[4] = {hm1.x, hm1.y, hm1.z, hm1.w};
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      dref_[0][qq] = static_cast<int8_t>((hr.x >> (8 * qq)) & 255u);
+      dref_[1][qq] = static_cast<int8_t>((hr.y >> (8 * qq)) & 255u);
+      dvx[0][qq] = static_cast<int16_t>(w0[qq] & 0xFFFFu);
+      dvy[0][qq] = static_cast<int16_t>(w0[qq] >> 16);
+      dvx[1][qq] = static_cast<int16_t>(w1_[qq] & 0xFFFFu);
+      dvy[1][qq] = static_cast<int16_t>(w1_[qq] >> 16);
+    }
+  }
+  const int dr = dref_[0][q] < 0 ? 0 : dref_[0][q];  // this lane's quadrant
+  const bool du0 = dref_[0][q] >= 0, du1 = dref_[1][q] >= 0;
   const size_t sd = route_index(a.rt, a.nbuf, slot, RO_L0 + (dr & 3));
   const uint8_t *GD = dr ? a.ref0k[dr] + (a.rt ? sd : slot) * g.ysize() : G0,
                 *HD = dr ? a.hp0k[dr] + (a.rt ? sd : slot) * hps : H0;
@@ -258,21 +369,26 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   if (!donly && !searched && a.have_direct) {
     // gated MB: B_Direct_16x16 with the pre-pass's prediction and cost
     if (lane == 0) {
-      MbHeader* h = a.hdr + o;
-      h->kind = h264::MBK_BDIRECT;
-      h->sub_direct = 0;
-      *reinterpret_cast<uint2*>(&h->ref[0][0]) = make_uint2(drw, 0u);
-      uint4* mvp = reinterpret_cast<uint4*>(&h->mv[0][0][0]);
-      const uint4* dv = reinterpret_cast<const uint4*>(dm);  // [list][quadrant][xy] int16
-      mvp[0] = dv[0];
-      mvp[1] = dv[1];
+      hrec->kind = h264::MBK_BDIRECT;
+      hrec->sub_direct = 0;
+      if (!sfast) {  // (spatial: the estimate is in the record already)
+        *reinterpret_cast<uint2*>(&hrec->ref[0][0]) = make_uint2(drw, 0u);
+        uint4* mvp = reinterpret_cast<uint4*>(&hrec->mv[0][0][0]);
+        const uint4* dv = reinterpret_cast<const uint4*>(dm);  // [list][quadrant][xy] int16
+        mvp[0] = dv[0];
+        mvp[1] = dv[1];
+      }
     }
     return;
   }
-  const uint32_t pd = (!donly && a.have_direct)
-                          ? *pout
-                          : wavg4b(mc4(GD, HD, W, H, X, Y, dm[q * 2], dm[q * 2 + 1]),
-                                   mc4(G1, H1, W, H, X, Y, dm[8 + q * 2], dm[8 + q * 2 + 1]), w1of(dr));
+  uint32_t pd;
+  if (!donly && a.have_direct) {
+    pd = *pout;
+  } else {
+    const uint32_t pl0 = du0 ? mc4(GD, HD, W, H, X, Y, dvx[0][q], dvy[0][q]) : 0u;
+    const uint32_t pl1 = du1 ? mc4(G1, H1, W, H, X, Y, dvx[1][q], dvy[1][q]) : 0u;
+    pd = (du0 && du1) ? wavg4b(pl0, pl1, w1of(dr)) : (du0 ? pl0 : pl1);
+  }
   if (donly) *pout = pd;
   const uint32_t pb = donly ? pd : wavg4b(mc4(G0, H0, W, H, X, Y, m0x, m0y), mc4(G1, H1, W, H, X, Y, m1x, m1y), w1of(0));
   // residuals of the four candidates: 0 direct, 1 bi (the two ME vectors), 2 L0, 3 L1 (the ME
@@ -321,13 +437,29 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   // mb_type / motion bits (CABAC-ish): direct "0"; L0 / L1 "10x"; Bi "110000" + two mvds
   const int c_direct = satd_direct + lambda * 1;
   if (donly) {
-    // spatial direct: only MBs whose co-located motion is static in every quadrant (temporal
-    // direct vectors within +-1, refIdxL0 0) may skip the searches -- there spatial direct
-    // predicts zero motion too (colZeroFlag); elsewhere it is unknown before the wavefront
-    bool stat = drw == 0;
+    if (lane == 0) {
+      if (a.spatial == 1) {
+        // spatial direct decided in the wavefront (b_spatial_decide): only MBs whose co-located
+        // motion is static in every quadrant (temporal direct vectors within +-1, refIdxL0 0)
+        // may skip the searches -- there spatial direct predicts zero motion too (colZeroFlag)
+        bool stat = drw == 0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) stat = stat && dm[k] >= -1 && dm[k] <= 1;
-    if (lane == 0) a.cost_out[o] = (a.spatial && !stat) ? kNoCostB : c_direct;
+        for (int k = 0; k < 16; ++k) stat = stat && dm[k] >= -1 && dm[k] <= 1;
+        a.cost_out[o] = stat ? c_direct : kNoCostB;
+      } else {
+        a.cost_out[o] = c_direct;
+      }
+      if (sfast) {  // the estimate, for the main pass (and for gated MBs: their motion)
+#pragma unroll
+        for (int l = 0; l < 2; ++l)
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            hrec->ref[l][qq] = static_cast<int8_t>(dref_[l][qq]);
+            hrec->mv[l][qq][0] = static_cast<int16_t>(dvx[l][qq]);
+            hrec->mv[l][qq][1] = static_cast<int16_t>(dvy[l][qq]);
+          }
+      }
+    }
     return;
   }
   const int c_l0 = a.cost0[o] + lambda * 3;
@@ -335,7 +467,7 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   const int mvb0 = mvbits_se(m0x - a.pm0[o * 2]) + mvbits_se(m0y - a.pm0[o * 2 + 1]);
   const int mvb1 = mvbits_se(m1x - a.pm1[o * 2]) + mvbits_se(m1y - a.pm1[o * 2 + 1]);
   const int c_bi = satd_bi + lambda * (6 + mvb0 + mvb1);
-  const bool no_direct = a.spatial && searched;
+  const bool no_direct = a.spatial == 1 && searched;
   const int dbias = no_direct ? 0 : a.dbias * lambda;
   int mode = 0, best = no_direct ? kNoCostB : c_direct - dbias;  // 0 direct, 1 L0, 2 L1, 3 Bi
   if (c_l0 < best) { mode = 1; best = c_l0; }
@@ -382,9 +514,9 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   uint32_t pw = lm == 0 ? pd : (lm == 1 ? pb : (lm == 2 ? p0w : p1w));
   *reinterpret_cast<uint32_t*>(a.pred_out + o * 256 + r * 16 + c0) = pw;
   if (lane == 0) {
-    MbHeader* h = a.hdr + o;
+    MbHeader* h = hrec;
     h->kind = static_cast<uint8_t>(kind);
-    int sd = 0;
+    int sd_ = 0;
     uint32_t w[2][4];
     int8_t rf[2][4];
 #pragma unroll
@@ -392,10 +524,10 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
       const int m = qm[qq];
       int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
       if (m == 0) {  // direct (the whole MB or a B_Direct_8x8 quadrant)
-        x0 = dm[qq * 2]; y0 = dm[qq * 2 + 1]; x1 = dm[8 + qq * 2]; y1 = dm[8 + qq * 2 + 1];
-        rf[0][qq] = static_cast<int8_t>((drw >> (8 * qq)) & 255);
-        rf[1][qq] = 0;
-        sd |= 1 << qq;
+        x0 = dvx[0][qq]; y0 = dvy[0][qq]; x1 = dvx[1][qq]; y1 = dvy[1][qq];
+        rf[0][qq] = static_cast<int8_t>(dref_[0][qq]);
+        rf[1][qq] = static_cast<int8_t>(dref_[1][qq]);
+        sd_ |= 1 << qq;
       } else {
         const bool u0 = m != 3, u1 = m != 2;
         if (u0) { x0 = m0x; y0 = m0y; }
@@ -406,7 +538,7 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
       w[0][qq] = (static_cast<uint32_t>(x0) & 0xFFFFu) | (static_cast<uint32_t>(y0) << 16);
       w[1][qq] = (static_cast<uint32_t>(x1) & 0xFFFFu) | (static_cast<uint32_t>(y1) << 16);
     }
-    h->sub_direct = static_cast<uint8_t>(kind == h264::MBK_B8x8 ? sd : 0);
+    h->sub_direct = static_cast<uint8_t>(kind == h264::MBK_B8x8 ? sd_ : 0);
 #pragma unroll
     for (int l = 0; l < 2; ++l)
 #pragma unroll
@@ -451,12 +583,6 @@ struct BSpatialArgs {
   int nbuf;
 };
 
-struct NbMv16 {
-  bool avail;
-  int ref;
-  int mv[2];
-};
-
 __device__ __forceinline__ NbMv16 nb16(const MbHeader* h, bool avail, bool intra, int l, int q) {
   NbMv16 n{avail, -1, {0, 0}};
   if (!avail || intra || h264::mbk_is_intra(h->kind)) return n;
@@ -467,8 +593,6 @@ __device__ __forceinline__ NbMv16 nb16(const MbHeader* h, bool avail, bool intra
   }
   return n;
 }
-
-__device__ __forceinline__ int med3i(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
 
 constexpr int kSpatialMaxCols = 480;  // MB columns (8K)
 constexpr int kSpatialWaves = 16;  // 16 row chains per slot: the chain (wmb + 2 hmb MBs) bounds it, not the MB count
@@ -706,6 +830,157 @@ __global__ __launch_bounds__(64 * kSpatialWaves) void b_spatial_decide(BSpatialA
       if (hl == 0 && act) __hip_atomic_store(prog + y, x + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
+}
+
+// ---------------------------------------------------------------- spatial direct, fast path
+// b_decide (spatial = 2) prices direct in parallel with an estimate of the spatial motion and
+// decides every MB; what it cannot know is the neighbours' *final* motion, which 8.4.1.2.2
+// derives the direct motion from.  b_spatial_exact walks each slot's MBs in decoding order --
+// integer work only, one lane per MB row (row y two MBs behind row y - 1, all rows of a slot in
+// one workgroup in lock step, a barrier per step) -- and writes the exact motion of every
+// direct MB / B_Direct_8x8 quadrant into its record, flagging the MBs whose motion changed;
+// b_spatial_fixup then re-predicts those (fully parallel).  The decisions and costs stay as
+// b_decide made them (encode_inter's intra-vs-inter rule, which the derivation must agree on,
+// reads the same costs), so the bitstream is exact while the serial chain costs microseconds
+// instead of b_spatial_decide's SATD per MB on the chain.
+struct BSpatialExactArgs {
+  Geom g;
+  MbHeader* hdr;          // [B, nmb] in / out
+  const int* intra_cost;  // [B, nmb]: an MB turns intra when intra_cost < cost (encode_inter)
+  const int* cost;        // [B, nmb]
+  const uint8_t* czero;   // [B, nmb] colZeroFlag bits (b_direct_mv)
+  uint8_t* fix;           // [B, nmb] out: 1 = the direct motion changed, re-predict
+  const SlotRoute* rt;
+};
+
+constexpr int kExactWaves = 5;  // one lane per MB row: 320 >= 8K's 270 rows
+
+__global__ __launch_bounds__(64 * kExactWaves) void b_spatial_exact(BSpatialExactArgs a) {
+  const Geom& g = a.g;
+  const int slot = blockIdx.x, nmb = g.nmb(), wmb = g.wmb, hmb = g.hmb;
+  if (!route_active(a.rt, slot, SK_B)) return;  // uniform per workgroup
+  __shared__ int nbq[2][kSpatialMaxCols][5];      // [row parity][column]: intra, L0 q2, L0 q3, L1 q2, L1 q3
+  const int y = threadIdx.x;
+  const bool row_ok = y < hmb;
+  MbHeader* H = a.hdr + static_cast<size_t>(slot) * nmb;
+  const int* IC = a.intra_cost + static_cast<size_t>(slot) * nmb;
+  const int* CB = a.cost + static_cast<size_t>(slot) * nmb;
+  const uint8_t* CZ = a.czero + static_cast<size_t>(slot) * nmb;
+  uint8_t* FX = a.fix + static_cast<size_t>(slot) * nmb;
+  int* cur_row = &nbq[y & 1][0][0];
+  const int* up_row = &nbq[(y & 1) ^ 1][0][0];
+  int left_intra = 0, left_q1[2] = {0, 0};
+  const int nsteps = wmb + 2 * (hmb - 1);
+  for (int step = 0; step < nsteps; ++step) {
+    const int x = step - 2 * y;
+    if (row_ok && x >= 0 && x < wmb) {
+      const int mb = y * wmb + x;
+      MbHeader& h = H[mb];
+      const int kind = h.kind;
+      const bool intra = IC[mb] < CB[mb];
+      const int sdir = kind == h264::MBK_BDIRECT ? 15 : (kind == h264::MBK_B8x8 ? h.sub_direct : 0);
+      int fin[4][2];
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+        for (int l = 0; l < 2; ++l)
+          fin[qq][l] = (h.ref[l][qq] & 255) | ((h.mv[l][qq][0] & 4095) << 8) | (h.mv[l][qq][1] << 20);
+      bool changed = false;
+      if (!intra && sdir) {
+        const bool aA = x > 0, aB = y > 0, aC = y > 0 && x + 1 < wmb, aD = x > 0 && y > 0;
+        int refs[2], pmv[2][2];
+#pragma unroll
+        for (int l = 0; l < 2; ++l) {
+          const NbMv16 A = nb_packed(aA, left_intra, left_q1[l]);
+          const NbMv16 Bn = aB ? nb_packed(true, up_row[x * 5], up_row[x * 5 + 1 + 2 * l]) : NbMv16{false, -1, {0, 0}};
+          const NbMv16 C = aC ? nb_packed(true, up_row[(x + 1) * 5], up_row[(x + 1) * 5 + 1 + 2 * l])
+                              : (aD ? nb_packed(true, up_row[(x - 1) * 5], up_row[(x - 1) * 5 + 2 + 2 * l])
+                                    : NbMv16{false, -1, {0, 0}});
+          spatial_pmv(A, Bn, C, refs[l], pmv[l][0], pmv[l][1]);
+        }
+        const bool zero = refs[0] < 0 && refs[1] < 0;
+        const int cz = CZ[mb];
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          if (!((sdir >> qq) & 1)) continue;
+#pragma unroll
+          for (int l = 0; l < 2; ++l) {
+            int rf = refs[l], vx = pmv[l][0], vy = pmv[l][1];
+            if (zero) {
+              rf = 0;
+              vx = vy = 0;
+            } else if (rf < 0 || (rf == 0 && ((cz >> qq) & 1))) {
+              vx = vy = 0;
+            }
+            const int pk = (rf & 255) | ((vx & 4095) << 8) | (vy << 20);
+            if (pk != fin[qq][l]) {
+              changed = true;
+              fin[qq][l] = pk;
+              h.ref[l][qq] = static_cast<int8_t>(rf);
+              h.mv[l][qq][0] = static_cast<int16_t>(vx);
+              h.mv[l][qq][1] = static_cast<int16_t>(vy);
+            }
+          }
+        }
+      }
+      FX[mb] = changed ? 1 : 0;
+      int* e = cur_row + x * 5;
+      e[0] = intra;
+      e[1] = fin[2][0];
+      e[2] = fin[3][0];
+      e[3] = fin[2][1];
+      e[4] = fin[3][1];
+      left_intra = intra;
+      left_q1[0] = fin[1][0];
+      left_q1[1] = fin[1][1];
+    }
+    __syncthreads();
+  }
+}
+
+// Re-prediction of the direct quadrants whose exact motion differs from b_decide's estimate.
+struct BSpatialFixArgs {
+  Geom g;
+  const MbHeader* hdr;
+  const uint8_t* fix;
+  const uint8_t *ref0, *hp0;  // pools [B, nbuf, plane] (every list-0 entry, by route)
+  const uint8_t *ref1, *hp1;
+  uint8_t* pred_out;
+  const SlotRoute* rt;
+  int nbuf;
+};
+
+__global__ __launch_bounds__(64) void b_spatial_fixup(BSpatialFixArgs a) {
+  const Geom& g = a.g;
+  const int nmb = g.nmb();
+  int mb, slot;
+  xcd_unit_slot(mb, slot);
+  if (!route_active(a.rt, slot, SK_B)) return;
+  const size_t o = static_cast<size_t>(slot) * nmb + mb;
+  if (!a.fix[o]) return;  // wave-uniform
+  const int lane = threadIdx.x;
+  const int mx = mb % g.wmb, my = mb / g.wmb;
+  const int W = g.W, H = g.H;
+  const int r = lane >> 2, c0 = (lane & 3) * 4;
+  const int X = mx * 16 + c0, Y = my * 16 + r;
+  const int q = (r >> 3) * 2 + (c0 >> 3);
+  const MbHeader& h = a.hdr[o];
+  const bool dq = h.kind == h264::MBK_BDIRECT || (h.kind == h264::MBK_B8x8 && ((h.sub_direct >> q) & 1));
+  if (!dq) return;  // (lane-divergent exit after the last wave-wide step)
+  const size_t hps = hp_plane_bytes(W, H);
+  const int r0 = h.ref[0][q], r1 = h.ref[1][q];
+  uint32_t p0 = 0, p1 = 0;
+  if (r0 >= 0) {
+    const size_t s0 = route_index(a.rt, a.nbuf, slot, RO_L0 + (r0 & 3));
+    p0 = mc4(a.ref0 + s0 * g.ysize(), a.hp0 + s0 * hps, W, H, X, Y, h.mv[0][q][0], h.mv[0][q][1]);
+  }
+  if (r1 >= 0) {
+    const size_t s1 = route_index(a.rt, a.nbuf, slot, RO_L1);
+    p1 = mc4(a.ref1 + s1 * g.ysize(), a.hp1 + s1 * hps, W, H, X, Y, h.mv[1][q][0], h.mv[1][q][1]);
+  }
+  const int w1 = a.rt ? a.rt[slot].w1[r0 & 3] : 32;
+  *reinterpret_cast<uint32_t*>(a.pred_out + o * 256 + r * 16 + c0) =
+      (r0 >= 0 && r1 >= 0) ? wavg4b(p0, p1, w1) : (r0 >= 0 ? p0 : p1);
 }
 
 // ---------------------------------------------------------------- P_Skip-aware vector choice
@@ -1351,8 +1626,9 @@ using namespace mivc::gpu;
 
 extern "C" void mivc_launch_b_direct(int B, int wmb, int hmb, const void* col, const int* dsf, const int* direct_copy,
                                      int nref, int16_t* dmv, int8_t* dref, int16_t* pm0, int16_t* pm1, void* stream,
-                                     const void* route, int nbuf) {
+                                     const void* route, int nbuf, uint8_t* czero) {
   BDirectArgs a;
+  a.czero = czero;
   a.rt = static_cast<const SlotRoute*>(route);
   a.nbuf = nbuf;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
@@ -1376,8 +1652,9 @@ extern "C" void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src
                                      const int* qp, const int8_t* aq, void* hdr, uint8_t* pred_out, int* cost_out,
                                      void* stream, const int* w1, int nref, const int8_t* dref,
                                      const uint8_t* const* ref0k, const uint8_t* const* hp0k, int direct_only, int bparts, int have_direct,
-                                     int spatial, int dbias, const void* route, int nbuf) {
+                                     int spatial, int dbias, const void* route, int nbuf, const uint8_t* czero) {
   BDecideArgs a;
+  a.czero = czero;
   a.rt = static_cast<const SlotRoute*>(route);
   a.nbuf = nbuf;
   a.spatial = spatial;
@@ -1546,4 +1823,36 @@ extern "C" void mivc_launch_b_spatial(int B, int wmb, int hmb, void* hdr, const 
   a.qp = qp;
   a.aq = aq;
   hipLaunchKernelGGL(b_spatial_decide, dim3(B), dim3(64 * kSpatialWaves), 0, static_cast<hipStream_t>(stream), a);
+}
+
+extern "C" void mivc_launch_b_spatial_exact(int B, int wmb, int hmb, void* hdr, const int* intra_cost, const int* cost,
+                                            const uint8_t* czero, uint8_t* fix, void* stream, const void* route) {
+  BSpatialExactArgs a;
+  a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
+  a.hdr = static_cast<MbHeader*>(hdr);
+  a.intra_cost = intra_cost;
+  a.cost = cost;
+  a.czero = czero;
+  a.fix = fix;
+  a.rt = static_cast<const SlotRoute*>(route);
+  const int waves = (hmb + 63) / 64;
+  hipLaunchKernelGGL(b_spatial_exact, dim3(B), dim3(64 * waves), 0, static_cast<hipStream_t>(stream), a);
+}
+
+extern "C" void mivc_launch_b_spatial_fixup(int B, int wmb, int hmb, const void* hdr, const uint8_t* fix,
+                                            const uint8_t* ref0, const uint8_t* hp0, const uint8_t* ref1,
+                                            const uint8_t* hp1, uint8_t* pred_out, void* stream, const void* route,
+                                            int nbuf) {
+  BSpatialFixArgs a;
+  a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
+  a.hdr = static_cast<const MbHeader*>(hdr);
+  a.fix = fix;
+  a.ref0 = ref0;
+  a.hp0 = hp0;
+  a.ref1 = ref1;
+  a.hp1 = hp1;
+  a.pred_out = pred_out;
+  a.rt = static_cast<const SlotRoute*>(route);
+  a.nbuf = nbuf;
+  hipLaunchKernelGGL(b_spatial_fixup, dim3(wmb * hmb, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
 }

@@ -35,7 +35,12 @@ void mivc_launch_b_spatial(int B, int wmb, int hmb, void* hdr, const void* col, 
                            const int* qp, const int8_t* aq, int bias, const void* route, int nbuf);
 void mivc_launch_b_direct(int B, int wmb, int hmb, const void* col, const int* dsf, const int* direct_copy, int nref,
                           int16_t* dmv, int8_t* dref, int16_t* pm0, int16_t* pm1, void* stream, const void* route,
-                          int nbuf);
+                          int nbuf, uint8_t* czero);
+void mivc_launch_b_spatial_exact(int B, int wmb, int hmb, void* hdr, const int* intra_cost, const int* cost,
+                                 const uint8_t* czero, uint8_t* fix, void* stream, const void* route);
+void mivc_launch_b_spatial_fixup(int B, int wmb, int hmb, const void* hdr, const uint8_t* fix, const uint8_t* ref0,
+                                 const uint8_t* hp0, const uint8_t* ref1, const uint8_t* hp1, uint8_t* pred_out,
+                                 void* stream, const void* route, int nbuf);
 void mivc_launch_p_refine(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref, const uint8_t* hp,
                           const int16_t* mv_in, int16_t* mv_out, int* cost, const int16_t* pm, uint8_t* pred,
                           const int* qp, const int8_t* aq, void* stream, const void* route, int nbuf);
@@ -46,7 +51,7 @@ void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src_y, const u
                           void* hdr, uint8_t* pred_out, int* cost_out, void* stream, const int* w1, int nref,
                           const int8_t* dref, const uint8_t* const* ref0k, const uint8_t* const* hp0k,
                           int direct_only, int bparts, int have_direct, int spatial, int dbias, const void* route,
-                          int nbuf);
+                          int nbuf, const uint8_t* czero);
 void mivc_launch_aq_offsets(int B, int wmb, int hmb, const uint8_t* sy, const uint8_t* su, const uint8_t* sv,
                             float strength, const float* extra, long long extra_stride, int8_t* out, void* stream,
                             const void* route);
@@ -234,16 +239,32 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("route") = 0, py::arg("nbuf") = 0);
   m.def("b_direct", [](int B, int wmb, int hmb, uintptr_t col, std::vector<int> dsf, std::vector<int> direct_copy,
                        uintptr_t dmv, uintptr_t pm0, uintptr_t pm1, uintptr_t stream, uintptr_t dref, uintptr_t route,
-                       int nbuf) {
+                       int nbuf, uintptr_t czero) {
     if (dsf.empty() || dsf.size() > 4 || dsf.size() != direct_copy.size())
       throw std::invalid_argument("b_direct: one (dsf, direct_copy) pair per list-0 picture, at most 4");
     if (route && nbuf < 1) throw std::invalid_argument("b_direct: a routed launch needs the pool size");
     mivc_launch_b_direct(B, wmb, hmb, P<void>(col), dsf.data(), direct_copy.data(), static_cast<int>(dsf.size()),
                          P<int16_t>(dmv), P<int8_t>(dref), P<int16_t>(pm0), P<int16_t>(pm1), S(stream), P<void>(route),
-                         nbuf);
+                         nbuf, P<uint8_t>(czero));
   }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("col"), py::arg("dsf"), py::arg("direct_copy"),
      py::arg("dmv"), py::arg("pm0"), py::arg("pm1"), py::arg("stream"), py::arg("dref") = 0, py::arg("route") = 0,
-     py::arg("nbuf") = 0);
+     py::arg("nbuf") = 0, py::arg("czero") = 0);
+  m.def("b_spatial_exact", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t intra_cost, uintptr_t cost,
+                              uintptr_t czero, uintptr_t fix, uintptr_t stream, uintptr_t route) {
+    // spatial direct, fast path: the exact direct motion in decoding order (one lane per MB row)
+    if (hmb > 320 || wmb > 480) throw std::invalid_argument("b_spatial_exact: at most 320 MB rows and 480 columns");
+    if (!hdr || !intra_cost || !cost || !czero || !fix) throw std::invalid_argument("b_spatial_exact: null buffer");
+    mivc_launch_b_spatial_exact(B, wmb, hmb, P<void>(hdr), P<int>(intra_cost), P<int>(cost), P<uint8_t>(czero),
+                                P<uint8_t>(fix), S(stream), P<void>(route));
+  });
+  m.def("b_spatial_fixup", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t fix, uintptr_t ref0, uintptr_t hp0,
+                              uintptr_t ref1, uintptr_t hp1, uintptr_t pred_out, uintptr_t stream, uintptr_t route,
+                              int nbuf) {
+    if (!route || nbuf < 1) throw std::invalid_argument("b_spatial_fixup: routed launches only");
+    mivc_launch_b_spatial_fixup(B, wmb, hmb, P<void>(hdr), P<uint8_t>(fix), P<uint8_t>(ref0), P<uint8_t>(hp0),
+                                P<uint8_t>(ref1), P<uint8_t>(hp1), P<uint8_t>(pred_out), S(stream), P<void>(route),
+                                nbuf);
+  });
   m.def("p_refine", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref, uintptr_t hp, uintptr_t mv_in,
                        uintptr_t mv_out, uintptr_t cost, uintptr_t pm, uintptr_t pred, uintptr_t qp, uintptr_t aq,
                        uintptr_t stream, uintptr_t route, int nbuf) {
@@ -259,7 +280,7 @@ PYBIND11_MODULE(_hip, m) {
                        uintptr_t pred1, uintptr_t pm0, uintptr_t pm1, uintptr_t dmv, uintptr_t qp, uintptr_t aq,
                        uintptr_t hdr, uintptr_t pred_out, uintptr_t cost_out, uintptr_t stream, std::vector<int> w1,
                        uintptr_t dref, std::vector<uintptr_t> ref0k, std::vector<uintptr_t> hp0k, int direct_only, int bparts, int have_direct,
-                       int spatial, int dbias, uintptr_t route, int nbuf) {
+                       int spatial, int dbias, uintptr_t route, int nbuf, uintptr_t czero) {
     // w1: implicit list-1 weight per list-0 picture; ref0k / hp0k: luma / half-sample planes of
     // RefPicList0[1..] (direct prediction of quadrants whose co-located block used a farther picture)
     if (w1.empty() || w1.size() > 4) throw std::invalid_argument("b_decide: one implicit weight per list-0 picture");
@@ -279,14 +300,14 @@ PYBIND11_MODULE(_hip, m) {
                          P<uint8_t>(pred0), P<uint8_t>(pred1), P<int16_t>(pm0), P<int16_t>(pm1), P<int16_t>(dmv),
                          P<int>(qp), P<int8_t>(aq), P<void>(hdr), P<uint8_t>(pred_out), P<int>(cost_out), S(stream),
                          w1.data(), static_cast<int>(n), (n > 1 || route) ? P<int8_t>(dref) : nullptr, rk, hk, direct_only,
-                         bparts, have_direct, spatial, dbias, P<void>(route), nbuf);
+                         bparts, have_direct, spatial, dbias, P<void>(route), nbuf, P<uint8_t>(czero));
   }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("src"), py::arg("ref0"), py::arg("ref1"), py::arg("hp0"),
      py::arg("hp1"), py::arg("mv0"), py::arg("mv1"), py::arg("cost0"), py::arg("cost1"), py::arg("pred0"),
      py::arg("pred1"), py::arg("pm0"), py::arg("pm1"), py::arg("dmv"), py::arg("qp"), py::arg("aq"), py::arg("hdr"),
      py::arg("pred_out"), py::arg("cost_out"), py::arg("stream"), py::arg("w1") = std::vector<int>{32},
      py::arg("dref") = 0, py::arg("ref0k") = std::vector<uintptr_t>{}, py::arg("hp0k") = std::vector<uintptr_t>{},
      py::arg("direct_only") = 0, py::arg("bparts") = 0, py::arg("have_direct") = 0, py::arg("spatial") = 0, py::arg("dbias") = 0,
-     py::arg("route") = 0, py::arg("nbuf") = 0);
+     py::arg("route") = 0, py::arg("nbuf") = 0, py::arg("czero") = 0);
   m.def("aq_offsets", [](int B, int wmb, int hmb, uintptr_t sy, uintptr_t su, uintptr_t sv, float strength,
                          uintptr_t out, uintptr_t stream, uintptr_t extra, long long extra_stride, uintptr_t route) {
     mivc_launch_aq_offsets(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), strength, P<float>(extra),

@@ -126,7 +126,14 @@ class H264Params:
     # spatial direct: direct is taken when its cost <= the explicit candidate's + direct_bias * lambda
     direct_bias: int = int(os.environ.get("MIVC_DIRECT_BIAS", 8))
     # spatial direct: the B gate skips the searches of MBs with static co-located motion only
+    # (wavefront decision) / of MBs whose estimated spatial direct cost passes b_gate (fast path)
     spatial_gate: bool = os.environ.get("MIVC_SPATIAL_GATE", "1") != "0"
+    # spatial direct decision: False (fast, default) = priced in parallel from an estimate of the
+    # neighbours' motion, then made exact by an integer-only decoding-order pass
+    # (b_spatial_exact) and re-predicted where the estimate was off (b_spatial_fixup); True =
+    # the exact derivation priced MB by MB inside the wavefront (b_spatial_decide, ~3.7 ms per
+    # picture of serial chain)
+    spatial_wavefront: bool = os.environ.get("MIVC_SPATIAL_WAVEFRONT", "0") != "0"
     # temporal direct: B_Direct_16x16 preferred by tdirect_bias * lambda in b_decide's choice
     # (-0.36 % BD-rate at 8, profiles/r3_direct_rd.md)
     tdirect_bias: int = int(os.environ.get("MIVC_TDIRECT_BIAS", 8))
@@ -339,6 +346,8 @@ class GpuH264Encoder:
             self.pm0 = torch.zeros((B, nmb, 2), dtype=i16, device=dev)
             self.pm1 = torch.zeros((B, nmb, 2), dtype=i16, device=dev)
             self.dmv = torch.zeros((B, nmb, 16), dtype=i16, device=dev)
+            self.czero = torch.zeros((B, nmb), dtype=u8, device=dev)  # colZeroFlag bits (spatial direct)
+            self.sfix = torch.zeros((B, nmb), dtype=u8, device=dev)   # direct MBs re-predicted after the exact pass
             # records of every reference picture (the co-located candidates of B pictures)
             self.col_pool = torch.zeros((B, NB, nmb, MB_HDR_BYTES), dtype=u8, device=dev)
         if params.eff_weightp():
@@ -575,17 +584,21 @@ class GpuH264Encoder:
                                       route=rt, nbuf=NB)
         if st["B"]:
             br = self.p.b_me_range
-            # spatial direct cannot be priced before the wavefront: its gate passes static MBs only
-            spatial = int(self.p.direct == "spatial")
-            bg = int(self.p.b_gate) if not spatial or self.p.spatial_gate else 0
+            spatial = self.p.direct == "spatial"
+            sfast = spatial and not self.p.spatial_wavefront
+            mode = 2 if sfast else int(spatial)
+            # wavefront spatial direct cannot be priced before the wavefront: its gate passes
+            # static MBs only; the fast path prices its estimate in the pre-pass, which it needs
+            bg = int(self.p.b_gate) if (not spatial or sfast or self.p.spatial_gate) else 0
+            dbias = int(self.p.tdirect_bias) if not spatial else (int(self.p.direct_bias) if sfast else 0)
             with stt("me_b"):
                 self.hip.b_direct(B, wmb, hmb, P(self.col_pool), [0], [1], P(self.dmv), P(self.pm0), P(self.pm1), s,
-                                  P(self.dref), rt, NB)
-                if bg != 0:  # direct costs first: MBs that direct already predicts well are not searched
+                                  P(self.dref), rt, NB, P(self.czero))
+                if bg != 0 or sfast:  # direct costs first: MBs that direct already predicts well are not searched
                     self.hip.b_decide(B, wmb, hmb, sy, py, py, hpp, hpp, P(self.mv), P(self.mv1), P(self.me_cost),
                                       P(self.me_cost1), P(self.pred), P(self.pred1), P(self.pm0), P(self.pm1),
                                       P(self.dmv), P(self.qp), aq, P(hdr), P(self.pred_b), P(self.cost_b), s, [32],
-                                      P(self.dref), [], [], 1, spatial=spatial, route=rt, nbuf=NB)
+                                      P(self.dref), [], [], 1, spatial=mode, route=rt, nbuf=NB, czero=P(self.czero))
                 gate = P(self.cost_b) if bg != 0 else 0
                 self.hip.me(B, wmb, hmb, sy, py, P(self.pm0), P(self.mv), P(self.me_cost), P(self.pred),
                             P(self.intra_cost), P(self.qp), br, self.p.subpel, s, hpp, aq, 1, self.p.b_early_sad,
@@ -599,9 +612,14 @@ class GpuH264Encoder:
                                   P(self.me_cost1), P(self.pred), P(self.pred1), P(self.pm0), P(self.pm1),
                                   P(self.dmv), P(self.qp), aq, P(hdr), P(self.pred_b), P(self.cost_b), s, [32],
                                   P(self.dref), [], [], 0, int(self.p.eff_partitions() and self.p.bpartitions),
-                                  int(bg != 0), spatial, int(self.p.tdirect_bias) if not spatial else 0,
-                                  route=rt, nbuf=NB)
-            if spatial:
+                                  int(bg != 0 or sfast), mode, dbias, route=rt, nbuf=NB, czero=P(self.czero))
+            if sfast:
+                with stt("b_spatial"):
+                    self.hip.b_spatial_exact(B, wmb, hmb, P(hdr), P(self.intra_cost), P(self.cost_b), P(self.czero),
+                                             P(self.sfix), s, rt)
+                    self.hip.b_spatial_fixup(B, wmb, hmb, P(hdr), P(self.sfix), py, hpp, py, hpp, P(self.pred_b), s,
+                                             rt, NB)
+            elif spatial:
                 with stt("b_spatial"):
                     self.hip.b_spatial(B, wmb, hmb, P(hdr), P(self.col_pool), sy, py, hpp, [py], [hpp], [32],
                                        P(self.pred_b), P(self.err), s, P(self.intra_cost), P(self.cost_b), P(self.qp),

@@ -442,3 +442,16 @@ def test_gpu_h264_pyramid_spatial_roundtrip_b8x8(host):
     _check_roundtrip(host, enc, res, 352, 288)
     assert any(q.kind == "B" and q.ref for q in enc.last_plans[0])
     enc.close()
+
+
+@pytest.mark.parametrize("wavefront", [False, True])
+def test_gpu_h264_spatial_direct_modes_roundtrip(host, wavefront):
+    """Spatial direct, both decision paths: the fast one (parallel pricing of an estimate, then
+    the exact decoding-order derivation + re-prediction) and the wavefront one -- every B
+    picture bit-exact against the CPU decoder, with direct MBs present."""
+    enc, res, _ = _run(352, 288, slots=2, frames=9, crf=26, bframes=3, direct="spatial",
+                       spatial_wavefront=wavefront)
+    _check_roundtrip(host, enc, res, 352, 288)
+    kinds = np.concatenate([np.asarray(p["mb_kind"]).ravel() for r in res for p in host.decode(r.bitstream)])
+    assert (kinds == 13).sum() > 0
+    enc.close()
