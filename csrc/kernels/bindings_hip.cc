@@ -146,6 +146,8 @@ void mivc_launch_sse(int B, int W, int H, int w, int h, const uint8_t* sy, const
                      const uint8_t* ry, const uint8_t* ru, const uint8_t* rv, unsigned long long* sse,
                      float* ssim_sum, void* stream, const void* route, int nbuf);
 long long mivc_lookahead_low_bytes(int w, int h, int N);
+int mivc_launch_lookahead_multi(const uint8_t* low, int w, int h, int N, int F, const int* blk_cost, const int* blk_mv,
+                                int D, int range, unsigned long long* out, void* stream);
 int mivc_launch_hevc_prep_frame(int B, const void* sy, const void* su, const void* sv, long long ss_y, long long ss_c,
                                 int pitch_y, int pitch_c, int bps, int w, int h, uint16_t* dy, uint16_t* du,
                                 uint16_t* dv, uint8_t* d8, int W, int H, int shift, int bd, void* stream);
@@ -660,6 +662,12 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("ry"), py::arg("ru"), py::arg("rv"), py::arg("sse"), py::arg("ssim"), py::arg("stream"),
      py::arg("route") = 0, py::arg("nbuf") = 0);
   m.def("lookahead_low_bytes", [](int w, int h, int n) { return mivc_lookahead_low_bytes(w, h, n); });
+  m.def("lookahead_multi", [](uintptr_t low, int w, int h, int n, int f, uintptr_t blk_cost, uintptr_t blk_mv, int D,
+                              int range, uintptr_t out, uintptr_t stream) {
+    const int r = mivc_launch_lookahead_multi(P<uint8_t>(low), w, h, n, f, P<int>(blk_cost), P<int>(blk_mv), D, range,
+                                              P<unsigned long long>(out), S(stream));
+    if (r != 0) throw std::invalid_argument("lookahead_multi: bad arguments (" + std::to_string(r) + ")");
+  });
   m.def("lookahead", [](uintptr_t y, int w, int h, long long fstride, int n, int f, uintptr_t low, uintptr_t frame_cost,
                         uintptr_t blk_cost, int range, uintptr_t stream, uintptr_t blk_mv) {
     int rc = mivc_launch_lookahead(P<uint8_t>(y), w, h, fstride, n, f, P<uint8_t>(low),

@@ -253,6 +253,182 @@ __global__ __launch_bounds__(256) void la_cost(LaArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- b-adapt costs (x264 --b-adapt 1)
+// x264's fast B-frame placement compares, per run of pictures, the lowres cost of coding a
+// picture as P from anchors 2..bframes+1 pictures back and as B between its two neighbours.
+// la_multi prices exactly those for every frame of every slot in one launch, reusing
+// la_cost's lowres planes, its per-block intra costs and distance-1 vectors:
+//   * P at distance d = 2..D: a (2R+1)^2 integer search centred on d times the block's
+//     distance-1 vector (constant motion), SATD of the best prediction on MFMA;
+//   * B between f - 1 and f + 1: list 0 = the distance-1 prediction, list 1 = a search of
+//     f + 1 centred on the reversed vector, bi = their rounded average; the block takes the
+//     cheapest of intra, L0, L1, bi.
+// Frame sums of min(intra, candidate) go to out[n][d] (d = 2..D) and out[n][0] (B).
+constexpr int kLaMultiCols = 8;
+
+struct LaMultiArgs {
+  LaGeom g;
+  const uint8_t* low;
+  const int* blk_cost;  // [N, 2, lbh, lbw] (la_cost): intra, inter at distance 1
+  const int* blk_mv;    // [N, lbh, lbw] (la_cost): distance-1 lowres vectors
+  int D;                // largest P distance (bframes + 1), <= kLaMultiCols - 1
+  unsigned long long* out;  // [N, kLaMultiCols]
+};
+
+// 8 lowres bytes of rows (y, y + 1) at column x (any alignment) as MFMA B-operand bytes
+__device__ __forceinline__ v4i la_rows8(const uint8_t* plane, long long ls, int x, int y) {
+  const int xa = x & ~3, sh = x & 3;
+  const uint32_t* q0 = reinterpret_cast<const uint32_t*>(plane + static_cast<long long>(y) * ls + xa);
+  const uint32_t* q1 = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(q0) + ls);
+  const uint32_t e0 = q0[0], e1 = q0[1], e2 = q0[2], f0 = q1[0], f1 = q1[1], f2 = q1[2];
+  return as_s8(__builtin_amdgcn_alignbyte(e1, e0, sh), __builtin_amdgcn_alignbyte(e2, e1, sh),
+               __builtin_amdgcn_alignbyte(f1, f0, sh), __builtin_amdgcn_alignbyte(f2, f1, sh));
+}
+
+// raw 8 bytes of rows (y, y + 1) at column x (the four dwords of la_rows8 before the bias)
+__device__ __forceinline__ uint4 la_raw8(const uint8_t* plane, long long ls, int x, int y) {
+  const int xa = x & ~3, sh = x & 3;
+  const uint32_t* q0 = reinterpret_cast<const uint32_t*>(plane + static_cast<long long>(y) * ls + xa);
+  const uint32_t* q1 = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(q0) + ls);
+  const uint32_t e0 = q0[0], e1 = q0[1], e2 = q0[2], f0 = q1[0], f1 = q1[1], f2 = q1[2];
+  return make_uint4(__builtin_amdgcn_alignbyte(e1, e0, sh), __builtin_amdgcn_alignbyte(e2, e1, sh),
+                    __builtin_amdgcn_alignbyte(f1, f0, sh), __builtin_amdgcn_alignbyte(f2, f1, sh));
+}
+
+// (2R+1)^2 integer search around (cx, cy) (clamped so the window stays inside the padded
+// plane); returns the best offset (SAD + 2 |offset from the centre|), the lane holding its
+// two rows of the block's column
+template <int R>
+__device__ __forceinline__ void la_small_search(const uint8_t* ref, const LaGeom& g, int X0, int ry, uint2 s0, uint2 s1,
+                                                int cx, int cy, int& bx, int& by) {
+  constexpr int side = 2 * R + 1;
+  // the window's 7 aligned dwords per row (from x0 & ~3) and its rows stay inside the plane
+  const int Yb = ry & ~7;  // the block's top row
+  cx = clampi(cx, R - X0, g.ls - 28 - X0 + R);
+  cy = clampi(cy, R - Yb, g.lrows - 8 - R - Yb);
+  const int x0 = X0 + cx - R;
+  const int xa = x0 & ~3, s = x0 & 3;
+  int best = 0x7FFFFFFF;
+  for (int dy = -R; dy <= R; ++dy) {
+    const uint32_t* p0 = reinterpret_cast<const uint32_t*>(ref + static_cast<long long>(ry + cy + dy) * g.ls + xa);
+    const uint32_t* p1 = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(p0) + g.ls);
+    uint32_t w0[6], w1[6];
+    {
+      uint32_t t0[7], t1[7];
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        t0[k] = p0[k];
+        t1[k] = p1[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {  // realign: w starts at column x0
+        w0[k] = __builtin_amdgcn_alignbyte(t0[k + 1], t0[k], s);
+        w1[k] = __builtin_amdgcn_alignbyte(t1[k + 1], t1[k], s);
+      }
+    }
+#pragma unroll
+    for (int dx = -R; dx <= R; ++dx) {
+      const int o = R + dx, wi = o >> 2, sh = o & 3;
+      const uint32_t a0 = __builtin_amdgcn_alignbyte(w0[wi + 1], w0[wi], sh);
+      const uint32_t a1 = __builtin_amdgcn_alignbyte(w0[wi + 2], w0[wi + 1], sh);
+      const uint32_t b0 = __builtin_amdgcn_alignbyte(w1[wi + 1], w1[wi], sh);
+      const uint32_t b1 = __builtin_amdgcn_alignbyte(w1[wi + 2], w1[wi + 1], sh);
+      uint32_t sad = sad4(s0.x, a0, 0);
+      sad = sad4(s0.y, a1, sad);
+      sad = sad4(s1.x, b0, sad);
+      sad = sad4(s1.y, b1, sad);
+      const int cost = sum_col_groups(static_cast<int>(sad)) + 2 * (abs(dx) + abs(dy));
+      best = min(best, (cost << 9) | ((dy + R) * side + (dx + R)));
+    }
+  }
+  const int bi = best & 511;
+  bx = cx + bi % side - R;
+  by = cy + bi / side - R;
+}
+
+template <int R>
+__global__ __launch_bounds__(256) void la_multi(LaMultiArgs a) {
+  const LaGeom& g = a.g;
+  const int nstrips = (g.lbw + 15) >> 4;
+  const int per_frame = nstrips * g.lbh;
+  const long long waves = static_cast<long long>(per_frame) * g.N;
+  const int nwg = static_cast<int>((waves + 3) >> 2);
+  int lin = blockIdx.x;
+  if ((nwg & 7) == 0) lin = (lin & 7) * (nwg >> 3) + (lin >> 3);
+  const long long wv = static_cast<long long>(lin) * 4 + wave_id();
+  if (wv >= waves) return;  // wave-uniform
+  const int n = static_cast<int>(wv / per_frame);
+  const int rem = static_cast<int>(wv - static_cast<long long>(n) * per_frame);
+  const int by = rem / nstrips, strip = rem - by * nstrips;
+  const int lane = lane_id(), c = lane & 15, grp = lane >> 4;
+  const int bx = strip * 16 + c;
+  const bool valid = bx < g.lbw;
+  const int bxc = valid ? bx : g.lbw - 1;
+  const int f = n % g.F;
+  if (f == 0) return;  // the IDR picture: neither P nor B candidates (frame-uniform)
+  v4i H[4], negH[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t wp = 0, wn = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int i = 16 * t + c, k = 16 * grp + 4 * q + b;
+        const bool neg = __builtin_popcount(i & k) & 1;
+        wp |= (neg ? 0xFFu : 0x01u) << (8 * b);
+        wn |= (neg ? 0x01u : 0xFFu) << (8 * b);
+      }
+      H[t][q] = static_cast<int>(wp);
+      negH[t][q] = static_cast<int>(wn);
+    }
+  }
+  const uint8_t* cur = a.low + n * g.lsize;
+  const int X0 = kLaPad + bxc * 8, Y0 = kLaPad + by * 8;
+  const int ry = Y0 + 2 * grp;
+  const uint8_t* c0 = cur + static_cast<long long>(ry) * g.ls + X0;
+  const uint2 s0 = *reinterpret_cast<const uint2*>(c0);
+  const uint2 s1 = *reinterpret_cast<const uint2*>(c0 + g.ls);
+  const v4i sf = as_s8(s0.x, s0.y, s1.x, s1.y);
+  v4i accS[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) accS[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[t], sf, v4i{0, 0, 0, 0}, 0, 0, 0);
+  const long long bo = static_cast<long long>(by) * g.lbw + bxc;
+  const long long plane_b = static_cast<long long>(g.lbh) * g.lbw;
+  const int intra = a.blk_cost[static_cast<long long>(n) * 2 * plane_b + bo];
+  const int inter1 = a.blk_cost[static_cast<long long>(n) * 2 * plane_b + plane_b + bo];
+  const int mv1 = a.blk_mv[static_cast<long long>(n) * plane_b + bo];
+  const int v1x = static_cast<int16_t>(mv1 & 0xFFFF), v1y = mv1 >> 16;
+  const bool mine = grp == 0 && valid;
+  // P at distances 2..D
+  for (int d = 2; d <= a.D && d <= f; ++d) {  // frame-uniform
+    const uint8_t* ref = cur - d * g.lsize;
+    int mx, my;
+    la_small_search<R>(ref, g, X0, ry, s0, s1, d * v1x, d * v1y, mx, my);
+    const int cst = satd_mfma(negH, accS, la_rows8(ref, g.ls, X0 + mx, ry + my)) +
+                    2 * (abs(mx - d * v1x) + abs(my - d * v1y)) + 2 * (abs(v1x) + abs(v1y));
+    const int s = sum64(mine ? min(intra, cst) : 0);
+    if (lane == 0) atomicAdd(a.out + static_cast<long long>(n) * kLaMultiCols + d, static_cast<unsigned long long>(s));
+  }
+  // B between f - 1 and f + 1
+  if (f + 1 < g.F) {  // frame-uniform
+    const uint8_t* r0 = cur - g.lsize;
+    const uint8_t* r1 = cur + g.lsize;
+    int mx, my;
+    la_small_search<R>(r1, g, X0, ry, s0, s1, -v1x, -v1y, mx, my);
+    const int c1 = satd_mfma(negH, accS, la_rows8(r1, g.ls, X0 + mx, ry + my)) + 2 * (abs(mx) + abs(my));
+    const int cx0 = clampi(v1x, -8, 8), cy0 = clampi(v1y, -8, 8);  // la_cost's range: |v1| <= 8
+    const uint4 p0 = la_raw8(r0, g.ls, X0 + cx0, ry + cy0);
+    const uint4 p1 = la_raw8(r1, g.ls, X0 + mx, ry + my);
+    auto avg = [](uint32_t x, uint32_t y) { return (x | y) - (((x ^ y) >> 1) & 0x7F7F7F7Fu); };
+    const int cbi = satd_mfma(negH, accS, as_s8(avg(p0.x, p1.x), avg(p0.y, p1.y), avg(p0.z, p1.z), avg(p0.w, p1.w))) +
+                    2 * (abs(mx) + abs(my) + abs(v1x) + abs(v1y));
+    const int bc = min(min(intra, inter1), min(c1, cbi));
+    const int s = sum64(mine ? bc : 0);
+    if (lane == 0) atomicAdd(a.out + static_cast<long long>(n) * kLaMultiCols, static_cast<unsigned long long>(s));
+  }
+}
+
 }  // namespace gpu
 }  // namespace mivc
 
@@ -295,5 +471,33 @@ extern "C" int mivc_launch_lookahead(const uint8_t* y, int w, int h, long long f
     case 6: hipLaunchKernelGGL(la_cost<6>, grid, dim3(256), 0, s, a); break;
     default: hipLaunchKernelGGL(la_cost<8>, grid, dim3(256), 0, s, a); break;
   }
+  return 0;
+}
+
+// b-adapt costs of N = B*F frames (la_multi): needs the lowres planes, block costs and vectors
+// of a preceding mivc_launch_lookahead on the same workspace.  out: [N, 8] u64 (zeroed here):
+// column d = 2..D the P cost at distance d, column 0 the B cost between the neighbours.
+extern "C" int mivc_launch_lookahead_multi(const uint8_t* low, int w, int h, int N, int F, const int* blk_cost,
+                                           const int* blk_mv, int D, int range, unsigned long long* out,
+                                           void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (w < 16 || h < 16 || (w & 1) || (h & 1) || N <= 0 || F <= 0 || N % F) return -1;
+  if (D < 2 || D >= kLaMultiCols || !blk_cost || !blk_mv || !low || !out) return -2;
+  LaGeom g{};
+  g.w = w;
+  g.h = h;
+  g.N = N;
+  g.F = F;
+  g.lbw = ((w >> 1) + 7) >> 3;
+  g.lbh = ((h >> 1) + 7) >> 3;
+  g.ls = g.lbw * 8 + 2 * kLaPad;
+  g.lrows = g.lbh * 8 + 2 * kLaPad;
+  g.lsize = static_cast<long long>(g.ls) * g.lrows;
+  hipMemsetAsync(out, 0, sizeof(unsigned long long) * kLaMultiCols * N, s);
+  LaMultiArgs a{g, low, blk_cost, blk_mv, D, out};
+  const long long waves = static_cast<long long>((g.lbw + 15) >> 4) * g.lbh * N;
+  const dim3 grid(static_cast<unsigned>((waves + 3) >> 2));
+  if (range <= 2) hipLaunchKernelGGL(la_multi<2>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(la_multi<4>, grid, dim3(256), 0, s, a);
   return 0;
 }

@@ -80,6 +80,9 @@ class H264Params:
     # offset (6 log2 1.3 = 2.27) over the distance-weighted QP of the B picture's references
     bframes: int = 3
     b_qp_offset: float = 6.0 * math.log2(1.3)
+    # x264 --b-adapt: 1 (its default, "fast") places B pictures per slot from the lookahead's
+    # lowres costs (rc/badapt.py, lookahead.hip la_multi); 0 = the fixed pattern
+    b_adapt: int = int(os.environ.get("MIVC_B_ADAPT", 1))
     # integer search radius of the two B-picture searches (their predictors are the scaled
     # co-located vectors of temporal direct, so a small window suffices)
     b_me_range: int = int(os.environ.get("MIVC_B_ME_RANGE", 4))
@@ -196,7 +199,8 @@ class H264Params:
         return (("High CABAC 8x8dct" if self.eff_t8x8() else "Main CABAC") + (" i8x8" if self.eff_t8x8() and self.i8x8 else "")
                 + (" p8x8" if self.eff_partitions() else "") + (" b8x8" if self.eff_partitions() and self.bpartitions and self.eff_bframes() else "") + (f" ref{self.eff_refs()}" if self.eff_refs() > 1 else "")
                 + (" weightp" if self.eff_weightp() else "")
-                + (f" {nb}B" + (" b-pyramid" if self.eff_pyramid() else "") + f" {self.direct}-direct" if nb else "")
+                + (f" {nb}B" + (" b-adapt" if self.b_adapt else "") + (" b-pyramid" if self.eff_pyramid() else "")
+                   + f" {self.direct}-direct" if nb else "")
                 + (" weightb" if nb and self.weightb else ""))
 
     def frame_qps(self) -> tuple[int, int]:
@@ -663,17 +667,26 @@ class GpuH264Encoder:
                     0, st["col_dst"], hdr.index_select(0, st["col_src"]))
 
     def _plans(self, F: int, cuts_h: np.ndarray, anchors_at) -> list[list[PicPlan]]:
-        """Per-slot coding-order plans: x264's fixed --b-adapt 0 pattern with anchors at the
-        forced positions and at each slot's own scene cuts.  ``anchors_at``: display indices
-        forced for every slot, or one iterable per slot."""
+        """Per-slot coding-order plans: B pictures placed by the lookahead (x264 --b-adapt 1,
+        rc/badapt.py) when its costs are at hand, else x264's fixed --b-adapt 0 pattern; anchors
+        at the forced positions and at each slot's own scene cuts.  ``anchors_at``: display
+        indices forced for every slot, or one iterable per slot."""
         per_slot = (isinstance(anchors_at, (list, tuple)) and len(anchors_at) == self.B and len(anchors_at) > 0
                     and all(isinstance(a, (list, tuple, set, frozenset)) for a in anchors_at))
         common = set() if per_slot else {int(d) for d in anchors_at}
         cache: dict[str, list[PicPlan]] = {}
         plans = []
+        multi = getattr(self, "_la_multi", None)
+        adaptive = multi is not None and multi.shape[:2] == (self.B, F)
+        if adaptive:
+            from ..rc.badapt import b_adapt_types
         for b in range(self.B):
             forced = {int(d) for d in anchors_at[b]} if per_slot else common
-            ty = fixed_types(F, self.nb, forced | {d for d in range(1, F) if cuts_h[b, d]})
+            forced = forced | {d for d in range(1, F) if cuts_h[b, d]}
+            if adaptive:
+                ty = b_adapt_types(self._la_costs[b, :, 1], multi[b], multi[b, :, 0], self.nb, self._la_blocks, forced)
+            else:
+                ty = fixed_types(F, self.nb, forced)
             if ty not in cache:
                 cache[ty] = h264_plan(ty, self.nref, self.p.eff_pyramid(), self.nref_frames)
             plans.append(cache[ty])
@@ -1017,30 +1030,66 @@ class GpuH264Encoder:
         return out
 
     # ------------------------------------------------------------------ rate control
-    def crf_qps(self, y: torch.Tensor) -> np.ndarray:
-        """[B, F] CRF QPs of a batch: GPU lookahead frame costs -> x264-style CRF curve."""
+    def _analyse(self, y: torch.Tensor) -> None:
+        """GPU lookahead of a batch: frame costs, scene cuts, MB-tree offsets and (b-adapt) the
+        multi-distance P / B costs (rc/lookahead.py, csrc/kernels/lookahead.hip)."""
         from ..rc.lookahead import GpuLookahead
-        from ..rc.ratecontrol import crf_qps_batch
+        from ..rc.ratecontrol import MBTREE_STRENGTH, scenecut_flags
 
         if getattr(self, "_la", None) is None:
             self._la = GpuLookahead(self.dev, self.p.la_range)
         t0 = time.perf_counter()
-        from ..rc.ratecontrol import MBTREE_STRENGTH, scenecut_flags
         lbw, lbh = GpuLookahead.block_grid(y.shape[3], y.shape[2])
         # MB-tree needs the lookahead's block grid to be the coded MB grid (no -s resize)
         use_mbtree = self.p.mbtree and lbw * lbh == self.nmb
+        badapt = bool(self.p.b_adapt) and self.nb > 0 and y.shape[1] >= 3
+        multi = None
         if use_mbtree:
             costs_d, self._mbtree = self._la.mbtree(y, MBTREE_STRENGTH)
-            costs = costs_d.cpu().numpy()
+            blk, mv = self._la.last_blk, self._la.last_mv
+        elif badapt:
+            costs_d, blk, mv = self._la.frame_costs(y, block_costs=True, block_mvs=True)
         else:
-            costs = self._la.frame_costs(y).cpu().numpy()
-        self._scenecuts = scenecut_flags(costs, float(self.p.scenecut))
-        q = crf_qps_batch(costs, float(self.p.crf), lbw * lbh, scenecuts=self._scenecuts, mbtree=use_mbtree,
-                          bframes=self.nb)
+            costs_d, blk, mv = self._la.frame_costs(y), None, None
+        if badapt:
+            multi = self._la.multi_costs(y, blk, mv, min(7, self.nb + 1)).cpu().numpy()
+        self._la_costs = costs_d.cpu().numpy()
+        self._la_multi = multi
+        self._la_blocks = lbw * lbh
+        self._use_mbtree = use_mbtree
+        self._scenecuts = scenecut_flags(self._la_costs, float(self.p.scenecut))
         self.stats["scenecuts"] = int(self._scenecuts.sum())
         self.timings["lookahead_s"] = self.timings.get("lookahead_s", 0.0) + time.perf_counter() - t0
+
+    def _crf_from_plans(self, plans: list[list[PicPlan]]) -> np.ndarray:
+        """[B, F] CRF QPs of the anchors (x264's curve over the anchors' complexity at their real
+        reference distance, rc/ratecontrol.crf_qps_anchors); B entries are set by the caller."""
+        from ..rc.badapt import anchor_complexity
+        from ..rc.ratecontrol import crf_qps_anchors
+        costs, multi = self._la_costs, self._la_multi
+        B, F = costs.shape[0], costs.shape[1]
+        cplx = np.empty((B, F))
+        for b in range(B):
+            types = [""] * F
+            for pic in plans[b]:
+                types[pic.d] = pic.kind
+            cplx[b] = anchor_complexity("".join(types), costs[b], multi[b] if multi is not None else None)
+        keys = np.zeros((B, F), dtype=bool)
+        keys[:, 0] = True
+        keys |= self._scenecuts
+        q = crf_qps_anchors(cplx, costs[:, :, 0], float(self.p.crf), self._la_blocks, keys,
+                            mbtree=self._use_mbtree, bframes=self.nb)
         self.stats["mean_qp"] = float(q.mean())
         return q
+
+    def crf_qps(self, y: torch.Tensor) -> np.ndarray:
+        """[B, F] CRF QPs of a batch (anchors; B pictures at their references' QP + pbratio):
+        GPU lookahead frame costs -> per-slot GOP plans -> x264-style CRF curve."""
+        from ..rc.ratecontrol import b_qps_from_refs
+        self._analyse(y)
+        plans = self._plans(y.shape[1], self._scenecuts, ())
+        q = self._crf_from_plans(plans)
+        return b_qps_from_refs(q, plans, float(self.p.b_qp_offset)) if self.nb else q
 
     # ------------------------------------------------------------------ public API
     @torch.no_grad()
@@ -1103,14 +1152,18 @@ class GpuH264Encoder:
         qp_i, qp_p = self.p.frame_qps()
         self._scenecuts = None
         self._mbtree = None
+        self._la_multi = None
         self._from_la = False
         if qps is None and self.p.crf is not None and self.p.lookahead:
-            qps = self.crf_qps(y)
+            self._analyse(y)
             self._from_la = True
         cuts_h = self._scenecuts if self._scenecuts is not None else np.zeros((B, F), dtype=bool)
         # a scene cut becomes an anchor of its slot, so the pictures after it predict from the
-        # new scene instead of across the cut (x264 places an I / P picture there)
+        # new scene instead of across the cut (x264 places an I / P picture there); with b-adapt
+        # the lookahead's costs place each slot's B pictures
         plans = self._plans(F, cuts_h, anchors_at)
+        if self._from_la:
+            qps = self._crf_from_plans(plans)
         self.last_plans = plans
         orders = np.array([[pic.d for pic in plans[b]] for b in range(B)], dtype=np.int64)  # [B, F] display per step
         steps_pics = [[plans[b][t] for b in range(B)] for t in range(F)]

@@ -55,6 +55,7 @@ class GpuLookahead:
         B, F, h, w = y.shape
         lbw, lbh = self.block_grid(w, h)
         costs, blk, mv = self.frame_costs(y, block_costs=True, block_mvs=True)
+        self.last_blk, self.last_mv = blk, mv  # for multi_costs (b-adapt)
         n = B * F * lbw * lbh
         if getattr(self, "_prop", None) is None or self._prop.numel() < n:
             self._prop = torch.empty((n,), dtype=torch.int64, device=self.dev)  # fixed-point accumulators
@@ -94,6 +95,24 @@ class GpuLookahead:
         if block_mvs:
             return out, blk, mv
         return (out, blk) if block_costs else out
+
+
+    @torch.no_grad()
+    def multi_costs(self, y: torch.Tensor, blk: torch.Tensor, mv: torch.Tensor, max_dist: int,
+                    search_range: int = 2) -> torch.Tensor:
+        """x264 --b-adapt costs (lookahead.hip la_multi) of the batch whose lowres planes, block
+        costs and distance-1 vectors the last :meth:`frame_costs` call produced: [B, F, 8] int64,
+        column d = 2..max_dist the P cost at distance d, column 0 the B cost between the
+        neighbours (frame sums of min(intra, candidate))."""
+        B, F, h, w = y.shape
+        if self._low is None or blk is None or mv is None:
+            raise ValueError("multi_costs needs a preceding frame_costs(block_costs=True, block_mvs=True)")
+        if not 2 <= int(max_dist) <= 7:
+            raise ValueError("max_dist in 2..7 (bframes 1..6)")
+        out = torch.empty((B * F, 8), dtype=torch.int64, device=self.dev)
+        self.hip.lookahead_multi(self._low.data_ptr(), w, h, B * F, F, blk.data_ptr(), mv.data_ptr(), int(max_dist),
+                                 int(search_range), out.data_ptr(), torch.cuda.current_stream(self.dev).cuda_stream)
+        return out.view(B, F, 8)
 
 
 def lookahead_reference(y: np.ndarray, search_range: int = 6) -> tuple[np.ndarray, np.ndarray]:
@@ -151,3 +170,79 @@ def lookahead_reference(y: np.ndarray, search_range: int = 6) -> tuple[np.ndarra
                     blk[b, f, 1, by, bx] = inter
     frame = np.stack([blk[:, :, 0].sum(axis=(2, 3)), np.minimum(blk[:, :, 0], blk[:, :, 1]).sum(axis=(2, 3))], axis=-1)
     return frame, blk
+
+
+def multi_reference(y: np.ndarray, search_range: int = 6, max_dist: int = 4, multi_range: int = 2) -> np.ndarray:
+    """Plain numpy model of ``la_multi`` (lookahead.hip): [B, F, 8] int64, column d = 2..max_dist
+    the P cost at distance d, column 0 the B cost between the neighbours (frame sums of
+    min(intra, candidate) over the lowres 8x8 blocks), from the same lowres planes, intra costs
+    and distance-1 vectors as :func:`lookahead_reference`."""
+    B, F, h, w = y.shape
+    R, pad, MR = search_range, 16, multi_range
+    lw, lh = w // 2, h // 2
+    lbw, lbh = (lw + 7) // 8, (lh + 7) // 8
+    ls, lr = lbw * 8 + 2 * pad, lbh * 8 + 2 * pad
+    px = np.clip(np.arange(ls) - pad, 0, lw - 1)
+    py = np.clip(np.arange(lr) - pad, 0, lh - 1)
+    yy = y.astype(np.int64)
+    s = (yy[..., 0::2, 0::2][..., :lh, :lw] + yy[..., 0::2, 1::2][..., :lh, :lw] +
+         yy[..., 1::2, 0::2][..., :lh, :lw] + yy[..., 1::2, 1::2][..., :lh, :lw] + 2) >> 2
+    low = s[..., py, :][..., :, px]
+    idx = np.arange(64)
+    pc = np.vectorize(lambda v: bin(v).count("1"))(idx[:, None] & idx[None, :])
+    Hm = np.where(pc % 2 == 1, -1, 1).astype(np.int64)
+
+    def satd(res: np.ndarray) -> int:
+        return int((np.abs(Hm @ res.reshape(64)).sum() + 2) >> 2)
+
+    def search(ref, S, X0, Y0, cx, cy, r):
+        side = 2 * r + 1
+        cx = min(max(cx, r - X0), ls - 28 - X0 + r)
+        cy = min(max(cy, r - Y0), lr - 8 - r - Y0)
+        best = None
+        for dy in range(-r, r + 1):
+            for dx in range(-r, r + 1):
+                P = ref[Y0 + cy + dy:Y0 + cy + dy + 8, X0 + cx + dx:X0 + cx + dx + 8]
+                key = (int(np.abs(S - P).sum()) + 2 * (abs(dx) + abs(dy)), (dy + r) * side + dx + r)
+                if best is None or key < best[0]:
+                    best = (key, cx + dx, cy + dy)
+        return best[1], best[2]
+
+    _, blk = lookahead_reference(y, search_range)
+    out = np.zeros((B, F, 8), dtype=np.int64)
+    for b in range(B):
+        for f in range(1, F):
+            cur = low[b, f]
+            for by in range(lbh):
+                for bx in range(lbw):
+                    X0, Y0 = pad + 8 * bx, pad + 8 * by
+                    S = cur[Y0:Y0 + 8, X0:X0 + 8]
+                    intra, inter1 = int(blk[b, f, 0, by, bx]), int(blk[b, f, 1, by, bx])
+                    # the distance-1 vector of la_cost (same search and tie-break)
+                    ref1 = low[b, f - 1]
+                    v1 = None
+                    side = 2 * R + 1
+                    for dy in range(-R, R + 1):
+                        for dx in range(-R, R + 1):
+                            P = ref1[Y0 + dy:Y0 + dy + 8, X0 + dx:X0 + dx + 8]
+                            key = (int(np.abs(S - P).sum()) + 2 * (abs(dx) + abs(dy)), (dy + R) * side + dx + R)
+                            if v1 is None or key < v1[0]:
+                                v1 = (key, dx, dy)
+                    vx, vy = v1[1], v1[2]
+                    for d in range(2, min(max_dist, f) + 1):
+                        ref = low[b, f - d]
+                        mx, my = search(ref, S, X0, Y0, d * vx, d * vy, MR)
+                        P = ref[Y0 + my:Y0 + my + 8, X0 + mx:X0 + mx + 8]
+                        cst = satd(S - P) + 2 * (abs(mx - d * vx) + abs(my - d * vy)) + 2 * (abs(vx) + abs(vy))
+                        out[b, f, d] += min(intra, cst)
+                    if f + 1 < F:
+                        r1 = low[b, f + 1]
+                        mx, my = search(r1, S, X0, Y0, -vx, -vy, MR)
+                        P1 = r1[Y0 + my:Y0 + my + 8, X0 + mx:X0 + mx + 8]
+                        c1 = satd(S - P1) + 2 * (abs(mx) + abs(my))
+                        cx0, cy0 = min(max(vx, -8), 8), min(max(vy, -8), 8)
+                        P0 = ref1[Y0 + cy0:Y0 + cy0 + 8, X0 + cx0:X0 + cx0 + 8]
+                        Pb = (P0 + P1 + 1) >> 1
+                        cbi = satd(S - Pb) + 2 * (abs(mx) + abs(my) + abs(vx) + abs(vy))
+                        out[b, f, 0] += min(min(intra, inter1), min(c1, cbi))
+    return out

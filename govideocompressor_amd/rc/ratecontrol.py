@@ -164,6 +164,39 @@ def crf_qps_batch(costs: np.ndarray, crf: float, mb_count: int, keyint: int | No
     return np.clip(np.round(qp), max(QP_MIN, qp_min), min(QP_MAX, qp_max)).astype(np.int32)
 
 
+def crf_qps_anchors(cplx: np.ndarray, intra: np.ndarray, crf: float, mb_count: int, keys: np.ndarray,
+                    blur: float = 0.5, qp_min: int = QP_MIN, qp_max: int = QP_MAX, mbtree: bool = False,
+                    bframes: int = 0) -> np.ndarray:
+    """CRF QPs of the anchor pictures of B segments with per-slot GOP structures.
+
+    ``cplx``: [B, F] complexity of every anchor at its real reference distance (NaN for B
+    pictures: x264 keeps their complexity out of the rate-control state and gives them their
+    references' QP, :func:`b_qps_from_refs`); ``intra``: [B, F] intra costs; ``keys``: [B, F]
+    pictures coded intra (the IDR, scene cuts: intra complexity, QP - ipratio).  Returns
+    [B, F] int32 with the B pictures' entries left at the anchors' curve value of their
+    neighbourhood (callers overwrite them)."""
+    c = np.asarray(cplx, dtype=np.float64)
+    B, F = c.shape
+    keys = np.asarray(keys, dtype=bool)
+    anchor = ~np.isnan(c)
+    cx = np.where(keys, np.asarray(intra, dtype=np.float64), np.nan_to_num(c, nan=1.0))
+    cx = np.maximum(cx, 1.0)
+    blurred = np.empty_like(cx)
+    acc = np.zeros(B)
+    wsum = np.zeros(B)
+    for t in range(F):
+        a = anchor[:, t] | keys[:, t]
+        acc = np.where(a, acc * blur + cx[:, t], acc)
+        wsum = np.where(a, wsum * blur + 1.0, wsum)
+        blurred[:, t] = acc / np.maximum(wsum, 1e-9)
+    base = crf_base_complexity(mb_count, bframes)
+    rate_factor = base ** (1.0 - QCOMP) / qp2qscale(crf + (MBTREE_CRF_OFFSET if mbtree else 0.0))
+    qs = np.maximum(blurred ** (1.0 - QCOMP) / rate_factor, 1e-9)
+    qp = 12.0 + 6.0 * np.log2(qs / 0.85)
+    qp[keys] -= IP_OFFSET
+    return np.clip(np.round(qp), max(QP_MIN, qp_min), min(QP_MAX, qp_max)).astype(np.int32)
+
+
 def b_qps_from_refs(qps: np.ndarray, plans, pb_offset: float = PB_OFFSET, ip_offset: float = IP_OFFSET_F,
                     qp_max: int = QP_MAX) -> np.ndarray:
     """B-picture QPs from their references, the x264 / x265 CRF rule: a B picture has no rate

@@ -134,3 +134,22 @@ def test_mbtree_matches_reference():
     got = off.cpu().numpy().reshape(ref.shape)
     assert np.allclose(got, ref, rtol=1e-4, atol=1e-3)
     assert (got[:, -1] == 0).all() and got[:, 0].mean() < -0.1  # early frames are referenced
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(2, 6, 64, 96), (1, 5, 70, 300)])
+def test_lookahead_multi_matches_reference(shape):
+    """x264 --b-adapt costs (la_multi): P at distances 2..4 and B between the neighbours,
+    from small searches around the scaled distance-1 vectors -- exact against the numpy model
+    (search clamps at the plane borders included: the 300-wide clip moves 5 px / frame)."""
+    import torch
+    from govideocompressor_amd.rc.lookahead import GpuLookahead, multi_reference
+
+    y = _clip(*shape, seed=11)
+    la = GpuLookahead("cuda", 6)
+    yd = torch.from_numpy(y).cuda()
+    _, blk, mv = la.frame_costs(yd, block_costs=True, block_mvs=True)
+    got = la.multi_costs(yd, blk, mv, 4).cpu().numpy()
+    ref = multi_reference(y, 6, 4)
+    assert np.array_equal(got, ref), (got[..., :5], ref[..., :5])
+    assert (ref[:, 2:, 2] > 0).all() and (ref[:, 1:-1, 0] > 0).all()
