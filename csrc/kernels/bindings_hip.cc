@@ -15,7 +15,7 @@ namespace py = pybind11;
 extern "C" {
 int mivc_launch_hevc_decode(const mivc::gpu::HevcDecParams* p, int stage, void* stream);
 void mivc_launch_synth(void* y, void* u, void* v, int width, int height, int slots, int frames, int frame0,
-                       uint32_t seed, int bit_depth, int slot0, void* stream);
+                       uint32_t seed, int bit_depth, int slot0, void* stream, int kind);
 void mivc_launch_prep(const uint8_t* in_y, const uint8_t* in_u, const uint8_t* in_v, int w, int h,
                       int64_t in_stride_y, int64_t in_stride_c, int nframes, uint8_t* out_y, uint8_t* out_u,
                       uint8_t* out_v, int ow, int oh, int W, int H, void* stream, const int* fsel);
@@ -25,7 +25,7 @@ void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t
                     int16_t* out_mv, int* out_cost, uint8_t* out_pred, int* out_intra_cost, const int* qp, int range,
                     int subpel, uint8_t* hp, const int8_t* aq, int planes_ready, int early_sad, void* stream,
                     const int* gate_cost, int gate_thresh, const int16_t* cost_mv, const void* route, int nbuf,
-                    int role, int want);
+                    int role, int want, const int16_t* seed_mv);
 void mivc_launch_me_ref_select(int B, int wmb, int hmb, int nref, int16_t* mv, int16_t* mv8, int* cost, uint8_t* pred,
                                const int16_t* xmv, const int* xcost, const uint8_t* xpred, int8_t* mref, const int* qp,
                                const int8_t* aq, void* stream, const void* route);
@@ -169,12 +169,14 @@ PYBIND11_MODULE(_hip, m) {
   m.attr("arch") = "gfx950";
 
   m.def("synth", [](uintptr_t y, uintptr_t u, uintptr_t v, int w, int h, int slots, int frames, int frame0,
-                    uint32_t seed, uintptr_t stream, int bit_depth, int slot0) {
+                    uint32_t seed, uintptr_t stream, int bit_depth, int slot0, int kind) {
     if (bit_depth != 8 && bit_depth != 10) throw std::invalid_argument("synth: bit_depth must be 8 or 10");
+    if (kind < 0 || kind > 6) throw std::invalid_argument("synth: content kind 0..6");
     mivc_launch_synth(P<void>(y), P<void>(u), P<void>(v), w, h, slots, frames, frame0, seed, bit_depth, slot0,
-                      S(stream));
+                      S(stream), kind);
   }, py::arg("y"), py::arg("u"), py::arg("v"), py::arg("w"), py::arg("h"), py::arg("slots"), py::arg("frames"),
-     py::arg("frame0"), py::arg("seed"), py::arg("stream"), py::arg("bit_depth") = 8, py::arg("slot0") = 0);
+     py::arg("frame0"), py::arg("seed"), py::arg("stream"), py::arg("bit_depth") = 8, py::arg("slot0") = 0,
+     py::arg("kind") = 0);
   m.def("prep", [](uintptr_t iy, uintptr_t iu, uintptr_t iv, int w, int h, int64_t sy, int64_t sc, int n,
                    uintptr_t oy, uintptr_t ou, uintptr_t ov, int ow, int oh, int W, int H, uintptr_t stream,
                    uintptr_t fsel) {
@@ -193,19 +195,20 @@ PYBIND11_MODULE(_hip, m) {
   m.def("me", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref, uintptr_t pred_mv, uintptr_t out_mv,
                  uintptr_t out_cost, uintptr_t out_pred, uintptr_t out_intra, uintptr_t qp, int range, int subpel,
                  uintptr_t stream, uintptr_t hp, uintptr_t aq, int planes_ready, int early_sad, uintptr_t gate_cost,
-                 int gate_thresh, uintptr_t cost_mv, uintptr_t route, int nbuf, int role, int want) {
+                 int gate_thresh, uintptr_t cost_mv, uintptr_t route, int nbuf, int role, int want, uintptr_t seed_mv) {
     if (planes_ready && !hp) throw std::invalid_argument("me: planes_ready needs the hp buffer");
     if (route && (nbuf < 1 || role < 0 || role > 4 || (want != 0 && want != 1) || !planes_ready))
       throw std::invalid_argument("me: a routed search needs nbuf, a role (list-0 0..3 / list-1 4), want P/B and the planes");
     mivc_launch_me(B, wmb, hmb, P<uint8_t>(src), P<uint8_t>(ref), P<int16_t>(pred_mv), P<int16_t>(out_mv),
                    P<int>(out_cost), P<uint8_t>(out_pred), P<int>(out_intra), P<int>(qp), range, subpel,
                    P<uint8_t>(hp), P<int8_t>(aq), planes_ready, early_sad, S(stream), P<int>(gate_cost), gate_thresh,
-                   P<int16_t>(cost_mv), P<void>(route), nbuf, role, want);
+                   P<int16_t>(cost_mv), P<void>(route), nbuf, role, want, P<int16_t>(seed_mv));
   }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("src"), py::arg("ref"), py::arg("pred_mv"),
      py::arg("out_mv"), py::arg("out_cost"), py::arg("out_pred"), py::arg("out_intra"), py::arg("qp"),
      py::arg("range"), py::arg("subpel"), py::arg("stream"), py::arg("hp") = 0, py::arg("aq") = 0,
      py::arg("planes_ready") = 0, py::arg("early_sad") = 0, py::arg("gate_cost") = 0, py::arg("gate_thresh") = 0,
-     py::arg("cost_mv") = 0, py::arg("route") = 0, py::arg("nbuf") = 0, py::arg("role") = 0, py::arg("want") = 0);
+     py::arg("cost_mv") = 0, py::arg("route") = 0, py::arg("nbuf") = 0, py::arg("role") = 0, py::arg("want") = 0,
+     py::arg("seed_mv") = 0);
   m.def("me_ref_select", [](int B, int wmb, int hmb, int nref, uintptr_t mv, uintptr_t mv8, uintptr_t cost,
                             uintptr_t pred, uintptr_t xmv, uintptr_t xcost, uintptr_t xpred, uintptr_t mref,
                             uintptr_t qp, uintptr_t aq, uintptr_t stream, uintptr_t route) {

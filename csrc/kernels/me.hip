@@ -56,6 +56,9 @@ struct MeArgs {
   // for RefPicList0[role], with more than `role` active entries) are searched
   const SlotRoute* rt;
   int nbuf, role, want;
+  // an extra candidate per MB (nullable): [B, nmb, 2] quarter-pel, the lookahead's lowres vector
+  // scaled to this picture's reference distance (x264 seeds its search from the lowres motion)
+  const int16_t* seed_mv;
 };
 
 constexpr int kNoCost = 0x3FFFFFFF;
@@ -367,7 +370,12 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   else if (lane < 32) nbv = mx > 0 ? src[static_cast<size_t>(Y0 + lane - 16) * W + X0 - 1] : 0;
   else if (lane == 32) nbv = (mx > 0 && my > 0) ? src[static_cast<size_t>(Y0 - 1) * W + X0 - 1] : 0;
   int pmx = 0, pmy = 0;
-  int cand_x[5] = {0, 0, 0, 0, 0}, cand_y[5] = {0, 0, 0, 0, 0};
+  int cand_x[6] = {0, 0, 0, 0, 0, 0}, cand_y[6] = {0, 0, 0, 0, 0, 0};
+  if (a.seed_mv) {
+    const size_t so = (static_cast<size_t>(slot) * nmb + mb) * 2;
+    cand_x[5] = (a.seed_mv[so] + 2) >> 2;
+    cand_y[5] = (a.seed_mv[so + 1] + 2) >> 2;
+  }
   if (a.pred_mv) {
     const int16_t* pm = a.pred_mv + static_cast<size_t>(slot) * nmb * 2;
     pmx = pm[mb * 2];
@@ -382,9 +390,9 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
     if (my > 0) { cand_x[2] = (pm[(mb - g.wmb) * 2] + 2) >> 2; cand_y[2] = (pm[(mb - g.wmb) * 2 + 1] + 2) >> 2; }
     if (mx < g.wmb - 1) { cand_x[3] = (pm[(mb + 1) * 2] + 2) >> 2; cand_y[3] = (pm[(mb + 1) * 2 + 1] + 2) >> 2; }
   }
-  uint32_t cref[5];
+  uint32_t cref[6];
 #pragma unroll
-  for (int k = 0; k < 5; ++k) {
+  for (int k = 0; k < 6; ++k) {
     cand_x[k] = clampi(cand_x[k], -128, 128);
     cand_y[k] = clampi(cand_y[k], -128, 128);
     const uint8_t* rp = ref + static_cast<size_t>(clampi(Y0 + r4 + cand_y[k], 0, H - 1)) * W;
@@ -464,19 +472,23 @@ __global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
   int cx = 0, cy = 0, best_sad = 0x7FFFFFFF;
   {
     // per-lane SADs are <= 1020, so two candidates share one wave reduction (16-bit halves)
-    int csad[5];
+    int csad[6];
     {
       const uint32_t p01 = static_cast<uint32_t>(wave_sum(static_cast<int>(sad4(my_src, cref[0], 0) | (sad4(my_src, cref[1], 0) << 16))));
       const uint32_t p23 = static_cast<uint32_t>(wave_sum(static_cast<int>(sad4(my_src, cref[2], 0) | (sad4(my_src, cref[3], 0) << 16))));
+      const uint32_t p45 = static_cast<uint32_t>(wave_sum(static_cast<int>(sad4(my_src, cref[4], 0) | (sad4(my_src, cref[5], 0) << 16))));
       csad[0] = p01 & 0xFFFFu;
       csad[1] = p01 >> 16;
       csad[2] = p23 & 0xFFFFu;
       csad[3] = p23 >> 16;
-      csad[4] = wave_sum(static_cast<int>(sad4(my_src, cref[4], 0)));
+      csad[4] = p45 & 0xFFFFu;
+      csad[5] = p45 >> 16;
     }
     int best = 0x7FFFFFFF;
+    const int ncand = a.seed_mv ? 6 : 5;
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {
+    for (int k = 0; k < 6; ++k) {
+      if (k >= ncand) break;
       int sad = csad[k];
       int cost = sad + lambda * (mvbits(cand_x[k] * 4 - pmx) + mvbits(cand_y[k] * 4 - pmy));
       if (cost < best) {
@@ -813,7 +825,7 @@ extern "C" void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, co
                                int* out_intra_cost, const int* qp, int range, int subpel, uint8_t* hp_buf,
                                const int8_t* aq, int planes_ready, int early_sad, void* stream,
                                const int* gate_cost, int gate_thresh, const int16_t* cost_mv, const void* route,
-                               int nbuf, int role, int want) {
+                               int nbuf, int role, int want, const int16_t* seed_mv) {
   // hp_buf: caller-owned [B, 3, H + 8, W + 8] (+64 bytes slack) half-sample plane scratch,
   // resident across frames; nullptr -> stream-ordered scratch for this call only.
   // planes_ready: hp_buf already holds ref_y's planes (an anchor's planes are built once
@@ -856,6 +868,7 @@ extern "C" void mivc_launch_me(int B, int wmb, int hmb, const uint8_t* src_y, co
   a.nbuf = nbuf;
   a.role = role;
   a.want = want;
+  a.seed_mv = seed_mv;
   if (a.range <= 8) hipLaunchKernelGGL(me_p16x16<8>, dim3(wmb * hmb, B), dim3(64), 0, s, a);
   else hipLaunchKernelGGL(me_p16x16<kMaxR>, dim3(wmb * hmb, B), dim3(64), 0, s, a);
   if (!hp_buf) (void)hipFreeAsync(hp, s);

@@ -8,6 +8,16 @@
 // noise -- chosen to exercise motion estimation, intra prediction and residual
 // coding the way camera content does.
 //
+// Content classes (SynthGeom::kind; the RD suite, tools/content_rd.py, measures encoder
+// defaults on all of them, not on the headline content alone):
+//   0 default   pan of up to +-3 / +-1.5 px per frame, objects at +-5 / +-3, a drifting sine
+//   1 pan-fast  pan of 16..32 px per frame (sports, fast camera moves)
+//   2 static    static background (no pan, no drifting pattern), small slow movers
+//   3 fade      the default content faded to near black and back (48-frame period)
+//   4 zoom      a steady zoom-in (1 % per frame) about the picture centre
+//   5 cuts      a scene cut every 30 frames (new background region, inverted luma, objects moved)
+//   6 noise     the default content with +-12 LSB sensor noise
+//
 // Cost structure: the 3-octave value noise is evaluated ONCE per slot into a
 // periodic canvas (its lattice wraps at the canvas size), and the three object
 // textures once into per-slot tiles; a frame is then a bilinear sample of the
@@ -53,7 +63,36 @@ struct SynthGeom {
   int frames, slots, frame0;
   uint32_t seed;
   int slot0;            // global index of slot 0 (content depends on seed and slot0 + slot only)
+  int kind;             // content class (see the file comment)
 };
+
+enum SynthKind : int { SK_DEFAULT = 0, SK_PAN_FAST, SK_STATIC, SK_FADE, SK_ZOOM, SK_CUTS, SK_NOISE, SK_NKINDS };
+
+// the luma pan offset (pixels) of slot seed ss at frame f
+__device__ __forceinline__ void pan_at(const SynthGeom& g, uint32_t ss, int f, float* px, float* py) {
+  const float h1 = (hash3(ss, 1, 0) & 255) / 255.f, h2 = (hash3(ss, 2, 0) & 255) / 255.f;
+  float vx = (h1 - 0.5f) * 6.f, vy = (h2 - 0.5f) * 3.f;
+  if (g.kind == SK_PAN_FAST) {
+    vx = (h1 < 0.5f ? -1.f : 1.f) * (16.f + 32.f * fabsf(h1 - 0.5f));
+    vy = (h2 - 0.5f) * 8.f;
+  } else if (g.kind == SK_STATIC || g.kind == SK_ZOOM) {
+    vx = vy = 0.f;
+  }
+  float ox = 0.f, oy = 0.f;
+  if (g.kind == SK_CUTS) {  // every 30 frames: a jump to another region of the canvas
+    const uint32_t hs = hash3(ss, 77, static_cast<uint32_t>(f / 30));
+    ox = static_cast<float>(hs % 997u);
+    oy = static_cast<float>((hs >> 12) % 613u);
+  }
+  *px = vx * f + ox;
+  *py = vy * f + oy;
+}
+
+// luma gain of the fade class at frame f (1 elsewhere)
+__device__ __forceinline__ float fade_gain(const SynthGeom& g, int f) {
+  if (g.kind != SK_FADE) return 1.f;
+  return 0.15f + 0.85f * (0.5f + 0.5f * __cosf(6.2831853f * f / 48.f));
+}
 
 __device__ __forceinline__ uint32_t slot_seed(const SynthGeom& g, int slot) {
   return g.seed * 7919u + static_cast<uint32_t>(g.slot0 + slot) * 104729u;
@@ -175,8 +214,11 @@ __device__ __forceinline__ FrameConst frame_const(const SynthGeom& g, int fz) {
   c.slot = fz / g.frames;
   c.f = fz % g.frames + g.frame0;
   c.ss = slot_seed(g, c.slot);
+  // static: small slow movers; cuts: the objects jump at every cut
+  const float vs = g.kind == SK_STATIC ? 0.4f : 1.f;
+  const int fo = g.kind == SK_CUTS ? c.f + 1000 * (c.f / 30) : c.f;
 #pragma unroll
-  for (int o = 0; o < 3; ++o) object_pos(g, c.slot, o, c.f, g.width, g.height, g.ow[o], g.oh[o], 1.f, &c.obx[o], &c.oby[o]);
+  for (int o = 0; o < 3; ++o) object_pos(g, c.slot, o, fo, g.width, g.height, g.ow[o], g.oh[o], vs, &c.obx[o], &c.oby[o]);
   return c;
 }
 
@@ -221,10 +263,9 @@ __global__ __launch_bounds__(256) void synth_frame_luma(FrameArgs a) {
     __syncthreads();
     if (threadIdx.x == 0) {
       F.fc = frame_const(g, fz);
-      // per-slot global motion (pan) in pixels/frame, sub-pixel
-      const float vx = ((hash3(F.fc.ss, 1, 0) & 255) / 255.f - 0.5f) * 6.f;
-      const float vy = ((hash3(F.fc.ss, 2, 0) & 255) / 255.f - 0.5f) * 3.f;
-      const float fx = vx * F.fc.f, fy = vy * F.fc.f;
+      // per-slot global motion (pan), sub-pixel
+      float fx, fy;
+      pan_at(g, F.fc.ss, F.fc.f, &fx, &fy);
       const float ixf = floorf(fx), iyf = floorf(fy);
       const float tx = fx - ixf, ty = fy - iyf;
       F.ix = static_cast<int>(ixf);
@@ -278,12 +319,36 @@ __global__ __launch_bounds__(256) void synth_frame_luma(FrameArgs a) {
     auto t0 = [&](int k) { return static_cast<float>((u0w[k >> 2] >> (8 * (k & 3))) & 255u); };
     auto t1 = [&](int k) { return static_cast<float>((u1w[k >> 2] >> (8 * (k & 3))) & 255u); };
     float sn[16];
-    sin_run(0.01f * (x16 + y) + 0.03f * fc.f, 0.01f, sn);
+    sin_run(0.01f * (x16 + y) + (g.kind == SK_STATIC ? 0.f : 0.03f * fc.f), 0.01f, sn);
+    float bg[16];
+    if (g.kind == SK_ZOOM) {
+      // per-pixel bilinear sample of the canvas at the zoomed position (1 % per frame)
+      const float inv = 1.f / (1.f + 0.01f * fc.f), cxm = 0.5f * g.width, cym = 0.5f * g.height;
+      const float sy = (y - cym) * inv + cym;
+      const int iy = static_cast<int>(floorf(sy));
+      const float ty = sy - iy;
+      int ry0 = iy % g.ch;
+      ry0 = ry0 < 0 ? ry0 + g.ch : ry0;
+      const int ry1 = ry0 + 1 == g.ch ? 0 : ry0 + 1;
+      const uint8_t* q0 = a.cy + (static_cast<size_t>(fc.slot) * g.ch + ry0) * g.cw;
+      const uint8_t* q1 = a.cy + (static_cast<size_t>(fc.slot) * g.ch + ry1) * g.cw;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const float sx = (x16 + k - cxm) * inv + cxm;
+        const int ix = static_cast<int>(floorf(sx));
+        const float tx = sx - ix;
+        int c0 = ix % g.cw;
+        c0 = c0 < 0 ? c0 + g.cw : c0;
+        const int c1 = c0 + 1 == g.cw ? 0 : c0 + 1;
+        bg[k] = (q0[c0] * (1.f - tx) + q0[c1] * tx) * (1.f - ty) + (q1[c0] * (1.f - tx) + q1[c1] * tx) * ty;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) bg[k] = t0(k) * F.w00 + t0(k + 1) * F.w10 + t1(k) * F.w01 + t1(k + 1) * F.w11;
+    }
     int lum[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k)
-      lum[k] = static_cast<int>(S * (t0(k) * F.w00 + t0(k + 1) * F.w10 + t1(k) * F.w01 + t1(k + 1) * F.w11 + 20.f * sn[k]) +
-                                0.5f);
+    for (int k = 0; k < 16; ++k) lum[k] = static_cast<int>(S * (bg[k] + 20.f * sn[k]) + 0.5f);
 #pragma unroll
     for (int o = 0; o < 3; ++o) {
       if (run_meets(x16, y, fc.obx[o], fc.oby[o], g.ow[o], g.oh[o], g.width, g.height)) {
@@ -297,12 +362,25 @@ __global__ __launch_bounds__(256) void synth_frame_luma(FrameArgs a) {
         }
       }
     }
+    if (g.kind == SK_FADE || g.kind == SK_CUTS) {
+      const float gain = fade_gain(g, fc.f);
+      const bool inv = g.kind == SK_CUTS && ((fc.f / 30) & 1);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        int v = static_cast<int>(16.f * S + (lum[k] - 16.f * S) * gain + 0.5f);
+        lum[k] = inv ? kMax - v : v;
+      }
+    }
+    const int namp = g.kind == SK_NOISE ? 12 : 2;  // +-LSB at 8 bits
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const uint32_t h = hash3(static_cast<uint32_t>(x16 + 4 * q), static_cast<uint32_t>(y), fc.ss ^ (fc.f * 2654435761u));
 #pragma unroll
-      for (int b = 0; b < 4; ++b)
-        lum[4 * q + b] = clampi(lum[4 * q + b] + (BD == 8 ? noise5(h, b) : noise17(h, b)), 0, kMax);
+      for (int b = 0; b < 4; ++b) {
+        const int nz = namp == 2 ? (BD == 8 ? noise5(h, b) : noise17(h, b))
+                                 : (static_cast<int>(((h >> (8 * b)) & 255u) % (2u * namp + 1u)) - namp) * (BD == 8 ? 1 : 4);
+        lum[4 * q + b] = clampi(lum[4 * q + b] + nz, 0, kMax);
+      }
     }
     store_run<BD>(a.y, (static_cast<size_t>(fz) * g.height + y) * g.width + x16, lum, g.width - x16);
     }
@@ -322,10 +400,10 @@ __global__ __launch_bounds__(256) void synth_frame_chroma(FrameArgs a) {
     __syncthreads();
     if (threadIdx.x == 0) {
       F.fc = frame_const(g, fz);
-      const float vx = ((hash3(F.fc.ss, 1, 0) & 255) / 255.f - 0.5f) * 3.f;
-      const float vy = ((hash3(F.fc.ss, 2, 0) & 255) / 255.f - 0.5f) * 1.5f;
-      F.ix = static_cast<int>(floorf(vx * F.fc.f));
-      F.iy = static_cast<int>(floorf(vy * F.fc.f));
+      float fx, fy;
+      pan_at(g, F.fc.ss, F.fc.f, &fx, &fy);  // chroma moves at half the luma pan
+      F.ix = static_cast<int>(floorf(0.5f * fx));
+      F.iy = static_cast<int>(floorf(0.5f * fy));
 #pragma unroll
       for (int o = 0; o < 3; ++o) {
         F.fc.obx[o] >>= 1;
@@ -392,6 +470,17 @@ __global__ __launch_bounds__(256) void synth_frame_chroma(FrameArgs a) {
         }
       }
     }
+    if (g.kind == SK_FADE || g.kind == SK_CUTS) {
+      const float gain = fade_gain(g, fc.f);
+      const bool swap = g.kind == SK_CUTS && ((fc.f / 30) & 1);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int a0 = static_cast<int>(128.f * S + (cu[k] - 128.f * S) * gain + 0.5f);
+        const int b0 = static_cast<int>(128.f * S + (cv[k] - 128.f * S) * gain + 0.5f);
+        cu[k] = swap ? b0 : a0;
+        cv[k] = swap ? a0 : b0;
+      }
+    }
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       cu[k] = clampi(cu[k], 0, kMax);
@@ -411,9 +500,10 @@ using namespace mivc::gpu;
 
 // bit_depth 8: uint8 planes; 10: uint16 planes holding 10-bit samples
 extern "C" void mivc_launch_synth(void* y, void* u, void* v, int width, int height, int slots, int frames, int frame0,
-                                  uint32_t seed, int bit_depth, int slot0, void* stream) {
+                                  uint32_t seed, int bit_depth, int slot0, void* stream, int kind) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   SynthGeom g{};
+  g.kind = kind;
   g.width = width;
   g.height = height;
   g.cw = (width + 191) / 192 * 192 + 192;

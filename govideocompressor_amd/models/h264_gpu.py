@@ -83,6 +83,10 @@ class H264Params:
     # x264 --b-adapt: 1 (its default, "fast") places B pictures per slot from the lookahead's
     # lowres costs (rc/badapt.py, lookahead.hip la_multi); 0 = the fixed pattern
     b_adapt: int = int(os.environ.get("MIVC_B_ADAPT", 1))
+    # x264 seeds its motion search from the lookahead's lowres motion: the P search and both B
+    # searches get one more candidate, the picture's lowres vector x 2 scaled to its reference
+    # distance (when the lookahead ran on the coded MB grid)
+    lowres_seed: bool = os.environ.get("MIVC_LA_SEED", "1") != "0"
     # integer search radius of the two B-picture searches (their predictors are the scaled
     # co-located vectors of temporal direct, so a small window suffices)
     b_me_range: int = int(os.environ.get("MIVC_B_ME_RANGE", 4))
@@ -333,6 +337,8 @@ class GpuH264Encoder:
         self.pred = torch.zeros((B, nmb, 256), dtype=u8, device=dev)
         self.mref = torch.zeros((B, nmb), dtype=torch.int8, device=dev)
         self.dref = torch.zeros((B, nmb, 4), dtype=torch.int8, device=dev)
+        self.seed = [torch.zeros((B, nmb, 2), dtype=i16, device=dev) for _ in range(2)]  # lowres search seeds L0 / L1
+        self._slot_ar = torch.arange(B, device=dev)
         if self.nref > 1:
             # searches of RefPicList0[1 ..] (P pictures) and the reference choice per MB
             K = self.nref - 1
@@ -532,6 +538,17 @@ class GpuH264Encoder:
         inter = st["P"] or st["B"]
         if inter:
             self.intra_count.zero_()
+        seed0 = seed1 = 0
+        if inter and self._la_mv is not None:
+            # the lookahead's lowres vector of each slot's picture (to the previous picture),
+            # scaled to the reference distances of its lists
+            v = self._la_mv[self._slot_ar, st["disp_d"].long()].reshape(B, self.nmb)
+            dxy = torch.stack((((v << 16) >> 16), v >> 16), -1).float()
+            self.seed[0].copy_((dxy * st["sscale"][0][:, None, None]).round_().clamp_(-2048, 2047))
+            seed0 = P(self.seed[0])
+            if st["B"]:
+                self.seed[1].copy_((dxy * st["sscale"][1][:, None, None]).round_().clamp_(-2048, 2047))
+                seed1 = P(self.seed[1])
         if st["P"]:
             sy_me, wp = sy, 0
             if st["wp"] is not None:
@@ -544,7 +561,7 @@ class GpuH264Encoder:
             with stt("me_p"):
                 self.hip.me(B, wmb, hmb, sy_me, py, P(self.prev_mv), P(self.mv), P(self.me_cost), P(self.pred),
                             P(self.intra_cost), P(self.qp), self.p.me_range, self.p.subpel, s, hpp, aq, 1,
-                            self.p.p_early_sad, 0, 0, 0, rt, NB, 0, SK["P"])
+                            self.p.p_early_sad, 0, 0, 0, rt, NB, 0, SK["P"], seed0)
                 for it in range(int(self.p.skip_refine)):
                     a_, b_ = (self.mv, self.mv_tmp) if it % 2 == 0 else (self.mv_tmp, self.mv)
                     self.hip.p_refine(B, wmb, hmb, sy_me, py, hpp, P(a_), P(b_), P(self.me_cost), P(self.prev_mv),
@@ -606,11 +623,11 @@ class GpuH264Encoder:
                 gate = P(self.cost_b) if bg != 0 else 0
                 self.hip.me(B, wmb, hmb, sy, py, P(self.pm0), P(self.mv), P(self.me_cost), P(self.pred),
                             P(self.intra_cost), P(self.qp), br, self.p.subpel, s, hpp, aq, 1, self.p.b_early_sad,
-                            gate, bg, 0, rt, NB, 0, SK["B"])
+                            gate, bg, 0, rt, NB, 0, SK["B"], seed0)
                 # the L1 search skips the open-loop intra estimate the L0 search just wrote
                 self.hip.me(B, wmb, hmb, sy, py, P(self.pm1), P(self.mv1), P(self.me_cost1), P(self.pred1), 0,
                             P(self.qp), br, self.p.subpel, s, hpp, aq, 1, self.p.b_early_sad, gate, bg, 0, rt, NB,
-                            4, SK["B"])
+                            4, SK["B"], seed1)
             with stt("b_decide"):
                 self.hip.b_decide(B, wmb, hmb, sy, py, py, hpp, hpp, P(self.mv), P(self.mv1), P(self.me_cost),
                                   P(self.me_cost1), P(self.pred), P(self.pred1), P(self.pm0), P(self.pm1),
@@ -705,6 +722,8 @@ class GpuH264Encoder:
         rt["dcopy"] = 1
         K = max(1, self.nref - 1)
         xscale = np.zeros((F, K, B), dtype=np.float32)
+        # lowres-seed scales (quarter-pel per lowres pixel): list 0 / P and list 1
+        sscale = np.zeros((F, 2, B), dtype=np.float32)
         deblock_nonref = bool(self._full_recon)
         col = {}
         colcache: dict[int, tuple] = {}  # one routing column per distinct plan (slots share plans)
@@ -717,6 +736,7 @@ class GpuH264Encoder:
                 c["w1"] = 32
                 c["dcopy"] = 1
                 xs = np.zeros((F, K), dtype=np.float32)
+                ss = np.zeros((F, 2), dtype=np.float32)
                 kinds = {pic.d: pic.kind for pic in plans[b]}
                 refs_at = []
                 for t, pic in enumerate(plans[b]):
@@ -727,6 +747,11 @@ class GpuH264Encoder:
                     r["l0"][:len(pic.bufs0)] = pic.bufs0
                     r["flags"] = (SF_REF if pic.ref else 0) | (SF_DEBLOCK if (pic.ref or deblock_nonref) else 0)
                     r["disp"] = pic.d
+                    if pic.kind != "I":
+                        # lowres vector of picture d points to d - 1: x 2 (full res) x 4 (quarter pel)
+                        ss[t, 0] = 8.0 * (pic.d - pic.refs0[0])
+                        if pic.kind == "B":
+                            ss[t, 1] = -8.0 * (pic.refs1[0] - pic.d)
                     if pic.kind == "P":
                         d0 = max(1, pic.d - pic.refs0[0])
                         for k in range(1, len(pic.refs0)):
@@ -741,15 +766,17 @@ class GpuH264Encoder:
                             r["w1"][k] = dsf >> 2 if self.p.weightb and not copy and -64 <= (dsf >> 2) <= 128 else 32
                     if pic.ref and pic.kind != "I":
                         refs_at.append((t, pic.buf))
-                colcache[key] = (c, xs, refs_at)
-            c, xs, refs_at = colcache[key]
+                colcache[key] = (c, xs, refs_at, ss)
+            c, xs, refs_at, ss = colcache[key]
             rt[:, b] = c
             xscale[:, :, b] = xs
+            sscale[:, :, b] = ss
             for t, buf in refs_at:
                 col.setdefault(t, []).append((b, b * NB + buf))
         rt_d = torch.from_numpy(rt.view(np.uint8).reshape(F, B * 32).copy()).to(dev)
         kinds_d = torch.from_numpy(np.ascontiguousarray(rt["kind"])).to(dev)
         xs_d = torch.from_numpy(xscale).to(dev)
+        ss_d = torch.from_numpy(sscale).to(dev)
         self._route_dev = rt_d  # keeps the table alive while the launches read it
         steps = []
         for t in range(F):
@@ -758,7 +785,7 @@ class GpuH264Encoder:
             st = dict(route=rt_d[t].data_ptr(), P=bool((k == 0).any()), B=bool((k == 1).any()),
                       pmask=kinds_d[t] == 0, maxn0=int(n0p.max()) if n0p.size else 1, xscale=xs_d[t],
                       deblock=bool((rt["flags"][t] & SF_DEBLOCK).any()), ref=bool((rt["flags"][t] & SF_REF).any()),
-                      wp=None, wp_src=None, col_src=None, col_dst=None, kinds=k)
+                      wp=None, wp_src=None, col_src=None, col_dst=None, kinds=k, sscale=ss_d[t])
             if t in col:
                 src, dst = zip(*col[t])
                 st["col_src"] = torch.tensor(src, dtype=torch.long, device=dev)
@@ -1055,6 +1082,8 @@ class GpuH264Encoder:
             multi = self._la.multi_costs(y, blk, mv, min(7, self.nb + 1)).cpu().numpy()
         self._la_costs = costs_d.cpu().numpy()
         self._la_multi = multi
+        # lowres vectors on the MB grid: the search seeds (lowres_seed)
+        self._la_mv = mv if (mv is not None and self.p.lowres_seed and lbw * lbh == self.nmb) else None
         self._la_blocks = lbw * lbh
         self._use_mbtree = use_mbtree
         self._scenecuts = scenecut_flags(self._la_costs, float(self.p.scenecut))
@@ -1153,6 +1182,7 @@ class GpuH264Encoder:
         self._scenecuts = None
         self._mbtree = None
         self._la_multi = None
+        self._la_mv = None
         self._from_la = False
         if qps is None and self.p.crf is not None and self.p.lookahead:
             self._analyse(y)
@@ -1244,6 +1274,7 @@ class GpuH264Encoder:
             self.timings["host_blocked_s"] = self.timings.get("host_blocked_s", 0.0) + time.perf_counter() - tw
             main.wait_event(self.copy_done[k]) if t >= 2 else None
             self._prep_step(y, u, v, orders[:, t], orders_d[t])
+            st["disp_d"] = orders_d[t]
             self.qp.copy_(qps_d[t])
             self._encode_step(st, self.hdr[k], self.coef[k], cuts_d[t] if (t > 0 and cuts_c[:, t].any()) else None)
             if metrics:
@@ -1351,16 +1382,23 @@ class GpuH264Encoder:
             self.copy_pool.shutdown(wait=True)
 
 
+CONTENT_KINDS = ("default", "pan-fast", "static", "fade", "zoom", "cuts", "noise")
+
+
 def synth_clip(slots: int, frames: int, width: int, height: int, seed: int = 0, frame0: int = 0,
-               device: str | torch.device = "cuda", bit_depth: int = 8, slot0: int = 0):
+               device: str | torch.device = "cuda", bit_depth: int = 8, slot0: int = 0, kind: int | str = 0):
     """Generate B x F synthetic I420 frames directly in HBM (see csrc/kernels/synth.hip).
 
     Slot ``b`` shows the content of global slot ``slot0 + b`` (a rank encoding slots
     [r * B, (r + 1) * B) of a global batch renders exactly what one process would).
     ``bit_depth=10`` renders the same content at 10-bit precision into int16 planes
-    (values 0..1023: the canvas interpolation, ramp and noise keep their low bits)."""
+    (values 0..1023: the canvas interpolation, ramp and noise keep their low bits).
+    ``kind``: content class (CONTENT_KINDS: the headline content, fast pan, static background
+    with small movers, fade, zoom, a cut every 30 frames, heavy noise)."""
     if bit_depth not in (8, 10):
         raise ValueError("synth_clip: bit_depth must be 8 or 10")
+    if isinstance(kind, str):
+        kind = CONTENT_KINDS.index(kind)
     hip = native.hip()
     dev = _resolve(device)
     dt = torch.uint8 if bit_depth == 8 else torch.int16
@@ -1368,5 +1406,5 @@ def synth_clip(slots: int, frames: int, width: int, height: int, seed: int = 0, 
     u = torch.empty((slots, frames, height // 2, width // 2), dtype=dt, device=dev)
     v = torch.empty_like(u)
     hip.synth(y.data_ptr(), u.data_ptr(), v.data_ptr(), width, height, slots, frames, frame0, seed & 0xFFFFFFFF,
-              torch.cuda.current_stream(dev).cuda_stream, bit_depth, slot0)
+              torch.cuda.current_stream(dev).cuda_stream, bit_depth, slot0, int(kind))
     return y, u, v

@@ -1,0 +1,118 @@
+"""Multi-content RD suite: encoder configurations x content classes x CRFs, BD-rate per class.
+
+Every default of the H.264 encoder (GOP decisions, direct mode, search ranges, gates) must
+hold up on more than the headline's easy panning content: this runs each content class of
+csrc/kernels/synth.hip (default, fast pan, static + small movers, fade, zoom, cuts, heavy
+noise) through several configurations at four CRFs and reports bitrate, PSNR-Y, frames/s
+and the Bjontegaard delta rate of every configuration against the first, per class.
+
+usage (GPU):  python tools/content_rd.py run OUT.json [--slots 32 --frames 60 --size 1920x1080]
+              python tools/content_rd.py table OUT.json > profiles/r4_content_rd.md
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+CRFS = (18, 23, 28, 33)
+# name -> H264Params overrides.  "r3" = round 3's GOP / direct decisions
+CONFIGS = {
+    "r3": dict(b_adapt=0, pyramid=False, direct="temporal"),
+    "badapt": dict(b_adapt=1, pyramid=False, direct="temporal"),
+    "spatial": dict(b_adapt=1, pyramid=False, direct="spatial"),
+    "pyramid": dict(b_adapt=1, pyramid=True, direct="spatial"),
+    "default": dict(),  # the current defaults
+}
+
+
+def run(args):
+    import torch
+    from govideocompressor_amd.models.h264_gpu import CONTENT_KINDS, GpuH264Encoder, H264Params, synth_clip
+
+    w, h = (int(x) for x in args.size.split("x"))
+    out = {"size": args.size, "slots": args.slots, "frames": args.frames, "points": []}
+    kinds = args.kinds.split(",") if args.kinds else list(CONTENT_KINDS)
+    configs = {k: CONFIGS[k] for k in (args.configs.split(",") if args.configs else CONFIGS)}
+    clips = {}
+    for kind in kinds:
+        clips[kind] = synth_clip(args.slots, args.frames, w, h, seed=17, kind=kind)
+    for cname, over in configs.items():
+        enc = GpuH264Encoder(H264Params(width=w, height=h, **over), slots=args.slots)
+        for kind in kinds:
+            y, u, v = clips[kind]
+            for crf in CRFS:
+                enc.p.crf = float(crf)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                res = enc.encode(y, u, v, metrics=True)
+                torch.cuda.synchronize()
+                dt = time.perf_counter() - t0
+                bits = sum(8 * r.nbytes() for r in res)
+                kbps = bits / (args.slots * args.frames / 30.0) / 1000.0
+                pt = dict(config=cname, kind=kind, crf=crf, kbps=kbps, psnr=float(np.mean([r.psnr_y for r in res])),
+                          ssim=float(np.mean([r.ssim_y for r in res])), fps=args.slots * args.frames / dt,
+                          b_ratio=enc.stats.get("b_ratio", 0.0), scenecuts=enc.stats.get("scenecuts", 0))
+                out["points"].append(pt)
+                print(json.dumps(pt), flush=True)
+        enc.close()
+        del enc
+        torch.cuda.empty_cache()
+    with open(args.out, "w") as f:
+        json.dump(out, f, indent=1)
+
+
+def table(args):
+    from rd_table import bd_rate
+    d = json.load(open(args.out))
+    pts = d["points"]
+    kinds = list(dict.fromkeys(p["kind"] for p in pts))
+    configs = list(dict.fromkeys(p["config"] for p in pts))
+    print(f"# Multi-content RD suite ({d['size']}, {d['slots']} segments x {d['frames']} frames per class, GPU lookahead CRF)\n")
+    print("Content classes of csrc/kernels/synth.hip; PSNR-Y / SSIM-Y are per-frame means over every")
+    print(f"segment; fps = the whole encode call of {d['slots']} segments (lookahead, encode, entropy).\n")
+    print("| class | config | CRF | kb/s | PSNR-Y dB | SSIM-Y | B share | fps |")
+    print("|---|---|---|---|---|---|---|---|")
+    for k in kinds:
+        for c in configs:
+            for p in (q for q in pts if q["kind"] == k and q["config"] == c):
+                print(f"| {k} | {c} | {p['crf']} | {p['kbps']:.1f} | {p['psnr']:.3f} | {p['ssim']:.4f} | "
+                      f"{p['b_ratio']:.2f} | {p['fps']:.0f} |")
+    base = configs[0]
+    print(f"\n| class | " + " | ".join(f"{c} vs {base} (BD-rate, PSNR-Y)" for c in configs[1:]) + " |")
+    print("|---|" + "---|" * (len(configs) - 1))
+    allv = {c: [] for c in configs[1:]}
+    for k in kinds:
+        ref = [(p["crf"], p["kbps"], p["psnr"]) for p in pts if p["kind"] == k and p["config"] == base]
+        row = []
+        for c in configs[1:]:
+            tst = [(p["crf"], p["kbps"], p["psnr"]) for p in pts if p["kind"] == k and p["config"] == c]
+            v = bd_rate(ref, tst)
+            allv[c].append(v)
+            row.append(f"{v:+.2f} %")
+        print(f"| {k} | " + " | ".join(row) + " |")
+    print("| **mean** | " + " | ".join(f"{np.mean(allv[c]):+.2f} %" for c in configs[1:]) + " |")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cmd", choices=("run", "table"))
+    ap.add_argument("out")
+    ap.add_argument("--slots", type=int, default=32)
+    ap.add_argument("--frames", type=int, default=60)
+    ap.add_argument("--size", default="1920x1080")
+    ap.add_argument("--kinds", default="")
+    ap.add_argument("--configs", default="")
+    args = ap.parse_args()
+    run(args) if args.cmd == "run" else table(args)
+
+
+if __name__ == "__main__":
+    main()
