@@ -124,59 +124,85 @@ def config2(args) -> list[dict]:
 
 
 def config3(args) -> list[dict]:
-    """4K30 H.264 (or HEVC) -> H.264: batched GPU decode (host parse of batch k+1 overlapping the
-    GPU work of batch k) + GPU re-encode (models/transcode.py)."""
+    """4K30 H.264 (or HEVC) -> H.264, segment-parallel over the ranks of one node: each rank
+    (one process per GPU, torch.distributed.run) transcodes its contiguous share of the
+    pieces -- batched GPU decode (host parse of batch k+1 overlapping the GPU work of batch k)
+    + GPU re-encode (models/transcode.py) -- and the per-rank outputs are merged into ONE
+    Annex-B stream on rank 0 in piece order (parallel/dist.py SegmentMerge: sizes all-gather,
+    point-to-point payload over xGMI).  The reference's equivalent is pull dispatch of pieces to
+    workers and concat.sh (server.go:161-191, client.go:37-80, server.go:349-361).  Timed:
+    barrier + sync, transcode of this rank's pieces, merge; the time is the max over ranks."""
     import torch
     if not torch.cuda.is_available():
         return [{"config": 3, "value": None, "note": "needs a GPU"}]
     from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
     from govideocompressor_amd.models.hevc_gpu import GpuHevcEncoder, HevcParams
     from govideocompressor_amd.models.transcode import GpuTranscoder
-    W, H, F, S, B = 3840, 2160, args.frames3, args.segments3, args.slots3
+    from govideocompressor_amd.parallel import dist as D
+    env = D.init(prefer_gpu=True)
+    W, H = (int(x) for x in args.size3.split("x"))
+    F, S, B = args.frames3, args.segments3, args.slots3
+    # this rank's contiguous share of the global pieces (rank-major = piece order when merged)
+    lo, hi = env.rank * S // env.world, (env.rank + 1) * S // env.world
     recs = []
     for codec in args.codec3.split(","):
-        # untimed: the 4K input pieces (closed GOPs of F frames), made by this framework's encoders
+        # untimed: the input pieces (closed GOPs of F frames) made by this framework's
+        # encoders; piece i's content depends on i only, not on the split over ranks
         pieces = []
-        mk = (GpuHevcEncoder(HevcParams(width=W, height=H, crf=22.0), slots=B) if codec == "hevc"
-              else GpuH264Encoder(H264Params(width=W, height=H, crf=20), slots=B))
-        for b0 in range(0, S, B):
-            y, u, v = synth_clip(B, F, W, H, seed=3 + b0)
-            pieces += [r.bitstream for r in mk.encode(y, u, v, metrics=False)][:S - b0]
+        mk = (GpuHevcEncoder(HevcParams(width=W, height=H, crf=22.0), slots=B, device=env.device) if codec == "hevc"
+              else GpuH264Encoder(H264Params(width=W, height=H, crf=20), slots=B, device=env.device))
+        for b0 in range(lo, hi, B):
+            y, u, v = synth_clip(B, F, W, H, seed=3, slot0=b0, device=env.device)
+            pieces += [r.bitstream for r in mk.encode(y, u, v, metrics=False)][:hi - b0]
             del y, u, v
         mk.close()
         del mk
         torch.cuda.empty_cache()
-        tc = GpuTranscoder(H264Params(width=W, height=H, crf=23.0), slots=B)
-        tc.run(pieces[:B], 30.0)                                   # warmup batch
+        tc = GpuTranscoder(H264Params(width=W, height=H, crf=23.0), slots=B, device=env.device)
+        if args.warmup:
+            tc.run(pieces[:B], 30.0)  # warmup batch
+        merger = D.SegmentMerge(env)
         torch.cuda.synchronize()
+        D.barrier(env)
         t0 = time.perf_counter()
         outs = tc.run(pieces, 30.0)
+        merged = merger.run(outs)
         torch.cuda.synchronize()
-        wall = time.perf_counter() - t0
+        D.barrier(env)
+        wall = D.max_over_ranks(env, time.perf_counter() - t0)
         tm = dict(tc.timings)
-        # encode-only reference on the same batch width: the decoded frames of one batch
-        codec_in, parsed, _ = tc._parse(pieces[:B])
-        y, u, v, counts = tc._frames(codec_in, parsed, 30.0)
-        del parsed
-        torch.cuda.synchronize()
-        te = time.perf_counter()
-        for _ in range(2):
-            tc._encode(y, u, v, counts)
-        torch.cuda.synchronize()
-        enc_fps = 2 * B * F / (time.perf_counter() - te)
-        del y, u, v
+        enc_fps = None
+        if args.encode_only3:
+            # encode-only reference on the same batch width: the decoded frames of one batch
+            codec_in, parsed, _ = tc._parse(pieces[:B])
+            y, u, v, counts = tc._frames(codec_in, parsed, 30.0)
+            del parsed
+            torch.cuda.synchronize()
+            te = time.perf_counter()
+            for _ in range(2):
+                tc._encode(y, u, v, counts)
+            torch.cuda.synchronize()
+            enc_fps = 2 * B * F / (time.perf_counter() - te)
+            del y, u, v
         tc.close()
         fps = S * F / wall
-        recs.append({"config": 3, "metric": f"transcoded frames/sec (whole node), 4K30 {codec.upper()}->H.264",
-                     "value": round(fps, 2), "unit": "frames/s", "n_gpus": 1, "frames": S * F, "segments": S,
-                     "segments_per_batch": B, "wall_s": round(wall, 3),
-                     "output_bytes": sum(len(o) for o in outs), "encode_only_fps_same_batch": round(enc_fps, 1),
-                     "transcode_vs_encode_only": round(fps / enc_fps, 3),
-                     "stage_s": {k: round(v, 3) for k, v in tm.items()},
-                     "data": f"synthetic 4K {codec.upper()} pieces made by this framework's encoder "
-                             "(no reference clips available)"})
+        if env.is_main:
+            if args.merged_out3:
+                with open(f"{args.merged_out3}.{codec}", "wb") as f:
+                    f.write(memoryview(merged))
+            recs.append({"config": 3, "metric": f"transcoded frames/sec (whole node), {args.size3} {codec.upper()}->H.264",
+                         "value": round(fps, 2), "unit": "frames/s", "n_gpus": env.world, "frames": S * F,
+                         "segments": S, "segments_per_gpu": hi - lo, "segments_per_batch": B,
+                         "parallelism": f"dp{env.world} (segment-parallel, merged on rank 0)",
+                         "wall_s": round(wall, 3), "merged_bytes": int(len(merged)),
+                         "encode_only_fps_same_batch_rank0": round(enc_fps, 1) if enc_fps else None,
+                         "transcode_vs_encode_only": round(fps / env.world / enc_fps, 3) if enc_fps else None,
+                         "stage_s_rank0": {k: round(v, 3) for k, v in tm.items()},
+                         "data": f"synthetic {codec.upper()} pieces made by this framework's encoder "
+                                 "(no reference clips available)"})
         del pieces, outs
         torch.cuda.empty_cache()
+    D.shutdown(env)
     return recs
 
 
@@ -300,6 +326,10 @@ def main():
     ap.add_argument("--segments3", type=int, default=256)
     ap.add_argument("--slots3", type=int, default=64)
     ap.add_argument("--codec3", default="h264,hevc")
+    ap.add_argument("--size3", default="3840x2160")
+    ap.add_argument("--merged-out3", default=None, help="rank 0 writes the merged stream to <path>.<codec>")
+    ap.add_argument("--no-encode-only3", dest="encode_only3", action="store_false",
+                    help="skip the encode-only reference rate of config 3")
     ap.add_argument("--slots4", type=int, default=64)
     ap.add_argument("--frames4", type=int, default=30)
     # 10 segments x 60 frames = a 10 s 8K60 clip (~60 GB of 10-bit samples) resident in HBM

@@ -55,3 +55,20 @@ def test_rccl_world1_collectives_on_device():
              {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
               "MASTER_PORT": str(_port()), "MIVC_DIST_FORCE": "1"}, timeout=200)
     assert r.stdout.strip().endswith("OK")
+
+
+def test_config3_transcode_world2_merge_matches_world1(tmp_path, host):
+    """BASELINE config 3 as an 8-GPU-ready harness: bench/run.py --config 3 under
+    torch.distributed.run shards the pieces over the ranks, each transcodes its share (GPU
+    decode + re-encode) and rank 0 merges ONE stream in piece order.  At world 2 (two ranks on
+    this GPU, host collectives) the merged stream is byte-identical to world 1's, and every
+    picture of it decodes."""
+    common = ["bench/run.py", "--config", "3", "--size3", "320x192", "--segments3", "8", "--slots3", "4",
+              "--frames3", "8", "--codec3", "h264", "--warmup", "0", "--no-encode-only3"]
+    w1, w2 = tmp_path / "w1", tmp_path / "w2"
+    _run([sys.executable, *common, "--merged-out3", str(w1)], {})
+    _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+          "127.0.0.1", "--master-port", str(_port()), *common, "--merged-out3", str(w2)], {"MIVC_DIST_BACKEND": "gloo"})
+    a, b = (tmp_path / "w1.h264").read_bytes(), (tmp_path / "w2.h264").read_bytes()
+    assert len(a) > 1000 and a == b
+    assert len(host.decode(a)) == 8 * 8
