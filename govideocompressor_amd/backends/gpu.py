@@ -288,57 +288,98 @@ class GpuBackend:
             keys.append(j.idx)
         return dict(zip(keys, self.decode_streams(streams, fps, keep_high_bit)))
 
+    def _decode_group(self, jobs: list[PieceJob], keep_high_bit: bool):
+        """Decode thread of :meth:`transcode`: one group of compressed pieces on the decode
+        stream; returns (idx -> DecodedSegment, completion event)."""
+        torch = self.torch
+        if getattr(self, "_dec_stream", None) is None:
+            self._dec_stream = torch.cuda.Stream(self.device)
+        with torch.cuda.stream(self._dec_stream):
+            dec = self._load_compressed(jobs, keep_high_bit)
+            ev = torch.cuda.Event()
+            ev.record(self._dec_stream)
+        return dec, ev
+
     def transcode(self, jobs: list[PieceJob], cfg: EncoderConfig) -> list[PieceResult]:
+        """Compressed pieces are decoded and encoded in groups of up to ``max_slots`` pieces, as
+        a two-stage pipeline (the layout of models/transcode.GpuTranscoder): the GPU decode of
+        group k+1 runs on its own stream, issued from a worker thread, while group k encodes
+        on the main stream -- the decode kernels fill the CUs the encoder's wavefront and
+        entropy stages leave idle.  Raw pieces load on the I/O pool and join the first group."""
         from ..segment.probe import kind_of
+        torch = self.torch
         tm = Timer()
         t0 = time.perf_counter()
         results: dict[str, PieceResult] = {}
-        items = []
         comp = [j for j in jobs if kind_of(j.in_path) in ("h264", "hevc", "mp4", "ts", "mkv")]
         raw = [j for j in jobs if j not in comp]
         futs = {j.idx: self._io.submit(load_clip, j.in_path) for j in raw}
+        # -pix_fmt yuv420p10le with libx265: Main 10 in, Main 10 out (no 8-bit detour)
+        keep = cfg.codec == "hevc" and cfg.bit_depth == 10
+        gsize = max(1, int(os.environ.get("MIVC_TRANSCODE_GROUP", self.max_slots)))
+        groups = [comp[i:i + gsize] for i in range(0, len(comp), gsize)] or [[]]
+        if getattr(self, "_dec_pool", None) is None:
+            self._dec_pool = cf.ThreadPoolExecutor(max_workers=1)
+        main = torch.cuda.current_stream(self.device)
         if comp:
-            try:
-                # -pix_fmt yuv420p10le with libx265: Main 10 in, Main 10 out (no 8-bit detour)
-                dec = self._load_compressed(comp, keep_high_bit=cfg.codec == "hevc" and cfg.bit_depth == 10)
-                items += [(j.idx, dec[j.idx]) for j in comp]
-            except Exception as e:  # noqa: BLE001 - reported to the coordinator
-                for j in comp:
-                    results[j.idx] = PieceResult(j.idx, False, f"decode: {e}")
-        for j in raw:
-            try:
-                items.append((j.idx, futs[j.idx].result()))
-            except Exception as e:  # noqa: BLE001 - reported to the coordinator
-                results[j.idx] = PieceResult(j.idx, False, f"load: {e}")
-        tm.add("load_s", time.perf_counter() - t0)
-        if items:
-            from ..rc import abr
-            rate_stats = None
-            paths = {j.idx: abr.stats_path_for(j.out_path, cfg.passlogfile) for j in jobs}
-            if cfg.two_pass == 1:
-                rate_stats = {}
-            elif cfg.two_pass == 2:
-                rate_stats = {}
-                for j in jobs:
-                    if os.path.exists(paths[j.idx]):
-                        rate_stats.update(abr.load_stats(paths[j.idx]))
+            if getattr(self, "_dec_stream", None) is None:
+                self._dec_stream = torch.cuda.Stream(self.device)
+            self._dec_stream.wait_stream(main)
+        nxt = self._dec_pool.submit(self._decode_group, groups[0], keep) if comp else None
+        from ..rc import abr
+        rate_stats = None
+        paths = {j.idx: abr.stats_path_for(j.out_path, cfg.passlogfile) for j in jobs}
+        if cfg.two_pass == 1:
+            rate_stats = {}
+        elif cfg.two_pass == 2:
+            rate_stats = {}
+            for j in jobs:
+                if os.path.exists(paths[j.idx]):
+                    rate_stats.update(abr.load_stats(paths[j.idx]))
+        for g, group in enumerate(groups):
+            items = []
+            tw = time.perf_counter()
+            if nxt is not None:
+                try:
+                    dec, ev = nxt.result()
+                    main.wait_event(ev)
+                    for d in dec.values():
+                        for x in (d.y, d.u, d.v):
+                            x.record_stream(main)
+                    items += [(j.idx, dec[j.idx]) for j in group]
+                except Exception as e:  # noqa: BLE001 - reported to the coordinator
+                    for j in group:
+                        results[j.idx] = PieceResult(j.idx, False, f"decode: {e}")
+                nxt = None
+            tm.add("decode_wait_s", time.perf_counter() - tw)
+            if g + 1 < len(groups):  # decode of the next group overlaps this group's encode
+                nxt = self._dec_pool.submit(self._decode_group, groups[g + 1], keep)
+            if g == 0:
+                for j in raw:
+                    try:
+                        items.append((j.idx, futs[j.idx].result()))
+                    except Exception as e:  # noqa: BLE001 - reported to the coordinator
+                        results[j.idx] = PieceResult(j.idx, False, f"load: {e}")
+                tm.add("load_s", time.perf_counter() - t0)
+            if not items:
+                continue
             try:
                 enc = self.encode_clips(items, cfg, tm, rate_stats=rate_stats)
-                if cfg.two_pass == 1:
-                    for j in jobs:
-                        if j.idx in rate_stats:
-                            abr.save_stats(paths[j.idx], {j.idx: rate_stats[j.idx]})
             except Exception as e:  # noqa: BLE001
                 for key, _ in items:
                     results[key] = PieceResult(key, False, f"encode: {e}")
                 enc = {}
+            del items
+            for key, (stream, st) in enc.items():
+                j = next(x for x in jobs if x.idx == key)
+                st["bytes"] = write_output(j, stream, st["fps"], cfg.codec, cfg.audio)
+                st["timings"] = dict(tm.t)
+                write_log(j, st)
+                results[key] = PieceResult(key, True, stats=st)
+        if cfg.two_pass == 1 and rate_stats is not None:
             for j in jobs:
-                if j.idx in enc:
-                    stream, st = enc[j.idx]
-                    st["bytes"] = write_output(j, stream, st["fps"], cfg.codec, cfg.audio)
-                    st["timings"] = dict(tm.t)
-                    write_log(j, st)
-                    results[j.idx] = PieceResult(j.idx, True, stats=st)
+                if j.idx in rate_stats:
+                    abr.save_stats(paths[j.idx], {j.idx: rate_stats[j.idx]})
         return [results[j.idx] for j in jobs]
 
     def _prepare_chunk(self, chunk, clips, w: int, h: int, tm: Timer):
@@ -402,3 +443,5 @@ class GpuBackend:
     def close(self):
         self._pool.close()
         self._io.shutdown(wait=False)
+        if getattr(self, "_dec_pool", None) is not None:
+            self._dec_pool.shutdown(wait=True)

@@ -72,3 +72,32 @@ def test_pipeline_encode_file_gpu(tmp_path, host):
     assert len(pics) == 40
     y = np.stack([p["i420"][: 320 * 240].reshape(240, 320) for p in pics])
     assert _psnr(y, c.y) > 27  # CRF 23 with AQ + MB-tree (x264 defaults)
+
+
+def test_gpu_backend_transcode_pipelined_groups(tmp_path, host, monkeypatch):
+    """Compressed pieces go through the two-stage pipeline of GpuBackend.transcode (decode of
+    group k+1 on its own stream while group k encodes): groups of 2 must give the same bytes
+    as one group holding every piece."""
+    from govideocompressor_amd.backends import PieceJob, get_backend
+    from govideocompressor_amd.utils import yuv
+
+    jobs = []
+    for i in range(5):
+        c = yuv.synth_clip_cpu(8, 176, 144, seed=20 + i)
+        y = tmp_path / f"{i}.y4m"
+        yuv.write_y4m(str(y), c)
+        jobs.append(PieceJob(str(i), str(y), str(tmp_path / f"{i}.264")))
+    be = get_backend("gpu")
+    for r in be.run(jobs, "-vcodec libx264 -qp 22"):
+        assert r.ok, r.reason
+    outs = {}
+    for g in ("2", "64"):
+        monkeypatch.setenv("MIVC_TRANSCODE_GROUP", g)
+        tj = [PieceJob(j.idx, j.out_path, str(tmp_path / f"t{g}_{j.idx}.264")) for j in jobs]
+        for r in be.run(tj, "-vcodec libx264 -crf 23"):
+            assert r.ok, r.reason
+        outs[g] = [open(j.out_path, "rb").read() for j in tj]
+    be.close()
+    assert outs["2"] == outs["64"]
+    for s in outs["2"]:
+        assert len(host.decode(s)) == 8

@@ -98,3 +98,13 @@ def test_gpu_transcoder_round_trip(host, src):
         ref = y[b].cpu().numpy().astype(np.float64)
         mse = np.mean((got - ref) ** 2)
         assert 10 * np.log10(255 ** 2 / max(mse, 1e-9)) > 30
+
+
+def test_gpu_hevc_decode_kat_streams(host):
+    """Streams of the independent known-answer writer (tests/hevc_kat.py): the CPU decoder
+    matches the clause formulas there (tests/test_hevc_kat.py); the GPU matches the CPU."""
+    from govideocompressor_amd.models.hevc_decode_gpu import GpuHevcDecoder
+    from hevc_kat import sample_streams
+    from test_hevc_kat import _content
+    streams = sample_streams(_content)
+    _check(host, streams, GpuHevcDecoder().decode(streams))
