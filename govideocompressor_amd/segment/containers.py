@@ -51,13 +51,16 @@ def _esds(asc: bytes, avg_bitrate: int = 0) -> bytes:
 
 
 def aac_track(asc: bytes, rate: int, channels: int, frames: list[bytes], pts0: float = 0.0) -> mp4.Track:
-    """Raw AAC frames (1024 samples each) -> an ``mp4a`` track; ``pts0`` (seconds, may be
-    negative) drops the frames before the video's first picture."""
+    """Raw AAC frames (1024 samples each) -> an ``mp4a`` track.  ``pts0``: the first frame's
+    time relative to the video's first picture, in seconds.  Negative: the frames before the
+    picture are dropped; positive: the track starts that much later (an empty edit, mp4.Track
+    negative ``media_time``), so the audio stays in sync."""
     entry = mp4._box(b"mp4a", bytes(6), struct.pack(">H", 1), bytes(8), struct.pack(">HHHH", channels, 16, 0, 0),
                      struct.pack(">I", rate << 16), _esds(asc))
     skip = int(round(-pts0 * rate / 1024.0)) if pts0 < 0 else 0
     frames = frames[skip:]
-    return mp4.Track(b"soun", rate, entry, list(frames), [1024] * len(frames))
+    delay = int(round(pts0 * rate)) if pts0 > 0.5 / rate else 0
+    return mp4.Track(b"soun", rate, entry, list(frames), [1024] * len(frames), media_time=-delay)
 
 
 def asc_of(profile: int, rate_idx: int, channels: int) -> bytes:
@@ -101,8 +104,8 @@ def is_ts(head: bytes) -> bool:
     return len(head) >= 189 and head[0] == 0x47 and head[188] == 0x47
 
 
-def _pes_payload(pes: bytes) -> tuple[bytes, float | None]:
-    """PES packet -> (payload, PTS in seconds or None)."""
+def _pes_payload(pes: bytes) -> tuple[bytes, int | None]:
+    """PES packet -> (payload, 33-bit PTS in 90 kHz ticks or None)."""
     if len(pes) < 9 or pes[:3] != b"\x00\x00\x01":
         raise ValueError("TS: PES without a start code prefix")
     sid = pes[3]
@@ -114,9 +117,72 @@ def _pes_payload(pes: bytes) -> tuple[bytes, float | None]:
     pts = None
     if flags & 0x80 and hlen >= 5:
         b = pes[9:14]
-        v = ((b[0] >> 1) & 7) << 30 | b[1] << 22 | (b[2] >> 1) << 15 | b[3] << 7 | b[4] >> 1
-        pts = v / 90000.0
+        pts = ((b[0] >> 1) & 7) << 30 | b[1] << 22 | (b[2] >> 1) << 15 | b[3] << 7 | b[4] >> 1
     return pes[9 + hlen:], pts
+
+
+PTS_WRAP = 1 << 33
+
+
+def unwrap_pts(ticks: list[int | None], anchor: int | None = None) -> list[int | None]:
+    """33-bit PTS values (one stream, decode order) made continuous across the wrap: each
+    value is moved by a multiple of 2^33 to the one nearest the previous value (the first
+    one: nearest ``anchor``, e.g. the video's first PTS, so streams stay comparable)."""
+    out: list[int | None] = []
+    prev = anchor
+    for v in ticks:
+        if v is None:
+            out.append(None)
+            continue
+        if prev is not None:
+            v += PTS_WRAP * round((prev - v) / PTS_WRAP)
+        out.append(v)
+        prev = v
+    return out
+
+
+def access_units(payload: bytes, codec: str) -> int:
+    """Pictures starting in a PES payload: H.264 slices with first_mb_in_slice 0 (the ue(v)
+    code '1'), HEVC VCL NAL units with first_slice_segment_in_pic_flag."""
+    n, i, end = 0, 0, len(payload)
+    while True:
+        i = payload.find(b"\x00\x00\x01", i)
+        if i < 0 or i + 5 > end:
+            return n
+        h = payload[i + 3]
+        if codec == "h264":
+            if (h & 0x1F) in (1, 5) and payload[i + 4] & 0x80:
+                n += 1
+        elif ((h >> 1) & 0x3F) < 32 and payload[i + 5] & 0x80:
+            n += 1
+        i += 3
+
+
+def per_picture_pts(pes: list[tuple[bytes, int | None]], codec: str) -> list[float]:
+    """One presentation time (seconds, unwrapped 90 kHz ticks / 90000) per picture, decode
+    order: a PES's PTS belongs to the first picture starting in it (ISO 13818-1 2.4.3.7);
+    pictures without one (later pictures of a multi-picture PES, PES packets without a PTS)
+    are interpolated from the previous picture at the stream's frame interval."""
+    ticks = unwrap_pts([t for _, t in pes])
+    per: list[float | None] = []
+    for (pl, _), t in zip(pes, ticks):
+        k = access_units(pl, codec)
+        if k == 0:
+            continue  # parameter sets / SEI / a continuation of the previous picture
+        per.append(None if t is None else t / 90000.0)
+        per += [None] * (k - 1)
+    # frame interval: the median of (time step / picture-count step) between known times
+    # (sorted by time: B-picture reordering makes decode-order steps negative)
+    known = sorted((x, i) for i, x in enumerate(per) if x is not None)
+    steps = [(b - a) / abs(j - i) for (a, i), (b, j) in zip(known, known[1:]) if b > a and j != i]
+    dt = sorted(steps)[len(steps) // 2] if steps else 1.0 / 30
+    out, last = [], None
+    for x in per:
+        if x is None:
+            x = (last + dt) if last is not None else 0.0
+        out.append(x)
+        last = x
+    return out
 
 
 def ts_demux(data: bytes) -> Demuxed:
@@ -205,10 +271,12 @@ def _ts_demux(data: bytes) -> Demuxed:
         raise ValueError("TS: no H.264 / HEVC video stream")
     vp = sorted(vpids)[0]
     vpes = pes.get(vp, [])
-    out = Demuxed(TS_VIDEO[streams[vp]], b"".join(pl for pl, _ in vpes))
-    vpts = [t for _, t in vpes if t is not None]
-    t0 = min(vpts) if vpts else 0.0
-    out.pts = [(t - t0) if t is not None else float("nan") for _, t in vpes]
+    codec = TS_VIDEO[streams[vp]]
+    out = Demuxed(codec, b"".join(pl for pl, _ in vpes))
+    first_tick = next((t for _, t in vpes if t is not None), None)
+    pics = per_picture_pts(vpes, codec)
+    t0 = min(pics) if pics else 0.0
+    out.pts = [t - t0 for t in pics]
     for pid, st in sorted(streams.items()):
         if pid == vp or st in TS_VIDEO:
             continue
@@ -219,7 +287,8 @@ def _ts_demux(data: bytes) -> Demuxed:
         if not apes:
             continue
         asc, rate, ch, frames = adts_frames(b"".join(pl for pl, _ in apes))
-        apts = next((t for _, t in apes if t is not None), t0)
+        at = unwrap_pts([next((t for _, t in apes if t is not None), None)], first_tick)[0]
+        apts = at / 90000.0 if at is not None else t0
         out.audio.append(aac_track(asc, rate, ch, frames, apts - t0))
     return out
 

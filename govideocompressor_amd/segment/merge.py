@@ -112,7 +112,13 @@ def merge_files(files: list[str], out_path: str, fps: float | None = None) -> in
         extra = []
         if any(audio):
             n = max(len(a) for a in audio)
-            extra = [mp4.concat([a[k] for a in audio if len(a) > k]) for k in range(n)]
+            # piece start times: an audio track that begins in a later piece keeps its delay
+            nfr = [h.hevc_stream_info(p)["frames"] if mp4_hevc.is_hevc_annexb(p) else h.stream_info(p)["frames"]
+                   for p in parts]
+            t_of = [sum(nfr[:i]) / (fps or 30.0) for i in range(len(parts))]
+            for k in range(n):
+                idx = [i for i, a in enumerate(audio) if len(a) > k]
+                extra.append(mp4.concat([audio[i][k] for i in idx], [t_of[i] for i in idx]))
         data = mp4.mux_video(stream, fps or 30.0, "hevc" if hevc else "h264", extra)
     else:
         data = stream

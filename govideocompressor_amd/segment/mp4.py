@@ -38,7 +38,9 @@ class Track:
     sync: list[bool] | None = None      # None: every sample is a sync sample
     width: int = 0
     height: int = 0
-    media_time: int = 0                 # first edit's media_time (media timescale), 0 = no edit list
+    # first edit's media_time (media timescale), 0 = no edit list; negative: the track starts
+    # that much after the movie (an empty edit of -media_time, then the media from 0)
+    media_time: int = 0
     language: int = 0x55C4              # 'und'
 
     @property
@@ -111,7 +113,7 @@ def is_mp4(data: bytes) -> bool:
 
 
 # ------------------------------------------------------------------------------- read
-def _read_trak(data: bytes, s: int, e: int) -> Track:
+def _read_trak(data: bytes, s: int, e: int, movie_ts: int = 1000) -> Track:
     tk = _need(data, s, e, b"tkhd")
     ver = data[tk[0]]
     wh = data[tk[1] - 8:tk[1]]
@@ -211,16 +213,19 @@ def _read_trak(data: bytes, s: int, e: int) -> Track:
             v = data[el[0]]
             ne = struct.unpack(">I", data[el[0] + 4:el[0] + 8])[0]
             p = el[0] + 8
+            empty = 0  # leading empty edits (media_time -1): a start delay, movie timescale
             for _ in range(ne):
                 if v == 1:
-                    _, mt = struct.unpack(">Qq", data[p:p + 16])
+                    sd, mt = struct.unpack(">Qq", data[p:p + 16])
                     p += 20
                 else:
-                    _, mt = struct.unpack(">Ii", data[p:p + 8])
+                    sd, mt = struct.unpack(">Ii", data[p:p + 8])
                     p += 12
-                if mt >= 0:  # skip empty edits (media_time -1)
-                    media_time = mt
-                    break
+                if mt < 0:
+                    empty += sd
+                    continue
+                media_time = mt - (empty * timescale + movie_ts // 2) // max(movie_ts, 1)
+                break
     del ver
     return Track(handler, timescale, entry, samples, durs, cts, sync, width >> 16, height >> 16, media_time, lang)
 
@@ -231,7 +236,11 @@ def read(data: bytes) -> list[Track]:
         mv = _child(data, 0, len(data), b"moov")
         if mv is None:
             raise ValueError("mp4: no moov box")
-        return [_read_trak(data, a, z) for k, a, z in children(data, mv[0], mv[1]) if k == b"trak"]
+        mts = 1000
+        mh = _child(data, mv[0], mv[1], b"mvhd")
+        if mh is not None:
+            mts = struct.unpack(">I", data[mh[0] + (20 if data[mh[0]] == 1 else 12):][:4])[0] or 1000
+        return [_read_trak(data, a, z, mts) for k, a, z in children(data, mv[0], mv[1]) if k == b"trak"]
     except (KeyError, struct.error, IndexError, OverflowError, MemoryError) as e:
         raise ValueError(f"mp4: malformed file ({type(e).__name__}: {e})") from None
 
@@ -314,11 +323,17 @@ def _trak(t: Track, track_id: int, chunks: list[tuple[int, int]], offs: list[int
         tkhd = _full(b"tkhd", 0, 3, struct.pack(">IIIII", 0, 0, track_id, 0, movie_dur), bytes(8),
                      struct.pack(">hhhH", 0, 0, vol, 0), _MATRIX, struct.pack(">II", t.width << 16, t.height << 16))
     boxes = [tkhd]
-    if t.media_time:
+    if t.media_time > 0:
         if v1:
             el = _full(b"elst", 1, 0, struct.pack(">IQqhh", 1, movie_dur, t.media_time, 1, 0))
         else:
             el = _full(b"elst", 0, 0, struct.pack(">IIihh", 1, movie_dur, t.media_time, 1, 0))
+        boxes.append(_box(b"edts", el))
+    elif t.media_time < 0:  # start delay: an empty edit, then the whole media
+        delay = (-t.media_time * movie_ts + t.timescale // 2) // t.timescale
+        media_movie = (media_dur * movie_ts + t.timescale - 1) // t.timescale
+        fmt = ">IQqhhQqhh" if v1 else ">IIihhIihh"
+        el = _full(b"elst", 1 if v1 else 0, 0, struct.pack(fmt, 2, delay, -1, 1, 0, media_movie, 0, 1, 0))
         boxes.append(_box(b"edts", el))
     return _box(b"trak", *boxes, mdia)
 
@@ -468,18 +483,36 @@ def cut(t: Track, t0: float, t1: float | None) -> Track:
     pts = t.pts_seconds()
     first = t0 <= 1e-9
     keep = [i for i, x in enumerate(pts) if (first or x >= t0 - 1e-9) and (t1 is None or x < t1 - 1e-9)]
+    mt = t.media_time if first else 0
+    if not first and keep and t.durations:
+        # a track that starts inside this piece (audio beginning after the video): keep the
+        # gap as a start delay instead of playing the samples from the piece's first instant
+        gap = pts[keep[0]] - t0
+        if gap * t.timescale > 2 * max(t.durations):
+            mt = -int(round(gap * t.timescale))
     return Track(t.handler, t.timescale, t.sample_entry, [t.samples[i] for i in keep], [t.durations[i] for i in keep],
                  [t.cts[i] for i in keep] if t.cts else None, [t.sync[i] for i in keep] if t.sync else None,
-                 t.width, t.height, t.media_time if first else 0, t.language)
+                 t.width, t.height, mt, t.language)
 
 
-def concat(parts: list[Track]) -> Track:
+def concat(parts: list[Track], starts: list[float] | None = None) -> Track:
     """Tracks appended in order (a merge's audio); every part needs the same sample entry.
-    The first part's edit (its priming samples' ``media_time``) is the result's."""
+    The first part's edit (its priming samples' ``media_time``) is the result's.  ``starts``
+    (seconds, one per part): where each part begins in the result -- when the first part
+    with samples is not the first part, or starts with a delay, the result starts late by
+    that much (audio beginning after the video)."""
+    if starts is not None and len(starts) != len(parts):
+        raise ValueError("mp4: one start time per part")
+    lead = next((i for i, p in enumerate(parts) if p.samples), None)
     parts = [p for p in parts if p.samples]
     if not parts:
         raise ValueError("mp4: no samples to concatenate")
     first = parts[0]
+    if starts is not None and starts[lead] > 0:
+        first = Track(first.handler, first.timescale, first.sample_entry, first.samples, first.durations, first.cts,
+                      first.sync, first.width, first.height,
+                      min(first.media_time, 0) - int(round(starts[lead] * first.timescale)), first.language)
+        parts[0] = first
     for p in parts[1:]:
         if p.sample_entry != first.sample_entry or p.timescale != first.timescale:
             raise ValueError("mp4: pieces carry different audio formats; cannot stream-copy them into one track")

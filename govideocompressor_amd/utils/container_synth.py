@@ -48,9 +48,12 @@ def _ts_time(prefix: int, v: int) -> bytes:
                   (v >> 7) & 0xFF, ((v & 0x7F) << 1) | 1])
 
 
-def _pes(stream_id: int, payload: bytes, pts: int, dts: int | None, bounded: bool) -> bytes:
-    hdr = _ts_time(3 if dts is not None else 2, pts) + (_ts_time(1, dts) if dts is not None else b"")
-    opt = bytes([0x80, 0xC0 if dts is not None else 0x80, len(hdr)]) + hdr
+def _pes(stream_id: int, payload: bytes, pts: int | None, dts: int | None, bounded: bool) -> bytes:
+    if pts is None:  # a PES without timestamps
+        opt = bytes([0x80, 0x00, 0])
+    else:
+        hdr = _ts_time(3 if dts is not None else 2, pts) + (_ts_time(1, dts) if dts is not None else b"")
+        opt = bytes([0x80, 0xC0 if dts is not None else 0x80, len(hdr)]) + hdr
     n = len(opt) + len(payload)
     return b"\x00\x00\x01" + bytes([stream_id]) + struct.pack(">H", n if bounded and n < 65536 else 0) + opt + payload
 
@@ -88,8 +91,14 @@ class _TsWriter:
 
 
 def write_ts(stream: bytes, fps: float = 25.0, audio: list[bytes] | None = None, rate: int = 48000,
-             channels: int = 2, base_s: float = 1.0) -> bytes:
-    """Annex-B video (+ raw AAC frames, 1024 samples each) -> an MPEG transport stream."""
+             channels: int = 2, base_s: float = 1.0, audio_delay_s: float = 0.0, pes_pictures: int = 1,
+             no_pts: tuple = ()) -> bytes:
+    """Annex-B video (+ raw AAC frames, 1024 samples each) -> an MPEG transport stream.
+
+    ``base_s``: the first PTS (values past 2^33 ticks wrap, as a long capture's do);
+    ``audio_delay_s``: the audio starts that much after the first picture;
+    ``pes_pictures``: pictures per video PES (only the first carries the PTS);
+    ``no_pts``: picture indexes whose PES is written without a PTS."""
     track, codec = video_track(stream, fps)
     w = _TsWriter()
     vpid, apid, pmt = 0x100, 0x101, 0x1000
@@ -109,10 +118,14 @@ def write_ts(stream: bytes, fps: float = 25.0, audio: list[bytes] | None = None,
     sfi = AAC_RATES.index(rate)
     ai = 0
     for k, s in enumerate(track.samples):
-        au = (params if k == 0 else b"") + _to_annexb(s)
-        p90 = base + int(round((pts[k] + delay) * 90000))
-        d90 = base + int(round(k / fps * 90000))
-        w.packets(vpid, _pes(0xE0, au, p90, d90 if d90 != p90 else None, bounded=False))
+        if k % pes_pictures == 0:
+            au = b"".join((params if j == 0 else b"") + _to_annexb(track.samples[j])
+                          for j in range(k, min(k + pes_pictures, len(track.samples))))
+            p90 = base + int(round((pts[k] + delay) * 90000))
+            d90 = base + int(round(k / fps * 90000))
+            if k in no_pts:
+                p90 = d90 = None
+            w.packets(vpid, _pes(0xE0, au, p90, d90 if d90 != p90 else None, bounded=False))
         # audio up to this picture's decode time, 4 frames per PES
         last = k + 1 == len(track.samples)
         while ai < len(aframes) and (last or ai * 1024 / rate <= (k + 1) / fps):
@@ -122,7 +135,7 @@ def write_ts(stream: bytes, fps: float = 25.0, audio: list[bytes] | None = None,
                 flen = len(fr) + 7
                 adts += bytes([0xFF, 0xF1, (1 << 6) | (sfi << 2) | (channels >> 2), ((channels & 3) << 6) | (flen >> 11),
                                (flen >> 3) & 0xFF, ((flen & 7) << 5) | 0x1F, 0xFC]) + fr
-            a90 = base + int(round((delay + ai * 1024 / rate) * 90000))
+            a90 = base + int(round((delay + audio_delay_s + ai * 1024 / rate) * 90000))
             w.packets(apid, _pes(0xC0, adts, a90, None, bounded=True))
             ai += len(chunk)
     return bytes(w.out)

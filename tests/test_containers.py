@@ -102,3 +102,54 @@ def test_split_ts_mkv_into_mp4_pieces_with_audio(tmp_path, host, ext):
     assert all(np.array_equal(a, b) for a, b in zip(got_frames, want))
     # audio: every AAC frame exactly once, in order (the last piece takes the tail)
     assert got_audio == frames
+
+
+def test_ts_audio_starting_after_the_video_keeps_its_delay(tmp_path, host):
+    """Audio whose first PTS is 0.5 s after the first picture: the demuxed track starts late
+    by 0.5 s (an empty edit), through split pieces and their merge."""
+    from govideocompressor_amd.segment import mp4
+    from govideocompressor_amd.segment.merge import merge_files
+    from govideocompressor_amd.segment.split import split
+    stream = _h264(host)
+    frames = _aac(40, seed=7)
+    ts = CS.write_ts(stream, 25.0, frames, audio_delay_s=0.5)
+    dm = C.ts_demux(ts)
+    a = dm.audio[0]
+    assert a.samples == frames and a.media_time == -24000
+    assert abs(a.pts_seconds()[0] - 0.5) < 1e-6
+    back = mp4.audio_tracks(mp4.read(mp4.mux_video(dm.annexb, 25.0, "h264", [a])))[0]
+    assert back.media_time == -24000 and abs(back.pts_seconds()[0] - 0.5) < 1e-3
+    # pieces of 4 pictures (0.16 s): the audio begins inside the fourth piece
+    src = tmp_path / "late.ts"
+    src.write_bytes(ts)
+    d, n = split(str(src), frames=4, out_root=str(tmp_path), log=lambda s: None)
+    assert n == 3
+    files = [str(tmp_path / d / f"{i}.mp4") for i in range(n)]
+    firsts = []
+    for f in files:
+        au = mp4.audio_tracks(mp4.read(open(f, "rb").read()))
+        firsts.append(au[0].pts_seconds()[0] if au else None)
+    assert firsts[0] is None and firsts[1] is None      # pictures 0..7 end at 0.32 s
+    assert abs(firsts[2] - (0.5 - 0.32)) < 1e-3          # the gap inside piece 2
+    merged = tmp_path / "m.mp4"
+    merge_files(files, str(merged), fps=25.0)
+    ma = mp4.audio_tracks(mp4.read(merged.read_bytes()))[0]
+    assert ma.samples == frames and abs(ma.pts_seconds()[0] - 0.5) < 2e-3
+
+
+def test_ts_pts_wrap_and_pes_without_pts(host):
+    """A capture crossing the 33-bit PTS wrap, two pictures per PES and a PES without a PTS:
+    one continuous presentation time per picture."""
+    stream = _h264(host)
+    frames = _aac(20, seed=8)
+    wrap_s = (1 << 33) / 90000.0
+    ts = CS.write_ts(stream, 25.0, frames, base_s=wrap_s - 0.2)
+    dm = C.ts_demux(ts)
+    assert len(dm.pts) == 12 and dm.pts[0] == 0.0 and abs(max(dm.pts) - 11 / 25.0) < 1e-3
+    assert dm.audio[0].media_time == 0
+    ts = CS.write_ts(stream, 25.0, frames, pes_pictures=2, no_pts=(4,))
+    dm = C.ts_demux(ts)
+    ref = C.ts_demux(CS.write_ts(stream, 25.0, frames))
+    assert len(dm.pts) == 12 and not any(np.isnan(dm.pts))
+    # P-only stream: decode order = display order, so interpolation recovers every time
+    assert np.allclose(dm.pts, ref.pts, atol=1e-3)
