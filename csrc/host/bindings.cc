@@ -65,6 +65,7 @@ EncoderConfig cfg_from(const py::dict& d) {
   c.refs = dget<int>(d, "refs", 1);
   c.weighted_bipred = dget<int>(d, "weighted_bipred", 0);
   c.weightp = dget<int>(d, "weightp", 0);
+  c.constrained_intra = dget<int>(d, "constrained_intra", 0);
   c.level_idc = dget<int>(d, "level_idc", 0);
   c.cqm = dget<int>(d, "cqm", 0);
   c.cqm_coded = dget<int>(d, "cqm_coded", 0xFF);

@@ -11,6 +11,7 @@ std::vector<uint8_t> cabac_slice_data(const SPS& sps, const PPS& pps, const Slic
                                       const int16_t* coef, int num_mbs, SliceStats* stats) {
   if (!pps.entropy_coding_mode) throw std::runtime_error("CABAC writer called with a CAVLC PPS");
   if (sh.cabac_init_idc != 0) throw std::runtime_error("CABAC writer codes cabac_init_idc 0 only");
+  if (pps.constrained_intra_pred) throw std::runtime_error("CABAC writer: constrained intra prediction is CAVLC-only");
   const int nmb = sps.width_mbs * sps.height_mbs;
   if (sh.first_mb < 0 || num_mbs <= 0 || sh.first_mb + num_mbs > nmb) throw std::runtime_error("bad MB range");
   for (int a = sh.first_mb; a < sh.first_mb + num_mbs; ++a) {

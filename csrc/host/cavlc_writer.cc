@@ -344,6 +344,9 @@ class SliceWriter {
     const MbCtx* A = nb_block(mx, my, &cur, bx - 1, by, &ra);
     const MbCtx* B = nb_block(mx, my, &cur, bx, by - 1, &rb);
     if (!A || !B) return 2;
+    // dcPredModePredictedFlag also when a neighbour is inter-coded under constrained intra
+    // prediction (8.3.1.1)
+    if (pps_.constrained_intra_pred && (!mbk_is_intra(A->kind) || !mbk_is_intra(B->kind))) return 2;
     int ma = (A->kind == MBK_I4x4 || A->kind == MBK_I8x8) ? A->i4[kRasterToBlk[ra]] : 2;
     int mb = (B->kind == MBK_I4x4 || B->kind == MBK_I8x8) ? B->i4[kRasterToBlk[rb]] : 2;
     return std::min(ma, mb);

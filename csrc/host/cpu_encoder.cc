@@ -73,6 +73,7 @@ PPS make_pps(const EncoderConfig& cfg) {
   p.num_ref_idx_l0_default = std::max(1, cfg.refs);
   p.weighted_bipred_idc = cfg.bframes > 0 ? cfg.weighted_bipred : 0;
   p.weighted_pred = cfg.weightp ? 1 : 0;
+  p.constrained_intra_pred = cfg.constrained_intra ? 1 : 0;
   p.chroma_qp_index_offset = cfg.chroma_qp_offset;
   p.second_chroma_qp_index_offset = cfg.chroma_qp_offset;
   p.deblocking_filter_control_present = 1;

@@ -37,6 +37,7 @@ struct EncoderConfig {
   int pyramid = 0;          // x264 --b-pyramid normal: some B pictures are references (reorder depth 2)
   int refs = 1;
   int weighted_bipred = 0;  // 2 = implicit weights (x264 --weightb)
+  int constrained_intra = 0;  // constrained_intra_pred_flag (writer / decoder tests)
   int weightp = 0;          // weighted_pred_flag: P slices carry pred_weight_table() (x264 --weightp)
   int level_idc = 0;        // > 0: written as level_idc (-level); must fit the size / rate
   // scaling matrices (High profile, t8x8): 0 flat; 1 the default matrices (x264 --cqm jvt: SPS

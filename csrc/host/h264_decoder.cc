@@ -772,15 +772,6 @@ struct Decoder::Impl {
     slices.push_back(spar);
     slice_idx = static_cast<int>(slices.size()) - 1;
     cur->nslices = static_cast<int>(slices.size());
-    if (p->constrained_intra_pred) cur->gpu_ok = false;
-    {  // non-flat scaling lists: the GPU reconstruction dequantises with flat weights only
-      bool flat = true;
-      for (int i = 0; i < 6; ++i)
-        for (int j = 0; j < 16; ++j) flat = flat && p->sl4[i][j] == 16;
-      for (int i = 0; i < 2 && p->transform_8x8_mode; ++i)
-        for (int j = 0; j < 64; ++j) flat = flat && p->sl8[i][j] == 16;
-      if (!flat) cur->gpu_ok = false;
-    }
     if (h.slice_type == SLICE_B) cur->slice_type = SLICE_B;
     else if (h.slice_type == SLICE_P && cur->slice_type == SLICE_I) cur->slice_type = SLICE_P;
     build_ref_lists();
@@ -1949,12 +1940,15 @@ struct Decoder::Impl {
       cur->qp[addr] = static_cast<int8_t>(qp);
       cur->qp_dbk[addr] = 0;
       for (int i = 0; i < 16; ++i) blk_done[i] = 1;
-      cur->gpu_ok = false;
       if (cabac) cab.init_engine();
       prev_qp_delta_nz = 0;
       if (parse_only) {
+        // the GPU copies the samples from the level pool: 24 chunks of 16 (luma raster, then
+        // Cb, Cr); QP 0 is the macroblock's deblocking QP (8.7.2.2, qPp of I_PCM)
         cur->rec_off[addr] = static_cast<uint32_t>(cur->rec_coef.size() / 16);
-        store_record(addr, MBK_IPCM, 0x2F, qp, 0, 0, nullptr, 0);
+        cur->rec_mask[addr] = 0;
+        cur->rec_coef.insert(cur->rec_coef.end(), pcm, pcm + 384);
+        store_record(addr, MBK_IPCM, 0x2F, 0, 0, 0, nullptr, 0);
       }
       return;
     }
@@ -2373,7 +2367,6 @@ struct Decoder::Impl {
       for (int cc = 0; cc < 2; ++cc)
         for (int b = 0; b < 4; ++b) put(18 + cc * 4 + b, s.cac[cc][b], 16, nullptr);
     cur->rec_mask[addr] = mask;
-    if (kind == MBK_IPCM) cur->gpu_ok = false;  // I_PCM samples are not carried by the records
     store_record(addr, kind, s.cbp, qp, s.i16_mode, s.chroma_mode, (kind == MBK_I4x4 || kind == MBK_I8x8) ? s.i4 : nullptr,
                  s.t8x8);
   }
@@ -2533,6 +2526,13 @@ struct Decoder::Impl {
       for (size_t i = 0; i < list[l].size() && i < 32; ++i) cur->list_ids[l * 32 + i] = list[l][i]->id;
     cur->wp.assign(kWpEntries, 0);
     int16_t* w = cur->wp.data();
+    // the picture's scaling lists (raster weights, 8.5.6) and constrained_intra_pred_flag ride
+    // in the same per-picture table
+    for (int i = 0; i < 6; ++i)
+      for (int j = 0; j < 16; ++j) w[kWpScale + i * 16 + j] = pp->sl4[i][j];
+    for (int i = 0; i < 2; ++i)
+      for (int j = 0; j < 64; ++j) w[kWpScale + 96 + i * 64 + j] = pp->sl8[i][j];
+    w[kWpFlags] = static_cast<int16_t>(pp->constrained_intra_pred ? 1 : 0);
     if (sh.has_weights) {
       w[0] = 1;
       w[1] = static_cast<int16_t>(sh.wt.luma_log2);

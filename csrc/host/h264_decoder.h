@@ -24,7 +24,11 @@ namespace h264 {
 // [2] chroma_log2_weight_denom, [kWpLw + l*32 + i] luma weight, [kWpLo + ...] luma offset,
 // [kWpCw + (l*32 + i)*2 + c] chroma weight, [kWpCo + ...] chroma offset,
 // [kWpImp + (i*8 + j)*2 + k] implicit weights w0/w1 of (refIdxL0 i, refIdxL1 j), i, j < 8.
-enum : int { kWpLw = 4, kWpLo = 68, kWpCw = 132, kWpCo = 260, kWpImp = 388, kWpEntries = 516 };
+// [kWpScale + list * 16 + raster] the PPS's 4x4 scaling lists (Intra Y/Cb/Cr, Inter Y/Cb/Cr),
+// [kWpScale + 96 + list * 64 + raster] its 8x8 lists (Intra Y, Inter Y),
+// [kWpFlags] bit 0: constrained_intra_pred_flag.
+enum : int { kWpLw = 4, kWpLo = 68, kWpCw = 132, kWpCo = 260, kWpImp = 388, kWpScale = 516, kWpFlags = 740,
+             kWpEntries = 742 };
 
 struct DecodedPicture {
   int width = 0, height = 0;          // cropped display size

@@ -54,7 +54,20 @@ struct DecodeArgs {
 };
 
 // weighted-prediction table layout (mirrors mivc::h264::kWp* in h264_decoder.h)
-enum : int { kWpLw = 4, kWpLo = 68, kWpCw = 132, kWpCo = 260, kWpImp = 388, kWpEntries = 516 };
+enum : int { kWpLw = 4, kWpLo = 68, kWpCw = 132, kWpCo = 260, kWpImp = 388, kWpScale = 516, kWpFlags = 740,
+             kWpEntries = 742 };
+
+// Scaling lists of a picture (8.5.6, raster weights; 16 everywhere when the stream sends
+// none): 4x4 list li = Intra Y / Cb / Cr, Inter Y / Cb / Cr (0..5), 8x8 list Intra / Inter Y.
+// A DPB launch without tables (wp null) dequantises with flat weights.
+struct Scaling {
+  const int16_t* t;  // [kWpScale ..] of the slot's table, or null
+  __device__ __forceinline__ int w4(int li, int x, int y) const { return t ? t[li * 16 + y * 4 + x] : 16; }
+  __device__ __forceinline__ int w8(int li, int x, int y) const { return t ? t[96 + li * 64 + y * 8 + x] : 16; }
+};
+__device__ __forceinline__ Scaling scaling_of(const DecodeArgs& a, int slot) {
+  return Scaling{a.wp ? a.wp + static_cast<size_t>(slot) * kWpEntries + kWpScale : nullptr};
+}
 
 // the picture being reconstructed (luma / chroma plane) of a slot
 __device__ __forceinline__ uint8_t* rec_plane(const DecodeArgs& a, uint8_t* base, int slot, size_t psize) {
@@ -73,10 +86,11 @@ __device__ __forceinline__ int level_at(const int16_t* coef, uint32_t mask, uint
   return coef[static_cast<size_t>(idx) * 16 + sp];
 }
 
-// dequantised AC/4x4 residual row gy of a block: v[x] = LevelScale * level << qp/6 (flat
-// weights; the >> 4 of 8.5.12.1 is folded into the table); skip_dc leaves (0, 0) at 0
+// dequantised AC/4x4 residual row gy of a block (8.5.12.1): LevelScale4x4 = weight *
+// normAdjust4x4; with the flat weight 16 this is level * normAdjust << qp/6.  skip_dc leaves
+// (0, 0) at 0; li = the block's 4x4 scaling list
 __device__ __forceinline__ void dequant_row(const int16_t* coef, uint32_t mask, uint32_t off, int bit, int gy, int qp,
-                                            bool skip_dc, int* v) {
+                                            bool skip_dc, int* v, const Scaling& sc, int li) {
   const int qm = qp % 6, qs = qp / 6;
   const int d0 = h264::kDequantV[qm][0], d1 = h264::kDequantV[qm][1], d2 = h264::kDequantV[qm][2];
   const bool have = (mask >> bit) & 1u;
@@ -84,20 +98,20 @@ __device__ __forceinline__ void dequant_row(const int16_t* coef, uint32_t mask, 
 #pragma unroll
   for (int x = 0; x < 4; ++x) {
     const int cls = pos_class(x, gy);
-    const int dq = cls == 0 ? d0 : (cls == 1 ? d1 : d2);
+    const int ls = sc.w4(li, x, gy) * (cls == 0 ? d0 : (cls == 1 ? d1 : d2));
     const int lv = (have && !(skip_dc && x == 0 && gy == 0)) ? c[zzinv(x, gy)] : 0;
-    v[x] = (lv * dq) << qs;
+    v[x] = qs >= 4 ? (lv * ls) << (qs - 4) : (lv * ls + (1 << (3 - qs))) >> (4 - qs);
   }
 }
 
 // chroma DC of block cb after the 2x2 inverse transform and scaling (8.5.11)
 __device__ __forceinline__ int chroma_dc_value(const int16_t* coef, uint32_t mask, uint32_t off, int comp, int cb,
-                                               int qpc) {
+                                               int qpc, int w00) {
   if (!((mask >> 17) & 1u)) return 0;
   const int16_t* c = coef + static_cast<size_t>(off + __builtin_popcount(mask & ((1u << 17) - 1u))) * 16 + comp * 4;
   const int c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3];
   const int f = cb == 0 ? c0 + c1 + c2 + c3 : (cb == 1 ? c0 - c1 + c2 - c3 : (cb == 2 ? c0 + c1 - c2 - c3 : c0 - c1 - c2 + c3));
-  const int ls = 16 * h264::kDequantV[qpc % 6][0];
+  const int ls = w00 * h264::kDequantV[qpc % 6][0];
   return ((f * ls) << (qpc / 6)) >> 5;
 }
 
@@ -113,8 +127,8 @@ __device__ __forceinline__ uint32_t pack4(const int* p) {
 // from a 9x9 LDS window per block, eighth-sample chroma MC, default / explicit / implicit
 // weighted sample prediction (8.4.2.3), and the 4x4 or 8x8 (8.5.13) inverse transform.
 
-// LevelScale8x8 with flat weights: 16 * normAdjust8x8 (8.5.9)
-__device__ __forceinline__ int level_scale8(int m, int x, int y) {
+// LevelScale8x8 = weight * normAdjust8x8 (8.5.9)
+__device__ __forceinline__ int level_scale8(int m, int x, int y, int w) {
   int k;
   if ((x & 3) == 0 && (y & 3) == 0) k = 0;
   else if ((x & 1) && (y & 1)) k = 1;
@@ -124,7 +138,7 @@ __device__ __forceinline__ int level_scale8(int m, int x, int y) {
   else k = 5;
   constexpr int t[6][6] = {{20, 18, 32, 19, 25, 24}, {22, 19, 35, 21, 28, 26}, {26, 23, 42, 24, 33, 31},
                            {28, 25, 45, 26, 35, 33}, {32, 28, 51, 30, 40, 38}, {36, 32, 58, 34, 46, 43}};
-  return 16 * t[m][k];
+  return w * t[m][k];
 }
 
 // one 8-point pass of the 8x8 inverse transform (8.5.13.2), in place, stride s
@@ -189,6 +203,7 @@ __global__ __launch_bounds__(64) void decode_inter_dpb(DecodeArgs a) {
     se = a.sub + static_cast<size_t>(si) * h264::kSubEntry;
   }
   const int16_t* wt = a.wp + static_cast<size_t>(slot) * kWpEntries;
+  const Scaling sc = scaling_of(a, slot);
   auto quad = [](int rb) { return ((rb & 3) >> 1) + 2 * (rb >> 3); };
   auto mv_of = [&](int l, int rb, int c) {
     return static_cast<int>(sub4 ? se[(l * 16 + rb) * 2 + c] : H->mv[l][quad(rb)][c]);
@@ -227,7 +242,7 @@ __global__ __launch_bounds__(64) void decode_inter_dpb(DecodeArgs a) {
       const int pos = h264::kZigzag8x8[i];
       const int x = pos & 7, y = pos >> 3;
       const int lv = level_at(a.coef, mask, off, b8 * 4 + (i >> 4), i & 15);
-      const int ls = level_scale8(qp % 6, x, y);
+      const int ls = level_scale8(qp % 6, x, y, sc.w8(1, x, y));
       d8[b8][pos] = qp >= 36 ? (lv * ls) << (qp / 6 - 6) : (lv * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
     }
   }
@@ -264,7 +279,7 @@ __global__ __launch_bounds__(64) void decode_inter_dpb(DecodeArgs a) {
         v[x] = (d8[(Y >> 3) * 2 + (X >> 3)][(Y & 7) * 8 + (X & 7)] + 32) >> 6;
       }
     } else {
-      dequant_row(a.coef, mask, off, blk, gy, qp, false, v);
+      dequant_row(a.coef, mask, off, blk, gy, qp, false, v, sc, 3);
       grp_inv4x4(v, lane & ~3, gy);
     }
 #pragma unroll
@@ -305,8 +320,8 @@ __global__ __launch_bounds__(64) void decode_inter_dpb(DecodeArgs a) {
       }
       pr[x] = weigh(wt, true, comp, r0, r1, pc[0], pc[1]);
     }
-    dequant_row(a.coef, mask, off, 18 + comp * 4 + cb, gy, qpc, true, v);
-    if (gy == 0) v[0] = chroma_dc_value(a.coef, mask, off, comp, cb, qpc);
+    dequant_row(a.coef, mask, off, 18 + comp * 4 + cb, gy, qpc, true, v, sc, 4 + comp);
+    if (gy == 0) v[0] = chroma_dc_value(a.coef, mask, off, comp, cb, qpc, sc.w4(4 + comp, 0, 0));
     grp_inv4x4(v, lane & ~3, gy);
 #pragma unroll
     for (int x = 0; x < 4; ++x) pr[x] = h264::clip1(pr[x] + v[x]);
@@ -377,12 +392,44 @@ __device__ __forceinline__ void decode_intra_mb(const DecodeArgs& a, DecIntraSha
   // neighbour MBs are available when inside the picture and in this MB's slice (the
   // parser's records carry the slice index in pad0; 6.4.8)
   const int sl = __builtin_amdgcn_readfirstlane(H->pad0);
-  auto same = [&](int dx, int dy) { return static_cast<int>(H[dy * g.wmb + dx].pad0) == sl; };
+  const Scaling sc = scaling_of(a, slot);
+  // constrained_intra_pred_flag: inter neighbours are not available for intra prediction
+  const bool cip = a.wp && (a.wp[static_cast<size_t>(slot) * kWpEntries + kWpFlags] & 1);
+  auto same = [&](int dx, int dy) {
+    const MbHeader& n = H[dy * g.wmb + dx];
+    return static_cast<int>(n.pad0) == sl && (!cip || h264::mbk_is_intra(n.kind));
+  };
   int mbav = 0;
   if (mx > 0 && same(-1, 0)) mbav |= h264::AV_LEFT;
   if (my > 0 && same(0, -1)) mbav |= h264::AV_TOP;
   if (mx > 0 && my > 0 && same(-1, -1)) mbav |= h264::AV_TOPLEFT;
   if (my > 0 && mx < g.wmb - 1 && same(1, -1)) mbav |= h264::AV_TOPRIGHT;
+
+  if (kind == h264::MBK_IPCM) {
+    // I_PCM: the samples ride in the level pool (24 chunks: luma raster, Cb, Cr)
+    const int16_t* pcm = a.coef + static_cast<size_t>(off) * 16;
+    {
+      const int y = lane >> 2, x4 = (lane & 3) * 4;
+      uint32_t word = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) word |= static_cast<uint32_t>(pcm[y * 16 + x4 + k] & 0xFF) << (8 * k);
+      *reinterpret_cast<uint32_t*>(recy + static_cast<size_t>(Y0 + y) * W + X0 + x4) = word;
+      if ((lane & 3) == 3) S.saved_y[y] = static_cast<uint8_t>(word >> 24);
+    }
+    if (lane < 32) {
+      const int comp = lane >> 4, y = (lane >> 1) & 7, x4 = (lane & 1) * 4;
+      uint32_t word = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) word |= static_cast<uint32_t>(pcm[256 + comp * 64 + y * 8 + x4 + k] & 0xFF) << (8 * k);
+      uint8_t* recc = rec_plane(a, comp == 0 ? a.rec_u : a.rec_v, slot, g.csize());
+      *reinterpret_cast<uint32_t*>(recc + static_cast<size_t>(my * 8 + y) * cw + mx * 8 + x4) = word;
+      if (lane & 1) S.saved_c[comp][y] = static_cast<uint8_t>(word >> 24);
+    }
+    if (lane < 16) a.nz[o * 16 + blk_x(lane) + 4 * blk_y(lane)] = 1;
+    if (lane == 0) S.saved_x = mx;
+    wave_sync();
+    return;
+  }
 
   // ---- stage the reconstructed neighbourhood
   if (lane < 21) {  // tile row 0: x = X0-1 .. X0+19
@@ -427,7 +474,7 @@ __device__ __forceinline__ void decode_intra_mb(const DecodeArgs& a, DecIntraSha
 #pragma unroll
       for (int i = 0; i < 16; ++i) d[h264::kZigzag4x4[i]] = level_at(a.coef, mask, off, 16, i);
       h264::hadamard4x4(d);
-      const int ls = 16 * h264::kDequantV[qp % 6][0];
+      const int ls = sc.w4(0, 0, 0) * h264::kDequantV[qp % 6][0];
 #pragma unroll
       for (int r = 0; r < 16; ++r)
         S.lv16dc[r] = qp >= 36 ? (d[r] * ls) << (qp / 6 - 6) : (d[r] * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
@@ -442,7 +489,7 @@ __device__ __forceinline__ void decode_intra_mb(const DecodeArgs& a, DecIntraSha
     if (mode16 == 3) h264::i16_plane_params(top, left, static_cast<int>(S.tile[0]), &pa, &pb, &pc);
     const int dc = mode16 == 2 ? h264::i16_dc(top, left, mbav) : 0;
     int v[4], pr[4];
-    dequant_row(a.coef, mask, off, blk, gy, qp, true, v);
+    dequant_row(a.coef, mask, off, blk, gy, qp, true, v, sc, 0);
     wave_sync();
     if (gy == 0) v[0] = S.lv16dc[bx + 4 * by];
     grp_inv4x4(v, lane & ~3, gy);
@@ -470,7 +517,7 @@ __device__ __forceinline__ void decode_intra_mb(const DecodeArgs& a, DecIntraSha
         const int pos = h264::kZigzag8x8[i];
         const int x = pos & 7, y = pos >> 3;
         const int lv = level_at(a.coef, mask, off, b8 * 4 + (i >> 4), i & 15);
-        const int ls = level_scale8(qp % 6, x, y);
+        const int ls = level_scale8(qp % 6, x, y, sc.w8(0, x, y));
         S.r8[(oy + y) * 16 + ox + x] = qp >= 36 ? (lv * ls) << (qp / 6 - 6) : (lv * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
       }
       wave_sync();
@@ -544,7 +591,7 @@ __device__ __forceinline__ void decode_intra_mb(const DecodeArgs& a, DecIntraSha
     // Intra4x4: all 16 residual blocks at once, then the 16 predictions in order
     {
       int v[4];
-      dequant_row(a.coef, mask, off, blk, gy, qp, false, v);
+      dequant_row(a.coef, mask, off, blk, gy, qp, false, v, sc, 0);
       grp_inv4x4(v, lane & ~3, gy);
 #pragma unroll
       for (int x = 0; x < 4; ++x) S.res[blk][gy * 4 + x] = static_cast<int16_t>(v[x]);
@@ -592,8 +639,8 @@ __device__ __forceinline__ void decode_intra_mb(const DecodeArgs& a, DecIntraSha
     int pa = 0, pb = 0, pc = 0;
     if (cmode == 3) h264::chroma_plane_params(S.ctop[comp] + 1, S.cleft[comp], static_cast<int>(S.ctop[comp][0]), &pa, &pb, &pc);
     int v[4], pr[4];
-    dequant_row(a.coef, mask, off, 18 + comp * 4 + cb, gy, qpc, true, v);
-    if (gy == 0) v[0] = chroma_dc_value(a.coef, mask, off, comp, cb, qpc);
+    dequant_row(a.coef, mask, off, 18 + comp * 4 + cb, gy, qpc, true, v, sc, 1 + comp);
+    if (gy == 0) v[0] = chroma_dc_value(a.coef, mask, off, comp, cb, qpc, sc.w4(1 + comp, 0, 0));
     grp_inv4x4(v, lane & ~3, gy);
     const int Yc = cby + gy;
 #pragma unroll

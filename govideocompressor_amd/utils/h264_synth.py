@@ -16,7 +16,7 @@ from .. import ops  # noqa: F401  (package import order)
 # MbHeader byte offsets (csrc/common/h264_mb.h)
 _KIND, _CBP, _QP, _I16, _CHROMA, _FLAGS, _REF, _MV, _I4 = 0, 1, 2, 3, 4, 5, 8, 16, 48
 HDR_BYTES = 64
-I4x4, I16x16, P16x16, PSKIP, P16x8, P8x16, P8x8, I8x8 = 0, 1, 2, 3, 5, 6, 7, 8
+I4x4, I16x16, P16x16, PSKIP, IPCM, P16x8, P8x16, P8x8, I8x8 = 0, 1, 2, 3, 4, 5, 6, 7, 8
 MBF_T8x8 = 2
 _ZZ8 = [0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6, 7, 14,
         21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53,
@@ -79,7 +79,26 @@ def _levels(rng, n: int, density: float, start: int = 0) -> np.ndarray:
     return v
 
 
-def _intra_record(rng, h, c, mx, my, qp, density, allow_i4=True, t8x8=False):
+def _intra_record(rng, h, c, mx, my, qp, density, allow_i4=True, t8x8=False, dc_only=False, pcm=0.0):
+    if pcm and rng.random() < pcm:
+        h[_KIND] = IPCM
+        c[:384] = rng.integers(0, 256, 384)
+        h[_QP] = qp
+        return
+    if dc_only:  # constrained intra in P pictures: DC modes are legal with any availability
+        h[_KIND] = I4x4 if rng.random() < 0.5 else I16x16
+        h[_I16] = 2
+        h[_I4:_I4 + 16] = 2
+        for b in range(16):
+            c[b * 16:(b + 1) * 16] = _levels(rng, 16, density, start=int(h[_KIND] == I16x16))
+        if h[_KIND] == I16x16:
+            c[256:272] = _levels(rng, 16, density * 2)
+        h[_CHROMA] = 0
+        h[_QP] = qp
+        c[272:280] = _levels(rng, 8, density)
+        for b in range(8):
+            c[280 + b * 16:280 + (b + 1) * 16] = _levels(rng, 16, density / 2, start=1)
+        return
     if t8x8 and rng.random() < 0.35:
         h[_KIND] = I8x8
         modes = _i8_modes_ok(rng, mx, my)
@@ -108,15 +127,20 @@ def _intra_record(rng, h, c, mx, my, qp, density, allow_i4=True, t8x8=False):
 def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp: int = 28,
                   density: float = 0.15, intra_in_p: float = 0.1, mv_range: int = 48, keyint: int = 0,
                   cabac: bool = False, t8x8: bool = False, records: list | None = None, refs: int = 1,
-                  slice_rows: int = 0) -> bytes:
+                  slice_rows: int = 0, pcm: float = 0.0, constrained_intra: bool = False,
+                  cqm: dict | None = None) -> bytes:
     """Annex-B stream of ``frames`` pictures (IDR + P) from random decision records.
 
     cabac / t8x8 select the entropy coder and the High-profile 8x8 transform (I8x8 MBs and
     8x8-transformed inter MBs).  ``records``, if given, receives (hdr, coef) per picture.
     ``slice_rows`` > 0: every picture is coded as several slices of that many MB rows (intra
-    modes then treat each slice's first row as having no row above)."""
+    modes then treat each slice's first row as having no row above).  ``pcm``: share of I_PCM
+    macroblocks (CAVLC); ``constrained_intra``: constrained_intra_pred_flag (CAVLC; intra MBs of
+    P pictures use DC modes); ``cqm``: scaling-matrix keys of the writer config (cqm, cqm4,
+    cqm8, cqm_coded; needs t8x8)."""
     rng = np.random.default_rng(seed)
-    cfg = dict(width=width, height=height, qp=qp, cabac=int(cabac), t8x8=int(t8x8), refs=int(refs))
+    cfg = dict(width=width, height=height, qp=qp, cabac=int(cabac), t8x8=int(t8x8), refs=int(refs),
+               constrained_intra=int(constrained_intra), **(cqm or {}))
     wmb, hmb = (width + 15) // 16, (height + 15) // 16
     nmb = wmb * hmb
     out = [host.parameter_sets(cfg)]
@@ -139,7 +163,8 @@ def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp:
             mqp = int(np.clip(sqp + rng.integers(-3, 4), 0, 51))
             if idr or rng.random() < intra_in_p:
                 r0 = (my // slice_rows) * slice_rows if slice_rows else 0
-                _intra_record(rng, h, c, mx, my - r0, mqp, density, t8x8=t8x8)
+                _intra_record(rng, h, c, mx, my - r0, mqp, density, t8x8=t8x8, dc_only=constrained_intra and not idr,
+                              pcm=pcm)
                 continue
             r = rng.random()
             kind = PSKIP if r < 0.25 else (P16x16 if r < 0.5 else (P16x8 if r < 0.65 else (P8x16 if r < 0.8 else P8x8)))

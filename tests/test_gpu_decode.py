@@ -119,3 +119,19 @@ def test_gpu_decode_multi_slice_pictures(host, dec):
                random_stream(host, 112, 80, 4, seed=62, slice_rows=1, cabac=True, t8x8=True, intra_in_p=0.4),
                random_stream(host, 96, 64, 3, seed=63, slice_rows=3, cabac=True)]
     _check(host, dec, streams)
+
+
+def test_gpu_decode_pcm_constrained_intra_scaling_lists(host, dec):
+    """Coding tools that used to drop a segment to the CPU decoder now reconstruct on the GPU:
+    I_PCM macroblocks (samples through the level pool, deblocking QP 0), constrained intra
+    prediction (inter neighbours unavailable to intra MBs of P pictures), and scaling matrices
+    (SPS lists; PPS lists with fall-back rule B; CAVLC and CABAC; 4x4 and 8x8)."""
+    rng = np.random.default_rng(5)
+    cqm4 = rng.integers(6, 60, (6, 16)).astype(np.uint8)
+    cqm8 = rng.integers(6, 60, (2, 64)).astype(np.uint8)
+    streams = [random_stream(host, 96, 64, 5, seed=31, pcm=0.25, intra_in_p=0.3),
+               random_stream(host, 96, 64, 5, seed=32, constrained_intra=True, intra_in_p=0.4, density=0.3),
+               random_stream(host, 96, 64, 5, seed=33, t8x8=True, cqm=dict(cqm=1, cqm4=cqm4, cqm8=cqm8), density=0.3),
+               random_stream(host, 96, 64, 5, seed=34, t8x8=True, cabac=True, intra_in_p=0.3,
+                             cqm=dict(cqm=3, cqm4=cqm4, cqm8=cqm8, cqm_coded=0x5A), density=0.3)]
+    _check(host, dec, streams)

@@ -246,3 +246,22 @@ def test_gpu_hevc_ctu64(host, ctu64, wpp):
     _compare(host, res, rec)
     res, rec = _encode(96, 64, 2, 2, intra_only=True, crf=None, qp=27, ctu64=ctu64, wpp=wpp)
     _compare(host, res, rec)
+
+
+@pytest.mark.parametrize("ctu64", [False, True])
+def test_gpu_hevc_1080p_matches_decoder(host, ctu64):
+    """Full-HD pictures: a 1080p-only fault (a non-inlined recon call site faulted at 1920x1080
+    and never at the small test sizes) must show up here.  CTU 32 and 64 (x265 --ctu),
+    2 slots x 4 pictures with the default GOP (B + P), bit-exact with the CPU decoder; then the
+    GPU decoder reproduces the same pictures from the bitstreams."""
+    from govideocompressor_amd.models.hevc_decode_gpu import GpuHevcDecoder
+    res, rec = _encode(1920, 1080, 4, 2, crf=26, ctu64=ctu64)
+    _compare(host, res, rec)
+    dec = GpuHevcDecoder().decode([r.bitstream for r in res])
+    for b, (r, d) in enumerate(zip(res, dec)):
+        pics = sorted((p for p in host.hevc_decode_full(r.bitstream, True, False) if p["display"] >= 0),
+                      key=lambda p: p["display"])
+        assert d.frames == len(pics) == r.frames
+        for t, p in enumerate(pics):
+            assert np.array_equal(d.y[t].cpu().numpy().astype(np.uint16), p["y"][:1080]), (b, t)
+            assert np.array_equal(d.v[t].cpu().numpy().astype(np.uint16), p["v"][:540]), (b, t)
