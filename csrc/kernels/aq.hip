@@ -117,11 +117,16 @@ __global__ __launch_bounds__(256) void h264_qp_flags(Geom g, const MbHeader* __r
   if (live && sub == 0) flags[o] = ((bal >> (16 * grp)) & 0xFFFFu) != 0 ? 1 : 0;
 }
 
-// One workgroup per slot: chunked segmented scan of "last MB with mb_qp_delta".
+// One workgroup per slice (slot-major, `per_slot` slices of `slice_mbs` MBs each): chunked
+// segmented scan of "last MB with mb_qp_delta"; QP_pred starts from the slice QP at every
+// slice's first MB (7.4.5).
 __global__ __launch_bounds__(1024) void h264_qp_fixup(Geom g, MbHeader* __restrict__ hdr,
-                                                      const uint8_t* __restrict__ flags, const int* __restrict__ slice_qp) {
-  const int slot = blockIdx.x, n = g.nmb();
-  const size_t base = static_cast<size_t>(slot) * n;
+                                                      const uint8_t* __restrict__ flags, const int* __restrict__ slice_qp,
+                                                      int slice_mbs, int per_slot) {
+  const int slot = blockIdx.x / per_slot, sl = blockIdx.x - slot * per_slot;
+  const int first = sl * slice_mbs;
+  const int n = min(g.nmb() - first, slice_mbs);
+  const size_t base = static_cast<size_t>(slot) * g.nmb() + first;
   __shared__ int s_last[1024];
   const int per = (n + blockDim.x - 1) / blockDim.x;
   const int i0 = threadIdx.x * per, i1 = min(n, i0 + per);
@@ -161,11 +166,13 @@ extern "C" void mivc_launch_aq_offsets(int B, int wmb, int hmb, const uint8_t* s
 }
 
 extern "C" void mivc_launch_qp_fixup(int B, int wmb, int hmb, void* hdr, const int16_t* coef, const uint8_t* nz,
-                                     uint8_t* flags, const int* slice_qp, void* stream) {
+                                     uint8_t* flags, const int* slice_qp, void* stream, int slice_rows) {
   const Geom g{B, wmb, hmb, wmb * 16, hmb * 16};
   hipStream_t s = static_cast<hipStream_t>(stream);
+  const int rows = (slice_rows > 0 && slice_rows < hmb) ? slice_rows : hmb;
+  const int per_slot = (hmb + rows - 1) / rows;
   hipLaunchKernelGGL(h264_qp_flags, dim3((wmb * hmb + 15) / 16, B), dim3(256), 0, s, g,
                      static_cast<const mivc::h264::MbHeader*>(hdr), coef, nz, flags);
-  hipLaunchKernelGGL(h264_qp_fixup, dim3(B), dim3(1024), 0, s, g, static_cast<mivc::h264::MbHeader*>(hdr), flags,
-                     slice_qp);
+  hipLaunchKernelGGL(h264_qp_fixup, dim3(B * per_slot), dim3(1024), 0, s, g, static_cast<mivc::h264::MbHeader*>(hdr),
+                     flags, slice_qp, rows * wmb, per_slot);
 }

@@ -58,7 +58,7 @@ void mivc_launch_aq_offsets(int B, int wmb, int hmb, const uint8_t* sy, const ui
 void mivc_launch_mbtree(int B, int F, int lbw, int lbh, const int* blk_cost, const int* blk_mv, void* prop,
                         float strength, float* out, void* stream);
 void mivc_launch_qp_fixup(int B, int wmb, int hmb, void* hdr, const int16_t* coef, const uint8_t* nz, uint8_t* flags,
-                          const int* slice_qp, void* stream);
+                          const int* slice_qp, void* stream, int slice_rows);
 void mivc_launch_me_halfpel(int B, int W, int H, const uint8_t* ref_y, uint8_t* hp, void* stream, const void* route,
                             int nbuf);
 void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* src_u,
@@ -80,7 +80,8 @@ void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t* src_y, con
                               const uint8_t* src_v, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const int* qp,
                               int chroma_qp_offset, void* hdr, int16_t* coef, uint8_t* nz,
                               const uint8_t* intra_flag, const int* intra_count, int* err, int use_i4x4,
-                              const int8_t* aq, void* stream, int use_i8x8, const void* route, int nbuf);
+                              const int8_t* aq, void* stream, int use_i8x8, const void* route, int nbuf,
+                              int slice_rows);
 void mivc_launch_deblock(int B, int wmb, int hmb, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const void* hdr,
                          const uint8_t* nz, int chroma_qp_offset, int alpha_off, int beta_off, int* err,
                          void* stream, const void* route, int nbuf);
@@ -133,7 +134,8 @@ int mivc_cabac_gap();
 void mivc_launch_cabac_bin(int B, int wmb, int hmb, const void* hdr, const int16_t* coef, uint32_t* mask, void* nb,
                            int* cnt, long long* off, int* tot, uint16_t* pool, long long pool_cap,
                            long long* pool_used, long long* base, int* total, const int* slot_qp, int slice_type,
-                           int num_ref_l0, int num_ref_l1, int t8x8_mode, int* err, void* stream, const void* route);
+                           int num_ref_l0, int num_ref_l1, int t8x8_mode, int* err, void* stream, const void* route,
+                           int slice_rows);
 void mivc_launch_cabac_code(int L, int B, uint16_t* pool, const long long* base, const int* total,
                             const uint32_t* hdr_bits, const int* hdr_nbits, const int* slot_qp,
                             unsigned long long itypes, int* bytes, uint8_t* out, long long* out_off, int* err,
@@ -325,10 +327,11 @@ PYBIND11_MODULE(_hip, m) {
                        S(stream));
   });
   m.def("qp_fixup", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t coef, uintptr_t nz, uintptr_t flags,
-                       uintptr_t slice_qp, uintptr_t stream) {
+                       uintptr_t slice_qp, uintptr_t stream, int slice_rows) {
     mivc_launch_qp_fixup(B, wmb, hmb, P<void>(hdr), P<int16_t>(coef), P<uint8_t>(nz), P<uint8_t>(flags),
-                         P<int>(slice_qp), S(stream));
-  });
+                         P<int>(slice_qp), S(stream), slice_rows);
+  }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("hdr"), py::arg("coef"), py::arg("nz"), py::arg("flags"),
+     py::arg("slice_qp"), py::arg("stream"), py::arg("slice_rows") = 0);
   m.def("me_halfpel", [](int B, int W, int H, uintptr_t ref, uintptr_t hp, uintptr_t stream, uintptr_t route, int nbuf) {
     if (route && nbuf < 1) throw std::invalid_argument("me_halfpel: a routed launch needs the pool size");
     mivc_launch_me_halfpel(B, W, H, P<uint8_t>(ref), P<uint8_t>(hp), S(stream), P<void>(route), nbuf);
@@ -395,15 +398,15 @@ PYBIND11_MODULE(_hip, m) {
   m.def("encode_intra", [](int B, int wmb, int hmb, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t ry,
                            uintptr_t ru, uintptr_t rv, uintptr_t qp, int cqo, uintptr_t hdr, uintptr_t coef,
                            uintptr_t nz, uintptr_t intra_flag, uintptr_t intra_count, uintptr_t err, int use_i4x4,
-                           uintptr_t stream, uintptr_t aq, int use_i8x8, uintptr_t route, int nbuf) {
+                           uintptr_t stream, uintptr_t aq, int use_i8x8, uintptr_t route, int nbuf, int slice_rows) {
     mivc_launch_encode_intra(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), P<uint8_t>(ry),
                              P<uint8_t>(ru), P<uint8_t>(rv), P<int>(qp), cqo, P<void>(hdr), P<int16_t>(coef),
                              P<uint8_t>(nz), P<uint8_t>(intra_flag), P<int>(intra_count), P<int>(err), use_i4x4,
-                             P<int8_t>(aq), S(stream), use_i8x8, P<void>(route), nbuf);
+                             P<int8_t>(aq), S(stream), use_i8x8, P<void>(route), nbuf, slice_rows);
   }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("sy"), py::arg("su"), py::arg("sv"), py::arg("ry"),
      py::arg("ru"), py::arg("rv"), py::arg("qp"), py::arg("cqo"), py::arg("hdr"), py::arg("coef"), py::arg("nz"),
      py::arg("intra_flag"), py::arg("intra_count"), py::arg("err"), py::arg("use_i4x4"), py::arg("stream"),
-     py::arg("aq") = 0, py::arg("use_i8x8") = 0, py::arg("route") = 0, py::arg("nbuf") = 0);
+     py::arg("aq") = 0, py::arg("use_i8x8") = 0, py::arg("route") = 0, py::arg("nbuf") = 0, py::arg("slice_rows") = 0);
   m.def("deblock", [](int B, int wmb, int hmb, uintptr_t ry, uintptr_t ru, uintptr_t rv, uintptr_t hdr, uintptr_t nz,
                       int cqo, int alpha_off, int beta_off, uintptr_t err, uintptr_t stream, uintptr_t route, int nbuf) {
     mivc_launch_deblock(B, wmb, hmb, P<uint8_t>(ry), P<uint8_t>(ru), P<uint8_t>(rv), P<void>(hdr), P<uint8_t>(nz),
@@ -624,17 +627,19 @@ PYBIND11_MODULE(_hip, m) {
   m.def("cabac_bin", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t coef, uintptr_t mask, uintptr_t nb,
                         uintptr_t cnt, uintptr_t off, uintptr_t tot, uintptr_t pool, long long pool_cap,
                         uintptr_t pool_used, uintptr_t base, uintptr_t total, uintptr_t slot_qp, int slice_type,
-                        int num_ref_l0, int num_ref_l1, int t8x8_mode, uintptr_t err, uintptr_t stream, uintptr_t route) {
+                        int num_ref_l0, int num_ref_l1, int t8x8_mode, uintptr_t err, uintptr_t stream, uintptr_t route,
+                        int slice_rows) {
     if ((pool & 15) != 0) throw std::invalid_argument("cabac_bin: symbol pool must be 16-byte aligned");
     if (B < 1 || wmb < 1 || hmb < 1) throw std::invalid_argument("cabac_bin: bad geometry");
     mivc_launch_cabac_bin(B, wmb, hmb, P<void>(hdr), P<int16_t>(coef), P<uint32_t>(mask), P<void>(nb), P<int>(cnt),
                           P<long long>(off), P<int>(tot), P<uint16_t>(pool), pool_cap, P<long long>(pool_used),
                           P<long long>(base), P<int>(total), P<int>(slot_qp), slice_type, num_ref_l0, num_ref_l1,
-                          t8x8_mode, P<int>(err), S(stream), P<void>(route));
+                          t8x8_mode, P<int>(err), S(stream), P<void>(route), slice_rows);
   }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("hdr"), py::arg("coef"), py::arg("mask"), py::arg("nb"),
      py::arg("cnt"), py::arg("off"), py::arg("tot"), py::arg("pool"), py::arg("pool_cap"), py::arg("pool_used"),
      py::arg("base"), py::arg("total"), py::arg("slot_qp"), py::arg("slice_type"), py::arg("num_ref_l0"),
-     py::arg("num_ref_l1"), py::arg("t8x8_mode"), py::arg("err"), py::arg("stream"), py::arg("route") = 0);
+     py::arg("num_ref_l1"), py::arg("t8x8_mode"), py::arg("err"), py::arg("stream"), py::arg("route") = 0,
+     py::arg("slice_rows") = 0);
   m.def("cabac_code", [](int L, int B, uintptr_t pool, uintptr_t base, uintptr_t total, uintptr_t hdr_bits,
                          uintptr_t hdr_nbits, uintptr_t slot_qp, unsigned long long itypes, uintptr_t bytes,
                          uintptr_t out, uintptr_t out_off, uintptr_t err, uintptr_t stream, uintptr_t host_out,

@@ -9,7 +9,7 @@
 // host writer's (tests/test_cabac.py pins the decomposition on the CPU).
 //
 // Two launches:
-//   mivc_launch_cabac_bin   one frame step (B slots, one slice each), into a symbol pool
+//   mivc_launch_cabac_bin   one frame step (B slots, S slices each), into a symbol pool
 //     cabac_mask    (nmb/2 x B, wave64)    non-zero mask of every 4x4 / DC block
 //     cabac_prep    (nmb/64 x B, 64)       lane per MB: coding state (skip, cbp, mvd, cbf ...)
 //     cabac_chain   (B, 64)                mb_qp_delta chain (QP_pred scan) per slot
@@ -64,14 +64,26 @@ struct CabacBinArgs {
   int* err;
   // routed (route.h): every slot's own slice type (its picture kind) and active list-0 size
   const SlotRoute* rt;
+  // slices (H264Params.slices): every picture is `per_slot` slices of `slice_mbs` MBs (whole
+  // MB rows; the last one may be shorter).  Slice index ls = slot * per_slot + mb / slice_mbs
+  // addresses tot / base / total; symbol offsets are relative to the slice.
+  int slice_mbs, per_slot;
 };
 
-__device__ __forceinline__ CabacSliceInfo slice_info(const CabacBinArgs& a, int slot) {
+__device__ __forceinline__ int slice_first(const CabacBinArgs& a, int mb) { return (mb / a.slice_mbs) * a.slice_mbs; }
+__device__ __forceinline__ int slice_end(const CabacBinArgs& a, int mb) {
+  return min(slice_first(a, mb) + a.slice_mbs, a.g.nmb());
+}
+__device__ __forceinline__ int slice_index(const CabacBinArgs& a, int slot, int mb) {
+  return slot * a.per_slot + mb / a.slice_mbs;
+}
+
+__device__ __forceinline__ CabacSliceInfo slice_info(const CabacBinArgs& a, int slot, int mb) {
   CabacSliceInfo si{};
   si.slice_type = a.rt ? a.rt[slot].kind : a.slice_type;
   si.wmb = a.g.wmb;
   si.hmb = a.g.hmb;
-  si.first_mb = 0;
+  si.first_mb = slice_first(a, mb);
   si.num_ref[0] = a.rt ? (a.rt[slot].kind == SK_I ? 1 : a.rt[slot].n0) : a.num_ref_l0;
   si.num_ref[1] = a.num_ref_l1;
   si.t8x8_mode = a.t8x8_mode;
@@ -118,7 +130,7 @@ __global__ __launch_bounds__(64) void cabac_mask(CabacBinArgs a) {
 __global__ __launch_bounds__(64) void cabac_prep(CabacBinArgs a) {
   const int mb = blockIdx.x * 64 + threadIdx.x, slot = blockIdx.y;
   if (mb >= a.g.nmb()) return;
-  const CabacSliceInfo si = slice_info(a, slot);
+  const CabacSliceInfo si = slice_info(a, slot, mb);
   const size_t base = static_cast<size_t>(slot) * a.g.nmb();
   h264::cabac_prepare_mb(si, a.hdr + base, mb, a.mask[base + mb], a.nb[base + mb]);
 }
@@ -147,10 +159,11 @@ __device__ __forceinline__ int wave_scan_max(int v) {
 
 // mb_qp_delta chain (cabac_qp_chain as a scan): MB i codes a delta iff it is not skipped
 // and (cbp != 0 or I16x16); its delta is QP_i - QP of the last earlier delta MB (or the
-// slice QP); its first-bin context is "MB i-1 coded a non-zero delta".  One wave per slot.
+// slice QP); its first-bin context is "MB i-1 coded a non-zero delta".  One wave per slice.
 __global__ __launch_bounds__(64) void cabac_chain(CabacBinArgs a) {
-  const int slot = blockIdx.x, n = a.g.nmb(), lane = threadIdx.x;
-  CabacNb* nb = a.nb + static_cast<size_t>(slot) * n;
+  const int slot = blockIdx.x / a.per_slot, first = (blockIdx.x - slot * a.per_slot) * a.slice_mbs;
+  const int n = min(a.g.nmb() - first, a.slice_mbs), lane = threadIdx.x;
+  CabacNb* nb = a.nb + static_cast<size_t>(slot) * a.g.nmb() + first;
   const int per = (n + 63) / 64;
   const int i0 = lane * per, i1 = min(n, i0 + per);
   auto has = [&](int i) { return !nb[i].skip && (nb[i].cbp != 0 || nb[i].kind == h264::MBK_I16x16); };
@@ -182,19 +195,20 @@ __global__ __launch_bounds__(64) void cabac_chain(CabacBinArgs a) {
 __global__ __launch_bounds__(64) void cabac_count(CabacBinArgs a) {
   const int mb = blockIdx.x * 64 + threadIdx.x, slot = blockIdx.y, n = a.g.nmb();
   if (mb >= n) return;
-  const CabacSliceInfo si = slice_info(a, slot);
+  const CabacSliceInfo si = slice_info(a, slot, mb);
   const size_t base = static_cast<size_t>(slot) * n;
   h264::CabacSymbolPacker<h264::CabacCountEmit> s;
   h264::CabacMbCoder<h264::CabacSymbolPacker<h264::CabacCountEmit>> coder(s, si, a.nb + base);
-  coder.code_mb(mb, a.hdr[base + mb], a.coef + (base + mb) * h264::kCoefPerMb, mb == n - 1);
+  coder.code_mb(mb, a.hdr[base + mb], a.coef + (base + mb) * h264::kCoefPerMb, mb == slice_end(a, mb) - 1);
   s.flush_bypass();
   a.cnt[base + mb] = s.out.n;
 }
 
-// Symbol offsets of every MB inside its slice: one wave per slot.
+// Symbol offsets of every MB inside its slice: one wave per slice.
 __global__ __launch_bounds__(64) void cabac_offsets(CabacBinArgs a) {
-  const int slot = blockIdx.x, n = a.g.nmb(), lane = threadIdx.x;
-  const size_t base = static_cast<size_t>(slot) * n;
+  const int slot = blockIdx.x / a.per_slot, first = (blockIdx.x - slot * a.per_slot) * a.slice_mbs;
+  const int n = min(a.g.nmb() - first, a.slice_mbs), lane = threadIdx.x;
+  const size_t base = static_cast<size_t>(slot) * a.g.nmb() + first;
   const int per = (n + 63) / 64;
   const int i0 = lane * per, i1 = min(n, i0 + per);
   long long loc = 0;
@@ -205,14 +219,14 @@ __global__ __launch_bounds__(64) void cabac_offsets(CabacBinArgs a) {
     a.off[base + i] = p;
     p += a.cnt[base + i];
   }
-  if (lane == 63) a.tot[slot] = static_cast<int>(incl);
+  if (lane == 63) a.tot[blockIdx.x] = static_cast<int>(incl);
 }
 
 // Slice regions of this frame step in the group's pool: kCabacGap + symbols, rounded to
 // 8 symbols (16-byte aligned), allocated back to back after the group's earlier steps.
 // One wave.
 __global__ __launch_bounds__(64) void cabac_alloc(CabacBinArgs a) {
-  const int B = a.g.B, lane = threadIdx.x;
+  const int B = a.g.B * a.per_slot, lane = threadIdx.x;  // slices of the step
   const int per = (B + 63) / 64;
   const int i0 = lane * per, i1 = min(B, i0 + per);
   auto region = [&](int s) { return (static_cast<long long>(a.tot[s]) + kCabacGap + 7) & ~7ll; };
@@ -266,16 +280,18 @@ struct StagedEmit {
 __global__ __launch_bounds__(64) void cabac_bins(CabacBinArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t stage[64 * 8];
   const int mb = blockIdx.x * 64 + threadIdx.x, slot = blockIdx.y, n = a.g.nmb();
-  if (mb >= n || a.total[slot] < 0) return;
-  const CabacSliceInfo si = slice_info(a, slot);
+  if (mb >= n) return;
+  const int ls = slice_index(a, slot, mb);
+  if (a.total[ls] < 0) return;
+  const CabacSliceInfo si = slice_info(a, slot, mb);
   const size_t base = static_cast<size_t>(slot) * n;
   h264::CabacSymbolPacker<StagedEmit> s;
-  s.out.g = a.pool + a.base[slot] + kCabacGap;
+  s.out.g = a.pool + a.base[ls] + kCabacGap;
   s.out.lds = stage + threadIdx.x * 8;
   s.out.start = s.out.pos = a.off[base + mb];
   s.out.n = 0;
   h264::CabacMbCoder<h264::CabacSymbolPacker<StagedEmit>> coder(s, si, a.nb + base);
-  coder.code_mb(mb, a.hdr[base + mb], a.coef + (base + mb) * h264::kCoefPerMb, mb == n - 1);
+  coder.code_mb(mb, a.hdr[base + mb], a.coef + (base + mb) * h264::kCoefPerMb, mb == slice_end(a, mb) - 1);
   s.flush_bypass();
   s.out.finish();
 }
@@ -541,8 +557,11 @@ extern "C" void mivc_launch_cabac_bin(int B, int wmb, int hmb, const void* hdr, 
                                       void* nb, int* cnt, long long* off, int* tot, uint16_t* pool,
                                       long long pool_cap, long long* pool_used, long long* base, int* total,
                                       const int* slot_qp, int slice_type, int num_ref_l0, int num_ref_l1,
-                                      int t8x8_mode, int* err, void* stream, const void* route) {
+                                      int t8x8_mode, int* err, void* stream, const void* route, int slice_rows) {
   CabacBinArgs a;
+  const int rows = (slice_rows > 0 && slice_rows < hmb) ? slice_rows : hmb;
+  a.slice_mbs = rows * wmb;
+  a.per_slot = (hmb + rows - 1) / rows;
   a.rt = static_cast<const SlotRoute*>(route);
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.hdr = static_cast<const MbHeader*>(hdr);
@@ -568,9 +587,9 @@ extern "C" void mivc_launch_cabac_bin(int B, int wmb, int hmb, const void* hdr, 
   const dim3 mbgrid((nmb + 63) / 64, B);
   hipLaunchKernelGGL(cabac_mask, dim3((nmb + 2 * kMaskSpan - 1) / (2 * kMaskSpan), B), dim3(64), 0, s, a);
   hipLaunchKernelGGL(cabac_prep, mbgrid, dim3(64), 0, s, a);
-  hipLaunchKernelGGL(cabac_chain, dim3(B), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(cabac_chain, dim3(B * a.per_slot), dim3(64), 0, s, a);
   hipLaunchKernelGGL(cabac_count, mbgrid, dim3(64), 0, s, a);
-  hipLaunchKernelGGL(cabac_offsets, dim3(B), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(cabac_offsets, dim3(B * a.per_slot), dim3(64), 0, s, a);
   hipLaunchKernelGGL(cabac_alloc, dim3(1), dim3(64), 0, s, a);
   hipLaunchKernelGGL(cabac_bins, mbgrid, dim3(64), 0, s, a);
 }

@@ -43,7 +43,14 @@ struct IntraArgs {
   int use_i8x8;  // High profile: Intra8x8 trial (x264 --partitions i8x8, with --8x8dct)
   const SlotRoute* rt;  // routed (route.h): rec_* are pools, each slot's current picture
   int nbuf;
+  // MB rows per slice (H264Params.slices): a slice's first row has no neighbours above
+  // (6.4.8) and starts without waiting for the row above; 0 = one slice per picture
+  int slice_rows;
 };
+
+__device__ __forceinline__ bool top_in_slice(int my, int slice_rows) {
+  return my > 0 && (slice_rows <= 0 || my % slice_rows != 0);
+}
 
 constexpr int TS = kTileStride;
 
@@ -157,11 +164,12 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
   const uint8_t* srcy = a.src_y + slot * g.ysize();
   const size_t rcur = route_index(a.rt, a.nbuf, slot, RO_CUR);
   uint8_t* recy = a.rec_y + rcur * g.ysize();
+  const bool top = top_in_slice(my, a.slice_rows);
   int mbav = 0;
   if (mx > 0) mbav |= h264::AV_LEFT;
-  if (my > 0) mbav |= h264::AV_TOP;
-  if (mx > 0 && my > 0) mbav |= h264::AV_TOPLEFT;
-  if (my > 0 && mx < g.wmb - 1) mbav |= h264::AV_TOPRIGHT;
+  if (top) mbav |= h264::AV_TOP;
+  if (mx > 0 && top) mbav |= h264::AV_TOPLEFT;
+  if (top && mx < g.wmb - 1) mbav |= h264::AV_TOPRIGHT;
 
   // ---- stage source and reconstructed neighbourhood
   {
@@ -176,7 +184,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
   }
   if (lane < 21) {  // tile row 0: x = X0-1 .. X0+19
     int x = X0 - 1 + lane;
-    bool ok = my > 0 && x >= 0 && x < W && (lane < 17 || (mbav & h264::AV_TOPRIGHT));
+    bool ok = top && x >= 0 && x < W && (lane < 17 || (mbav & h264::AV_TOPRIGHT));
     S.tile[lane] = ok ? recy[static_cast<size_t>(Y0 - 1) * W + x] : 0;
   } else if (lane >= 21 && lane < 29) {  // top-right MB's bottom row x = X0+16 .. X0+23 (Intra8x8 block 1)
     int x = X0 + 16 + lane - 21;
@@ -192,7 +200,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
     int c = lane / 9, i = lane % 9;
     const uint8_t* rc = (c == 0 ? a.rec_u : a.rec_v) + rcur * g.csize();
     int x = mx * 8 - 1 + i;
-    bool ok = my > 0 && x >= 0;
+    bool ok = top && x >= 0;
     S.ctop[c][i] = ok ? rc[static_cast<size_t>(my * 8 - 1) * cw + x] : 0;
   } else if (lane >= 48) {  // chroma left
     int c = (lane - 48) >> 3, i = (lane - 48) & 7;
@@ -212,7 +220,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
         lm = (L.kind == h264::MBK_I4x4 || L.kind == h264::MBK_I8x8) ? L.i4_modes[h264::kRasterToBlk[3 + 4 * i]] : 2;
       }
     }
-    if (my > 0) {
+    if (top) {
       const MbHeader& T = a.hdr[o - g.wmb];
       tm = (T.kind == h264::MBK_I4x4 || T.kind == h264::MBK_I8x8) ? T.i4_modes[h264::kRasterToBlk[i + 12]] : 2;
     }
@@ -674,7 +682,7 @@ __global__ __launch_bounds__(64 * kIntraWaves) void encode_intra_wavefront(Intra
   for (int y = w; y < g.hmb; y += kIntraWaves) {
     if (!a.intra_flag) {  // I frame: every MB
       for (int x = 0; x < g.wmb; ++x) {
-        if (y > 0) row_wait(prog, y - 1, min(x + 2, g.wmb), a.err);
+        if (top_in_slice(y, a.slice_rows)) row_wait(prog, y - 1, min(x + 2, g.wmb), a.err);
         encode_intra_mb(a, S, slot, x, y, tapw);
         row_publish(prog, y, x + 1);
 #ifdef MIVC_INTRA_PROFILE
@@ -692,7 +700,7 @@ __global__ __launch_bounds__(64 * kIntraWaves) void encode_intra_wavefront(Intra
         const int x = x0 + __builtin_ctzll(mask);
         mask &= mask - 1;
         if (x > 0) row_publish(prog, y, x);  // MBs before x in this row are final (inter)
-        if (y > 0) row_wait(prog, y - 1, min(x + 2, g.wmb), a.err);
+        if (top_in_slice(y, a.slice_rows)) row_wait(prog, y - 1, min(x + 2, g.wmb), a.err);
         encode_intra_mb(a, S, slot, x, y, tapw);
         row_publish(prog, y, x + 1);
       }
@@ -710,10 +718,12 @@ extern "C" void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t*
                                          const uint8_t* src_v, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v,
                                          const int* qp, int chroma_qp_offset, void* hdr, int16_t* coef, uint8_t* nz,
                                          const uint8_t* intra_flag, const int* intra_count, int* err, int use_i4x4,
-                                         const int8_t* aq, void* stream, int use_i8x8, const void* route, int nbuf) {
+                                         const int8_t* aq, void* stream, int use_i8x8, const void* route, int nbuf,
+                                         int slice_rows) {
   IntraArgs a;
   a.rt = static_cast<const SlotRoute*>(route);
   a.nbuf = nbuf;
+  a.slice_rows = slice_rows;
   a.aq = aq;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.src_y = src_y;

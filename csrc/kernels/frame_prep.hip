@@ -42,28 +42,36 @@ __global__ void prep_plane(PrepArgs a, int plane) {
   out[static_cast<size_t>(y) * W + x] = in[static_cast<size_t>(cy) * w + cx];
 }
 
-// Fast path (no resampling, 16-byte aligned rows): one thread per 16 output bytes.
-__global__ void prep_plane_copy16(PrepArgs a, int plane) {
-  int x = (blockIdx.x * blockDim.x + threadIdx.x) * 16;
-  int y = blockIdx.y;
-  int n = blockIdx.z;
-  int sh = plane ? 1 : 0;
-  int W = a.W >> sh, H = a.H >> sh;
-  if (x >= W) return;
-  int w = a.w >> sh, h = a.h >> sh;
+// Fast path (no resampling, 16-byte aligned rows): a 256-thread workgroup copies kPrepRows
+// rows of one frame as 16-byte chunks, every thread several (the one-wave-per-1 KiB grid of
+// round 3 made half a million tiny workgroups per plane and step at 1080p x 256 slots).
+constexpr int kPrepRows = 8;
+
+__global__ __launch_bounds__(256) void prep_plane_copy16(PrepArgs a, int plane) {
+  const int sh = plane ? 1 : 0;
+  const int W = a.W >> sh, H = a.H >> sh;
+  const int w = a.w >> sh, h = a.h >> sh;
+  const int n = blockIdx.y;
+  const int cpr = W >> 4;  // 16-byte chunks per output row
+  const int y0 = blockIdx.x * kPrepRows;
+  const int rows = min(kPrepRows, H - y0);
   const uint8_t* in = plane == 0 ? a.in_y : (plane == 1 ? a.in_u : a.in_v);
   in += n * (plane ? a.in_frame_stride_c : a.in_frame_stride_y);
   if (a.fsel) in += a.fsel[n] * (plane ? a.fstep_c : a.fstep_y);
-  uint8_t* out = plane == 0 ? a.out_y : (plane == 1 ? a.out_u : a.out_v);
-  out += static_cast<size_t>(n) * W * H + static_cast<size_t>(y) * W + x;
-  const uint8_t* row = in + static_cast<size_t>(min(y, h - 1)) * w;
-  if (x + 16 <= w) {
-    *reinterpret_cast<uint4*>(out) = *reinterpret_cast<const uint4*>(row + x);
-  } else {
-    uint8_t b[16];
+  uint8_t* out = (plane == 0 ? a.out_y : (plane == 1 ? a.out_u : a.out_v)) + static_cast<size_t>(n) * W * H;
+  for (int i = threadIdx.x; i < rows * cpr; i += 256) {
+    const int r = i / cpr, x = (i - r * cpr) * 16, y = y0 + r;
+    const uint8_t* row = in + static_cast<size_t>(min(y, h - 1)) * w;
+    uint4 v;
+    if (x + 16 <= w) {
+      v = *reinterpret_cast<const uint4*>(row + x);
+    } else {
+      uint8_t b[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) b[k] = row[min(x + k, w - 1)];
-    *reinterpret_cast<uint4*>(out) = *reinterpret_cast<const uint4*>(b);
+      for (int k = 0; k < 16; ++k) b[k] = row[min(x + k, w - 1)];
+      v = *reinterpret_cast<const uint4*>(b);
+    }
+    *reinterpret_cast<uint4*>(out + static_cast<size_t>(y) * W + x) = v;
   }
 }
 
@@ -106,9 +114,9 @@ extern "C" void mivc_launch_prep(const uint8_t* in_y, const uint8_t* in_u, const
                  (reinterpret_cast<uintptr_t>(in_v) % 16 == 0) && W % 32 == 0;
   if (ow != w || oh != h) return;  // scale.hip resamples before prep (the binding rejects this)
   if (aligned) {
-    hipLaunchKernelGGL(prep_plane_copy16, dim3((W / 16 + 63) / 64, H, nframes), dim3(64), 0, s, a, 0);
-    hipLaunchKernelGGL(prep_plane_copy16, dim3((W / 32 + 63) / 64, H / 2, nframes), dim3(64), 0, s, a, 1);
-    hipLaunchKernelGGL(prep_plane_copy16, dim3((W / 32 + 63) / 64, H / 2, nframes), dim3(64), 0, s, a, 2);
+    hipLaunchKernelGGL(prep_plane_copy16, dim3((H + kPrepRows - 1) / kPrepRows, nframes), dim3(256), 0, s, a, 0);
+    hipLaunchKernelGGL(prep_plane_copy16, dim3((H / 2 + kPrepRows - 1) / kPrepRows, nframes), dim3(256), 0, s, a, 1);
+    hipLaunchKernelGGL(prep_plane_copy16, dim3((H / 2 + kPrepRows - 1) / kPrepRows, nframes), dim3(256), 0, s, a, 2);
     return;
   }
   hipLaunchKernelGGL(prep_plane, dim3((W + 255) / 256, H, nframes), dim3(256), 0, s, a, 0);

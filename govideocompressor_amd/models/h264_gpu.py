@@ -170,6 +170,24 @@ class H264Params:
     wp_min_scale: float = 0.08
     ref_range: int = int(os.environ.get("MIVC_REF_RANGE", 4))
     ref_gate: int = int(os.environ.get("MIVC_REF_GATE", 1500))
+    # slices per picture (x264 --slices): whole MB rows each.  The GPU arithmetic coder codes
+    # one slice per lane, so S slices give S times the independent serial chains per picture
+    # (and the intra wavefront restarts at every slice); each slice costs a header and the
+    # prediction across its top edge.  CABAC only; temporal direct only (spatial direct's
+    # neighbour derivation is not slice-aware).
+    slices: int = int(os.environ.get("MIVC_SLICES", 1))
+
+    def slice_rows(self) -> int:
+        """MB rows per slice (0: one slice per picture)."""
+        hmb = (self.height + 15) // 16
+        n = max(1, int(self.slices))
+        if n <= 1 or not self.cabac:
+            return 0
+        return max(1, -(-hmb // n))
+
+    def eff_slices(self) -> int:
+        r = self.slice_rows()
+        return 1 if r == 0 else -(-((self.height + 15) // 16) // r)
 
     def eff_bframes(self) -> int:
         return max(0, int(self.bframes)) if self.cabac else 0
@@ -205,7 +223,8 @@ class H264Params:
                 + (" weightp" if self.eff_weightp() else "")
                 + (f" {nb}B" + (" b-adapt" if self.b_adapt else "") + (" b-pyramid" if self.eff_pyramid() else "")
                    + f" {self.direct}-direct" if nb else "")
-                + (" weightb" if nb and self.weightb else ""))
+                + (" weightb" if nb and self.weightb else "")
+                + (f" slices{self.eff_slices()}" if self.eff_slices() > 1 else ""))
 
     def frame_qps(self) -> tuple[int, int]:
         """(qp_I, qp_P).  CRF maps to the P-frame QP (x264 scale without MB-tree);
@@ -286,8 +305,12 @@ class GpuH264Encoder:
             raise ValueError("b-pyramid needs spatial direct prediction (direct='spatial')")
         if entropy not in ("gpu", "cpu"):
             raise ValueError("entropy must be 'gpu' or 'cpu'")
+        if params.eff_slices() > 1 and params.direct == "spatial" and params.eff_bframes():
+            raise ValueError("slices > 1 need temporal direct (the spatial direct kernels are not slice-aware)")
         self.entropy = entropy
         self.p = params
+        self.slice_rows = params.slice_rows()
+        self.S = params.eff_slices()
         self.B = int(slots)
         self.dev = _resolve(device)
         self.hip = native.hip()
@@ -431,7 +454,7 @@ class GpuH264Encoder:
         peak_mb = int(os.environ.get("MIVC_CABAC_PEAK_SYMS_PER_MB", 768)) * grow
         self.cab_grow = grow
         gap = int(self.hip.cabac_gap())
-        L = G * B
+        L = G * B * self.S  # one lane per slice: G steps x B slots x S slices
         self.cab_pool_cap = B * nmb * (G * per_mb + peak_mb) + L * (gap + 8) + 64
         self.cab_pool = [torch.empty((self.cab_pool_cap + 64,), dtype=torch.int16, device=dev) for _ in range(2)]
         self.cab_pool_used = torch.zeros((2,), dtype=i64, device=dev)
@@ -452,7 +475,7 @@ class GpuH264Encoder:
         self.cab_nb = torch.zeros((B, nmb, int(self.hip.cabac_nb_bytes())), dtype=u8, device=dev)
         self.cab_cnt = torch.zeros((B, nmb), dtype=i32, device=dev)
         self.cab_off = torch.zeros((B, nmb), dtype=i64, device=dev)
-        self.cab_tot = torch.zeros((B,), dtype=i32, device=dev)
+        self.cab_tot = torch.zeros((B * self.S,), dtype=i32, device=dev)
         self.entropy_stream = torch.cuda.Stream(device=dev)
         self.cab_bin_done = [torch.cuda.Event() for _ in range(2)]
         self.cab_done = [torch.cuda.Event() for _ in range(2)]
@@ -661,11 +684,11 @@ class GpuH264Encoder:
         with stt("intra"):
             self.hip.encode_intra(B, wmb, hmb, sy, su, sv, py, pu, pv, P(self.qp), cqo, P(hdr), P(coef), P(self.nz),
                                   flag_ptr, count_ptr, P(self.err), int(self.p.i4x4 and trial), s, aq,
-                                  int(self.p.i8x8 and self.p.eff_t8x8() and trial), rt, NB)
+                                  int(self.p.i8x8 and self.p.eff_t8x8() and trial), rt, NB, self.slice_rows)
         if aq:
             # MBs without mb_qp_delta take QP_pred (clause 7.4.5): their records must say so
             # before deblocking reads every MB's QP
-            self.hip.qp_fixup(B, wmb, hmb, P(hdr), P(coef), P(self.nz), P(self.qp_flags), P(self.qp), s)
+            self.hip.qp_fixup(B, wmb, hmb, P(hdr), P(coef), P(self.nz), P(self.qp_flags), P(self.qp), s, self.slice_rows)
         # A non-reference B picture's reconstruction feeds nothing but its own intra MBs
         # (which predict from unfiltered samples), so its in-loop filter only matters when
         # someone looks at the picture: metrics (PSNR / SSIM) or keep_recon.  The bitstream
@@ -885,24 +908,24 @@ class GpuH264Encoder:
         again once this is done, whatever the arithmetic coder is doing.  Every slot's slice
         type and list size come from the step's routing.
         qp_dev: [B] int32 slice QPs of this step in a buffer that outlives the launch."""
-        B = self.B
+        B, BS = self.B, self.B * self.S
         r = g & 1
         if j == 0:
             self.cab_pool_used[r].zero_()
-        self._header_bits_into(self.h_cab_hdr_bits[r][j * B:(j + 1) * B], self.h_cab_hdr_nbits[r][j * B:(j + 1) * B],
-                               self.cab_hdr_bits[r][j * B:(j + 1) * B], self.cab_hdr_nbits[r][j * B:(j + 1) * B],
+        self._header_bits_into(self.h_cab_hdr_bits[r][j * BS:(j + 1) * BS], self.h_cab_hdr_nbits[r][j * BS:(j + 1) * BS],
+                               self.cab_hdr_bits[r][j * BS:(j + 1) * BS], self.cab_hdr_nbits[r][j * BS:(j + 1) * BS],
                                pics, t, qps_t, idr_ids)
         P = self._ptr
         self.hip.cabac_bin(B, self.wmb, self.hmb, P(self.hdr[k]), P(self.coef[k]), P(self.cab_mask), P(self.cab_nb),
                            P(self.cab_cnt), P(self.cab_off), P(self.cab_tot), P(self.cab_pool[r]), self.cab_pool_cap,
-                           self.cab_pool_used[r].data_ptr(), self.cab_base[r][j * B:].data_ptr(),
-                           self.cab_total[r][j * B:].data_ptr(), P(qp_dev), pics[0].slice_type, 1, 1,
-                           int(self.p.eff_t8x8()), P(self.err), self.copy_stream.cuda_stream, route)
+                           self.cab_pool_used[r].data_ptr(), self.cab_base[r][j * BS:].data_ptr(),
+                           self.cab_total[r][j * BS:].data_ptr(), P(qp_dev), pics[0].slice_type, 1, 1,
+                           int(self.p.eff_t8x8()), P(self.err), self.copy_stream.cuda_stream, route, self.slice_rows)
 
     def _gpu_cabac_code(self, g: int, t0: int, n: int, qps_d: torch.Tensor):
         """Arithmetic-code the n frame steps t0 .. t0 + n - 1 of a group (n * B slices) on
         the entropy stream, after their binarisation; sizes go to pinned host memory."""
-        B = self.B
+        BS = self.B * self.S
         r = g & 1
         self.cab_bin_done[r].record(self.copy_stream)
         itypes = 1 if t0 == 0 else 0  # frame step 0 is the IDR picture of every slot
@@ -910,11 +933,12 @@ class GpuH264Encoder:
         es = self.entropy_stream
         with torch.cuda.stream(es):
             es.wait_event(self.cab_bin_done[r])
-            self.hip.cabac_code(n * B, B, P(self.cab_pool[r]), P(self.cab_base[r]), P(self.cab_total[r]),
+            # qps_d: [F, B * S] slice QPs, lane order (step, slot, slice)
+            self.hip.cabac_code(n * BS, BS, P(self.cab_pool[r]), P(self.cab_base[r]), P(self.cab_total[r]),
                                 P(self.cab_hdr_bits[r]), P(self.cab_hdr_nbits[r]), qps_d[t0].data_ptr(), itypes,
                                 P(self.cab_bytes[r]), P(self.cab_comp[r]), P(self.cab_comp_off[r]), P(self.err),
                                 es.cuda_stream, P(self.h_cab_out[r]), self.cab_host_cap)
-            self.h_cab_bytes[r][: n * B].copy_(self.cab_bytes[r][: n * B], non_blocking=True)
+            self.h_cab_bytes[r][: n * BS].copy_(self.cab_bytes[r][: n * BS], non_blocking=True)
             self.h_pool_used[r].copy_(self.cab_pool_used[r:r + 1], non_blocking=True)
             self.cab_done[r].record(es)
 
@@ -924,7 +948,7 @@ class GpuH264Encoder:
         ``copied[g]`` (set once the wraps are submitted) releases ring g % 2 (pool, headers,
         pinned sizes) for group g + 2; the host buffer itself is reused by group g + 2's
         coder only after these wraps finished (the main thread waits for them)."""
-        B = self.B
+        B = self.B * self.S  # lanes (slices) per step
         r = g & 1
         t_0 = time.perf_counter()
         self.cab_done[r].synchronize()
@@ -937,7 +961,7 @@ class GpuH264Encoder:
         if (sizes < 0).any():
             err = int(self.err.item())
             for f in range(t0, t0 + n):  # nothing of this group will be wrapped
-                wrap_futs[f] = self.pool.submit(lambda: [(b"", 0)] * B)
+                wrap_futs[f] = self.pool.submit(lambda: [(b"", 0)] * self.B)
             copied[g].set()
             if err & 4:
                 raise CabacPoolExhausted("GPU CABAC: symbol pool exhausted (raise MIVC_CABAC_SYMS_PER_MB / "
@@ -972,21 +996,28 @@ class GpuH264Encoder:
                                pics, t, qps_t, idr_ids)
 
     def _header_bits_into(self, hb, hn, db, dn, pics: list[PicPlan], t: int, qps_t, idr_ids: list[int]):
+        """Slice headers of one step, lane order (slot, slice) -- rows of ``hb`` / ``hn``."""
         hbn, hnn = hb.numpy(), hn.numpy()
         cache = {}
         wp = self._wp
+        S, first = self.S, self.slice_rows * self.wmb
         for b in range(self.B):
             pic = pics[b]
-            # slots sharing a plan share its PicPlan objects: the header differs only by QP,
-            # the IDR id and the explicit weights
-            key = (id(pic), int(qps_t[b]), idr_ids[b] & 0xFFFF if pic.kind == "I" else -1,
-                   tuple(wp[t, b]) if (wp is not None and pic.kind == "P") else None)
-            if key not in cache:
-                cache[key] = self.host.slice_header_bits(self.cfg, self._frame_params(b, pic, t, int(qps_t[b]), idr_ids))
-            words, nbits = cache[key]
-            hbn[b, :] = 0
-            hbn[b, : len(words)] = np.array(words, dtype=np.uint32).view(np.int32)
-            hnn[b] = nbits
+            for si in range(S):
+                # slots sharing a plan share its PicPlan objects: the header differs only by QP,
+                # the IDR id, the explicit weights and the slice's first MB
+                key = (id(pic), int(qps_t[b]), idr_ids[b] & 0xFFFF if pic.kind == "I" else -1,
+                       tuple(wp[t, b]) if (wp is not None and pic.kind == "P") else None, si)
+                if key not in cache:
+                    fp = self._frame_params(b, pic, t, int(qps_t[b]), idr_ids)
+                    if si:
+                        fp["first_mb"] = si * first
+                    cache[key] = self.host.slice_header_bits(self.cfg, fp)
+                words, nbits = cache[key]
+                ln = b * S + si
+                hbn[ln, :] = 0
+                hbn[ln, : len(words)] = np.array(words, dtype=np.uint32).view(np.int32)
+                hnn[ln] = nbits
         db.copy_(hb, non_blocking=True)
         dn.copy_(hn, non_blocking=True)
 
@@ -1030,10 +1061,14 @@ class GpuH264Encoder:
         wrap_futs[t] = self.pool.submit(self._wrap, buf, total, sizes, pics)
 
     def _wrap(self, buf, total: int, sizes: list[int], pics: list[PicPlan], align: int = 1) -> list[tuple[bytes, int]]:
+        """Slice RBSPs of one step -> one entry per slot: its S slice NAL units back to back."""
         t0 = time.perf_counter()
-        refs = [pic.nal_ref_idc for pic in pics]
-        types = [5 if pic.kind == "I" else 1 for pic in pics]
+        S = len(sizes) // len(pics)
+        refs = [pic.nal_ref_idc for pic in pics for _ in range(S)]
+        types = [5 if pic.kind == "I" else 1 for pic in pics for _ in range(S)]
         nals = self.host.nal_wrap_many(buf[:total].numpy(), sizes, refs[0], types[0], align, refs, types)
+        if S > 1:
+            nals = [b"".join(nals[b * S:(b + 1) * S]) for b in range(len(pics))]
         self.timings["entropy_s"] = self.timings.get("entropy_s", 0.0) + (time.perf_counter() - t0)
         return [(n, len(n) * 8) for n in nals]
 
@@ -1045,10 +1080,21 @@ class GpuH264Encoder:
         hdr = self.h_hdr[k].numpy()
         coef = self.h_coef[k].numpy()
 
+        S, rows = self.S, self.slice_rows
+
         def one(b: int):
             fp = self._frame_params(b, pics[b], t, int(qps_t[b]), idr_ids)
-            nal, st = self.host.write_slice(self.cfg, fp, hdr[b], coef[b])
-            return nal, st["bits"]
+            if S == 1:
+                nal, st = self.host.write_slice(self.cfg, fp, hdr[b], coef[b])
+                return nal, st["bits"]
+            nals, bits = [], 0
+            for si in range(S):
+                r0 = si * rows
+                n = min(rows, self.hmb - r0) * self.wmb
+                nal, st = self.host.write_slice(self.cfg, dict(fp, first_mb=r0 * self.wmb, num_mbs=n), hdr[b], coef[b])
+                nals.append(nal)
+                bits += st["bits"]
+            return b"".join(nals), bits
 
         out = list(self.pool.map(one, range(self.B)))
         t2 = time.perf_counter()
@@ -1217,6 +1263,8 @@ class GpuH264Encoder:
         # per coding step (rows), [F, B]: the kernels and the entropy stages index coding steps
         qps_c = np.take_along_axis(qps_h, orders, axis=1)
         qps_d = torch.from_numpy(np.ascontiguousarray(qps_c.T)).to(self.dev)
+        # the arithmetic coder's per-lane slice QPs (lanes: slot-major slices of each step)
+        qps_ls_d = qps_d.repeat_interleave(self.S, dim=1).contiguous() if self.S > 1 else qps_d
         cuts_c = np.take_along_axis(cuts_h, orders, axis=1)
         cuts_d = torch.from_numpy(np.ascontiguousarray(cuts_c.T)).to(self.dev)  # [F, B] coding order
         if self._wp_steps is not None:
@@ -1313,7 +1361,7 @@ class GpuH264Encoder:
                         for tt in range(a0, a0 + an):
                             wrap_futs[tt].result()
                         self.timings["host_blocked_s"] += time.perf_counter() - tw
-                    self._gpu_cabac_code(gi, t0, t - t0 + 1, qps_d)
+                    self._gpu_cabac_code(gi, t0, t - t0 + 1, qps_ls_d)
                     group_futs[gi] = self.copy_pool.submit(self._copy_out_group, gi, t0, t - t0 + 1, group_copied,
                                                            wrap_futs, steps_pics, groups)
             elif self.entropy == "gpu":

@@ -10,6 +10,8 @@ launch, and the decision runs per slot on the host (a few integer comparisons pe
 * picture i is the last anchor.  Coding i+1 as P then i+2 as P costs
   ``P(i+1 | i) + P(i+2 | i+1)``; coding i+1 as B between i and i+2 costs
   ``B(i+1 | i, i+2) + P(i+2 | i)``.  The cheaper wins;
+* B costs enter every comparison scaled by 100 / (120 + bframe_bias) (x264 prices a lowres B
+  frame that much cheaper than its raw SATD sum: B pictures are coded at a higher QP);
 * a B run then grows picture by picture while the P that would close it, predicted from i
   across the whole run, stays below ``INTER_THRESH - P_SENS_BIAS * (run - 1)`` per macroblock
   (x264's thresholds, 300 and 50: fast motion or a change of content ends the run early);
@@ -24,6 +26,7 @@ import numpy as np
 
 INTER_THRESH = 300
 P_SENS_BIAS = 50
+B_COST_SCALE = 100.0 / 120.0  # x264 slicetype frame cost of a B frame, --b-bias 0
 
 
 def b_adapt_types(p1: np.ndarray, pd: np.ndarray, bcost: np.ndarray, bframes: int, mb_count: int,
@@ -50,7 +53,7 @@ def b_adapt_types(p1: np.ndarray, pd: np.ndarray, bcost: np.ndarray, bframes: in
             i += 1  # i + 1 is an anchor (forced, or the last picture)
             continue
         keep_p = pcost(i + 1, 1) + pcost(i + 2, 1)
-        as_b = float(bcost[i + 1]) + pcost(i + 2, 2)
+        as_b = B_COST_SCALE * float(bcost[i + 1]) + pcost(i + 2, 2)
         if keep_p < as_b:
             i += 1
             continue

@@ -65,3 +65,10 @@ def test_crf_anchor_curve_ignores_b_pictures_and_uses_the_b_constant():
     # base complexity 120 (B pictures on) vs 80: the same anchor is coded finer
     assert q3[0, 4] < q0[0, 4]
     assert q3[0, 0] == q3[1, 0]
+
+
+def test_b_costs_are_scaled_like_x264():
+    """x264 prices a lowres B frame at 100 / 120 of its SATD sum (slicetype frame cost with
+    --b-bias 0): a B that costs 125 against a 120 P pair still wins (0.833 * 45 + 80 < 120)."""
+    p1, pd, bc = _costs(4, lambda d: {1: 60.0, 2: 80.0}.get(d, 900.0), b_cost=45.0)
+    assert b_adapt_types(p1, pd, bc, 3, 100)[:3] == "IBP"

@@ -455,3 +455,24 @@ def test_gpu_h264_spatial_direct_modes_roundtrip(host, wavefront):
     kinds = np.concatenate([np.asarray(p["mb_kind"]).ravel() for r in res for p in host.decode(r.bitstream)])
     assert (kinds == 13).sum() > 0
     enc.close()
+
+
+@pytest.mark.parametrize("entropy", ["gpu", "cpu"])
+def test_gpu_h264_slices_roundtrip(host, entropy):
+    """--slices 4 (whole MB rows): the intra wavefront treats every slice's first row as having
+    nothing above, QP prediction restarts per slice, the GPU CABAC codes one slice per lane --
+    the CPU decoder reconstructs the encoder's pictures from the multi-slice stream (with
+    B pictures, AQ and intra MBs in P / B pictures), and the picture really holds 4 slices."""
+    import torch
+    from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
+    w, h = 352, 288  # 18 MB rows -> slices of 5, 5, 5, 3 rows
+    p = H264Params(width=w, height=h, crf=24.0, slices=4)
+    assert p.eff_slices() == 4 and p.slice_rows() == 5
+    enc = GpuH264Encoder(p, slots=3, entropy=entropy)
+    y, u, v = synth_clip(3, 9, w, h, seed=11, kind="cuts")
+    res = enc.encode(y, u, v, keep_recon=True)
+    torch.cuda.synchronize()
+    _check_roundtrip(host, enc, res, w, h)
+    for r in res:
+        for nal in r.nals:
+            assert nal.count(b"\x00\x00\x01") == 4   # four slice NAL units per picture

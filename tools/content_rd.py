@@ -23,6 +23,11 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 CRFS = (18, 23, 28, 33)
+HEVC_CRFS = (22, 26, 30, 34)
+
+
+def _nbytes(r) -> int:
+    return r.nbytes() if hasattr(r, "nbytes") else len(r.bitstream)
 # name -> H264Params overrides.  "r3" = round 3's GOP / direct decisions
 CONFIGS = {
     "r3": dict(b_adapt=0, pyramid=False, direct="temporal"),
@@ -31,6 +36,13 @@ CONFIGS = {
     "pyramid": dict(b_adapt=1, pyramid=True, direct="spatial"),
     "default": dict(),  # the current defaults
 }
+# HEVC (GpuHevcEncoder) configurations: x265 --signhide, --bframes variants
+HEVC_CONFIGS = {
+    "default": dict(),
+    "signhide": dict(sdh=True),
+    "bf0": dict(bframes=0),
+    "bf3": dict(bframes=3, b_qp_offset=2),
+}
 
 
 def run(args):
@@ -38,28 +50,36 @@ def run(args):
     from govideocompressor_amd.models.h264_gpu import CONTENT_KINDS, GpuH264Encoder, H264Params, synth_clip
 
     w, h = (int(x) for x in args.size.split("x"))
-    out = {"size": args.size, "slots": args.slots, "frames": args.frames, "points": []}
+    out = {"size": args.size, "slots": args.slots, "frames": args.frames, "codec": args.codec, "points": []}
     kinds = args.kinds.split(",") if args.kinds else list(CONTENT_KINDS)
-    configs = {k: CONFIGS[k] for k in (args.configs.split(",") if args.configs else CONFIGS)}
+    table = HEVC_CONFIGS if args.codec == "hevc" else CONFIGS
+    configs = {k: table[k] for k in (args.configs.split(",") if args.configs else table)}
+    crfs = HEVC_CRFS if args.codec == "hevc" else CRFS
+    if args.codec == "hevc":
+        from govideocompressor_amd.models.hevc_gpu import GpuHevcEncoder, HevcParams
+        make = lambda over: GpuHevcEncoder(HevcParams(width=w, height=h, **over), slots=args.slots)  # noqa: E731
+    else:
+        make = lambda over: GpuH264Encoder(H264Params(width=w, height=h, **over), slots=args.slots)  # noqa: E731
     clips = {}
     for kind in kinds:
         clips[kind] = synth_clip(args.slots, args.frames, w, h, seed=17, kind=kind)
     for cname, over in configs.items():
-        enc = GpuH264Encoder(H264Params(width=w, height=h, **over), slots=args.slots)
+        enc = make(over)
         for kind in kinds:
             y, u, v = clips[kind]
-            for crf in CRFS:
+            for crf in crfs:
                 enc.p.crf = float(crf)
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 res = enc.encode(y, u, v, metrics=True)
                 torch.cuda.synchronize()
                 dt = time.perf_counter() - t0
-                bits = sum(8 * r.nbytes() for r in res)
+                bits = sum(8 * _nbytes(r) for r in res)
                 kbps = bits / (args.slots * args.frames / 30.0) / 1000.0
+                stats = getattr(enc, "stats", {}) or {}
                 pt = dict(config=cname, kind=kind, crf=crf, kbps=kbps, psnr=float(np.mean([r.psnr_y for r in res])),
-                          ssim=float(np.mean([r.ssim_y for r in res])), fps=args.slots * args.frames / dt,
-                          b_ratio=enc.stats.get("b_ratio", 0.0), scenecuts=enc.stats.get("scenecuts", 0))
+                          ssim=float(np.mean([getattr(r, "ssim_y", 0.0) for r in res])), fps=args.slots * args.frames / dt,
+                          b_ratio=stats.get("b_ratio", 0.0), scenecuts=stats.get("scenecuts", 0))
                 out["points"].append(pt)
                 print(json.dumps(pt), flush=True)
         enc.close()
@@ -75,7 +95,8 @@ def table(args):
     pts = d["points"]
     kinds = list(dict.fromkeys(p["kind"] for p in pts))
     configs = list(dict.fromkeys(p["config"] for p in pts))
-    print(f"# Multi-content RD suite ({d['size']}, {d['slots']} segments x {d['frames']} frames per class, GPU lookahead CRF)\n")
+    print(f"# Multi-content RD suite, {d.get('codec', 'h264').upper()} ({d['size']}, {d['slots']} segments x "
+          f"{d['frames']} frames per class, GPU lookahead CRF)\n")
     print("Content classes of csrc/kernels/synth.hip; PSNR-Y / SSIM-Y are per-frame means over every")
     print(f"segment; fps = the whole encode call of {d['slots']} segments (lookahead, encode, entropy).\n")
     print("| class | config | CRF | kb/s | PSNR-Y dB | SSIM-Y | B share | fps |")
@@ -110,6 +131,7 @@ def main():
     ap.add_argument("--size", default="1920x1080")
     ap.add_argument("--kinds", default="")
     ap.add_argument("--configs", default="")
+    ap.add_argument("--codec", default="h264", choices=("h264", "hevc"))
     args = ap.parse_args()
     run(args) if args.cmd == "run" else table(args)
 
