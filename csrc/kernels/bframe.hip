@@ -851,6 +851,7 @@ struct BSpatialExactArgs {
   const uint8_t* czero;   // [B, nmb] colZeroFlag bits (b_direct_mv)
   uint8_t* fix;           // [B, nmb] out: 1 = the direct motion changed, re-predict
   const SlotRoute* rt;
+  int slice_rows;         // MB rows per slice (0: one slice): no neighbours above a slice's first row
 };
 
 constexpr int kExactWaves = 5;  // one lane per MB row: 320 >= 8K's 270 rows
@@ -887,7 +888,8 @@ __global__ __launch_bounds__(64 * kExactWaves) void b_spatial_exact(BSpatialExac
           fin[qq][l] = (h.ref[l][qq] & 255) | ((h.mv[l][qq][0] & 4095) << 8) | (h.mv[l][qq][1] << 20);
       bool changed = false;
       if (!intra && sdir) {
-        const bool aA = x > 0, aB = y > 0, aC = y > 0 && x + 1 < wmb, aD = x > 0 && y > 0;
+        const bool top = y > 0 && (a.slice_rows <= 0 || y % a.slice_rows != 0);
+        const bool aA = x > 0, aB = top, aC = top && x + 1 < wmb, aD = x > 0 && top;
         int refs[2], pmv[2][2];
 #pragma unroll
         for (int l = 0; l < 2; ++l) {
@@ -1826,8 +1828,10 @@ extern "C" void mivc_launch_b_spatial(int B, int wmb, int hmb, void* hdr, const 
 }
 
 extern "C" void mivc_launch_b_spatial_exact(int B, int wmb, int hmb, void* hdr, const int* intra_cost, const int* cost,
-                                            const uint8_t* czero, uint8_t* fix, void* stream, const void* route) {
+                                            const uint8_t* czero, uint8_t* fix, void* stream, const void* route,
+                                            int slice_rows) {
   BSpatialExactArgs a;
+  a.slice_rows = slice_rows;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.hdr = static_cast<MbHeader*>(hdr);
   a.intra_cost = intra_cost;

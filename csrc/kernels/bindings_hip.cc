@@ -37,7 +37,7 @@ void mivc_launch_b_direct(int B, int wmb, int hmb, const void* col, const int* d
                           int16_t* dmv, int8_t* dref, int16_t* pm0, int16_t* pm1, void* stream, const void* route,
                           int nbuf, uint8_t* czero);
 void mivc_launch_b_spatial_exact(int B, int wmb, int hmb, void* hdr, const int* intra_cost, const int* cost,
-                                 const uint8_t* czero, uint8_t* fix, void* stream, const void* route);
+                                 const uint8_t* czero, uint8_t* fix, void* stream, const void* route, int slice_rows);
 void mivc_launch_b_spatial_fixup(int B, int wmb, int hmb, const void* hdr, const uint8_t* fix, const uint8_t* ref0,
                                  const uint8_t* hp0, const uint8_t* ref1, const uint8_t* hp1, uint8_t* pred_out,
                                  void* stream, const void* route, int nbuf);
@@ -155,7 +155,9 @@ int mivc_launch_hevc_prep_frame(int B, const void* sy, const void* su, const voi
                                 uint16_t* dv, uint8_t* d8, int W, int H, int shift, int bd, void* stream);
 int mivc_launch_hevc_proxy8(const uint16_t* src, uint8_t* dst, long long n, int shift, void* stream);
 int mivc_launch_lookahead(const uint8_t* y, int w, int h, long long fstride, int N, int F, uint8_t* low,
-                          unsigned long long* frame_cost, int* blk_cost, int* blk_mv, int range, void* stream);
+                          unsigned long long* frame_cost, int* blk_cost, int* blk_mv, int range, void* stream,
+                          uint8_t* low4, int* mv4, unsigned long long* cost4);
+long long mivc_lookahead_quarter_bytes(int w, int h, int N);
 }
 
 namespace {
@@ -257,13 +259,14 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("dmv"), py::arg("pm0"), py::arg("pm1"), py::arg("stream"), py::arg("dref") = 0, py::arg("route") = 0,
      py::arg("nbuf") = 0, py::arg("czero") = 0);
   m.def("b_spatial_exact", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t intra_cost, uintptr_t cost,
-                              uintptr_t czero, uintptr_t fix, uintptr_t stream, uintptr_t route) {
+                              uintptr_t czero, uintptr_t fix, uintptr_t stream, uintptr_t route, int slice_rows) {
     // spatial direct, fast path: the exact direct motion in decoding order (one lane per MB row)
     if (hmb > 320 || wmb > 480) throw std::invalid_argument("b_spatial_exact: at most 320 MB rows and 480 columns");
     if (!hdr || !intra_cost || !cost || !czero || !fix) throw std::invalid_argument("b_spatial_exact: null buffer");
     mivc_launch_b_spatial_exact(B, wmb, hmb, P<void>(hdr), P<int>(intra_cost), P<int>(cost), P<uint8_t>(czero),
-                                P<uint8_t>(fix), S(stream), P<void>(route));
-  });
+                                P<uint8_t>(fix), S(stream), P<void>(route), slice_rows);
+  }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("hdr"), py::arg("intra_cost"), py::arg("cost"),
+     py::arg("czero"), py::arg("fix"), py::arg("stream"), py::arg("route") = 0, py::arg("slice_rows") = 0);
   m.def("b_spatial_fixup", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t fix, uintptr_t ref0, uintptr_t hp0,
                               uintptr_t ref1, uintptr_t hp1, uintptr_t pred_out, uintptr_t stream, uintptr_t route,
                               int nbuf) {
@@ -670,6 +673,7 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("ry"), py::arg("ru"), py::arg("rv"), py::arg("sse"), py::arg("ssim"), py::arg("stream"),
      py::arg("route") = 0, py::arg("nbuf") = 0);
   m.def("lookahead_low_bytes", [](int w, int h, int n) { return mivc_lookahead_low_bytes(w, h, n); });
+  m.def("lookahead_quarter_bytes", [](int w, int h, int n) { return mivc_lookahead_quarter_bytes(w, h, n); });
   m.def("lookahead_multi", [](uintptr_t low, int w, int h, int n, int f, uintptr_t blk_cost, uintptr_t blk_mv, int D,
                               int range, uintptr_t out, uintptr_t stream) {
     const int r = mivc_launch_lookahead_multi(P<uint8_t>(low), w, h, n, f, P<int>(blk_cost), P<int>(blk_mv), D, range,
@@ -677,11 +681,13 @@ PYBIND11_MODULE(_hip, m) {
     if (r != 0) throw std::invalid_argument("lookahead_multi: bad arguments (" + std::to_string(r) + ")");
   });
   m.def("lookahead", [](uintptr_t y, int w, int h, long long fstride, int n, int f, uintptr_t low, uintptr_t frame_cost,
-                        uintptr_t blk_cost, int range, uintptr_t stream, uintptr_t blk_mv) {
+                        uintptr_t blk_cost, int range, uintptr_t stream, uintptr_t blk_mv, uintptr_t low4, uintptr_t mv4,
+                        uintptr_t cost4) {
     int rc = mivc_launch_lookahead(P<uint8_t>(y), w, h, fstride, n, f, P<uint8_t>(low),
                                    P<unsigned long long>(frame_cost), P<int>(blk_cost), P<int>(blk_mv), range,
-                                   S(stream));
+                                   S(stream), P<uint8_t>(low4), P<int>(mv4), P<unsigned long long>(cost4));
     if (rc != 0) throw std::invalid_argument("lookahead: bad geometry or range (4, 6, 8)");
   }, py::arg("y"), py::arg("w"), py::arg("h"), py::arg("fstride"), py::arg("n"), py::arg("f"), py::arg("low"),
-     py::arg("frame_cost"), py::arg("blk_cost"), py::arg("range"), py::arg("stream"), py::arg("blk_mv") = 0);
+     py::arg("frame_cost"), py::arg("blk_cost"), py::arg("range"), py::arg("stream"), py::arg("blk_mv") = 0,
+     py::arg("low4") = 0, py::arg("mv4") = 0, py::arg("cost4") = 0);
 }

@@ -121,7 +121,99 @@ struct LaArgs {
   unsigned long long* frame_cost;  // [N, 2]: sum intra, sum min(intra, inter)
   int* blk_cost;                   // optional [N, 2, lbh, lbw]: intra, inter (inter = intra on key frames)
   int* blk_mv;                     // optional [N, lbh, lbw]: lowres integer vector (dx & 0xFFFF) | (dy << 16)
+  // hierarchical search (optional): [N, cbh, cbw] quarter-resolution vectors (la_cost on the
+  // quarter planes); lowres block (bx, by) searches around twice the vector of its quarter
+  // block (bx / 2, by / 2) instead of around zero, and keeps the zero vector as a candidate
+  const int* center;
+  int cbw, cbs;  // quarter blocks per row / per frame
 };
+
+// Quarter-resolution planes from the lowres ones (2x2 box of the lowres interior, replicated
+// border): the coarse level of the hierarchical lookahead search.  q: the quarter geometry
+// (q.w x q.h = the lowres size).
+__global__ void la_downscale_low(const uint8_t* __restrict__ low, LaGeom g, LaGeom q, uint8_t* __restrict__ low4) {
+  const long long total = static_cast<long long>(q.N) * q.lsize;
+  const long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int n = static_cast<int>(i / q.lsize);
+  const int rem = static_cast<int>(i - static_cast<long long>(n) * q.lsize);
+  const int py = rem / q.ls, px = rem - py * q.ls;
+  const int qw = q.w >> 1, qh = q.h >> 1;
+  const int ly = clampi(py - kLaPad, 0, qh - 1), lx = clampi(px - kLaPad, 0, qw - 1);
+  const uint8_t* sp = low + n * g.lsize + static_cast<long long>(kLaPad + 2 * ly) * g.ls + kLaPad + 2 * lx;
+  low4[i] = static_cast<uint8_t>((sp[0] + sp[1] + sp[g.ls] + sp[g.ls + 1] + 2) >> 2);
+}
+
+// 8 lowres bytes of rows (y, y + 1) at column x (any alignment) as MFMA B-operand bytes
+__device__ __forceinline__ v4i la_rows8(const uint8_t* plane, long long ls, int x, int y) {
+  const int xa = x & ~3, sh = x & 3;
+  const uint32_t* q0 = reinterpret_cast<const uint32_t*>(plane + static_cast<long long>(y) * ls + xa);
+  const uint32_t* q1 = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(q0) + ls);
+  const uint32_t e0 = q0[0], e1 = q0[1], e2 = q0[2], f0 = q1[0], f1 = q1[1], f2 = q1[2];
+  return as_s8(__builtin_amdgcn_alignbyte(e1, e0, sh), __builtin_amdgcn_alignbyte(e2, e1, sh),
+               __builtin_amdgcn_alignbyte(f1, f0, sh), __builtin_amdgcn_alignbyte(f2, f1, sh));
+}
+
+// raw 8 bytes of rows (y, y + 1) at column x (the four dwords of la_rows8 before the bias)
+__device__ __forceinline__ uint4 la_raw8(const uint8_t* plane, long long ls, int x, int y) {
+  const int xa = x & ~3, sh = x & 3;
+  const uint32_t* q0 = reinterpret_cast<const uint32_t*>(plane + static_cast<long long>(y) * ls + xa);
+  const uint32_t* q1 = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(q0) + ls);
+  const uint32_t e0 = q0[0], e1 = q0[1], e2 = q0[2], f0 = q1[0], f1 = q1[1], f2 = q1[2];
+  return make_uint4(__builtin_amdgcn_alignbyte(e1, e0, sh), __builtin_amdgcn_alignbyte(e2, e1, sh),
+                    __builtin_amdgcn_alignbyte(f1, f0, sh), __builtin_amdgcn_alignbyte(f2, f1, sh));
+}
+
+// (2R+1)^2 integer search around (cx, cy) (clamped so the window stays inside the padded
+// plane); returns the best offset (SAD + 2 |offset from the centre|), the lane holding its
+// two rows of the block's column
+template <int R>
+__device__ __forceinline__ void la_small_search(const uint8_t* ref, const LaGeom& g, int X0, int ry, uint2 s0, uint2 s1,
+                                                int cx, int cy, int& bx, int& by) {
+  constexpr int side = 2 * R + 1;
+  // the window's 7 aligned dwords per row (from x0 & ~3) and its rows stay inside the plane
+  const int Yb = ry & ~7;  // the block's top row
+  cx = clampi(cx, R - X0, g.ls - 28 - X0 + R);
+  cy = clampi(cy, R - Yb, g.lrows - 8 - R - Yb);
+  const int x0 = X0 + cx - R;
+  const int xa = x0 & ~3, s = x0 & 3;
+  int best = 0x7FFFFFFF;
+  for (int dy = -R; dy <= R; ++dy) {
+    const uint32_t* p0 = reinterpret_cast<const uint32_t*>(ref + static_cast<long long>(ry + cy + dy) * g.ls + xa);
+    const uint32_t* p1 = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(p0) + g.ls);
+    uint32_t w0[6], w1[6];
+    {
+      uint32_t t0[7], t1[7];
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        t0[k] = p0[k];
+        t1[k] = p1[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {  // realign: w starts at column x0
+        w0[k] = __builtin_amdgcn_alignbyte(t0[k + 1], t0[k], s);
+        w1[k] = __builtin_amdgcn_alignbyte(t1[k + 1], t1[k], s);
+      }
+    }
+#pragma unroll
+    for (int dx = -R; dx <= R; ++dx) {
+      const int o = R + dx, wi = o >> 2, sh = o & 3;
+      const uint32_t a0 = __builtin_amdgcn_alignbyte(w0[wi + 1], w0[wi], sh);
+      const uint32_t a1 = __builtin_amdgcn_alignbyte(w0[wi + 2], w0[wi + 1], sh);
+      const uint32_t b0 = __builtin_amdgcn_alignbyte(w1[wi + 1], w1[wi], sh);
+      const uint32_t b1 = __builtin_amdgcn_alignbyte(w1[wi + 2], w1[wi + 1], sh);
+      uint32_t sad = sad4(s0.x, a0, 0);
+      sad = sad4(s0.y, a1, sad);
+      sad = sad4(s1.x, b0, sad);
+      sad = sad4(s1.y, b1, sad);
+      const int cost = sum_col_groups(static_cast<int>(sad)) + 2 * (abs(dx) + abs(dy));
+      best = min(best, (cost << 9) | ((dy + R) * side + (dx + R)));
+    }
+  }
+  const int bi = best & 511;
+  bx = cx + bi % side - R;
+  by = cy + bi / side - R;
+}
 
 template <int R>
 __global__ __launch_bounds__(256) void la_cost(LaArgs a) {
@@ -193,7 +285,18 @@ __global__ __launch_bounds__(256) void la_cost(LaArgs a) {
 
   int inter = intra;
   int mvx = 0, mvy = 0;
-  if (has_ref) {  // frame-uniform
+  if (has_ref && a.center) {  // frame-uniform: hierarchical search around the coarse vector
+    const uint8_t* ref = cur - g.lsize;
+    const int cv = a.center[static_cast<long long>(n) * a.cbs + (by >> 1) * a.cbw + (bxc >> 1)];
+    const int cx = 2 * static_cast<int16_t>(cv & 0xFFFF), cy = 2 * (cv >> 16);
+    int mx, my;
+    la_small_search<R>(ref, g, X0, ry, s0, s1, cx, cy, mx, my);
+    const int cst = satd_mfma(negH, accS, la_rows8(ref, g.ls, X0 + mx, ry + my)) + 2 * (abs(mx) + abs(my));
+    const int c0 = satd_mfma(negH, accS, la_rows8(ref, g.ls, X0, ry));
+    inter = min(cst, c0);
+    mvx = cst < c0 ? mx : 0;
+    mvy = cst < c0 ? my : 0;
+  } else if (has_ref) {  // frame-uniform
     const uint8_t* ref = cur - g.lsize;
     // ---- integer full search: lane accumulates the SAD of its two rows, then the column sum
     int best = 0x7FFFFFFF;
@@ -274,77 +377,6 @@ struct LaMultiArgs {
   int D;                // largest P distance (bframes + 1), <= kLaMultiCols - 1
   unsigned long long* out;  // [N, kLaMultiCols]
 };
-
-// 8 lowres bytes of rows (y, y + 1) at column x (any alignment) as MFMA B-operand bytes
-__device__ __forceinline__ v4i la_rows8(const uint8_t* plane, long long ls, int x, int y) {
-  const int xa = x & ~3, sh = x & 3;
-  const uint32_t* q0 = reinterpret_cast<const uint32_t*>(plane + static_cast<long long>(y) * ls + xa);
-  const uint32_t* q1 = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(q0) + ls);
-  const uint32_t e0 = q0[0], e1 = q0[1], e2 = q0[2], f0 = q1[0], f1 = q1[1], f2 = q1[2];
-  return as_s8(__builtin_amdgcn_alignbyte(e1, e0, sh), __builtin_amdgcn_alignbyte(e2, e1, sh),
-               __builtin_amdgcn_alignbyte(f1, f0, sh), __builtin_amdgcn_alignbyte(f2, f1, sh));
-}
-
-// raw 8 bytes of rows (y, y + 1) at column x (the four dwords of la_rows8 before the bias)
-__device__ __forceinline__ uint4 la_raw8(const uint8_t* plane, long long ls, int x, int y) {
-  const int xa = x & ~3, sh = x & 3;
-  const uint32_t* q0 = reinterpret_cast<const uint32_t*>(plane + static_cast<long long>(y) * ls + xa);
-  const uint32_t* q1 = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(q0) + ls);
-  const uint32_t e0 = q0[0], e1 = q0[1], e2 = q0[2], f0 = q1[0], f1 = q1[1], f2 = q1[2];
-  return make_uint4(__builtin_amdgcn_alignbyte(e1, e0, sh), __builtin_amdgcn_alignbyte(e2, e1, sh),
-                    __builtin_amdgcn_alignbyte(f1, f0, sh), __builtin_amdgcn_alignbyte(f2, f1, sh));
-}
-
-// (2R+1)^2 integer search around (cx, cy) (clamped so the window stays inside the padded
-// plane); returns the best offset (SAD + 2 |offset from the centre|), the lane holding its
-// two rows of the block's column
-template <int R>
-__device__ __forceinline__ void la_small_search(const uint8_t* ref, const LaGeom& g, int X0, int ry, uint2 s0, uint2 s1,
-                                                int cx, int cy, int& bx, int& by) {
-  constexpr int side = 2 * R + 1;
-  // the window's 7 aligned dwords per row (from x0 & ~3) and its rows stay inside the plane
-  const int Yb = ry & ~7;  // the block's top row
-  cx = clampi(cx, R - X0, g.ls - 28 - X0 + R);
-  cy = clampi(cy, R - Yb, g.lrows - 8 - R - Yb);
-  const int x0 = X0 + cx - R;
-  const int xa = x0 & ~3, s = x0 & 3;
-  int best = 0x7FFFFFFF;
-  for (int dy = -R; dy <= R; ++dy) {
-    const uint32_t* p0 = reinterpret_cast<const uint32_t*>(ref + static_cast<long long>(ry + cy + dy) * g.ls + xa);
-    const uint32_t* p1 = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(p0) + g.ls);
-    uint32_t w0[6], w1[6];
-    {
-      uint32_t t0[7], t1[7];
-#pragma unroll
-      for (int k = 0; k < 7; ++k) {
-        t0[k] = p0[k];
-        t1[k] = p1[k];
-      }
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {  // realign: w starts at column x0
-        w0[k] = __builtin_amdgcn_alignbyte(t0[k + 1], t0[k], s);
-        w1[k] = __builtin_amdgcn_alignbyte(t1[k + 1], t1[k], s);
-      }
-    }
-#pragma unroll
-    for (int dx = -R; dx <= R; ++dx) {
-      const int o = R + dx, wi = o >> 2, sh = o & 3;
-      const uint32_t a0 = __builtin_amdgcn_alignbyte(w0[wi + 1], w0[wi], sh);
-      const uint32_t a1 = __builtin_amdgcn_alignbyte(w0[wi + 2], w0[wi + 1], sh);
-      const uint32_t b0 = __builtin_amdgcn_alignbyte(w1[wi + 1], w1[wi], sh);
-      const uint32_t b1 = __builtin_amdgcn_alignbyte(w1[wi + 2], w1[wi + 1], sh);
-      uint32_t sad = sad4(s0.x, a0, 0);
-      sad = sad4(s0.y, a1, sad);
-      sad = sad4(s1.x, b0, sad);
-      sad = sad4(s1.y, b1, sad);
-      const int cost = sum_col_groups(static_cast<int>(sad)) + 2 * (abs(dx) + abs(dy));
-      best = min(best, (cost << 9) | ((dy + R) * side + (dx + R)));
-    }
-  }
-  const int bi = best & 511;
-  bx = cx + bi % side - R;
-  by = cy + bi / side - R;
-}
 
 template <int R>
 __global__ __launch_bounds__(256) void la_multi(LaMultiArgs a) {
@@ -443,9 +475,19 @@ extern "C" long long mivc_lookahead_low_bytes(int w, int h, int N) {
 // y: luma of N = B*F frames (slot-major), frame f of slot b at y + (b*F + f) * fstride.
 // low: workspace of mivc_lookahead_low_bytes(); frame_cost: [N, 2] u64 (zeroed here);
 // blk_cost: optional [N, 2, lbh, lbw] int32.
+// Hierarchical (low4 / mv4 / cost4 non-null): quarter-resolution planes of the lowres ones,
+// an integer full search +-8 there (= +-32 full-resolution pixels) into mv4, and the lowres
+// search centred on twice those vectors.  low4: mivc_lookahead_quarter_bytes(); mv4:
+// [N, cbh, cbw] int32 with cbw x cbh the quarter 8x8 blocks; cost4: [N, 2] u64 scratch.
+extern "C" long long mivc_lookahead_quarter_bytes(int w, int h, int N) {
+  const int qw = (w >> 1) & ~1, qh = (h >> 1) & ~1;
+  const int qbw = ((qw >> 1) + 7) >> 3, qbh = ((qh >> 1) + 7) >> 3;
+  return static_cast<long long>(N) * (qbw * 8 + 2 * kLaPad) * (qbh * 8 + 2 * kLaPad);
+}
+
 extern "C" int mivc_launch_lookahead(const uint8_t* y, int w, int h, long long fstride, int N, int F, uint8_t* low,
                                      unsigned long long* frame_cost, int* blk_cost, int* blk_mv, int range,
-                                     void* stream) {
+                                     void* stream, uint8_t* low4, int* mv4, unsigned long long* cost4) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (w < 16 || h < 16 || (w & 1) || (h & 1) || N <= 0 || F <= 0 || N % F) return -1;
   if (range != 4 && range != 6 && range != 8) return -2;
@@ -463,7 +505,30 @@ extern "C" int mivc_launch_lookahead(const uint8_t* y, int w, int h, long long f
   hipMemsetAsync(frame_cost, 0, sizeof(unsigned long long) * 2 * N, s);
   const long long dwords = static_cast<long long>(N) * g.lrows * (g.ls >> 2);
   hipLaunchKernelGGL(la_downscale, dim3(static_cast<unsigned>((dwords + 255) / 256)), dim3(256), 0, s, y, g, low);
-  LaArgs a{g, low, frame_cost, blk_cost, blk_mv};
+  LaArgs a{g, low, frame_cost, blk_cost, blk_mv, nullptr, 0, 0};
+  if (low4 && mv4 && cost4 && w >= 64 && h >= 64) {
+    LaGeom q{};
+    q.w = (w >> 1) & ~1;
+    q.h = (h >> 1) & ~1;
+    q.fstride = 0;
+    q.N = N;
+    q.F = F;
+    q.lbw = ((q.w >> 1) + 7) >> 3;
+    q.lbh = ((q.h >> 1) + 7) >> 3;
+    q.ls = q.lbw * 8 + 2 * kLaPad;
+    q.lrows = q.lbh * 8 + 2 * kLaPad;
+    q.lsize = static_cast<long long>(q.ls) * q.lrows;
+    const long long qbytes = static_cast<long long>(N) * q.lsize;
+    hipLaunchKernelGGL(la_downscale_low, dim3(static_cast<unsigned>((qbytes + 255) / 256)), dim3(256), 0, s, low, g, q,
+                       low4);
+    hipMemsetAsync(cost4, 0, sizeof(unsigned long long) * 2 * N, s);
+    LaArgs aq{q, low4, cost4, nullptr, mv4, nullptr, 0, 0};
+    const long long qwaves = static_cast<long long>((q.lbw + 15) >> 4) * q.lbh * N;
+    hipLaunchKernelGGL(la_cost<8>, dim3(static_cast<unsigned>((qwaves + 3) >> 2)), dim3(256), 0, s, aq);
+    a.center = mv4;
+    a.cbw = q.lbw;
+    a.cbs = q.lbw * q.lbh;
+  }
   const long long waves = static_cast<long long>((g.lbw + 15) >> 4) * g.lbh * N;
   const dim3 grid(static_cast<unsigned>((waves + 3) >> 2));
   switch (range) {

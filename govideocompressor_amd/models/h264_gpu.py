@@ -83,6 +83,8 @@ class H264Params:
     # x264 --b-adapt: 1 (its default, "fast") places B pictures per slot from the lookahead's
     # lowres costs (rc/badapt.py, lookahead.hip la_multi); 0 = the fixed pattern
     b_adapt: int = int(os.environ.get("MIVC_B_ADAPT", 1))
+    # x264 --b-bias: > 0 places more B pictures (B costs * 100 / (120 + bias), run thresholds)
+    b_bias: int = int(os.environ.get("MIVC_B_BIAS", 0))
     # x264 seeds its motion search from the lookahead's lowres motion: the P search and both B
     # searches get one more candidate, the picture's lowres vector x 2 scaled to its reference
     # distance (when the lookahead ran on the coded MB grid)
@@ -173,8 +175,7 @@ class H264Params:
     # slices per picture (x264 --slices): whole MB rows each.  The GPU arithmetic coder codes
     # one slice per lane, so S slices give S times the independent serial chains per picture
     # (and the intra wavefront restarts at every slice); each slice costs a header and the
-    # prediction across its top edge.  CABAC only; temporal direct only (spatial direct's
-    # neighbour derivation is not slice-aware).
+    # prediction across its top edge.  CABAC only (spatial direct: the fast path).
     slices: int = int(os.environ.get("MIVC_SLICES", 1))
 
     def slice_rows(self) -> int:
@@ -305,8 +306,8 @@ class GpuH264Encoder:
             raise ValueError("b-pyramid needs spatial direct prediction (direct='spatial')")
         if entropy not in ("gpu", "cpu"):
             raise ValueError("entropy must be 'gpu' or 'cpu'")
-        if params.eff_slices() > 1 and params.direct == "spatial" and params.eff_bframes():
-            raise ValueError("slices > 1 need temporal direct (the spatial direct kernels are not slice-aware)")
+        if params.eff_slices() > 1 and params.direct == "spatial" and params.eff_bframes() and params.spatial_wavefront:
+            raise ValueError("slices > 1: spatial direct needs the fast path (spatial_wavefront=False)")
         self.entropy = entropy
         self.p = params
         self.slice_rows = params.slice_rows()
@@ -660,7 +661,7 @@ class GpuH264Encoder:
             if sfast:
                 with stt("b_spatial"):
                     self.hip.b_spatial_exact(B, wmb, hmb, P(hdr), P(self.intra_cost), P(self.cost_b), P(self.czero),
-                                             P(self.sfix), s, rt)
+                                             P(self.sfix), s, rt, self.slice_rows)
                     self.hip.b_spatial_fixup(B, wmb, hmb, P(hdr), P(self.sfix), py, hpp, py, hpp, P(self.pred_b), s,
                                              rt, NB)
             elif spatial:
@@ -724,7 +725,8 @@ class GpuH264Encoder:
             forced = {int(d) for d in anchors_at[b]} if per_slot else common
             forced = forced | {d for d in range(1, F) if cuts_h[b, d]}
             if adaptive:
-                ty = b_adapt_types(self._la_costs[b, :, 1], multi[b], multi[b, :, 0], self.nb, self._la_blocks, forced)
+                ty = b_adapt_types(self._la_costs[b, :, 1], multi[b], multi[b, :, 0], self.nb, self._la_blocks, forced,
+                                   int(self.p.b_bias))
             else:
                 ty = fixed_types(F, self.nb, forced)
             if ty not in cache:

@@ -30,11 +30,14 @@ B_COST_SCALE = 100.0 / 120.0  # x264 slicetype frame cost of a B frame, --b-bias
 
 
 def b_adapt_types(p1: np.ndarray, pd: np.ndarray, bcost: np.ndarray, bframes: int, mb_count: int,
-                  forced=()) -> str:
+                  forced=(), b_bias: int = 0) -> str:
     """Display-order picture types of one segment (``"IPBBP..."``).
 
     p1[f]: P cost of f from f - 1; pd[f, d]: P cost of f from f - d (d = 2..bframes + 1,
-    columns of la_multi); bcost[f]: B cost of f between f - 1 and f + 1."""
+    columns of la_multi); bcost[f]: B cost of f between f - 1 and f + 1.  ``b_bias``: x264
+    --b-bias (B costs scaled by 100 / (120 + b_bias), run threshold slope 50 - b_bias)."""
+    b_scale = 100.0 / (120.0 + b_bias)
+    sens = P_SENS_BIAS - b_bias
     F = len(p1)
     if F == 0:
         return ""
@@ -53,14 +56,14 @@ def b_adapt_types(p1: np.ndarray, pd: np.ndarray, bcost: np.ndarray, bframes: in
             i += 1  # i + 1 is an anchor (forced, or the last picture)
             continue
         keep_p = pcost(i + 1, 1) + pcost(i + 2, 1)
-        as_b = B_COST_SCALE * float(bcost[i + 1]) + pcost(i + 2, 2)
+        as_b = b_scale * float(bcost[i + 1]) + pcost(i + 2, 2)
         if keep_p < as_b:
             i += 1
             continue
         types[i + 1] = "B"
         j = i + 2
         while j <= min(i + bframes, F - 2) and j not in forced:
-            pthresh = max(INTER_THRESH - P_SENS_BIAS * (j - i - 1), INTER_THRESH / 10)
+            pthresh = max(INTER_THRESH - sens * (j - i - 1), INTER_THRESH / 10)
             if j + 1 - i > bframes + 1 or pcost(j + 1, j + 1 - i) > pthresh * mb_count:
                 break
             types[j] = "B"
@@ -69,13 +72,15 @@ def b_adapt_types(p1: np.ndarray, pd: np.ndarray, bcost: np.ndarray, bframes: in
     return "".join(types)
 
 
-def b_adapt_batch(costs: np.ndarray, multi: np.ndarray, bframes: int, mb_count: int, forced_per_slot) -> list[str]:
+def b_adapt_batch(costs: np.ndarray, multi: np.ndarray, bframes: int, mb_count: int, forced_per_slot,
+                  b_bias: int = 0) -> list[str]:
     """Per-slot types of a batch: costs [B, F, 2] (la_cost frame sums: intra, min(intra,
     inter at distance 1)), multi [B, F, 8] (la_multi), forced_per_slot: one iterable per slot."""
     B = costs.shape[0]
     out = []
     for b in range(B):
-        out.append(b_adapt_types(costs[b, :, 1], multi[b], multi[b, :, 0], bframes, mb_count, forced_per_slot[b]))
+        out.append(b_adapt_types(costs[b, :, 1], multi[b], multi[b, :, 0], bframes, mb_count, forced_per_slot[b],
+                                 b_bias))
     return out
 
 

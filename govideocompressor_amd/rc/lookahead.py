@@ -22,9 +22,14 @@ RANGES = (4, 6, 8)
 class GpuLookahead:
     """Lowres cost analysis on gfx950 (workspace cached across calls)."""
 
-    def __init__(self, device: str | torch.device = "cuda", search_range: int = 6):
+    def __init__(self, device: str | torch.device = "cuda", search_range: int = 6, hierarchical: bool = True):
+        """``hierarchical``: search every lowres block around twice its quarter-resolution
+        block's vector (a +-8 full search at quarter resolution, +-32 full-resolution pixels)
+        instead of around zero -- fast pans, which the lowres window alone (+-2 * range
+        pixels) cannot follow, would otherwise look like scene cuts."""
         if search_range not in RANGES:
             raise ValueError(f"search_range must be one of {RANGES}")
+        self.hierarchical = bool(hierarchical)
         self.dev = torch.device(device)
         if self.dev.type == "cuda" and self.dev.index is None:
             self.dev = torch.device("cuda", torch.cuda.current_device())
@@ -88,9 +93,20 @@ class GpuLookahead:
             blk = torch.zeros((B, F, 2, lbh, lbw), dtype=torch.int32, device=self.dev)
         if block_mvs:
             mv = torch.zeros((B, F, lbh, lbw), dtype=torch.int32, device=self.dev)
+        low4 = mv4 = cost4 = 0
+        if self.hierarchical and w >= 64 and h >= 64:
+            qbytes = int(self.hip.lookahead_quarter_bytes(w, h, n))
+            qbw, qbh = ((((w >> 1) & ~1) >> 1) + 7) // 8, ((((h >> 1) & ~1) >> 1) + 7) // 8
+            if getattr(self, "_low4", None) is None or self._low4.numel() < qbytes:
+                self._low4 = torch.empty((qbytes,), dtype=torch.uint8, device=self.dev)
+            if getattr(self, "_mv4", None) is None or self._mv4.numel() < n * qbw * qbh:
+                self._mv4 = torch.empty((n * qbw * qbh,), dtype=torch.int32, device=self.dev)
+                self._cost4 = torch.empty((n, 2), dtype=torch.int64, device=self.dev)
+            low4, mv4, cost4 = self._low4.data_ptr(), self._mv4.data_ptr(), self._cost4.data_ptr()
         self.hip.lookahead(y.data_ptr(), w, h, y.stride(1), n, F, low.data_ptr(), cost.data_ptr(),
                            blk.data_ptr() if blk is not None else 0, self.range,
-                           torch.cuda.current_stream(self.dev).cuda_stream, mv.data_ptr() if mv is not None else 0)
+                           torch.cuda.current_stream(self.dev).cuda_stream, mv.data_ptr() if mv is not None else 0,
+                           low4, mv4, cost4)
         out = cost.view(B, F, 2)
         if block_mvs:
             return out, blk, mv

@@ -110,24 +110,43 @@ def crf_qps(intra: np.ndarray, inter: np.ndarray, crf: float, mb_count: int, key
     return np.array([clamp_qp(q) for q in qp], dtype=np.int32)
 
 
-def scenecut_flags(costs: np.ndarray, scenecut: float = 40.0, keyint: int | None = None) -> np.ndarray:
+def scenecut_flags(costs: np.ndarray, scenecut: float = 40.0, keyint: int | None = None,
+                   keyint_max: int = 250, keyint_min: int | None = None) -> np.ndarray:
     """[B, F] scene-cut decisions from lowres frame costs (x264 ``--scenecut``, default 40).
 
-    Frame t of a segment is a scene cut when motion compensation from t - 1 saves less
-    than ``scenecut`` percent of its intra cost: ``cost_best >= (1 - scenecut / 100) *
-    cost_intra`` with ``cost_best = sum of per-block min(intra, inter)`` (x264 compares the
-    P cost with the I cost of the candidate frame the same way, slicetype.c
-    ``scenecut_internal``).  Key frames (frame 0, every ``keyint``-th) are not flagged:
-    they are intra already.  ``scenecut <= 0`` disables detection."""
+    x264 (slicetype.c ``scenecut_internal``) flags frame t when its P cost from t - 1 is
+    ``pcost >= (1 - bias) * icost`` (``cost_best = sum of per-block min(intra, inter)``,
+    ``icost`` the intra sum), with a bias that grows with the distance from the last key
+    frame: ``thresh_max = scenecut / 100``, ``thresh_min = thresh_max / 4``; up to
+    keyint_min / 4 frames after a key frame ``bias = thresh_min / 4``, up to keyint_min
+    ``thresh_min * gop / keyint_min``, then linear up to thresh_max at keyint_max.  So a cut
+    right after a key frame needs the inter prediction to save almost nothing (x264's
+    defaults: keyint 250, keyint_min = min(250 / 10, fps) = 25).  Key frames (frame 0, every
+    ``keyint``-th) are not flagged; a flagged frame restarts the distance.  ``scenecut <= 0``
+    disables detection."""
     c = np.asarray(costs, dtype=np.float64)
     B, F = c.shape[0], c.shape[1]
     flags = np.zeros((B, F), dtype=bool)
     if scenecut <= 0 or F < 2:
         return flags
     intra, best = c[:, :, 0], c[:, :, 1]
-    flags = best >= (1.0 - scenecut / 100.0) * np.maximum(intra, 1.0)
+    tmax = scenecut / 100.0
+    tmin = tmax * 0.25
+    kmax = int(keyint) if keyint and keyint > 0 else int(keyint_max)
+    kmin = int(keyint_min) if keyint_min else max(1, min(kmax // 10, 25))
     g = keyint if keyint and keyint > 0 else F
-    flags[:, ::g] = False
+    last = np.zeros(B, dtype=np.int64)
+    for t in range(1, F):
+        if t % g == 0:
+            last[:] = t
+            continue
+        gop = t - last
+        bias = np.where(gop <= kmin / 4, tmin / 4,
+                        np.where(gop <= kmin, tmin * gop / kmin,
+                                 tmin + (tmax - tmin) * (gop - kmin) / max(1, kmax - kmin)))
+        cut = best[:, t] >= (1.0 - bias) * np.maximum(intra[:, t], 1.0)
+        flags[:, t] = cut
+        last[cut] = t
     return flags
 
 

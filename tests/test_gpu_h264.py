@@ -476,3 +476,16 @@ def test_gpu_h264_slices_roundtrip(host, entropy):
     for r in res:
         for nal in r.nals:
             assert nal.count(b"\x00\x00\x01") == 4   # four slice NAL units per picture
+
+
+def test_gpu_h264_slices_spatial_direct_roundtrip(host):
+    """Spatial direct over slices: the exact decoding-order derivation (b_spatial_exact) treats a
+    slice's first MB row as having no neighbours above, as the decoder does."""
+    import torch
+    from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
+    p = H264Params(width=352, height=288, crf=24.0, slices=3, direct="spatial")
+    enc = GpuH264Encoder(p, slots=2)
+    y, u, v = synth_clip(2, 9, 352, 288, seed=12)
+    res = enc.encode(y, u, v, keep_recon=True)
+    torch.cuda.synchronize()
+    _check_roundtrip(host, enc, res, 352, 288)

@@ -62,7 +62,7 @@ def test_lookahead_matches_reference(R, shape):
 
     B, F, h, w = shape
     y = _clip(B, F, h, w, seed=R * 10 + w)
-    la = GpuLookahead("cuda:0", search_range=R)
+    la = GpuLookahead("cuda:0", search_range=R, hierarchical=False)
     yd = torch.from_numpy(y).to("cuda:0")
     frame, blk = la.frame_costs(yd, block_costs=True)
     torch.cuda.synchronize()
@@ -126,7 +126,7 @@ def test_mbtree_matches_reference():
     from govideocompressor_amd.rc.lookahead import GpuLookahead
 
     y, _, _ = synth_clip(2, 5, 160, 96, seed=3, device="cuda:0")
-    la = GpuLookahead("cuda:0", 6)
+    la = GpuLookahead("cuda:0", 6, hierarchical=False)
     _, blk, mv = la.frame_costs(y, block_costs=True, block_mvs=True)
     _, off = la.mbtree(y, 2.0)
     torch.cuda.synchronize()
@@ -146,10 +146,40 @@ def test_lookahead_multi_matches_reference(shape):
     from govideocompressor_amd.rc.lookahead import GpuLookahead, multi_reference
 
     y = _clip(*shape, seed=11)
-    la = GpuLookahead("cuda", 6)
+    la = GpuLookahead("cuda", 6, hierarchical=False)
     yd = torch.from_numpy(y).cuda()
     _, blk, mv = la.frame_costs(yd, block_costs=True, block_mvs=True)
     got = la.multi_costs(yd, blk, mv, 4).cpu().numpy()
     ref = multi_reference(y, 6, 4)
     assert np.array_equal(got, ref), (got[..., :5], ref[..., :5])
     assert (ref[:, 2:, 2] > 0).all() and (ref[:, 1:-1, 0] > 0).all()
+
+
+@pytest.mark.gpu
+def test_hierarchical_lookahead_follows_fast_pans():
+    """A texture panning 24 px / frame (12 lowres px, twice the lowres window of 6): the
+    quarter-resolution search finds the motion, the lowres vectors follow it and inter costs
+    stay far below intra; the window-only search cannot and prices the frames as new scenes."""
+    import torch
+    from govideocompressor_amd.rc.lookahead import GpuLookahead
+
+    rng = np.random.default_rng(3)
+    tex = rng.integers(0, 256, (40, 120)).astype(np.float64)
+    tex = np.kron(tex, np.ones((4, 4)))  # 4-pixel texels: coarse enough to survive the downscales
+    tex = (tex + np.roll(tex, 1, 0) + np.roll(tex, 1, 1)) / 3
+    B, F, h, w = 1, 4, 128, 256
+    y = np.stack([tex[:h, 24 * t:24 * t + w] for t in range(F)])[None].astype(np.uint8)
+    yd = torch.from_numpy(np.ascontiguousarray(y)).cuda()
+    out = {}
+    for hier in (False, True):
+        la = GpuLookahead("cuda", 6, hierarchical=hier)
+        cost, blk, mv = la.frame_costs(yd, block_costs=True, block_mvs=True)
+        torch.cuda.synchronize()
+        c = cost.cpu().numpy()[0]
+        m = mv.cpu().numpy()[0]
+        dx = ((m & 0xFFFF) ^ 0x8000) - 0x8000
+        out[hier] = (c[1:, 1].sum() / c[1:, 0].sum(), np.median(dx[1:, 2:-2, 2:-4]))
+    ratio_h, dx_h = out[True]
+    assert dx_h == 12, out          # frame t matches frame t - 1 twelve lowres pixels to the right
+    assert ratio_h < 0.35, out      # inter prediction works
+    assert out[False][0] > 2 * ratio_h, out

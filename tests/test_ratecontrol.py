@@ -48,7 +48,8 @@ def test_scenecut_flags_and_keyframe_qps():
     costs = np.zeros((B, F, 2))
     costs[:, :, 0] = 1000.0          # intra cost
     costs[:, :, 1] = 200.0           # inter predicts well ...
-    costs[0, 3, 1] = 950.0           # ... except at a cut in slot 0, frame 3
+    costs[0, 3, 1] = 990.0           # ... except at a cut in slot 0, frame 3
+    costs[1, 3, 1] = 950.0           # saving 5 % right after a key frame is no cut (x264 bias 0.025)
     costs[1, 0, 1] = 1000.0          # frame 0 is a key frame anyway: never flagged
     f = rc.scenecut_flags(costs, 40.0)
     assert f.tolist() == [[False, False, False, True, False, False], [False] * 6]
@@ -57,3 +58,17 @@ def test_scenecut_flags_and_keyframe_qps():
     q0 = rc.crf_qps_batch(costs, 23.0, 100)
     assert q[0, 3] < q0[0, 3]        # intra complexity and the I-frame offset at the cut
     assert (q[1] == q0[1]).all()
+
+
+def test_scenecut_bias_grows_with_the_distance_from_the_key_frame():
+    """x264 scenecut_internal: 50 frames after the key frame (past keyint_min 25) the bias is
+    0.1 + 0.3 * 25 / 225 = 0.133: a frame whose inter prediction saves 10 % is a cut there,
+    one saving 15 % is not; 5 frames in, neither is."""
+    costs = np.zeros((1, 60, 2))
+    costs[..., 0] = 1000.0
+    costs[..., 1] = 300.0
+    costs[0, 50, 1] = 900.0
+    costs[0, 55, 1] = 850.0
+    costs[0, 5, 1] = 900.0
+    f = rc.scenecut_flags(costs, 40.0)
+    assert f[0, 50] and not f[0, 55] and not f[0, 5]

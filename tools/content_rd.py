@@ -34,6 +34,10 @@ CONFIGS = {
     "badapt": dict(b_adapt=1, pyramid=False, direct="temporal"),
     "spatial": dict(b_adapt=1, pyramid=False, direct="spatial"),
     "pyramid": dict(b_adapt=1, pyramid=True, direct="spatial"),
+    "bias20": dict(b_adapt=1, b_bias=20),
+    "bias40": dict(b_adapt=1, b_bias=40),
+    "slices4": dict(slices=4),
+    "noseed": dict(lowres_seed=False),
     "default": dict(),  # the current defaults
 }
 # HEVC (GpuHevcEncoder) configurations: x265 --signhide, --bframes variants
