@@ -438,7 +438,9 @@ def test_gpu_h264_pyramid_spatial_roundtrip_b8x8(host):
     """b-pyramid with spatial direct at the default partitions (B_8x8 with direct quadrants):
     the co-located picture of the non-reference B pictures is a reference B, whose list-1-only
     blocks give their list-1 motion to colZeroFlag (8.4.1.2.1) -- bit-exact vs the CPU decoder."""
-    enc, res, _ = _run(352, 288, slots=2, frames=17, crf=24, bframes=3, refs=3, pyramid=True, direct="spatial")
+    # b-adapt 0: x264's fixed pattern, so the runs of 3 B pictures (and their reference B) occur
+    enc, res, _ = _run(352, 288, slots=2, frames=17, crf=24, bframes=3, refs=3, pyramid=True, direct="spatial",
+                       b_adapt=0)
     _check_roundtrip(host, enc, res, 352, 288)
     assert any(q.kind == "B" and q.ref for q in enc.last_plans[0])
     enc.close()
