@@ -80,9 +80,13 @@ class H264Params:
     # offset (6 log2 1.3 = 2.27) over the distance-weighted QP of the B picture's references
     bframes: int = 3
     b_qp_offset: float = 6.0 * math.log2(1.3)
-    # x264 --b-adapt: 1 (its default, "fast") places B pictures per slot from the lookahead's
-    # lowres costs (rc/badapt.py, lookahead.hip la_multi); 0 = the fixed pattern
-    b_adapt: int = int(os.environ.get("MIVC_B_ADAPT", 1))
+    # x264 --b-adapt: 1 ("fast", x264's default) places B pictures per slot from the lookahead's
+    # lowres costs (rc/badapt.py, lookahead.hip la_multi); 0 = the fixed pattern.  Measured
+    # over the seven content classes (profiles/r4_content_rd.md): x264's rule on these lowres
+    # costs (integer-pel, no lowres weighting) places too few B pictures for this encoder,
+    # whose B pictures are cheap -- +10 % BD-rate against the fixed pattern (+6 % at
+    # --b-bias 40), a gain on fast pans only -- so the fixed pattern is the default
+    b_adapt: int = int(os.environ.get("MIVC_B_ADAPT", 0))
     # x264 --b-bias: > 0 places more B pictures (B costs * 100 / (120 + bias), run thresholds)
     b_bias: int = int(os.environ.get("MIVC_B_BIAS", 0))
     # x264 seeds its motion search from the lookahead's lowres motion: the P search and both B
