@@ -343,6 +343,7 @@ hevc::HevcConfig hevc_cfg_from(const py::dict& d) {
   c.tmvp = dget<int>(d, "tmvp", 0);
   c.pyramid = dget<int>(d, "pyramid", 0);
   c.ctu64 = dget<int>(d, "ctu64", 0);
+  c.weightp = dget<int>(d, "weightp", 0);
   if (c.tu_inter_depth < 0 || c.tu_inter_depth > 1) throw std::runtime_error("HEVC: tu_inter_depth in 0..1");
   if (c.threads < 1 || c.threads > 256) throw std::runtime_error("HEVC: threads in 1..256");
   if (c.width <= 0 || c.height <= 0 || (c.width & 1) || (c.height & 1)) throw std::runtime_error("HEVC: bad size");
@@ -537,6 +538,17 @@ hevc::HevcFrameParams hevc_frame_from(const py::dict& fp, std::vector<py::array>
       const py::tuple e = l[i].cast<py::tuple>();
       f.rps_poc[i] = e[0].cast<int>();
       f.rps_used[i] = static_cast<uint8_t>(e[1].cast<int>() ? 1 : 0);
+    }
+  }
+  if (fp.contains("wp") && !fp["wp"].is_none()) {  // [w_y, o_y, w_cb, o_cb, w_cr, o_cr]
+    const py::list l = fp["wp"].cast<py::list>();
+    if (l.size() != 6) throw std::runtime_error("wp: 6 entries (weight, offset per component)");
+    f.wp = 1;
+    for (int c = 0; c < 3; ++c) {
+      f.wp_w[c] = l[2 * c].cast<int>();
+      f.wp_o[c] = l[2 * c + 1].cast<int>();
+      if (f.wp_w[c] < -64 || f.wp_w[c] > 191 || f.wp_o[c] < -128 || f.wp_o[c] > 127)
+        throw std::runtime_error("wp: weight in -64..191, offset in -128..127");
     }
   }
   if (fp.contains("col_poc")) {

@@ -42,6 +42,9 @@ struct HevcConfig {
   // parameters from the CTU's first block, and a 64x64 skip CU where the four blocks are one
   // uniform residual-free motion that is in the 64x64 merge list
   int ctu64 = 0;
+  // weighted_pred_flag (x265 --weightp): P slices carry pred_weight_table() with log2
+  // denominators 6 (luma and chroma) and the picture's FrameParams::wp weights
+  int weightp = 0;
   int ctb_log2() const { return ctu64 ? 6 : kCtbLog2; }
   int wctu() const { return (coded_width() + (1 << ctb_log2()) - 1) >> ctb_log2(); }
   int hctu() const { return (coded_height() + (1 << ctb_log2()) - 1) >> ctb_log2(); }
@@ -75,6 +78,11 @@ struct HevcFrameParams {
   int rps_poc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint8_t rps_used[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   HevcColPic col;       // with HevcConfig::tmvp: the collocated picture (L1[0] in B, L0[0] in P)
+  // with HevcConfig::weightp, P slices: explicit weights of RefPicList0[0] (wp = 0: flags off)
+  // -- luma weight / offset, then Cb, Cr (weights over 2^6, offsets in 8-bit units)
+  int wp = 0;
+  int wp_w[3] = {64, 64, 64};
+  int wp_o[3] = {0, 0, 0};
 };
 
 struct HevcSliceStats {

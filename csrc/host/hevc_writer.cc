@@ -176,7 +176,7 @@ std::vector<uint8_t> hevc_parameter_sets(const HevcConfig& c) {
     bw.put_se(0);   // pps_cb_qp_offset
     bw.put_se(0);   // pps_cr_qp_offset
     bw.put_bit(0);  // pps_slice_chroma_qp_offsets_present_flag
-    bw.put_bit(0);  // weighted_pred_flag
+    bw.put_bit(c.weightp ? 1 : 0);  // weighted_pred_flag
     bw.put_bit(0);  // weighted_bipred_flag
     bw.put_bit(0);  // transquant_bypass_enabled_flag
     bw.put_bit(0);  // tiles_enabled_flag
@@ -1274,6 +1274,22 @@ std::vector<uint8_t> hevc_write_slice(const HevcConfig& c, const HevcFrameParams
     bw.put_bit(0);            // num_ref_idx_active_override_flag (one picture per list)
     if (bslice) bw.put_bit(0);  // mvd_l1_zero_flag
     if (c.tmvp && bslice) bw.put_bit(0);  // collocated_from_l0_flag: the collocated picture is RefPicList1[0]
+    if (c.weightp && !bslice) {
+      // pred_weight_table (7.3.6.3), one list-0 entry: log2 denominators 6 / 6; the chroma
+      // offset is coded as its difference from the weight-dependent prediction (7.4.7.3)
+      bw.put_ue(6);                 // luma_log2_weight_denom
+      bw.put_se(0);                 // delta_chroma_log2_weight_denom
+      bw.put_bit(fp.wp ? 1 : 0);    // luma_weight_l0_flag[0]
+      bw.put_bit(fp.wp ? 1 : 0);    // chroma_weight_l0_flag[0]
+      if (fp.wp) {
+        bw.put_se(fp.wp_w[0] - 64);  // delta_luma_weight_l0
+        bw.put_se(fp.wp_o[0]);       // luma_offset_l0
+        for (int j = 1; j < 3; ++j) {
+          bw.put_se(fp.wp_w[j] - 64);  // delta_chroma_weight_l0
+          bw.put_se(fp.wp_o[j] - 128 + ((128 * fp.wp_w[j]) >> 6));  // delta_chroma_offset_l0
+        }
+      }
+    }
     bw.put_ue(5 - c.max_merge);  // five_minus_max_num_merge_cand
   }
   bw.put_se(fp.qp - 26);      // slice_qp_delta (init_qp 26)

@@ -106,7 +106,8 @@ void mivc_launch_hevc_inter(int B, int W, int H, const uint16_t* sy, const uint1
                             uint16_t* rv, void* ctu, void* cu, int16_t* cy, int16_t* cu_, int16_t* cv, const int* qp,
                             const int8_t* run, const int* cand, const int16_t* mv, const int* me_cost, int bd,
                             int tu_split, int sdh, int intra_bias, void* stream, const int16_t* mvb,
-                            const uint8_t* dirb, const uint16_t* f1y, const uint16_t* f1u, const uint16_t* f1v);
+                            const uint8_t* dirb, const uint16_t* f1y, const uint16_t* f1u, const uint16_t* f1v,
+                            const int16_t* wp);
 void mivc_launch_hevc_b(int mode, int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref0, const uint8_t* ref1,
                         const uint8_t* hp0, const uint8_t* hp1, const int16_t* mv0, const int16_t* mv1, const int* cost0,
                         const int* cost1, const int16_t* pm0, const int16_t* pm1, const int16_t* tmv, const uint8_t* tdir,
@@ -474,18 +475,19 @@ PYBIND11_MODULE(_hip, m) {
                          uintptr_t fv, uintptr_t ry, uintptr_t ru, uintptr_t rv, uintptr_t ctu, uintptr_t cu, uintptr_t cy,
                          uintptr_t cu_, uintptr_t cv, uintptr_t qp, uintptr_t run, uintptr_t cand, uintptr_t mv,
                          uintptr_t me_cost, int bd, uintptr_t stream, int tu_split, int sdh, int intra_bias,
-                         uintptr_t mvb, uintptr_t dirb, uintptr_t f1y, uintptr_t f1u, uintptr_t f1v) {
+                         uintptr_t mvb, uintptr_t dirb, uintptr_t f1y, uintptr_t f1u, uintptr_t f1v, uintptr_t wp) {
     if (dirb && (!mvb || !f1y || !f1u || !f1v)) throw std::invalid_argument("hevc_inter: B motion needs mvb and list-1 planes");
     mivc_launch_hevc_inter(B, W, H, P<uint16_t>(sy), P<uint16_t>(su), P<uint16_t>(sv), P<uint16_t>(fy), P<uint16_t>(fu),
                            P<uint16_t>(fv), P<uint16_t>(ry), P<uint16_t>(ru), P<uint16_t>(rv), P<void>(ctu), P<void>(cu),
                            P<int16_t>(cy), P<int16_t>(cu_), P<int16_t>(cv), P<int>(qp), P<int8_t>(run), P<int>(cand),
                            P<int16_t>(mv), P<int>(me_cost), bd, tu_split, sdh, intra_bias, S(stream), P<int16_t>(mvb),
-                           P<uint8_t>(dirb), P<uint16_t>(f1y), P<uint16_t>(f1u), P<uint16_t>(f1v));
+                           P<uint8_t>(dirb), P<uint16_t>(f1y), P<uint16_t>(f1u), P<uint16_t>(f1v), P<int16_t>(wp));
   }, py::arg("B"), py::arg("W"), py::arg("H"), py::arg("sy"), py::arg("su"), py::arg("sv"), py::arg("fy"), py::arg("fu"),
      py::arg("fv"), py::arg("ry"), py::arg("ru"), py::arg("rv"), py::arg("ctu"), py::arg("cu"), py::arg("cy"),
      py::arg("cu_"), py::arg("cv"), py::arg("qp"), py::arg("run"), py::arg("cand"), py::arg("mv"), py::arg("me_cost"),
      py::arg("bd"), py::arg("stream"), py::arg("tu_split") = 0, py::arg("sdh") = 0, py::arg("intra_bias") = 0,
-     py::arg("mvb") = 0, py::arg("dirb") = 0, py::arg("f1y") = 0, py::arg("f1u") = 0, py::arg("f1v") = 0);
+     py::arg("mvb") = 0, py::arg("dirb") = 0, py::arg("f1y") = 0, py::arg("f1u") = 0, py::arg("f1v") = 0,
+     py::arg("wp") = 0);
   m.def("hevc_b", [](int mode, int B, int wmb, int hmb, uintptr_t src, uintptr_t ref0, uintptr_t ref1, uintptr_t hp0,
                      uintptr_t hp1, uintptr_t mv0, uintptr_t mv1, uintptr_t cost0, uintptr_t cost1, uintptr_t pm0,
                      uintptr_t pm1, uintptr_t tmv, uintptr_t tdir, uintptr_t mvb_in, uintptr_t dir_in, uintptr_t mvb_out,

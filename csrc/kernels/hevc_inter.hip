@@ -42,7 +42,13 @@ struct HevcInterArgs {
   int tu_split;          // inter CUs may code their residual as four quarter TUs (RD choice)
   int sdh;               // sign data hiding in the quantiser
   int intra_bias;        // lambda multiples added to the open-loop intra costs of P pictures
+  // explicit weighted prediction of P pictures (x265 --weightp; pred_weight_table with
+  // log2 denominators kWpLog2 for luma and chroma): [B][6] = weight, offset (8-bit units) of
+  // Y, Cb, Cr; weight 0 = the slot's picture is not weighted.  Null: default weighting.
+  const int16_t* wp;
 };
+
+constexpr int kWpLog2 = 6;
 
 __device__ __forceinline__ int lambda_satd_i(int qp, int bd) {
   return static_cast<int>(0.755f * exp2f((qp - 12) / 6.0f) * static_cast<float>(1 << (bd - 8)) + 0.5f);
@@ -250,7 +256,8 @@ __device__ __forceinline__ void mc_inter(InterShared& S, const uint16_t* ref, in
 // prediction (8.5.3.3.4.2) of one list, or the average of both (bi-prediction)
 template <int NT>
 __device__ __forceinline__ void mc_block(InterShared& S, const uint16_t* ref0, const uint16_t* ref1, int pw, int ph,
-                                         int bx, int by, int n, int dir, int mvx, int mvy, int mv1x, int mv1y, int bd) {
+                                         int bx, int by, int n, int dir, int mvx, int mvy, int mv1x, int mv1y, int bd,
+                                         int ww = 0, int wo = 0) {
   const int lane = lane_id();
   const int maxv = (1 << bd) - 1;
   if (dir == hevc::DIR_BI) {
@@ -264,10 +271,18 @@ __device__ __forceinline__ void mc_block(InterShared& S, const uint16_t* ref0, c
   } else {
     const bool l1 = dir == hevc::DIR_L1;
     mc_inter<NT>(S, l1 ? ref1 : ref0, pw, ph, bx, by, n, l1 ? mv1x : mvx, l1 ? mv1y : mvy, bd, S.R);
-    const int wsh = 14 - bd, woff = 1 << (wsh - 1);
-    for (int i = lane; i < n * n; i += 64) {
-      const int v = (S.R[i] + woff) >> wsh;
-      S.pred[i] = static_cast<uint16_t>(v < 0 ? 0 : (v > maxv ? maxv : v));
+    if (ww) {  // explicit weighted sample prediction, uni-directional (8.5.3.3.4.3)
+      const int lwd = kWpLog2 + 14 - bd, rnd = 1 << (lwd - 1), o = wo * (1 << (bd - 8));
+      for (int i = lane; i < n * n; i += 64) {
+        const int v = ((S.R[i] * ww + rnd) >> lwd) + o;
+        S.pred[i] = static_cast<uint16_t>(v < 0 ? 0 : (v > maxv ? maxv : v));
+      }
+    } else {
+      const int wsh = 14 - bd, woff = 1 << (wsh - 1);
+      for (int i = lane; i < n * n; i += 64) {
+        const int v = (S.R[i] + woff) >> wsh;
+        S.pred[i] = static_cast<uint16_t>(v < 0 ? 0 : (v > maxv ? maxv : v));
+      }
     }
   }
   wave_sync();
@@ -317,8 +332,10 @@ __global__ __launch_bounds__(64) void hevc_inter_cu(HevcInterArgs a) {
     const uint16_t* src = (c == 0 ? a.src_y : (c == 1 ? a.src_u : a.src_v)) + slot * ps;
     uint16_t* rec = (c == 0 ? a.rec_y : (c == 1 ? a.rec_u : a.rec_v)) + slot * ps;
     int16_t* lev = (c == 0 ? a.coef_y : (c == 1 ? a.coef_u : a.coef_v)) + slot * ps + static_cast<size_t>(by) * pw + bx;
-    if (c == 0) mc_block<8>(S, ref, ref1, pw, ph, bx, by, bs, dir, mvx, mvy, mv1x, mv1y, bd);
-    else mc_block<4>(S, ref, ref1, pw, ph, bx, by, bs, dir, mvx, mvy, mv1x, mv1y, bd);
+    const int ww = (a.wp && dir == hevc::DIR_L0) ? a.wp[slot * 6 + 2 * c] : 0;
+    const int wo = ww ? a.wp[slot * 6 + 2 * c + 1] : 0;
+    if (c == 0) mc_block<8>(S, ref, ref1, pw, ph, bx, by, bs, dir, mvx, mvy, mv1x, mv1y, bd, ww, wo);
+    else mc_block<4>(S, ref, ref1, pw, ph, bx, by, bs, dir, mvx, mvy, mv1x, mv1y, bd, ww, wo);
     for (int i = lane; i < bs * bs; i += 64) {
       const int y = i / bs, x = i - y * bs;
       const int r = static_cast<int>(src[static_cast<size_t>(by + y) * pw + bx + x]) - S.pred[i];
@@ -397,8 +414,10 @@ extern "C" void mivc_launch_hevc_inter(int B, int W, int H, const uint16_t* sy, 
                                        int16_t* cv, const int* qp, const int8_t* run, const int* cand,
                                        const int16_t* mv, const int* me_cost, int bd, int tu_split, int sdh,
                                        int intra_bias, void* stream, const int16_t* mvb, const uint8_t* dirb,
-                                       const uint16_t* f1y, const uint16_t* f1u, const uint16_t* f1v) {
+                                       const uint16_t* f1y, const uint16_t* f1u, const uint16_t* f1v,
+                                       const int16_t* wp) {
   HevcInterArgs a;
+  a.wp = wp;
   a.g = HevcGeom{B, W, H, W / 32, H / 32};
   a.src_y = sy;
   a.src_u = su;

@@ -111,6 +111,17 @@ class HevcParams:
     # blocks are the CTU's quantization groups and are reconstructed in z-order; one SAO
     # parameter set per CTU; 64x64 skip CUs where four blocks agree) -- False: 32x32 CTBs
     ctu64: bool = bool(int(os.environ.get("MIVC_HEVC_CTU64", "1")))
+    # x265 --weightp (its default): explicit weights of a P picture's reference where the
+    # source statistics say the brightness or contrast changed (fades, flashes): weight =
+    # sqrt(var_cur / var_ref) over 2^6, offset = mean_cur - weight * mean_ref, per component,
+    # used when the luma mean moved >= wp_min_mean levels or the contrast >= wp_min_scale.
+    # 8-bit input (Main 10: off)
+    weightp: bool = True
+    wp_min_mean: float = 2.0
+    wp_min_scale: float = 0.08
+
+    def eff_weightp(self) -> bool:
+        return bool(self.weightp and self.bit_depth == 8 and not self.intra_only)
 
     def eff_bframes(self) -> int:
         return 0 if (self.intra_only or self.keyint > 0) else max(0, int(self.bframes))
@@ -123,7 +134,7 @@ class HevcParams:
                     sao=int(self.sao), deblock=int(self.deblock), max_merge=self.max_merge, wpp=int(self.wpp),
                     cu_qp_delta=int(self.adaptive_qp()), tu_inter_depth=int(self.tu_inter_depth), sdh=int(self.sdh),
                     level_idc=int(self.level_idc), bframes=self.eff_bframes(), tmvp=int(self.tmvp and not self.intra_only),
-                    pyramid=int(self.pyramid), ctu64=int(self.ctu64))
+                    pyramid=int(self.pyramid), ctu64=int(self.ctu64), weightp=int(self.eff_weightp()))
 
     def frame_qps(self) -> tuple[int, int]:
         qp_p = int(round(self.crf)) if self.crf is not None else int(self.qp)
@@ -190,6 +201,7 @@ class GpuHevcEncoder:
         nmb = self.wmb * self.hmb
         self.nmb = nmb
         self.src8 = torch.zeros((B, H, W), dtype=torch.uint8, device=dev)   # motion-search proxies
+        self.src8w = torch.zeros_like(self.src8) if params.eff_weightp() else None  # inverse-weighted proxy
         # 8-bit proxies of the reference pictures and their half-sample planes (per DPB slot),
         # built once per reference picture and shared by every picture that references it
         self.ref8s = [torch.zeros((B, H, W), dtype=torch.uint8, device=dev) for _ in range(self.ref_slots)]
@@ -402,6 +414,46 @@ class GpuHevcEncoder:
             self.tmv[..., 2 * x:2 * x + 2].copy_(v * avail[..., None].to(torch.int32))
         self.tdir.copy_(avail.to(torch.uint8) * (3 if targets[1] >= 0 else 1))
 
+    def _weights(self, y, u, v, plan) -> dict:
+        """x265 --weightp: per P picture (coding step) and slot, the explicit weights of its
+        reference from the source statistics (kernels/weightp.hip wp_stats: means and variances
+        of the two source pictures' planes).  Returns {step: (host rows [B] of [w, o] x 3 or
+        None, device int16 [B, 6] with weight 0 = not weighted, device int32 [B, 3] luma
+        (w, o, log2) for the search's inverse-weighted source)}."""
+        if not self.p.eff_weightp() or y.dtype != torch.uint8:
+            return {}
+        steps = [(t, pic) for t, pic in enumerate(plan) if pic.kind == "P"]
+        if not steps:
+            return {}
+        B, F, h, w = y.shape
+        st = torch.empty((B, F, 6), dtype=torch.int64, device=self.dev)
+        self.hip.wp_stats(y.data_ptr(), u.data_ptr(), v.data_ptr(), w, h, B * F, st.data_ptr(), self._stream())
+        sh = st.cpu().numpy().astype(np.float64)
+        n = np.array([w * h, w * h / 4, w * h / 4])
+        mean = sh[..., 0::2] / n
+        var = np.maximum(sh[..., 1::2] / n - mean ** 2, 0.0)
+        out = {}
+        for t, pic in steps:
+            m1, m0 = mean[:, pic.d], mean[:, pic.l0]
+            v1, v0 = var[:, pic.d], var[:, pic.l0]
+            scale = np.where(v0 > 1e-3, np.sqrt(v1 / np.maximum(v0, 1e-3)), 1.0)
+            use = (np.abs(m1[:, 0] - m0[:, 0]) >= self.p.wp_min_mean) | (np.abs(scale[:, 0] - 1) >= self.p.wp_min_scale)
+            if not use.any():
+                continue
+            wq = np.clip(np.round(scale * 64), 0, 127).astype(np.int64)
+            oq = np.clip(np.round(m1 - wq / 64.0 * m0), -128, 127).astype(np.int64)
+            rows = [[int(x) for c in range(3) for x in (wq[b, c], oq[b, c])] if use[b] else None for b in range(B)]
+            dev = np.zeros((B, 6), np.int16)
+            wsrc = np.zeros((B, 3), np.int32)
+            wsrc[:, 0], wsrc[:, 2] = 64, 6
+            for b in range(B):
+                if use[b]:
+                    dev[b] = rows[b]
+                    wsrc[b, 0], wsrc[b, 1] = rows[b][0], rows[b][1]
+            out[t] = (rows, torch.from_numpy(dev).to(self.dev), torch.from_numpy(wsrc).to(self.dev))
+        self.stats["weightp_pictures"] = int(sum(sum(r is not None for r in v[0]) for v in out.values()))
+        return out
+
     def _plan(self, F: int, cuts_h: np.ndarray, anchors_at) -> list:
         from .gop import GopPic, hevc_gop_plan
         if self.nb:
@@ -445,6 +497,7 @@ class GpuHevcEncoder:
         plan = self._plan(F, cuts_h, anchors_at)
         order = [pic.d for pic in plan]
         self.last_order = order
+        wps = self._weights(y, u, v, plan)  # coding step -> (host [B, 6] or None rows, device tables)
         if qps is None:
             qps = np.array([[qi if pic.kind == "I" else qpp for pic in sorted(plan, key=lambda q: q.d)]
                             for _ in range(B)], dtype=np.int32)
@@ -534,9 +587,16 @@ class GpuHevcEncoder:
                 self.run.fill_(2)
                 ref8, hp = self.ref8s[r0], self.me_hps[r0]
                 inter_kw = {}
+                s8 = p(self.src8)
+                if t in wps:
+                    # weighted P picture: the searches see the inverse-weighted source proxy
+                    # against the unweighted reference (kernels/weightp.hip wp_src)
+                    self.hip.wp_src(p(self.src8), p(self.src8w), p(wps[t][2]), B, self.H * self.W, s)
+                    s8 = p(self.src8w)
+                    inter_kw["wp"] = p(wps[t][1])
                 if pic.kind == "P":
                     with st("me"):
-                        self.hip.me(B, self.wmb, self.hmb, p(self.src8), p(ref8), p(self.prev_mv), p(self.mv),
+                        self.hip.me(B, self.wmb, self.hmb, s8, p(ref8), p(self.prev_mv), p(self.mv),
                                     p(self.me_cost), p(self.me_pred), p(self.me_intra), p(self.qp), self.p.me_range,
                                     self.p.subpel, s, p(hp), p(self.mb_aq), 1)
                     with st("merge_refine"):
@@ -547,7 +607,7 @@ class GpuHevcEncoder:
                             if tmvp and plan_refs.get(pic.l0, "I") != "I":
                                 self._temporal_for(pic, r0, pic.l0, ref_lists[pic.l0], (pic.l0, -1))
                                 tm_, td_ = p(self.tmv), p(self.tdir)
-                            pargs = (B, self.wmb, self.hmb, p(self.src8), p(ref8), p(ref8), p(hp), p(hp))
+                            pargs = (B, self.wmb, self.hmb, s8, p(ref8), p(ref8), p(hp), p(hp))
                             self.hip.hevc_b(2, *pargs, p(self.mv), 0, p(self.me_cost), 0, p(self.prev_mv), 0, 0, 0, 0, 0,
                                             p(self.mvb[0]), p(self.dirb[0]), p(self.bcost), p(self.bbits), p(self.qp),
                                             p(self.mb_aq), s, 0, int(self.p.max_merge), int(self.p.ctu64))
@@ -559,12 +619,12 @@ class GpuHevcEncoder:
                             fin = int(self.p.merge_refine) % 2
                             self.me_cost.copy_(self.bcost)
                             self.mv.copy_(self.mvb[fin][..., 0:2])
-                            inter_kw = dict(mvb=p(self.mvb[fin]), dirb=p(self.dirb[fin]), f1y=p(ref[0]), f1u=p(ref[1]),
+                            inter_kw.update(mvb=p(self.mvb[fin]), dirb=p(self.dirb[fin]), f1y=p(ref[0]), f1u=p(ref[1]),
                                             f1v=p(ref[2]))
                         else:
                             for it in range(int(self.p.merge_refine)):
                                 a_, b_ = (self.mv, self.mv_tmp) if it % 2 == 0 else (self.mv_tmp, self.mv)
-                                self.hip.hevc_merge_refine(B, self.wmb, self.hmb, p(self.src8), p(ref8), p(hp), p(a_),
+                                self.hip.hevc_merge_refine(B, self.wmb, self.hmb, s8, p(ref8), p(hp), p(a_),
                                                            p(b_), p(self.me_cost), p(self.prev_mv), p(self.qp),
                                                            p(self.mb_aq), s)
                             if int(self.p.merge_refine) % 2:
@@ -676,8 +736,9 @@ class GpuHevcEncoder:
             t1 = time.perf_counter()
             t_gpu += t1 - t0
             qcol = qps_c[:, t].copy()
+            wrow = wps[t][0] if t in wps else None
 
-            def job(done=done, pic=pic, qcol=qcol, ctu=ctu, cu=cu, nz=nz, off=off, lv=lv, i0=idr_d):
+            def job(done=done, pic=pic, qcol=qcol, ctu=ctu, cu=cu, nz=nz, off=off, lv=lv, i0=idr_d, wrow=wrow):
                 done.synchronize()
                 tj = time.perf_counter()
                 # POC counts display pictures from the latest IDR
@@ -695,6 +756,8 @@ class GpuHevcEncoder:
                 fps = []
                 for b in range(B):
                     fp = dict(base, qp=int(qcol[b]))
+                    if wrow is not None and wrow[b] is not None:
+                        fp["wp"] = wrow[b]
                     if col is not None:
                         fp["col_cu"] = None if col[0] is None else col[0][b]
                     fps.append(fp)

@@ -265,3 +265,23 @@ def test_gpu_hevc_1080p_matches_decoder(host, ctu64):
         for t, p in enumerate(pics):
             assert np.array_equal(d.y[t].cpu().numpy().astype(np.uint16), p["y"][:1080]), (b, t)
             assert np.array_equal(d.v[t].cpu().numpy().astype(np.uint16), p["v"][:540]), (b, t)
+
+
+def test_gpu_hevc_weightp_fade_matches_decoder(host):
+    """x265 --weightp: on a fade the P pictures carry explicit weights (pred_weight_table,
+    luma and chroma offsets) and the GPU reconstruction stays bit-exact with the CPU decoder;
+    the weighted stream is smaller than the unweighted one."""
+    from govideocompressor_amd.models.h264_gpu import synth_clip
+    from govideocompressor_amd.models.hevc_gpu import GpuHevcEncoder, HevcParams
+    y, u, v = synth_clip(2, 8, 192, 128, seed=9, kind="fade")
+    sizes = {}
+    for wp in (False, True):
+        enc = GpuHevcEncoder(HevcParams(width=192, height=128, crf=27.0, bframes=0, weightp=wp), slots=2)
+        res = enc.encode(y, u, v, keep_recon=True)
+        rec = enc.last_recon
+        if wp:
+            assert enc.stats.get("weightp_pictures", 0) > 0
+            _compare(host, res, rec)
+        sizes[wp] = sum(len(r.bitstream) for r in res)
+        enc.close()
+    assert sizes[True] < sizes[False], sizes
