@@ -398,6 +398,7 @@ class GpuH264Encoder:
         self.err = torch.zeros((1,), dtype=i32, device=dev)
         self.p_intra_mbs = torch.zeros((), dtype=torch.int64, device=dev)  # intra MBs coded in P frames
         self.far_ref_mbs = torch.zeros((), dtype=torch.int64, device=dev)  # P MBs choosing RefPicList0[1 ..]
+        self.sfix_mbs = torch.zeros((), dtype=torch.int64, device=dev)  # fast spatial direct: MBs re-predicted
         # pinned staging for the entropy stage (double-buffered)
         if entropy == "cpu":
             self.h_hdr = [torch.empty((B, nmb, MB_HDR_BYTES), dtype=u8).pin_memory() for _ in range(2)]
@@ -666,6 +667,7 @@ class GpuH264Encoder:
                 with stt("b_spatial"):
                     self.hip.b_spatial_exact(B, wmb, hmb, P(hdr), P(self.intra_cost), P(self.cost_b), P(self.czero),
                                              P(self.sfix), s, rt, self.slice_rows)
+                    self.sfix_mbs += (self.sfix != 0).sum()
                     self.hip.b_spatial_fixup(B, wmb, hmb, P(hdr), P(self.sfix), py, hpp, py, hpp, P(self.pred_b), s,
                                              rt, NB)
             elif spatial:
@@ -1398,6 +1400,11 @@ class GpuH264Encoder:
                 self.stats["p_far_ref_ratio"] = float(self.far_ref_mbs.item()) / (n_p * self.nmb)
             nbp = sum(1 for plan in plans for pic in plan if pic.kind == "B")
             self.stats["b_ratio"] = nbp / float(B * F)
+            if nbp and self.p.direct == "spatial":
+                # fast spatial direct: share of B-picture MBs whose direct motion the exact
+                # decoding-order pass changed after they were priced on the estimate
+                self.stats["spatial_fix_ratio"] = float(self.sfix_mbs.item()) / (nbp * self.nmb)
+                self.sfix_mbs.zero_()
         self.p_intra_mbs.zero_()
         self.far_ref_mbs.zero_()
         err = int(self.err.item())

@@ -83,7 +83,8 @@ def run(args):
                 stats = getattr(enc, "stats", {}) or {}
                 pt = dict(config=cname, kind=kind, crf=crf, kbps=kbps, psnr=float(np.mean([r.psnr_y for r in res])),
                           ssim=float(np.mean([getattr(r, "ssim_y", 0.0) for r in res])), fps=args.slots * args.frames / dt,
-                          b_ratio=stats.get("b_ratio", 0.0), scenecuts=stats.get("scenecuts", 0))
+                          b_ratio=stats.get("b_ratio", 0.0), scenecuts=stats.get("scenecuts", 0),
+                          spatial_fix_ratio=stats.get("spatial_fix_ratio"))
                 out["points"].append(pt)
                 print(json.dumps(pt), flush=True)
         enc.close()
