@@ -163,8 +163,8 @@ def test_gpu_hevc_scenecut(host):
     from govideocompressor_amd.models.hevc_gpu import GpuHevcEncoder, HevcParams
     w, h, B, F, cut = 128, 96, 2, 5, 2
     a = synth_clip(B, F, w, h, seed=7)
-    b = synth_clip(B, F, w, h, seed=99)
-    y, u, v = (torch.cat([pa[:, :cut], pb[:, cut:]], dim=1).contiguous() for pa, pb in zip(a, b))
+    # the new scene: the texture in negative (nothing before the cut predicts it)
+    y, u, v = (torch.cat([pa[:, :cut], 255 - pa[:, cut:]], dim=1).contiguous() for pa in a)
     enc = GpuHevcEncoder(HevcParams(width=w, height=h), slots=B)
     res = enc.encode(y, u, v, keep_recon=True)
     rec = enc.last_recon
