@@ -849,9 +849,13 @@ struct BSpatialExactArgs {
   const int* intra_cost;  // [B, nmb]: an MB turns intra when intra_cost < cost (encode_inter)
   const int* cost;        // [B, nmb]
   const uint8_t* czero;   // [B, nmb] colZeroFlag bits (b_direct_mv)
-  uint8_t* fix;           // [B, nmb] out: 1 = the direct motion changed, re-predict
+  uint8_t* fix;           // [B, nmb] out: 1 = the direct motion changed, re-predict; 2 = made explicit
   const SlotRoute* rt;
   int slice_rows;         // MB rows per slice (0: one slice): no neighbours above a slice's first row
+  // quarter-sample tolerance: a direct quadrant whose exact motion is further than this from
+  // the estimate b_decide priced keeps the estimate as explicit motion; -1 = never (the direct
+  // MB is always re-predicted with the exact motion)
+  int tol;
 };
 
 constexpr int kExactWaves = 5;  // one lane per MB row: 320 >= 8K's 270 rows
@@ -886,7 +890,7 @@ __global__ __launch_bounds__(64 * kExactWaves) void b_spatial_exact(BSpatialExac
 #pragma unroll
         for (int l = 0; l < 2; ++l)
           fin[qq][l] = (h.ref[l][qq] & 255) | ((h.mv[l][qq][0] & 4095) << 8) | (h.mv[l][qq][1] << 20);
-      bool changed = false;
+      bool changed = false, converted = false;
       if (!intra && sdir) {
         const bool top = y > 0 && (a.slice_rows <= 0 || y % a.slice_rows != 0);
         const bool aA = x > 0, aB = top, aC = top && x + 1 < wmb, aD = x > 0 && top;
@@ -902,6 +906,9 @@ __global__ __launch_bounds__(64 * kExactWaves) void b_spatial_exact(BSpatialExac
         }
         const bool zero = refs[0] < 0 && refs[1] < 0;
         const int cz = CZ[mb];
+        int ex[4][2][3];    // exact motion of the direct quadrants: ref, mvx, mvy per list
+        int conv = 0;       // quadrants whose exact motion is off the estimate by more than tol
+        int moved = 0;      // quadrants whose exact motion differs at all
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
           if (!((sdir >> qq) & 1)) continue;
@@ -914,18 +921,48 @@ __global__ __launch_bounds__(64 * kExactWaves) void b_spatial_exact(BSpatialExac
             } else if (rf < 0 || (rf == 0 && ((cz >> qq) & 1))) {
               vx = vy = 0;
             }
-            const int pk = (rf & 255) | ((vx & 4095) << 8) | (vy << 20);
-            if (pk != fin[qq][l]) {
-              changed = true;
-              fin[qq][l] = pk;
-              h.ref[l][qq] = static_cast<int8_t>(rf);
-              h.mv[l][qq][0] = static_cast<int16_t>(vx);
-              h.mv[l][qq][1] = static_cast<int16_t>(vy);
-            }
+            ex[qq][l][0] = rf;
+            ex[qq][l][1] = vx;
+            ex[qq][l][2] = vy;
+            const int er = h.ref[l][qq], evx = h.mv[l][qq][0], evy = h.mv[l][qq][1];
+            if (((rf & 255) | ((vx & 4095) << 8) | (vy << 20)) != fin[qq][l]) moved |= 1 << qq;
+            if (rf != er || (rf >= 0 && (abs(vx - evx) > a.tol || abs(vy - evy) > a.tol))) conv |= 1 << qq;
+          }
+        }
+        if (conv && a.tol >= 0) {
+          converted = true;
+          // The prediction b_decide priced (and encode_inter will subtract) is the estimate's:
+          // instead of re-predicting with motion nobody priced, the MB keeps the estimated
+          // motion and codes it explicitly -- B_L0 / L1 / Bi partitions of the shape the
+          // quadrant motion allows (B_Direct_16x16) or explicit 8x8 sub-blocks (B_8x8).  Its
+          // final motion (what later MBs derive from) is then the estimate, already in `fin`.
+          if (kind == h264::MBK_BDIRECT) {
+            auto same = [&](int p, int q) { return fin[p][0] == fin[q][0] && fin[p][1] == fin[q][1]; };
+            h.kind = (same(0, 1) && same(2, 3)) ? (same(0, 2) ? h264::MBK_B16x16 : h264::MBK_B16x8)
+                                                : ((same(0, 2) && same(1, 3)) ? h264::MBK_B8x16 : h264::MBK_B8x8);
+            h.sub_direct = 0;
+            moved = 0;  // no quadrant keeps direct
+          } else {
+            h.sub_direct = static_cast<uint8_t>(h.sub_direct & ~conv);
+            moved &= ~conv;
+          }
+        }
+        // the remaining direct quadrants take the exact motion (re-predicted by b_spatial_fixup)
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          if (!((moved >> qq) & 1)) continue;
+          changed = true;
+#pragma unroll
+          for (int l = 0; l < 2; ++l) {
+            const int rf = ex[qq][l][0], vx = ex[qq][l][1], vy = ex[qq][l][2];
+            fin[qq][l] = (rf & 255) | ((vx & 4095) << 8) | (vy << 20);
+            h.ref[l][qq] = static_cast<int8_t>(rf);
+            h.mv[l][qq][0] = static_cast<int16_t>(vx);
+            h.mv[l][qq][1] = static_cast<int16_t>(vy);
           }
         }
       }
-      FX[mb] = changed ? 1 : 0;
+      FX[mb] = changed ? 1 : (converted ? 2 : 0);  // 2: explicit now, prediction unchanged
       int* e = cur_row + x * 5;
       e[0] = intra;
       e[1] = fin[2][0];
@@ -959,7 +996,7 @@ __global__ __launch_bounds__(64) void b_spatial_fixup(BSpatialFixArgs a) {
   xcd_unit_slot(mb, slot);
   if (!route_active(a.rt, slot, SK_B)) return;
   const size_t o = static_cast<size_t>(slot) * nmb + mb;
-  if (!a.fix[o]) return;  // wave-uniform
+  if (a.fix[o] != 1) return;  // wave-uniform
   const int lane = threadIdx.x;
   const int mx = mb % g.wmb, my = mb / g.wmb;
   const int W = g.W, H = g.H;
@@ -1829,9 +1866,10 @@ extern "C" void mivc_launch_b_spatial(int B, int wmb, int hmb, void* hdr, const 
 
 extern "C" void mivc_launch_b_spatial_exact(int B, int wmb, int hmb, void* hdr, const int* intra_cost, const int* cost,
                                             const uint8_t* czero, uint8_t* fix, void* stream, const void* route,
-                                            int slice_rows) {
+                                            int slice_rows, int tol) {
   BSpatialExactArgs a;
   a.slice_rows = slice_rows;
+  a.tol = tol;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.hdr = static_cast<MbHeader*>(hdr);
   a.intra_cost = intra_cost;

@@ -37,7 +37,8 @@ void mivc_launch_b_direct(int B, int wmb, int hmb, const void* col, const int* d
                           int16_t* dmv, int8_t* dref, int16_t* pm0, int16_t* pm1, void* stream, const void* route,
                           int nbuf, uint8_t* czero);
 void mivc_launch_b_spatial_exact(int B, int wmb, int hmb, void* hdr, const int* intra_cost, const int* cost,
-                                 const uint8_t* czero, uint8_t* fix, void* stream, const void* route, int slice_rows);
+                                 const uint8_t* czero, uint8_t* fix, void* stream, const void* route, int slice_rows,
+                                 int tol);
 void mivc_launch_b_spatial_fixup(int B, int wmb, int hmb, const void* hdr, const uint8_t* fix, const uint8_t* ref0,
                                  const uint8_t* hp0, const uint8_t* ref1, const uint8_t* hp1, uint8_t* pred_out,
                                  void* stream, const void* route, int nbuf);
@@ -260,14 +261,16 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("dmv"), py::arg("pm0"), py::arg("pm1"), py::arg("stream"), py::arg("dref") = 0, py::arg("route") = 0,
      py::arg("nbuf") = 0, py::arg("czero") = 0);
   m.def("b_spatial_exact", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t intra_cost, uintptr_t cost,
-                              uintptr_t czero, uintptr_t fix, uintptr_t stream, uintptr_t route, int slice_rows) {
+                              uintptr_t czero, uintptr_t fix, uintptr_t stream, uintptr_t route, int slice_rows,
+                              int tol) {
     // spatial direct, fast path: the exact direct motion in decoding order (one lane per MB row)
     if (hmb > 320 || wmb > 480) throw std::invalid_argument("b_spatial_exact: at most 320 MB rows and 480 columns");
     if (!hdr || !intra_cost || !cost || !czero || !fix) throw std::invalid_argument("b_spatial_exact: null buffer");
     mivc_launch_b_spatial_exact(B, wmb, hmb, P<void>(hdr), P<int>(intra_cost), P<int>(cost), P<uint8_t>(czero),
-                                P<uint8_t>(fix), S(stream), P<void>(route), slice_rows);
+                                P<uint8_t>(fix), S(stream), P<void>(route), slice_rows, tol);
   }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("hdr"), py::arg("intra_cost"), py::arg("cost"),
-     py::arg("czero"), py::arg("fix"), py::arg("stream"), py::arg("route") = 0, py::arg("slice_rows") = 0);
+     py::arg("czero"), py::arg("fix"), py::arg("stream"), py::arg("route") = 0, py::arg("slice_rows") = 0,
+     py::arg("tol") = -1);
   m.def("b_spatial_fixup", [](int B, int wmb, int hmb, uintptr_t hdr, uintptr_t fix, uintptr_t ref0, uintptr_t hp0,
                               uintptr_t ref1, uintptr_t hp1, uintptr_t pred_out, uintptr_t stream, uintptr_t route,
                               int nbuf) {

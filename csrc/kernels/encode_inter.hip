@@ -50,8 +50,9 @@ struct InterArgs {
   // explicit weighted prediction of RefPicList0[0] in P pictures (nullable): [B, 8] = luma
   // weight, offset, log2 denominator, Cb weight, offset, Cr weight, offset, chroma denominator
   const int* wp;
-  // x264 --trellis 1 (its default: on the final encode of each MB): 4x4 luma levels by a
-  // rate-distortion choice instead of the dead-zone rounding (trellis_lite below); 0 = off
+  // x264 --trellis 1 (its default: on the final encode of each MB): levels by a rate-distortion
+  // choice instead of the dead-zone rounding (trellis_lite below); 0 = off, 1 = 4x4 luma only
+  // (round 3), 2 = also the 8x8 luma blocks and the chroma AC blocks
   int trellis;
   float trellis_lambda;    // multiplier of the SSD lambda 0.85 * 2^((QP - 12) / 3)
   // routed (route.h): ref_* / refs_* / ref1_* / rec_* are pools [B, nbuf, plane]; slots coding a
@@ -67,13 +68,27 @@ struct InterArgs {
 // costs for significance / last (a coefficient above every non-zero one would become the last
 // one), greater-than-one and the unary level bins, and the sign.  Levels after the block's
 // last non-zero one are never coded, so trailing small coefficients are dropped first.
+constexpr float kSig0 = 0.55f, kSig1 = 1.35f, kLast0 = 0.25f, kLast1 = 2.2f, kGt1No = 0.6f, kGt1Yes = 1.7f;
+
+// static CABAC bits of a non-zero level l >= 1 (significance, last, sign, greater-than-one,
+// unary and Exp-Golomb suffix); `seen`: a non-zero level follows in scan order
+__device__ __forceinline__ float trellis_level_bits(int l, bool seen) {
+  return kSig1 + (seen ? kLast0 : kLast1) + 1.0f +
+         (l == 1 ? kGt1No : kGt1Yes + 0.9f * static_cast<float>(min(l - 2, 13)) +
+                                (l > 15 ? 2.0f * (31 - __clz(l - 14)) + 1.0f : 0.0f));
+}
+
+// start: first scan index coded (1 for chroma AC: the DC goes through the 2x2 Hadamard)
 __device__ __forceinline__ void trellis_lite4x4(const int (&w)[16], int (&lv)[16], const int (&mf)[3], int qbits,
-                                                float lam) {
+                                                float lam, int start = 0) {
   constexpr float kInvNorm[3] = {1.0f / 16.0f, 1.0f / 100.0f, 1.0f / 40.0f};
-  constexpr float kSig0 = 0.55f, kSig1 = 1.35f, kLast0 = 0.25f, kLast1 = 2.2f, kGt1No = 0.6f, kGt1Yes = 1.7f;
   bool seen = false;
 #pragma unroll
   for (int i = 15; i >= 0; --i) {
+    if (i < start) {
+      lv[h264::kZigzag4x4[i]] = 0;
+      continue;
+    }
     const int r = h264::kZigzag4x4[i];
     const int cls = h264::kPosClass[r];
     const int a = w[r] < 0 ? -w[r] : w[r];
@@ -88,16 +103,41 @@ __device__ __forceinline__ void trellis_lite4x4(const int (&w)[16], int (&lv)[16
       const int l = zr - d;
       if (l < 1) continue;
       const float e = static_cast<float>(a) - static_cast<float>(l) * step;
-      const float bits = kSig1 + (seen ? kLast0 : kLast1) + 1.0f +
-                         (l == 1 ? kGt1No : kGt1Yes + 0.9f * static_cast<float>(min(l - 2, 13)) +
-                                                (l > 15 ? 2.0f * (31 - __clz(l - 14)) + 1.0f : 0.0f));
-      const float j = e * e * inv_n + lam * bits;
+      const float j = e * e * inv_n + lam * trellis_level_bits(l, seen);
       if (j < best) {
         best = j;
         bl = l;
       }
     }
     lv[r] = w[r] < 0 ? -bl : bl;
+    seen |= bl != 0;
+  }
+}
+
+// The same greedy choice for one 16-coefficient chunk (scan positions 16k .. 16k + 15) of an 8x8
+// block, in the quantiser's own domain: the 8x8 scaling gives every position the same
+// pixel-domain step Qstep, so a level l of exact quotient z costs (z - l)^2 Qstep^2 of SSD and
+// lambda / Qstep^2 = 0.85 * 2^((QP - 12) / 3) / (0.390625 * 2^(QP / 3)) = 0.136 per bit (QP-free).
+// seen: a later chunk of the block keeps a non-zero level.  lv keeps its sign from z.
+__device__ __forceinline__ void trellis_lite8_chunk(const float (&z)[16], int (&lv)[16], float lamq, bool seen) {
+#pragma unroll
+  for (int i = 15; i >= 0; --i) {
+    const float az = fabsf(z[i]);
+    const int zr = static_cast<int>(az + 0.5f);
+    float best = az * az + lamq * (seen ? kSig0 : 0.0f);
+    int bl = 0;
+#pragma unroll
+    for (int d = 1; d >= 0; --d) {
+      const int l = zr - d;
+      if (l < 1) continue;
+      const float e = az - static_cast<float>(l);
+      const float j = e * e + lamq * trellis_level_bits(l, seen);
+      if (j < best) {
+        best = j;
+        bl = l;
+      }
+    }
+    lv[i] = z[i] < 0.0f ? -bl : bl;
     seen |= bl != 0;
   }
 }
@@ -214,6 +254,7 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
   __shared__ int16_t s_l8[2][4][64];
   __shared__ int s_cost[2][2][16];   // [half][0: satd per 4x4 lane, 1: sa8d partial per (b8, k)]
   __shared__ int s_t8[2][3];         // [half][0] use 8x8, [1] keep mask of the 8x8 blocks, [2] 8x8 tried
+  __shared__ int s_nz8[2][4][4];     // trellis: [half][b8][chunk] the dead-zone levels are non-zero
 
   const int mvx = a.bmode ? 0 : a.mv[o * 2], mvy = a.bmode ? 0 : a.mv[o * 2 + 1];
   const bool go_intra = a.intra_cost[o] < a.me_cost[o];
@@ -353,12 +394,37 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
       const int m = qp % 6;
       int lastnz = -1, firstnz = -1, inner = 0;
       bool big = false;
+      int q8[16];
+      if (a.trellis >= 2) {
+        // x264 --trellis on the 8x8 blocks too: the dead-zone levels say which later chunks
+        // keep a non-zero level, then each chunk runs the greedy choice back to front
+        float z[16];
+        bool nzc = false;
+        const float inv = exp2f(-static_cast<float>(qbits8));
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int pos = kZz8[k * 16 + i];
+          const int mf8 = kQuant8MF[m][pos8(pos & 7, pos >> 3)];
+          z[i] = static_cast<float>(dd[pos]) * static_cast<float>(mf8) * inv;
+          nzc |= h264::quant_coef(dd[pos], mf8, qbits8, 11) != 0;
+        }
+        s_nz8[half][tb][k] = nzc;
+        wave_sync();
+        bool later = false;
+#pragma unroll
+        for (int j = 1; j < 4; ++j) later |= (j > k) && s_nz8[half][tb][j];
+        trellis_lite8_chunk(z, q8, a.trellis_lambda * 0.136f, later);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int pos = kZz8[k * 16 + i];
+          q8[i] = h264::quant_coef(dd[pos], kQuant8MF[m][pos8(pos & 7, pos >> 3)], qbits8, 11);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int idx = k * 16 + i;
-        const int pos = kZz8[idx];
-        const int mf8 = kQuant8MF[m][pos8(pos & 7, pos >> 3)];
-        const int v = h264::quant_coef(dd[pos], mf8, qbits8, 11);
+        const int v = q8[i];
         s_l8[half][tb][idx] = static_cast<int16_t>(v);
         const bool nzv = v != 0;
         big |= v > 1 || v < -1;
@@ -446,9 +512,13 @@ __global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
     h264::forward_core4x4(res);
     s_cdc[half][comp][cb] = res[0];
     const int qbits = 15 + qpc / 6;
+    if (a.trellis >= 2) {  // chroma AC by the same rate-distortion choice, at the chroma QP's lambda
+      trellis_lite4x4(res, lv, mfc, qbits, a.trellis_lambda * 0.85f * exp2f((qpc - 12) * (1.0f / 3.0f)), 1);
+    } else {
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
-      lv[r] = r == 0 ? 0 : h264::quant_coef(res[r], mfc[h264::kPosClass[r]], qbits, 11);
+      for (int r = 0; r < 16; ++r)
+        lv[r] = r == 0 ? 0 : h264::quant_coef(res[r], mfc[h264::kPosClass[r]], qbits, 11);
+    }
     int scan[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) scan[i] = lv[h264::kZigzag4x4[i]];

@@ -191,7 +191,7 @@ H264_PARAMS = {
     "weightp": ("weightp", lambda v: _int_in(0, 2)(v) > 0),
     "weightb": ("weightb", _flag),
     "no-weightb": ("weightb", lambda v: not _flag(v)),
-    "trellis": ("trellis", lambda v: int(_int_in(0, 2)(v) > 0)),
+    "trellis": ("trellis", lambda v: 2 if _int_in(0, 2)(v) > 0 else 0),
     # direct=spatial: decided in an MB wavefront (bframe.hip b_spatial_decide), -1.9 % BD-rate
     # and ~26 % fewer frames/s than temporal on the benchmark content (profiles/r3_direct_rd.md)
     "direct": ("direct", _only("temporal", "spatial")),

@@ -127,9 +127,10 @@ class H264Params:
     # direct termination); 0 disables.  1080p RD sweep (profiles/r3_b_gate_rd.md): 2400 ->
     # -8.8 % BD-rate (PSNR-Y) and +7..20 % fps against no gate
     b_gate: int = int(os.environ.get("MIVC_B_GATE", 2400))
-    # x264 --trellis 1 (default): rate-distortion choice of the 4x4 luma levels of inter MBs
-    # (encode_inter.hip trellis_lite4x4); trellis_lambda scales its SSD lambda
-    trellis: int = int(os.environ.get("MIVC_TRELLIS", 1))
+    # x264 --trellis 1 (default): rate-distortion choice of the levels of inter MBs
+    # (encode_inter.hip trellis_lite4x4 / trellis_lite8_chunk); 1 = the 4x4 luma blocks only,
+    # 2 = also the 8x8 luma and the chroma AC blocks; trellis_lambda scales its SSD lambda
+    trellis: int = int(os.environ.get("MIVC_TRELLIS", 2))
     # x264 --direct: "temporal" (co-located motion scaled by POC distances: every MB decides in
     # parallel) or "spatial" (the neighbours' motion: b_decide keeps each searched MB's best
     # explicit candidate, then bframe.hip b_spatial_decide derives the exact spatial motion in
@@ -147,6 +148,13 @@ class H264Params:
     # the exact derivation priced MB by MB inside the wavefront (b_spatial_decide, ~3.7 ms per
     # picture of serial chain)
     spatial_wavefront: bool = os.environ.get("MIVC_SPATIAL_WAVEFRONT", "0") != "0"
+    # fast path: a direct quadrant whose exact motion lies further than this many quarter
+    # samples from the priced estimate keeps the estimate as explicit motion (B_L0 / L1 / Bi
+    # partitions, explicit 8x8 sub-blocks: the priced prediction, plus mvd bits) instead of being
+    # re-predicted with motion nobody priced -- round 4's first measurement (always re-predict,
+    # -1) cost +57 % BD-rate on the panning content, most of it in gated MBs that have no
+    # explicit alternative
+    spatial_fix_tol: int = int(os.environ.get("MIVC_SPATIAL_FIX_TOL", 0))
     # temporal direct: B_Direct_16x16 preferred by tdirect_bias * lambda in b_decide's choice
     # (-0.36 % BD-rate at 8, profiles/r3_direct_rd.md)
     tdirect_bias: int = int(os.environ.get("MIVC_TDIRECT_BIAS", 8))
@@ -399,6 +407,7 @@ class GpuH264Encoder:
         self.p_intra_mbs = torch.zeros((), dtype=torch.int64, device=dev)  # intra MBs coded in P frames
         self.far_ref_mbs = torch.zeros((), dtype=torch.int64, device=dev)  # P MBs choosing RefPicList0[1 ..]
         self.sfix_mbs = torch.zeros((), dtype=torch.int64, device=dev)  # fast spatial direct: MBs re-predicted
+        self.sconv_mbs = torch.zeros((), dtype=torch.int64, device=dev)  # ... and MBs made explicit
         # pinned staging for the entropy stage (double-buffered)
         if entropy == "cpu":
             self.h_hdr = [torch.empty((B, nmb, MB_HDR_BYTES), dtype=u8).pin_memory() for _ in range(2)]
@@ -666,8 +675,9 @@ class GpuH264Encoder:
             if sfast:
                 with stt("b_spatial"):
                     self.hip.b_spatial_exact(B, wmb, hmb, P(hdr), P(self.intra_cost), P(self.cost_b), P(self.czero),
-                                             P(self.sfix), s, rt, self.slice_rows)
-                    self.sfix_mbs += (self.sfix != 0).sum()
+                                             P(self.sfix), s, rt, self.slice_rows, int(self.p.spatial_fix_tol))
+                    self.sfix_mbs += (self.sfix == 1).sum()
+                    self.sconv_mbs += (self.sfix == 2).sum()
                     self.hip.b_spatial_fixup(B, wmb, hmb, P(hdr), P(self.sfix), py, hpp, py, hpp, P(self.pred_b), s,
                                              rt, NB)
             elif spatial:
@@ -1404,7 +1414,9 @@ class GpuH264Encoder:
                 # fast spatial direct: share of B-picture MBs whose direct motion the exact
                 # decoding-order pass changed after they were priced on the estimate
                 self.stats["spatial_fix_ratio"] = float(self.sfix_mbs.item()) / (nbp * self.nmb)
+                self.stats["spatial_conv_ratio"] = float(self.sconv_mbs.item()) / (nbp * self.nmb)
                 self.sfix_mbs.zero_()
+                self.sconv_mbs.zero_()
         self.p_intra_mbs.zero_()
         self.far_ref_mbs.zero_()
         err = int(self.err.item())

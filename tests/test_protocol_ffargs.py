@@ -188,7 +188,7 @@ def test_ffargs_reference_and_weighting_knobs():
     p = ffargs.parse("-vcodec libx264 -x264-params ref=1:weightp=0:trellis=0:no-weightb=1").apply_opts(H264Params(64, 64))
     assert (p.refs, p.weightp, p.trellis, p.weightb) == (1, False, 0, False)
     p = ffargs.parse("-vcodec libx264 -x264-params ref=4:weightp=2:trellis=2:direct=temporal").apply_opts(H264Params(64, 64))
-    assert (p.refs, p.weightp, p.trellis, p.eff_refs(), p.direct) == (4, True, 1, 4, "temporal")
+    assert (p.refs, p.weightp, p.trellis, p.eff_refs(), p.direct) == (4, True, 2, 4, "temporal")
     p = ffargs.parse("-vcodec libx264 -x264-params direct=spatial").apply_opts(H264Params(64, 64))
     assert p.direct == "spatial"
     assert presets.apply(H264Params(64, 64), "slower").direct == "spatial"

@@ -38,6 +38,13 @@ CONFIGS = {
     "bias40": dict(b_adapt=1, b_bias=40),
     "slices4": dict(slices=4),
     "noseed": dict(lowres_seed=False),
+    "trellis1": dict(trellis=1),  # round 3's trellis scope (4x4 luma only)
+    # fast spatial direct with the fixed GOP pattern: exact motion re-predicted (tol -1, round 4's
+    # first version) / estimate kept as explicit motion beyond 0 / 4 quarter samples; b-pyramid
+    "sp_repredict": dict(direct="spatial", spatial_fix_tol=-1),
+    "sp_tol0": dict(direct="spatial", spatial_fix_tol=0),
+    "sp_tol4": dict(direct="spatial", spatial_fix_tol=4),
+    "sp_pyramid": dict(direct="spatial", pyramid=True),
     "default": dict(),  # the current defaults
 }
 # HEVC (GpuHevcEncoder) configurations: x265 --signhide, --bframes variants
@@ -84,7 +91,8 @@ def run(args):
                 pt = dict(config=cname, kind=kind, crf=crf, kbps=kbps, psnr=float(np.mean([r.psnr_y for r in res])),
                           ssim=float(np.mean([getattr(r, "ssim_y", 0.0) for r in res])), fps=args.slots * args.frames / dt,
                           b_ratio=stats.get("b_ratio", 0.0), scenecuts=stats.get("scenecuts", 0),
-                          spatial_fix_ratio=stats.get("spatial_fix_ratio"))
+                          spatial_fix_ratio=stats.get("spatial_fix_ratio"),
+                          spatial_conv_ratio=stats.get("spatial_conv_ratio"))
                 out["points"].append(pt)
                 print(json.dumps(pt), flush=True)
         enc.close()
