@@ -45,6 +45,9 @@ CONFIGS = {
     "sp_tol0": dict(direct="spatial", spatial_fix_tol=0),
     "sp_tol4": dict(direct="spatial", spatial_fix_tol=4),
     "sp_pyramid": dict(direct="spatial", pyramid=True),
+    # spatial direct decided exactly inside the MB wavefront (b_spatial_decide), + b-pyramid
+    "sp_wave": dict(direct="spatial", spatial_wavefront=True),
+    "sp_wave_pyr": dict(direct="spatial", spatial_wavefront=True, pyramid=True),
     "default": dict(),  # the current defaults
 }
 # HEVC (GpuHevcEncoder) configurations: x265 --signhide, --bframes variants
