@@ -25,6 +25,12 @@ import os
 import sys
 import time
 
+# eight hardware queues (HIP's default is 4), before anything can load the HIP runtime: the
+# encoder's compute, binarisation and arithmetic-coding streams plus the next step's input /
+# lookahead stream must not share queues (govideocompressor_amd/__init__.py)
+if not os.environ.get("GPU_MAX_HW_QUEUES", "").isdigit() or int(os.environ["GPU_MAX_HW_QUEUES"]) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -105,17 +111,33 @@ def main() -> None:
         with torch.cuda.device(env.device), torch.cuda.stream(merge_stream):
             return merger.run([r.parts() for r in res])
 
+    synth_stream = torch.cuda.Stream(device=env.device)
+
+    def synth_async(step: int):
+        """Input of a later step on a side stream (it overlaps the current step's encode the way
+        a decoder feeding the encoder would), with the event that ends it."""
+        with torch.cuda.stream(synth_stream):
+            clip = synth(step)
+            ev = torch.cuda.Event()
+            ev.record(synth_stream)
+        return clip, ev
+
     def run_steps(first: int, n: int, metrics_first: bool = False):
         """n steps: synthesize (new content) -> lookahead + encode -> merge on rank 0.
-        The next step's input synthesis is queued on the GPU before this step's merge
-        runs on the host, and the merge of step k overlaps the encode of step k + 1."""
-        clip = synth(first)
+        Step k + 1's input synthesis and lookahead run on side streams while step k encodes
+        (every one of them inside the n steps: nothing is prepared beyond the last step), and
+        the merge of step k overlaps the encode of step k + 1."""
+        clip, ev = synth_async(first)
+        ana = enc.analyse_async(clip[0], stream=synth_stream)
         fut = None
         for k in range(n):
-            y, u, v = clip
-            res = enc.encode(y, u, v, idr_base=env.rank * B, metrics=(metrics_first and k == 0))
+            (y, u, v), cur_ev, cur_ana = clip, ev, ana
+            if k + 1 < n:
+                clip, ev = synth_async(first + k + 1)
+                ana = enc.analyse_async(clip[0], stream=synth_stream)
+            torch.cuda.current_stream().wait_event(cur_ev)
+            res = enc.encode(y, u, v, idr_base=env.rank * B, metrics=(metrics_first and k == 0), analysis=cur_ana)
             del y, u, v
-            clip = synth(first + k + 1) if k + 1 < n else None
             if fut is not None:
                 fut.result()
             fut = merge_pool.submit(merge, res)
@@ -136,8 +158,9 @@ def main() -> None:
         stage_ms = {k: round(v["s"] * 1000.0 / a.warmup, 2) for k, v in enc.stage_timer.summary().items()}
         enc.stage_timer.enabled = False
         # the timed loop keeps two input batches alive (step k encodes while k + 1 is
-        # synthesized): let the caching allocator map the second one before the clock starts
-        spare = synth(-99)
+        # synthesized): let the caching allocator map the second one (on the synthesis
+        # stream, whose pool it comes from) before the clock starts
+        spare = synth_async(-99)
         torch.cuda.synchronize()
         del spare
     D.barrier(env)

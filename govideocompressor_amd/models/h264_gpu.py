@@ -151,10 +151,12 @@ class H264Params:
     # fast path: a direct quadrant whose exact motion lies further than this many quarter
     # samples from the priced estimate keeps the estimate as explicit motion (B_L0 / L1 / Bi
     # partitions, explicit 8x8 sub-blocks: the priced prediction, plus mvd bits) instead of being
-    # re-predicted with motion nobody priced -- round 4's first measurement (always re-predict,
-    # -1) cost +57 % BD-rate on the panning content, most of it in gated MBs that have no
-    # explicit alternative
-    spatial_fix_tol: int = int(os.environ.get("MIVC_SPATIAL_FIX_TOL", 0))
+    # re-predicted with motion nobody priced.  Content suite (profiles/r4_content_rd.md), BD-rate
+    # vs temporal direct: -1 (always re-predict) +111 %, 0 (always explicit) +68 %, 4 +25 %.
+    # The exact direct field follows the *sequential* decisions (the first MBs of a picture
+    # derive zero motion and spread it unless they are coded explicitly), which no parallel
+    # estimate reproduces -- temporal direct stays the default
+    spatial_fix_tol: int = int(os.environ.get("MIVC_SPATIAL_FIX_TOL", 4))
     # temporal direct: B_Direct_16x16 preferred by tdirect_bias * lambda in b_decide's choice
     # (-0.36 % BD-rate at 8, profiles/r3_direct_rd.md)
     tdirect_bias: int = int(os.environ.get("MIVC_TDIRECT_BIAS", 8))
@@ -819,18 +821,28 @@ class GpuH264Encoder:
         xs_d = torch.from_numpy(xscale).to(dev)
         ss_d = torch.from_numpy(sscale).to(dev)
         self._route_dev = rt_d  # keeps the table alive while the launches read it
+        pmask_d = kinds_d == 0
+        # the co-located motion copies of every reference step: one upload, sliced per step (a
+        # pair of small uploads per step cost ~1 ms of host latency each between two batches)
+        cts = sorted(col)
+        flat = np.array([e for t in cts for e in col[t]], dtype=np.int64).reshape(-1, 2)
+        flat_d = torch.from_numpy(np.ascontiguousarray(flat.T)).to(dev) if len(flat) else None
+        cofs, o = {}, 0
+        for t in cts:
+            cofs[t] = (o, o + len(col[t]))
+            o += len(col[t])
         steps = []
         for t in range(F):
             k = rt["kind"][t]
             n0p = rt["n0"][t][k == 0]
             st = dict(route=rt_d[t].data_ptr(), P=bool((k == 0).any()), B=bool((k == 1).any()),
-                      pmask=kinds_d[t] == 0, maxn0=int(n0p.max()) if n0p.size else 1, xscale=xs_d[t],
+                      pmask=pmask_d[t], maxn0=int(n0p.max()) if n0p.size else 1, xscale=xs_d[t],
                       deblock=bool((rt["flags"][t] & SF_DEBLOCK).any()), ref=bool((rt["flags"][t] & SF_REF).any()),
                       wp=None, wp_src=None, col_src=None, col_dst=None, kinds=k, sscale=ss_d[t])
-            if t in col:
-                src, dst = zip(*col[t])
-                st["col_src"] = torch.tensor(src, dtype=torch.long, device=dev)
-                st["col_dst"] = torch.tensor(dst, dtype=torch.long, device=dev)
+            if t in cofs:
+                a0, a1 = cofs[t]
+                st["col_src"] = flat_d[0, a0:a1]
+                st["col_dst"] = flat_d[1, a0:a1]
             steps.append(st)
         return steps
 
@@ -906,13 +918,18 @@ class GpuH264Encoder:
 
     @staticmethod
     def _cabac_groups(F: int, G: int) -> list[tuple[int, int]]:
-        """(first step, steps) of the arithmetic-coder groups of an F-step batch: G steps each,
-        the last full-size group split in two so the coder's tail after the final encode
-        kernel (nothing left to overlap it with) is half a group."""
-        sizes = [G] * (F // G) + ([F % G] if F % G else [])
+        """(first step, steps) of the arithmetic-coder groups of an F-step batch: the IDR step
+        alone (its slices hold several times the symbols of a P / B slice, so in a group of G
+        steps they set the whole launch's length: 205 of 270 ms per batch in round 4's trace),
+        then G steps each, the last full-size group split in two so the coder's tail after
+        the final encode kernel (nothing left to overlap it with) is half a group."""
+        head = [1] if (F > 2 and G > 1) else []
+        R = F - len(head)
+        sizes = [G] * (R // G) + ([R % G] if R % G else [])
         if sizes and sizes[-1] > max(1, G // 2):
             last = sizes.pop()
             sizes += [(last + 1) // 2, last // 2]
+        sizes = head + sizes
         out, t0 = [], 0
         for n in sizes:
             out.append((t0, n))
@@ -1125,34 +1142,71 @@ class GpuH264Encoder:
         """GPU lookahead of a batch: frame costs, scene cuts, MB-tree offsets and (b-adapt) the
         multi-distance P / B costs (rc/lookahead.py, csrc/kernels/lookahead.hip)."""
         from ..rc.lookahead import GpuLookahead
-        from ..rc.ratecontrol import MBTREE_STRENGTH, scenecut_flags
 
         if getattr(self, "_la", None) is None:
             self._la = GpuLookahead(self.dev, self.p.la_range)
         t0 = time.perf_counter()
+        self._apply_analysis(self._analysis(y, self._la))
+        self.timings["lookahead_s"] = self.timings.get("lookahead_s", 0.0) + time.perf_counter() - t0
+
+    def _analysis(self, y: torch.Tensor, la) -> dict:
+        """The lookahead of one batch on the current stream (host results synchronised, device
+        results -- MB-tree offsets, lowres vectors -- left on the device)."""
+        from ..rc.lookahead import GpuLookahead
+        from ..rc.ratecontrol import MBTREE_STRENGTH, scenecut_flags
+
         lbw, lbh = GpuLookahead.block_grid(y.shape[3], y.shape[2])
         # MB-tree needs the lookahead's block grid to be the coded MB grid (no -s resize)
         use_mbtree = self.p.mbtree and lbw * lbh == self.nmb
         badapt = bool(self.p.b_adapt) and self.nb > 0 and y.shape[1] >= 3
-        multi = None
+        multi = mbtree = None
         if use_mbtree:
-            costs_d, self._mbtree = self._la.mbtree(y, MBTREE_STRENGTH)
-            blk, mv = self._la.last_blk, self._la.last_mv
+            costs_d, mbtree = la.mbtree(y, MBTREE_STRENGTH)
+            blk, mv = la.last_blk, la.last_mv
         elif badapt:
-            costs_d, blk, mv = self._la.frame_costs(y, block_costs=True, block_mvs=True)
+            costs_d, blk, mv = la.frame_costs(y, block_costs=True, block_mvs=True)
         else:
-            costs_d, blk, mv = self._la.frame_costs(y), None, None
+            costs_d, blk, mv = la.frame_costs(y), None, None
         if badapt:
-            multi = self._la.multi_costs(y, blk, mv, min(7, self.nb + 1)).cpu().numpy()
-        self._la_costs = costs_d.cpu().numpy()
-        self._la_multi = multi
-        # lowres vectors on the MB grid: the search seeds (lowres_seed)
-        self._la_mv = mv if (mv is not None and self.p.lowres_seed and lbw * lbh == self.nmb) else None
-        self._la_blocks = lbw * lbh
-        self._use_mbtree = use_mbtree
-        self._scenecuts = scenecut_flags(self._la_costs, float(self.p.scenecut))
+            multi = la.multi_costs(y, blk, mv, min(7, self.nb + 1)).cpu().numpy()
+        costs = costs_d.cpu().numpy()
+        return dict(costs=costs, multi=multi, mbtree=mbtree, use_mbtree=use_mbtree, blocks=lbw * lbh,
+                    # lowres vectors on the MB grid: the search seeds (lowres_seed)
+                    mv=mv if (mv is not None and self.p.lowres_seed and lbw * lbh == self.nmb) else None,
+                    scenecuts=scenecut_flags(costs, float(self.p.scenecut)), shape=tuple(y.shape))
+
+    def _apply_analysis(self, a: dict) -> None:
+        self._la_costs, self._la_multi, self._mbtree = a["costs"], a["multi"], a["mbtree"]
+        self._la_mv, self._la_blocks, self._use_mbtree = a["mv"], a["blocks"], a["use_mbtree"]
+        self._scenecuts = a["scenecuts"]
         self.stats["scenecuts"] = int(self._scenecuts.sum())
-        self.timings["lookahead_s"] = self.timings.get("lookahead_s", 0.0) + time.perf_counter() - t0
+
+    def analyse_async(self, y: torch.Tensor, after: torch.cuda.Event | None = None,
+                      stream: torch.cuda.Stream | None = None):
+        """Start the lookahead of a *later* batch while the current one encodes: it runs on its
+        own stream (after ``after``, e.g. the event that ends the batch's synthesis / decode)
+        and host thread, with its own lookahead workspace, and the returned future's state
+        goes to :meth:`encode` (``analysis=``).  Its kernels fill the encode's idle gaps
+        instead of sitting on the critical path between two batches.  ``stream``: run on the
+        caller's stream instead (e.g. the one that produced ``y``: one hardware queue fewer)."""
+        from ..rc.lookahead import GpuLookahead
+        if getattr(self, "_la_async", None) is None:
+            self._la_async = GpuLookahead(self.dev, self.p.la_range)
+            self._la_stream = torch.cuda.Stream(device=self.dev)
+            self._la_pool = cf.ThreadPoolExecutor(max_workers=1)
+
+        def job():
+            t0 = time.perf_counter()
+            st = stream if stream is not None else self._la_stream
+            with torch.cuda.device(self.dev), torch.cuda.stream(st):
+                if after is not None:
+                    st.wait_event(after)
+                a = self._analysis(y, self._la_async)
+                a["event"] = torch.cuda.Event()
+                a["event"].record(st)
+            a["seconds"] = time.perf_counter() - t0
+            return a
+        return self._la_pool.submit(job)
 
     def _crf_from_plans(self, plans: list[list[PicPlan]]) -> np.ndarray:
         """[B, F] CRF QPs of the anchors (x264's curve over the anchors' complexity at their real
@@ -1188,13 +1242,16 @@ class GpuH264Encoder:
     @torch.no_grad()
     def encode(self, y: torch.Tensor, u: torch.Tensor, v: torch.Tensor, idr_base: int = 0,
                keep_recon: bool = False, metrics: bool = True, idr_ids: list[int] | None = None,
-               qps=None, anchors_at=(), qp_delta=None) -> list[SegmentResult]:
+               qps=None, anchors_at=(), qp_delta=None, analysis=None) -> list[SegmentResult]:
         """See :meth:`_encode`.  A batch whose CABAC symbols overflow the pool (QPs far below
         the budgeted ones) is encoded again with a pool grown 4x (encoding is a pure
         function of the inputs, so the retry gives the same bytes a big pool would)."""
+        if isinstance(analysis, cf.Future):
+            analysis = analysis.result()
         for attempt in range(3):
             try:
-                return self._encode(y, u, v, idr_base, keep_recon, metrics, idr_ids, qps, anchors_at, qp_delta)
+                return self._encode(y, u, v, idr_base, keep_recon, metrics, idr_ids, qps, anchors_at, qp_delta,
+                                    analysis)
             except CabacPoolExhausted:
                 if attempt == 2 or not (self.entropy == "gpu" and self.p.cabac):
                     raise
@@ -1205,7 +1262,7 @@ class GpuH264Encoder:
 
     def _encode(self, y: torch.Tensor, u: torch.Tensor, v: torch.Tensor, idr_base: int = 0,
                 keep_recon: bool = False, metrics: bool = True, idr_ids: list[int] | None = None,
-                qps=None, anchors_at=(), qp_delta=None) -> list[SegmentResult]:
+                qps=None, anchors_at=(), qp_delta=None, analysis=None) -> list[SegmentResult]:
         """Encode B segments of F frames each.
 
         y: [B, F, h, w] uint8 (device), u/v: [B, F, h/2, w/2].  Each slot's output is a
@@ -1219,6 +1276,8 @@ class GpuH264Encoder:
         to the final frame QPs -- after the lookahead CRF curve and the B-picture offset --
         with ordered dithering, so fractional offsets move the bitrate smoothly
         (:mod:`govideocompressor_amd.rc.abr`: -b:v, -pass 2, VBV).
+        ``analysis``: this batch's lookahead state from :meth:`analyse_async` (computed while
+        the previous batch encoded); None = run the lookahead here.
         """
         B, F = y.shape[0], y.shape[1]
         if B != self.B:
@@ -1249,7 +1308,12 @@ class GpuH264Encoder:
         self._la_mv = None
         self._from_la = False
         if qps is None and self.p.crf is not None and self.p.lookahead:
-            self._analyse(y)
+            if analysis is not None and analysis["shape"] == tuple(y.shape):
+                torch.cuda.current_stream(self.dev).wait_event(analysis["event"])
+                self._apply_analysis(analysis)
+                self.timings["lookahead_async_s"] = self.timings.get("lookahead_async_s", 0.0) + analysis["seconds"]
+            else:
+                self._analyse(y)
             self._from_la = True
         cuts_h = self._scenecuts if self._scenecuts is not None else np.zeros((B, F), dtype=bool)
         # a scene cut becomes an anchor of its slot, so the pictures after it predict from the

@@ -175,11 +175,10 @@ def test_gpu_scenecut_codes_cut_frames_intra(host):
     import torch
     from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
 
-    w, h, B, F, cut = 176, 144, 2, 6, 3
-    a = synth_clip(B, F, w, h, seed=2)
-    # the new scene: the same texture in negative -- nothing in the old scene predicts it (x264's
-    # scenecut needs the inter prediction to save almost nothing this soon after a key frame)
-    y, u, v = (torch.cat([pa[:, :cut], 255 - pa[:, cut:]], dim=1).contiguous() for pa in a)
+    # past keyint_min (25) from the IDR, where x264's scene-cut bias allows a cut at an inter
+    # cost of 90 % of the intra cost (right after a key frame it needs ~97.5 %)
+    w, h, B, F, cut = 176, 144, 2, 30, 27
+    y, u, v = _cut_clip(B, F, w, h, cut, seed=2)
     enc = GpuH264Encoder(H264Params(width=w, height=h), slots=B)
     res = enc.encode(y, u, v, keep_recon=True)
     torch.cuda.synchronize()
@@ -191,7 +190,7 @@ def test_gpu_scenecut_codes_cut_frames_intra(host):
         assert np.isin(kinds, [0, 1, 4, 8]).all()       # I4x4 / I16x16 / I_PCM / I8x8 only
         inter = [2, 3, 5, 6, 7, 9, 10, 11, 12, 13]  # P and B kinds: the cut is an anchor
         assert np.isin(np.asarray(pics[cut + 1]["mb_kind"]), inter).mean() > 0.5
-        assert r.psnr_y > 30
+        assert r.psnr_y > 25   # (uniform noise after the cut)
     enc.close()
 
 
@@ -493,3 +492,46 @@ def test_gpu_h264_slices_spatial_direct_roundtrip(host):
     res = enc.encode(y, u, v, keep_recon=True)
     torch.cuda.synchronize()
     _check_roundtrip(host, enc, res, 352, 288)
+
+
+def test_gpu_async_lookahead_same_bytes():
+    """analyse_async (the next batch's lookahead on a side stream while the current one
+    encodes, bench.py) must give the bytes of the inline lookahead."""
+    import torch
+    from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
+
+    enc = GpuH264Encoder(H264Params(width=320, height=240, crf=23), slots=3)
+    a = synth_clip(3, 12, 320, 240, seed=5, kind="cuts")
+    b = synth_clip(3, 12, 320, 240, seed=6)
+    ref = [[r.bitstream for r in enc.encode(*c, metrics=False)] for c in (a, b)]
+    side = torch.cuda.Stream()
+    fa = enc.analyse_async(a[0])
+    with torch.cuda.stream(side):
+        ev = torch.cuda.Event()
+        ev.record(side)
+    fb = enc.analyse_async(b[0], after=ev)
+    got_a = [r.bitstream for r in enc.encode(*a, metrics=False, analysis=fa)]
+    got_b = [r.bitstream for r in enc.encode(*b, metrics=False, analysis=fb)]
+    assert got_a == ref[0] and got_b == ref[1]
+    assert enc.timings.get("lookahead_async_s", 0) > 0
+
+
+def _cut_clip(B, F, w, h, cut, seed):
+    """synth_clip frames, then from frame ``cut`` a new scene: uniform noise panning by whole
+    pixels -- the old scene predicts none of it (the cut frame's inter cost is ~intra, a cut
+    even right after a key frame under x264's scene-cut bias), while the frames after the cut
+    predict each other exactly."""
+    import numpy as np
+    import torch
+    from govideocompressor_amd.models.h264_gpu import synth_clip
+    a = synth_clip(B, F, w, h, seed=seed)
+    rng = np.random.default_rng(seed)
+    out = []
+    for c, pa in enumerate(a):
+        ph, pw = pa.shape[2], pa.shape[3]
+        sh = 1 if c == 0 else 2
+        canvas = rng.integers(0, 256, (B, ph + 2 * F, pw + 4 * F), dtype=np.uint8)
+        new = np.stack([canvas[:, t // sh:t // sh + ph, (2 * t) // sh:(2 * t) // sh + pw] for t in range(F)], axis=1)
+        new = torch.from_numpy(np.ascontiguousarray(new)).to(pa.device)
+        out.append(torch.cat([pa[:, :cut], new[:, cut:]], dim=1).contiguous())
+    return out

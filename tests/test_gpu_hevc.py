@@ -159,12 +159,12 @@ def test_gpu_backend_hevc_mp4_piece(host, tmp_path):
 def test_gpu_hevc_scenecut(host):
     """A hard cut inside a segment is detected by the lookahead and the cut picture is
     coded with intra CUs only; the reconstruction stays bit-exact with the decoder."""
-    from govideocompressor_amd.models.h264_gpu import synth_clip
     from govideocompressor_amd.models.hevc_gpu import GpuHevcEncoder, HevcParams
-    w, h, B, F, cut = 128, 96, 2, 5, 2
-    a = synth_clip(B, F, w, h, seed=7)
-    # the new scene: the texture in negative (nothing before the cut predicts it)
-    y, u, v = (torch.cat([pa[:, :cut], 255 - pa[:, cut:]], dim=1).contiguous() for pa in a)
+    # the cut lies past keyint_min (25) from the IDR: x264 / x265's scene-cut bias makes a cut
+    # right after a key frame need an inter cost of ~97.5 % of the intra cost, which a motion
+    # search over hundreds of candidates undercuts even on unrelated noise
+    w, h, B, F, cut = 128, 96, 2, 30, 27
+    y, u, v = _cut_clip(B, F, w, h, cut, seed=7)
     enc = GpuHevcEncoder(HevcParams(width=w, height=h), slots=B)
     res = enc.encode(y, u, v, keep_recon=True)
     rec = enc.last_recon
@@ -173,8 +173,9 @@ def test_gpu_hevc_scenecut(host):
     _compare(host, res, rec)
     for r in res:
         bits = dict(zip(r.order, r.bits))
-        assert cut in r.order[:2]                      # the cut picture became an anchor
-        assert bits[cut] > 1.3 * bits[cut + 1]        # the all-intra cut picture costs more than a B picture
+        pics = host.hevc_decode(r.bitstream)
+        assert not (pics[cut]["cu"][:, 0] == 1).any()   # intra CUs only
+        assert bits[cut] > 1.3 * bits[cut + 1]        # the all-intra cut picture costs more than the next one
 
 
 @pytest.mark.parametrize("wpp", [True, False])
@@ -285,3 +286,24 @@ def test_gpu_hevc_weightp_fade_matches_decoder(host):
         sizes[wp] = sum(len(r.bitstream) for r in res)
         enc.close()
     assert sizes[True] < sizes[False], sizes
+
+
+def _cut_clip(B, F, w, h, cut, seed):
+    """synth_clip frames, then from frame ``cut`` a new scene: uniform noise panning by whole
+    pixels -- the old scene predicts none of it (the cut frame's inter cost is ~intra, a cut
+    even right after a key frame under x264's scene-cut bias), while the frames after the cut
+    predict each other exactly."""
+    import numpy as np
+    import torch
+    from govideocompressor_amd.models.h264_gpu import synth_clip
+    a = synth_clip(B, F, w, h, seed=seed)
+    rng = np.random.default_rng(seed)
+    out = []
+    for c, pa in enumerate(a):
+        ph, pw = pa.shape[2], pa.shape[3]
+        sh = 1 if c == 0 else 2
+        canvas = rng.integers(0, 256, (B, ph + 2 * F, pw + 4 * F), dtype=np.uint8)
+        new = np.stack([canvas[:, t // sh:t // sh + ph, (2 * t) // sh:(2 * t) // sh + pw] for t in range(F)], axis=1)
+        new = torch.from_numpy(np.ascontiguousarray(new)).to(pa.device)
+        out.append(torch.cat([pa[:, :cut], new[:, cut:]], dim=1).contiguous())
+    return out

@@ -39,6 +39,7 @@ CONFIGS = {
     "slices4": dict(slices=4),
     "noseed": dict(lowres_seed=False),
     "trellis1": dict(trellis=1),  # round 3's trellis scope (4x4 luma only)
+    "bf0": dict(bframes=0),       # P pictures only
     # fast spatial direct with the fixed GOP pattern: exact motion re-predicted (tol -1, round 4's
     # first version) / estimate kept as explicit motion beyond 0 / 4 quarter samples; b-pyramid
     "sp_repredict": dict(direct="spatial", spatial_fix_tol=-1),
