@@ -256,23 +256,31 @@ def test_gpu_bframes_roundtrip(host, bframes, frames):
 
 
 def test_gpu_bframes_save_bits(host):
-    """x264's --bframes 3 trade at fixed QP (B pictures at +pbratio) on 1080p bench content: a
-    real saving -- at least 8 % fewer bits -- for at most 1 dB of PSNR-Y (at CIF the same
-    content moves too fast relative to the picture for 4-picture anchor distances to pay;
-    the 1080p RD tables in profiles/ measure the BD-rate per content class)."""
+    """x264's --bframes 3 on 1080p bench content in CRF mode (B pictures at their references'
+    QP + pbratio): a real saving -- the rate at equal PSNR-Y, interpolated between CRF 21 and
+    27 (log rate vs PSNR), at least 10 % below P-only (the content suite measures -36 % on this
+    class: profiles/r4_bframes_rd.md)."""
     import torch
     from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
 
-    y, u, v = synth_clip(2, 13, 1920, 1080, seed=7)
-    out = {}
+    y, u, v = synth_clip(2, 25, 1920, 1080, seed=7)
+    pts = {}
     for nb in (0, 3):
-        enc = GpuH264Encoder(H264Params(width=1920, height=1080, crf=None, qp=27, bframes=nb), slots=2)
-        res = enc.encode(y, u, v)
-        out[nb] = (sum(len(r.bitstream) for r in res), float(np.mean([r.psnr_y for r in res])))
+        enc = GpuH264Encoder(H264Params(width=1920, height=1080, crf=21.0, bframes=nb), slots=2)
+        pts[nb] = []
+        for crf in (21.0, 27.0):
+            enc.p.crf = crf
+            res = enc.encode(y, u, v)
+            pts[nb].append((float(np.log(sum(len(r.bitstream) for r in res))), float(np.mean([r.psnr_y for r in res]))))
         enc.close()
     torch.cuda.synchronize()
-    assert out[3][0] < 0.92 * out[0][0], out
-    assert out[3][1] > out[0][1] - 1.0, out
+    # log rate of the B configuration at the P-only configuration's mean PSNR
+    (r0a, q0a), (r0b, q0b) = pts[0]
+    (r3a, q3a), (r3b, q3b) = pts[3]
+    q = 0.5 * (q0a + q0b)
+    lr0 = r0a + (r0b - r0a) * (q - q0a) / (q0b - q0a)
+    lr3 = r3a + (r3b - r3a) * (q - q3a) / (q3b - q3a)
+    assert np.exp(lr3 - lr0) < 0.90, pts
 
 
 def test_gpu_short_segment_display_prefix(host):
