@@ -124,25 +124,38 @@ def main() -> None:
 
     def run_steps(first: int, n: int, metrics_first: bool = False):
         """n steps: synthesize (new content) -> lookahead + encode -> merge on rank 0.
-        Step k + 1's input synthesis and lookahead run on side streams while step k encodes
-        (every one of them inside the n steps: nothing is prepared beyond the last step), and
-        the merge of step k overlaps the encode of step k + 1."""
+        Step k + 1's input synthesis and lookahead run on a side stream while step k encodes,
+        step k's entropy tail overlaps step k + 1's first kernels (encode_async), and the
+        merge of step k overlaps the encode of step k + 1 -- all inside the n steps: nothing is
+        prepared beyond the last step, and the last step is collected before the clock stops."""
         clip, ev = synth_async(first)
         ana = enc.analyse_async(clip[0], stream=synth_stream)
-        fut = None
+        fut = prev = first_res = res = None
+
+        def collect(pend):
+            # step k - 1's results once step k is issued: its last coder groups and NAL
+            # wrapping ran beside step k's first kernels (encode_async)
+            nonlocal fut, first_res, res
+            res = pend.result()
+            if fut is not None:
+                fut.result()
+            fut = merge_pool.submit(merge, res)
+            if first_res is None:
+                first_res = res
+
         for k in range(n):
             (y, u, v), cur_ev, cur_ana = clip, ev, ana
             if k + 1 < n:
                 clip, ev = synth_async(first + k + 1)
                 ana = enc.analyse_async(clip[0], stream=synth_stream)
             torch.cuda.current_stream().wait_event(cur_ev)
-            res = enc.encode(y, u, v, idr_base=env.rank * B, metrics=(metrics_first and k == 0), analysis=cur_ana)
+            pend = enc.encode_async(y, u, v, idr_base=env.rank * B, metrics=(metrics_first and k == 0),
+                                    analysis=cur_ana)
             del y, u, v
-            if fut is not None:
-                fut.result()
-            fut = merge_pool.submit(merge, res)
-            if k == 0:
-                first_res = res
+            if prev is not None:
+                collect(prev)
+            prev = pend
+        collect(prev)
         merged = fut.result()
         return first_res, res, merged
 

@@ -300,6 +300,49 @@ class CabacPoolExhausted(RuntimeError):
     """The batch's CABAC symbols outgrew the pool (very low QPs); encode() grows it and retries."""
 
 
+class PendingEncode:
+    """A batch issued by :meth:`GpuH264Encoder.encode_async`."""
+
+    def __init__(self, enc, finish, planes, kw, results=None):
+        self._enc, self._finish, self._planes, self._kw = enc, finish, planes, kw
+        self._res = results
+        self._exc: BaseException | None = None
+        self._done = finish is None
+
+    def done(self) -> bool:
+        return self._done
+
+    def _complete(self) -> None:
+        """Run the batch's finish once; a pool overflow is kept for result() to redo."""
+        if self._done:
+            return
+        try:
+            self._res = self._finish()
+        except BaseException as e:  # noqa: BLE001
+            self._exc = e
+        self._done = True
+        self._finish = None
+        if self in self._enc._inflight:
+            self._enc._inflight.remove(self)
+
+    def result(self) -> list:
+        self._complete()
+        if isinstance(self._exc, CabacPoolExhausted):
+            # drain the other batch in flight (its copy threads read the pools), grow, redo
+            enc = self._enc
+            for other in list(enc._inflight):
+                other._complete()
+            torch.cuda.synchronize(enc.dev)
+            enc._alloc_cabac(enc.cab_G, grow=enc.cab_grow * 4)
+            enc.stats["cabac_pool_regrow"] = enc.stats.get("cabac_pool_regrow", 0) + 1
+            self._exc = None
+            self._res = enc.encode(*self._planes, **self._kw)
+        if self._exc is not None:
+            raise self._exc
+        self._planes = None
+        return self._res
+
+
 class GpuH264Encoder:
     """Batched gfx950 H.264 encoder: Main profile with GPU CABAC (default) or Constrained
     Baseline with GPU CAVLC; ``entropy="cpu"`` codes the slices with the host writers."""
@@ -408,7 +451,14 @@ class GpuH264Encoder:
         self.qp_flags = torch.zeros((B, nmb), dtype=u8, device=dev)       # MB carries mb_qp_delta
         self.intra_count = torch.zeros((B,), dtype=i32, device=dev)
         self.qp = torch.zeros((B,), dtype=i32, device=dev)
-        self.err = torch.zeros((1,), dtype=i32, device=dev)
+        # error flags, one buffer per batch in flight (encode_async: the next batch zeroes its own
+        # while the previous one's coder may still report); pinned host copies of them
+        self.err_bufs = [torch.zeros((1,), dtype=i32, device=dev) for _ in range(2)]
+        self.err = self.err_bufs[0]
+        self.h_err = [torch.zeros((1,), dtype=i32).pin_memory() for _ in range(2)]
+        self._batch_no = 0
+        self._ring_last: list = [None, None]  # per CABAC ring: (copied event, future, wrap futures) of its last group
+        self._inflight: list = []             # encode_async batches not yet finished (oldest first)
         self.p_intra_mbs = torch.zeros((), dtype=torch.int64, device=dev)  # intra MBs coded in P frames
         self.far_ref_mbs = torch.zeros((), dtype=torch.int64, device=dev)  # P MBs choosing RefPicList0[1 ..]
         self.sfix_mbs = torch.zeros((), dtype=torch.int64, device=dev)  # fast spatial direct: MBs re-predicted
@@ -960,9 +1010,10 @@ class GpuH264Encoder:
                            self.cab_total[r][j * BS:].data_ptr(), P(qp_dev), pics[0].slice_type, 1, 1,
                            int(self.p.eff_t8x8()), P(self.err), self.copy_stream.cuda_stream, route, self.slice_rows)
 
-    def _gpu_cabac_code(self, g: int, t0: int, n: int, qps_d: torch.Tensor):
+    def _gpu_cabac_code(self, g: int, t0: int, n: int, qps_d: torch.Tensor, err_to: torch.Tensor | None = None):
         """Arithmetic-code the n frame steps t0 .. t0 + n - 1 of a group (n * B slices) on
-        the entropy stream, after their binarisation; sizes go to pinned host memory."""
+        the entropy stream, after their binarisation; sizes go to pinned host memory (and,
+        for a batch's last group, its error flags to ``err_to``)."""
         BS = self.B * self.S
         r = g & 1
         self.cab_bin_done[r].record(self.copy_stream)
@@ -978,6 +1029,8 @@ class GpuH264Encoder:
                                 es.cuda_stream, P(self.h_cab_out[r]), self.cab_host_cap)
             self.h_cab_bytes[r][: n * BS].copy_(self.cab_bytes[r][: n * BS], non_blocking=True)
             self.h_pool_used[r].copy_(self.cab_pool_used[r:r + 1], non_blocking=True)
+            if err_to is not None:
+                err_to.copy_(self.err, non_blocking=True)
             self.cab_done[r].record(es)
 
     def _copy_out_group(self, g: int, t0: int, n: int, copied, wrap_futs, steps_pics: list[list[PicPlan]], groups):
@@ -1251,6 +1304,7 @@ class GpuH264Encoder:
         function of the inputs, so the retry gives the same bytes a big pool would)."""
         if isinstance(analysis, cf.Future):
             analysis = analysis.result()
+        self.drain()
         for attempt in range(3):
             try:
                 return self._encode(y, u, v, idr_base, keep_recon, metrics, idr_ids, qps, anchors_at, qp_delta,
@@ -1263,9 +1317,37 @@ class GpuH264Encoder:
                 self.stats["cabac_pool_regrow"] = self.stats.get("cabac_pool_regrow", 0) + 1
         raise AssertionError("unreachable")
 
+    def encode_async(self, y: torch.Tensor, u: torch.Tensor, v: torch.Tensor, **kw) -> "PendingEncode":
+        """Issue a batch and return before its last arithmetic-coder groups, NAL wrapping and
+        result assembly finish (GPU CABAC; other entropy paths complete here).  The batch's
+        tail then overlaps the next batch's first steps -- one 256 x 60 1080p batch spends
+        ~100 ms in that tail with the compute stream idle.  At most two batches are in
+        flight: issuing a third completes the oldest.  ``PendingEncode.result()`` gives what
+        :meth:`encode` would have returned (a symbol-pool overflow re-encodes the batch
+        synchronously with a grown pool).  ``kw``: :meth:`encode`'s keyword arguments."""
+        ana = kw.pop("analysis", None)
+        if isinstance(ana, cf.Future):
+            ana = ana.result()
+        while len(self._inflight) >= 2:
+            self._inflight[0].result()
+        if not (self.entropy == "gpu" and self.p.cabac):
+            return PendingEncode(self, None, (y, u, v), dict(kw, analysis=ana), self.encode(y, u, v, analysis=ana, **kw))
+        args = dict(kw)
+        fin = self._encode(y, u, v, args.get("idr_base", 0), args.get("keep_recon", False), args.get("metrics", True),
+                           args.get("idr_ids"), args.get("qps"), args.get("anchors_at", ()), args.get("qp_delta"),
+                           ana, defer=True)
+        pend = PendingEncode(self, fin, (y, u, v), dict(kw, analysis=ana))
+        self._inflight.append(pend)
+        return pend
+
+    def drain(self) -> None:
+        """Complete every batch issued by :meth:`encode_async` (their results stay available)."""
+        while self._inflight:
+            self._inflight[0].result()
+
     def _encode(self, y: torch.Tensor, u: torch.Tensor, v: torch.Tensor, idr_base: int = 0,
                 keep_recon: bool = False, metrics: bool = True, idr_ids: list[int] | None = None,
-                qps=None, anchors_at=(), qp_delta=None, analysis=None) -> list[SegmentResult]:
+                qps=None, anchors_at=(), qp_delta=None, analysis=None, defer: bool = False):
         """Encode B segments of F frames each.
 
         y: [B, F, h, w] uint8 (device), u/v: [B, F, h/2, w/2].  Each slot's output is a
@@ -1281,6 +1363,9 @@ class GpuH264Encoder:
         (:mod:`govideocompressor_amd.rc.abr`: -b:v, -pass 2, VBV).
         ``analysis``: this batch's lookahead state from :meth:`analyse_async` (computed while
         the previous batch encoded); None = run the lookahead here.
+        ``defer`` (GPU CABAC): return a callable that completes the batch (waits for its coder
+        and NAL wrapping, checks errors, builds the results) instead of the results, so the
+        next batch can be issued while this one's last arithmetic-coder groups still run.
         """
         B, F = y.shape[0], y.shape[1]
         if B != self.B:
@@ -1356,6 +1441,9 @@ class GpuH264Encoder:
             for t, st in enumerate(steps):
                 if self._wp_steps[t] is not None:
                     st["wp"], st["wp_src"] = self._wp_steps[t]
+        bno = self._batch_no
+        self._batch_no += 1
+        self.err = self.err_bufs[bno & 1]
         self.err.zero_()
         sse = torch.zeros((F, B, 3), dtype=torch.int64, device=self.dev)   # coding order
         ssim = torch.zeros((F, B), dtype=torch.float32, device=self.dev)
@@ -1399,13 +1487,20 @@ class GpuH264Encoder:
                 gi, jj = step_group[t]
                 if jj == 0 and gi >= 2:
                     wait_group(gi - 2)  # ring gi % 2 is free again
+                elif jj == 0 and self._ring_last[gi & 1] is not None:
+                    # the ring's last group of the previous batch (encode_async)
+                    ev, fut, _ = self._ring_last[gi & 1]
+                    while not ev.wait(0.5):
+                        if fut.done() and fut.exception() is not None:
+                            break
             elif self.entropy == "gpu" and t >= 2:
                 wait_copied(t - 2)
             elif pending[k] is not None:
                 outs[t - 2] = pending[k].result()
                 pending[k] = None
             self.timings["host_blocked_s"] = self.timings.get("host_blocked_s", 0.0) + time.perf_counter() - tw
-            main.wait_event(self.copy_done[k]) if t >= 2 else None
+            # (steps 0 / 1: the previous batch's last steps, when it is still in flight)
+            main.wait_event(self.copy_done[k])
             self._prep_step(y, u, v, orders[:, t], orders_d[t])
             st["disp_d"] = orders_d[t]
             self.qp.copy_(qps_d[t])
@@ -1438,83 +1533,124 @@ class GpuH264Encoder:
             if cabac_gpu:
                 if jj == groups[gi][1] - 1:
                     t0 = groups[gi][0]
+                    tw = time.perf_counter()
                     if gi >= 2:
                         # this group's compaction overwrites host buffer gi % 2: group gi - 2's
                         # wraps must be done reading it (copied[gi - 2] was waited for above)
-                        tw = time.perf_counter()
                         a0, an = groups[gi - 2]
                         for tt in range(a0, a0 + an):
                             wrap_futs[tt].result()
-                        self.timings["host_blocked_s"] += time.perf_counter() - tw
-                    self._gpu_cabac_code(gi, t0, t - t0 + 1, qps_ls_d)
+                    elif self._ring_last[gi & 1] is not None:
+                        for f in self._ring_last[gi & 1][2]:
+                            try:
+                                f.result()
+                            except Exception:  # noqa: BLE001  (reported by that batch's finish)
+                                pass
+                        self._ring_last[gi & 1] = None
+                    self.timings["host_blocked_s"] += time.perf_counter() - tw
+                    self._gpu_cabac_code(gi, t0, t - t0 + 1, qps_ls_d,
+                                         err_to=self.h_err[bno & 1] if gi == ngroups - 1 else None)
                     group_futs[gi] = self.copy_pool.submit(self._copy_out_group, gi, t0, t - t0 + 1, group_copied,
                                                            wrap_futs, steps_pics, groups)
             elif self.entropy == "gpu":
                 copy_futs[t] = self.copy_pool.submit(self._copy_out, t, k, pics, copied, wrap_futs)
             else:
                 pending[k] = self.pool.submit(self._write_slices, k, t, pics, qpt, idr_ids)
-        if cabac_gpu:
-            for f in group_futs:
-                f.result()
-            for t in range(F):
-                outs[t] = wrap_futs[t].result()
-        elif self.entropy == "gpu":
-            for t in range(F):
-                copy_futs[t].result()
-            for t in range(F):
-                outs[t] = wrap_futs[t].result()
-        for t in range(max(0, F - 2), F):
-            k = t & 1
-            if pending[k] is not None:
-                outs[t] = pending[k].result()
-                pending[k] = None
-        torch.cuda.synchronize(self.dev)
-        if F > 1:
-            self.stats["p_intra_ratio"] = float(self.p_intra_mbs.item()) / (B * (F - 1) * self.nmb)
-            n_p = sum(1 for plan in plans for pic in plan if pic.kind == "P")
-            if self.nref > 1 and n_p:
-                # share of P-picture MBs (inter decisions before the intra override) on a farther picture
-                self.stats["p_far_ref_ratio"] = float(self.far_ref_mbs.item()) / (n_p * self.nmb)
-            nbp = sum(1 for plan in plans for pic in plan if pic.kind == "B")
-            self.stats["b_ratio"] = nbp / float(B * F)
-            if nbp and self.p.direct == "spatial":
-                # fast spatial direct: share of B-picture MBs whose direct motion the exact
-                # decoding-order pass changed after they were priced on the estimate
-                self.stats["spatial_fix_ratio"] = float(self.sfix_mbs.item()) / (nbp * self.nmb)
-                self.stats["spatial_conv_ratio"] = float(self.sconv_mbs.item()) / (nbp * self.nmb)
-                self.sfix_mbs.zero_()
-                self.sconv_mbs.zero_()
+        # ---- end of the batch's issue: snapshot its counters (async) so the next batch can
+        # reuse the accumulators, and note which groups last used the two CABAC rings
+        B_ = B
+        counters = torch.stack([self.p_intra_mbs, self.far_ref_mbs, self.sfix_mbs, self.sconv_mbs]).to(torch.int64)
         self.p_intra_mbs.zero_()
         self.far_ref_mbs.zero_()
-        err = int(self.err.item())
-        if err & 4:
-            raise CabacPoolExhausted(f"GPU CABAC: symbol pool exhausted (err={err:#x})")
-        if err & 14:
-            raise RuntimeError(f"GPU CABAC failed (err={err:#x}: 4 = symbol pool exhausted, 8 = coder error)")
-        if err != 0:
-            raise RuntimeError("wavefront progress timeout in an encode kernel")
-        ps = self.parameter_sets()
-        results = []
-        sse_h = sse.cpu().numpy().astype(np.float64)
-        ssim_h = ssim.cpu().numpy()
-        npx = self.p.width * self.p.height
-        nwin = (self.p.width // 8) * (self.p.height // 8)
-        for b in range(B):
-            nals = [outs[t][b][0] for t in range(F)]
-            r = SegmentResult(frames=F, nals=nals, bits=[outs[t][b][1] for t in range(F)], header=ps,
-                              order=orders[b].tolist())
-            if metrics:
-                def psnr(ssev, n):
-                    mse = ssev / n
-                    return 100.0 if mse <= 1e-10 else 10.0 * math.log10(255.0 ** 2 / mse)
-                r.psnr_y = float(np.mean([psnr(sse_h[t, b, 0], npx) for t in range(F)]))
-                r.psnr_u = float(np.mean([psnr(sse_h[t, b, 1], npx / 4) for t in range(F)]))
-                r.psnr_v = float(np.mean([psnr(sse_h[t, b, 2], npx / 4) for t in range(F)]))
-                r.ssim_y = float(ssim_h[:, b].sum() / (F * max(1, nwin)))
-            results.append(r)
-        if keep_recon:
-            self.last_recon = recons
-        return results
+        self.sfix_mbs.zero_()
+        self.sconv_mbs.zero_()
+        h_counters = torch.empty((4,), dtype=torch.int64).pin_memory()
+        h_counters.copy_(counters, non_blocking=True)
+        h_sse = h_ssim = None
+        if metrics:
+            h_sse = torch.empty(sse.shape, dtype=sse.dtype).pin_memory()
+            h_ssim = torch.empty(ssim.shape, dtype=ssim.dtype).pin_memory()
+            h_sse.copy_(sse, non_blocking=True)
+            h_ssim.copy_(ssim, non_blocking=True)
+        batch_done = torch.cuda.Event()
+        batch_done.record(main)
+        if cabac_gpu:
+            for gi in range(max(0, ngroups - 2), ngroups):
+                a0, an = groups[gi]
+                self._ring_last[gi & 1] = (group_copied[gi], group_futs[gi], wrap_futs[a0:a0 + an])
+        # tensors the in-flight kernels and copy threads still read (freed only after finish)
+        keep = (y, u, v, steps, qps_d, qps_ls_d, orders_d, cuts_d, self._route_dev, self._wp_steps, self._la_mv,
+                self._mbtree, sse, ssim, counters, analysis)
+        err_h = self.h_err[bno & 1]
+
+        def finish() -> list[SegmentResult]:
+            if cabac_gpu:
+                for f in group_futs:
+                    f.result()
+                for t in range(F):
+                    outs[t] = wrap_futs[t].result()
+            elif self.entropy == "gpu":
+                for t in range(F):
+                    copy_futs[t].result()
+                for t in range(F):
+                    outs[t] = wrap_futs[t].result()
+            for t in range(max(0, F - 2), F):
+                k = t & 1
+                if pending[k] is not None:
+                    outs[t] = pending[k].result()
+                    pending[k] = None
+            batch_done.synchronize()
+            nonlocal keep
+            keep = None  # released only now: the batch's kernels have finished
+            c = h_counters.numpy()
+            if F > 1:
+                self.stats["p_intra_ratio"] = float(c[0]) / (B_ * (F - 1) * self.nmb)
+                n_p = sum(1 for plan in plans for pic in plan if pic.kind == "P")
+                if self.nref > 1 and n_p:
+                    # share of P-picture MBs (inter decisions before the intra override) on a farther picture
+                    self.stats["p_far_ref_ratio"] = float(c[1]) / (n_p * self.nmb)
+                nbp = sum(1 for plan in plans for pic in plan if pic.kind == "B")
+                self.stats["b_ratio"] = nbp / float(B_ * F)
+                if nbp and self.p.direct == "spatial":
+                    # fast spatial direct: share of B-picture MBs whose direct motion the exact
+                    # decoding-order pass changed after they were priced on the estimate / made explicit
+                    self.stats["spatial_fix_ratio"] = float(c[2]) / (nbp * self.nmb)
+                    self.stats["spatial_conv_ratio"] = float(c[3]) / (nbp * self.nmb)
+            # the batch's error flags: with the GPU coder from its last group (copied behind the
+            # coder on the entropy stream), else from the device after the batch's own work
+            err = int(err_h[0]) if cabac_gpu else int(self.err_bufs[bno & 1].cpu()[0])
+            if err & 4:
+                raise CabacPoolExhausted(f"GPU CABAC: symbol pool exhausted (err={err:#x})")
+            if err & 14:
+                raise RuntimeError(f"GPU CABAC failed (err={err:#x}: 4 = symbol pool exhausted, 8 = coder error)")
+            if err != 0:
+                raise RuntimeError("wavefront progress timeout in an encode kernel")
+            ps = self.parameter_sets()
+            results = []
+            npx = self.p.width * self.p.height
+            nwin = (self.p.width // 8) * (self.p.height // 8)
+            sse_h = h_sse.numpy().astype(np.float64) if metrics else None
+            ssim_h = h_ssim.numpy() if metrics else None
+            for b in range(B_):
+                nals = [outs[t][b][0] for t in range(F)]
+                r = SegmentResult(frames=F, nals=nals, bits=[outs[t][b][1] for t in range(F)], header=ps,
+                                  order=orders[b].tolist())
+                if metrics:
+                    def psnr(ssev, n):
+                        mse = ssev / n
+                        return 100.0 if mse <= 1e-10 else 10.0 * math.log10(255.0 ** 2 / mse)
+                    r.psnr_y = float(np.mean([psnr(sse_h[t, b, 0], npx) for t in range(F)]))
+                    r.psnr_u = float(np.mean([psnr(sse_h[t, b, 1], npx / 4) for t in range(F)]))
+                    r.psnr_v = float(np.mean([psnr(sse_h[t, b, 2], npx / 4) for t in range(F)]))
+                    r.ssim_y = float(ssim_h[:, b].sum() / (F * max(1, nwin)))
+                results.append(r)
+            if keep_recon:
+                self.last_recon = recons
+            return results
+
+        if defer and cabac_gpu:
+            return finish
+        return finish()
 
     def close(self):
         self.pool.shutdown(wait=True)

@@ -543,3 +543,29 @@ def _cut_clip(B, F, w, h, cut, seed):
         new = torch.from_numpy(np.ascontiguousarray(new)).to(pa.device)
         out.append(torch.cat([pa[:, :cut], new[:, cut:]], dim=1).contiguous())
     return out
+
+
+@pytest.mark.parametrize("tiny_pool", [False, True])
+def test_gpu_encode_async_same_bytes(monkeypatch, tiny_pool):
+    """encode_async (bench.py: batch k's entropy tail overlaps batch k + 1's first kernels;
+    the CABAC rings, error flags and counters cross the batch boundary) gives the bytes of
+    the synchronous encode, batch by batch -- also when a batch overflows the symbol pool
+    and is re-encoded with a grown pool while the next one is in flight."""
+    import torch
+    from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
+
+    clips = [synth_clip(3, 10, 320, 240, seed=s, kind=k) for s, k in ((11, "default"), (12, "cuts"), (13, "fade"))]
+    ref_enc = GpuH264Encoder(H264Params(width=320, height=240, crf=23), slots=3)
+    ref = [[r.bitstream for r in ref_enc.encode(*c, metrics=False)] for c in clips]
+    ref_enc.close()
+    if tiny_pool:
+        monkeypatch.setenv("MIVC_CABAC_SYMS_PER_MB", "2")
+        monkeypatch.setenv("MIVC_CABAC_PEAK_SYMS_PER_MB", "4")
+    enc = GpuH264Encoder(H264Params(width=320, height=240, crf=23), slots=3)
+    pend = [enc.encode_async(*c, metrics=False) for c in clips]
+    got = [[r.bitstream for r in p.result()] for p in pend]
+    torch.cuda.synchronize()
+    assert got == ref
+    if tiny_pool:
+        assert enc.stats.get("cabac_pool_regrow", 0) >= 1
+    enc.close()
