@@ -112,6 +112,7 @@ def main() -> None:
             return merger.run([r.parts() for r in res])
 
     synth_stream = torch.cuda.Stream(device=env.device)
+    step_wall: list[float] = []  # host time at which each step's results were complete
 
     def synth_async(step: int):
         """Input of a later step on a side stream (it overlaps the current step's encode the way
@@ -137,6 +138,7 @@ def main() -> None:
             # wrapping ran beside step k's first kernels (encode_async)
             nonlocal fut, first_res, res
             res = pend.result()
+            step_wall.append(time.perf_counter())
             if fut is not None:
                 fut.result()
             fut = merge_pool.submit(merge, res)
@@ -179,6 +181,8 @@ def main() -> None:
     D.barrier(env)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    step_wall.clear()
+    step_wall.append(time.perf_counter())
     _, res, merged = run_steps(0, a.steps)
     torch.cuda.synchronize()
     D.barrier(env)
@@ -221,6 +225,9 @@ def main() -> None:
                         "measured_on": "first warmup step (untimed)" if q else "n/a (no warmup step)",
                         "merged_bytes": len(merged) if merged is not None else 0},
             "timings_rank0_s": {k: round(v, 3) for k, v in enc.timings.items()},
+            # interval between consecutive timed steps' completion on rank 0 (the first includes
+            # the first input's synthesis and lookahead; the last is not shortened by the merge)
+            "step_wall_ms_rank0": [round(1000.0 * (b - a_), 1) for a_, b in zip(step_wall, step_wall[1:])],
             "stage_device_ms_per_step_rank0": {"measured_on": "warmup steps (untimed)", **stage_ms},
             "encoder_stats_rank0": {k: round(v, 4) for k, v in enc.stats.items()},
             "memory_rank0": _memory(env, merged),

@@ -82,6 +82,20 @@ __device__ __forceinline__ float trellis_level_bits(int l, bool seen) {
 __device__ __forceinline__ void trellis_lite4x4(const int (&w)[16], int (&lv)[16], const int (&mf)[3], int qbits,
                                                 float lam, int start = 0) {
   constexpr float kInvNorm[3] = {1.0f / 16.0f, 1.0f / 100.0f, 1.0f / 40.0f};
+  // a block whose every rounded quotient is 0 quantises to zeros whatever the choice: most
+  // blocks of B pictures -- skip the pass (wave-wide when every lane's block is such)
+  int zmax = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int r = h264::kZigzag4x4[i];
+    const int a = w[r] < 0 ? -w[r] : w[r];
+    if (i >= start) zmax |= (a * mf[h264::kPosClass[r]] + (1 << (qbits - 1))) >> qbits;
+  }
+  if (zmax == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) lv[r] = 0;
+    return;
+  }
   bool seen = false;
 #pragma unroll
   for (int i = 15; i >= 0; --i) {
@@ -120,6 +134,14 @@ __device__ __forceinline__ void trellis_lite4x4(const int (&w)[16], int (&lv)[16
 // lambda / Qstep^2 = 0.85 * 2^((QP - 12) / 3) / (0.390625 * 2^(QP / 3)) = 0.136 per bit (QP-free).
 // seen: a later chunk of the block keeps a non-zero level.  lv keeps its sign from z.
 __device__ __forceinline__ void trellis_lite8_chunk(const float (&z)[16], int (&lv)[16], float lamq, bool seen) {
+  float zmax = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) zmax = fmaxf(zmax, fabsf(z[i]));
+  if (zmax < 0.5f) {  // every rounded quotient is 0
+#pragma unroll
+    for (int i = 0; i < 16; ++i) lv[i] = 0;
+    return;
+  }
 #pragma unroll
   for (int i = 15; i >= 0; --i) {
     const float az = fabsf(z[i]);

@@ -40,6 +40,7 @@ CONFIGS = {
     "noseed": dict(lowres_seed=False),
     "trellis1": dict(trellis=1),  # round 3's trellis scope (4x4 luma only)
     "bf0": dict(bframes=0),       # P pictures only
+    "la4": dict(la_range=4),      # lowres search +-4 around the quarter-resolution seed (default +-6)
     # fast spatial direct with the fixed GOP pattern: exact motion re-predicted (tol -1, round 4's
     # first version) / estimate kept as explicit motion beyond 0 / 4 quarter samples; b-pyramid
     "sp_repredict": dict(direct="spatial", spatial_fix_tol=-1),
