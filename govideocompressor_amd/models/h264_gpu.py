@@ -63,7 +63,10 @@ class H264Params:
     vui: bool = True
     # CRF per-frame QPs from the GPU lookahead (rc/lookahead.py); False = flat CRF QP
     lookahead: bool = True
-    la_range: int = 6
+    # lowres search range around the quarter-resolution seed (rc/lookahead.py RANGES): +-4 and
+    # +-6 are BD-rate-identical on the content suite (-0.01 %, profiles/r4_la_range_rd.json),
+    # +-4 searches 81 positions instead of 169
+    la_range: int = int(os.environ.get("MIVC_LA_RANGE", 4))
     # x264 --scenecut: a P frame whose lowres inter cost saves less than this percent of
     # its intra cost is coded all-intra (I4x4/I16x16 MBs) at the I-frame QP; 0 disables
     scenecut: int = 40
