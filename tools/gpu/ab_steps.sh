@@ -1,7 +1,7 @@
 #!/bin/bash
 # Same-box A/B of bench.py settings: every setting runs `bench.py --steps S --warmup W` once per
 # round, settings interleaved (A B C A B C ...), so box-to-box spread cancels.
-#   tools/gpu/ab_steps.sh OUTDIR ROUNDS STEPS "label=ENV=V ENV2=V2" "label2=" ...
+#   [AB_ARGS="--width 3840 --height 2160 ..."] tools/gpu/ab_steps.sh OUTDIR ROUNDS STEPS "label=ENV=V ENV2=V2" "label2=" ...
 set -o pipefail
 export TMPDIR=/tmp
 out=$1; rounds=$2; steps=$3; shift 3
@@ -9,7 +9,7 @@ mkdir -p "$out"
 for r in $(seq 1 "$rounds"); do
   for spec in "$@"; do
     label=${spec%%=*}; envs=${spec#*=}
-    env $envs timeout -k 10 240 python bench.py --steps "$steps" --warmup 2 --no-quality > "$out/$label.r$r.log" 2>&1
+    env $envs timeout -k 10 240 python bench.py --steps "$steps" --warmup 2 --no-quality $AB_ARGS > "$out/$label.r$r.log" 2>&1
     rc=$?
     echo "$label round $r rc=$rc $(grep -h '"metric"' "$out/$label.r$r.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])' 2>/dev/null)" | tee -a "$out/ab.txt"
     case $rc in 0) ;; *) exit $rc ;; esac
