@@ -664,7 +664,13 @@ __global__ __launch_bounds__(64 * kIntraWaves) void encode_intra_wavefront(Intra
   __shared__ IntraShared SS[kIntraWaves];
   __shared__ int prog[kMaxRows];
   const Geom& g = a.g;
-  const int slot = blockIdx.x;
+  // one workgroup per slice: intra prediction never crosses a slice's top edge, so the slices
+  // of a picture are independent wavefronts (a 4K batch of 64 slots in 4 slices fills the chip
+  // with 256 workgroups instead of 64)
+  const int per = a.slice_rows > 0 ? (g.hmb + a.slice_rows - 1) / a.slice_rows : 1;
+  const int slot = blockIdx.x / per, sl = blockIdx.x - slot * per;
+  const int y_begin = a.slice_rows > 0 ? sl * a.slice_rows : 0;
+  const int y_end = a.slice_rows > 0 ? min(g.hmb, y_begin + a.slice_rows) : g.hmb;
   if (!route_active(a.rt, slot, -1)) return;  // uniform per workgroup
   if (a.intra_flag && a.intra_count[slot] == 0) return;
   for (int i = threadIdx.x; i < g.hmb; i += blockDim.x) prog[i] = 0;
@@ -679,7 +685,7 @@ __global__ __launch_bounds__(64 * kIntraWaves) void encode_intra_wavefront(Intra
 #pragma unroll
     for (int x = 0; x < 4; ++x) tapw[x] = h264::kI4Taps[m][r * 4 + x];
   }
-  for (int y = w; y < g.hmb; y += kIntraWaves) {
+  for (int y = y_begin + w; y < y_end; y += kIntraWaves) {
     if (!a.intra_flag) {  // I frame: every MB
       for (int x = 0; x < g.wmb; ++x) {
         if (top_in_slice(y, a.slice_rows)) row_wait(prog, y - 1, min(x + 2, g.wmb), a.err);
@@ -742,7 +748,9 @@ extern "C" void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t*
   a.err = err;
   a.use_i4x4 = use_i4x4;
   a.use_i8x8 = use_i8x8;
-  hipLaunchKernelGGL(encode_intra_wavefront, dim3(B), dim3(64 * kIntraWaves), 0, static_cast<hipStream_t>(stream), a);
+  const int per = slice_rows > 0 ? (hmb + slice_rows - 1) / slice_rows : 1;
+  hipLaunchKernelGGL(encode_intra_wavefront, dim3(B * per), dim3(64 * kIntraWaves), 0, static_cast<hipStream_t>(stream),
+                     a);
 }
 
 #ifdef MIVC_INTRA_PROFILE
