@@ -705,9 +705,11 @@ std::vector<uint8_t> CpuEncoder::encode(const uint8_t* frames, int nframes, int 
   recon_unf_.clear();
   size_t fsize = static_cast<size_t>(cfg_.width) * cfg_.height * 3 / 2;
   int frame_num = 0;
+  // keyint <= 0: the first picture is the only IDR (as the GPU encoders' keyint 0)
+  const int keyint = cfg_.keyint > 0 ? cfg_.keyint : std::max(1, nframes);
   for (int f = 0; f < nframes; ++f) {
     pad_frame(frames + f * fsize, cfg_.width, cfg_.height, src);
-    bool idr = (f % cfg_.keyint) == 0;
+    bool idr = (f % keyint) == 0;
     if (idr) frame_num = 0;
     int qp = std::max(0, std::min(51, cfg_.qp + (idr ? -3 : 0)));
     fe.encode(src, idr ? nullptr : &ref, idr, qp);
@@ -716,7 +718,7 @@ std::vector<uint8_t> CpuEncoder::encode(const uint8_t* frames, int nframes, int 
     sh.nal_ref_idc = idr ? 3 : 2;
     sh.slice_type = idr ? SLICE_I : SLICE_P;
     sh.frame_num = frame_num;
-    sh.idr_pic_id = (idr_pic_id + f / cfg_.keyint) & 0xFFFF;
+    sh.idr_pic_id = (idr_pic_id + f / keyint) & 0xFFFF;
     sh.slice_qp_delta = qp - pps.pic_init_qp;
     sh.disable_deblocking_filter_idc = cfg_.deblock ? 0 : 1;
     std::vector<uint8_t> nal =
