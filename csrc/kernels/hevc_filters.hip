@@ -378,79 +378,85 @@ __global__ __launch_bounds__(256) void hevc_sao(HevcSaoArgs a) {
     if (tid < 3) S.band[tid] = t0->sao_band[tid];
   }
   if (a.mode != 2) {
-  // ---- decision (thread 0: luma, thread 1: chroma pair)
-  if (tid < 2) {
-    const int qp = a.qp[static_cast<size_t>(slot) * a.wctb * a.hctb + ci];
-    const double lam = 0.57 * exp2((qp - 12) / 3.0) * static_cast<double>(1 << (2 * (bd - 8)));
-    const int cmax = (1 << (min(bd, 10) - 5)) - 1;
-    const int c0 = tid == 0 ? 0 : 1, nc = tid == 0 ? 1 : 2;
-    double best = 0.0;  // "off": no change, ~1 bit for the type
-    int btype = 0, bcls = 0, bband[2] = {0, 0}, boff[2][4] = {};
-    best = lam * 1.0;
-    if (a.enable) {
-      for (int k = 0; k < 4; ++k) {  // edge offset classes
-        double cost = lam * (1 + 2);
-        int o[2][4];
-        for (int cc = 0; cc < nc; ++cc) {
-          const int c = c0 + cc;
-          for (int e = 0; e < 4; ++e) {
-            int v = sao_round_div(S.eo_sum[c][k][e], S.eo_cnt[c][k][e]);
-            v = e < 2 ? clampi(v, 0, cmax) : clampi(v, -cmax, 0);
-            // shrink while it does not pay
-            while (v != 0) {
-              const double d0 = static_cast<double>(sao_dd(S.eo_cnt[c][k][e], S.eo_sum[c][k][e], v)) + lam * (v < 0 ? -v : v);
-              const int v2 = v > 0 ? v - 1 : v + 1;
-              const double d1 = static_cast<double>(sao_dd(S.eo_cnt[c][k][e], S.eo_sum[c][k][e], v2)) + lam * (v2 < 0 ? -v2 : v2);
-              if (d1 <= d0) v = v2;
-              else break;
-            }
-            o[cc][e] = v;
-            cost += static_cast<double>(sao_dd(S.eo_cnt[c][k][e], S.eo_sum[c][k][e], v)) + lam * ((v < 0 ? -v : v) + 1);
-          }
+  // ---- decision.  Every candidate is priced by its own lane (lanes 0-7: edge-offset class k
+  // for luma / the chroma pair, lanes 32-127: band position p of Y / Cb / Cr), then lanes 0 / 1
+  // pick in the serial order (edge classes 0..3, then the band offsets; the first of equal
+  // costs) -- the choice a single-lane scan makes, without 300 serial candidate evaluations
+  __shared__ double s_eo_cost[2][4];
+  __shared__ int s_eo_off[2][4][2][4];
+  __shared__ double s_bo_w[3][32];
+  __shared__ int s_bo_off[3][32][4];
+  const int qp_ctb = a.qp[static_cast<size_t>(slot) * a.wctb * a.hctb + ci];
+  const double lam = 0.57 * exp2((qp_ctb - 12) / 3.0) * static_cast<double>(1 << (2 * (bd - 8)));
+  const int cmax = (1 << (min(bd, 10) - 5)) - 1;
+  if (a.enable && tid < 8) {  // edge offset class k, components of group tid >> 2
+    const int g = tid >> 2, k = tid & 3, c0 = g ? 1 : 0, nc = g ? 2 : 1;
+    double cost = lam * (1 + 2);
+    for (int cc = 0; cc < nc; ++cc) {
+      const int c = c0 + cc;
+      for (int e = 0; e < 4; ++e) {
+        int v = sao_round_div(S.eo_sum[c][k][e], S.eo_cnt[c][k][e]);
+        v = e < 2 ? clampi(v, 0, cmax) : clampi(v, -cmax, 0);
+        // shrink while it does not pay
+        while (v != 0) {
+          const double d0 = static_cast<double>(sao_dd(S.eo_cnt[c][k][e], S.eo_sum[c][k][e], v)) + lam * (v < 0 ? -v : v);
+          const int v2 = v > 0 ? v - 1 : v + 1;
+          const double d1 = static_cast<double>(sao_dd(S.eo_cnt[c][k][e], S.eo_sum[c][k][e], v2)) + lam * (v2 < 0 ? -v2 : v2);
+          if (d1 <= d0) v = v2;
+          else break;
         }
+        s_eo_off[g][k][cc][e] = v;
+        cost += static_cast<double>(sao_dd(S.eo_cnt[c][k][e], S.eo_sum[c][k][e], v)) + lam * ((v < 0 ? -v : v) + 1);
+      }
+    }
+    s_eo_cost[g][k] = cost;
+  } else if (a.enable && tid >= 32 && tid < 128) {  // band offset window at position p of component c
+    const int c = (tid - 32) >> 5, p = tid & 31;
+    double w = lam * 5;
+    for (int k = 0; k < 4; ++k) {
+      const int b = (p + k) & 31;
+      int v = clampi(sao_round_div(S.bo_sum[c][b], S.bo_cnt[c][b]), -cmax, cmax);
+      const double dv = static_cast<double>(sao_dd(S.bo_cnt[c][b], S.bo_sum[c][b], v)) + lam * ((v < 0 ? -v : v) + (v != 0));
+      if (dv > lam) v = 0;
+      s_bo_off[c][p][k] = v;
+      w += v ? static_cast<double>(sao_dd(S.bo_cnt[c][b], S.bo_sum[c][b], v)) + lam * ((v < 0 ? -v : v) + 1) : lam;
+    }
+    s_bo_w[c][p] = w;
+  }
+  __syncthreads();
+  if (tid < 2) {  // lane 0: luma, lane 1: the chroma pair
+    const int c0 = tid == 0 ? 0 : 1, nc = tid == 0 ? 1 : 2;
+    double best = lam * 1.0;  // "off": no change, ~1 bit for the type
+    int btype = 0, bcls = 0, bband[2] = {0, 0}, boff[2][4] = {};
+    if (a.enable) {
+      for (int k = 0; k < 4; ++k) {
+        const double cost = s_eo_cost[tid][k];
         if (cost < best) {
           best = cost;
           btype = 2;
           bcls = k;
           for (int cc = 0; cc < nc; ++cc)
-            for (int e = 0; e < 4; ++e) boff[cc][e] = o[cc][e];
+            for (int e = 0; e < 4; ++e) boff[cc][e] = s_eo_off[tid][k][cc][e];
         }
       }
-      {  // band offset: best 4-band window per component
-        double cost = lam * 1;
-        int o[2][4], pos[2];
+      double cost = lam * 1;
+      int pos[2] = {0, 0};
+      for (int cc = 0; cc < nc; ++cc) {
+        const int c = c0 + cc;
+        double bestw = 1e300;
+        for (int p = 0; p < 32; ++p)
+          if (s_bo_w[c][p] < bestw) {
+            bestw = s_bo_w[c][p];
+            pos[cc] = p;
+          }
+        cost += bestw;
+      }
+      if (cost < best) {
+        best = cost;
+        btype = 1;
         for (int cc = 0; cc < nc; ++cc) {
-          const int c = c0 + cc;
-          double bestw = 1e300;
-          int bpos = 0, bo[4] = {};
-          for (int p = 0; p < 32; ++p) {
-            double w = lam * 5;
-            int oo[4];
-            for (int k = 0; k < 4; ++k) {
-              const int b = (p + k) & 31;
-              int v = clampi(sao_round_div(S.bo_sum[c][b], S.bo_cnt[c][b]), -cmax, cmax);
-              const double dv = static_cast<double>(sao_dd(S.bo_cnt[c][b], S.bo_sum[c][b], v)) + lam * ((v < 0 ? -v : v) + (v != 0));
-              if (dv > lam) v = 0;
-              oo[k] = v;
-              w += v ? static_cast<double>(sao_dd(S.bo_cnt[c][b], S.bo_sum[c][b], v)) + lam * ((v < 0 ? -v : v) + 1) : lam;
-            }
-            if (w < bestw) {
-              bestw = w;
-              bpos = p;
-              for (int k = 0; k < 4; ++k) bo[k] = oo[k];
-            }
-          }
-          cost += bestw;
-          pos[cc] = bpos;
-          for (int k = 0; k < 4; ++k) o[cc][k] = bo[k];
-        }
-        if (cost < best) {
-          best = cost;
-          btype = 1;
-          for (int cc = 0; cc < nc; ++cc) {
-            bband[cc] = pos[cc];
-            for (int k = 0; k < 4; ++k) boff[cc][k] = o[cc][k];
-          }
+          bband[cc] = pos[cc];
+          for (int k = 0; k < 4; ++k) boff[cc][k] = s_bo_off[c0 + cc][pos[cc]][k];
         }
       }
     }
