@@ -41,6 +41,14 @@ CONFIGS = {
     "trellis1": dict(trellis=1),  # round 3's trellis scope (4x4 luma only)
     "bf0": dict(bframes=0),       # P pictures only
     "la4": dict(la_range=4),      # lowres search +-4 around the quarter-resolution seed (default +-6)
+    # knob sweep (VERDICT r3 task 2: re-tune the gates and ranges on all classes together)
+    "bgate1200": dict(b_gate=1200),
+    "bgate4800": dict(b_gate=4800),
+    "bme8": dict(b_me_range=8),
+    "refgate750": dict(ref_gate=750),
+    "refgate3000": dict(ref_gate=3000),
+    "tl07": dict(trellis_lambda=0.7),
+    "tl14": dict(trellis_lambda=1.4),
     # fast spatial direct with the fixed GOP pattern: exact motion re-predicted (tol -1, round 4's
     # first version) / estimate kept as explicit motion beyond 0 / 4 quarter samples; b-pyramid
     "sp_repredict": dict(direct="spatial", spatial_fix_tol=-1),
