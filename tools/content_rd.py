@@ -66,6 +66,9 @@ HEVC_CONFIGS = {
     "signhide": dict(sdh=True),
     "bf0": dict(bframes=0),
     "bf3": dict(bframes=3, b_qp_offset=2),
+    "bqp2": dict(b_qp_offset=2),
+    "bqp3": dict(b_qp_offset=3),
+    "bqp6": dict(b_qp_offset=6),
 }
 
 
