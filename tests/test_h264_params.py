@@ -29,3 +29,49 @@ def test_cabac_groups_isolate_the_idr_step():
             assert groups[0] == (0, 1)
             assert all(n <= G for _, n in groups)
     assert GpuH264Encoder._cabac_groups(60, 20) == [(0, 1), (1, 20), (21, 20), (41, 10), (51, 9)]
+
+
+def test_pending_encode_redoes_a_pool_overflow(monkeypatch):
+    """PendingEncode.result(): a symbol-pool overflow in a deferred batch drains the other
+    batch in flight, grows the pool and re-encodes synchronously; other errors propagate."""
+    import pytest
+    import torch
+    from govideocompressor_amd.models.h264_gpu import CabacPoolExhausted, PendingEncode
+
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
+    calls = []
+
+    class FakeEnc:
+        dev = "cpu"
+        cab_G, cab_grow = 20, 1
+        stats: dict = {}
+
+        def __init__(self):
+            self._inflight = []
+
+        def _alloc_cabac(self, g, grow):
+            calls.append(("grow", grow))
+            self.cab_grow = grow
+
+        def encode(self, *planes, **kw):
+            calls.append(("encode", planes, kw))
+            return ["redone"]
+
+    enc = FakeEnc()
+
+    def overflow():
+        raise CabacPoolExhausted("pool")
+
+    other = PendingEncode(enc, lambda: ["other"], ("y2",), {})
+    bad = PendingEncode(enc, overflow, ("y", "u", "v"), {"analysis": None})
+    enc._inflight += [bad, other]
+    assert bad.result() == ["redone"]
+    assert other.done() and other.result() == ["other"]     # drained before the pool grew
+    assert calls[0] == ("grow", 4) and calls[1][0] == "encode" and calls[1][1] == ("y", "u", "v")
+    assert enc._inflight == []
+
+    def boom():
+        raise RuntimeError("coder error")
+    p = PendingEncode(enc, boom, ("y",), {})
+    with pytest.raises(RuntimeError, match="coder error"):
+        p.result()
