@@ -11,6 +11,8 @@
 #include "h264_t8.h"
 #include "../common/h264_i4_taps.h"
 
+#include <cstdlib>
+
 namespace mivc {
 namespace gpu {
 
@@ -660,8 +662,12 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
   PROF(7);
 }
 
-__global__ __launch_bounds__(64 * kIntraWaves) void encode_intra_wavefront(IntraArgs a) {
-  __shared__ IntraShared SS[kIntraWaves];
+// NW waves per workgroup, one MB row each (rows y, y + NW, ...): 8 by default (256 VGPRs, two
+// waves per SIMD); 16 (MIVC_INTRA_WAVES=16) halves each slot's serial row passes at a 128-VGPR
+// budget (spills) -- the A/B knob for the IDR pictures' throughput-bound intra pass
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void encode_intra_wavefront(IntraArgs a) {
+  __shared__ IntraShared SS[NW];
   __shared__ int prog[kMaxRows];
   const Geom& g = a.g;
   // one workgroup per slice: intra prediction never crosses a slice's top edge, so the slices
@@ -685,7 +691,7 @@ __global__ __launch_bounds__(64 * kIntraWaves) void encode_intra_wavefront(Intra
 #pragma unroll
     for (int x = 0; x < 4; ++x) tapw[x] = h264::kI4Taps[m][r * 4 + x];
   }
-  for (int y = y_begin + w; y < y_end; y += kIntraWaves) {
+  for (int y = y_begin + w; y < y_end; y += NW) {
     if (!a.intra_flag) {  // I frame: every MB
       for (int x = 0; x < g.wmb; ++x) {
         if (top_in_slice(y, a.slice_rows)) row_wait(prog, y - 1, min(x + 2, g.wmb), a.err);
@@ -749,8 +755,15 @@ extern "C" void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t*
   a.use_i4x4 = use_i4x4;
   a.use_i8x8 = use_i8x8;
   const int per = slice_rows > 0 ? (hmb + slice_rows - 1) / slice_rows : 1;
-  hipLaunchKernelGGL(encode_intra_wavefront, dim3(B * per), dim3(64 * kIntraWaves), 0, static_cast<hipStream_t>(stream),
-                     a);
+  static const int nw = [] {
+    const char* e = std::getenv("MIVC_INTRA_WAVES");
+    return (e && std::atoi(e) == 16) ? 16 : kIntraWaves;
+  }();
+  if (nw == 16)
+    hipLaunchKernelGGL(encode_intra_wavefront<16>, dim3(B * per), dim3(64 * 16), 0, static_cast<hipStream_t>(stream), a);
+  else
+    hipLaunchKernelGGL(encode_intra_wavefront<kIntraWaves>, dim3(B * per), dim3(64 * kIntraWaves), 0,
+                       static_cast<hipStream_t>(stream), a);
 }
 
 #ifdef MIVC_INTRA_PROFILE

@@ -188,7 +188,8 @@ class H264Params:
     wp_min_mean: float = 2.0
     wp_min_scale: float = 0.08
     ref_range: int = int(os.environ.get("MIVC_REF_RANGE", 4))
-    ref_gate: int = int(os.environ.get("MIVC_REF_GATE", 1500))
+    # content suite (profiles/r4_knob_sweep.md): 3000 is -0.67 % BD-rate and +1.5 % fps vs 1500
+    ref_gate: int = int(os.environ.get("MIVC_REF_GATE", 3000))
     # slices per picture (x264 --slices): whole MB rows each.  The GPU arithmetic coder codes
     # one slice per lane, so S slices give S times the independent serial chains per picture
     # (and the intra wavefront restarts at every slice); each slice costs a header and the
