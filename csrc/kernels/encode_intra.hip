@@ -18,7 +18,7 @@ namespace gpu {
 
 using h264::MbHeader;
 
-constexpr int kIntraWaves = 8;
+constexpr int kIntraWaves = 16;  // default workgroup width of encode_intra_wavefront (see below)
 
 #ifdef MIVC_INTRA_PROFILE
 __device__ unsigned long long g_intra_prof[16][16];  // [mb][phase] for slot 0, wave 0
@@ -662,9 +662,9 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
   PROF(7);
 }
 
-// NW waves per workgroup, one MB row each (rows y, y + NW, ...): 8 by default (256 VGPRs, two
-// waves per SIMD); 16 (MIVC_INTRA_WAVES=16) halves each slot's serial row passes at a 128-VGPR
-// budget (spills) -- the A/B knob for the IDR pictures' throughput-bound intra pass
+// NW waves per workgroup, one MB row each (rows y, y + NW, ...): 16 by default -- twice the rows
+// of a slot in flight at a 128-VGPR budget (some spills), same-box A/B +1.0 % headline fps and
+// +2.1 % at 4K over 8 waves at 256 VGPRs; MIVC_INTRA_WAVES=8 selects the 8-wave instance
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void encode_intra_wavefront(IntraArgs a) {
   __shared__ IntraShared SS[NW];
@@ -757,13 +757,12 @@ extern "C" void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t*
   const int per = slice_rows > 0 ? (hmb + slice_rows - 1) / slice_rows : 1;
   static const int nw = [] {
     const char* e = std::getenv("MIVC_INTRA_WAVES");
-    return (e && std::atoi(e) == 16) ? 16 : kIntraWaves;
+    return (e && std::atoi(e) == 8) ? 8 : 16;
   }();
   if (nw == 16)
     hipLaunchKernelGGL(encode_intra_wavefront<16>, dim3(B * per), dim3(64 * 16), 0, static_cast<hipStream_t>(stream), a);
   else
-    hipLaunchKernelGGL(encode_intra_wavefront<kIntraWaves>, dim3(B * per), dim3(64 * kIntraWaves), 0,
-                       static_cast<hipStream_t>(stream), a);
+    hipLaunchKernelGGL(encode_intra_wavefront<8>, dim3(B * per), dim3(64 * 8), 0, static_cast<hipStream_t>(stream), a);
 }
 
 #ifdef MIVC_INTRA_PROFILE

@@ -338,7 +338,9 @@ def test_gpu_h264_multiref_roundtrip(host, bframes):
     references) and B pictures' temporal direct follows the co-located block's reference
     (per-reference DistScaleFactor and implicit weights) -- bit-exact against the CPU decoder,
     and farther pictures are actually chosen."""
-    enc, res, _ = _run(352, 288, slots=2, frames=13, crf=None, qp=26, bframes=bframes, refs=3)
+    # ref_gate 0: every MB searches the farther pictures (the default gate 3000 leaves this
+    # small clip on the nearest one)
+    enc, res, _ = _run(352, 288, slots=2, frames=13, crf=None, qp=26, bframes=bframes, refs=3, ref_gate=0)
     _check_roundtrip(host, enc, res, 352, 288)
     assert enc.stats.get("p_far_ref_ratio", 0.0) > 0.0, enc.stats
 
