@@ -43,6 +43,7 @@ CONFIGS = {
     "la4": dict(la_range=4),      # lowres search +-4 around the quarter-resolution seed (default +-6)
     # knob sweep (VERDICT r3 task 2: re-tune the gates and ranges on all classes together)
     "bgate1200": dict(b_gate=1200),
+    "bgate1800": dict(b_gate=1800),
     "bgate4800": dict(b_gate=4800),
     "bme8": dict(b_me_range=8),
     "refgate750": dict(ref_gate=750),
