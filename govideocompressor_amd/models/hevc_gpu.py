@@ -97,7 +97,9 @@ class HevcParams:
     # 2-4 B pictures lose there (+2.6 .. +7.9 % at +2 QP: the far anchors cost more than the B
     # pictures save on this content)
     bframes: int = 1
-    b_qp_offset: int = 4
+    # content suite (profiles/r4_hevc_bqp_rd.json, BD-rate vs +4): +2 +1.85 %, +3 +0.79 %,
+    # +6 -1.36 % -- the B picture between two anchors is worth less than x265's pbratio prices it
+    b_qp_offset: int = 6
     # x265 --b-pyramid (default on): the middle B of a run of 2+ is a reference picture (at half
     # the B QP offset) and the others predict from their nearest references (models/gop.py)
     pyramid: bool = True
