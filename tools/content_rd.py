@@ -44,6 +44,8 @@ CONFIGS = {
     # knob sweep (VERDICT r3 task 2: re-tune the gates and ranges on all classes together)
     "bgate1200": dict(b_gate=1200),
     "bgate1800": dict(b_gate=1800),
+    "bq3": dict(b_qp_offset=3.0),   # B pictures above their references (x264 pbratio 1.3 = +2.27)
+    "bq4": dict(b_qp_offset=4.0),
     "bgate4800": dict(b_gate=4800),
     "bme8": dict(b_me_range=8),
     "refgate750": dict(ref_gate=750),
@@ -70,6 +72,8 @@ HEVC_CONFIGS = {
     "bqp2": dict(b_qp_offset=2),
     "bqp3": dict(b_qp_offset=3),
     "bqp6": dict(b_qp_offset=6),
+    "bqp4": dict(b_qp_offset=4),
+    "bqp8": dict(b_qp_offset=8),
 }
 
 
