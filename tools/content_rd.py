@@ -44,6 +44,13 @@ CONFIGS = {
     # knob sweep (VERDICT r3 task 2: re-tune the gates and ranges on all classes together)
     "bgate1200": dict(b_gate=1200),
     "bgate1800": dict(b_gate=1800),
+    "skr1": dict(skip_refine=1),
+    "skr3": dict(skip_refine=3),
+    "pms1000": dict(part_min_satd=1000),
+    "pms4000": dict(part_min_satd=4000),
+    "mer6": dict(me_range=6),
+    "mer12": dict(me_range=12),
+    "besad0": dict(b_early_sad=0),
     "bq3": dict(b_qp_offset=3.0),   # B pictures above their references (x264 pbratio 1.3 = +2.27)
     "bq4": dict(b_qp_offset=4.0),
     "bgate4800": dict(b_gate=4800),
