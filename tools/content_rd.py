@@ -46,6 +46,8 @@ CONFIGS = {
     "bgate1800": dict(b_gate=1800),
     "skr1": dict(skip_refine=1),
     "skr3": dict(skip_refine=3),
+    "skr4": dict(skip_refine=4),
+    "skr5": dict(skip_refine=5),
     "pms1000": dict(part_min_satd=1000),
     "pms4000": dict(part_min_satd=4000),
     "mer6": dict(me_range=6),
