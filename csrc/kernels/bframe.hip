@@ -1050,13 +1050,21 @@ struct PRefineArgs {
 
 __device__ __forceinline__ int median3(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
 
+// Four MBs per wave, one 16-lane row each: a lane prices one 4x4 block of its MB straight
+// from registers (no LDS) and the row sums them with DPP.  The kernel is a short chain of
+// dependent loads (neighbour vectors -> prediction -> cost) per MB, so it is bound by how
+// many MBs are in flight; one MB per wave left it at ~1.5 ms per launch at the headline.
+constexpr int kRefineMbsPerWave = 4;
+
 __global__ __launch_bounds__(64) void p_mv_refine(PRefineArgs a) {
   const Geom& g = a.g;
   const int nmb = g.nmb();
-  int mb, slot;
-  xcd_unit_slot(mb, slot);
+  int unit, slot;
+  xcd_unit_slot(unit, slot);
   if (!route_active(a.rt, slot, SK_P)) return;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 15;
+  const int mb = unit * kRefineMbsPerWave + (threadIdx.x >> 4);
+  if (mb >= nmb) return;   // whole 16-lane rows only: the DPP sums below stay row-local
   const size_t o = static_cast<size_t>(slot) * nmb + mb;
   const int mx = mb % g.wmb, my = mb / g.wmb;
   const int16_t* mv = a.mv_in + static_cast<size_t>(slot) * nmb * 2;
@@ -1082,37 +1090,33 @@ __global__ __launch_bounds__(64) void p_mv_refine(PRefineArgs a) {
     return;
   }
   const int W = g.W, H = g.H;
-  const int r = lane >> 2, c0 = (lane & 3) * 4;
-  const int X = mx * 16 + c0, Y = my * 16 + r;
+  const int bx4 = (lane & 3) * 4, by4 = (lane >> 2) * 4;
+  const int X = mx * 16 + bx4, Y = my * 16 + by4;
   const size_t yo = static_cast<size_t>(slot) * g.ysize();
   const size_t s0 = route_index(a.rt, a.nbuf, slot, RO_L0);
   const uint8_t* G0 = a.ref + s0 * g.ysize();
   const uint8_t* H0 = a.hp + s0 * hp_plane_bytes(W, H);
-  const uint32_t src = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y) * W + X);
-  const uint32_t ps = mc4(G0, H0, W, H, X, Y, sx, sy);
-  __shared__ int s_res[256];
+  uint32_t ps[4];
+  int rr[16];
 #pragma unroll
-  for (int k = 0; k < 4; ++k)
-    s_res[r * 16 + c0 + k] = static_cast<int>((src >> (8 * k)) & 255u) - static_cast<int>((ps >> (8 * k)) & 255u);
-  wave_sync();
-  int satd = 0;
-  if (lane < 16) {
-    const int bx = (lane & 3) * 4, by = (lane >> 2) * 4;
-    int rr[16];
+  for (int y = 0; y < 4; ++y) {
+    const uint32_t src = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y + y) * W + X);
+    ps[y] = mc4(G0, H0, W, H, X, Y + y, sx, sy);
 #pragma unroll
-    for (int y = 0; y < 4; ++y)
-#pragma unroll
-      for (int x = 0; x < 4; ++x) rr[y * 4 + x] = s_res[(by + y) * 16 + bx + x];
-    satd = h264::satd4x4(rr);
+    for (int k = 0; k < 4; ++k)
+      rr[y * 4 + k] = static_cast<int>((src >> (8 * k)) & 255u) - static_cast<int>((ps[y] >> (8 * k)) & 255u);
   }
-  satd = __builtin_amdgcn_readlane(sum16(satd), 0);
+  const int satd = sum16(h264::satd4x4(rr));
   const int qp = clampi(a.qp[slot] + (a.aq ? a.aq[o] : 0), 0, 51);
   const int lambda = h264::kLambda[qp];
   const int pmx = a.pm ? a.pm[o * 2] : 0, pmy = a.pm ? a.pm[o * 2 + 1] : 0;
   const int satd_me = a.cost[o] - lambda * (mvbits_se(cx - pmx) + mvbits_se(cy - pmy));
   const int c_me = satd_me + lambda * (mvbits_se(cx - sx) + mvbits_se(cy - sy) + 1);
   const bool take = satd <= c_me;
-  if (take) *reinterpret_cast<uint32_t*>(a.pred + o * 256 + r * 16 + c0) = ps;
+  if (take) {
+#pragma unroll
+    for (int y = 0; y < 4; ++y) *reinterpret_cast<uint32_t*>(a.pred + o * 256 + (by4 + y) * 16 + bx4) = ps[y];
+  }
   if (lane == 0) {
     a.mv_out[o * 2] = static_cast<int16_t>(take ? sx : cx);
     a.mv_out[o * 2 + 1] = static_cast<int16_t>(take ? sy : cy);
@@ -1749,7 +1753,8 @@ extern "C" void mivc_launch_p_refine(int B, int wmb, int hmb, const uint8_t* src
   a.pred = pred;
   a.qp = qp;
   a.aq = aq;
-  hipLaunchKernelGGL(p_mv_refine, dim3(wmb * hmb, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
+  hipLaunchKernelGGL(p_mv_refine, dim3((wmb * hmb + kRefineMbsPerWave - 1) / kRefineMbsPerWave, B), dim3(64), 0,
+                     static_cast<hipStream_t>(stream), a);
 }
 
 extern "C" void mivc_launch_p_part8(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref,

@@ -100,8 +100,9 @@ class H264Params:
     # co-located vectors of temporal direct, so a small window suffices)
     b_me_range: int = int(os.environ.get("MIVC_B_ME_RANGE", 4))
     # Jacobi passes of the P_Skip-aware vector choice after ME (csrc/kernels/bframe.hip
-    # p_mv_refine): 0 disables
-    skip_refine: int = int(os.environ.get("MIVC_SKIP_REFINE", 2))
+    # p_mv_refine): 0 disables.  Each pass settles the field one MB further: 2 -> 4 passes is
+    # -2.55 % BD-rate on the content suite for -1.3 % headline fps (profiles/r4_knob_sweep.md)
+    skip_refine: int = int(os.environ.get("MIVC_SKIP_REFINE", 4))
     # x264 --8x8dct (default on): High profile, the 8x8 transform chosen per inter MB where
     # its sa8d beats the 4x4 satd; CABAC only (the CAVLC path stays Constrained Baseline)
     t8x8: bool = True

@@ -15,13 +15,14 @@ superfast   CABAC + 3 B, half-pel, radius 4, no MB-tree, no P/B partitions, 1 re
             trellis (--subme 1 --me dia --no-mbtree --partitions i8x8,i4x4 --ref 1)
 veryfast    half-pel, radius 8, 1 reference, no trellis (--subme 2 --ref 1 --trellis 0)
 faster      quarter-pel, radius 8, one skip-refine pass, 2 references (--subme 4 --ref 2)
-fast        quarter-pel, radius 8, 2 references (--subme 6 --ref 2)
-medium      defaults (x264 defaults, the reference's "264" preset: --ref 3, weightp, trellis 1)
-slow        radius 12, B radius 6, Intra4x4 in P pictures, 4 references, 4 skip-refine passes
+fast        quarter-pel, radius 8, 2 skip-refine passes, 2 references (--subme 6 --ref 2)
+medium      defaults (x264 defaults, the reference's "264" preset: --ref 3, weightp, trellis 1;
+            4 skip-refine passes)
+slow        radius 12, B radius 6, Intra4x4 in P pictures, 4 references, 5 skip-refine passes
             (--me umh --subme 8 --ref 5)
-slower      radius 16, B radius 8, lookahead radius 8, 4 references, spatial direct, 5
+slower      radius 16, B radius 8, lookahead radius 8, 4 references, spatial direct, 6
             skip-refine passes (--subme 9 --me umh --ref 8 --direct spatial)
-veryslow    slower + 6 skip-refine passes (--subme 10 --me umh --merange 24 --ref 16)
+veryslow    slower + 8 skip-refine passes (--subme 10 --me umh --merange 24 --ref 16)
 placebo     = veryslow
 ==========  ========================================================================
 
@@ -45,17 +46,17 @@ H264 = {
                       partitions=False, bpartitions=False),
     "veryfast": dict(subpel=1, me_range=8, skip_refine=1, refs=1, trellis=0),
     "faster": dict(subpel=2, me_range=8, skip_refine=1, refs=2),
-    "fast": dict(subpel=2, me_range=8, refs=2),
+    "fast": dict(subpel=2, me_range=8, skip_refine=2, refs=2),
     "medium": dict(),
     # slow and up: B gate 1200 (-1.95 % BD-rate, -11 % fps on the content suite,
     # profiles/r4_knob_sweep.md); slower and up: spatial direct decided exactly in the MB
     # wavefront (-2.2 % vs temporal, profiles/r3_direct_rd.md -- the parallel fast path loses,
-    # profiles/r4_trellis_spatial_rd.md).  Skip-refine passes beyond medium's 2: each one
-    # -0.7..-1.5 % BD-rate and -1.4 % fps at the headline (profiles/r4_knob_sweep.md)
-    "slow": dict(me_range=12, b_me_range=6, i4x4_in_p=True, refs=4, b_gate=1200, skip_refine=4),
-    "slower": dict(me_range=16, b_me_range=8, i4x4_in_p=True, la_range=8, skip_refine=5, refs=4, direct="spatial",
+    # profiles/r4_trellis_spatial_rd.md).  Skip-refine passes beyond medium's 4: each one
+    # ~-0.7 % BD-rate and ~-0.65 % fps at the headline (profiles/r4_knob_sweep.md)
+    "slow": dict(me_range=12, b_me_range=6, i4x4_in_p=True, refs=4, b_gate=1200, skip_refine=5),
+    "slower": dict(me_range=16, b_me_range=8, i4x4_in_p=True, la_range=8, skip_refine=6, refs=4, direct="spatial",
                    spatial_wavefront=True, b_gate=1200),
-    "veryslow": dict(me_range=16, b_me_range=8, i4x4_in_p=True, la_range=8, skip_refine=6, refs=4, direct="spatial",
+    "veryslow": dict(me_range=16, b_me_range=8, i4x4_in_p=True, la_range=8, skip_refine=8, refs=4, direct="spatial",
                      spatial_wavefront=True, b_gate=1200),
 }
 H264["placebo"] = H264["veryslow"]

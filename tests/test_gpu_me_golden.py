@@ -225,3 +225,87 @@ def test_me_halfpel_planes_match_numpy(W, H):
         for k, plane in enumerate((pl.b, pl.h, pl.j)):
             d = np.argwhere(got[b, k] != plane[sl])
             assert len(d) == 0, (b, "bhj"[k], len(d), d[:8], [(int(got[b, k][tuple(e)]), int(plane[sl][tuple(e)])) for e in d[:8]])
+
+
+def _refine_ref(src, planes, mv_in, cost, pm, pred, qps, lam_tab, wmb, hmb):
+    """One Jacobi pass of the P_Skip-aware vector choice (bframe.hip p_mv_refine) in numpy:
+    each MB is offered the P_Skip predictor of its neighbours' current vectors (8.4.1.1) and
+    takes it when SATD <= its own SATD + lambda * (mvd bits vs that predictor + 1)."""
+    B = src.shape[0]
+    mv_out, cost, pred = mv_in.copy(), cost.copy(), pred.copy()
+    for b in range(B):
+        lam = lam_tab[int(qps[b])]
+        for mb in range(wmb * hmb):
+            mx, my = mb % wmb, mb // wmb
+            cx, cy = (int(v) for v in mv_in[b, mb])
+            sx = sy = 0
+            if mx > 0 and my > 0:
+                A, Bn = mv_in[b, mb - 1], mv_in[b, mb - wmb]
+                if A.any() and Bn.any():
+                    C = mv_in[b, mb - wmb + 1] if mx < wmb - 1 else mv_in[b, mb - wmb - 1]
+                    sx, sy = (int(np.median([A[i], Bn[i], C[i]])) for i in range(2))
+            if (sx, sy) == (cx, cy):
+                continue
+            X0, Y0 = mx * 16, my * 16
+            P = planes[b].block(X0, Y0, sx, sy)
+            R = src[b, Y0:Y0 + 16, X0:X0 + 16].astype(np.int64) - P
+            satd = sum(_satd(R[y:y + 4, x:x + 4]) for y in range(0, 16, 4) for x in range(0, 16, 4))
+            pmx, pmy = (int(v) for v in pm[b, mb])
+            satd_me = int(cost[b, mb]) - lam * (_se_bits(cx - pmx) + _se_bits(cy - pmy))
+            if satd <= satd_me + lam * (_se_bits(cx - sx) + _se_bits(cy - sy) + 1):
+                mv_out[b, mb] = (sx, sy)
+                cost[b, mb] = satd + lam * (_se_bits(sx - pmx) + _se_bits(sy - pmy))
+                pred[b, mb] = P.reshape(256)
+    return mv_out, cost, pred
+
+
+def test_p_refine_matches_numpy(host):
+    """p_mv_refine (four MBs per wave, one 4x4 block per lane) against the numpy statement of
+    the pass, over three passes on a near-uniform field; 117 MBs leave a partial last wave."""
+    import torch
+    from govideocompressor_amd.ops import native
+    hip = native.hip()
+    rng = np.random.default_rng(5)
+    B, wmb, hmb = 2, 13, 9
+    W, H, nmb = wmb * 16, hmb * 16, wmb * hmb
+    dev = torch.device("cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    k = np.ones(5) / 5
+    refs, srcs = [], []
+    for _ in range(B):
+        base = rng.integers(0, 256, size=(H + 40, W + 40)).astype(np.float64)
+        base = np.apply_along_axis(lambda r: np.convolve(r, k, "same"), 1, base)
+        base = np.apply_along_axis(lambda r: np.convolve(r, k, "same"), 0, base)
+        refs.append(np.clip(base[10:10 + H, 12:12 + W], 0, 255))
+        srcs.append(np.clip(base[12:12 + H, 13:13 + W] + rng.normal(0, 3, size=(H, W)), 0, 255))
+    refs = np.ascontiguousarray(np.stack(refs).astype(np.uint8))
+    srcs = np.ascontiguousarray(np.stack(srcs).astype(np.uint8))
+    ref, src = torch.from_numpy(refs).to(dev), torch.from_numpy(srcs).to(dev)
+    hp = torch.zeros((B, 3, H + 8, W + 8), dtype=torch.uint8, device=dev)
+    hip.me_halfpel(B, W, H, ref.data_ptr(), hp.data_ptr(), s)
+    planes = [_Planes(refs[b]) for b in range(B)]
+    # a near-uniform field (4, 8) with scattered quarter-sample deviations
+    mv = np.tile(np.array([4, 8], dtype=np.int16), (B, nmb, 1))
+    dmask = rng.random((B, nmb)) < 0.6
+    mv[dmask] += rng.integers(-3, 4, size=(int(dmask.sum()), 2)).astype(np.int16)
+    cost = rng.integers(400, 4000, size=(B, nmb)).astype(np.int32)
+    pred = rng.integers(0, 256, size=(B, nmb, 256)).astype(np.uint8)
+    pm = np.zeros((B, nmb, 2), dtype=np.int16)
+    qps = np.array([26, 32], dtype=np.int32)
+    t_mv = [torch.from_numpy(mv.copy()).to(dev), torch.zeros((B, nmb, 2), dtype=torch.int16, device=dev)]
+    t_cost, t_pred = torch.from_numpy(cost.copy()).to(dev), torch.from_numpy(pred.copy()).to(dev)
+    t_pm, t_qp = torch.from_numpy(pm).to(dev), torch.from_numpy(qps).to(dev)
+    lam = host.table("lambda")[0]
+    took = 0
+    for it in range(3):
+        a_, b_ = t_mv[it % 2], t_mv[(it + 1) % 2]
+        hip.p_refine(B, wmb, hmb, src.data_ptr(), ref.data_ptr(), hp.data_ptr(), a_.data_ptr(), b_.data_ptr(),
+                     t_cost.data_ptr(), t_pm.data_ptr(), t_pred.data_ptr(), t_qp.data_ptr(), 0, s)
+        torch.cuda.synchronize()
+        r_mv, r_cost, r_pred = _refine_ref(srcs, planes, mv, cost, pm, pred, qps, lam, wmb, hmb)
+        took += int((r_mv != mv).any(axis=2).sum())
+        assert np.array_equal(b_.cpu().numpy(), r_mv), it
+        assert np.array_equal(t_cost.cpu().numpy(), r_cost), it
+        assert np.array_equal(t_pred.cpu().numpy(), r_pred.astype(np.uint8)), it
+        mv, cost, pred = r_mv, r_cost, r_pred
+    assert took > 0
