@@ -1285,6 +1285,18 @@ __device__ __forceinline__ int satd16_words(int* s_res, uint32_t src, uint32_t p
   return satd;
 }
 
+// 16-lane-row form (four blocks per wave): this lane's 4x4 block = rows by4..by4+3 of src / pw,
+// summed over the row with DPP (every lane of a row holds the same block's total)
+__device__ __forceinline__ int satd16_rows(const uint32_t* src, const uint32_t* pw) {
+  int rr[16];
+#pragma unroll
+  for (int y = 0; y < 4; ++y)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      rr[y * 4 + k] = static_cast<int>((src[y] >> (8 * k)) & 255u) - static_cast<int>((pw[y] >> (8 * k)) & 255u);
+  return sum16(h264::satd4x4(rr));
+}
+
 __global__ __launch_bounds__(64) void hevc_b_choose(HevcBArgs a) {
   const Geom& g = a.g;
   const int nmb = g.nmb();
@@ -1346,12 +1358,19 @@ __global__ __launch_bounds__(256) void hevc_b_init_p(HevcBArgs a) {
 // quadrant 3; pruning A1-B1, B1-B0, A1-A0, A1/B1-B2; the temporal candidate, combined
 // bi-predictive and zero candidates; MaxNumMergeCand entries); the cheapest by SATD + lambda *
 // (merge_flag + merge_idx bins) replaces the block's motion when it beats its cost.
+//
+// Four blocks per wave (one 16-lane row each, a 4x4 sub-block per lane, SATD in registers), as
+// p_mv_refine: the pass is a chain of dependent loads per block, bound by blocks in flight.
+constexpr int kMergeMbsPerWave = 4;
+
 __global__ __launch_bounds__(64) void hevc_b_merge(HevcBArgs a) {
   const Geom& g = a.g;
   const int nmb = g.nmb();
-  int mb, slot;
-  xcd_unit_slot(mb, slot);
-  const int lane = threadIdx.x;
+  int unit, slot;
+  xcd_unit_slot(unit, slot);
+  const int lane = threadIdx.x & 15;
+  const int mb = unit * kMergeMbsPerWave + (threadIdx.x >> 4);
+  if (mb >= nmb) return;   // whole rows only: the DPP sums stay row-local
   const size_t o = static_cast<size_t>(slot) * nmb + mb;
   const size_t sb = static_cast<size_t>(slot) * nmb;
   const int mx = mb % g.wmb, my = mb / g.wmb;
@@ -1428,23 +1447,27 @@ __global__ __launch_bounds__(64) void hevc_b_merge(HevcBArgs a) {
   const int lam = h264::kLambda[qp];
   const int c_cur = a.cost[o];
   const int satd_cur = c_cur - lam * a.bits[o];
-  const int r = lane >> 2, c0 = (lane & 3) * 4;
-  const int X = mx * 16 + c0, Y = my * 16 + r;
+  const int X = mx * 16 + (lane & 3) * 4, Y = my * 16 + (lane >> 2) * 4;
   const size_t yo = static_cast<size_t>(slot) * g.ysize();
   const size_t ho = static_cast<size_t>(slot) * 3 * (g.W + 2 * kHpMargin) * (g.H + 2 * kHpMargin);
   const uint8_t *G0 = a.ref0 + yo, *H0 = a.hp0 + ho;
   const uint8_t *G1 = a.bslice ? a.ref1 + yo : G0, *H1 = a.bslice ? a.hp1 + ho : H0;
-  const uint32_t src = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y) * g.W + X);
-  __shared__ int s_res[256];
+  uint32_t src[4];
+#pragma unroll
+  for (int y = 0; y < 4; ++y)
+    src[y] = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y + y) * g.W + X);
   int best = c_cur, bbits = a.bits[o], bj = -1;
   for (int j = 0; j < nk; ++j) {
     bool dup = false;  // the same motion earlier in the list: never cheaper
     for (int i = 0; i < j; ++i) dup = dup || same(kd[i], kv[i], kd[j], kv[j]);
     if (dup) continue;
-    const int sat = same(kd[j], kv[j], cd, cw)
-                        ? satd_cur
-                        : satd16_words(s_res, src, mc4_b(a, G0, H0, G1, H1, X, Y, kd[j], kv[j][0], kv[j][1], kv[j][2], kv[j][3]),
-                                       r, c0);
+    int sat = satd_cur;
+    if (!same(kd[j], kv[j], cd, cw)) {
+      uint32_t pw[4];
+#pragma unroll
+      for (int y = 0; y < 4; ++y) pw[y] = mc4_b(a, G0, H0, G1, H1, X, Y + y, kd[j], kv[j][0], kv[j][1], kv[j][2], kv[j][3]);
+      sat = satd16_rows(src, pw);
+    }
     const int nb = 1 + (maxc > 1 ? min(j + 1, maxc - 1) : 0);  // merge_flag + truncated-unary merge_idx
     const int cst = sat + lam * nb;
     if (cst < best) {
@@ -1835,7 +1858,8 @@ extern "C" void mivc_launch_hevc_b(int mode, int B, int wmb, int hmb, const uint
   a.max_merge = max_merge;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (mode == 0) hipLaunchKernelGGL(hevc_b_choose, dim3(wmb * hmb, B), dim3(64), 0, st, a);
-  else if (mode == 1) hipLaunchKernelGGL(hevc_b_merge, dim3(wmb * hmb, B), dim3(64), 0, st, a);
+  else if (mode == 1)
+    hipLaunchKernelGGL(hevc_b_merge, dim3((wmb * hmb + kMergeMbsPerWave - 1) / kMergeMbsPerWave, B), dim3(64), 0, st, a);
   else hipLaunchKernelGGL(hevc_b_init_p, dim3((wmb * hmb + 255) / 256, B), dim3(256), 0, st, a);
 }
 
