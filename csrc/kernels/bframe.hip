@@ -261,20 +261,28 @@ __device__ __forceinline__ void spatial_pmv(NbMv16 A, NbMv16 B, NbMv16 C, int& r
   }
 }
 
-// One wave per MB: lane = (row lane >> 2, columns 4 * (lane & 3) .. +3).
+// Four MBs per wave, one 16-lane row each: a lane owns one 4x4 block (raster order) of its MB
+// and prices it for every candidate from registers; quadrant sums go through a pair DPP and a
+// small LDS table.  The pass is a chain of dependent loads per MB (vectors -> predictions ->
+// costs), so MBs in flight set its speed (one MB per wave, the round-3 layout, was half as
+// fast for p_mv_refine).
+constexpr int kDecideMbsPerWave = 4;
+
 __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   const Geom& g = a.g;
   const int nmb = g.nmb();
-  int mb, slot;
-  xcd_unit_slot(mb, slot);
+  int unit, slot;
+  xcd_unit_slot(unit, slot);
   if (!route_active(a.rt, slot, SK_B)) return;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 15, wrow = threadIdx.x >> 4;
+  const int mb = unit * kDecideMbsPerWave + wrow;
+  if (mb >= nmb) return;   // whole rows only: the DPP below stays row-local
   const size_t o = static_cast<size_t>(slot) * nmb + mb;
   const int mx = mb % g.wmb, my = mb / g.wmb;
   const int W = g.W, H = g.H;
-  const int r = lane >> 2, c0 = (lane & 3) * 4;
-  const int X = mx * 16 + c0, Y = my * 16 + r;
-  const int q = (r >> 3) * 2 + (c0 >> 3);  // 8x8 quadrant of this lane's samples
+  const int by4 = (lane >> 2) * 4, bx4 = (lane & 3) * 4;
+  const int X = mx * 16 + bx4, Y = my * 16 + by4;
+  const int q = (by4 >> 3) * 2 + (bx4 >> 3);  // 8x8 quadrant of this lane's block
   const size_t yo = static_cast<size_t>(slot) * g.ysize();
   const size_t hps = hp_plane_bytes(W, H);
   const size_t s0 = route_index(a.rt, a.nbuf, slot, RO_L0), s1 = route_index(a.rt, a.nbuf, slot, RO_L1);
@@ -287,7 +295,9 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   const bool sfast = a.spatial == 2;
   const int m0x = donly ? 0 : a.mv0[o * 2], m0y = donly ? 0 : a.mv0[o * 2 + 1];
   const int m1x = donly ? 0 : a.mv1[o * 2], m1y = donly ? 0 : a.mv1[o * 2 + 1];
-  const uint32_t src = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y) * W + X);
+  uint32_t src[4];
+#pragma unroll
+  for (int y = 0; y < 4; ++y) src[y] = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y + y) * W + X);
   MbHeader* hrec = a.hdr + o;
   // The direct candidate per quadrant and list: refIdx (-1: list unused) and vector.
   //   temporal: the co-located block's scaled motion (b_direct_mv), list 1 from RefPicList1[0];
@@ -365,7 +375,7 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   const uint8_t *GD = dr ? a.ref0k[dr] + (a.rt ? sd : slot) * g.ysize() : G0,
                 *HD = dr ? a.hp0k[dr] + (a.rt ? sd : slot) * hps : H0;
   const bool searched = !donly && a.cost0[o] < kNoCostB && a.cost1[o] < kNoCostB;
-  uint32_t* pout = reinterpret_cast<uint32_t*>(a.pred_out + o * 256 + r * 16 + c0);
+  uint8_t* pout = a.pred_out + o * 256 + by4 * 16 + bx4;   // row y at pout + 16 * y
   if (!donly && !searched && a.have_direct) {
     // gated MB: B_Direct_16x16 with the pre-pass's prediction and cost
     if (lane == 0) {
@@ -381,55 +391,56 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
     }
     return;
   }
-  uint32_t pd;
-  if (!donly && a.have_direct) {
-    pd = *pout;
-  } else {
-    const uint32_t pl0 = du0 ? mc4(GD, HD, W, H, X, Y, dvx[0][q], dvy[0][q]) : 0u;
-    const uint32_t pl1 = du1 ? mc4(G1, H1, W, H, X, Y, dvx[1][q], dvy[1][q]) : 0u;
-    pd = (du0 && du1) ? wavg4b(pl0, pl1, w1of(dr)) : (du0 ? pl0 : pl1);
-  }
-  if (donly) *pout = pd;
-  const uint32_t pb = donly ? pd : wavg4b(mc4(G0, H0, W, H, X, Y, m0x, m0y), mc4(G1, H1, W, H, X, Y, m1x, m1y), w1of(0));
-  // residuals of the four candidates: 0 direct, 1 bi (the two ME vectors), 2 L0, 3 L1 (the ME
-  // predictions; not needed by the direct-only pre-pass or for MBs the gate left unsearched)
-  const uint32_t p0w = searched ? *reinterpret_cast<const uint32_t*>(a.pred0 + o * 256 + r * 16 + c0) : pd;
-  const uint32_t p1w = searched ? *reinterpret_cast<const uint32_t*>(a.pred1 + o * 256 + r * 16 + c0) : pd;
-  __shared__ int s_res[4][256];
-  __shared__ int s_satd[4][16];
-  const int ncand = donly ? 1 : 4;  // the pre-pass prices direct only
+  uint32_t pd[4], pb[4], p0w[4], p1w[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int sv = static_cast<int>((src >> (8 * k)) & 255u);
-    s_res[0][r * 16 + c0 + k] = sv - static_cast<int>((pd >> (8 * k)) & 255u);
-    if (!donly) {
-      s_res[1][r * 16 + c0 + k] = sv - static_cast<int>((pb >> (8 * k)) & 255u);
-      s_res[2][r * 16 + c0 + k] = sv - static_cast<int>((p0w >> (8 * k)) & 255u);
-      s_res[3][r * 16 + c0 + k] = sv - static_cast<int>((p1w >> (8 * k)) & 255u);
+  for (int y = 0; y < 4; ++y) {
+    if (!donly && a.have_direct) {
+      pd[y] = *reinterpret_cast<const uint32_t*>(pout + 16 * y);
+    } else {
+      const uint32_t pl0 = du0 ? mc4(GD, HD, W, H, X, Y + y, dvx[0][q], dvy[0][q]) : 0u;
+      const uint32_t pl1 = du1 ? mc4(G1, H1, W, H, X, Y + y, dvx[1][q], dvy[1][q]) : 0u;
+      pd[y] = (du0 && du1) ? wavg4b(pl0, pl1, w1of(dr)) : (du0 ? pl0 : pl1);
     }
+    if (donly) *reinterpret_cast<uint32_t*>(pout + 16 * y) = pd[y];
+    pb[y] = donly ? pd[y]
+                  : wavg4b(mc4(G0, H0, W, H, X, Y + y, m0x, m0y), mc4(G1, H1, W, H, X, Y + y, m1x, m1y), w1of(0));
+    // candidates: 0 direct, 1 bi (the two ME vectors), 2 L0, 3 L1 (the ME predictions; not
+    // needed by the direct-only pre-pass or for MBs the gate left unsearched)
+    p0w[y] = searched ? *reinterpret_cast<const uint32_t*>(a.pred0 + o * 256 + (by4 + y) * 16 + bx4) : pd[y];
+    p1w[y] = searched ? *reinterpret_cast<const uint32_t*>(a.pred1 + o * 256 + (by4 + y) * 16 + bx4) : pd[y];
   }
-  wave_sync();
-  if (lane < 16 * ncand) {  // one 4x4 SATD per lane: candidate lane >> 4, block lane & 15 (raster)
-    const int cand = lane >> 4, blk = lane & 15, bx = (blk & 3) * 4, by = (blk >> 2) * 4;
+  auto blk_satd = [&](const uint32_t* pw) {
     int rr[16];
 #pragma unroll
     for (int y = 0; y < 4; ++y)
 #pragma unroll
-      for (int x = 0; x < 4; ++x) rr[y * 4 + x] = s_res[cand][(by + y) * 16 + bx + x];
-    s_satd[cand][blk] = h264::satd4x4(rr);
+      for (int x = 0; x < 4; ++x)
+        rr[y * 4 + x] = static_cast<int>((src[y] >> (8 * x)) & 255u) - static_cast<int>((pw[y] >> (8 * x)) & 255u);
+    return h264::satd4x4(rr);
+  };
+  // per 8x8 quadrant and candidate: horizontal block pairs by DPP, then the two pair rows of
+  // each quadrant from LDS (pair sums at lanes 8 * qy + 4 * {0, 1} + 2 * qx)
+  __shared__ int s_pair[kDecideMbsPerWave][4][16];
+  const int ncand = donly ? 1 : 4;  // the pre-pass prices direct only
+  {
+    const int s0 = blk_satd(pd);
+    s_pair[wrow][0][lane] = s0 + dpp<kDppQuadXor1>(s0);
+    if (!donly) {
+      const int s1 = blk_satd(pb), s2 = blk_satd(p0w), s3 = blk_satd(p1w);
+      s_pair[wrow][1][lane] = s1 + dpp<kDppQuadXor1>(s1);
+      s_pair[wrow][2][lane] = s2 + dpp<kDppQuadXor1>(s2);
+      s_pair[wrow][3][lane] = s3 + dpp<kDppQuadXor1>(s3);
+    }
   }
   wave_sync();
-  // per 8x8 quadrant and candidate (lanes 0..15: candidate lane >> 2, quadrant lane & 3)
-  int qs = 0;
-  if (lane < 4 * ncand) {
-    const int cand = lane >> 2, qq = lane & 3, b0 = (qq >> 1) * 8 + (qq & 1) * 2;
-    qs = s_satd[cand][b0] + s_satd[cand][b0 + 1] + s_satd[cand][b0 + 4] + s_satd[cand][b0 + 5];
-  }
   int qsat[4][4];  // [candidate][quadrant] (the pre-pass: candidate 0 only)
 #pragma unroll
   for (int c = 0; c < 4; ++c)
 #pragma unroll
-    for (int qq = 0; qq < 4; ++qq) qsat[c][qq] = __builtin_amdgcn_readlane(qs, c * 4 + qq);
+    for (int qq = 0; qq < 4; ++qq) {
+      const int l0 = (qq >> 1) * 8 + (qq & 1) * 2;
+      qsat[c][qq] = c < ncand ? s_pair[wrow][c][l0] + s_pair[wrow][c][l0 + 4] : 0;
+    }
   const int satd_direct = qsat[0][0] + qsat[0][1] + qsat[0][2] + qsat[0][3];
   const int satd_bi = qsat[1][0] + qsat[1][1] + qsat[1][2] + qsat[1][3];
   const int qp = clampi(a.qp[slot] + (a.aq ? a.aq[o] : 0), 0, 51);
@@ -511,8 +522,9 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
     }
   }
   const int lm = qm[q];  // this lane's quadrant
-  uint32_t pw = lm == 0 ? pd : (lm == 1 ? pb : (lm == 2 ? p0w : p1w));
-  *reinterpret_cast<uint32_t*>(a.pred_out + o * 256 + r * 16 + c0) = pw;
+#pragma unroll
+  for (int y = 0; y < 4; ++y)
+    *reinterpret_cast<uint32_t*>(pout + 16 * y) = lm == 0 ? pd[y] : (lm == 1 ? pb[y] : (lm == 2 ? p0w[y] : p1w[y]));
   if (lane == 0) {
     MbHeader* h = hrec;
     h->kind = static_cast<uint8_t>(kind);
@@ -1755,7 +1767,8 @@ extern "C" void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src
   a.hdr = static_cast<MbHeader*>(hdr);
   a.pred_out = pred_out;
   a.cost_out = cost_out;
-  hipLaunchKernelGGL(b_decide, dim3(wmb * hmb, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
+  hipLaunchKernelGGL(b_decide, dim3((wmb * hmb + kDecideMbsPerWave - 1) / kDecideMbsPerWave, B), dim3(64), 0,
+                     static_cast<hipStream_t>(stream), a);
 }
 
 extern "C" void mivc_launch_p_refine(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref,
