@@ -1137,6 +1137,18 @@ __global__ __launch_bounds__(64) void p_mv_refine(PRefineArgs a) {
 }
 
 
+// 16-lane-row form (four blocks per wave): this lane's 4x4 block = rows by4..by4+3 of src / pw,
+// summed over the row with DPP (every lane of a row holds the same block's total)
+__device__ __forceinline__ int satd16_rows(const uint32_t* src, const uint32_t* pw) {
+  int rr[16];
+#pragma unroll
+  for (int y = 0; y < 4; ++y)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      rr[y * 4 + k] = static_cast<int>((src[y] >> (8 * k)) & 255u) - static_cast<int>((pw[y] >> (8 * k)) & 255u);
+  return sum16(h264::satd4x4(rr));
+}
+
 // ---- HEVC merge-aware vector choice (the H.265 analogue of p_mv_refine): after the 16x16
 // search each block is offered the current vectors of its spatial merge neighbours (A1 left,
 // B1 above, B0 above-right, A0 below-left, B2 above-left; 8.5.3.2.3) and the zero vector;
@@ -1147,9 +1159,11 @@ __global__ __launch_bounds__(64) void p_mv_refine(PRefineArgs a) {
 __global__ __launch_bounds__(64) void hevc_merge_refine(PRefineArgs a) {
   const Geom& g = a.g;
   const int nmb = g.nmb();
-  int mb, slot;
-  xcd_unit_slot(mb, slot);
-  const int lane = threadIdx.x;
+  int unit, slot;
+  xcd_unit_slot(unit, slot);
+  const int lane = threadIdx.x & 15;   // four blocks per wave, as p_mv_refine
+  const int mb = unit * kRefineMbsPerWave + (threadIdx.x >> 4);
+  if (mb >= nmb) return;
   const size_t o = static_cast<size_t>(slot) * nmb + mb;
   const int mx = mb % g.wmb, my = mb / g.wmb;
   const int16_t* mv = a.mv_in + static_cast<size_t>(slot) * nmb * 2;
@@ -1183,36 +1197,23 @@ __global__ __launch_bounds__(64) void hevc_merge_refine(PRefineArgs a) {
   const int pmx = a.pm ? a.pm[o * 2] : 0, pmy = a.pm ? a.pm[o * 2 + 1] : 0;
   const int c_me = a.cost[o];  // SATD + lambda * mvd bits against the search predictor
   const int W = g.W, H = g.H;
-  const int r = lane >> 2, c0 = (lane & 3) * 4;
-  const int X = mx * 16 + c0, Y = my * 16 + r;
+  const int X = mx * 16 + (lane & 3) * 4, Y = my * 16 + (lane >> 2) * 4;
   const size_t yo = static_cast<size_t>(slot) * g.ysize();
   const uint8_t* G0 = a.ref + yo;
   const uint8_t* H0 = a.hp + static_cast<size_t>(slot) * 3 * (W + 2 * kHpMargin) * (H + 2 * kHpMargin);
-  const uint32_t src = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y) * W + X);
-  __shared__ int s_res[256];
+  uint32_t src[4];
+#pragma unroll
+  for (int y = 0; y < 4; ++y) src[y] = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y + y) * W + X);
   int best = c_me, bx_ = cx, by_ = cy;
   for (int j = 0; j < nk; ++j) {
     if (kx[j] == cx && ky[j] == cy) {  // the searched vector is itself a merge candidate
       best = min(best, c_me - lambda * (mvbits_se(cx - pmx) + mvbits_se(cy - pmy)) + lambda * (1 + j));
       continue;
     }
-    const uint32_t ps = mc4(G0, H0, W, H, X, Y, kx[j], ky[j]);
+    uint32_t ps[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      s_res[r * 16 + c0 + k] = static_cast<int>((src >> (8 * k)) & 255u) - static_cast<int>((ps >> (8 * k)) & 255u);
-    wave_sync();
-    int satd = 0;
-    if (lane < 16) {
-      const int bx = (lane & 3) * 4, by = (lane >> 2) * 4;
-      int rr[16];
-#pragma unroll
-      for (int y = 0; y < 4; ++y)
-#pragma unroll
-        for (int x = 0; x < 4; ++x) rr[y * 4 + x] = s_res[(by + y) * 16 + bx + x];
-      satd = h264::satd4x4(rr);
-    }
-    satd = __builtin_amdgcn_readlane(sum16(satd), 0);
-    wave_sync();
+    for (int y = 0; y < 4; ++y) ps[y] = mc4(G0, H0, W, H, X, Y + y, kx[j], ky[j]);
+    const int satd = satd16_rows(src, ps);
     const int cst = satd + lambda * (1 + j);  // merge_flag + truncated-unary merge_idx
     if (cst < best) {
       best = cst;
@@ -1275,57 +1276,29 @@ __device__ __forceinline__ uint32_t mc4_b(const HevcBArgs& a, const uint8_t* G0,
   return avg4b(mc4(G0, H0, W, H, X, Y, x0, y0), mc4(G1, H1, W, H, X, Y, x1, y1));
 }
 
-// SATD of a 16x16 block's residual against a prediction word per lane (whole wave calls)
-__device__ __forceinline__ int satd16_words(int* s_res, uint32_t src, uint32_t pw, int r, int c0) {
-  const int lane = threadIdx.x;
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    s_res[r * 16 + c0 + k] = static_cast<int>((src >> (8 * k)) & 255u) - static_cast<int>((pw >> (8 * k)) & 255u);
-  wave_sync();
-  int satd = 0;
-  if (lane < 16) {
-    const int bx = (lane & 3) * 4, by = (lane >> 2) * 4;
-    int rr[16];
-#pragma unroll
-    for (int y = 0; y < 4; ++y)
-#pragma unroll
-      for (int x = 0; x < 4; ++x) rr[y * 4 + x] = s_res[(by + y) * 16 + bx + x];
-    satd = h264::satd4x4(rr);
-  }
-  satd = __builtin_amdgcn_readlane(sum16(satd), 0);
-  wave_sync();
-  return satd;
-}
-
-// 16-lane-row form (four blocks per wave): this lane's 4x4 block = rows by4..by4+3 of src / pw,
-// summed over the row with DPP (every lane of a row holds the same block's total)
-__device__ __forceinline__ int satd16_rows(const uint32_t* src, const uint32_t* pw) {
-  int rr[16];
-#pragma unroll
-  for (int y = 0; y < 4; ++y)
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      rr[y * 4 + k] = static_cast<int>((src[y] >> (8 * k)) & 255u) - static_cast<int>((pw[y] >> (8 * k)) & 255u);
-  return sum16(h264::satd4x4(rr));
-}
-
+// four blocks per wave (16-lane rows, a 4x4 sub-block per lane), as hevc_b_merge
 __global__ __launch_bounds__(64) void hevc_b_choose(HevcBArgs a) {
   const Geom& g = a.g;
   const int nmb = g.nmb();
-  int mb, slot;
-  xcd_unit_slot(mb, slot);
-  const int lane = threadIdx.x;
+  int unit, slot;
+  xcd_unit_slot(unit, slot);
+  const int lane = threadIdx.x & 15;
+  const int mb = unit * 4 + (threadIdx.x >> 4);
+  if (mb >= nmb) return;
   const size_t o = static_cast<size_t>(slot) * nmb + mb;
   const int mx = mb % g.wmb, my = mb / g.wmb;
-  const int r = lane >> 2, c0 = (lane & 3) * 4;
-  const int X = mx * 16 + c0, Y = my * 16 + r;
+  const int X = mx * 16 + (lane & 3) * 4, Y = my * 16 + (lane >> 2) * 4;
   const size_t yo = static_cast<size_t>(slot) * g.ysize();
   const size_t ho = static_cast<size_t>(slot) * 3 * (g.W + 2 * kHpMargin) * (g.H + 2 * kHpMargin);
   const uint8_t *G0 = a.ref0 + yo, *G1 = a.ref1 + yo, *H0 = a.hp0 + ho, *H1 = a.hp1 + ho;
   const int x0 = a.mv0[o * 2], y0 = a.mv0[o * 2 + 1], x1 = a.mv1[o * 2], y1 = a.mv1[o * 2 + 1];
-  const uint32_t src = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y) * g.W + X);
-  __shared__ int s_res[256];
-  const int satd_bi = satd16_words(s_res, src, mc4_b(a, G0, H0, G1, H1, X, Y, 3, x0, y0, x1, y1), r, c0);
+  uint32_t src[4], pw[4];
+#pragma unroll
+  for (int y = 0; y < 4; ++y) {
+    src[y] = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y + y) * g.W + X);
+    pw[y] = mc4_b(a, G0, H0, G1, H1, X, Y + y, 3, x0, y0, x1, y1);
+  }
+  const int satd_bi = satd16_rows(src, pw);
   const int qp = clampi(a.qp[slot] + (a.aq ? a.aq[o] : 0), 0, 51);
   const int lam = h264::kLambda[qp];
   const int b0 = mvbits_se(x0 - a.pm0[o * 2]) + mvbits_se(y0 - a.pm0[o * 2 + 1]);
@@ -1833,7 +1806,8 @@ extern "C" void mivc_launch_hevc_merge_refine(int B, int wmb, int hmb, const uin
   a.pred = nullptr;
   a.qp = qp;
   a.aq = aq;
-  hipLaunchKernelGGL(hevc_merge_refine, dim3(wmb * hmb, B), dim3(64), 0, static_cast<hipStream_t>(stream), a);
+  hipLaunchKernelGGL(hevc_merge_refine, dim3((wmb * hmb + kRefineMbsPerWave - 1) / kRefineMbsPerWave, B), dim3(64), 0,
+                     static_cast<hipStream_t>(stream), a);
 }
 
 extern "C" void mivc_launch_hevc_b(int mode, int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref0,
@@ -1870,7 +1844,7 @@ extern "C" void mivc_launch_hevc_b(int mode, int B, int wmb, int hmb, const uint
   a.bslice = bslice;
   a.max_merge = max_merge;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (mode == 0) hipLaunchKernelGGL(hevc_b_choose, dim3(wmb * hmb, B), dim3(64), 0, st, a);
+  if (mode == 0) hipLaunchKernelGGL(hevc_b_choose, dim3((wmb * hmb + 3) / 4, B), dim3(64), 0, st, a);
   else if (mode == 1)
     hipLaunchKernelGGL(hevc_b_merge, dim3((wmb * hmb + kMergeMbsPerWave - 1) / kMergeMbsPerWave, B), dim3(64), 0, st, a);
   else hipLaunchKernelGGL(hevc_b_init_p, dim3((wmb * hmb + 255) / 256, B), dim3(256), 0, st, a);
