@@ -25,7 +25,7 @@ int first_mb_of(const uint8_t* p, size_t n) {
   if (n < 2) return -1;
   BitReader br(p + 1, std::min<size_t>(n - 1, 8));
   try {
-    return static_cast<int>(br.get_ue());
+    return br.get_ue_max((1u << 20) - 1, "first_mb_in_slice");
   } catch (...) {
     return -1;
   }

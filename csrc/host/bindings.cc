@@ -114,7 +114,7 @@ py::dict picture_to_dict(const DecodedPicture& p) {
   std::memcpy(q.mutable_data(), p.mb_qp.data(), p.mb_qp.size());
   d["mb_qp"] = q;
   py::array_t<int16_t> mv(static_cast<py::ssize_t>(p.mv.size()));
-  std::memcpy(mv.mutable_data(), p.mv.data(), p.mv.size() * 2);
+  if (!p.mv.empty()) std::memcpy(mv.mutable_data(), p.mv.data(), p.mv.size() * 2);
   d["mv"] = mv;
   return d;
 }
@@ -126,7 +126,7 @@ py::array_t<T> vec_array(const std::vector<std::vector<T>*>& parts, std::vector<
   py::array_t<T> a(shape);
   T* d = a.mutable_data();
   for (const std::vector<T>* v : parts) {
-    std::memcpy(d, v->data(), v->size() * sizeof(T));
+    if (!v->empty()) std::memcpy(d, v->data(), v->size() * sizeof(T));
     d += v->size();
   }
   return a;
@@ -355,7 +355,7 @@ hevc::HevcConfig hevc_cfg_from(const py::dict& d) {
 template <class T>
 py::array_t<T> to_array(const std::vector<T>& v, std::vector<py::ssize_t> shape) {
   py::array_t<T> a(shape);
-  std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(T));
+  if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(T));
   return a;
 }
 

@@ -98,12 +98,33 @@ class BitReader {
       if (++lz > 32) throw std::runtime_error("invalid exp-golomb code");
     }
     if (lz == 0) return 0;
-    uint64_t v = (1ull << lz) - 1 + get(lz);
+    const uint64_t v = (1ull << lz) - 1 + get(lz);
+    if (v > 0xffffffffull) throw std::runtime_error("exp-golomb code above 2^32 - 1");  // no silent wrap
     return static_cast<uint32_t>(v);
   }
   int32_t get_se() {
-    uint32_t k = get_ue();
-    return (k & 1) ? static_cast<int32_t>((k + 1) / 2) : -static_cast<int32_t>(k / 2);
+    const uint32_t k = get_ue();
+    if (!(k & 1)) return -static_cast<int32_t>(k / 2);
+    const uint64_t m = (static_cast<uint64_t>(k) + 1) / 2;  // (k + 1) / 2 without the 32-bit wrap
+    if (m > 0x7fffffffu) throw std::runtime_error("se(v) out of range");
+    return static_cast<int32_t>(m);
+  }
+  // Range-checked Exp-Golomb reads.  Every syntax element that is narrowed to `int`, used as
+  // an index or a count, or has a constant added goes through these: the raw code is compared
+  // with the element's legal range BEFORE any narrowing or arithmetic, so a crafted 32-leading-
+  // zero code (up to 2^32-1) can neither wrap into a small / negative int nor overflow later.
+  int get_ue_max(uint32_t maxv, const char* what) {
+    if (maxv > 0x7fffffffu) maxv = 0x7fffffffu;
+    const uint32_t v = get_ue();
+    if (v > maxv) throw std::runtime_error(std::string(what) + " out of range");
+    return static_cast<int>(v);
+  }
+  int get_se_range(int lo, int hi, const char* what) {
+    const uint32_t k = get_ue();
+    // se(v) magnitude is ceil(k / 2); compare in 64 bits before forming the signed value
+    const int64_t v = (k & 1) ? static_cast<int64_t>(k / 2) + 1 : -static_cast<int64_t>(k / 2);
+    if (v < lo || v > hi) throw std::runtime_error(std::string(what) + " out of range");
+    return static_cast<int>(v);
   }
   uint32_t get_te(uint32_t range) { return range == 1 ? !get_bit() : get_ue(); }
   bool byte_aligned() const { return (pos_ & 7) == 0; }

@@ -811,7 +811,7 @@ struct Decoder::Impl {
     while (more) {
       if (addr >= nmb) throw std::runtime_error("slice runs past the picture");
       if (sh.slice_type != SLICE_I) {
-        int run = br.get_ue();
+        const int run = br.get_ue_max(static_cast<uint32_t>(nmb), "mb_skip_run");
         for (int i = 0; i < run; ++i) {
           if (addr >= nmb) throw std::runtime_error("skip run past the picture");
           decode_skip(addr, qp);
@@ -1884,7 +1884,7 @@ struct Decoder::Impl {
         else s.btype = bt;
       }
     } else {
-      int mb_type = br.get_ue();
+      const int mb_type = br.get_ue_max(48, "mb_type");
       if (st == SLICE_P) {
         if (mb_type < 5) ptype = mb_type;
         else itype = mb_type - 5;
@@ -1959,8 +1959,8 @@ struct Decoder::Impl {
     if (sub8) {
       // sub_mb_pred (7.3.5.2)
       for (int q = 0; q < 4; ++q) {
-        if (st == SLICE_P) s.sub[q] = cabac ? cabac_sub_p() : static_cast<int>(br.get_ue());
-        else s.sub[q] = cabac ? cabac_sub_b() : static_cast<int>(br.get_ue());
+        if (st == SLICE_P) s.sub[q] = cabac ? cabac_sub_p() : br.get_ue_max(3, "sub_mb_type");
+        else s.sub[q] = cabac ? cabac_sub_b() : br.get_ue_max(12, "sub_mb_type");
         if (s.sub[q] < 0 || s.sub[q] > (st == SLICE_P ? 3 : 12)) throw std::runtime_error("bad sub_mb_type");
         const SubInfo& si = st == SLICE_P ? kPSub[s.sub[q]] : kBSub[s.sub[q]];
         if (st == SLICE_B && s.sub[q] == 0) {
@@ -1999,8 +1999,8 @@ struct Decoder::Impl {
               d0 = cabac_mvd(addr, l, 0, x4, y4);
               d1 = cabac_mvd(addr, l, 1, x4, y4);
             } else {
-              d0 = br.get_se();
-              d1 = br.get_se();
+              d0 = br.get_se_range(-32768, 32767, "mvd_l0");
+              d1 = br.get_se_range(-32768, 32767, "mvd_l1");
             }
             s.mvd[l][q][k][0] = d0;
             s.mvd[l][q][k][1] = d1;
@@ -2041,7 +2041,7 @@ struct Decoder::Impl {
           }
         }
       }
-      s.chroma_mode = cabac ? cabac_chroma_mode(addr) : static_cast<int>(br.get_ue());
+      s.chroma_mode = cabac ? cabac_chroma_mode(addr) : br.get_ue_max(3, "intra_chroma_pred_mode");
       if (s.chroma_mode > 3) throw std::runtime_error("bad intra_chroma_pred_mode");
       cur->chroma_mode[addr] = static_cast<int8_t>(s.chroma_mode);
     } else if (kind != MBK_BDIRECT) {
@@ -2077,8 +2077,8 @@ struct Decoder::Impl {
             d0 = cabac_mvd(addr, l, 0, x4, y4);
             d1 = cabac_mvd(addr, l, 1, x4, y4);
           } else {
-            d0 = br.get_se();
-            d1 = br.get_se();
+            d0 = br.get_se_range(-32768, 32767, "mvd");
+            d1 = br.get_se_range(-32768, 32767, "mvd");
           }
           s.mvd[l][p][0][0] = d0;
           s.mvd[l][p][0][1] = d1;
@@ -2098,8 +2098,7 @@ struct Decoder::Impl {
       if (cabac) {
         s.cbp = cabac_cbp(addr);
       } else {
-        int code = br.get_ue();
-        if (code > 47) throw std::runtime_error("bad coded_block_pattern");
+        const int code = br.get_ue_max(47, "coded_block_pattern");
         s.cbp = intra ? kGolombToIntraCbp[code] : kGolombToInterCbp[code];
       }
       if ((s.cbp & 15) && pp->transform_8x8_mode && !intra && no_sub_lt8 &&
@@ -2111,7 +2110,7 @@ struct Decoder::Impl {
     cur->cbp[addr] = static_cast<uint8_t>(s.cbp);
     int cbp_luma = s.cbp & 15, cbp_chroma = s.cbp >> 4;
     if (cbp_luma || cbp_chroma || kind == MBK_I16x16) {
-      int d = cabac ? cabac_qp_delta() : br.get_se();
+      const int d = cabac ? cabac_qp_delta() : br.get_se_range(-26, 25, "mb_qp_delta");
       if (d < -26 || d > 25) throw std::runtime_error("mb_qp_delta out of range");
       qp = ((qp + d + 52) % 52);
       prev_qp_delta_nz = d != 0;

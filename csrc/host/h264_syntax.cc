@@ -27,8 +27,7 @@ bool read_scaling_list(BitReader& br, uint8_t* out_raster, int n) {
   bool use_default = false;
   for (int j = 0; j < n; ++j) {
     if (next != 0) {
-      const int delta = br.get_se();
-      if (delta < -128 || delta > 127) throw std::runtime_error("delta_scale out of range");
+      const int delta = br.get_se_range(-128, 127, "delta_scale");
       next = (last + delta + 256) % 256;
       use_default = j == 0 && next == 0;
     }
@@ -256,7 +255,7 @@ void write_slice_header(BitWriter& bw, const SliceHeader& h, const SPS& s, const
 
 
 static void skip_hrd(BitReader& br) {
-  int cpb_cnt = br.get_ue() + 1;
+  const int cpb_cnt = br.get_ue_max(31, "cpb_cnt_minus1") + 1;
   br.get(4);
   br.get(4);
   for (int i = 0; i < cpb_cnt; ++i) {
@@ -275,13 +274,12 @@ SPS parse_sps(BitReader& br) {
   s.profile_idc = br.get(8);
   s.constraint_flags = br.get(8);
   s.level_idc = br.get(8);
-  s.sps_id = br.get_ue();
-  if (s.sps_id > 31) throw std::runtime_error("bad sps id");
+  s.sps_id = br.get_ue_max(31, "seq_parameter_set_id");
   if (high_profile(s.profile_idc)) {
-    s.chroma_format_idc = br.get_ue();
+    s.chroma_format_idc = br.get_ue_max(3, "chroma_format_idc");
     if (s.chroma_format_idc == 3) br.get_bit();
-    s.bit_depth_luma = br.get_ue() + 8;
-    s.bit_depth_chroma = br.get_ue() + 8;
+    s.bit_depth_luma = br.get_ue_max(6, "bit_depth_luma_minus8") + 8;
+    s.bit_depth_chroma = br.get_ue_max(6, "bit_depth_chroma_minus8") + 8;
     br.get_bit();
     s.scaling_present = br.get_bit();
     if (s.scaling_present) {
@@ -290,32 +288,32 @@ SPS parse_sps(BitReader& br) {
     }
   }
   if (s.chroma_format_idc != 1 || s.bit_depth_luma != 8) throw std::runtime_error("only 8-bit 4:2:0 supported");
-  s.log2_max_frame_num = br.get_ue() + 4;
-  s.poc_type = br.get_ue();
+  s.log2_max_frame_num = br.get_ue_max(12, "log2_max_frame_num_minus4") + 4;
+  s.poc_type = br.get_ue_max(2, "pic_order_cnt_type");
   if (s.poc_type == 0) {
-    s.log2_max_poc_lsb = br.get_ue() + 4;
+    s.log2_max_poc_lsb = br.get_ue_max(12, "log2_max_pic_order_cnt_lsb_minus4") + 4;
   } else if (s.poc_type == 1) {
     s.delta_pic_order_always_zero = br.get_bit();
-    s.offset_for_non_ref_pic = br.get_se();
-    s.offset_for_top_to_bottom = br.get_se();
-    int n = br.get_ue();
-    if (n > 255) throw std::runtime_error("bad num_ref_frames_in_pic_order_cnt_cycle");
-    for (int i = 0; i < n; ++i) s.offset_for_ref_frame.push_back(br.get_se());
-  } else if (s.poc_type != 2) {
-    throw std::runtime_error("bad pic_order_cnt_type");
+    // offsets are bounded to +-2^31-1 by the spec; keep them in 2^24 so the POC sums cannot overflow
+    s.offset_for_non_ref_pic = br.get_se_range(-(1 << 24), 1 << 24, "offset_for_non_ref_pic");
+    s.offset_for_top_to_bottom = br.get_se_range(-(1 << 24), 1 << 24, "offset_for_top_to_bottom_field");
+    const int n = br.get_ue_max(255, "num_ref_frames_in_pic_order_cnt_cycle");
+    for (int i = 0; i < n; ++i) s.offset_for_ref_frame.push_back(br.get_se_range(-(1 << 24), 1 << 24, "offset_for_ref_frame"));
   }
-  s.max_num_ref_frames = br.get_ue();
+  s.max_num_ref_frames = br.get_ue_max(16, "max_num_ref_frames");
   s.gaps_allowed = br.get_bit();
-  s.width_mbs = br.get_ue() + 1;
-  s.height_mbs = br.get_ue() + 1;
+  s.width_mbs = br.get_ue_max(1023, "pic_width_in_mbs_minus1") + 1;
+  s.height_mbs = br.get_ue_max(1023, "pic_height_in_map_units_minus1") + 1;
   s.frame_mbs_only = br.get_bit();
   if (!s.frame_mbs_only) throw std::runtime_error("interlaced streams not supported");
   s.direct_8x8_inference = br.get_bit();
   if (br.get_bit()) {
-    s.crop_left = br.get_ue();
-    s.crop_right = br.get_ue();
-    s.crop_top = br.get_ue();
-    s.crop_bottom = br.get_ue();
+    s.crop_left = br.get_ue_max(8 * s.width_mbs, "frame_crop_left_offset");
+    s.crop_right = br.get_ue_max(8 * s.width_mbs, "frame_crop_right_offset");
+    s.crop_top = br.get_ue_max(8 * s.height_mbs, "frame_crop_top_offset");
+    s.crop_bottom = br.get_ue_max(8 * s.height_mbs, "frame_crop_bottom_offset");
+    if (2 * (s.crop_left + s.crop_right) >= 16 * s.width_mbs || 2 * (s.crop_top + s.crop_bottom) >= 16 * s.height_mbs)
+      throw std::runtime_error("frame cropping removes the whole picture");
   }
   s.vui_present = br.get_bit();
   if (s.vui_present) {
@@ -354,7 +352,7 @@ SPS parse_sps(BitReader& br) {
       s.vui_reorder_present = 1;
       br.get_bit();
       for (int i = 0; i < 4; ++i) br.get_ue();
-      s.max_num_reorder = br.get_ue();
+      s.max_num_reorder = br.get_ue_max(16, "max_num_reorder_frames");
       br.get_ue();
     }
   }
@@ -363,19 +361,18 @@ SPS parse_sps(BitReader& br) {
 
 PPS parse_pps(BitReader& br, const SPS* sps_table) {
   PPS p;
-  p.pps_id = br.get_ue();
-  p.sps_id = br.get_ue();
-  if (p.pps_id > 255 || p.sps_id > 31) throw std::runtime_error("bad pps");
+  p.pps_id = br.get_ue_max(255, "pic_parameter_set_id");
+  p.sps_id = br.get_ue_max(31, "seq_parameter_set_id");
   p.entropy_coding_mode = br.get_bit();
   p.bottom_field_pic_order_present = br.get_bit();
   if (br.get_ue() != 0) throw std::runtime_error("slice groups (FMO) not supported");
-  p.num_ref_idx_l0_default = br.get_ue() + 1;
-  p.num_ref_idx_l1_default = br.get_ue() + 1;
+  p.num_ref_idx_l0_default = br.get_ue_max(31, "num_ref_idx_l0_default_active_minus1") + 1;
+  p.num_ref_idx_l1_default = br.get_ue_max(31, "num_ref_idx_l1_default_active_minus1") + 1;
   p.weighted_pred = br.get_bit();
   p.weighted_bipred_idc = br.get(2);
-  p.pic_init_qp = 26 + br.get_se();
-  p.pic_init_qs = 26 + br.get_se();
-  p.chroma_qp_index_offset = br.get_se();
+  p.pic_init_qp = 26 + br.get_se_range(-26 - 6 * 6, 25, "pic_init_qp_minus26");
+  p.pic_init_qs = 26 + br.get_se_range(-26, 25, "pic_init_qs_minus26");
+  p.chroma_qp_index_offset = br.get_se_range(-12, 12, "chroma_qp_index_offset");
   p.deblocking_filter_control_present = br.get_bit();
   p.constrained_intra_pred = br.get_bit();
   p.redundant_pic_cnt_present = br.get_bit();
@@ -396,7 +393,7 @@ PPS parse_pps(BitReader& br, const SPS* sps_table) {
       std::memcpy(p.sl4, sl4, sizeof(sl4));
       std::memcpy(p.sl8, sl8, sizeof(sl8));
     }
-    p.second_chroma_qp_index_offset = br.get_se();
+    p.second_chroma_qp_index_offset = br.get_se_range(-12, 12, "second_chroma_qp_index_offset");
   }
   return p;
 }
@@ -406,22 +403,22 @@ SliceHeader parse_slice_header(BitReader& br, int nal_unit_type, int nal_ref_idc
   SliceHeader h;
   h.nal_unit_type = nal_unit_type;
   h.nal_ref_idc = nal_ref_idc;
-  h.first_mb = br.get_ue();
-  int st = br.get_ue();
+  h.first_mb = br.get_ue_max((1u << 20) - 1, "first_mb_in_slice");
+  const int st = br.get_ue_max(9, "slice_type");
   h.slice_type = st % 5;
   if (h.slice_type > 2) throw std::runtime_error("SP/SI slices not supported");
-  h.pps_id = br.get_ue();
+  h.pps_id = br.get_ue_max(255, "pic_parameter_set_id");
   const PPS& p = pps_table[h.pps_id];
   const SPS& s = sps_table[p.sps_id];
   h.frame_num = br.get(s.log2_max_frame_num);
-  if (nal_unit_type == NAL_IDR) h.idr_pic_id = br.get_ue();
+  if (nal_unit_type == NAL_IDR) h.idr_pic_id = br.get_ue_max(65535, "idr_pic_id");
   if (s.poc_type == 0) {
     h.poc_lsb = br.get(s.log2_max_poc_lsb);
-    if (p.bottom_field_pic_order_present) h.poc_bottom_delta = br.get_se();
+    if (p.bottom_field_pic_order_present) h.poc_bottom_delta = br.get_se_range(-(1 << 24), 1 << 24, "delta_pic_order_cnt_bottom");
   }
   if (s.poc_type == 1 && !s.delta_pic_order_always_zero) {
-    h.delta_poc[0] = br.get_se();
-    if (p.bottom_field_pic_order_present) h.delta_poc[1] = br.get_se();
+    h.delta_poc[0] = br.get_se_range(-(1 << 24), 1 << 24, "delta_pic_order_cnt[0]");
+    if (p.bottom_field_pic_order_present) h.delta_poc[1] = br.get_se_range(-(1 << 24), 1 << 24, "delta_pic_order_cnt[1]");
   }
   if (p.redundant_pic_cnt_present && br.get_ue() != 0) throw std::runtime_error("redundant pictures not supported");
   if (h.slice_type == SLICE_B) h.direct_spatial = br.get_bit();
@@ -430,27 +427,25 @@ SliceHeader parse_slice_header(BitReader& br, int nal_unit_type, int nal_ref_idc
   if (h.slice_type == SLICE_P || h.slice_type == SLICE_B) {
     h.num_ref_idx_override = br.get_bit();
     if (h.num_ref_idx_override) {
-      h.num_ref_idx_l0_active = br.get_ue() + 1;
-      if (h.slice_type == SLICE_B) h.num_ref_idx_l1_active = br.get_ue() + 1;
+      h.num_ref_idx_l0_active = br.get_ue_max(31, "num_ref_idx_l0_active_minus1") + 1;
+      if (h.slice_type == SLICE_B) h.num_ref_idx_l1_active = br.get_ue_max(31, "num_ref_idx_l1_active_minus1") + 1;
     }
-    if (h.num_ref_idx_l0_active > 32 || h.num_ref_idx_l1_active > 32) throw std::runtime_error("too many references");
     for (int l = 0; l < (h.slice_type == SLICE_B ? 2 : 1); ++l) {
       if (!br.get_bit()) continue;  // ref_pic_list_modification_flag_lX
       for (int guard = 0;; ++guard) {
         if (guard > 64) throw std::runtime_error("ref_pic_list_modification too long");
-        int idc = br.get_ue();
+        const int idc = br.get_ue_max(3, "modification_of_pic_nums_idc");
         if (idc == 3) break;
-        if (idc > 2) throw std::runtime_error("bad modification_of_pic_nums_idc");
-        h.mods[l].push_back(RefMod{idc, static_cast<int>(br.get_ue())});
+        // abs_diff_pic_num_minus1 < MaxPicNum (<= 2^16) or long_term_pic_num < 32
+        h.mods[l].push_back(RefMod{idc, br.get_ue_max(idc == 2 ? 31 : 65535, "ref_pic_list_modification value")});
       }
     }
   }
   if ((p.weighted_pred && h.slice_type == SLICE_P) || (p.weighted_bipred_idc == 1 && h.slice_type == SLICE_B)) {
     h.has_weights = true;
     WeightTable& w = h.wt;
-    w.luma_log2 = br.get_ue();
-    w.chroma_log2 = br.get_ue();
-    if (w.luma_log2 > 7 || w.chroma_log2 > 7) throw std::runtime_error("bad weight denominator");
+    w.luma_log2 = br.get_ue_max(7, "luma_log2_weight_denom");
+    w.chroma_log2 = br.get_ue_max(7, "chroma_log2_weight_denom");
     for (int l = 0; l < (h.slice_type == SLICE_B ? 2 : 1); ++l) {
       int n = l ? h.num_ref_idx_l1_active : h.num_ref_idx_l0_active;
       for (int i = 0; i < n; ++i) {
@@ -458,8 +453,8 @@ SliceHeader parse_slice_header(BitReader& br, int nal_unit_type, int nal_ref_idc
         w.lw[l][i] = 1 << w.luma_log2;
         w.lo[l][i] = 0;
         if (w.lflag[l][i]) {
-          w.lw[l][i] = br.get_se();
-          w.lo[l][i] = br.get_se();
+          w.lw[l][i] = br.get_se_range(-128, 127, "luma_weight");
+          w.lo[l][i] = br.get_se_range(-128, 127, "luma_offset");
         }
         w.cflag[l][i] = static_cast<uint8_t>(br.get_bit());
         for (int c = 0; c < 2; ++c) {
@@ -468,8 +463,8 @@ SliceHeader parse_slice_header(BitReader& br, int nal_unit_type, int nal_ref_idc
         }
         if (w.cflag[l][i])
           for (int c = 0; c < 2; ++c) {
-            w.cw[l][i][c] = br.get_se();
-            w.co[l][i][c] = br.get_se();
+            w.cw[l][i][c] = br.get_se_range(-128, 127, "chroma_weight");
+            w.co[l][i][c] = br.get_se_range(-128, 127, "chroma_offset");
           }
       }
     }
@@ -484,26 +479,25 @@ SliceHeader parse_slice_header(BitReader& br, int nal_unit_type, int nal_ref_idc
         for (int guard = 0;; ++guard) {
           if (guard > 128) throw std::runtime_error("dec_ref_pic_marking too long");
           Mmco m;
-          m.op = br.get_ue();
+          m.op = br.get_ue_max(6, "memory_management_control_operation");
           if (m.op == 0) break;
-          if (m.op > 6) throw std::runtime_error("bad memory_management_control_operation");
-          if (m.op == 1 || m.op == 3) m.diff_minus1 = br.get_ue();
-          if (m.op == 2) m.long_term_pic_num = br.get_ue();
-          if (m.op == 3 || m.op == 6) m.long_term_frame_idx = br.get_ue();
-          if (m.op == 4) m.max_long_term_frame_idx_plus1 = br.get_ue();
+          if (m.op == 1 || m.op == 3) m.diff_minus1 = br.get_ue_max(65535, "difference_of_pic_nums_minus1");
+          if (m.op == 2) m.long_term_pic_num = br.get_ue_max(31, "long_term_pic_num");
+          if (m.op == 3 || m.op == 6) m.long_term_frame_idx = br.get_ue_max(15, "long_term_frame_idx");
+          if (m.op == 4) m.max_long_term_frame_idx_plus1 = br.get_ue_max(16, "max_long_term_frame_idx_plus1");
           h.mmco.push_back(m);
         }
       }
     }
   }
-  if (p.entropy_coding_mode && h.slice_type != SLICE_I) h.cabac_init_idc = br.get_ue();
-  h.slice_qp_delta = br.get_se();
+  if (p.entropy_coding_mode && h.slice_type != SLICE_I) h.cabac_init_idc = br.get_ue_max(2, "cabac_init_idc");
+  h.slice_qp_delta = br.get_se_range(-87, 77, "slice_qp_delta");
   h.qp = p.pic_init_qp + h.slice_qp_delta;
   if (p.deblocking_filter_control_present) {
-    h.disable_deblocking_filter_idc = br.get_ue();
+    h.disable_deblocking_filter_idc = br.get_ue_max(2, "disable_deblocking_filter_idc");
     if (h.disable_deblocking_filter_idc != 1) {
-      h.alpha_offset_div2 = br.get_se();
-      h.beta_offset_div2 = br.get_se();
+      h.alpha_offset_div2 = br.get_se_range(-6, 6, "slice_alpha_c0_offset_div2");
+      h.beta_offset_div2 = br.get_se_range(-6, 6, "slice_beta_offset_div2");
     }
   }
   return h;

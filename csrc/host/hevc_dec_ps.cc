@@ -105,9 +105,8 @@ void parse_scaling_list_data(BitReader& br, ScalingList& sl) {
     const int coefs = std::min(64, 1 << (4 + (sid << 1)));
     for (int m = 0; m < 6; m += (sid == 3) ? 3 : 1) {
       if (!br.get(1)) {  // scaling_list_pred_mode_flag = 0: copy (or default)
-        const uint32_t delta = br.get_ue();
-        const int d = static_cast<int>(delta) * (sid == 3 ? 3 : 1);
-        if (d > m) fail("scaling_list_pred_matrix_id_delta out of range");
+        const int d = br.get_ue_max(static_cast<uint32_t>(m / (sid == 3 ? 3 : 1)), "scaling_list_pred_matrix_id_delta") *
+                      (sid == 3 ? 3 : 1);
         if (d == 0) {
           if (sid == 0) std::memset(L.c[0][m], 16, 16);
           else std::memcpy(L.c[sid][m], m < 3 ? kDefIntra8 : kDefInter8, 64);
@@ -119,14 +118,12 @@ void parse_scaling_list_data(BitReader& br, ScalingList& sl) {
       } else {
         int next = 8;
         if (sid > 1) {
-          const int dc = br.get_se() + 8;
-          if (dc < 1 || dc > 255) fail("scaling_list_dc_coef_minus8 out of range");
+          const int dc = br.get_se_range(-7, 247, "scaling_list_dc_coef_minus8") + 8;
           next = dc;
           L.dc[sid][m] = static_cast<uint8_t>(dc);
         }
         for (int i = 0; i < coefs; ++i) {
-          const int dlt = br.get_se();
-          if (dlt < -128 || dlt > 127) fail("scaling_list_delta_coef out of range");
+          const int dlt = br.get_se_range(-128, 127, "scaling_list_delta_coef");
           next = (next + dlt + 256) % 256;
           if (next == 0) fail("scaling list entry 0");
           L.c[sid][m][i] = static_cast<uint8_t>(next);
@@ -145,12 +142,10 @@ void parse_st_rps(BitReader& br, int idx, int num_in_sps, const std::vector<Shor
   if (idx != 0) inter = br.get(1);
   if (inter) {
     int delta_idx = 1;
-    if (idx == num_in_sps) delta_idx = static_cast<int>(br.get_ue()) + 1;
-    if (delta_idx > idx) fail("delta_idx_minus1 out of range");
+    if (idx == num_in_sps) delta_idx = br.get_ue_max(static_cast<uint32_t>(idx - 1), "delta_idx_minus1") + 1;
     const ShortTermRps& ref = sets[idx - delta_idx];
     const int sign = br.get(1);
-    const int abs_delta = static_cast<int>(br.get_ue()) + 1;
-    if (abs_delta > 32768) fail("abs_delta_rps_minus1 out of range");
+    const int abs_delta = br.get_ue_max(32767, "abs_delta_rps_minus1") + 1;
     const int delta_rps = (1 - 2 * sign) * abs_delta;
     const int nd = ref.num_delta();
     uint8_t used[33], use_delta[33];
@@ -224,13 +219,13 @@ void parse_st_rps(BitReader& br, int idx, int num_in_sps, const std::vector<Shor
     out.num_pos = static_cast<int>(npos);
     int poc = 0;
     for (int k = 0; k < out.num_neg; ++k) {
-      poc -= static_cast<int>(br.get_ue()) + 1;
+      poc -= br.get_ue_max(32767, "delta_poc_s0_minus1") + 1;
       out.delta[k] = poc;
       out.used[k] = static_cast<uint8_t>(br.get(1));
     }
     poc = 0;
     for (int k = 0; k < out.num_pos; ++k) {
-      poc += static_cast<int>(br.get_ue()) + 1;
+      poc += br.get_ue_max(32767, "delta_poc_s1_minus1") + 1;
       out.delta[out.num_neg + k] = poc;
       out.used[out.num_neg + k] = static_cast<uint8_t>(br.get(1));
     }
@@ -279,32 +274,31 @@ void parse_sps(BitReader& br, Sps& s) {
   const uint32_t id = br.get_ue();
   if (id > 15) fail("sps id out of range");
   s.id = static_cast<int>(id);
-  s.chroma_format = static_cast<int>(br.get_ue());
+  s.chroma_format = br.get_ue_max(3, "chroma_format_idc");
   if (s.chroma_format != 1) fail("only 4:2:0 (Main / Main 10) is supported");
-  s.W = static_cast<int>(br.get_ue());
-  s.H = static_cast<int>(br.get_ue());
+  s.W = br.get_ue_max(1u << 16, "pic_width_in_luma_samples");
+  s.H = br.get_ue_max(1u << 16, "pic_height_in_luma_samples");
   if (br.get(1))
-    for (int i = 0; i < 4; ++i) s.conf[i] = static_cast<int>(br.get_ue());
-  s.bit_depth = 8 + static_cast<int>(br.get_ue());
-  s.bit_depth_c = 8 + static_cast<int>(br.get_ue());
+    for (int i = 0; i < 4; ++i) s.conf[i] = br.get_ue_max(1u << 16, "conf_win_offset");
+  s.bit_depth = 8 + br.get_ue_max(8, "bit_depth_luma_minus8");
+  s.bit_depth_c = 8 + br.get_ue_max(8, "bit_depth_chroma_minus8");
   if (s.bit_depth > 10 || s.bit_depth_c > 10) fail("bit depth above 10 (Main 10) is not supported");
-  s.log2_max_poc_lsb = static_cast<int>(br.get_ue()) + 4;
-  if (s.log2_max_poc_lsb > 16) fail("log2_max_pic_order_cnt_lsb out of range");
+  s.log2_max_poc_lsb = br.get_ue_max(12, "log2_max_pic_order_cnt_lsb_minus4") + 4;
   const int sub = br.get(1);
   for (int i = sub ? 0 : msl; i <= msl; ++i) {
-    s.max_dec_pic_buffering = static_cast<int>(br.get_ue()) + 1;
-    s.max_num_reorder = static_cast<int>(br.get_ue());
+    s.max_dec_pic_buffering = br.get_ue_max(15, "sps_max_dec_pic_buffering_minus1") + 1;
+    s.max_num_reorder = br.get_ue_max(15, "sps_max_num_reorder_pics");
     br.get_ue();
   }
-  s.log2_min_cb = static_cast<int>(br.get_ue()) + 3;
-  s.log2_ctb = s.log2_min_cb + static_cast<int>(br.get_ue());
-  s.log2_min_tb = static_cast<int>(br.get_ue()) + 2;
-  s.log2_max_tb = s.log2_min_tb + static_cast<int>(br.get_ue());
+  s.log2_min_cb = br.get_ue_max(3, "log2_min_luma_coding_block_size_minus3") + 3;
+  s.log2_ctb = s.log2_min_cb + br.get_ue_max(3, "log2_diff_max_min_luma_coding_block_size");
+  s.log2_min_tb = br.get_ue_max(3, "log2_min_luma_transform_block_size_minus2") + 2;
+  s.log2_max_tb = s.log2_min_tb + br.get_ue_max(3, "log2_diff_max_min_luma_transform_block_size");
   if (s.log2_ctb < 4 || s.log2_ctb > 6) fail("CTB size must be 16, 32 or 64");
   if (s.log2_min_cb > s.log2_ctb || s.log2_max_tb > 5 || s.log2_min_tb >= s.log2_min_cb || s.log2_max_tb > s.log2_ctb)
     fail("coding / transform block sizes out of range");
-  s.depth_inter = static_cast<int>(br.get_ue());
-  s.depth_intra = static_cast<int>(br.get_ue());
+  s.depth_inter = br.get_ue_max(4, "max_transform_hierarchy_depth_inter");
+  s.depth_intra = br.get_ue_max(4, "max_transform_hierarchy_depth_intra");
   if (s.depth_inter > s.log2_ctb - s.log2_min_tb || s.depth_intra > s.log2_ctb - s.log2_min_tb)
     fail("max_transform_hierarchy_depth out of range");
   s.scaling_enabled = br.get(1);
@@ -316,8 +310,8 @@ void parse_sps(BitReader& br, Sps& s) {
   if (s.pcm) {
     s.pcm_bd = static_cast<int>(br.get(4)) + 1;
     s.pcm_bd_c = static_cast<int>(br.get(4)) + 1;
-    s.log2_min_pcm = static_cast<int>(br.get_ue()) + 3;
-    s.log2_max_pcm = s.log2_min_pcm + static_cast<int>(br.get_ue());
+    s.log2_min_pcm = br.get_ue_max(2, "log2_min_pcm_luma_coding_block_size_minus3") + 3;
+    s.log2_max_pcm = s.log2_min_pcm + br.get_ue_max(2, "log2_diff_max_min_pcm_luma_coding_block_size");
     s.pcm_loop_filter_disabled = br.get(1);
     if (s.pcm_bd > s.bit_depth || s.pcm_bd_c > s.bit_depth_c || s.log2_max_pcm > std::min(s.log2_ctb, 5))
       fail("PCM parameters out of range");
@@ -371,14 +365,13 @@ void parse_pps(BitReader& br, Pps& p, const Sps* sps_by_id[16]) {
     p.num_ref_l0 = static_cast<int>(n0) + 1;
     p.num_ref_l1 = static_cast<int>(n1) + 1;
   }
-  p.init_qp = 26 + br.get_se();
+  p.init_qp = 26 + br.get_se_range(-38, 25, "init_qp_minus26");
   p.constrained_intra = br.get(1);
   p.transform_skip = br.get(1);
   p.cu_qp_delta = br.get(1);
-  if (p.cu_qp_delta) p.diff_cu_qp_delta_depth = static_cast<int>(br.get_ue());
-  p.cb_qp_off = br.get_se();
-  p.cr_qp_off = br.get_se();
-  if (p.cb_qp_off < -12 || p.cb_qp_off > 12 || p.cr_qp_off < -12 || p.cr_qp_off > 12) fail("pps chroma qp offset out of range");
+  if (p.cu_qp_delta) p.diff_cu_qp_delta_depth = br.get_ue_max(3, "diff_cu_qp_delta_depth");
+  p.cb_qp_off = br.get_se_range(-12, 12, "pps_cb_qp_offset");
+  p.cr_qp_off = br.get_se_range(-12, 12, "pps_cr_qp_offset");
   p.slice_chroma_qp_offsets = br.get(1);
   p.weighted_pred = br.get(1);
   p.weighted_bipred = br.get(1);
@@ -386,13 +379,13 @@ void parse_pps(BitReader& br, Pps& p, const Sps* sps_by_id[16]) {
   p.tiles = br.get(1);
   p.wpp = br.get(1);
   if (p.tiles) {
-    p.tile_cols = static_cast<int>(br.get_ue()) + 1;
-    p.tile_rows = static_cast<int>(br.get_ue()) + 1;
-    if (p.tile_cols > 20 || p.tile_rows > 22) fail("too many tiles");
+    p.tile_cols = br.get_ue_max(19, "num_tile_columns_minus1") + 1;
+    p.tile_rows = br.get_ue_max(21, "num_tile_rows_minus1") + 1;
     p.uniform_spacing = br.get(1);
     if (!p.uniform_spacing) {
-      for (int i = 0; i < p.tile_cols - 1; ++i) p.col_width.push_back(static_cast<int>(br.get_ue()) + 1);
-      for (int i = 0; i < p.tile_rows - 1; ++i) p.row_height.push_back(static_cast<int>(br.get_ue()) + 1);
+      // a CTB count is < 2^11 for any picture the SPS accepts; build_tiles checks the sum
+      for (int i = 0; i < p.tile_cols - 1; ++i) p.col_width.push_back(br.get_ue_max(1u << 11, "column_width_minus1") + 1);
+      for (int i = 0; i < p.tile_rows - 1; ++i) p.row_height.push_back(br.get_ue_max(1u << 11, "row_height_minus1") + 1);
     }
     p.lf_across_tiles = br.get(1);
   }
@@ -401,14 +394,14 @@ void parse_pps(BitReader& br, Pps& p, const Sps* sps_by_id[16]) {
     p.deblock_override_enabled = br.get(1);
     p.deblock_disabled = br.get(1);
     if (!p.deblock_disabled) {
-      p.beta_off = br.get_se() * 2;
-      p.tc_off = br.get_se() * 2;
+      p.beta_off = br.get_se_range(-6, 6, "pps_beta_offset_div2") * 2;
+      p.tc_off = br.get_se_range(-6, 6, "pps_tc_offset_div2") * 2;
     }
   }
   p.scaling_present = br.get(1);
   if (p.scaling_present) parse_scaling_list_data(br, p.scaling);
   p.lists_modification = br.get(1);
-  p.log2_par_mrg_level = static_cast<int>(br.get_ue()) + 2;
+  p.log2_par_mrg_level = br.get_ue_max(4, "log2_parallel_merge_level_minus2") + 2;
   p.slice_header_ext = br.get(1);
   // pps_extension_present_flag: range / multilayer / SCC extensions are outside Main
   if (br.get(1)) {
@@ -472,8 +465,8 @@ void parse_slice_header(BitReader& br, int nal_type, const Sps* const* sps_tab, 
       }
       if (sps.long_term) {
         int nsps = 0;
-        if (!sps.lt_poc_lsb.empty()) nsps = static_cast<int>(br.get_ue());
-        const int npics = static_cast<int>(br.get_ue());
+        if (!sps.lt_poc_lsb.empty()) nsps = br.get_ue_max(32, "num_long_term_sps");
+        const int npics = br.get_ue_max(32, "num_long_term_pics");
         if (nsps > static_cast<int>(sps.lt_poc_lsb.size()) || nsps + npics > 32) fail("long-term picture count out of range");
         h.num_lt = nsps + npics;
         int msb_cycle_prev = 0;
@@ -492,7 +485,8 @@ void parse_slice_header(BitReader& br, int nal_type, const Sps* const* sps_tab, 
           h.lt_used[i] = used != 0;
           h.lt_msb_present[i] = br.get(1);
           int cyc = 0;
-          if (h.lt_msb_present[i]) cyc = static_cast<int>(br.get_ue());
+          // bounded so that the accumulated cycle (<= 32 entries) times MaxPicOrderCntLsb stays below 2^30
+          if (h.lt_msb_present[i]) cyc = br.get_ue_max((1u << (30 - sps.log2_max_poc_lsb)) / 32, "delta_poc_msb_cycle_lt");
           // DeltaPocMsbCycleLt (7-52): accumulates within the SPS entries and within the slice entries
           const int acc = (i == 0 || i == nsps) ? cyc : cyc + msb_cycle_prev;
           msb_cycle_prev = acc;
@@ -544,15 +538,13 @@ void parse_slice_header(BitReader& br, int nal_type, const Sps* const* sps_tab, 
         h.col_from_l0 = true;
         if (h.slice_type == 0) h.col_from_l0 = br.get(1);
         const int nr = h.num_ref[h.col_from_l0 ? 0 : 1];
-        if (nr > 1) h.col_ref_idx = static_cast<int>(br.get_ue());
-        if (h.col_ref_idx >= nr) fail("collocated_ref_idx out of range");
+        if (nr > 1) h.col_ref_idx = br.get_ue_max(static_cast<uint32_t>(nr - 1), "collocated_ref_idx");
       }
       h.weighted = (pps.weighted_pred && h.slice_type == 1) || (pps.weighted_bipred && h.slice_type == 0);
       if (h.weighted) {  // 7.3.6.3 pred_weight_table()
         PredWeights& w = h.pw;
-        w.log2_denom_y = static_cast<int>(br.get_ue());
-        if (w.log2_denom_y > 7) fail("luma_log2_weight_denom out of range");
-        w.log2_denom_c = w.log2_denom_y + br.get_se();
+        w.log2_denom_y = br.get_ue_max(7, "luma_log2_weight_denom");
+        w.log2_denom_c = w.log2_denom_y + br.get_se_range(-7, 7, "delta_chroma_log2_weight_denom");
         if (w.log2_denom_c < 0 || w.log2_denom_c > 7) fail("ChromaLog2WeightDenom out of range");
         for (int l = 0; l < (h.slice_type == 0 ? 2 : 1); ++l) {
           bool lf[16], cf[16];
@@ -563,8 +555,8 @@ void parse_slice_header(BitReader& br, int nal_type, const Sps* const* sps_tab, 
             w.o[l][i][0] = 0;
             w.flag[l][i][0] = lf[i];
             if (lf[i]) {
-              const int dw = br.get_se(), off = br.get_se();
-              if (dw < -128 || dw > 127 || off < -128 || off > 127) fail("luma weight out of range");
+              const int dw = br.get_se_range(-128, 127, "delta_luma_weight");
+              const int off = br.get_se_range(-128, 127, "luma_offset");
               w.w[l][i][0] += dw;
               w.o[l][i][0] = off;
             }
@@ -575,8 +567,8 @@ void parse_slice_header(BitReader& br, int nal_type, const Sps* const* sps_tab, 
             }
             if (cf[i]) {
               for (int j = 1; j < 3; ++j) {
-                const int dw = br.get_se(), doff = br.get_se();
-                if (dw < -128 || dw > 127 || doff < -512 || doff > 511) fail("chroma weight out of range");
+                const int dw = br.get_se_range(-128, 127, "delta_chroma_weight");
+                const int doff = br.get_se_range(-512, 511, "delta_chroma_offset");
                 const int cw = (1 << w.log2_denom_c) + dw;
                 w.w[l][i][j] = cw;
                 // (7-56) ChromaOffset, wpOffsetHalfRangeC = 128
@@ -591,11 +583,10 @@ void parse_slice_header(BitReader& br, int nal_type, const Sps* const* sps_tab, 
       if (fm > 4) fail("five_minus_max_num_merge_cand out of range");
       h.max_merge = 5 - static_cast<int>(fm);
     }
-    h.qp_delta = br.get_se();
+    h.qp_delta = br.get_se_range(-128, 128, "slice_qp_delta");
     if (pps.slice_chroma_qp_offsets) {
-      h.cb_qp_off = br.get_se();
-      h.cr_qp_off = br.get_se();
-      if (h.cb_qp_off < -12 || h.cb_qp_off > 12 || h.cr_qp_off < -12 || h.cr_qp_off > 12) fail("slice chroma qp offset out of range");
+      h.cb_qp_off = br.get_se_range(-12, 12, "slice_cb_qp_offset");
+      h.cr_qp_off = br.get_se_range(-12, 12, "slice_cr_qp_offset");
     }
     h.deblock_disabled = pps.deblock_disabled;
     h.beta_off = pps.beta_off;
@@ -605,9 +596,8 @@ void parse_slice_header(BitReader& br, int nal_type, const Sps* const* sps_tab, 
     if (override_flag) {
       h.deblock_disabled = br.get(1);
       if (!h.deblock_disabled) {
-        h.beta_off = br.get_se() * 2;
-        h.tc_off = br.get_se() * 2;
-        if (h.beta_off < -12 || h.beta_off > 12 || h.tc_off < -12 || h.tc_off > 12) fail("deblocking offsets out of range");
+        h.beta_off = br.get_se_range(-6, 6, "slice_beta_offset_div2") * 2;
+        h.tc_off = br.get_se_range(-6, 6, "slice_tc_offset_div2") * 2;
       }
     }
     h.lf_across_slices = pps.lf_across_slices;
@@ -617,8 +607,7 @@ void parse_slice_header(BitReader& br, int nal_type, const Sps* const* sps_tab, 
     const uint32_t ne = br.get_ue();
     if (ne > static_cast<uint32_t>(nctb)) fail("num_entry_point_offsets out of range");
     if (ne > 0) {
-      const int len = static_cast<int>(br.get_ue()) + 1;
-      if (len > 32) fail("offset_len_minus1 out of range");
+      const int len = br.get_ue_max(31, "offset_len_minus1") + 1;
       for (uint32_t k = 0; k < ne; ++k) h.entry_points.push_back(br.get(len) + 1);
     }
   }
@@ -777,9 +766,9 @@ std::vector<std::vector<uint8_t>> hevc_split_pieces(const uint8_t* p, size_t n, 
         }
         if (lp[i]) br.get(8);
       }
-      return static_cast<int>(br.get_ue());
+      return br.get_ue_max(15, "sps_seq_parameter_set_id");
     }
-    return static_cast<int>(br.get_ue());
+    return br.get_ue_max(63, "pps_pic_parameter_set_id");
   };
   for (size_t c = 0; c < cuts.size(); ++c) {
     const size_t a0 = cuts[c], a1 = c + 1 < cuts.size() ? cuts[c + 1] : aus.size();

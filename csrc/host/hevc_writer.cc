@@ -432,7 +432,9 @@ struct Writer {
               for (int g0 = 0; g0 < 2; ++g0)
                 for (int p = 0; p < 16; ++p) {
                   const int q = scans().t[sc][2][p];
-                  const int xs = g0 ? 0 : 1, ys = 0;  // any sub-block other than the first
+                  // any sub-block other than the first (a 4x4 TU has only the first: the g0 = 0
+                  // entries of l = 0 are never read, keep them in range)
+                  const int xs = (g0 || l == 0) ? 0 : 1, ys = 0;
                   t[l][c][sc][pc][g0][p] = static_cast<uint8_t>(
                       sig_ctx(xs * 4 + (q & 15), ys * 4 + (q >> 4), l + 2, c, sc, pc, xs, ys));
                 }

@@ -73,12 +73,14 @@ DEFAULT_8x8_INTER = [16, 16, 16, 16, 16, 16, 16, 16, 16, 16, 17, 17, 17, 17, 17,
 class Bits:
     def __init__(self):
         self.b: list[int] = []
+        self.ue_sites: list[int] = []   # bit index of every ue(v) / se(v) code (for the range tests)
 
     def u(self, v: int, n: int):
         for k in range(n - 1, -1, -1):
             self.b.append((v >> k) & 1)
 
     def ue(self, v: int):
+        self.ue_sites.append(len(self.b))
         v += 1
         n = v.bit_length()
         self.u(0, n - 1)
@@ -86,6 +88,23 @@ class Bits:
 
     def se(self, v: int):
         self.ue(2 * v - 1 if v > 0 else -2 * v)
+
+    def with_ue(self, site: int, value: int) -> "Bits":
+        """A copy whose ``site``-th Exp-Golomb code carries ``value`` instead (any size up to
+        2^33 - 2, i.e. up to 32 leading zeros): the rest of the bits follow unchanged."""
+        start = self.ue_sites[site]
+        lz = 0
+        while self.b[start + lz] == 0:
+            lz += 1
+        out = Bits()
+        out.b = self.b[:start]
+        v = value + 1
+        n = v.bit_length()
+        out.u(0, n - 1)
+        out.u(v, n)
+        out.b += self.b[start + 2 * lz + 1:]
+        out.align_zero()
+        return out
 
     def align_zero(self):
         while len(self.b) % 8:
@@ -250,13 +269,30 @@ class KatStream:
     """One coded video sequence: an IDR of PCM CUs, then P pictures built CTU by CTU."""
 
     def __init__(self, w: int, h: int, bit_depth: int = 8, ctb_log2: int = 4, max_tb_log2: int | None = None,
-                 weighted: bool = False, scaling: dict | None = None, max_merge: int = 1):
+                 weighted: bool = False, scaling: dict | None = None, max_merge: int = 1, sps_st_rps: int = 0):
         self.w, self.h, self.bd, self.ctb = w, h, bit_depth, ctb_log2
         self.max_tb = max_tb_log2 if max_tb_log2 is not None else min(5, ctb_log2)
         self.weighted, self.scaling, self.max_merge = weighted, scaling, max_merge
+        self.sps_st_rps = sps_st_rps
         assert w % (1 << ctb_log2) == 0 and h % (1 << ctb_log2) == 0
         self.out = bytearray()
+        self.units: list[tuple[int, Bits]] = []
         self._params()
+
+    def _emit(self, ntype: int, b: Bits):
+        self.units.append((ntype, b))
+        self.out += nal(ntype, b.bytes())
+
+    def ue_sites(self) -> list[tuple[int, int]]:
+        """(unit, site) of every Exp-Golomb code written so far."""
+        return [(k, j) for k, (_, b) in enumerate(self.units) for j in range(len(b.ue_sites))]
+
+    def with_ue(self, unit: int, site: int, value: int) -> bytes:
+        """The stream with one Exp-Golomb code replaced (parser range / wrap tests)."""
+        out = bytearray()
+        for k, (t, b) in enumerate(self.units):
+            out += nal(t, (b.with_ue(site, value) if k == unit else b).bytes())
+        return bytes(out)
 
     # ------------------------------------------------------------ parameter sets
     def _params(self):
@@ -277,7 +313,7 @@ class KatStream:
         b.u(0, 1)
         b.u(0, 1)
         b.trailing()
-        self.out += nal(32, b.bytes())
+        self._emit(32, b)
 
         b = Bits()
         b.u(0, 4)
@@ -314,14 +350,22 @@ class KatStream:
         b.ue(0)            # min PCM CB 8
         b.ue(min(self.ctb, 5) - 3)
         b.u(1, 1)          # pcm_loop_filter_disabled_flag
-        b.ue(0)            # num_short_term_ref_pic_sets: every RPS in the slice header
+        # num_short_term_ref_pic_sets (0: every RPS in the slice header); SPS sets are {-1}
+        b.ue(self.sps_st_rps)
+        for i in range(self.sps_st_rps):
+            if i:
+                b.u(0, 1)  # inter_ref_pic_set_prediction_flag
+            b.ue(1)
+            b.ue(0)
+            b.ue(0)
+            b.u(1, 1)
         b.u(0, 1)          # long_term_ref_pics_present_flag
         b.u(1, 1)          # sps_temporal_mvp_enabled_flag
         b.u(0, 1)          # strong intra smoothing
         b.u(0, 1)          # vui
         b.u(0, 1)          # extensions
         b.trailing()
-        self.out += nal(33, b.bytes())
+        self._emit(33, b)
 
         b = Bits()
         b.ue(0)
@@ -355,7 +399,7 @@ class KatStream:
         b.u(0, 1)
         b.u(0, 1)
         b.trailing()
-        self.out += nal(34, b.bytes())
+        self._emit(34, b)
 
     # ------------------------------------------------------------ pictures
     def idr_pcm(self, y, u, v, qp: int = 26):
@@ -391,10 +435,10 @@ class KatStream:
                     c.start()
             c.terminate(1 if k == len(ctus) - 1 else 0)  # end_of_slice_segment_flag
         b.align_zero()
-        self.out += nal(19, b.bytes())
+        self._emit(19, b)
 
     def p_picture(self, poc: int, refs: list[int], cus: list[dict], tmvp: bool = False, qp: int = 26,
-                  wp: dict | None = None):
+                  wp: dict | None = None, nref: int | None = None, inter_rps: bool = False):
         """TRAIL_R P picture.  ``refs``: POCs of the RPS (all used by the current picture, the
         first is RefPicList0[0]; ordered by decreasing POC as 8.3.2 builds StCurrBefore);
         ``cus``: one dict per CTU in raster order, each one CU of CTB size:
@@ -405,7 +449,10 @@ class KatStream:
         * ``{"mvd": (x, y), "dc": [level per TB]}``       -- plus one DC coefficient per luma TB.
 
         ``wp``: {"denom", "w", "o", "cdenom_delta", "cw": [(w, o)] * 2} (delta-coded by the
-        writer the way pred_weight_table codes them) or None."""
+        writer the way pred_weight_table codes them) or None.  ``nref``: code
+        num_ref_idx_l0_active_minus1 (skip CUs only when > 1: no ref_idx is written).
+        ``inter_rps``: predict the slice RPS from the last SPS set (needs ``sps_st_rps`` >= 1;
+        delta_rps -1 on the set {-1}: gives {-1, -2})."""
         b = Bits()
         b.u(1, 1)
         b.ue(0)
@@ -413,15 +460,31 @@ class KatStream:
         b.u(poc & 255, 8)
         b.u(0, 1)          # short_term_ref_pic_set_sps_flag
         assert all(r < poc for r in refs) and refs == sorted(refs, reverse=True)
-        b.ue(len(refs))
-        b.ue(0)
-        prev = poc
-        for r in refs:
-            b.ue(prev - r - 1)
-            b.u(1, 1)
-            prev = r
+        if inter_rps:
+            assert self.sps_st_rps and refs == [poc - 1, poc - 2]
+            b.u(1, 1)      # inter_ref_pic_set_prediction_flag
+            b.ue(0)        # delta_idx_minus1
+            b.u(1, 1)      # delta_rps_sign: negative
+            b.ue(0)        # abs_delta_rps_minus1
+            b.u(1, 1)      # used_by_curr_pic_flag[0]
+            b.u(1, 1)      # used_by_curr_pic_flag[1]
+        else:
+            if self.sps_st_rps:
+                b.u(0, 1)  # inter_ref_pic_set_prediction_flag (stRpsIdx > 0)
+            b.ue(len(refs))
+            b.ue(0)
+            prev = poc
+            for r in refs:
+                b.ue(prev - r - 1)
+                b.u(1, 1)
+                prev = r
         b.u(1 if tmvp else 0, 1)
-        b.u(0, 1)          # num_ref_idx_active_override_flag
+        b.u(1 if nref else 0, 1)  # num_ref_idx_active_override_flag
+        if nref:
+            assert all(cu.get("skip") for cu in cus)
+            b.ue(nref - 1)
+        if tmvp and nref and nref > 1:
+            b.ue(0)        # collocated_ref_idx
         if self.weighted:
             self._pred_weight_table(b, wp)
         b.ue(5 - self.max_merge)
@@ -463,7 +526,7 @@ class KatStream:
                     self._transform_tree(c, self.ctb, dc)
             c.terminate(1 if k == len(ctus) - 1 else 0)
         b.align_zero()
-        self.out += nal(1, b.bytes())
+        self._emit(1, b)
 
     def _pred_weight_table(self, b: Bits, wp: dict | None):
         wp = wp or {}

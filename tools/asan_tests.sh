@@ -13,6 +13,6 @@ export ASAN_OPTIONS=detect_leaks=0:abort_on_error=1:halt_on_error=1
 export UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1
 # -s: a sanitizer report goes to stderr just before the process exits; pytest capture would eat it
 LD_PRELOAD="$asan $ubsan" python -m pytest -s -q -p no:warnings -p no:cacheprovider \
-  tests/test_fuzz_parsers.py tests/test_host_codec.py tests/test_decode_parse.py tests/test_cabac.py \
+  tests/test_fuzz_parsers.py tests/test_parser_ranges.py tests/test_host_codec.py tests/test_decode_parse.py tests/test_cabac.py \
   tests/test_h264_bframes.py tests/test_hevc_codec.py tests/test_mp4_tracks.py tests/test_mp4_hevc.py \
   tests/test_segment_media.py "$@"
