@@ -49,7 +49,10 @@ SPS make_sps(const EncoderConfig& cfg) {
   } else {
     s.poc_type = 2;
   }
+  // must equal models/gop.py dpb_frames(): the active references plus one with B pictures; a
+  // pyramid needs >= 4 (see dpb_frames)
   s.max_num_ref_frames = std::max(1, cfg.refs) + (cfg.bframes > 0 ? 1 : 0);
+  if (cfg.pyramid && cfg.bframes >= 2) s.max_num_ref_frames = std::max(s.max_num_ref_frames, 4);
   s.vui_present = cfg.vui;
   if (cfg.cqm && !cfg.t8x8) throw std::runtime_error("H.264: scaling matrices need the High profile (t8x8)");
   if (cfg.cqm == 3) s.scaling_present = 1;  // the default matrices, overridden by the PPS lists (rule B)

@@ -69,8 +69,15 @@ def fixed_types(frames: int, bframes: int, anchors_at=()) -> str:
 
 def dpb_frames(refs: int, pyramid: bool, bframes: int) -> int:
     """max_num_ref_frames of the stream (the SPS value, csrc/host/cpu_encoder.cc): the active
-    references plus one when B pictures are on (a reference B or the next anchor's slot)."""
-    return max(1, int(refs)) + (1 if int(bframes) > 0 else 0)
+    references plus one when B pictures are on (a reference B or the next anchor's slot).  A
+    pyramid (runs of two or more B) needs at least 4 even with ``refs`` 1: the window (no MMCO,
+    oldest frame_num out) holds the run's anchors a0 / a1 and its reference B, plus the previous
+    run's reference B, which sits between a0 and a1 in frame_num order -- with fewer, storing
+    the new reference B evicts a0 and the B pictures after it lose their list-0 anchor."""
+    n = max(1, int(refs)) + (1 if int(bframes) > 0 else 0)
+    if pyramid and int(bframes) >= 2:
+        n = max(n, 4)
+    return n
 
 
 def h264_plan(types: str, refs: int = 1, pyramid: bool = False, nref_frames: int | None = None) -> list[PicPlan]:

@@ -442,7 +442,10 @@ class GpuHevcEncoder:
             use = (np.abs(m1[:, 0] - m0[:, 0]) >= self.p.wp_min_mean) | (np.abs(scale[:, 0] - 1) >= self.p.wp_min_scale)
             if not use.any():
                 continue
-            wq = np.clip(np.round(scale * 64), 0, 127).astype(np.int64)
+            # weight >= 1: the kernels read weight 0 as "this slot is not weighted" (hevc_inter.hip),
+            # so a fade to a flat plane (variance -> 0) must not quantise to 0 while the writer
+            # still codes the flag -- the decoder would predict offset-only samples
+            wq = np.clip(np.round(scale * 64), 1, 127).astype(np.int64)
             oq = np.clip(np.round(m1 - wq / 64.0 * m0), -128, 127).astype(np.int64)
             rows = [[int(x) for c in range(3) for x in (wq[b, c], oq[b, c])] if use[b] else None for b in range(B)]
             dev = np.zeros((B, 6), np.int16)

@@ -158,11 +158,14 @@ def access_units(payload: bytes, codec: str) -> int:
         i += 3
 
 
-def per_picture_pts(pes: list[tuple[bytes, int | None]], codec: str) -> list[float]:
+def per_picture_pts(pes: list[tuple[bytes, int | None]], codec: str, display: list[int] | None = None) -> list[float]:
     """One presentation time (seconds, unwrapped 90 kHz ticks / 90000) per picture, decode
     order: a PES's PTS belongs to the first picture starting in it (ISO 13818-1 2.4.3.7);
     pictures without one (later pictures of a multi-picture PES, PES packets without a PTS)
-    are interpolated from the previous picture at the stream's frame interval."""
+    are placed at the stream's frame interval from the nearest picture with a PTS in DISPLAY
+    order -- ``display``: each picture's display index (decode order, from the POCs; None:
+    no reordering), since with B pictures the previous picture in decode order is usually a
+    later anchor."""
     ticks = unwrap_pts([t for _, t in pes])
     per: list[float | None] = []
     for (pl, _), t in zip(pes, ticks):
@@ -176,13 +179,35 @@ def per_picture_pts(pes: list[tuple[bytes, int | None]], codec: str) -> list[flo
     known = sorted((x, i) for i, x in enumerate(per) if x is not None)
     steps = [(b - a) / abs(j - i) for (a, i), (b, j) in zip(known, known[1:]) if b > a and j != i]
     dt = sorted(steps)[len(steps) // 2] if steps else 1.0 / 30
-    out, last = [], None
-    for x in per:
+    if display is None or len(display) != len(per):
+        display = list(range(len(per)))
+    known_d = sorted((display[i], x) for i, x in enumerate(per) if x is not None)
+    out = []
+    for i, x in enumerate(per):
         if x is None:
-            x = (last + dt) if last is not None else 0.0
+            d = display[i]
+            before = [(kd, kx) for kd, kx in known_d if kd < d]
+            after = [(kd, kx) for kd, kx in known_d if kd > d]
+            if before:
+                x = before[-1][1] + (d - before[-1][0]) * dt
+            elif after:
+                x = after[0][1] - (after[0][0] - d) * dt
+            else:
+                x = d * dt
         out.append(x)
-        last = x
     return out
+
+
+def _display_order(stream: bytes, codec: str) -> list[int] | None:
+    """Display index per picture (decode order) from the stream's POCs; None if unparsable."""
+    try:
+        if codec == "h264":
+            from ..ops import native
+            return list(native.host().h264_samples(stream)["display"])
+        from .mp4_hevc import display_order
+        return display_order(stream)
+    except Exception:  # noqa: BLE001 -- a damaged stream still demuxes, with decode-order fill
+        return None
 
 
 def ts_demux(data: bytes) -> Demuxed:
@@ -274,7 +299,7 @@ def _ts_demux(data: bytes) -> Demuxed:
     codec = TS_VIDEO[streams[vp]]
     out = Demuxed(codec, b"".join(pl for pl, _ in vpes))
     first_tick = next((t for _, t in vpes if t is not None), None)
-    pics = per_picture_pts(vpes, codec)
+    pics = per_picture_pts(vpes, codec, _display_order(out.annexb, codec))
     t0 = min(pics) if pics else 0.0
     out.pts = [t - t0 for t in pics]
     for pid, st in sorted(streams.items()):

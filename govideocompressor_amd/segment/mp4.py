@@ -38,10 +38,20 @@ class Track:
     sync: list[bool] | None = None      # None: every sample is a sync sample
     width: int = 0
     height: int = 0
-    # first edit's media_time (media timescale), 0 = no edit list; negative: the track starts
-    # that much after the movie (an empty edit of -media_time, then the media from 0)
+    # the media edit's media_time (media timescale): samples before it are hidden (B-picture
+    # reordering delay, AAC priming); 0 = the media plays from its start
     media_time: int = 0
     language: int = 0x55C4              # 'und'
+    # start delay (media timescale): an empty edit of this length plays before the media edit
+    # (audio beginning after the video).  Independent of media_time, so a late AAC track keeps
+    # its priming skip.  A negative media_time given to the constructor means a delay (older
+    # callers' convention) and is moved here.
+    delay: int = 0
+
+    def __post_init__(self):
+        if self.media_time < 0:
+            self.delay += -self.media_time
+            self.media_time = 0
 
     @property
     def codec(self) -> bytes:
@@ -61,7 +71,7 @@ class Track:
     def pts_seconds(self) -> list[float]:
         """Presentation time of every sample (decode order), edit list applied."""
         c = self.cts or [0] * len(self.samples)
-        return [(d + o - self.media_time) / self.timescale for d, o in zip(self.dts(), c)]
+        return [(d + o - self.media_time + self.delay) / self.timescale for d, o in zip(self.dts(), c)]
 
 
 # ------------------------------------------------------------------------------- boxes
@@ -205,7 +215,7 @@ def _read_trak(data: bytes, s: int, e: int, movie_ts: int = 1000) -> Track:
         ne = struct.unpack(">I", data[a + 4:a + 8])[0]
         marks = set(struct.unpack(f">{ne}I", data[a + 8:a + 8 + 4 * ne]))
         sync = [(i + 1) in marks for i in range(n)]
-    media_time = 0
+    media_time = delay = 0
     ed = _child(data, s, e, b"edts")
     if ed is not None:
         el = _child(data, ed[0], ed[1], b"elst")
@@ -224,10 +234,11 @@ def _read_trak(data: bytes, s: int, e: int, movie_ts: int = 1000) -> Track:
                 if mt < 0:
                     empty += sd
                     continue
-                media_time = mt - (empty * timescale + movie_ts // 2) // max(movie_ts, 1)
+                media_time = mt
+                delay = (empty * timescale + movie_ts // 2) // max(movie_ts, 1)
                 break
     del ver
-    return Track(handler, timescale, entry, samples, durs, cts, sync, width >> 16, height >> 16, media_time, lang)
+    return Track(handler, timescale, entry, samples, durs, cts, sync, width >> 16, height >> 16, media_time, lang, delay)
 
 
 def read(data: bytes) -> list[Track]:
@@ -271,7 +282,7 @@ def _trak(t: Track, track_id: int, chunks: list[tuple[int, int]], offs: list[int
     n = len(t.samples)
     media_dur = t.duration
     edit_dur = media_dur - t.media_time
-    movie_dur = (edit_dur * movie_ts + t.timescale - 1) // t.timescale
+    movie_dur = ((edit_dur + t.delay) * movie_ts + t.timescale - 1) // t.timescale
     v1 = media_dur > 0xFFFFFFFF or movie_dur > 0xFFFFFFFF
     stts = _full(b"stts", 0, 0, struct.pack(">I", len(r := _runs(t.durations))), *(struct.pack(">II", c, d) for c, d in r))
     parts = [_full(b"stsd", 0, 0, struct.pack(">I", 1), t.sample_entry), stts]
@@ -323,17 +334,17 @@ def _trak(t: Track, track_id: int, chunks: list[tuple[int, int]], offs: list[int
         tkhd = _full(b"tkhd", 0, 3, struct.pack(">IIIII", 0, 0, track_id, 0, movie_dur), bytes(8),
                      struct.pack(">hhhH", 0, 0, vol, 0), _MATRIX, struct.pack(">II", t.width << 16, t.height << 16))
     boxes = [tkhd]
-    if t.media_time > 0:
+    if t.delay > 0:  # start delay: an empty edit, then the media from media_time
+        delay = (t.delay * movie_ts + t.timescale // 2) // t.timescale
+        media_movie = (edit_dur * movie_ts + t.timescale - 1) // t.timescale
+        fmt = ">IQqhhQqhh" if v1 else ">IIihhIihh"
+        el = _full(b"elst", 1 if v1 else 0, 0, struct.pack(fmt, 2, delay, -1, 1, 0, media_movie, t.media_time, 1, 0))
+        boxes.append(_box(b"edts", el))
+    elif t.media_time > 0:
         if v1:
             el = _full(b"elst", 1, 0, struct.pack(">IQqhh", 1, movie_dur, t.media_time, 1, 0))
         else:
             el = _full(b"elst", 0, 0, struct.pack(">IIihh", 1, movie_dur, t.media_time, 1, 0))
-        boxes.append(_box(b"edts", el))
-    elif t.media_time < 0:  # start delay: an empty edit, then the whole media
-        delay = (-t.media_time * movie_ts + t.timescale // 2) // t.timescale
-        media_movie = (media_dur * movie_ts + t.timescale - 1) // t.timescale
-        fmt = ">IQqhhQqhh" if v1 else ">IIihhIihh"
-        el = _full(b"elst", 1 if v1 else 0, 0, struct.pack(fmt, 2, delay, -1, 1, 0, media_movie, 0, 1, 0))
         boxes.append(_box(b"edts", el))
     return _box(b"trak", *boxes, mdia)
 
@@ -373,7 +384,7 @@ def write(tracks: list[Track], brand: bytes = b"isom", chunk_seconds: float = 0.
         s0, cnt = per_track[ti][ci]
         for s in tracks[ti].samples[s0:s0 + cnt]:
             body += s
-    moov_dur = max((t.duration - t.media_time) * movie_ts // t.timescale for t in tracks)
+    moov_dur = max((t.duration - t.media_time + t.delay) * movie_ts // t.timescale for t in tracks)
     v1 = moov_dur > 0xFFFFFFFF
     if v1:
         mvhd = _full(b"mvhd", 1, 0, struct.pack(">QQIQ", 0, 0, movie_ts, moov_dur), struct.pack(">IH", 0x10000, 0x100),
@@ -481,18 +492,24 @@ def cut(t: Track, t0: float, t1: float | None) -> Track:
     ``media_time``, so the piece, and the merge that starts with it, play the same samples
     from the same instant as the input."""
     pts = t.pts_seconds()
+    # samples the media edit hides (dts + cts < media_time: AAC priming) travel with the track's
+    # first presented sample, whichever piece that lands in (a late-starting track included)
+    c = t.cts or [0] * len(t.samples)
+    hidden = [d + o < t.media_time for d, o in zip(t.dts(), c)]
+    eff = [t.delay / t.timescale if h else x for x, h in zip(pts, hidden)]
     first = t0 <= 1e-9
-    keep = [i for i, x in enumerate(pts) if (first or x >= t0 - 1e-9) and (t1 is None or x < t1 - 1e-9)]
-    mt = t.media_time if first else 0
+    keep = [i for i, x in enumerate(eff) if (first or x >= t0 - 1e-9) and (t1 is None or x < t1 - 1e-9)]
+    mt = t.media_time if any(hidden[i] for i in keep) else 0
+    delay = t.delay if first else 0
     if not first and keep and t.durations:
         # a track that starts inside this piece (audio beginning after the video): keep the
         # gap as a start delay instead of playing the samples from the piece's first instant
-        gap = pts[keep[0]] - t0
+        gap = eff[keep[0]] - t0
         if gap * t.timescale > 2 * max(t.durations):
-            mt = -int(round(gap * t.timescale))
+            delay = int(round(gap * t.timescale))
     return Track(t.handler, t.timescale, t.sample_entry, [t.samples[i] for i in keep], [t.durations[i] for i in keep],
                  [t.cts[i] for i in keep] if t.cts else None, [t.sync[i] for i in keep] if t.sync else None,
-                 t.width, t.height, mt, t.language)
+                 t.width, t.height, mt, t.language, delay)
 
 
 def concat(parts: list[Track], starts: list[float] | None = None) -> Track:
@@ -509,15 +526,16 @@ def concat(parts: list[Track], starts: list[float] | None = None) -> Track:
         raise ValueError("mp4: no samples to concatenate")
     first = parts[0]
     if starts is not None and starts[lead] > 0:
+        # the part's own delay plus where it begins; its media_time (a priming skip) stays
         first = Track(first.handler, first.timescale, first.sample_entry, first.samples, first.durations, first.cts,
-                      first.sync, first.width, first.height,
-                      min(first.media_time, 0) - int(round(starts[lead] * first.timescale)), first.language)
+                      first.sync, first.width, first.height, first.media_time, first.language,
+                      first.delay + int(round(starts[lead] * first.timescale)))
         parts[0] = first
     for p in parts[1:]:
         if p.sample_entry != first.sample_entry or p.timescale != first.timescale:
             raise ValueError("mp4: pieces carry different audio formats; cannot stream-copy them into one track")
     out = Track(first.handler, first.timescale, first.sample_entry, [], [], None, None, first.width, first.height,
-                first.media_time, first.language)
+                first.media_time, first.language, first.delay)
     any_cts = any(p.cts for p in parts)
     any_sync = any(p.sync is not None for p in parts)
     cts, sync = [], []

@@ -8,8 +8,10 @@ with ``ffmpeg -f concat -c copy`` (server.go:349-361).  The native muxer in
 arrays, 4-byte NAL length prefixes in ``mdat``).  Container-only work on host
 bytes, so it is plain Python: a piece is a few MB and this runs once per piece.
 
-The encoder's HEVC streams are IDR + P in output order (no reordering), so decode
-time == composition time and no ``ctts`` box is needed.
+B pictures (the encoder's default GOP codes one B between anchors, x265 --bframes) are
+stored in decode order, so the track carries composition offsets (``ctts``) and an edit
+list from the pictures' PicOrderCnt (8.3.1, parsed here from the slice headers) like the
+``avc1`` track of segment/mp4.py.
 """
 from __future__ import annotations
 
@@ -88,7 +90,7 @@ def parse_sps(sps_nal: bytes) -> dict:
         br.p += 2 * (8 - max_sub)
     for i in range(max_sub):
         br.p += 88 * sub_prof[i] + 8 * sub_lvl[i]
-    br.ue()
+    sps_id = br.ue()
     chroma = br.ue()
     if chroma == 3:
         br.u(1)
@@ -99,8 +101,71 @@ def parse_sps(sps_nal: bytes) -> dict:
         w -= sw * (left + right)
         h -= sh * (top + bottom)
     bdl, bdc = br.ue(), br.ue()
+    log2_poc = br.ue() + 4
     return dict(ptl=ptl, max_sub_layers=max_sub + 1, temporal_nesting=nesting, chroma_format_idc=chroma,
-                width=w, height=h, bit_depth_luma=bdl + 8, bit_depth_chroma=bdc + 8)
+                width=w, height=h, bit_depth_luma=bdl + 8, bit_depth_chroma=bdc + 8, sps_id=sps_id,
+                log2_max_poc_lsb=log2_poc)
+
+
+def display_order(stream: bytes) -> list[int]:
+    """Display index of every picture of an Annex-B HEVC stream, in decode order: PicOrderCnt
+    (8.3.1: slice_pic_order_cnt_lsb plus the MSB carried from the previous TemporalId-0
+    reference picture) ranked within each coded video sequence (an IDR / BLA, or a CRA that
+    starts the stream), sequences following each other."""
+    sps_lsb: dict[int, int] = {}
+    pps: dict[int, tuple[int, int, int]] = {}   # id -> (sps id, output_flag_present, extra bits)
+    pocs: list[tuple[int, int]] = []            # (cvs ordinal, POC) per picture, decode order
+    cvs, prev_lsb, prev_msb, first = -1, 0, 0, True
+    for nal in split_nals(stream):
+        t = (nal[0] >> 1) & 0x3F
+        if t == _SPS:
+            info = parse_sps(nal)
+            sps_lsb[info["sps_id"]] = info["log2_max_poc_lsb"]
+            continue
+        if t == _PPS:
+            br = _Bits(_rbsp(nal)[2:])
+            pid, sid = br.ue(), br.ue()
+            br.u(1)
+            pps[pid] = (sid, br.u(1), br.u(3))
+            continue
+        if t >= 32 or len(nal) < 3 or not nal[2] & 0x80:
+            continue  # non-VCL, or not the first slice segment of a picture
+        br = _Bits(_rbsp(nal)[2:])
+        br.u(1)
+        if 16 <= t <= 23:
+            br.u(1)
+        sid, out_flag, extra = pps[br.ue()]
+        br.u(extra)
+        br.ue()   # slice_type
+        if out_flag:
+            br.u(1)
+        log2 = sps_lsb[sid]
+        irap_reset = t in (16, 17, 18, 19, 20) or (t == 21 and first)
+        if t in (19, 20):       # IDR: PicOrderCnt 0
+            lsb = 0
+        else:
+            lsb = br.u(log2)
+        if irap_reset:
+            msb = 0
+            cvs += 1
+        else:
+            half = 1 << (log2 - 1)
+            if lsb < prev_lsb and prev_lsb - lsb >= half:
+                msb = prev_msb + (1 << log2)
+            elif lsb > prev_lsb and lsb - prev_lsb > half:
+                msb = prev_msb - (1 << log2)
+            else:
+                msb = prev_msb
+        first = False
+        tid = (nal[1] & 7) - 1
+        if tid == 0 and not (t <= 14 and t % 2 == 0) and t not in (6, 7, 8, 9):  # not SLNR / RADL / RASL
+            prev_lsb, prev_msb = lsb, msb
+        pocs.append((cvs, msb + lsb))
+    ranks = sorted(range(len(pocs)), key=lambda i: pocs[i])
+    out = [0] * len(pocs)
+    for r, i in enumerate(ranks):
+        out[i] = r
+    return out
 
 
 def _box(kind: bytes, *payload: bytes) -> bytes:
@@ -170,8 +235,12 @@ def hevc_track(stream: bytes, fps: float | None = 30.0):
     timescale, delta = int(round(fps * 1000)), 1000
     entry = mp4._visual_entry(b"hvc1", w, h, _box(b"hvcC", hvcc_record(vps, sps, pps)))
     marks = set(sync)
-    return mp4.Track(b"vide", timescale, entry, [bytes(x) for x in samples], [delta] * len(samples), None,
-                     [(i + 1) in marks for i in range(len(samples))], w, h)
+    disp = display_order(stream)
+    if len(disp) != len(samples):
+        raise ValueError("hevc mp4 mux: picture count and slice headers disagree")
+    cts, media_time = mp4.reorder_offsets(disp, delta)
+    return mp4.Track(b"vide", timescale, entry, [bytes(x) for x in samples], [delta] * len(samples),
+                     cts if media_time else None, [(i + 1) in marks for i in range(len(samples))], w, h, media_time)
 
 
 def mux(stream: bytes, fps: float = 30.0) -> bytes:

@@ -115,10 +115,10 @@ def test_ts_audio_starting_after_the_video_keeps_its_delay(tmp_path, host):
     ts = CS.write_ts(stream, 25.0, frames, audio_delay_s=0.5)
     dm = C.ts_demux(ts)
     a = dm.audio[0]
-    assert a.samples == frames and a.media_time == -24000
+    assert a.samples == frames and a.delay == 24000 and a.media_time == 0
     assert abs(a.pts_seconds()[0] - 0.5) < 1e-6
     back = mp4.audio_tracks(mp4.read(mp4.mux_video(dm.annexb, 25.0, "h264", [a])))[0]
-    assert back.media_time == -24000 and abs(back.pts_seconds()[0] - 0.5) < 1e-3
+    assert back.delay == 24000 and abs(back.pts_seconds()[0] - 0.5) < 1e-3
     # pieces of 4 pictures (0.16 s): the audio begins inside the fourth piece
     src = tmp_path / "late.ts"
     src.write_bytes(ts)
@@ -153,3 +153,50 @@ def test_ts_pts_wrap_and_pes_without_pts(host):
     assert len(dm.pts) == 12 and not any(np.isnan(dm.pts))
     # P-only stream: decode order = display order, so interpolation recovers every time
     assert np.allclose(dm.pts, ref.pts, atol=1e-3)
+
+
+def _hevc_b(host, frames=9):
+    from govideocompressor_amd.models.gop import hevc_gop_plan
+    from govideocompressor_amd.utils.hevc_synth import random_gop_stream
+    stream, _ = random_gop_stream(host, 64, 64, frames, bframes=3, seed=61, pyramid=True)
+    return stream, [p.d for p in hevc_gop_plan(frames, 3, True)]
+
+
+def test_hevc_mp4_track_carries_composition_offsets(host):
+    """HEVC pieces with B pictures: the hvc1 track's composition times follow the POCs
+    (display order), not the decode order (round-4 review found no ctts for HEVC)."""
+    from govideocompressor_amd.segment import mp4, mp4_hevc
+    stream, disp = _hevc_b(host)
+    assert mp4_hevc.display_order(stream) == disp
+    tr = mp4_hevc.hevc_track(stream, 25.0)
+    pts = tr.pts_seconds()
+    assert [round(x * 25) for x in pts] == disp
+    back = mp4.video_track(mp4.read(mp4.write([tr])))
+    assert [round(x * 25) for x in back.pts_seconds()] == disp
+
+
+@pytest.mark.parametrize("codec", ["h264", "hevc"])
+def test_ts_missing_pts_filled_in_display_order(host, codec):
+    """Two pictures per PES with B-picture reordering: the picture without its own PTS gets
+    one from its display-order neighbour, not from the previous (later) anchor in decode
+    order."""
+    if codec == "hevc":
+        stream, _ = _hevc_b(host)
+    else:
+        from govideocompressor_amd.models.gop import h264_plan
+        from test_h264_pyramid import _pic_records
+        rng = np.random.default_rng(62)
+        cfg = dict(width=64, height=48, qp=28, cabac=1, bframes=3, refs=1, pyramid=0, deblock=0, weighted_bipred=0)
+        parts = [host.parameter_sets(cfg)]
+        for pic in h264_plan("IBBBPBBBP", refs=1):
+            hdr, coef = _pic_records(rng, 12, 4, pic.kind, 28)
+            fp = dict(idr=int(pic.kind == "I"), qp=28, frame_num=pic.frame_num, poc=pic.poc,
+                      slice_type=pic.slice_type, nal_ref_idc=pic.nal_ref_idc, direct_spatial=1)
+            if pic.kind != "I":
+                fp["num_ref_l0"], fp["num_ref_l1"] = len(pic.refs0), 1
+            parts.append(host.write_slice(cfg, fp, hdr, coef)[0])
+        stream = b"".join(parts)
+    ref = C.ts_demux(CS.write_ts(stream, 25.0, []))
+    assert sorted(round(x * 25) for x in ref.pts) == list(range(9))
+    dm = C.ts_demux(CS.write_ts(stream, 25.0, [], pes_pictures=2))
+    assert np.allclose(dm.pts, ref.pts, atol=1e-3), (dm.pts, ref.pts)

@@ -288,6 +288,26 @@ def test_gpu_hevc_weightp_fade_matches_decoder(host):
     assert sizes[True] < sizes[False], sizes
 
 
+def test_gpu_hevc_weightp_fade_to_flat_matches_decoder(host):
+    """A fade to a flat picture: the current plane's variance collapses, so the luma / chroma
+    weight quantises towards 0.  The slot must stay weighted (weight >= 1, the kernels read 0 as
+    "not weighted") so encoder and decoder predict the same samples (round-4 review)."""
+    from govideocompressor_amd.models.h264_gpu import synth_clip
+    from govideocompressor_amd.models.hevc_gpu import GpuHevcEncoder, HevcParams
+    y, u, v = synth_clip(2, 8, 192, 128, seed=11)
+    a = torch.tensor([1.0, 0.7, 0.4, 0.15, 0.0, 0.0, 0.0, 0.0], device=y.device).view(1, 8, 1, 1)
+    y = (16 + (y.float() - 16) * a).round().clamp(0, 255).to(torch.uint8)
+    u = (128 + (u.float() - 128) * a).round().clamp(0, 255).to(torch.uint8)
+    v = (128 + (v.float() - 128) * a).round().clamp(0, 255).to(torch.uint8)
+    enc = GpuHevcEncoder(HevcParams(width=192, height=128, crf=27.0, bframes=0, weightp=True, wp_min_scale=0.05),
+                         slots=2)
+    res = enc.encode(y, u, v, keep_recon=True)
+    rec = enc.last_recon
+    assert enc.stats.get("weightp_pictures", 0) > 0
+    _compare(host, res, rec)
+    enc.close()
+
+
 def _cut_clip(B, F, w, h, cut, seed):
     """synth_clip frames, then from frame ``cut`` a new scene: uniform noise panning by whole
     pixels -- the old scene predicts none of it (the cut frame's inter cost is ~intra, a cut

@@ -127,3 +127,35 @@ def test_pyramid_stream_decodes_with_modified_lists(host, seed):
             other = np.asarray(q["y_coded"]).reshape(h, w)[my * 16:(my + 1) * 16, mx * 16:(mx + 1) * 16]
             if d == want:
                 assert np.array_equal(blk, other), (mb, want)
+
+
+def test_pyramid_with_one_reference_keeps_both_anchors(host):
+    """--ref 1 (veryfast / superfast presets) with a pyramid: the DPB must hold I0, P4 and the
+    reference B2 at once, and P4 must survive the store of B6 while B2 is still in the window
+    (round-4 review: a window of refs + 1 = 2 evicted I0 when B2 was stored, leaving B1
+    without a list 0)."""
+    assert dpb_frames(1, True, 3) == 4 and dpb_frames(1, False, 3) == 2 and dpb_frames(3, True, 3) == 4
+    plan = h264_plan("IBBBPBBBP", refs=1, pyramid=True)
+    by_d = {p.d: p for p in plan}
+    assert by_d[1].refs0 == (0,) and by_d[1].refs1 == (2,)
+    assert by_d[3].refs0 == (2,) and by_d[3].refs1 == (4,)
+    assert by_d[5].refs0 == (4,) and by_d[7].refs1 == (8,)
+    # the SPS max_num_ref_frames agrees (the decoder's sliding window is what the plan simulates)
+    rng = np.random.default_rng(5)
+    w, h = 48, 32
+    wmb = w // 16
+    nmb = wmb * (h // 16)
+    cfg = dict(width=w, height=h, qp=28, cabac=1, bframes=3, refs=1, pyramid=1, deblock=0, weighted_bipred=0)
+    out = [host.parameter_sets(cfg)]
+    for p in plan:
+        hdr, coef = _pic_records(rng, nmb, wmb, p.kind, 28)
+        fp = dict(idr=int(p.kind == "I"), qp=28, frame_num=p.frame_num, poc=p.poc, slice_type=p.slice_type,
+                  nal_ref_idc=p.nal_ref_idc, direct_spatial=1)
+        if p.kind != "I":
+            fp["num_ref_l0"] = len(p.refs0)
+            fp["num_ref_l1"] = 1
+            if p.mod_l0:
+                fp["mod_l0"] = list(p.mod_l0)
+        out.append(host.write_slice(cfg, fp, hdr, coef)[0])
+    pics = host.decode(b"".join(out))
+    assert [q["poc"] // 2 for q in pics] == list(range(9))

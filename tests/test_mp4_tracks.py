@@ -82,6 +82,30 @@ def test_audio_priming_edit_survives_cut_and_concat():
     assert rt.media_time == 1024 and rt.samples == a.samples
 
 
+def test_late_audio_with_priming_keeps_both_edits():
+    """Audio that starts 0.4 s after the video AND hides one AAC priming frame: the empty
+    edit (delay) and the media edit (media_time 1024) are both kept through write / read,
+    cut and concat with the pieces' start times (round-4 review: the concat dropped the
+    positive media_time, so the priming frame played and the audio landed 1024 samples
+    early)."""
+    a = _audio_track(1.5, seed=13)
+    a.media_time, a.delay = 1024, int(0.4 * a.timescale)
+    t_first = a.pts_seconds()[1]          # the first presented frame: 0.4 s
+    assert abs(t_first - 0.4) < 1e-9
+    rt = mp4.read(mp4.write([a]))[0]
+    assert rt.media_time == 1024 and abs(rt.delay - a.delay) <= 1 and rt.samples == a.samples
+    bounds = [0.0, 0.25, 0.75, None]
+    parts = [mp4.cut(a, bounds[i], bounds[i + 1]) for i in range(3)]
+    assert not parts[0].samples
+    assert parts[1].media_time == 1024 and parts[1].samples[0] == a.samples[0]
+    assert abs(parts[1].pts_seconds()[1] - (0.4 - 0.25)) < 1e-3
+    back = mp4.concat(parts, starts=[0.0, 0.25, 0.75])
+    assert back.samples == a.samples and back.media_time == 1024
+    assert abs(back.pts_seconds()[1] - 0.4) < 1e-3
+    rt = mp4.read(mp4.write([back]))[0]
+    assert rt.media_time == 1024 and abs(rt.pts_seconds()[1] - 0.4) < 1e-3
+
+
 def test_split_worker_merge_keeps_audio(tmp_path, host):
     """server s (mp4 with audio) -> every piece carries its audio span -> worker transcode
     with -acodec copy -> merge: the output audio == the input audio, sample for sample."""
