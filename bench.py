@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import argparse
 import concurrent.futures as cf
+import dataclasses
 import json
 import os
 import sys
@@ -33,6 +34,12 @@ if not os.environ.get("GPU_MAX_HW_QUEUES", "").isdigit() or int(os.environ["GPU_
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+
+
+def _knob_env() -> bool:
+    """--allow-knobs, read before argparse so the MIVC_BENCH_* shape defaults below only apply
+    with it (models/knobs.py)."""
+    return "--allow-knobs" in sys.argv
 
 
 def _memory(env, merged) -> dict:
@@ -57,14 +64,16 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--slots", type=int, default=int(os.environ.get("MIVC_BENCH_SLOTS", "256")),
+    knobs = _knob_env()
+    env_ = os.environ if knobs else {}
+    ap.add_argument("--slots", type=int, default=int(env_.get("MIVC_BENCH_SLOTS", "256")),
                     help="segments encoded concurrently per GPU")
-    ap.add_argument("--frames", type=int, default=int(os.environ.get("MIVC_BENCH_FRAMES", "60")),
+    ap.add_argument("--frames", type=int, default=int(env_.get("MIVC_BENCH_FRAMES", "60")),
                     help="frames per segment (GOP length)")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--crf", type=float, default=23.0)
-    ap.add_argument("--bframes", type=int, default=int(os.environ.get("MIVC_BENCH_BFRAMES", "3")),
+    ap.add_argument("--bframes", type=int, default=int(env_.get("MIVC_BENCH_BFRAMES", "3")),
                     help="B pictures between anchors (x264 default 3)")
     ap.add_argument("--cavlc", action="store_true",
                     help="Constrained Baseline CAVLC (the round-1 encoder) instead of Main CABAC")
@@ -77,7 +86,12 @@ def main() -> None:
                     help="rank 0 writes the last timed step's merged Annex-B stream here")
     ap.add_argument("--no-quality", dest="quality", action="store_false",
                     help="skip the PSNR/SSIM measurement of the first warmup step")
+    ap.add_argument("--allow-knobs", action="store_true",
+                    help="apply MIVC_* encoder / bench knobs from the environment (refused otherwise); "
+                         "every applied value is reported under config.env")
     a = ap.parse_args()
+    from govideocompressor_amd.models import knobs as K
+    env_knobs = K.check_environment(a.allow_knobs)
 
     import torch
 
@@ -90,8 +104,9 @@ def main() -> None:
     if env.world != a.gpus:
         if env.is_main:
             print(f"warning: --gpus {a.gpus} but WORLD_SIZE {env.world}", file=sys.stderr)
-    p = H264Params(width=a.width, height=a.height, fps=30.0, crf=a.crf, bframes=a.bframes, cabac=not a.cavlc,
-                   t8x8=a.t8x8, partitions=a.partitions)
+    overrides = K.encoder_overrides(H264Params) if a.allow_knobs else {}
+    p = H264Params(**{**dict(width=a.width, height=a.height, fps=30.0, crf=a.crf, bframes=a.bframes, cabac=not a.cavlc,
+                             t8x8=a.t8x8, partitions=a.partitions), **overrides})
     enc = GpuH264Encoder(p, slots=a.slots, device=env.device,
                          entropy_threads=int(os.environ.get("MIVC_ENTROPY_THREADS", "16")))
     B, F = a.slots, a.frames
@@ -220,6 +235,13 @@ def main() -> None:
                 "seq_len": F,
                 "segments_per_gpu": B,
                 "parallelism": f"dp{env.world} (segment-parallel)",
+                # every effective encoder setting (H264Params), environment knobs included
+                "encoder": dataclasses.asdict(p),
+                "slices_per_picture": p.eff_slices(),
+                "env": {"allow_knobs": a.allow_knobs, "encoder_overrides": overrides, **{
+                    k: v for k, v in env_knobs.items() if k != "unknown" and v}},
+                "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+                "entropy_threads": enc.entropy_threads,
             },
             "quality": {"psnr_y_db": round(psnr, 3), "ssim_y": round(ssim, 4), "bitrate_kbps": round(kbps, 1),
                         "measured_on": "first warmup step (untimed)" if q else "n/a (no warmup step)",

@@ -149,8 +149,8 @@ def config3(args) -> list[dict]:
         # untimed: the input pieces (closed GOPs of F frames) made by this framework's
         # encoders; piece i's content depends on i only, not on the split over ranks
         pieces = []
-        mk = (GpuHevcEncoder(HevcParams(width=W, height=H, crf=22.0), slots=B, device=env.device) if codec == "hevc"
-              else GpuH264Encoder(H264Params(width=W, height=H, crf=20), slots=B, device=env.device))
+        mk = (GpuHevcEncoder(_params(HevcParams, width=W, height=H, crf=22.0), slots=B, device=env.device) if codec == "hevc"
+              else GpuH264Encoder(_params(H264Params, width=W, height=H, crf=20), slots=B, device=env.device))
         for b0 in range(lo, hi, B):
             y, u, v = synth_clip(B, F, W, H, seed=3, slot0=b0, device=env.device)
             pieces += [r.bitstream for r in mk.encode(y, u, v, metrics=False)][:hi - b0]
@@ -158,7 +158,7 @@ def config3(args) -> list[dict]:
         mk.close()
         del mk
         torch.cuda.empty_cache()
-        tc = GpuTranscoder(H264Params(width=W, height=H, crf=23.0), slots=B, device=env.device)
+        tc = GpuTranscoder(_params(H264Params, width=W, height=H, crf=23.0), slots=B, device=env.device)
         if args.warmup:
             tc.run(pieces[:B], 30.0)  # warmup batch
         merger = D.SegmentMerge(env)
@@ -222,7 +222,7 @@ def _hevc_run(args, W, H, B, F, bd, crf, two_pass_kbps=None, fps=30.0, resident=
     from govideocompressor_amd.rc import GlobalStats, TwoPassFeedback, abr_solve
 
     env = D.init(prefer_gpu=True)
-    enc = GpuHevcEncoder(HevcParams(width=W, height=H, fps=fps, crf=crf, bit_depth=bd), slots=B, device=env.device)
+    enc = GpuHevcEncoder(_params(HevcParams, width=W, height=H, fps=fps, crf=crf, bit_depth=bd), slots=B, device=env.device)
 
     held = None
     if resident:
@@ -310,6 +310,16 @@ def config5(args) -> list[dict]:
              **d}]
 
 
+_ALLOW_KNOBS = False
+
+
+def _params(cls, **kw):
+    """Encoder parameters of a config: its own settings, plus the MIVC_* encoder knobs of the
+    environment when --allow-knobs was given (models/knobs.py)."""
+    from govideocompressor_amd.models import knobs as K
+    return cls(**{**kw, **(K.encoder_overrides(cls) if _ALLOW_KNOBS else {})})
+
+
 def config_na(n: int, what: str) -> list[dict]:
     return [{"config": n, "value": None, "note": f"not implemented in this build: {what}"}]
 
@@ -337,7 +347,12 @@ def main():
     ap.add_argument("--frames5", type=int, default=60)
     ap.add_argument("--kbps5", type=float, default=80000.0)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--allow-knobs", action="store_true", help="apply MIVC_* encoder knobs (models/knobs.py)")
     a = ap.parse_args()
+    global _ALLOW_KNOBS
+    from govideocompressor_amd.models import knobs as K
+    K.check_environment(a.allow_knobs)
+    _ALLOW_KNOBS = a.allow_knobs
     todo = [1, 2, 3, 4, 5] if a.all else [a.config]
     for c in todo:
         if c == 1:

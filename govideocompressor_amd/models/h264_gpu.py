@@ -53,7 +53,7 @@ class H264Params:
     i4x4: bool = True
     # x264 --partitions i8x8 (its default with --8x8dct): Intra8x8 MBs (High profile) tried where
     # Intra4x4 is (I pictures, scene cuts), closed loop with the 8x8 transform, sa8d ranking
-    i8x8: bool = bool(int(os.environ.get("MIVC_I8X8", "1")))
+    i8x8: bool = True
     # Intra4x4 trial for the (rare) intra MBs of P frames.  Off by default: a P-frame
     # intra MB is coded by the wavefront kernel, whose latency (x chain length) is
     # dominated by the 16 serial I4x4 block trials; these MBs are ~0.1-1% of a P frame.
@@ -66,7 +66,7 @@ class H264Params:
     # lowres search range around the quarter-resolution seed (rc/lookahead.py RANGES): +-4 and
     # +-6 are BD-rate-identical on the content suite (-0.01 %, profiles/r4_la_range_rd.json),
     # +-4 searches 81 positions instead of 169
-    la_range: int = int(os.environ.get("MIVC_LA_RANGE", 4))
+    la_range: int = 4
     # x264 --scenecut: a P frame whose lowres inter cost saves less than this percent of
     # its intra cost is coded all-intra (I4x4/I16x16 MBs) at the I-frame QP; 0 disables
     scenecut: int = 40
@@ -89,20 +89,20 @@ class H264Params:
     # costs (integer-pel, no lowres weighting) places too few B pictures for this encoder,
     # whose B pictures are cheap -- +10 % BD-rate against the fixed pattern (+6 % at
     # --b-bias 40), a gain on fast pans only -- so the fixed pattern is the default
-    b_adapt: int = int(os.environ.get("MIVC_B_ADAPT", 0))
+    b_adapt: int = 0
     # x264 --b-bias: > 0 places more B pictures (B costs * 100 / (120 + bias), run thresholds)
-    b_bias: int = int(os.environ.get("MIVC_B_BIAS", 0))
+    b_bias: int = 0
     # x264 seeds its motion search from the lookahead's lowres motion: the P search and both B
     # searches get one more candidate, the picture's lowres vector x 2 scaled to its reference
     # distance (when the lookahead ran on the coded MB grid)
-    lowres_seed: bool = os.environ.get("MIVC_LA_SEED", "1") != "0"
+    lowres_seed: bool = True
     # integer search radius of the two B-picture searches (their predictors are the scaled
     # co-located vectors of temporal direct, so a small window suffices)
-    b_me_range: int = int(os.environ.get("MIVC_B_ME_RANGE", 4))
+    b_me_range: int = 4
     # Jacobi passes of the P_Skip-aware vector choice after ME (csrc/kernels/bframe.hip
     # p_mv_refine): 0 disables.  Each pass settles the field one MB further: 2 -> 4 passes is
     # -2.55 % BD-rate on the content suite for -1.3 % headline fps (profiles/r4_knob_sweep.md)
-    skip_refine: int = int(os.environ.get("MIVC_SKIP_REFINE", 4))
+    skip_refine: int = 4
     # x264 --8x8dct (default on): High profile, the 8x8 transform chosen per inter MB where
     # its sa8d beats the 4x4 satd; CABAC only (the CAVLC path stays Constrained Baseline)
     t8x8: bool = True
@@ -116,42 +116,42 @@ class H264Params:
     partitions: bool = True
     # x264 --partitions b8x8: B macroblocks split into quadrants that pick their own candidate
     # (direct, L0, L1, bi of the MB's two searched vectors): B_16x8 / B_8x16 / B_8x8
-    bpartitions: bool = bool(int(os.environ.get("MIVC_BPARTS", "1")))
+    bpartitions: bool = True
     # (1080p CRF23 sweep, profiles/r2_partition_sweep.txt: 8 / 2000 -> -0.5% bits at equal
     # PSNR for ~1% of the step time; a threshold of 0 searches every MB for the same bits)
-    part_overhead: int = int(os.environ.get("MIVC_PART_OVERHEAD", 8))
-    part_min_satd: int = int(os.environ.get("MIVC_PART_MIN_SATD", 2000))
+    part_overhead: int = 8
+    part_min_satd: int = 2000
     # x264-style ME early termination: a search whose best candidate (the predictors and
     # their neighbours) already has SAD <= this skips the window and the integer search
     # (B pictures: the temporal-direct predictor); 0 disables
-    p_early_sad: int = int(os.environ.get("MIVC_P_EARLY_SAD", 0))
-    b_early_sad: int = int(os.environ.get("MIVC_B_EARLY_SAD", 1024))
+    p_early_sad: int = 0
+    b_early_sad: int = 1024
     # B macroblocks whose temporal-direct cost (SATD + lambda, a b_decide pre-pass) is <= b_gate
     # (< 0: -b_gate lambdas) skip both list searches and take direct (x264's early B_Skip /
     # direct termination); 0 disables.  1080p RD sweep (profiles/r3_b_gate_rd.md): 2400 ->
     # -8.8 % BD-rate (PSNR-Y) and +7..20 % fps against no gate
-    b_gate: int = int(os.environ.get("MIVC_B_GATE", 2400))
+    b_gate: int = 2400
     # x264 --trellis 1 (default): rate-distortion choice of the levels of inter MBs
     # (encode_inter.hip trellis_lite4x4 / trellis_lite8_chunk); 1 = the 4x4 luma blocks only,
     # 2 = also the 8x8 luma and the chroma AC blocks; trellis_lambda scales its SSD lambda
-    trellis: int = int(os.environ.get("MIVC_TRELLIS", 2))
+    trellis: int = 2
     # x264 --direct: "temporal" (co-located motion scaled by POC distances: every MB decides in
     # parallel) or "spatial" (the neighbours' motion: b_decide keeps each searched MB's best
     # explicit candidate, then bframe.hip b_spatial_decide derives the exact spatial motion in
     # an MB wavefront and takes direct where its SATD + lambda is not dearer; RD in
     # profiles/r3_direct_rd.md)
-    direct: str = os.environ.get("MIVC_DIRECT", "temporal")
+    direct: str = "temporal"
     # spatial direct: direct is taken when its cost <= the explicit candidate's + direct_bias * lambda
-    direct_bias: int = int(os.environ.get("MIVC_DIRECT_BIAS", 8))
+    direct_bias: int = 8
     # spatial direct: the B gate skips the searches of MBs with static co-located motion only
     # (wavefront decision) / of MBs whose estimated spatial direct cost passes b_gate (fast path)
-    spatial_gate: bool = os.environ.get("MIVC_SPATIAL_GATE", "1") != "0"
+    spatial_gate: bool = True
     # spatial direct decision: False (fast, default) = priced in parallel from an estimate of the
     # neighbours' motion, then made exact by an integer-only decoding-order pass
     # (b_spatial_exact) and re-predicted where the estimate was off (b_spatial_fixup); True =
     # the exact derivation priced MB by MB inside the wavefront (b_spatial_decide, ~3.7 ms per
     # picture of serial chain)
-    spatial_wavefront: bool = os.environ.get("MIVC_SPATIAL_WAVEFRONT", "0") != "0"
+    spatial_wavefront: bool = False
     # fast path: a direct quadrant whose exact motion lies further than this many quarter
     # samples from the priced estimate keeps the estimate as explicit motion (B_L0 / L1 / Bi
     # partitions, explicit 8x8 sub-blocks: the priced prediction, plus mvd bits) instead of being
@@ -160,15 +160,15 @@ class H264Params:
     # The exact direct field follows the *sequential* decisions (the first MBs of a picture
     # derive zero motion and spread it unless they are coded explicitly), which no parallel
     # estimate reproduces -- temporal direct stays the default
-    spatial_fix_tol: int = int(os.environ.get("MIVC_SPATIAL_FIX_TOL", 4))
+    spatial_fix_tol: int = 4
     # temporal direct: B_Direct_16x16 preferred by tdirect_bias * lambda in b_decide's choice
     # (-0.36 % BD-rate at 8, profiles/r3_direct_rd.md)
-    tdirect_bias: int = int(os.environ.get("MIVC_TDIRECT_BIAS", 8))
+    tdirect_bias: int = 8
     # x264 --b-pyramid normal: in a run of two or more B pictures the middle one is a reference
     # picture (coded first, predicted from the two anchors, then a reference of the others and of
     # the next P); needs spatial direct (temporal direct's co-located motion would come from a B)
-    pyramid: bool = os.environ.get("MIVC_PYRAMID", "0") != "0"
-    trellis_lambda: float = float(os.environ.get("MIVC_TRELLIS_LAMBDA", 1.0))
+    pyramid: bool = False
+    trellis_lambda: float = 1.0
     # deblock non-reference B pictures even when neither metrics nor the reconstruction
     # are requested (x264 --full-recon); the bitstream does not depend on it
     full_recon: bool = False
@@ -179,7 +179,7 @@ class H264Params:
     # vector, radius ref_range); B pictures' temporal direct follows the co-located block's
     # reference.  CABAC only (the Baseline CAVLC path keeps one reference).  ref_gate: MBs
     # whose list-0[0] cost (SATD + lambda * bits) is <= ref_gate are not searched in the farther pictures
-    refs: int = int(os.environ.get("MIVC_REFS", 3))
+    refs: int = 3
     # x264 --weightp (default 2 outside Baseline): explicit weighted prediction of a P picture's
     # RefPicList0[0] (luma and chroma weight / offset, denominator 2^6) where the source
     # statistics say the brightness or contrast changed (fades, flashes): the weights come from
@@ -188,9 +188,9 @@ class H264Params:
     weightp: bool = True
     wp_min_mean: float = 2.0
     wp_min_scale: float = 0.08
-    ref_range: int = int(os.environ.get("MIVC_REF_RANGE", 4))
+    ref_range: int = 4
     # content suite (profiles/r4_knob_sweep.md): 3000 is -0.67 % BD-rate and +1.5 % fps vs 1500
-    ref_gate: int = int(os.environ.get("MIVC_REF_GATE", 3000))
+    ref_gate: int = 3000
     # slices per picture (x264 --slices): whole MB rows each.  The GPU arithmetic coder codes
     # one slice per lane, so S slices give S times the independent serial chains per picture
     # (and the intra wavefront restarts at every slice); each slice costs a header and the
@@ -199,7 +199,7 @@ class H264Params:
     # a 4K picture in one slice is a 4x longer serial chain for the arithmetic coder at a
     # quarter of the slots per batch (4K encode-only, 64 x 30 frames: 1105 fps with 1 slice,
     # 1693 with 4, 1742 with 8; at 1080p 4 slices cost +2.3 % BD-rate for +2 % fps)
-    slices: int = int(os.environ.get("MIVC_SLICES", 0))
+    slices: int = 0
 
     def slice_count(self) -> int:
         hmb = (self.height + 15) // 16
@@ -514,6 +514,7 @@ class GpuH264Encoder:
         self.copy_done = [torch.cuda.Event() for _ in range(2)]
         self.compute_done = [torch.cuda.Event() for _ in range(2)]
         nthreads = entropy_threads or min(16, max(2, (os.cpu_count() or 4)))
+        self.entropy_threads = nthreads
         self.pool = cf.ThreadPoolExecutor(max_workers=nthreads)
         self.cfg = params.host_cfg()
         self.timings: dict[str, float] = {}

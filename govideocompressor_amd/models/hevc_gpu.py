@@ -112,7 +112,7 @@ class HevcParams:
     # x265 --ctu 64 (its default): 64x64 coding tree units over the 32x32 record blocks (the
     # blocks are the CTU's quantization groups and are reconstructed in z-order; one SAO
     # parameter set per CTU; 64x64 skip CUs where four blocks agree) -- False: 32x32 CTBs
-    ctu64: bool = bool(int(os.environ.get("MIVC_HEVC_CTU64", "1")))
+    ctu64: bool = True
     # x265 --weightp (its default): explicit weights of a P picture's reference where the
     # source statistics say the brightness or contrast changed (fades, flashes): weight =
     # sqrt(var_cur / var_ref) over 2^6, offset = mean_cur - weight * mean_ref, per component,

@@ -1,4 +1,5 @@
 """H264Params / GpuH264Encoder host-side rules that need no GPU."""
+import pytest
 from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params
 
 
@@ -75,3 +76,34 @@ def test_pending_encode_redoes_a_pool_overflow(monkeypatch):
     p = PendingEncode(enc, boom, ("y",), {})
     with pytest.raises(RuntimeError, match="coder error"):
         p.result()
+
+
+def test_env_knobs_are_explicit(monkeypatch):
+    """MIVC_* encoder knobs no longer change H264Params defaults behind the caller's back:
+    they apply only through models/knobs.py encoder_overrides (bench.py --allow-knobs), and
+    check_environment refuses unknown names and unrequested encoder knobs (round-4 review)."""
+    import dataclasses
+
+    from govideocompressor_amd.models import knobs as K
+    from govideocompressor_amd.models.h264_gpu import H264Params
+    from govideocompressor_amd.models.hevc_gpu import HevcParams
+    monkeypatch.setenv("MIVC_TRELLIS", "1")
+    monkeypatch.setenv("MIVC_DIRECT", "spatial")
+    monkeypatch.setenv("MIVC_LA_SEED", "0")
+    monkeypatch.setenv("MIVC_TRELLIS_LAMBDA", "0.75")
+    monkeypatch.setenv("MIVC_ENTROPY_THREADS", "4")
+    p = H264Params(width=64, height=64)
+    assert p.trellis == 2 and p.direct == "temporal" and p.lowres_seed
+    assert K.encoder_overrides(H264Params) == dict(trellis=1, direct="spatial", lowres_seed=False, trellis_lambda=0.75)
+    assert K.encoder_overrides(HevcParams) == {}
+    with pytest.raises(SystemExit, match="allow-knobs"):
+        K.check_environment(False)
+    s = K.check_environment(True)
+    assert s["runtime"] == {"MIVC_ENTROPY_THREADS": "4"} and "MIVC_TRELLIS" in s["encoder"]
+    monkeypatch.setenv("MIVC_TRELIS", "1")  # typo
+    with pytest.raises(SystemExit, match="unknown"):
+        K.check_environment(True)
+    # every knob names a real field
+    for table, cls in ((K.H264, H264Params), (K.HEVC, HevcParams)):
+        names = {f.name for f in dataclasses.fields(cls)}
+        assert set(table.values()) <= names

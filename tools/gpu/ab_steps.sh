@@ -9,7 +9,7 @@ mkdir -p "$out"
 for r in $(seq 1 "$rounds"); do
   for spec in "$@"; do
     label=${spec%%=*}; envs=${spec#*=}
-    env $envs timeout -k 10 240 python bench.py --steps "$steps" --warmup 2 --no-quality $AB_ARGS > "$out/$label.r$r.log" 2>&1
+    env $envs timeout -k 10 240 python bench.py --allow-knobs --steps "$steps" --warmup 2 --no-quality $AB_ARGS > "$out/$label.r$r.log" 2>&1
     rc=$?
     echo "$label round $r rc=$rc $(grep -h '"metric"' "$out/$label.r$r.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])' 2>/dev/null)" | tee -a "$out/ab.txt"
     case $rc in 0) ;; *) exit $rc ;; esac

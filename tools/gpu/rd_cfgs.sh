@@ -8,7 +8,7 @@ mkdir -p $out
 for spec in "$@"; do
   name=${spec%%|*}; envs=${spec#*|}
   for crf in $crfs; do
-    env $envs timeout -k 10 200 python bench.py --steps 1 --warmup 1 --slots 64 --crf $crf > $out/${name}_${crf}.log 2>&1 || exit 1
+    env $envs timeout -k 10 200 python bench.py --allow-knobs --steps 1 --warmup 1 --slots 64 --crf $crf > $out/${name}_${crf}.log 2>&1 || exit 1
     echo "$name $crf $(tail -1 $out/${name}_${crf}.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); q=d["quality"]; print(q["bitrate_kbps"], q["psnr_y_db"], d["value"])')" >> $out/summary.txt
   done
 done
