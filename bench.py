@@ -21,6 +21,7 @@ from __future__ import annotations
 import argparse
 import concurrent.futures as cf
 import dataclasses
+import hashlib
 import json
 import os
 import sys
@@ -245,7 +246,11 @@ def main() -> None:
             },
             "quality": {"psnr_y_db": round(psnr, 3), "ssim_y": round(ssim, 4), "bitrate_kbps": round(kbps, 1),
                         "measured_on": "first warmup step (untimed)" if q else "n/a (no warmup step)",
-                        "merged_bytes": len(merged) if merged is not None else 0},
+                        "merged_bytes": len(merged) if merged is not None else 0,
+                        # identity of the last timed step's merged stream (same seed: byte-identity
+                        # check of kernel changes, tools/gpu/ab_steps.sh)
+                        "merged_sha256_16": hashlib.sha256(memoryview(merged)).hexdigest()[:16]
+                        if merged is not None else None},
             "timings_rank0_s": {k: round(v, 3) for k, v in enc.timings.items()},
             # interval between consecutive timed steps' completion on rank 0 (the first includes
             # the first input's synthesis and lookahead; the last is not shortened by the merge)

@@ -146,6 +146,7 @@ void mivc_launch_cavlc(int B, int wmb, int hmb, const void* hdr, const int16_t* 
                        long long* off, int* trail, long long* total_bits, int* slot_bytes, uint32_t* words,
                        long long cap_words, const uint32_t* hdr_bits, const int* hdr_nbits, int pslice, int slice_qp,
                        const int* slot_qp, uint8_t* out, long long* out_off, const uint8_t* nz, void* stream);
+void mivc_launch_satd_blocks(const uint8_t* src, const uint8_t* pred, int* out, int n, int mode, void* stream);
 void mivc_launch_sse(int B, int W, int H, int w, int h, const uint8_t* sy, const uint8_t* su, const uint8_t* sv,
                      const uint8_t* ry, const uint8_t* ru, const uint8_t* rv, unsigned long long* sse,
                      float* ssim_sum, void* stream, const void* route, int nbuf);
@@ -677,6 +678,10 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("B"), py::arg("W"), py::arg("H"), py::arg("w"), py::arg("h"), py::arg("sy"), py::arg("su"), py::arg("sv"),
      py::arg("ry"), py::arg("ru"), py::arg("rv"), py::arg("sse"), py::arg("ssim"), py::arg("stream"),
      py::arg("route") = 0, py::arg("nbuf") = 0);
+  m.def("satd_blocks", [](uintptr_t src, uintptr_t pred, uintptr_t out, int n, int mode, uintptr_t stream) {
+    if (n <= 0) throw std::invalid_argument("satd_blocks: n must be positive");
+    mivc_launch_satd_blocks(P<uint8_t>(src), P<uint8_t>(pred), P<int>(out), n, mode, S(stream));
+  });
   m.def("lookahead_low_bytes", [](int w, int h, int n) { return mivc_lookahead_low_bytes(w, h, n); });
   m.def("lookahead_quarter_bytes", [](int w, int h, int n) { return mivc_lookahead_quarter_bytes(w, h, n); });
   m.def("lookahead_multi", [](uintptr_t low, int w, int h, int n, int f, uintptr_t blk_cost, uintptr_t blk_mv, int D,

@@ -235,7 +235,10 @@ __device__ __forceinline__ uint32_t ld4(const uint8_t* row, int x) {
 // code the luma 4x4 blocks (blkIdx order), 16-23 the chroma 4x4 blocks, 24-31 records.
 // Rows move as dwords (prediction, source, reference, reconstruction), levels as
 // 16-byte stores, and the decimation score is branch-free.
-__global__ __launch_bounds__(64) void encode_inter_mb(InterArgs a) {
+// 4 waves per SIMD (128 VGPRs, a 16-byte spill) instead of the compiler's 3 at 140: inter
+// 316 -> 274 ms per headline step, bytes unchanged (profiles/r5_occupancy_ab.md); at 5 waves
+// the 132-byte spill made it slower (380 ms)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void encode_inter_mb(InterArgs a) {
   const Geom& g = a.g;
   const int lane = threadIdx.x, half = lane >> 5, hl = lane & 31;
   const int nmb = g.nmb();

@@ -54,6 +54,49 @@ __device__ __forceinline__ int satd16(int* r) {
   return h264::satd4x4(r);
 }
 
+// 4x4 SATD of packed 8-bit rows (s: source, p: prediction, 4 samples per dword) on packed
+// 16-bit lanes: equal to satd16 of the residual, with about half the VALU work.
+//   * bytes 0/2 and 1/3 of each row go to the two 16-bit halves of two registers (v_perm),
+//     so one v_pk_sub_i16 forms two residuals and the vertical Hadamard is 16 packed ops;
+//   * the horizontal pass needs e = c0 + c1, f = c0 - c1 per half (columns (0, 1) / (2, 3)),
+//     and |a + b| + |a - b| = 2 max(|a|, |b|) replaces the last butterfly stage: the SATD
+//     (sum / 2) is the sum of max(|e.lo|, |e.hi|) + max(|f.lo|, |f.hi|), formed by one
+//     v_perm pairing the halves, a v_pk_max_i16 and a v_dot2 accumulate.
+// Ranges: residuals +-255, after the vertical pass +-1020, e / f +-2040: int16 throughout.
+typedef short v2i16 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ v2i16 as_v2i16(uint32_t x) { return __builtin_bit_cast(v2i16, x); }
+__device__ __forceinline__ uint32_t as_u32(v2i16 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ int satd4x4_u8(const uint32_t (&s)[4], const uint32_t (&p)[4]) {
+  v2i16 lo[4], hi[4];  // row y: (x0, x2) and (x1, x3) residuals
+#pragma unroll
+  for (int y = 0; y < 4; ++y) {
+    // v_perm_b32 selector bytes: 0x0c = zero; byte 0/2 -> halves of lo, 1/3 -> halves of hi
+    const uint32_t s02 = __builtin_amdgcn_perm(0u, s[y], 0x0c020c00u), s13 = __builtin_amdgcn_perm(0u, s[y], 0x0c030c01u);
+    const uint32_t p02 = __builtin_amdgcn_perm(0u, p[y], 0x0c020c00u), p13 = __builtin_amdgcn_perm(0u, p[y], 0x0c030c01u);
+    lo[y] = as_v2i16(s02) - as_v2i16(p02);
+    hi[y] = as_v2i16(s13) - as_v2i16(p13);
+  }
+  // vertical 4-point Hadamard on both register sets
+  const v2i16 a0 = lo[0] + lo[1], a1 = lo[0] - lo[1], a2 = lo[2] + lo[3], a3 = lo[2] - lo[3];
+  const v2i16 b0 = hi[0] + hi[1], b1 = hi[0] - hi[1], b2 = hi[2] + hi[3], b3 = hi[2] - hi[3];
+  const v2i16 vl[4] = {a0 + a2, a0 - a2, a1 + a3, a1 - a3};
+  const v2i16 vh[4] = {b0 + b2, b0 - b2, b1 + b3, b1 - b3};
+  int acc = 0;
+  const v2i16 one = {1, 1};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v2i16 e = vl[k] + vh[k], f = vl[k] - vh[k];  // (c0 + c1, c2 + c3), (c0 - c1, c2 - c3)
+    e = __builtin_elementwise_max(e, -e);
+    f = __builtin_elementwise_max(f, -f);
+    // (|e.lo|, |f.lo|) vs (|e.hi|, |f.hi|)
+    const uint32_t ue = as_u32(e), uf = as_u32(f);
+    const v2i16 m = __builtin_elementwise_max(as_v2i16(__builtin_amdgcn_perm(uf, ue, 0x05040100u)),
+                                              as_v2i16(__builtin_amdgcn_perm(uf, ue, 0x07060302u)));
+    acc = __builtin_amdgcn_sdot2(m, one, acc, false);
+  }
+  return acc;
+}
+
 // ---------------------------------------------------------------- in-workgroup wavefront
 // The serial stages (intra coding, deblocking) run one workgroup per frame with
 // kWaves waves; wave w owns MB rows w, w + kWaves, ...  Row progress lives in LDS

@@ -322,8 +322,10 @@ __device__ unsigned long long g_me_prof[64][12];
 #define MPROF(ph) do {} while (0)
 #endif
 
+// 8 waves per SIMD (64 VGPRs + a 20-byte spill; the compiler chose 5 at 65 VGPRs + 20 AGPRs):
+// me_p 180 -> 170 and me_b 265 -> 248 ms per headline step (profiles/r5_occupancy_ab.md)
 template <int MAXR>
-__global__ __launch_bounds__(64) void me_p16x16(MeArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void me_p16x16(MeArgs a) {
   const Geom& g = a.g;
   // XCD-aware remap: hardware deals workgroups round-robin over the 8 XCDs; give each XCD
   // a contiguous range of (slot, MB) so neighbouring windows share its L2.

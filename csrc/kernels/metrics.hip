@@ -91,10 +91,42 @@ __global__ void ssim8(const uint8_t* sy, const uint8_t* ry, int W, int H, int w,
   if ((threadIdx.x & 63) == 0) atomicAdd(ssim_sum + slot, s);
 }
 
+// Known-answer check of the SATD primitives the decision kernels use (tests/test_gpu_satd.py):
+// block i = 16 source and 16 prediction bytes (raster 4x4); mode 0 = satd16 on unpacked
+// residuals (the reference form), 1 = satd4x4_u8 (packed 16-bit), 2 = satd4x4_mfma (a wave
+// prices 16 blocks per MFMA; n a multiple of 64).
+__global__ __launch_bounds__(64) void satd_blocks(const uint8_t* src, const uint8_t* pred, int* out, int n, int mode) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  const int ic = i < n ? i : n - 1;
+  uint32_t a[4], b[4];
+#pragma unroll
+  for (int y = 0; y < 4; ++y) {
+    a[y] = reinterpret_cast<const uint32_t*>(src + static_cast<size_t>(ic) * 16)[y];
+    b[y] = reinterpret_cast<const uint32_t*>(pred + static_cast<size_t>(ic) * 16)[y];
+  }
+  int v;
+  if (mode == 0) {
+    int r[16];
+#pragma unroll
+    for (int y = 0; y < 4; ++y)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) r[y * 4 + x] = static_cast<int>((a[y] >> (8 * x)) & 255u) - static_cast<int>((b[y] >> (8 * x)) & 255u);
+    v = satd16(r);
+  } else {
+    v = satd4x4_u8(a, b);
+  }
+  if (i < n) out[i] = v;
+}
+
 }  // namespace gpu
 }  // namespace mivc
 
 using namespace mivc::gpu;
+
+extern "C" void mivc_launch_satd_blocks(const uint8_t* src, const uint8_t* pred, int* out, int n, int mode, void* stream) {
+  hipLaunchKernelGGL(satd_blocks, dim3((n + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), src, pred, out, n,
+                     mode);
+}
 
 extern "C" void mivc_launch_sse(int B, int W, int H, int w, int h, const uint8_t* sy, const uint8_t* su,
                                 const uint8_t* sv, const uint8_t* ry, const uint8_t* ru, const uint8_t* rv,

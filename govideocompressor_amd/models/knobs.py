@@ -58,7 +58,8 @@ HEVC = {
     "MIVC_HEVC_CTU64": "ctu64",
 }
 # bench.py shape knobs (they change what is measured, so they also need --allow-knobs)
-BENCH = {"MIVC_BENCH_SLOTS", "MIVC_BENCH_FRAMES", "MIVC_BENCH_BFRAMES"}
+# (MIVC_HIP_LIB: an alternative kernel library, tools/build_variant.py -- same-box A/B timing)
+BENCH = {"MIVC_BENCH_SLOTS", "MIVC_BENCH_FRAMES", "MIVC_BENCH_BFRAMES", "MIVC_HIP_LIB"}
 # never change the coded bytes (see the module docstring)
 RUNTIME = {
     "MIVC_ENTROPY_THREADS", "MIVC_PINNED_BUDGET_MB", "MIVC_CABAC_GROUP", "MIVC_CABAC_SYMS_PER_MB",

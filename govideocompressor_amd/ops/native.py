@@ -25,7 +25,9 @@ def _load(name: str, builder):
     with _lock:
         if name in _cache:
             return _cache[name]
-        override = os.environ.get("MIVC_HOST_LIB") if name == "_host" else None
+        # MIVC_HOST_LIB: e.g. the ASan/UBSan build; MIVC_HIP_LIB: a kernel variant for same-box A/B
+        # timing (tools/build_variant.py; bench.py --allow-knobs)
+        override = os.environ.get("MIVC_HOST_LIB" if name == "_host" else "MIVC_HIP_LIB")
         if override:  # e.g. the ASan/UBSan build (_build.build_host(sanitize=True))
             full = f"govideocompressor_amd.{name}"
             loader = importlib.machinery.ExtensionFileLoader(full, override)
