@@ -826,18 +826,17 @@ struct CabacMbCoder {
       if (cbf_inc >= 0) e.decision(CTX_CBF + kCbfCatOffset[cat] + cbf_inc, 0);
       return;
     }
-    int vals[64];
+    // levels are read in place (no local copy: on the GPU a 64-entry array lives in scratch
+    // memory -- 256 bytes per lane of cabac_bins / cabac_count)
     int last = -1;
-    for (int i = 0; i < n; ++i) {
-      vals[i] = c[i];
-      if (vals[i]) last = i;
-    }
+    for (int i = 0; i < n; ++i)
+      if (c[i]) last = i;
     if (cbf_inc >= 0) {
       e.decision(CTX_CBF + kCbfCatOffset[cat] + cbf_inc, last >= 0);
       if (last < 0) return;
     }
     for (int i = 0; i < n - 1; ++i) {
-      const int sig = vals[i] != 0;
+      const int sig = c[i] != 0;
       int sctx, lctx;
       if (cat == 5) {
         sctx = CTX_SIG8x8 + kSig8x8Frame[i];
@@ -857,7 +856,7 @@ struct CabacMbCoder {
     const int gmax = cat == 3 ? 3 : 4;
     int ngt1 = 0, neq1 = 0;
     for (int i = last; i >= 0; --i) {
-      const int val = vals[i];
+      const int val = c[i];
       if (!val) continue;
       const int a1 = (val < 0 ? -val : val) - 1;
       e.decision(abase + (ngt1 ? 0 : (neq1 + 1 < 4 ? neq1 + 1 : 4)), a1 > 0);

@@ -270,13 +270,7 @@ constexpr int kDecideMbsPerWave = 4;
 
 // 4x4 SATD of this lane's block against 4 packed prediction rows
 __device__ __forceinline__ int blk_satd4(const uint32_t (&src)[4], const uint32_t (&pw)[4]) {
-  int rr[16];
-#pragma unroll
-  for (int y = 0; y < 4; ++y)
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-      rr[y * 4 + x] = static_cast<int>((src[y] >> (8 * x)) & 255u) - static_cast<int>((pw[y] >> (8 * x)) & 255u);
-  return h264::satd4x4(rr);
+  return satd4x4_u8(src, pw);  // packed 16-bit (kcommon.h), = h264::satd4x4 of the residual
 }
 
 // The main pass of b_decide after the direct-only pre-pass, for a searched MB (the caller
@@ -469,8 +463,8 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   const int16_t* w1t = a.rt ? a.rt[slot].w1 : nullptr;
   auto w1of = [&](int rr) { return w1t ? static_cast<int>(w1t[rr & 3]) : a.w1[rr & 3]; };
   const int16_t* dm = a.dmv + o * 16;
-  const bool donly = K == 1 ? true : (K == 2 ? false : static_cast<bool>(a.direct_only));
-  const bool have_direct = K == 2 ? true : (K == 1 ? false : static_cast<bool>(a.have_direct));
+  const bool donly = (K == 1 || K == 3) ? true : (K == 2 ? false : static_cast<bool>(a.direct_only));
+  const bool have_direct = K == 2 ? true : ((K == 1 || K == 3) ? false : static_cast<bool>(a.have_direct));
   const bool sfast = a.spatial == 2;
   const int m0x = donly ? 0 : a.mv0[o * 2], m0y = donly ? 0 : a.mv0[o * 2 + 1];
   const int m1x = donly ? 0 : a.mv1[o * 2], m1y = donly ? 0 : a.mv1[o * 2 + 1];
@@ -487,8 +481,9 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
   int dref_[2][4], dvx[2][4], dvy[2][4];
   uint32_t drw = 0;  // refIdxL0 of the four temporal-direct quadrants (bytes)
   if (a.dref) drw = *reinterpret_cast<const uint32_t*>(a.dref + o * 4);
-  if (K == 2) {
-    // the lean main pass: nothing here (lane 0 re-reads the direct motion for the record)
+  if (K == 2 || K == 3) {
+    // the lean passes: nothing here (each lane reads its own quadrant's direct motion, lane 0
+    // re-reads it for the record)
   } else if (!sfast) {
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) {
@@ -571,6 +566,27 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
     b_decide_main(a, src, o, slot, mb, lane, wrow, q, X, Y, pout, hrec, drw, dm, G0, G1, H0, H1, w1of);
     return;
   }
+  if constexpr (K == 3) {
+    // the temporal-direct pre-pass: this lane's quadrant only
+    const int dr = (drw >> (8 * q)) & 255;
+    const int dvx0 = dm[q * 2], dvy0 = dm[q * 2 + 1], dvx1 = dm[8 + q * 2], dvy1 = dm[8 + q * 2 + 1];
+    const size_t sd = route_index(a.rt, a.nbuf, slot, RO_L0 + (dr & 3));
+    const uint8_t *GD = dr ? a.ref0k[dr] + (a.rt ? sd : slot) * g.ysize() : G0,
+                  *HD = dr ? a.hp0k[dr] + (a.rt ? sd : slot) * hps : H0;
+    const int w1 = w1of(dr);
+    uint32_t pd[4];
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      pd[y] = wavg4b(mc4(GD, HD, W, H, X, Y + y, dvx0, dvy0), mc4(G1, H1, W, H, X, Y + y, dvx1, dvy1), w1);
+      *reinterpret_cast<uint32_t*>(pout + 16 * y) = pd[y];
+    }
+    const int sat = sum16(satd4x4_u8(src, pd));
+    if (lane == 0) {
+      const int qp = clampi(a.qp[slot] + (a.aq ? a.aq[o] : 0), 0, 51);
+      a.cost_out[o] = sat + h264::kLambda[qp] * 1;
+    }
+    return;
+  }
   const int dr = dref_[0][q] < 0 ? 0 : dref_[0][q];  // this lane's quadrant
   const bool du0 = dref_[0][q] >= 0, du1 = dref_[1][q] >= 0;
   const size_t sd = route_index(a.rt, a.nbuf, slot, RO_L0 + (dr & 3));
@@ -595,13 +611,8 @@ __global__ __launch_bounds__(64) void b_decide(BDecideArgs a) {
     p1w[y] = searched ? *reinterpret_cast<const uint32_t*>(a.pred1 + o * 256 + (by4 + y) * 16 + bx4) : pd[y];
   }
   auto blk_satd = [&](const uint32_t* pw) {
-    int rr[16];
-#pragma unroll
-    for (int y = 0; y < 4; ++y)
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-        rr[y * 4 + x] = static_cast<int>((src[y] >> (8 * x)) & 255u) - static_cast<int>((pw[y] >> (8 * x)) & 255u);
-    return h264::satd4x4(rr);
+    const uint32_t w4[4] = {pw[0], pw[1], pw[2], pw[3]};
+    return satd4x4_u8(src, w4);
   };
   // per 8x8 quadrant and candidate: horizontal block pairs by DPP, then the two pair rows of
   // each quadrant from LDS (pair sums at lanes 8 * qy + 4 * {0, 1} + 2 * qx)
@@ -1293,17 +1304,13 @@ __global__ __launch_bounds__(64) void p_mv_refine(PRefineArgs a) {
   const size_t s0 = route_index(a.rt, a.nbuf, slot, RO_L0);
   const uint8_t* G0 = a.ref + s0 * g.ysize();
   const uint8_t* H0 = a.hp + s0 * hp_plane_bytes(W, H);
-  uint32_t ps[4];
-  int rr[16];
+  uint32_t ps[4], sw[4];
 #pragma unroll
   for (int y = 0; y < 4; ++y) {
-    const uint32_t src = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y + y) * W + X);
+    sw[y] = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y + y) * W + X);
     ps[y] = mc4(G0, H0, W, H, X, Y + y, sx, sy);
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      rr[y * 4 + k] = static_cast<int>((src >> (8 * k)) & 255u) - static_cast<int>((ps[y] >> (8 * k)) & 255u);
   }
-  const int satd = sum16(h264::satd4x4(rr));
+  const int satd = sum16(satd4x4_u8(sw, ps));
   const int qp = clampi(a.qp[slot] + (a.aq ? a.aq[o] : 0), 0, 51);
   const int lambda = h264::kLambda[qp];
   const int pmx = a.pm ? a.pm[o * 2] : 0, pmy = a.pm ? a.pm[o * 2 + 1] : 0;
@@ -1325,13 +1332,8 @@ __global__ __launch_bounds__(64) void p_mv_refine(PRefineArgs a) {
 // 16-lane-row form (four blocks per wave): this lane's 4x4 block = rows by4..by4+3 of src / pw,
 // summed over the row with DPP (every lane of a row holds the same block's total)
 __device__ __forceinline__ int satd16_rows(const uint32_t* src, const uint32_t* pw) {
-  int rr[16];
-#pragma unroll
-  for (int y = 0; y < 4; ++y)
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      rr[y * 4 + k] = static_cast<int>((src[y] >> (8 * k)) & 255u) - static_cast<int>((pw[y] >> (8 * k)) & 255u);
-  return sum16(h264::satd4x4(rr));
+  const uint32_t s4[4] = {src[0], src[1], src[2], src[3]}, p4[4] = {pw[0], pw[1], pw[2], pw[3]};
+  return sum16(satd4x4_u8(s4, p4));
 }
 
 // ---- HEVC merge-aware vector choice (the H.265 analogue of p_mv_refine): after the 16x16
@@ -1765,15 +1767,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
   for (int y = 0; y < 4; ++y) srow[y] = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y + y) * W + X);
   // SATD of this quadrant at vector (x, y), summed over its four blocks
   auto qsatd = [&](int x, int y) -> int {
-    int r[16];
+    uint32_t p4[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t p = mc4(G0, H0, W, H, X, Y + k, x, y);
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-        r[k * 4 + b] = static_cast<int>((srow[k] >> (8 * b)) & 255u) - static_cast<int>((p >> (8 * b)) & 255u);
-    }
-    int s = h264::satd4x4(r);
+    for (int k = 0; k < 4; ++k) p4[k] = mc4(G0, H0, W, H, X, Y + k, x, y);
+    int s = satd4x4_u8(srow, p4);
     s += __shfl_xor(s, 4, 64);
     s += __shfl_xor(s, 8, 64);
     return s;
@@ -1928,7 +1925,9 @@ extern "C" void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src
   a.cost_out = cost_out;
   const dim3 grid((wmb * hmb + kDecideMbsPerWave - 1) / kDecideMbsPerWave, B);
   const hipStream_t st = static_cast<hipStream_t>(stream);
-  if (direct_only)
+  if (direct_only && spatial == 0)
+    hipLaunchKernelGGL(b_decide<3>, grid, dim3(64), 0, st, a);
+  else if (direct_only)
     hipLaunchKernelGGL(b_decide<1>, grid, dim3(64), 0, st, a);
   else if (have_direct)
     hipLaunchKernelGGL(b_decide<2>, grid, dim3(64), 0, st, a);

@@ -289,7 +289,8 @@ struct StagedEmit {
   }
 };
 
-__global__ __launch_bounds__(64) void cabac_bins(CabacBinArgs a) {
+// 6 waves per SIMD: 80 VGPRs instead of 94, no extra spill (it runs beside the encode kernels)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void cabac_bins(CabacBinArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t stage[64 * 8];
   const int mb = blockIdx.x * 64 + threadIdx.x, slot = blockIdx.y, n = a.g.nmb();
   if (mb >= n) return;
