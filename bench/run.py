@@ -260,16 +260,50 @@ def _hevc_run(args, W, H, B, F, bd, crf, two_pass_kbps=None, fps=30.0, resident=
                         pass2_vs_target=round(got / share, 4), exponent=round(fb.e, 3),
                         feedback_updates=len(fb.history))
 
+    synth_stream = torch.cuda.Stream(device=env.device)
+
+    def run_pipelined(first, n, quality=False):
+        """n CRF steps pipelined like bench.py: step k + 1's synthesis and lookahead on a side
+        stream while step k encodes, step k's CABAC tail (host entropy jobs) beside step k + 1's
+        GPU work (encode_async); the last step is collected before returning."""
+        def synth_async(k):
+            with torch.cuda.stream(synth_stream):
+                c = clip(k)
+                ev = torch.cuda.Event()
+                ev.record(synth_stream)
+            return c, ev
+        c, ev = synth_async(first)
+        ana = enc.analyse_async(c[0], stream=synth_stream)
+        prev = res = None
+        for k in range(n):
+            (y, u, v), cur_ev, cur_ana = c, ev, ana
+            if k + 1 < n:
+                c, ev = synth_async(first + k + 1)
+                ana = enc.analyse_async(c[0], stream=synth_stream)
+            torch.cuda.current_stream().wait_event(cur_ev)
+            pend = enc.encode_async(y, u, v, metrics=quality and k == 0, analysis=cur_ana)
+            del y, u, v
+            if prev is not None:
+                r = prev.result()
+                res = r if res is None or not quality else res
+            prev = pend
+        r = prev.result()
+        return (res if (quality and res is not None) else r), None
+
+    pipelined = two_pass_kbps is None and held is None
     enc.stage_timer.enabled = True                                     # HIP-event stage times, warmup only
-    res, info = step(-1, quality=True)                                 # warmup (+ PSNR)
+    res, info = run_pipelined(-1, 1, quality=True) if pipelined else step(-1, quality=True)  # warmup (+ PSNR)
     stage_ms = {k: round(v["s"] * 1000.0, 1) for k, v in enc.stage_timer.summary().items()}
     enc.stage_timer.enabled = False
     psnr = float(np.mean([r.psnr_y for r in res]))
     torch.cuda.synchronize()
     D.barrier(env)
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        res, info = step(k)
+    if pipelined:
+        res, info = run_pipelined(0, args.steps)
+    else:
+        for k in range(args.steps):
+            res, info = step(k)
     torch.cuda.synchronize()
     D.barrier(env)
     dt = D.max_over_ranks(env, time.perf_counter() - t0)

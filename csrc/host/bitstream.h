@@ -92,6 +92,7 @@ class BitReader {
     return v;
   }
   void skip(int nbits) { pos_ += nbits; }
+  void seek(size_t bitpos) { pos_ = bitpos; }
   uint32_t get_ue() {
     int lz = 0;
     while (get_bit() == 0) {

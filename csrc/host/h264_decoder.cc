@@ -237,44 +237,76 @@ int read_vlc(BitReader& br, const uint8_t* lens, const uint8_t* bits, int n) {
 
 // ---------------------------------------------------------------- CABAC decoding engine (9.3.1.2, 9.3.3.2)
 struct CabacDec {
+  // The 9.3.3.2 engine (codIRange / codIOffset, spec arithmetic) over a direct view of the
+  // slice data: renormalisation takes all its bits in one read (count of leading zeros of the
+  // range) from a big-endian 64-bit window instead of bit by bit through BitReader (the host
+  // parse of the transcode path was bound by that).  `pos` is the exact bit position of the
+  // next unread bit; BitReader is re-synchronised when the engine hands the stream back
+  // (end of slice, I_PCM samples).
   BitReader* br = nullptr;
+  const uint8_t* data = nullptr;
+  size_t nbytes = 0, pos = 0;
   uint32_t range = 510, offset = 0;
   uint8_t st[kCabacContexts];
-  int bit() {
-    if (br->pos() >= br->size_bits()) return 0;  // past the end: zeros (malformed streams only)
-    return static_cast<int>(br->get_bit());
+  // n (1..25) bits at pos; zeros past the end (malformed streams only)
+  uint32_t read_bits(int n) {
+    const size_t byte = pos >> 3;
+    uint64_t w;
+    if (byte + 8 <= nbytes) {
+      std::memcpy(&w, data + byte, 8);
+      w = __builtin_bswap64(w);
+    } else {
+      w = 0;
+      for (int k = 0; k < 8; ++k) w |= static_cast<uint64_t>(byte + k < nbytes ? data[byte + k] : 0) << (56 - 8 * k);
+    }
+    const uint32_t v = static_cast<uint32_t>((w << (pos & 7)) >> (64 - n));
+    pos += static_cast<size_t>(n);
+    return v;
   }
   void init_engine() {
+    data = br->data();
+    nbytes = br->size_bits() / 8;
+    pos = br->pos();
     range = 510;
-    offset = 0;
-    for (int i = 0; i < 9; ++i) offset = (offset << 1) | bit();
+    offset = read_bits(9);
     if (offset == 510 || offset == 511) throw std::runtime_error("CABAC: bad initial codIOffset");
   }
+  void renorm() {  // range in [2, 255]: shift it back to [256, 510] in one step
+    const int n = __builtin_clz(range) - 23;
+    range <<= n;
+    offset = (offset << n) | read_bits(n);
+  }
+  // next state (pStateIdx << 1 | valMPS) after an MPS / an LPS, 9.3.3.2.1.1 (Table 9-45)
+  struct NextState {
+    uint8_t mps[128], lps[128];
+    NextState() {
+      for (int s = 0; s < 128; ++s) {
+        const int pst = s >> 1, m = s & 1;
+        mps[s] = static_cast<uint8_t>(((pst < 62 ? pst + 1 : 62) << 1) | m);
+        lps[s] = static_cast<uint8_t>((kCabacTransLPS[pst] << 1) | (pst == 0 ? 1 - m : m));
+      }
+    }
+  };
+  static const NextState& next_state() {
+    static const NextState t;
+    return t;
+  }
+  // DecodeDecision without a data-dependent branch (the bin is unpredictable): the MPS / LPS
+  // outcome selects offset, range and state by conditional moves
   int decision(int ctx) {
-    int s = st[ctx];
-    int pst = s >> 1, mps = s & 1;
-    uint32_t rlps = kCabacRangeLPS[pst][(range >> 6) & 3];
-    range -= rlps;
-    int bin;
-    if (offset >= range) {
-      bin = !mps;
-      offset -= range;
-      range = rlps;
-      if (pst == 0) mps = 1 - mps;
-      pst = kCabacTransLPS[pst];
-    } else {
-      bin = mps;
-      pst = pst < 62 ? pst + 1 : 62;
-    }
-    st[ctx] = static_cast<uint8_t>((pst << 1) | mps);
-    while (range < 256) {
-      range <<= 1;
-      offset = (offset << 1) | bit();
-    }
-    return bin;
+    const int s = st[ctx];
+    const uint32_t rlps = kCabacRangeLPS[s >> 1][(range >> 6) & 3];
+    const uint32_t rmps = range - rlps;
+    const bool lps = offset >= rmps;
+    offset = lps ? offset - rmps : offset;
+    range = lps ? rlps : rmps;
+    const NextState& ns = next_state();
+    st[ctx] = lps ? ns.lps[s] : ns.mps[s];
+    if (range < 256) renorm();
+    return (s & 1) ^ static_cast<int>(lps);
   }
   int bypass() {
-    offset = (offset << 1) | bit();
+    offset = (offset << 1) | read_bits(1);
     if (offset >= range) {
       offset -= range;
       return 1;
@@ -283,11 +315,11 @@ struct CabacDec {
   }
   int terminate() {
     range -= 2;
-    if (offset >= range) return 1;
-    while (range < 256) {
-      range <<= 1;
-      offset = (offset << 1) | bit();
+    if (offset >= range) {
+      br->seek(pos);  // the stream continues with BitReader (PCM samples / trailing bits)
+      return 1;
     }
+    if (range < 256) renorm();
     return 0;
   }
   int eg(int k) {  // exp-Golomb suffix, bypass bins

@@ -163,6 +163,31 @@ class HevcSegmentResult:
         return out
 
 
+class PendingHevc:
+    """A batch issued by :meth:`GpuHevcEncoder.encode_async`."""
+
+    def __init__(self, enc, finish):
+        self._enc, self._finish = enc, finish
+        self._res = None
+        self._exc: BaseException | None = None
+
+    def done(self) -> bool:
+        return self._finish is None
+
+    def result(self) -> list:
+        if self._finish is not None:
+            try:
+                self._res = self._finish()
+            except BaseException as e:  # noqa: BLE001
+                self._exc = e
+            self._finish = None
+            if self in self._enc._inflight:
+                self._enc._inflight.remove(self)
+        if self._exc is not None:
+            raise self._exc
+        return self._res
+
+
 class GpuHevcEncoder:
     """Batched gfx950 HEVC encoder (Main / Main 10, CABAC)."""
 
@@ -257,6 +282,8 @@ class GpuHevcEncoder:
         # codes them on `entropy_threads` C++ threads with the GIL released
         self.entropy_threads = entropy_threads or min(16, os.cpu_count() or 4)
         self.pool = cf.ThreadPoolExecutor(max_workers=1)
+        self._inflight: list = []               # encode_async batches not yet finished (oldest first)
+        self._pending: list[list] = [[], [], []]  # CABAC jobs per pinned host buffer set
         self.timings: dict[str, float] = {}
         self.stats: dict[str, float] = {}
         self.ctb_need = torch.ones((B, self.nctb), dtype=torch.uint8, device=dev)
@@ -289,7 +316,10 @@ class GpuHevcEncoder:
         return self.params_nal
 
     def close(self):
+        self.drain()
         self.pool.shutdown(wait=True)
+        if getattr(self, "_la_pool", None) is not None:
+            self._la_pool.shutdown(wait=True)
 
     # ------------------------------------------------------------------ helpers
     @staticmethod
@@ -315,36 +345,77 @@ class GpuHevcEncoder:
                                  self.p.bit_depth, self._stream())
 
     # ------------------------------------------------------------------ rate control
-    def crf_qps(self, y: torch.Tensor) -> np.ndarray:
-        """[B, F] CRF QPs: GPU lookahead on the (8-bit proxy of the) luma -> CRF curve."""
+    def _analysis(self, y: torch.Tensor, la) -> dict:
+        """The lookahead of one batch on the current stream: host results (frame costs, scene
+        cuts) synchronised, the cutree offsets left on the device."""
         from ..rc.lookahead import GpuLookahead
-        from ..rc.ratecontrol import crf_qps_batch
+        from ..rc.ratecontrol import MBTREE_STRENGTH, scenecut_flags
 
-        if getattr(self, "_la", None) is None:
-            self._la = GpuLookahead(self.dev, self.p.la_range)
-        t0 = time.perf_counter()
         y8 = y
         if y.dtype != torch.uint8:
             y8 = (y >> (self.p.bit_depth - 8)).clamp_(0, 255).to(torch.uint8)
         lbw, lbh = GpuLookahead.block_grid(y.shape[3], y.shape[2])
-        from ..rc.ratecontrol import MBTREE_STRENGTH, scenecut_flags
         # cutree needs the lookahead's block grid to be the coded 16x16 grid (no -s resize); the
         # 32-aligned coded height may add one 16-row below the lookahead's last row
         # Pieces shorter than 8 pictures give the propagation too little to offset cutree's
         # constant CRF compensation ((1 - qcomp) x 13.5 QP): they keep the plain CRF QPs.
         use_tree = self.p.cutree and lbw == self.wmb and lbh <= self.hmb and y.shape[1] >= 8
-        self._cutree_rows = lbh
+        cutree = None
         if use_tree:
-            costs_d, self._cutree = self._la.mbtree(y8.contiguous(), MBTREE_STRENGTH)
+            costs_d, cutree = la.mbtree(y8.contiguous(), MBTREE_STRENGTH)
             costs = costs_d.cpu().numpy()
         else:
-            costs = self._la.frame_costs(y8.contiguous()).cpu().numpy()
-        self._scenecuts = scenecut_flags(costs, float(self.p.scenecut), keyint=self.p.keyint or None)
-        q = crf_qps_batch(costs, float(self.p.crf), lbw * lbh, keyint=self.p.keyint or None,
-                          scenecuts=self._scenecuts, mbtree=use_tree, bframes=self.nb)
+            costs = la.frame_costs(y8.contiguous()).cpu().numpy()
+        return dict(costs=costs, cutree=cutree, use_tree=use_tree, rows=lbh, blocks=lbw * lbh,
+                    scenecuts=scenecut_flags(costs, float(self.p.scenecut), keyint=self.p.keyint or None),
+                    shape=tuple(y.shape))
+
+    def crf_qps(self, y: torch.Tensor, analysis: dict | None = None) -> np.ndarray:
+        """[B, F] CRF QPs: GPU lookahead on the (8-bit proxy of the) luma -> CRF curve.
+        ``analysis``: the batch's lookahead from :meth:`analyse_async` (None: run it here)."""
+        from ..rc.lookahead import GpuLookahead
+        from ..rc.ratecontrol import crf_qps_batch
+
+        t0 = time.perf_counter()
+        if analysis is None or analysis["shape"] != tuple(y.shape):
+            if getattr(self, "_la", None) is None:
+                self._la = GpuLookahead(self.dev, self.p.la_range)
+            analysis = self._analysis(y, self._la)
+        else:
+            torch.cuda.current_stream(self.dev).wait_event(analysis["event"])
+            self.timings["lookahead_async_s"] = self.timings.get("lookahead_async_s", 0.0) + analysis["seconds"]
+        self._cutree, self._cutree_rows = analysis["cutree"], analysis["rows"]
+        self._scenecuts = analysis["scenecuts"]
+        q = crf_qps_batch(analysis["costs"], float(self.p.crf), analysis["blocks"], keyint=self.p.keyint or None,
+                          scenecuts=self._scenecuts, mbtree=analysis["use_tree"], bframes=self.nb)
         self.stats["scenecuts"] = int(self._scenecuts.sum())
         self.timings["lookahead_s"] = self.timings.get("lookahead_s", 0.0) + time.perf_counter() - t0
         return q
+
+    def analyse_async(self, y: torch.Tensor, after: torch.cuda.Event | None = None,
+                      stream: torch.cuda.Stream | None = None) -> cf.Future:
+        """Start the lookahead of a *later* batch while the current one encodes (as
+        GpuH264Encoder.analyse_async): its own stream (after ``after``, e.g. the end of the
+        batch's synthesis or decode), host thread and lookahead workspace; the returned future
+        goes to :meth:`encode_async` / :meth:`encode` as ``analysis=``."""
+        from ..rc.lookahead import GpuLookahead
+        if getattr(self, "_la_async", None) is None:
+            self._la_async = GpuLookahead(self.dev, self.p.la_range)
+            self._la_stream = torch.cuda.Stream(device=self.dev)
+            self._la_pool = cf.ThreadPoolExecutor(max_workers=1)
+
+        def job():
+            t0 = time.perf_counter()
+            st = stream if stream is not None else self._la_stream
+            with torch.cuda.device(self.dev), torch.cuda.stream(st):
+                if after is not None:
+                    st.wait_event(after)
+                a = self._analysis(y, self._la_async)
+                a["event"] = torch.cuda.Event()
+                a["event"].record(st)
+            a["seconds"] = time.perf_counter() - t0
+            return a
+        return self._la_pool.submit(job)
 
     # ------------------------------------------------------------------ B-picture helpers
     @staticmethod
@@ -475,7 +546,38 @@ class GpuHevcEncoder:
     # ------------------------------------------------------------------ encode
     def encode(self, y: torch.Tensor, u: torch.Tensor, v: torch.Tensor, qps: np.ndarray | None = None,
                keep_recon: bool = False, metrics: bool = True, qp_delta=None, rate_fb=None,
-               anchors_at=()) -> list[HevcSegmentResult]:
+               anchors_at=(), analysis=None) -> list[HevcSegmentResult]:
+        """See :meth:`_encode`; completes the batch (and any batch still in flight first)."""
+        self.drain()
+        if isinstance(analysis, cf.Future):
+            analysis = analysis.result()
+        return self._encode(y, u, v, qps, keep_recon, metrics, qp_delta, rate_fb, anchors_at, analysis)()
+
+    def encode_async(self, y: torch.Tensor, u: torch.Tensor, v: torch.Tensor, **kw) -> "PendingHevc":
+        """Issue a batch and return before its CABAC tail finishes: the last steps' entropy jobs
+        (host threads) and the result assembly overlap the next batch's GPU work.  At most two
+        batches are in flight (issuing a third completes the oldest).  ``.result()`` gives what
+        :meth:`encode` returns.  ``kw``: :meth:`encode`'s keyword arguments; ``analysis`` may be
+        the future from :meth:`analyse_async`."""
+        ana = kw.pop("analysis", None)
+        if isinstance(ana, cf.Future):
+            ana = ana.result()
+        while len(self._inflight) >= 2:
+            self._inflight[0].result()
+        fin = self._encode(y, u, v, kw.get("qps"), kw.get("keep_recon", False), kw.get("metrics", True),
+                           kw.get("qp_delta"), kw.get("rate_fb"), kw.get("anchors_at", ()), ana)
+        pend = PendingHevc(self, fin)
+        self._inflight.append(pend)
+        return pend
+
+    def drain(self) -> None:
+        """Complete every batch issued by :meth:`encode_async`."""
+        while self._inflight:
+            self._inflight[0].result()
+
+    def _encode(self, y: torch.Tensor, u: torch.Tensor, v: torch.Tensor, qps: np.ndarray | None = None,
+                keep_recon: bool = False, metrics: bool = True, qp_delta=None, rate_fb=None,
+                anchors_at=(), analysis=None):
         """y: [B, F, h, w] (uint8, or uint16 holding bit_depth-bit samples), u/v half size.
         Every segment starts with an IDR picture; then P anchors and (bframes) the B pictures
         between them, in coding order (models/gop.py; a scene cut becomes an anchor coded all
@@ -489,6 +591,8 @@ class GpuHevcEncoder:
         B, F, h, w = y.shape
         if B != self.B or (w, h) != (self.p.width, self.p.height):
             raise ValueError(f"expected [{self.B}, F, {self.p.height}, {self.p.width}], got {list(y.shape)}")
+        # Returns the batch's finisher: waits for its CABAC jobs, checks the device error flag
+        # and builds the results (encode calls it at once, encode_async later).
         if y.device != self.dev:
             raise ValueError("inputs must live on the encoder's device")
         qi, qpp = self.p.frame_qps()
@@ -496,7 +600,7 @@ class GpuHevcEncoder:
         self._cutree = None
         from_la = False
         if qps is None and self.p.crf is not None and self.p.lookahead and not self.p.intra_only:
-            qps = self.crf_qps(y)
+            qps = self.crf_qps(y, analysis)
             from_la = True
         cuts_h = self._scenecuts if self._scenecuts is not None else np.zeros((B, F), dtype=bool)
         plan = self._plan(F, cuts_h, anchors_at)
@@ -528,7 +632,7 @@ class GpuHevcEncoder:
         fb_known, fb_spent, fb_stage = 0, np.zeros((B, F)), []
         nals: list[list] = [[None] * F for _ in range(B)]
         futs = []
-        pending: list[list] = [[], [], []]
+        pending = self._pending  # per pinned host buffer set: CABAC jobs still reading it (across batches)
         sse = []
         recon = [None] * F if keep_recon else None
         t_gpu = t_host = t_blocked = 0.0
@@ -791,6 +895,11 @@ class GpuHevcEncoder:
         qps = np.empty_like(qps_c)
         qps[:, order] = qps_c
         self.last_qps = qps.copy()
+        return lambda: self._finish(futs, nals, B, F, h, w, bd, sse, metrics, keep_recon, recon, order, gate_sum,
+                                    st, t_gpu, t_blocked, cabac_s)
+
+    def _finish(self, futs, nals, B, F, h, w, bd, sse, metrics, keep_recon, recon, order, gate_sum, st, t_gpu,
+                t_blocked, cabac_s) -> list[HevcSegmentResult]:
         if int(self.err.item()) != 0:
             raise RuntimeError("HEVC encoder: wavefront progress timeout")
         t2 = time.perf_counter()
@@ -809,7 +918,7 @@ class GpuHevcEncoder:
         # loop_waits_on_step_t_minus_3_s: the frame loop waiting for the CABAC jobs of step
         # t - 3 to release their pinned host buffers -- those jobs first wait for their
         # records' device-to-host copy, so this includes GPU completion, not only entropy coding
-        self.timings = dict(loop_s=t_gpu, loop_waits_on_step_t_minus_3_s=t_blocked, host_wait_s=t_host,
+        self.timings.update(loop_s=t_gpu, loop_waits_on_step_t_minus_3_s=t_blocked, host_wait_s=t_host,
                             cabac_batch_s=cabac_s[0], cabac_ms_per_picture_wall=1000.0 * cabac_s[0] / max(1, B * F),
                             entropy_threads=self.entropy_threads)
         out = []
