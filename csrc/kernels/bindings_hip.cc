@@ -82,7 +82,7 @@ void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t* src_y, con
                               int chroma_qp_offset, void* hdr, int16_t* coef, uint8_t* nz,
                               const uint8_t* intra_flag, const int* intra_count, int* err, int use_i4x4,
                               const int8_t* aq, void* stream, int use_i8x8, const void* route, int nbuf,
-                              int slice_rows);
+                              int slice_rows, int trellis, float trellis_lambda);
 void mivc_launch_deblock(int B, int wmb, int hmb, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const void* hdr,
                          const uint8_t* nz, int chroma_qp_offset, int alpha_off, int beta_off, int* err,
                          void* stream, const void* route, int nbuf);
@@ -147,6 +147,7 @@ void mivc_launch_cavlc(int B, int wmb, int hmb, const void* hdr, const int16_t* 
                        long long cap_words, const uint32_t* hdr_bits, const int* hdr_nbits, int pslice, int slice_qp,
                        const int* slot_qp, uint8_t* out, long long* out_off, const uint8_t* nz, void* stream);
 void mivc_launch_satd_blocks(const uint8_t* src, const uint8_t* pred, int* out, int n, int mode, void* stream);
+void mivc_launch_trellis_blocks(const int* w, int* out, int n, int qp, int mode, int skip_dc, void* stream);
 void mivc_launch_sse(int B, int W, int H, int w, int h, const uint8_t* sy, const uint8_t* su, const uint8_t* sv,
                      const uint8_t* ry, const uint8_t* ru, const uint8_t* rv, unsigned long long* sse,
                      float* ssim_sum, void* stream, const void* route, int nbuf);
@@ -406,15 +407,18 @@ PYBIND11_MODULE(_hip, m) {
   m.def("encode_intra", [](int B, int wmb, int hmb, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t ry,
                            uintptr_t ru, uintptr_t rv, uintptr_t qp, int cqo, uintptr_t hdr, uintptr_t coef,
                            uintptr_t nz, uintptr_t intra_flag, uintptr_t intra_count, uintptr_t err, int use_i4x4,
-                           uintptr_t stream, uintptr_t aq, int use_i8x8, uintptr_t route, int nbuf, int slice_rows) {
+                           uintptr_t stream, uintptr_t aq, int use_i8x8, uintptr_t route, int nbuf, int slice_rows,
+                           int trellis, float trellis_lambda) {
     mivc_launch_encode_intra(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), P<uint8_t>(ry),
                              P<uint8_t>(ru), P<uint8_t>(rv), P<int>(qp), cqo, P<void>(hdr), P<int16_t>(coef),
                              P<uint8_t>(nz), P<uint8_t>(intra_flag), P<int>(intra_count), P<int>(err), use_i4x4,
-                             P<int8_t>(aq), S(stream), use_i8x8, P<void>(route), nbuf, slice_rows);
+                             P<int8_t>(aq), S(stream), use_i8x8, P<void>(route), nbuf, slice_rows, trellis,
+                             trellis_lambda);
   }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("sy"), py::arg("su"), py::arg("sv"), py::arg("ry"),
      py::arg("ru"), py::arg("rv"), py::arg("qp"), py::arg("cqo"), py::arg("hdr"), py::arg("coef"), py::arg("nz"),
      py::arg("intra_flag"), py::arg("intra_count"), py::arg("err"), py::arg("use_i4x4"), py::arg("stream"),
-     py::arg("aq") = 0, py::arg("use_i8x8") = 0, py::arg("route") = 0, py::arg("nbuf") = 0, py::arg("slice_rows") = 0);
+     py::arg("aq") = 0, py::arg("use_i8x8") = 0, py::arg("route") = 0, py::arg("nbuf") = 0, py::arg("slice_rows") = 0,
+     py::arg("trellis") = 0, py::arg("trellis_lambda") = 1.0f);
   m.def("deblock", [](int B, int wmb, int hmb, uintptr_t ry, uintptr_t ru, uintptr_t rv, uintptr_t hdr, uintptr_t nz,
                       int cqo, int alpha_off, int beta_off, uintptr_t err, uintptr_t stream, uintptr_t route, int nbuf) {
     mivc_launch_deblock(B, wmb, hmb, P<uint8_t>(ry), P<uint8_t>(ru), P<uint8_t>(rv), P<void>(hdr), P<uint8_t>(nz),
@@ -681,6 +685,10 @@ PYBIND11_MODULE(_hip, m) {
   m.def("satd_blocks", [](uintptr_t src, uintptr_t pred, uintptr_t out, int n, int mode, uintptr_t stream) {
     if (n <= 0) throw std::invalid_argument("satd_blocks: n must be positive");
     mivc_launch_satd_blocks(P<uint8_t>(src), P<uint8_t>(pred), P<int>(out), n, mode, S(stream));
+  });
+  m.def("trellis_blocks", [](uintptr_t w, uintptr_t out, int n, int qp, int mode, int skip_dc, uintptr_t stream) {
+    if (n <= 0 || qp < 0 || qp > 51) throw std::invalid_argument("trellis_blocks: n > 0, 0 <= qp <= 51");
+    mivc_launch_trellis_blocks(P<int>(w), P<int>(out), n, qp, mode, skip_dc, S(stream));
   });
   m.def("lookahead_low_bytes", [](int w, int h, int n) { return mivc_lookahead_low_bytes(w, h, n); });
   m.def("lookahead_quarter_bytes", [](int w, int h, int n) { return mivc_lookahead_quarter_bytes(w, h, n); });

@@ -9,7 +9,7 @@
 //     reconstruction written here is exactly what a decoder produces.
 // SURVEY.md K-C8.  One wave64 per macroblock: lanes 0-15 luma 4x4 blocks,
 // lanes 16-23 chroma 4x4 blocks (two MBs per wave, see encode_inter_mb).
-#include "h264_t8.h"
+#include "h264_trellis.h"
 
 namespace mivc {
 namespace gpu {
@@ -61,108 +61,7 @@ struct InterArgs {
   int nbuf;
 };
 
-// Rate-distortion quantisation of one 4x4 block (x264 --trellis 1, simplified to a greedy pass
-// in reverse scan order): every coefficient chooses among 0 and the two levels around the
-// rounded quotient by SSD (pixel domain: the error of coefficient (i, j) weighs 1 / (n_i n_j),
-// n = 4, 10, 4, 10 the row norms of the core transform) + lambda * CABAC bits, with static bin
-// costs for significance / last (a coefficient above every non-zero one would become the last
-// one), greater-than-one and the unary level bins, and the sign.  Levels after the block's
-// last non-zero one are never coded, so trailing small coefficients are dropped first.
-constexpr float kSig0 = 0.55f, kSig1 = 1.35f, kLast0 = 0.25f, kLast1 = 2.2f, kGt1No = 0.6f, kGt1Yes = 1.7f;
-
-// static CABAC bits of a non-zero level l >= 1 (significance, last, sign, greater-than-one,
-// unary and Exp-Golomb suffix); `seen`: a non-zero level follows in scan order
-__device__ __forceinline__ float trellis_level_bits(int l, bool seen) {
-  return kSig1 + (seen ? kLast0 : kLast1) + 1.0f +
-         (l == 1 ? kGt1No : kGt1Yes + 0.9f * static_cast<float>(min(l - 2, 13)) +
-                                (l > 15 ? 2.0f * (31 - __clz(l - 14)) + 1.0f : 0.0f));
-}
-
-// start: first scan index coded (1 for chroma AC: the DC goes through the 2x2 Hadamard)
-__device__ __forceinline__ void trellis_lite4x4(const int (&w)[16], int (&lv)[16], const int (&mf)[3], int qbits,
-                                                float lam, int start = 0) {
-  constexpr float kInvNorm[3] = {1.0f / 16.0f, 1.0f / 100.0f, 1.0f / 40.0f};
-  // a block whose every rounded quotient is 0 quantises to zeros whatever the choice: most
-  // blocks of B pictures -- skip the pass (wave-wide when every lane's block is such)
-  int zmax = 0;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int r = h264::kZigzag4x4[i];
-    const int a = w[r] < 0 ? -w[r] : w[r];
-    if (i >= start) zmax |= (a * mf[h264::kPosClass[r]] + (1 << (qbits - 1))) >> qbits;
-  }
-  if (zmax == 0) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) lv[r] = 0;
-    return;
-  }
-  bool seen = false;
-#pragma unroll
-  for (int i = 15; i >= 0; --i) {
-    if (i < start) {
-      lv[h264::kZigzag4x4[i]] = 0;
-      continue;
-    }
-    const int r = h264::kZigzag4x4[i];
-    const int cls = h264::kPosClass[r];
-    const int a = w[r] < 0 ? -w[r] : w[r];
-    const float fm = static_cast<float>(mf[cls]);
-    const int zr = (a * mf[cls] + (1 << (qbits - 1))) >> qbits;  // |W| < 2^14, MF < 2^14
-    const float step = static_cast<float>(1 << qbits) / fm;
-    const float inv_n = kInvNorm[cls];
-    float best = static_cast<float>(a) * static_cast<float>(a) * inv_n + lam * (seen ? kSig0 : 0.0f);
-    int bl = 0;
-#pragma unroll
-    for (int d = 1; d >= 0; --d) {
-      const int l = zr - d;
-      if (l < 1) continue;
-      const float e = static_cast<float>(a) - static_cast<float>(l) * step;
-      const float j = e * e * inv_n + lam * trellis_level_bits(l, seen);
-      if (j < best) {
-        best = j;
-        bl = l;
-      }
-    }
-    lv[r] = w[r] < 0 ? -bl : bl;
-    seen |= bl != 0;
-  }
-}
-
-// The same greedy choice for one 16-coefficient chunk (scan positions 16k .. 16k + 15) of an 8x8
-// block, in the quantiser's own domain: the 8x8 scaling gives every position the same
-// pixel-domain step Qstep, so a level l of exact quotient z costs (z - l)^2 Qstep^2 of SSD and
-// lambda / Qstep^2 = 0.85 * 2^((QP - 12) / 3) / (0.390625 * 2^(QP / 3)) = 0.136 per bit (QP-free).
-// seen: a later chunk of the block keeps a non-zero level.  lv keeps its sign from z.
-__device__ __forceinline__ void trellis_lite8_chunk(const float (&z)[16], int (&lv)[16], float lamq, bool seen) {
-  float zmax = 0.0f;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) zmax = fmaxf(zmax, fabsf(z[i]));
-  if (zmax < 0.5f) {  // every rounded quotient is 0
-#pragma unroll
-    for (int i = 0; i < 16; ++i) lv[i] = 0;
-    return;
-  }
-#pragma unroll
-  for (int i = 15; i >= 0; --i) {
-    const float az = fabsf(z[i]);
-    const int zr = static_cast<int>(az + 0.5f);
-    float best = az * az + lamq * (seen ? kSig0 : 0.0f);
-    int bl = 0;
-#pragma unroll
-    for (int d = 1; d >= 0; --d) {
-      const int l = zr - d;
-      if (l < 1) continue;
-      const float e = az - static_cast<float>(l);
-      const float j = e * e + lamq * trellis_level_bits(l, seen);
-      if (j < best) {
-        best = j;
-        bl = l;
-      }
-    }
-    lv[i] = z[i] < 0.0f ? -bl : bl;
-    seen |= bl != 0;
-  }
-}
+// trellis_lite4x4 / trellis_lite8_chunk: h264_trellis.h
 
 // clause 8.4.2.3.2 for one sample: ((p * w + 2^(d-1)) >> d) + o, clipped
 __device__ __forceinline__ int wp_sample(int p, int w, int o, int d) {
@@ -335,7 +234,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     {
       const int qbits = 15 + qp / 6;
       if (a.trellis) {
-        trellis_lite4x4(res, lv, mf, qbits, a.trellis_lambda * 0.85f * exp2f((qp - 12) * (1.0f / 3.0f)));
+        trellis_lite4x4(res, lv, mf, qbits, trellis_lambda4(a.trellis_lambda, qp));
       } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) lv[r] = h264::quant_coef(res[r], mf[h264::kPosClass[r]], qbits, 11);
@@ -538,7 +437,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     s_cdc[half][comp][cb] = res[0];
     const int qbits = 15 + qpc / 6;
     if (a.trellis >= 2) {  // chroma AC by the same rate-distortion choice, at the chroma QP's lambda
-      trellis_lite4x4(res, lv, mfc, qbits, a.trellis_lambda * 0.85f * exp2f((qpc - 12) * (1.0f / 3.0f)), 1);
+      trellis_lite4x4(res, lv, mfc, qbits, trellis_lambda4(a.trellis_lambda, qpc), 1);
     } else {
 #pragma unroll
       for (int r = 0; r < 16; ++r)

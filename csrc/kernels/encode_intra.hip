@@ -8,7 +8,7 @@
 //
 // For P frames only MBs flagged by encode_inter (intra_flag) are coded here; the
 // others were reconstructed by encode_inter and only advance the row counter.
-#include "h264_t8.h"
+#include "h264_trellis.h"
 #include "../common/h264_i4_taps.h"
 
 #include <cstdlib>
@@ -48,6 +48,10 @@ struct IntraArgs {
   // MB rows per slice (H264Params.slices): a slice's first row has no neighbours above
   // (6.4.8) and starts without waiting for the row above; 0 = one slice per picture
   int slice_rows;
+  // x264 --trellis on the intra MBs' final levels (h264_trellis.h, the lane-parallel form):
+  // 1 = 4x4 luma (Intra4x4, Intra16x16 AC), 2 = also Intra8x8 and chroma AC; 0 = dead-zone
+  int trellis;
+  float trellis_lambda;
 };
 
 __device__ __forceinline__ bool top_in_slice(int my, int slice_rows) {
@@ -162,6 +166,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
   const int qp = clampi(a.qp[slot] + (a.aq ? a.aq[o] : 0), 0, 51);
   const int qpc = h264::chroma_qp(qp, a.chroma_qp_offset);
   const int lambda = h264::kLambda[qp];
+  const float lam4 = trellis_lambda4(a.trellis_lambda, qp);
   const int qbits = 15 + qp / 6, qbits_c = 15 + qpc / 6;
   const uint8_t* srcy = a.src_y + slot * g.ysize();
   const size_t rcur = route_index(a.rt, a.nbuf, slot, RO_CUR);
@@ -346,12 +351,14 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
         v[x] = static_cast<int>(S.src[(by * 4 + gy) * 16 + bx * 4 + x]) - pr[x];
       }
       grp_fwd4x4(v, gb, gy);
+      int tl[4];
+      if (a.trellis) grp_trellis4x4(v, tl, gy, mf0, mf1, mf2, qbits, lam4, false);
 #pragma unroll
       for (int x = 0; x < 4; ++x) {
         int cls = pos_class(x, gy);
         int mf = cls == 0 ? mf0 : (cls == 1 ? mf1 : mf2);
         int dq = cls == 0 ? dv0 : (cls == 1 ? dv1 : dv2);
-        int lv = h264::quant_coef(v[x], mf, qbits, 21);
+        int lv = a.trellis ? tl[x] : h264::quant_coef(v[x], mf, qbits, 21);
         if (lane < 4) S.c4[blk][zzinv(x, gy)] = static_cast<int16_t>(lv);
         v[x] = (lv * dq) << qs;
       }
@@ -480,7 +487,19 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
       {
         const int pos = kZz8[lane];
         const int cls = pos8(pos & 7, pos >> 3);
-        const int lv = h264::quant_coef(S.d8[pos], kQuant8MF[qm][cls], qbits8, 21);
+        const int mf8 = kQuant8MF[qm][cls];
+        int lv;
+        if (a.trellis >= 2) {  // the whole 8x8 block at once: lane = scan index
+          const float az = fabsf(static_cast<float>(S.d8[pos]) * static_cast<float>(mf8) * exp2f(-static_cast<float>(qbits8)));
+          int lf, lt;
+          trellis_both(az, 1.0f, 1.0f, a.trellis_lambda * 0.136f, static_cast<int>(az + 0.5f), lf, lt);
+          const unsigned long long fm = __ballot(lf != 0);
+          const int istar = fm ? 63 - __builtin_clzll(fm) : -1;
+          const int l = lane > istar ? 0 : (lane == istar ? lf : lt);
+          lv = S.d8[pos] < 0 ? -l : l;
+        } else {
+          lv = h264::quant_coef(S.d8[pos], mf8, qbits8, 21);
+        }
         S.c8[b8][lane] = static_cast<int16_t>(lv);
         const int ls = 16 * kNorm8[qm][cls];
         S.d8[pos] = q6 >= 6 ? (lv * ls) << (q6 - 6) : (lv * ls + (1 << (5 - q6))) >> (6 - q6);
@@ -545,10 +564,13 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
     if (gy == 0) S.dc16[h264::kBlkX[blk] + 4 * h264::kBlkY[blk]] = v[0];
     const int qm = qp % 6, qs = qp / 6;
     bool any = false;
+    int tl[4];
+    if (a.trellis)
+      grp_trellis4x4(v, tl, gy, h264::kQuantMF[qm][0], h264::kQuantMF[qm][1], h264::kQuantMF[qm][2], qbits, lam4, true);
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
       int cls = pos_class(x, gy);
-      int lv = (gy == 0 && x == 0) ? 0 : h264::quant_coef(v[x], h264::kQuantMF[qm][cls], qbits, 21);
+      int lv = (gy == 0 && x == 0) ? 0 : (a.trellis ? tl[x] : h264::quant_coef(v[x], h264::kQuantMF[qm][cls], qbits, 21));
       S.c16[blk][zzinv(x, gy)] = static_cast<int16_t>(lv);
       any |= lv != 0;
       v[x] = (lv * h264::kDequantV[qm][cls]) << qs;
@@ -601,10 +623,15 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
     }
     grp_fwd4x4(v, gb, gy);
     if (gy == 0 && lane < 32) S.cdc[ccomp][cb] = v[0];
+    int tl[4];
+    if (a.trellis >= 2)
+      grp_trellis4x4(v, tl, gy, h264::kQuantMF[qm][0], h264::kQuantMF[qm][1], h264::kQuantMF[qm][2], qbits_c,
+                     trellis_lambda4(a.trellis_lambda, qpc), true);
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
       int cls = pos_class(x, gy);
-      int lv = (gy == 0 && x == 0) ? 0 : h264::quant_coef(v[x], h264::kQuantMF[qm][cls], qbits_c, 21);
+      int lv = (gy == 0 && x == 0) ? 0
+                                   : (a.trellis >= 2 ? tl[x] : h264::quant_coef(v[x], h264::kQuantMF[qm][cls], qbits_c, 21));
       if (lane < 32) coef[h264::COEF_CHROMA_AC + (ccomp * 4 + cb) * 16 + zzinv(x, gy)] = static_cast<int16_t>(lv);
       v[x] = (lv * h264::kDequantV[qm][cls]) << qs;
     }
@@ -731,8 +758,10 @@ extern "C" void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t*
                                          const int* qp, int chroma_qp_offset, void* hdr, int16_t* coef, uint8_t* nz,
                                          const uint8_t* intra_flag, const int* intra_count, int* err, int use_i4x4,
                                          const int8_t* aq, void* stream, int use_i8x8, const void* route, int nbuf,
-                                         int slice_rows) {
+                                         int slice_rows, int trellis, float trellis_lambda) {
   IntraArgs a;
+  a.trellis = trellis;
+  a.trellis_lambda = trellis_lambda;
   a.rt = static_cast<const SlotRoute*>(route);
   a.nbuf = nbuf;
   a.slice_rows = slice_rows;

@@ -366,8 +366,11 @@ __global__ __launch_bounds__(256) void la_cost(LaArgs a) {
 //   * B between f - 1 and f + 1: list 0 = the distance-1 prediction, list 1 = a search of
 //     f + 1 centred on the reversed vector, bi = their rounded average; the block takes the
 //     cheapest of intra, L0, L1, bi.
-// Frame sums of min(intra, candidate) go to out[n][d] (d = 2..D) and out[n][0] (B).
+// Frame sums of min(intra, candidate) go to out[n][d] (d = 2..D) and out[n][0] (B), each
+// plus (number of blocks that chose intra) << kLaIntraShift: x264's b-adapt guards force P
+// pictures when a P candidate is mostly intra (rc/badapt.py).
 constexpr int kLaMultiCols = 8;
+constexpr int kLaIntraShift = 40;  // frame cost sums stay far below 2^40
 
 struct LaMultiArgs {
   LaGeom g;
@@ -440,7 +443,10 @@ __global__ __launch_bounds__(256) void la_multi(LaMultiArgs a) {
     const int cst = satd_mfma(negH, accS, la_rows8(ref, g.ls, X0 + mx, ry + my)) +
                     2 * (abs(mx - d * v1x) + abs(my - d * v1y)) + 2 * (abs(v1x) + abs(v1y));
     const int s = sum64(mine ? min(intra, cst) : 0);
-    if (lane == 0) atomicAdd(a.out + static_cast<long long>(n) * kLaMultiCols + d, static_cast<unsigned long long>(s));
+    const int ni = sum64(mine && intra < cst ? 1 : 0);
+    if (lane == 0)
+      atomicAdd(a.out + static_cast<long long>(n) * kLaMultiCols + d,
+                static_cast<unsigned long long>(s) + (static_cast<unsigned long long>(ni) << kLaIntraShift));
   }
   // B between f - 1 and f + 1
   if (f + 1 < g.F) {  // frame-uniform
@@ -457,7 +463,10 @@ __global__ __launch_bounds__(256) void la_multi(LaMultiArgs a) {
                     2 * (abs(mx) + abs(my) + abs(v1x) + abs(v1y));
     const int bc = min(min(intra, inter1), min(c1, cbi));
     const int s = sum64(mine ? bc : 0);
-    if (lane == 0) atomicAdd(a.out + static_cast<long long>(n) * kLaMultiCols, static_cast<unsigned long long>(s));
+    const int ni = sum64(mine && intra < min(inter1, min(c1, cbi)) ? 1 : 0);
+    if (lane == 0)
+      atomicAdd(a.out + static_cast<long long>(n) * kLaMultiCols,
+                static_cast<unsigned long long>(s) + (static_cast<unsigned long long>(ni) << kLaIntraShift));
   }
 }
 
@@ -541,7 +550,8 @@ extern "C" int mivc_launch_lookahead(const uint8_t* y, int w, int h, long long f
 
 // b-adapt costs of N = B*F frames (la_multi): needs the lowres planes, block costs and vectors
 // of a preceding mivc_launch_lookahead on the same workspace.  out: [N, 8] u64 (zeroed here):
-// column d = 2..D the P cost at distance d, column 0 the B cost between the neighbours.
+// column d = 2..D the P cost at distance d, column 0 the B cost between the neighbours; bits
+// 40.. of each the number of lowres blocks that chose intra.
 extern "C" int mivc_launch_lookahead_multi(const uint8_t* low, int w, int h, int N, int F, const int* blk_cost,
                                            const int* blk_mv, int D, int range, unsigned long long* out,
                                            void* stream) {

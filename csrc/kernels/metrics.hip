@@ -1,7 +1,7 @@
 // Quality metrics: per-slot sum of squared errors between the
 // source and the deblocked reconstruction over the display window, per plane,
 // plus an 8x8-window SSIM sum on luma.  PSNR/SSIM are finished on the host.
-#include "kcommon.h"
+#include "h264_trellis.h"
 
 namespace mivc {
 namespace gpu {
@@ -93,8 +93,7 @@ __global__ void ssim8(const uint8_t* sy, const uint8_t* ry, int W, int H, int w,
 
 // Known-answer check of the SATD primitives the decision kernels use (tests/test_gpu_satd.py):
 // block i = 16 source and 16 prediction bytes (raster 4x4); mode 0 = satd16 on unpacked
-// residuals (the reference form), 1 = satd4x4_u8 (packed 16-bit), 2 = satd4x4_mfma (a wave
-// prices 16 blocks per MFMA; n a multiple of 64).
+// residuals (the reference form), 1 = satd4x4_u8 (packed 16-bit).
 __global__ __launch_bounds__(64) void satd_blocks(const uint8_t* src, const uint8_t* pred, int* out, int n, int mode) {
   const int i = blockIdx.x * 64 + threadIdx.x;
   const int ic = i < n ? i : n - 1;
@@ -118,10 +117,49 @@ __global__ __launch_bounds__(64) void satd_blocks(const uint8_t* src, const uint
   if (i < n) out[i] = v;
 }
 
+// Known-answer check of the two trellis forms (tests/test_gpu_satd.py): w = [n, 16] raster
+// forward-transform coefficients, out = [n, 16] raster levels.  mode 0: the serial pass
+// (trellis_lite4x4, one lane per block); mode 1: the lane-parallel grp_trellis4x4 (4 lanes per
+// block, one row each).  skip_dc: scan index 0 is coded elsewhere (start = 1).
+__global__ __launch_bounds__(64) void trellis_blocks(const int* w, int* out, int n, int qp, int mode, int skip_dc) {
+  const int qm = qp % 6, qbits = 15 + qp / 6;
+  const float lam = trellis_lambda4(1.0f, qp);
+  const int mf0 = h264::kQuantMF[qm][0], mf1 = h264::kQuantMF[qm][1], mf2 = h264::kQuantMF[qm][2];
+  if (mode == 0) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    const int ic = i < n ? i : n - 1;
+    int c[16], lv[16];
+    const int mf[3] = {mf0, mf1, mf2};
+#pragma unroll
+    for (int r = 0; r < 16; ++r) c[r] = w[static_cast<size_t>(ic) * 16 + r];
+    trellis_lite4x4(c, lv, mf, qbits, lam, skip_dc ? 1 : 0);
+    if (i < n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) out[static_cast<size_t>(i) * 16 + r] = lv[r];
+  } else {
+    const int lane = threadIdx.x, gy = lane & 3;
+    const int b = blockIdx.x * 16 + (lane >> 2);
+    const int bc = b < n ? b : n - 1;
+    int c[4], lv[4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) c[x] = w[static_cast<size_t>(bc) * 16 + gy * 4 + x];
+    grp_trellis4x4(c, lv, gy, mf0, mf1, mf2, qbits, lam, skip_dc != 0);
+    if (b < n)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) out[static_cast<size_t>(b) * 16 + gy * 4 + x] = lv[x];
+  }
+}
+
 }  // namespace gpu
 }  // namespace mivc
 
 using namespace mivc::gpu;
+
+extern "C" void mivc_launch_trellis_blocks(const int* w, int* out, int n, int qp, int mode, int skip_dc, void* stream) {
+  const int grid = mode == 0 ? (n + 63) / 64 : (n + 15) / 16;
+  hipLaunchKernelGGL(trellis_blocks, dim3(grid), dim3(64), 0, static_cast<hipStream_t>(stream), w, out, n, qp, mode,
+                     skip_dc);
+}
 
 extern "C" void mivc_launch_satd_blocks(const uint8_t* src, const uint8_t* pred, int* out, int n, int mode, void* stream) {
   hipLaunchKernelGGL(satd_blocks, dim3((n + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), src, pred, out, n,

@@ -92,6 +92,9 @@ class H264Params:
     b_adapt: int = 0
     # x264 --b-bias: > 0 places more B pictures (B costs * 100 / (120 + bias), run thresholds)
     b_bias: int = 0
+    # x264's intra-MB guards on the b-adapt decision (rc/badapt.py): P(i+2 | i) more than half
+    # intra keeps both pictures P, a closing P more than a third intra ends the B run
+    badapt_guard: bool = True
     # x264 seeds its motion search from the lookahead's lowres motion: the P search and both B
     # searches get one more candidate, the picture's lowres vector x 2 scaled to its reference
     # distance (when the lookahead ran on the coded MB grid)
@@ -169,6 +172,10 @@ class H264Params:
     # the next P); needs spatial direct (temporal direct's co-located motion would come from a B)
     pyramid: bool = False
     trellis_lambda: float = 1.0
+    # the same rate-distortion levels on the intra MBs' final encode (encode_intra.hip,
+    # lane-parallel h264_trellis.h grp_trellis4x4; x264 applies --trellis 1 to every MB):
+    # -1 = follow `trellis`, 0 = dead-zone quantisation (rounding 1/3), 1 / 2 as `trellis`
+    intra_trellis: int = -1
     # deblock non-reference B pictures even when neither metrics nor the reconstruction
     # are requested (x264 --full-recon); the bitstream does not depend on it
     full_recon: bool = False
@@ -235,6 +242,9 @@ class H264Params:
 
     def eff_t8x8(self) -> bool:
         return bool(self.t8x8 and self.cabac)
+
+    def eff_intra_trellis(self) -> int:
+        return int(self.trellis if self.intra_trellis < 0 else self.intra_trellis)
 
     def eff_partitions(self) -> bool:
         return bool(self.partitions and self.cabac)
@@ -774,7 +784,8 @@ class GpuH264Encoder:
         with stt("intra"):
             self.hip.encode_intra(B, wmb, hmb, sy, su, sv, py, pu, pv, P(self.qp), cqo, P(hdr), P(coef), P(self.nz),
                                   flag_ptr, count_ptr, P(self.err), int(self.p.i4x4 and trial), s, aq,
-                                  int(self.p.i8x8 and self.p.eff_t8x8() and trial), rt, NB, self.slice_rows)
+                                  int(self.p.i8x8 and self.p.eff_t8x8() and trial), rt, NB, self.slice_rows,
+                                  trellis=self.p.eff_intra_trellis(), trellis_lambda=float(self.p.trellis_lambda))
         if aq:
             # MBs without mb_qp_delta take QP_pred (clause 7.4.5): their records must say so
             # before deblocking reads every MB's QP
@@ -807,6 +818,7 @@ class GpuH264Encoder:
         cache: dict[str, list[PicPlan]] = {}
         plans = []
         multi = getattr(self, "_la_multi", None)
+        multi_intra = getattr(self, "_la_multi_intra", None) if self.p.badapt_guard else None
         adaptive = multi is not None and multi.shape[:2] == (self.B, F)
         if adaptive:
             from ..rc.badapt import b_adapt_types
@@ -815,7 +827,7 @@ class GpuH264Encoder:
             forced = forced | {d for d in range(1, F) if cuts_h[b, d]}
             if adaptive:
                 ty = b_adapt_types(self._la_costs[b, :, 1], multi[b], multi[b, :, 0], self.nb, self._la_blocks, forced,
-                                   int(self.p.b_bias))
+                                   int(self.p.b_bias), None if multi_intra is None else multi_intra[b])
             else:
                 ty = fixed_types(F, self.nb, forced)
             if ty not in cache:
@@ -1233,7 +1245,7 @@ class GpuH264Encoder:
         # MB-tree needs the lookahead's block grid to be the coded MB grid (no -s resize)
         use_mbtree = self.p.mbtree and lbw * lbh == self.nmb
         badapt = bool(self.p.b_adapt) and self.nb > 0 and y.shape[1] >= 3
-        multi = mbtree = None
+        multi = multi_intra = mbtree = None
         if use_mbtree:
             costs_d, mbtree = la.mbtree(y, MBTREE_STRENGTH)
             blk, mv = la.last_blk, la.last_mv
@@ -1243,14 +1255,16 @@ class GpuH264Encoder:
             costs_d, blk, mv = la.frame_costs(y), None, None
         if badapt:
             multi = la.multi_costs(y, blk, mv, min(7, self.nb + 1)).cpu().numpy()
+            multi_intra = la.last_multi_intra.cpu().numpy()
         costs = costs_d.cpu().numpy()
-        return dict(costs=costs, multi=multi, mbtree=mbtree, use_mbtree=use_mbtree, blocks=lbw * lbh,
+        return dict(costs=costs, multi=multi, multi_intra=multi_intra, mbtree=mbtree, use_mbtree=use_mbtree, blocks=lbw * lbh,
                     # lowres vectors on the MB grid: the search seeds (lowres_seed)
                     mv=mv if (mv is not None and self.p.lowres_seed and lbw * lbh == self.nmb) else None,
                     scenecuts=scenecut_flags(costs, float(self.p.scenecut)), shape=tuple(y.shape))
 
     def _apply_analysis(self, a: dict) -> None:
         self._la_costs, self._la_multi, self._mbtree = a["costs"], a["multi"], a["mbtree"]
+        self._la_multi_intra = a.get("multi_intra")
         self._la_mv, self._la_blocks, self._use_mbtree = a["mv"], a["blocks"], a["use_mbtree"]
         self._scenecuts = a["scenecuts"]
         self.stats["scenecuts"] = int(self._scenecuts.sum())
@@ -1410,7 +1424,7 @@ class GpuH264Encoder:
         qp_i, qp_p = self.p.frame_qps()
         self._scenecuts = None
         self._mbtree = None
-        self._la_multi = None
+        self._la_multi = self._la_multi_intra = None
         self._la_mv = None
         self._from_la = False
         if qps is None and self.p.crf is not None and self.p.lookahead:

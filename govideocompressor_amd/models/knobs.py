@@ -30,6 +30,7 @@ H264 = {
     "MIVC_LA_RANGE": "la_range",
     "MIVC_B_ADAPT": "b_adapt",
     "MIVC_B_BIAS": "b_bias",
+    "MIVC_BADAPT_GUARD": "badapt_guard",
     "MIVC_LA_SEED": "lowres_seed",
     "MIVC_B_ME_RANGE": "b_me_range",
     "MIVC_SKIP_REFINE": "skip_refine",
@@ -48,6 +49,7 @@ H264 = {
     "MIVC_TDIRECT_BIAS": "tdirect_bias",
     "MIVC_PYRAMID": "pyramid",
     "MIVC_TRELLIS_LAMBDA": "trellis_lambda",
+    "MIVC_INTRA_TRELLIS": "intra_trellis",
     "MIVC_REFS": "refs",
     "MIVC_REF_RANGE": "ref_range",
     "MIVC_REF_GATE": "ref_gate",

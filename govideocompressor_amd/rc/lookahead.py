@@ -17,6 +17,7 @@ import torch
 from ..ops import native
 
 RANGES = (4, 6, 8)
+INTRA_SHIFT = 40  # la_multi packs its intra block counts above the cost sums (lookahead.hip kLaIntraShift)
 
 
 class GpuLookahead:
@@ -119,7 +120,9 @@ class GpuLookahead:
         """x264 --b-adapt costs (lookahead.hip la_multi) of the batch whose lowres planes, block
         costs and distance-1 vectors the last :meth:`frame_costs` call produced: [B, F, 8] int64,
         column d = 2..max_dist the P cost at distance d, column 0 the B cost between the
-        neighbours (frame sums of min(intra, candidate))."""
+        neighbours (frame sums of min(intra, candidate)).  The number of lowres blocks that
+        chose intra in each (x264's ``i_intra_mbs``, the b-adapt guards) is left in
+        ``self.last_multi_intra`` ([B, F, 8] int64, same columns)."""
         B, F, h, w = y.shape
         if self._low is None or blk is None or mv is None:
             raise ValueError("multi_costs needs a preceding frame_costs(block_costs=True, block_mvs=True)")
@@ -128,7 +131,9 @@ class GpuLookahead:
         out = torch.empty((B * F, 8), dtype=torch.int64, device=self.dev)
         self.hip.lookahead_multi(self._low.data_ptr(), w, h, B * F, F, blk.data_ptr(), mv.data_ptr(), int(max_dist),
                                  int(search_range), out.data_ptr(), torch.cuda.current_stream(self.dev).cuda_stream)
-        return out.view(B, F, 8)
+        out = out.view(B, F, 8)
+        self.last_multi_intra = out >> INTRA_SHIFT
+        return out & ((1 << INTRA_SHIFT) - 1)
 
 
 def lookahead_reference(y: np.ndarray, search_range: int = 6) -> tuple[np.ndarray, np.ndarray]:
@@ -188,11 +193,13 @@ def lookahead_reference(y: np.ndarray, search_range: int = 6) -> tuple[np.ndarra
     return frame, blk
 
 
-def multi_reference(y: np.ndarray, search_range: int = 6, max_dist: int = 4, multi_range: int = 2) -> np.ndarray:
+def multi_reference(y: np.ndarray, search_range: int = 6, max_dist: int = 4, multi_range: int = 2,
+                    with_intra: bool = False):
     """Plain numpy model of ``la_multi`` (lookahead.hip): [B, F, 8] int64, column d = 2..max_dist
     the P cost at distance d, column 0 the B cost between the neighbours (frame sums of
     min(intra, candidate) over the lowres 8x8 blocks), from the same lowres planes, intra costs
-    and distance-1 vectors as :func:`lookahead_reference`."""
+    and distance-1 vectors as :func:`lookahead_reference`.  with_intra: also the intra block
+    counts of each (``GpuLookahead.last_multi_intra``), returned as a second array."""
     B, F, h, w = y.shape
     R, pad, MR = search_range, 16, multi_range
     lw, lh = w // 2, h // 2
@@ -226,6 +233,7 @@ def multi_reference(y: np.ndarray, search_range: int = 6, max_dist: int = 4, mul
 
     _, blk = lookahead_reference(y, search_range)
     out = np.zeros((B, F, 8), dtype=np.int64)
+    cnt = np.zeros((B, F, 8), dtype=np.int64)
     for b in range(B):
         for f in range(1, F):
             cur = low[b, f]
@@ -251,6 +259,7 @@ def multi_reference(y: np.ndarray, search_range: int = 6, max_dist: int = 4, mul
                         P = ref[Y0 + my:Y0 + my + 8, X0 + mx:X0 + mx + 8]
                         cst = satd(S - P) + 2 * (abs(mx - d * vx) + abs(my - d * vy)) + 2 * (abs(vx) + abs(vy))
                         out[b, f, d] += min(intra, cst)
+                        cnt[b, f, d] += intra < cst
                     if f + 1 < F:
                         r1 = low[b, f + 1]
                         mx, my = search(r1, S, X0, Y0, -vx, -vy, MR)
@@ -261,4 +270,5 @@ def multi_reference(y: np.ndarray, search_range: int = 6, max_dist: int = 4, mul
                         Pb = (P0 + P1 + 1) >> 1
                         cbi = satd(S - Pb) + 2 * (abs(mx) + abs(my) + abs(vx) + abs(vy))
                         out[b, f, 0] += min(min(intra, inter1), min(c1, cbi))
-    return out
+                        cnt[b, f, 0] += intra < min(inter1, c1, cbi)
+    return (out, cnt) if with_intra else out

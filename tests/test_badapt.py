@@ -72,3 +72,20 @@ def test_b_costs_are_scaled_like_x264():
     --b-bias 0): a B that costs 125 against a 120 P pair still wins (0.833 * 45 + 80 < 120)."""
     p1, pd, bc = _costs(4, lambda d: {1: 60.0, 2: 80.0}.get(d, 900.0), b_cost=45.0)
     assert b_adapt_types(p1, pd, bc, 3, 100)[:3] == "IBP"
+
+
+def test_intra_guards_force_p_like_x264():
+    """x264's i_intra_mbs checks: a P two pictures away that is mostly intra (> mb / 2) keeps
+    both pictures P; a closing P more than a third intra ends a B run early."""
+    p1, pd, bc = _costs(13, lambda d: 20.0 + 2 * d, b_cost=8.0)
+    assert b_adapt_types(p1, pd, bc, 3, 100) == "IBBBPBBBPBBBP"
+    intra = np.zeros((13, 8), np.int64)
+    intra[2, 2] = 51  # P(2 | 0) mostly intra: 1 and 2 stay P
+    t = b_adapt_types(p1, pd, bc, 3, 100, pd_intra=intra)
+    assert t.startswith("IPP"), t
+    intra[:] = 0
+    intra[4, 4] = 34  # closing the run at 4 from 0 is a third intra: the run stops at 2 B
+    t = b_adapt_types(p1, pd, bc, 3, 100, pd_intra=intra)
+    assert t.startswith("IBBP"), t
+    intra[4, 4] = 33  # not more than a third: unchanged
+    assert b_adapt_types(p1, pd, bc, 3, 100, pd_intra=intra) == "IBBBPBBBPBBBP"

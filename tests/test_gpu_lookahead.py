@@ -150,8 +150,10 @@ def test_lookahead_multi_matches_reference(shape):
     yd = torch.from_numpy(y).cuda()
     _, blk, mv = la.frame_costs(yd, block_costs=True, block_mvs=True)
     got = la.multi_costs(yd, blk, mv, 4).cpu().numpy()
-    ref = multi_reference(y, 6, 4)
+    got_intra = la.last_multi_intra.cpu().numpy()
+    ref, ref_intra = multi_reference(y, 6, 4, with_intra=True)
     assert np.array_equal(got, ref), (got[..., :5], ref[..., :5])
+    assert np.array_equal(got_intra, ref_intra), (got_intra[..., :5], ref_intra[..., :5])
     assert (ref[:, 2:, 2] > 0).all() and (ref[:, 1:-1, 0] > 0).all()
 
 

@@ -36,6 +36,9 @@ CONFIGS = {
     "pyramid": dict(b_adapt=1, pyramid=True, direct="spatial"),
     "bias20": dict(b_adapt=1, b_bias=20),
     "bias40": dict(b_adapt=1, b_bias=40),
+    "bias70": dict(b_adapt=1, b_bias=70),
+    "bias100": dict(b_adapt=1, b_bias=100),
+    "badapt_ng": dict(b_adapt=1, badapt_guard=False),  # without x264's intra-MB guards
     "slices4": dict(slices=4),
     "noseed": dict(lowres_seed=False),
     "trellis1": dict(trellis=1),  # round 3's trellis scope (4x4 luma only)
@@ -61,6 +64,7 @@ CONFIGS = {
     "refgate3000": dict(ref_gate=3000),
     "tl07": dict(trellis_lambda=0.7),
     "tl14": dict(trellis_lambda=1.4),
+    "itr0": dict(intra_trellis=0),  # dead-zone levels on intra MBs (round 4)
     # fast spatial direct with the fixed GOP pattern: exact motion re-predicted (tol -1, round 4's
     # first version) / estimate kept as explicit motion beyond 0 / 4 quarter samples; b-pyramid
     "sp_repredict": dict(direct="spatial", spatial_fix_tol=-1),
