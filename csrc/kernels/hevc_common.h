@@ -352,7 +352,8 @@ __device__ __forceinline__ void filter_refs(const int* p, int* q, int n, int bd,
 
 // one predicted sample (8.4.4.2.4 - 8.4.4.2.6); dc: precomputed DC value (mode 1);
 // edge: luma block smaller than 32 (DC / pure horizontal / pure vertical boundary filters)
-__device__ __forceinline__ int intra_pred_sample(const int* p, int n, int log2n, int mode, int x, int y, int dc,
+template <typename RT>
+__device__ __forceinline__ int intra_pred_sample(const RT* p, int n, int log2n, int mode, int x, int y, int dc,
                                                  bool edge, int maxv) {
   const int c = 2 * n;
   auto L = [&](int yy) { return p[c - 1 - yy]; };
@@ -395,7 +396,8 @@ __device__ __forceinline__ int intra_pred_sample(const int* p, int n, int log2n,
 // angular interpolation position is the same for all four samples and 5 reference loads
 // serve them (the Hadamard SATD of a block equals that of its transpose).  *transposed tells
 // the caller which layout was produced.
-__device__ __forceinline__ void intra_pred4(const int* p, int n, int log2n, int mode, int bx, int by, int g, int dc,
+template <typename RT>
+__device__ __forceinline__ void intra_pred4(const RT* p, int n, int log2n, int mode, int bx, int by, int g, int dc,
                                             bool edge, int maxv, int (&o)[4], bool* transposed) {
   const int c = 2 * n;
   auto L = [&](int yy) { return p[c - 1 - yy]; };

@@ -170,6 +170,24 @@ struct InterShared {
   uint16_t pred[32 * 32];
 };
 
+// The default instance's LDS (15.8 KB with the DCT matrix instead of 26.5 KB: 10 workgroups
+// per CU instead of 6): the motion-compensation window and horizontal pass live only until
+// the residual is formed, the transform scratch S only after, so they share storage; the
+// 16-bit intermediates (horizontal pass, the list-0 prediction of bi-prediction) are what
+// the standard bounds them to (8.5.3.3.3: 14-bit predSamples, 16-bit first stage)
+struct InterSharedLean {
+  union {
+    struct {
+      uint16_t win[39 * 39];
+      int16_t tmp[39 * 32];
+    };
+    int S[32 * 32];
+  };
+  int R[32 * 32];
+  int16_t R2[32 * 32];  // list-0 prediction samples of a bi-predicted block
+  uint16_t pred[32 * 32];
+};
+
 // rate proxy of a block's levels (bits): ~3 + 2 log2|l| per non-zero level (wave reduction)
 __device__ __forceinline__ int level_bits(const int16_t* lev, int stride, int n) {
   int b = 0;
@@ -182,7 +200,8 @@ __device__ __forceinline__ int level_bits(const int16_t* lev, int stride, int n)
 }
 
 // SSD of clip(pred + R) against the source block (wave reduction; 64-bit: 32x32 at 10 bits)
-__device__ __forceinline__ long long recon_ssd(const InterShared& S, const int* R, const uint16_t* src, int pw, int bx,
+template <typename SH>
+__device__ __forceinline__ long long recon_ssd(const SH& S, const int* R, const uint16_t* src, int pw, int bx,
                                                int by, int n, int maxv) {
   long long e = 0;
   for (int i = lane_id(); i < n * n; i += 64) {
@@ -198,9 +217,9 @@ __device__ __forceinline__ long long recon_ssd(const InterShared& S, const int* 
 
 // motion-compensated prediction samples predSamplesLX (14-bit intermediate, 8.5.3.3.3
 // fractional interpolation) of one n x n block of a component into dst[y * n + x]
-template <int NT>
-__device__ __forceinline__ void mc_inter(InterShared& S, const uint16_t* ref, int pw, int ph, int bx, int by, int n,
-                                         int mvx, int mvy, int bd, int* dst) {
+template <int NT, typename SH, typename DT>
+__device__ __forceinline__ void mc_inter(SH& S, const uint16_t* ref, int pw, int ph, int bx, int by, int n,
+                                         int mvx, int mvy, int bd, DT* dst) {
   const int lane = lane_id();
   const int fb = NT == 8 ? 2 : 3;  // fraction bits
   const int half = NT / 2 - 1;     // taps before the sample
@@ -222,7 +241,7 @@ __device__ __forceinline__ void mc_inter(InterShared& S, const uint16_t* ref, in
       int s = 0;
 #pragma unroll
       for (int k = 0; k < NT; ++k) s += tap(fx, k) * S.win[r * wn + x + k];
-      S.tmp[r * 32 + x] = s >> sh1;
+      S.tmp[r * 32 + x] = static_cast<std::remove_reference_t<decltype(S.tmp[0])>>(s >> sh1);
     }
     wave_sync();
   }
@@ -247,15 +266,15 @@ __device__ __forceinline__ void mc_inter(InterShared& S, const uint16_t* ref, in
       for (int k = 0; k < NT; ++k) s += tap(fy, k) * S.tmp[(y + k) * 32 + x];
       v = s >> 6;
     }
-    dst[i] = v;
+    dst[i] = static_cast<DT>(v);
   }
   wave_sync();
 }
 
 // prediction of one n x n block of a component into S.pred: default weighted sample
 // prediction (8.5.3.3.4.2) of one list, or the average of both (bi-prediction)
-template <int NT>
-__device__ __forceinline__ void mc_block(InterShared& S, const uint16_t* ref0, const uint16_t* ref1, int pw, int ph,
+template <int NT, typename SH>
+__device__ __forceinline__ void mc_block(SH& S, const uint16_t* ref0, const uint16_t* ref1, int pw, int ph,
                                          int bx, int by, int n, int dir, int mvx, int mvy, int mv1x, int mv1y, int bd,
                                          int ww = 0, int wo = 0) {
   const int lane = lane_id();
@@ -292,7 +311,7 @@ __device__ __forceinline__ void mc_block(InterShared& S, const uint16_t* ref0, c
 // the default instance)
 template <bool TSPLIT>
 __global__ __launch_bounds__(64) void hevc_inter_cu(HevcInterArgs a) {
-  __shared__ InterShared S;
+  __shared__ typename std::conditional<TSPLIT, InterShared, InterSharedLean>::type S;
   __shared__ hv::DctLds D;
   const HevcGeom& g = a.g;
   const int task = blockIdx.x, slot = blockIdx.y;
@@ -340,49 +359,54 @@ __global__ __launch_bounds__(64) void hevc_inter_cu(HevcInterArgs a) {
       const int y = i / bs, x = i - y * bs;
       const int r = static_cast<int>(src[static_cast<size_t>(by + y) * pw + bx + x]) - S.pred[i];
       S.R[y * 32 + x] = r;
-      if (c == 0) S.R2[y * 32 + x] = r;
+      if (TSPLIT && c == 0) S.R2[y * 32 + x] = r;
     }
     wave_sync();
     const int l2 = c ? lg - 1 : lg;
     const int qc = c ? qpc : qpl;
-    if (TSPLIT && c == 0) {
-      const bool nz = hv::transform_quant_block(D, S.R, S.S, lev, pw, hv::TqParams{l2, bd, qc, false, false, a.sdh ? 0 : -1});
-      for (int k = 0; k < 4; ++k) cbfq[k] = nz;
-      {
-        bool nzq[4];
-        for (int k = 0; k < 4; ++k) {
-          const int o = (k >> 1) * h * 32 + (k & 1) * h;
-          nzq[k] = hv::transform_quant_block(D, S.R2 + o, S.S, S.lev2 + o, 32, hv::TqParams{l2 - 1, bd, qc, false, false, a.sdh ? 0 : -1});
-        }
-        const bool any = nzq[0] || nzq[1] || nzq[2] || nzq[3];
-        if (any) {
-          // lambda for SSD (HM: 0.57 * 2^((QP - 12) / 3), at the coded bit depth)
-          const float lam = 0.57f * exp2f((qpy - 12) / 3.0f) * static_cast<float>(1 << (2 * (bd - 8)));
-          const long long d1 = recon_ssd(S, S.R, src, pw, bx, by, n, maxv);
-          const long long d4 = recon_ssd(S, S.R2, src, pw, bx, by, n, maxv);
-          const int b1 = level_bits(lev, pw, n) + (nz ? 2 * lg + 2 : 0);
-          const int b4 = level_bits(S.lev2, 32, n) + 4 + (nzq[0] + nzq[1] + nzq[2] + nzq[3]) * (2 * lg);
-          split = static_cast<float>(d4) + lam * b4 < static_cast<float>(d1) + lam * b1;
-        }
-        if (split) {
-          for (int i = lane; i < n * n; i += 64) {
-            const int y = i / n, x = i - y * n;
-            lev[y * pw + x] = S.lev2[y * 32 + x];
-            S.R[y * 32 + x] = S.R2[y * 32 + x];
+    bool coded = false;
+    if constexpr (TSPLIT) {
+      coded = c == 0 || split;
+      if (c == 0) {
+        const bool nz = hv::transform_quant_block(D, S.R, S.S, lev, pw, hv::TqParams{l2, bd, qc, false, false, a.sdh ? 0 : -1});
+        for (int k = 0; k < 4; ++k) cbfq[k] = nz;
+        {
+          bool nzq[4];
+          for (int k = 0; k < 4; ++k) {
+            const int o = (k >> 1) * h * 32 + (k & 1) * h;
+            nzq[k] = hv::transform_quant_block(D, S.R2 + o, S.S, S.lev2 + o, 32, hv::TqParams{l2 - 1, bd, qc, false, false, a.sdh ? 0 : -1});
           }
-          for (int k = 0; k < 4; ++k) cbfq[k] = nzq[k];
+          const bool any = nzq[0] || nzq[1] || nzq[2] || nzq[3];
+          if (any) {
+            // lambda for SSD (HM: 0.57 * 2^((QP - 12) / 3), at the coded bit depth)
+            const float lam = 0.57f * exp2f((qpy - 12) / 3.0f) * static_cast<float>(1 << (2 * (bd - 8)));
+            const long long d1 = recon_ssd(S, S.R, src, pw, bx, by, n, maxv);
+            const long long d4 = recon_ssd(S, S.R2, src, pw, bx, by, n, maxv);
+            const int b1 = level_bits(lev, pw, n) + (nz ? 2 * lg + 2 : 0);
+            const int b4 = level_bits(S.lev2, 32, n) + 4 + (nzq[0] + nzq[1] + nzq[2] + nzq[3]) * (2 * lg);
+            split = static_cast<float>(d4) + lam * b4 < static_cast<float>(d1) + lam * b1;
+          }
+          if (split) {
+            for (int i = lane; i < n * n; i += 64) {
+              const int y = i / n, x = i - y * n;
+              lev[y * pw + x] = S.lev2[y * 32 + x];
+              S.R[y * 32 + x] = S.R2[y * 32 + x];
+            }
+            for (int k = 0; k < 4; ++k) cbfq[k] = nzq[k];
+          }
+          wave_sync();
         }
-        wave_sync();
+      } else if (split) {
+        const int hc = bs >> 1;
+        for (int k = 0; k < 4; ++k) {
+          const int o = (k >> 1) * hc * 32 + (k & 1) * hc;
+          const bool nz = hv::transform_quant_block(D, S.R + o, S.S, lev + (k >> 1) * hc * pw + (k & 1) * hc, pw,
+                                                    hv::TqParams{l2 - 1, bd, qc, false, false, a.sdh ? 0 : -1});
+          cbfq[k] |= nz << c;
+        }
       }
-    } else if (TSPLIT && split) {
-      const int hc = bs >> 1;
-      for (int k = 0; k < 4; ++k) {
-        const int o = (k >> 1) * hc * 32 + (k & 1) * hc;
-        const bool nz = hv::transform_quant_block(D, S.R + o, S.S, lev + (k >> 1) * hc * pw + (k & 1) * hc, pw,
-                                                  hv::TqParams{l2 - 1, bd, qc, false, false, a.sdh ? 0 : -1});
-        cbfq[k] |= nz << c;
-      }
-    } else {
+    }
+    if (!coded) {
       const bool nz = hv::transform_quant_block(D, S.R, S.S, lev, pw, hv::TqParams{l2, bd, qc, false, false, a.sdh ? 0 : -1});
       for (int k = 0; k < 4; ++k) cbfq[k] |= nz << c;
     }

@@ -79,12 +79,12 @@ constexpr int kCuCount = 21;  // 1 x 32, 4 x 16, 16 x 8
 constexpr int kPuCount = 64;  // PART_NxN: four 4x4 PUs of each 8x8 CU (z-order)
 struct AnalyzeShared {
   int16_t ext[65 * 65];        // source samples, x, y in [-1, 63] relative to the CTB
-  int refs[2][917];            // per CU: unfiltered / filtered reference arrays
+  int16_t refs[2][917];        // per CU: unfiltered / filtered reference arrays (samples: 16 bits)
   int cost[kCuCount][36];
   uint8_t done[kCuCount][36];  // (CU, mode) evaluated
   int dc[kCuCount];
   int best_mode[kCuCount], best_cost[kCuCount];
-  int refs4[kPuCount][17];     // 4x4 PUs: reference arrays (no filtering at 4x4)
+  int16_t refs4[kPuCount][17]; // 4x4 PUs: reference arrays (no filtering at 4x4)
   int cost4[kPuCount][36];
   uint8_t done4[kPuCount][36];
   int dc4[kPuCount];
@@ -189,7 +189,7 @@ __global__ __launch_bounds__(256, 4) void hevc_intra_analyze(HevcIntraArgs a) {
     cu_of(tid, &cx, &cy, &n, &off);
     const int zc = 4 * zorder8(cx >> 3, cy >> 3);
     const int E = 4 * n + 1;
-    int* p = S.refs[0] + off;
+    int16_t* p = S.refs[0] + off;
     int first = -1;
     for (int i = 0; i < E; ++i) {
       int x, y;
@@ -209,7 +209,7 @@ __global__ __launch_bounds__(256, 4) void hevc_intra_analyze(HevcIntraArgs a) {
         if (p[i] < 0) p[i] = p[i - 1];
     }
     // filtered copy (8.4.4.2.3; strong smoothing for 32x32)
-    int* q = S.refs[1] + off;
+    int16_t* q = S.refs[1] + off;
     const int c = 2 * n, tl = p[c], bl = p[0], tr = p[E - 1];
     const bool bi = n == 32 && abs(tl + tr - 2 * p[c + n]) < (1 << (bd - 5)) && abs(tl + bl - 2 * p[c - n]) < (1 << (bd - 5));
     for (int i = 0; i < E; ++i) {
@@ -226,7 +226,7 @@ __global__ __launch_bounds__(256, 4) void hevc_intra_analyze(HevcIntraArgs a) {
     const int pu = tid - 64;
     int px, py;
     pu_of(pu, &px, &py);
-    int* p = S.refs4[pu];
+    int16_t* p = S.refs4[pu];
     int first = -1;
     for (int i = 0; i < 17; ++i) {
       int x, y;
@@ -282,7 +282,7 @@ __global__ __launch_bounds__(256, 4) void hevc_intra_analyze(HevcIntraArgs a) {
     int cx, cy, n, off;
     cu_of(c, &cx, &cy, &n, &off);
     const int lg = n == 32 ? 5 : (n == 16 ? 4 : 3);
-    const int* p = S.refs[hv::intra_filter_flag(mode, n) ? 1 : 0] + off;
+    const int16_t* p = S.refs[hv::intra_filter_flag(mode, n) ? 1 : 0] + off;
     const int b4 = lane & 3, row = lane >> 4;
     const int X = bx * 8 + (b4 & 1) * 4, Y = by * 8 + (b4 >> 1) * 4;  // the 4x4 block in the CU
     int pr[4], r[4];
@@ -306,7 +306,7 @@ __global__ __launch_bounds__(256, 4) void hevc_intra_analyze(HevcIntraArgs a) {
   auto eval4_q = [&](int pu, int mode, bool active) {
     int px, py;
     pu_of(pu, &px, &py);
-    const int* p = S.refs4[pu];
+    const int16_t* p = S.refs4[pu];
     const int row = lane >> 4;
     int pr[4], r[4];
     bool tr;
