@@ -1578,11 +1578,18 @@ __global__ __launch_bounds__(64) void hevc_b_merge(HevcBArgs a) {
   if (a0 && a1 && same(dA1, wA1, dA0, wA0)) a0 = false;
   if (b2 && ((a1 && same(dA1, wA1, dB2, wB2)) || (av_b1 && same(dB1, wB1, dB2, wB2)))) b2 = false;
   if (static_cast<int>(a0) + a1 + b0 + b1 == 4) b2 = false;
+  // the list lives in registers: every index below is a compile-time one (selects over the
+  // six entries), so no scratch memory
   auto push = [&](int d, const int* w) {
-    if (nk >= 6) return;
-    kd[nk] = d;
-    for (int c = 0; c < 4; ++c) kv[nk][c] = w[c];
-    ++nk;
+#pragma unroll
+    for (int t = 0; t < 6; ++t) {
+      if (t == nk) {
+        kd[t] = d;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) kv[t][c] = w[c];
+      }
+    }
+    nk += nk < 6;
   };
   if (a1) push(dA1, wA1);
   if (b1) push(dB1, wB1);
@@ -1599,8 +1606,10 @@ __global__ __launch_bounds__(64) void hevc_b_merge(HevcBArgs a) {
   if (a.bslice && orig > 1 && orig < maxc) {
     const int l0i[12] = {0, 1, 0, 2, 1, 2, 0, 3, 1, 3, 2, 3};
     const int l1i[12] = {1, 0, 2, 0, 2, 1, 3, 0, 3, 1, 3, 2};
-    for (int c = 0; c < orig * (orig - 1) && nk < maxc; ++c) {
-      const int i0 = l0i[c], i1 = l1i[c];
+#pragma unroll
+    for (int c = 0; c < 12; ++c) {
+      if (c >= orig * (orig - 1) || nk >= maxc) break;
+      const int i0 = l0i[c], i1 = l1i[c];  // compile-time after unrolling
       if ((kd[i0] & 1) && (kd[i1] & 2)) {
         const int w[4] = {kv[i0][0], kv[i0][1], kv[i1][2], kv[i1][3]};
         push(3, w);
@@ -1629,8 +1638,11 @@ __global__ __launch_bounds__(64) void hevc_b_merge(HevcBArgs a) {
   for (int y = 0; y < 4; ++y)
     src[y] = *reinterpret_cast<const uint32_t*>(a.src_y + yo + static_cast<size_t>(Y + y) * g.W + X);
   int best = c_cur, bbits = a.bits[o], bj = -1;
-  for (int j = 0; j < nk; ++j) {
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    if (j >= nk) break;
     bool dup = false;  // the same motion earlier in the list: never cheaper
+#pragma unroll
     for (int i = 0; i < j; ++i) dup = dup || same(kd[i], kv[i], kd[j], kv[j]);
     if (dup) continue;
     int sat = satd_cur;
@@ -1651,8 +1663,17 @@ __global__ __launch_bounds__(64) void hevc_b_merge(HevcBArgs a) {
   if (lane == 0) {
     int16_t* m = a.mvb_out + o * 4;
     if (bj >= 0) {
-      for (int c = 0; c < 4; ++c) m[c] = static_cast<int16_t>(kv[bj][c]);
-      a.dir_out[o] = static_cast<uint8_t>(kd[bj]);
+      int bd = 0, bw[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int t = 0; t < 6; ++t) {
+        if (t == bj) {
+          bd = kd[t];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) bw[c] = kv[t][c];
+        }
+      }
+      for (int c = 0; c < 4; ++c) m[c] = static_cast<int16_t>(bw[c]);
+      a.dir_out[o] = static_cast<uint8_t>(bd);
     } else {
       for (int c = 0; c < 4; ++c) m[c] = cvp[c];
       a.dir_out[o] = static_cast<uint8_t>(cd);

@@ -71,6 +71,8 @@ void mivc_launch_encode_inter(int B, int wmb, int hmb, const uint8_t* src_y, con
                               int bmode, int t8, const int16_t* mv8, void* stream, const int* w1, int nref,
                               const uint8_t* const* xref_u, const uint8_t* const* xref_v, const int8_t* mref,
                               const int* wp, int trellis, float trellis_lambda, const void* route, int nbuf);
+void mivc_launch_wp_stats16(const uint16_t* y, const uint16_t* u, const uint16_t* v, int w, int h, int npics,
+                            unsigned long long* out, void* stream);
 void mivc_launch_wp_stats(const uint8_t* y, const uint8_t* u, const uint8_t* v, int w, int h, int npics,
                           unsigned long long* out, void* stream);
 void mivc_launch_wp_src(const uint8_t* src, uint8_t* dst, const int* wt, int B, long long plane_bytes, void* stream);
@@ -385,6 +387,11 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("w1") = std::vector<int>{32}, py::arg("xref_u") = std::vector<uintptr_t>{},
         py::arg("xref_v") = std::vector<uintptr_t>{}, py::arg("mref") = 0, py::arg("wp") = 0, py::arg("trellis") = 0,
         py::arg("trellis_lambda") = 1.0f, py::arg("route") = 0, py::arg("nbuf") = 0);
+  m.def("wp_stats16", [](uintptr_t y, uintptr_t u, uintptr_t v, int w, int h, int npics, uintptr_t out, uintptr_t stream) {
+    if (w % 2 || h % 2 || npics <= 0) throw std::invalid_argument("wp_stats16: even picture sizes, npics > 0");
+    mivc_launch_wp_stats16(P<uint16_t>(y), P<uint16_t>(u), P<uint16_t>(v), w, h, npics, P<unsigned long long>(out),
+                           S(stream));
+  });
   m.def("wp_stats", [](uintptr_t y, uintptr_t u, uintptr_t v, int w, int h, int npics, uintptr_t out, uintptr_t stream) {
     if (w % 2 || h % 2 || (w * h) % 4) throw std::invalid_argument("wp_stats: even picture sizes");
     mivc_launch_wp_stats(P<uint8_t>(y), P<uint8_t>(u), P<uint8_t>(v), w, h, npics, P<unsigned long long>(out),

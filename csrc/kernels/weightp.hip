@@ -77,6 +77,42 @@ __global__ __launch_bounds__(256) void wp_stats(const uint8_t* __restrict__ y, c
   }
 }
 
+// The same statistics of 16-bit samples (Main 10 input, int16 planes holding 0..1023)
+__global__ __launch_bounds__(256) void wp_stats16(const uint16_t* __restrict__ y, const uint16_t* __restrict__ u,
+                                                  const uint16_t* __restrict__ v, int w, int h,
+                                                  unsigned long long* __restrict__ out) {
+  const int pic = blockIdx.y;
+  const size_t ny = static_cast<size_t>(w) * h, nc = ny / 4;
+  const uint16_t* P[3] = {y + pic * ny, u + pic * nc, v + pic * nc};
+  const size_t N[3] = {ny, nc, nc};
+  __shared__ unsigned long long red[6][4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const size_t per = (N[c] + gridDim.x - 1) / gridDim.x;
+    const size_t i0 = blockIdx.x * per, i1 = min(N[c], i0 + per);
+    unsigned long long s = 0, s2 = 0;
+    for (size_t i = i0 + threadIdx.x; i < i1; i += 256) {
+      const unsigned int b = P[c][i];
+      s += b;
+      s2 += b * b;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      s += __shfl_xor(s, off, 64);
+      s2 += __shfl_xor(s2, off, 64);
+    }
+    if (lane == 0) {
+      red[2 * c][wv] = s;
+      red[2 * c + 1][wv] = s2;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const unsigned long long t = red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] + red[threadIdx.x][3];
+    atomicAdd(out + static_cast<size_t>(pic) * 6 + threadIdx.x, t);
+  }
+}
+
 // wt: [B, 3] (w, o, log2 denominator) of the luma weight per slot; w == 1 << d && o == 0:
 // identity (plain copy)
 __global__ __launch_bounds__(256) void wp_src(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
@@ -116,6 +152,14 @@ extern "C" void mivc_launch_wp_stats(const uint8_t* y, const uint8_t* u, const u
   (void)hipMemsetAsync(out, 0, static_cast<size_t>(npics) * 6 * sizeof(unsigned long long), s);
   const int chunks = max(1, min(64, (w * h) / (256 * 64)));
   hipLaunchKernelGGL(wp_stats, dim3(chunks, npics), dim3(256), 0, s, y, u, v, w, h, out);
+}
+
+extern "C" void mivc_launch_wp_stats16(const uint16_t* y, const uint16_t* u, const uint16_t* v, int w, int h,
+                                       int npics, unsigned long long* out, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  (void)hipMemsetAsync(out, 0, static_cast<size_t>(npics) * 6 * sizeof(unsigned long long), s);
+  const int chunks = max(1, min(64, (w * h) / (256 * 64)));
+  hipLaunchKernelGGL(wp_stats16, dim3(chunks, npics), dim3(256), 0, s, y, u, v, w, h, out);
 }
 
 extern "C" void mivc_launch_wp_src(const uint8_t* src, uint8_t* dst, const int* wt, int B, long long plane_bytes,

@@ -116,14 +116,15 @@ class HevcParams:
     # x265 --weightp (its default): explicit weights of a P picture's reference where the
     # source statistics say the brightness or contrast changed (fades, flashes): weight =
     # sqrt(var_cur / var_ref) over 2^6, offset = mean_cur - weight * mean_ref, per component,
-    # used when the luma mean moved >= wp_min_mean levels or the contrast >= wp_min_scale.
-    # 8-bit input (Main 10: off)
+    # used when the luma mean moved >= wp_min_mean levels (8-bit scale) or the contrast >=
+    # wp_min_scale.  Main 10 too: statistics of the 16-bit planes (weightp.hip wp_stats16),
+    # offsets coded in 8-bit units as the standard scales them
     weightp: bool = True
     wp_min_mean: float = 2.0
     wp_min_scale: float = 0.08
 
     def eff_weightp(self) -> bool:
-        return bool(self.weightp and self.bit_depth == 8 and not self.intra_only)
+        return bool(self.weightp and not self.intra_only)
 
     def eff_bframes(self) -> int:
         return 0 if (self.intra_only or self.keyint > 0) else max(0, int(self.bframes))
@@ -493,18 +494,23 @@ class GpuHevcEncoder:
         of the two source pictures' planes).  Returns {step: (host rows [B] of [w, o] x 3 or
         None, device int16 [B, 6] with weight 0 = not weighted, device int32 [B, 3] luma
         (w, o, log2) for the search's inverse-weighted source)}."""
-        if not self.p.eff_weightp() or y.dtype != torch.uint8:
+        if not self.p.eff_weightp():
             return {}
         steps = [(t, pic) for t, pic in enumerate(plan) if pic.kind == "P"]
         if not steps:
             return {}
         B, F, h, w = y.shape
         st = torch.empty((B, F, 6), dtype=torch.int64, device=self.dev)
-        self.hip.wp_stats(y.data_ptr(), u.data_ptr(), v.data_ptr(), w, h, B * F, st.data_ptr(), self._stream())
+        stats = self.hip.wp_stats if y.dtype == torch.uint8 else self.hip.wp_stats16
+        stats(y.data_ptr(), u.data_ptr(), v.data_ptr(), w, h, B * F, st.data_ptr(), self._stream())
         sh = st.cpu().numpy().astype(np.float64)
         n = np.array([w * h, w * h / 4, w * h / 4])
-        mean = sh[..., 0::2] / n
-        var = np.maximum(sh[..., 1::2] / n - mean ** 2, 0.0)
+        # weights are unit-free; offsets are coded in 8-bit units (7.4.7.3, no high-precision
+        # offsets: the decoder scales them by 2^(BitDepth - 8)), so 10-bit input is measured
+        # at 8-bit scale
+        unit = 1.0 if y.dtype == torch.uint8 else float(1 << (self.p.bit_depth - 8))
+        mean = sh[..., 0::2] / n / unit
+        var = np.maximum(sh[..., 1::2] / n / unit ** 2 - mean ** 2, 0.0)
         out = {}
         for t, pic in steps:
             m1, m0 = mean[:, pic.d], mean[:, pic.l0]

@@ -288,6 +288,26 @@ def test_gpu_hevc_weightp_fade_matches_decoder(host):
     assert sizes[True] < sizes[False], sizes
 
 
+def test_gpu_hevc_weightp_main10_fade_matches_decoder(host):
+    """Main 10 weightp: statistics of the 16-bit planes (wp_stats16), offsets coded in 8-bit
+    units and scaled by 4 in the prediction -- GPU reconstruction bit-exact with the CPU
+    decoder, and the weighted stream smaller than the unweighted one."""
+    from govideocompressor_amd.models.h264_gpu import synth_clip
+    from govideocompressor_amd.models.hevc_gpu import GpuHevcEncoder, HevcParams
+    y, u, v = synth_clip(2, 8, 192, 128, seed=9, kind="fade", bit_depth=10)
+    sizes = {}
+    for wp in (False, True):
+        enc = GpuHevcEncoder(HevcParams(width=192, height=128, crf=27.0, bframes=0, weightp=wp, bit_depth=10), slots=2)
+        res = enc.encode(y, u, v, keep_recon=True)
+        rec = enc.last_recon
+        if wp:
+            assert enc.stats.get("weightp_pictures", 0) > 0
+            _compare(host, res, rec)
+        sizes[wp] = sum(len(r.bitstream) for r in res)
+        enc.close()
+    assert sizes[True] < sizes[False], sizes
+
+
 def test_gpu_hevc_weightp_fade_to_flat_matches_decoder(host):
     """A fade to a flat picture: the current plane's variance collapses, so the luma / chroma
     weight quantises towards 0.  The slot must stay weighted (weight >= 1, the kernels read 0 as
