@@ -328,21 +328,27 @@ MIVC_HD int cabac_b_code(const MbHeader& h) {
 
 // Partition layout of an inter MB kind: np partitions starting at quadrants qfirst[],
 // width w4[] (4x4 units), shape 0 generic / 1 16x8 / 2 8x16, quadrant masks pm[].
+// Partitions of an inter MB: np partitions of one shape (0: 16x16 when np == 1, else 8x8
+// quadrants; 1: 16x8; 2: 8x16).  Per-partition values are computed, not tabulated: an array
+// indexed by the partition loop counter made the GPU coder keep the struct in scratch memory.
 struct CabacParts {
   int np, shape;
-  int qfirst[4], w4[4], pm[4];
+  MIVC_HD int qfirst(int p) const { return shape == 1 ? 2 * p : p; }  // first quadrant
+  MIVC_HD int w4(int p) const { (void)p; return np == 1 || shape == 1 ? 4 : 2; }  // width in 4x4 blocks
+  MIVC_HD int pm(int p) const {  // quadrant mask
+    return np == 1 ? 0xF : (shape == 1 ? (p ? 0xC : 0x3) : (shape == 2 ? (p ? 0xA : 0x5) : 1 << p));
+  }
 };
 MIVC_HD CabacParts cabac_parts(int kind) {
   CabacParts p{};
   if (kind == MBK_P16x16 || kind == MBK_B16x16 || kind == MBK_PSKIP) {
-    p.np = 1; p.shape = 0; p.qfirst[0] = 0; p.w4[0] = 4; p.pm[0] = 0xF;
+    p.np = 1; p.shape = 0;
   } else if (kind == MBK_P16x8 || kind == MBK_B16x8) {
-    p.np = 2; p.shape = 1; p.qfirst[0] = 0; p.qfirst[1] = 2; p.w4[0] = p.w4[1] = 4; p.pm[0] = 0x3; p.pm[1] = 0xC;
+    p.np = 2; p.shape = 1;
   } else if (kind == MBK_P8x16 || kind == MBK_B8x16) {
-    p.np = 2; p.shape = 2; p.qfirst[0] = 0; p.qfirst[1] = 1; p.w4[0] = p.w4[1] = 2; p.pm[0] = 0x5; p.pm[1] = 0xA;
+    p.np = 2; p.shape = 2;
   } else {
     p.np = 4; p.shape = 0;
-    for (int q = 0; q < 4; ++q) { p.qfirst[q] = q; p.w4[q] = 2; p.pm[q] = 1 << q; }
   }
   return p;
 }
@@ -515,20 +521,20 @@ MIVC_HD void cabac_prepare_mb(const CabacSliceInfo& si, const MbHeader* hdr, int
     for (int l = 0; l < 2; ++l) {
       int done = 0;
       for (int p = 0; p < P.np; ++p) {
-        const int q = P.qfirst[p];
+        const int q = P.qfirst(p);
         if (((dir_mask >> q) & 1) || h.ref[l][q] < 0) {
-          done |= P.pm[p];
+          done |= P.pm(p);
           continue;
         }
         int pm[2];
-        cabac_mvp(v, hdr, l, h.ref[l][q], (q & 1) * 2, (q >> 1) * 2, P.w4[p], P.shape, p, done, pm);
+        cabac_mvp(v, hdr, l, h.ref[l][q], (q & 1) * 2, (q >> 1) * 2, P.w4(p), P.shape, p, done, pm);
         const int dx = h.mv[l][q][0] - pm[0], dy = h.mv[l][q][1] - pm[1];
         for (int k = 0; k < 4; ++k)
-          if ((P.pm[p] >> k) & 1) {
+          if ((P.pm(p) >> k) & 1) {
             n.mvd[l][k][0] = static_cast<int16_t>(dx);
             n.mvd[l][k][1] = static_cast<int16_t>(dy);
           }
-        done |= P.pm[p];
+        done |= P.pm(p);
       }
     }
   }
@@ -926,14 +932,14 @@ struct CabacMbCoder {
     for (int l = 0; l < 2; ++l) {
       if (si.num_ref[l] <= 1) continue;
       for (int p = 0; p < P.np; ++p) {
-        const int q = P.qfirst[p];
+        const int q = P.qfirst(p);
         if (((dir_mask >> q) & 1) || h.ref[l][q] < 0) continue;
         put_ref_idx(l, q, h.ref[l][q]);
       }
     }
     for (int l = 0; l < 2; ++l)
       for (int p = 0; p < P.np; ++p) {
-        const int q = P.qfirst[p];
+        const int q = P.qfirst(p);
         if (((dir_mask >> q) & 1) || h.ref[l][q] < 0) continue;
         put_mvd(l, q, 0, cur->mvd[l][q][0]);
         put_mvd(l, q, 1, cur->mvd[l][q][1]);

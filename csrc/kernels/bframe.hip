@@ -1729,7 +1729,7 @@ __device__ __forceinline__ void med_pred(int ax, int ay, bool ha, int bx, int by
 }
 
 // 8 waves per SIMD (64 VGPRs, a 60-byte spill; 6 at the compiler's 80): 19.1 -> 16.6 ms per step
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void p_part8x8(PPartArgs a) {
+__global__ __launch_bounds__(64) void p_part8x8(PPartArgs a) {
   const Geom& g = a.g;
   const int nmb = g.nmb();
   int mb, slot;
@@ -1805,13 +1805,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     const int i = it * 4 + c;
-    const int x = clampi(cvx[i], -2048, 2047), y = clampi(cvy[i], -512, 511);
+    // candidate i by selects (an index by lane would put cvx / cvy in scratch memory)
+    int ix = 0, iy = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      ix = c == t ? cvx[it * 4 + t] : ix;
+      iy = c == t ? cvy[it * 4 + t] : iy;
+    }
+    const int x = clampi(ix, -2048, 2047), y = clampi(iy, -512, 511);
     const int cst = qsatd(x, y) + lambda * (mvbits_se(x - spx) + mvbits_se(y - spy));
     const int key = qmin((cst << 3) | i);
+    // the winner's vector from the lane of the quad that priced it
+    const int wl = (lane & ~3) | (key & 3);
+    const int wx = __shfl(x, wl, 64), wy = __shfl(y, wl, 64);
     if ((key >> 3) < bcost) {
       bcost = key >> 3;
-      bvx = clampi(cvx[key & 7], -2048, 2047);
-      bvy = clampi(cvy[key & 7], -512, 511);
+      bvx = wx;
+      bvy = wy;
     }
   }
   // stages 2-3: half- then quarter-sample rings around the best

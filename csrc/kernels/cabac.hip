@@ -269,7 +269,7 @@ struct StagedEmit {
   long long start; // first symbol index of this MB
   long long pos;   // next symbol index
   int n;
-  __device__ void emit(uint16_t s) {
+  __device__ __forceinline__ void emit(uint16_t s) {
     lds[pos & 7] = s;
     ++pos;
     ++n;
@@ -283,7 +283,7 @@ struct StagedEmit {
       }
     }
   }
-  __device__ void finish() {
+  __device__ __forceinline__ void finish() {
     const long long c0 = pos & ~7ll;
     for (long long i = c0 > start ? c0 : start; i < pos; ++i) g[i] = lds[i & 7];
   }
@@ -375,7 +375,7 @@ struct RingOut {
     ++n;
     return true;
   }
-  __device__ void finish() {
+  __device__ __forceinline__ void finish() {
     hold = n;  // every byte is final
     flush_words();
     for (; flushed < n; ++flushed)

@@ -562,13 +562,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     }
     store_levels(coef + h264::COEF_CHROMA_AC + (comp * 4 + cb) * 16, sv);
     const int* cl = s_clev[half][comp];
-    const int f[4] = {cl[0] + cl[1] + cl[2] + cl[3], cl[0] - cl[1] + cl[2] - cl[3], cl[0] + cl[1] - cl[2] - cl[3],
-                      cl[0] - cl[1] - cl[2] + cl[3]};
+    // this block's row of the 2x2 Hadamard (signs by cb: no dynamically indexed array)
+    const int c0 = cl[0], c1 = cl[1], c2 = cl[2], c3 = cl[3];
+    const int fcb = cb == 0 ? c0 + c1 + c2 + c3 : (cb == 1 ? c0 - c1 + c2 - c3 : (cb == 2 ? c0 + c1 - c2 - c3 : c0 - c1 - c2 + c3));
     const int ls = 16 * dvc[0];
 #pragma unroll
     for (int r = 0; r < 16; ++r) res[r] = (keep_ac && r > 0) ? (lv[r] * dvc[h264::kPosClass[r]]) << (qpc / 6) : 0;
-    res[0] = ((f[cb] * ls) << (qpc / 6)) >> 5;
-    const bool any = any_ac || cl[0] || cl[1] || cl[2] || cl[3];
+    res[0] = ((fcb * ls) << (qpc / 6)) >> 5;
+    const bool any = any_ac || c0 || c1 || c2 || c3;
     if (any) h264::inverse_core4x4(res);
     uint8_t* recc = (comp == 0 ? a.rec_u : a.rec_v) + rcur * g.csize() + static_cast<size_t>(my * 8 + cby) * cw + mx * 8 + cbx;
 #pragma unroll
