@@ -1728,8 +1728,9 @@ __device__ __forceinline__ void med_pred(int ax, int ay, bool ha, int bx, int by
   *py = median3(ay, by, cy);
 }
 
-// 8 waves per SIMD (64 VGPRs, a 60-byte spill; 6 at the compiler's 80): 19.1 -> 16.6 ms per step
-__global__ __launch_bounds__(64) void p_part8x8(PPartArgs a) {
+// 8 waves per SIMD (64 VGPRs, a 60-byte spill; 6 at the compiler's 80 without spill): 18.9 -> 16.6 ms per
+// step, +0.3 % headline (round-5 same-box A/B, profiles/r5_scratch_ab.md)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void p_part8x8(PPartArgs a) {
   const Geom& g = a.g;
   const int nmb = g.nmb();
   int mb, slot;

@@ -250,7 +250,12 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
   int pa16 = 0, pb16 = 0, pc16 = 0;
   if ((mbav & (h264::AV_TOP | h264::AV_LEFT | h264::AV_TOPLEFT)) == (h264::AV_TOP | h264::AV_LEFT | h264::AV_TOPLEFT))
     h264::i16_plane_params(S.top16, S.left16, tl16, &pa16, &pb16, &pc16);
-  const int dc16 = h264::i16_dc(S.top16, S.left16, mbav);
+  // wave-uniform: scalar registers (the LDS reads above leave them in vector registers,
+  // which this kernel's 128-VGPR budget cannot spare)
+  pa16 = __builtin_amdgcn_readfirstlane(pa16);
+  pb16 = __builtin_amdgcn_readfirstlane(pb16);
+  pc16 = __builtin_amdgcn_readfirstlane(pc16);
+  const int dc16 = __builtin_amdgcn_readfirstlane(h264::i16_dc(S.top16, S.left16, mbav));
   int mode16 = 2, cost16 = 0x3FFFFFFF;
   {
     const int rb = lane >> 2, rbx = (rb & 3) * 4, rby = (rb >> 2) * 4;
@@ -308,21 +313,21 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
     const int mf0 = h264::kQuantMF[qm][0], mf1 = h264::kQuantMF[qm][1], mf2 = h264::kQuantMF[qm][2];
     const int dv0 = h264::kDequantV[qm][0], dv1 = h264::kDequantV[qm][1], dv2 = h264::kDequantV[qm][2];
     for (int blk = 0; blk < 16; ++blk) {
-      int e[13], av;
-      i4_neighbours(S.t4, blk, mbav, e, &av);
-      if (lane < 13) S.e4[lane] = e[lane < 13 ? lane : 0];
+      int av;
+      const int el = i4_neighbour_lane(S.t4, blk, mbav, lane, &av);
+      if (lane < 13) S.e4[lane] = el;
       const int bx = h264::kBlkX[blk], by = h264::kBlkY[blk];
       int ma = bx > 0 ? S.modes4[h264::kRasterToBlk[(bx - 1) + 4 * by]] : S.left_modes[by];
       int mb_ = by > 0 ? S.modes4[h264::kRasterToBlk[bx + 4 * (by - 1)]] : S.top_modes[bx];
       bool dcpred = (bx == 0 && !(mbav & h264::AV_LEFT)) || (by == 0 && !(mbav & h264::AV_TOP));
       int pm = dcpred ? 2 : min(ma, mb_);
+      wave_sync();
       int dcv;
       {
         bool t = av & h264::AV_TOP, l = av & h264::AV_LEFT;
-        int st = e[1] + e[2] + e[3] + e[4], sl = e[9] + e[10] + e[11] + e[12];
-        dcv = (t && l) ? (st + sl + 4) >> 3 : (l ? (sl + 2) >> 2 : (t ? (st + 2) >> 2 : 128));
+        int st = S.e4[1] + S.e4[2] + S.e4[3] + S.e4[4], sl = S.e4[9] + S.e4[10] + S.e4[11] + S.e4[12];
+        dcv = __builtin_amdgcn_readfirstlane((t && l) ? (st + sl + 4) >> 3 : (l ? (sl + 2) >> 2 : (t ? (st + 2) >> 2 : 128)));
       }
-      wave_sync();
       // mode ranking: lane = mode * 4 + row (lanes 0..35)
       int m = lane >> 2;
       bool valid = m < 9 && h264::i4_mode_ok(m, av);
@@ -372,7 +377,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
       wave_sync();
     }
     use4 = total < cost16;
-    cost4 = total;
+    cost4 = __builtin_amdgcn_readfirstlane(total);
   }
 
   // ---- Intra8x8 trial (closed loop over the four 8x8 blocks, 9 modes ranked on sa8d)

@@ -320,7 +320,10 @@ __device__ __forceinline__ int pos_class(int x, int y) {
 constexpr int kTileStride = 24;
 
 // Intra4x4 neighbour vector e[13] of block blk (see h264::i4_pred_sample) + availability
-__device__ __forceinline__ void i4_neighbours(const uint8_t* t, int blk, int mbav, int* e, int* av_out) {
+// Intra4x4 neighbour vector e[0..12] of block blk (0: top-left, 1-8: above and above-right,
+// 9-12: left) from the tile: lane i < 13 returns entry i (the other lanes 0) -- one register
+// per lane instead of the 13-entry vector in every lane.  *av_out: availability (uniform).
+__device__ __forceinline__ int i4_neighbour_lane(const uint8_t* t, int blk, int mbav, int lane, int* av_out) {
   int bx = h264::kBlkX[blk], by = h264::kBlkY[blk];
   bool left = bx > 0 || (mbav & h264::AV_LEFT), top = by > 0 || (mbav & h264::AV_TOP);
   int av = 0;
@@ -333,15 +336,12 @@ __device__ __forceinline__ void i4_neighbours(const uint8_t* t, int blk, int mba
   else if (blk == 0 || blk == 1 || blk == 4) tr = (mbav & h264::AV_TOP) != 0;
   else tr = true;
   if (tr) av |= h264::AV_TOPRIGHT;
-  const uint8_t* row = t + (by * 4) * kTileStride + bx * 4;  // tile row above the block, col of x = -1
-  e[0] = row[0];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) e[1 + i] = row[1 + i];
-#pragma unroll
-  for (int i = 4; i < 8; ++i) e[1 + i] = tr ? row[1 + i] : row[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) e[9 + i] = t[(by * 4 + 1 + i) * kTileStride + bx * 4];
   *av_out = av;
+  const uint8_t* row = t + (by * 4) * kTileStride + bx * 4;  // tile row above the block, col of x = -1
+  if (lane >= 13) return 0;
+  if (lane < 5) return row[lane];
+  if (lane < 9) return tr ? row[lane] : row[4];
+  return t[(by * 4 + 1 + lane - 9) * kTileStride + bx * 4];
 }
 
 }  // namespace gpu
