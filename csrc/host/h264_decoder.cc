@@ -756,6 +756,22 @@ struct Decoder::Impl {
       while (static_cast<int>(list[l].size()) < n) list[l].push_back(list[l].back());
       list[l].resize(n);
     }
+    // temporal direct (8.4.1.2.3): DistScaleFactor per RefPicList0 entry, once per slice
+    tdir_n = 0;
+    if (sh.slice_type == SLICE_B && !sh.direct_spatial && !list[1].empty()) {
+      const Pic& p1 = *list[1][0];
+      tdir_n = std::min<int>(static_cast<int>(list[0].size()), kMaxTdir);
+      for (int i = 0; i < tdir_n; ++i) {
+        const Pic& p0 = *list[0][i];
+        const int tb = clampi(cur->poc - p0.poc, -128, 127), td = clampi(p1.poc - p0.poc, -128, 127);
+        tdir_id[i] = p0.id;
+        tdir_copy[i] = td == 0 || p0.long_ref;
+        if (!tdir_copy[i]) {
+          const int tx = (16384 + std::abs(td / 2)) / td;
+          tdir_dsf[i] = clampi((tb * tx + 32) >> 6, -1024, 1023);
+        }
+      }
+    }
     // implicit bi-prediction weights (8.4.2.3.1)
     if (sh.slice_type == SLICE_B && pp->weighted_bipred_idc == 2) {
       for (int i = 0; i < sh.num_ref_idx_l0_active; ++i)
@@ -882,6 +898,14 @@ struct Decoder::Impl {
     cur->cbp[addr] = 0;
     cur->direct[addr] = 0;
   }
+
+  // temporal direct table of the current slice (8.4.1.2.3): RefPicList0 picture ids,
+  // DistScaleFactor and the "copy the co-located vector" case (td == 0 or long-term)
+  static constexpr int kMaxTdir = 32;
+  int tdir_n = 0;
+  int tdir_id[kMaxTdir];
+  int tdir_dsf[kMaxTdir];
+  bool tdir_copy[kMaxTdir];
 
   // ------------------------------------------------------------ motion vector prediction (8.4.1.3)
   struct NbMv {
@@ -1011,6 +1035,69 @@ struct Decoder::Impl {
       return;
     }
     // 8.4.1.2.3 temporal
+    if (sp->direct_8x8_inference && tdir_n > 0) {
+      // the common case: one co-located corner block per quadrant, DistScaleFactor from the
+      // slice table (the picture is found among RefPicList0's first tdir_n entries)
+      const Pic& col = *list[1][0];
+      const bool col_intra = mbk_is_intra(col.kind[addr]);
+      for (int q = 0; q < 4; ++q) {
+        if (!((quads >> q) & 1)) continue;
+        const int r = (q & 1) * 2 + (q >> 1) * 8;                    // top-left 4x4 of the quadrant
+        const int rr = ((q & 1) ? 3 : 0) + ((q >> 1) ? 12 : 0);      // its co-located corner
+        int mvc0 = 0, mvc1 = 0, ref0 = 0;
+        if (!col_intra) {
+          const int l = col.ref[0][addr * 16 + rr] >= 0 ? 0 : 1;
+          mvc0 = col.mv[l][addr * 32 + 2 * rr];
+          mvc1 = col.mv[l][addr * 32 + 2 * rr + 1];
+          if (col.ref[l][addr * 16 + rr] >= 0) {
+            const int rpc = col.refpic[l][addr * 16 + rr];
+            ref0 = -1;
+            for (int i = 0; i < tdir_n; ++i)
+              if (tdir_id[i] == rpc) {
+                ref0 = i;
+                break;
+              }
+            if (ref0 < 0) {  // beyond the table: the general path
+              ref0 = -2;
+            }
+          }
+        }
+        if (ref0 == -2) {
+          direct_temporal_general(addr, 1 << q);
+          continue;
+        }
+        int m0x, m0y, m1x, m1y;
+        if (tdir_copy[ref0]) {
+          m0x = mvc0;
+          m0y = mvc1;
+          m1x = m1y = 0;
+        } else {
+          const int dsf = tdir_dsf[ref0];
+          m0x = (dsf * mvc0 + 128) >> 8;
+          m0y = (dsf * mvc1 + 128) >> 8;
+          m1x = m0x - mvc0;
+          m1y = m0y - mvc1;
+        }
+        assign2x2(addr, 0, r, ref0, tdir_id[ref0], m0x, m0y);
+        assign2x2(addr, 1, r, 0, list[1][0]->id, m1x, m1y);
+      }
+      return;
+    }
+    direct_temporal_general(addr, quads);
+  }
+
+  // 2x2 group of 4x4 blocks at raster index r (top-left), list l
+  void assign2x2(int addr, int l, int r, int ref, int refid, int mvx, int mvy) {
+    int8_t* rf = &cur->ref[l][addr * 16 + r];
+    int* rp = &cur->refpic[l][addr * 16 + r];
+    int16_t* mv = &cur->mv[l][addr * 32 + 2 * r];
+    rf[0] = rf[1] = rf[4] = rf[5] = static_cast<int8_t>(ref);
+    rp[0] = rp[1] = rp[4] = rp[5] = refid;
+    mv[0] = mv[2] = mv[8] = mv[10] = static_cast<int16_t>(mvx);
+    mv[1] = mv[3] = mv[9] = mv[11] = static_cast<int16_t>(mvy);
+  }
+
+  void direct_temporal_general(int addr, int quads) {
     const Pic& p1 = *list[1][0];
     const int step = sp->direct_8x8_inference ? 2 : 1;  // as in the spatial case
     for (int r = 0; r < 16; r += (step == 2 && (r & 3) == 2) ? 6 : step) {
@@ -1094,6 +1181,9 @@ struct Decoder::Impl {
     h.flags = static_cast<uint8_t>(t8 ? MBF_T8x8 : 0);
     h.sub_direct = cur->direct[addr];
     h.pad0 = static_cast<uint8_t>(slice_idx);  // slice of the MB (GPU intra availability)
+    // P_Skip motion is one vector for the MB, B_Skip / B_Direct_16x16 with direct_8x8_inference
+    // one per quadrant: no 4x4 scan needed for them (nor for intra MBs)
+    const bool known = kind == MBK_PSKIP || mbk_is_intra(kind) || (kind == MBK_BDIRECT && sp->direct_8x8_inference);
     bool quad_uniform = true;
     for (int l = 0; l < 2; ++l)
       for (int q = 0; q < 4; ++q) {
@@ -1103,12 +1193,17 @@ struct Decoder::Impl {
         h.mv[l][q][0] = m0[0];
         h.mv[l][q][1] = m0[1];
         h.ref[l][q] = f0[0];
+        if (known) continue;
         for (int k = 1; k < 4; ++k) {
           int dr = (k & 1) + 4 * (k >> 1);
           quad_uniform = quad_uniform && f0[dr] == f0[0] && m0[2 * dr] == m0[0] && m0[2 * dr + 1] == m0[1];
         }
       }
-    for (int b = 0; b < 16; ++b) h.i4_modes[b] = static_cast<uint8_t>(i4modes ? i4modes[b] : 2);
+    if (i4modes) {
+      for (int b = 0; b < 16; ++b) h.i4_modes[b] = static_cast<uint8_t>(i4modes[b]);
+    } else {
+      std::memset(h.i4_modes, 2, 16);
+    }
     if (!quad_uniform && !mbk_is_intra(kind)) {
       // motion below 8x8: the whole MB's vectors go to the side pool, i4_modes[0..3] (unused
       // by inter MBs) hold the entry index
@@ -2625,15 +2720,45 @@ struct Decoder::Impl {
             for (int k = 0; k < 4; ++k) put(base + k, e == 0 ? 4 : 3);
             continue;
           }
-          if (e == 0 && flat_q && flat_[mbp] && same_motion(mbp, addr)) continue;
+          if (e == 0 && flat_q && flat_[mbp]) {
+            // two flat MBs: every segment of the edge compares the same two motions
+            if (same_motion(mbp, addr)) continue;
+            const int v = bs_inter(mbp, dir == 0 ? 3 : 12, addr, 0);
+            for (int k = 0; k < 4; ++k) put(base + k, v);
+            continue;
+          }
           for (int k = 0; k < 4; ++k) {
             int blkq = dir == 0 ? (e + 4 * k) : (k + 4 * e);
             int blkp = dir == 0 ? (e == 0 ? 3 + 4 * k : e - 1 + 4 * k) : (e == 0 ? k + 12 : k + 4 * (e - 1));
-            put(base + k, bs_of(mbp, blkp, addr, blkq, e == 0));
+            put(base + k, bs_inter(mbp, blkp, addr, blkq));
           }
         }
     }
     return out;
+  }
+  // bs_of for two inter MBs (the callers above have taken the intra cases)
+  int bs_inter(int mbp, int blkp, int mbq, int blkq) const {
+    if (cur->nz[mbp * 16 + blkp] | cur->nz[mbq * 16 + blkq]) return 2;
+    const int p0 = cur->refpic[0][mbp * 16 + blkp], p1 = cur->refpic[1][mbp * 16 + blkp];
+    const int q0 = cur->refpic[0][mbq * 16 + blkq], q1 = cur->refpic[1][mbq * 16 + blkq];
+    const int np = (p0 >= 0) + (p1 >= 0), nq = (q0 >= 0) + (q1 >= 0);
+    if (np != nq) return 1;
+    const int16_t* mp0 = &cur->mv[0][mbp * 32 + 2 * blkp];
+    const int16_t* mp1 = &cur->mv[1][mbp * 32 + 2 * blkp];
+    const int16_t* mq0 = &cur->mv[0][mbq * 32 + 2 * blkq];
+    const int16_t* mq1 = &cur->mv[1][mbq * 32 + 2 * blkq];
+    auto far = [](const int16_t* a, const int16_t* b) { return std::abs(a[0] - b[0]) >= 4 || std::abs(a[1] - b[1]) >= 4; };
+    if (np == 1) {
+      const int pp = p0 >= 0 ? p0 : p1, qq = q0 >= 0 ? q0 : q1;
+      if (pp != qq) return 1;
+      return far(p0 >= 0 ? mp0 : mp1, q0 >= 0 ? mq0 : mq1) ? 1 : 0;
+    }
+    if (!((p0 == q0 && p1 == q1) || (p0 == q1 && p1 == q0))) return 1;
+    if (p0 != p1) {
+      if (p0 == q0) return (far(mp0, mq0) || far(mp1, mq1)) ? 1 : 0;
+      return (far(mp0, mq1) || far(mp1, mq0)) ? 1 : 0;
+    }
+    return ((far(mp0, mq0) || far(mp1, mq1)) && (far(mp0, mq1) || far(mp1, mq0))) ? 1 : 0;
   }
   std::vector<uint8_t> flat_;  // boundary_strengths: inter MB, no coded luma, one motion
   bool no_nz(int a) const {
@@ -2644,11 +2769,11 @@ struct Decoder::Impl {
   }
   // all 16 blocks share each list's picture and vector
   bool one_motion(int a) const {
+    // every entry equals its successor (pictures) / the pair after it (vectors)
     for (int l = 0; l < 2; ++l) {
       const int* rp = &cur->refpic[l][a * 16];
       const int16_t* m = &cur->mv[l][a * 32];
-      for (int r = 1; r < 16; ++r)
-        if (rp[r] != rp[0] || m[2 * r] != m[0] || m[2 * r + 1] != m[1]) return false;
+      if (std::memcmp(rp, rp + 1, 15 * sizeof(int)) != 0 || std::memcmp(m, m + 2, 30 * sizeof(int16_t)) != 0) return false;
     }
     return true;
   }
