@@ -93,8 +93,10 @@ class H264Params:
     # x264 --b-bias: > 0 places more B pictures (B costs * 100 / (120 + bias), run thresholds)
     b_bias: int = 0
     # x264's intra-MB guards on the b-adapt decision (rc/badapt.py): P(i+2 | i) more than half
-    # intra keeps both pictures P, a closing P more than a third intra ends the B run
-    badapt_guard: bool = True
+    # intra keeps both pictures P, a closing P more than a third intra ends the B run.  Off:
+    # measured +4 % BD-rate on top of b-adapt's own loss (profiles/r5_content_rd.md -- they
+    # force P pictures where this encoder's B pictures are cheap, fades above all)
+    badapt_guard: bool = False
     # x264 seeds its motion search from the lookahead's lowres motion: the P search and both B
     # searches get one more candidate, the picture's lowres vector x 2 scaled to its reference
     # distance (when the lookahead ran on the coded MB grid)
@@ -174,8 +176,11 @@ class H264Params:
     trellis_lambda: float = 1.0
     # the same rate-distortion levels on the intra MBs' final encode (encode_intra.hip,
     # lane-parallel h264_trellis.h grp_trellis4x4; x264 applies --trellis 1 to every MB):
-    # -1 = follow `trellis`, 0 = dead-zone quantisation (rounding 1/3), 1 / 2 as `trellis`
-    intra_trellis: int = -1
+    # -1 = follow `trellis`, 0 = dead-zone quantisation (rounding 1/3), 1 / 2 as `trellis`.
+    # Off by default: on the content suite (profiles/r5_content_rd.md) intra trellis at the
+    # inter lambda is +1.1 % BD-rate (worse on 6 of 7 classes: the coarser intra pictures cost
+    # the pictures predicted from them more than the levels save) and -0.7 % fps
+    intra_trellis: int = 0
     # deblock non-reference B pictures even when neither metrics nor the reconstruction
     # are requested (x264 --full-recon); the bitstream does not depend on it
     full_recon: bool = False
