@@ -155,14 +155,15 @@ void mivc_launch_sse(int B, int W, int H, int w, int h, const uint8_t* sy, const
                      float* ssim_sum, void* stream, const void* route, int nbuf);
 long long mivc_lookahead_low_bytes(int w, int h, int N);
 int mivc_launch_lookahead_multi(const uint8_t* low, int w, int h, int N, int F, const int* blk_cost, const int* blk_mv,
-                                int D, int range, unsigned long long* out, void* stream);
+                                int D, int range, unsigned long long* out, void* stream, const float* wt);
 int mivc_launch_hevc_prep_frame(int B, const void* sy, const void* su, const void* sv, long long ss_y, long long ss_c,
                                 int pitch_y, int pitch_c, int bps, int w, int h, uint16_t* dy, uint16_t* du,
                                 uint16_t* dv, uint8_t* d8, int W, int H, int shift, int bd, void* stream);
 int mivc_launch_hevc_proxy8(const uint16_t* src, uint8_t* dst, long long n, int shift, void* stream);
 int mivc_launch_lookahead(const uint8_t* y, int w, int h, long long fstride, int N, int F, uint8_t* low,
                           unsigned long long* frame_cost, int* blk_cost, int* blk_mv, int range, void* stream,
-                          uint8_t* low4, int* mv4, unsigned long long* cost4);
+                          uint8_t* low4, int* mv4, unsigned long long* cost4, float* wt, unsigned long long* wstats,
+                          float thr_mean, float thr_scale);
 long long mivc_lookahead_quarter_bytes(int w, int h, int N);
 }
 
@@ -700,19 +701,22 @@ PYBIND11_MODULE(_hip, m) {
   m.def("lookahead_low_bytes", [](int w, int h, int n) { return mivc_lookahead_low_bytes(w, h, n); });
   m.def("lookahead_quarter_bytes", [](int w, int h, int n) { return mivc_lookahead_quarter_bytes(w, h, n); });
   m.def("lookahead_multi", [](uintptr_t low, int w, int h, int n, int f, uintptr_t blk_cost, uintptr_t blk_mv, int D,
-                              int range, uintptr_t out, uintptr_t stream) {
+                              int range, uintptr_t out, uintptr_t stream, uintptr_t wt) {
     const int r = mivc_launch_lookahead_multi(P<uint8_t>(low), w, h, n, f, P<int>(blk_cost), P<int>(blk_mv), D, range,
-                                              P<unsigned long long>(out), S(stream));
+                                              P<unsigned long long>(out), S(stream), P<float>(wt));
     if (r != 0) throw std::invalid_argument("lookahead_multi: bad arguments (" + std::to_string(r) + ")");
-  });
+  }, py::arg("low"), py::arg("w"), py::arg("h"), py::arg("n"), py::arg("f"), py::arg("blk_cost"), py::arg("blk_mv"),
+     py::arg("D"), py::arg("range"), py::arg("out"), py::arg("stream"), py::arg("wt") = 0);
   m.def("lookahead", [](uintptr_t y, int w, int h, long long fstride, int n, int f, uintptr_t low, uintptr_t frame_cost,
                         uintptr_t blk_cost, int range, uintptr_t stream, uintptr_t blk_mv, uintptr_t low4, uintptr_t mv4,
-                        uintptr_t cost4) {
+                        uintptr_t cost4, uintptr_t wt, uintptr_t wstats, float thr_mean, float thr_scale) {
     int rc = mivc_launch_lookahead(P<uint8_t>(y), w, h, fstride, n, f, P<uint8_t>(low),
                                    P<unsigned long long>(frame_cost), P<int>(blk_cost), P<int>(blk_mv), range,
-                                   S(stream), P<uint8_t>(low4), P<int>(mv4), P<unsigned long long>(cost4));
+                                   S(stream), P<uint8_t>(low4), P<int>(mv4), P<unsigned long long>(cost4), P<float>(wt),
+                                   P<unsigned long long>(wstats), thr_mean, thr_scale);
     if (rc != 0) throw std::invalid_argument("lookahead: bad geometry or range (4, 6, 8)");
   }, py::arg("y"), py::arg("w"), py::arg("h"), py::arg("fstride"), py::arg("n"), py::arg("f"), py::arg("low"),
      py::arg("frame_cost"), py::arg("blk_cost"), py::arg("range"), py::arg("stream"), py::arg("blk_mv") = 0,
-     py::arg("low4") = 0, py::arg("mv4") = 0, py::arg("cost4") = 0);
+     py::arg("low4") = 0, py::arg("mv4") = 0, py::arg("cost4") = 0, py::arg("wt") = 0, py::arg("wstats") = 0,
+     py::arg("thr_mean") = 2.0f, py::arg("thr_scale") = 0.08f);
 }

@@ -126,7 +126,71 @@ struct LaArgs {
   // block (bx / 2, by / 2) instead of around zero, and keeps the zero vector as a candidate
   const int* center;
   int cbw, cbs;  // quarter blocks per row / per frame
+  // lowres weighting (nullable): [N][kLaWtCols] (w, o) per reference distance d (column d);
+  // w == 0: not weighted.  A weighted P candidate is priced with the source mapped through
+  // the inverse weight, s' = (s - o) / w, and its SATD scaled back by w -- the lowres form of
+  // the weighted prediction the encoder will use (x264 analyses weights in its lookahead too:
+  // unweighted fades look like new content and break the P / B decisions and the CRF curve)
+  const float2* wt;
 };
+constexpr int kLaWtCols = 8;
+
+// inverse weight of 4 packed samples: clamp(round((s - o) / w), 0, 255)
+__device__ __forceinline__ uint32_t la_inv_weight4(uint32_t s, float inv_w, float o) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float v = (static_cast<float>((s >> (8 * k)) & 255u) - o) * inv_w;
+    const int q = clampi(static_cast<int>(rintf(v)), 0, 255);
+    r |= static_cast<uint32_t>(q) << (8 * k);
+  }
+  return r;
+}
+
+// per-frame sums of the lowres interior (lw x lh): [N][2] = sum, sum of squares
+__global__ __launch_bounds__(256) void la_stats(const uint8_t* __restrict__ low, LaGeom g,
+                                                unsigned long long* __restrict__ st) {
+  const int n = blockIdx.y;
+  const int lw = g.w >> 1, lh = g.h >> 1;
+  const uint8_t* p = low + n * g.lsize + static_cast<long long>(kLaPad) * g.ls + kLaPad;
+  unsigned long long s = 0, s2 = 0;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < lw * lh; i += gridDim.x * 256) {
+    const int y = i / lw, x = i - y * lw;
+    const unsigned int v = p[static_cast<long long>(y) * g.ls + x];
+    s += v;
+    s2 += v * v;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    s += __shfl_xor(s, off, 64);
+    s2 += __shfl_xor(s2, off, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(st + 2 * n, s);
+    atomicAdd(st + 2 * n + 1, s2);
+  }
+}
+
+// weights of every (frame, distance) pair from the statistics: x264-style weightp rule --
+// w = sqrt(var_cur / var_ref), o = mean_cur - w * mean_ref, used when the mean moved by >=
+// thr_mean levels or the contrast by >= thr_scale
+__global__ __launch_bounds__(256) void la_weights(const unsigned long long* __restrict__ st, LaGeom g, float thr_mean,
+                                                  float thr_scale, float2* __restrict__ wt) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= g.N * kLaWtCols) return;
+  const int n = i / kLaWtCols, d = i - n * kLaWtCols;
+  const int f = n % g.F;
+  float2 r = make_float2(0.f, 0.f);
+  if (d >= 1 && d <= f) {
+    const double cnt = static_cast<double>(g.w >> 1) * static_cast<double>(g.h >> 1);
+    const double mc = static_cast<double>(st[2 * n]) / cnt, mr = static_cast<double>(st[2 * (n - d)]) / cnt;
+    const double vc = fmax(static_cast<double>(st[2 * n + 1]) / cnt - mc * mc, 0.0);
+    const double vr = fmax(static_cast<double>(st[2 * (n - d) + 1]) / cnt - mr * mr, 0.0);
+    const double w = vr > 1e-3 ? sqrt(vc / vr) : 1.0;
+    if ((fabs(mc - mr) >= thr_mean || fabs(w - 1.0) >= thr_scale) && w > 1.0 / 64)
+      r = make_float2(static_cast<float>(w), static_cast<float>(mc - w * mr));
+  }
+  wt[i] = r;
+}
 
 // Quarter-resolution planes from the lowres ones (2x2 box of the lowres interior, replicated
 // border): the coarse level of the hierarchical lookahead search.  q: the quarter geometry
@@ -215,7 +279,9 @@ __device__ __forceinline__ void la_small_search(const uint8_t* ref, const LaGeom
   by = cy + bi / side - R;
 }
 
-template <int R>
+// WT: the instance with lowres weighting (a.wt non-null): its extra registers stay out of the
+// plain instance
+template <int R, bool WT = false>
 __global__ __launch_bounds__(256) void la_cost(LaArgs a) {
   const LaGeom& g = a.g;
   constexpr int side = 2 * R + 1;
@@ -260,8 +326,8 @@ __global__ __launch_bounds__(256) void la_cost(LaArgs a) {
   const int X0 = kLaPad + bxc * 8, Y0 = kLaPad + by * 8;
   const int ry = Y0 + 2 * grp;  // this lane's two rows
   const uint8_t* c0 = cur + static_cast<long long>(ry) * g.ls + X0;
-  const uint2 s0 = *reinterpret_cast<const uint2*>(c0);
-  const uint2 s1 = *reinterpret_cast<const uint2*>(c0 + g.ls);
+  uint2 s0 = *reinterpret_cast<const uint2*>(c0);
+  uint2 s1 = *reinterpret_cast<const uint2*>(c0 + g.ls);
   // intra neighbours: the row above (8 bytes) and this lane's two left samples
   const uint2 top = *reinterpret_cast<const uint2*>(cur + static_cast<long long>(Y0 - 1) * g.ls + X0);
   const uint32_t l0 = c0[-1], l1 = c0[g.ls - 1];
@@ -283,6 +349,24 @@ __global__ __launch_bounds__(256) void la_cost(LaArgs a) {
   intra = min(intra, satd_mfma(negH, accS, as_s8(top.x, top.y, top.x, top.y)));
   intra += 5;  // mode-cost bias
 
+  // weighted reference (lowres weighting): the source through the inverse weight, its
+  // Hadamard half recomputed (intra is done with the plain source)
+  float wsc = 0.f;
+  if (WT && has_ref && a.wt) {
+    const float2 wo = a.wt[static_cast<long long>(n) * kLaWtCols + 1];
+    if (wo.x > 0.f) {  // frame-uniform
+      const float inv = 1.0f / wo.x;
+      s0 = make_uint2(la_inv_weight4(s0.x, inv, wo.y), la_inv_weight4(s0.y, inv, wo.y));
+      s1 = make_uint2(la_inv_weight4(s1.x, inv, wo.y), la_inv_weight4(s1.y, inv, wo.y));
+      const v4i sw = as_s8(s0.x, s0.y, s1.x, s1.y);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) accS[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[t], sw, v4i{0, 0, 0, 0}, 0, 0, 0);
+      wsc = wo.x;
+    }
+  }
+  // SATD of a weighted candidate in the source's units
+  auto wsatd = [&](int v) { return WT && wsc > 0.f ? static_cast<int>(rintf(wsc * static_cast<float>(v))) : v; };
+
   int inter = intra;
   int mvx = 0, mvy = 0;
   if (has_ref && a.center) {  // frame-uniform: hierarchical search around the coarse vector
@@ -291,8 +375,8 @@ __global__ __launch_bounds__(256) void la_cost(LaArgs a) {
     const int cx = 2 * static_cast<int16_t>(cv & 0xFFFF), cy = 2 * (cv >> 16);
     int mx, my;
     la_small_search<R>(ref, g, X0, ry, s0, s1, cx, cy, mx, my);
-    const int cst = satd_mfma(negH, accS, la_rows8(ref, g.ls, X0 + mx, ry + my)) + 2 * (abs(mx) + abs(my));
-    const int c0 = satd_mfma(negH, accS, la_rows8(ref, g.ls, X0, ry));
+    const int cst = wsatd(satd_mfma(negH, accS, la_rows8(ref, g.ls, X0 + mx, ry + my))) + 2 * (abs(mx) + abs(my));
+    const int c0 = wsatd(satd_mfma(negH, accS, la_rows8(ref, g.ls, X0, ry)));
     inter = min(cst, c0);
     mvx = cst < c0 ? mx : 0;
     mvy = cst < c0 ? my : 0;
@@ -335,7 +419,7 @@ __global__ __launch_bounds__(256) void la_cost(LaArgs a) {
     const uint32_t e0 = q0[0], e1 = q0[1], e2 = q0[2], f0 = q1[0], f1 = q1[1], f2 = q1[2];
     const v4i pf = as_s8(__builtin_amdgcn_alignbyte(e1, e0, shb), __builtin_amdgcn_alignbyte(e2, e1, shb),
                          __builtin_amdgcn_alignbyte(f1, f0, shb), __builtin_amdgcn_alignbyte(f2, f1, shb));
-    inter = satd_mfma(negH, accS, pf) + 2 * (abs(mdx) + abs(mdy));
+    inter = wsatd(satd_mfma(negH, accS, pf)) + 2 * (abs(mdx) + abs(mdy));
     mvx = mdx;
     mvy = mdy;
   }
@@ -379,9 +463,10 @@ struct LaMultiArgs {
   const int* blk_mv;    // [N, lbh, lbw] (la_cost): distance-1 lowres vectors
   int D;                // largest P distance (bframes + 1), <= kLaMultiCols - 1
   unsigned long long* out;  // [N, kLaMultiCols]
+  const float2* wt;         // lowres weighting (LaArgs::wt), nullable
 };
 
-template <int R>
+template <int R, bool WT = false>
 __global__ __launch_bounds__(256) void la_multi(LaMultiArgs a) {
   const LaGeom& g = a.g;
   const int nstrips = (g.lbw + 15) >> 4;
@@ -438,9 +523,21 @@ __global__ __launch_bounds__(256) void la_multi(LaMultiArgs a) {
   // P at distances 2..D
   for (int d = 2; d <= a.D && d <= f; ++d) {  // frame-uniform
     const uint8_t* ref = cur - d * g.lsize;
+    const float2 wo = WT ? a.wt[static_cast<long long>(n) * kLaWtCols + d] : make_float2(0.f, 0.f);
+    uint2 w0 = s0, w1 = s1;
+    v4i accW[4] = {accS[0], accS[1], accS[2], accS[3]};
+    if (wo.x > 0.f) {  // frame-uniform: weighted reference at this distance
+      const float inv = 1.0f / wo.x;
+      w0 = make_uint2(la_inv_weight4(s0.x, inv, wo.y), la_inv_weight4(s0.y, inv, wo.y));
+      w1 = make_uint2(la_inv_weight4(s1.x, inv, wo.y), la_inv_weight4(s1.y, inv, wo.y));
+      const v4i sw = as_s8(w0.x, w0.y, w1.x, w1.y);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) accW[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[t], sw, v4i{0, 0, 0, 0}, 0, 0, 0);
+    }
     int mx, my;
-    la_small_search<R>(ref, g, X0, ry, s0, s1, d * v1x, d * v1y, mx, my);
-    const int cst = satd_mfma(negH, accS, la_rows8(ref, g.ls, X0 + mx, ry + my)) +
+    la_small_search<R>(ref, g, X0, ry, w0, w1, d * v1x, d * v1y, mx, my);
+    const int sraw = satd_mfma(negH, accW, la_rows8(ref, g.ls, X0 + mx, ry + my));
+    const int cst = (wo.x > 0.f ? static_cast<int>(rintf(wo.x * static_cast<float>(sraw))) : sraw) +
                     2 * (abs(mx - d * v1x) + abs(my - d * v1y)) + 2 * (abs(v1x) + abs(v1y));
     const int s = sum64(mine ? min(intra, cst) : 0);
     const int ni = sum64(mine && intra < cst ? 1 : 0);
@@ -496,7 +593,8 @@ extern "C" long long mivc_lookahead_quarter_bytes(int w, int h, int N) {
 
 extern "C" int mivc_launch_lookahead(const uint8_t* y, int w, int h, long long fstride, int N, int F, uint8_t* low,
                                      unsigned long long* frame_cost, int* blk_cost, int* blk_mv, int range,
-                                     void* stream, uint8_t* low4, int* mv4, unsigned long long* cost4) {
+                                     void* stream, uint8_t* low4, int* mv4, unsigned long long* cost4, float* wt,
+                                     unsigned long long* wstats, float thr_mean, float thr_scale) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (w < 16 || h < 16 || (w & 1) || (h & 1) || N <= 0 || F <= 0 || N % F) return -1;
   if (range != 4 && range != 6 && range != 8) return -2;
@@ -514,7 +612,14 @@ extern "C" int mivc_launch_lookahead(const uint8_t* y, int w, int h, long long f
   hipMemsetAsync(frame_cost, 0, sizeof(unsigned long long) * 2 * N, s);
   const long long dwords = static_cast<long long>(N) * g.lrows * (g.ls >> 2);
   hipLaunchKernelGGL(la_downscale, dim3(static_cast<unsigned>((dwords + 255) / 256)), dim3(256), 0, s, y, g, low);
-  LaArgs a{g, low, frame_cost, blk_cost, blk_mv, nullptr, 0, 0};
+  LaArgs a{g, low, frame_cost, blk_cost, blk_mv, nullptr, 0, 0, nullptr};
+  if (wt && wstats) {  // lowres weighting: statistics of the lowres planes, then the weights
+    hipMemsetAsync(wstats, 0, sizeof(unsigned long long) * 2 * N, s);
+    hipLaunchKernelGGL(la_stats, dim3(8, N), dim3(256), 0, s, low, g, wstats);
+    hipLaunchKernelGGL(la_weights, dim3((N * kLaWtCols + 255) / 256), dim3(256), 0, s, wstats, g, thr_mean, thr_scale,
+                       reinterpret_cast<float2*>(wt));
+    a.wt = reinterpret_cast<const float2*>(wt);
+  }
   if (low4 && mv4 && cost4 && w >= 64 && h >= 64) {
     LaGeom q{};
     q.w = (w >> 1) & ~1;
@@ -531,7 +636,7 @@ extern "C" int mivc_launch_lookahead(const uint8_t* y, int w, int h, long long f
     hipLaunchKernelGGL(la_downscale_low, dim3(static_cast<unsigned>((qbytes + 255) / 256)), dim3(256), 0, s, low, g, q,
                        low4);
     hipMemsetAsync(cost4, 0, sizeof(unsigned long long) * 2 * N, s);
-    LaArgs aq{q, low4, cost4, nullptr, mv4, nullptr, 0, 0};
+    LaArgs aq{q, low4, cost4, nullptr, mv4, nullptr, 0, 0, nullptr};
     const long long qwaves = static_cast<long long>((q.lbw + 15) >> 4) * q.lbh * N;
     hipLaunchKernelGGL(la_cost<8>, dim3(static_cast<unsigned>((qwaves + 3) >> 2)), dim3(256), 0, s, aq);
     a.center = mv4;
@@ -540,10 +645,18 @@ extern "C" int mivc_launch_lookahead(const uint8_t* y, int w, int h, long long f
   }
   const long long waves = static_cast<long long>((g.lbw + 15) >> 4) * g.lbh * N;
   const dim3 grid(static_cast<unsigned>((waves + 3) >> 2));
-  switch (range) {
-    case 4: hipLaunchKernelGGL(la_cost<4>, grid, dim3(256), 0, s, a); break;
-    case 6: hipLaunchKernelGGL(la_cost<6>, grid, dim3(256), 0, s, a); break;
-    default: hipLaunchKernelGGL(la_cost<8>, grid, dim3(256), 0, s, a); break;
+  if (a.wt) {
+    switch (range) {
+      case 4: hipLaunchKernelGGL((la_cost<4, true>), grid, dim3(256), 0, s, a); break;
+      case 6: hipLaunchKernelGGL((la_cost<6, true>), grid, dim3(256), 0, s, a); break;
+      default: hipLaunchKernelGGL((la_cost<8, true>), grid, dim3(256), 0, s, a); break;
+    }
+  } else {
+    switch (range) {
+      case 4: hipLaunchKernelGGL(la_cost<4>, grid, dim3(256), 0, s, a); break;
+      case 6: hipLaunchKernelGGL(la_cost<6>, grid, dim3(256), 0, s, a); break;
+      default: hipLaunchKernelGGL(la_cost<8>, grid, dim3(256), 0, s, a); break;
+    }
   }
   return 0;
 }
@@ -554,7 +667,7 @@ extern "C" int mivc_launch_lookahead(const uint8_t* y, int w, int h, long long f
 // 40.. of each the number of lowres blocks that chose intra.
 extern "C" int mivc_launch_lookahead_multi(const uint8_t* low, int w, int h, int N, int F, const int* blk_cost,
                                            const int* blk_mv, int D, int range, unsigned long long* out,
-                                           void* stream) {
+                                           void* stream, const float* wt) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (w < 16 || h < 16 || (w & 1) || (h & 1) || N <= 0 || F <= 0 || N % F) return -1;
   if (D < 2 || D >= kLaMultiCols || !blk_cost || !blk_mv || !low || !out) return -2;
@@ -569,10 +682,15 @@ extern "C" int mivc_launch_lookahead_multi(const uint8_t* low, int w, int h, int
   g.lrows = g.lbh * 8 + 2 * kLaPad;
   g.lsize = static_cast<long long>(g.ls) * g.lrows;
   hipMemsetAsync(out, 0, sizeof(unsigned long long) * kLaMultiCols * N, s);
-  LaMultiArgs a{g, low, blk_cost, blk_mv, D, out};
+  LaMultiArgs a{g, low, blk_cost, blk_mv, D, out, reinterpret_cast<const float2*>(wt)};
   const long long waves = static_cast<long long>((g.lbw + 15) >> 4) * g.lbh * N;
   const dim3 grid(static_cast<unsigned>((waves + 3) >> 2));
-  if (range <= 2) hipLaunchKernelGGL(la_multi<2>, grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(la_multi<4>, grid, dim3(256), 0, s, a);
+  if (a.wt) {
+    if (range <= 2) hipLaunchKernelGGL((la_multi<2, true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((la_multi<4, true>), grid, dim3(256), 0, s, a);
+  } else {
+    if (range <= 2) hipLaunchKernelGGL(la_multi<2>, grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(la_multi<4>, grid, dim3(256), 0, s, a);
+  }
   return 0;
 }

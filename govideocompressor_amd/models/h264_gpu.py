@@ -67,6 +67,9 @@ class H264Params:
     # +-6 are BD-rate-identical on the content suite (-0.01 %, profiles/r4_la_range_rd.json),
     # +-4 searches 81 positions instead of 169
     la_range: int = 4
+    # lowres weighted prediction in the lookahead (rc/lookahead.py GpuLookahead(weighted=True)):
+    # P candidates of fades / flashes priced with the weights the encoder's weightp will use
+    la_weights: bool = True
     # x264 --scenecut: a P frame whose lowres inter cost saves less than this percent of
     # its intra cost is coded all-intra (I4x4/I16x16 MBs) at the I-frame QP; 0 disables
     scenecut: int = 40
@@ -1235,7 +1238,7 @@ class GpuH264Encoder:
         from ..rc.lookahead import GpuLookahead
 
         if getattr(self, "_la", None) is None:
-            self._la = GpuLookahead(self.dev, self.p.la_range)
+            self._la = GpuLookahead(self.dev, self.p.la_range, weighted=self.p.la_weights)
         t0 = time.perf_counter()
         self._apply_analysis(self._analysis(y, self._la))
         self.timings["lookahead_s"] = self.timings.get("lookahead_s", 0.0) + time.perf_counter() - t0
@@ -1284,7 +1287,7 @@ class GpuH264Encoder:
         caller's stream instead (e.g. the one that produced ``y``: one hardware queue fewer)."""
         from ..rc.lookahead import GpuLookahead
         if getattr(self, "_la_async", None) is None:
-            self._la_async = GpuLookahead(self.dev, self.p.la_range)
+            self._la_async = GpuLookahead(self.dev, self.p.la_range, weighted=self.p.la_weights)
             self._la_stream = torch.cuda.Stream(device=self.dev)
             self._la_pool = cf.ThreadPoolExecutor(max_workers=1)
 

@@ -53,6 +53,9 @@ class HevcParams:
     # CRF per-frame QPs from the GPU lookahead (rc/lookahead.py); False = flat CRF QP
     lookahead: bool = True
     la_range: int = 6
+    # lowres weighted prediction in the lookahead (rc/lookahead.py GpuLookahead(weighted=True)):
+    # P candidates of fades / flashes priced with the weights the encoder's weightp will use
+    la_weights: bool = True
     scenecut: int = 40   # x264/x265 --scenecut: cut frames are coded all-intra at the I QP (0: off)
     # x265 --wpp (its default): one CABAC substream per CTB row; the host codes the rows of
     # one picture on several threads when fewer pictures than entropy threads are in flight
@@ -380,7 +383,7 @@ class GpuHevcEncoder:
         t0 = time.perf_counter()
         if analysis is None or analysis["shape"] != tuple(y.shape):
             if getattr(self, "_la", None) is None:
-                self._la = GpuLookahead(self.dev, self.p.la_range)
+                self._la = GpuLookahead(self.dev, self.p.la_range, weighted=self.p.la_weights)
             analysis = self._analysis(y, self._la)
         else:
             torch.cuda.current_stream(self.dev).wait_event(analysis["event"])
@@ -401,7 +404,7 @@ class GpuHevcEncoder:
         goes to :meth:`encode_async` / :meth:`encode` as ``analysis=``."""
         from ..rc.lookahead import GpuLookahead
         if getattr(self, "_la_async", None) is None:
-            self._la_async = GpuLookahead(self.dev, self.p.la_range)
+            self._la_async = GpuLookahead(self.dev, self.p.la_range, weighted=self.p.la_weights)
             self._la_stream = torch.cuda.Stream(device=self.dev)
             self._la_pool = cf.ThreadPoolExecutor(max_workers=1)
 

@@ -28,6 +28,7 @@ import os
 H264 = {
     "MIVC_I8X8": "i8x8",
     "MIVC_LA_RANGE": "la_range",
+    "MIVC_LA_WEIGHTS": "la_weights",
     "MIVC_B_ADAPT": "b_adapt",
     "MIVC_B_BIAS": "b_bias",
     "MIVC_BADAPT_GUARD": "badapt_guard",
@@ -58,6 +59,7 @@ H264 = {
 # env name -> HevcParams field
 HEVC = {
     "MIVC_HEVC_CTU64": "ctu64",
+    "MIVC_HEVC_LA_WEIGHTS": "la_weights",
 }
 # bench.py shape knobs (they change what is measured, so they also need --allow-knobs)
 # (MIVC_HIP_LIB: an alternative kernel library, tools/build_variant.py -- same-box A/B timing)

@@ -23,11 +23,19 @@ INTRA_SHIFT = 40  # la_multi packs its intra block counts above the cost sums (l
 class GpuLookahead:
     """Lowres cost analysis on gfx950 (workspace cached across calls)."""
 
-    def __init__(self, device: str | torch.device = "cuda", search_range: int = 6, hierarchical: bool = True):
+    def __init__(self, device: str | torch.device = "cuda", search_range: int = 6, hierarchical: bool = True,
+                 weighted: bool = False, wt_min_mean: float = 2.0, wt_min_scale: float = 0.08):
         """``hierarchical``: search every lowres block around twice its quarter-resolution
         block's vector (a +-8 full search at quarter resolution, +-32 full-resolution pixels)
         instead of around zero -- fast pans, which the lowres window alone (+-2 * range
-        pixels) cannot follow, would otherwise look like scene cuts."""
+        pixels) cannot follow, would otherwise look like scene cuts.
+
+        ``weighted``: lowres weighted prediction (x264 analyses weights in its lookahead):
+        per (picture, reference distance) weights from the lowres planes' means and variances
+        (w = sqrt(var_cur / var_ref), o = mean_cur - w * mean_ref, used when the mean moves by
+        >= ``wt_min_mean`` levels or the contrast by >= ``wt_min_scale``); weighted P
+        candidates are priced as the encoder's weighted prediction will code them, so fades
+        stop looking like new content to the P / B placement, the CRF curve and MB-tree."""
         if search_range not in RANGES:
             raise ValueError(f"search_range must be one of {RANGES}")
         self.hierarchical = bool(hierarchical)
@@ -35,6 +43,9 @@ class GpuLookahead:
         if self.dev.type == "cuda" and self.dev.index is None:
             self.dev = torch.device("cuda", torch.cuda.current_device())
         self.range = int(search_range)
+        self.weighted = bool(weighted)
+        self.wt_min_mean, self.wt_min_scale = float(wt_min_mean), float(wt_min_scale)
+        self.last_weights: torch.Tensor | None = None  # [B, F, 8, 2] (w, o) per distance, w = 0: none
         self.hip = native.hip()
         self._low: torch.Tensor | None = None
         self._cost: torch.Tensor | None = None
@@ -104,10 +115,16 @@ class GpuLookahead:
                 self._mv4 = torch.empty((n * qbw * qbh,), dtype=torch.int32, device=self.dev)
                 self._cost4 = torch.empty((n, 2), dtype=torch.int64, device=self.dev)
             low4, mv4, cost4 = self._low4.data_ptr(), self._mv4.data_ptr(), self._cost4.data_ptr()
+        wt = wst = 0
+        if self.weighted:
+            self._wt = torch.empty((B, F, 8, 2), dtype=torch.float32, device=self.dev)
+            self._wst = torch.empty((n, 2), dtype=torch.int64, device=self.dev)
+            wt, wst = self._wt.data_ptr(), self._wst.data_ptr()
+            self.last_weights = self._wt
         self.hip.lookahead(y.data_ptr(), w, h, y.stride(1), n, F, low.data_ptr(), cost.data_ptr(),
                            blk.data_ptr() if blk is not None else 0, self.range,
                            torch.cuda.current_stream(self.dev).cuda_stream, mv.data_ptr() if mv is not None else 0,
-                           low4, mv4, cost4)
+                           low4, mv4, cost4, wt, wst, self.wt_min_mean, self.wt_min_scale)
         out = cost.view(B, F, 2)
         if block_mvs:
             return out, blk, mv
@@ -129,19 +146,54 @@ class GpuLookahead:
         if not 2 <= int(max_dist) <= 7:
             raise ValueError("max_dist in 2..7 (bframes 1..6)")
         out = torch.empty((B * F, 8), dtype=torch.int64, device=self.dev)
+        wt = self._wt.data_ptr() if (self.weighted and getattr(self, "_wt", None) is not None
+                                     and self._wt.shape[:2] == (B, F)) else 0
         self.hip.lookahead_multi(self._low.data_ptr(), w, h, B * F, F, blk.data_ptr(), mv.data_ptr(), int(max_dist),
-                                 int(search_range), out.data_ptr(), torch.cuda.current_stream(self.dev).cuda_stream)
+                                 int(search_range), out.data_ptr(), torch.cuda.current_stream(self.dev).cuda_stream,
+                                 wt)
         out = out.view(B, F, 8)
         self.last_multi_intra = out >> INTRA_SHIFT
         return out & ((1 << INTRA_SHIFT) - 1)
 
 
-def lookahead_reference(y: np.ndarray, search_range: int = 6) -> tuple[np.ndarray, np.ndarray]:
+def lowres_weights(y: np.ndarray, min_mean: float = 2.0, min_scale: float = 0.08) -> np.ndarray:
+    """numpy model of la_stats / la_weights: [B, F, 8, 2] float32 (w, o) of every picture
+    against the picture d back (column d = 1..7, within the segment); w = 0: not weighted."""
+    B, F, h, w = y.shape
+    lw, lh = w // 2, h // 2
+    yy = y.astype(np.int64)
+    s = (yy[..., 0::2, 0::2][..., :lh, :lw] + yy[..., 0::2, 1::2][..., :lh, :lw] +
+         yy[..., 1::2, 0::2][..., :lh, :lw] + yy[..., 1::2, 1::2][..., :lh, :lw] + 2) >> 2
+    cnt = float(lw * lh)
+    mean = s.sum(axis=(2, 3)).astype(np.float64) / cnt
+    var = np.maximum((s * s).sum(axis=(2, 3)).astype(np.float64) / cnt - mean * mean, 0.0)
+    out = np.zeros((B, F, 8, 2), np.float32)
+    for b in range(B):
+        for f in range(F):
+            for d in range(1, min(8, f + 1)):
+                mc, mr, vc, vr = mean[b, f], mean[b, f - d], var[b, f], var[b, f - d]
+                wv = np.sqrt(vc / vr) if vr > 1e-3 else 1.0
+                if (abs(mc - mr) >= min_mean or abs(wv - 1.0) >= min_scale) and wv > 1.0 / 64:
+                    out[b, f, d] = (np.float32(wv), np.float32(mc - wv * mr))
+    return out
+
+
+def _inv_weight(S: np.ndarray, wv: np.float32, o: np.float32) -> np.ndarray:
+    """la_inv_weight4: clamp(rint((s - o) * (1 / w)), 0, 255) in float32."""
+    inv = np.float32(1.0) / wv
+    v = (S.astype(np.float32) - o) * inv
+    return np.clip(np.rint(v), 0, 255).astype(np.int64)
+
+
+def lookahead_reference(y: np.ndarray, search_range: int = 6, weights: np.ndarray | None = None
+                        ) -> tuple[np.ndarray, np.ndarray]:
     """Plain numpy model of ``lookahead.hip`` (the numerics-test oracle).
 
     y: [B, F, h, w] uint8.  Returns (frame costs [B, F, 2] int64, block costs
     [B, F, 2, lbh, lbw] int64).  SATD = (sum |H64 . vec(S - P)| + 2) >> 2 with
-    H64[i, k] = (-1)^popcount(i & k) and vec index k = 8 * row + col.
+    H64[i, k] = (-1)^popcount(i & k) and vec index k = 8 * row + col.  ``weights``
+    (:func:`lowres_weights`): the weighted inter cost -- search and SATD on the inverse-weighted
+    source, SATD scaled back by w.
     """
     B, F, h, w = y.shape
     R, pad = search_range, 16
@@ -177,16 +229,21 @@ def lookahead_reference(y: np.ndarray, search_range: int = 6) -> tuple[np.ndarra
                     intra = min(satd(S - dc), satd(S - left[:, None]), satd(S - top[None, :])) + 5
                     inter = intra
                     if ref is not None:
+                        wv = weights[b, f, 1, 0] if weights is not None else np.float32(0)
+                        Sw = _inv_weight(S, wv, weights[b, f, 1, 1]) if wv > 0 else S
                         best = None
                         for dy in range(-R, R + 1):
                             for dx in range(-R, R + 1):
                                 P = ref[Y0 + dy:Y0 + dy + 8, X0 + dx:X0 + dx + 8]
-                                key = (int(np.abs(S - P).sum()) + 2 * (abs(dx) + abs(dy)), (dy + R) * side + dx + R)
+                                key = (int(np.abs(Sw - P).sum()) + 2 * (abs(dx) + abs(dy)), (dy + R) * side + dx + R)
                                 if best is None or key < best[0]:
                                     best = (key, dx, dy)
                         _, mdx, mdy = best
                         P = ref[Y0 + mdy:Y0 + mdy + 8, X0 + mdx:X0 + mdx + 8]
-                        inter = satd(S - P) + 2 * (abs(mdx) + abs(mdy))
+                        sv = satd(Sw - P)
+                        if wv > 0:
+                            sv = int(np.rint(np.float32(wv) * np.float32(sv)))
+                        inter = sv + 2 * (abs(mdx) + abs(mdy))
                     blk[b, f, 0, by, bx] = intra
                     blk[b, f, 1, by, bx] = inter
     frame = np.stack([blk[:, :, 0].sum(axis=(2, 3)), np.minimum(blk[:, :, 0], blk[:, :, 1]).sum(axis=(2, 3))], axis=-1)

@@ -185,3 +185,54 @@ def test_hierarchical_lookahead_follows_fast_pans():
     assert dx_h == 12, out          # frame t matches frame t - 1 twelve lowres pixels to the right
     assert ratio_h < 0.35, out      # inter prediction works
     assert out[False][0] > 2 * ratio_h, out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [4, 6])
+def test_weighted_lookahead_matches_reference_on_a_fade(R):
+    """Lowres weighting: on a fade (brightness and contrast scaled per frame) the weights of
+    every (picture, distance) pair equal the numpy model's, the weighted block costs match
+    the model exactly (search and SATD on the inverse-weighted source, SATD scaled back), and
+    the P costs drop well below the unweighted ones -- the fade stops looking like new content."""
+    import torch
+
+    from govideocompressor_amd.rc.lookahead import GpuLookahead, lowres_weights
+
+    B, F, h, w = 2, 4, 64, 96
+    y = _clip(B, F, h, w, seed=R + 7).astype(np.float64)
+    gain = np.array([1.0, 0.8, 0.62, 0.47])[None, :, None, None]
+    y = np.clip(np.rint(16 + (y - 16) * gain + 6 * np.arange(F)[None, :, None, None]), 0, 255).astype(np.uint8)
+    yd = torch.from_numpy(y).to("cuda:0")
+    plain = GpuLookahead("cuda:0", search_range=R, hierarchical=False)
+    la = GpuLookahead("cuda:0", search_range=R, hierarchical=False, weighted=True)
+    frame0 = plain.frame_costs(yd).cpu().numpy()
+    frame, blk = la.frame_costs(yd, block_costs=True)
+    torch.cuda.synchronize()
+    wt_ref = lowres_weights(y)
+    wt = la.last_weights.cpu().numpy()
+    assert (wt_ref[:, 1:, 1, 0] > 0).all(), "every picture of the fade is weighted"
+    np.testing.assert_allclose(wt, wt_ref, rtol=1e-6, atol=1e-4)
+    ref_frame, ref_blk = lookahead_reference(y, search_range=R, weights=wt)
+    got_blk = blk.cpu().numpy().astype(np.int64)
+    bad = np.argwhere(got_blk != ref_blk)
+    assert bad.size == 0, f"{len(bad)} block mismatches, first {bad[:4].tolist()}"
+    assert np.array_equal(frame.cpu().numpy(), ref_frame)
+    # P costs (min(intra, inter)) of the faded pictures: weighted well below unweighted
+    assert (frame[:, 1:, 1] < 0.8 * frame0[:, 1:, 1]).all(), (frame[:, :, 1], frame0[:, :, 1])
+
+
+@pytest.mark.gpu
+def test_weighted_lookahead_leaves_steady_content_alone():
+    """No brightness or contrast change (the headline content class): no pair is weighted and
+    the costs equal the unweighted lookahead's, so the default encode is unchanged."""
+    import torch
+
+    from govideocompressor_amd.rc.lookahead import GpuLookahead
+
+    y = _clip(2, 4, 64, 96, seed=5)
+    yd = torch.from_numpy(y).to("cuda:0")
+    a = GpuLookahead("cuda:0", 6, hierarchical=True).frame_costs(yd).cpu().numpy()
+    la = GpuLookahead("cuda:0", 6, hierarchical=True, weighted=True)
+    b = la.frame_costs(yd).cpu().numpy()
+    assert (la.last_weights.cpu().numpy()[..., 0] == 0).all()
+    assert np.array_equal(a, b)

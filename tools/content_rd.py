@@ -65,6 +65,11 @@ CONFIGS = {
     "tl07": dict(trellis_lambda=0.7),
     "tl14": dict(trellis_lambda=1.4),
     "itr0": dict(intra_trellis=0),  # dead-zone levels on intra MBs (round 4)
+    "itr1": dict(intra_trellis=2),  # RD levels on intra MBs too
+    "law0": dict(la_weights=False),  # lookahead without lowres weighting (round 4)
+    "ba100w": dict(b_adapt=1, b_bias=100),  # b-adapt at --b-bias 100 (lowres weighting on)
+    "ba100w0": dict(b_adapt=1, b_bias=100, la_weights=False),
+    "ba40w": dict(b_adapt=1, b_bias=40),
     # fast spatial direct with the fixed GOP pattern: exact motion re-predicted (tol -1, round 4's
     # first version) / estimate kept as explicit motion beyond 0 / 4 quarter samples; b-pyramid
     "sp_repredict": dict(direct="spatial", spatial_fix_tol=-1),
