@@ -216,7 +216,8 @@ def test_weighted_lookahead_matches_reference_on_a_fade(R):
     got_blk = blk.cpu().numpy().astype(np.int64)
     bad = np.argwhere(got_blk != ref_blk)
     assert bad.size == 0, f"{len(bad)} block mismatches, first {bad[:4].tolist()}"
-    assert np.array_equal(frame.cpu().numpy(), ref_frame)
+    frame = frame.cpu().numpy()
+    assert np.array_equal(frame, ref_frame)
     # P costs (min(intra, inter)) of the faded pictures: weighted well below unweighted
     assert (frame[:, 1:, 1] < 0.8 * frame0[:, 1:, 1]).all(), (frame[:, :, 1], frame0[:, :, 1])
 
