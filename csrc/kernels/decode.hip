@@ -182,7 +182,11 @@ __global__ __launch_bounds__(64) void decode_inter_dpb(DecodeArgs a) {
   const size_t o = static_cast<size_t>(slot) * g.nmb() + mb;
   const MbHeader* H = a.hdr + o;
   if (h264::mbk_is_intra(H->kind)) return;
-  __shared__ uint8_t win[2][16][kBW * kBW];
+  // reference windows: per (list, 4x4 block) 9x9 when the MB carries sub-8x8 motion, else per
+  // (list, 8x8 quadrant) 13x13 (one vector per quadrant: the four blocks' windows overlap)
+  // in rows of kQP bytes, staged a row per lane with dword loads
+  constexpr int kQP = 16, kQW = 13;
+  __shared__ __attribute__((aligned(16))) uint8_t win[2][16][kBW * kBW];
   __shared__ int d8[4][64];
   const int lane = threadIdx.x;
   const int mx = mb % g.wmb, my = mb / g.wmb;
@@ -220,17 +224,55 @@ __global__ __launch_bounds__(64) void decode_inter_dpb(DecodeArgs a) {
     return di;
   };
 
-  // ---- stage the 9x9 window of every block and list (clamped: unrestricted vectors)
-  for (int i = lane; i < 2 * 16 * kBW * kBW; i += 64) {
-    const int l = i / (16 * kBW * kBW), j0 = i - l * 16 * kBW * kBW;
-    const int rb = j0 / (kBW * kBW), j = j0 - rb * kBW * kBW;
-    const int r = ref_of(l, rb);
-    if (r < 0) continue;
-    const int di = pic_of(l, r);
-    const int rr = j / kBW, cc = j - rr * kBW;
-    const int x = clampi(X0 + (rb & 3) * 4 + (mv_of(l, rb, 0) >> 2) - 2 + cc, 0, W - 1);
-    const int y = clampi(Y0 + (rb >> 2) * 4 + (mv_of(l, rb, 1) >> 2) - 2 + rr, 0, Hh - 1);
-    win[l][rb][j] = a.rec_y[(static_cast<size_t>(slot) * D + di) * g.ysize() + static_cast<size_t>(y) * W + x];
+  // ---- stage the reference windows (clamped: unrestricted vectors)
+  uint8_t* qwin = &win[0][0][0];  // quadrant mode: [l][q][kQW rows][kQP] inside the same storage
+  static_assert(2 * 4 * kQW * kQP <= 2 * 16 * kBW * kBW, "quadrant windows fit the block windows' storage");
+  if (sub4) {
+    for (int i = lane; i < 2 * 16 * kBW * kBW; i += 64) {
+      const int l = i / (16 * kBW * kBW), j0 = i - l * 16 * kBW * kBW;
+      const int rb = j0 / (kBW * kBW), j = j0 - rb * kBW * kBW;
+      const int r = ref_of(l, rb);
+      if (r < 0) continue;
+      const int di = pic_of(l, r);
+      const int rr = j / kBW, cc = j - rr * kBW;
+      const int x = clampi(X0 + (rb & 3) * 4 + (mv_of(l, rb, 0) >> 2) - 2 + cc, 0, W - 1);
+      const int y = clampi(Y0 + (rb >> 2) * 4 + (mv_of(l, rb, 1) >> 2) - 2 + rr, 0, Hh - 1);
+      win[l][rb][j] = a.rec_y[(static_cast<size_t>(slot) * D + di) * g.ysize() + static_cast<size_t>(y) * W + x];
+    }
+  } else {
+    for (int i = lane; i < 2 * 4 * kQW; i += 64) {  // one window row per lane
+      const int l = i / (4 * kQW), j = i - l * 4 * kQW;
+      const int q = j / kQW, rr = j - q * kQW;
+      const int r = H->ref[l][q];
+      if (r < 0) continue;
+      const int di = pic_of(l, r);
+      const int x0 = X0 + (q & 1) * 8 + (H->mv[l][q][0] >> 2) - 2;
+      const int y = clampi(Y0 + (q >> 1) * 8 + (H->mv[l][q][1] >> 2) - 2 + rr, 0, Hh - 1);
+      const uint8_t* row = a.rec_y + (static_cast<size_t>(slot) * D + di) * g.ysize() + static_cast<size_t>(y) * W;
+      uint32_t* dst = reinterpret_cast<uint32_t*>(qwin + ((l * 4 + q) * kQW + rr) * kQP);
+      if (x0 >= 0 && x0 + 16 <= W) {  // inside the row: four aligned dwords cover the 13 bytes
+        const int xa = x0 & ~3, sh = x0 & 3;
+        const uint32_t* s4 = reinterpret_cast<const uint32_t*>(row + xa);
+        const uint32_t e0 = s4[0], e1 = s4[1], e2 = s4[2], e3 = s4[3];
+        dst[0] = __builtin_amdgcn_alignbyte(e1, e0, sh);
+        dst[1] = __builtin_amdgcn_alignbyte(e2, e1, sh);
+        dst[2] = __builtin_amdgcn_alignbyte(e3, e2, sh);
+        dst[3] = __builtin_amdgcn_alignbyte(0u, e3, sh);  // byte 12 (the last one used) lies in e3
+      } else {
+        uint32_t w4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          uint32_t v = 0;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) v |= static_cast<uint32_t>(row[clampi(x0 + 4 * k + b, 0, W - 1)]) << (8 * b);
+          w4[k] = v;
+        }
+        dst[0] = w4[0];
+        dst[1] = w4[1];
+        dst[2] = w4[2];
+        dst[3] = w4[3];
+      }
+    }
   }
   // ---- 8x8 transform: dequantise (lane = b8 * 16 + t, four levels each), then row and
   // column passes in LDS
@@ -264,9 +306,11 @@ __global__ __launch_bounds__(64) void decode_inter_dpb(DecodeArgs a) {
 #pragma unroll
     for (int l = 0; l < 2; ++l) {
       const int r = l ? r1 : r0;
-      const uint8_t* w = win[l][rb];
-      auto ref = [&](int x, int y) { return static_cast<int>(w[(y + 2) * kBW + x + 2]); };
       const int fx = mv_of(l, rb, 0) & 3, fy = mv_of(l, rb, 1) & 3;
+      // this block's 9x9 window: its own (sub-8x8 motion) or inside its quadrant's 13x13
+      const uint8_t* w = sub4 ? win[l][rb] : qwin + (l * 4 + quad(rb)) * kQW * kQP + (by & 1) * 4 * kQP + (bx & 1) * 4;
+      const int pitch = sub4 ? kBW : kQP;
+      auto ref = [&](int x, int y) { return static_cast<int>(w[(y + 2) * pitch + x + 2]); };
 #pragma unroll
       for (int x = 0; x < 4; ++x) pl[l][x] = r >= 0 ? h264::mc_luma_sample(ref, x, gy, fx, fy) : 0;
     }

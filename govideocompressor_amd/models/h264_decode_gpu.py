@@ -218,12 +218,14 @@ class GpuH264Decoder:
         if any(pl is None for pl in plans):
             return None
         run = np.zeros((F, B), np.int8)
+        nonref = np.ones((F,), bool)  # every active slot's picture of the step is a non-reference one
         cur = np.zeros((F, B), np.int16)
         reftab = np.full((F, B, 64), -1, np.int16)
         for j, s in enumerate(infos):
             Pn = ns[j]
             st = s["meta"][:, M["slice_type"]] % 5
             run[:Pn, j] = np.where(st == 2, 1, 2)
+            nonref[:Pn] &= s["meta"][:, M["nal_ref"]] == 0
             cur[:Pn, j] = plans[j][0]
             reftab[:Pn, j] = plans[j][1].reshape(Pn, 64)
         d_run = torch.from_numpy(run).to(dev)
@@ -239,7 +241,9 @@ class GpuH264Decoder:
         y_d = torch.empty((B, F, Hc, Wc), dtype=torch.uint8, device=dev)
         u_d = torch.empty((B, F, Hc // 2, Wc // 2), dtype=torch.uint8, device=dev)
         v_d = torch.empty_like(u_d)
-        nz = torch.zeros((B, nmb, 16), dtype=torch.uint8, device=dev)
+        # per step parity: a non-reference step's deblocking (side stream) reads its nz while the
+        # next step's reconstruction writes the other
+        nzs = torch.zeros((2, B, nmb, 16), dtype=torch.uint8, device=dev)
         err = torch.zeros((1,), dtype=torch.int32, device=dev)
         comp = torch.cuda.current_stream(dev)
         copy = getattr(self, "_copy_stream", None)
@@ -247,6 +251,11 @@ class GpuH264Decoder:
             copy = self._copy_stream = torch.cuda.Stream(dev)
         copied = [torch.cuda.Event(), torch.cuda.Event()]
         consumed = [torch.cuda.Event(), torch.cuda.Event()]
+        side = getattr(self, "_dbk_stream", None)
+        if side is None:
+            side = self._dbk_stream = torch.cuda.Stream(dev)
+        side.wait_stream(comp)
+        decoded = [torch.cuda.Event(), torch.cuda.Event()]
         for k in range(2):
             consumed[k].record(comp)
         s_ = comp.cuda_stream
@@ -265,13 +274,25 @@ class GpuH264Decoder:
             base = dev_buf.data_ptr()
             a = {n: base + int(L[n]) for n in ("hdr", "mask", "off", "bs", "wp", "coef", "sub")}
             any_inter = bool(np.any(run[t] == 2))
+            nz = nzs[k]
             self.hip.decode_picture_dpb(B, wmb, hmb, F, P_(y_d), P_(u_d), P_(v_d), P_(d_cur[t]), P_(d_reftab[t]),
                                         a["wp"], a["sub"], a["hdr"], a["mask"], a["off"], a["coef"], P_(d_run[t]),
                                         int(any_inter), cqp, P_(nz), P_(err), s_)
+            if deblock and nonref[t]:
+                # nothing predicts from these pictures: their in-loop filter runs on a side stream
+                # beside the next steps' reconstruction (the step's staging buffer and nz parity are
+                # released after it)
+                decoded[k].record(comp)
+                side.wait_event(decoded[k])
+                self.hip.deblock_dpb(B, wmb, hmb, F, P_(y_d), P_(u_d), P_(v_d), P_(d_cur[t]), a["hdr"], P_(nz),
+                                     a["bs"], cqp, alpha, beta, P_(err), side.cuda_stream)
+                consumed[k].record(side)
+                continue
             if deblock:
                 self.hip.deblock_dpb(B, wmb, hmb, F, P_(y_d), P_(u_d), P_(v_d), P_(d_cur[t]), a["hdr"], P_(nz),
                                      a["bs"], cqp, alpha, beta, P_(err), s_)
             consumed[k].record(comp)
+        comp.wait_stream(side)  # the side-stream filters are part of the output
         if crop:
             y_out = y_d[:, :, cy:cy + h, cx:cx + w].contiguous()
             u_out = u_d[:, :, cy // 2:(cy + h) // 2, cx // 2:(cx + w) // 2].contiguous()

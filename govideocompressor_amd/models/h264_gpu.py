@@ -100,6 +100,11 @@ class H264Params:
     # measured +4 % BD-rate on top of b-adapt's own loss (profiles/r5_content_rd.md -- they
     # force P pictures where this encoder's B pictures are cheap, fades above all)
     badapt_guard: bool = False
+    # b-adapt decides ONE pattern for the batch from the lowres costs summed over its slots (each
+    # slot still anchors at its own cuts / forced positions): per-slot patterns mix P and B
+    # pictures in every coding step, so each step runs both the P and the B kernels at partial
+    # width (same-box A/B: 9.9k vs 13.0k fps at the headline config, profiles/r5_badapt_ab.md)
+    badapt_shared: bool = True
     # x264 seeds its motion search from the lookahead's lowres motion: the P search and both B
     # searches get one more candidate, the picture's lowres vector x 2 scaled to its reference
     # distance (when the lookahead ran on the coded MB grid)
@@ -828,12 +833,19 @@ class GpuH264Encoder:
         multi = getattr(self, "_la_multi", None)
         multi_intra = getattr(self, "_la_multi_intra", None) if self.p.badapt_guard else None
         adaptive = multi is not None and multi.shape[:2] == (self.B, F)
+        shared = None
         if adaptive:
-            from ..rc.badapt import b_adapt_types
+            from ..rc.badapt import b_adapt_types, with_anchors
+            if self.p.badapt_shared:
+                mi = None if multi_intra is None else multi_intra.sum(axis=0)
+                shared = b_adapt_types(self._la_costs[:, :, 1].sum(axis=0), multi.sum(axis=0), multi[:, :, 0].sum(axis=0),
+                                       self.nb, self._la_blocks * self.B, common, int(self.p.b_bias), mi)
         for b in range(self.B):
             forced = {int(d) for d in anchors_at[b]} if per_slot else common
             forced = forced | {d for d in range(1, F) if cuts_h[b, d]}
-            if adaptive:
+            if shared is not None:
+                ty = with_anchors(shared, forced)
+            elif adaptive:
                 ty = b_adapt_types(self._la_costs[b, :, 1], multi[b], multi[b, :, 0], self.nb, self._la_blocks, forced,
                                    int(self.p.b_bias), None if multi_intra is None else multi_intra[b])
             else:

@@ -32,6 +32,7 @@ H264 = {
     "MIVC_B_ADAPT": "b_adapt",
     "MIVC_B_BIAS": "b_bias",
     "MIVC_BADAPT_GUARD": "badapt_guard",
+    "MIVC_BADAPT_SHARED": "badapt_shared",
     "MIVC_LA_SEED": "lowres_seed",
     "MIVC_B_ME_RANGE": "b_me_range",
     "MIVC_SKIP_REFINE": "skip_refine",

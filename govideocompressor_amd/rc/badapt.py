@@ -85,6 +85,17 @@ def b_adapt_types(p1: np.ndarray, pd: np.ndarray, bcost: np.ndarray, bframes: in
     return "".join(types)
 
 
+def with_anchors(types: str, anchors) -> str:
+    """``types`` with the pictures at ``anchors`` turned into P anchors (B runs only split, so
+    they stay within the pattern's run length); picture 0 keeps its type."""
+    t = list(types)
+    for d in anchors:
+        d = int(d)
+        if 0 < d < len(t) and t[d] == "B":
+            t[d] = "P"
+    return "".join(t)
+
+
 def b_adapt_batch(costs: np.ndarray, multi: np.ndarray, bframes: int, mb_count: int, forced_per_slot,
                   b_bias: int = 0, multi_intra: np.ndarray | None = None) -> list[str]:
     """Per-slot types of a batch: costs [B, F, 2] (la_cost frame sums: intra, min(intra,

@@ -89,3 +89,9 @@ def test_intra_guards_force_p_like_x264():
     assert t.startswith("IBBP"), t
     intra[4, 4] = 33  # not more than a third: unchanged
     assert b_adapt_types(p1, pd, bc, 3, 100, pd_intra=intra) == "IBBBPBBBPBBBP"
+
+
+def test_with_anchors_splits_b_runs_only():
+    from govideocompressor_amd.rc.badapt import with_anchors
+    assert with_anchors("IBBBPBBBP", {2, 6}) == "IBPBPBPBP"
+    assert with_anchors("IBBBPBBBP", {0, 4, 8}) == "IBBBPBBBP"
