@@ -163,7 +163,7 @@ int mivc_launch_hevc_proxy8(const uint16_t* src, uint8_t* dst, long long n, int 
 int mivc_launch_lookahead(const uint8_t* y, int w, int h, long long fstride, int N, int F, uint8_t* low,
                           unsigned long long* frame_cost, int* blk_cost, int* blk_mv, int range, void* stream,
                           uint8_t* low4, int* mv4, unsigned long long* cost4, float* wt, unsigned long long* wstats,
-                          float thr_mean, float thr_scale);
+                          float thr_mean, float thr_scale, int stage);
 long long mivc_lookahead_quarter_bytes(int w, int h, int N);
 }
 
@@ -709,14 +709,14 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("D"), py::arg("range"), py::arg("out"), py::arg("stream"), py::arg("wt") = 0);
   m.def("lookahead", [](uintptr_t y, int w, int h, long long fstride, int n, int f, uintptr_t low, uintptr_t frame_cost,
                         uintptr_t blk_cost, int range, uintptr_t stream, uintptr_t blk_mv, uintptr_t low4, uintptr_t mv4,
-                        uintptr_t cost4, uintptr_t wt, uintptr_t wstats, float thr_mean, float thr_scale) {
+                        uintptr_t cost4, uintptr_t wt, uintptr_t wstats, float thr_mean, float thr_scale, int stage) {
     int rc = mivc_launch_lookahead(P<uint8_t>(y), w, h, fstride, n, f, P<uint8_t>(low),
                                    P<unsigned long long>(frame_cost), P<int>(blk_cost), P<int>(blk_mv), range,
                                    S(stream), P<uint8_t>(low4), P<int>(mv4), P<unsigned long long>(cost4), P<float>(wt),
-                                   P<unsigned long long>(wstats), thr_mean, thr_scale);
+                                   P<unsigned long long>(wstats), thr_mean, thr_scale, stage);
     if (rc != 0) throw std::invalid_argument("lookahead: bad geometry or range (4, 6, 8)");
   }, py::arg("y"), py::arg("w"), py::arg("h"), py::arg("fstride"), py::arg("n"), py::arg("f"), py::arg("low"),
      py::arg("frame_cost"), py::arg("blk_cost"), py::arg("range"), py::arg("stream"), py::arg("blk_mv") = 0,
      py::arg("low4") = 0, py::arg("mv4") = 0, py::arg("cost4") = 0, py::arg("wt") = 0, py::arg("wstats") = 0,
-     py::arg("thr_mean") = 2.0f, py::arg("thr_scale") = 0.08f);
+     py::arg("thr_mean") = 2.0f, py::arg("thr_scale") = 0.08f, py::arg("stage") = 3);
 }

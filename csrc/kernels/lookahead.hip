@@ -594,7 +594,10 @@ extern "C" long long mivc_lookahead_quarter_bytes(int w, int h, int N) {
 extern "C" int mivc_launch_lookahead(const uint8_t* y, int w, int h, long long fstride, int N, int F, uint8_t* low,
                                      unsigned long long* frame_cost, int* blk_cost, int* blk_mv, int range,
                                      void* stream, uint8_t* low4, int* mv4, unsigned long long* cost4, float* wt,
-                                     unsigned long long* wstats, float thr_mean, float thr_scale) {
+                                     unsigned long long* wstats, float thr_mean, float thr_scale, int stage) {
+  // stage bit 0: lowres planes (+ the weights when wt and wstats are given); bit 1: the costs
+  // (the weighted instances when wt is given).  The caller may look at the weights between
+  // the two and run the plain instances when no picture is weighted.
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (w < 16 || h < 16 || (w & 1) || (h & 1) || N <= 0 || F <= 0 || N % F) return -1;
   if (range != 4 && range != 6 && range != 8) return -2;
@@ -609,17 +612,19 @@ extern "C" int mivc_launch_lookahead(const uint8_t* y, int w, int h, long long f
   g.ls = g.lbw * 8 + 2 * kLaPad;
   g.lrows = g.lbh * 8 + 2 * kLaPad;
   g.lsize = static_cast<long long>(g.ls) * g.lrows;
-  hipMemsetAsync(frame_cost, 0, sizeof(unsigned long long) * 2 * N, s);
-  const long long dwords = static_cast<long long>(N) * g.lrows * (g.ls >> 2);
-  hipLaunchKernelGGL(la_downscale, dim3(static_cast<unsigned>((dwords + 255) / 256)), dim3(256), 0, s, y, g, low);
-  LaArgs a{g, low, frame_cost, blk_cost, blk_mv, nullptr, 0, 0, nullptr};
-  if (wt && wstats) {  // lowres weighting: statistics of the lowres planes, then the weights
-    hipMemsetAsync(wstats, 0, sizeof(unsigned long long) * 2 * N, s);
-    hipLaunchKernelGGL(la_stats, dim3(8, N), dim3(256), 0, s, low, g, wstats);
-    hipLaunchKernelGGL(la_weights, dim3((N * kLaWtCols + 255) / 256), dim3(256), 0, s, wstats, g, thr_mean, thr_scale,
-                       reinterpret_cast<float2*>(wt));
-    a.wt = reinterpret_cast<const float2*>(wt);
+  LaArgs a{g, low, frame_cost, blk_cost, blk_mv, nullptr, 0, 0, reinterpret_cast<const float2*>(wt)};
+  if (stage & 1) {
+    const long long dwords = static_cast<long long>(N) * g.lrows * (g.ls >> 2);
+    hipLaunchKernelGGL(la_downscale, dim3(static_cast<unsigned>((dwords + 255) / 256)), dim3(256), 0, s, y, g, low);
+    if (wt && wstats) {  // lowres weighting: statistics of the lowres planes, then the weights
+      hipMemsetAsync(wstats, 0, sizeof(unsigned long long) * 2 * N, s);
+      hipLaunchKernelGGL(la_stats, dim3(8, N), dim3(256), 0, s, low, g, wstats);
+      hipLaunchKernelGGL(la_weights, dim3((N * kLaWtCols + 255) / 256), dim3(256), 0, s, wstats, g, thr_mean, thr_scale,
+                         reinterpret_cast<float2*>(wt));
+    }
   }
+  if (!(stage & 2)) return 0;
+  hipMemsetAsync(frame_cost, 0, sizeof(unsigned long long) * 2 * N, s);
   if (low4 && mv4 && cost4 && w >= 64 && h >= 64) {
     LaGeom q{};
     q.w = (w >> 1) & ~1;
@@ -686,10 +691,12 @@ extern "C" int mivc_launch_lookahead_multi(const uint8_t* low, int w, int h, int
   const long long waves = static_cast<long long>((g.lbw + 15) >> 4) * g.lbh * N;
   const dim3 grid(static_cast<unsigned>((waves + 3) >> 2));
   if (a.wt) {
-    if (range <= 2) hipLaunchKernelGGL((la_multi<2, true>), grid, dim3(256), 0, s, a);
+    if (range <= 1) hipLaunchKernelGGL((la_multi<1, true>), grid, dim3(256), 0, s, a);
+    else if (range <= 2) hipLaunchKernelGGL((la_multi<2, true>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((la_multi<4, true>), grid, dim3(256), 0, s, a);
   } else {
-    if (range <= 2) hipLaunchKernelGGL(la_multi<2>, grid, dim3(256), 0, s, a);
+    if (range <= 1) hipLaunchKernelGGL(la_multi<1>, grid, dim3(256), 0, s, a);
+    else if (range <= 2) hipLaunchKernelGGL(la_multi<2>, grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL(la_multi<4>, grid, dim3(256), 0, s, a);
   }
   return 0;

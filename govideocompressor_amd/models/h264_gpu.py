@@ -105,6 +105,9 @@ class H264Params:
     # pictures in every coding step, so each step runs both the P and the B kernels at partial
     # width (same-box A/B: 9.9k vs 13.0k fps at the headline config, profiles/r5_badapt_ab.md)
     badapt_shared: bool = True
+    # radius of the lowres refinement around the distance-scaled vector in la_multi (the P
+    # costs at distance >= 2 and the list-1 search of the B cost): 2 = +-2 lowres pixels
+    badapt_range: int = 2
     # x264 seeds its motion search from the lookahead's lowres motion: the P search and both B
     # searches get one more candidate, the picture's lowres vector x 2 scaled to its reference
     # distance (when the lookahead ran on the coded MB grid)
@@ -1274,7 +1277,7 @@ class GpuH264Encoder:
         else:
             costs_d, blk, mv = la.frame_costs(y), None, None
         if badapt:
-            multi = la.multi_costs(y, blk, mv, min(7, self.nb + 1)).cpu().numpy()
+            multi = la.multi_costs(y, blk, mv, min(7, self.nb + 1), search_range=int(self.p.badapt_range)).cpu().numpy()
             multi_intra = la.last_multi_intra.cpu().numpy()
         costs = costs_d.cpu().numpy()
         return dict(costs=costs, multi=multi, multi_intra=multi_intra, mbtree=mbtree, use_mbtree=use_mbtree, blocks=lbw * lbh,

@@ -33,6 +33,7 @@ H264 = {
     "MIVC_B_BIAS": "b_bias",
     "MIVC_BADAPT_GUARD": "badapt_guard",
     "MIVC_BADAPT_SHARED": "badapt_shared",
+    "MIVC_BADAPT_RANGE": "badapt_range",
     "MIVC_LA_SEED": "lowres_seed",
     "MIVC_B_ME_RANGE": "b_me_range",
     "MIVC_SKIP_REFINE": "skip_refine",

@@ -115,16 +115,23 @@ class GpuLookahead:
                 self._mv4 = torch.empty((n * qbw * qbh,), dtype=torch.int32, device=self.dev)
                 self._cost4 = torch.empty((n, 2), dtype=torch.int64, device=self.dev)
             low4, mv4, cost4 = self._low4.data_ptr(), self._mv4.data_ptr(), self._cost4.data_ptr()
-        wt = wst = 0
+        args = (y.data_ptr(), w, h, y.stride(1), n, F, low.data_ptr(), cost.data_ptr(),
+                blk.data_ptr() if blk is not None else 0, self.range, torch.cuda.current_stream(self.dev).cuda_stream,
+                mv.data_ptr() if mv is not None else 0, low4, mv4, cost4)
+        self._any_weighted = False
         if self.weighted:
+            # planes and weights first; the weighted cost kernels (more registers) only when some
+            # picture is weighted -- steady content runs the plain ones (one host sync, on the
+            # lookahead's own stream / thread)
             self._wt = torch.empty((B, F, 8, 2), dtype=torch.float32, device=self.dev)
             self._wst = torch.empty((n, 2), dtype=torch.int64, device=self.dev)
-            wt, wst = self._wt.data_ptr(), self._wst.data_ptr()
             self.last_weights = self._wt
-        self.hip.lookahead(y.data_ptr(), w, h, y.stride(1), n, F, low.data_ptr(), cost.data_ptr(),
-                           blk.data_ptr() if blk is not None else 0, self.range,
-                           torch.cuda.current_stream(self.dev).cuda_stream, mv.data_ptr() if mv is not None else 0,
-                           low4, mv4, cost4, wt, wst, self.wt_min_mean, self.wt_min_scale)
+            self.hip.lookahead(*args, self._wt.data_ptr(), self._wst.data_ptr(), self.wt_min_mean, self.wt_min_scale, 1)
+            self._any_weighted = bool((self._wt[..., 0] > 0).any().item())
+            self.hip.lookahead(*args, self._wt.data_ptr() if self._any_weighted else 0, 0, self.wt_min_mean,
+                               self.wt_min_scale, 2)
+        else:
+            self.hip.lookahead(*args, 0, 0, self.wt_min_mean, self.wt_min_scale, 3)
         out = cost.view(B, F, 2)
         if block_mvs:
             return out, blk, mv
@@ -146,7 +153,7 @@ class GpuLookahead:
         if not 2 <= int(max_dist) <= 7:
             raise ValueError("max_dist in 2..7 (bframes 1..6)")
         out = torch.empty((B * F, 8), dtype=torch.int64, device=self.dev)
-        wt = self._wt.data_ptr() if (self.weighted and getattr(self, "_wt", None) is not None
+        wt = self._wt.data_ptr() if (self.weighted and getattr(self, "_any_weighted", False)
                                      and self._wt.shape[:2] == (B, F)) else 0
         self.hip.lookahead_multi(self._low.data_ptr(), w, h, B * F, F, blk.data_ptr(), mv.data_ptr(), int(max_dist),
                                  int(search_range), out.data_ptr(), torch.cuda.current_stream(self.dev).cuda_stream,

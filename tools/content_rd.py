@@ -73,6 +73,7 @@ CONFIGS = {
     "ba100s": dict(b_adapt=1, b_bias=100, badapt_shared=True),   # one pattern per batch
     "ba100p": dict(b_adapt=1, b_bias=100, badapt_shared=False),  # one pattern per slot
     "ba70s": dict(b_adapt=1, b_bias=70, badapt_shared=True),
+    "ba100r1": dict(b_adapt=1, b_bias=100, badapt_range=1),  # la_multi refinement +-1
     # fast spatial direct with the fixed GOP pattern: exact motion re-predicted (tol -1, round 4's
     # first version) / estimate kept as explicit motion beyond 0 / 4 quarter samples; b-pyramid
     "sp_repredict": dict(direct="spatial", spatial_fix_tol=-1),

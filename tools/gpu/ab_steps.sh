@@ -11,7 +11,7 @@ for r in $(seq 1 "$rounds"); do
     label=${spec%%=*}; envs=${spec#*=}
     env $envs timeout -k 10 240 python bench.py --allow-knobs --steps "$steps" --warmup 2 --no-quality $AB_ARGS > "$out/$label.r$r.log" 2>&1
     rc=$?
-    echo "$label round $r rc=$rc $(grep -h '"metric"' "$out/$label.r$r.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); q=d["quality"]; print(d["value"], d["ms_per_step"], q.get("merged_sha256_16"), " ".join(f"{k}={v}" for k, v in d["stage_device_ms_per_step_rank0"].items() if k != "measured_on"))' 2>/dev/null)" | tee -a "$out/ab.txt"
+    echo "$label round $r rc=$rc $(grep -h '"metric"' "$out/$label.r$r.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); q=d["quality"]; print(d["value"], d["ms_per_step"], q.get("merged_sha256_16"), "host_blocked_s=%s" % d.get("timings_rank0_s", {}).get("host_blocked_s"), " ".join(f"{k}={v}" for k, v in d["stage_device_ms_per_step_rank0"].items() if k != "measured_on"))' 2>/dev/null)" | tee -a "$out/ab.txt"
     case $rc in 0) ;; *) exit $rc ;; esac
   done
 done
