@@ -87,11 +87,13 @@ class H264Params:
     bframes: int = 3
     b_qp_offset: float = 6.0 * math.log2(1.3)
     # x264 --b-adapt: 1 ("fast", x264's default) places B pictures per slot from the lookahead's
-    # lowres costs (rc/badapt.py, lookahead.hip la_multi); 0 = the fixed pattern.  Measured
-    # over the seven content classes (profiles/r4_content_rd.md): x264's rule on these lowres
-    # costs (integer-pel, no lowres weighting) places too few B pictures for this encoder,
-    # whose B pictures are cheap -- +10 % BD-rate against the fixed pattern (+6 % at
-    # --b-bias 40), a gain on fast pans only -- so the fixed pattern is the default
+    # lowres costs (rc/badapt.py, lookahead.hip la_multi); 0 = the fixed pattern.  Round 4
+    # measured +10 % BD-rate against the fixed pattern (profiles/r4_content_rd.md: the
+    # unweighted integer-pel lowres costs made fades look like new content and the rule placed
+    # too few of this encoder's cheap B pictures).  With lowres weighting (la_weights) and
+    # --b-bias 100, one pattern per batch: -1.85 % BD-rate on the suite mean, but -3.2 % fps at
+    # the headline (profiles/r5_badapt_rd.md) -- the default keeps the fixed pattern's
+    # throughput, -preset slow and up place B pictures adaptively
     b_adapt: int = 0
     # x264 --b-bias: > 0 places more B pictures (B costs * 100 / (120 + bias), run thresholds)
     b_bias: int = 0

@@ -18,8 +18,8 @@ faster      quarter-pel, radius 8, one skip-refine pass, 2 references (--subme 4
 fast        quarter-pel, radius 8, 2 skip-refine passes, 2 references (--subme 6 --ref 2)
 medium      defaults (x264 defaults, the reference's "264" preset: --ref 3, weightp, trellis 1;
             4 skip-refine passes)
-slow        radius 12, B radius 6, Intra4x4 in P pictures, 4 references, 5 skip-refine passes
-            (--me umh --subme 8 --ref 5)
+slow        radius 12, B radius 6, Intra4x4 in P pictures, 4 references, 5 skip-refine passes,
+            adaptive B placement (--me umh --subme 8 --ref 5 --b-adapt 1)
 slower      radius 16, B radius 8, lookahead radius 8, 4 references, spatial direct, 6
             skip-refine passes (--subme 9 --me umh --ref 8 --direct spatial)
 veryslow    slower + 8 skip-refine passes (--subme 10 --me umh --merange 24 --ref 16)
@@ -53,7 +53,10 @@ H264 = {
     # wavefront (-2.2 % vs temporal, profiles/r3_direct_rd.md -- the parallel fast path loses,
     # profiles/r4_trellis_spatial_rd.md).  Skip-refine passes beyond medium's 4: each one
     # ~-0.7 % BD-rate and ~-0.65 % fps at the headline (profiles/r4_knob_sweep.md)
-    "slow": dict(me_range=12, b_me_range=6, i4x4_in_p=True, refs=4, b_gate=1200, skip_refine=5),
+    # slow also places its B pictures adaptively (x264 --b-adapt 1 at --b-bias 100 on weighted
+    # lowres costs, one pattern per batch): -1.85 % BD-rate on the content suite for -3.2 % fps
+    # at the headline (profiles/r5_badapt_rd.md) -- medium keeps the fixed pattern's throughput
+    "slow": dict(me_range=12, b_me_range=6, i4x4_in_p=True, refs=4, b_gate=1200, skip_refine=5, b_adapt=1, b_bias=100),
     "slower": dict(me_range=16, b_me_range=8, i4x4_in_p=True, la_range=8, skip_refine=6, refs=4, direct="spatial",
                    spatial_wavefront=True, b_gate=1200),
     "veryslow": dict(me_range=16, b_me_range=8, i4x4_in_p=True, la_range=8, skip_refine=8, refs=4, direct="spatial",
