@@ -147,26 +147,34 @@ __device__ __forceinline__ uint32_t la_inv_weight4(uint32_t s, float inv_w, floa
   return r;
 }
 
-// per-frame sums of the lowres interior (lw x lh): [N][2] = sum, sum of squares
+// per-frame sums of the lowres interior (lw x lh): [N][2] = sum, sum of squares.  Grid
+// (row groups, N): a block walks rows blockIdx.x, + gridDim.x, ...; a lane takes 4 samples
+// per dword load (the interior starts kLaPad = 16 bytes into a row of a multiple of 8), sums
+// and squares on the dot-product unit
 __global__ __launch_bounds__(256) void la_stats(const uint8_t* __restrict__ low, LaGeom g,
                                                 unsigned long long* __restrict__ st) {
   const int n = blockIdx.y;
   const int lw = g.w >> 1, lh = g.h >> 1;
+  const int w4 = (lw + 3) >> 2, tail = lw & 3;
   const uint8_t* p = low + n * g.lsize + static_cast<long long>(kLaPad) * g.ls + kLaPad;
-  unsigned long long s = 0, s2 = 0;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < lw * lh; i += gridDim.x * 256) {
-    const int y = i / lw, x = i - y * lw;
-    const unsigned int v = p[static_cast<long long>(y) * g.ls + x];
-    s += v;
-    s2 += v * v;
+  uint32_t s = 0, s2 = 0;
+  for (int y = blockIdx.x; y < lh; y += gridDim.x) {
+    const uint32_t* row = reinterpret_cast<const uint32_t*>(p + static_cast<long long>(y) * g.ls);
+    for (int x = threadIdx.x; x < w4; x += 256) {
+      uint32_t v = row[x];
+      if (tail && x == w4 - 1) v &= (1u << (8 * tail)) - 1u;  // samples past lw (the border copy)
+      s = __builtin_amdgcn_udot4(v, 0x01010101u, s, false);
+      s2 = __builtin_amdgcn_udot4(v, v, s2, false);
+    }
   }
+  unsigned long long s64 = s, q64 = s2;
   for (int off = 32; off > 0; off >>= 1) {
-    s += __shfl_xor(s, off, 64);
-    s2 += __shfl_xor(s2, off, 64);
+    s64 += __shfl_xor(s64, off, 64);
+    q64 += __shfl_xor(q64, off, 64);
   }
   if ((threadIdx.x & 63) == 0) {
-    atomicAdd(st + 2 * n, s);
-    atomicAdd(st + 2 * n + 1, s2);
+    atomicAdd(st + 2 * n, s64);
+    atomicAdd(st + 2 * n + 1, q64);
   }
 }
 
@@ -618,7 +626,7 @@ extern "C" int mivc_launch_lookahead(const uint8_t* y, int w, int h, long long f
     hipLaunchKernelGGL(la_downscale, dim3(static_cast<unsigned>((dwords + 255) / 256)), dim3(256), 0, s, y, g, low);
     if (wt && wstats) {  // lowres weighting: statistics of the lowres planes, then the weights
       hipMemsetAsync(wstats, 0, sizeof(unsigned long long) * 2 * N, s);
-      hipLaunchKernelGGL(la_stats, dim3(8, N), dim3(256), 0, s, low, g, wstats);
+      hipLaunchKernelGGL(la_stats, dim3(8, N), dim3(256), 0, s, low, g, wstats);  // 8 row groups per picture
       hipLaunchKernelGGL(la_weights, dim3((N * kLaWtCols + 255) / 256), dim3(256), 0, s, wstats, g, thr_mean, thr_scale,
                          reinterpret_cast<float2*>(wt));
     }
