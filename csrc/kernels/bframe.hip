@@ -1254,6 +1254,12 @@ struct PRefineArgs {
   const int8_t* aq;
   const SlotRoute* rt;      // routed (route.h): ref / hp are pools, P slots' RefPicList0[0]
   int nbuf;
+  // Jacobi passes after the first (p_mv_refine): which MBs changed their vector in the previous
+  // pass (nullable: every MB is evaluated).  An MB whose own and whose neighbours' (A, B, C,
+  // D) vectors stayed put would derive the same skip predictor at the same cost -- it only
+  // copies its vector through.  chg_out: this pass's changes
+  const uint8_t* chg_in;
+  uint8_t* chg_out;
 };
 
 __device__ __forceinline__ int median3(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
@@ -1277,6 +1283,20 @@ __global__ __launch_bounds__(64) void p_mv_refine(PRefineArgs a) {
   const int mx = mb % g.wmb, my = mb / g.wmb;
   const int16_t* mv = a.mv_in + static_cast<size_t>(slot) * nmb * 2;
   const int cx = mv[mb * 2], cy = mv[mb * 2 + 1];
+  if (a.chg_in) {  // row-uniform
+    const uint8_t* c = a.chg_in + static_cast<size_t>(slot) * nmb;
+    bool any = c[mb];
+    if (mx > 0) any = any || c[mb - 1];
+    if (my > 0) any = any || c[mb - g.wmb] || (mx + 1 < g.wmb && c[mb - g.wmb + 1]) || (mx > 0 && c[mb - g.wmb - 1]);
+    if (!any) {
+      if (lane == 0) {
+        a.mv_out[o * 2] = static_cast<int16_t>(cx);
+        a.mv_out[o * 2 + 1] = static_cast<int16_t>(cy);
+        if (a.chg_out) a.chg_out[o] = 0;
+      }
+      return;
+    }
+  }
   // P_Skip predictor from the neighbours' current vectors (all list 0, ref 0)
   const bool hasA = mx > 0, hasB = my > 0, hasC = my > 0 && mx < g.wmb - 1, hasD = mx > 0 && my > 0;
   int sx = 0, sy = 0;
@@ -1294,6 +1314,7 @@ __global__ __launch_bounds__(64) void p_mv_refine(PRefineArgs a) {
     if (lane == 0) {
       a.mv_out[o * 2] = static_cast<int16_t>(cx);
       a.mv_out[o * 2 + 1] = static_cast<int16_t>(cy);
+      if (a.chg_out) a.chg_out[o] = 0;
     }
     return;
   }
@@ -1325,6 +1346,7 @@ __global__ __launch_bounds__(64) void p_mv_refine(PRefineArgs a) {
     a.mv_out[o * 2] = static_cast<int16_t>(take ? sx : cx);
     a.mv_out[o * 2 + 1] = static_cast<int16_t>(take ? sy : cy);
     if (take) a.cost[o] = satd + lambda * (mvbits_se(sx - pmx) + mvbits_se(sy - pmy));
+    if (a.chg_out) a.chg_out[o] = take;  // (take moves the vector: sx, sy != cx, cy here)
   }
 }
 
@@ -1441,6 +1463,11 @@ struct HevcBArgs {
   int bslice;                   // 0: P picture (list 0 only)
   int max_merge;                // MaxNumMergeCand
   int ctu_shift;                // log2(CTU size / 16): 1 for 32x32 CTBs, 2 for 64x64 CTUs
+  // merge passes: blocks whose motion the previous pass changed (nullable: every block is
+  // re-evaluated); a block whose own and whose neighbours' motion stayed put would rebuild the
+  // same list at the same costs, so it only copies its motion through
+  const uint8_t* chg_in;
+  uint8_t* chg_out;
 };
 
 // z-scan availability (6.4.1) of the 16x16 block (nx, ny) for the block (mx, my) on the 16x16
@@ -1548,6 +1575,20 @@ __global__ __launch_bounds__(64) void hevc_b_merge(HevcBArgs a) {
   const int mx = mb % g.wmb, my = mb / g.wmb;
   const int q = (mx & 1) | ((my & 1) << 1);
   const int maxc = a.max_merge;
+  if (a.chg_in) {  // row-uniform (one MB per 16-lane row)
+    const uint8_t* c = a.chg_in + sb;
+    bool any = c[mb];
+    if (mx > 0) any = any || c[mb - 1] || (my + 1 < g.hmb && c[mb + g.wmb - 1]);
+    if (my > 0) any = any || c[mb - g.wmb] || (mx > 0 && c[mb - g.wmb - 1]) || (mx + 1 < g.wmb && c[mb - g.wmb + 1]);
+    if (!any) {
+      if (lane == 0) {
+        *reinterpret_cast<uint2*>(a.mvb_out + o * 4) = *reinterpret_cast<const uint2*>(a.mvb_in + o * 4);
+        a.dir_out[o] = a.dir_in[o];
+        if (a.chg_out) a.chg_out[o] = 0;
+      }
+      return;
+    }
+  }
   int kd[6], kv[6][4], nk = 0;
   auto load = [&](int n, int* d, int* w) {
     const int dd = a.dir_in[sb + n];
@@ -1662,6 +1703,13 @@ __global__ __launch_bounds__(64) void hevc_b_merge(HevcBArgs a) {
   }
   if (lane == 0) {
     int16_t* m = a.mvb_out + o * 4;
+    if (a.chg_out) {  // the motion (not just its cost) differs from the pass's input
+      bool moved = false;
+#pragma unroll
+      for (int t = 0; t < 6; ++t)
+        if (t == bj) moved = !same(kd[t], kv[t], cd, cw);
+      a.chg_out[o] = moved;
+    }
     if (bj >= 0) {
       int bd = 0, bw[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -1970,8 +2018,11 @@ extern "C" void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src
 extern "C" void mivc_launch_p_refine(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref,
                                      const uint8_t* hp, const int16_t* mv_in, int16_t* mv_out, int* cost,
                                      const int16_t* pm, uint8_t* pred, const int* qp, const int8_t* aq,
-                                     void* stream, const void* route, int nbuf) {
+                                     void* stream, const void* route, int nbuf, const uint8_t* chg_in,
+                                     uint8_t* chg_out) {
   PRefineArgs a;
+  a.chg_in = chg_in;
+  a.chg_out = chg_out;
   a.rt = static_cast<const SlotRoute*>(route);
   a.nbuf = nbuf;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
@@ -2016,6 +2067,8 @@ extern "C" void mivc_launch_hevc_merge_refine(int B, int wmb, int hmb, const uin
                                               const uint8_t* hp, const int16_t* mv_in, int16_t* mv_out, int* cost,
                                               const int16_t* pm, const int* qp, const int8_t* aq, void* stream) {
   PRefineArgs a;
+  a.chg_in = nullptr;
+  a.chg_out = nullptr;
   a.rt = nullptr;
   a.nbuf = 0;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
@@ -2039,8 +2092,10 @@ extern "C" void mivc_launch_hevc_b(int mode, int B, int wmb, int hmb, const uint
                                    const int16_t* pm1, const int16_t* tmv, const uint8_t* tdir, const int16_t* mvb_in,
                                    const uint8_t* dir_in, int16_t* mvb_out, uint8_t* dir_out, int* cost, int* bits,
                                    const int* qp, const int8_t* aq, void* stream, int bslice, int max_merge,
-                                   int ctu64) {
+                                   int ctu64, const uint8_t* chg_in, uint8_t* chg_out) {
   HevcBArgs a;
+  a.chg_in = chg_in;
+  a.chg_out = chg_out;
   a.ctu_shift = ctu64 ? 2 : 1;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};
   a.src_y = src_y;

@@ -44,7 +44,8 @@ void mivc_launch_b_spatial_fixup(int B, int wmb, int hmb, const void* hdr, const
                                  void* stream, const void* route, int nbuf);
 void mivc_launch_p_refine(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref, const uint8_t* hp,
                           const int16_t* mv_in, int16_t* mv_out, int* cost, const int16_t* pm, uint8_t* pred,
-                          const int* qp, const int8_t* aq, void* stream, const void* route, int nbuf);
+                          const int* qp, const int8_t* aq, void* stream, const void* route, int nbuf,
+                          const uint8_t* chg_in, uint8_t* chg_out);
 void mivc_launch_b_decide(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref0, const uint8_t* ref1,
                           const uint8_t* hp0, const uint8_t* hp1, const int16_t* mv0, const int16_t* mv1,
                           const int* cost0, const int* cost1, const uint8_t* pred0, const uint8_t* pred1,
@@ -115,7 +116,7 @@ void mivc_launch_hevc_b(int mode, int B, int wmb, int hmb, const uint8_t* src_y,
                         const uint8_t* hp0, const uint8_t* hp1, const int16_t* mv0, const int16_t* mv1, const int* cost0,
                         const int* cost1, const int16_t* pm0, const int16_t* pm1, const int16_t* tmv, const uint8_t* tdir,
                         const int16_t* mvb_in, const uint8_t* dir_in, int16_t* mvb_out, uint8_t* dir_out, int* cost,
-                        int* bits, const int* qp, const int8_t* aq, void* stream, int bslice, int max_merge, int ctu64);
+                        int* bits, const int* qp, const int8_t* aq, void* stream, int bslice, int max_merge, int ctu64, const uint8_t* chg_in, uint8_t* chg_out);
 void mivc_launch_hevc_deblock(int B, int W, int H, int bd, uint16_t* y, uint16_t* u, uint16_t* v, const void* cu,
                               const void* ctu, const int8_t* run, void* stream);
 void mivc_launch_hevc_aq(int B, int W, int H, int bd, const uint16_t* sy, const uint16_t* su, const uint16_t* sv,
@@ -286,14 +287,15 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("p_refine", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref, uintptr_t hp, uintptr_t mv_in,
                        uintptr_t mv_out, uintptr_t cost, uintptr_t pm, uintptr_t pred, uintptr_t qp, uintptr_t aq,
-                       uintptr_t stream, uintptr_t route, int nbuf) {
+                       uintptr_t stream, uintptr_t route, int nbuf, uintptr_t chg_in, uintptr_t chg_out) {
     if (mv_in == mv_out) throw std::invalid_argument("p_refine: mv_in and mv_out must differ (Jacobi pass)");
+    if (chg_in && chg_in == chg_out) throw std::invalid_argument("p_refine: chg_in and chg_out must differ");
     mivc_launch_p_refine(B, wmb, hmb, P<uint8_t>(src), P<uint8_t>(ref), P<uint8_t>(hp), P<int16_t>(mv_in),
                          P<int16_t>(mv_out), P<int>(cost), P<int16_t>(pm), P<uint8_t>(pred), P<int>(qp),
-                         P<int8_t>(aq), S(stream), P<void>(route), nbuf);
+                         P<int8_t>(aq), S(stream), P<void>(route), nbuf, P<uint8_t>(chg_in), P<uint8_t>(chg_out));
   }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("src"), py::arg("ref"), py::arg("hp"), py::arg("mv_in"),
      py::arg("mv_out"), py::arg("cost"), py::arg("pm"), py::arg("pred"), py::arg("qp"), py::arg("aq"),
-     py::arg("stream"), py::arg("route") = 0, py::arg("nbuf") = 0);
+     py::arg("stream"), py::arg("route") = 0, py::arg("nbuf") = 0, py::arg("chg_in") = 0, py::arg("chg_out") = 0);
   m.def("b_decide", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref0, uintptr_t ref1, uintptr_t hp0,
                        uintptr_t hp1, uintptr_t mv0, uintptr_t mv1, uintptr_t cost0, uintptr_t cost1, uintptr_t pred0,
                        uintptr_t pred1, uintptr_t pm0, uintptr_t pm1, uintptr_t dmv, uintptr_t qp, uintptr_t aq,
@@ -508,7 +510,7 @@ PYBIND11_MODULE(_hip, m) {
                      uintptr_t hp1, uintptr_t mv0, uintptr_t mv1, uintptr_t cost0, uintptr_t cost1, uintptr_t pm0,
                      uintptr_t pm1, uintptr_t tmv, uintptr_t tdir, uintptr_t mvb_in, uintptr_t dir_in, uintptr_t mvb_out,
                      uintptr_t dir_out, uintptr_t cost, uintptr_t bits, uintptr_t qp, uintptr_t aq, uintptr_t stream,
-                     int bslice, int max_merge, int ctu64) {
+                     int bslice, int max_merge, int ctu64, uintptr_t chg_in, uintptr_t chg_out) {
     // mode 0: L0 / L1 / bi choice from the two searches; 1: one merge-aware Jacobi pass;
     // 2: a P picture's list-0 search in the same motion form
     if (mode < 0 || mode > 2) throw std::invalid_argument("hevc_b: mode 0 (choose), 1 (merge pass) or 2 (P init)");
@@ -527,12 +529,12 @@ PYBIND11_MODULE(_hip, m) {
                        P<uint8_t>(hp1), P<int16_t>(mv0), P<int16_t>(mv1), P<int>(cost0), P<int>(cost1), P<int16_t>(pm0),
                        P<int16_t>(pm1), P<int16_t>(tmv), P<uint8_t>(tdir), P<int16_t>(mvb_in), P<uint8_t>(dir_in),
                        P<int16_t>(mvb_out), P<uint8_t>(dir_out), P<int>(cost), P<int>(bits), P<int>(qp), P<int8_t>(aq),
-                       S(stream), bslice, max_merge, ctu64);
+                       S(stream), bslice, max_merge, ctu64, P<uint8_t>(chg_in), P<uint8_t>(chg_out));
   }, py::arg("mode"), py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("src"), py::arg("ref0"), py::arg("ref1"),
      py::arg("hp0"), py::arg("hp1"), py::arg("mv0"), py::arg("mv1"), py::arg("cost0"), py::arg("cost1"), py::arg("pm0"),
      py::arg("pm1"), py::arg("tmv"), py::arg("tdir"), py::arg("mvb_in"), py::arg("dir_in"), py::arg("mvb_out"),
      py::arg("dir_out"), py::arg("cost"), py::arg("bits"), py::arg("qp"), py::arg("aq"), py::arg("stream"),
-     py::arg("bslice") = 1, py::arg("max_merge") = 5, py::arg("ctu64") = 0);
+     py::arg("bslice") = 1, py::arg("max_merge") = 5, py::arg("ctu64") = 0, py::arg("chg_in") = 0, py::arg("chg_out") = 0);
   m.def("hevc_deblock", [](int B, int W, int H, int bd, uintptr_t y, uintptr_t u, uintptr_t v, uintptr_t cu,
                            uintptr_t ctu, uintptr_t run, uintptr_t stream) {
     mivc_launch_hevc_deblock(B, W, H, bd, P<uint16_t>(y), P<uint16_t>(u), P<uint16_t>(v), P<void>(cu), P<void>(ctu),

@@ -121,6 +121,10 @@ class H264Params:
     # p_mv_refine): 0 disables.  Each pass settles the field one MB further: 2 -> 4 passes is
     # -2.55 % BD-rate on the content suite for -1.3 % headline fps (profiles/r4_knob_sweep.md)
     skip_refine: int = 4
+    # skip-refine passes after the first re-evaluate only MBs next to an MB the previous pass
+    # moved (exact: the others derive the same predictor at the same cost); False = every MB
+    # every pass (A/B switch)
+    refine_skip: bool = True
     # x264 --8x8dct (default on): High profile, the 8x8 transform chosen per inter MB where
     # its sa8d beats the 4x4 satd; CABAC only (the CAVLC path stays Constrained Baseline)
     t8x8: bool = True
@@ -701,10 +705,14 @@ class GpuH264Encoder:
                 self.hip.me(B, wmb, hmb, sy_me, py, P(self.prev_mv), P(self.mv), P(self.me_cost), P(self.pred),
                             P(self.intra_cost), P(self.qp), self.p.me_range, self.p.subpel, s, hpp, aq, 1,
                             self.p.p_early_sad, 0, 0, 0, rt, NB, 0, SK["P"], seed0)
+                if getattr(self, "_chg", None) is None:  # p_mv_refine change masks (passes >= 2 skip settled MBs)
+                    self._chg = [torch.zeros((B, self.nmb), dtype=torch.uint8, device=self.dev) for _ in range(2)]
                 for it in range(int(self.p.skip_refine)):
                     a_, b_ = (self.mv, self.mv_tmp) if it % 2 == 0 else (self.mv_tmp, self.mv)
                     self.hip.p_refine(B, wmb, hmb, sy_me, py, hpp, P(a_), P(b_), P(self.me_cost), P(self.prev_mv),
-                                      P(self.pred), P(self.qp), aq, s, rt, NB)
+                                      P(self.pred), P(self.qp), aq, s, rt, NB,
+                                      0 if (it == 0 or not self.p.refine_skip) else P(self._chg[(it - 1) % 2]),
+                                      P(self._chg[it % 2]) if self.p.refine_skip else 0)
                 if int(self.p.skip_refine) % 2:
                     self.mv.copy_(torch.where(st["pmask"][:, None, None], self.mv_tmp, self.mv))
             mv8 = 0

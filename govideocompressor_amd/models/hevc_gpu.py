@@ -112,6 +112,10 @@ class HevcParams:
     # (bframe.hip hevc_b_merge; P and B pictures); False: P pictures use the neighbour-vector
     # approximation of round 2 (hevc_merge_refine)
     merge_exact: bool = True
+    # merge passes after the first re-evaluate only blocks next to a block the previous pass
+    # moved (exact: the others would rebuild the same lists at the same costs); False = every
+    # block every pass (A/B switch)
+    merge_skip: bool = True
     # x265 --ctu 64 (its default): 64x64 coding tree units over the 32x32 record blocks (the
     # blocks are the CTU's quantization groups and are reconstructed in z-order; one SAO
     # parameter set per CTU; 64x64 skip CUs where four blocks agree) -- False: 32x32 CTBs
@@ -295,6 +299,16 @@ class GpuHevcEncoder:
         # per-stage device time (HIP events, resolved once per encode): MIVC_STAGE_TIMING=1
         from ..obs.timers import EventTimer
         self.stage_timer = EventTimer(enabled=os.environ.get("MIVC_STAGE_TIMING", "0") == "1")
+
+    def _chg_args(self, it: int) -> tuple[int, int]:
+        """(chg_in, chg_out) of merge pass ``it``: the first pass evaluates every block and
+        records which moved; later passes re-evaluate only blocks next to a moved one
+        (bframe.hip hevc_b_merge -- the skipped blocks would reach the same decision)."""
+        if not self.p.merge_skip:
+            return 0, 0
+        if getattr(self, "_chg", None) is None:
+            self._chg = [torch.zeros((self.B, self.nmb), dtype=torch.uint8, device=self.dev) for _ in range(2)]
+        return (0 if it == 0 else self._chg[(it - 1) % 2].data_ptr()), self._chg[it % 2].data_ptr()
 
     def _intra_gate(self) -> torch.Tensor:
         """[B, nctb] uint8: CTBs of a P picture where intra may beat the motion search (see
@@ -733,7 +747,8 @@ class GpuHevcEncoder:
                                 i_, o_ = it % 2, (it + 1) % 2
                                 self.hip.hevc_b(1, *pargs, 0, 0, 0, 0, 0, 0, tm_, td_, p(self.mvb[i_]), p(self.dirb[i_]),
                                                 p(self.mvb[o_]), p(self.dirb[o_]), p(self.bcost), p(self.bbits),
-                                                p(self.qp), p(self.mb_aq), s, 0, int(self.p.max_merge), int(self.p.ctu64))
+                                                p(self.qp), p(self.mb_aq), s, 0, int(self.p.max_merge), int(self.p.ctu64),
+                                                *self._chg_args(it))
                             fin = int(self.p.merge_refine) % 2
                             self.me_cost.copy_(self.bcost)
                             self.mv.copy_(self.mvb[fin][..., 0:2])
@@ -768,7 +783,8 @@ class GpuHevcEncoder:
                             i_, o_ = it % 2, (it + 1) % 2
                             self.hip.hevc_b(1, *bargs, 0, 0, 0, 0, 0, 0, tm_, td_, p(self.mvb[i_]), p(self.dirb[i_]),
                                             p(self.mvb[o_]), p(self.dirb[o_]), p(self.bcost), p(self.bbits), p(self.qp),
-                                            p(self.mb_aq), s, 1, int(self.p.max_merge), int(self.p.ctu64))
+                                            p(self.mb_aq), s, 1, int(self.p.max_merge), int(self.p.ctu64),
+                                            *self._chg_args(it))
                         fin = int(self.p.merge_refine) % 2
                         self.me_cost.copy_(self.bcost)
                     r1p = self.rec[r1]

@@ -37,6 +37,7 @@ H264 = {
     "MIVC_LA_SEED": "lowres_seed",
     "MIVC_B_ME_RANGE": "b_me_range",
     "MIVC_SKIP_REFINE": "skip_refine",
+    "MIVC_REFINE_SKIP": "refine_skip",
     "MIVC_BPARTS": "bpartitions",
     "MIVC_PART_OVERHEAD": "part_overhead",
     "MIVC_PART_MIN_SATD": "part_min_satd",
@@ -62,6 +63,7 @@ H264 = {
 HEVC = {
     "MIVC_HEVC_CTU64": "ctu64",
     "MIVC_HEVC_LA_WEIGHTS": "la_weights",
+    "MIVC_HEVC_MERGE_SKIP": "merge_skip",
 }
 # bench.py shape knobs (they change what is measured, so they also need --allow-knobs)
 # (MIVC_HIP_LIB: an alternative kernel library, tools/build_variant.py -- same-box A/B timing)

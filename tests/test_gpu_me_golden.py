@@ -259,9 +259,12 @@ def _refine_ref(src, planes, mv_in, cost, pm, pred, qps, lam_tab, wmb, hmb):
     return mv_out, cost, pred
 
 
-def test_p_refine_matches_numpy(host):
+@pytest.mark.parametrize("masks", [False, True])
+def test_p_refine_matches_numpy(host, masks):
     """p_mv_refine (four MBs per wave, one 4x4 block per lane) against the numpy statement of
-    the pass, over three passes on a near-uniform field; 117 MBs leave a partial last wave."""
+    the pass, over four passes on a near-uniform field; 117 MBs leave a partial last wave.
+    ``masks``: passes after the first skip MBs whose own and whose neighbours' vectors did not
+    move in the previous pass (change masks) -- the fields must still equal the full passes'."""
     import torch
     from govideocompressor_amd.ops import native
     hip = native.hip()
@@ -297,10 +300,13 @@ def test_p_refine_matches_numpy(host):
     t_pm, t_qp = torch.from_numpy(pm).to(dev), torch.from_numpy(qps).to(dev)
     lam = host.table("lambda")[0]
     took = 0
-    for it in range(3):
+    chg = [torch.zeros((B, nmb), dtype=torch.uint8, device=dev) for _ in range(2)]
+    for it in range(4):
         a_, b_ = t_mv[it % 2], t_mv[(it + 1) % 2]
+        cin = chg[(it - 1) % 2].data_ptr() if (masks and it > 0) else 0
+        cout = chg[it % 2].data_ptr() if masks else 0
         hip.p_refine(B, wmb, hmb, src.data_ptr(), ref.data_ptr(), hp.data_ptr(), a_.data_ptr(), b_.data_ptr(),
-                     t_cost.data_ptr(), t_pm.data_ptr(), t_pred.data_ptr(), t_qp.data_ptr(), 0, s)
+                     t_cost.data_ptr(), t_pm.data_ptr(), t_pred.data_ptr(), t_qp.data_ptr(), 0, s, 0, 0, cin, cout)
         torch.cuda.synchronize()
         r_mv, r_cost, r_pred = _refine_ref(srcs, planes, mv, cost, pm, pred, qps, lam, wmb, hmb)
         took += int((r_mv != mv).any(axis=2).sum())
