@@ -470,7 +470,7 @@ __device__ __forceinline__ void decode_intra_mb(const DecodeArgs& a, DecIntraSha
       if (lane & 1) S.saved_c[comp][y] = static_cast<uint8_t>(word >> 24);
     }
     if (lane < 16) a.nz[o * 16 + blk_x(lane) + 4 * blk_y(lane)] = 1;
-    if (lane == 0) S.saved_x = mx;
+    if (lane == 0) S.saved_x = my * g.wmb + mx;  // raster index: rows differ
     wave_sync();
     return;
   }
@@ -488,7 +488,7 @@ __device__ __forceinline__ void decode_intra_mb(const DecodeArgs& a, DecIntraSha
   } else if (lane >= 32 && lane < 48) {  // tile col 0, rows 1..16
     const int r = lane - 32;
     uint8_t v = 0;
-    if (mbav & h264::AV_LEFT) v = S.saved_x == mx - 1 ? S.saved_y[r] : recy[static_cast<size_t>(Y0 + r) * W + X0 - 1];
+    if (mbav & h264::AV_LEFT) v = S.saved_x == my * g.wmb + mx - 1 ? S.saved_y[r] : recy[static_cast<size_t>(Y0 + r) * W + X0 - 1];
     S.tile[(r + 1) * TS] = v;
   }
   if (lane < 18) {
@@ -500,7 +500,7 @@ __device__ __forceinline__ void decode_intra_mb(const DecodeArgs& a, DecIntraSha
     const int c = (lane - 48) >> 3, i = (lane - 48) & 7;
     const uint8_t* rc = rec_plane(a, c == 0 ? a.rec_u : a.rec_v, slot, g.csize());
     uint8_t v = 0;
-    if (mbav & h264::AV_LEFT) v = S.saved_x == mx - 1 ? S.saved_c[c][i] : rc[static_cast<size_t>(my * 8 + i) * cw + mx * 8 - 1];
+    if (mbav & h264::AV_LEFT) v = S.saved_x == my * g.wmb + mx - 1 ? S.saved_c[c][i] : rc[static_cast<size_t>(my * 8 + i) * cw + mx * 8 - 1];
     S.cleft[c][i] = v;
   }
   wave_sync();
@@ -703,7 +703,7 @@ __device__ __forceinline__ void decode_intra_mb(const DecodeArgs& a, DecIntraSha
     }
   }
   if (lane < 16) S.saved_y[lane] = S.tile[(lane + 1) * TS + 16];
-  if (lane == 0) S.saved_x = mx;
+  if (lane == 0) S.saved_x = my * g.wmb + mx;  // raster index: rows differ
   wave_sync();
 }
 

@@ -163,6 +163,9 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
   const int W = g.W, cw = g.cw();
   const int X0 = mx * 16, Y0 = my * 16;
   const size_t o = static_cast<size_t>(slot) * g.nmb() + my * g.wmb + mx;
+  // the left MB's edge is in LDS when this wave coded it last: keyed by raster index, not x, so a
+  // P row whose first intra MB is one column right of its previous row's last reads global memory
+  const bool left_saved = S.saved_x == my * g.wmb + mx - 1;
   const int qp = clampi(a.qp[slot] + (a.aq ? a.aq[o] : 0), 0, 51);
   const int qpc = h264::chroma_qp(qp, a.chroma_qp_offset);
   const int lambda = h264::kLambda[qp];
@@ -200,7 +203,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
   } else if (lane >= 32 && lane < 48) {  // tile col 0, rows 1..16
     int r = lane - 32;
     uint8_t v = 0;
-    if (mx > 0) v = S.saved_x == mx - 1 ? S.saved_y[r] : recy[static_cast<size_t>(Y0 + r) * W + X0 - 1];
+    if (mx > 0) v = left_saved ? S.saved_y[r] : recy[static_cast<size_t>(Y0 + r) * W + X0 - 1];
     S.tile[(r + 1) * TS] = v;
   }
   if (lane < 18) {  // chroma neighbours: top-left + top
@@ -213,14 +216,14 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
     int c = (lane - 48) >> 3, i = (lane - 48) & 7;
     const uint8_t* rc = (c == 0 ? a.rec_u : a.rec_v) + rcur * g.csize();
     uint8_t v = 0;
-    if (mx > 0) v = S.saved_x == mx - 1 ? S.saved_c[c][i] : rc[static_cast<size_t>(my * 8 + i) * cw + mx * 8 - 1];
+    if (mx > 0) v = left_saved ? S.saved_c[c][i] : rc[static_cast<size_t>(my * 8 + i) * cw + mx * 8 - 1];
     S.cleft[c][i] = v;
   }
   if (lane >= 24 && lane < 28) {
     int i = lane - 24;  // most-probable-mode context
     int lm = 2, tm = 2;
     if (mx > 0) {
-      if (S.saved_x == mx - 1) {
+      if (left_saved) {
         lm = S.saved_modes[i];
       } else {
         const MbHeader& L = a.hdr[o - 1];
@@ -679,7 +682,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
     S.saved_modes[i] = use4 ? S.modes4[h264::kRasterToBlk[3 + 4 * i]] : (use8 ? S.modes8[(i >> 1) * 2 + 1] : 2);
   }
   if (lane == 63) {
-    S.saved_x = mx;
+    S.saved_x = my * g.wmb + mx;
     h->kind = use8 ? h264::MBK_I8x8 : (use4 ? h264::MBK_I4x4 : h264::MBK_I16x16);
     h->qp = static_cast<int8_t>(qp);
     h->i16_mode = static_cast<uint8_t>(mode16);

@@ -571,3 +571,70 @@ def test_gpu_encode_async_same_bytes(monkeypatch, tiny_pool):
     if tiny_pool:
         assert enc.stats.get("cabac_pool_regrow", 0) >= 1
     enc.close()
+
+
+def test_gpu_intra_in_p_rows_of_one_wave(host):
+    """Intra MBs in a P picture, in two rows the same wave codes (rows y and y + 16 of the
+    16-wave encoder, y and y + 8 / y + 16 of the 8-wave decoder): the second row's first intra
+    MB is one column right of the first row's last one.  The LDS copy of the left MB's
+    right edge must not be taken for it (it used to be keyed by the column alone, which
+    showed as different bytes from the 8- and 16-wave intra kernels): the encoder's recon
+    equals the CPU decoder's, and the GPU decoder reconstructs the same pictures."""
+    from tests.test_gpu_decode import _check
+
+    w, h = 320, 288
+    enc, res, spots = _intra_spots_encode(w, h)
+    pics = host.decode(res[0].bitstream)
+    kinds = np.asarray(pics[1]["mb_kind"]).reshape(h // 16, w // 16)
+    intra = np.isin(kinds, [0, 1, 4, 8])
+    assert all(intra[my, mx] for mx, my in spots), kinds
+    for my in (0, 1):  # nothing between the spots that would refresh the cache legitimately
+        assert not intra[my, spots[2 * my][0] + 1:].any() and not intra[my + 16, :spots[2 * my + 1][0]].any(), kinds
+    _check_roundtrip(host, enc, res, w, h)
+    enc.close()
+    from govideocompressor_amd.models.h264_decode_gpu import GpuH264Decoder
+    _check(host, GpuH264Decoder(), [res[0].bitstream])
+
+
+def _intra_spots_encode(w=320, h=288):
+    """Noise background, static; in the second (P) picture four MBs whose rows repeat the
+    sample left of the MB (Intra16x16 H predicts them, the reference does not)."""
+    import torch
+    from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params
+
+    rng = np.random.default_rng(17)
+    planes = []
+    for ph, pw in ((h, w), (h // 2, w // 2), (h // 2, w // 2)):
+        bg = rng.integers(0, 256, (ph, pw), dtype=np.uint8)
+        planes.append(np.stack([bg, bg.copy()])[None])
+    y1 = planes[0][0, 1]
+    spots = [(3, 0), (4, 16), (10, 1), (11, 17)]
+    for mx, my in spots:
+        rows = slice(my * 16, my * 16 + 16)
+        y1[rows, mx * 16:mx * 16 + 16] = y1[rows, mx * 16 - 1:mx * 16]
+    y, u, v = (torch.from_numpy(np.ascontiguousarray(p)).cuda() for p in planes)
+    enc = GpuH264Encoder(H264Params(width=w, height=h, crf=None, qp=26, bframes=0), slots=1)
+    res = enc.encode(y, u, v, keep_recon=True)
+    torch.cuda.synchronize()
+    return enc, res, spots
+
+
+def test_gpu_intra_waves_knob_keeps_bytes():
+    """MIVC_INTRA_WAVES=8 (the 8-wave intra kernel) is a speed knob: same bytes as the
+    default 16-wave instance (the launcher reads the variable once, so the 8-wave run is a
+    child process)."""
+    import hashlib
+    import os
+    import subprocess
+    import sys
+
+    enc, res, _ = _intra_spots_encode()
+    here = hashlib.sha256(res[0].bitstream).hexdigest()
+    enc.close()
+    code = ("import hashlib; from tests.test_gpu_h264 import _intra_spots_encode; "
+            "print(hashlib.sha256(_intra_spots_encode()[1][0].bitstream).hexdigest())")
+    env = dict(os.environ, MIVC_INTRA_WAVES="8")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.split()[-1] == here
