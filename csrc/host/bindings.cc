@@ -67,6 +67,8 @@ EncoderConfig cfg_from(const py::dict& d) {
   c.weightp = dget<int>(d, "weightp", 0);
   c.constrained_intra = dget<int>(d, "constrained_intra", 0);
   c.level_idc = dget<int>(d, "level_idc", 0);
+  c.bit_depth = dget<int>(d, "bit_depth", 8);
+  if (c.bit_depth < 8 || c.bit_depth > 14) throw std::runtime_error("bit_depth in 8..14");
   c.cqm = dget<int>(d, "cqm", 0);
   c.cqm_coded = dget<int>(d, "cqm_coded", 0xFF);
   if (c.cqm < 0 || c.cqm > 3) throw std::runtime_error("cqm in 0..3");
@@ -94,19 +96,24 @@ py::dict picture_to_dict(const DecodedPicture& p) {
   d["poc"] = p.poc;
   d["idr"] = p.idr;
   d["slice_type"] = p.slice_type;
-  std::vector<uint8_t> i420 = p.cropped_i420();
-  py::array_t<uint8_t> a(static_cast<py::ssize_t>(i420.size()));
-  std::memcpy(a.mutable_data(), i420.data(), i420.size());
-  d["i420"] = a;
-  py::array_t<uint8_t> y({p.coded_height, p.coded_width});
-  std::memcpy(y.mutable_data(), p.y.data(), p.y.size());
-  d["y_coded"] = y;
-  py::array_t<uint8_t> u({p.coded_height / 2, p.coded_width / 2});
-  std::memcpy(u.mutable_data(), p.u.data(), p.u.size());
-  d["u_coded"] = u;
-  py::array_t<uint8_t> v({p.coded_height / 2, p.coded_width / 2});
-  std::memcpy(v.mutable_data(), p.v.data(), p.v.size());
-  d["v_coded"] = v;
+  d["bit_depth"] = p.bit_depth;
+  auto planes = [&](auto tag, const auto& i420, const auto& y, const auto& u, const auto& v) {
+    using T = decltype(tag);
+    py::array_t<T> a(static_cast<py::ssize_t>(i420.size()));
+    std::memcpy(a.mutable_data(), i420.data(), i420.size() * sizeof(T));
+    d["i420"] = a;
+    py::array_t<T> ya({p.coded_height, p.coded_width});
+    std::memcpy(ya.mutable_data(), y.data(), y.size() * sizeof(T));
+    d["y_coded"] = ya;
+    py::array_t<T> ua({p.coded_height / 2, p.coded_width / 2});
+    std::memcpy(ua.mutable_data(), u.data(), u.size() * sizeof(T));
+    d["u_coded"] = ua;
+    py::array_t<T> va({p.coded_height / 2, p.coded_width / 2});
+    std::memcpy(va.mutable_data(), v.data(), v.size() * sizeof(T));
+    d["v_coded"] = va;
+  };
+  if (p.bit_depth > 8) planes(uint16_t{}, p.cropped_i420_16(), p.y16, p.u16, p.v16);  // High 10: uint16 planes
+  else planes(uint8_t{}, p.cropped_i420(), p.y, p.u, p.v);
   py::array_t<int8_t> k(static_cast<py::ssize_t>(p.mb_kind.size()));
   std::memcpy(k.mutable_data(), p.mb_kind.data(), p.mb_kind.size());
   d["mb_kind"] = k;

@@ -381,7 +381,11 @@ class SliceWriter {
     }
     if (kind == MBK_IPCM) {
       bw.align_zero();
-      for (int i = 0; i < 384; ++i) bw.put(static_cast<uint32_t>(c[i]) & 255, 8);
+      // pcm_sample_luma / chroma: BitDepthY / BitDepthC bits each (7.3.5)
+      for (int i = 0; i < 384; ++i) {
+        const int bd = i < 256 ? sps_.bit_depth_luma : sps_.bit_depth_chroma;
+        bw.put(static_cast<uint32_t>(c[i]) & ((1u << bd) - 1), bd);
+      }
       std::fill(m.tc, m.tc + 24, 16);
       qp_prev = qp_prev;  // QP unchanged (QP'Y of I_PCM for deblocking handled by decoder: qPp = 0)
       return;
@@ -483,9 +487,11 @@ class SliceWriter {
     }
     if (cbp_luma == 0 && cbp_chroma == 0 && kind != MBK_I16x16) return;
     // ---- mb_qp_delta
+    // mb_qp_delta in -(26 + QpBdOffsetY / 2) .. 25 + QpBdOffsetY / 2, modulo 52 + QpBdOffsetY (7.4.5)
+    const int qpbd = 6 * (sps_.bit_depth_luma - 8);
     int d = mb.qp - qp_prev;
-    if (d < -26) d += 52;
-    if (d > 25) d -= 52;
+    if (d < -(26 + qpbd / 2)) d += 52 + qpbd;
+    if (d > 25 + qpbd / 2) d -= 52 + qpbd;
     bw.put_se(d);
     qp_prev = mb.qp;
     // ---- residual

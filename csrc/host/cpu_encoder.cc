@@ -21,7 +21,11 @@ SPS make_sps(const EncoderConfig& cfg) {
   s.height_mbs = (cfg.height + 15) / 16;
   s.crop_right = (s.width_mbs * 16 - cfg.width) / 2;
   s.crop_bottom = (s.height_mbs * 16 - cfg.height) / 2;
-  if (cfg.t8x8) {
+  if (cfg.bit_depth > 8) {
+    s.profile_idc = 110;  // High 10 (A.2.5; bit depths up to 10 -- deeper ones are written as such)
+    s.constraint_flags = 0;
+    s.bit_depth_luma = s.bit_depth_chroma = cfg.bit_depth;
+  } else if (cfg.t8x8) {
     s.profile_idc = 100;  // High
     s.constraint_flags = 0;
   } else if (cfg.cabac || cfg.bframes > 0) {

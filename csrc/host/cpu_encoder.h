@@ -33,6 +33,9 @@ struct EncoderConfig {
   // bframes = consecutive B pictures (POC type 0 and reordering); refs = active L0 refs
   int cabac = 0;
   int t8x8 = 0;
+  // sample bit depth of the written stream: 9..14 = High 10 SPS (the CPU encoder itself is 8-bit;
+  // the record writer takes deeper I_PCM samples and QPs down to -QpBdOffsetY)
+  int bit_depth = 8;
   int bframes = 0;
   int pyramid = 0;          // x264 --b-pyramid normal: some B pictures are references (reorder depth 2)
   int refs = 1;

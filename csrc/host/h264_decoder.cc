@@ -40,6 +40,23 @@ std::vector<uint8_t> DecodedPicture::cropped_i420() const {
   return o;
 }
 
+std::vector<uint16_t> DecodedPicture::cropped_i420_16() const {
+  std::vector<uint16_t> o(static_cast<size_t>(width) * height * 3 / 2);
+  uint16_t* dst = o.data();
+  const int cw = coded_width / 2, w2 = width / 2, h2 = height / 2;
+  for (int yy = 0; yy < height; ++yy)
+    std::memcpy(dst + static_cast<size_t>(yy) * width, y16.data() + static_cast<size_t>(yy + crop_y) * coded_width + crop_x,
+                width * sizeof(uint16_t));
+  dst += static_cast<size_t>(width) * height;
+  for (const std::vector<uint16_t>* pl : {&u16, &v16}) {
+    for (int yy = 0; yy < h2; ++yy)
+      std::memcpy(dst + static_cast<size_t>(yy) * w2, pl->data() + static_cast<size_t>(yy + crop_y / 2) * cw + crop_x / 2,
+                  w2 * sizeof(uint16_t));
+    dst += static_cast<size_t>(w2) * h2;
+  }
+  return o;
+}
+
 namespace {
 
 struct Pic {
@@ -48,7 +65,7 @@ struct Pic {
   bool short_ref = false, long_ref = false;
   int long_idx = -1;
   bool mmco5 = false;
-  std::vector<uint8_t> Y, U, V;
+  std::vector<uint16_t> Y, U, V;  // samples of BitDepthY / BitDepthC bits
   std::vector<int> slice;        // per MB slice index, -1 = not decoded
   std::vector<int8_t> kind, qp, qp_dbk, t8x8, skip, chroma_mode;
   std::vector<uint8_t> cbp, direct;  // direct: bit q = quadrant predicted in direct mode
@@ -145,7 +162,7 @@ struct SliceParams {
 };
 
 inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
-inline int clip_px(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
+inline int clip_px(int v, int maxv) { return v < 0 ? 0 : (v > maxv ? maxv : v); }
 inline int med3(int a, int b, int c) { return std::max(std::min(a, b), std::min(std::max(a, b), c)); }
 
 // --- independent implementations of the normative arithmetic ------------------
@@ -391,6 +408,16 @@ struct Decoder::Impl {
   int max_frame_num = 16;
   bool skip_deblock = false;
   bool parse_only = false;
+  // sample bit depths of the active SPS (High 10 and up: 9..14 bits; 7.4.2.1.1) and the QP
+  // range extension QpBdOffset = 6 * (BitDepth - 8) (7-4, 7-6)
+  int bdY = 8, bdC = 8, maxY = 255, maxC = 255, qpbdY = 0, qpbdC = 0;
+  int clipY(int v) const { return clip_px(v, maxY); }
+  int clipC(int v) const { return clip_px(v, maxC); }
+  // QPc (8.5.8, Table 8-15) for a luma QP and offset: qPI = Clip3(-QpBdOffsetC, 51, QPY + offset)
+  int qpc_of(int qpy, int off) const {
+    const int qpi = clampi(qpy + off, -qpbdC, 51);
+    return qpi < 0 ? qpi : chroma_qp(qpi, 0);
+  }
   // POC state (8.2.1)
   int prev_poc_msb = 0, prev_poc_lsb = 0, prev_frame_num_offset = 0, prev_frame_num = 0, frame_num_offset = 0;
   int poc_msb = 0;
@@ -478,9 +505,16 @@ struct Decoder::Impl {
   void emit(const Pic& p) {
     DecodedPicture d;
     fill_common(d, p);
-    d.y = p.Y;
-    d.u = p.U;
-    d.v = p.V;
+    d.bit_depth = bdY;
+    if (bdY == 8 && bdC == 8) {
+      d.y.assign(p.Y.begin(), p.Y.end());
+      d.u.assign(p.U.begin(), p.U.end());
+      d.v.assign(p.V.begin(), p.V.end());
+    } else {
+      d.y16 = p.Y;
+      d.u16 = p.U;
+      d.v16 = p.V;
+    }
     out_->push_back(std::move(d));
   }
 
@@ -689,8 +723,15 @@ struct Decoder::Impl {
   }
 
   void start_picture(const SliceHeader& h) {
+    bdY = sp->bit_depth_luma;
+    bdC = sp->bit_depth_chroma;
+    maxY = (1 << bdY) - 1;
+    maxC = (1 << bdC) - 1;
+    qpbdY = 6 * (bdY - 8);
+    qpbdC = 6 * (bdC - 8);
     cur = new_pic();
     cur->init(sp->width_mbs, sp->height_mbs, !parse_only);
+    if (bdY != 8 || bdC != 8) cur->gpu_ok = false;  // the GPU reconstruction kernels are 8-bit
     if (parse_only) cur->init_records();
     cur->slice_qp = h.qp;
     pic_ref_id = -1;
@@ -855,7 +896,7 @@ struct Decoder::Impl {
     int addr = h.first_mb;
     int qp = h.qp;
     if (h.first_mb >= nmb) throw std::runtime_error("first_mb_in_slice past the picture");
-    if (qp < 0 || qp > 51) throw std::runtime_error("slice QP out of range");
+    if (qp < -qpbdY || qp > 51) throw std::runtime_error("slice QP out of range");
     if (cabac) {
       while (!br.byte_aligned())  // cabac_alignment_one_bit
         if (!br.get_bit()) throw std::runtime_error("cabac_alignment_one_bit is 0");
@@ -1262,13 +1303,13 @@ struct Decoder::Impl {
     return tap6(ref_y(r, x, y - 2), ref_y(r, x, y - 1), ref_y(r, x, y), ref_y(r, x, y + 1), ref_y(r, x, y + 2),
                 ref_y(r, x, y + 3));
   }
-  static int luma_sample(const Pic& r, int xi, int yi, int xf, int yf) {
-    auto b = [&](int x, int y) { return clip_px((half_h1(r, x, y) + 16) >> 5); };
-    auto h = [&](int x, int y) { return clip_px((half_v1(r, x, y) + 16) >> 5); };
+  static int luma_sample(const Pic& r, int xi, int yi, int xf, int yf, int maxv) {
+    auto b = [&](int x, int y) { return clip_px((half_h1(r, x, y) + 16) >> 5, maxv); };
+    auto h = [&](int x, int y) { return clip_px((half_v1(r, x, y) + 16) >> 5, maxv); };
     auto j = [&](int x, int y) {
       int j1 = tap6(half_h1(r, x, y - 2), half_h1(r, x, y - 1), half_h1(r, x, y), half_h1(r, x, y + 1),
                     half_h1(r, x, y + 2), half_h1(r, x, y + 3));
-      return clip_px((j1 + 512) >> 10);
+      return clip_px((j1 + 512) >> 10, maxv);
     };
     int G = ref_y(r, xi, yi);
     switch (yf * 4 + xf) {
@@ -1291,7 +1332,7 @@ struct Decoder::Impl {
     }
     return 0;
   }
-  static int chroma_sample(const std::vector<uint8_t>& plane, int cw, int ch, int xi, int yi, int xf, int yf) {
+  static int chroma_sample(const std::vector<uint16_t>& plane, int cw, int ch, int xi, int yi, int xf, int yf) {
     auto P = [&](int x, int y) {
       return static_cast<int>(plane[static_cast<size_t>(clampi(y, 0, ch - 1)) * cw + clampi(x, 0, cw - 1)]);
     };
@@ -1302,6 +1343,7 @@ struct Decoder::Impl {
   // weighted sample prediction (8.4.2.3) from the per-list predictions
   int weigh(int comp, int r0, int r1, int p0, int p1) const {
     const bool b0 = r0 >= 0, b1 = r1 >= 0;
+    const int maxv = comp ? maxC : maxY;
     if (sh.has_weights) {
       const WeightTable& w = sh.wt;
       int logwd = comp ? w.chroma_log2 : w.luma_log2;
@@ -1314,15 +1356,19 @@ struct Decoder::Impl {
         w1 = comp ? w.cw[1][r1][comp - 1] : w.lw[1][r1];
         o1 = comp ? w.co[1][r1][comp - 1] : w.lo[1][r1];
       }
-      if (b0 && b1) return clip_px(((p0 * w0 + p1 * w1 + (1 << logwd)) >> (logwd + 1)) + ((o0 + o1 + 1) >> 1));
+      // offsets are in units of the 8-bit range (8.4.2.3.2: o = offset * 2^(BitDepth - 8))
+      const int osh = (comp ? bdC : bdY) - 8;
+      o0 *= 1 << osh;
+      o1 *= 1 << osh;
+      if (b0 && b1) return clip_px(((p0 * w0 + p1 * w1 + (1 << logwd)) >> (logwd + 1)) + ((o0 + o1 + 1) >> 1), maxv);
       int p = b0 ? p0 : p1, ww = b0 ? w0 : w1, o = b0 ? o0 : o1;
-      if (logwd >= 1) return clip_px(((p * ww + (1 << (logwd - 1))) >> logwd) + o);
-      return clip_px(p * ww + o);
+      if (logwd >= 1) return clip_px(((p * ww + (1 << (logwd - 1))) >> logwd) + o, maxv);
+      return clip_px(p * ww + o, maxv);
     }
     if (b0 && b1) {
       if (sh.slice_type == SLICE_B && pp->weighted_bipred_idc == 2) {
         int w0 = implicit_w[r0][r1][0], w1 = implicit_w[r0][r1][1];
-        return clip_px((p0 * w0 + p1 * w1 + 32) >> 6);
+        return clip_px((p0 * w0 + p1 * w1 + 32) >> 6, maxv);
       }
       return (p0 + p1 + 1) >> 1;
     }
@@ -1344,7 +1390,7 @@ struct Decoder::Impl {
         for (int y = 0; y < 4; ++y)
           for (int x = 0; x < 4; ++x) {
             int px = mx * 16 + bx * 4 + x, py = my * 16 + by * 4 + y;
-            ly[l][y * 4 + x] = luma_sample(ref, px + (mvx >> 2), py + (mvy >> 2), mvx & 3, mvy & 3);
+            ly[l][y * 4 + x] = luma_sample(ref, px + (mvx >> 2), py + (mvy >> 2), mvx & 3, mvy & 3, maxY);
           }
         for (int y = 0; y < 2; ++y)
           for (int x = 0; x < 2; ++x) {
@@ -1358,15 +1404,15 @@ struct Decoder::Impl {
         for (int x = 0; x < 4; ++x) {
           int px = mx * 16 + bx * 4 + x, py = my * 16 + by * 4 + y;
           cur->Y[static_cast<size_t>(py) * cur->W + px] =
-              static_cast<uint8_t>(weigh(0, refs[0], refs[1], ly[0][y * 4 + x], ly[1][y * 4 + x]));
+              static_cast<uint16_t>(weigh(0, refs[0], refs[1], ly[0][y * 4 + x], ly[1][y * 4 + x]));
         }
       for (int y = 0; y < 2; ++y)
         for (int x = 0; x < 2; ++x) {
           int px = mx * 8 + bx * 2 + x, py = my * 8 + by * 2 + y;
           cur->U[static_cast<size_t>(py) * cw + px] =
-              static_cast<uint8_t>(weigh(1, refs[0], refs[1], lu[0][y * 2 + x], lu[1][y * 2 + x]));
+              static_cast<uint16_t>(weigh(1, refs[0], refs[1], lu[0][y * 2 + x], lu[1][y * 2 + x]));
           cur->V[static_cast<size_t>(py) * cw + px] =
-              static_cast<uint8_t>(weigh(2, refs[0], refs[1], lv[0][y * 2 + x], lv[1][y * 2 + x]));
+              static_cast<uint16_t>(weigh(2, refs[0], refs[1], lv[0][y * 2 + x], lv[1][y * 2 + x]));
         }
     }
   }
@@ -1696,7 +1742,7 @@ struct Decoder::Impl {
     return 1;
   }
 
-  void pred4x4(int addr, int blkidx, int mode, uint8_t* pred) {
+  void pred4x4(int addr, int blkidx, int mode, uint16_t* pred) {
     int mx = addr % cur->wmb, my = addr / cur->wmb;
     int bx = kBlkX[blkidx] * 4, by = kBlkY[blkidx] * 4;
     int X0 = mx * 16 + bx, Y0 = my * 16 + by;
@@ -1734,7 +1780,7 @@ struct Decoder::Impl {
             if (has_top && has_left) v = (top[0] + top[1] + top[2] + top[3] + left[0] + left[1] + left[2] + left[3] + 4) >> 3;
             else if (has_left) v = (left[0] + left[1] + left[2] + left[3] + 2) >> 2;
             else if (has_top) v = (top[0] + top[1] + top[2] + top[3] + 2) >> 2;
-            else v = 128;
+            else v = 1 << (bdY - 1);
             break;
           }
           case 3:
@@ -1782,12 +1828,12 @@ struct Decoder::Impl {
           }
           default: throw std::runtime_error("bad intra4x4 mode");
         }
-        pred[y * 4 + x] = static_cast<uint8_t>(v);
+        pred[y * 4 + x] = static_cast<uint16_t>(v);
       }
   }
 
   // Intra_8x8 (8.3.2) with reference sample filtering (8.3.2.2.1)
-  void pred8x8(int addr, int b8, int mode, uint8_t* pred) {
+  void pred8x8(int addr, int b8, int mode, uint16_t* pred) {
     int mx = addr % cur->wmb, my = addr / cur->wmb;
     int bx = (b8 & 1) * 8, by = (b8 >> 1) * 8;
     int X0 = mx * 16 + bx, Y0 = my * 16 + by;
@@ -1827,7 +1873,7 @@ struct Decoder::Impl {
     if ((mode == 4 || mode == 5 || mode == 6) && !(has_top && has_left && has_tl))
       throw std::runtime_error("intra 8x8 mode needs top, left and top-left samples");
     if (mode < 0 || mode > 8) throw std::runtime_error("bad intra8x8 mode");
-    int dc = 128;
+    int dc = 1 << (bdY - 1);
     if (mode == 2) {
       int st = 0, sl = 0;
       for (int i = 0; i < 8; ++i) {
@@ -1883,11 +1929,11 @@ struct Decoder::Impl {
             break;
           }
         }
-        pred[y * 8 + x] = static_cast<uint8_t>(v);
+        pred[y * 8 + x] = static_cast<uint16_t>(v);
       }
   }
 
-  void pred16x16(int addr, int mode, uint8_t* pred) {
+  void pred16x16(int addr, int mode, uint16_t* pred) {
     int mx = addr % cur->wmb, my = addr / cur->wmb;
     int X0 = mx * 16, Y0 = my * 16;
     bool has_top = intra_avail(addr, 0, -1), has_left = intra_avail(addr, -1, 0), has_tl = intra_avail(addr, -1, -1);
@@ -1899,7 +1945,7 @@ struct Decoder::Impl {
     if (mode == 0 && !has_top) throw std::runtime_error("I16 V without top");
     if (mode == 1 && !has_left) throw std::runtime_error("I16 H without left");
     if (mode == 3 && !(has_top && has_left && has_tl)) throw std::runtime_error("I16 plane without neighbours");
-    int dc = 128;
+    int dc = 1 << (bdY - 1);
     if (mode == 2) {
       int st = 0, sl = 0;
       for (int i = 0; i < 16; ++i) {
@@ -1928,13 +1974,13 @@ struct Decoder::Impl {
           case 0: v = top[x]; break;
           case 1: v = left[y]; break;
           case 2: v = dc; break;
-          default: v = clip_px((a + b * (x - 7) + c * (y - 7) + 16) >> 5); break;
+          default: v = clipY((a + b * (x - 7) + c * (y - 7) + 16) >> 5); break;
         }
-        pred[y * 16 + x] = static_cast<uint8_t>(v);
+        pred[y * 16 + x] = static_cast<uint16_t>(v);
       }
   }
 
-  void pred_chroma(int addr, int mode, const std::vector<uint8_t>& plane, uint8_t* pred) {
+  void pred_chroma(int addr, int mode, const std::vector<uint16_t>& plane, uint16_t* pred) {
     int mx = addr % cur->wmb, my = addr / cur->wmb;
     int cw = cur->W / 2;
     int X0 = mx * 8, Y0 = my * 8;
@@ -1958,18 +2004,18 @@ struct Decoder::Impl {
           if (has_top && has_left) dc = (st + sl + 4) >> 3;
           else if (has_left) dc = (sl + 2) >> 2;
           else if (has_top) dc = (st + 2) >> 2;
-          else dc = 128;
+          else dc = 1 << (bdC - 1);
         } else if (xo > 0 && yo == 0) {
           if (has_top) dc = (st + 2) >> 2;
           else if (has_left) dc = (sl + 2) >> 2;
-          else dc = 128;
+          else dc = 1 << (bdC - 1);
         } else {
           if (has_left) dc = (sl + 2) >> 2;
           else if (has_top) dc = (st + 2) >> 2;
-          else dc = 128;
+          else dc = 1 << (bdC - 1);
         }
         for (int y = 0; y < 4; ++y)
-          for (int x = 0; x < 4; ++x) pred[(yo + y) * 8 + xo + x] = static_cast<uint8_t>(dc);
+          for (int x = 0; x < 4; ++x) pred[(yo + y) * 8 + xo + x] = static_cast<uint16_t>(dc);
       }
       return;
     }
@@ -1992,8 +2038,8 @@ struct Decoder::Impl {
         int v;
         if (mode == 1) v = left[y];
         else if (mode == 2) v = top[x];
-        else v = clip_px((a + b * (x - 3) + c * (y - 3) + 16) >> 5);
-        pred[y * 8 + x] = static_cast<uint8_t>(v);
+        else v = clipC((a + b * (x - 3) + c * (y - 3) + 16) >> 5);
+        pred[y * 8 + x] = static_cast<uint16_t>(v);
       }
   }
 
@@ -2072,8 +2118,8 @@ struct Decoder::Impl {
       while (!br.byte_aligned()) {
         if (br.get_bit()) throw std::runtime_error("pcm_alignment_zero_bit is 1");
       }
-      uint8_t pcm[384];
-      for (int i = 0; i < 384; ++i) pcm[i] = static_cast<uint8_t>(br.get(8));
+      int16_t pcm[384];
+      for (int i = 0; i < 384; ++i) pcm[i] = static_cast<int16_t>(br.get(i < 256 ? bdY : bdC));
       if (!parse_only) {
         for (int y = 0; y < 16; ++y)
           for (int x = 0; x < 16; ++x) cur->Y[static_cast<size_t>(my * 16 + y) * cur->W + mx * 16 + x] = pcm[y * 16 + x];
@@ -2262,9 +2308,10 @@ struct Decoder::Impl {
     cur->cbp[addr] = static_cast<uint8_t>(s.cbp);
     int cbp_luma = s.cbp & 15, cbp_chroma = s.cbp >> 4;
     if (cbp_luma || cbp_chroma || kind == MBK_I16x16) {
-      const int d = cabac ? cabac_qp_delta() : br.get_se_range(-26, 25, "mb_qp_delta");
-      if (d < -26 || d > 25) throw std::runtime_error("mb_qp_delta out of range");
-      qp = ((qp + d + 52) % 52);
+      const int dlo = -(26 + qpbdY / 2), dhi = 25 + qpbdY / 2;
+      const int d = cabac ? cabac_qp_delta() : br.get_se_range(dlo, dhi, "mb_qp_delta");
+      if (d < dlo || d > dhi) throw std::runtime_error("mb_qp_delta out of range");
+      qp = ((qp + d + 52 + 2 * qpbdY) % (52 + qpbdY)) - qpbdY;
       prev_qp_delta_nz = d != 0;
     } else {
       prev_qp_delta_nz = 0;
@@ -2535,8 +2582,8 @@ struct Decoder::Impl {
     idct4(d);
     for (int y = 0; y < 4; ++y)
       for (int x = 0; x < 4; ++x) {
-        uint8_t& o = cur->Y[static_cast<size_t>(Y0 + by + y) * cur->W + X0 + bx + x];
-        o = static_cast<uint8_t>(clip_px(o + d[y * 4 + x]));
+        uint16_t& o = cur->Y[static_cast<size_t>(Y0 + by + y) * cur->W + X0 + bx + x];
+        o = static_cast<uint16_t>(clipY(o + d[y * 4 + x]));
       }
   }
   void add_residual8(int addr, int b8, const int* lv, int qp, const uint8_t* w8) {
@@ -2550,12 +2597,13 @@ struct Decoder::Impl {
     idct8(d);
     for (int y = 0; y < 8; ++y)
       for (int x = 0; x < 8; ++x) {
-        uint8_t& o = cur->Y[static_cast<size_t>(Y0 + y) * cur->W + X0 + x];
-        o = static_cast<uint8_t>(clip_px(o + d[y * 8 + x]));
+        uint16_t& o = cur->Y[static_cast<size_t>(Y0 + y) * cur->W + X0 + x];
+        o = static_cast<uint16_t>(clipY(o + d[y * 8 + x]));
       }
   }
 
-  void reconstruct(int addr, int kind, const MbSyn& s, int qp) {
+  void reconstruct(int addr, int kind, const MbSyn& s, int qp_y) {
+    const int qp = qp_y + qpbdY;  // QP'Y (8.5.12.1)
     int mx = addr % cur->wmb, my = addr / cur->wmb;
     int cw = cur->W / 2;
     int X0 = mx * 16, Y0 = my * 16;
@@ -2566,7 +2614,7 @@ struct Decoder::Impl {
     const uint8_t* wy8 = pp->sl8[li ? 1 : 0];
     if (kind == MBK_I4x4) {
       for (int blk = 0; blk < 16; ++blk) {
-        uint8_t pred[16];
+        uint16_t pred[16];
         pred4x4(addr, blk, s.i4[blk], pred);
         int bx = kBlkX[blk] * 4, by = kBlkY[blk] * 4;
         for (int y = 0; y < 4; ++y)
@@ -2576,7 +2624,7 @@ struct Decoder::Impl {
       }
     } else if (kind == MBK_I8x8) {
       for (int b8 = 0; b8 < 4; ++b8) {
-        uint8_t pred[64];
+        uint16_t pred[64];
         pred8x8(addr, b8, s.i4[b8 * 4], pred);
         int bx = (b8 & 1) * 8, by = (b8 >> 1) * 8;
         for (int y = 0; y < 8; ++y)
@@ -2585,7 +2633,7 @@ struct Decoder::Impl {
         mark_done(bx >> 2, by >> 2, 2, 2);
       }
     } else if (kind == MBK_I16x16) {
-      uint8_t pred[256];
+      uint16_t pred[256];
       pred16x16(addr, s.i16_mode, pred);
       for (int y = 0; y < 16; ++y)
         for (int x = 0; x < 16; ++x) cur->Y[static_cast<size_t>(Y0 + y) * cur->W + X0 + x] = pred[y * 16 + x];
@@ -2628,15 +2676,15 @@ struct Decoder::Impl {
     // chroma
     const bool intra = mbk_is_intra(kind);
     for (int comp = 0; comp < 2; ++comp) {
-      std::vector<uint8_t>& plane = comp == 0 ? cur->U : cur->V;
-      uint8_t pred[64];
+      std::vector<uint16_t>& plane = comp == 0 ? cur->U : cur->V;
+      uint16_t pred[64];
       if (intra) {
         pred_chroma(addr, s.chroma_mode, plane, pred);
       } else {
         for (int y = 0; y < 8; ++y)
           for (int x = 0; x < 8; ++x) pred[y * 8 + x] = plane[static_cast<size_t>(my * 8 + y) * cw + mx * 8 + x];
       }
-      int qpc = chroma_qp(qp, comp == 0 ? pp->chroma_qp_index_offset : pp->second_chroma_qp_index_offset);
+      const int qpc = qpc_of(qp_y, comp == 0 ? pp->chroma_qp_index_offset : pp->second_chroma_qp_index_offset) + qpbdC;
       int c0 = s.cdc[comp][0], c1 = s.cdc[comp][1], c2 = s.cdc[comp][2], c3 = s.cdc[comp][3];
       int f[4] = {c0 + c1 + c2 + c3, c0 - c1 + c2 - c3, c0 + c1 - c2 - c3, c0 - c1 - c2 + c3};
       const uint8_t* wc4 = pp->sl4[li + 1 + comp];
@@ -2656,7 +2704,7 @@ struct Decoder::Impl {
         for (int y = 0; y < 4; ++y)
           for (int x = 0; x < 4; ++x) {
             int v = pred[(yo + y) * 8 + xo + x] + (any ? d[y * 4 + x] : 0);
-            plane[static_cast<size_t>(my * 8 + yo + y) * cw + mx * 8 + xo + x] = static_cast<uint8_t>(clip_px(v));
+            plane[static_cast<size_t>(my * 8 + yo + y) * cw + mx * 8 + xo + x] = static_cast<uint16_t>(clipC(v));
           }
       }
     }
@@ -2841,7 +2889,7 @@ struct Decoder::Impl {
   }
 
   // filter one line of samples across an edge; q0p points to q0, step = distance p0 -> q0
-  static void filter_line(uint8_t* q0p, int step, int bs, int alpha, int beta, int tc0, bool chroma) {
+  static void filter_line(uint16_t* q0p, int step, int bs, int alpha, int beta, int tc0, bool chroma, int maxv) {
     int p0 = q0p[-step], p1 = q0p[-2 * step], q0 = q0p[0], q1 = q0p[step];
     if (!(std::abs(p0 - q0) < alpha && std::abs(p1 - p0) < beta && std::abs(q1 - q0) < beta)) return;
     int p2 = chroma ? 0 : q0p[-3 * step], q2 = chroma ? 0 : q0p[2 * step];
@@ -2849,28 +2897,28 @@ struct Decoder::Impl {
     if (bs < 4) {
       int tc = chroma ? tc0 + 1 : tc0 + (ap < beta) + (aq < beta);
       int delta = clampi((((q0 - p0) << 2) + (p1 - q1) + 4) >> 3, -tc, tc);
-      q0p[-step] = static_cast<uint8_t>(clip_px(p0 + delta));
-      q0p[0] = static_cast<uint8_t>(clip_px(q0 - delta));
+      q0p[-step] = static_cast<uint16_t>(clip_px(p0 + delta, maxv));
+      q0p[0] = static_cast<uint16_t>(clip_px(q0 - delta, maxv));
       if (!chroma) {
-        if (ap < beta) q0p[-2 * step] = static_cast<uint8_t>(p1 + clampi((p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1, -tc0, tc0));
-        if (aq < beta) q0p[step] = static_cast<uint8_t>(q1 + clampi((q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1, -tc0, tc0));
+        if (ap < beta) q0p[-2 * step] = static_cast<uint16_t>(p1 + clampi((p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1, -tc0, tc0));
+        if (aq < beta) q0p[step] = static_cast<uint16_t>(q1 + clampi((q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1, -tc0, tc0));
       }
     } else {
       if (!chroma && ap < beta && std::abs(p0 - q0) < ((alpha >> 2) + 2)) {
         int p3 = q0p[-4 * step];
-        q0p[-step] = static_cast<uint8_t>((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
-        q0p[-2 * step] = static_cast<uint8_t>((p2 + p1 + p0 + q0 + 2) >> 2);
-        q0p[-3 * step] = static_cast<uint8_t>((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
+        q0p[-step] = static_cast<uint16_t>((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
+        q0p[-2 * step] = static_cast<uint16_t>((p2 + p1 + p0 + q0 + 2) >> 2);
+        q0p[-3 * step] = static_cast<uint16_t>((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
       } else {
-        q0p[-step] = static_cast<uint8_t>((2 * p1 + p0 + q1 + 2) >> 2);
+        q0p[-step] = static_cast<uint16_t>((2 * p1 + p0 + q1 + 2) >> 2);
       }
       if (!chroma && aq < beta && std::abs(p0 - q0) < ((alpha >> 2) + 2)) {
         int q3 = q0p[3 * step];
-        q0p[0] = static_cast<uint8_t>((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
-        q0p[step] = static_cast<uint8_t>((p0 + q0 + q1 + q2 + 2) >> 2);
-        q0p[2 * step] = static_cast<uint8_t>((2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3);
+        q0p[0] = static_cast<uint16_t>((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
+        q0p[step] = static_cast<uint16_t>((p0 + q0 + q1 + q2 + 2) >> 2);
+        q0p[2 * step] = static_cast<uint16_t>((2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3);
       } else {
-        q0p[0] = static_cast<uint8_t>((2 * q1 + q0 + p1 + 2) >> 2);
+        q0p[0] = static_cast<uint16_t>((2 * q1 + q0 + p1 + 2) >> 2);
       }
     }
   }
@@ -2900,12 +2948,13 @@ struct Decoder::Impl {
           // luma
           int qpav = (cur->qp_dbk[mbp] + cur->qp_dbk[addr] + 1) >> 1;
           int ia = clampi(qpav + spar.alpha_off, 0, 51), ib = clampi(qpav + spar.beta_off, 0, 51);
-          int alpha = kAlpha[ia], beta = kBeta[ib];
+          const int sy = 1 << (bdY - 8);
+          int alpha = kAlpha[ia] * sy, beta = kBeta[ib] * sy;
           for (int i = 0; i < 16; ++i) {
             int bs = bS[i >> 2];
             if (!bs) continue;
-            int tc0 = bs < 4 ? kTc0[ia][bs - 1] : 0;
-            uint8_t* q0;
+            int tc0 = bs < 4 ? kTc0[ia][bs - 1] * sy : 0;
+            uint16_t* q0;
             int step;
             if (dir == 0) {
               q0 = &cur->Y[static_cast<size_t>(my * 16 + i) * W + mx * 16 + e * 4];
@@ -2914,24 +2963,25 @@ struct Decoder::Impl {
               q0 = &cur->Y[static_cast<size_t>(my * 16 + e * 4) * W + mx * 16 + i];
               step = W;
             }
-            filter_line(q0, step, bs, alpha, beta, tc0, false);
+            filter_line(q0, step, bs, alpha, beta, tc0, false, maxY);
           }
           // chroma: edges 0 and 2 (luma) map to chroma edges 0 and 4
           if (e == 0 || e == 2) {
             int ce = e / 2;
             for (int comp = 0; comp < 2; ++comp) {
               int off = comp == 0 ? spar.cb_off : spar.cr_off;
-              int qpp = cur->kind[mbp] == MBK_IPCM ? chroma_qp(0, off) : chroma_qp(cur->qp_dbk[mbp], off);
-              int qpq = cur->kind[addr] == MBK_IPCM ? chroma_qp(0, off) : chroma_qp(cur->qp_dbk[addr], off);
+              int qpp = cur->kind[mbp] == MBK_IPCM ? qpc_of(0, off) : qpc_of(cur->qp_dbk[mbp], off);
+              int qpq = cur->kind[addr] == MBK_IPCM ? qpc_of(0, off) : qpc_of(cur->qp_dbk[addr], off);
               int qa = (qpp + qpq + 1) >> 1;
               int iac = clampi(qa + spar.alpha_off, 0, 51), ibc = clampi(qa + spar.beta_off, 0, 51);
-              int ac = kAlpha[iac], bc = kBeta[ibc];
-              std::vector<uint8_t>& pl = comp == 0 ? cur->U : cur->V;
+              const int sc = 1 << (bdC - 8);
+              int ac = kAlpha[iac] * sc, bc = kBeta[ibc] * sc;
+              std::vector<uint16_t>& pl = comp == 0 ? cur->U : cur->V;
               for (int i = 0; i < 8; ++i) {
                 int bs = bS[i >> 1];
                 if (!bs) continue;
-                int tc0 = bs < 4 ? kTc0[iac][bs - 1] : 0;
-                uint8_t* q0;
+                int tc0 = bs < 4 ? kTc0[iac][bs - 1] * sc : 0;
+                uint16_t* q0;
                 int step;
                 if (dir == 0) {
                   q0 = &pl[static_cast<size_t>(my * 8 + i) * cw + mx * 8 + ce * 4];
@@ -2940,7 +2990,7 @@ struct Decoder::Impl {
                   q0 = &pl[static_cast<size_t>(my * 8 + ce * 4) * cw + mx * 8 + i];
                   step = cw;
                 }
-                filter_line(q0, step, bs, ac, bc, tc0, true);
+                filter_line(q0, step, bs, ac, bc, tc0, true, maxC);
               }
             }
           }

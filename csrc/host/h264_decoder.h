@@ -1,5 +1,5 @@
-// Independent H.264 decoder (CAVLC + CABAC; I, P and B slices; Baseline/Main/High;
-// 8-bit 4:2:0; progressive).
+// Independent H.264 decoder (CAVLC + CABAC; I, P and B slices; Baseline/Main/High/High 10;
+// 8- to 14-bit 4:2:0; progressive).
 //
 // Written directly from ITU-T H.264 clauses 7-9 and kept deliberately separate
 // from the encoder-side writer (cavlc_writer.cc) and the HIP kernels: it shares
@@ -38,7 +38,9 @@ struct DecodedPicture {
   int poc = 0;                        // PicOrderCnt (pictures come out in increasing POC)
   int idr = 0;
   int slice_type = 0;
-  std::vector<uint8_t> y, u, v;       // coded size planes
+  int bit_depth = 8;                  // BitDepthY (chroma has the SPS's BitDepthC)
+  std::vector<uint8_t> y, u, v;       // coded size planes (8-bit streams)
+  std::vector<uint16_t> y16, u16, v16; // coded size planes of High 10 (9..14-bit) streams
   // per-MB side info (coded raster order)
   std::vector<int8_t> mb_kind;        // MbKind as decoded (P_Skip = MBK_PSKIP)
   std::vector<int8_t> mb_qp;          // QP_Y
@@ -67,6 +69,7 @@ struct DecodedPicture {
   std::vector<int16_t> wp;            // kWpEntries: weighted-prediction table (see kWp* below)
   // copy the cropped planes out as one contiguous I420 frame
   std::vector<uint8_t> cropped_i420() const;
+  std::vector<uint16_t> cropped_i420_16() const;  // the 16-bit planes (bit_depth > 8)
 };
 
 class Decoder {

@@ -287,7 +287,9 @@ SPS parse_sps(BitReader& br) {
       read_matrix(br, 2, s.sl4, s.sl8, nullptr, nullptr);  // fall-back rule A
     }
   }
-  if (s.chroma_format_idc != 1 || s.bit_depth_luma != 8) throw std::runtime_error("only 8-bit 4:2:0 supported");
+  // 4:2:0 at 8 bits (Baseline .. High) or 9..14 bits (High 10 and the 4:2:0 intra / predictive profiles)
+  if (s.chroma_format_idc != 1) throw std::runtime_error("only 4:2:0 supported");
+  if (s.bit_depth_luma > 14 || s.bit_depth_chroma > 14) throw std::runtime_error("bit depth above 14");
   s.log2_max_frame_num = br.get_ue_max(12, "log2_max_frame_num_minus4") + 4;
   s.poc_type = br.get_ue_max(2, "pic_order_cnt_type");
   if (s.poc_type == 0) {

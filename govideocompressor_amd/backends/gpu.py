@@ -267,9 +267,10 @@ class GpuBackend:
             for k, v in dec.stats.items():
                 self.decode_stats[k] = self.decode_stats.get(k, 0) + v
             for i, d in zip(idxs, got):
-                if d.y.dtype != torch.uint8 and not keep_high_bit:  # Main 10 input, 8-bit output
+                if d.y.dtype != torch.uint8 and not keep_high_bit:  # Main 10 / High 10 input, 8-bit output
                     from ..models.h264_decode_gpu import DecodedSegment
-                    d = DecodedSegment(yuv.to_8bit(d.y), yuv.to_8bit(d.u), yuv.to_8bit(d.v), d.fps, d.path)
+                    bd = d.bit_depth if d.bit_depth > 8 else 10  # (the HEVC decoder's segments: Main 10)
+                    d = DecodedSegment(yuv.to_8bit(d.y, bd), yuv.to_8bit(d.u, bd), yuv.to_8bit(d.v, bd), d.fps, d.path)
                 out[i] = d
         return out
 

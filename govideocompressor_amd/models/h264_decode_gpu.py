@@ -21,7 +21,7 @@ weighted prediction, several references) reconstruct on the GPU; Intra 4x4 / 8x8
 too, and pictures of several slices (the records carry each MB's slice for the intra
 neighbour availability).  Segments the GPU path does not cover (I_PCM, constrained intra
 prediction, mmco 5, slices of one picture with different reference lists or filter offsets,
-per-picture filter parameters that differ from the batch) are decoded by the CPU decoder
+per-picture filter parameters that differ from the batch, High 10 streams) are decoded by the CPU decoder
 instead (``h264_decoder.cc``) and uploaded; the result is identical
 either way (the CPU decoder is the bit-exact oracle of ``tests/test_gpu_decode.py``).
 """
@@ -45,6 +45,9 @@ class DecodedSegment:
     v: torch.Tensor
     fps: float = 30.0
     path: str = "gpu"  # "gpu" or "cpu" (fallback decoder)
+    # High 10 streams (CPU decoder): int16 planes holding samples of this many bits -- the
+    # layout of the encoders' 10-bit input (models/hevc_gpu.py Main 10)
+    bit_depth: int = 8
 
     @property
     def frames(self) -> int:
@@ -178,13 +181,16 @@ class GpuH264Decoder:
             raise ValueError("segment holds no pictures")
         w, h = pics[0]["width"], pics[0]["height"]
         buf = np.concatenate([p["i420"] for p in pics]).reshape(len(pics), -1)
+        bd = int(pics[0].get("bit_depth", 8))
+        if buf.dtype != np.uint8:
+            buf = buf.astype(np.int16)  # <= 14-bit samples
         ys = w * h
         cs = (w // 2) * (h // 2)
         t = torch.from_numpy(buf).to(self.dev)
         y = t[:, :ys].reshape(len(pics), h, w)
         u = t[:, ys:ys + cs].reshape(len(pics), h // 2, w // 2)
         v = t[:, ys + cs:].reshape(len(pics), h // 2, w // 2)
-        return DecodedSegment(y, u, v, fps, "cpu")
+        return DecodedSegment(y, u, v, fps, "cpu", bd)
 
     def _staging(self, cap: int) -> list[tuple[torch.Tensor, torch.Tensor]]:
         """Two (pinned host, device) step buffers of at least ``cap`` bytes, kept across calls."""

@@ -78,9 +78,9 @@ class GpuTranscoder:
         v = torch.empty_like(u)
         for b, s in enumerate(segs):
             for dst, src in ((y, s.y), (u, s.u), (v, s.v)):
-                if src.dtype != torch.uint8:  # Main 10 input -> 8-bit encoder input (rounded)
+                if src.dtype != torch.uint8:  # Main 10 / High 10 input -> 8-bit encoder input (rounded)
                     from ..utils.yuv import to_8bit
-                    src = to_8bit(src)
+                    src = to_8bit(src, s.bit_depth if s.bit_depth > 8 else 10)
                 c = src.shape[0]
                 dst[b, :c].copy_(src)
                 if c < F:

@@ -79,10 +79,11 @@ def _levels(rng, n: int, density: float, start: int = 0) -> np.ndarray:
     return v
 
 
-def _intra_record(rng, h, c, mx, my, qp, density, allow_i4=True, t8x8=False, dc_only=False, pcm=0.0):
+def _intra_record(rng, h, c, mx, my, qp, density, allow_i4=True, t8x8=False, dc_only=False, pcm=0.0, bit_depth=8):
+    qp &= 0xFF  # int8 QP_Y (negative below QP 0 at High 10)
     if pcm and rng.random() < pcm:
         h[_KIND] = IPCM
-        c[:384] = rng.integers(0, 256, 384)
+        c[:384] = rng.integers(0, 1 << bit_depth, 384)
         h[_QP] = qp
         return
     if dc_only:  # constrained intra in P pictures: DC modes are legal with any availability
@@ -128,7 +129,7 @@ def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp:
                   density: float = 0.15, intra_in_p: float = 0.1, mv_range: int = 48, keyint: int = 0,
                   cabac: bool = False, t8x8: bool = False, records: list | None = None, refs: int = 1,
                   slice_rows: int = 0, pcm: float = 0.0, constrained_intra: bool = False,
-                  cqm: dict | None = None) -> bytes:
+                  cqm: dict | None = None, bit_depth: int = 8) -> bytes:
     """Annex-B stream of ``frames`` pictures (IDR + P) from random decision records.
 
     cabac / t8x8 select the entropy coder and the High-profile 8x8 transform (I8x8 MBs and
@@ -137,10 +138,12 @@ def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp:
     modes then treat each slice's first row as having no row above).  ``pcm``: share of I_PCM
     macroblocks (CAVLC); ``constrained_intra``: constrained_intra_pred_flag (CAVLC; intra MBs of
     P pictures use DC modes); ``cqm``: scaling-matrix keys of the writer config (cqm, cqm4,
-    cqm8, cqm_coded; needs t8x8)."""
+    cqm8, cqm_coded; needs t8x8); ``bit_depth`` > 8: a High 10 stream (PCM samples of that many
+    bits, QPs down to -6 * (bit_depth - 8))."""
     rng = np.random.default_rng(seed)
     cfg = dict(width=width, height=height, qp=qp, cabac=int(cabac), t8x8=int(t8x8), refs=int(refs),
-               constrained_intra=int(constrained_intra), **(cqm or {}))
+               constrained_intra=int(constrained_intra), bit_depth=int(bit_depth), **(cqm or {}))
+    qmin = -6 * (int(bit_depth) - 8)
     wmb, hmb = (width + 15) // 16, (height + 15) // 16
     nmb = wmb * hmb
     out = [host.parameter_sets(cfg)]
@@ -153,18 +156,18 @@ def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp:
             fn = 0
             since_idr = 0
         nref = max(1, min(int(refs), since_idr))  # references held by the sliding window
-        sqp = int(np.clip(qp + rng.integers(-2, 3), 10, 48))
+        sqp = int(np.clip(qp + rng.integers(-2, 3), max(10 + qmin, qmin), 48))
         hdr = np.zeros((nmb, HDR_BYTES), np.uint8)
         hdr[:, _REF:_REF + 8] = 0xFF
         coef = np.zeros((nmb, 408), np.int16)
         for mb in range(nmb):
             mx, my = mb % wmb, mb // wmb
             h, c = hdr[mb], coef[mb]
-            mqp = int(np.clip(sqp + rng.integers(-3, 4), 0, 51))
+            mqp = int(np.clip(sqp + rng.integers(-3, 4), qmin, 51))
             if idr or rng.random() < intra_in_p:
                 r0 = (my // slice_rows) * slice_rows if slice_rows else 0
                 _intra_record(rng, h, c, mx, my - r0, mqp, density, t8x8=t8x8, dc_only=constrained_intra and not idr,
-                              pcm=pcm)
+                              pcm=pcm, bit_depth=bit_depth)
                 continue
             r = rng.random()
             kind = PSKIP if r < 0.25 else (P16x16 if r < 0.5 else (P16x8 if r < 0.65 else (P8x16 if r < 0.8 else P8x8)))
@@ -176,7 +179,7 @@ def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp:
             elif kind == P8x16:
                 mv[2], mv[3] = mv[0], mv[1]
             h[_KIND] = kind
-            h[_QP] = mqp
+            h[_QP] = mqp & 0xFF
             h[_MV:_MV + 16] = np.frombuffer(mv.astype(np.int16).tobytes(), np.uint8)
             rf = rng.integers(0, nref, 4) if kind != PSKIP else np.zeros(4, np.int64)
             if kind == P16x16:

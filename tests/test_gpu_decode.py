@@ -135,3 +135,26 @@ def test_gpu_decode_pcm_constrained_intra_scaling_lists(host, dec):
                random_stream(host, 96, 64, 5, seed=34, t8x8=True, cabac=True, intra_in_p=0.3,
                              cqm=dict(cqm=3, cqm4=cqm4, cqm8=cqm8, cqm_coded=0x5A), density=0.3)]
     _check(host, dec, streams)
+
+
+def test_gpu_decode_high10_segments(host, dec):
+    """High 10 segments (the CPU decoder's 16-bit path) come back as int16 planes of the
+    decoded samples next to 8-bit segments reconstructed on the GPU in the same call, and a
+    transcode of High 10 pieces (models/transcode.py) rounds them to the 8-bit encoder's input."""
+    import torch
+    from govideocompressor_amd.models.h264_gpu import H264Params
+    from govideocompressor_amd.models.transcode import GpuTranscoder
+    s10 = random_stream(host, 96, 64, 4, seed=71, bit_depth=10, intra_in_p=0.3, t8x8=True, cabac=True)
+    s8 = random_stream(host, 96, 64, 4, seed=72)
+    out = dec.decode([s10, s8])
+    assert out[0].path == "cpu" and out[0].bit_depth == 10 and out[0].y.dtype == torch.int16
+    assert out[1].path == "gpu"
+    for t, p in enumerate(host.decode(s10)):
+        ry, ru, rv = _planes(p)
+        assert np.array_equal(out[0].y[t].cpu().numpy(), ry.astype(np.int16))
+        assert np.array_equal(out[0].u[t].cpu().numpy(), ru.astype(np.int16))
+        assert np.array_equal(out[0].v[t].cpu().numpy(), rv.astype(np.int16))
+    tc = GpuTranscoder(H264Params(width=96, height=64, crf=20.0), slots=2)
+    outs = tc.run([s10, s10], 30.0)
+    tc.close()
+    assert [len(host.decode(o)) for o in outs] == [4, 4]
