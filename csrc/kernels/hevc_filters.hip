@@ -283,101 +283,10 @@ __device__ __forceinline__ long long sao_dd(int n, int s, int o) {
   return static_cast<long long>(n) * o * o - 2ll * o * s;
 }
 
-__global__ __launch_bounds__(256) void hevc_sao(HevcSaoArgs a) {
-  __shared__ SaoShared S;
-  const int slot = blockIdx.y;
-  if (a.run[slot] == 0) return;
-  const int tid = threadIdx.x;
-  int ci = blockIdx.x, rx = ci % a.wctb, ry = ci / a.wctb;
-  int nblk = 1;  // record blocks whose statistics feed the decision
-  if (a.mode == 1) {
-    const int wctu = (a.wctb + 1) / 2;
-    rx = (blockIdx.x % wctu) * 2;
-    ry = (blockIdx.x / wctu) * 2;
-    ci = ry * a.wctb + rx;
-    nblk = 4;
-  }
-  const int bd = a.bd, maxv = (1 << bd) - 1;
-  for (int i = tid; i < 3 * 16; i += 256) {
-    (&S.eo_cnt[0][0][0])[i] = 0;
-    (&S.eo_sum[0][0][0])[i] = 0;
-  }
-  for (int i = tid; i < 3 * 32; i += 256) {
-    (&S.bo_cnt[0][0])[i] = 0;
-    (&S.bo_sum[0][0])[i] = 0;
-  }
-  // sample (x, y) of component c relative to its CTB block, x, y in [-1, cs]
-  auto T = [&](int c, int x, int y) -> int {
-    return c == 0 ? S.tile[(y + 1) * 34 + x + 1] : S.tile[34 * 34 + (c - 1) * 18 * 18 + (y + 1) * 18 + x + 1];
-  };
-  static constexpr int hp[4][2] = {{-1, 1}, {0, 0}, {-1, 1}, {1, -1}};
-  static constexpr int vp[4][2] = {{0, 0}, {-1, 1}, {-1, 1}, {-1, 1}};
-  for (int j = 0; j < nblk; ++j) {
-  if (a.mode == 1) {
-    rx = (ci % a.wctb) + (j & 1);
-    ry = (ci / a.wctb) + (j >> 1);
-    if (rx >= a.wctb || ry >= a.hctb) continue;  // (uniform) partial CTU at the picture edge
-    __syncthreads();  // the previous block's statistics are done with the tile
-  }
-  for (int i = tid; i < 34 * 34 + 2 * 18 * 18; i += 256) {
-    int c = 0, k = i;
-    if (i >= 34 * 34) {
-      c = 1 + (i - 34 * 34) / (18 * 18);
-      k = (i - 34 * 34) % (18 * 18);
-    }
-    const int ts = c ? 18 : 34, cs = c ? 16 : 32;
-    const int pw = c ? a.W / 2 : a.W, ph = c ? a.H / 2 : a.H;
-    const int X = clampi(rx * cs + k % ts - 1, 0, pw - 1), Y = clampi(ry * cs + k / ts - 1, 0, ph - 1);
-    const uint16_t* d = (c == 0 ? a.dy : (c == 1 ? a.du : a.dv)) + slot * static_cast<size_t>(pw) * ph;
-    S.tile[i] = d[static_cast<size_t>(Y) * pw + X];  // border samples outside the picture: never used
-  }
-  __syncthreads();
-  // ---- statistics (luma 1024 samples, chroma 2 x 256)
-  if (a.enable && a.mode != 2) {
-    for (int i = tid; i < 1024 + 512; i += 256) {
-      int c, x, y;
-      if (i < 1024) {
-        c = 0;
-        x = i & 31;
-        y = i >> 5;
-      } else {
-        c = 1 + ((i - 1024) >> 8);
-        x = (i - 1024) & 15;
-        y = ((i - 1024) >> 4) & 15;
-      }
-      const int pw = c ? a.W / 2 : a.W, ph = c ? a.H / 2 : a.H, cs = c ? 16 : 32;
-      const size_t ps = static_cast<size_t>(pw) * ph;
-      const uint16_t* s = (c == 0 ? a.sy : (c == 1 ? a.su : a.sv)) + slot * ps;
-      const int X = rx * cs + x, Y = ry * cs + y;
-      const int v = T(c, x, y);
-      const int diff = static_cast<int>(s[static_cast<size_t>(Y) * pw + X]) - v;
-      const int b = v >> (bd - 5);
-      atomicAdd(&S.bo_cnt[c][b], 1);
-      atomicAdd(&S.bo_sum[c][b], diff);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int xa = X + hp[k][0], ya = Y + vp[k][0], xb = X + hp[k][1], yb = Y + vp[k][1];
-        if (xa < 0 || ya < 0 || xb < 0 || yb < 0 || xa >= pw || xb >= pw || ya >= ph || yb >= ph) continue;
-        int e = 2 + sgn(v - T(c, x + hp[k][0], y + vp[k][0])) + sgn(v - T(c, x + hp[k][1], y + vp[k][1]));
-        if (e <= 2) e = (e == 2) ? 0 : e + 1;
-        if (!e) continue;
-        atomicAdd(&S.eo_cnt[c][k][e - 1], 1);
-        atomicAdd(&S.eo_sum[c][k][e - 1], diff);
-      }
-    }
-  }
-  }  // record blocks
-  __syncthreads();
-  if (a.mode == 2) {  // apply the parameters its CTU's first record block carries
-    const CtuInfo* t0 = a.ctu + static_cast<size_t>(slot) * a.wctb * a.hctb + (ry & ~1) * a.wctb + (rx & ~1);
-    if (tid < 2) {
-      S.type[tid] = t0->sao_type[tid];
-      S.cls[tid] = t0->sao_class[tid];
-    }
-    if (tid < 12) S.off[tid >> 2][tid & 3] = t0->sao_off[tid >> 2][tid & 3];
-    if (tid < 3) S.band[tid] = t0->sao_band[tid];
-  }
-  if (a.mode != 2) {
+// SAO decision of a CTB / CTU from the statistics in S (eo_* / bo_*): parameters into S and
+// into the records of its nblk record blocks (ci = the first one)
+__device__ __forceinline__ void sao_decide(const HevcSaoArgs& a, SaoShared& S, int slot, int ci, int nblk, int tid) {
+  const int bd = a.bd;
   // ---- decision.  Every candidate is priced by its own lane (lanes 0-7: edge-offset class k
   // for luma / the chroma pair, lanes 32-127: band position p of Y / Cb / Cr), then lanes 0 / 1
   // pick in the serial order (edge classes 0..3, then the band offsets; the first of equal
@@ -482,7 +391,103 @@ __global__ __launch_bounds__(256) void hevc_sao(HevcSaoArgs a) {
       }
     }
   }
-  }  // decision (mode != 2)
+}
+
+__global__ __launch_bounds__(256) void hevc_sao(HevcSaoArgs a) {
+  __shared__ SaoShared S;
+  const int slot = blockIdx.y;
+  if (a.run[slot] == 0) return;
+  const int tid = threadIdx.x;
+  int ci = blockIdx.x, rx = ci % a.wctb, ry = ci / a.wctb;
+  int nblk = 1;  // record blocks whose statistics feed the decision
+  if (a.mode == 1) {
+    const int wctu = (a.wctb + 1) / 2;
+    rx = (blockIdx.x % wctu) * 2;
+    ry = (blockIdx.x / wctu) * 2;
+    ci = ry * a.wctb + rx;
+    nblk = 4;
+  }
+  const int bd = a.bd, maxv = (1 << bd) - 1;
+  for (int i = tid; i < 3 * 16; i += 256) {
+    (&S.eo_cnt[0][0][0])[i] = 0;
+    (&S.eo_sum[0][0][0])[i] = 0;
+  }
+  for (int i = tid; i < 3 * 32; i += 256) {
+    (&S.bo_cnt[0][0])[i] = 0;
+    (&S.bo_sum[0][0])[i] = 0;
+  }
+  // sample (x, y) of component c relative to its CTB block, x, y in [-1, cs]
+  auto T = [&](int c, int x, int y) -> int {
+    return c == 0 ? S.tile[(y + 1) * 34 + x + 1] : S.tile[34 * 34 + (c - 1) * 18 * 18 + (y + 1) * 18 + x + 1];
+  };
+  static constexpr int hp[4][2] = {{-1, 1}, {0, 0}, {-1, 1}, {1, -1}};
+  static constexpr int vp[4][2] = {{0, 0}, {-1, 1}, {-1, 1}, {-1, 1}};
+  for (int j = 0; j < nblk; ++j) {
+  if (a.mode == 1) {
+    rx = (ci % a.wctb) + (j & 1);
+    ry = (ci / a.wctb) + (j >> 1);
+    if (rx >= a.wctb || ry >= a.hctb) continue;  // (uniform) partial CTU at the picture edge
+    __syncthreads();  // the previous block's statistics are done with the tile
+  }
+  for (int i = tid; i < 34 * 34 + 2 * 18 * 18; i += 256) {
+    int c = 0, k = i;
+    if (i >= 34 * 34) {
+      c = 1 + (i - 34 * 34) / (18 * 18);
+      k = (i - 34 * 34) % (18 * 18);
+    }
+    const int ts = c ? 18 : 34, cs = c ? 16 : 32;
+    const int pw = c ? a.W / 2 : a.W, ph = c ? a.H / 2 : a.H;
+    const int X = clampi(rx * cs + k % ts - 1, 0, pw - 1), Y = clampi(ry * cs + k / ts - 1, 0, ph - 1);
+    const uint16_t* d = (c == 0 ? a.dy : (c == 1 ? a.du : a.dv)) + slot * static_cast<size_t>(pw) * ph;
+    S.tile[i] = d[static_cast<size_t>(Y) * pw + X];  // border samples outside the picture: never used
+  }
+  __syncthreads();
+  // ---- statistics (luma 1024 samples, chroma 2 x 256)
+  if (a.enable && a.mode != 2) {
+    for (int i = tid; i < 1024 + 512; i += 256) {
+      int c, x, y;
+      if (i < 1024) {
+        c = 0;
+        x = i & 31;
+        y = i >> 5;
+      } else {
+        c = 1 + ((i - 1024) >> 8);
+        x = (i - 1024) & 15;
+        y = ((i - 1024) >> 4) & 15;
+      }
+      const int pw = c ? a.W / 2 : a.W, ph = c ? a.H / 2 : a.H, cs = c ? 16 : 32;
+      const size_t ps = static_cast<size_t>(pw) * ph;
+      const uint16_t* s = (c == 0 ? a.sy : (c == 1 ? a.su : a.sv)) + slot * ps;
+      const int X = rx * cs + x, Y = ry * cs + y;
+      const int v = T(c, x, y);
+      const int diff = static_cast<int>(s[static_cast<size_t>(Y) * pw + X]) - v;
+      const int b = v >> (bd - 5);
+      atomicAdd(&S.bo_cnt[c][b], 1);
+      atomicAdd(&S.bo_sum[c][b], diff);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int xa = X + hp[k][0], ya = Y + vp[k][0], xb = X + hp[k][1], yb = Y + vp[k][1];
+        if (xa < 0 || ya < 0 || xb < 0 || yb < 0 || xa >= pw || xb >= pw || ya >= ph || yb >= ph) continue;
+        int e = 2 + sgn(v - T(c, x + hp[k][0], y + vp[k][0])) + sgn(v - T(c, x + hp[k][1], y + vp[k][1]));
+        if (e <= 2) e = (e == 2) ? 0 : e + 1;
+        if (!e) continue;
+        atomicAdd(&S.eo_cnt[c][k][e - 1], 1);
+        atomicAdd(&S.eo_sum[c][k][e - 1], diff);
+      }
+    }
+  }
+  }  // record blocks
+  __syncthreads();
+  if (a.mode == 2) {  // apply the parameters its CTU's first record block carries
+    const CtuInfo* t0 = a.ctu + static_cast<size_t>(slot) * a.wctb * a.hctb + (ry & ~1) * a.wctb + (rx & ~1);
+    if (tid < 2) {
+      S.type[tid] = t0->sao_type[tid];
+      S.cls[tid] = t0->sao_class[tid];
+    }
+    if (tid < 12) S.off[tid >> 2][tid & 3] = t0->sao_off[tid >> 2][tid & 3];
+    if (tid < 3) S.band[tid] = t0->sao_band[tid];
+  }
+  if (a.mode != 2) sao_decide(a, S, slot, ci, nblk, tid);
   if (a.mode == 1) return;  // applied by the per-block launch
   __syncthreads();
   // ---- apply (reads the deblocked copy, writes the output)
@@ -520,6 +525,205 @@ __global__ __launch_bounds__(256) void hevc_sao(HevcSaoArgs a) {
   }
 }
 
+
+// ---- 64x64 CTUs: statistics without an LDS tile.  Lane = column (luma: 64 columns; chroma:
+// 32 columns per half wave), each lane walks its rows with the rows above / below in
+// registers and the horizontal neighbours by lane shuffles (the CTU's edge columns load theirs);
+// edge-offset counts and sums accumulate in registers and reach LDS once per wave, the band
+// histogram takes one 64-bit LDS add per sample (count in bits 0-15, sum above).  Integer sums:
+// the statistics, and so the decision, equal those of hevc_sao's tile pass.
+__global__ __launch_bounds__(256) void hevc_sao_stats64(HevcSaoArgs a) {
+  __shared__ SaoShared S;
+  __shared__ unsigned long long bo64[3][32];
+  const int slot = blockIdx.y;
+  if (a.run[slot] == 0) return;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wctu = (a.wctb + 1) / 2;
+  const int rx = (blockIdx.x % wctu) * 2, ry = (blockIdx.x / wctu) * 2;
+  const int ci = ry * a.wctb + rx;
+  for (int i = tid; i < 3 * 16; i += 256) {
+    (&S.eo_cnt[0][0][0])[i] = 0;
+    (&S.eo_sum[0][0][0])[i] = 0;
+  }
+  if (tid < 96) (&bo64[0][0])[tid] = 0;
+  __syncthreads();
+  if (a.enable) {
+    const int bd = a.bd;
+#pragma unroll 1
+    for (int c = 0; c < 3; ++c) {
+      const int pw = c ? a.W / 2 : a.W, ph = c ? a.H / 2 : a.H;
+      const size_t ps = static_cast<size_t>(pw) * ph;
+      const uint16_t* d = (c == 0 ? a.dy : (c == 1 ? a.du : a.dv)) + slot * ps;
+      const uint16_t* src = (c == 0 ? a.sy : (c == 1 ? a.su : a.sv)) + slot * ps;
+      const int xw = c ? 32 : 64;               // shuffle segment = one CTU row of this component
+      const int x = c ? (lane & 31) : lane;
+      const int nrows = c ? 4 : 16;
+      const int X = (c ? rx * 16 : rx * 32) + x;
+      const int Y0 = (c ? ry * 16 + (w * 2 + (lane >> 5)) * 4 : ry * 32 + w * 16);
+      const bool xin = X < pw;
+      auto ld = [&](int xx, int yy) -> int {
+        return d[static_cast<size_t>(clampi(yy, 0, ph - 1)) * pw + clampi(xx, 0, pw - 1)];
+      };
+      // neighbour columns X - 1 / X + 1 of a row: lane shuffles inside the CTU row, loads at its edges
+      auto lft = [&](int v, int yy) { const int t = __shfl_up(v, 1, xw); return x == 0 ? ld(X - 1, yy) : t; };
+      auto rgt = [&](int v, int yy) { const int t = __shfl_down(v, 1, xw); return x == xw - 1 ? ld(X + 1, yy) : t; };
+      int cnt[4][4], sm[4][4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cnt[k][e] = sm[k][e] = 0;
+      int cp = ld(X, Y0 - 1), cc = ld(X, Y0);
+      int lp = lft(cp, Y0 - 1), rp = rgt(cp, Y0 - 1), lc = lft(cc, Y0), rc = rgt(cc, Y0);
+      const bool hx = X - 1 >= 0 && X + 1 < pw;
+#pragma unroll 1
+      for (int i = 0; i < nrows; ++i) {
+        const int Y = Y0 + i;
+        const int cn = ld(X, Y + 1);
+        const int ln = lft(cn, Y + 1), rn = rgt(cn, Y + 1);
+        if (xin && Y < ph) {
+          const int v = cc;
+          const int diff = static_cast<int>(src[static_cast<size_t>(Y) * pw + X]) - v;
+          atomicAdd(&bo64[c][v >> (bd - 5)],
+                    (static_cast<unsigned long long>(static_cast<long long>(diff)) << 16) + 1ull);
+          const bool hy = Y - 1 >= 0 && Y + 1 < ph;
+          const int A[4] = {lc, cp, lp, rp}, Bn[4] = {rc, cn, rn, ln};
+          const bool ok[4] = {hx, hy, hx && hy, hx && hy};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            int e = 2 + sgn(v - A[k]) + sgn(v - Bn[k]);
+            e = e < 2 ? e + 1 : (e == 2 ? 0 : e);
+            e = ok[k] ? e : 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const bool hit = e == q + 1;
+              cnt[k][q] += hit;
+              sm[k][q] += hit ? diff : 0;
+            }
+          }
+        }
+        cp = cc;
+        cc = cn;
+        lp = lc;
+        lc = ln;
+        rp = rc;
+        rc = rn;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int n = sum64(cnt[k][q]), t = sum64(sm[k][q]);
+          if (lane == 0 && n) {
+            atomicAdd(&S.eo_cnt[c][k][q], n);
+            atomicAdd(&S.eo_sum[c][k][q], t);
+          }
+        }
+    }
+  }
+  __syncthreads();
+  if (tid < 96) {
+    const unsigned long long v = (&bo64[0][0])[tid];
+    (&S.bo_cnt[0][0])[tid] = static_cast<int>(v & 0xFFFFull);
+    (&S.bo_sum[0][0])[tid] = static_cast<int>(static_cast<long long>(v) >> 16);
+  }
+  __syncthreads();
+  sao_decide(a, S, slot, ci, 4, tid);
+}
+
+// ---- apply: one lane per 4 horizontally adjacent samples of every plane, parameters from the
+// sample's record block, neighbours straight from the deblocked picture (L1 / L2 hits)
+__global__ __launch_bounds__(256) void hevc_sao_apply(HevcSaoArgs a) {
+  const int slot = blockIdx.y;
+  if (a.run[slot] == 0) return;
+  const int gwl = a.W / 4, gwc = a.W / 8;
+  const int gl = gwl * a.H, gc = gwc * (a.H / 2);
+  int gi = blockIdx.x * 256 + threadIdx.x;
+  if (gi >= gl + 2 * gc) return;
+  int c, X, Y;
+  if (gi < gl) {
+    c = 0;
+    Y = gi / gwl;
+    X = (gi - Y * gwl) * 4;
+  } else {
+    gi -= gl;
+    c = 1 + (gi >= gc);
+    gi -= (c - 1) * gc;
+    Y = gi / gwc;
+    X = (gi - Y * gwc) * 4;
+  }
+  const int pw = c ? a.W / 2 : a.W, ph = c ? a.H / 2 : a.H;
+  const size_t ps = static_cast<size_t>(pw) * ph;
+  const uint16_t* d = (c == 0 ? a.dy : (c == 1 ? a.du : a.dv)) + slot * ps;
+  uint16_t* o = (c == 0 ? a.y : (c == 1 ? a.u : a.v)) + slot * ps;
+  const int bsh = c ? 4 : 5;  // record block of the sample (32 luma / 16 chroma samples)
+  const CtuInfo& t = a.ctu[static_cast<size_t>(slot) * a.wctb * a.hctb + (Y >> bsh) * a.wctb + (X >> bsh)];
+  const int type = t.sao_type[c ? 1 : 0];
+  const size_t ro = static_cast<size_t>(Y) * pw + X;
+  const uint2 cw = *reinterpret_cast<const uint2*>(d + ro);
+  int v[4] = {static_cast<int>(cw.x & 0xFFFF), static_cast<int>(cw.x >> 16), static_cast<int>(cw.y & 0xFFFF),
+              static_cast<int>(cw.y >> 16)};
+  const int maxv = (1 << a.bd) - 1;
+  int r[4] = {v[0], v[1], v[2], v[3]};
+  if (type == 1) {
+    const int band = t.sao_band[c];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = ((v[i] >> (a.bd - 5)) - band) & 31;
+      if (k < 4) r[i] = clampi(v[i] + t.sao_off[c][k], 0, maxv);
+    }
+  } else if (type == 2) {
+    const int k = t.sao_class[c ? 1 : 0];
+    // the 6 samples X - 1 .. X + 4 of row yy (clamped loads; unavailable ones are never used)
+    auto row6 = [&](int yy, int* q) {
+      const uint16_t* rp = d + static_cast<size_t>(clampi(yy, 0, ph - 1)) * pw;
+      const uint2 m = *reinterpret_cast<const uint2*>(rp + X);
+      q[0] = rp[X > 0 ? X - 1 : 0];
+      q[1] = m.x & 0xFFFF;
+      q[2] = m.x >> 16;
+      q[3] = m.y & 0xFFFF;
+      q[4] = m.y >> 16;
+      q[5] = rp[X + 4 < pw ? X + 4 : pw - 1];
+    };
+    int up[6], mid[6], dn[6];
+    row6(Y, mid);
+    if (k != 0) {
+      row6(Y - 1, up);
+      row6(Y + 1, dn);
+    }
+    // class k's neighbour pair of sample i with constant register indices (k: 0 horizontal,
+    // 1 vertical, 2 135 degrees, 3 45 degrees)
+    const bool hx0 = X > 0, hx1 = X + 4 < pw, hy = Y > 0 && Y + 1 < ph;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool lok = i > 0 || hx0, rok = i < 3 || hx1;
+      int A, Bv;
+      bool ok;
+      if (k == 0) {
+        A = mid[i];
+        Bv = mid[i + 2];
+        ok = lok && rok;
+      } else if (k == 1) {
+        A = up[i + 1];
+        Bv = dn[i + 1];
+        ok = hy;
+      } else if (k == 2) {
+        A = up[i];
+        Bv = dn[i + 2];
+        ok = hy && lok && rok;
+      } else {
+        A = up[i + 2];
+        Bv = dn[i];
+        ok = hy && lok && rok;
+      }
+      if (!ok) continue;
+      int e = 2 + sgn(v[i] - A) + sgn(v[i] - Bv);
+      if (e <= 2) e = (e == 2) ? 0 : e + 1;
+      if (e) r[i] = clampi(v[i] + t.sao_off[c][e - 1], 0, maxv);
+    }
+  }
+  *reinterpret_cast<uint2*>(o + ro) = make_uint2(static_cast<uint32_t>(r[0]) | static_cast<uint32_t>(r[1]) << 16,
+                                                 static_cast<uint32_t>(r[2]) | static_cast<uint32_t>(r[3]) << 16);
+}
 
 // ============================================================== adaptive quantisation
 // Per-CTB QP (x265 --aq-mode 1 --qg-size 32, the libx265 default family of the
@@ -808,10 +1012,20 @@ extern "C" void mivc_launch_hevc_sao(int B, int W, int H, int bd, const uint16_t
     hipLaunchKernelGGL(hevc_sao, dim3((W / 32) * (H / 32), B), dim3(256), 0, s, a);
     return;
   }
+  static const bool tile_pass = [] {  // MIVC_HEVC_SAO_TILE=1: the LDS-tile pass (A/B switch)
+    const char* e = std::getenv("MIVC_HEVC_SAO_TILE");
+    return e && std::atoi(e) == 1;
+  }();
   a.mode = 1;
-  hipLaunchKernelGGL(hevc_sao, dim3(((W / 32 + 1) / 2) * ((H / 32 + 1) / 2), B), dim3(256), 0, s, a);
-  a.mode = 2;
-  hipLaunchKernelGGL(hevc_sao, dim3((W / 32) * (H / 32), B), dim3(256), 0, s, a);
+  if (tile_pass) {
+    hipLaunchKernelGGL(hevc_sao, dim3(((W / 32 + 1) / 2) * ((H / 32 + 1) / 2), B), dim3(256), 0, s, a);
+    a.mode = 2;
+    hipLaunchKernelGGL(hevc_sao, dim3((W / 32) * (H / 32), B), dim3(256), 0, s, a);
+    return;
+  }
+  hipLaunchKernelGGL(hevc_sao_stats64, dim3(((W / 32 + 1) / 2) * ((H / 32 + 1) / 2), B), dim3(256), 0, s, a);
+  const int groups = (W / 4) * H + 2 * (W / 8) * (H / 2);
+  hipLaunchKernelGGL(hevc_sao_apply, dim3((groups + 255) / 256, B), dim3(256), 0, s, a);
 }
 
 // ctb_qp: [B, nctb] int32 out; mb_aq: [B, nmb16] int8 out (may be null); extra: optional
