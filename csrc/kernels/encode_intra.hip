@@ -697,9 +697,11 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
   PROF(7);
 }
 
-// NW waves per workgroup, one MB row each (rows y, y + NW, ...): 16 by default -- twice the rows
-// of a slot in flight at a 128-VGPR budget (some spills), same-box A/B +1.0 % headline fps and
-// +2.1 % at 4K over 8 waves at 256 VGPRs; MIVC_INTRA_WAVES=8 selects the 8-wave instance
+// NW waves per workgroup, one MB row each (rows y, y + NW, ...): 12 by default -- 1.5x the rows
+// of a slot in flight of the 8-wave instance at a 168-VGPR budget (the 16-wave one spills 640
+// B/lane at 128 VGPRs); same-box A/B of the headline (profiles/r5_intra_waves_ab.md): 12 waves
+// 13,114 fps, 16 waves 13,071, 8 waves 13,012, identical bytes.  MIVC_INTRA_WAVES=8 / 16 select
+// the other instances
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void encode_intra_wavefront(IntraArgs a) {
   __shared__ IntraShared SS[NW];
@@ -794,10 +796,13 @@ extern "C" void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t*
   const int per = slice_rows > 0 ? (hmb + slice_rows - 1) / slice_rows : 1;
   static const int nw = [] {
     const char* e = std::getenv("MIVC_INTRA_WAVES");
-    return (e && std::atoi(e) == 8) ? 8 : 16;
+    const int v = e ? std::atoi(e) : 12;
+    return (v == 8 || v == 16) ? v : 12;
   }();
   if (nw == 16)
     hipLaunchKernelGGL(encode_intra_wavefront<16>, dim3(B * per), dim3(64 * 16), 0, static_cast<hipStream_t>(stream), a);
+  else if (nw == 12)
+    hipLaunchKernelGGL(encode_intra_wavefront<12>, dim3(B * per), dim3(64 * 12), 0, static_cast<hipStream_t>(stream), a);
   else
     hipLaunchKernelGGL(encode_intra_wavefront<8>, dim3(B * per), dim3(64 * 8), 0, static_cast<hipStream_t>(stream), a);
 }

@@ -619,10 +619,11 @@ def _intra_spots_encode(w=320, h=288):
     return enc, res, spots
 
 
-def test_gpu_intra_waves_knob_keeps_bytes():
-    """MIVC_INTRA_WAVES=8 (the 8-wave intra kernel) is a speed knob: same bytes as the
-    default 16-wave instance (the launcher reads the variable once, so the 8-wave run is a
-    child process)."""
+@pytest.mark.parametrize("waves", ["8", "16"])
+def test_gpu_intra_waves_knob_keeps_bytes(waves):
+    """MIVC_INTRA_WAVES=8 / 16 (the other intra kernel instances) is a speed knob: same bytes
+    as the default 12-wave instance (the launcher reads the variable once, so the other run is
+    a child process)."""
     import hashlib
     import os
     import subprocess
@@ -633,7 +634,7 @@ def test_gpu_intra_waves_knob_keeps_bytes():
     enc.close()
     code = ("import hashlib; from tests.test_gpu_h264 import _intra_spots_encode; "
             "print(hashlib.sha256(_intra_spots_encode()[1][0].bitstream).hexdigest())")
-    env = dict(os.environ, MIVC_INTRA_WAVES="8")
+    env = dict(os.environ, MIVC_INTRA_WAVES=waves)
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110,
                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert out.returncode == 0, out.stderr[-2000:]
