@@ -319,6 +319,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
       int av;
       const int el = i4_neighbour_lane(S.t4, blk, mbav, lane, &av);
       if (lane < 13) S.e4[lane] = el;
+      if (blk == 1) PROF(10);
       const int bx = h264::kBlkX[blk], by = h264::kBlkY[blk];
       int ma = bx > 0 ? S.modes4[h264::kRasterToBlk[(bx - 1) + 4 * by]] : S.left_modes[by];
       int mb_ = by > 0 ? S.modes4[h264::kRasterToBlk[bx + 4 * (by - 1)]] : S.top_modes[bx];
@@ -331,6 +332,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
         int st = S.e4[1] + S.e4[2] + S.e4[3] + S.e4[4], sl = S.e4[9] + S.e4[10] + S.e4[11] + S.e4[12];
         dcv = __builtin_amdgcn_readfirstlane((t && l) ? (st + sl + 4) >> 3 : (l ? (sl + 2) >> 2 : (t ? (st + 2) >> 2 : 128)));
       }
+      if (blk == 1) PROF(11);
       // mode ranking: lane = mode * 4 + row (lanes 0..35)
       int m = lane >> 2;
       bool valid = m < 9 && h264::i4_mode_ok(m, av);
@@ -349,6 +351,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
       key = wave_min(key);
       const int mode = key & 15;
       total += key >> 4;
+      if (blk == 1) PROF(12);
       // transform / quantise / reconstruct the chosen mode (every group computes the same block)
       int pr[4];
       wave_sync();
@@ -378,10 +381,12 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
       }
       if (lane == 0) S.modes4[blk] = static_cast<uint8_t>(mode);
       wave_sync();
+      if (blk == 1) PROF(13);
     }
     use4 = total < cost16;
     cost4 = __builtin_amdgcn_readfirstlane(total);
   }
+  PROF(9);  // (profile builds: I4x4 trial done, I8x8 next)
 
   // ---- Intra8x8 trial (closed loop over the four 8x8 blocks, 9 modes ranked on sa8d)
   bool use8 = false;
