@@ -7,7 +7,7 @@
 //   matrix cores (v_mfma_f32_16x16x16_f16: 16 blocks per instruction); the
 //   CTB then picks the best mode per CU and the split that minimises SATD + lambda *
 //   bits.  No dependency between CTBs: the whole picture is analysed in parallel.
-// * hevc_intra_recon (grid = slots, 8 waves per workgroup): CTBs in wavefront order
+// * hevc_intra_recon (grid = slots x 3 components, 8 waves per workgroup): CTBs in wavefront order
 //   (MB-row progress counters in LDS, 2-CTB lag as the H.264 kernels), CUs in z-order
 //   inside a CTB: reference samples from the reconstruction, prediction, forward
 //   transform, quantisation, dequantisation and the normative inverse transform
@@ -573,57 +573,44 @@ __device__ __forceinline__ bool recon_block(const HevcIntraArgs& a, ReconShared&
 }
 
 // (inlined at its single call site: its LDS structures stay ds_ addressed, no call frame)
+// One colour component per workgroup (comp = blockIdx.y): the three planes of a picture are
+// independent intra wavefronts (no cross-component prediction in Main / Main 10), so a slot's
+// luma, Cb and Cr run side by side on three CUs instead of one after another in one wave.
 __device__ __forceinline__ void hevc_recon_ctb(const HevcIntraArgs& a, ReconShared& S, const hv::DctLds& D, int slot,
-                                               int rx, int ry, int run) {
+                                               int rx, int ry, int run, int comp) {
   const HevcGeom& g = a.g;
   const int lane = lane_id();
   const int X0 = rx * 32, Y0 = ry * 32;
   const size_t cb = static_cast<size_t>(slot) * g.nctb() + ry * g.wctb + rx;
-  const uint16_t* recy = a.rec_y + slot * g.ysize();
-  const uint16_t* recu = a.rec_u + slot * g.csize();
-  const uint16_t* recv = a.rec_v + slot * g.csize();
-  const int cw = g.W / 2;
-  // ---- stage the neighbourhood: row above (x -1..63), left column, and (P) the CTB interior
-  for (int i = lane; i < 65; i += 64) {
-    const int x = X0 - 1 + i;
-    S.rt[i] = (ry > 0 && x >= 0 && x < g.W) ? recy[static_cast<size_t>(Y0 - 1) * g.W + x] : 0;
+  const bool luma = comp == 0;
+  const int c1 = comp - 1;
+  // the component's plane, its width and the CTB's extent in it
+  const uint16_t* rp = luma ? a.rec_y + slot * g.ysize() : (comp == 1 ? a.rec_u : a.rec_v) + slot * g.csize();
+  const int pw = luma ? g.W : g.W / 2;
+  const int n = luma ? 32 : 16, st = luma ? RT : CT2;
+  const int x0 = luma ? X0 : X0 / 2, y0 = luma ? Y0 : Y0 / 2;
+  uint16_t* tile = luma ? S.rt : S.rc[c1];
+  const bool same_left = S.saved_x == rx - 1 && S.saved_ry == ry;
+  // ---- stage the neighbourhood: row above (x -1 .. 2n - 1), left column, and (P) the CTB interior
+  for (int i = lane; i < 2 * n + 1; i += 64) {
+    const int x = x0 - 1 + i;
+    tile[i] = (ry > 0 && x >= 0 && x < pw) ? rp[static_cast<size_t>(y0 - 1) * pw + x] : 0;
   }
-  if (lane < 32) {
+  if (lane < n) {
     uint16_t v = 0;
-    if (rx > 0) v = (S.saved_x == rx - 1 && S.saved_ry == ry) ? S.saved_y[lane] : recy[static_cast<size_t>(Y0 + lane) * g.W + X0 - 1];
-    S.rt[(lane + 1) * RT] = v;
-  } else {
-    const int c = (lane - 32) >> 4, i = (lane - 32) & 15;
-    const uint16_t* rc = c == 0 ? recu : recv;
-    uint16_t v = 0;
-    if (rx > 0) v = (S.saved_x == rx - 1 && S.saved_ry == ry) ? S.saved_c[c][i] : rc[static_cast<size_t>(Y0 / 2 + i) * cw + X0 / 2 - 1];
-    S.rc[c][(i + 1) * CT2] = v;
+    if (rx > 0) v = same_left ? (luma ? S.saved_y[lane] : S.saved_c[c1][lane]) : rp[static_cast<size_t>(y0 + lane) * pw + x0 - 1];
+    tile[(lane + 1) * st] = v;
   }
-  if (a.ctu64 && !((rx | ry) & 1) && rx > 0 && ry + 1 < g.hctb) {
-    // the top-left block of a CTU: the left column below it (x -1, y 32..63; chroma y 16..31,
-    // in the previous CTU's bottom-right block) into the tile's last column (x 63 / 31 of
-    // rows 0..31 / 0..15: right of the block, never referenced by it)
-    if (lane < 32) {
-      S.rt[(lane + 1) * RT + RT - 1] = recy[static_cast<size_t>(Y0 + 32 + lane) * g.W + X0 - 1];
-    } else {
-      const int c = (lane - 32) >> 4, i = (lane - 32) & 15;
-      S.rc[c][(i + 1) * CT2 + CT2 - 1] = (c == 0 ? recu : recv)[static_cast<size_t>(Y0 / 2 + 16 + i) * cw + X0 / 2 - 1];
-    }
-  }
-  for (int i = lane; i < 2 * 33; i += 64) {
-    const int c = i / 33, k = i % 33;
-    const uint16_t* rc = c == 0 ? recu : recv;
-    const int x = X0 / 2 - 1 + k;
-    S.rc[c][k] = (ry > 0 && x >= 0 && x < cw) ? rc[static_cast<size_t>(Y0 / 2 - 1) * cw + x] : 0;
+  if (a.ctu64 && !((rx | ry) & 1) && rx > 0 && ry + 1 < g.hctb && lane < n) {
+    // the top-left block of a CTU: the left column below it (x -1, y n .. 2n - 1, in the previous
+    // CTU's bottom-right block) into the tile's last column (x 2n - 1 of rows 0 .. n - 1: right of
+    // the block, never referenced by it)
+    tile[(lane + 1) * st + st - 1] = rp[static_cast<size_t>(y0 + n + lane) * pw + x0 - 1];
   }
   if (run == 2) {  // P picture: inter CUs of this CTB are already reconstructed
-    for (int i = lane; i < 32 * 32; i += 64) {
-      const int y = i >> 5, x = i & 31;
-      S.rt[(y + 1) * RT + x + 1] = recy[static_cast<size_t>(Y0 + y) * g.W + X0 + x];
-    }
-    for (int i = lane; i < 2 * 256; i += 64) {
-      const int c = i >> 8, k = i & 255, y = k >> 4, x = k & 15;
-      S.rc[c][(y + 1) * CT2 + x + 1] = (c == 0 ? recu : recv)[static_cast<size_t>(Y0 / 2 + y) * cw + X0 / 2 + x];
+    for (int i = lane; i < n * n; i += 64) {
+      const int y = i / n, x = i - y * n;
+      tile[(y + 1) * st + x + 1] = rp[static_cast<size_t>(y0 + y) * pw + x0 + x];
     }
   }
   wave_sync();
@@ -646,31 +633,36 @@ __device__ __forceinline__ void hevc_recon_ctb(const HevcIntraArgs& a, ReconShar
       const int mode = __builtin_amdgcn_readfirstlane(cu->mode);
       const int gx = (k & 1) | ((k >> 1) & 2), gy = ((k >> 1) & 1) | ((k >> 2) & 2);
       const int cx = gx * 8, cy = gy * 8;
-      bool ny = false;
-      if (log2n == 3 && (__builtin_amdgcn_readfirstlane(cu->flags) & 8)) {
+      bool nz = false;
+      if (!luma) {
+        nz = recon_block<false>(a, S, D, slot, comp, rx, ry, cx / 2, cy / 2, log2n - 1, mode, 4 * k, qpc);
+      } else if (log2n == 3 && (__builtin_amdgcn_readfirstlane(cu->flags) & 8)) {
         // PART_NxN: four 4x4 luma PUs in z-order, DST, each predicted from the previous ones
         const uint32_t pm = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t*>(cu->mv));
         for (int j = 0; j < 4; ++j)
-          ny |= recon_block<true>(a, S, D, slot, 0, rx, ry, cx + (j & 1) * 4, cy + (j >> 1) * 4, 2,
+          nz |= recon_block<true>(a, S, D, slot, 0, rx, ry, cx + (j & 1) * 4, cy + (j >> 1) * 4, 2,
                                   static_cast<int>((pm >> (8 * j)) & 255u), 4 * k + j, qpl, true);
       } else {
-        ny = recon_block<true>(a, S, D, slot, 0, rx, ry, cx, cy, log2n, mode, 4 * k, qpl);
+        nz = recon_block<true>(a, S, D, slot, 0, rx, ry, cx, cy, log2n, mode, 4 * k, qpl);
       }
-      const bool nu = recon_block<false>(a, S, D, slot, 1, rx, ry, cx / 2, cy / 2, log2n - 1, mode, 4 * k, qpc);
-      const bool nv = recon_block<false>(a, S, D, slot, 2, rx, ry, cx / 2, cy / 2, log2n - 1, mode, 4 * k, qpc);
       if (lane < step) {
+        // cbf bit `comp` of the granule's record (byte 2 of its first word): the three
+        // component workgroups set their own bits of the same byte, so one atomic each
         CuInfo* c = a.cu + cb * 16 + k + lane;
-        c->cbf = static_cast<uint8_t>(ny | (nu << 1) | (nv << 2));
-        c->pred = hevc::CU_INTRA;
+        unsigned int* w0 = reinterpret_cast<unsigned int*>(c);
+        const unsigned int bit = 1u << (16 + comp);
+        if (nz) atomicOr(w0, bit);
+        else atomicAnd(w0, ~bit);
+        if (luma) c->pred = hevc::CU_INTRA;
       }
     }
     k += step;
   }
   // ---- keep this CTB's right column for the next CTB of the row
-  if (lane < 32) S.saved_y[lane] = S.rt[(lane + 1) * RT + 32];
-  else {
-    const int c = (lane - 32) >> 4, i = (lane - 32) & 15;
-    S.saved_c[c][i] = S.rc[c][(i + 1) * CT2 + 16];
+  if (lane < n) {
+    const uint16_t v = tile[(lane + 1) * st + n];
+    if (luma) S.saved_y[lane] = v;
+    else S.saved_c[c1][lane] = v;
   }
   if (lane == 0) {
     S.saved_x = rx;
@@ -688,7 +680,7 @@ __global__ __launch_bounds__(64 * kHevcIntraWaves) void hevc_intra_recon(HevcInt
   __shared__ hv::DctLds D;
   __shared__ int prog[kMaxRows];
   const HevcGeom& g = a.g;
-  const int slot = blockIdx.x;
+  const int slot = blockIdx.x, comp = blockIdx.y;
   const int run = a.run[slot];
   if (run == 0) return;
   hv::dct_lds_init(D);
@@ -720,7 +712,7 @@ __global__ __launch_bounds__(64 * kHevcIntraWaves) void hevc_intra_recon(HevcInt
         if (work) {
           if (y > 0 && !waited) row_wait(prog, y - 1, min(x + 2, wu), a.err);
           waited = true;
-          hevc_recon_ctb(a, S, D, slot, bx, by, run);
+          hevc_recon_ctb(a, S, D, slot, bx, by, run, comp);
         } else {
           if (lane_id() == 0) S.saved_x = -2;
           wave_sync();
@@ -775,5 +767,5 @@ extern "C" void mivc_launch_hevc_intra(int B, int W, int H, const uint16_t* sy, 
   a.ctu64 = ctu64;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (analyze) hipLaunchKernelGGL(hevc_intra_analyze, dim3(a.g.nctb(), B), dim3(256), 0, s, a);
-  if (recon) hipLaunchKernelGGL(hevc_intra_recon, dim3(B), dim3(64 * kHevcIntraWaves), 0, s, a);
+  if (recon) hipLaunchKernelGGL(hevc_intra_recon, dim3(B, 3), dim3(64 * kHevcIntraWaves), 0, s, a);
 }
