@@ -52,6 +52,11 @@ struct IntraArgs {
   // 1 = 4x4 luma (Intra4x4, Intra16x16 AC), 2 = also Intra8x8 and chroma AC; 0 = dead-zone
   int trellis;
   float trellis_lambda;
+  // workgroups per slice (I pictures of small batches): the slice's rows are dealt round-robin
+  // to wg_per_slice x NW waves on as many CUs, their progress in gprog ([units][kMaxRows],
+  // device memory, zeroed by the launcher); 1 = one workgroup, progress in LDS
+  int wg_per_slice;
+  int* gprog;
 };
 
 __device__ __forceinline__ bool top_in_slice(int my, int slice_rows) {
@@ -710,18 +715,25 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void encode_intra_wavefront(IntraArgs a) {
   __shared__ IntraShared SS[NW];
-  __shared__ int prog[kMaxRows];
+  __shared__ int lprog[kMaxRows];
   const Geom& g = a.g;
-  // one workgroup per slice: intra prediction never crosses a slice's top edge, so the slices
-  // of a picture are independent wavefronts (a 4K batch of 64 slots in 4 slices fills the chip
-  // with 256 workgroups instead of 64)
+  // one workgroup per slice, or wg_per_slice of them: intra prediction never crosses a slice's
+  // top edge, so the slices of a picture are independent wavefronts (a 4K batch of 64 slots in
+  // 4 slices fills the chip with 256 workgroups instead of 64); a 1080p I picture of 64 slots
+  // deals each slice's rows to 4 workgroups.  Workgroup k of unit u is blockIdx k * units + u:
+  // with units a multiple of 8 the unit's workgroups share an XCD (blockIdx mod 8).
+  const int K = a.wg_per_slice;
   const int per = a.slice_rows > 0 ? (g.hmb + a.slice_rows - 1) / a.slice_rows : 1;
-  const int slot = blockIdx.x / per, sl = blockIdx.x - slot * per;
+  const int units = g.B * per;
+  const int kk = blockIdx.x / units, unit = blockIdx.x - kk * units;
+  const int slot = unit / per, sl = unit - slot * per;
   const int y_begin = a.slice_rows > 0 ? sl * a.slice_rows : 0;
   const int y_end = a.slice_rows > 0 ? min(g.hmb, y_begin + a.slice_rows) : g.hmb;
   if (!route_active(a.rt, slot, -1)) return;  // uniform per workgroup
   if (a.intra_flag && a.intra_count[slot] == 0) return;
-  for (int i = threadIdx.x; i < g.hmb; i += blockDim.x) prog[i] = 0;
+  int* prog = K > 1 ? a.gprog + static_cast<size_t>(unit) * kMaxRows : lprog;
+  if (K == 1)
+    for (int i = threadIdx.x; i < g.hmb; i += blockDim.x) lprog[i] = 0;
   const int w = wave_id();
   if (lane_id() == 0) SS[w].saved_x = -2;
   __syncthreads();
@@ -733,12 +745,28 @@ __global__ __launch_bounds__(64 * NW) void encode_intra_wavefront(IntraArgs a) {
 #pragma unroll
     for (int x = 0; x < 4; ++x) tapw[x] = h264::kI4Taps[m][r * 4 + x];
   }
-  for (int y = y_begin + w; y < y_end; y += NW) {
+  // the row above's progress this wave has already acquired (device-scope waits only when it
+  // is not far enough yet: one acquire covers every MB it admits)
+  int seen = -1, seen_row = -1;
+  auto wait = [&](int row, int target) {
+    if (K == 1) {
+      row_wait(prog, row, target, a.err);
+      return;
+    }
+    if (seen_row == row && seen >= target) return;
+    seen = __builtin_amdgcn_readfirstlane(row_wait_agent(prog, row, target, a.err));
+    seen_row = row;
+  };
+  auto publish = [&](int row, int value) {
+    if (K == 1) row_publish(prog, row, value);
+    else row_publish_agent(prog, row, value);
+  };
+  for (int y = y_begin + kk * NW + w; y < y_end; y += K * NW) {
     if (!a.intra_flag) {  // I frame: every MB
       for (int x = 0; x < g.wmb; ++x) {
-        if (top_in_slice(y, a.slice_rows)) row_wait(prog, y - 1, min(x + 2, g.wmb), a.err);
+        if (top_in_slice(y, a.slice_rows)) wait(y - 1, min(x + 2, g.wmb));
         encode_intra_mb(a, S, slot, x, y, tapw);
-        row_publish(prog, y, x + 1);
+        publish(y, x + 1);
 #ifdef MIVC_INTRA_PROFILE
         if (slot == 0 && w == 0 && lane == 0 && y == 0 && x < 16) g_intra_prof[x][8] = clock64();
 #endif
@@ -753,13 +781,13 @@ __global__ __launch_bounds__(64 * NW) void encode_intra_wavefront(IntraArgs a) {
       while (mask) {
         const int x = x0 + __builtin_ctzll(mask);
         mask &= mask - 1;
-        if (x > 0) row_publish(prog, y, x);  // MBs before x in this row are final (inter)
-        if (top_in_slice(y, a.slice_rows)) row_wait(prog, y - 1, min(x + 2, g.wmb), a.err);
+        if (x > 0) publish(y, x);  // MBs before x in this row are final (inter)
+        if (top_in_slice(y, a.slice_rows)) wait(y - 1, min(x + 2, g.wmb));
         encode_intra_mb(a, S, slot, x, y, tapw);
-        row_publish(prog, y, x + 1);
+        publish(y, x + 1);
       }
     }
-    row_publish(prog, y, g.wmb);
+    publish(y, g.wmb);
   }
 }
 
@@ -799,17 +827,51 @@ extern "C" void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t*
   a.use_i4x4 = use_i4x4;
   a.use_i8x8 = use_i8x8;
   const int per = slice_rows > 0 ? (hmb + slice_rows - 1) / slice_rows : 1;
+  // I pictures of a batch with fewer slice wavefronts than CUs / 4: several workgroups per
+  // slice (all of them resident: at most 256 workgroups of <= 80 KB LDS, two fit a CU), each
+  // unit's in one XCD when the unit count is a multiple of 8.  MIVC_INTRA_WG=1: one per slice.
+  static const int wg_cap = [] {
+    const char* e = std::getenv("MIVC_INTRA_WG");
+    const int v = e ? std::atoi(e) : 4;
+    return v < 1 ? 1 : (v > 8 ? 8 : v);
+  }();
+  const int units = B * per;
+  int K = 1;
+  if (!intra_flag && units % 8 == 0)
+    while (K * 2 <= wg_cap && units * K * 2 <= 256) K *= 2;
+  a.wg_per_slice = K;
+  a.gprog = nullptr;
+  if (K > 1) {
+    static int* gprog = nullptr;
+    static size_t gcap = 0;
+    const size_t need = static_cast<size_t>(units) * kMaxRows * sizeof(int);
+    if (need > gcap) {
+      if (gprog) (void)hipFree(gprog);
+      if (hipMalloc(&gprog, need) != hipSuccess) {
+        gprog = nullptr;
+        gcap = 0;
+      } else {
+        gcap = need;
+      }
+    }
+    if (gprog) {
+      a.gprog = gprog;
+      (void)hipMemsetAsync(gprog, 0, need, static_cast<hipStream_t>(stream));
+    } else {
+      a.wg_per_slice = K = 1;
+    }
+  }
   static const int nw = [] {
     const char* e = std::getenv("MIVC_INTRA_WAVES");
     const int v = e ? std::atoi(e) : 12;
     return (v == 8 || v == 16) ? v : 12;
   }();
   if (nw == 16)
-    hipLaunchKernelGGL(encode_intra_wavefront<16>, dim3(B * per), dim3(64 * 16), 0, static_cast<hipStream_t>(stream), a);
+    hipLaunchKernelGGL(encode_intra_wavefront<16>, dim3(B * per * K), dim3(64 * 16), 0, static_cast<hipStream_t>(stream), a);
   else if (nw == 12)
-    hipLaunchKernelGGL(encode_intra_wavefront<12>, dim3(B * per), dim3(64 * 12), 0, static_cast<hipStream_t>(stream), a);
+    hipLaunchKernelGGL(encode_intra_wavefront<12>, dim3(B * per * K), dim3(64 * 12), 0, static_cast<hipStream_t>(stream), a);
   else
-    hipLaunchKernelGGL(encode_intra_wavefront<8>, dim3(B * per), dim3(64 * 8), 0, static_cast<hipStream_t>(stream), a);
+    hipLaunchKernelGGL(encode_intra_wavefront<8>, dim3(B * per * K), dim3(64 * 8), 0, static_cast<hipStream_t>(stream), a);
 }
 
 #ifdef MIVC_INTRA_PROFILE

@@ -175,6 +175,27 @@ __device__ __forceinline__ void row_publish_lds(int* prog, int row, int value) {
   if (lane_id() == 0) __hip_atomic_store(prog + row, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// device-scope progress counters (several workgroups share one wavefront): the acquire /
+// release order the reconstruction's global loads and stores across CUs (and XCDs)
+// returns the progress it observed (>= target): the acquire covers everything up to it
+__device__ __forceinline__ int row_wait_agent(int* prog, int row, int target, int* err) {
+  int spins = 0, v;
+  while ((v = __hip_atomic_load(prog + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < target) {
+    __builtin_amdgcn_s_sleep(2);
+    if (++spins > (1 << 22)) {
+      if (lane_id() == 0) atomicOr(err, 1);
+      v = target;
+      break;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return v;
+}
+__device__ __forceinline__ void row_publish_agent(int* prog, int row, int value) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  if (lane_id() == 0) __hip_atomic_store(prog + row, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // publish prog[row] = value after this wave's global stores
 __device__ __forceinline__ void row_publish(int* prog, int row, int value) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");

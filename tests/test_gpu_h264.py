@@ -639,3 +639,32 @@ def test_gpu_intra_waves_knob_keeps_bytes(waves):
                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert out.returncode == 0, out.stderr[-2000:]
     assert out.stdout.split()[-1] == here
+
+
+def _multi_wg_bytes():
+    import hashlib
+    import torch
+    from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
+    enc = GpuH264Encoder(H264Params(width=320, height=240, crf=None, qp=24), slots=8)
+    y, u, v = synth_clip(8, 3, 320, 240, seed=29)
+    res = enc.encode(y, u, v, keep_recon=True)
+    torch.cuda.synchronize()
+    return enc, res, hashlib.sha256(b"".join(r.bitstream for r in res)).hexdigest()
+
+
+def test_gpu_intra_multi_workgroup_wavefront(host):
+    """I pictures of a batch with few slice wavefronts deal each slice's MB rows to several
+    workgroups (device-scope progress counters, 8 slots -> 4 workgroups per slot here): the
+    reconstruction still equals the CPU decoder's, and the bytes equal the one-workgroup
+    wavefront's (MIVC_INTRA_WG=1 in a child process)."""
+    import os
+    import subprocess
+    import sys
+    enc, res, here = _multi_wg_bytes()
+    _check_roundtrip(host, enc, res, 320, 240)
+    enc.close()
+    code = "from tests.test_gpu_h264 import _multi_wg_bytes; print(_multi_wg_bytes()[2])"
+    out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, MIVC_INTRA_WG="1"), capture_output=True,
+                         text=True, timeout=110, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.split()[-1] == here
