@@ -696,30 +696,57 @@ __global__ __launch_bounds__(64 * kHevcIntraWaves) void hevc_intra_recon(HevcInt
   // CTBs, or (ctu64) 64x64 CTUs whose four 32x32 blocks follow in z-order
   const int c64 = a.ctu64 ? 1 : 0;
   const int wu = (g.wctb + c64) >> c64, hu = (g.hctb + c64) >> c64, nq = c64 ? 4 : 1;
+  // a block's "has intra CUs" flag (P pictures): any of its 16 granule records is intra
+  auto block_work = [&](int bx, int by) {
+    const size_t cb = (static_cast<size_t>(slot) * g.nctb() + by * g.wctb + bx) * 16;
+    return __ballot(lane_id() < 16 && a.cu[cb + lane_id()].pred == hevc::CU_INTRA) != 0;
+  };
   for (int y = w; y < hu; y += kHevcIntraWaves) {
-    for (int x = 0; x < wu; ++x) {
-      bool waited = false;
-      for (int q = 0; q < nq; ++q) {
-        const int bx = (x << c64) + (q & 1), by = (y << c64) + (q >> 1);
-        if (bx >= g.wctb || by >= g.hctb) continue;
-        // P picture: a block without intra CUs was fully reconstructed by hevc_inter -- no
-        // wait, no staging (the next block then reads its left column from memory)
-        bool work = true;
-        if (run == 2) {
-          const size_t cb = (static_cast<size_t>(slot) * g.nctb() + by * g.wctb + bx) * 16;
-          work = __ballot(lane_id() < 16 && a.cu[cb + lane_id()].pred == hevc::CU_INTRA) != 0;
-        }
-        if (work) {
-          if (y > 0 && !waited) row_wait(prog, y - 1, min(x + 2, wu), a.err);
-          waited = true;
+    if (run == 1) {  // I picture: every unit
+      for (int x = 0; x < wu; ++x) {
+        if (y > 0) row_wait(prog, y - 1, min(x + 2, wu), a.err);
+        for (int q = 0; q < nq; ++q) {
+          const int bx = (x << c64) + (q & 1), by = (y << c64) + (q >> 1);
+          if (bx >= g.wctb || by >= g.hctb) continue;
           hevc_recon_ctb(a, S, D, slot, bx, by, run, comp);
-        } else {
-          if (lane_id() == 0) S.saved_x = -2;
-          wave_sync();
         }
+        row_publish(prog, y, x + 1);
       }
-      row_publish(prog, y, x + 1);
+      continue;
     }
+    // P / B picture: the units of the row with intra CUs, 64 at a time (one lane per unit, its
+    // blocks' 16 records each); the others were fully reconstructed by hevc_inter and need
+    // neither a wait nor staging (the next block then reads its left column from memory)
+    for (int x0 = 0; x0 < wu; x0 += 64) {
+      const int xl = x0 + lane_id();
+      bool any = false;
+      if (xl < wu)
+        for (int q = 0; q < nq && !any; ++q) {
+          const int bx = (xl << c64) + (q & 1), by = (y << c64) + (q >> 1);
+          if (bx >= g.wctb || by >= g.hctb) continue;
+          const CuInfo* c = a.cu + (static_cast<size_t>(slot) * g.nctb() + by * g.wctb + bx) * 16;
+          for (int k = 0; k < 16 && !any; ++k) any = c[k].pred == hevc::CU_INTRA;
+        }
+      unsigned long long mask = __ballot(any);
+      while (mask) {
+        const int x = x0 + __builtin_ctzll(mask);
+        mask &= mask - 1;
+        if (x > 0) row_publish(prog, y, x);  // the units before x in this row are final
+        if (y > 0) row_wait(prog, y - 1, min(x + 2, wu), a.err);
+        for (int q = 0; q < nq; ++q) {
+          const int bx = (x << c64) + (q & 1), by = (y << c64) + (q >> 1);
+          if (bx >= g.wctb || by >= g.hctb) continue;
+          if (block_work(bx, by)) {
+            hevc_recon_ctb(a, S, D, slot, bx, by, run, comp);
+          } else {
+            if (lane_id() == 0) S.saved_x = -2;
+            wave_sync();
+          }
+        }
+        row_publish(prog, y, x + 1);
+      }
+    }
+    row_publish(prog, y, wu);
   }
 }
 
