@@ -470,7 +470,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
         int v[8];
 #pragma unroll
         for (int x = 0; x < 8; ++x)
-          v[x] = m < 9 ? static_cast<int>(S.src[(by + r) * 16 + bx + x]) - i8_pred_sample(m, x, r, S.f8t, S.f8l, S.f8tl, dc8) : 0;
+          v[x] = m < 9 ? static_cast<int>(S.src[(by + r) * 16 + bx + x]) - i8_pred_tap(m, x, r, S.f8t, dc8) : 0;
         had8_pass(v, 1);
 #pragma unroll
         for (int x = 0; x < 8; ++x) S.h8[lane >> 3][r * 8 + x] = v[x];

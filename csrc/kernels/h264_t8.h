@@ -120,5 +120,75 @@ __device__ __forceinline__ int i8_pred_sample(int mode, int x, int y, const int*
   }
 }
 
+// The same predictions as taps into the filtered references E = {ft[0..15], fl[0..7], ftl}
+// (IntraShared's f8t / f8l / f8tl, contiguous): one table word per (mode, sample) -- for the mode
+// ranking, where every 8 lanes evaluate another mode and the switch above would run all nine
+// cases under divergent masks.  code = i0 | i1 << 5 | i2 << 10 | kind << 15; kind 0: E[i0],
+// 1: (E[i0] + E[i1] + 1) >> 1, 2: (E[i0] + 2 E[i1] + E[i2] + 2) >> 2, 3: (E[i0] + 3 E[i1] + 2) >> 2.
+namespace i8tap {
+constexpr int T(int i) { return i < 0 ? 24 : i; }
+constexpr int L(int i) { return i < 0 ? 24 : 16 + i; }
+constexpr uint32_t t1(int a) { return static_cast<uint32_t>(a); }
+constexpr uint32_t t2(int a, int b) { return static_cast<uint32_t>(a | b << 5 | 1 << 15); }
+constexpr uint32_t t3(int a, int b, int c) { return static_cast<uint32_t>(a | b << 5 | c << 10 | 2 << 15); }
+constexpr uint32_t t13(int a, int b) { return static_cast<uint32_t>(a | b << 5 | 3 << 15); }
+constexpr uint32_t code(int mode, int x, int y) {
+  switch (mode) {
+    case 0: return t1(T(x));
+    case 1: return t1(L(y));
+    case 2: return 0;  // DC: the caller's value
+    case 3:
+      if (x == 7 && y == 7) return t13(T(14), T(15));
+      return t3(T(x + y), T(x + y + 1), T(x + y + 2));
+    case 4:
+      if (x > y) return t3(T(x - y - 2), T(x - y - 1), T(x - y));
+      if (x < y) return t3(L(y - x - 2), L(y - x - 1), L(y - x));
+      return t3(T(0), 24, L(0));
+    case 5: {
+      const int z = 2 * x - y;
+      if (z >= 0 && (z & 1) == 0) return t2(T(x - (y >> 1) - 1), T(x - (y >> 1)));
+      if (z >= 0) return t3(T(x - (y >> 1) - 2), T(x - (y >> 1) - 1), T(x - (y >> 1)));
+      if (z == -1) return t3(L(0), 24, T(0));
+      return t3(L(y - 2 * x - 1), L(y - 2 * x - 2), L(y - 2 * x - 3));
+    }
+    case 6: {
+      const int z = 2 * y - x;
+      if (z >= 0 && (z & 1) == 0) return t2(L(y - (x >> 1) - 1), L(y - (x >> 1)));
+      if (z >= 0) return t3(L(y - (x >> 1) - 2), L(y - (x >> 1) - 1), L(y - (x >> 1)));
+      if (z == -1) return t3(L(0), 24, T(0));
+      return t3(T(x - 2 * y - 1), T(x - 2 * y - 2), T(x - 2 * y - 3));
+    }
+    case 7:
+      if ((y & 1) == 0) return t2(T(x + (y >> 1)), T(x + (y >> 1) + 1));
+      return t3(T(x + (y >> 1)), T(x + (y >> 1) + 1), T(x + (y >> 1) + 2));
+    default: {
+      const int z = x + 2 * y;
+      if (z < 13 && (z & 1) == 0) return t2(L(y + (x >> 1)), L(y + (x >> 1) + 1));
+      if (z < 13) return t3(L(y + (x >> 1)), L(y + (x >> 1) + 1), L(y + (x >> 1) + 2));
+      if (z == 13) return t13(L(6), L(7));
+      return t1(L(7));
+    }
+  }
+}
+struct Table {
+  uint32_t c[9][64];
+  constexpr Table() : c() {
+    for (int m = 0; m < 9; ++m)
+      for (int i = 0; i < 64; ++i) c[m][i] = code(m, i & 7, i >> 3);
+  }
+};
+}  // namespace i8tap
+__device__ constexpr i8tap::Table kI8Taps{};
+
+__device__ __forceinline__ int i8_pred_tap(int mode, int x, int y, const int* E, int dc) {
+  if (mode == 2) return dc;
+  const uint32_t c = kI8Taps.c[mode][y * 8 + x];
+  const int kind = static_cast<int>(c >> 15);
+  const int e0 = E[c & 31], e1 = E[(c >> 5) & 31], e2 = E[(c >> 10) & 31];
+  const int w1 = kind == 0 ? 0 : (kind == 2 ? 2 : (kind == 3 ? 3 : 1));
+  const int sh = kind == 0 ? 0 : (kind == 1 ? 1 : 2);
+  return (e0 + w1 * e1 + (kind == 2 ? e2 : 0) + ((1 << sh) >> 1)) >> sh;
+}
+
 }  // namespace gpu
 }  // namespace mivc
