@@ -76,7 +76,6 @@ struct IntraShared {
   int dc16[16];            // forward DC coefficients (raster)
   uint8_t top16[16], left16[16];
   int e4[16];              // Intra4x4 neighbour vector of the current block
-  uint32_t p4[40];         // Intra4x4 ranking: predicted row (4 packed samples) per (mode, row)
   int cdcp[2][4];          // chroma DC predictions per (comp, block)
   uint8_t modes4[16];
   int cost4;
@@ -232,12 +231,12 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
         lm = S.saved_modes[i];
       } else {
         const MbHeader& L = a.hdr[o - 1];
-        lm = (L.kind == h264::MBK_I4x4 || L.kind == h264::MBK_I8x8) ? L.i4_modes[h264::kRasterToBlk[3 + 4 * i]] : 2;
+        lm = (L.kind == h264::MBK_I4x4 || L.kind == h264::MBK_I8x8) ? L.i4_modes[raster_to_blkidx(3 + 4 * i)] : 2;
       }
     }
     if (top) {
       const MbHeader& T = a.hdr[o - g.wmb];
-      tm = (T.kind == h264::MBK_I4x4 || T.kind == h264::MBK_I8x8) ? T.i4_modes[h264::kRasterToBlk[i + 12]] : 2;
+      tm = (T.kind == h264::MBK_I4x4 || T.kind == h264::MBK_I8x8) ? T.i4_modes[raster_to_blkidx(i + 12)] : 2;
     }
     S.left_modes[i] = lm;
     S.top_modes[i] = tm;
@@ -325,9 +324,9 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
       const int el = i4_neighbour_lane(S.t4, blk, mbav, lane, &av);
       if (lane < 13) S.e4[lane] = el;
       if (blk == 1) PROF(10);
-      const int bx = h264::kBlkX[blk], by = h264::kBlkY[blk];
-      int ma = bx > 0 ? S.modes4[h264::kRasterToBlk[(bx - 1) + 4 * by]] : S.left_modes[by];
-      int mb_ = by > 0 ? S.modes4[h264::kRasterToBlk[bx + 4 * (by - 1)]] : S.top_modes[bx];
+      const int bx = blkidx_x(blk), by = blkidx_y(blk);
+      int ma = bx > 0 ? S.modes4[raster_to_blkidx((bx - 1) + 4 * by)] : S.left_modes[by];
+      int mb_ = by > 0 ? S.modes4[raster_to_blkidx(bx + 4 * (by - 1))] : S.top_modes[bx];
       bool dcpred = (bx == 0 && !(mbav & h264::AV_LEFT)) || (by == 0 && !(mbav & h264::AV_TOP));
       int pm = dcpred ? 2 : min(ma, mb_);
       wave_sync();
@@ -350,7 +349,6 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
         pw |= static_cast<uint32_t>(pv) << (8 * x);
         v[x] = static_cast<int>(S.src[(by * 4 + gy) * 16 + bx * 4 + x]) - pv;
       }
-      if (lane < 36) S.p4[lane] = pw;
       int sblk = grp_satd4x4(v, gy);
       int key = (valid && gy == 0) ? ((sblk + lambda * (m == pm ? 1 : 4)) << 4) | m : 0x7FFFFFFF;
       key = wave_min(key);
@@ -359,8 +357,8 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
       if (blk == 1) PROF(12);
       // transform / quantise / reconstruct the chosen mode (every group computes the same block)
       int pr[4];
-      wave_sync();
-      const uint32_t prw = S.p4[mode * 4 + gy];
+      // the chosen mode's prediction row gy, from the lane that ranked it
+      const uint32_t prw = static_cast<uint32_t>(__shfl(static_cast<int>(pw), mode * 4 + gy));
 #pragma unroll
       for (int x = 0; x < 4; ++x) {
         pr[x] = static_cast<int>((prw >> (8 * x)) & 255u);
@@ -565,13 +563,13 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
       bool any = false;
 #pragma unroll
       for (int k = 0; k < 16; ++k) any |= S.c4[lane][k] != 0;
-      a.nz[o * 16 + h264::kBlkX[lane] + 4 * h264::kBlkY[lane]] = any;
+      a.nz[o * 16 + blkidx_x(lane) + 4 * blkidx_y(lane)] = any;
       h->i4_modes[lane] = S.modes4[lane];
     }
   } else {
     // ---- Intra16x16 encode: lane = blkIdx * 4 + row
     const int blk = lane >> 2;
-    const int bx4 = h264::kBlkX[blk] * 4, by4 = h264::kBlkY[blk] * 4;
+    const int bx4 = blkidx_x(blk) * 4, by4 = blkidx_y(blk) * 4;
     int pr[4], v[4];
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
@@ -579,7 +577,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
       v[x] = static_cast<int>(S.src[(by4 + gy) * 16 + bx4 + x]) - pr[x];
     }
     grp_fwd4x4(v, gb, gy);
-    if (gy == 0) S.dc16[h264::kBlkX[blk] + 4 * h264::kBlkY[blk]] = v[0];
+    if (gy == 0) S.dc16[blkidx_x(blk) + 4 * blkidx_y(blk)] = v[0];
     const int qm = qp % 6, qs = qp / 6;
     bool any = false;
     int tl[4];
@@ -611,13 +609,13 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
         S.lv16dc[r] = qp >= 36 ? (lvd[r] * ls) << (qp / 6 - 6) : (lvd[r] * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
     }
     wave_sync();
-    if (gy == 0) v[0] = S.lv16dc[h264::kBlkX[blk] + 4 * h264::kBlkY[blk]];
+    if (gy == 0) v[0] = S.lv16dc[blkidx_x(blk) + 4 * blkidx_y(blk)];
     grp_inv4x4(v, gb, gy);
     uint8_t* row = S.tile + (by4 + gy + 1) * TS + bx4 + 1;
 #pragma unroll
     for (int x = 0; x < 4; ++x) row[x] = static_cast<uint8_t>(h264::clip1(pr[x] + v[x]));
     any = sum4(static_cast<int>(any)) != 0;
-    if (gy == 0) a.nz[o * 16 + h264::kBlkX[blk] + 4 * h264::kBlkY[blk]] = any;
+    if (gy == 0) a.nz[o * 16 + blkidx_x(blk) + 4 * blkidx_y(blk)] = any;
     wave_sync();
     for (int i = lane; i < 256; i += 64) coef[h264::COEF_LUMA + i] = S.c16[i >> 4][i & 15];
   }
@@ -689,7 +687,7 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
   if (lane < 16) S.saved_y[lane] = S.tile[(lane + 1) * TS + 16];
   if (lane >= 16 && lane < 20) {
     int i = lane - 16;
-    S.saved_modes[i] = use4 ? S.modes4[h264::kRasterToBlk[3 + 4 * i]] : (use8 ? S.modes8[(i >> 1) * 2 + 1] : 2);
+    S.saved_modes[i] = use4 ? S.modes4[raster_to_blkidx(3 + 4 * i)] : (use8 ? S.modes8[(i >> 1) * 2 + 1] : 2);
   }
   if (lane == 63) {
     S.saved_x = my * g.wmb + mx;

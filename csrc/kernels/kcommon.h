@@ -344,8 +344,17 @@ constexpr int kTileStride = 24;
 // Intra4x4 neighbour vector e[0..12] of block blk (0: top-left, 1-8: above and above-right,
 // 9-12: left) from the tile: lane i < 13 returns entry i (the other lanes 0) -- one register
 // per lane instead of the 13-entry vector in every lane.  *av_out: availability (uniform).
+// luma4x4BlkIdx <-> 4x4 block column / row and raster index, by bit arithmetic (a table lookup
+// with a run-time index is a memory load on the dependency chain of every block)
+__device__ __forceinline__ int blkidx_x(int b) { return (b & 1) | ((b >> 1) & 2); }
+__device__ __forceinline__ int blkidx_y(int b) { return ((b >> 1) & 1) | ((b >> 2) & 2); }
+__device__ __forceinline__ int raster_to_blkidx(int r) {
+  const int x = r & 3, y = r >> 2;
+  return (x & 1) | ((y & 1) << 1) | ((x & 2) << 1) | ((y & 2) << 2);
+}
+
 __device__ __forceinline__ int i4_neighbour_lane(const uint8_t* t, int blk, int mbav, int lane, int* av_out) {
-  int bx = h264::kBlkX[blk], by = h264::kBlkY[blk];
+  int bx = blkidx_x(blk), by = blkidx_y(blk);
   bool left = bx > 0 || (mbav & h264::AV_LEFT), top = by > 0 || (mbav & h264::AV_TOP);
   int av = 0;
   if (left) av |= h264::AV_LEFT;
