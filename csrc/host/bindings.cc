@@ -69,6 +69,9 @@ EncoderConfig cfg_from(const py::dict& d) {
   c.level_idc = dget<int>(d, "level_idc", 0);
   c.bit_depth = dget<int>(d, "bit_depth", 8);
   if (c.bit_depth < 8 || c.bit_depth > 14) throw std::runtime_error("bit_depth in 8..14");
+  c.bit_depth_chroma = dget<int>(d, "bit_depth_chroma", 0);
+  if (c.bit_depth_chroma != 0 && (c.bit_depth_chroma < 8 || c.bit_depth_chroma > 14))
+    throw std::runtime_error("bit_depth_chroma in 8..14");
   c.cqm = dget<int>(d, "cqm", 0);
   c.cqm_coded = dget<int>(d, "cqm_coded", 0xFF);
   if (c.cqm < 0 || c.cqm > 3) throw std::runtime_error("cqm in 0..3");

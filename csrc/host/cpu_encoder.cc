@@ -25,6 +25,7 @@ SPS make_sps(const EncoderConfig& cfg) {
     s.profile_idc = 110;  // High 10 (A.2.5; bit depths up to 10 -- deeper ones are written as such)
     s.constraint_flags = 0;
     s.bit_depth_luma = s.bit_depth_chroma = cfg.bit_depth;
+    if (cfg.bit_depth_chroma > 0) s.bit_depth_chroma = cfg.bit_depth_chroma;
   } else if (cfg.t8x8) {
     s.profile_idc = 100;  // High
     s.constraint_flags = 0;

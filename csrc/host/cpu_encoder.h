@@ -36,6 +36,7 @@ struct EncoderConfig {
   // sample bit depth of the written stream: 9..14 = High 10 SPS (the CPU encoder itself is 8-bit;
   // the record writer takes deeper I_PCM samples and QPs down to -QpBdOffsetY)
   int bit_depth = 8;
+  int bit_depth_chroma = 0;  // 0: = bit_depth (else written as BitDepthC; decoder-rejection tests)
   int bframes = 0;
   int pyramid = 0;          // x264 --b-pyramid normal: some B pictures are references (reorder depth 2)
   int refs = 1;

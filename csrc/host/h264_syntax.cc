@@ -290,13 +290,17 @@ SPS parse_sps(BitReader& br) {
   // 4:2:0 at 8 bits (Baseline .. High) or 9..14 bits (High 10 and the 4:2:0 intra / predictive profiles)
   if (s.chroma_format_idc != 1) throw std::runtime_error("only 4:2:0 supported");
   if (s.bit_depth_luma > 14 || s.bit_depth_chroma > 14) throw std::runtime_error("bit depth above 14");
+  // one sample depth for all planes: the picture records (DecodedPicture, the int16 batch planes) carry one
+  // depth, so a stream with BitDepthC != BitDepthY is refused here rather than mis-scaled downstream
+  if (s.bit_depth_luma != s.bit_depth_chroma) throw std::runtime_error("luma and chroma bit depths differ");
   s.log2_max_frame_num = br.get_ue_max(12, "log2_max_frame_num_minus4") + 4;
   s.poc_type = br.get_ue_max(2, "pic_order_cnt_type");
   if (s.poc_type == 0) {
     s.log2_max_poc_lsb = br.get_ue_max(12, "log2_max_pic_order_cnt_lsb_minus4") + 4;
   } else if (s.poc_type == 1) {
     s.delta_pic_order_always_zero = br.get_bit();
-    // offsets are bounded to +-2^31-1 by the spec; keep them in 2^24 so the POC sums cannot overflow
+    // deliberate restriction: the spec bounds these offsets to +-(2^31-1); this decoder accepts +-2^24
+    // so the 32-bit expected-POC sums (8.2.1.2) cannot overflow, and refuses anything larger
     s.offset_for_non_ref_pic = br.get_se_range(-(1 << 24), 1 << 24, "offset_for_non_ref_pic");
     s.offset_for_top_to_bottom = br.get_se_range(-(1 << 24), 1 << 24, "offset_for_top_to_bottom_field");
     const int n = br.get_ue_max(255, "num_ref_frames_in_pic_order_cnt_cycle");
@@ -304,8 +308,9 @@ SPS parse_sps(BitReader& br) {
   }
   s.max_num_ref_frames = br.get_ue_max(16, "max_num_ref_frames");
   s.gaps_allowed = br.get_bit();
-  s.width_mbs = br.get_ue_max(1023, "pic_width_in_mbs_minus1") + 1;
-  s.height_mbs = br.get_ue_max(1023, "pic_height_in_map_units_minus1") + 1;
+  // level 6.2 (MaxFS 139264 MBs, A.3.1 f/g): each side is at most sqrt(8 * MaxFS) = 1055 MBs
+  s.width_mbs = br.get_ue_max(1054, "pic_width_in_mbs_minus1") + 1;
+  s.height_mbs = br.get_ue_max(1054, "pic_height_in_map_units_minus1") + 1;
   s.frame_mbs_only = br.get_bit();
   if (!s.frame_mbs_only) throw std::runtime_error("interlaced streams not supported");
   s.direct_8x8_inference = br.get_bit();

@@ -85,7 +85,7 @@ void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t* src_y, con
                               int chroma_qp_offset, void* hdr, int16_t* coef, uint8_t* nz,
                               const uint8_t* intra_flag, const int* intra_count, int* err, int use_i4x4,
                               const int8_t* aq, void* stream, int use_i8x8, const void* route, int nbuf,
-                              int slice_rows, int trellis, float trellis_lambda);
+                              int slice_rows, int trellis, float trellis_lambda, int* gprog, long long gprog_ints);
 void mivc_launch_deblock(int B, int wmb, int hmb, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const void* hdr,
                          const uint8_t* nz, int chroma_qp_offset, int alpha_off, int beta_off, int* err,
                          void* stream, const void* route, int nbuf);
@@ -418,17 +418,17 @@ PYBIND11_MODULE(_hip, m) {
                            uintptr_t ru, uintptr_t rv, uintptr_t qp, int cqo, uintptr_t hdr, uintptr_t coef,
                            uintptr_t nz, uintptr_t intra_flag, uintptr_t intra_count, uintptr_t err, int use_i4x4,
                            uintptr_t stream, uintptr_t aq, int use_i8x8, uintptr_t route, int nbuf, int slice_rows,
-                           int trellis, float trellis_lambda) {
+                           int trellis, float trellis_lambda, uintptr_t gprog, long long gprog_ints) {
     mivc_launch_encode_intra(B, wmb, hmb, P<uint8_t>(sy), P<uint8_t>(su), P<uint8_t>(sv), P<uint8_t>(ry),
                              P<uint8_t>(ru), P<uint8_t>(rv), P<int>(qp), cqo, P<void>(hdr), P<int16_t>(coef),
                              P<uint8_t>(nz), P<uint8_t>(intra_flag), P<int>(intra_count), P<int>(err), use_i4x4,
                              P<int8_t>(aq), S(stream), use_i8x8, P<void>(route), nbuf, slice_rows, trellis,
-                             trellis_lambda);
+                             trellis_lambda, P<int>(gprog), gprog_ints);
   }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("sy"), py::arg("su"), py::arg("sv"), py::arg("ry"),
      py::arg("ru"), py::arg("rv"), py::arg("qp"), py::arg("cqo"), py::arg("hdr"), py::arg("coef"), py::arg("nz"),
      py::arg("intra_flag"), py::arg("intra_count"), py::arg("err"), py::arg("use_i4x4"), py::arg("stream"),
      py::arg("aq") = 0, py::arg("use_i8x8") = 0, py::arg("route") = 0, py::arg("nbuf") = 0, py::arg("slice_rows") = 0,
-     py::arg("trellis") = 0, py::arg("trellis_lambda") = 1.0f);
+     py::arg("trellis") = 0, py::arg("trellis_lambda") = 1.0f, py::arg("gprog") = 0, py::arg("gprog_ints") = 0);
   m.def("deblock", [](int B, int wmb, int hmb, uintptr_t ry, uintptr_t ru, uintptr_t rv, uintptr_t hdr, uintptr_t nz,
                       int cqo, int alpha_off, int beta_off, uintptr_t err, uintptr_t stream, uintptr_t route, int nbuf) {
     mivc_launch_deblock(B, wmb, hmb, P<uint8_t>(ry), P<uint8_t>(ru), P<uint8_t>(rv), P<void>(hdr), P<uint8_t>(nz),

@@ -11,6 +11,7 @@
 #include "h264_trellis.h"
 #include "../common/h264_i4_taps.h"
 
+#include <atomic>
 #include <cstdlib>
 
 namespace mivc {
@@ -794,12 +795,40 @@ __global__ __launch_bounds__(64 * NW) void encode_intra_wavefront(IntraArgs a) {
 
 using namespace mivc::gpu;
 
+// Workgroups of encode_intra_wavefront<nw> that can be resident on the current device at once
+// (occupancy x CU count), per device: the multi-workgroup wavefront spins on progress across
+// workgroups, so every one of them must be resident (a partitioned or smaller GPU, or CUs held
+// by side-stream kernels, would otherwise leave a waiter spinning on an unscheduled producer).
+static int intra_resident_capacity(int nw) {
+  constexpr int kDev = 64;
+  static std::atomic<int> cap[kDev][3];  // 0 = not measured yet
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kDev) return 0;
+  const int slot = nw == 16 ? 2 : (nw == 12 ? 1 : 0);
+  int c = cap[dev][slot].load(std::memory_order_relaxed);
+  if (c > 0) return c;
+  int per_cu = 0, cus = 0;
+  hipError_t e;
+  if (nw == 16) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, encode_intra_wavefront<16>, 64 * 16, 0);
+  else if (nw == 12) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, encode_intra_wavefront<12>, 64 * 12, 0);
+  else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, encode_intra_wavefront<8>, 64 * 8, 0);
+  if (e != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  c = per_cu * cus;
+  cap[dev][slot].store(c > 0 ? c : 0, std::memory_order_relaxed);
+  return c;
+}
+
+// gprog / gprog_ints: the caller's device buffer for the cross-workgroup row progress
+// (per encoder, on the launch stream: no buffer is shared between streams or devices);
+// K > 1 needs units * kMaxRows ints of it, else the launch runs one workgroup per slice
 extern "C" void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* src_u,
                                          const uint8_t* src_v, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v,
                                          const int* qp, int chroma_qp_offset, void* hdr, int16_t* coef, uint8_t* nz,
                                          const uint8_t* intra_flag, const int* intra_count, int* err, int use_i4x4,
                                          const int8_t* aq, void* stream, int use_i8x8, const void* route, int nbuf,
-                                         int slice_rows, int trellis, float trellis_lambda) {
+                                         int slice_rows, int trellis, float trellis_lambda, int* gprog,
+                                         long long gprog_ints) {
   IntraArgs a;
   a.trellis = trellis;
   a.trellis_lambda = trellis_lambda;
@@ -824,10 +853,15 @@ extern "C" void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t*
   a.err = err;
   a.use_i4x4 = use_i4x4;
   a.use_i8x8 = use_i8x8;
+  static const int nw = [] {
+    const char* e = std::getenv("MIVC_INTRA_WAVES");
+    const int v = e ? std::atoi(e) : 12;
+    return (v == 8 || v == 16) ? v : 12;
+  }();
   const int per = slice_rows > 0 ? (hmb + slice_rows - 1) / slice_rows : 1;
   // I pictures of a batch with fewer slice wavefronts than CUs / 4: several workgroups per
-  // slice (all of them resident: at most 256 workgroups of <= 80 KB LDS, two fit a CU), each
-  // unit's in one XCD when the unit count is a multiple of 8.  MIVC_INTRA_WG=1: one per slice.
+  // slice, each unit's in one XCD when the unit count is a multiple of 8, all of them resident
+  // (units * K <= the device's resident capacity).  MIVC_INTRA_WG=1: one per slice.
   static const int wg_cap = [] {
     const char* e = std::getenv("MIVC_INTRA_WG");
     const int v = e ? std::atoi(e) : 4;
@@ -835,35 +869,17 @@ extern "C" void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t*
   }();
   const int units = B * per;
   int K = 1;
-  if (!intra_flag && units % 8 == 0)
-    while (K * 2 <= wg_cap && units * K * 2 <= 256) K *= 2;
-  a.wg_per_slice = K;
-  a.gprog = nullptr;
-  if (K > 1) {
-    static int* gprog = nullptr;
-    static size_t gcap = 0;
-    const size_t need = static_cast<size_t>(units) * kMaxRows * sizeof(int);
-    if (need > gcap) {
-      if (gprog) (void)hipFree(gprog);
-      if (hipMalloc(&gprog, need) != hipSuccess) {
-        gprog = nullptr;
-        gcap = 0;
-      } else {
-        gcap = need;
-      }
-    }
-    if (gprog) {
-      a.gprog = gprog;
-      (void)hipMemsetAsync(gprog, 0, need, static_cast<hipStream_t>(stream));
-    } else {
-      a.wg_per_slice = K = 1;
-    }
+  if (!intra_flag && units % 8 == 0 && gprog != nullptr) {
+    const int resident = std::min(256, intra_resident_capacity(nw));
+    while (K * 2 <= wg_cap && units * K * 2 <= resident &&
+           static_cast<long long>(units) * kMaxRows <= gprog_ints)
+      K *= 2;
   }
-  static const int nw = [] {
-    const char* e = std::getenv("MIVC_INTRA_WAVES");
-    const int v = e ? std::atoi(e) : 12;
-    return (v == 8 || v == 16) ? v : 12;
-  }();
+  a.wg_per_slice = K;
+  a.gprog = K > 1 ? gprog : nullptr;
+  if (K > 1)
+    (void)hipMemsetAsync(gprog, 0, static_cast<size_t>(units) * kMaxRows * sizeof(int),
+                         static_cast<hipStream_t>(stream));
   if (nw == 16)
     hipLaunchKernelGGL(encode_intra_wavefront<16>, dim3(B * per * K), dim3(64 * 16), 0, static_cast<hipStream_t>(stream), a);
   else if (nw == 12)

@@ -267,10 +267,15 @@ class GpuBackend:
             for k, v in dec.stats.items():
                 self.decode_stats[k] = self.decode_stats.get(k, 0) + v
             for i, d in zip(idxs, got):
-                if d.y.dtype != torch.uint8 and not keep_high_bit:  # Main 10 / High 10 input, 8-bit output
+                if d.y.dtype != torch.uint8:
                     from ..models.h264_decode_gpu import DecodedSegment
                     bd = d.bit_depth if d.bit_depth > 8 else 10  # (the HEVC decoder's segments: Main 10)
-                    d = DecodedSegment(yuv.to_8bit(d.y, bd), yuv.to_8bit(d.u, bd), yuv.to_8bit(d.v, bd), d.fps, d.path)
+                    if not keep_high_bit:  # Main 10 / High 10 input, 8-bit output
+                        d = DecodedSegment(yuv.to_8bit(d.y, bd), yuv.to_8bit(d.u, bd), yuv.to_8bit(d.v, bd),
+                                           d.fps, d.path)
+                    elif bd != 10:  # 9/12/14-bit High 10-family input, Main 10 output: rescale to 10 bits
+                        d = DecodedSegment(yuv.rescale_bits(d.y, bd), yuv.rescale_bits(d.u, bd),
+                                           yuv.rescale_bits(d.v, bd), d.fps, d.path, bit_depth=10)
                 out[i] = d
         return out
 

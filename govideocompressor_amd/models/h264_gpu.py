@@ -807,11 +807,17 @@ class GpuH264Encoder:
             self.prev_mv.zero_()
             flag_ptr, count_ptr = 0, 0
         trial = not inter or self.p.i4x4_in_p or cut is not None
+        if getattr(self, "_intra_prog", None) is None:
+            # cross-workgroup row progress of the multi-workgroup I-picture wavefront (this
+            # encoder's own: [slice units][kMaxRows = 272] ints, zeroed by the launcher on `s`)
+            per = -(-hmb // self.slice_rows) if self.slice_rows > 0 else 1
+            self._intra_prog = torch.zeros(B * per * 272, dtype=torch.int32, device=self.dev)
         with stt("intra"):
             self.hip.encode_intra(B, wmb, hmb, sy, su, sv, py, pu, pv, P(self.qp), cqo, P(hdr), P(coef), P(self.nz),
                                   flag_ptr, count_ptr, P(self.err), int(self.p.i4x4 and trial), s, aq,
                                   int(self.p.i8x8 and self.p.eff_t8x8() and trial), rt, NB, self.slice_rows,
-                                  trellis=self.p.eff_intra_trellis(), trellis_lambda=float(self.p.trellis_lambda))
+                                  trellis=self.p.eff_intra_trellis(), trellis_lambda=float(self.p.trellis_lambda),
+                                  gprog=P(self._intra_prog), gprog_ints=self._intra_prog.numel())
         if aq:
             # MBs without mb_qp_delta take QP_pred (clause 7.4.5): their records must say so
             # before deblocking reads every MB's QP

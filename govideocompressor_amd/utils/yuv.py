@@ -77,6 +77,28 @@ def to_8bit(x, bit_depth: int = 10):
     return np.clip((a + (1 << (s - 1))) >> s, 0, 255).astype(np.uint8)
 
 
+def rescale_bits(x, from_bd: int, to_bd: int = 10):
+    """Samples of ``from_bd`` bits -> ``to_bd`` bits (both > 8, int16 planes): a left shift when
+    widening, a rounded right shift (clipped) when narrowing -- e.g. 12-bit High 10-family input
+    feeding the Main 10 encoder.  Works on numpy arrays and torch tensors."""
+    s = int(from_bd) - int(to_bd)
+    if s == 0:
+        return x
+    hi = (1 << int(to_bd)) - 1
+    try:
+        import torch
+        if isinstance(x, torch.Tensor):
+            if s < 0:
+                return (x.to(torch.int32) << -s).to(torch.int16)
+            return ((x.to(torch.int32) + (1 << (s - 1))) >> s).clamp_(0, hi).to(torch.int16)
+    except ImportError:  # pragma: no cover
+        pass
+    a = np.asarray(x).astype(np.int32)
+    if s < 0:
+        return (a << -s).astype(np.int16)
+    return np.clip((a + (1 << (s - 1))) >> s, 0, hi).astype(np.int16)
+
+
 def frame_bytes(width: int, height: int, bit_depth: int = 8) -> int:
     return (width * height + 2 * (width // 2) * (height // 2)) * (1 if bit_depth == 8 else 2)
 

@@ -158,3 +158,23 @@ def test_gpu_decode_high10_segments(host, dec):
     outs = tc.run([s10, s10], 30.0)
     tc.close()
     assert [len(host.decode(o)) for o in outs] == [4, 4]
+
+
+def test_gpu_decode_high12_to_main10(host):
+    """A 12-bit High 10-family segment feeding a Main 10 output (keep_high_bit) is rescaled to
+    10 bits with rounding (DecodedSegment.bit_depth 10) instead of reaching the encoder unscaled;
+    a 10-bit segment passes through untouched."""
+    import torch
+    from govideocompressor_amd.backends.gpu import GpuBackend
+    s12 = random_stream(host, 96, 64, 3, seed=81, bit_depth=12, intra_in_p=0.3, cabac=True)
+    s10 = random_stream(host, 96, 64, 3, seed=82, bit_depth=10, intra_in_p=0.3, cabac=True)
+    b = GpuBackend()
+    out = b.decode_streams([s12, s10], 30.0, keep_high_bit=True)
+    assert out[0].bit_depth == 10 and out[0].y.dtype == torch.int16
+    for t, p in enumerate(host.decode(s12)):
+        ry, ru, rv = _planes(p)
+        for got, ref in ((out[0].y[t], ry), (out[0].u[t], ru), (out[0].v[t], rv)):
+            want = np.clip((ref.astype(np.int32) + 2) >> 2, 0, 1023)
+            assert np.array_equal(got.cpu().numpy().astype(np.int32), want)
+    for t, p in enumerate(host.decode(s10)):
+        assert np.array_equal(out[1].y[t].cpu().numpy(), _planes(p)[0].astype(np.int16))

@@ -370,3 +370,17 @@ def test_gpu_hevc_encode_async_same_bytes():
     torch.cuda.synchronize()
     assert got == ref
     enc.close()
+
+
+def test_gpu_hevc_ctb32_config4_shape(host):
+    """-preset ultrafast's geometry (32x32 CTBs, ctu64=False) at config-4 shape with B pictures:
+    16 slots x 8 pictures of 1080p in one batch (the round-4 scratch log had hevc_intra_recon
+    fault here when its per-CTB call was not inlined: a 544 B call frame on a 147 KB-LDS
+    workgroup; the call is now inlined and each component is its own workgroup).  Three slots
+    are compared bit-exactly with the CPU decoder, every slot must decode."""
+    res, rec = _encode(1920, 1080, 8, 16, crf=26, ctu64=False, bframes=1)
+    assert len(res) == 16
+    pick = [0, 7, 15]
+    _compare(host, [res[b] for b in pick], [tuple(plane[pick] for plane in t) for t in rec])
+    for r in res:
+        assert r.frames == 8 and len(r.bitstream) > 0

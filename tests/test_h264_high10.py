@@ -236,3 +236,24 @@ def test_high10_random_streams_decode(host, cabac):
         assert all(np.array_equal(a["i420"], b["i420"]) for a, b in zip(pics, again))
         seg = host.parse([s])[0]
         assert not np.all(seg["meta"][:, 10] == 1)  # gpu_ok column (models/h264_decode_gpu.py _META)
+
+
+def test_mixed_luma_chroma_depth_refused(host):
+    """BitDepthC != BitDepthY is refused at the SPS (the picture records carry one depth; the
+    old path emitted an empty 8-bit plane set for bdY 8 / bdC 10 and mis-scaled chroma)."""
+    from govideocompressor_amd.utils.h264_synth import random_stream
+    ok = random_stream(host, 32, 32, 1, seed=3, bit_depth=10)
+    ps_ok = host.parameter_sets(dict(width=32, height=32, bit_depth=10))
+    assert ok.startswith(ps_ok)
+    bad = host.parameter_sets(dict(width=32, height=32, bit_depth=10, bit_depth_chroma=12)) + ok[len(ps_ok):]
+    with pytest.raises(Exception, match="bit depths differ"):
+        host.decode(bad)
+    assert len(host.decode(ok)) == 1
+
+
+def test_rescale_bits_model():
+    from govideocompressor_amd.utils import yuv
+    a = np.array([0, 1, 2, 3, 4095, 2048], np.int16)
+    assert yuv.rescale_bits(a, 12, 10).tolist() == [0, 0, 1, 1, 1023, 512]
+    assert yuv.rescale_bits(np.array([0, 511, 300], np.int16), 9, 10).tolist() == [0, 1022, 600]
+    assert yuv.rescale_bits(a, 10, 10) is a

@@ -26,7 +26,7 @@ cur = enc.rec[0]
 s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 lib.mivc_launch_encode_intra(B, enc.wmb, enc.hmb, P(enc.src[0]), P(enc.src[1]), P(enc.src[2]), P(cur[0]), P(cur[1]),
                              P(cur[2]), P(enc.qp), 0, P(enc.hdr[0]), P(enc.coef[0]), P(enc.nz), None, None,
-                             P(enc.err), 1, None, s, 1, None, 0, 0, 0, ctypes.c_float(1.0))
+                             P(enc.err), 1, None, s, 1, None, 0, 0, 0, ctypes.c_float(1.0), None, ctypes.c_longlong(0))
 torch.cuda.synchronize()
 buf = (ctypes.c_ulonglong * 256)()
 lib.mivc_intra_prof_read(buf)
