@@ -200,7 +200,7 @@ struct alignas(8) CuInfo {
   int16_t mv[2];  // quarter-sample L0 motion vector (inter)
   int16_t mv1[2]; // quarter-sample L1 motion vector (inter, B slices)
   uint8_t dir;    // CuDir of an inter CU (0 is read as DIR_L0: P-slice records)
-  uint8_t pad[3];
+  uint8_t pad[3]; // pad[0] / pad[1]: refIdx L0 / L1 of an inter CU (x265 --ref); pad[2] unused
 };
 static_assert(sizeof(CuInfo) == 16, "CuInfo is 16 bytes");
 constexpr int kCuInfoBytes = 16;

@@ -354,6 +354,8 @@ hevc::HevcConfig hevc_cfg_from(const py::dict& d) {
   c.pyramid = dget<int>(d, "pyramid", 0);
   c.ctu64 = dget<int>(d, "ctu64", 0);
   c.weightp = dget<int>(d, "weightp", 0);
+  c.refs = dget<int>(d, "refs", 1);
+  if (c.refs < 1 || c.refs > hevc::kMaxRefs) throw std::runtime_error("HEVC: refs in 1..4");
   if (c.tu_inter_depth < 0 || c.tu_inter_depth > 1) throw std::runtime_error("HEVC: tu_inter_depth in 0..1");
   if (c.threads < 1 || c.threads > 256) throw std::runtime_error("HEVC: threads in 1..256");
   if (c.width <= 0 || c.height <= 0 || (c.width & 1) || (c.height & 1)) throw std::runtime_error("HEVC: bad size");
@@ -540,6 +542,17 @@ hevc::HevcFrameParams hevc_frame_from(const py::dict& fp, std::vector<py::array>
   f.nal_ref = dget<int>(fp, "nal_ref", 1);
   f.ref_poc[0] = dget<int>(fp, "ref_poc0", -1);
   f.ref_poc[1] = dget<int>(fp, "ref_poc1", -1);
+  // several active pictures per list: "refs0" / "refs1" = RefPicListX POCs (entry 0 = ref_pocX)
+  for (int l = 0; l < 2; ++l) {
+    const char* key = l ? "refs1" : "refs0";
+    if (!fp.contains(key) || fp[key].is_none()) continue;
+    const py::list r = fp[key].cast<py::list>();
+    if (r.size() < 1 || r.size() > static_cast<size_t>(hevc::kMaxRefs)) throw std::runtime_error("refsX: 1..4 entries");
+    f.num_ref[l] = static_cast<int>(r.size());
+    for (size_t i = 0; i < r.size(); ++i) f.list_poc[l][i] = r[i].cast<int>();
+    if (f.ref_poc[l] < 0) f.ref_poc[l] = f.list_poc[l][0];
+    if (f.list_poc[l][0] != f.ref_poc[l]) throw std::runtime_error("refsX[0] != ref_pocX");
+  }
   if (fp.contains("rps")) {  // [(poc, used), ...]
     const py::list l = fp["rps"].cast<py::list>();
     if (l.size() > 8) throw std::runtime_error("rps: at most 8 entries");
@@ -566,6 +579,14 @@ hevc::HevcFrameParams hevc_frame_from(const py::dict& fp, std::vector<py::array>
     f.col.poc = dget<int>(fp, "col_poc", 0);
     f.col.ref_poc[0] = dget<int>(fp, "col_ref_poc0", 0);
     f.col.ref_poc[1] = dget<int>(fp, "col_ref_poc1", 0);
+    for (int l = 0; l < 2; ++l) {  // "col_refs0" / "col_refs1": the col picture's list POCs
+      for (int i = 0; i < hevc::kMaxRefs; ++i) f.col.list_poc[l][i] = f.col.ref_poc[l];
+      const char* key = l ? "col_refs1" : "col_refs0";
+      if (!fp.contains(key) || fp[key].is_none()) continue;
+      const py::list r = fp[key].cast<py::list>();
+      if (r.size() > static_cast<size_t>(hevc::kMaxRefs)) throw std::runtime_error("col_refsX: at most 4 entries");
+      for (size_t i = 0; i < r.size(); ++i) f.col.list_poc[l][i] = r[i].cast<int>();
+    }
     if (fp.contains("col_cu") && !fp["col_cu"].is_none()) {
       auto a = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>::ensure(fp["col_cu"]);
       if (!a || static_cast<size_t>(a.size()) != cu_bytes) throw std::runtime_error("col_cu: wrong size");

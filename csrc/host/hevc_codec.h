@@ -45,6 +45,9 @@ struct HevcConfig {
   // weighted_pred_flag (x265 --weightp): P slices carry pred_weight_table() with log2
   // denominators 6 (luma and chroma) and the picture's FrameParams::wp weights
   int weightp = 0;
+  // x265 --ref: the most active list-0 pictures of a P slice (HevcFrameParams::num_ref); sizes
+  // the DPB (sps_max_dec_pic_buffering)
+  int refs = 1;
   int ctb_log2() const { return ctu64 ? 6 : kCtbLog2; }
   int wctu() const { return (coded_width() + (1 << ctb_log2()) - 1) >> ctb_log2(); }
   int hctu() const { return (coded_height() + (1 << ctb_log2()) - 1) >> ctb_log2(); }
@@ -56,11 +59,16 @@ struct HevcConfig {
 
 // The collocated picture of temporal motion vector prediction (8.5.3.2.8): its decision
 // records (same layout as the current picture's) and the POCs its motion points to.
+constexpr int kMaxRefs = 4;   // active pictures per reference list this encoder codes
+
 struct HevcColPic {
   int set = 0;                 // must be 1 in P / B slices when HevcConfig::tmvp is on
   const CuInfo* cu = nullptr;  // nullptr: an intra picture (no temporal candidates)
   int poc = 0;
   int ref_poc[2] = {0, 0};     // POC of the col picture's RefPicList0[0] / RefPicList1[0]
+  // POCs of the col picture's RefPicListX[i] (its CuInfo records carry refIdx in pad[0] / pad[1]);
+  // entries past the list's end repeat ref_poc[X]
+  int list_poc[2][kMaxRefs] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
 };
 
 struct HevcFrameParams {
@@ -72,6 +80,11 @@ struct HevcFrameParams {
   // one reference picture per list: RefPicList0[0] / RefPicList1[0] POCs (-1: P slices use
   // poc - 1); the slice's short-term RPS holds exactly these pictures
   int ref_poc[2] = {-1, -1};
+  // several active pictures per list (x265 --ref): num_ref[X] entries of RefPicListX, whose POCs
+  // are list_poc[X][0 ..] (list_poc[X][0] = ref_poc[X]); the lists must be the default
+  // construction (8.3.4) from the RPS's used pictures.  CuInfo pad[0] / pad[1] = refIdx L0 / L1
+  int num_ref[2] = {1, 1};
+  int list_poc[2][kMaxRefs] = {{-1, -1, -1, -1}, {-1, -1, -1, -1}};
   // explicit short-term RPS (n_rps >= 0): every picture the DPB keeps, with used_by_curr;
   // RefPicList0[0] / RefPicList1[0] must be the closest used picture before / after
   int n_rps = -1;

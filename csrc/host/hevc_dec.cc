@@ -2478,6 +2478,8 @@ struct HevcStreamDecoder::Impl {
           c.mv1[0] = (m.pred & 2) ? m.mv[1][0] : 0;
           c.mv1[1] = (m.pred & 2) ? m.mv[1][1] : 0;
           c.dir = m.pred;
+          c.pad[0] = static_cast<uint8_t>((m.pred & 1) ? m.ref[0] : 0);  // refIdx L0 / L1
+          c.pad[1] = static_cast<uint8_t>((m.pred & 2) ? m.ref[1] : 0);
         }
       }
   }

@@ -64,7 +64,11 @@ int auto_level_idc(const HevcConfig& c) {
 // DPB size / reordering of the GOP structures this encoder writes (models/gop.py): P only
 // (1 reference + current), B pictures between two anchors (2 + current, 1 reordered),
 // a pyramid with a reference B (3 + current, 2 reordered)
-int dpb_minus1(const HevcConfig& c) { return c.bframes <= 0 ? 1 : (c.pyramid && c.bframes > 1 ? 3 : 2); }
+// (x265 --ref R: R list-0 pictures + the current one, one more with a reference B)
+int dpb_minus1(const HevcConfig& c) {
+  const int base = c.bframes <= 0 ? 1 : (c.pyramid && c.bframes > 1 ? 3 : 2);
+  return std::max(base, c.refs + (c.pyramid && c.bframes > 1 ? 1 : 0));
+}
 int num_reorder(const HevcConfig& c) { return c.bframes <= 0 ? 0 : (c.pyramid && c.bframes > 1 ? 2 : 1); }
 
 void profile_tier_level(BitWriter& bw, const HevcConfig& c) {
@@ -205,12 +209,14 @@ struct Mv {
   int x, y;
   bool operator==(const Mv& o) const { return x == o.x && y == o.y; }
 };
-// motion of a PU: direction (bit 0 list 0, bit 1 list 1; refIdx 0 in each used list) + vectors
+// motion of a PU: direction (bit 0 list 0, bit 1 list 1), refIdx and vector per used list
 struct Motion {
   uint8_t dir = 0;
+  int8_t r[2] = {0, 0};
   Mv m[2] = {{0, 0}, {0, 0}};
   bool operator==(const Motion& o) const {
-    return dir == o.dir && (!(dir & 1) || m[0] == o.m[0]) && (!(dir & 2) || m[1] == o.m[1]);
+    return dir == o.dir && (!(dir & 1) || (m[0] == o.m[0] && r[0] == o.r[0])) &&
+           (!(dir & 2) || (m[1] == o.m[1] && r[1] == o.r[1]));
   }
 };
 
@@ -276,7 +282,9 @@ struct Writer {
     bslice = fp.slice_type == 0;
     tmvp = inter_slice && c.tmvp;
     col_l1 = bslice;
-    no_backward = ref_poc(0) <= fp.poc && (!bslice || ref_poc(1) <= fp.poc);
+    no_backward = true;  // NoBackwardPredFlag: no picture of either list follows the current one
+    for (int l = 0; l < (bslice ? 2 : 1); ++l)
+      for (int i = 0; i < nref(l); ++i) no_backward = no_backward && list_poc(l, i) <= fp.poc;
     L = c.ctb_log2();
     init_contexts(ctx, bslice ? 2 : (inter_slice ? 1 : 0), fp.qp);
     qp_prev = fp.qp;
@@ -694,12 +702,13 @@ struct Writer {
   bool any_nonzero(int cidx, int x, int y, int n) const { return block_mask(cidx, x, y, n) != 0; }
 
   // ---------------------------------------------------------------- inter prediction helpers
-  // One reference picture per list (refIdx 0): a PU's motion is its direction (bit 0 list 0,
-  // bit 1 list 1) and one vector per used list.  RefPicList0[0] / RefPicList1[0] are
-  // different pictures in every B slice this writer codes.
+  // A PU's motion is its direction (bit 0 list 0, bit 1 list 1) and a refIdx + vector per used
+  // list; RefPicListX holds num_ref[X] pictures (POC list_poc(X, i)).
   bool inter_avail(int x, int y) const { return avail(x, y) && pred[g(x, y)] == CU_INTER; }
   const Motion& mot_at(int x, int y) const { return mot[g(x, y)]; }
   int ref_poc(int l) const { return l == 0 ? (fp.ref_poc[0] >= 0 ? fp.ref_poc[0] : fp.poc - 1) : fp.ref_poc[1]; }
+  int nref(int l) const { return std::max(1, fp.num_ref[l]); }
+  int list_poc(int l, int i) const { return i == 0 ? ref_poc(l) : fp.list_poc[l][i]; }
 
   static Mv scale_mv(Mv v, int td0, int tb0) {  // 8.5.3.2.8 (8-209 .. 8-213)
     const int td = std::clamp(td0, -128, 127), tb = std::clamp(tb0, -128, 127);
@@ -712,8 +721,8 @@ struct Writer {
     return Mv{sc(v.x), sc(v.y)};
   }
 
-  // 8.5.3.2.8 / 8.5.3.2.9 temporal vector of list X (refIdx 0) for the PU (x, y, n x n)
-  bool col_at(int xc, int yc, int X, Mv* out) const {
+  // 8.5.3.2.8 / 8.5.3.2.9 temporal vector of list X (target refIdx ri) for the PU (x, y, n x n)
+  bool col_at(int xc, int yc, int X, int ri, Mv* out) const {
     if (!fp.col.cu || xc >= W || yc >= H) return false;
     const int ci = (yc >> kCtbLog2) * wctb + (xc >> kCtbLog2);
     const CuInfo& cc = fp.col.cu[static_cast<size_t>(ci) * kCusPerCtb + zorder8((xc & (kCtb - 1)) >> 3, (yc & (kCtb - 1)) >> 3)];
@@ -724,18 +733,20 @@ struct Writer {
     else if (dir == DIR_L0) list = 0;
     else list = no_backward ? X : (col_l1 ? 0 : 1);  // N = collocated_from_l0_flag
     Mv v = list == 0 ? Mv{cc.mv[0], cc.mv[1]} : Mv{cc.mv1[0], cc.mv1[1]};
-    const int col_diff = fp.col.poc - fp.col.ref_poc[list];
-    const int cur_diff = fp.poc - ref_poc(X);
+    const int cr = cc.pad[list];
+    if (cr >= kMaxRefs) throw std::runtime_error("HEVC: collocated refIdx out of range");
+    const int col_diff = fp.col.poc - (cr == 0 ? fp.col.ref_poc[list] : fp.col.list_poc[list][cr]);
+    const int cur_diff = fp.poc - list_poc(X, ri);
     if (col_diff != cur_diff && col_diff != 0) v = scale_mv(v, col_diff, cur_diff);
     *out = v;
     return true;
   }
-  bool temporal(int x, int y, int n, int X, Mv* out) const {
+  bool temporal(int x, int y, int n, int X, int ri, Mv* out) const {
     if (!tmvp) return false;
     const int xbr = x + n, ybr = y + n;
-    if ((y >> L) == (ybr >> L) && ybr < H && xbr < W && col_at((xbr >> 4) << 4, (ybr >> 4) << 4, X, out))
+    if ((y >> L) == (ybr >> L) && ybr < H && xbr < W && col_at((xbr >> 4) << 4, (ybr >> 4) << 4, X, ri, out))
       return true;
-    return col_at(((x + (n >> 1)) >> 4) << 4, ((y + (n >> 1)) >> 4) << 4, X, out);
+    return col_at(((x + (n >> 1)) >> 4) << 4, ((y + (n >> 1)) >> 4) << 4, X, ri, out);
   }
 
   // 8.5.3.2.2-8.5.3.2.5 merge candidates of a 2Nx2N PU (MaxNumMergeCand entries)
@@ -760,8 +771,8 @@ struct Writer {
     if (b2) cand[k++] = mb2;
     if (k < c.max_merge && tmvp) {
       Motion t{};
-      if (temporal(x, y, n, 0, &t.m[0])) t.dir |= DIR_L0;
-      if (bslice && temporal(x, y, n, 1, &t.m[1])) t.dir |= DIR_L1;
+      if (temporal(x, y, n, 0, 0, &t.m[0])) t.dir |= DIR_L0;  // refIdx 0 (8.5.3.2.8 merge: refIdxLXCol 0)
+      if (bslice && temporal(x, y, n, 1, 0, &t.m[1])) t.dir |= DIR_L1;
       if (t.dir) cand[k++] = t;
     }
     const int orig = k;
@@ -770,27 +781,33 @@ struct Writer {
       static const int l1i[12] = {1, 0, 2, 0, 2, 1, 3, 0, 3, 1, 3, 2};
       for (int comb = 0; comb < orig * (orig - 1) && k < c.max_merge; ++comb) {
         const Motion &c0 = cand[l0i[comb]], &c1 = cand[l1i[comb]];
-        // (list 0 and list 1 hold different pictures: every such pair is a new candidate)
-        if ((c0.dir & DIR_L0) && (c1.dir & DIR_L1)) cand[k++] = Motion{DIR_BI, {c0.m[0], c1.m[1]}};
+        if ((c0.dir & DIR_L0) && (c1.dir & DIR_L1) &&
+            (list_poc(0, c0.r[0]) != list_poc(1, c1.r[1]) || !(c0.m[0] == c1.m[1])))
+          cand[k++] = Motion{DIR_BI, {c0.r[0], c1.r[1]}, {c0.m[0], c1.m[1]}};
       }
     }
-    while (k < c.max_merge) cand[k++] = Motion{static_cast<uint8_t>(bslice ? DIR_BI : DIR_L0), {{0, 0}, {0, 0}}};
+    // zero candidates (8.5.3.2.5): refIdx 0, 1, .. up to the active list size, then 0
+    const int nzr = bslice ? std::min(nref(0), nref(1)) : nref(0);
+    for (int zi = 0; k < c.max_merge; ++zi) {
+      const int8_t r = static_cast<int8_t>(zi < nzr ? zi : 0);
+      cand[k++] = Motion{static_cast<uint8_t>(bslice ? DIR_BI : DIR_L0), {r, r}, {{0, 0}, {0, 0}}};
+    }
     const int nm = std::min(k, c.max_merge);
     std::copy(cand, cand + nm, out);
     return nm;
   }
 
-  // 8.5.3.2.6-8.5.3.2.7 AMVP candidates of list X (refIdx 0)
-  void amvp_list(int x, int y, int n, int X, Mv* out) const {
+  // 8.5.3.2.6-8.5.3.2.7 AMVP candidates of list X, refIdx ri
+  void amvp_list(int x, int y, int n, int X, int ri, Mv* out) const {
     const int Y = 1 - X;
-    const int tgt = ref_poc(X);
+    const int tgt = list_poc(X, ri);
     auto same = [&](int xn, int yn, Mv* v) {  // a neighbour vector pointing at the target picture
       const Motion& m = mot_at(xn, yn);
-      if ((m.dir >> X) & 1 && ref_poc(X) == tgt) {
+      if ((m.dir >> X) & 1 && list_poc(X, m.r[X]) == tgt) {
         *v = m.m[X];
         return true;
       }
-      if ((m.dir >> Y) & 1 && ref_poc(Y) == tgt) {
+      if ((m.dir >> Y) & 1 && list_poc(Y, m.r[Y]) == tgt) {
         *v = m.m[Y];
         return true;
       }
@@ -800,7 +817,7 @@ struct Writer {
       const Motion& m = mot_at(xn, yn);
       for (int L : {X, Y}) {
         if (!((m.dir >> L) & 1)) continue;
-        const int td = fp.poc - ref_poc(L), tb = fp.poc - tgt;
+        const int td = fp.poc - list_poc(L, m.r[L]), tb = fp.poc - tgt;
         *v = (td != tb && td != 0) ? scale_mv(m.m[L], td, tb) : m.m[L];
         return true;
       }
@@ -833,7 +850,7 @@ struct Writer {
     if (fb && !(fa && ma == mb)) out[k++] = mb;
     if (k < 2) {
       Mv t;
-      if (temporal(x, y, n, X, &t)) out[k++] = t;
+      if (temporal(x, y, n, X, ri, &t)) out[k++] = t;
     }
     while (k < 2) out[k++] = Mv{0, 0};
   }
@@ -872,11 +889,18 @@ struct Writer {
     const bool cb_y = any_nonzero(0, x, y, n);
     const bool cb_cb = any_nonzero(1, x / 2, y / 2, n / 2), cb_cr = any_nonzero(2, x / 2, y / 2, n / 2);
     const bool intra = ci.pred == CU_INTRA || !inter_slice;
-    Motion mv{static_cast<uint8_t>(cu_dir(ci)), {{ci.mv[0], ci.mv[1]}, {ci.mv1[0], ci.mv1[1]}}};
+    Motion mv{static_cast<uint8_t>(cu_dir(ci)), {static_cast<int8_t>(ci.pad[0]), static_cast<int8_t>(ci.pad[1])},
+              {{ci.mv[0], ci.mv[1]}, {ci.mv1[0], ci.mv1[1]}}};
     if (!intra && (mv.dir & ~3 || (!bslice && mv.dir != DIR_L0)))
       throw std::runtime_error("HEVC: inter CU direction not allowed in this slice");
-    if (!(mv.dir & DIR_L0)) mv.m[0] = Mv{0, 0};
-    if (!(mv.dir & DIR_L1)) mv.m[1] = Mv{0, 0};
+    if (!intra && (((mv.dir & DIR_L0) && (mv.r[0] < 0 || mv.r[0] >= nref(0))) ||
+                   ((mv.dir & DIR_L1) && (mv.r[1] < 0 || mv.r[1] >= nref(1)))))
+      throw std::runtime_error("HEVC: inter CU refIdx outside the active list");
+    for (int X = 0; X < 2; ++X)
+      if (!((mv.dir >> X) & 1)) {
+        mv.m[X] = Mv{0, 0};
+        mv.r[X] = 0;
+      }
     if (inter_slice) {
       int skip_ctx = (avail(x - 1, y) && skip[g(x - 1, y)]) + (avail(x, y - 1) && skip[g(x, y - 1)]);
       int midx = -1;
@@ -909,8 +933,9 @@ struct Writer {
           if (bslice) write_inter_pred_idc(mv.dir, d);
           for (int X = 0; X < 2; ++X) {
             if (!((mv.dir >> X) & 1)) continue;
+            if (nref(X) > 1) write_ref_idx(mv.r[X], nref(X) - 1);
             Mv ap[2];
-            amvp_list(x, y, n, X, ap);
+            amvp_list(x, y, n, X, mv.r[X], ap);
             const Mv& v = mv.m[X];
             auto cost = [&](const Mv& p) { return std::abs(v.x - p.x) + std::abs(v.y - p.y); };
             const int idx = cost(ap[1]) < cost(ap[0]) ? 1 : 0;
@@ -1005,6 +1030,16 @@ struct Writer {
     }
     if (cb_cb) write_residual(1, x / 2, y / 2, 2, mdcs(m[0]), 1);
     if (cb_cr) write_residual(2, x / 2, y / 2, 2, mdcs(m[0]), 1);
+  }
+
+  // ref_idx_lX (9.3.3.1 TR, cMax = num_ref_idx_active - 1): two context-coded bins, then bypass
+  void write_ref_idx(int r, int cmax) {
+    for (int i = 0; i < cmax; ++i) {
+      const int b = r > i;
+      if (i < 2) e.encode(b, ctx[CTX_REF_IDX + i]);
+      else e.bypass(b);
+      if (!b) break;
+    }
   }
 
   void write_merge_idx(int idx) {
@@ -1172,9 +1207,13 @@ struct Writer {
       const CtuInfo& t = ctu[by * wctb + bx];
       const CuInfo& ci = cu[static_cast<size_t>(by * wctb + bx) * kCusPerCtb];
       if ((t.split & 1) || ci.pred != CU_INTER) return false;
-      Motion m{static_cast<uint8_t>(cu_dir(ci)), {{ci.mv[0], ci.mv[1]}, {ci.mv1[0], ci.mv1[1]}}};
-      if (!(m.dir & DIR_L0)) m.m[0] = Mv{0, 0};
-      if (!(m.dir & DIR_L1)) m.m[1] = Mv{0, 0};
+      Motion m{static_cast<uint8_t>(cu_dir(ci)), {static_cast<int8_t>(ci.pad[0]), static_cast<int8_t>(ci.pad[1])},
+               {{ci.mv[0], ci.mv[1]}, {ci.mv1[0], ci.mv1[1]}}};
+      for (int X = 0; X < 2; ++X)
+        if (!((m.dir >> X) & 1)) {
+          m.m[X] = Mv{0, 0};
+          m.r[X] = 0;
+        }
       if (q == 0) m0 = m;
       else if (!(m == m0)) return false;
       scan_ctb_nz(bx << 5, by << 5);
@@ -1245,6 +1284,22 @@ std::vector<uint8_t> hevc_write_slice(const HevcConfig& c, const HevcFrameParams
       if (e.second && l1 < 0) l1 = e.first;
     if (inter && (l0 != r0 || (bslice && l1 != fp.ref_poc[1])))
       throw std::runtime_error("HEVC: RefPicList0 must precede and RefPicList1 follow the current picture (closest used RPS entries)");
+    // several active pictures per list: each list must be the default construction (8.3.4,
+    // RefPicListTemp0 = used pictures before, closest first, then after; list 1 the other way)
+    for (int l = 0; l < (bslice ? 2 : (inter ? 1 : 0)); ++l) {
+      const int nr = fp.num_ref[l];
+      if (nr < 1 || nr > kMaxRefs) throw std::runtime_error("HEVC: num_ref outside 1..4");
+      if (nr == 1) continue;
+      std::vector<int> tmp;
+      for (auto& e : l == 0 ? neg : pos)
+        if (e.second) tmp.push_back(e.first);
+      for (auto& e : l == 0 ? pos : neg)
+        if (e.second) tmp.push_back(e.first);
+      if (tmp.empty()) throw std::runtime_error("HEVC: no used reference picture");
+      for (int i = 0; i < nr; ++i)
+        if ((i == 0 ? (l == 0 ? r0 : fp.ref_poc[1]) : fp.list_poc[l][i]) != tmp[i % tmp.size()])
+          throw std::runtime_error("HEVC: list_poc is not the default RefPicList construction of the RPS");
+    }
     if (inter && !bslice && neg.size() == 1 && pos.empty() && neg[0].first == fp.poc - 1 && neg[0].second) {
       bw.put_bit(1);          // short_term_ref_pic_set_sps_flag (the single SPS set: no index bits)
     } else {
@@ -1273,16 +1328,26 @@ std::vector<uint8_t> hevc_write_slice(const HevcConfig& c, const HevcFrameParams
     bw.put_bit(1);            // slice_sao_chroma_flag
   }
   if (inter) {
-    bw.put_bit(0);            // num_ref_idx_active_override_flag (one picture per list)
+    // num_ref_idx_active_override_flag: the PPS defaults are one picture per list
+    const int n0 = fp.num_ref[0], n1 = bslice ? fp.num_ref[1] : 1;
+    const bool over = n0 != 1 || n1 != 1;
+    bw.put_bit(over ? 1 : 0);
+    if (over) {
+      bw.put_ue(n0 - 1);              // num_ref_idx_l0_active_minus1
+      if (bslice) bw.put_ue(n1 - 1);  // num_ref_idx_l1_active_minus1
+    }
     if (bslice) bw.put_bit(0);  // mvd_l1_zero_flag
     if (c.tmvp && bslice) bw.put_bit(0);  // collocated_from_l0_flag: the collocated picture is RefPicList1[0]
+    // collocated_ref_idx 0: RefPicList1[0] (B) / RefPicList0[0] (P)
+    if (c.tmvp && ((bslice && n1 > 1) || (!bslice && n0 > 1))) bw.put_ue(0);
     if (c.weightp && !bslice) {
-      // pred_weight_table (7.3.6.3), one list-0 entry: log2 denominators 6 / 6; the chroma
-      // offset is coded as its difference from the weight-dependent prediction (7.4.7.3)
+      // pred_weight_table (7.3.6.3): log2 denominators 6 / 6; weights on RefPicList0[0] only
+      // (the other entries' flags are 0); the chroma offset is coded as its difference from the
+      // weight-dependent prediction (7.4.7.3)
       bw.put_ue(6);                 // luma_log2_weight_denom
       bw.put_se(0);                 // delta_chroma_log2_weight_denom
-      bw.put_bit(fp.wp ? 1 : 0);    // luma_weight_l0_flag[0]
-      bw.put_bit(fp.wp ? 1 : 0);    // chroma_weight_l0_flag[0]
+      for (int i = 0; i < n0; ++i) bw.put_bit(i == 0 && fp.wp ? 1 : 0);  // luma_weight_l0_flag[i]
+      for (int i = 0; i < n0; ++i) bw.put_bit(i == 0 && fp.wp ? 1 : 0);  // chroma_weight_l0_flag[i]
       if (fp.wp) {
         bw.put_se(fp.wp_w[0] - 64);  // delta_luma_weight_l0
         bw.put_se(fp.wp_o[0]);       // luma_offset_l0

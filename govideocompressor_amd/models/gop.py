@@ -179,7 +179,8 @@ class GopPic:
     current picture)`` for every picture the DPB must still hold; ``slot``: the
     reconstruction buffer (0 .. ref_slots - 1 for reference pictures, ``ref_slots`` for
     non-reference B pictures); ``l0`` / ``l1``: display indices of RefPicList0[0] /
-    RefPicList1[0] and ``s0`` / ``s1`` their buffers."""
+    RefPicList1[0] and ``s0`` / ``s1`` their buffers; ``refs0`` / ``srefs0``: every active
+    RefPicList0 entry (nearest first; P pictures with x265 --ref > 1) and its buffer."""
     d: int
     kind: str                # "I", "P", "B"
     ref: bool                # referenced by later pictures (I, P, the pyramid's middle B)
@@ -189,18 +190,34 @@ class GopPic:
     l1: int = -1
     s0: int = -1
     s1: int = -1
+    refs0: tuple = ()
+    srefs0: tuple = ()
 
 
-def hevc_gop_plan(frames: int, bframes: int, pyramid: bool = True, anchors_at=(), ref_slots: int = 3) -> list[GopPic]:
+def hevc_ref_slots(bframes: int, pyramid: bool, refs: int = 1) -> int:
+    """Reconstruction buffers of reference pictures :func:`hevc_gop_plan` needs: the list-0
+    pictures a P anchor keeps for itself and the next anchors plus the one being coded, one more
+    for a pyramid's reference B (at least 2 for P-only GOPs and 3 with B pictures, the round-4
+    layout)."""
+    nb = max(0, int(bframes))
+    need = max(1, int(refs)) + 1 + (1 if pyramid and nb >= 2 else 0)
+    return max(need, 3 if nb else 2)
+
+
+def hevc_gop_plan(frames: int, bframes: int, pyramid: bool = True, anchors_at=(), ref_slots: int = 3,
+                  refs: int = 1) -> list[GopPic]:
     """x265-style closed GOP: I0, P anchors every ``bframes + 1`` pictures (plus the last
     picture and ``anchors_at``), each followed by the B pictures before it.  With
     ``pyramid`` and two or more B pictures in a run, the middle one is a reference B
     (list 0 = the previous anchor, list 1 = the new one) coded first, and the others are
     non-reference b pictures predicting from their nearest references on both sides
-    (x265 --b-pyramid).  The DPB is simulated to give every picture its RPS and buffer."""
+    (x265 --b-pyramid).  ``refs`` (x265 --ref): a P anchor's list 0 holds up to that many
+    reference pictures, nearest first.  The DPB is simulated to give every picture its RPS
+    and buffer."""
     if frames < 1:
         return []
     step = max(0, int(bframes)) + 1
+    nref = max(1, int(refs))
     anchors = sorted(set(range(0, frames, step)) | {frames - 1} | {int(d) for d in anchors_at if 0 <= int(d) < frames})
     if step > 1:  # keep every B run <= bframes after inserting the extra anchors
         out_a, prev = [0], 0
@@ -223,20 +240,35 @@ def hevc_gop_plan(frames: int, bframes: int, pyramid: bool = True, anchors_at=()
             seq += [(d, "B", False, mid, a1) for d in run if d > mid]
         else:
             seq += [(d, "B", False, a0, a1) for d in run]
+    # list 0 of every P anchor: the nearest reference pictures coded before it (in its closed GOP)
+    lists0 = []
+    coded_refs: list = []
+    for d, kind, ref, l0, l1 in seq:
+        if kind == "I":
+            coded_refs = []
+        if kind == "P":
+            near = sorted((r for r in coded_refs if r < d), key=lambda r: -r)[:nref]
+            assert near and near[0] == l0, (d, near, l0)
+            lists0.append(tuple(near))
+        else:
+            lists0.append((l0,) if l0 >= 0 else ())
+        if ref:
+            coded_refs.append(d)
     # a reference picture stays in the DPB until the last picture that uses it
     last_use: dict = {}
-    for i, (d, kind, ref, l0, l1) in enumerate(seq):
-        for r in (l0, l1):
+    for i, ((d, kind, ref, l0, l1), r0) in enumerate(zip(seq, lists0)):
+        for r in (*r0, l0, l1):
             if r >= 0:
                 last_use[r] = i
     dpb: dict = {}  # display index -> slot
     out = []
-    for i, (d, kind, ref, l0, l1) in enumerate(seq):
+    for i, ((d, kind, ref, l0, l1), r0) in enumerate(zip(seq, lists0)):
         if kind == "I":
             dpb = {}
         keep = {r: s for r, s in dpb.items() if last_use.get(r, -1) >= i}
         dpb = keep
-        rps = tuple(sorted((r, r in (l0, l1)) for r in keep))
+        used = set(r0) | {l0, l1}
+        rps = tuple(sorted((r, r in used) for r in keep))
         if ref:
             free = [s for s in range(ref_slots) if s not in dpb.values()]
             if not free:
@@ -244,7 +276,8 @@ def hevc_gop_plan(frames: int, bframes: int, pyramid: bool = True, anchors_at=()
             slot = free[0]
         else:
             slot = ref_slots
-        out.append(GopPic(d, kind, ref, slot, rps, l0, l1, dpb.get(l0, -1), dpb.get(l1, -1)))
+        out.append(GopPic(d, kind, ref, slot, rps, l0, l1, dpb.get(l0, -1), dpb.get(l1, -1), r0,
+                          tuple(dpb.get(r, -1) for r in r0)))
         if ref:
             dpb[d] = slot
     return out

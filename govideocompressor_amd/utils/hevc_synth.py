@@ -46,7 +46,7 @@ def _levels(rng, n: int, density: float) -> np.ndarray:
 def random_records(rng, width: int, height: int, pslice: bool, bit_depth: int = 8, density: float = 0.08,
                    intra_in_p: float = 0.2, mv_range: int = 64, sao: bool = True, ctb_qp: tuple | None = None,
                    nxn: float = 0.0, tu_split: float = 0.0, force_split: int | None = None, bslice: bool = False,
-                   mv_pool: int = 0, uniform64: float = 0.0):
+                   mv_pool: int = 0, uniform64: float = 0.0, nref: tuple = (1, 1)):
     """``ctb_qp = (qp, spread)``: per-CTB QPs qp + U[-spread, spread] (cu_qp_delta streams);
     ``nxn``: probability of an 8x8 intra CU being split into four 4x4 PUs; ``tu_split``: of a
     16x16 / 32x32 inter CU coding its residual as four quarter TUs (needs tu_inter_depth 1);
@@ -54,7 +54,8 @@ def random_records(rng, width: int, height: int, pslice: bool, bit_depth: int = 
     vectors drawn from that many values, so merge candidates (spatial, temporal, combined
     bi-predictive, zero) match often; ``uniform64``: probability that a 64x64-aligned group of
     four blocks is one residual-free inter motion (the CTU-64 writer codes it as a 64x64 skip CU
-    when the motion is a merge candidate)."""
+    when the motion is a merge candidate); ``nref``: active pictures of list 0 / list 1 -- inter CUs
+    draw a refIdx per used list (CuInfo pad[0] / pad[1], bytes 13 / 14)."""
     pool = rng.integers(-mv_range, mv_range + 1, (max(1, mv_pool), 2)).astype(np.int16) if mv_pool else None
 
     def rand_mv():
@@ -119,10 +120,13 @@ def random_records(rng, width: int, height: int, pslice: bool, bit_depth: int = 
                     rec[12] = d
                     if d & 1:
                         rec[4:8] = mv.view(np.uint8)
+                        rec[13] = int(rng.integers(0, nref[0]))
                     if d & 2:
                         rec[8:12] = mv1.view(np.uint8)
+                        rec[14] = int(rng.integers(0, nref[1]))
                 else:
                     rec[4:8] = mv.view(np.uint8)
+                    rec[13] = int(rng.integers(0, nref[0]))
             for gy in range(y // 8, (y + n) // 8):
                 for gx in range(x // 8, (x + n) // 8):
                     cu[i * 16 + _zorder8(gx, gy)] = rec
@@ -174,35 +178,39 @@ def random_stream(host, width: int, height: int, frames: int, seed: int = 0, qp:
 
 def random_gop_stream(host, width: int, height: int, frames: int, bframes: int = 3, seed: int = 0, qp: int = 30,
                       bit_depth: int = 8, tmvp: bool = True, pyramid: bool = False, host_cfg: dict | None = None,
-                      **kw) -> tuple[bytes, list]:
+                      refs: int = 1, **kw) -> tuple[bytes, list]:
     """Annex-B HEVC stream of one closed GOP with B pictures (models/gop.py hevc_gop_plan:
     I, P anchors, B pictures referencing the pictures on both sides; ``pyramid``: the middle
     B of a run is a reference picture) from random records, with each picture's RPS; TMVP
     takes the collocated picture's records.  Returns the stream and the records per
-    *display* index (the decoder outputs pictures in POC order)."""
-    from ..models.gop import hevc_gop_plan
+    *display* index (the decoder outputs pictures in POC order).  ``refs`` > 1: P pictures
+    predict from up to that many earlier reference pictures (x265 --ref; refIdx per CU)."""
+    from ..models.gop import hevc_gop_plan, hevc_ref_slots
 
     rng = np.random.default_rng(seed)
     cfg = dict(width=width, height=height, bit_depth=bit_depth, bframes=bframes, tmvp=int(tmvp), pyramid=int(pyramid),
-               **(host_cfg or {}))
+               refs=int(refs), **(host_cfg or {}))
     out = [host.hevc_parameter_sets(cfg)]
     recs: list = [None] * frames
-    refs: dict = {}    # display index -> (cu records or None for intra, its L0 / L1 reference indices)
-    for pic in hevc_gop_plan(frames, bframes, pyramid):
+    nrefs = int(refs)
+    held = {}    # display index -> (cu records or None for intra, its L0 / L1 references, its list 0)
+    for pic in hevc_gop_plan(frames, bframes, pyramid, refs=nrefs, ref_slots=hevc_ref_slots(bframes, pyramid, nrefs)):
         fqp = int(np.clip(qp + rng.integers(-3, 4), 0, 51))
-        r = random_records(rng, width, height, pslice=pic.kind != "I", bit_depth=bit_depth, bslice=pic.kind == "B", **kw)
+        r = random_records(rng, width, height, pslice=pic.kind != "I", bit_depth=bit_depth, bslice=pic.kind == "B",
+                           nref=(max(1, len(pic.refs0)), 1), **kw)
         fp = dict(idr=int(pic.kind == "I"), poc=pic.d, qp=fqp, slice_type={"I": 2, "P": 1, "B": 0}[pic.kind],
                   nal_ref=int(pic.ref), rps=[(d, int(u)) for d, u in pic.rps])
         if pic.kind != "I":
             fp["ref_poc0"] = pic.l0
+            fp["refs0"] = list(pic.refs0)
             col = pic.l1 if pic.kind == "B" else pic.l0
             if pic.kind == "B":
                 fp["ref_poc1"] = pic.l1
-            ccu, c0, c1 = refs[col]
-            fp.update(col_poc=col, col_ref_poc0=c0, col_ref_poc1=c1, col_cu=ccu)
+            ccu, c0, c1, cl0 = held[col]
+            fp.update(col_poc=col, col_ref_poc0=c0, col_ref_poc1=c1, col_cu=ccu, col_refs0=cl0)
         nal, _ = host.hevc_write_slice(cfg, fp, *r)
         if pic.ref:
-            refs[pic.d] = (None if pic.kind == "I" else r[1].copy(), pic.l0, pic.l1)
+            held[pic.d] = (None if pic.kind == "I" else r[1].copy(), pic.l0, pic.l1, list(pic.refs0) or None)
         out.append(nal)
         recs[pic.d] = r
     return b"".join(out), recs

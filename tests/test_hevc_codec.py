@@ -316,3 +316,31 @@ def test_hevc_ctu64_b_gop_roundtrip(host, seed, pyramid):
         assert np.array_equal(p["coef_y"], cy)
         inter = cu[:, 0] == 1
         assert np.array_equal(p["cu"][inter, 4:12], cu[inter, 4:12])
+
+
+@pytest.mark.parametrize("seed,refs,bframes,tmvp,pyramid,wpp", [(0, 3, 1, 1, 0, 1), (1, 3, 0, 1, 0, 0),
+                                                               (2, 2, 3, 1, 1, 0), (3, 4, 1, 0, 0, 1),
+                                                               (4, 3, 3, 1, 1, 1)])
+def test_hevc_multiref_roundtrip(host, seed, refs, bframes, tmvp, pyramid, wpp):
+    """x265 --ref N: P slices with several active list-0 pictures (num_ref_idx_active_override,
+    ref_idx_l0 in AMVP CUs, the RPS marking every list entry used), merge candidates carrying
+    their refIdx (spatial neighbours, refIdx-0 temporal candidates, zero candidates counting up
+    through the list), AMVP spatial candidates scaled by each neighbour's own reference
+    distance, and TMVP from a collocated picture whose blocks point at different pictures.  The
+    decoder must recover every CU's direction, refIdx and vector."""
+    from govideocompressor_amd.utils.hevc_synth import random_gop_stream
+
+    s, recs = random_gop_stream(host, 128, 96, 10, bframes=bframes, seed=seed, tmvp=bool(tmvp), mv_pool=3,
+                                intra_in_p=0.05, density=0.02, host_cfg=dict(wpp=wpp, threads=2), pyramid=bool(pyramid),
+                                refs=refs)
+    pics = host.hevc_decode(s)
+    assert len(pics) == 10
+    far = 0
+    for d, (p, (ctu, cu, cy, cb, cr)) in enumerate(zip(pics, recs)):
+        assert p["poc"] == d
+        assert np.array_equal(p["coef_y"], cy) and np.array_equal(p["coef_cb"], cb)
+        inter = cu[:, 0] == 1
+        assert np.array_equal(p["cu"][inter, 4:12], cu[inter, 4:12])
+        assert np.array_equal(p["cu"][inter, 13:15], cu[inter, 13:15])   # refIdx L0 / L1
+        far += int((cu[inter, 13] > 0).sum())
+    assert far > 0
