@@ -1468,7 +1468,28 @@ struct HevcBArgs {
   // same list at the same costs, so it only copies its motion through
   const uint8_t* chg_in;
   uint8_t* chg_out;
+  // x265 --ref: P pictures with nref0 > 1 active list-0 pictures.  A motion's direction byte
+  // carries its list-0 refIdx in bits 2-3 (CuDir in bits 0-1); xref / xhp are the proxies and
+  // half-sample planes of RefPicList0[1 ..], and the P init pass picks per block among the
+  // list-0[0] search (mv0 / cost0 / pm0) and the farther searches xmv / xcost / xpm
+  // ([nref0 - 1, B, nmb, ...]; xcost kNoCost = not searched) at cost + lambda * ref_idx bins
+  int nref0;
+  const uint8_t* xref[3];
+  const uint8_t* xhp[3];
+  const int16_t* xmv;
+  const int* xcost;
+  const int16_t* xpm;
 };
+
+// RefPicList0[r]'s 8-bit proxy / half-sample planes (constant indices only: no scratch)
+__device__ __forceinline__ const uint8_t* l0_ref(const HevcBArgs& a, int r) {
+  return r == 0 ? a.ref0 : (r == 1 ? a.xref[0] : (r == 2 ? a.xref[1] : a.xref[2]));
+}
+__device__ __forceinline__ const uint8_t* l0_hp(const HevcBArgs& a, int r) {
+  return r == 0 ? a.hp0 : (r == 1 ? a.xhp[0] : (r == 2 ? a.xhp[1] : a.xhp[2]));
+}
+// ref_idx_l0 bins (TR, cMax nref - 1)
+__device__ __forceinline__ int ref_bins(int r, int nref) { return nref <= 1 ? 0 : min(r + 1, nref - 1); }
 
 // z-scan availability (6.4.1) of the 16x16 block (nx, ny) for the block (mx, my) on the 16x16
 // grid: CTUs in raster order, blocks inside a CTU in z-order
@@ -1535,20 +1556,42 @@ __global__ __launch_bounds__(64) void hevc_b_choose(HevcBArgs a) {
   }
 }
 
-// P pictures enter the merge passes in the same form: one list-0 search, bits = its mvd bits
+// P pictures enter the merge passes in the same form: the list-0 search, bits = its mvd bits;
+// with several list-0 pictures the cheapest search at cost + lambda * ref_idx bins
 __global__ __launch_bounds__(256) void hevc_b_init_p(HevcBArgs a) {
   const int nmb = a.g.nmb();
   const int i = blockIdx.x * 256 + threadIdx.x, slot = blockIdx.y;
   if (i >= nmb) return;
   const size_t o = static_cast<size_t>(slot) * nmb + i;
-  const int x0 = a.mv0[o * 2], y0 = a.mv0[o * 2 + 1];
+  int x0 = a.mv0[o * 2], y0 = a.mv0[o * 2 + 1];
+  int best = a.cost0[o], bits = mvbits_se(x0 - a.pm0[o * 2]) + mvbits_se(y0 - a.pm0[o * 2 + 1]), br = 0;
+  if (a.nref0 > 1) {
+    const int qp = clampi(a.qp[slot] + (a.aq ? a.aq[o] : 0), 0, 51);
+    const int lam = h264::kLambda[qp];
+    best += lam * ref_bins(0, a.nref0);
+    bits += ref_bins(0, a.nref0);
+    const size_t plane = static_cast<size_t>(a.g.B) * nmb;
+    for (int r = 1; r < a.nref0; ++r) {
+      const size_t xo = (r - 1) * plane + o;
+      const int c = a.xcost[xo];
+      if (c >= kNoCostB) continue;
+      const int rb = ref_bins(r, a.nref0);
+      if (c + lam * rb < best) {
+        best = c + lam * rb;
+        br = r;
+        x0 = a.xmv[xo * 2];
+        y0 = a.xmv[xo * 2 + 1];
+        bits = mvbits_se(x0 - a.xpm[xo * 2]) + mvbits_se(y0 - a.xpm[xo * 2 + 1]) + rb;
+      }
+    }
+  }
   int16_t* m = a.mvb_out + o * 4;
   m[0] = static_cast<int16_t>(x0);
   m[1] = static_cast<int16_t>(y0);
   m[2] = m[3] = 0;
-  a.dir_out[o] = 1;
-  a.cost[o] = a.cost0[o];
-  a.bits[o] = mvbits_se(x0 - a.pm0[o * 2]) + mvbits_se(y0 - a.pm0[o * 2 + 1]);
+  a.dir_out[o] = static_cast<uint8_t>(1 | (br << 2));
+  a.cost[o] = best;
+  a.bits[o] = bits;
 }
 
 // Jacobi pass.  Each block is offered the merge list the CABAC writer would build for it as a
@@ -1658,8 +1701,9 @@ __global__ __launch_bounds__(64) void hevc_b_merge(HevcBArgs a) {
     }
   }
   {
+    // zero candidates: refIdx 0, 1, .. through the active list-0 size (P), then 0
     const int z[4] = {0, 0, 0, 0};
-    while (nk < maxc) push(a.bslice ? 3 : 1, z);
+    for (int zi = 0; nk < maxc; ++zi) push(a.bslice ? 3 : (1 | ((zi < a.nref0 ? zi : 0) << 2)), z);
   }
   if (nk > maxc) nk = maxc;
   const int cd = a.dir_in[o];
@@ -1672,8 +1716,7 @@ __global__ __launch_bounds__(64) void hevc_b_merge(HevcBArgs a) {
   const int X = mx * 16 + (lane & 3) * 4, Y = my * 16 + (lane >> 2) * 4;
   const size_t yo = static_cast<size_t>(slot) * g.ysize();
   const size_t ho = static_cast<size_t>(slot) * 3 * (g.W + 2 * kHpMargin) * (g.H + 2 * kHpMargin);
-  const uint8_t *G0 = a.ref0 + yo, *H0 = a.hp0 + ho;
-  const uint8_t *G1 = a.bslice ? a.ref1 + yo : G0, *H1 = a.bslice ? a.hp1 + ho : H0;
+  const uint8_t *G1 = a.bslice ? a.ref1 + yo : a.ref0 + yo, *H1 = a.bslice ? a.hp1 + ho : a.hp0 + ho;
   uint32_t src[4];
 #pragma unroll
   for (int y = 0; y < 4; ++y)
@@ -1689,8 +1732,11 @@ __global__ __launch_bounds__(64) void hevc_b_merge(HevcBArgs a) {
     int sat = satd_cur;
     if (!same(kd[j], kv[j], cd, cw)) {
       uint32_t pw[4];
+      const int r0 = (kd[j] >> 2) & 3;  // list-0 refIdx (P pictures with several list-0 pictures)
+      const uint8_t *G0 = l0_ref(a, r0) + yo, *H0 = l0_hp(a, r0) + ho;
 #pragma unroll
-      for (int y = 0; y < 4; ++y) pw[y] = mc4_b(a, G0, H0, G1, H1, X, Y + y, kd[j], kv[j][0], kv[j][1], kv[j][2], kv[j][3]);
+      for (int y = 0; y < 4; ++y)
+        pw[y] = mc4_b(a, G0, H0, G1, H1, X, Y + y, kd[j] & 3, kv[j][0], kv[j][1], kv[j][2], kv[j][3]);
       sat = satd16_rows(src, pw);
     }
     const int nb = 1 + (maxc > 1 ? min(j + 1, maxc - 1) : 0);  // merge_flag + truncated-unary merge_idx
@@ -2092,8 +2138,18 @@ extern "C" void mivc_launch_hevc_b(int mode, int B, int wmb, int hmb, const uint
                                    const int16_t* pm1, const int16_t* tmv, const uint8_t* tdir, const int16_t* mvb_in,
                                    const uint8_t* dir_in, int16_t* mvb_out, uint8_t* dir_out, int* cost, int* bits,
                                    const int* qp, const int8_t* aq, void* stream, int bslice, int max_merge,
-                                   int ctu64, const uint8_t* chg_in, uint8_t* chg_out) {
+                                   int ctu64, const uint8_t* chg_in, uint8_t* chg_out, int nref0,
+                                   const uint8_t* const* xref, const uint8_t* const* xhp, const int16_t* xmv,
+                                   const int* xcost, const int16_t* xpm) {
   HevcBArgs a;
+  a.nref0 = nref0 < 1 ? 1 : nref0;
+  for (int r = 0; r < 3; ++r) {
+    a.xref[r] = r + 1 < a.nref0 ? xref[r] : ref0;
+    a.xhp[r] = r + 1 < a.nref0 ? xhp[r] : hp0;
+  }
+  a.xmv = xmv;
+  a.xcost = xcost;
+  a.xpm = xpm;
   a.chg_in = chg_in;
   a.chg_out = chg_out;
   a.ctu_shift = ctu64 ? 2 : 1;

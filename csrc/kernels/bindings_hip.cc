@@ -7,6 +7,7 @@
 
 #include <cstdint>
 #include <stdexcept>
+#include <vector>
 
 #include "hevc_decode.h"
 
@@ -111,12 +112,14 @@ void mivc_launch_hevc_inter(int B, int W, int H, const uint16_t* sy, const uint1
                             const int8_t* run, const int* cand, const int16_t* mv, const int* me_cost, int bd,
                             int tu_split, int sdh, int intra_bias, void* stream, const int16_t* mvb,
                             const uint8_t* dirb, const uint16_t* f1y, const uint16_t* f1u, const uint16_t* f1v,
-                            const int16_t* wp);
+                            const int16_t* wp, const uint16_t* const* xref);
 void mivc_launch_hevc_b(int mode, int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref0, const uint8_t* ref1,
                         const uint8_t* hp0, const uint8_t* hp1, const int16_t* mv0, const int16_t* mv1, const int* cost0,
                         const int* cost1, const int16_t* pm0, const int16_t* pm1, const int16_t* tmv, const uint8_t* tdir,
                         const int16_t* mvb_in, const uint8_t* dir_in, int16_t* mvb_out, uint8_t* dir_out, int* cost,
-                        int* bits, const int* qp, const int8_t* aq, void* stream, int bslice, int max_merge, int ctu64, const uint8_t* chg_in, uint8_t* chg_out);
+                        int* bits, const int* qp, const int8_t* aq, void* stream, int bslice, int max_merge, int ctu64, const uint8_t* chg_in, uint8_t* chg_out,
+                        int nref0, const uint8_t* const* xref, const uint8_t* const* xhp, const int16_t* xmv,
+                        const int* xcost, const int16_t* xpm);
 void mivc_launch_hevc_deblock(int B, int W, int H, int bd, uint16_t* y, uint16_t* u, uint16_t* v, const void* cu,
                               const void* ctu, const int8_t* run, void* stream);
 void mivc_launch_hevc_aq(int B, int W, int H, int bd, const uint16_t* sy, const uint16_t* su, const uint16_t* sv,
@@ -493,24 +496,43 @@ PYBIND11_MODULE(_hip, m) {
                          uintptr_t fv, uintptr_t ry, uintptr_t ru, uintptr_t rv, uintptr_t ctu, uintptr_t cu, uintptr_t cy,
                          uintptr_t cu_, uintptr_t cv, uintptr_t qp, uintptr_t run, uintptr_t cand, uintptr_t mv,
                          uintptr_t me_cost, int bd, uintptr_t stream, int tu_split, int sdh, int intra_bias,
-                         uintptr_t mvb, uintptr_t dirb, uintptr_t f1y, uintptr_t f1u, uintptr_t f1v, uintptr_t wp) {
+                         uintptr_t mvb, uintptr_t dirb, uintptr_t f1y, uintptr_t f1u, uintptr_t f1v, uintptr_t wp,
+                         std::vector<uintptr_t> xref) {
     if (dirb && (!mvb || !f1y || !f1u || !f1v)) throw std::invalid_argument("hevc_inter: B motion needs mvb and list-1 planes");
+    // xref: (y, u, v) of RefPicList0[1 ..] (x265 --ref), at most 3 pictures
+    if (xref.size() % 3 || xref.size() > 9) throw std::invalid_argument("hevc_inter: xref = (y, u, v) x up to 3 pictures");
+    const uint16_t* xr[9] = {};
+    for (size_t i = 0; i < xref.size(); ++i) xr[i] = P<uint16_t>(xref[i]);
     mivc_launch_hevc_inter(B, W, H, P<uint16_t>(sy), P<uint16_t>(su), P<uint16_t>(sv), P<uint16_t>(fy), P<uint16_t>(fu),
                            P<uint16_t>(fv), P<uint16_t>(ry), P<uint16_t>(ru), P<uint16_t>(rv), P<void>(ctu), P<void>(cu),
                            P<int16_t>(cy), P<int16_t>(cu_), P<int16_t>(cv), P<int>(qp), P<int8_t>(run), P<int>(cand),
                            P<int16_t>(mv), P<int>(me_cost), bd, tu_split, sdh, intra_bias, S(stream), P<int16_t>(mvb),
-                           P<uint8_t>(dirb), P<uint16_t>(f1y), P<uint16_t>(f1u), P<uint16_t>(f1v), P<int16_t>(wp));
+                           P<uint8_t>(dirb), P<uint16_t>(f1y), P<uint16_t>(f1u), P<uint16_t>(f1v), P<int16_t>(wp), xr);
   }, py::arg("B"), py::arg("W"), py::arg("H"), py::arg("sy"), py::arg("su"), py::arg("sv"), py::arg("fy"), py::arg("fu"),
      py::arg("fv"), py::arg("ry"), py::arg("ru"), py::arg("rv"), py::arg("ctu"), py::arg("cu"), py::arg("cy"),
      py::arg("cu_"), py::arg("cv"), py::arg("qp"), py::arg("run"), py::arg("cand"), py::arg("mv"), py::arg("me_cost"),
      py::arg("bd"), py::arg("stream"), py::arg("tu_split") = 0, py::arg("sdh") = 0, py::arg("intra_bias") = 0,
      py::arg("mvb") = 0, py::arg("dirb") = 0, py::arg("f1y") = 0, py::arg("f1u") = 0, py::arg("f1v") = 0,
-     py::arg("wp") = 0);
+     py::arg("wp") = 0, py::arg("xref") = std::vector<uintptr_t>{});
   m.def("hevc_b", [](int mode, int B, int wmb, int hmb, uintptr_t src, uintptr_t ref0, uintptr_t ref1, uintptr_t hp0,
                      uintptr_t hp1, uintptr_t mv0, uintptr_t mv1, uintptr_t cost0, uintptr_t cost1, uintptr_t pm0,
                      uintptr_t pm1, uintptr_t tmv, uintptr_t tdir, uintptr_t mvb_in, uintptr_t dir_in, uintptr_t mvb_out,
                      uintptr_t dir_out, uintptr_t cost, uintptr_t bits, uintptr_t qp, uintptr_t aq, uintptr_t stream,
-                     int bslice, int max_merge, int ctu64, uintptr_t chg_in, uintptr_t chg_out) {
+                     int bslice, int max_merge, int ctu64, uintptr_t chg_in, uintptr_t chg_out, int nref0,
+                     std::vector<uintptr_t> xref, std::vector<uintptr_t> xhp, uintptr_t xmv, uintptr_t xcost,
+                     uintptr_t xpm) {
+    // nref0 > 1 (P pictures, x265 --ref): xref / xhp = RefPicList0[1 ..] proxies and planes; the
+    // P init pass also needs the farther searches xmv / xcost / xpm
+    if (nref0 < 1 || nref0 > 4) throw std::invalid_argument("hevc_b: nref0 in 1..4");
+    if (nref0 > 1 && (bslice || xref.size() + 1 < static_cast<size_t>(nref0) || xhp.size() + 1 < static_cast<size_t>(nref0)))
+      throw std::invalid_argument("hevc_b: nref0 > 1 needs P pictures and nref0 - 1 extra proxies / planes");
+    if (nref0 > 1 && mode == 2 && (!xmv || !xcost || !xpm)) throw std::invalid_argument("hevc_b: P init with several refs needs xmv / xcost / xpm");
+    const uint8_t* xr[3] = {nullptr, nullptr, nullptr};
+    const uint8_t* xh[3] = {nullptr, nullptr, nullptr};
+    for (int r = 0; r + 1 < nref0; ++r) {
+      xr[r] = P<uint8_t>(xref[r]);
+      xh[r] = P<uint8_t>(xhp[r]);
+    }
     // mode 0: L0 / L1 / bi choice from the two searches; 1: one merge-aware Jacobi pass;
     // 2: a P picture's list-0 search in the same motion form
     if (mode < 0 || mode > 2) throw std::invalid_argument("hevc_b: mode 0 (choose), 1 (merge pass) or 2 (P init)");
@@ -529,12 +551,15 @@ PYBIND11_MODULE(_hip, m) {
                        P<uint8_t>(hp1), P<int16_t>(mv0), P<int16_t>(mv1), P<int>(cost0), P<int>(cost1), P<int16_t>(pm0),
                        P<int16_t>(pm1), P<int16_t>(tmv), P<uint8_t>(tdir), P<int16_t>(mvb_in), P<uint8_t>(dir_in),
                        P<int16_t>(mvb_out), P<uint8_t>(dir_out), P<int>(cost), P<int>(bits), P<int>(qp), P<int8_t>(aq),
-                       S(stream), bslice, max_merge, ctu64, P<uint8_t>(chg_in), P<uint8_t>(chg_out));
+                       S(stream), bslice, max_merge, ctu64, P<uint8_t>(chg_in), P<uint8_t>(chg_out), nref0,
+                       xr, xh, P<int16_t>(xmv), P<int>(xcost), P<int16_t>(xpm));
   }, py::arg("mode"), py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("src"), py::arg("ref0"), py::arg("ref1"),
      py::arg("hp0"), py::arg("hp1"), py::arg("mv0"), py::arg("mv1"), py::arg("cost0"), py::arg("cost1"), py::arg("pm0"),
      py::arg("pm1"), py::arg("tmv"), py::arg("tdir"), py::arg("mvb_in"), py::arg("dir_in"), py::arg("mvb_out"),
      py::arg("dir_out"), py::arg("cost"), py::arg("bits"), py::arg("qp"), py::arg("aq"), py::arg("stream"),
-     py::arg("bslice") = 1, py::arg("max_merge") = 5, py::arg("ctu64") = 0, py::arg("chg_in") = 0, py::arg("chg_out") = 0);
+     py::arg("bslice") = 1, py::arg("max_merge") = 5, py::arg("ctu64") = 0, py::arg("chg_in") = 0, py::arg("chg_out") = 0,
+     py::arg("nref0") = 1, py::arg("xref") = std::vector<uintptr_t>{}, py::arg("xhp") = std::vector<uintptr_t>{},
+     py::arg("xmv") = 0, py::arg("xcost") = 0, py::arg("xpm") = 0);
   m.def("hevc_deblock", [](int B, int W, int H, int bd, uintptr_t y, uintptr_t u, uintptr_t v, uintptr_t cu,
                            uintptr_t ctu, uintptr_t run, uintptr_t stream) {
     mivc_launch_hevc_deblock(B, W, H, bd, P<uint16_t>(y), P<uint16_t>(u), P<uint16_t>(v), P<void>(cu), P<void>(ctu),

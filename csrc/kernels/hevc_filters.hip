@@ -170,10 +170,11 @@ __global__ void hevc_deblock(HevcDbkArgs a) {
   if (P.pred == hevc::CU_INTRA || Q.pred == hevc::CU_INTRA) bs = 2;
   else if ((P.cbf & 1) || (Q.cbf & 1)) bs = 1;
   else {
-    // 8.7.2.4 with one picture per list and RefPicList0[0] != RefPicList1[0]: the direction
-    // fixes the set of reference pictures; equal sets compare the vectors list by list
+    // 8.7.2.4: the direction and the refIdx of each used list fix the set of reference pictures
+    // (one slice per picture: equal refIdx = the same picture; the B pictures this encoder codes
+    // hold different pictures in list 0 and list 1); equal sets compare the vectors list by list
     const int dp = hevc::cu_dir(P), dq = hevc::cu_dir(Q);
-    if (dp != dq) bs = 1;
+    if (dp != dq || ((dp & 1) && P.pad[0] != Q.pad[0]) || ((dp & 2) && P.pad[1] != Q.pad[1])) bs = 1;
     else if ((dp & 1) && (abs(P.mv[0] - Q.mv[0]) >= 4 || abs(P.mv[1] - Q.mv[1]) >= 4)) bs = 1;
     else if ((dp & 2) && (abs(P.mv1[0] - Q.mv1[0]) >= 4 || abs(P.mv1[1] - Q.mv1[1]) >= 4)) bs = 1;
     else bs = 0;

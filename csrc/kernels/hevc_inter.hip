@@ -46,7 +46,17 @@ struct HevcInterArgs {
   // log2 denominators kWpLog2 for luma and chroma): [B][6] = weight, offset (8-bit units) of
   // Y, Cb, Cr; weight 0 = the slot's picture is not weighted.  Null: default weighting.
   const int16_t* wp;
+  // x265 --ref: RefPicList0[1 ..] reconstructions of a P picture (a motion's direction byte in
+  // dirb carries its list-0 refIdx in bits 2-3; the CU records take it in pad[0]); explicit
+  // weights apply to RefPicList0[0] only
+  const uint16_t *xref_y[3], *xref_u[3], *xref_v[3];
 };
+
+// plane c of RefPicList0[r] (constant indices only: no scratch)
+__device__ __forceinline__ const uint16_t* l0_plane(const HevcInterArgs& a, int c, int r) {
+  const uint16_t* const* x = c == 0 ? a.xref_y : (c == 1 ? a.xref_u : a.xref_v);
+  return r == 0 ? (c == 0 ? a.ref_y : (c == 1 ? a.ref_u : a.ref_v)) : (r == 1 ? x[0] : (r == 2 ? x[1] : x[2]));
+}
 
 constexpr int kWpLog2 = 6;
 
@@ -142,7 +152,8 @@ __global__ __launch_bounds__(64) void hevc_p_decide(HevcInterArgs a) {
       c.mv[1] = static_cast<int16_t>(s_mvy[q]);
       c.mv1[0] = static_cast<int16_t>(s_mv1x[q]);
       c.mv1[1] = static_cast<int16_t>(s_mv1y[q]);
-      c.dir = static_cast<uint8_t>(s_dir[q]);
+      c.dir = static_cast<uint8_t>(s_dir[q] & 3);
+      c.pad[0] = static_cast<uint8_t>((s_dir[q] >> 2) & 3);  // list-0 refIdx
     } else {
       c.pred = hevc::CU_INTRA;
       const int idx = lg == 5 ? 0 : (lg == 4 ? 1 + q : 5 + k);
@@ -333,6 +344,7 @@ __global__ __launch_bounds__(64) void hevc_inter_cu(HevcInterArgs a) {
   const int X0 = rx * 32 + (lg == 5 ? 0 : (q & 1) * 16), Y0 = ry * 32 + (lg == 5 ? 0 : (q >> 1) * 16);
   const int mvx = cu[kq].mv[0], mvy = cu[kq].mv[1], mv1x = cu[kq].mv1[0], mv1y = cu[kq].mv1[1];
   const int dir = hevc::cu_dir(cu[kq]);
+  const int r0 = cu[kq].pad[0] & 3;  // list-0 refIdx
   const int bd = a.bd, maxv = (1 << bd) - 1;
   const int qpy = a.qp[cb], off = 6 * (bd - 8);
   const int qpl = qpy + off, qpc = hevc::chroma_qp_map(clampi(qpy, -off, 57)) + off;
@@ -346,12 +358,12 @@ __global__ __launch_bounds__(64) void hevc_inter_cu(HevcInterArgs a) {
     const int pw = c ? g.W / 2 : g.W, ph = c ? g.H / 2 : g.H, bs = c ? n / 2 : n;
     const int bx = c ? X0 / 2 : X0, by = c ? Y0 / 2 : Y0;
     const size_t ps = c ? g.csize() : g.ysize();
-    const uint16_t* ref = (c == 0 ? a.ref_y : (c == 1 ? a.ref_u : a.ref_v)) + slot * ps;
+    const uint16_t* ref = l0_plane(a, c, r0) + slot * ps;
     const uint16_t* ref1 = a.ref1_y ? (c == 0 ? a.ref1_y : (c == 1 ? a.ref1_u : a.ref1_v)) + slot * ps : ref;
     const uint16_t* src = (c == 0 ? a.src_y : (c == 1 ? a.src_u : a.src_v)) + slot * ps;
     uint16_t* rec = (c == 0 ? a.rec_y : (c == 1 ? a.rec_u : a.rec_v)) + slot * ps;
     int16_t* lev = (c == 0 ? a.coef_y : (c == 1 ? a.coef_u : a.coef_v)) + slot * ps + static_cast<size_t>(by) * pw + bx;
-    const int ww = (a.wp && dir == hevc::DIR_L0) ? a.wp[slot * 6 + 2 * c] : 0;
+    const int ww = (a.wp && dir == hevc::DIR_L0 && r0 == 0) ? a.wp[slot * 6 + 2 * c] : 0;
     const int wo = ww ? a.wp[slot * 6 + 2 * c + 1] : 0;
     if (c == 0) mc_block<8>(S, ref, ref1, pw, ph, bx, by, bs, dir, mvx, mvy, mv1x, mv1y, bd, ww, wo);
     else mc_block<4>(S, ref, ref1, pw, ph, bx, by, bs, dir, mvx, mvy, mv1x, mv1y, bd, ww, wo);
@@ -439,9 +451,14 @@ extern "C" void mivc_launch_hevc_inter(int B, int W, int H, const uint16_t* sy, 
                                        const int16_t* mv, const int* me_cost, int bd, int tu_split, int sdh,
                                        int intra_bias, void* stream, const int16_t* mvb, const uint8_t* dirb,
                                        const uint16_t* f1y, const uint16_t* f1u, const uint16_t* f1v,
-                                       const int16_t* wp) {
+                                       const int16_t* wp, const uint16_t* const* xref) {
   HevcInterArgs a;
   a.wp = wp;
+  for (int r = 0; r < 3; ++r) {  // xref: [3 x (y, u, v)] of RefPicList0[1 ..] (null: list-0[0])
+    a.xref_y[r] = xref && xref[3 * r] ? xref[3 * r] : fy;
+    a.xref_u[r] = xref && xref[3 * r + 1] ? xref[3 * r + 1] : fu;
+    a.xref_v[r] = xref && xref[3 * r + 2] ? xref[3 * r + 2] : fv;
+  }
   a.g = HevcGeom{B, W, H, W / 32, H / 32};
   a.src_y = sy;
   a.src_u = su;

@@ -129,6 +129,20 @@ class HevcParams:
     weightp: bool = True
     wp_min_mean: float = 2.0
     wp_min_scale: float = 0.08
+    # x265 --ref: active list-0 pictures of a P picture (its nearest earlier reference pictures;
+    # models/gop.py hevc_gop_plan).  The farther pictures get 16x16 searches seeded by the
+    # distance-scaled list-0[0] vectors (radius ref_range), skipped where the list-0[0] cost is
+    # already <= ref_gate; the P init pass picks per block at cost + lambda * ref_idx bins and
+    # the merge passes carry each candidate's refIdx.  B pictures keep one picture per list.
+    refs: int = 1
+    ref_range: int = 4
+    ref_gate: int = 3000
+
+    def eff_refs(self) -> int:
+        """Active list-0 pictures of P pictures (1 for intra-only and keyint GOPs)."""
+        if self.intra_only or self.keyint > 0:
+            return 1
+        return max(1, min(4, int(self.refs)))
 
     def eff_weightp(self) -> bool:
         return bool(self.weightp and not self.intra_only)
@@ -144,7 +158,8 @@ class HevcParams:
                     sao=int(self.sao), deblock=int(self.deblock), max_merge=self.max_merge, wpp=int(self.wpp),
                     cu_qp_delta=int(self.adaptive_qp()), tu_inter_depth=int(self.tu_inter_depth), sdh=int(self.sdh),
                     level_idc=int(self.level_idc), bframes=self.eff_bframes(), tmvp=int(self.tmvp and not self.intra_only),
-                    pyramid=int(self.pyramid), ctu64=int(self.ctu64), weightp=int(self.eff_weightp()))
+                    pyramid=int(self.pyramid), ctu64=int(self.ctu64), weightp=int(self.eff_weightp()),
+                    refs=self.eff_refs())
 
     def frame_qps(self) -> tuple[int, int]:
         qp_p = int(round(self.crf)) if self.crf is not None else int(self.qp)
@@ -225,9 +240,12 @@ class GpuHevcEncoder:
 
         self.src = planes()
         self.nb = params.eff_bframes()
+        self.nrefs = params.eff_refs()
         # reconstruction buffers: one per DPB slot of a reference picture (models/gop.py
-        # hevc_gop_plan: 2 for P-only GOPs, 3 with B pictures) + one for non-reference B pictures
-        self.ref_slots = 3 if self.nb else 2
+        # hevc_ref_slots: 2 for P-only GOPs, 3 with B pictures, more with x265 --ref) + one for
+        # non-reference B pictures
+        from .gop import hevc_ref_slots
+        self.ref_slots = hevc_ref_slots(self.nb, params.pyramid, self.nrefs)
         self.rec = [planes() for _ in range(self.ref_slots)] + ([planes()] if self.nb else [])
         self.dbk = planes()                  # SAO output ping-pong buffer
         self.coefs = [planes(i16), planes(i16)]  # double-buffered: copy-out of t overlaps t + 1
@@ -263,6 +281,15 @@ class GpuHevcEncoder:
         self.col_dir = torch.zeros((R, B, self.hmb, self.wmb), dtype=u8_, device=dev)
         self.col_mv0 = torch.zeros((R, B, self.hmb, self.wmb, 2), dtype=i32_, device=dev)
         self.col_mv1 = torch.zeros((R, B, self.hmb, self.wmb, 2), dtype=i32_, device=dev)
+        # x265 --ref: a collocated P picture whose blocks point at different list-0 pictures keeps
+        # each block's list-0 POC distance (None for the slot: every block uses RefPicList0[0])
+        self.col_td0 = [None] * R
+        if self.nrefs > 1:
+            nx = self.nrefs - 1
+            self.xmv = torch.zeros((nx, B, nmb, 2), dtype=i16_, device=dev)    # farther list-0 searches
+            self.xcost = torch.zeros((nx, B, nmb), dtype=i32_, device=dev)
+            self.xpm = torch.zeros((nx, B, nmb, 2), dtype=i16_, device=dev)    # their seeds / predictors
+            self.xpred = torch.zeros((B, nmb, 256), dtype=u8_, device=dev)     # (prediction scratch)
         if self.nb:
             self.mv1 = torch.zeros((B, nmb, 2), dtype=i16_, device=dev)
             self.me_cost1 = torch.zeros((B, nmb), dtype=i32_, device=dev)
@@ -446,13 +473,23 @@ class GpuHevcEncoder:
         return max(-4096, min(4095, (tb * tx + 32) >> 6))
 
     @staticmethod
-    def _scale(mv: torch.Tensor, td: int, tb: int) -> torch.Tensor:
-        if td == tb or td == 0:
-            return mv
-        p = mv * GpuHevcEncoder._dsf(td, tb)
-        return (torch.sign(p) * ((p.abs() + 127) >> 8)).clamp_(-32768, 32767)
+    def _scale(mv: torch.Tensor, td, tb: int) -> torch.Tensor:
+        """8.5.3.2.8 vector scaling by tb / td; ``td``: one distance or a per-block int tensor
+        (shaped like mv without its last axis)."""
+        if not isinstance(td, torch.Tensor):
+            if td == tb or td == 0:
+                return mv
+            p = mv * GpuHevcEncoder._dsf(td, tb)
+            return (torch.sign(p) * ((p.abs() + 127) >> 8)).clamp_(-32768, 32767)
+        tdc = td.clamp(-128, 127)
+        tbc = max(-128, min(127, tb))
+        q = (16384 + (tdc.abs() >> 1)) // tdc.abs().clamp(min=1)
+        dsf = ((tbc * torch.where(tdc > 0, q, -q) + 32) >> 6).clamp_(-4096, 4095)
+        p = mv * dsf[..., None]
+        out = (torch.sign(p) * ((p.abs() + 127) >> 8)).clamp_(-32768, 32767)
+        return torch.where(((td == tb) | (td == 0))[..., None], mv, out)
 
-    def _store_col(self, slot: int):
+    def _store_col(self, slot: int, pic=None):
         """A reference picture just coded may become the collocated picture of later B
         pictures: its records at each 16x16 block's top-left granule (z-order granules
         0 / 4 / 8 / 12), kept per DPB slot."""
@@ -464,6 +501,12 @@ class GpuHevcEncoder:
         self.col_dir[slot].copy_(torch.where(inter, torch.where(d == 0, torch.ones_like(d), d), torch.zeros_like(d)))
         self.col_mv0[slot].copy_(rec[..., 4:8].contiguous().view(torch.int16).to(torch.int32))
         self.col_mv1[slot].copy_(rec[..., 8:12].contiguous().view(torch.int16).to(torch.int32))
+        self.col_td0[slot] = None
+        if pic is not None and len(pic.refs0) > 1:
+            # each block's list-0 POC distance through its refIdx (CuInfo pad[0])
+            lut = torch.tensor([pic.d - r for r in pic.refs0] + [pic.d - pic.refs0[0]] * (4 - len(pic.refs0)),
+                               dtype=torch.int32, device=self.dev)
+            self.col_td0[slot] = lut[rec[..., 13].long().clamp_(0, 3)]
 
     def _temporal_candidates(self, pic, col_refs: tuple):
         """See _temporal_for; B pictures: the collocated picture is RefPicList1[0]."""
@@ -488,6 +531,7 @@ class GpuHevcEncoder:
         br_ok[:, :-1, :-1] = ok[:, 1:, 1:]
         br_mv[:, :-1, :-1] = mv[:, 1:, 1:]
         br_1[:, :-1, :-1] = use1[:, 1:, 1:]
+        ctd0 = self.col_td0[cs]  # per-block list-0 distances of a multi-reference col picture
         # the bottom-right block must lie in the same CTU row (16x16 rows per CTU: 2 or 4)
         rows = 4 if self.p.ctu64 else 2
         even = (torch.arange(self.hmb, device=self.dev) % rows != rows - 1)[None, :, None]
@@ -496,6 +540,10 @@ class GpuHevcEncoder:
         sel1 = torch.where(use_br, br_1, use1)[..., None]
         avail = (use_br | ok).reshape(self.B, self.nmb)
         td0, td1 = col - col_refs[0], col - col_refs[1]   # the col block's own POC distance per list
+        if ctd0 is not None:
+            br_td = torch.zeros_like(ctd0)
+            br_td[:, :-1, :-1] = ctd0[:, 1:, 1:]
+            td0 = torch.where(use_br, br_td, ctd0)
         for x, tgt in enumerate(targets):
             if tgt < 0:
                 self.tmv[..., 2 * x:2 * x + 2].zero_()
@@ -555,8 +603,9 @@ class GpuHevcEncoder:
 
     def _plan(self, F: int, cuts_h: np.ndarray, anchors_at) -> list:
         from .gop import GopPic, hevc_gop_plan
-        if self.nb:
-            return hevc_gop_plan(F, self.nb, self.p.pyramid, set(anchors_at) | {d for d in range(1, F) if cuts_h[:, d].any()})
+        if self.nb or self.nrefs > 1:
+            return hevc_gop_plan(F, self.nb, self.p.pyramid, set(anchors_at) | {d for d in range(1, F) if cuts_h[:, d].any()},
+                                 ref_slots=self.ref_slots, refs=self.nrefs)
         out = []
         for t in range(F):
             idr = t == 0 or self.p.intra_only or (self.p.keyint > 0 and t % self.p.keyint == 0)
@@ -731,6 +780,24 @@ class GpuHevcEncoder:
                         self.hip.me(B, self.wmb, self.hmb, s8, p(ref8), p(self.prev_mv), p(self.mv),
                                     p(self.me_cost), p(self.me_pred), p(self.me_intra), p(self.qp), self.p.me_range,
                                     self.p.subpel, s, p(hp), p(self.mb_aq), 1)
+                    nr = len(pic.refs0) if self.nrefs > 1 else 1
+                    far = {}
+                    if nr > 1:
+                        # x265 --ref: the farther list-0 pictures, 16x16 searches seeded by the list-0[0]
+                        # vectors scaled by the temporal distances (unweighted source: explicit
+                        # weights belong to RefPicList0[0]), skipped where list-0[0] is good enough
+                        sk = pic.srefs0[1:]
+                        with st("me_ref"):
+                            for k in range(1, nr):
+                                scale = (pic.d - pic.refs0[k]) / float(pic.d - pic.refs0[0])
+                                self.xpm[k - 1].copy_((self.mv.float() * scale).round_().clamp_(-2048, 2047))
+                                self.hip.me(B, self.wmb, self.hmb, p(self.src8), p(self.ref8s[sk[k - 1]]),
+                                            p(self.xpm[k - 1]), p(self.xmv[k - 1]), p(self.xcost[k - 1]), p(self.xpred),
+                                            0, p(self.qp), int(self.p.ref_range), self.p.subpel, s,
+                                            p(self.me_hps[sk[k - 1]]), p(self.mb_aq), 1, gate_cost=p(self.me_cost),
+                                            gate_thresh=int(self.p.ref_gate))
+                        far = dict(nref0=nr, xref=[p(self.ref8s[k]) for k in sk], xhp=[p(self.me_hps[k]) for k in sk])
+                        inter_kw["xref"] = [p(c) for k in sk for c in self.rec[k]]
                     with st("merge_refine"):
                         if self.p.merge_exact:
                             # the search as list-0 motion, then the writer-exact merge passes
@@ -740,21 +807,24 @@ class GpuHevcEncoder:
                                 self._temporal_for(pic, r0, pic.l0, ref_lists[pic.l0], (pic.l0, -1))
                                 tm_, td_ = p(self.tmv), p(self.tdir)
                             pargs = (B, self.wmb, self.hmb, s8, p(ref8), p(ref8), p(hp), p(hp))
+                            xs = dict(xmv=p(self.xmv), xcost=p(self.xcost), xpm=p(self.xpm)) if far else {}
                             self.hip.hevc_b(2, *pargs, p(self.mv), 0, p(self.me_cost), 0, p(self.prev_mv), 0, 0, 0, 0, 0,
                                             p(self.mvb[0]), p(self.dirb[0]), p(self.bcost), p(self.bbits), p(self.qp),
-                                            p(self.mb_aq), s, 0, int(self.p.max_merge), int(self.p.ctu64))
+                                            p(self.mb_aq), s, 0, int(self.p.max_merge), int(self.p.ctu64), **far, **xs)
                             for it in range(int(self.p.merge_refine)):
                                 i_, o_ = it % 2, (it + 1) % 2
                                 self.hip.hevc_b(1, *pargs, 0, 0, 0, 0, 0, 0, tm_, td_, p(self.mvb[i_]), p(self.dirb[i_]),
                                                 p(self.mvb[o_]), p(self.dirb[o_]), p(self.bcost), p(self.bbits),
                                                 p(self.qp), p(self.mb_aq), s, 0, int(self.p.max_merge), int(self.p.ctu64),
-                                                *self._chg_args(it))
+                                                *self._chg_args(it), **far)
                             fin = int(self.p.merge_refine) % 2
                             self.me_cost.copy_(self.bcost)
                             self.mv.copy_(self.mvb[fin][..., 0:2])
                             inter_kw.update(mvb=p(self.mvb[fin]), dirb=p(self.dirb[fin]), f1y=p(ref[0]), f1u=p(ref[1]),
                                             f1v=p(ref[2]))
                         else:
+                            if far:
+                                raise ValueError("HevcParams.refs > 1 needs merge_exact")
                             for it in range(int(self.p.merge_refine)):
                                 a_, b_ = (self.mv, self.mv_tmp) if it % 2 == 0 else (self.mv_tmp, self.mv)
                                 self.hip.hevc_merge_refine(B, self.wmb, self.hmb, s8, p(ref8), p(hp), p(a_),
@@ -834,8 +904,9 @@ class GpuHevcEncoder:
                 if tmvp:
                     if idr:
                         self.col_dir[ci].zero_()
+                        self.col_td0[ci] = None
                     else:
-                        self._store_col(ci)
+                        self._store_col(ci, pic)
             if metrics:
                 dd = (cur[0][:, :h, :w].to(torch.int32) - self.src[0][:, :h, :w].to(torch.int32))
                 sse.append((dd * dd).sum(dim=(1, 2)).to(torch.float64))
@@ -880,6 +951,8 @@ class GpuHevcEncoder:
                             nal_ref=int(pic.ref), rps=[(rd - i0, int(u)) for rd, u in pic.rps])
                 if pic.kind != "I":
                     base["ref_poc0"] = pic.l0 - i0
+                    if len(pic.refs0) > 1:
+                        base["refs0"] = [r - i0 for r in pic.refs0]
                 if pic.kind == "B":
                     base["ref_poc1"] = pic.l1 - i0
                 col = None
@@ -887,6 +960,8 @@ class GpuHevcEncoder:
                     cd = pic.l1 if pic.kind == "B" else pic.l0
                     col = anchor_cu[cd]
                     base.update(col_poc=cd - i0, col_ref_poc0=col[1] - i0, col_ref_poc1=col[2] - i0)
+                    if len(col[3]) > 1:
+                        base["col_refs0"] = [r - i0 for r in col[3]]
                 fps = []
                 for b in range(B):
                     fp = dict(base, qp=int(qcol[b]))
@@ -907,7 +982,7 @@ class GpuHevcEncoder:
                 if tmvp and pic.ref:
                     # later pictures' collocated records (the host buffer set is reused at t + 3);
                     # only pictures still in the DPB can be collocated pictures
-                    anchor_cu[pic.d] = (None if pic.kind == "I" else cu[:B].copy(), pic.l0, pic.l1)
+                    anchor_cu[pic.d] = (None if pic.kind == "I" else cu[:B].copy(), pic.l0, pic.l1, pic.refs0)
                     live = {rd for rd, _ in pic.rps} | {pic.d}
                     for k in [k for k in anchor_cu if k not in live]:
                         del anchor_cu[k]

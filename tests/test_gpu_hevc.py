@@ -384,3 +384,35 @@ def test_gpu_hevc_ctb32_config4_shape(host):
     _compare(host, [res[b] for b in pick], [tuple(plane[pick] for plane in t) for t in rec])
     for r in res:
         assert r.frames == 8 and len(r.bitstream) > 0
+
+
+@pytest.mark.parametrize("bframes,kind,ctu64", [(0, 0, True), (1, 0, False), (1, "fade", True)])
+def test_gpu_hevc_multiref_matches_decoder(host, bframes, kind, ctu64):
+    """x265 --ref 3: P pictures search their farther list-0 pictures (scaled-vector seeds), pick
+    per block at cost + ref_idx bins, and the merge passes carry candidates' refIdx (zero
+    candidates counting through the list); motion compensation, deblocking (refIdx in the
+    boundary strength), TMVP from multi-reference collocated pictures and explicit weights on
+    RefPicList0[0] only (fade) -- bit-exact with the CPU decoder.  Content that repeats every
+    second anchor makes the farther pictures win, so refIdx > 0 must occur."""
+    from govideocompressor_amd.models.h264_gpu import synth_clip
+    from govideocompressor_amd.models.hevc_gpu import GpuHevcEncoder, HevcParams
+    w, h, F, B = 160, 96, 8, 3
+    y, u, v = synth_clip(B, F, w, h, seed=9, kind=kind)
+    # anchors of equal content every other anchor: d -> source frame
+    step = bframes + 1
+    perm = [d if d % step else (0 if (d // step) % 2 == 0 else step) for d in range(F)]
+    idx = torch.tensor(perm, device=y.device)
+    y, u, v = (t.index_select(1, idx).contiguous() for t in (y, u, v))
+    enc = GpuHevcEncoder(HevcParams(width=w, height=h, crf=28, bframes=bframes, refs=3, ref_gate=0, ctu64=ctu64),
+                         slots=B)
+    res = enc.encode(y, u, v, keep_recon=True)
+    rec = enc.last_recon
+    enc.close()
+    _compare(host, res, rec)
+    far = 0
+    for r in res:
+        for p in host.hevc_decode(r.bitstream):
+            if p["slice_type"] == 1:
+                cu = p["cu"]
+                far += int(((cu[:, 0] == 1) & (cu[:, 13] > 0)).sum())
+    assert far > 0
