@@ -64,6 +64,10 @@ HEVC = {
     "MIVC_HEVC_CTU64": "ctu64",
     "MIVC_HEVC_LA_WEIGHTS": "la_weights",
     "MIVC_HEVC_MERGE_SKIP": "merge_skip",
+    "MIVC_HEVC_REFS": "refs",
+    "MIVC_HEVC_REF_GATE": "ref_gate",
+    "MIVC_HEVC_REF_RANGE": "ref_range",
+    "MIVC_HEVC_BFRAMES": "bframes",
 }
 # bench.py shape knobs (they change what is measured, so they also need --allow-knobs)
 # (MIVC_HIP_LIB: an alternative kernel library, tools/build_variant.py -- same-box A/B timing)

@@ -31,7 +31,8 @@ CTUs, as x265), fast and medium the defaults (3
 merge candidates, as x265), slow and slower radius 12 (slower 4 candidates), veryslow/placebo
 radius 16 and 5 candidates;
 slow and slower presets add the inter residual quadtree (--tu-inter-depth 1), veryslow and
-placebo also sign data hiding (--signhide).
+placebo also sign data hiding (--signhide); --ref follows x265 (1 up to superfast, 2 for
+veryfast / faster, 3 for fast / medium, 4 from slow).
 """
 from __future__ import annotations
 
@@ -64,16 +65,17 @@ H264 = {
 }
 H264["placebo"] = H264["veryslow"]
 
+# --ref as x265's presets (1 / 1 / 2 / 2 / 3 / 3 / 4 / 5 / 5: capped at 4 list-0 pictures here)
 HEVC = {
-    "ultrafast": dict(me_range=4, subpel=1, max_merge=3, la_range=4, ctu64=False),
-    "superfast": dict(me_range=4, subpel=1, max_merge=3, la_range=4, ctu64=False),
-    "veryfast": dict(me_range=4, subpel=2, max_merge=3),
-    "faster": dict(me_range=8, max_merge=3),
+    "ultrafast": dict(me_range=4, subpel=1, max_merge=3, la_range=4, ctu64=False, refs=1),
+    "superfast": dict(me_range=4, subpel=1, max_merge=3, la_range=4, ctu64=False, refs=1),
+    "veryfast": dict(me_range=4, subpel=2, max_merge=3, refs=2),
+    "faster": dict(me_range=8, max_merge=3, refs=2),
     "fast": dict(me_range=8),
     "medium": dict(),
-    "slow": dict(me_range=12, tu_inter_depth=1),
-    "slower": dict(me_range=12, la_range=8, tu_inter_depth=1, max_merge=4),
-    "veryslow": dict(me_range=16, la_range=8, tu_inter_depth=1, sdh=True, max_merge=5),
+    "slow": dict(me_range=12, tu_inter_depth=1, refs=4),
+    "slower": dict(me_range=12, la_range=8, tu_inter_depth=1, max_merge=4, refs=4),
+    "veryslow": dict(me_range=16, la_range=8, tu_inter_depth=1, sdh=True, max_merge=5, refs=4),
 }
 HEVC["placebo"] = HEVC["veryslow"]
 

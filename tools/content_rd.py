@@ -96,6 +96,12 @@ HEVC_CONFIGS = {
     "bqp6": dict(b_qp_offset=6),
     "bqp4": dict(b_qp_offset=4),
     "bqp8": dict(b_qp_offset=8),
+    # x265 --ref (round 6): farther list-0 pictures of P pictures, gated / ungated searches
+    "ref2": dict(refs=2),
+    "ref3": dict(refs=3),
+    "ref3g0": dict(refs=3, ref_gate=0),
+    "ref3g1500": dict(refs=3, ref_gate=1500),
+    "ref3g6000": dict(refs=3, ref_gate=6000),
 }
 
 
