@@ -1805,6 +1805,11 @@ struct PPartArgs {
   int min_satd;         // 16x16 SATD at or below this: no split search
   const SlotRoute* rt;  // routed (route.h): ref / hp are pools, P slots' RefPicList0[0]
   int nbuf;
+  // HEVC 8x8 inter CUs (x265's minimum CU): the 16x16 cost is the merge passes' (SATD +
+  // lambda * bits16, merge-aware), so it is compared as it stands; only blocks whose motion is
+  // RefPicList0[0] list-0 (dir16 == 1) may split; pred is not rewritten (may be null)
+  const int* bits16;
+  const uint8_t* dir16;
 };
 
 __device__ __forceinline__ void med_pred(int ax, int ay, bool ha, int bx, int by, bool hb, int cx, int cy, bool hc,
@@ -1839,10 +1844,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
   const int lambda = h264::kLambda[qp];
   const int pmx = a.pm ? a.pm[o * 2] : 0, pmy = a.pm ? a.pm[o * 2 + 1] : 0;
   const int cost_in = a.cost[o];
-  const int satd16 = cost_in - lambda * (mvbits_se(vx - pmx) + mvbits_se(vy - pmy));
+  const int satd16 = a.bits16 ? cost_in - lambda * a.bits16[o] : cost_in - lambda * (mvbits_se(vx - pmx) + mvbits_se(vy - pmy));
   int16_t* m8 = a.mv8 + o * 8;
   const uint32_t vw = (static_cast<uint32_t>(vx) & 0xFFFFu) | (static_cast<uint32_t>(vy) << 16);
-  if (satd16 <= a.min_satd) {
+  if (satd16 <= a.min_satd || (a.dir16 && a.dir16[o] != 1)) {
     if (lane == 0) *reinterpret_cast<uint4*>(m8) = make_uint4(vw, vw, vw, vw);
     return;
   }
@@ -1958,11 +1963,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
   const int bits8 = mvbits_se(qx[0] - p0x) + mvbits_se(qy[0] - p0y) + mvbits_se(qx[1] - p1x) + mvbits_se(qy[1] - p1y) +
                     mvbits_se(qx[2] - p2x) + mvbits_se(qy[2] - p2y) + mvbits_se(qx[3] - p3x) + mvbits_se(qy[3] - p3y);
   const int cost8 = qs[0] + qs[1] + qs[2] + qs[3] + lambda * (bits8 + a.overhead);
-  const int cost16 = satd16 + lambda * (mvbits_se(vx - p16x) + mvbits_se(vy - p16y));
+  const int cost16 = a.bits16 ? cost_in : satd16 + lambda * (mvbits_se(vx - p16x) + mvbits_se(vy - p16y));
   const bool uniform = qx[0] == qx[1] && qx[0] == qx[2] && qx[0] == qx[3] && qy[0] == qy[1] && qy[0] == qy[2] &&
                        qy[0] == qy[3];
   const bool split = !uniform && cost8 < cost16;
-  if (split) {
+  if (split && a.pred) {
     // lane (q, blk, c) rewrites row c of its block
     const uint32_t p = mc4(G0, H0, W, H, X, Y + c, bvx, bvy);
     const int lx = (q & 1) * 8 + (blk & 1) * 4, ly = (q >> 1) * 8 + (blk >> 1) * 4 + c;
@@ -2089,8 +2094,11 @@ extern "C" void mivc_launch_p_refine(int B, int wmb, int hmb, const uint8_t* src
 extern "C" void mivc_launch_p_part8(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref,
                                     const uint8_t* hp, const int16_t* mv, const int16_t* pm, int* cost, uint8_t* pred,
                                     int16_t* mv8, const int* qp, const int8_t* aq, int overhead, int min_satd,
-                                    void* stream, const void* route, int nbuf) {
+                                    void* stream, const void* route, int nbuf, const int* bits16,
+                                    const uint8_t* dir16) {
   PPartArgs a;
+  a.bits16 = bits16;
+  a.dir16 = dir16;
   a.rt = static_cast<const SlotRoute*>(route);
   a.nbuf = nbuf;
   a.g = Geom{B, wmb, hmb, wmb * 16, hmb * 16};

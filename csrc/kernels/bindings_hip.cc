@@ -80,7 +80,8 @@ void mivc_launch_wp_stats(const uint8_t* y, const uint8_t* u, const uint8_t* v, 
 void mivc_launch_wp_src(const uint8_t* src, uint8_t* dst, const int* wt, int B, long long plane_bytes, void* stream);
 void mivc_launch_p_part8(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref, const uint8_t* hp,
                          const int16_t* mv, const int16_t* pm, int* cost, uint8_t* pred, int16_t* mv8, const int* qp,
-                         const int8_t* aq, int overhead, int min_satd, void* stream, const void* route, int nbuf);
+                         const int8_t* aq, int overhead, int min_satd, void* stream, const void* route, int nbuf,
+                         const int* bits16, const uint8_t* dir16);
 void mivc_launch_encode_intra(int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* src_u,
                               const uint8_t* src_v, uint8_t* rec_y, uint8_t* rec_u, uint8_t* rec_v, const int* qp,
                               int chroma_qp_offset, void* hdr, int16_t* coef, uint8_t* nz,
@@ -112,7 +113,7 @@ void mivc_launch_hevc_inter(int B, int W, int H, const uint16_t* sy, const uint1
                             const int8_t* run, const int* cand, const int16_t* mv, const int* me_cost, int bd,
                             int tu_split, int sdh, int intra_bias, void* stream, const int16_t* mvb,
                             const uint8_t* dirb, const uint16_t* f1y, const uint16_t* f1u, const uint16_t* f1v,
-                            const int16_t* wp, const uint16_t* const* xref);
+                            const int16_t* wp, const uint16_t* const* xref, const int16_t* mv8);
 void mivc_launch_hevc_b(int mode, int B, int wmb, int hmb, const uint8_t* src_y, const uint8_t* ref0, const uint8_t* ref1,
                         const uint8_t* hp0, const uint8_t* hp1, const int16_t* mv0, const int16_t* mv1, const int* cost0,
                         const int* cost1, const int16_t* pm0, const int16_t* pm1, const int16_t* tmv, const uint8_t* tdir,
@@ -409,14 +410,16 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("p_part8", [](int B, int wmb, int hmb, uintptr_t src, uintptr_t ref, uintptr_t hp, uintptr_t mv, uintptr_t pm,
                       uintptr_t cost, uintptr_t pred, uintptr_t mv8, uintptr_t qp, uintptr_t aq, int overhead,
-                      int min_satd, uintptr_t stream, uintptr_t route, int nbuf) {
+                      int min_satd, uintptr_t stream, uintptr_t route, int nbuf, uintptr_t bits16, uintptr_t dir16) {
     if (!hp || !mv8) throw std::invalid_argument("p_part8: needs the half-sample planes and an mv8 buffer");
+    if (!pred && !bits16) throw std::invalid_argument("p_part8: the H.264 form rewrites pred");
     mivc_launch_p_part8(B, wmb, hmb, P<uint8_t>(src), P<uint8_t>(ref), P<uint8_t>(hp), P<int16_t>(mv), P<int16_t>(pm),
                         P<int>(cost), P<uint8_t>(pred), P<int16_t>(mv8), P<int>(qp), P<int8_t>(aq), overhead, min_satd,
-                        S(stream), P<void>(route), nbuf);
+                        S(stream), P<void>(route), nbuf, P<int>(bits16), P<uint8_t>(dir16));
   }, py::arg("B"), py::arg("wmb"), py::arg("hmb"), py::arg("src"), py::arg("ref"), py::arg("hp"), py::arg("mv"),
      py::arg("pm"), py::arg("cost"), py::arg("pred"), py::arg("mv8"), py::arg("qp"), py::arg("aq"), py::arg("overhead"),
-     py::arg("min_satd"), py::arg("stream"), py::arg("route") = 0, py::arg("nbuf") = 0);
+     py::arg("min_satd"), py::arg("stream"), py::arg("route") = 0, py::arg("nbuf") = 0, py::arg("bits16") = 0,
+     py::arg("dir16") = 0);
   m.def("encode_intra", [](int B, int wmb, int hmb, uintptr_t sy, uintptr_t su, uintptr_t sv, uintptr_t ry,
                            uintptr_t ru, uintptr_t rv, uintptr_t qp, int cqo, uintptr_t hdr, uintptr_t coef,
                            uintptr_t nz, uintptr_t intra_flag, uintptr_t intra_count, uintptr_t err, int use_i4x4,
@@ -497,7 +500,7 @@ PYBIND11_MODULE(_hip, m) {
                          uintptr_t cu_, uintptr_t cv, uintptr_t qp, uintptr_t run, uintptr_t cand, uintptr_t mv,
                          uintptr_t me_cost, int bd, uintptr_t stream, int tu_split, int sdh, int intra_bias,
                          uintptr_t mvb, uintptr_t dirb, uintptr_t f1y, uintptr_t f1u, uintptr_t f1v, uintptr_t wp,
-                         std::vector<uintptr_t> xref) {
+                         std::vector<uintptr_t> xref, uintptr_t mv8) {
     if (dirb && (!mvb || !f1y || !f1u || !f1v)) throw std::invalid_argument("hevc_inter: B motion needs mvb and list-1 planes");
     // xref: (y, u, v) of RefPicList0[1 ..] (x265 --ref), at most 3 pictures
     if (xref.size() % 3 || xref.size() > 9) throw std::invalid_argument("hevc_inter: xref = (y, u, v) x up to 3 pictures");
@@ -507,13 +510,14 @@ PYBIND11_MODULE(_hip, m) {
                            P<uint16_t>(fv), P<uint16_t>(ry), P<uint16_t>(ru), P<uint16_t>(rv), P<void>(ctu), P<void>(cu),
                            P<int16_t>(cy), P<int16_t>(cu_), P<int16_t>(cv), P<int>(qp), P<int8_t>(run), P<int>(cand),
                            P<int16_t>(mv), P<int>(me_cost), bd, tu_split, sdh, intra_bias, S(stream), P<int16_t>(mvb),
-                           P<uint8_t>(dirb), P<uint16_t>(f1y), P<uint16_t>(f1u), P<uint16_t>(f1v), P<int16_t>(wp), xr);
+                           P<uint8_t>(dirb), P<uint16_t>(f1y), P<uint16_t>(f1u), P<uint16_t>(f1v), P<int16_t>(wp), xr,
+                           P<int16_t>(mv8));
   }, py::arg("B"), py::arg("W"), py::arg("H"), py::arg("sy"), py::arg("su"), py::arg("sv"), py::arg("fy"), py::arg("fu"),
      py::arg("fv"), py::arg("ry"), py::arg("ru"), py::arg("rv"), py::arg("ctu"), py::arg("cu"), py::arg("cy"),
      py::arg("cu_"), py::arg("cv"), py::arg("qp"), py::arg("run"), py::arg("cand"), py::arg("mv"), py::arg("me_cost"),
      py::arg("bd"), py::arg("stream"), py::arg("tu_split") = 0, py::arg("sdh") = 0, py::arg("intra_bias") = 0,
      py::arg("mvb") = 0, py::arg("dirb") = 0, py::arg("f1y") = 0, py::arg("f1u") = 0, py::arg("f1v") = 0,
-     py::arg("wp") = 0, py::arg("xref") = std::vector<uintptr_t>{});
+     py::arg("wp") = 0, py::arg("xref") = std::vector<uintptr_t>{}, py::arg("mv8") = 0);
   m.def("hevc_b", [](int mode, int B, int wmb, int hmb, uintptr_t src, uintptr_t ref0, uintptr_t ref1, uintptr_t hp0,
                      uintptr_t hp1, uintptr_t mv0, uintptr_t mv1, uintptr_t cost0, uintptr_t cost1, uintptr_t pm0,
                      uintptr_t pm1, uintptr_t tmv, uintptr_t tdir, uintptr_t mvb_in, uintptr_t dir_in, uintptr_t mvb_out,

@@ -50,6 +50,9 @@ struct HevcInterArgs {
   // dirb carries its list-0 refIdx in bits 2-3; the CU records take it in pad[0]); explicit
   // weights apply to RefPicList0[0] only
   const uint16_t *xref_y[3], *xref_u[3], *xref_v[3];
+  // 8x8 inter CUs (P pictures, x265's minimum CU): [B, nmb16, 4, 2] per-quadrant vectors of
+  // each 16x16 block (p_part8x8 in its HEVC form; all equal = no split); null: 16x16 / 32x32 only
+  const int16_t* mv8;
 };
 
 // plane c of RefPicList0[r] (constant indices only: no scratch)
@@ -76,7 +79,8 @@ __global__ __launch_bounds__(64) void hevc_p_decide(HevcInterArgs a) {
   const int wmb = g.W / 16, nmb = wmb * (g.H / 16);
   const int qp = a.qp[cb];
   const int lam = lambda_satd_i(qp, a.bd);
-  __shared__ int s_inter[4], s_mvx[4], s_mvy[4], s_mv1x[4], s_mv1y[4], s_dir[4], s_split8[4], s_intra[4];
+  __shared__ int s_inter[4], s_mvx[4], s_mvy[4], s_mv1x[4], s_mv1y[4], s_dir[4], s_split8[4], s_intra[4], s_isplit[4];
+  __shared__ uint32_t s_mv8[4][4];
   __shared__ int s_split;
   if (lane < 4) {
     const int q = lane;
@@ -102,6 +106,14 @@ __global__ __launch_bounds__(64) void hevc_p_decide(HevcInterArgs a) {
       s_mv1x[q] = s_mv1y[q] = 0;
       s_dir[q] = hevc::DIR_L0;
     }
+    // an inter quadrant split into four 8x8 inter CUs: RefPicList0[0] list-0 motion whose four
+    // quadrant vectors differ
+    s_isplit[q] = 0;
+    if (a.mv8 && s_dir[q] == hevc::DIR_L0) {
+      const uint32_t* m8 = reinterpret_cast<const uint32_t*>(a.mv8 + o * 8);
+      for (int k = 0; k < 4; ++k) s_mv8[q][k] = m8[k];
+      s_isplit[q] = m8[0] != m8[1] || m8[0] != m8[2] || m8[0] != m8[3];
+    }
   }
   __syncthreads();
   if (lane == 0) {
@@ -119,14 +131,15 @@ __global__ __launch_bounds__(64) void hevc_p_decide(HevcInterArgs a) {
       for (int q = 0; q < 4; ++q) split |= (split & 1) && s_split8[q] ? 1 << (1 + q) : 0;
       for (int q = 0; q < 4; ++q) s_inter[q] = 0x7FFFFFFF;  // mark intra
     } else {
-      bool same = n_inter == 4;
+      bool same = n_inter == 4 && !s_isplit[0];
       for (int q = 1; q < 4; ++q)
         same = same && s_dir[q] == s_dir[0] && s_mvx[q] == s_mvx[0] && s_mvy[q] == s_mvy[0] && s_mv1x[q] == s_mv1x[0] &&
-               s_mv1y[q] == s_mv1y[0];
+               s_mv1y[q] == s_mv1y[0] && !s_isplit[q];
       split = same ? 0 : 1;
       for (int q = 0; q < 4; ++q) {
         const bool inter = s_inter[q] < s_intra[q];
         if (!inter && s_split8[q]) split |= 1 << (1 + q);
+        if (inter && s_isplit[q]) split |= 1 << (1 + q);
         if (!inter) s_inter[q] = 0x7FFFFFFF;
       }
     }
@@ -150,6 +163,11 @@ __global__ __launch_bounds__(64) void hevc_p_decide(HevcInterArgs a) {
       c.pred = hevc::CU_INTER;
       c.mv[0] = static_cast<int16_t>(s_mvx[q]);
       c.mv[1] = static_cast<int16_t>(s_mvy[q]);
+      if (lg == 3) {  // an 8x8 inter CU: its quadrant's vector of the 16x16 block
+        const uint32_t w = s_mv8[q][(gx & 1) | ((gy & 1) << 1)];
+        c.mv[0] = static_cast<int16_t>(w & 0xFFFFu);
+        c.mv[1] = static_cast<int16_t>(w >> 16);
+      }
       c.mv1[0] = static_cast<int16_t>(s_mv1x[q]);
       c.mv1[1] = static_cast<int16_t>(s_mv1y[q]);
       c.dir = static_cast<uint8_t>(s_dir[q] & 3);
@@ -335,22 +353,26 @@ __global__ __launch_bounds__(64) void hevc_inter_cu(HevcInterArgs a) {
   const int lg = 3 + ((cu[kq].flags >> 1) & 3);
   if (pred != hevc::CU_INTER) return;
   if (lg == 5 && q != 0) return;  // the 32x32 CU is handled by quadrant 0
-  if (lg == 3) return;            // inter CUs are 16x16 or 32x32
   hv::dct_lds_init(D);
   __syncthreads();
   const int lane = lane_id();
   const int n = 1 << lg;
   const int rx = ci % g.wctb, ry = ci / g.wctb;
-  const int X0 = rx * 32 + (lg == 5 ? 0 : (q & 1) * 16), Y0 = ry * 32 + (lg == 5 ? 0 : (q >> 1) * 16);
-  const int mvx = cu[kq].mv[0], mvy = cu[kq].mv[1], mv1x = cu[kq].mv1[0], mv1y = cu[kq].mv1[1];
-  const int dir = hevc::cu_dir(cu[kq]);
-  const int r0 = cu[kq].pad[0] & 3;  // list-0 refIdx
   const int bd = a.bd, maxv = (1 << bd) - 1;
   const int qpy = a.qp[cb], off = 6 * (bd - 8);
   const int qpl = qpy + off, qpc = hevc::chroma_qp_map(clampi(qpy, -off, 57)) + off;
+  // a quadrant split into 8x8 inter CUs (x265's minimum CU) codes them one after another
+  const int ncu = lg == 3 ? 4 : 1;
+  for (int j = 0; j < ncu; ++j) {
+  const int kc = kq + j;  // the CU's first granule (z-order)
+  const int X0 = rx * 32 + (lg == 5 ? 0 : (q & 1) * 16 + (lg == 3 ? (j & 1) * 8 : 0));
+  const int Y0 = ry * 32 + (lg == 5 ? 0 : (q >> 1) * 16 + (lg == 3 ? (j >> 1) * 8 : 0));
+  const int mvx = cu[kc].mv[0], mvy = cu[kc].mv[1], mv1x = cu[kc].mv1[0], mv1y = cu[kc].mv1[1];
+  const int dir = hevc::cu_dir(cu[kc]);
+  const int r0 = cu[kc].pad[0] & 3;  // list-0 refIdx
   // residual quadtree: the luma residual is transformed both as one TU and as four quarter
   // TUs; the cheaper by SSD + lambda * (level-bit proxy + TU overhead) wins, and chroma
-  // follows the chosen structure (max_transform_hierarchy_depth_inter 1)
+  // follows the chosen structure (max_transform_hierarchy_depth_inter 1; 16x16+ CUs)
   int cbfq[4] = {0, 0, 0, 0};  // per quarter: bit c = component c has levels in that quarter's TU
   bool split = false;
   const int h = n >> 1;
@@ -378,6 +400,7 @@ __global__ __launch_bounds__(64) void hevc_inter_cu(HevcInterArgs a) {
     const int qc = c ? qpc : qpl;
     bool coded = false;
     if constexpr (TSPLIT) {
+      if (lg >= 4) {
       coded = c == 0 || split;
       if (c == 0) {
         const bool nz = hv::transform_quant_block(D, S.R, S.S, lev, pw, hv::TqParams{l2, bd, qc, false, false, a.sdh ? 0 : -1});
@@ -417,6 +440,7 @@ __global__ __launch_bounds__(64) void hevc_inter_cu(HevcInterArgs a) {
           cbfq[k] |= nz << c;
         }
       }
+      }
     }
     if (!coded) {
       const bool nz = hv::transform_quant_block(D, S.R, S.S, lev, pw, hv::TqParams{l2, bd, qc, false, false, a.sdh ? 0 : -1});
@@ -431,11 +455,12 @@ __global__ __launch_bounds__(64) void hevc_inter_cu(HevcInterArgs a) {
     wave_sync();
   }
   // granule records: split flag; cbf = that of the TU covering the granule
-  const int ng = lg == 5 ? 16 : 4;
+  const int ng = lg == 5 ? 16 : (lg == 4 ? 4 : 1);
   if (lane < ng) {
     const int k = lg == 5 ? lane >> 2 : lane;  // z-order: the quarter of a 32x32 CU holds 4 granules
-    cu[kq + lane].cbf = static_cast<uint8_t>(split ? cbfq[k] : cbfq[0]);
-    if (split) cu[kq + lane].flags |= 16;
+    cu[kc + lane].cbf = static_cast<uint8_t>(split ? cbfq[k] : cbfq[0]);
+    if (split) cu[kc + lane].flags |= 16;
+  }
   }
 }
 
@@ -451,9 +476,10 @@ extern "C" void mivc_launch_hevc_inter(int B, int W, int H, const uint16_t* sy, 
                                        const int16_t* mv, const int* me_cost, int bd, int tu_split, int sdh,
                                        int intra_bias, void* stream, const int16_t* mvb, const uint8_t* dirb,
                                        const uint16_t* f1y, const uint16_t* f1u, const uint16_t* f1v,
-                                       const int16_t* wp, const uint16_t* const* xref) {
+                                       const int16_t* wp, const uint16_t* const* xref, const int16_t* mv8) {
   HevcInterArgs a;
   a.wp = wp;
+  a.mv8 = mv8;
   for (int r = 0; r < 3; ++r) {  // xref: [3 x (y, u, v)] of RefPicList0[1 ..] (null: list-0[0])
     a.xref_y[r] = xref && xref[3 * r] ? xref[3 * r] : fy;
     a.xref_u[r] = xref && xref[3 * r + 1] ? xref[3 * r + 1] : fu;

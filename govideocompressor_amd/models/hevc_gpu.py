@@ -139,6 +139,14 @@ class HevcParams:
     refs: int = 3
     ref_range: int = 4
     ref_gate: int = 6000
+    # 8x8 inter CUs (x265 searches CUs down to its 8x8 minimum): after the merge passes, each
+    # 16x16 block of a P picture whose motion is RefPicList0[0] searches one vector per 8x8
+    # quadrant (p_part8x8, HEVC form: candidates, half / quarter rings); the four 8x8 CUs win
+    # when their SATD + lambda * (mvd bits + inter8_overhead) beats the merge-aware 16x16 cost.
+    # Blocks at or below inter8_min_satd are not searched.  B pictures keep 16x16 / 32x32 CUs.
+    inter8: bool = False
+    inter8_overhead: int = 16
+    inter8_min_satd: int = 2000
 
     def eff_refs(self) -> int:
         """Active list-0 pictures of P pictures (1 for intra-only and keyint GOPs)."""
@@ -286,6 +294,8 @@ class GpuHevcEncoder:
         # x265 --ref: a collocated P picture whose blocks point at different list-0 pictures keeps
         # each block's list-0 POC distance (None for the slot: every block uses RefPicList0[0])
         self.col_td0 = [None] * R
+        if params.inter8 and not params.intra_only:
+            self.mv8 = torch.zeros((B, nmb, 4, 2), dtype=i16_, device=dev)
         if self.nrefs > 1:
             nx = self.nrefs - 1
             self.xmv = torch.zeros((nx, B, nmb, 2), dtype=i16_, device=dev)    # farther list-0 searches
@@ -824,6 +834,16 @@ class GpuHevcEncoder:
                             self.mv.copy_(self.mvb[fin][..., 0:2])
                             inter_kw.update(mvb=p(self.mvb[fin]), dirb=p(self.dirb[fin]), f1y=p(ref[0]), f1u=p(ref[1]),
                                             f1v=p(ref[2]))
+                            if self.p.inter8:
+                                # 8x8 inter CUs: per-quadrant vectors of RefPicList0[0] blocks, priced
+                                # against the merge-aware 16x16 cost (me_cost updated where they win)
+                                with st("inter8"):
+                                    self.hip.p_part8(B, self.wmb, self.hmb, s8, p(ref8), p(hp), p(self.mv),
+                                                     p(self.prev_mv), p(self.me_cost), 0, p(self.mv8), p(self.qp),
+                                                     p(self.mb_aq), int(self.p.inter8_overhead),
+                                                     int(self.p.inter8_min_satd), s, bits16=p(self.bbits),
+                                                     dir16=p(self.dirb[fin]))
+                                inter_kw["mv8"] = p(self.mv8)
                         else:
                             if far:
                                 raise ValueError("HevcParams.refs > 1 needs merge_exact")

@@ -68,6 +68,8 @@ HEVC = {
     "MIVC_HEVC_REF_GATE": "ref_gate",
     "MIVC_HEVC_REF_RANGE": "ref_range",
     "MIVC_HEVC_BFRAMES": "bframes",
+    "MIVC_HEVC_INTER8": "inter8",
+    "MIVC_HEVC_INTER8_OVERHEAD": "inter8_overhead",
 }
 # bench.py shape knobs (they change what is measured, so they also need --allow-knobs)
 # (MIVC_HIP_LIB: an alternative kernel library, tools/build_variant.py -- same-box A/B timing)

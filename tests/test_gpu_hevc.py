@@ -416,3 +416,21 @@ def test_gpu_hevc_multiref_matches_decoder(host, bframes, kind, ctu64):
                 cu = p["cu"]
                 far += int(((cu[:, 0] == 1) & (cu[:, 13] > 0)).sum())
     assert far > 0
+
+
+@pytest.mark.parametrize("bd,ctu64", [(8, True), (10, False)])
+def test_gpu_hevc_inter8_matches_decoder(host, bd, ctu64):
+    """8x8 inter CUs in P pictures (per-quadrant vectors from the HEVC form of p_part8x8): the
+    split quadrant's four CUs are predicted, transformed (8x8 luma / 4x4 chroma TUs) and
+    reconstructed one after another in hevc_inter_cu, deblocked on the 8x8 grid, and the writer
+    codes them with their own merge / AMVP decisions -- bit-exact with the CPU decoder, and
+    some 8x8 inter CUs must occur (split overhead 0, no SATD floor)."""
+    res, rec = _encode(160, 96, 6, 3, bd=bd, crf=24, bframes=1, ctu64=ctu64, inter8=True, inter8_overhead=0,
+                       inter8_min_satd=0)
+    _compare(host, res, rec)
+    n8 = 0
+    for r in res:
+        for p in host.hevc_decode(r.bitstream):
+            cu = p["cu"]
+            n8 += int(((cu[:, 0] == 1) & (((cu[:, 3] >> 1) & 3) == 0)).sum())
+    assert n8 > 0

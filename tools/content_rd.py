@@ -102,6 +102,11 @@ HEVC_CONFIGS = {
     "ref3g0": dict(refs=3, ref_gate=0),
     "ref3g1500": dict(refs=3, ref_gate=1500),
     "ref3g6000": dict(refs=3, ref_gate=6000),
+    # 8x8 inter CUs in P pictures (round 6), split overhead in bits
+    "i8o8": dict(inter8=True, inter8_overhead=8),
+    "i8o16": dict(inter8=True, inter8_overhead=16),
+    "i8o24": dict(inter8=True, inter8_overhead=24),
+    "i8o16m1000": dict(inter8=True, inter8_overhead=16, inter8_min_satd=1000),
 }
 
 
