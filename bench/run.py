@@ -123,6 +123,17 @@ def config2(args) -> list[dict]:
     return [rec]
 
 
+def transcode_batch(n: int, max_slots: int, min_batches: int = 3) -> int:
+    """Pieces per GPU batch for a rank holding ``n`` pieces: the largest batch <= max_slots that
+    divides ``n`` into >= min_batches equal batches (the parse / decode / encode pipeline of
+    models/transcode.py needs several batches to overlap, and an uneven last batch encodes
+    padding), else the largest divisor of n <= max_slots, else max_slots."""
+    n, max_slots = max(1, int(n)), max(1, int(max_slots))
+    divs = [b for b in range(1, min(n, max_slots) + 1) if n % b == 0]
+    good = [b for b in divs if n // b >= min_batches]
+    return max(good) if good else (max(divs) if divs else max_slots)
+
+
 def config3(args) -> list[dict]:
     """4K30 H.264 (or HEVC) -> H.264, segment-parallel over the ranks of one node: each rank
     (one process per GPU, torch.distributed.run) transcodes its contiguous share of the
@@ -141,9 +152,12 @@ def config3(args) -> list[dict]:
     from govideocompressor_amd.parallel import dist as D
     env = D.init(prefer_gpu=True)
     W, H = (int(x) for x in args.size3.split("x"))
-    F, S, B = args.frames3, args.segments3, args.slots3
+    F, S = args.frames3, args.segments3
     # this rank's contiguous share of the global pieces (rank-major = piece order when merged)
     lo, hi = env.rank * S // env.world, (env.rank + 1) * S // env.world
+    # batches sized from the share: >= 3 per rank (parse / decode / encode overlap), no padded slots
+    B = transcode_batch(hi - lo, args.slots3)
+    threads = args.threads3 or None
     recs = []
     for codec in args.codec3.split(","):
         # untimed: the input pieces (closed GOPs of F frames) made by this framework's
@@ -158,7 +172,7 @@ def config3(args) -> list[dict]:
         mk.close()
         del mk
         torch.cuda.empty_cache()
-        tc = GpuTranscoder(_params(H264Params, width=W, height=H, crf=23.0), slots=B, device=env.device)
+        tc = GpuTranscoder(_params(H264Params, width=W, height=H, crf=23.0), slots=B, device=env.device, threads=threads)
         if args.warmup:
             tc.run(pieces[:B], 30.0)  # warmup batch
         merger = D.SegmentMerge(env)
@@ -193,6 +207,7 @@ def config3(args) -> list[dict]:
             recs.append({"config": 3, "metric": f"transcoded frames/sec (whole node), {args.size3} {codec.upper()}->H.264",
                          "value": round(fps, 2), "unit": "frames/s", "n_gpus": env.world, "frames": S * F,
                          "segments": S, "segments_per_gpu": hi - lo, "segments_per_batch": B,
+                         "batches_per_gpu": -(-(hi - lo) // B), "parse_threads": tc.dec["h264"].threads,
                          "parallelism": f"dp{env.world} (segment-parallel, merged on rank 0)",
                          "wall_s": round(wall, 3), "merged_bytes": int(len(merged)),
                          "encode_only_fps_same_batch_rank0": round(enc_fps, 1) if enc_fps else None,
@@ -368,7 +383,8 @@ def main():
     ap.add_argument("--workers", type=int, default=4)
     ap.add_argument("--frames3", type=int, default=30)
     ap.add_argument("--segments3", type=int, default=256)
-    ap.add_argument("--slots3", type=int, default=64)
+    ap.add_argument("--slots3", type=int, default=64, help="largest transcode batch (sized down per rank share)")
+    ap.add_argument("--threads3", type=int, default=0, help="host parse threads per rank (0: decoder default)")
     ap.add_argument("--codec3", default="h264,hevc")
     ap.add_argument("--size3", default="3840x2160")
     ap.add_argument("--merged-out3", default=None, help="rank 0 writes the merged stream to <path>.<codec>")
