@@ -179,6 +179,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   __shared__ int s_cost[2][2][16];   // [half][0: satd per 4x4 lane, 1: sa8d partial per (b8, k)]
   __shared__ int s_t8[2][3];         // [half][0] use 8x8, [1] keep mask of the 8x8 blocks, [2] 8x8 tried
   __shared__ int s_nz8[2][4][4];     // trellis: [half][b8][chunk] the dead-zone levels are non-zero
+  __shared__ uint32_t s_px[2][2][16][4];  // a.t8: [half][source / prediction][row][dword] luma samples
 
   const int mvx = a.bmode ? 0 : a.mv[o * 2], mvy = a.bmode ? 0 : a.mv[o * 2 + 1];
   const bool go_intra = a.intra_cost[o] < a.me_cost[o];
@@ -245,63 +246,163 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       s_score[half][hl] = decimate_score(scan, 0);
     }
     if (a.t8) {
-      // High profile: an MB whose 4x4 luma levels survive decimation also tries the 8x8
-      // transform -- sa8d of the residual < its satd picks it (x264 analyse), and only then
-      // is it transformed and quantised; MBs without luma residual keep the 4x4 flag-free
-      // coding (transform_size_8x8_flag is not even coded for them)
-      wave_sync();
-      if (hl == 0) {
-        int total = 0, any = 0;
+      // stage this block's source and prediction rows for the 8x8 trial (s_px[half][0 / 1])
 #pragma unroll
-        for (int b8 = 0; b8 < 4; ++b8) {
-          const int sc = s_score[half][b8 * 4] + s_score[half][b8 * 4 + 1] + s_score[half][b8 * 4 + 2] +
-                         s_score[half][b8 * 4 + 3];
-          any |= sc >= 4;
-          total += sc;
-        }
-        s_t8[half][2] = any && total >= 6;
-        s_t8[half][0] = 0;
+      for (int y = 0; y < 4; ++y) {
+        s_px[half][0][lby + y][lbx >> 2] = sw[y];
+        s_px[half][1][lby + y][lbx >> 2] = prw[y];
       }
-      wave_sync();
-      if (s_t8[half][2]) {
+    }
+  } else if (work && hl < 24) {
+    // ---- chroma block: eighth-sample MC (clause 8.4.2.2.2) + residual + forward + AC quant
+    const uint8_t* srcc = (comp == 0 ? a.src_u : a.src_v) + slot * g.csize();
+    const int px0 = mx * 8 + cbx, py0 = my * 8 + cby;
+    int pv[4][4];
+    if (!a.bmode) {
+      // the 4x4 chroma block cb covers luma quadrant cb (its partition's vector)
+      const int cmx = a.mv8 ? a.mv8[o * 8 + cb * 2] : mvx, cmy = a.mv8 ? a.mv8[o * 8 + cb * 2 + 1] : mvy;
+      const int r = a.mref ? a.mref[o] : 0;
+      chroma_mc4x4((comp == 0 ? a.refs_u[r] : a.refs_v[r]) + route_index(a.rt, a.nbuf, slot, RO_L0 + r) * g.csize(), cw,
+                   CH, px0, py0, cmx, cmy, pv);
+      if (a.wp && r == 0) {
+        const int* wt = a.wp + slot * 8;
+        const int w = wt[3 + 2 * comp], wo = wt[4 + 2 * comp], d = wt[7];
+        if (w != (1 << d) || wo != 0) {
+#pragma unroll
+          for (int y = 0; y < 4; ++y)
+#pragma unroll
+            for (int x = 0; x < 4; ++x) pv[y][x] = wp_sample(pv[y][x], w, wo, d);
+        }
+      }
+    } else {
+      // the 4x4 chroma block cb covers luma quadrant cb: its lists and vectors
+      const int r0 = h->ref[0][cb];
+      const bool u0 = r0 >= 0, u1 = h->ref[1][cb] >= 0;
+      const int w1 = a.rt ? a.rt[slot].w1[r0 & 3] : a.w1[r0 & 3];
+      int p1[4][4];
+      if (u0) chroma_mc4x4((comp == 0 ? a.refs_u[r0 & 3] : a.refs_v[r0 & 3]) +
+                               route_index(a.rt, a.nbuf, slot, RO_L0 + (r0 & 3)) * g.csize(), cw, CH, px0, py0,
+                           h->mv[0][cb][0], h->mv[0][cb][1], pv);
+      if (u1) chroma_mc4x4((comp == 0 ? a.ref1_u : a.ref1_v) + route_index(a.rt, a.nbuf, slot, RO_L1) * g.csize(), cw,
+                           CH, px0, py0,
+                           h->mv[1][cb][0], h->mv[1][cb][1], p1);
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int x = 0; x < 4; ++x)  // implicit weights (a.w1 = 32: the plain average)
+          pv[y][x] = u0 ? (u1 ? h264::clip1((pv[y][x] * (64 - w1) + p1[y][x] * w1 + 32) >> 6) : pv[y][x]) : p1[y][x];
+    }
+    uint32_t sw[4];
+#pragma unroll
+    for (int y = 0; y < 4; ++y) sw[y] = *reinterpret_cast<const uint32_t*>(srcc + static_cast<size_t>(py0 + y) * cw + px0);
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+#pragma unroll
+      for (int x = 0; x < 4; ++x) res[y * 4 + x] = static_cast<int>(__builtin_amdgcn_ubfe(sw[y], 8 * x, 8)) - pv[y][x];
+      prw[y] = pack4_u8(pv[y]);
+    }
+    h264::forward_core4x4(res);
+    s_cdc[half][comp][cb] = res[0];
+    const int qbits = 15 + qpc / 6;
+    if (a.trellis >= 2) {  // chroma AC by the same rate-distortion choice, at the chroma QP's lambda
+      trellis_lite4x4(res, lv, mfc, qbits, trellis_lambda4(a.trellis_lambda, qpc), 1);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        lv[r] = r == 0 ? 0 : h264::quant_coef(res[r], mfc[h264::kPosClass[r]], qbits, 11);
+    }
+    int scan[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) scan[i] = lv[h264::kZigzag4x4[i]];
+    s_score[half][hl] = decimate_score(scan, 1);
+  }
+  if (a.t8) {
+    // High profile: an MB whose 4x4 luma levels survive decimation also tries the 8x8
+    // transform -- sa8d of the residual < its satd picks it (x264 analyse), and only then is it
+    // transformed and quantised; MBs without luma residual keep the 4x4 flag-free coding
+    // (transform_size_8x8_flag is not even coded for them).  The whole wave meets here (the
+    // sa8d runs on the matrix cores for both MBs at once).
+    wave_sync();
+    if (hl == 0) {
+      int total = 0, any = 0;
+#pragma unroll
+      for (int b8 = 0; b8 < 4; ++b8) {
+        const int sc = s_score[half][b8 * 4] + s_score[half][b8 * 4 + 1] + s_score[half][b8 * 4 + 2] +
+                       s_score[half][b8 * 4 + 3];
+        any |= sc >= 4;
+        total += sc;
+      }
+      s_t8[half][2] = work && any && total >= 6;
+      s_t8[half][0] = 0;
+      s_t8[half][1] = 0;
+    }
+    wave_sync();
+    const bool try0 = s_t8[0][2], try1 = s_t8[1][2];
+    if (try0 || try1) {  // wave-uniform
+      const bool mine = half ? try1 : try0;
+      if (mine && hl < 16) {
+        // this 4x4 block's residual: the 8x8 transform input (s_d8) and its 4x4 satd
         const int b8 = (lby >> 3) * 2 + (lbx >> 3), ox = lbx & 4, oy = lby & 4;
         int r2[16];
 #pragma unroll
-        for (int y = 0; y < 4; ++y)
+        for (int y = 0; y < 4; ++y) {
+          const uint32_t sv = s_px[half][0][lby + y][lbx >> 2], pv = s_px[half][1][lby + y][lbx >> 2];
 #pragma unroll
           for (int x = 0; x < 4; ++x) {
-            r2[y * 4 + x] = static_cast<int>(__builtin_amdgcn_ubfe(sw[y], 8 * x, 8)) -
-                            static_cast<int>(__builtin_amdgcn_ubfe(prw[y], 8 * x, 8));
-            s_h8[half][b8][(oy + y) * 8 + ox + x] = r2[y * 4 + x];
+            r2[y * 4 + x] = static_cast<int>(__builtin_amdgcn_ubfe(sv, 8 * x, 8)) -
+                            static_cast<int>(__builtin_amdgcn_ubfe(pv, 8 * x, 8));
             s_d8[half][b8][(oy + y) * 8 + ox + x] = r2[y * 4 + x];
           }
-        s_cost[half][0][hl] = h264::satd4x4(r2);
-        wave_sync();
-        const int tb = hl >> 2, k = hl & 3;
-        int* hd = s_h8[half][tb];
-        had8_pass(hd + (2 * k) * 8, 1);
-        had8_pass(hd + (2 * k + 1) * 8, 1);
-        wave_sync();
-        had8_pass(hd + 2 * k, 8);
-        had8_pass(hd + 2 * k + 1, 8);
-        wave_sync();
-        int sa = 0;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sa += abs(hd[k * 16 + i]);
-        s_cost[half][1][hl] = sa;
-        wave_sync();
-        if (hl == 0) {
-          int satd = 0, sa8d = 0;
-#pragma unroll
-          for (int i = 0; i < 16; ++i) satd += s_cost[half][0][i];
-#pragma unroll
-          for (int b = 0; b < 4; ++b)
-            sa8d += (s_cost[half][1][b * 4] + s_cost[half][1][b * 4 + 1] + s_cost[half][1][b * 4 + 2] +
-                     s_cost[half][1][b * 4 + 3] + 2) >> 2;
-          s_t8[half][0] = sa8d < satd;
         }
-        wave_sync();
-        if (s_t8[half][0]) {
+        s_cost[half][0][hl] = h264::satd4x4(r2);
+      }
+      // sa8d of the 8 8x8 blocks (columns 4 * half + b8; columns 8..15 idle) on the int8 matrix
+      // cores: vec(H8 X H8^T) = H64 vec(X) with H64 = H8 (x) H8 (Sylvester: (-1)^popcount(i & k)),
+      // X = S - P split as (S - 128) - (P - 128) so both operands fit int8 (exact)
+      const int col = lane & 15, grp = lane >> 4;
+      mfma_i32x4 sop = {0, 0, 0, 0}, pop = {0, 0, 0, 0};
+      if (col < 8) {
+        const int ch = col >> 2, b8 = col & 3, r0 = (b8 >> 1) * 8 + 2 * grp, c0 = (b8 & 1) * 2;
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) {
+          mfma_i32x4& op = sp ? pop : sop;
+          op[0] = static_cast<int>(s_px[ch][sp][r0][c0] ^ 0x80808080u);
+          op[1] = static_cast<int>(s_px[ch][sp][r0][c0 + 1] ^ 0x80808080u);
+          op[2] = static_cast<int>(s_px[ch][sp][r0 + 1][c0] ^ 0x80808080u);
+          op[3] = static_cast<int>(s_px[ch][sp][r0 + 1][c0 + 1] ^ 0x80808080u);
+        }
+      }
+      // this lane's A rows: H64[16 t + col][16 grp + j] = (-1)^popcount(t & grp) H16[col][j]
+      mfma_i32x4 hp, hn;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) w |= ((__builtin_popcount(col & (4 * q + b)) & 1) ? 0xFFu : 0x01u) << (8 * b);
+        hp[q] = static_cast<int>(w);
+        hn[q] = static_cast<int>(w ^ 0xFEFEFEFEu);  // 0x01 <-> 0xFF: the negation
+      }
+      int sa = 0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bool neg = __builtin_popcount(t & grp) & 1;
+        mfma_i32x4 d = __builtin_amdgcn_mfma_i32_16x16x64_i8(neg ? hn : hp, sop, mfma_i32x4{0, 0, 0, 0}, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_i32_16x16x64_i8(neg ? hp : hn, pop, d, 0, 0, 0);
+        sa += abs(d[0]) + abs(d[1]) + abs(d[2]) + abs(d[3]);
+      }
+      sa = sum_row_groups(sa);  // |coefficients| of column col, summed over its 4 lane groups
+      int sa8d = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) sa8d += (__shfl(sa, 4 * half + b, 64) + 2) >> 2;
+      wave_sync();
+      if (mine && hl == 0) {
+        int satd = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) satd += s_cost[half][0][i];
+        s_t8[half][0] = sa8d < satd;
+      }
+      wave_sync();
+      if (work && hl < 16 && s_t8[half][0]) {
       // ---- 8x8 transform: forward passes, quantisation of scan positions 16k .. 16k + 15
       // with this chunk's share of x264's decimate_score64 (zero runs priced 3 / 2 / 1 / 0;
       // 9 once any |level| > 1): runs inside the chunk here, the run into its first
@@ -382,71 +483,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         if (total < 6) keep = 0;
         s_t8[half][1] = keep;
       }
-        }
       }
     }
-  } else if (work && hl < 24) {
-    // ---- chroma block: eighth-sample MC (clause 8.4.2.2.2) + residual + forward + AC quant
-    const uint8_t* srcc = (comp == 0 ? a.src_u : a.src_v) + slot * g.csize();
-    const int px0 = mx * 8 + cbx, py0 = my * 8 + cby;
-    int pv[4][4];
-    if (!a.bmode) {
-      // the 4x4 chroma block cb covers luma quadrant cb (its partition's vector)
-      const int cmx = a.mv8 ? a.mv8[o * 8 + cb * 2] : mvx, cmy = a.mv8 ? a.mv8[o * 8 + cb * 2 + 1] : mvy;
-      const int r = a.mref ? a.mref[o] : 0;
-      chroma_mc4x4((comp == 0 ? a.refs_u[r] : a.refs_v[r]) + route_index(a.rt, a.nbuf, slot, RO_L0 + r) * g.csize(), cw,
-                   CH, px0, py0, cmx, cmy, pv);
-      if (a.wp && r == 0) {
-        const int* wt = a.wp + slot * 8;
-        const int w = wt[3 + 2 * comp], wo = wt[4 + 2 * comp], d = wt[7];
-        if (w != (1 << d) || wo != 0) {
-#pragma unroll
-          for (int y = 0; y < 4; ++y)
-#pragma unroll
-            for (int x = 0; x < 4; ++x) pv[y][x] = wp_sample(pv[y][x], w, wo, d);
-        }
-      }
-    } else {
-      // the 4x4 chroma block cb covers luma quadrant cb: its lists and vectors
-      const int r0 = h->ref[0][cb];
-      const bool u0 = r0 >= 0, u1 = h->ref[1][cb] >= 0;
-      const int w1 = a.rt ? a.rt[slot].w1[r0 & 3] : a.w1[r0 & 3];
-      int p1[4][4];
-      if (u0) chroma_mc4x4((comp == 0 ? a.refs_u[r0 & 3] : a.refs_v[r0 & 3]) +
-                               route_index(a.rt, a.nbuf, slot, RO_L0 + (r0 & 3)) * g.csize(), cw, CH, px0, py0,
-                           h->mv[0][cb][0], h->mv[0][cb][1], pv);
-      if (u1) chroma_mc4x4((comp == 0 ? a.ref1_u : a.ref1_v) + route_index(a.rt, a.nbuf, slot, RO_L1) * g.csize(), cw,
-                           CH, px0, py0,
-                           h->mv[1][cb][0], h->mv[1][cb][1], p1);
-#pragma unroll
-      for (int y = 0; y < 4; ++y)
-#pragma unroll
-        for (int x = 0; x < 4; ++x)  // implicit weights (a.w1 = 32: the plain average)
-          pv[y][x] = u0 ? (u1 ? h264::clip1((pv[y][x] * (64 - w1) + p1[y][x] * w1 + 32) >> 6) : pv[y][x]) : p1[y][x];
-    }
-    uint32_t sw[4];
-#pragma unroll
-    for (int y = 0; y < 4; ++y) sw[y] = *reinterpret_cast<const uint32_t*>(srcc + static_cast<size_t>(py0 + y) * cw + px0);
-#pragma unroll
-    for (int y = 0; y < 4; ++y) {
-#pragma unroll
-      for (int x = 0; x < 4; ++x) res[y * 4 + x] = static_cast<int>(__builtin_amdgcn_ubfe(sw[y], 8 * x, 8)) - pv[y][x];
-      prw[y] = pack4_u8(pv[y]);
-    }
-    h264::forward_core4x4(res);
-    s_cdc[half][comp][cb] = res[0];
-    const int qbits = 15 + qpc / 6;
-    if (a.trellis >= 2) {  // chroma AC by the same rate-distortion choice, at the chroma QP's lambda
-      trellis_lite4x4(res, lv, mfc, qbits, trellis_lambda4(a.trellis_lambda, qpc), 1);
-    } else {
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        lv[r] = r == 0 ? 0 : h264::quant_coef(res[r], mfc[h264::kPosClass[r]], qbits, 11);
-    }
-    int scan[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) scan[i] = lv[h264::kZigzag4x4[i]];
-    s_score[half][hl] = decimate_score(scan, 1);
   }
   wave_sync();
   if (work && (hl == 16 || hl == 20)) {

@@ -245,6 +245,16 @@ __device__ __forceinline__ int sum64(int v) {
   auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
   return static_cast<int>(p[0]) + static_cast<int>(p[1]);
 }
+// int8 / int32 MFMA operands (v_mfma_i32_16x16x64_i8: A / B 16 bytes per lane, D 4 ints)
+typedef int mfma_i32x4 __attribute__((ext_vector_type(4)));
+// v(l) + v(l ^ 16) + v(l ^ 32) + v(l ^ 48): a 16x16 MFMA result column summed over its four
+// lane groups (rows 4 g .. 4 g + 3 of the tile live in lane group g)
+__device__ __forceinline__ int sum_row_groups(int v) {
+  auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  v = static_cast<int>(p[0]) + static_cast<int>(p[1]);
+  auto q = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return static_cast<int>(q[0]) + static_cast<int>(q[1]);
+}
 __device__ __forceinline__ int min16(int v) {
   v = min(v, dpp<kDppQuadXor1>(v));
   v = min(v, dpp<kDppQuadXor2>(v));
