@@ -106,6 +106,9 @@ struct TqParams {
   bool intra;
   bool dst = false;   // 4x4 intra luma: DST-VII instead of the DCT
   int sdh_scan = -1;  // >= 0: sign data hiding with this scanIdx (0 diagonal, 1 horizontal, 2 vertical)
+  // 16 / 32-point TUs on the matrix cores (transform_quant_mfma); false: the LDS wave products
+  // (the CTB-wavefront intra kernel keeps them: the MFMA form's registers would spill there)
+  bool mfma = true;
 };
 
 // scanIdx of a TU (7.4.9.11): intra luma 4x4 / 8x8 and intra chroma 4x4 follow the mode
@@ -114,9 +117,141 @@ __device__ __forceinline__ int tu_scan_idx(bool intra, bool luma, int log2n, int
   return (mode >= 6 && mode <= 14) ? 2 : ((mode >= 22 && mode <= 30) ? 1 : 0);
 }
 
+// ---------------------------------------------------------------- 16 / 32-point transforms on the matrix cores
+// The four 1-D passes of a TU (forward rows, forward columns, inverse columns, inverse rows) as
+// v_mfma_f32_32x32x16_f16 products that stay in registers between passes: each pass's result has
+// its column on the lane and its rows in the 16 accumulator registers, so the next pass takes it
+// as an operand without lane movement (the accumulator-as-operand order: element j of lane half h
+// in k-step s is row kperm(s, h, j) of it).  fwd: S = R C^T, coef = C S; inv: Z = Rq^T C (= S'^T),
+// R = Z^T C.  Exact integer arithmetic in f16 x f16 -> f32: residuals (<= 10 bits) and DCT entries
+// (|c| <= 90) are exact in f16; the 16-bit intermediates enter as hi * 64 + lo (|hi| <= 718,
+// lo in 0..63, two products combined in int32); every f32 sum stays below 2^24 (32 x 90 x 1023).
+// A 16-point TU fills the top-left quarter of the 32x32 tiles (the other rows / columns are zero).
+typedef _Float16 hv_half8 __attribute__((ext_vector_type(8)));
+typedef float hv_float16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ int kperm(int s, int h, int j) { return 16 * s + 8 * (j >> 2) + 4 * h + (j & 3); }
+// row of accumulator register g (32x32 C/D layout: col = lane & 31)
+__device__ __forceinline__ int acc_row(int g, int h) { return (g & 3) + 8 * (g >> 2) + 4 * h; }
+
+template <int LG>
+__device__ __forceinline__ bool transform_quant_mfma(const DctLds& D, int* R, int16_t* lev, int lstride, const TqParams& p) {
+  constexpr int N = 1 << LG, KS = N / 16;
+  const int lane = lane_id(), r = lane & 31, h = lane >> 5;
+  const bool rv = r < N;
+  auto C = [&](int k, int m) { return static_cast<int>(D.m[k << (5 - LG)][m]); };  // N-point entry (k, m)
+  // ---- forward rows: S[y][u] = (sum_x R[y][x] C[u][x] + rnd) >> sh1 (A = R, B = C^T)
+  hv_float16 acc = {};
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    hv_half8 a, b;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int x = 16 * s + 8 * h + j;
+      a[j] = static_cast<_Float16>(rv ? R[r * 32 + x] : 0);
+      b[j] = static_cast<_Float16>(rv ? C(r, x) : 0);
+    }
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc, 0, 0, 0);
+  }
+  const int sh1 = LG + p.bd - 9, r1 = 1 << (sh1 - 1);
+  int v[16];
+#pragma unroll
+  for (int g = 0; g < 16; ++g) v[g] = (static_cast<int>(acc[g]) + r1) >> sh1;
+  // ---- forward columns: coef[v][u] = (sum_y C[v][y] S[y][u] + rnd) >> sh2 (A = C, B = S)
+  hv_float16 chi = {}, clo = {};
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    hv_half8 a, bh, bl;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      a[j] = static_cast<_Float16>(rv ? C(r, kperm(s, h, j)) : 0);
+      bh[j] = static_cast<_Float16>(v[8 * s + j] >> 6);
+      bl[j] = static_cast<_Float16>(v[8 * s + j] & 63);
+    }
+    chi = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bh, chi, 0, 0, 0);
+    clo = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bl, clo, 0, 0, 0);
+  }
+  const int sh2 = LG + 6, r2 = 1 << (sh2 - 1);
+  const int qm = p.qp % 6, qs = p.qp / 6;
+  const int qbits = 14 + qs + (15 - p.bd - LG);
+  const int qscale = hevc::kQuantScale[qm];
+  const int64_t qoff = static_cast<int64_t>(p.intra ? 171 : 85) << (qbits - 9);
+  const int dscale = 16 * hevc::kLevelScale[qm];
+  const int dsh = p.bd + LG - 5;
+  const int64_t drnd = 1ll << (dsh - 1);
+  int any = 0;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const int vr = acc_row(g, h);
+    int c = (static_cast<int>(chi[g]) * 64 + static_cast<int>(clo[g]) + r2) >> sh2;
+    const int a = c < 0 ? -c : c;
+    int l = static_cast<int>((static_cast<int64_t>(a) * qscale + qoff) >> qbits);
+    l = l > 32767 ? 32767 : l;
+    l = c < 0 ? -l : l;
+    const bool in = rv && vr < N;
+    if (in) lev[vr * lstride + r] = static_cast<int16_t>(l);
+    any |= in && l != 0;
+    // dequantise (8.6.3, flat scaling): the inverse's input, kept in the register
+    int64_t d = ((static_cast<int64_t>(in ? l : 0) * dscale) << qs) + drnd;
+    d >>= dsh;
+    v[g] = static_cast<int>(d < -32768 ? -32768 : (d > 32767 ? 32767 : d));
+  }
+  if (__ballot(any) == 0) {
+    for (int i = lane; i < N * N; i += 64) R[(i >> LG) * 32 + (i & (N - 1))] = 0;
+    wave_sync();
+    return false;
+  }
+  // ---- inverse columns: Z[x][y] = S'[y][x] = clip16((sum_k C[k][y] Rq[k][x] + 64) >> 7)
+  // (A = Rq as the transposed operand, B = C with B[k][y] = C[k][y])
+  hv_float16 zhi = {}, zlo = {};
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    hv_half8 ah, al, b;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ah[j] = static_cast<_Float16>(v[8 * s + j] >> 6);
+      al[j] = static_cast<_Float16>(v[8 * s + j] & 63);
+      b[j] = static_cast<_Float16>(rv ? C(kperm(s, h, j), r) : 0);
+    }
+    zhi = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, b, zhi, 0, 0, 0);
+    zlo = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, b, zlo, 0, 0, 0);
+  }
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const int z = (static_cast<int>(zhi[g]) * 64 + static_cast<int>(zlo[g]) + 64) >> 7;
+    v[g] = z < -32768 ? -32768 : (z > 32767 ? 32767 : z);
+  }
+  // ---- inverse rows: R[y][x] = (sum_k S'[y][k] C[k][x] + rnd) >> (20 - bd) (A = Z transposed)
+  hv_float16 rhi = {}, rlo = {};
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    hv_half8 ah, al, b;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ah[j] = static_cast<_Float16>(v[8 * s + j] >> 6);
+      al[j] = static_cast<_Float16>(v[8 * s + j] & 63);
+      b[j] = static_cast<_Float16>(rv ? C(kperm(s, h, j), r) : 0);
+    }
+    rhi = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, b, rhi, 0, 0, 0);
+    rlo = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, b, rlo, 0, 0, 0);
+  }
+  const int sh4 = 20 - p.bd, r4 = 1 << (sh4 - 1);
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const int y = acc_row(g, h);
+    if (rv && y < N) R[y * 32 + r] = (static_cast<int>(rhi[g]) * 64 + static_cast<int>(rlo[g]) + r4) >> sh4;
+  }
+  wave_sync();
+  return true;
+}
+
 __device__ __forceinline__ bool transform_quant_block(const DctLds& D, int* R, int* S, int16_t* lev, int lstride,
                                                       const TqParams& p) {
   const int n = 1 << p.log2n, lg = p.log2n;
+  if (p.mfma && !p.dst && p.sdh_scan < 0 && (lg == 4 || lg == 5)) {
+    wave_sync();  // R was written by other lanes
+    return lg == 5 ? transform_quant_mfma<5>(D, R, lev, lstride, p) : transform_quant_mfma<4>(D, R, lev, lstride, p);
+  }
   const bool dst = p.dst;
   auto cn = [&](const DctLds& M, int l2, int k, int m) { return dst ? static_cast<int>(M.dst[k][m]) : hv::cn(M, l2, k, m); };
   // forward, stage 1 (rows): S[y][k] = (sum_x R[y][x] * C[k][x] + rnd) >> sh1

@@ -559,6 +559,7 @@ __device__ __forceinline__ bool recon_block(const HevcIntraArgs& a, ReconShared&
   int16_t* lev = (LUMA ? a.coef_y : (comp == 1 ? a.coef_u : a.coef_v)) + slot * (LUMA ? g.ysize() : g.csize()) +
                  static_cast<size_t>(Y0) * pw + X0;
   hv::TqParams tp{log2n, bd, qpp, true, dst, a.sdh ? hv::tu_scan_idx(true, LUMA, log2n, mode) : -1};
+  tp.mfma = false;
   const bool nz = hv::transform_quant_block(D, S.R, S.S, lev, pw, tp);
   uint16_t* rec = (LUMA ? a.rec_y : (comp == 1 ? a.rec_u : a.rec_v)) + slot * (LUMA ? g.ysize() : g.csize());
   for (int i = lane; i < n * n; i += 64) {
