@@ -460,54 +460,33 @@ __device__ __forceinline__ void encode_intra_mb(const IntraArgs& a, IntraShared&
       const int mb_ = by > 0 ? S.modes8[b8 - 2] : S.top_modes[bx >> 2];
       const bool dcpred = (bx == 0 && !(mbav & h264::AV_LEFT)) || (by == 0 && !(mbav & h264::AV_TOP));
       const int pm = dcpred ? 2 : min(ma, mb_);
-      // mode ranking on the int8 matrix cores: column m of the MFMA B operands holds mode m's
-      // prediction (m < 9; lane = (row pair lane >> 4, column lane & 15)), the A operand the 64x64
-      // Sylvester Hadamard H64 = H8 (x) H8, so D = H64 (S - 128) - H64 (P_m - 128) is mode m's 2-D
-      // 8x8 Hadamard of the residual, exact in int32; sa8d = sum |D| over the column
+      // mode ranking: lane = (mode group lane >> 3, row lane & 7); two passes cover modes 0..8
       int key = 0x7FFFFFFF;
-      {
-        const int m = lane & 15, grp = lane >> 4, r0 = 2 * grp;
+      for (int pass = 0; pass < 2; ++pass) {
+        const int m = pass * 8 + (lane >> 3), r = lane & 7;
         const bool valid = m < 9 && (m == 2 || ((m == 0 || m == 3 || m == 7) && has_top) || ((m == 1 || m == 8) && has_left) ||
                                      ((m == 4 || m == 5 || m == 6) && has_top && has_left && has_tl));
-        mfma_i32x4 sop, pop;
+        int v[8];
 #pragma unroll
-        for (int rr = 0; rr < 2; ++rr) {
+        for (int x = 0; x < 8; ++x)
+          v[x] = m < 9 ? static_cast<int>(S.src[(by + r) * 16 + bx + x]) - i8_pred_tap(m, x, r, S.f8t, dc8) : 0;
+        had8_pass(v, 1);
 #pragma unroll
-          for (int h4 = 0; h4 < 2; ++h4) {
-            const uint32_t sw = *reinterpret_cast<const uint32_t*>(S.src + (by + r0 + rr) * 16 + bx + 4 * h4);
-            uint32_t pw = sw;  // idle columns: a zero residual
-            if (m < 9) {
-              pw = 0;
+        for (int x = 0; x < 8; ++x) S.h8[lane >> 3][r * 8 + x] = v[x];
+        wave_sync();
+        const int c = lane & 7;
 #pragma unroll
-              for (int b = 0; b < 4; ++b)
-                pw |= static_cast<uint32_t>(i8_pred_tap(m, 4 * h4 + b, r0 + rr, S.f8t, dc8)) << (8 * b);
-            }
-            sop[2 * rr + h4] = static_cast<int>(sw ^ 0x80808080u);
-            pop[2 * rr + h4] = static_cast<int>(pw ^ 0x80808080u);
-          }
-        }
-        // this lane's A rows: H64[16 t + c][16 grp + j] = (-1)^popcount(t & grp) H16[c][j], c = lane & 15
-        // (tile t's rows are H16 row c times that sign: x ^ 0xFE flips 0x01 <-> 0xFF, the negation)
-        mfma_i32x4 hp;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          uint32_t w = 0;
-#pragma unroll
-          for (int b = 0; b < 4; ++b) w |= ((__builtin_popcount(m & (4 * q + b)) & 1) ? 0xFFu : 0x01u) << (8 * b);
-          hp[q] = static_cast<int>(w);
-        }
+        for (int y = 0; y < 8; ++y) v[y] = S.h8[lane >> 3][y * 8 + c];
+        had8_pass(v, 1);
         int sa = 0;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int flip = (__builtin_popcount(t & grp) & 1) ? static_cast<int>(0xFEFEFEFEu) : 0;
-          const mfma_i32x4 ht = hp ^ flip, hnt = hp ^ (flip ^ static_cast<int>(0xFEFEFEFEu));
-          mfma_i32x4 d = __builtin_amdgcn_mfma_i32_16x16x64_i8(ht, sop, mfma_i32x4{0, 0, 0, 0}, 0, 0, 0);
-          d = __builtin_amdgcn_mfma_i32_16x16x64_i8(hnt, pop, d, 0, 0, 0);
-          sa += abs(d[0]) + abs(d[1]) + abs(d[2]) + abs(d[3]);
-        }
-        sa = sum_row_groups(sa);
+        for (int y = 0; y < 8; ++y) sa += v[y] < 0 ? -v[y] : v[y];
+        sa += __shfl_xor(sa, 1);
+        sa += __shfl_xor(sa, 2);
+        sa += __shfl_xor(sa, 4);
         const int cost = ((sa + 2) >> 2) + lambda * (m == pm ? 1 : 4);
-        if (valid && grp == 0) key = (cost << 4) | m;
+        if (valid && c == 0) key = min(key, (cost << 4) | m);
+        wave_sync();
       }
       key = wave_min(key);
       const int mode = key & 15;

@@ -339,7 +339,7 @@ __device__ __forceinline__ void mc_block(SH& S, const uint16_t* ref0, const uint
 // TSPLIT: the instance with the residual-quadtree choice (its register footprint stays out of
 // the default instance)
 template <bool TSPLIT>
-__global__ __launch_bounds__(64) void hevc_inter_cu(HevcInterArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8))) void hevc_inter_cu(HevcInterArgs a) {
   __shared__ typename std::conditional<TSPLIT, InterShared, InterSharedLean>::type S;
   __shared__ hv::DctLds D;
   const HevcGeom& g = a.g;

@@ -144,9 +144,12 @@ class HevcParams:
     # quadrant (p_part8x8, HEVC form: candidates, half / quarter rings); the four 8x8 CUs win
     # when their SATD + lambda * (mvd bits + inter8_overhead) beats the merge-aware 16x16 cost.
     # Blocks at or below inter8_min_satd are not searched.  B pictures keep 16x16 / 32x32 CUs.
-    inter8: bool = False
+    # Content suite (profiles/r6_hevc_inter8_rd.md, BD-rate vs 16x16 / 32x32 only): overhead 8
+    # -0.34 %, 16 -0.28 %, 24 -0.23 %, 16 with a 1000 floor -0.37 % (no class worse); config 4
+    # about -0.5 % fps
+    inter8: bool = True
     inter8_overhead: int = 16
-    inter8_min_satd: int = 2000
+    inter8_min_satd: int = 1000
 
     def eff_refs(self) -> int:
         """Active list-0 pictures of P pictures (1 for intra-only and keyint GOPs)."""
