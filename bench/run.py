@@ -237,7 +237,11 @@ def _hevc_run(args, W, H, B, F, bd, crf, two_pass_kbps=None, fps=30.0, resident=
     from govideocompressor_amd.rc import GlobalStats, TwoPassFeedback, abr_solve
 
     env = D.init(prefer_gpu=True)
-    enc = GpuHevcEncoder(_params(HevcParams, width=W, height=H, fps=fps, crf=crf, bit_depth=bd), slots=B, device=env.device)
+    # MIVC_ENTROPY_THREADS (a runtime knob): host CABAC threads of this rank (a rank of an 8-GPU
+    # node gets cores / 8; tools/gpu/r6_hevc_rehearse.sh)
+    threads = int(os.environ["MIVC_ENTROPY_THREADS"]) if os.environ.get("MIVC_ENTROPY_THREADS") else None
+    enc = GpuHevcEncoder(_params(HevcParams, width=W, height=H, fps=fps, crf=crf, bit_depth=bd), slots=B, device=env.device,
+                         entropy_threads=threads)
 
     held = None
     if resident:
