@@ -394,7 +394,7 @@ def main():
     ap.add_argument("--merged-out3", default=None, help="rank 0 writes the merged stream to <path>.<codec>")
     ap.add_argument("--no-encode-only3", dest="encode_only3", action="store_false",
                     help="skip the encode-only reference rate of config 3")
-    ap.add_argument("--slots4", type=int, default=64)
+    ap.add_argument("--slots4", type=int, default=256, help="config 4 batch width (sweep 64 / 128 / 256: 2304 / 2408 / 2469 fps, profiles/r6_hevc_rank_rehearsal.md)")
     ap.add_argument("--frames4", type=int, default=30)
     # 10 segments x 60 frames = a 10 s 8K60 clip (~60 GB of 10-bit samples) resident in HBM
     ap.add_argument("--slots5", type=int, default=10)
