@@ -27,6 +27,7 @@ import os
 # env name -> H264Params field
 H264 = {
     "MIVC_I8X8": "i8x8",
+    "MIVC_I4X4_IN_P": "i4x4_in_p",
     "MIVC_LA_RANGE": "la_range",
     "MIVC_LA_WEIGHTS": "la_weights",
     "MIVC_B_ADAPT": "b_adapt",

@@ -83,6 +83,7 @@ CONFIGS = {
     # spatial direct decided exactly inside the MB wavefront (b_spatial_decide), + b-pyramid
     "sp_wave": dict(direct="spatial", spatial_wavefront=True),
     "sp_wave_pyr": dict(direct="spatial", spatial_wavefront=True, pyramid=True),
+    "i4p": dict(i4x4_in_p=True),  # x264's analysis: Intra4x4 trials in P / B pictures too
     "default": dict(),  # the current defaults
 }
 # HEVC (GpuHevcEncoder) configurations: x265 --signhide, --bframes variants
