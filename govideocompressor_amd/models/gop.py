@@ -205,20 +205,30 @@ def hevc_ref_slots(bframes: int, pyramid: bool, refs: int = 1) -> int:
 
 
 def hevc_gop_plan(frames: int, bframes: int, pyramid: bool = True, anchors_at=(), ref_slots: int = 3,
-                  refs: int = 1) -> list[GopPic]:
+                  refs: int = 1, types: str | None = None) -> list[GopPic]:
     """x265-style closed GOP: I0, P anchors every ``bframes + 1`` pictures (plus the last
     picture and ``anchors_at``), each followed by the B pictures before it.  With
     ``pyramid`` and two or more B pictures in a run, the middle one is a reference B
     (list 0 = the previous anchor, list 1 = the new one) coded first, and the others are
     non-reference b pictures predicting from their nearest references on both sides
     (x265 --b-pyramid).  ``refs`` (x265 --ref): a P anchor's list 0 holds up to that many
-    reference pictures, nearest first.  The DPB is simulated to give every picture its RPS
-    and buffer."""
+    reference pictures, nearest first.  ``types``: display-order picture types of an adaptive
+    placement (x265 --b-adapt, ``"IPBBP..."``: every non-B picture is an anchor, runs of at most
+    ``bframes`` B pictures) instead of the fixed pattern.  The DPB is simulated to give every
+    picture its RPS and buffer."""
     if frames < 1:
         return []
     step = max(0, int(bframes)) + 1
     nref = max(1, int(refs))
-    anchors = sorted(set(range(0, frames, step)) | {frames - 1} | {int(d) for d in anchors_at if 0 <= int(d) < frames})
+    if types is not None:
+        if len(types) != frames or types[0] != "I" or types[-1] == "B":
+            raise ValueError(f"hevc_gop_plan: types must cover the frames, start with I and end on an anchor: {types!r}")
+        anchors = [d for d, t in enumerate(types) if t != "B"]
+        if any(b - a - 1 > max(0, int(bframes)) for a, b in zip(anchors, anchors[1:])):
+            raise ValueError("hevc_gop_plan: a B run longer than bframes")
+        step = 1  # the runs are as given
+    else:
+        anchors = sorted(set(range(0, frames, step)) | {frames - 1} | {int(d) for d in anchors_at if 0 <= int(d) < frames})
     if step > 1:  # keep every B run <= bframes after inserting the extra anchors
         out_a, prev = [0], 0
         for a in anchors[1:]:

@@ -103,6 +103,14 @@ class HevcParams:
     # content suite (profiles/r4_hevc_bqp_rd.json, BD-rate vs +4): +2 +1.85 %, +3 +0.79 %,
     # +6 -1.36 % -- the B picture between two anchors is worth less than x265's pbratio prices it
     b_qp_offset: int = 6
+    # x265 --b-adapt: B runs of up to ``bframes`` pictures placed from the lookahead's lowres
+    # costs (rc/badapt.py, x264's fast algorithm on la_multi's P-at-distance and B costs) instead
+    # of the fixed pattern; one pattern per batch (the summed costs of every slot, each slot's
+    # scene cuts still forced anchors) -- the HEVC kernels code one picture type per step.
+    # ``b_bias`` = x264/x265 --b-bias; 0 = the fixed pattern
+    b_adapt: int = 0
+    b_bias: int = 0
+    badapt_range: int = 2
     # x265 --b-pyramid (default on): the middle B of a run of 2+ is a reference picture (at half
     # the B QP offset) and the others predict from their nearest references (models/gop.py)
     pyramid: bool = True
@@ -420,13 +428,20 @@ class GpuHevcEncoder:
         # Pieces shorter than 8 pictures give the propagation too little to offset cutree's
         # constant CRF compensation ((1 - qcomp) x 13.5 QP): they keep the plain CRF QPs.
         use_tree = self.p.cutree and lbw == self.wmb and lbh <= self.hmb and y.shape[1] >= 8
-        cutree = None
+        badapt = bool(self.p.b_adapt) and self.nb > 0 and y.shape[1] >= 3
+        cutree = multi = None
         if use_tree:
             costs_d, cutree = la.mbtree(y8.contiguous(), MBTREE_STRENGTH)
-            costs = costs_d.cpu().numpy()
+            blk, mv = la.last_blk, la.last_mv
+        elif badapt:
+            costs_d, blk, mv = la.frame_costs(y8.contiguous(), block_costs=True, block_mvs=True)
         else:
-            costs = la.frame_costs(y8.contiguous()).cpu().numpy()
-        return dict(costs=costs, cutree=cutree, use_tree=use_tree, rows=lbh, blocks=lbw * lbh,
+            costs_d, blk, mv = la.frame_costs(y8.contiguous()), None, None
+        if badapt:
+            multi = la.multi_costs(y8.contiguous(), blk, mv, min(7, self.nb + 1),
+                                   search_range=int(self.p.badapt_range)).cpu().numpy()
+        costs = costs_d.cpu().numpy()
+        return dict(costs=costs, cutree=cutree, use_tree=use_tree, rows=lbh, blocks=lbw * lbh, multi=multi,
                     scenecuts=scenecut_flags(costs, float(self.p.scenecut), keyint=self.p.keyint or None),
                     shape=tuple(y.shape))
 
@@ -446,6 +461,7 @@ class GpuHevcEncoder:
             self.timings["lookahead_async_s"] = self.timings.get("lookahead_async_s", 0.0) + analysis["seconds"]
         self._cutree, self._cutree_rows = analysis["cutree"], analysis["rows"]
         self._scenecuts = analysis["scenecuts"]
+        self._la_costs, self._la_multi, self._la_blocks = analysis["costs"], analysis.get("multi"), analysis["blocks"]
         q = crf_qps_batch(analysis["costs"], float(self.p.crf), analysis["blocks"], keyint=self.p.keyint or None,
                           scenecuts=self._scenecuts, mbtree=analysis["use_tree"], bframes=self.nb)
         self.stats["scenecuts"] = int(self._scenecuts.sum())
@@ -618,9 +634,19 @@ class GpuHevcEncoder:
 
     def _plan(self, F: int, cuts_h: np.ndarray, anchors_at) -> list:
         from .gop import GopPic, hevc_gop_plan
+        forced = set(anchors_at) | {d for d in range(1, F) if cuts_h[:, d].any()}
+        types = None
+        multi = getattr(self, "_la_multi", None)
+        if self.p.b_adapt and self.nb and multi is not None and multi.shape[:2] == (self.B, F):
+            # x265 --b-adapt, one pattern for the batch: the slots' summed lowres costs
+            from ..rc.badapt import b_adapt_types
+            costs = self._la_costs
+            types = b_adapt_types(costs[:, :, 1].sum(axis=0), multi.sum(axis=0), multi[:, :, 0].sum(axis=0), self.nb,
+                                  self._la_blocks * self.B, forced, int(self.p.b_bias))
+            self.stats["b_ratio"] = types.count("B") / max(1, F)
         if self.nb or self.nrefs > 1:
-            return hevc_gop_plan(F, self.nb, self.p.pyramid, set(anchors_at) | {d for d in range(1, F) if cuts_h[:, d].any()},
-                                 ref_slots=self.ref_slots, refs=self.nrefs)
+            return hevc_gop_plan(F, self.nb, self.p.pyramid, forced, ref_slots=self.ref_slots, refs=self.nrefs,
+                                 types=types)
         out = []
         for t in range(F):
             idr = t == 0 or self.p.intra_only or (self.p.keyint > 0 and t % self.p.keyint == 0)
@@ -685,6 +711,7 @@ class GpuHevcEncoder:
         qi, qpp = self.p.frame_qps()
         self._scenecuts = None
         self._cutree = None
+        self._la_multi = None
         from_la = False
         if qps is None and self.p.crf is not None and self.p.lookahead and not self.p.intra_only:
             qps = self.crf_qps(y, analysis)

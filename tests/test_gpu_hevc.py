@@ -434,3 +434,21 @@ def test_gpu_hevc_inter8_matches_decoder(host, bd, ctu64):
             cu = p["cu"]
             n8 += int(((cu[:, 0] == 1) & (((cu[:, 3] >> 1) & 3) == 0)).sum())
     assert n8 > 0
+
+
+def test_gpu_hevc_badapt_matches_decoder(host):
+    """x265 --b-adapt (one lowres-cost placement per batch, runs of up to 3 B pictures with the
+    pyramid's reference B, 3 list-0 pictures): bit-exact with the CPU decoder, and the placement
+    is not the fixed pattern on static content (longer runs)."""
+    from govideocompressor_amd.models.h264_gpu import synth_clip
+    from govideocompressor_amd.models.hevc_gpu import GpuHevcEncoder, HevcParams
+    w, h, F, B = 160, 96, 10, 2
+    y, u, v = synth_clip(B, F, w, h, seed=11, kind="static")
+    enc = GpuHevcEncoder(HevcParams(width=w, height=h, crf=28, bframes=3, b_adapt=1), slots=B)
+    res = enc.encode(y, u, v, keep_recon=True)
+    rec = enc.last_recon
+    order = list(enc.last_order)
+    enc.close()
+    _compare(host, res, rec)
+    assert order != list(range(F))          # B pictures were placed
+    assert enc.stats.get("b_ratio", 0) > 0

@@ -344,3 +344,58 @@ def test_hevc_multiref_roundtrip(host, seed, refs, bframes, tmvp, pyramid, wpp):
         assert np.array_equal(p["cu"][inter, 13:15], cu[inter, 13:15])   # refIdx L0 / L1
         far += int((cu[inter, 13] > 0).sum())
     assert far > 0
+
+
+def test_hevc_gop_plan_adaptive_types():
+    """x265 --b-adapt placements (rc/badapt.py types) become HEVC GOP plans: every non-B
+    picture an anchor, each run coded after its closing anchor (the pyramid's middle B first),
+    every reference used by a picture still held in the DPB, runs longer than bframes refused."""
+    from govideocompressor_amd.models.gop import hevc_gop_plan, hevc_ref_slots
+    for types, bf, pyr, refs in (("IBBPBPBBP", 3, True, 3), ("IPPBPBBBP", 3, False, 1), ("IBPBBBBP", 4, True, 2)):
+        plan = hevc_gop_plan(len(types), bf, pyr, types=types, ref_slots=hevc_ref_slots(bf, pyr, refs), refs=refs)
+        assert sorted(p.d for p in plan) == list(range(len(types)))
+        assert all((p.kind == "B") == (types[p.d] == "B") for p in plan)
+        coded = set()
+        for p in plan:
+            held = {d for d, _ in p.rps}
+            for r in (*p.refs0, p.l0, p.l1):
+                if r >= 0:
+                    assert r in coded and r in held, (types, p)
+            coded.add(p.d)
+    with pytest.raises(ValueError, match="longer than bframes"):
+        hevc_gop_plan(7, 2, True, types="IBBBBBP")
+
+
+def test_hevc_adaptive_gop_stream_decodes(host):
+    """A stream written from an adaptive plan (uneven B runs, pyramid, 3 list-0 pictures, TMVP)
+    decodes with every picture's records intact."""
+    from govideocompressor_amd.models.gop import hevc_gop_plan, hevc_ref_slots
+    from govideocompressor_amd.utils.hevc_synth import random_records
+    rng = np.random.default_rng(3)
+    types = "IBPBBBPP"
+    cfg = dict(width=96, height=64, bframes=3, tmvp=1, pyramid=1, refs=3)
+    out = [host.hevc_parameter_sets(cfg)]
+    held, recs = {}, {}
+    for pic in hevc_gop_plan(len(types), 3, True, types=types, ref_slots=hevc_ref_slots(3, True, 3), refs=3):
+        r = random_records(rng, 96, 64, pslice=pic.kind != "I", bslice=pic.kind == "B", nref=(max(1, len(pic.refs0)), 1),
+                           mv_pool=2, density=0.03)
+        fp = dict(idr=int(pic.kind == "I"), poc=pic.d, qp=30, slice_type={"I": 2, "P": 1, "B": 0}[pic.kind],
+                  nal_ref=int(pic.ref), rps=[(d, int(u)) for d, u in pic.rps])
+        if pic.kind != "I":
+            col = pic.l1 if pic.kind == "B" else pic.l0
+            ccu, c0, c1, cl0 = held[col]
+            fp.update(ref_poc0=pic.l0, refs0=list(pic.refs0), col_poc=col, col_ref_poc0=c0, col_ref_poc1=c1, col_cu=ccu,
+                      col_refs0=cl0)
+            if pic.kind == "B":
+                fp["ref_poc1"] = pic.l1
+        out.append(host.hevc_write_slice(cfg, fp, *r)[0])
+        if pic.ref:
+            held[pic.d] = (None if pic.kind == "I" else r[1].copy(), pic.l0, pic.l1, list(pic.refs0) or None)
+        recs[pic.d] = r
+    pics = host.hevc_decode(b"".join(out))
+    assert [p["poc"] for p in pics] == list(range(len(types)))
+    for p in pics:
+        cu = recs[p["poc"]][1]
+        inter = cu[:, 0] == 1
+        assert np.array_equal(p["cu"][inter, 4:12], cu[inter, 4:12])     # vectors
+        assert np.array_equal(p["cu"][inter, 13:15], cu[inter, 13:15])   # refIdx

@@ -108,6 +108,11 @@ HEVC_CONFIGS = {
     "i8o16": dict(inter8=True, inter8_overhead=16),
     "i8o24": dict(inter8=True, inter8_overhead=24),
     "i8o16m1000": dict(inter8=True, inter8_overhead=16, inter8_min_satd=1000),
+    # x265 --b-adapt (round 6): adaptive B runs, one pattern per batch
+    "ba_b2": dict(b_adapt=1, bframes=2),
+    "ba_b3": dict(b_adapt=1, bframes=3),
+    "ba_b3bias100": dict(b_adapt=1, bframes=3, b_bias=100),
+    "ba_b4": dict(b_adapt=1, bframes=4),
 }
 
 
