@@ -18,12 +18,14 @@ decodes many closed-GOP segments at once:
 
 P and B pictures (sub-8x8 partitions, B_8x8, spatial / temporal direct, explicit / implicit
 weighted prediction, several references) reconstruct on the GPU; Intra 4x4 / 8x8 / 16x16
-too, and pictures of several slices (the records carry each MB's slice for the intra
-neighbour availability).  Segments the GPU path does not cover (I_PCM, constrained intra
-prediction, mmco 5, slices of one picture with different reference lists or filter offsets,
-per-picture filter parameters that differ from the batch, High 10 streams) are decoded by the CPU decoder
-instead (``h264_decoder.cc``) and uploaded; the result is identical
-either way (the CPU decoder is the bit-exact oracle of ``tests/test_gpu_decode.py``).
+too, I_PCM macroblocks, constrained intra prediction, scaling matrices, and pictures of several
+slices (the records carry each MB's slice for the intra neighbour availability).  Segments the
+GPU path does not cover (High 10 and deeper streams -- the reconstruction kernels are 8-bit --,
+mmco 5, implicit-weighted B slices with more than 8 references in a list, slices of one
+picture with different reference lists or weights, per-picture filter parameters that differ
+from the batch) are decoded by the CPU decoder instead (``h264_decoder.cc``) and uploaded; the
+result is identical either way (the CPU decoder is the bit-exact oracle of
+``tests/test_gpu_decode.py``).
 """
 from __future__ import annotations
 

@@ -97,6 +97,21 @@ def timeline(path, top=12):
         before = ends[i][2][:40] if i >= 0 else "-"
         after = starts[j][2][:40] if j < len(starts) else "-"
         out.append(f"| {g / 1e6:.2f} | {(at - t0) / 1e6:.1f} | {before} | {after} |")
+    # steady state: the trailing half of the span (a bench run's timed steps, past its startup
+    # and warmup), where a throughput number is measured
+    w0 = t1 - span // 2
+    clip = [(max(r[0], w0), r[1]) for r in rows if r[1] > w0]
+    sb = sum(e - s for s, e in _union(clip))
+    out += ["", f"## Steady state (the last {span / 2e6:.1f} ms): device busy {100.0 * sb / (t1 - w0):.1f} %", ""]
+    if qcol:
+        out += [f"| {qcol} | busy % of the window |", "|---|---|"]
+        per = defaultdict(list)
+        for r in rows:
+            if r[1] > w0:
+                per[r[3]].append((max(r[0], w0), r[1]))
+        for q, iv in sorted(per.items(), key=lambda kv: -len(kv[1])):
+            b = sum(e - s for s, e in _union(iv))
+            out.append(f"| {q} | {100.0 * b / (t1 - w0):.1f} |")
     return out
 
 
