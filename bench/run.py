@@ -179,7 +179,7 @@ def config3(args) -> list[dict]:
         torch.cuda.synchronize()
         D.barrier(env)
         t0 = time.perf_counter()
-        outs = tc.run(pieces, 30.0)
+        outs = tc.run(pieces, 30.0, first_index=lo)
         merged = merger.run(outs)
         torch.cuda.synchronize()
         D.barrier(env)

@@ -87,7 +87,10 @@ class GpuTranscoder:
                     dst[b, c:].copy_(src[c - 1].expand(F - c, *src.shape[1:]))
         return y, u, v, counts
 
-    def _encode(self, y, u, v, counts: list[int]) -> list[bytes]:
+    def _encode(self, y, u, v, counts: list[int], first: int = 0) -> list[bytes]:
+        """``first``: global index of the batch's first piece -- each piece's idr_pic_id derives
+        from its own index, so a piece codes the same bytes whatever batch or rank it lands in
+        (and neighbouring pieces of a merged stream still alternate)."""
         B = y.shape[0]
         if B < self.slots:  # a short last batch: repeat the first piece in the spare slots
             pad = self.slots - B
@@ -96,7 +99,8 @@ class GpuTranscoder:
         if self.hevc_out:
             res = self.enc.encode(y, u, v, metrics=False)
         else:
-            res = self.enc.encode(y, u, v, idr_ids=list(range(self.slots)), anchors_at=sorted({c - 1 for c in counts}),
+            res = self.enc.encode(y, u, v, idr_ids=[(first + b) & 0xFFFF for b in range(self.slots)],
+                                  anchors_at=sorted({c - 1 for c in counts}),
                                   metrics=False)
         return [ps + b"".join(res[b].display_prefix(counts[b])) for b in range(B)]
 
@@ -113,7 +117,8 @@ class GpuTranscoder:
             ev.synchronize()
             return y, u, v, counts, ev, dt, time.perf_counter() - t0
 
-    def run(self, pieces: list[bytes], fps: float = 30.0) -> list[bytes]:
+    def run(self, pieces: list[bytes], fps: float = 30.0, first_index: int = 0) -> list[bytes]:
+        """``first_index``: global index of pieces[0] (a rank's share of a larger job)."""
         batches = [pieces[i:i + self.slots] for i in range(0, len(pieces), self.slots)]
         out: list[bytes] = []
         t = dict(parse_s=0.0, decode_s=0.0, encode_s=0.0, decode_wait_s=0.0)
@@ -143,7 +148,7 @@ class GpuTranscoder:
             for x in (y, u, v):
                 x.record_stream(main)
             te = time.perf_counter()
-            out += self._encode(y, u, v, counts)
+            out += self._encode(y, u, v, counts, first_index + k * self.slots)
             main.synchronize()
             t["encode_s"] += time.perf_counter() - te
             del y, u, v
