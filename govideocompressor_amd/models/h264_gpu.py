@@ -982,7 +982,11 @@ class GpuH264Encoder:
             fp["num_ref_l1"] = 1
             if pic.mod_l0:
                 fp["mod_l0"] = [tuple(m) for m in pic.mod_l0]
-        if pic.kind == "P" and self._wp is not None:
+        # identity weights (this slot's picture did not qualify, another slot's of the step
+        # did) write the same all-default table as a step without weights, so a segment's
+        # bytes do not depend on the other segments of its batch
+        if pic.kind == "P" and self._wp is not None and any(
+                int(x) != (1 << WP_LOG2 if i % 2 == 0 else 0) for i, x in enumerate(self._wp[t, b])):
             fp["wp"] = [WP_LOG2, WP_LOG2] + [int(x) for x in self._wp[t, b]]
         return fp
 

@@ -388,6 +388,26 @@ def test_gpu_h264_weightp_fade(host, bframes, refs):
     assert out[True][0] < out[False][0] * 0.97, out
 
 
+def test_gpu_h264_segment_bytes_independent_of_batch_neighbours():
+    """A segment's bytes do not depend on what else its batch holds: a static segment encoded
+    next to a fading one (whose P pictures get explicit weights, so the step runs the
+    weighted path) equals its encode alone -- no identity pred_weight_table.  Segment-parallel
+    jobs (bench/run.py config 3 over any rank count) rely on it."""
+    import torch
+    from govideocompressor_amd.models.h264_gpu import GpuH264Encoder, H264Params, synth_clip
+    fy, fu, fv = _fade_clip(1, 8, 320, 192)
+    sy, su, sv = synth_clip(1, 8, 320, 192, seed=9)
+    both = [torch.cat([a, b]).contiguous() for a, b in ((sy, fy), (su, fu), (sv, fv))]
+    out = []
+    for clip, B in ((both, 2), ((sy, su, sv), 1)):
+        enc = GpuH264Encoder(H264Params(width=320, height=192, crf=23.0), slots=B)
+        out.append(enc.encode(*clip, idr_ids=[0] * B, metrics=False)[0].bitstream)
+        if B == 2:
+            assert enc.stats.get("weightp_pictures", 0) > 0, enc.stats
+        enc.close()
+    assert out[0] == out[1]
+
+
 def test_gpu_h264_weightp_static_content_unweighted(host):
     """Content without brightness changes gets no weights (no pred_weight_table entries)."""
     enc, res, _ = _run(176, 144, slots=2, frames=5, crf=None, qp=28, bframes=0)
