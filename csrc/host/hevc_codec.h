@@ -15,6 +15,7 @@
 #include <memory>
 #include <vector>
 
+#include "../common/hevc_ctu_coder.h"
 #include "../common/hevc_tables.h"
 
 namespace mivc {
@@ -126,6 +127,16 @@ std::vector<uint8_t> hevc_write_slice(const HevcConfig& cfg, const HevcFramePara
                                       const CuInfo* cu, const int16_t* coef_y, const int16_t* coef_cb,
                                       const int16_t* coef_cr, HevcSliceStats* stats,
                                       const PackedLevels* packed = nullptr);
+
+// The slice-data coder's view of a picture (hevc_ctu_coder.h): sizes, tools, slice type, QP,
+// reference / collocated POCs (the collocated records pointer is passed separately)
+CoderPic hevc_coder_pic(const HevcConfig& cfg, const HevcFrameParams& fp);
+
+// One slice NAL from substreams coded elsewhere (the GPU entropy kernel): the slice header of
+// `fp`, the entry points of the nsub substreams (one per CTU row with WPP, else one), the
+// substreams, emulation prevention -- byte-identical to hevc_write_slice on the same records.
+std::vector<uint8_t> hevc_assemble_slice(const HevcConfig& cfg, const HevcFrameParams& fp, const uint8_t* const* sub,
+                                         const uint32_t* sizes, int nsub);
 
 struct HevcPicture {
   int width = 0, height = 0;            // cropped (display) size
