@@ -16,6 +16,16 @@
 #include "../host/hevc_ctx_tables.h"
 #include "hevc_tables.h"
 
+// the slice coder's member functions: host + device without forced inlining, the large ones
+// kept out of line on the device (one call site each in the kernel instead of copies)
+#if defined(__HIPCC__)
+#define HV_FN __host__ __device__
+#define HV_BIG __host__ __device__ __attribute__((noinline))
+#else
+#define HV_FN inline
+#define HV_BIG inline
+#endif
+
 namespace mivc {
 namespace hevc {
 
@@ -434,12 +444,12 @@ struct CtuCoder {
   int cu64_midx = -1;
   Motion cu64_mot;
 
-  MIVC_HD void fail(int code) {
+  HV_FN void fail(int code) {
     if (err == CE_NONE) err = code;
   }
 
   // contexts initialised, engine started on `sink`
-  MIVC_HD void begin(const CoderPic* pic, const CtuInfo* ct, const CuInfo* cu_, const CuInfo* col, const CoderLevels& l,
+  HV_BIG void begin(const CoderPic* pic, const CtuInfo* ct, const CuInfo* cu_, const CuInfo* col, const CoderLevels& l,
                      const CoderState& s, CtxState* ctx_mem, Sink* sink) {
     P = pic;
     ctu = ct;
@@ -467,19 +477,19 @@ struct CtuCoder {
     cu64_mot = motion_none();
   }
 
-  MIVC_HD size_t g(int x, int y) const { return static_cast<size_t>(y >> 3) * w8 + (x >> 3); }
-  MIVC_HD size_t g4(int x, int y) const { return static_cast<size_t>(y >> 2) * (2 * w8) + (x >> 2); }
-  MIVC_HD bool inside(int x, int y) const { return x >= 0 && y >= 0 && x < W && y < H; }
+  HV_FN size_t g(int x, int y) const { return static_cast<size_t>(y >> 3) * w8 + (x >> 3); }
+  HV_FN size_t g4(int x, int y) const { return static_cast<size_t>(y >> 2) * (2 * w8) + (x >> 2); }
+  HV_FN bool inside(int x, int y) const { return x >= 0 && y >= 0 && x < W && y < H; }
   // 6.4.1 z-scan availability at 8x8 granularity (the granule is coded iff already visited)
-  MIVC_HD bool avail(int x, int y) const { return inside(x, y) && S.coded[g(x, y)]; }
+  HV_FN bool avail(int x, int y) const { return inside(x, y) && S.coded[g(x, y)]; }
 
-  MIVC_HD const CuInfo& cu_at(int x, int y) const {
+  HV_FN const CuInfo& cu_at(int x, int y) const {
     const int ci = (y >> kCtbLog2) * wctb + (x >> kCtbLog2);
     return cu[static_cast<size_t>(ci) * kCusPerCtb + zorder8((x & (kCtb - 1)) >> 3, (y & (kCtb - 1)) >> 3)];
   }
 
   // ---------------------------------------------------------------- SAO (7.3.8.3)
-  MIVC_HD static bool same_sao(const CtuInfo& a, const CtuInfo& b) {
+  HV_FN static bool same_sao(const CtuInfo& a, const CtuInfo& b) {
     for (int k = 0; k < 2; ++k)
       if (a.sao_type[k] != b.sao_type[k] || (a.sao_type[k] == 2 && a.sao_class[k] != b.sao_class[k])) return false;
     for (int ci = 0; ci < 3; ++ci) {
@@ -493,11 +503,11 @@ struct CtuCoder {
   }
 
   // SAO parameters of CTU (cx, cy): those of its first 32x32 record block
-  MIVC_HD const CtuInfo& ctu_sao(int cx, int cy) const {
+  HV_FN const CtuInfo& ctu_sao(int cx, int cy) const {
     const int k = P->ctu64 ? 1 : 0;
     return ctu[(cy << k) * wctb + (cx << k)];
   }
-  MIVC_HD void write_sao(int rx, int ry) {
+  HV_BIG void write_sao(int rx, int ry) {
     const CtuInfo& t = ctu_sao(rx, ry);
     if (rx > 0 && same_sao(t, ctu_sao(rx - 1, ry))) {
       e.encode(1, ctx[CTX_SAO_MERGE]);
@@ -543,7 +553,7 @@ struct CtuCoder {
   }
 
   // ---------------------------------------------------------------- residual coding (7.3.8.11)
-  MIVC_HD void write_last(int v, int log2, int cidx, int ctx_base) {
+  HV_FN void write_last(int v, int log2, int cidx, int ctx_base) {
     const int prefix = kLastGroup[v];
     const int cmax = (log2 << 1) - 1;
     int off, shift;
@@ -557,12 +567,12 @@ struct CtuCoder {
     for (int i = 0; i < prefix; ++i) e.encode(1, ctx[ctx_base + off + (i >> shift)]);
     if (prefix < cmax) e.encode(0, ctx[ctx_base + off + (prefix >> shift)]);
   }
-  MIVC_HD void write_last_suffix(int v) {
+  HV_FN void write_last_suffix(int v) {
     const int prefix = kLastGroup[v];
     if (prefix > 3) e.bypass_bits(v - kLastGroupMin[prefix], (prefix >> 1) - 1);
   }
 
-  MIVC_HD void write_remaining(int v, int rice) {
+  HV_BIG void write_remaining(int v, int rice) {
     if (v < (3 << rice)) {
       const int len = v >> rice;
       e.bypass_bits((1u << (len + 1)) - 2, len + 1);
@@ -583,7 +593,7 @@ struct CtuCoder {
   }
 
   // levels of the 4x4 block at plane position (px, py) of component cidx (in the current CTB)
-  MIVC_HD void load4x4(int cidx, int px, int py, int16_t (&rows)[4][4]) {
+  HV_FN void load4x4(int cidx, int px, int py, int16_t (&rows)[4][4]) {
     if (lv.levels) {
       const int side = cidx ? 4 : 8, m = cidx ? 15 : 31;
       const int bit = ((py & m) >> 2) * side + ((px & m) >> 2);
@@ -609,7 +619,7 @@ struct CtuCoder {
     for (int r = 0; r < 4; ++r) memcpy(rows[r], b + static_cast<size_t>(r) * stride, sizeof(rows[r]));
   }
 
-  MIVC_HD static bool any_row(const int16_t (&rows)[4][4]) {
+  HV_FN static bool any_row(const int16_t (&rows)[4][4]) {
     uint64_t a = 0;
     for (int r = 0; r < 4; ++r) {
       uint64_t w;
@@ -622,7 +632,7 @@ struct CtuCoder {
   // residual_coding of the (1 << log2)^2 block of component cidx at plane position (bx0, by0);
   // gmask: bit (ys * nsb + xs) set for every non-zero 4x4 sub-block of the TU (from the CTB's
   // sub-block map), so all-zero sub-blocks are never loaded
-  MIVC_HD void write_residual(int cidx, int bx0, int by0, int log2, int scan_idx, uint64_t gmask) {
+  HV_BIG void write_residual(int cidx, int bx0, int by0, int log2, int scan_idx, uint64_t gmask) {
     const int log2sb = log2 - 2, nsb = 1 << log2sb, nsbsq = nsb * nsb;
     const uint8_t* sbs = kScans.t[scan_idx][log2sb];
     const uint8_t* ps = kScans.t[scan_idx][2];
@@ -760,9 +770,9 @@ struct CtuCoder {
     }
   }
 
-  MIVC_HD static int mdcs(int mode) { return (mode >= 6 && mode <= 14) ? 2 : ((mode >= 22 && mode <= 30) ? 1 : 0); }
+  HV_FN static int mdcs(int mode) { return (mode >= 6 && mode <= 14) ? 2 : ((mode >= 22 && mode <= 30) ? 1 : 0); }
 
-  MIVC_HD void scan_ctb_nz(int x0, int y0) {
+  HV_BIG void scan_ctb_nz(int x0, int y0) {
     const size_t ci = static_cast<size_t>(y0 / kCtb) * wctb + x0 / kCtb;
     if (lv.nzmap) {
       nz_luma = lv.nzmap[2 * ci];
@@ -801,7 +811,7 @@ struct CtuCoder {
   }
   // sub-block mask of an n x n block at plane position (x, y) inside the current CTB, in
   // the block's own raster order (bit ys * (n / 4) + xs)
-  MIVC_HD uint64_t block_mask(int cidx, int x, int y, int n) const {
+  HV_FN uint64_t block_mask(int cidx, int x, int y, int n) const {
     const int side = cidx ? 4 : 8, m = cidx ? 15 : 31;
     const uint64_t src = cidx ? nz_chroma[cidx - 1] : nz_luma;
     const int bx0 = (x & m) >> 2, by0 = (y & m) >> 2, nb = n >> 2;
@@ -809,20 +819,20 @@ struct CtuCoder {
     for (int r = 0; r < nb; ++r) out |= ((src >> ((by0 + r) * side + bx0)) & ((1ull << nb) - 1ull)) << (r * nb);
     return out;
   }
-  MIVC_HD bool any_nonzero(int cidx, int x, int y, int n) const { return block_mask(cidx, x, y, n) != 0; }
+  HV_FN bool any_nonzero(int cidx, int x, int y, int n) const { return block_mask(cidx, x, y, n) != 0; }
 
   // ---------------------------------------------------------------- inter prediction helpers
   // A PU's motion is its direction (bit 0 list 0, bit 1 list 1) and a refIdx + vector per used
   // list; RefPicListX holds num_ref[X] pictures (POC list_poc(X, i)).
-  MIVC_HD bool inter_avail(int x, int y) const { return avail(x, y) && S.pred[g(x, y)] == CU_INTER; }
-  MIVC_HD const Motion& mot_at(int x, int y) const { return S.mot[g(x, y)]; }
-  MIVC_HD int ref_poc(int l) const {
+  HV_FN bool inter_avail(int x, int y) const { return avail(x, y) && S.pred[g(x, y)] == CU_INTER; }
+  HV_FN const Motion& mot_at(int x, int y) const { return S.mot[g(x, y)]; }
+  HV_FN int ref_poc(int l) const {
     return l == 0 ? (P->ref_poc[0] >= 0 ? P->ref_poc[0] : P->poc - 1) : P->ref_poc[1];
   }
-  MIVC_HD int nref(int l) const { return hv_max(1, P->num_ref[l]); }
-  MIVC_HD int list_poc(int l, int i) const { return i == 0 ? ref_poc(l) : P->list_poc[l][i]; }
+  HV_FN int nref(int l) const { return hv_max(1, P->num_ref[l]); }
+  HV_FN int list_poc(int l, int i) const { return i == 0 ? ref_poc(l) : P->list_poc[l][i]; }
 
-  MIVC_HD static Mv scale_mv(Mv v, int td0, int tb0) {  // 8.5.3.2.8 (8-209 .. 8-213)
+  HV_FN static Mv scale_mv(Mv v, int td0, int tb0) {  // 8.5.3.2.8 (8-209 .. 8-213)
     const int td = hv_clamp(td0, -128, 127), tb = hv_clamp(tb0, -128, 127);
     const int tx = (16384 + (hv_abs(td) >> 1)) / td;
     const int dsf = hv_clamp((tb * tx + 32) >> 6, -4096, 4095);
@@ -833,7 +843,7 @@ struct CtuCoder {
   }
 
   // 8.5.3.2.8 / 8.5.3.2.9 temporal vector of list X (target refIdx ri) for the PU (x, y, n x n)
-  MIVC_HD bool col_at(int xc, int yc, int X, int ri, Mv* out) {
+  HV_BIG bool col_at(int xc, int yc, int X, int ri, Mv* out) {
     if (!col_cu || xc >= W || yc >= H) return false;
     const int ci = (yc >> kCtbLog2) * wctb + (xc >> kCtbLog2);
     const CuInfo& cc = col_cu[static_cast<size_t>(ci) * kCusPerCtb + zorder8((xc & (kCtb - 1)) >> 3, (yc & (kCtb - 1)) >> 3)];
@@ -855,7 +865,7 @@ struct CtuCoder {
     *out = v;
     return true;
   }
-  MIVC_HD bool temporal(int x, int y, int n, int X, int ri, Mv* out) {
+  HV_FN bool temporal(int x, int y, int n, int X, int ri, Mv* out) {
     if (!tmvp) return false;
     const int xbr = x + n, ybr = y + n;
     if ((y >> L) == (ybr >> L) && ybr < H && xbr < W && col_at((xbr >> 4) << 4, (ybr >> 4) << 4, X, ri, out))
@@ -864,7 +874,7 @@ struct CtuCoder {
   }
 
   // 8.5.3.2.2-8.5.3.2.5 merge candidates of a 2Nx2N PU (MaxNumMergeCand entries)
-  MIVC_HD int merge_list(int x, int y, int n, Motion* out) {
+  HV_BIG int merge_list(int x, int y, int n, Motion* out) {
     Motion cand[8];
     int k = 0;
     const Motion none = motion_none();
@@ -921,7 +931,7 @@ struct CtuCoder {
   }
 
   // a neighbour vector pointing at the target picture (8.5.3.2.7, no scaling)
-  MIVC_HD bool amvp_same(int xn, int yn, int X, int tgt, Mv* v) const {
+  HV_FN bool amvp_same(int xn, int yn, int X, int tgt, Mv* v) const {
     const Motion& m = mot_at(xn, yn);
     const int Y = 1 - X;
     if ((m.dir >> X) & 1 && list_poc(X, m.r[X]) == tgt) {
@@ -935,7 +945,7 @@ struct CtuCoder {
     return false;
   }
   // any vector of the neighbour, scaled by the POC distances
-  MIVC_HD bool amvp_scaled(int xn, int yn, int X, int tgt, Mv* v) const {
+  HV_FN bool amvp_scaled(int xn, int yn, int X, int tgt, Mv* v) const {
     const Motion& m = mot_at(xn, yn);
     for (int j = 0; j < 2; ++j) {
       const int Lx = j == 0 ? X : 1 - X;
@@ -948,7 +958,7 @@ struct CtuCoder {
   }
 
   // 8.5.3.2.6-8.5.3.2.7 AMVP candidates of list X, refIdx ri
-  MIVC_HD void amvp_list(int x, int y, int n, int X, int ri, Mv* out) {
+  HV_BIG void amvp_list(int x, int y, int n, int X, int ri, Mv* out) {
     const int tgt = list_poc(X, ri);
     const int xa[2] = {x - 1, x - 1}, ya[2] = {y + n, y + n - 1};
     const bool ava[2] = {inter_avail(xa[0], ya[0]), inter_avail(xa[1], ya[1])};
@@ -983,7 +993,7 @@ struct CtuCoder {
   }
 
   // ---------------------------------------------------------------- coding unit (7.3.8.5)
-  MIVC_HD void mark(int x, int y, int n, int d, int sk, int pm, int md, const Motion& mv) {
+  HV_FN void mark(int x, int y, int n, int d, int sk, int pm, int md, const Motion& mv) {
     for (int yy = y; yy < y + n; yy += 8)
       for (int xx = x; xx < x + n; xx += 8) {
         const size_t k = g(xx, yy);
@@ -997,21 +1007,21 @@ struct CtuCoder {
   }
 
   // inter_pred_idc (9.3.3.7, 2Nx2N PU of a CU at depth d): PRED_BI "1", PRED_L0 "00", PRED_L1 "01"
-  MIVC_HD void write_inter_pred_idc(int dir, int d) {
+  HV_FN void write_inter_pred_idc(int dir, int d) {
     e.encode(dir == DIR_BI, ctx[CTX_INTER_PRED + d]);
     if (dir != DIR_BI) e.encode(dir == DIR_L1, ctx[CTX_INTER_PRED + 4]);
   }
 
   // a CU, then the QpY of its granules (8.6.1: the quantization group's prediction until a
   // cu_qp_delta has been coded, the coded QP from then on)
-  MIVC_HD void write_cu(int x, int y, int log2, int d) {
+  HV_FN void write_cu(int x, int y, int log2, int d) {
     write_cu_body(x, y, log2, d);
     const int q = qp_coded ? qp_ctb : qp_pred_cur, n = 1 << log2;
     for (int yy = y; yy < y + n; yy += 8)
       for (int xx = x; xx < x + n; xx += 8) S.qpy[g(xx, yy)] = static_cast<int8_t>(q);
   }
 
-  MIVC_HD Motion cu_motion(const CuInfo& ci) const {
+  HV_FN Motion cu_motion(const CuInfo& ci) const {
     Motion mv = motion_none();
     mv.dir = static_cast<uint8_t>(cu_dir(ci));
     mv.r[0] = static_cast<int8_t>(ci.pad[0]);
@@ -1021,7 +1031,7 @@ struct CtuCoder {
     return mv;
   }
 
-  MIVC_HD void write_cu_body(int x, int y, int log2, int d) {
+  HV_BIG void write_cu_body(int x, int y, int log2, int d) {
     const int n = 1 << log2;
     const CuInfo& ci = cu_at(x, y);
     const bool cb_y = any_nonzero(0, x, y, n);
@@ -1154,7 +1164,7 @@ struct CtuCoder {
 
   // MPM candidate (8.4.2) from the neighbour (xn, yn) of the PU at row yk of the CU at (x, y)
   // with PUs of size h and modes m
-  MIVC_HD int mpm_cand(int x, int y, int h, const int* m, int xn, int yn, int yk, bool above) const {
+  HV_FN int mpm_cand(int x, int y, int h, const int* m, int xn, int yn, int yk, bool above) const {
     if (xn >= x && yn >= y) return m[(xn - x >= h) + 2 * (yn - y >= h)];
     if (!avail(xn, yn) || S.pred[g(xn, yn)] != CU_INTRA) return 1;
     if (above && (yn >> L) != (yk >> L)) return 1;
@@ -1165,7 +1175,7 @@ struct CtuCoder {
   // split_transform_flag inferred (IntraSplitFlag), four 4x4 luma TUs with cbf_luma at
   // depth 1; cbfChroma of every 4x4 TU is the parent's, and the 4x4 chroma blocks follow
   // the last luma TU (blkIdx 3)
-  MIVC_HD void write_tu_nxn(int x, int y, const int* m, bool cb_cb, bool cb_cr) {
+  HV_BIG void write_tu_nxn(int x, int y, const int* m, bool cb_cb, bool cb_cr) {
     e.encode(cb_cb, ctx[CTX_CBF_CHROMA + 0]);
     e.encode(cb_cr, ctx[CTX_CBF_CHROMA + 0]);
     for (int k = 0; k < 4; ++k) {
@@ -1180,7 +1190,7 @@ struct CtuCoder {
   }
 
   // ref_idx_lX (9.3.3.1 TR, cMax = num_ref_idx_active - 1): two context-coded bins, then bypass
-  MIVC_HD void write_ref_idx(int r, int cmax) {
+  HV_FN void write_ref_idx(int r, int cmax) {
     for (int i = 0; i < cmax; ++i) {
       const int b = r > i;
       if (i < 2) e.encode(b, ctx[CTX_REF_IDX + i]);
@@ -1189,13 +1199,13 @@ struct CtuCoder {
     }
   }
 
-  MIVC_HD void write_merge_idx(int idx) {
+  HV_FN void write_merge_idx(int idx) {
     if (P->max_merge <= 1) return;
     e.encode(idx > 0, ctx[CTX_MERGE_IDX]);
     for (int k = 1; k < P->max_merge - 1 && idx >= k; ++k) e.bypass(idx > k);
   }
 
-  MIVC_HD void write_mvd_pair(int dx, int dy) {
+  HV_FN void write_mvd_pair(int dx, int dy) {
     const int ax = hv_abs(dx), ay = hv_abs(dy);
     e.encode(ax > 0, ctx[CTX_MVD_G0]);
     e.encode(ay > 0, ctx[CTX_MVD_G0]);
@@ -1214,7 +1224,7 @@ struct CtuCoder {
   // inter CU whose residual quadtree splits once (CuInfo flags bit 4): split_transform_flag,
   // chroma cbfs at depth 0, then per quarter TU (z-order) its chroma cbfs under a set parent,
   // cbf_luma (always coded below depth 0) and the transform unit
-  MIVC_HD void write_tu_inter_split(int x, int y, int log2, bool cb_cb, bool cb_cr) {
+  HV_BIG void write_tu_inter_split(int x, int y, int log2, bool cb_cb, bool cb_cr) {
     if (P->tu_inter_depth < 1 || log2 < 4) fail(CE_INTER_SPLIT);
     e.encode(1, ctx[CTX_SPLIT_TRANSFORM + 5 - log2]);
     e.encode(cb_cb, ctx[CTX_CBF_CHROMA + 0]);
@@ -1236,7 +1246,7 @@ struct CtuCoder {
   }
 
   // transform_tree at depth 0 with TU = CU (7.3.8.8 / 7.3.8.10)
-  MIVC_HD void write_tu(int x, int y, int log2, bool intra, int m, bool cb_y, bool cb_cb, bool cb_cr) {
+  HV_BIG void write_tu(int x, int y, int log2, bool intra, int m, bool cb_y, bool cb_cb, bool cb_cr) {
     // split_transform_flag 0 where the inter depth allows a split (intra: depth 0 at 2Nx2N)
     if (!intra && P->tu_inter_depth > 0 && log2 > 2) e.encode(0, ctx[CTX_SPLIT_TRANSFORM + 5 - log2]);
     e.encode(cb_cb, ctx[CTX_CBF_CHROMA + 0]);
@@ -1256,7 +1266,7 @@ struct CtuCoder {
 
   // cu_qp_delta_abs (9.3.3.10: TR prefix cMax 5, ctxInc 0 then 1; EG0 bypass suffix) and
   // the bypass sign, in the first TU of the quantization group with a coded block
-  MIVC_HD void write_qp_delta() {
+  HV_BIG void write_qp_delta() {
     const int d = qp_ctb - qp_pred_cur;
     const int qbd = 6 * (P->bit_depth - 8);
     if (d < -(26 + qbd / 2) || d > 25 + qbd / 2) fail(CE_QP_DELTA);
@@ -1267,7 +1277,7 @@ struct CtuCoder {
     if (a) e.bypass(d < 0);
     qp_coded = true;
   }
-  MIVC_HD void write_egk(uint32_t v, int k) {  // 9.3.3.3 k-th order Exp-Golomb, bypass
+  HV_FN void write_egk(uint32_t v, int k) {  // 9.3.3.3 k-th order Exp-Golomb, bypass
     while (v >= (1u << k)) {
       e.bypass(1);
       v -= 1u << k;
@@ -1279,7 +1289,7 @@ struct CtuCoder {
 
   // qPY_PRED of the quantization group at (xq, yq) (8.6.1): the average of the QpY left of and
   // above it when those lie in the same CTB, each replaced by qPY_PREV otherwise
-  MIVC_HD int qg_pred(int xq, int yq) const {
+  HV_FN int qg_pred(int xq, int yq) const {
     const bool la = avail(xq - 1, yq) && ((xq - 1) >> L) == (xq >> L) && (yq >> L) == (yq >> L);
     const bool lb = avail(xq, yq - 1) && (xq >> L) == (xq >> L) && ((yq - 1) >> L) == (yq >> L);
     const int qa = la ? S.qpy[g(xq - 1, yq)] : qp_prev;
@@ -1288,7 +1298,7 @@ struct CtuCoder {
   }
 
   // coding_quadtree (7.3.8.4) of one CTU (CTU coordinates)
-  MIVC_HD void write_ctu(int cx, int cy) {
+  HV_BIG void write_ctu(int cx, int cy) {
     if (!P->ctu64) {
       write_block_tree(cx, cy, 0);
       return;
@@ -1307,12 +1317,12 @@ struct CtuCoder {
     }
   }
 
-  MIVC_HD int split_ctx(int x, int y, int d) const {
+  HV_FN int split_ctx(int x, int y, int d) const {
     return (avail(x - 1, y) && S.depth[g(x - 1, y)] > d) + (avail(x, y - 1) && S.depth[g(x, y - 1)] > d);
   }
 
   // one 32x32 record block = one quantization group; dofs: its depth in the CTU quadtree
-  MIVC_HD void write_block_tree(int rx, int ry, int dofs) {
+  HV_BIG void write_block_tree(int rx, int ry, int dofs) {
     const CtuInfo& t = ctu[ry * wctb + rx];
     const int x0 = rx * kCtb, y0 = ry * kCtb;
     qp_ctb = t.qp;
@@ -1343,7 +1353,7 @@ struct CtuCoder {
   // one motion, no level anywhere, and that motion is in the 64x64 CU's merge list (the
   // reconstruction is the same: motion compensation is per sample and every inner edge has
   // boundary strength 0)
-  MIVC_HD bool cu64_ok(int cx, int cy) {
+  HV_BIG bool cu64_ok(int cx, int cy) {
     const int x0 = cx << 6, y0 = cy << 6;
     if (!inter_slice) return false;
     Motion m0 = motion_none();
@@ -1371,7 +1381,7 @@ struct CtuCoder {
     cu64_mot = m0;
     return cu64_midx >= 0;
   }
-  MIVC_HD void write_cu64_skip(int x0, int y0) {
+  HV_FN void write_cu64_skip(int x0, int y0) {
     const int skip_ctx = (avail(x0 - 1, y0) && S.skip[g(x0 - 1, y0)]) + (avail(x0, y0 - 1) && S.skip[g(x0, y0 - 1)]);
     e.encode(1, ctx[CTX_CU_SKIP + skip_ctx]);
     write_merge_idx(cu64_midx);
@@ -1386,7 +1396,7 @@ struct CtuCoder {
 
   // SAO + coding quadtree of CTU (rx, ry) and its end_of_slice_segment_flag; with WPP, a
   // row's last CTU also codes end_of_subset_one_bit, flushes and byte-aligns its substream
-  MIVC_HD void code_ctu(int rx, int ry) {
+  HV_BIG void code_ctu(int rx, int ry) {
     if (P->sao) write_sao(rx, ry);
     write_ctu(rx, ry);
     const bool last = ry == P->hctu - 1 && rx == P->wctu - 1;

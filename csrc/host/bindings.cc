@@ -854,6 +854,68 @@ PYBIND11_MODULE(_host, m) {
       },
       py::arg("cfg"), py::arg("frame"), py::arg("ctu"), py::arg("cu"), py::arg("nzmap"), py::arg("ctb_off"),
       py::arg("levels"));
+  m.def("hevc_coder_pic", [](const py::dict& cfg, const py::dict& fp) {
+    // the GPU entropy kernel's view of a picture (hevc_ctu_coder.h CoderPic) as bytes
+    const hevc::HevcConfig c = hevc_cfg_from(cfg);
+    std::vector<py::array> keep;
+    const hevc::HevcFrameParams f =
+        hevc_frame_from(fp, keep, static_cast<size_t>(c.wctb()) * c.hctb() * hevc::kCusPerCtb * hevc::kCuInfoBytes);
+    const hevc::CoderPic p = hevc::hevc_coder_pic(c, f);
+    return py::bytes(reinterpret_cast<const char*>(&p), sizeof(p));
+  });
+  m.def(
+      "hevc_assemble_slices",
+      [](const py::dict& cfg, const py::list& frames, py::array_t<uint8_t, py::array::c_style> data,
+         py::array_t<uint64_t, py::array::c_style> offs, py::array_t<uint32_t, py::array::c_style> sizes,
+         py::array_t<int32_t, py::array::c_style> errs, int threads) {
+        // slice NALs of B pictures whose substreams the GPU coded (kernels/hevc_entropy.hip):
+        // substream r of picture b is data[offs[b * nsub + r] ..][: sizes[b * nsub + r]]
+        const hevc::HevcConfig c = hevc_cfg_from(cfg);
+        const py::ssize_t B = static_cast<py::ssize_t>(frames.size());
+        const int nsub = c.wpp ? c.hctu() : 1;
+        const py::ssize_t n = B * nsub;
+        if (offs.size() < n + 1 || sizes.size() < n || errs.size() < n) throw std::runtime_error("substream tables: wrong size");
+        const uint64_t* po = offs.data();
+        const uint32_t* psz = sizes.data();
+        for (py::ssize_t i = 0; i < n; ++i) {
+          if (errs.data()[i] != 0)
+            throw std::runtime_error("HEVC slice " + std::to_string(i / nsub) + ": " + hevc::coder_error_text(errs.data()[i]));
+          if (po[i] + psz[i] > static_cast<uint64_t>(data.size())) throw std::runtime_error("substream outside the buffer");
+        }
+        std::vector<hevc::HevcFrameParams> fps(B);
+        std::vector<py::array> keep;
+        for (py::ssize_t b = 0; b < B; ++b) fps[b] = hevc_frame_from(frames[b].cast<py::dict>(), keep, 0);
+        std::vector<std::vector<uint8_t>> nals(B);
+        std::vector<std::string> msg(B);
+        {
+          py::gil_scoped_release rel;
+          std::atomic<py::ssize_t> next{0};
+          auto work = [&] {
+            std::vector<const uint8_t*> ptr(nsub);
+            for (py::ssize_t b = next++; b < B; b = next++) {
+              try {
+                for (int r = 0; r < nsub; ++r) ptr[r] = data.data() + po[b * nsub + r];
+                nals[b] = hevc::hevc_assemble_slice(c, fps[b], ptr.data(), psz + b * nsub, nsub);
+              } catch (const std::exception& e) {
+                msg[b] = e.what();
+              }
+            }
+          };
+          const int nt = std::max(1, std::min<int>(threads, static_cast<int>(B)));
+          std::vector<std::thread> pool;
+          for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+          work();
+          for (std::thread& th : pool) th.join();
+        }
+        py::list out;
+        for (py::ssize_t b = 0; b < B; ++b) {
+          if (!msg[b].empty()) throw std::runtime_error("HEVC slice " + std::to_string(b) + ": " + msg[b]);
+          out.append(to_bytes(nals[b]));
+        }
+        return out;
+      },
+      py::arg("cfg"), py::arg("frames"), py::arg("data"), py::arg("offs"), py::arg("sizes"), py::arg("errs"),
+      py::arg("threads") = 1);
   m.def(
       "hevc_write_slices_packed",
       [](const py::dict& cfg, const py::list& frames, py::array_t<uint8_t, py::array::c_style> ctu,

@@ -9,11 +9,18 @@
 #include <stdexcept>
 #include <vector>
 
+#include "../common/hevc_ctu_coder.h"
 #include "hevc_decode.h"
 
 namespace py = pybind11;
 
 extern "C" {
+long long mivc_hevc_entropy_state_bytes(int W, int H);
+int mivc_launch_hevc_entropy(const void* pic, int B, const int* qp, const void* ctu, const void* cu, const void* col,
+                             const unsigned long long* nzmap, const int16_t* cy, const int16_t* cb, const int16_t* cr,
+                             uint8_t* state, long long state_bytes, uint8_t* out, unsigned cap, unsigned* sizes,
+                             int* errs, unsigned long long* offs, unsigned long long* offs_host, uint8_t* dst,
+                             unsigned long long dst_cap, int* overflow, void* stream);
 int mivc_launch_hevc_decode(const mivc::gpu::HevcDecParams* p, int stage, void* stream);
 void mivc_launch_synth(void* y, void* u, void* v, int width, int height, int slots, int frames, int frame0,
                        uint32_t seed, int bit_depth, int slot0, void* stream, int kind);
@@ -594,6 +601,25 @@ PYBIND11_MODULE(_hip, m) {
     if (!hp) throw std::invalid_argument("hevc_merge_refine: needs the half-sample planes");
     mivc_launch_hevc_merge_refine(B, wmb, hmb, P<uint8_t>(src), P<uint8_t>(ref), P<uint8_t>(hp), P<int16_t>(mv_in),
                                   P<int16_t>(mv_out), P<int>(cost), P<int16_t>(pm), P<int>(qp), P<int8_t>(aq), S(stream));
+  });
+  m.def("hevc_entropy_state_bytes", [](int W, int H) { return mivc_hevc_entropy_state_bytes(W, H); });
+  // GPU CABAC slice data of B pictures of one coding step (kernels/hevc_entropy.hip); `pic` is
+  // the step's hevc::CoderPic (host module hevc_coder_pic), substreams packed into pinned `dst`
+  m.def("hevc_entropy", [](py::bytes pic, int B, uintptr_t qp, uintptr_t ctu, uintptr_t cu, uintptr_t col,
+                           uintptr_t nzmap, uintptr_t cy, uintptr_t cb, uintptr_t cr, uintptr_t state,
+                           long long state_bytes, uintptr_t out, unsigned cap, uintptr_t sizes, uintptr_t errs,
+                           uintptr_t offs, uintptr_t offs_host, uintptr_t dst, unsigned long long dst_cap,
+                           uintptr_t overflow, uintptr_t stream) {
+    const std::string ps = pic;
+    if (ps.size() != sizeof(mivc::hevc::CoderPic)) throw std::invalid_argument("hevc_entropy: pic is not a CoderPic");
+    if (!ctu || !cu || !nzmap || !cy || !cb || !cr || !state || !out || !sizes || !errs || !offs || !offs_host || !dst)
+      throw std::invalid_argument("hevc_entropy: null buffer");
+    if (mivc_launch_hevc_entropy(ps.data(), B, P<int>(qp), P<void>(ctu), P<void>(cu), P<void>(col),
+                                 P<unsigned long long>(nzmap), P<int16_t>(cy), P<int16_t>(cb), P<int16_t>(cr),
+                                 P<uint8_t>(state), state_bytes, P<uint8_t>(out), cap, P<unsigned>(sizes), P<int>(errs),
+                                 P<unsigned long long>(offs), P<unsigned long long>(offs_host), P<uint8_t>(dst), dst_cap,
+                                 P<int>(overflow), S(stream)) != 0)
+      throw std::invalid_argument("hevc_entropy: unsupported geometry (substreams <= 100, cap % 16, state size)");
   });
   m.def("hevc_qp_fixup", [](int B, int W, int H, uintptr_t ctu, uintptr_t cu, uintptr_t qp, uintptr_t run, int wpp,
                             uintptr_t stream, int ctu64) {

@@ -1046,13 +1046,15 @@ extern "C" void mivc_launch_hevc_qp_fixup(int B, int W, int H, void* ctu, const 
 }
 
 // levels of B slots -> packed form: nzmap [B, nctb, 2] u64, off [B, nctb] u32, out: B slots of
-// cap_blocks 4x4 blocks (pinned host memory, device-visible); cnt: [B, nctb] int scratch
+// cap_blocks 4x4 blocks (pinned host memory, device-visible); cnt: [B, nctb] int scratch.
+// out == null: the sub-block maps only (the GPU entropy coder reads the level planes)
 extern "C" void mivc_launch_hevc_pack_levels(int B, int W, int H, const int16_t* cy, const int16_t* cb,
                                              const int16_t* cr, unsigned long long* nzmap, int* cnt, unsigned* off,
                                              long long cap_blocks, int16_t* out, int* err, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int nctb = (W / 32) * (H / 32);
   hipLaunchKernelGGL(hevc_nz_map, dim3(nctb, B), dim3(64), 0, s, W, H, cy, cb, cr, nzmap, cnt);
+  if (!out) return;
   hipLaunchKernelGGL(hevc_nz_scan, dim3(B), dim3(1024), 0, s, nctb, cnt, off, cap_blocks, err);
   hipLaunchKernelGGL(hevc_nz_pack, dim3(nctb, B), dim3(64), 0, s, W, H, cy, cb, cr, nzmap, off, cap_blocks, out);
 }

@@ -235,7 +235,8 @@ class PendingHevc:
 class GpuHevcEncoder:
     """Batched gfx950 HEVC encoder (Main / Main 10, CABAC)."""
 
-    def __init__(self, params: HevcParams, slots: int, device="cuda", entropy_threads: int | None = None):
+    def __init__(self, params: HevcParams, slots: int, device="cuda", entropy_threads: int | None = None,
+                 entropy: str | None = None):
         if params.width % 2 or params.height % 2:
             raise ValueError("width and height must be even")
         if params.bit_depth not in (8, 10):
@@ -339,6 +340,15 @@ class GpuHevcEncoder:
         # one Python worker hands each step's B pictures to the native batch writer, which
         # codes them on `entropy_threads` C++ threads with the GIL released
         self.entropy_threads = entropy_threads or min(16, os.cpu_count() or 4)
+        # entropy "gpu": the slice data is CABAC-coded on the device (kernels/hevc_entropy.hip,
+        # the host writer's coder) and only the slice headers, entry points and emulation
+        # prevention stay on the host; "host": the native writer codes the records on
+        # entropy_threads host threads (csrc/host/hevc_writer.cc)
+        self.entropy = (entropy or os.environ.get("MIVC_HEVC_ENTROPY", "gpu")).lower()
+        if self.entropy not in ("gpu", "host"):
+            raise ValueError("entropy must be 'gpu' or 'host'")
+        if self.entropy == "gpu":
+            self._alloc_entropy()
         self.pool = cf.ThreadPoolExecutor(max_workers=1)
         self._inflight: list = []               # encode_async batches not yet finished (oldest first)
         self._pending: list[list] = [[], [], []]  # CABAC jobs per pinned host buffer set
@@ -370,6 +380,44 @@ class GpuHevcEncoder:
         need = (inter >= intra_lb).view(self.B, self.hctb, 2, self.wctb, 2)
         self.ctb_need.copy_(need.any(dim=4).any(dim=2).view(self.B, self.nctb))
         return self.ctb_need
+
+    def _alloc_entropy(self) -> None:
+        """Device buffers of the GPU entropy stage: per-picture coder state, one bounded region
+        per substream (WPP: one per CTU row) and the collocated pictures' records per DPB slot;
+        the packed substreams go to pinned host sets (:meth:`_entropy_host`)."""
+        dev, B = self.dev, self.B
+        W, H = self.W, self.H
+        ctu_log2 = 6 if self.p.ctu64 else 5
+        wctu, hctu = -(-W // (1 << ctu_log2)), -(-H // (1 << ctu_log2))
+        self.ent_nsub = hctu if self.p.wpp else 1
+        if self.ent_nsub > 100:
+            raise ValueError("GPU entropy: at most 100 CTU rows (use entropy='host')")
+        # bytes per substream: 12 KiB per CTU of a row (about 2 bytes per 4:2:0 sample of a
+        # 64x64 CTU), the whole picture without WPP
+        per_ctu = 12288 if self.p.ctu64 else 3072
+        self.ent_cap = ((per_ctu * wctu * (1 if self.p.wpp else hctu)) + 15) // 16 * 16
+        self.ent_state_bytes = int(self.hip.hevc_entropy_state_bytes(W, H))
+        self.ent_state = torch.empty((B, self.ent_state_bytes), dtype=torch.uint8, device=dev)
+        self.ent_out = torch.empty((B * self.ent_nsub * self.ent_cap,), dtype=torch.uint8, device=dev)
+        n = B * self.ent_nsub
+        self.ent_sizes = torch.zeros((n,), dtype=torch.int32, device=dev)
+        self.ent_errs = torch.zeros((n,), dtype=torch.int32, device=dev)
+        self.ent_offs = torch.zeros((n + 1,), dtype=torch.int64, device=dev)
+        self.ent_over = torch.zeros((1,), dtype=torch.int32, device=dev)
+        # pinned output per host set: half a byte per luma sample of every picture of a step
+        self.ent_dst_cap = max(1 << 22, B * W * H // 2)
+        self.ent_host = None
+        self.col_cus = None  # per DPB slot: [B, nctb * 16, 16] records of the picture in it (TMVP)
+
+    def _entropy_host(self):
+        if self.ent_host is None:
+            n = self.B * self.ent_nsub
+
+            def pinned(shape, dtype):
+                return torch.empty(shape, dtype=dtype).pin_memory()
+            self.ent_host = [dict(dst=pinned((self.ent_dst_cap,), torch.uint8), offs=pinned((n + 1,), torch.int64),
+                                  sizes=pinned((n,), torch.int32), errs=pinned((n,), torch.int32)) for _ in range(3)]
+        return self.ent_host
 
     def _host_buffers(self):
         if self.host_bufs is None:
@@ -759,6 +807,7 @@ class GpuHevcEncoder:
         tmvp = bool(cfg.get("tmvp", 0))
         anchor_cu: dict = {}   # display index of a reference picture -> (host copy of its CU records or None, l0, l1)
         ref_lists: dict = {}   # display index of a reference picture -> its (l0, l1) display indices
+        anchor_meta: dict = {}  # (GPU entropy) display index of a reference picture -> (DPB slot, l0, l1, refs0)
         plan_refs = {pic.d: pic.kind for pic in plan if pic.ref}
         idr_d = 0              # display index of the latest IDR picture (POC 0)
         for t in range(F):
@@ -974,72 +1023,78 @@ class GpuHevcEncoder:
                     f.result()
                 pending[hb] = []
                 t_blocked += time.perf_counter() - tb
-            host = self._host_buffers()[hb]
             nzmap, nzoff = self.nzmaps[kb], self.nzoffs[kb]
-            # non-zero level blocks straight into this step's pinned host buffer
-            self.hip.hevc_pack_levels(B, self.W, self.H, p(self.coef[0]), p(self.coef[1]), p(self.coef[2]), p(nzmap),
-                                      p(self.nzcnt), p(nzoff), self.pack_cap, host[4].data_ptr(), p(self.err), s)
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(self.dev))
-            with torch.cuda.stream(self.copy_stream):
-                self.copy_stream.wait_event(ev)
-                for dst, src_t in zip(host[:4], (self.ctu, self.cu, nzmap, nzoff)):
-                    dst.copy_(src_t, non_blocking=True)
-                done = torch.cuda.Event()
-                done.record(self.copy_stream)
-                self.copy_done[kb].record(self.copy_stream)
-            ctu, cu = host[0].numpy(), host[1].numpy()
-            nz, off, lv = host[2].numpy().view(np.uint64), host[3].numpy().view(np.uint32), host[4].numpy()
-            t1 = time.perf_counter()
-            t_gpu += t1 - t0
             qcol = qps_c[:, t].copy()
             wrow = wps[t][0] if t in wps else None
+            if self.entropy == "gpu":
+                job = self._gpu_entropy_step(t, pic, idr_d, kb, hb, cfg, qps_d[t], qcol, wrow, tmvp, anchor_meta,
+                                             ref_lists, cabac_s)
+                t1 = time.perf_counter()
+                t_gpu += t1 - t0
+            else:
+                host = self._host_buffers()[hb]
+                # non-zero level blocks straight into this step's pinned host buffer
+                self.hip.hevc_pack_levels(B, self.W, self.H, p(self.coef[0]), p(self.coef[1]), p(self.coef[2]), p(nzmap),
+                                          p(self.nzcnt), p(nzoff), self.pack_cap, host[4].data_ptr(), p(self.err), s)
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(self.dev))
+                with torch.cuda.stream(self.copy_stream):
+                    self.copy_stream.wait_event(ev)
+                    for dst, src_t in zip(host[:4], (self.ctu, self.cu, nzmap, nzoff)):
+                        dst.copy_(src_t, non_blocking=True)
+                    done = torch.cuda.Event()
+                    done.record(self.copy_stream)
+                    self.copy_done[kb].record(self.copy_stream)
+                ctu, cu = host[0].numpy(), host[1].numpy()
+                nz, off, lv = host[2].numpy().view(np.uint64), host[3].numpy().view(np.uint32), host[4].numpy()
+                t1 = time.perf_counter()
+                t_gpu += t1 - t0
 
-            def job(done=done, pic=pic, qcol=qcol, ctu=ctu, cu=cu, nz=nz, off=off, lv=lv, i0=idr_d, wrow=wrow):
-                done.synchronize()
-                tj = time.perf_counter()
-                # POC counts display pictures from the latest IDR
-                base = dict(idr=int(pic.kind == "I"), poc=pic.d - i0, slice_type={"I": 2, "P": 1, "B": 0}[pic.kind],
-                            nal_ref=int(pic.ref), rps=[(rd - i0, int(u)) for rd, u in pic.rps])
-                if pic.kind != "I":
-                    base["ref_poc0"] = pic.l0 - i0
-                    if len(pic.refs0) > 1:
-                        base["refs0"] = [r - i0 for r in pic.refs0]
-                if pic.kind == "B":
-                    base["ref_poc1"] = pic.l1 - i0
-                col = None
-                if tmvp and pic.kind != "I":
-                    cd = pic.l1 if pic.kind == "B" else pic.l0
-                    col = anchor_cu[cd]
-                    base.update(col_poc=cd - i0, col_ref_poc0=col[1] - i0, col_ref_poc1=col[2] - i0)
-                    if len(col[3]) > 1:
-                        base["col_refs0"] = [r - i0 for r in col[3]]
-                fps = []
-                for b in range(B):
-                    fp = dict(base, qp=int(qcol[b]))
-                    if wrow is not None and wrow[b] is not None:
-                        fp["wp"] = wrow[b]
-                    if col is not None:
-                        fp["col_cu"] = None if col[0] is None else col[0][b]
-                    fps.append(fp)
-                if self.cu_stats is None:
-                    r = self.host.hevc_write_slices_packed(cfg, fps, ctu, cu, nz, off, lv, self.entropy_threads)
-                else:  # diagnostics: CU mix per picture type (tools/diag/hevc_bframe_stats.py)
-                    rs = self.host.hevc_write_slices_packed(cfg, fps, ctu, cu, nz, off, lv, self.entropy_threads, True)
-                    r = [n for n, _ in rs]
-                    agg = self.cu_stats.setdefault(pic.kind + ("ref" if pic.kind == "B" and pic.ref else ""), {})
-                    for _, stt in rs:
-                        for k_, v_ in stt.items():
-                            agg[k_] = agg.get(k_, 0) + v_
-                if tmvp and pic.ref:
-                    # later pictures' collocated records (the host buffer set is reused at t + 3);
-                    # only pictures still in the DPB can be collocated pictures
-                    anchor_cu[pic.d] = (None if pic.kind == "I" else cu[:B].copy(), pic.l0, pic.l1, pic.refs0)
-                    live = {rd for rd, _ in pic.rps} | {pic.d}
-                    for k in [k for k in anchor_cu if k not in live]:
-                        del anchor_cu[k]
-                cabac_s[0] += time.perf_counter() - tj
-                return r
+                def job(done=done, pic=pic, qcol=qcol, ctu=ctu, cu=cu, nz=nz, off=off, lv=lv, i0=idr_d, wrow=wrow):
+                    done.synchronize()
+                    tj = time.perf_counter()
+                    # POC counts display pictures from the latest IDR
+                    base = dict(idr=int(pic.kind == "I"), poc=pic.d - i0, slice_type={"I": 2, "P": 1, "B": 0}[pic.kind],
+                                nal_ref=int(pic.ref), rps=[(rd - i0, int(u)) for rd, u in pic.rps])
+                    if pic.kind != "I":
+                        base["ref_poc0"] = pic.l0 - i0
+                        if len(pic.refs0) > 1:
+                            base["refs0"] = [r - i0 for r in pic.refs0]
+                    if pic.kind == "B":
+                        base["ref_poc1"] = pic.l1 - i0
+                    col = None
+                    if tmvp and pic.kind != "I":
+                        cd = pic.l1 if pic.kind == "B" else pic.l0
+                        col = anchor_cu[cd]
+                        base.update(col_poc=cd - i0, col_ref_poc0=col[1] - i0, col_ref_poc1=col[2] - i0)
+                        if len(col[3]) > 1:
+                            base["col_refs0"] = [r - i0 for r in col[3]]
+                    fps = []
+                    for b in range(B):
+                        fp = dict(base, qp=int(qcol[b]))
+                        if wrow is not None and wrow[b] is not None:
+                            fp["wp"] = wrow[b]
+                        if col is not None:
+                            fp["col_cu"] = None if col[0] is None else col[0][b]
+                        fps.append(fp)
+                    if self.cu_stats is None:
+                        r = self.host.hevc_write_slices_packed(cfg, fps, ctu, cu, nz, off, lv, self.entropy_threads)
+                    else:  # diagnostics: CU mix per picture type (tools/diag/hevc_bframe_stats.py)
+                        rs = self.host.hevc_write_slices_packed(cfg, fps, ctu, cu, nz, off, lv, self.entropy_threads, True)
+                        r = [n for n, _ in rs]
+                        agg = self.cu_stats.setdefault(pic.kind + ("ref" if pic.kind == "B" and pic.ref else ""), {})
+                        for _, stt in rs:
+                            for k_, v_ in stt.items():
+                                agg[k_] = agg.get(k_, 0) + v_
+                    if tmvp and pic.ref:
+                        # later pictures' collocated records (the host buffer set is reused at t + 3);
+                        # only pictures still in the DPB can be collocated pictures
+                        anchor_cu[pic.d] = (None if pic.kind == "I" else cu[:B].copy(), pic.l0, pic.l1, pic.refs0)
+                        live = {rd for rd, _ in pic.rps} | {pic.d}
+                        for k in [k for k in anchor_cu if k not in live]:
+                            del anchor_cu[k]
+                    cabac_s[0] += time.perf_counter() - tj
+                    return r
 
             f = self.pool.submit(job)
             futs.append((t, f))
@@ -1049,6 +1104,89 @@ class GpuHevcEncoder:
         self.last_qps = qps.copy()
         return lambda: self._finish(futs, nals, B, F, h, w, bd, sse, metrics, keep_recon, recon, order, gate_sum,
                                     st, t_gpu, t_blocked, cabac_s)
+
+    @staticmethod
+    def _slice_base(pic, i0: int, col_meta) -> dict:
+        """Frame parameters shared by the B pictures of a coding step (POCs count display
+        pictures from the latest IDR ``i0``); ``col_meta``: (l0, l1, refs0) of the collocated
+        picture, or None."""
+        base = dict(idr=int(pic.kind == "I"), poc=pic.d - i0, slice_type={"I": 2, "P": 1, "B": 0}[pic.kind],
+                    nal_ref=int(pic.ref), rps=[(rd - i0, int(u)) for rd, u in pic.rps])
+        if pic.kind != "I":
+            base["ref_poc0"] = pic.l0 - i0
+            if len(pic.refs0) > 1:
+                base["refs0"] = [r - i0 for r in pic.refs0]
+        if pic.kind == "B":
+            base["ref_poc1"] = pic.l1 - i0
+        if col_meta is not None:
+            cd = pic.l1 if pic.kind == "B" else pic.l0
+            base.update(col_poc=cd - i0, col_ref_poc0=col_meta[0] - i0, col_ref_poc1=col_meta[1] - i0)
+            if len(col_meta[2]) > 1:
+                base["col_refs0"] = [r - i0 for r in col_meta[2]]
+        return base
+
+    def _gpu_entropy_step(self, t, pic, i0, kb, hb, cfg, qp_row, qcol, wrow, tmvp, anchor_meta, ref_lists, cabac_s):
+        """Issue coding step t's GPU entropy on the copy stream (after the step's records are
+        final): the nz maps, the CABAC substreams of the B pictures (kernels/hevc_entropy.hip)
+        packed into pinned host set ``hb``, and -- for a reference picture with TMVP -- a device
+        copy of its records for the pictures that will use it as collocated picture.  The
+        compute stream moves on to step t + 1 at once; buffers of step t are released through
+        ``copy_done[kb]``.  Returns the host job: the slice headers, entry points and emulation
+        prevention of the step's pictures (hevc_assemble_slices)."""
+        B, p = self.B, self._p
+        nzmap, nzoff = self.nzmaps[kb], self.nzoffs[kb]
+        eh = self._entropy_host()[hb]
+        col_meta, col_ptr = None, 0
+        if tmvp and pic.kind != "I":
+            cd = pic.l1 if pic.kind == "B" else pic.l0
+            slot, l0, l1, refs0 = anchor_meta[cd]
+            col_meta = (l0, l1, refs0)
+            col_ptr = p(self.col_cus[slot])
+        base = self._slice_base(pic, i0, col_meta)
+        pic_bytes = self.host.hevc_coder_pic(cfg, dict(base, qp=0))
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.dev))
+        cs = self.copy_stream
+        with torch.cuda.stream(cs):
+            cs.wait_event(ev)
+            sc = cs.cuda_stream
+            self.hip.hevc_pack_levels(B, self.W, self.H, p(self.coef[0]), p(self.coef[1]), p(self.coef[2]), p(nzmap),
+                                      p(self.nzcnt), p(nzoff), self.pack_cap, 0, p(self.err), sc)
+            self.hip.hevc_entropy(pic_bytes, B, p(qp_row), p(self.ctu), p(self.cu), col_ptr, p(nzmap), p(self.coef[0]),
+                                  p(self.coef[1]), p(self.coef[2]), p(self.ent_state), self.ent_state_bytes,
+                                  p(self.ent_out), self.ent_cap, p(self.ent_sizes), p(self.ent_errs), p(self.ent_offs),
+                                  eh["offs"].data_ptr(), eh["dst"].data_ptr(), self.ent_dst_cap, p(self.ent_over), sc)
+            eh["sizes"].copy_(self.ent_sizes, non_blocking=True)
+            eh["errs"].copy_(self.ent_errs, non_blocking=True)
+            if tmvp and pic.ref:
+                if self.col_cus is None:
+                    self.col_cus = [torch.empty_like(self.cus[0]) for _ in range(self.ref_slots)]
+                self.col_cus[pic.slot].copy_(self.cu, non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(cs)
+            self.copy_done[kb].record(cs)
+        if tmvp and pic.ref:
+            anchor_meta[pic.d] = (pic.slot, pic.l0, pic.l1, pic.refs0)
+        n = B * self.ent_nsub
+
+        def job(done=done, base=base, qcol=qcol, wrow=wrow, eh=eh):
+            done.synchronize()
+            tj = time.perf_counter()
+            offs = eh["offs"].numpy().view(np.uint64)
+            if int(offs[n]) > self.ent_dst_cap:
+                raise RuntimeError(f"HEVC GPU entropy: a step's slice data ({int(offs[n])} bytes) exceeds the host "
+                                   f"buffer ({self.ent_dst_cap}); encode with entropy='host'")
+            fps = []
+            for b in range(B):
+                fp = dict(base, qp=int(qcol[b]))
+                if wrow is not None and wrow[b] is not None:
+                    fp["wp"] = wrow[b]
+                fps.append(fp)
+            r = self.host.hevc_assemble_slices(cfg, fps, eh["dst"].numpy(), offs, eh["sizes"].numpy().view(np.uint32),
+                                               eh["errs"].numpy(), self.entropy_threads)
+            cabac_s[0] += time.perf_counter() - tj
+            return r
+        return job
 
     def _finish(self, futs, nals, B, F, h, w, bd, sse, metrics, keep_recon, recon, order, gate_sum, st, t_gpu,
                 t_blocked, cabac_s) -> list[HevcSegmentResult]:
