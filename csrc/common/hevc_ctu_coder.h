@@ -21,9 +21,11 @@
 #if defined(__HIPCC__)
 #define HV_FN __host__ __device__
 #define HV_BIG __host__ __device__ __attribute__((noinline))
+#define HV_CYCLES() __builtin_readcyclecounter()
 #else
 #define HV_FN inline
 #define HV_BIG inline
+#define HV_CYCLES() __builtin_ia32_rdtsc()
 #endif
 
 namespace mivc {
@@ -101,6 +103,19 @@ struct NextStateTable {
 };
 static constexpr NextStateTable kNextStateT{};
 
+// one word per (state, quarter of the range): rangeTabLps | next state after an LPS << 8 |
+// next state after an MPS << 16 -- a single table read per bin (the GPU coder keeps it in LDS)
+struct CabacStepTable {
+  uint32_t t[256];
+  constexpr CabacStepTable() : t() {
+    for (int s = 0; s < 64; ++s)
+      for (int q = 0; q < 4; ++q)
+        t[(s << 2) | q] = static_cast<uint32_t>(kRangeLps[s][q]) | (static_cast<uint32_t>(kTransIdxLps[s]) << 8) |
+                          (static_cast<uint32_t>(s < 62 ? s + 1 : s) << 16);
+  }
+};
+static constexpr CabacStepTable kCabacStep{};
+
 MIVC_HD int hv_clz32(uint32_t v) { return __builtin_clz(v); }
 
 // Arithmetic encoder (9.3.4.3): low / range with deferred carry (outstanding 0xFF bytes).
@@ -108,6 +123,7 @@ MIVC_HD int hv_clz32(uint32_t v) { return __builtin_clz(v); }
 template <class Sink>
 struct CabacEngine {
   Sink* out = nullptr;
+  const uint32_t* step = kCabacStep.t;  // CabacStepTable (or a copy of it in faster memory)
   uint32_t low_ = 0, range_ = 510;
   int bits_left_ = 23;
   int num_buffered_ = 0;
@@ -129,7 +145,8 @@ struct CabacEngine {
   MIVC_HD void encode(int bin, CtxState& c) {
     const uint32_t s = c.state, mps = c.mps;
     uint32_t range = range_, low = low_;
-    const uint32_t lps = kRangeLps[s][(range >> 6) & 3];
+    const uint32_t ent = step[(s << 2) | ((range >> 6) & 3)];
+    const uint32_t lps = ent & 0xFFu;
     const uint32_t rmps = range - lps;
     const bool is_lps = static_cast<uint32_t>(bin) != mps;
     const uint32_t r = is_lps ? lps : rmps;
@@ -141,7 +158,7 @@ struct CabacEngine {
     bits_left_ = left;
     ++bins_;
     c.mps = static_cast<uint8_t>(mps ^ static_cast<uint32_t>(is_lps && s == 0));
-    c.state = kNextStateT.t[is_lps][s];
+    c.state = static_cast<uint8_t>((ent >> (is_lps ? 8 : 16)) & 63u);
     if (left < 12) write_out();
   }
 
@@ -277,6 +294,9 @@ struct CoderLevels {
   const int16_t* levels = nullptr;
   size_t nblocks = 0;
   const int16_t* plane[3] = {nullptr, nullptr, nullptr};
+  // staged per CTU (GPU): `levels` holds the first `nblocks` non-zero blocks of the current CTU
+  // (its 32x32 blocks in z-order, each in packed order), the rest are read from the planes
+  int stage_ctu = 0;
 };
 
 // picture-wide state of coded CUs, one entry per 8x8 granule (mode4: per 4x4 block); shared by
@@ -329,6 +349,18 @@ inline const char* coder_error_text(int e) {
 
 struct CoderStats {
   int intra_cus = 0, inter_cus = 0, skip_cus = 0, merge_cus = 0;
+};
+
+// optional cycle accounting of the coder's parts (diagnostics): slot k of `acc` gets the cycles
+// spent inside the scope (cycle counter of the CPU / the GPU's s_memtime)
+enum CoderProf : int { CP_RESIDUAL = 0, CP_MERGE, CP_AMVP, CP_CU, CP_SAO, CP_CTU, CP_SCAN, CP_N };
+struct ProfScope {
+  uint64_t* acc;
+  uint64_t t0;
+  MIVC_HD ProfScope(uint64_t* a, int k) : acc(a ? a + k : nullptr), t0(a ? HV_CYCLES() : 0) {}
+  MIVC_HD ~ProfScope() {
+    if (acc) *acc += HV_CYCLES() - t0;
+  }
 };
 
 // ------------------------------------------------------------------ constant tables
@@ -443,14 +475,19 @@ struct CtuCoder {
   uint32_t ctb_base = 0;
   int cu64_midx = -1;
   Motion cu64_mot;
+  uint64_t* prof = nullptr;  // CP_N cycle counters (diagnostics), or null
+  // constant tables (kScans, kSig) or copies of them in faster memory (GPU LDS)
+  const uint8_t* scans_tab = &kScans.t[0][0][0];
+  const uint8_t* sig_tab = &kSig.t[0][0][0][0][0][0];
 
-  HV_FN void fail(int code) {
+  HV_FN void fail(int code) __restrict__ {
     if (err == CE_NONE) err = code;
   }
 
   // contexts initialised, engine started on `sink`
   HV_BIG void begin(const CoderPic* pic, const CtuInfo* ct, const CuInfo* cu_, const CuInfo* col, const CoderLevels& l,
-                     const CoderState& s, CtxState* ctx_mem, Sink* sink) {
+                     const CoderState& s, CtxState* ctx_mem, Sink* sink, const uint32_t* step_tab = nullptr,
+                     const uint8_t* scans = nullptr, const uint8_t* sig = nullptr) __restrict__ {
     P = pic;
     ctu = ct;
     cu = cu_;
@@ -459,7 +496,22 @@ struct CtuCoder {
     S = s;
     ctx = ctx_mem;
     e.out = sink;
+    e.step = step_tab ? step_tab : kCabacStep.t;
+    scans_tab = scans ? scans : &kScans.t[0][0][0];
+    sig_tab = sig ? sig : &kSig.t[0][0][0][0][0][0];
     e.start();
+    // every field set here: a coder may sit in raw (unconstructed) memory, e.g. GPU LDS
+    err = CE_NONE;
+    st = CoderStats();
+    qp_ctb = qp_pred_cur = 0;
+    qp_coded = false;
+    nz_luma = 0;
+    nz_chroma[0] = nz_chroma[1] = 0;
+    ctb_base = 0;
+    cu64_midx = -1;
+    cu_stage = nullptr;
+    stage_cx = stage_cy = -1;
+    prof = nullptr;
     W = P->W;
     H = P->H;
     wctb = P->wctb;
@@ -477,13 +529,20 @@ struct CtuCoder {
     cu64_mot = motion_none();
   }
 
-  HV_FN size_t g(int x, int y) const { return static_cast<size_t>(y >> 3) * w8 + (x >> 3); }
-  HV_FN size_t g4(int x, int y) const { return static_cast<size_t>(y >> 2) * (2 * w8) + (x >> 2); }
-  HV_FN bool inside(int x, int y) const { return x >= 0 && y >= 0 && x < W && y < H; }
+  HV_FN size_t g(int x, int y) const __restrict__ { return static_cast<size_t>(y >> 3) * w8 + (x >> 3); }
+  HV_FN size_t g4(int x, int y) const __restrict__ { return static_cast<size_t>(y >> 2) * (2 * w8) + (x >> 2); }
+  HV_FN bool inside(int x, int y) const __restrict__ { return x >= 0 && y >= 0 && x < W && y < H; }
   // 6.4.1 z-scan availability at 8x8 granularity (the granule is coded iff already visited)
-  HV_FN bool avail(int x, int y) const { return inside(x, y) && S.coded[g(x, y)]; }
+  HV_FN bool avail(int x, int y) const __restrict__ { return inside(x, y) && S.coded[g(x, y)]; }
 
-  HV_FN const CuInfo& cu_at(int x, int y) const {
+  // records of the current CTU staged in faster memory (GPU): [4 blocks in z-order][16 granules]
+  const CuInfo* cu_stage = nullptr;
+  int stage_cx = -1, stage_cy = -1;
+  HV_FN const CuInfo& cu_at(int x, int y) const __restrict__ {
+    if (cu_stage && (x >> L) == stage_cx && (y >> L) == stage_cy) {
+      const int q = L == 6 ? ((((y >> 5) & 1) << 1) | ((x >> 5) & 1)) : 0;
+      return cu_stage[q * kCusPerCtb + zorder8((x & (kCtb - 1)) >> 3, (y & (kCtb - 1)) >> 3)];
+    }
     const int ci = (y >> kCtbLog2) * wctb + (x >> kCtbLog2);
     return cu[static_cast<size_t>(ci) * kCusPerCtb + zorder8((x & (kCtb - 1)) >> 3, (y & (kCtb - 1)) >> 3)];
   }
@@ -503,11 +562,12 @@ struct CtuCoder {
   }
 
   // SAO parameters of CTU (cx, cy): those of its first 32x32 record block
-  HV_FN const CtuInfo& ctu_sao(int cx, int cy) const {
+  HV_FN const CtuInfo& ctu_sao(int cx, int cy) const __restrict__ {
     const int k = P->ctu64 ? 1 : 0;
     return ctu[(cy << k) * wctb + (cx << k)];
   }
-  HV_BIG void write_sao(int rx, int ry) {
+  HV_BIG void write_sao(int rx, int ry) __restrict__ {
+    const ProfScope prof_scope(prof, CP_SAO);
     const CtuInfo& t = ctu_sao(rx, ry);
     if (rx > 0 && same_sao(t, ctu_sao(rx - 1, ry))) {
       e.encode(1, ctx[CTX_SAO_MERGE]);
@@ -553,7 +613,8 @@ struct CtuCoder {
   }
 
   // ---------------------------------------------------------------- residual coding (7.3.8.11)
-  HV_FN void write_last(int v, int log2, int cidx, int ctx_base) {
+  template <class En>
+  HV_FN static void write_last(En& en, CtxState* cx, int v, int log2, int cidx, int ctx_base) {
     const int prefix = kLastGroup[v];
     const int cmax = (log2 << 1) - 1;
     int off, shift;
@@ -564,19 +625,21 @@ struct CtuCoder {
       off = 15;
       shift = log2 - 2;
     }
-    for (int i = 0; i < prefix; ++i) e.encode(1, ctx[ctx_base + off + (i >> shift)]);
-    if (prefix < cmax) e.encode(0, ctx[ctx_base + off + (prefix >> shift)]);
+    for (int i = 0; i < prefix; ++i) en.encode(1, cx[ctx_base + off + (i >> shift)]);
+    if (prefix < cmax) en.encode(0, cx[ctx_base + off + (prefix >> shift)]);
   }
-  HV_FN void write_last_suffix(int v) {
+  template <class En>
+  HV_FN static void write_last_suffix(En& en, int v) {
     const int prefix = kLastGroup[v];
-    if (prefix > 3) e.bypass_bits(v - kLastGroupMin[prefix], (prefix >> 1) - 1);
+    if (prefix > 3) en.bypass_bits(v - kLastGroupMin[prefix], (prefix >> 1) - 1);
   }
 
-  HV_BIG void write_remaining(int v, int rice) {
+  template <class En>
+  HV_FN static void write_remaining(En& en, int v, int rice) {
     if (v < (3 << rice)) {
       const int len = v >> rice;
-      e.bypass_bits((1u << (len + 1)) - 2, len + 1);
-      e.bypass_bits(v & ((1 << rice) - 1), rice);
+      en.bypass_bits((1u << (len + 1)) - 2, len + 1);
+      en.bypass_bits(v & ((1 << rice) - 1), rice);
     } else {
       int len = rice;
       int s = v - (3 << rice);
@@ -586,14 +649,14 @@ struct CtuCoder {
       }
       const int ones = 3 + len + 1 - rice;
       // ones-1 ones and a zero, then len bits
-      for (int i = 0; i < ones - 1; ++i) e.bypass(1);
-      e.bypass(0);
-      e.bypass_bits(static_cast<uint32_t>(s), len);
+      for (int i = 0; i < ones - 1; ++i) en.bypass(1);
+      en.bypass(0);
+      en.bypass_bits(static_cast<uint32_t>(s), len);
     }
   }
 
   // levels of the 4x4 block at plane position (px, py) of component cidx (in the current CTB)
-  HV_FN void load4x4(int cidx, int px, int py, int16_t (&rows)[4][4]) {
+  HV_FN void load4x4(int cidx, int px, int py, int16_t (&rows)[4][4]) __restrict__ {
     if (lv.levels) {
       const int side = cidx ? 4 : 8, m = cidx ? 15 : 31;
       const int bit = ((py & m) >> 2) * side + ((px & m) >> 2);
@@ -606,13 +669,15 @@ struct CtuCoder {
         rank += static_cast<uint32_t>(__builtin_popcount(nz_chroma[cidx - 1] & ((1u << bit) - 1u)));
       }
       const size_t at = static_cast<size_t>(ctb_base) + rank;
-      if (at >= lv.nblocks) {
+      if (at < lv.nblocks) {
+        memcpy(rows, lv.levels + at * 16, 32);
+        return;
+      }
+      if (!lv.plane[0]) {
         fail(CE_PACKED_RANGE);
         memset(rows, 0, 32);
         return;
       }
-      memcpy(rows, lv.levels + at * 16, 32);
-      return;
     }
     const int stride = cidx ? W / 2 : W;
     const int16_t* b = lv.plane[cidx] + static_cast<size_t>(py) * stride + px;
@@ -632,10 +697,11 @@ struct CtuCoder {
   // residual_coding of the (1 << log2)^2 block of component cidx at plane position (bx0, by0);
   // gmask: bit (ys * nsb + xs) set for every non-zero 4x4 sub-block of the TU (from the CTB's
   // sub-block map), so all-zero sub-blocks are never loaded
-  HV_BIG void write_residual(int cidx, int bx0, int by0, int log2, int scan_idx, uint64_t gmask) {
+  HV_BIG void write_residual(int cidx, int bx0, int by0, int log2, int scan_idx, uint64_t gmask) __restrict__ {
+    const ProfScope prof_scope(prof, CP_RESIDUAL);
     const int log2sb = log2 - 2, nsb = 1 << log2sb, nsbsq = nsb * nsb;
-    const uint8_t* sbs = kScans.t[scan_idx][log2sb];
-    const uint8_t* ps = kScans.t[scan_idx][2];
+    const uint8_t* sbs = scans_tab + (scan_idx * 4 + log2sb) * 64;
+    const uint8_t* ps = scans_tab + (scan_idx * 4 + 2) * 64;
     // last significant group / position
     int last_i = -1, last_p = -1;
     int16_t lvx[16];
@@ -656,16 +722,20 @@ struct CtuCoder {
       fail(CE_ALL_ZERO_BLOCK);
       return;
     }
+    // the engine state in locals for the block (registers on the device; the member lives in
+    // memory because the coder's address crosses the out-of-line calls)
+    CabacEngine<Sink> en = e;
+    CtxState* const cx = ctx;  // a local: stores through the contexts cannot move it
     int lx = (sbs[last_i] & 15) * 4 + (ps[last_p] & 15), ly = (sbs[last_i] >> 4) * 4 + (ps[last_p] >> 4);
     if (scan_idx == 2) {
       const int t = lx;
       lx = ly;
       ly = t;
     }
-    write_last(lx, log2, cidx, CTX_LAST_X);
-    write_last(ly, log2, cidx, CTX_LAST_Y);
-    write_last_suffix(lx);
-    write_last_suffix(ly);
+    write_last(en, cx, lx, log2, cidx, CTX_LAST_X);
+    write_last(en, cx, ly, log2, cidx, CTX_LAST_Y);
+    write_last_suffix(en, lx);
+    write_last_suffix(en, ly);
 
     uint8_t csbf[8][8];
     memset(csbf, 0, sizeof(csbf));
@@ -692,7 +762,7 @@ struct CtuCoder {
         int cs = 0;
         if (xs < nsb - 1) cs += csbf[xs + 1][ys];
         if (ys < nsb - 1) cs += csbf[xs][ys + 1];
-        e.encode(nonzero, ctx[CTX_CSBF + hv_min(cs, 1) + (cidx ? 2 : 0)]);
+        en.encode(nonzero, cx[CTX_CSBF + hv_min(cs, 1) + (cidx ? 2 : 0)]);
         csbf[xs][ys] = nonzero;
         infer_dc = true;
       } else {
@@ -706,12 +776,13 @@ struct CtuCoder {
       // significance
       int vals[16], nsig = 0;
       if (i == last_i) vals[nsig++] = lvl[last_p];
-      const uint8_t* sct = kSig.t[log2 - 2][cidx ? 1 : 0][scan_idx][prev_csbf][xs + ys == 0 ? 1 : 0];
-      CtxState* sctx = ctx + CTX_SIG;
+      const uint8_t* sct = sig_tab + ((((log2 - 2) * 2 + (cidx ? 1 : 0)) * 3 + scan_idx) * 4 + prev_csbf) * 32 +
+                           (xs + ys == 0 ? 16 : 0);
+      CtxState* sctx = cx + CTX_SIG;
       for (int p = (i == last_i ? last_p - 1 : 15); p >= 0; --p) {
         const int v = lvl[p];
         if (p > 0 || !infer_dc) {
-          e.encode(v != 0, sctx[sct[p]]);
+          en.encode(v != 0, sctx[sct[p]]);
           if (v != 0) infer_dc = false;
         }
         if (v != 0) vals[nsig++] = v;
@@ -727,7 +798,7 @@ struct CtuCoder {
       for (int k = 0; k < nsig && k < 8; ++k) {
         const int a = hv_abs(vals[k]);
         g1[k] = a > 1;
-        e.encode(g1[k], ctx[CTX_GT1 + (cidx ? 16 : 0) + ctx_set * 4 + c1]);
+        en.encode(g1[k], cx[CTX_GT1 + (cidx ? 16 : 0) + ctx_set * 4 + c1]);
         if (g1[k]) {
           c1 = 0;
           if (g1_first < 0) g1_first = k;
@@ -738,7 +809,7 @@ struct CtuCoder {
       int g2 = 0;
       if (g1_first >= 0) {
         g2 = hv_abs(vals[g1_first]) > 2;
-        e.encode(g2, ctx[CTX_GT2 + (cidx ? 4 : 0) + ctx_set]);
+        en.encode(g2, cx[CTX_GT2 + (cidx ? 4 : 0) + ctx_set]);
       }
       uint32_t signs = 0;
       for (int k = 0; k < nsig; ++k) signs = (signs << 1) | (vals[k] < 0);
@@ -753,9 +824,9 @@ struct CtuCoder {
         int sum = 0;
         for (int k = 0; k < nsig; ++k) sum += hv_abs(vals[k]);
         if ((sum & 1) != (vals[nsig - 1] < 0 ? 1 : 0)) fail(CE_SDH_PARITY);
-        e.bypass_bits(signs >> 1, nsig - 1);
+        en.bypass_bits(signs >> 1, nsig - 1);
       } else {
-        e.bypass_bits(signs, nsig);
+        en.bypass_bits(signs, nsig);
       }
       int rice = 0;
       for (int k = 0; k < nsig; ++k) {
@@ -763,22 +834,35 @@ struct CtuCoder {
         const int base = 1 + (k < 8 ? g1[k] : 0) + (k == g1_first ? g2 : 0);
         const int thr = k < 8 ? (k == g1_first ? 3 : 2) : 1;
         if (base == thr) {
-          write_remaining(a - base, rice);
+          write_remaining(en, a - base, rice);
           if (a > 3 * (1 << rice)) rice = hv_min(rice + 1, 4);
         }
       }
     }
+    e = en;
   }
 
   HV_FN static int mdcs(int mode) { return (mode >= 6 && mode <= 14) ? 2 : ((mode >= 22 && mode <= 30) ? 1 : 0); }
 
-  HV_BIG void scan_ctb_nz(int x0, int y0) {
+  HV_BIG void scan_ctb_nz(int x0, int y0) __restrict__ {
+    const ProfScope prof_scope(prof, CP_SCAN);
     const size_t ci = static_cast<size_t>(y0 / kCtb) * wctb + x0 / kCtb;
     if (lv.nzmap) {
       nz_luma = lv.nzmap[2 * ci];
       nz_chroma[0] = static_cast<uint32_t>(lv.nzmap[2 * ci + 1] & 0xFFFFu);
       nz_chroma[1] = static_cast<uint32_t>((lv.nzmap[2 * ci + 1] >> 16) & 0xFFFFu);
       ctb_base = lv.ctb_off ? lv.ctb_off[ci] : 0;
+      if (lv.stage_ctu && P->ctu64) {  // blocks of the CTU's earlier 32x32 blocks (z-order)
+        const int bx = x0 / kCtb, by = y0 / kCtb, q = ((by & 1) << 1) | (bx & 1);
+        ctb_base = 0;
+        for (int k = 0; k < q; ++k) {
+          const int qx = (bx & ~1) + (k & 1), qy = (by & ~1) + (k >> 1);
+          if (qx * kCtb >= W || qy * kCtb >= H) continue;
+          const size_t cj = static_cast<size_t>(qy) * wctb + qx;
+          ctb_base += static_cast<uint32_t>(__builtin_popcountll(lv.nzmap[2 * cj]) +
+                                            __builtin_popcountll(lv.nzmap[2 * cj + 1] & 0xFFFFFFFFull));
+        }
+      }
       return;
     }
     nz_luma = 0;
@@ -811,7 +895,7 @@ struct CtuCoder {
   }
   // sub-block mask of an n x n block at plane position (x, y) inside the current CTB, in
   // the block's own raster order (bit ys * (n / 4) + xs)
-  HV_FN uint64_t block_mask(int cidx, int x, int y, int n) const {
+  HV_FN uint64_t block_mask(int cidx, int x, int y, int n) const __restrict__ {
     const int side = cidx ? 4 : 8, m = cidx ? 15 : 31;
     const uint64_t src = cidx ? nz_chroma[cidx - 1] : nz_luma;
     const int bx0 = (x & m) >> 2, by0 = (y & m) >> 2, nb = n >> 2;
@@ -819,18 +903,18 @@ struct CtuCoder {
     for (int r = 0; r < nb; ++r) out |= ((src >> ((by0 + r) * side + bx0)) & ((1ull << nb) - 1ull)) << (r * nb);
     return out;
   }
-  HV_FN bool any_nonzero(int cidx, int x, int y, int n) const { return block_mask(cidx, x, y, n) != 0; }
+  HV_FN bool any_nonzero(int cidx, int x, int y, int n) const __restrict__ { return block_mask(cidx, x, y, n) != 0; }
 
   // ---------------------------------------------------------------- inter prediction helpers
   // A PU's motion is its direction (bit 0 list 0, bit 1 list 1) and a refIdx + vector per used
   // list; RefPicListX holds num_ref[X] pictures (POC list_poc(X, i)).
-  HV_FN bool inter_avail(int x, int y) const { return avail(x, y) && S.pred[g(x, y)] == CU_INTER; }
-  HV_FN const Motion& mot_at(int x, int y) const { return S.mot[g(x, y)]; }
-  HV_FN int ref_poc(int l) const {
+  HV_FN bool inter_avail(int x, int y) const __restrict__ { return avail(x, y) && S.pred[g(x, y)] == CU_INTER; }
+  HV_FN const Motion& mot_at(int x, int y) const __restrict__ { return S.mot[g(x, y)]; }
+  HV_FN int ref_poc(int l) const __restrict__ {
     return l == 0 ? (P->ref_poc[0] >= 0 ? P->ref_poc[0] : P->poc - 1) : P->ref_poc[1];
   }
-  HV_FN int nref(int l) const { return hv_max(1, P->num_ref[l]); }
-  HV_FN int list_poc(int l, int i) const { return i == 0 ? ref_poc(l) : P->list_poc[l][i]; }
+  HV_FN int nref(int l) const __restrict__ { return hv_max(1, P->num_ref[l]); }
+  HV_FN int list_poc(int l, int i) const __restrict__ { return i == 0 ? ref_poc(l) : P->list_poc[l][i]; }
 
   HV_FN static Mv scale_mv(Mv v, int td0, int tb0) {  // 8.5.3.2.8 (8-209 .. 8-213)
     const int td = hv_clamp(td0, -128, 127), tb = hv_clamp(tb0, -128, 127);
@@ -843,7 +927,7 @@ struct CtuCoder {
   }
 
   // 8.5.3.2.8 / 8.5.3.2.9 temporal vector of list X (target refIdx ri) for the PU (x, y, n x n)
-  HV_BIG bool col_at(int xc, int yc, int X, int ri, Mv* out) {
+  HV_BIG bool col_at(int xc, int yc, int X, int ri, Mv* out) __restrict__ {
     if (!col_cu || xc >= W || yc >= H) return false;
     const int ci = (yc >> kCtbLog2) * wctb + (xc >> kCtbLog2);
     const CuInfo& cc = col_cu[static_cast<size_t>(ci) * kCusPerCtb + zorder8((xc & (kCtb - 1)) >> 3, (yc & (kCtb - 1)) >> 3)];
@@ -865,7 +949,7 @@ struct CtuCoder {
     *out = v;
     return true;
   }
-  HV_FN bool temporal(int x, int y, int n, int X, int ri, Mv* out) {
+  HV_FN bool temporal(int x, int y, int n, int X, int ri, Mv* out) __restrict__ {
     if (!tmvp) return false;
     const int xbr = x + n, ybr = y + n;
     if ((y >> L) == (ybr >> L) && ybr < H && xbr < W && col_at((xbr >> 4) << 4, (ybr >> 4) << 4, X, ri, out))
@@ -874,7 +958,8 @@ struct CtuCoder {
   }
 
   // 8.5.3.2.2-8.5.3.2.5 merge candidates of a 2Nx2N PU (MaxNumMergeCand entries)
-  HV_BIG int merge_list(int x, int y, int n, Motion* out) {
+  HV_BIG int merge_list(int x, int y, int n, Motion* out) __restrict__ {
+    const ProfScope prof_scope(prof, CP_MERGE);
     Motion cand[8];
     int k = 0;
     const Motion none = motion_none();
@@ -931,7 +1016,7 @@ struct CtuCoder {
   }
 
   // a neighbour vector pointing at the target picture (8.5.3.2.7, no scaling)
-  HV_FN bool amvp_same(int xn, int yn, int X, int tgt, Mv* v) const {
+  HV_FN bool amvp_same(int xn, int yn, int X, int tgt, Mv* v) const __restrict__ {
     const Motion& m = mot_at(xn, yn);
     const int Y = 1 - X;
     if ((m.dir >> X) & 1 && list_poc(X, m.r[X]) == tgt) {
@@ -945,7 +1030,7 @@ struct CtuCoder {
     return false;
   }
   // any vector of the neighbour, scaled by the POC distances
-  HV_FN bool amvp_scaled(int xn, int yn, int X, int tgt, Mv* v) const {
+  HV_FN bool amvp_scaled(int xn, int yn, int X, int tgt, Mv* v) const __restrict__ {
     const Motion& m = mot_at(xn, yn);
     for (int j = 0; j < 2; ++j) {
       const int Lx = j == 0 ? X : 1 - X;
@@ -958,7 +1043,8 @@ struct CtuCoder {
   }
 
   // 8.5.3.2.6-8.5.3.2.7 AMVP candidates of list X, refIdx ri
-  HV_BIG void amvp_list(int x, int y, int n, int X, int ri, Mv* out) {
+  HV_BIG void amvp_list(int x, int y, int n, int X, int ri, Mv* out) __restrict__ {
+    const ProfScope prof_scope(prof, CP_AMVP);
     const int tgt = list_poc(X, ri);
     const int xa[2] = {x - 1, x - 1}, ya[2] = {y + n, y + n - 1};
     const bool ava[2] = {inter_avail(xa[0], ya[0]), inter_avail(xa[1], ya[1])};
@@ -993,7 +1079,7 @@ struct CtuCoder {
   }
 
   // ---------------------------------------------------------------- coding unit (7.3.8.5)
-  HV_FN void mark(int x, int y, int n, int d, int sk, int pm, int md, const Motion& mv) {
+  HV_FN void mark(int x, int y, int n, int d, int sk, int pm, int md, const Motion& mv) __restrict__ {
     for (int yy = y; yy < y + n; yy += 8)
       for (int xx = x; xx < x + n; xx += 8) {
         const size_t k = g(xx, yy);
@@ -1007,21 +1093,21 @@ struct CtuCoder {
   }
 
   // inter_pred_idc (9.3.3.7, 2Nx2N PU of a CU at depth d): PRED_BI "1", PRED_L0 "00", PRED_L1 "01"
-  HV_FN void write_inter_pred_idc(int dir, int d) {
+  HV_FN void write_inter_pred_idc(int dir, int d) __restrict__ {
     e.encode(dir == DIR_BI, ctx[CTX_INTER_PRED + d]);
     if (dir != DIR_BI) e.encode(dir == DIR_L1, ctx[CTX_INTER_PRED + 4]);
   }
 
   // a CU, then the QpY of its granules (8.6.1: the quantization group's prediction until a
   // cu_qp_delta has been coded, the coded QP from then on)
-  HV_FN void write_cu(int x, int y, int log2, int d) {
+  HV_FN void write_cu(int x, int y, int log2, int d) __restrict__ {
     write_cu_body(x, y, log2, d);
     const int q = qp_coded ? qp_ctb : qp_pred_cur, n = 1 << log2;
     for (int yy = y; yy < y + n; yy += 8)
       for (int xx = x; xx < x + n; xx += 8) S.qpy[g(xx, yy)] = static_cast<int8_t>(q);
   }
 
-  HV_FN Motion cu_motion(const CuInfo& ci) const {
+  HV_FN Motion cu_motion(const CuInfo& ci) const __restrict__ {
     Motion mv = motion_none();
     mv.dir = static_cast<uint8_t>(cu_dir(ci));
     mv.r[0] = static_cast<int8_t>(ci.pad[0]);
@@ -1031,7 +1117,8 @@ struct CtuCoder {
     return mv;
   }
 
-  HV_BIG void write_cu_body(int x, int y, int log2, int d) {
+  HV_BIG void write_cu_body(int x, int y, int log2, int d) __restrict__ {
+    const ProfScope prof_scope(prof, CP_CU);
     const int n = 1 << log2;
     const CuInfo& ci = cu_at(x, y);
     const bool cb_y = any_nonzero(0, x, y, n);
@@ -1164,7 +1251,7 @@ struct CtuCoder {
 
   // MPM candidate (8.4.2) from the neighbour (xn, yn) of the PU at row yk of the CU at (x, y)
   // with PUs of size h and modes m
-  HV_FN int mpm_cand(int x, int y, int h, const int* m, int xn, int yn, int yk, bool above) const {
+  HV_FN int mpm_cand(int x, int y, int h, const int* m, int xn, int yn, int yk, bool above) const __restrict__ {
     if (xn >= x && yn >= y) return m[(xn - x >= h) + 2 * (yn - y >= h)];
     if (!avail(xn, yn) || S.pred[g(xn, yn)] != CU_INTRA) return 1;
     if (above && (yn >> L) != (yk >> L)) return 1;
@@ -1175,7 +1262,7 @@ struct CtuCoder {
   // split_transform_flag inferred (IntraSplitFlag), four 4x4 luma TUs with cbf_luma at
   // depth 1; cbfChroma of every 4x4 TU is the parent's, and the 4x4 chroma blocks follow
   // the last luma TU (blkIdx 3)
-  HV_BIG void write_tu_nxn(int x, int y, const int* m, bool cb_cb, bool cb_cr) {
+  HV_BIG void write_tu_nxn(int x, int y, const int* m, bool cb_cb, bool cb_cr) __restrict__ {
     e.encode(cb_cb, ctx[CTX_CBF_CHROMA + 0]);
     e.encode(cb_cr, ctx[CTX_CBF_CHROMA + 0]);
     for (int k = 0; k < 4; ++k) {
@@ -1190,7 +1277,7 @@ struct CtuCoder {
   }
 
   // ref_idx_lX (9.3.3.1 TR, cMax = num_ref_idx_active - 1): two context-coded bins, then bypass
-  HV_FN void write_ref_idx(int r, int cmax) {
+  HV_FN void write_ref_idx(int r, int cmax) __restrict__ {
     for (int i = 0; i < cmax; ++i) {
       const int b = r > i;
       if (i < 2) e.encode(b, ctx[CTX_REF_IDX + i]);
@@ -1199,13 +1286,13 @@ struct CtuCoder {
     }
   }
 
-  HV_FN void write_merge_idx(int idx) {
+  HV_FN void write_merge_idx(int idx) __restrict__ {
     if (P->max_merge <= 1) return;
     e.encode(idx > 0, ctx[CTX_MERGE_IDX]);
     for (int k = 1; k < P->max_merge - 1 && idx >= k; ++k) e.bypass(idx > k);
   }
 
-  HV_FN void write_mvd_pair(int dx, int dy) {
+  HV_FN void write_mvd_pair(int dx, int dy) __restrict__ {
     const int ax = hv_abs(dx), ay = hv_abs(dy);
     e.encode(ax > 0, ctx[CTX_MVD_G0]);
     e.encode(ay > 0, ctx[CTX_MVD_G0]);
@@ -1224,7 +1311,7 @@ struct CtuCoder {
   // inter CU whose residual quadtree splits once (CuInfo flags bit 4): split_transform_flag,
   // chroma cbfs at depth 0, then per quarter TU (z-order) its chroma cbfs under a set parent,
   // cbf_luma (always coded below depth 0) and the transform unit
-  HV_BIG void write_tu_inter_split(int x, int y, int log2, bool cb_cb, bool cb_cr) {
+  HV_BIG void write_tu_inter_split(int x, int y, int log2, bool cb_cb, bool cb_cr) __restrict__ {
     if (P->tu_inter_depth < 1 || log2 < 4) fail(CE_INTER_SPLIT);
     e.encode(1, ctx[CTX_SPLIT_TRANSFORM + 5 - log2]);
     e.encode(cb_cb, ctx[CTX_CBF_CHROMA + 0]);
@@ -1246,7 +1333,7 @@ struct CtuCoder {
   }
 
   // transform_tree at depth 0 with TU = CU (7.3.8.8 / 7.3.8.10)
-  HV_BIG void write_tu(int x, int y, int log2, bool intra, int m, bool cb_y, bool cb_cb, bool cb_cr) {
+  HV_BIG void write_tu(int x, int y, int log2, bool intra, int m, bool cb_y, bool cb_cb, bool cb_cr) __restrict__ {
     // split_transform_flag 0 where the inter depth allows a split (intra: depth 0 at 2Nx2N)
     if (!intra && P->tu_inter_depth > 0 && log2 > 2) e.encode(0, ctx[CTX_SPLIT_TRANSFORM + 5 - log2]);
     e.encode(cb_cb, ctx[CTX_CBF_CHROMA + 0]);
@@ -1266,7 +1353,7 @@ struct CtuCoder {
 
   // cu_qp_delta_abs (9.3.3.10: TR prefix cMax 5, ctxInc 0 then 1; EG0 bypass suffix) and
   // the bypass sign, in the first TU of the quantization group with a coded block
-  HV_BIG void write_qp_delta() {
+  HV_BIG void write_qp_delta() __restrict__ {
     const int d = qp_ctb - qp_pred_cur;
     const int qbd = 6 * (P->bit_depth - 8);
     if (d < -(26 + qbd / 2) || d > 25 + qbd / 2) fail(CE_QP_DELTA);
@@ -1277,7 +1364,7 @@ struct CtuCoder {
     if (a) e.bypass(d < 0);
     qp_coded = true;
   }
-  HV_FN void write_egk(uint32_t v, int k) {  // 9.3.3.3 k-th order Exp-Golomb, bypass
+  HV_FN void write_egk(uint32_t v, int k) __restrict__ {  // 9.3.3.3 k-th order Exp-Golomb, bypass
     while (v >= (1u << k)) {
       e.bypass(1);
       v -= 1u << k;
@@ -1289,7 +1376,7 @@ struct CtuCoder {
 
   // qPY_PRED of the quantization group at (xq, yq) (8.6.1): the average of the QpY left of and
   // above it when those lie in the same CTB, each replaced by qPY_PREV otherwise
-  HV_FN int qg_pred(int xq, int yq) const {
+  HV_FN int qg_pred(int xq, int yq) const __restrict__ {
     const bool la = avail(xq - 1, yq) && ((xq - 1) >> L) == (xq >> L) && (yq >> L) == (yq >> L);
     const bool lb = avail(xq, yq - 1) && (xq >> L) == (xq >> L) && ((yq - 1) >> L) == (yq >> L);
     const int qa = la ? S.qpy[g(xq - 1, yq)] : qp_prev;
@@ -1298,7 +1385,7 @@ struct CtuCoder {
   }
 
   // coding_quadtree (7.3.8.4) of one CTU (CTU coordinates)
-  HV_BIG void write_ctu(int cx, int cy) {
+  HV_BIG void write_ctu(int cx, int cy) __restrict__ {
     if (!P->ctu64) {
       write_block_tree(cx, cy, 0);
       return;
@@ -1317,12 +1404,12 @@ struct CtuCoder {
     }
   }
 
-  HV_FN int split_ctx(int x, int y, int d) const {
+  HV_FN int split_ctx(int x, int y, int d) const __restrict__ {
     return (avail(x - 1, y) && S.depth[g(x - 1, y)] > d) + (avail(x, y - 1) && S.depth[g(x, y - 1)] > d);
   }
 
   // one 32x32 record block = one quantization group; dofs: its depth in the CTU quadtree
-  HV_BIG void write_block_tree(int rx, int ry, int dofs) {
+  HV_BIG void write_block_tree(int rx, int ry, int dofs) __restrict__ {
     const CtuInfo& t = ctu[ry * wctb + rx];
     const int x0 = rx * kCtb, y0 = ry * kCtb;
     qp_ctb = t.qp;
@@ -1353,14 +1440,14 @@ struct CtuCoder {
   // one motion, no level anywhere, and that motion is in the 64x64 CU's merge list (the
   // reconstruction is the same: motion compensation is per sample and every inner edge has
   // boundary strength 0)
-  HV_BIG bool cu64_ok(int cx, int cy) {
+  HV_BIG bool cu64_ok(int cx, int cy) __restrict__ {
     const int x0 = cx << 6, y0 = cy << 6;
     if (!inter_slice) return false;
     Motion m0 = motion_none();
     for (int q = 0; q < 4; ++q) {
       const int bx = (x0 >> 5) + (q & 1), by = (y0 >> 5) + (q >> 1);
       const CtuInfo& t = ctu[by * wctb + bx];
-      const CuInfo& ci = cu[static_cast<size_t>(by * wctb + bx) * kCusPerCtb];
+      const CuInfo& ci = cu_at(bx << 5, by << 5);
       if ((t.split & 1) || ci.pred != CU_INTER) return false;
       Motion m = cu_motion(ci);
       for (int X = 0; X < 2; ++X)
@@ -1381,7 +1468,7 @@ struct CtuCoder {
     cu64_mot = m0;
     return cu64_midx >= 0;
   }
-  HV_FN void write_cu64_skip(int x0, int y0) {
+  HV_FN void write_cu64_skip(int x0, int y0) __restrict__ {
     const int skip_ctx = (avail(x0 - 1, y0) && S.skip[g(x0 - 1, y0)]) + (avail(x0, y0 - 1) && S.skip[g(x0, y0 - 1)]);
     e.encode(1, ctx[CTX_CU_SKIP + skip_ctx]);
     write_merge_idx(cu64_midx);
@@ -1396,7 +1483,8 @@ struct CtuCoder {
 
   // SAO + coding quadtree of CTU (rx, ry) and its end_of_slice_segment_flag; with WPP, a
   // row's last CTU also codes end_of_subset_one_bit, flushes and byte-aligns its substream
-  HV_BIG void code_ctu(int rx, int ry) {
+  HV_BIG void code_ctu(int rx, int ry) __restrict__ {
+    const ProfScope prof_scope(prof, CP_CTU);
     if (P->sao) write_sao(rx, ry);
     write_ctu(rx, ry);
     const bool last = ry == P->hctu - 1 && rx == P->wctu - 1;

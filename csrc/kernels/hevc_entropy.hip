@@ -2,12 +2,13 @@
 // run per picture on the device, so the entropy stage no longer binds to the host cores of a
 // rank (profiles/r6_hevc_rank_rehearsal.md: 2 cores per rank held config 4 to 731 fps).
 //
-// One workgroup per picture, one lane per WPP substream (CTU row).  The rows advance as a
-// wavefront in lock step: at step t row r codes CTU t - 2r, so CTU (x, r - 1) and (x + 1,
-// r - 1), the above and above-right neighbours, were coded at steps <= t - 1, and row r starts
-// (step 2r) with the contexts row r - 1 saved after its CTU 1 (step 2r - 1) -- 9.3.2.4.  A
-// barrier between steps orders the rows' writes to the picture state (global) and contexts
-// (LDS).  Without WPP lane 0 codes the slice alone.  Each lane writes its substream to its own
+// One workgroup per picture; lane 0 of each of its (up to 16) waves codes WPP substreams (CTU
+// rows wave, wave + 16, ...): one active lane per wave, because the rows' code paths differ and
+// lanes of one wavefront would serialise them.  The rows advance as a wavefront: in each round
+// a row codes its next CTU x when the row above has coded CTU x + 1 (the above-right
+// neighbour), and row r starts with the contexts row r - 1 saved after its CTU 1 (9.3.2.4).
+// Barriers between the rounds order the rows' writes to the picture state (global) and the
+// contexts / progress (LDS).  Without WPP lane 0 of wave 0 codes the slice alone.  Each lane writes its substream to its own
 // bounded region; hevc_entropy_scan / _gather then pack the substreams into pinned host memory
 // at 16-byte aligned offsets, so only the coded bytes cross to the host, where
 // hevc_assemble_slice (hevc_writer.cc) adds the slice header, entry points and emulation
@@ -70,6 +71,7 @@ struct HevcEntropyArgs {
   unsigned* sizes;             // [B][nsub] bytes written (may exceed cap: overflow)
   int* errs;                   // [B][nsub] CoderError
   int nsub;
+  unsigned long long* prof;    // diagnostics: [B][16 waves][CP_N + 2] cycle counters, or null
 };
 
 __host__ __device__ inline long long entropy_state_bytes(int W, int H) {
@@ -90,60 +92,165 @@ __device__ inline CoderState entropy_state(uint8_t* base, int W, int H) {
   return s;
 }
 
-__global__ __launch_bounds__(256) void hevc_entropy(HevcEntropyArgs a) {
+constexpr int kStageBlocks = 128;  // 4x4 level blocks staged per CTU and wave (4 KiB)
+
+__global__ __launch_bounds__(1024) void hevc_entropy(HevcEntropyArgs a) {
   extern __shared__ CtxState s_ctx[];  // [2][nsub][kNumCtx]: working contexts, saved after CTU 1
   __shared__ CoderPic sP;
-  const int b = blockIdx.x, r = threadIdx.x, nl = blockDim.x;
+  __shared__ int s_prog[128];          // CTUs coded per row
+  // the coder's constant tables in LDS (read once or more per bin / coefficient)
+  __shared__ uint32_t s_step[256];
+  __shared__ uint8_t s_scans[sizeof(hevc::kScans.t)];
+  __shared__ uint8_t s_sig[sizeof(hevc::kSig.t)];
+  const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const int wave = tid >> 6, nwave = nt >> 6;
+  const bool lead = (tid & 63) == 0;
   const int W = a.pic.W, H = a.pic.H, nctb = a.pic.wctb * a.pic.hctb;
-  if (r == 0) {
+  if (tid == 0) {
     sP = a.pic;
     sP.qp = a.qp[b];
   }
+  for (int i = tid; i < a.nsub; i += nt) s_prog[i] = 0;
+  for (int i = tid; i < 256; i += nt) s_step[i] = hevc::kCabacStep.t[i];
+  for (int i = tid; i < static_cast<int>(sizeof(s_scans)); i += nt) s_scans[i] = (&hevc::kScans.t[0][0][0])[i];
+  for (int i = tid; i < static_cast<int>(sizeof(s_sig)); i += nt) s_sig[i] = (&hevc::kSig.t[0][0][0][0][0][0])[i];
   uint8_t* st = a.state + static_cast<size_t>(b) * a.state_bytes;
   const CoderState cs = entropy_state(st, W, H);
   const long long n8 = static_cast<long long>(W / 8) * (H / 8);
-  for (long long i = r; i < n8; i += nl) cs.coded[i] = 0;
+  for (long long i = tid; i < n8; i += nt) cs.coded[i] = 0;
   __syncthreads();
   CoderLevels lv;
   lv.nzmap = reinterpret_cast<const uint64_t*>(a.nzmap) + static_cast<size_t>(b) * nctb * 2;
   lv.plane[0] = a.coef[0] + static_cast<size_t>(b) * W * H;
   lv.plane[1] = a.coef[1] + static_cast<size_t>(b) * (W / 2) * (H / 2);
   lv.plane[2] = a.coef[2] + static_cast<size_t>(b) * (W / 2) * (H / 2);
+  lv.stage_ctu = 1;  // with WPP (below) levels come from the per-CTU staging area first
   const CtuInfo* ctu = a.ctu + static_cast<size_t>(b) * nctb;
   const CuInfo* cu = a.cu + static_cast<size_t>(b) * nctb * hevc::kCusPerCtb;
   const CuInfo* col = (a.col && sP.col_set && sP.tmvp && sP.slice_type != 2)
                           ? a.col + static_cast<size_t>(b) * nctb * hevc::kCusPerCtb
                           : nullptr;
-  const bool active = r < a.nsub;
-  DevSink sink{a.out + (static_cast<size_t>(b) * a.nsub + (active ? r : 0)) * a.cap, a.cap, 0, 0, 0};
-  CtxState* ctx = s_ctx + static_cast<size_t>(r) * hevc::kNumCtx;  // valid for active lanes
-  CtxState* saved = s_ctx + static_cast<size_t>(a.nsub + r) * hevc::kNumCtx;
-  CtuCoder<DevSink> w;
-  if (active) w.begin(&sP, ctu, cu, col, lv, cs, ctx, &sink);
   const int wctu = sP.wctu, hctu = sP.hctu;
-  if (!sP.wpp) {
-    if (r == 0)
-      for (int i = 0; i < wctu * hctu; ++i) w.code_ctu(i % wctu, i / wctu);
-  } else {
-    const int steps = wctu + 2 * (hctu - 1);
-    for (int t = 0; t < steps; ++t) {
-      const int rx = t - 2 * r;
-      if (active && rx >= 0 && rx < wctu) {
-        if (rx == 0 && r > 0 && wctu >= 2) {  // 9.3.2.4 sync from CTU (1, r - 1)
-          const CtxState* src = s_ctx + static_cast<size_t>(a.nsub + r - 1) * hevc::kNumCtx;
-          for (int i = 0; i < hevc::kNumCtx; ++i) ctx[i] = src[i];
-        }
-        w.code_ctu(rx, r);
-        if (rx == 1)
-          for (int i = 0; i < hevc::kNumCtx; ++i) saved[i] = ctx[i];
-      }
-      __syncthreads();
-    }
-  }
-  if (active) {
+  // lane 0 of each wave codes rows wave, wave + nwave, ...: one active lane per wave, so the
+  // rows' different code paths never share (serialise within) a wavefront
+  int row = wave;
+  // each wave's coder and sink in LDS: their fields are read and written around every bin, and
+  // the out-of-line calls would otherwise keep them in scratch memory
+  __shared__ __attribute__((aligned(16))) unsigned char s_coder[16][sizeof(CtuCoder<DevSink>)];
+  __shared__ DevSink s_sink[16];
+  __shared__ __attribute__((aligned(16))) int16_t s_lv[16][kStageBlocks * 16];
+  __shared__ CuInfo s_cu[16][4 * hevc::kCusPerCtb];
+  CtuCoder<DevSink>& w = *reinterpret_cast<CtuCoder<DevSink>*>(s_coder[wave]);
+  DevSink& sink = s_sink[wave];
+  auto start_row = [&](int r) {
+    sink = DevSink{a.out + (static_cast<size_t>(b) * a.nsub + r) * a.cap, a.cap, 0, 0, 0};
+    w.begin(&sP, ctu, cu, col, lv, cs, s_ctx + static_cast<size_t>(r) * hevc::kNumCtx, &sink, s_step, s_scans, s_sig);
+  };
+  auto end_row = [&](int r) {
     const size_t o = static_cast<size_t>(b) * a.nsub + r;
     a.sizes[o] = sink.n;
     a.errs[o] = w.err ? w.err : (sink.n > a.cap ? static_cast<int>(hevc::CE_OVERFLOW) : 0);
+  };
+  if (!sP.wpp) {  // one substream: lane 0 of wave 0 codes the slice
+    sink = DevSink{nullptr, a.cap, 0, 0, 0};
+    if (tid == 0) {
+      start_row(0);
+      for (int i = 0; i < wctu * hctu; ++i) w.code_ctu(i % wctu, i / wctu);
+      end_row(0);
+    }
+    return;
+  }
+  // this wave's staging area: the current CTU's records and its first kStageBlocks non-zero
+  // 4x4 level blocks, copied by all 64 lanes at once (one memory latency instead of one per
+  // access of the serial coder)
+  const int lane = tid & 63;
+  auto stage = [&](int cx, int cy) {
+    const int per = sP.ctu64 ? 2 : 1;
+    int base = 0;
+    for (int q = 0; q < per * per; ++q) {
+      const int bx = cx * per + (q & 1), by = cy * per + (q >> 1);
+      if (bx >= sP.wctb || by >= sP.hctb) continue;
+      const size_t ci = static_cast<size_t>(by) * sP.wctb + bx;
+      if (lane < hevc::kCusPerCtb) s_cu[wave][q * hevc::kCusPerCtb + lane] = cu[ci * hevc::kCusPerCtb + lane];
+      const unsigned long long lm = lv.nzmap[2 * ci], cm = lv.nzmap[2 * ci + 1] & 0xFFFFFFFFull;
+      if ((lm >> lane) & 1ull) {
+        const int rank = base + __popcll(lm & ((1ull << lane) - 1ull));
+        if (rank < kStageBlocks) {
+          const int16_t* src = lv.plane[0] + static_cast<size_t>(by * 32 + (lane >> 3) * 4) * W + bx * 32 + (lane & 7) * 4;
+          uint64_t* d = reinterpret_cast<uint64_t*>(&s_lv[wave][rank * 16]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) d[r] = *reinterpret_cast<const uint64_t*>(src + static_cast<size_t>(r) * W);
+        }
+      }
+      if (lane < 32 && ((cm >> lane) & 1ull)) {
+        const int rank = base + __popcll(lm) + __popcll(cm & ((1ull << lane) - 1ull));
+        if (rank < kStageBlocks) {
+          const int k = lane & 15, cw = W / 2;
+          const int16_t* src = lv.plane[lane < 16 ? 1 : 2] + static_cast<size_t>(by * 16 + (k >> 2) * 4) * cw + bx * 16 + (k & 3) * 4;
+          uint64_t* d = reinterpret_cast<uint64_t*>(&s_lv[wave][rank * 16]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) d[r] = *reinterpret_cast<const uint64_t*>(src + static_cast<size_t>(r) * cw);
+        }
+      }
+      base += __popcll(lm) + __popcll(cm);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  __shared__ uint64_t s_prof[16][hevc::CP_N + 2];  // + cycles waiting at barriers, + CTUs coded
+  if (a.prof && lead) {
+    for (int k = 0; k < hevc::CP_N + 2; ++k) s_prof[wave][k] = 0;
+  }
+  uint64_t t_wait = 0;
+  if (lead && row < a.nsub) start_row(row);
+  for (;;) {
+    const uint64_t tw = a.prof ? __builtin_readcyclecounter() : 0;
+    // barrier: the previous iteration's CTUs (picture state, contexts, progress) are visible.
+    // Every lane of a wave follows its row (wave-uniform control), lane 0 codes.
+    if (!__syncthreads_or(lead && row < a.nsub)) break;
+    int x = 0;
+    bool ready = false;
+    if (row < a.nsub) {
+      x = s_prog[row];
+      ready = row == 0 || s_prog[row - 1] >= min(x + 2, wctu);  // above-right CTU coded (9.3.2.4: CTU 1)
+    }
+    __syncthreads();  // every wave has read the progress before any wave advances it
+    if (a.prof) t_wait += __builtin_readcyclecounter() - tw;
+    if (ready) {
+      stage(x, row);
+      if (lead) {
+        CtxState* ctx = s_ctx + static_cast<size_t>(row) * hevc::kNumCtx;
+        if (x == 0 && row > 0 && wctu >= 2) {  // sync from CTU (1, row - 1)
+          const CtxState* src = s_ctx + static_cast<size_t>(a.nsub + row - 1) * hevc::kNumCtx;
+          for (int i = 0; i < hevc::kNumCtx; ++i) ctx[i] = src[i];
+        }
+        w.lv.levels = &s_lv[wave][0];
+        w.lv.nblocks = kStageBlocks;
+        w.cu_stage = &s_cu[wave][0];
+        w.stage_cx = x;
+        w.stage_cy = row;
+        w.prof = a.prof ? &s_prof[wave][0] : nullptr;
+        w.code_ctu(x, row);
+        if (a.prof) s_prof[wave][hevc::CP_N + 1] += 1;
+        if (x == 1) {
+          CtxState* sv = s_ctx + static_cast<size_t>(a.nsub + row) * hevc::kNumCtx;
+          for (int i = 0; i < hevc::kNumCtx; ++i) sv[i] = ctx[i];
+        }
+        s_prog[row] = x + 1;
+        if (x + 1 == wctu) end_row(row);
+      }
+      if (x + 1 == wctu) {
+        row += nwave;
+        if (lead && row < a.nsub) start_row(row);
+      }
+      __builtin_amdgcn_wave_barrier();  // lane 0 is done with the staging area
+    }
+  }
+  if (a.prof && lead) {
+    s_prof[wave][hevc::CP_N] = t_wait;
+    unsigned long long* o = a.prof + (static_cast<size_t>(b) * 16 + wave) * (hevc::CP_N + 2);
+    for (int k = 0; k < hevc::CP_N + 2; ++k) o[k] = s_prof[wave][k];
   }
 }
 
@@ -208,8 +315,10 @@ extern "C" int mivc_launch_hevc_entropy(const void* pic, int B, const int* qp, c
                                         const int16_t* cb, const int16_t* cr, uint8_t* state, long long state_bytes,
                                         uint8_t* out, unsigned cap, unsigned* sizes, int* errs,
                                         unsigned long long* offs, unsigned long long* offs_host, uint8_t* dst,
-                                        unsigned long long dst_cap, int* overflow, void* stream) {
+                                        unsigned long long dst_cap, int* overflow, void* stream,
+                                        unsigned long long* prof) {
   HevcEntropyArgs a{};
+  a.prof = prof;
   a.pic = *static_cast<const CoderPic*>(pic);
   const int nsub = a.pic.wpp ? a.pic.hctu : 1;
   if (nsub < 1 || nsub > 100 || (cap & 15) || a.pic.W % 32 || a.pic.H % 32 ||
@@ -230,7 +339,7 @@ extern "C" int mivc_launch_hevc_entropy(const void* pic, int B, const int* qp, c
   a.sizes = sizes;
   a.errs = errs;
   a.nsub = nsub;
-  const int lanes = ((nsub + 63) / 64) * 64;
+  const int lanes = 64 * (nsub < 16 ? nsub : 16);  // a wave per row, rows beyond 16 round-robin
   const size_t lds = static_cast<size_t>(2) * nsub * mivc::hevc::kNumCtx * sizeof(CtxState);  // <= 60 KB
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(hevc_entropy, dim3(B), dim3(lanes), lds, s, a);

@@ -1,7 +1,7 @@
 """MI355X HEVC (H.265) encoder: B closed-GOP segments encoded concurrently on one GPU.
 
 Replaces the reference's ``-vcodec libx265 -crf 26`` worker call (server.go:67-68,
-client.go:115) with gfx950 kernels + a host CABAC writer:
+client.go:115) with gfx950 kernels, CABAC included:
 
 per frame step t (frame t of every slot):
   prep (u8/u16 -> padded u16 planes)
@@ -12,10 +12,13 @@ per frame step t (frame t of every slot):
   -> hevc_qp_fixup (QpY of CTBs / CUs without a coded delta, 8.6.1)
   -> hevc_deblock (vertical, then horizontal edges; picture-parallel)
   -> hevc_sao (per-CTB statistics, decision, apply)
-then the decision records go to pinned host memory, the non-zero 4x4 level blocks are
-packed straight into pinned host memory (hevc_pack_levels: only coded levels cross
-PCIe), and a host thread pool writes one CABAC slice per picture
-(csrc/host/hevc_writer.cc) while the GPU works on the next step.
+then, on the copy stream while the compute stream runs the next step, hevc_entropy codes
+the slice data of the step's pictures on the GPU (one lane per WPP substream, the coder of
+csrc/common/hevc_ctu_coder.h) and packs the substreams into pinned host memory, where a
+host thread adds slice headers, entry points and emulation prevention
+(hevc_assemble_slices).  ``entropy="host"`` instead ships the records and the packed non-zero
+level blocks to pinned memory and codes the slices on host threads (csrc/host/hevc_writer.cc,
+the same coder: byte-identical output).
 
 Main (8-bit) and Main 10 share one code path: samples are uint16 on the device.
 """
@@ -344,9 +347,16 @@ class GpuHevcEncoder:
         # the host writer's coder) and only the slice headers, entry points and emulation
         # prevention stay on the host; "host": the native writer codes the records on
         # entropy_threads host threads (csrc/host/hevc_writer.cc)
-        self.entropy = (entropy or os.environ.get("MIVC_HEVC_ENTROPY", "gpu")).lower()
-        if self.entropy not in ("gpu", "host"):
-            raise ValueError("entropy must be 'gpu' or 'host'")
+        # "auto": host threads when this process has cores for them (8+ usable cores and
+        # entropy threads), else the GPU -- one rank's share of an 8-GPU node (2 cores) codes
+        # config 4 at 731 fps on the host and 1754 on the GPU, the whole 1-GPU box at 2465 on
+        # the host and 1754 on the GPU (profiles/r6_hevc_gpu_entropy.md)
+        self.entropy = (entropy or os.environ.get("MIVC_HEVC_ENTROPY", "auto")).lower()
+        if self.entropy not in ("gpu", "host", "auto"):
+            raise ValueError("entropy must be 'gpu', 'host' or 'auto'")
+        if self.entropy == "auto":
+            cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+            self.entropy = "host" if min(cores, self.entropy_threads) >= 8 else "gpu"
         if self.entropy == "gpu":
             self._alloc_entropy()
         self.pool = cf.ThreadPoolExecutor(max_workers=1)
@@ -408,6 +418,27 @@ class GpuHevcEncoder:
         self.ent_dst_cap = max(1 << 22, B * W * H // 2)
         self.ent_host = None
         self.col_cus = None  # per DPB slot: [B, nctb * 16, 16] records of the picture in it (TMVP)
+
+    def _entropy_prof(self, kind: str) -> int:
+        """MIVC_HEVC_ENTROPY_PROF=1 (diagnostics): device pointer of a cycle-counter buffer of the
+        GPU coder for this step (one per picture type, summed by :meth:`entropy_profile`), else 0."""
+        if os.environ.get("MIVC_HEVC_ENTROPY_PROF", "0") != "1":
+            return 0
+        if getattr(self, "_ent_prof", None) is None:
+            self._ent_prof = {}
+        buf = torch.zeros((self.B * 16 * 9,), dtype=torch.int64, device=self.dev)
+        self._ent_prof.setdefault(kind, []).append(buf)
+        return buf.data_ptr()
+
+    def entropy_profile(self) -> dict:
+        """Cycles per picture type of the GPU coder's parts (MIVC_HEVC_ENTROPY_PROF=1 runs):
+        residual, merge list, AMVP, CU, SAO, whole CTU, nz scan, barrier wait; CTUs coded."""
+        names = ("residual", "merge", "amvp", "cu", "sao", "ctu", "scan", "wait", "ctus")
+        out = {}
+        for kind, bufs in (getattr(self, "_ent_prof", None) or {}).items():
+            tot = torch.stack([b.view(-1, 9) for b in bufs]).sum(dim=(0, 1)).cpu().tolist()
+            out[kind] = dict(zip(names, tot))
+        return out
 
     def _entropy_host(self):
         if self.ent_host is None:
@@ -808,6 +839,8 @@ class GpuHevcEncoder:
         anchor_cu: dict = {}   # display index of a reference picture -> (host copy of its CU records or None, l0, l1)
         ref_lists: dict = {}   # display index of a reference picture -> its (l0, l1) display indices
         anchor_meta: dict = {}  # (GPU entropy) display index of a reference picture -> (DPB slot, l0, l1, refs0)
+        # the writer's CU statistics (cu_stats diagnostics) come from the host writer
+        gpu_entropy = self.entropy == "gpu" and self.cu_stats is None
         plan_refs = {pic.d: pic.kind for pic in plan if pic.ref}
         idr_d = 0              # display index of the latest IDR picture (POC 0)
         for t in range(F):
@@ -1026,7 +1059,7 @@ class GpuHevcEncoder:
             nzmap, nzoff = self.nzmaps[kb], self.nzoffs[kb]
             qcol = qps_c[:, t].copy()
             wrow = wps[t][0] if t in wps else None
-            if self.entropy == "gpu":
+            if gpu_entropy:
                 job = self._gpu_entropy_step(t, pic, idr_d, kb, hb, cfg, qps_d[t], qcol, wrow, tmvp, anchor_meta,
                                              ref_lists, cabac_s)
                 t1 = time.perf_counter()
@@ -1155,7 +1188,11 @@ class GpuHevcEncoder:
             self.hip.hevc_entropy(pic_bytes, B, p(qp_row), p(self.ctu), p(self.cu), col_ptr, p(nzmap), p(self.coef[0]),
                                   p(self.coef[1]), p(self.coef[2]), p(self.ent_state), self.ent_state_bytes,
                                   p(self.ent_out), self.ent_cap, p(self.ent_sizes), p(self.ent_errs), p(self.ent_offs),
-                                  eh["offs"].data_ptr(), eh["dst"].data_ptr(), self.ent_dst_cap, p(self.ent_over), sc)
+                                  eh["offs"].data_ptr(), eh["dst"].data_ptr(), self.ent_dst_cap, p(self.ent_over), sc,
+                                  self._entropy_prof(pic.kind))
+            # the batch's QP table is freed when the encode returns: keep its block from being
+            # reused (by the compute stream's next batch) before this stream has read it
+            qp_row.record_stream(cs)
             eh["sizes"].copy_(self.ent_sizes, non_blocking=True)
             eh["errs"].copy_(self.ent_errs, non_blocking=True)
             if tmvp and pic.ref:

@@ -349,18 +349,19 @@ def _cut_clip(B, F, w, h, cut, seed):
     return out
 
 
-def test_gpu_hevc_encode_async_same_bytes():
+@pytest.mark.parametrize("entropy", ["host", "gpu"])
+def test_gpu_hevc_encode_async_same_bytes(entropy):
     """encode_async + analyse_async (bench/run.py config 4: batch k's CABAC jobs and result
     assembly overlap batch k + 1's GPU work, the next batch's lookahead runs on a side stream;
     the pinned host buffer sets, record double buffers and copy events cross the batch boundary)
-    give the bytes of the synchronous encode, batch by batch."""
+    give the bytes of the synchronous encode, batch by batch -- host or GPU entropy stage."""
     from govideocompressor_amd.models.h264_gpu import synth_clip
     from govideocompressor_amd.models.hevc_gpu import GpuHevcEncoder, HevcParams
     clips = [synth_clip(2, 9, 192, 128, seed=s, kind=k) for s, k in ((21, "default"), (22, "cuts"), (23, "fade"))]
-    ref_enc = GpuHevcEncoder(HevcParams(width=192, height=128, crf=27.0), slots=2)
+    ref_enc = GpuHevcEncoder(HevcParams(width=192, height=128, crf=27.0), slots=2, entropy=entropy)
     ref = [[r.bitstream for r in ref_enc.encode(*c, metrics=False)] for c in clips]
     ref_enc.close()
-    enc = GpuHevcEncoder(HevcParams(width=192, height=128, crf=27.0), slots=2)
+    enc = GpuHevcEncoder(HevcParams(width=192, height=128, crf=27.0), slots=2, entropy=entropy)
     side = torch.cuda.Stream()
     pend = []
     for c in clips:
