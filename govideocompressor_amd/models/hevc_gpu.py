@@ -348,15 +348,19 @@ class GpuHevcEncoder:
         # prevention stay on the host; "host": the native writer codes the records on
         # entropy_threads host threads (csrc/host/hevc_writer.cc)
         # "auto": host threads when this process has cores for them (8+ usable cores and
-        # entropy threads), else the GPU -- one rank's share of an 8-GPU node (2 cores) codes
-        # config 4 at 731 fps on the host and 1754 on the GPU, the whole 1-GPU box at 2465 on
-        # the host and 1754 on the GPU (profiles/r6_hevc_gpu_entropy.md)
+        # entropy threads) or when the batch is too narrow to fill the GPU's coder (fewer than
+        # 1024 substream waves: slots x min(16, CTU rows)), else the GPU.  One rank's share of an
+        # 8-GPU node (2 cores): config 4 (256 x 1080p) 731 fps on the host, 1846 on the GPU;
+        # config 5 (10 x 8K) 27.0 on the host, 11.8 on the GPU.  The whole 1-GPU box: config 4
+        # 2471 on the host, 1844 on the GPU (profiles/r6_hevc_gpu_entropy.md)
         self.entropy = (entropy or os.environ.get("MIVC_HEVC_ENTROPY", "auto")).lower()
         if self.entropy not in ("gpu", "host", "auto"):
             raise ValueError("entropy must be 'gpu', 'host' or 'auto'")
         if self.entropy == "auto":
             cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-            self.entropy = "host" if min(cores, self.entropy_threads) >= 8 else "gpu"
+            rows = -(-self.H // (64 if params.ctu64 else 32)) if params.wpp else 1
+            wide = self.B * min(16, rows) >= 1024
+            self.entropy = "gpu" if (min(cores, self.entropy_threads) < 8 and wide) else "host"
         if self.entropy == "gpu":
             self._alloc_entropy()
         self.pool = cf.ThreadPoolExecutor(max_workers=1)
