@@ -28,6 +28,18 @@
 #define HV_CYCLES() __builtin_ia32_rdtsc()
 #endif
 
+// On the device the coder object, its contexts, tables and sink live in LDS: telling the
+// compiler lets it use LDS instructions and exclude aliasing with global stores
+#if defined(__HIP_DEVICE_COMPILE__)
+#define HV_LDS(p) __builtin_assume(__builtin_amdgcn_is_shared(reinterpret_cast<const void*>(p)))
+#define HV_GLOBAL(p)                                                                 \
+  __builtin_assume(!__builtin_amdgcn_is_shared(reinterpret_cast<const void*>(p)) && \
+                   !__builtin_amdgcn_is_private(reinterpret_cast<const void*>(p)))
+#else
+#define HV_LDS(p) ((void)0)
+#define HV_GLOBAL(p) ((void)0)
+#endif
+
 namespace mivc {
 namespace hevc {
 
@@ -143,6 +155,8 @@ struct CabacEngine {
   // conditional moves, the renormalisation shift is a count of leading zeros, and the
   // state transition is one table entry
   MIVC_HD void encode(int bin, CtxState& c) {
+    HV_LDS(&c);
+    HV_LDS(step);
     const uint32_t s = c.state, mps = c.mps;
     uint32_t range = range_, low = low_;
     const uint32_t ent = step[(s << 2) | ((range >> 6) & 3)];
@@ -225,6 +239,7 @@ struct CabacEngine {
     if (bits_left_ < 12) write_out();
   }
   MIVC_HD void write_out() {
+    HV_LDS(out);
     const uint32_t lead = low_ >> (24 - bits_left_);
     bits_left_ += 8;
     low_ &= 0xFFFFFFFFu >> bits_left_;
@@ -488,6 +503,9 @@ struct CtuCoder {
   HV_BIG void begin(const CoderPic* pic, const CtuInfo* ct, const CuInfo* cu_, const CuInfo* col, const CoderLevels& l,
                      const CoderState& s, CtxState* ctx_mem, Sink* sink, const uint32_t* step_tab = nullptr,
                      const uint8_t* scans = nullptr, const uint8_t* sig = nullptr) __restrict__ {
+    HV_LDS(this);
+    HV_LDS(ctx);
+    HV_LDS(P);
     P = pic;
     ctu = ct;
     cu = cu_;
@@ -533,13 +551,17 @@ struct CtuCoder {
   HV_FN size_t g4(int x, int y) const __restrict__ { return static_cast<size_t>(y >> 2) * (2 * w8) + (x >> 2); }
   HV_FN bool inside(int x, int y) const __restrict__ { return x >= 0 && y >= 0 && x < W && y < H; }
   // 6.4.1 z-scan availability at 8x8 granularity (the granule is coded iff already visited)
-  HV_FN bool avail(int x, int y) const __restrict__ { return inside(x, y) && S.coded[g(x, y)]; }
+  HV_FN bool avail(int x, int y) const __restrict__ {
+    HV_GLOBAL(S.coded);
+    return inside(x, y) && S.coded[g(x, y)];
+  }
 
   // records of the current CTU staged in faster memory (GPU): [4 blocks in z-order][16 granules]
   const CuInfo* cu_stage = nullptr;
   int stage_cx = -1, stage_cy = -1;
   HV_FN const CuInfo& cu_at(int x, int y) const __restrict__ {
     if (cu_stage && (x >> L) == stage_cx && (y >> L) == stage_cy) {
+      HV_LDS(cu_stage);
       const int q = L == 6 ? ((((y >> 5) & 1) << 1) | ((x >> 5) & 1)) : 0;
       return cu_stage[q * kCusPerCtb + zorder8((x & (kCtb - 1)) >> 3, (y & (kCtb - 1)) >> 3)];
     }
@@ -567,6 +589,9 @@ struct CtuCoder {
     return ctu[(cy << k) * wctb + (cx << k)];
   }
   HV_BIG void write_sao(int rx, int ry) __restrict__ {
+    HV_LDS(this);
+    HV_LDS(ctx);
+    HV_LDS(P);
     const ProfScope prof_scope(prof, CP_SAO);
     const CtuInfo& t = ctu_sao(rx, ry);
     if (rx > 0 && same_sao(t, ctu_sao(rx - 1, ry))) {
@@ -670,6 +695,7 @@ struct CtuCoder {
       }
       const size_t at = static_cast<size_t>(ctb_base) + rank;
       if (at < lv.nblocks) {
+        HV_LDS(lv.levels);  // the device stages the CTU's blocks in LDS
         memcpy(rows, lv.levels + at * 16, 32);
         return;
       }
@@ -698,6 +724,9 @@ struct CtuCoder {
   // gmask: bit (ys * nsb + xs) set for every non-zero 4x4 sub-block of the TU (from the CTB's
   // sub-block map), so all-zero sub-blocks are never loaded
   HV_BIG void write_residual(int cidx, int bx0, int by0, int log2, int scan_idx, uint64_t gmask) __restrict__ {
+    HV_LDS(this);
+    HV_LDS(ctx);
+    HV_LDS(P);
     const ProfScope prof_scope(prof, CP_RESIDUAL);
     const int log2sb = log2 - 2, nsb = 1 << log2sb, nsbsq = nsb * nsb;
     const uint8_t* sbs = scans_tab + (scan_idx * 4 + log2sb) * 64;
@@ -726,6 +755,10 @@ struct CtuCoder {
     // memory because the coder's address crosses the out-of-line calls)
     CabacEngine<Sink> en = e;
     CtxState* const cx = ctx;  // a local: stores through the contexts cannot move it
+    HV_LDS(cx);
+    HV_LDS(sig_tab);
+    HV_LDS(scans_tab);
+    HV_LDS(en.out);
     int lx = (sbs[last_i] & 15) * 4 + (ps[last_p] & 15), ly = (sbs[last_i] >> 4) * 4 + (ps[last_p] >> 4);
     if (scan_idx == 2) {
       const int t = lx;
@@ -845,6 +878,9 @@ struct CtuCoder {
   HV_FN static int mdcs(int mode) { return (mode >= 6 && mode <= 14) ? 2 : ((mode >= 22 && mode <= 30) ? 1 : 0); }
 
   HV_BIG void scan_ctb_nz(int x0, int y0) __restrict__ {
+    HV_LDS(this);
+    HV_LDS(ctx);
+    HV_LDS(P);
     const ProfScope prof_scope(prof, CP_SCAN);
     const size_t ci = static_cast<size_t>(y0 / kCtb) * wctb + x0 / kCtb;
     if (lv.nzmap) {
@@ -908,8 +944,31 @@ struct CtuCoder {
   // ---------------------------------------------------------------- inter prediction helpers
   // A PU's motion is its direction (bit 0 list 0, bit 1 list 1) and a refIdx + vector per used
   // list; RefPicListX holds num_ref[X] pictures (POC list_poc(X, i)).
-  HV_FN bool inter_avail(int x, int y) const __restrict__ { return avail(x, y) && S.pred[g(x, y)] == CU_INTER; }
-  HV_FN const Motion& mot_at(int x, int y) const __restrict__ { return S.mot[g(x, y)]; }
+  HV_FN bool inter_avail(int x, int y) const __restrict__ {
+    HV_GLOBAL(S.pred);
+    return avail(x, y) && S.pred[g(x, y)] == CU_INTER;
+  }
+  HV_FN const Motion& mot_at(int x, int y) const __restrict__ {
+    HV_GLOBAL(S.mot);
+    return S.mot[g(x, y)];
+  }
+  // a neighbour granule's inter availability and motion, loaded unconditionally (coordinates
+  // clamped into the picture): the probes of a candidate list issue together instead of one
+  // dependent load after another (the motion is meaningful only where `inter`)
+  struct Nb {
+    bool inter;
+    Motion m;
+  };
+  HV_FN Nb probe(int xn, int yn) const __restrict__ {
+    const bool in = inside(xn, yn);
+    const size_t k = g(hv_clamp(xn, 0, W - 1), hv_clamp(yn, 0, H - 1));
+    const uint8_t cd = S.coded[k];
+    const int8_t pr = S.pred[k];
+    Nb r;
+    r.m = S.mot[k];
+    r.inter = in && cd && pr == CU_INTER;
+    return r;
+  }
   HV_FN int ref_poc(int l) const __restrict__ {
     return l == 0 ? (P->ref_poc[0] >= 0 ? P->ref_poc[0] : P->poc - 1) : P->ref_poc[1];
   }
@@ -928,6 +987,9 @@ struct CtuCoder {
 
   // 8.5.3.2.8 / 8.5.3.2.9 temporal vector of list X (target refIdx ri) for the PU (x, y, n x n)
   HV_BIG bool col_at(int xc, int yc, int X, int ri, Mv* out) __restrict__ {
+    HV_LDS(this);
+    HV_LDS(ctx);
+    HV_LDS(P);
     if (!col_cu || xc >= W || yc >= H) return false;
     const int ci = (yc >> kCtbLog2) * wctb + (xc >> kCtbLog2);
     const CuInfo& cc = col_cu[static_cast<size_t>(ci) * kCusPerCtb + zorder8((xc & (kCtb - 1)) >> 3, (yc & (kCtb - 1)) >> 3)];
@@ -959,17 +1021,21 @@ struct CtuCoder {
 
   // 8.5.3.2.2-8.5.3.2.5 merge candidates of a 2Nx2N PU (MaxNumMergeCand entries)
   HV_BIG int merge_list(int x, int y, int n, Motion* out) __restrict__ {
+    HV_LDS(this);
+    HV_LDS(ctx);
+    HV_LDS(P);
     const ProfScope prof_scope(prof, CP_MERGE);
     Motion cand[8];
     int k = 0;
     const Motion none = motion_none();
-    const int xa1 = x - 1, ya1 = y + n - 1, xb1 = x + n - 1, yb1 = y - 1;
-    const bool a1 = inter_avail(xa1, ya1), av_b1 = inter_avail(xb1, yb1);
-    const Motion ma1 = a1 ? mot_at(xa1, ya1) : none, mb1 = av_b1 ? mot_at(xb1, yb1) : none;
+    const Nb na1 = probe(x - 1, y + n - 1), nb1 = probe(x + n - 1, y - 1), nb0 = probe(x + n, y - 1);
+    const Nb na0 = probe(x - 1, y + n), nb2 = probe(x - 1, y - 1);
+    const bool a1 = na1.inter, av_b1 = nb1.inter;
+    const Motion ma1 = a1 ? na1.m : none, mb1 = av_b1 ? nb1.m : none;
     const bool b1 = av_b1 && !(a1 && ma1 == mb1);
-    bool b0 = inter_avail(x + n, y - 1), a0 = inter_avail(x - 1, y + n), b2 = inter_avail(x - 1, y - 1);
-    const Motion mb0 = b0 ? mot_at(x + n, y - 1) : none, ma0 = a0 ? mot_at(x - 1, y + n) : none;
-    const Motion mb2 = b2 ? mot_at(x - 1, y - 1) : none;
+    bool b0 = nb0.inter, a0 = na0.inter, b2 = nb2.inter;
+    const Motion mb0 = b0 ? nb0.m : none, ma0 = a0 ? na0.m : none;
+    const Motion mb2 = b2 ? nb2.m : none;
     if (b0 && av_b1 && mb1 == mb0) b0 = false;
     if (a0 && a1 && ma1 == ma0) a0 = false;
     if (b2 && ((a1 && ma1 == mb2) || (av_b1 && mb1 == mb2))) b2 = false;
@@ -1016,8 +1082,7 @@ struct CtuCoder {
   }
 
   // a neighbour vector pointing at the target picture (8.5.3.2.7, no scaling)
-  HV_FN bool amvp_same(int xn, int yn, int X, int tgt, Mv* v) const __restrict__ {
-    const Motion& m = mot_at(xn, yn);
+  HV_FN bool amvp_same(const Motion& m, int X, int tgt, Mv* v) const __restrict__ {
     const int Y = 1 - X;
     if ((m.dir >> X) & 1 && list_poc(X, m.r[X]) == tgt) {
       *v = m.m[X];
@@ -1030,8 +1095,7 @@ struct CtuCoder {
     return false;
   }
   // any vector of the neighbour, scaled by the POC distances
-  HV_FN bool amvp_scaled(int xn, int yn, int X, int tgt, Mv* v) const __restrict__ {
-    const Motion& m = mot_at(xn, yn);
+  HV_FN bool amvp_scaled(const Motion& m, int X, int tgt, Mv* v) const __restrict__ {
     for (int j = 0; j < 2; ++j) {
       const int Lx = j == 0 ? X : 1 - X;
       if (!((m.dir >> Lx) & 1)) continue;
@@ -1044,21 +1108,22 @@ struct CtuCoder {
 
   // 8.5.3.2.6-8.5.3.2.7 AMVP candidates of list X, refIdx ri
   HV_BIG void amvp_list(int x, int y, int n, int X, int ri, Mv* out) __restrict__ {
+    HV_LDS(this);
+    HV_LDS(ctx);
+    HV_LDS(P);
     const ProfScope prof_scope(prof, CP_AMVP);
     const int tgt = list_poc(X, ri);
-    const int xa[2] = {x - 1, x - 1}, ya[2] = {y + n, y + n - 1};
-    const bool ava[2] = {inter_avail(xa[0], ya[0]), inter_avail(xa[1], ya[1])};
-    const bool is_scaled = ava[0] || ava[1];
+    const Nb pa[2] = {probe(x - 1, y + n), probe(x - 1, y + n - 1)};
+    const Nb pb[3] = {probe(x + n, y - 1), probe(x + n - 1, y - 1), probe(x - 1, y - 1)};
+    const bool is_scaled = pa[0].inter || pa[1].inter;
     bool fa = false, fb = false;
     Mv ma{0, 0}, mb{0, 0};
     for (int k = 0; k < 2 && !fa; ++k)
-      if (ava[k]) fa = amvp_same(xa[k], ya[k], X, tgt, &ma);
+      if (pa[k].inter) fa = amvp_same(pa[k].m, X, tgt, &ma);
     for (int k = 0; k < 2 && !fa; ++k)
-      if (ava[k]) fa = amvp_scaled(xa[k], ya[k], X, tgt, &ma);
-    const int xb[3] = {x + n, x + n - 1, x - 1}, yb = y - 1;
-    const bool avb[3] = {inter_avail(xb[0], yb), inter_avail(xb[1], yb), inter_avail(xb[2], yb)};
+      if (pa[k].inter) fa = amvp_scaled(pa[k].m, X, tgt, &ma);
     for (int k = 0; k < 3 && !fb; ++k)
-      if (avb[k]) fb = amvp_same(xb[k], yb, X, tgt, &mb);
+      if (pb[k].inter) fb = amvp_same(pb[k].m, X, tgt, &mb);
     if (!is_scaled && fb) {
       ma = mb;
       fa = true;
@@ -1066,7 +1131,7 @@ struct CtuCoder {
     if (!is_scaled) {
       fb = false;
       for (int k = 0; k < 3 && !fb; ++k)
-        if (avb[k]) fb = amvp_scaled(xb[k], yb, X, tgt, &mb);
+        if (pb[k].inter) fb = amvp_scaled(pb[k].m, X, tgt, &mb);
     }
     int k = 0;
     if (fa) out[k++] = ma;
@@ -1080,6 +1145,12 @@ struct CtuCoder {
 
   // ---------------------------------------------------------------- coding unit (7.3.8.5)
   HV_FN void mark(int x, int y, int n, int d, int sk, int pm, int md, const Motion& mv) __restrict__ {
+    HV_GLOBAL(S.depth);
+    HV_GLOBAL(S.skip);
+    HV_GLOBAL(S.pred);
+    HV_GLOBAL(S.mode4);
+    HV_GLOBAL(S.mot);
+    HV_GLOBAL(S.coded);
     for (int yy = y; yy < y + n; yy += 8)
       for (int xx = x; xx < x + n; xx += 8) {
         const size_t k = g(xx, yy);
@@ -1118,6 +1189,9 @@ struct CtuCoder {
   }
 
   HV_BIG void write_cu_body(int x, int y, int log2, int d) __restrict__ {
+    HV_LDS(this);
+    HV_LDS(ctx);
+    HV_LDS(P);
     const ProfScope prof_scope(prof, CP_CU);
     const int n = 1 << log2;
     const CuInfo& ci = cu_at(x, y);
@@ -1263,6 +1337,9 @@ struct CtuCoder {
   // depth 1; cbfChroma of every 4x4 TU is the parent's, and the 4x4 chroma blocks follow
   // the last luma TU (blkIdx 3)
   HV_BIG void write_tu_nxn(int x, int y, const int* m, bool cb_cb, bool cb_cr) __restrict__ {
+    HV_LDS(this);
+    HV_LDS(ctx);
+    HV_LDS(P);
     e.encode(cb_cb, ctx[CTX_CBF_CHROMA + 0]);
     e.encode(cb_cr, ctx[CTX_CBF_CHROMA + 0]);
     for (int k = 0; k < 4; ++k) {
@@ -1312,6 +1389,9 @@ struct CtuCoder {
   // chroma cbfs at depth 0, then per quarter TU (z-order) its chroma cbfs under a set parent,
   // cbf_luma (always coded below depth 0) and the transform unit
   HV_BIG void write_tu_inter_split(int x, int y, int log2, bool cb_cb, bool cb_cr) __restrict__ {
+    HV_LDS(this);
+    HV_LDS(ctx);
+    HV_LDS(P);
     if (P->tu_inter_depth < 1 || log2 < 4) fail(CE_INTER_SPLIT);
     e.encode(1, ctx[CTX_SPLIT_TRANSFORM + 5 - log2]);
     e.encode(cb_cb, ctx[CTX_CBF_CHROMA + 0]);
@@ -1334,6 +1414,9 @@ struct CtuCoder {
 
   // transform_tree at depth 0 with TU = CU (7.3.8.8 / 7.3.8.10)
   HV_BIG void write_tu(int x, int y, int log2, bool intra, int m, bool cb_y, bool cb_cb, bool cb_cr) __restrict__ {
+    HV_LDS(this);
+    HV_LDS(ctx);
+    HV_LDS(P);
     // split_transform_flag 0 where the inter depth allows a split (intra: depth 0 at 2Nx2N)
     if (!intra && P->tu_inter_depth > 0 && log2 > 2) e.encode(0, ctx[CTX_SPLIT_TRANSFORM + 5 - log2]);
     e.encode(cb_cb, ctx[CTX_CBF_CHROMA + 0]);
@@ -1354,6 +1437,9 @@ struct CtuCoder {
   // cu_qp_delta_abs (9.3.3.10: TR prefix cMax 5, ctxInc 0 then 1; EG0 bypass suffix) and
   // the bypass sign, in the first TU of the quantization group with a coded block
   HV_BIG void write_qp_delta() __restrict__ {
+    HV_LDS(this);
+    HV_LDS(ctx);
+    HV_LDS(P);
     const int d = qp_ctb - qp_pred_cur;
     const int qbd = 6 * (P->bit_depth - 8);
     if (d < -(26 + qbd / 2) || d > 25 + qbd / 2) fail(CE_QP_DELTA);
@@ -1386,6 +1472,9 @@ struct CtuCoder {
 
   // coding_quadtree (7.3.8.4) of one CTU (CTU coordinates)
   HV_BIG void write_ctu(int cx, int cy) __restrict__ {
+    HV_LDS(this);
+    HV_LDS(ctx);
+    HV_LDS(P);
     if (!P->ctu64) {
       write_block_tree(cx, cy, 0);
       return;
@@ -1410,6 +1499,9 @@ struct CtuCoder {
 
   // one 32x32 record block = one quantization group; dofs: its depth in the CTU quadtree
   HV_BIG void write_block_tree(int rx, int ry, int dofs) __restrict__ {
+    HV_LDS(this);
+    HV_LDS(ctx);
+    HV_LDS(P);
     const CtuInfo& t = ctu[ry * wctb + rx];
     const int x0 = rx * kCtb, y0 = ry * kCtb;
     qp_ctb = t.qp;
@@ -1441,6 +1533,9 @@ struct CtuCoder {
   // reconstruction is the same: motion compensation is per sample and every inner edge has
   // boundary strength 0)
   HV_BIG bool cu64_ok(int cx, int cy) __restrict__ {
+    HV_LDS(this);
+    HV_LDS(ctx);
+    HV_LDS(P);
     const int x0 = cx << 6, y0 = cy << 6;
     if (!inter_slice) return false;
     Motion m0 = motion_none();
@@ -1484,6 +1579,9 @@ struct CtuCoder {
   // SAO + coding quadtree of CTU (rx, ry) and its end_of_slice_segment_flag; with WPP, a
   // row's last CTU also codes end_of_subset_one_bit, flushes and byte-aligns its substream
   HV_BIG void code_ctu(int rx, int ry) __restrict__ {
+    HV_LDS(this);
+    HV_LDS(ctx);
+    HV_LDS(P);
     const ProfScope prof_scope(prof, CP_CTU);
     if (P->sao) write_sao(rx, ry);
     write_ctu(rx, ry);
