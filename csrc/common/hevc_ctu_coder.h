@@ -959,6 +959,20 @@ struct CtuCoder {
     bool inter;
     Motion m;
   };
+  // neighbour flag probes with unconditional (clamped) loads, so a context's two probes
+  // overlap: skip flag of a coded neighbour, depth of a coded neighbour deeper than d
+  HV_FN int nb_skip(int xn, int yn) const __restrict__ {
+    const size_t k = g(hv_clamp(xn, 0, W - 1), hv_clamp(yn, 0, H - 1));
+    const uint8_t cd = S.coded[k];
+    const int8_t sk = S.skip[k];
+    return (inside(xn, yn) && cd && sk) ? 1 : 0;
+  }
+  HV_FN int nb_deeper(int xn, int yn, int d) const __restrict__ {
+    const size_t k = g(hv_clamp(xn, 0, W - 1), hv_clamp(yn, 0, H - 1));
+    const uint8_t cd = S.coded[k];
+    const int8_t dp = S.depth[k];
+    return (inside(xn, yn) && cd && dp > d) ? 1 : 0;
+  }
   HV_FN Nb probe(int xn, int yn) const __restrict__ {
     const bool in = inside(xn, yn);
     const size_t k = g(hv_clamp(xn, 0, W - 1), hv_clamp(yn, 0, H - 1));
@@ -1209,7 +1223,7 @@ struct CtuCoder {
         mv.r[X] = 0;
       }
     if (inter_slice) {
-      const int skip_ctx = (avail(x - 1, y) && S.skip[g(x - 1, y)]) + (avail(x, y - 1) && S.skip[g(x, y - 1)]);
+      const int skip_ctx = nb_skip(x - 1, y) + nb_skip(x, y - 1);
       int midx = -1;
       if (!intra) {
         Motion ml[5];
@@ -1327,9 +1341,14 @@ struct CtuCoder {
   // with PUs of size h and modes m
   HV_FN int mpm_cand(int x, int y, int h, const int* m, int xn, int yn, int yk, bool above) const __restrict__ {
     if (xn >= x && yn >= y) return m[(xn - x >= h) + 2 * (yn - y >= h)];
-    if (!avail(xn, yn) || S.pred[g(xn, yn)] != CU_INTRA) return 1;
+    // the three loads unconditional (clamped), then the availability logic
+    const int xc = hv_clamp(xn, 0, W - 1), yc = hv_clamp(yn, 0, H - 1);
+    const uint8_t cd = S.coded[g(xc, yc)];
+    const int8_t pr = S.pred[g(xc, yc)];
+    const int md = S.mode4[g4(xc, yc)];
+    if (!inside(xn, yn) || !cd || pr != CU_INTRA) return 1;
     if (above && (yn >> L) != (yk >> L)) return 1;
-    return static_cast<int>(S.mode4[g4(xn, yn)]);
+    return md;
   }
 
   // transform_tree of an intra PART_NxN CU (7.3.8.8 / 7.3.8.10): chroma cbfs at depth 0,
@@ -1494,7 +1513,7 @@ struct CtuCoder {
   }
 
   HV_FN int split_ctx(int x, int y, int d) const __restrict__ {
-    return (avail(x - 1, y) && S.depth[g(x - 1, y)] > d) + (avail(x, y - 1) && S.depth[g(x, y - 1)] > d);
+    return nb_deeper(x - 1, y, d) + nb_deeper(x, y - 1, d);
   }
 
   // one 32x32 record block = one quantization group; dofs: its depth in the CTU quadtree
@@ -1564,7 +1583,7 @@ struct CtuCoder {
     return cu64_midx >= 0;
   }
   HV_FN void write_cu64_skip(int x0, int y0) __restrict__ {
-    const int skip_ctx = (avail(x0 - 1, y0) && S.skip[g(x0 - 1, y0)]) + (avail(x0, y0 - 1) && S.skip[g(x0, y0 - 1)]);
+    const int skip_ctx = nb_skip(x0 - 1, y0) + nb_skip(x0, y0 - 1);
     e.encode(1, ctx[CTX_CU_SKIP + skip_ctx]);
     write_merge_idx(cu64_midx);
     mark(x0, y0, 64, 0, 1, CU_INTER, 1, cu64_mot);

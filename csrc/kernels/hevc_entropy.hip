@@ -15,6 +15,8 @@
 // prevention.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "../common/hevc_ctu_coder.h"
 #include "kcommon.h"
 
@@ -339,7 +341,16 @@ extern "C" int mivc_launch_hevc_entropy(const void* pic, int B, const int* qp, c
   a.sizes = sizes;
   a.errs = errs;
   a.nsub = nsub;
-  const int lanes = 64 * (nsub < 16 ? nsub : 16);  // a wave per row, rows beyond 16 round-robin
+  // a wave per row up to MIVC_HEVC_ENTROPY_WAVES (default 8: config 4 2052 fps vs 1953 at 16
+  // and 1986 at 4, profiles/r6_hevc_gpu_entropy.md) per picture, further rows
+  // round-robin: fewer waves leave more of each CU's registers to the compute stream's
+  // kernels running concurrently, at a longer critical path per picture
+  static const int max_waves = [] {
+    const char* e = std::getenv("MIVC_HEVC_ENTROPY_WAVES");
+    const int v = e ? std::atoi(e) : 8;
+    return v < 1 ? 1 : (v > 16 ? 16 : v);
+  }();
+  const int lanes = 64 * (nsub < max_waves ? nsub : max_waves);
   const size_t lds = static_cast<size_t>(2) * nsub * mivc::hevc::kNumCtx * sizeof(CtxState);  // <= 60 KB
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(hevc_entropy, dim3(B), dim3(lanes), lds, s, a);
