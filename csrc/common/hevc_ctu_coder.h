@@ -1000,13 +1000,30 @@ struct CtuCoder {
   }
 
   // 8.5.3.2.8 / 8.5.3.2.9 temporal vector of list X (target refIdx ri) for the PU (x, y, n x n)
-  HV_BIG bool col_at(int xc, int yc, int X, int ri, Mv* out) __restrict__ {
-    HV_LDS(this);
-    HV_LDS(ctx);
-    HV_LDS(P);
-    if (!col_cu || xc >= W || yc >= H) return false;
+  // the collocated records of a PU (8.5.3.2.8): bottom-right and centre candidates, both loaded
+  // up front (one memory latency for the pair, shared by the L0 and L1 derivations)
+  struct ColPair {
+    CuInfo br, ce;
+    bool br_ok, ce_ok;
+  };
+  HV_FN const CuInfo& col_rec(int xc, int yc) const __restrict__ {
     const int ci = (yc >> kCtbLog2) * wctb + (xc >> kCtbLog2);
-    const CuInfo& cc = col_cu[static_cast<size_t>(ci) * kCusPerCtb + zorder8((xc & (kCtb - 1)) >> 3, (yc & (kCtb - 1)) >> 3)];
+    return col_cu[static_cast<size_t>(ci) * kCusPerCtb + zorder8((xc & (kCtb - 1)) >> 3, (yc & (kCtb - 1)) >> 3)];
+  }
+  HV_FN ColPair col_pair(int x, int y, int n) const __restrict__ {
+    ColPair c;
+    const int xbr = ((x + n) >> 4) << 4, ybr = ((y + n) >> 4) << 4;
+    const int xce = ((x + (n >> 1)) >> 4) << 4, yce = ((y + (n >> 1)) >> 4) << 4;
+    c.br_ok = tmvp && col_cu && (y >> L) == ((y + n) >> L) && y + n < H && x + n < W && xbr < W && ybr < H;
+    c.ce_ok = tmvp && col_cu && xce < W && yce < H;
+    if (col_cu) {
+      c.br = col_rec(hv_min(xbr, W - 1), hv_min(ybr, H - 1));
+      c.ce = col_rec(hv_min(xce, W - 1), hv_min(yce, H - 1));
+    }
+    return c;
+  }
+  // 8.5.3.2.9 temporal vector of list X (target refIdx ri) from a collocated record
+  HV_FN bool col_mv(const CuInfo& cc, int X, int ri, Mv* out) __restrict__ {
     if (cc.pred != CU_INTER) return false;
     const int dir = cu_dir(cc);
     int list;
@@ -1025,12 +1042,9 @@ struct CtuCoder {
     *out = v;
     return true;
   }
-  HV_FN bool temporal(int x, int y, int n, int X, int ri, Mv* out) __restrict__ {
-    if (!tmvp) return false;
-    const int xbr = x + n, ybr = y + n;
-    if ((y >> L) == (ybr >> L) && ybr < H && xbr < W && col_at((xbr >> 4) << 4, (ybr >> 4) << 4, X, ri, out))
-      return true;
-    return col_at(((x + (n >> 1)) >> 4) << 4, ((y + (n >> 1)) >> 4) << 4, X, ri, out);
+  HV_FN bool temporal(const ColPair& c, int X, int ri, Mv* out) __restrict__ {
+    if (c.br_ok && col_mv(c.br, X, ri, out)) return true;
+    return c.ce_ok && col_mv(c.ce, X, ri, out);
   }
 
   // 8.5.3.2.2-8.5.3.2.5 merge candidates of a 2Nx2N PU (MaxNumMergeCand entries)
@@ -1061,8 +1075,9 @@ struct CtuCoder {
     if (b2) cand[k++] = mb2;
     if (k < P->max_merge && tmvp) {
       Motion t = none;
-      if (temporal(x, y, n, 0, 0, &t.m[0])) t.dir |= DIR_L0;  // refIdx 0 (8.5.3.2.8 merge: refIdxLXCol 0)
-      if (bslice && temporal(x, y, n, 1, 0, &t.m[1])) t.dir |= DIR_L1;
+      const ColPair cp = col_pair(x, y, n);
+      if (temporal(cp, 0, 0, &t.m[0])) t.dir |= DIR_L0;  // refIdx 0 (8.5.3.2.8 merge: refIdxLXCol 0)
+      if (bslice && temporal(cp, 1, 0, &t.m[1])) t.dir |= DIR_L1;
       if (t.dir) cand[k++] = t;
     }
     const int orig = k;
@@ -1127,6 +1142,7 @@ struct CtuCoder {
     HV_LDS(P);
     const ProfScope prof_scope(prof, CP_AMVP);
     const int tgt = list_poc(X, ri);
+    const ColPair cp = col_pair(x, y, n);  // issued with the spatial probes
     const Nb pa[2] = {probe(x - 1, y + n), probe(x - 1, y + n - 1)};
     const Nb pb[3] = {probe(x + n, y - 1), probe(x + n - 1, y - 1), probe(x - 1, y - 1)};
     const bool is_scaled = pa[0].inter || pa[1].inter;
@@ -1152,7 +1168,7 @@ struct CtuCoder {
     if (fb && !(fa && ma == mb)) out[k++] = mb;
     if (k < 2) {
       Mv t{0, 0};
-      if (temporal(x, y, n, X, ri, &t)) out[k++] = t;
+      if (temporal(cp, X, ri, &t)) out[k++] = t;
     }
     while (k < 2) out[k++] = Mv{0, 0};
   }
