@@ -854,6 +854,31 @@ PYBIND11_MODULE(_host, m) {
       },
       py::arg("cfg"), py::arg("frame"), py::arg("ctu"), py::arg("cu"), py::arg("nzmap"), py::arg("ctb_off"),
       py::arg("levels"));
+  m.def(
+      "hevc_slice_substreams",
+      [](const py::dict& cfg, const py::dict& fp, py::array_t<uint8_t, py::array::c_style> ctu,
+         py::array_t<uint8_t, py::array::c_style> cu, py::array_t<int16_t, py::array::c_style> cy,
+         py::array_t<int16_t, py::array::c_style> cb, py::array_t<int16_t, py::array::c_style> cr) {
+        // the slice data substreams the host writer codes for a picture (one per CTU row with
+        // WPP), for checking hevc_assemble_slices against hevc_write_slice
+        hevc::HevcConfig c = hevc_cfg_from(cfg);
+        const py::ssize_t nctu = static_cast<py::ssize_t>(c.wctb()) * c.hctb();
+        std::vector<py::array> keep;
+        const hevc::HevcFrameParams f = hevc_frame_from(fp, keep, static_cast<size_t>(nctu) * hevc::kCusPerCtb * hevc::kCuInfoBytes);
+        const py::ssize_t W = c.coded_width(), H = c.coded_height();
+        if (ctu.size() != nctu * 32 || cu.size() != nctu * hevc::kCusPerCtb * hevc::kCuInfoBytes ||
+            cy.size() != W * H || cb.size() != W * H / 4 || cr.size() != W * H / 4)
+          throw std::runtime_error("records / planes: wrong size");
+        std::vector<std::vector<uint8_t>> subs;
+        hevc::hevc_write_slice(c, f, reinterpret_cast<const hevc::CtuInfo*>(ctu.data()),
+                               reinterpret_cast<const hevc::CuInfo*>(cu.data()), cy.data(), cb.data(), cr.data(), nullptr,
+                               nullptr, &subs);
+        py::list out;
+        for (auto& v : subs) out.append(to_bytes(v));
+        return out;
+      },
+      py::arg("cfg"), py::arg("frame"), py::arg("ctu"), py::arg("cu"), py::arg("coef_y"), py::arg("coef_cb"),
+      py::arg("coef_cr"));
   m.def("hevc_coder_pic", [](const py::dict& cfg, const py::dict& fp) {
     // the GPU entropy kernel's view of a picture (hevc_ctu_coder.h CoderPic) as bytes
     const hevc::HevcConfig c = hevc_cfg_from(cfg);

@@ -126,7 +126,8 @@ struct PackedLevels {
 std::vector<uint8_t> hevc_write_slice(const HevcConfig& cfg, const HevcFrameParams& fp, const CtuInfo* ctu,
                                       const CuInfo* cu, const int16_t* coef_y, const int16_t* coef_cb,
                                       const int16_t* coef_cr, HevcSliceStats* stats,
-                                      const PackedLevels* packed = nullptr);
+                                      const PackedLevels* packed = nullptr,
+                                      std::vector<std::vector<uint8_t>>* substreams = nullptr);
 
 // The slice-data coder's view of a picture (hevc_ctu_coder.h): sizes, tools, slice type, QP,
 // reference / collocated POCs (the collocated records pointer is passed separately)

@@ -420,7 +420,8 @@ std::vector<uint8_t> hevc_assemble_slice(const HevcConfig& c, const HevcFramePar
 
 std::vector<uint8_t> hevc_write_slice(const HevcConfig& c, const HevcFrameParams& fp, const CtuInfo* ctu,
                                       const CuInfo* cu, const int16_t* coef_y, const int16_t* coef_cb,
-                                      const int16_t* coef_cr, HevcSliceStats* stats, const PackedLevels* packed) {
+                                      const int16_t* coef_cr, HevcSliceStats* stats, const PackedLevels* packed,
+                                      std::vector<std::vector<uint8_t>>* substreams) {
   BitWriter bw;
   slice_header(bw, c, fp);
   // CTUs (64x64 with ctu64, else the 32x32 record blocks themselves): one substream per CTU
@@ -518,6 +519,8 @@ std::vector<uint8_t> hevc_write_slice(const HevcConfig& c, const HevcFrameParams
     total.skip_cus += rst[r].skip_cus;
     total.merge_cus += rst[r].merge_cus;
   }
+  if (substreams)  // the slice data as coded, before the entry points (tests of hevc_assemble_slice)
+    for (int r = 0; r < nsub; ++r) substreams->push_back(sub[r].bytes());
   std::vector<uint8_t> out = finish_slice(bw, c, fp, ptrs.data(), sizes.data(), nsub);
   if (stats) {
     *stats = total;

@@ -399,3 +399,37 @@ def test_hevc_adaptive_gop_stream_decodes(host):
         inter = cu[:, 0] == 1
         assert np.array_equal(p["cu"][inter, 4:12], cu[inter, 4:12])     # vectors
         assert np.array_equal(p["cu"][inter, 13:15], cu[inter, 13:15])   # refIdx
+
+
+@pytest.mark.parametrize("wpp,ctu64,w,h", [(1, 1, 192, 160), (0, 1, 192, 160), (1, 0, 160, 96), (0, 0, 96, 64)])
+def test_hevc_assemble_slices_matches_writer(host, wpp, ctu64, w, h):
+    """The GPU entropy path's host half (hevc_assemble_slices: slice header, WPP entry points,
+    byte alignment, emulation prevention around substreams coded elsewhere) rebuilds exactly the
+    NAL the host writer produces from the same substreams -- I and P slices, CTU 64 / 32, WPP
+    on / off, several substreams packed at 16-byte aligned offsets as the GPU gather leaves them."""
+    from govideocompressor_amd.utils.hevc_synth import random_records
+
+    rng = np.random.default_rng(17 + wpp + 2 * ctu64)
+    cfg = dict(width=w, height=h, wpp=wpp, ctu64=ctu64, cu_qp_delta=1)
+    frames = [dict(idr=1, poc=0, qp=30, slice_type=2), dict(idr=0, poc=1, qp=31, slice_type=1)]
+    recs = [random_records(rng, w, h, pslice=False, ctb_qp=(30, 4)),
+            random_records(rng, w, h, pslice=True, ctb_qp=(31, 4))]
+    data, offs, sizes, want = bytearray(), [], [], []
+    for fp, r in zip(frames, recs):
+        want.append(host.hevc_write_slice(cfg, fp, *r)[0])
+        subs = host.hevc_slice_substreams(cfg, fp, *r)
+        assert len(subs) == ((-(-h // (64 if ctu64 else 32))) if wpp else 1)
+        for sb in subs:
+            offs.append(len(data))
+            sizes.append(len(sb))
+            data += sb + bytes(-len(sb) % 16)
+    offs.append(len(data))
+    got = host.hevc_assemble_slices(cfg, frames, np.frombuffer(bytes(data), np.uint8), np.array(offs, np.uint64),
+                                    np.array(sizes, np.uint32), np.zeros(len(sizes), np.int32), 2)
+    assert got == want
+    # a coder error reported by the GPU for any substream is raised with its message
+    errs = np.zeros(len(sizes), np.int32)
+    errs[-1] = 1
+    with pytest.raises(RuntimeError, match="all-zero block"):
+        host.hevc_assemble_slices(cfg, frames, np.frombuffer(bytes(data), np.uint8), np.array(offs, np.uint64),
+                                  np.array(sizes, np.uint32), errs, 1)
