@@ -412,7 +412,10 @@ class GpuHevcEncoder:
         self.ent_cap = ((per_ctu * wctu * (1 if self.p.wpp else hctu)) + 15) // 16 * 16
         self.ent_state_bytes = int(self.hip.hevc_entropy_state_bytes(W, H))
         self.ent_state = torch.empty((B, self.ent_state_bytes), dtype=torch.uint8, device=dev)
-        self.ent_out = torch.empty((B * self.ent_nsub * self.ent_cap,), dtype=torch.uint8, device=dev)
+        # one substream area per pinned host set: a step whose slice data outgrows the pinned
+        # buffer is read back from its own area, which the next steps do not overwrite
+        self.ent_outs = [torch.empty((B * self.ent_nsub * self.ent_cap,), dtype=torch.uint8, device=dev)
+                         for _ in range(3)]
         n = B * self.ent_nsub
         self.ent_sizes = torch.zeros((n,), dtype=torch.int32, device=dev)
         self.ent_errs = torch.zeros((n,), dtype=torch.int32, device=dev)
@@ -1191,7 +1194,7 @@ class GpuHevcEncoder:
                                       p(self.nzcnt), p(nzoff), self.pack_cap, 0, p(self.err), sc)
             self.hip.hevc_entropy(pic_bytes, B, p(qp_row), p(self.ctu), p(self.cu), col_ptr, p(nzmap), p(self.coef[0]),
                                   p(self.coef[1]), p(self.coef[2]), p(self.ent_state), self.ent_state_bytes,
-                                  p(self.ent_out), self.ent_cap, p(self.ent_sizes), p(self.ent_errs), p(self.ent_offs),
+                                  p(self.ent_outs[hb]), self.ent_cap, p(self.ent_sizes), p(self.ent_errs), p(self.ent_offs),
                                   eh["offs"].data_ptr(), eh["dst"].data_ptr(), self.ent_dst_cap, p(self.ent_over), sc,
                                   self._entropy_prof(pic.kind))
             # the batch's QP table is freed when the encode returns: keep its block from being
@@ -1210,21 +1213,28 @@ class GpuHevcEncoder:
             anchor_meta[pic.d] = (pic.slot, pic.l0, pic.l1, pic.refs0)
         n = B * self.ent_nsub
 
-        def job(done=done, base=base, qcol=qcol, wrow=wrow, eh=eh):
+        def job(done=done, base=base, qcol=qcol, wrow=wrow, eh=eh, hb=hb):
             done.synchronize()
             tj = time.perf_counter()
             offs = eh["offs"].numpy().view(np.uint64)
+            sizes = eh["sizes"].numpy().view(np.uint32)
+            data = eh["dst"].numpy()
             if int(offs[n]) > self.ent_dst_cap:
-                raise RuntimeError(f"HEVC GPU entropy: a step's slice data ({int(offs[n])} bytes) exceeds the host "
-                                   f"buffer ({self.ent_dst_cap}); encode with entropy='host'")
+                # the step's slice data outgrew the pinned buffer (the gather skipped it): read the
+                # substreams back from this host set's device area (dense content, low QPs)
+                cap = self.ent_cap
+                dev = self.ent_outs[hb].view(n, cap)
+                data = np.concatenate([dev[i, :int(sizes[i])].cpu().numpy() for i in range(n)]) if n else data
+                offs = np.zeros(n + 1, dtype=np.uint64)
+                offs[1:] = np.cumsum(sizes.astype(np.uint64))
+                self.stats["entropy_readback_steps"] = self.stats.get("entropy_readback_steps", 0) + 1
             fps = []
             for b in range(B):
                 fp = dict(base, qp=int(qcol[b]))
                 if wrow is not None and wrow[b] is not None:
                     fp["wp"] = wrow[b]
                 fps.append(fp)
-            r = self.host.hevc_assemble_slices(cfg, fps, eh["dst"].numpy(), offs, eh["sizes"].numpy().view(np.uint32),
-                                               eh["errs"].numpy(), self.entropy_threads)
+            r = self.host.hevc_assemble_slices(cfg, fps, data, offs, sizes, eh["errs"].numpy(), self.entropy_threads)
             cabac_s[0] += time.perf_counter() - tj
             return r
         return job

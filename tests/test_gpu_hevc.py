@@ -475,3 +475,22 @@ def test_gpu_hevc_entropy_matches_host_writer(host, kw):
     assert out["gpu"] == out["host"]
     for bs in out["gpu"]:
         assert len(host.hevc_decode(bs, False)) == F
+
+
+def test_gpu_hevc_entropy_4k_dense_matches_host_writer():
+    """4K at a low QP: 34 CTU rows over the coder's 8 waves (rows round-robin per wave), CTUs
+    with more non-zero 4x4 blocks than the per-CTU LDS stage holds (the rest read from the level
+    planes), and an I picture larger than the pinned output buffer (read back from the device
+    area instead) -- the GPU coder still gives the host writer's bytes."""
+    from govideocompressor_amd.models.h264_gpu import synth_clip
+    from govideocompressor_amd.models.hevc_gpu import GpuHevcEncoder, HevcParams
+    y, u, v = synth_clip(1, 3, 3840, 2160, seed=12, kind="noise")
+    out = {}
+    for ent in ("gpu", "host"):
+        enc = GpuHevcEncoder(HevcParams(width=3840, height=2160, crf=None, qp=14, lookahead=False), slots=1, entropy=ent)
+        out[ent] = enc.encode(y, u, v, metrics=False)[0].bitstream
+        if ent == "gpu":
+            assert enc.stats.get("entropy_readback_steps", 0) >= 1, enc.stats
+        enc.close()
+    assert len(out["gpu"]) > 1_000_000
+    assert out["gpu"] == out["host"]
