@@ -71,6 +71,8 @@ HEVC = {
     "MIVC_HEVC_BFRAMES": "bframes",
     "MIVC_HEVC_INTER8": "inter8",
     "MIVC_HEVC_INTER8_OVERHEAD": "inter8_overhead",
+    "MIVC_HEVC_TU_INTER_DEPTH": "tu_inter_depth",
+    "MIVC_HEVC_SDH": "sdh",
 }
 # bench.py shape knobs (they change what is measured, so they also need --allow-knobs)
 # (MIVC_HIP_LIB: an alternative kernel library, tools/build_variant.py -- same-box A/B timing)

@@ -113,6 +113,9 @@ HEVC_CONFIGS = {
     "ba_b3": dict(b_adapt=1, bframes=3),
     "ba_b3bias100": dict(b_adapt=1, bframes=3, b_bias=100),
     "ba_b4": dict(b_adapt=1, bframes=4),
+    # x265 medium's --tu-inter-depth 1 and --signhide, re-measured on the round-6 encoder
+    "tud1": dict(tu_inter_depth=1),
+    "sdh": dict(sdh=True),
 }
 
 
