@@ -347,9 +347,10 @@ class GpuHevcEncoder:
         # the host writer's coder) and only the slice headers, entry points and emulation
         # prevention stay on the host; "host": the native writer codes the records on
         # entropy_threads host threads (csrc/host/hevc_writer.cc)
-        # "auto": host threads when this process has cores for them (8+ usable cores and
-        # entropy threads) or when the batch is too narrow to fill the GPU's coder (fewer than
-        # 1024 substream waves: slots x min(16, CTU rows)), else the GPU.  One rank's share of an
+        # "auto": host threads when this process has cores for them (6+ usable cores and
+        # entropy threads: the writer codes a 1080p picture in ~2.5 ms per core, so 6 cores
+        # keep up with the GPU's ~2,450 pictures/s) or when the batch is too narrow to fill the
+        # GPU's coder (fewer than 1024 substream waves: slots x min(16, CTU rows)), else the GPU.  One rank's share of an
         # 8-GPU node (2 cores): config 4 (256 x 1080p) 731 fps on the host, 1846 on the GPU;
         # config 5 (10 x 8K) 27.0 on the host, 11.8 on the GPU.  The whole 1-GPU box: config 4
         # 2471 on the host, 1844 on the GPU (profiles/r6_hevc_gpu_entropy.md)
@@ -360,7 +361,7 @@ class GpuHevcEncoder:
             cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
             rows = -(-self.H // (64 if params.ctu64 else 32)) if params.wpp else 1
             wide = self.B * min(16, rows) >= 1024
-            self.entropy = "gpu" if (min(cores, self.entropy_threads) < 8 and wide) else "host"
+            self.entropy = "gpu" if (min(cores, self.entropy_threads) < 6 and wide) else "host"
         if self.entropy == "gpu":
             self._alloc_entropy()
         self.pool = cf.ThreadPoolExecutor(max_workers=1)
