@@ -341,6 +341,7 @@ enum CoderError : int {
   CE_QP_DELTA,
   CE_SDH_PARITY,
   CE_OVERFLOW,
+  CE_TIMEOUT,
   CE_COUNT
 };
 inline const char* coder_error_text(int e) {
@@ -358,6 +359,7 @@ inline const char* coder_error_text(int e) {
     case CE_QP_DELTA: return "HEVC: CuQpDeltaVal out of range";
     case CE_SDH_PARITY: return "HEVC: sign data hiding parity does not match the hidden sign";
     case CE_OVERFLOW: return "HEVC entropy: substream buffer overflow";
+    case CE_TIMEOUT: return "HEVC GPU entropy: wavefront progress timeout";
     default: return "HEVC slice coder error";
   }
 }

@@ -20,7 +20,8 @@ int mivc_launch_hevc_entropy(const void* pic, int B, const int* qp, const void* 
                              const unsigned long long* nzmap, const int16_t* cy, const int16_t* cb, const int16_t* cr,
                              uint8_t* state, long long state_bytes, uint8_t* out, unsigned cap, unsigned* sizes,
                              int* errs, unsigned long long* offs, unsigned long long* offs_host, uint8_t* dst,
-                             unsigned long long dst_cap, int* overflow, void* stream, unsigned long long* prof);
+                             unsigned long long dst_cap, int* overflow, void* stream, unsigned long long* prof,
+                             int* gprog, void* gctx);
 int mivc_launch_hevc_decode(const mivc::gpu::HevcDecParams* p, int stage, void* stream);
 void mivc_launch_synth(void* y, void* u, void* v, int width, int height, int slots, int frames, int frame0,
                        uint32_t seed, int bit_depth, int slot0, void* stream, int kind);
@@ -609,7 +610,7 @@ PYBIND11_MODULE(_hip, m) {
                            uintptr_t nzmap, uintptr_t cy, uintptr_t cb, uintptr_t cr, uintptr_t state,
                            long long state_bytes, uintptr_t out, unsigned cap, uintptr_t sizes, uintptr_t errs,
                            uintptr_t offs, uintptr_t offs_host, uintptr_t dst, unsigned long long dst_cap,
-                           uintptr_t overflow, uintptr_t stream, uintptr_t prof) {
+                           uintptr_t overflow, uintptr_t stream, uintptr_t prof, uintptr_t gprog, uintptr_t gctx) {
     const std::string ps = pic;
     if (ps.size() != sizeof(mivc::hevc::CoderPic)) throw std::invalid_argument("hevc_entropy: pic is not a CoderPic");
     if (!ctu || !cu || !nzmap || !cy || !cb || !cr || !state || !out || !sizes || !errs || !offs || !offs_host || !dst)
@@ -618,12 +619,13 @@ PYBIND11_MODULE(_hip, m) {
                                  P<unsigned long long>(nzmap), P<int16_t>(cy), P<int16_t>(cb), P<int16_t>(cr),
                                  P<uint8_t>(state), state_bytes, P<uint8_t>(out), cap, P<unsigned>(sizes), P<int>(errs),
                                  P<unsigned long long>(offs), P<unsigned long long>(offs_host), P<uint8_t>(dst), dst_cap,
-                                 P<int>(overflow), S(stream), P<unsigned long long>(prof)) != 0)
+                                 P<int>(overflow), S(stream), P<unsigned long long>(prof), P<int>(gprog),
+                                 P<void>(gctx)) != 0)
       throw std::invalid_argument("hevc_entropy: unsupported geometry (substreams <= 100, cap % 16, state size)");
   }, py::arg("pic"), py::arg("B"), py::arg("qp"), py::arg("ctu"), py::arg("cu"), py::arg("col"), py::arg("nzmap"),
      py::arg("cy"), py::arg("cb"), py::arg("cr"), py::arg("state"), py::arg("state_bytes"), py::arg("out"), py::arg("cap"),
      py::arg("sizes"), py::arg("errs"), py::arg("offs"), py::arg("offs_host"), py::arg("dst"), py::arg("dst_cap"),
-     py::arg("overflow"), py::arg("stream"), py::arg("prof") = 0);
+     py::arg("overflow"), py::arg("stream"), py::arg("prof") = 0, py::arg("gprog") = 0, py::arg("gctx") = 0);
   m.def("hevc_qp_fixup", [](int B, int W, int H, uintptr_t ctu, uintptr_t cu, uintptr_t qp, uintptr_t run, int wpp,
                             uintptr_t stream, int ctu64) {
     mivc_launch_hevc_qp_fixup(B, W, H, P<void>(ctu), P<void>(cu), P<int>(qp), P<int8_t>(run), wpp, S(stream), ctu64);

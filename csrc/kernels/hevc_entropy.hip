@@ -74,6 +74,12 @@ struct HevcEntropyArgs {
   int* errs;                   // [B][nsub] CoderError
   int nsub;
   unsigned long long* prof;    // diagnostics: [B][16 waves][CP_N + 2] cycle counters, or null
+  // workgroups per picture: 1 = the rows advance in barrier-separated rounds inside one
+  // workgroup; K > 1 (narrow batches: few pictures, many CTU rows) = the picture's rows are
+  // dealt to K x waves waves, which hand progress and row contexts over through device memory
+  int K;
+  int* gprog;                  // [B][nsub] CTUs coded per row (K > 1; zeroed by the launcher)
+  CtxState* gctx;              // [B][nsub][kNumCtx] contexts after each row's CTU 1 (K > 1)
 };
 
 __host__ __device__ inline long long entropy_state_bytes(int W, int H) {
@@ -96,6 +102,7 @@ __device__ inline CoderState entropy_state(uint8_t* base, int W, int H) {
 
 constexpr int kStageBlocks = 128;  // 4x4 level blocks staged per CTU and wave (4 KiB)
 
+template <bool kMulti>
 __global__ __launch_bounds__(1024) void hevc_entropy(HevcEntropyArgs a) {
   extern __shared__ CtxState s_ctx[];  // [2][nsub][kNumCtx]: working contexts, saved after CTU 1
   __shared__ CoderPic sP;
@@ -104,7 +111,10 @@ __global__ __launch_bounds__(1024) void hevc_entropy(HevcEntropyArgs a) {
   __shared__ uint32_t s_step[256];
   __shared__ uint8_t s_scans[sizeof(hevc::kScans.t)];
   __shared__ uint8_t s_sig[sizeof(hevc::kSig.t)];
-  const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  // workgroup kk of picture b is blockIdx kk * B + b: with B a multiple of 8 a picture's
+  // workgroups share an XCD (blockIdx mod 8)
+  const int B = gridDim.x / a.K;
+  const int kk = blockIdx.x / B, b = blockIdx.x - kk * B, tid = threadIdx.x, nt = blockDim.x;
   const int wave = tid >> 6, nwave = nt >> 6;
   const bool lead = (tid & 63) == 0;
   const int W = a.pic.W, H = a.pic.H, nctb = a.pic.wctb * a.pic.hctb;
@@ -119,7 +129,8 @@ __global__ __launch_bounds__(1024) void hevc_entropy(HevcEntropyArgs a) {
   uint8_t* st = a.state + static_cast<size_t>(b) * a.state_bytes;
   const CoderState cs = entropy_state(st, W, H);
   const long long n8 = static_cast<long long>(W / 8) * (H / 8);
-  for (long long i = tid; i < n8; i += nt) cs.coded[i] = 0;
+  if (!kMulti)  // K > 1: the launcher zeroed the state (every workgroup of the picture reads it)
+    for (long long i = tid; i < n8; i += nt) cs.coded[i] = 0;
   __syncthreads();
   CoderLevels lv;
   lv.nzmap = reinterpret_cast<const uint64_t*>(a.nzmap) + static_cast<size_t>(b) * nctb * 2;
@@ -200,6 +211,62 @@ __global__ __launch_bounds__(1024) void hevc_entropy(HevcEntropyArgs a) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
+  if constexpr (kMulti) {
+    // each wave on its own: wait (device scope) until the row above has coded the above-right
+    // CTU, code, publish; row contexts after CTU 1 go through device memory
+    const int TW = a.K * nwave;
+    int* prog = a.gprog + static_cast<size_t>(b) * a.nsub;
+    CtxState* gctx = a.gctx + static_cast<size_t>(b) * a.nsub * hevc::kNumCtx;
+    CtxState* ctx = s_ctx + static_cast<size_t>(wave) * hevc::kNumCtx;
+    for (int r = kk * nwave + wave; r < a.nsub; r += TW) {
+      if (lead) {
+        sink = DevSink{a.out + (static_cast<size_t>(b) * a.nsub + r) * a.cap, a.cap, 0, 0, 0};
+        w.begin(&sP, ctu, cu, col, lv, cs, ctx, &sink, s_step, s_scans, s_sig);
+      }
+      bool timeout = false;
+      for (int x = 0; x < wctu && !timeout; ++x) {
+        if (r > 0) {
+          const int target = min(x + 2, wctu);
+          int spins = 0;
+          while (__hip_atomic_load(prog + r - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1 << 24)) {
+              timeout = true;
+              break;
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          if (timeout) break;
+        }
+        stage(x, r);
+        if (lead) {
+          if (x == 0 && r > 0 && wctu >= 2)  // sync from CTU (1, r - 1)
+            for (int i = 0; i < hevc::kNumCtx; ++i) ctx[i] = gctx[static_cast<size_t>(r - 1) * hevc::kNumCtx + i];
+          w.lv.levels = &s_lv[wave][0];
+          w.lv.nblocks = kStageBlocks;
+          w.cu_stage = &s_cu[wave][0];
+          w.stage_cx = x;
+          w.stage_cy = r;
+          w.prof = nullptr;
+          w.code_ctu(x, r);
+          if (x == 1)
+            for (int i = 0; i < hevc::kNumCtx; ++i) gctx[static_cast<size_t>(r) * hevc::kNumCtx + i] = ctx[i];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (lead) __hip_atomic_store(prog + r, x + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_wave_barrier();  // lane 0 is done with the staging area
+      }
+      if (lead) {
+        const size_t o = static_cast<size_t>(b) * a.nsub + r;
+        a.sizes[o] = sink.n;
+        a.errs[o] = timeout ? static_cast<int>(hevc::CE_TIMEOUT)
+                            : (w.err ? w.err : (sink.n > a.cap ? static_cast<int>(hevc::CE_OVERFLOW) : 0));
+        if (timeout)  // let the rows below finish (their bytes are discarded with this error)
+          __hip_atomic_store(prog + r, wctu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    return;
+  }
   __shared__ uint64_t s_prof[16][hevc::CP_N + 2];  // + cycles waiting at barriers, + CTUs coded
   if (a.prof && lead) {
     for (int k = 0; k < hevc::CP_N + 2; ++k) s_prof[wave][k] = 0;
@@ -318,7 +385,7 @@ extern "C" int mivc_launch_hevc_entropy(const void* pic, int B, const int* qp, c
                                         uint8_t* out, unsigned cap, unsigned* sizes, int* errs,
                                         unsigned long long* offs, unsigned long long* offs_host, uint8_t* dst,
                                         unsigned long long dst_cap, int* overflow, void* stream,
-                                        unsigned long long* prof) {
+                                        unsigned long long* prof, int* gprog, void* gctx) {
   HevcEntropyArgs a{};
   a.prof = prof;
   a.pic = *static_cast<const CoderPic*>(pic);
@@ -350,10 +417,31 @@ extern "C" int mivc_launch_hevc_entropy(const void* pic, int B, const int* qp, c
     const int v = e ? std::atoi(e) : 8;
     return v < 1 ? 1 : (v > 16 ? 16 : v);
   }();
-  const int lanes = 64 * (nsub < max_waves ? nsub : max_waves);
+  const int nw = nsub < max_waves ? nsub : max_waves;
+  const int lanes = 64 * nw;
+  // narrow batches (fewer than 512 substream waves, e.g. 10 x 8K) spread each picture's rows
+  // over up to 8 workgroups; MIVC_HEVC_ENTROPY_WG forces K (tests)
+  static const int wg_env = [] {
+    const char* e = std::getenv("MIVC_HEVC_ENTROPY_WG");
+    return e ? std::atoi(e) : 0;
+  }();
+  int K = 1;
+  if (a.pic.wpp && gprog && gctx) {
+    const int need = (nsub + nw - 1) / nw;
+    K = wg_env > 0 ? wg_env : (B * nw < 512 ? need : 1);
+    K = K < 1 ? 1 : (K > 8 ? 8 : (K > need ? need : K));
+  }
+  a.K = K;
+  a.gprog = gprog;
+  a.gctx = static_cast<CtxState*>(gctx);
   const size_t lds = static_cast<size_t>(2) * nsub * mivc::hevc::kNumCtx * sizeof(CtxState);  // <= 60 KB
   hipStream_t s = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(hevc_entropy, dim3(B), dim3(lanes), lds, s, a);
+  if (K > 1) {
+    (void)hipMemsetAsync(gprog, 0, static_cast<size_t>(B) * nsub * sizeof(int), s);
+    (void)hipMemsetAsync(state, 0, static_cast<size_t>(B) * state_bytes, s);
+  }
+  if (K > 1) hipLaunchKernelGGL(hevc_entropy<true>, dim3(B * K), dim3(lanes), lds, s, a);
+  else hipLaunchKernelGGL(hevc_entropy<false>, dim3(B), dim3(lanes), lds, s, a);
   const int n = B * nsub;
   hipLaunchKernelGGL(hevc_entropy_scan, dim3(1), dim3(1024), 0, s, n, sizes, cap, offs, offs_host, dst_cap, overflow);
   hipLaunchKernelGGL(hevc_entropy_gather, dim3(n), dim3(256), 0, s, out, cap, sizes, offs, n, dst, overflow);

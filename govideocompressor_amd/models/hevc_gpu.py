@@ -349,19 +349,17 @@ class GpuHevcEncoder:
         # entropy_threads host threads (csrc/host/hevc_writer.cc)
         # "auto": host threads when this process has cores for them (6+ usable cores and
         # entropy threads: the writer codes a 1080p picture in ~2.5 ms per core, so 6 cores
-        # keep up with the GPU's ~2,450 pictures/s) or when the batch is too narrow to fill the
-        # GPU's coder (fewer than 1024 substream waves: slots x min(16, CTU rows)), else the GPU.  One rank's share of an
-        # 8-GPU node (2 cores): config 4 (256 x 1080p) 731 fps on the host, 1846 on the GPU;
-        # config 5 (10 x 8K) 27.0 on the host, 11.8 on the GPU.  The whole 1-GPU box: config 4
-        # 2471 on the host, 1844 on the GPU (profiles/r6_hevc_gpu_entropy.md)
+        # keep up with the GPU's ~2,450 pictures/s), else the GPU.  One rank's share of an
+        # 8-GPU node (2 cores): config 4 (256 x 1080p) 731 fps on the host, 2051 on the GPU;
+        # config 5 (10 x 8K, a picture's rows spread over 8 workgroups) 27.0 on the host, 36.6
+        # on the GPU.  The whole 1-GPU box: config 4 2452 on the host, 2062 on the GPU
+        # (profiles/r6_hevc_gpu_entropy.md)
         self.entropy = (entropy or os.environ.get("MIVC_HEVC_ENTROPY", "auto")).lower()
         if self.entropy not in ("gpu", "host", "auto"):
             raise ValueError("entropy must be 'gpu', 'host' or 'auto'")
         if self.entropy == "auto":
             cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-            rows = -(-self.H // (64 if params.ctu64 else 32)) if params.wpp else 1
-            wide = self.B * min(16, rows) >= 1024
-            self.entropy = "gpu" if (min(cores, self.entropy_threads) < 6 and wide) else "host"
+            self.entropy = "gpu" if min(cores, self.entropy_threads) < 6 else "host"
         if self.entropy == "gpu":
             self._alloc_entropy()
         self.pool = cf.ThreadPoolExecutor(max_workers=1)
@@ -422,6 +420,10 @@ class GpuHevcEncoder:
         self.ent_errs = torch.zeros((n,), dtype=torch.int32, device=dev)
         self.ent_offs = torch.zeros((n + 1,), dtype=torch.int64, device=dev)
         self.ent_over = torch.zeros((1,), dtype=torch.int32, device=dev)
+        # narrow batches spread a picture over several workgroups (kernels/hevc_entropy.hip):
+        # row progress and the row contexts after CTU 1 then go through device memory
+        self.ent_gprog = torch.zeros((n,), dtype=torch.int32, device=dev)
+        self.ent_gctx = torch.zeros((n * 151 * 2,), dtype=torch.uint8, device=dev)  # kNumCtx CtxStates per row
         # pinned output per host set: half a byte per luma sample of every picture of a step
         self.ent_dst_cap = max(1 << 22, B * W * H // 2)
         self.ent_host = None
@@ -1197,7 +1199,7 @@ class GpuHevcEncoder:
                                   p(self.coef[1]), p(self.coef[2]), p(self.ent_state), self.ent_state_bytes,
                                   p(self.ent_outs[hb]), self.ent_cap, p(self.ent_sizes), p(self.ent_errs), p(self.ent_offs),
                                   eh["offs"].data_ptr(), eh["dst"].data_ptr(), self.ent_dst_cap, p(self.ent_over), sc,
-                                  self._entropy_prof(pic.kind))
+                                  self._entropy_prof(pic.kind), p(self.ent_gprog), p(self.ent_gctx))
             # the batch's QP table is freed when the encode returns: keep its block from being
             # reused (by the compute stream's next batch) before this stream has read it
             qp_row.record_stream(cs)

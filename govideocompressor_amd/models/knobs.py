@@ -79,7 +79,7 @@ HEVC = {
 BENCH = {"MIVC_BENCH_SLOTS", "MIVC_BENCH_FRAMES", "MIVC_BENCH_BFRAMES", "MIVC_HIP_LIB"}
 # never change the coded bytes (see the module docstring)
 RUNTIME = {
-    "MIVC_ENTROPY_THREADS", "MIVC_HEVC_ENTROPY", "MIVC_HEVC_ENTROPY_PROF", "MIVC_HEVC_ENTROPY_WAVES", "MIVC_PINNED_BUDGET_MB", "MIVC_CABAC_GROUP", "MIVC_CABAC_SYMS_PER_MB",
+    "MIVC_ENTROPY_THREADS", "MIVC_HEVC_ENTROPY", "MIVC_HEVC_ENTROPY_PROF", "MIVC_HEVC_ENTROPY_WAVES", "MIVC_HEVC_ENTROPY_WG", "MIVC_PINNED_BUDGET_MB", "MIVC_CABAC_GROUP", "MIVC_CABAC_SYMS_PER_MB",
     "MIVC_CABAC_HOST_MB", "MIVC_CABAC_PEAK_SYMS_PER_MB", "MIVC_INTRA_WAVES", "MIVC_INTRA_WG", "MIVC_HEVC_SAO_TILE", "MIVC_STAGE_TIMING", "MIVC_LOG_JSON", "MIVC_DIST_BACKEND",
     "MIVC_DIST_FORCE", "MIVC_HOST_LIB", "MIVC_NO_AUTOBUILD", "MIVC_GPU_ARCH", "MIVC_TRANSPORT", "MIVC_FAULT",
     "MIVC_WORKER_ID", "MIVC_TRANSCODE_GROUP", "MIVC_SRC_ROOT", "MIVC_OUT_ROOT", "MIVC_FLEET_STATE",
