@@ -214,11 +214,15 @@ __global__ __launch_bounds__(1024) void hevc_entropy(HevcEntropyArgs a) {
   if constexpr (kMulti) {
     // each wave on its own: wait (device scope) until the row above has coded the above-right
     // CTU, code, publish; row contexts after CTU 1 go through device memory
-    const int TW = a.K * nwave;
+    // workgroup kk codes the contiguous rows [kk R, (kk + 1) R), its waves round-robin: every
+    // row waits only on rows of its own workgroup or of workgroup kk - 1 (a lower blockIdx,
+    // dispatched first), so progress never depends on a workgroup that is not yet resident
+    const int R = (a.nsub + a.K - 1) / a.K;
+    const int r_end = min(a.nsub, (kk + 1) * R);
     int* prog = a.gprog + static_cast<size_t>(b) * a.nsub;
     CtxState* gctx = a.gctx + static_cast<size_t>(b) * a.nsub * hevc::kNumCtx;
     CtxState* ctx = s_ctx + static_cast<size_t>(wave) * hevc::kNumCtx;
-    for (int r = kk * nwave + wave; r < a.nsub; r += TW) {
+    for (int r = kk * R + wave; r < r_end; r += nwave) {
       if (lead) {
         sink = DevSink{a.out + (static_cast<size_t>(b) * a.nsub + r) * a.cap, a.cap, 0, 0, 0};
         w.begin(&sP, ctu, cu, col, lv, cs, ctx, &sink, s_step, s_scans, s_sig);
@@ -420,16 +424,20 @@ extern "C" int mivc_launch_hevc_entropy(const void* pic, int B, const int* qp, c
   const int nw = nsub < max_waves ? nsub : max_waves;
   const int lanes = 64 * nw;
   // narrow batches (fewer than 512 substream waves, e.g. 10 x 8K) spread each picture's rows
-  // over up to 8 workgroups; MIVC_HEVC_ENTROPY_WG forces K (tests)
+  // over ceil(rows / waves) workgroups (contiguous row blocks); MIVC_HEVC_ENTROPY_WG forces K
   static const int wg_env = [] {
     const char* e = std::getenv("MIVC_HEVC_ENTROPY_WG");
     return e ? std::atoi(e) : 0;
   }();
   int K = 1;
   if (a.pic.wpp && gprog && gctx) {
+    // K workgroups per picture while the launch stays at most 1024 waves (a quarter of the
+    // device's resident waves at this kernel's registers: room for the concurrent compute)
+    // and at most nw rows per workgroup (a wave per row: a second row of a wave would wait for
+    // its first to finish and delay every row below it)
     const int need = (nsub + nw - 1) / nw;
-    K = wg_env > 0 ? wg_env : (B * nw < 512 ? need : 1);
-    K = K < 1 ? 1 : (K > 8 ? 8 : (K > need ? need : K));
+    K = wg_env > 0 ? wg_env : (B * nw < 512 && B * need * nw <= 1024 ? need : 1);
+    K = K < 1 ? 1 : (K > 16 ? 16 : (K > need ? need : K));
   }
   a.K = K;
   a.gprog = gprog;
