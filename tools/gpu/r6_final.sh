@@ -3,7 +3,7 @@
 # (auto entropy = host on the whole box), config 4 at one rank's share (auto = GPU entropy)
 set -o pipefail
 export TMPDIR=/tmp
-out=gpurun_out/r6y
+out=${1:-gpurun_out/r6y}
 mkdir -p $out
 CORES=$(python3 -c "import os; print(','.join(map(str, sorted(os.sched_getaffinity(0))[:2])))")
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $out/tests.txt 2>&1 || exit $?
