@@ -95,6 +95,15 @@ class EncoderConfig:
         bad = sorted(k for k in over if k not in fields)
         if bad:
             raise FfArgsError(f"{type(params).__name__} has no knob(s) {', '.join(bad)}")
+        if "direct" in fields:  # H.264: b-pyramid needs spatial direct prediction here
+            if over.get("pyramid") and over.get("direct", "spatial") != "spatial":
+                raise FfArgsError("b-pyramid needs direct=spatial with this encoder")
+            if over.get("pyramid") and "direct" not in over:
+                over.update(direct="spatial", spatial_wavefront=True)
+            res = dataclasses.replace(params, **over)
+            if res.pyramid and res.direct != "spatial":  # a preset's pyramid under direct=temporal
+                res = dataclasses.replace(res, pyramid=False)
+            return res
         return dataclasses.replace(params, **over)
 
 
@@ -196,7 +205,9 @@ H264_PARAMS = {
     # and ~26 % fewer frames/s than temporal on the benchmark content (profiles/r3_direct_rd.md)
     "direct": ("direct", _only("temporal", "spatial")),
     "b-adapt": ("@b-adapt", _only("0")),
-    "b-pyramid": ("@b-pyramid", _only("none")),
+    # b-pyramid=normal: the middle B of a run is a reference; this encoder needs spatial direct
+    # for it (decided in the MB wavefront), so it implies direct=spatial (apply_opts)
+    "b-pyramid": ("pyramid", lambda v: _only("none", "normal")(v) == "normal"),
     "crf": ("@crf", _float_in(0.0, 51.0)),
     "qp": ("@qp", _int_in(0, 51)),
     "threads": ("@threads", int),

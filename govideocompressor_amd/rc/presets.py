@@ -20,8 +20,8 @@ medium      defaults (x264 defaults, the reference's "264" preset: --ref 3, weig
             4 skip-refine passes)
 slow        radius 12, B radius 6, Intra4x4 in P pictures, 4 references, 5 skip-refine passes,
             adaptive B placement (--me umh --subme 8 --ref 5 --b-adapt 1)
-slower      radius 16, B radius 8, lookahead radius 8, 4 references, spatial direct, 6
-            skip-refine passes (--subme 9 --me umh --ref 8 --direct spatial)
+slower      radius 16, B radius 8, lookahead radius 8, 4 references, spatial direct, b-pyramid,
+            6 skip-refine passes (--subme 9 --me umh --ref 8 --direct spatial --b-pyramid normal)
 veryslow    slower + 8 skip-refine passes (--subme 10 --me umh --merange 24 --ref 16)
 placebo     = veryslow
 ==========  ========================================================================
@@ -56,12 +56,15 @@ H264 = {
     # ~-0.7 % BD-rate and ~-0.65 % fps at the headline (profiles/r4_knob_sweep.md)
     # slow also places its B pictures adaptively (x264 --b-adapt 1 at --b-bias 100 on weighted
     # lowres costs, one pattern per batch): -1.85 % BD-rate on the content suite for -3.2 % fps
-    # at the headline (profiles/r5_badapt_rd.md) -- medium keeps the fixed pattern's throughput
+    # at the headline (profiles/r5_badapt_rd.md) -- medium keeps the fixed pattern's throughput.
+    # slower and up also keep the middle B of a run as a reference (x264 --b-pyramid normal):
+    # wavefront spatial direct + pyramid -3.37 % BD-rate against medium's temporal direct, vs
+    # -2.95 % without the pyramid (profiles/r6_spatial_direct_rd.md)
     "slow": dict(me_range=12, b_me_range=6, i4x4_in_p=True, refs=4, b_gate=1200, skip_refine=5, b_adapt=1, b_bias=100),
     "slower": dict(me_range=16, b_me_range=8, i4x4_in_p=True, la_range=8, skip_refine=6, refs=4, direct="spatial",
-                   spatial_wavefront=True, b_gate=1200),
+                   spatial_wavefront=True, pyramid=True, b_gate=1200),
     "veryslow": dict(me_range=16, b_me_range=8, i4x4_in_p=True, la_range=8, skip_refine=8, refs=4, direct="spatial",
-                     spatial_wavefront=True, b_gate=1200),
+                     spatial_wavefront=True, pyramid=True, b_gate=1200),
 }
 H264["placebo"] = H264["veryslow"]
 

@@ -169,7 +169,7 @@ def test_ffargs_strict_rejections():
     for bad in ("-vcodec libx264 -tune film", "-vcodec libx264 -tune ssim", "-vcodec libx264 -profile:v high10",
                 "-vcodec libx264 -profile:v high444", "-vcodec libx265 -profile:v main12",
                 "-vcodec libx264 -x264-params ref=5", "-vcodec libx264 -x264-params direct=auto",
-                "-vcodec libx264 -x264-params b-adapt=2", "-vcodec libx264 -x264-params b-pyramid=normal",
+                "-vcodec libx264 -x264-params b-adapt=2", "-vcodec libx264 -x264-params b-pyramid=strict",
                 "-vcodec libx264 -x264-params foo=1", "-vcodec libx264 -x265-params sao=0",
                 "-vcodec libx265 -x265-params bframes=9", "-vcodec libx265 -x265-params ctu=16",
                 "-vcodec libx264 -x264-params aq-mode=2", "-vcodec libx264 -x264-params deblock=1,1",
@@ -192,6 +192,15 @@ def test_ffargs_reference_and_weighting_knobs():
     p = ffargs.parse("-vcodec libx264 -x264-params direct=spatial").apply_opts(H264Params(64, 64))
     assert p.direct == "spatial"
     assert presets.apply(H264Params(64, 64), "slower").direct == "spatial"
+    # x264 --b-pyramid normal: slower and up, or asked for (implies spatial direct here)
+    sl = presets.apply(H264Params(64, 64), "slower")
+    assert sl.pyramid and sl.spatial_wavefront and not presets.apply(H264Params(64, 64), "medium").pyramid
+    p = ffargs.parse("-vcodec libx264 -x264-params b-pyramid=normal").apply_opts(H264Params(64, 64))
+    assert (p.pyramid, p.direct, p.spatial_wavefront) == (True, "spatial", True)
+    p = ffargs.parse("-vcodec libx264 -x264-params direct=temporal").apply_opts(sl)
+    assert (p.pyramid, p.direct) == (False, "temporal")
+    with pytest.raises(ffargs.FfArgsError):
+        ffargs.parse("-vcodec libx264 -x264-params b-pyramid=normal:direct=temporal").apply_opts(H264Params(64, 64))
     assert presets.apply(H264Params(64, 64), "medium").direct == "temporal"
     assert H264Params(64, 64, cabac=False, refs=3).eff_refs() == 1     # Constrained Baseline: one reference
     assert presets.apply(H264Params(64, 64), "ultrafast").refs == 1
