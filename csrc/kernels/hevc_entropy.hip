@@ -102,9 +102,14 @@ __device__ inline CoderState entropy_state(uint8_t* base, int W, int H) {
 
 constexpr int kStageBlocks = 128;  // 4x4 level blocks staged per CTU and wave (4 KiB)
 
-template <bool kMulti>
+// kMW: the most waves a launch uses (8 or 16); it sizes the per-wave LDS, so the default
+// 8-wave launch leaves more of a CU's LDS to the concurrent compute stream's kernels.
+// __launch_bounds__(1024) either way: the 128-VGPR budget measured best
+template <bool kMulti, int kMW>
 __global__ __launch_bounds__(1024) void hevc_entropy(HevcEntropyArgs a) {
-  extern __shared__ CtxState s_ctx[];  // [2][nsub][kNumCtx]: working contexts, saved after CTU 1
+  // working contexts per wave [nwave][kNumCtx], then (one workgroup per picture) the contexts
+  // of each row after its CTU 1 [nsub][kNumCtx]
+  extern __shared__ CtxState s_ctx[];
   __shared__ CoderPic sP;
   __shared__ int s_prog[128];          // CTUs coded per row
   // the coder's constant tables in LDS (read once or more per bin / coefficient)
@@ -149,15 +154,15 @@ __global__ __launch_bounds__(1024) void hevc_entropy(HevcEntropyArgs a) {
   int row = wave;
   // each wave's coder and sink in LDS: their fields are read and written around every bin, and
   // the out-of-line calls would otherwise keep them in scratch memory
-  __shared__ __attribute__((aligned(16))) unsigned char s_coder[16][sizeof(CtuCoder<DevSink>)];
-  __shared__ DevSink s_sink[16];
-  __shared__ __attribute__((aligned(16))) int16_t s_lv[16][kStageBlocks * 16];
-  __shared__ CuInfo s_cu[16][4 * hevc::kCusPerCtb];
+  __shared__ __attribute__((aligned(16))) unsigned char s_coder[kMW][sizeof(CtuCoder<DevSink>)];
+  __shared__ DevSink s_sink[kMW];
+  __shared__ __attribute__((aligned(16))) int16_t s_lv[kMW][kStageBlocks * 16];
+  __shared__ CuInfo s_cu[kMW][4 * hevc::kCusPerCtb];
   CtuCoder<DevSink>& w = *reinterpret_cast<CtuCoder<DevSink>*>(s_coder[wave]);
   DevSink& sink = s_sink[wave];
   auto start_row = [&](int r) {
     sink = DevSink{a.out + (static_cast<size_t>(b) * a.nsub + r) * a.cap, a.cap, 0, 0, 0};
-    w.begin(&sP, ctu, cu, col, lv, cs, s_ctx + static_cast<size_t>(r) * hevc::kNumCtx, &sink, s_step, s_scans, s_sig);
+    w.begin(&sP, ctu, cu, col, lv, cs, s_ctx + static_cast<size_t>(wave) * hevc::kNumCtx, &sink, s_step, s_scans, s_sig);
   };
   auto end_row = [&](int r) {
     const size_t o = static_cast<size_t>(b) * a.nsub + r;
@@ -271,7 +276,7 @@ __global__ __launch_bounds__(1024) void hevc_entropy(HevcEntropyArgs a) {
     }
     return;
   }
-  __shared__ uint64_t s_prof[16][hevc::CP_N + 2];  // + cycles waiting at barriers, + CTUs coded
+  __shared__ uint64_t s_prof[kMW][hevc::CP_N + 2];  // + cycles waiting at barriers, + CTUs coded
   if (a.prof && lead) {
     for (int k = 0; k < hevc::CP_N + 2; ++k) s_prof[wave][k] = 0;
   }
@@ -293,9 +298,9 @@ __global__ __launch_bounds__(1024) void hevc_entropy(HevcEntropyArgs a) {
     if (ready) {
       stage(x, row);
       if (lead) {
-        CtxState* ctx = s_ctx + static_cast<size_t>(row) * hevc::kNumCtx;
+        CtxState* ctx = s_ctx + static_cast<size_t>(wave) * hevc::kNumCtx;
         if (x == 0 && row > 0 && wctu >= 2) {  // sync from CTU (1, row - 1)
-          const CtxState* src = s_ctx + static_cast<size_t>(a.nsub + row - 1) * hevc::kNumCtx;
+          const CtxState* src = s_ctx + static_cast<size_t>(nwave + row - 1) * hevc::kNumCtx;
           for (int i = 0; i < hevc::kNumCtx; ++i) ctx[i] = src[i];
         }
         w.lv.levels = &s_lv[wave][0];
@@ -307,7 +312,7 @@ __global__ __launch_bounds__(1024) void hevc_entropy(HevcEntropyArgs a) {
         w.code_ctu(x, row);
         if (a.prof) s_prof[wave][hevc::CP_N + 1] += 1;
         if (x == 1) {
-          CtxState* sv = s_ctx + static_cast<size_t>(a.nsub + row) * hevc::kNumCtx;
+          CtxState* sv = s_ctx + static_cast<size_t>(nwave + row) * hevc::kNumCtx;
           for (int i = 0; i < hevc::kNumCtx; ++i) sv[i] = ctx[i];
         }
         s_prog[row] = x + 1;
@@ -442,14 +447,20 @@ extern "C" int mivc_launch_hevc_entropy(const void* pic, int B, const int* qp, c
   a.K = K;
   a.gprog = gprog;
   a.gctx = static_cast<CtxState*>(gctx);
-  const size_t lds = static_cast<size_t>(2) * nsub * mivc::hevc::kNumCtx * sizeof(CtxState);  // <= 60 KB
+  // working contexts per wave, plus (K == 1) each row's contexts after CTU 1: <= 35 KB
+  const size_t lds = static_cast<size_t>(K > 1 ? nw : nw + nsub) * mivc::hevc::kNumCtx * sizeof(CtxState);
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (K > 1) {
     (void)hipMemsetAsync(gprog, 0, static_cast<size_t>(B) * nsub * sizeof(int), s);
     (void)hipMemsetAsync(state, 0, static_cast<size_t>(B) * state_bytes, s);
   }
-  if (K > 1) hipLaunchKernelGGL(hevc_entropy<true>, dim3(B * K), dim3(lanes), lds, s, a);
-  else hipLaunchKernelGGL(hevc_entropy<false>, dim3(B), dim3(lanes), lds, s, a);
+  if (K > 1) {
+    if (nw <= 8) hipLaunchKernelGGL((hevc_entropy<true, 8>), dim3(B * K), dim3(lanes), lds, s, a);
+    else hipLaunchKernelGGL((hevc_entropy<true, 16>), dim3(B * K), dim3(lanes), lds, s, a);
+  } else {
+    if (nw <= 8) hipLaunchKernelGGL((hevc_entropy<false, 8>), dim3(B), dim3(lanes), lds, s, a);
+    else hipLaunchKernelGGL((hevc_entropy<false, 16>), dim3(B), dim3(lanes), lds, s, a);
+  }
   const int n = B * nsub;
   hipLaunchKernelGGL(hevc_entropy_scan, dim3(1), dim3(1024), 0, s, n, sizes, cap, offs, offs_host, dst_cap, overflow);
   hipLaunchKernelGGL(hevc_entropy_gather, dim3(n), dim3(256), 0, s, out, cap, sizes, offs, n, dst, overflow);
