@@ -36,6 +36,24 @@ struct RenormTable {
 };
 constexpr RenormTable kRenorm{};
 
+// scan orders (6.5.3-6.5.5) of every (scanIdx, log2 size 0..3) as position tables, and their
+// inverse (raster position -> scan index): residual_coding looks positions up instead of
+// walking the diagonal per coefficient (scan_pos is O(p))
+struct ScanTables {
+  uint8_t x[3][4][64], y[3][4][64], inv[3][4][64];
+  ScanTables() : x(), y(), inv() {
+    for (int s = 0; s < 3; ++s)
+      for (int l = 0; l < 4; ++l)
+        for (int p = 0; p < (1 << (2 * l)); ++p) {
+          const int v = scan_pos(s, l, p);
+          x[s][l][p] = static_cast<uint8_t>(v & 255);
+          y[s][l][p] = static_cast<uint8_t>(v >> 8);
+          inv[s][l][((v >> 8) << l) + (v & 255)] = static_cast<uint8_t>(p);
+        }
+  }
+};
+const ScanTables kScan;
+
 // CABAC arithmetic decoding engine (9.3.4.3), byte-refilled: `value` holds the 9-bit
 // offset scaled by 2^7 plus look-ahead bits.  After a terminating bin equal to 1 the
 // next byte-aligned syntax (PCM samples, the next substream) starts at `p`.
@@ -1720,26 +1738,10 @@ struct HevcStreamDecoder::Impl {
     if (lx >= n || ly >= n) fail("last significant position outside the block");
     if (scan == 2) std::swap(lx, ly);
     const int log2sb = log2 - 2, nsb = 1 << log2sb;
-    int sbx[64], sby[64], px[16], py[16];
-    for (int i = 0; i < nsb * nsb; ++i) {
-      const int p = scan_pos(scan, log2sb, i);
-      sbx[i] = p & 255;
-      sby[i] = p >> 8;
-    }
-    for (int i = 0; i < 16; ++i) {
-      const int p = scan_pos(scan, 2, i);
-      px[i] = p & 255;
-      py[i] = p >> 8;
-    }
-    int last_sb = -1, last_pos = -1;
-    for (int i = nsb * nsb - 1; i >= 0 && last_sb < 0; --i)
-      if (sbx[i] == (lx >> 2) && sby[i] == (ly >> 2))
-        for (int p = 0; p < 16; ++p)
-          if (px[p] == (lx & 3) && py[p] == (ly & 3)) {
-            last_sb = i;
-            last_pos = p;
-          }
-    if (last_sb < 0) fail("last position not in the scan");
+    const uint8_t *sbx = kScan.x[scan][log2sb], *sby = kScan.y[scan][log2sb];
+    const uint8_t *px = kScan.x[scan][2], *py = kScan.y[scan][2];
+    const int last_sb = kScan.inv[scan][log2sb][((ly >> 2) << log2sb) + (lx >> 2)];
+    const int last_pos = kScan.inv[scan][2][((ly & 3) << 2) + (lx & 3)];
     uint8_t csbf[8][8] = {};
     int g1ctx_prev = 1;
     bool first_sb = true;
@@ -2162,13 +2164,12 @@ struct HevcStreamDecoder::Impl {
     d.slice_qp = pps->init_qp + slices[0].qp_delta;
     if (opt.gpu_records) {
       d.bs = bsv;
-      const size_t n4 = static_cast<size_t>(w4) * h4;
-      std::vector<DecMv4> m4(n4);
-      for (size_t k = 0; k < n4; ++k) {
-        DecMv4& m = m4[k];
+      std::vector<int> ref_base(2 * slices.size());  // slice_ref_base of every (slice, list)
+      for (size_t s = 0; s < slices.size(); ++s)
+        for (int l = 0; l < 2; ++l) ref_base[2 * s + l] = slice_ref_base(static_cast<int>(s), l);
+      // the GPU record of 4x4 block k (slice segment sidx)
+      auto rec4 = [&](size_t k, int sidx, DecMv4& m) {
         const MvField& f = cur->mvf[k];
-        const int x = static_cast<int>(k % w4) * 4, y = static_cast<int>(k / w4) * 4;
-        const int sidx = ctb_slice[(y >> log2_ctb) * wctb + (x >> log2_ctb)];
         m.qp = qp_y[k];
         m.flags = 0;
         if (cu_flags[k] & CF_INTRA) m.flags |= DM_INTRA;
@@ -2178,7 +2179,7 @@ struct HevcStreamDecoder::Impl {
           m.flags |= DM_INTER;
           for (int l = 0; l < 2; ++l)
             if (f.pred & (1 << l)) {
-              m.ref[l] = static_cast<uint8_t>(slice_ref_base(sidx, l) + f.ref[l]);
+              m.ref[l] = static_cast<uint8_t>(ref_base[2 * sidx + l] + f.ref[l]);
               m.mv[l][0] = f.mv[l][0];
               m.mv[l][1] = f.mv[l][1];
             } else {
@@ -2187,26 +2188,31 @@ struct HevcStreamDecoder::Impl {
         } else {
           m.mv[0][0] = m.mv[0][1] = m.mv[1][0] = m.mv[1][1] = 0;
         }
-      }
+      };
       // 8x8 records: a coding block is >= 8x8, so flags and QpY are uniform per 8x8; only
       // 8x4 / 4x8 prediction blocks differ inside one -- those become DM_SPLIT records whose
-      // first 4 bytes index 4 per-4x4 records (raster) in mvf_sub
+      // first 4 bytes index 4 per-4x4 records (raster) in mvf_sub.  Built straight from the
+      // 4x4 motion field (an 8x8 block lies in one CTB, so in one slice segment)
       const int w8 = w4 / 2, h8 = h4 / 2;
-      d.mvf.assign(static_cast<size_t>(w8) * h8, DecMv4{});
+      d.mvf.resize(static_cast<size_t>(w8) * h8);
       for (int by = 0; by < h8; ++by)
         for (int bx = 0; bx < w8; ++bx) {
-          const DecMv4* c[4] = {&m4[static_cast<size_t>(2 * by) * w4 + 2 * bx], &m4[static_cast<size_t>(2 * by) * w4 + 2 * bx + 1],
-                                &m4[static_cast<size_t>(2 * by + 1) * w4 + 2 * bx],
-                                &m4[static_cast<size_t>(2 * by + 1) * w4 + 2 * bx + 1]};
+          const int sidx = ctb_slice[((by * 8) >> log2_ctb) * wctb + ((bx * 8) >> log2_ctb)];
+          const size_t k0 = static_cast<size_t>(2 * by) * w4 + 2 * bx;
+          DecMv4 c[4] = {};
+          rec4(k0, sidx, c[0]);
+          rec4(k0 + 1, sidx, c[1]);
+          rec4(k0 + w4, sidx, c[2]);
+          rec4(k0 + w4 + 1, sidx, c[3]);
           DecMv4& o = d.mvf[static_cast<size_t>(by) * w8 + bx];
-          o = *c[0];
+          o = c[0];
           bool same = true;
-          for (int i = 1; i < 4; ++i) same = same && std::memcmp(c[i], c[0], sizeof(DecMv4)) == 0;
+          for (int i = 1; i < 4; ++i) same = same && std::memcmp(&c[i], &c[0], sizeof(DecMv4)) == 0;
           if (same) continue;
           const uint32_t idx = static_cast<uint32_t>(d.mvf_sub.size() / 4);
           std::memcpy(o.mv, &idx, 4);
           o.flags |= DM_SPLIT;
-          for (int i = 0; i < 4; ++i) d.mvf_sub.push_back(*c[i]);
+          for (int i = 0; i < 4; ++i) d.mvf_sub.push_back(c[i]);
         }
       uint32_t off = 0;
       for (int r = 0; r < nctb; ++r) {
@@ -2252,7 +2258,14 @@ struct HevcStreamDecoder::Impl {
   // reference picture identity of list entry (slice, list, idx)
   const StoredPic* ref_pic_of(int sidx, int l, int idx) const;
 
+  // compute_bs: the DPB picture of every (slice segment, list, ref_idx) of the current picture,
+  // resolved once per picture (ref_pic_of walks the DPB)
+  std::vector<std::array<const StoredPic*, 32>> bs_refs_;
   void compute_bs(std::vector<uint8_t>& bsv) {
+    bs_refs_.assign(cur->slices.size(), {});
+    for (size_t s = 0; s < cur->slices.size(); ++s)
+      for (int l = 0; l < 2; ++l)
+        for (int i = 0; i < 16; ++i) bs_refs_[s][l * 16 + i] = ref_pic_of(static_cast<int>(s), l, i);
     for (int y = 0; y < H; y += 4)
       for (int x = 0; x < W; x += 4) {
         uint8_t v = 0;
@@ -2284,7 +2297,7 @@ struct HevcStreamDecoder::Impl {
     const MvField& B = cur->mvf[q];
     const int sa = slice_of(xp, yp), sb = slice_of(xq, yq);
     auto pic = [&](int s, const MvField& m, int l) -> const void* {
-      return m.pred & (1 << l) ? static_cast<const void*>(ref_pic_of(s, l, m.ref[l])) : nullptr;
+      return m.pred & (1 << l) ? static_cast<const void*>(bs_refs_[s][l * 16 + (m.ref[l] & 15)]) : nullptr;
     };
     const int na = __builtin_popcount(A.pred), nb = __builtin_popcount(B.pred);
     if (na != nb) return 1;
