@@ -2266,6 +2266,7 @@ struct HevcStreamDecoder::Impl {
     for (size_t s = 0; s < cur->slices.size(); ++s)
       for (int l = 0; l < 2; ++l)
         for (int i = 0; i < 16; ++i) bs_refs_[s][l * 16 + i] = ref_pic_of(static_cast<int>(s), l, i);
+    const bool one_slice = slices.size() == 1;  // no slice lookups per edge
     for (int y = 0; y < H; y += 4)
       for (int x = 0; x < W; x += 4) {
         uint8_t v = 0;
@@ -2278,24 +2279,24 @@ struct HevcStreamDecoder::Impl {
           if (!tu && !pu) continue;
           const int xp = dir == 0 ? x - 1 : x, yp = dir == 0 ? y : y - 1;
           // edge filtering restrictions of the q-side (current) coding block's slice
-          const int sq = slice_of(x, y), sp = slice_of(xp, yp);
+          const int sq = one_slice ? 0 : slice_of(x, y), sp = one_slice ? 0 : slice_of(xp, yp);
           const SliceHeader& S = slices[sq];
           if (S.deblock_disabled) continue;
           if (sq != sp && slice_addr_of(sq) != slice_addr_of(sp) && !S.lf_across_slices) continue;
           if (!pps->lf_across_tiles && tile_of(x, y) != tile_of(xp, yp)) continue;
-          const int b = bs_value(xp, yp, x, y, tu);
+          const int b = bs_value(xp, yp, x, y, tu, sp, sq);
           v |= static_cast<uint8_t>(b << (dir * 2));
         }
         bsv[g4(x, y)] = v;
       }
   }
-  int bs_value(int xp, int yp, int xq, int yq, bool tu_edge) const {
+  // sa / sb: slice segments of the p / q blocks
+  int bs_value(int xp, int yp, int xq, int yq, bool tu_edge, int sa, int sb) const {
     const size_t p = g4(xp, yp), q = g4(xq, yq);
     if ((cu_flags[p] & CF_INTRA) || (cu_flags[q] & CF_INTRA)) return 2;
     if (tu_edge && (cbf_y[p] || cbf_y[q])) return 1;
     const MvField& A = cur->mvf[p];
     const MvField& B = cur->mvf[q];
-    const int sa = slice_of(xp, yp), sb = slice_of(xq, yq);
     auto pic = [&](int s, const MvField& m, int l) -> const void* {
       return m.pred & (1 << l) ? static_cast<const void*>(bs_refs_[s][l * 16 + (m.ref[l] & 15)]) : nullptr;
     };
