@@ -1761,12 +1761,12 @@ struct HevcStreamDecoder::Impl {
       int prev_csbf = 0;
       if (xs < nsb - 1) prev_csbf += csbf[xs + 1][ys];
       if (ys < nsb - 1) prev_csbf += csbf[xs][ys + 1] << 1;
+      const uint8_t* sig_row = kSigCtx.t[cidx ? 1 : 0][log2 - 2][scan][prev_csbf][(xs | ys) ? 1 : 0];
       int sig[16] = {};
       if (i == last_sb) sig[last_pos] = 1;
       for (int p = (i == last_sb ? last_pos - 1 : 15); p >= 0; --p) {
-        const int xc = xs * 4 + px[p], yc = ys * 4 + py[p];
         if (csbf[xs][ys] && (p > 0 || !infer_dc)) {
-          sig[p] = eng.decode(ctx[C_SIG + sig_ctx(xc, yc, log2, cidx, scan, prev_csbf, xs, ys)]);
+          sig[p] = eng.decode(ctx[C_SIG + sig_row[(py[p] << 2) + px[p]]]);
           if (sig[p]) infer_dc = false;
         } else if (p == 0 && infer_dc && csbf[xs][ys]) {
           sig[p] = 1;
@@ -1878,6 +1878,25 @@ struct HevcStreamDecoder::Impl {
     }
     return cidx == 0 ? s : 27 + s;
   }
+  // sig_coeff_flag ctxInc (9.3.4.2.5) of every (chroma, log2 - 2, scanIdx, prevCsbf, sub-block
+  // not the first, raster position in the sub-block), from sig_ctx once
+  struct SigCtxTable {
+    uint8_t t[2][4][3][4][2][16];
+    SigCtxTable() : t() {
+      for (int c = 0; c < 2; ++c)
+        for (int l = 0; l < 4; ++l)
+          for (int sc = 0; sc < 3; ++sc)
+            for (int pc = 0; pc < 4; ++pc)
+              for (int nf = 0; nf < 2; ++nf)
+                for (int q = 0; q < 16; ++q) {
+                  if (l == 0 && (nf || q == 15)) continue;  // one sub-block; (3, 3) is never a sig_coeff_flag
+                  const int xs = nf, ys = 0;
+                  t[c][l][sc][pc][nf][q] =
+                      static_cast<uint8_t>(sig_ctx(xs * 4 + (q & 3), ys * 4 + (q >> 2), l + 2, c, sc, pc, xs, ys));
+                }
+    }
+  };
+  inline static const SigCtxTable kSigCtx;
 
   // ======================================================================== CPU reconstruction
   // 8.6.2 - 8.6.4: scaling, transform (or skip / bypass), residual added to the prediction
