@@ -1315,10 +1315,22 @@ struct HevcStreamDecoder::Impl {
     auto nbmv = [&](int x, int y) -> const MvField& { return cur->mvf[g4(x, y)]; };
     auto par_same = [&](int xn, int yn) { return (xpb >> par) == (xn >> par) && (ypb >> par) == (yn >> par); };
     const int part = (par > 2 && ncbs == 8) ? P_2Nx2N : cu_part;
+    // the chosen candidate; 8x4 / 4x8 PUs are uni-predicted.  Spatial candidates only depend on
+    // the ones before them, so the list stops as soon as it holds merge_idx + 1 entries
+    auto done = [&](const MvField& m) {
+      out = m;
+      if (out.pred == 3 && w0 + h0 == 12) {
+        out.pred = 1;
+        out.ref[1] = -1;
+        out.mv[1][0] = out.mv[1][1] = 0;
+      }
+    };
     // A1
     const int xa1 = xpb - 1, ya1 = ypb + ph - 1;
     bool a1 = !par_same(xa1, ya1) && !((part == P_Nx2N || part == P_nLx2N || part == P_nRx2N) && pidx == 1) &&
               avail_pb(cu_x, cu_y, ncbs, xpb, ypb, pw, ph, pidx, xa1, ya1);
+    if (a1) cand[nc++] = nbmv(xa1, ya1);
+    if (merge_idx < nc) return done(cand[merge_idx]);
     // B1
     const int xb1 = xpb + pw - 1, yb1 = ypb - 1;
     bool b1 = !par_same(xb1, yb1) && !((part == P_2NxN || part == P_2NxnU || part == P_2NxnD) && pidx == 1) &&
@@ -1326,24 +1338,26 @@ struct HevcStreamDecoder::Impl {
     // pruning compares against availableA1 / availableB1 (before their own pruning)
     const bool av_b1 = b1;
     if (b1 && a1 && same_motion(nbmv(xa1, ya1), nbmv(xb1, yb1))) b1 = false;
+    if (b1) cand[nc++] = nbmv(xb1, yb1);
+    if (merge_idx < nc) return done(cand[merge_idx]);
     // B0
     const int xb0 = xpb + pw, yb0 = ypb - 1;
     bool b0 = !par_same(xb0, yb0) && avail_pb(cu_x, cu_y, ncbs, xpb, ypb, pw, ph, pidx, xb0, yb0);
     if (b0 && av_b1 && same_motion(nbmv(xb1, yb1), nbmv(xb0, yb0))) b0 = false;
+    if (b0) cand[nc++] = nbmv(xb0, yb0);
+    if (merge_idx < nc) return done(cand[merge_idx]);
     // A0
     const int xa0 = xpb - 1, ya0 = ypb + ph;
     bool a0 = !par_same(xa0, ya0) && avail_pb(cu_x, cu_y, ncbs, xpb, ypb, pw, ph, pidx, xa0, ya0);
     if (a0 && a1 && same_motion(nbmv(xa1, ya1), nbmv(xa0, ya0))) a0 = false;
+    if (a0) cand[nc++] = nbmv(xa0, ya0);
+    if (merge_idx < nc) return done(cand[merge_idx]);
     // B2
     const int xb2 = xpb - 1, yb2 = ypb - 1;
     bool b2 = !par_same(xb2, yb2) && avail_pb(cu_x, cu_y, ncbs, xpb, ypb, pw, ph, pidx, xb2, yb2);
     if (b2 && a1 && same_motion(nbmv(xa1, ya1), nbmv(xb2, yb2))) b2 = false;
     if (b2 && av_b1 && same_motion(nbmv(xb1, yb1), nbmv(xb2, yb2))) b2 = false;
     if (a0 + a1 + b0 + b1 == 4) b2 = false;
-    if (a1) cand[nc++] = nbmv(xa1, ya1);
-    if (b1) cand[nc++] = nbmv(xb1, yb1);
-    if (b0) cand[nc++] = nbmv(xb0, yb0);
-    if (a0) cand[nc++] = nbmv(xa0, ya0);
     if (b2) cand[nc++] = nbmv(xb2, yb2);
     if (merge_idx < nc) {
       out = cand[merge_idx];
